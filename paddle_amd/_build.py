@@ -1,0 +1,141 @@
+"""In-tree native build for paddle_amd.
+
+Two native artefacts, both built in place so they travel with the repo snapshot:
+
+* ``paddle_amd/lib/libpaddle_amd_kernels.so`` -- the CDNA4 (gfx950) HIP kernel
+  library (``csrc/kernels/*.hip``), compiled with ``hipcc --offload-arch=gfx950``.
+  It exposes a flat C ABI (``pa_*`` launchers taking raw device pointers and a
+  ``hipStream_t``) so it has no dependency on PyTorch headers and compiles in
+  seconds.
+* ``paddle_amd/lib/libpaddle_amd_runtime.so`` -- the C++17 runtime
+  (``csrc/runtime/*.cc``): buddy allocator, LoDTensor stream serialisation,
+  RecordIO, thread pool / blocking queue, SSA dependency scheduler, profiler
+  event buffers.  Plain C ABI as well, bound with ctypes.
+
+Object files are cached under ``build/`` keyed by source mtime + flags, and the
+link step is skipped when the library is newer than every object.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(ROOT)
+LIBDIR = os.path.join(ROOT, "lib")
+BUILDDIR = os.path.join(REPO, "build", "native")
+ARCH = os.environ.get("PADDLE_AMD_ARCH", "gfx950")
+
+KERNEL_LIB = os.path.join(LIBDIR, "libpaddle_amd_kernels.so")
+RUNTIME_LIB = os.path.join(LIBDIR, "libpaddle_amd_runtime.so")
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found: the paddle_amd kernel library needs ROCm's hipcc")
+
+
+def _torch_lib_dir() -> str | None:
+    try:
+        import torch  # noqa: F401
+
+        return os.path.join(os.path.dirname(torch.__file__), "lib")
+    except Exception:  # pragma: no cover
+        return None
+
+
+def _needs(obj: str, deps: list[str], stamp: str) -> bool:
+    if not os.path.exists(obj) or not os.path.exists(obj + ".flags"):
+        return True
+    if open(obj + ".flags").read() != stamp:
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _compile(cmd: list[str], obj: str, stamp: str, verbose: bool):
+    if verbose:
+        print("[paddle_amd build]", " ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"native build failed for {obj}:\n{r.stderr[-6000:]}")
+    with open(obj + ".flags", "w") as f:
+        f.write(stamp)
+
+
+def _build_lib(srcs, hdrs, out, compiler, cflags, ldflags, verbose, jobs):
+    os.makedirs(BUILDDIR, exist_ok=True)
+    os.makedirs(LIBDIR, exist_ok=True)
+    objs, todo = [], []
+    stamp = hashlib.sha1(" ".join([compiler] + cflags).encode()).hexdigest()
+    for s in srcs:
+        obj = os.path.join(BUILDDIR, os.path.basename(s) + ".o")
+        objs.append(obj)
+        if _needs(obj, [s] + hdrs, stamp):
+            todo.append(([compiler] + cflags + ["-c", s, "-o", obj], obj))
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            list(ex.map(lambda a: _compile(a[0], a[1], stamp, verbose), todo))
+    if todo or not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
+        cmd = [compiler, "-shared", "-o", out + ".tmp"] + objs + ldflags
+        if verbose:
+            print("[paddle_amd build]", " ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed for {out}:\n{r.stderr[-4000:]}")
+        os.replace(out + ".tmp", out)
+    return out
+
+
+def build_kernels(verbose: bool = False, jobs: int | None = None) -> str:
+    srcs = sorted(glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip")))
+    hdrs = sorted(glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.h")))
+    cflags = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-fvisibility=hidden",
+              "-ffp-contract=fast", "-munsafe-fp-atomics"]
+    ldflags = [f"--offload-arch={ARCH}"]
+    tl = _torch_lib_dir()
+    if tl:
+        # link the same libamdhip64 (SONAME libamdhip64.so.7) torch itself loads
+        ldflags += [f"-L{tl}", f"-Wl,-rpath,{tl}"]
+    ldflags += ["-lamdhip64"]
+    return _build_lib(srcs, hdrs, KERNEL_LIB, _hipcc(), cflags, ldflags, verbose,
+                      jobs or min(8, os.cpu_count() or 4))
+
+
+def build_runtime(verbose: bool = False, jobs: int | None = None) -> str:
+    srcs = sorted(glob.glob(os.path.join(ROOT, "csrc", "runtime", "*.cc")))
+    if not srcs:
+        return ""
+    hdrs = sorted(glob.glob(os.path.join(ROOT, "csrc", "runtime", "*.h")))
+    cxx = shutil.which("g++") or "c++"
+    cflags = ["-O2", "-fPIC", "-std=c++17", "-fvisibility=hidden", "-Wall", "-pthread",
+              "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]
+    ldflags = ["-pthread", "-lz"]
+    tl = _torch_lib_dir()
+    if tl:
+        ldflags += [f"-L{tl}", f"-Wl,-rpath,{tl}", "-lamdhip64"]
+    else:
+        ldflags += ["-L/opt/rocm/lib", "-lamdhip64"]
+    extra = os.environ.get("PADDLE_AMD_RUNTIME_CFLAGS", "").split()
+    return _build_lib(srcs, hdrs, RUNTIME_LIB, cxx, cflags + extra, ldflags, verbose,
+                      jobs or min(8, os.cpu_count() or 4))
+
+
+def build_all(verbose: bool = False) -> list[str]:
+    out = [build_kernels(verbose)]
+    rt = build_runtime(verbose)
+    if rt:
+        out.append(rt)
+    return out
+
+
+if __name__ == "__main__":
+    for p in build_all(verbose="-v" in sys.argv):
+        print(p)

@@ -1,0 +1,545 @@
+// Flash attention forward + backward for gfx950 (CDNA4), bf16 in / fp32 accumulate.
+//
+// The reference has no fused attention at all: nets.scaled_dot_product_attention
+// (python/paddle/fluid/nets.py:332-460) materialises QK^T -> softmax -> PV as
+// separate ops.  This is the north-star MI355X kernel.
+//
+// Forward (per workgroup: 4 waves x 32 query rows = 128 rows of one (b, head)):
+//   * "swapped" QK^T: each wave computes S^T = K * Q^T with v_mfma_f32_32x32x16_bf16,
+//     so a lane owns ONE query row (col = lane & 31) and the kv scores sit in its
+//     registers: the online-softmax max/sum is lane-local + one xor-32 exchange.
+//   * the S^T accumulator is fed straight back as the B operand of O^T += V^T P^T
+//     (no LDS round trip for P); V^T fragments come from ds_read_b64_tr_b16
+//     transposed LDS reads of a row-major V tile (T10).
+//   * K tile XOR-swizzled at 16-B granularity (conflict-free ds_read_b128, T2);
+//     V tile XOR-swizzled at 64-B granularity (conflict-free tr reads).
+//   * next K/V tile prefetched into registers under the current tile's MFMAs and
+//     written to LDS after the barrier (T14); the alpha rescale is a per-lane scalar.
+//   * heaviest causal tiles are dispatched first (m-tile on grid.z, reversed), and
+//     all m-tiles of one head land on the same XCD (head index on grid.x).
+// Backward (per workgroup: 4 waves x 32 keys = 128 keys of one (b, head)):
+//   * key on the MFMA lane for S and dP (their accumulators are the B operands of
+//     dV^T += dO^T P and dK^T += Q^T dS), dK/dV accumulated in registers over all
+//     query tiles, dS crosses LDS once (as dS^T) for dQ = dS K, which is reduced over
+//     the workgroup's 128 keys on the MFMA before one f32 atomic add per element.
+//   * Q/dO/K tiles use one LDS image for both row (b128) and transposed (tr_b16)
+//     reads (guide T10 layout (b)).
+#include "common.h"
+
+namespace pa {
+
+typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4v lds_s4v;
+
+__device__ __forceinline__ f32x16 mfma32(bf8v a, bf8v b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ bf8v as_bf8(u16x8 v) { return __builtin_bit_cast(bf8v, v); }
+__device__ __forceinline__ s4v tr_read(const char* lds_base, int byte_off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(lds_base + byte_off));
+}
+__device__ __forceinline__ bf8v cat_tr(s4v lo, s4v hi) {
+  typedef short s8v __attribute__((ext_vector_type(8)));
+  s8v r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf8v, r);
+}
+__device__ __forceinline__ bf8v pack_p(const f32x16& x, int base) {
+  bf8v r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)x[base + j];
+  return r;
+}
+
+struct FwdParams {
+  const u16 *q, *k, *v;
+  u16* o;
+  float* lse;  // [B, Hq, Sq]
+  long q_bs, q_ss, q_hs, k_bs, k_ss, k_hs, v_bs, v_ss, v_hs, o_bs, o_ss, o_hs;
+  int B, Sq, Sk, Hq, Hkv;
+  float scale_log2;  // softmax_scale * log2(e)
+};
+
+// ---- LDS image helpers --------------------------------------------------------
+// K (fwd): 16-B chunks XOR row (conflict-free b128 row reads of 16 distinct rows)
+template <int D>
+__device__ __forceinline__ int k_off(int row, int ch) {
+  constexpr int KCH = D / 8;
+  const int sw = (D == 128) ? (row & 15) : ((row >> 1) & (KCH - 1));
+  return row * D * 2 + ((ch ^ sw) * 16);
+}
+// V (fwd): 64-B segments XOR row (conflict-free 4-row tr reads)
+template <int D>
+__device__ __forceinline__ int v_off_bytes(int row, int byte_in_row) {
+  const int seg = byte_in_row >> 6;
+  const int sw = (D == 128) ? (row & 3) : ((row >> 1) & 1);
+  return row * D * 2 + (((seg ^ sw) << 6) | (byte_in_row & 63));
+}
+// dual-use image (bwd, D = 128 layout (b) of guide T10; generic for D = 64)
+template <int D>
+__device__ __forceinline__ int dual_off(int row, int byte_in_row) {
+  constexpr int KCH = D / 8;
+  const int ch = byte_in_row >> 4;
+  int sw;
+  if (D == 128) sw = ((row & 3) << 2) | ((row >> 2) & 3);
+  else sw = ((row >> 1) & (KCH - 1));
+  return row * D * 2 + (((ch ^ sw) << 4) | (byte_in_row & 15));
+}
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdParams p) {
+  constexpr int BM = 128, BN = 64;
+  constexpr int KCH = D / 8;              // 16-B chunks per row
+  constexpr int NCH = BN * KCH / 256;     // chunks per thread per tile
+  constexpr int KS = D / 16;              // k-steps over head dim
+  constexpr int DB = D / 32;              // 32-wide d blocks of O^T
+  __shared__ __attribute__((aligned(16))) char smem[2 * BN * D * 2];
+  char* Ks = smem;
+  char* Vs = smem + BN * D * 2;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int mt = gridDim.z - 1 - blockIdx.z;
+  const int kvh = h / (p.Hq / p.Hkv);
+  const long q0 = (long)mt * BM;
+  const long qw = q0 + w * 32;
+  const long qrow = qw + r;
+  const long offs = CAUSAL ? (long)p.Sk - p.Sq : 0;
+
+  const u16* qp = p.q + (long)b * p.q_bs + (long)h * p.q_hs;
+  const u16* kp = p.k + (long)b * p.k_bs + (long)kvh * p.k_hs;
+  const u16* vp = p.v + (long)b * p.v_bs + (long)kvh * p.v_hs;
+
+  bf8v qf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    u16x8 t = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (qrow < p.Sq) t = *reinterpret_cast<const u16x8*>(qp + qrow * p.q_ss + ks * 16 + hh * 8);
+    qf[ks] = as_bf8(t);
+  }
+
+  long kv_end = p.Sk;
+  if (CAUSAL) kv_end = min((long)p.Sk, q0 + BM + offs);
+  const int nt = kv_end > 0 ? (int)((kv_end + BN - 1) / BN) : 0;
+
+  f32x16 oacc[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) oacc[i][e] = 0.f;
+  float m = -1e30f, lsum = 0.f;
+
+  u16x8 kst[NCH], vst[NCH];
+  auto load_regs = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int idx = tid + 256 * i, row = idx / KCH, ch = idx % KCH;
+      const long kr = (long)t * BN + row;
+      if (kr < p.Sk) {
+        kst[i] = *reinterpret_cast<const u16x8*>(kp + kr * p.k_ss + ch * 8);
+        vst[i] = *reinterpret_cast<const u16x8*>(vp + kr * p.v_ss + ch * 8);
+      } else {
+        kst[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        vst[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    }
+  };
+  auto store_lds = [&]() {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int idx = tid + 256 * i, row = idx / KCH, ch = idx % KCH;
+      *reinterpret_cast<u16x8*>(Ks + k_off<D>(row, ch)) = kst[i];
+      *reinterpret_cast<u16x8*>(Vs + v_off_bytes<D>(row, ch * 16)) = vst[i];
+    }
+  };
+
+  if (nt > 0) {
+    load_regs(0);
+    store_lds();
+  }
+  __syncthreads();
+
+  // lane coordinates for the V^T transposed reads
+  const int g = lane >> 4, gi = lane & 15, gq = gi >> 2, gp = gi & 3;
+
+  for (int t = 0; t < nt; ++t) {
+    if (t + 1 < nt) load_regs(t + 1);
+    const long kv0 = (long)t * BN;
+    const bool skip = CAUSAL && (kv0 > qw + 31 + offs);
+    if (!skip) {
+      f32x16 s[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) s[c][e] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const u16x8 kf = *reinterpret_cast<const u16x8*>(Ks + k_off<D>(32 * c + r, 2 * ks + hh));
+          s[c] = mfma32(as_bf8(kf), qf[ks], s[c]);
+        }
+      }
+      const bool need_mask = (kv0 + BN > p.Sk) || (CAUSAL && (kv0 + BN - 1 > qw + offs));
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          float x = s[c][e] * p.scale_log2;
+          if (need_mask) {
+            const long kv = kv0 + 32 * c + (e & 3) + 8 * (e >> 2) + 4 * hh;
+            if (kv >= p.Sk || (CAUSAL && kv > qrow + offs)) x = -INFINITY;
+          }
+          s[c][e] = x;
+          tmax = fmaxf(tmax, x);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = fmaxf(m, tmax);
+      const float alpha = exp2f(m - mnew);
+      m = mnew;
+      float ps = 0.f;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const float pv = exp2f(s[c][e] - mnew);
+          s[c][e] = pv;
+          ps += pv;
+        }
+      lsum = lsum * alpha + ps;
+#pragma unroll
+      for (int i = 0; i < DB; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) oacc[i][e] *= alpha;
+      // O^T += V^T P^T over 4 k-steps of 16 kv
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const int c = st >> 1, half = st & 1;
+        const bf8v pf = pack_p(s[c], 8 * half);
+        const int rowb = 32 * c + 16 * half + 4 * (g >> 1) + gq;
+#pragma unroll
+        for (int db = 0; db < DB; ++db) {
+          const int colb = (32 * db + 16 * (g & 1) + 4 * gp) * 2;
+          const s4v lo = tr_read(Vs, v_off_bytes<D>(rowb, colb));
+          const s4v hi = tr_read(Vs, v_off_bytes<D>(rowb + 8, colb));
+          oacc[db] = mfma32(cat_tr(lo, hi), pf, oacc[db]);
+        }
+      }
+    }
+    __syncthreads();
+    if (t + 1 < nt) {
+      store_lds();
+      __syncthreads();
+    }
+  }
+
+  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  const float inv = ltot > 0.f ? 1.f / ltot : 0.f;
+  if (qrow < p.Sq) {
+    u16* op = p.o + (long)b * p.o_bs + (long)h * p.o_hs + qrow * p.o_ss;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        const int d = 32 * db + 8 * e4 + 4 * hh;
+        u16x4 o4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o4[j] = f2bf(oacc[db][4 * e4 + j] * inv);
+        *reinterpret_cast<u16x4*>(op + d) = o4;
+      }
+    if (hh == 0)
+      p.lse[((long)b * p.Hq + h) * p.Sq + qrow] =
+          ltot > 0.f ? (m + __log2f(ltot)) * 0.69314718056f : -INFINITY;
+  }
+}
+
+// ------------------------------------------------------------------ backward
+struct BwdParams {
+  const u16 *q, *k, *v, *o, *dout;
+  const float* lse;  // [B, Hq, Sq]
+  float* delta;      // [B, Hq, Sq]
+  float* dq_acc;     // [B, Sq, Hq, D] fp32
+  u16 *dk, *dv;      // [B, Sk, Hq, D] (expanded per q-head for GQA)
+  long q_bs, q_ss, q_hs, k_bs, k_ss, k_hs, v_bs, v_ss, v_hs, o_bs, o_ss, o_hs, do_bs, do_ss, do_hs;
+  long dk_bs, dk_ss, dk_hs;
+  int B, Sq, Sk, Hq, Hkv;
+  float scale;       // softmax scale
+  float scale_log2;  // scale * log2(e)
+};
+
+// delta[b,h,q] = sum_d dO * O ; 16 lanes per row (8 elems each for D=128)
+template <int D>
+__global__ void fa_bwd_pre_kernel(BwdParams p) {
+  constexpr int LPR = D / 8;  // lanes per row
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long row = gid / LPR;  // over B*Hq*Sq, ordered (b, h, q)
+  const int c = (int)(gid % LPR);
+  const long total = (long)p.B * p.Hq * p.Sq;
+  float s = 0.f;
+  if (row < total) {
+    const long q = row % p.Sq;
+    const long bh = row / p.Sq;
+    const int h = (int)(bh % p.Hq), b = (int)(bh / p.Hq);
+    float a[8], d[8];
+    load8(p.o + (long)b * p.o_bs + q * p.o_ss + (long)h * p.o_hs + c * 8, a);
+    load8(p.dout + (long)b * p.do_bs + q * p.do_ss + (long)h * p.do_hs + c * 8, d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += a[j] * d[j];
+  }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (row < total && c == 0) p.delta[row] = s;
+}
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdParams p) {
+  constexpr int BK = 128, BQ = 32;
+  constexpr int KS = D / 16, DB = D / 32;
+  constexpr int KCH = D / 8;
+  // LDS: K [BK][D] dual image | Q [BQ][D] | dO [BQ][D] | dS^T [BK][BQ] | lse2, delta [BQ]
+  constexpr int K_BYTES = BK * D * 2, Q_BYTES = BQ * D * 2, DS_BYTES = BK * BQ * 2;
+  __shared__ __attribute__((aligned(16))) char smem[K_BYTES + 2 * Q_BYTES + DS_BYTES + 2 * BQ * 4];
+  char* Ks = smem;
+  char* Qs = Ks + K_BYTES;
+  char* Os = Qs + Q_BYTES;
+  char* DSs = Os + Q_BYTES;
+  float* L2s = (float*)(DSs + DS_BYTES);
+  float* DLs = L2s + BQ;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int kt = blockIdx.z;  // causal: early key tiles carry the most query tiles -> dispatch first
+  const int kvh = h / (p.Hq / p.Hkv);
+  const long n0 = (long)kt * BK;
+  const long offs = CAUSAL ? (long)p.Sk - p.Sq : 0;
+
+  const u16* qp = p.q + (long)b * p.q_bs + (long)h * p.q_hs;
+  const u16* dop = p.dout + (long)b * p.do_bs + (long)h * p.do_hs;
+  const u16* kp = p.k + (long)b * p.k_bs + (long)kvh * p.k_hs;
+  const u16* vp = p.v + (long)b * p.v_bs + (long)kvh * p.v_hs;
+  const float* lsep = p.lse + ((long)b * p.Hq + h) * p.Sq;
+  const float* dlp = p.delta + ((long)b * p.Hq + h) * p.Sq;
+  float* dqp = p.dq_acc + (long)b * p.Sq * p.Hq * D + (long)h * D;  // row stride Hq*D
+
+  // K tile -> LDS (dual image)
+  for (int idx = tid; idx < BK * KCH; idx += 256) {
+    const int row = idx / KCH, ch = idx % KCH;
+    const long kr = n0 + row;
+    u16x8 t = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (kr < p.Sk) t = *reinterpret_cast<const u16x8*>(kp + kr * p.k_ss + ch * 8);
+    *reinterpret_cast<u16x8*>(Ks + dual_off<D>(row, ch * 16)) = t;
+  }
+  // V fragments (B operand of dP = dO V^T): lane holds V[kv = 32w + r][16ks + 8hh + j]
+  bf8v vf[KS];
+  const long mykv = n0 + 32 * w + r;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    u16x8 t = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (mykv < p.Sk) t = *reinterpret_cast<const u16x8*>(vp + mykv * p.v_ss + ks * 16 + hh * 8);
+    vf[ks] = as_bf8(t);
+  }
+
+  f32x16 dk[DB], dv[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) { dk[i][e] = 0.f; dv[i][e] = 0.f; }
+
+  long qstart = 0;
+  if (CAUSAL) qstart = max(0L, n0 - offs);
+  qstart = (qstart / BQ) * BQ;
+  const int g = lane >> 4, gi = lane & 15, gq = gi >> 2, gp = gi & 3;
+  const int wkv = 32 * w;  // this wave's key offset inside the tile
+
+  for (long qt0 = qstart; qt0 < p.Sq; qt0 += BQ) {
+    // stage Q, dO tiles + row constants
+    for (int idx = tid; idx < BQ * KCH; idx += 256) {
+      const int row = idx / KCH, ch = idx % KCH;
+      const long qr = qt0 + row;
+      u16x8 a = {0, 0, 0, 0, 0, 0, 0, 0}, d = a;
+      if (qr < p.Sq) {
+        a = *reinterpret_cast<const u16x8*>(qp + qr * p.q_ss + ch * 8);
+        d = *reinterpret_cast<const u16x8*>(dop + qr * p.do_ss + ch * 8);
+      }
+      *reinterpret_cast<u16x8*>(Qs + dual_off<D>(row, ch * 16)) = a;
+      *reinterpret_cast<u16x8*>(Os + dual_off<D>(row, ch * 16)) = d;
+    }
+    if (tid < BQ) {
+      const long qr = qt0 + tid;
+      L2s[tid] = qr < p.Sq ? lsep[qr] * 1.44269504089f : 0.f;
+      DLs[tid] = qr < p.Sq ? dlp[qr] : 0.f;
+    }
+    __syncthreads();
+
+    const bool wave_active = !(CAUSAL && (n0 + wkv > qt0 + BQ - 1 + offs)) && (n0 + wkv < p.Sk);
+    f32x16 sacc, dpacc;
+    if (wave_active) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) { sacc[e] = 0.f; dpacc[e] = 0.f; }
+      // S = Q K^T (A = Q rows, B = K rows of this wave's keys), dP = dO V^T
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const u16x8 qa = *reinterpret_cast<const u16x8*>(Qs + dual_off<D>(r, (2 * ks + hh) * 16));
+        const u16x8 kb = *reinterpret_cast<const u16x8*>(Ks + dual_off<D>(wkv + r, (2 * ks + hh) * 16));
+        sacc = mfma32(as_bf8(qa), as_bf8(kb), sacc);
+        const u16x8 oa = *reinterpret_cast<const u16x8*>(Os + dual_off<D>(r, (2 * ks + hh) * 16));
+        dpacc = mfma32(as_bf8(oa), vf[ks], dpacc);
+      }
+      // P and dS; rows (queries) in registers, key on the lane
+      const long kv = mykv;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int qi = (e & 3) + 8 * (e >> 2) + 4 * hh;
+        const long q = qt0 + qi;
+        float pv = exp2f(sacc[e] * p.scale_log2 - L2s[qi]);
+        if (q >= p.Sq || kv >= p.Sk || (CAUSAL && kv > q + offs)) pv = 0.f;
+        sacc[e] = pv;
+        dpacc[e] = pv * (dpacc[e] - DLs[qi]) * p.scale;
+      }
+      // dV^T += dO^T P ; dK^T += Q^T dS   (sum over the 32 queries: 2 k-steps)
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const bf8v pf = pack_p(sacc, 8 * st);
+        const bf8v sf = pack_p(dpacc, 8 * st);
+        const int rowb = 16 * st + 4 * (g >> 1) + gq;
+#pragma unroll
+        for (int db = 0; db < DB; ++db) {
+          const int colb = (32 * db + 16 * (g & 1) + 4 * gp) * 2;
+          const bf8v oa = cat_tr(tr_read(Os, dual_off<D>(rowb, colb)), tr_read(Os, dual_off<D>(rowb + 8, colb)));
+          dv[db] = mfma32(oa, pf, dv[db]);
+          const bf8v qa = cat_tr(tr_read(Qs, dual_off<D>(rowb, colb)), tr_read(Qs, dual_off<D>(rowb + 8, colb)));
+          dk[db] = mfma32(qa, sf, dk[db]);
+        }
+      }
+      // dS^T -> LDS: [key][query] with 64-B rows; lane writes 4 consecutive queries
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        u16x4 v4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v4[j] = f2bf(dpacc[4 * e4 + j]);
+        *reinterpret_cast<u16x4*>(DSs + (wkv + r) * (BQ * 2) + (8 * e4 + 4 * hh) * 2) = v4;
+      }
+    } else {
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4)
+        *reinterpret_cast<u16x4*>(DSs + (wkv + r) * (BQ * 2) + (8 * e4 + 4 * hh) * 2) = u16x4{0, 0, 0, 0};
+    }
+    __syncthreads();
+    // dQ[q, d-block w] = sum over the tile's 128 keys dS[q, kv] K[kv, d]
+    if (w < DB) {
+      f32x16 dq;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) dq[e] = 0.f;
+      const int kend = CAUSAL ? (int)min((long)BK, max(0L, qt0 + BQ + offs - n0)) : BK;
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        if (ks * 16 < kend) {
+          // A = dS[q = r][kv = 16ks + 8hh + j] from dS^T via transposed reads
+          const int arow = 16 * ks + 8 * hh + gq;  // kv rows for this lane's group
+          const int acol = (16 * (g & 1) + 4 * gp) * 2;
+          const bf8v af = cat_tr(tr_read(DSs, arow * (BQ * 2) + acol),
+                                 tr_read(DSs, (arow + 4) * (BQ * 2) + acol));
+          // B = K[kv = 16ks + 8hh + j][d = 32w + r]
+          const int brow = 16 * ks + 8 * hh + gq;
+          const int bcol = (32 * w + 16 * (g & 1) + 4 * gp) * 2;
+          const bf8v bfk = cat_tr(tr_read(Ks, dual_off<D>(brow, bcol)), tr_read(Ks, dual_off<D>(brow + 4, bcol)));
+          dq = mfma32(af, bfk, dq);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int qi = (e & 3) + 8 * (e >> 2) + 4 * hh;
+        const long q = qt0 + qi;
+        if (q < p.Sq) atomicAdd(dqp + q * ((long)p.Hq * D) + 32 * w + r, dq[e]);
+      }
+    }
+    __syncthreads();
+  }
+
+  // write dK, dV (per q-head layout [B, Sk, Hq, D])
+  if (mykv < p.Sk) {
+    u16* dkp = p.dk + (long)b * p.dk_bs + mykv * p.dk_ss + (long)h * p.dk_hs;
+    u16* dvp = p.dv + (long)b * p.dk_bs + mykv * p.dk_ss + (long)h * p.dk_hs;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        const int d = 32 * db + 8 * e4 + 4 * hh;
+        u16x4 a4, b4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a4[j] = f2bf(dk[db][4 * e4 + j]);
+          b4[j] = f2bf(dv[db][4 * e4 + j]);
+        }
+        *reinterpret_cast<u16x4*>(dkp + d) = a4;
+        *reinterpret_cast<u16x4*>(dvp + d) = b4;
+      }
+  }
+}
+
+}  // namespace pa
+
+using namespace pa;
+
+PA_EXPORT int pa_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
+                                const long* strides /*12: q b,s,h k b,s,h v b,s,h o b,s,h*/,
+                                int B, int Sq, int Sk, int Hq, int Hkv, int D, float scale,
+                                int causal, hipStream_t st) {
+  if (Hq % Hkv) return (int)hipErrorInvalidValue;
+  FwdParams p;
+  p.q = (const u16*)q; p.k = (const u16*)k; p.v = (const u16*)v; p.o = (u16*)o; p.lse = lse;
+  p.q_bs = strides[0]; p.q_ss = strides[1]; p.q_hs = strides[2];
+  p.k_bs = strides[3]; p.k_ss = strides[4]; p.k_hs = strides[5];
+  p.v_bs = strides[6]; p.v_ss = strides[7]; p.v_hs = strides[8];
+  p.o_bs = strides[9]; p.o_ss = strides[10]; p.o_hs = strides[11];
+  p.B = B; p.Sq = Sq; p.Sk = Sk; p.Hq = Hq; p.Hkv = Hkv;
+  p.scale_log2 = scale * 1.44269504089f;
+  dim3 grid(Hq, B, (Sq + 127) / 128);
+  if (D == 128) {
+    if (causal) hipLaunchKernelGGL((fa_fwd_kernel<128, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((fa_fwd_kernel<128, false>), grid, dim3(256), 0, st, p);
+  } else if (D == 64) {
+    if (causal) hipLaunchKernelGGL((fa_fwd_kernel<64, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((fa_fwd_kernel<64, false>), grid, dim3(256), 0, st, p);
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
+  PA_LAUNCH_CHECK();
+}
+
+// dq_acc ([B, Sq, Hq, D] fp32) must be zeroed by the caller; dk/dv share strides
+// strides[15..17] and are indexed by the q-head (GQA callers reduce head groups).
+PA_EXPORT int pa_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o,
+                                const void* dout, const float* lse, float* delta, float* dq_acc,
+                                void* dk, void* dv, const long* strides /*18: q k v o do dk(b,s,h)*/, int B, int Sq,
+                                int Sk, int Hq, int Hkv, int D, float scale, int causal,
+                                hipStream_t st) {
+  if (Hq % Hkv) return (int)hipErrorInvalidValue;
+  BwdParams p;
+  p.q = (const u16*)q; p.k = (const u16*)k; p.v = (const u16*)v; p.o = (const u16*)o;
+  p.dout = (const u16*)dout; p.lse = lse; p.delta = delta; p.dq_acc = dq_acc;
+  p.dk = (u16*)dk; p.dv = (u16*)dv;
+  p.q_bs = strides[0]; p.q_ss = strides[1]; p.q_hs = strides[2];
+  p.k_bs = strides[3]; p.k_ss = strides[4]; p.k_hs = strides[5];
+  p.v_bs = strides[6]; p.v_ss = strides[7]; p.v_hs = strides[8];
+  p.o_bs = strides[9]; p.o_ss = strides[10]; p.o_hs = strides[11];
+  p.do_bs = strides[12]; p.do_ss = strides[13]; p.do_hs = strides[14];
+  p.dk_bs = strides[15]; p.dk_ss = strides[16]; p.dk_hs = strides[17];
+  p.B = B; p.Sq = Sq; p.Sk = Sk; p.Hq = Hq; p.Hkv = Hkv;
+  p.scale = scale;
+  p.scale_log2 = scale * 1.44269504089f;
+  const long rows = (long)B * Hq * Sq;
+  const int lpr = D / 8;
+  const long pre_threads = rows * lpr;
+  if (D == 128) hipLaunchKernelGGL(fa_bwd_pre_kernel<128>, dim3((pre_threads + 255) / 256), dim3(256), 0, st, p);
+  else if (D == 64) hipLaunchKernelGGL(fa_bwd_pre_kernel<64>, dim3((pre_threads + 255) / 256), dim3(256), 0, st, p);
+  else return (int)hipErrorInvalidValue;
+  dim3 grid(Hq, B, (Sk + 127) / 128);
+  if (D == 128) {
+    if (causal) hipLaunchKernelGGL((fa_bwd_kernel<128, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((fa_bwd_kernel<128, false>), grid, dim3(256), 0, st, p);
+  } else {
+    if (causal) hipLaunchKernelGGL((fa_bwd_kernel<64, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((fa_bwd_kernel<64, false>), grid, dim3(256), 0, st, p);
+  }
+  PA_LAUNCH_CHECK();
+}

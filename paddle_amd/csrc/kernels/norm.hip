@@ -1,0 +1,285 @@
+// RMSNorm / LayerNorm forward + backward for gfx950.
+//
+// Parity: reference layer_norm (paddle/fluid/operators/layer_norm_op.cu:66-406,
+// one block per row with cub BlockReduce, 3 backward kernels).  Redesigned for
+// CDNA4: one wave64 per row, the whole row lives in VGPRs (H/512 x 16-byte
+// vectors per lane), reductions are pure in-wave shuffles (no LDS, no barrier),
+// and the residual add of a pre-norm transformer block is fused in
+// (h = x + residual; y = norm(h)) so the residual stream is read once.
+// dgamma/dbeta are accumulated in registers across the rows a wave owns,
+// folded across the block's waves with LDS float atomics and written as one
+// fp32 partial row per block; a second tiny kernel sums the partials.
+#include "common.h"
+
+namespace pa {
+
+template <typename T, int MAXV, bool RMS, bool HAS_RES, bool HAS_BIAS>
+__global__ __launch_bounds__(256) void norm_fwd_kernel(
+    const T* __restrict__ x, const T* __restrict__ res, const T* __restrict__ w,
+    const T* __restrict__ b, T* __restrict__ y, T* __restrict__ hout,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out, long N, int H, float eps) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const T* xr = x + row * H;
+  float v[MAXV][8];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int c = (k * 64 + lane) * 8;
+    if (c < H) {
+      load8(xr + c, v[k]);
+      if (HAS_RES) {
+        float r[8];
+        load8(res + row * H + c, r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] += r[j];
+        if (hout) store8(hout + row * H + c, v[k]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += RMS ? v[k][j] * v[k][j] : v[k][j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[k][j] = 0.f;
+    }
+  }
+  s = wave_sum(s);
+  float mean = 0.f, rstd;
+  if (RMS) {
+    rstd = rsqrtf(s / H + eps);
+  } else {
+    mean = s / H;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < H) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { float d = v[k][j] - mean; q += d * d; }
+      }
+    }
+    q = wave_sum(q);
+    rstd = rsqrtf(q / H + eps);
+  }
+  if (lane == 0) {
+    rstd_out[row] = rstd;
+    if (!RMS && mean_out) mean_out[row] = mean;
+  }
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int c = (k * 64 + lane) * 8;
+    if (c < H) {
+      float g[8], o[8];
+      load8(w + c, g);
+      if (HAS_BIAS) {
+        float bb[8];
+        load8(b + c, bb);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (v[k][j] - mean) * rstd * g[j] + bb[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (v[k][j] - mean) * rstd * g[j];
+      }
+      store8(y + row * H + c, o);
+    }
+  }
+}
+
+// Backward.  dx = rstd*(g*dy - mean(g*dy) [LN only] - xhat*mean(g*dy*xhat)) + dres
+// Each block owns a contiguous range of rows; waves take rows round-robin.  The
+// row's h and dy stay in VGPRs in their storage dtype (packed bf16 = 4 VGPRs per
+// 8 elements); gamma is re-read from L1 each row.  dgamma/dbeta accumulate in
+// registers (MAXV <= 8) or directly in LDS (wider rows) to stay spill-free.
+template <typename T> struct Raw8;
+template <> struct Raw8<u16> {
+  u16x8 v;
+  __device__ __forceinline__ void load(const u16* p) { v = *reinterpret_cast<const u16x8*>(p); }
+  __device__ __forceinline__ float operator[](int j) const { return bf2f(v[j]); }
+};
+template <> struct Raw8<float> {
+  f32x4 a, b;
+  __device__ __forceinline__ void load(const float* p) {
+    a = *reinterpret_cast<const f32x4*>(p);
+    b = *reinterpret_cast<const f32x4*>(p + 4);
+  }
+  __device__ __forceinline__ float operator[](int j) const { return j < 4 ? a[j] : b[j - 4]; }
+};
+
+template <typename T, int MAXV, bool RMS, bool HAS_DRES>
+__global__ __launch_bounds__(256) void norm_bwd_kernel(
+    const T* __restrict__ dy, const T* __restrict__ h, const T* __restrict__ w,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    const T* __restrict__ dres, T* __restrict__ dx, float* __restrict__ dw_part,
+    float* __restrict__ db_part, long N, int H, long rows_per_block) {
+  constexpr bool ACC_REG = MAXV <= 8;
+  constexpr int AV = ACC_REG ? MAXV : 1;
+  extern __shared__ __attribute__((aligned(16))) float sm[];  // [2*H] dw, db
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < 2 * H; i += 256) sm[i] = 0.f;
+  __syncthreads();
+  float aw[AV][8], ab[AV][8];
+#pragma unroll
+  for (int k = 0; k < AV; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { aw[k][j] = 0.f; ab[k][j] = 0.f; }
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  const long r1 = min(N, r0 + rows_per_block);
+  for (long row = r0 + wv; row < r1; row += 4) {
+    const float rstd = rstd_in[row];
+    const float mean = RMS ? 0.f : mean_in[row];
+    Raw8<T> hx[MAXV], dd[MAXV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < H) {
+        hx[k].load(h + row * H + c);
+        dd[k].load(dy + row * H + c);
+        float g[8];
+        load8(w + c, g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (hx[k][j] - mean) * rstd;
+          const float gd = g[j] * dd[k][j];
+          s1 += gd;
+          s2 += gd * xh;
+          if (ACC_REG) {
+            aw[ACC_REG ? k : 0][j] += dd[k][j] * xh;
+            ab[ACC_REG ? k : 0][j] += dd[k][j];
+          } else {
+            atomicAdd(&sm[c + j], dd[k][j] * xh);
+            if (!RMS) atomicAdd(&sm[H + c + j], dd[k][j]);
+          }
+        }
+      }
+    }
+    s2 = wave_sum(s2) / H;
+    if (!RMS) s1 = wave_sum(s1) / H;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < H) {
+        float o[8], g[8];
+        load8(w + c, g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (hx[k][j] - mean) * rstd;
+          o[j] = rstd * (g[j] * dd[k][j] - (RMS ? 0.f : s1) - xh * s2);
+        }
+        if (HAS_DRES) {
+          float r[8];
+          load8(dres + row * H + c, r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += r[j];
+        }
+        store8(dx + row * H + c, o);
+      }
+    }
+  }
+  if (ACC_REG) {
+#pragma unroll
+    for (int k = 0; k < AV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < H) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          atomicAdd(&sm[c + j], aw[k][j]);
+          if (!RMS) atomicAdd(&sm[H + c + j], ab[k][j]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < H; i += 256) {
+    dw_part[(long)blockIdx.x * H + i] = sm[i];
+    if (!RMS) db_part[(long)blockIdx.x * H + i] = sm[H + i];
+  }
+}
+
+// Column sum of a [G, H] fp32 partial matrix into out[H] (dtype T).
+template <typename T>
+__global__ void colsum_kernel(const float* __restrict__ part, T* __restrict__ out, int G, int H) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= H) return;
+  float s = 0.f;
+  for (int g = 0; g < G; ++g) s += part[(long)g * H + c];
+  IO<T>::st(out, c, s);
+}
+
+template <typename T, int MAXV>
+static int launch_fwd(bool rms, const void* x, const void* res, const void* w, const void* b,
+                      void* y, void* hout, float* mean, float* rstd, long N, int H, float eps,
+                      hipStream_t st) {
+  dim3 grid((N + 3) / 4), blk(256);
+  const T *X = (const T*)x, *R = (const T*)res, *W = (const T*)w, *B = (const T*)b;
+  T *Y = (T*)y, *HO = (T*)hout;
+#define PA_NF(RMS_, RES_, BIAS_) \
+  hipLaunchKernelGGL((norm_fwd_kernel<T, MAXV, RMS_, RES_, BIAS_>), grid, blk, 0, st, X, R, W, B, Y, HO, mean, rstd, N, H, eps)
+  if (rms) {
+    if (res) PA_NF(true, true, false); else PA_NF(true, false, false);
+  } else {
+    if (res) { if (b) PA_NF(false, true, true); else PA_NF(false, true, false); }
+    else { if (b) PA_NF(false, false, true); else PA_NF(false, false, false); }
+  }
+#undef PA_NF
+  PA_LAUNCH_CHECK();
+}
+
+template <typename T, int MAXV>
+static int launch_bwd(bool rms, const void* dy, const void* h, const void* w, const float* mean,
+                      const float* rstd, const void* dres, void* dx, void* dw, void* db,
+                      float* ws, long N, int H, hipStream_t st) {
+  long G0 = (N + 3) / 4; int G = (int)(G0 < 512 ? G0 : 512);
+  if (G < 1) G = 1;
+  long rpb = (N + G - 1) / G;
+  G = (int)((N + rpb - 1) / rpb);
+  float* dwp = ws;
+  float* dbp = ws + (long)G * H;
+  size_t shm = 2 * H * sizeof(float);
+  const T *DY = (const T*)dy, *Hh = (const T*)h, *W = (const T*)w, *DR = (const T*)dres;
+  T* DX = (T*)dx;
+#define PA_NB(RMS_, DRES_) \
+  hipLaunchKernelGGL((norm_bwd_kernel<T, MAXV, RMS_, DRES_>), dim3(G), dim3(256), shm, st, DY, Hh, W, mean, rstd, DR, DX, dwp, dbp, N, H, rpb)
+  if (rms) { if (dres) PA_NB(true, true); else PA_NB(true, false); }
+  else { if (dres) PA_NB(false, true); else PA_NB(false, false); }
+#undef PA_NB
+  hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 255) / 256), dim3(256), 0, st, dwp, (T*)dw, G, H);
+  if (!rms && db) hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 255) / 256), dim3(256), 0, st, dbp, (T*)db, G, H);
+  PA_LAUNCH_CHECK();
+}
+
+}  // namespace pa
+
+using namespace pa;
+
+// dtype: 0 = fp32, 1 = bf16.  Returns hipError_t.  H must be a multiple of 8, <= 8192.
+PA_EXPORT int pa_norm_fwd(int dtype, int rms, const void* x, const void* res, const void* w,
+                          const void* b, void* y, void* hout, float* mean, float* rstd, long N,
+                          int H, float eps, hipStream_t st) {
+  const int nv = (H + 511) / 512;
+#define PA_D(T)                                                                          \
+  if (nv <= 1) return launch_fwd<T, 1>(rms, x, res, w, b, y, hout, mean, rstd, N, H, eps, st); \
+  if (nv <= 2) return launch_fwd<T, 2>(rms, x, res, w, b, y, hout, mean, rstd, N, H, eps, st); \
+  if (nv <= 4) return launch_fwd<T, 4>(rms, x, res, w, b, y, hout, mean, rstd, N, H, eps, st); \
+  if (nv <= 8) return launch_fwd<T, 8>(rms, x, res, w, b, y, hout, mean, rstd, N, H, eps, st); \
+  if (nv <= 16) return launch_fwd<T, 16>(rms, x, res, w, b, y, hout, mean, rstd, N, H, eps, st);
+  if (dtype == 1) { PA_D(u16) } else { PA_D(float) }
+#undef PA_D
+  return (int)hipErrorInvalidValue;
+}
+
+// Workspace: ws must hold 2 * min(512, ceil(N/4)) * H floats.
+PA_EXPORT int pa_norm_bwd(int dtype, int rms, const void* dy, const void* h, const void* w,
+                          const float* mean, const float* rstd, const void* dres, void* dx,
+                          void* dw, void* db, float* ws, long N, int H, hipStream_t st) {
+  const int nv = (H + 511) / 512;
+#define PA_D(T)                                                                                 \
+  if (nv <= 1) return launch_bwd<T, 1>(rms, dy, h, w, mean, rstd, dres, dx, dw, db, ws, N, H, st); \
+  if (nv <= 2) return launch_bwd<T, 2>(rms, dy, h, w, mean, rstd, dres, dx, dw, db, ws, N, H, st); \
+  if (nv <= 4) return launch_bwd<T, 4>(rms, dy, h, w, mean, rstd, dres, dx, dw, db, ws, N, H, st); \
+  if (nv <= 8) return launch_bwd<T, 8>(rms, dy, h, w, mean, rstd, dres, dx, dw, db, ws, N, H, st); \
+  if (nv <= 16) return launch_bwd<T, 16>(rms, dy, h, w, mean, rstd, dres, dx, dw, db, ws, N, H, st);
+  if (dtype == 1) { PA_D(u16) } else { PA_D(float) }
+#undef PA_D
+  return (int)hipErrorInvalidValue;
+}

@@ -1,0 +1,139 @@
+// Fused optimizer updates for gfx950 over flat (multi-tensor) buffers.
+//
+// Parity: reference adam/momentum/sgd ops (paddle/fluid/operators/adam_op.h:35-321
+// ForRange<AdamFunctor> 1024-thread blocks; momentum_op.cu:67; sgd_op.cu:73).
+// Redesigned: parameters, grads and optimizer state live in ONE flat buffer each
+// (the fused-parameter layout the sharded DP engine uses), so a whole model's
+// step is one grid-stride launch; bf16 grads are read and the bf16 model copy is
+// written in the same pass as the fp32 master update (no separate cast kernel).
+// lr / beta-pow may come from device memory (static-graph ops) or by value.
+#include "common.h"
+
+namespace pa {
+
+template <typename TG, typename TP>
+__global__ void adamw_kernel(float* __restrict__ p, const TG* __restrict__ g, float* __restrict__ m,
+                             float* __restrict__ v, TP* __restrict__ pout, long n, float lr,
+                             const float* __restrict__ lr_ptr, float b1, float b2, float eps,
+                             float wd, float bc1, float bc2, const float* __restrict__ b1pow,
+                             const float* __restrict__ b2pow, long decay_end, float gscale,
+                             const float* __restrict__ gscale_ptr) {
+  float lr_ = lr_ptr ? lr_ptr[0] : lr;
+  float c1 = b1pow ? 1.f - b1pow[0] : bc1;
+  float c2 = b2pow ? 1.f - b2pow[0] : bc2;
+  const float gs = gscale_ptr ? gscale_ptr[0] * gscale : gscale;
+  const float step = lr_ / c1;
+  const float rc2 = rsqrtf(c2);
+  const long n4 = n / 4;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (long)gridDim.x * blockDim.x) {
+    const long e = i * 4;
+    f32x4 pp = *reinterpret_cast<f32x4*>(p + e);
+    f32x4 mm = *reinterpret_cast<f32x4*>(m + e);
+    f32x4 vv = *reinterpret_cast<f32x4*>(v + e);
+    float gg[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gg[j] = IO<TG>::ld(g, e + j) * gs;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mm[j] = b1 * mm[j] + (1.f - b1) * gg[j];
+      vv[j] = b2 * vv[j] + (1.f - b2) * gg[j] * gg[j];
+      const float decay = (e + j) < decay_end ? wd : 0.f;
+      pp[j] = pp[j] * (1.f - lr_ * decay) - step * mm[j] / (sqrtf(vv[j]) * rc2 + eps);
+    }
+    *reinterpret_cast<f32x4*>(p + e) = pp;
+    *reinterpret_cast<f32x4*>(m + e) = mm;
+    *reinterpret_cast<f32x4*>(v + e) = vv;
+    if (pout) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) IO<TP>::st(pout, e + j, pp[j]);
+    }
+  }
+  // tail
+  for (long e = n4 * 4 + (long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (long)gridDim.x * blockDim.x) {
+    const float gg = IO<TG>::ld(g, e) * gs;
+    float mm = b1 * m[e] + (1.f - b1) * gg;
+    float vv = b2 * v[e] + (1.f - b2) * gg * gg;
+    const float decay = e < decay_end ? wd : 0.f;
+    float pp = p[e] * (1.f - lr_ * decay) - step * mm / (sqrtf(vv) * rc2 + eps);
+    p[e] = pp; m[e] = mm; v[e] = vv;
+    if (pout) IO<TP>::st(pout, e, pp);
+  }
+}
+
+// Momentum (optionally Nesterov) and plain SGD, fp32 params.
+template <typename TG>
+__global__ void momentum_kernel(float* __restrict__ p, const TG* __restrict__ g,
+                                float* __restrict__ vel, long n, float lr,
+                                const float* __restrict__ lr_ptr, float mu, int nesterov, float wd,
+                                float gscale) {
+  const float lr_ = lr_ptr ? lr_ptr[0] : lr;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
+    const float gg = IO<TG>::ld(g, i) * gscale + wd * p[i];
+    if (vel) {
+      const float v = mu * vel[i] + gg;
+      vel[i] = v;
+      p[i] -= nesterov ? lr_ * (gg + mu * v) : lr_ * v;
+    } else {
+      p[i] -= lr_ * gg;
+    }
+  }
+}
+
+// sum of squares (for global-norm clipping): out[0] += sum(x^2) (fp32 atomics, one per block)
+template <typename T>
+__global__ void sumsq_kernel(const T* __restrict__ x, long n, float* __restrict__ out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
+    const float v = IO<T>::ld(x, i);
+    s += v * v;
+  }
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) atomicAdd(out, s);
+}
+
+}  // namespace pa
+
+using namespace pa;
+
+// gdtype: grad dtype (0 fp32, 1 bf16); pdtype: model-copy dtype (0 fp32, 1 bf16, -1 none)
+PA_EXPORT int pa_adamw(int gdtype, int pdtype, float* p, const void* g, float* m, float* v,
+                       void* pout, long n, float lr, const float* lr_ptr, float b1, float b2,
+                       float eps, float wd, float bc1, float bc2, const float* b1pow,
+                       const float* b2pow, long decay_end, float gscale, const float* gscale_ptr,
+                       hipStream_t st) {
+  if (n == 0) return 0;
+  const int grid = stream_grid((n + 3) / 4, 256);
+#define PA_A(TG, TP) \
+  hipLaunchKernelGGL((adamw_kernel<TG, TP>), dim3(grid), dim3(256), 0, st, p, (const TG*)g, m, v, (TP*)pout, n, lr, lr_ptr, b1, b2, eps, wd, bc1, bc2, b1pow, b2pow, decay_end, gscale, gscale_ptr)
+  if (gdtype == 1) { if (pdtype == 1) PA_A(u16, u16); else PA_A(u16, float); }
+  else { if (pdtype == 1) PA_A(float, u16); else PA_A(float, float); }
+#undef PA_A
+  PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_momentum(int gdtype, float* p, const void* g, float* vel, long n, float lr,
+                          const float* lr_ptr, float mu, int nesterov, float wd, float gscale,
+                          hipStream_t st) {
+  if (n == 0) return 0;
+  const int grid = stream_grid(n, 256);
+  if (gdtype == 1)
+    hipLaunchKernelGGL(momentum_kernel<u16>, dim3(grid), dim3(256), 0, st, p, (const u16*)g, vel, n, lr, lr_ptr, mu, nesterov, wd, gscale);
+  else
+    hipLaunchKernelGGL(momentum_kernel<float>, dim3(grid), dim3(256), 0, st, p, (const float*)g, vel, n, lr, lr_ptr, mu, nesterov, wd, gscale);
+  PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_sumsq(int dtype, const void* x, long n, float* out, hipStream_t st) {
+  if (n == 0) return 0;
+  const int grid = stream_grid(n, 256);
+  if (dtype == 1)
+    hipLaunchKernelGGL(sumsq_kernel<u16>, dim3(grid), dim3(256), 0, st, (const u16*)x, n, out);
+  else
+    hipLaunchKernelGGL(sumsq_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)x, n, out);
+  PA_LAUNCH_CHECK();
+}

@@ -1,0 +1,176 @@
+"""LLaMA decoder-only transformer (the BASELINE.json flagship: LLaMA-7B).
+
+North-star model (not in the Fluid 0.14 reference).  Paddle-side
+reference behaviour is PaddleNLP's ``LlamaForCausalLM`` with
+``fuse_attention_qkv`` / ``fuse_attention_ffn``: pre-RMSNorm blocks, rotary
+(neox "rotate-half") positions, SwiGLU MLP, untied LM head.
+
+MI355X design:
+  * one fused QKV GEMM and one fused gate|up GEMM per block (hipBLASLt), weights in
+    Paddle's ``[in, out]`` layout;
+  * rotary + causal flash attention in one autograd node on the packed QKV output
+    (``ops.rope_attention``: gfx950 MFMA kernels, no q/k/v copies);
+  * the residual add is fused into the following RMSNorm (``residual=`` path), so
+    each block reads the residual stream once per norm;
+  * SwiGLU and the vocab-sized softmax-cross-entropy are single-pass kernels; the
+    CE gradient is written in place over the logits.
+  * parameters are created directly on the target device in the compute dtype.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+from .. import ops
+from ..nn import Layer
+
+
+@dataclass
+class LlamaConfig:
+    vocab_size: int = 32000
+    hidden_size: int = 4096
+    intermediate_size: int = 11008
+    num_hidden_layers: int = 32
+    num_attention_heads: int = 32
+    num_key_value_heads: int | None = None
+    max_position_embeddings: int = 2048
+    rms_norm_eps: float = 1e-6
+    rope_theta: float = 10000.0
+    initializer_range: float = 0.02
+    tie_word_embeddings: bool = False
+    recompute: bool = False
+    dtype: str = "bfloat16"
+    # tensor parallel degree/rank (column/row split of the GEMMs); 1 = off
+    tensor_parallel_degree: int = 1
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def head_dim(self):
+        return self.hidden_size // self.num_attention_heads
+
+    @property
+    def kv_heads(self):
+        return self.num_key_value_heads or self.num_attention_heads
+
+    def num_params(self):
+        H, I, V, L = self.hidden_size, self.intermediate_size, self.vocab_size, self.num_hidden_layers
+        kvd = self.kv_heads * self.head_dim
+        per = H * (H + 2 * kvd) + H * H + 3 * H * I + 2 * H
+        return V * H * (1 if self.tie_word_embeddings else 2) + L * per + H
+
+
+LLAMA_CONFIGS = {
+    "llama-7b": dict(hidden_size=4096, intermediate_size=11008, num_hidden_layers=32, num_attention_heads=32),
+    "llama-13b": dict(hidden_size=5120, intermediate_size=13824, num_hidden_layers=40, num_attention_heads=40),
+    "llama-tiny": dict(vocab_size=512, hidden_size=256, intermediate_size=688, num_hidden_layers=2,
+                       num_attention_heads=2, max_position_embeddings=256),
+}
+
+
+def _dt(s):
+    return {"bfloat16": torch.bfloat16, "float32": torch.float32, "float16": torch.float16}[s]
+
+
+def _param(shape, device, dtype, std=None, value=None):
+    t = torch.empty(*shape, device=device, dtype=torch.float32)
+    if value is not None:
+        t.fill_(value)
+    else:
+        t.normal_(0.0, std)
+    return torch.nn.Parameter(t.to(dtype))
+
+
+class LlamaDecoderLayer(Layer):
+    def __init__(self, cfg: LlamaConfig, device=None, layer_idx=0, tp=None):
+        super().__init__("llama_decoder")
+        H, I = cfg.hidden_size, cfg.intermediate_size
+        dt = _dt(cfg.dtype)
+        std = cfg.initializer_range
+        self.cfg = cfg
+        self.tp = tp  # optional parallel.tensor_parallel.TPGroup
+        tpd = tp.world_size if tp is not None else 1
+        self.nh = cfg.num_attention_heads // tpd
+        self.nkv = cfg.kv_heads // tpd
+        D = cfg.head_dim
+        self.input_layernorm = _param([H], device, dt, value=1.0)
+        self.qkv_proj = _param([H, (self.nh + 2 * self.nkv) * D], device, dt, std)
+        self.o_proj = _param([self.nh * D, H], device, dt, std / math.sqrt(2 * cfg.num_hidden_layers))
+        self.post_attention_layernorm = _param([H], device, dt, value=1.0)
+        self.gate_up_proj = _param([H, 2 * I // tpd], device, dt, std)
+        self.down_proj = _param([I // tpd, H], device, dt, std / math.sqrt(2 * cfg.num_hidden_layers))
+        for n in ("input_layernorm", "post_attention_layernorm"):
+            getattr(self, n).no_weight_decay = True
+
+    def forward(self, x, residual, cos, sin):
+        cfg = self.cfg
+        eps = cfg.rms_norm_eps
+        if residual is None:
+            h = x
+            y = ops.rms_norm(x, self.input_layernorm, eps)
+        else:
+            y, h = ops.rms_norm(x, self.input_layernorm, eps, residual=residual)
+        if self.tp is not None:
+            y = self.tp.copy_to_region(y)
+        qkv = torch.matmul(y, self.qkv_proj)
+        a = ops.rope_attention(qkv, cos, sin, self.nh, self.nkv, causal=True)
+        a = torch.matmul(a, self.o_proj)
+        if self.tp is not None:
+            a = self.tp.reduce_from_region(a)
+        y2, h2 = ops.rms_norm(a, self.post_attention_layernorm, eps, residual=h)
+        if self.tp is not None:
+            y2 = self.tp.copy_to_region(y2)
+        m = torch.matmul(ops.swiglu(torch.matmul(y2, self.gate_up_proj)), self.down_proj)
+        if self.tp is not None:
+            m = self.tp.reduce_from_region(m)
+        return m, h2
+
+
+class LlamaForCausalLM(Layer):
+    def __init__(self, cfg: LlamaConfig, device=None, tp=None):
+        super().__init__("llama")
+        self.cfg = cfg
+        dt = _dt(cfg.dtype)
+        std = cfg.initializer_range
+        H = cfg.hidden_size
+        self.embed_tokens = _param([cfg.vocab_size, H], device, dt, std)
+        self.layers = torch.nn.ModuleList(
+            [LlamaDecoderLayer(cfg, device, i, tp) for i in range(cfg.num_hidden_layers)])
+        self.norm = _param([H], device, dt, value=1.0)
+        self.norm.no_weight_decay = True
+        self.lm_head = None if cfg.tie_word_embeddings else _param([H, cfg.vocab_size], device, dt, std)
+        cos, sin = ops.rope_tables(cfg.max_position_embeddings, cfg.head_dim, cfg.rope_theta, device=device)
+        self.register_buffer("rope_cos", cos, persistent=False)
+        self.register_buffer("rope_sin", sin, persistent=False)
+
+    def hidden_states(self, input_ids):
+        x = ops.embedding(input_ids, self.embed_tokens)
+        residual = None
+        cos, sin = self.rope_cos, self.rope_sin
+        for layer in self.layers:
+            if self.cfg.recompute and self.training and torch.is_grad_enabled():
+                x, residual = torch.utils.checkpoint.checkpoint(layer, x, residual, cos, sin,
+                                                                use_reentrant=False)
+            else:
+                x, residual = layer(x, residual, cos, sin)
+        y, _ = ops.rms_norm(x, self.norm, self.cfg.rms_norm_eps, residual=residual)
+        return y
+
+    def forward(self, input_ids, labels=None):
+        y = self.hidden_states(input_ids)
+        w = self.lm_head if self.lm_head is not None else self.embed_tokens.t()
+        logits = torch.matmul(y, w)
+        if labels is None:
+            return logits
+        # in-place CE gradient over the logits buffer (nothing else consumes it)
+        return ops.softmax_cross_entropy(logits, labels, inplace_grad=True)
+
+
+def llama_flops_per_token(cfg: LlamaConfig, seq_len: int) -> float:
+    """Training FLOPs per token (fwd+bwd = 3x fwd), dense GEMMs + causal attention."""
+    H, I, L, V = cfg.hidden_size, cfg.intermediate_size, cfg.num_hidden_layers, cfg.vocab_size
+    kvd = cfg.kv_heads * cfg.head_dim
+    gemm = 2 * (H * (H + 2 * kvd) + H * H + 3 * H * I)
+    attn = 2 * 2 * seq_len * H / 2  # QK^T + PV, causal half
+    return 3 * (L * (gemm + attn) + 2 * H * V)

@@ -1,0 +1,110 @@
+"""ctypes binding of the gfx950 kernel library (``lib/libpaddle_amd_kernels.so``).
+
+Every launcher has a flat C ABI: raw device pointers, sizes, scalars and the
+``hipStream_t`` of torch's *current* stream, so launches are ordered with the
+rest of the step and are capturable into HIP graphs.
+
+Policy (mirrors the reference's CPU-kernel / CUDA-kernel split):
+GPU tensors ALWAYS go through these kernels -- if the library is missing on a
+machine with a GPU we raise instead of silently falling back; CPU tensors use the
+PyTorch reference implementations in :mod:`paddle_amd.ops.reference`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+from .. import _build
+
+_lock = threading.Lock()
+_lib = None
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_long
+_F = ctypes.c_float
+_LP = ctypes.POINTER(ctypes.c_long)
+
+_SIGS = {
+    "pa_norm_fwd": [_I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _F, _P],
+    "pa_norm_bwd": [_I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
+    "pa_rope": [_I, _I, _P, _L, _P, _L, _P, _P, _P, _L, _L, _I, _I, _I, _I, _P],
+    "pa_swiglu_fwd": [_I, _P, _P, _L, _I, _P],
+    "pa_swiglu_bwd": [_I, _P, _P, _P, _L, _I, _P],
+    "pa_embedding_fwd": [_I, _P, _P, _P, _L, _I, _L, _P],
+    "pa_embedding_bwd": [_I, _P, _P, _P, _L, _I, _L, _P],
+    "pa_cast": [_I, _I, _P, _P, _L, _P],
+    "pa_softmax_ce_fwd": [_I, _P, _P, _P, _P, _P, _L, _I, _L, _P],
+    "pa_softmax_ce_bwd": [_I, _P, _P, _P, _P, _P, _P, _L, _I, _L, _F, _P],
+    "pa_softmax_fwd": [_I, _P, _P, _L, _I, _I, _P],
+    "pa_softmax_bwd": [_I, _P, _P, _P, _L, _I, _I, _P],
+    "pa_adamw": [_I, _I, _P, _P, _P, _P, _P, _L, _F, _P, _F, _F, _F, _F, _F, _F, _P, _P, _L, _F, _P, _P],
+    "pa_momentum": [_I, _P, _P, _P, _L, _F, _P, _F, _I, _F, _F, _P],
+    "pa_sumsq": [_I, _P, _L, _P, _P],
+    "pa_flash_attn_fwd": [_P, _P, _P, _P, _P, _LP, _I, _I, _I, _I, _I, _I, _F, _I, _P],
+    "pa_flash_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _LP, _I, _I, _I, _I, _I, _I, _F, _I, _P],
+}
+
+
+def lib():
+    """Load (building on first use if hipcc is available) the kernel library."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = _build.KERNEL_LIB
+        if not os.path.exists(path):
+            try:
+                _build.build_kernels()
+            except Exception as e:  # pragma: no cover - exercised only without a prebuilt lib
+                raise RuntimeError(
+                    f"paddle_amd HIP kernel library missing ({path}) and could not be built: {e}. "
+                    "Run `python -m paddle_amd._build` (or __graft_entry__.build()).") from e
+        L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        for name, args in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = _I
+        _lib = L
+        return _lib
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except Exception:
+        return False
+
+
+def stream():
+    return _P(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    if t is None:
+        return None
+    return _P(t.data_ptr())
+
+
+def dt(t) -> int:
+    if t.dtype == torch.bfloat16:
+        return 1
+    if t.dtype == torch.float32:
+        return 0
+    raise TypeError(f"paddle_amd kernels support float32/bfloat16, got {t.dtype}")
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"paddle_amd kernel {what} failed: hipError {rc}")
+
+
+def call(name: str, *args):
+    rc = getattr(lib(), name)(*args)
+    check(rc, name)

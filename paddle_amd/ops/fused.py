@@ -1,0 +1,460 @@
+"""Fused hot ops: autograd wrappers over the gfx950 kernels (GPU) and PyTorch
+reference math (CPU).
+
+Each op has exactly two kernels, like the reference's CPU/CUDA kernel pair
+(SURVEY §2.1 #5): a GPU tensor always runs the hand-written HIP kernel from
+``libpaddle_amd_kernels.so`` (loading fails loudly if it is missing) and a CPU
+tensor runs the plain PyTorch definition below, which is also the fp32 oracle
+the GPU numerics tests compare against.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _native as N
+
+# --------------------------------------------------------------------------- utils
+
+
+def _ws(n: int, device, dtype=torch.float32):
+    return torch.empty(n, dtype=dtype, device=device)
+
+
+def _c(t):
+    return t if t.is_contiguous() else t.contiguous()
+
+
+# ====================================================================== RMS / Layer norm
+
+
+def _norm_ref(x, res, w, b, eps, rms):
+    h = x.float() + res.float() if res is not None else x.float()
+    if rms:
+        rstd = torch.rsqrt(h.pow(2).mean(-1, keepdim=True) + eps)
+        y = h * rstd * w.float()
+        mean = None
+    else:
+        mean = h.mean(-1, keepdim=True)
+        var = (h - mean).pow(2).mean(-1, keepdim=True)
+        rstd = torch.rsqrt(var + eps)
+        y = (h - mean) * rstd * w.float()
+        if b is not None:
+            y = y + b.float()
+    return y.to(x.dtype), h.to(x.dtype)
+
+
+class _NormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, res, w, b, eps, rms):
+        H = x.shape[-1]
+        x2 = _c(x).view(-1, H)
+        Nr = x2.shape[0]
+        dev = x.device
+        y = torch.empty_like(x2)
+        hout = torch.empty_like(x2) if res is not None else None
+        rstd = _ws(Nr, dev)
+        mean = None if rms else _ws(Nr, dev)
+        N.call("pa_norm_fwd", N.dt(x2), int(rms), N.ptr(x2), N.ptr(_c(res).view(-1, H) if res is not None else None),
+               N.ptr(w), N.ptr(b), N.ptr(y), N.ptr(hout), N.ptr(mean), N.ptr(rstd), Nr, H, float(eps), N.stream())
+        h = hout if res is not None else x2
+        ctx.save_for_backward(h, w, mean, rstd)
+        ctx.rms, ctx.has_res, ctx.has_b, ctx.shape = rms, res is not None, b is not None, x.shape
+        if res is not None:
+            return y.view(x.shape), hout.view(x.shape)
+        return y.view(x.shape), None
+
+    @staticmethod
+    def backward(ctx, dy, dh):
+        h, w, mean, rstd = ctx.saved_tensors
+        H = h.shape[-1]
+        Nr = h.shape[0]
+        dy2 = _c(dy).view(-1, H)
+        dres = _c(dh).view(-1, H) if (ctx.has_res and dh is not None) else None
+        dx = torch.empty_like(h)
+        dw = torch.empty_like(w)
+        db = torch.empty_like(w) if ctx.has_b else None
+        G = min(512, (Nr + 3) // 4)
+        ws = _ws(2 * max(G, 1) * H, h.device)
+        N.call("pa_norm_bwd", N.dt(h), int(ctx.rms), N.ptr(dy2), N.ptr(h), N.ptr(w), N.ptr(mean), N.ptr(rstd),
+               N.ptr(dres), N.ptr(dx), N.ptr(dw), N.ptr(db), N.ptr(ws), Nr, H, N.stream())
+        dx = dx.view(ctx.shape)
+        return dx, (dx if ctx.has_res else None), dw, db, None, None
+
+
+def rms_norm(x, weight, eps=1e-6, residual=None):
+    """y = x * rsqrt(mean(x^2) + eps) * weight.  With ``residual``: h = x + residual,
+    returns (rms_norm(h), h) with the add fused into the same pass."""
+    if x.is_cuda:
+        y, h = _NormFn.apply(x, residual, weight, None, eps, True)
+        return (y, h) if residual is not None else y
+    y, h = _norm_ref(x, residual, weight, None, eps, True)
+    return (y, h) if residual is not None else y
+
+
+def layer_norm(x, weight, bias=None, eps=1e-5, residual=None):
+    if x.is_cuda and weight is not None and x.shape[-1] % 8 == 0 and x.shape[-1] <= 8192:
+        y, h = _NormFn.apply(x, residual, weight, bias, eps, False)
+        return (y, h) if residual is not None else y
+    if weight is None:
+        h = x + residual if residual is not None else x
+        y = torch.nn.functional.layer_norm(h, h.shape[-1:], None, bias, eps)
+        return (y, h) if residual is not None else y
+    y, h = _norm_ref(x, residual, weight, bias, eps, False)
+    return (y, h) if residual is not None else y
+
+
+# ====================================================================== rotary
+
+
+def rope_tables(seq_len: int, head_dim: int, base: float = 10000.0, device=None):
+    inv = 1.0 / (base ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    t = torch.arange(seq_len, dtype=torch.float64)
+    f = torch.outer(t, inv)
+    return f.cos().float().contiguous().to(device), f.sin().float().contiguous().to(device)
+
+
+def _rope_ref(x, cos, sin, sign=1.0):
+    # x [..., S, nh, D] (token dim = -3)
+    D = x.shape[-1]
+    S = x.shape[-3]
+    c = cos[:S].view(S, 1, D // 2)
+    s = sin[:S].view(S, 1, D // 2) * sign
+    a, b = x[..., : D // 2].float(), x[..., D // 2:].float()
+    return torch.cat([a * c - b * s, b * c + a * s], -1).to(x.dtype)
+
+
+# ====================================================================== flash attention
+
+
+def _attn_ref(q, k, v, causal, scale):
+    # [B, S, H, D] layout
+    B, Sq, Hq, D = q.shape
+    Hk = k.shape[2]
+    if Hk != Hq:
+        k = k.repeat_interleave(Hq // Hk, dim=2)
+        v = v.repeat_interleave(Hq // Hk, dim=2)
+    qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if causal:
+        Sk = k.shape[1]
+        m = torch.ones(Sq, Sk, dtype=torch.bool, device=q.device).tril(Sk - Sq)
+        s = s.masked_fill(~m, float("-inf"))
+    p = torch.softmax(s, -1)
+    o = torch.matmul(p, vf).transpose(1, 2)
+    return o.to(q.dtype)
+
+
+def _fa_strides(t):
+    # [B, S, H, D] view with unit stride on D
+    assert t.stride(-1) == 1, "flash attention needs a unit stride on the head dim"
+    return [t.stride(0), t.stride(1), t.stride(2)]
+
+
+def _fa_fwd(q, k, v, causal, scale):
+    B, Sq, Hq, D = q.shape
+    Sk, Hk = k.shape[1], k.shape[2]
+    o = torch.empty(B, Sq, Hq, D, dtype=q.dtype, device=q.device)
+    lse = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
+    st = ctypes_long_array(_fa_strides(q) + _fa_strides(k) + _fa_strides(v) + _fa_strides(o))
+    N.call("pa_flash_attn_fwd", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(o), N.ptr(lse), st,
+           B, Sq, Sk, Hq, Hk, D, float(scale), int(causal), N.stream())
+    return o, lse
+
+
+def _fa_bwd(q, k, v, o, do, lse, causal, scale, dk, dv):
+    """dk/dv: [B, Sk, Hq, D] views (expanded over q heads) written by the kernel."""
+    B, Sq, Hq, D = q.shape
+    Sk, Hk = k.shape[1], k.shape[2]
+    dq_acc = torch.zeros(B, Sq, Hq, D, dtype=torch.float32, device=q.device)
+    delta = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
+    st = ctypes_long_array(_fa_strides(q) + _fa_strides(k) + _fa_strides(v) + _fa_strides(o)
+                           + _fa_strides(do) + _fa_strides(dk))
+    assert dk.stride() == dv.stride()
+    N.call("pa_flash_attn_bwd", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(o), N.ptr(do), N.ptr(lse),
+           N.ptr(delta), N.ptr(dq_acc), N.ptr(dk), N.ptr(dv), st, B, Sq, Sk, Hq, Hk, D,
+           float(scale), int(causal), N.stream())
+    return dq_acc
+
+
+def ctypes_long_array(vals):
+    import ctypes
+    return (ctypes.c_long * len(vals))(*[int(x) for x in vals])
+
+
+class _FlashAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale):
+        o, lse = _fa_fwd(q, k, v, causal, scale)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.causal, ctx.scale = causal, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        do = _c(do)
+        B, Sq, Hq, D = q.shape
+        Sk, Hk = k.shape[1], k.shape[2]
+        dk = torch.empty(B, Sk, Hq, D, dtype=q.dtype, device=q.device)
+        dv = torch.empty_like(dk)
+        dq_acc = _fa_bwd(q, k, v, o, do, lse, ctx.causal, ctx.scale, dk, dv)
+        dq = dq_acc.to(q.dtype)
+        if Hk != Hq:
+            dk = dk.view(B, Sk, Hk, Hq // Hk, D).sum(3)
+            dv = dv.view(B, Sk, Hk, Hq // Hk, D).sum(3)
+        return dq, dk, dv, None, None
+
+
+def flash_attention(q, k, v, causal=True, scale=None):
+    """Fused attention over [B, S, H, D] tensors (GQA when k/v have fewer heads)."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    if q.is_cuda:
+        if q.dtype != torch.bfloat16 or q.shape[-1] not in (64, 128):
+            raise NotImplementedError("flash_attention kernel: bf16 with head_dim 64/128")
+        return _FlashAttnFn.apply(q, k, v, causal, scale)
+    return _attn_ref(q, k, v, causal, scale)
+
+
+class _RopeAttnFn(torch.autograd.Function):
+    """Fused rotary + flash attention over a packed QKV projection output.
+
+    qkv: [B, S, (Hq + 2*Hk) * D].  Forward repacks rotated q|k plus v into one
+    buffer in a single pass (the only activation saved), runs the attention
+    kernel on strided views of it; backward writes dk/dv straight into the
+    packed dqkv gradient and fuses the fp32 dq-accumulator cast with the inverse
+    rotation, so dqkv feeds the QKV GEMM backward with no copies.
+    """
+
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, Hq, Hk, D, causal, scale):
+        B, S, W = qkv.shape
+        nh = Hq + 2 * Hk
+        qkv = _c(qkv)
+        packed = torch.empty_like(qkv)
+        N.call("pa_rope", 1, 1, N.ptr(qkv), W, N.ptr(packed), W, N.ptr(cos), N.ptr(sin), None,
+               B, S, nh, Hq + Hk, D, 0, N.stream())
+        p4 = packed.view(B, S, nh, D)
+        q, k, v = p4[:, :, :Hq], p4[:, :, Hq:Hq + Hk], p4[:, :, Hq + Hk:]
+        o, lse = _fa_fwd(q, k, v, causal, scale)
+        ctx.save_for_backward(packed, o, lse, cos, sin)
+        ctx.cfg = (Hq, Hk, D, causal, scale)
+        return o.view(B, S, Hq * D)
+
+    @staticmethod
+    def backward(ctx, do):
+        packed, o, lse, cos, sin = ctx.saved_tensors
+        Hq, Hk, D, causal, scale = ctx.cfg
+        B, S, W = packed.shape
+        nh = Hq + 2 * Hk
+        p4 = packed.view(B, S, nh, D)
+        q, k, v = p4[:, :, :Hq], p4[:, :, Hq:Hq + Hk], p4[:, :, Hq + Hk:]
+        do = _c(do).view(B, S, Hq, D)
+        dqkv = torch.empty_like(packed)
+        d4 = dqkv.view(B, S, nh, D)
+        if Hk == Hq:
+            dk, dv = d4[:, :, Hq:2 * Hq], d4[:, :, 2 * Hq:]
+            dq_acc = _fa_bwd(q, k, v, o, do, lse, causal, scale, dk, dv)
+        else:
+            dk_e = torch.empty(B, S, Hq, D, dtype=packed.dtype, device=packed.device)
+            dv_e = torch.empty_like(dk_e)
+            dq_acc = _fa_bwd(q, k, v, o, do, lse, causal, scale, dk_e, dv_e)
+            d4[:, :, Hq:Hq + Hk] = dk_e.view(B, S, Hk, Hq // Hk, D).sum(3)
+            d4[:, :, Hq + Hk:] = dv_e.view(B, S, Hk, Hq // Hk, D).sum(3)
+        # dq: fp32 accumulator -> inverse rotation -> bf16 slot of dqkv (one pass)
+        N.call("pa_rope", 0, 1, N.ptr(dq_acc), Hq * D, N.ptr(dqkv), W, N.ptr(cos), N.ptr(sin), None,
+               B, S, Hq, Hq, D, 1, N.stream())
+        # dk: inverse rotation in place inside dqkv
+        kview = dqkv.view(B, S, nh * D)[:, :, Hq * D:]
+        N.call("pa_rope", 1, 1, N.ptr(kview), W, N.ptr(kview), W, N.ptr(cos), N.ptr(sin), None,
+               B, S, Hk, Hk, D, 1, N.stream())
+        return dqkv, None, None, None, None, None, None, None
+
+
+def rope_attention(qkv, cos, sin, num_heads, num_kv_heads=None, causal=True, scale=None):
+    """Rotary (neox) + causal flash attention on a packed [B, S, (Hq+2Hk)*D] tensor.
+    Returns [B, S, Hq*D]."""
+    Hk = num_kv_heads or num_heads
+    B, S, W = qkv.shape
+    D = W // (num_heads + 2 * Hk)
+    if scale is None:
+        scale = 1.0 / math.sqrt(D)
+    if qkv.is_cuda:
+        return _RopeAttnFn.apply(qkv, cos, sin, num_heads, Hk, D, causal, scale)
+    x = qkv.view(B, S, num_heads + 2 * Hk, D)
+    q = _rope_ref(x[:, :, :num_heads], cos, sin)
+    k = _rope_ref(x[:, :, num_heads:num_heads + Hk], cos, sin)
+    v = x[:, :, num_heads + Hk:]
+    return _attn_ref(q, k, v, causal, scale).reshape(B, S, num_heads * D)
+
+
+def apply_rotary(x, cos, sin, inverse=False):
+    """Rotate [B, S, H, D] (neox convention)."""
+    if x.is_cuda:
+        return _RopeFn.apply(x, cos, sin, inverse)
+    return _rope_ref(x, cos, sin, -1.0 if inverse else 1.0)
+
+
+class _RopeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cos, sin, inverse):
+        x = _c(x)
+        B, S, H, D = x.shape
+        y = torch.empty_like(x)
+        N.call("pa_rope", N.dt(x), N.dt(y), N.ptr(x), H * D, N.ptr(y), H * D, N.ptr(cos), N.ptr(sin), None,
+               B, S, H, H, D, int(inverse), N.stream())
+        ctx.save_for_backward(cos, sin)
+        ctx.inverse = inverse
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        cos, sin = ctx.saved_tensors
+        dy = _c(dy)
+        B, S, H, D = dy.shape
+        dx = torch.empty_like(dy)
+        N.call("pa_rope", N.dt(dy), N.dt(dx), N.ptr(dy), H * D, N.ptr(dx), H * D, N.ptr(cos), N.ptr(sin), None,
+               B, S, H, H, D, int(not ctx.inverse), N.stream())
+        return dx, None, None, None
+
+
+# ====================================================================== SwiGLU
+
+
+class _SwiGLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        gu = _c(gu)
+        I2 = gu.shape[-1]
+        I = I2 // 2
+        Nr = gu.numel() // I2
+        out = torch.empty(*gu.shape[:-1], I, dtype=gu.dtype, device=gu.device)
+        N.call("pa_swiglu_fwd", N.dt(gu), N.ptr(gu), N.ptr(out), Nr, I, N.stream())
+        ctx.save_for_backward(gu)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (gu,) = ctx.saved_tensors
+        dout = _c(dout)
+        I2 = gu.shape[-1]
+        dgu = torch.empty_like(gu)
+        N.call("pa_swiglu_bwd", N.dt(gu), N.ptr(gu), N.ptr(dout), N.ptr(dgu), gu.numel() // I2, I2 // 2, N.stream())
+        return dgu
+
+
+def swiglu(x, y=None):
+    """silu(gate) * up.  With one argument, x = [gate | up] along the last axis."""
+    if y is not None:
+        x = torch.cat([x, y], -1)
+    if x.is_cuda and (x.shape[-1] // 2) % 8 == 0:
+        return _SwiGLUFn.apply(x)
+    g, u = x.chunk(2, -1)
+    return (torch.nn.functional.silu(g.float()) * u.float()).to(x.dtype)
+
+
+# ====================================================================== softmax CE
+
+
+class _SoftmaxCEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, label, ignore_index, inplace_grad):
+        V = logits.shape[-1]
+        x = _c(logits).view(-1, V)
+        lab = _c(label).view(-1).long()
+        Nr = x.shape[0]
+        loss = torch.empty(Nr, dtype=torch.float32, device=x.device)
+        lse = torch.empty(Nr, dtype=torch.float32, device=x.device)
+        N.call("pa_softmax_ce_fwd", N.dt(x), N.ptr(x), N.ptr(lab), None, N.ptr(loss), N.ptr(lse), Nr, V,
+               int(ignore_index), N.stream())
+        ctx.save_for_backward(x, lab, lse)
+        ctx.ignore_index, ctx.inplace, ctx.shape = ignore_index, inplace_grad, logits.shape
+        ctx.mark_non_differentiable(lse)
+        return loss.view(label.shape), lse
+
+    @staticmethod
+    def backward(ctx, dloss, _dlse):
+        x, lab, lse = ctx.saved_tensors
+        Nr, V = x.shape
+        dx = x if ctx.inplace else torch.empty_like(x)
+        dl = _c(dloss.float()).view(-1)
+        N.call("pa_softmax_ce_bwd", N.dt(x), N.ptr(x), N.ptr(lab), None, N.ptr(lse), N.ptr(dl), N.ptr(dx),
+               Nr, V, int(ctx.ignore_index), 1.0, N.stream())
+        return dx.view(ctx.shape), None, None, None
+
+
+def softmax_cross_entropy(logits, label, ignore_index=-100, reduction="mean", inplace_grad=False):
+    """Fused log-softmax + NLL over the last axis.  loss is fp32."""
+    if logits.is_cuda:
+        loss, _ = _SoftmaxCEFn.apply(logits, label, ignore_index, inplace_grad)
+    else:
+        lf = logits.float().reshape(-1, logits.shape[-1])
+        loss = torch.nn.functional.cross_entropy(lf, label.reshape(-1).long(), ignore_index=ignore_index,
+                                                 reduction="none").view(label.shape)
+    if reduction == "none":
+        return loss
+    if reduction == "sum":
+        return loss.sum()
+    valid = (label != ignore_index).sum().clamp_min(1)
+    return loss.sum() / valid
+
+
+class _SoftmaxFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, log):
+        V = x.shape[-1]
+        x2 = _c(x).view(-1, V)
+        y = torch.empty_like(x2)
+        N.call("pa_softmax_fwd", N.dt(x2), N.ptr(x2), N.ptr(y), x2.shape[0], V, int(log), N.stream())
+        ctx.save_for_backward(y)
+        ctx.log = log
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        V = y.shape[-1]
+        dy2 = _c(dy).view(-1, V)
+        dx = torch.empty_like(y)
+        N.call("pa_softmax_bwd", N.dt(y), N.ptr(y), N.ptr(dy2), N.ptr(dx), y.shape[0], V, int(ctx.log), N.stream())
+        return dx.view(dy.shape), None
+
+
+def softmax(x, axis=-1, log=False):
+    if x.is_cuda and (axis == -1 or axis == x.dim() - 1) and x.dtype in (torch.float32, torch.bfloat16):
+        return _SoftmaxFn.apply(x, log)
+    return torch.log_softmax(x, axis) if log else torch.softmax(x, axis)
+
+
+# ====================================================================== embedding
+
+
+class _EmbeddingFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, weight, padding_idx):
+        ids_ = _c(ids).view(-1).long()
+        H = weight.shape[1]
+        out = torch.empty(ids_.numel(), H, dtype=weight.dtype, device=weight.device)
+        N.call("pa_embedding_fwd", N.dt(weight), N.ptr(ids_), N.ptr(weight), N.ptr(out), ids_.numel(), H,
+               int(padding_idx), N.stream())
+        ctx.save_for_backward(ids_)
+        ctx.wshape, ctx.wdtype, ctx.pad = weight.shape, weight.dtype, padding_idx
+        return out.view(*ids.shape, H)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (ids_,) = ctx.saved_tensors
+        H = ctx.wshape[1]
+        d = _c(dout).view(-1, H)
+        dW = torch.zeros(ctx.wshape, dtype=torch.float32, device=d.device)
+        N.call("pa_embedding_bwd", N.dt(d), N.ptr(ids_), N.ptr(d), N.ptr(dW), ids_.numel(), H, int(ctx.pad), N.stream())
+        return None, dW.to(ctx.wdtype), None
+
+
+def embedding(ids, weight, padding_idx=None):
+    pad = -1 if padding_idx is None else int(padding_idx)
+    if weight.is_cuda and weight.shape[1] % 8 == 0:
+        return _EmbeddingFn.apply(ids, weight, pad)
+    return torch.nn.functional.embedding(ids.long(), weight, padding_idx=padding_idx)

@@ -1,0 +1,204 @@
+"""Numerics of the hand-written gfx950 kernels against plain PyTorch fp32 references.
+
+Methodology follows the reference's OpTest (python/paddle/fluid/tests/unittests/
+op_test.py:363 check_output / :395 check_grad): forward compared with a tolerance,
+backward compared against an independent gradient (here autograd of the fp32
+reference instead of finite differences).
+"""
+import math
+
+import pytest
+import torch
+
+from paddle_amd.ops import fused as F
+from paddle_amd.ops import _native
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def test_native_library_loaded():
+    assert _native.available()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("H", [4096, 1000, 8192])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_rms_norm(dtype, H, with_res):
+    torch.manual_seed(0)
+    Nr = 257
+    x = torch.randn(Nr, H, device=dev, dtype=dtype, requires_grad=True)
+    r = torch.randn(Nr, H, device=dev, dtype=dtype, requires_grad=True) if with_res else None
+    w = (1 + 0.1 * torch.randn(H, device=dev, dtype=dtype)).requires_grad_()
+    if with_res:
+        y, h = F.rms_norm(x, w, 1e-6, residual=r)
+        (y.float().pow(2).sum() + (h.float() * 0.5).sum()).backward()
+    else:
+        y = F.rms_norm(x, w, 1e-6)
+        y.float().pow(2).sum().backward()
+    xr = x.detach().float().requires_grad_()
+    rr = r.detach().float().requires_grad_() if with_res else None
+    wr = w.detach().float().requires_grad_()
+    hr = xr + rr if with_res else xr
+    yr = hr * torch.rsqrt(hr.pow(2).mean(-1, keepdim=True) + 1e-6) * wr
+    loss = yr.pow(2).sum() + ((hr * 0.5).sum() if with_res else 0)
+    loss.backward()
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    assert _rel(y, yr) < tol
+    assert _rel(x.grad, xr.grad) < tol
+    assert _rel(w.grad, wr.grad) < tol
+    if with_res:
+        assert _rel(r.grad, rr.grad) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_layer_norm(dtype):
+    torch.manual_seed(0)
+    x = torch.randn(300, 1024, device=dev, dtype=dtype, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(1024, device=dev, dtype=dtype)).requires_grad_()
+    b = (0.1 * torch.randn(1024, device=dev, dtype=dtype)).requires_grad_()
+    y = F.layer_norm(x, w, b, 1e-5)
+    y.float().pow(2).sum().backward()
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = torch.nn.functional.layer_norm(xr, (1024,), wr, br, 1e-5)
+    yr.pow(2).sum().backward()
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    assert _rel(y, yr) < tol
+    for a, b_ in ((x, xr), (w, wr), (b, br)):
+        assert _rel(a.grad, b_.grad) < tol
+
+
+def test_swiglu():
+    torch.manual_seed(0)
+    gu = torch.randn(513, 2 * 1376, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    y = F.swiglu(gu)
+    y.float().pow(2).sum().backward()
+    gr = gu.detach().float().requires_grad_()
+    g, u = gr.chunk(2, -1)
+    yr = torch.nn.functional.silu(g) * u
+    yr.pow(2).sum().backward()
+    assert _rel(y, yr) < 1e-2
+    assert _rel(gu.grad, gr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("V", [32000, 1001])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_softmax_ce(V, dtype):
+    torch.manual_seed(0)
+    x = (3 * torch.randn(129, V, device=dev)).to(dtype).requires_grad_()
+    lab = torch.randint(0, V, (129,), device=dev)
+    lab[5] = -100
+    loss = F.softmax_cross_entropy(x, lab)
+    loss.backward()
+    xr = x.detach().float().requires_grad_()
+    lr = torch.nn.functional.cross_entropy(xr, lab, ignore_index=-100)
+    lr.backward()
+    assert abs(loss.item() - lr.item()) < 1e-3 * max(1, abs(lr.item()))
+    assert _rel(x.grad, xr.grad) < (2e-2 if dtype == torch.bfloat16 else 1e-4)
+
+
+def test_softmax():
+    torch.manual_seed(0)
+    x = torch.randn(64, 777, device=dev, requires_grad=True)
+    y = F.softmax(x)
+    (y * torch.arange(777, device=dev)).sum().backward()
+    xr = x.detach().requires_grad_()
+    yr = torch.softmax(xr, -1)
+    (yr * torch.arange(777, device=dev)).sum().backward()
+    assert _rel(y, yr) < 1e-5
+    assert _rel(x.grad, xr.grad) < 1e-4
+
+
+def test_embedding():
+    torch.manual_seed(0)
+    W = torch.randn(1000, 256, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    ids = torch.randint(0, 1000, (4, 77), device=dev)
+    y = F.embedding(ids, W)
+    (y.float() * 2).sum().backward()
+    Wr = W.detach().float().requires_grad_()
+    yr = torch.nn.functional.embedding(ids, Wr)
+    (yr * 2).sum().backward()
+    assert _rel(y, yr) < 1e-6
+    assert _rel(W.grad, Wr.grad) < 1e-2
+
+
+def test_rope():
+    torch.manual_seed(0)
+    B, S, H, D = 2, 100, 4, 128
+    cos, sin = F.rope_tables(S, D, device=dev)
+    x = torch.randn(B, S, H, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    y = F.apply_rotary(x, cos, sin)
+    (y.float() * torch.linspace(-1, 1, D, device=dev)).sum().backward()
+    xr = x.detach().float().requires_grad_()
+    yr = F._rope_ref(xr, cos, sin)
+    (yr * torch.linspace(-1, 1, D, device=dev)).sum().backward()
+    assert _rel(y, yr) < 1e-2
+    assert _rel(x.grad, xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("S,D,Hq,Hk", [(256, 128, 4, 4), (384, 128, 4, 2), (200, 64, 2, 2), (1024, 128, 2, 2)])
+def test_flash_attention(causal, S, D, Hq, Hk):
+    torch.manual_seed(0)
+    B = 2
+    q = torch.randn(B, S, Hq, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, Hk, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, Hk, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    do = torch.randn(B, S, Hq, D, device=dev, dtype=torch.bfloat16)
+    o = F.flash_attention(q, k, v, causal=causal)
+    o.backward(do)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = F._attn_ref(qr, kr, vr, causal, 1 / math.sqrt(D))
+    orf.backward(do.float())
+    assert _rel(o, orf) < 1e-2, _rel(o, orf)
+    assert _rel(q.grad, qr.grad) < 2e-2, _rel(q.grad, qr.grad)
+    assert _rel(k.grad, kr.grad) < 2e-2, _rel(k.grad, kr.grad)
+    assert _rel(v.grad, vr.grad) < 2e-2, _rel(v.grad, vr.grad)
+
+
+def test_rope_attention_packed():
+    torch.manual_seed(0)
+    B, S, H, D = 2, 256, 4, 128
+    cos, sin = F.rope_tables(S, D, device=dev)
+    qkv = torch.randn(B, S, 3 * H * D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    o = F.rope_attention(qkv, cos, sin, H)
+    do = torch.randn_like(o)
+    o.backward(do)
+    xr = qkv.detach().float().requires_grad_()
+    x4 = xr.view(B, S, 3 * H, D)
+    q = F._rope_ref(x4[:, :, :H], cos, sin)
+    k = F._rope_ref(x4[:, :, H:2 * H], cos, sin)
+    orf = F._attn_ref(q, k, x4[:, :, 2 * H:], True, 1 / math.sqrt(D)).reshape(B, S, H * D)
+    orf.backward(do.float())
+    assert _rel(o, orf) < 1e-2
+    assert _rel(qkv.grad, xr.grad) < 2e-2
+
+
+def test_adamw_flat():
+    from paddle_amd.ops import optim
+
+    torch.manual_seed(0)
+    n = 10007
+    p = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev).to(torch.bfloat16)
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    pb = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    pr, mr, vr = p.clone(), m.clone(), v.clone()
+    for step in range(1, 4):
+        optim.adamw_flat(p, g, m, v, lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.1, step=step,
+                         param_out=pb, decay_end=5000)
+        gf = g.float()
+        mr = 0.9 * mr + 0.1 * gf
+        vr = 0.95 * vr + 0.05 * gf * gf
+        decay = torch.where(torch.arange(n, device=dev) < 5000, 0.1, 0.0)
+        pr = pr * (1 - 1e-3 * decay)
+        pr = pr - 1e-3 * (mr / (1 - 0.9 ** step)) / ((vr / (1 - 0.95 ** step)).sqrt() + 1e-8)
+    assert _rel(p, pr) < 1e-5
+    assert _rel(pb, pr) < 1e-2
