@@ -288,6 +288,16 @@ __global__ void fa_bwd_pre_kernel(BwdParams p) {
 #pragma unroll
   for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   if (row < total && c == 0) p.delta[row] = s;
+  // fused zero-init of this row's fp32 dQ accumulator ([B, Sq, Hq, D])
+  if (row < total) {
+    const long q = row % p.Sq;
+    const long bh = row / p.Sq;
+    const int h = (int)(bh % p.Hq), b = (int)(bh / p.Hq);
+    float* dq = p.dq_acc + (((long)b * p.Sq + q) * p.Hq + h) * D + c * 8;
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<f32x4*>(dq) = z;
+    *reinterpret_cast<f32x4*>(dq + 4) = z;
+  }
 }
 
 template <int D, bool CAUSAL>
@@ -506,7 +516,7 @@ PA_EXPORT int pa_flash_attn_fwd(const void* q, const void* k, const void* v, voi
   PA_LAUNCH_CHECK();
 }
 
-// dq_acc ([B, Sq, Hq, D] fp32) must be zeroed by the caller; dk/dv share strides
+// dq_acc ([B, Sq, Hq, D] fp32) is zeroed by the pre-pass; dk/dv share strides
 // strides[15..17] and are indexed by the q-head (GQA callers reduce head groups).
 PA_EXPORT int pa_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o,
                                 const void* dout, const float* lse, float* delta, float* dq_acc,

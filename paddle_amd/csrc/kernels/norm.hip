@@ -196,14 +196,20 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
   }
 }
 
-// Column sum of a [G, H] fp32 partial matrix into out[H] (dtype T).
+// Column sum of a [G, H] fp32 partial matrix into out[H] (dtype T).  Each block
+// owns 64 columns; its 4 waves split the G rows and fold through LDS, so H/64
+// blocks x 4 waves cover the chip even for H = 4096 (64 blocks).
 template <typename T>
-__global__ void colsum_kernel(const float* __restrict__ part, T* __restrict__ out, int G, int H) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= H) return;
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, T* __restrict__ out, int G, int H) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int g = 0; g < G; ++g) s += part[(long)g * H + c];
-  IO<T>::st(out, c, s);
+  if (c < H)
+    for (int g = w; g < G; g += 4) s += part[(long)g * H + c];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c < H) IO<T>::st(out, c, red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
 }
 
 template <typename T, int MAXV>
@@ -243,8 +249,8 @@ static int launch_bwd(bool rms, const void* dy, const void* h, const void* w, co
   if (rms) { if (dres) PA_NB(true, true); else PA_NB(true, false); }
   else { if (dres) PA_NB(false, true); else PA_NB(false, false); }
 #undef PA_NB
-  hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 255) / 256), dim3(256), 0, st, dwp, (T*)dw, G, H);
-  if (!rms && db) hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 255) / 256), dim3(256), 0, st, dbp, (T*)db, G, H);
+  hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 63) / 64), dim3(256), 0, st, dwp, (T*)dw, G, H);
+  if (!rms && db) hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 63) / 64), dim3(256), 0, st, dbp, (T*)db, G, H);
   PA_LAUNCH_CHECK();
 }
 

@@ -82,13 +82,20 @@ __global__ void momentum_kernel(float* __restrict__ p, const TG* __restrict__ g,
   }
 }
 
-// sum of squares (for global-norm clipping): out[0] += sum(x^2) (fp32 atomics, one per block)
+// sum of squares (for global-norm clipping): out[0] += sum(x^2); 16-B vector loads,
+// one fp32 atomic per block.
 template <typename T>
-__global__ void sumsq_kernel(const T* __restrict__ x, long n, float* __restrict__ out) {
+__global__ __launch_bounds__(256) void sumsq_kernel(const T* __restrict__ x, long n, float* __restrict__ out) {
   __shared__ float red[4];
   float s = 0.f;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (long)gridDim.x * blockDim.x) {
+  const long n8 = n / 8;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float v[8];
+    load8(x + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[j] * v[j];
+  }
+  for (long i = n8 * 8 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float v = IO<T>::ld(x, i);
     s += v * v;
   }
@@ -130,7 +137,7 @@ PA_EXPORT int pa_momentum(int gdtype, float* p, const void* g, float* vel, long 
 
 PA_EXPORT int pa_sumsq(int dtype, const void* x, long n, float* out, hipStream_t st) {
   if (n == 0) return 0;
-  const int grid = stream_grid(n, 256);
+  const int grid = stream_grid((n + 7) / 8, 256);
   if (dtype == 1)
     hipLaunchKernelGGL(sumsq_kernel<u16>, dim3(grid), dim3(256), 0, st, (const u16*)x, n, out);
   else

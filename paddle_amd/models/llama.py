@@ -113,15 +113,15 @@ class LlamaDecoderLayer(Layer):
             y, h = ops.rms_norm(x, self.input_layernorm, eps, residual=residual)
         if self.tp is not None:
             y = self.tp.copy_to_region(y)
-        qkv = torch.matmul(y, self.qkv_proj)
+        qkv = ops.linear(y, self.qkv_proj)
         a = ops.rope_attention(qkv, cos, sin, self.nh, self.nkv, causal=True)
-        a = torch.matmul(a, self.o_proj)
+        a = ops.linear(a, self.o_proj)
         if self.tp is not None:
             a = self.tp.reduce_from_region(a)
         y2, h2 = ops.rms_norm(a, self.post_attention_layernorm, eps, residual=h)
         if self.tp is not None:
             y2 = self.tp.copy_to_region(y2)
-        m = torch.matmul(ops.swiglu(torch.matmul(y2, self.gate_up_proj)), self.down_proj)
+        m = ops.linear(ops.swiglu(ops.linear(y2, self.gate_up_proj)), self.down_proj)
         if self.tp is not None:
             m = self.tp.reduce_from_region(m)
         return m, h2
@@ -159,8 +159,10 @@ class LlamaForCausalLM(Layer):
 
     def forward(self, input_ids, labels=None):
         y = self.hidden_states(input_ids)
-        w = self.lm_head if self.lm_head is not None else self.embed_tokens.t()
-        logits = torch.matmul(y, w)
+        if self.lm_head is not None:
+            logits = ops.linear(y, self.lm_head)
+        else:
+            logits = torch.matmul(y, self.embed_tokens.t())
         if labels is None:
             return logits
         # in-place CE gradient over the logits buffer (nothing else consumes it)

@@ -167,7 +167,7 @@ def _fa_bwd(q, k, v, o, do, lse, causal, scale, dk, dv):
     """dk/dv: [B, Sk, Hq, D] views (expanded over q heads) written by the kernel."""
     B, Sq, Hq, D = q.shape
     Sk, Hk = k.shape[1], k.shape[2]
-    dq_acc = torch.zeros(B, Sq, Hq, D, dtype=torch.float32, device=q.device)
+    dq_acc = torch.empty(B, Sq, Hq, D, dtype=torch.float32, device=q.device)  # zeroed in-kernel
     delta = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
     st = ctypes_long_array(_fa_strides(q) + _fa_strides(k) + _fa_strides(v) + _fa_strides(o)
                            + _fa_strides(do) + _fa_strides(dk))
@@ -458,3 +458,48 @@ def embedding(ids, weight, padding_idx=None):
     if weight.is_cuda and weight.shape[1] % 8 == 0:
         return _EmbeddingFn.apply(ids, weight, pad)
     return torch.nn.functional.embedding(ids.long(), weight, padding_idx=padding_idx)
+
+
+# ====================================================================== linear
+
+
+class _LinearFn(torch.autograd.Function):
+    """y = x W (+ b) with W in Paddle's [in, out] layout.
+
+    If the weight carries ``_pa_main_grad`` (a view into a flat gradient buffer
+    owned by the sharded DP engine), the weight-gradient GEMM accumulates straight
+    into it (hipBLASLt beta=1: dW += x^T dy, one rounding); the engine's
+    post-accumulate-grad hook still fires for w, so bucket readiness is unchanged
+    -- no temporary dW, no separate accumulate kernel.
+    """
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        y = torch.matmul(x, w)
+        if b is not None:
+            y = y + b
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = torch.matmul(dy, w.t()) if ctx.needs_input_grad[0] else None
+        dw = db = None
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if ctx.needs_input_grad[1]:
+            x2 = x.reshape(-1, x.shape[-1])
+            mg = getattr(w, "_pa_main_grad", None)
+            if mg is not None:
+                # the engine's post-accumulate hook still fires for w (grad None)
+                mg.addmm_(x2.t(), dy2)
+            else:
+                dw = torch.matmul(x2.t(), dy2)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = dy2.sum(0).to(dy.dtype)
+        return dx, dw, db
+
+
+def linear(x, weight, bias=None):
+    return _LinearFn.apply(x, weight, bias)

@@ -99,6 +99,8 @@ class FlatShardedOptimizer:
                 self.flat_param[o:o + p.numel()].copy_(p.data.reshape(-1))
                 p.data = self.flat_param[o:o + p.numel()].view(p.shape)
                 p.grad = self.flat_grad[o:o + p.numel()].view(p.shape)
+                # fused-GEMM gradient accumulation target (ops.linear)
+                p._pa_main_grad = p.grad
         self.buckets = buckets
         # --- shard layout: rank r owns slice r of every bucket
         self.shard_slices = []  # (bucket_start + r*L, L, shard_off)
@@ -150,7 +152,7 @@ class FlatShardedOptimizer:
         return _Ctx()
 
     def _on_grad(self, p):
-        if not self._sync:
+        if self.W == 1 or not self._sync:
             return
         b = self._bucket_of[id(p)]
         self._ready[b] += 1

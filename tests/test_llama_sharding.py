@@ -1,0 +1,93 @@
+"""LLaMA + flat sharded DP engine on CPU (gloo), in the spirit of the reference's
+parallel_executor_test_base.check_network_convergence
+(python/paddle/fluid/tests/unittests/parallel_executor_test_base.py:29):
+the same model trained data-parallel on 2 ranks must match single-process
+training on the concatenated batch."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from paddle_amd.models.llama import LLAMA_CONFIGS, LlamaConfig, LlamaForCausalLM
+from paddle_amd.parallel.sharding import FlatShardedOptimizer
+
+
+def _cfg():
+    return LlamaConfig(**LLAMA_CONFIGS["llama-tiny"], dtype="float32")
+
+
+def _batches(n, B=4, S=33, V=512):
+    g = torch.Generator().manual_seed(7)
+    return [torch.randint(0, V, (B, S), generator=g) for _ in range(n)]
+
+
+def _train_single(steps):
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(_cfg(), device="cpu")
+    opt = FlatShardedOptimizer(m.named_parameters(), lr=1e-3, grad_clip=1.0, bucket_mb=1)
+    losses = []
+    for b in _batches(steps):
+        loss = m(b[:, :-1], b[:, 1:])
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        losses.append(loss.item())
+    return losses, torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+
+
+def _worker(rank, world, port, steps, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(_cfg(), device="cpu")
+    opt = FlatShardedOptimizer(m.named_parameters(), lr=1e-3, grad_clip=1.0, bucket_mb=1)
+    assert len(opt.buckets) > 1
+    losses = []
+    for b in _batches(steps):
+        part = b.chunk(world)[rank]
+        loss = m(part[:, :-1], part[:, 1:])
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        t = torch.tensor([loss.item()])
+        dist.all_reduce(t)
+        losses.append(t.item() / world)
+    if rank == 0:
+        q.put((losses, torch.cat([p.detach().reshape(-1) for p in m.parameters()])))
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_tiny_llama_cpu_converges():
+    losses, _ = _train_single(15)
+    assert losses[-1] < losses[0]
+
+
+def test_sharded_dp_matches_single_process():
+    steps = 4
+    ref_losses, ref_params = _train_single(steps)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, steps, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    losses, params = q.get(timeout=300)
+    for p in procs:
+        p.join(60)
+    assert all(p.exitcode == 0 for p in procs)
+    for a, b in zip(losses, ref_losses):
+        assert abs(a - b) < 1e-4, (losses, ref_losses)
+    assert torch.allclose(params, ref_params, atol=1e-5, rtol=1e-4)
