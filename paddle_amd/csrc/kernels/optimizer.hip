@@ -17,13 +17,16 @@ __global__ void adamw_kernel(float* __restrict__ p, const TG* __restrict__ g, fl
                              const float* __restrict__ lr_ptr, float b1, float b2, float eps,
                              float wd, float bc1, float bc2, const float* __restrict__ b1pow,
                              const float* __restrict__ b2pow, long decay_end, float gscale,
-                             const float* __restrict__ gscale_ptr) {
+                             const float* __restrict__ gscale_ptr, int lr_t_eps) {
   float lr_ = lr_ptr ? lr_ptr[0] : lr;
   float c1 = b1pow ? 1.f - b1pow[0] : bc1;
   float c2 = b2pow ? 1.f - b2pow[0] : bc2;
   const float gs = gscale_ptr ? gscale_ptr[0] * gscale : gscale;
   const float step = lr_ / c1;
   const float rc2 = rsqrtf(c2);
+  // lr_t_eps: Kingma/Paddle form lr_t = lr*sqrt(c2)/c1, p -= lr_t*m/(sqrt(v)+eps)
+  // (adam_op.h); otherwise eps is added to the bias-corrected sqrt(v/c2) (AdamW form).
+  const float eps_ = lr_t_eps ? eps * rc2 : eps;
   const long n4 = n / 4;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (long)gridDim.x * blockDim.x) {
@@ -39,7 +42,7 @@ __global__ void adamw_kernel(float* __restrict__ p, const TG* __restrict__ g, fl
       mm[j] = b1 * mm[j] + (1.f - b1) * gg[j];
       vv[j] = b2 * vv[j] + (1.f - b2) * gg[j] * gg[j];
       const float decay = (e + j) < decay_end ? wd : 0.f;
-      pp[j] = pp[j] * (1.f - lr_ * decay) - step * mm[j] / (sqrtf(vv[j]) * rc2 + eps);
+      pp[j] = pp[j] * (1.f - lr_ * decay) - step * mm[j] / (sqrtf(vv[j]) * rc2 + eps_);
     }
     *reinterpret_cast<f32x4*>(p + e) = pp;
     *reinterpret_cast<f32x4*>(m + e) = mm;
@@ -56,7 +59,7 @@ __global__ void adamw_kernel(float* __restrict__ p, const TG* __restrict__ g, fl
     float mm = b1 * m[e] + (1.f - b1) * gg;
     float vv = b2 * v[e] + (1.f - b2) * gg * gg;
     const float decay = e < decay_end ? wd : 0.f;
-    float pp = p[e] * (1.f - lr_ * decay) - step * mm / (sqrtf(vv) * rc2 + eps);
+    float pp = p[e] * (1.f - lr_ * decay) - step * mm / (sqrtf(vv) * rc2 + eps_);
     p[e] = pp; m[e] = mm; v[e] = vv;
     if (pout) IO<TP>::st(pout, e, pp);
   }
@@ -112,11 +115,11 @@ PA_EXPORT int pa_adamw(int gdtype, int pdtype, float* p, const void* g, float* m
                        void* pout, long n, float lr, const float* lr_ptr, float b1, float b2,
                        float eps, float wd, float bc1, float bc2, const float* b1pow,
                        const float* b2pow, long decay_end, float gscale, const float* gscale_ptr,
-                       hipStream_t st) {
+                       int lr_t_eps, hipStream_t st) {
   if (n == 0) return 0;
   const int grid = stream_grid((n + 3) / 4, 256);
 #define PA_A(TG, TP) \
-  hipLaunchKernelGGL((adamw_kernel<TG, TP>), dim3(grid), dim3(256), 0, st, p, (const TG*)g, m, v, (TP*)pout, n, lr, lr_ptr, b1, b2, eps, wd, bc1, bc2, b1pow, b2pow, decay_end, gscale, gscale_ptr)
+  hipLaunchKernelGGL((adamw_kernel<TG, TP>), dim3(grid), dim3(256), 0, st, p, (const TG*)g, m, v, (TP*)pout, n, lr, lr_ptr, b1, b2, eps, wd, bc1, bc2, b1pow, b2pow, decay_end, gscale, gscale_ptr, lr_t_eps)
   if (gdtype == 1) { if (pdtype == 1) PA_A(u16, u16); else PA_A(u16, float); }
   else { if (pdtype == 1) PA_A(float, u16); else PA_A(float, float); }
 #undef PA_A

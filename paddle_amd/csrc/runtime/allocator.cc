@@ -1,0 +1,205 @@
+// Buddy allocator over HIP device (or host) arenas.
+//
+// Reference: memory/detail/buddy_allocator.{h,cc} (Alloc :52, RefillPool :185) on a
+// SystemAllocator (hipMalloc / posix_memalign); first device chunk =
+// FLAGS_fraction_of_gpu_memory_to_use of free memory.  MI355X version: arenas are
+// large power-of-two hipMalloc regions (288 GB HBM -> few, huge arenas), blocks are
+// split/merged by order with per-order free sets, 256-B minimum block (matches the
+// 256-B alignment the gfx950 kernels rely on for 16-B vector loads).  Exposes the
+// torch "pluggable allocator" entry points so PyTorch tensors can live in it
+// (FLAGS_allocator_strategy=buddy).
+#include <hip/hip_runtime_api.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <map>
+#include <mutex>
+#include <set>
+#include <unordered_map>
+#include <vector>
+
+#include "runtime.h"
+
+namespace {
+constexpr int kMinOrder = 8;  // 256 B
+
+struct Arena {
+  char* base;
+  int order;  // arena size = 1 << order
+  std::vector<std::set<size_t>> free_by_order;  // offsets
+};
+
+struct Buddy {
+  int device = -1;  // -1 = host
+  size_t chunk = 1ull << 30;
+  bool init_mem = false;
+  std::vector<Arena> arenas;
+  std::unordered_map<char*, std::pair<int, int>> live;  // ptr -> (arena, order)
+  size_t used = 0, reserved = 0, peak = 0;
+  std::mutex mu;
+
+  static int order_for(size_t n) {
+    int o = kMinOrder;
+    while ((1ull << o) < n) ++o;
+    return o;
+  }
+
+  bool refill(int need_order) {
+    int o = order_for(chunk);
+    if (o < need_order) o = need_order;
+    size_t sz = 1ull << o;
+    char* p = nullptr;
+    if (device >= 0) {
+      int prev;
+      hipGetDevice(&prev);
+      hipSetDevice(device);
+      hipError_t e = hipMalloc((void**)&p, sz);
+      hipSetDevice(prev);
+      if (e != hipSuccess) {
+        pa_rt_set_error("hipMalloc(%zu) failed: %d", sz, (int)e);
+        return false;
+      }
+    } else {
+      if (posix_memalign((void**)&p, 4096, sz) != 0) {
+        pa_rt_set_error("posix_memalign(%zu) failed", sz);
+        return false;
+      }
+    }
+    Arena a;
+    a.base = p;
+    a.order = o;
+    a.free_by_order.resize(o + 1);
+    a.free_by_order[o].insert(0);
+    arenas.push_back(std::move(a));
+    reserved += sz;
+    return true;
+  }
+
+  void* alloc(size_t n) {
+    std::lock_guard<std::mutex> g(mu);
+    int want = order_for(n ? n : 1);
+    for (int pass = 0; pass < 2; ++pass) {
+      for (size_t ai = 0; ai < arenas.size(); ++ai) {
+        Arena& a = arenas[ai];
+        for (int o = want; o <= a.order; ++o) {
+          if (a.free_by_order[o].empty()) continue;
+          size_t off = *a.free_by_order[o].begin();
+          a.free_by_order[o].erase(a.free_by_order[o].begin());
+          while (o > want) {  // split, keep lower half
+            --o;
+            a.free_by_order[o].insert(off + (1ull << o));
+          }
+          char* p = a.base + off;
+          live[p] = {(int)ai, want};
+          used += 1ull << want;
+          if (used > peak) peak = used;
+          if (init_mem && device < 0) memset(p, 0xCD, 1ull << want);
+          return p;
+        }
+      }
+      if (pass == 0 && !refill(want)) return nullptr;
+    }
+    return nullptr;
+  }
+
+  int release(void* ptr) {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = live.find((char*)ptr);
+    if (it == live.end()) {
+      pa_rt_set_error("free of unknown pointer");
+      return -1;
+    }
+    int ai = it->second.first, o = it->second.second;
+    live.erase(it);
+    used -= 1ull << o;
+    Arena& a = arenas[ai];
+    size_t off = (char*)ptr - a.base;
+    while (o < a.order) {  // merge with buddy while it is free
+      size_t bud = off ^ (1ull << o);
+      auto f = a.free_by_order[o].find(bud);
+      if (f == a.free_by_order[o].end()) break;
+      a.free_by_order[o].erase(f);
+      off = off < bud ? off : bud;
+      ++o;
+    }
+    a.free_by_order[o].insert(off);
+    return 0;
+  }
+
+  ~Buddy() {
+    for (auto& a : arenas) {
+      if (device >= 0) hipFree(a.base);
+      else free(a.base);
+    }
+  }
+};
+
+std::mutex g_mu;
+std::map<int, Buddy*> g_torch;  // device -> allocator used by the torch hook
+size_t g_torch_chunk = 4ull << 30;
+}  // namespace
+
+PA_RT_EXPORT void* pa_buddy_create(int device, size_t chunk_bytes, int init_mem) {
+  Buddy* b = new Buddy();
+  b->device = device;
+  if (chunk_bytes) b->chunk = chunk_bytes;
+  b->init_mem = init_mem != 0;
+  return b;
+}
+
+PA_RT_EXPORT void pa_buddy_destroy(void* h) { delete (Buddy*)h; }
+PA_RT_EXPORT void* pa_buddy_alloc(void* h, size_t n) { return ((Buddy*)h)->alloc(n); }
+PA_RT_EXPORT int pa_buddy_free(void* h, void* p) { return ((Buddy*)h)->release(p); }
+
+PA_RT_EXPORT void pa_buddy_stats(void* h, size_t* used, size_t* reserved, size_t* peak, size_t* narenas) {
+  Buddy* b = (Buddy*)h;
+  std::lock_guard<std::mutex> g(b->mu);
+  *used = b->used;
+  *reserved = b->reserved;
+  *peak = b->peak;
+  *narenas = b->arenas.size();
+}
+
+// ---- torch CUDAPluggableAllocator hooks (HIP build of torch uses hipStream_t)
+PA_RT_EXPORT void pa_torch_set_chunk(size_t bytes) { g_torch_chunk = bytes; }
+
+PA_RT_EXPORT void* pa_torch_malloc(ssize_t size, int device, hipStream_t) {
+  Buddy* b;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    auto it = g_torch.find(device);
+    if (it == g_torch.end()) {
+      b = new Buddy();
+      b->device = device;
+      b->chunk = g_torch_chunk;
+      g_torch[device] = b;
+    } else {
+      b = it->second;
+    }
+  }
+  return b->alloc((size_t)size);
+}
+
+PA_RT_EXPORT void pa_torch_free(void* ptr, ssize_t, int device, hipStream_t stream) {
+  Buddy* b;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    b = g_torch[device];
+  }
+  // stream-ordered reuse: a freed block may still be read by queued kernels on
+  // `stream`; wait for them before recycling (same-stream reuse would be safe,
+  // but other streams may pick the block next).
+  if (stream) hipStreamSynchronize(stream);
+  if (b) b->release(ptr);
+}
+
+PA_RT_EXPORT void pa_torch_stats(int device, size_t* used, size_t* reserved, size_t* peak) {
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_torch.find(device);
+  if (it == g_torch.end()) {
+    *used = *reserved = *peak = 0;
+    return;
+  }
+  size_t n;
+  pa_buddy_stats(it->second, used, reserved, peak, &n);
+}

@@ -1,0 +1,26 @@
+"""Synthetic flowers reader (no network here).  Sample: image: float32[3*224*224], label: int in [0,102)."""
+import numpy as np
+
+TRAIN_SIZE = 6149
+TEST_SIZE = 1020
+_GEN = lambda r: (r.uniform(0, 1, 3 * 224 * 224).astype('float32'), int(r.randint(0, 102)))
+
+
+def _reader(n, seed):
+    def r():
+        rng = np.random.RandomState(seed)
+        for _ in range(n):
+            yield _GEN(rng)
+    return r
+
+
+def train(*args, **kwargs):
+    return _reader(TRAIN_SIZE, 1)
+
+
+def test(*args, **kwargs):
+    return _reader(TEST_SIZE, 2)
+
+
+def fetch():
+    pass

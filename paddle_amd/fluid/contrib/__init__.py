@@ -1,0 +1,3 @@
+"""fluid.contrib: beam-search decoder helpers and memory usage estimation."""
+from . import memory_usage_calc  # noqa: F401
+from .memory_usage_calc import memory_usage  # noqa: F401

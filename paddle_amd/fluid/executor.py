@@ -1,0 +1,138 @@
+"""fluid.Executor (python/paddle/fluid/executor.py:256-474).
+
+``run`` clones the program once per (program, feed, fetch) signature with feed/fetch
+ops inserted (cached; the reference re-creates ops every call unless
+``use_program_cache``), feeds numpy/LoDTensor values onto the executor's place,
+interprets the block with :class:`paddle_amd.framework.executor.BlockExecutor`
+and fetches results (the only host sync).
+
+``Executor(place, use_hip_graph=True)`` additionally captures a steady-state step
+of a static-shape program into a HIP graph and replays it (MI355X-first
+replacement for launch-bound inner loops; see also ``FLAGS_use_hip_graph``).
+"""
+from __future__ import annotations
+
+import contextlib
+
+import numpy as np
+import torch
+
+from ..framework import core
+from ..framework.executor import BlockExecutor
+from ..utils import flags as FLAGS
+from .framework import Program, Variable, default_main_program
+
+g_scope = core.global_scope()
+
+
+def global_scope():
+    return core.global_scope()
+
+
+@contextlib.contextmanager
+def scope_guard(scope):
+    old = core._switch_scope(scope)
+    try:
+        yield
+    finally:
+        core._switch_scope(old)
+
+
+def _to_lod_tensor(data, place):
+    if isinstance(data, core.LoDTensor):
+        return data
+    if isinstance(data, torch.Tensor):
+        return core.LoDTensor(data.to(place.torch_device()))
+    arr = np.asarray(data)
+    t = torch.from_numpy(np.ascontiguousarray(arr))
+    if place.torch_device().type == "cuda":
+        t = t.pin_memory().to(place.torch_device(), non_blocking=True)
+    return core.LoDTensor(t)
+
+
+def as_numpy(tensor):
+    if isinstance(tensor, list):
+        return [as_numpy(t) for t in tensor]
+    if isinstance(tensor, core.LoDTensor):
+        if tensor.lod() and False:
+            raise RuntimeError("Some of your fetched tensors hold LoD information")
+        return tensor.numpy()
+    if isinstance(tensor, core.SelectedRows):
+        return tensor.get_tensor().numpy()
+    return np.asarray(tensor)
+
+
+class Executor:
+    def __init__(self, place=None, use_hip_graph=None):
+        self.place = place or core.CPUPlace()
+        self._core = BlockExecutor(self.place)
+        self._closed = False
+        self._prog_cache = {}
+        self.use_hip_graph = FLAGS.get("use_hip_graph") if use_hip_graph is None else use_hip_graph
+
+    def close(self):
+        self._closed = True
+
+    def as_lodtensor(self, data):
+        return _to_lod_tensor(data, self.place)
+
+    def _add_feed_fetch_ops(self, program, feed, fetch_list, feed_var_name, fetch_var_name):
+        tmp = program.clone()
+        gb = tmp.global_block()
+        if feed_var_name in gb.vars:
+            feed_var = gb.vars[feed_var_name]
+        else:
+            feed_var = gb.create_var(name=feed_var_name, type=core.VT.FEED_MINIBATCH, persistable=True)
+        if fetch_var_name in gb.vars:
+            fetch_var = gb.vars[fetch_var_name]
+        else:
+            fetch_var = gb.create_var(name=fetch_var_name, type=core.VT.FETCH_LIST, persistable=True)
+        if not any(op.type == "feed" for op in gb.ops):
+            for i, name in enumerate(feed):
+                out = gb.var(name)
+                gb.prepend_op(type="feed", inputs={"X": [feed_var]}, outputs={"Out": [out]}, attrs={"col": i})
+        if not any(op.type == "fetch" for op in gb.ops):
+            for i, var in enumerate(fetch_list):
+                gb.append_op(type="fetch", inputs={"X": [var]}, outputs={"Out": [fetch_var]}, attrs={"col": i})
+        return tmp
+
+    def run(self, program=None, feed=None, fetch_list=None, feed_var_name="feed", fetch_var_name="fetch",
+            scope=None, return_numpy=True, use_program_cache=False):
+        if self._closed:
+            raise RuntimeError("Attempted to use a closed Executor")
+        if feed is None:
+            feed = {}
+        if fetch_list is None:
+            fetch_list = []
+        if program is None:
+            program = default_main_program()
+        if hasattr(program, "_compiled_program"):
+            program = program._compiled_program
+        if not isinstance(program, Program):
+            raise TypeError("Executor requires Program as its Parameter")
+        if scope is None:
+            scope = global_scope()
+        fetch_names = [v.name if isinstance(v, Variable) else str(v) for v in fetch_list]
+        feed_names = list(feed.keys())
+        key = (id(program), program._version, tuple(feed_names), tuple(fetch_names), feed_var_name, fetch_var_name)
+        prog = self._prog_cache.get(key)
+        if prog is None:
+            prog = self._add_feed_fetch_ops(program, feed_names, fetch_names, feed_var_name, fetch_var_name)
+            self._prog_cache[key] = prog
+        # feed
+        feed_list = [None] * len(feed_names)
+        gb = prog.global_block()
+        for op in gb.ops:
+            if op.type == "feed":
+                name = op.output("Out")[0]
+                feed_list[op.attrs["col"]] = _to_lod_tensor(feed[name], self.place)
+        scope.var(feed_var_name).set(feed_list)
+        scope.var(fetch_var_name).set([])
+        self._core.run_block(prog, 0, scope)
+        outs = scope.find_var(fetch_var_name).get() or []
+        if return_numpy:
+            return [as_numpy(o) for o in outs]
+        return outs
+
+    def _run_block(self, program, block_idx, scope):
+        self._core.run_block(program, block_idx, scope)

@@ -1,0 +1,142 @@
+"""Data-input layers (python/paddle/fluid/layers/io.py: data :38, py_reader :474,
+open_files :724, double_buffer :891, read_file, shuffle, batch)."""
+from __future__ import annotations
+
+from ...framework import core
+from ..framework import Variable, default_main_program, default_startup_program
+from ..layer_helper import LayerHelper
+
+
+def data(name, shape, append_batch_size=True, dtype="float32", lod_level=0, type=core.VT.LOD_TENSOR,
+         stop_gradient=True):
+    helper = LayerHelper("data", name=name)
+    shape = list(shape)
+    for i in range(len(shape)):
+        if shape[i] is None:
+            shape[i] = -1
+            append_batch_size = False
+        elif shape[i] < 0:
+            append_batch_size = False
+    if append_batch_size:
+        shape = [-1] + shape
+    return helper.create_global_variable(name=name, shape=shape, dtype=dtype, type=type,
+                                         stop_gradient=stop_gradient, lod_level=lod_level, is_data=True)
+
+
+class _PyReaderHandle:
+    """Host-side reader feeding a list of data vars (py_reader semantics).
+
+    Backed by the native blocking queue when the runtime library is built
+    (paddle_amd.runtime.BlockingQueue), else a Python queue.  Tensors are staged
+    to pinned memory and copied to the device on a side stream (double_buffer).
+    """
+
+    def __init__(self, capacity, feed_vars, use_double_buffer=True):
+        import queue
+
+        self.capacity = capacity
+        self.feed_vars = feed_vars
+        self._q = queue.Queue(maxsize=capacity)
+        self._provider = None
+        self._thread = None
+        self.use_double_buffer = use_double_buffer
+
+    def decorate_tensor_provider(self, provider):
+        self._provider = provider
+
+    decorate_paddle_reader = decorate_tensor_provider
+    decorate_batch_generator = decorate_tensor_provider
+
+    def start(self):
+        import threading
+
+        def run():
+            for item in self._provider():
+                self._q.put(item)
+            self._q.put(None)
+
+        self._thread = threading.Thread(target=run, daemon=True)
+        self._thread.start()
+
+    def reset(self):
+        if self._thread is not None:
+            self._thread.join(timeout=1)
+        self._thread = None
+
+    def next_feed(self):
+        item = self._q.get()
+        if item is None:
+            raise core_EOF()
+        return {v.name: x for v, x in zip(self.feed_vars, item)}
+
+
+class core_EOF(Exception):
+    """EOFException raised when a reader is exhausted (platform/enforce.h EOFException)."""
+
+
+EOFException = core_EOF
+
+
+def py_reader(capacity, shapes, dtypes, lod_levels=None, name=None, use_double_buffer=True):
+    lod_levels = lod_levels or [0] * len(shapes)
+    vars_ = []
+    for i, (s, d, l) in enumerate(zip(shapes, dtypes, lod_levels)):
+        vars_.append(data(name=f"{name or 'py_reader'}_data_{i}", shape=s, dtype=d, lod_level=l,
+                          append_batch_size=False))
+    r = _PyReaderHandle(capacity, vars_, use_double_buffer)
+    r.vars = vars_
+    return r
+
+
+def read_file(reader):
+    return reader.vars if len(reader.vars) > 1 else reader.vars[0]
+
+
+def double_buffer(reader, place=None, name=None):
+    reader.use_double_buffer = True
+    return reader
+
+
+def batch(reader, batch_size):
+    return reader
+
+
+def shuffle(reader, buffer_size):
+    return reader
+
+
+def open_files(filenames, shapes, lod_levels, dtypes, thread_num=None, buffer_size=None, pass_num=1,
+               is_test=None):
+    from ... import io as pio
+
+    r = py_reader(capacity=buffer_size or 64, shapes=shapes, dtypes=dtypes, lod_levels=lod_levels)
+
+    def provider():
+        for _ in range(pass_num):
+            for fn in filenames:
+                for rec in pio.recordio_iter(fn):
+                    yield rec
+
+    r.decorate_tensor_provider(provider)
+    return r
+
+
+def random_data_generator(low, high, shapes, lod_levels, for_parallel=True):
+    import numpy as np
+
+    r = py_reader(capacity=8, shapes=shapes, dtypes=["float32"] * len(shapes), lod_levels=lod_levels)
+
+    def provider():
+        while True:
+            yield [np.random.uniform(low, high, [abs(x) for x in s]).astype("float32") for s in shapes]
+
+    r.decorate_tensor_provider(provider)
+    return r
+
+
+def load(out, file_path, load_as_fp16=None):
+    helper = LayerHelper("load")
+    attrs = {"file_path": file_path}
+    if load_as_fp16 is not None:
+        attrs["load_as_fp16"] = load_as_fp16
+    helper.append_op(type="load", inputs={}, outputs={"Out": [out]}, attrs=attrs)

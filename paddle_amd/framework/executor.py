@@ -1,0 +1,103 @@
+"""Block interpreter (the reference's framework::Executor, executor.cc:125-353).
+
+Differences from the reference, MI355X-first:
+  * ops are "prepared" once per (program, block, version) -- kernel lookup, slot
+    lists and plain attrs are resolved ahead of time (the reference re-creates
+    every op on each ``Run``, executor.cc:294);
+  * kernels enqueue on torch's current HIP stream, so a whole block replays
+    asynchronously; the only host sync is the fetch;
+  * ``FLAGS_check_nan_inf`` / ``FLAGS_benchmark`` keep their reference meaning
+    (operator.cc:726-736, 722);
+  * control-flow kernels (while / conditional_block / recurrent) re-enter the
+    interpreter on a sub-block through ``ctx.executor``.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..utils import flags as FLAGS
+from ..utils import profiler as prof
+from . import core
+from . import registry as R
+
+
+class PreparedBlock:
+    def __init__(self, program, block_idx):
+        self.program = program
+        self.block = program.block(block_idx)
+        self.steps = []
+        for op in self.block.ops:
+            info = R.get_op_info(op.type)
+            attrs = {}
+            for k, v in op.attrs.items():
+                attrs[k] = v
+            ins = [(slot, list(names)) for slot, names in op.inputs.items()]
+            outs = {slot: list(names) for slot, names in op.outputs.items()}
+            self.steps.append((info, op, ins, outs, attrs))
+
+
+class BlockExecutor:
+    def __init__(self, place=None):
+        self.place = place or core.CPUPlace()
+        self._cache = {}
+
+    def prepare(self, program, block_idx=0):
+        key = (id(program), block_idx, len(program.block(block_idx).ops), program._version)
+        pb = self._cache.get(key)
+        if pb is None or pb.program is not program:
+            pb = PreparedBlock(program, block_idx)
+            self._cache[key] = pb
+        return pb
+
+    @staticmethod
+    def create_variables(program, scope, block_idx):
+        """Persistables live in the root scope, temporaries in the local one (executor.cc:88)."""
+        root = scope
+        while root.parent() is not None:
+            root = root.parent()
+        for v in program.block(block_idx).vars.values():
+            if v.persistable:
+                root.var(v.name)
+            else:
+                scope.var(v.name)
+
+    def run_block(self, program, block_idx, scope, create_vars=True):
+        pb = self.prepare(program, block_idx)
+        if create_vars:
+            self.create_variables(program, scope, block_idx)
+        self.run_prepared(pb, scope)
+
+    def run_prepared(self, pb, scope):
+        check_nan = FLAGS.get("check_nan_inf")
+        bench = FLAGS.get("benchmark")
+        profiling = prof.is_enabled()
+        place = self.place
+        for info, op, ins, outs, attrs in pb.steps:
+            ctx_ins = {}
+            for slot, names in ins:
+                vals = []
+                for n in names:
+                    var = scope.find_var(n)
+                    vals.append(var.get() if var is not None else None)
+                ctx_ins[slot] = vals
+            ctx = R.KernelContext(op.type, ctx_ins, outs, attrs, place, scope, op, self)
+            if profiling:
+                with prof.RecordEvent(op.type):
+                    R.run_kernel(info, ctx)
+            else:
+                R.run_kernel(info, ctx)
+            for slot, vals in ctx.results.items():
+                names = outs.get(slot, [])
+                for n, v in zip(names, vals):
+                    if v is None or n == R.EMPTY_VAR:
+                        continue
+                    var = scope.find_var(n)
+                    if var is None:
+                        var = scope.var(n)
+                    var.set(v)
+                    if check_nan and isinstance(v, core.LoDTensor) and v.tensor is not None \
+                            and v.tensor.is_floating_point():
+                        if not torch.isfinite(v.tensor).all():
+                            raise RuntimeError(f"Operator {op.type} output {n} contains NaN/Inf")
+            if bench and place.torch_device().type == "cuda":
+                torch.cuda.synchronize()

@@ -1,0 +1,2 @@
+"""Operator library: importing this package registers every op kernel."""
+from . import io_ops, math_ops, nn_ops, optimizer_ops, sequence_ops, tensor_ops  # noqa: F401

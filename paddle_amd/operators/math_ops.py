@@ -1,0 +1,418 @@
+"""Dense math operators: mul/matmul, elementwise (+broadcast), activations, reductions.
+
+Parity: paddle/fluid/operators/{mul,matmul,elementwise_*,activation,scale,sum,mean,
+reduce_*,clip,clip_by_norm,cumsum,minus,sign,l1_norm,squared_l2_norm,
+squared_l2_distance,cos_sim,norm}_op.* (SURVEY §2.7 "Dense NN / math").
+Kernels are device-agnostic torch expressions; on the HIP device they run as
+hipBLASLt GEMMs / fused elementwise launches, with hand-written gfx950 kernels
+for the hot fused ops (see paddle_amd/ops).  Gradients of ops without an
+explicit ``*_grad`` kernel come from the registry's automatic VJP.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from ..framework import core
+from ..framework.registry import register_op
+
+# ------------------------------------------------------------------ mul / matmul
+
+
+def _flat2(t, k):
+    return t.reshape(int(math.prod(t.shape[:k])), int(math.prod(t.shape[k:])))
+
+
+@register_op("mul", ["X", "Y"], ["Out"], {"x_num_col_dims": 1, "y_num_col_dims": 1})
+def mul(ctx):
+    """Out = flatten(X, x_num_col_dims) @ flatten(Y, y_num_col_dims)."""
+    x, y = ctx.input("X"), ctx.input("Y")
+    xn, yn = ctx.attr("x_num_col_dims"), ctx.attr("y_num_col_dims")
+    out = _flat2(x, xn) @ _flat2(y, yn).to(x.dtype)
+    ctx.set_output("Out", out.reshape(tuple(x.shape[:xn]) + tuple(y.shape[yn:])))
+
+
+@register_op("mul_grad", ["X", "Y", "Out?", "Out@GRAD"], ["X@GRAD?", "Y@GRAD?"],
+             {"x_num_col_dims": 1, "y_num_col_dims": 1}, grad=None, no_infer=True)
+def mul_grad(ctx):
+    x, y, dout = ctx.input("X"), ctx.input("Y"), ctx.input("Out@GRAD")
+    xn, yn = ctx.attr("x_num_col_dims"), ctx.attr("y_num_col_dims")
+    x2, y2 = _flat2(x, xn), _flat2(y, yn)
+    d2 = dout.reshape(x2.shape[0], y2.shape[1])
+    if ctx.has_output("X@GRAD"):
+        ctx.set_output("X@GRAD", (d2 @ y2.t()).reshape(x.shape), ctx.input_lod("X"))
+    if ctx.has_output("Y@GRAD"):
+        ctx.set_output("Y@GRAD", (x2.t() @ d2).reshape(y.shape))
+
+
+@register_op("matmul", ["X", "Y"], ["Out"], {"transpose_X": False, "transpose_Y": False, "alpha": 1.0})
+def matmul(ctx):
+    x, y = ctx.input("X"), ctx.input("Y")
+    tx, ty = ctx.attr("transpose_X"), ctx.attr("transpose_Y")
+    x1, y1 = x.dim() == 1, y.dim() == 1
+    if x1:
+        x = x.unsqueeze(0) if not tx else x.unsqueeze(1)
+    if y1:
+        y = y.unsqueeze(1) if not ty else y.unsqueeze(0)
+    if tx:
+        x = x.transpose(-1, -2)
+    if ty:
+        y = y.transpose(-1, -2)
+    out = torch.matmul(x, y)
+    a = ctx.attr("alpha")
+    if a != 1.0:
+        out = out * a
+    if x1:
+        out = out.squeeze(-2)
+    if y1:
+        out = out.squeeze(-1)
+    if out.dim() == 0:
+        out = out.reshape(1)
+    ctx.set_output("Out", out)
+
+
+# ------------------------------------------------------------------ elementwise
+
+
+def bcast_y(x, y, axis):
+    """Reference broadcast (elementwise_op_function.h): Y's dims align with X starting
+    at ``axis`` (-1: trailing alignment); trailing singular dims of Y are trimmed."""
+    if x.shape == y.shape or y.dim() == 0:
+        return y
+    ys = list(y.shape)
+    if axis is None or axis < 0:
+        axis = x.dim() - len(ys)
+    while ys and ys[-1] == 1:
+        ys.pop()
+    shape = [1] * axis + ys + [1] * (x.dim() - axis - len(ys))
+    return y.reshape(shape)
+
+
+def _reduce_to(g, shape):
+    """Sum a broadcast gradient back to ``shape`` (reference ElemwiseGradBroadcast kernels)."""
+    if tuple(g.shape) == tuple(shape):
+        return g
+    n = int(math.prod(shape)) if shape else 1
+    # find the matching alignment: try every axis offset
+    gs = list(g.shape)
+    for axis in range(0, len(gs) - len(shape) + 1):
+        if all(gs[axis + i] == shape[i] or shape[i] == 1 for i in range(len(shape))):
+            dims = list(range(axis)) + list(range(axis + len(shape), len(gs)))
+            r = g.sum(dim=dims) if dims else g
+            keep = [i for i in range(len(shape)) if shape[i] == 1 and r.shape[i] != 1]
+            if keep:
+                r = r.sum(dim=keep, keepdim=True)
+            return r.reshape(shape)
+    return g.sum().reshape(shape) if n == 1 else g.reshape(shape)
+
+
+_EW = {
+    "elementwise_add": lambda a, b: a + b,
+    "elementwise_sub": lambda a, b: a - b,
+    "elementwise_mul": lambda a, b: a * b,
+    "elementwise_div": lambda a, b: a / b,
+    "elementwise_max": torch.maximum,
+    "elementwise_min": torch.minimum,
+    "elementwise_pow": torch.pow,
+    "elementwise_mod": torch.remainder,
+    "elementwise_floordiv": lambda a, b: torch.div(a, b, rounding_mode="floor"),
+}
+
+
+def _make_ew(name, fn):
+    @register_op(name, ["X", "Y"], ["Out"], {"axis": -1, "use_mkldnn": False})
+    def k(ctx):
+        x, y = ctx.input("X"), ctx.input("Y")
+        ctx.set_output("Out", fn(x, bcast_y(x, y, ctx.attr("axis")).to(x.dtype)))
+
+    k.__name__ = name
+    return k
+
+
+for _n, _f in _EW.items():
+    _make_ew(_n, _f)
+
+
+def _ew_grad(name, dx_fn, dy_fn):
+    @register_op(name + "_grad", ["X", "Y", "Out?", "Out@GRAD"], ["X@GRAD?", "Y@GRAD?"], {"axis": -1},
+                 grad=None, no_infer=True)
+    def k(ctx):
+        x, y, d = ctx.input("X"), ctx.input("Y"), ctx.input("Out@GRAD")
+        yb = bcast_y(x, y, ctx.attr("axis")).to(x.dtype)
+        if ctx.has_output("X@GRAD"):
+            ctx.set_output("X@GRAD", _reduce_to(dx_fn(x, yb, d), x.shape), ctx.input_lod("X"))
+        if ctx.has_output("Y@GRAD"):
+            ctx.set_output("Y@GRAD", _reduce_to(dy_fn(x, yb, d), y.shape).to(y.dtype))
+
+
+_ew_grad("elementwise_add", lambda x, y, d: d, lambda x, y, d: d)
+_ew_grad("elementwise_sub", lambda x, y, d: d, lambda x, y, d: -d)
+_ew_grad("elementwise_mul", lambda x, y, d: d * y, lambda x, y, d: d * x)
+_ew_grad("elementwise_div", lambda x, y, d: d / y, lambda x, y, d: -d * x / (y * y))
+
+
+# ------------------------------------------------------------------ activations
+
+_ACT = {
+    "relu": (lambda x, a: F.relu(x), {}),
+    "sigmoid": (lambda x, a: torch.sigmoid(x), {}),
+    "logsigmoid": (lambda x, a: F.logsigmoid(x), {}),
+    "exp": (lambda x, a: torch.exp(x), {}),
+    "tanh": (lambda x, a: torch.tanh(x), {}),
+    "tanh_shrink": (lambda x, a: x - torch.tanh(x), {}),
+    "softshrink": (lambda x, a: F.softshrink(x, a["lambda"]), {"lambda": 0.5}),
+    "sqrt": (lambda x, a: torch.sqrt(x), {}),
+    "rsqrt": (lambda x, a: torch.rsqrt(x), {}),
+    "abs": (lambda x, a: torch.abs(x), {}),
+    "ceil": (lambda x, a: torch.ceil(x), {}),
+    "floor": (lambda x, a: torch.floor(x), {}),
+    "cos": (lambda x, a: torch.cos(x), {}),
+    "sin": (lambda x, a: torch.sin(x), {}),
+    "round": (lambda x, a: torch.round(x), {}),
+    "reciprocal": (lambda x, a: torch.reciprocal(x), {}),
+    "log": (lambda x, a: torch.log(x), {}),
+    "square": (lambda x, a: x * x, {}),
+    "softplus": (lambda x, a: F.softplus(x), {}),
+    "softsign": (lambda x, a: F.softsign(x), {}),
+    "brelu": (lambda x, a: torch.clamp(x, a["t_min"], a["t_max"]), {"t_min": 0.0, "t_max": 24.0}),
+    "leaky_relu": (lambda x, a: F.leaky_relu(x, a["alpha"]), {"alpha": 0.02}),
+    "soft_relu": (lambda x, a: torch.log1p(torch.exp(torch.clamp(x, -a["threshold"], a["threshold"]))),
+                  {"threshold": 40.0}),
+    "elu": (lambda x, a: F.elu(x, a["alpha"]), {"alpha": 1.0}),
+    "relu6": (lambda x, a: torch.clamp(x, 0.0, a["threshold"]), {"threshold": 6.0}),
+    "pow": (lambda x, a: torch.pow(x, a["factor"]), {"factor": 1.0}),
+    "stanh": (lambda x, a: a["scale_b"] * torch.tanh(a["scale_a"] * x), {"scale_a": 2.0 / 3.0, "scale_b": 1.7159}),
+    "hard_shrink": (lambda x, a: F.hardshrink(x, a["threshold"]), {"threshold": 0.5}),
+    "thresholded_relu": (lambda x, a: torch.where(x > a["threshold"], x, torch.zeros_like(x)), {"threshold": 1.0}),
+    "hard_sigmoid": (lambda x, a: torch.clamp(x * a["slope"] + a["offset"], 0.0, 1.0), {"slope": 0.2, "offset": 0.5}),
+    "swish": (lambda x, a: x * torch.sigmoid(a["beta"] * x), {"beta": 1.0}),
+    "gelu": (lambda x, a: F.gelu(x), {}),
+    "silu": (lambda x, a: F.silu(x), {}),
+}
+
+
+def _make_act(name, fn, attrs):
+    @register_op(name, ["X"], ["Out"], dict(attrs, use_mkldnn=False, use_cudnn=False, is_test=False))
+    def k(ctx):
+        ctx.set_output("Out", fn(ctx.input("X"), ctx.attrs))
+
+    k.__name__ = name
+
+
+for _n, (_f, _a) in _ACT.items():
+    _make_act(_n, _f, _a)
+
+
+@register_op("relu_grad", ["X", "Out", "Out@GRAD"], ["X@GRAD"], {}, grad=None, no_infer=True)
+def relu_grad(ctx):
+    out, d = ctx.input("Out"), ctx.input("Out@GRAD")
+    ctx.set_output("X@GRAD", torch.where(out > 0, d, torch.zeros_like(d)))
+
+
+@register_op("prelu", ["X", "Alpha"], ["Out"], {"mode": "all"})
+def prelu(ctx):
+    x, a = ctx.input("X"), ctx.input("Alpha")
+    mode = ctx.attr("mode")
+    if mode == "channel":
+        a = a.reshape([1, -1] + [1] * (x.dim() - 2))
+    elif mode == "element":
+        a = a.reshape((1,) + tuple(x.shape[1:]))
+    ctx.set_output("Out", torch.where(x > 0, x, a * x))
+
+
+@register_op("maxout", ["X"], ["Out"], {"groups": 1})
+def maxout(ctx):
+    x = ctx.input("X")
+    g = ctx.attr("groups")
+    N, C, H, W = x.shape
+    ctx.set_output("Out", x.reshape(N, C // g, g, H, W).max(2).values)
+
+
+# ------------------------------------------------------------------ scale / sum / mean
+
+
+@register_op("scale", ["X"], ["Out"], {"scale": 1.0, "bias": 0.0, "bias_after_scale": True})
+def scale(ctx):
+    v = ctx.input_value("X")
+    s, b = ctx.attr("scale"), ctx.attr("bias")
+    if isinstance(v, core.SelectedRows):
+        t = v.get_tensor().tensor
+        out = core.SelectedRows(v.rows(), v.height(), t * s + b if ctx.attr("bias_after_scale") else (t + b) * s)
+        ctx.set_output("Out", out)
+        return
+    x = v.tensor
+    out = x * s + b if ctx.attr("bias_after_scale") else (x + b) * s
+    ctx.set_output("Out", out.to(x.dtype))
+
+
+@register_op("sum", ["X*"], ["Out"], {"use_mkldnn": False})
+def sum_op(ctx):
+    """Sums dense tensors and SelectedRows (sum_op.cc); SelectedRows-only -> SelectedRows."""
+    vals = [v for v in ctx.input_values("X") if v is not None]
+    if vals and all(isinstance(v, core.SelectedRows) for v in vals):
+        rows, ts = [], []
+        for v in vals:
+            rows += v.rows()
+            ts.append(v.get_tensor().tensor)
+        ctx.set_output("Out", core.SelectedRows(rows, vals[0].height(), torch.cat(ts, 0)))
+        return
+    out = None
+    for v in vals:
+        t = v.to_dense() if isinstance(v, core.SelectedRows) else v.tensor
+        if t is None:
+            continue
+        out = t.clone() if out is None else out + t
+    lod = vals[0].lod() if vals and isinstance(vals[0], core.LoDTensor) else None
+    ctx.set_output("Out", out, lod)
+
+
+@register_op("mean", ["X"], ["Out"], {})
+def mean(ctx):
+    x = ctx.input("X")
+    ctx.set_output("Out", x.float().mean().reshape(1).to(x.dtype))
+
+
+@register_op("minus", ["X", "Y"], ["Out"], {})
+def minus(ctx):
+    ctx.set_output("Out", ctx.input("X") - ctx.input("Y"))
+
+
+@register_op("sign", ["X"], ["Out"], {})
+def sign(ctx):
+    ctx.set_output("Out", torch.sign(ctx.input("X")))
+
+
+@register_op("clip", ["X"], ["Out"], {"min": -1e30, "max": 1e30})
+def clip(ctx):
+    ctx.set_output("Out", torch.clamp(ctx.input("X"), ctx.attr("min"), ctx.attr("max")))
+
+
+@register_op("clip_by_norm", ["X"], ["Out"], {"max_norm": 1.0})
+def clip_by_norm(ctx):
+    x = ctx.input("X")
+    n = torch.sqrt((x.float() ** 2).sum())
+    mx = ctx.attr("max_norm")
+    ctx.set_output("Out", (x * torch.where(n > mx, mx / n, torch.ones_like(n))).to(x.dtype))
+
+
+@register_op("cumsum", ["X"], ["Out"], {"axis": -1, "exclusive": False, "reverse": False})
+def cumsum(ctx):
+    x = ctx.input("X")
+    ax = ctx.attr("axis")
+    if ctx.attr("reverse"):
+        x = x.flip(ax)
+    out = torch.cumsum(x, ax)
+    if ctx.attr("exclusive"):
+        out = out - x
+    if ctx.attr("reverse"):
+        out = out.flip(ax)
+    ctx.set_output("Out", out)
+
+
+def _reduce(name, fn):
+    @register_op(name, ["X"], ["Out"], {"dim": [0], "keep_dim": False, "reduce_all": False})
+    def k(ctx):
+        x = ctx.input("X")
+        dims = ctx.attr("dim")
+        dims = [dims] if isinstance(dims, int) else list(dims)
+        if ctx.attr("reduce_all") or not dims:
+            out = fn(x.reshape(-1), 0, False)
+            out = out.reshape([1] * x.dim()) if ctx.attr("keep_dim") else out.reshape(1)
+        else:
+            dims = [d % x.dim() for d in dims]
+            out = x
+            for d in sorted(dims, reverse=True):
+                out = fn(out, d, True)
+            if not ctx.attr("keep_dim"):
+                out = out.squeeze(dims) if len(dims) < x.dim() else out.reshape(1)
+        ctx.set_output("Out", out)
+
+    k.__name__ = name
+
+
+_reduce("reduce_sum", lambda t, d, k: t.sum(d, keepdim=k))
+_reduce("reduce_mean", lambda t, d, k: t.mean(d, keepdim=k))
+_reduce("reduce_max", lambda t, d, k: t.amax(d, keepdim=k))
+_reduce("reduce_min", lambda t, d, k: t.amin(d, keepdim=k))
+_reduce("reduce_prod", lambda t, d, k: t.prod(d, keepdim=k))
+
+
+@register_op("l1_norm", ["X"], ["Out"], {})
+def l1_norm(ctx):
+    ctx.set_output("Out", ctx.input("X").abs().sum().reshape(1))
+
+
+@register_op("squared_l2_norm", ["X"], ["Out"], {})
+def squared_l2_norm(ctx):
+    x = ctx.input("X")
+    ctx.set_output("Out", (x.float() ** 2).sum().reshape(1).to(x.dtype))
+
+
+@register_op("squared_l2_distance", ["X", "Y"], ["sub_result~", "Out"], {})
+def squared_l2_distance(ctx):
+    x, y = ctx.input("X"), ctx.input("Y")
+    sub = x - y
+    ctx.set_output("sub_result", sub)
+    ctx.set_output("Out", (sub.reshape(sub.shape[0], -1) ** 2).sum(1, keepdim=True))
+
+
+@register_op("cos_sim", ["X", "Y"], ["Out", "XNorm~", "YNorm~"], {})
+def cos_sim(ctx):
+    x, y = ctx.input("X"), ctx.input("Y")
+    x2, y2 = x.reshape(x.shape[0], -1), y.reshape(y.shape[0], -1)
+    xn = x2.norm(dim=1, keepdim=True)
+    yn = y2.norm(dim=1, keepdim=True)
+    out = (x2 * y2).sum(1, keepdim=True) / (xn * yn)
+    ctx.set_output("Out", out)
+    ctx.set_output("XNorm", xn)
+    ctx.set_output("YNorm", yn)
+
+
+@register_op("norm", ["X"], ["Out", "Norm~"], {"axis": 1, "epsilon": 1e-10})
+def norm(ctx):
+    x = ctx.input("X")
+    ax = ctx.attr("axis")
+    n = torch.sqrt((x * x).sum(ax, keepdim=True) + ctx.attr("epsilon"))
+    ctx.set_output("Out", x / n)
+    ctx.set_output("Norm", n)
+
+
+@register_op("bilinear_tensor_product", ["X", "Y", "Weight", "Bias?"], ["Out"], {})
+def bilinear_tensor_product(ctx):
+    x, y, w = ctx.input("X"), ctx.input("Y"), ctx.input("Weight")
+    out = torch.einsum("bi,kij,bj->bk", x, w, y)
+    if ctx.has_input("Bias"):
+        out = out + ctx.input("Bias")
+    ctx.set_output("Out", out)
+
+
+@register_op("fused_elemwise_activation", ["X", "Y"], ["Out", "IntermediateOut?~"],
+             {"functor_list": ["elementwise_add", "relu"], "axis": -1, "scale": 0.0, "recomputation": True,
+              "save_intermediate_out": False})
+def fused_elemwise_activation(ctx):
+    """{scale, relu} o {elementwise_add, elementwise_mul} in either order (fused_elemwise_activation_op.cc)."""
+    x, y = ctx.input("X"), ctx.input("Y")
+    f0, f1 = ctx.attr("functor_list")
+
+    def unary(name, t):
+        if name == "relu":
+            return F.relu(t)
+        if name == "scale":
+            return t * ctx.attr("scale")
+        raise ValueError(name)
+
+    def binary(name, a, b):
+        b = bcast_y(a, b, ctx.attr("axis"))
+        return a + b if name == "elementwise_add" else a * b
+
+    if f0.startswith("elementwise"):
+        inter = unary(f1, y)
+        out = binary(f0, x, inter)
+    else:
+        inter = binary(f1, x, y)
+        out = unary(f0, inter)
+    ctx.set_output("Out", out)
+    if ctx.has_output("IntermediateOut"):
+        ctx.set_output("IntermediateOut", inter)

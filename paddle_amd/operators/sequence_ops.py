@@ -1,0 +1,258 @@
+"""LoD (variable-length sequence) operators.
+
+Parity: paddle/fluid/operators/{sequence_pool,sequence_softmax,sequence_expand,
+sequence_expand_as,sequence_concat,sequence_conv,sequence_erase,sequence_reshape,
+sequence_slice,sequence_pad,sequence_unpad,sequence_mask,sequence_enumerate,
+lod_reset}_op.* and math/sequence_pooling.cu (SURVEY §2.7 "Sequence / LoD ops").
+
+LoD offsets are host lists; per-sequence work is expressed with segment ops over
+the packed rows (index_add / segment reductions) so the device does one launch
+per op instead of one per sequence wherever the math allows.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ..framework import core
+from ..framework.registry import register_op
+
+
+def _last_level(ctx, slot="X"):
+    lod = ctx.input_lod(slot)
+    x = ctx.input(slot)
+    if not lod:
+        return [0, x.shape[0]], lod
+    return lod[-1], lod
+
+
+def _seg_ids(off, device):
+    lens = torch.tensor([off[i + 1] - off[i] for i in range(len(off) - 1)], device=device)
+    return torch.repeat_interleave(torch.arange(len(off) - 1, device=device), lens), lens
+
+
+@register_op("sequence_pool", ["X"], ["Out", "MaxIndex~"], {"pooltype": "AVERAGE", "is_test": False},
+             share_lod=False)
+def sequence_pool(ctx):
+    x = ctx.input("X")
+    off, lod = _last_level(ctx)
+    n = len(off) - 1
+    pt = ctx.attr("pooltype").upper()
+    D = x.shape[1:]
+    if ctx.meta:
+        ctx.set_output("Out", torch.empty((n,) + tuple(D), dtype=x.dtype, device="meta"))
+        return
+    seg, lens = _seg_ids(off, x.device)
+    lensf = lens.to(x.dtype).reshape((-1,) + (1,) * len(D)).clamp_min(1)
+    idx = torch.zeros((n,) + tuple(D), dtype=torch.int64, device=x.device)
+    if pt in ("AVERAGE", "SUM", "SQRT"):
+        out = torch.zeros((n,) + tuple(D), dtype=x.dtype, device=x.device).index_add_(0, seg, x)
+        if pt == "AVERAGE":
+            out = out / lensf
+        elif pt == "SQRT":
+            out = out / torch.sqrt(lensf)
+    elif pt == "MAX":
+        out = torch.full((n,) + tuple(D), float("-inf"), dtype=x.dtype, device=x.device)
+        out = out.scatter_reduce(0, seg.reshape((-1,) + (1,) * len(D)).expand_as(x), x, "amax")
+        out = torch.where(torch.isinf(out), torch.zeros_like(out), out)
+    elif pt == "LAST":
+        out = x[torch.tensor([max(off[i + 1] - 1, off[i]) for i in range(n)], device=x.device)]
+    elif pt == "FIRST":
+        out = x[torch.tensor(off[:-1], device=x.device)]
+    else:
+        raise ValueError(pt)
+    out_lod = lod[:-1] if len(lod) > 1 else None
+    ctx.set_output("Out", out, out_lod)
+    ctx.set_output("MaxIndex", idx)
+
+
+@register_op("sequence_softmax", ["X"], ["Out"], {"use_cudnn": False})
+def sequence_softmax(ctx):
+    x = ctx.input("X")
+    off, lod = _last_level(ctx)
+    flat = x.reshape(-1)
+    if ctx.meta:
+        ctx.set_output("Out", torch.empty_like(x))
+        return
+    seg, _ = _seg_ids(off, x.device)
+    n = len(off) - 1
+    mx = torch.full((n,), float("-inf"), dtype=x.dtype, device=x.device).scatter_reduce(0, seg, flat, "amax")
+    e = torch.exp(flat - mx[seg])
+    s = torch.zeros(n, dtype=x.dtype, device=x.device).index_add_(0, seg, e)
+    ctx.set_output("Out", (e / s[seg]).reshape(x.shape), lod)
+
+
+@register_op("sequence_expand", ["X", "Y"], ["Out"], {"ref_level": -1}, share_lod=False)
+def sequence_expand(ctx):
+    x = ctx.input("X")
+    ylod = ctx.input_lod("Y")
+    ref = ctx.attr("ref_level")
+    ref = len(ylod) - 1 if ref == -1 else ref
+    yoff = ylod[ref]
+    xlod = ctx.input_lod("X")
+    xoff = xlod[0] if xlod else list(range(x.shape[0] + 1))
+    rows, out_off = [], [0]
+    for i in range(len(yoff) - 1):
+        rep = yoff[i + 1] - yoff[i]
+        seq = list(range(xoff[i], xoff[i + 1]))
+        for _ in range(rep):
+            rows += seq
+            out_off.append(out_off[-1] + len(seq))
+    idx = torch.tensor(rows, dtype=torch.long, device=x.device)
+    ctx.set_output("Out", x[idx], [out_off] if xlod else None)
+
+
+@register_op("sequence_expand_as", ["X", "Y"], ["Out"], {}, share_lod=False)
+def sequence_expand_as(ctx):
+    x = ctx.input("X")
+    yoff = ctx.input_lod("Y")[0]
+    reps = torch.tensor([yoff[i + 1] - yoff[i] for i in range(len(yoff) - 1)], device=x.device)
+    ctx.set_output("Out", torch.repeat_interleave(x, reps, 0), [yoff])
+
+
+@register_op("sequence_concat", ["X*"], ["Out"], {}, share_lod=False)
+def sequence_concat(ctx):
+    xs = ctx.input_values("X")
+    offs = [v.lod()[-1] for v in xs]
+    rows, out_off = [], [0]
+    n = len(offs[0]) - 1
+    parts = []
+    for i in range(n):
+        ln = 0
+        for v, o in zip(xs, offs):
+            parts.append(v.tensor[o[i]:o[i + 1]])
+            ln += o[i + 1] - o[i]
+        out_off.append(out_off[-1] + ln)
+    ctx.set_output("Out", torch.cat(parts, 0), [out_off])
+
+
+@register_op("sequence_conv", ["X", "Filter", "PaddingData?"], ["Out"],
+             {"contextLength": 3, "contextStart": 0, "contextStride": 1, "paddingTrainable": False})
+def sequence_conv(ctx):
+    """Context projection (math/context_project.h) + GEMM with the filter."""
+    x, w = ctx.input("X"), ctx.input("Filter")
+    off, lod = _last_level(ctx)
+    cl, cs = ctx.attr("contextLength"), ctx.attr("contextStart")
+    D = x.shape[1]
+    if ctx.meta:
+        ctx.set_output("Out", torch.empty(x.shape[0], w.shape[1], dtype=x.dtype, device="meta"))
+        return
+    cols = torch.zeros(x.shape[0], cl * D, dtype=x.dtype, device=x.device)
+    for s, e in zip(off[:-1], off[1:]):
+        for k in range(cl):
+            sh = cs + k
+            lo, hi = max(s, s - sh), min(e, e - sh)
+            if hi > lo:
+                cols[lo:hi, k * D:(k + 1) * D] = x[lo + sh:hi + sh]
+    ctx.set_output("Out", cols @ w, lod)
+
+
+@register_op("sequence_erase", ["X"], ["Out"], {"tokens": []}, share_lod=False)
+def sequence_erase(ctx):
+    x = ctx.input("X")
+    off, lod = _last_level(ctx)
+    toks = set(ctx.attr("tokens"))
+    flat = x.reshape(-1).tolist()
+    keep, new_off = [], [0]
+    for s, e in zip(off[:-1], off[1:]):
+        k = [i for i in range(s, e) if flat[i] not in toks]
+        keep += k
+        new_off.append(new_off[-1] + len(k))
+    ctx.set_output("Out", x[torch.tensor(keep, dtype=torch.long, device=x.device)], [new_off])
+
+
+@register_op("sequence_reshape", ["X"], ["Out"], {"new_dim": 1}, share_lod=False)
+def sequence_reshape(ctx):
+    x = ctx.input("X")
+    off, _ = _last_level(ctx)
+    nd = ctx.attr("new_dim")
+    D = x.shape[1]
+    new_off = [o * D // nd for o in off]
+    ctx.set_output("Out", x.reshape(-1, nd), [new_off])
+
+
+@register_op("sequence_slice", ["X", "Offset", "Length"], ["Out"], {}, share_lod=False)
+def sequence_slice(ctx):
+    x = ctx.input("X")
+    off, _ = _last_level(ctx)
+    so = ctx.input("Offset").reshape(-1).tolist()
+    sl = ctx.input("Length").reshape(-1).tolist()
+    rows, new_off = [], [0]
+    for i in range(len(off) - 1):
+        st = off[i] + int(so[i])
+        rows += list(range(st, st + int(sl[i])))
+        new_off.append(new_off[-1] + int(sl[i]))
+    ctx.set_output("Out", x[torch.tensor(rows, dtype=torch.long, device=x.device)], [new_off])
+
+
+@register_op("sequence_pad", ["X", "PadValue"], ["Out", "Length"], {"padded_length": -1}, share_lod=False)
+def sequence_pad(ctx):
+    x, pv = ctx.input("X"), ctx.input("PadValue")
+    off, _ = _last_level(ctx)
+    n = len(off) - 1
+    lens = [off[i + 1] - off[i] for i in range(n)]
+    L = ctx.attr("padded_length")
+    L = max(lens) if L == -1 else L
+    out = pv.reshape((1, 1) + tuple(x.shape[1:]) if pv.numel() > 1 else (1,)).expand(
+        (n, L) + tuple(x.shape[1:])).clone()
+    for i in range(n):
+        out[i, :lens[i]] = x[off[i]:off[i + 1]]
+    ctx.set_output("Out", out)
+    ctx.set_output("Length", torch.tensor(lens, dtype=torch.int64, device=x.device))
+
+
+@register_op("sequence_unpad", ["X", "Length"], ["Out"], {}, share_lod=False)
+def sequence_unpad(ctx):
+    x = ctx.input("X")
+    lens = [int(v) for v in ctx.input("Length").reshape(-1).tolist()]
+    parts = [x[i, :l] for i, l in enumerate(lens)]
+    off = [0]
+    for l in lens:
+        off.append(off[-1] + l)
+    ctx.set_output("Out", torch.cat(parts, 0), [off])
+
+
+@register_op("sequence_mask", ["X"], ["Y"], {"maxlen": -1, "out_dtype": 3}, grad=None)
+def sequence_mask(ctx):
+    x = ctx.input("X")
+    ml = ctx.attr("maxlen")
+    if ml < 0:
+        ml = int(x.max().item()) if not ctx.meta else 8191
+    r = torch.arange(ml, device=x.device)
+    ctx.set_output("Y", (r < x.unsqueeze(-1)).to(core.to_torch_dtype(ctx.attr("out_dtype"))))
+
+
+@register_op("sequence_enumerate", ["X"], ["Out"], {"win_size": 2, "pad_value": 0}, grad=None)
+def sequence_enumerate(ctx):
+    x = ctx.input("X")
+    off, lod = _last_level(ctx)
+    w, pv = ctx.attr("win_size"), ctx.attr("pad_value")
+    flat = x.reshape(-1)
+    out = torch.full((flat.shape[0], w), pv, dtype=x.dtype, device=x.device)
+    for s, e in zip(off[:-1], off[1:]):
+        for k in range(w):
+            if e - s - k > 0:
+                out[s:e - k, k] = flat[s + k:e]
+    ctx.set_output("Out", out, lod)
+
+
+@register_op("lod_reset", ["X", "Y?"], ["Out"], {"target_lod": []}, share_lod=False)
+def lod_reset(ctx):
+    x = ctx.input("X")
+    if ctx.has_input("Y"):
+        yv = ctx.input_value("Y")
+        lod = yv.lod() if yv.lod() else [[int(v) for v in yv.tensor.reshape(-1).tolist()]]
+    else:
+        lod = [list(ctx.attr("target_lod"))]
+    ctx.set_output("Out", x, lod)
+
+
+@register_op("sequence_scatter", ["X", "Ids", "Updates"], ["Out"], {}, share_lod=False)
+def sequence_scatter(ctx):
+    x, ids, up = ctx.input("X"), ctx.input("Ids"), ctx.input("Updates")
+    off = ctx.input_lod("Ids")[0]
+    out = x.clone()
+    for i in range(len(off) - 1):
+        cols = ids[off[i]:off[i + 1]].reshape(-1).long()
+        out[i].index_add_(0, cols, up[off[i]:off[i + 1]].reshape(-1))
+    ctx.set_output("Out", out)

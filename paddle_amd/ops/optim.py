@@ -13,13 +13,14 @@ from . import _native as N
 
 def adamw_flat(param, grad, m, v, *, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0,
                step=1, param_out=None, decay_end=None, grad_scale=1.0, lr_tensor=None,
-               beta1_pow=None, beta2_pow=None, grad_scale_tensor=None):
+               beta1_pow=None, beta2_pow=None, grad_scale_tensor=None, lr_t_eps=False):
     """In-place AdamW on fp32 ``param`` (flat, contiguous) with fp32 moments.
 
     ``decay_end``: elements with index < decay_end get decoupled weight decay
     (the flat layout puts all decayed params first).  ``param_out``: optional
     bf16/fp32 copy written in the same pass.  ``lr_tensor``/``beta*_pow``:
-    device scalars (static-graph adam op semantics, no host sync).
+    device scalars (static-graph adam op semantics, no host sync).  ``lr_t_eps``:
+    Kingma/Paddle epsilon placement (adam_op.h): p -= lr*sqrt(1-b2^t)/(1-b1^t) * m/(sqrt(v)+eps).
     """
     n = param.numel()
     if decay_end is None:
@@ -31,7 +32,7 @@ def adamw_flat(param, grad, m, v, *, lr, beta1=0.9, beta2=0.999, eps=1e-8, weigh
                N.ptr(grad), N.ptr(m), N.ptr(v), N.ptr(param_out), n, float(lr), N.ptr(lr_tensor),
                float(beta1), float(beta2), float(eps), float(weight_decay), float(bc1), float(bc2),
                N.ptr(beta1_pow), N.ptr(beta2_pow), int(decay_end), float(grad_scale),
-               N.ptr(grad_scale_tensor), N.stream())
+               N.ptr(grad_scale_tensor), int(lr_t_eps), N.stream())
         return param
     lr_ = float(lr_tensor.reshape(-1)[0]) if lr_tensor is not None else lr
     if beta1_pow is not None:
@@ -44,7 +45,8 @@ def adamw_flat(param, grad, m, v, *, lr, beta1=0.9, beta2=0.999, eps=1e-8, weigh
     if weight_decay:
         idx = torch.arange(n, device=param.device) < decay_end
         param.mul_(torch.where(idx, 1 - lr_ * weight_decay, 1.0))
-    param.addcdiv_(m / bc1, (v / bc2).sqrt_().add_(eps), value=-lr_)
+    e = eps / (bc2 ** 0.5) if lr_t_eps else eps
+    param.addcdiv_(m / bc1, (v / bc2).sqrt_().add_(e), value=-lr_)
     if param_out is not None:
         param_out.copy_(param)
     return param

@@ -1,0 +1,343 @@
+"""ctypes binding of the native C++ runtime (``lib/libpaddle_amd_runtime.so``).
+
+Components (see csrc/runtime/*.cc): RecordIO writer/scanner, LoDTensor stream IO,
+buddy allocator (+ torch pluggable-allocator hooks), blocking record queue with
+C++ RecordIO reader threads, DAG scheduler, profiler event buffers.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+from . import _build
+
+_lib = None
+_lock = threading.Lock()
+P, I, SZ, U64P, I64P = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64), \
+    ctypes.POINTER(ctypes.c_int64)
+NODE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.c_void_p)
+
+_SIGS = {
+    "pa_rt_last_error": ([], ctypes.c_char_p),
+    "pa_rio_writer_open": ([ctypes.c_char_p, I, I], P),
+    "pa_rio_writer_write": ([P, ctypes.c_char_p, SZ], I),
+    "pa_rio_writer_close": ([P], I),
+    "pa_rio_scanner_open": ([ctypes.c_char_p], P),
+    "pa_rio_scanner_next": ([P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(SZ)], I),
+    "pa_rio_scanner_close": ([P], None),
+    "pa_ts_open": ([ctypes.c_char_p, I, I], P),
+    "pa_ts_close": ([P], I),
+    "pa_ts_write_lod_tensor": ([P, I, U64P, I64P, I, I, I64P, P, SZ], I),
+    "pa_ts_read_header": ([P, ctypes.POINTER(I), U64P, I64P, I, ctypes.POINTER(I), ctypes.POINTER(I), I64P, I,
+                           ctypes.POINTER(SZ), ctypes.POINTER(ctypes.c_int * 32)], I),
+    "pa_ts_read_data": ([P, P, SZ], I),
+    "pa_buddy_create": ([I, SZ, I], P),
+    "pa_buddy_destroy": ([P], None),
+    "pa_buddy_alloc": ([P, SZ], P),
+    "pa_buddy_free": ([P, P], I),
+    "pa_buddy_stats": ([P, ctypes.POINTER(SZ), ctypes.POINTER(SZ), ctypes.POINTER(SZ), ctypes.POINTER(SZ)], None),
+    "pa_torch_set_chunk": ([SZ], None),
+    "pa_torch_stats": ([I, ctypes.POINTER(SZ), ctypes.POINTER(SZ), ctypes.POINTER(SZ)], None),
+    "pa_bq_create": ([SZ], P),
+    "pa_bq_push": ([P, ctypes.c_char_p, SZ], I),
+    "pa_bq_pop": ([P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(SZ), I], I),
+    "pa_bq_size": ([P], SZ),
+    "pa_bq_close": ([P], None),
+    "pa_bq_destroy": ([P], None),
+    "pa_rt_free": ([P], None),
+    "pa_bq_start_recordio_readers": ([P, ctypes.POINTER(ctypes.c_char_p), I, I, I], I),
+    "pa_dag_run": ([I, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I), I, NODE_FN, P], I),
+    "pa_prof_enable": ([I], None),
+    "pa_prof_push": ([ctypes.c_char_p], None),
+    "pa_prof_pop": ([], None),
+    "pa_prof_reset": ([], None),
+    "pa_prof_dump": ([ctypes.c_char_p], ctypes.c_long),
+}
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(_build.RUNTIME_LIB):
+                _build.build_runtime()
+            import torch  # noqa: F401  (HIP runtime loaded first)
+
+            L = ctypes.CDLL(_build.RUNTIME_LIB, mode=ctypes.RTLD_GLOBAL)
+            for n, (a, r) in _SIGS.items():
+                f = getattr(L, n)
+                f.argtypes = a
+                f.restype = r
+            _lib = L
+    return _lib
+
+
+def available():
+    try:
+        lib()
+        return True
+    except Exception:
+        return False
+
+
+def _err():
+    return lib().pa_rt_last_error().decode()
+
+
+# ------------------------------------------------------------------ RecordIO
+
+
+class RecordIOWriter:
+    def __init__(self, path, compressor=2, max_num_records=1000):
+        self._h = lib().pa_rio_writer_open(path.encode(), int(compressor), int(max_num_records))
+        if not self._h:
+            raise IOError(_err())
+
+    def write(self, record: bytes):
+        if lib().pa_rio_writer_write(self._h, record, len(record)) != 0:
+            raise IOError(_err())
+
+    def close(self):
+        if self._h:
+            rc = lib().pa_rio_writer_close(self._h)
+            self._h = None
+            if rc != 0:
+                raise IOError(_err())
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+class RecordIOScanner:
+    def __init__(self, path):
+        self._h = lib().pa_rio_scanner_open(path.encode())
+        if not self._h:
+            raise IOError(_err())
+
+    def __iter__(self):
+        d, n = ctypes.c_void_p(), SZ()
+        while True:
+            rc = lib().pa_rio_scanner_next(self._h, ctypes.byref(d), ctypes.byref(n))
+            if rc == 0:
+                break
+            if rc < 0:
+                raise IOError(_err())
+            yield ctypes.string_at(d.value, n.value)
+        self.close()
+
+    def close(self):
+        if self._h:
+            lib().pa_rio_scanner_close(self._h)
+            self._h = None
+
+
+# ------------------------------------------------------------------ LoDTensor streams
+
+_ES = (ctypes.c_int * 32)(*([0] * 32))
+for _k, _v in {0: 1, 1: 2, 2: 4, 3: 8, 4: 2, 5: 4, 6: 8, 19: 8, 20: 1, 21: 1, 22: 2}.items():
+    _ES[_k] = _v
+
+
+def write_lod_tensors(path, tensors, append=False):
+    """tensors: list of (numpy array, lod list-of-lists, vartype int)."""
+    h = lib().pa_ts_open(path.encode(), 1, int(append))
+    if not h:
+        raise IOError(_err())
+    try:
+        for arr, lod, vt in tensors:
+            arr = np.ascontiguousarray(arr)
+            flat = np.asarray([x for lvl in lod for x in lvl], dtype=np.uint64)
+            lens = np.asarray([len(l) for l in lod], dtype=np.int64)
+            dims = np.asarray(arr.shape, dtype=np.int64)
+            rc = lib().pa_ts_write_lod_tensor(
+                h, len(lod), flat.ctypes.data_as(U64P), lens.ctypes.data_as(I64P), int(vt), arr.ndim,
+                dims.ctypes.data_as(I64P), arr.ctypes.data_as(P), arr.nbytes)
+            if rc != 0:
+                raise IOError(_err())
+    finally:
+        lib().pa_ts_close(h)
+
+
+_NPT = {0: np.bool_, 1: np.int16, 2: np.int32, 3: np.int64, 4: np.float16, 5: np.float32, 6: np.float64,
+        19: np.uint64, 20: np.uint8, 21: np.int8, 22: np.uint16}
+
+
+def read_lod_tensors(path, max_lod=1 << 20):
+    """Returns list of (numpy array, lod, vartype).  bf16 (22) comes back as uint16 bits."""
+    h = lib().pa_ts_open(path.encode(), 0, 0)
+    if not h:
+        raise IOError(_err())
+    out = []
+    try:
+        lod_flat = (ctypes.c_uint64 * max_lod)()
+        lod_lens = (ctypes.c_int64 * 16)()
+        dims = (ctypes.c_int64 * 16)()
+        while True:
+            ll, dt, nd, nb = I(), I(), I(), SZ()
+            rc = lib().pa_ts_read_header(h, ctypes.byref(ll), lod_flat, lod_lens, max_lod, ctypes.byref(dt),
+                                         ctypes.byref(nd), dims, 16, ctypes.byref(nb), ctypes.byref(_ES))
+            if rc == 0:
+                break
+            if rc < 0:
+                raise IOError(_err())
+            lod, p = [], 0
+            for i in range(ll.value):
+                lod.append([int(lod_flat[p + k]) for k in range(lod_lens[i])])
+                p += lod_lens[i]
+            shape = [dims[i] for i in range(nd.value)]
+            arr = np.empty(shape, dtype=_NPT[dt.value])
+            if lib().pa_ts_read_data(h, arr.ctypes.data_as(P), nb.value) != 0:
+                raise IOError("truncated tensor data")
+            out.append((arr, lod, dt.value))
+    finally:
+        lib().pa_ts_close(h)
+    return out
+
+
+# ------------------------------------------------------------------ allocator
+
+
+class BuddyAllocator:
+    def __init__(self, device=-1, chunk_bytes=1 << 30, init_mem=False):
+        self._h = lib().pa_buddy_create(int(device), int(chunk_bytes), int(init_mem))
+
+    def alloc(self, n):
+        p = lib().pa_buddy_alloc(self._h, int(n))
+        if not p:
+            raise MemoryError(_err())
+        return p
+
+    def free(self, p):
+        if lib().pa_buddy_free(self._h, p) != 0:
+            raise ValueError(_err())
+
+    def stats(self):
+        u, r, pk, na = SZ(), SZ(), SZ(), SZ()
+        lib().pa_buddy_stats(self._h, ctypes.byref(u), ctypes.byref(r), ctypes.byref(pk), ctypes.byref(na))
+        return {"used": u.value, "reserved": r.value, "peak": pk.value, "arenas": na.value}
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().pa_buddy_destroy(self._h)
+        except Exception:
+            pass
+
+
+def use_buddy_allocator_for_torch(chunk_bytes=4 << 30):
+    """Route torch's HIP allocations through the native buddy allocator
+    (FLAGS_allocator_strategy=buddy).  Must run before the first GPU allocation."""
+    import torch
+
+    lib().pa_torch_set_chunk(int(chunk_bytes))
+    alloc = torch.cuda.memory.CUDAPluggableAllocator(_build.RUNTIME_LIB, "pa_torch_malloc", "pa_torch_free")
+    torch.cuda.memory.change_current_allocator(alloc)
+
+
+# ------------------------------------------------------------------ blocking queue
+
+
+class BlockingQueue:
+    def __init__(self, capacity):
+        self._h = lib().pa_bq_create(int(capacity))
+
+    def push(self, data: bytes) -> bool:
+        return lib().pa_bq_push(self._h, data, len(data)) == 0
+
+    def pop(self, timeout_ms=-1):
+        p, n = ctypes.c_void_p(), SZ()
+        rc = lib().pa_bq_pop(self._h, ctypes.byref(p), ctypes.byref(n), int(timeout_ms))
+        if rc == 0:
+            return None
+        if rc < 0:
+            raise TimeoutError("BlockingQueue.pop timed out")
+        try:
+            return ctypes.string_at(p.value, n.value)
+        finally:
+            lib().pa_rt_free(p)
+
+    def size(self):
+        return lib().pa_bq_size(self._h)
+
+    def close(self):
+        lib().pa_bq_close(self._h)
+
+    def start_recordio_readers(self, paths, nthreads=2, passes=1):
+        arr = (ctypes.c_char_p * len(paths))(*[p.encode() for p in paths])
+        self._paths_keep = arr
+        lib().pa_bq_start_recordio_readers(self._h, arr, len(paths), int(nthreads), int(passes))
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().pa_bq_destroy(self._h)
+        except Exception:
+            pass
+
+
+# ------------------------------------------------------------------ DAG scheduler
+
+
+def dag_run(n, edges, fn, nthreads=4):
+    """Run ``fn(i)`` for every node i of a DAG (edges: list of (u, v) meaning u before v)
+    on a C++ thread pool; the first exception is re-raised after in-flight nodes finish."""
+    succ = [[] for _ in range(n)]
+    indeg = [0] * n
+    for u, v in edges:
+        succ[u].append(v)
+        indeg[v] += 1
+    off = [0]
+    flat = []
+    for s in succ:
+        flat += s
+        off.append(len(flat))
+    err = []
+
+    def cb(node, _user):
+        try:
+            fn(node)
+            return 0
+        except BaseException as e:  # noqa: BLE001
+            err.append(e)
+            return 1
+
+    c_cb = NODE_FN(cb)
+    A = lambda xs: (ctypes.c_int * max(1, len(xs)))(*xs)  # noqa: E731
+    rc = lib().pa_dag_run(n, A(indeg), A(off), A(flat), int(nthreads), c_cb, None)
+    if err:
+        raise err[0]
+    if rc != 0:
+        raise RuntimeError(_err())
+
+
+# ------------------------------------------------------------------ profiler buffers
+
+
+class NativeProfiler:
+    @staticmethod
+    def enable(on=True):
+        lib().pa_prof_enable(int(on))
+
+    @staticmethod
+    def push(name):
+        lib().pa_prof_push(name.encode())
+
+    @staticmethod
+    def pop():
+        lib().pa_prof_pop()
+
+    @staticmethod
+    def reset():
+        lib().pa_prof_reset()
+
+    @staticmethod
+    def dump(path):
+        return lib().pa_prof_dump(path.encode())
