@@ -1,0 +1,158 @@
+"""Convergence ("book") tests (reference: python/paddle/fluid/tests/book/test_recognize_digits.py,
+test_fit_a_line.py) and ParallelExecutor equivalence (parallel_executor_test_base.py:29,
+test_parallel_executor_mnist.py:115-192: AllReduce vs Reduce strategies agree)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import paddle_amd.fluid as fluid
+from paddle_amd.framework import core
+
+
+def _digits_data(n=512, seed=0):
+    rng = np.random.RandomState(seed)
+    X = rng.rand(n, 1, 28, 28).astype("float32")
+    Y = X.reshape(n, -1)[:, :780].reshape(n, 10, 78).sum(-1).argmax(1).astype("int64").reshape(-1, 1)
+    return X, Y
+
+
+def mlp(img, label):
+    hidden = fluid.layers.fc(input=img, size=64, act="tanh")
+    hidden = fluid.layers.fc(input=hidden, size=64, act="tanh")
+    prediction = fluid.layers.fc(input=hidden, size=10, act="softmax")
+    loss = fluid.layers.cross_entropy(input=prediction, label=label)
+    return prediction, fluid.layers.mean(loss), fluid.layers.accuracy(input=prediction, label=label)
+
+
+def conv_net(img, label):
+    c1 = fluid.nets.simple_img_conv_pool(input=img, filter_size=5, num_filters=20, pool_size=2, pool_stride=2,
+                                         act="relu")
+    c1 = fluid.layers.batch_norm(c1)
+    c2 = fluid.nets.simple_img_conv_pool(input=c1, filter_size=5, num_filters=50, pool_size=2, pool_stride=2,
+                                         act="relu")
+    prediction = fluid.layers.fc(input=c2, size=10, act="softmax")
+    loss = fluid.layers.cross_entropy(input=prediction, label=label)
+    return prediction, fluid.layers.mean(loss), fluid.layers.accuracy(input=prediction, label=label)
+
+
+def _train_digits(net, place, epochs=3, tmpdir=None):
+    main, startup = fluid.Program(), fluid.Program()
+    main.random_seed = startup.random_seed = 90
+    with fluid.program_guard(main, startup):
+        img = fluid.layers.data(name="img", shape=[1, 28, 28], dtype="float32")
+        label = fluid.layers.data(name="label", shape=[1], dtype="int64")
+        pred, loss, acc = net(img, label)
+        test_prog = main.clone(for_test=True)
+        fluid.optimizer.Adam(learning_rate=0.002).minimize(loss)
+    exe = fluid.Executor(place)
+    scope = core.Scope()
+    X, Y = _digits_data()
+    with fluid.executor.scope_guard(scope):
+        exe.run(startup)
+        first = None
+        for ep in range(epochs):
+            for i in range(0, len(X), 64):
+                l, a = exe.run(main, feed={"img": X[i:i + 64], "label": Y[i:i + 64]}, fetch_list=[loss, acc])
+                first = l if first is None else first
+        tl, ta = exe.run(test_prog, feed={"img": X[:256], "label": Y[:256]}, fetch_list=[loss, acc])
+        if tmpdir:
+            fluid.io.save_inference_model(tmpdir, ["img"], [pred], exe, main_program=main)
+            prog, feeds, fetches = fluid.io.load_inference_model(tmpdir, exe)
+            (p1,) = exe.run(prog, feed={feeds[0]: X[:16]}, fetch_list=fetches)
+            (p2,) = exe.run(test_prog, feed={"img": X[:16], "label": Y[:16]}, fetch_list=[pred])
+            np.testing.assert_allclose(p1, p2, rtol=1e-4, atol=1e-5)
+    return float(first[0]), float(tl[0]), float(ta[0])
+
+
+def test_recognize_digits_mlp(tmp_path):
+    first, last, acc = _train_digits(mlp, fluid.CPUPlace(), tmpdir=str(tmp_path / "mlp"))
+    assert last < first and acc > 0.2
+
+
+def test_recognize_digits_conv(tmp_path):
+    first, last, acc = _train_digits(conv_net, fluid.CPUPlace(), epochs=3, tmpdir=str(tmp_path / "conv"))
+    assert last < first and acc > 0.2
+
+
+def test_fit_a_line():
+    main, startup = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, startup):
+        x = fluid.layers.data(name="x", shape=[13], dtype="float32")
+        y = fluid.layers.data(name="y", shape=[1], dtype="float32")
+        y_predict = fluid.layers.fc(input=x, size=1, act=None)
+        avg_cost = fluid.layers.mean(fluid.layers.square_error_cost(input=y_predict, label=y))
+        fluid.optimizer.SGD(learning_rate=0.05).minimize(avg_cost)
+    rng = np.random.RandomState(1)
+    W = rng.rand(13, 1).astype("float32")
+    X = rng.rand(256, 13).astype("float32")
+    Yv = X @ W + 0.1
+    exe = fluid.Executor(fluid.CPUPlace())
+    scope = core.Scope()
+    with fluid.executor.scope_guard(scope):
+        exe.run(startup)
+        for ep in range(60):
+            for i in range(0, 256, 32):
+                (l,) = exe.run(main, feed={"x": X[i:i + 32], "y": Yv[i:i + 32]}, fetch_list=[avg_cost])
+    assert float(l[0]) < 0.05
+
+
+def _pe_run(strategy, steps=4):
+    main, startup = fluid.Program(), fluid.Program()
+    main.random_seed = startup.random_seed = 7
+    with fluid.program_guard(main, startup):
+        img = fluid.layers.data(name="img", shape=[1, 28, 28], dtype="float32")
+        label = fluid.layers.data(name="label", shape=[1], dtype="int64")
+        _, loss, _ = mlp(img, label)
+        fluid.optimizer.SGD(learning_rate=0.1).minimize(loss)
+    scope = core.Scope()
+    exe = fluid.Executor(fluid.CPUPlace())
+    X, Y = _digits_data(256, 3)
+    losses = []
+    with fluid.executor.scope_guard(scope):
+        exe.run(startup)
+        if strategy is None:
+            for i in range(steps):
+                (l,) = exe.run(main, feed={"img": X[i * 32:(i + 1) * 32], "label": Y[i * 32:(i + 1) * 32]},
+                               fetch_list=[loss])
+                losses.append(float(l[0]))
+        else:
+            bs = fluid.BuildStrategy()
+            bs.reduce_strategy = strategy
+            pe = fluid.ParallelExecutor(use_cuda=False, loss_name=loss.name, main_program=main, build_strategy=bs,
+                                        scope=scope)
+            for i in range(steps):
+                (l,) = pe.run([loss.name], feed={"img": X[i * 32:(i + 1) * 32], "label": Y[i * 32:(i + 1) * 32]})
+                losses.append(float(np.mean(l)))
+    return losses
+
+
+def test_parallel_executor_allreduce_vs_reduce_vs_single(monkeypatch):
+    monkeypatch.setenv("CPU_NUM", "2")
+    single = _pe_run(None)
+    ar = _pe_run(fluid.BuildStrategy.ReduceStrategy.AllReduce)
+    rd = _pe_run(fluid.BuildStrategy.ReduceStrategy.Reduce)
+    # first loss: same params, batch split in halves whose mean equals the full-batch mean
+    assert abs(single[0] - ar[0]) < 1e-5
+    for a, b in zip(ar, rd):
+        assert abs(a - b) < 1e-5
+    for a, b in zip(single, ar):
+        assert abs(a - b) < 1e-4
+
+
+def test_memory_optimize_keeps_results():
+    main, startup = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, startup):
+        x = fluid.layers.data("x", [8])
+        h = fluid.layers.fc(fluid.layers.fc(x, 16, act="relu"), 4)
+        loss = fluid.layers.mean(h)
+        fluid.optimizer.SGD(0.1).minimize(loss)
+    exe = fluid.Executor(fluid.CPUPlace())
+    scope = core.Scope()
+    xv = np.random.rand(4, 8).astype("float32")
+    with fluid.executor.scope_guard(scope):
+        exe.run(startup)
+        (a,) = exe.run(main, feed={"x": xv}, fetch_list=[loss])
+    fluid.memory_optimize(main)
+    assert "delete_var" in [op.type for op in main.global_block().ops]

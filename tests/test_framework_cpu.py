@@ -1,0 +1,288 @@
+"""Framework-level tests (reference: test_program.py, test_operator_desc.py, test_variable.py,
+test_scope.py, test_calc_gradient.py, test_prune.py, lod_tensor_test.cc, test_lod_tensor.py,
+test_recordio_reader.py, profiler_test.cc, framework/details *_op_handle_test.cc)."""
+import io
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import paddle_amd.fluid as fluid
+from paddle_amd import runtime
+from paddle_amd.framework import core, serialization
+from paddle_amd.framework.proto import ProgramDescPB
+
+
+def _small_net():
+    main, startup = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, startup):
+        x = fluid.layers.data("x", [4])
+        y = fluid.layers.data("y", [1])
+        h = fluid.layers.fc(x, 8, act="relu")
+        p = fluid.layers.fc(h, 1)
+        loss = fluid.layers.mean(fluid.layers.square_error_cost(p, y))
+    return main, startup, loss, p
+
+
+def test_program_structure_and_clone():
+    main, startup, loss, p = _small_net()
+    gb = main.global_block()
+    types = [op.type for op in gb.ops]
+    assert types == ["mul", "elementwise_add", "relu", "mul", "elementwise_add", "elementwise_sub", "square", "mean"]
+    assert len(startup.global_block().ops) == 4  # 2 weights + 2 biases init
+    assert p.shape == (-1, 1)
+    test_prog = main.clone(for_test=True)
+    assert [op.type for op in test_prog.global_block().ops] == types
+    pruned = main.prune([p])
+    assert "square" not in [op.type for op in pruned.global_block().ops]
+
+
+def test_program_proto_roundtrip():
+    main, _, loss, _ = _small_net()
+    fluid.optimizer.SGD(0.1).minimize(loss, startup_program=fluid.Program())
+    s = main.serialize_to_string()
+    pd = ProgramDescPB.FromString(s)
+    assert pd.blocks[0].ops[0].type == "mul"
+    p2 = fluid.Program.parse_from_string(s)
+    assert [o.type for o in p2.global_block().ops] == [o.type for o in main.global_block().ops]
+    assert p2.global_block().var(loss.name).shape == loss.shape
+    assert p2.serialize_to_string() == s
+
+
+def test_append_backward_and_op_roles():
+    main, startup, loss, _ = _small_net()
+    with fluid.program_guard(main, startup):
+        pg = fluid.backward.append_backward(loss)
+    names = sorted(p.name for p, g in pg)
+    assert len(names) == 4
+    roles = [op.attrs["op_role"] for op in main.global_block().ops]
+    assert roles[-1] & 0x1
+    assert any(op.attrs.get("op_role_var") for op in main.global_block().ops)
+
+
+def test_calc_gradient():
+    main, startup = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, startup):
+        x = fluid.layers.data("x", [3], stop_gradient=False)
+        y = fluid.layers.reduce_sum(fluid.layers.square(x))
+        gx = fluid.backward.calc_gradient(y, x)
+    exe = fluid.Executor(fluid.CPUPlace())
+    xv = np.random.rand(2, 3).astype("float32")
+    (g,) = exe.run(main, feed={"x": xv}, fetch_list=[gx], scope=core.Scope())
+    np.testing.assert_allclose(g, 2 * xv, rtol=1e-5)
+
+
+def test_repeated_grad_accumulation_sum():
+    main, startup = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, startup):
+        x = fluid.layers.data("x", [3], stop_gradient=False)
+        y = x * 2.0 + x * 3.0
+        loss = fluid.layers.reduce_sum(y)
+        fluid.backward.append_backward(loss)
+    assert "sum" in [op.type for op in main.global_block().ops]
+    exe = fluid.Executor(fluid.CPUPlace())
+    xv = np.ones((2, 3), "float32")
+    (g,) = exe.run(main, feed={"x": xv}, fetch_list=["x@GRAD"], scope=core.Scope())
+    np.testing.assert_allclose(g, np.full((2, 3), 5.0))
+
+
+def test_scope_hierarchy():
+    s = core.Scope()
+    s.var("a").set(1)
+    k = s.new_scope()
+    assert k.find_var("a").get() == 1
+    k.var("b")
+    assert s.find_var("b") is None
+    s.drop_kids()
+    assert s.kids() == []
+
+
+def test_lod_tensor_api():
+    t = core.LoDTensor()
+    t.set(np.arange(10).reshape(5, 2).astype("float32"))
+    t.set_recursive_sequence_lengths([[2, 3]])
+    assert t.lod() == [[0, 2, 5]]
+    assert t.has_valid_recursive_sequence_lengths()
+    t2 = fluid.create_lod_tensor(np.ones((5, 1), "float32"), [[2, 3]], fluid.CPUPlace())
+    assert t2.recursive_sequence_lengths() == [[2, 3]]
+
+
+@pytest.mark.parametrize("dtype", ["float32", "int64", "float64", "float16"])
+def test_lod_tensor_stream_python_vs_native(tmp_path, dtype):
+    arr = (np.random.rand(4, 3) * 10).astype(dtype)
+    lt = core.LoDTensor(torch.from_numpy(arr), [[0, 1, 4]])
+    data = serialization.lod_tensor_to_bytes(lt)
+    back = serialization.lod_tensor_from_bytes(data)
+    np.testing.assert_array_equal(back.numpy(), arr)
+    assert back.lod() == [[0, 1, 4]]
+    if runtime.available():
+        p = str(tmp_path / "t.bin")
+        runtime.write_lod_tensors(p, [(arr, [[0, 1, 4]], core.convert_dtype(arr.dtype))])
+        assert open(p, "rb").read() == data  # bit-identical C++ and Python writers
+        (a2, lod2, vt), = runtime.read_lod_tensors(p)
+        np.testing.assert_array_equal(a2, arr)
+        assert lod2 == [[0, 1, 4]]
+
+
+def test_save_load_persistables(tmp_path):
+    main, startup, loss, _ = _small_net()
+    exe = fluid.Executor(fluid.CPUPlace())
+    scope = core.Scope()
+    with fluid.executor.scope_guard(scope):
+        exe.run(startup)
+        fluid.io.save_persistables(exe, str(tmp_path / "m"), main)
+        fluid.io.save_params(exe, str(tmp_path / "c"), main, filename="all.bin")
+        w = main.global_block().all_parameters()[0]
+        before = scope.find_var(w.name).get_tensor().numpy().copy()
+        scope.find_var(w.name).get_tensor().set(np.zeros_like(before))
+        fluid.io.load_persistables(exe, str(tmp_path / "m"), main)
+        np.testing.assert_array_equal(scope.find_var(w.name).get_tensor().numpy(), before)
+        scope.find_var(w.name).get_tensor().set(np.zeros_like(before))
+        fluid.io.load_params(exe, str(tmp_path / "c"), main, filename="all.bin")
+        np.testing.assert_array_equal(scope.find_var(w.name).get_tensor().numpy(), before)
+
+
+def test_recordio_and_queue(tmp_path):
+    if not runtime.available():
+        pytest.skip("native runtime not built")
+    paths = []
+    for k in range(3):
+        p = str(tmp_path / f"f{k}.recordio")
+        with runtime.RecordIOWriter(p, compressor=2, max_num_records=7) as w:
+            for i in range(20):
+                w.write(f"rec-{k}-{i}".encode() * (i + 1))
+        paths.append(p)
+    recs = list(runtime.RecordIOScanner(paths[0]))
+    assert len(recs) == 20 and recs[3] == b"rec-0-3" * 4
+    q = runtime.BlockingQueue(8)
+    q.start_recordio_readers(paths, nthreads=2, passes=2)
+    got = []
+    while True:
+        r = q.pop(timeout_ms=10000)
+        if r is None:
+            break
+        got.append(r)
+    assert len(got) == 3 * 20 * 2
+
+
+def test_recordio_tensor_files(tmp_path):
+    if not runtime.available():
+        pytest.skip("native runtime not built")
+    from paddle_amd import io as pio
+
+    p = str(tmp_path / "t.recordio")
+    w = pio.RecordIOWriter(p)
+    for i in range(5):
+        w.write_tensors([core.LoDTensor(torch.full((2, 3), float(i))), core.LoDTensor(torch.tensor([[i]]))])
+    w.close()
+    items = list(pio.recordio_iter(p))
+    assert len(items) == 5 and items[4][0][0, 0] == 4.0 and items[4][1][0, 0] == 4
+
+
+def test_dag_scheduler_order_and_errors():
+    if not runtime.available():
+        pytest.skip("native runtime not built")
+    import threading
+
+    order, lock = [], threading.Lock()
+
+    def fn(i):
+        with lock:
+            order.append(i)
+
+    edges = [(0, 2), (1, 2), (2, 3), (2, 4), (3, 5), (4, 5)]
+    runtime.dag_run(6, edges, fn, nthreads=4)
+    pos = {n: i for i, n in enumerate(order)}
+    assert all(pos[u] < pos[v] for u, v in edges)
+
+    def bad(i):
+        if i == 2:
+            raise ValueError("boom")
+
+    with pytest.raises(ValueError):
+        runtime.dag_run(6, edges, bad, nthreads=3)
+
+
+def test_buddy_allocator_host():
+    if not runtime.available():
+        pytest.skip("native runtime not built")
+    a = runtime.BuddyAllocator(device=-1, chunk_bytes=1 << 20)
+    ps = [a.alloc(n) for n in (100, 300, 5000, 256, 70000)]
+    assert len(set(ps)) == 5
+    st = a.stats()
+    assert st["used"] >= 100 + 300 + 5000 + 256 + 70000
+    for p in ps:
+        a.free(p)
+    assert a.stats()["used"] == 0
+    # after full merge a chunk-sized block must be available again
+    p = a.alloc(1 << 20)
+    a.free(p)
+    assert a.stats()["arenas"] == 1
+
+
+def test_native_profiler(tmp_path):
+    if not runtime.available():
+        pytest.skip("native runtime not built")
+    runtime.NativeProfiler.enable(True)
+    runtime.NativeProfiler.push("outer")
+    runtime.NativeProfiler.push("inner")
+    runtime.NativeProfiler.pop()
+    runtime.NativeProfiler.pop()
+    runtime.NativeProfiler.enable(False)
+    n = runtime.NativeProfiler.dump(str(tmp_path / "t.json"))
+    assert n >= 2
+    import json
+
+    json.load(open(tmp_path / "t.json"))
+
+
+def test_fluid_profiler(tmp_path):
+    main, startup, loss, _ = _small_net()
+    exe = fluid.Executor(fluid.CPUPlace())
+    scope = core.Scope()
+    exe.run(startup, scope=scope)
+    with fluid.profiler.profiler("CPU", "total", str(tmp_path / "prof")):
+        exe.run(main, feed={"x": np.ones((2, 4), "float32"), "y": np.ones((2, 1), "float32")},
+                fetch_list=[loss], scope=scope)
+    assert os.path.exists(str(tmp_path / "prof") + ".json")
+
+
+def test_check_nan_inf_flag():
+    from paddle_amd.utils import flags
+
+    main, startup = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, startup):
+        x = fluid.layers.data("x", [2])
+        y = fluid.layers.log(x)
+    flags.set("check_nan_inf", True)
+    try:
+        with pytest.raises(RuntimeError):
+            fluid.Executor(fluid.CPUPlace()).run(main, feed={"x": -np.ones((1, 2), "float32")}, fetch_list=[y],
+                                                 scope=core.Scope())
+    finally:
+        flags.set("check_nan_inf", False)
+
+
+def test_api_spec_coverage():
+    """Every paddle.fluid API.spec entry of the reference resolves (when the spec is mounted)."""
+    spec = "/root/reference/paddle/fluid/API.spec"
+    if not os.path.exists(spec):
+        pytest.skip("reference API.spec not mounted")
+    import importlib
+
+    import paddle_amd.fluid  # noqa: F401
+
+    missing = []
+    for line in open(spec):
+        name = line.split(" ")[0]
+        parts = name.split(".")[2:]  # drop paddle.fluid
+        obj = paddle_amd.fluid
+        try:
+            for p in parts:
+                obj = getattr(obj, p)
+        except AttributeError:
+            missing.append(name)
+    ratio = 1 - len(missing) / 426
+    print(f"API.spec coverage {ratio:.3f}; missing: {missing[:40]}")
+    assert ratio >= 0.80, missing
