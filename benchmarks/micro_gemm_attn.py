@@ -73,8 +73,16 @@ def attn():
     def pa_bwd():
         torch.autograd.grad(o, (q, k, v), do, retain_graph=True)
 
-    t = timeit(pa_bwd)
-    out["pa_bwd_ms"], out["pa_bwd_TF"] = round(t, 3), round(2.5 * flop_f / t / 1e9, 1)
+    from paddle_amd.ops import _native as N
+
+    variants = [int(x) for x in os.environ.get("PA_FA_BWD_VARIANTS", "1").split(",")]
+    for rep in range(2):
+        for var in variants:
+            N.call("pa_fa_bwd_set_variant", var)
+            t = timeit(pa_bwd)
+            out[f"pa_bwd_v{var}_ms_r{rep}"] = round(t, 3)
+            out[f"pa_bwd_v{var}_TF_r{rep}"] = round(2.5 * flop_f / t / 1e9, 1)
+    N.call("pa_fa_bwd_set_variant", 1)
     qt, kt, vt = (x.detach().transpose(1, 2).contiguous().requires_grad_() for x in (q, k, v))
     sd = lambda: torch.nn.functional.scaled_dot_product_attention(qt, kt, vt, is_causal=True)  # noqa: E731
     try:

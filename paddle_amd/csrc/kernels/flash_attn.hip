@@ -486,9 +486,273 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdParams p) {
   }
 }
 
+// LDS-only workgroup barrier: waits for this wave's LDS traffic, not for its
+// outstanding global loads / fire-and-forget dQ atomics (which __syncthreads'
+// release fence would drain with vmcnt(0)).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Pipelined backward: same math and per-wave ownership as fa_bwd_kernel, but
+//   * the next query tile (Q, dO, lse, delta) is prefetched into registers while the
+//     current one is on the MFMAs, and written into the other half of a
+//     double-buffered LDS stage -> ONE barrier per query tile;
+//   * this wave's K rows are also kept in registers (B operand of S), so the S GEMM
+//     reads only Q from LDS;
+//   * NOATOMIC is a measurement probe (plain stores instead of dQ atomics).
+template <int D, bool CAUSAL, bool NOATOMIC>
+__global__ __launch_bounds__(256, 1) void fa_bwd_kernel2(BwdParams p) {
+  constexpr int BK = 128, BQ = 32;
+  constexpr int KS = D / 16, DB = D / 32;
+  constexpr int KCH = D / 8;
+  constexpr int NQ = BQ * KCH / 256;  // 16-B chunks per thread per Q (and dO) tile
+  constexpr int K_BYTES = BK * D * 2, Q_BYTES = BQ * D * 2, DS_BYTES = BK * BQ * 2;
+  constexpr int STAGE = 2 * Q_BYTES + DS_BYTES + 2 * BQ * 4;
+  __shared__ __attribute__((aligned(16))) char smem[K_BYTES + 2 * STAGE];
+  char* Ks = smem;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int kt = blockIdx.z;
+  const int kvh = h / (p.Hq / p.Hkv);
+  const long n0 = (long)kt * BK;
+  const long offs = CAUSAL ? (long)p.Sk - p.Sq : 0;
+
+  const u16* qp = p.q + (long)b * p.q_bs + (long)h * p.q_hs;
+  const u16* dop = p.dout + (long)b * p.do_bs + (long)h * p.do_hs;
+  const u16* kp = p.k + (long)b * p.k_bs + (long)kvh * p.k_hs;
+  const u16* vp = p.v + (long)b * p.v_bs + (long)kvh * p.v_hs;
+  const float* lsep = p.lse + ((long)b * p.Hq + h) * p.Sq;
+  const float* dlp = p.delta + ((long)b * p.Hq + h) * p.Sq;
+  float* dqp = p.dq_acc + (long)b * p.Sq * p.Hq * D + (long)h * D;
+
+  long qstart = 0;
+  if (CAUSAL) qstart = max(0L, n0 - offs);
+  qstart = (qstart / BQ) * BQ;
+
+  // Buffer descriptors (wave-uniform, 32-bit offsets): no 64-bit per-lane pointers live
+  // across the loop, and the hardware range check zero-fills / drops the rows >= Sq of
+  // a ragged last query tile (host guarantees every extent fits in 32 bits).
+  const auto q_rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)qp, 0, (int)(unsigned)(((long)(p.Sq - 1) * p.q_ss + D) * 2), 0x00020000);
+  const auto do_rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)dop, 0, (int)(unsigned)(((long)(p.Sq - 1) * p.do_ss + D) * 2), 0x00020000);
+  const auto lse_rs = __builtin_amdgcn_make_buffer_rsrc((void*)lsep, 0, p.Sq * 4, 0x00020000);
+  const auto dl_rs = __builtin_amdgcn_make_buffer_rsrc((void*)dlp, 0, p.Sq * 4, 0x00020000);
+  const long dq_rstride = (long)p.Hq * D;
+  const auto dq_rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)dqp, 0, (int)(unsigned)(((long)(p.Sq - 1) * dq_rstride + D) * 4), 0x00020000);
+  unsigned qoff[NQ], ooff[NQ];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const int idx = tid + 256 * i, row = idx / KCH, ch = idx % KCH;
+    qoff[i] = (unsigned)(row * p.q_ss * 2 + ch * 16);
+    ooff[i] = (unsigned)(row * p.do_ss * 2 + ch * 16);
+  }
+
+  u16x8 qst[NQ], ost[NQ];
+  float lst = 0.f, dst = 0.f;
+  auto load_regs = [&](long qt0) {
+    const unsigned qb = (unsigned)(qt0 * p.q_ss * 2), ob = (unsigned)(qt0 * p.do_ss * 2);
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      qst[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(q_rs, (int)(qb + qoff[i]), 0, 0));
+      ost[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(do_rs, (int)(ob + ooff[i]), 0, 0));
+    }
+    const int lo = (int)(qt0 + (tid & (BQ - 1))) * 4;
+    // (raw values: scaling here would make the issuing code wait on the prefetch)
+    lst = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lse_rs, lo, 0, 0));
+    dst = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dl_rs, lo, 0, 0));
+  };
+  auto store_lds = [&](int buf) {
+    char* st = smem + K_BYTES + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const int idx = tid + 256 * i, row = idx / KCH, ch = idx % KCH;
+      *reinterpret_cast<u16x8*>(st + dual_off<D>(row, ch * 16)) = qst[i];
+      *reinterpret_cast<u16x8*>(st + Q_BYTES + dual_off<D>(row, ch * 16)) = ost[i];
+    }
+    if (tid < BQ) {
+      float* l2 = (float*)(st + 2 * Q_BYTES + DS_BYTES);
+      l2[tid] = lst * 1.44269504089f;
+      l2[BQ + tid] = dst;
+    }
+  };
+
+  load_regs(qstart);
+  // K tile -> LDS (dual image, read transposed by the dQ GEMM)
+  for (int idx = tid; idx < BK * KCH; idx += 256) {
+    const int row = idx / KCH, ch = idx % KCH;
+    const long kr = n0 + row;
+    u16x8 t = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (kr < p.Sk) t = *reinterpret_cast<const u16x8*>(kp + kr * p.k_ss + ch * 8);
+    *reinterpret_cast<u16x8*>(Ks + dual_off<D>(row, ch * 16)) = t;
+  }
+  // this wave's K and V rows as MFMA B operands: lane holds X[kv = 32w + r][16ks + 8hh + j]
+  bf8v vf[KS], kf[KS];
+  const long mykv = n0 + 32 * w + r;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    u16x8 t = {0, 0, 0, 0, 0, 0, 0, 0}, u = t;
+    if (mykv < p.Sk) {
+      t = *reinterpret_cast<const u16x8*>(vp + mykv * p.v_ss + ks * 16 + hh * 8);
+      u = *reinterpret_cast<const u16x8*>(kp + mykv * p.k_ss + ks * 16 + hh * 8);
+    }
+    vf[ks] = as_bf8(t);
+    kf[ks] = as_bf8(u);
+  }
+  store_lds(0);
+  lds_barrier();
+
+  f32x16 dk[DB], dv[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) { dk[i][e] = 0.f; dv[i][e] = 0.f; }
+
+  const int g = lane >> 4, gi = lane & 15, gq = gi >> 2, gp = gi & 3;
+  const int wkv = 32 * w;
+  // dQ of query tile t is flushed (atomics) at the start of iteration t + 1, so a whole
+  // compute phase separates the atomics from the reuse of their source registers
+  // (otherwise the next MFMA waits on vmcnt(0) for every atomic in flight).
+  f32x16 dq_prev;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) dq_prev[e] = 0.f;
+  auto flush_dq = [&](long qt_prev) {
+    // rows >= Sq fall outside dq_rs and are dropped by the range check
+    const unsigned base = (unsigned)(((qt_prev + 4 * hh) * dq_rstride + 32 * w + r) * 4);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int voff = (int)(base + (unsigned)(((e & 3) + 8 * (e >> 2)) * dq_rstride * 4));
+      if (NOATOMIC) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dq_prev[e]), dq_rs, voff, 0, 0);
+      else __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(dq_prev[e], dq_rs, voff, 0, 0);
+    }
+  };
+  int buf = 0;
+  for (long qt0 = qstart; qt0 < p.Sq; qt0 += BQ, buf ^= 1) {
+    // unconditional prefetch: past the end the range check returns zeros
+    load_regs(qt0 + BQ);
+    __builtin_amdgcn_sched_barrier(0);
+    if (w < DB && qt0 > qstart) flush_dq(qt0 - BQ);
+    char* Qs = smem + K_BYTES + buf * STAGE;
+    char* Os = Qs + Q_BYTES;
+    char* DSs = Os + Q_BYTES;
+    const float* L2s = (const float*)(DSs + DS_BYTES);
+    const float* DLs = L2s + BQ;
+
+    // Branch-free body (uniform control flow keeps dK/dV/dQ accumulators in place):
+    // fully masked waves on the causal diagonal just accumulate zeros.
+    f32x16 sacc, dpacc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) { sacc[e] = 0.f; dpacc[e] = 0.f; }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const u16x8 qa = *reinterpret_cast<const u16x8*>(Qs + dual_off<D>(r, (2 * ks + hh) * 16));
+      sacc = mfma32(as_bf8(qa), kf[ks], sacc);
+      const u16x8 oa = *reinterpret_cast<const u16x8*>(Os + dual_off<D>(r, (2 * ks + hh) * 16));
+      dpacc = mfma32(as_bf8(oa), vf[ks], dpacc);
+    }
+    {
+      // element e holds query qb + c_e (c_e = (e&3) + 8(e>>2)); valid iff lo <= c_e < hi
+      const int qb = (int)qt0 + 4 * hh;
+      const int lo = CAUSAL ? (int)(mykv - qb - offs) : 0;
+      const int hi = mykv < p.Sk ? p.Sq - qb : -1;
+      const unsigned span = hi > lo ? (unsigned)(hi - lo) : 0u;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int c = (e & 3) + 8 * (e >> 2);
+        const int qi = c + 4 * hh;
+        float pv = __builtin_amdgcn_exp2f(sacc[e] * p.scale_log2 - L2s[qi]);
+        pv = ((unsigned)(c - lo) < span) ? pv : 0.f;
+        sacc[e] = pv;
+        dpacc[e] = pv * (dpacc[e] - DLs[qi]) * p.scale;
+      }
+    }
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const bf8v pf = pack_p(sacc, 8 * st);
+      const bf8v sf = pack_p(dpacc, 8 * st);
+      const int rowb = 16 * st + 4 * (g >> 1) + gq;
+#pragma unroll
+      for (int db = 0; db < DB; ++db) {
+        const int colb = (32 * db + 16 * (g & 1) + 4 * gp) * 2;
+        const bf8v oa = cat_tr(tr_read(Os, dual_off<D>(rowb, colb)), tr_read(Os, dual_off<D>(rowb + 8, colb)));
+        dv[db] = mfma32(oa, pf, dv[db]);
+        const bf8v qa = cat_tr(tr_read(Qs, dual_off<D>(rowb, colb)), tr_read(Qs, dual_off<D>(rowb + 8, colb)));
+        dk[db] = mfma32(qa, sf, dk[db]);
+      }
+    }
+#pragma unroll
+    for (int e4 = 0; e4 < 4; ++e4) {
+      u16x4 v4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v4[j] = f2bf(dpacc[4 * e4 + j]);
+      *reinterpret_cast<u16x4*>(DSs + (wkv + r) * (BQ * 2) + (8 * e4 + 4 * hh) * 2) = v4;
+    }
+    // the other stage's Q/dO/lse/delta were last read before the previous barrier
+    store_lds(buf ^ 1);
+    // keep the flushed dQ registers allocated across the compute phase (see flush_dq)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) asm volatile("" ::"v"(dq_prev[e]));
+    lds_barrier();
+    if (w < DB) {
+      f32x16 dq;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) dq[e] = 0.f;
+      // the K-image swizzle only uses row bits 0..3, so the 16-row k-step offsets are
+      // plain immediates on two per-lane base addresses
+      const int arow0 = 8 * hh + gq;
+      const int acol = (16 * (g & 1) + 4 * gp) * 2;
+      const int bcol = (32 * w + 16 * (g & 1) + 4 * gp) * 2;
+      const char* kb0 = Ks + dual_off<D>(arow0, bcol);
+      const char* kb1 = Ks + dual_off<D>(arow0 + 4, bcol);
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        const int arow = 16 * ks + arow0;
+        const bf8v af = cat_tr(tr_read(DSs, arow * (BQ * 2) + acol),
+                               tr_read(DSs, (arow + 4) * (BQ * 2) + acol));
+        const bf8v bfk = cat_tr(tr_read(kb0, ks * 16 * D * 2), tr_read(kb1, ks * 16 * D * 2));
+        dq = mfma32(af, bfk, dq);
+      }
+      dq_prev = dq;
+    }
+  }
+  if (w < DB && qstart < p.Sq) {
+    const long last = qstart + ((p.Sq - 1 - qstart) / BQ) * BQ;
+    flush_dq(last);
+  }
+
+  if (mykv < p.Sk) {
+    u16* dkp = p.dk + (long)b * p.dk_bs + mykv * p.dk_ss + (long)h * p.dk_hs;
+    u16* dvp = p.dv + (long)b * p.dk_bs + mykv * p.dk_ss + (long)h * p.dk_hs;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        const int d = 32 * db + 8 * e4 + 4 * hh;
+        u16x4 a4, b4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a4[j] = f2bf(dk[db][4 * e4 + j]);
+          b4[j] = f2bf(dv[db][4 * e4 + j]);
+        }
+        *reinterpret_cast<u16x4*>(dkp + d) = a4;
+        *reinterpret_cast<u16x4*>(dvp + d) = b4;
+      }
+  }
+}
+
+// 0 = fa_bwd_kernel, 1 = pipelined (default), 2 = probe without dQ atomics (wrong dQ)
+static int g_fa_bwd_variant = 1;
+
 }  // namespace pa
 
 using namespace pa;
+
+PA_EXPORT int pa_fa_bwd_set_variant(int v) {
+  g_fa_bwd_variant = v;
+  return 0;
+}
 
 PA_EXPORT int pa_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
                                 const long* strides /*12: q b,s,h k b,s,h v b,s,h o b,s,h*/,
@@ -544,12 +808,22 @@ PA_EXPORT int pa_flash_attn_bwd(const void* q, const void* k, const void* v, con
   else if (D == 64) hipLaunchKernelGGL(fa_bwd_pre_kernel<64>, dim3((pre_threads + 255) / 256), dim3(256), 0, st, p);
   else return (int)hipErrorInvalidValue;
   dim3 grid(Hq, B, (Sk + 127) / 128);
-  if (D == 128) {
-    if (causal) hipLaunchKernelGGL((fa_bwd_kernel<128, true>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((fa_bwd_kernel<128, false>), grid, dim3(256), 0, st, p);
-  } else {
-    if (causal) hipLaunchKernelGGL((fa_bwd_kernel<64, true>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((fa_bwd_kernel<64, false>), grid, dim3(256), 0, st, p);
+  // the pipelined kernel addresses Q/dO/dQ of one (b, head) with 32-bit buffer offsets
+  const long lim = 1L << 31;
+  const bool fits32 = (long)Sq * strides[1] * 2 < lim && (long)Sq * strides[13] * 2 < lim &&
+                      (long)Sq * Hq * D * 4 < lim;
+  const int variant = fits32 ? g_fa_bwd_variant : 0;
+#define PA_FA_BWD_LAUNCH(DD, CC)                                                                    \
+  switch (variant) {                                                                      \
+    case 0: hipLaunchKernelGGL((fa_bwd_kernel<DD, CC>), grid, dim3(256), 0, st, p); break;         \
+    case 2: hipLaunchKernelGGL((fa_bwd_kernel2<DD, CC, true>), grid, dim3(256), 0, st, p); break;  \
+    default: hipLaunchKernelGGL((fa_bwd_kernel2<DD, CC, false>), grid, dim3(256), 0, st, p); break; \
   }
+  if (D == 128) {
+    if (causal) { PA_FA_BWD_LAUNCH(128, true) } else { PA_FA_BWD_LAUNCH(128, false) }
+  } else {
+    if (causal) { PA_FA_BWD_LAUNCH(64, true) } else { PA_FA_BWD_LAUNCH(64, false) }
+  }
+#undef PA_FA_BWD_LAUNCH
   PA_LAUNCH_CHECK();
 }

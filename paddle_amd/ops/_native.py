@@ -45,6 +45,7 @@ _SIGS = {
     "pa_momentum": [_I, _P, _P, _P, _L, _F, _P, _F, _I, _F, _F, _P],
     "pa_sumsq": [_I, _P, _L, _P, _P],
     "pa_flash_attn_fwd": [_P, _P, _P, _P, _P, _LP, _I, _I, _I, _I, _I, _I, _F, _I, _P],
+    "pa_fa_bwd_set_variant": [_I],
     "pa_flash_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _LP, _I, _I, _I, _I, _I, _I, _F, _I, _P],
 }
 
