@@ -1,0 +1,229 @@
+"""``fleet``: collective (hybrid-parallel) training entry points.
+
+Fleet is the north-star API named by BASELINE.json ("LLaMA-7B Fleet
+hybrid-parallel").  The reference's closest equivalents are the env-driven
+``fluid.Trainer`` NCCL2 / pserver auto-transpile (python/paddle/fluid/trainer.py:
+295-330, reading PADDLE_TRAINER_ID / PADDLE_TRAINERS_NUM / PADDLE_PSERVER_*) and
+``DistributeTranspiler`` -- both flat data parallel.
+
+``fleet.init(is_collective=True, strategy)`` builds the process group (RCCL) and
+the ``[dp, pp, sharding, sep, mp]`` topology from ``strategy.hybrid_configs``;
+``distributed_model`` wraps by the active axes (PipelineParallel /
+TensorParallel / DataParallel); ``distributed_optimizer`` returns a
+``HybridParallelOptimizer`` that syncs data-parallel gradients (unless the model
+wrapper already did), computes the global gradient norm across mp/pp/sharding
+ranks for clipping (each distributed parameter counted once), and steps.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ...parallel import comm
+from ..topology import CommunicateTopology, HybridCommunicateGroup
+
+
+class DistributedStrategy:
+    def __init__(self):
+        self.hybrid_configs = {"dp_degree": -1, "mp_degree": 1, "pp_degree": 1, "sharding_degree": 1,
+                               "sep_degree": 1}
+        self.pipeline_configs = {"accumulate_steps": 1, "micro_batch_size": 1}
+        self.tensor_parallel_configs = {"tensor_init_seed": -1}
+        self.sharding = False
+        self.sharding_configs = {"stage": 1, "sharding_degree": 1, "segment_broadcast_MB": 32}
+        self.recompute = False
+        self.recompute_configs = {}
+        self.amp = False
+        self.amp_configs = {"init_loss_scaling": 32768.0, "use_pure_fp16": False}
+        self.gradient_merge = False
+        self.gradient_merge_configs = {"k_steps": 1, "avg": True}
+        self.fuse_all_reduce_ops = True
+        self.fuse_grad_size_in_MB = 64
+        self.find_unused_parameters = False
+        self.lamb = self.lars = self.dgc = self.localsgd = False
+        self.a_sync = False
+        self.a_sync_configs = {}
+
+    def __setattr__(self, k, v):
+        if k == "hybrid_configs" and "hybrid_configs" in self.__dict__:
+            d = dict(self.__dict__["hybrid_configs"])
+            d.update(v)
+            v = d
+        object.__setattr__(self, k, v)
+
+
+class _Fleet:
+    def __init__(self):
+        self._hcg = None
+        self._strategy = None
+        self._is_collective = True
+
+    def init(self, role_maker=None, is_collective=True, strategy=None):
+        self._is_collective = is_collective
+        self._strategy = strategy or DistributedStrategy()
+        comm.init_parallel_env()
+        world = comm.get_world_size()
+        hc = dict(self._strategy.hybrid_configs)
+        deg = {a: int(hc.get(f"{a}_degree", 1) or 1) for a in ("mp", "pp", "sharding", "sep")}
+        prod = math.prod(deg.values())
+        dp = int(hc.get("dp_degree", -1))
+        if dp in (-1, 0):
+            if world % prod:
+                raise ValueError(f"world {world} not divisible by mp*pp*sharding*sep = {prod}")
+            dp = world // prod
+        topo = CommunicateTopology(dict(dp=dp, **deg))
+        self._hcg = HybridCommunicateGroup(topo)
+        return self
+
+    # ---- queries
+    def get_hybrid_communicate_group(self):
+        return self._hcg
+
+    def worker_index(self):
+        return comm.get_rank()
+
+    def worker_num(self):
+        return comm.get_world_size()
+
+    def is_first_worker(self):
+        return comm.get_rank() == 0
+
+    def barrier_worker(self):
+        comm.barrier()
+
+    @property
+    def user_defined_strategy(self):
+        return self._strategy
+
+    # ---- wrappers
+    def distributed_model(self, model):
+        hcg = self._hcg
+        if hcg is None:
+            raise RuntimeError("call fleet.init first")
+        from .pipeline import PipelineLayer, PipelineParallel
+
+        if hcg.get_pipe_parallel_world_size() > 1:
+            if not isinstance(model, PipelineLayer):
+                raise TypeError("pp_degree > 1 needs a PipelineLayer model")
+            return PipelineParallel(model, hcg, self._strategy)
+        if hcg.get_model_parallel_world_size() > 1:
+            return TensorParallel(model, hcg, self._strategy)
+        if hcg.get_data_parallel_world_size() > 1 and hcg.get_sharding_parallel_world_size() == 1:
+            from ..parallel import DataParallel
+
+            return DataParallel(model, group=hcg.get_data_parallel_group(),
+                                bucket_mb=self._strategy.fuse_grad_size_in_MB)
+        return model
+
+    def distributed_optimizer(self, optimizer, strategy=None):
+        if strategy is not None:
+            self._strategy = strategy
+        return HybridParallelOptimizer(optimizer, self._hcg, self._strategy)
+
+    # ---- checkpoint helpers (rank-0 writes the dp replica)
+    def save_persistables(self, executor=None, dirname=None, main_program=None):
+        from ... import fluid
+
+        if comm.get_rank() == 0:
+            fluid.io.save_persistables(executor, dirname, main_program)
+
+
+class TensorParallel(torch.nn.Module):
+    """mp > 1 (optionally with dp): broadcast replicated (non-distributed) parameters
+    from the mp group's first rank so every TP rank starts from identical copies; dp
+    gradient sync is left to the HybridParallelOptimizer."""
+
+    def __init__(self, layers, hcg, strategy=None):
+        super().__init__()
+        self._layers = layers
+        self.hcg = hcg
+        g = hcg.get_model_parallel_group()
+        src = hcg.get_model_parallel_group_src_rank()
+        with torch.no_grad():
+            for p in layers.parameters():
+                if not getattr(p, "is_distributed", False):
+                    comm.broadcast(p.data, src=src, group=g)
+
+    def forward(self, *a, **k):
+        return self._layers(*a, **k)
+
+
+class HybridParallelOptimizer:
+    def __init__(self, optimizer, hcg, strategy):
+        self._inner = optimizer
+        self.hcg = hcg
+        self.strategy = strategy
+        self.grad_clip = getattr(optimizer, "_grad_clip", None) or getattr(optimizer, "grad_clip", None)
+
+    def __getattr__(self, k):
+        return getattr(self._inner, k)
+
+    def _params(self):
+        if hasattr(self._inner, "param_groups"):
+            return [p for g in self._inner.param_groups for p in g["params"]]
+        return list(getattr(self._inner, "_parameter_list", []) or [])
+
+    @torch.no_grad()
+    def _dp_sync(self, params):
+        hcg = self.hcg
+        W = hcg.get_dp_sharding_world_size() if hcg else 1
+        ps = [p for p in params if p.grad is not None]
+        if W <= 1 or not ps:
+            return
+        flat = torch.cat([p.grad.reshape(-1).float() for p in ps])
+        comm.all_reduce(flat, group=hcg.get_dp_sharding_group())
+        flat /= W
+        o = 0
+        for p in ps:
+            p.grad.copy_(flat[o:o + p.numel()].view_as(p.grad))
+            o += p.numel()
+
+    @torch.no_grad()
+    def global_grad_norm(self, params):
+        """sqrt(sum g^2) over the WHOLE model: distributed (TP-sharded) params are summed
+        across mp ranks, replicated ones counted once; then summed across pp stages."""
+        hcg = self.hcg
+        dev = params[0].device if params else "cpu"
+        dist_sq = torch.zeros(1, dtype=torch.float32, device=dev)
+        rep_sq = torch.zeros(1, dtype=torch.float32, device=dev)
+        for p in params:
+            if p.grad is None:
+                continue
+            s = p.grad.float().pow(2).sum()
+            if getattr(p, "is_distributed", False):
+                dist_sq += s
+            else:
+                rep_sq += s
+        if hcg is not None and hcg.get_model_parallel_world_size() > 1:
+            comm.all_reduce(dist_sq, group=hcg.get_model_parallel_group())
+        tot = dist_sq + rep_sq
+        if hcg is not None and hcg.get_pipe_parallel_world_size() > 1:
+            comm.all_reduce(tot, group=hcg.get_pipe_parallel_group())
+        return tot.sqrt()
+
+    def step(self):
+        params = self._params()
+        from .pipeline import PipelineParallel  # noqa: F401  (pipeline syncs dp itself)
+
+        if not getattr(self, "_skip_dp_sync", False):
+            self._dp_sync(params)
+        clip = self.grad_clip
+        max_norm = getattr(clip, "clip_norm", clip if isinstance(clip, (int, float)) else None)
+        if max_norm:
+            norm = self.global_grad_norm(params)
+            coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
+            for p in params:
+                if p.grad is not None:
+                    p.grad.mul_(coef.to(p.grad.dtype))
+        self._inner.step()
+
+    def clear_grad(self, set_to_zero=False):
+        if hasattr(self._inner, "clear_grad"):
+            return self._inner.clear_grad()
+        return self._inner.zero_grad(set_to_none=not set_to_zero)
+
+    zero_grad = clear_grad
+
+
+fleet = _Fleet()

@@ -1,0 +1,136 @@
+"""Mixture-of-Experts with expert parallelism (all-to-all token dispatch).
+
+North-star component (SURVEY §2.5 row "Expert parallel": "No all-to-all or MoE
+gating op" in the reference).  API follows Paddle's ``incubate.distributed.models
+.moe.MoELayer`` (gate = "naive" / "gshard" / "switch", ``top_k``, ``l_aux``).
+
+MI355X design:
+  * routing = one [T, E] gate GEMM + softmax + top-k on device; tokens are sorted by
+    destination expert with a single stable argsort (no Python loops over tokens);
+  * dispatch / combine are ``all_to_all_single`` with exact (uneven) split sizes --
+    no capacity padding on the wire unless a capacity factor is set, in which case
+    overflow tokens are dropped before the exchange (GShard semantics);
+  * experts on a rank run back to back on contiguous token slices; the EP group is
+    meant to be the node's 8 GPUs (xGMI all-to-all is 7 concurrent P2P links).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ...nn import Layer
+from ...parallel import comm
+
+
+class _AllToAll(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, in_splits, out_splits, group):
+        ctx.in_splits, ctx.out_splits, ctx.group = in_splits, out_splits, group
+        out = x.new_empty((sum(out_splits),) + tuple(x.shape[1:]))
+        comm.all_to_all(out, x.contiguous(), group=group, out_splits=out_splits, in_splits=in_splits)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        out = g.new_empty((sum(ctx.in_splits),) + tuple(g.shape[1:]))
+        comm.all_to_all(out, g.contiguous(), group=ctx.group, out_splits=ctx.in_splits, in_splits=ctx.out_splits)
+        return out, None, None, None
+
+
+def all_to_all(x, in_splits, out_splits, group):
+    if comm.get_world_size(group) == 1:
+        return x
+    return _AllToAll.apply(x, in_splits, out_splits, group)
+
+
+class TopKGate(Layer):
+    def __init__(self, d_model, num_experts, top_k=2, gate_type="gshard", capacity_factor=None, dtype="float32"):
+        super().__init__("moe_gate", dtype)
+        self.weight = self.create_parameter([d_model, num_experts])
+        self.num_experts, self.top_k, self.gate_type = num_experts, top_k, gate_type
+        self.capacity_factor = capacity_factor
+
+    def forward(self, x):
+        logits = (x @ self.weight).float()
+        probs = F.softmax(logits, dim=-1)
+        val, idx = probs.topk(self.top_k, dim=-1)
+        if self.gate_type != "naive" and self.top_k > 1:
+            val = val / val.sum(-1, keepdim=True).clamp_min(1e-9)
+        # GShard / Switch load-balancing loss: E * sum_e(frac_tokens_e * mean_prob_e)
+        me = probs.mean(0)
+        ce = F.one_hot(idx[:, 0], self.num_experts).float().mean(0)
+        l_aux = (me * ce).sum() * self.num_experts
+        return val, idx, l_aux
+
+
+class MoELayer(Layer):
+    """``experts``: the LOCAL experts of this rank (``num_experts = len(experts) *
+    ep_world``); global expert ``e`` lives on rank ``e // len(experts)``."""
+
+    def __init__(self, d_model, experts, gate=None, top_k=2, group=None, capacity_factor=None,
+                 gate_type="gshard"):
+        super().__init__("moe_layer")
+        self.group = group
+        self.ep = comm.get_world_size(group)
+        self.experts = torch.nn.ModuleList(experts)
+        self.n_local = len(experts)
+        self.num_experts = self.n_local * self.ep
+        self.gate = gate or TopKGate(d_model, self.num_experts, top_k, gate_type, capacity_factor)
+        self.top_k = self.gate.top_k
+        self.capacity_factor = capacity_factor
+        self.l_aux = None
+
+    def forward(self, x):
+        shape = x.shape
+        x = x.reshape(-1, shape[-1])
+        T, k, E = x.shape[0], self.top_k, self.num_experts
+        val, idx, self.l_aux = self.gate(x)
+        flat_e = idx.reshape(-1)                       # [T*k] expert of each (token, slot)
+        flat_w = val.reshape(-1)
+        tok = torch.arange(T, device=x.device).repeat_interleave(k)
+        keep = torch.ones_like(flat_e, dtype=torch.bool)
+        if self.capacity_factor is not None:
+            cap = max(1, int(self.capacity_factor * T * k / E))
+            order = torch.argsort(flat_e, stable=True)
+            se = flat_e[order]
+            first = torch.searchsorted(se, se, right=False)
+            pos = torch.arange(se.numel(), device=x.device) - first
+            keep[order] = pos < cap
+        sel = keep.nonzero().squeeze(-1)
+        flat_e, flat_w, tok = flat_e[sel], flat_w[sel], tok[sel]
+        order = torch.argsort(flat_e, stable=True)
+        e_sorted = flat_e[order]
+        src_tok = tok[order]
+        counts = torch.bincount(e_sorted, minlength=E)  # per global expert, from this rank
+        send = x[src_tok]
+        # exchange counts, then tokens: rank r receives, for each local expert, the
+        # tokens of every peer (peer-major)
+        if self.ep > 1:
+            counts_all = torch.empty(self.ep * E, dtype=counts.dtype, device=counts.device)
+            comm.all_gather(counts_all, counts, group=self.group)
+            counts_all = counts_all.view(self.ep, E)
+            r = comm.get_rank(self.group)
+            lo, hi = r * self.n_local, (r + 1) * self.n_local
+            in_splits = counts.view(self.ep, self.n_local).sum(1).tolist()
+            recv_mat = counts_all[:, lo:hi]               # [peer, local expert]
+            out_splits = recv_mat.sum(1).tolist()
+            recv = all_to_all(send, in_splits, out_splits, self.group)
+            # regroup peer-major -> expert-major
+            per = recv_mat.reshape(-1).tolist()
+            chunks = list(recv.split(per))
+            by_expert = [torch.cat([chunks[p * self.n_local + e] for p in range(self.ep)])
+                         for e in range(self.n_local)]
+            outs = [self.experts[e](by_expert[e]) if by_expert[e].shape[0] else by_expert[e]
+                    for e in range(self.n_local)]
+            # back to peer-major order
+            sizes = [[int(recv_mat[p, e]) for p in range(self.ep)] for e in range(self.n_local)]
+            split_out = [list(o.split(s)) for o, s in zip(outs, sizes)]
+            back = torch.cat([split_out[e][p] for p in range(self.ep) for e in range(self.n_local)])
+            y_sorted = all_to_all(back, out_splits, in_splits, self.group)
+        else:
+            parts = list(send.split(counts.tolist()))
+            y_sorted = torch.cat([self.experts[e](parts[e]) if parts[e].shape[0] else parts[e]
+                                  for e in range(E)])
+        y = torch.zeros_like(x)
+        y.index_add_(0, src_tok, y_sorted * flat_w[order].unsqueeze(-1).to(y_sorted.dtype))
+        return y.reshape(shape)

@@ -1,0 +1,382 @@
+"""Pipeline parallelism: ``PipelineLayer`` + 1F1B ``PipelineParallel``.
+
+North-star component (SURVEY §2.5 row "Pipeline parallel": absent from the
+reference; its only model parallelism is the legacy layer->device placement of
+``ParallelNeuralNetwork``, paddle/legacy/gserver/gradientmachines/
+ParallelNeuralNetwork.cpp:45-98, one thread per device, no micro-batching).
+
+Design (one process per GPU, RCCL point-to-point over xGMI):
+  * ``PipelineLayer`` takes a flat list of ``LayerDesc`` and builds ONLY this
+    stage's segment (uniform or class-count partition).  Each layer is built
+    under its own seed (``seed + index``), so a layer's initial weights do not
+    depend on the partition -- pipelined and single-stage models start identical.
+  * ``PipelineParallel.train_batch`` runs the 1F1B schedule: ``pp - stage - 1``
+    warm-up forwards, steady one-forward-one-backward, cool-down backwards.  Every
+    transfer is a batched isend/irecv pair (``send_forward_recv_backward`` etc.),
+    so neighbouring stages never deadlock; tensor metadata travels in a small
+    int64 header before the payload.
+  * activations are tuples of tensors; floating ones carry gradients back.
+  * after the schedule: data-parallel gradient all-reduce (dp group), shared-weight
+    gradient all-reduce (tied embeddings), then the optimizer step.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.distributed as dist
+
+from ...nn import Layer
+from ...parallel import comm
+
+_DTYPES = [torch.float32, torch.bfloat16, torch.float16, torch.int64, torch.int32, torch.bool, torch.float64]
+_MAXT, _MAXD = 8, 8
+
+
+class LayerDesc:
+    def __init__(self, layer_cls, *args, **kwargs):
+        self.layer_cls, self.args, self.kwargs = layer_cls, args, kwargs
+
+    def build(self):
+        return self.layer_cls(*self.args, **self.kwargs)
+
+    def __repr__(self):
+        return f"LayerDesc({self.layer_cls.__name__})"
+
+
+class SharedLayerDesc(LayerDesc):
+    """A layer whose parameter ``shared_weight_attr`` is shared (tied) between the
+    stages that instantiate ``key`` (e.g. input embedding and LM head)."""
+
+    def __init__(self, key, layer_cls, forward_func=None, shared_weight_attr="weight", *args, **kwargs):
+        super().__init__(layer_cls, *args, **kwargs)
+        self.key, self.forward_func, self.shared_weight_attr = key, forward_func, shared_weight_attr
+
+
+class _SharedCall(torch.nn.Module):
+    def __init__(self, layer, fn):
+        super().__init__()
+        self.layer, self.fn = layer, fn
+
+    def forward(self, *a):
+        return self.fn(self.layer, *a) if self.fn is not None else self.layer(*a)
+
+
+def _partition(descs, num_stages, method):
+    n = len(descs)
+    if method.startswith("layer:"):
+        name = method.split(":", 1)[1]
+        marks = [i for i, d in enumerate(descs) if getattr(d, "layer_cls", type(d)).__name__ == name]
+        per = [len(marks) // num_stages + (1 if s < len(marks) % num_stages else 0) for s in range(num_stages)]
+        bounds, c = [0], 0
+        for s in range(num_stages - 1):
+            c += per[s]
+            bounds.append(marks[c] if c < len(marks) else n)
+        bounds.append(n)
+        return bounds
+    per = [n // num_stages + (1 if s < n % num_stages else 0) for s in range(num_stages)]
+    bounds = [0]
+    for p in per:
+        bounds.append(bounds[-1] + p)
+    return bounds
+
+
+class PipelineLayer(Layer):
+    def __init__(self, layers, num_stages=None, hcg=None, loss_fn=None, seg_method="uniform", seed=1234,
+                 recompute_interval=0):
+        super().__init__("pipeline_layer")
+        self.hcg = hcg
+        self.num_stages = num_stages or (hcg.get_pipe_parallel_world_size() if hcg else 1)
+        self.stage_id = hcg.get_stage_id() if hcg else 0
+        self.loss_fn = loss_fn
+        self.recompute_interval = recompute_interval
+        self.bounds = _partition(layers, self.num_stages, seg_method)
+        lo, hi = self.bounds[self.stage_id], self.bounds[self.stage_id + 1]
+        self.run_function = torch.nn.ModuleList()
+        self.shared = {}  # key -> parameter (for tied-weight gradient sync)
+        built_shared = {}
+        rng = torch.random.get_rng_state()
+        for i in range(lo, hi):
+            d = layers[i]
+            torch.manual_seed(seed + i)
+            if isinstance(d, SharedLayerDesc):
+                if d.key not in built_shared:
+                    # shared layers are seeded by their FIRST occurrence so every stage agrees
+                    first = next(j for j, x in enumerate(layers) if isinstance(x, SharedLayerDesc) and x.key == d.key)
+                    torch.manual_seed(seed + first)
+                    built_shared[d.key] = d.build()
+                    self.shared[d.key] = getattr(built_shared[d.key], d.shared_weight_attr)
+                self.run_function.append(_SharedCall(built_shared[d.key], d.forward_func))
+            elif isinstance(d, LayerDesc):
+                self.run_function.append(d.build())
+            else:
+                self.run_function.append(d)
+        torch.random.set_rng_state(rng)
+        # which stages hold each shared key (for the tied-gradient all-reduce)
+        self.shared_stages = {}
+        for s in range(self.num_stages):
+            for i in range(self.bounds[s], self.bounds[s + 1]):
+                d = layers[i]
+                if isinstance(d, SharedLayerDesc):
+                    self.shared_stages.setdefault(d.key, set()).add(s)
+
+    def forward(self, x):
+        for i, layer in enumerate(self.run_function):
+            args = x if isinstance(x, tuple) else (x,)
+            if self.recompute_interval and self.training and torch.is_grad_enabled() and i % self.recompute_interval == 0:
+                x = torch.utils.checkpoint.checkpoint(layer, *args, use_reentrant=False)
+            else:
+                x = layer(*args)
+        return x
+
+
+# ------------------------------------------------------------------ p2p plumbing
+def _meta(tensors):
+    m = torch.zeros(1 + _MAXT * (2 + _MAXD), dtype=torch.int64)
+    m[0] = len(tensors)
+    for i, t in enumerate(tensors):
+        b = 1 + i * (2 + _MAXD)
+        m[b] = _DTYPES.index(t.dtype)
+        m[b + 1] = t.dim()
+        m[b + 2:b + 2 + t.dim()] = torch.tensor(t.shape, dtype=torch.int64)
+    return m
+
+
+def _unmeta(m, device):
+    out = []
+    for i in range(int(m[0])):
+        b = 1 + i * (2 + _MAXD)
+        dt = _DTYPES[int(m[b])]
+        shape = [int(x) for x in m[b + 2:b + 2 + int(m[b + 1])]]
+        out.append(torch.empty(shape, dtype=dt, device=device))
+    return out
+
+
+class _P2P:
+    def __init__(self, hcg, device):
+        self.hcg, self.device = hcg, device
+        self.stage = hcg.get_stage_id()
+        self.nst = hcg.get_pipe_parallel_world_size()
+        self.prev = hcg.stage_rank(self.stage - 1) if self.stage > 0 else None
+        self.next = hcg.stage_rank(self.stage + 1) if self.stage < self.nst - 1 else None
+        self.nccl = comm.is_dist() and dist.get_backend() == "nccl"
+
+    def _meta_dev(self):
+        return self.device if self.nccl else "cpu"
+
+    def exchange(self, send_next=None, send_prev=None, recv_next=False, recv_prev=False):
+        """One batched round: optional sends to next/prev, optional receives from
+        next/prev.  Returns (from_next, from_prev) as tensor lists."""
+        mdev = self._meta_dev()
+        ops = []
+        got_next_m = got_prev_m = None
+        if send_next is not None:
+            ops.append(dist.P2POp(dist.isend, _meta(send_next).to(mdev), self.next))
+        if send_prev is not None:
+            ops.append(dist.P2POp(dist.isend, _meta(send_prev).to(mdev), self.prev))
+        if recv_next:
+            got_next_m = torch.empty(1 + _MAXT * (2 + _MAXD), dtype=torch.int64, device=mdev)
+            ops.append(dist.P2POp(dist.irecv, got_next_m, self.next))
+        if recv_prev:
+            got_prev_m = torch.empty(1 + _MAXT * (2 + _MAXD), dtype=torch.int64, device=mdev)
+            ops.append(dist.P2POp(dist.irecv, got_prev_m, self.prev))
+        self._run(ops)
+        ops = []
+        from_next = _unmeta(got_next_m.cpu(), self.device) if recv_next else None
+        from_prev = _unmeta(got_prev_m.cpu(), self.device) if recv_prev else None
+        for t in send_next or []:
+            ops.append(dist.P2POp(dist.isend, t.contiguous(), self.next))
+        for t in send_prev or []:
+            ops.append(dist.P2POp(dist.isend, t.contiguous(), self.prev))
+        for t in from_next or []:
+            ops.append(dist.P2POp(dist.irecv, t, self.next))
+        for t in from_prev or []:
+            ops.append(dist.P2POp(dist.irecv, t, self.prev))
+        self._run(ops)
+        return from_next, from_prev
+
+    @staticmethod
+    def _run(ops):
+        if not ops:
+            return
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+
+
+def _as_tuple(x):
+    return x if isinstance(x, tuple) else (x,)
+
+
+class PipelineParallel(Layer):
+    def __init__(self, layers: PipelineLayer, hcg, strategy=None):
+        super().__init__("pipeline_parallel")
+        self._layers = layers
+        self.hcg = hcg
+        cfg = (getattr(strategy, "pipeline_configs", None) or {}) if strategy is not None else {}
+        self.accumulate_steps = int(cfg.get("accumulate_steps", 1))
+        self.micro_batch_size = cfg.get("micro_batch_size")
+        self.stage = hcg.get_stage_id()
+        self.nst = hcg.get_pipe_parallel_world_size()
+        self.is_first, self.is_last = hcg.is_first_stage(), hcg.is_last_stage()
+        self.total_loss = None
+
+    def parameters(self, recurse=True):
+        return self._layers.parameters(recurse)
+
+    def named_parameters(self, *a, **k):
+        return self._layers.named_parameters(*a, **k)
+
+    def forward(self, *a):
+        return self._layers(*a)
+
+    # -------------------------------------------------------------------- helpers
+    def _split(self, data):
+        inputs, labels = data
+        M = self.accumulate_steps
+        ins = [tuple(x.chunk(M)[i] for x in _as_tuple(inputs)) for i in range(M)]
+        labs = [tuple(x.chunk(M)[i] for x in _as_tuple(labels)) for i in range(M)] if labels is not None else [None] * M
+        return ins, labs
+
+    def _fwd(self, x, label):
+        out = self._layers(x if len(x) > 1 else x[0])
+        if self.is_last:
+            fn = self._layers.loss_fn
+            lab = label if label is None or len(label) > 1 else label[0]
+            loss = fn(out, lab) if fn is not None else out
+            return loss / self.accumulate_steps
+        return out
+
+    def _sync_grads(self):
+        dp_group = self.hcg.get_data_parallel_group()
+        W = self.hcg.get_data_parallel_world_size()
+        params = [p for p in self._layers.parameters() if p.requires_grad and p.grad is not None]
+        if W > 1 and params:
+            flat = torch.cat([p.grad.reshape(-1).float() for p in params])
+            comm.all_reduce(flat, group=dp_group)
+            flat /= W
+            o = 0
+            for p in params:
+                n = p.numel()
+                p.grad.copy_(flat[o:o + n].view_as(p.grad))
+                o += n
+        # tied weights: sum the gradients of every stage holding the key
+        for key, p in self._layers.shared.items():
+            stages = sorted(self._layers.shared_stages[key])
+            if len(stages) > 1:
+                g = comm.new_group([self.hcg.stage_rank(s) for s in stages])
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+                comm.all_reduce(p.grad, group=g)
+
+    # ------------------------------------------------------------------ schedule
+    def forward_backward_pipeline(self, data):
+        dev = next(self._layers.parameters()).device
+        p2p = _P2P(self.hcg, dev)
+        ins, labs = self._split(data)
+        M = self.accumulate_steps
+        warm = min(self.nst - self.stage - 1, M)
+        inputs_q, outputs_q = [], []
+        losses = []
+
+        def recv_fwd_input(i):
+            if self.is_first:
+                return ins[i]
+            _, got = p2p.exchange(recv_prev=True)
+            return tuple(t.requires_grad_() if t.is_floating_point() else t for t in got)
+
+        def run_fwd(i, x):
+            out = self._fwd(x, labs[i])
+            inputs_q.append(x)
+            outputs_q.append(out)
+            if self.is_last:
+                losses.append(out.detach())
+            return out
+
+        def run_bwd(grads):
+            x = inputs_q.pop(0)
+            out = outputs_q.pop(0)
+            if self.is_last:
+                out.backward()
+            else:
+                # the next stage returns one gradient per FLOATING activation, in order
+                outs = [o for o in _as_tuple(out) if o.is_floating_point()]
+                pairs = [(o, g) for o, g in zip(outs, grads) if o.requires_grad]
+                torch.autograd.backward([o for o, _ in pairs], [g for _, g in pairs])
+            return tuple(t.grad if (t.is_floating_point() and t.grad is not None) else torch.zeros_like(t)
+                         for t in x if t.is_floating_point()) if not self.is_first else None
+
+        # warm-up
+        for i in range(warm):
+            x = recv_fwd_input(i)
+            out = run_fwd(i, x)
+            if not self.is_last:
+                p2p.exchange(send_next=[t.detach() for t in _as_tuple(out)])
+        # steady 1F1B
+        steady = M - warm
+        x = recv_fwd_input(warm) if steady > 0 else None
+        for j in range(steady):
+            i = warm + j
+            out = run_fwd(i, x)
+            if self.is_last:
+                grads = None
+            else:
+                grads, _ = p2p.exchange(send_next=[t.detach() for t in _as_tuple(out)], recv_next=True)
+            gin = run_bwd(grads)
+            last = j == steady - 1
+            if self.is_first:
+                if not last:
+                    x = recv_fwd_input(i + 1)
+            elif last:
+                p2p.exchange(send_prev=list(gin))
+            else:
+                _, got = p2p.exchange(send_prev=list(gin), recv_prev=True)
+                x = tuple(t.requires_grad_() if t.is_floating_point() else t for t in got)
+        # cool-down
+        for _ in range(warm):
+            grads = None
+            if not self.is_last:
+                grads, _ = p2p.exchange(recv_next=True)
+            gin = run_bwd(grads)
+            if not self.is_first:
+                p2p.exchange(send_prev=list(gin))
+        # loss of the batch, visible on every pp rank
+        t = torch.stack(losses).sum().float().reshape(1) if self.is_last else torch.zeros(1, device=dev)
+        if self.nst > 1:
+            comm.all_reduce(t, group=self.hcg.get_pipe_parallel_group())
+        self.total_loss = t
+        return t
+
+    def train_batch(self, data, optimizer, lr_scheduler=None, scaler=None):
+        self._layers.train()
+        loss = self.forward_backward_pipeline(data)
+        self._sync_grads()
+        if hasattr(optimizer, "_dp_sync"):  # HybridParallelOptimizer: dp already synced here
+            optimizer._skip_dp_sync = True
+        optimizer.step()
+        (optimizer.clear_grad if hasattr(optimizer, "clear_grad") else optimizer.zero_grad)()
+        if lr_scheduler is not None:
+            lr_scheduler.step()
+        return loss
+
+    @torch.no_grad()
+    def eval_batch(self, data, compute_loss=True):
+        self._layers.eval()
+        dev = next(self._layers.parameters()).device
+        p2p = _P2P(self.hcg, dev)
+        ins, labs = self._split(data)
+        outs = []
+        for i in range(self.accumulate_steps):
+            if self.is_first:
+                x = ins[i]
+            else:
+                _, x = p2p.exchange(recv_prev=True)
+                x = tuple(x)
+            out = self._layers(x if len(x) > 1 else x[0])
+            if self.is_last:
+                if compute_loss and self._layers.loss_fn is not None:
+                    lab = labs[i] if labs[i] is None or len(labs[i]) > 1 else labs[i][0]
+                    out = self._layers.loss_fn(out, lab)
+                outs.append(out)
+            else:
+                p2p.exchange(send_next=list(_as_tuple(out)))
+        return outs

@@ -128,24 +128,43 @@ class LlamaDecoderLayer(Layer):
 
 
 class LlamaForCausalLM(Layer):
+    """``tp``: optional ``distributed.fleet.TPGroup`` -- Megatron tensor parallelism:
+    QKV / gate|up column-parallel, o / down row-parallel (one all-reduce each),
+    vocab-parallel embedding, vocab-sharded LM head + parallel cross entropy."""
+
     def __init__(self, cfg: LlamaConfig, device=None, tp=None):
         super().__init__("llama")
         self.cfg = cfg
+        self.tp = tp if (tp is not None and tp.world_size > 1) else None
         dt = _dt(cfg.dtype)
         std = cfg.initializer_range
         H = cfg.hidden_size
-        self.embed_tokens = _param([cfg.vocab_size, H], device, dt, std)
+        tpd = self.tp.world_size if self.tp else 1
+        if cfg.vocab_size % tpd:
+            raise ValueError("vocab_size must be divisible by the tensor-parallel degree")
+        self.embed_tokens = _param([cfg.vocab_size // tpd, H], device, dt, std)
         self.layers = torch.nn.ModuleList(
-            [LlamaDecoderLayer(cfg, device, i, tp) for i in range(cfg.num_hidden_layers)])
+            [LlamaDecoderLayer(cfg, device, i, self.tp) for i in range(cfg.num_hidden_layers)])
         self.norm = _param([H], device, dt, value=1.0)
         self.norm.no_weight_decay = True
-        self.lm_head = None if cfg.tie_word_embeddings else _param([H, cfg.vocab_size], device, dt, std)
+        self.lm_head = None if cfg.tie_word_embeddings else _param([H, cfg.vocab_size // tpd], device, dt, std)
+        if self.tp:
+            for name, prm in self.named_parameters():
+                if prm.dim() == 2:
+                    prm.is_distributed = True
         cos, sin = ops.rope_tables(cfg.max_position_embeddings, cfg.head_dim, cfg.rope_theta, device=device)
         self.register_buffer("rope_cos", cos, persistent=False)
         self.register_buffer("rope_sin", sin, persistent=False)
 
+    def embed(self, input_ids):
+        if self.tp:
+            from ..distributed.fleet.mp_layers import vocab_parallel_embedding
+
+            return vocab_parallel_embedding(input_ids, self.embed_tokens, self.tp.group)
+        return ops.embedding(input_ids, self.embed_tokens)
+
     def hidden_states(self, input_ids):
-        x = ops.embedding(input_ids, self.embed_tokens)
+        x = self.embed(input_ids)
         residual = None
         cos, sin = self.rope_cos, self.rope_sin
         for layer in self.layers:
@@ -157,8 +176,14 @@ class LlamaForCausalLM(Layer):
         y, _ = ops.rms_norm(x, self.norm, self.cfg.rms_norm_eps, residual=residual)
         return y
 
-    def forward(self, input_ids, labels=None):
-        y = self.hidden_states(input_ids)
+    def logits_and_loss(self, y, labels):
+        if self.tp:
+            from ..distributed.fleet.mp_layers import parallel_cross_entropy
+
+            logits = ops.linear(self.tp.copy_to_region(y), self.lm_head)
+            if labels is None:
+                return logits
+            return parallel_cross_entropy(logits, labels, self.tp.group)
         if self.lm_head is not None:
             logits = ops.linear(y, self.lm_head)
         else:
@@ -167,6 +192,103 @@ class LlamaForCausalLM(Layer):
             return logits
         # in-place CE gradient over the logits buffer (nothing else consumes it)
         return ops.softmax_cross_entropy(logits, labels, inplace_grad=True)
+
+    def forward(self, input_ids, labels=None):
+        return self.logits_and_loss(self.hidden_states(input_ids), labels)
+
+
+def shard_llama_state_dict(full: dict, cfg: LlamaConfig, rank: int, world: int) -> dict:
+    """Full (single-rank) LLaMA state dict -> tensor-parallel shard ``rank`` of ``world``
+    (column splits keep the [q|k|v] and [gate|up] packing per rank)."""
+    if world == 1:
+        return dict(full)
+    D = cfg.head_dim
+    nh, nkv, I = cfg.num_attention_heads, cfg.kv_heads, cfg.intermediate_size
+    out = {}
+    for k, v in full.items():
+        if k.endswith("qkv_proj"):
+            q, kk, vv = v.split([nh * D, nkv * D, nkv * D], dim=1)
+            out[k] = torch.cat([t.chunk(world, dim=1)[rank] for t in (q, kk, vv)], dim=1).contiguous()
+        elif k.endswith("gate_up_proj"):
+            g, u = v.split([I, I], dim=1)
+            out[k] = torch.cat([g.chunk(world, dim=1)[rank], u.chunk(world, dim=1)[rank]], dim=1).contiguous()
+        elif k.endswith("o_proj") or k.endswith("down_proj") or k == "embed_tokens":
+            out[k] = v.chunk(world, dim=0)[rank].contiguous()
+        elif k == "lm_head":
+            out[k] = v.chunk(world, dim=1)[rank].contiguous()
+        else:
+            out[k] = v.clone()
+    return out
+
+
+# ---------------------------------------------------------------- pipeline stages
+class LlamaEmbeddingPipe(Layer):
+    def __init__(self, cfg: LlamaConfig, device=None, tp=None):
+        super().__init__("llama_embed_pipe")
+        self.cfg = cfg
+        self.tp = tp if (tp is not None and tp.world_size > 1) else None
+        tpd = self.tp.world_size if self.tp else 1
+        self.embed_tokens = _param([cfg.vocab_size // tpd, cfg.hidden_size], device, _dt(cfg.dtype),
+                                   cfg.initializer_range)
+
+    def forward(self, input_ids):
+        if self.tp:
+            from ..distributed.fleet.mp_layers import vocab_parallel_embedding
+
+            return vocab_parallel_embedding(input_ids, self.embed_tokens, self.tp.group)
+        return ops.embedding(input_ids, self.embed_tokens)
+
+
+class LlamaDecoderLayerPipe(LlamaDecoderLayer):
+    """Decoder block speaking the pipeline tuple protocol: (x[, residual]) -> (x, residual)."""
+
+    def __init__(self, cfg: LlamaConfig, device=None, layer_idx=0, tp=None):
+        super().__init__(cfg, device, layer_idx, tp if (tp is not None and tp.world_size > 1) else None)
+        cos, sin = ops.rope_tables(cfg.max_position_embeddings, cfg.head_dim, cfg.rope_theta, device=device)
+        self.register_buffer("rope_cos", cos, persistent=False)
+        self.register_buffer("rope_sin", sin, persistent=False)
+
+    def forward(self, x, residual=None):
+        return super().forward(x, residual, self.rope_cos, self.rope_sin)
+
+
+class LlamaNormHeadPipe(Layer):
+    def __init__(self, cfg: LlamaConfig, device=None, tp=None):
+        super().__init__("llama_head_pipe")
+        self.cfg = cfg
+        self.tp = tp if (tp is not None and tp.world_size > 1) else None
+        tpd = self.tp.world_size if self.tp else 1
+        dt = _dt(cfg.dtype)
+        self.norm = _param([cfg.hidden_size], device, dt, value=1.0)
+        self.norm.no_weight_decay = True
+        self.lm_head = _param([cfg.hidden_size, cfg.vocab_size // tpd], device, dt, cfg.initializer_range)
+
+    def forward(self, x, residual):
+        y, _ = ops.rms_norm(x, self.norm, self.cfg.rms_norm_eps, residual=residual)
+        if self.tp:
+            y = self.tp.copy_to_region(y)
+        return ops.linear(y, self.lm_head)
+
+
+class LlamaPretrainingCriterion:
+    def __init__(self, tp=None):
+        self.tp = tp if (tp is not None and tp.world_size > 1) else None
+
+    def __call__(self, logits, labels):
+        if self.tp:
+            from ..distributed.fleet.mp_layers import parallel_cross_entropy
+
+            return parallel_cross_entropy(logits, labels, self.tp.group)
+        return ops.softmax_cross_entropy(logits, labels, inplace_grad=True)
+
+
+def llama_pipeline_descs(cfg: LlamaConfig, device=None, tp=None):
+    from ..distributed.fleet.pipeline import LayerDesc
+
+    descs = [LayerDesc(LlamaEmbeddingPipe, cfg, device, tp)]
+    descs += [LayerDesc(LlamaDecoderLayerPipe, cfg, device, i, tp) for i in range(cfg.num_hidden_layers)]
+    descs.append(LayerDesc(LlamaNormHeadPipe, cfg, device, tp))
+    return descs
 
 
 def llama_flops_per_token(cfg: LlamaConfig, seq_len: int) -> float:

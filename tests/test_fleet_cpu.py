@@ -1,0 +1,335 @@
+"""Fleet hybrid parallelism on CPU (gloo, multi-process): every axis is checked
+against a single-process reference run of the same model on the same data."""
+import pytest
+import torch
+
+from dist_util import run_dist
+from paddle_amd.distributed.topology import CommunicateTopology
+from paddle_amd.models.llama import (LLAMA_CONFIGS, LlamaConfig, LlamaForCausalLM, LlamaPretrainingCriterion,
+                                     llama_pipeline_descs, shard_llama_state_dict)
+
+
+def _cfg(**kw):
+    c = dict(LLAMA_CONFIGS["llama-tiny"])
+    c.update(kw)
+    return LlamaConfig(**c, dtype="float32")
+
+
+def _batch(B=4, S=17, V=512, seed=3):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randint(0, V, (B, S), generator=g)
+
+
+def test_topology_axes():
+    t = CommunicateTopology(dict(dp=2, pp=2, mp=2))
+    assert t.world_size == 8
+    assert t.coord(5) == dict(dp=1, pp=0, sharding=0, sep=0, mp=1)
+    assert t.axis_groups("mp")[0] == [0, 1]
+    assert t.axis_groups("pp")[0] == [0, 2]
+    assert t.axis_groups("dp")[0] == [0, 4]
+
+
+# ----------------------------------------------------------------- tensor parallel
+def _tp_worker(rank, world):
+    from paddle_amd.distributed.fleet import TPGroup
+
+    cfg = _cfg()
+    torch.manual_seed(0)
+    full = LlamaForCausalLM(cfg, "cpu")
+    b = _batch()
+    loss_ref = full(b[:, :-1], b[:, 1:])
+    loss_ref.backward()
+    grads_ref = {n: p.grad for n, p in full.named_parameters()}
+    tp = TPGroup(None)
+    m = LlamaForCausalLM(cfg, "cpu", tp=tp)
+    sd = shard_llama_state_dict({k: v.detach() for k, v in full.state_dict().items()}, cfg, rank, world)
+    m.load_state_dict(sd)
+    loss = m(b[:, :-1], b[:, 1:])
+    loss.backward()
+    gshard = shard_llama_state_dict(grads_ref, cfg, rank, world)
+    errs = {n: (p.grad - gshard[n]).abs().max().item() for n, p in m.named_parameters()}
+    return loss.item(), loss_ref.item(), max(errs.values())
+
+
+def test_tensor_parallel_llama_matches_single():
+    res = run_dist(_tp_worker, 2)
+    for loss, ref, gerr in res:
+        assert abs(loss - ref) < 1e-5
+        assert gerr < 1e-5
+
+
+# --------------------------------------------------------------- pipeline parallel
+def _pp_ref(M, steps):
+    from paddle_amd.distributed.fleet.pipeline import PipelineLayer
+
+    cfg = _cfg(num_hidden_layers=4)
+    crit = LlamaPretrainingCriterion()
+    model = PipelineLayer(llama_pipeline_descs(cfg, "cpu"), num_stages=1, loss_fn=crit, seed=11)
+    opt = torch.optim.SGD(model.parameters(), lr=0.5)
+    losses = []
+    for s in range(steps):
+        b = _batch(B=8, seed=s)
+        tot = 0.0
+        for mb in b.chunk(M):
+            loss = crit(model(mb[:, :-1]), mb[:, 1:]) / M
+            loss.backward()
+            tot += loss.item()
+        opt.step()
+        opt.zero_grad()
+        losses.append(tot)
+    return losses, model
+
+
+def _pp_worker(rank, world, M, steps):
+    from paddle_amd.distributed.fleet import DistributedStrategy, fleet
+    from paddle_amd.distributed.fleet.pipeline import PipelineLayer
+
+    st = DistributedStrategy()
+    st.hybrid_configs = {"dp_degree": 1, "pp_degree": world}
+    st.pipeline_configs = {"accumulate_steps": M}
+    fleet.init(is_collective=True, strategy=st)
+    hcg = fleet.get_hybrid_communicate_group()
+    cfg = _cfg(num_hidden_layers=4)
+    layer = PipelineLayer(llama_pipeline_descs(cfg, "cpu"), hcg=hcg, loss_fn=LlamaPretrainingCriterion(), seed=11)
+    model = fleet.distributed_model(layer)
+    opt = torch.optim.SGD(model.parameters(), lr=0.5)
+    losses = []
+    for s in range(steps):
+        b = _batch(B=8, seed=s)
+        losses.append(model.train_batch((b[:, :-1], b[:, 1:]), opt).item())
+    lo = layer.bounds[hcg.get_stage_id()]
+    params = {f"run_function.{lo + int(n.split('.')[1])}.{'.'.join(n.split('.')[2:])}": p.detach().clone()
+              for n, p in layer.named_parameters()}
+    return losses, params
+
+
+@pytest.mark.parametrize("world,M", [(2, 4), (4, 8)])
+def test_pipeline_1f1b_llama_matches_single(world, M):
+    steps = 2
+    ref_losses, ref_model = _pp_ref(M, steps)
+    ref = dict(ref_model.named_parameters())
+    res = run_dist(_pp_worker, world, M, steps)
+    for losses, params in res:
+        for a, b in zip(losses, ref_losses):
+            assert abs(a - b) < 1e-5, (losses, ref_losses)
+        for n, p in params.items():
+            assert torch.allclose(p, ref[n].detach(), atol=1e-5), n
+
+
+# ------------------------------------------------------------------ expert parallel
+def _experts(n, d, seed):
+    out = []
+    for e in range(n):
+        torch.manual_seed(seed + e)
+        out.append(torch.nn.Sequential(torch.nn.Linear(d, 2 * d), torch.nn.GELU(), torch.nn.Linear(2 * d, d)))
+    return out
+
+
+def _moe_worker(rank, world, cap):
+    from paddle_amd.distributed.fleet import MoELayer, TopKGate
+
+    d, E, T = 16, 4, 24
+    torch.manual_seed(100)
+    gate_w = torch.randn(d, E) * 0.5
+    xs = [torch.randn(T, d, generator=torch.Generator().manual_seed(50 + r)) for r in range(world)]
+    # reference: all experts, all tokens, one process
+    ref_gate = TopKGate(d, E, top_k=2, capacity_factor=cap)
+    ref_gate.weight.data.copy_(gate_w)
+    ref = MoELayer(d, _experts(E, d, 7), gate=ref_gate, group=None, capacity_factor=cap)
+    if cap is None:
+        xr = torch.cat(xs).requires_grad_()
+        yr = ref(xr)
+        yr.pow(2).sum().backward()
+        y_ref, g_ref = yr.detach()[rank * T:(rank + 1) * T], xr.grad[rank * T:(rank + 1) * T]
+    else:  # capacity is per source rank: reference runs each rank's tokens separately
+        xr = xs[rank].clone().requires_grad_()
+        y_ref, g_ref = None, None
+    n_local = E // world
+    gate = TopKGate(d, E, top_k=2, capacity_factor=cap)
+    gate.weight.data.copy_(gate_w)
+    allex = _experts(E, d, 7)
+    moe = MoELayer(d, allex[rank * n_local:(rank + 1) * n_local], gate=gate, group=None if world == 1 else
+                   torch.distributed.group.WORLD, capacity_factor=cap)
+    x = xs[rank].clone().requires_grad_()
+    y = moe(x)
+    y.pow(2).sum().backward()
+    if y_ref is None:
+        return None
+    return (y.detach() - y_ref).abs().max().item(), (x.grad - g_ref).abs().max().item()
+
+
+def test_moe_expert_parallel_matches_single():
+    for yerr, gerr in run_dist(_moe_worker, 2, None):
+        assert yerr < 1e-5 and gerr < 1e-5
+
+
+def test_moe_capacity_drop_runs():
+    run_dist(_moe_worker, 2, 0.5)
+
+
+# -------------------------------------------------------------- sharding stage 3
+def _stage3_run(rank, world, steps):
+    from paddle_amd.distributed import group_sharded_parallel
+
+    cfg = _cfg()
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(cfg, "cpu")
+    m, opt = group_sharded_parallel(m, level="p_g_os", lr=1e-2, weight_decay=0.1, grad_clip=1.0)
+    losses = []
+    for s in range(steps):
+        b = _batch(B=4, seed=s)
+        part = b.chunk(world)[rank]
+        loss = m(part[:, :-1], part[:, 1:])
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        t = torch.tensor([loss.item()])
+        if world > 1:
+            torch.distributed.all_reduce(t)
+        losses.append(t.item() / world)
+    sd = opt.full_state_dict()
+    return losses, {k: v for k, v in sd.items() if not k.startswith("rope")}
+
+
+def test_sharding_stage3_matches_single():
+    ref_losses, ref_sd = _stage3_run(0, 1, 3)
+    res = run_dist(_stage3_run, 2, 3)
+    for losses, sd in res:
+        for a, b in zip(losses, ref_losses):
+            assert abs(a - b) < 1e-4, (losses, ref_losses)
+        for k in ref_sd:
+            # (Adam normalises near-zero gradients: fp32 summation order shows at ~1e-4 of lr)
+            assert torch.allclose(sd[k], ref_sd[k], atol=3e-4, rtol=1e-3), k
+
+
+# ---------------------------------------------------------------- context parallel
+def _cp_worker(rank, world, kind):
+    from paddle_amd.distributed.fleet import allgather_kv_attention, ulysses_attention
+    from paddle_amd.ops.fused import _attn_ref
+
+    B, S, H, D = 2, 16, 4, 8
+    g = torch.Generator().manual_seed(5)
+    q, k, v = (torch.randn(B, S, H, D, generator=g) for _ in range(3))
+    qf, kf, vf = (t.clone().requires_grad_() for t in (q, k, v))
+    o = _attn_ref(qf, kf, vf, True, 0.3)
+    o.pow(2).sum().backward()
+    s = S // world
+    sl = slice(rank * s, (rank + 1) * s)
+    ql, kl, vl = (t[:, sl].clone().requires_grad_() for t in (q, k, v))
+    fn = ulysses_attention if kind == "ulysses" else allgather_kv_attention
+    ol = fn(ql, kl, vl, torch.distributed.group.WORLD, causal=True, scale=0.3)
+    ol.pow(2).sum().backward()
+    errs = [(ol.detach() - o.detach()[:, sl]).abs().max().item()]
+    for a, b in ((ql, qf), (kl, kf), (vl, vf)):
+        errs.append((a.grad - b.grad[:, sl]).abs().max().item())
+    return max(errs)
+
+
+@pytest.mark.parametrize("kind", ["ulysses", "allgather_kv"])
+def test_context_parallel_attention_matches_full(kind):
+    for err in run_dist(_cp_worker, 2, kind):
+        assert err < 1e-5
+
+
+# ------------------------------------------------------- DataParallel + fleet dp x mp
+def _dp_mp_worker(rank, world, steps):
+    from paddle_amd.distributed.fleet import DistributedStrategy, TPGroup, fleet
+
+    st = DistributedStrategy()
+    st.hybrid_configs = {"dp_degree": 2, "mp_degree": 2}
+    fleet.init(is_collective=True, strategy=st)
+    hcg = fleet.get_hybrid_communicate_group()
+    cfg = _cfg()
+    torch.manual_seed(0)
+    full = LlamaForCausalLM(cfg, "cpu")
+    sd_full = {k: v.detach() for k, v in full.state_dict().items()}
+    tp = TPGroup(hcg.get_model_parallel_group())
+    m = LlamaForCausalLM(cfg, "cpu", tp=tp)
+    m.load_state_dict(shard_llama_state_dict(sd_full, cfg, hcg.get_model_parallel_rank(), 2))
+    model = fleet.distributed_model(m)
+    inner = torch.optim.SGD(m.parameters(), lr=0.5)
+    inner.grad_clip = 1.0
+    opt = fleet.distributed_optimizer(inner)
+    for s in range(steps):
+        b = _batch(B=4, seed=s).chunk(2)[hcg.get_data_parallel_rank()]
+        loss = model(b[:, :-1], b[:, 1:])
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+    return hcg.get_model_parallel_rank(), {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+
+def _dp_mp_ref(steps):
+    cfg = _cfg()
+    torch.manual_seed(0)
+    full = LlamaForCausalLM(cfg, "cpu")
+    opt = torch.optim.SGD(full.parameters(), lr=0.5)
+    for s in range(steps):
+        b = _batch(B=4, seed=s)
+        loss = full(b[:, :-1], b[:, 1:])
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(full.parameters(), 1.0)
+        opt.step()
+        opt.zero_grad()
+    return cfg, {k: v.detach() for k, v in full.state_dict().items()}
+
+
+def test_fleet_dp2_mp2_llama_matches_single():
+    steps = 2
+    cfg, ref = _dp_mp_ref(steps)
+    for mp_rank, sd in run_dist(_dp_mp_worker, 4, steps):
+        want = shard_llama_state_dict(ref, cfg, mp_rank, 2)
+        for k in want:
+            assert torch.allclose(sd[k], want[k], atol=2e-5, rtol=1e-4), k
+
+
+def _ddp_worker(rank, world):
+    from paddle_amd.distributed import DataParallel
+
+    torch.manual_seed(rank)  # different init: DataParallel must broadcast rank 0's
+    net = torch.nn.Sequential(torch.nn.Linear(8, 32), torch.nn.Tanh(), torch.nn.Linear(32, 4))
+    dp = DataParallel(net, bucket_mb=0.0005)
+    assert len(dp.buckets) > 1
+    opt = torch.optim.SGD(net.parameters(), lr=0.1)
+    x = torch.randn(8, 8, generator=torch.Generator().manual_seed(1))
+    for _ in range(3):
+        dp(x.chunk(world)[rank]).pow(2).mean().backward()
+        opt.step()
+        opt.zero_grad()
+    return [p.detach().clone() for p in net.parameters()]
+
+
+def test_data_parallel_buckets_match_single():
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(8, 32), torch.nn.Tanh(), torch.nn.Linear(32, 4))
+    opt = torch.optim.SGD(net.parameters(), lr=0.1)
+    x = torch.randn(8, 8, generator=torch.Generator().manual_seed(1))
+    for _ in range(3):
+        # mean over ranks of per-rank means == full-batch mean for equal chunks
+        net(x).pow(2).mean().backward()
+        opt.step()
+        opt.zero_grad()
+    res = run_dist(_ddp_worker, 2)
+    for ps in res:
+        for a, b in zip(ps, net.parameters()):
+            assert torch.allclose(a, b.detach(), atol=1e-6)
+
+
+def test_launcher_runs_two_ranks(tmp_path):
+    import subprocess
+    import sys
+
+    script = tmp_path / "w.py"
+    script.write_text(
+        "import os, torch, torch.distributed as dist\n"
+        "dist.init_process_group('gloo')\n"
+        "t = torch.tensor([dist.get_rank() + 1.0]); dist.all_reduce(t)\n"
+        "open(os.path.join(os.path.dirname(__file__), 'out%s' % os.environ['PADDLE_TRAINER_ID']), 'w')"
+        ".write(str(t.item()))\n")
+    from dist_util import _free_port
+
+    rc = subprocess.call([sys.executable, "-m", "paddle_amd.distributed.launch", "--nproc_per_node", "2",
+                          "--master_port", str(_free_port()), str(script)],
+                         cwd="/root/repo", timeout=120)
+    assert rc == 0
+    assert (tmp_path / "out0").read_text() == "3.0" and (tmp_path / "out1").read_text() == "3.0"
