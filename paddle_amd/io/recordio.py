@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import io as _io
 
-from .framework import serialization as S
+from ..framework import serialization as S
 
 
 class Compressor:
@@ -19,7 +19,7 @@ class Compressor:
 
 class RecordIOWriter:
     def __init__(self, filename, compressor=Compressor.Gzip, max_num_records=1000):
-        from .runtime import RecordIOWriter as _W
+        from ..runtime import RecordIOWriter as _W
 
         self._w = _W(filename, compressor, max_num_records)
 
@@ -37,7 +37,7 @@ class RecordIOWriter:
 
 
 def recordio_records(filename):
-    from .runtime import RecordIOScanner
+    from ..runtime import RecordIOScanner
 
     yield from RecordIOScanner(filename)
 

@@ -15,6 +15,36 @@ from .. import ops
 from . import initializer as I
 
 
+class ParamBase(torch.nn.Parameter):
+    """DyGraph parameter: a torch Parameter with Paddle's writable ``name``
+    (``torch.Tensor.name`` is a read-only C attribute) and ``trainable``."""
+
+    @property
+    def name(self):
+        return self.__dict__.get("_pd_name")
+
+    @name.setter
+    def name(self, v):
+        self.__dict__["_pd_name"] = v
+
+    @property
+    def trainable(self):
+        return self.requires_grad
+
+    @trainable.setter
+    def trainable(self, v):
+        self.requires_grad_(bool(v))
+
+    def __deepcopy__(self, memo):
+        p = ParamBase(self.data.clone(memory_format=torch.preserve_format), self.requires_grad)
+        p.__dict__.update({k: v for k, v in self.__dict__.items()})
+        memo[id(self)] = p
+        return p
+
+    def __reduce_ex__(self, proto):
+        return (ParamBase, (self.data, self.requires_grad))
+
+
 class Layer(torch.nn.Module):
     """Paddle-style layer: ``create_parameter``, ``parameters``, ``state_dict`` /
     ``set_state_dict``, ``train`` / ``eval``, ``full_name``."""
@@ -41,12 +71,32 @@ class Layer(torch.nn.Module):
         if init is None:
             init = I.Constant(0.0) if is_bias else I.XavierUniform()
         init(t)
-        p = torch.nn.Parameter(t.to(dt))
+        p = ParamBase(t.to(dt))
         if attr is not None and getattr(attr, "trainable", True) is False:
             p.requires_grad_(False)
         if attr is not None and getattr(attr, "name", None):
             p.name = attr.name
+        else:  # Paddle's naming (<layer>.w_<k> / <layer>.b_<k>): keys of .pdopt accumulators
+            kind = "b" if is_bias else "w"
+            cnt = self.__dict__.setdefault("_pa_pcount", {})
+            k = cnt.get(kind, 0)
+            cnt[kind] = k + 1
+            p.name = f"{self._full_name}.{kind}_{k}"
         return p
+
+    def add_sublayer(self, name, sublayer):
+        self.add_module(name, sublayer)
+        return sublayer
+
+    def sublayers(self, include_self=False):
+        subs = [m for m in self.modules() if m is not self]
+        return ([self] if include_self else []) + subs
+
+    def named_sublayers(self, prefix="", include_self=False):
+        for n, m in self.named_modules(prefix=prefix):
+            if m is self and not include_self:
+                continue
+            yield n, m
 
     def add_parameter(self, name, parameter):
         self.register_parameter(name, parameter)
