@@ -51,7 +51,7 @@ class TopKGate(Layer):
         self.capacity_factor = capacity_factor
 
     def forward(self, x):
-        logits = (x @ self.weight).float()
+        logits = x.float() @ self.weight.float()  # routing in fp32 whatever the activation dtype
         probs = F.softmax(logits, dim=-1)
         val, idx = probs.topk(self.top_k, dim=-1)
         if self.gate_type != "naive" and self.top_k > 1:

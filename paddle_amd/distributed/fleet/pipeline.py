@@ -219,6 +219,17 @@ class PipelineParallel(Layer):
         self.nst = hcg.get_pipe_parallel_world_size()
         self.is_first, self.is_last = hcg.is_first_stage(), hcg.is_last_stage()
         self.total_loss = None
+        # tied-weight groups: new_group is collective, so every rank creates the group
+        # of every pp slice (same order everywhere) and keeps the one it belongs to
+        self._shared_groups = {}
+        for key, stages in sorted(layers.shared_stages.items()):
+            if len(stages) < 2:
+                continue
+            for sl in hcg.topo.axis_groups("pp"):
+                ranks = [sl[s] for s in sorted(stages)]
+                g = comm.new_group(ranks) if comm.is_dist() else None
+                if hcg.global_rank in ranks:
+                    self._shared_groups[key] = g
 
     def parameters(self, recurse=True):
         return self._layers.parameters(recurse)
@@ -261,12 +272,10 @@ class PipelineParallel(Layer):
                 o += n
         # tied weights: sum the gradients of every stage holding the key
         for key, p in self._layers.shared.items():
-            stages = sorted(self._layers.shared_stages[key])
-            if len(stages) > 1:
-                g = comm.new_group([self.hcg.stage_rank(s) for s in stages])
+            if key in self._shared_groups:
                 if p.grad is None:
                     p.grad = torch.zeros_like(p)
-                comm.all_reduce(p.grad, group=g)
+                comm.all_reduce(p.grad, group=self._shared_groups[key])
 
     # ------------------------------------------------------------------ schedule
     def forward_backward_pipeline(self, data):

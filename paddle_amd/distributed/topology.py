@@ -69,12 +69,14 @@ class HybridCommunicateGroup:
         self._groups, self._ranks = {}, {}
         for axis in AXES:
             for ranks in topo.axis_groups(axis):
-                g = comm.new_group(ranks) if comm.is_dist() and len(ranks) > 1 else None
+                g = comm.new_group(ranks) if comm.is_dist() and len(ranks) > 1 else (
+                    comm.SELF if comm.is_dist() else None)
                 if self.global_rank in ranks:
                     self._groups[axis], self._ranks[axis] = g, ranks
         # data-parallel gradient reduction spans dp x sharding (sharding is a dp axis)
         for ranks in self._dp_sharding_slices():
-            g = comm.new_group(ranks) if comm.is_dist() and len(ranks) > 1 else None
+            g = comm.new_group(ranks) if comm.is_dist() and len(ranks) > 1 else (
+                comm.SELF if comm.is_dist() else None)
             if self.global_rank in ranks:
                 self._groups["dp_sharding"], self._ranks["dp_sharding"] = g, ranks
 

@@ -1,0 +1,164 @@
+"""ERNIE-MoE: decoder-only LM with mixture-of-experts FFNs, expert parallelism over
+an all-to-all group and optional fp8 expert weights (BASELINE.json config
+"ERNIE-MoE Fleet expert-parallel all-to-all + fp8 MFMA weights").
+
+Not in the reference (no MoE / all-to-all anywhere).  Architecture
+follows the ERNIE-4.5-MoE family: pre-RMSNorm blocks with rotary attention (the
+LLaMA attention path: fused QKV GEMM + fused rope/flash-attention kernel), the
+first ``first_k_dense`` layers use a dense SwiGLU MLP, the rest an MoE FFN with
+``num_experts`` SwiGLU experts, top-k softmax gating and a GShard auxiliary
+load-balancing loss (``aux_loss_coeff``), optionally plus shared (always-on)
+experts.  Expert GEMMs can run in fp8 (e4m3 weights, see :mod:`..ops.fp8`).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from .. import ops
+from ..distributed.fleet.moe import MoELayer, TopKGate
+from ..nn import Layer
+from ..ops.fp8 import fp8_linear
+from .llama import _dt, _param
+
+
+@dataclass
+class ErnieMoEConfig:
+    vocab_size: int = 103424
+    hidden_size: int = 2560
+    intermediate_size: int = 12288       # dense MLP
+    moe_intermediate_size: int = 1536    # per expert
+    num_hidden_layers: int = 28
+    num_attention_heads: int = 20
+    num_key_value_heads: int = 4
+    num_experts: int = 64
+    num_shared_experts: int = 0
+    top_k: int = 6
+    first_k_dense: int = 1
+    capacity_factor: float | None = None
+    aux_loss_coeff: float = 1e-2
+    max_position_embeddings: int = 4096
+    rms_norm_eps: float = 1e-5
+    rope_theta: float = 500000.0
+    initializer_range: float = 0.02
+    use_fp8_experts: bool = False
+    dtype: str = "bfloat16"
+
+    @property
+    def head_dim(self):
+        return self.hidden_size // self.num_attention_heads
+
+    @property
+    def kv_heads(self):
+        return self.num_key_value_heads or self.num_attention_heads
+
+
+ERNIE_MOE_CONFIGS = {
+    # ERNIE-4.5-21B-A3B-like shape
+    "ernie-moe-21b-a3b": dict(),
+    "ernie-moe-tiny": dict(vocab_size=512, hidden_size=128, intermediate_size=256, moe_intermediate_size=64,
+                           num_hidden_layers=3, num_attention_heads=4, num_key_value_heads=2, num_experts=4,
+                           top_k=2, max_position_embeddings=128),
+}
+
+
+class SwiGLUExpert(Layer):
+    def __init__(self, H, I, device, dt, std, fp8=False):
+        super().__init__("moe_expert")
+        self.gate_up = _param([H, 2 * I], device, dt, std)
+        self.down = _param([I, H], device, dt, std)
+        self.fp8 = fp8
+
+    def forward(self, x):
+        lin = fp8_linear if self.fp8 else ops.linear
+        return lin(ops.swiglu(lin(x, self.gate_up)), self.down)
+
+
+class ErnieMoEDecoderLayer(Layer):
+    def __init__(self, cfg: ErnieMoEConfig, device=None, layer_idx=0, ep_group=None):
+        super().__init__("ernie_moe_decoder")
+        self.cfg = cfg
+        H, D, dt, std = cfg.hidden_size, cfg.head_dim, _dt(cfg.dtype), cfg.initializer_range
+        self.nh, self.nkv = cfg.num_attention_heads, cfg.kv_heads
+        self.input_layernorm = _param([H], device, dt, value=1.0)
+        self.qkv_proj = _param([H, (self.nh + 2 * self.nkv) * D], device, dt, std)
+        self.o_proj = _param([self.nh * D, H], device, dt, std / math.sqrt(2 * cfg.num_hidden_layers))
+        self.post_attention_layernorm = _param([H], device, dt, value=1.0)
+        for n in ("input_layernorm", "post_attention_layernorm"):
+            getattr(self, n).no_weight_decay = True
+        self.is_moe = layer_idx >= cfg.first_k_dense
+        if self.is_moe:
+            from ..parallel import comm
+
+            ep = comm.get_world_size(ep_group)
+            if cfg.num_experts % ep:
+                raise ValueError("num_experts must be divisible by the expert-parallel degree")
+            r = comm.get_rank(ep_group)
+            n_local = cfg.num_experts // ep
+            experts = []
+            for e in range(r * n_local, (r + 1) * n_local):
+                # per-expert seed: expert e has the same init whatever the EP layout
+                state = torch.random.get_rng_state()
+                torch.manual_seed(7919 * (layer_idx + 1) + e)
+                experts.append(SwiGLUExpert(H, cfg.moe_intermediate_size, device, dt, std, cfg.use_fp8_experts))
+                torch.random.set_rng_state(state)
+            gate = TopKGate(H, cfg.num_experts, cfg.top_k, "gshard", cfg.capacity_factor)
+            gate.to(device=device)
+            self.moe = MoELayer(H, experts, gate=gate, group=ep_group, capacity_factor=cfg.capacity_factor)
+            self.shared = SwiGLUExpert(H, cfg.moe_intermediate_size * cfg.num_shared_experts, device, dt, std) \
+                if cfg.num_shared_experts else None
+        else:
+            self.mlp = SwiGLUExpert(H, cfg.intermediate_size, device, dt, std)
+
+    def forward(self, x, residual, cos, sin):
+        cfg, eps = self.cfg, self.cfg.rms_norm_eps
+        if residual is None:
+            h = x
+            y = ops.rms_norm(x, self.input_layernorm, eps)
+        else:
+            y, h = ops.rms_norm(x, self.input_layernorm, eps, residual=residual)
+        a = ops.linear(ops.rope_attention(ops.linear(y, self.qkv_proj), cos, sin, self.nh, self.nkv, causal=True),
+                       self.o_proj)
+        y2, h2 = ops.rms_norm(a, self.post_attention_layernorm, eps, residual=h)
+        if self.is_moe:
+            m = self.moe(y2)
+            if self.shared is not None:
+                m = m + self.shared(y2)
+        else:
+            m = self.mlp(y2)
+        return m, h2
+
+
+class ErnieMoEForCausalLM(Layer):
+    def __init__(self, cfg: ErnieMoEConfig, device=None, ep_group=None):
+        super().__init__("ernie_moe")
+        self.cfg = cfg
+        dt, std, H = _dt(cfg.dtype), cfg.initializer_range, cfg.hidden_size
+        self.embed_tokens = _param([cfg.vocab_size, H], device, dt, std)
+        self.layers = torch.nn.ModuleList([ErnieMoEDecoderLayer(cfg, device, i, ep_group)
+                                           for i in range(cfg.num_hidden_layers)])
+        self.norm = _param([H], device, dt, value=1.0)
+        self.norm.no_weight_decay = True
+        self.lm_head = _param([H, cfg.vocab_size], device, dt, std)
+        cos, sin = ops.rope_tables(cfg.max_position_embeddings, cfg.head_dim, cfg.rope_theta, device=device)
+        self.register_buffer("rope_cos", cos, persistent=False)
+        self.register_buffer("rope_sin", sin, persistent=False)
+
+    def forward(self, input_ids, labels=None):
+        x = ops.embedding(input_ids, self.embed_tokens)
+        residual = None
+        aux = []
+        for layer in self.layers:
+            x, residual = layer(x, residual, self.rope_cos, self.rope_sin)
+            if layer.is_moe and layer.moe.l_aux is not None:
+                aux.append(layer.moe.l_aux)
+        y, _ = ops.rms_norm(x, self.norm, self.cfg.rms_norm_eps, residual=residual)
+        logits = ops.linear(y, self.lm_head)
+        if labels is None:
+            return logits
+        loss = ops.softmax_cross_entropy(logits, labels, inplace_grad=True)
+        if aux and self.cfg.aux_loss_coeff:
+            loss = loss + self.cfg.aux_loss_coeff * torch.stack(aux).mean()
+        return loss

@@ -50,11 +50,26 @@ def is_dist():
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
+class _SelfGroup:
+    """A one-rank group (an axis of degree 1 in a hybrid topology).  ``None`` means
+    the WORLD group everywhere in this module, so size-1 axes need their own token."""
+
+    def __repr__(self):
+        return "SELF"
+
+
+SELF = _SelfGroup()
+
+
 def get_rank(group=None):
+    if group is SELF:
+        return 0
     return dist.get_rank(group) if is_dist() else 0
 
 
 def get_world_size(group=None):
+    if group is SELF:
+        return 1
     return dist.get_world_size(group) if is_dist() else 1
 
 
@@ -137,6 +152,8 @@ def new_group(ranks):
 
 
 def barrier(group=None):
+    if group is SELF:
+        return
     if is_dist():
         if dist.get_backend(group) == "nccl":
             dist.barrier(group=group, device_ids=[torch.cuda.current_device()])
