@@ -58,6 +58,8 @@ class ErnieMoEConfig:
 ERNIE_MOE_CONFIGS = {
     # ERNIE-4.5-21B-A3B-like shape
     "ernie-moe-21b-a3b": dict(),
+    # same block shapes, 8 layers: fits one MI355X with unsharded optimizer state
+    "ernie-moe-a3b-8l": dict(num_hidden_layers=8),
     "ernie-moe-tiny": dict(vocab_size=512, hidden_size=128, intermediate_size=256, moe_intermediate_size=64,
                            num_hidden_layers=3, num_attention_heads=4, num_key_value_heads=2, num_experts=4,
                            top_k=2, max_position_embeddings=128),
