@@ -10,3 +10,5 @@ from .ops import *  # noqa: F401,F403
 from .tensor import *  # noqa: F401,F403
 from .sequence import *  # noqa: F401,F403
 from .detection import *  # noqa: F401,F403
+from . import rnn  # noqa: F401,E402
+from .rnn import *  # noqa: F401,F403,E402

@@ -1,0 +1,390 @@
+"""RNN / CRF / CTC / sampled-loss / beam-search / metric / detection operators vs
+NumPy (or brute-force) references of the reference kernels' semantics
+(reference tests: test_lstm_op.py, test_gru_op.py, test_linear_chain_crf_op.py,
+test_crf_decoding_op.py, test_chunk_eval_op.py, test_warpctc_op.py,
+test_edit_distance_op.py, test_nce.py, test_hsigmoid_op.py, test_beam_search_op.py,
+test_auc_op.py, test_prior_box_op.py, test_box_coder_op.py, test_multiclass_nms_op.py)."""
+import itertools
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import paddle_amd.fluid as fluid
+from op_test import OpTest
+from paddle_amd.framework import core
+
+rng = np.random.RandomState(7)
+sig = lambda x: 1 / (1 + np.exp(-x))  # noqa: E731
+
+
+def _offs(lens):
+    return np.concatenate([[0], np.cumsum(lens)]).astype(int)
+
+
+def _run(op, inputs, outputs, attrs=None, atol=1e-5, grad=None, grad_out=None, tol=0.02):
+    t = OpTest()
+    t.op_type, t.inputs, t.outputs, t.attrs = op, inputs, outputs, attrs or {}
+    t.check_output(atol=atol, rtol=1e-4, places=[fluid.CPUPlace()])
+    if grad:
+        t.check_grad(grad, [grad_out], max_relative_error=tol, places=[fluid.CPUPlace()])
+
+
+# ------------------------------------------------------------------------- LSTM
+def _lstm_ref(x, w, b, lens, D, peep, reverse):
+    H, C = np.zeros((x.shape[0], D)), np.zeros((x.shape[0], D))
+    off = _offs(lens)
+    for s in range(len(lens)):
+        rows = list(range(off[s], off[s + 1]))
+        if reverse:
+            rows = rows[::-1]
+        h, c = np.zeros(D), np.zeros(D)
+        for r in rows:
+            g = x[r] + b[0, :4 * D] + h @ w
+            gc, gi, gf, go = np.split(g, 4)
+            if peep:
+                gi = gi + c * b[0, 4 * D:5 * D]
+                gf = gf + c * b[0, 5 * D:6 * D]
+            c = np.tanh(gc) * sig(gi) + c * sig(gf)
+            if peep:
+                go = go + c * b[0, 6 * D:7 * D]
+            h = sig(go) * np.tanh(c)
+            H[r], C[r] = h, c
+    return H.astype("float32"), C.astype("float32")
+
+
+@pytest.mark.parametrize("peep,reverse", [(True, False), (False, True)])
+def test_lstm_op(peep, reverse):
+    D, lens = 3, [2, 3]
+    x = rng.uniform(-0.5, 0.5, (5, 4 * D)).astype("float32")
+    w = rng.uniform(-0.5, 0.5, (D, 4 * D)).astype("float32")
+    b = rng.uniform(-0.5, 0.5, (1, 7 * D if peep else 4 * D)).astype("float32")
+    H, C = _lstm_ref(x, w, b, lens, D, peep, reverse)
+    _run("lstm", {"Input": (x, [lens]), "Weight": w, "Bias": b}, {"Hidden": H, "Cell": C},
+         {"use_peepholes": peep, "is_reverse": reverse}, grad=["Input", "Weight"], grad_out="Hidden")
+
+
+def test_gru_op():
+    D, lens = 3, [3, 1]
+    x = rng.uniform(-0.5, 0.5, (4, 3 * D)).astype("float32")
+    w = rng.uniform(-0.5, 0.5, (D, 3 * D)).astype("float32")
+    b = rng.uniform(-0.5, 0.5, (1, 3 * D)).astype("float32")
+    Hr = np.zeros((4, D))
+    off = _offs(lens)
+    for s in range(2):
+        h = np.zeros(D)
+        for r in range(off[s], off[s + 1]):
+            g = x[r] + b[0]
+            u = sig(g[:D] + h @ w[:, :D])
+            rr = sig(g[D:2 * D] + h @ w[:, D:2 * D])
+            c = np.tanh(g[2 * D:] + (rr * h) @ w[:, 2 * D:])
+            h = h - u * h + u * c
+            Hr[r] = h
+    _run("gru", {"Input": (x, [lens]), "Weight": w, "Bias": b}, {"Hidden": Hr.astype("float32")},
+         grad=["Input", "Weight"], grad_out="Hidden")
+
+
+def test_lstm_unit_and_gru_unit():
+    x = rng.uniform(-1, 1, (2, 8)).astype("float32")
+    cp = rng.uniform(-1, 1, (2, 2)).astype("float32")
+    i, f, o, g = np.split(x, 4, 1)
+    c = sig(f + 0.5) * cp + sig(i) * np.tanh(g)
+    _run("lstm_unit", {"X": x, "C_prev": cp}, {"C": c, "H": sig(o) * np.tanh(c)}, {"forget_bias": 0.5},
+         grad=["X"], grad_out="H")
+    D = 2
+    xi = rng.uniform(-1, 1, (3, 3 * D)).astype("float32")
+    hp = rng.uniform(-1, 1, (3, D)).astype("float32")
+    w = rng.uniform(-1, 1, (D, 3 * D)).astype("float32")
+    u = sig(xi[:, :D] + hp @ w[:, :D])
+    r = sig(xi[:, D:2 * D] + hp @ w[:, D:2 * D])
+    cc = np.tanh(xi[:, 2 * D:] + (r * hp) @ w[:, 2 * D:])
+    _run("gru_unit", {"Input": xi, "HiddenPrev": hp, "Weight": w}, {"Hidden": hp - u * hp + u * cc},
+         grad=["Input", "HiddenPrev"], grad_out="Hidden")
+
+
+# -------------------------------------------------------------------------- CRF
+def _crf_brute(em, tr, lab):
+    T, D = em.shape
+
+    def score(y):
+        s = tr[0, y[0]] + em[0, y[0]] + tr[1, y[-1]]
+        for t in range(1, T):
+            s += em[t, y[t]] + tr[2 + y[t - 1], y[t]]
+        return s
+
+    logz = np.log(sum(np.exp(score(y)) for y in itertools.product(range(D), repeat=T)))
+    best = max(itertools.product(range(D), repeat=T), key=score)
+    return logz - score(lab), best
+
+
+def test_linear_chain_crf_and_decoding():
+    D, lens = 3, [3, 2]
+    em = rng.uniform(-1, 1, (5, D)).astype("float32")
+    tr = rng.uniform(-0.5, 0.5, (D + 2, D)).astype("float32")
+    lab = rng.randint(0, D, (5, 1)).astype("int64")
+    off = _offs(lens)
+    nll, paths = [], []
+    for s in range(2):
+        v, best = _crf_brute(em[off[s]:off[s + 1]].astype("float64"), tr.astype("float64"),
+                             lab[off[s]:off[s + 1], 0])
+        nll.append([v])
+        paths += list(best)
+    _run("linear_chain_crf", {"Emission": (em, [lens]), "Transition": tr, "Label": (lab, [lens])},
+         {"LogLikelihood": np.array(nll, "float32")}, atol=1e-4, grad=["Emission", "Transition"],
+         grad_out="LogLikelihood")
+    _run("crf_decoding", {"Emission": (em, [lens]), "Transition": tr},
+         {"ViterbiPath": np.array(paths, "int64").reshape(-1, 1)})
+
+
+def test_chunk_eval_iob():
+    # types: 0,1 ; IOB tags: B=0 I=1 ; label = type*2 + tag ; O = 4
+    lab = np.array([0, 1, 4, 2, 3, 4, 0], "int64").reshape(-1, 1)   # chunks: (0-1,t0) (3-4,t1) (6,t0)
+    inf = np.array([0, 1, 4, 2, 4, 4, 0], "int64").reshape(-1, 1)   # chunks: (0-1,t0) (3,t1) (6,t0)
+    lens = [7]
+    p, r = 2 / 3, 2 / 3
+    _run("chunk_eval", {"Inference": (inf, [lens]), "Label": (lab, [lens])},
+         {"Precision": np.array([p], "float32"), "Recall": np.array([r], "float32"),
+          "F1-Score": np.array([2 * p * r / (p + r)], "float32"), "NumInferChunks": np.array([3], "int64"),
+          "NumLabelChunks": np.array([3], "int64"), "NumCorrectChunks": np.array([2], "int64")},
+         {"num_chunk_types": 2, "chunk_scheme": "IOB"})
+
+
+# -------------------------------------------------------------------------- CTC
+def test_warpctc_matches_ctc_loss_and_grad():
+    C, xl, ll = 4, [5, 4], [2, 2]
+    x = rng.uniform(-1, 1, (9, C)).astype("float32")
+    lab = np.array([1, 2, 3, 1], "int64").reshape(-1, 1)
+    logp = torch.log_softmax(torch.from_numpy(x), -1)
+    want = []
+    for s in range(2):
+        xo, lo = _offs(xl), _offs(ll)
+        want.append(float(torch.nn.functional.ctc_loss(logp[xo[s]:xo[s + 1]].unsqueeze(1),
+                                                       torch.from_numpy(lab[lo[s]:lo[s + 1], 0]).unsqueeze(0),
+                                                       [xl[s]], [ll[s]], blank=0, reduction="sum")))
+    _run("warpctc", {"Logits": (x, [xl]), "Label": (lab, [ll])}, {"Loss": np.array(want, "float32").reshape(-1, 1)},
+         {"blank": 0}, atol=1e-4, grad=["Logits"], grad_out="Loss")
+
+
+def test_ctc_align_and_edit_distance():
+    x = np.array([0, 1, 1, 0, 2, 2, 0, 3, 3, 3], "int64").reshape(-1, 1)
+    t = OpTest()
+    t.op_type, t.inputs, t.attrs = "ctc_align", {"Input": (x, [[6, 4]])}, {"blank": 0, "merge_repeated": True}
+    t.outputs = {"Output": (np.array([1, 2, 3], "int64").reshape(-1, 1), [[2, 1]])}
+    t.check_output(places=[fluid.CPUPlace()])
+    h = np.array([1, 2, 3, 4, 5], "int64").reshape(-1, 1)
+    r = np.array([1, 3, 3, 5, 5, 5], "int64").reshape(-1, 1)
+    # "123" vs "13" -> 1 ; "45" vs "5555" -> 3
+    _run("edit_distance", {"Hyps": (h, [[3, 2]]), "Refs": (r, [[2, 4]])},
+         {"Out": np.array([[1.0], [3.0]], "float32"), "SequenceNum": np.array([2], "int64")})
+
+
+# ------------------------------------------------------------- sampled losses
+def test_nce_custom_negatives():
+    N, D, C = 3, 4, 6
+    x = rng.uniform(-1, 1, (N, D)).astype("float32")
+    w = rng.uniform(-1, 1, (C, D)).astype("float32")
+    b = rng.uniform(-1, 1, (C, 1)).astype("float32")
+    lab = np.array([[1], [4], [2]], "int64")
+    neg = [0, 5]
+    bb = 2.0 / C
+    cost = []
+    for i in range(N):
+        cls = [lab[i, 0]] + neg
+        o = sig(np.array([x[i] @ w[c] + b[c, 0] for c in cls]))
+        cost.append(-math.log(o[0] / (o[0] + bb)) - sum(math.log(bb / (v + bb)) for v in o[1:]))
+    _run("nce", {"Input": x, "Label": lab, "Weight": w, "Bias": b}, {"Cost": np.array(cost, "float32").reshape(-1, 1)},
+         {"num_total_classes": C, "num_neg_samples": 2, "custom_neg_classes": neg}, atol=1e-4,
+         grad=["Input", "Weight"], grad_out="Cost")
+
+
+def test_hierarchical_sigmoid():
+    N, D, C = 4, 5, 6
+    x = rng.uniform(-1, 1, (N, D)).astype("float32")
+    w = rng.uniform(-1, 1, (C - 1, D)).astype("float32")
+    lab = np.array([[0], [3], [5], [2]], "int64")
+    out = []
+    for i in range(N):
+        c = int(lab[i, 0]) + C
+        L = int(math.floor(math.log2(c)))
+        tot = 0.0
+        for j in range(L):
+            idx = (c >> (j + 1)) - 1
+            bit = (c >> j) & 1
+            pre = float(np.clip(x[i] @ w[idx], -40, 40))
+            tot += math.log1p(math.exp(pre)) - bit * pre
+        out.append([tot])
+    _run("hierarchical_sigmoid", {"X": x, "W": w, "Label": lab}, {"Out": np.array(out, "float32")},
+         {"num_classes": C}, atol=1e-4, grad=["X", "W"], grad_out="Out")
+
+
+# ---------------------------------------------------------------- beam search
+def test_beam_search_and_decode():
+    # 1 source, 2 prefixes; candidates (top-2 per prefix)
+    pre_ids = np.array([[1], [2]], "int64")
+    pre_scores = np.array([[0.1], [0.2]], "float32")
+    ids = np.array([[3, 4], [5, 6]], "int64")
+    scores = np.array([[0.5, 0.3], [0.9, 0.1]], "float32")
+    lod = [[0, 2], [0, 1, 2]]
+    t = OpTest()
+    t.op_type = "beam_search"
+    t.inputs = {"pre_ids": (pre_ids, None), "pre_scores": pre_scores, "ids": (ids, [[2], [1, 1]]), "scores": scores}
+    t.attrs = {"level": 0, "beam_size": 2, "end_id": 0}
+    t.outputs = {"selected_ids": (np.array([[3], [5]], "int64"), [[0, 2], [0, 1, 2]]),
+                 "selected_scores": (np.array([[0.5], [0.9]], "float32"), [[0, 2], [0, 1, 2]])}
+    t.check_output(places=[fluid.CPUPlace()])
+
+    from paddle_amd.operators.structured_ops import beam_search_decode as dec  # noqa: F401
+    from paddle_amd.framework.registry import KernelContext, get_op_info
+
+    # two steps, beam 2, one source: step0 ids [7, 8]; step1: prefix0 -> 9, prefix1 -> 0(end)
+    s0 = core.LoDTensor(torch.tensor([[7], [8]]), [[0, 2], [0, 1, 2]])
+    s1 = core.LoDTensor(torch.tensor([[9], [0]]), [[0, 2], [0, 1, 2]])
+    c0 = core.LoDTensor(torch.tensor([[0.5], [0.4]]), [[0, 2], [0, 1, 2]])
+    c1 = core.LoDTensor(torch.tensor([[0.9], [0.6]]), [[0, 2], [0, 1, 2]])
+    ctx = KernelContext("beam_search_decode", {"Ids": [core.LoDTensorArray([s0, s1])],
+                                               "Scores": [core.LoDTensorArray([c0, c1])]},
+                        {"SentenceIds": ["a"], "SentenceScores": ["b"]}, {"beam_size": 2, "end_id": 0})
+    get_op_info("beam_search_decode").kernel(ctx)
+    out = ctx.results["SentenceIds"][0]
+    assert out.tensor.tolist() == [7, 9, 8, 0] and out.lod() == [[0, 2], [0, 2, 4]]
+
+
+# ------------------------------------------------------------------- metrics
+def test_auc_op_close_to_exact():
+    from sklearn.metrics import roc_auc_score
+
+    p = rng.uniform(0, 1, 200).astype("float32")
+    lab = (rng.uniform(0, 1, 200) < p).astype("int64").reshape(-1, 1)
+    pred = np.stack([1 - p, p], 1)
+    t = OpTest()
+    t.op_type, t.inputs, t.attrs = "auc", {"Predict": pred, "Label": lab}, {"num_thresholds": 200}
+    t.outputs = {"AUC": np.array([roc_auc_score(lab[:, 0], p)], "float64")}
+    t.check_output(atol=0.01, places=[fluid.CPUPlace()])
+
+
+def test_mean_iou_and_precision_recall():
+    pred = np.array([0, 1, 1, 2, 2, 0], "int32")
+    lab = np.array([0, 1, 2, 2, 1, 1], "int32")
+    # class0: c=1 w=1 ; class1: c=1 w=(pred1!=lab: idx2)1 + (lab1!=pred: idx4, idx5) 2 = 3 ; class2: c=1 w=1+1=2
+    miou = (1 / 2 + 1 / 4 + 1 / 3) / 3
+    _run("mean_iou", {"Predictions": pred, "Labels": lab},
+         {"OutMeanIou": np.array([miou], "float32"), "OutCorrect": np.array([1, 1, 1], "int32")},
+         {"num_classes": 3})
+
+
+# ----------------------------------------------------------------- detection
+def test_prior_box_and_box_coder_roundtrip():
+    main, startup = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, startup):
+        feat = fluid.layers.data("feat", [8, 4, 4])
+        img = fluid.layers.data("img", [3, 32, 32])
+        box, var = fluid.layers.prior_box(feat, img, min_sizes=[8.0], max_sizes=[16.0], aspect_ratios=[2.0],
+                                          flip=True, clip=True)
+        tgt = fluid.layers.data("tgt", [4], append_batch_size=True)
+        enc = fluid.layers.box_coder(fluid.layers.reshape(box, [-1, 4]), fluid.layers.reshape(var, [-1, 4]), tgt)
+        dec = fluid.layers.box_coder(fluid.layers.reshape(box, [-1, 4]), fluid.layers.reshape(var, [-1, 4]), enc,
+                                     code_type="decode_center_size")
+    exe = fluid.Executor(fluid.CPUPlace())
+    t = np.array([[0.1, 0.2, 0.5, 0.6], [0.3, 0.3, 0.9, 0.8]], "float32")
+    b, e, d = exe.run(main, feed={"feat": np.zeros((1, 8, 4, 4), "float32"), "img": np.zeros((1, 3, 32, 32), "float32"),
+                                  "tgt": t}, fetch_list=[box, enc, d if False else dec], scope=core.Scope())
+    assert b.shape == (4, 4, 4, 4)  # ars {1, 2, 1/2} + sqrt(min*max) box
+    # first cell, first prior: centre (4, 4) px, size 8 -> [0, 0, 8, 8] / 32
+    np.testing.assert_allclose(b[0, 0, 0], [0.0, 0.0, 0.25, 0.25], atol=1e-6)
+    np.testing.assert_allclose(d[:, 5], t, atol=1e-5)
+
+
+def test_iou_bipartite_nms_polygon():
+    a = np.array([[0, 0, 1, 1], [0.5, 0.5, 1.5, 1.5]], "float32")
+    bx = np.array([[0, 0, 1, 1], [1, 1, 2, 2], [0.5, 0, 1.5, 1]], "float32")
+    iou = np.array([[1, 0, 1 / 3], [1 / 7, 1 / 7, 1 / 3]], "float32")
+    _run("iou_similarity", {"X": a, "Y": bx}, {"Out": iou}, atol=1e-5)
+    dist = np.array([[0.9, 0.1, 0.6], [0.8, 0.2, 0.7]], "float32")
+    _run("bipartite_match", {"DistMat": (dist, [[2]])},
+         {"ColToRowMatchIndices": np.array([[0, -1, 1]], "int32"),
+          "ColToRowMatchDist": np.array([[0.9, 0.0, 0.7]], "float32")})
+    boxes = np.array([[[0, 0, 1, 1], [0, 0, 1.05, 1], [2, 2, 3, 3]]], "float32")
+    scores = np.array([[[0.0, 0.0, 0.0], [0.9, 0.8, 0.7]]], "float32")  # [N, C, M]
+    t = OpTest()
+    t.op_type, t.inputs = "multiclass_nms", {"BBoxes": boxes, "Scores": scores}
+    t.attrs = {"background_label": 0, "score_threshold": 0.1, "nms_top_k": 10, "nms_threshold": 0.5,
+               "keep_top_k": 10}
+    t.outputs = {"Out": (np.array([[1, 0.9, 0, 0, 1, 1], [1, 0.7, 2, 2, 3, 3]], "float32"), [[2]])}
+    t.check_output(places=[fluid.CPUPlace()])
+    x = rng.uniform(0, 1, (1, 4, 2, 3)).astype("float32")
+    gw = np.tile(np.arange(3), (2, 1))
+    gh = np.tile(np.arange(2).reshape(2, 1), (1, 3))
+    want = np.stack([gw - x[0, 0], gh - x[0, 1], gw - x[0, 2], gh - x[0, 3]])[None].astype("float32")
+    _run("polygon_box_transform", {"Input": x}, {"Output": want})
+
+
+def test_anchor_generator_values():
+    t = OpTest()
+    t.op_type = "anchor_generator"
+    t.inputs = {"Input": np.zeros((1, 2, 1, 1), "float32")}
+    t.attrs = {"anchor_sizes": [32.0], "aspect_ratios": [1.0], "stride": [16.0, 16.0], "offset": 0.5,
+               "variances": [0.1, 0.1, 0.2, 0.2]}
+    # base_w = round(sqrt(256)) = 16, scale 2 -> w = 32 ; centre 0.5*15 = 7.5 ; half-extent (32-1)/2
+    t.outputs = {"Anchors": np.array([[[[7.5 - 15.5, 7.5 - 15.5, 7.5 + 15.5, 7.5 + 15.5]]]], "float32")}
+    t.check_output(places=[fluid.CPUPlace()])
+
+
+# ------------------------------------------------------ layers end to end
+def test_dynamic_lstm_sentiment_model_trains():
+    main, startup = fluid.Program(), fluid.Program()
+    main.random_seed = startup.random_seed = 3
+    with fluid.program_guard(main, startup):
+        words = fluid.layers.data("words", [1], dtype="int64", lod_level=1)
+        label = fluid.layers.data("label", [1], dtype="int64")
+        emb = fluid.layers.embedding(words, size=[20, 8])
+        fc0 = fluid.layers.fc(emb, size=4 * 8)
+        h, _ = fluid.layers.dynamic_lstm(fc0, size=4 * 8)
+        g = fluid.layers.dynamic_gru(fluid.layers.fc(h, 3 * 8), size=8)
+        pooled = fluid.layers.sequence_pool(g, "max")
+        pred = fluid.layers.fc(pooled, 2, act="softmax")
+        loss = fluid.layers.mean(fluid.layers.cross_entropy(pred, label))
+        fluid.optimizer.Adam(0.02).minimize(loss)
+    exe = fluid.Executor(fluid.CPUPlace())
+    scope = core.Scope()
+    r = np.random.RandomState(0)
+    lens = [3, 5, 2, 4]
+    seqs = [r.randint(0, 20, n) for n in lens]
+    labels = np.array([[int(s.sum() % 2)] for s in seqs], "int64")
+    t = fluid.create_lod_tensor(np.concatenate(seqs).reshape(-1, 1).astype("int64"), [lens], fluid.CPUPlace())
+    losses = []
+    with fluid.executor.scope_guard(scope):
+        exe.run(startup)
+        for _ in range(40):
+            (l,) = exe.run(main, feed={"words": t, "label": labels}, fetch_list=[loss])
+            losses.append(float(l[0]))
+    assert losses[-1] < 0.5 * losses[0]
+
+
+def test_crf_tagging_model_trains_and_decodes():
+    main, startup = fluid.Program(), fluid.Program()
+    main.random_seed = startup.random_seed = 5
+    with fluid.program_guard(main, startup):
+        x = fluid.layers.data("x", [6], lod_level=1)
+        y = fluid.layers.data("y", [1], dtype="int64", lod_level=1)
+        em = fluid.layers.fc(x, 3)
+        nll = fluid.layers.linear_chain_crf(em, y, param_attr=fluid.ParamAttr(name="crfw"))
+        loss = fluid.layers.mean(nll)
+        path = fluid.layers.crf_decoding(em, param_attr=fluid.ParamAttr(name="crfw"))
+        fluid.optimizer.SGD(0.1).minimize(loss)
+    exe = fluid.Executor(fluid.CPUPlace())
+    scope = core.Scope()
+    r = np.random.RandomState(1)
+    xs = r.uniform(-1, 1, (9, 6)).astype("float32")
+    ys = (xs[:, :3].argmax(1)).reshape(-1, 1).astype("int64")
+    lens = [4, 5]
+    xt = fluid.create_lod_tensor(xs, [lens], fluid.CPUPlace())
+    yt = fluid.create_lod_tensor(ys, [lens], fluid.CPUPlace())
+    with fluid.executor.scope_guard(scope):
+        exe.run(startup)
+        first = None
+        for _ in range(60):
+            l, p = exe.run(main, feed={"x": xt, "y": yt}, fetch_list=[loss, path])
+            first = float(l[0]) if first is None else first
+    assert float(l[0]) < first
+    assert (np.asarray(p).reshape(-1) == ys.reshape(-1)).mean() > 0.7
