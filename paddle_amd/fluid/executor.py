@@ -71,6 +71,17 @@ class Executor:
         self.use_hip_graph = FLAGS.get("use_hip_graph") if use_hip_graph is None else use_hip_graph
 
     def close(self):
+        """Reference executor.py close(): tell every parameter server this trainer
+        talked to that it is done (SendComplete), so sync pservers can exit."""
+        import sys
+
+        if not self._closed and "paddle_amd.distributed.ps.rpc" in sys.modules:
+            from ..distributed.ps import RPCClient
+
+            c = RPCClient.instance()
+            if c.endpoints:
+                c.complete(sorted(c.endpoints))
+                c.endpoints.clear()
         self._closed = True
 
     def as_lodtensor(self, data):

@@ -1,3 +1,3 @@
 """Operator library: importing this package registers every op kernel."""
 from . import io_ops, math_ops, nn_ops, optimizer_ops, sequence_ops, tensor_ops  # noqa: F401
-from . import detection_ops, metric_ops, rnn_ops, structured_ops  # noqa: F401
+from . import detection_ops, dist_ops, metric_ops, rnn_ops, structured_ops  # noqa: F401
