@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--recompute", action="store_true")
     ap.add_argument("--bucket-mb", type=int, default=256)
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--no-tuned-gemm", action="store_true",
+                    help="use hipBLASLt's heuristic GEMM pick instead of the stored tuned solutions")
     args = ap.parse_args()
 
     from paddle_amd.models.llama import LLAMA_CONFIGS, LlamaConfig, LlamaForCausalLM, llama_flops_per_token
@@ -58,6 +60,11 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     torch.manual_seed(1234 + rank)
+    tuned = False
+    if not args.no_tuned_gemm:
+        from paddle_amd.utils import gemm_tuning
+
+        tuned = gemm_tuning.enable(args.model, verbose=rank == 0)
 
     cfgd = dict(LLAMA_CONFIGS[args.model])
     if args.layers:
@@ -146,6 +153,7 @@ def main():
                 "params_b": round(nparams / 1e9, 3),
                 "mfu_bf16_dense": round(mfu, 4),
                 "recompute": bool(args.recompute),
+                "tuned_gemm": tuned,
             },
         }
         print(json.dumps(out), flush=True)
