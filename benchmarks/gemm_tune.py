@@ -95,7 +95,7 @@ def main():
             r[f"{k}_default_TF"] = round(flop / r[f"{k}_default_ms"] / 1e9, 1)
             r[f"{k}_tuned_TF"] = round(flop / t / 1e9, 1)
         print(json.dumps({"shape": name, **res[name]}), flush=True)
-    torch.cuda.tunable.write_file()
+    # TunableOp writes the results file itself at process exit
     tot_d = sum(v for r in res.values() for k, v in r.items() if k.endswith("default_ms"))
     tot_t = sum(v for r in res.values() for k, v in r.items() if k.endswith("tuned_ms"))
     print(json.dumps({"summary": True, "default_ms": round(tot_d, 3), "tuned_ms": round(tot_t, 3),

@@ -34,6 +34,32 @@ def mul(ctx):
     ctx.set_output("Out", out.reshape(tuple(x.shape[:xn]) + tuple(y.shape[yn:])))
 
 
+@register_op("fc", ["Input", "W", "Bias?"], ["Out"], {"in_num_col_dims": 1, "activation_type": ""})
+def fc(ctx):
+    """Fused fully-connected op produced by ``fc_fuse_pass`` (reference fc_op.cc:154):
+    Out = act(flatten(Input, in_num_col_dims) @ W + Bias).  On the HIP device the
+    bias (and ReLU/GELU) ride the hipBLASLt epilogue of one GEMM instead of
+    separate elementwise passes over the output."""
+    x, w = ctx.input("Input"), ctx.input("W")
+    n = ctx.attr("in_num_col_dims")
+    x2 = _flat2(x, n)
+    w = w.to(x2.dtype)
+    act = ctx.attr("activation_type") or ""
+    if ctx.has_input("Bias"):
+        b = ctx.input("Bias").reshape(-1).to(x2.dtype)
+        if act in ("relu", "gelu") and x2.is_cuda:
+            out = torch._addmm_activation(b, x2, w, use_gelu=(act == "gelu"))
+            act = ""
+        else:
+            out = torch.addmm(b, x2, w)
+    else:
+        out = x2 @ w
+    if act:
+        out = {"relu": torch.relu, "gelu": torch.nn.functional.gelu, "tanh": torch.tanh,
+               "sigmoid": torch.sigmoid}[act](out)
+    ctx.set_output("Out", out.reshape(tuple(x.shape[:n]) + (w.shape[1],)), ctx.input_lod("Input"))
+
+
 @register_op("mul_grad", ["X", "Y", "Out?", "Out@GRAD"], ["X@GRAD?", "Y@GRAD?"],
              {"x_num_col_dims": 1, "y_num_col_dims": 1}, grad=None, no_infer=True)
 def mul_grad(ctx):

@@ -1,0 +1,143 @@
+"""IR graph/pass framework and the inference predictor (reference tests:
+framework/ir/graph_test.cc, pass_test.cc, graph_pattern_detector_tester.cc,
+fc_fuse_pass_tester.cc; inference/api/api_impl_tester.cc which loads a model
+saved by the book tests and compares the predictor with the executor)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import paddle_amd.fluid as fluid
+from paddle_amd import inference
+from paddle_amd.framework import core, ir
+
+
+def _mlp_program():
+    main, startup = fluid.Program(), fluid.Program()
+    main.random_seed = startup.random_seed = 5
+    with fluid.program_guard(main, startup):
+        x = fluid.layers.data(name="x", shape=[16], dtype="float32")
+        h = fluid.layers.fc(input=x, size=32, act="relu")
+        h = fluid.layers.dropout(h, dropout_prob=0.1, dropout_implementation="upscale_in_train")
+        h = fluid.layers.fc(input=h, size=32, act="tanh")
+        y = fluid.layers.fc(input=h, size=4)
+    return main, startup, y
+
+
+def test_graph_build_topo_sort_and_cycle_check():
+    main, _, _ = _mlp_program()
+    g = ir.Graph(main.global_block())
+    assert len(g.op_nodes()) == len(main.global_block().ops)
+    order = [n.op for n in ir.topology_sort(g)]
+    assert order == main.global_block().ops  # already a valid order: stable sort keeps it
+    assert not ir.has_circle(g)
+    # SSA: a var written twice gets two nodes
+    names = [n.name for n in g.var_nodes()]
+    assert len(names) >= len(set(names))
+
+
+def test_pattern_detector_finds_mul_add_pairs():
+    main, _, _ = _mlp_program()
+    g = ir.Graph(main.global_block())
+    d = ir.GraphPatternDetector()
+    p = d.pattern
+    mul = p.new_node("mul").assert_op("mul")
+    t = p.new_node("t").assert_is_op_output("mul", "Out").assert_is_op_input("elementwise_add", "X")
+    add = p.new_node("add").assert_op("elementwise_add")
+    t.as_output(mul).as_input(add)
+    assert len(d.detect(g)) == 3
+
+
+def test_fc_fuse_pass_preserves_numerics(tmp_path):
+    main, startup, y = _mlp_program()
+    test_prog = main.clone(for_test=True)
+    exe = fluid.Executor(fluid.CPUPlace())
+    scope = core.Scope()
+    x = np.random.RandomState(0).rand(8, 16).astype("float32")
+    with fluid.executor.scope_guard(scope):
+        exe.run(startup)
+        (ref,) = exe.run(test_prog, feed={"x": x}, fetch_list=[y])
+        g = ir.apply_passes(test_prog, ["is_test_pass", "identity_op_clean_pass", "fc_fuse_pass",
+                                        "fc_act_fuse_pass", "graph_viz_pass"],
+                            graph_viz_path=str(tmp_path / "g.dot"))
+        types = [op.type for op in test_prog.global_block().ops]
+        assert g.get("fc_fuse_count") == 3 and g.get("fc_act_fuse_count") == 2, types
+        assert "mul" not in types and "dropout" not in types and "relu" not in types
+        (out,) = exe.run(test_prog, feed={"x": x}, fetch_list=[y])
+    np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-6)
+    assert os.path.getsize(tmp_path / "g.dot") > 0
+
+
+def test_pass_registry_and_builder():
+    assert {"fc_fuse_pass", "graph_viz_pass", "graph_to_program_pass", "infer_clean_graph_pass"} <= \
+        set(ir.all_passes())
+    b = ir.PassBuilder(["is_test_pass"])
+    b.append_pass("fc_fuse_pass")
+    b.insert_pass(0, "infer_clean_graph_pass")
+    assert [p.name for p in b.all_passes()] == ["infer_clean_graph_pass", "is_test_pass", "fc_fuse_pass"]
+    b.remove_pass(0)
+    assert len(b.all_passes()) == 2
+    with pytest.raises(KeyError):
+        ir.get_pass("no_such_pass")
+
+
+def _save_conv_model(d):
+    main, startup = fluid.Program(), fluid.Program()
+    main.random_seed = startup.random_seed = 3
+    with fluid.program_guard(main, startup):
+        img = fluid.layers.data(name="img", shape=[1, 12, 12], dtype="float32")
+        c = fluid.layers.conv2d(img, num_filters=6, filter_size=3, bias_attr=False)
+        c = fluid.layers.batch_norm(c, act="relu")
+        c = fluid.layers.pool2d(c, pool_size=2, pool_stride=2)
+        h = fluid.layers.fc(input=c, size=16, act="relu")
+        pred = fluid.layers.fc(input=h, size=3, act="softmax")
+    exe = fluid.Executor(fluid.CPUPlace())
+    scope = core.Scope()
+    x = np.random.RandomState(1).rand(4, 1, 12, 12).astype("float32")
+    with fluid.executor.scope_guard(scope):
+        exe.run(startup)
+        # give BN non-trivial statistics
+        for n in list(scope.local_var_names()) if hasattr(scope, "local_var_names") else []:
+            pass
+        for v in main.global_block().vars.values():
+            if v.persistable and ("mean" in v.name or "variance" in v.name):
+                t = scope.find_var(v.name).get()
+                t.set_tensor(torch.rand_like(t.tensor) + 0.5)
+        test_prog = main.clone(for_test=True)
+        (ref,) = exe.run(test_prog, feed={"img": x}, fetch_list=[pred])
+        fluid.io.save_inference_model(d, ["img"], [pred], exe, main_program=main)
+    return x, ref
+
+
+def test_native_and_analysis_predictor_match_executor(tmp_path):
+    d = str(tmp_path / "model")
+    x, ref = _save_conv_model(d)
+    nat = inference.create_paddle_predictor(inference.NativeConfig(model_dir=d, use_gpu=False))
+    (o1,) = nat.run([inference.PaddleTensor(x, name="img")])
+    np.testing.assert_allclose(o1.as_ndarray(), ref, rtol=1e-5, atol=1e-6)
+
+    cfg = inference.AnalysisConfig(model_dir=d, use_gpu=False)
+    ana = inference.create_paddle_predictor(cfg)
+    types = [op.type for op in ana.program.global_block().ops]
+    assert "batch_norm" not in types and "fc" in types, types
+    assert ana.pass_stats.get("conv_bn_fuse_count") == 1
+    (o2,) = ana.run([inference.PaddleTensor(x, name="img")])
+    np.testing.assert_allclose(o2.as_ndarray(), ref, rtol=1e-4, atol=1e-5)
+
+    # Clone shares parameters; reference spelling Run(inputs, outputs)
+    c = ana.clone()
+    outs = []
+    assert c.Run([inference.PaddleTensor(x)], outs)
+    np.testing.assert_allclose(outs[0].as_ndarray(), ref, rtol=1e-4, atol=1e-5)
+    assert c.root_scope is ana.root_scope
+
+
+def test_analysis_predictor_bf16(tmp_path):
+    d = str(tmp_path / "model")
+    x, ref = _save_conv_model(d)
+    cfg = inference.AnalysisConfig(model_dir=d, use_gpu=False)
+    cfg.enable_bf16()
+    p = inference.create_paddle_predictor(cfg)
+    (o,) = p.run([inference.PaddleTensor(x)])
+    np.testing.assert_allclose(o.as_ndarray(), ref, rtol=5e-2, atol=2e-2)
