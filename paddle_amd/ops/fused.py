@@ -460,6 +460,38 @@ def embedding(ids, weight, padding_idx=None):
     return torch.nn.functional.embedding(ids.long(), weight, padding_idx=padding_idx)
 
 
+# ====================================================================== transpose
+
+
+def transpose2d(x):
+    """out = x.T (contiguous) for a 2-D (or batched 3-D: last two dims) tensor.
+    bf16/fp16 on the GPU run the LDS-tiled HIP kernel (csrc/kernels/transpose.hip)."""
+    if x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and x.shape[-1] % 8 == 0 \
+            and x.shape[-2] % 8 == 0 and x.stride(-1) == 1 and x.stride(-2) % 8 == 0:
+        R, C = x.shape[-2], x.shape[-1]
+        if x.dim() == 2:
+            out = torch.empty(C, R, device=x.device, dtype=x.dtype)
+            N.call("pa_transpose2d", 1, N.ptr(x), N.ptr(out), R, C, x.stride(0), R, 1, 0, 0, N.stream())
+            return out
+        if x.dim() == 3 and (x.stride(0) % 8 == 0):
+            out = torch.empty(x.shape[0], C, R, device=x.device, dtype=x.dtype)
+            N.call("pa_transpose2d", 1, N.ptr(x), N.ptr(out), R, C, x.stride(1), R, x.shape[0], x.stride(0),
+                   R * C, N.stream())
+            return out
+    return x.transpose(-1, -2).contiguous()
+
+
+# dW = X^T dY through the K-inner ("NT") GEMM form on transposed copies; see
+# csrc/kernels/transpose.hip for why.  Off on CPU (no effect on numerics).
+_DW_VIA_TRANSPOSE = True
+
+
+def _dw_nt_ok(x2, dy2):
+    return (_DW_VIA_TRANSPOSE and x2.is_cuda and x2.dtype == torch.bfloat16 and dy2.dtype == torch.bfloat16
+            and x2.shape[0] % 8 == 0 and x2.shape[1] % 8 == 0 and dy2.shape[1] % 8 == 0
+            and x2.shape[0] >= 1024)
+
+
 # ====================================================================== linear
 
 
@@ -491,11 +523,15 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
             mg = getattr(w, "_pa_main_grad", None)
+            if _dw_nt_ok(x2, dy2):
+                xa, dyb = transpose2d(_c(x2)), transpose2d(_c(dy2)).t()   # [K, T] @ [T, N], both T-inner
+            else:
+                xa, dyb = x2.t(), dy2
             if mg is not None:
                 # the engine's post-accumulate hook still fires for w (grad None)
-                mg.addmm_(x2.t(), dy2)
+                mg.addmm_(xa, dyb)
             else:
-                dw = torch.matmul(x2.t(), dy2)
+                dw = torch.matmul(xa, dyb)
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = dy2.sum(0).to(dy.dtype)
         return dx, dw, db

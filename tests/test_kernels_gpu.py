@@ -202,3 +202,31 @@ def test_adamw_flat():
         pr = pr - 1e-3 * (mr / (1 - 0.9 ** step)) / ((vr / (1 - 0.95 ** step)).sqrt() + 1e-8)
     assert _rel(p, pr) < 1e-5
     assert _rel(pb, pr) < 1e-2
+
+
+@pytest.mark.parametrize("R,C", [(64, 64), (128, 4096), (1000, 520), (16384, 4096), (72, 136)])
+def test_transpose2d(R, C):
+    x = torch.randn(R, C, device=dev, dtype=torch.bfloat16)
+    assert torch.equal(F.transpose2d(x), x.t().contiguous())
+    # strided rows (a view into a wider buffer) and batched 3-D
+    big = torch.randn(R, C + 16, device=dev, dtype=torch.bfloat16)
+    assert torch.equal(F.transpose2d(big[:, :C]), big[:, :C].t().contiguous())
+    b = torch.randn(3, R, C, device=dev, dtype=torch.bfloat16)
+    assert torch.equal(F.transpose2d(b), b.transpose(1, 2).contiguous())
+
+
+def test_linear_dw_via_transpose_matches_tn():
+    torch.manual_seed(0)
+    T, K, Nn = 2048, 512, 768
+    x = torch.randn(T, K, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(K, Nn, device=dev, dtype=torch.bfloat16) * 0.05).requires_grad_()
+    dy = torch.randn(T, Nn, device=dev, dtype=torch.bfloat16)
+    F.linear(x, w).backward(dy)
+    ref = (x.detach().float().t() @ dy.float())
+    assert _rel(w.grad, ref) < 1e-2
+    # accumulate-into-main-grad path
+    mg = torch.ones(K, Nn, device=dev, dtype=torch.bfloat16)
+    w2 = w.detach().clone().requires_grad_()
+    w2._pa_main_grad = mg
+    F.linear(x.detach(), w2).backward(dy)
+    assert _rel(mg, ref + 1) < 1e-2
