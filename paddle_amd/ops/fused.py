@@ -487,9 +487,36 @@ _DW_VIA_TRANSPOSE = True
 
 
 def _dw_nt_ok(x2, dy2):
+    # measured (benchmarks/dw_transpose.py, profiles/r1_dw_transpose.jsonl): the NT form
+    # saves more than the two transposes cost unless X is much wider than dY (down_proj)
     return (_DW_VIA_TRANSPOSE and x2.is_cuda and x2.dtype == torch.bfloat16 and dy2.dtype == torch.bfloat16
             and x2.shape[0] % 8 == 0 and x2.shape[1] % 8 == 0 and dy2.shape[1] % 8 == 0
-            and x2.shape[0] >= 1024)
+            and x2.shape[0] >= 1024 and x2.shape[1] <= dy2.shape[1])
+
+
+# Forward y = x W through the NT form as well: a transposed copy W^T of each weight
+# is kept next to it and refreshed lazily when the weight changes (optimizer steps
+# bump the epoch; plain in-place torch updates bump the tensor version).
+_FWD_VIA_WT = True
+_WEIGHT_EPOCH = [0]
+
+
+def bump_weight_epoch():
+    """Call after writing parameters through raw pointers (fused optimizers, all-gathers)."""
+    _WEIGHT_EPOCH[0] += 1
+
+
+def _weight_t(w, tokens):
+    if not (_FWD_VIA_WT and w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2 and tokens >= 1024
+            and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0):
+        return None
+    key = (_WEIGHT_EPOCH[0], w._version, w.data_ptr())
+    wt = getattr(w, "_pa_wt", None)
+    if wt is None or getattr(w, "_pa_wt_key", None) != key:
+        with torch.no_grad():
+            wt = transpose2d(w.detach())
+        w._pa_wt, w._pa_wt_key = wt, key
+    return wt
 
 
 # ====================================================================== linear
@@ -507,7 +534,8 @@ class _LinearFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b):
-        y = torch.matmul(x, w)
+        wt = _weight_t(w, x.numel() // max(x.shape[-1], 1))
+        y = torch.matmul(x, wt.t()) if wt is not None else torch.matmul(x, w)
         if b is not None:
             y = y + b
         ctx.save_for_backward(x, w)

@@ -9,6 +9,7 @@ from __future__ import annotations
 import torch
 
 from . import _native as N
+from . import fused as _fused
 
 
 def adamw_flat(param, grad, m, v, *, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0,
@@ -28,6 +29,7 @@ def adamw_flat(param, grad, m, v, *, lr, beta1=0.9, beta2=0.999, eps=1e-8, weigh
     bc1 = 1.0 - beta1 ** step
     bc2 = 1.0 - beta2 ** step
     if param.is_cuda:
+        _fused.bump_weight_epoch()
         N.call("pa_adamw", N.dt(grad), (N.dt(param_out) if param_out is not None else -1), N.ptr(param),
                N.ptr(grad), N.ptr(m), N.ptr(v), N.ptr(param_out), n, float(lr), N.ptr(lr_tensor),
                float(beta1), float(beta2), float(eps), float(weight_decay), float(bc1), float(bc2),
@@ -56,6 +58,7 @@ def momentum_flat(param, grad, velocity=None, *, lr, mu=0.9, nesterov=False, wei
                   grad_scale=1.0, lr_tensor=None):
     n = param.numel()
     if param.is_cuda:
+        _fused.bump_weight_epoch()
         N.call("pa_momentum", N.dt(grad), N.ptr(param), N.ptr(grad), N.ptr(velocity), n, float(lr),
                N.ptr(lr_tensor), float(mu), int(nesterov), float(weight_decay), float(grad_scale), N.stream())
         return param

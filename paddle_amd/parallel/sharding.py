@@ -28,6 +28,7 @@ import math
 
 import torch
 
+from ..ops import fused
 from ..ops import optim as fused_optim
 from . import comm
 
@@ -208,6 +209,7 @@ class FlatShardedOptimizer:
         if self.W > 1:
             for (bs, be, _), (s0, L, so) in zip(self.buckets, self.shard_slices):
                 comm.all_gather(self.flat_param[bs:be], self.param_shard[so:so + L], self.group)
+        fused.bump_weight_epoch()
 
     def zero_grad(self, set_to_none=False):
         self.flat_grad.zero_()
@@ -230,6 +232,7 @@ class FlatShardedOptimizer:
             if self.W > 1:
                 for (bs, be, _), (s0, L, so) in zip(self.buckets, self.shard_slices):
                     comm.all_gather(self.flat_param[bs:be], self.param_shard[so:so + L], self.group)
+        fused.bump_weight_epoch()
 
     def memory_bytes(self):
         es = self.flat_param.element_size()

@@ -230,3 +230,21 @@ def test_linear_dw_via_transpose_matches_tn():
     w2._pa_main_grad = mg
     F.linear(x.detach(), w2).backward(dy)
     assert _rel(mg, ref + 1) < 1e-2
+
+
+def test_linear_fwd_via_transposed_weight_tracks_updates():
+    torch.manual_seed(0)
+    x = torch.randn(2048, 512, device=dev, dtype=torch.bfloat16)
+    w = (torch.randn(512, 256, device=dev, dtype=torch.bfloat16) * 0.05).requires_grad_()
+    y1 = F.linear(x, w)
+    assert _rel(y1, x.float() @ w.detach().float()) < 1e-2
+    with torch.no_grad():
+        w.mul_(2.0)  # in-place update bumps the tensor version -> fresh W^T
+    assert _rel(F.linear(x, w), x.float() @ w.detach().float()) < 1e-2
+    # raw-pointer update (fused optimizer) + epoch bump
+    from paddle_amd.ops import optim
+    g = torch.ones_like(w)
+    m, v = torch.zeros_like(w, dtype=torch.float32), torch.zeros_like(w, dtype=torch.float32)
+    master = w.detach().float().clone()
+    optim.adamw_flat(master.view(-1), g.view(-1), m.view(-1), v.view(-1), lr=0.1, param_out=w.data.view(-1))
+    assert _rel(F.linear(x, w), x.float() @ w.detach().float()) < 1e-2
