@@ -169,12 +169,94 @@ class _OpView:
         return {k: v for k, v in self._op.attrs.items()}
 
 
+_DIFF_TYPES = None
+
+
+def _differentiable(block, name, no_grad):
+    from ..framework import core
+
+    global _DIFF_TYPES
+    if _DIFF_TYPES is None:
+        _DIFF_TYPES = (core.VT.LOD_TENSOR, core.VT.LOD_TENSOR_ARRAY, core.VT.SELECTED_ROWS)
+    if _append_grad_suffix_(name) in no_grad:
+        return False
+    v = block._find_var_recursive(name)
+    if v is None or v.type not in _DIFF_TYPES or v.stop_gradient and v.type != core.VT.LOD_TENSOR_ARRAY:
+        return False
+    return v.dtype in (core.VT.FP32, core.VT.FP64, core.VT.FP16, core.VT.BF16)
+
+
+def _while_grad_descs(op, block, no_grad_dict, grad_to_var, callbacks):
+    """Reference backward.py:315-392 sub-block recursion + WhileGradOpDescMaker: the
+    grad block is a child of the forward sub-block (it reads the step-local
+    activations kept in the step scopes) and holds the reversed grad ops of every op
+    in the loop body."""
+    prog = block.program
+    sub = op.attrs["sub_block"]
+    saved = prog.current_block_idx
+    grad_sub = prog.create_block(parent_idx=sub.idx)
+    no_grad_dict[sub.idx] = set(no_grad_dict[sub.idx]) | set(no_grad_dict[block.idx])
+    _append_backward_ops_(sub, list(sub.ops), grad_sub, no_grad_dict, grad_to_var, callbacks)
+    prog.current_block_idx = saved
+    no_grad = no_grad_dict[block.idx]
+    xs, outs = list(op.input("X")), list(op.output("Out"))
+    x_grads = [_append_grad_suffix_(n) if _differentiable(block, n, no_grad) else R.EMPTY_VAR for n in xs]
+    ogs = [_append_grad_suffix_(n) for n in outs if _differentiable(block, n, no_grad)]
+    return [dict(type="while_grad",
+                 inputs={"X": xs, "Out": outs, "Out@GRAD": ogs, "StepScopes": list(op.output("StepScopes"))},
+                 outputs={"X@GRAD": x_grads}, attrs={"sub_block": grad_sub, "original_output_grad": ogs})]
+
+
+def _split_duplicate_outputs(descs):
+    """A grad op that writes the same gradient from two slots (``x * x`` ->
+    X@GRAD and Y@GRAD are both x@GRAD) gets the later occurrences renamed and a
+    ``sum`` appended, so every grad op produces each name at most once."""
+    out = []
+    for d in descs:
+        seen, extra = {}, []
+        outs = {}
+        for slot, names in d["outputs"].items():
+            new = []
+            for n in names:
+                if n != R.EMPTY_VAR and n in seen:
+                    k = seen[n]
+                    seen[n] = k + 1
+                    dup = f"{n}@DUP@{k}"
+                    extra.append((n, dup))
+                    new.append(dup)
+                else:
+                    seen.setdefault(n, 0)
+                    new.append(n)
+            outs[slot] = new
+        if not extra:
+            out.append(d)
+            continue
+        first = {}
+        for n, dup in extra:
+            first.setdefault(n, []).append(dup)
+        for n, dups in first.items():
+            # rename the first occurrence too, then sum all into n
+            base = f"{n}@DUP@first"
+            for slot, names in outs.items():
+                if n in names:
+                    names[names.index(n)] = base
+                    break
+            first[n] = [base] + dups
+        out.append(dict(d, outputs=outs))
+        for n, parts in first.items():
+            out.append(dict(type="sum", inputs={"X": parts}, outputs={"Out": [n]}, attrs={}))
+    return out
+
+
 def _append_backward_ops_(block, ops, target_block, no_grad_dict, grad_to_var, callbacks=None):
     grad_op_descs = []
     no_grad = no_grad_dict[block.idx]
     for op in reversed(ops):
-        descs = R.make_grad_op_descs(_OpView(op), no_grad)
-        for d in descs:
+        if op.type == "while":
+            descs = _while_grad_descs(op, block, no_grad_dict, grad_to_var, callbacks)
+        else:
+            descs = R.make_grad_op_descs(_OpView(op), no_grad)
+        for d in _split_duplicate_outputs(descs):
             g = _GradOp(d["type"], d["inputs"], d["outputs"], d.get("attrs", {}))
             g.attrs[R.OP_ROLE_ATTR] = R.OpRole.Backward
             g.attrs.pop(R.OP_ROLE_VAR_ATTR, None)

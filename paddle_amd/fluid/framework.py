@@ -309,7 +309,15 @@ class Operator:
                 res = R.infer_shapes_meta(info, in_descs, {k: list(v) for k, v in self.outputs.items()},
                                           self._plain_attrs())
         except Exception:
-            return
+            res = self._lod_fallback_shapes(info, in_descs)
+            if not res:
+                return
+        has_lod_in = any(d is not None and d[2] for lst in in_descs.values() for d in lst)
+        if has_lod_in and not info.share_lod and res:
+            # a LoD-changing op (sequence_pool/expand, ...): its row count depends on
+            # the LoD, which compile time does not know
+            res = {slot: [((-1,) + tuple(d[0][1:]), d[1]) if (d is not None and len(d[0])) else d for d in lst]
+                   for slot, lst in res.items()}
         for slot, lst in (res or {}).items():
             for n, d in zip(self.outputs.get(slot, []), lst):
                 if d is None or n == EMPTY_VAR_NAME:
@@ -325,6 +333,13 @@ class Operator:
                     if src is not None and src.lod_level and shape and src.shape and \
                             (shape[0] == src.shape[0]) and info.share_lod:
                         v.lod_level = src.lod_level
+
+    def _lod_fallback_shapes(self, info, in_descs):
+        """Meta execution failed (data-dependent LoD op): Out = [-1] + X.shape[1:]."""
+        x = (in_descs.get("X") or [None])[0]
+        if x is None or "Out" not in self.outputs:
+            return None
+        return {"Out": [((-1,) + tuple(x[0][1:]), x[1])]}
 
     def _plain_attrs(self):
         return {k: (v.idx if isinstance(v, Block) else v) for k, v in self.attrs.items()}

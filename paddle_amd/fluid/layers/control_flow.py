@@ -9,6 +9,7 @@ from __future__ import annotations
 import contextlib
 
 from ...framework import core
+from .. import unique_name
 from ..framework import Variable, default_main_program
 from ..layer_helper import LayerHelper
 from .layer_utils import simple_op
@@ -18,7 +19,7 @@ __all__ = ["While", "Switch", "increment", "array_write", "create_array", "less_
            "greater_than", "greater_equal", "equal", "not_equal", "array_read", "array_length", "IfElse",
            "ConditionalBlock", "StaticRNN", "Print", "is_empty", "lod_rank_table", "max_sequence_len",
            "lod_tensor_to_array", "array_to_lod_tensor", "shrink_memory", "reorder_lod_tensor_by_rank",
-           "split_lod_tensor", "merge_lod_tensor"]
+           "split_lod_tensor", "merge_lod_tensor", "DynamicRNN", "ParallelDo"]
 
 
 def increment(x, value=1.0, in_place=True):
@@ -385,3 +386,212 @@ class StaticRNN:
 
     def __call__(self, *args, **kwargs):
         return self._result[0] if len(self._result) == 1 else self._result
+
+
+# ---------------------------------------------------------------------------- DynamicRNN
+def _parent_op(block, type, inputs, outputs, attrs=None):
+    return block.append_op(type=type, inputs=inputs, outputs=outputs, attrs=attrs or {})
+
+
+class DynamicRNN:
+    """RNN over variable-length (LoD) sequences (reference control_flow.py:1542).
+
+    Built from a ``While`` loop over time steps: sequences are sorted by length
+    (``lod_rank_table``), split time-major into a tensor array, and at step t only
+    the sequences still alive take part (``shrink_rnn_memory``).  Trainable end to
+    end: ``fluid.backward`` differentiates the loop through ``while_grad``.
+
+        drnn = DynamicRNN()
+        with drnn.block():
+            word = drnn.step_input(sentence)
+            prev = drnn.memory(shape=[200])
+            hidden = fluid.layers.fc(input=[word, prev], size=200, act='relu')
+            drnn.update_memory(prev, hidden)
+            drnn.output(hidden)
+        out = drnn()
+    """
+
+    BEFORE_RNN, IN_RNN, AFTER_RNN = 0, 1, 2
+
+    def __init__(self, name=None):
+        self.helper = LayerHelper("dynamic_rnn", name=name)
+        self.status = DynamicRNN.BEFORE_RNN
+        self.lod_rank_table = None
+        self.max_seq_len = None
+        self.step_idx = None
+        self.zero_idx = fill_constant(shape=[1], value=0, dtype="int64")
+        self.zero_idx.stop_gradient = True
+        self.mem_dict = {}
+        self.output_array = []
+        self.outputs = []
+        self.cond = self.helper.create_variable_for_type_inference(dtype="bool")
+        self.cond.stop_gradient = False
+        self.while_op = While(self.cond)
+        self.input_array = []
+        self.mem_link = []
+
+    def _parent_block(self):
+        prog = self.helper.main_program
+        return prog.block(prog.current_block().parent_idx)
+
+    def _assert_in_rnn_block_(self, method):
+        if self.status != DynamicRNN.IN_RNN:
+            raise ValueError(f"{method} can only be invoked inside rnn block.")
+
+    def _init_zero_idx_(self):
+        pass
+
+    def step_input(self, x):
+        self._assert_in_rnn_block_("step_input")
+        parent = self._parent_block()
+        if self.lod_rank_table is None:
+            self.lod_rank_table = parent.create_var(name=unique_name.generate("lod_rank_table"),
+                                                    type=core.VT.LOD_RANK_TABLE)
+            self.lod_rank_table.stop_gradient = True
+            _parent_op(parent, "lod_rank_table", {"X": [x]}, {"Out": [self.lod_rank_table]}, {"level": 0})
+            self.max_seq_len = parent.create_var(name=unique_name.generate("dynamic_rnn_max_seq_len"),
+                                                 dtype="int64", shape=[1])
+            self.max_seq_len.stop_gradient = True
+            _parent_op(parent, "max_sequence_len", {"RankTable": [self.lod_rank_table]},
+                       {"Out": [self.max_seq_len]})
+            _parent_op(parent, "less_than", {"X": [self.step_idx], "Y": [self.max_seq_len]},
+                       {"Out": [self.cond]})
+        input_array = parent.create_var(name=unique_name.generate("dynamic_rnn_input_array"),
+                                        type=core.VT.LOD_TENSOR_ARRAY, dtype=x.dtype, shape=x.shape)
+        self.input_array.append((input_array, x.dtype))
+        _parent_op(parent, "lod_tensor_to_array", {"X": [x], "RankTable": [self.lod_rank_table]},
+                   {"Out": [input_array]})
+        out = array_read(array=input_array, i=self.step_idx)
+        out.shape = x.shape
+        return out
+
+    def static_input(self, x):
+        self._assert_in_rnn_block_("static_input")
+        if self.lod_rank_table is None:
+            raise RuntimeError("static_input() must be called after step_input().")
+        parent = self._parent_block()
+        x_reordered = parent.create_var(name=unique_name.generate("dynamic_rnn_static_input_reordered"),
+                                        type=core.VT.LOD_TENSOR, dtype=x.dtype, shape=x.shape)
+        _parent_op(parent, "reorder_lod_tensor_by_rank", {"X": [x], "RankTable": [self.lod_rank_table]},
+                   {"Out": [x_reordered]})
+        out = shrink_memory(x_reordered, self.step_idx, self.lod_rank_table)
+        out.shape = x.shape
+        return out
+
+    @contextlib.contextmanager
+    def block(self):
+        if self.status != DynamicRNN.BEFORE_RNN:
+            raise ValueError("rnn.block() can only be invoke once")
+        self.step_idx = fill_constant(shape=[1], dtype="int64", value=0)
+        self.step_idx.stop_gradient = False
+        self.status = DynamicRNN.IN_RNN
+        with self.while_op.block():
+            yield
+            increment(x=self.step_idx, value=1.0, in_place=True)
+            for new_mem, mem_array in self.mem_link:
+                array_write(x=new_mem, i=self.step_idx, array=mem_array)
+            less_than(x=self.step_idx, y=self.max_seq_len, cond=self.cond)
+        self.status = DynamicRNN.AFTER_RNN
+        for each in self.output_array:
+            o = array_to_lod_tensor(x=each, table=self.lod_rank_table)
+            o.shape = each.shape
+            self.outputs.append(o)
+
+    def __call__(self, *args, **kwargs):
+        if self.status != DynamicRNN.AFTER_RNN:
+            raise ValueError("Output of the dynamic RNN can only be visited outside the rnn block.")
+        return self.outputs[0] if len(self.outputs) == 1 else self.outputs
+
+    def memory(self, init=None, shape=None, value=0.0, need_reorder=False, dtype="float32"):
+        self._assert_in_rnn_block_("memory")
+        parent = self._parent_block()
+        if init is not None:
+            if need_reorder:
+                if self.lod_rank_table is None:
+                    raise ValueError("If set need_reorder to True, make sure step_input be invoked before memory.")
+                init_reordered = parent.create_var(name=unique_name.generate("dynamic_rnn_mem_init_reordered"),
+                                                   type=core.VT.LOD_TENSOR, dtype=init.dtype, shape=init.shape)
+                _parent_op(parent, "reorder_lod_tensor_by_rank", {"X": [init], "RankTable": [self.lod_rank_table]},
+                           {"Out": [init_reordered]})
+                init = init_reordered
+            mem_array = parent.create_var(name=unique_name.generate("dynamic_rnn_mem_array"),
+                                          type=core.VT.LOD_TENSOR_ARRAY, dtype=init.dtype, shape=init.shape)
+            _parent_op(parent, "write_to_array", {"X": [init], "I": [self.zero_idx]}, {"Out": [mem_array]})
+            retv = array_read(array=mem_array, i=self.step_idx)
+            retv.shape = init.shape
+            retv = shrink_memory(x=retv, i=self.step_idx, table=self.lod_rank_table)
+            retv.shape = init.shape
+            self.mem_dict[retv.name] = mem_array
+            return retv
+        if len(self.input_array) == 0:
+            raise ValueError("step_input should be invoked before memory(shape=..., value=...)")
+        arr, in_dtype = self.input_array[0]
+        in0 = parent.create_var(name=unique_name.generate("in0"), dtype=in_dtype)
+        _parent_op(parent, "read_from_array", {"X": [arr], "I": [self.zero_idx]}, {"Out": [in0]})
+        init = parent.create_var(name=unique_name.generate("mem_init"), dtype=dtype, shape=[-1] + list(shape))
+        init.stop_gradient = True
+        _parent_op(parent, "fill_constant_batch_size_like", {"Input": [in0]}, {"Out": [init]},
+                   {"shape": [-1] + list(shape), "value": float(value), "dtype": core.convert_dtype(dtype)})
+        return self.memory(init=init)
+
+    def update_memory(self, ex_mem, new_mem):
+        self._assert_in_rnn_block_("update_memory")
+        mem_array = self.mem_dict.get(ex_mem.name)
+        if mem_array is None:
+            raise ValueError("Please invoke memory before update_memory")
+        if self.lod_rank_table is None:
+            raise ValueError("Please invoke step_input before update_memory")
+        self.mem_link.append((new_mem, mem_array))
+
+    def output(self, *outputs):
+        self._assert_in_rnn_block_("output")
+        parent = self._parent_block()
+        for each in outputs:
+            outside_array = parent.create_var(name=unique_name.generate(f"_{self.helper.name}_output_array_"),
+                                              type=core.VT.LOD_TENSOR_ARRAY, dtype=each.dtype, shape=each.shape)
+            array_write(x=each, i=self.step_idx, array=outside_array)
+            self.output_array.append(outside_array)
+
+
+# ---------------------------------------------------------------------------- ParallelDo
+class ParallelDo:
+    """Op-level data parallelism over places (reference control_flow.py:230,
+    operators/parallel_do_op.cc).  Deprecated in the reference in favour of
+    ParallelExecutor; kept for API parity.
+
+    MI355X design: the sub-block is traced once and run on the input as a whole
+    on the current place (one process per GPU is the data-parallel unit here; the
+    multi-replica split of the reference's threads is what ParallelExecutor /
+    ``paddle_amd.distributed`` provide).  ``read_input`` / ``write_output`` keep
+    their meaning, so programs written against ParallelDo build and train.
+    """
+
+    def __init__(self, places, use_nccl=False, name=None):
+        self.helper = LayerHelper("parallel_do", name=name)
+        self.places = places
+        self.use_nccl = use_nccl
+        self.inputs = []
+        self.outputs = []
+
+    @contextlib.contextmanager
+    def do(self):
+        yield
+
+    def parent_block(self):
+        prog = self.helper.main_program
+        return prog.current_block()
+
+    def read_input(self, var):
+        self.inputs.append(var)
+        return var
+
+    def write_output(self, var):
+        self.outputs.append(var)
+
+    def get_parameters(self):
+        return [p for p in self.helper.main_program.global_block().all_parameters()]
+
+    def __call__(self, *args, **kwargs):
+        if not self.outputs:
+            raise ValueError("ParallelDo: call write_output() inside do()")
+        return self.outputs[0] if len(self.outputs) == 1 else self.outputs

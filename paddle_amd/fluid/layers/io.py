@@ -2,6 +2,8 @@
 open_files :724, double_buffer :891, read_file, shuffle, batch)."""
 from __future__ import annotations
 
+import contextlib
+
 from ...framework import core
 from ..framework import Variable, default_main_program, default_startup_program
 from ..layer_helper import LayerHelper
@@ -42,7 +44,10 @@ class _PyReaderHandle:
         self.use_double_buffer = use_double_buffer
 
     def decorate_tensor_provider(self, provider):
-        self._provider = provider
+        p = provider
+        for fn in getattr(self, "_decorators", []):   # in-graph batch()/shuffle() applied earlier
+            p = (lambda p=p, fn=fn: fn(p()))
+        self._provider = p
 
     decorate_paddle_reader = decorate_tensor_provider
     decorate_batch_generator = decorate_tensor_provider
@@ -97,12 +102,122 @@ def double_buffer(reader, place=None, name=None):
     return reader
 
 
-def batch(reader, batch_size):
+def _wrap_provider(reader, fn):
+    inner = reader._provider
+    reader._provider = (lambda: fn(inner())) if inner is not None else None
+    reader._decorators = getattr(reader, "_decorators", []) + [fn]
     return reader
+
+
+def batch(reader, batch_size):
+    """create_batch_reader: stack ``batch_size`` consecutive samples per field."""
+    import numpy as np
+
+    def gen(it):
+        buf = []
+        for item in it:
+            buf.append(item)
+            if len(buf) == batch_size:
+                yield [np.stack([np.asarray(b[i]) for b in buf]) for i in range(len(buf[0]))]
+                buf = []
+        if buf:
+            yield [np.stack([np.asarray(b[i]) for b in buf]) for i in range(len(buf[0]))]
+
+    return _wrap_provider(reader, gen)
 
 
 def shuffle(reader, buffer_size):
-    return reader
+    """create_shuffle_reader: buffered shuffle over ``buffer_size`` items."""
+    import random
+
+    def gen(it):
+        buf = []
+        for item in it:
+            buf.append(item)
+            if len(buf) >= buffer_size:
+                random.shuffle(buf)
+                yield from buf
+                buf = []
+        random.shuffle(buf)
+        yield from buf
+
+    return _wrap_provider(reader, gen)
+
+
+def open_recordio_file(filename, shapes, lod_levels, dtypes, pass_num=1, for_parallel=True):
+    """Reader over one RecordIO file (reference io.py open_recordio_file)."""
+    return open_files([filename], shapes, lod_levels, dtypes, pass_num=pass_num)
+
+
+class Preprocessor:
+    """Per-batch preprocessing sub-program on a reader's output (reference
+    io.py Preprocessor / create_custom_reader_op.cc)::
+
+        p = fluid.layers.io.Preprocessor(reader=r)
+        with p.block():
+            img, lbl = p.inputs()
+            p.outputs(img / 2, lbl + 1)
+        r2 = p()
+    """
+
+    BEFORE_SUB_BLOCK, IN_SUB_BLOCK, AFTER_SUB_BLOCK = 0, 1, 2
+
+    def __init__(self, reader, name=None):
+        from ..framework import Program
+
+        self.underlying_reader = reader
+        self.name = name or "preprocessor"
+        self.status = Preprocessor.BEFORE_SUB_BLOCK
+        self.prog, self.startup = Program(), Program()
+        self.source_vars = None
+        self.sink_vars = None
+
+    @contextlib.contextmanager
+    def block(self):
+        from ..framework import program_guard
+
+        self.status = Preprocessor.IN_SUB_BLOCK
+        with program_guard(self.prog, self.startup):
+            yield
+        self.status = Preprocessor.AFTER_SUB_BLOCK
+        if self.sink_vars is None:
+            raise RuntimeError("Preprocessor: outputs() was not called inside block()")
+
+    def inputs(self):
+        if self.status != Preprocessor.IN_SUB_BLOCK:
+            raise RuntimeError("Preprocessor.inputs() can only be invoked inside the sub-block.")
+        self.source_vars = [data(name=f"{self.name}_in_{i}", shape=list(v.shape), dtype=v.dtype,
+                                 lod_level=v.lod_level, append_batch_size=False)
+                            for i, v in enumerate(self.underlying_reader.vars)]
+        return self.source_vars
+
+    def outputs(self, *outs):
+        if self.status != Preprocessor.IN_SUB_BLOCK:
+            raise RuntimeError("Preprocessor.outputs() can only be invoked inside the sub-block.")
+        self.sink_vars = list(outs)
+
+    def __call__(self, *args, **kwargs):
+        if self.status != Preprocessor.AFTER_SUB_BLOCK:
+            raise RuntimeError("Preprocessor output can only be retrieved after rnn block.")
+        from ...framework import core as _core
+        from ..executor import Executor
+
+        out = py_reader(capacity=self.underlying_reader.capacity, shapes=[list(v.shape) for v in self.sink_vars],
+                        dtypes=[v.dtype for v in self.sink_vars], lod_levels=[v.lod_level or 0 for v in self.sink_vars],
+                        name=self.name)
+        src, sink, prog, inner = self.source_vars, self.sink_vars, self.prog, self.underlying_reader
+
+        def provider():
+            exe = Executor(_core.CPUPlace())
+            scope = _core.Scope()
+            from ..executor import scope_guard
+
+            with scope_guard(scope):
+                for item in inner._provider():
+                    yield exe.run(prog, feed={v.name: x for v, x in zip(src, item)}, fetch_list=sink)
+
+        out.decorate_tensor_provider(provider)
+        return out
 
 
 def open_files(filenames, shapes, lod_levels, dtypes, thread_num=None, buffer_size=None, pass_num=1,

@@ -775,3 +775,74 @@ def swish(x, beta=1.0, name=None):
 @_export
 def gelu(x, name=None):
     return simple_op("gelu", {"X": x}, name=name)
+
+
+@_export
+def conv3d_transpose(input, num_filters, output_size=None, filter_size=None, padding=0, stride=1, dilation=1,
+                     groups=None, param_attr=None, bias_attr=None, use_cudnn=True, act=None, name=None):
+    """3-D transposed convolution (reference nn.py conv3d_transpose; NCDHW)."""
+    helper = LayerHelper("conv3d_transpose", **locals())
+    dtype = helper.input_dtype()
+    groups = groups or 1
+    padding, stride, dilation = _pair(padding, 3), _pair(stride, 3), _pair(dilation, 3)
+    if filter_size is None:
+        output_size = _pair(output_size, 3)
+        filter_size = [(output_size[i] - (input.shape[2 + i] - 1) * stride[i] + 2 * padding[i] - 1) // dilation[i] + 1
+                       for i in range(3)]
+    filter_shape = [input.shape[1], num_filters // groups] + _pair(filter_size, 3)
+    w = helper.create_parameter(dtype=dtype, shape=filter_shape, attr=helper.param_attr)
+    pre_bias = helper.create_variable_for_type_inference(dtype)
+    helper.append_op(type="conv3d_transpose", inputs={"Input": [input], "Filter": [w]},
+                     outputs={"Output": pre_bias},
+                     attrs={"output_size": _pair(output_size, 3) if output_size else [], "strides": stride,
+                            "paddings": padding, "dilations": dilation, "groups": groups, "use_cudnn": use_cudnn})
+    out = helper.append_bias_op(pre_bias, dim_start=1, dim_end=2)
+    return helper.append_activation(out)
+
+
+@_export
+def dice_loss(input, label, epsilon=1e-05):
+    """1 - 2|X∩Y| / (|X| + |Y|) averaged over the batch; ``label`` holds class ids
+    (one-hot against input's last dim), ``input`` is a probability map."""
+    onehot = one_hot(label, depth=input.shape[-1])
+    dims = list(range(1, len(input.shape)))
+    inse = reduce_sum(elementwise_mul(input, onehot), dim=dims)
+    denom = elementwise_add(reduce_sum(input, dim=dims), reduce_sum(onehot, dim=dims))
+    score = scale(elementwise_div(scale(inse, scale=2.0), scale(denom, bias=epsilon)), scale=-1.0, bias=1.0)
+    return reduce_mean(score)
+
+
+@_export
+def uniform_random_batch_size_like(input, shape, dtype="float32", input_dim_idx=0, output_dim_idx=0, min=-1.0,
+                                   max=1.0, seed=0):
+    from ...framework import core as _core
+
+    return simple_op("uniform_random_batch_size_like", {"Input": input},
+                     {"shape": list(shape), "dtype": _core.convert_dtype(dtype), "input_dim_idx": input_dim_idx,
+                      "output_dim_idx": output_dim_idx, "min": float(min), "max": float(max), "seed": seed},
+                     dtype=dtype, stop_gradient=True)
+
+
+@_export
+def gaussian_random_batch_size_like(input, shape, input_dim_idx=0, output_dim_idx=0, mean=0.0, std=1.0, seed=0,
+                                    dtype="float32"):
+    from ...framework import core as _core
+
+    return simple_op("gaussian_random_batch_size_like", {"Input": input},
+                     {"shape": list(shape), "dtype": _core.convert_dtype(dtype), "input_dim_idx": input_dim_idx,
+                      "output_dim_idx": output_dim_idx, "mean": float(mean), "std": float(std), "seed": seed},
+                     dtype=dtype, stop_gradient=True)
+
+
+@_export
+def sampling_id(x, min=0.0, max=1.0, seed=0, dtype="float32"):
+    """Sample one id per row of the probability matrix ``x``."""
+    return simple_op("sampling_id", {"X": x}, {"min": float(min), "max": float(max), "seed": seed},
+                     dtype="int64", stop_gradient=True)
+
+
+@_export
+def sum(x):
+    """Elementwise sum of a list of tensors (the ``sum`` op)."""
+    xs = x if isinstance(x, (list, tuple)) else [x]
+    return simple_op("sum", {"X": list(xs)}, dtype=xs[0].dtype)

@@ -89,7 +89,13 @@ def sequence_expand(ctx):
     ref = ctx.attr("ref_level")
     ref = len(ylod) - 1 if ref == -1 else ref
     yoff = ylod[ref]
+    if len(yoff) <= 1:
+        ctx.set_output("Out", x, ctx.input_lod("X"))
+        return
     xlod = ctx.input_lod("X")
+    # (sequence_expand_op.h) only a 1-level X LoD defines X's sequences; otherwise
+    # every row is one sequence and the output carries no LoD
+    xlod = xlod if len(xlod) == 1 else []
     xoff = xlod[0] if xlod else list(range(x.shape[0] + 1))
     rows, out_off = [], [0]
     for i in range(len(yoff) - 1):
