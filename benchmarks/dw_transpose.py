@@ -36,7 +36,7 @@ def main():
     T = 16384
     shapes = {"qkv": (4096, 12288), "o": (4096, 4096), "gate_up": (4096, 22016), "down": (11008, 4096),
               "lm_head": (4096, 32000)}
-    tot = {"tn": 0.0, "tr_nt": 0.0, "fwd_nn": 0.0, "fwd_nt": 0.0}
+    tot = {"tn": 0.0, "tr_nt": 0.0, "trx_nn": 0.0, "fwd_nn": 0.0, "fwd_nt": 0.0}
     for name, (K, N) in shapes.items():
         x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
         dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
@@ -48,6 +48,8 @@ def main():
         r["dw_tr_nt_ms"] = timeit(lambda: g.addmm_(F.transpose2d(x), F.transpose2d(dy).t()))
         xt, dyt = F.transpose2d(x), F.transpose2d(dy)
         r["dw_nt_only_ms"] = timeit(lambda: g.addmm_(xt, dyt.t()))
+        r["dw_trx_nn_ms"] = timeit(lambda: g.addmm_(F.transpose2d(x), dy))
+        r["dw_nn_only_ms"] = timeit(lambda: g.addmm_(xt, dy))
         r["tr_x_ms"] = timeit(lambda: F.transpose2d(x))
         r["tr_x_torch_ms"] = timeit(lambda: x.t().contiguous())
         r["tr_x_TBps"] = 2 * x.numel() * 2 / r["tr_x_ms"] / 1e9
@@ -59,6 +61,7 @@ def main():
         r["transpose_exact"] = bool(ok)
         tot["tn"] += r["dw_tn_ms"]
         tot["tr_nt"] += r["dw_tr_nt_ms"]
+        tot["trx_nn"] += r["dw_trx_nn_ms"]
         tot["fwd_nn"] += r["fwd_nn_ms"]
         tot["fwd_nt"] += r["fwd_nt_ms"]
         print(json.dumps({"shape": name, "K": K, "N": N, **r}), flush=True)

@@ -13,7 +13,7 @@ import torch.multiprocessing as mp
 from paddle_amd.models.llama import LLAMA_CONFIGS, LlamaConfig, LlamaForCausalLM
 from paddle_amd.parallel.sharding import FlatShardedOptimizer
 
-from dist_util import assert_adam_close
+from dist_util import assert_adam_close, run_dist
 
 
 def _cfg():
@@ -39,12 +39,7 @@ def _train_single(steps):
     return losses, torch.cat([p.detach().reshape(-1) for p in m.parameters()])
 
 
-def _worker(rank, world, port, steps, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
-    import torch.distributed as dist
-
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, steps):
     torch.manual_seed(0)
     m = LlamaForCausalLM(_cfg(), device="cpu")
     opt = FlatShardedOptimizer(m.named_parameters(), lr=1e-3, grad_clip=1.0, bucket_mb=1)
@@ -57,11 +52,9 @@ def _worker(rank, world, port, steps, q):
         opt.step()
         opt.zero_grad()
         t = torch.tensor([loss.item()])
-        dist.all_reduce(t)
+        torch.distributed.all_reduce(t)
         losses.append(t.item() / world)
-    if rank == 0:
-        q.put((losses, torch.cat([p.detach().reshape(-1) for p in m.parameters()])))
-    dist.destroy_process_group()
+    return losses, torch.cat([p.detach().reshape(-1) for p in m.parameters()])
 
 
 def _free_port():
@@ -80,16 +73,7 @@ def test_tiny_llama_cpu_converges():
 def test_sharded_dp_matches_single_process():
     steps = 4
     ref_losses, ref_params = _train_single(steps)
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, steps, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    losses, params = q.get(timeout=300)
-    for p in procs:
-        p.join(60)
-    assert all(p.exitcode == 0 for p in procs)
+    losses, params = run_dist(_worker, 2, steps)[0]
     for a, b in zip(losses, ref_losses):
         assert abs(a - b) < 1e-4, (losses, ref_losses)
     assert_adam_close(params, ref_params, atol=1e-5, rtol=1e-4, lr=1e-3, steps=steps)
