@@ -552,7 +552,9 @@ class _LinearFn(torch.autograd.Function):
             x2 = x.reshape(-1, x.shape[-1])
             mg = getattr(w, "_pa_main_grad", None)
             if _dw_nt_ok(x2, dy2):
-                xa, dyb = transpose2d(_c(x2)), transpose2d(_c(dy2)).t()   # [K, T] @ [T, N], both T-inner
+                # X^T materialised token-inner, dY as is: the "NN" form, which measured
+                # faster than both TN and (X^T, dY^T) NT once the dY transpose is paid
+                xa, dyb = transpose2d(_c(x2)), dy2
             else:
                 xa, dyb = x2.t(), dy2
             if mg is not None:
