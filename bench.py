@@ -41,7 +41,8 @@ def main():
     ap.add_argument("--model", default="llama-7b")
     ap.add_argument("--seq-len", type=int, default=2048)
     ap.add_argument("--micro-batch", type=int, default=8)
-    ap.add_argument("--accum", type=int, default=1)
+    ap.add_argument("--accum", type=int, default=2,
+                    help="gradient accumulation micro-steps per optimizer step (Fleet accumulate_steps)")
     ap.add_argument("--layers", type=int, default=None, help="debug only: override layer count (result INVALID)")
     ap.add_argument("--recompute", action="store_true")
     ap.add_argument("--bucket-mb", type=int, default=256)
