@@ -11,6 +11,8 @@ from ..framework.core import (CPUPlace, CUDAPinnedPlace, CUDAPlace, LoDTensor, L
 from . import (backward, clip, data_feeder, executor, framework, initializer, io, layers, nets,  # noqa: F401
                optimizer, param_attr, profiler, regularizer, unique_name)
 from .backward import append_backward, calc_gradient, gradients  # noqa: F401
+from . import concurrency  # noqa: F401,E402
+from .concurrency import Go, Select, channel_close, channel_recv, channel_send, make_channel  # noqa: F401,E402
 from .data_feeder import DataFeeder  # noqa: F401
 from .executor import Executor, global_scope, scope_guard  # noqa: F401
 from .framework import (Operator, Parameter, Program, Variable, default_main_program,  # noqa: F401
