@@ -31,6 +31,8 @@ def _parse(argv):
     ap.add_argument("--master_addr", "--ips", type=str, default="127.0.0.1")
     ap.add_argument("--master_port", "--started_port", type=int, default=29500)
     ap.add_argument("--log_dir", type=str, default=None)
+    ap.add_argument("--max_restarts", type=int, default=0,
+                    help="restart the whole process group up to N times after a failure (elastic)")
     ap.add_argument("script")
     ap.add_argument("script_args", nargs=argparse.REMAINDER)
     return ap.parse_args(argv)
@@ -63,17 +65,14 @@ def child_envs(nproc, nnodes=1, node_rank=0, master_addr="127.0.0.1", master_por
     return envs
 
 
-def launch(argv=None):
-    a = _parse(argv if argv is not None else sys.argv[1:])
-    gpus = [int(x) for x in a.gpus.split(",")] if a.gpus else None
-    nproc = a.nproc_per_node or (len(gpus) if gpus else _count_gpus())
-    envs = child_envs(nproc, a.nnodes, a.node_rank, a.master_addr, a.master_port, gpus)
+def _run_group(a, envs, attempt):
     procs = []
     for i, e in enumerate(envs):
+        e = dict(e, PADDLE_RESTART_COUNT=str(attempt))
         out = None
         if a.log_dir:
             os.makedirs(a.log_dir, exist_ok=True)
-            out = open(os.path.join(a.log_dir, f"workerlog.{i}"), "w")
+            out = open(os.path.join(a.log_dir, f"workerlog.{i}" + (f".restart{attempt}" if attempt else "")), "w")
         procs.append(subprocess.Popen([sys.executable, "-u", a.script] + a.script_args, env=e,
                                       stdout=out, stderr=subprocess.STDOUT if out else None))
     rc = 0
@@ -87,13 +86,37 @@ def launch(argv=None):
                 alive.remove(p)
                 if r != 0 and rc == 0:
                     rc = r
+                    # one rank died: the survivors would block in their next collective
                     for q in alive:
                         q.send_signal(signal.SIGTERM)
+                    deadline = time.time() + 15
+                    for q in alive:
+                        try:
+                            q.wait(max(0.1, deadline - time.time()))
+                        except subprocess.TimeoutExpired:
+                            q.kill()
             time.sleep(0.2)
     except KeyboardInterrupt:
         for p in procs:
             p.send_signal(signal.SIGTERM)
-        rc = 130
+        return 130, True
+    return rc, False
+
+
+def launch(argv=None):
+    a = _parse(argv if argv is not None else sys.argv[1:])
+    gpus = [int(x) for x in a.gpus.split(",")] if a.gpus else None
+    nproc = a.nproc_per_node or (len(gpus) if gpus else _count_gpus())
+    rc = 0
+    for attempt in range(a.max_restarts + 1):
+        # a fresh rendezvous port per attempt (the old one may sit in TIME_WAIT)
+        envs = child_envs(nproc, a.nnodes, a.node_rank, a.master_addr, a.master_port + 17 * attempt, gpus)
+        rc, interrupted = _run_group(a, envs, attempt)
+        if rc == 0 or interrupted:
+            return rc
+        sys.stderr.write(f"[launch] process group failed (rc={rc}); "
+                         f"{'restarting' if attempt < a.max_restarts else 'giving up'} "
+                         f"({attempt + 1}/{a.max_restarts + 1})\n")
     return rc
 
 
