@@ -141,3 +141,21 @@ def test_analysis_predictor_bf16(tmp_path):
     p = inference.create_paddle_predictor(cfg)
     (o,) = p.run([inference.PaddleTensor(x)])
     np.testing.assert_allclose(o.as_ndarray(), ref, rtol=5e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("which", ["BF16Transpiler", "Float16Transpiler"])
+def test_reduced_precision_transpiler(tmp_path, which):
+    from paddle_amd.fluid import transpiler
+
+    d = str(tmp_path / "model")
+    x, ref = _save_conv_model(d)
+    exe = fluid.Executor(fluid.CPUPlace())
+    scope = core.Scope()
+    with fluid.executor.scope_guard(scope):
+        prog, feeds, fetches = fluid.io.load_inference_model(d, exe)
+        getattr(transpiler, which)().transpile(prog, fluid.CPUPlace(), scope)
+        types = [op.type for op in prog.global_block().ops]
+        assert types.count("cast") == 2, types
+        (out,) = exe.run(prog, feed={feeds[0]: x}, fetch_list=fetches)
+    assert out.dtype == np.float32
+    np.testing.assert_allclose(out, ref, rtol=5e-2, atol=2e-2)
