@@ -16,6 +16,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -207,7 +208,8 @@ struct ThreadBuf {
 std::atomic<bool> g_prof_on{false};
 std::mutex g_prof_mu;
 std::vector<std::string> g_names;
-std::vector<ThreadBuf*> g_bufs;
+// owned here (freed at exit); a thread keeps a raw pointer to its own buffer
+std::vector<std::unique_ptr<ThreadBuf>> g_bufs;
 thread_local ThreadBuf* t_buf = nullptr;
 uint64_t now_ns() {
   return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -225,7 +227,7 @@ ThreadBuf* buf() {
     t_buf = new ThreadBuf();
     t_buf->tid = std::hash<std::thread::id>()(std::this_thread::get_id());
     std::lock_guard<std::mutex> l(g_prof_mu);
-    g_bufs.push_back(t_buf);
+    g_bufs.emplace_back(t_buf);
   }
   return t_buf;
 }
@@ -249,7 +251,7 @@ PA_RT_EXPORT void pa_prof_pop() {
 
 PA_RT_EXPORT void pa_prof_reset() {
   std::lock_guard<std::mutex> l(g_prof_mu);
-  for (auto* b : g_bufs) {
+  for (auto& b : g_bufs) {
     b->done.clear();
     b->stack.clear();
   }
@@ -262,7 +264,7 @@ PA_RT_EXPORT long pa_prof_dump(const char* path) {
   if (!f) return -1;
   fprintf(f, "{\"traceEvents\":[");
   long n = 0;
-  for (auto* b : g_bufs)
+  for (auto& b : g_bufs)
     for (auto& e : b->done) {
       fprintf(f, "%s{\"name\":\"%s\",\"ph\":\"X\",\"pid\":0,\"tid\":%llu,\"ts\":%.3f,\"dur\":%.3f}", n ? "," : "",
               g_names[e.name].c_str(), (unsigned long long)(e.tid % 1000000), e.t0 / 1e3, (e.t1 - e.t0) / 1e3);
