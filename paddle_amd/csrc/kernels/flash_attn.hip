@@ -742,7 +742,253 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel2(BwdParams p) {
   }
 }
 
-// 0 = fa_bwd_kernel, 1 = pipelined (default), 2 = probe without dQ atomics (wrong dQ)
+// ---------------------------------------------------------------------------------
+// Backward v3: 8 waves x 16 keys (128 keys per workgroup), MFMA 16x16x32, TWO waves
+// per SIMD.  v2 (fa_bwd_kernel2) keeps 32 keys x D=128 dK/dV accumulators per wave
+// (128 regs) plus K/V operand registers -> 365 VGPR+AGPR, one wave per SIMD, and its
+// per-tile chain (S/dP MFMAs -> exp -> dV/dK -> dS -> barrier -> dQ -> atomics) runs
+// with nothing to overlap it (~13 % MFMA busy).  Here a wave owns 16 keys:
+//   * S = Q K^T and dP = dO V^T with queries on the MFMA rows and the wave's keys on
+//     the lanes: Q/dO rows are b128 LDS reads, K/V^T fragments stay in 32 registers;
+//   * the S/dP accumulators (q = 16qt + 4g + i on registers, key on lane) ARE the A
+//     operands of dV = P^T dO and dK = dS^T Q once the 32-query k-slots are permuted
+//     (slot (g, j) <-> q = 4g + j for j < 4, 16 + 4g + j - 4 otherwise); the dO / Q
+//     B fragments come from two ds_read_b64_tr_b16 of the same permuted rows;
+//   * dS goes to LDS as [key][q] (two ds_write_b64 per lane) and dQ (32 q x 16 d per
+//     wave) reads it back transposed, K from the dual-use image; fp32 atomics on dQ
+//     are deferred by one tile as in v2.
+// Accumulators: dK/dV 64 regs, S/dP 16, dQ 2x8 -> fits 256 VGPRs (2 waves / SIMD).
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x4 mfma16(bf16x8v a, bf16x8v b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
+  constexpr int D = 128, BK = 128, BQ = 32;
+  constexpr int KCH = D / 8;                     // 16-B chunks per 128-d row
+  constexpr int K_BYTES = BK * D * 2;            // 32 KB  K image (dual layout)
+  constexpr int Q_BYTES = BQ * D * 2;            // 8 KB
+  constexpr int DS_BYTES = BK * BQ * 2;          // 8 KB   dS^T [key][q]
+  constexpr int STAGE = 2 * Q_BYTES + DS_BYTES + 2 * BQ * 4;
+  __shared__ __attribute__((aligned(16))) char smem[K_BYTES + 2 * STAGE];
+  char* Ks = smem;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;       // MFMA16 lane row / lane group
+  const int gq = li >> 2, gp = li & 3;           // tr-read block row / column quad
+  const int h = blockIdx.x, b = blockIdx.y, kt = blockIdx.z;
+  const int kvh = h / (p.Hq / p.Hkv);
+  const long n0 = (long)kt * BK;
+  const long offs = CAUSAL ? (long)p.Sk - p.Sq : 0;
+
+  const u16* qp = p.q + (long)b * p.q_bs + (long)h * p.q_hs;
+  const u16* dop = p.dout + (long)b * p.do_bs + (long)h * p.do_hs;
+  const u16* kp = p.k + (long)b * p.k_bs + (long)kvh * p.k_hs;
+  const u16* vp = p.v + (long)b * p.v_bs + (long)kvh * p.v_hs;
+  const float* lsep = p.lse + ((long)b * p.Hq + h) * p.Sq;
+  const float* dlp = p.delta + ((long)b * p.Hq + h) * p.Sq;
+  float* dqp = p.dq_acc + (long)b * p.Sq * p.Hq * D + (long)h * D;
+
+  long qstart = 0;
+  if (CAUSAL) qstart = max(0L, n0 - offs);
+  qstart = (qstart / BQ) * BQ;
+
+  const auto q_rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)qp, 0, (int)(unsigned)(((long)(p.Sq - 1) * p.q_ss + D) * 2), 0x00020000);
+  const auto do_rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)dop, 0, (int)(unsigned)(((long)(p.Sq - 1) * p.do_ss + D) * 2), 0x00020000);
+  const auto lse_rs = __builtin_amdgcn_make_buffer_rsrc((void*)lsep, 0, p.Sq * 4, 0x00020000);
+  const auto dl_rs = __builtin_amdgcn_make_buffer_rsrc((void*)dlp, 0, p.Sq * 4, 0x00020000);
+  const long dq_rstride = (long)p.Hq * D;
+  const auto dq_rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)dqp, 0, (int)(unsigned)(((long)(p.Sq - 1) * dq_rstride + D) * 4), 0x00020000);
+
+  // one 16-B chunk of Q and of dO per thread per tile (32 rows x 16 chunks = 512)
+  const int srow = tid / KCH, sch = tid % KCH;
+  const unsigned qoff = (unsigned)(srow * p.q_ss * 2 + sch * 16);
+  const unsigned ooff = (unsigned)(srow * p.do_ss * 2 + sch * 16);
+  u16x8 qst, ost;
+  float lst = 0.f, dst = 0.f;
+  auto load_regs = [&](long qt0) {
+    qst = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                        q_rs, (int)((unsigned)(qt0 * p.q_ss * 2) + qoff), 0, 0));
+    ost = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                        do_rs, (int)((unsigned)(qt0 * p.do_ss * 2) + ooff), 0, 0));
+    const int lo = (int)(qt0 + (tid & (BQ - 1))) * 4;
+    lst = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lse_rs, lo, 0, 0));
+    dst = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dl_rs, lo, 0, 0));
+  };
+  auto store_lds = [&](int buf) {
+    char* st = smem + K_BYTES + buf * STAGE;
+    *reinterpret_cast<u16x8*>(st + dual_off<D>(srow, sch * 16)) = qst;
+    *reinterpret_cast<u16x8*>(st + Q_BYTES + dual_off<D>(srow, sch * 16)) = ost;
+    if (tid < BQ) {
+      float* l2 = (float*)(st + 2 * Q_BYTES + DS_BYTES);
+      l2[tid] = lst * 1.44269504089f;
+      l2[BQ + tid] = dst;
+    }
+  };
+
+  load_regs(qstart);
+  for (int idx = tid; idx < BK * KCH; idx += 512) {
+    const int row = idx / KCH, ch = idx % KCH;
+    const long kr = n0 + row;
+    u16x8 t = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (kr < p.Sk) t = *reinterpret_cast<const u16x8*>(kp + kr * p.k_ss + ch * 8);
+    *reinterpret_cast<u16x8*>(Ks + dual_off<D>(row, ch * 16)) = t;
+  }
+  // this wave's 16 keys as MFMA16 B operands: lane holds X[key = 16w + li][32ks + 8g + j]
+  bf16x8v kf[4], vf[4];
+  const long mykey = n0 + 16 * w + li;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    u16x8 t = {0, 0, 0, 0, 0, 0, 0, 0}, u = t;
+    if (mykey < p.Sk) {
+      u = *reinterpret_cast<const u16x8*>(kp + mykey * p.k_ss + ks * 32 + g * 8);
+      t = *reinterpret_cast<const u16x8*>(vp + mykey * p.v_ss + ks * 32 + g * 8);
+    }
+    kf[ks] = __builtin_bit_cast(bf16x8v, u);
+    vf[ks] = __builtin_bit_cast(bf16x8v, t);
+  }
+  store_lds(0);
+  lds_barrier();
+
+  f32x4 dk[8], dv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { dk[i][e] = 0.f; dv[i][e] = 0.f; }
+  f32x4 dq_prev[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dq_prev[t][e] = 0.f;
+  // dQ element (qt, i): row q = 16qt + 4g + i, column d = 16w + li
+  auto flush_dq = [&](long qt_prev) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long q = qt_prev + 16 * t + 4 * g + i;
+        const int voff = (int)(unsigned)((q * dq_rstride + 16 * w + li) * 4);
+        __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(dq_prev[t][i], dq_rs, voff, 0, 0);
+      }
+  };
+
+  int buf = 0;
+  for (long qt0 = qstart; qt0 < p.Sq; qt0 += BQ, buf ^= 1) {
+    load_regs(qt0 + BQ);
+    __builtin_amdgcn_sched_barrier(0);
+    if (qt0 > qstart) flush_dq(qt0 - BQ);
+    char* Qs = smem + K_BYTES + buf * STAGE;
+    char* Os = Qs + Q_BYTES;
+    char* DSs = Os + Q_BYTES;
+    const float* L2s = (const float*)(DSs + DS_BYTES);
+    const float* DLs = L2s + BQ;
+
+    // ---- S = Q K^T, dP = dO V^T  (rows: queries 16qt + 4g + i, lanes: keys)
+    f32x4 sacc[2], dpacc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { sacc[t][e] = 0.f; dpacc[t][e] = 0.f; }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int r = 16 * t + li, cb = (4 * ks + g) * 16;
+        const u16x8 qa = *reinterpret_cast<const u16x8*>(Qs + dual_off<D>(r, cb));
+        sacc[t] = mfma16(__builtin_bit_cast(bf16x8v, qa), kf[ks], sacc[t]);
+        const u16x8 oa = *reinterpret_cast<const u16x8*>(Os + dual_off<D>(r, cb));
+        dpacc[t] = mfma16(__builtin_bit_cast(bf16x8v, oa), vf[ks], dpacc[t]);
+      }
+    // ---- P, dS (element (t, i): query qt0 + 16t + 4g + i, key mykey)
+    bf16x8v pa, da;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const f32x4 l2 = *reinterpret_cast<const f32x4*>(L2s + 16 * t + 4 * g);
+      const f32x4 dl = *reinterpret_cast<const f32x4*>(DLs + 16 * t + 4 * g);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long q = qt0 + 16 * t + 4 * g + i;
+        float pv = __builtin_amdgcn_exp2f(sacc[t][i] * p.scale_log2 - l2[i]);
+        bool ok = q < p.Sq && mykey < p.Sk;
+        if (CAUSAL) ok = ok && (mykey <= q + offs);
+        pv = ok ? pv : 0.f;
+        const float ds = pv * (dpacc[t][i] - dl[i]) * p.scale;
+        pa[4 * t + i] = (__bf16)pv;
+        da[4 * t + i] = (__bf16)ds;
+      }
+    }
+    // ---- dV += P^T dO, dK += dS^T Q  (k-slot (g, j) <-> query 4g + j | 16 + 4g + j - 4)
+#pragma unroll
+    for (int db = 0; db < 8; ++db) {
+      const int colb = (16 * db + 4 * gp) * 2;
+      const bf8v ob = cat_tr(tr_read(Os, dual_off<D>(4 * g + gq, colb)),
+                             tr_read(Os, dual_off<D>(16 + 4 * g + gq, colb)));
+      dv[db] = mfma16(pa, ob, dv[db]);
+      const bf8v qb = cat_tr(tr_read(Qs, dual_off<D>(4 * g + gq, colb)),
+                             tr_read(Qs, dual_off<D>(16 + 4 * g + gq, colb)));
+      dk[db] = mfma16(da, qb, dk[db]);
+    }
+    // ---- dS^T -> LDS [key][q]: this lane's 4 consecutive queries per tile t
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      u16x4 v4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v4[i] = __builtin_bit_cast(u16, da[4 * t + i]);
+      *reinterpret_cast<u16x4*>(DSs + (16 * w + li) * (BQ * 2) + (16 * t + 4 * g) * 2) = v4;
+    }
+    store_lds(buf ^ 1);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) asm volatile("" ::"v"(dq_prev[t][e]));
+    lds_barrier();
+    // ---- dQ[32 q x 16 d (cols 16w..)] = dS[q][keys] K[keys][d]
+    f32x4 dq[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dq[t][e] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int kr = 32 * ks + 8 * g + gq;
+      const int kcol = (16 * w + 4 * gp) * 2;
+      const bf8v kb = cat_tr(tr_read(Ks, dual_off<D>(kr, kcol)), tr_read(Ks, dual_off<D>(kr + 4, kcol)));
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int acol = (16 * t + 4 * gp) * 2;
+        const bf8v af = cat_tr(tr_read(DSs, kr * (BQ * 2) + acol), tr_read(DSs, (kr + 4) * (BQ * 2) + acol));
+        dq[t] = mfma16(af, kb, dq[t]);
+      }
+    }
+    dq_prev[0] = dq[0];
+    dq_prev[1] = dq[1];
+  }
+  if (qstart < p.Sq) {
+    const long last = qstart + ((p.Sq - 1 - qstart) / BQ) * BQ;
+    flush_dq(last);
+  }
+  // ---- dK / dV: element (db, i) = key 16w + 4g + i, d = 16db + li
+  u16* dkp = p.dk + (long)b * p.dk_bs + (long)h * p.dk_hs;
+  u16* dvp = p.dv + (long)b * p.dk_bs + (long)h * p.dk_hs;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long key = n0 + 16 * w + 4 * g + i;
+    if (key < p.Sk) {
+#pragma unroll
+      for (int db = 0; db < 8; ++db) {
+        dkp[key * p.dk_ss + 16 * db + li] = f2bf(dk[db][i]);
+        dvp[key * p.dk_ss + 16 * db + li] = f2bf(dv[db][i]);
+      }
+    }
+  }
+}
+
+// 0 = fa_bwd_kernel, 1 = pipelined, 2 = probe without dQ atomics (wrong dQ),
+// 3 = 8-wave MFMA16 (D = 128)
 static int g_fa_bwd_variant = 1;
 
 }  // namespace pa
@@ -813,6 +1059,12 @@ PA_EXPORT int pa_flash_attn_bwd(const void* q, const void* k, const void* v, con
   const bool fits32 = (long)Sq * strides[1] * 2 < lim && (long)Sq * strides[13] * 2 < lim &&
                       (long)Sq * Hq * D * 4 < lim;
   const int variant = fits32 ? g_fa_bwd_variant : 0;
+  if (D == 128 && variant == 3) {
+    dim3 g3(Hq, B, (Sk + 127) / 128);
+    if (causal) hipLaunchKernelGGL((fa_bwd_kernel3<true>), g3, dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((fa_bwd_kernel3<false>), g3, dim3(512), 0, st, p);
+    PA_LAUNCH_CHECK();
+  }
 #define PA_FA_BWD_LAUNCH(DD, CC)                                                                    \
   switch (variant) {                                                                      \
     case 0: hipLaunchKernelGGL((fa_bwd_kernel<DD, CC>), grid, dim3(256), 0, st, p); break;         \

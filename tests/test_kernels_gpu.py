@@ -248,3 +248,26 @@ def test_linear_fwd_via_transposed_weight_tracks_updates():
     master = w.detach().float().clone()
     optim.adamw_flat(master.view(-1), g.view(-1), m.view(-1), v.view(-1), lr=0.1, param_out=w.data.view(-1))
     assert _rel(F.linear(x, w), x.float() @ w.detach().float()) < 1e-2
+
+
+@pytest.mark.parametrize("variant", [1, 3])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("S,Hq,Hk", [(256, 4, 4), (384, 4, 2), (200, 2, 2), (1000, 2, 1)])
+def test_flash_attention_bwd_variants(variant, causal, S, Hq, Hk):
+    """Every backward kernel variant against the fp32 reference (D = 128)."""
+    torch.manual_seed(1)
+    B, D = 2, 128
+    q = torch.randn(B, S, Hq, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, Hk, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, Hk, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    do = torch.randn(B, S, Hq, D, device=dev, dtype=torch.bfloat16)
+    _native.call("pa_fa_bwd_set_variant", variant)
+    try:
+        o = F.flash_attention(q, k, v, causal=causal)
+        o.backward(do)
+    finally:
+        _native.call("pa_fa_bwd_set_variant", 1)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    F._attn_ref(qr, kr, vr, causal, 1 / math.sqrt(D)).backward(do.float())
+    for a, b_ in ((q.grad, qr.grad), (k.grad, kr.grad), (v.grad, vr.grad)):
+        assert _rel(a, b_) < 2e-2, _rel(a, b_)
