@@ -258,6 +258,7 @@ struct BwdParams {
   const float* lse;  // [B, Hq, Sq]
   float* delta;      // [B, Hq, Sq]
   float* dq_acc;     // [B, Sq, Hq, D] fp32
+  float* dq_part;    // v4: per-key-block dQ partials [nkb, B, Hq, Sq, D] fp32 (or null)
   u16 *dk, *dv;      // [B, Sk, Hq, D] (expanded per q-head for GQA)
   long q_bs, q_ss, q_hs, k_bs, k_ss, k_hs, v_bs, v_ss, v_hs, o_bs, o_ss, o_hs, do_bs, do_ss, do_hs;
   long dk_bs, dk_ss, dk_hs;
@@ -763,7 +764,7 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8v a, bf16x8v b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-template <bool CAUSAL>
+template <bool CAUSAL, bool PARTIAL>
 __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
   constexpr int D = 128, BK = 128, BQ = 32;
   constexpr int KCH = D / 8;                     // 16-B chunks per 128-d row
@@ -864,15 +865,26 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int e = 0; e < 4; ++e) dq_prev[t][e] = 0.f;
-  // dQ element (qt, i): row q = 16qt + 4g + i, column d = 16w + li
+  // dQ element (qt, i): row q = 16qt + 4g + i, column d = 16w + li.
+  // PARTIAL (v4): plain stores of this key block's partial into its own [Sq][D] slab
+  // (HBM store rate, ~6 TB/s) instead of fp32 atomics (~1.3 TB/s chip-wide, which
+  // bound v2/v3: 16 KB of adds per 128x32 tile); fa_bwd_dq_reduce sums the slabs.
+  const auto part_rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(PARTIAL ? p.dq_part + (((long)kt * p.B + b) * p.Hq + h) * (long)p.Sq * D : nullptr), 0,
+      PARTIAL ? p.Sq * D * 4 : 0, 0x00020000);
   auto flush_dq = [&](long qt_prev) {
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const long q = qt_prev + 16 * t + 4 * g + i;
-        const int voff = (int)(unsigned)((q * dq_rstride + 16 * w + li) * 4);
-        __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(dq_prev[t][i], dq_rs, voff, 0, 0);
+        if (PARTIAL) {
+          const int poff = (int)(unsigned)((q * D + 16 * w + li) * 4);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dq_prev[t][i]), part_rs, poff, 0, 0);
+        } else {
+          const int voff = (int)(unsigned)((q * dq_rstride + 16 * w + li) * 4);
+          __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(dq_prev[t][i], dq_rs, voff, 0, 0);
+        }
       }
   };
 
@@ -933,12 +945,15 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
       dk[db] = mfma16(da, qb, dk[db]);
     }
     // ---- dS^T -> LDS [key][q]: this lane's 4 consecutive queries per tile t
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      u16x4 v4;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v4[i] = __builtin_bit_cast(u16, da[4 * t + i]);
-      *reinterpret_cast<u16x4*>(DSs + (16 * w + li) * (BQ * 2) + (16 * t + 4 * g) * 2) = v4;
+    {
+      // (bit-cast the whole vector: per-element __bf16 -> u16 casts of `da` were
+      // miscompiled into two stores of the t = 0 half)
+      const u16x8 du = __builtin_bit_cast(u16x8, da);
+      const u16x4 lo = __builtin_shufflevector(du, du, 0, 1, 2, 3);
+      const u16x4 hi = __builtin_shufflevector(du, du, 4, 5, 6, 7);
+      char* drow = DSs + (16 * w + li) * (BQ * 2) + (4 * g) * 2;
+      *reinterpret_cast<u16x4*>(drow) = lo;
+      *reinterpret_cast<u16x4*>(drow + 32) = hi;
     }
     store_lds(buf ^ 1);
 #pragma unroll
@@ -987,8 +1002,38 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
   }
 }
 
+// dq_acc[b, q, h, :] = sum of the key-block partials that cover query q (v4).  The
+// causal kernel for key block kb starts at query floor(max(0, 128kb - offs) / 32) * 32
+// and writes every query from there (masked ones as zeros), so exactly those blocks
+// are summed.  One thread per 4 consecutive d (16-B loads/stores).
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256) void fa_bwd_dq_reduce(BwdParams p, int nkb) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)p.B * p.Hq * p.Sq * (D / 4);
+  if (gid >= total) return;
+  const int d4 = (int)(gid % (D / 4));
+  const long r = gid / (D / 4);           // (b, h, q)
+  const long q = r % p.Sq;
+  const long bh = r / p.Sq;
+  const int h = (int)(bh % p.Hq), b = (int)(bh / p.Hq);
+  const long offs = CAUSAL ? (long)p.Sk - p.Sq : 0;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const long slab = (long)p.B * p.Hq * p.Sq * D;
+  const float* src = p.dq_part + ((long)b * p.Hq + h) * p.Sq * D + q * D + 4 * d4;
+  for (int kb = 0; kb < nkb; ++kb) {
+    if (CAUSAL) {
+      long qs = 128L * kb - offs;
+      qs = qs > 0 ? (qs / 32) * 32 : 0;
+      if (qs > q) break;
+    }
+    const f32x4 v = *reinterpret_cast<const f32x4*>(src + kb * slab);
+    acc += v;
+  }
+  *reinterpret_cast<f32x4*>(p.dq_acc + (((long)b * p.Sq + q) * p.Hq + h) * D + 4 * d4) = acc;
+}
+
 // 0 = fa_bwd_kernel, 1 = pipelined, 2 = probe without dQ atomics (wrong dQ),
-// 3 = 8-wave MFMA16 (D = 128)
+// 3 = 8-wave MFMA16 (D = 128), 4 = v3 with per-key-block dQ partials + reduce (needs dq_part)
 static int g_fa_bwd_variant = 1;
 
 }  // namespace pa
@@ -999,6 +1044,8 @@ PA_EXPORT int pa_fa_bwd_set_variant(int v) {
   g_fa_bwd_variant = v;
   return 0;
 }
+
+PA_EXPORT int pa_fa_bwd_get_variant() { return g_fa_bwd_variant; }
 
 PA_EXPORT int pa_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
                                 const long* strides /*12: q b,s,h k b,s,h v b,s,h o b,s,h*/,
@@ -1031,12 +1078,12 @@ PA_EXPORT int pa_flash_attn_fwd(const void* q, const void* k, const void* v, voi
 PA_EXPORT int pa_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o,
                                 const void* dout, const float* lse, float* delta, float* dq_acc,
                                 void* dk, void* dv, const long* strides /*18: q k v o do dk(b,s,h)*/, int B, int Sq,
-                                int Sk, int Hq, int Hkv, int D, float scale, int causal,
+                                int Sk, int Hq, int Hkv, int D, float scale, int causal, float* dq_part,
                                 hipStream_t st) {
   if (Hq % Hkv) return (int)hipErrorInvalidValue;
   BwdParams p;
   p.q = (const u16*)q; p.k = (const u16*)k; p.v = (const u16*)v; p.o = (const u16*)o;
-  p.dout = (const u16*)dout; p.lse = lse; p.delta = delta; p.dq_acc = dq_acc;
+  p.dout = (const u16*)dout; p.lse = lse; p.delta = delta; p.dq_acc = dq_acc; p.dq_part = dq_part;
   p.dk = (u16*)dk; p.dv = (u16*)dv;
   p.q_bs = strides[0]; p.q_ss = strides[1]; p.q_hs = strides[2];
   p.k_bs = strides[3]; p.k_ss = strides[4]; p.k_hs = strides[5];
@@ -1058,11 +1105,21 @@ PA_EXPORT int pa_flash_attn_bwd(const void* q, const void* k, const void* v, con
   const long lim = 1L << 31;
   const bool fits32 = (long)Sq * strides[1] * 2 < lim && (long)Sq * strides[13] * 2 < lim &&
                       (long)Sq * Hq * D * 4 < lim;
-  const int variant = fits32 ? g_fa_bwd_variant : 0;
-  if (D == 128 && variant == 3) {
-    dim3 g3(Hq, B, (Sk + 127) / 128);
-    if (causal) hipLaunchKernelGGL((fa_bwd_kernel3<true>), g3, dim3(512), 0, st, p);
-    else hipLaunchKernelGGL((fa_bwd_kernel3<false>), g3, dim3(512), 0, st, p);
+  int variant = fits32 ? g_fa_bwd_variant : 0;
+  if (variant == 4 && (D != 128 || dq_part == nullptr)) variant = 1;
+  if (D == 128 && (variant == 3 || (variant == 4 && dq_part != nullptr))) {
+    const int nkb = (Sk + 127) / 128;
+    dim3 g3(Hq, B, nkb);
+    if (variant == 4) {
+      if (causal) hipLaunchKernelGGL((fa_bwd_kernel3<true, true>), g3, dim3(512), 0, st, p);
+      else hipLaunchKernelGGL((fa_bwd_kernel3<false, true>), g3, dim3(512), 0, st, p);
+      const long n = (long)B * Hq * Sq * (D / 4);
+      if (causal) hipLaunchKernelGGL((fa_bwd_dq_reduce<128, true>), dim3((n + 255) / 256), dim3(256), 0, st, p, nkb);
+      else hipLaunchKernelGGL((fa_bwd_dq_reduce<128, false>), dim3((n + 255) / 256), dim3(256), 0, st, p, nkb);
+    } else {
+      if (causal) hipLaunchKernelGGL((fa_bwd_kernel3<true, false>), g3, dim3(512), 0, st, p);
+      else hipLaunchKernelGGL((fa_bwd_kernel3<false, false>), g3, dim3(512), 0, st, p);
+    }
     PA_LAUNCH_CHECK();
   }
 #define PA_FA_BWD_LAUNCH(DD, CC)                                                                    \

@@ -172,9 +172,13 @@ def _fa_bwd(q, k, v, o, do, lse, causal, scale, dk, dv):
     st = ctypes_long_array(_fa_strides(q) + _fa_strides(k) + _fa_strides(v) + _fa_strides(o)
                            + _fa_strides(do) + _fa_strides(dk))
     assert dk.stride() == dv.stride()
+    part = None
+    if D == 128 and N.lib().pa_fa_bwd_get_variant() == 4:
+        # per-key-block dQ partial slabs (plain stores) summed by a reduce kernel
+        part = torch.empty((Sk + 127) // 128, B, Hq, Sq, D, dtype=torch.float32, device=q.device)
     N.call("pa_flash_attn_bwd", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(o), N.ptr(do), N.ptr(lse),
            N.ptr(delta), N.ptr(dq_acc), N.ptr(dk), N.ptr(dv), st, B, Sq, Sk, Hq, Hk, D,
-           float(scale), int(causal), N.stream())
+           float(scale), int(causal), N.ptr(part), N.stream())
     return dq_acc
 
 
