@@ -625,7 +625,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel2(BwdParams p) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int voff = (int)(base + (unsigned)(((e & 3) + 8 * (e >> 2)) * dq_rstride * 4));
-      if (NOATOMIC) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dq_prev[e]), dq_rs, voff, 0, 0);
+      if (NOATOMIC) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dq_prev[e]), dq_rs, voff, 0, 0);
       else __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(dq_prev[e], dq_rs, voff, 0, 0);
     }
   };
@@ -824,11 +824,11 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
     char* st = smem + K_BYTES + buf * STAGE;
     *reinterpret_cast<u16x8*>(st + dual_off<D>(srow, sch * 16)) = qst;
     *reinterpret_cast<u16x8*>(st + Q_BYTES + dual_off<D>(srow, sch * 16)) = ost;
-    if (tid < BQ) {
-      float* l2 = (float*)(st + 2 * Q_BYTES + DS_BYTES);
-      l2[tid] = lst * 1.44269504089f;
-      l2[BQ + tid] = dst;
-    }
+    // every thread writes its (tid & 31) slot (16 identical writers per slot): no
+    // branch, so hipcc's vmcnt accounting for the prefetch stays static
+    float* l2 = (float*)(st + 2 * Q_BYTES + DS_BYTES);
+    l2[tid & (BQ - 1)] = lst * 1.44269504089f;
+    l2[BQ + (tid & (BQ - 1))] = dst;
   };
 
   load_regs(qstart);
@@ -880,7 +880,9 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
         const long q = qt_prev + 16 * t + 4 * g + i;
         if (PARTIAL) {
           const int poff = (int)(unsigned)((q * D + 16 * w + li) * 4);
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dq_prev[t][i]), part_rs, poff, 0, 0);
+          // (__builtin_bit_cast of an ext_vector element miscompiles to element 0 on this
+          // toolchain: go through a scalar)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dq_prev[t][i]), part_rs, poff, 0, 0);
         } else {
           const int voff = (int)(unsigned)((q * dq_rstride + 16 * w + li) * 4);
           __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(dq_prev[t][i], dq_rs, voff, 0, 0);
@@ -892,7 +894,11 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
   for (long qt0 = qstart; qt0 < p.Sq; qt0 += BQ, buf ^= 1) {
     load_regs(qt0 + BQ);
     __builtin_amdgcn_sched_barrier(0);
-    if (qt0 > qstart) flush_dq(qt0 - BQ);
+    // Unconditional (the first iteration flushes zeros: rows < qstart or out of range)
+    // and issued AFTER the prefetch, so waiting for the prefetch is vmcnt(8), not a
+    // drain of the memory-side atomics / stores (which bound v3 at ~4 us per tile).
+    flush_dq(qt0 - BQ);
+    __builtin_amdgcn_sched_barrier(0);
     char* Qs = smem + K_BYTES + buf * STAGE;
     char* Os = Qs + Q_BYTES;
     char* DSs = Os + Q_BYTES;
