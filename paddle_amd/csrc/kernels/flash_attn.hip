@@ -905,7 +905,11 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
     const float* L2s = (const float*)(DSs + DS_BYTES);
     const float* DLs = L2s + BQ;
 
-    // ---- S = Q K^T, dP = dO V^T  (rows: queries 16qt + 4g + i, lanes: keys)
+    // ---- S = Q K^T, dP = dO V^T  (lanes: keys).  Tile t row m holds query
+    // 8(m>>2) + 4t + (m&3), so lane group g's accumulator rows are queries 8g .. 8g+7
+    // (t-major): the P / dS operands are then in natural k order and the dO / Q
+    // transposed reads of the two groups of a 32-lane half sit 8 rows apart
+    // (conflict-free on the dual image, guide T10) instead of stacked (2-way).
     f32x4 sacc[2], dpacc[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -915,21 +919,21 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
     for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const int r = 16 * t + li, cb = (4 * ks + g) * 16;
+        const int r = 8 * (li >> 2) + 4 * t + (li & 3), cb = (4 * ks + g) * 16;
         const u16x8 qa = *reinterpret_cast<const u16x8*>(Qs + dual_off<D>(r, cb));
         sacc[t] = mfma16(__builtin_bit_cast(bf16x8v, qa), kf[ks], sacc[t]);
         const u16x8 oa = *reinterpret_cast<const u16x8*>(Os + dual_off<D>(r, cb));
         dpacc[t] = mfma16(__builtin_bit_cast(bf16x8v, oa), vf[ks], dpacc[t]);
       }
-    // ---- P, dS (element (t, i): query qt0 + 16t + 4g + i, key mykey)
+    // ---- P, dS (element (t, i): query qt0 + 8g + 4t + i, key mykey)
     bf16x8v pa, da;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const f32x4 l2 = *reinterpret_cast<const f32x4*>(L2s + 16 * t + 4 * g);
-      const f32x4 dl = *reinterpret_cast<const f32x4*>(DLs + 16 * t + 4 * g);
+      const f32x4 l2 = *reinterpret_cast<const f32x4*>(L2s + 8 * g + 4 * t);
+      const f32x4 dl = *reinterpret_cast<const f32x4*>(DLs + 8 * g + 4 * t);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const long q = qt0 + 16 * t + 4 * g + i;
+        const long q = qt0 + 8 * g + 4 * t + i;
         float pv = __builtin_amdgcn_exp2f(sacc[t][i] * p.scale_log2 - l2[i]);
         bool ok = q < p.Sq && mykey < p.Sk;
         if (CAUSAL) ok = ok && (mykey <= q + offs);
@@ -939,28 +943,24 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
         da[4 * t + i] = (__bf16)ds;
       }
     }
-    // ---- dV += P^T dO, dK += dS^T Q  (k-slot (g, j) <-> query 4g + j | 16 + 4g + j - 4)
+    // ---- dV += P^T dO, dK += dS^T Q  (k-slot (g, j) <-> query 8g + j)
 #pragma unroll
     for (int db = 0; db < 8; ++db) {
       const int colb = (16 * db + 4 * gp) * 2;
-      const bf8v ob = cat_tr(tr_read(Os, dual_off<D>(4 * g + gq, colb)),
-                             tr_read(Os, dual_off<D>(16 + 4 * g + gq, colb)));
+      const bf8v ob = cat_tr(tr_read(Os, dual_off<D>(8 * g + gq, colb)),
+                             tr_read(Os, dual_off<D>(8 * g + 4 + gq, colb)));
       dv[db] = mfma16(pa, ob, dv[db]);
-      const bf8v qb = cat_tr(tr_read(Qs, dual_off<D>(4 * g + gq, colb)),
-                             tr_read(Qs, dual_off<D>(16 + 4 * g + gq, colb)));
+      const bf8v qb = cat_tr(tr_read(Qs, dual_off<D>(8 * g + gq, colb)),
+                             tr_read(Qs, dual_off<D>(8 * g + 4 + gq, colb)));
       dk[db] = mfma16(da, qb, dk[db]);
     }
     // ---- dS^T -> LDS [key][q]: this lane's 4 consecutive queries per tile t
-    {
-      // (bit-cast the whole vector: per-element __bf16 -> u16 casts of `da` were
-      // miscompiled into two stores of the t = 0 half)
-      const u16x8 du = __builtin_bit_cast(u16x8, da);
-      const u16x4 lo = __builtin_shufflevector(du, du, 0, 1, 2, 3);
-      const u16x4 hi = __builtin_shufflevector(du, du, 4, 5, 6, 7);
-      char* drow = DSs + (16 * w + li) * (BQ * 2) + (4 * g) * 2;
-      *reinterpret_cast<u16x4*>(drow) = lo;
-      *reinterpret_cast<u16x4*>(drow + 32) = hi;
-    }
+    // dS^T image [key][q] (64-B rows): queries 8g..8g+7 of this lane's key in one
+    // 16-B store; the q column is XOR-ed with 16 on odd 8-key groups so the dQ
+    // transposed reads of the two groups in a 32-lane half hit disjoint banks.
+    // (bit-cast the whole vector: per-element __bf16 -> u16 casts miscompile)
+    *reinterpret_cast<u16x8*>(DSs + (16 * w + li) * (BQ * 2) + ((8 * g) ^ (((li >> 3) & 1) << 4)) * 2) =
+        __builtin_bit_cast(u16x8, da);
     store_lds(buf ^ 1);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -980,7 +980,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
       const bf8v kb = cat_tr(tr_read(Ks, dual_off<D>(kr, kcol)), tr_read(Ks, dual_off<D>(kr + 4, kcol)));
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const int acol = (16 * t + 4 * gp) * 2;
+        const int acol = ((16 * t + 4 * gp) ^ ((g & 1) << 4)) * 2;   // key group (kr >> 3) & 1 == g & 1
         const bf8v af = cat_tr(tr_read(DSs, kr * (BQ * 2) + acol), tr_read(DSs, (kr + 4) * (BQ * 2) + acol));
         dq[t] = mfma16(af, kb, dq[t]);
       }
