@@ -772,8 +772,12 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
   constexpr int Q_BYTES = BQ * D * 2;            // 8 KB
   constexpr int DS_BYTES = BK * BQ * 2;          // 8 KB   dS^T [key][q]
   constexpr int STAGE = 2 * Q_BYTES + DS_BYTES + 2 * BQ * 4;
-  __shared__ __attribute__((aligned(16))) char smem[K_BYTES + 2 * STAGE];
+  // K and V images (dual layout): K feeds S (row reads) and dQ (transposed reads),
+  // V feeds dP; keeping the wave's K/V fragments in LDS instead of 32 registers is
+  // what lets the two prefetch register sets fit in 256 VGPRs.
+  __shared__ __attribute__((aligned(16))) char smem[2 * K_BYTES + 2 * STAGE];
   char* Ks = smem;
+  char* Vs = smem + K_BYTES;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, g = lane >> 4;       // MFMA16 lane row / lane group
@@ -809,50 +813,50 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
   const int srow = tid / KCH, sch = tid % KCH;
   const unsigned qoff = (unsigned)(srow * p.q_ss * 2 + sch * 16);
   const unsigned ooff = (unsigned)(srow * p.do_ss * 2 + sch * 16);
-  u16x8 qst, ost;
-  float lst = 0.f, dst = 0.f;
-  auto load_regs = [&](long qt0) {
-    qst = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(
+  // Two prefetch register sets (A/B): tile t+2 is loaded while tile t computes, so
+  // the vmcnt wait before staging a tile only drains VM ops issued >= 2 tiles ago --
+  // the dQ flush (memory-side atomics / stores, ~3k cycles in vmcnt under load) of
+  // the previous tile no longer sits in front of the prefetch it must wait for.
+  struct Pf {
+    u16x8 q, o;
+    float l, d;
+  };
+  Pf pa_, pb_;
+  auto load_regs = [&](Pf& r, long qt0) {
+    r.q = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(
                                         q_rs, (int)((unsigned)(qt0 * p.q_ss * 2) + qoff), 0, 0));
-    ost = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(
+    r.o = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(
                                         do_rs, (int)((unsigned)(qt0 * p.do_ss * 2) + ooff), 0, 0));
     const int lo = (int)(qt0 + (tid & (BQ - 1))) * 4;
-    lst = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lse_rs, lo, 0, 0));
-    dst = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dl_rs, lo, 0, 0));
+    r.l = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lse_rs, lo, 0, 0));
+    r.d = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dl_rs, lo, 0, 0));
   };
-  auto store_lds = [&](int buf) {
-    char* st = smem + K_BYTES + buf * STAGE;
-    *reinterpret_cast<u16x8*>(st + dual_off<D>(srow, sch * 16)) = qst;
-    *reinterpret_cast<u16x8*>(st + Q_BYTES + dual_off<D>(srow, sch * 16)) = ost;
+  auto store_lds = [&](const Pf& r, int buf) {
+    char* st = smem + 2 * K_BYTES + buf * STAGE;
+    *reinterpret_cast<u16x8*>(st + dual_off<D>(srow, sch * 16)) = r.q;
+    *reinterpret_cast<u16x8*>(st + Q_BYTES + dual_off<D>(srow, sch * 16)) = r.o;
     // every thread writes its (tid & 31) slot (16 identical writers per slot): no
     // branch, so hipcc's vmcnt accounting for the prefetch stays static
     float* l2 = (float*)(st + 2 * Q_BYTES + DS_BYTES);
-    l2[tid & (BQ - 1)] = lst * 1.44269504089f;
-    l2[BQ + (tid & (BQ - 1))] = dst;
+    l2[tid & (BQ - 1)] = r.l * 1.44269504089f;
+    l2[BQ + (tid & (BQ - 1))] = r.d;
   };
 
-  load_regs(qstart);
+  load_regs(pa_, qstart);
+  load_regs(pb_, qstart + BQ);
   for (int idx = tid; idx < BK * KCH; idx += 512) {
     const int row = idx / KCH, ch = idx % KCH;
     const long kr = n0 + row;
-    u16x8 t = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (kr < p.Sk) t = *reinterpret_cast<const u16x8*>(kp + kr * p.k_ss + ch * 8);
-    *reinterpret_cast<u16x8*>(Ks + dual_off<D>(row, ch * 16)) = t;
-  }
-  // this wave's 16 keys as MFMA16 B operands: lane holds X[key = 16w + li][32ks + 8g + j]
-  bf16x8v kf[4], vf[4];
-  const long mykey = n0 + 16 * w + li;
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
     u16x8 t = {0, 0, 0, 0, 0, 0, 0, 0}, u = t;
-    if (mykey < p.Sk) {
-      u = *reinterpret_cast<const u16x8*>(kp + mykey * p.k_ss + ks * 32 + g * 8);
-      t = *reinterpret_cast<const u16x8*>(vp + mykey * p.v_ss + ks * 32 + g * 8);
+    if (kr < p.Sk) {
+      t = *reinterpret_cast<const u16x8*>(kp + kr * p.k_ss + ch * 8);
+      u = *reinterpret_cast<const u16x8*>(vp + kr * p.v_ss + ch * 8);
     }
-    kf[ks] = __builtin_bit_cast(bf16x8v, u);
-    vf[ks] = __builtin_bit_cast(bf16x8v, t);
+    *reinterpret_cast<u16x8*>(Ks + dual_off<D>(row, ch * 16)) = t;
+    *reinterpret_cast<u16x8*>(Vs + dual_off<D>(row, ch * 16)) = u;
   }
-  store_lds(0);
+  const long mykey = n0 + 16 * w + li;
+  store_lds(pa_, 0);
   lds_barrier();
 
   f32x4 dk[8], dv[8];
@@ -860,11 +864,6 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int e = 0; e < 4; ++e) { dk[i][e] = 0.f; dv[i][e] = 0.f; }
-  f32x4 dq_prev[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) dq_prev[t][e] = 0.f;
   // dQ element (qt, i): row q = 16qt + 4g + i, column d = 16w + li.
   // PARTIAL (v4): plain stores of this key block's partial into its own [Sq][D] slab
   // (HBM store rate, ~6 TB/s) instead of fp32 atomics (~1.3 TB/s chip-wide, which
@@ -872,7 +871,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
   const auto part_rs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(PARTIAL ? p.dq_part + (((long)kt * p.B + b) * p.Hq + h) * (long)p.Sq * D : nullptr), 0,
       PARTIAL ? p.Sq * D * 4 : 0, 0x00020000);
-  auto flush_dq = [&](long qt_prev) {
+  auto flush_dq = [&](long qt_prev, const f32x4 (&dq_prev)[2]) {
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -890,16 +889,11 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
       }
   };
 
-  int buf = 0;
-  for (long qt0 = qstart; qt0 < p.Sq; qt0 += BQ, buf ^= 1) {
-    load_regs(qt0 + BQ);
+  // one query tile: compute on stage `buf`, prefetch tile +2 into `ld`, stage tile +1 from `st`
+  auto body = [&](long qt0, int buf, Pf& ld, const Pf& stg) {
+    load_regs(ld, qt0 + 2 * BQ);
     __builtin_amdgcn_sched_barrier(0);
-    // Unconditional (the first iteration flushes zeros: rows < qstart or out of range)
-    // and issued AFTER the prefetch, so waiting for the prefetch is vmcnt(8), not a
-    // drain of the memory-side atomics / stores (which bound v3 at ~4 us per tile).
-    flush_dq(qt0 - BQ);
-    __builtin_amdgcn_sched_barrier(0);
-    char* Qs = smem + K_BYTES + buf * STAGE;
+    char* Qs = smem + 2 * K_BYTES + buf * STAGE;
     char* Os = Qs + Q_BYTES;
     char* DSs = Os + Q_BYTES;
     const float* L2s = (const float*)(DSs + DS_BYTES);
@@ -920,10 +914,13 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int r = 8 * (li >> 2) + 4 * t + (li & 3), cb = (4 * ks + g) * 16;
+        // B fragments: lane holds X[key = 16w + li][32ks + 8g + j] (row read of K / V)
+        const bf16x8v kfr = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u16x8*>(Ks + dual_off<D>(16 * w + li, cb)));
+        const bf16x8v vfr = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u16x8*>(Vs + dual_off<D>(16 * w + li, cb)));
         const u16x8 qa = *reinterpret_cast<const u16x8*>(Qs + dual_off<D>(r, cb));
-        sacc[t] = mfma16(__builtin_bit_cast(bf16x8v, qa), kf[ks], sacc[t]);
+        sacc[t] = mfma16(__builtin_bit_cast(bf16x8v, qa), kfr, sacc[t]);
         const u16x8 oa = *reinterpret_cast<const u16x8*>(Os + dual_off<D>(r, cb));
-        dpacc[t] = mfma16(__builtin_bit_cast(bf16x8v, oa), vf[ks], dpacc[t]);
+        dpacc[t] = mfma16(__builtin_bit_cast(bf16x8v, oa), vfr, dpacc[t]);
       }
     // ---- P, dS (element (t, i): query qt0 + 8g + 4t + i, key mykey)
     bf16x8v pa, da;
@@ -961,11 +958,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
     // (bit-cast the whole vector: per-element __bf16 -> u16 casts miscompile)
     *reinterpret_cast<u16x8*>(DSs + (16 * w + li) * (BQ * 2) + ((8 * g) ^ (((li >> 3) & 1) << 4)) * 2) =
         __builtin_bit_cast(u16x8, da);
-    store_lds(buf ^ 1);
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) asm volatile("" ::"v"(dq_prev[t][e]));
+    store_lds(stg, buf ^ 1);
     lds_barrier();
     // ---- dQ[32 q x 16 d (cols 16w..)] = dS[q][keys] K[keys][d]
     f32x4 dq[2];
@@ -985,12 +978,16 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
         dq[t] = mfma16(af, kb, dq[t]);
       }
     }
-    dq_prev[0] = dq[0];
-    dq_prev[1] = dq[1];
-  }
-  if (qstart < p.Sq) {
-    const long last = qstart + ((p.Sq - 1 - qstart) / BQ) * BQ;
-    flush_dq(last);
+    // flushed right away: the prefetch waited on next is 2 tiles old, so these
+    // memory-side atomics / stores stay in flight instead of being drained by it
+    flush_dq(qt0, dq);
+  };
+  for (long qt0 = qstart; qt0 < p.Sq;) {
+    body(qt0, 0, pa_, pb_);
+    qt0 += BQ;
+    if (qt0 >= p.Sq) break;
+    body(qt0, 1, pb_, pa_);
+    qt0 += BQ;
   }
   // ---- dK / dV: element (db, i) = key 16w + 4g + i, d = 16db + li
   u16* dkp = p.dk + (long)b * p.dk_bs + (long)h * p.dk_hs;
