@@ -82,7 +82,7 @@ def attn():
             t = timeit(pa_bwd)
             out[f"pa_bwd_v{var}_ms_r{rep}"] = round(t, 3)
             out[f"pa_bwd_v{var}_TF_r{rep}"] = round(2.5 * flop_f / t / 1e9, 1)
-    N.call("pa_fa_bwd_set_variant", 1)
+    N.call("pa_fa_bwd_set_variant", 4)
     qt, kt, vt = (x.detach().transpose(1, 2).contiguous().requires_grad_() for x in (q, k, v))
     sd = lambda: torch.nn.functional.scaled_dot_product_attention(qt, kt, vt, is_causal=True)  # noqa: E731
     try:

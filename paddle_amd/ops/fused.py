@@ -173,7 +173,7 @@ def _fa_bwd(q, k, v, o, do, lse, causal, scale, dk, dv):
                            + _fa_strides(do) + _fa_strides(dk))
     assert dk.stride() == dv.stride()
     part = None
-    if D == 128 and N.lib().pa_fa_bwd_get_variant() == 4:
+    if D == 128 and causal and N.lib().pa_fa_bwd_get_variant() == 4:
         # per-key-block dQ partial slabs (plain stores) summed by a reduce kernel
         part = torch.empty((Sk + 127) // 128, B, Hq, Sq, D, dtype=torch.float32, device=q.device)
     N.call("pa_flash_attn_bwd", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(o), N.ptr(do), N.ptr(lse),

@@ -266,7 +266,7 @@ def test_flash_attention_bwd_variants(variant, causal, S, Hq, Hk):
         o = F.flash_attention(q, k, v, causal=causal)
         o.backward(do)
     finally:
-        _native.call("pa_fa_bwd_set_variant", 1)
+        _native.call("pa_fa_bwd_set_variant", 4)
     qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
     F._attn_ref(qr, kr, vr, causal, 1 / math.sqrt(D)).backward(do.float())
     for a, b_ in ((q.grad, qr.grad), (k.grad, kr.grad), (v.grad, vr.grad)):

@@ -17,7 +17,7 @@ def run(variant, B, S, H, causal):
     N.call("pa_fa_bwd_set_variant", variant)
     o = F.flash_attention(q, k, v, causal=causal)
     o.backward(do)
-    N.call("pa_fa_bwd_set_variant", 1)
+    N.call("pa_fa_bwd_set_variant", 4)
     qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
     F._attn_ref(qr, kr, vr, causal, 1 / math.sqrt(D)).backward(do.float())
     out = {}
