@@ -77,7 +77,7 @@ def main():
     model.train()
     opt = FlatShardedOptimizer(model.named_parameters(), lr=3e-4, betas=(0.9, 0.95), eps=1e-8,
                                weight_decay=0.1, grad_clip=1.0, bucket_mb=args.bucket_mb,
-                               overlap=not args.no_overlap)
+                               overlap=not args.no_overlap, overlap_allgather=not args.no_overlap)
     nparams = sum(p.numel() for p in model.parameters())
     if rank == 0:
         log(f"[bench] model {args.model} params={nparams/1e9:.3f}B layers={cfg.num_hidden_layers} "

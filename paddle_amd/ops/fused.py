@@ -83,9 +83,18 @@ class _NormFn(torch.autograd.Function):
         return dx, (dx if ctx.has_res else None), dw, db, None, None
 
 
+def param_ready(w):
+    """Wait for a deferred parameter all-gather (``FlatShardedOptimizer`` with
+    ``overlap_allgather``) before the first read of ``w`` in a step."""
+    f = getattr(w, "_pa_pending", None)
+    if f is not None:
+        f(w)
+
+
 def rms_norm(x, weight, eps=1e-6, residual=None):
     """y = x * rsqrt(mean(x^2) + eps) * weight.  With ``residual``: h = x + residual,
     returns (rms_norm(h), h) with the add fused into the same pass."""
+    param_ready(weight)
     if x.is_cuda:
         y, h = _NormFn.apply(x, residual, weight, None, eps, True)
         return (y, h) if residual is not None else y
@@ -94,6 +103,10 @@ def rms_norm(x, weight, eps=1e-6, residual=None):
 
 
 def layer_norm(x, weight, bias=None, eps=1e-5, residual=None):
+    if weight is not None:
+        param_ready(weight)
+    if bias is not None:
+        param_ready(bias)
     if x.is_cuda and weight is not None and x.shape[-1] % 8 == 0 and x.shape[-1] <= 8192:
         y, h = _NormFn.apply(x, residual, weight, bias, eps, False)
         return (y, h) if residual is not None else y
@@ -458,6 +471,7 @@ class _EmbeddingFn(torch.autograd.Function):
 
 
 def embedding(ids, weight, padding_idx=None):
+    param_ready(weight)
     pad = -1 if padding_idx is None else int(padding_idx)
     if weight.is_cuda and weight.shape[1] % 8 == 0:
         return _EmbeddingFn.apply(ids, weight, pad)
@@ -572,4 +586,7 @@ class _LinearFn(torch.autograd.Function):
 
 
 def linear(x, weight, bias=None):
+    param_ready(weight)
+    if bias is not None:
+        param_ready(bias)
     return _LinearFn.apply(x, weight, bias)

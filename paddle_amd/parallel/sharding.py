@@ -20,7 +20,12 @@ seed of what is done here, MI355X-first:
   bf16 parameter shard; an **all-gather** per bucket re-assembles parameters;
 * no-weight-decay parameters (norm gains, biases) are placed at the end of the
   buffer so decay is a prefix of every shard (one kernel, no masks);
-* global-norm clipping is computed on device (no host sync).
+* global-norm clipping is computed on device (no host sync);
+* with ``overlap_allgather`` the parameter all-gathers are issued on the comm
+  stream in FORWARD order right after the AdamW launch and each bucket is waited
+  for only when the next forward first touches one of its parameters (the fused
+  ops call :func:`ops.fused.param_ready`), hiding the all-gather behind the next
+  step's forward instead of exposing it after the optimizer.
 """
 from __future__ import annotations
 
@@ -44,7 +49,7 @@ class FlatShardedOptimizer:
 
     def __init__(self, named_params, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1,
                  group=None, bucket_mb=256, grad_clip=None, overlap=True, stage=1,
-                 no_decay_fn=None):
+                 no_decay_fn=None, overlap_allgather=False):
         named = [(n, p) for n, p in named_params if p.requires_grad]
         if not named:
             raise ValueError("no trainable parameters")
@@ -132,6 +137,9 @@ class FlatShardedOptimizer:
         self._ready = [0] * len(buckets)
         self._launched = [False] * len(buckets)
         self._sync = True
+        # deferred all-gathers: [(bucket, cuda event | deferred callable)] in issue order
+        self.overlap_allgather = bool(overlap_allgather) and self.W > 1
+        self._ag_queue = []
         self._hooks = []
         if self.W > 1:
             for p in self.params:
@@ -194,10 +202,63 @@ class FlatShardedOptimizer:
         norm = sq.sqrt() / self.W  # gradients are sums over W ranks
         return torch.clamp(self.grad_clip / (norm + 1e-6), max=1.0)
 
+    # ------------------------------------------------------------------ all-gather
+    def _gather(self, b):
+        bs, be, _ = self.buckets[b]
+        s0, L, so = self.shard_slices[b]
+        comm.all_gather(self.flat_param[bs:be], self.param_shard[so:so + L], self.group)
+
+    def _issue_allgathers(self):
+        """Queue every bucket's all-gather, forward order first (the last bucket
+        holds the embedding, the norms and the first blocks), and mark its
+        parameters pending.  On the GPU the gathers run on the comm stream now; on
+        the CPU (gloo, tests) they are deferred until first use, which makes a
+        missed wait show up as stale parameters."""
+        cuda = self.overlap and self.comm_stream is not None
+        if cuda:
+            self.comm_stream.wait_event(torch.cuda.current_stream(self.device).record_event())
+        for b in reversed(range(len(self.buckets))):
+            if cuda:
+                with torch.cuda.stream(self.comm_stream):
+                    self._gather(b)
+                h = self.comm_stream.record_event()
+            else:
+                h = b
+            self._ag_queue.append((b, h))
+            for p in self.buckets[b][2]:
+                p._pa_pending = self._param_wait
+
+    def _param_wait(self, p):
+        self._wait_bucket(self._bucket_of[id(p)])
+
+    def _wait_bucket(self, b=None):
+        """Complete queued all-gathers up to and including bucket ``b`` (all if None)."""
+        if not self._ag_queue:
+            return
+        last = None
+        while self._ag_queue:
+            bb, h = self._ag_queue.pop(0)
+            if isinstance(h, int):
+                self._gather(bb)          # deferred: every rank reaches this in the same order
+            else:
+                last = h
+            for p in self.buckets[bb][2]:
+                p._pa_pending = None
+            if bb == b:
+                break
+        if last is not None:
+            torch.cuda.current_stream(self.device).wait_event(last)
+
+    def sync_params(self):
+        """Make every parameter current (before reading them outside the fused ops,
+        e.g. for a checkpoint or an evaluation with plain torch ops)."""
+        self._wait_bucket(None)
+
     @torch.no_grad()
     def step(self, lr=None):
         if lr is not None:
             self.lr = lr
+        self.sync_params()
         self._finish_comm()
         self.step_count += 1
         gst = self._grad_scale_tensor()
@@ -207,8 +268,11 @@ class FlatShardedOptimizer:
                                decay_end=self.shard_decay_end, grad_scale=1.0 / self.W,
                                grad_scale_tensor=gst)
         if self.W > 1:
-            for (bs, be, _), (s0, L, so) in zip(self.buckets, self.shard_slices):
-                comm.all_gather(self.flat_param[bs:be], self.param_shard[so:so + L], self.group)
+            if self.overlap_allgather:
+                self._issue_allgathers()
+            else:
+                for b in range(len(self.buckets)):
+                    self._gather(b)
         fused.bump_weight_epoch()
 
     def zero_grad(self, set_to_none=False):
@@ -217,10 +281,12 @@ class FlatShardedOptimizer:
     clear_grad = zero_grad
 
     def state_dict(self):
+        self.sync_params()
         return {"master": self.master, "m": self.m, "v": self.v, "step": self.step_count,
                 "lr": self.lr, "world": self.W, "rank": self.r}
 
     def set_state_dict(self, sd):
+        self.sync_params()
         self.master.copy_(sd["master"])
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])

@@ -39,10 +39,11 @@ def _train_single(steps):
     return losses, torch.cat([p.detach().reshape(-1) for p in m.parameters()])
 
 
-def _worker(rank, world, steps):
+def _worker(rank, world, steps, overlap_allgather=False):
     torch.manual_seed(0)
     m = LlamaForCausalLM(_cfg(), device="cpu")
-    opt = FlatShardedOptimizer(m.named_parameters(), lr=1e-3, grad_clip=1.0, bucket_mb=1)
+    opt = FlatShardedOptimizer(m.named_parameters(), lr=1e-3, grad_clip=1.0, bucket_mb=1,
+                               overlap_allgather=overlap_allgather)
     assert len(opt.buckets) > 1
     losses = []
     for b in _batches(steps):
@@ -51,9 +52,13 @@ def _worker(rank, world, steps):
         loss.backward()
         opt.step()
         opt.zero_grad()
+        if overlap_allgather:
+            # gathers are deferred to first use in the next forward
+            assert all(getattr(p, "_pa_pending", None) is not None for p in m.parameters())
         t = torch.tensor([loss.item()])
         torch.distributed.all_reduce(t)
         losses.append(t.item() / world)
+    opt.sync_params()
     return losses, torch.cat([p.detach().reshape(-1) for p in m.parameters()])
 
 
@@ -70,10 +75,11 @@ def test_tiny_llama_cpu_converges():
     assert losses[-1] < losses[0]
 
 
-def test_sharded_dp_matches_single_process():
+@pytest.mark.parametrize("overlap_allgather", [False, True])
+def test_sharded_dp_matches_single_process(overlap_allgather):
     steps = 4
     ref_losses, ref_params = _train_single(steps)
-    losses, params = run_dist(_worker, 2, steps)[0]
+    losses, params = run_dist(_worker, 2, steps, overlap_allgather)[0]
     for a, b in zip(losses, ref_losses):
         assert abs(a - b) < 1e-4, (losses, ref_losses)
     assert_adam_close(params, ref_params, atol=1e-5, rtol=1e-4, lr=1e-3, steps=steps)
