@@ -1,0 +1,376 @@
+#!/usr/bin/env python3
+"""The reference's own published benchmark rows, re-measured on one MI355X.
+
+Rows (reference doc/fluid/new_docs/advanced_usage/benchmark.rst:111-119
+-- "the unit is samples/s" -- models from benchmark/fluid/models/*.py; inference
+rows from paddle/contrib/float16/float16_benchmark.md:21-44):
+
+  vgg16          VGG-16 train, Flowers102 shape (224x224, 102 classes)    59.83 images/s
+  stacked_lstm   IMDB sentiment: emb 512 -> fc tanh 512 -> LSTM 512 ->    1319.99 samples/s
+                 last step -> fc 2 (benchmark/fluid/models/stacked_dynamic_lstm.py)
+  seq2seq        wmt14 attention seq2seq, dict 30000, emb/enc/dec 512,    7147.89 samples/s
+                 bi-LSTM encoder + LSTM decoder with additive attention
+                 (benchmark/fluid/models/machine_translation.py)
+  infer          ResNet-50 / VGG-16 ImageNet inference, batch 64,         67.93 / 178.95 ms (fp32)
+                 fp32 and reduced precision                               33.20 / 60.23 ms (fp16)
+
+All data is synthetic with the datasets' shapes (IMDB review lengths ~ lognormal,
+mean ~230 words, cropped < 1500 like the reference; wmt14 sentence lengths ~ 5-80
+tokens); weights are random-init.  ``stacked_lstm --impl fluid`` runs the
+reference's Fluid program (DynamicRNN over LoD sequences, Adam) through this
+framework's executor; ``--impl dygraph`` runs the same network on MIOpen's fused
+LSTM.  Prints one JSON line per measurement.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+BASE = {"vgg16": 59.83327, "stacked_lstm": 1319.99315, "seq2seq": 7147.89081,
+        "infer_resnet50_fp32": 67.93, "infer_resnet50_lowp": 33.20,
+        "infer_vgg16_fp32": 178.95, "infer_vgg16_lowp": 60.23}
+
+
+def _sync():
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def _timeit(step, steps, warmup):
+    for _ in range(warmup):
+        step()
+    _sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = step()
+    _sync()
+    return (time.perf_counter() - t0) / steps, out
+
+
+def _emit(d):
+    print(json.dumps(d), flush=True)
+
+
+# ------------------------------------------------------------------ VGG-16 train
+def vgg16_bn_drop(num_classes=102, data_format="NHWC"):
+    """The benchmark's network (benchmark/fluid/models/vgg.py:28-52): five groups of
+    conv3x3+BN+ReLU (with the listed dropouts) and a 2x2 max-pool each, then
+    dropout, fc 512, BN+ReLU, dropout, fc 512, fc num_classes; Adam."""
+    from paddle_amd import nn
+
+    layers, c = [], 3
+    for nf, drops in ((64, [0.3, 0]), (128, [0.4, 0]), (256, [0.4, 0.4, 0]), (512, [0.4, 0.4, 0]),
+                      (512, [0.4, 0.4, 0])):
+        for d in drops:
+            layers += [nn.Conv2D(c, nf, 3, padding=1, data_format=data_format),
+                       nn.BatchNorm2D(nf, data_format=data_format), nn.ReLU()]
+            if d:
+                layers.append(nn.Dropout(d))
+            c = nf
+        layers.append(nn.MaxPool2D(2, 2, data_format=data_format))
+    return nn.Sequential(*layers, nn.Flatten(), nn.Dropout(0.5), nn.Linear(512 * 7 * 7, 512),
+                         nn.BatchNorm1D(512), nn.ReLU(), nn.Dropout(0.5), nn.Linear(512, 512),
+                         nn.Linear(512, num_classes))
+
+
+def bench_vgg16(a, dev):
+    import paddle_amd as paddle
+    from paddle_amd import nn
+
+    paddle.seed(0)
+    model = vgg16_bn_drop().to(dev)
+    opt = paddle.optimizer.Adam(learning_rate=1e-3, parameters=model.parameters())
+    model, opt = paddle.amp.decorate(model, opt, level="O2", dtype="bfloat16")
+    B = a.batch or 64
+    x = torch.randn(B, 224, 224, 3, device=dev, dtype=torch.bfloat16)
+    y = torch.randint(0, 102, (B, 1), device=dev)
+    loss_fn = nn.CrossEntropyLoss()
+
+    def step():
+        loss = loss_fn(model(x).float(), y)
+        loss.backward()
+        opt.step()
+        opt.clear_grad(set_to_zero=False)
+        return loss
+
+    dt, loss = _timeit(step, a.steps, a.warmup)
+    v = B / dt
+    _emit({"bench": "vgg16_train", "model": "vgg16_bn_drop (reference benchmark net)", "value": round(v, 1),
+           "unit": "images/s", "batch": B, "dtype": "bf16", "layout": "NHWC",
+           "ms_per_step": round(dt * 1e3, 2), "baseline": BASE["vgg16"], "vs_baseline": round(v / BASE["vgg16"], 2),
+           "loss": float(loss.detach())})
+
+
+# ------------------------------------------------------------------ stacked LSTM (IMDB)
+def _imdb_lengths(rng, n):
+    return np.clip(rng.lognormal(5.25, 0.65, n), 10, 1499).astype(np.int64)
+
+
+def bench_stacked_lstm_dygraph(a, dev):
+    V, E, Hs = 5147, 512, 512
+    B = a.batch or 32
+    torch.manual_seed(0)
+    emb = torch.nn.Embedding(V, E).to(dev)
+    fc0 = torch.nn.Linear(E, Hs).to(dev)
+    lstm = torch.nn.LSTM(Hs, Hs, batch_first=True).to(dev)
+    head = torch.nn.Linear(Hs, 2).to(dev)
+    params = [*emb.parameters(), *fc0.parameters(), *lstm.parameters(), *head.parameters()]
+    from paddle_amd.optimizer import Adam
+
+    opt = Adam(learning_rate=1e-3, parameters=params)
+    rng = np.random.RandomState(0)
+    batches = []
+    for _ in range(8):
+        lens = torch.from_numpy(_imdb_lengths(rng, B))
+        T = int(lens.max())
+        ids = torch.randint(0, V, (B, T), device=dev)
+        lab = torch.randint(0, 2, (B,), device=dev)
+        batches.append((ids, lens, lab))
+    it = [0]
+
+    def step():
+        ids, lens, lab = batches[it[0] % len(batches)]
+        it[0] += 1
+        x = torch.tanh(fc0(emb(ids)))
+        packed = torch.nn.utils.rnn.pack_padded_sequence(x, lens, batch_first=True, enforce_sorted=False)
+        _, (h, _) = lstm(packed)          # h = hidden state at each sequence's last step
+        loss = torch.nn.functional.cross_entropy(head(h[-1]), lab)
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        return loss
+
+    dt, loss = _timeit(step, a.steps, a.warmup)
+    words = float(np.mean([b[1].float().mean().item() for b in batches]))
+    v = B / dt
+    _emit({"bench": "stacked_lstm_train", "impl": "dygraph (MIOpen LSTM)", "value": round(v, 1),
+           "unit": "samples/s", "words_per_s": round(v * words, 1), "avg_len": round(words, 1), "batch": B,
+           "dtype": "fp32", "ms_per_step": round(dt * 1e3, 2), "baseline": BASE["stacked_lstm"],
+           "vs_baseline": round(v / BASE["stacked_lstm"], 2), "loss": float(loss.detach())})
+
+
+def bench_stacked_lstm_fluid(a, dev):
+    import paddle_amd.fluid as fluid
+    from paddle_amd.framework import core
+
+    V, E, Hs = 5147, 512, 512
+    B = a.batch or 32
+    main, startup = fluid.Program(), fluid.Program()
+    main.random_seed = startup.random_seed = 1
+    with fluid.program_guard(main, startup):
+        words = fluid.layers.data(name="words", shape=[1], lod_level=1, dtype="int64")
+        label = fluid.layers.data(name="label", shape=[1], dtype="int64")
+        sent = fluid.layers.embedding(input=words, size=[V, E])
+        sent = fluid.layers.fc(input=sent, size=Hs, act="tanh")
+        rnn = fluid.layers.DynamicRNN()
+        with rnn.block():
+            w = rnn.step_input(sent)
+            ph = rnn.memory(value=0.0, shape=[Hs])
+            pc = rnn.memory(value=0.0, shape=[Hs])
+
+            def gate(act):
+                g = fluid.layers.sums(input=[fluid.layers.fc(input=w, size=Hs),
+                                             fluid.layers.fc(input=ph, size=Hs, bias_attr=False)])
+                return act(g)
+
+            f, i, o = (gate(fluid.layers.sigmoid) for _ in range(3))
+            cg = gate(fluid.layers.tanh)
+            c = fluid.layers.sums(input=[fluid.layers.elementwise_mul(f, pc), fluid.layers.elementwise_mul(i, cg)])
+            h = fluid.layers.elementwise_mul(o, fluid.layers.tanh(c))
+            rnn.update_memory(pc, c)
+            rnn.update_memory(ph, h)
+            rnn.output(h)
+        last = fluid.layers.sequence_pool(rnn(), "last")
+        logit = fluid.layers.fc(input=last, size=2, act="softmax")
+        loss = fluid.layers.mean(fluid.layers.cross_entropy(input=logit, label=label))
+        fluid.optimizer.Adam(learning_rate=1e-3).minimize(loss)
+    place = fluid.CUDAPlace(0) if dev.type == "cuda" else fluid.CPUPlace()
+    exe = fluid.Executor(place)
+    scope = core.Scope()
+    rng = np.random.RandomState(0)
+    feeds = []
+    for _ in range(4):
+        lens = _imdb_lengths(rng, B)
+        if a.max_len:
+            lens = np.minimum(lens, a.max_len)
+        off = np.concatenate([[0], np.cumsum(lens)]).tolist()
+        ids = torch.randint(0, V, (off[-1], 1), device=dev)
+        lab = torch.randint(0, 2, (B, 1), device=dev)
+        feeds.append(({"words": core.LoDTensor(ids, [off]), "label": core.LoDTensor(lab)}, float(lens.mean())))
+    it = [0]
+    with fluid.executor.scope_guard(scope):
+        exe.run(startup)
+
+        def step():
+            fd, _ = feeds[it[0] % len(feeds)]
+            it[0] += 1
+            return exe.run(main, feed=fd, fetch_list=[loss], return_numpy=False)[0]
+
+        dt, out = _timeit(step, a.steps, a.warmup)
+    avg = float(np.mean([f[1] for f in feeds]))
+    v = B / dt
+    _emit({"bench": "stacked_lstm_train", "impl": "fluid DynamicRNN program (executor)", "value": round(v, 1),
+           "unit": "samples/s", "words_per_s": round(v * avg, 1), "avg_len": round(avg, 1), "batch": B,
+           "dtype": "fp32", "ms_per_step": round(dt * 1e3, 2), "baseline": BASE["stacked_lstm"],
+           "vs_baseline": round(v / BASE["stacked_lstm"], 2)})
+
+
+# ------------------------------------------------------------------ seq2seq (wmt14)
+class Seq2Seq(torch.nn.Module):
+    """Reference machine_translation.py network: bi-LSTM encoder, decoder boot =
+    tanh(fc(first step of the backward encoder)), additive attention
+    score = tanh(w . (enc_proj + fc(h))), LSTM step over [context, word], softmax
+    over the 30000-word target dictionary."""
+
+    def __init__(self, V=30000, E=512, H=512):
+        super().__init__()
+        self.H = H
+        self.src_emb = torch.nn.Embedding(V, E)
+        self.trg_emb = torch.nn.Embedding(V, E)
+        self.enc = torch.nn.LSTM(E, H, batch_first=True, bidirectional=True)
+        self.enc_proj = torch.nn.Linear(2 * H, H, bias=False)
+        self.boot = torch.nn.Linear(H, H)
+        self.state_proj = torch.nn.Linear(H, H, bias=False)
+        self.score = torch.nn.Linear(H, 1, bias=False)
+        self.x_gates = torch.nn.Linear(2 * H + E, 4 * H)
+        self.h_gates = torch.nn.Linear(H, 4 * H, bias=False)
+        self.out = torch.nn.Linear(H, V)
+
+    def forward(self, src, slen, trg_in, trg_out, tmask):
+        B, Ts = src.shape
+        x = self.src_emb(src)
+        packed = torch.nn.utils.rnn.pack_padded_sequence(x, slen, batch_first=True, enforce_sorted=False)
+        enc, _ = self.enc(packed)
+        enc, _ = torch.nn.utils.rnn.pad_packed_sequence(enc, batch_first=True, total_length=Ts)
+        smask = (torch.arange(Ts, device=src.device)[None] < slen.to(src.device)[:, None])
+        ep = self.enc_proj(enc)                                   # [B, Ts, H]
+        h = torch.tanh(self.boot(enc[:, 0, self.H:]))             # backward direction, first step
+        c = torch.zeros_like(h)
+        y = self.trg_emb(trg_in)                                  # [B, Tt, E]
+        hs = []
+        neg = torch.finfo(ep.dtype).min
+        for t in range(trg_in.shape[1]):
+            e = self.score(torch.tanh(ep + self.state_proj(h)[:, None])).squeeze(-1)
+            att = torch.softmax(e.masked_fill(~smask, neg), dim=1)
+            ctx = torch.bmm(att[:, None], enc).squeeze(1)           # [B, 2H]
+            g = self.x_gates(torch.cat([ctx, y[:, t]], 1)) + self.h_gates(h)
+            i, f, o, gg = g.chunk(4, 1)
+            c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+            h = torch.sigmoid(o) * torch.tanh(c)
+            hs.append(h)
+        logits = self.out(torch.stack(hs, 1))                     # [B, Tt, V]
+        nll = torch.nn.functional.cross_entropy(logits.flatten(0, 1).float(), trg_out.flatten(), reduction="none")
+        return (nll * tmask.flatten()).sum() / tmask.sum()
+
+
+def bench_seq2seq(a, dev):
+    B = a.batch or 128
+    torch.manual_seed(0)
+    model = Seq2Seq().to(dev)
+    from paddle_amd.optimizer import Adam
+
+    opt = Adam(learning_rate=1e-3, parameters=list(model.parameters()))
+    rng = np.random.RandomState(0)
+    batches = []
+    for _ in range(4):
+        sl = np.clip(rng.lognormal(3.2, 0.5, B), 5, 80).astype(np.int64)
+        tl = np.clip((sl * rng.uniform(0.8, 1.2, B)).astype(np.int64), 5, 80)
+        Ts, Tt = int(sl.max()), int(tl.max())
+        src = torch.randint(0, 30000, (B, Ts), device=dev)
+        trg = torch.randint(0, 30000, (B, Tt + 1), device=dev)
+        tmask = (torch.arange(Tt)[None] < torch.from_numpy(tl)[:, None]).float().to(dev)
+        batches.append((src, torch.from_numpy(sl), trg[:, :-1], trg[:, 1:], tmask, float(tl.mean())))
+    it = [0]
+    amp = a.dtype == "bf16"
+
+    def step():
+        src, sl, ti, to, tm, _ = batches[it[0] % len(batches)]
+        it[0] += 1
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp and dev.type == "cuda"):
+            loss = model(src, sl, ti, to, tm)
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        return loss
+
+    dt, loss = _timeit(step, a.steps, a.warmup)
+    avg = float(np.mean([b[-1] for b in batches]))
+    v = B / dt
+    _emit({"bench": "seq2seq_train", "value": round(v, 1), "unit": "samples/s", "trg_words_per_s": round(v * avg, 1),
+           "avg_trg_len": round(avg, 1), "batch": B, "dtype": a.dtype, "ms_per_step": round(dt * 1e3, 2),
+           "baseline": BASE["seq2seq"], "vs_baseline": round(v / BASE["seq2seq"], 2), "loss": float(loss.detach())})
+
+
+# ------------------------------------------------------------------ inference
+def bench_infer(a, dev):
+    import paddle_amd as paddle
+
+    B = a.batch or 64
+    for name in ("resnet50", "vgg16"):
+        for prec in ("fp32", "lowp"):
+            paddle.seed(0)
+            fmt = "NHWC" if prec == "lowp" else "NCHW"
+            kw = {"data_format": fmt} if name == "resnet50" else {"data_format": fmt}
+            m = getattr(paddle.vision.models, name)(num_classes=1000, **kw).to(dev).eval()
+            dt_ = torch.bfloat16 if prec == "lowp" else torch.float32
+            m = m.to(dt_)
+            shape = (B, 224, 224, 3) if fmt == "NHWC" else (B, 3, 224, 224)
+            x = torch.randn(shape, device=dev, dtype=dt_)
+            graph = None
+            with torch.no_grad():
+                run = lambda: m(x)  # noqa: E731
+                if a.graph and dev.type == "cuda":
+                    s = torch.cuda.Stream()
+                    s.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(s):
+                        for _ in range(3):
+                            m(x)
+                    torch.cuda.current_stream().wait_stream(s)
+                    graph = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(graph):
+                        m(x)
+                    run = graph.replay
+                dt, _ = _timeit(run, a.steps, a.warmup)
+            key = f"infer_{name}_{prec}"
+            _emit({"bench": key, "value": round(dt * 1e3, 3), "unit": "ms/batch", "batch": B,
+                   "dtype": "bf16" if prec == "lowp" else "fp32", "layout": fmt, "hip_graph": graph is not None,
+                   "higher_is_better": False, "baseline_ms": BASE[key],
+                   "speedup_vs_baseline": round(BASE[key] / (dt * 1e3), 2)})
+            del m, x, graph
+            torch.cuda.empty_cache() if dev.type == "cuda" else None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("which", nargs="+", choices=["vgg16", "stacked_lstm", "seq2seq", "infer"])
+    ap.add_argument("--impl", default="both", choices=["both", "dygraph", "fluid"])
+    ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--graph", action="store_true", help="replay inference as a HIP graph")
+    ap.add_argument("--max-len", type=int, default=0, help="cap IMDB lengths (fluid path smoke runs)")
+    a = ap.parse_args()
+    dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    for w in a.which:
+        if w == "vgg16":
+            bench_vgg16(a, dev)
+        elif w == "stacked_lstm":
+            if a.impl in ("both", "dygraph"):
+                bench_stacked_lstm_dygraph(a, dev)
+            if a.impl in ("both", "fluid"):
+                bench_stacked_lstm_fluid(a, dev)
+        elif w == "seq2seq":
+            bench_seq2seq(a, dev)
+        else:
+            bench_infer(a, dev)
+
+
+if __name__ == "__main__":
+    main()

@@ -290,7 +290,7 @@ __global__ void fa_bwd_pre_kernel(BwdParams p) {
   for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   if (row < total && c == 0) p.delta[row] = s;
   // fused zero-init of this row's fp32 dQ accumulator ([B, Sq, Hq, D])
-  if (row < total) {
+  if (row < total && p.dq_acc != nullptr) {  // null: v4 (the reduce writes every element)
     const long q = row % p.Sq;
     const long bh = row / p.Sq;
     const int h = (int)(bh % p.Hq), b = (int)(bh / p.Hq);
@@ -1035,6 +1035,50 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_reduce(BwdParams p, int nkb) {
   *reinterpret_cast<f32x4*>(p.dq_acc + (((long)b * p.Sq + q) * p.Hq + h) * D + 4 * d4) = acc;
 }
 
+// v4 dQ epilogue fused with the inverse (neox) rotary and the bf16 cast, writing the
+// dq slot of the packed dqkv gradient directly: the slabs are read once and the
+// fp32 [B, Sq, Hq, D] accumulator is never materialised (D = 128; position = q).
+// Thread = 4 consecutive d of the low half plus the same 4 of the high half.
+template <bool CAUSAL>
+__global__ __launch_bounds__(256) void fa_dq_reduce_rope(const float* __restrict__ part, int nkb, int B,
+                                                         int Sq, int Sk, int Hq, u16* __restrict__ out,
+                                                         long out_ts, const float* __restrict__ cosT,
+                                                         const float* __restrict__ sinT) {
+  constexpr int D = 128, HALF = 64;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)B * Hq * Sq * (HALF / 4);
+  if (gid >= total) return;
+  const int c = (int)(gid & 15);
+  const long r = gid >> 4;  // (b, h, q)
+  const long q = r % Sq;
+  const long bh = r / Sq;
+  const int h = (int)(bh % Hq), b = (int)(bh / Hq);
+  const long offs = CAUSAL ? (long)Sk - Sq : 0;
+  const long slab = (long)B * Hq * Sq * D;
+  const float* src = part + (bh * Sq + q) * D + 4 * c;
+  f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
+  for (int kb = 0; kb < nkb; ++kb) {
+    if (CAUSAL) {
+      long qs = 128L * kb - offs;
+      qs = qs > 0 ? (qs / 32) * 32 : 0;
+      if (qs > q) break;
+    }
+    lo += *reinterpret_cast<const f32x4*>(src + kb * slab);
+    hi += *reinterpret_cast<const f32x4*>(src + kb * slab + HALF);
+  }
+  const f32x4 co = *reinterpret_cast<const f32x4*>(cosT + q * HALF + 4 * c);
+  const f32x4 si = *reinterpret_cast<const f32x4*>(sinT + q * HALF + 4 * c);
+  u16x4 ol, oh;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {  // inverse rotation: sin -> -sin
+    ol[j] = f2bf(lo[j] * co[j] + hi[j] * si[j]);
+    oh[j] = f2bf(hi[j] * co[j] - lo[j] * si[j]);
+  }
+  u16* dst = out + ((long)b * Sq + q) * out_ts + (long)h * D + 4 * c;
+  *reinterpret_cast<u16x4*>(dst) = ol;
+  *reinterpret_cast<u16x4*>(dst + HALF) = oh;
+}
+
 // 0 = fa_bwd_kernel, 1 = pipelined, 2 = probe without dQ atomics (wrong dQ),
 // 3 = 8-wave MFMA16 (D = 128), 4 = v3 with per-key-block dQ partials + reduce (needs dq_part)
 // default: v4 (causal D = 128: 1.50 ms + 0.46 ms reduce vs v2 2.18 ms at B8 H32 S2048);
@@ -1099,25 +1143,32 @@ PA_EXPORT int pa_flash_attn_bwd(const void* q, const void* k, const void* v, con
   p.B = B; p.Sq = Sq; p.Sk = Sk; p.Hq = Hq; p.Hkv = Hkv;
   p.scale = scale;
   p.scale_log2 = scale * 1.44269504089f;
-  const long rows = (long)B * Hq * Sq;
-  const int lpr = D / 8;
-  const long pre_threads = rows * lpr;
-  if (D == 128) hipLaunchKernelGGL(fa_bwd_pre_kernel<128>, dim3((pre_threads + 255) / 256), dim3(256), 0, st, p);
-  else if (D == 64) hipLaunchKernelGGL(fa_bwd_pre_kernel<64>, dim3((pre_threads + 255) / 256), dim3(256), 0, st, p);
-  else return (int)hipErrorInvalidValue;
-  dim3 grid(Hq, B, (Sk + 127) / 128);
   // the pipelined kernel addresses Q/dO/dQ of one (b, head) with 32-bit buffer offsets
   const long lim = 1L << 31;
   const bool fits32 = (long)Sq * strides[1] * 2 < lim && (long)Sq * strides[13] * 2 < lim &&
                       (long)Sq * Hq * D * 4 < lim;
   int variant = fits32 ? g_fa_bwd_variant : 0;
   if (variant == 4 && (D != 128 || dq_part == nullptr || !causal)) variant = 1;
-  if (D == 128 && (variant == 3 || (variant == 4 && dq_part != nullptr))) {
+  if (variant != 4 && dq_acc == nullptr) return (int)hipErrorInvalidValue;
+  const long rows = (long)B * Hq * Sq;
+  const int lpr = D / 8;
+  const long pre_threads = rows * lpr;
+  BwdParams pp = p;
+  if (variant == 4) pp.dq_acc = nullptr;  // partial slabs: no accumulator to zero
+  if (D == 128) hipLaunchKernelGGL(fa_bwd_pre_kernel<128>, dim3((pre_threads + 255) / 256), dim3(256), 0, st, pp);
+  else if (D == 64) hipLaunchKernelGGL(fa_bwd_pre_kernel<64>, dim3((pre_threads + 255) / 256), dim3(256), 0, st, pp);
+  else return (int)hipErrorInvalidValue;
+  dim3 grid(Hq, B, (Sk + 127) / 128);
+  if (D == 128 && (variant == 3 || variant == 4)) {
     const int nkb = (Sk + 127) / 128;
     dim3 g3(Hq, B, nkb);
     if (variant == 4) {
       if (causal) hipLaunchKernelGGL((fa_bwd_kernel3<true, true>), g3, dim3(512), 0, st, p);
       else hipLaunchKernelGGL((fa_bwd_kernel3<false, true>), g3, dim3(512), 0, st, p);
+      // dq_acc == nullptr: the caller runs the fused reduce (pa_fa_dq_reduce_rope)
+      if (dq_acc == nullptr) {
+        PA_LAUNCH_CHECK();
+      }
       const long n = (long)B * Hq * Sq * (D / 4);
       if (causal) hipLaunchKernelGGL((fa_bwd_dq_reduce<128, true>), dim3((n + 255) / 256), dim3(256), 0, st, p, nkb);
       else hipLaunchKernelGGL((fa_bwd_dq_reduce<128, false>), dim3((n + 255) / 256), dim3(256), 0, st, p, nkb);
@@ -1139,5 +1190,22 @@ PA_EXPORT int pa_flash_attn_bwd(const void* q, const void* k, const void* v, con
     if (causal) { PA_FA_BWD_LAUNCH(64, true) } else { PA_FA_BWD_LAUNCH(64, false) }
   }
 #undef PA_FA_BWD_LAUNCH
+  PA_LAUNCH_CHECK();
+}
+
+// Fused v4 dQ epilogue: sum the per-key-block slabs, inverse-rotate (neox, position
+// = query index) and store bf16 into ``out`` rows of stride ``out_ts`` elements
+// (the dq columns of the packed dqkv gradient).  D = 128.
+PA_EXPORT int pa_fa_dq_reduce_rope(const float* part, int nkb, int B, int Sq, int Sk, int Hq, int causal,
+                                   void* out, long out_ts, const float* cosT, const float* sinT,
+                                   hipStream_t st) {
+  const long n = (long)B * Hq * Sq * 16;
+  const dim3 g((unsigned)((n + 255) / 256));
+  if (causal)
+    hipLaunchKernelGGL(fa_dq_reduce_rope<true>, g, dim3(256), 0, st, part, nkb, B, Sq, Sk, Hq, (u16*)out,
+                       out_ts, cosT, sinT);
+  else
+    hipLaunchKernelGGL(fa_dq_reduce_rope<false>, g, dim3(256), 0, st, part, nkb, B, Sq, Sk, Hq, (u16*)out,
+                       out_ts, cosT, sinT);
   PA_LAUNCH_CHECK();
 }

@@ -176,22 +176,34 @@ def _fa_fwd(q, k, v, causal, scale):
     return o, lse
 
 
-def _fa_bwd(q, k, v, o, do, lse, causal, scale, dk, dv):
-    """dk/dv: [B, Sk, Hq, D] views (expanded over q heads) written by the kernel."""
+def _fa_bwd(q, k, v, o, do, lse, causal, scale, dk, dv, dq_rope_out=None):
+    """dk/dv: [B, Sk, Hq, D] views (expanded over q heads) written by the kernel.
+
+    Returns the fp32 dQ accumulator [B, Sq, Hq, D] -- or, with ``dq_rope_out =
+    (out, row_stride, cos, sin)`` on the partial-slab path, writes the
+    inverse-rotated bf16 dQ straight into ``out`` and returns None."""
     B, Sq, Hq, D = q.shape
     Sk, Hk = k.shape[1], k.shape[2]
-    dq_acc = torch.empty(B, Sq, Hq, D, dtype=torch.float32, device=q.device)  # zeroed in-kernel
     delta = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
     st = ctypes_long_array(_fa_strides(q) + _fa_strides(k) + _fa_strides(v) + _fa_strides(o)
                            + _fa_strides(do) + _fa_strides(dk))
     assert dk.stride() == dv.stride()
     part = None
+    nkb = (Sk + 127) // 128
     if D == 128 and causal and N.lib().pa_fa_bwd_get_variant() == 4:
         # per-key-block dQ partial slabs (plain stores) summed by a reduce kernel
-        part = torch.empty((Sk + 127) // 128, B, Hq, Sq, D, dtype=torch.float32, device=q.device)
+        part = torch.empty(nkb, B, Hq, Sq, D, dtype=torch.float32, device=q.device)
+    fused = part is not None and dq_rope_out is not None
+    dq_acc = None if fused else torch.empty(B, Sq, Hq, D, dtype=torch.float32, device=q.device)
     N.call("pa_flash_attn_bwd", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(o), N.ptr(do), N.ptr(lse),
            N.ptr(delta), N.ptr(dq_acc), N.ptr(dk), N.ptr(dv), st, B, Sq, Sk, Hq, Hk, D,
            float(scale), int(causal), N.ptr(part), N.stream())
+    if fused:
+        out, ts, cos, sin = dq_rope_out
+        assert cos.dtype == torch.float32 and cos.is_contiguous() and sin.is_contiguous()
+        assert cos.shape[0] >= Sq and cos.shape[1] == D // 2
+        N.call("pa_fa_dq_reduce_rope", N.ptr(part), nkb, B, Sq, Sk, Hq, int(causal), N.ptr(out), ts,
+               N.ptr(cos), N.ptr(sin), N.stream())
     return dq_acc
 
 
@@ -271,18 +283,21 @@ class _RopeAttnFn(torch.autograd.Function):
         do = _c(do).view(B, S, Hq, D)
         dqkv = torch.empty_like(packed)
         d4 = dqkv.view(B, S, nh, D)
+        # dq: summed, inverse-rotated and cast straight into dqkv's dq slot when the
+        # partial-slab kernel runs (else via the fp32 accumulator + one rope pass)
+        rope_out = (dqkv, W, cos, sin)
         if Hk == Hq:
             dk, dv = d4[:, :, Hq:2 * Hq], d4[:, :, 2 * Hq:]
-            dq_acc = _fa_bwd(q, k, v, o, do, lse, causal, scale, dk, dv)
+            dq_acc = _fa_bwd(q, k, v, o, do, lse, causal, scale, dk, dv, rope_out)
         else:
             dk_e = torch.empty(B, S, Hq, D, dtype=packed.dtype, device=packed.device)
             dv_e = torch.empty_like(dk_e)
-            dq_acc = _fa_bwd(q, k, v, o, do, lse, causal, scale, dk_e, dv_e)
+            dq_acc = _fa_bwd(q, k, v, o, do, lse, causal, scale, dk_e, dv_e, rope_out)
             d4[:, :, Hq:Hq + Hk] = dk_e.view(B, S, Hk, Hq // Hk, D).sum(3)
             d4[:, :, Hq + Hk:] = dv_e.view(B, S, Hk, Hq // Hk, D).sum(3)
-        # dq: fp32 accumulator -> inverse rotation -> bf16 slot of dqkv (one pass)
-        N.call("pa_rope", 0, 1, N.ptr(dq_acc), Hq * D, N.ptr(dqkv), W, N.ptr(cos), N.ptr(sin), None,
-               B, S, Hq, Hq, D, 1, N.stream())
+        if dq_acc is not None:
+            N.call("pa_rope", 0, 1, N.ptr(dq_acc), Hq * D, N.ptr(dqkv), W, N.ptr(cos), N.ptr(sin), None,
+                   B, S, Hq, Hq, D, 1, N.stream())
         # dk: inverse rotation in place inside dqkv
         kview = dqkv.view(B, S, nh * D)[:, :, Hq * D:]
         N.call("pa_rope", 1, 1, N.ptr(kview), W, N.ptr(kview), W, N.ptr(cos), N.ptr(sin), None,

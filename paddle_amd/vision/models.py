@@ -167,12 +167,13 @@ def resnext50_32x4d(pretrained=False, **kw):
 
 
 class VGG(nn.Layer):
-    def __init__(self, features, num_classes=1000, with_pool=True):
+    def __init__(self, features, num_classes=1000, with_pool=True, data_format="NCHW"):
         super().__init__()
         self.features = features
         self.num_classes, self.with_pool = num_classes, with_pool
+        self.data_format = data_format
         if with_pool:
-            self.avgpool = nn.AdaptiveAvgPool2D((7, 7))
+            self.avgpool = nn.AdaptiveAvgPool2D((7, 7), data_format=data_format)
         if num_classes > 0:
             self.classifier = nn.Sequential(nn.Linear(512 * 7 * 7, 4096), nn.ReLU(), nn.Dropout(),
                                             nn.Linear(4096, 4096), nn.ReLU(), nn.Dropout(),
@@ -183,19 +184,21 @@ class VGG(nn.Layer):
         if self.with_pool:
             x = self.avgpool(x)
         if self.num_classes > 0:
+            if self.data_format == "NHWC":   # classifier weights keep the NCHW flatten order
+                x = x.permute(0, 3, 1, 2)
             x = self.classifier(torch.flatten(x, 1))
         return x
 
 
-def _vgg_features(cfg, batch_norm=False):
+def _vgg_features(cfg, batch_norm=False, data_format="NCHW"):
     layers, c = [], 3
     for v in cfg:
         if v == "M":
-            layers.append(nn.MaxPool2D(2, 2))
+            layers.append(nn.MaxPool2D(2, 2, data_format=data_format))
         else:
-            layers.append(nn.Conv2D(c, v, 3, padding=1))
+            layers.append(nn.Conv2D(c, v, 3, padding=1, data_format=data_format))
             if batch_norm:
-                layers.append(nn.BatchNorm2D(v))
+                layers.append(nn.BatchNorm2D(v, data_format=data_format))
             layers.append(nn.ReLU())
             c = v
     return nn.Sequential(*layers)
@@ -208,19 +211,19 @@ _VGG = {16: [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M",
 
 
 def vgg16(pretrained=False, batch_norm=False, **kw):
-    return VGG(_vgg_features(_VGG[16], batch_norm), **kw)
+    return VGG(_vgg_features(_VGG[16], batch_norm, kw.get("data_format", "NCHW")), **kw)
 
 
 def vgg19(pretrained=False, batch_norm=False, **kw):
-    return VGG(_vgg_features(_VGG[19], batch_norm), **kw)
+    return VGG(_vgg_features(_VGG[19], batch_norm, kw.get("data_format", "NCHW")), **kw)
 
 
 def vgg11(pretrained=False, batch_norm=False, **kw):
-    return VGG(_vgg_features(_VGG[11], batch_norm), **kw)
+    return VGG(_vgg_features(_VGG[11], batch_norm, kw.get("data_format", "NCHW")), **kw)
 
 
 def vgg13(pretrained=False, batch_norm=False, **kw):
-    return VGG(_vgg_features(_VGG[13], batch_norm), **kw)
+    return VGG(_vgg_features(_VGG[13], batch_norm, kw.get("data_format", "NCHW")), **kw)
 
 
 class _InvertedResidual(nn.Layer):

@@ -162,22 +162,30 @@ def test_flash_attention(causal, S, D, Hq, Hk):
     assert _rel(v.grad, vr.grad) < 2e-2, _rel(v.grad, vr.grad)
 
 
-def test_rope_attention_packed():
+@pytest.mark.parametrize("S,H,Hk", [(256, 4, 4), (320, 4, 2), (1024, 8, 8)])
+def test_rope_attention_packed(S, H, Hk):
+    # D = 128 causal runs the partial-slab backward whose dQ epilogue is fused with
+    # the inverse rotary (pa_fa_dq_reduce_rope) -- check the dq section separately
     torch.manual_seed(0)
-    B, S, H, D = 2, 256, 4, 128
+    B, D = 2, 128
     cos, sin = F.rope_tables(S, D, device=dev)
-    qkv = torch.randn(B, S, 3 * H * D, device=dev, dtype=torch.bfloat16, requires_grad=True)
-    o = F.rope_attention(qkv, cos, sin, H)
+    qkv = torch.randn(B, S, (H + 2 * Hk) * D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    o = F.rope_attention(qkv, cos, sin, H, Hk)
     do = torch.randn_like(o)
     o.backward(do)
     xr = qkv.detach().float().requires_grad_()
-    x4 = xr.view(B, S, 3 * H, D)
+    x4 = xr.view(B, S, H + 2 * Hk, D)
     q = F._rope_ref(x4[:, :, :H], cos, sin)
-    k = F._rope_ref(x4[:, :, H:2 * H], cos, sin)
-    orf = F._attn_ref(q, k, x4[:, :, 2 * H:], True, 1 / math.sqrt(D)).reshape(B, S, H * D)
+    k = F._rope_ref(x4[:, :, H:H + Hk], cos, sin)
+    v = x4[:, :, H + Hk:]
+    k, v = k.repeat_interleave(H // Hk, 2), v.repeat_interleave(H // Hk, 2)
+    orf = F._attn_ref(q, k, v, True, 1 / math.sqrt(D)).reshape(B, S, H * D)
     orf.backward(do.float())
     assert _rel(o, orf) < 1e-2
-    assert _rel(qkv.grad, xr.grad) < 2e-2
+    g, gr = qkv.grad.view(B, S, -1, D), xr.grad.view(B, S, -1, D)
+    assert _rel(g[:, :, :H], gr[:, :, :H]) < 2e-2, "dq"
+    assert _rel(g[:, :, H:H + Hk], gr[:, :, H:H + Hk]) < 2e-2, "dk"
+    assert _rel(g[:, :, H + Hk:], gr[:, :, H + Hk:]) < 2e-2, "dv"
 
 
 def test_adamw_flat():
