@@ -118,7 +118,9 @@ def bench_stacked_lstm_dygraph(a, dev):
     torch.manual_seed(0)
     emb = torch.nn.Embedding(V, E).to(dev)
     fc0 = torch.nn.Linear(E, Hs).to(dev)
-    lstm = torch.nn.LSTM(Hs, Hs, batch_first=True).to(dev)
+    import paddle_amd as paddle
+
+    lstm = paddle.nn.LSTM(Hs, Hs).to(dev)  # persistent gfx950 kernel on the GPU
     head = torch.nn.Linear(Hs, 2).to(dev)
     params = [*emb.parameters(), *fc0.parameters(), *lstm.parameters(), *head.parameters()]
     from paddle_amd.optimizer import Adam
@@ -129,6 +131,7 @@ def bench_stacked_lstm_dygraph(a, dev):
     for _ in range(8):
         lens = torch.from_numpy(_imdb_lengths(rng, B))
         T = int(lens.max())
+        lens = lens.to(dev)
         ids = torch.randint(0, V, (B, T), device=dev)
         lab = torch.randint(0, 2, (B,), device=dev)
         batches.append((ids, lens, lab))
@@ -138,8 +141,7 @@ def bench_stacked_lstm_dygraph(a, dev):
         ids, lens, lab = batches[it[0] % len(batches)]
         it[0] += 1
         x = torch.tanh(fc0(emb(ids)))
-        packed = torch.nn.utils.rnn.pack_padded_sequence(x, lens, batch_first=True, enforce_sorted=False)
-        _, (h, _) = lstm(packed)          # h = hidden state at each sequence's last step
+        _, (h, _) = lstm(x, sequence_length=lens)  # h = hidden state at each sequence's last step
         loss = torch.nn.functional.cross_entropy(head(h[-1]), lab)
         loss.backward()
         opt.step()
@@ -149,7 +151,7 @@ def bench_stacked_lstm_dygraph(a, dev):
     dt, loss = _timeit(step, a.steps, a.warmup)
     words = float(np.mean([b[1].float().mean().item() for b in batches]))
     v = B / dt
-    _emit({"bench": "stacked_lstm_train", "impl": "dygraph (MIOpen LSTM)", "value": round(v, 1),
+    _emit({"bench": "stacked_lstm_train", "impl": "dygraph paddle.nn.LSTM (persistent gfx950 kernel)", "value": round(v, 1),
            "unit": "samples/s", "words_per_s": round(v * words, 1), "avg_len": round(words, 1), "batch": B,
            "dtype": "fp32", "ms_per_step": round(dt * 1e3, 2), "baseline": BASE["stacked_lstm"],
            "vs_baseline": round(v / BASE["stacked_lstm"], 2), "loss": float(loss.detach())})
@@ -233,7 +235,9 @@ class Seq2Seq(torch.nn.Module):
         self.H = H
         self.src_emb = torch.nn.Embedding(V, E)
         self.trg_emb = torch.nn.Embedding(V, E)
-        self.enc = torch.nn.LSTM(E, H, batch_first=True, bidirectional=True)
+        import paddle_amd as paddle
+
+        self.enc = paddle.nn.LSTM(E, H, direction="bidirect")   # persistent gfx950 kernel on the GPU
         self.enc_proj = torch.nn.Linear(2 * H, H, bias=False)
         self.boot = torch.nn.Linear(H, H)
         self.state_proj = torch.nn.Linear(H, H, bias=False)
@@ -243,12 +247,11 @@ class Seq2Seq(torch.nn.Module):
         self.out = torch.nn.Linear(H, V)
 
     def forward(self, src, slen, trg_in, trg_out, tmask):
+        """slen: [B] device tensor of source lengths (no host sync: graph-capturable)."""
         B, Ts = src.shape
         x = self.src_emb(src)
-        packed = torch.nn.utils.rnn.pack_padded_sequence(x, slen, batch_first=True, enforce_sorted=False)
-        enc, _ = self.enc(packed)
-        enc, _ = torch.nn.utils.rnn.pad_packed_sequence(enc, batch_first=True, total_length=Ts)
-        smask = (torch.arange(Ts, device=src.device)[None] < slen.to(src.device)[:, None])
+        enc, _ = self.enc(x, sequence_length=slen)                # [B, Ts, 2H], padded rows zero
+        smask = (torch.arange(Ts, device=src.device)[None] < slen[:, None])
         ep = self.enc_proj(enc)                                   # [B, Ts, H]
         h = torch.tanh(self.boot(enc[:, 0, self.H:]))             # backward direction, first step
         c = torch.zeros_like(h)
@@ -270,41 +273,83 @@ class Seq2Seq(torch.nn.Module):
 
 
 def bench_seq2seq(a, dev):
+    """Lengths are bucketed to multiples of 16 and, on the GPU, each bucket's
+    forward+backward is captured once as a HIP graph and replayed (the decoder's
+    per-step attention is launch-bound: ~40 small kernels per target word)."""
     B = a.batch or 128
     torch.manual_seed(0)
     model = Seq2Seq().to(dev)
     from paddle_amd.optimizer import Adam
 
-    opt = Adam(learning_rate=1e-3, parameters=list(model.parameters()))
+    params = list(model.parameters())
+    opt = Adam(learning_rate=1e-3, parameters=params)
     rng = np.random.RandomState(0)
+    bucket = lambda n: (n + 15) // 16 * 16  # noqa: E731
     batches = []
     for _ in range(4):
         sl = np.clip(rng.lognormal(3.2, 0.5, B), 5, 80).astype(np.int64)
         tl = np.clip((sl * rng.uniform(0.8, 1.2, B)).astype(np.int64), 5, 80)
-        Ts, Tt = int(sl.max()), int(tl.max())
+        Ts, Tt = bucket(int(sl.max())), bucket(int(tl.max()))
         src = torch.randint(0, 30000, (B, Ts), device=dev)
         trg = torch.randint(0, 30000, (B, Tt + 1), device=dev)
         tmask = (torch.arange(Tt)[None] < torch.from_numpy(tl)[:, None]).float().to(dev)
-        batches.append((src, torch.from_numpy(sl), trg[:, :-1], trg[:, 1:], tmask, float(tl.mean())))
+        batches.append((src, torch.from_numpy(sl).to(dev), trg[:, :-1], trg[:, 1:], tmask, float(tl.mean())))
     it = [0]
     amp = a.dtype == "bf16"
+    use_graph = dev.type == "cuda" and not a.no_graph
+    graphs = {}  # (Ts, Tt) -> (graph, static inputs, static loss, grads)
+
+    def fwd_bwd(src, sl, ti, to, tm):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp and dev.type == "cuda"):
+            loss = model(src, sl, ti, to, tm)
+        loss.backward()
+        return loss
+
+    def capture(inputs):
+        static = [t.clone() for t in inputs]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                for p in params:
+                    p.grad = None
+                fwd_bwd(*static)
+        torch.cuda.current_stream().wait_stream(s)
+        for p in params:
+            p.grad = None
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            loss = fwd_bwd(*static)
+        return g, static, loss, [p.grad for p in params]
 
     def step():
         src, sl, ti, to, tm, _ = batches[it[0] % len(batches)]
         it[0] += 1
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp and dev.type == "cuda"):
-            loss = model(src, sl, ti, to, tm)
-        loss.backward()
+        inputs = (src, sl, ti, to, tm)
+        if use_graph:
+            key = (src.shape[1], ti.shape[1])
+            if key not in graphs:
+                graphs[key] = capture(inputs)
+            g, static, loss, grads = graphs[key]
+            for d, x in zip(static, inputs):
+                d.copy_(x)
+            g.replay()
+            for p, gr in zip(params, grads):
+                p.grad = gr
+        else:
+            loss = fwd_bwd(*inputs)
         opt.step()
-        opt.clear_grad()
+        if not use_graph:
+            opt.clear_grad()
         return loss
 
-    dt, loss = _timeit(step, a.steps, a.warmup)
+    dt, loss = _timeit(step, a.steps, max(a.warmup, len(batches)))
     avg = float(np.mean([b[-1] for b in batches]))
     v = B / dt
     _emit({"bench": "seq2seq_train", "value": round(v, 1), "unit": "samples/s", "trg_words_per_s": round(v * avg, 1),
-           "avg_trg_len": round(avg, 1), "batch": B, "dtype": a.dtype, "ms_per_step": round(dt * 1e3, 2),
-           "baseline": BASE["seq2seq"], "vs_baseline": round(v / BASE["seq2seq"], 2), "loss": float(loss.detach())})
+           "avg_trg_len": round(avg, 1), "batch": B, "dtype": a.dtype, "hip_graph": use_graph,
+           "ms_per_step": round(dt * 1e3, 2), "baseline": BASE["seq2seq"],
+           "vs_baseline": round(v / BASE["seq2seq"], 2), "loss": float(loss.detach())})
 
 
 # ------------------------------------------------------------------ inference
@@ -355,6 +400,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--graph", action="store_true", help="replay inference as a HIP graph")
+    ap.add_argument("--no-graph", action="store_true", help="seq2seq: eager steps instead of HIP-graph replay")
     ap.add_argument("--max-len", type=int, default=0, help="cap IMDB lengths (fluid path smoke runs)")
     a = ap.parse_args()
     dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")

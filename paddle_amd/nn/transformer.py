@@ -4,9 +4,12 @@
 sub-layers (``[in, out]`` weights) and runs the attention core on the gfx950
 flash-attention kernel when there is no explicit mask / dropout (bf16, head_dim
 64/128 on the GPU); otherwise the masked path uses SDPA.  ``LSTM``/``GRU``/
-``SimpleRNN`` use MIOpen's fused RNN through PyTorch-ROCm with Paddle's parameter
-names (``weight_ih_l{k}``, ``weight_hh_l{k}``, ``bias_ih_l{k}``, ``bias_hh_l{k}``;
-``direction="bidirect"`` adds the ``_reverse`` set) and gate order.
+``SimpleRNN`` keep Paddle's parameter names (``weight_ih_l{k}``, ``weight_hh_l{k}``,
+``bias_ih_l{k}``, ``bias_hh_l{k}``; ``direction="bidirect"`` adds the ``_reverse``
+set) and gate order.  On the GPU, LSTM runs every layer/direction on the
+persistent gfx950 kernel (``ops/rnn.py``: one launch per sequence, W_hh resident in
+registers; 1.9x MIOpen at B 32, H 512, T 833) when H is 128/256/512/1024 and the
+batch is <= 128; other shapes and GRU/SimpleRNN use MIOpen through PyTorch-ROCm.
 """
 from __future__ import annotations
 
@@ -189,7 +192,53 @@ class _RNNBase(Layer):
         self.time_major, self.num_directions = time_major, 2 if bidir else 1
         self.hidden_size, self.num_layers = hidden_size, num_layers
 
+    def _persistent_ok(self, x):
+        import os
+
+        from ..ops import rnn as R
+
+        if self._mode != "LSTM" or os.environ.get("PADDLE_AMD_PERSISTENT_LSTM", "1") == "0":
+            return False
+        B = x.shape[1 if self.time_major else 0]
+        return R.persistent_ok(x, self.hidden_size, B)
+
+    def _persistent_lstm(self, x, initial_states, lens):
+        """Every layer/direction on the persistent gfx950 LSTM kernel (ops/rnn.py);
+        same outputs as torch's (padded positions zeroed, h_n/c_n = last states)."""
+        from ..ops import rnn as R
+
+        inp = x if self.time_major else x.transpose(0, 1)
+        T = inp.shape[0]
+        h_n, c_n = [], []
+        for layer in range(self.num_layers):
+            outs = []
+            for d in range(self.num_directions):
+                sfx = f"_l{layer}" + ("_reverse" if d else "")
+                w_ih = getattr(self.rnn, "weight_ih" + sfx).t()
+                w_hh = getattr(self.rnn, "weight_hh" + sfx).t()
+                b = getattr(self.rnn, "bias_ih" + sfx) + getattr(self.rnn, "bias_hh" + sfx)
+                k = layer * self.num_directions + d
+                h0 = initial_states[0][k] if initial_states is not None else None
+                c0 = initial_states[1][k] if initial_states is not None else None
+                xi = R.reverse_padded(inp, lens) if d else inp
+                hs, h, c = R.lstm(xi, w_ih, w_hh, b, h0, c0, lens=lens)
+                outs.append(R.reverse_padded(hs, lens) if d else hs)
+                h_n.append(h)
+                c_n.append(c)
+            inp = torch.cat(outs, -1) if len(outs) > 1 else outs[0]
+            if self.rnn.dropout and self.training and layer < self.num_layers - 1:
+                inp = torch.nn.functional.dropout(inp, self.rnn.dropout)
+        out = inp
+        if lens is not None:
+            m = torch.arange(T, device=out.device).unsqueeze(1) < lens.to(out.device).unsqueeze(0)
+            out = out * m.unsqueeze(-1).to(out.dtype)
+        if not self.time_major:
+            out = out.transpose(0, 1)
+        return out, (torch.stack(h_n), torch.stack(c_n))
+
     def forward(self, inputs, initial_states=None, sequence_length=None):
+        if self._persistent_ok(inputs):
+            return self._persistent_lstm(inputs, initial_states, sequence_length)
         x = inputs
         if sequence_length is not None:
             x = torch.nn.utils.rnn.pack_padded_sequence(x, sequence_length.cpu(), batch_first=not self.time_major,

@@ -326,6 +326,15 @@ def _cmp(name, fn):
     @register_op(name, ["X", "Y"], ["Out"], {"axis": -1, "force_cpu": False}, grad=None)
     def k(ctx):
         x, y = ctx.input("X"), ctx.input("Y")
+        if x.device != y.device:
+            # loop counters / array lengths live on the host: compare scalars there (the
+            # While condition is read on the host anyway), else follow the larger operand
+            if x.numel() == 1 and y.numel() == 1:
+                x, y = x.cpu(), y.cpu()
+            elif x.numel() >= y.numel():
+                y = y.to(x.device)
+            else:
+                x = x.to(y.device)
         ctx.set_output("Out", fn(x, y.to(x.dtype) if y.dtype != x.dtype else y))
 
 

@@ -1,0 +1,78 @@
+"""Persistent LSTM kernel (csrc/kernels/rnn.hip) vs a plain fp32 PyTorch recurrence
+with the same length-freezing semantics (ops/rnn.py::_lstm_ref)."""
+import pytest
+import torch
+
+from paddle_amd.ops import rnn
+
+pytestmark = pytest.mark.gpu
+dev = torch.device("cuda")
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("T,B,I,H,with_state", [(7, 3, 24, 128, False), (40, 32, 64, 512, True),
+                                                (33, 50, 32, 256, False), (5, 64, 16, 1024, True), (9, 100, 32, 512, True)])
+def test_lstm_persistent_matches_reference(T, B, I, H, with_state):
+    torch.manual_seed(0)
+    x = torch.randn(T, B, I, device=dev)
+    w_ih = (torch.randn(I, 4 * H, device=dev) / I ** 0.5).requires_grad_()
+    w_hh = (torch.randn(H, 4 * H, device=dev) / H ** 0.5).requires_grad_()
+    b = (0.1 * torch.randn(4 * H, device=dev)).requires_grad_()
+    lens = torch.randint(1, T + 1, (B,))
+    lens[0] = T
+    h0 = (0.5 * torch.randn(B, H, device=dev)).requires_grad_() if with_state else None
+    c0 = (0.5 * torch.randn(B, H, device=dev)).requires_grad_() if with_state else None
+    xr = x.clone().requires_grad_()
+    x.requires_grad_()
+    hs, h, c = rnn.lstm(x, w_ih, w_hh, b, h0, c0, lens=lens)
+    torch.cuda.synchronize()
+    ref_leaves = [t.detach().clone().requires_grad_() if t is not None else None for t in (w_ih, w_hh, b, h0, c0)]
+    hr, hlr, clr = rnn._lstm_ref(xr, *ref_leaves, lens=lens)
+    assert _rel(hs, hr) < 2e-2, _rel(hs, hr)
+    assert _rel(h, hlr) < 2e-2 and _rel(c, clr) < 2e-2
+    gh = torch.randn_like(hs)
+    gl = torch.randn_like(h)
+    (hs * gh).sum().backward(retain_graph=True)
+    (h * gl).sum().backward()
+    ((hr * gh).sum() + (hlr * gl).sum()).backward()
+    assert _rel(x.grad, xr.grad) < 3e-2, _rel(x.grad, xr.grad)
+    for got, ref, name in zip((w_ih, w_hh, b, h0, c0), ref_leaves, ("w_ih", "w_hh", "b", "h0", "c0")):
+        if got is not None:
+            assert _rel(got.grad, ref.grad) < 3e-2, (name, _rel(got.grad, ref.grad))
+
+
+def test_reverse_padded_roundtrip():
+    x = torch.arange(5 * 3, device=dev, dtype=torch.float32).view(5, 3, 1)
+    lens = torch.tensor([5, 2, 3])
+    r = rnn.reverse_padded(x, lens)
+    assert r[:2, 1, 0].tolist() == [4.0, 1.0] and r[2:, 1, 0].tolist() == x[2:, 1, 0].tolist()
+    assert torch.equal(rnn.reverse_padded(r, lens), x)
+
+
+@pytest.mark.parametrize("direction,layers", [("forward", 1), ("bidirect", 2)])
+def test_nn_lstm_persistent_matches_miopen(monkeypatch, direction, layers):
+    """paddle.nn.LSTM on the persistent kernel vs the same module on MIOpen."""
+    import paddle_amd as paddle
+
+    torch.manual_seed(0)
+    B, T, I, H = 12, 30, 48, 256
+    m = paddle.nn.LSTM(I, H, num_layers=layers, direction=direction).to(dev)
+    x = torch.randn(B, T, I, device=dev)
+    lens = torch.randint(3, T + 1, (B,))
+    lens[0] = T
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PADDLE_AMD_PERSISTENT_LSTM", flag)
+        m.zero_grad()
+        xi = x.clone().requires_grad_()
+        out, (h, c) = m(xi, sequence_length=lens)
+        (out.square().sum() + h.sum() + c.sum()).backward()
+        outs[flag] = (out.detach(), h.detach(), c.detach(), xi.grad, [p.grad.clone() for p in m.parameters()])
+    a, r = outs["1"], outs["0"]
+    for got, ref in zip(a[:4], r[:4]):
+        assert _rel(got, ref) < 3e-2, _rel(got, ref)
+    for got, ref in zip(a[4], r[4]):
+        assert _rel(got, ref) < 5e-2, _rel(got, ref)
