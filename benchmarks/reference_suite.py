@@ -227,49 +227,45 @@ def bench_stacked_lstm_fluid(a, dev):
 class Seq2Seq(torch.nn.Module):
     """Reference machine_translation.py network: bi-LSTM encoder, decoder boot =
     tanh(fc(first step of the backward encoder)), additive attention
-    score = tanh(w . (enc_proj + fc(h))), LSTM step over [context, word], softmax
-    over the 30000-word target dictionary."""
+    score = w . tanh(enc_proj + fc(h)), LSTM step over [context, word, h], softmax
+    over the 30000-word target dictionary.  The decoder recurrence runs on the
+    fused attention-decoder kernels (ops/rnn.py::attention_lstm_decoder)."""
 
     def __init__(self, V=30000, E=512, H=512):
         super().__init__()
+        import paddle_amd as paddle
+
         self.H = H
         self.src_emb = torch.nn.Embedding(V, E)
         self.trg_emb = torch.nn.Embedding(V, E)
-        import paddle_amd as paddle
-
         self.enc = paddle.nn.LSTM(E, H, direction="bidirect")   # persistent gfx950 kernel on the GPU
         self.enc_proj = torch.nn.Linear(2 * H, H, bias=False)
         self.boot = torch.nn.Linear(H, H)
         self.state_proj = torch.nn.Linear(H, H, bias=False)
         self.score = torch.nn.Linear(H, 1, bias=False)
-        self.x_gates = torch.nn.Linear(2 * H + E, 4 * H)
-        self.h_gates = torch.nn.Linear(H, 4 * H, bias=False)
+        self.w_ctx_h = torch.nn.Parameter(torch.randn(2 * H + H, 4 * H) / (3 * H) ** 0.5)  # [ctx, h] -> gates
+        self.y_gates = torch.nn.Linear(E, 4 * H)                                            # word -> gates (+ bias)
         self.out = torch.nn.Linear(H, V)
 
     def forward(self, src, slen, trg_in, trg_out, tmask):
         """slen: [B] device tensor of source lengths (no host sync: graph-capturable)."""
-        B, Ts = src.shape
+        from paddle_amd.ops import rnn
+
         x = self.src_emb(src)
         enc, _ = self.enc(x, sequence_length=slen)                # [B, Ts, 2H], padded rows zero
-        smask = (torch.arange(Ts, device=src.device)[None] < slen[:, None])
         ep = self.enc_proj(enc)                                   # [B, Ts, H]
-        h = torch.tanh(self.boot(enc[:, 0, self.H:]))             # backward direction, first step
-        c = torch.zeros_like(h)
-        y = self.trg_emb(trg_in)                                  # [B, Tt, E]
-        hs = []
-        neg = torch.finfo(ep.dtype).min
-        for t in range(trg_in.shape[1]):
-            e = self.score(torch.tanh(ep + self.state_proj(h)[:, None])).squeeze(-1)
-            att = torch.softmax(e.masked_fill(~smask, neg), dim=1)
-            ctx = torch.bmm(att[:, None], enc).squeeze(1)           # [B, 2H]
-            g = self.x_gates(torch.cat([ctx, y[:, t]], 1)) + self.h_gates(h)
-            i, f, o, gg = g.chunk(4, 1)
-            c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
-            h = torch.sigmoid(o) * torch.tanh(c)
-            hs.append(h)
-        logits = self.out(torch.stack(hs, 1))                     # [B, Tt, V]
-        nll = torch.nn.functional.cross_entropy(logits.flatten(0, 1).float(), trg_out.flatten(), reduction="none")
-        return (nll * tmask.flatten()).sum() / tmask.sum()
+        h0 = torch.tanh(self.boot(enc[:, 0, self.H:]))            # backward direction, first step
+        c0 = torch.zeros_like(h0)
+        Y = self.y_gates(self.trg_emb(trg_in)).transpose(0, 1)    # [Tt, B, 4H]
+        hs = rnn.attention_lstm_decoder(enc, ep, slen, Y, h0, c0, self.state_proj.weight.t(),
+                                        self.score.weight[0], self.w_ctx_h)
+        from paddle_amd import ops
+
+        logits = self.out(hs.transpose(0, 1))                     # [B, Tt, V]
+        labels = torch.where(tmask > 0, trg_out, torch.full_like(trg_out, -100))
+        # fused log-softmax + NLL over the 30000-word vocabulary (gradient written in place)
+        return ops.softmax_cross_entropy(logits.flatten(0, 1), labels.flatten(), ignore_index=-100,
+                                         inplace_grad=logits.is_cuda)
 
 
 def bench_seq2seq(a, dev):

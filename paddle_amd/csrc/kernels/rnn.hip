@@ -101,13 +101,17 @@ struct LstmArgs {
 };
 
 // -------------------------------------------------------------------- forward
-// grid = H/16 workgroups x 256 threads; wave w computes gate w of the 16 units.
-template <int NRT, int KS>  // row tiles = BP / 16; k-steps = H / 32
+// grid = (H/16 unit blocks, row blocks of 16 NRT batch rows); wave w computes gate w
+// of the 16 units.  Row blocks never exchange data (a row's recurrence only reads
+// its own row), so each row block has its own barrier counter.
+template <int NRT, int KS>  // row tiles per workgroup; k-steps = H / 32
 __global__ __launch_bounds__(256) void lstm_fwd_persistent(LstmArgs a) {
   __shared__ float gs[4][NRT * 16][16];
   __shared__ int abort_s;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int j = blockIdx.x, H = a.H, G = 4 * H, B = a.B, BP = NRT * 16;
+  const int j = blockIdx.x, H = a.H, G = 4 * H, B = a.B, BP = a.BP;
+  const int row0 = blockIdx.y * NRT * 16;
+  unsigned* cnt = a.cnt + 16 * blockIdx.y;
   const int n = lane & 15, kq = lane >> 4;
   const int col = w * H + 16 * j + n;  // this lane's W_hh / gate column
   // resident W_hh fragments: B[k][n] = W_hh[k][col], k = 32 ks + 8 kq + e
@@ -119,20 +123,30 @@ __global__ __launch_bounds__(256) void lstm_fwd_persistent(LstmArgs a) {
     for (int e = 0; e < 8; ++e) v[e] = a.whh[(long)(32 * ks + 8 * kq + e) * G + col];
     wf[ks] = v;
   }
-  // pointwise ownership: pairs p = tid + 256 r over (b, u) with b < BP
-  constexpr int NP = (NRT * 16 * 16 + 255) / 256;
+  // pointwise ownership: local pairs p = tid + 256 r over (row, unit)
+  constexpr int NP = NRT;  // NRT * 16 rows * 16 units / 256 threads
   float creg[NP], hreg[NP];
 #pragma unroll
   for (int r = 0; r < NP; ++r) {
     const int p = threadIdx.x + 256 * r;
-    const int b = p >> 4, u = 16 * j + (p & 15);
+    const int b = row0 + (p >> 4), u = 16 * j + (p & 15);
     creg[r] = (b < B && a.c0) ? a.c0[(long)b * H + u] : 0.f;
     hreg[r] = (b < B && a.h0) ? a.h0[(long)b * H + u] : 0.f;
   }
   if (threadIdx.x == 0) abort_s = 0;
   for (int t = 0; t < a.T; ++t) {
-    if (t > 0 && !rnn_wait(a.cnt, (unsigned)(gridDim.x * t), a.err, &abort_s)) return;
-    const u16* hin = a.hbuf + (long)(t & 1) * BP * H;
+    // this step's input projection does not depend on other workgroups: issue it
+    // before the barrier so its latency hides behind the wait
+    float xv[NRT][4];
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = row0 + 16 * rt + 4 * kq + i;
+        xv[rt][i] = b < B ? a.xproj[((long)t * B + b) * G + col] : 0.f;
+      }
+    if (t > 0 && !rnn_wait(cnt, (unsigned)(gridDim.x * t), a.err, &abort_s)) return;
+    const u16* hin = a.hbuf + (long)(t & 1) * BP * H + (long)row0 * H;
     f32x4 acc[NRT];
 #pragma unroll
     for (int rt = 0; rt < NRT; ++rt) acc[rt] = {0.f, 0.f, 0.f, 0.f};
@@ -144,15 +158,13 @@ __global__ __launch_bounds__(256) void lstm_fwd_persistent(LstmArgs a) {
         acc[rt] = rnn_mfma(av, wf[ks], acc[rt]);
       }
     }
-    // epilogue: + x W_ih + b, activation, to LDS (row b = 16 rt + 4 kq + i, unit n)
+    // epilogue: + x W_ih + b, activation, to LDS (local row 16 rt + 4 kq + i, unit n)
 #pragma unroll
     for (int rt = 0; rt < NRT; ++rt) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int b = 16 * rt + 4 * kq + i;
-        float v = acc[rt][i];
-        if (b < B) v += a.xproj[((long)t * B + b) * G + col];
-        gs[w][b][n] = (w == 2) ? tanh_f(v) : sigm(v);
+        const float v = acc[rt][i] + xv[rt][i];
+        gs[w][16 * rt + 4 * kq + i][n] = (w == 2) ? tanh_f(v) : sigm(v);
       }
     }
     __syncthreads();
@@ -160,12 +172,10 @@ __global__ __launch_bounds__(256) void lstm_fwd_persistent(LstmArgs a) {
 #pragma unroll
     for (int r = 0; r < NP; ++r) {
       const int p = threadIdx.x + 256 * r;
-      const int b = p >> 4, nn = p & 15, u = 16 * j + nn;
-      if (b >= BP) continue;
+      const int lb = p >> 4, nn = p & 15, u = 16 * j + nn, b = row0 + lb;
       if (b < B) {
-        const float ig = gs[0][b][nn], fg = gs[1][b][nn], gg = gs[2][b][nn], og = gs[3][b][nn];
-        const bool active = t < a.lens[b];
-        if (active) {
+        const float ig = gs[0][lb][nn], fg = gs[1][lb][nn], gg = gs[2][lb][nn], og = gs[3][lb][nn];
+        if (t < a.lens[b]) {
           creg[r] = fg * creg[r] + ig * gg;
           hreg[r] = og * tanh_f(creg[r]);
         }
@@ -180,7 +190,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_persistent(LstmArgs a) {
       }
       hout[(long)b * H + u] = f2bf(b < B ? hreg[r] : 0.f);
     }
-    rnn_arrive(a.cnt);
+    rnn_arrive(cnt);
   }
 }
 
@@ -192,7 +202,9 @@ __global__ __launch_bounds__(256) void lstm_bwd_persistent(LstmArgs a) {
   __shared__ float red[4][NRT * 16][16];
   __shared__ int abort_s;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int j = blockIdx.x, H = a.H, G = 4 * H, B = a.B, BP = NRT * 16;
+  const int j = blockIdx.x, H = a.H, G = 4 * H, B = a.B, BP = a.BP;
+  const int row0 = blockIdx.y * NRT * 16;
+  unsigned* cnt = a.cnt + 16 * blockIdx.y;
   const int n = lane & 15, kq = lane >> 4;
   const int u_mine = 16 * j + n;
   const int KQ = G / 4;  // K range per wave (= H = 32 KS)
@@ -200,12 +212,12 @@ __global__ __launch_bounds__(256) void lstm_bwd_persistent(LstmArgs a) {
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks)
     wf[ks] = *reinterpret_cast<const u16x8*>(a.whh + (long)u_mine * G + w * KQ + 32 * ks + 8 * kq);
-  constexpr int NP = (NRT * 16 * 16 + 255) / 256;
+  constexpr int NP = NRT;
   float dh[NP], dc[NP];
 #pragma unroll
   for (int r = 0; r < NP; ++r) {
     const int p = threadIdx.x + 256 * r;
-    const int b = p >> 4, u = 16 * j + (p & 15);
+    const int b = row0 + (p >> 4), u = 16 * j + (p & 15);
     dh[r] = (b < B && a.dh_last) ? a.dh_last[(long)b * H + u] : 0.f;
     dc[r] = (b < B && a.dc_last) ? a.dc_last[(long)b * H + u] : 0.f;
   }
@@ -217,9 +229,8 @@ __global__ __launch_bounds__(256) void lstm_bwd_persistent(LstmArgs a) {
 #pragma unroll
     for (int r = 0; r < NP; ++r) {
       const int p = threadIdx.x + 256 * r;
-      const int b = p >> 4, u = 16 * j + (p & 15);
+      const int b = row0 + (p >> 4), u = 16 * j + (p & 15);
       act[r] = false;
-      if (b >= BP) continue;
       u16* dg = a.dgates + ((long)t * BP + b) * G + u;
       if (b >= B) {
         dg[0] = 0; dg[H] = 0; dg[2 * H] = 0; dg[3 * H] = 0;
@@ -245,10 +256,10 @@ __global__ __launch_bounds__(256) void lstm_bwd_persistent(LstmArgs a) {
       dg[2 * H] = f2bf(dG * (1.f - gg * gg));
       dg[3 * H] = f2bf(dO * og * (1.f - og));
     }
-    rnn_arrive(a.cnt);
-    if (!rnn_wait(a.cnt, (unsigned)(gridDim.x * (steps + 1)), a.err, &abort_s)) return;
+    rnn_arrive(cnt);
+    if (!rnn_wait(cnt, (unsigned)(gridDim.x * (steps + 1)), a.err, &abort_s)) return;
     // recurrent product over this wave's K quarter
-    const u16* dgt = a.dgates + (long)t * BP * G;
+    const u16* dgt = a.dgates + ((long)t * BP + row0) * G;
     f32x4 acc[NRT];
 #pragma unroll
     for (int rt = 0; rt < NRT; ++rt) acc[rt] = {0.f, 0.f, 0.f, 0.f};
@@ -268,9 +279,9 @@ __global__ __launch_bounds__(256) void lstm_bwd_persistent(LstmArgs a) {
 #pragma unroll
     for (int r = 0; r < NP; ++r) {
       const int p = threadIdx.x + 256 * r;
-      const int b = p >> 4, nn = p & 15;
-      if (b >= B) continue;
-      if (act[r]) dh[r] = red[0][b][nn] + red[1][b][nn] + red[2][b][nn] + red[3][b][nn];
+      const int lb = p >> 4, nn = p & 15;
+      if (row0 + lb >= B) continue;
+      if (act[r]) dh[r] = red[0][lb][nn] + red[1][lb][nn] + red[2][lb][nn] + red[3][lb][nn];
       // inactive step: h_t == h_{t-1}, the gradient passes through unchanged
     }
     __syncthreads();  // red is rewritten next step
@@ -278,7 +289,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_persistent(LstmArgs a) {
 #pragma unroll
   for (int r = 0; r < NP; ++r) {
     const int p = threadIdx.x + 256 * r;
-    const int b = p >> 4, u = 16 * j + (p & 15);
+    const int b = row0 + (p >> 4), u = 16 * j + (p & 15);
     if (b >= B) continue;
     if (a.dh0) a.dh0[(long)b * H + u] = dh[r];
     if (a.dc0) a.dc0[(long)b * H + u] = dc[r];
@@ -289,7 +300,8 @@ __global__ __launch_bounds__(256) void lstm_bwd_persistent(LstmArgs a) {
 
 using namespace pa;
 
-// ws: >= 64 bytes of device scratch for {cnt, err} (zeroed here).
+// ws: >= 512 bytes of device scratch: err word + one barrier counter per row block
+// (64-B lines), zeroed here every call.
 PA_EXPORT int pa_lstm_persistent(int backward, const float* xproj, const void* whh, const int* lens, void* hbuf,
                                  float* hs, float* cs, void* gates, const float* h0, const float* c0,
                                  const float* dhs, const float* dh_last, const float* dc_last, void* dgates,
@@ -297,35 +309,273 @@ PA_EXPORT int pa_lstm_persistent(int backward, const float* xproj, const void* w
   const int KS = H / 32;
   if (H % 32 || !(KS == 4 || KS == 8 || KS == 16 || KS == 32) || B < 1 || B > 128 || T < 1)
     return (int)hipErrorInvalidValue;
-  const int NRT = B <= 16 ? 1 : B <= 32 ? 2 : B <= 64 ? 4 : 8;  // row tiles; BP = 16 NRT
-  const int BP = 16 * NRT;
+  const int NRT_ALL = B <= 16 ? 1 : B <= 32 ? 2 : B <= 64 ? 4 : 8;  // BP = 16 NRT_ALL rows
+  const int NRT = NRT_ALL < 2 ? NRT_ALL : 2;                         // rows per workgroup / 16
   LstmArgs a;
   a.xproj = xproj; a.whh = (const u16*)whh; a.lens = lens; a.hbuf = (u16*)hbuf;
   a.hs = hs; a.cs = cs; a.gates = (u16*)gates; a.h0 = h0; a.c0 = c0;
   a.dhs = dhs; a.dh_last = dh_last; a.dc_last = dc_last; a.dgates = (u16*)dgates;
   a.dh0 = dh0; a.dc0 = dc0;
-  a.cnt = ws; a.err = ws + 16;  // separate 64-B lines
-  a.T = T; a.B = B; a.BP = BP; a.H = H;
-  hipError_t e = hipMemsetAsync(ws, 0, 128, st);
+  a.err = ws; a.cnt = ws + 16;  // counters at ws[16 (1 + y)], one 64-B line each
+  a.T = T; a.B = B; a.BP = 16 * NRT_ALL; a.H = H;
+  hipError_t e = hipMemsetAsync(ws, 0, 512, st);
   if (e != hipSuccess) return (int)e;
-  const dim3 grid(H / 16), blk(256);
-#define PA_LSTM_K(NRT, K)                                                                   \
-  if (backward) hipLaunchKernelGGL((lstm_bwd_persistent<NRT, K>), grid, blk, 0, st, a);     \
-  else hipLaunchKernelGGL((lstm_fwd_persistent<NRT, K>), grid, blk, 0, st, a);
-#define PA_LSTM(NRT)                                  \
+  const dim3 grid(H / 16, NRT_ALL / NRT), blk(256);
+#define PA_LSTM_K(R, K)                                                                   \
+  if (backward) hipLaunchKernelGGL((lstm_bwd_persistent<R, K>), grid, blk, 0, st, a);     \
+  else hipLaunchKernelGGL((lstm_fwd_persistent<R, K>), grid, blk, 0, st, a);
+#define PA_LSTM(R)                                    \
   switch (KS) {                                       \
-    case 4: PA_LSTM_K(NRT, 4) break;                  \
-    case 8: PA_LSTM_K(NRT, 8) break;                  \
-    case 16: PA_LSTM_K(NRT, 16) break;                \
-    default: PA_LSTM_K(NRT, 32) break;                \
+    case 4: PA_LSTM_K(R, 4) break;                    \
+    case 8: PA_LSTM_K(R, 8) break;                    \
+    case 16: PA_LSTM_K(R, 16) break;                  \
+    default: PA_LSTM_K(R, 32) break;                  \
   }
-  switch (NRT) {
-    case 1: PA_LSTM(1) break;
-    case 2: PA_LSTM(2) break;
-    case 4: PA_LSTM(4) break;
-    default: PA_LSTM(8) break;
+  if (NRT == 1) {
+    PA_LSTM(1)
+  } else {
+    PA_LSTM(2)
   }
 #undef PA_LSTM
 #undef PA_LSTM_K
+  PA_LAUNCH_CHECK();
+}
+
+// ============================================================================
+// Attention-LSTM decoder step kernels (seq2seq, reference
+// benchmark/fluid/models/machine_translation.py: simple_attention + lstm_step).
+// The decoder loop itself is driven from ops/rnn.py (4 launches per step forward,
+// 4 backward, all graph-capturable); these fuse what would otherwise be ~15
+// elementwise / reduction kernels per step.
+// ============================================================================
+namespace pa {
+
+// score[b, s] = sum_a w[a] tanh(ep[b, s, a] + sp[b, a]) over s < len[b]; att = softmax;
+// ctx[b, :] = sum_s att[s] enc[b, s, :].  One workgroup (256) per batch row; wave per
+// source position for the scores (8 a per lane per 512-chunk), thread per 4 ctx columns.
+__global__ __launch_bounds__(1024) void add_attn_fwd(const u16* __restrict__ ep, const u16* __restrict__ sp,
+                                                      const float* __restrict__ w, const u16* __restrict__ enc,
+                                                      const int* __restrict__ lens, u16* __restrict__ ctx, long ctx_ld,
+                                                      float* __restrict__ att, int Ts, int A, int E) {
+  extern __shared__ float sm[];  // [Ts] scores -> probabilities | [4][E] ctx partials
+  float* part = sm + Ts;
+  const int b = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int L = min(lens[b], Ts);
+  for (int s = wv; s < Ts; s += 16) {
+    float acc = 0.f;
+    if (s < L) {
+      for (int a0 = 8 * lane; a0 < A; a0 += 512) {
+        float e8[8], s8[8], w8[8];
+        load8(ep + ((long)b * Ts + s) * A + a0, e8);
+        load8(sp + (long)b * A + a0, s8);
+        load8(w + a0, w8);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc += w8[k] * tanhf(e8[k] + s8[k]);
+      }
+      acc = wave_sum(acc);
+    }
+    if (lane == 0) sm[s] = s < L ? acc : -INFINITY;
+  }
+  __syncthreads();
+  if (wv == 0) {
+    float m = -INFINITY;
+    for (int s = lane; s < Ts; s += 64) m = fmaxf(m, sm[s]);
+    m = wave_max(m);
+    float z = 0.f;
+    for (int s = lane; s < Ts; s += 64) z += (sm[s] == -INFINITY) ? 0.f : __expf(sm[s] - m);
+    z = wave_sum(z);
+    const float inv = z > 0.f ? 1.f / z : 0.f;
+    for (int s = lane; s < Ts; s += 64) {
+      const float p = (sm[s] == -INFINITY) ? 0.f : __expf(sm[s] - m) * inv;
+      sm[s] = p;
+      att[(long)b * Ts + s] = p;
+    }
+  }
+  __syncthreads();
+  // ctx: 4 thread groups split the source positions (s = g mod 4), 4 columns per thread
+  const int g = threadIdx.x >> 8, tt = threadIdx.x & 255;
+  for (int e0 = 4 * tt; e0 < E; e0 += 1024) {
+    float c4[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int s = g; s < L; s += 4) {
+      const float p = sm[s];
+      const u16x4 v = *reinterpret_cast<const u16x4*>(enc + ((long)b * Ts + s) * E + e0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) c4[k] += p * bf2f(v[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) part[g * E + e0 + k] = c4[k];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < E; e += 1024)
+    ctx[(long)b * ctx_ld + e] = f2bf(part[e] + part[E + e] + part[2 * E + e] + part[3 * E + e]);
+}
+
+// Backward of add_attn_fwd for one decoder step (enc's gradient is formed once,
+// after the loop, as att^T dctx; not here):
+//   da[s] = dctx . enc[b, s, :];  de = att * (da - sum att da)
+//   dz[s, a] = de[s] w[a] (1 - tanh^2(ep + sp)):  dep_acc += dz (fp32, across steps),
+//   dsp[b, a] = sum_s dz;  dw_acc[a] += sum_{b, s} de[s] tanh(ep + sp)
+__global__ __launch_bounds__(1024) void add_attn_bwd(const u16* __restrict__ dctx, long dctx_ld,
+                                                     const float* __restrict__ att, const u16* __restrict__ ep,
+                                                     const u16* __restrict__ sp, const float* __restrict__ w,
+                                                     const u16* __restrict__ enc, const int* __restrict__ lens,
+                                                     float* __restrict__ dep_acc, u16* __restrict__ dsp,
+                                                     float* __restrict__ dw_acc, int Ts, int A, int E) {
+  extern __shared__ float sm[];  // [Ts] de | [16][A] dsp partial | [16][A] dw partial
+  float* de = sm;
+  float* pd = sm + Ts;
+  float* pw = pd + 16 * A;
+  const int b = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int L = min(lens[b], Ts);
+  // da[s] (wave per s, 8 columns per lane per 512-chunk)
+  for (int s = wv; s < Ts; s += 16) {
+    float acc = 0.f;
+    if (s < L) {
+      for (int e0 = 8 * lane; e0 < E; e0 += 512) {
+        float d8[8], x8[8];
+        load8(dctx + (long)b * dctx_ld + e0, d8);
+        load8(enc + ((long)b * Ts + s) * E + e0, x8);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc += d8[k] * x8[k];
+      }
+      acc = wave_sum(acc);
+    }
+    if (lane == 0) de[s] = acc;
+  }
+  __syncthreads();
+  if (wv == 0) {
+    float sad = 0.f;
+    for (int s = lane; s < L; s += 64) sad += att[(long)b * Ts + s] * de[s];
+    sad = wave_sum(sad);
+    for (int s = lane; s < Ts; s += 64) de[s] = s < L ? att[(long)b * Ts + s] * (de[s] - sad) : 0.f;
+  }
+  for (int i = threadIdx.x; i < 32 * A; i += 1024) pd[i] = 0.f;  // pd and pw
+  __syncthreads();
+  for (int a0 = 8 * lane; a0 < A; a0 += 512) {
+    float s8[8], w8[8], accd[8], accw[8];
+    load8(sp + (long)b * A + a0, s8);
+    load8(w + a0, w8);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) accd[k] = accw[k] = 0.f;
+    for (int s = wv; s < L; s += 16) {
+      const float d = de[s];
+      float e8[8], g8[8];
+      load8(ep + ((long)b * Ts + s) * A + a0, e8);
+      float* dp = dep_acc + ((long)b * Ts + s) * A + a0;
+      load8(dp, g8);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float t = tanhf(e8[k] + s8[k]);
+        const float dz = d * w8[k] * (1.f - t * t);
+        g8[k] += dz;
+        accd[k] += dz;
+        accw[k] += d * t;
+      }
+      store8(dp, g8);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      pd[wv * A + a0 + k] = accd[k];
+      pw[wv * A + a0 + k] = accw[k];
+    }
+  }
+  __syncthreads();
+  for (int a = threadIdx.x; a < A; a += 1024) {
+    float d = 0.f, g = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      d += pd[k * A + a];
+      g += pw[k * A + a];
+    }
+    dsp[(long)b * A + a] = f2bf(d);
+    if (g != 0.f) atomicAdd(dw_acc + a, g);
+  }
+}
+
+// gates = gp[b, :] (+ y[b, :]); i f g o; c = f c_prev + i g; h = o tanh(c).
+// Writes c (fp32), post-activation gates (bf16) and h (bf16) to up to two places.
+__global__ __launch_bounds__(256) void lstm_cell_fwd(const u16* __restrict__ gp, const float* __restrict__ y,
+                                                      const float* __restrict__ cp, float* __restrict__ c_out,
+                                                      u16* __restrict__ gates, u16* __restrict__ h1, long ld1,
+                                                      u16* __restrict__ h2, long ld2, int B, int H) {
+  const long n = (long)B * H;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / H), j = (int)(i % H);
+    const long g0 = (long)b * 4 * H + j;
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = bf2f(gp[g0 + k * H]) + (y ? y[g0 + k * H] : 0.f);
+    const float ig = 1.f / (1.f + __expf(-v[0])), fg = 1.f / (1.f + __expf(-v[1]));
+    const float gg = tanhf(v[2]), og = 1.f / (1.f + __expf(-v[3]));
+    const float c = fg * (cp ? cp[i] : 0.f) + ig * gg;
+    const float h = og * tanhf(c);
+    c_out[i] = c;
+    gates[g0] = f2bf(ig);
+    gates[g0 + H] = f2bf(fg);
+    gates[g0 + 2 * H] = f2bf(gg);
+    gates[g0 + 3 * H] = f2bf(og);
+    h1[(long)b * ld1 + j] = f2bf(h);
+    if (h2) h2[(long)b * ld2 + j] = f2bf(h);
+  }
+}
+
+// dh = dh_out (+ dh_rec, row stride ld_rec); pre-activation gate grads -> dgp (bf16);
+// dc (fp32, in place) becomes dc_prev.
+__global__ __launch_bounds__(256) void lstm_cell_bwd(const u16* __restrict__ dh_out, const u16* __restrict__ dh_rec,
+                                                      long ld_rec, float* __restrict__ dc, const u16* __restrict__ gates,
+                                                      const float* __restrict__ c, const float* __restrict__ cp,
+                                                      u16* __restrict__ dgp, int B, int H) {
+  const long n = (long)B * H;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / H), j = (int)(i % H);
+    const long g0 = (long)b * 4 * H + j;
+    const float dh = (dh_out ? bf2f(dh_out[i]) : 0.f) + (dh_rec ? bf2f(dh_rec[(long)b * ld_rec + j]) : 0.f);
+    const float ig = bf2f(gates[g0]), fg = bf2f(gates[g0 + H]), gg = bf2f(gates[g0 + 2 * H]),
+                og = bf2f(gates[g0 + 3 * H]);
+    const float tc = tanhf(c[i]);
+    const float dct = dc[i] + dh * og * (1.f - tc * tc);
+    const float cpv = cp ? cp[i] : 0.f;
+    dgp[g0] = f2bf(dct * gg * ig * (1.f - ig));
+    dgp[g0 + H] = f2bf(dct * cpv * fg * (1.f - fg));
+    dgp[g0 + 2 * H] = f2bf(dct * ig * (1.f - gg * gg));
+    dgp[g0 + 3 * H] = f2bf(dh * tc * og * (1.f - og));
+    dc[i] = dct * fg;
+  }
+}
+
+}  // namespace pa
+
+PA_EXPORT int pa_add_attn_fwd(const void* ep, const void* sp, const float* w, const void* enc, const int* lens,
+                              void* ctx, long ctx_ld, float* att, int B, int Ts, int A, int E, hipStream_t st) {
+  if (A % 512 || E % 1024 || Ts < 1 || (Ts + 4 * E) * 4 > 160 * 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(add_attn_fwd, dim3(B), dim3(1024), (Ts + 4 * E) * sizeof(float), st, (const u16*)ep, (const u16*)sp, w,
+                     (const u16*)enc, lens, (u16*)ctx, ctx_ld, att, Ts, A, E);
+  PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_add_attn_bwd(const void* dctx, long dctx_ld, const float* att, const void* ep, const void* sp,
+                              const float* w, const void* enc, const int* lens, float* dep_acc, void* dsp,
+                              float* dw_acc, int B, int Ts, int A, int E, hipStream_t st) {
+  if (A % 512 || E % 512 || Ts < 1) return (int)hipErrorInvalidValue;
+  const size_t lds = (Ts + 32 * A) * sizeof(float);
+  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(add_attn_bwd, dim3(B), dim3(1024), lds, st, (const u16*)dctx, dctx_ld, att, (const u16*)ep,
+                     (const u16*)sp, w, (const u16*)enc, lens, dep_acc, (u16*)dsp, dw_acc, Ts, A, E);
+  PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_lstm_cell_fwd(const void* gp, const float* y, const float* cp, float* c_out, void* gates, void* h1,
+                               long ld1, void* h2, long ld2, int B, int H, hipStream_t st) {
+  const int g = stream_grid((long)B * H, 256);
+  hipLaunchKernelGGL(lstm_cell_fwd, dim3(g), dim3(256), 0, st, (const u16*)gp, y, cp, c_out, (u16*)gates, (u16*)h1,
+                     ld1, (u16*)h2, ld2, B, H);
+  PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_lstm_cell_bwd(const void* dh_out, const void* dh_rec, long ld_rec, float* dc, const void* gates,
+                               const float* c, const float* cp, void* dgp, int B, int H, hipStream_t st) {
+  const int g = stream_grid((long)B * H, 256);
+  hipLaunchKernelGGL(lstm_cell_bwd, dim3(g), dim3(256), 0, st, (const u16*)dh_out, (const u16*)dh_rec, ld_rec, dc,
+                     (const u16*)gates, c, cp, (u16*)dgp, B, H);
   PA_LAUNCH_CHECK();
 }

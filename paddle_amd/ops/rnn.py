@@ -52,7 +52,7 @@ class _LstmFn(torch.autograd.Function):
         hs = torch.empty(T, B, H, dtype=torch.float32, device=dev)
         cs = torch.empty_like(hs)
         gates = torch.empty(T, B, 4 * H, dtype=torch.bfloat16, device=dev)
-        ws = torch.zeros(32, dtype=torch.int32, device=dev)
+        ws = torch.zeros(128, dtype=torch.int32, device=dev)  # err + per-row-block counters
         h0f = h0.float().contiguous() if h0 is not None else None
         c0f = c0.float().contiguous() if c0 is not None else None
         N.call("pa_lstm_persistent", 0, N.ptr(xp), N.ptr(whh), N.ptr(lens), N.ptr(hbuf), N.ptr(hs), N.ptr(cs),
@@ -153,3 +153,114 @@ def reverse_padded(x, lens, time_major=True):
     idx = torch.where(t < L, L - 1 - t, t)                       # [T, B]
     out = xt.gather(0, idx.view(T, B, *([1] * (xt.dim() - 2))).expand_as(xt))
     return out if time_major else out.transpose(0, 1)
+
+
+# ---------------------------------------------------------------- attention decoder
+class _AttnDecoderFn(torch.autograd.Function):
+    """Teacher-forced LSTM decoder with additive attention over an encoder output.
+
+    Per step t (h_{-1} = h0, c_{-1} = c0):
+        sp = h_{t-1} Wsp;  att = softmax_s(w . tanh(ep + sp)) over s < slen
+        ctx = att . enc;   gates = [ctx, h_{t-1}] Wg + Y[t];  (h_t, c_t) = LSTM cell
+    Forward = 4 launches per step (GEMM, fused attention, GEMM, fused cell); the
+    backward walks the steps in reverse with 4 launches per step and forms every
+    weight gradient (and enc's) after the loop as single large GEMMs.
+    """
+
+    @staticmethod
+    def forward(ctx_, enc, ep, lens, Y, h0, c0, Wsp, w, Wg):
+        B, Ts, E = enc.shape
+        A = ep.shape[2]
+        Tt, _, G = Y.shape
+        H = G // 4
+        dev, bf = enc.device, torch.bfloat16
+        enc_b, ep_b = enc.to(bf).contiguous(), ep.to(bf).contiguous()
+        Wsp_b, Wg_b = Wsp.detach().to(bf).contiguous(), Wg.detach().to(bf).contiguous()
+        wf = w.detach().float().contiguous()
+        Yf = Y.float().contiguous()
+        XH = torch.empty(Tt, B, E + H, dtype=bf, device=dev)      # [ctx_t, h_{t-1}]
+        XH[0, :, E:] = h0.to(bf)
+        Hs = torch.empty(Tt, B, H, dtype=bf, device=dev)
+        Cs = torch.empty(Tt, B, H, dtype=torch.float32, device=dev)
+        gates = torch.empty(Tt, B, G, dtype=bf, device=dev)
+        SP = torch.empty(Tt, B, A, dtype=bf, device=dev)
+        att = torch.empty(Tt, B, Ts, dtype=torch.float32, device=dev)
+        c0f = c0.float().contiguous()
+        st = N.stream()
+        for t in range(Tt):
+            hprev = XH[t, :, E:]
+            torch.mm(hprev, Wsp_b, out=SP[t])
+            N.call("pa_add_attn_fwd", N.ptr(ep_b), N.ptr(SP[t]), N.ptr(wf), N.ptr(enc_b), N.ptr(lens),
+                   N.ptr(XH[t]), E + H, N.ptr(att[t]), B, Ts, A, E, st)
+            gp = torch.mm(XH[t], Wg_b)
+            nxt = XH[t + 1, :, E:] if t + 1 < Tt else None
+            N.call("pa_lstm_cell_fwd", N.ptr(gp), N.ptr(Yf[t]), N.ptr(Cs[t - 1] if t else c0f), N.ptr(Cs[t]),
+                   N.ptr(gates[t]), N.ptr(Hs[t]), H, N.ptr(nxt), E + H, B, H, st)
+        ctx_.save_for_backward(enc_b, ep_b, lens, Wsp_b, wf, Wg_b, XH, Cs, gates, SP, att, c0f)
+        ctx_.dt = (enc.dtype, ep.dtype, Y.dtype, h0.dtype, c0.dtype, Wsp.dtype, w.dtype, Wg.dtype)
+        return Hs.to(Y.dtype) if Y.dtype != torch.float32 else Hs.float()
+
+    @staticmethod
+    def backward(ctx_, dHs):
+        enc_b, ep_b, lens, Wsp_b, wf, Wg_b, XH, Cs, gates, SP, att, c0f = ctx_.saved_tensors
+        d_enc, d_ep, d_Y, d_h0, d_c0, d_Wsp, d_w, d_Wg = ctx_.dt
+        Tt, B, EH = XH.shape
+        Ts, E, A = enc_b.shape[1], enc_b.shape[2], ep_b.shape[2]
+        H = EH - E
+        G = 4 * H
+        dev, bf = XH.device, torch.bfloat16
+        dHs_b = dHs.to(bf).contiguous()
+        dGP = torch.empty(Tt, B, G, dtype=bf, device=dev)
+        dSP = torch.empty(Tt, B, A, dtype=bf, device=dev)
+        dXH = torch.empty(Tt, B, E + H, dtype=bf, device=dev)          # [dctx_t, dh_{t-1} via Wg]
+        dep = torch.zeros(B, Ts, A, dtype=torch.float32, device=dev)
+        dw = torch.zeros(A, dtype=torch.float32, device=dev)
+        dc = torch.zeros(B, H, dtype=torch.float32, device=dev)
+        WgT, WspT = Wg_b.t(), Wsp_b.t()
+        st = N.stream()
+        dh_rec = None
+        for t in range(Tt - 1, -1, -1):
+            N.call("pa_lstm_cell_bwd", N.ptr(dHs_b[t]), N.ptr(dh_rec), H, N.ptr(dc), N.ptr(gates[t]),
+                   N.ptr(Cs[t]), N.ptr(Cs[t - 1] if t else c0f), N.ptr(dGP[t]), B, H, st)
+            torch.mm(dGP[t], WgT, out=dXH[t])
+            N.call("pa_add_attn_bwd", N.ptr(dXH[t]), E + H, N.ptr(att[t]), N.ptr(ep_b), N.ptr(SP[t]), N.ptr(wf),
+                   N.ptr(enc_b), N.ptr(lens), N.ptr(dep), N.ptr(dSP[t]), N.ptr(dw), B, Ts, A, E, st)
+            dh_rec = torch.addmm(dXH[t, :, E:], dSP[t], WspT)            # dh_{t-1} from this step
+        TB = Tt * B
+        dWg = torch.mm(XH.view(TB, EH).t(), dGP.view(TB, G))
+        hprev = XH[:, :, E:].reshape(TB, H)
+        dWsp = torch.mm(hprev.t(), dSP.view(TB, A))
+        # enc gradient: sum_t att_t^T dctx_t, batched over b
+        denc = torch.bmm(att.permute(1, 2, 0).to(bf), dXH[:, :, :E].permute(1, 0, 2))   # [B, Ts, E]
+        return (denc.to(d_enc), dep.to(d_ep), None, dGP.to(d_Y), dh_rec.to(d_h0), dc.to(d_c0), dWsp.to(d_Wsp),
+                dw.to(d_w), dWg.to(d_Wg))
+
+
+def attention_lstm_decoder(enc, ep, lens, Y, h0, c0, Wsp, w, Wg):
+    """enc [B, Ts, E], ep [B, Ts, A] (= enc projected), lens [B] source lengths,
+    Y [Tt, B, 4H] (target-word gate inputs incl. bias), h0/c0 [B, H],
+    Wsp [H, A], w [A], Wg [E + H, 4H].  Returns the decoder states [Tt, B, H]."""
+    B, Ts, E = enc.shape
+    A = ep.shape[2]
+    if enc.is_cuda and A % 512 == 0 and E % 1024 == 0 and (Ts + 32 * A) * 4 <= 160 * 1024 and \
+            (Ts + 4 * E) * 4 <= 160 * 1024:
+        return _AttnDecoderFn.apply(enc, ep, lens.to(device=enc.device, dtype=torch.int32), Y, h0, c0, Wsp, w, Wg)
+    return _attn_decoder_ref(enc, ep, lens, Y, h0, c0, Wsp, w, Wg)
+
+
+def _attn_decoder_ref(enc, ep, lens, Y, h0, c0, Wsp, w, Wg):
+    B, Ts, E = enc.shape
+    Tt = Y.shape[0]
+    smask = torch.arange(Ts, device=enc.device)[None] < lens.to(enc.device)[:, None]
+    h, c = h0, c0
+    out = []
+    for t in range(Tt):
+        e = torch.tanh(ep + (h @ Wsp)[:, None]) @ w
+        att = torch.softmax(e.masked_fill(~smask, float("-inf")), 1)
+        ctx = torch.bmm(att[:, None].to(enc.dtype), enc).squeeze(1)
+        g = torch.cat([ctx, h], 1) @ Wg + Y[t]
+        i, f, gg, o = g.chunk(4, 1)
+        c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+        h = torch.sigmoid(o) * torch.tanh(c)
+        out.append(h)
+    return torch.stack(out)

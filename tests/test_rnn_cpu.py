@@ -40,3 +40,19 @@ def test_reverse_padded_cpu():
     assert r[:, 0].tolist() == [9.0, 6.0, 3.0, 0.0]
     assert r[:, 1].tolist() == x[:, 1].tolist()
     assert r[:3, 2].tolist() == [8.0, 5.0, 2.0] and r[3, 2] == 11.0
+
+
+def test_attention_decoder_ref_grad_shapes():
+    torch.manual_seed(0)
+    B, Ts, E, A, H, Tt = 2, 5, 8, 6, 4, 3
+    enc = torch.randn(B, Ts, E, requires_grad=True)
+    ep = torch.randn(B, Ts, A, requires_grad=True)
+    lens = torch.tensor([5, 2])
+    Y = torch.randn(Tt, B, 4 * H, requires_grad=True)
+    h0, c0 = torch.zeros(B, H), torch.zeros(B, H)
+    Wsp, w, Wg = torch.randn(H, A), torch.randn(A), torch.randn(E + H, 4 * H)
+    out = rnn.attention_lstm_decoder(enc, ep, lens, Y, h0, c0, Wsp, w, Wg)
+    assert out.shape == (Tt, B, H)
+    out.sum().backward()
+    # masked source positions get no attention and no gradient
+    assert enc.grad[1, 2:].abs().sum() == 0 and ep.grad[1, 2:].abs().sum() == 0

@@ -76,3 +76,31 @@ def test_nn_lstm_persistent_matches_miopen(monkeypatch, direction, layers):
         assert _rel(got, ref) < 3e-2, _rel(got, ref)
     for got, ref in zip(a[4], r[4]):
         assert _rel(got, ref) < 5e-2, _rel(got, ref)
+
+
+@pytest.mark.parametrize("B,Ts,Tt", [(4, 9, 5), (32, 40, 12)])
+def test_attention_lstm_decoder_matches_reference(B, Ts, Tt):
+    """Fused attention-decoder kernels vs the plain fp32 recurrence (values + all grads)."""
+    torch.manual_seed(0)
+    E, A, H = 1024, 512, 512
+    enc = (0.5 * torch.randn(B, Ts, E, device=dev)).requires_grad_()
+    ep = (0.5 * torch.randn(B, Ts, A, device=dev)).requires_grad_()
+    lens = torch.randint(1, Ts + 1, (B,), device=dev)
+    Y = (0.5 * torch.randn(Tt, B, 4 * H, device=dev)).requires_grad_()
+    h0 = (0.5 * torch.randn(B, H, device=dev)).requires_grad_()
+    c0 = (0.5 * torch.randn(B, H, device=dev)).requires_grad_()
+    Wsp = (torch.randn(H, A, device=dev) / H ** 0.5).requires_grad_()
+    w = (torch.randn(A, device=dev) / A ** 0.5).requires_grad_()
+    Wg = (torch.randn(E + H, 4 * H, device=dev) / (E + H) ** 0.5).requires_grad_()
+    leaves = [enc, ep, Y, h0, c0, Wsp, w, Wg]
+    out = rnn.attention_lstm_decoder(enc, ep, lens, Y, h0, c0, Wsp, w, Wg)
+    ref_leaves = [t.detach().clone().requires_grad_() for t in leaves]
+    r = ref_leaves
+    ref = rnn._attn_decoder_ref(r[0], r[1], lens, r[2], r[3], r[4], r[5], r[6], r[7])
+    assert _rel(out, ref) < 2e-2, _rel(out, ref)
+    g = torch.randn_like(ref)
+    (out.float() * g).sum().backward()
+    (ref * g).sum().backward()
+    names = ["enc", "ep", "Y", "h0", "c0", "Wsp", "w", "Wg"]
+    for got, want, nm in zip(leaves, ref_leaves, names):
+        assert _rel(got.grad, want.grad) < 4e-2, (nm, _rel(got.grad, want.grad))
