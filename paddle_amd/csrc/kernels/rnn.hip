@@ -90,6 +90,7 @@ struct LstmArgs {
   const float* c0;
   // backward
   const float* dhs;     // [T, B, H] or null: gradient into every h_t output
+  const float* dcs;     // [T, B, H] or null: gradient into every c_t output
   const float* dh_last; // [B, H] or null: gradient into h[T-1]
   const float* dc_last; // [B, H] or null
   u16* dgates;          // [T, BP, 4H]
@@ -237,6 +238,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_persistent(LstmArgs a) {
         continue;
       }
       if (a.dhs) dh[r] += a.dhs[((long)t * B + b) * H + u];
+      if (a.dcs) dc[r] += a.dcs[((long)t * B + b) * H + u];
       act[r] = t < a.lens[b];
       if (!act[r]) {
         dg[0] = 0; dg[H] = 0; dg[2 * H] = 0; dg[3 * H] = 0;
@@ -304,8 +306,9 @@ using namespace pa;
 // (64-B lines), zeroed here every call.
 PA_EXPORT int pa_lstm_persistent(int backward, const float* xproj, const void* whh, const int* lens, void* hbuf,
                                  float* hs, float* cs, void* gates, const float* h0, const float* c0,
-                                 const float* dhs, const float* dh_last, const float* dc_last, void* dgates,
-                                 float* dh0, float* dc0, unsigned* ws, int T, int B, int H, hipStream_t st) {
+                                 const float* dhs, const float* dcs, const float* dh_last, const float* dc_last,
+                                 void* dgates, float* dh0, float* dc0, unsigned* ws, int T, int B, int H,
+                                 hipStream_t st) {
   const int KS = H / 32;
   if (H % 32 || !(KS == 4 || KS == 8 || KS == 16 || KS == 32) || B < 1 || B > 128 || T < 1)
     return (int)hipErrorInvalidValue;
@@ -314,7 +317,7 @@ PA_EXPORT int pa_lstm_persistent(int backward, const float* xproj, const void* w
   LstmArgs a;
   a.xproj = xproj; a.whh = (const u16*)whh; a.lens = lens; a.hbuf = (u16*)hbuf;
   a.hs = hs; a.cs = cs; a.gates = (u16*)gates; a.h0 = h0; a.c0 = c0;
-  a.dhs = dhs; a.dh_last = dh_last; a.dc_last = dc_last; a.dgates = (u16*)dgates;
+  a.dhs = dhs; a.dcs = dcs; a.dh_last = dh_last; a.dc_last = dc_last; a.dgates = (u16*)dgates;
   a.dh0 = dh0; a.dc0 = dc0;
   a.err = ws; a.cnt = ws + 16;  // counters at ws[16 (1 + y)], one 64-B line each
   a.T = T; a.B = B; a.BP = 16 * NRT_ALL; a.H = H;

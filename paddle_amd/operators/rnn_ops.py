@@ -101,6 +101,30 @@ def _lstm_core(gx, W, bias, h0, c0, D, peep, acts, idx, mask, T, proj=None, proj
     return st(hs), st(cs), st(gates), st(pre)
 
 
+def _persistent_lstm_ok(ctx, x, D, nseq):
+    import os
+
+    from ..ops import rnn as R
+
+    return (not ctx.attr("use_peepholes") and os.environ.get("PADDLE_AMD_PERSISTENT_LSTM", "1") != "0"
+            and _act(ctx.attr("gate_activation")) is torch.sigmoid and _act(ctx.attr("cell_activation")) is torch.tanh
+            and _act(ctx.attr("candidate_activation")) is torch.tanh and R.persistent_ok(x, D, nseq))
+
+
+def _lstm_persistent(gx, W, h0, c0, D, idx, mask, T):
+    """The LoD LSTM on the persistent gfx950 kernel (ops/rnn.py).  Fluid's gate
+    order {c~, i, f, o} is permuted to the kernel's {i, f, c~, o}."""
+    from ..ops import rnn as R
+
+    perm = torch.cat([torch.arange(D, 2 * D), torch.arange(2 * D, 3 * D), torch.arange(0, D),
+                      torch.arange(3 * D, 4 * D)]).to(gx.device)
+    lens = mask.sum(1).to(torch.int32)
+    xt = gx.index_select(2, perm).transpose(0, 1)            # [L, N, 4D] time-major
+    hs, _, _, cs = R.lstm(xt, None, W.index_select(1, perm), None, h0, c0, lens=lens, return_cells=True)
+    return (_scatter(hs.transpose(0, 1), idx, mask, T),       # [N, L, D] -> LoD rows
+            _scatter(cs.transpose(0, 1), idx, mask, T))
+
+
 def _lstm_attrs(extra=None):
     a = {"use_peepholes": True, "is_reverse": False, "gate_activation": "sigmoid", "cell_activation": "tanh",
          "candidate_activation": "tanh"}
@@ -125,6 +149,13 @@ def lstm(ctx):
             _act(ctx.attr("candidate_activation")))
     h0 = ctx.input("H0") if ctx.has_input("H0") else None
     c0 = ctx.input("C0") if ctx.has_input("C0") else None
+    if _persistent_lstm_ok(ctx, x, D, idx.shape[0]):
+        H, C = _lstm_persistent(gx, W, h0, c0, D, idx, mask, T)
+        ctx.set_output("Hidden", H, lod)
+        ctx.set_output("Cell", C, lod)
+        ctx.set_output("BatchGate", _scatter(gx.detach(), idx, mask, T))
+        ctx.set_output("BatchCellPreAct", C.detach())
+        return
     H, C, G, P = _lstm_core(gx, W, b, h0, c0, D, ctx.attr("use_peepholes"), acts, idx, mask, T)
     ctx.set_output("Hidden", H, lod)
     ctx.set_output("Cell", C, lod)

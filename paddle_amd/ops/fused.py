@@ -56,7 +56,8 @@ class _NormFn(torch.autograd.Function):
         hout = torch.empty_like(x2) if res is not None else None
         rstd = _ws(Nr, dev)
         mean = None if rms else _ws(Nr, dev)
-        N.call("pa_norm_fwd", N.dt(x2), int(rms), N.ptr(x2), N.ptr(_c(res).view(-1, H) if res is not None else None),
+        res2 = _c(res).view(-1, H) if res is not None else None  # referenced until the launch
+        N.call("pa_norm_fwd", N.dt(x2), int(rms), N.ptr(x2), N.ptr(res2),
                N.ptr(w), N.ptr(b), N.ptr(y), N.ptr(hout), N.ptr(mean), N.ptr(rstd), Nr, H, float(eps), N.stream())
         h = hout if res is not None else x2
         ctx.save_for_backward(h, w, mean, rstd)

@@ -40,7 +40,8 @@ class _LstmFn(torch.autograd.Function):
         H = w_hh.shape[0]
         dev = x.device
         x2 = x.reshape(T * B, I)
-        xp = torch.matmul(x2, w_ih.to(x2.dtype)).float()
+        # w_ih None: x already holds the gate pre-activations (Fluid's lstm op input)
+        xp = x2.float() if w_ih is None else torch.matmul(x2, w_ih.to(x2.dtype)).float()
         if b is not None:
             xp = xp + b.float()
         xp = xp.contiguous()
@@ -56,15 +57,15 @@ class _LstmFn(torch.autograd.Function):
         h0f = h0.float().contiguous() if h0 is not None else None
         c0f = c0.float().contiguous() if c0 is not None else None
         N.call("pa_lstm_persistent", 0, N.ptr(xp), N.ptr(whh), N.ptr(lens), N.ptr(hbuf), N.ptr(hs), N.ptr(cs),
-               N.ptr(gates), N.ptr(h0f), N.ptr(c0f), None, None, None, None, None, None, N.ptr(ws), T, B, H,
-               N.stream())
+               N.ptr(gates), N.ptr(h0f), N.ptr(c0f), None, None, None, None, None, None, None, N.ptr(ws), T, B,
+               H, N.stream())
         ctx.save_for_backward(x, lens, w_ih, whh, hs, cs, gates, h0f, c0f)
-        ctx.flags = (b is not None, h0 is not None, c0 is not None, x.dtype, w_ih.dtype)
+        ctx.flags = (b is not None, h0 is not None, c0 is not None, x.dtype, w_ih.dtype if w_ih is not None else None)
         ctx.ws = ws
-        return hs.to(x.dtype), hs[-1].clone().to(x.dtype), cs[-1].clone().to(x.dtype)
+        return hs.to(x.dtype), hs[-1].clone().to(x.dtype), cs[-1].clone().to(x.dtype), cs.to(x.dtype)
 
     @staticmethod
-    def backward(ctx, dhs, dh_last, dc_last):
+    def backward(ctx, dhs, dh_last, dc_last, dcs):
         x, lens, w_ih, whh, hs, cs, gates, h0f, c0f = ctx.saved_tensors
         has_b, has_h0, has_c0, xdt, wdt = ctx.flags
         T, B, I = x.shape
@@ -75,46 +76,55 @@ class _LstmFn(torch.autograd.Function):
         dh0 = torch.empty(B, H, dtype=torch.float32, device=dev)
         dc0 = torch.empty_like(dh0)
         f = lambda t: t.float().contiguous() if t is not None else None  # noqa: E731
+        # keep the converted gradients referenced until the launch: a temporary freed
+        # inside the argument list can be handed straight to the next conversion
+        dhs_, dcs_, dhl_, dcl_ = f(dhs), f(dcs), f(dh_last), f(dc_last)
         N.call("pa_lstm_persistent", 1, None, N.ptr(whh), N.ptr(lens), None, N.ptr(hs), N.ptr(cs), N.ptr(gates),
-               N.ptr(h0f), N.ptr(c0f), N.ptr(f(dhs)), N.ptr(f(dh_last)), N.ptr(f(dc_last)), N.ptr(dgates),
+               N.ptr(h0f), N.ptr(c0f), N.ptr(dhs_), N.ptr(dcs_), N.ptr(dhl_), N.ptr(dcl_), N.ptr(dgates),
                N.ptr(dh0), N.ptr(dc0), N.ptr(ctx.ws), T, B, H, N.stream())
         dG = dgates[:, :B].reshape(T * B, 4 * H)
         hprev = torch.empty(T, B, H, dtype=torch.bfloat16, device=dev)
         hprev[0] = h0f.to(torch.bfloat16) if h0f is not None else 0
         hprev[1:] = hs[:-1].to(torch.bfloat16)
         hp2 = hprev.reshape(T * B, H)
-        dw_hh = (torch.matmul(hp2.t().float(), dG.float()) if wdt == torch.float32 else torch.matmul(hp2.t(), dG))
+        dw_hh = (torch.matmul(hp2.t(), dG) if wdt == torch.bfloat16 else torch.matmul(hp2.t().float(), dG.float()))
         x2 = x.reshape(T * B, I)
         dGx = dG.to(x2.dtype)
-        dx = torch.matmul(dGx, w_ih.to(x2.dtype).t()).view(T, B, I) if ctx.needs_input_grad[0] else None
-        dw_ih = torch.matmul(x2.t(), dGx).to(wdt) if ctx.needs_input_grad[2] else None
+        wdt_hh = wdt if wdt is not None else xdt
+        if w_ih is None:
+            dx, dw_ih = (dGx.view(T, B, I) if ctx.needs_input_grad[0] else None), None
+        else:
+            dx = torch.matmul(dGx, w_ih.to(x2.dtype).t()).view(T, B, I) if ctx.needs_input_grad[0] else None
+            dw_ih = torch.matmul(x2.t(), dGx).to(wdt) if ctx.needs_input_grad[2] else None
         db = dG.float().sum(0) if has_b else None
-        return (dx, None, dw_ih, dw_hh.to(wdt), db, dh0.to(xdt) if has_h0 else None,
+        return (dx, None, dw_ih, dw_hh.to(wdt_hh), db, dh0.to(xdt) if has_h0 else None,
                 dc0.to(xdt) if has_c0 else None)
 
 
-def lstm(x, w_ih, w_hh, b=None, h0=None, c0=None, lens=None, time_major=True):
+def lstm(x, w_ih, w_hh, b=None, h0=None, c0=None, lens=None, time_major=True, return_cells=False):
     """Single-layer unidirectional LSTM.
 
-    x [T, B, I] (or [B, T, I] with ``time_major=False``), w_ih [I, 4H], w_hh [H, 4H],
+    x [T, B, I] (or [B, T, I] with ``time_major=False``), w_ih [I, 4H] (None: x is
+    already the [.., 4H] gate pre-activation), w_hh [H, 4H],
     b [4H] (= b_ih + b_hh), gate order (i, f, g, o); ``lens`` [B] valid lengths.
-    Returns (hs [T, B, H] (batch-major if input was), h_last [B, H], c_last [B, H]);
-    past a sequence's end its (h, c) stay frozen, so h_last is its final state.
+    Returns (hs [T, B, H] (batch-major if input was), h_last [B, H], c_last [B, H])
+    (+ cs, the cell states laid out like hs, with ``return_cells``); past a
+    sequence's end its (h, c) stay frozen, so h_last is its final state.
     """
     if not time_major:
         x = x.transpose(0, 1)
     T, B, _ = x.shape
     H = w_hh.shape[0]
     if not persistent_ok(x, H, B):
-        hs, h, c = _lstm_ref(x, w_ih, w_hh, b, h0, c0, lens)
+        hs, h, c, cs = _lstm_ref(x, w_ih, w_hh, b, h0, c0, lens, cells=True)
     else:
-        hs, h, c = _LstmFn.apply(x.contiguous(), _lens_dev(lens, T, B, x.device), w_ih, w_hh, b, h0, c0)
+        hs, h, c, cs = _LstmFn.apply(x.contiguous(), _lens_dev(lens, T, B, x.device), w_ih, w_hh, b, h0, c0)
     if not time_major:
-        hs = hs.transpose(0, 1)
-    return hs, h, c
+        hs, cs = hs.transpose(0, 1), cs.transpose(0, 1)
+    return (hs, h, c, cs) if return_cells else (hs, h, c)
 
 
-def _lstm_ref(x, w_ih, w_hh, b=None, h0=None, c0=None, lens=None):
+def _lstm_ref(x, w_ih, w_hh, b=None, h0=None, c0=None, lens=None, cells=False):
     """Plain PyTorch recurrence with the same length-freezing semantics (CPU path
     and numerics reference)."""
     T, B, _ = x.shape
@@ -122,12 +132,12 @@ def _lstm_ref(x, w_ih, w_hh, b=None, h0=None, c0=None, lens=None):
     dt = x.dtype
     h = h0.to(dt) if h0 is not None else x.new_zeros(B, H)
     c = c0.to(dt) if c0 is not None else x.new_zeros(B, H)
-    xp = x.reshape(T * B, -1) @ w_ih.to(dt)
+    xp = x.reshape(T * B, -1) if w_ih is None else x.reshape(T * B, -1) @ w_ih.to(dt)
     if b is not None:
         xp = xp + b.to(dt)
     xp = xp.view(T, B, 4 * H)
     L = lens.to(x.device) if lens is not None else None
-    out = []
+    out, cout = [], []
     for t in range(T):
         g = xp[t] + h @ w_hh.to(dt)
         i, f, gg, o = g.chunk(4, 1)
@@ -139,6 +149,9 @@ def _lstm_ref(x, w_ih, w_hh, b=None, h0=None, c0=None, lens=None):
             hn = m * hn + (1 - m) * h
         h, c = hn, cn
         out.append(h)
+        cout.append(c)
+    if cells:
+        return torch.stack(out), h, c, torch.stack(cout)
     return torch.stack(out), h, c
 
 

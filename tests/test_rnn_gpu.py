@@ -27,17 +27,18 @@ def test_lstm_persistent_matches_reference(T, B, I, H, with_state):
     c0 = (0.5 * torch.randn(B, H, device=dev)).requires_grad_() if with_state else None
     xr = x.clone().requires_grad_()
     x.requires_grad_()
-    hs, h, c = rnn.lstm(x, w_ih, w_hh, b, h0, c0, lens=lens)
+    hs, h, c, cs = rnn.lstm(x, w_ih, w_hh, b, h0, c0, lens=lens, return_cells=True)
     torch.cuda.synchronize()
     ref_leaves = [t.detach().clone().requires_grad_() if t is not None else None for t in (w_ih, w_hh, b, h0, c0)]
-    hr, hlr, clr = rnn._lstm_ref(xr, *ref_leaves, lens=lens)
+    hr, hlr, clr, csr = rnn._lstm_ref(xr, *ref_leaves, lens=lens, cells=True)
     assert _rel(hs, hr) < 2e-2, _rel(hs, hr)
-    assert _rel(h, hlr) < 2e-2 and _rel(c, clr) < 2e-2
+    assert _rel(h, hlr) < 2e-2 and _rel(c, clr) < 2e-2 and _rel(cs, csr) < 2e-2
     gh = torch.randn_like(hs)
     gl = torch.randn_like(h)
-    (hs * gh).sum().backward(retain_graph=True)
+    gc = torch.randn_like(cs)
+    ((hs * gh).sum() + (cs * gc).sum()).backward(retain_graph=True)
     (h * gl).sum().backward()
-    ((hr * gh).sum() + (hlr * gl).sum()).backward()
+    ((hr * gh).sum() + (csr * gc).sum() + (hlr * gl).sum()).backward()
     assert _rel(x.grad, xr.grad) < 3e-2, _rel(x.grad, xr.grad)
     for got, ref, name in zip((w_ih, w_hh, b, h0, c0), ref_leaves, ("w_ih", "w_hh", "b", "h0", "c0")):
         if got is not None:
@@ -104,3 +105,41 @@ def test_attention_lstm_decoder_matches_reference(B, Ts, Tt):
     names = ["enc", "ep", "Y", "h0", "c0", "Wsp", "w", "Wg"]
     for got, want, nm in zip(leaves, ref_leaves, names):
         assert _rel(got.grad, want.grad) < 4e-2, (nm, _rel(got.grad, want.grad))
+
+
+def test_fluid_dynamic_lstm_persistent_matches_generic(monkeypatch):
+    """fluid.layers.dynamic_lstm (no peepholes) on the persistent kernel vs the generic
+    per-step path of the same op: hidden, cell and parameter gradients."""
+    import numpy as np
+
+    import paddle_amd.fluid as fluid
+    from paddle_amd.framework import core
+
+    D, LOD = 128, [0, 5, 7, 15]
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PADDLE_AMD_PERSISTENT_LSTM", flag)
+        main, startup = fluid.Program(), fluid.Program()
+        main.random_seed = startup.random_seed = 4
+        with fluid.program_guard(main, startup):
+            x = fluid.layers.data(name="x", shape=[4 * D], dtype="float32", lod_level=1)
+            h, c = fluid.layers.dynamic_lstm(input=x, size=4 * D, use_peepholes=False,
+                                             param_attr=fluid.ParamAttr(name="lw"),
+                                             bias_attr=fluid.ParamAttr(name="lb"))
+            loss = fluid.layers.mean(h * h) + fluid.layers.mean(c)
+            fluid.backward.append_backward(loss)
+        exe = fluid.Executor(fluid.CUDAPlace(0))
+        xv = np.random.RandomState(0).randn(LOD[-1], 4 * D).astype("float32")
+        scope = core.Scope()
+        with fluid.executor.scope_guard(scope):
+            exe.run(startup)
+            # the device RNG is not reseeded per program: pin the parameters
+            g = torch.Generator().manual_seed(1)
+            for name, scale in (("lw", D ** -0.5), ("lb", 0.1)):
+                t = scope.find_var(name).get()
+                t.set_tensor((scale * torch.randn(t.tensor.shape, generator=g)).to(t.tensor.device))
+            res[flag] = exe.run(main, feed={"x": core.LoDTensor(torch.from_numpy(xv), [LOD])},
+                                fetch_list=[h, c, "lw@GRAD", "lb@GRAD"])
+    errs = [_rel(torch.as_tensor(np.asarray(got)), torch.as_tensor(np.asarray(ref)))
+            for got, ref in zip(res["1"], res["0"])]
+    assert max(errs) < 3e-2, dict(zip(["hidden", "cell", "dW", "db"], errs))
