@@ -157,12 +157,12 @@ def bench_stacked_lstm_dygraph(a, dev):
            "vs_baseline": round(v / BASE["stacked_lstm"], 2), "loss": float(loss.detach())})
 
 
-def bench_stacked_lstm_fluid(a, dev):
+def stacked_lstm_program(V=5147, E=512, Hs=512):
+    """The reference benchmark program (benchmark/fluid/models/stacked_dynamic_lstm.py):
+    embedding -> fc tanh -> DynamicRNN LSTM written with fc/sums/elementwise ops ->
+    sequence_pool last -> fc softmax -> cross entropy, Adam."""
     import paddle_amd.fluid as fluid
-    from paddle_amd.framework import core
 
-    V, E, Hs = 5147, 512, 512
-    B = a.batch or 32
     main, startup = fluid.Program(), fluid.Program()
     main.random_seed = startup.random_seed = 1
     with fluid.program_guard(main, startup):
@@ -192,6 +192,16 @@ def bench_stacked_lstm_fluid(a, dev):
         logit = fluid.layers.fc(input=last, size=2, act="softmax")
         loss = fluid.layers.mean(fluid.layers.cross_entropy(input=logit, label=label))
         fluid.optimizer.Adam(learning_rate=1e-3).minimize(loss)
+    return main, startup, loss
+
+
+def bench_stacked_lstm_fluid(a, dev):
+    import paddle_amd.fluid as fluid
+    from paddle_amd.framework import core
+
+    V, E, Hs = 5147, 512, 512
+    B = a.batch or 32
+    main, startup, loss = stacked_lstm_program(V, E, Hs)
     place = fluid.CUDAPlace(0) if dev.type == "cuda" else fluid.CPUPlace()
     exe = fluid.Executor(place)
     scope = core.Scope()

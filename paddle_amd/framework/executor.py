@@ -59,7 +59,12 @@ class BlockExecutor:
             if v.persistable:
                 root.var(v.name)
             else:
-                scope.var(v.name)
+                var = scope.var(v.name)
+                # temporaries start every run empty (the reference drops its local scope
+                # after each Run): a tensor array left from the previous batch would
+                # otherwise be appended to / accumulated into with stale shapes
+                if isinstance(var.get(), core.LoDTensorArray):
+                    var.set(core.LoDTensorArray())
 
     def run_block(self, program, block_idx, scope, create_vars=True):
         pb = self.prepare(program, block_idx)

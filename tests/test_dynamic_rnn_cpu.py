@@ -97,3 +97,27 @@ def test_dynamic_rnn_trains():
                                                    "y": core.LoDTensor(torch.from_numpy(yv), [LOD])},
                                        fetch_list=[loss])[0]).reshape(-1)[0]) for _ in range(30)]
     assert ls[-1] < 0.5 * ls[0], ls
+
+
+def test_dynamic_rnn_consecutive_batches_same_scope():
+    """Batches of different length profiles run back to back in one scope (the
+    reference's stacked_dynamic_lstm benchmark loop): tensor arrays and their
+    gradients must not carry over from the previous run."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "benchmarks"))
+    import reference_suite as rs
+
+    main, startup, loss = rs.stacked_lstm_program(50, 8, 8)
+    exe = fluid.Executor(fluid.CPUPlace())
+    with fluid.executor.scope_guard(core.Scope()):
+        exe.run(startup)
+        for seed in range(3):
+            lens = np.random.RandomState(seed).randint(1, 25, 6).tolist()
+            off = np.concatenate([[0], np.cumsum(lens)]).tolist()
+            ids = torch.randint(0, 50, (off[-1], 1))
+            lab = torch.randint(0, 2, (len(lens), 1))
+            (lv,) = exe.run(main, feed={"words": core.LoDTensor(ids, [off]), "label": core.LoDTensor(lab)},
+                            fetch_list=[loss])
+            assert np.isfinite(np.asarray(lv)).all()
