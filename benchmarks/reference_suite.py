@@ -195,13 +195,34 @@ def stacked_lstm_program(V=5147, E=512, Hs=512):
     return main, startup, loss
 
 
-def bench_stacked_lstm_fluid(a, dev):
+def stacked_lstm_op_program(V=5147, E=512, Hs=512):
+    """The same network with the recurrence as ONE Fluid op: fc -> dynamic_lstm (the
+    reference's lstm op, no peepholes) instead of a DynamicRNN of fc/sums ops."""
+    import paddle_amd.fluid as fluid
+
+    main, startup = fluid.Program(), fluid.Program()
+    main.random_seed = startup.random_seed = 1
+    with fluid.program_guard(main, startup):
+        words = fluid.layers.data(name="words", shape=[1], lod_level=1, dtype="int64")
+        label = fluid.layers.data(name="label", shape=[1], dtype="int64")
+        sent = fluid.layers.embedding(input=words, size=[V, E])
+        sent = fluid.layers.fc(input=sent, size=Hs, act="tanh")
+        proj = fluid.layers.fc(input=sent, size=4 * Hs)
+        hidden, _ = fluid.layers.dynamic_lstm(input=proj, size=4 * Hs, use_peepholes=False)
+        last = fluid.layers.sequence_pool(hidden, "last")
+        logit = fluid.layers.fc(input=last, size=2, act="softmax")
+        loss = fluid.layers.mean(fluid.layers.cross_entropy(input=logit, label=label))
+        fluid.optimizer.Adam(learning_rate=1e-3).minimize(loss)
+    return main, startup, loss
+
+
+def bench_stacked_lstm_fluid(a, dev, lstm_op=False):
     import paddle_amd.fluid as fluid
     from paddle_amd.framework import core
 
     V, E, Hs = 5147, 512, 512
     B = a.batch or 32
-    main, startup, loss = stacked_lstm_program(V, E, Hs)
+    main, startup, loss = (stacked_lstm_op_program if lstm_op else stacked_lstm_program)(V, E, Hs)
     place = fluid.CUDAPlace(0) if dev.type == "cuda" else fluid.CPUPlace()
     exe = fluid.Executor(place)
     scope = core.Scope()
@@ -227,7 +248,9 @@ def bench_stacked_lstm_fluid(a, dev):
         dt, out = _timeit(step, a.steps, a.warmup)
     avg = float(np.mean([f[1] for f in feeds]))
     v = B / dt
-    _emit({"bench": "stacked_lstm_train", "impl": "fluid DynamicRNN program (executor)", "value": round(v, 1),
+    impl = ("fluid program, dynamic_lstm op (persistent kernel)" if lstm_op
+            else "fluid DynamicRNN program of fc/sums ops (op-by-op executor)")
+    _emit({"bench": "stacked_lstm_train", "impl": impl, "value": round(v, 1),
            "unit": "samples/s", "words_per_s": round(v * avg, 1), "avg_len": round(avg, 1), "batch": B,
            "dtype": "fp32", "ms_per_step": round(dt * 1e3, 2), "baseline": BASE["stacked_lstm"],
            "vs_baseline": round(v / BASE["stacked_lstm"], 2)})
@@ -400,7 +423,7 @@ def bench_infer(a, dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("which", nargs="+", choices=["vgg16", "stacked_lstm", "seq2seq", "infer"])
-    ap.add_argument("--impl", default="both", choices=["both", "dygraph", "fluid"])
+    ap.add_argument("--impl", default="both", choices=["both", "dygraph", "fluid", "fluid_lstm_op"])
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
@@ -416,7 +439,9 @@ def main():
         elif w == "stacked_lstm":
             if a.impl in ("both", "dygraph"):
                 bench_stacked_lstm_dygraph(a, dev)
-            if a.impl in ("both", "fluid"):
+            if a.impl in ("both", "fluid_lstm_op"):
+                bench_stacked_lstm_fluid(a, dev, lstm_op=True)
+            if a.impl == "fluid":
                 bench_stacked_lstm_fluid(a, dev)
         elif w == "seq2seq":
             bench_seq2seq(a, dev)

@@ -34,6 +34,20 @@ class PreparedBlock:
             ins = [(slot, list(names)) for slot, names in op.inputs.items()]
             outs = {slot: list(names) for slot, names in op.outputs.items()}
             self.steps.append((info, op, ins, outs, attrs))
+        # forward ops whose auto-VJP grad op is in this program keep their graph
+        # (registry.run_kernel_stash) so backward does not re-run them
+        grads = _program_grad_types(program)
+        self.stash = [FLAGS.get("stash_forward") and (op.type + "_grad") in grads
+                      and R.is_auto_grad(op.type + "_grad") for _, op, _, _, _ in self.steps]
+
+
+def _program_grad_types(program):
+    cached = getattr(program, "_pa_grad_types", None)
+    if cached is not None and cached[0] == program._version:
+        return cached[1]
+    types = {op.type for blk in program.blocks for op in blk.ops if op.type.endswith("_grad")}
+    program._pa_grad_types = (program._version, types)
+    return types
 
 
 class BlockExecutor:
@@ -67,6 +81,8 @@ class BlockExecutor:
                     var.set(core.LoDTensorArray())
 
     def run_block(self, program, block_idx, scope, create_vars=True):
+        if block_idx == 0 and create_vars:
+            R.clear_stash()  # graphs of a previous run whose grads never ran
         pb = self.prepare(program, block_idx)
         if create_vars:
             self.create_variables(program, scope, block_idx)
@@ -77,7 +93,7 @@ class BlockExecutor:
         bench = FLAGS.get("benchmark")
         profiling = prof.is_enabled()
         place = self.place
-        for info, op, ins, outs, attrs in pb.steps:
+        for k, (info, op, ins, outs, attrs) in enumerate(pb.steps):
             ctx_ins = {}
             for slot, names in ins:
                 vals = []
@@ -86,11 +102,12 @@ class BlockExecutor:
                     vals.append(var.get() if var is not None else None)
                 ctx_ins[slot] = vals
             ctx = R.KernelContext(op.type, ctx_ins, outs, attrs, place, scope, op, self)
+            run = R.run_kernel_stash if pb.stash[k] else R.run_kernel
             if profiling:
                 with prof.RecordEvent(op.type):
-                    R.run_kernel(info, ctx)
+                    run(info, ctx)
             else:
-                R.run_kernel(info, ctx)
+                run(info, ctx)
             for slot, vals in ctx.results.items():
                 names = outs.get(slot, [])
                 for n, v in zip(names, vals):

@@ -313,10 +313,117 @@ def _make_auto_grad_info(fwd_type):
     return info
 
 
+# Forward graphs kept for the auto-VJP grad ops of a training program: the forward
+# op runs once under autograd (BlockExecutor marks the ops whose grads are auto
+# and present in the program) and its grad op takes the VJP of the stashed graph
+# instead of re-running the forward kernel.  Keyed by id() of every output tensor
+# the forward op stored in the scope; cleared at the start of every top-level run.
+_STASH: dict = {}
+
+
+def clear_stash():
+    _STASH.clear()
+
+
+def is_auto_grad(grad_type):
+    """True when ``grad_type`` is served by auto_grad_kernel (not a hand-written grad)."""
+    if not grad_type.endswith("_grad"):
+        return False
+    try:
+        info = get_op_info(grad_type)
+    except Exception:  # noqa: BLE001
+        return False
+    return _AUTO_GRAD.get(grad_type[:-5]) is info
+
+
+def run_kernel_stash(info: OpInfo, ctx: KernelContext):
+    """Run a forward kernel with its float inputs as autograd leaves, keep the
+    graph for the grad op, hand detached outputs to the scope."""
+    op = ctx.op
+    inplace = set()
+    if op is not None:
+        outs_names = {n for names in op.outputs.values() for n in names}
+        inplace = {n for names in op.inputs.values() for n in names if n in outs_names}
+    leaves = {}
+    for s in info.inputs:
+        vals = ctx.ins.get(s.name) or []
+        names = op.input(s.name) if op is not None else []
+        new = []
+        for i, v in enumerate(vals):
+            n = names[i] if i < len(names) else None
+            if isinstance(v, core.LoDTensor) and v.tensor is not None and v.tensor.is_floating_point() \
+                    and n not in inplace:
+                t = v.tensor.detach().requires_grad_(True)
+                leaves[(s.name, i)] = t
+                new.append(core.LoDTensor(t, v.lod()))
+            else:
+                new.append(v)
+        ctx.ins[s.name] = new
+    with torch.enable_grad():
+        info.kernel(ctx)
+    if info.share_lod:
+        _default_share_lod(info, ctx)
+    graph_outs = {}
+    for slot, vals in ctx.results.items():
+        for i, r in enumerate(vals):
+            rt = r.tensor if isinstance(r, core.LoDTensor) else r
+            if isinstance(rt, torch.Tensor) and rt.requires_grad:
+                graph_outs[(slot, i)] = rt
+                d = rt.detach()
+                vals[i] = core.LoDTensor(d, r.lod()) if isinstance(r, core.LoDTensor) else d
+    if graph_outs and leaves:
+        entry = (leaves, graph_outs)
+        for (slot, i) in graph_outs:
+            r = ctx.results[slot][i]
+            _STASH[id(r.tensor if isinstance(r, core.LoDTensor) else r)] = entry
+    return ctx.results
+
+
+def _stashed_vjp(fwd: OpInfo, ctx: KernelContext):
+    entry = None
+    for s in fwd.outputs:
+        for v in ctx.input_values(s.name):
+            t = v.tensor if isinstance(v, core.LoDTensor) else v
+            if isinstance(t, torch.Tensor) and id(t) in _STASH:
+                entry = _STASH[id(t)]
+                break
+        if entry is not None:
+            break
+    if entry is None:
+        return None
+    leaves, graph_outs = entry
+    for (slot, i), rt in graph_outs.items():
+        vals = ctx.input_values(slot)
+        if i < len(vals):
+            t = vals[i].tensor if isinstance(vals[i], core.LoDTensor) else vals[i]
+            _STASH.pop(id(t), None)
+    outs, gouts = [], []
+    for (slot, i), rt in graph_outs.items():
+        gvals = ctx.input_values(slot + GRAD_SUFFIX)
+        if i >= len(gvals) or gvals[i] is None:
+            continue
+        gt = gvals[i].tensor if isinstance(gvals[i], core.LoDTensor) else gvals[i]
+        if gt is None:
+            continue
+        outs.append(rt)
+        gouts.append(gt.to(rt.dtype).reshape(rt.shape))
+    keys = list(leaves.keys())
+    if outs and keys:
+        grads = torch.autograd.grad(outs, [leaves[k] for k in keys], gouts, allow_unused=True)
+    else:
+        grads = [None] * len(keys)
+    return dict(zip(keys, grads))
+
+
 def auto_grad_kernel(fwd: OpInfo, ctx: KernelContext):
-    """Gradient of any registered forward kernel: re-run it under autograd on leaf
-    copies of the float inputs and take the vector-Jacobian product with the
-    incoming output gradients (replaces per-op GradOpMaker + grad kernel pairs)."""
+    """Gradient of any registered forward kernel: the VJP of the forward graph the
+    executor stashed, or else re-run the forward under autograd on leaf copies of
+    the float inputs and take the vector-Jacobian product with the incoming output
+    gradients (replaces per-op GradOpMaker + grad kernel pairs)."""
+    gmap = _stashed_vjp(fwd, ctx)
+    if gmap is not None:
+        _write_input_grads(fwd, ctx, gmap)
+        return
     leaves = {}
     fins = {}
     for s in fwd.inputs:
@@ -352,7 +459,10 @@ def auto_grad_kernel(fwd: OpInfo, ctx: KernelContext):
         grads = torch.autograd.grad(outs, [leaves[k] for k in keys], gouts, allow_unused=True)
     else:
         grads = [None] * len(keys)
-    gmap = dict(zip(keys, grads))
+    _write_input_grads(fwd, ctx, dict(zip(keys, grads)))
+
+
+def _write_input_grads(fwd, ctx, gmap):
     for s in fwd.inputs:
         slot = s.name + GRAD_SUFFIX
         if not ctx.has_output(slot):

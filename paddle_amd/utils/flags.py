@@ -16,6 +16,7 @@ _DEFAULTS = {
     "init_allocated_mem": False,
     "free_idle_memory": False,
     "benchmark": False,
+    "stash_forward": True,  # keep forward autograd graphs for auto-VJP grad ops (no forward re-run)
     "eager_delete_scope": True,
     "check_nan_inf": False,
     "use_mkldnn": False,
