@@ -258,7 +258,7 @@ struct BwdParams {
   const float* lse;  // [B, Hq, Sq]
   float* delta;      // [B, Hq, Sq]
   float* dq_acc;     // [B, Sq, Hq, D] fp32
-  float* dq_part;    // v4: per-key-block dQ partials [nkb, B, Hq, Sq, D] fp32 (or null)
+  float* dq_part;    // v4: per-key-block dQ partials [nkb, B, Hq, Sq, D] bf16 bits (or null)
   u16 *dk, *dv;      // [B, Sk, Hq, D] (expanded per q-head for GQA)
   long q_bs, q_ss, q_hs, k_bs, k_ss, k_hs, v_bs, v_ss, v_hs, o_bs, o_ss, o_hs, do_bs, do_ss, do_hs;
   long dk_bs, dk_ss, dk_hs;
@@ -868,9 +868,11 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
   // PARTIAL (v4): plain stores of this key block's partial into its own [Sq][D] slab
   // (HBM store rate, ~6 TB/s) instead of fp32 atomics (~1.3 TB/s chip-wide, which
   // bound v2/v3: 16 KB of adds per 128x32 tile); fa_bwd_dq_reduce sums the slabs.
+  // slabs are bf16: each partial is an fp32 sum over 128 keys rounded once; the
+  // reduce adds <= Sk/128 of them in fp32 (halves the slab store + reduce traffic)
   const auto part_rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(PARTIAL ? p.dq_part + (((long)kt * p.B + b) * p.Hq + h) * (long)p.Sq * D : nullptr), 0,
-      PARTIAL ? p.Sq * D * 4 : 0, 0x00020000);
+      (void*)(PARTIAL ? (u16*)p.dq_part + (((long)kt * p.B + b) * p.Hq + h) * (long)p.Sq * D : nullptr), 0,
+      PARTIAL ? p.Sq * D * 2 : 0, 0x00020000);
   auto flush_dq = [&](long qt_prev, const f32x4 (&dq_prev)[2]) {
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -878,10 +880,11 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
       for (int i = 0; i < 4; ++i) {
         const long q = qt_prev + 16 * t + 4 * g + i;
         if (PARTIAL) {
-          const int poff = (int)(unsigned)((q * D + 16 * w + li) * 4);
+          const int poff = (int)(unsigned)((q * D + 16 * w + li) * 2);
           // (__builtin_bit_cast of an ext_vector element miscompiles to element 0 on this
           // toolchain: go through a scalar)
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dq_prev[t][i]), part_rs, poff, 0, 0);
+          const float v = dq_prev[t][i];
+          __builtin_amdgcn_raw_buffer_store_b16(f2bf(v), part_rs, poff, 0, 0);
         } else {
           const int voff = (int)(unsigned)((q * dq_rstride + 16 * w + li) * 4);
           __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(dq_prev[t][i], dq_rs, voff, 0, 0);
@@ -1022,15 +1025,16 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_reduce(BwdParams p, int nkb) {
   const long offs = CAUSAL ? (long)p.Sk - p.Sq : 0;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   const long slab = (long)p.B * p.Hq * p.Sq * D;
-  const float* src = p.dq_part + ((long)b * p.Hq + h) * p.Sq * D + q * D + 4 * d4;
+  const u16* src = (const u16*)p.dq_part + ((long)b * p.Hq + h) * p.Sq * D + q * D + 4 * d4;
   for (int kb = 0; kb < nkb; ++kb) {
     if (CAUSAL) {
       long qs = 128L * kb - offs;
       qs = qs > 0 ? (qs / 32) * 32 : 0;
       if (qs > q) break;
     }
-    const f32x4 v = *reinterpret_cast<const f32x4*>(src + kb * slab);
-    acc += v;
+    const u16x4 v = *reinterpret_cast<const u16x4*>(src + kb * slab);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] += bf2f(v[k]);
   }
   *reinterpret_cast<f32x4*>(p.dq_acc + (((long)b * p.Sq + q) * p.Hq + h) * D + 4 * d4) = acc;
 }
@@ -1055,7 +1059,7 @@ __global__ __launch_bounds__(256) void fa_dq_reduce_rope(const float* __restrict
   const int h = (int)(bh % Hq), b = (int)(bh / Hq);
   const long offs = CAUSAL ? (long)Sk - Sq : 0;
   const long slab = (long)B * Hq * Sq * D;
-  const float* src = part + (bh * Sq + q) * D + 4 * c;
+  const u16* src = (const u16*)part + (bh * Sq + q) * D + 4 * c;
   f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
   for (int kb = 0; kb < nkb; ++kb) {
     if (CAUSAL) {
@@ -1063,8 +1067,13 @@ __global__ __launch_bounds__(256) void fa_dq_reduce_rope(const float* __restrict
       qs = qs > 0 ? (qs / 32) * 32 : 0;
       if (qs > q) break;
     }
-    lo += *reinterpret_cast<const f32x4*>(src + kb * slab);
-    hi += *reinterpret_cast<const f32x4*>(src + kb * slab + HALF);
+    const u16x4 vl = *reinterpret_cast<const u16x4*>(src + kb * slab);
+    const u16x4 vh = *reinterpret_cast<const u16x4*>(src + kb * slab + HALF);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      lo[k] += bf2f(vl[k]);
+      hi[k] += bf2f(vh[k]);
+    }
   }
   const f32x4 co = *reinterpret_cast<const f32x4*>(cosT + q * HALF + 4 * c);
   const f32x4 si = *reinterpret_cast<const f32x4*>(sinT + q * HALF + 4 * c);

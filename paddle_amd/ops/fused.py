@@ -193,7 +193,7 @@ def _fa_bwd(q, k, v, o, do, lse, causal, scale, dk, dv, dq_rope_out=None):
     nkb = (Sk + 127) // 128
     if D == 128 and causal and N.lib().pa_fa_bwd_get_variant() == 4:
         # per-key-block dQ partial slabs (plain stores) summed by a reduce kernel
-        part = torch.empty(nkb, B, Hq, Sq, D, dtype=torch.float32, device=q.device)
+        part = torch.empty(nkb, B, Hq, Sq, D, dtype=torch.bfloat16, device=q.device)
     fused = part is not None and dq_rope_out is not None
     dq_acc = None if fused else torch.empty(B, Sq, Hq, D, dtype=torch.float32, device=q.device)
     N.call("pa_flash_attn_bwd", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(o), N.ptr(do), N.ptr(lse),
