@@ -13,6 +13,9 @@ Differences from the reference, MI355X-first:
 """
 from __future__ import annotations
 
+import contextlib
+import threading
+
 import torch
 
 from ..utils import flags as FLAGS
@@ -39,6 +42,22 @@ class PreparedBlock:
         grads = _program_grad_types(program)
         self.stash = [FLAGS.get("stash_forward") and (op.type + "_grad") in grads
                       and R.is_auto_grad(op.type + "_grad") for _, op, _, _, _ in self.steps]
+
+
+_TLS = threading.local()
+
+
+@contextlib.contextmanager
+def no_stash():
+    """Run nested blocks without detaching stashed outputs: an op whose kernel
+    executes a sub-block (recurrent, parallel_do) is differentiated as a whole by
+    its auto-VJP, which needs the autograd graph through the inner ops."""
+    prev = getattr(_TLS, "off", False)
+    _TLS.off = True
+    try:
+        yield
+    finally:
+        _TLS.off = prev
 
 
 def _program_grad_types(program):
@@ -93,6 +112,7 @@ class BlockExecutor:
         bench = FLAGS.get("benchmark")
         profiling = prof.is_enabled()
         place = self.place
+        stash = pb.stash if not getattr(_TLS, "off", False) else [False] * len(pb.steps)
         for k, (info, op, ins, outs, attrs) in enumerate(pb.steps):
             ctx_ins = {}
             for slot, names in ins:
@@ -102,7 +122,7 @@ class BlockExecutor:
                     vals.append(var.get() if var is not None else None)
                 ctx_ins[slot] = vals
             ctx = R.KernelContext(op.type, ctx_ins, outs, attrs, place, scope, op, self)
-            run = R.run_kernel_stash if pb.stash[k] else R.run_kernel
+            run = R.run_kernel_stash if stash[k] else R.run_kernel
             if profiling:
                 with prof.RecordEvent(op.type):
                     run(info, ctx)
