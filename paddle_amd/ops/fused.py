@@ -314,8 +314,9 @@ def rope_attention(qkv, cos, sin, num_heads, num_kv_heads=None, causal=True, sca
     D = W // (num_heads + 2 * Hk)
     if scale is None:
         scale = 1.0 / math.sqrt(D)
-    if qkv.is_cuda:
+    if qkv.is_cuda and qkv.dtype == torch.bfloat16 and D in (64, 128):
         return _RopeAttnFn.apply(qkv, cos, sin, num_heads, Hk, D, causal, scale)
+    # other dtypes / head sizes: plain rotary + attention (the kernels are bf16)
     x = qkv.view(B, S, num_heads + 2 * Hk, D)
     q = _rope_ref(x[:, :, :num_heads], cos, sin)
     k = _rope_ref(x[:, :, num_heads:num_heads + Hk], cos, sin)

@@ -55,3 +55,24 @@ def test_ernie_moe_fp8_experts_train_step():
         opt.zero_grad()
         losses.append(loss.item())
     assert losses[-1] < losses[0]
+
+
+def test_llama_fp32_on_gpu_matches_cpu():
+    """fp32 LLaMA on the device (kernels are bf16: fp32 takes the plain rotary +
+    attention path) against the same model on the CPU."""
+    from paddle_amd.models.llama import LLAMA_CONFIGS, LlamaConfig, LlamaForCausalLM
+
+    torch.manual_seed(0)
+    cfg = LlamaConfig(**LLAMA_CONFIGS["llama-tiny"], dtype="float32")
+    cpu = LlamaForCausalLM(cfg, device="cpu")
+    gpu = LlamaForCausalLM(cfg, device="cuda")
+    gpu.load_state_dict({k: v.cuda() for k, v in cpu.state_dict().items()})
+    ids = torch.randint(0, cfg.vocab_size, (2, 33))
+    lc = cpu(ids[:, :-1], ids[:, 1:])
+    lg = gpu(ids[:, :-1].cuda(), ids[:, 1:].cuda())
+    lc.backward()
+    lg.backward()
+    assert torch.isfinite(lg) and abs(lc.item() - lg.item()) < 1e-3, (lc.item(), lg.item())
+    for (n, pc), pg in zip(cpu.named_parameters(), gpu.parameters()):
+        rel = ((pg.grad.cpu() - pc.grad).norm() / (pc.grad.norm() + 1e-12)).item()
+        assert rel < 1e-2, (n, rel)
