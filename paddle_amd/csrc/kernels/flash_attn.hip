@@ -93,9 +93,10 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdParams p) {
   constexpr int NCH = BN * KCH / 256;     // chunks per thread per tile
   constexpr int KS = D / 16;              // k-steps over head dim
   constexpr int DB = D / 32;              // 32-wide d blocks of O^T
-  __shared__ __attribute__((aligned(16))) char smem[2 * BN * D * 2];
-  char* Ks = smem;
-  char* Vs = smem + BN * D * 2;
+  // two K|V stages: tile t+1 is stored into the other stage while tile t is
+  // consumed, so one barrier per tile orders both the reads and the stores
+  constexpr int STG = 2 * BN * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
   const int h = blockIdx.x, b = blockIdx.y;
@@ -144,7 +145,9 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdParams p) {
       }
     }
   };
-  auto store_lds = [&]() {
+  auto store_lds = [&](int stage) {
+    char* Ks = smem + stage * STG;
+    char* Vs = Ks + BN * D * 2;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int idx = tid + 256 * i, row = idx / KCH, ch = idx % KCH;
@@ -155,7 +158,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdParams p) {
 
   if (nt > 0) {
     load_regs(0);
-    store_lds();
+    store_lds(0);
   }
   __syncthreads();
 
@@ -164,52 +167,70 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdParams p) {
 
   for (int t = 0; t < nt; ++t) {
     if (t + 1 < nt) load_regs(t + 1);
+    const char* Ks = smem + (t & 1) * STG;
+    const char* Vs = Ks + BN * D * 2;
     const long kv0 = (long)t * BN;
     const bool skip = CAUSAL && (kv0 > qw + 31 + offs);
     if (!skip) {
       f32x16 s[2];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
+      for (int c = 0; c < 2; ++c)
 #pragma unroll
         for (int e = 0; e < 16; ++e) s[c][e] = 0.f;
+      // the two key halves are independent accumulator chains: interleave them so
+      // consecutive MFMAs never wait on each other's result
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
+      for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
           const u16x8 kf = *reinterpret_cast<const u16x8*>(Ks + k_off<D>(32 * c + r, 2 * ks + hh));
           s[c] = mfma32(as_bf8(kf), qf[ks], s[c]);
         }
       }
       const bool need_mask = (kv0 + BN > p.Sk) || (CAUSAL && (kv0 + BN - 1 > qw + offs));
+      // max over raw scores (scale > 0 commutes with max); the log2e*scale factor is
+      // folded into one fma per element; raw v_exp_f32 (no denormal fix-up path)
       float tmax = -INFINITY;
+      if (need_mask) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const long kv = kv0 + 32 * c + (e & 3) + 8 * (e >> 2) + 4 * hh;
+            if (kv >= p.Sk || (CAUSAL && kv > qrow + offs)) s[c][e] = -INFINITY;
+          }
+      }
 #pragma unroll
       for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          float x = s[c][e] * p.scale_log2;
-          if (need_mask) {
-            const long kv = kv0 + 32 * c + (e & 3) + 8 * (e >> 2) + 4 * hh;
-            if (kv >= p.Sk || (CAUSAL && kv > qrow + offs)) x = -INFINITY;
-          }
-          s[c][e] = x;
-          tmax = fmaxf(tmax, x);
-        }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mnew = fmaxf(m, tmax);
-      const float alpha = exp2f(m - mnew);
-      m = mnew;
+        for (int e = 0; e < 16; ++e) tmax = fmaxf(tmax, s[c][e]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * p.scale_log2;
+      // lazy rescaling: keep a stale running max unless some row's max grew by more
+      // than 2^8 (exp2 values stay <= 256, safe in fp32 sums and bf16 P); the O
+      // rescale then runs on a small fraction of tiles
+      float alpha = 1.f;
+      if (__any(tmax > m + 8.f)) {
+        const float mnew = fmaxf(m, tmax);
+        alpha = __builtin_amdgcn_exp2f(m - mnew);
+        m = mnew;
+      }
+      const float mnew = m;
       float ps = 0.f;
 #pragma unroll
       for (int c = 0; c < 2; ++c)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const float pv = exp2f(s[c][e] - mnew);
+          const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[c][e], p.scale_log2, -mnew));
           s[c][e] = pv;
           ps += pv;
         }
       lsum = lsum * alpha + ps;
+      if (__any(alpha != 1.f)) {
 #pragma unroll
-      for (int i = 0; i < DB; ++i)
+        for (int i = 0; i < DB; ++i)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) oacc[i][e] *= alpha;
+          for (int e = 0; e < 16; ++e) oacc[i][e] *= alpha;
+      }
       // O^T += V^T P^T over 4 k-steps of 16 kv
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
@@ -225,11 +246,10 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdParams p) {
         }
       }
     }
+    // stage (t+1)&1 was last read in iteration t-1, which every wave finished
+    // before the barrier that closed it
+    if (t + 1 < nt) store_lds((t + 1) & 1);
     __syncthreads();
-    if (t + 1 < nt) {
-      store_lds();
-      __syncthreads();
-    }
   }
 
   const float ltot = lsum + __shfl_xor(lsum, 32, 64);
