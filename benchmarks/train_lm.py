@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--recompute", action="store_true")
     ap.add_argument("--fp8-experts", action="store_true")
     ap.add_argument("--bucket-mb", type=int, default=512)
+    ap.add_argument("--accum", type=int, default=1, help="gradient accumulation micro-steps per optimizer step")
     a = ap.parse_args()
 
     from paddle_amd.parallel import comm
@@ -69,26 +70,35 @@ def main():
     ids = torch.randint(0, V, (a.micro_batch, a.seq_len + 1), device=dev, generator=g)
 
     def step():
-        loss = model(ids[:, :-1], ids[:, 1:])
-        loss.backward()
+        # Fleet accumulate_steps: gradient sync only on the last micro-step
+        for m in range(a.accum):
+            if m < a.accum - 1:
+                with opt.no_sync():
+                    loss = model(ids[:, :-1], ids[:, 1:]) / a.accum
+                    loss.backward()
+            else:
+                loss = model(ids[:, :-1], ids[:, 1:]) / a.accum
+                loss.backward()
         opt.step()
         opt.zero_grad()
         return loss
 
+    hist = []
     for _ in range(a.warmup):
-        step()
+        hist.append(step().detach())
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss = step()
+        hist.append(loss.detach())
     torch.cuda.synchronize()
     comm.barrier()
     dt = torch.tensor([time.perf_counter() - t0], device=dev)
     if world > 1:
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     sec = dt.item() / a.steps
-    tok = a.micro_batch * a.seq_len * world / sec
+    tok = a.accum * a.micro_batch * a.seq_len * world / sec
     if rank == 0:
         print(json.dumps({"metric": f"tokens/sec (whole job) {a.model} training", "value": round(tok, 1),
                           "unit": "tokens/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -96,9 +106,10 @@ def main():
                                                                                     else ""),
                           "data": "synthetic", "mfu_bf16_dense": round(tok * fpt / world / 2.5e15, 4),
                           "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
-                          "config": {"model": a.model, "micro_batch": a.micro_batch, "seq_len": a.seq_len,
+                          "config": {"model": a.model, "micro_batch": a.micro_batch, "grad_accum": a.accum, "seq_len": a.seq_len,
                                      "recompute": a.recompute, "parallelism": f"dp{world}+sharding_stage1"},
-                          "loss": float(loss)}))
+                          "loss": float(loss) * a.accum,
+                          "losses": [round(float(x) * a.accum, 4) for x in hist]}))
 
 
 if __name__ == "__main__":

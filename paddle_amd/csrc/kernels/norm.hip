@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(
 // Each block owns a contiguous range of rows; waves take rows round-robin.  The
 // row's h and dy stay in VGPRs in their storage dtype (packed bf16 = 4 VGPRs per
 // 8 elements); gamma is re-read from L1 each row.  dgamma/dbeta accumulate in
-// registers (MAXV <= 8) or directly in LDS (wider rows) to stay spill-free.
+// registers; rows wider than 4096 are split over two waves (WPR) to keep that.
 template <typename T> struct Raw8;
 template <> struct Raw8<u16> {
   u16x8 v;
@@ -105,16 +105,22 @@ template <> struct Raw8<float> {
   __device__ __forceinline__ float operator[](int j) const { return j < 4 ? a[j] : b[j - 4]; }
 };
 
-template <typename T, int MAXV, bool RMS, bool HAS_DRES>
+template <typename T, int MAXV, bool RMS, bool HAS_DRES, int WPR>
 __global__ __launch_bounds__(256) void norm_bwd_kernel(
     const T* __restrict__ dy, const T* __restrict__ h, const T* __restrict__ w,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const T* __restrict__ dres, T* __restrict__ dx, float* __restrict__ dw_part,
     float* __restrict__ db_part, long N, int H, long rows_per_block) {
+  // WPR waves share one row (WPR = 2 for 4096 < H <= 8192): every lane then holds
+  // at most 8 x 8 elements, so dgamma/dbeta stay in registers instead of per-row
+  // LDS atomics (8-way bank-conflicted with the 8-float lane stride).
   constexpr bool ACC_REG = MAXV <= 8;
   constexpr int AV = ACC_REG ? MAXV : 1;
-  extern __shared__ __attribute__((aligned(16))) float sm[];  // [2*H] dw, db
+  constexpr int RPI = 4 / WPR;  // rows in flight per block iteration
+  extern __shared__ __attribute__((aligned(16))) float sm[];  // [2*H] dw, db; [8] row partials
+  float* xred = sm + 2 * H;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int tir = (wv % WPR) * 64 + lane, rg = wv / WPR;
   for (int i = threadIdx.x; i < 2 * H; i += 256) sm[i] = 0.f;
   __syncthreads();
   float aw[AV][8], ab[AV][8];
@@ -124,15 +130,19 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
     for (int j = 0; j < 8; ++j) { aw[k][j] = 0.f; ab[k][j] = 0.f; }
   const long r0 = (long)blockIdx.x * rows_per_block;
   const long r1 = min(N, r0 + rows_per_block);
-  for (long row = r0 + wv; row < r1; row += 4) {
-    const float rstd = rstd_in[row];
-    const float mean = RMS ? 0.f : mean_in[row];
+  // block-uniform trip count: the WPR > 1 exchange below has a barrier
+  const long iters = (r1 - r0 + RPI - 1) / RPI;
+  for (long it = 0; it < iters; ++it) {
+    const long row = r0 + it * RPI + rg;
+    const bool live = row < r1;
+    const float rstd = live ? rstd_in[row] : 0.f;
+    const float mean = (RMS || !live) ? 0.f : mean_in[row];
     Raw8<T> hx[MAXV], dd[MAXV];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
-      const int c = (k * 64 + lane) * 8;
-      if (c < H) {
+      const int c = (k * 64 * WPR + tir) * 8;
+      if (live && c < H) {
         hx[k].load(h + row * H + c);
         dd[k].load(dy + row * H + c);
         float g[8];
@@ -153,12 +163,23 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
         }
       }
     }
-    s2 = wave_sum(s2) / H;
-    if (!RMS) s1 = wave_sum(s1) / H;
+    s2 = wave_sum(s2);
+    if (!RMS) s1 = wave_sum(s1);
+    if (WPR > 1) {
+      if (lane == 0) { xred[wv * 2] = s1; xred[wv * 2 + 1] = s2; }
+      __syncthreads();
+      float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int q = 0; q < WPR; ++q) { t1 += xred[(rg * WPR + q) * 2]; t2 += xred[(rg * WPR + q) * 2 + 1]; }
+      s1 = t1; s2 = t2;
+      __syncthreads();  // xred is rewritten next iteration
+    }
+    s2 /= H;
+    s1 /= H;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
-      const int c = (k * 64 + lane) * 8;
-      if (c < H) {
+      const int c = (k * 64 * WPR + tir) * 8;
+      if (live && c < H) {
         float o[8], g[8];
         load8(w + c, g);
 #pragma unroll
@@ -179,7 +200,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
   if (ACC_REG) {
 #pragma unroll
     for (int k = 0; k < AV; ++k) {
-      const int c = (k * 64 + lane) * 8;
+      const int c = (k * 64 * WPR + tir) * 8;
       if (c < H) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -241,11 +262,14 @@ static int launch_bwd(bool rms, const void* dy, const void* h, const void* w, co
   G = (int)((N + rpb - 1) / rpb);
   float* dwp = ws;
   float* dbp = ws + (long)G * H;
-  size_t shm = 2 * H * sizeof(float);
+  size_t shm = (2 * H + 8) * sizeof(float);
+  // rows wider than 4096 elements: two waves per row, 8 vectors per lane
+  constexpr int WPR = MAXV > 8 ? 2 : 1;
+  constexpr int MV = MAXV > 8 ? MAXV / 2 : MAXV;
   const T *DY = (const T*)dy, *Hh = (const T*)h, *W = (const T*)w, *DR = (const T*)dres;
   T* DX = (T*)dx;
 #define PA_NB(RMS_, DRES_) \
-  hipLaunchKernelGGL((norm_bwd_kernel<T, MAXV, RMS_, DRES_>), dim3(G), dim3(256), shm, st, DY, Hh, W, mean, rstd, DR, DX, dwp, dbp, N, H, rpb)
+  hipLaunchKernelGGL((norm_bwd_kernel<T, MV, RMS_, DRES_, WPR>), dim3(G), dim3(256), shm, st, DY, Hh, W, mean, rstd, DR, DX, dwp, dbp, N, H, rpb)
   if (rms) { if (dres) PA_NB(true, true); else PA_NB(true, false); }
   else { if (dres) PA_NB(false, true); else PA_NB(false, false); }
 #undef PA_NB

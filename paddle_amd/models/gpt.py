@@ -19,7 +19,6 @@ import math
 from dataclasses import dataclass
 
 import torch
-import torch.nn.functional as F
 
 from .. import ops
 from ..nn import Layer
@@ -95,9 +94,12 @@ class GPTDecoderLayer(Layer):
             for n in ("qkv_w", "qkv_b", "out_w", "fc1_w", "fc1_b", "fc2_w"):
                 getattr(self, n).is_distributed = True
 
-    def _row_bias(self, y, b):
-        # bias of a row-parallel GEMM is added once, after the all-reduce
-        return y + b
+    def _row_linear(self, x, w, b):
+        # bias of a row-parallel GEMM is added once, after the all-reduce; without
+        # TP it rides the GEMM epilogue
+        if not self.tp:
+            return ops.linear(x, w, b)
+        return self.tp.reduce_from_region(ops.linear(x, w)) + b
 
     def forward(self, x, residual=None):
         cfg, eps = self.cfg, self.cfg.layer_norm_eps
@@ -108,21 +110,14 @@ class GPTDecoderLayer(Layer):
             y, h = ops.layer_norm(x, self.ln1_w, self.ln1_b, eps, residual=residual)
         if self.tp:
             y = self.tp.copy_to_region(y)
-        B, S, _ = y.shape
-        D = cfg.head_dim
-        qkv = ops.linear(y, self.qkv_w, self.qkv_b).view(B, S, 3, self.nh, D)
-        a = ops.flash_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=True)
-        a = ops.linear(a.reshape(B, S, self.nh * D), self.out_w)
-        if self.tp:
-            a = self.tp.reduce_from_region(a)
-        a = self._row_bias(a, self.out_b)
+        # packed q|k|v straight into the attention kernel; dqkv comes back packed
+        a = ops.packed_attention(ops.linear(y, self.qkv_w, self.qkv_b), self.nh, causal=True)
+        a = self._row_linear(a, self.out_w, self.out_b)
         y2, h2 = ops.layer_norm(a, self.ln2_w, self.ln2_b, eps, residual=h)
         if self.tp:
             y2 = self.tp.copy_to_region(y2)
-        m = ops.linear(F.gelu(ops.linear(y2, self.fc1_w, self.fc1_b), approximate="tanh"), self.fc2_w)
-        if self.tp:
-            m = self.tp.reduce_from_region(m)
-        return self._row_bias(m, self.fc2_b), h2
+        m = self._row_linear(ops.linear_gelu(y2, self.fc1_w, self.fc1_b), self.fc2_w, self.fc2_b)
+        return m, h2
 
 
 class GPTEmbeddings(Layer):

@@ -33,6 +33,9 @@ _SIGS = {
     "pa_norm_bwd": [_I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
     "pa_rope": [_I, _I, _P, _L, _P, _L, _P, _P, _P, _L, _L, _I, _I, _I, _I, _P],
     "pa_swiglu_fwd": [_I, _P, _P, _L, _I, _P],
+    "pa_gelu_fwd": [_I, _P, _P, _L, _P],
+    "pa_bias_grad_blocks": [_L, _I],
+    "pa_bias_act_bwd": [_I, _I, _P, _P, _P, _P, _P, _L, _I, _P],
     "pa_swiglu_bwd": [_I, _P, _P, _P, _L, _I, _P],
     "pa_embedding_fwd": [_I, _P, _P, _P, _L, _I, _L, _P],
     "pa_embedding_bwd": [_I, _P, _P, _P, _L, _I, _L, _P],

@@ -12,6 +12,7 @@ from __future__ import annotations
 import math
 
 import torch
+import torch.nn.functional as F
 
 from . import _native as N
 
@@ -324,6 +325,68 @@ def rope_attention(qkv, cos, sin, num_heads, num_kv_heads=None, causal=True, sca
     return _attn_ref(q, k, v, causal, scale).reshape(B, S, num_heads * D)
 
 
+_IDENT_ROPE = {}
+
+
+def _identity_rope(S, D, device):
+    """cos = 1, sin = 0 tables: lets the no-rotary path reuse the fused dQ
+    slab-reduce + bf16 store into the packed gradient (``pa_fa_dq_reduce_rope``)."""
+    key = (S, D, str(device))
+    t = _IDENT_ROPE.get(key)
+    if t is None:
+        t = (torch.ones(S, D // 2, dtype=torch.float32, device=device),
+             torch.zeros(S, D // 2, dtype=torch.float32, device=device))
+        _IDENT_ROPE[key] = t
+    return t
+
+
+class _PackedAttnFn(torch.autograd.Function):
+    """Causal flash attention straight off a packed [B, S, 3*H*D] QKV projection
+    (GPT / ERNIE layout q|k|v): the kernel reads strided q/k/v views of the GEMM
+    output (no split copies), backward writes dq/dk/dv into one packed dqkv --
+    instead of autograd's three zero-filled select-backward buffers and two adds."""
+
+    @staticmethod
+    def forward(ctx, qkv, H, D, causal, scale):
+        B, S, W = qkv.shape
+        qkv = _c(qkv)
+        p4 = qkv.view(B, S, 3 * H, D)
+        o, lse = _fa_fwd(p4[:, :, :H], p4[:, :, H:2 * H], p4[:, :, 2 * H:], causal, scale)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.cfg = (H, D, causal, scale)
+        return o.view(B, S, H * D)
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        H, D, causal, scale = ctx.cfg
+        B, S, W = qkv.shape
+        p4 = qkv.view(B, S, 3 * H, D)
+        do = _c(do).view(B, S, H, D)
+        dqkv = torch.empty_like(qkv)
+        d4 = dqkv.view(B, S, 3 * H, D)
+        cos, sin = _identity_rope(S, D, qkv.device)
+        dq_acc = _fa_bwd(p4[:, :, :H], p4[:, :, H:2 * H], p4[:, :, 2 * H:], o, do, lse, causal, scale,
+                         d4[:, :, H:2 * H], d4[:, :, 2 * H:], (dqkv, W, cos, sin))
+        if dq_acc is not None:
+            N.call("pa_rope", 0, 1, N.ptr(dq_acc), H * D, N.ptr(dqkv), W, N.ptr(cos), N.ptr(sin), None,
+                   B, S, H, H, D, 1, N.stream())
+        return dqkv, None, None, None, None
+
+
+def packed_attention(qkv, num_heads, causal=True, scale=None):
+    """Flash attention on a packed [B, S, 3*H*D] (q|k|v) tensor; returns [B, S, H*D]."""
+    B, S, W = qkv.shape
+    D = W // (3 * num_heads)
+    if scale is None:
+        scale = 1.0 / math.sqrt(D)
+    if qkv.is_cuda and qkv.dtype == torch.bfloat16 and D in (64, 128):
+        return _PackedAttnFn.apply(qkv, num_heads, D, causal, scale)
+    x = qkv.view(B, S, 3 * num_heads, D)
+    q, k, v = x[:, :, :num_heads], x[:, :, num_heads:2 * num_heads], x[:, :, 2 * num_heads:]
+    return _attn_ref(q, k, v, causal, scale).reshape(B, S, num_heads * D)
+
+
 def apply_rotary(x, cos, sin, inverse=False):
     """Rotate [B, S, H, D] (neox convention)."""
     if x.is_cuda:
@@ -557,6 +620,62 @@ def _weight_t(w, tokens):
 # ====================================================================== linear
 
 
+def _bias_act_bwd(dy2, z2=None):
+    """(dZ, db) for Z = XW + b [-> gelu]: ``pa_bias_act_bwd`` computes dZ = dY * gelu'(Z)
+    (if ``z2``) and the bias gradient in one pass over dY; returns dZ = dY without z2."""
+    Nr, H = dy2.shape
+    G = int(N.lib().pa_bias_grad_blocks(Nr, H))
+    part = _ws(G * H, dy2.device)
+    db = torch.empty(H, dtype=dy2.dtype, device=dy2.device)
+    dz = torch.empty_like(dy2) if z2 is not None else dy2
+    N.call("pa_bias_act_bwd", N.dt(dy2), int(z2 is not None), N.ptr(dy2), N.ptr(z2),
+           N.ptr(dz) if z2 is not None else None, N.ptr(db), N.ptr(part), Nr, H, N.stream())
+    return dz, db
+
+
+def _fast_bias_ok(t):
+    return t.is_cuda and t.dtype in (torch.bfloat16, torch.float32) and t.shape[-1] % 8 == 0
+
+
+def _gelu_tanh(z):
+    if _fast_bias_ok(z) and z.is_contiguous():
+        g = torch.empty_like(z)
+        N.call("pa_gelu_fwd", N.dt(z), N.ptr(z), N.ptr(g), z.numel(), N.stream())
+        return g
+    return F.gelu(z, approximate="tanh")
+
+
+def _linear_fwd(x, w, b):
+    """x W (+ b); a 1-D bias rides the GEMM epilogue (addmm) instead of a separate add."""
+    wt = _weight_t(w, x.numel() // max(x.shape[-1], 1))
+    wm = wt.t() if wt is not None else w
+    if b is None:
+        return torch.matmul(x, wm)
+    x2 = x.reshape(-1, x.shape[-1])
+    return torch.addmm(b, x2, wm).view(*x.shape[:-1], wm.shape[-1])
+
+
+def _linear_bwd(ctx, x, w, dy, need_dx, need_dw):
+    dx = torch.matmul(dy, w.t()) if need_dx else None
+    dw = None
+    dy2 = dy.reshape(-1, dy.shape[-1])
+    if need_dw:
+        x2 = x.reshape(-1, x.shape[-1])
+        mg = getattr(w, "_pa_main_grad", None)
+        if _dw_nt_ok(x2, dy2):
+            # X^T materialised token-inner, dY as is: the "NN" form, which measured
+            # faster than both TN and (X^T, dY^T) NT once the dY transpose is paid
+            xa, dyb = transpose2d(_c(x2)), dy2
+        else:
+            xa, dyb = x2.t(), dy2
+        if mg is not None:
+            # the engine's post-accumulate hook still fires for w (grad None)
+            mg.addmm_(xa, dyb)
+        else:
+            dw = torch.matmul(xa, dyb)
+    return dx, dw
+
+
 class _LinearFn(torch.autograd.Function):
     """y = x W (+ b) with W in Paddle's [in, out] layout.
 
@@ -564,15 +683,13 @@ class _LinearFn(torch.autograd.Function):
     owned by the sharded DP engine), the weight-gradient GEMM accumulates straight
     into it (hipBLASLt beta=1: dW += x^T dy, one rounding); the engine's
     post-accumulate-grad hook still fires for w, so bucket readiness is unchanged
-    -- no temporary dW, no separate accumulate kernel.
+    -- no temporary dW, no separate accumulate kernel.  The bias is added in the
+    GEMM epilogue and its gradient is one HIP column reduction (``pa_bias_act_bwd``).
     """
 
     @staticmethod
     def forward(ctx, x, w, b):
-        wt = _weight_t(w, x.numel() // max(x.shape[-1], 1))
-        y = torch.matmul(x, wt.t()) if wt is not None else torch.matmul(x, w)
-        if b is not None:
-            y = y + b
+        y = _linear_fwd(x, w, b)
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
         return y
@@ -580,26 +697,53 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        dx = torch.matmul(dy, w.t()) if ctx.needs_input_grad[0] else None
-        dw = db = None
-        dy2 = dy.reshape(-1, dy.shape[-1])
-        if ctx.needs_input_grad[1]:
-            x2 = x.reshape(-1, x.shape[-1])
-            mg = getattr(w, "_pa_main_grad", None)
-            if _dw_nt_ok(x2, dy2):
-                # X^T materialised token-inner, dY as is: the "NN" form, which measured
-                # faster than both TN and (X^T, dY^T) NT once the dY transpose is paid
-                xa, dyb = transpose2d(_c(x2)), dy2
-            else:
-                xa, dyb = x2.t(), dy2
-            if mg is not None:
-                # the engine's post-accumulate hook still fires for w (grad None)
-                mg.addmm_(xa, dyb)
-            else:
-                dw = torch.matmul(xa, dyb)
+        dx, dw = _linear_bwd(ctx, x, w, dy, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        db = None
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = dy2.sum(0).to(dy.dtype)
+            dy2 = dy.reshape(-1, dy.shape[-1])
+            if _fast_bias_ok(dy2):
+                _, db = _bias_act_bwd(_c(dy2))
+            else:
+                db = dy2.sum(0).to(dy.dtype)
         return dx, dw, db
+
+
+class _LinearGeluFn(torch.autograd.Function):
+    """g = gelu_tanh(x W + b): bias in the GEMM epilogue, GELU in one HIP pass;
+    backward computes dZ = dG * gelu'(Z) and db together (``pa_bias_act_bwd``),
+    then the dX / dW GEMMs consume dZ."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        z = _linear_fwd(x, w, b)
+        g = _gelu_tanh(z)
+        ctx.save_for_backward(x, w, z)
+        return g
+
+    @staticmethod
+    def backward(ctx, dg):
+        x, w, z = ctx.saved_tensors
+        H = z.shape[-1]
+        dg2 = _c(dg).reshape(-1, H)
+        z2 = z.reshape(-1, H)
+        if _fast_bias_ok(dg2) and dg2.dtype == z2.dtype:
+            dz2, db = _bias_act_bwd(dg2, _c(z2))
+        else:
+            with torch.enable_grad():
+                zz = z2.detach().requires_grad_(True)
+                gg = F.gelu(zz, approximate="tanh")
+            dz2, = torch.autograd.grad(gg, zz, dg2)
+            db = dz2.sum(0).to(dg.dtype)
+        dz = dz2.view(z.shape)
+        dx, dw = _linear_bwd(ctx, x, w, dz, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        return dx, dw, (db if ctx.needs_input_grad[2] else None)
+
+
+def linear_gelu(x, weight, bias):
+    """gelu(x W + b, approximate='tanh') as one fused autograd node."""
+    param_ready(weight)
+    param_ready(bias)
+    return _LinearGeluFn.apply(x, weight, bias)
 
 
 def linear(x, weight, bias=None):

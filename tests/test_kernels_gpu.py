@@ -74,6 +74,54 @@ def test_layer_norm(dtype):
         assert _rel(a.grad, b_.grad) < tol
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("H", [5120, 8192, 4104])
+def test_layer_norm_wide_rows(dtype, H):
+    # 4096 < H <= 8192 takes the two-waves-per-row backward (WPR = 2); odd row count
+    # leaves the last block iteration half-populated
+    torch.manual_seed(0)
+    Nr = 301
+    x = torch.randn(Nr, H, device=dev, dtype=dtype, requires_grad=True)
+    r = torch.randn(Nr, H, device=dev, dtype=dtype, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(H, device=dev, dtype=dtype)).requires_grad_()
+    b = (0.1 * torch.randn(H, device=dev, dtype=dtype)).requires_grad_()
+    y, h = F.layer_norm(x, w, b, 1e-5, residual=r)
+    (y.float().pow(2).sum() + (h.float() * 0.5).sum()).backward()
+    xr, rr, wr, br = (t.detach().float().requires_grad_() for t in (x, r, w, b))
+    hr = xr + rr
+    yr = torch.nn.functional.layer_norm(hr, (H,), wr, br, 1e-5)
+    (yr.pow(2).sum() + (hr * 0.5).sum()).backward()
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    assert _rel(y, yr) < tol
+    for a, b_ in ((x, xr), (r, rr), (w, wr), (b, br)):
+        assert _rel(a.grad, b_.grad) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("Nr,K,M", [(2048, 512, 5120), (77, 256, 1000)])
+def test_linear_bias_and_gelu(dtype, Nr, K, M):
+    # bias in the GEMM epilogue; db (and dZ = dG * gelu'(Z)) from pa_bias_act_bwd
+    torch.manual_seed(0)
+    x = torch.randn(Nr, K, device=dev, dtype=dtype, requires_grad=True)
+    w = (torch.randn(K, M, device=dev, dtype=dtype) / math.sqrt(K)).requires_grad_()
+    b = torch.randn(M, device=dev, dtype=dtype).requires_grad_()
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    for fused in (F.linear, F.linear_gelu):
+        for t in (x, w, b):
+            t.grad = None
+        y = fused(x, w, b)
+        gy = torch.randn_like(y.float())
+        (y.float() * gy).sum().backward()
+        xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+        yr = xr @ wr + br
+        if fused is F.linear_gelu:
+            yr = torch.nn.functional.gelu(yr, approximate="tanh")
+        (yr * gy).sum().backward()
+        assert _rel(y, yr) < tol
+        for a, b_ in ((x, xr), (w, wr), (b, br)):
+            assert _rel(a.grad, b_.grad) < tol, fused.__name__
+
+
 def test_swiglu():
     torch.manual_seed(0)
     gu = torch.randn(513, 2 * 1376, device=dev, dtype=torch.bfloat16, requires_grad=True)
@@ -186,6 +234,28 @@ def test_rope_attention_packed(S, H, Hk):
     assert _rel(g[:, :, :H], gr[:, :, :H]) < 2e-2, "dq"
     assert _rel(g[:, :, H:H + Hk], gr[:, :, H:H + Hk]) < 2e-2, "dk"
     assert _rel(g[:, :, H + Hk:], gr[:, :, H + Hk:]) < 2e-2, "dv"
+
+
+@pytest.mark.parametrize("S,H,D,causal", [(256, 4, 128, True), (320, 2, 128, True), (256, 4, 64, True),
+                                          (256, 4, 128, False)])
+def test_packed_attention(S, H, D, causal):
+    # GPT layout q|k|v, no rotary; causal D = 128 goes through the fused slab
+    # reduce with identity cos/sin tables, the rest through the fp32 dQ accumulator
+    torch.manual_seed(0)
+    B = 2
+    qkv = torch.randn(B, S, 3 * H * D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    o = F.packed_attention(qkv, H, causal=causal)
+    do = torch.randn_like(o)
+    o.backward(do)
+    xr = qkv.detach().float().requires_grad_()
+    x4 = xr.view(B, S, 3 * H, D)
+    orf = F._attn_ref(x4[:, :, :H], x4[:, :, H:2 * H], x4[:, :, 2 * H:], causal,
+                      1 / math.sqrt(D)).reshape(B, S, H * D)
+    orf.backward(do.float())
+    assert _rel(o, orf) < 1e-2
+    g, gr = qkv.grad.view(B, S, 3, H * D), xr.grad.view(B, S, 3, H * D)
+    for i, n in enumerate(("dq", "dk", "dv")):
+        assert _rel(g[:, :, i], gr[:, :, i]) < 2e-2, n
 
 
 def test_adamw_flat():

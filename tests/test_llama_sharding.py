@@ -83,3 +83,34 @@ def test_sharded_dp_matches_single_process(overlap_allgather):
     for a, b in zip(losses, ref_losses):
         assert abs(a - b) < 1e-4, (losses, ref_losses)
     assert_adam_close(params, ref_params, atol=1e-5, rtol=1e-4, lr=1e-3, steps=steps)
+
+
+def _worker_accum(rank, world, steps, accum):
+    # Fleet accumulate_steps: `accum` micro-batches per optimizer step, the first
+    # accum-1 under no_sync (no reduce-scatter), the last one syncing the sum
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(_cfg(), device="cpu")
+    opt = FlatShardedOptimizer(m.named_parameters(), lr=1e-3, grad_clip=1.0, bucket_mb=1)
+    for b in _batches(steps):
+        mbs = b.chunk(world)[rank].chunk(accum)
+        for i, mb in enumerate(mbs):
+            if i < accum - 1:
+                with opt.no_sync():
+                    (m(mb[:, :-1], mb[:, 1:]) / accum).backward()
+            else:
+                (m(mb[:, :-1], mb[:, 1:]) / accum).backward()
+        opt.step()
+        opt.zero_grad()
+    opt.sync_params()
+    return torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_grad_accumulation_matches_full_batch(world):
+    steps = 3
+    _, ref_params = _train_single(steps)
+    if world == 1:
+        params = _worker_accum(0, 1, steps, 2)
+    else:
+        params = run_dist(_worker_accum, 2, steps, 2)[0]
+    assert_adam_close(params, ref_params, atol=1e-5, rtol=1e-4, lr=1e-3, steps=steps)
