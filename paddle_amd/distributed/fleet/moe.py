@@ -72,8 +72,12 @@ class MoELayer(Layer):
         super().__init__("moe_layer")
         self.group = group
         self.ep = comm.get_world_size(group)
-        self.experts = torch.nn.ModuleList(experts)
-        self.n_local = len(experts)
+        # either a list of per-expert layers (one GEMM chain each) or one grouped
+        # module exposing ``forward_grouped(x_sorted, counts)`` (all local experts in
+        # one batched GEMM per projection)
+        self.grouped = hasattr(experts, "forward_grouped")
+        self.experts = experts if self.grouped else torch.nn.ModuleList(experts)
+        self.n_local = experts.num_experts if self.grouped else len(experts)
         self.num_experts = self.n_local * self.ep
         self.gate = gate or TopKGate(d_model, self.num_experts, top_k, gate_type, capacity_factor)
         self.top_k = self.gate.top_k
@@ -120,13 +124,19 @@ class MoELayer(Layer):
             chunks = list(recv.split(per))
             by_expert = [torch.cat([chunks[p * self.n_local + e] for p in range(self.ep)])
                          for e in range(self.n_local)]
-            outs = [self.experts[e](by_expert[e]) if by_expert[e].shape[0] else by_expert[e]
-                    for e in range(self.n_local)]
             # back to peer-major order
             sizes = [[int(recv_mat[p, e]) for p in range(self.ep)] for e in range(self.n_local)]
+            if self.grouped:
+                outs = list(self.experts.forward_grouped(torch.cat(by_expert),
+                                                         [sum(sz) for sz in sizes]).split([sum(sz) for sz in sizes]))
+            else:
+                outs = [self.experts[e](by_expert[e]) if by_expert[e].shape[0] else by_expert[e]
+                        for e in range(self.n_local)]
             split_out = [list(o.split(s)) for o, s in zip(outs, sizes)]
             back = torch.cat([split_out[e][p] for p in range(self.ep) for e in range(self.n_local)])
             y_sorted = all_to_all(back, out_splits, in_splits, self.group)
+        elif self.grouped:
+            y_sorted = self.experts.forward_grouped(send, counts.tolist())
         else:
             parts = list(send.split(counts.tolist()))
             y_sorted = torch.cat([self.experts[e](parts[e]) if parts[e].shape[0] else parts[e]
