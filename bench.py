@@ -12,16 +12,24 @@ all-gather of bf16 params) -- Paddle fleet `dp_degree=N, sharding stage 1`.
 The timed region contains the full step: forward, backward, gradient
 reduce-scatter, fused AdamW on the shard, parameter all-gather.
 Data: synthetic random token ids; weights: random init (no network here).
+
+``--gpus N`` outside a launcher (no WORLD_SIZE in the env) makes this process a
+pure parent: it never touches the GPU, starts ``torch.distributed.run`` with N
+ranks on 127.0.0.1 as a CHILD process and exits with its code.  Every rank
+asserts WORLD_SIZE == --gpus, so a scaling point can never silently be a 1-GPU
+number.  ``--device cpu`` (gloo) is the debug mode the CPU tests use.
+Gradients are accumulated and reduce-scattered in fp32 (Fleet ``main_grad``);
+``--bf16-grads`` restores the round-1 bf16 gradient buffer.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
@@ -31,6 +39,26 @@ METRIC = "tokens/sec (whole node) LLaMA-7B Fleet hybrid-parallel at 1/2/4/8 MI35
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _self_launch(args, argv) -> int:
+    """Parent of an N-rank run: no GPU call happens in this process (it does not
+    even import torch); the ranks are a child ``torch.distributed.run``."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(args.master_port or _free_port()),
+           os.path.abspath(__file__)] + argv
+    log(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}")
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -49,20 +77,39 @@ def main():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-tuned-gemm", action="store_true",
                     help="use hipBLASLt's heuristic GEMM pick instead of the stored tuned solutions")
-    args = ap.parse_args()
+    ap.add_argument("--bf16-grads", action="store_true",
+                    help="accumulate / reduce-scatter gradients in bf16 instead of fp32 main_grad")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu = gloo debug mode for tests (tiny models only)")
+    ap.add_argument("--master-port", type=int, default=0)
+    argv = sys.argv[1:]
+    args = ap.parse_args(argv)
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_self_launch(args, argv))
+
+    import torch
 
     from paddle_amd.models.llama import LLAMA_CONFIGS, LlamaConfig, LlamaForCausalLM, llama_flops_per_token
     from paddle_amd.parallel import comm
     from paddle_amd.parallel.sharding import FlatShardedOptimizer
 
     rank, world, local = comm.env_rank_world()
+    if world != args.gpus:
+        raise SystemExit(f"[bench] rank {rank}: WORLD_SIZE={world} but --gpus {args.gpus}")
+    cuda = args.device == "cuda"
     if world > 1:
-        comm.init_parallel_env("nccl")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    torch.manual_seed(1234 + rank)
+        comm.init_parallel_env("nccl" if cuda else "gloo")
+        log(f"[bench] {'RCCL' if cuda else 'gloo'} world={world} rank={rank} local={local}")
+    if cuda:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+    sync = torch.cuda.synchronize if cuda else (lambda *a: None)
+    torch.manual_seed(1234)  # identical init on every rank (DP replicas)
     tuned = False
-    if not args.no_tuned_gemm:
+    if cuda and not args.no_tuned_gemm:
         from paddle_amd.utils import gemm_tuning
 
         tuned = gemm_tuning.enable(args.model, verbose=rank == 0)
@@ -77,16 +124,21 @@ def main():
     model.train()
     opt = FlatShardedOptimizer(model.named_parameters(), lr=3e-4, betas=(0.9, 0.95), eps=1e-8,
                                weight_decay=0.1, grad_clip=1.0, bucket_mb=args.bucket_mb,
-                               overlap=not args.no_overlap, overlap_allgather=not args.no_overlap)
+                               overlap=not args.no_overlap, overlap_allgather=not args.no_overlap,
+                               grad_dtype=None if args.bf16_grads else torch.float32)
     nparams = sum(p.numel() for p in model.parameters())
+    mem = (lambda: torch.cuda.memory_allocated(dev) / 2**30) if cuda else (lambda: 0.0)
+    peak = (lambda: torch.cuda.max_memory_allocated(dev) / 2**30) if cuda else (lambda: 0.0)
     if rank == 0:
         log(f"[bench] model {args.model} params={nparams/1e9:.3f}B layers={cfg.num_hidden_layers} "
-            f"world={world} build {time.time()-t0:.1f}s mem={torch.cuda.memory_allocated(dev)/2**30:.1f}GiB")
+            f"world={world} grads={opt.grad_dtype} build {time.time()-t0:.1f}s mem={mem():.1f}GiB")
 
     mb, S = args.micro_batch, args.seq_len
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(42 + rank)
-    pool = [torch.randint(0, cfg.vocab_size, (mb, S + 1), device=dev, generator=gen) for _ in range(4)]
+    # one global synthetic batch pool; rank r trains on rows [r*mb, (r+1)*mb) of every
+    # micro-batch, so an N-rank run sees exactly the data of a 1-rank run at N x batch
+    gen = torch.Generator().manual_seed(42)
+    pool = [torch.randint(0, cfg.vocab_size, (world * mb, S + 1), generator=gen)[rank * mb:(rank + 1) * mb]
+            .to(dev) for _ in range(4)]
 
     def train_step(i):
         for a in range(args.accum):
@@ -105,31 +157,35 @@ def main():
 
     for i in range(args.warmup):
         l = train_step(i)
-        torch.cuda.synchronize()
+        sync()
         if rank == 0:
-            log(f"[bench] warmup {i} loss={l.item()*args.accum:.4f} mem_peak={torch.cuda.max_memory_allocated(dev)/2**30:.1f}GiB")
+            log(f"[bench] warmup {i} loss={l.item()*args.accum:.4f} mem_peak={peak():.1f}GiB")
     comm.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         l = train_step(args.warmup + i)
         if rank == 0 and (i % 2 == 0 or i == args.steps - 1):
             log(f"[bench] step {i} issued")
     comm.barrier()
-    torch.cuda.synchronize()
+    sync()
     el = time.perf_counter() - t0
     elt = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
         torch.distributed.all_reduce(elt, op=torch.distributed.ReduceOp.MAX)
     el = float(elt.item())
+    lt = (l.detach().float() * args.accum).reshape(1)
+    if world > 1:
+        torch.distributed.all_reduce(lt)
+    final_loss = float(lt.item()) / world
     tokens_per_step = world * args.accum * mb * S
     tps = tokens_per_step * args.steps / el
     ms = el / args.steps * 1000
     fpt = llama_flops_per_token(cfg, S)
     mfu = tps / world * fpt / 2.5e15
     if rank == 0:
-        log(f"[bench] final loss={l.item()*args.accum:.4f} tokens/s={tps:.0f} per-gpu={tps/world:.0f} "
-            f"ms/step={ms:.1f} MFU(2.5PF bf16 dense)={mfu*100:.1f}% peak_mem={torch.cuda.max_memory_allocated(dev)/2**30:.1f}GiB")
+        log(f"[bench] final loss={final_loss:.4f} tokens/s={tps:.0f} per-gpu={tps/world:.0f} "
+            f"ms/step={ms:.1f} MFU(2.5PF bf16 dense)={mfu*100:.1f}% peak_mem={peak():.1f}GiB")
         invalid = args.layers is not None
         out = {
             "metric": METRIC,
@@ -142,7 +198,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if cfg.dtype in ("bfloat16", "bf16") else str(cfg.dtype),
             "data": "synthetic random token ids, random-init weights",
             "config": {
                 "model": args.model + (f"(DEBUG {args.layers} layers: INVALID)" if invalid else ""),
@@ -155,7 +211,10 @@ def main():
                 "mfu_bf16_dense": round(mfu, 4),
                 "recompute": bool(args.recompute),
                 "tuned_gemm": tuned,
+                "grad_dtype": str(opt.grad_dtype).replace("torch.", ""),
+                "device": args.device,
             },
+            "final_loss": round(final_loss, 5),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -262,6 +262,11 @@ static int launch_bwd(bool rms, const void* dy, const void* h, const void* w, co
   G = (int)((N + rpb - 1) / rpb);
   float* dwp = ws;
   float* dbp = ws + (long)G * H;
+  // (2H+8) fp32 of dynamic LDS: 65,568 B at H = 8192.  That is over the 64 KiB
+  // per-workgroup limit of older CDNA parts, so this launcher is gfx950-only
+  // (160 KB of LDS per CU, up to 160 KB per workgroup); the build targets gfx950
+  // exclusively and the launch below fails loudly (hipError) rather than falling
+  // back if it ever ran on a part with less LDS.
   size_t shm = (2 * H + 8) * sizeof(float);
   // rows wider than 4096 elements: two waves per row, 8 vectors per lane
   constexpr int WPR = MAXV > 8 ? 2 : 1;

@@ -31,6 +31,7 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -71,6 +72,9 @@ bool write_all(int fd, const void* buf, size_t n) {
 }
 
 #pragma pack(push, 1)
+constexpr uint32_t kMaxName = 4096;
+constexpr uint64_t kDefaultMaxBody = 1ull << 32;  // 4 GiB (PADDLE_AMD_RPC_MAX_BODY overrides)
+
 struct ReqHdr {
   uint32_t magic;
   uint8_t type;
@@ -109,11 +113,25 @@ struct Server {
   uint64_t fetch_round = 0;
   std::deque<std::string> checkpoints;
 
+  // Frames come from the network: bound every length before allocating
+  // (reference: the gRPC transport's FLAGS_rpc_max_message_size); a bad frame or
+  // an allocation failure closes only that connection, never the server.
+  uint64_t max_body = kDefaultMaxBody;
+
   void serve(int fd) {
+    try {
+      serve_loop(fd);
+    } catch (...) {
+    }
+    ::close(fd);
+  }
+
+  void serve_loop(int fd) {
     std::string name, payload;
     for (;;) {
       ReqHdr h;
       if (!read_all(fd, &h, sizeof(h)) || h.magic != kMagic) break;
+      if (h.name_len > kMaxName || h.payload_len > max_body) break;
       name.resize(h.name_len);
       payload.resize(h.payload_len);
       if ((h.name_len && !read_all(fd, &name[0], h.name_len)) ||
@@ -194,7 +212,6 @@ struct Server {
       RepHdr r{kMagic, status, out.size()};
       if (!write_all(fd, &r, sizeof(r)) || (!out.empty() && !write_all(fd, out.data(), out.size()))) break;
     }
-    ::close(fd);
   }
 
   void accept_loop() {
@@ -307,15 +324,29 @@ int call(const char* ep, uint8_t type, const char* name, const void* payload, si
 }  // namespace
 
 // ------------------------------------------------------------------ server C ABI
-PA_RT_EXPORT void* pa_rpc_server_create(int port, int fanin) {
+// host: address to bind (the pserver's configured endpoint); NULL or "" = all interfaces.
+PA_RT_EXPORT void* pa_rpc_server_create(const char* host, int port, int fanin) {
   auto* s = new Server();
   s->fanin = fanin;
+  if (const char* mb = std::getenv("PADDLE_AMD_RPC_MAX_BODY")) s->max_body = std::strtoull(mb, nullptr, 10);
   s->listen_fd = ::socket(AF_INET, SOCK_STREAM, 0);
   int one = 1;
   setsockopt(s->listen_fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
   sockaddr_in addr{};
   addr.sin_family = AF_INET;
   addr.sin_addr.s_addr = htonl(INADDR_ANY);
+  if (host && *host && std::strcmp(host, "0.0.0.0") != 0) {
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_INET;
+    if (getaddrinfo(host, nullptr, &hints, &res) != 0 || !res) {
+      pa_rt_set_error("rpc: cannot resolve bind address %s", host);
+      ::close(s->listen_fd);
+      delete s;
+      return nullptr;
+    }
+    addr.sin_addr = reinterpret_cast<sockaddr_in*>(res->ai_addr)->sin_addr;
+    freeaddrinfo(res);
+  }
   addr.sin_port = htons(static_cast<uint16_t>(port));
   if (::bind(s->listen_fd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0 || ::listen(s->listen_fd, 128)) {
     pa_rt_set_error("rpc: cannot listen on port %d", port);

@@ -19,7 +19,7 @@ from ...framework import serialization as S
 _P, _I, _SZ, _C = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_char_p
 _PP = ctypes.POINTER(ctypes.c_void_p)
 _SIGS = {
-    "pa_rpc_server_create": ([_I, _I], _P),
+    "pa_rpc_server_create": ([ctypes.c_char_p, _I, _I], _P),
     "pa_rpc_server_port": ([_P], _I),
     "pa_rpc_server_wait": ([_P, _I, _I], _I),
     "pa_rpc_server_pop": ([_P, _PP, _PP, ctypes.POINTER(_SZ)], _I),
@@ -144,8 +144,9 @@ class RPCClient:
 
 # ------------------------------------------------------------------------ server
 class RPCServer:
-    def __init__(self, port, fanin):
-        self.h = lib().pa_rpc_server_create(int(port), int(fanin))
+    def __init__(self, port, fanin, host=None):
+        """``host``: bind address (the pserver endpoint's host); None = all interfaces."""
+        self.h = lib().pa_rpc_server_create((host or "").encode(), int(port), int(fanin))
         if not self.h:
             raise RuntimeError(runtime.lib().pa_rt_last_error().decode())
         self.port = lib().pa_rpc_server_port(self.h)

@@ -158,7 +158,8 @@ def listen_and_serv(ctx):
     op, scope, exe = ctx.op, ctx.scope, ctx.executor
     ep = ctx.attr("endpoint")
     fanin = ctx.attr("Fanin")
-    server = RPCServer(int(ep.rsplit(":", 1)[1]), fanin)
+    host, port = ep.rsplit(":", 1)
+    server = RPCServer(int(port), fanin, host=os.environ.get("PADDLE_AMD_RPC_BIND", host))
     blocks = ctx.attr("optimize_blocks") or []
     prog = blocks[0].program if blocks else None
     g2b = dict(s.split(":", 1) for s in ctx.attr("grad_to_block_id"))

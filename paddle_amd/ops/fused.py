@@ -655,6 +655,17 @@ def _linear_fwd(x, w, b):
     return torch.addmm(b, x2, wm).view(*x.shape[:-1], wm.shape[-1])
 
 
+def _acc_mm(acc, a, b):
+    """acc += a @ b; ``acc`` may be fp32 while a, b are bf16 (fp32 main_grad):
+    one GEMM with an fp32 accumulator, never rounded through bf16."""
+    if acc.dtype == a.dtype:
+        acc.addmm_(a, b)
+    elif acc.is_cuda:
+        acc.add_(torch.mm(a, b, out_dtype=acc.dtype))
+    else:
+        acc.add_(a.to(acc.dtype) @ b.to(acc.dtype))
+
+
 def _linear_bwd(ctx, x, w, dy, need_dx, need_dw):
     dx = torch.matmul(dy, w.t()) if need_dx else None
     dw = None
@@ -670,7 +681,7 @@ def _linear_bwd(ctx, x, w, dy, need_dx, need_dw):
             xa, dyb = x2.t(), dy2
         if mg is not None:
             # the engine's post-accumulate hook still fires for w (grad None)
-            mg.addmm_(xa, dyb)
+            _acc_mm(mg, xa, dyb)
         else:
             dw = torch.matmul(xa, dyb)
     return dx, dw

@@ -9,7 +9,12 @@ The never-used ``FuseVarsOpHandle`` (details/fuse_vars_op_handle.cc:21-47) is th
 seed of what is done here, MI355X-first:
 
 * every trainable parameter is a view into ONE flat bf16 buffer, every gradient a
-  view into ONE flat bf16 gradient buffer (AccumulateGrad adds in place);
+  view into ONE flat gradient buffer.  With ``grad_dtype=torch.float32`` (the
+  default for bf16 models, Fleet's fp32 ``main_grad``) that buffer is fp32: the
+  fused linear dW GEMMs accumulate into it directly and every other gradient
+  is added by a post-accumulate hook, so micro-batch accumulation and the
+  reduce-scatter never round through bf16; with ``grad_dtype=None`` it shares the
+  parameter dtype and AccumulateGrad adds in place;
 * parameters are laid out in reverse forward order, so gradients complete front
   to back during backward; the buffer is cut into buckets (default 256 MB, sized
   for the per-link bound of ring collectives over 7 point-to-point xGMI links);
@@ -49,7 +54,7 @@ class FlatShardedOptimizer:
 
     def __init__(self, named_params, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1,
                  group=None, bucket_mb=256, grad_clip=None, overlap=True, stage=1,
-                 no_decay_fn=None, overlap_allgather=False):
+                 no_decay_fn=None, overlap_allgather=False, grad_dtype="auto"):
         named = [(n, p) for n, p in named_params if p.requires_grad]
         if not named:
             raise ValueError("no trainable parameters")
@@ -64,11 +69,16 @@ class FlatShardedOptimizer:
         dev = named[0][1].device
         dt = named[0][1].dtype
         self.device, self.dtype = dev, dt
+        if grad_dtype == "auto":
+            grad_dtype = torch.float32 if dt in (torch.bfloat16, torch.float16) else dt
+        self.grad_dtype = grad_dtype or dt
+        # fp32 main-grad mode: gradients live outside p.grad (dtype differs from p)
+        self.main_grad = self.grad_dtype != dt
         decay = [(n, p) for n, p in reversed(named) if not nd(n, p)]
         nodec = [(n, p) for n, p in reversed(named) if nd(n, p)]
         order = decay + nodec
         unit = self.W * 256
-        bucket_elems = max(unit, int(bucket_mb * 2**20 / max(1, torch.empty((), dtype=dt).element_size())))
+        bucket_elems = max(unit, int(bucket_mb * 2**20 / torch.empty((), dtype=self.grad_dtype).element_size()))
         # --- assign offsets and buckets
         offs, buckets = [], []
         off = 0
@@ -93,7 +103,7 @@ class FlatShardedOptimizer:
         self.offsets = offs
         # --- flat buffers; parameters/grads become views
         self.flat_param = torch.zeros(total, dtype=dt, device=dev)
-        self.flat_grad = torch.zeros(total, dtype=dt, device=dev)
+        self.flat_grad = torch.zeros(total, dtype=self.grad_dtype, device=dev)
         self._bucket_of = {}
         bi = 0
         with torch.no_grad():
@@ -104,9 +114,13 @@ class FlatShardedOptimizer:
                 self._bucket_of[id(p)] = bi
                 self.flat_param[o:o + p.numel()].copy_(p.data.reshape(-1))
                 p.data = self.flat_param[o:o + p.numel()].view(p.shape)
-                p.grad = self.flat_grad[o:o + p.numel()].view(p.shape)
+                g = self.flat_grad[o:o + p.numel()].view(p.shape)
+                if self.main_grad:
+                    p.grad = None
+                else:
+                    p.grad = g
                 # fused-GEMM gradient accumulation target (ops.linear)
-                p._pa_main_grad = p.grad
+                p._pa_main_grad = g
         self.buckets = buckets
         # --- shard layout: rank r owns slice r of every bucket
         self.shard_slices = []  # (bucket_start + r*L, L, shard_off)
@@ -124,7 +138,7 @@ class FlatShardedOptimizer:
             self.grad_shard = self.flat_grad
             self.param_shard = self.flat_param
         else:
-            self.grad_shard = torch.empty(so, dtype=dt, device=dev)
+            self.grad_shard = torch.empty(so, dtype=self.grad_dtype, device=dev)
             self.param_shard = torch.empty(so, dtype=dt, device=dev)
         self.master = torch.empty(so, dtype=torch.float32, device=dev)
         for s0, L, sof in self.shard_slices:
@@ -141,7 +155,7 @@ class FlatShardedOptimizer:
         self.overlap_allgather = bool(overlap_allgather) and self.W > 1
         self._ag_queue = []
         self._hooks = []
-        if self.W > 1:
+        if self.W > 1 or self.main_grad:
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
 
@@ -161,6 +175,10 @@ class FlatShardedOptimizer:
         return _Ctx()
 
     def _on_grad(self, p):
+        if self.main_grad and p.grad is not None:
+            # autograd produced a bf16 gradient (non-fused op): fold it into fp32 main_grad
+            p._pa_main_grad.add_(p.grad)
+            p.grad = None
         if self.W == 1 or not self._sync:
             return
         b = self._bucket_of[id(p)]
@@ -302,5 +320,5 @@ class FlatShardedOptimizer:
 
     def memory_bytes(self):
         es = self.flat_param.element_size()
-        return {"flat_param": self.total * es, "flat_grad": self.total * es,
+        return {"flat_param": self.total * es, "flat_grad": self.total * self.flat_grad.element_size(),
                 "optimizer_fp32": 3 * self.shard_size * 4}

@@ -31,7 +31,7 @@ _SIGS = {
     "pa_ts_open": ([ctypes.c_char_p, I, I], P),
     "pa_ts_close": ([P], I),
     "pa_ts_write_lod_tensor": ([P, I, U64P, I64P, I, I, I64P, P, SZ], I),
-    "pa_ts_read_header": ([P, ctypes.POINTER(I), U64P, I64P, I, ctypes.POINTER(I), ctypes.POINTER(I), I64P, I,
+    "pa_ts_read_header": ([P, ctypes.POINTER(I), U64P, I64P, I, I, ctypes.POINTER(I), ctypes.POINTER(I), I64P, I,
                            ctypes.POINTER(SZ), ctypes.POINTER(ctypes.c_int * 32)], I),
     "pa_ts_read_data": ([P, P, SZ], I),
     "pa_buddy_create": ([I, SZ, I], P),
@@ -176,13 +176,14 @@ def read_lod_tensors(path, max_lod=1 << 20):
     if not h:
         raise IOError(_err())
     out = []
+    fsize = os.path.getsize(path)
     try:
         lod_flat = (ctypes.c_uint64 * max_lod)()
         lod_lens = (ctypes.c_int64 * 16)()
         dims = (ctypes.c_int64 * 16)()
         while True:
             ll, dt, nd, nb = I(), I(), I(), SZ()
-            rc = lib().pa_ts_read_header(h, ctypes.byref(ll), lod_flat, lod_lens, max_lod, ctypes.byref(dt),
+            rc = lib().pa_ts_read_header(h, ctypes.byref(ll), lod_flat, lod_lens, 16, max_lod, ctypes.byref(dt),
                                          ctypes.byref(nd), dims, 16, ctypes.byref(nb), ctypes.byref(_ES))
             if rc == 0:
                 break
@@ -193,6 +194,10 @@ def read_lod_tensors(path, max_lod=1 << 20):
                 lod.append([int(lod_flat[p + k]) for k in range(lod_lens[i])])
                 p += lod_lens[i]
             shape = [dims[i] for i in range(nd.value)]
+            if dt.value not in _NPT:
+                raise IOError(f"unsupported tensor dtype {dt.value} in {path}")
+            if nb.value > fsize:
+                raise IOError(f"tensor of {nb.value} bytes declared in a {fsize}-byte file {path}")
             arr = np.empty(shape, dtype=_NPT[dt.value])
             if lib().pa_ts_read_data(h, arr.ctypes.data_as(P), nb.value) != 0:
                 raise IOError("truncated tensor data")

@@ -35,7 +35,7 @@ void* pa_ts_open(const char* path, int write, int append);
 int pa_ts_close(void* h);
 int pa_ts_write_lod_tensor(void* h, int lod_level, const uint64_t* lod_flat, const int64_t* lod_lens, int dtype,
                            int ndims, const int64_t* dims, const void* data, size_t nbytes);
-int pa_ts_read_header(void* h, int* lod_level, uint64_t* lod_flat, int64_t* lod_lens, int lod_cap, int* dtype,
+int pa_ts_read_header(void* h, int* lod_level, uint64_t* lod_flat, int64_t* lod_lens, int lod_levels_cap, int lod_cap, int* dtype,
                       int* ndims, int64_t* dims, int dims_cap, size_t* nbytes, int elem_size_by_dtype[32]);
 int pa_ts_read_data(void* h, void* dst, size_t nbytes);
 void* pa_bq_create(size_t capacity);
@@ -124,7 +124,7 @@ static void test_tensor_stream(const std::string& dir) {
   size_t nbytes;
   int esz[32] = {0};
   esz[5] = 4;
-  CHECK(pa_ts_read_header(f, &lod_level, lod2, lens2, 8, &dtype, &ndims, dims2, 8, &nbytes, esz) == 1);
+  CHECK(pa_ts_read_header(f, &lod_level, lod2, lens2, 4, 8, &dtype, &ndims, dims2, 8, &nbytes, esz) == 1);
   CHECK(lod_level == 1 && lens2[0] == 3 && lod2[2] == 5 && ndims == 2 && dims2[1] == 4 && nbytes == 80);
   std::vector<float> back(20);
   CHECK(pa_ts_read_data(f, back.data(), nbytes) == 0);
