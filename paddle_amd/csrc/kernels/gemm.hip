@@ -1,0 +1,404 @@
+// Hand-written gfx950 bf16 GEMM on MFMA (v_mfma_f32_16x16x32_bf16), fp32 accumulate.
+//
+//   C[m, n] (=|+=) alpha * sum_k A(m, k) B(n, k)  (+ bias[n])
+//
+// Each operand is either K-contiguous ("K-major": X[mn * ld + k]) or MN-contiguous
+// ("MN-major": X[k * ld + mn]), so one kernel family covers every linear-layer
+// GEMM of a training step without transposed copies (Paddle weights are [in, out]):
+//   forward   y  = x W      : A = x (K-major),   B = W (MN-major)
+//   backward  dx = dy W^T   : A = dy (K-major),  B = W (K-major)
+//   backward  dW = x^T dy   : A = x (MN-major),  B = dy (MN-major), fp32 += into main_grad
+// Reference: paddle/fluid/operators/math/blas_impl.cu.h:27-200 (cuBLAS gemm /
+// batched gemm behind mul_op / matmul_op / fc); here the library call is replaced.
+//
+// Design (MI355X-first; guide §5 "256² 8-phase template", re-derived):
+//  * 256x256 block tile, BK = 64, 512 threads = 8 waves as 2 (M) x 4 (N); each wave
+//    owns a 128 x 64 output (8 x 4 tiles of 16x16 = 128 fp32 accumulators/lane).
+//  * Operands arrive in LDS by LDS-DMA (`buffer_load_dwordx4 ... lds`, 1 KiB per
+//    wave-instruction); the buffer descriptor's range check zero-fills every edge
+//    (M, N, K need only be multiples of 8), so there is no edge code in the loop.
+//  * LDS holds 2 K-tile stages of 16 "units" (32 mn x 64 k, 4 KiB each).  A unit is
+//    XOR-swizzled for conflict-free reads: K-major units are read by ds_read_b128,
+//    MN-major units by ds_read_b64_tr_b16 (hardware transpose); the swizzle is
+//    applied to the per-lane SOURCE address because LDS-DMA writes lane-linearly.
+//  * 4 phases per K-tile, one 64x32 quadrant (16 MFMA) per phase.  The two wave
+//    groups (wr = 0/1, one wave of each per SIMD) run one barrier apart, so one
+//    group's LDS reads + DMA issue overlap the other group's MFMA cluster.
+//  * LDS regions are refilled as soon as their last reader has passed a barrier;
+//    every wave waits with a counted `s_waitcnt vmcnt(6)` (never 0 in the loop),
+//    leaving 3 DMA groups (~4 phases) in flight.
+//  * blockIdx -> tile is XCD-aware (contiguous tile bands per XCD, bijective).
+#include "common.h"
+
+namespace pa {
+namespace gemm {
+
+constexpr int BM = 256, BN = 256, BKT = 64, NT = 512;
+constexpr int UNIT = 4096;            // bytes: 32 (mn) x 64 (k) bf16
+constexpr int OPND = 8 * UNIT;        // one operand of one stage (256 x 64 bf16)
+constexpr int STAGE = 2 * OPND;       // A + B
+constexpr int LDS_BYTES = 2 * STAGE;  // 128 KiB
+constexpr unsigned OOB = 0xFFFFFFF0u; // voffset beyond num_records -> DMA writes zeros
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+struct Params {
+  const void* A;
+  const void* B;
+  void* C;
+  const void* bias;  // [N], same dtype as C (bf16 or fp32); may be null
+  int M, N, K;
+  long lda, ldb, ldc;
+  long sA, sB, sC;   // batch strides (elements)
+  float alpha;
+  int accumulate;    // C += result (beta = 1)
+  int tiles_m, tiles_n;
+};
+
+// Regions of a stage (per operand: 8 units of 32 mn).  A: the wave group wr owns
+// units 4wr..4wr+3; quadrant rows 0-63 are units {4wr, 4wr+1} (A_first), rows
+// 64-127 units {4wr+2, 4wr+3} (A_sec).  B: wave column wc owns units 2wc (cols 0-31
+// of its 64, Bp1) and 2wc+1 (Bp2).
+enum Region { A_FIRST = 0, A_SEC = 1, B_P1 = 2, B_P2 = 3 };
+
+__device__ __forceinline__ int region_unit(int region, int ui) {
+  switch (region) {
+    case A_FIRST: return (ui & 1) + 4 * (ui >> 1);
+    case A_SEC: return 2 + (ui & 1) + 4 * (ui >> 1);
+    case B_P1: return 2 * ui;
+    default: return 2 * ui + 1;
+  }
+}
+
+// Per-lane byte offset (relative to the operand's tile origin at k = 0) of one 16-B
+// chunk that this lane DMAs for piece `pc` (0..3) of unit `u`, plus the (mn, k)
+// coordinates relative to the tile, for the range checks.
+template <bool KMAJ>
+__device__ __forceinline__ void dma_coords(int u, int pc, int lane, int& mn, int& k) {
+  if (KMAJ) {  // unit image: 32 rows (mn) x 128 B (64 k); chunk' = chunk ^ ((row>>1)&7)
+    const int row = 8 * pc + (lane >> 3);
+    const int ch = (lane & 7) ^ ((row >> 1) & 7);
+    mn = 32 * u + row;
+    k = 8 * ch;
+  } else {     // unit image: 64 rows (k) x 64 B (32 mn); chunk' = chunk ^ (2*((row>>3)&1))
+    const int row = 16 * pc + (lane >> 2);
+    const int ch = (lane & 3) ^ (2 * ((row >> 3) & 1));
+    mn = 32 * u + 8 * ch;
+    k = row;
+  }
+}
+
+// One operand's DMA plan for one wave: 2 pieces in each of its 2 regions.
+struct DmaLane {
+  unsigned off[2][2];  // [region slot][piece] byte offset at k-tile 0
+  int kk[2][2];        // k coordinate within the tile
+  bool mnok[2][2];
+};
+
+template <bool KMAJ>
+__device__ __forceinline__ void dma_plan(DmaLane& d, const int (&regions)[2], int wid, int lane,
+                                         int mn_tile0, int MN, long ld) {
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int piece = 2 * wid + j;  // 16 pieces per region, 2 per wave
+      const int u = region_unit(regions[r], piece >> 2);
+      int mn, k;
+      dma_coords<KMAJ>(u, piece & 3, lane, mn, k);
+      const int gmn = mn_tile0 + mn;
+      d.mnok[r][j] = gmn < MN;
+      d.kk[r][j] = k;
+      d.off[r][j] = KMAJ ? (unsigned)(((long)gmn * ld + k) * 2) : (unsigned)(((long)k * ld + gmn) * 2);
+    }
+}
+
+// Issue the 2 DMA pieces of region slot r for k-tile kt into `stage_opnd`.
+template <bool KMAJ>
+__device__ __forceinline__ void dma_issue(const DmaLane& d, int r, __amdgpu_buffer_rsrc_t rs,
+                                          char* stage_opnd, int region, int wid, int kt, int K, long ld) {
+  const int k0 = kt * BKT;
+  const unsigned kstep = KMAJ ? (unsigned)(k0 * 2) : (unsigned)((long)k0 * ld * 2);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int piece = 2 * wid + j;
+    const int u = region_unit(region, piece >> 2);
+    const bool ok = d.mnok[r][j] && (k0 + d.kk[r][j] < K);
+    const unsigned vo = ok ? d.off[r][j] + kstep : OOB;
+    char* dst = stage_opnd + u * UNIT + (piece & 3) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16, vo, 0, 0, 0);
+  }
+}
+
+// Fragment (16 mn x 32 k, MFMA operand layout: lane l holds X[mn = l&15][k = 8(l>>4) + j])
+// of tile `i` (0/1: 16-row half of a 32-mn unit) at k-step kk (0/1) of a unit.
+__device__ __forceinline__ bf16x8 frag_kmaj(const char* unit, int i, int kk, int lane) {
+  const int row = 16 * i + (lane & 15);
+  const int ch = (4 * kk + (lane >> 4)) ^ ((row >> 1) & 7);
+  return *reinterpret_cast<const bf16x8*>(unit + row * 128 + ch * 16);
+}
+
+__device__ __forceinline__ bf16x8 frag_mnmaj(const char* unit, int i, int kk, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int k0 = 32 * kk + 8 * g + q;
+  const int ch = (2 * i + (p >> 1)) ^ (2 * (g & 1));
+  const char* a0 = unit + k0 * 64 + ch * 16 + 8 * (p & 1);
+  s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+  s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * 64));
+  i16x8 v = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8 frag(const char* unit, int i, int kk, int lane) {
+  return KMAJ ? frag_kmaj(unit, i, kk, lane) : frag_mnmaj(unit, i, kk, lane);
+}
+
+__device__ __forceinline__ void wait_vm6() { asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); }
+__device__ __forceinline__ void wait_vm8() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// Bijective XCD-aware remap: blocks that share an XCD (bid % 8) get a contiguous
+// range of tile ids (guide §5 "XCD swizzle must be bijective").
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+template <bool AK, bool BK, bool OUTF32>
+__global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+
+  // ---- tile of this block: XCD remap, then bands of 8 tile-rows for L2 reuse
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int t = xcd_remap(blockIdx.x, nwg);
+  constexpr int GM = 8;
+  const int band = t / (GM * p.tiles_n);
+  const int m_in_band = min(GM, p.tiles_m - band * GM);
+  const int tin = t - band * GM * p.tiles_n;
+  const int tm = band * GM + tin % m_in_band;
+  const int tn = tin / m_in_band;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const long bz = blockIdx.y;
+  const char* Ab = (const char*)p.A + bz * p.sA * 2;
+  const char* Bb = (const char*)p.B + bz * p.sB * 2;
+  // descriptors over this batch's whole operand (host guarantees < 4 GiB)
+  const unsigned a_bytes = AK ? (unsigned)(((long)(p.M - 1) * p.lda + p.K) * 2)
+                              : (unsigned)(((long)(p.K - 1) * p.lda + p.M) * 2);
+  const unsigned b_bytes = BK ? (unsigned)(((long)(p.N - 1) * p.ldb + p.K) * 2)
+                              : (unsigned)(((long)(p.K - 1) * p.ldb + p.N) * 2);
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, 0, a_bytes, 0x00020000);
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, 0, b_bytes, 0x00020000);
+
+  // ---- DMA plans (A regions: first/sec; B regions: p1/p2)
+  DmaLane da, db;
+  const int ra[2] = {A_FIRST, A_SEC};
+  const int rb[2] = {B_P1, B_P2};
+  dma_plan<AK>(da, ra, wid, lane, m0, p.M, p.lda);
+  dma_plan<BK>(db, rb, wid, lane, n0, p.N, p.ldb);
+
+  const int nk = (p.K + BKT - 1) / BKT;
+  auto sA = [&](int kt) { return smem + (kt & 1) * STAGE; };
+  auto sB = [&](int kt) { return smem + (kt & 1) * STAGE + OPND; };
+
+  // ---- prologue: k-tile 0 complete, k-tile 1 first regions (issue order matters
+  // for the counted waits: A_first(0) Bp1(0) Bp2(0) A_sec(0) A_first(1) Bp1(1))
+  dma_issue<AK>(da, 0, rsA, sA(0), A_FIRST, wid, 0, p.K, p.lda);
+  dma_issue<BK>(db, 0, rsB, sB(0), B_P1, wid, 0, p.K, p.ldb);
+  dma_issue<BK>(db, 1, rsB, sB(0), B_P2, wid, 0, p.K, p.ldb);
+  dma_issue<AK>(da, 1, rsA, sA(0), A_SEC, wid, 0, p.K, p.lda);
+  dma_issue<AK>(da, 0, rsA, sA(1), A_FIRST, wid, 1, p.K, p.lda);
+  dma_issue<BK>(db, 0, rsB, sB(1), B_P1, wid, 1, p.K, p.ldb);
+  wait_vm8();
+  bar();
+  if (wr == 1) bar();  // stagger: group 1 runs one barrier behind group 0
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+  const int ua0 = 4 * wr, ub0 = 2 * wc;
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* A_ = sA(kt);
+    const char* B_ = sB(kt);
+    // ---------------- phase 1: quadrant (rows 0-63, cols 0-31)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fa[i][kk] = frag<AK>(A_ + (ua0 + (i >> 1)) * UNIT, i & 1, kk, lane);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fb0[i][kk] = frag<BK>(B_ + ub0 * UNIT, i, kk, lane);
+    wait_vm6();
+    dma_issue<BK>(db, 1, rsB, sB(kt + 1), B_P2, wid, kt + 1, p.K, p.ldb);
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][kk], fa[i][kk], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // ---------------- phase 2: quadrant (rows 0-63, cols 32-63)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fb1[i][kk] = frag<BK>(B_ + (ub0 + 1) * UNIT, i, kk, lane);
+    wait_vm6();
+    dma_issue<AK>(da, 1, rsA, sA(kt + 1), A_SEC, wid, kt + 1, p.K, p.lda);
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][kk], fa[i][kk], acc[i][2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // ---------------- phase 3: quadrant (rows 64-127, cols 32-63)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fa[i][kk] = frag<AK>(A_ + (ua0 + 2 + (i >> 1)) * UNIT, i & 1, kk, lane);
+    wait_vm6();
+    dma_issue<AK>(da, 0, rsA, sA(kt + 2), A_FIRST, wid, kt + 2, p.K, p.lda);
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][kk], fa[i][kk], acc[4 + i][2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // ---------------- phase 4: quadrant (rows 64-127, cols 0-31)
+    wait_vm6();
+    dma_issue<BK>(db, 0, rsB, sB(kt + 2), B_P1, wid, kt + 2, p.K, p.ldb);
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][kk], fa[i][kk], acc[4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+  }
+  if (wr == 0) bar();  // match group 1's extra barrier
+  wait_vm0();          // drain the zero-filling DMAs past the last k-tile
+
+  // ---- epilogue: lane holds C[m = .. + (l&15)][n = .. + 4(l>>4) + r], r = 0..3
+  const long cz = bz * p.sC;
+  const int mrow = m0 + 128 * wr + (lane & 15);
+  const int ncol = n0 + 64 * wc + 4 * (lane >> 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = ncol + 16 * j;
+    if (n >= p.N) continue;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias) {
+      if (OUTF32) {
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>((const float*)p.bias + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = b4[r];
+      } else {
+        const u16x4 b4 = *reinterpret_cast<const u16x4*>((const u16*)p.bias + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = bf2f(b4[r]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = mrow + 16 * i;
+      if (m >= p.M) continue;
+      const long off = cz + (long)m * p.ldc + n;
+      if (OUTF32) {
+        float* c = (float*)p.C + off;
+        f32x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = p.alpha * acc[i][j][r] + bv[r];
+        if (p.accumulate) v += *reinterpret_cast<const f32x4*>(c);
+        *reinterpret_cast<f32x4*>(c) = v;
+      } else {
+        u16* c = (u16*)p.C + off;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = p.alpha * acc[i][j][r] + bv[r];
+        if (p.accumulate) {
+          const u16x4 o = *reinterpret_cast<const u16x4*>(c);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += bf2f(o[r]);
+        }
+        uint2 w;
+        w.x = pack2bf(v[0], v[1]);
+        w.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(c) = w;
+      }
+    }
+  }
+}
+
+template <bool AK, bool BK, bool F32>
+static int launch(const Params& p0, int batch, hipStream_t st) {
+  Params p = p0;
+  p.tiles_m = (p.M + BM - 1) / BM;
+  p.tiles_n = (p.N + BN - 1) / BN;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)gemm_kernel<AK, BK, F32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        LDS_BYTES);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((gemm_kernel<AK, BK, F32>), dim3(p.tiles_m * p.tiles_n, batch), dim3(NT), LDS_BYTES, st, p);
+  return (int)hipGetLastError();
+}
+
+}  // namespace gemm
+}  // namespace pa
+
+using namespace pa;
+
+// Returns 0 on success, a hipError on launch failure, -1 for an unsupported shape
+// (the caller checks shapes first: M, N, K multiples of 8, 16-B aligned rows,
+// every operand < 4 GiB).
+//   a_kmaj: A is [M][lda] K-contiguous (else [K][lda] M-contiguous)
+//   b_kmaj: B is [N][ldb] K-contiguous (else [K][ldb] N-contiguous)
+//   out_f32: C is fp32 (else bf16); accumulate: C += alpha*AB (+bias)
+PA_EXPORT int pa_gemm(int a_kmaj, int b_kmaj, int out_f32, const void* A, const void* B, void* C,
+                      const void* bias, int M, int N, int K, long lda, long ldb, long ldc, long sA, long sB,
+                      long sC, int batch, float alpha, int accumulate, hipStream_t st) {
+  if (M <= 0 || N <= 0 || batch <= 0) return 0;
+  if ((M | N | K) & 7) return -1;
+  gemm::Params p{A, B, C, bias, M, N, K, lda, ldb, ldc, sA, sB, sC, alpha, accumulate, 0, 0};
+  if (K <= 0) return -1;
+#define PA_G(AK, BK, F)                                                \
+  if (a_kmaj == AK && b_kmaj == BK && out_f32 == F) return gemm::launch<AK, BK, F>(p, batch, st);
+  PA_G(1, 1, 0) PA_G(1, 0, 0) PA_G(0, 1, 0) PA_G(0, 0, 0)
+  PA_G(1, 1, 1) PA_G(1, 0, 1) PA_G(0, 1, 1) PA_G(0, 0, 1)
+#undef PA_G
+  return -1;
+}

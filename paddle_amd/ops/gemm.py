@@ -1,0 +1,98 @@
+"""Hand-written gfx950 MFMA GEMM (csrc/kernels/gemm.hip) -- the matmul behind every
+linear layer, replacing the vendor BLAS call of the reference
+(paddle/fluid/operators/math/blas_impl.cu.h:27-200; mul_op.cc, matmul_op.cc, fc_op).
+
+``gemm`` computes C (=|+=) alpha * A.B^T-style products where each operand is
+either K-contiguous ("K-major", the reduction axis is the fastest one) or
+MN-contiguous ("MN-major").  The three linear-layer products map onto it with no
+transposed copies (Paddle weights are [in, out]):
+
+* ``linear_fwd``  y  = x W        A = x  (K-major)   B = W  (MN-major)
+* ``linear_dx``   dx = dy W^T     A = dy (K-major)   B = W  (K-major)
+* ``linear_dw``   dW (+)= x^T dy  A = x  (MN-major)  B = dy (MN-major), fp32 out
+
+Shapes: M, N, K multiples of 8, 16-B aligned row strides, each operand < 4 GiB;
+``supported()`` says whether a call qualifies (callers fall back to torch only for
+shapes the kernel does not cover, never silently on CUDA for covered ones).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from . import _native as _nat
+
+_ENABLED = os.environ.get("PADDLE_AMD_GEMM", "1") != "0"
+_LIMIT = 0xFFFFFF00
+
+
+def enabled() -> bool:
+    return _ENABLED
+
+
+def set_enabled(flag: bool):
+    global _ENABLED
+    _ENABLED = bool(flag)
+
+
+def supported(M, N, K, *mats) -> bool:
+    if not _ENABLED or M % 8 or N % 8 or K % 8 or M <= 0 or N <= 0 or K <= 0:
+        return False
+    for t in mats:
+        if not (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1
+                and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0 and t.shape[0] * t.stride(0) * 2 < _LIMIT):
+            return False
+    return True
+
+
+def gemm(a, b, M, N, K, *, a_kmaj, b_kmaj, out=None, out_dtype=torch.bfloat16, bias=None, alpha=1.0,
+         accumulate=False, batch=1, sA=0, sB=0, sC=0, ldc=None):
+    """Raw launcher.  ``a``/``b``: bf16 CUDA tensors with unit inner stride, row
+    stride = their ld.  ``out``: [M, ldc] (bf16 or fp32) written or accumulated."""
+    if out is None:
+        out = torch.empty(M, N, dtype=out_dtype, device=a.device) if batch == 1 else \
+            torch.empty(batch, M, N, dtype=out_dtype, device=a.device)
+        sC = M * N if batch > 1 else 0
+    f32 = out.dtype == torch.float32
+    if bias is not None and bias.dtype != out.dtype:
+        bias = bias.to(out.dtype)
+    lda, ldb = a.stride(-2), b.stride(-2)
+    if ldc is None:
+        ldc = out.stride(-2)
+    rc = _nat.lib().pa_gemm(int(a_kmaj), int(b_kmaj), int(f32), _nat.ptr(a), _nat.ptr(b), _nat.ptr(out),
+                           _nat.ptr(bias),
+                         M, N, K, lda, ldb, ldc, sA, sB, sC, batch, float(alpha), int(accumulate), _nat.stream())
+    if rc != 0:
+        raise RuntimeError(f"pa_gemm failed (rc={rc}) M={M} N={N} K={K} a_kmaj={a_kmaj} b_kmaj={b_kmaj}")
+    return out
+
+
+def linear_fwd(x2, w, bias=None):
+    """x2 [M, K] @ w [K, N] (+ bias) -> [M, N] bf16."""
+    M, K = x2.shape
+    Nn = w.shape[1]
+    return gemm(x2, w, M, Nn, K, a_kmaj=True, b_kmaj=False, bias=bias)
+
+
+def linear_dx(dy2, w):
+    """dy2 [M, N] @ w[K, N]^T -> [M, K] bf16."""
+    M, Nn = dy2.shape
+    K = w.shape[0]
+    return gemm(dy2, w, M, K, Nn, a_kmaj=True, b_kmaj=True)
+
+
+def linear_dw(x2, dy2, out=None, accumulate=False):
+    """x2[M, K]^T @ dy2[M, N] -> [K, N]; fp32 ``out`` (main_grad) accumulates."""
+    M, K = x2.shape
+    Nn = dy2.shape[1]
+    if out is None:
+        out = torch.empty(K, Nn, dtype=torch.float32, device=x2.device)
+        accumulate = False
+    return gemm(x2, dy2, K, Nn, M, a_kmaj=False, b_kmaj=False, out=out, accumulate=accumulate)
+
+
+def matmul_nt(a, b):
+    """a [M, K] @ b [N, K]^T -> [M, N] bf16."""
+    M, K = a.shape
+    return gemm(a, b, M, b.shape[0], K, a_kmaj=True, b_kmaj=True)

@@ -1,0 +1,96 @@
+"""Numerics of the hand-written gfx950 MFMA GEMM (csrc/kernels/gemm.hip) against a
+plain PyTorch fp32 reference of the same product, for every operand layout, both
+output dtypes, accumulate, bias, batch, and shapes that are not tile multiples."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(8, 8, 8), (264, 136, 72), (520, 1032, 4104), (1024, 768, 512), (256, 256, 64), (2056, 512, 136)]
+
+
+def _operand(rows_mn, K, kmaj, gen):
+    # K-major: [MN, K]; MN-major: stored [K, MN]; returns (stored tensor, logical [MN, K] fp32)
+    if kmaj:
+        t = torch.randn(rows_mn, K, generator=gen, device="cuda").to(torch.bfloat16)
+        return t, t.float()
+    t = torch.randn(K, rows_mn, generator=gen, device="cuda").to(torch.bfloat16)
+    return t, t.float().t()
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("a_kmaj", [True, False])
+@pytest.mark.parametrize("b_kmaj", [True, False])
+def test_gemm_layouts_bf16(M, N, K, a_kmaj, b_kmaj):
+    from paddle_amd.ops import gemm as G
+
+    gen = torch.Generator(device="cuda").manual_seed(M * 7 + N * 3 + K)
+    a, af = _operand(M, K, a_kmaj, gen)
+    b, bf = _operand(N, K, b_kmaj, gen)
+    c = G.gemm(a, b, M, N, K, a_kmaj=a_kmaj, b_kmaj=b_kmaj)
+    ref = af @ bf.t()
+    err = (c.float() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err <= 1e-2 * scale + 1e-3, (err, scale)
+
+
+@pytest.mark.parametrize("M,N,K", [(264, 136, 72), (1024, 768, 4104)])
+@pytest.mark.parametrize("a_kmaj,b_kmaj", [(True, False), (False, False), (True, True)])
+def test_gemm_fp32_accumulate_and_bias(M, N, K, a_kmaj, b_kmaj):
+    from paddle_amd.ops import gemm as G
+
+    gen = torch.Generator(device="cuda").manual_seed(11)
+    a, af = _operand(M, K, a_kmaj, gen)
+    b, bf = _operand(N, K, b_kmaj, gen)
+    c0 = torch.randn(M, N, generator=gen, device="cuda")
+    c = c0.clone()
+    G.gemm(a, b, M, N, K, a_kmaj=a_kmaj, b_kmaj=b_kmaj, out=c, accumulate=True, alpha=0.5)
+    ref = c0 + 0.5 * (af @ bf.t())
+    assert torch.allclose(c, ref, atol=2e-3 * K ** 0.5, rtol=1e-4), (c - ref).abs().max()
+    bias = torch.randn(N, generator=gen, device="cuda").to(torch.bfloat16)
+    y = G.gemm(a, b, M, N, K, a_kmaj=a_kmaj, b_kmaj=b_kmaj, bias=bias)
+    ref = af @ bf.t() + bias.float()
+    assert (y.float() - ref).abs().max() <= 1e-2 * ref.abs().max() + 1e-3
+
+
+def test_gemm_identity_asymmetric():
+    # A = I with an asymmetric B catches a transposed C write (guide §3)
+    from paddle_amd.ops import gemm as G
+
+    n = 256
+    a = torch.eye(n, device="cuda", dtype=torch.bfloat16)
+    b = (torch.arange(n, device="cuda")[:, None] * 3 + torch.arange(n, device="cuda")[None, :] * 0.01
+         ).to(torch.bfloat16)
+    c = G.matmul_nt(a, b)
+    assert torch.equal(c, b.t().contiguous())
+
+
+def test_gemm_batched():
+    from paddle_amd.ops import gemm as G
+
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    Bt, M, N, K = 3, 136, 264, 200
+    a = torch.randn(Bt, M, K, generator=gen, device="cuda").to(torch.bfloat16)
+    b = torch.randn(Bt, K, N, generator=gen, device="cuda").to(torch.bfloat16)
+    c = G.gemm(a, b, M, N, K, a_kmaj=True, b_kmaj=False, batch=Bt, sA=M * K, sB=K * N)
+    ref = a.float() @ b.float()
+    assert (c.float() - ref).abs().max() <= 1e-2 * ref.abs().max()
+
+
+def test_linear_helpers_match_torch():
+    from paddle_amd.ops import gemm as G
+
+    gen = torch.Generator(device="cuda").manual_seed(9)
+    M, K, Nn = 2048, 1024, 1536
+    x = torch.randn(M, K, generator=gen, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(K, Nn, generator=gen, device="cuda") * 0.02).to(torch.bfloat16)
+    dy = torch.randn(M, Nn, generator=gen, device="cuda").to(torch.bfloat16)
+    y = G.linear_fwd(x, w)
+    assert torch.allclose(y.float(), x.float() @ w.float(), atol=5e-2, rtol=2e-2)
+    dx = G.linear_dx(dy, w)
+    assert torch.allclose(dx.float(), dy.float() @ w.float().t(), atol=5e-2, rtol=2e-2)
+    mg = torch.zeros(K, Nn, device="cuda")
+    G.linear_dw(x, dy, out=mg, accumulate=True)
+    G.linear_dw(x, dy, out=mg, accumulate=True)
+    ref = 2 * (x.float().t() @ dy.float())
+    assert torch.allclose(mg, ref, atol=1e-2 * M ** 0.5, rtol=1e-4), (mg - ref).abs().max()
