@@ -17,16 +17,18 @@
 //  * Operands arrive in LDS by LDS-DMA (`buffer_load_dwordx4 ... lds`, 1 KiB per
 //    wave-instruction); the buffer descriptor's range check zero-fills every edge
 //    (M, N, K need only be multiples of 8), so there is no edge code in the loop.
-//  * LDS holds 2 K-tile stages of 16 "units" (32 mn x 64 k, 4 KiB each).  A unit is
-//    XOR-swizzled for conflict-free reads: K-major units are read by ds_read_b128,
-//    MN-major units by ds_read_b64_tr_b16 (hardware transpose); the swizzle is
-//    applied to the per-lane SOURCE address because LDS-DMA writes lane-linearly.
+//  * LDS holds 2 K-tile stages of 8 slabs (64 mn x 64 k, 8 KiB each), XOR-swizzled
+//    for conflict-free reads: K-major slabs are read by ds_read_b128, MN-major slabs
+//    by ds_read_b64_tr_b16 (hardware transpose); the swizzle is applied to the
+//    per-lane SOURCE address because LDS-DMA writes lane-linearly, and every DMA
+//    wave-instruction reads 8 full 128-B global lines in either layout.
 //  * 4 phases per K-tile, one 64x32 quadrant (16 MFMA) per phase.  The two wave
 //    groups (wr = 0/1, one wave of each per SIMD) run one barrier apart, so one
 //    group's LDS reads + DMA issue overlap the other group's MFMA cluster.
-//  * LDS regions are refilled as soon as their last reader has passed a barrier;
-//    every wave waits with a counted `s_waitcnt vmcnt(6)` (never 0 in the loop),
-//    leaving 3 DMA groups (~4 phases) in flight.
+//  * LDS regions are refilled as soon as their last reader has passed a barrier
+//    (A rows 0-63 after phase 1, B after phase 2, A rows 64-127 after phase 3);
+//    waits are counted `s_waitcnt vmcnt(N)` (never 0 in the loop) so each DMA has
+//    ~4 phases of MFMA work to land under.
 //  * blockIdx -> tile is XCD-aware (contiguous tile bands per XCD, bijective).
 #include "common.h"
 
@@ -56,105 +58,139 @@ struct Params {
   int tiles_m, tiles_n;
 };
 
-// Regions of a stage (per operand: 8 units of 32 mn).  A: the wave group wr owns
-// units 4wr..4wr+3; quadrant rows 0-63 are units {4wr, 4wr+1} (A_first), rows
-// 64-127 units {4wr+2, 4wr+3} (A_sec).  B: wave column wc owns units 2wc (cols 0-31
-// of its 64, Bp1) and 2wc+1 (Bp2).
-enum Region { A_FIRST = 0, A_SEC = 1, B_P1 = 2, B_P2 = 3 };
+// LDS image of one operand of one stage: 4 "slabs" of 64 mn x 64 k (8 KiB each);
+// slab s covers mn 64s .. 64s+63 of the 256-wide tile.
+//  * K-major slab: two 4-KiB units of 32 rows (mn) x 128 B (64 k);
+//    16-B chunk' = chunk ^ ((row >> 1) & 7)   (conflict-free ds_read_b128)
+//  * MN-major slab: 64 rows (k) x 128 B (64 mn);
+//    chunk' = chunk ^ s(k), s(k) = 2*(((k>>1)&1) | (((k>>3)&1)<<1))  (conflict-free tr_b16)
+// One LDS-DMA wave-instruction ("piece", 1 KiB) fills 8 rows of 128 B, i.e. full
+// 128-B global lines in both layouts.  Regions (DMA'd as a unit): A_FIRST = slabs
+// {0, 2} (rows 0-63 of each wave group), A_SEC = {1, 3}, B = all four slabs.
+enum Region { A_FIRST = 0, A_SEC = 1, B_ALL = 2 };
 
-__device__ __forceinline__ int region_unit(int region, int ui) {
-  switch (region) {
-    case A_FIRST: return (ui & 1) + 4 * (ui >> 1);
-    case A_SEC: return 2 + (ui & 1) + 4 * (ui >> 1);
-    case B_P1: return 2 * ui;
-    default: return 2 * ui + 1;
-  }
-}
+__device__ __forceinline__ int mn_swz(int k) { return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1)); }
 
-// Per-lane byte offset (relative to the operand's tile origin at k = 0) of one 16-B
-// chunk that this lane DMAs for piece `pc` (0..3) of unit `u`, plus the (mn, k)
-// coordinates relative to the tile, for the range checks.
+// (mn, k) of the 16-B chunk this lane DMAs for piece pc (0..7) of slab sl.
 template <bool KMAJ>
-__device__ __forceinline__ void dma_coords(int u, int pc, int lane, int& mn, int& k) {
-  if (KMAJ) {  // unit image: 32 rows (mn) x 128 B (64 k); chunk' = chunk ^ ((row>>1)&7)
-    const int row = 8 * pc + (lane >> 3);
+__device__ __forceinline__ void dma_coords(int sl, int pc, int lane, int& mn, int& k) {
+  const int row = 8 * (pc & 3) + (lane >> 3);
+  if (KMAJ) {
     const int ch = (lane & 7) ^ ((row >> 1) & 7);
-    mn = 32 * u + row;
+    mn = 64 * sl + 32 * (pc >> 2) + row;
     k = 8 * ch;
-  } else {     // unit image: 64 rows (k) x 64 B (32 mn); chunk' = chunk ^ (2*((row>>3)&1))
-    const int row = 16 * pc + (lane >> 2);
-    const int ch = (lane & 3) ^ (2 * ((row >> 3) & 1));
-    mn = 32 * u + 8 * ch;
-    k = row;
+  } else {
+    const int kr = 8 * pc + (lane >> 3);
+    const int ch = (lane & 7) ^ mn_swz(kr);
+    mn = 64 * sl + 8 * ch;
+    k = kr;
   }
 }
 
-// One operand's DMA plan for one wave: 2 pieces in each of its 2 regions.
+// Pieces of a region issued by wave w: A regions have 16 pieces (2 per wave),
+// B has 32 (4 per wave).  Returns the slab and the piece within it.
+__device__ __forceinline__ void region_piece(int region, int wid, int j, int& sl, int& pc) {
+  if (region == B_ALL) {
+    const int q = 4 * wid + j;
+    sl = q >> 3;
+    pc = q & 7;
+  } else {
+    const int q = 2 * wid + j;
+    sl = 2 * (q >> 3) + (region == A_SEC ? 1 : 0);
+    pc = q & 7;
+  }
+}
+
+template <int NP>
 struct DmaLane {
-  unsigned off[2][2];  // [region slot][piece] byte offset at k-tile 0
-  int kk[2][2];        // k coordinate within the tile
-  bool mnok[2][2];
+  unsigned off[NP];  // byte offset at k-tile 0
+  int kk[NP];        // k coordinate within the tile
+  bool mnok[NP];
 };
 
-template <bool KMAJ>
-__device__ __forceinline__ void dma_plan(DmaLane& d, const int (&regions)[2], int wid, int lane,
-                                         int mn_tile0, int MN, long ld) {
+template <bool KMAJ, int NP>
+__device__ __forceinline__ void dma_plan(DmaLane<NP>& d, int region, int j0, int wid, int lane, int mn_tile0,
+                                         int MN, long ld) {
 #pragma unroll
-  for (int r = 0; r < 2; ++r)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int piece = 2 * wid + j;  // 16 pieces per region, 2 per wave
-      const int u = region_unit(regions[r], piece >> 2);
-      int mn, k;
-      dma_coords<KMAJ>(u, piece & 3, lane, mn, k);
-      const int gmn = mn_tile0 + mn;
-      d.mnok[r][j] = gmn < MN;
-      d.kk[r][j] = k;
-      d.off[r][j] = KMAJ ? (unsigned)(((long)gmn * ld + k) * 2) : (unsigned)(((long)k * ld + gmn) * 2);
-    }
+  for (int j = 0; j < NP; ++j) {
+    int sl, pc, mn, k;
+    region_piece(region, wid, j0 + j, sl, pc);
+    dma_coords<KMAJ>(sl, pc, lane, mn, k);
+    const int gmn = mn_tile0 + mn;
+    d.mnok[j] = gmn < MN;
+    d.kk[j] = k;
+    d.off[j] = KMAJ ? (unsigned)(((long)gmn * ld + k) * 2) : (unsigned)(((long)k * ld + gmn) * 2);
+  }
 }
 
-// Issue the 2 DMA pieces of region slot r for k-tile kt into `stage_opnd`.
-template <bool KMAJ>
-__device__ __forceinline__ void dma_issue(const DmaLane& d, int r, __amdgpu_buffer_rsrc_t rs,
-                                          char* stage_opnd, int region, int wid, int kt, int K, long ld) {
+// Issue this wave's pieces j0 .. j0+NP-1 of `region` for k-tile kt.
+template <bool KMAJ, int NP>
+__device__ __forceinline__ void dma_issue(const DmaLane<NP>& d, __amdgpu_buffer_rsrc_t rs, char* stage_opnd,
+                                          int region, int j0, int wid, int kt, int K, long ld) {
   const int k0 = kt * BKT;
   const unsigned kstep = KMAJ ? (unsigned)(k0 * 2) : (unsigned)((long)k0 * ld * 2);
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int piece = 2 * wid + j;
-    const int u = region_unit(region, piece >> 2);
-    const bool ok = d.mnok[r][j] && (k0 + d.kk[r][j] < K);
-    const unsigned vo = ok ? d.off[r][j] + kstep : OOB;
-    char* dst = stage_opnd + u * UNIT + (piece & 3) * 1024;
+  for (int j = 0; j < NP; ++j) {
+    int sl, pc;
+    region_piece(region, wid, j0 + j, sl, pc);
+    const bool ok = d.mnok[j] && (k0 + d.kk[j] < K);
+    const unsigned vo = ok ? d.off[j] + kstep : OOB;
+    char* dst = stage_opnd + sl * 8192 + pc * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16, vo, 0, 0, 0);
   }
 }
 
 // Fragment (16 mn x 32 k, MFMA operand layout: lane l holds X[mn = l&15][k = 8(l>>4) + j])
-// of tile `i` (0/1: 16-row half of a 32-mn unit) at k-step kk (0/1) of a unit.
-__device__ __forceinline__ bf16x8 frag_kmaj(const char* unit, int i, int kk, int lane) {
+// of 32-mn block `u` (0..7), 16-row half i (0/1), k-step kk (0/1).
+__device__ __forceinline__ bf16x8 frag_kmaj(const char* opnd, int u, int i, int kk, int lane) {
   const int row = 16 * i + (lane & 15);
   const int ch = (4 * kk + (lane >> 4)) ^ ((row >> 1) & 7);
-  return *reinterpret_cast<const bf16x8*>(unit + row * 128 + ch * 16);
+  return *reinterpret_cast<const bf16x8*>(opnd + u * 4096 + row * 128 + ch * 16);
 }
 
-__device__ __forceinline__ bf16x8 frag_mnmaj(const char* unit, int i, int kk, int lane) {
-  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-  const int k0 = 32 * kk + 8 * g + q;
-  const int ch = (2 * i + (p >> 1)) ^ (2 * (g & 1));
-  const char* a0 = unit + k0 * 64 + ch * 16 + 8 * (p & 1);
-  s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
-  s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * 64));
-  i16x8 v = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
-  return __builtin_bit_cast(bf16x8, v);
+// MN-major fragments use the hardware transpose read.  It is issued by inline asm:
+// hipcc cannot prove the ds_read_b64_tr_b16 builtin does not alias the in-flight
+// LDS-DMA and puts an `s_waitcnt vmcnt(0)` in front of it, draining the whole
+// prefetch pipeline every k-tile.  The asm destinations are then fenced by a
+// wait statement that names them ("+v"), so nothing reads them before they land
+// (guide §5.7 item 1, form ii).  LDS reads complete in order, so hipcc's own
+// counted lgkmcnt waits for the K-major reads stay conservative-correct.
+__device__ __forceinline__ unsigned lds_addr(const char* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
 template <bool KMAJ>
-__device__ __forceinline__ bf16x8 frag(const char* unit, int i, int kk, int lane) {
-  return KMAJ ? frag_kmaj(unit, i, kk, lane) : frag_mnmaj(unit, i, kk, lane);
-}
+struct Frag;
 
+template <>
+struct Frag<true> {
+  bf16x8 v;
+  __device__ __forceinline__ void load(const char* opnd, int u, int i, int kk, int lane) {
+    v = frag_kmaj(opnd, u, i, kk, lane);
+  }
+  __device__ __forceinline__ void wait() {}
+  __device__ __forceinline__ bf16x8 get() const { return v; }
+};
+
+template <>
+struct Frag<false> {
+  s16x4 x, y;
+  __device__ __forceinline__ void load(const char* opnd, int u, int i, int kk, int lane) {
+    const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    const int k0 = 32 * kk + 8 * g + q;
+    const int ch = (4 * (u & 1) + 2 * i + (p >> 1)) ^ mn_swz(k0);
+    const unsigned a = lds_addr(opnd + (u >> 1) * 8192 + k0 * 128 + ch * 16 + 8 * (p & 1));
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(x) : "v"(a));
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:512" : "=v"(y) : "v"(a));
+  }
+  __device__ __forceinline__ void wait() { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(x), "+v"(y)); }
+  __device__ __forceinline__ bf16x8 get() const {
+    i16x8 v = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+};
+
+__device__ __forceinline__ void wait_vm4() { asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
 __device__ __forceinline__ void wait_vm6() { asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); }
 __device__ __forceinline__ void wait_vm8() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
 __device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -170,6 +206,10 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
+
+#define WAIT_FRAGS(F, NI)                    \
+  _Pragma("unroll") for (int i_ = 0; i_ < NI; ++i_) \
+    _Pragma("unroll") for (int k_ = 0; k_ < 2; ++k_) F[i_][k_].wait();
 
 template <bool AK, bool BK, bool OUTF32>
 __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
@@ -200,26 +240,29 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, 0, a_bytes, 0x00020000);
   const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, 0, b_bytes, 0x00020000);
 
-  // ---- DMA plans (A regions: first/sec; B regions: p1/p2)
-  DmaLane da, db;
-  const int ra[2] = {A_FIRST, A_SEC};
-  const int rb[2] = {B_P1, B_P2};
-  dma_plan<AK>(da, ra, wid, lane, m0, p.M, p.lda);
-  dma_plan<BK>(db, rb, wid, lane, n0, p.N, p.ldb);
+  // ---- DMA plans: A_FIRST / A_SEC 2 pieces each, B 4 pieces per wave
+  DmaLane<2> daf, das;
+  DmaLane<4> db;
+  dma_plan<AK, 2>(daf, A_FIRST, 0, wid, lane, m0, p.M, p.lda);
+  dma_plan<AK, 2>(das, A_SEC, 0, wid, lane, m0, p.M, p.lda);
+  dma_plan<BK, 4>(db, B_ALL, 0, wid, lane, n0, p.N, p.ldb);
 
   const int nk = (p.K + BKT - 1) / BKT;
   auto sA = [&](int kt) { return smem + (kt & 1) * STAGE; };
   auto sB = [&](int kt) { return smem + (kt & 1) * STAGE + OPND; };
+#define DMA_AF(kt) dma_issue<AK, 2>(daf, rsA, sA(kt), A_FIRST, 0, wid, (kt), p.K, p.lda)
+#define DMA_AS(kt) dma_issue<AK, 2>(das, rsA, sA(kt), A_SEC, 0, wid, (kt), p.K, p.lda)
+#define DMA_B(kt) dma_issue<BK, 4>(db, rsB, sB(kt), B_ALL, 0, wid, (kt), p.K, p.ldb)
 
-  // ---- prologue: k-tile 0 complete, k-tile 1 first regions (issue order matters
-  // for the counted waits: A_first(0) Bp1(0) Bp2(0) A_sec(0) A_first(1) Bp1(1))
-  dma_issue<AK>(da, 0, rsA, sA(0), A_FIRST, wid, 0, p.K, p.lda);
-  dma_issue<BK>(db, 0, rsB, sB(0), B_P1, wid, 0, p.K, p.ldb);
-  dma_issue<BK>(db, 1, rsB, sB(0), B_P2, wid, 0, p.K, p.ldb);
-  dma_issue<AK>(da, 1, rsA, sA(0), A_SEC, wid, 0, p.K, p.lda);
-  dma_issue<AK>(da, 0, rsA, sA(1), A_FIRST, wid, 1, p.K, p.lda);
-  dma_issue<BK>(db, 0, rsB, sB(1), B_P1, wid, 1, p.K, p.ldb);
-  wait_vm8();
+  // ---- prologue, in the steady-state issue order (the counted waits depend on it):
+  //   A_first(0) B(0) A_sec(0) A_first(1) B(1); loop k-tile t issues A_sec(t+1) in
+  //   phase 2, A_first(t+2) in phase 3, B(t+2) in phase 4.
+  DMA_AF(0);
+  DMA_B(0);
+  DMA_AS(0);
+  DMA_AF(1);
+  DMA_B(1);
+  wait_vm8();  // A_first(0), B(0) landed
   bar();
   if (wr == 1) bar();  // stagger: group 1 runs one barrier behind group 0
 
@@ -229,8 +272,9 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
-  const int ua0 = 4 * wr, ub0 = 2 * wc;
+  Frag<AK> fa[4][2];
+  Frag<BK> fb0[2][2], fb1[2][2];
+  const int ua0 = 4 * wr, ub0 = 2 * wc;  // 32-mn blocks of this wave
 
   for (int kt = 0; kt < nk; ++kt) {
     const char* A_ = sA(kt);
@@ -239,14 +283,14 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) fa[i][kk] = frag<AK>(A_ + (ua0 + (i >> 1)) * UNIT, i & 1, kk, lane);
+      for (int kk = 0; kk < 2; ++kk) fa[i][kk].load(A_, ua0 + (i >> 1), i & 1, kk, lane);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) fb0[i][kk] = frag<BK>(B_ + ub0 * UNIT, i, kk, lane);
-    wait_vm6();
-    dma_issue<BK>(db, 1, rsB, sB(kt + 1), B_P2, wid, kt + 1, p.K, p.ldb);
+      for (int kk = 0; kk < 2; ++kk) fb0[i][kk].load(B_, ub0, i, kk, lane);
     bar();
+    WAIT_FRAGS(fa, 4);
+    WAIT_FRAGS(fb0, 2);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -254,17 +298,18 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][kk], fa[i][kk], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][kk].get(), fa[i][kk].get(), acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     bar();
     // ---------------- phase 2: quadrant (rows 0-63, cols 32-63)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) fb1[i][kk] = frag<BK>(B_ + (ub0 + 1) * UNIT, i, kk, lane);
-    wait_vm6();
-    dma_issue<AK>(da, 1, rsA, sA(kt + 1), A_SEC, wid, kt + 1, p.K, p.lda);
+      for (int kk = 0; kk < 2; ++kk) fb1[i][kk].load(B_, ub0 + 1, i, kk, lane);
+    wait_vm6();  // A_sec(kt) landed (read in phase 3)
+    DMA_AS(kt + 1);
     bar();
+    WAIT_FRAGS(fb1, 2);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -272,17 +317,17 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][kk], fa[i][kk], acc[i][2 + j], 0, 0, 0);
+          acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][kk].get(), fa[i][kk].get(), acc[i][2 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     bar();
     // ---------------- phase 3: quadrant (rows 64-127, cols 32-63)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) fa[i][kk] = frag<AK>(A_ + (ua0 + 2 + (i >> 1)) * UNIT, i & 1, kk, lane);
-    wait_vm6();
-    dma_issue<AK>(da, 0, rsA, sA(kt + 2), A_FIRST, wid, kt + 2, p.K, p.lda);
+      for (int kk = 0; kk < 2; ++kk) fa[i][kk].load(A_, ua0 + 2 + (i >> 1), i & 1, kk, lane);
+    DMA_AF(kt + 2);
     bar();
+    WAIT_FRAGS(fa, 4);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -290,12 +335,12 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][kk], fa[i][kk], acc[4 + i][2 + j], 0, 0, 0);
+          acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][kk].get(), fa[i][kk].get(), acc[4 + i][2 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     bar();
     // ---------------- phase 4: quadrant (rows 64-127, cols 0-31)
-    wait_vm6();
-    dma_issue<BK>(db, 0, rsB, sB(kt + 2), B_P1, wid, kt + 2, p.K, p.ldb);
+    wait_vm4();  // A_first(kt+1), B(kt+1) landed (read in the next phase 1)
+    DMA_B(kt + 2);
     bar();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -304,10 +349,13 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][kk], fa[i][kk], acc[4 + i][j], 0, 0, 0);
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][kk].get(), fa[i][kk].get(), acc[4 + i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     bar();
   }
+#undef DMA_AF
+#undef DMA_AS
+#undef DMA_B
   if (wr == 0) bar();  // match group 1's extra barrier
   wait_vm0();          // drain the zero-filling DMAs past the last k-tile
 
