@@ -39,7 +39,7 @@ constexpr int BM = 256, BN = 256, BKT = 64, NT = 512;
 constexpr int UNIT = 4096;            // bytes: 32 (mn) x 64 (k) bf16
 constexpr int OPND = 8 * UNIT;        // one operand of one stage (256 x 64 bf16)
 constexpr int STAGE = 2 * OPND;       // A + B
-constexpr int LDS_BYTES = 2 * STAGE;  // 128 KiB
+constexpr int LDS_BYTES = 256 * 528;  // 2 stages (128 KiB) or the padded bf16 C tile (132 KiB)
 constexpr unsigned OOB = 0xFFFFFFF0u; // voffset beyond num_records -> DMA writes zeros
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -357,56 +357,95 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
 #undef DMA_AS
 #undef DMA_B
   if (wr == 0) bar();  // match group 1's extra barrier
-  wait_vm0();          // drain the zero-filling DMAs past the last k-tile
+  wait_vm0();          // drain the zero-filling DMAs past the last k-tile (they write LDS)
 
-  // ---- epilogue: lane holds C[m = .. + (l&15)][n = .. + 4(l>>4) + r], r = 0..3
+  // ---- epilogue, staged through LDS so every global access is a full-line 16-B
+  // vector (per-lane fragments would store 32 B per row and 16 rows per
+  // instruction; the store tail is issue-bound, guide T21).  Lane holds
+  // C[m = .. + (l&15)][n = .. + 4(l>>4) + r], r = 0..3.  bf16: the whole 256x256 tile
+  // in one pass (rows of 512 B + 16 B pad: conflict-free ds_write_b64); fp32: two
+  // passes of 128 rows (rows of 1024 + 16 B), one per wave group.
+  __builtin_amdgcn_s_barrier();  // every wave drained its DMAs (above): LDS is free
   const long cz = bz * p.sC;
-  const int mrow = m0 + 128 * wr + (lane & 15);
-  const int ncol = n0 + 64 * wc + 4 * (lane >> 4);
+  constexpr int ROWB = OUTF32 ? 1040 : 528;
+  const int ml = 16 * 0 + (lane & 15);
+  const int nl = 64 * wc + 4 * (lane >> 4);
+  float bv[4][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = ncol + 16 * j;
-    if (n >= p.N) continue;
-    float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (p.bias) {
-      if (OUTF32) {
-        const f32x4 b4 = *reinterpret_cast<const f32x4*>((const float*)p.bias + n);
+  for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bv[r] = b4[r];
-      } else {
-        const u16x4 b4 = *reinterpret_cast<const u16x4*>((const u16*)p.bias + n);
+    for (int r = 0; r < 4; ++r) bv[j][r] = 0.f;
+  if (p.bias) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bv[r] = bf2f(b4[r]);
-      }
-    }
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + nl + 16 * j;
+      if (n < p.N) {
+        if (OUTF32) {
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>((const float*)p.bias + n);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = mrow + 16 * i;
-      if (m >= p.M) continue;
-      const long off = cz + (long)m * p.ldc + n;
-      if (OUTF32) {
-        float* c = (float*)p.C + off;
-        f32x4 v;
+          for (int r = 0; r < 4; ++r) bv[j][r] = b4[r];
+        } else {
+          const u16x4 b4 = *reinterpret_cast<const u16x4*>((const u16*)p.bias + n);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = p.alpha * acc[i][j][r] + bv[r];
-        if (p.accumulate) v += *reinterpret_cast<const f32x4*>(c);
-        *reinterpret_cast<f32x4*>(c) = v;
-      } else {
-        u16* c = (u16*)p.C + off;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = p.alpha * acc[i][j][r] + bv[r];
-        if (p.accumulate) {
-          const u16x4 o = *reinterpret_cast<const u16x4*>(c);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] += bf2f(o[r]);
+          for (int r = 0; r < 4; ++r) bv[j][r] = bf2f(b4[r]);
         }
-        uint2 w;
-        w.x = pack2bf(v[0], v[1]);
-        w.y = pack2bf(v[2], v[3]);
-        *reinterpret_cast<uint2*>(c) = w;
       }
     }
+  }
+  constexpr int PASSES = OUTF32 ? 2 : 1;
+#pragma unroll
+  for (int ps = 0; ps < PASSES; ++ps) {
+    // (a) fragments -> LDS
+    if (!OUTF32 || wr == ps) {
+      const int rbase = OUTF32 ? 0 : 128 * wr;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          char* dst = smem + (rbase + 16 * i + ml) * ROWB + (nl + 16 * j) * (OUTF32 ? 4 : 2);
+          if (OUTF32) {
+            f32x4 v;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = p.alpha * acc[i][j][r] + bv[j][r];
+            *reinterpret_cast<f32x4*>(dst) = v;
+          } else {
+            uint2 w;
+            w.x = pack2bf(p.alpha * acc[i][j][0] + bv[j][0], p.alpha * acc[i][j][1] + bv[j][1]);
+            w.y = pack2bf(p.alpha * acc[i][j][2] + bv[j][2], p.alpha * acc[i][j][3] + bv[j][3]);
+            *reinterpret_cast<uint2*>(dst) = w;
+          }
+        }
+    }
+    __syncthreads();
+    // (b) LDS rows -> global, 16 B per lane, consecutive lanes along a row
+    constexpr int CPR = OUTF32 ? 64 : 32;           // 16-B chunks per 256-wide row
+    constexpr int ROWS = OUTF32 ? 128 : 256;        // rows staged in this pass
+    constexpr int RPI = NT / CPR;                   // rows per iteration
+#pragma unroll 4
+    for (int it = 0; it < ROWS / RPI; ++it) {
+      const int rr = it * RPI + tid / CPR, ch = tid % CPR;
+      const int m = m0 + (OUTF32 ? 128 * ps : 0) + rr;
+      const int n = n0 + ch * (OUTF32 ? 4 : 8);
+      const f32x4 v = *reinterpret_cast<const f32x4*>(smem + rr * ROWB + ch * 16);
+      if (m < p.M && n < p.N) {
+        char* g = (char*)p.C + (cz + (long)m * p.ldc + n) * (OUTF32 ? 4 : 2);
+        if (OUTF32) {
+          f32x4 o = v;
+          if (p.accumulate) o += *reinterpret_cast<const f32x4*>(g);
+          *reinterpret_cast<f32x4*>(g) = o;
+        } else if (p.accumulate) {
+          const u16x8 o = *reinterpret_cast<const u16x8*>(g);
+          const u16x8 c = __builtin_bit_cast(u16x8, v);
+          u16x8 w;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) w[e] = f2bf(bf2f(c[e]) + bf2f(o[e]));
+          *reinterpret_cast<u16x8*>(g) = w;
+        } else {
+          *reinterpret_cast<f32x4*>(g) = v;
+        }
+      }
+    }
+    if (PASSES > 1) __syncthreads();
   }
 }
 
