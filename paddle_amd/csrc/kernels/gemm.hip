@@ -211,7 +211,14 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   _Pragma("unroll") for (int i_ = 0; i_ < NI; ++i_) \
     _Pragma("unroll") for (int k_ = 0; k_ < 2; ++k_) F[i_][k_].wait();
 
-template <bool AK, bool BK, bool OUTF32>
+// PF_IN_CLUSTER: schedule variant.  false = every fragment is read in a load
+// section (phase 1 reads A rows 0-63 and B cols 0-31, phase 2 B cols 32-63, phase 3
+// A rows 64-127); true = only B cols 0-31 are read in a load section, the rest are
+// prefetched inside the preceding MFMA cluster (A double-buffered).  Measured
+// (profiles/r2_gemm_v4_sched_ab.jsonl): the prefetch schedule wins ~5 % when both
+// operands take transposed reads (24 tr_b16 in one phase-1 load section
+// otherwise), and loses 2-5 % when an operand is K-major.
+template <bool AK, bool BK, bool OUTF32, bool PF_IN_CLUSTER = (!AK && !BK)>
 __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -255,8 +262,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
 #define DMA_B(kt) dma_issue<BK, 4>(db, rsB, sB(kt), B_ALL, 0, wid, (kt), p.K, p.ldb)
 
   // ---- prologue, in the steady-state issue order (the counted waits depend on it):
-  //   A_first(0) B(0) A_sec(0) A_first(1) B(1); loop k-tile t issues A_sec(t+1) in
-  //   phase 2, A_first(t+2) in phase 3, B(t+2) in phase 4.
+  //   A_first(0) B(0) A_sec(0) A_first(1) B(1); the loop at k-tile t issues
+  //   A_sec(t+1) in phase 2, A_first(t+2) in phase 3, B(t+2) in phase 4.
   DMA_AF(0);
   DMA_B(0);
   DMA_AS(0);
@@ -264,94 +271,175 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   DMA_B(1);
   wait_vm8();  // A_first(0), B(0) landed
   bar();
-  if (wr == 1) bar();  // stagger: group 1 runs one barrier behind group 0
 
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (!PF_IN_CLUSTER) {
+    if (wr == 1) bar();  // stagger: group 1 runs one barrier behind group 0
 
-  Frag<AK> fa[4][2];
-  Frag<BK> fb0[2][2], fb1[2][2];
-  const int ua0 = 4 * wr, ub0 = 2 * wc;  // 32-mn blocks of this wave
+    Frag<AK> fa[4][2];
+    Frag<BK> fb0[2][2], fb1[2][2];
+    const int ua0 = 4 * wr, ub0 = 2 * wc;  // 32-mn blocks of this wave
 
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* A_ = sA(kt);
-    const char* B_ = sB(kt);
-    // ---------------- phase 1: quadrant (rows 0-63, cols 0-31)
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* A_ = sA(kt);
+      const char* B_ = sB(kt);
+      // ---------------- phase 1: quadrant (rows 0-63, cols 0-31)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) fa[i][kk].load(A_, ua0 + (i >> 1), i & 1, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) fb0[i][kk].load(B_, ub0, i, kk, lane);
+      bar();
+      WAIT_FRAGS(fa, 4);
+      WAIT_FRAGS(fb0, 2);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][kk].get(), fa[i][kk].get(), acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      bar();
+      // ---------------- phase 2: quadrant (rows 0-63, cols 32-63)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) fb1[i][kk].load(B_, ub0 + 1, i, kk, lane);
+      wait_vm6();  // A_sec(kt) landed (read in phase 3)
+      DMA_AS(kt + 1);
+      bar();
+      WAIT_FRAGS(fb1, 2);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][kk].get(), fa[i][kk].get(), acc[i][2 + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      bar();
+      // ---------------- phase 3: quadrant (rows 64-127, cols 32-63)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) fa[i][kk].load(A_, ua0 + 2 + (i >> 1), i & 1, kk, lane);
+      DMA_AF(kt + 2);
+      bar();
+      WAIT_FRAGS(fa, 4);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][kk].get(), fa[i][kk].get(), acc[4 + i][2 + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      bar();
+      // ---------------- phase 4: quadrant (rows 64-127, cols 0-31)
+      wait_vm4();  // A_first(kt+1), B(kt+1) landed (read in the next phase 1)
+      DMA_B(kt + 2);
+      bar();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][kk].get(), fa[i][kk].get(), acc[4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      bar();
+    }
+  } else {
+
+    // Fragment registers: fx = A rows 0-63 (A_first), fy = A rows 64-127 (A_sec),
+    // fb0 / fb1 = B cols 0-31 / 32-63 of the wave.  Only fb0 is read in a load
+    // section; fb1, fy and the next k-tile's fx are prefetched INSIDE the MFMA
+    // clusters (one read per 2-4 MFMAs), into registers that cluster does not use.
+    Frag<AK> fx[4][2], fy[4][2];
+    Frag<BK> fb0[2][2], fb1[2][2];
+    const int ua0 = 4 * wr, ub0 = 2 * wc;  // 32-mn blocks of this wave
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) fa[i][kk].load(A_, ua0 + (i >> 1), i & 1, kk, lane);
+      for (int kk = 0; kk < 2; ++kk) fx[i][kk].load(sA(0), ua0 + (i >> 1), i & 1, kk, lane);
+    if (wr == 1) bar();  // stagger: group 1 runs one barrier behind group 0
+
+  // one 64x32 quadrant: 16 MFMAs (kk, i, j order); after MFMA q issue prefetch q/STEP
+  #define QUAD(FA, FB, I0, J0, PF, STEP)                                                          \
+    _Pragma("unroll") for (int q_ = 0; q_ < 16; ++q_) {                                          \
+      const int kk_ = q_ >> 3, i_ = (q_ >> 1) & 3, j_ = q_ & 1;                                  \
+      acc[I0 + i_][J0 + j_] =                                                                    \
+          __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j_][kk_].get(), FA[i_][kk_].get(), acc[I0 + i_][J0 + j_], 0, 0, 0); \
+      if ((q_ % STEP) == STEP - 1) { PF(q_ / STEP); }                                            \
+    }
+  #define NOPF(x) \
+    do {          \
+    } while (0)
+
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* A_ = sA(kt);
+      const char* B_ = sB(kt);
+      const char* An = sA(kt + 1);
+      // ---------------- phase 1: quadrant (rows 0-63, cols 0-31); prefetch B cols 32-63
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) fb0[i][kk].load(B_, ub0, i, kk, lane);
-    bar();
-    WAIT_FRAGS(fa, 4);
-    WAIT_FRAGS(fb0, 2);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][kk].get(), fa[i][kk].get(), acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    bar();
-    // ---------------- phase 2: quadrant (rows 0-63, cols 32-63)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) fb1[i][kk].load(B_, ub0 + 1, i, kk, lane);
-    wait_vm6();  // A_sec(kt) landed (read in phase 3)
-    DMA_AS(kt + 1);
-    bar();
-    WAIT_FRAGS(fb1, 2);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][kk].get(), fa[i][kk].get(), acc[i][2 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    bar();
-    // ---------------- phase 3: quadrant (rows 64-127, cols 32-63)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) fa[i][kk].load(A_, ua0 + 2 + (i >> 1), i & 1, kk, lane);
-    DMA_AF(kt + 2);
-    bar();
-    WAIT_FRAGS(fa, 4);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][kk].get(), fa[i][kk].get(), acc[4 + i][2 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    bar();
-    // ---------------- phase 4: quadrant (rows 64-127, cols 0-31)
-    wait_vm4();  // A_first(kt+1), B(kt+1) landed (read in the next phase 1)
-    DMA_B(kt + 2);
-    bar();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][kk].get(), fa[i][kk].get(), acc[4 + i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    bar();
+        for (int kk = 0; kk < 2; ++kk) fb0[i][kk].load(B_, ub0, i, kk, lane);
+      wait_vm6();  // A_sec(kt) landed (prefetched in phase 2)
+      bar();
+      WAIT_FRAGS(fx, 4);
+      WAIT_FRAGS(fb0, 2);
+      __builtin_amdgcn_s_setprio(1);
+  #define PF1(f) fb1[(f) >> 1][(f) & 1].load(B_, ub0 + 1, (f) >> 1, (f) & 1, lane)
+      QUAD(fx, fb0, 0, 0, PF1, 4)
+  #undef PF1
+      __builtin_amdgcn_s_setprio(0);
+      bar();
+      // ---------------- phase 2: quadrant (rows 0-63, cols 32-63); prefetch A rows 64-127
+      DMA_AS(kt + 1);
+      bar();
+      WAIT_FRAGS(fb1, 2);
+      __builtin_amdgcn_s_setprio(1);
+  #define PF2(f) fy[(f) >> 1][(f) & 1].load(A_, ua0 + 2 + ((f) >> 2), ((f) >> 1) & 1, (f) & 1, lane)
+      QUAD(fx, fb1, 0, 2, PF2, 2)
+  #undef PF2
+      __builtin_amdgcn_s_setprio(0);
+      bar();
+      // ---------------- phase 3: quadrant (rows 64-127, cols 32-63)
+      wait_vm6();  // A_first(kt+1) landed (prefetched in phase 4)
+      DMA_AF(kt + 2);
+      bar();
+      WAIT_FRAGS(fy, 4);
+      __builtin_amdgcn_s_setprio(1);
+      QUAD(fy, fb1, 4, 2, NOPF, 16)
+      __builtin_amdgcn_s_setprio(0);
+      bar();
+      // ---------------- phase 4: quadrant (rows 64-127, cols 0-31); prefetch next A rows 0-63
+      wait_vm4();  // B(kt+1) landed (read in the next phase 1)
+      DMA_B(kt + 2);
+      bar();
+      __builtin_amdgcn_s_setprio(1);
+  #define PF4(f) fx[(f) >> 1][(f) & 1].load(An, ua0 + ((f) >> 2), ((f) >> 1) & 1, (f) & 1, lane)
+      QUAD(fy, fb0, 4, 0, PF4, 2)
+  #undef PF4
+      __builtin_amdgcn_s_setprio(0);
+      bar();
+    }
+    WAIT_FRAGS(fx, 4);  // the last (unused) prefetch must land before LDS is reused
+  #undef QUAD
+  #undef NOPF
   }
 #undef DMA_AF
 #undef DMA_AS
@@ -449,25 +537,36 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   }
 }
 
+static int g_sched = -1;  // -1: per-layout default; 0 / 1: force PF_IN_CLUSTER (A/B runs)
+
+template <bool AK, bool BK, bool F32, bool PF>
+static int launch_v(const Params& p, int batch, hipStream_t st) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_kernel<AK, BK, F32, PF>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((gemm_kernel<AK, BK, F32, PF>), dim3(p.tiles_m * p.tiles_n, batch), dim3(NT), LDS_BYTES, st, p);
+  return (int)hipGetLastError();
+}
+
 template <bool AK, bool BK, bool F32>
 static int launch(const Params& p0, int batch, hipStream_t st) {
   Params p = p0;
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (p.N + BN - 1) / BN;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute((const void*)gemm_kernel<AK, BK, F32>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        LDS_BYTES);
-    attr_set = true;
-  }
-  hipLaunchKernelGGL((gemm_kernel<AK, BK, F32>), dim3(p.tiles_m * p.tiles_n, batch), dim3(NT), LDS_BYTES, st, p);
-  return (int)hipGetLastError();
+  const bool pf = g_sched < 0 ? (!AK && !BK) : g_sched == 1;
+  return pf ? launch_v<AK, BK, F32, true>(p, batch, st) : launch_v<AK, BK, F32, false>(p, batch, st);
 }
 
 }  // namespace gemm
 }  // namespace pa
 
 using namespace pa;
+
+PA_EXPORT void pa_gemm_set_sched(int s) { gemm::g_sched = s; }
 
 // Returns 0 on success, a hipError on launch failure, -1 for an unsupported shape
 // (the caller checks shapes first: M, N, K multiples of 8, 16-B aligned rows,

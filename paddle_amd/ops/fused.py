@@ -15,6 +15,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _native as N
+from . import gemm as _G
 
 # --------------------------------------------------------------------------- utils
 
@@ -646,12 +647,16 @@ def _gelu_tanh(z):
 
 
 def _linear_fwd(x, w, b):
-    """x W (+ b); a 1-D bias rides the GEMM epilogue (addmm) instead of a separate add."""
+    """x W (+ b).  On the GPU: the hand-written MFMA GEMM (ops/gemm.py) with the
+    bias in its epilogue; torch only for shapes that kernel does not cover."""
+    K, Nn = w.shape
+    x2 = x.reshape(-1, K)
+    if _G.supported(x2.shape[0], Nn, K, x2, w):
+        return _G.linear_fwd(x2, w, b).view(*x.shape[:-1], Nn)
     wt = _weight_t(w, x.numel() // max(x.shape[-1], 1))
     wm = wt.t() if wt is not None else w
     if b is None:
         return torch.matmul(x, wm)
-    x2 = x.reshape(-1, x.shape[-1])
     return torch.addmm(b, x2, wm).view(*x.shape[:-1], wm.shape[-1])
 
 
@@ -667,12 +672,24 @@ def _acc_mm(acc, a, b):
 
 
 def _linear_bwd(ctx, x, w, dy, need_dx, need_dw):
+    K, Nn = w.shape
+    dy2 = _c(dy).reshape(-1, Nn)
+    x2 = x.reshape(-1, K)
+    mg = getattr(w, "_pa_main_grad", None)
+    if _G.supported(dy2.shape[0], Nn, K, dy2, w, x2):
+        # dX = dY W^T (both K-major), dW = X^T dY (both MN-major) straight from the
+        # stored layouts; dW accumulates into the fp32 main_grad in the epilogue
+        dx = _G.linear_dx(dy2, w).view(x.shape) if need_dx else None
+        dw = None
+        if need_dw:
+            if mg is not None:
+                _G.linear_dw(x2, dy2, out=mg, accumulate=True)
+            else:
+                dw = _G.linear_dw(x2, dy2, out=torch.empty(K, Nn, dtype=w.dtype, device=w.device))
+        return dx, dw
     dx = torch.matmul(dy, w.t()) if need_dx else None
     dw = None
-    dy2 = dy.reshape(-1, dy.shape[-1])
     if need_dw:
-        x2 = x.reshape(-1, x.shape[-1])
-        mg = getattr(w, "_pa_main_grad", None)
         if _dw_nt_ok(x2, dy2):
             # X^T materialised token-inner, dY as is: the "NN" form, which measured
             # faster than both TN and (X^T, dY^T) NT once the dY transpose is paid
