@@ -652,7 +652,15 @@ def _linear_fwd(x, w, b):
     K, Nn = w.shape
     x2 = x.reshape(-1, K)
     if _G.supported(x2.shape[0], Nn, K, x2, w):
-        return _G.linear_fwd(x2, w, b).view(*x.shape[:-1], Nn)
+        # a K-major copy W^T (refreshed once per optimizer step, reused by every
+        # micro-batch) lets the forward run the both-K-major form, 6-11 % faster
+        # than transposed LDS reads of W (profiles/r2_gemm_v4_sched_ab.jsonl)
+        wt = _weight_t(w, x2.shape[0])
+        if wt is not None:
+            y = _G.gemm(x2, wt, x2.shape[0], Nn, K, a_kmaj=True, b_kmaj=True, bias=b)
+        else:
+            y = _G.linear_fwd(x2, w, b)
+        return y.view(*x.shape[:-1], Nn)
     wt = _weight_t(w, x.numel() // max(x.shape[-1], 1))
     wm = wt.t() if wt is not None else w
     if b is None:
@@ -683,7 +691,10 @@ def _linear_bwd(ctx, x, w, dy, need_dx, need_dw):
         dw = None
         if need_dw:
             if mg is not None:
-                _G.linear_dw(x2, dy2, out=mg, accumulate=True)
+                # the first write after zero_grad() overwrites (no zero fill, no read)
+                fresh = getattr(w, "_pa_grad_fresh", False)
+                _G.linear_dw(x2, dy2, out=mg, accumulate=not fresh)
+                w._pa_grad_fresh = False
             else:
                 dw = _G.linear_dw(x2, dy2, out=torch.empty(K, Nn, dtype=w.dtype, device=w.device))
         return dx, dw
@@ -698,6 +709,9 @@ def _linear_bwd(ctx, x, w, dy, need_dx, need_dw):
             xa, dyb = x2.t(), dy2
         if mg is not None:
             # the engine's post-accumulate hook still fires for w (grad None)
+            if getattr(w, "_pa_grad_fresh", False):
+                mg.zero_()
+                w._pa_grad_fresh = False
             _acc_mm(mg, xa, dyb)
         else:
             dw = torch.matmul(xa, dyb)

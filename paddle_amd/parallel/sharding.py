@@ -121,6 +121,8 @@ class FlatShardedOptimizer:
                     p.grad = g
                 # fused-GEMM gradient accumulation target (ops.linear)
                 p._pa_main_grad = g
+                p._pa_flat_off = o
+                p._pa_grad_fresh = False
         self.buckets = buckets
         # --- shard layout: rank r owns slice r of every bucket
         self.shard_slices = []  # (bucket_start + r*L, L, shard_off)
@@ -177,7 +179,11 @@ class FlatShardedOptimizer:
     def _on_grad(self, p):
         if self.main_grad and p.grad is not None:
             # autograd produced a bf16 gradient (non-fused op): fold it into fp32 main_grad
-            p._pa_main_grad.add_(p.grad)
+            if p._pa_grad_fresh:
+                p._pa_main_grad.copy_(p.grad)
+            else:
+                p._pa_main_grad.add_(p.grad)
+            p._pa_grad_fresh = False
             p.grad = None
         if self.W == 1 or not self._sync:
             return
@@ -190,6 +196,7 @@ class FlatShardedOptimizer:
         if self._launched[b]:
             return
         self._launched[b] = True
+        self._zero_untouched(b)
         bs, be, _ = self.buckets[b]
         s0, L, so = self.shard_slices[b]
         if self.overlap:
@@ -277,6 +284,7 @@ class FlatShardedOptimizer:
         if lr is not None:
             self.lr = lr
         self.sync_params()
+        self._finish_fresh()
         self._finish_comm()
         self.step_count += 1
         gst = self._grad_scale_tensor()
@@ -294,7 +302,34 @@ class FlatShardedOptimizer:
         fused.bump_weight_epoch()
 
     def zero_grad(self, set_to_none=False):
+        if self.main_grad:
+            # lazy zero: the first gradient write of the next step overwrites its
+            # slice (fused dW GEMM with beta = 0, or copy_ in the hook); slices that
+            # receive no gradient are zeroed in _finish_fresh() before they are read
+            for p in self.params:
+                p._pa_grad_fresh = True
+            self._lazy_zero = True
+            return
         self.flat_grad.zero_()
+
+    def _zero_untouched(self, b):
+        """Zero the slices of bucket ``b`` that got no gradient this step (lazy zero)."""
+        if not getattr(self, "_lazy_zero", False):
+            return
+        for p in self.buckets[b][2]:
+            if p._pa_grad_fresh:
+                o = p._pa_flat_off
+                self.flat_grad[o:o + p.numel()].zero_()
+                p._pa_grad_fresh = False
+
+    def _finish_fresh(self):
+        if not getattr(self, "_lazy_zero", False):
+            return
+        self._lazy_zero = False
+        for p, o in zip(self.params, self.offsets):
+            if p._pa_grad_fresh:
+                self.flat_grad[o:o + p.numel()].zero_()
+                p._pa_grad_fresh = False
 
     clear_grad = zero_grad
 

@@ -80,3 +80,28 @@ def test_fp32_main_grad_accumulation_matches_fp64_oracle():
     e16 = (accumulated(None) - oracle).norm() / nrm
     assert e32 < 1e-5, e32
     assert e16 > 10 * e32, (e16, e32)
+
+
+def test_lazy_zero_grad_overwrites_stale_main_grad():
+    """zero_grad() in fp32 main_grad mode does not fill the buffer: the first write
+    of the next backward overwrites each slice (dW GEMM with beta = 0 / copy_)."""
+    from paddle_amd.parallel.sharding import FlatShardedOptimizer
+
+    g = torch.Generator().manual_seed(4)
+    mb1, mb2 = (torch.randint(0, 512, (2, 65), generator=g) for _ in range(2))
+    m = _model()
+    opt = FlatShardedOptimizer(m.named_parameters(), lr=1e-3, grad_dtype=torch.float32)
+    m(mb1[:, :-1], mb1[:, 1:]).backward()
+    opt.zero_grad()
+    m(mb2[:, :-1], mb2[:, 1:]).backward()
+    got = opt.flat_grad.clone()
+    m2 = _model()
+    opt2 = FlatShardedOptimizer(m2.named_parameters(), lr=1e-3, grad_dtype=torch.float32)
+    m2(mb2[:, :-1], mb2[:, 1:]).backward()
+    assert torch.equal(got, opt2.flat_grad)
+    # a step after zero_grad with no backward at all must see zero gradients
+    opt.zero_grad()
+    before = opt.master.clone()
+    opt.wd = 0.0
+    opt.step()
+    assert torch.equal(opt.master, before)
