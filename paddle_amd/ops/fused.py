@@ -10,6 +10,7 @@ the GPU numerics tests compare against.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -679,6 +680,33 @@ def _acc_mm(acc, a, b):
         acc.add_(a.to(acc.dtype) @ b.to(acc.dtype))
 
 
+_DW_SIDE = {}
+_DW_PENDING = set()
+# Off by default: measured 26.7k -> 13.9k tok/s on LLaMA-7B (gpurun_out/r2_bench_pagemm4):
+# two 132-KiB-LDS GEMMs contend for CUs and record_stream() delays frees.
+_DW_SIDE_ENABLED = os.environ.get("PADDLE_AMD_DW_STREAM", "0") == "1"
+
+
+def _dw_side_stream(dev):
+    if not (_DW_SIDE_ENABLED and dev.type == "cuda"):
+        return None
+    s = _DW_SIDE.get(dev)
+    if s is None:
+        s = _DW_SIDE[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def join_dw_streams(device=None):
+    """Make the current stream wait for every dW GEMM issued on the side stream
+    (call before reading main_grad: optimizer step, gradient reduce-scatter)."""
+    if not _DW_PENDING:
+        return
+    for dev in list(_DW_PENDING):
+        if device is None or dev == device:
+            torch.cuda.current_stream(dev).wait_stream(_DW_SIDE[dev])
+            _DW_PENDING.discard(dev)
+
+
 def _linear_bwd(ctx, x, w, dy, need_dx, need_dw):
     K, Nn = w.shape
     dy2 = _c(dy).reshape(-1, Nn)
@@ -693,8 +721,24 @@ def _linear_bwd(ctx, x, w, dy, need_dx, need_dw):
             if mg is not None:
                 # the first write after zero_grad() overwrites (no zero fill, no read)
                 fresh = getattr(w, "_pa_grad_fresh", False)
-                _G.linear_dw(x2, dy2, out=mg, accumulate=not fresh)
                 w._pa_grad_fresh = False
+                side = _dw_side_stream(w.device)
+                if side is None:
+                    _G.linear_dw(x2, dy2, out=mg, accumulate=not fresh)
+                else:
+                    # dW is a leaf of the backward graph: run it on a side stream so it
+                    # fills the CUs the dX chain leaves idle (partial last rounds of
+                    # 688/1376-tile dW grids, launch gaps); readers of main_grad join
+                    # the side stream first (join_dw_streams)
+                    side.wait_stream(torch.cuda.current_stream(w.device))
+                    with torch.cuda.stream(side):
+                        _G.linear_dw(x2, dy2, out=mg, accumulate=not fresh)
+                    x2.record_stream(side)
+                    dy2.record_stream(side)
+                    if not _DW_PENDING:
+                        # everything after this backward pass sees finished dW
+                        torch.autograd.Variable._execution_engine.queue_callback(join_dw_streams)
+                    _DW_PENDING.add(w.device)
             else:
                 dw = _G.linear_dw(x2, dy2, out=torch.empty(K, Nn, dtype=w.dtype, device=w.device))
         return dx, dw

@@ -197,6 +197,8 @@ class FlatShardedOptimizer:
             return
         self._launched[b] = True
         self._zero_untouched(b)
+        if self.device.type == "cuda":
+            fused.join_dw_streams(self.device)
         bs, be, _ = self.buckets[b]
         s0, L, so = self.shard_slices[b]
         if self.overlap:
@@ -284,6 +286,8 @@ class FlatShardedOptimizer:
         if lr is not None:
             self.lr = lr
         self.sync_params()
+        if self.device.type == "cuda":
+            fused.join_dw_streams(self.device)
         self._finish_fresh()
         self._finish_comm()
         self.step_count += 1
