@@ -1,5 +1,7 @@
-"""A/B of the two pa_gemm schedules (load-section reads vs in-cluster prefetch) per
-form on the LLaMA-7B shapes, interleaved in one process (guide §5.4 rule 24)."""
+"""A/B of pa_gemm variants per form on the LLaMA-7B shapes, interleaved in one
+process (guide §5.4 rule 24).  usage: gemm_sched_ab.py [sched|persistent]
+  sched: load-section reads (0) vs in-cluster prefetch (1)
+  persistent: one tile per block (0) vs persistent blocks (1)"""
 import json
 import os
 import sys
@@ -24,6 +26,9 @@ def timeit(fn, reps=5):
     return e0.elapsed_time(e1) / reps
 
 
+what = sys.argv[1] if len(sys.argv) > 1 else "sched"
+setter = N.lib().pa_gemm_set_sched if what == "sched" else N.lib().pa_gemm_set_persistent
+default = -1 if what == "sched" else 1
 for name, (K, Nn) in SHAPES.items():
     x = torch.randn(T, K, device="cuda").to(torch.bfloat16)
     w = (torch.randn(K, Nn, device="cuda") * 0.02).to(torch.bfloat16)
@@ -35,10 +40,10 @@ for name, (K, Nn) in SHAPES.items():
         res = {0: [], 1: []}
         for r in range(6):
             for sch in (0, 1):
-                N.lib().pa_gemm_set_sched(sch)
+                setter(sch)
                 f()
                 res[sch].append(timeit(f))
-        N.lib().pa_gemm_set_sched(-1)
+        setter(default)
         med = {k: sorted(v)[len(v) // 2] for k, v in res.items()}
-        print(json.dumps({"shape": name, "form": form, "load_section_ms": round(med[0], 4),
-                          "prefetch_ms": round(med[1], 4), "prefetch_speedup": round(med[0] / med[1], 3)}), flush=True)
+        print(json.dumps({"ab": what, "shape": name, "form": form, "off_ms": round(med[0], 4),
+                          "on_ms": round(med[1], 4), "on_speedup": round(med[0] / med[1], 3)}), flush=True)

@@ -39,7 +39,7 @@ constexpr int BM = 256, BN = 256, BKT = 64, NT = 512;
 constexpr int UNIT = 4096;            // bytes: 32 (mn) x 64 (k) bf16
 constexpr int OPND = 8 * UNIT;        // one operand of one stage (256 x 64 bf16)
 constexpr int STAGE = 2 * OPND;       // A + B
-constexpr int LDS_BYTES = 256 * 528;  // 2 stages (128 KiB) or the padded bf16 C tile (132 KiB)
+constexpr int LDS_BYTES = STAGE + 128 * 528;  // 2 stages (128 KiB); C staging above stage 0
 constexpr unsigned OOB = 0xFFFFFFF0u; // voffset beyond num_records -> DMA writes zeros
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -101,39 +101,44 @@ __device__ __forceinline__ void region_piece(int region, int wid, int j, int& sl
   }
 }
 
-template <int NP>
+// One wave's DMA plan for one region: byte offset of each piece at k-tile 0 (OOB
+// when its mn row/col is outside the matrix) and, for K not a multiple of 64, the
+// k coordinate within the tile for the per-lane range check of the last k-tile.
+template <int NP, bool KFULL>
 struct DmaLane {
-  unsigned off[NP];  // byte offset at k-tile 0
-  int kk[NP];        // k coordinate within the tile
-  bool mnok[NP];
+  unsigned off[NP];
+  int kk[KFULL ? 1 : NP];
 };
 
-template <bool KMAJ, int NP>
-__device__ __forceinline__ void dma_plan(DmaLane<NP>& d, int region, int j0, int wid, int lane, int mn_tile0,
-                                         int MN, long ld) {
+template <bool KMAJ, int NP, bool KFULL>
+__device__ __forceinline__ void dma_plan(DmaLane<NP, KFULL>& d, int region, int j0, int wid, int lane,
+                                         int mn_tile0, int MN, long ld) {
 #pragma unroll
   for (int j = 0; j < NP; ++j) {
     int sl, pc, mn, k;
     region_piece(region, wid, j0 + j, sl, pc);
     dma_coords<KMAJ>(sl, pc, lane, mn, k);
     const int gmn = mn_tile0 + mn;
-    d.mnok[j] = gmn < MN;
-    d.kk[j] = k;
-    d.off[j] = KMAJ ? (unsigned)(((long)gmn * ld + k) * 2) : (unsigned)(((long)k * ld + gmn) * 2);
+    if (!KFULL) d.kk[j] = k;
+    d.off[j] = gmn >= MN ? OOB
+                         : (KMAJ ? (unsigned)(((long)gmn * ld + k) * 2) : (unsigned)(((long)k * ld + gmn) * 2));
   }
 }
 
-// Issue this wave's pieces j0 .. j0+NP-1 of `region` for k-tile kt.
-template <bool KMAJ, int NP>
-__device__ __forceinline__ void dma_issue(const DmaLane<NP>& d, __amdgpu_buffer_rsrc_t rs, char* stage_opnd,
+// Issue this wave's pieces j0 .. j0+NP-1 of `region` for k-tile kt (kt >= nk: the
+// whole wave writes zeros, no memory traffic).
+template <bool KMAJ, int NP, bool KFULL>
+__device__ __forceinline__ void dma_issue(const DmaLane<NP, KFULL>& d, __amdgpu_buffer_rsrc_t rs, char* stage_opnd,
                                           int region, int j0, int wid, int kt, int K, long ld) {
   const int k0 = kt * BKT;
   const unsigned kstep = KMAJ ? (unsigned)(k0 * 2) : (unsigned)((long)k0 * ld * 2);
+  const bool kt_ok = k0 < K;  // wave-uniform
 #pragma unroll
   for (int j = 0; j < NP; ++j) {
     int sl, pc;
     region_piece(region, wid, j0 + j, sl, pc);
-    const bool ok = d.mnok[j] && (k0 + d.kk[j] < K);
+    bool ok = kt_ok && d.off[j] != OOB;
+    if (!KFULL) ok = ok && (k0 + d.kk[j] < K);
     const unsigned vo = ok ? d.off[j] + kstep : OOB;
     char* dst = stage_opnd + sl * 8192 + pc * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16, vo, 0, 0, 0);
@@ -218,24 +223,14 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // (profiles/r2_gemm_v4_sched_ab.jsonl): the prefetch schedule wins ~5 % when both
 // operands take transposed reads (24 tr_b16 in one phase-1 load section
 // otherwise), and loses 2-5 % when an operand is K-major.
-template <bool AK, bool BK, bool OUTF32, bool PF_IN_CLUSTER = (!AK && !BK)>
+template <bool AK, bool BK, bool OUTF32, bool PF_IN_CLUSTER, bool KFULL>
 __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 2, wc = wid & 3;
 
-  // ---- tile of this block: XCD remap, then bands of 8 tile-rows for L2 reuse
   const int nwg = p.tiles_m * p.tiles_n;
-  const int t = xcd_remap(blockIdx.x, nwg);
-  constexpr int GM = 8;
-  const int band = t / (GM * p.tiles_n);
-  const int m_in_band = min(GM, p.tiles_m - band * GM);
-  const int tin = t - band * GM * p.tiles_n;
-  const int tm = band * GM + tin % m_in_band;
-  const int tn = tin / m_in_band;
-  const int m0 = tm * BM, n0 = tn * BN;
-
   const long bz = blockIdx.y;
   const char* Ab = (const char*)p.A + bz * p.sA * 2;
   const char* Bb = (const char*)p.B + bz * p.sB * 2;
@@ -247,29 +242,55 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, 0, a_bytes, 0x00020000);
   const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, 0, b_bytes, 0x00020000);
 
+  // ---- persistent tiles: virtual block vb = blockIdx.x + i * gridDim.x; XCD remap
+  // (gridDim.x is a multiple of 8 or covers every tile, so a block keeps its XCD
+  // group), then bands of 8 tile-rows for L2 reuse
+  auto tile_of = [&](int vb, int& tm0, int& tn0) {
+    const int t = xcd_remap(vb, nwg);
+    constexpr int GM = 8;
+    const int band = t / (GM * p.tiles_n);
+    const int m_in_band = min(GM, p.tiles_m - band * GM);
+    const int tin = t - band * GM * p.tiles_n;
+    tm0 = (band * GM + tin % m_in_band) * BM;
+    tn0 = (tin / m_in_band) * BN;
+  };
+
   // ---- DMA plans: A_FIRST / A_SEC 2 pieces each, B 4 pieces per wave
-  DmaLane<2> daf, das;
-  DmaLane<4> db;
-  dma_plan<AK, 2>(daf, A_FIRST, 0, wid, lane, m0, p.M, p.lda);
-  dma_plan<AK, 2>(das, A_SEC, 0, wid, lane, m0, p.M, p.lda);
-  dma_plan<BK, 4>(db, B_ALL, 0, wid, lane, n0, p.N, p.ldb);
+  DmaLane<2, KFULL> daf, das;
+  DmaLane<4, KFULL> db;
+  auto plan = [&](int mm0, int nn0) {
+    dma_plan<AK, 2, KFULL>(daf, A_FIRST, 0, wid, lane, mm0, p.M, p.lda);
+    dma_plan<AK, 2, KFULL>(das, A_SEC, 0, wid, lane, mm0, p.M, p.lda);
+    dma_plan<BK, 4, KFULL>(db, B_ALL, 0, wid, lane, nn0, p.N, p.ldb);
+  };
 
   const int nk = (p.K + BKT - 1) / BKT;
   auto sA = [&](int kt) { return smem + (kt & 1) * STAGE; };
   auto sB = [&](int kt) { return smem + (kt & 1) * STAGE + OPND; };
-#define DMA_AF(kt) dma_issue<AK, 2>(daf, rsA, sA(kt), A_FIRST, 0, wid, (kt), p.K, p.lda)
-#define DMA_AS(kt) dma_issue<AK, 2>(das, rsA, sA(kt), A_SEC, 0, wid, (kt), p.K, p.lda)
-#define DMA_B(kt) dma_issue<BK, 4>(db, rsB, sB(kt), B_ALL, 0, wid, (kt), p.K, p.ldb)
+#define DMA_AF(kt) dma_issue<AK, 2, KFULL>(daf, rsA, sA(kt), A_FIRST, 0, wid, (kt), p.K, p.lda)
+#define DMA_AS(kt) dma_issue<AK, 2, KFULL>(das, rsA, sA(kt), A_SEC, 0, wid, (kt), p.K, p.lda)
+#define DMA_B(kt) dma_issue<BK, 4, KFULL>(db, rsB, sB(kt), B_ALL, 0, wid, (kt), p.K, p.ldb)
 
-  // ---- prologue, in the steady-state issue order (the counted waits depend on it):
+  // ---- DMA issue order (the counted waits depend on it):
   //   A_first(0) B(0) A_sec(0) A_first(1) B(1); the loop at k-tile t issues
-  //   A_sec(t+1) in phase 2, A_first(t+2) in phase 3, B(t+2) in phase 4.
+  //   A_sec(t+1) in phase 2, A_first(t+2) in phase 3, B(t+2) in phase 4.  A tile's
+  //   k-tile 0 is issued before the previous tile's epilogue, so its latency hides
+  //   under the epilogue (which stages C in LDS above stage 0).
+  int vb = blockIdx.x, m0, n0;
+  tile_of(vb, m0, n0);
+  plan(m0, n0);
   DMA_AF(0);
   DMA_B(0);
   DMA_AS(0);
+  bool first = true;
+  for (;;) {
   DMA_AF(1);
   DMA_B(1);
-  wait_vm8();  // A_first(0), B(0) landed
+  if (first) {
+    wait_vm8();  // A_first(0), B(0) landed
+  } else {
+    wait_vm6();  // k-tile 0 and the previous epilogue's memory ops retired
+  }
   bar();
 
   f32x4 acc[8][4];
@@ -441,22 +462,33 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   #undef QUAD
   #undef NOPF
   }
-#undef DMA_AF
-#undef DMA_AS
-#undef DMA_B
   if (wr == 0) bar();  // match group 1's extra barrier
   wait_vm0();          // drain the zero-filling DMAs past the last k-tile (they write LDS)
+  __builtin_amdgcn_s_barrier();  // every wave drained its DMAs: LDS is free
 
-  // ---- epilogue, staged through LDS so every global access is a full-line 16-B
-  // vector (per-lane fragments would store 32 B per row and 16 rows per
-  // instruction; the store tail is issue-bound, guide T21).  Lane holds
-  // C[m = .. + (l&15)][n = .. + 4(l>>4) + r], r = 0..3.  bf16: the whole 256x256 tile
-  // in one pass (rows of 512 B + 16 B pad: conflict-free ds_write_b64); fp32: two
-  // passes of 128 rows (rows of 1024 + 16 B), one per wave group.
-  __builtin_amdgcn_s_barrier();  // every wave drained its DMAs (above): LDS is free
+  // next tile's k-tile 0 (stage 0) goes out now and lands under this epilogue
+  const int vb_next = vb + (int)gridDim.x;
+  const bool has_next = vb_next < nwg;
+  int m0n = 0, n0n = 0;
+  if (has_next) {
+    tile_of(vb_next, m0n, n0n);
+    plan(m0n, n0n);
+    DMA_AF(0);
+    DMA_B(0);
+    DMA_AS(0);
+  }
+
+  // ---- epilogue, staged through LDS (above stage 0) so every global access is a
+  // full-line 16-B vector (per-lane fragments would store 32 B per row and 16 rows
+  // per instruction; the store tail is issue-bound, guide T21).  Lane holds
+  // C[m = .. + (l&15)][n = .. + 4(l>>4) + r], r = 0..3.  bf16: 2 passes of 128 rows
+  // (512 B + 16 B pad: conflict-free ds_write_b64), one per wave group; fp32: 4
+  // passes of 64 rows (1024 + 16 B).
+  {
+  char* stg = smem + STAGE;
   const long cz = bz * p.sC;
   constexpr int ROWB = OUTF32 ? 1040 : 528;
-  const int ml = 16 * 0 + (lane & 15);
+  const int ml = lane & 15;
   const int nl = 64 * wc + 4 * (lane >> 4);
   float bv[4][4];
 #pragma unroll
@@ -480,41 +512,42 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
       }
     }
   }
-  constexpr int PASSES = OUTF32 ? 2 : 1;
+  // pass ps stages m-tiles [PI*ps, PI*ps + PI) of BOTH wave groups, so each pass
+  // retires a slice of every wave's accumulators (register pressure falls as it goes)
+  constexpr int PASSES = OUTF32 ? 4 : 2;
+  constexpr int PI = 8 / PASSES;           // 16-row m-tiles per group per pass
+  constexpr int GR = 16 * PI;              // staged rows per group per pass
 #pragma unroll
   for (int ps = 0; ps < PASSES; ++ps) {
-    // (a) fragments -> LDS
-    if (!OUTF32 || wr == ps) {
-      const int rbase = OUTF32 ? 0 : 128 * wr;
+    // (a) fragments -> LDS (staged row = GR * wr + 16 * ii + ml)
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+    for (int ii = 0; ii < PI; ++ii)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          char* dst = smem + (rbase + 16 * i + ml) * ROWB + (nl + 16 * j) * (OUTF32 ? 4 : 2);
-          if (OUTF32) {
-            f32x4 v;
+      for (int j = 0; j < 4; ++j) {
+        const int i = PI * ps + ii;
+        char* dst = stg + (GR * wr + 16 * ii + ml) * ROWB + (nl + 16 * j) * (OUTF32 ? 4 : 2);
+        if (OUTF32) {
+          f32x4 v;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = p.alpha * acc[i][j][r] + bv[j][r];
-            *reinterpret_cast<f32x4*>(dst) = v;
-          } else {
-            uint2 w;
-            w.x = pack2bf(p.alpha * acc[i][j][0] + bv[j][0], p.alpha * acc[i][j][1] + bv[j][1]);
-            w.y = pack2bf(p.alpha * acc[i][j][2] + bv[j][2], p.alpha * acc[i][j][3] + bv[j][3]);
-            *reinterpret_cast<uint2*>(dst) = w;
-          }
+          for (int r = 0; r < 4; ++r) v[r] = p.alpha * acc[i][j][r] + bv[j][r];
+          *reinterpret_cast<f32x4*>(dst) = v;
+        } else {
+          uint2 w;
+          w.x = pack2bf(p.alpha * acc[i][j][0] + bv[j][0], p.alpha * acc[i][j][1] + bv[j][1]);
+          w.y = pack2bf(p.alpha * acc[i][j][2] + bv[j][2], p.alpha * acc[i][j][3] + bv[j][3]);
+          *reinterpret_cast<uint2*>(dst) = w;
         }
-    }
+      }
     __syncthreads();
     // (b) LDS rows -> global, 16 B per lane, consecutive lanes along a row
-    constexpr int CPR = OUTF32 ? 64 : 32;           // 16-B chunks per 256-wide row
-    constexpr int ROWS = OUTF32 ? 128 : 256;        // rows staged in this pass
-    constexpr int RPI = NT / CPR;                   // rows per iteration
-#pragma unroll 4
-    for (int it = 0; it < ROWS / RPI; ++it) {
+    constexpr int CPR = OUTF32 ? 64 : 32;  // 16-B chunks per 256-wide row
+    constexpr int RPI = NT / CPR;          // rows per iteration
+#pragma unroll 2
+    for (int it = 0; it < 2 * GR / RPI; ++it) {
       const int rr = it * RPI + tid / CPR, ch = tid % CPR;
-      const int m = m0 + (OUTF32 ? 128 * ps : 0) + rr;
+      const int m = m0 + 128 * (rr / GR) + GR * ps + rr % GR;
       const int n = n0 + ch * (OUTF32 ? 4 : 8);
-      const f32x4 v = *reinterpret_cast<const f32x4*>(smem + rr * ROWB + ch * 16);
+      const f32x4 v = *reinterpret_cast<const f32x4*>(stg + rr * ROWB + ch * 16);
       if (m < p.M && n < p.N) {
         char* g = (char*)p.C + (cz + (long)m * p.ldc + n) * (OUTF32 ? 4 : 2);
         if (OUTF32) {
@@ -533,22 +566,42 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
         }
       }
     }
-    if (PASSES > 1) __syncthreads();
+    __syncthreads();  // staging reads done (next pass / next tile's DMA into stage 1)
   }
+  }
+  if (!has_next) break;
+  vb = vb_next;
+  m0 = m0n;
+  n0 = n0n;
+  first = false;
+  }  // persistent tile loop
+#undef DMA_AF
+#undef DMA_AS
+#undef DMA_B
 }
 
-static int g_sched = -1;  // -1: per-layout default; 0 / 1: force PF_IN_CLUSTER (A/B runs)
+static int g_sched = -1;      // -1: per-layout default; 0 / 1: force PF_IN_CLUSTER (A/B runs)
+static int g_persistent = 1;  // 0: one tile per block (grid = tiles), for A/B runs
 
-template <bool AK, bool BK, bool F32, bool PF>
+template <bool AK, bool BK, bool F32, bool PF, bool KFULL>
 static int launch_v(const Params& p, int batch, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_kernel<AK, BK, F32, PF>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_kernel<AK, BK, F32, PF, KFULL>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemm_kernel<AK, BK, F32, PF>), dim3(p.tiles_m * p.tiles_n, batch), dim3(NT), LDS_BYTES, st, p);
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+    ncu = ncu / 8 * 8;  // keep gridDim.x a multiple of the XCD count
+  }
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int grid = (nwg < ncu || !g_persistent) ? nwg : ncu;  // persistent: one resident block per CU
+  hipLaunchKernelGGL((gemm_kernel<AK, BK, F32, PF, KFULL>), dim3(grid, batch), dim3(NT), LDS_BYTES, st, p);
   return (int)hipGetLastError();
 }
 
@@ -558,7 +611,9 @@ static int launch(const Params& p0, int batch, hipStream_t st) {
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (p.N + BN - 1) / BN;
   const bool pf = g_sched < 0 ? (!AK && !BK) : g_sched == 1;
-  return pf ? launch_v<AK, BK, F32, true>(p, batch, st) : launch_v<AK, BK, F32, false>(p, batch, st);
+  if (p.K % BKT == 0)  // every k-tile full: the k range check is wave-uniform
+    return pf ? launch_v<AK, BK, F32, true, true>(p, batch, st) : launch_v<AK, BK, F32, false, true>(p, batch, st);
+  return pf ? launch_v<AK, BK, F32, true, false>(p, batch, st) : launch_v<AK, BK, F32, false, false>(p, batch, st);
 }
 
 }  // namespace gemm
@@ -567,6 +622,7 @@ static int launch(const Params& p0, int batch, hipStream_t st) {
 using namespace pa;
 
 PA_EXPORT void pa_gemm_set_sched(int s) { gemm::g_sched = s; }
+PA_EXPORT void pa_gemm_set_persistent(int s) { gemm::g_persistent = s; }
 
 // Returns 0 on success, a hipError on launch failure, -1 for an unsupported shape
 // (the caller checks shapes first: M, N, K multiples of 8, 16-B aligned rows,
