@@ -3,7 +3,6 @@ startup-program initialisation, temp vars, bias / activation appending."""
 from __future__ import annotations
 
 import copy
-import itertools
 
 from ..framework import core
 from . import unique_name
@@ -36,18 +35,20 @@ class LayerHelper:
         return self.main_program.current_block().append_op(*args, **kwargs)
 
     def multiple_input(self, input_param_name="input"):
-        inputs = self.kwargs.get(input_param_name, [])
-        if isinstance(inputs, Variable):
-            return [inputs]
-        if isinstance(inputs, (list, tuple)):
-            return list(inputs)
-        raise TypeError(f"{input_param_name} must be Variable or list")
+        """The layer argument ``input_param_name`` as a list of Variables."""
+        got = self.kwargs.get(input_param_name, [])
+        if isinstance(got, Variable):
+            return [got]
+        if not isinstance(got, (list, tuple)):
+            raise TypeError(f"{self.layer_type}: argument {input_param_name!r} must be a Variable or a list "
+                            f"of Variables, got {type(got).__name__}")
+        return list(got)
 
     def input(self, input_param_name="input"):
-        inputs = self.multiple_input(input_param_name)
-        if len(inputs) != 1:
-            raise ValueError(f"{self.layer_type} layer only takes one input")
-        return inputs[0]
+        got = self.multiple_input(input_param_name)
+        if len(got) != 1:
+            raise ValueError(f"{self.layer_type} expects exactly one {input_param_name!r}, got {len(got)}")
+        return got[0]
 
     @property
     def param_attr(self):
@@ -58,33 +59,26 @@ class LayerHelper:
         return ParamAttr._to_attr(self.kwargs.get("bias_attr", None))
 
     def multiple_param_attr(self, length):
-        pa = self.param_attr
-        if isinstance(pa, ParamAttr):
-            pa = [pa]
-        if len(pa) != 1 and len(pa) != length:
-            raise ValueError("parameter number mismatch")
-        if len(pa) == 1 and length != 1:
-            tmp = [None] * length
-            for i in range(length):
-                tmp[i] = copy.deepcopy(pa[0])
-            pa = tmp
-        return pa
+        """One ParamAttr per input: a single attribute is replicated (each copy
+        independent, so generated names differ); otherwise the counts must match."""
+        attrs = self.param_attr
+        attrs = [attrs] if isinstance(attrs, ParamAttr) else list(attrs)
+        if len(attrs) == length:
+            return attrs
+        if len(attrs) == 1:
+            return [copy.deepcopy(attrs[0]) for _ in range(length)]
+        raise ValueError(f"{self.layer_type}: {len(attrs)} param_attr entries for {length} inputs")
 
     def iter_inputs_and_params(self, input_param_name="input"):
-        inputs = self.multiple_input(input_param_name)
-        param_attrs = self.multiple_param_attr(len(inputs))
-        for ipt, pa in zip(inputs, param_attrs):
-            yield ipt, pa
+        ins = self.multiple_input(input_param_name)
+        return zip(ins, self.multiple_param_attr(len(ins)))
 
     def input_dtype(self, input_param_name="input"):
-        inputs = self.multiple_input(input_param_name)
-        dtype = None
-        for each in inputs:
-            if dtype is None:
-                dtype = each.dtype
-            elif dtype != each.dtype:
-                raise ValueError(f"Data Type mismatch: {dtype} to {each.dtype}")
-        return dtype
+        """The common dtype of the inputs (None when there are none)."""
+        dtypes = {v.dtype for v in self.multiple_input(input_param_name)}
+        if len(dtypes) > 1:
+            raise ValueError(f"{self.layer_type}: inputs mix dtypes {sorted(map(str, dtypes))}")
+        return next(iter(dtypes), None)
 
     def create_parameter(self, attr, shape, dtype, is_bias=False, default_initializer=None):
         if attr is False:

@@ -1,4 +1,10 @@
-"""Host-side streaming metrics (python/paddle/fluid/metrics.py)."""
+"""Host-side streaming metrics (API of python/paddle/fluid/metrics.py, written from
+its documented behaviour).
+
+Every metric declares its accumulator fields in ``_STATE`` (name -> zero value);
+``reset`` restores them and ``get_config`` snapshots them, so the base class never
+has to guess which instance attributes are state.  Updates are vectorised numpy.
+"""
 from __future__ import annotations
 
 import copy
@@ -9,58 +15,53 @@ __all__ = ["MetricBase", "CompositeMetric", "Precision", "Recall", "Accuracy", "
            "DetectionMAP", "Auc"]
 
 
-def _is_numpy_(var):
-    return isinstance(var, (np.ndarray, np.generic))
+def _scalar(x):
+    """First element of a number / array / 1-element tensor as a Python number."""
+    return np.asarray(x).reshape(-1)[0].item()
 
 
-def _is_number_(var):
-    return isinstance(var, (int, float, np.integer, np.floating)) or (isinstance(var, np.ndarray) and var.shape == (1,))
-
-
-def _is_number_or_matrix_(var):
-    return _is_number_(var) or isinstance(var, np.ndarray)
+def _check_number_or_array(x, what):
+    if not isinstance(x, (int, float, np.integer, np.floating, np.ndarray)):
+        raise ValueError(f"{what} must be a number or a numpy array, got {type(x).__name__}")
 
 
 class MetricBase:
+    """Base of all metrics: ``update`` accumulates a mini-batch, ``eval`` reports."""
+
+    _STATE: dict = {}
+
     def __init__(self, name):
-        self._name = str(name) if name is not None else self.__class__.__name__
+        self._name = self.__class__.__name__ if name is None else str(name)
+        self.reset()
 
     def __str__(self):
         return self._name
 
     def reset(self):
-        states = {a: v for a, v in self.__dict__.items() if not a.startswith("_")}
-        for attr, value in states.items():
-            if isinstance(value, int):
-                setattr(self, attr, 0)
-            elif isinstance(value, float):
-                setattr(self, attr, 0.0)
-            elif isinstance(value, (np.ndarray, np.generic)):
-                setattr(self, attr, np.zeros_like(value))
-            else:
-                setattr(self, attr, None)
+        for field, zero in self._STATE.items():
+            setattr(self, field, copy.copy(zero))
 
     def get_config(self):
-        states = {a: v for a, v in self.__dict__.items() if not a.startswith("_")}
-        config = {}
-        config.update({"name": self._name, "states": copy.deepcopy(states)})
-        return config
+        return {"name": self._name,
+                "states": {f: copy.deepcopy(getattr(self, f)) for f in self._STATE}}
 
     def update(self, preds, labels):
-        raise NotImplementedError()
+        raise NotImplementedError(f"{type(self).__name__}.update")
 
     def eval(self):
-        raise NotImplementedError()
+        raise NotImplementedError(f"{type(self).__name__}.eval")
 
 
 class CompositeMetric(MetricBase):
+    """Several metrics fed the same (preds, labels)."""
+
     def __init__(self, name=None):
         super().__init__(name)
         self._metrics = []
 
     def add_metric(self, metric):
         if not isinstance(metric, MetricBase):
-            raise ValueError("SubMetric should be inherit from MetricBase.")
+            raise ValueError(f"add_metric expects a MetricBase, got {type(metric).__name__}")
         self._metrics.append(metric)
 
     def update(self, preds, labels):
@@ -71,154 +72,157 @@ class CompositeMetric(MetricBase):
         return [m.eval() for m in self._metrics]
 
 
+def _binary(preds, labels):
+    return np.rint(np.asarray(preds)).astype(np.int64).ravel(), np.asarray(labels).astype(np.int64).ravel()
+
+
 class Precision(MetricBase):
+    """Binary precision tp / (tp + fp); predictions are rounded to 0/1."""
+
+    _STATE = {"tp": 0, "fp": 0}
+
     def __init__(self, name=None):
         super().__init__(name)
-        self.tp = 0
-        self.fp = 0
 
     def update(self, preds, labels):
-        preds = np.rint(np.asarray(preds)).astype("int32").reshape(-1)
-        labels = np.asarray(labels).reshape(-1)
-        for p, l in zip(preds, labels):
-            if p == 1:
-                if p == l:
-                    self.tp += 1
-                else:
-                    self.fp += 1
+        p, l = _binary(preds, labels)
+        pos = p == 1
+        self.tp += int(np.count_nonzero(pos & (l == 1)))
+        self.fp += int(np.count_nonzero(pos & (l != 1)))
 
     def eval(self):
-        ap = self.tp + self.fp
-        return float(self.tp) / ap if ap != 0 else 0.0
+        n = self.tp + self.fp
+        return self.tp / n if n else 0.0
 
 
 class Recall(MetricBase):
+    """Binary recall tp / (tp + fn); predictions are rounded to 0/1."""
+
+    _STATE = {"tp": 0, "fn": 0}
+
     def __init__(self, name=None):
         super().__init__(name)
-        self.tp = 0
-        self.fn = 0
 
     def update(self, preds, labels):
-        preds = np.rint(np.asarray(preds)).astype("int32").reshape(-1)
-        labels = np.asarray(labels).reshape(-1)
-        for p, l in zip(preds, labels):
-            if l == 1:
-                if p == l:
-                    self.tp += 1
-                else:
-                    self.fn += 1
+        p, l = _binary(preds, labels)
+        actual = l == 1
+        self.tp += int(np.count_nonzero(actual & (p == 1)))
+        self.fn += int(np.count_nonzero(actual & (p != 1)))
 
     def eval(self):
-        recall = self.tp + self.fn
-        return float(self.tp) / recall if recall != 0 else 0.0
+        n = self.tp + self.fn
+        return self.tp / n if n else 0.0
 
 
 class Accuracy(MetricBase):
+    """Weighted running mean of per-batch accuracies."""
+
+    _STATE = {"value": 0.0, "weight": 0.0}
+
     def __init__(self, name=None):
         super().__init__(name)
-        self.value = 0.0
-        self.weight = 0.0
 
     def update(self, value, weight):
-        if not _is_number_or_matrix_(value):
-            raise ValueError("The 'value' must be a number(int, float) or a numpy ndarray.")
-        self.value += float(np.asarray(value).reshape(-1)[0]) * weight
+        _check_number_or_array(value, "Accuracy value")
+        self.value += float(_scalar(value)) * weight
         self.weight += weight
 
     def eval(self):
-        if self.weight == 0:
-            raise ValueError("There is no data in Accuracy Metrics.")
+        if not self.weight:
+            raise ValueError("Accuracy.eval() called before any update")
         return self.value / self.weight
 
 
 class ChunkEvaluator(MetricBase):
+    """Chunk precision / recall / F1 from the chunk_eval op's three counters."""
+
+    _STATE = {"num_infer_chunks": 0, "num_label_chunks": 0, "num_correct_chunks": 0}
+
     def __init__(self, name=None):
         super().__init__(name)
-        self.num_infer_chunks = 0
-        self.num_label_chunks = 0
-        self.num_correct_chunks = 0
 
     def update(self, num_infer_chunks, num_label_chunks, num_correct_chunks):
-        self.num_infer_chunks += int(np.asarray(num_infer_chunks).reshape(-1)[0])
-        self.num_label_chunks += int(np.asarray(num_label_chunks).reshape(-1)[0])
-        self.num_correct_chunks += int(np.asarray(num_correct_chunks).reshape(-1)[0])
+        self.num_infer_chunks += int(_scalar(num_infer_chunks))
+        self.num_label_chunks += int(_scalar(num_label_chunks))
+        self.num_correct_chunks += int(_scalar(num_correct_chunks))
 
     def eval(self):
-        precision = float(self.num_correct_chunks) / self.num_infer_chunks if self.num_infer_chunks else 0
-        recall = float(self.num_correct_chunks) / self.num_label_chunks if self.num_label_chunks else 0
-        f1 = float(2 * precision * recall) / (precision + recall) if self.num_correct_chunks else 0
-        return precision, recall, f1
+        c = float(self.num_correct_chunks)
+        prec = c / self.num_infer_chunks if self.num_infer_chunks else 0.0
+        rec = c / self.num_label_chunks if self.num_label_chunks else 0.0
+        f1 = 2.0 * prec * rec / (prec + rec) if c else 0.0
+        return prec, rec, f1
 
 
 class EditDistance(MetricBase):
+    """Mean edit distance per sequence and the fraction of sequences with any error."""
+
+    _STATE = {"total_distance": 0.0, "seq_num": 0, "instance_error": 0}
+
     def __init__(self, name):
         super().__init__(name)
-        self.total_distance = 0.0
-        self.seq_num = 0
-        self.instance_error = 0
 
     def update(self, distances, seq_num):
-        distances = np.asarray(distances)
-        seq_right_count = np.sum(distances == 0)
-        total_distance = np.sum(distances)
-        self.seq_num += int(seq_num)
-        self.instance_error += int(seq_num) - int(seq_right_count)
-        self.total_distance += float(total_distance)
+        d = np.asarray(distances).ravel()
+        n = int(seq_num)
+        self.seq_num += n
+        self.instance_error += n - int(np.count_nonzero(d == 0))
+        self.total_distance += float(d.sum())
 
     def eval(self):
-        if self.seq_num == 0:
-            raise ValueError("There is no data in EditDistance Metric.")
+        if not self.seq_num:
+            raise ValueError("EditDistance.eval() called before any update")
         return self.total_distance / self.seq_num, self.instance_error / float(self.seq_num)
 
 
 class DetectionMAP(MetricBase):
+    """Weighted running mean of per-batch mAP values (detection_map op outputs)."""
+
+    _STATE = {"value": 0.0, "weight": 0.0}
+
     def __init__(self, name=None):
         super().__init__(name)
-        self.value = 0.0
-        self.weight = 0.0
 
     def update(self, value, weight):
-        self.value += float(np.asarray(value).reshape(-1)[0]) * weight
+        self.value += float(_scalar(value)) * weight
         self.weight += weight
 
     def eval(self):
-        if self.weight == 0:
-            raise ValueError("There is no data in DetectionMAP Metrics.")
+        if not self.weight:
+            raise ValueError("DetectionMAP.eval() called before any update")
         return self.value / self.weight
 
 
 class Auc(MetricBase):
+    """Streaming ROC AUC over ``num_thresholds + 1`` score bins."""
+
     def __init__(self, name, curve="ROC", num_thresholds=4095):
-        super().__init__(name=name)
         self._curve = curve
         self._num_thresholds = num_thresholds
-        self._stat_pos = [0] * (num_thresholds + 1)
-        self._stat_neg = [0] * (num_thresholds + 1)
+        super().__init__(name=name)
+
+    def reset(self):
+        self._stat_pos = np.zeros(self._num_thresholds + 1, dtype=np.float64)
+        self._stat_neg = np.zeros(self._num_thresholds + 1, dtype=np.float64)
+
+    def get_config(self):
+        return {"name": self._name, "states": {"stat_pos": self._stat_pos.copy(), "stat_neg": self._stat_neg.copy()}}
 
     def update(self, preds, labels):
-        preds = np.asarray(preds)
-        labels = np.asarray(labels).reshape(-1)
-        for i, lbl in enumerate(labels):
-            value = preds[i, 1] if preds.ndim > 1 else preds[i]
-            bin_idx = int(value * self._num_thresholds)
-            assert bin_idx <= self._num_thresholds
-            if lbl:
-                self._stat_pos[bin_idx] += 1.0
-            else:
-                self._stat_neg[bin_idx] += 1.0
-
-    @staticmethod
-    def trapezoid_area(x1, x2, y1, y2):
-        return abs(x1 - x2) * (y1 + y2) / 2.0
+        p = np.asarray(preds)
+        score = p[:, 1] if p.ndim > 1 else p.ravel()
+        bins = (score * self._num_thresholds).astype(np.int64)
+        if bins.size and (bins.max() > self._num_thresholds or bins.min() < 0):
+            raise ValueError("Auc expects probabilities in [0, 1]")
+        pos = np.asarray(labels).ravel().astype(bool)
+        self._stat_pos += np.bincount(bins[pos], minlength=self._num_thresholds + 1)
+        self._stat_neg += np.bincount(bins[~pos], minlength=self._num_thresholds + 1)
 
     def eval(self):
-        tot_pos = tot_neg = 0.0
-        auc = 0.0
-        idx = self._num_thresholds
-        while idx >= 0:
-            tot_pos_prev, tot_neg_prev = tot_pos, tot_neg
-            tot_pos += self._stat_pos[idx]
-            tot_neg += self._stat_neg[idx]
-            auc += self.trapezoid_area(tot_neg, tot_neg_prev, tot_pos, tot_pos_prev)
-            idx -= 1
-        return auc / tot_pos / tot_neg if tot_pos > 0.0 and tot_neg > 0.0 else 0.0
+        # sweep thresholds from high to low: cumulative TP / FP counts trace the ROC
+        tp = np.concatenate([[0.0], np.cumsum(self._stat_pos[::-1])])
+        fp = np.concatenate([[0.0], np.cumsum(self._stat_neg[::-1])])
+        if tp[-1] <= 0 or fp[-1] <= 0:
+            return 0.0
+        area = np.sum((fp[1:] - fp[:-1]) * (tp[1:] + tp[:-1]) / 2.0)
+        return float(area / tp[-1] / fp[-1])
