@@ -56,6 +56,14 @@ struct Params {
   float alpha;
   int accumulate;    // C += result (beta = 1)
   int tiles_m, tiles_n;
+  // split-K through the batch index: batch b reduces k in [b*K, min((b+1)*K, k_total))
+  // (k_total = 0: batches are independent GEMMs of depth K)
+  int k_total;
+  // implicit-GEMM convolution (GA kernels): A(m, k) gathered from an NHWC source
+  // tensor: m = (n, oy, ox) over an OH x OW grid, k = (kh, kw, c) with Cc % 64 == 0.
+  // Source pixel: ny = oy*sy - py + kh*dy; with a zero-insertion factor 2^uy
+  // (dgrad of a stride-2^uy conv) only ny % 2^uy == 0 hits, at row ny >> uy.
+  int H, W, Cc, OH, OW, KW, sy, sx, py, px, dy, dx, uy, ux;
 };
 
 // LDS image of one operand of one stage: 4 "slabs" of 64 mn x 64 k (8 KiB each);
@@ -145,6 +153,61 @@ __device__ __forceinline__ void dma_issue(const DmaLane<NP, KFULL>& d, __amdgpu_
   }
 }
 
+// Conv-gather plan of one A region for one wave: per piece the element offset of the
+// image (plus this lane's 8-channel chunk) and the packed (ybase, xbase) of its
+// output pixel (ybase = -32768 marks a row past M: every range check fails).
+template <int NP>
+struct GatherLane {
+  int nb[NP];
+  int yx[NP];
+};
+
+template <int NP>
+__device__ __forceinline__ void gather_plan(GatherLane<NP>& d, int region, int wid, int lane, int m_tile0,
+                                            const Params& p) {
+  const int hw = p.OH * p.OW;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    int sl, pc, mn, k;
+    region_piece(region, wid, j, sl, pc);
+    dma_coords<true>(sl, pc, lane, mn, k);
+    const int gm = m_tile0 + mn;
+    if (gm < p.M) {
+      const int n = gm / hw, r = gm - n * hw;
+      const int oy = r / p.OW, ox = r - oy * p.OW;
+      d.nb[j] = n * p.H * p.W * p.Cc + k;
+      d.yx[j] = ((oy * p.sy - p.py) << 16) | ((ox * p.sx - p.px) & 0xffff);
+    } else {
+      d.nb[j] = 0;
+      d.yx[j] = (int)0x80008000u;
+    }
+  }
+}
+
+template <int NP>
+__device__ __forceinline__ void gather_issue(const GatherLane<NP>& d, __amdgpu_buffer_rsrc_t rs, char* stage_opnd,
+                                             int region, int wid, int kt, const Params& p) {
+  const int k0 = kt * BKT;
+  const bool kt_ok = k0 < p.K;
+  // (kh, kw, c0) of this k-tile: wave-uniform scalars (a k-tile never crosses a tap, C % 64 == 0)
+  const int c0 = k0 % p.Cc, tap = k0 / p.Cc;
+  const int kh = tap / p.KW, kw = tap - kh * p.KW;
+  const int my = (1 << p.uy) - 1, mx = (1 << p.ux) - 1;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    int sl, pc;
+    region_piece(region, wid, j, sl, pc);
+    const int ny = (d.yx[j] >> 16) + kh * p.dy;
+    const int nx = (int)(short)(d.yx[j] & 0xffff) + kw * p.dx;
+    const int iy = ny >> p.uy, ix = nx >> p.ux;
+    const bool ok = kt_ok && ((ny & my) | (nx & mx)) == 0 && (unsigned)iy < (unsigned)p.H &&
+                    (unsigned)ix < (unsigned)p.W;
+    const unsigned vo = ok ? (unsigned)(d.nb[j] + (iy * p.W + ix) * p.Cc + c0) * 2u : OOB;
+    char* dst = stage_opnd + sl * 8192 + pc * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16, vo, 0, 0, 0);
+  }
+}
+
 // Fragment (16 mn x 32 k, MFMA operand layout: lane l holds X[mn = l&15][k = 8(l>>4) + j])
 // of 32-mn block `u` (0..7), 16-row half i (0/1), k-step kk (0/1).
 __device__ __forceinline__ bf16x8 frag_kmaj(const char* opnd, int u, int i, int kk, int lane) {
@@ -223,7 +286,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // (profiles/r2_gemm_v4_sched_ab.jsonl): the prefetch schedule wins ~5 % when both
 // operands take transposed reads (24 tr_b16 in one phase-1 load section
 // otherwise), and loses 2-5 % when an operand is K-major.
-template <bool AK, bool BK, bool OUTF32, bool PF_IN_CLUSTER, bool KFULL>
+template <bool AK, bool BK, bool OUTF32, bool PF_IN_CLUSTER, bool KFULL, bool GA = false>
 __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -232,13 +295,15 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
 
   const int nwg = p.tiles_m * p.tiles_n;
   const long bz = blockIdx.y;
+  const int Kb = p.k_total ? min(p.K, p.k_total - (int)bz * p.K) : p.K;  // valid depth of this batch
   const char* Ab = (const char*)p.A + bz * p.sA * 2;
   const char* Bb = (const char*)p.B + bz * p.sB * 2;
   // descriptors over this batch's whole operand (host guarantees < 4 GiB)
-  const unsigned a_bytes = AK ? (unsigned)(((long)(p.M - 1) * p.lda + p.K) * 2)
-                              : (unsigned)(((long)(p.K - 1) * p.lda + p.M) * 2);
-  const unsigned b_bytes = BK ? (unsigned)(((long)(p.N - 1) * p.ldb + p.K) * 2)
-                              : (unsigned)(((long)(p.K - 1) * p.ldb + p.N) * 2);
+  const unsigned a_bytes = GA ? (unsigned)((long)(p.M / (p.OH * p.OW)) * p.H * p.W * p.Cc * 2)
+                         : AK ? (unsigned)(((long)(p.M - 1) * p.lda + Kb) * 2)
+                              : (unsigned)(((long)(Kb - 1) * p.lda + p.M) * 2);
+  const unsigned b_bytes = BK ? (unsigned)(((long)(p.N - 1) * p.ldb + Kb) * 2)
+                              : (unsigned)(((long)(Kb - 1) * p.ldb + p.N) * 2);
   const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, 0, a_bytes, 0x00020000);
   const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, 0, b_bytes, 0x00020000);
 
@@ -257,19 +322,37 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
 
   // ---- DMA plans: A_FIRST / A_SEC 2 pieces each, B 4 pieces per wave
   DmaLane<2, KFULL> daf, das;
+  GatherLane<2> gaf, gas;
   DmaLane<4, KFULL> db;
   auto plan = [&](int mm0, int nn0) {
-    dma_plan<AK, 2, KFULL>(daf, A_FIRST, 0, wid, lane, mm0, p.M, p.lda);
-    dma_plan<AK, 2, KFULL>(das, A_SEC, 0, wid, lane, mm0, p.M, p.lda);
+    if constexpr (GA) {
+      gather_plan<2>(gaf, A_FIRST, wid, lane, mm0, p);
+      gather_plan<2>(gas, A_SEC, wid, lane, mm0, p);
+    } else {
+      dma_plan<AK, 2, KFULL>(daf, A_FIRST, 0, wid, lane, mm0, p.M, p.lda);
+      dma_plan<AK, 2, KFULL>(das, A_SEC, 0, wid, lane, mm0, p.M, p.lda);
+    }
     dma_plan<BK, 4, KFULL>(db, B_ALL, 0, wid, lane, nn0, p.N, p.ldb);
   };
 
-  const int nk = (p.K + BKT - 1) / BKT;
+  const int nk = (Kb + BKT - 1) / BKT;
   auto sA = [&](int kt) { return smem + (kt & 1) * STAGE; };
   auto sB = [&](int kt) { return smem + (kt & 1) * STAGE + OPND; };
-#define DMA_AF(kt) dma_issue<AK, 2, KFULL>(daf, rsA, sA(kt), A_FIRST, 0, wid, (kt), p.K, p.lda)
-#define DMA_AS(kt) dma_issue<AK, 2, KFULL>(das, rsA, sA(kt), A_SEC, 0, wid, (kt), p.K, p.lda)
-#define DMA_B(kt) dma_issue<BK, 4, KFULL>(db, rsB, sB(kt), B_ALL, 0, wid, (kt), p.K, p.ldb)
+#define DMA_AF(kt)                                                        \
+  do {                                                                    \
+    if constexpr (GA)                                                     \
+      gather_issue<2>(gaf, rsA, sA(kt), A_FIRST, wid, (kt), p);           \
+    else                                                                  \
+      dma_issue<AK, 2, KFULL>(daf, rsA, sA(kt), A_FIRST, 0, wid, (kt), Kb, p.lda); \
+  } while (0)
+#define DMA_AS(kt)                                                        \
+  do {                                                                    \
+    if constexpr (GA)                                                     \
+      gather_issue<2>(gas, rsA, sA(kt), A_SEC, wid, (kt), p);             \
+    else                                                                  \
+      dma_issue<AK, 2, KFULL>(das, rsA, sA(kt), A_SEC, 0, wid, (kt), Kb, p.lda); \
+  } while (0)
+#define DMA_B(kt) dma_issue<BK, 4, KFULL>(db, rsB, sB(kt), B_ALL, 0, wid, (kt), Kb, p.ldb)
 
   // ---- DMA issue order (the counted waits depend on it):
   //   A_first(0) B(0) A_sec(0) A_first(1) B(1); the loop at k-tile t issues
@@ -583,11 +666,11 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
 static int g_sched = -1;      // -1: per-layout default; 0 / 1: force PF_IN_CLUSTER (A/B runs)
 static int g_persistent = 1;  // 0: one tile per block (grid = tiles), for A/B runs
 
-template <bool AK, bool BK, bool F32, bool PF, bool KFULL>
+template <bool AK, bool BK, bool F32, bool PF, bool KFULL, bool GA = false>
 static int launch_v(const Params& p, int batch, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_kernel<AK, BK, F32, PF, KFULL>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_kernel<AK, BK, F32, PF, KFULL, GA>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
@@ -601,7 +684,7 @@ static int launch_v(const Params& p, int batch, hipStream_t st) {
   }
   const int nwg = p.tiles_m * p.tiles_n;
   const int grid = (nwg < ncu || !g_persistent) ? nwg : ncu;  // persistent: one resident block per CU
-  hipLaunchKernelGGL((gemm_kernel<AK, BK, F32, PF, KFULL>), dim3(grid, batch), dim3(NT), LDS_BYTES, st, p);
+  hipLaunchKernelGGL((gemm_kernel<AK, BK, F32, PF, KFULL, GA>), dim3(grid, batch), dim3(NT), LDS_BYTES, st, p);
   return (int)hipGetLastError();
 }
 
@@ -611,7 +694,7 @@ static int launch(const Params& p0, int batch, hipStream_t st) {
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (p.N + BN - 1) / BN;
   const bool pf = g_sched < 0 ? (!AK && !BK) : g_sched == 1;
-  if (p.K % BKT == 0)  // every k-tile full: the k range check is wave-uniform
+  if (p.K % BKT == 0 && p.k_total % BKT == 0)  // every k-tile full: the k range check is wave-uniform
     return pf ? launch_v<AK, BK, F32, true, true>(p, batch, st) : launch_v<AK, BK, F32, false, true>(p, batch, st);
   return pf ? launch_v<AK, BK, F32, true, false>(p, batch, st) : launch_v<AK, BK, F32, false, false>(p, batch, st);
 }
@@ -625,17 +708,27 @@ PA_EXPORT void pa_gemm_set_sched(int s) { gemm::g_sched = s; }
 PA_EXPORT void pa_gemm_set_persistent(int s) { gemm::g_persistent = s; }
 
 // Returns 0 on success, a hipError on launch failure, -1 for an unsupported shape
-// (the caller checks shapes first: M, N, K multiples of 8, 16-B aligned rows,
+// (the caller checks shapes first: N a multiple of 8, K a multiple of 8 when an
+// operand is K-major, M a multiple of 8 when A is M-major; 16-B aligned rows;
 // every operand < 4 GiB).
 //   a_kmaj: A is [M][lda] K-contiguous (else [K][lda] M-contiguous)
 //   b_kmaj: B is [N][ldb] K-contiguous (else [K][ldb] N-contiguous)
 //   out_f32: C is fp32 (else bf16); accumulate: C += alpha*AB (+bias)
+//   k_total > 0: split-K, batch b covers k in [b*K, min((b+1)*K, k_total)) (sA/sB are
+//   the k offsets of one split; the caller sums the per-batch outputs)
 PA_EXPORT int pa_gemm(int a_kmaj, int b_kmaj, int out_f32, const void* A, const void* B, void* C,
                       const void* bias, int M, int N, int K, long lda, long ldb, long ldc, long sA, long sB,
-                      long sC, int batch, float alpha, int accumulate, hipStream_t st) {
+                      long sC, int batch, float alpha, int accumulate, int k_total, hipStream_t st) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
-  if ((M | N | K) & 7) return -1;
-  gemm::Params p{A, B, C, bias, M, N, K, lda, ldb, ldc, sA, sB, sC, alpha, accumulate, 0, 0};
+  // 16-B chunks: along K for a K-major operand, along M / N for an MN-major one,
+  // along N for the output
+  if ((N & 7) || ((a_kmaj || b_kmaj) && (K & 7)) || (!a_kmaj && (M & 7))) return -1;
+  gemm::Params p{};
+  p.A = A; p.B = B; p.C = C; p.bias = bias;
+  p.M = M; p.N = N; p.K = K;
+  p.lda = lda; p.ldb = ldb; p.ldc = ldc;
+  p.sA = sA; p.sB = sB; p.sC = sC;
+  p.alpha = alpha; p.accumulate = accumulate; p.k_total = k_total;
   if (K <= 0) return -1;
 #define PA_G(AK, BK, F)                                                \
   if (a_kmaj == AK && b_kmaj == BK && out_f32 == F) return gemm::launch<AK, BK, F>(p, batch, st);
@@ -643,4 +736,27 @@ PA_EXPORT int pa_gemm(int a_kmaj, int b_kmaj, int out_f32, const void* A, const 
   PA_G(1, 1, 1) PA_G(1, 0, 1) PA_G(0, 1, 1) PA_G(0, 0, 1)
 #undef PA_G
   return -1;
+}
+
+// Implicit-GEMM convolution, NHWC bf16 (forward, or dgrad with up = log2 stride):
+//   out[(n, oy, ox)][co] = sum_{kh, kw, c} src[n, iy, ix, c] * wt[co][kh][kw][c]
+// src: [N, H, W, C] (C % 64 == 0), wt: [Cout][KH*KW*C] K-major, out: [N*OH*OW][Cout]
+// (ldc = Cout), bias [Cout] or null.  Returns -1 for shapes the kernel does not cover.
+PA_EXPORT int pa_conv_gemm(const void* src, const void* wt, void* out, const void* bias, int Nb, int H, int W, int C,
+                           int OH, int OW, int Cout, int KH, int KW, int sy, int sx, int py, int px, int dy, int dx,
+                           int uy, int ux, hipStream_t st) {
+  const long M = (long)Nb * OH * OW;
+  if (M <= 0 || Cout <= 0) return 0;
+  if (C % 64 || Cout % 8 || M > 0x7fffffffL || (long)Nb * H * W * C >= 0x7fffffffL || H > 32767 || W > 32767)
+    return -1;
+  gemm::Params p{};
+  p.A = src; p.B = wt; p.C = out; p.bias = bias;
+  p.M = (int)M; p.N = Cout; p.K = KH * KW * C;
+  p.lda = C; p.ldb = p.K; p.ldc = Cout;
+  p.alpha = 1.f;
+  p.H = H; p.W = W; p.Cc = C; p.OH = OH; p.OW = OW; p.KW = KW;
+  p.sy = sy; p.sx = sx; p.py = py; p.px = px; p.dy = dy; p.dx = dx; p.uy = uy; p.ux = ux;
+  p.tiles_m = (p.M + gemm::BM - 1) / gemm::BM;
+  p.tiles_n = (p.N + gemm::BN - 1) / gemm::BN;
+  return gemm::launch_v<true, true, false, false, true, true>(p, 1, st);
 }

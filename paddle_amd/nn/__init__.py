@@ -11,3 +11,10 @@ from ..optimizer.clip import ClipGradByGlobalNorm, ClipGradByNorm, ClipGradByVal
 from . import utils  # noqa: F401,E402
 
 Dropout2D = Dropout
+
+
+def layer_bn_types():
+    """BatchNorm layer classes (for fused BN+activation fast paths)."""
+    from .layers_common import _BatchNormBase
+
+    return (_BatchNormBase,)

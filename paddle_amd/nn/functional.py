@@ -15,6 +15,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
+from ..ops import conv as _conv
 
 
 def _pair(v, n=2):
@@ -208,6 +209,9 @@ def _conv_padding(padding, nd):
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCHW", name=None):
     pad = _conv_padding(padding, 2)
+    if not _nchw(x, data_format) and _conv.supported_conv(x, weight, stride, pad, dilation, groups):
+        # NHWC bf16 on the GPU: implicit-GEMM MFMA kernel (ops/conv.py)
+        return _conv.conv2d_nhwc(x, weight, bias, stride, pad, dilation)
     if not _nchw(x, data_format):
         y = F.conv2d(x.permute(0, 3, 1, 2), weight, bias, _pair(stride), pad, _pair(dilation), groups)
         return y.permute(0, 2, 3, 1)
@@ -246,6 +250,9 @@ def conv3d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0
 def max_pool2d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False, data_format="NCHW",
                name=None):
     stride = kernel_size if stride is None else stride
+    if not _nchw(x, data_format) and not return_mask and _conv.supported_pool(x, ceil_mode) \
+            and not isinstance(padding, str):
+        return _conv.max_pool2d_nhwc(x, kernel_size, stride, _conv_padding(padding, 2))
     if not _nchw(x, data_format):
         x = x.permute(0, 3, 1, 2)
     y = F.max_pool2d(x, _pair(kernel_size), _pair(stride), _conv_padding(padding, 2), ceil_mode=ceil_mode,
@@ -289,6 +296,8 @@ def avg_pool3d(x, kernel_size, stride=None, padding=0, ceil_mode=False, exclusiv
 
 
 def adaptive_avg_pool2d(x, output_size, data_format="NCHW", name=None):
+    if not _nchw(x, data_format) and tuple(_pair(output_size)) == (1, 1) and _conv.supported_pool(x):
+        return _conv.global_avg_pool_nhwc(x)
     if not _nchw(x, data_format):
         return F.adaptive_avg_pool2d(x.permute(0, 3, 1, 2), output_size).permute(0, 2, 3, 1)
     return F.adaptive_avg_pool2d(x, output_size)
@@ -316,6 +325,10 @@ def batch_norm(x, running_mean, running_var, weight, bias, training=False, momen
     """Paddle momentum convention: running = running * momentum + batch * (1 - momentum)."""
     if use_global_stats:
         training = False
+    if x.dim() == 4 and not _nchw(x, data_format) and _conv.supported_bn(x):
+        if training:
+            return _conv.batch_norm_nhwc_train(x, weight, bias, running_mean, running_var, momentum, epsilon)
+        return _conv.batch_norm_nhwc_eval(x, weight, bias, running_mean, running_var, epsilon)
     nchw = _nchw(x, data_format) or x.dim() == 2
     if not nchw:
         x = x.movedim(-1, 1)

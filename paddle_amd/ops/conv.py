@@ -1,0 +1,316 @@
+"""NHWC bf16 convolution, batch norm and pooling on the hand-written gfx950 kernels.
+
+* conv2d forward: implicit GEMM (csrc/kernels/gemm.hip ``pa_conv_gemm``: the MFMA
+  GEMM with an NHWC gather of the A operand; padding/edges are zero-filled by the
+  buffer range check).  Input channels not a multiple of 64 (the 3-channel stem)
+  take an explicit im2col (``pa_im2col_nhwc``) + the plain GEMM.
+* conv2d dgrad: the same implicit GEMM over dY with the flipped, transposed kernel
+  and a zero-insertion factor = stride (power of two), i.e. no col2im scatter.
+* conv2d wgrad: dW = dY^T im2col(X) with both operands MN-major (1x1 / stride-1
+  convs read X directly); fp32 output.
+* batch norm: shifted fp32 sums per block + fp64 finalize; optional fused ReLU
+  (the backward masks dY with the saved output).
+* max pool: argmax byte per element, gather backward; global average pool.
+
+Reference behaviour: paddle/fluid/operators/conv_cudnn_op.cu.cc:43-171,
+batch_norm_op.cu.cc:170, math/pooling.cu:25-189, math/im2col.cu.
+``supported_*`` decide eligibility; callers use the torch path only for shapes or
+dtypes these kernels do not cover.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _native as _nat
+from . import gemm as _G
+
+
+_ENABLED = [True]
+
+
+def set_enabled(flag: bool):
+    """Route NHWC conv / BN / pool to the native kernels (True) or to ATen (False)."""
+    _ENABLED[0] = bool(flag)
+
+
+def _i(v):
+    return int(v)
+
+
+def _pair(v):
+    return tuple(v) if isinstance(v, (list, tuple)) else (v, v)
+
+
+def _pow2(v):
+    return v > 0 and (v & (v - 1)) == 0
+
+
+def supported_conv(x, w, stride, padding, dilation, groups):
+    if not (_ENABLED[0] and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and groups == 1 and _G.enabled()):
+        return False
+    if not x.is_contiguous():
+        return False
+    N, H, W, C = x.shape
+    Cout = w.shape[0]
+    sy, sx = _pair(stride)
+    if Cout % 8 or not (_pow2(sy) and _pow2(sx)):
+        return False
+    if isinstance(padding, str):
+        return False
+    return True
+
+
+def _out_hw(H, W, KH, KW, s, p, d):
+    return (H + 2 * p[0] - d[0] * (KH - 1) - 1) // s[0] + 1, (W + 2 * p[1] - d[1] * (KW - 1) - 1) // s[1] + 1
+
+
+def _im2col(x, KH, KW, s, p, d, OH, OW, Kp):
+    N, H, W, C = x.shape
+    col = torch.empty(N * OH * OW, Kp, dtype=x.dtype, device=x.device)
+    _nat.call("pa_im2col_nhwc", _nat.ptr(x), _nat.ptr(col), N, H, W, C, OH, OW, KH, KW, s[0], s[1], p[0], p[1],
+              d[0], d[1], Kp, _nat.stream())
+    return col
+
+
+def _conv_fwd(x, w, b, s, p, d):
+    N, H, W, C = x.shape
+    Cout, _, KH, KW = w.shape
+    OH, OW = _out_hw(H, W, KH, KW, s, p, d)
+    K = KH * KW * C
+    wk = w.to(x.dtype).permute(0, 2, 3, 1).reshape(Cout, K)  # [Cout][(kh, kw, c)]
+    bias = b.to(x.dtype) if b is not None else None
+    if C % 64 == 0:
+        wk = wk.contiguous()
+        y = torch.empty(N, OH, OW, Cout, dtype=x.dtype, device=x.device)
+        rc = _nat.lib().pa_conv_gemm(_nat.ptr(x), _nat.ptr(wk), _nat.ptr(y), _nat.ptr(bias), N, H, W, C, OH, OW,
+                                     Cout, KH, KW, s[0], s[1], p[0], p[1], d[0], d[1], 0, 0, _nat.stream())
+        _nat.check(rc, "pa_conv_gemm")
+        return y
+    Kp = (K + 7) // 8 * 8
+    col = _im2col(x, KH, KW, s, p, d, OH, OW, Kp)
+    wp = torch.zeros(Cout, Kp, dtype=x.dtype, device=x.device)
+    wp[:, :K] = wk
+    y = _G.gemm(col, wp, N * OH * OW, Cout, Kp, a_kmaj=True, b_kmaj=True, bias=bias)
+    return y.view(N, OH, OW, Cout)
+
+
+def _conv_dgrad(dy, w, x_shape, s, p, d):
+    N, H, W, C = x_shape
+    Cout, _, KH, KW = w.shape
+    OH, OW = dy.shape[1], dy.shape[2]
+    if Cout % 64 == 0 and C % 8 == 0:
+        # dX = conv(zero-inserted dY, flipped W^T): wd[c][kh][kw][co] = w[co][c][KH-1-kh][KW-1-kw]
+        wd = w.to(dy.dtype).flip(2, 3).permute(1, 2, 3, 0).reshape(C, KH * KW * Cout).contiguous()
+        dx = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
+        pyy, pxx = d[0] * (KH - 1) - p[0], d[1] * (KW - 1) - p[1]
+        rc = _nat.lib().pa_conv_gemm(_nat.ptr(dy), _nat.ptr(wd), _nat.ptr(dx), None, N, OH, OW, Cout, H, W, C, KH,
+                                     KW, 1, 1, pyy, pxx, d[0], d[1], int(math.log2(s[0])), int(math.log2(s[1])),
+                                     _nat.stream())
+        if rc == 0:
+            return dx
+    # rare shapes: autograd of the torch convolution
+    xs = torch.zeros(N, C, H, W, dtype=dy.dtype, device=dy.device)
+    return torch.nn.grad.conv2d_input(xs.shape, w.to(dy.dtype), dy.permute(0, 3, 1, 2), s, p, d).permute(
+        0, 2, 3, 1).contiguous()
+
+
+def _conv_wgrad(dy, x, w_shape, s, p, d):
+    N, H, W, C = x.shape
+    Cout, _, KH, KW = w_shape
+    OH, OW = dy.shape[1], dy.shape[2]
+    M = N * OH * OW
+    K = KH * KW * C
+    if KH == 1 and KW == 1 and s == (1, 1) and p == (0, 0) and C % 8 == 0:
+        col, Kp = x.reshape(M, C), C
+    else:
+        Kp = (K + 7) // 8 * 8
+        col = _im2col(x, KH, KW, s, p, d, OH, OW, Kp)
+    dwk = torch.empty(Cout, Kp, dtype=torch.float32, device=x.device)
+    # dW[co][k] = sum_m dY[m][co] col[m][k]: both operands stored [m][..] (MN-major);
+    # few output tiles, very deep reduction -> split-K across the chip
+    _G.gemm_splitk(dy.reshape(M, Cout), col, Cout, Kp, M, a_kmaj=False, b_kmaj=False, out=dwk)
+    return dwk[:, :K].reshape(Cout, KH, KW, C).permute(0, 3, 1, 2)
+
+
+class _Conv2dNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, s, p, d):
+        y = _conv_fwd(x, w, b, s, p, d)
+        ctx.save_for_backward(x, w)
+        ctx.conf = (s, p, d, b is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        s, p, d, has_b = ctx.conf
+        dy = dy.contiguous()
+        dx = _conv_dgrad(dy, w, tuple(x.shape), s, p, d) if ctx.needs_input_grad[0] else None
+        dw = _conv_wgrad(dy, x, tuple(w.shape), s, p, d).to(w.dtype) if ctx.needs_input_grad[1] else None
+        db = dy.reshape(-1, dy.shape[-1]).float().sum(0).to(w.dtype) if has_b and ctx.needs_input_grad[2] else None
+        return dx, dw, db, None, None, None
+
+
+def conv2d_nhwc(x, weight, bias=None, stride=1, padding=0, dilation=1):
+    """x [N, H, W, C] bf16 contiguous, weight [Cout, Cin, KH, KW] (Paddle layout)."""
+    s, p, d = _pair(stride), _pair(padding), _pair(dilation)
+    return _Conv2dNHWC.apply(x, weight, bias, tuple(map(_i, s)), tuple(map(_i, p)), tuple(map(_i, d)))
+
+
+# ------------------------------------------------------------------ batch norm
+
+
+def supported_bn(x):
+    return _ENABLED[0] and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.shape[-1] % 8 == 0 and x.dim() >= 2
+
+
+def _wdt(w):
+    if w is None:
+        return 0, None
+    if w.dtype == torch.float32:
+        return 0, w.contiguous()
+    return 1, w.to(torch.bfloat16).contiguous()
+
+
+class _BatchNormNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, run_mean, run_var, momentum, eps, relu):
+        C = x.shape[-1]
+        rows = x.numel() // C
+        wdt, wc = _wdt(w)
+        _, bc = _wdt(b) if b is not None else (0, None)
+        if b is not None and w is not None and bc.dtype != wc.dtype:
+            bc = bc.to(wc.dtype)
+        G = int(_nat.lib().pa_bn_blocks(rows, C))
+        part = torch.empty(G * 2 * C, dtype=torch.float32, device=x.device)
+        mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(C, dtype=torch.float32, device=x.device)
+        y = torch.empty_like(x)
+        rm = run_mean if (run_mean is not None and run_mean.dtype == torch.float32) else None
+        rv = run_var if rm is not None else None
+        _nat.call("pa_bn_fwd_train", _nat.ptr(x), _nat.ptr(y), _nat.ptr(wc), _nat.ptr(bc), wdt, _nat.ptr(rm),
+                  _nat.ptr(rv), _nat.ptr(mean), _nat.ptr(rstd), _nat.ptr(part), rows, C, float(eps),
+                  float(momentum), int(relu), _nat.stream())
+        if run_mean is not None and rm is None:  # running stats kept in another dtype: update on the side
+            with torch.no_grad():
+                var = 1.0 / (rstd.double() ** 2) - eps
+                unb = var * rows / max(rows - 1, 1)
+                run_mean.mul_(momentum).add_((1 - momentum) * mean.to(run_mean.dtype))
+                run_var.mul_(momentum).add_((1 - momentum) * unb.to(run_var.dtype))
+        ctx.save_for_backward(x, y if relu else None, mean, rstd, wc)
+        ctx.conf = (relu, wdt, w is not None, b is not None)
+        ctx.wdtype = w.dtype if w is not None else None
+        ctx.bdtype = b.dtype if b is not None else None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, rstd, wc = ctx.saved_tensors
+        relu, wdt, has_w, has_b = ctx.conf
+        C = x.shape[-1]
+        rows = x.numel() // C
+        dy = dy.contiguous()
+        G = int(_nat.lib().pa_bn_blocks(rows, C))
+        part = torch.empty(G * 2 * C, dtype=torch.float32, device=x.device)
+        coef = torch.empty(3 * C, dtype=torch.float32, device=x.device)
+        dw = torch.empty(C, dtype=torch.float32, device=x.device)
+        db = torch.empty(C, dtype=torch.float32, device=x.device)
+        dx = torch.empty_like(x)
+        _nat.call("pa_bn_bwd", _nat.ptr(x), _nat.ptr(dy), _nat.ptr(y), _nat.ptr(mean), _nat.ptr(rstd), _nat.ptr(wc),
+                  wdt, _nat.ptr(dx), _nat.ptr(dw), _nat.ptr(db), _nat.ptr(coef), _nat.ptr(part), rows, C, int(relu),
+                  _nat.stream())
+        return (dx, dw.to(ctx.wdtype) if has_w else None, db.to(ctx.bdtype) if has_b else None,
+                None, None, None, None, None)
+
+
+def batch_norm_nhwc_train(x, weight, bias, running_mean, running_var, momentum=0.9, eps=1e-5, relu=False):
+    """Training-mode BatchNorm over all axes but the last (channels) (+ fused ReLU).
+    ``momentum``: Paddle convention, running = momentum * running + (1 - momentum) * batch."""
+    return _BatchNormNHWC.apply(x, weight, bias, running_mean, running_var, float(momentum), float(eps), bool(relu))
+
+
+def batch_norm_nhwc_eval(x, weight, bias, running_mean, running_var, eps=1e-5, relu=False):
+    C = x.shape[-1]
+    mean = running_mean.float().contiguous()
+    rstd = torch.rsqrt(running_var.float() + eps).contiguous()
+    wdt, wc = _wdt(weight)
+    _, bc = _wdt(bias) if bias is not None else (0, None)
+    if bc is not None and wc is not None and bc.dtype != wc.dtype:
+        bc = bc.to(wc.dtype)
+    if torch.is_grad_enabled() and (x.requires_grad or (weight is not None and weight.requires_grad)):
+        # differentiable eval-mode BN (rare): plain torch expression
+        sh = mean.to(x.dtype), rstd.to(x.dtype)
+        y = (x - sh[0]) * sh[1]
+        if weight is not None:
+            y = y * weight.to(x.dtype)
+        if bias is not None:
+            y = y + bias.to(x.dtype)
+        return torch.relu(y) if relu else y
+    y = torch.empty_like(x)
+    _nat.call("pa_bn_apply", _nat.ptr(x), _nat.ptr(y), _nat.ptr(mean), _nat.ptr(rstd), _nat.ptr(wc), _nat.ptr(bc),
+              wdt, x.numel() // C, C, int(relu), _nat.stream())
+    return y
+
+
+# --------------------------------------------------------------------- pooling
+
+
+class _MaxPoolNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        N, H, W, C = x.shape
+        OH = (H + 2 * p[0] - k[0]) // s[0] + 1
+        OW = (W + 2 * p[1] - k[1]) // s[1] + 1
+        y = torch.empty(N, OH, OW, C, dtype=x.dtype, device=x.device)
+        idx = torch.empty(N, OH, OW, C, dtype=torch.uint8, device=x.device)
+        _nat.call("pa_maxpool_nhwc_fwd", _nat.ptr(x), _nat.ptr(y), _nat.ptr(idx), N, H, W, C, OH, OW, k[0], k[1],
+                  s[0], s[1], p[0], p[1], _nat.stream())
+        ctx.save_for_backward(idx)
+        ctx.conf = (x.shape, k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        (N, H, W, C), k, s, p = ctx.conf
+        dy = dy.contiguous()
+        dx = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
+        _nat.call("pa_maxpool_nhwc_bwd", _nat.ptr(dy), _nat.ptr(idx), _nat.ptr(dx), N, H, W, C, dy.shape[1],
+                  dy.shape[2], k[0], k[1], s[0], s[1], p[0], p[1], _nat.stream())
+        return dx, None, None, None
+
+
+def supported_pool(x, ceil_mode=False):
+    return (_ENABLED[0] and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.is_contiguous() and x.shape[-1] % 8 == 0
+            and not ceil_mode)
+
+
+def max_pool2d_nhwc(x, kernel_size, stride=None, padding=0):
+    k = tuple(map(_i, _pair(kernel_size)))
+    s = tuple(map(_i, _pair(stride if stride is not None else kernel_size)))
+    p = tuple(map(_i, _pair(padding)))
+    return _MaxPoolNHWC.apply(x, k, s, p)
+
+
+class _GapNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        N, H, W, C = x.shape
+        y = torch.empty(N, 1, 1, C, dtype=x.dtype, device=x.device)
+        _nat.call("pa_gap_nhwc_fwd", _nat.ptr(x), _nat.ptr(y), N, H * W, C, _nat.stream())
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, H, W, C = ctx.shape
+        dy = dy.contiguous()
+        dx = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
+        _nat.call("pa_gap_nhwc_bwd", _nat.ptr(dy), _nat.ptr(dx), N, H * W, C, _nat.stream())
+        return dx
+
+
+def global_avg_pool_nhwc(x):
+    return _GapNHWC.apply(x)

@@ -14,6 +14,7 @@ from __future__ import annotations
 import torch
 
 from .. import nn
+from ..ops import conv as _conv
 
 
 class LeNet(nn.Layer):
@@ -33,6 +34,16 @@ class LeNet(nn.Layer):
         return x
 
 
+def _bn_relu(bn, x):
+    """relu(bn(x)); one fused HIP pass (BatchNorm with the ReLU in its epilogue and
+    the ReLU mask applied in its backward) for NHWC bf16 training on the GPU."""
+    if isinstance(bn, nn.layer_bn_types()) and bn.training and not bn._use_global_stats \
+            and bn._data_format == "NHWC" and _conv.supported_bn(x):
+        return _conv.batch_norm_nhwc_train(x, bn.weight, bn.bias, bn._mean, bn._variance, bn._momentum,
+                                           bn._epsilon, relu=True)
+    return torch.relu(bn(x))
+
+
 class BasicBlock(nn.Layer):
     expansion = 1
 
@@ -50,7 +61,7 @@ class BasicBlock(nn.Layer):
 
     def forward(self, x):
         identity = x
-        out = self.relu(self.bn1(self.conv1(x)))
+        out = _bn_relu(self.bn1, self.conv1(x))
         out = self.bn2(self.conv2(out))
         if self.downsample is not None:
             identity = self.downsample(x)
@@ -77,8 +88,8 @@ class BottleneckBlock(nn.Layer):
 
     def forward(self, x):
         identity = x
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
+        out = _bn_relu(self.bn1, self.conv1(x))
+        out = _bn_relu(self.bn2, self.conv2(out))
         out = self.bn3(self.conv3(out))
         if self.downsample is not None:
             identity = self.downsample(x)
@@ -123,7 +134,7 @@ class ResNet(nn.Layer):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(_bn_relu(self.bn1, self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         if self.with_pool:
             x = self.avgpool(x)

@@ -94,3 +94,17 @@ def test_linear_helpers_match_torch():
     G.linear_dw(x, dy, out=mg, accumulate=True)
     ref = 2 * (x.float().t() @ dy.float())
     assert torch.allclose(mg, ref, atol=1e-2 * M ** 0.5, rtol=1e-4), (mg - ref).abs().max()
+
+
+@pytest.mark.parametrize("M,N,K,a_kmaj,b_kmaj", [(64, 576, 100352, False, False), (128, 1152, 25000, False, False),
+                                                 (256, 256, 9216, True, True)])
+def test_gemm_splitk(M, N, K, a_kmaj, b_kmaj):
+    from paddle_amd.ops import gemm as G
+
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    a, af = _operand(M, K, a_kmaj, gen)
+    b, bf = _operand(N, K, b_kmaj, gen)
+    out = torch.full((M, N), 0.5, device="cuda")
+    G.gemm_splitk(a, b, M, N, K, a_kmaj=a_kmaj, b_kmaj=b_kmaj, out=out, accumulate=True)
+    ref = 0.5 + af @ bf.t()
+    assert torch.allclose(out, ref, atol=3e-3 * K ** 0.5, rtol=1e-4), (out - ref).abs().max()
