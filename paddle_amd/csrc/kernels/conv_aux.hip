@@ -192,7 +192,7 @@ __global__ __launch_bounds__(1024) void bn_finalize_fwd_kernel(const float* __re
 // chunk for its whole grid-stride loop and folds (mean, rstd, w, b) into one FMA.
 __global__ void bn_apply_kernel(const u16* __restrict__ x, u16* __restrict__ y, const float* __restrict__ mean,
                                 const float* __restrict__ rstd, const void* __restrict__ w, const void* __restrict__ b,
-                                int wdt, long rows, int C, int relu) {
+                                int wdt, long rows, int C, int relu, const u16* __restrict__ res) {
   const int chunks = C / 8;
   const long total = rows * chunks;
   const long stride = (long)gridDim.x * blockDim.x;  // multiple of chunks
@@ -208,11 +208,17 @@ __global__ void bn_apply_kernel(const u16* __restrict__ x, u16* __restrict__ y, 
     sf[j] = bb - mean[c] * sc[j];
   }
   for (long i = i0; i < total; i += stride) {
-    float a[8];
+    float a[8], r[8];
     load8(x + i * 8, a);
+    if (res) {
+      load8(res + i * 8, r);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = 0.f;
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float v = fmaf(a[j], sc[j], sf[j]);
+      const float v = fmaf(a[j], sc[j], sf[j]) + r[j];
       a[j] = relu ? fmaxf(v, 0.f) : v;
     }
     store8(y + i * 8, a);
@@ -241,7 +247,7 @@ __global__ __launch_bounds__(1024) void bn_finalize_bwd_kernel(const float* __re
 // dx = k1 * dy' - k1 * k2 - k3 * (x - mean)   (fixed channel chunk per thread, as bn_apply)
 __global__ void bn_dx_kernel(const u16* __restrict__ x, const u16* __restrict__ dy, const u16* __restrict__ y,
                              const float* __restrict__ mean, const float* __restrict__ coef, u16* __restrict__ dx,
-                             long rows, int C, int relu) {
+                             long rows, int C, int relu, u16* __restrict__ dres) {
   const int chunks = C / 8;
   const long total = rows * chunks;
   const long stride = (long)gridDim.x * blockDim.x;
@@ -265,6 +271,7 @@ __global__ void bn_dx_kernel(const u16* __restrict__ x, const u16* __restrict__ 
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = yy[j] > 0.f ? g[j] : 0.f;
     }
+    if (dres) store8(dres + i * 8, g);  // gradient of the residual input of relu(bn(x) + res)
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[j] = fmaf(k1[j], g[j], fmaf(-k3[j], a[j], k0[j]));
     store8(dx + i * 8, a);
@@ -391,12 +398,44 @@ __global__ void gap_bwd_kernel(const u16* __restrict__ dy, u16* __restrict__ dx,
 
 using namespace pa;
 
+// C < 8 (image stems): a thread copies one (pixel, kh) segment of KW*C contiguous
+// source values (the kw taps of one input row are adjacent in NHWC)
+__global__ void im2col_rowseg_kernel(const u16* __restrict__ x, u16* __restrict__ col, int N, int H, int W, int C,
+                                     int OH, int OW, int KH, int KW, int sy, int sx, int py, int px, int dy, int Kp) {
+  const long total = (long)N * OH * OW * KH;
+  const int seg = KW * C;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int kh = (int)(idx % KH);
+    const long row = idx / KH;
+    const int ox = (int)(row % OW);
+    const long t = row / OW;
+    const int oy = (int)(t % OH), n = (int)(t / OH);
+    const int iy = oy * sy - py + kh * dy;
+    const int ix0 = ox * sx - px;
+    u16* dst = col + row * Kp + kh * seg;
+    const bool yok = (unsigned)iy < (unsigned)H;
+    const u16* src = x + (((long)n * H + (yok ? iy : 0)) * W) * C;
+    for (int e = 0; e < seg; ++e) {
+      const int ix = ix0 + e / C;
+      dst[e] = (yok && (unsigned)ix < (unsigned)W) ? src[(long)ix * C + e % C] : (u16)0;
+    }
+    if (kh == KH - 1)
+      for (int e = KH * seg; e < Kp; ++e) col[row * Kp + e] = 0;
+  }
+}
+
 PA_EXPORT int pa_im2col_nhwc(const void* x, void* col, int N, int H, int W, int C, int OH, int OW, int KH, int KW,
                              int sy, int sx, int py, int px, int dy, int dx, int Kp, hipStream_t st) {
   const long rows = (long)N * OH * OW;
   const bool vec = C % 8 == 0 && Kp % 8 == 0;
   const long work = rows * (vec ? Kp / 8 : Kp);
   const int grid = stream_grid(work, 256) * 4;
+  if (!vec && dx == 1 && C < 8) {
+    const long segs = rows * KH;
+    hipLaunchKernelGGL(im2col_rowseg_kernel, dim3(stream_grid(segs, 256) * 4), dim3(256), 0, st, (const u16*)x,
+                       (u16*)col, N, H, W, C, OH, OW, KH, KW, sy, sx, py, px, dy, Kp);
+    PA_LAUNCH_CHECK();
+  }
   if (vec)
     hipLaunchKernelGGL(im2col_nhwc_kernel<true>, dim3(grid), dim3(256), 0, st, (const u16*)x, (u16*)col, N, H, W, C,
                        OH, OW, KH, KW, sy, sx, py, px, dy, dx, Kp);
@@ -438,9 +477,10 @@ static size_t bn_shm(int C) {
 
 // training forward: y = BN(x) (+ relu); writes mean / rstd for backward and updates
 // the running statistics.  part: >= pa_bn_blocks * 2 * C floats of workspace.
+// res (optional): y = relu(BN(x) + res) -- the residual add of a bottleneck block
 PA_EXPORT int pa_bn_fwd_train(const void* x, void* y, const void* w, const void* b, int wdt, float* run_mean,
                               float* run_var, float* mean, float* rstd, float* part, long rows, int C, float eps,
-                              float momentum, int relu, hipStream_t st) {
+                              float momentum, int relu, const void* res, hipStream_t st) {
   if (C % 8) return -1;
   const int G = pa_bn_blocks(rows, C);
   hipLaunchKernelGGL(bn_reduce_kernel<false>, dim3(G), dim3(BN_T), bn_shm(C), st, (const u16*)x, nullptr, nullptr,
@@ -450,7 +490,7 @@ PA_EXPORT int pa_bn_fwd_train(const void* x, void* y, const void* w, const void*
   int eg, eb;
   bn_ew_launch(rows, C, eg, eb);
   hipLaunchKernelGGL(bn_apply_kernel, dim3(eg), dim3(eb), 0, st, (const u16*)x, (u16*)y, mean, rstd, w, b, wdt, rows,
-                     C, relu);
+                     C, relu, (const u16*)res);
   PA_LAUNCH_CHECK();
 }
 
@@ -461,15 +501,16 @@ PA_EXPORT int pa_bn_apply(const void* x, void* y, const float* mean, const float
   int eg, eb;
   bn_ew_launch(rows, C, eg, eb);
   hipLaunchKernelGGL(bn_apply_kernel, dim3(eg), dim3(eb), 0, st, (const u16*)x, (u16*)y, mean, rstd, w, b, wdt, rows,
-                     C, relu);
+                     C, relu, (const u16*)nullptr);
   PA_LAUNCH_CHECK();
 }
 
 // backward: dx, dw, db (fp32) from x, dy, the saved mean / rstd and (relu) the output y.
 // coef: 3*C floats of workspace, part: pa_bn_blocks * 2 * C floats.
+// dres (optional): also write the residual gradient (= dY masked by the ReLU)
 PA_EXPORT int pa_bn_bwd(const void* x, const void* dy, const void* y, const float* mean, const float* rstd,
                         const void* w, int wdt, void* dx, float* dw, float* db, float* coef, float* part, long rows,
-                        int C, int relu, hipStream_t st) {
+                        int C, int relu, void* dres, hipStream_t st) {
   if (C % 8) return -1;
   const int G = pa_bn_blocks(rows, C);
   hipLaunchKernelGGL(bn_reduce_kernel<true>, dim3(G), dim3(BN_T), bn_shm(C), st, (const u16*)x, (const u16*)dy,
@@ -479,7 +520,7 @@ PA_EXPORT int pa_bn_bwd(const void* x, const void* dy, const void* y, const floa
   int eg, eb;
   bn_ew_launch(rows, C, eg, eb);
   hipLaunchKernelGGL(bn_dx_kernel, dim3(eg), dim3(eb), 0, st, (const u16*)x, (const u16*)dy, (const u16*)y, mean, coef,
-                     (u16*)dx, rows, C, relu);
+                     (u16*)dx, rows, C, relu, (u16*)dres);
   PA_LAUNCH_CHECK();
 }
 

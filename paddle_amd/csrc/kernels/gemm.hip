@@ -59,6 +59,7 @@ struct Params {
   // split-K through the batch index: batch b reduces k in [b*K, min((b+1)*K, k_total))
   // (k_total = 0: batches are independent GEMMs of depth K)
   int k_total;
+  int atomic;  // fp32 C only: C += tile with float atomics (split-K partials, no bias)
   // implicit-GEMM convolution (GA kernels): A(m, k) gathered from an NHWC source
   // tensor: m = (n, oy, ox) over an OH x OW grid, k = (kh, kw, c) with Cc % 64 == 0.
   // Source pixel: ny = oy*sy - py + kh*dy; with a zero-insertion factor 2^uy
@@ -622,6 +623,21 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
         }
       }
     __syncthreads();
+    if (OUTF32 && p.atomic) {
+      // split-K: one float per lane, 64 consecutive floats (256 B) per wave-instruction
+      // (guide Guideline 12: atomic wave-instructions shaped as contiguous 256 B)
+#pragma unroll 4
+      for (int it = 0; it < 2 * GR * 256 / NT; ++it) {
+        const int idx = it * NT + tid;
+        const int rr = idx >> 8, cc = idx & 255;
+        const int m = m0 + 128 * (rr / GR) + GR * ps + rr % GR;
+        const int n = n0 + cc;
+        const float v = *reinterpret_cast<const float*>(stg + rr * ROWB + cc * 4);
+        if (m < p.M && n < p.N) atomicAdd((float*)p.C + cz + (long)m * p.ldc + n, v);
+      }
+      __syncthreads();
+      continue;
+    }
     // (b) LDS rows -> global, 16 B per lane, consecutive lanes along a row
     constexpr int CPR = OUTF32 ? 64 : 32;  // 16-B chunks per 256-wide row
     constexpr int RPI = NT / CPR;          // rows per iteration
@@ -715,10 +731,11 @@ PA_EXPORT void pa_gemm_set_persistent(int s) { gemm::g_persistent = s; }
 //   b_kmaj: B is [N][ldb] K-contiguous (else [K][ldb] N-contiguous)
 //   out_f32: C is fp32 (else bf16); accumulate: C += alpha*AB (+bias)
 //   k_total > 0: split-K, batch b covers k in [b*K, min((b+1)*K, k_total)) (sA/sB are
-//   the k offsets of one split; the caller sums the per-batch outputs)
+//   the k offsets of one split); atomic (fp32 C, sC = 0): every split adds its tile
+//   into C with float atomics, otherwise the caller sums the per-batch outputs
 PA_EXPORT int pa_gemm(int a_kmaj, int b_kmaj, int out_f32, const void* A, const void* B, void* C,
                       const void* bias, int M, int N, int K, long lda, long ldb, long ldc, long sA, long sB,
-                      long sC, int batch, float alpha, int accumulate, int k_total, hipStream_t st) {
+                      long sC, int batch, float alpha, int accumulate, int k_total, int atomic, hipStream_t st) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
   // 16-B chunks: along K for a K-major operand, along M / N for an MN-major one,
   // along N for the output
@@ -729,6 +746,8 @@ PA_EXPORT int pa_gemm(int a_kmaj, int b_kmaj, int out_f32, const void* A, const 
   p.lda = lda; p.ldb = ldb; p.ldc = ldc;
   p.sA = sA; p.sB = sB; p.sC = sC;
   p.alpha = alpha; p.accumulate = accumulate; p.k_total = k_total;
+  p.atomic = atomic && out_f32;
+  if (p.atomic && bias) return -1;
   if (K <= 0) return -1;
 #define PA_G(AK, BK, F)                                                \
   if (a_kmaj == AK && b_kmaj == BK && out_f32 == F) return gemm::launch<AK, BK, F>(p, batch, st);

@@ -60,16 +60,16 @@ _SIGS = {
     "pa_conv_gemm": [_P, _P, _P, _P] + [_I] * 17 + [_P],
     "pa_im2col_nhwc": [_P, _P] + [_I] * 15 + [_P],
     "pa_bn_blocks": [_L, _I],
-    "pa_bn_fwd_train": [_P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _L, _I, _F, _F, _I, _P],
+    "pa_bn_fwd_train": [_P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _L, _I, _F, _F, _I, _P, _P],
     "pa_bn_apply": [_P, _P, _P, _P, _P, _P, _I, _L, _I, _I, _P],
-    "pa_bn_bwd": [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _L, _I, _I, _P],
+    "pa_bn_bwd": [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _L, _I, _I, _P, _P],
     "pa_maxpool_nhwc_fwd": [_P, _P, _P] + [_I] * 12 + [_P],
     "pa_maxpool_nhwc_bwd": [_P, _P, _P] + [_I] * 12 + [_P],
     "pa_gap_nhwc_fwd": [_P, _P, _I, _I, _I, _P],
     "pa_gap_nhwc_bwd": [_P, _P, _I, _I, _I, _P],
     "pa_gemm_set_sched": [_I],
     "pa_gemm_set_persistent": [_I],
-    "pa_gemm": [_I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _L, _L, _I, _F, _I, _I, _P],
+    "pa_gemm": [_I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _L, _L, _I, _F, _I, _I, _I, _P],
     "pa_splitk_reduce": [_P, _P, _L, _I, _I, _P],
     "pa_flash_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _LP, _I, _I, _I, _I, _I, _I, _F, _I, _P, _P],
 }

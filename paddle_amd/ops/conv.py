@@ -176,7 +176,7 @@ def _wdt(w):
 
 class _BatchNormNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, run_mean, run_var, momentum, eps, relu):
+    def forward(ctx, x, w, b, run_mean, run_var, momentum, eps, relu, res):
         C = x.shape[-1]
         rows = x.numel() // C
         wdt, wc = _wdt(w)
@@ -192,7 +192,7 @@ class _BatchNormNHWC(torch.autograd.Function):
         rv = run_var if rm is not None else None
         _nat.call("pa_bn_fwd_train", _nat.ptr(x), _nat.ptr(y), _nat.ptr(wc), _nat.ptr(bc), wdt, _nat.ptr(rm),
                   _nat.ptr(rv), _nat.ptr(mean), _nat.ptr(rstd), _nat.ptr(part), rows, C, float(eps),
-                  float(momentum), int(relu), _nat.stream())
+                  float(momentum), int(relu), _nat.ptr(res), _nat.stream())
         if run_mean is not None and rm is None:  # running stats kept in another dtype: update on the side
             with torch.no_grad():
                 var = 1.0 / (rstd.double() ** 2) - eps
@@ -200,7 +200,7 @@ class _BatchNormNHWC(torch.autograd.Function):
                 run_mean.mul_(momentum).add_((1 - momentum) * mean.to(run_mean.dtype))
                 run_var.mul_(momentum).add_((1 - momentum) * unb.to(run_var.dtype))
         ctx.save_for_backward(x, y if relu else None, mean, rstd, wc)
-        ctx.conf = (relu, wdt, w is not None, b is not None)
+        ctx.conf = (relu, wdt, w is not None, b is not None, res is not None)
         ctx.wdtype = w.dtype if w is not None else None
         ctx.bdtype = b.dtype if b is not None else None
         return y
@@ -208,7 +208,7 @@ class _BatchNormNHWC(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, y, mean, rstd, wc = ctx.saved_tensors
-        relu, wdt, has_w, has_b = ctx.conf
+        relu, wdt, has_w, has_b, has_res = ctx.conf
         C = x.shape[-1]
         rows = x.numel() // C
         dy = dy.contiguous()
@@ -218,17 +218,25 @@ class _BatchNormNHWC(torch.autograd.Function):
         dw = torch.empty(C, dtype=torch.float32, device=x.device)
         db = torch.empty(C, dtype=torch.float32, device=x.device)
         dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if has_res else None
         _nat.call("pa_bn_bwd", _nat.ptr(x), _nat.ptr(dy), _nat.ptr(y), _nat.ptr(mean), _nat.ptr(rstd), _nat.ptr(wc),
                   wdt, _nat.ptr(dx), _nat.ptr(dw), _nat.ptr(db), _nat.ptr(coef), _nat.ptr(part), rows, C, int(relu),
-                  _nat.stream())
+                  _nat.ptr(dres), _nat.stream())
         return (dx, dw.to(ctx.wdtype) if has_w else None, db.to(ctx.bdtype) if has_b else None,
-                None, None, None, None, None)
+                None, None, None, None, None, dres)
 
 
-def batch_norm_nhwc_train(x, weight, bias, running_mean, running_var, momentum=0.9, eps=1e-5, relu=False):
-    """Training-mode BatchNorm over all axes but the last (channels) (+ fused ReLU).
+def batch_norm_nhwc_train(x, weight, bias, running_mean, running_var, momentum=0.9, eps=1e-5, relu=False,
+                          residual=None):
+    """Training-mode BatchNorm over all axes but the last (channels), optionally
+    fused with a residual add and a ReLU: relu(BN(x) + residual).
     ``momentum``: Paddle convention, running = momentum * running + (1 - momentum) * batch."""
-    return _BatchNormNHWC.apply(x, weight, bias, running_mean, running_var, float(momentum), float(eps), bool(relu))
+    if residual is not None:
+        if not relu:
+            raise ValueError("the fused residual form is relu(bn(x) + residual)")
+        residual = residual.contiguous()
+    return _BatchNormNHWC.apply(x, weight, bias, running_mean, running_var, float(momentum), float(eps), bool(relu),
+                                residual)
 
 
 def batch_norm_nhwc_eval(x, weight, bias, running_mean, running_var, eps=1e-5, relu=False):

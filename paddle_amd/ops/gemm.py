@@ -47,7 +47,7 @@ def supported(M, N, K, *mats) -> bool:
 
 
 def gemm(a, b, M, N, K, *, a_kmaj, b_kmaj, out=None, out_dtype=torch.bfloat16, bias=None, alpha=1.0,
-         accumulate=False, batch=1, sA=0, sB=0, sC=0, ldc=None, k_total=0):
+         accumulate=False, batch=1, sA=0, sB=0, sC=0, ldc=None, k_total=0, atomic=False):
     """Raw launcher.  ``a``/``b``: bf16 CUDA tensors with unit inner stride, row
     stride = their ld.  ``out``: [M, ldc] (bf16 or fp32) written or accumulated."""
     if out is None:
@@ -63,7 +63,7 @@ def gemm(a, b, M, N, K, *, a_kmaj, b_kmaj, out=None, out_dtype=torch.bfloat16, b
     rc = _nat.lib().pa_gemm(int(a_kmaj), int(b_kmaj), int(f32), _nat.ptr(a), _nat.ptr(b), _nat.ptr(out),
                            _nat.ptr(bias),
                          M, N, K, lda, ldb, ldc, sA, sB, sC, batch, float(alpha), int(accumulate), int(k_total),
-                         _nat.stream())
+                         int(atomic), _nat.stream())
     if rc != 0:
         raise RuntimeError(f"pa_gemm failed (rc={rc}) M={M} N={N} K={K} a_kmaj={a_kmaj} b_kmaj={b_kmaj}")
     return out
@@ -102,18 +102,19 @@ def matmul_nt(a, b):
 def gemm_splitk(a, b, M, N, K, *, a_kmaj, b_kmaj, out, accumulate=False, target_blocks=512):
     """C (+)= A.B with the reduction split over enough batches to fill the chip
     (tall-K products with few output tiles: conv weight gradients).  fp32 ``out``;
-    the per-split fp32 partials are summed by ``pa_splitk_reduce``."""
+    every split adds its tile into ``out`` with float atomics in the GEMM epilogue
+    (summation order varies run to run in the last bits)."""
     tiles = ((M + 255) // 256) * ((N + 255) // 256)
     S = max(1, min(target_blocks // max(tiles, 1), K // 256))
     if S <= 1:
         return gemm(a, b, M, N, K, a_kmaj=a_kmaj, b_kmaj=b_kmaj, out=out, accumulate=accumulate)
     Ks = ((K + S - 1) // S + 63) // 64 * 64
     S = (K + Ks - 1) // Ks
-    part = torch.empty(S, M, N, dtype=torch.float32, device=out.device)
+    if not accumulate:
+        out.zero_()
     # k offset of one split, in elements: K-major operands advance along a row, MN-major by rows
     sA = Ks if a_kmaj else Ks * a.stride(-2)
     sB = Ks if b_kmaj else Ks * b.stride(-2)
-    gemm(a, b, M, N, Ks, a_kmaj=a_kmaj, b_kmaj=b_kmaj, out=part, batch=S, sA=sA, sB=sB, sC=M * N, ldc=N,
-         k_total=K)
-    _nat.call("pa_splitk_reduce", _nat.ptr(part), _nat.ptr(out), M * N, S, int(accumulate), _nat.stream())
+    gemm(a, b, M, N, Ks, a_kmaj=a_kmaj, b_kmaj=b_kmaj, out=out, batch=S, sA=sA, sB=sB, sC=0, ldc=out.stride(0),
+         k_total=K, atomic=True)
     return out

@@ -34,14 +34,20 @@ class LeNet(nn.Layer):
         return x
 
 
-def _bn_relu(bn, x):
-    """relu(bn(x)); one fused HIP pass (BatchNorm with the ReLU in its epilogue and
-    the ReLU mask applied in its backward) for NHWC bf16 training on the GPU."""
-    if isinstance(bn, nn.layer_bn_types()) and bn.training and not bn._use_global_stats \
-            and bn._data_format == "NHWC" and _conv.supported_bn(x):
+def _fusable(bn, x):
+    return isinstance(bn, nn.layer_bn_types()) and bn.training and not bn._use_global_stats \
+        and bn._data_format == "NHWC" and _conv.supported_bn(x)
+
+
+def _bn_relu(bn, x, residual=None):
+    """relu(bn(x) [+ residual]); one fused HIP pass (BatchNorm with the residual add
+    and the ReLU in its epilogue, the ReLU mask applied in its backward) for NHWC
+    bf16 training on the GPU."""
+    if _fusable(bn, x) and (residual is None or residual.shape == x.shape):
         return _conv.batch_norm_nhwc_train(x, bn.weight, bn.bias, bn._mean, bn._variance, bn._momentum,
-                                           bn._epsilon, relu=True)
-    return torch.relu(bn(x))
+                                           bn._epsilon, relu=True, residual=residual)
+    y = bn(x)
+    return torch.relu(y if residual is None else y + residual)
 
 
 class BasicBlock(nn.Layer):
@@ -62,10 +68,9 @@ class BasicBlock(nn.Layer):
     def forward(self, x):
         identity = x
         out = _bn_relu(self.bn1, self.conv1(x))
-        out = self.bn2(self.conv2(out))
         if self.downsample is not None:
             identity = self.downsample(x)
-        return self.relu(out + identity)
+        return _bn_relu(self.bn2, self.conv2(out), identity)
 
 
 class BottleneckBlock(nn.Layer):
@@ -90,10 +95,9 @@ class BottleneckBlock(nn.Layer):
         identity = x
         out = _bn_relu(self.bn1, self.conv1(x))
         out = _bn_relu(self.bn2, self.conv2(out))
-        out = self.bn3(self.conv3(out))
         if self.downsample is not None:
             identity = self.downsample(x)
-        return self.relu(out + identity)
+        return _bn_relu(self.bn3, self.conv3(out), identity)
 
 
 class ResNet(nn.Layer):
