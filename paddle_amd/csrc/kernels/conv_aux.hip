@@ -398,29 +398,38 @@ __global__ void gap_bwd_kernel(const u16* __restrict__ dy, u16* __restrict__ dx,
 
 using namespace pa;
 
-// C < 8 (image stems): a thread copies one (pixel, kh) segment of KW*C contiguous
-// source values (the kw taps of one input row are adjacent in NHWC)
-__global__ void im2col_rowseg_kernel(const u16* __restrict__ x, u16* __restrict__ col, int N, int H, int W, int C,
-                                     int OH, int OW, int KH, int KW, int sy, int sx, int py, int px, int dy, int Kp) {
-  const long total = (long)N * OH * OW * KH;
-  const int seg = KW * C;
+// C < 8 (image stems): compile-time C; a thread writes 8 consecutive columns of
+// one row (one 16-byte store) and walks (kh, kw, c) incrementally, no divisions.
+template <int CC>
+__global__ void im2col_smallc_kernel(const u16* __restrict__ x, u16* __restrict__ col, int N, int H, int W, int OH,
+                                     int OW, int KH, int KW, int sy, int sx, int py, int px, int dy, int dx, int Kp) {
+  const int K = KH * KW * CC;
+  const int per_row = Kp / 8;
+  const long total = (long)N * OH * OW * per_row;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
-    const int kh = (int)(idx % KH);
-    const long row = idx / KH;
+    const long row = idx / per_row;
+    const int e0 = (int)(idx - row * per_row) * 8;
     const int ox = (int)(row % OW);
     const long t = row / OW;
     const int oy = (int)(t % OH), n = (int)(t / OH);
-    const int iy = oy * sy - py + kh * dy;
-    const int ix0 = ox * sx - px;
-    u16* dst = col + row * Kp + kh * seg;
-    const bool yok = (unsigned)iy < (unsigned)H;
-    const u16* src = x + (((long)n * H + (yok ? iy : 0)) * W) * C;
-    for (int e = 0; e < seg; ++e) {
-      const int ix = ix0 + e / C;
-      dst[e] = (yok && (unsigned)ix < (unsigned)W) ? src[(long)ix * C + e % C] : (u16)0;
+    int tap = e0 / CC, c = e0 - tap * CC;
+    int kh = tap / KW, kw = tap - kh * KW;
+    const u16* img = x + (long)n * H * W * CC;
+    u16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int iy = oy * sy - py + kh * dy, ix = ox * sx - px + kw * dx;
+      const bool ok = e0 + j < K && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      v[j] = ok ? img[((long)iy * W + ix) * CC + c] : (u16)0;
+      if (++c == CC) {
+        c = 0;
+        if (++kw == KW) {
+          kw = 0;
+          ++kh;
+        }
+      }
     }
-    if (kh == KH - 1)
-      for (int e = KH * seg; e < Kp; ++e) col[row * Kp + e] = 0;
+    *reinterpret_cast<u16x8*>(col + row * Kp + e0) = v;
   }
 }
 
@@ -430,10 +439,17 @@ PA_EXPORT int pa_im2col_nhwc(const void* x, void* col, int N, int H, int W, int 
   const bool vec = C % 8 == 0 && Kp % 8 == 0;
   const long work = rows * (vec ? Kp / 8 : Kp);
   const int grid = stream_grid(work, 256) * 4;
-  if (!vec && dx == 1 && C < 8) {
-    const long segs = rows * KH;
-    hipLaunchKernelGGL(im2col_rowseg_kernel, dim3(stream_grid(segs, 256) * 4), dim3(256), 0, st, (const u16*)x,
-                       (u16*)col, N, H, W, C, OH, OW, KH, KW, sy, sx, py, px, dy, Kp);
+  if (!vec && C <= 4 && Kp % 8 == 0) {
+    const long work8 = rows * (Kp / 8);
+    const dim3 g(stream_grid(work8, 256) * 4), b(256);
+#define PA_SMALLC(CC)                                                                                              \
+  hipLaunchKernelGGL(im2col_smallc_kernel<CC>, g, b, 0, st, (const u16*)x, (u16*)col, N, H, W, OH, OW, KH, KW, sy, \
+                     sx, py, px, dy, dx, Kp)
+    if (C == 1) PA_SMALLC(1);
+    else if (C == 2) PA_SMALLC(2);
+    else if (C == 3) PA_SMALLC(3);
+    else PA_SMALLC(4);
+#undef PA_SMALLC
     PA_LAUNCH_CHECK();
   }
   if (vec)
