@@ -31,7 +31,8 @@ def build(name, device, args):
     if name.startswith("ernie"):
         from paddle_amd.models.ernie_moe import ERNIE_MOE_CONFIGS, ErnieMoEConfig, ErnieMoEForCausalLM
 
-        cfg = ErnieMoEConfig(**ERNIE_MOE_CONFIGS[name], use_fp8_experts=args.fp8_experts)
+        cfg = ErnieMoEConfig(**ERNIE_MOE_CONFIGS[name], use_fp8_experts=args.fp8_experts,
+                             grouped_experts=args.grouped_experts)
         H, L, V = cfg.hidden_size, cfg.num_hidden_layers, cfg.vocab_size
         kvd = cfg.kv_heads * cfg.head_dim
         active = H * (H + 2 * kvd) + H * H + 3 * H * cfg.moe_intermediate_size * cfg.top_k
@@ -52,6 +53,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--recompute", action="store_true")
     ap.add_argument("--fp8-experts", action="store_true")
+    ap.add_argument("--grouped-experts", action="store_true", help="MoE experts as ragged grouped GEMMs")
     ap.add_argument("--bucket-mb", type=int, default=512)
     ap.add_argument("--accum", type=int, default=1, help="gradient accumulation micro-steps per optimizer step")
     a = ap.parse_args()
@@ -107,7 +109,7 @@ def main():
                           "data": "synthetic", "mfu_bf16_dense": round(tok * fpt / world / 2.5e15, 4),
                           "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
                           "config": {"model": a.model, "micro_batch": a.micro_batch, "grad_accum": a.accum, "seq_len": a.seq_len,
-                                     "recompute": a.recompute, "parallelism": f"dp{world}+sharding_stage1"},
+                                     "recompute": a.recompute, "grouped_experts": a.grouped_experts, "parallelism": f"dp{world}+sharding_stage1"},
                           "loss": float(loss) * a.accum,
                           "losses": [round(float(x) * a.accum, 4) for x in hist]}))
 

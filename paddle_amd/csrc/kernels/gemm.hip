@@ -60,6 +60,13 @@ struct Params {
   // (k_total = 0: batches are independent GEMMs of depth K)
   int k_total;
   int atomic;  // fp32 C only: C += tile with float atomics (split-K partials, no bias)
+  // grouped (ragged) GEMM over batch = group: grp[0..G] are row offsets (device).
+  //  grp_mode 1: group g owns rows [grp[g], grp[g+1]) of A (K-major) and of C; M is
+  //              the largest group (sizes the grid), B advances by sB per group
+  //  grp_mode 2: group g reduces over rows [grp[g], grp[g+1]) of A and B (both
+  //              MN-major: dW of grouped experts); C advances by sC per group
+  const int* grp;
+  int grp_mode;
   // implicit-GEMM convolution (GA kernels): A(m, k) gathered from an NHWC source
   // tensor: m = (n, oy, ox) over an OH x OW grid, k = (kh, kw, c) with Cc % 64 == 0.
   // Source pixel: ny = oy*sy - py + kh*dy; with a zero-insertion factor 2^uy
@@ -294,16 +301,35 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 2, wc = wid & 3;
 
-  const int nwg = p.tiles_m * p.tiles_n;
   const long bz = blockIdx.y;
-  const int Kb = p.k_total ? min(p.K, p.k_total - (int)bz * p.K) : p.K;  // valid depth of this batch
-  const char* Ab = (const char*)p.A + bz * p.sA * 2;
-  const char* Bb = (const char*)p.B + bz * p.sB * 2;
+  int Mb = p.M;  // rows of this batch / group
+  int Kb = p.k_total ? min(p.K, p.k_total - (int)bz * p.K) : p.K;  // valid depth of this batch
+  long a_off = bz * p.sA, b_off = bz * p.sB, c_row0 = 0;
+  if (p.grp_mode) {
+    const int r0 = p.grp[bz], r1 = p.grp[bz + 1];
+    if (p.grp_mode == 1) {
+      Mb = r1 - r0;
+      a_off = (long)r0 * p.lda;
+      c_row0 = r0;
+    } else {
+      Kb = r1 - r0;
+      a_off = (long)r0 * p.lda;
+      b_off = (long)r0 * p.ldb;
+    }
+  }
+  const int tiles_m = (Mb + BM - 1) / BM;
+  const int nwg = tiles_m * p.tiles_n;
+  if (Mb <= 0 || (int)blockIdx.x >= nwg) return;  // wave-uniform: nothing for this block
+  const char* Ab = (const char*)p.A + a_off * 2;
+  const char* Bb = (const char*)p.B + b_off * 2;
   // descriptors over this batch's whole operand (host guarantees < 4 GiB)
+  // (an empty group, Kb == 0, gets a zero-size range: every load returns 0)
   const unsigned a_bytes = GA ? (unsigned)((long)(p.M / (p.OH * p.OW)) * p.H * p.W * p.Cc * 2)
-                         : AK ? (unsigned)(((long)(p.M - 1) * p.lda + Kb) * 2)
-                              : (unsigned)(((long)(Kb - 1) * p.lda + p.M) * 2);
-  const unsigned b_bytes = BK ? (unsigned)(((long)(p.N - 1) * p.ldb + Kb) * 2)
+                         : Kb <= 0 ? 0u
+                         : AK ? (unsigned)(((long)(Mb - 1) * p.lda + Kb) * 2)
+                              : (unsigned)(((long)(Kb - 1) * p.lda + Mb) * 2);
+  const unsigned b_bytes = Kb <= 0 ? 0u
+                         : BK ? (unsigned)(((long)(p.N - 1) * p.ldb + Kb) * 2)
                               : (unsigned)(((long)(Kb - 1) * p.ldb + p.N) * 2);
   const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, 0, a_bytes, 0x00020000);
   const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, 0, b_bytes, 0x00020000);
@@ -315,7 +341,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
     const int t = xcd_remap(vb, nwg);
     constexpr int GM = 8;
     const int band = t / (GM * p.tiles_n);
-    const int m_in_band = min(GM, p.tiles_m - band * GM);
+    const int m_in_band = min(GM, tiles_m - band * GM);
     const int tin = t - band * GM * p.tiles_n;
     tm0 = (band * GM + tin % m_in_band) * BM;
     tn0 = (tin / m_in_band) * BN;
@@ -330,8 +356,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
       gather_plan<2>(gaf, A_FIRST, wid, lane, mm0, p);
       gather_plan<2>(gas, A_SEC, wid, lane, mm0, p);
     } else {
-      dma_plan<AK, 2, KFULL>(daf, A_FIRST, 0, wid, lane, mm0, p.M, p.lda);
-      dma_plan<AK, 2, KFULL>(das, A_SEC, 0, wid, lane, mm0, p.M, p.lda);
+      dma_plan<AK, 2, KFULL>(daf, A_FIRST, 0, wid, lane, mm0, Mb, p.lda);
+      dma_plan<AK, 2, KFULL>(das, A_SEC, 0, wid, lane, mm0, Mb, p.lda);
     }
     dma_plan<BK, 4, KFULL>(db, B_ALL, 0, wid, lane, nn0, p.N, p.ldb);
   };
@@ -633,7 +659,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
         const int m = m0 + 128 * (rr / GR) + GR * ps + rr % GR;
         const int n = n0 + cc;
         const float v = *reinterpret_cast<const float*>(stg + rr * ROWB + cc * 4);
-        if (m < p.M && n < p.N) atomicAdd((float*)p.C + cz + (long)m * p.ldc + n, v);
+        if (m < Mb && n < p.N) atomicAdd((float*)p.C + cz + (c_row0 + m) * p.ldc + n, v);
       }
       __syncthreads();
       continue;
@@ -647,8 +673,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
       const int m = m0 + 128 * (rr / GR) + GR * ps + rr % GR;
       const int n = n0 + ch * (OUTF32 ? 4 : 8);
       const f32x4 v = *reinterpret_cast<const f32x4*>(stg + rr * ROWB + ch * 16);
-      if (m < p.M && n < p.N) {
-        char* g = (char*)p.C + (cz + (long)m * p.ldc + n) * (OUTF32 ? 4 : 2);
+      if (m < Mb && n < p.N) {
+        char* g = (char*)p.C + (cz + (c_row0 + m) * p.ldc + n) * (OUTF32 ? 4 : 2);
         if (OUTF32) {
           f32x4 o = v;
           if (p.accumulate) o += *reinterpret_cast<const f32x4*>(g);
@@ -710,7 +736,7 @@ static int launch(const Params& p0, int batch, hipStream_t st) {
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (p.N + BN - 1) / BN;
   const bool pf = g_sched < 0 ? (!AK && !BK) : g_sched == 1;
-  if (p.K % BKT == 0 && p.k_total % BKT == 0)  // every k-tile full: the k range check is wave-uniform
+  if (p.K % BKT == 0 && p.k_total % BKT == 0 && p.grp_mode != 2)  // every k-tile full: uniform k check
     return pf ? launch_v<AK, BK, F32, true, true>(p, batch, st) : launch_v<AK, BK, F32, false, true>(p, batch, st);
   return pf ? launch_v<AK, BK, F32, true, false>(p, batch, st) : launch_v<AK, BK, F32, false, false>(p, batch, st);
 }
@@ -730,12 +756,14 @@ PA_EXPORT void pa_gemm_set_persistent(int s) { gemm::g_persistent = s; }
 //   a_kmaj: A is [M][lda] K-contiguous (else [K][lda] M-contiguous)
 //   b_kmaj: B is [N][ldb] K-contiguous (else [K][ldb] N-contiguous)
 //   out_f32: C is fp32 (else bf16); accumulate: C += alpha*AB (+bias)
+//   grp (device int[batch + 1]) + grp_mode: grouped / ragged GEMM (see Params)
 //   k_total > 0: split-K, batch b covers k in [b*K, min((b+1)*K, k_total)) (sA/sB are
 //   the k offsets of one split); atomic (fp32 C, sC = 0): every split adds its tile
 //   into C with float atomics, otherwise the caller sums the per-batch outputs
 PA_EXPORT int pa_gemm(int a_kmaj, int b_kmaj, int out_f32, const void* A, const void* B, void* C,
                       const void* bias, int M, int N, int K, long lda, long ldb, long ldc, long sA, long sB,
-                      long sC, int batch, float alpha, int accumulate, int k_total, int atomic, hipStream_t st) {
+                      long sC, int batch, float alpha, int accumulate, int k_total, int atomic, const int* grp,
+                      int grp_mode, hipStream_t st) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
   // 16-B chunks: along K for a K-major operand, along M / N for an MN-major one,
   // along N for the output
@@ -747,6 +775,8 @@ PA_EXPORT int pa_gemm(int a_kmaj, int b_kmaj, int out_f32, const void* A, const 
   p.sA = sA; p.sB = sB; p.sC = sC;
   p.alpha = alpha; p.accumulate = accumulate; p.k_total = k_total;
   p.atomic = atomic && out_f32;
+  p.grp = grp;
+  p.grp_mode = grp ? grp_mode : 0;
   if (p.atomic && bias) return -1;
   if (K <= 0) return -1;
 #define PA_G(AK, BK, F)                                                \

@@ -13,7 +13,6 @@ experts.  Expert GEMMs can run in fp8 (e4m3 weights, see :mod:`..ops.fp8`).
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 
 import torch
@@ -21,6 +20,7 @@ import torch
 from .. import ops
 from ..distributed.fleet.moe import MoELayer, TopKGate
 from ..nn import Layer
+from ..ops import grouped as _grouped
 from ..ops.fp8 import fp8_linear
 from ..ops.fused import param_ready
 from .llama import _dt, _param
@@ -46,7 +46,7 @@ class ErnieMoEConfig:
     rope_theta: float = 500000.0
     initializer_range: float = 0.02
     use_fp8_experts: bool = False
-    grouped_experts: bool = False         # one batched GEMM per projection over all local experts (CPU-verified; GPU run pending)
+    grouped_experts: bool = False         # ragged grouped GEMMs over all local experts (ops/grouped.py)
     dtype: str = "bfloat16"
 
     @property
@@ -83,14 +83,16 @@ class SwiGLUExpert(Layer):
 
 class GroupedSwiGLUExperts(Layer):
     """All local experts of one MoE layer as stacked weights: gate_up [n, H, 2I],
-    down [n, I, H].  ``forward_grouped`` pads each expert's (expert-sorted) tokens to
-    the largest count rounded up to 16 rows and runs each projection as ONE batched
-    GEMM (hipBLASLt strided-batched) with the fused SwiGLU kernel between them, in
-    place of ``n`` separate GEMM chains: at 64 experts x ~768 tokens each the
-    per-expert loop is launch-bound (ernie-moe-a3b-8l ran at 12 % MFU).  Expert ``e``
-    is initialised from the same per-expert seed as ``SwiGLUExpert`` so the layout
-    (grouped or not, any EP degree) does not change the model.  Reference: the
-    MoE layer of Fleet (SURVEY.md §2.5 EP row) runs experts one by one."""
+    down [n, I, H].  On the GPU ``forward_grouped`` runs the expert-sorted tokens
+    through :mod:`..ops.grouped` -- ragged grouped MFMA GEMMs (each workgroup reads
+    its expert's row range, no padding) with the fused SwiGLU kernel between them
+    and per-expert dW accumulated into the fp32 main_grad -- in place of ``n``
+    separate GEMM chains, which are launch-bound at 64 experts x ~768 tokens
+    (ernie-moe-a3b-8l ran at 12 % MFU that way).  The CPU path pads each expert to
+    the largest count and uses batched matmuls.  Expert ``e`` is initialised from
+    the same per-expert seed as ``SwiGLUExpert`` so the layout (grouped or not, any
+    EP degree) does not change the model.  Reference: the MoE layer of Fleet
+    (SURVEY.md §2.5 EP row) runs experts one by one."""
 
     def __init__(self, H, I, experts, device, dt, std, seed_of):
         super().__init__("moe_grouped_experts")
@@ -112,6 +114,8 @@ class GroupedSwiGLUExperts(Layer):
             return x
         param_ready(self.gate_up)
         param_ready(self.down)
+        if _grouped.supported(x, self.gate_up, self.down):
+            return _grouped.grouped_swiglu_mlp(x, self.gate_up, self.down, counts)
         ct = torch.tensor(counts, device=x.device)
         e_of_row = torch.repeat_interleave(torch.arange(n, device=x.device), ct, output_size=N)
         starts = torch.cumsum(ct, 0) - ct
@@ -144,12 +148,6 @@ class ErnieMoEDecoderLayer(Layer):
             n_local = cfg.num_experts // ep
             experts = []
             if cfg.grouped_experts and not cfg.use_fp8_experts:
-                if device is not None and torch.device(device).type == "cuda" \
-                        and os.environ.get("PADDLE_AMD_MOE_GROUPED_UNSAFE") != "1":
-                    # profiles/r1_moe_grouped_probe.md: hipErrorIllegalAddress in the
-                    # step-1 backward on MI355X; refuse until the GPU regression test passes
-                    raise NotImplementedError("grouped_experts is not yet verified on the GPU "
-                                              "(set PADDLE_AMD_MOE_GROUPED_UNSAFE=1 to probe it)")
                 experts = GroupedSwiGLUExperts(H, cfg.moe_intermediate_size, range(r * n_local, (r + 1) * n_local),
                                                device, dt, std, lambda e: 7919 * (layer_idx + 1) + e)
             for e in (range(r * n_local, (r + 1) * n_local) if isinstance(experts, list) else ()):

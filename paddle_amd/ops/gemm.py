@@ -47,7 +47,7 @@ def supported(M, N, K, *mats) -> bool:
 
 
 def gemm(a, b, M, N, K, *, a_kmaj, b_kmaj, out=None, out_dtype=torch.bfloat16, bias=None, alpha=1.0,
-         accumulate=False, batch=1, sA=0, sB=0, sC=0, ldc=None, k_total=0, atomic=False):
+         accumulate=False, batch=1, sA=0, sB=0, sC=0, ldc=None, k_total=0, atomic=False, grp=None, grp_mode=0):
     """Raw launcher.  ``a``/``b``: bf16 CUDA tensors with unit inner stride, row
     stride = their ld.  ``out``: [M, ldc] (bf16 or fp32) written or accumulated."""
     if out is None:
@@ -63,7 +63,7 @@ def gemm(a, b, M, N, K, *, a_kmaj, b_kmaj, out=None, out_dtype=torch.bfloat16, b
     rc = _nat.lib().pa_gemm(int(a_kmaj), int(b_kmaj), int(f32), _nat.ptr(a), _nat.ptr(b), _nat.ptr(out),
                            _nat.ptr(bias),
                          M, N, K, lda, ldb, ldc, sA, sB, sC, batch, float(alpha), int(accumulate), int(k_total),
-                         int(atomic), _nat.stream())
+                         int(atomic), _nat.ptr(grp), int(grp_mode), _nat.stream())
     if rc != 0:
         raise RuntimeError(f"pa_gemm failed (rc={rc}) M={M} N={N} K={K} a_kmaj={a_kmaj} b_kmaj={b_kmaj}")
     return out
@@ -117,4 +117,30 @@ def gemm_splitk(a, b, M, N, K, *, a_kmaj, b_kmaj, out, accumulate=False, target_
     sB = Ks if b_kmaj else Ks * b.stride(-2)
     gemm(a, b, M, N, Ks, a_kmaj=a_kmaj, b_kmaj=b_kmaj, out=out, batch=S, sA=sA, sB=sB, sC=0, ldc=out.stride(0),
          k_total=K, atomic=True)
+    return out
+
+
+def grouped_rows(a, b, offsets, max_rows, *, b_kmaj, out, bias=None):
+    """Ragged grouped GEMM, one group per expert: rows [offsets[g], offsets[g+1]) of
+    ``a`` (K-major, [rows, K]) times expert matrix ``b[g]`` (``b``: [G, K, N] MN-major or
+    [G, N, K] K-major) into the same rows of ``out`` [rows, N].  ``offsets``: int32
+    device tensor of G+1 row offsets; ``max_rows``: the largest group (sizes the grid)."""
+    G = b.shape[0]
+    if b_kmaj:
+        Nn, K = b.shape[1], b.shape[2]
+    else:
+        K, Nn = b.shape[1], b.shape[2]
+    if G and max_rows > 0:
+        gemm(a, b[0], int(max_rows), Nn, K, a_kmaj=True, b_kmaj=b_kmaj, out=out, bias=bias, batch=G, sA=0,
+             sB=b.stride(0), sC=0, ldc=out.stride(0), grp=offsets, grp_mode=1)
+    return out
+
+
+def grouped_dw(a, b, offsets, out, accumulate=True):
+    """Per-group weight gradient out[g] (+)= a[rows_g]^T b[rows_g]: ``a`` [rows, M] and
+    ``b`` [rows, N] (both MN-major), ``out`` [G, M, N] (fp32 main_grad or bf16)."""
+    G, M, Nn = out.shape
+    if G:
+        gemm(a, b, M, Nn, 64, a_kmaj=False, b_kmaj=False, out=out[0], accumulate=accumulate, batch=G, sA=0, sB=0,
+             sC=out.stride(0), ldc=out.stride(1), grp=offsets, grp_mode=2)
     return out

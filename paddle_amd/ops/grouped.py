@@ -1,0 +1,96 @@
+"""Grouped (ragged) SwiGLU expert MLP on the hand-written MFMA GEMM.
+
+All local experts of an MoE layer run as THREE kinds of grouped GEMM launches
+instead of one GEMM chain per expert (launch-bound at 64 experts x ~768 rows) or
+a padded batched GEMM (wasted rows, a scatter and a gather):
+
+* forward  ``h = x_g @ gate_up[g]``, ``y = swiglu(h)_g @ down[g]`` -- grp_mode 1:
+  group g owns rows ``[off[g], off[g+1])`` of the expert-sorted token matrix and of
+  the output; each workgroup reads ``off[g]`` / ``off[g+1]`` and masks its tile
+  rows, so no padding and no copies.
+* backward dX -- the same ragged-row launch with the weights read K-major.
+* backward dW -- grp_mode 2: ``dW[g] (+)= x_g^T dY_g``, a per-group reduction over
+  the group's rows, accumulated in fp32 straight into the sharded optimizer's
+  ``main_grad`` (the same contract as ``ops.linear``).
+
+The reference has no MoE; the per-expert loop it would imply is
+``MoELayer`` with a list of experts (distributed/fleet/moe.py).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native as N
+from . import gemm as _G
+
+
+def _c(t):
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def supported(x, gate_up, down) -> bool:
+    if not (x.is_cuda and _G.enabled() and x.dtype == torch.bfloat16 and x.dim() == 2):
+        return False
+    if gate_up.dtype != x.dtype or down.dtype != x.dtype or gate_up.dim() != 3 or down.dim() != 3:
+        return False
+    H, I2 = gate_up.shape[1:]
+    return H % 8 == 0 and I2 % 16 == 0 and tuple(down.shape[1:]) == (I2 // 2, H) \
+        and gate_up.is_contiguous() and down.is_contiguous()
+
+
+def _wgrad(w, a, b, offs):
+    """Per-expert weight gradient into the main_grad view (or a fresh tensor)."""
+    mg = getattr(w, "_pa_main_grad", None)
+    if mg is not None:
+        # the first write after zero_grad() overwrites (beta = 0): no zero fill
+        fresh = getattr(w, "_pa_grad_fresh", False)
+        w._pa_grad_fresh = False
+        _G.grouped_dw(a, b, offs, out=mg, accumulate=not fresh)
+        return None
+    return _G.grouped_dw(a, b, offs, out=torch.empty_like(w), accumulate=False)
+
+
+class _GroupedSwiGLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gate_up, down, offs, max_rows):
+        x = _c(x)
+        R, H = x.shape
+        I2 = gate_up.shape[2]
+        I = I2 // 2
+        h = torch.empty(R, I2, dtype=x.dtype, device=x.device)
+        _G.grouped_rows(x, gate_up, offs, max_rows, b_kmaj=False, out=h)
+        a = torch.empty(R, I, dtype=x.dtype, device=x.device)
+        N.call("pa_swiglu_fwd", N.dt(h), N.ptr(h), N.ptr(a), R, I, N.stream())
+        y = torch.empty(R, H, dtype=x.dtype, device=x.device)
+        _G.grouped_rows(a, down, offs, max_rows, b_kmaj=False, out=y)
+        ctx.save_for_backward(x, gate_up, down, offs, h, a)
+        ctx.max_rows = max_rows
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gate_up, down, offs, h, a = ctx.saved_tensors
+        dy = _c(dy)
+        R, H = x.shape
+        I = a.shape[1]
+        # da = dy down[g]^T: down[g] is [I, H] = [n][k], read K-major
+        da = torch.empty(R, I, dtype=x.dtype, device=x.device)
+        _G.grouped_rows(dy, down, offs, ctx.max_rows, b_kmaj=True, out=da)
+        dh = torch.empty_like(h)
+        N.call("pa_swiglu_bwd", N.dt(h), N.ptr(h), N.ptr(da), N.ptr(dh), R, I, N.stream())
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(R, H, dtype=x.dtype, device=x.device)
+            _G.grouped_rows(dh, gate_up, offs, ctx.max_rows, b_kmaj=True, out=dx)
+        d_down = _wgrad(down, a, dy, offs) if ctx.needs_input_grad[2] else None
+        d_gu = _wgrad(gate_up, x, dh, offs) if ctx.needs_input_grad[1] else None
+        return dx, d_gu, d_down, None, None
+
+
+def grouped_swiglu_mlp(x, gate_up, down, counts):
+    """``x``: [R, H] tokens sorted by expert, ``counts``: rows per expert (host ints,
+    sum R); ``gate_up`` [G, H, 2I], ``down`` [G, I, H].  Returns [R, H]."""
+    import itertools
+
+    offs = torch.tensor([0, *itertools.accumulate(counts)], dtype=torch.int32).to(x.device, non_blocking=True)
+    return _GroupedSwiGLUFn.apply(x, gate_up, down, offs, max(counts) if counts else 0)
