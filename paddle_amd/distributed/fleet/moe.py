@@ -19,6 +19,7 @@ import torch
 import torch.nn.functional as F
 
 from ...nn import Layer
+from ...ops import moe_route as _route
 from ...parallel import comm
 
 
@@ -91,22 +92,19 @@ class MoELayer(Layer):
         val, idx, self.l_aux = self.gate(x)
         flat_e = idx.reshape(-1)                       # [T*k] expert of each (token, slot)
         flat_w = val.reshape(-1)
-        tok = torch.arange(T, device=x.device).repeat_interleave(k)
-        keep = torch.ones_like(flat_e, dtype=torch.bool)
+        keep = None
         if self.capacity_factor is not None:
             cap = max(1, int(self.capacity_factor * T * k / E))
             order = torch.argsort(flat_e, stable=True)
             se = flat_e[order]
             first = torch.searchsorted(se, se, right=False)
-            pos = torch.arange(se.numel(), device=x.device) - first
-            keep[order] = pos < cap
-        sel = keep.nonzero().squeeze(-1)
-        flat_e, flat_w, tok = flat_e[sel], flat_w[sel], tok[sel]
-        order = torch.argsort(flat_e, stable=True)
-        e_sorted = flat_e[order]
-        src_tok = tok[order]
+            rank_in_e = torch.arange(se.numel(), device=x.device) - first
+            keep = torch.empty_like(flat_e, dtype=torch.bool)
+            keep[order] = rank_in_e < cap
+        # expert-sorted kept slots: src = token of each sorted row, pos = its inverse
+        _, src, pos, e_sorted = _route.routing(flat_e, T, k, keep)
         counts = torch.bincount(e_sorted, minlength=E)  # per global expert, from this rank
-        send = x[src_tok]
+        send = _route.dispatch(x, src, pos, k)
         # exchange counts, then tokens: rank r receives, for each local expert, the
         # tokens of every peer (peer-major)
         if self.ep > 1:
@@ -141,6 +139,4 @@ class MoELayer(Layer):
             parts = list(send.split(counts.tolist()))
             y_sorted = torch.cat([self.experts[e](parts[e]) if parts[e].shape[0] else parts[e]
                                   for e in range(E)])
-        y = torch.zeros_like(x)
-        y.index_add_(0, src_tok, y_sorted * flat_w[order].unsqueeze(-1).to(y_sorted.dtype))
-        return y.reshape(shape)
+        return _route.combine(y_sorted, flat_w, pos, k).reshape(shape)

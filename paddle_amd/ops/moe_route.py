@@ -1,0 +1,103 @@
+"""MoE token dispatch / combine (csrc/kernels/moe.hip) as autograd functions.
+
+``routing(flat_e, T, k, keep)`` turns the gate's expert choice per (token, slot)
+into the expert-sorted order of the kept slots: ``src`` (token of each sorted
+row), ``pos`` (sorted row of each slot, -1 if dropped) and the sorted experts.
+``dispatch`` gathers token rows into that order; ``combine`` sums each token's k
+expert outputs weighted by the gate.  Both backward passes are gathers over
+``pos`` -- no atomics, no sort-based ``index_put`` -- and the combine backward
+produces the gate-weight gradient in the same pass.  CPU tensors take the
+equivalent torch indexing path.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native as N
+
+
+def _c(t):
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def routing(flat_e, T, k, keep=None):
+    """-> (slot_sorted [R] long, src [R] int32, pos [T*k] int32, e_sorted [R] long)."""
+    if keep is None:
+        slots = torch.argsort(flat_e, stable=True)
+    else:
+        sel = keep.nonzero().squeeze(-1)
+        slots = sel[torch.argsort(flat_e[sel], stable=True)]
+    R = slots.numel()
+    pos = torch.full((T * k,), -1, dtype=torch.int32, device=flat_e.device)
+    pos[slots] = torch.arange(R, dtype=torch.int32, device=flat_e.device)
+    src = torch.div(slots, k, rounding_mode="floor").to(torch.int32)
+    return slots, src, pos, flat_e[slots]
+
+
+def _native_ok(x):
+    return x.is_cuda and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0
+
+
+class _DispatchFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, src, pos, k):
+        x = _c(x)
+        T, H = x.shape
+        out = torch.empty(src.numel(), H, dtype=x.dtype, device=x.device)
+        N.call("pa_moe_gather", N.ptr(x), N.ptr(src), N.ptr(out), src.numel(), H, N.stream())
+        ctx.save_for_backward(pos)
+        ctx.k, ctx.T = k, T
+        return out
+
+    @staticmethod
+    def backward(ctx, ds):
+        (pos,) = ctx.saved_tensors
+        ds = _c(ds)
+        dx = torch.empty(ctx.T, ds.shape[1], dtype=ds.dtype, device=ds.device)
+        N.call("pa_moe_reduce", N.ptr(ds), N.ptr(pos), None, N.ptr(dx), ctx.T, ctx.k, ds.shape[1], N.stream())
+        return dx, None, None, None
+
+
+class _CombineFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ys, w, pos, k):
+        ys = _c(ys)
+        w = _c(w.float())
+        T, H = pos.numel() // k, ys.shape[1]
+        y = torch.empty(T, H, dtype=ys.dtype, device=ys.device)
+        N.call("pa_moe_reduce", N.ptr(ys), N.ptr(pos), N.ptr(w), N.ptr(y), T, k, H, N.stream())
+        ctx.save_for_backward(ys, w, pos)
+        ctx.k = k
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        ys, w, pos = ctx.saved_tensors
+        dy = _c(dy)
+        k, H = ctx.k, ys.shape[1]
+        T = pos.numel() // k
+        dys = torch.empty_like(ys)
+        dw = torch.empty(T * k, dtype=torch.float32, device=dy.device)
+        N.call("pa_moe_combine_bwd", N.ptr(dy), N.ptr(ys), N.ptr(pos), N.ptr(w), N.ptr(dys), N.ptr(dw), T, k, H,
+               N.stream())
+        return dys, dw, None, None
+
+
+def dispatch(x, src, pos, k):
+    """x [T, H] -> rows in sorted order [R, H]."""
+    if _native_ok(x):
+        return _DispatchFn.apply(x, src, pos, k)
+    return x[src.long()]
+
+
+def combine(ys, w, pos, k):
+    """ys [R, H] (sorted order), w [T*k] gate weights -> y [T, H]."""
+    if _native_ok(ys):
+        return _CombineFn.apply(ys, w, pos, k)
+    T = pos.numel() // k
+    keep = pos >= 0
+    slots = keep.nonzero().squeeze(-1)
+    rows = pos[slots].long()
+    y = torch.zeros(T, ys.shape[1], dtype=ys.dtype, device=ys.device)
+    contrib = ys[rows] * w[slots].unsqueeze(-1).to(ys.dtype)
+    return y.index_add(0, torch.div(slots, k, rounding_mode="floor"), contrib)
