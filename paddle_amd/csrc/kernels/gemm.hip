@@ -62,11 +62,18 @@ struct Params {
   int atomic;  // fp32 C only: C += tile with float atomics (split-K partials, no bias)
   // grouped (ragged) GEMM over batch = group: grp[0..G] are row offsets (device).
   //  grp_mode 1: group g owns rows [grp[g], grp[g+1]) of A (K-major) and of C; M is
-  //              the largest group (sizes the grid), B advances by sB per group
+  //              the total row count (sizes the grid), B advances by sB per group
   //  grp_mode 2: group g reduces over rows [grp[g], grp[g+1]) of A and B (both
   //              MN-major: dW of grouped experts); C advances by sC per group
   const int* grp;
   int grp_mode;
+  // F8 kernels: C = alpha * sa[row] * sb[col] * (A_q B_q^T); sa indexed by the
+  // global row of A (grouped: the ragged row), sb by b * sbs + n
+  const float* sa;
+  const float* sb;
+  int sbs;
+  int ngrp;  // grp_mode 1: number of groups (M = total rows)
+  const int* grp_tiles;  // grp_mode 1: per global tile row, group << 16 | row tile in group (-1: none)
   // implicit-GEMM convolution (GA kernels): A(m, k) gathered from an NHWC source
   // tensor: m = (n, oy, ox) over an OH x OW grid, k = (kh, kw, c) with Cc % 64 == 0.
   // Source pixel: ny = oy*sy - py + kh*dy; with a zero-insertion factor 2^uy
@@ -294,56 +301,119 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // (profiles/r2_gemm_v4_sched_ab.jsonl): the prefetch schedule wins ~5 % when both
 // operands take transposed reads (24 tr_b16 in one phase-1 load section
 // otherwise), and loses 2-5 % when an operand is K-major.
-template <bool AK, bool BK, bool OUTF32, bool PF_IN_CLUSTER, bool KFULL, bool GA = false>
+// One 64x32 quadrant of the non-prefetch schedule: 8 (i, j) accumulators over the
+// two 32-k halves of the k-tile.  bf16: two v_mfma_f32_16x16x32_bf16 per (i, j),
+// kk-outer so each accumulator has 7 independent MFMAs between its two updates.
+// F8 (fp8 e4m3 operands, a "k unit" = 2 fp8 bytes): the two 16-B halves of a lane
+// are one 32-byte operand of ONE block-scaled v_mfma_scale_f32_16x16x128_f8f6f4
+// (unit E8M0 scales; the per-row / per-column fp32 scales are applied in the
+// epilogue) -- the same cycles as the two bf16 MFMAs for twice the k.  A and B are
+// both read by the K-major fragment loads, so the lane -> k permutation is common
+// to both operands and the products pair up correctly.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+template <bool F8, class FA, class FB>
+__device__ __forceinline__ void quad_mma(f32x4 (&acc)[8][4], const FA (&fa)[4][2], const FB (&fb)[2][2], int I0,
+                                         int J0) {
+  if constexpr (F8) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const i32x4 a0 = __builtin_bit_cast(i32x4, fa[i][0].get()), a1 = __builtin_bit_cast(i32x4, fa[i][1].get());
+        const i32x4 b0 = __builtin_bit_cast(i32x4, fb[j][0].get()), b1 = __builtin_bit_cast(i32x4, fb[j][1].get());
+        const i32x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        const i32x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+        acc[I0 + i][J0 + j] =
+            __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bv, av, acc[I0 + i][J0 + j], 0, 0, 0, 127, 0, 127);
+      }
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[I0 + i][J0 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][kk].get(), fa[i][kk].get(), acc[I0 + i][J0 + j], 0, 0, 0);
+  }
+}
+
+template <bool AK, bool BK, bool OUTF32, bool PF_IN_CLUSTER, bool KFULL, bool GA = false, bool F8 = false, int GM = 0>
 __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 2, wc = wid & 3;
 
-  const long bz = blockIdx.y;
-  int Mb = p.M;  // rows of this batch / group
-  int Kb = p.k_total ? min(p.K, p.k_total - (int)bz * p.K) : p.K;  // valid depth of this batch
-  long a_off = bz * p.sA, b_off = bz * p.sB, c_row0 = 0;
-  if (p.grp_mode) {
-    const int r0 = p.grp[bz], r1 = p.grp[bz + 1];
-    if (p.grp_mode == 1) {
-      Mb = r1 - r0;
-      a_off = (long)r0 * p.lda;
-      c_row0 = r0;
-    } else {
-      Kb = r1 - r0;
-      a_off = (long)r0 * p.lda;
-      b_off = (long)r0 * p.ldb;
-    }
+  long bz = blockIdx.y;
+  int vb0 = blockIdx.x;  // this block's first tile (within its batch / group)
+  if constexpr (GM == 1) {
+    // grouped rows: flat tile v = (global tile row q, tile column) with q looked up in
+    // the routing's tile table (grp_tiles[q] = group << 16 | tile row within it, -1
+    // past the end), so the grid is sized from the total row count alone and the
+    // host never needs the group sizes.  One tile per block.
+    const int q = blockIdx.x / p.tiles_n;
+    const int e = p.grp_tiles[q];
+    if (e < 0) return;
+    bz = e >> 16;
+    vb0 = (e & 0xffff) * p.tiles_n + (blockIdx.x - q * p.tiles_n);  // row-major local tile
   }
-  const int tiles_m = (Mb + BM - 1) / BM;
-  const int nwg = tiles_m * p.tiles_n;
-  if (Mb <= 0 || (int)blockIdx.x >= nwg) return;  // wave-uniform: nothing for this block
-  const char* Ab = (const char*)p.A + a_off * 2;
-  const char* Bb = (const char*)p.B + b_off * 2;
-  // descriptors over this batch's whole operand (host guarantees < 4 GiB)
-  // (an empty group, Kb == 0, gets a zero-size range: every load returns 0)
-  const unsigned a_bytes = GA ? (unsigned)((long)(p.M / (p.OH * p.OW)) * p.H * p.W * p.Cc * 2)
-                         : Kb <= 0 ? 0u
-                         : AK ? (unsigned)(((long)(Mb - 1) * p.lda + Kb) * 2)
-                              : (unsigned)(((long)(Kb - 1) * p.lda + Mb) * 2);
-  const unsigned b_bytes = Kb <= 0 ? 0u
-                         : BK ? (unsigned)(((long)(p.N - 1) * p.ldb + Kb) * 2)
-                              : (unsigned)(((long)(Kb - 1) * p.ldb + p.N) * 2);
-  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, 0, a_bytes, 0x00020000);
-  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, 0, b_bytes, 0x00020000);
-
+  // per-group state (GM == 1 switches groups between persistent tiles)
+  int Mb, Kb, tiles_m, nwg;
+  long c_row0;
+  __amdgpu_buffer_rsrc_t rsA, rsB;
+  auto set_group = [&](long g) {
+    Mb = p.M;  // rows of this batch / group
+    Kb = p.k_total ? min(p.K, p.k_total - (int)g * p.K) : p.K;  // valid depth of this batch
+    long a_off = g * p.sA, b_off = g * p.sB;
+    c_row0 = 0;
+    if constexpr (GM != 0) {  // grouped: this group's row range (see Params::grp)
+      const int r0 = p.grp[g], r1 = p.grp[g + 1];
+      if constexpr (GM == 1) {
+        Mb = r1 - r0;
+        a_off = (long)r0 * p.lda;
+        c_row0 = r0;
+      } else {
+        Kb = r1 - r0;
+        a_off = (long)r0 * p.lda;
+        b_off = (long)r0 * p.ldb;
+      }
+    }
+    tiles_m = (Mb + BM - 1) / BM;
+    nwg = tiles_m * p.tiles_n;
+    const char* Ab = (const char*)p.A + a_off * 2;
+    const char* Bb = (const char*)p.B + b_off * 2;
+    // descriptors over this batch's whole operand (host guarantees < 4 GiB)
+    // (an empty group, Kb == 0, gets a zero-size range: every load returns 0)
+    const unsigned a_bytes = GA ? (unsigned)((long)(p.M / (p.OH * p.OW)) * p.H * p.W * p.Cc * 2)
+                           : Kb <= 0 ? 0u
+                           : AK ? (unsigned)(((long)(Mb - 1) * p.lda + Kb) * 2)
+                                : (unsigned)(((long)(Kb - 1) * p.lda + Mb) * 2);
+    const unsigned b_bytes = Kb <= 0 ? 0u
+                           : BK ? (unsigned)(((long)(p.N - 1) * p.ldb + Kb) * 2)
+                                : (unsigned)(((long)(Kb - 1) * p.ldb + p.N) * 2);
+    rsA = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, 0, a_bytes, 0x00020000);
+    rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, 0, b_bytes, 0x00020000);
+  };
+  set_group(bz);
+  if (Mb <= 0 || vb0 >= nwg) return;  // wave-uniform: nothing for this block
   // ---- persistent tiles: virtual block vb = blockIdx.x + i * gridDim.x; XCD remap
   // (gridDim.x is a multiple of 8 or covers every tile, so a block keeps its XCD
   // group), then bands of 8 tile-rows for L2 reuse
   auto tile_of = [&](int vb, int& tm0, int& tn0) {
+    if constexpr (GM == 1) {
+      tm0 = (vb / p.tiles_n) * BM;
+      tn0 = (vb % p.tiles_n) * BN;
+      return;
+    }
     const int t = xcd_remap(vb, nwg);
-    constexpr int GM = 8;
-    const int band = t / (GM * p.tiles_n);
-    const int m_in_band = min(GM, tiles_m - band * GM);
-    const int tin = t - band * GM * p.tiles_n;
-    tm0 = (band * GM + tin % m_in_band) * BM;
+    constexpr int BAND = 8;
+    const int band = t / (BAND * p.tiles_n);
+    const int m_in_band = min(BAND, tiles_m - band * BAND);
+    const int tin = t - band * BAND * p.tiles_n;
+    tm0 = (band * BAND + tin % m_in_band) * BM;
     tn0 = (tin / m_in_band) * BN;
   };
 
@@ -386,7 +456,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   //   A_sec(t+1) in phase 2, A_first(t+2) in phase 3, B(t+2) in phase 4.  A tile's
   //   k-tile 0 is issued before the previous tile's epilogue, so its latency hides
   //   under the epilogue (which stages C in LDS above stage 0).
-  int vb = blockIdx.x, m0, n0;
+  int vb = vb0, m0, n0;
   tile_of(vb, m0, n0);
   plan(m0, n0);
   DMA_AF(0);
@@ -431,13 +501,17 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
       WAIT_FRAGS(fa, 4);
       WAIT_FRAGS(fb0, 2);
       __builtin_amdgcn_s_setprio(1);
+      if constexpr (F8) {
+        quad_mma<true>(acc, fa, fb0, 0, 0);
+      } else {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+        for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][kk].get(), fa[i][kk].get(), acc[i][j], 0, 0, 0);
+            for (int j = 0; j < 2; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][kk].get(), fa[i][kk].get(), acc[i][j], 0, 0, 0);
+      }
       __builtin_amdgcn_s_setprio(0);
       bar();
       // ---------------- phase 2: quadrant (rows 0-63, cols 32-63)
@@ -450,13 +524,17 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
       bar();
       WAIT_FRAGS(fb1, 2);
       __builtin_amdgcn_s_setprio(1);
+      if constexpr (F8) {
+        quad_mma<true>(acc, fa, fb1, 0, 2);
+      } else {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+        for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][kk].get(), fa[i][kk].get(), acc[i][2 + j], 0, 0, 0);
+            for (int j = 0; j < 2; ++j)
+              acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][kk].get(), fa[i][kk].get(), acc[i][2 + j], 0, 0, 0);
+      }
       __builtin_amdgcn_s_setprio(0);
       bar();
       // ---------------- phase 3: quadrant (rows 64-127, cols 32-63)
@@ -468,13 +546,17 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
       bar();
       WAIT_FRAGS(fa, 4);
       __builtin_amdgcn_s_setprio(1);
+      if constexpr (F8) {
+        quad_mma<true>(acc, fa, fb1, 4, 2);
+      } else {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+        for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][kk].get(), fa[i][kk].get(), acc[4 + i][2 + j], 0, 0, 0);
+            for (int j = 0; j < 2; ++j)
+              acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][kk].get(), fa[i][kk].get(), acc[4 + i][2 + j], 0, 0, 0);
+      }
       __builtin_amdgcn_s_setprio(0);
       bar();
       // ---------------- phase 4: quadrant (rows 64-127, cols 0-31)
@@ -482,13 +564,17 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
       DMA_B(kt + 2);
       bar();
       __builtin_amdgcn_s_setprio(1);
+      if constexpr (F8) {
+        quad_mma<true>(acc, fa, fb0, 4, 0);
+      } else {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+        for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][kk].get(), fa[i][kk].get(), acc[4 + i][j], 0, 0, 0);
+            for (int j = 0; j < 2; ++j)
+              acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][kk].get(), fa[i][kk].get(), acc[4 + i][j], 0, 0, 0);
+      }
       __builtin_amdgcn_s_setprio(0);
       bar();
     }
@@ -577,8 +663,11 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   __builtin_amdgcn_s_barrier();  // every wave drained its DMAs: LDS is free
 
   // next tile's k-tile 0 (stage 0) goes out now and lands under this epilogue
+  // the epilogue below writes THIS tile; the next tile may belong to another group
+  const int eMb = Mb;
+  const long erow0 = c_row0, ebz = bz;
   const int vb_next = vb + (int)gridDim.x;
-  const bool has_next = vb_next < nwg;
+  const bool has_next = GM != 1 && vb_next < nwg;
   int m0n = 0, n0n = 0;
   if (has_next) {
     tile_of(vb_next, m0n, n0n);
@@ -596,7 +685,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   // passes of 64 rows (1024 + 16 B).
   {
   char* stg = smem + STAGE;
-  const long cz = bz * p.sC;
+  const long cz = ebz * p.sC;
   constexpr int ROWB = OUTF32 ? 1040 : 528;
   const int ml = lane & 15;
   const int nl = 64 * wc + 4 * (lane >> 4);
@@ -605,6 +694,16 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) bv[j][r] = 0.f;
+  float sbv[4][4];
+  if constexpr (F8) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + nl + 16 * j + r;
+        sbv[j][r] = n < p.N ? p.sb[ebz * p.sbs + n] : 0.f;
+      }
+  }
   if (p.bias) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -636,6 +735,12 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
       for (int j = 0; j < 4; ++j) {
         const int i = PI * ps + ii;
         char* dst = stg + (GR * wr + 16 * ii + ml) * ROWB + (nl + 16 * j) * (OUTF32 ? 4 : 2);
+        if constexpr (F8) {
+          const int m = m0 + 128 * wr + 16 * i + ml;
+          const float sam = m < eMb ? p.alpha * p.sa[erow0 + m] : 0.f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] *= sam * sbv[j][r];
+        }
         if (OUTF32) {
           f32x4 v;
 #pragma unroll
@@ -659,7 +764,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
         const int m = m0 + 128 * (rr / GR) + GR * ps + rr % GR;
         const int n = n0 + cc;
         const float v = *reinterpret_cast<const float*>(stg + rr * ROWB + cc * 4);
-        if (m < Mb && n < p.N) atomicAdd((float*)p.C + cz + (c_row0 + m) * p.ldc + n, v);
+        if (m < eMb && n < p.N) atomicAdd((float*)p.C + cz + (erow0 + m) * p.ldc + n, v);
       }
       __syncthreads();
       continue;
@@ -673,8 +778,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
       const int m = m0 + 128 * (rr / GR) + GR * ps + rr % GR;
       const int n = n0 + ch * (OUTF32 ? 4 : 8);
       const f32x4 v = *reinterpret_cast<const f32x4*>(stg + rr * ROWB + ch * 16);
-      if (m < Mb && n < p.N) {
-        char* g = (char*)p.C + (cz + (c_row0 + m) * p.ldc + n) * (OUTF32 ? 4 : 2);
+      if (m < eMb && n < p.N) {
+        char* g = (char*)p.C + (cz + (erow0 + m) * p.ldc + n) * (OUTF32 ? 4 : 2);
         if (OUTF32) {
           f32x4 o = v;
           if (p.accumulate) o += *reinterpret_cast<const f32x4*>(g);
@@ -708,11 +813,11 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
 static int g_sched = -1;      // -1: per-layout default; 0 / 1: force PF_IN_CLUSTER (A/B runs)
 static int g_persistent = 1;  // 0: one tile per block (grid = tiles), for A/B runs
 
-template <bool AK, bool BK, bool F32, bool PF, bool KFULL, bool GA = false>
+template <bool AK, bool BK, bool F32, bool PF, bool KFULL, bool GA = false, bool F8 = false, int GM = 0>
 static int launch_v(const Params& p, int batch, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_kernel<AK, BK, F32, PF, KFULL, GA>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_kernel<AK, BK, F32, PF, KFULL, GA, F8, GM>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
@@ -725,9 +830,30 @@ static int launch_v(const Params& p, int batch, hipStream_t st) {
     ncu = ncu / 8 * 8;  // keep gridDim.x a multiple of the XCD count
   }
   const int nwg = p.tiles_m * p.tiles_n;
-  const int grid = (nwg < ncu || !g_persistent) ? nwg : ncu;  // persistent: one resident block per CU
-  hipLaunchKernelGGL((gemm_kernel<AK, BK, F32, PF, KFULL, GA>), dim3(grid, batch), dim3(NT), LDS_BYTES, st, p);
+  // persistent: one resident block per CU; grouped rows: one block per tile of the
+  // flat schedule (tiles_m bounds the groups' tile rows), a single grid row
+  const int grid = (GM == 1 || nwg < ncu || !g_persistent) ? nwg : ncu;
+  hipLaunchKernelGGL((gemm_kernel<AK, BK, F32, PF, KFULL, GA, F8, GM>), dim3(grid, GM == 1 ? 1 : batch), dim3(NT),
+                     LDS_BYTES, st, p);
   return (int)hipGetLastError();
+}
+
+// GM (grouped mode) is a template parameter so plain GEMMs carry no group state
+// (registers): mode 1 needs a K-major A, mode 2 two MN-major operands.
+template <bool AK, bool BK, bool F32, int GM>
+static int launch_g(const Params& p, int batch, hipStream_t st) {
+  if constexpr ((GM == 1 && !AK) || (GM == 2 && (AK || BK))) {
+    return -1;
+  } else {
+    const bool pf = g_sched < 0 ? (!AK && !BK) : g_sched == 1;
+    if constexpr (GM != 2) {
+      if (p.K % BKT == 0 && p.k_total % BKT == 0)  // every k-tile full: the k range check is wave-uniform
+        return pf ? launch_v<AK, BK, F32, true, true, false, false, GM>(p, batch, st)
+                  : launch_v<AK, BK, F32, false, true, false, false, GM>(p, batch, st);
+    }
+    return pf ? launch_v<AK, BK, F32, true, false, false, false, GM>(p, batch, st)
+              : launch_v<AK, BK, F32, false, false, false, false, GM>(p, batch, st);
+  }
 }
 
 template <bool AK, bool BK, bool F32>
@@ -735,16 +861,92 @@ static int launch(const Params& p0, int batch, hipStream_t st) {
   Params p = p0;
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (p.N + BN - 1) / BN;
-  const bool pf = g_sched < 0 ? (!AK && !BK) : g_sched == 1;
-  if (p.K % BKT == 0 && p.k_total % BKT == 0 && p.grp_mode != 2)  // every k-tile full: uniform k check
-    return pf ? launch_v<AK, BK, F32, true, true>(p, batch, st) : launch_v<AK, BK, F32, false, true>(p, batch, st);
-  return pf ? launch_v<AK, BK, F32, true, false>(p, batch, st) : launch_v<AK, BK, F32, false, false>(p, batch, st);
+  if (p.grp_mode == 1) {
+    // every group adds at most one partial tile row beyond total_rows / BM
+    p.ngrp = batch;
+    p.tiles_m = (p.M + BM - 1) / BM + batch;
+    return launch_g<AK, BK, F32, 1>(p, batch, st);
+  }
+  if (p.grp_mode == 2) return launch_g<AK, BK, F32, 2>(p, batch, st);
+  return launch_g<AK, BK, F32, 0>(p, batch, st);
+}
+
+template <bool F32, int GM>
+static int launch_f8(const Params& p, int batch, hipStream_t st) {
+  if (p.K % BKT == 0) return launch_v<true, true, F32, false, true, false, true, GM>(p, batch, st);
+  return launch_v<true, true, F32, false, false, false, true, GM>(p, batch, st);
+}
+
+// Tile table of a grouped-rows GEMM (grp_mode 1), built on the device from the row
+// offsets grp[0..G]: tab[q] = g << 16 | j for the j-th 256-row tile of group g, in
+// group order; -1 for the unused tail up to ntab = ceil(total / 256) + G entries.
+// One block: each thread owns a contiguous chunk of groups; a block scan of the
+// chunk totals gives every chunk its first tile row.
+__global__ __launch_bounds__(1024) void group_tile_table_kernel(const int* __restrict__ grp, int G,
+                                                                int* __restrict__ tab, int ntab) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  const int per = (G + 1023) / 1024;
+  const int g0 = min(G, t * per), g1 = min(G, g0 + per);
+  int sum = 0;
+  for (int g = g0; g < g1; ++g) sum += (grp[g + 1] - grp[g] + BM - 1) / BM;
+  part[t] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
+    const int v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int q = part[t] - sum;  // first tile row of this chunk
+  for (int g = g0; g < g1; ++g) {
+    const int n = (grp[g + 1] - grp[g] + BM - 1) / BM;
+    for (int j = 0; j < n && q < ntab; ++j) tab[q++] = (g << 16) | j;
+  }
+  for (int i = part[1023] + t; i < ntab; i += 1024) tab[i] = -1;
 }
 
 }  // namespace gemm
 }  // namespace pa
 
 using namespace pa;
+
+// fp8 (OCP e4m3) GEMM, both operands K-major: C[m, n] (=|+=) alpha * sa[m] * sb[g*N + n]
+//   * sum_k A[m, k] B[n, k].  K, lda, ldb, sB in fp8 elements (multiples of 16);
+//   grp/grp_mode 1 as pa_gemm (ragged rows per group, B and sb advance per group).
+PA_EXPORT int pa_gemm_f8(int out_f32, const void* A, const void* B, void* C, const float* sa, const float* sb,
+                         int M, int N, int K, long lda, long ldb, long ldc, long sB, long sC, int batch, float alpha,
+                         int accumulate, const int* grp, int grp_mode, hipStream_t st) {
+  if (M <= 0 || N <= 0 || batch <= 0) return 0;
+  if ((N & 7) || (K & 15) || (lda & 15) || (ldb & 15) || (sB & 15) || K <= 0 || !sa || !sb) return -1;
+  gemm::Params p{};
+  p.A = A; p.B = B; p.C = C;
+  p.M = M; p.N = N; p.K = K / 2;  // k units of 2 fp8 bytes: the bf16 DMA / LDS machinery as is
+  p.lda = lda / 2; p.ldb = ldb / 2; p.ldc = ldc;
+  p.sB = sB / 2; p.sC = sC;
+  p.alpha = alpha; p.accumulate = accumulate;
+  p.grp = grp;
+  p.grp_mode = grp ? grp_mode : 0;
+  if (p.grp_mode == 2) return -1;
+  p.grp_tiles = grp ? grp + batch + 1 : nullptr;
+  p.sa = sa; p.sb = sb;
+  p.sbs = batch > 1 ? N : 0;
+  p.tiles_m = (p.M + gemm::BM - 1) / gemm::BM + (p.grp_mode ? batch : 0);
+  p.tiles_n = (p.N + gemm::BN - 1) / gemm::BN;
+  p.ngrp = batch;
+  if (out_f32) return p.grp_mode ? gemm::launch_f8<true, 1>(p, batch, st) : gemm::launch_f8<true, 0>(p, batch, st);
+  return p.grp_mode ? gemm::launch_f8<false, 1>(p, batch, st) : gemm::launch_f8<false, 0>(p, batch, st);
+}
+
+// grp: int[G + 1 + ceil(total_rows / 256) + G] -- the row offsets, then the tile
+// table of a grouped-rows GEMM (grp_mode 1), filled here from the offsets.
+PA_EXPORT int pa_group_tile_table(int* grp, int G, long total_rows, hipStream_t st) {
+  if (G <= 0 || G >= 32768 || total_rows < 0) return -1;
+  const int ntab = (int)((total_rows + gemm::BM - 1) / gemm::BM) + G;
+  hipLaunchKernelGGL(gemm::group_tile_table_kernel, dim3(1), dim3(1024), 0, st, (const int*)grp, G, grp + G + 1,
+                     ntab);
+  return (int)hipGetLastError();
+}
 
 PA_EXPORT void pa_gemm_set_sched(int s) { gemm::g_sched = s; }
 PA_EXPORT void pa_gemm_set_persistent(int s) { gemm::g_persistent = s; }
@@ -756,7 +958,8 @@ PA_EXPORT void pa_gemm_set_persistent(int s) { gemm::g_persistent = s; }
 //   a_kmaj: A is [M][lda] K-contiguous (else [K][lda] M-contiguous)
 //   b_kmaj: B is [N][ldb] K-contiguous (else [K][ldb] N-contiguous)
 //   out_f32: C is fp32 (else bf16); accumulate: C += alpha*AB (+bias)
-//   grp (device int[batch + 1]) + grp_mode: grouped / ragged GEMM (see Params)
+//   grp (device int[batch + 1], + the tile table for mode 1: pa_group_tile_table)
+//   + grp_mode: grouped / ragged GEMM (see Params)
 //   k_total > 0: split-K, batch b covers k in [b*K, min((b+1)*K, k_total)) (sA/sB are
 //   the k offsets of one split); atomic (fp32 C, sC = 0): every split adds its tile
 //   into C with float atomics, otherwise the caller sums the per-batch outputs
@@ -777,6 +980,7 @@ PA_EXPORT int pa_gemm(int a_kmaj, int b_kmaj, int out_f32, const void* A, const 
   p.atomic = atomic && out_f32;
   p.grp = grp;
   p.grp_mode = grp ? grp_mode : 0;
+  p.grp_tiles = grp ? grp + batch + 1 : nullptr;  // grp_mode 1: table after the offsets
   if (p.atomic && bias) return -1;
   if (K <= 0) return -1;
 #define PA_G(AK, BK, F)                                                \

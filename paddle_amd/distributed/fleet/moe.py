@@ -103,7 +103,8 @@ class MoELayer(Layer):
             keep[order] = rank_in_e < cap
         # expert-sorted kept slots: src = token of each sorted row, pos = its inverse
         _, src, pos, e_sorted = _route.routing(flat_e, T, k, keep)
-        counts = torch.bincount(e_sorted, minlength=E)  # per global expert, from this rank
+        # per global expert, from this rank (index_add: bincount would sync on its max)
+        counts = torch.zeros(E, dtype=torch.int64, device=x.device).index_add_(0, e_sorted, torch.ones_like(e_sorted))
         send = _route.dispatch(x, src, pos, k)
         # exchange counts, then tokens: rank r receives, for each local expert, the
         # tokens of every peer (peer-major)
@@ -134,7 +135,7 @@ class MoELayer(Layer):
             back = torch.cat([split_out[e][p] for p in range(self.ep) for e in range(self.n_local)])
             y_sorted = all_to_all(back, out_splits, in_splits, self.group)
         elif self.grouped:
-            y_sorted = self.experts.forward_grouped(send, counts.tolist())
+            y_sorted = self.experts.forward_grouped(send, counts)
         else:
             parts = list(send.split(counts.tolist()))
             y_sorted = torch.cat([self.experts[e](parts[e]) if parts[e].shape[0] else parts[e]

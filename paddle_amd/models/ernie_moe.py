@@ -94,8 +94,9 @@ class GroupedSwiGLUExperts(Layer):
     EP degree) does not change the model.  Reference: the MoE layer of Fleet
     (SURVEY.md §2.5 EP row) runs experts one by one."""
 
-    def __init__(self, H, I, experts, device, dt, std, seed_of):
+    def __init__(self, H, I, experts, device, dt, std, seed_of, fp8=False):
         super().__init__("moe_grouped_experts")
+        self.fp8 = fp8
         gu, dn = [], []
         state = torch.random.get_rng_state()
         for e in experts:
@@ -108,14 +109,20 @@ class GroupedSwiGLUExperts(Layer):
         self.num_experts = len(experts)
 
     def forward_grouped(self, x, counts):
-        n, N = self.num_experts, x.shape[0]
-        C = (max(counts) + 15) // 16 * 16 if counts else 0
-        if N == 0 or C == 0:
+        """``counts``: rows per local expert (device tensor: no host sync on the GPU
+        path; or host ints)."""
+        if x.shape[0] == 0:
             return x
         param_ready(self.gate_up)
         param_ready(self.down)
+        if self.fp8 and _grouped.supported_f8(x, self.gate_up, self.down):
+            return _grouped.grouped_swiglu_mlp(x, self.gate_up, self.down, counts, fp8=True)
         if _grouped.supported(x, self.gate_up, self.down):
             return _grouped.grouped_swiglu_mlp(x, self.gate_up, self.down, counts)
+        if torch.is_tensor(counts):
+            counts = counts.tolist()
+        n, N = self.num_experts, x.shape[0]
+        C = (max(counts) + 15) // 16 * 16
         ct = torch.tensor(counts, device=x.device)
         e_of_row = torch.repeat_interleave(torch.arange(n, device=x.device), ct, output_size=N)
         starts = torch.cumsum(ct, 0) - ct
@@ -147,9 +154,10 @@ class ErnieMoEDecoderLayer(Layer):
             r = comm.get_rank(ep_group)
             n_local = cfg.num_experts // ep
             experts = []
-            if cfg.grouped_experts and not cfg.use_fp8_experts:
+            if cfg.grouped_experts:
                 experts = GroupedSwiGLUExperts(H, cfg.moe_intermediate_size, range(r * n_local, (r + 1) * n_local),
-                                               device, dt, std, lambda e: 7919 * (layer_idx + 1) + e)
+                                               device, dt, std, lambda e: 7919 * (layer_idx + 1) + e,
+                                               fp8=cfg.use_fp8_experts)
             for e in (range(r * n_local, (r + 1) * n_local) if isinstance(experts, list) else ()):
                 # per-expert seed: expert e has the same init whatever the EP layout
                 state = torch.random.get_rng_state()

@@ -72,6 +72,10 @@ _SIGS = {
     "pa_gemm": [_I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _L, _L, _I, _F, _I, _I, _I, _P, _I, _P],
     "pa_splitk_reduce": [_P, _P, _L, _I, _I, _P],
     "pa_moe_gather": [_P, _P, _P, _L, _I, _P],
+    "pa_group_tile_table": [_P, _I, _L, _P],
+    "pa_gemm_f8": [_I, _P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _L, _I, _F, _I, _P, _I, _P],
+    "pa_quant_rows_f8": [_P, _L, _P, _L, _P, _L, _I, _P],
+    "pa_quant_cols_t_f8": [_P, _P, _P, _I, _I, _I, _P],
     "pa_moe_reduce": [_P, _P, _P, _P, _L, _I, _I, _P],
     "pa_moe_combine_bwd": [_P, _P, _P, _P, _P, _P, _L, _I, _I, _P],
     "pa_flash_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _LP, _I, _I, _I, _I, _I, _I, _F, _I, _P, _P],

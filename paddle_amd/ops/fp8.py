@@ -98,3 +98,64 @@ def fp8_linear(x, weight, bias=None, cache=None):
             except Exception:  # noqa: BLE001
                 pass
     return _FP8LinearFn.apply(x, weight, bias, cache)
+
+
+# ---------------------------------------------------------------- native fp8 GEMM
+# gemm.hip ``pa_gemm_f8``: block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 (2x the
+# bf16 MFMA rate), both operands K-major e4m3, fp32 per-row (A) / per-column (B)
+# scales applied in the epilogue.  fp8.hip quantises rows (activations, weights
+# read as stored) or transposes + quantises columns (Paddle [in, out] weights).
+
+
+def quant_rows(x):
+    """x [R, K] bf16 (K % 16 == 0) -> (q [R, K] e4m3, scale [R] fp32), x ~= q * scale[:, None]."""
+    from . import _native as N
+
+    R, K = x.shape
+    q = torch.empty(R, K, dtype=_FP8, device=x.device)
+    s = torch.empty(R, dtype=torch.float32, device=x.device)
+    N.call("pa_quant_rows_f8", N.ptr(x), x.stride(0), N.ptr(q), K, N.ptr(s), R, K, N.stream())
+    return q, s
+
+
+def quant_cols_t(w):
+    """w [G, K, N] bf16 -> (qt [G, N, K] e4m3, scale [G, N]): per-output-channel scales."""
+    from . import _native as N
+
+    w = w.contiguous()
+    G, K, Nn = w.shape
+    qt = torch.empty(G, Nn, K, dtype=_FP8, device=w.device)
+    s = torch.empty(G, Nn, dtype=torch.float32, device=w.device)
+    N.call("pa_quant_cols_t_f8", N.ptr(w), N.ptr(qt), N.ptr(s), G, K, Nn, N.stream())
+    return qt, s
+
+
+def gemm_f8(aq, sa, bq, sb, M, Nn, K, *, out, batch=1, sB=0, grp=None, grp_mode=0, alpha=1.0, accumulate=False):
+    """out[m, n] (=|+=) alpha * sa[m] * sb[g, n] * sum_k aq[m, k] bq[g][n, k]."""
+    from . import _native as N
+
+    rc = N.lib().pa_gemm_f8(int(out.dtype == torch.float32), N.ptr(aq), N.ptr(bq), N.ptr(out), N.ptr(sa), N.ptr(sb),
+                            M, Nn, K, aq.stride(0), bq.stride(-2), out.stride(0), sB, 0, batch, float(alpha),
+                            int(accumulate), N.ptr(grp), int(grp_mode), N.stream())
+    if rc != 0:
+        raise RuntimeError(f"pa_gemm_f8 failed (rc={rc}) M={M} N={Nn} K={K}")
+    return out
+
+
+class VersionedCache:
+    """Holds derived tensors of a parameter (fp8 copies), rebuilt when the weight
+    changes: its version counter or the optimizer weight epoch moves."""
+
+    def __init__(self, build):
+        self.build = build
+        self.version = None
+        self.value = None
+
+    def get(self, w):
+        from .fused import _WEIGHT_EPOCH  # bumped by optimizers that write through raw pointers
+
+        v = (_WEIGHT_EPOCH[0], w.data_ptr(), w._version)
+        if self.version != v:
+            self.value = self.build(w.detach())
+            self.version = v
+        return self.value

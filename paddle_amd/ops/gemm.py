@@ -120,18 +120,32 @@ def gemm_splitk(a, b, M, N, K, *, a_kmaj, b_kmaj, out, accumulate=False, target_
     return out
 
 
-def grouped_rows(a, b, offsets, max_rows, *, b_kmaj, out, bias=None):
+def group_table(offsets, total_rows):
+    """int32 device row offsets [G + 1] -> the buffer a grouped-rows GEMM reads: the
+    offsets followed by the tile table (group and row tile of every 256-row tile,
+    ``pa_group_tile_table``), built on the device."""
+    G = offsets.numel() - 1
+    buf = torch.empty(G + 1 + (int(total_rows) + 255) // 256 + G, dtype=torch.int32, device=offsets.device)
+    buf[:G + 1].copy_(offsets)
+    rc = _nat.lib().pa_group_tile_table(_nat.ptr(buf), G, int(total_rows), _nat.stream())
+    if rc != 0:
+        raise RuntimeError(f"pa_group_tile_table failed (rc={rc}) G={G}")
+    return buf
+
+
+def grouped_rows(a, b, offsets, *, b_kmaj, out, bias=None):
     """Ragged grouped GEMM, one group per expert: rows [offsets[g], offsets[g+1]) of
     ``a`` (K-major, [rows, K]) times expert matrix ``b[g]`` (``b``: [G, K, N] MN-major or
-    [G, N, K] K-major) into the same rows of ``out`` [rows, N].  ``offsets``: int32
-    device tensor of G+1 row offsets; ``max_rows``: the largest group (sizes the grid)."""
+    [G, N, K] K-major) into the same rows of ``out`` [rows, N].  ``offsets``: the
+    int32 buffer of :func:`group_table` (G+1 row offsets + tile table), read only on
+    the device (no host sync)."""
     G = b.shape[0]
     if b_kmaj:
         Nn, K = b.shape[1], b.shape[2]
     else:
         K, Nn = b.shape[1], b.shape[2]
-    if G and max_rows > 0:
-        gemm(a, b[0], int(max_rows), Nn, K, a_kmaj=True, b_kmaj=b_kmaj, out=out, bias=bias, batch=G, sA=0,
+    if G and a.shape[0] > 0:
+        gemm(a, b[0], a.shape[0], Nn, K, a_kmaj=True, b_kmaj=b_kmaj, out=out, bias=bias, batch=G, sA=0,
              sB=b.stride(0), sC=0, ldc=out.stride(0), grp=offsets, grp_mode=1)
     return out
 

@@ -21,6 +21,7 @@ from __future__ import annotations
 import torch
 
 from . import _native as N
+from . import fp8 as _F8
 from . import gemm as _G
 
 
@@ -52,19 +53,18 @@ def _wgrad(w, a, b, offs):
 
 class _GroupedSwiGLUFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gate_up, down, offs, max_rows):
+    def forward(ctx, x, gate_up, down, offs):
         x = _c(x)
         R, H = x.shape
         I2 = gate_up.shape[2]
         I = I2 // 2
         h = torch.empty(R, I2, dtype=x.dtype, device=x.device)
-        _G.grouped_rows(x, gate_up, offs, max_rows, b_kmaj=False, out=h)
+        _G.grouped_rows(x, gate_up, offs, b_kmaj=False, out=h)
         a = torch.empty(R, I, dtype=x.dtype, device=x.device)
         N.call("pa_swiglu_fwd", N.dt(h), N.ptr(h), N.ptr(a), R, I, N.stream())
         y = torch.empty(R, H, dtype=x.dtype, device=x.device)
-        _G.grouped_rows(a, down, offs, max_rows, b_kmaj=False, out=y)
+        _G.grouped_rows(a, down, offs, b_kmaj=False, out=y)
         ctx.save_for_backward(x, gate_up, down, offs, h, a)
-        ctx.max_rows = max_rows
         return y
 
     @staticmethod
@@ -75,22 +75,105 @@ class _GroupedSwiGLUFn(torch.autograd.Function):
         I = a.shape[1]
         # da = dy down[g]^T: down[g] is [I, H] = [n][k], read K-major
         da = torch.empty(R, I, dtype=x.dtype, device=x.device)
-        _G.grouped_rows(dy, down, offs, ctx.max_rows, b_kmaj=True, out=da)
+        _G.grouped_rows(dy, down, offs, b_kmaj=True, out=da)
         dh = torch.empty_like(h)
         N.call("pa_swiglu_bwd", N.dt(h), N.ptr(h), N.ptr(da), N.ptr(dh), R, I, N.stream())
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(R, H, dtype=x.dtype, device=x.device)
-            _G.grouped_rows(dh, gate_up, offs, ctx.max_rows, b_kmaj=True, out=dx)
+            _G.grouped_rows(dh, gate_up, offs, b_kmaj=True, out=dx)
         d_down = _wgrad(down, a, dy, offs) if ctx.needs_input_grad[2] else None
         d_gu = _wgrad(gate_up, x, dh, offs) if ctx.needs_input_grad[1] else None
-        return dx, d_gu, d_down, None, None
+        return dx, d_gu, d_down, None
 
 
-def grouped_swiglu_mlp(x, gate_up, down, counts):
-    """``x``: [R, H] tokens sorted by expert, ``counts``: rows per expert (host ints,
-    sum R); ``gate_up`` [G, H, 2I], ``down`` [G, I, H].  Returns [R, H]."""
-    import itertools
+class _F8Weights:
+    """fp8 copies of one expert weight stack [G, K, N]: K-major per-output-channel
+    for the forward (B = W^T) and row-quantised as stored for the dX GEMM."""
 
-    offs = torch.tensor([0, *itertools.accumulate(counts)], dtype=torch.int32).to(x.device, non_blocking=True)
-    return _GroupedSwiGLUFn.apply(x, gate_up, down, offs, max(counts) if counts else 0)
+    def __init__(self):
+        self.fwd = _F8.VersionedCache(_F8.quant_cols_t)
+        self.bwd = _F8.VersionedCache(lambda w: _F8.quant_rows(w.reshape(-1, w.shape[-1])))
+
+
+def _f8_cache(w):
+    c = getattr(w, "_pa_f8_grouped", None)
+    if c is None:
+        c = w._pa_f8_grouped = _F8Weights()
+    return c
+
+
+def _rows_f8(a, bq, sb, offs, N_, out):
+    """out[rows_g] = a[rows_g] @ B_g^T with B_g = bq[g] ([N_, K] e4m3, scales sb[g])."""
+    aq, sa = _F8.quant_rows(a)
+    G = sb.numel() // N_
+    if G and a.shape[0] > 0:
+        _F8.gemm_f8(aq, sa, bq, sb, a.shape[0], N_, a.shape[1], out=out, batch=G, sB=N_ * a.shape[1], grp=offs,
+                    grp_mode=1)
+    return out
+
+
+class _GroupedSwiGLUF8Fn(torch.autograd.Function):
+    """fp8 e4m3 forward and dX GEMMs (block-scaled MFMA, per-token and per-channel
+    scales); the weight gradients stay bf16 x bf16 -> fp32 main_grad."""
+
+    @staticmethod
+    def forward(ctx, x, gate_up, down, offs):
+        x = _c(x)
+        R, H = x.shape
+        G, _, I2 = gate_up.shape
+        I = I2 // 2
+        gq, gs = _f8_cache(gate_up).fwd.get(gate_up)  # [G, 2I, H]
+        dq, ds = _f8_cache(down).fwd.get(down)        # [G, H, I]
+        h = _rows_f8(x, gq, gs, offs, I2, torch.empty(R, I2, dtype=x.dtype, device=x.device))
+        a = torch.empty(R, I, dtype=x.dtype, device=x.device)
+        N.call("pa_swiglu_fwd", N.dt(h), N.ptr(h), N.ptr(a), R, I, N.stream())
+        y = _rows_f8(a, dq, ds, offs, H, torch.empty(R, H, dtype=x.dtype, device=x.device))
+        ctx.save_for_backward(x, gate_up, down, offs, h, a)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gate_up, down, offs, h, a = ctx.saved_tensors
+        dy = _c(dy)
+        R, H = x.shape
+        I = a.shape[1]
+        dbq, dbs = _f8_cache(down).bwd.get(down)      # [G*I, H]: B = down[g] as [I][H]
+        da = _rows_f8(dy, dbq, dbs, offs, I, torch.empty(R, I, dtype=x.dtype, device=x.device))
+        dh = torch.empty_like(h)
+        N.call("pa_swiglu_bwd", N.dt(h), N.ptr(h), N.ptr(da), N.ptr(dh), R, I, N.stream())
+        dx = None
+        if ctx.needs_input_grad[0]:
+            gbq, gbs = _f8_cache(gate_up).bwd.get(gate_up)  # [G*H, 2I]: B = gate_up[g] as [H][2I]
+            dx = _rows_f8(dh, gbq, gbs, offs, H, torch.empty(R, H, dtype=x.dtype, device=x.device))
+        d_down = _wgrad(down, a, dy, offs) if ctx.needs_input_grad[2] else None
+        d_gu = _wgrad(gate_up, x, dh, offs) if ctx.needs_input_grad[1] else None
+        return dx, d_gu, d_down, None
+
+
+def supported_f8(x, gate_up, down) -> bool:
+    H, I2 = gate_up.shape[1:]
+    return supported(x, gate_up, down) and H % 16 == 0 and I2 % 32 == 0 and _F8._FP8 is not None
+
+
+def expert_offsets(counts, device, total_rows):
+    """Row offsets + tile table (``gemm.group_table``) from per-expert row counts (a
+    device tensor -- no host sync -- or host ints)."""
+    if torch.is_tensor(counts):
+        offs = torch.zeros(counts.numel() + 1, dtype=torch.int32, device=device)
+        offs[1:] = torch.cumsum(counts, 0)
+    else:
+        import itertools
+
+        offs = torch.tensor([0, *itertools.accumulate(counts)], dtype=torch.int32).to(device, non_blocking=True)
+    return _G.group_table(offs, total_rows)
+
+
+def grouped_swiglu_mlp(x, gate_up, down, counts, fp8=False):
+    """``x``: [R, H] tokens sorted by expert, ``counts``: rows per expert (device
+    tensor or host ints, sum R); ``gate_up`` [G, H, 2I], ``down`` [G, I, H].  Returns
+    [R, H].  ``fp8``: forward and dX GEMMs in e4m3 (weights quantised once per
+    optimizer step)."""
+    offs = expert_offsets(counts, x.device, x.shape[0])
+    fn = _GroupedSwiGLUF8Fn if fp8 else _GroupedSwiGLUFn
+    return fn.apply(x, gate_up, down, offs)

@@ -24,22 +24,26 @@ def _offs(counts):
     return o
 
 
-@pytest.mark.parametrize("b_kmaj", [False, True])
-def test_grouped_rows(b_kmaj):
+# > 64 groups: the device-side tile schedule scans the offsets in chunks of 64
+MANY = [(7 * i) % 23 * (i % 3 != 0) for i in range(130)]
+
+
+@pytest.mark.parametrize("b_kmaj,counts", [(False, COUNTS), (True, COUNTS), (False, MANY)])
+def test_grouped_rows(b_kmaj, counts):
     from paddle_amd.ops import gemm as G
 
     g = torch.Generator(device=dev).manual_seed(int(b_kmaj))
-    K, Nn, R = 192, 320, sum(COUNTS)
-    o = _offs(COUNTS)
+    K, Nn, R = 192, 320, sum(counts)
+    o = _offs(counts)
     a = torch.randn(R, K, generator=g, device=dev).to(torch.bfloat16)
-    shape = (len(COUNTS), Nn, K) if b_kmaj else (len(COUNTS), K, Nn)
+    shape = (len(counts), Nn, K) if b_kmaj else (len(counts), K, Nn)
     b = (torch.randn(*shape, generator=g, device=dev) / K ** 0.5).to(torch.bfloat16)
     out = torch.full((R, Nn), float("nan"), device=dev).to(torch.bfloat16)
-    G.grouped_rows(a, b, torch.tensor(o, dtype=torch.int32, device=dev), max(COUNTS), b_kmaj=b_kmaj, out=out)
-    for e in range(len(COUNTS)):
+    G.grouped_rows(a, b, G.group_table(torch.tensor(o, dtype=torch.int32, device=dev), R), b_kmaj=b_kmaj, out=out)
+    for e in range(len(counts)):
         w = b[e].float().t() if b_kmaj else b[e].float()
         ref = a[o[e]:o[e + 1]].float() @ w
-        if COUNTS[e]:
+        if counts[e]:
             assert _rel(out[o[e]:o[e + 1]], ref) < 1e-2, e
 
 
