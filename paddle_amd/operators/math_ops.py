@@ -17,6 +17,7 @@ import torch.nn.functional as F
 
 from ..framework import core
 from ..framework.registry import register_op
+from ..ops import oplib as _oplib
 
 # ------------------------------------------------------------------ mul / matmul
 
@@ -147,11 +148,18 @@ _EW = {
 }
 
 
+_EW_NATIVE = {"elementwise_add": "add", "elementwise_sub": "sub", "elementwise_mul": "mul",
+              "elementwise_div": "div", "elementwise_max": "max", "elementwise_min": "min",
+              "elementwise_pow": "pow"}
+
+
 def _make_ew(name, fn):
     @register_op(name, ["X", "Y"], ["Out"], {"axis": -1, "use_mkldnn": False})
     def k(ctx):
         x, y = ctx.input("X"), ctx.input("Y")
-        ctx.set_output("Out", fn(x, bcast_y(x, y, ctx.attr("axis")).to(x.dtype)))
+        yb = bcast_y(x, y, ctx.attr("axis")).to(x.dtype)
+        out = _oplib.ew(_EW_NATIVE[name], x, yb) if (x.is_cuda and name in _EW_NATIVE) else None
+        ctx.set_output("Out", out if out is not None else fn(x, yb))
 
     k.__name__ = name
     return k
@@ -167,10 +175,31 @@ def _ew_grad(name, dx_fn, dy_fn):
     def k(ctx):
         x, y, d = ctx.input("X"), ctx.input("Y"), ctx.input("Out@GRAD")
         yb = bcast_y(x, y, ctx.attr("axis")).to(x.dtype)
+        if x.is_cuda and yb.dim() == x.dim() and not (x.requires_grad or yb.requires_grad):
+            # native: the same broadcast kernels forward and backward, broadcast
+            # gradients summed by the reduce kernel (ElemwiseGradBroadcast)
+            with torch.no_grad():
+                res = _oplib._BinaryFn.backward(_NativeGradCtx(name, x, yb), d.to(x.dtype).contiguous()) \
+                    if _oplib._ok(x, yb, d) and x.dtype == yb.dtype else None
+            if res is not None and res[1] is not None:
+                if ctx.has_output("X@GRAD"):
+                    ctx.set_output("X@GRAD", res[1], ctx.input_lod("X"))
+                if ctx.has_output("Y@GRAD"):
+                    ctx.set_output("Y@GRAD", res[2].reshape(y.shape).to(y.dtype))
+                return
         if ctx.has_output("X@GRAD"):
             ctx.set_output("X@GRAD", _reduce_to(dx_fn(x, yb, d), x.shape), ctx.input_lod("X"))
         if ctx.has_output("Y@GRAD"):
             ctx.set_output("Y@GRAD", _reduce_to(dy_fn(x, yb, d), y.shape).to(y.dtype))
+
+
+class _NativeGradCtx:
+    """Stands in for an autograd ctx so the grad op reuses ``_BinaryFn.backward``."""
+
+    def __init__(self, name, x, y):
+        self.op = name[len("elementwise_"):]
+        self.saved_tensors = (x, y)
+        self.needs_input_grad = (False, True, True)
 
 
 _ew_grad("elementwise_add", lambda x, y, d: d, lambda x, y, d: d)
@@ -343,6 +372,14 @@ def _reduce(name, fn):
         x = ctx.input("X")
         dims = ctx.attr("dim")
         dims = [dims] if isinstance(dims, int) else list(dims)
+        if x.is_cuda and x.dim() > 0:
+            rdims = list(range(x.dim())) if (ctx.attr("reduce_all") or not dims) else dims
+            out = _oplib.reduce_op(name[len("reduce_"):], x, rdims, ctx.attr("keep_dim"))
+            if out is not None:
+                if out.dim() == 0 or (not ctx.attr("keep_dim") and len(set(d % x.dim() for d in rdims)) == x.dim()):
+                    out = out.reshape([1] * x.dim()) if ctx.attr("keep_dim") else out.reshape(1)
+                ctx.set_output("Out", out)
+                return
         if ctx.attr("reduce_all") or not dims:
             out = fn(x.reshape(-1), 0, False)
             out = out.reshape([1] * x.dim()) if ctx.attr("keep_dim") else out.reshape(1)

@@ -19,6 +19,7 @@ import torch.nn.functional as F
 from .. import ops as K
 from ..framework import core
 from ..framework.registry import register_op
+from ..ops import oplib as _oplib
 
 # ------------------------------------------------------------------ conv
 
@@ -242,6 +243,13 @@ def dropout(ctx):
     if ctx.attr("is_test"):
         ctx.set_output("Out", x if upscale else x * (1.0 - p))
         return
+    if x.is_cuda and not ctx.meta:
+        # Philox4x32-10 counter RNG kernel (dropout_op.cu:27 uses curand); uint8 mask
+        r = _oplib.dropout_op(x, p, int(ctx.attr("seed")) if ctx.attr("fix_seed") else None, upscale)
+        if r is not None:
+            ctx.set_output("Out", r[0])
+            ctx.set_output("Mask", r[1])
+            return
     g = None
     if ctx.attr("fix_seed") and not ctx.meta:
         g = torch.Generator(device=x.device)
@@ -259,6 +267,11 @@ def dropout(ctx):
 def dropout_grad(ctx):
     m, d = ctx.input("Mask"), ctx.input("Out@GRAD")
     p = ctx.attr("dropout_prob")
+    if m.dtype == torch.uint8:  # native Philox mask
+        sc = 1.0 / (1.0 - p) if (ctx.attr("dropout_implementation") == "upscale_in_train" and p < 1.0) else 1.0
+        g = _oplib.mask_mul(d, m, sc)
+        ctx.set_output("X@GRAD", g if g is not None else d * m.to(d.dtype) * sc)
+        return
     g = d * m
     if ctx.attr("dropout_implementation") == "upscale_in_train" and p < 1.0:
         g = g / (1.0 - p)
@@ -510,7 +523,8 @@ def one_hot(ctx):
 @register_op("top_k", ["X"], ["Out", "Indices"], {"k": 1})
 def top_k(ctx):
     x = ctx.input("X")
-    v, i = torch.topk(x, ctx.attr("k"), -1)
+    r = _oplib.topk_op(x, ctx.attr("k")) if x.is_cuda else None
+    v, i = r if r is not None else torch.topk(x, ctx.attr("k"), -1)
     ctx.set_output("Out", v)
     ctx.set_output("Indices", i)
 

@@ -12,6 +12,7 @@ import torch
 
 from ..framework import core
 from ..framework.registry import register_op
+from ..ops import oplib as _oplib
 from ..ops import optim as fopt
 
 
@@ -27,6 +28,15 @@ def _lr(ctx):
 def sgd(ctx):
     p = ctx.input("Param")
     g = _grad(ctx)
+    if p.is_cuda:
+        out = p.clone()
+        if isinstance(g, core.SelectedRows):
+            done = _oplib.sgd_sparse_(out, g.rows(), g.get_tensor().tensor, ctx.input("LearningRate"))
+        else:
+            done = _oplib.sgd_(out, g.tensor.to(p.dtype), ctx.input("LearningRate"))
+        if done is not None:
+            ctx.set_output("ParamOut", out)
+            return
     lr = _lr(ctx).to(p.dtype)
     out = p.clone()
     if isinstance(g, core.SelectedRows):
@@ -140,6 +150,11 @@ def adagrad(ctx):
         p2[uniq] = p[uniq] - lr * gm / (torch.sqrt(m2[uniq]) + eps)
     else:
         g = g.tensor
+        p2, m2 = p.clone(), m.clone()
+        if p.is_cuda and _oplib.adagrad_(p2, g, m2, ctx.input("LearningRate"), eps) is not None:
+            ctx.set_output("ParamOut", p2)
+            ctx.set_output("MomentOut", m2)
+            return
         m2 = m + g * g
         p2 = p - lr * g / (torch.sqrt(m2) + eps)
     ctx.set_output("ParamOut", p2)

@@ -22,6 +22,7 @@ from __future__ import annotations
 import torch
 
 from ..framework.registry import register_op
+from ..ops import oplib as _oplib
 
 _ACTS = {"sigmoid": torch.sigmoid, "tanh": torch.tanh, "relu": torch.relu, "identity": lambda x: x,
          "linear": lambda x: x}
@@ -194,6 +195,11 @@ def lstmp(ctx):
 
 
 def _gru_step(g, h, W, D, act, act_gate):
+    if g.is_cuda and act is torch.tanh and act_gate is torch.sigmoid:
+        # fused gate / output kernels (math/detail/gru_gpu_kernel.h)
+        r = _oplib.gru_step(g, h, W, D)
+        if r is not None:
+            return r
     ur = g[:, :2 * D] + h @ W[:, :2 * D]
     u, r = act_gate(ur[:, :D]), act_gate(ur[:, D:])
     rh = r * h

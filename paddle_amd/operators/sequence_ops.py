@@ -16,6 +16,7 @@ import torch.nn.functional as F
 
 from ..framework import core
 from ..framework.registry import register_op
+from ..ops import oplib as _oplib
 
 
 def _last_level(ctx, slot="X"):
@@ -41,6 +42,12 @@ def sequence_pool(ctx):
     D = x.shape[1:]
     if ctx.meta:
         ctx.set_output("Out", torch.empty((n,) + tuple(D), dtype=x.dtype, device="meta"))
+        return
+    out_lod = lod[:-1] if len(lod) > 1 else None
+    r = _oplib.seq_pool_op(x, off, pt) if x.is_cuda else None
+    if r is not None:  # math/sequence_pooling.cu on the native kernel (MaxIndex int32)
+        ctx.set_output("Out", r[0], out_lod)
+        ctx.set_output("MaxIndex", r[1])
         return
     seg, lens = _seg_ids(off, x.device)
     lensf = lens.to(x.dtype).reshape((-1,) + (1,) * len(D)).clamp_min(1)
@@ -104,8 +111,10 @@ def sequence_expand(ctx):
         for _ in range(rep):
             rows += seq
             out_off.append(out_off[-1] + len(seq))
-    idx = torch.tensor(rows, dtype=torch.long, device=x.device)
-    ctx.set_output("Out", x[idx], [out_off] if xlod else None)
+    out = _oplib.gather_rows_op(x, rows) if x.is_cuda and rows else None
+    if out is None:
+        out = x[torch.tensor(rows, dtype=torch.long, device=x.device)]
+    ctx.set_output("Out", out, [out_off] if xlod else None)
 
 
 @register_op("sequence_expand_as", ["X", "Y"], ["Out"], {}, share_lod=False)
@@ -199,6 +208,14 @@ def sequence_pad(ctx):
     lens = [off[i + 1] - off[i] for i in range(n)]
     L = ctx.attr("padded_length")
     L = max(lens) if L == -1 else L
+    if x.is_cuda and pv.numel() == 1 and x.dim() >= 1:
+        # one row gather: padded slot (i, t) <- row off[i] + t, or the pad value
+        src = [off[i] + t if t < lens[i] else -1 for i in range(n) for t in range(L)]
+        out = _oplib.gather_rows_op(x, src, float(pv.reshape(-1)[0].item())) if src else None
+        if out is not None:
+            ctx.set_output("Out", out.reshape((n, L) + tuple(x.shape[1:])))
+            ctx.set_output("Length", torch.tensor(lens, dtype=torch.int64, device=x.device))
+            return
     out = pv.reshape((1, 1) + tuple(x.shape[1:]) if pv.numel() > 1 else (1,)).expand(
         (n, L) + tuple(x.shape[1:])).clone()
     for i in range(n):
@@ -211,6 +228,16 @@ def sequence_pad(ctx):
 def sequence_unpad(ctx):
     x = ctx.input("X")
     lens = [int(v) for v in ctx.input("Length").reshape(-1).tolist()]
+    if x.is_cuda and x.dim() >= 2 and sum(lens):
+        L = x.shape[1]
+        out = _oplib.gather_rows_op(x.reshape((-1,) + tuple(x.shape[2:])),
+                                    [i * L + t for i, l in enumerate(lens) for t in range(l)])
+        if out is not None:
+            off = [0]
+            for l in lens:
+                off.append(off[-1] + l)
+            ctx.set_output("Out", out, [off])
+            return
     parts = [x[i, :l] for i, l in enumerate(lens)]
     off = [0]
     for l in lens:

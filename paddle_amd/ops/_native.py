@@ -73,6 +73,22 @@ _SIGS = {
     "pa_splitk_reduce": [_P, _P, _L, _I, _I, _P],
     "pa_moe_gather": [_P, _P, _P, _L, _I, _P],
     "pa_group_tile_table": [_P, _I, _L, _P],
+    "pa_binary": [_I, _I, _P, _P, _P, _L, _I, _P, _P, _P, _I, _P],
+    "pa_reduce": [_I, _I, _P, _P, _L, _L, _L, _P],
+    "pa_dropout": [_I, _P, _P, _P, _L, _F, _F, ctypes.c_ulonglong, ctypes.c_ulonglong, _P],
+    "pa_mask_mul": [_I, _P, _P, _P, _L, _F, _P],
+    "pa_topk": [_I, _P, _P, _P, _L, _I, _I, _P],
+    "pa_sgd": [_I, _P, _P, _P, _L, _P],
+    "pa_sgd_sparse": [_P, _P, _P, _P, _L, _I, _P],
+    "pa_adagrad": [_P, _P, _P, _P, _L, _F, _P],
+    "pa_gather_rows": [_I, _P, _P, _P, _L, _I, _F, _P],
+    "pa_scatter_add_rows": [_P, _P, _P, _L, _I, _P],
+    "pa_seq_pool": [_I, _P, _P, _P, _P, _I, _I, _I, _F, _P],
+    "pa_seq_pool_grad": [_I, _P, _P, _P, _P, _I, _I, _I, _P],
+    "pa_gru_gate": [_P, _P, _P, _P, _P, _L, _I, _P],
+    "pa_gru_out": [_P, _P, _P, _P, _P, _L, _P],
+    "pa_gru_out_bwd": [_P, _P, _P, _P, _P, _P, _P, _L, _P],
+    "pa_gru_gate_bwd": [_P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
     "pa_gemm_f8": [_I, _P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _L, _I, _F, _I, _P, _I, _P],
     "pa_quant_rows_f8": [_P, _L, _P, _L, _P, _L, _I, _P],
     "pa_quant_cols_t_f8": [_P, _P, _P, _I, _I, _I, _P],
