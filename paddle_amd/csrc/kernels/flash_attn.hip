@@ -455,8 +455,9 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdParams p) {
         *reinterpret_cast<u16x4*>(DSs + (wkv + r) * (BQ * 2) + (8 * e4 + 4 * hh) * 2) = u16x4{0, 0, 0, 0};
     }
     __syncthreads();
-    // dQ[q, d-block w] = sum over the tile's 128 keys dS[q, kv] K[kv, d]
-    if (w < DB) {
+    // dQ[q, d-block db] = sum over the tile's 128 keys dS[q, kv] K[kv, d]; wave w owns
+    // d-blocks w, w + 4, ... (DB = 2 / 4 / 8 for D = 64 / 128 / 256)
+    for (int db = w; db < DB; db += 4) {
       f32x16 dq;
 #pragma unroll
       for (int e = 0; e < 16; ++e) dq[e] = 0.f;
@@ -469,9 +470,9 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdParams p) {
           const int acol = (16 * (g & 1) + 4 * gp) * 2;
           const bf8v af = cat_tr(tr_read(DSs, arow * (BQ * 2) + acol),
                                  tr_read(DSs, (arow + 4) * (BQ * 2) + acol));
-          // B = K[kv = 16ks + 8hh + j][d = 32w + r]
+          // B = K[kv = 16ks + 8hh + j][d = 32db + r]
           const int brow = 16 * ks + 8 * hh + gq;
-          const int bcol = (32 * w + 16 * (g & 1) + 4 * gp) * 2;
+          const int bcol = (32 * db + 16 * (g & 1) + 4 * gp) * 2;
           const bf8v bfk = cat_tr(tr_read(Ks, dual_off<D>(brow, bcol)), tr_read(Ks, dual_off<D>(brow + 4, bcol)));
           dq = mfma32(af, bfk, dq);
         }
@@ -480,7 +481,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdParams p) {
       for (int e = 0; e < 16; ++e) {
         const int qi = (e & 3) + 8 * (e >> 2) + 4 * hh;
         const long q = qt0 + qi;
-        if (q < p.Sq) atomicAdd(dqp + q * ((long)p.Hq * D) + 32 * w + r, dq[e]);
+        if (q < p.Sq) atomicAdd(dqp + q * ((long)p.Hq * D) + 32 * db + r, dq[e]);
       }
     }
     __syncthreads();
@@ -1145,6 +1146,9 @@ PA_EXPORT int pa_flash_attn_fwd(const void* q, const void* k, const void* v, voi
   } else if (D == 64) {
     if (causal) hipLaunchKernelGGL((fa_fwd_kernel<64, true>), grid, dim3(256), 0, st, p);
     else hipLaunchKernelGGL((fa_fwd_kernel<64, false>), grid, dim3(256), 0, st, p);
+  } else if (D == 256) {
+    if (causal) hipLaunchKernelGGL((fa_fwd_kernel<256, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((fa_fwd_kernel<256, false>), grid, dim3(256), 0, st, p);
   } else {
     return (int)hipErrorInvalidValue;
   }
@@ -1186,6 +1190,7 @@ PA_EXPORT int pa_flash_attn_bwd(const void* q, const void* k, const void* v, con
   if (variant == 4) pp.dq_acc = nullptr;  // partial slabs: no accumulator to zero
   if (D == 128) hipLaunchKernelGGL(fa_bwd_pre_kernel<128>, dim3((pre_threads + 255) / 256), dim3(256), 0, st, pp);
   else if (D == 64) hipLaunchKernelGGL(fa_bwd_pre_kernel<64>, dim3((pre_threads + 255) / 256), dim3(256), 0, st, pp);
+  else if (D == 256) hipLaunchKernelGGL(fa_bwd_pre_kernel<256>, dim3((pre_threads + 255) / 256), dim3(256), 0, st, pp);
   else return (int)hipErrorInvalidValue;
   dim3 grid(Hq, B, (Sk + 127) / 128);
   if (D == 128 && (variant == 3 || variant == 4)) {
@@ -1215,6 +1220,9 @@ PA_EXPORT int pa_flash_attn_bwd(const void* q, const void* k, const void* v, con
   }
   if (D == 128) {
     if (causal) { PA_FA_BWD_LAUNCH(128, true) } else { PA_FA_BWD_LAUNCH(128, false) }
+  } else if (D == 256) {
+    if (causal) hipLaunchKernelGGL((fa_bwd_kernel<256, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((fa_bwd_kernel<256, false>), grid, dim3(256), 0, st, p);
   } else {
     if (causal) { PA_FA_BWD_LAUNCH(64, true) } else { PA_FA_BWD_LAUNCH(64, false) }
   }

@@ -1,6 +1,7 @@
 """Fleet collective training API (hybrid parallel: dp / mp / pp / sharding / sep / ep)."""
 from .base import DistributedStrategy, HybridParallelOptimizer, TensorParallel, fleet  # noqa: F401
-from .context_parallel import allgather_kv_attention, ulysses_attention  # noqa: F401
+from .context_parallel import (allgather_kv_attention, ring_attention, ulysses_attention,  # noqa: F401
+                               zigzag_merge, zigzag_split)
 from .moe import MoELayer, TopKGate  # noqa: F401
 from .mp_layers import (ColumnParallelLinear, ParallelCrossEntropy, RowParallelLinear, TPGroup,  # noqa: F401
                         VocabParallelEmbedding, parallel_cross_entropy, vocab_parallel_embedding)

@@ -169,10 +169,10 @@ def _fa_strides(t):
     return [t.stride(0), t.stride(1), t.stride(2)]
 
 
-def _fa_fwd(q, k, v, causal, scale):
+def _fa_fwd(q, k, v, causal, scale, out=None):
     B, Sq, Hq, D = q.shape
     Sk, Hk = k.shape[1], k.shape[2]
-    o = torch.empty(B, Sq, Hq, D, dtype=q.dtype, device=q.device)
+    o = torch.empty(B, Sq, Hq, D, dtype=q.dtype, device=q.device) if out is None else out
     lse = torch.empty(B, Hq, Sq, dtype=torch.float32, device=q.device)
     st = ctypes_long_array(_fa_strides(q) + _fa_strides(k) + _fa_strides(v) + _fa_strides(o))
     N.call("pa_flash_attn_fwd", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(o), N.ptr(lse), st,
@@ -241,14 +241,85 @@ class _FlashAttnFn(torch.autograd.Function):
 
 
 def flash_attention(q, k, v, causal=True, scale=None):
-    """Fused attention over [B, S, H, D] tensors (GQA when k/v have fewer heads)."""
+    """Fused attention over [B, S, H, D] tensors (GQA when k/v have fewer heads).
+    Head dims 64 / 128 run the tuned kernels; 256 runs the same kernels
+    instantiated at D = 256 (register-spilling: a correctness path)."""
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
     if q.is_cuda:
-        if q.dtype != torch.bfloat16 or q.shape[-1] not in (64, 128):
-            raise NotImplementedError("flash_attention kernel: bf16 with head_dim 64/128")
+        if q.dtype != torch.bfloat16 or q.shape[-1] not in (64, 128, 256):
+            raise NotImplementedError("flash_attention kernel: bf16 with head_dim 64/128/256")
         return _FlashAttnFn.apply(q, k, v, causal, scale)
     return _attn_ref(q, k, v, causal, scale)
+
+
+class _FlashAttnVarlenFn(torch.autograd.Function):
+    """Packed variable-length batch: sequence i owns rows [cu_q[i], cu_q[i+1]) of q and
+    [cu_k[i], cu_k[i+1]) of k / v.  Each sequence runs the flash kernels on strided
+    [1, L, H, D] views of the packed tensors (no padding, no copies in, the output
+    written in place); the per-sequence launches are the varlen schedule."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, cu_q, cu_k, causal, scale):
+        o = torch.empty_like(q)
+        lses = []
+        for i in range(len(cu_q) - 1):
+            a, b, c, d = cu_q[i], cu_q[i + 1], cu_k[i], cu_k[i + 1]
+            if b == a:
+                lses.append(None)
+                continue
+            if d == c:
+                o[a:b].zero_()
+                lses.append(None)
+                continue
+            _, lse = _fa_fwd(q[a:b].unsqueeze(0), k[c:d].unsqueeze(0), v[c:d].unsqueeze(0), causal, scale,
+                             out=o[a:b].unsqueeze(0))
+            lses.append(lse)
+        ctx.save_for_backward(q, k, v, o)
+        ctx.lses, ctx.cu_q, ctx.cu_k, ctx.causal, ctx.scale = lses, cu_q, cu_k, causal, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o = ctx.saved_tensors
+        do = _c(do)
+        Hq, Hk, D = q.shape[1], k.shape[1], q.shape[2]
+        dq = torch.zeros_like(q)
+        dk = torch.zeros(k.shape[0], Hq, D, dtype=q.dtype, device=q.device)
+        dv = torch.zeros_like(dk)
+        for i, lse in enumerate(ctx.lses):
+            if lse is None:
+                continue
+            a, b, c, d = ctx.cu_q[i], ctx.cu_q[i + 1], ctx.cu_k[i], ctx.cu_k[i + 1]
+            acc = _fa_bwd(q[a:b].unsqueeze(0), k[c:d].unsqueeze(0), v[c:d].unsqueeze(0), o[a:b].unsqueeze(0),
+                          do[a:b].unsqueeze(0), lse, ctx.causal, ctx.scale, dk[c:d].unsqueeze(0),
+                          dv[c:d].unsqueeze(0))
+            dq[a:b] = acc[0].to(q.dtype)
+        if Hk != Hq:
+            dk = dk.view(-1, Hk, Hq // Hk, D).sum(2)
+            dv = dv.view(-1, Hk, Hq // Hk, D).sum(2)
+        return dq, dk, dv, None, None, None, None
+
+
+def flash_attention_varlen(q, k, v, cu_seqlens_q, cu_seqlens_k=None, causal=True, scale=None):
+    """Attention over packed variable-length sequences: q [total_q, Hq, D], k / v
+    [total_k, Hk, D], cu_seqlens_* host lists (or tensors) of n+1 offsets (the LoD
+    of the reference's sequence ops).  Returns [total_q, Hq, D]."""
+    cu_q = [int(x) for x in (cu_seqlens_q.tolist() if torch.is_tensor(cu_seqlens_q) else cu_seqlens_q)]
+    cu_k = cu_q if cu_seqlens_k is None else \
+        [int(x) for x in (cu_seqlens_k.tolist() if torch.is_tensor(cu_seqlens_k) else cu_seqlens_k)]
+    if len(cu_q) != len(cu_k):
+        raise ValueError("cu_seqlens_q and cu_seqlens_k describe different batch sizes")
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    if q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in (64, 128, 256):
+        return _FlashAttnVarlenFn.apply(q, k, v, cu_q, cu_k, causal, scale)
+    outs = []
+    for i in range(len(cu_q) - 1):
+        qs, ks, vs = (t[a:b].unsqueeze(0) for t, a, b in ((q, cu_q[i], cu_q[i + 1]), (k, cu_k[i], cu_k[i + 1]),
+                                                         (v, cu_k[i], cu_k[i + 1])))
+        outs.append(_attn_ref(qs, ks, vs, causal, scale)[0] if ks.shape[1] else torch.zeros_like(qs[0]))
+    return torch.cat(outs, 0) if outs else q.new_zeros(q.shape)
 
 
 class _RopeAttnFn(torch.autograd.Function):
