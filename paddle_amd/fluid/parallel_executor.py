@@ -13,19 +13,27 @@ single-process multi-place mode (several CUDAPlaces or CPU_NUM CPU places) is ke
 for API parity: replicas run on their own devices and gradients are reduced on
 device 0 and broadcast.  Both can combine (places x processes).
 
-Step = [forward+backward ops on every replica] -> gradient sync (AllReduce: sum,
-scaled by 1/N; Reduce: reduce to the size-balanced owner replica) -> [optimizer
-ops] (AllReduce: every replica; Reduce: owner replica, then parameter broadcast).
+A step is ONE SSA graph (framework/details.py, multi_devices_graph_pass.cc):
+per-replica computation nodes for the forward/backward ops (edges from
+read/write hazards), one gradient-sync node per bucket of gradients (in-process
+sum over replicas + RCCL all-reduce across processes on the communication
+stream, scaled by 1/N), sparse-gradient gather nodes, and the optimizer nodes
+(AllReduce: every replica; Reduce: the size-balanced owner replica, then a
+parameter broadcast).  The graph runs on the native DAG thread pool, so a
+bucket's all-reduce starts as soon as its gradients exist on every replica,
+overlapping the rest of the backward.
 """
 from __future__ import annotations
 
 import math
 import os
+from collections import defaultdict
 
 import numpy as np
 import torch
 
 from ..framework import core
+from ..framework import details as D
 from ..framework import registry as R
 from ..framework.executor import BlockExecutor
 from ..parallel import comm
@@ -132,6 +140,10 @@ class ParallelExecutor:
                               v.type not in (core.VT.FEED_MINIBATCH, core.VT.FETCH_LIST, core.VT.RAW)]
         self._bcast_params()
         self._step = 0
+        self._graph = None
+        self._streams = None
+        self._trace_on = bool(kwargs.get("trace", False))
+        self.trace = None
 
     # ---- helpers
     def _balance_owners(self):
@@ -192,70 +204,199 @@ class ParallelExecutor:
                     out[i][k] = core.LoDTensor(c)
         return out
 
-    def _grads(self, scope, names):
-        res = []
-        for g in names:
-            v = scope.find_var(g)
-            res.append(v.get() if v is not None else None)
-        return res
+    # ---- SSA graph
+    def _grad_buckets(self):
+        """Dense gradient buckets in backward-production order + sparse grads."""
+        gb = self._program.global_block()
+        prod = {}
+        for k, op in enumerate(self._fb_ops):
+            for n in op.output_arg_names:
+                prod[n] = k
+        items = []
+        for i, (p, g) in enumerate(self._param_grads):
+            if g not in prod:
+                continue
+            v = gb._find_var_recursive(g)
+            sparse = v is not None and v.type == core.VT.SELECTED_ROWS
+            pv = gb._find_var_recursive(p)
+            nbytes = 4 * (int(np.prod([abs(x) for x in pv.shape])) if pv is not None and pv.shape else 1)
+            items.append((prod[g], i, sparse, nbytes))
+        items.sort()
+        cap = FLAGS.get("rccl_bucket_mb") * (1 << 20)
+        buckets, sparse, cur, cur_b = [], [], [], 0
+        for k, i, sp, nb in items:
+            if sp:
+                sparse.append(i)
+                continue
+            cur.append(i)
+            cur_b += nb
+            if cur_b >= cap:
+                buckets.append(cur)
+                cur, cur_b = [], 0
+        if cur:
+            buckets.append(cur)
+        return buckets, sparse
 
-    def _sync_grads(self):
+    def _build_graph(self):
+        g = D.SSAGraph()
+        R_ = len(self._places)
+        fb_pbs = [ex.prepare(self._fb_prog, 0) for ex in self._executors]
+        opt_pbs = [ex.prepare(self._opt_prog, 0) for ex in self._executors]
+        deps = D.op_deps(self._fb_ops)
+        comp = [[None] * len(self._fb_ops) for _ in range(R_)]
+        for r in range(R_):
+            ex, sc, pb = self._executors[r], self._local_scopes[r], fb_pbs[r]
+            for k, op in enumerate(self._fb_ops):
+                comp[r][k] = g.add("compute", r, k, lambda ex=ex, pb=pb, k=k, sc=sc, r=r: self._run_op(r, ex, pb, k, sc),
+                                   op.type)
+                for d in deps[k]:
+                    g.edge(comp[r][d], comp[r][k])
+        names = [gn for _, gn in self._param_grads]
+        readers, writer = defaultdict(list), {}
+        for k, op in enumerate(self._fb_ops):
+            for n in op.input_arg_names:
+                readers[n].append(k)
+            for n in op.output_arg_names:
+                writer[n] = k
+        buckets, sparse = self._grad_buckets()
+        sync_of = {}
+        if self.device_count > 1:
+            for b, idxs in enumerate(buckets):
+                node = g.add("allreduce", -1, b, lambda idxs=idxs: self._allreduce_bucket(idxs), f"bucket{b}")
+                for i in idxs:
+                    sync_of[names[i]] = node
+                    # after the gradient's last writer and every backward reader of it
+                    for r in range(R_):
+                        for k in readers.get(names[i], []) + [writer[names[i]]]:
+                            g.edge(comp[r][k], node)
+            for i in sparse:
+                node = g.add("gather_sparse", -1, i, lambda i=i: self._gather_sparse(i), names[i])
+                sync_of[names[i]] = node
+                for r in range(R_):
+                    for k in readers.get(names[i], []) + [writer[names[i]]]:
+                        g.edge(comp[r][k], node)
+        # optimizer: after this replica's whole backward and the syncs of the grads it reads
+        reduce_mode = self._build_strategy.reduce_strategy == BuildStrategy.ReduceStrategy.Reduce and R_ > 1
+        odeps = D.op_deps(self._opt_ops)
+        opt_nodes = []
+        for r in range(R_):
+            ex, sc, pb = self._executors[r], self._local_scopes[r], opt_pbs[r]
+            done = g.add("fb_done", r, -1, lambda r=r: self._join_comm(r), "fb_done")
+            for k in range(len(self._fb_ops)):
+                g.edge(comp[r][k], done)
+            row = []
+            for j, op in enumerate(self._opt_ops):
+                if reduce_mode:
+                    rv = op.attrs.get(R.OP_ROLE_VAR_ATTR) or []
+                    owner = self._owners.get(rv[0], 0) if rv else 0
+                    if owner != r:
+                        row.append(None)
+                        continue
+                node = g.add("optimize", r, j, lambda ex=ex, pb=pb, j=j, sc=sc, r=r: self._run_op(r, ex, pb, j, sc),
+                             op.type)
+                g.edge(done, node)
+                for n in op.input_arg_names:
+                    if n in sync_of:
+                        g.edge(sync_of[n], node)
+                for d in odeps[j]:
+                    if row[d] is not None:
+                        g.edge(row[d], node)
+                row.append(node)
+            opt_nodes.append(row)
+        if reduce_mode:
+            bc = g.add("broadcast", -1, 0, self._broadcast_owned, "broadcast_params")
+            for row in opt_nodes:
+                for n in row:
+                    if n is not None:
+                        g.edge(n, bc)
+        return g
+
+    def _device(self, r):
+        return self._places[r].torch_device()
+
+    def _run_op(self, r, ex, pb, k, scope):
+        dev = self._device(r)
+        if dev.type == "cuda":
+            with torch.cuda.device(dev):
+                ex.run_op(pb, k, scope)
+        else:
+            ex.run_op(pb, k, scope)
+
+    def _join_comm(self, r):
+        """Compute stream of replica r waits for the communication stream (issued once
+        its backward is fully enqueued, so the all-reduces overlap that backward)."""
+        dev = self._device(r)
+        if dev.type == "cuda" and self._streams is not None:
+            torch.cuda.current_stream(dev).wait_stream(self._streams.comm(dev))
+
+    def _scale(self):
         bs = self._build_strategy
-        n_total = self.device_count
-        scale = 1.0 / n_total if bs.gradient_scale_strategy == BuildStrategy.GradientScaleStrategy.CoeffNumDevice \
-            else 1.0
-        names = [g for _, g in self._param_grads]
-        per_rep = [self._grads(s, names) for s in self._local_scopes]
-        dense_idx = [i for i, v in enumerate(per_rep[0]) if isinstance(v, core.LoDTensor) and v.tensor is not None]
-        sparse_idx = [i for i, v in enumerate(per_rep[0]) if isinstance(v, core.SelectedRows)]
-        dev0 = self._places[0].torch_device()
-        # 1) in-process reduction onto replica 0
-        summed = []
-        for i in dense_idx:
-            t = per_rep[0][i].tensor.clone() if len(self._places) > 1 else per_rep[0][i].tensor
-            for r in range(1, len(self._places)):
-                t = t + per_rep[r][i].tensor.to(dev0)
-            summed.append(t)
-        # 2) cross-process bucketed all-reduce over RCCL
-        if self._world > 1 and summed:
-            bucket = FLAGS.get("rccl_bucket_mb") * (1 << 20)
-            groups, cur, cur_b = [], [], 0
-            for t in summed:
-                cur.append(t)
-                cur_b += t.numel() * t.element_size()
-                if cur_b >= bucket:
-                    groups.append(cur)
-                    cur, cur_b = [], 0
-            if cur:
-                groups.append(cur)
-            for grp in groups:
-                flat = torch.cat([t.reshape(-1).float() for t in grp])
-                comm.all_reduce(flat)
-                off = 0
-                for t in grp:
-                    n = t.numel()
-                    t.copy_(flat[off:off + n].view_as(t))
-                    off += n
-        # 3) sparse grads: gather rows (reference: SelectedRows to device 0, then broadcast)
-        for i in sparse_idx:
-            rows, vals = [], []
+        return 1.0 / self.device_count if bs.gradient_scale_strategy == \
+            BuildStrategy.GradientScaleStrategy.CoeffNumDevice else 1.0
+
+    def _allreduce_bucket(self, idxs):
+        """AllReduceOpHandle for one bucket: sum over replicas onto replica 0, RCCL
+        all-reduce across processes (one flat fp32 buffer), scale, write back."""
+        dev0 = self._device(0)
+        cuda = dev0.type == "cuda"
+        comm_s = self._streams.comm(dev0) if cuda else None
+        if cuda:
             for r in range(len(self._places)):
-                sr = per_rep[r][i]
-                rows += sr.rows()
-                vals.append(sr.get_tensor().tensor.to(dev0))
-            merged = core.SelectedRows(rows, per_rep[0][i].height(), torch.cat(vals, 0) * scale)
-            for s in self._local_scopes:
-                s.var(names[i]).set(merged)
-        # 4) scale + write back
-        reduce_mode = bs.reduce_strategy == BuildStrategy.ReduceStrategy.Reduce
-        for k, i in enumerate(dense_idx):
-            t = summed[k] * scale if scale != 1.0 else summed[k]
-            lod = per_rep[0][i].lod()
-            p_name = self._param_grads[i][0]
-            for r, (s, pl) in enumerate(zip(self._local_scopes, self._places)):
-                if reduce_mode and r != self._owners.get(p_name, 0):
-                    continue
-                s.var(names[i]).set(core.LoDTensor(t if r == 0 else t.to(pl.torch_device()), lod))
+                comm_s.wait_stream(torch.cuda.current_stream(self._device(r)))
+        ctx = torch.cuda.stream(comm_s) if cuda else _Null()
+        with ctx:
+            live = []  # (param index, grad name, per-replica LoDTensors)
+            for i in idxs:
+                n = self._param_grads[i][1]
+                per = []
+                for sc in self._local_scopes:
+                    v = sc.find_var(n)
+                    per.append(v.get() if v is not None else None)
+                if isinstance(per[0], core.LoDTensor) and per[0].tensor is not None:
+                    live.append((i, n, per))
+            if not live:
+                return
+            flat = torch.cat([torch.stack([p.tensor.reshape(-1).float().to(dev0) for p in per]).sum(0)
+                              for _, _, per in live])
+            if self._world > 1:
+                comm.all_reduce(flat)
+            sc_ = self._scale()
+            if sc_ != 1.0:
+                flat.mul_(sc_)
+            off = 0
+            reduce_mode = self._build_strategy.reduce_strategy == BuildStrategy.ReduceStrategy.Reduce
+            for i, n, per in live:
+                t0 = per[0].tensor
+                cnt = t0.numel()
+                seg = flat[off:off + cnt].view(t0.shape).to(t0.dtype)
+                off += cnt
+                pname = self._param_grads[i][0]
+                for r, sc in enumerate(self._local_scopes):
+                    if reduce_mode and len(self._places) > 1 and r != self._owners.get(pname, 0):
+                        continue
+                    sc.var(n).set(core.LoDTensor(seg if r == 0 else seg.to(self._device(r)), per[0].lod()))
+
+    def _gather_sparse(self, i):
+        """Sparse (SelectedRows) gradients: rows of every replica gathered on replica 0,
+        scaled, shared by all replicas (reference: kSparse gather + broadcast)."""
+        name = self._param_grads[i][1]
+        dev0 = self._device(0)
+        rows, vals = [], []
+        per = [sc.find_var(name).get() for sc in self._local_scopes]
+        for sr in per:
+            rows += sr.rows()
+            vals.append(sr.get_tensor().tensor.to(dev0))
+        merged = core.SelectedRows(rows, per[0].height(), torch.cat(vals, 0) * self._scale())
+        for sc in self._local_scopes:
+            sc.var(name).set(merged)
+
+    def _broadcast_owned(self):
+        for p, _ in self._param_grads:
+            o = self._owners.get(p, 0)
+            src = self._local_scopes[o].find_var(p).get()
+            for r, sc in enumerate(self._local_scopes):
+                if r != o:
+                    sc.var(p).set(core.LoDTensor(src.tensor.to(self._device(r)), src.lod()))
 
     def run(self, fetch_list, feed=None, feed_dict=None, return_numpy=True):
         if feed is None and feed_dict is not None:
@@ -263,31 +404,17 @@ class ParallelExecutor:
         feed = feed or {}
         fetch_names = [v.name if isinstance(v, Variable) else v for v in fetch_list]
         feeds = self._split_feed(feed)
+        R.clear_stash()
         for s, ex, fd in zip(self._local_scopes, self._executors, feeds):
+            BlockExecutor.create_variables(self._fb_prog, s, 0)
             for k, v in fd.items():
                 s.var(k).set(_to_lod_tensor(v, ex.place))
-            ex.run_block(self._fb_prog, 0, s)
-        if self.device_count > 1:
-            self._sync_grads()
-        if self._build_strategy.reduce_strategy == BuildStrategy.ReduceStrategy.Reduce and len(self._places) > 1:
-            owner_ops = {}
-            for op in self._opt_ops:
-                rv = op.attrs.get(R.OP_ROLE_VAR_ATTR) or []
-                owner_ops.setdefault(self._owners.get(rv[0], 0) if rv else 0, []).append(op)
-            for r, (s, ex) in enumerate(zip(self._local_scopes, self._executors)):
-                ops = owner_ops.get(r, [])
-                if ops:
-                    ex.run_block(_sub_program(self._program, ops), 0, s)
-            # broadcast updated params from owners
-            for p, _ in self._param_grads:
-                o = self._owners.get(p, 0)
-                src = self._local_scopes[o].find_var(p).get()
-                for r, (s, pl) in enumerate(zip(self._local_scopes, self._places)):
-                    if r != o:
-                        s.var(p).set(core.LoDTensor(src.tensor.to(pl.torch_device()), src.lod()))
-        else:
-            for s, ex in zip(self._local_scopes, self._executors):
-                ex.run_block(self._opt_prog, 0, s)
+        if self._graph is None:
+            self._streams = D.StreamSet() if self._device(0).type == "cuda" else None
+            self._graph = self._build_graph()
+        self.trace = D.Trace() if self._trace_on else None
+        nthreads = max(1, self._exec_strategy.num_threads or (len(self._places) + 1))
+        D.run_graph(self._graph, nthreads, self.trace)
         self._step += 1
         if self._step % max(1, self._exec_strategy.num_iteration_per_drop_scope) == 0:
             for s in self._local_scopes:
@@ -310,3 +437,11 @@ class ParallelExecutor:
     def drop_local_exe_scopes(self):
         for s in self._local_scopes:
             s.drop_kids()
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

@@ -108,12 +108,19 @@ class BlockExecutor:
         self.run_prepared(pb, scope)
 
     def run_prepared(self, pb, scope):
+        stash_off = getattr(_TLS, "off", False)
+        for k in range(len(pb.steps)):
+            self.run_op(pb, k, scope, stash_off)
+
+    def run_op(self, pb, k, scope, stash_off=False):
+        """Run step ``k`` of a prepared block (the unit the SSA-graph executor
+        schedules: one ComputationOpHandle, details/computation_op_handle.cc)."""
         check_nan = FLAGS.get("check_nan_inf")
         bench = FLAGS.get("benchmark")
         profiling = prof.is_enabled()
         place = self.place
-        stash = pb.stash if not getattr(_TLS, "off", False) else [False] * len(pb.steps)
-        for k, (info, op, ins, outs, attrs) in enumerate(pb.steps):
+        if True:
+            info, op, ins, outs, attrs = pb.steps[k]
             ctx_ins = {}
             for slot, names in ins:
                 vals = []
@@ -122,7 +129,7 @@ class BlockExecutor:
                     vals.append(var.get() if var is not None else None)
                 ctx_ins[slot] = vals
             ctx = R.KernelContext(op.type, ctx_ins, outs, attrs, place, scope, op, self)
-            run = R.run_kernel_stash if stash[k] else R.run_kernel
+            run = R.run_kernel_stash if (pb.stash[k] and not stash_off) else R.run_kernel
             if profiling:
                 with prof.RecordEvent(op.type):
                     run(info, ctx)

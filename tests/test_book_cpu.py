@@ -141,6 +141,81 @@ def test_parallel_executor_allreduce_vs_reduce_vs_single(monkeypatch):
         assert abs(a - b) < 1e-4
 
 
+def test_parallel_executor_ssa_graph_overlaps_allreduce(monkeypatch):
+    """The step runs as one SSA graph on the native DAG pool: per-replica compute
+    nodes, one all-reduce node per gradient bucket, optimizer nodes.  With
+    one-gradient buckets the first bucket's all-reduce starts while the backward
+    of earlier layers is still running (the trace of the step shows it)."""
+    from paddle_amd.utils import flags as FLAGS
+
+    monkeypatch.setenv("CPU_NUM", "2")
+    old = FLAGS.get("rccl_bucket_mb")
+    FLAGS.set("rccl_bucket_mb", 0)  # every gradient is its own bucket
+    try:
+        main, startup = fluid.Program(), fluid.Program()
+        main.random_seed = startup.random_seed = 3
+        with fluid.program_guard(main, startup):
+            x = fluid.layers.data("x", [64])
+            h = x
+            for _ in range(6):
+                h = fluid.layers.fc(h, 64, act="relu")
+            loss = fluid.layers.mean(fluid.layers.fc(h, 1))
+            fluid.optimizer.SGD(0.01).minimize(loss)
+        scope = core.Scope()
+        with fluid.executor.scope_guard(scope):
+            fluid.Executor(fluid.CPUPlace()).run(startup)
+            pe = fluid.ParallelExecutor(use_cuda=False, loss_name=loss.name, main_program=main, scope=scope,
+                                        trace=True)
+            pe.run([loss.name], feed={"x": np.random.rand(16, 64).astype("float32")})
+        ev = pe.trace.events
+        kinds = {e[0] for e in ev}
+        assert {"compute", "allreduce", "optimize"} <= kinds
+        n_ar = sum(1 for e in ev if e[0] == "allreduce")
+        assert n_ar == 14  # 7 fc layers x (w, b)
+        first_ar_start = min(e[3] for e in ev if e[0] == "allreduce")
+        last_compute_end = max(e[4] for e in ev if e[0] == "compute")
+        assert first_ar_start < last_compute_end, "all-reduce did not overlap the backward"
+        # both replicas ran every forward/backward op
+        assert {e[2] for e in ev if e[0] == "compute"} == {0, 1}
+    finally:
+        FLAGS.set("rccl_bucket_mb", old)
+
+
+def _pe_mp_worker(rank, world):
+    import os
+
+    os.environ["CPU_NUM"] = "1"
+    main, startup = fluid.Program(), fluid.Program()
+    main.random_seed = startup.random_seed = 7
+    with fluid.program_guard(main, startup):
+        img = fluid.layers.data(name="img", shape=[1, 28, 28], dtype="float32")
+        label = fluid.layers.data(name="label", shape=[1], dtype="int64")
+        _, loss, _ = mlp(img, label)
+        fluid.optimizer.SGD(learning_rate=0.1).minimize(loss)
+    scope = core.Scope()
+    X, Y = _digits_data(256, 3)
+    out = []
+    with fluid.executor.scope_guard(scope):
+        fluid.Executor(fluid.CPUPlace()).run(startup)
+        pe = fluid.ParallelExecutor(use_cuda=False, loss_name=loss.name, main_program=main, scope=scope)
+        for i in range(4):
+            lo = i * 32 + rank * 16
+            (l,) = pe.run([loss.name], feed={"img": X[lo:lo + 16], "label": Y[lo:lo + 16]})
+            out.append(float(np.mean(l)))
+    return out
+
+
+def test_parallel_executor_two_processes_matches_single():
+    """One replica per process (gloo here, RCCL on the GPU): bucket all-reduce
+    nodes across processes give the single-process full-batch trajectory."""
+    from dist_util import run_dist
+
+    single = _pe_run(None)
+    res = run_dist(_pe_mp_worker, 2)
+    for step in range(4):
+        assert abs((res[0][step] + res[1][step]) / 2 - single[step]) < 1e-4, (res, single)
+
+
 def test_memory_optimize_keeps_results():
     main, startup = fluid.Program(), fluid.Program()
     with fluid.program_guard(main, startup):
