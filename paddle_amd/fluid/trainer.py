@@ -144,6 +144,7 @@ class Trainer:
                 loss = self.train_func_outputs[0]
                 optimizer = optimizer_func()
                 optimizer.minimize(loss)
+                self._dist_transpile_if_necessary()
         self.place = place or core.CPUPlace()
         with scope_guard(self.scope):
             exe = Executor(self.place)
@@ -157,10 +158,68 @@ class Trainer:
             if param_path and os.path.isdir(param_path):
                 io.load_persistables(exe, dirname=param_path, main_program=self.startup_program)
 
+    # ------------------------------------------------------------------ cluster roles
+    def _dist_transpile_if_necessary(self):
+        """Environment-driven distribution (reference trainer.py:295-360).
+
+        * ``PADDLE_TRAINER_IPS`` (+ ``PADDLE_PSERVER_PORT``, ``PADDLE_TRAINER_ID``,
+          ``PADDLE_CURRENT_IP``): collective data parallelism -- the reference's NCCL2
+          mode -- one process per trainer over ``torch.distributed`` (RCCL on the GPU),
+          gradients synchronised by the ParallelExecutor's bucket all-reduce.
+        * ``PADDLE_TRAINING_ROLE`` = TRAINER / PSERVER (+ ``PADDLE_PSERVER_IPS``,
+          ``PADDLE_PSERVER_PORT``, ``PADDLE_TRAINERS``, ``PADDLE_CURRENT_IP``):
+          DistributeTranspiler parameter-server training; a PSERVER's ``train``
+          serves until every trainer has finished."""
+        self.training_role = None
+        self.nccl_mode = False
+        ips = os.environ.get("PADDLE_TRAINER_IPS")
+        if ips:
+            from ..parallel import comm
+
+            port = os.environ.get("PADDLE_PSERVER_PORT", "6174")
+            ips = [ip for ip in ips.split(",") if ip]
+            self.trainer_id = int(os.environ.get("PADDLE_TRAINER_ID", "0"))
+            self.num_trainers = len(ips)
+            os.environ.setdefault("MASTER_ADDR", ips[0])
+            os.environ.setdefault("MASTER_PORT", port)
+            os.environ.setdefault("RANK", str(self.trainer_id))
+            os.environ.setdefault("WORLD_SIZE", str(self.num_trainers))
+            if self.num_trainers > 1:
+                comm.init_parallel_env()
+            self.nccl_mode = True
+            self.parallel = True
+            return
+        role = os.environ.get("PADDLE_TRAINING_ROLE")
+        if not role:
+            return
+        from .transpiler.distribute_transpiler import DistributeTranspiler
+
+        port = os.environ.get("PADDLE_PSERVER_PORT", "6174")
+        eps = [f"{ip}:{port}" for ip in os.environ.get("PADDLE_PSERVER_IPS", "").split(",") if ip]
+        trainers = int(os.environ.get("PADDLE_TRAINERS", "1"))
+        current = os.environ.get("PADDLE_CURRENT_IP", "") + ":" + port
+        self.trainer_id = int(os.environ.get("PADDLE_TRAINER_ID", "0"))
+        t = DistributeTranspiler()
+        t.transpile(self.trainer_id, program=self.train_program, pservers=",".join(eps), trainers=trainers,
+                    startup_program=self.startup_program)
+        if role == "PSERVER":
+            if self.checkpoint_cfg is not None:
+                self.checkpoint_cfg.pserver_id = eps.index(current)
+            self.train_program, self.startup_program = t.get_pserver_programs(current)
+        elif role == "TRAINER":
+            self.train_program = t.get_trainer_program()
+        else:
+            raise ValueError("PADDLE_TRAINING_ROLE must be TRAINER or PSERVER")
+        self.training_role = role
+
     def stop(self):
         self.__stop = True
 
     def train(self, num_epochs, event_handler, reader=None, feed_order=None):
+        if self.training_role == "PSERVER":
+            with scope_guard(self.scope):
+                Executor(self.place).run(self.train_program)  # listen_and_serv until trainers finish
+            return
         with scope_guard(self.scope):
             feed_vars = [self.train_program.global_block().var(n) for n in (feed_order or [])]
             feeder = DataFeeder(feed_list=feed_vars, place=self.place, program=self.train_program)
@@ -189,6 +248,8 @@ class Trainer:
                 event_handler(EndEpochEvent(epoch_id))
             if self.checkpoint_cfg:
                 clean_checkpoint(self.checkpoint_cfg.checkpoint_dir)
+            if self.training_role == "TRAINER" and hasattr(exe, "close"):
+                exe.close()  # tells the pservers this trainer is done
 
     def test(self, reader, feed_order):
         with scope_guard(self.scope):

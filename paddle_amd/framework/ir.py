@@ -610,3 +610,183 @@ def apply_passes(program, names, block_idx=0, **attrs):
     for nme in list(names) + ["graph_to_program_pass"]:
         g = get_pass(nme).apply(g)
     return g
+
+
+# ------------------------------------------------------------------ sequence / attention fusions
+_SEQ_FC_ACTS = ("sigmoid", "tanh", "relu", "identity")
+
+
+@register_pass("seq_concat_fc_fuse_pass")
+class SeqConcatFcFusePass(Pass):
+    """concat(X0, sequence_expand(A), sequence_expand(B)) -> mul(W) -> elementwise_add(b)
+    -> act  ==>  fusion_seqexpand_concat_fc(X=[X0, A, B], W, b, fc_activation=act)
+    (seq_concat_fc_fuse_pass.cc): the expanded copies of A and B, the concat and the
+    fc temporaries are never materialised."""
+
+    def apply_impl(self, graph):
+        fused = 0
+        for cat in list(graph.op_nodes()):
+            if cat not in graph.nodes or not cat.is_op("concat") or len(cat.op.input("X")) != 3:
+                continue
+            xs = cat.op.input("X")
+            by_name = {v.name: v for v in cat.inputs}
+            exp_ops = []
+            for nm in xs[1:]:
+                v = by_name.get(nm)
+                prod = [p for p in (v.inputs if v is not None else []) if p.is_op("sequence_expand")]
+                if not prod or len(v.outputs) != 1:
+                    break
+                exp_ops.append((prod[0], v))
+            if len(exp_ops) != 2:
+                continue
+            cat_out = [v for v in cat.outputs if v.name in cat.op.output("Out")]
+            if len(cat_out) != 1 or len(cat_out[0].outputs) != 1 or not cat_out[0].outputs[0].is_op("mul"):
+                continue
+            mul = cat_out[0].outputs[0]
+            w = [v for v in mul.inputs if v.name in mul.op.input("Y")]
+            if not w or w[0].var is None or not w[0].var.persistable:
+                continue
+            mul_out = [v for v in mul.outputs if v.name in mul.op.output("Out")][0]
+            if len(mul_out.outputs) != 1 or not mul_out.outputs[0].is_op("elementwise_add"):
+                continue
+            add = mul_out.outputs[0]
+            b = [v for v in add.inputs if v.name in add.op.input("Y")]
+            if not b or b[0].var is None or not b[0].var.persistable:
+                continue
+            add_out = [v for v in add.outputs if v.name in add.op.output("Out")][0]
+            if len(add_out.outputs) != 1 or add_out.outputs[0].op.type not in _SEQ_FC_ACTS:
+                continue
+            act = add_out.outputs[0]
+            fc_out = [v for v in act.outputs if v.name in act.op.output("Out")][0]
+            ins = {"X": [xs[0]] + [e.op.input("X")[0] for e, _ in exp_ops], "FCWeight": [w[0].name],
+                   "FCBias": [b[0].name]}
+            newop = _new_op(graph.block, "fusion_seqexpand_concat_fc", ins, {"Out": [fc_out.name]},
+                            {"fc_activation": act.op.type})
+            n = _replace_ops(graph, [e for e, _ in exp_ops] + [cat, mul, add, act], newop,
+                             dead_vars=[v for _, v in exp_ops] + [cat_out[0], mul_out, add_out])
+            # the expanded inputs A and B now feed the fused op directly
+            for e, _ in exp_ops:
+                for v in e.inputs:
+                    if v.name == e.op.input("X")[0] and v not in n.inputs:
+                        _link(v, n)
+            fused += 1
+        graph.set("seq_concat_fc_fuse_count", fused)
+        return graph
+
+
+@register_pass("attention_lstm_fuse_pass")
+class AttentionLSTMFusePass(Pass):
+    """Replace the while-loop attention-LSTM decoder of the reference's attention
+    model with one ``attention_lstm`` op (attention_lstm_fuse_pass.cc).  The loop is
+    recognised by the gate parameters its sub-block reads ({forget,input,output,c}
+    .{w_0,w_1,b_0}); the pass concatenates them into the fused op's LSTMWeight
+    [D + M, 4D] / LSTMBias [1, 4D] (gate order f, i, o, c) in the parameter scope
+    (graph attr ``param_scope``), reshapes the attention biases to [1, n], removes
+    the loop and the ops only it used, and wires X / C0 / H0 -> Hidden.  Variable
+    names default to the reference's and can be overridden by pass attrs."""
+
+    required_graph_attrs = ("param_scope",)
+    DEFAULTS = dict(X="concat_0.tmp_0", C0="cell_init", H0="hidden_init", AttentionWeight="attention_fc.w_0",
+                    AttentionBias="attention_fc.b_0", AttentionScalar="attention_output.w_0",
+                    AttentionScalarBias="attention_output.b_0", LSTMWeight="attention_w.new",
+                    LSTMBias="attention_b.new", Hidden="array_to_lod_tensor_0.tmp_0", Cell="at.cell.new",
+                    AttentionedX="at.x.new", AttentionFCOut="at.fc.new", LSTMX="at.lstmx.new",
+                    LSTMOUT="at.lstmout.new")
+    GATES = ("forget", "input", "output", "c")
+
+    def _reads(self, block):
+        names = set()
+        for op in block.ops:
+            names.update(op.input_arg_names)
+            sb = op.attrs.get("sub_block")
+            if sb is not None:
+                names |= self._reads(sb if hasattr(sb, "ops") else block.program.block(sb))
+        return names
+
+    def apply_impl(self, graph):
+        P = dict(self.DEFAULTS, **{k: v for k, v in self.attrs.items() if k in self.DEFAULTS})
+        gate_params = [f"{g}.{s}" for g in self.GATES for s in ("w_0", "w_1", "b_0")]
+        loops = []
+        for n in graph.op_nodes():
+            if n.is_op("while"):
+                sb = n.op.attrs.get("sub_block")
+                blk = sb if hasattr(sb, "ops") else graph.program.block(sb)
+                if set(gate_params) <= self._reads(blk):
+                    loops.append(n)
+        if not loops:
+            graph.set("attention_lstm_fused", 0)
+            return graph
+        self._prepare_parameters(graph.get("param_scope"), P)
+        dead = set(loops)
+        hid = [n for n in graph.op_nodes() if P["Hidden"] in n.op.output_arg_names]
+        dead.update(hid)
+        keep_names = {P["X"], P["C0"], P["H0"]}
+        # ops whose results only the removed loop consumed
+        changed = True
+        while changed:
+            changed = False
+            for n in graph.op_nodes():
+                if n in dead or n.op.type in ("feed", "fetch"):
+                    continue
+                outs = n.outputs
+                if not outs or any(v.name in keep_names for v in outs):
+                    continue
+                if any(v.var is not None and v.var.persistable for v in outs):
+                    continue
+                if all(all(c in dead for c in v.outputs) for v in outs) and \
+                        any(c in dead for v in outs for c in v.outputs):
+                    dead.add(n)
+                    changed = True
+        ins = {k: [P[k]] for k in ("X", "C0", "H0", "AttentionWeight", "AttentionBias", "AttentionScalar",
+                                   "AttentionScalarBias", "LSTMWeight", "LSTMBias")}
+        outs = {k: [P[k]] for k in ("Hidden", "Cell", "AttentionedX", "AttentionFCOut", "LSTMX", "LSTMOUT")}
+        blk = graph.block
+        for nm in ("LSTMWeight", "LSTMBias"):
+            if blk._find_var_recursive(P[nm]) is None:
+                blk.create_var(name=P[nm], persistable=True)
+        for nm in ("Cell", "AttentionedX", "AttentionFCOut", "LSTMX", "LSTMOUT"):
+            if blk._find_var_recursive(P[nm]) is None:
+                blk.create_var(name=P[nm])
+        newop = _new_op(blk, "attention_lstm", ins, outs, {})
+        node = graph.create_op_node(newop)
+        node.order = min(n.order for n in loops)
+        latest = {}
+        for v in graph.var_nodes():
+            latest[v.name] = v
+        for nm in newop.input_arg_names:
+            v = latest.get(nm) or graph.create_var_node(nm)
+            _link(v, node)
+        hidden_vars = [v for n in hid for v in n.outputs if v.name == P["Hidden"]]
+        for nm in newop.output_arg_names:
+            v = next((hv for hv in hidden_vars if hv.name == nm), None)
+            if v is None:
+                v = graph.create_var_node(nm)
+            v.inputs = []
+            _link(node, v)
+        graph.remove_nodes([n for n in dead])
+        graph.remove_nodes([v for v in graph.var_nodes() if not v.inputs and not v.outputs])
+        graph.set("attention_lstm_fused", len(loops))
+        return graph
+
+    def _prepare_parameters(self, scope, P):
+        import torch
+
+        from . import core
+
+        def get(name):
+            v = scope.find_var(name)
+            if v is None or v.get() is None:
+                raise KeyError(f"attention_lstm_fuse_pass: parameter {name} not in scope")
+            return v.get().tensor
+
+        w0 = [get(f"{g}.w_0") for g in self.GATES]   # [D, D] hidden part
+        w1 = [get(f"{g}.w_1") for g in self.GATES]   # [M, D] input part
+        bs = [get(f"{g}.b_0").reshape(-1) for g in self.GATES]
+        W = torch.cat([torch.cat(w0, 1), torch.cat(w1, 1)], 0)
+        b = torch.cat(bs).reshape(1, -1)
+        scope.var(P["LSTMWeight"]).set(core.LoDTensor(W.contiguous()))
+        scope.var(P["LSTMBias"]).set(core.LoDTensor(b.contiguous()))
+        for nm in ("AttentionBias", "AttentionScalarBias"):
+            v = scope.find_var(P[nm])
+            if v is not None and v.get() is not None and v.get().tensor.dim() == 1:
+                v.set(core.LoDTensor(v.get().tensor.reshape(1, -1)))

@@ -231,3 +231,42 @@ def test_memory_optimize_keeps_results():
         (a,) = exe.run(main, feed={"x": xv}, fetch_list=[loss])
     fluid.memory_optimize(main)
     assert "delete_var" in [op.type for op in main.global_block().ops]
+
+
+def test_memory_optimize_with_while_sub_block():
+    """Control-flow aware liveness: parent-scope vars the loop body reads stay alive
+    through the loop; body-local temporaries are released inside the body; the
+    result is unchanged."""
+    main, startup = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, startup):
+        x = fluid.layers.data("x", shape=[4], dtype="float32")
+        scale = fluid.layers.scale(x, scale=2.0)          # read only inside the loop
+        acc = fluid.layers.fill_constant([2, 4], "float32", 0.0)
+        i = fluid.layers.fill_constant([1], "int64", 0)
+        n = fluid.layers.fill_constant([1], "int64", 3)
+        cond = fluid.layers.less_than(i, n)
+        loop = fluid.layers.While(cond)
+        with loop.block():
+            t = fluid.layers.elementwise_mul(scale, scale)   # body-local temporary
+            t2 = fluid.layers.scale(t, scale=0.5)
+            fluid.layers.assign(fluid.layers.elementwise_add(acc, t2), acc)
+            fluid.layers.increment(i, in_place=True)
+            fluid.layers.less_than(i, n, cond=cond)
+        out = fluid.layers.reduce_sum(acc)
+    exe = fluid.Executor(fluid.CPUPlace())
+    xv = np.arange(8, dtype="float32").reshape(2, 4)
+    scope = core.Scope()
+    with fluid.executor.scope_guard(scope):
+        exe.run(startup)
+        (ref,) = exe.run(main, feed={"x": xv}, fetch_list=[out])
+        n_freed = fluid.memory_optimize(main, skip_opt_set=[out.name])  # fetch targets are kept by the caller
+        assert n_freed and n_freed > 0
+        gb = main.global_block()
+        wi = [k for k, op in enumerate(gb.ops) if op.type == "while"][0]
+        freed_before_loop = {nm for op in gb.ops[:wi] if op.type == "delete_var" for nm in op.input("X")}
+        assert scale.name not in freed_before_loop  # still needed by the loop body
+        body = main.block(1)
+        assert any(op.type == "delete_var" for op in body.ops)
+        (res,) = exe.run(main, feed={"x": xv}, fetch_list=[out])
+    np.testing.assert_allclose(res, ref)
+    np.testing.assert_allclose(res, [3 * 0.5 * float(((2 * xv) ** 2).sum())], rtol=1e-5)

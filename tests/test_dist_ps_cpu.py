@@ -174,3 +174,65 @@ def test_pserver_async_trains():
     for k in range(2):
         losses = res[("trainer", k)]
         assert all(np.isfinite(losses))
+
+
+# ------------------------------------------------------------------ Trainer env roles
+def _trainer_role_worker(env, q):
+    try:
+        os.environ.update(env)
+        import paddle_amd.fluid as fluid
+
+        def train_func():
+            x = fluid.layers.data("x", shape=[16], dtype="float32")
+            y = fluid.layers.data("y", shape=[1], dtype="float32")
+            pred = fluid.layers.fc(fluid.layers.fc(x, 32, act="tanh"), 1)
+            return fluid.layers.mean(fluid.layers.square_error_cost(pred, y))
+
+        tr = fluid.Trainer(train_func, lambda: fluid.optimizer.SGD(0.1), place=fluid.CPUPlace())
+        losses = []
+        X, Y, _ = _data()
+        idx, n_tr = int(env.get("PADDLE_TRAINER_ID", "0")), int(env.get("PADDLE_TRAINERS", "1"))
+        per = 16 // n_tr
+
+        def reader():  # the same batch every step: the loss must fall
+            for _ in range(STEPS):
+                yield list(zip(X[0, idx * per:(idx + 1) * per], Y[0, idx * per:(idx + 1) * per]))
+
+        def handler(ev):
+            if isinstance(ev, fluid.EndStepEvent):
+                losses.append(float(np.asarray(ev.metrics[0]).reshape(-1)[0]))
+
+        tr.train(1, handler, reader=reader, feed_order=["x", "y"])
+        q.put((env["PADDLE_TRAINING_ROLE"], idx, losses if env["PADDLE_TRAINING_ROLE"] == "TRAINER" else "ok"))
+    except Exception:
+        q.put((env.get("PADDLE_TRAINING_ROLE"), env.get("PADDLE_TRAINER_ID"), "ERR " + traceback.format_exc()))
+
+
+def test_trainer_transpiles_from_environment():
+    """fluid.Trainer reads PADDLE_TRAINING_ROLE / PADDLE_PSERVER_IPS / ... and becomes a
+    parameter server or a transpiled trainer (reference trainer.py:295-360)."""
+    port = str(_free_port())
+    base = {"PADDLE_PSERVER_IPS": "127.0.0.1", "PADDLE_PSERVER_PORT": port, "PADDLE_TRAINERS": "2",
+            "PADDLE_CURRENT_IP": "127.0.0.1"}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    envs = [dict(base, PADDLE_TRAINING_ROLE="PSERVER", PADDLE_TRAINER_ID="0")]
+    envs += [dict(base, PADDLE_TRAINING_ROLE="TRAINER", PADDLE_TRAINER_ID=str(i)) for i in range(2)]
+    procs = [ctx.Process(target=_trainer_role_worker, args=(e, q)) for e in envs]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in procs:
+            role, idx, r = q.get(timeout=240)
+            assert not (isinstance(r, str) and r.startswith("ERR")), f"{role}{idx}: {r}"
+            res[(role, idx)] = r
+    finally:
+        for p in procs:
+            p.join(timeout=10)
+            if p.is_alive():
+                p.kill()
+    a, b = res[("TRAINER", 0)], res[("TRAINER", 1)]
+    assert len(a) == STEPS and len(b) == STEPS
+    mean = [(u + v) / 2 for u, v in zip(a, b)]
+    assert mean[-1] < mean[0]

@@ -159,3 +159,96 @@ def test_reduced_precision_transpiler(tmp_path, which):
         (out,) = exe.run(prog, feed={feeds[0]: x}, fetch_list=fetches)
     assert out.dtype == np.float32
     np.testing.assert_allclose(out, ref, rtol=5e-2, atol=2e-2)
+
+
+def test_seq_concat_fc_fuse_pass_preserves_numerics():
+    """concat(x, seq_expand(a), seq_expand(b)) -> fc(act) becomes one
+    fusion_seqexpand_concat_fc op (seq_concat_fc_fuse_pass.cc) with equal output."""
+    main, startup = fluid.Program(), fluid.Program()
+    main.random_seed = startup.random_seed = 3
+    with fluid.program_guard(main, startup):
+        x = fluid.layers.data("x", shape=[6], dtype="float32", lod_level=1)
+        a = fluid.layers.data("a", shape=[4], dtype="float32")
+        b = fluid.layers.data("b", shape=[3], dtype="float32")
+        ea = fluid.layers.sequence_expand(a, x)
+        eb = fluid.layers.sequence_expand(b, x)
+        cat = fluid.layers.concat([x, ea, eb], axis=1)
+        y = fluid.layers.fc(cat, 5, act="tanh")
+    rs = np.random.RandomState(0)
+    xt = fluid.create_lod_tensor(rs.rand(7, 6).astype("float32"), [[3, 4]], fluid.CPUPlace())
+    feed = {"x": xt, "a": rs.rand(2, 4).astype("float32"), "b": rs.rand(2, 3).astype("float32")}
+    exe = fluid.Executor(fluid.CPUPlace())
+    scope = core.Scope()
+    with fluid.executor.scope_guard(scope):
+        exe.run(startup)
+        (ref,) = exe.run(main, feed=feed, fetch_list=[y], return_numpy=False)
+        g = ir.apply_passes(main, ["seq_concat_fc_fuse_pass"])
+        types = [op.type for op in main.global_block().ops]
+        assert g.get("seq_concat_fc_fuse_count") == 1, types
+        assert "fusion_seqexpand_concat_fc" in types and "sequence_expand" not in types and "concat" not in types
+        (out,) = exe.run(main, feed=feed, fetch_list=[y], return_numpy=False)
+    np.testing.assert_allclose(np.array(out), np.array(ref), rtol=1e-5, atol=1e-6)
+
+
+def _attention_loop_program(D=4, M=6):
+    """A while-loop decoder reading the reference attention model's gate parameters."""
+    main, startup = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, startup):
+        x = fluid.layers.data("concat_0.tmp_0", shape=[M], dtype="float32", lod_level=1)
+        c0 = fluid.layers.data("cell_init", shape=[D], dtype="float32")
+        h0 = fluid.layers.data("hidden_init", shape=[D], dtype="float32")
+        params = {}
+        for gname in ("forget", "input", "output", "c"):
+            params[gname] = (fluid.layers.create_parameter([D, D], "float32", name=f"{gname}.w_0"),
+                             fluid.layers.create_parameter([M, D], "float32", name=f"{gname}.w_1"),
+                             fluid.layers.create_parameter([D], "float32", name=f"{gname}.b_0", is_bias=True))
+        for nm, shp in (("attention_fc.w_0", [M + D, 1]), ("attention_fc.b_0", [1]),
+                        ("attention_output.w_0", [1, 1]), ("attention_output.b_0", [1])):
+            fluid.layers.create_parameter(shp, "float32", name=nm)
+        i = fluid.layers.fill_constant([1], "int64", 0)
+        n = fluid.layers.fill_constant([1], "int64", 2)
+        arr = fluid.layers.create_array("float32")
+        cond = fluid.layers.less_than(i, n)
+        loop = fluid.layers.While(cond)
+        with loop.block():
+            acc = fluid.layers.matmul(h0, params["forget"][0])
+            for gname in ("input", "output", "c"):
+                acc = fluid.layers.elementwise_add(acc, fluid.layers.matmul(h0, params[gname][0]))
+            for gname in ("forget", "input", "output", "c"):
+                acc = fluid.layers.elementwise_add(acc, params[gname][2])
+                acc = fluid.layers.elementwise_add(acc, fluid.layers.reduce_sum(params[gname][1]))
+            fluid.layers.array_write(acc, i, arr)
+            fluid.layers.increment(i, in_place=True)
+            fluid.layers.less_than(i, n, cond=cond)
+        hidden = fluid.layers.array_read(arr, fluid.layers.fill_constant([1], "int64", 0))
+        out = main.global_block().create_var(name="array_to_lod_tensor_0.tmp_0", dtype="float32")
+        fluid.layers.assign(hidden, out)
+    return main, startup
+
+
+def test_attention_lstm_fuse_pass_replaces_loop():
+    D, M = 4, 6
+    main, startup = _attention_loop_program(D, M)
+    exe = fluid.Executor(fluid.CPUPlace())
+    scope = core.Scope()
+    with fluid.executor.scope_guard(scope):
+        exe.run(startup)
+        g = ir.apply_passes(main, ["attention_lstm_fuse_pass"], param_scope=scope)
+        types = [op.type for op in main.global_block().ops]
+        assert g.get("attention_lstm_fused") == 1, types
+        assert "while" not in types and "attention_lstm" in types
+        W = np.array(scope.find_var("attention_w.new").get().tensor)
+        b = np.array(scope.find_var("attention_b.new").get().tensor)
+        assert W.shape == (D + M, 4 * D) and b.shape == (1, 4 * D)
+        gates = ("forget", "input", "output", "c")
+        for k, gname in enumerate(gates):
+            np.testing.assert_array_equal(W[:D, k * D:(k + 1) * D], np.array(scope.find_var(f"{gname}.w_0").get().tensor))
+            np.testing.assert_array_equal(W[D:, k * D:(k + 1) * D], np.array(scope.find_var(f"{gname}.w_1").get().tensor))
+            np.testing.assert_array_equal(b[0, k * D:(k + 1) * D], np.array(scope.find_var(f"{gname}.b_0").get().tensor))
+        assert tuple(scope.find_var("attention_fc.b_0").get().tensor.shape) == (1, 1)
+        rs = np.random.RandomState(1)
+        feed = {"concat_0.tmp_0": fluid.create_lod_tensor(rs.rand(5, M).astype("float32"), [[2, 3]],
+                                                          fluid.CPUPlace()),
+                "cell_init": rs.rand(2, D).astype("float32"), "hidden_init": rs.rand(2, D).astype("float32")}
+        (h,) = exe.run(main, feed=feed, fetch_list=["array_to_lod_tensor_0.tmp_0"], return_numpy=False)
+        assert np.array(h).shape == (5, D)
