@@ -20,7 +20,7 @@ from collections import defaultdict
 
 import torch
 
-_state = {"enabled": False, "gpu": False, "events": [], "t0": 0.0}
+_state = {"enabled": False, "gpu": False, "events": [], "t0": 0.0, "base": None}
 _lock = threading.Lock()
 _tls = threading.local()
 
@@ -68,6 +68,14 @@ def start(state="All"):
     _state["gpu"] = state in ("GPU", "All") and torch.cuda.is_available()
     _state["events"] = []
     _state["t0"] = time.perf_counter()
+    if _state["gpu"]:
+        # device time origin: every range's HIP events are placed relative to it, so
+        # the GPU track of the timeline is an in-process device activity trace
+        # (the reference's CUPTI DeviceTracer, platform/device_tracer.cc:98-121)
+        _state["base"] = torch.cuda.Event(enable_timing=True)
+        _state["base"].record()
+        torch.cuda.synchronize()
+        _state["base_host"] = time.perf_counter()
 
 
 def reset():
@@ -83,6 +91,35 @@ def _gather():
         dev_ms = e0.elapsed_time(e1) if (e0 is not None and e1 is not None) else None
         rows.append((name, tid, t0, t1, dev_ms))
     return rows
+
+
+def device_events():
+    """(name, device_start_ms, device_end_ms) of every GPU range, on the device clock
+    measured from the profiler start event."""
+    if not _state["gpu"] or _state["base"] is None:
+        return []
+    torch.cuda.synchronize()
+    base = _state["base"]
+    out = []
+    for name, tid, t0, t1, e0, e1 in _state["events"]:
+        if e0 is not None and e1 is not None:
+            out.append((name, base.elapsed_time(e0), base.elapsed_time(e1)))
+    return out
+
+
+def profile_dict():
+    """The profile as a plain dict (the reference's profiler.proto Profile):
+    ``events``: {name, type CPU|GPUKernel, device_id, sub_device_id (thread /
+    stream), start_ns, end_ns}."""
+    t0 = _state["t0"]
+    ev = [{"name": n, "type": "CPU", "device_id": 0, "sub_device_id": tid % 1000000,
+           "start_ns": int((a - t0) * 1e9), "end_ns": int((b - t0) * 1e9)} for n, tid, a, b, _ in _gather()]
+    if _state["gpu"]:
+        off = (_state["base_host"] - t0) * 1e3
+        dev = torch.cuda.current_device()
+        ev += [{"name": n, "type": "GPUKernel", "device_id": dev, "sub_device_id": 0,
+                "start_ns": int((off + a) * 1e6), "end_ns": int((off + b) * 1e6)} for n, a, b in device_events()]
+    return {"start_ns": 0, "end_ns": max([e["end_ns"] for e in ev], default=0), "events": ev}
 
 
 def summary(sorted_key=None):
@@ -111,17 +148,34 @@ def stop(sorted_key=None, profile_path="/tmp/profile"):
         return None
     text, items = summary(sorted_key)
     print(text)
-    rows = _gather()
-    t0 = _state["t0"]
-    trace = {"traceEvents": [
-        {"name": n, "ph": "X", "pid": os.getpid(), "tid": tid, "ts": (a - t0) * 1e6, "dur": (b - a) * 1e6,
-         "args": ({"device_ms": d} if d is not None else {})}
-        for n, tid, a, b, d in rows]}
     if profile_path:
+        # the profile itself (tools/timeline.py turns one or more into a Chrome
+        # trace), plus the single-process Chrome trace next to it
         try:
-            with open(profile_path + ".json" if not profile_path.endswith(".json") else profile_path, "w") as f:
-                json.dump(trace, f)
+            prof = profile_dict()
+            with open(profile_path, "w") as f:
+                json.dump(prof, f)
+            with open(profile_path + ".trace.json", "w") as f:
+                f.write(chrome_trace({"trainer": prof}))
         except OSError:
             pass
     _state["enabled"] = False
     return items
+
+
+def chrome_trace(profiles):
+    """Chrome trace JSON of {label: profile_dict} (tools/timeline.py Timeline):
+    one pid per (label, device, CPU | GPUKernel) track, tid = sub_device_id."""
+    pids, out = {}, []
+    for k, prof in profiles.items():
+        for e in prof["events"]:
+            key = (k, e["device_id"], e["type"])
+            if key not in pids:
+                pids[key] = len(pids)
+                kind = "cpu:block" if e["type"] == "CPU" else "gpu"
+                out.append({"name": "process_name", "ph": "M", "pid": pids[key],
+                            "args": {"name": f"{k}:{kind}:{e['device_id']}"}})
+            out.append({"name": e["name"], "cat": "Op", "ph": "X", "pid": pids[key], "tid": e["sub_device_id"],
+                        "ts": e["start_ns"] / 1e3, "dur": (e["end_ns"] - e["start_ns"]) / 1e3,
+                        "args": {"name": e["name"]}})
+    return json.dumps({"traceEvents": out, "displayTimeUnit": "ns"})
