@@ -82,6 +82,8 @@ def main():
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = gloo debug mode for tests (tiny models only)")
     ap.add_argument("--master-port", type=int, default=0)
+    ap.add_argument("--autograd", default="tape", choices=["tape", "torch"],
+                    help="tape: the framework's own reverse pass (torch autograd off); torch: torch.autograd")
     argv = sys.argv[1:]
     args = ap.parse_args(argv)
 
@@ -90,6 +92,7 @@ def main():
 
     import torch
 
+    from paddle_amd.autograd import tape
     from paddle_amd.models.llama import LLAMA_CONFIGS, LlamaConfig, LlamaForCausalLM, llama_flops_per_token
     from paddle_amd.parallel import comm
     from paddle_amd.parallel.sharding import FlatShardedOptimizer
@@ -140,17 +143,29 @@ def main():
     pool = [torch.randint(0, cfg.vocab_size, (world * mb, S + 1), generator=gen)[rank * mb:(rank + 1) * mb]
             .to(dev) for _ in range(4)]
 
+    use_tape = args.autograd == "tape" and cuda and not args.recompute
+
+    def micro(x, y):
+        if use_tape:
+            # forward recorded on the framework tape with torch autograd disabled; the
+            # 1/accum loss scale is the seed gradient of the reverse pass
+            with tape.recording() as t:
+                loss = model(x, y)
+            t.backward(loss, torch.full_like(loss, 1.0 / args.accum))
+            return loss / args.accum
+        loss = model(x, y) / args.accum
+        loss.backward()
+        return loss
+
     def train_step(i):
         for a in range(args.accum):
             batch = pool[(i * args.accum + a) % len(pool)]
             x, y = batch[:, :-1], batch[:, 1:]
             if a < args.accum - 1:
                 with opt.no_sync():
-                    loss = model(x, y) / args.accum
-                    loss.backward()
+                    loss = micro(x, y)
             else:
-                loss = model(x, y) / args.accum
-                loss.backward()
+                loss = micro(x, y)
         opt.step()
         opt.zero_grad()
         return loss
@@ -212,6 +227,7 @@ def main():
                 "recompute": bool(args.recompute),
                 "tuned_gemm": tuned,
                 "grad_dtype": str(opt.grad_dtype).replace("torch.", ""),
+                "autograd": "tape" if use_tape else "torch",
                 "device": args.device,
             },
             "final_loss": round(final_loss, 5),

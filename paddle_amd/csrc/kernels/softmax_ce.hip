@@ -233,3 +233,46 @@ PA_EXPORT int pa_softmax_bwd(int dtype, const void* y, const void* dy, void* dx,
     hipLaunchKernelGGL(softmax_bwd_kernel<float>, dim3(N), dim3(256), 0, st, (const float*)y, (const float*)dy, (float*)dx, N, V, log_softmax);
   PA_LAUNCH_CHECK();
 }
+
+// ---------------------------------------------------------------- mean reduction
+// out[0] = sum_r loss[r] / max(1, #rows with a valid label); cnt[0] = that count.
+// One block; the fused CE + mean node of the framework tape (no framework ops
+// between the kernel and the scalar loss).
+__global__ __launch_bounds__(1024) void ce_mean_fwd_kernel(const float* __restrict__ loss,
+                                                           const long* __restrict__ label, long N, int V,
+                                                           long ignore_index, float* __restrict__ out,
+                                                           float* __restrict__ cnt) {
+  __shared__ float red[16];
+  float s = 0.f, c = 0.f;
+  for (long r = threadIdx.x; r < N; r += blockDim.x) {
+    const long lb = label[r];
+    const bool ok = !(lb == ignore_index || lb < 0 || lb >= V);
+    s += loss[r];
+    c += ok ? 1.f : 0.f;
+  }
+  s = block_sum<1024>(s, red);
+  __syncthreads();
+  c = block_sum<1024>(c, red);
+  if (threadIdx.x == 0) {
+    cnt[0] = c;
+    out[0] = s / fmaxf(c, 1.f);
+  }
+}
+
+__global__ void ce_mean_bwd_rows_kernel(const float* __restrict__ g, const float* __restrict__ cnt,
+                                        float* __restrict__ dl, long N) {
+  const float v = g[0] / fmaxf(cnt[0], 1.f);
+  for (long r = (long)blockIdx.x * blockDim.x + threadIdx.x; r < N; r += (long)gridDim.x * blockDim.x) dl[r] = v;
+}
+
+PA_EXPORT int pa_ce_mean_fwd(const float* loss, const long* label, long N, int V, long ignore_index, float* out,
+                             float* cnt, hipStream_t st) {
+  hipLaunchKernelGGL(ce_mean_fwd_kernel, dim3(1), dim3(1024), 0, st, loss, label, N, V, ignore_index, out, cnt);
+  PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_ce_mean_bwd_rows(const float* g, const float* cnt, float* dl, long N, hipStream_t st) {
+  if (N <= 0) return 0;
+  hipLaunchKernelGGL(ce_mean_bwd_rows_kernel, dim3(stream_grid(N, 256)), dim3(256), 0, st, g, cnt, dl, N);
+  PA_LAUNCH_CHECK();
+}

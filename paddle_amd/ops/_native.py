@@ -73,6 +73,8 @@ _SIGS = {
     "pa_splitk_reduce": [_P, _P, _L, _I, _I, _P],
     "pa_moe_gather": [_P, _P, _P, _L, _I, _P],
     "pa_group_tile_table": [_P, _I, _L, _P],
+    "pa_ce_mean_fwd": [_P, _P, _L, _I, _L, _P, _P, _P],
+    "pa_ce_mean_bwd_rows": [_P, _P, _P, _L, _P],
     "pa_binary": [_I, _I, _P, _P, _P, _L, _I, _P, _P, _P, _I, _P],
     "pa_reduce": [_I, _I, _P, _P, _L, _L, _L, _P],
     "pa_dropout": [_I, _P, _P, _P, _L, _F, _F, ctypes.c_ulonglong, ctypes.c_ulonglong, _P],

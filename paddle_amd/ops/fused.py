@@ -16,6 +16,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _native as N
+from ..autograd import tape as _tape
 from . import gemm as _G
 
 # --------------------------------------------------------------------------- utils
@@ -100,7 +101,7 @@ def rms_norm(x, weight, eps=1e-6, residual=None):
     returns (rms_norm(h), h) with the add fused into the same pass."""
     param_ready(weight)
     if x.is_cuda:
-        y, h = _NormFn.apply(x, residual, weight, None, eps, True)
+        y, h = _tape.apply(_NormFn, x, residual, weight, None, eps, True)
         return (y, h) if residual is not None else y
     y, h = _norm_ref(x, residual, weight, None, eps, True)
     return (y, h) if residual is not None else y
@@ -112,7 +113,7 @@ def layer_norm(x, weight, bias=None, eps=1e-5, residual=None):
     if bias is not None:
         param_ready(bias)
     if x.is_cuda and weight is not None and x.shape[-1] % 8 == 0 and x.shape[-1] <= 8192:
-        y, h = _NormFn.apply(x, residual, weight, bias, eps, False)
+        y, h = _tape.apply(_NormFn, x, residual, weight, bias, eps, False)
         return (y, h) if residual is not None else y
     if weight is None:
         h = x + residual if residual is not None else x
@@ -249,7 +250,7 @@ def flash_attention(q, k, v, causal=True, scale=None):
     if q.is_cuda:
         if q.dtype != torch.bfloat16 or q.shape[-1] not in (64, 128, 256):
             raise NotImplementedError("flash_attention kernel: bf16 with head_dim 64/128/256")
-        return _FlashAttnFn.apply(q, k, v, causal, scale)
+        return _tape.apply(_FlashAttnFn, q, k, v, causal, scale)
     return _attn_ref(q, k, v, causal, scale)
 
 
@@ -313,7 +314,7 @@ def flash_attention_varlen(q, k, v, cu_seqlens_q, cu_seqlens_k=None, causal=True
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
     if q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in (64, 128, 256):
-        return _FlashAttnVarlenFn.apply(q, k, v, cu_q, cu_k, causal, scale)
+        return _tape.apply(_FlashAttnVarlenFn, q, k, v, cu_q, cu_k, causal, scale)
     outs = []
     for i in range(len(cu_q) - 1):
         qs, ks, vs = (t[a:b].unsqueeze(0) for t, a, b in ((q, cu_q[i], cu_q[i + 1]), (k, cu_k[i], cu_k[i + 1]),
@@ -389,7 +390,7 @@ def rope_attention(qkv, cos, sin, num_heads, num_kv_heads=None, causal=True, sca
     if scale is None:
         scale = 1.0 / math.sqrt(D)
     if qkv.is_cuda and qkv.dtype == torch.bfloat16 and D in (64, 128):
-        return _RopeAttnFn.apply(qkv, cos, sin, num_heads, Hk, D, causal, scale)
+        return _tape.apply(_RopeAttnFn, qkv, cos, sin, num_heads, Hk, D, causal, scale)
     # other dtypes / head sizes: plain rotary + attention (the kernels are bf16)
     x = qkv.view(B, S, num_heads + 2 * Hk, D)
     q = _rope_ref(x[:, :, :num_heads], cos, sin)
@@ -454,7 +455,7 @@ def packed_attention(qkv, num_heads, causal=True, scale=None):
     if scale is None:
         scale = 1.0 / math.sqrt(D)
     if qkv.is_cuda and qkv.dtype == torch.bfloat16 and D in (64, 128):
-        return _PackedAttnFn.apply(qkv, num_heads, D, causal, scale)
+        return _tape.apply(_PackedAttnFn, qkv, num_heads, D, causal, scale)
     x = qkv.view(B, S, 3 * num_heads, D)
     q, k, v = x[:, :, :num_heads], x[:, :, num_heads:2 * num_heads], x[:, :, 2 * num_heads:]
     return _attn_ref(q, k, v, causal, scale).reshape(B, S, num_heads * D)
@@ -463,7 +464,7 @@ def packed_attention(qkv, num_heads, causal=True, scale=None):
 def apply_rotary(x, cos, sin, inverse=False):
     """Rotate [B, S, H, D] (neox convention)."""
     if x.is_cuda:
-        return _RopeFn.apply(x, cos, sin, inverse)
+        return _tape.apply(_RopeFn, x, cos, sin, inverse)
     return _rope_ref(x, cos, sin, -1.0 if inverse else 1.0)
 
 
@@ -520,7 +521,7 @@ def swiglu(x, y=None):
     if y is not None:
         x = torch.cat([x, y], -1)
     if x.is_cuda and (x.shape[-1] // 2) % 8 == 0:
-        return _SwiGLUFn.apply(x)
+        return _tape.apply(_SwiGLUFn, x)
     g, u = x.chunk(2, -1)
     return (torch.nn.functional.silu(g.float()) * u.float()).to(x.dtype)
 
@@ -555,10 +556,47 @@ class _SoftmaxCEFn(torch.autograd.Function):
         return dx.view(ctx.shape), None, None, None
 
 
+class _SoftmaxCEMeanFn(torch.autograd.Function):
+    """CE + mean over the valid labels as ONE node (per-row kernel, then a one-block
+    reduce that also counts the valid rows): the scalar loss comes straight out of
+    a fused op, so the framework tape can start its reverse pass there."""
+
+    @staticmethod
+    def forward(ctx, logits, label, ignore_index, inplace_grad):
+        V = logits.shape[-1]
+        x = _c(logits).view(-1, V)
+        lab = _c(label).view(-1).long()
+        Nr = x.shape[0]
+        loss = torch.empty(Nr, dtype=torch.float32, device=x.device)
+        lse = torch.empty(Nr, dtype=torch.float32, device=x.device)
+        N.call("pa_softmax_ce_fwd", N.dt(x), N.ptr(x), N.ptr(lab), None, N.ptr(loss), N.ptr(lse), Nr, V,
+               int(ignore_index), N.stream())
+        out = torch.empty((), dtype=torch.float32, device=x.device)
+        cnt = torch.empty(1, dtype=torch.float32, device=x.device)
+        N.call("pa_ce_mean_fwd", N.ptr(loss), N.ptr(lab), Nr, V, int(ignore_index), N.ptr(out), N.ptr(cnt),
+               N.stream())
+        ctx.save_for_backward(x, lab, lse, cnt)
+        ctx.ignore_index, ctx.inplace, ctx.shape = ignore_index, inplace_grad, logits.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, lab, lse, cnt = ctx.saved_tensors
+        Nr, V = x.shape
+        dl = torch.empty(Nr, dtype=torch.float32, device=x.device)
+        N.call("pa_ce_mean_bwd_rows", N.ptr(_c(g.float()).reshape(1)), N.ptr(cnt), N.ptr(dl), Nr, N.stream())
+        dx = x if ctx.inplace else torch.empty_like(x)
+        N.call("pa_softmax_ce_bwd", N.dt(x), N.ptr(x), N.ptr(lab), None, N.ptr(lse), N.ptr(dl), N.ptr(dx),
+               Nr, V, int(ctx.ignore_index), 1.0, N.stream())
+        return dx.view(ctx.shape), None, None, None
+
+
 def softmax_cross_entropy(logits, label, ignore_index=-100, reduction="mean", inplace_grad=False):
     """Fused log-softmax + NLL over the last axis.  loss is fp32."""
+    if logits.is_cuda and reduction == "mean":
+        return _tape.apply(_SoftmaxCEMeanFn, logits, label, ignore_index, inplace_grad)
     if logits.is_cuda:
-        loss, _ = _SoftmaxCEFn.apply(logits, label, ignore_index, inplace_grad)
+        loss, _ = _tape.apply(_SoftmaxCEFn, logits, label, ignore_index, inplace_grad)
     else:
         lf = logits.float().reshape(-1, logits.shape[-1])
         loss = torch.nn.functional.cross_entropy(lf, label.reshape(-1).long(), ignore_index=ignore_index,
@@ -594,7 +632,7 @@ class _SoftmaxFn(torch.autograd.Function):
 
 def softmax(x, axis=-1, log=False):
     if x.is_cuda and (axis == -1 or axis == x.dim() - 1) and x.dtype in (torch.float32, torch.bfloat16):
-        return _SoftmaxFn.apply(x, log)
+        return _tape.apply(_SoftmaxFn, x, log)
     return torch.log_softmax(x, axis) if log else torch.softmax(x, axis)
 
 
@@ -627,7 +665,7 @@ def embedding(ids, weight, padding_idx=None):
     param_ready(weight)
     pad = -1 if padding_idx is None else int(padding_idx)
     if weight.is_cuda and weight.shape[1] % 8 == 0:
-        return _EmbeddingFn.apply(ids, weight, pad)
+        return _tape.apply(_EmbeddingFn, ids, weight, pad)
     return torch.nn.functional.embedding(ids.long(), weight, padding_idx=padding_idx)
 
 
@@ -907,11 +945,11 @@ def linear_gelu(x, weight, bias):
     """gelu(x W + b, approximate='tanh') as one fused autograd node."""
     param_ready(weight)
     param_ready(bias)
-    return _LinearGeluFn.apply(x, weight, bias)
+    return _tape.apply(_LinearGeluFn, x, weight, bias)
 
 
 def linear(x, weight, bias=None):
     param_ready(weight)
     if bias is not None:
         param_ready(bias)
-    return _LinearFn.apply(x, weight, bias)
+    return _tape.apply(_LinearFn, x, weight, bias)

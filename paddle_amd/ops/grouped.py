@@ -21,6 +21,7 @@ from __future__ import annotations
 import torch
 
 from . import _native as N
+from ..autograd import tape as _tape
 from . import fp8 as _F8
 from . import gemm as _G
 
@@ -176,4 +177,4 @@ def grouped_swiglu_mlp(x, gate_up, down, counts, fp8=False):
     optimizer step)."""
     offs = expert_offsets(counts, x.device, x.shape[0])
     fn = _GroupedSwiGLUF8Fn if fp8 else _GroupedSwiGLUFn
-    return fn.apply(x, gate_up, down, offs)
+    return _tape.apply(fn, x, gate_up, down, offs)

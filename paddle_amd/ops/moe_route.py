@@ -14,6 +14,7 @@ from __future__ import annotations
 import torch
 
 from . import _native as N
+from ..autograd import tape as _tape
 
 
 def _c(t):
@@ -86,14 +87,14 @@ class _CombineFn(torch.autograd.Function):
 def dispatch(x, src, pos, k):
     """x [T, H] -> rows in sorted order [R, H]."""
     if _native_ok(x):
-        return _DispatchFn.apply(x, src, pos, k)
+        return _tape.apply(_DispatchFn, x, src, pos, k)
     return x[src.long()]
 
 
 def combine(ys, w, pos, k):
     """ys [R, H] (sorted order), w [T*k] gate weights -> y [T, H]."""
     if _native_ok(ys):
-        return _CombineFn.apply(ys, w, pos, k)
+        return _tape.apply(_CombineFn, ys, w, pos, k)
     T = pos.numel() // k
     keep = pos >= 0
     slots = keep.nonzero().squeeze(-1)

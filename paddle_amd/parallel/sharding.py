@@ -160,6 +160,9 @@ class FlatShardedOptimizer:
         if self.W > 1 or self.main_grad:
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+                # the framework tape (autograd/tape.py) fires these at the same point
+                p._pa_grad_ready_hooks = [h for h in getattr(p, "_pa_grad_ready_hooks", ())
+                                          if getattr(h, "__self__", None) is not self] + [self._on_grad]
 
     # ------------------------------------------------------------------ comm
     def no_sync(self):
