@@ -123,12 +123,12 @@ class Tape:
                     if h[0] == "act":
                         if g is not None:
                             prev = grads.get(h[1])
-                            grads[h[1]] = g if prev is None else prev + g
+                            grads[h[1]] = g if prev is None else _add(prev, g)
                     else:
                         p = h[1]
                         if g is not None:
                             g = g.to(p.dtype)
-                            p.grad = g if p.grad is None else p.grad + g
+                            p.grad = g if p.grad is None else _add(p.grad, g)
                         self._param_done(p)
                 e.ctx = None
         self.entries.clear()
@@ -146,6 +146,17 @@ class Tape:
         if n == 0:
             for hook in getattr(p, "_pa_grad_ready_hooks", ()):
                 hook(p)
+
+
+def _add(a, b):
+    """Gradient accumulation on the op library's broadcast kernel (oplib.hip)."""
+    if a.is_cuda and a.shape == b.shape and a.dtype == b.dtype:
+        from ..ops import oplib
+
+        r = oplib.binary("add", a, b)
+        if r is not None:
+            return r
+    return a + b
 
 
 @contextlib.contextmanager

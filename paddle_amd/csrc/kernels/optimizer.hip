@@ -147,3 +147,15 @@ PA_EXPORT int pa_sumsq(int dtype, const void* x, long n, float* out, hipStream_t
     hipLaunchKernelGGL(sumsq_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)x, n, out);
   PA_LAUNCH_CHECK();
 }
+
+// Global-norm clip coefficient on the device (no host sync, no framework scalar ops):
+// coef = min(1, max_norm / (sqrt(sumsq) * norm_scale + 1e-6)).
+__global__ void clip_coef_kernel(const float* __restrict__ sumsq, float norm_scale, float max_norm,
+                                 float* __restrict__ coef) {
+  if (threadIdx.x == 0) coef[0] = fminf(1.f, max_norm / (sqrtf(sumsq[0]) * norm_scale + 1e-6f));
+}
+
+PA_EXPORT int pa_clip_coef(const float* sumsq, float norm_scale, float max_norm, float* coef, hipStream_t st) {
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(64), 0, st, sumsq, norm_scale, max_norm, coef);
+  PA_LAUNCH_CHECK();
+}

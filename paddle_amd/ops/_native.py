@@ -73,6 +73,7 @@ _SIGS = {
     "pa_splitk_reduce": [_P, _P, _L, _I, _I, _P],
     "pa_moe_gather": [_P, _P, _P, _L, _I, _P],
     "pa_group_tile_table": [_P, _I, _L, _P],
+    "pa_clip_coef": [_P, _F, _F, _P, _P],
     "pa_ce_mean_fwd": [_P, _P, _L, _I, _L, _P, _P, _P],
     "pa_ce_mean_bwd_rows": [_P, _P, _P, _L, _P],
     "pa_binary": [_I, _I, _P, _P, _P, _L, _I, _P, _P, _P, _I, _P],

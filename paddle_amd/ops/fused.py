@@ -649,6 +649,7 @@ class _EmbeddingFn(torch.autograd.Function):
                int(padding_idx), N.stream())
         ctx.save_for_backward(ids_)
         ctx.wshape, ctx.wdtype, ctx.pad = weight.shape, weight.dtype, padding_idx
+        ctx.weight = weight if getattr(weight, "_pa_main_grad", None) is not None else None
         return out.view(*ids.shape, H)
 
     @staticmethod
@@ -656,6 +657,17 @@ class _EmbeddingFn(torch.autograd.Function):
         (ids_,) = ctx.saved_tensors
         H = ctx.wshape[1]
         d = _c(dout).view(-1, H)
+        w = ctx.weight
+        mg = getattr(w, "_pa_main_grad", None) if w is not None else None
+        if mg is not None and mg.dtype == torch.float32:
+            # scatter-add straight into the fp32 main_grad (zeroed first on the first
+            # write after zero_grad), like the fused linear's dW epilogue
+            if getattr(w, "_pa_grad_fresh", False):
+                mg.zero_()
+                w._pa_grad_fresh = False
+            N.call("pa_embedding_bwd", N.dt(d), N.ptr(ids_), N.ptr(d), N.ptr(mg), ids_.numel(), H, int(ctx.pad),
+                   N.stream())
+            return None, None, None
         dW = torch.zeros(ctx.wshape, dtype=torch.float32, device=d.device)
         N.call("pa_embedding_bwd", N.dt(d), N.ptr(ids_), N.ptr(d), N.ptr(dW), ids_.numel(), H, int(ctx.pad), N.stream())
         return None, dW.to(ctx.wdtype), None

@@ -229,7 +229,14 @@ class FlatShardedOptimizer:
             return None
         sq = fused_optim.sumsq(self.grad_shard)
         comm.all_reduce(sq, group=self.group)
-        norm = sq.sqrt() / self.W  # gradients are sums over W ranks
+        # gradients are sums over W ranks: norm = sqrt(sq) / W
+        if sq.is_cuda:
+            from ..ops import _native as N
+
+            coef = torch.empty(1, dtype=torch.float32, device=sq.device)
+            N.call("pa_clip_coef", N.ptr(sq), 1.0 / self.W, float(self.grad_clip), N.ptr(coef), N.stream())
+            return coef
+        norm = sq.sqrt() / self.W
         return torch.clamp(self.grad_clip / (norm + 1e-6), max=1.0)
 
     # ------------------------------------------------------------------ all-gather
