@@ -132,6 +132,12 @@ def main():
     nparams = sum(p.numel() for p in model.parameters())
     mem = (lambda: torch.cuda.memory_allocated(dev) / 2**30) if cuda else (lambda: 0.0)
     peak = (lambda: torch.cuda.max_memory_allocated(dev) / 2**30) if cuda else (lambda: 0.0)
+    if cuda and os.environ.get("FLAGS_allocator_strategy") == "buddy":
+        # torch's pluggable-allocator hook keeps no statistics: ask the buddy allocator
+        from paddle_amd import runtime as _rt
+
+        mem = lambda: _rt.torch_allocator_stats(dev.index)["used"] / 2**30  # noqa: E731
+        peak = lambda: _rt.torch_allocator_stats(dev.index)["peak"] / 2**30  # noqa: E731
     if rank == 0:
         log(f"[bench] model {args.model} params={nparams/1e9:.3f}B layers={cfg.num_hidden_layers} "
             f"world={world} grads={opt.grad_dtype} build {time.time()-t0:.1f}s mem={mem():.1f}GiB")

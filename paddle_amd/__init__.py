@@ -15,6 +15,23 @@ import torch  # noqa: F401  (loads the HIP runtime our kernel library links agai
 
 __version__ = "0.1.0"
 
+
+def _install_allocator():
+    """FLAGS_allocator_strategy=buddy: torch's device tensors come from the native
+    buddy allocator (csrc/runtime/allocator.cc).  Has to happen before the first
+    device allocation, hence at import."""
+    import os
+
+    if os.environ.get("FLAGS_allocator_strategy", "") != "buddy" or not torch.cuda.is_available():
+        return
+    from . import runtime
+
+    mb = int(os.environ.get("FLAGS_buddy_chunk_mb", "4096"))
+    runtime.use_buddy_allocator_for_torch(chunk_bytes=mb << 20)
+
+
+_install_allocator()
+
 from . import ops  # noqa: E402,F401
 from . import tensor_api as _tensor_api  # noqa: E402
 

@@ -137,6 +137,46 @@ struct Buddy {
 std::mutex g_mu;
 std::map<int, Buddy*> g_torch;  // device -> allocator used by the torch hook
 size_t g_torch_chunk = 4ull << 30;
+
+// Stream-ordered release for the torch hook: a freed block may still be read by
+// kernels queued on its stream, so free() records an event there and the block
+// returns to the buddy pool once the event has completed (polled on the next
+// allocation; all pending events are waited for only when an allocation would
+// otherwise fail) -- no host synchronisation on the free path.
+struct Pending {
+  void* ptr;
+  hipEvent_t ev;
+};
+std::map<int, std::vector<Pending>> g_pending;
+std::vector<hipEvent_t> g_event_pool;
+
+hipEvent_t take_event() {
+  if (!g_event_pool.empty()) {
+    hipEvent_t e = g_event_pool.back();
+    g_event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  return e;
+}
+
+// caller holds g_mu; wait == true blocks on every pending event
+void drain(int device, Buddy* b, bool wait) {
+  auto& pend = g_pending[device];
+  size_t keep = 0;
+  for (size_t i = 0; i < pend.size(); ++i) {
+    Pending& q = pend[i];
+    const hipError_t st = wait ? hipEventSynchronize(q.ev) : hipEventQuery(q.ev);
+    if (st == hipSuccess) {
+      b->release(q.ptr);
+      g_event_pool.push_back(q.ev);
+    } else {
+      pend[keep++] = q;
+    }
+  }
+  pend.resize(keep);
+}
 }  // namespace
 
 PA_RT_EXPORT void* pa_buddy_create(int device, size_t chunk_bytes, int init_mem) {
@@ -164,33 +204,38 @@ PA_RT_EXPORT void pa_buddy_stats(void* h, size_t* used, size_t* reserved, size_t
 PA_RT_EXPORT void pa_torch_set_chunk(size_t bytes) { g_torch_chunk = bytes; }
 
 PA_RT_EXPORT void* pa_torch_malloc(ssize_t size, int device, hipStream_t) {
+  std::lock_guard<std::mutex> g(g_mu);
   Buddy* b;
-  {
-    std::lock_guard<std::mutex> g(g_mu);
-    auto it = g_torch.find(device);
-    if (it == g_torch.end()) {
-      b = new Buddy();
-      b->device = device;
-      b->chunk = g_torch_chunk;
-      g_torch[device] = b;
-    } else {
-      b = it->second;
-    }
+  auto it = g_torch.find(device);
+  if (it == g_torch.end()) {
+    b = new Buddy();
+    b->device = device;
+    b->chunk = g_torch_chunk;
+    g_torch[device] = b;
+  } else {
+    b = it->second;
   }
-  return b->alloc((size_t)size);
+  drain(device, b, false);
+  void* p = b->alloc((size_t)size);
+  if (!p && !g_pending[device].empty()) {  // blocks still in flight: wait for them, retry
+    drain(device, b, true);
+    p = b->alloc((size_t)size);
+  }
+  return p;
 }
 
 PA_RT_EXPORT void pa_torch_free(void* ptr, ssize_t, int device, hipStream_t stream) {
-  Buddy* b;
-  {
-    std::lock_guard<std::mutex> g(g_mu);
-    b = g_torch[device];
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_torch.find(device);
+  if (it == g_torch.end() || !ptr) return;
+  hipEvent_t ev = take_event();
+  if (ev && hipEventRecord(ev, stream) == hipSuccess) {
+    g_pending[device].push_back({ptr, ev});
+  } else {  // no event: fall back to a synchronous release
+    if (ev) g_event_pool.push_back(ev);
+    if (stream) hipStreamSynchronize(stream);
+    it->second->release(ptr);
   }
-  // stream-ordered reuse: a freed block may still be read by queued kernels on
-  // `stream`; wait for them before recycling (same-stream reuse would be safe,
-  // but other streams may pick the block next).
-  if (stream) hipStreamSynchronize(stream);
-  if (b) b->release(ptr);
 }
 
 PA_RT_EXPORT void pa_torch_stats(int device, size_t* used, size_t* reserved, size_t* peak) {

@@ -247,6 +247,15 @@ def use_buddy_allocator_for_torch(chunk_bytes=4 << 30):
     torch.cuda.memory.change_current_allocator(alloc)
 
 
+def torch_allocator_stats(device=0):
+    """(used, reserved, peak) bytes of the buddy allocator behind torch on ``device``
+    (all zero when it is not installed).  ``used`` includes blocks whose release is
+    still waiting for their stream."""
+    u, r, pk = SZ(), SZ(), SZ()
+    lib().pa_torch_stats(int(device), ctypes.byref(u), ctypes.byref(r), ctypes.byref(pk))
+    return {"used": u.value, "reserved": r.value, "peak": pk.value}
+
+
 # ------------------------------------------------------------------ blocking queue
 
 

@@ -1,5 +1,8 @@
-"""A few LLaMA-tiny training steps on the framework tape (for kernel traces):
-``rocprofv3 --kernel-trace --stats -d DIR -- python tools/llama_tiny_step.py``."""
+"""A few LLaMA-tiny training steps on the framework tape (for kernel traces and
+allocator A/B runs): ``rocprofv3 --kernel-trace --stats -d DIR -- python
+tools/llama_tiny_step.py [steps]``.  Prints one JSON line with the per-step losses
+and, under FLAGS_allocator_strategy=buddy, the buddy allocator's statistics."""
+import json
 import os
 import sys
 
@@ -7,6 +10,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
+import paddle_amd  # noqa: E402,F401  (installs the allocator selected by FLAGS_allocator_strategy)
+from paddle_amd import runtime  # noqa: E402
 from paddle_amd.autograd import tape  # noqa: E402
 from paddle_amd.models.llama import LLAMA_CONFIGS, LlamaConfig, LlamaForCausalLM  # noqa: E402
 from paddle_amd.parallel.sharding import FlatShardedOptimizer  # noqa: E402
@@ -19,11 +24,16 @@ opt = FlatShardedOptimizer(model.named_parameters(), lr=1e-3, weight_decay=0.1, 
 ids = torch.randint(0, cfg.vocab_size, (4, 257), generator=torch.Generator().manual_seed(1)).cuda()
 torch.cuda.synchronize()
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+losses = []
 for step in range(steps):
     with tape.recording() as t:
         loss = model(ids[:, :-1], ids[:, 1:])
     t.backward(loss)
     opt.step()
     opt.zero_grad()
+    losses.append(float(loss))
 torch.cuda.synchronize()
-print("loss", float(loss))
+out = {"losses": losses, "allocator": os.environ.get("FLAGS_allocator_strategy", "torch_caching")}
+if out["allocator"] == "buddy" and runtime.available():
+    out["buddy"] = runtime.torch_allocator_stats(0)
+print(json.dumps(out))
