@@ -33,6 +33,8 @@ ARCH = os.environ.get("PADDLE_AMD_ARCH", "gfx950")
 
 KERNEL_LIB = os.path.join(LIBDIR, "libpaddle_amd_kernels.so")
 RUNTIME_LIB = os.path.join(LIBDIR, "libpaddle_amd_runtime.so")
+NATIVE_LIB = os.path.join(LIBDIR, "libpaddle_amd_native.so")
+NATIVE_INC = os.path.join(ROOT, "csrc", "native")
 
 
 def _hipcc() -> str:
@@ -128,11 +130,70 @@ def build_runtime(verbose: bool = False, jobs: int | None = None) -> str:
                       jobs or min(8, os.cpu_count() or 4))
 
 
+def _hip_ldflags() -> list[str]:
+    tl = _torch_lib_dir()
+    if tl:  # the same libamdhip64 torch loads, so ctypes users share one HIP runtime
+        return [f"-L{tl}", f"-Wl,-rpath,{tl}", "-lamdhip64"]
+    return ["-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lamdhip64"]
+
+
+def build_native(verbose: bool = False, jobs: int | None = None) -> str:
+    """The native C++ executor + inference API (``csrc/native``): host kernels
+    compiled with g++ (AVX2/FMA), device kernels with hipcc for gfx950, one shared
+    library with public C++ symbols (paddle_inference_api.h) and a C ABI."""
+    d = os.path.join(ROOT, "csrc", "native")
+    ccs = sorted(glob.glob(os.path.join(d, "*.cc")))
+    hips = sorted(glob.glob(os.path.join(d, "*.hip")))
+    hdrs = sorted(glob.glob(os.path.join(d, "*.h")))
+    os.makedirs(BUILDDIR, exist_ok=True)
+    os.makedirs(LIBDIR, exist_ok=True)
+    cxx = shutil.which("g++") or "c++"
+    ccflags = ["-O3", "-fPIC", "-std=c++17", "-Wall", "-pthread", "-mavx2", "-mfma",
+               "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]
+    hipflags = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-ffp-contract=fast"]
+    objs, todo = [], []
+    for srcs, comp, fl in ((ccs, cxx, ccflags), (hips, _hipcc(), hipflags)):
+        stamp = hashlib.sha1(" ".join([comp] + fl).encode()).hexdigest()
+        for s in srcs:
+            obj = os.path.join(BUILDDIR, "native_" + os.path.basename(s) + ".o")
+            objs.append(obj)
+            if _needs(obj, [s] + hdrs, stamp):
+                todo.append(([comp] + fl + ["-c", s, "-o", obj], obj, stamp))
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=jobs or min(8, os.cpu_count() or 4)) as ex:
+            list(ex.map(lambda a: _compile(a[0], a[1], a[2], verbose), todo))
+    out = NATIVE_LIB
+    if todo or not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
+        cmd = [_hipcc(), "-shared", f"--offload-arch={ARCH}", "-o", out + ".tmp"] + objs + ["-pthread"] + _hip_ldflags()
+        if verbose:
+            print("[paddle_amd build]", " ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed for {out}:\n{r.stderr[-4000:]}")
+        os.replace(out + ".tmp", out)
+    return out
+
+
+def build_native_program(src: str, out: str, extra: list[str] | None = None) -> str:
+    """Compiles a C++ program against the native library's public headers
+    (paddle_inference_api.h / framework.h) and links libpaddle_amd_native.so."""
+    lib = build_native()
+    cxx = shutil.which("g++") or "c++"
+    cmd = [cxx, "-O2", "-std=c++17", "-pthread", src, f"-I{NATIVE_INC}", f"-L{LIBDIR}", "-lpaddle_amd_native",
+           f"-Wl,-rpath,{LIBDIR}", "-o", out] + (extra or [])
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"building {src} failed:\n{r.stderr[-4000:]}")
+    assert os.path.exists(lib)
+    return out
+
+
 def build_all(verbose: bool = False) -> list[str]:
     out = [build_kernels(verbose)]
     rt = build_runtime(verbose)
     if rt:
         out.append(rt)
+    out.append(build_native(verbose))
     return out
 
 

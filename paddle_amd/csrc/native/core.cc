@@ -1,0 +1,793 @@
+// Native executor core: error reporting, dtypes, ProgramDesc wire-format decoding,
+// tensors / scopes, host worker pool, kernel registry, Executor, LoDTensor IO.
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <fstream>
+#include <set>
+#include <sstream>
+#include <thread>
+
+#include "framework.h"
+
+namespace pa {
+
+void fail(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  throw Error(buf);
+}
+
+size_t dt_size(DT t) {
+  switch (t) {
+    case DT::BOOL: case DT::UINT8: case DT::INT8: return 1;
+    case DT::INT16: case DT::FP16: case DT::BF16: return 2;
+    case DT::INT32: case DT::FP32: return 4;
+    case DT::INT64: case DT::FP64: return 8;
+  }
+  fail("unsupported dtype %d", (int)t);
+}
+
+const char* dt_name(DT t) {
+  switch (t) {
+    case DT::BOOL: return "bool";
+    case DT::INT16: return "int16";
+    case DT::INT32: return "int32";
+    case DT::INT64: return "int64";
+    case DT::FP16: return "float16";
+    case DT::FP32: return "float32";
+    case DT::FP64: return "float64";
+    case DT::UINT8: return "uint8";
+    case DT::INT8: return "int8";
+    case DT::BF16: return "bfloat16";
+  }
+  return "?";
+}
+
+// ================================================================ OpDesc accessors
+static const std::vector<std::string> kEmpty;
+
+const std::vector<std::string>& OpDesc::Inputs(const std::string& slot) const {
+  for (auto& kv : inputs)
+    if (kv.first == slot) return kv.second;
+  return kEmpty;
+}
+const std::vector<std::string>& OpDesc::Outputs(const std::string& slot) const {
+  for (auto& kv : outputs)
+    if (kv.first == slot) return kv.second;
+  return kEmpty;
+}
+std::string OpDesc::Input(const std::string& slot) const {
+  auto& v = Inputs(slot);
+  return v.empty() ? "" : v[0];
+}
+std::string OpDesc::Output(const std::string& slot) const {
+  auto& v = Outputs(slot);
+  return v.empty() ? "" : v[0];
+}
+int64_t OpDesc::GetInt(const std::string& a, int64_t def) const {
+  auto it = attrs.find(a);
+  if (it == attrs.end()) return def;
+  if (it->second.type == A_FLOAT) return (int64_t)it->second.f;
+  return it->second.i;
+}
+float OpDesc::GetFloat(const std::string& a, float def) const {
+  auto it = attrs.find(a);
+  if (it == attrs.end()) return def;
+  if (it->second.type == A_FLOAT) return it->second.f;
+  return (float)it->second.i;
+}
+bool OpDesc::GetBool(const std::string& a, bool def) const {
+  auto it = attrs.find(a);
+  return it == attrs.end() ? def : it->second.i != 0;
+}
+std::string OpDesc::GetString(const std::string& a, const std::string& def) const {
+  auto it = attrs.find(a);
+  return it == attrs.end() ? def : it->second.s;
+}
+std::vector<int64_t> OpDesc::GetInts(const std::string& a) const {
+  auto it = attrs.find(a);
+  if (it == attrs.end()) return {};
+  if (it->second.type == A_INT || it->second.type == A_LONG) return {it->second.i};
+  return it->second.ints;
+}
+std::vector<float> OpDesc::GetFloats(const std::string& a) const {
+  auto it = attrs.find(a);
+  return it == attrs.end() ? std::vector<float>{} : it->second.floats;
+}
+
+const VarDesc* BlockDesc::FindVar(const std::string& n) const {
+  for (auto& v : vars)
+    if (v.name == n) return &v;
+  return nullptr;
+}
+
+// ================================================================ proto2 decoding
+// Minimal wire-format reader: varint (0), fixed64 (1), length-delimited (2),
+// fixed32 (5).  Repeated scalars are accepted both packed and unpacked.
+namespace {
+struct Reader {
+  const unsigned char* p;
+  const unsigned char* end;
+
+  bool more() const { return p < end; }
+  uint64_t varint() {
+    uint64_t v = 0;
+    for (int shift = 0; shift < 64; shift += 7) {
+      PA_CHECK(p < end, "ProgramDesc: truncated varint");
+      uint8_t b = *p++;
+      v |= (uint64_t)(b & 0x7f) << shift;
+      if (!(b & 0x80)) return v;
+    }
+    fail("ProgramDesc: varint too long");
+  }
+  Reader sub() {
+    uint64_t n = varint();
+    PA_CHECK(n <= (uint64_t)(end - p), "ProgramDesc: length %llu runs past the message",
+             (unsigned long long)n);
+    Reader r{p, p + n};
+    p += n;
+    return r;
+  }
+  std::string str() {
+    Reader r = sub();
+    return std::string((const char*)r.p, (size_t)(r.end - r.p));
+  }
+  float f32() {
+    PA_CHECK(end - p >= 4, "ProgramDesc: truncated fixed32");
+    float f;
+    memcpy(&f, p, 4);
+    p += 4;
+    return f;
+  }
+  void skip(int wt) {
+    switch (wt) {
+      case 0: varint(); break;
+      case 1: PA_CHECK(end - p >= 8, "ProgramDesc: truncated fixed64"); p += 8; break;
+      case 2: sub(); break;
+      case 5: PA_CHECK(end - p >= 4, "ProgramDesc: truncated fixed32"); p += 4; break;
+      default: fail("ProgramDesc: unsupported wire type %d", wt);
+    }
+  }
+  template <class F> void ints(int wt, F push) {  // repeated varint field
+    if (wt == 2) {
+      Reader r = sub();
+      while (r.more()) push((int64_t)r.varint());
+    } else {
+      push((int64_t)varint());
+    }
+  }
+};
+
+int64_t zz32(uint64_t v) { return (int64_t)(int32_t)(uint32_t)v; }  // int32 stored as varint
+
+Attr parse_attr(Reader r) {
+  Attr a;
+  while (r.more()) {
+    uint64_t tag = r.varint();
+    int fn = (int)(tag >> 3), wt = (int)(tag & 7);
+    switch (fn) {
+      case 1: a.name = r.str(); break;
+      case 2: a.type = (int)r.varint(); break;
+      case 3: a.i = zz32(r.varint()); break;
+      case 4: a.f = r.f32(); break;
+      case 5: a.s = r.str(); break;
+      case 6: r.ints(wt, [&](int64_t v) { a.ints.push_back((int64_t)(int32_t)v); }); break;
+      case 7:
+        if (wt == 2) {
+          Reader s = r.sub();
+          while (s.more()) a.floats.push_back(s.f32());
+        } else {
+          a.floats.push_back(r.f32());
+        }
+        break;
+      case 8: a.strings.push_back(r.str()); break;
+      case 10: a.i = (int64_t)r.varint(); break;
+      case 11: r.ints(wt, [&](int64_t v) { a.ints.push_back(v != 0); }); break;
+      case 12: a.i = zz32(r.varint()); break;
+      case 13: a.i = (int64_t)r.varint(); break;
+      case 14: r.ints(wt, [&](int64_t v) { a.ints.push_back(v); }); break;
+      default: r.skip(wt);
+    }
+  }
+  return a;
+}
+
+std::pair<std::string, std::vector<std::string>> parse_opvar(Reader r) {
+  std::pair<std::string, std::vector<std::string>> v;
+  while (r.more()) {
+    uint64_t tag = r.varint();
+    int fn = (int)(tag >> 3), wt = (int)(tag & 7);
+    if (fn == 1) v.first = r.str();
+    else if (fn == 2) v.second.push_back(r.str());
+    else r.skip(wt);
+  }
+  return v;
+}
+
+OpDesc parse_op(Reader r) {
+  OpDesc op;
+  while (r.more()) {
+    uint64_t tag = r.varint();
+    int fn = (int)(tag >> 3), wt = (int)(tag & 7);
+    switch (fn) {
+      case 1: op.inputs.push_back(parse_opvar(r.sub())); break;
+      case 2: op.outputs.push_back(parse_opvar(r.sub())); break;
+      case 3: op.type = r.str(); break;
+      case 4: {
+        Attr a = parse_attr(r.sub());
+        std::string n = a.name;
+        op.attrs[n] = std::move(a);
+        break;
+      }
+      default: r.skip(wt);
+    }
+  }
+  return op;
+}
+
+void parse_tensor_desc(Reader r, VarDesc* v) {
+  while (r.more()) {
+    uint64_t tag = r.varint();
+    int fn = (int)(tag >> 3), wt = (int)(tag & 7);
+    if (fn == 1) v->dtype = (DT)r.varint();
+    else if (fn == 2) r.ints(wt, [&](int64_t d) { v->dims.push_back(d); });
+    else r.skip(wt);
+  }
+}
+
+void parse_lod_desc(Reader r, VarDesc* v) {
+  while (r.more()) {
+    uint64_t tag = r.varint();
+    int fn = (int)(tag >> 3), wt = (int)(tag & 7);
+    if (fn == 1) parse_tensor_desc(r.sub(), v);
+    else if (fn == 2) v->lod_level = (int)r.varint();
+    else r.skip(wt);
+  }
+}
+
+void parse_vartype(Reader r, VarDesc* v) {
+  while (r.more()) {
+    uint64_t tag = r.varint();
+    int fn = (int)(tag >> 3), wt = (int)(tag & 7);
+    if (fn == 1) v->type = (int)r.varint();
+    else if (fn == 2) parse_tensor_desc(r.sub(), v);  // selected_rows
+    else if (fn == 3 || fn == 4) parse_lod_desc(r.sub(), v);  // lod_tensor / tensor_array
+    else r.skip(wt);
+  }
+}
+
+VarDesc parse_var(Reader r) {
+  VarDesc v;
+  while (r.more()) {
+    uint64_t tag = r.varint();
+    int fn = (int)(tag >> 3), wt = (int)(tag & 7);
+    if (fn == 1) v.name = r.str();
+    else if (fn == 2) parse_vartype(r.sub(), &v);
+    else if (fn == 3) v.persistable = r.varint() != 0;
+    else r.skip(wt);
+  }
+  return v;
+}
+
+BlockDesc parse_block(Reader r) {
+  BlockDesc b;
+  while (r.more()) {
+    uint64_t tag = r.varint();
+    int fn = (int)(tag >> 3), wt = (int)(tag & 7);
+    switch (fn) {
+      case 1: b.idx = (int)zz32(r.varint()); break;
+      case 2: b.parent_idx = (int)zz32(r.varint()); break;
+      case 3: b.vars.push_back(parse_var(r.sub())); break;
+      case 4: b.ops.push_back(parse_op(r.sub())); break;
+      case 5: b.forward_block_idx = (int)zz32(r.varint()); break;
+      default: r.skip(wt);
+    }
+  }
+  return b;
+}
+}  // namespace
+
+ProgramDesc ProgramDesc::Parse(const std::string& bytes) {
+  ProgramDesc prog;
+  Reader r{(const unsigned char*)bytes.data(), (const unsigned char*)bytes.data() + bytes.size()};
+  while (r.more()) {
+    uint64_t tag = r.varint();
+    if ((tag >> 3) == 1 && (tag & 7) == 2) prog.blocks.push_back(parse_block(r.sub()));
+    else r.skip((int)(tag & 7));
+  }
+  PA_CHECK(!prog.blocks.empty(), "ProgramDesc: no blocks");
+  return prog;
+}
+
+ProgramDesc ProgramDesc::Load(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  PA_CHECK((bool)f, "cannot open program file %s", path.c_str());
+  std::stringstream ss;
+  ss << f.rdbuf();
+  return Parse(ss.str());
+}
+
+// ================================================================ buffers / tensors
+Buffer::Buffer(size_t n, int dev) : bytes(n), device(dev) {
+  size_t sz = n ? n : 1;
+  if (dev < 0) {
+    ptr = aligned_alloc(64, (sz + 63) / 64 * 64);
+    PA_CHECK(ptr != nullptr, "host allocation of %zu bytes failed", n);
+  } else {
+    ptr = device_alloc(sz, dev);
+  }
+}
+
+Buffer::~Buffer() {
+  if (device < 0) free(ptr);
+  else device_free(ptr, device);
+}
+
+int64_t Tensor::numel() const {
+  int64_t n = 1;
+  for (auto d : dims) n *= d;
+  return n;
+}
+
+void* Tensor::alloc(DT t, const std::vector<int64_t>& d, int dev) {
+  for (auto x : d) PA_CHECK(x >= 0, "negative dimension in %s", shape_str().c_str());
+  dtype = t;
+  dims = d;
+  const size_t need = nbytes();
+  if (!buf || buf->device != dev || buf->bytes < need || buf.use_count() > 1)
+    buf = std::make_shared<Buffer>(need, dev);
+  device = dev;
+  return buf->ptr;
+}
+
+template <class T> T* Tensor::alloc(const std::vector<int64_t>& d, int dev) {
+  DT t = std::is_same<T, float>::value ? DT::FP32
+         : std::is_same<T, int64_t>::value ? DT::INT64
+         : std::is_same<T, int32_t>::value ? DT::INT32
+         : std::is_same<T, double>::value ? DT::FP64
+         : std::is_same<T, uint8_t>::value ? DT::UINT8
+                                           : DT::BOOL;
+  return static_cast<T*>(alloc(t, d, dev));
+}
+template float* Tensor::alloc<float>(const std::vector<int64_t>&, int);
+template int64_t* Tensor::alloc<int64_t>(const std::vector<int64_t>&, int);
+template int32_t* Tensor::alloc<int32_t>(const std::vector<int64_t>&, int);
+template double* Tensor::alloc<double>(const std::vector<int64_t>&, int);
+template uint8_t* Tensor::alloc<uint8_t>(const std::vector<int64_t>&, int);
+
+Tensor Tensor::to(int dev, void* stream) const {
+  Tensor o;
+  o.lod = lod;
+  o.alloc(dtype, dims, dev);
+  if (nbytes()) device_copy(o.raw(), dev, raw(), device, nbytes(), stream);
+  return o;
+}
+
+std::string Tensor::shape_str() const {
+  std::string s = "[";
+  for (size_t i = 0; i < dims.size(); ++i) s += (i ? ", " : "") + std::to_string(dims[i]);
+  return s + "]";
+}
+
+// ================================================================ scopes
+Variable* Scope::Var(const std::string& name) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto& v = vars_[name];
+  if (!v) v.reset(new Variable());
+  return v.get();
+}
+
+Variable* Scope::FindLocal(const std::string& name) const {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = vars_.find(name);
+  return it == vars_.end() ? nullptr : it->second.get();
+}
+
+Variable* Scope::Find(const std::string& name) const {
+  for (const Scope* s = this; s; s = s->parent_) {
+    Variable* v = s->FindLocal(name);
+    if (v) return v;
+  }
+  return nullptr;
+}
+
+Scope& Scope::NewScope() {
+  std::lock_guard<std::mutex> g(mu_);
+  kids_.emplace_back(new Scope(this));
+  return *kids_.back();
+}
+
+void Scope::Erase(const std::string& name) {
+  std::lock_guard<std::mutex> g(mu_);
+  vars_.erase(name);
+}
+
+std::vector<std::string> Scope::LocalNames() const {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<std::string> out;
+  for (auto& kv : vars_) out.push_back(kv.first);
+  return out;
+}
+
+// ================================================================ host worker pool
+struct ThreadPool {
+  std::vector<std::thread> workers;
+  std::mutex mu;
+  std::condition_variable cv, done_cv;
+  const std::function<void(int64_t, int64_t)>* job = nullptr;
+  int64_t n = 0, chunk = 0;
+  std::atomic<int64_t> next{0};
+  int active = 0;
+  uint64_t gen = 0;
+  bool stop = false;
+  std::mutex run_mu;  // one parallel_for at a time (nested calls run serially)
+
+  explicit ThreadPool(int nt) {
+    for (int i = 0; i < nt; ++i) workers.emplace_back([this] { loop(); });
+  }
+  ~ThreadPool() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto& t : workers) t.join();
+  }
+  void drain() {
+    for (;;) {
+      int64_t b = next.fetch_add(chunk);
+      if (b >= n) return;
+      (*job)(b, std::min(n, b + chunk));
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> l(mu);
+        cv.wait(l, [&] { return stop || gen != seen; });
+        if (stop) return;
+        seen = gen;
+        ++active;
+      }
+      drain();
+      {
+        std::lock_guard<std::mutex> g(mu);
+        if (--active == 0) done_cv.notify_all();
+      }
+    }
+  }
+  void run(int64_t total, int64_t ch, const std::function<void(int64_t, int64_t)>& fn) {
+    std::unique_lock<std::mutex> busy(run_mu, std::try_to_lock);
+    if (!busy.owns_lock() || workers.empty()) {  // nested or single-threaded
+      fn(0, total);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(mu);
+      job = &fn;
+      n = total;
+      chunk = ch;
+      next = 0;
+      ++gen;
+    }
+    cv.notify_all();
+    drain();
+    std::unique_lock<std::mutex> l(mu);
+    done_cv.wait(l, [&] { return active == 0 && next.load() >= n; });
+    job = nullptr;
+  }
+};
+
+static int pool_threads() {
+  const char* e = getenv("PADDLE_NUM_THREADS");
+  int n = e ? atoi(e) : (int)std::thread::hardware_concurrency();
+  if (n > 32) n = 32;  // host kernels are a fallback path: bounded footprint
+  return n > 1 ? n - 1 : 0;
+}
+
+ThreadPool& host_pool() {
+  static ThreadPool pool(pool_threads());
+  return pool;
+}
+
+void parallel_for(int64_t n, int64_t grain, const std::function<void(int64_t, int64_t)>& fn) {
+  if (n <= 0) return;
+  ThreadPool& p = host_pool();
+  const int64_t nt = (int64_t)p.workers.size() + 1;
+  if (n < 2 * grain || nt == 1) {
+    fn(0, n);
+    return;
+  }
+  int64_t chunk = std::max<int64_t>(grain, (n + 4 * nt - 1) / (4 * nt));
+  p.run(n, chunk, fn);
+}
+
+// ================================================================ registry
+namespace {
+std::unordered_map<std::string, Kernel>& reg(bool device) {
+  static std::unordered_map<std::string, Kernel> host, dev;
+  return device ? dev : host;
+}
+}  // namespace
+
+void register_kernel(const std::string& type, bool device, Kernel k) { reg(device)[type] = std::move(k); }
+
+const Kernel* find_kernel(const std::string& type, bool device) {
+  auto& r = reg(device);
+  auto it = r.find(type);
+  return it == r.end() ? nullptr : &it->second;
+}
+
+std::vector<std::string> registered_ops(bool device) {
+  std::vector<std::string> out;
+  for (auto& kv : reg(device)) out.push_back(kv.first);
+  return out;
+}
+
+// ================================================================ OpRun helpers
+Variable* OpRun::var(const std::string& name) const {
+  Variable* v = scope.Find(name);
+  PA_CHECK(v != nullptr, "%s: variable %s not found", op.type.c_str(), name.c_str());
+  return v;
+}
+
+Tensor& OpRun::in(const std::string& slot, size_t i) const {
+  auto& names = op.Inputs(slot);
+  PA_CHECK(i < names.size(), "%s: missing input %s[%zu]", op.type.c_str(), slot.c_str(), i);
+  Tensor& t = var(names[i])->tensor;
+  PA_CHECK(t.initialized(), "%s: input %s (%s) is not initialised", op.type.c_str(), slot.c_str(),
+           names[i].c_str());
+  return t;
+}
+
+Tensor* OpRun::in_opt(const std::string& slot, size_t i) const {
+  auto& names = op.Inputs(slot);
+  if (i >= names.size()) return nullptr;
+  Variable* v = scope.Find(names[i]);
+  return v && v->tensor.initialized() ? &v->tensor : nullptr;
+}
+
+std::vector<Tensor*> OpRun::ins(const std::string& slot) const {
+  std::vector<Tensor*> out;
+  for (size_t i = 0; i < op.Inputs(slot).size(); ++i) out.push_back(&in(slot, i));
+  return out;
+}
+
+Tensor* OpRun::out(const std::string& slot, size_t i) const {
+  auto& names = op.Outputs(slot);
+  if (i >= names.size() || names[i].empty() || names[i] == "@EMPTY@") return nullptr;
+  Variable* v = scope.Find(names[i]);
+  if (!v) v = scope.Var(names[i]);
+  return &v->tensor;
+}
+
+// ================================================================ executor
+Executor::Executor(int device) {
+  ctx_.device = device;
+  if (device >= 0) {
+    link_device_kernels();
+    ctx_.stream = device_stream_create(device);
+  }
+  link_host_kernels();
+}
+
+Executor::~Executor() {
+  if (ctx_.stream) device_stream_destroy(ctx_.stream);
+}
+
+void Executor::Sync() {
+  if (ctx_.stream) device_stream_sync(ctx_.stream);
+}
+
+void Executor::RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* scope) {
+  (void)prog;
+  const bool dev = ctx_.device >= 0;
+  // kernels that only move metadata / holders work on tensors of any device
+  static const std::set<std::string> agnostic = {"feed", "fetch", "reshape", "reshape2", "flatten", "flatten2",
+                                                 "squeeze", "squeeze2", "unsqueeze", "unsqueeze2", "delete_var",
+                                                 "reshape_grad", "reshape2_grad"};
+  for (const OpDesc& op : block.ops) {
+    const Kernel* k = dev ? find_kernel(op.type, true) : nullptr;
+    bool host_fallback = false;
+    if (!k) {
+      k = find_kernel(op.type, false);
+      host_fallback = dev && !agnostic.count(op.type);
+    }
+    PA_CHECK(k != nullptr, "no kernel registered for op type '%s'", op.type.c_str());
+    if (host_fallback) {
+      // run the host kernel on host copies of device inputs; results go back to HBM
+      Scope& tmp = scope->NewScope();
+      for (auto& slot : op.inputs)
+        for (auto& n : slot.second) {
+          Variable* v = scope->Find(n);
+          if (v && v->tensor.initialized() && v->tensor.device >= 0) {
+            Variable* h = tmp.Var(n);
+            h->kind = v->kind;
+            h->tensor = v->tensor.to(-1, ctx_.stream);
+          }
+        }
+      device_stream_sync(ctx_.stream);
+      for (auto& slot : op.outputs)
+        for (auto& n : slot.second) {
+          Variable* v = scope->Find(n);
+          if (v && !tmp.FindLocal(n)) {
+            Variable* h = tmp.Var(n);
+            h->kind = v->kind;
+            h->list = v->list;
+            if (v->tensor.initialized()) h->tensor = v->tensor.to(-1, ctx_.stream);
+          }
+        }
+      device_stream_sync(ctx_.stream);
+      ExecContext hctx = ctx_;
+      hctx.device = -1;
+      (*k)(OpRun{op, tmp, hctx});
+      for (auto& slot : op.outputs)
+        for (auto& n : slot.second) {
+          Variable* h = tmp.FindLocal(n);
+          if (!h) continue;
+          Variable* v = scope->Find(n);
+          if (!v) v = scope->Var(n);
+          v->kind = h->kind;
+          v->list = h->list;
+          if (h->tensor.initialized())
+            v->tensor = (h->kind == VK_FETCH_LIST) ? h->tensor : h->tensor.to(ctx_.device, ctx_.stream);
+        }
+      continue;
+    }
+    if (profile) {
+      Sync();
+      auto t0 = std::chrono::steady_clock::now();
+      (*k)(OpRun{op, *scope, ctx_});
+      Sync();
+      auto& e = op_time_ms[op.type];
+      e.first += 1;
+      e.second += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    } else {
+      (*k)(OpRun{op, *scope, ctx_});
+    }
+  }
+}
+
+void Executor::Run(const ProgramDesc& prog, Scope* scope, int block_id, Scope* local) {
+  const BlockDesc& block = prog.Block(block_id);
+  Scope* tmp = local ? local : scope;
+  for (const VarDesc& v : block.vars) {
+    // feed / fetch holders are per-run state: they live with the temporaries so
+    // predictors sharing one parameter scope never share them
+    const bool io = v.type == VK_FEED_MINIBATCH || v.type == VK_FETCH_LIST;
+    Scope* s = v.persistable && !io ? scope : tmp;
+    if (tmp->Find(v.name)) continue;
+    Variable* var = s->Var(v.name);
+    var->kind = v.type;
+  }
+  RunBlock(prog, block, tmp);
+}
+
+// ================================================================ LoDTensor IO
+// LoDTensor := u32 version | u64 lod_level | lod_level x (u64 nbytes | u64[]) | Tensor
+// Tensor    := u32 version | i32 desc_size | TensorDesc proto | raw data
+bool read_lod_tensor(FILE* f, Tensor* t) {
+  uint32_t ver;
+  size_t got = fread(&ver, 1, 4, f);
+  if (got == 0) return false;
+  PA_CHECK(got == 4, "LoDTensor: truncated header");
+  uint64_t ll;
+  PA_CHECK(fread(&ll, 8, 1, f) == 1 && ll <= 16, "LoDTensor: bad lod level");
+  t->lod.assign(ll, {});
+  for (uint64_t i = 0; i < ll; ++i) {
+    uint64_t nb;
+    PA_CHECK(fread(&nb, 8, 1, f) == 1 && nb % 8 == 0 && nb <= (1ull << 36), "LoDTensor: bad lod size");
+    std::vector<uint64_t> tmp(nb / 8);
+    PA_CHECK(fread(tmp.data(), 8, tmp.size(), f) == tmp.size(), "LoDTensor: truncated lod");
+    t->lod[i].assign(tmp.begin(), tmp.end());
+  }
+  int32_t dsz;
+  PA_CHECK(fread(&ver, 4, 1, f) == 1 && fread(&dsz, 4, 1, f) == 1 && dsz >= 0 && dsz < (1 << 16),
+           "LoDTensor: bad tensor desc");
+  std::string desc((size_t)dsz, '\0');
+  PA_CHECK(fread(&desc[0], 1, desc.size(), f) == desc.size(), "LoDTensor: truncated desc");
+  VarDesc vd;
+  parse_tensor_desc(Reader{(const unsigned char*)desc.data(), (const unsigned char*)desc.data() + desc.size()},
+                    &vd);
+  for (auto d : vd.dims) PA_CHECK(d >= 0 && d < (1ll << 40), "LoDTensor: implausible dim");
+  LoD lod = t->lod;
+  t->alloc(vd.dtype, vd.dims, -1);
+  t->lod = lod;
+  PA_CHECK(fread(t->raw(), 1, t->nbytes(), f) == t->nbytes(), "LoDTensor: truncated data");
+  return true;
+}
+
+void write_lod_tensor(FILE* f, const Tensor& t0) {
+  Tensor t = t0.device >= 0 ? t0.to(-1) : t0;
+  uint32_t ver = 0;
+  uint64_t ll = t.lod.size();
+  fwrite(&ver, 4, 1, f);
+  fwrite(&ll, 8, 1, f);
+  for (auto& lv : t.lod) {
+    uint64_t nb = lv.size() * 8;
+    fwrite(&nb, 8, 1, f);
+    std::vector<uint64_t> tmp(lv.begin(), lv.end());
+    fwrite(tmp.data(), 8, tmp.size(), f);
+  }
+  std::string desc;
+  auto put = [&](uint64_t v) {
+    while (v >= 0x80) {
+      desc.push_back((char)(v | 0x80));
+      v >>= 7;
+    }
+    desc.push_back((char)v);
+  };
+  desc.push_back(0x08);
+  put((uint64_t)t.dtype);
+  for (auto d : t.dims) {
+    desc.push_back(0x10);
+    put((uint64_t)d);
+  }
+  int32_t dsz = (int32_t)desc.size();
+  fwrite(&ver, 4, 1, f);
+  fwrite(&dsz, 4, 1, f);
+  fwrite(desc.data(), 1, desc.size(), f);
+  fwrite(t.raw(), 1, t.nbytes(), f);
+}
+
+void load_persistables(const ProgramDesc& prog, Scope* scope, const std::string& dir,
+                       const std::string& combined_file, int device, void* stream) {
+  std::vector<const VarDesc*> vars;
+  for (const VarDesc& v : prog.Block(0).vars) {
+    if (!v.persistable || v.type == VK_FEED_MINIBATCH || v.type == VK_FETCH_LIST || v.type == VK_RAW ||
+        v.type == VK_READER)
+      continue;
+    vars.push_back(&v);
+  }
+  auto place = [&](const VarDesc* v, Tensor&& host) {
+    Variable* var = scope->Var(v->name);
+    var->kind = v->type;
+    var->tensor = device >= 0 ? host.to(device, stream) : std::move(host);
+  };
+  if (!combined_file.empty()) {
+    // save_combine writes the variables sorted by name (fluid/io.py save_vars)
+    std::sort(vars.begin(), vars.end(), [](const VarDesc* a, const VarDesc* b) { return a->name < b->name; });
+    FILE* f = fopen(combined_file.c_str(), "rb");
+    PA_CHECK(f != nullptr, "cannot open params file %s", combined_file.c_str());
+    try {
+      for (const VarDesc* v : vars) {
+        Tensor t;
+        PA_CHECK(read_lod_tensor(f, &t), "params file %s ends before %s", combined_file.c_str(), v->name.c_str());
+        place(v, std::move(t));
+      }
+    } catch (...) {
+      fclose(f);
+      throw;
+    }
+    fclose(f);
+  } else {
+    for (const VarDesc* v : vars) {
+      const std::string path = dir + "/" + v->name;
+      FILE* f = fopen(path.c_str(), "rb");
+      PA_CHECK(f != nullptr, "cannot open parameter file %s", path.c_str());
+      Tensor t;
+      bool ok = false;
+      try {
+        ok = read_lod_tensor(f, &t);
+      } catch (...) {
+        fclose(f);
+        throw;
+      }
+      fclose(f);
+      PA_CHECK(ok, "empty parameter file %s", path.c_str());
+      place(v, std::move(t));
+    }
+  }
+  if (device >= 0) device_stream_sync(stream);
+}
+
+}  // namespace pa

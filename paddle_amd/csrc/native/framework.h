@@ -1,0 +1,253 @@
+// Native C++ executor core: ProgramDesc (decoded from the wire format of the
+// reference's framework.proto), tensors, scopes, the op-kernel registry and the
+// block executor.  No Python, no torch: a C++ program links libpaddle_amd_native.so
+// and runs saved programs (inference models, the training demo) directly.
+//
+// Reference parity: framework/{program_desc,block_desc,op_desc,var_desc}.h (desc
+// objects), framework/{tensor,lod_tensor,scope,variable}.h, framework/executor.cc:125
+// (Executor::Run: create block vars, run ops in order), op_registry.h (kernel lookup
+// by op type + place).
+//
+// MI355X-first: tensors carry a device id (-1 = host); device tensors live in HBM
+// (hipMalloc) and device kernels run on one HIP stream per executor context
+// (ops_gpu.hip).  Host kernels run on a persistent worker pool (parallel_for).
+#pragma once
+
+#include <stdint.h>
+
+#include <atomic>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace pa {
+
+// ---------------------------------------------------------------- errors
+struct Error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+[[noreturn]] void fail(const char* fmt, ...);
+#define PA_CHECK(cond, ...) \
+  do {                      \
+    if (!(cond)) ::pa::fail(__VA_ARGS__); \
+  } while (0)
+
+// ---------------------------------------------------------------- dtypes
+// VarType.Type values of framework.proto
+enum class DT : int {
+  BOOL = 0, INT16 = 1, INT32 = 2, INT64 = 3, FP16 = 4, FP32 = 5, FP64 = 6,
+  UINT8 = 20, INT8 = 21, BF16 = 22,
+};
+size_t dt_size(DT t);
+const char* dt_name(DT t);
+
+// ---------------------------------------------------------------- program desc
+enum AttrType { A_INT = 0, A_FLOAT, A_STRING, A_INTS, A_FLOATS, A_STRINGS, A_BOOLEAN, A_BOOLEANS,
+                A_BLOCK, A_LONG, A_BLOCKS };
+
+struct Attr {
+  std::string name;
+  int type = A_INT;
+  int64_t i = 0;  // INT / LONG / BOOLEAN / BLOCK
+  float f = 0.f;
+  std::string s;
+  std::vector<int64_t> ints;  // INTS / BOOLEANS / BLOCKS
+  std::vector<float> floats;
+  std::vector<std::string> strings;
+};
+
+// VarType.Type values that are not tensors
+enum VarKind { VK_LOD_TENSOR = 7, VK_SELECTED_ROWS = 8, VK_FEED_MINIBATCH = 9, VK_FETCH_LIST = 10,
+               VK_STEP_SCOPES = 11, VK_LOD_TENSOR_ARRAY = 13, VK_READER = 15, VK_RAW = 17 };
+
+struct VarDesc {
+  std::string name;
+  int type = VK_LOD_TENSOR;
+  DT dtype = DT::FP32;
+  std::vector<int64_t> dims;
+  int lod_level = 0;
+  bool persistable = false;
+};
+
+struct OpDesc {
+  std::string type;
+  std::vector<std::pair<std::string, std::vector<std::string>>> inputs, outputs;
+  std::map<std::string, Attr> attrs;
+
+  const std::vector<std::string>& Inputs(const std::string& slot) const;
+  const std::vector<std::string>& Outputs(const std::string& slot) const;
+  std::string Input(const std::string& slot) const;   // first argument or ""
+  std::string Output(const std::string& slot) const;  // first argument or ""
+  bool Has(const std::string& a) const { return attrs.count(a) != 0; }
+  int64_t GetInt(const std::string& a, int64_t def = 0) const;
+  float GetFloat(const std::string& a, float def = 0.f) const;
+  bool GetBool(const std::string& a, bool def = false) const;
+  std::string GetString(const std::string& a, const std::string& def = "") const;
+  std::vector<int64_t> GetInts(const std::string& a) const;
+  std::vector<float> GetFloats(const std::string& a) const;
+};
+
+struct BlockDesc {
+  int idx = 0, parent_idx = -1, forward_block_idx = -1;
+  std::vector<VarDesc> vars;
+  std::vector<OpDesc> ops;
+  const VarDesc* FindVar(const std::string& n) const;
+};
+
+struct ProgramDesc {
+  std::vector<BlockDesc> blocks;
+  // Decodes a serialized ProgramDesc (proto2 wire format); throws pa::Error on
+  // malformed input (the file is untrusted: every length is bounds-checked).
+  static ProgramDesc Parse(const std::string& bytes);
+  static ProgramDesc Load(const std::string& path);
+  const BlockDesc& Block(int i) const { return blocks.at(i); }
+};
+
+// ---------------------------------------------------------------- tensors
+struct Buffer {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  int device = -1;
+  Buffer(size_t n, int dev);
+  ~Buffer();
+  Buffer(const Buffer&) = delete;
+  Buffer& operator=(const Buffer&) = delete;
+};
+
+using LoD = std::vector<std::vector<size_t>>;
+
+struct Tensor {
+  DT dtype = DT::FP32;
+  std::vector<int64_t> dims;
+  LoD lod;
+  std::shared_ptr<Buffer> buf;
+  int device = -1;
+
+  int64_t numel() const;
+  size_t nbytes() const { return (size_t)numel() * dt_size(dtype); }
+  bool initialized() const { return buf != nullptr; }
+  void* raw() const { return buf ? buf->ptr : nullptr; }
+  template <class T> T* data() const { return static_cast<T*>(raw()); }
+  // (Re)allocates when the existing buffer is too small or on another device;
+  // keeps the buffer otherwise (steady-state runs reuse their memory).
+  void* alloc(DT t, const std::vector<int64_t>& d, int dev);
+  template <class T> T* alloc(const std::vector<int64_t>& d, int dev);
+  void share(const Tensor& o) { *this = o; }  // same buffer, own dims/lod copies
+  Tensor to(int dev, void* stream = nullptr) const;
+  std::string shape_str() const;
+};
+
+// ---------------------------------------------------------------- variables / scopes
+struct Variable {
+  int kind = VK_LOD_TENSOR;
+  Tensor tensor;
+  std::vector<Tensor> list;  // FEED_MINIBATCH / FETCH_LIST / LOD_TENSOR_ARRAY
+};
+
+class Scope {
+ public:
+  explicit Scope(const Scope* parent = nullptr) : parent_(parent) {}
+  Variable* Var(const std::string& name);           // find or create locally
+  Variable* Find(const std::string& name) const;    // walks up the parents
+  Variable* FindLocal(const std::string& name) const;
+  Scope& NewScope();
+  void Erase(const std::string& name);
+  std::vector<std::string> LocalNames() const;
+  const Scope* parent() const { return parent_; }
+
+ private:
+  const Scope* parent_;
+  std::unordered_map<std::string, std::unique_ptr<Variable>> vars_;
+  std::vector<std::unique_ptr<Scope>> kids_;
+  mutable std::mutex mu_;
+};
+
+// ---------------------------------------------------------------- execution context
+struct ThreadPool;
+ThreadPool& host_pool();
+// Runs fn(begin, end) over [0, n) split across the host workers (serial when
+// n < grain).
+void parallel_for(int64_t n, int64_t grain, const std::function<void(int64_t, int64_t)>& fn);
+
+struct ExecContext {
+  int device = -1;        // -1 host, else HIP device id
+  void* stream = nullptr;  // hipStream_t of the device kernels
+  std::mt19937_64 rng{0x5eed};
+  bool is_test = false;   // inference predictor: force is_test semantics
+};
+
+struct OpRun {
+  const OpDesc& op;
+  Scope& scope;
+  ExecContext& ctx;
+  Tensor& in(const std::string& slot, size_t i = 0) const;
+  Tensor* in_opt(const std::string& slot, size_t i = 0) const;  // null if absent/uninitialised
+  std::vector<Tensor*> ins(const std::string& slot) const;
+  Tensor* out(const std::string& slot, size_t i = 0) const;      // null if the slot is empty
+  Variable* var(const std::string& name) const;
+};
+
+using Kernel = std::function<void(const OpRun&)>;
+// device < 0: host kernel; device >= 0: HIP kernel
+void register_kernel(const std::string& type, bool device, Kernel k);
+const Kernel* find_kernel(const std::string& type, bool device);
+std::vector<std::string> registered_ops(bool device);
+
+struct KernelRegistrar {
+  KernelRegistrar(const char* type, bool device, Kernel k) { register_kernel(type, device, std::move(k)); }
+};
+#define PA_HOST_KERNEL(name, fn) static ::pa::KernelRegistrar _pa_hk_##name(#name, false, fn)
+#define PA_DEVICE_KERNEL(name, fn) static ::pa::KernelRegistrar _pa_dk_##name(#name, true, fn)
+
+// forces the static registrars of every kernel translation unit to be linked
+void link_host_kernels();
+void link_device_kernels();
+
+// ---------------------------------------------------------------- executor
+class Executor {
+ public:
+  explicit Executor(int device = -1);
+  ~Executor();
+  // Executor::Run of the reference: creates the block's variables (persistables in
+  // `scope`, temporaries in `local` when given, else in `scope`) and runs the ops.
+  void Run(const ProgramDesc& prog, Scope* scope, int block_id = 0, Scope* local = nullptr);
+  void RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* scope);
+  ExecContext& context() { return ctx_; }
+  void Sync();  // waits for the device stream
+  // per-op wall time accumulation (the reference's kCPU profiler in the demo)
+  bool profile = false;
+  std::map<std::string, std::pair<int64_t, double>> op_time_ms;  // type -> (calls, ms)
+
+ private:
+  ExecContext ctx_;
+};
+
+// ---------------------------------------------------------------- tensor IO
+// LoDTensor stream (framework/lod_tensor.cc SerializeToStream): one tensor per
+// call; returns false at a clean end of stream.
+bool read_lod_tensor(FILE* f, Tensor* t);
+void write_lod_tensor(FILE* f, const Tensor& t);
+void load_persistables(const ProgramDesc& prog, Scope* scope, const std::string& dir,
+                       const std::string& combined_file, int device, void* stream);
+
+// ---------------------------------------------------------------- host math
+// C[M,N] = alpha * op(A) op(B) + beta * C, row-major, fp32, multithreaded.
+void sgemm(bool ta, bool tb, int64_t M, int64_t N, int64_t K, float alpha, const float* A, int64_t lda,
+           const float* B, int64_t ldb, float beta, float* C, int64_t ldc);
+
+// device helpers (ops_gpu.hip; no-ops that fail when built without HIP devices)
+void* device_alloc(size_t n, int dev);
+void device_free(void* p, int dev);
+void device_copy(void* dst, int dst_dev, const void* src, int src_dev, size_t n, void* stream);
+void* device_stream_create(int dev);
+void device_stream_destroy(void* s);
+void device_stream_sync(void* s);
+int device_count();
+
+}  // namespace pa

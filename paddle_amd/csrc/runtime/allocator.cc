@@ -35,6 +35,13 @@ struct Buddy {
   bool init_mem = false;
   std::vector<Arena> arenas;
   std::unordered_map<char*, std::pair<int, int>> live;  // ptr -> (arena, order)
+  // Large requests skip the power-of-two buddy (up to 2x waste at these sizes):
+  // they get exact-size blocks (2 MiB granularity) cached by size for reuse
+  // (reference buddy_allocator.cc: requests above max_chunk_size go straight to
+  // the system allocator).
+  size_t large = 32ull << 20;
+  std::multimap<size_t, char*> large_free;       // size -> block
+  std::unordered_map<char*, size_t> large_live;  // block -> size
   size_t used = 0, reserved = 0, peak = 0;
   std::mutex mu;
 
@@ -44,10 +51,7 @@ struct Buddy {
     return o;
   }
 
-  bool refill(int need_order) {
-    int o = order_for(chunk);
-    if (o < need_order) o = need_order;
-    size_t sz = 1ull << o;
+  char* sys_alloc(size_t sz) {
     char* p = nullptr;
     if (device >= 0) {
       int prev;
@@ -56,15 +60,59 @@ struct Buddy {
       hipError_t e = hipMalloc((void**)&p, sz);
       hipSetDevice(prev);
       if (e != hipSuccess) {
+        hipGetLastError();  // clear the sticky OOM so the caller can retry
         pa_rt_set_error("hipMalloc(%zu) failed: %d", sz, (int)e);
-        return false;
+        return nullptr;
       }
-    } else {
-      if (posix_memalign((void**)&p, 4096, sz) != 0) {
-        pa_rt_set_error("posix_memalign(%zu) failed", sz);
-        return false;
+    } else if (posix_memalign((void**)&p, 4096, sz) != 0) {
+      pa_rt_set_error("posix_memalign(%zu) failed", sz);
+      return nullptr;
+    }
+    return p;
+  }
+
+  void sys_free(char* p) {
+    if (device >= 0) hipFree(p);
+    else free(p);
+  }
+
+  // gives cached large blocks and wholly free arenas back to the system
+  bool trim() {
+    bool any = !large_free.empty();
+    for (auto& kv : large_free) {
+      sys_free(kv.second);
+      reserved -= kv.first;
+    }
+    large_free.clear();
+    for (size_t ai = 0; ai < arenas.size(); ++ai) {
+      Arena& a = arenas[ai];
+      if (a.base && a.free_by_order[a.order].count(0)) {
+        sys_free(a.base);
+        reserved -= 1ull << a.order;
+        a.base = nullptr;  // slot kept so live (arena index) entries stay valid
+        a.free_by_order.assign(a.order + 1, {});
+        any = true;
       }
     }
+    return any;
+  }
+
+  bool refill(int need_order) {
+    int o = order_for(chunk);
+    if (o < need_order) o = need_order;
+    size_t sz = 1ull << o;
+    char* p = sys_alloc(sz);
+    if (!p && trim()) p = sys_alloc(sz);
+    if (!p) return false;
+    for (auto& a : arenas)  // reuse a trimmed slot
+      if (!a.base) {
+        a.base = p;
+        a.order = o;
+        a.free_by_order.assign(o + 1, {});
+        a.free_by_order[o].insert(0);
+        reserved += sz;
+        return true;
+      }
     Arena a;
     a.base = p;
     a.order = o;
@@ -75,12 +123,37 @@ struct Buddy {
     return true;
   }
 
+  void* alloc_large(size_t n) {
+    const size_t sz = (n + (2ull << 20) - 1) & ~((2ull << 20) - 1);
+    // best fit within 1/8 slack
+    auto it = large_free.lower_bound(sz);
+    if (it != large_free.end() && it->first <= sz + sz / 8) {
+      char* p = it->second;
+      const size_t have = it->first;
+      large_free.erase(it);
+      large_live[p] = have;
+      used += have;
+      if (used > peak) peak = used;
+      return p;
+    }
+    char* p = sys_alloc(sz);
+    if (!p && trim()) p = sys_alloc(sz);
+    if (!p) return nullptr;
+    reserved += sz;
+    large_live[p] = sz;
+    used += sz;
+    if (used > peak) peak = used;
+    return p;
+  }
+
   void* alloc(size_t n) {
     std::lock_guard<std::mutex> g(mu);
+    if (n >= large) return alloc_large(n);
     int want = order_for(n ? n : 1);
     for (int pass = 0; pass < 2; ++pass) {
       for (size_t ai = 0; ai < arenas.size(); ++ai) {
         Arena& a = arenas[ai];
+        if (!a.base) continue;
         for (int o = want; o <= a.order; ++o) {
           if (a.free_by_order[o].empty()) continue;
           size_t off = *a.free_by_order[o].begin();
@@ -104,6 +177,13 @@ struct Buddy {
 
   int release(void* ptr) {
     std::lock_guard<std::mutex> g(mu);
+    auto lg = large_live.find((char*)ptr);
+    if (lg != large_live.end()) {
+      used -= lg->second;
+      large_free.emplace(lg->second, lg->first);
+      large_live.erase(lg);
+      return 0;
+    }
     auto it = live.find((char*)ptr);
     if (it == live.end()) {
       pa_rt_set_error("free of unknown pointer");
@@ -127,10 +207,10 @@ struct Buddy {
   }
 
   ~Buddy() {
-    for (auto& a : arenas) {
-      if (device >= 0) hipFree(a.base);
-      else free(a.base);
-    }
+    for (auto& a : arenas)
+      if (a.base) sys_free(a.base);
+    for (auto& kv : large_free) sys_free(kv.second);
+    for (auto& kv : large_live) sys_free(kv.first);
   }
 };
 

@@ -1,86 +1,81 @@
-// C++ training driver (reference paddle/fluid/train/demo/demo_trainer.cc).
+// C++ training driver on the native executor (reference
+// paddle/fluid/train/demo/demo_trainer.cc): load the serialized startup / main
+// ProgramDescs, initialise the parameters, own the input tensors, run the training
+// program step by step and report the loss and a per-op time profile.  Links
+// libpaddle_amd_native.so only -- no Python interpreter.
 //
-// Loads serialized startup / main ProgramDescs, initialises the parameters, owns
-// the input buffers and runs the training loop from C++.  The executor, the op
-// kernels and the gfx950 kernel library are reached through the embedded
-// interpreter (paddle_amd.train_demo.DemoTrainer): this framework's executor is
-// Python over native kernels, so a C++ host embeds it instead of linking a C++
-// executor.
+//   demo_trainer <model_dir> [steps] [params_dir] [device]
 //
-//   demo_trainer <model_dir> [steps] [gpu]
-#include <Python.h>
+// params_dir (optional, "-" for none): LoDTensor files overriding the startup
+// initialisation (used by the tests to start from the Python executor's weights).
+// device >= 0 runs the device kernels on that HIP device.
+#include <stdio.h>
+#include <stdlib.h>
 
+#include <algorithm>
 #include <chrono>
-#include <cstdio>
-#include <cstdlib>
 #include <string>
 #include <vector>
 
-namespace {
-
-[[noreturn]] void die(const char* what) {
-  std::fprintf(stderr, "demo_trainer: %s\n", what);
-  if (PyErr_Occurred()) PyErr_Print();
-  std::exit(1);
-}
-
-PyObject* call(PyObject* obj, const char* method, PyObject* args) {
-  PyObject* fn = PyObject_GetAttrString(obj, method);
-  if (!fn) die(method);
-  PyObject* r = PyObject_CallObject(fn, args);
-  Py_DECREF(fn);
-  Py_XDECREF(args);
-  if (!r) die(method);
-  return r;
-}
-
-void set_input(PyObject* trainer, const char* name, const std::vector<float>& buf, long rows, long cols) {
-  PyObject* mem = PyMemoryView_FromMemory(reinterpret_cast<char*>(const_cast<float*>(buf.data())),
-                                          static_cast<Py_ssize_t>(buf.size() * sizeof(float)), PyBUF_READ);
-  PyObject* shape = Py_BuildValue("(ll)", rows, cols);
-  PyObject* r = call(trainer, "set_input", Py_BuildValue("(sNN)", name, mem, shape));
-  Py_DECREF(r);
-}
-
-}  // namespace
+#include "framework.h"
 
 int main(int argc, char** argv) {
   if (argc < 2) {
-    std::fprintf(stderr, "usage: %s <model_dir> [steps] [gpu]\n", argv[0]);
+    fprintf(stderr, "usage: %s <model_dir> [steps] [params_dir] [device]\n", argv[0]);
     return 2;
   }
-  const std::string model_dir = argv[1];
-  const int steps = argc > 2 ? std::atoi(argv[2]) : 10;
-  const int use_gpu = argc > 3 ? std::atoi(argv[3]) : 0;
+  const std::string dir = argv[1];
+  const int steps = argc > 2 ? atoi(argv[2]) : 10;
+  const std::string params = argc > 3 ? argv[3] : "-";
+  const int device = argc > 4 ? atoi(argv[4]) : -1;
+  try {
+    const pa::ProgramDesc startup = pa::ProgramDesc::Load(dir + "/startup_program");
+    const pa::ProgramDesc main_prog = pa::ProgramDesc::Load(dir + "/main_program");
+    std::string loss_name;
+    for (const pa::OpDesc& op : main_prog.Block(0).ops)
+      if (op.type == "mean") {
+        loss_name = op.Output("Out");
+        break;
+      }
+    if (loss_name.empty()) {
+      fprintf(stderr, "demo_trainer: no mean op (loss) in the main program\n");
+      return 1;
+    }
+    // the demo network's ops are host kernels; `device` places the tensors in HBM
+    // and runs whatever has a device kernel there
+    pa::Executor exe(device);
+    pa::Scope scope;
+    exe.Run(startup, &scope, 0);
+    if (params != "-") pa::load_persistables(main_prog, &scope, params, "", device, exe.context().stream);
 
-  Py_Initialize();
-  PyObject* mod = PyImport_ImportModule("paddle_amd.train_demo");
-  if (!mod) die("import paddle_amd.train_demo");
-  PyObject* cls = PyObject_GetAttrString(mod, "DemoTrainer");
-  if (!cls) die("DemoTrainer");
-  PyObject* trainer = PyObject_CallFunction(cls, "si", model_dir.c_str(), use_gpu);
-  if (!trainer) die("DemoTrainer(model_dir)");
-  Py_DECREF(call(trainer, "run_startup", nullptr));
+    // inputs: x [2, 13] = 0..25, y [2, 1] = 0..1 (as the reference demo)
+    pa::Tensor x, y;
+    float* xp = x.alloc<float>({2, 13}, -1);
+    for (int i = 0; i < 26; ++i) xp[i] = (float)i;
+    float* yp = y.alloc<float>({2, 1}, -1);
+    for (int i = 0; i < 2; ++i) yp[i] = (float)i;
+    scope.Var("x")->tensor = device >= 0 ? x.to(device) : x;
+    scope.Var("y")->tensor = device >= 0 ? y.to(device) : y;
 
-  // prepare data: x [2, 13] = 0..25, y [2, 1] = 0..1 (as the reference demo)
-  std::vector<float> x(2 * 13), y(2);
-  for (int i = 0; i < 2 * 13; ++i) x[i] = static_cast<float>(i);
-  for (int i = 0; i < 2; ++i) y[i] = static_cast<float>(i);
-  set_input(trainer, "x", x, 2, 13);
-  set_input(trainer, "y", y, 2, 1);
-
-  const auto t0 = std::chrono::steady_clock::now();
-  for (int i = 0; i < steps; ++i) {
-    PyObject* loss = call(trainer, "step", nullptr);
-    std::printf("step: %d loss: %.6f\n", i, PyFloat_AsDouble(loss));
-    Py_DECREF(loss);
+    exe.profile = true;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < steps; ++i) {
+      exe.Run(main_prog, &scope, 0);
+      pa::Tensor loss = scope.Find(loss_name)->tensor;
+      if (loss.device >= 0) loss = loss.to(-1, exe.context().stream);
+      printf("step: %d loss: %.9g\n", i, loss.data<float>()[0]);
+    }
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    printf("run_time_ms = %.3f\n", ms);
+    // profiler summary sorted by total time (reference: DisableProfiler(kTotal, ...))
+    std::vector<std::pair<std::string, std::pair<int64_t, double>>> rows(exe.op_time_ms.begin(), exe.op_time_ms.end());
+    std::sort(rows.begin(), rows.end(), [](auto& a, auto& b) { return a.second.second > b.second.second; });
+    printf("%-28s %8s %12s\n", "op", "calls", "total_ms");
+    for (auto& r : rows) printf("%-28s %8lld %12.4f\n", r.first.c_str(), (long long)r.second.first, r.second.second);
+    fflush(stdout);
+  } catch (const std::exception& e) {
+    fprintf(stderr, "demo_trainer: %s\n", e.what());
+    return 1;
   }
-  const double ms =
-      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  std::printf("run_time_ms = %.3f\n", ms);
-  std::fflush(stdout);
-  Py_DECREF(trainer);
-  Py_DECREF(cls);
-  Py_DECREF(mod);
-  return Py_FinalizeEx() < 0 ? 1 : 0;
+  return 0;
 }

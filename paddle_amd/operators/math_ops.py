@@ -190,7 +190,16 @@ def _ew_grad(name, dx_fn, dy_fn):
         if ctx.has_output("X@GRAD"):
             ctx.set_output("X@GRAD", _reduce_to(dx_fn(x, yb, d), x.shape), ctx.input_lod("X"))
         if ctx.has_output("Y@GRAD"):
-            ctx.set_output("Y@GRAD", _reduce_to(dy_fn(x, yb, d), y.shape).to(y.dtype))
+            # sum over the dims Y was broadcast along, in Y's aligned (op-axis) layout;
+            # matching Y's raw shape against the gradient instead is ambiguous when two
+            # dims have Y's size (bias [16] of a [16, 16] activation)
+            g = dy_fn(x, yb, d)
+            if g.dim() == yb.dim():
+                dims = [i for i in range(g.dim()) if yb.shape[i] == 1 and g.shape[i] != 1]
+                g = g.sum(dim=dims, keepdim=True) if dims else g
+                ctx.set_output("Y@GRAD", g.reshape(y.shape).to(y.dtype))
+            else:
+                ctx.set_output("Y@GRAD", _reduce_to(g, y.shape).to(y.dtype))
 
 
 class _NativeGradCtx:

@@ -221,6 +221,26 @@ def test_buddy_allocator_host():
     assert a.stats()["arenas"] == 1
 
 
+def test_buddy_allocator_large_blocks_exact_size_reuse():
+    """Requests >= 32 MiB bypass the power-of-two buddy: 2 MiB-granular exact
+    blocks (no 2x rounding waste), reused best-fit within 1/8 slack after free."""
+    if not runtime.available():
+        pytest.skip("native runtime not built")
+    a = runtime.BuddyAllocator(device=-1, chunk_bytes=1 << 20)
+    p = a.alloc(40 << 20)
+    st = a.stats()
+    assert st["used"] == 40 << 20 and st["reserved"] == 40 << 20  # not 64 MiB
+    a.free(p)
+    assert a.stats()["used"] == 0
+    q = a.alloc(39 << 20)  # fits the cached 40 MiB block
+    assert q == p and a.stats()["reserved"] == 40 << 20
+    r = a.alloc(100 << 20)  # too large for any cached block: a new one
+    assert r not in (p, q)
+    a.free(q)
+    a.free(r)
+    assert a.stats()["used"] == 0
+
+
 def test_native_profiler(tmp_path):
     if not runtime.available():
         pytest.skip("native runtime not built")

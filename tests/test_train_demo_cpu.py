@@ -1,14 +1,15 @@
-"""C++ training demo (reference paddle/fluid/train/demo): build the C++ driver with
-the embedded interpreter, save the demo programs, train from C++ and see the
-loss fall."""
+"""C++ training demo (reference paddle/fluid/train/demo): the driver links the
+native executor (libpaddle_amd_native.so, no Python), trains the demo network from
+its own startup initialisation and the loss falls.  The trajectory match against
+the Python executor is tests/test_native_cpu.py::test_cpp_demo_trainer_matches_python."""
 import os
 import re
 import shutil
 import subprocess
-import sys
-import sysconfig
 
 import pytest
+
+from paddle_amd import _build
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -19,17 +20,13 @@ def test_cpp_demo_trainer(tmp_path):
 
     model = tmp_path / "model"
     save_demo_programs(str(model))
-    exe = tmp_path / "demo_trainer"
-    inc = sysconfig.get_paths()["include"]
-    libdir = sysconfig.get_config_var("LIBDIR")
-    ver = sysconfig.get_config_var("LDVERSION")
-    src = os.path.join(ROOT, "paddle_amd", "csrc", "train_demo", "demo_trainer.cc")
-    subprocess.run(["g++", "-O2", "-std=c++17", src, f"-I{inc}", f"-L{libdir}", f"-lpython{ver}",
-                    f"-Wl,-rpath,{libdir}", "-o", str(exe)], check=True, timeout=120)
-    env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""),
-               PYTHONHOME=sys.base_prefix)
-    out = subprocess.run([str(exe), str(model), "20"], capture_output=True, text=True, timeout=300, env=env)
+    exe = _build.build_native_program(os.path.join(ROOT, "paddle_amd", "csrc", "train_demo", "demo_trainer.cc"),
+                                      str(tmp_path / "demo_trainer"))
+    out = subprocess.run([exe, str(model), "20"], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     losses = [float(m) for m in re.findall(r"loss: ([0-9.eE+-]+)", out.stdout)]
     assert len(losses) == 20 and losses[-1] < losses[0], out.stdout
     assert "run_time_ms" in out.stdout
+    # the binary is a native program: no libpython in its dependencies
+    ldd = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout
+    assert "libpython" not in ldd and "libpaddle_amd_native" in ldd
