@@ -40,8 +40,15 @@ struct Buddy {
   // (reference buddy_allocator.cc: requests above max_chunk_size go straight to
   // the system allocator).
   size_t large = 32ull << 20;
-  std::multimap<size_t, char*> large_free;       // size -> block
-  std::unordered_map<char*, size_t> large_live;  // block -> size
+  struct Blk {
+    size_t size;
+    int seg;
+    bool free;
+  };
+  std::map<char*, Blk> blocks;                  // every large block by address
+  std::set<std::pair<size_t, char*>> free_set;  // free large blocks by (size, address)
+  std::vector<std::pair<char*, size_t>> segs;   // large segments (base, size); base null once trimmed
+  size_t seg_min = 1ull << 30;                  // segments of at least 1 GiB (exact for larger requests)
   size_t used = 0, reserved = 0, peak = 0;
   std::mutex mu;
 
@@ -60,7 +67,7 @@ struct Buddy {
       hipError_t e = hipMalloc((void**)&p, sz);
       hipSetDevice(prev);
       if (e != hipSuccess) {
-        hipGetLastError();  // clear the sticky OOM so the caller can retry
+        (void)hipGetLastError();  // clear the sticky OOM so the caller can retry
         pa_rt_set_error("hipMalloc(%zu) failed: %d", sz, (int)e);
         return nullptr;
       }
@@ -76,14 +83,21 @@ struct Buddy {
     else free(p);
   }
 
-  // gives cached large blocks and wholly free arenas back to the system
+  // gives wholly free large segments and arenas back to the system
   bool trim() {
-    bool any = !large_free.empty();
-    for (auto& kv : large_free) {
-      sys_free(kv.second);
-      reserved -= kv.first;
+    bool any = false;
+    for (size_t si = 0; si < segs.size(); ++si) {
+      char* base = segs[si].first;
+      if (!base) continue;
+      auto it = blocks.find(base);
+      if (it == blocks.end() || !it->second.free || it->second.size != segs[si].second) continue;
+      free_set.erase({it->second.size, base});
+      blocks.erase(it);
+      sys_free(base);
+      reserved -= segs[si].second;
+      segs[si].first = nullptr;
+      any = true;
     }
-    large_free.clear();
     for (size_t ai = 0; ai < arenas.size(); ++ai) {
       Arena& a = arenas[ai];
       if (a.base && a.free_by_order[a.order].count(0)) {
@@ -123,27 +137,66 @@ struct Buddy {
     return true;
   }
 
+  // Large pool: best-fit over free blocks of the segments, split on allocation,
+  // coalesced with free neighbours of the same segment on release (the
+  // reference buddy_allocator.cc pool semantics, at 512-B granularity).
   void* alloc_large(size_t n) {
-    const size_t sz = (n + (2ull << 20) - 1) & ~((2ull << 20) - 1);
-    // best fit within 1/8 slack
-    auto it = large_free.lower_bound(sz);
-    if (it != large_free.end() && it->first <= sz + sz / 8) {
-      char* p = it->second;
-      const size_t have = it->first;
-      large_free.erase(it);
-      large_live[p] = have;
-      used += have;
-      if (used > peak) peak = used;
-      return p;
+    const size_t sz = (n + 511) & ~(size_t)511;
+    auto it = free_set.lower_bound({sz, nullptr});
+    if (it == free_set.end()) {
+      size_t seg_sz = std::max<size_t>(seg_min, (sz + (2ull << 20) - 1) & ~((size_t)(2ull << 20) - 1));
+      char* base = sys_alloc(seg_sz);
+      if (!base && trim()) base = sys_alloc(seg_sz);
+      if (!base && seg_sz > sz) {  // no room for a full segment: an exact one
+        seg_sz = sz;
+        base = sys_alloc(seg_sz);
+      }
+      if (!base) return nullptr;
+      segs.push_back({base, seg_sz});
+      reserved += seg_sz;
+      blocks[base] = {seg_sz, (int)segs.size() - 1, true};
+      it = free_set.insert({seg_sz, base}).first;
     }
-    char* p = sys_alloc(sz);
-    if (!p && trim()) p = sys_alloc(sz);
-    if (!p) return nullptr;
-    reserved += sz;
-    large_live[p] = sz;
-    used += sz;
+    char* p = it->second;
+    Blk b = blocks[p];
+    free_set.erase(it);
+    if (b.size - sz >= (1ull << 20)) {  // split: remainder stays free
+      char* rest = p + sz;
+      blocks[rest] = {b.size - sz, b.seg, true};
+      free_set.insert({b.size - sz, rest});
+      b.size = sz;
+    }
+    b.free = false;
+    blocks[p] = b;
+    used += b.size;
     if (used > peak) peak = used;
     return p;
+  }
+
+  bool release_large(char* p) {
+    auto it = blocks.find(p);
+    if (it == blocks.end() || it->second.free) return false;
+    used -= it->second.size;
+    it->second.free = true;
+    // merge with the next block of the same segment
+    auto nx = std::next(it);
+    if (nx != blocks.end() && nx->second.free && nx->second.seg == it->second.seg && it->first + it->second.size == nx->first) {
+      free_set.erase({nx->second.size, nx->first});
+      it->second.size += nx->second.size;
+      blocks.erase(nx);
+    }
+    // merge into the previous block of the same segment
+    if (it != blocks.begin()) {
+      auto pv = std::prev(it);
+      if (pv->second.free && pv->second.seg == it->second.seg && pv->first + pv->second.size == it->first) {
+        free_set.erase({pv->second.size, pv->first});
+        pv->second.size += it->second.size;
+        blocks.erase(it);
+        it = pv;
+      }
+    }
+    free_set.insert({it->second.size, it->first});
+    return true;
   }
 
   void* alloc(size_t n) {
@@ -177,13 +230,7 @@ struct Buddy {
 
   int release(void* ptr) {
     std::lock_guard<std::mutex> g(mu);
-    auto lg = large_live.find((char*)ptr);
-    if (lg != large_live.end()) {
-      used -= lg->second;
-      large_free.emplace(lg->second, lg->first);
-      large_live.erase(lg);
-      return 0;
-    }
+    if (release_large((char*)ptr)) return 0;
     auto it = live.find((char*)ptr);
     if (it == live.end()) {
       pa_rt_set_error("free of unknown pointer");
@@ -209,53 +256,28 @@ struct Buddy {
   ~Buddy() {
     for (auto& a : arenas)
       if (a.base) sys_free(a.base);
-    for (auto& kv : large_free) sys_free(kv.second);
-    for (auto& kv : large_live) sys_free(kv.first);
+    for (auto& sg : segs)
+      if (sg.first) sys_free(sg.first);
   }
 };
 
 std::mutex g_mu;
-std::map<int, Buddy*> g_torch;  // device -> allocator used by the torch hook
 size_t g_torch_chunk = 4ull << 30;
+// Torch hook pools: one allocator per (device, stream).  torch's pluggable
+// allocator frees a block with the stream it was allocated on, and a block only
+// ever returns to its own stream's pool, so reuse is ordered by that stream and a
+// free needs no event or host synchronisation (cross-stream users must order
+// themselves, as with record_stream on torch's caching allocator).
+std::map<std::pair<int, hipStream_t>, Buddy*> g_torch;
 
-// Stream-ordered release for the torch hook: a freed block may still be read by
-// kernels queued on its stream, so free() records an event there and the block
-// returns to the buddy pool once the event has completed (polled on the next
-// allocation; all pending events are waited for only when an allocation would
-// otherwise fail) -- no host synchronisation on the free path.
-struct Pending {
-  void* ptr;
-  hipEvent_t ev;
-};
-std::map<int, std::vector<Pending>> g_pending;
-std::vector<hipEvent_t> g_event_pool;
-
-hipEvent_t take_event() {
-  if (!g_event_pool.empty()) {
-    hipEvent_t e = g_event_pool.back();
-    g_event_pool.pop_back();
-    return e;
+Buddy* torch_pool(int device, hipStream_t s) {
+  auto& b = g_torch[{device, s}];
+  if (!b) {
+    b = new Buddy();
+    b->device = device;
+    b->chunk = g_torch_chunk;
   }
-  hipEvent_t e = nullptr;
-  hipEventCreateWithFlags(&e, hipEventDisableTiming);
-  return e;
-}
-
-// caller holds g_mu; wait == true blocks on every pending event
-void drain(int device, Buddy* b, bool wait) {
-  auto& pend = g_pending[device];
-  size_t keep = 0;
-  for (size_t i = 0; i < pend.size(); ++i) {
-    Pending& q = pend[i];
-    const hipError_t st = wait ? hipEventSynchronize(q.ev) : hipEventQuery(q.ev);
-    if (st == hipSuccess) {
-      b->release(q.ptr);
-      g_event_pool.push_back(q.ev);
-    } else {
-      pend[keep++] = q;
-    }
-  }
-  pend.resize(keep);
+  return b;
 }
 }  // namespace
 
@@ -283,48 +305,39 @@ PA_RT_EXPORT void pa_buddy_stats(void* h, size_t* used, size_t* reserved, size_t
 // ---- torch CUDAPluggableAllocator hooks (HIP build of torch uses hipStream_t)
 PA_RT_EXPORT void pa_torch_set_chunk(size_t bytes) { g_torch_chunk = bytes; }
 
-PA_RT_EXPORT void* pa_torch_malloc(ssize_t size, int device, hipStream_t) {
+PA_RT_EXPORT void* pa_torch_malloc(ssize_t size, int device, hipStream_t stream) {
   std::lock_guard<std::mutex> g(g_mu);
-  Buddy* b;
-  auto it = g_torch.find(device);
-  if (it == g_torch.end()) {
-    b = new Buddy();
-    b->device = device;
-    b->chunk = g_torch_chunk;
-    g_torch[device] = b;
-  } else {
-    b = it->second;
-  }
-  drain(device, b, false);
+  Buddy* b = torch_pool(device, stream);
   void* p = b->alloc((size_t)size);
-  if (!p && !g_pending[device].empty()) {  // blocks still in flight: wait for them, retry
-    drain(device, b, true);
+  if (!p) {  // out of memory: return other streams' wholly free segments, retry
+    for (auto& kv : g_torch)
+      if (kv.first.first == device && kv.second != b) {
+        std::lock_guard<std::mutex> gb(kv.second->mu);
+        kv.second->trim();
+      }
     p = b->alloc((size_t)size);
   }
   return p;
 }
 
 PA_RT_EXPORT void pa_torch_free(void* ptr, ssize_t, int device, hipStream_t stream) {
+  if (!ptr) return;
   std::lock_guard<std::mutex> g(g_mu);
-  auto it = g_torch.find(device);
-  if (it == g_torch.end() || !ptr) return;
-  hipEvent_t ev = take_event();
-  if (ev && hipEventRecord(ev, stream) == hipSuccess) {
-    g_pending[device].push_back({ptr, ev});
-  } else {  // no event: fall back to a synchronous release
-    if (ev) g_event_pool.push_back(ev);
-    if (stream) hipStreamSynchronize(stream);
-    it->second->release(ptr);
-  }
+  auto it = g_torch.find({device, stream});
+  if (it != g_torch.end() && it->second->release(ptr) == 0) return;
+  for (auto& kv : g_torch)  // defensive: a block freed with another stream
+    if (kv.first.first == device && kv.second->release(ptr) == 0) return;
 }
 
 PA_RT_EXPORT void pa_torch_stats(int device, size_t* used, size_t* reserved, size_t* peak) {
   std::lock_guard<std::mutex> g(g_mu);
-  auto it = g_torch.find(device);
-  if (it == g_torch.end()) {
-    *used = *reserved = *peak = 0;
-    return;
-  }
-  size_t n;
-  pa_buddy_stats(it->second, used, reserved, peak, &n);
+  *used = *reserved = *peak = 0;
+  for (auto& kv : g_torch)
+    if (kv.first.first == device) {
+      size_t u, r, pk, n;
+      pa_buddy_stats(kv.second, &u, &r, &pk, &n);
+      *used += u;
+      *reserved += r;
+      *peak += pk;  // sum of per-stream peaks (an upper bound of the joint peak)
+    }
 }

@@ -1,7 +1,7 @@
 """The native buddy allocator installed behind torch (FLAGS_allocator_strategy=buddy,
 csrc/runtime/allocator.cc pa_torch_malloc / pa_torch_free) carries a full
 LLaMA-tiny training run on the framework tape: same losses as torch's caching
-allocator, blocks come from the buddy arenas, stream-ordered frees drain.
+allocator, blocks come from the buddy pools and frees return them.
 
 Reference: memory/detail/buddy_allocator.cc + memory/malloc.cc (the reference's
 only device allocator); its tests (buddy_allocator_test / malloc_test) exercise

@@ -221,24 +221,27 @@ def test_buddy_allocator_host():
     assert a.stats()["arenas"] == 1
 
 
-def test_buddy_allocator_large_blocks_exact_size_reuse():
-    """Requests >= 32 MiB bypass the power-of-two buddy: 2 MiB-granular exact
-    blocks (no 2x rounding waste), reused best-fit within 1/8 slack after free."""
+def test_buddy_allocator_large_pool_best_fit():
+    """Requests >= 32 MiB bypass the power-of-two buddy: they are carved best-fit
+    out of >= 1 GiB segments at 512-B granularity (no 2x rounding waste), split
+    on allocation and coalesced on release."""
     if not runtime.available():
         pytest.skip("native runtime not built")
     a = runtime.BuddyAllocator(device=-1, chunk_bytes=1 << 20)
-    p = a.alloc(40 << 20)
+    mb = 1 << 20
+    p = a.alloc(40 * mb)
     st = a.stats()
-    assert st["used"] == 40 << 20 and st["reserved"] == 40 << 20  # not 64 MiB
+    assert st["used"] == 40 * mb and st["reserved"] == 1 << 30  # one segment, exact block
+    q = a.alloc(100 * mb)
+    assert q == p + 40 * mb  # split from the same segment
     a.free(p)
-    assert a.stats()["used"] == 0
-    q = a.alloc(39 << 20)  # fits the cached 40 MiB block
-    assert q == p and a.stats()["reserved"] == 40 << 20
-    r = a.alloc(100 << 20)  # too large for any cached block: a new one
-    assert r not in (p, q)
-    a.free(q)
+    r = a.alloc(39 * mb)
+    assert r == p  # best fit: the 40 MiB hole, not the large tail
     a.free(r)
+    a.free(q)
     assert a.stats()["used"] == 0
+    assert a.alloc(900 * mb) == p  # the segment coalesced back into one free block
+    assert a.stats()["reserved"] == 1 << 30
 
 
 def test_native_profiler(tmp_path):
