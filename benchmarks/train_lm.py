@@ -56,6 +56,7 @@ def main():
     ap.add_argument("--grouped-experts", action="store_true", help="MoE experts as ragged grouped GEMMs")
     ap.add_argument("--bucket-mb", type=int, default=512)
     ap.add_argument("--accum", type=int, default=1, help="gradient accumulation micro-steps per optimizer step")
+    ap.add_argument("--bf16-grads", action="store_true", help="bf16 gradient buffer instead of fp32 main_grad")
     a = ap.parse_args()
 
     from paddle_amd.parallel import comm
@@ -66,7 +67,7 @@ def main():
     torch.manual_seed(1234)
     model, cfg, fpt = build(a.model, dev, a)
     opt = FlatShardedOptimizer(model.named_parameters(), lr=1e-4, weight_decay=0.1, grad_clip=1.0,
-                               bucket_mb=a.bucket_mb)
+                               bucket_mb=a.bucket_mb, grad_dtype=None if a.bf16_grads else torch.float32)
     V = cfg.vocab_size
     g = torch.Generator(device=dev).manual_seed(rank)
     ids = torch.randint(0, V, (a.micro_batch, a.seq_len + 1), device=dev, generator=g)
@@ -109,7 +110,8 @@ def main():
                           "data": "synthetic", "mfu_bf16_dense": round(tok * fpt / world / 2.5e15, 4),
                           "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
                           "config": {"model": a.model, "micro_batch": a.micro_batch, "grad_accum": a.accum, "seq_len": a.seq_len,
-                                     "recompute": a.recompute, "grouped_experts": a.grouped_experts, "parallelism": f"dp{world}+sharding_stage1"},
+                                     "recompute": a.recompute, "grouped_experts": a.grouped_experts,
+                                     "grad_dtype": str(opt.grad_dtype), "dw_kmajor": os.environ.get("PADDLE_AMD_DW_KMAJ", "1"), "parallelism": f"dp{world}+sharding_stage1"},
                           "loss": float(loss) * a.accum,
                           "losses": [round(float(x) * a.accum, 4) for x in hist]}))
 

@@ -159,3 +159,23 @@ PA_EXPORT int pa_clip_coef(const float* sumsq, float norm_scale, float max_norm,
   hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(64), 0, st, sumsq, norm_scale, max_norm, coef);
   PA_LAUNCH_CHECK();
 }
+
+// Fold a bf16 / fp32 gradient into the fp32 main_grad: dst = (fresh ? 0 : dst) + g.
+// The sharded optimizer's post-accumulate hook runs this for parameters whose
+// backward returned a plain gradient (biases, norm weights) instead of writing
+// main_grad in a GEMM epilogue.
+template <typename T>
+__global__ void fold_grad_kernel(float* __restrict__ dst, const T* __restrict__ g, long n, int fresh) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    dst[i] = (fresh ? 0.f : dst[i]) + IO<T>::ld(g, i);
+}
+
+PA_EXPORT int pa_fold_grad(int gdtype, float* dst, const void* g, long n, int fresh, hipStream_t st) {
+  if (n == 0) return 0;
+  const int grid = stream_grid(n, 256);
+  if (gdtype == 1)
+    hipLaunchKernelGGL(fold_grad_kernel<u16>, dim3(grid), dim3(256), 0, st, dst, (const u16*)g, n, fresh);
+  else
+    hipLaunchKernelGGL(fold_grad_kernel<float>, dim3(grid), dim3(256), 0, st, dst, (const float*)g, n, fresh);
+  PA_LAUNCH_CHECK();
+}

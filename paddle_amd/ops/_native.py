@@ -74,6 +74,18 @@ _SIGS = {
     "pa_moe_gather": [_P, _P, _P, _L, _I, _P],
     "pa_group_tile_table": [_P, _I, _L, _P],
     "pa_clip_coef": [_P, _F, _F, _P, _P],
+    "pa_fold_grad": [_I, _P, _P, _L, _I, _P],
+    "pa_p2p_alloc": [ctypes.POINTER(_P), ctypes.c_size_t],
+    "pa_p2p_free": [_P],
+    "pa_p2p_ipc_handle": [_P, _P],
+    "pa_p2p_ipc_handle_size": [],
+    "pa_p2p_ipc_open": [_P, ctypes.POINTER(_P)],
+    "pa_p2p_ipc_close": [_P],
+    "pa_p2p_barrier": [_P, _P, _I, _I, ctypes.c_uint, _L, _P, _P],
+    "pa_p2p_reduce": [_I, _P, _P, _I, _I, _P, _L, _L, _P],
+    "pa_p2p_gather": [_I, _P, _P, _I, _I, _P, _L, _L, _P],
+    "pa_p2p_zero": [_P, ctypes.c_size_t],
+    "pa_p2p_copy": [_P, _P, ctypes.c_size_t, _P],
     "pa_ce_mean_fwd": [_P, _P, _L, _I, _L, _P, _P, _P],
     "pa_ce_mean_bwd_rows": [_P, _P, _P, _L, _P],
     "pa_binary": [_I, _I, _P, _P, _P, _L, _I, _P, _P, _P, _I, _P],

@@ -1,0 +1,131 @@
+"""Direct intra-node all-reduce over IPC-mapped peer buffers.
+
+A ring all-reduce drives one outbound and one inbound xGMI link per GPU; on a
+fully connected 8-GPU MI355X node each GPU has 7 links.  Here every rank exports
+an uncached staging buffer and a signal array (hipIpcGetMemHandle), maps every
+peer's (hipIpcOpenMemHandle, exchanged over the process group), and the
+collective is three or four plain kernels on the caller's stream
+(csrc/kernels/p2p.hip):
+
+* one-shot (messages <= ``one_shot_bytes``): copy-in, barrier, every rank sums
+  all P stagings into its output (reads the 7 peers concurrently), barrier;
+* two-shot: copy-in, barrier, rank r reduces chunk r of all stagings into its own
+  staging, barrier, every rank gathers the P reduced chunks, barrier.
+
+Barriers are bounded spins on system-scope signals: a missing peer makes the op
+fail (``DirectAllReduce.check``) instead of hanging the device.  Reference
+counterpart: platform/nccl_helper.h + details/all_reduce_op_handle.cc, which
+only ever call ncclAllReduce.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _native as N
+from . import comm
+
+_P = ctypes.c_void_p
+
+
+class DirectAllReduce:
+    def __init__(self, group=None, max_bytes=64 << 20, one_shot_bytes=1 << 20, max_spins=1 << 25):
+        self.group = group
+        self.world = comm.get_world_size(group)
+        self.rank = comm.get_rank(group)
+        if not 1 <= self.world <= 8:
+            raise ValueError("DirectAllReduce: 1..8 ranks (one node)")
+        self.max_bytes = (int(max_bytes) + 4095) // 4096 * 4096
+        self.one_shot_bytes = int(one_shot_bytes)
+        self.max_spins = int(max_spins)
+        self.device = torch.device("cuda", torch.cuda.current_device())
+        lib = N.lib()
+        self._own = []
+        stage, sig = _P(), _P()
+        N.check(lib.pa_p2p_alloc(ctypes.byref(stage), self.max_bytes), "pa_p2p_alloc")
+        self._own.append(stage.value)
+        N.check(lib.pa_p2p_alloc(ctypes.byref(sig), 4096), "pa_p2p_alloc")
+        self._own.append(sig.value)
+        N.check(lib.pa_p2p_zero(sig, 4096), "pa_p2p_zero")
+        torch.cuda.synchronize()
+        hs = lib.pa_p2p_ipc_handle_size()
+        h_stage, h_sig = ctypes.create_string_buffer(hs), ctypes.create_string_buffer(hs)
+        N.check(lib.pa_p2p_ipc_handle(stage, h_stage), "pa_p2p_ipc_handle")
+        N.check(lib.pa_p2p_ipc_handle(sig, h_sig), "pa_p2p_ipc_handle")
+        allh = [None] * self.world
+        dist.all_gather_object(allh, (h_stage.raw, h_sig.raw), group=group)
+        self._opened = []
+        stages, sigs = [], []
+        for r, (hst, hsg) in enumerate(allh):
+            if r == self.rank:
+                stages.append(stage.value)
+                sigs.append(sig.value)
+                continue
+            ps, pg = _P(), _P()
+            N.check(lib.pa_p2p_ipc_open(ctypes.create_string_buffer(hst, hs), ctypes.byref(ps)), "pa_p2p_ipc_open")
+            N.check(lib.pa_p2p_ipc_open(ctypes.create_string_buffer(hsg, hs), ctypes.byref(pg)), "pa_p2p_ipc_open")
+            self._opened += [ps.value, pg.value]
+            stages.append(ps.value)
+            sigs.append(pg.value)
+        self._stage = (_P * 8)(*stages)
+        self._sig = (_P * 8)(*sigs)
+        self._err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.epoch = 0
+        comm.barrier(group)
+
+    # ------------------------------------------------------------------ pieces
+    def _barrier(self):
+        self.epoch += 1
+        N.call("pa_p2p_barrier", self._stage, self._sig, self.world, self.rank, ctypes.c_uint(self.epoch & 0xffffffff),
+               self.max_spins, N.ptr(self._err), N.stream())
+
+    def check(self):
+        """Raises if any barrier timed out (synchronises the stream)."""
+        e = int(self._err.item())
+        if e:
+            raise RuntimeError(f"DirectAllReduce: rank {self.rank} timed out waiting for peer {e - 1}")
+
+    def supports(self, t):
+        return (t.is_cuda and t.is_contiguous() and t.dtype in (torch.float32, torch.bfloat16)
+                and t.numel() % 8 == 0 and t.numel() * t.element_size() <= self.max_bytes)
+
+    # ------------------------------------------------------------------ collective
+    def all_reduce(self, t, algo="auto"):
+        """In-place sum over the group.  ``algo``: "one_shot", "two_shot" or "auto"."""
+        if self.world == 1:
+            return t
+        if not self.supports(t):
+            comm.all_reduce(t, group=self.group)
+            return t
+        nbytes = t.numel() * t.element_size()
+        if algo == "auto":
+            algo = "one_shot" if nbytes <= self.one_shot_bytes else "two_shot"
+        dt = N.dt(t)
+        n = t.numel()
+        own = _P(self._stage[self.rank])
+        N.call("pa_p2p_copy", own, N.ptr(t), nbytes, N.stream())
+        self._barrier()
+        if algo == "one_shot":
+            N.call("pa_p2p_reduce", dt, self._stage, self._sig, self.world, self.rank, N.ptr(t), 0, n, N.stream())
+        else:
+            chunk = (n + 8 * self.world - 1) // (8 * self.world) * 8
+            b, e = min(n, self.rank * chunk), min(n, (self.rank + 1) * chunk)
+            if e > b:
+                N.call("pa_p2p_reduce", dt, self._stage, self._sig, self.world, self.rank, own, b, e, N.stream())
+            self._barrier()
+            N.call("pa_p2p_gather", dt, self._stage, self._sig, self.world, self.rank, N.ptr(t), n, chunk, N.stream())
+        self._barrier()  # nobody refills its staging before every peer has read it
+        return t
+
+    def close(self):
+        lib = N.lib()
+        torch.cuda.synchronize()
+        for p in self._opened:
+            lib.pa_p2p_ipc_close(_P(p))
+        self._opened = []
+        comm.barrier(self.group)
+        for p in self._own:
+            lib.pa_p2p_free(_P(p))
+        self._own = []

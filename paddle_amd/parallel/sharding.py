@@ -182,10 +182,16 @@ class FlatShardedOptimizer:
     def _on_grad(self, p):
         if self.main_grad and p.grad is not None:
             # autograd produced a bf16 gradient (non-fused op): fold it into fp32 main_grad
-            if p._pa_grad_fresh:
-                p._pa_main_grad.copy_(p.grad)
+            g, mg = p.grad, p._pa_main_grad
+            if (g.is_cuda and g.is_contiguous() and mg.is_contiguous() and g.numel() == mg.numel()
+                    and g.dtype in (torch.bfloat16, torch.float32)):
+                from ..ops import _native as N
+
+                N.call("pa_fold_grad", N.dt(g), N.ptr(mg), N.ptr(g), g.numel(), int(p._pa_grad_fresh), N.stream())
+            elif p._pa_grad_fresh:
+                mg.copy_(g)
             else:
-                p._pa_main_grad.add_(p.grad)
+                mg.add_(g)
             p._pa_grad_fresh = False
             p.grad = None
         if self.W == 1 or not self._sync:

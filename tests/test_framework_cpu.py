@@ -268,7 +268,9 @@ def test_fluid_profiler(tmp_path):
     with fluid.profiler.profiler("CPU", "total", str(tmp_path / "prof")):
         exe.run(main, feed={"x": np.ones((2, 4), "float32"), "y": np.ones((2, 1), "float32")},
                 fetch_list=[loss], scope=scope)
-    assert os.path.exists(str(tmp_path / "prof") + ".json")
+    # the profile (tools/timeline.py input) and its single-process Chrome trace
+    assert os.path.exists(str(tmp_path / "prof"))
+    assert os.path.exists(str(tmp_path / "prof") + ".trace.json")
 
 
 def test_check_nan_inf_flag():
