@@ -5,9 +5,9 @@ DyGraph layer: ``guard()`` selects the device, ``to_variable`` makes a tensor,
 layers are :mod:`paddle_amd.nn` layers (1.x names ``Linear``/``FC``, ``Conv2D``,
 ``Pool2D``, ``BatchNorm``, ``Embedding``).  What runs where: tensors are PyTorch
 tensors and autograd is PyTorch's tape; the hot ops (GEMM / linear, attention,
-norms, softmax-CE, SwiGLU/GELU, embedding, AdamW/momentum, RoPE) go to the
-hand-written gfx950 kernels of ``paddle_amd/csrc/kernels``; every other op is an
-ATen call (vendor code: MIOpen for conv/BN/pool at the time of writing).
+norms, softmax-CE, SwiGLU/GELU, embedding, AdamW/momentum, RoPE, NHWC conv / BN /
+pool) go to the hand-written gfx950 kernels of ``paddle_amd/csrc/kernels``; every
+other op is an ATen call.
 """
 from __future__ import annotations
 
