@@ -1,8 +1,11 @@
-"""paddle.dataset: synthetic stand-ins with the reference's reader signatures.
+"""paddle.dataset: the reference's dataset readers (python/paddle/dataset/*).
 
-There is no network in this environment, so the dataset modules generate
-deterministic synthetic samples of the right shapes/dtypes (documented as such);
-the reader API (train()/test() returning sample iterators) matches
-python/paddle/dataset/*.
+There is no network: each module parses its files from the cache directory
+(``common.DATA_HOME``: ``PADDLE_DATA_HOME`` or ``~/.cache/paddle/dataset``) when
+they are present -- mnist (IDX), uci_housing (text), imikolov (PTB tgz), imdb
+(aclImdb tgz), cifar (binary releases), movielens (ml-1m zip) -- and otherwise
+serves deterministic synthetic samples of the same shapes with a one-time
+warning.  conll05, wmt14, wmt16 and flowers are synthetic only.
 """
+from . import common  # noqa: F401
 from . import cifar, flowers, imdb, imikolov, mnist, movielens, uci_housing, wmt14, wmt16, conll05  # noqa: F401
