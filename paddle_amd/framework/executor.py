@@ -14,6 +14,7 @@ Differences from the reference, MI355X-first:
 from __future__ import annotations
 
 import contextlib
+import os
 import threading
 
 import torch
@@ -22,6 +23,9 @@ from ..utils import flags as FLAGS
 from ..utils import profiler as prof
 from . import core
 from . import registry as R
+from .. import platform as _platform
+
+_LOG_MEM = os.environ.get("FLAGS_log_memory_stats") == "1"
 
 
 class PreparedBlock:
@@ -111,6 +115,10 @@ class BlockExecutor:
         stash_off = getattr(_TLS, "off", False)
         for k in range(len(pb.steps)):
             self.run_op(pb, k, scope, stash_off)
+        if _platform.vlog_level() >= 1 or _LOG_MEM:
+            if self.place.torch_device().type == "cuda":
+                _platform.log_memory(f"block {pb.block_idx if hasattr(pb, 'block_idx') else 0}",
+                                     self.place.torch_device().index or 0)
 
     def run_op(self, pb, k, scope, stash_off=False):
         """Run step ``k`` of a prepared block (the unit the SSA-graph executor
@@ -129,6 +137,8 @@ class BlockExecutor:
                     vals.append(var.get() if var is not None else None)
                 ctx_ins[slot] = vals
             ctx = R.KernelContext(op.type, ctx_ins, outs, attrs, place, scope, op, self)
+            if _platform._V >= 3:
+                _platform.vlog(3, f"run op {op.type} inputs {dict(ins)} outputs {dict(outs)}")
             run = R.run_kernel_stash if (pb.stash[k] and not stash_off) else R.run_kernel
             if profiling:
                 with prof.RecordEvent(op.type):

@@ -226,8 +226,14 @@ def layer_norm(ctx):
 def lrn(ctx):
     x = ctx.input("X")
     n, k, a, b = ctx.attr("n"), ctx.attr("k"), ctx.attr("alpha"), ctx.attr("beta")
+    r = _oplib.lrn_op(x, n, k, a, b) if x.is_cuda else None
+    if r is not None:
+        ctx.set_output("Out", r[0])
+        ctx.set_output("MidOut", r[1])
+        return
     sq = (x * x).unsqueeze(1)
-    pad = F.pad(sq, (0, 0, 0, 0, n // 2, (n - 1) // 2))
+    # window [c - (n-1)//2, c - (n-1)//2 + n) (lrn_op.cc: start = -(n - 1) / 2)
+    pad = F.pad(sq, (0, 0, 0, 0, (n - 1) // 2, n // 2))
     s = F.avg_pool3d(pad, (n, 1, 1), stride=1).squeeze(1) * n
     mid = k + a * s
     ctx.set_output("Out", x / mid.pow(b))
@@ -512,6 +518,12 @@ _REG["lookup_table"].grad_maker = _lt_grad_maker
 def one_hot(ctx):
     x = ctx.input("X").long()
     d = ctx.attr("depth")
+    if x.is_cuda and not ctx.meta:
+        xs = x.reshape(x.shape[:-1] if x.dim() > 1 and x.shape[-1] == 1 else x.shape)
+        r = _oplib.one_hot(xs, d)
+        if r is not None:
+            ctx.set_output("Out", r.to(core.to_torch_dtype(ctx.attr("dtype"))))
+            return
     out = F.one_hot(x.reshape(x.shape[:-1] if x.dim() > 1 and x.shape[-1] == 1 else x.shape), d) if not ctx.meta \
         else torch.empty(tuple(x.shape[:-1]) + (d,), device="meta")
     ctx.set_output("Out", out.to(core.to_torch_dtype(ctx.attr("dtype"))))
@@ -532,6 +544,12 @@ def top_k(ctx):
 @register_op("accuracy", ["Out", "Indices", "Label"], ["Accuracy", "Correct", "Total"], {}, grad=None)
 def accuracy(ctx):
     idx, lab = ctx.input("Indices"), ctx.input("Label")
+    r = _oplib.accuracy_op(idx, lab) if idx.is_cuda else None
+    if r is not None:
+        ctx.set_output("Accuracy", r[0])
+        ctx.set_output("Correct", r[1])
+        ctx.set_output("Total", r[2])
+        return
     lab = lab.reshape(-1, 1).to(idx.dtype)
     correct = (idx == lab).any(1).sum()
     total = torch.tensor(idx.shape[0], device=idx.device)
@@ -577,9 +595,14 @@ def pad(ctx):
                                        "data_format": "NCHW"})
 def pad2d(ctx):
     x = ctx.input("X")
-    t, b, l, r = ctx.attr("paddings")
+    t, b, l, r_ = ctx.attr("paddings")
+    r = r_
     mode = {"constant": "constant", "reflect": "reflect", "edge": "replicate"}[ctx.attr("mode")]
     nhwc = ctx.attr("data_format") == "NHWC"
+    r = _oplib.pad2d_op(x, (t, b, l, r_), ctx.attr("mode"), ctx.attr("pad_value"), nhwc) if x.is_cuda else None
+    if r is not None:
+        ctx.set_output("Out", r)
+        return
     xc = x.permute(0, 3, 1, 2) if nhwc else x
     kw = {"value": ctx.attr("pad_value")} if mode == "constant" else {}
     y = F.pad(xc, (l, r, t, b), mode=mode, **kw)
@@ -645,6 +668,10 @@ def row_conv(ctx):
     x, w = ctx.input("X"), ctx.input("Filter")
     lod = ctx.input_lod("X")
     off = lod[0] if lod else [0, x.shape[0]]
+    r = _oplib.row_conv_op(x, w, off) if x.is_cuda else None
+    if r is not None:
+        ctx.set_output("Out", r, lod)
+        return
     out = torch.zeros_like(x)
     ctxlen = w.shape[0]
     for s, e in zip(off[:-1], off[1:]):

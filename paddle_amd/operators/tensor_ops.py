@@ -12,6 +12,8 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from ..ops import oplib as _oplib
+
 from ..framework import core
 from ..framework.registry import register_op
 
@@ -83,7 +85,9 @@ _reg_t2 = register_op("transpose2", ["X"], ["Out", "XShape~"], {"axis": []})(
 def concat(ctx):
     xs = [t for t in ctx.inputs("X") if t is not None]
     ax = ctx.attr("axis")
-    out = torch.cat(xs, ax)
+    out = _oplib.concat_op(xs, ax) if xs and xs[0].is_cuda else None
+    if out is None:
+        out = torch.cat(xs, ax)
     lod = None
     if ax == 0:
         lods = [v.lod() for v in ctx.input_values("X")]
@@ -106,10 +110,13 @@ def split(ctx):
         if -1 in secs:
             i = secs.index(-1)
             secs[i] = x.shape[ax] - (sum(secs) + 1)
-        parts = torch.split(x, secs, ax)
     else:
         n = ctx.attr("num") or len(ctx.output_names("Out"))
-        parts = torch.chunk(x, n, ax)
+        secs = [c.shape[0] for c in torch.chunk(torch.empty(x.shape[ax], device="meta"), n, 0)] \
+            if x.shape[ax] else [0] * n
+    parts = _oplib.split_op(x, secs, ax) if x.is_cuda else None
+    if parts is None:
+        parts = torch.split(x, secs, ax)
     ctx.set_outputs("Out", list(parts))
 
 
@@ -380,7 +387,9 @@ def arg_min(ctx):
 
 @register_op("argsort", ["X"], ["Out", "Indices"], {"axis": -1}, grad=None)
 def argsort(ctx):
-    v, i = torch.sort(ctx.input("X"), ctx.attr("axis"))
+    x = ctx.input("X")
+    r = _oplib.argsort_op(x, ctx.attr("axis")) if x.is_cuda else None
+    v, i = r if r is not None else torch.sort(x, ctx.attr("axis"))
     ctx.set_output("Out", v)
     ctx.set_output("Indices", i)
 

@@ -85,6 +85,22 @@ _SIGS = {
     "pa_p2p_reduce": [_I, _P, _P, _I, _I, _P, _L, _L, _P],
     "pa_p2p_gather": [_I, _P, _P, _I, _I, _P, _L, _L, _P],
     "pa_p2p_zero": [_P, ctypes.c_size_t],
+    "pa_device_count": [ctypes.POINTER(_I)],
+    "pa_clear_error": [],
+    "pa_one_hot": [_P, _P, _L, _I, _P, _P],
+    "pa_pad2d": [_I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _F, _I, _P],
+    "pa_pad2d_bwd": [_I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "pa_lrn_fwd": [_I, _P, _P, _P, _I, _I, _L, _I, _F, _F, _F, _P],
+    "pa_lrn_bwd": [_I, _P, _P, _P, _P, _I, _I, _L, _I, _F, _F, _P],
+    "pa_row_conv_fwd": [_I, _P, _P, _P, _P, _L, _I, _I, _P],
+    "pa_row_conv_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _P],
+    "pa_argsort_rows": [_I, _P, _P, _P, _L, _I, _I, _P],
+    "pa_accuracy": [_P, _P, _L, _I, _P, _P, _P, _P],
+    "pa_copy2d": [_P, ctypes.c_size_t, _P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, _P],
+    "pa_can_access_peer": [_I, _I, ctypes.POINTER(_I)],
+    "pa_enable_peer_access": [_I, _I],
+    "pa_memcpy_peer_async": [_P, _I, _P, _I, ctypes.c_size_t, _P],
+    "pa_mem_info": [_I, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)],
     "pa_p2p_copy": [_P, _P, ctypes.c_size_t, _P],
     "pa_ce_mean_fwd": [_P, _P, _L, _I, _L, _P, _P, _P],
     "pa_ce_mean_bwd_rows": [_P, _P, _P, _L, _P],
@@ -164,9 +180,40 @@ def dt(t) -> int:
     raise TypeError(f"paddle_amd kernels support float32/bfloat16, got {t.dtype}")
 
 
+class EnforceError(RuntimeError):
+    """A failed HIP call or launch (reference platform/enforce.h PADDLE_ENFORCE with
+    the cuda/nccl error decoders): carries the HIP error code and its name."""
+
+    def __init__(self, what, rc):
+        self.rc = rc
+        super().__init__(f"paddle_amd kernel {what} failed: {error_name(rc)} ({rc}): {error_string(rc)}")
+
+
+def error_name(rc: int) -> str:
+    try:
+        f = lib().pa_error_name
+        f.restype, f.argtypes = ctypes.c_char_p, [_I]
+        return (f(int(rc)) or b"?").decode()
+    except Exception:  # library unavailable: the code alone
+        return f"hipError {rc}"
+
+
+def error_string(rc: int) -> str:
+    try:
+        f = lib().pa_error_string
+        f.restype, f.argtypes = ctypes.c_char_p, [_I]
+        return (f(int(rc)) or b"").decode()
+    except Exception:
+        return ""
+
+
 def check(rc: int, what: str):
     if rc != 0:
-        raise RuntimeError(f"paddle_amd kernel {what} failed: hipError {rc}")
+        try:  # reset the sticky last-error so later (torch) launch checks stay clean
+            lib().pa_clear_error()
+        except Exception:
+            pass
+        raise EnforceError(what, rc)
 
 
 def call(name: str, *args):

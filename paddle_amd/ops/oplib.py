@@ -16,6 +16,7 @@ import numpy as np
 import torch
 
 from . import _native as N
+from ..autograd import tape as _tape
 
 _ENABLED = os.environ.get("PADDLE_AMD_OPLIB", "1") != "0"
 _DT = {torch.float32: 0, torch.bfloat16: 1}
@@ -487,3 +488,227 @@ def dropout_op(x, p, seed=None, upscale=False):
     if not _ok(x):
         return None
     return _DropoutFn.apply(x, float(p), seed, bool(upscale))
+
+
+# ------------------------------------------------------------------ misc Fluid kernels (misc.hip)
+
+
+def one_hot(x, depth):
+    """x int64 [...] -> float32 [..., depth]; raises on out-of-range ids."""
+    if not (_ENABLED and x.is_cuda):
+        return None
+    xl = x.to(torch.int64).contiguous()
+    out = torch.empty(tuple(x.shape) + (depth,), dtype=torch.float32, device=x.device)
+    bad = torch.zeros(1, dtype=torch.int32, device=x.device)
+    N.call("pa_one_hot", N.ptr(xl), N.ptr(out), xl.numel(), int(depth), N.ptr(bad), N.stream())
+    if int(bad.item()):
+        raise ValueError(f"one_hot: an id is outside [0, {depth})")
+    return out
+
+
+_PAD_MODE = {"constant": 0, "reflect": 1, "edge": 2}
+
+
+class _Pad2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, pads, mode, value, nhwc):
+        x = x.contiguous()
+        if nhwc:
+            Nn, H, W, C = x.shape
+        else:
+            Nn, C, H, W = x.shape
+        t, b, l, r = pads
+        shape = (Nn, H + t + b, W + l + r, C) if nhwc else (Nn, C, H + t + b, W + l + r)
+        y = torch.empty(shape, dtype=x.dtype, device=x.device)
+        N.call("pa_pad2d", _DT[x.dtype], N.ptr(x), N.ptr(y), Nn, C, H, W, t, b, l, r, _PAD_MODE[mode], float(value),
+               int(nhwc), N.stream())
+        ctx.meta = (Nn, C, H, W, t, b, l, r, _PAD_MODE[mode], int(nhwc), x.shape, x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        Nn, C, H, W, t, b, l, r, mode, nhwc, shape, dt = ctx.meta
+        dy = dy.contiguous()
+        dx = torch.zeros(shape, dtype=torch.float32, device=dy.device)
+        N.call("pa_pad2d_bwd", _DT[dy.dtype], N.ptr(dy), N.ptr(dx), Nn, C, H, W, t, b, l, r, mode, nhwc, N.stream())
+        return dx.to(dt), None, None, None, None
+
+
+def pad2d_op(x, pads, mode="constant", value=0.0, nhwc=False):
+    if not _ok(x) or x.dim() != 4 or mode not in _PAD_MODE:
+        return None
+    H, W = (x.shape[1], x.shape[2]) if nhwc else (x.shape[2], x.shape[3])
+    t, b, l, r = pads
+    if mode == "reflect" and (t >= H or b >= H or l >= W or r >= W):
+        return None
+    return _tape.apply(_Pad2dFn, x, tuple(int(v) for v in pads), mode, float(value), bool(nhwc))
+
+
+class _LrnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, n, k, alpha, beta):
+        x = x.contiguous()
+        Nn, C = x.shape[0], x.shape[1]
+        HW = x.numel() // max(Nn * C, 1)
+        out = torch.empty_like(x)
+        mid = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+        N.call("pa_lrn_fwd", _DT[x.dtype], N.ptr(x), N.ptr(out), N.ptr(mid), Nn, C, HW, int(n), float(k),
+               float(alpha), float(beta), N.stream())
+        ctx.save_for_backward(x, mid)
+        ctx.args = (Nn, C, HW, int(n), float(alpha), float(beta))
+        ctx.mark_non_differentiable(mid)
+        return out, mid
+
+    @staticmethod
+    def backward(ctx, dout, dmid):
+        x, mid = ctx.saved_tensors
+        Nn, C, HW, n, alpha, beta = ctx.args
+        dout = dout.contiguous()
+        dx = torch.empty_like(x)
+        N.call("pa_lrn_bwd", _DT[x.dtype], N.ptr(x), N.ptr(dout), N.ptr(mid), N.ptr(dx), Nn, C, HW, n, alpha, beta,
+               N.stream())
+        return dx, None, None, None, None
+
+
+def lrn_op(x, n, k, alpha, beta):
+    """(out, mid) of cross-channel LRN (NCHW) or None."""
+    if not _ok(x) or x.dim() < 2:
+        return None
+    return _tape.apply(_LrnFn, x, n, k, alpha, beta)
+
+
+class _RowConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, seq_start, seq_end):
+        x, w = x.contiguous(), w.contiguous()
+        rows, D = x.shape[0], x.numel() // max(x.shape[0], 1)
+        out = torch.empty_like(x)
+        N.call("pa_row_conv_fwd", _DT[x.dtype], N.ptr(x), N.ptr(w), N.ptr(seq_end), N.ptr(out), rows, D, w.shape[0],
+               N.stream())
+        ctx.save_for_backward(x, w, seq_start, seq_end)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, seq_start, seq_end = ctx.saved_tensors
+        dy = dy.contiguous()
+        rows, D = x.shape[0], x.numel() // max(x.shape[0], 1)
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dw = torch.empty(w.shape, dtype=torch.float32, device=w.device) if ctx.needs_input_grad[1] else None
+        N.call("pa_row_conv_bwd", _DT[x.dtype], N.ptr(dy), N.ptr(x), N.ptr(w), N.ptr(seq_start), N.ptr(seq_end),
+               N.ptr(dx), N.ptr(dw), rows, D, w.shape[0], N.stream())
+        return dx, (dw.to(w.dtype) if dw is not None else None), None, None
+
+
+def row_conv_op(x, w, offsets):
+    """Lookahead row convolution over LoD sequences ``offsets`` (level-0 offsets)."""
+    if not _ok(x, w) or x.dtype != w.dtype:
+        return None
+    rows = x.shape[0]
+    start = np.zeros(rows, dtype=np.int32)
+    end = np.zeros(rows, dtype=np.int32)
+    for s, e in zip(offsets[:-1], offsets[1:]):
+        start[s:e], end[s:e] = s, e
+    st = torch.as_tensor(start).to(x.device)
+    en = torch.as_tensor(end).to(x.device)
+    return _tape.apply(_RowConvFn, x, w, st, en)
+
+
+def argsort_op(x, axis=-1, descending=False):
+    """(sorted values, int64 indices) along the last axis for rows of <= 2048."""
+    if not _ok(x) or x.dim() == 0:
+        return None
+    ax = axis % x.dim()
+    if ax != x.dim() - 1 or x.shape[-1] > 2048 or x.shape[-1] == 0:
+        return None
+    xc = x.detach().contiguous()
+    n = xc.shape[-1]
+    rows = xc.numel() // n
+    vals = torch.empty_like(xc)
+    idx = torch.empty(xc.shape, dtype=torch.int64, device=x.device)
+    N.call("pa_argsort_rows", _DT[xc.dtype], N.ptr(xc), N.ptr(vals), N.ptr(idx), rows, n, int(descending), N.stream())
+    return vals, idx
+
+
+def accuracy_op(indices, label):
+    """(accuracy float32[1], correct int32[1], total int32[1])."""
+    if not (_ENABLED and indices.is_cuda):
+        return None
+    ind = indices.to(torch.int64).contiguous()
+    lab = label.reshape(-1).to(torch.int64).contiguous()
+    rows, k = ind.shape[0], ind.numel() // max(ind.shape[0], 1)
+    correct = torch.empty(1, dtype=torch.int32, device=ind.device)
+    total = torch.empty(1, dtype=torch.int32, device=ind.device)
+    acc = torch.empty(1, dtype=torch.float32, device=ind.device)
+    N.call("pa_accuracy", N.ptr(ind), N.ptr(lab), rows, k, N.ptr(correct), N.ptr(acc), N.ptr(total), N.stream())
+    return acc, correct, total
+
+
+def _cat_into(xs, axis, out):
+    pre = int(np.prod(out.shape[:axis])) if axis else 1
+    post = int(np.prod(out.shape[axis + 1:])) if axis + 1 < out.dim() else 1
+    es = out.element_size()
+    dpitch = out.shape[axis] * post * es
+    off = 0
+    for x in xs:
+        w = x.shape[axis] * post * es
+        N.call("pa_copy2d", ctypes.c_void_p(out.data_ptr() + off), dpitch, N.ptr(x), w, w, pre, N.stream())
+        off += w
+
+
+class _ConcatFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, axis, *xs):
+        xs = [x.contiguous() for x in xs]
+        shape = list(xs[0].shape)
+        shape[axis] = sum(x.shape[axis] for x in xs)
+        out = torch.empty(shape, dtype=xs[0].dtype, device=xs[0].device)
+        _cat_into(xs, axis, out)
+        ctx.axis, ctx.sizes = axis, [x.shape[axis] for x in xs]
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return (None,) + tuple(split_op(g, ctx.sizes, ctx.axis))
+
+
+class _SplitFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, axis, sizes):
+        x = x.contiguous()
+        pre = int(np.prod(x.shape[:axis])) if axis else 1
+        post = int(np.prod(x.shape[axis + 1:])) if axis + 1 < x.dim() else 1
+        es = x.element_size()
+        spitch = x.shape[axis] * post * es
+        outs, off = [], 0
+        for s in sizes:
+            shape = list(x.shape)
+            shape[axis] = s
+            o = torch.empty(shape, dtype=x.dtype, device=x.device)
+            w = s * post * es
+            N.call("pa_copy2d", N.ptr(o), w, ctypes.c_void_p(x.data_ptr() + off), spitch, w, pre, N.stream())
+            outs.append(o)
+            off += w
+        ctx.axis = axis
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        gs = [g if g is not None else None for g in gs]
+        if any(g is None for g in gs):
+            return None, None, None
+        return concat_op(list(gs), ctx.axis), None, None
+
+
+def concat_op(xs, axis=0):
+    if not xs or not all(_ok(x) for x in xs) or len({x.dtype for x in xs}) != 1:
+        return None
+    axis = axis % xs[0].dim()
+    return _tape.apply(_ConcatFn, axis, *xs)
+
+
+def split_op(x, sizes, axis=0):
+    if not _ok(x):
+        return None
+    axis = axis % x.dim()
+    return list(_tape.apply(_SplitFn, x, axis, list(sizes)))

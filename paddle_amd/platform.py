@@ -1,0 +1,113 @@
+"""Platform services (reference paddle/fluid/platform: init.cc InitDevices / InitP2P,
+gpu_info.cc memory queries, enforce.h, and the glog VLOG / GLOG_v verbosity used
+throughout the C++ core).
+
+* ``vlog(level, msg)``: printed to stderr when ``GLOG_v`` (or ``FLAGS_v``) >= level;
+  the executor logs every op at level 3 and memory statistics at level 1 (or every
+  run when ``FLAGS_log_memory_stats=1``);
+* ``enforce(cond, msg)`` / ``EnforceError`` (the kernel library's HIP errors carry
+  the error name, ``ops._native.EnforceError``);
+* ``init_p2p(devices)`` enables peer access between every pair of the node's GPUs
+  that supports it (xGMI), ``memcpy_peer(dst, src)`` copies across devices without
+  staging through the host;
+* ``device_memory_info(dev)`` / ``memory_stats(dev)``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import sys
+import time
+
+import torch
+
+from .ops import _native as N
+from .ops._native import EnforceError  # noqa: F401
+
+_V = int(os.environ.get("GLOG_v", os.environ.get("FLAGS_v", "0")) or 0)
+
+
+def vlog_level() -> int:
+    return _V
+
+
+def set_vlog_level(v: int):
+    global _V
+    _V = int(v)
+
+
+def vlog(level: int, msg: str):
+    if _V >= level:
+        t = time.strftime("%H:%M:%S")
+        sys.stderr.write(f"I{t} {os.getpid()} paddle_amd] {msg}\n")
+
+
+def enforce(cond, msg="enforce failed", *args):
+    if not cond:
+        raise EnforceError.__bases__[0](msg % args if args else msg)
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    N.check(N.lib().pa_device_count(ctypes.byref(n)), "pa_device_count")
+    return n.value
+
+
+def init_p2p(devices=None):
+    """Enable peer access for every ordered pair of ``devices`` that can access
+    each other (reference platform/init.cc InitP2P).  Returns the enabled pairs."""
+    lib = N.lib()
+    devs = list(range(device_count())) if devices is None else list(devices)
+    pairs = []
+    for a in devs:
+        for b in devs:
+            if a == b:
+                continue
+            can = ctypes.c_int(0)
+            N.check(lib.pa_can_access_peer(a, b, ctypes.byref(can)), "pa_can_access_peer")
+            if can.value:
+                N.check(lib.pa_enable_peer_access(a, b), "pa_enable_peer_access")
+                pairs.append((a, b))
+    vlog(1, f"init_p2p: {len(pairs)} peer pairs enabled over devices {devs}")
+    return pairs
+
+
+def memcpy_peer(dst: torch.Tensor, src: torch.Tensor):
+    """dst[...] = src[...] across devices on the current stream (hipMemcpyPeerAsync)."""
+    enforce(dst.is_cuda and src.is_cuda, "memcpy_peer: device tensors")
+    enforce(dst.is_contiguous() and src.is_contiguous() and dst.dtype == src.dtype
+            and dst.numel() == src.numel(), "memcpy_peer: matching contiguous tensors")
+    N.call("pa_memcpy_peer_async", N.ptr(dst), dst.device.index, N.ptr(src), src.device.index,
+           src.numel() * src.element_size(), N.stream())
+    return dst
+
+
+def device_memory_info(dev=0):
+    """(free, total) bytes of HBM on ``dev`` (hipMemGetInfo)."""
+    f, t = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    N.check(N.lib().pa_mem_info(int(dev), ctypes.byref(f), ctypes.byref(t)), "pa_mem_info")
+    return f.value, t.value
+
+
+def memory_stats(dev=0):
+    """Allocator + device view of memory (reference: the memory-usage VLOGs of
+    buddy_allocator.cc / gpu_info.cc)."""
+    out = {}
+    if os.environ.get("FLAGS_allocator_strategy") == "buddy":
+        from . import runtime
+
+        out.update({f"buddy_{k}": v for k, v in runtime.torch_allocator_stats(dev).items()})
+    else:
+        out["allocated"] = torch.cuda.memory_allocated(dev)
+        out["reserved"] = torch.cuda.memory_reserved(dev)
+        out["peak"] = torch.cuda.max_memory_allocated(dev)
+    free, total = device_memory_info(dev)
+    out.update(device_free=free, device_total=total)
+    return out
+
+
+def log_memory(tag, dev=0):
+    if torch.cuda.is_available():
+        st = memory_stats(dev)
+        vlog(0 if os.environ.get("FLAGS_log_memory_stats") == "1" else 1,
+             f"memory[{tag}] " + " ".join(f"{k}={v / 2**30:.2f}GiB" for k, v in st.items()))
