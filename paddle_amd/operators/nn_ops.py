@@ -156,11 +156,17 @@ def spp(ctx):
     N, C, H, W = x.shape
     outs = []
     for lvl in range(ctx.attr("pyramid_height")):
+        # spp_op.h: kernel = ceil(size / bins), stride = kernel, padding =
+        # (kernel * bins - size + 1) / 2; avg pooling counts valid elements only
         bins = 2 ** lvl
+        kh, kw = -(-H // bins), -(-W // bins)
+        ph, pw = (kh * bins - H + 1) // 2, (kw * bins - W + 1) // 2
+        pad = (pw, kw * bins - W - pw, ph, kh * bins - H - ph)
         if ctx.attr("pooling_type") == "max":
-            o = F.adaptive_max_pool2d(x, bins)
+            o = F.max_pool2d(F.pad(x, pad, value=float("-inf")), (kh, kw), (kh, kw))
         else:
-            o = F.adaptive_avg_pool2d(x, bins)
+            ones = F.pad(torch.ones(1, 1, H, W, dtype=x.dtype, device=x.device), pad)
+            o = F.avg_pool2d(F.pad(x, pad), (kh, kw), (kh, kw)) / F.avg_pool2d(ones, (kh, kw), (kh, kw))
         outs.append(o.reshape(N, -1))
     ctx.set_output("Out", torch.cat(outs, 1))
 
@@ -595,13 +601,12 @@ def pad(ctx):
                                        "data_format": "NCHW"})
 def pad2d(ctx):
     x = ctx.input("X")
-    t, b, l, r_ = ctx.attr("paddings")
-    r = r_
+    t, b, l, r = ctx.attr("paddings")
     mode = {"constant": "constant", "reflect": "reflect", "edge": "replicate"}[ctx.attr("mode")]
     nhwc = ctx.attr("data_format") == "NHWC"
-    r = _oplib.pad2d_op(x, (t, b, l, r_), ctx.attr("mode"), ctx.attr("pad_value"), nhwc) if x.is_cuda else None
-    if r is not None:
-        ctx.set_output("Out", r)
+    res = _oplib.pad2d_op(x, (t, b, l, r), ctx.attr("mode"), ctx.attr("pad_value"), nhwc) if x.is_cuda else None
+    if res is not None:
+        ctx.set_output("Out", res)
         return
     xc = x.permute(0, 3, 1, 2) if nhwc else x
     kw = {"value": ctx.attr("pad_value")} if mode == "constant" else {}

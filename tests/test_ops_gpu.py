@@ -9,6 +9,7 @@ import torch
 
 from op_test import OpTest
 from test_ops_cpu import CASES
+from test_ops_more_cpu import MORE
 
 pytestmark = pytest.mark.gpu
 dev = "cuda"
@@ -23,6 +24,19 @@ def _gpu_place():
 @pytest.mark.parametrize("op,inputs,outputs,attrs,grad,grad_out,tol,atol,no_check", CASES,
                          ids=[f"{c[0]}_{i}" for i, c in enumerate(CASES)])
 def test_op_on_device(op, inputs, outputs, attrs, grad, grad_out, tol, atol, no_check):
+    t = OpTest()
+    t.op_type, t.inputs, t.attrs = op, inputs, attrs
+    t.outputs = {k: v for k, v in outputs.items() if v is not None}
+    if t.outputs:
+        t.check_output(atol=max(atol, 1e-4), rtol=1e-3, no_check_set=no_check, places=[_gpu_place()])
+    else:
+        t.outputs = {k: np.zeros(1, "float32") for k in outputs}
+        t.check_output(exec_only=True, places=[_gpu_place()])
+
+
+@pytest.mark.parametrize("op,inputs,outputs,attrs,grad,grad_out,tol,atol,no_check", MORE,
+                         ids=[f"{c[0]}_{i}" for i, c in enumerate(MORE)])
+def test_more_ops_on_device(op, inputs, outputs, attrs, grad, grad_out, tol, atol, no_check):
     t = OpTest()
     t.op_type, t.inputs, t.attrs = op, inputs, attrs
     t.outputs = {k: v for k, v in outputs.items() if v is not None}
