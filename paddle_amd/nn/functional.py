@@ -209,6 +209,9 @@ def _conv_padding(padding, nd):
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCHW", name=None):
     pad = _conv_padding(padding, 2)
+    if (not _nchw(x, data_format) and groups > 1 and not isinstance(pad, str)
+            and _conv.supported_dwconv(x, weight, groups)):
+        return _conv.dwconv2d_nhwc(x, weight, bias, stride, pad, dilation)
     if not _nchw(x, data_format) and _conv.supported_conv(x, weight, stride, pad, dilation, groups):
         # NHWC bf16 on the GPU: implicit-GEMM MFMA kernel (ops/conv.py)
         return _conv.conv2d_nhwc(x, weight, bias, stride, pad, dilation)

@@ -96,6 +96,9 @@ _SIGS = {
     "pa_row_conv_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _P],
     "pa_argsort_rows": [_I, _P, _P, _P, _L, _I, _I, _P],
     "pa_accuracy": [_P, _P, _L, _I, _P, _P, _P, _P],
+    "pa_dwconv_fwd": [_P, _P, _P, _P] + [_I] * 13 + [_P],
+    "pa_dwconv_dgrad": [_P, _P, _P] + [_I] * 13 + [_P],
+    "pa_dwconv_wgrad": [_P, _P, _P] + [_I] * 13 + [_P],
     "pa_copy2d": [_P, ctypes.c_size_t, _P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, _P],
     "pa_can_access_peer": [_I, _I, ctypes.POINTER(_I)],
     "pa_enable_peer_access": [_I, _I],

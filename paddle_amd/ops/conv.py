@@ -159,6 +159,58 @@ def conv2d_nhwc(x, weight, bias=None, stride=1, padding=0, dilation=1):
     return _Conv2dNHWC.apply(x, weight, bias, tuple(map(_i, s)), tuple(map(_i, p)), tuple(map(_i, d)))
 
 
+# ------------------------------------------------------------------ depthwise conv (dwconv.hip)
+
+
+def supported_dwconv(x, w, groups):
+    """Depthwise NHWC bf16: groups == C, weight [C * mult, 1, KH, KW], C % 8 == 0."""
+    return (_ENABLED[0] and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.is_contiguous()
+            and w.dim() == 4 and w.shape[1] == 1 and groups == x.shape[3] and x.shape[3] % 8 == 0
+            and w.shape[0] % x.shape[3] == 0)
+
+
+class _DwConvNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, s, p, d):
+        Nn, H, W, C = x.shape
+        Cout, _, KH, KW = w.shape
+        OH, OW = (H + 2 * p[0] - d[0] * (KH - 1) - 1) // s[0] + 1, (W + 2 * p[1] - d[1] * (KW - 1) - 1) // s[1] + 1
+        wb = w.to(torch.bfloat16).reshape(Cout, KH * KW).t().contiguous()  # [taps, Cout] for 16-B loads
+        bb = b.to(torch.bfloat16).contiguous() if b is not None else None
+        y = torch.empty(Nn, OH, OW, Cout, dtype=torch.bfloat16, device=x.device)
+        _nat.call("pa_dwconv_fwd", _nat.ptr(x), _nat.ptr(wb), _nat.ptr(bb), _nat.ptr(y), Nn, H, W, C, Cout, KH, KW, s[0], s[1],
+               p[0], p[1], d[0], d[1], _nat.stream())
+        ctx.save_for_backward(x, wb)
+        ctx.conf = (s, p, d, b is not None, w.dtype, tuple(w.shape))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wb = ctx.saved_tensors
+        s, p, d, has_b, wdt, (Cout, _, KH, KW) = ctx.conf
+        dy = dy.contiguous().to(torch.bfloat16)
+        Nn, H, W, C = x.shape
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            _nat.call("pa_dwconv_dgrad", _nat.ptr(dy), _nat.ptr(wb), _nat.ptr(dx), Nn, H, W, C, Cout, KH, KW, s[0], s[1], p[0],
+                   p[1], d[0], d[1], _nat.stream())
+        if ctx.needs_input_grad[1]:
+            dw32 = torch.zeros(wb.shape, dtype=torch.float32, device=x.device)  # [taps, Cout]
+            _nat.call("pa_dwconv_wgrad", _nat.ptr(dy), _nat.ptr(x), _nat.ptr(dw32), Nn, H, W, C, Cout, KH, KW, s[0], s[1], p[0],
+                   p[1], d[0], d[1], _nat.stream())
+            dw = dw32.t().reshape(Cout, 1, KH, KW).to(wdt)
+        if has_b and ctx.needs_input_grad[2]:
+            db = dy.reshape(-1, Cout).float().sum(0).to(wdt)
+        return dx, dw, db, None, None, None
+
+
+def dwconv2d_nhwc(x, weight, bias=None, stride=1, padding=0, dilation=1):
+    """Depthwise conv: x [N, H, W, C] bf16, weight [C * mult, 1, KH, KW]."""
+    s, p, d = _pair(stride), _pair(padding), _pair(dilation)
+    return _DwConvNHWC.apply(x, weight, bias, tuple(map(_i, s)), tuple(map(_i, p)), tuple(map(_i, d)))
+
+
 # ------------------------------------------------------------------ batch norm
 
 
