@@ -68,12 +68,23 @@ class GradScaler:
         if not self.enable or self._unscaled:
             return
         inv = 1.0 / self.scale_v
-        found = torch.zeros(1)
+        # one device flag for every gradient (native isfinite kernel), one host read
+        from ..ops import oplib as _oplib
+
+        flags = {}
+        found = False
         for p in optimizer._parameter_list:
             if p.grad is not None:
                 p.grad.mul_(inv)
-                found = found + (~torch.isfinite(p.grad)).any().float().cpu()
-        self._found_inf = bool(found.item() > 0)
+                g = p.grad
+                if g.is_cuda:
+                    bad = flags.setdefault(g.device, torch.zeros(1, dtype=torch.int32, device=g.device))
+                    if _oplib.isfinite_op(g, bad):
+                        continue
+                    bad.add_((~torch.isfinite(g)).any().int())
+                else:
+                    found = found or not bool(torch.isfinite(g).all())
+        self._found_inf = found or any(int(b.item()) > 0 for b in flags.values())
         self._unscaled = True
 
     def step(self, optimizer):

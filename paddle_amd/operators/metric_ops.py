@@ -19,6 +19,7 @@ import torch
 
 from ..framework import core
 from ..framework.registry import register_op
+from ..ops import oplib as _oplib
 
 
 @register_op("auc", ["Predict", "Label", "TP?", "FP?", "TN?", "FN?"], ["AUC", "TPOut", "FPOut", "TNOut", "FNOut"],
@@ -124,8 +125,12 @@ def mean_iou(ctx):
     C = ctx.attr("num_classes")
     p = ctx.input("Predictions").reshape(-1).long()
     l = ctx.input("Labels").reshape(-1).long()
-    correct = torch.bincount(l[p == l], minlength=C)
-    wrong = torch.bincount(p[p != l], minlength=C) + torch.bincount(l[p != l], minlength=C)
+    hist = _oplib.mean_iou_hist(p, l, C) if p.is_cuda else None
+    if hist is not None:
+        correct, wrong = hist[0].long(), hist[1].long()
+    else:
+        correct = torch.bincount(l[p == l], minlength=C)
+        wrong = torch.bincount(p[p != l], minlength=C) + torch.bincount(l[p != l], minlength=C)
     for t in ctx.inputs("InWrongs"):
         wrong = wrong + t.reshape(-1).long()
     for t in ctx.inputs("InCorrects"):
@@ -303,6 +308,11 @@ def merge_ids(ctx):
 @register_op("fake_quantize_abs_max", ["X"], ["Out", "OutScale"], {"bit_length": 8}, grad=None)
 def fake_quantize_abs_max(ctx):
     x = ctx.input("X")
+    r = _oplib.fake_quant_op(x, ctx.attr("bit_length")) if x.is_cuda else None
+    if r is not None:
+        ctx.set_output("Out", r[0])
+        ctx.set_output("OutScale", r[1])
+        return
     bins = (1 << (ctx.attr("bit_length") - 1)) - 1
     s = x.detach().abs().max().reshape(1)
     ctx.set_output("Out", torch.round(x / s.clamp(min=1e-30) * bins))
@@ -315,6 +325,13 @@ def fake_quantize_range_abs_max(ctx):
     x = ctx.input("X")
     bins = (1 << (ctx.attr("bit_length") - 1)) - 1
     in_s = ctx.input("InScale").reshape(1)
+    r = _oplib.fake_quant_op(x, ctx.attr("bit_length"), in_s, ctx.attr("is_test"), True) if x.is_cuda else None
+    if r is not None:
+        ctx.set_output("Out", r[0])
+        ctx.set_output("OutScale", r[1])
+        if ctx.has_output("OutScales"):
+            ctx.set_output("OutScales", r[1].expand(ctx.attr("window_size")).clone())
+        return
     if ctx.attr("is_test"):
         s = in_s
     else:

@@ -647,6 +647,9 @@ def im2sequence(ctx):
 @register_op("roi_pool", ["X", "ROIs"], ["Out", "Argmax~"], {"spatial_scale": 1.0, "pooled_height": 1,
                                                              "pooled_width": 1})
 def roi_pool(ctx):
+    """Max pooling over ROI bins (roi_pool_op.cu): the ROI corners are rounded half
+    away from zero after scaling, bins are floor/ceil of ph * roi_h / PH offset by the
+    ROI start and clipped to the map; an empty bin gives 0 with Argmax -1."""
     x, rois = ctx.input("X"), ctx.input("ROIs")
     lod = ctx.input_lod("ROIs")
     ph, pw, sc = ctx.attr("pooled_height"), ctx.attr("pooled_width"), ctx.attr("spatial_scale")
@@ -657,14 +660,41 @@ def roi_pool(ctx):
             batch_ids += [b] * (off[b + 1] - off[b])
     else:
         batch_ids = [0] * rois.shape[0]
-    outs = []
+    r = _oplib.roi_pool_op(x, rois, batch_ids, ph, pw, sc) if x.is_cuda and rois.shape[0] else None
+    if r is not None:
+        ctx.set_output("Out", r[0])
+        ctx.set_output("Argmax", r[1])
+        return
+    import math
+
+    def rnd(v):
+        return int(math.copysign(math.floor(abs(v) + 0.5), v))
+
+    B, C, H, W = x.shape
+    outs, args = [], []
     for i in range(rois.shape[0]):
-        x1, y1, x2, y2 = [int(round(float(v) * sc)) for v in rois[i].tolist()]
-        feat = x[batch_ids[i], :, max(0, y1):max(y1 + 1, y2 + 1), max(0, x1):max(x1 + 1, x2 + 1)]
-        outs.append(F.adaptive_max_pool2d(feat, (ph, pw)))
-    out = torch.stack(outs) if outs else torch.zeros(0, x.shape[1], ph, pw, device=x.device, dtype=x.dtype)
+        x1, y1, x2, y2 = [rnd(float(v) * sc) for v in rois[i].tolist()]
+        rw, rh = max(x2 - x1 + 1, 1), max(y2 - y1 + 1, 1)
+        o = torch.zeros(C, ph, pw, dtype=x.dtype, device=x.device)
+        a = torch.full((C, ph, pw), -1, dtype=torch.int64, device=x.device)
+        for py in range(ph):
+            hs = min(max(math.floor(py * rh / ph) + y1, 0), H)
+            he = min(max(math.ceil((py + 1) * rh / ph) + y1, 0), H)
+            for px in range(pw):
+                ws = min(max(math.floor(px * rw / pw) + x1, 0), W)
+                we = min(max(math.ceil((px + 1) * rw / pw) + x1, 0), W)
+                if he <= hs or we <= ws:
+                    continue
+                win = x[batch_ids[i], :, hs:he, ws:we].reshape(C, -1)
+                m, j = win.max(1)
+                o[:, py, px] = m
+                a[:, py, px] = (j // (we - ws) + hs) * W + j % (we - ws) + ws
+        outs.append(o)
+        args.append(a)
+    out = torch.stack(outs) if outs else torch.zeros(0, C, ph, pw, device=x.device, dtype=x.dtype)
     ctx.set_output("Out", out)
-    ctx.set_output("Argmax", torch.zeros(out.shape, dtype=torch.int64, device=x.device))
+    ctx.set_output("Argmax", torch.stack(args) if args else torch.zeros(out.shape, dtype=torch.int64,
+                                                                         device=x.device))
 
 
 @register_op("row_conv", ["X", "Filter"], ["Out"], {})

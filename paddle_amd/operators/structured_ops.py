@@ -23,6 +23,7 @@ import torch.nn.functional as F
 
 from ..framework import core
 from ..framework.registry import register_op
+from ..ops import oplib as _oplib
 from .rnn_ops import _gather, _pack_index
 
 
@@ -173,6 +174,10 @@ def chunk_eval(ctx):
 @register_op("warpctc", ["Logits", "Label"], ["WarpCTCGrad~", "Loss"], {"blank": 0, "norm_by_times": False},
              share_lod=False)
 def warpctc(ctx):
+    """CTC loss (warpctc_op.h).  As in the reference, Loss is the plain -log p(l|x)
+    and ``norm_by_times`` scales only the gradient by 1/T (UnpaddingLoDTensorFunctor
+    with norm_by_times); impossible alignments give 0 (zero_infinity).  GPU:
+    native alpha/beta lattice + fused softmax gradient (seqdet.hip)."""
     x, lab = ctx.input("Logits"), ctx.input("Label")
     xo, lo = _off(ctx, "Logits"), _off(ctx, "Label")
     N = len(xo) - 1
@@ -180,23 +185,46 @@ def warpctc(ctx):
         ctx.set_output("Loss", torch.empty(N, 1, dtype=x.dtype, device="meta"))
         ctx.set_output("WarpCTCGrad", torch.empty_like(x))
         return
-    idx, mask = _pack_index(xo, False, x.device)
-    logp = torch.log_softmax(_gather(x.float(), idx, mask), -1).transpose(0, 1)      # [L, N, C]
-    xl = torch.tensor([xo[i + 1] - xo[i] for i in range(N)], device=x.device)
-    ll = torch.tensor([lo[i + 1] - lo[i] for i in range(N)], device=x.device)
-    tgt = lab.reshape(-1).long()
-    loss = F.ctc_loss(logp, tgt, xl, ll, blank=ctx.attr("blank"), reduction="none", zero_infinity=True)
-    if ctx.attr("norm_by_times"):
-        loss = loss / xl.to(loss.dtype)
-    ctx.set_output("Loss", loss.unsqueeze(1).to(x.dtype))
+    blank, norm = ctx.attr("blank"), ctx.attr("norm_by_times")
+    loss = _oplib.ctc_loss_op(x, lab, xo, lo, blank, norm) if x.is_cuda else None
+    if loss is None:
+        idx, mask = _pack_index(xo, False, x.device)
+        logp = torch.log_softmax(_gather(x.float(), idx, mask), -1).transpose(0, 1)      # [L, N, C]
+        xl = torch.tensor([xo[i + 1] - xo[i] for i in range(N)], device=x.device)
+        ll = torch.tensor([lo[i + 1] - lo[i] for i in range(N)], device=x.device)
+        tgt = lab.reshape(-1).long()
+        loss = F.ctc_loss(logp, tgt, xl, ll, blank=blank, reduction="none", zero_infinity=True)
+        if norm:
+            loss = _GradScale.apply(loss, 1.0 / xl.clamp(min=1).to(loss.dtype))
+        loss = loss.unsqueeze(1).to(x.dtype)
+    ctx.set_output("Loss", loss)
     ctx.set_output("WarpCTCGrad", torch.zeros_like(x))
+
+
+class _GradScale(torch.autograd.Function):
+    """Identity forward; backward multiplies the incoming gradient by ``w``."""
+
+    @staticmethod
+    def forward(ctx, v, w):
+        ctx.save_for_backward(w)
+        return v.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        (w,) = ctx.saved_tensors
+        return g * w, None
 
 
 @register_op("ctc_align", ["Input"], ["Output"], {"blank": 0, "merge_repeated": True}, grad=None, no_infer=True)
 def ctc_align(ctx):
-    x = ctx.input("Input").reshape(-1).tolist()
     off = _off(ctx, "Input")
     blank, merge = ctx.attr("blank"), ctx.attr("merge_repeated")
+    xin = ctx.input("Input")
+    r = _oplib.ctc_align_op(xin, off, blank, merge) if xin.is_cuda else None
+    if r is not None:
+        ctx.set_output("Output", r[0], [r[1]])
+        return
+    x = xin.reshape(-1).tolist()
     out, new_off = [], [0]
     for i in range(len(off) - 1):
         prev = None
@@ -224,8 +252,14 @@ def _levenshtein(a, b):
 @register_op("edit_distance", ["Hyps", "Refs"], ["SequenceNum", "Out"], {"normalized": False}, grad=None,
              no_infer=True)
 def edit_distance(ctx):
-    h, r = ctx.input("Hyps").reshape(-1).tolist(), ctx.input("Refs").reshape(-1).tolist()
     ho, ro = _off(ctx, "Hyps"), _off(ctx, "Refs")
+    hyp = ctx.input("Hyps")
+    d = _oplib.edit_distance_op(hyp, ctx.input("Refs"), ho, ro, ctx.attr("normalized")) if hyp.is_cuda else None
+    if d is not None:
+        ctx.set_output("Out", d)
+        ctx.set_output("SequenceNum", torch.tensor([len(ho) - 1], dtype=torch.int64, device=hyp.device))
+        return
+    h, r = hyp.reshape(-1).tolist(), ctx.input("Refs").reshape(-1).tolist()
     out = []
     for i in range(len(ho) - 1):
         a, b = h[ho[i]:ho[i + 1]], r[ro[i]:ro[i + 1]]

@@ -96,6 +96,17 @@ _SIGS = {
     "pa_row_conv_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _P],
     "pa_argsort_rows": [_I, _P, _P, _P, _L, _I, _I, _P],
     "pa_accuracy": [_P, _P, _L, _I, _P, _P, _P, _P],
+    "pa_ctc_loss": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P],
+    "pa_roi_pool_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P, _P, _P],
+    "pa_roi_pool_bwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
+    "pa_edit_distance": [_P, _P, _P, _P, _I, _I, _P, _I, _P, _P],
+    "pa_ctc_align": [_P, _P, _I, _I, _I, _P, _P, _P],
+    "pa_mean_iou_hist": [_P, _P, _L, _I, _I, _P, _P, _P],
+    "pa_fake_quant": [_P, _L, _I, _P, _I, _I, _P, _P, _P, _P],
+    "pa_isfinite": [_P, _L, _I, _P, _P],
+    "pa_seq_pad": [_P, _P, _I, _I, _L, _P, _I, _I, _P, _P],
+    "pa_seq_unpad": [_P, _P, _I, _I, _L, _L, _I, _P, _P],
+    "pa_seq_scale": [_P, _P, _I, _L, _L, _P, _I, _P],
     "pa_dwconv_fwd": [_P, _P, _P, _P] + [_I] * 13 + [_P],
     "pa_dwconv_dgrad": [_P, _P, _P] + [_I] * 13 + [_P],
     "pa_dwconv_wgrad": [_P, _P, _P] + [_I] * 13 + [_P],

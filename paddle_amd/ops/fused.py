@@ -584,7 +584,8 @@ class _SoftmaxCEMeanFn(torch.autograd.Function):
         x, lab, lse, cnt = ctx.saved_tensors
         Nr, V = x.shape
         dl = torch.empty(Nr, dtype=torch.float32, device=x.device)
-        N.call("pa_ce_mean_bwd_rows", N.ptr(_c(g.float()).reshape(1)), N.ptr(cnt), N.ptr(dl), Nr, N.stream())
+        g1 = _c(g.float()).reshape(1)
+        N.call("pa_ce_mean_bwd_rows", N.ptr(g1), N.ptr(cnt), N.ptr(dl), Nr, N.stream())
         dx = x if ctx.inplace else torch.empty_like(x)
         N.call("pa_softmax_ce_bwd", N.dt(x), N.ptr(x), N.ptr(lab), None, N.ptr(lse), N.ptr(dl), N.ptr(dx),
                Nr, V, int(ctx.ignore_index), 1.0, N.stream())

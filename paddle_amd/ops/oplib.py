@@ -123,7 +123,8 @@ def mask_mul(d, mask, scale=1.0):
         return None
     d = d.contiguous()
     out = torch.empty_like(d)
-    N.call("pa_mask_mul", _DT[d.dtype], N.ptr(d), N.ptr(mask.contiguous()), N.ptr(out), d.numel(), float(scale),
+    mask = mask.contiguous()  # bound: a temporary passed to ptr() is freed before the launch
+    N.call("pa_mask_mul", _DT[d.dtype], N.ptr(d), N.ptr(mask), N.ptr(out), d.numel(), float(scale),
            N.stream())
     return out
 
@@ -154,7 +155,8 @@ def _lr(lr, dev):
 def sgd_(p, g, lr):
     if not _ok(p, g) or p.dtype != g.dtype or not p.is_contiguous():
         return None
-    N.call("pa_sgd", _DT[p.dtype], N.ptr(p), N.ptr(g.contiguous()), N.ptr(_lr(lr, p.device)), p.numel(), N.stream())
+    g, lr_t = g.contiguous(), _lr(lr, p.device)
+    N.call("pa_sgd", _DT[p.dtype], N.ptr(p), N.ptr(g), N.ptr(lr_t), p.numel(), N.stream())
     return p
 
 
@@ -164,7 +166,8 @@ def sgd_sparse_(p, rows, values, lr):
         return None
     rows = torch.as_tensor(rows, dtype=torch.int64).to(p.device)
     D = p.numel() // p.shape[0]
-    N.call("pa_sgd_sparse", N.ptr(p), N.ptr(rows), N.ptr(values.contiguous()), N.ptr(_lr(lr, p.device)),
+    values, lr_t = values.contiguous(), _lr(lr, p.device)
+    N.call("pa_sgd_sparse", N.ptr(p), N.ptr(rows), N.ptr(values), N.ptr(lr_t),
            rows.numel(), D, N.stream())
     return p
 
@@ -173,7 +176,8 @@ def adagrad_(p, g, m, lr, eps):
     if not (_ok(p, g, m) and p.dtype == g.dtype == m.dtype == torch.float32 and p.is_contiguous()
             and m.is_contiguous()):
         return None
-    N.call("pa_adagrad", N.ptr(p), N.ptr(g.contiguous()), N.ptr(m), N.ptr(_lr(lr, p.device)), p.numel(), float(eps),
+    g, lr_t = g.contiguous(), _lr(lr, p.device)
+    N.call("pa_adagrad", N.ptr(p), N.ptr(g), N.ptr(m), N.ptr(lr_t), p.numel(), float(eps),
            N.stream())
     return p
 
@@ -712,3 +716,225 @@ def split_op(x, sizes, axis=0):
         return None
     axis = axis % x.dim()
     return list(_tape.apply(_SplitFn, x, axis, list(sizes)))
+
+
+# ------------------------------------------------ sequence / detection / metric (seqdet.hip)
+
+
+def _i32(vals, dev):
+    return torch.as_tensor(np.asarray(vals, dtype=np.int32)).to(dev)
+
+
+class _CtcFn(torch.autograd.Function):
+    """CTC loss with the warp-ctc gradient contract (warpctc_op.h): the loss is the
+    plain -log p; ``norm_by_times`` only scales the gradient by 1/T_n."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, xoff, loff, blank, norm_by_times):
+        x = logits.detach().float().contiguous()
+        T, C = x.shape
+        n = len(xoff) - 1
+        lens = [b - a for a, b in zip(loff[:-1], loff[1:])]
+        smax = 2 * max(lens + [0]) + 1
+        dev = x.device
+        xo, lo = _i32(xoff, dev), _i32(loff, dev)
+        lab = labels.reshape(-1).to(torch.int32).contiguous()
+        if lab.numel() == 0:
+            lab = torch.zeros(1, dtype=torch.int32, device=dev)
+        lse = torch.empty(max(T, 1), dtype=torch.float32, device=dev)
+        alpha = torch.empty(max(T, 1) * smax, dtype=torch.float32, device=dev)
+        beta = torch.empty_like(alpha)
+        loss = torch.empty(n, dtype=torch.float32, device=dev)
+        grad = torch.empty_like(x)
+        N.call("pa_ctc_loss", N.ptr(x), N.ptr(xo), N.ptr(lab), N.ptr(lo), n, T, C, smax, int(blank), N.ptr(lse),
+               N.ptr(alpha), N.ptr(beta), N.ptr(loss), N.ptr(grad), N.stream())
+        tl = torch.as_tensor([b - a for a, b in zip(xoff[:-1], xoff[1:])], dtype=torch.float32)
+        seq = torch.repeat_interleave(torch.arange(n), tl.long()).to(dev)
+        ctx.save_for_backward(grad, seq, tl.to(dev))
+        ctx.norm, ctx.dt, ctx.xoff = norm_by_times, logits.dtype, xoff
+        return loss.reshape(n, 1).to(logits.dtype)
+
+    @staticmethod
+    def backward(ctx, dloss):
+        grad, seq, tl = ctx.saved_tensors
+        w = dloss.reshape(-1).float()
+        if ctx.norm:
+            w = w / tl.clamp(min=1)
+        g = seq_scale_op(grad, ctx.xoff, w)  # sequence_scale.cu: row *= w[sequence(row)]
+        return g.to(ctx.dt), None, None, None, None, None
+
+
+def ctc_loss_op(logits, labels, xoff, loff, blank=0, norm_by_times=False):
+    """Per-sequence CTC loss [N, 1] over LoD-packed logits [T_total, C] (softmax inside)."""
+    if not (_ENABLED and logits.is_cuda and logits.dim() == 2 and logits.dtype in _DT):
+        return None
+    if 2 * max([b - a for a, b in zip(loff[:-1], loff[1:])] + [0]) + 1 > 8192:
+        return None
+    return _tape.apply(_CtcFn, logits, labels, list(xoff), list(loff), int(blank), bool(norm_by_times))
+
+
+class _RoiPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, rois, bid, ph, pw, scale):
+        xc = x.float().contiguous()
+        B, C, H, W = xc.shape
+        R = rois.shape[0]
+        out = torch.empty(R, C, ph, pw, dtype=torch.float32, device=x.device)
+        am = torch.empty(R, C, ph, pw, dtype=torch.int64, device=x.device)
+        r = rois.float().contiguous()
+        N.call("pa_roi_pool_fwd", N.ptr(xc), N.ptr(r), N.ptr(bid), R, C, H, W, ph, pw, float(scale), N.ptr(out),
+               N.ptr(am), N.stream())
+        ctx.save_for_backward(am, bid)
+        ctx.shape, ctx.dt = (B, C, H, W), x.dtype
+        ctx.mark_non_differentiable(am)
+        return out.to(x.dtype), am
+
+    @staticmethod
+    def backward(ctx, dy, _dam):
+        am, bid = ctx.saved_tensors
+        B, C, H, W = ctx.shape
+        R, _, ph, pw = am.shape
+        dx = torch.zeros(B, C, H, W, dtype=torch.float32, device=am.device)
+        d = dy.float().contiguous()
+        N.call("pa_roi_pool_bwd", N.ptr(d), N.ptr(am), N.ptr(bid), R, C, H, W, ph, pw, N.ptr(dx), N.stream())
+        return dx.to(ctx.dt), None, None, None, None, None
+
+
+def roi_pool_op(x, rois, batch_ids, pooled_h, pooled_w, scale):
+    """(Out [R, C, ph, pw], Argmax int64) with roi_pool_op.cu's bin boundaries."""
+    if not (_ENABLED and x.is_cuda and x.dim() == 4 and x.dtype in _DT):
+        return None
+    bid = _i32(batch_ids if len(batch_ids) else [0], x.device)
+    return _tape.apply(_RoiPoolFn, x, rois, bid, int(pooled_h), int(pooled_w), float(scale))
+
+
+def edit_distance_op(hyps, refs, hoff, roff, normalized=False):
+    """Levenshtein distance per (hyp, ref) sequence pair, float32 [N, 1]."""
+    if not (_ENABLED and hyps.is_cuda):
+        return None
+    n = len(hoff) - 1
+    if n <= 0:
+        return None
+    dev = hyps.device
+    h = hyps.reshape(-1).to(torch.int64).contiguous()
+    r = refs.reshape(-1).to(torch.int64).contiguous()
+    h = h if h.numel() else torch.zeros(1, dtype=torch.int64, device=dev)
+    r = r if r.numel() else torch.zeros(1, dtype=torch.int64, device=dev)
+    wsw = max(b - a for a, b in zip(roff[:-1], roff[1:])) + 1
+    ws = torch.empty(n * 2 * wsw, dtype=torch.int32, device=dev)
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+    ho, ro = _i32(hoff, dev), _i32(roff, dev)  # held: a freed temporary's block would be reused
+    N.call("pa_edit_distance", N.ptr(h), N.ptr(ho), N.ptr(r), N.ptr(ro), n, wsw, N.ptr(ws),
+           int(normalized), N.ptr(out), N.stream())
+    return out.reshape(n, 1)
+
+
+def ctc_align_op(x, offsets, blank=0, merge_repeated=True):
+    """(int64 [M, 1] aligned tokens, new level-0 offsets); one -1 when all were removed."""
+    if not (_ENABLED and x.is_cuda):
+        return None
+    n = len(offsets) - 1
+    if n <= 0:
+        return None
+    dev = x.device
+    xi = x.reshape(-1).to(torch.int64).contiguous()
+    if xi.numel() == 0:
+        return None
+    out = torch.empty_like(xi)
+    counts = torch.empty(n, dtype=torch.int32, device=dev)
+    off = _i32(offsets, dev)
+    N.call("pa_ctc_align", N.ptr(xi), N.ptr(off), n, int(blank), int(merge_repeated), N.ptr(out),
+           N.ptr(counts), N.stream())
+    cnt = counts.cpu().tolist()
+    if sum(cnt) == 0:
+        return torch.full((1, 1), -1, dtype=torch.int64, device=dev), [0, 1]
+    idx = torch.cat([torch.arange(s, s + c) for s, c in zip(offsets[:-1], cnt)]).to(dev)
+    new_off = np.concatenate([[0], np.cumsum(cnt)]).astype(int).tolist()
+    return out.index_select(0, idx).reshape(-1, 1), new_off
+
+
+def mean_iou_hist(pred, label, num_classes):
+    """(correct int32 [C], wrong int32 [C]) class histograms of mean_iou_op.cu."""
+    if not (_ENABLED and pred.is_cuda):
+        return None
+    p, l = pred.reshape(-1).contiguous(), label.reshape(-1).contiguous()
+    if p.dtype not in (torch.int32, torch.int64) or l.dtype != p.dtype or p.numel() != l.numel():
+        return None
+    correct = torch.zeros(num_classes, dtype=torch.int32, device=p.device)
+    wrong = torch.zeros(num_classes, dtype=torch.int32, device=p.device)
+    N.call("pa_mean_iou_hist", N.ptr(p), N.ptr(l), p.numel(), int(num_classes), int(p.dtype == torch.int64),
+           N.ptr(correct), N.ptr(wrong), N.stream())
+    return correct, wrong
+
+
+def fake_quant_op(x, bit_length=8, in_scale=None, use_in_scale=False, clip=False):
+    """(round(x / s * (2^(b-1) - 1)), s): s = |x|max (abs_max), max(|x|max, in_scale)
+    (range_abs_max training, with clip) or in_scale (is_test)."""
+    if not (_ENABLED and x.is_cuda and x.dtype == torch.float32):
+        return None
+    xc = x.contiguous()
+    amax = torch.zeros(1, dtype=torch.int32, device=x.device)
+    out = torch.empty_like(xc)
+    s = torch.empty(1, dtype=torch.float32, device=x.device)
+    ins = in_scale.reshape(1).float().contiguous() if in_scale is not None else None
+    N.call("pa_fake_quant", N.ptr(xc), xc.numel(), int(bit_length), N.ptr(ins), int(use_in_scale), int(clip),
+           N.ptr(amax), N.ptr(out), N.ptr(s), N.stream())
+    return out, s
+
+
+def isfinite_op(x, bad=None):
+    """bool [1]: every element finite.  With ``bad`` (int32 [1] on the device) the
+    check only ORs into that flag (no host sync), so a caller can test many tensors and
+    read one flag; returns False when the kernel does not cover ``x``."""
+    if not _ok(x):
+        return None if bad is None else False
+    xc = x.contiguous()
+    flag = torch.zeros(1, dtype=torch.int32, device=x.device) if bad is None else bad
+    N.call("pa_isfinite", N.ptr(xc), xc.numel(), _DT[x.dtype], N.ptr(flag), N.stream())
+    return (flag == 0) if bad is None else True
+
+
+def seq_pad_op(x, offsets, maxlen, pad_value):
+    """LoD rows [T_total, ...] -> [N, maxlen, ...]; pad_value scalar or one row."""
+    if not _ok(x) or x.dim() < 1:
+        return None
+    n = len(offsets) - 1
+    xc = x.contiguous()
+    D = xc.numel() // max(xc.shape[0], 1) if xc.shape[0] else int(np.prod(xc.shape[1:]))
+    pv = torch.as_tensor(pad_value, dtype=x.dtype).reshape(-1).to(x.device).contiguous()
+    if pv.numel() not in (1, D):
+        return None
+    out = torch.empty((n, maxlen) + tuple(xc.shape[1:]), dtype=x.dtype, device=x.device)
+    off = _i32(offsets, x.device)
+    N.call("pa_seq_pad", N.ptr(xc), N.ptr(off), n, int(maxlen), D, N.ptr(pv), pv.numel(),
+           xc.element_size(), N.ptr(out), N.stream())
+    return out
+
+
+def seq_unpad_op(p, offsets):
+    """[N, maxlen, ...] -> LoD rows [T_total, ...]."""
+    if not _ok(p) or p.dim() < 2:
+        return None
+    n, maxlen = p.shape[0], p.shape[1]
+    pc = p.contiguous()
+    D = int(np.prod(pc.shape[2:])) if pc.dim() > 2 else 1
+    rows = offsets[-1]
+    out = torch.empty((rows,) + tuple(pc.shape[2:]), dtype=p.dtype, device=p.device)
+    off = _i32(offsets, p.device)
+    N.call("pa_seq_unpad", N.ptr(pc), N.ptr(off), n, maxlen, D, rows, pc.element_size(),
+           N.ptr(out), N.stream())
+    return out
+
+
+def seq_scale_op(x, offsets, scales):
+    """x[row] * scales[sequence(row)] (sequence_scale.cu), returned as a new tensor."""
+    if not _ok(x):
+        return None
+    out = x.contiguous().clone()
+    n = len(offsets) - 1
+    D = out.numel() // max(out.shape[0], 1)
+    sc = torch.as_tensor(scales, dtype=torch.float32).reshape(-1).to(x.device).contiguous()
+    off = _i32(offsets, x.device)
+    N.call("pa_seq_scale", N.ptr(out), N.ptr(off), n, D, out.shape[0], N.ptr(sc), _DT[x.dtype],
+           N.stream())
+    return out

@@ -388,3 +388,56 @@ def test_crf_tagging_model_trains_and_decodes():
             first = float(l[0]) if first is None else first
     assert float(l[0]) < first
     assert (np.asarray(p).reshape(-1) == ys.reshape(-1)).mean() > 0.7
+
+
+def test_roi_pool_reference_bins():
+    """roi_pool_op.cu semantics: corners rounded half away from zero, floor/ceil bins
+    offset by the ROI start and clipped, empty bins 0 with Argmax -1."""
+    x = rng.randn(2, 3, 12, 10).astype("float32")
+    rois = np.array([[0, 0, 7, 7], [2.4, 1.5, 9.6, 11.2], [5, 5, 4, 4], [-3, -2, 3, 20], [1, 1, 1, 1]], "float32")
+    t = OpTest()
+    t.op_type, t.inputs = "roi_pool", {"X": x, "ROIs": (rois, [[3, 2]])}
+    t.outputs = {"Out": np.zeros((5, 3, 3, 4), "float32")}
+    t.attrs = {"spatial_scale": 0.8, "pooled_height": 3, "pooled_width": 4}
+    prog, _, feed, _, ov, _ = t._build()
+    o, a = fluid.Executor(fluid.CPUPlace()).run(prog, feed=feed, fetch_list=[ov["Out"][0], ov["Argmax"][0]],
+                                                scope=core.Scope())
+    o, a = np.asarray(o), np.asarray(a)
+
+    def rnd(v):
+        return int(math.copysign(math.floor(abs(v) + 0.5), v))
+
+    for r, b in enumerate([0, 0, 0, 1, 1]):
+        x1, y1, x2, y2 = [rnd(float(v) * 0.8) for v in rois[r]]
+        rw, rh = max(x2 - x1 + 1, 1), max(y2 - y1 + 1, 1)
+        for c, ph, pw in itertools.product(range(3), range(3), range(4)):
+            hs, he = [min(max(f(v * rh / 3) + y1, 0), 12) for f, v in ((math.floor, ph), (math.ceil, ph + 1))]
+            ws, we = [min(max(f(v * rw / 4) + x1, 0), 10) for f, v in ((math.floor, pw), (math.ceil, pw + 1))]
+            m, mi = (0.0, -1) if (he <= hs or we <= ws) else (-3e38, -1)
+            for h, w in itertools.product(range(hs, he), range(ws, we)):
+                if x[b, c, h, w] > m:
+                    m, mi = x[b, c, h, w], h * 10 + w
+            assert o[r, c, ph, pw] == np.float32(m) and a[r, c, ph, pw] == mi
+
+
+def test_warpctc_norm_by_times_scales_only_the_gradient():
+    C, xl, ll = 4, [5, 4], [2, 1]
+    x = rng.uniform(-1, 1, (9, C)).astype("float32")
+    lab = np.array([1, 2, 3], "int64").reshape(-1, 1)
+    from paddle_amd.framework import registry as R
+
+    outs = {}
+    for norm in (False, True):
+        xt = torch.from_numpy(x).requires_grad_(True)
+        ctx = R.KernelContext("warpctc", {"Logits": [core.LoDTensor(xt, [[0, 5, 9]])],
+                                          "Label": [core.LoDTensor(torch.from_numpy(lab), [[0, 2, 3]])]},
+                              {"Loss": ["l"], "WarpCTCGrad": ["g"]},
+                              dict(R.get_op_info("warpctc").attrs, norm_by_times=norm))
+        R.run_kernel(R.get_op_info("warpctc"), ctx)
+        loss = ctx.results["Loss"][0]
+        loss = loss.tensor if isinstance(loss, core.LoDTensor) else loss
+        loss.sum().backward()
+        outs[norm] = (loss.detach().clone(), xt.grad.clone())
+    assert torch.equal(outs[False][0], outs[True][0])
+    scale = torch.tensor([1 / 5] * 5 + [1 / 4] * 4)[:, None]
+    torch.testing.assert_close(outs[True][1], outs[False][1] * scale)
