@@ -467,6 +467,14 @@ def fused_elemwise_activation(ctx):
     """{scale, relu} o {elementwise_add, elementwise_mul} in either order (fused_elemwise_activation_op.cc)."""
     x, y = ctx.input("X"), ctx.input("Y")
     f0, f1 = ctx.attr("functor_list")
+    if x.is_cuda:
+        r = _oplib.fused_ew_act(x, y, (f0, f1), ctx.attr("axis"), ctx.attr("scale"),
+                                ctx.has_output("IntermediateOut"))
+        if r is not None:
+            ctx.set_output("Out", r[0])
+            if ctx.has_output("IntermediateOut"):
+                ctx.set_output("IntermediateOut", r[1])
+            return
 
     def unary(name, t):
         if name == "relu":

@@ -24,6 +24,22 @@ def _lr(ctx):
     return ctx.input("LearningRate").reshape(-1)[0:1]
 
 
+def _native(ctx, kind, p, g, states, outs, lr=True, **h):
+    """Run the fused optim_ext.hip update on clones of Param / states; True when done."""
+    if not p.is_cuda:
+        return False
+    p2 = p.clone()
+    s2 = [s.clone() if s is not None else None for s in states]
+    lr_t = ctx.input("LearningRate") if lr else None
+    if _oplib.opt_update_(kind, p2, g, s2, lr_t, **h) is None:
+        return False
+    ctx.set_output("ParamOut", p2)
+    for name, t in zip(outs, s2):
+        if name is not None and t is not None:
+            ctx.set_output(name, t)
+    return True
+
+
 @register_op("sgd", ["Param", "Grad", "LearningRate"], ["ParamOut"], {}, grad=None, no_infer=True)
 def sgd(ctx):
     p = ctx.input("Param")
@@ -71,9 +87,11 @@ def momentum(ctx):
              {"mu": 0.9, "lars_coeff": 0.001, "lars_weight_decay": 0.0005}, grad=None, no_infer=True)
 def lars_momentum(ctx):
     p, v, g = ctx.input("Param"), ctx.input("Velocity"), _grad(ctx).tensor
+    wd = ctx.attr("lars_weight_decay")
+    if _native(ctx, "lars", p, g, [v], ["VelocityOut"], mu=ctx.attr("mu"), coeff=ctx.attr("lars_coeff"), wd=wd):
+        return
     lr = _lr(ctx)
     pn, gn = p.norm(), g.norm()
-    wd = ctx.attr("lars_weight_decay")
     local = lr * ctx.attr("lars_coeff") * pn / (gn + wd * pn + 1e-12)
     v2 = ctx.attr("mu") * v + local * (g + wd * p)
     ctx.set_output("ParamOut", p - v2)
@@ -126,6 +144,9 @@ def adam(ctx):
 def adamax(ctx):
     p, m, u, g = ctx.input("Param"), ctx.input("Moment"), ctx.input("InfNorm"), _grad(ctx).tensor
     b1, b2, eps = ctx.attr("beta1"), ctx.attr("beta2"), ctx.attr("epsilon")
+    if _native(ctx, "adamax", p, g, [m, u], ["MomentOut", "InfNormOut"], bp1=ctx.input("Beta1Pow"), b1=b1, b2=b2,
+               eps=eps):
+        return
     lr, bp1 = _lr(ctx), ctx.input("Beta1Pow").reshape(-1)[0]
     m2 = b1 * m + (1 - b1) * g
     u2 = torch.maximum(b2 * u + eps, g.abs())
@@ -166,6 +187,8 @@ def adagrad(ctx):
 def decayed_adagrad(ctx):
     p, m, g = ctx.input("Param"), ctx.input("Moment"), _grad(ctx).tensor
     d, eps, lr = ctx.attr("decay"), ctx.attr("epsilon"), _lr(ctx)
+    if _native(ctx, "decayed_adagrad", p, g, [m], ["MomentOut"], decay=d, eps=eps):
+        return
     m2 = d * m + (1 - d) * g * g
     ctx.set_output("ParamOut", p - lr * g / (torch.sqrt(m2) + eps))
     ctx.set_output("MomentOut", m2)
@@ -178,6 +201,9 @@ def adadelta(ctx):
     p, g = ctx.input("Param"), _grad(ctx).tensor
     ag, au = ctx.input("AvgSquaredGrad"), ctx.input("AvgSquaredUpdate")
     rho, eps = ctx.attr("rho"), ctx.attr("epsilon")
+    if _native(ctx, "adadelta", p, g, [ag, au], ["AvgSquaredGradOut", "AvgSquaredUpdateOut"], lr=False, rho=rho,
+               eps=eps):
+        return
     ag2 = rho * ag + (1 - rho) * g * g
     upd = -torch.sqrt((au + eps) / (ag2 + eps)) * g
     au2 = rho * au + (1 - rho) * upd * upd
@@ -192,6 +218,10 @@ def adadelta(ctx):
 def rmsprop(ctx):
     p, ms, mom, g = ctx.input("Param"), ctx.input("MeanSquare"), ctx.input("Moment"), _grad(ctx).tensor
     eps, rho, mu, lr = ctx.attr("epsilon"), ctx.attr("decay"), ctx.attr("momentum"), _lr(ctx)
+    mg = ctx.input("MeanGrad") if ctx.attr("centered") else None
+    if _native(ctx, "rmsprop", p, g, [ms, mom, mg], ["MeanSquareOut", "MomentOut", "MeanGradOut"], rho=rho, mu=mu,
+               eps=eps):
+        return
     ms2 = rho * ms + (1 - rho) * g * g
     if ctx.attr("centered"):
         mg = ctx.input("MeanGrad")
@@ -212,6 +242,8 @@ def ftrl(ctx):
     p, sq, lin, g = (ctx.input("Param"), ctx.input("SquaredAccumulator"), ctx.input("LinearAccumulator"),
                      _grad(ctx).tensor)
     l1, l2, lp, lr = ctx.attr("l1"), ctx.attr("l2"), ctx.attr("lr_power"), _lr(ctx)
+    if _native(ctx, "ftrl", p, g, [sq, lin], ["SquaredAccumOut", "LinearAccumOut"], l1=l1, l2=l2, lr_power=lp):
+        return
     nsq = sq + g * g
     if lp == -0.5:
         sigma = (torch.sqrt(nsq) - torch.sqrt(sq)) / lr
@@ -231,6 +263,8 @@ def ftrl(ctx):
 def proximal_gd(ctx):
     p, g, lr = ctx.input("Param"), _grad(ctx).tensor, _lr(ctx)
     l1, l2 = ctx.attr("l1"), ctx.attr("l2")
+    if _native(ctx, "proximal", p, g, [None], [None], l1=l1, l2=l2):
+        return
     prox = p - lr * g
     out = torch.sign(prox) * torch.clamp(prox.abs() - lr * l1, min=0) / (1 + lr * l2)
     ctx.set_output("ParamOut", out)
@@ -241,6 +275,8 @@ def proximal_gd(ctx):
 def proximal_adagrad(ctx):
     p, m, g, lr = ctx.input("Param"), ctx.input("Moment"), _grad(ctx).tensor, _lr(ctx)
     l1, l2 = ctx.attr("l1"), ctx.attr("l2")
+    if _native(ctx, "proximal", p, g, [m], ["MomentOut"], l1=l1, l2=l2):
+        return
     m2 = m + g * g
     lr_t = lr / torch.sqrt(m2)
     prox = p - lr_t * g

@@ -96,6 +96,15 @@ _SIGS = {
     "pa_row_conv_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _P],
     "pa_argsort_rows": [_I, _P, _P, _P, _L, _I, _I, _P],
     "pa_accuracy": [_P, _P, _L, _I, _P, _P, _P, _P],
+    "pa_fused_ew_act": [_I, _I, _I, _I, _F, _P, _P, _P, _P, _L, _L, _L, _P],
+    "pa_fused_ew_act_bwd": [_I, _I, _I, _I, _F, _P, _P, _P, _P, _P, _L, _L, _L, _P],
+    "pa_opt_adamax": [_P, _P, _P, _P, _P, _P, _F, _F, _F, _L, _P],
+    "pa_opt_decayed_adagrad": [_P, _P, _P, _P, _F, _F, _L, _P],
+    "pa_opt_adadelta": [_P, _P, _P, _P, _F, _F, _L, _P],
+    "pa_opt_rmsprop": [_P, _P, _P, _P, _P, _P, _F, _F, _F, _L, _P],
+    "pa_opt_ftrl": [_P, _P, _P, _P, _P, _F, _F, _F, _L, _P],
+    "pa_opt_proximal": [_P, _P, _P, _P, _F, _F, _L, _P],
+    "pa_opt_lars": [_P, _P, _P, _P, _P, _F, _F, _F, _L, _P],
     "pa_ctc_loss": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P],
     "pa_roi_pool_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P, _P, _P],
     "pa_roi_pool_bwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P],

@@ -938,3 +938,109 @@ def seq_scale_op(x, offsets, scales):
     N.call("pa_seq_scale", N.ptr(out), N.ptr(off), n, D, out.shape[0], N.ptr(sc), _DT[x.dtype],
            N.stream())
     return out
+
+
+# ------------------------------------------------------------------ optimizers (optim_ext.hip)
+
+
+def opt_update_(kind, p, g, states, lr, **h):
+    """In-place fp32 update of ``p`` and its ``states`` (list; ``None`` entries are
+    optional states such as RMSProp's MeanGrad).  ``kind``: adamax (h: bp1, b1, b2,
+    eps), decayed_adagrad (decay, eps), adadelta (rho, eps), rmsprop (rho, mu, eps),
+    ftrl (l1, l2, lr_power), proximal (l1, l2), lars (mu, coeff, wd).  Returns None
+    when the kernel does not cover the tensors (then the caller runs its torch path)."""
+    ts = [p, g] + [s for s in states if s is not None]
+    if not (_ENABLED and all(t.is_cuda and t.dtype == torch.float32 for t in ts)):
+        return None
+    if not (p.is_contiguous() and all(s is None or s.is_contiguous() for s in states)):
+        return None
+    n = p.numel()
+    if any(t.numel() != n for t in ts):
+        return None
+    g = g.contiguous()
+    lr_t = _lr(lr, p.device).reshape(-1)[:1].contiguous() if lr is not None else None
+    st = [N.ptr(s) for s in states]
+    if kind == "adamax":
+        bp1 = _lr(h["bp1"], p.device).reshape(-1)[:1].contiguous()
+        N.call("pa_opt_adamax", N.ptr(p), N.ptr(g), *st, N.ptr(lr_t), N.ptr(bp1), h["b1"], h["b2"], h["eps"], n,
+               N.stream())
+    elif kind == "decayed_adagrad":
+        N.call("pa_opt_decayed_adagrad", N.ptr(p), N.ptr(g), *st, N.ptr(lr_t), h["decay"], h["eps"], n, N.stream())
+    elif kind == "adadelta":
+        N.call("pa_opt_adadelta", N.ptr(p), N.ptr(g), *st, h["rho"], h["eps"], n, N.stream())
+    elif kind == "rmsprop":
+        N.call("pa_opt_rmsprop", N.ptr(p), N.ptr(g), *st, N.ptr(lr_t), h["rho"], h["mu"], h["eps"], n, N.stream())
+    elif kind == "ftrl":
+        N.call("pa_opt_ftrl", N.ptr(p), N.ptr(g), *st, N.ptr(lr_t), h["l1"], h["l2"], h["lr_power"], n, N.stream())
+    elif kind == "proximal":
+        N.call("pa_opt_proximal", N.ptr(p), N.ptr(g), *st, N.ptr(lr_t), h["l1"], h["l2"], n, N.stream())
+    elif kind == "lars":
+        acc = torch.zeros(2, dtype=torch.float32, device=p.device)
+        N.call("pa_opt_lars", N.ptr(p), N.ptr(g), *st, N.ptr(lr_t), N.ptr(acc), h["mu"], h["coeff"], h["wd"], n,
+               N.stream())
+    else:
+        raise ValueError(kind)
+    return p
+
+
+# ------------------------------------------------------------------ fused_elemwise_activation (fused_ew.hip)
+
+
+class _FusedEwActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, y, mode, bop, uop, scale, post, want_inter):
+        x, y = x.contiguous(), y.contiguous()
+        out = torch.empty_like(x)
+        inter = torch.empty_like(x) if want_inter else None
+        N.call("pa_fused_ew_act", _DT[x.dtype], mode, bop, uop, float(scale), N.ptr(x), N.ptr(y), N.ptr(out),
+               N.ptr(inter), x.numel(), y.numel(), post, N.stream())
+        ctx.save_for_backward(x, y)
+        ctx.conf = (mode, bop, uop, float(scale), post)
+        if inter is not None:
+            ctx.mark_non_differentiable(inter)
+        return out, inter
+
+    @staticmethod
+    def backward(ctx, dout, _dinter):
+        x, y = ctx.saved_tensors
+        mode, bop, uop, scale, post = ctx.conf
+        dout = dout.contiguous()
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dyf = torch.empty(x.shape, dtype=torch.float32, device=x.device) if ctx.needs_input_grad[1] else None
+        N.call("pa_fused_ew_act_bwd", _DT[x.dtype], mode, bop, uop, scale, N.ptr(x), N.ptr(y), N.ptr(dout),
+               N.ptr(dx), N.ptr(dyf), x.numel(), y.numel(), post, N.stream())
+        dy = None
+        if dyf is not None:
+            ny = y.numel()
+            dy = dyf.view(-1, ny, post).sum((0, 2)) if dyf.numel() != ny else dyf.view(-1)
+            dy = dy.reshape(y.shape).to(y.dtype)
+        return dx, dy, None, None, None, None, None, None
+
+
+def fused_ew_act(x, y, functors, axis=-1, scale=0.0, want_inter=False):
+    """(Out, IntermediateOut or None) of fused_elemwise_activation for
+    functors in {elementwise_add, elementwise_mul} x {relu, scale}; None if uncovered."""
+    f0, f1 = functors
+    bops = {"elementwise_add": 0, "elementwise_mul": 1}
+    uops = {"relu": 0, "scale": 1}
+    if f0 in bops and f1 in uops:
+        mode, bop, uop = 0, bops[f0], uops[f1]
+    elif f0 in uops and f1 in bops:
+        mode, bop, uop = 1, bops[f1], uops[f0]
+    else:
+        return None
+    if not _ok(x, y) or x.dtype != y.dtype or y.numel() == 0:
+        return None
+    if tuple(y.shape) == tuple(x.shape):
+        post = 1
+        yv = y
+    else:
+        ax = axis if axis >= 0 else x.dim() - y.dim()
+        ys = list(y.shape)
+        while ys and ys[-1] == 1 and len(ys) > 1:  # trailing 1s (Paddle trims them)
+            ys.pop()
+        if ax < 0 or ax + len(ys) > x.dim() or list(x.shape[ax:ax + len(ys)]) != ys:
+            return None
+        post = int(np.prod(x.shape[ax + len(ys):])) if ax + len(ys) < x.dim() else 1
+        yv = y
+    return _tape.apply(_FusedEwActFn, x, yv, mode, bop, uop, scale, post, bool(want_inter))
