@@ -96,6 +96,9 @@ _SIGS = {
     "pa_row_conv_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _P],
     "pa_argsort_rows": [_I, _P, _P, _P, _L, _I, _I, _P],
     "pa_accuracy": [_P, _P, _L, _I, _P, _P, _P, _P],
+    "pa_iou_matrix": [_P, _P, _I, _I, _I, _P, _P],
+    "pa_box_coder": [_I, _P, _P, _P, _I, _I, _I, _P, _P],
+    "pa_nms_bitmask": [_P, _P, _P, _I, _I, _I, _I, _F, _I, _P, _P],
     "pa_fused_ew_act": [_I, _I, _I, _I, _F, _P, _P, _P, _P, _L, _L, _L, _P],
     "pa_fused_ew_act_bwd": [_I, _I, _I, _I, _F, _P, _P, _P, _P, _P, _L, _L, _L, _P],
     "pa_opt_adamax": [_P, _P, _P, _P, _P, _P, _F, _F, _F, _L, _P],

@@ -1044,3 +1044,90 @@ def fused_ew_act(x, y, functors, axis=-1, scale=0.0, want_inter=False):
         post = int(np.prod(x.shape[ax + len(ys):])) if ax + len(ys) < x.dim() else 1
         yv = y
     return _tape.apply(_FusedEwActFn, x, yv, mode, bop, uop, scale, post, bool(want_inter))
+
+
+# ------------------------------------------------------------------ detection (detect.hip)
+
+
+def _f32c(t):
+    return t.float().contiguous()
+
+
+def iou_matrix_op(a, b, normalized=True):
+    """[Na, Nb] IoU of box sets a [Na, 4], b [Nb, 4] (iou_similarity_op.h)."""
+    if not (_ENABLED and a.is_cuda and b.is_cuda and a.dim() == 2 and b.dim() == 2):
+        return None
+    a, b = _f32c(a), _f32c(b)
+    out = torch.empty(a.shape[0], b.shape[0], dtype=torch.float32, device=a.device)
+    N.call("pa_iou_matrix", N.ptr(a), N.ptr(b), a.shape[0], b.shape[0], int(normalized), N.ptr(out), N.stream())
+    return out
+
+
+def box_coder_op(decode, prior, var, target, normalized=True):
+    """encode_center_size: target [N, 4] -> [N, M, 4]; decode_center_size: target
+    [N, M, 4] (or [N, 4] as [N, 1, 4] against M == 1 ...) -> boxes [N, M, 4]."""
+    if not (_ENABLED and prior.is_cuda and target.is_cuda):
+        return None
+    pr = _f32c(prior)
+    M = pr.shape[0]
+    v = _f32c(var) if var is not None else None
+    if v is not None and v.numel() != M * 4:
+        return None
+    t = _f32c(target)
+    if decode:
+        if t.dim() == 2:
+            t = t.unsqueeze(1)
+        if t.dim() != 3 or t.shape[1] != M:
+            return None
+        n = t.shape[0]
+    else:
+        if t.dim() != 2:
+            return None
+        n = t.shape[0]
+    out = torch.empty(n, M, 4, dtype=torch.float32, device=t.device)
+    N.call("pa_box_coder", int(decode), N.ptr(pr), N.ptr(v), N.ptr(t), n, M, int(normalized), N.ptr(out), N.stream())
+    return out
+
+
+def multiclass_nms_op(boxes, scores, background, score_thr, nms_top_k, nms_thr, keep_top_k, normalized=True):
+    """(rows [R, 6] = (label, score, x1, y1, x2, y2), level-0 offsets) of
+    multiclass_nms_op.cc for boxes [N, M, 4], scores [N, C, M]; per-class greedy NMS
+    on the device (bitmask kernel).  None when uncovered (top-K > 512)."""
+    if not (_ENABLED and boxes.is_cuda and scores.is_cuda and boxes.dim() == 3 and scores.dim() == 3):
+        return None
+    Nn, C, M = scores.shape
+    K = M if nms_top_k is None or nms_top_k < 0 else min(int(nms_top_k), M)
+    if K <= 0 or K > 512 or boxes.shape[1] != M:
+        return None
+    dev = scores.device
+    s = scores.float()
+    valid = s > score_thr
+    masked = torch.where(valid, s, torch.full_like(s, -float("inf")))
+    ss, order = torch.sort(masked, dim=-1, descending=True, stable=True)
+    ss, order = ss[..., :K].contiguous(), order[..., :K].to(torch.int32).contiguous()
+    count = valid.sum(-1).clamp(max=K).to(torch.int32)
+    if 0 <= background < C:
+        count[:, background] = 0
+    count = count.contiguous()
+    keep = torch.empty(Nn, C, K, dtype=torch.uint8, device=dev)
+    bx = _f32c(boxes)
+    N.call("pa_nms_bitmask", N.ptr(bx), N.ptr(order), N.ptr(count), Nn * C, C, M, K, float(nms_thr), int(normalized),
+           N.ptr(keep), N.stream())
+    kept = keep.bool()
+    flat = torch.where(kept, ss, torch.full_like(ss, -float("inf"))).reshape(Nn, C * K)
+    fs, fi = torch.sort(flat, dim=-1, descending=True, stable=True)  # class-major, then score: as the host loop
+    nkeep = kept.reshape(Nn, -1).sum(-1)
+    if keep_top_k is not None and keep_top_k > -1:
+        nkeep = nkeep.clamp(max=int(keep_top_k))
+    T = int(nkeep.max().item()) if Nn else 0
+    counts = nkeep.cpu().tolist()
+    if T == 0:
+        return torch.full((1, 6), -1.0, dtype=torch.float32, device=dev), [0, 1]
+    fs, fi = fs[:, :T], fi[:, :T]
+    cls = (fi // K).float()
+    bidx = order.reshape(Nn, C * K).gather(1, fi).long()
+    bsel = bx.gather(1, bidx.unsqueeze(-1).expand(Nn, T, 4))
+    rows = torch.cat([cls.unsqueeze(-1), fs.unsqueeze(-1), bsel], -1)  # [N, T, 6]
+    sel = torch.arange(T, device=dev).unsqueeze(0) < torch.as_tensor(counts, device=dev).unsqueeze(1)
+    off = np.concatenate([[0], np.cumsum(counts)]).astype(int).tolist()
+    return rows[sel], off
