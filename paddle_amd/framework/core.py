@@ -159,11 +159,19 @@ def check_lod(lod, numel_rows=None):
 class LoDTensor:
     """Dense tensor + level-of-detail offsets (lod_tensor.h:110)."""
 
-    __slots__ = ("_t", "_lod")
+    __slots__ = ("_t", "_lod", "_layout")
 
-    def __init__(self, tensor=None, lod=None):
+    def __init__(self, tensor=None, lod=None, layout="AnyLayout"):
         self._t = tensor
         self._lod = [list(map(int, l)) for l in (lod or [])]
+        self._layout = layout  # DataLayout tag read by the data transform (tensor.h layout_)
+
+    @property
+    def layout(self):
+        return self._layout
+
+    def set_layout(self, layout):
+        self._layout = layout
 
     # -- storage
     @property

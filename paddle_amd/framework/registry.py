@@ -81,6 +81,11 @@ class OpInfo:
     comment: str = ""
     no_infer: bool = False  # skip compile-time meta inference (side-effecting ops)
     share_lod: bool = True
+    # typed kernels (op_kernel_type.register_op_kernel): OpKernelType -> fn; None = the
+    # single place-agnostic ``kernel``
+    kernels: dict | None = None
+    expected_kernel_type: callable = None  # ctx -> OpKernelType (GetExpectedKernelType override)
+    host_slots: tuple | None = None  # input slots the data transform leaves in place
 
     def input_names(self):
         return [s.name for s in self.inputs]
@@ -239,8 +244,23 @@ class KernelContext:
         return torch.float32
 
 
+def call_kernel(info: OpInfo, ctx: KernelContext):
+    """OperatorWithKernel::RunImpl: typed kernel selection + input data transform
+    (op_kernel_type.py) when the op registered typed kernels, else its one kernel.
+    Shape inference on meta tensors always runs the place-agnostic kernel."""
+    if info.kernels and not ctx.meta:
+        from . import op_kernel_type as K
+
+        fn, kt = K.select(info, K.expected_kernel_type(info, ctx))
+        if kt is not None:
+            K.prepare_inputs(info, ctx, kt)
+        fn(ctx)
+    else:
+        info.kernel(ctx)
+
+
 def run_kernel(info: OpInfo, ctx: KernelContext):
-    info.kernel(ctx)
+    call_kernel(info, ctx)
     if info.share_lod:
         _default_share_lod(info, ctx)
     return ctx.results
@@ -360,7 +380,7 @@ def run_kernel_stash(info: OpInfo, ctx: KernelContext):
                 new.append(v)
         ctx.ins[s.name] = new
     with torch.enable_grad():
-        info.kernel(ctx)
+        call_kernel(info, ctx)
     if info.share_lod:
         _default_share_lod(info, ctx)
     graph_outs = {}
@@ -439,7 +459,7 @@ def auto_grad_kernel(fwd: OpInfo, ctx: KernelContext):
     fctx = KernelContext(fwd.type, fins, {s.name: [f"{s.name}#{k}" for k in range(max(1, len(ctx.input_values(s.name))))]
                                           for s in fwd.outputs}, ctx.attrs, ctx.place)
     with torch.enable_grad():
-        fwd.kernel(fctx)
+        call_kernel(fwd, fctx)
     outs, gouts = [], []
     for s in fwd.outputs:
         gvals = ctx.input_values(s.name + GRAD_SUFFIX)

@@ -20,6 +20,7 @@ import math
 import numpy as np
 import torch
 
+from ..framework.op_kernel_type import LibraryType, register_op_kernel
 from ..framework.registry import register_op
 from ..ops import oplib as _oplib
 
@@ -110,12 +111,6 @@ def box_coder(ctx):
     prior, tgt = ctx.input("PriorBox"), ctx.input("TargetBox")
     var = ctx.input("PriorBoxVar") if ctx.has_input("PriorBoxVar") else None
     norm = ctx.attr("box_normalized")
-    if prior.is_cuda and not ctx.meta:
-        dec = not ctx.attr("code_type").lower().startswith("encode")
-        r = _oplib.box_coder_op(dec, prior, var, tgt, norm)
-        if r is not None:
-            ctx.set_output("OutputBox", r.to(tgt.dtype))
-            return
     pw, ph = _wh(prior, norm)
     pcx, pcy = (prior[:, 0] + prior[:, 2]) / 2, (prior[:, 1] + prior[:, 3]) / 2
     if ctx.attr("code_type").lower().startswith("encode"):
@@ -152,10 +147,7 @@ def _iou_matrix(a, b, normalized=True):
 @register_op("iou_similarity", ["X", "Y"], ["Out"], {"box_normalized": True}, grad=None)
 def iou_similarity(ctx):
     x, y = ctx.input("X"), ctx.input("Y")
-    r = _oplib.iou_matrix_op(x, y, ctx.attr("box_normalized")) if x.is_cuda and not ctx.meta else None
-    if r is None:
-        r = _iou_matrix(x, y, ctx.attr("box_normalized"))
-    ctx.set_output("Out", r.to(x.dtype), ctx.input_lod("X"))
+    ctx.set_output("Out", _iou_matrix(x, y, ctx.attr("box_normalized")), ctx.input_lod("X"))
 
 
 @register_op("bipartite_match", ["DistMat"], ["ColToRowMatchIndices", "ColToRowMatchDist"],
@@ -281,13 +273,6 @@ def _nms(boxes, scores, thr, top_k, eta=1.0, normalized=True):
 def multiclass_nms(ctx):
     boxes, scores = ctx.input("BBoxes").detach().float(), ctx.input("Scores").detach().float()
     N, C, M = scores.shape
-    if boxes.is_cuda and ctx.attr("nms_eta") >= 1.0:  # adaptive thresholds stay on the host loop
-        r = _oplib.multiclass_nms_op(boxes, scores, ctx.attr("background_label"), ctx.attr("score_threshold"),
-                                     ctx.attr("nms_top_k"), ctx.attr("nms_threshold"), ctx.attr("keep_top_k"),
-                                     ctx.attr("normalized"))
-        if r is not None:
-            ctx.set_output("Out", r[0], [r[1]])
-            return
     rows, off = [], [0]
     for b in range(N):
         dets = []
@@ -311,6 +296,40 @@ def multiclass_nms(ctx):
     if not rows:  # the reference emits one row of -1 when nothing survives
         rows, off = [[-1.0] * 6], [0, 1]
     ctx.set_output("Out", torch.tensor(rows, dtype=torch.float32, device=boxes.device), [off])
+
+
+# ---------------------------------------------------------------- typed GPU kernels (detect.hip)
+
+
+@register_op_kernel("iou_similarity", "GPU", [torch.float32], library=LibraryType.NATIVE)
+def iou_similarity_native(ctx):
+    r = _oplib.iou_matrix_op(ctx.input("X"), ctx.input("Y"), ctx.attr("box_normalized"))
+    if r is None:
+        return iou_similarity(ctx)
+    ctx.set_output("Out", r, ctx.input_lod("X"))
+
+
+@register_op_kernel("box_coder", "GPU", [torch.float32], library=LibraryType.NATIVE)
+def box_coder_native(ctx):
+    dec = not ctx.attr("code_type").lower().startswith("encode")
+    var = ctx.input("PriorBoxVar") if ctx.has_input("PriorBoxVar") else None
+    r = _oplib.box_coder_op(dec, ctx.input("PriorBox"), var, ctx.input("TargetBox"), ctx.attr("box_normalized"))
+    if r is None:
+        return box_coder(ctx)
+    ctx.set_output("OutputBox", r)
+
+
+@register_op_kernel("multiclass_nms", "GPU", [torch.float32], library=LibraryType.NATIVE)
+def multiclass_nms_native(ctx):
+    """Batched bitmask NMS; adaptive thresholds (nms_eta < 1) stay on the host loop."""
+    r = None
+    if ctx.attr("nms_eta") >= 1.0:
+        r = _oplib.multiclass_nms_op(ctx.input("BBoxes"), ctx.input("Scores"), ctx.attr("background_label"),
+                                     ctx.attr("score_threshold"), ctx.attr("nms_top_k"), ctx.attr("nms_threshold"),
+                                     ctx.attr("keep_top_k"), ctx.attr("normalized"))
+    if r is None:
+        return multiclass_nms(ctx)
+    ctx.set_output("Out", r[0], [r[1]])
 
 
 @register_op("polygon_box_transform", ["Input"], ["Output"], {}, grad=None)

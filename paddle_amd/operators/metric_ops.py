@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 from ..framework import core
+from ..framework.op_kernel_type import LibraryType, register_op_kernel
 from ..framework.registry import register_op
 from ..ops import oplib as _oplib
 
@@ -308,11 +309,6 @@ def merge_ids(ctx):
 @register_op("fake_quantize_abs_max", ["X"], ["Out", "OutScale"], {"bit_length": 8}, grad=None)
 def fake_quantize_abs_max(ctx):
     x = ctx.input("X")
-    r = _oplib.fake_quant_op(x, ctx.attr("bit_length")) if x.is_cuda else None
-    if r is not None:
-        ctx.set_output("Out", r[0])
-        ctx.set_output("OutScale", r[1])
-        return
     bins = (1 << (ctx.attr("bit_length") - 1)) - 1
     s = x.detach().abs().max().reshape(1)
     ctx.set_output("Out", torch.round(x / s.clamp(min=1e-30) * bins))
@@ -325,13 +321,6 @@ def fake_quantize_range_abs_max(ctx):
     x = ctx.input("X")
     bins = (1 << (ctx.attr("bit_length") - 1)) - 1
     in_s = ctx.input("InScale").reshape(1)
-    r = _oplib.fake_quant_op(x, ctx.attr("bit_length"), in_s, ctx.attr("is_test"), True) if x.is_cuda else None
-    if r is not None:
-        ctx.set_output("Out", r[0])
-        ctx.set_output("OutScale", r[1])
-        if ctx.has_output("OutScales"):
-            ctx.set_output("OutScales", r[1].expand(ctx.attr("window_size")).clone())
-        return
     if ctx.attr("is_test"):
         s = in_s
     else:
@@ -340,6 +329,28 @@ def fake_quantize_range_abs_max(ctx):
     ctx.set_output("OutScale", s)
     if ctx.has_output("OutScales"):
         ctx.set_output("OutScales", s.expand(ctx.attr("window_size")).clone())
+
+
+@register_op_kernel("fake_quantize_abs_max", "GPU", [torch.float32], library=LibraryType.NATIVE)
+def fake_quantize_abs_max_native(ctx):
+    """GPU kernel (seqdet.hip): |x|max reduction + round(x / s * bins) in two passes."""
+    r = _oplib.fake_quant_op(ctx.input("X"), ctx.attr("bit_length"))
+    if r is None:
+        return fake_quantize_abs_max(ctx)
+    ctx.set_output("Out", r[0])
+    ctx.set_output("OutScale", r[1])
+
+
+@register_op_kernel("fake_quantize_range_abs_max", "GPU", [torch.float32], library=LibraryType.NATIVE)
+def fake_quantize_range_abs_max_native(ctx):
+    r = _oplib.fake_quant_op(ctx.input("X"), ctx.attr("bit_length"), ctx.input("InScale").reshape(1),
+                             ctx.attr("is_test"), True)
+    if r is None:
+        return fake_quantize_range_abs_max(ctx)
+    ctx.set_output("Out", r[0])
+    ctx.set_output("OutScale", r[1])
+    if ctx.has_output("OutScales"):
+        ctx.set_output("OutScales", r[1].expand(ctx.attr("window_size")).clone())
 
 
 @register_op("fake_dequantize_max_abs", ["X", "Scale"], ["Out"], {"max_range": 127.0})

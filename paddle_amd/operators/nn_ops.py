@@ -18,6 +18,7 @@ import torch.nn.functional as F
 
 from .. import ops as K
 from ..framework import core
+from ..framework.op_kernel_type import LibraryType, register_op_kernel
 from ..framework.registry import register_op
 from ..ops import oplib as _oplib
 
@@ -644,6 +645,16 @@ def im2sequence(ctx):
     ctx.set_output("Out", out, [list(range(0, N * L + 1, L))])
 
 
+def _roi_batch_ids(ctx, rois):
+    lod = ctx.input_lod("ROIs")
+    if not lod:
+        return [0] * rois.shape[0]
+    off, ids = lod[0], []
+    for b in range(len(off) - 1):
+        ids += [b] * (off[b + 1] - off[b])
+    return ids
+
+
 @register_op("roi_pool", ["X", "ROIs"], ["Out", "Argmax~"], {"spatial_scale": 1.0, "pooled_height": 1,
                                                              "pooled_width": 1})
 def roi_pool(ctx):
@@ -651,20 +662,8 @@ def roi_pool(ctx):
     away from zero after scaling, bins are floor/ceil of ph * roi_h / PH offset by the
     ROI start and clipped to the map; an empty bin gives 0 with Argmax -1."""
     x, rois = ctx.input("X"), ctx.input("ROIs")
-    lod = ctx.input_lod("ROIs")
     ph, pw, sc = ctx.attr("pooled_height"), ctx.attr("pooled_width"), ctx.attr("spatial_scale")
-    batch_ids = []
-    if lod:
-        off = lod[0]
-        for b in range(len(off) - 1):
-            batch_ids += [b] * (off[b + 1] - off[b])
-    else:
-        batch_ids = [0] * rois.shape[0]
-    r = _oplib.roi_pool_op(x, rois, batch_ids, ph, pw, sc) if x.is_cuda and rois.shape[0] else None
-    if r is not None:
-        ctx.set_output("Out", r[0])
-        ctx.set_output("Argmax", r[1])
-        return
+    batch_ids = _roi_batch_ids(ctx, rois)
     import math
 
     def rnd(v):
@@ -695,6 +694,19 @@ def roi_pool(ctx):
     ctx.set_output("Out", out)
     ctx.set_output("Argmax", torch.stack(args) if args else torch.zeros(out.shape, dtype=torch.int64,
                                                                          device=x.device))
+
+
+@register_op_kernel("roi_pool", "GPU", [torch.float32], library=LibraryType.NATIVE)
+def roi_pool_native(ctx):
+    """GPU kernel of roi_pool (seqdet.hip), fp32 as roi_pool_op.cu; other float
+    types reach it through the data transform."""
+    x, rois = ctx.input("X"), ctx.input("ROIs")
+    r = _oplib.roi_pool_op(x, rois, _roi_batch_ids(ctx, rois), ctx.attr("pooled_height"), ctx.attr("pooled_width"),
+                           ctx.attr("spatial_scale")) if rois.shape[0] else None
+    if r is None:
+        return roi_pool(ctx)
+    ctx.set_output("Out", r[0])
+    ctx.set_output("Argmax", r[1])
 
 
 @register_op("row_conv", ["X", "Filter"], ["Out"], {})

@@ -11,7 +11,8 @@ from __future__ import annotations
 import torch
 
 from ..framework import core
-from ..framework.registry import register_op
+from ..framework.op_kernel_type import LibraryType, register_op_kernel
+from ..framework.registry import OP_REGISTRY, register_op
 from ..ops import oplib as _oplib
 from ..ops import optim as fopt
 
@@ -88,8 +89,6 @@ def momentum(ctx):
 def lars_momentum(ctx):
     p, v, g = ctx.input("Param"), ctx.input("Velocity"), _grad(ctx).tensor
     wd = ctx.attr("lars_weight_decay")
-    if _native(ctx, "lars", p, g, [v], ["VelocityOut"], mu=ctx.attr("mu"), coeff=ctx.attr("lars_coeff"), wd=wd):
-        return
     lr = _lr(ctx)
     pn, gn = p.norm(), g.norm()
     local = lr * ctx.attr("lars_coeff") * pn / (gn + wd * pn + 1e-12)
@@ -144,9 +143,6 @@ def adam(ctx):
 def adamax(ctx):
     p, m, u, g = ctx.input("Param"), ctx.input("Moment"), ctx.input("InfNorm"), _grad(ctx).tensor
     b1, b2, eps = ctx.attr("beta1"), ctx.attr("beta2"), ctx.attr("epsilon")
-    if _native(ctx, "adamax", p, g, [m, u], ["MomentOut", "InfNormOut"], bp1=ctx.input("Beta1Pow"), b1=b1, b2=b2,
-               eps=eps):
-        return
     lr, bp1 = _lr(ctx), ctx.input("Beta1Pow").reshape(-1)[0]
     m2 = b1 * m + (1 - b1) * g
     u2 = torch.maximum(b2 * u + eps, g.abs())
@@ -187,8 +183,6 @@ def adagrad(ctx):
 def decayed_adagrad(ctx):
     p, m, g = ctx.input("Param"), ctx.input("Moment"), _grad(ctx).tensor
     d, eps, lr = ctx.attr("decay"), ctx.attr("epsilon"), _lr(ctx)
-    if _native(ctx, "decayed_adagrad", p, g, [m], ["MomentOut"], decay=d, eps=eps):
-        return
     m2 = d * m + (1 - d) * g * g
     ctx.set_output("ParamOut", p - lr * g / (torch.sqrt(m2) + eps))
     ctx.set_output("MomentOut", m2)
@@ -201,9 +195,6 @@ def adadelta(ctx):
     p, g = ctx.input("Param"), _grad(ctx).tensor
     ag, au = ctx.input("AvgSquaredGrad"), ctx.input("AvgSquaredUpdate")
     rho, eps = ctx.attr("rho"), ctx.attr("epsilon")
-    if _native(ctx, "adadelta", p, g, [ag, au], ["AvgSquaredGradOut", "AvgSquaredUpdateOut"], lr=False, rho=rho,
-               eps=eps):
-        return
     ag2 = rho * ag + (1 - rho) * g * g
     upd = -torch.sqrt((au + eps) / (ag2 + eps)) * g
     au2 = rho * au + (1 - rho) * upd * upd
@@ -219,9 +210,6 @@ def rmsprop(ctx):
     p, ms, mom, g = ctx.input("Param"), ctx.input("MeanSquare"), ctx.input("Moment"), _grad(ctx).tensor
     eps, rho, mu, lr = ctx.attr("epsilon"), ctx.attr("decay"), ctx.attr("momentum"), _lr(ctx)
     mg = ctx.input("MeanGrad") if ctx.attr("centered") else None
-    if _native(ctx, "rmsprop", p, g, [ms, mom, mg], ["MeanSquareOut", "MomentOut", "MeanGradOut"], rho=rho, mu=mu,
-               eps=eps):
-        return
     ms2 = rho * ms + (1 - rho) * g * g
     if ctx.attr("centered"):
         mg = ctx.input("MeanGrad")
@@ -242,8 +230,6 @@ def ftrl(ctx):
     p, sq, lin, g = (ctx.input("Param"), ctx.input("SquaredAccumulator"), ctx.input("LinearAccumulator"),
                      _grad(ctx).tensor)
     l1, l2, lp, lr = ctx.attr("l1"), ctx.attr("l2"), ctx.attr("lr_power"), _lr(ctx)
-    if _native(ctx, "ftrl", p, g, [sq, lin], ["SquaredAccumOut", "LinearAccumOut"], l1=l1, l2=l2, lr_power=lp):
-        return
     nsq = sq + g * g
     if lp == -0.5:
         sigma = (torch.sqrt(nsq) - torch.sqrt(sq)) / lr
@@ -263,8 +249,6 @@ def ftrl(ctx):
 def proximal_gd(ctx):
     p, g, lr = ctx.input("Param"), _grad(ctx).tensor, _lr(ctx)
     l1, l2 = ctx.attr("l1"), ctx.attr("l2")
-    if _native(ctx, "proximal", p, g, [None], [None], l1=l1, l2=l2):
-        return
     prox = p - lr * g
     out = torch.sign(prox) * torch.clamp(prox.abs() - lr * l1, min=0) / (1 + lr * l2)
     ctx.set_output("ParamOut", out)
@@ -275,8 +259,6 @@ def proximal_gd(ctx):
 def proximal_adagrad(ctx):
     p, m, g, lr = ctx.input("Param"), ctx.input("Moment"), _grad(ctx).tensor, _lr(ctx)
     l1, l2 = ctx.attr("l1"), ctx.attr("l2")
-    if _native(ctx, "proximal", p, g, [m], ["MomentOut"], l1=l1, l2=l2):
-        return
     m2 = m + g * g
     lr_t = lr / torch.sqrt(m2)
     prox = p - lr_t * g
@@ -318,3 +300,44 @@ def average_accumulates(ctx):
     ctx.set_output("out_num_accumulates", torch.tensor([na], dtype=torch.int64, device=dev))
     ctx.set_output("out_old_num_accumulates", torch.tensor([ona], dtype=torch.int64, device=dev))
     ctx.set_output("out_num_updates", torch.tensor([nu], dtype=torch.int64, device=dev))
+
+
+# ---------------------------------------------------------------- typed GPU kernels
+# Dense fp32 updates on the device run one fused optim_ext.hip kernel, registered as
+# the NATIVE (GPU, fp32) kernel of the op; a bf16 / fp16 parameter is cast by the
+# data transform, sparse gradients and uncovered shapes run the PLAIN kernel.
+
+
+def _native_opt(op_type, kind, state_slots, out_slots, hyper, lr=True):
+    plain = OP_REGISTRY[op_type].kernel
+
+    def kernel(ctx):
+        gv = _grad(ctx)
+        if not isinstance(gv, core.SelectedRows):
+            states = [ctx.input(s) if ctx.has_input(s) and (s != "MeanGrad" or ctx.attr("centered")) else None
+                      for s in state_slots]
+            if _native(ctx, kind, ctx.input("Param"), gv.tensor, states, out_slots, lr=lr, **hyper(ctx)):
+                return
+        plain(ctx)
+
+    kernel.__name__ = f"{op_type}_native_kernel"
+    register_op_kernel(op_type, "GPU", [torch.float32], library=LibraryType.NATIVE)(kernel)
+
+
+_native_opt("adamax", "adamax", ["Moment", "InfNorm"], ["MomentOut", "InfNormOut"],
+            lambda c: {"bp1": c.input("Beta1Pow"), "b1": c.attr("beta1"), "b2": c.attr("beta2"),
+                       "eps": c.attr("epsilon")})
+_native_opt("decayed_adagrad", "decayed_adagrad", ["Moment"], ["MomentOut"],
+            lambda c: {"decay": c.attr("decay"), "eps": c.attr("epsilon")})
+_native_opt("adadelta", "adadelta", ["AvgSquaredGrad", "AvgSquaredUpdate"],
+            ["AvgSquaredGradOut", "AvgSquaredUpdateOut"], lambda c: {"rho": c.attr("rho"), "eps": c.attr("epsilon")},
+            lr=False)
+_native_opt("rmsprop", "rmsprop", ["MeanSquare", "Moment", "MeanGrad"], ["MeanSquareOut", "MomentOut", "MeanGradOut"],
+            lambda c: {"rho": c.attr("decay"), "mu": c.attr("momentum"), "eps": c.attr("epsilon")})
+_native_opt("ftrl", "ftrl", ["SquaredAccumulator", "LinearAccumulator"], ["SquaredAccumOut", "LinearAccumOut"],
+            lambda c: {"l1": c.attr("l1"), "l2": c.attr("l2"), "lr_power": c.attr("lr_power")})
+_native_opt("proximal_gd", "proximal", [], [], lambda c: {"l1": c.attr("l1"), "l2": c.attr("l2")})
+_native_opt("proximal_adagrad", "proximal", ["Moment"], ["MomentOut"],
+            lambda c: {"l1": c.attr("l1"), "l2": c.attr("l2")})
+_native_opt("lars_momentum", "lars", ["Velocity"], ["VelocityOut"],
+            lambda c: {"mu": c.attr("mu"), "coeff": c.attr("lars_coeff"), "wd": c.attr("lars_weight_decay")})

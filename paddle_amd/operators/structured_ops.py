@@ -22,6 +22,7 @@ import torch
 import torch.nn.functional as F
 
 from ..framework import core
+from ..framework.op_kernel_type import LibraryType, register_op_kernel
 from ..framework.registry import register_op
 from ..ops import oplib as _oplib
 from .rnn_ops import _gather, _pack_index
@@ -186,17 +187,26 @@ def warpctc(ctx):
         ctx.set_output("WarpCTCGrad", torch.empty_like(x))
         return
     blank, norm = ctx.attr("blank"), ctx.attr("norm_by_times")
-    loss = _oplib.ctc_loss_op(x, lab, xo, lo, blank, norm) if x.is_cuda else None
+    idx, mask = _pack_index(xo, False, x.device)
+    logp = torch.log_softmax(_gather(x.float(), idx, mask), -1).transpose(0, 1)      # [L, N, C]
+    xl = torch.tensor([xo[i + 1] - xo[i] for i in range(N)], device=x.device)
+    ll = torch.tensor([lo[i + 1] - lo[i] for i in range(N)], device=x.device)
+    tgt = lab.reshape(-1).long()
+    loss = F.ctc_loss(logp, tgt, xl, ll, blank=blank, reduction="none", zero_infinity=True)
+    if norm:
+        loss = _GradScale.apply(loss, 1.0 / xl.clamp(min=1).to(loss.dtype))
+    ctx.set_output("Loss", loss.unsqueeze(1).to(x.dtype))
+    ctx.set_output("WarpCTCGrad", torch.zeros_like(x))
+
+
+@register_op_kernel("warpctc", "GPU", [torch.float32, torch.bfloat16], library=LibraryType.NATIVE)
+def warpctc_native(ctx):
+    """GPU kernel: alpha / beta lattices + fused softmax gradient (seqdet.hip)."""
+    x, lab = ctx.input("Logits"), ctx.input("Label")
+    loss = _oplib.ctc_loss_op(x, lab, _off(ctx, "Logits"), _off(ctx, "Label"), ctx.attr("blank"),
+                              ctx.attr("norm_by_times"))
     if loss is None:
-        idx, mask = _pack_index(xo, False, x.device)
-        logp = torch.log_softmax(_gather(x.float(), idx, mask), -1).transpose(0, 1)      # [L, N, C]
-        xl = torch.tensor([xo[i + 1] - xo[i] for i in range(N)], device=x.device)
-        ll = torch.tensor([lo[i + 1] - lo[i] for i in range(N)], device=x.device)
-        tgt = lab.reshape(-1).long()
-        loss = F.ctc_loss(logp, tgt, xl, ll, blank=blank, reduction="none", zero_infinity=True)
-        if norm:
-            loss = _GradScale.apply(loss, 1.0 / xl.clamp(min=1).to(loss.dtype))
-        loss = loss.unsqueeze(1).to(x.dtype)
+        return warpctc(ctx)
     ctx.set_output("Loss", loss)
     ctx.set_output("WarpCTCGrad", torch.zeros_like(x))
 

@@ -973,7 +973,8 @@ def opt_update_(kind, p, g, states, lr, **h):
     elif kind == "ftrl":
         N.call("pa_opt_ftrl", N.ptr(p), N.ptr(g), *st, N.ptr(lr_t), h["l1"], h["l2"], h["lr_power"], n, N.stream())
     elif kind == "proximal":
-        N.call("pa_opt_proximal", N.ptr(p), N.ptr(g), *st, N.ptr(lr_t), h["l1"], h["l2"], n, N.stream())
+        m = st[0] if st else None  # proximal_gd has no Moment
+        N.call("pa_opt_proximal", N.ptr(p), N.ptr(g), m, N.ptr(lr_t), h["l1"], h["l2"], n, N.stream())
     elif kind == "lars":
         acc = torch.zeros(2, dtype=torch.float32, device=p.device)
         N.call("pa_opt_lars", N.ptr(p), N.ptr(g), *st, N.ptr(lr_t), N.ptr(acc), h["mu"], h["coeff"], h["wd"], n,
