@@ -282,9 +282,13 @@ def fusion_lstm(ctx):
     gx = _gather(xx + b[:, :4 * D], idx, mask)
     acts = (_act(ctx.attr("gate_activation")), _act(ctx.attr("cell_activation")),
             _act(ctx.attr("candidate_activation")))
-    H, C, _, _ = _lstm_core(gx, WH, b, ctx.input("H0") if ctx.has_input("H0") else None,
-                            ctx.input("C0") if ctx.has_input("C0") else None, D, ctx.attr("use_peepholes"), acts,
-                            idx, mask, T)
+    h0 = ctx.input("H0") if ctx.has_input("H0") else None
+    c0 = ctx.input("C0") if ctx.has_input("C0") else None
+    if _persistent_lstm_ok(ctx, x, D, idx.shape[0]):
+        # all time steps of the recurrence in one persistent kernel launch (rnn.hip)
+        H, C = _lstm_persistent(gx, WH, h0, c0, D, idx, mask, T)
+    else:
+        H, C, _, _ = _lstm_core(gx, WH, b, h0, c0, D, ctx.attr("use_peepholes"), acts, idx, mask, T)
     ctx.set_output("Hidden", H, lod)
     ctx.set_output("Cell", C, lod)
     ctx.set_output("XX", xx.detach())

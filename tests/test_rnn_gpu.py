@@ -143,3 +143,29 @@ def test_fluid_dynamic_lstm_persistent_matches_generic(monkeypatch):
     errs = [_rel(torch.as_tensor(np.asarray(got)), torch.as_tensor(np.asarray(ref)))
             for got, ref in zip(res["1"], res["0"])]
     assert max(errs) < 3e-2, dict(zip(["hidden", "cell", "dW", "db"], errs))
+
+
+def test_fusion_lstm_persistent_matches_generic(monkeypatch):
+    """fusion_lstm (X @ WeightX for all steps, then the recurrence) on the persistent
+    kernel vs the generic per-step path of the same op."""
+    from paddle_amd.framework import core
+    from paddle_amd.framework import registry as Rg
+
+    D, M, LOD = 128, 64, [0, 6, 9, 17]
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(LOD[-1], M, generator=g).cuda()
+    wx = (torch.randn(M, 4 * D, generator=g) * M ** -0.5).cuda()
+    wh = (torch.randn(D, 4 * D, generator=g) * D ** -0.5).cuda()
+    b = (torch.randn(1, 4 * D, generator=g) * 0.1).cuda()
+    info = Rg.get_op_info("fusion_lstm")
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PADDLE_AMD_PERSISTENT_LSTM", flag)
+        ctx = Rg.KernelContext("fusion_lstm", {"X": [core.LoDTensor(x, [LOD])], "WeightX": [core.LoDTensor(wx)],
+                                               "WeightH": [core.LoDTensor(wh)], "Bias": [core.LoDTensor(b)]},
+                               {"Hidden": ["h"], "Cell": ["c"], "XX": ["xx"]},
+                               dict(info.attrs, use_peepholes=False), core.CUDAPlace(0))
+        Rg.run_kernel(info, ctx)
+        res[flag] = [ctx.results[s][0].tensor.float().cpu() for s in ("Hidden", "Cell")]
+    for got, ref in zip(res["1"], res["0"]):
+        assert _rel(got, ref) < 3e-2
