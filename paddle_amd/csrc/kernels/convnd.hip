@@ -1,0 +1,514 @@
+// Channel-first (NCHW / NCDHW) convolution, transposed convolution and pooling on
+// gfx950 for the Fluid operators (conv2d / conv3d / conv2d_transpose /
+// conv3d_transpose / pool2d / pool3d / max_pool{2,3}d_with_index / unpool / maxout).
+// The NHWC bf16 training path of the models lives in gemm.hip / conv_aux.hip; this
+// file serves the reference's channel-first, usually fp32, Fluid programs.
+//
+// * sgemm: exact-fp32 GEMM on v_mfma_f32_32x32x2f32 (128x128x16 tiles, 4 waves of
+//   64x64), fully strided operands, two batch dimensions on blockIdx.z (image x
+//   group), an inner "k-batch" that sums several strided GEMMs in registers (weight
+//   gradients over a chunk of images), row bias, alpha/beta, or float-atomic
+//   accumulation for split reductions.
+// * vol2col / col2vol: the 3-D lowering (2-D = depth 1) of math/vol2col.cu and
+//   math/im2col.cu (CFO layout: rows (c, kd, kh, kw), columns (od, oh, ow));
+//   col2vol gathers per input element over the kernel taps (no atomics).
+// * pooling: max / avg (exclusive or not, ceil-mode output sizes computed by the
+//   caller) with the int32 in-plane argmax of KernelMaxPool{2,3}dWithIdx; the
+//   backward gathers over the windows that cover an input element (max: through
+//   the argmax, i.e. the first maximum as in KernelMaxPool2DGrad).
+// * unpool (max) scatter / gather, maxout (first maximum gets the gradient).
+//
+// Reference behaviour: operators/math/{vol2col,im2col,pooling,maxouting,
+// unpooling}.cu, conv_cudnn_op.cu.cc, conv_transpose_cudnn_op.cu.cc, pool_op.cc
+// (output size), pool_with_index_op.cc.
+#include "common.h"
+
+namespace pa {
+namespace {
+
+inline int grid_for(long n, int block = 256) {
+  long g = (n + block - 1) / block;
+  return (int)(g < 1 ? 1 : (g > 16384 ? 16384 : g));
+}
+
+#define GRID_STRIDE(i, n) for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < (n); i += (long)gridDim.x * blockDim.x)
+
+// ================================================================ fp32 MFMA GEMM
+struct SgemmArgs {
+  const float* A;
+  const float* B;
+  float* C;
+  const float* bias_m;  // [M] (+ z2 * bsBias2) or null
+  long bsBias2;
+  long M, N, K;
+  long sam, sak;  // A(m, k) = A[m * sam + k * sak]
+  long sbk, sbn;  // B(k, n) = B[k * sbk + n * sbn]
+  long ldc;
+  int Z2;                   // blockIdx.z = z1 * Z2 + z2
+  long bsA1, bsB1, bsC1;    // strides of z1
+  long bsA2, bsB2, bsC2;    // strides of z2
+  int kb;                   // inner k-batch: sum over kb GEMMs ...
+  long kbA, kbB;            // ... whose operands are offset by these strides
+  float alpha, beta;
+  int atomic;               // C += alpha * AB with float atomics (beta / bias ignored)
+};
+
+constexpr int SBM = 128, SBN = 128, SBK = 16, SPAD = 4;
+
+__global__ __launch_bounds__(256) void sgemm_kernel(SgemmArgs g) {
+  __shared__ float As[SBK][SBM + SPAD];
+  __shared__ float Bs[SBK][SBN + SPAD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long z1 = blockIdx.z / g.Z2, z2 = blockIdx.z % g.Z2;
+  const float* A0 = g.A + z1 * g.bsA1 + z2 * g.bsA2;
+  const float* B0 = g.B + z1 * g.bsB1 + z2 * g.bsB2;
+  float* C = g.C + z1 * g.bsC1 + z2 * g.bsC2;
+  const float* bias = g.bias_m ? g.bias_m + z2 * g.bsBias2 : nullptr;
+  const long m0 = (long)blockIdx.y * SBM, n0 = (long)blockIdx.x * SBN;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // loader orientation: walk the operand's contiguous dimension across lanes
+  const bool a_k_fast = g.sak == 1, b_n_fast = g.sbn == 1;
+  for (int b = 0; b < g.kb; ++b) {
+    const float* A = A0 + b * g.kbA;
+    const float* B = B0 + b * g.kbB;
+    for (long k0 = 0; k0 < g.K; k0 += SBK) {
+#pragma unroll
+      for (int e0 = 0; e0 < SBM * SBK; e0 += 256) {
+        const int e = e0 + tid;
+        int mm, kk;
+        if (a_k_fast) { mm = e / SBK; kk = e % SBK; } else { kk = e / SBM; mm = e % SBM; }
+        const long m = m0 + mm, k = k0 + kk;
+        As[kk][mm] = (m < g.M && k < g.K) ? A[m * g.sam + k * g.sak] : 0.f;
+      }
+#pragma unroll
+      for (int e0 = 0; e0 < SBN * SBK; e0 += 256) {
+        const int e = e0 + tid;
+        int nn, kk;
+        if (b_n_fast) { kk = e / SBN; nn = e % SBN; } else { nn = e / SBK; kk = e % SBK; }
+        const long n = n0 + nn, k = k0 + kk;
+        Bs[kk][nn] = (n < g.N && k < g.K) ? B[k * g.sbk + n * g.sbn] : 0.f;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int kk = 0; kk < SBK; kk += 2) {
+        const int k = kk + (lane >> 5);
+        const float a0 = As[k][wm + (lane & 31)], a1 = As[k][wm + 32 + (lane & 31)];
+        const float b0 = Bs[k][wn + (lane & 31)], b1 = Bs[k][wn + 32 + (lane & 31)];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+      }
+      __syncthreads();
+    }
+  }
+  // 32x32 accumulator map: column = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const long n = n0 + wn + 32 * j + (lane & 31);
+      if (n >= g.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m >= g.M) continue;
+        float* c = C + m * g.ldc + n;
+        if (g.atomic) {
+          atomicAdd(c, g.alpha * acc[i][j][r]);
+        } else {
+          float v = g.alpha * acc[i][j][r] + (bias ? bias[m] : 0.f);
+          if (g.beta != 0.f) v += g.beta * *c;
+          *c = v;
+        }
+      }
+    }
+}
+
+// ================================================================ vol2col / col2vol
+struct Geo {
+  int C, D, H, W;        // input (image) dims
+  int OD, OH, OW;        // column dims
+  int kd, kh, kw;
+  int sd, sh, sw;
+  int pd, ph, pw;
+  int dd, dh, dw;
+};
+
+// col[n][(c, kd, kh, kw)][(od, oh, ow)] for nb images
+template <typename T>
+__global__ void vol2col_kernel(const T* __restrict__ x, T* __restrict__ col, Geo g, int nb) {
+  const long S = (long)g.OD * g.OH * g.OW;
+  const int KT = g.kd * g.kh * g.kw;
+  const long rows = (long)g.C * KT;
+  const long total = (long)nb * rows * S;
+  const long img = (long)g.C * g.D * g.H * g.W;
+  GRID_STRIDE(i, total) {
+    const long s = i % S;
+    const long r = (i / S) % rows;
+    const long n = i / (S * rows);
+    const int ow = (int)(s % g.OW), oh = (int)((s / g.OW) % g.OH), od = (int)(s / ((long)g.OW * g.OH));
+    const int tap = (int)(r % KT), c = (int)(r / KT);
+    const int tw = tap % g.kw, th = (tap / g.kw) % g.kh, td = tap / (g.kw * g.kh);
+    const int d = od * g.sd - g.pd + td * g.dd, h = oh * g.sh - g.ph + th * g.dh, w = ow * g.sw - g.pw + tw * g.dw;
+    T v = (T)0;
+    if (d >= 0 && d < g.D && h >= 0 && h < g.H && w >= 0 && w < g.W)
+      v = x[n * img + (((long)c * g.D + d) * g.H + h) * g.W + w];
+    col[i] = v;
+  }
+}
+
+// x[n][c][d][h][w] (+)= sum over taps of col at the output position that read it
+__global__ void col2vol_kernel(const float* __restrict__ col, float* __restrict__ x, Geo g, int nb, int accumulate) {
+  const long S = (long)g.OD * g.OH * g.OW;
+  const int KT = g.kd * g.kh * g.kw;
+  const long plane = (long)g.D * g.H * g.W;
+  const long total = (long)nb * g.C * plane;
+  GRID_STRIDE(i, total) {
+    const int w = (int)(i % g.W), h = (int)((i / g.W) % g.H), d = (int)((i / ((long)g.W * g.H)) % g.D);
+    const long nc = i / plane;  // n * C + c
+    const float* cb = col + nc * KT * S;  // rows (c, taps) of image n start at (n * C + c) * KT
+    float acc = 0.f;
+    for (int td = 0; td < g.kd; ++td) {
+      const int zd = d + g.pd - td * g.dd;
+      if (zd < 0 || zd % g.sd) continue;
+      const int od = zd / g.sd;
+      if (od >= g.OD) continue;
+      for (int th = 0; th < g.kh; ++th) {
+        const int zh = h + g.ph - th * g.dh;
+        if (zh < 0 || zh % g.sh) continue;
+        const int oh = zh / g.sh;
+        if (oh >= g.OH) continue;
+        for (int tw = 0; tw < g.kw; ++tw) {
+          const int zw = w + g.pw - tw * g.dw;
+          if (zw < 0 || zw % g.sw) continue;
+          const int ow = zw / g.sw;
+          if (ow >= g.OW) continue;
+          const int tap = (td * g.kh + th) * g.kw + tw;
+          acc += cb[(long)tap * S + ((long)od * g.OH + oh) * g.OW + ow];
+        }
+      }
+    }
+    x[i] = accumulate ? x[i] + acc : acc;
+  }
+}
+
+// per-channel sum of y[n][c][s] (bias gradient): one workgroup per channel
+__global__ __launch_bounds__(256) void chan_sum_kernel(const float* __restrict__ y, float* __restrict__ out, int N,
+                                                       int C, long S, int accumulate) {
+  __shared__ float red[4];
+  const int c = blockIdx.x;
+  float acc = 0.f;
+  for (int n = 0; n < N; ++n) {
+    const float* p = y + ((long)n * C + c) * S;
+    for (long s = threadIdx.x; s < S; s += 256) acc += p[s];
+  }
+  acc = block_sum<256>(acc, red);
+  if (threadIdx.x == 0) out[c] = accumulate ? out[c] + acc : acc;
+}
+
+// ================================================================ pooling (NC[D]HW)
+struct PoolGeo {
+  long NC;
+  int D, H, W, OD, OH, OW;
+  int kd, kh, kw, sd, sh, sw, pd, ph, pw;
+};
+
+// type 0 max (writes the in-plane argmax when mask != null), 1 avg
+template <typename T>
+__global__ void pool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int* __restrict__ mask, PoolGeo g,
+                                int type, int exclusive) {
+  const long OS = (long)g.OD * g.OH * g.OW;
+  const long IS = (long)g.D * g.H * g.W;
+  GRID_STRIDE(i, g.NC * OS) {
+    const long nc = i / OS;
+    const int ow = (int)(i % g.OW), oh = (int)((i / g.OW) % g.OH), od = (int)((i / ((long)g.OW * g.OH)) % g.OD);
+    int d0 = od * g.sd - g.pd, h0 = oh * g.sh - g.ph, w0 = ow * g.sw - g.pw;
+    const int d1 = min(d0 + g.kd, g.D), h1 = min(h0 + g.kh, g.H), w1 = min(w0 + g.kw, g.W);
+    d0 = max(d0, 0);
+    h0 = max(h0, 0);
+    w0 = max(w0, 0);
+    const T* p = x + nc * IS;
+    if (type == 0) {
+      float best = -3.402823466e+38f;
+      int arg = -1;
+      for (int d = d0; d < d1; ++d)
+        for (int h = h0; h < h1; ++h)
+          for (int w = w0; w < w1; ++w) {
+            const int idx = (d * g.H + h) * g.W + w;
+            const float v = IO<T>::ld(p, idx);
+            if (v > best) { best = v; arg = idx; }
+          }
+      IO<T>::st(y, i, best);
+      if (mask) mask[i] = arg;
+    } else {
+      float s = 0.f;
+      for (int d = d0; d < d1; ++d)
+        for (int h = h0; h < h1; ++h)
+          for (int w = w0; w < w1; ++w) s += IO<T>::ld(p, (d * g.H + h) * g.W + w);
+      const int cnt = exclusive ? (d1 - d0) * (h1 - h0) * (w1 - w0) : g.kd * g.kh * g.kw;
+      IO<T>::st(y, i, cnt > 0 ? s / (float)cnt : 0.f);
+    }
+  }
+}
+
+// output range [lo, hi] whose windows (start o * s - p, length k) cover input i
+__device__ __forceinline__ void cover(int i, int k, int s, int p, int O, int& lo, int& hi) {
+  const int t = i + p - k + 1;
+  lo = t <= 0 ? 0 : (t + s - 1) / s;
+  hi = min((i + p) / s, O - 1);
+}
+
+template <typename T>
+__global__ void pool_bwd_kernel(const T* __restrict__ dy, const int* __restrict__ mask, T* __restrict__ dx, PoolGeo g,
+                                int type, int exclusive) {
+  const long OS = (long)g.OD * g.OH * g.OW;
+  const long IS = (long)g.D * g.H * g.W;
+  GRID_STRIDE(i, g.NC * IS) {
+    const long nc = i / IS;
+    const int idx = (int)(i % IS);
+    const int w = idx % g.W, h = (idx / g.W) % g.H, d = idx / (g.W * g.H);
+    int dl, dh_, hl, hh, wl, wh;
+    cover(d, g.kd, g.sd, g.pd, g.OD, dl, dh_);
+    cover(h, g.kh, g.sh, g.ph, g.OH, hl, hh);
+    cover(w, g.kw, g.sw, g.pw, g.OW, wl, wh);
+    const T* gy = dy + nc * OS;
+    float acc = 0.f;
+    for (int od = dl; od <= dh_; ++od)
+      for (int oh = hl; oh <= hh; ++oh)
+        for (int ow = wl; ow <= wh; ++ow) {
+          const long o = ((long)od * g.OH + oh) * g.OW + ow;
+          if (type == 0) {
+            if (mask[nc * OS + o] == idx) acc += IO<T>::ld(gy, o);
+          } else {
+            int cnt = g.kd * g.kh * g.kw;
+            if (exclusive) {
+              const int d0 = od * g.sd - g.pd, h0 = oh * g.sh - g.ph, w0 = ow * g.sw - g.pw;
+              cnt = (min(d0 + g.kd, g.D) - max(d0, 0)) * (min(h0 + g.kh, g.H) - max(h0, 0)) *
+                    (min(w0 + g.kw, g.W) - max(w0, 0));
+            }
+            acc += IO<T>::ld(gy, o) / (float)cnt;
+          }
+        }
+    IO<T>::st(dx, i, acc);
+  }
+}
+
+// ================================================================ unpool / maxout
+// unpool (max): out[nc][mask[nc][i]] = x[nc][i]; out zero-filled by the caller
+template <typename T>
+__global__ void unpool_fwd_kernel(const T* __restrict__ x, const int* __restrict__ mask, T* __restrict__ out, long NC,
+                                  long IS, long OS, int* __restrict__ bad) {
+  GRID_STRIDE(i, NC * IS) {
+    const long nc = i / IS;
+    const int m = mask[i];
+    if (m < 0 || m >= OS) { *bad = 1; continue; }
+    out[nc * OS + m] = x[i];
+  }
+}
+
+template <typename T>
+__global__ void unpool_bwd_kernel(const T* __restrict__ dout, const int* __restrict__ mask, T* __restrict__ dx, long NC,
+                                  long IS, long OS) {
+  GRID_STRIDE(i, NC * IS) {
+    const long nc = i / IS;
+    const int m = mask[i];
+    dx[i] = (m >= 0 && m < OS) ? dout[nc * OS + m] : (T)0;
+  }
+}
+
+// maxout: y[n][c][s] = max_g x[n][c * groups + g][s]  (math/maxouting.cu)
+template <typename T>
+__global__ void maxout_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int N, int Co, int groups, long S) {
+  GRID_STRIDE(i, (long)N * Co * S) {
+    const long s = i % S;
+    const long nc = i / S;  // n * Co + c
+    const T* p = x + nc * groups * S + s;
+    float best = IO<T>::ld(p, 0);
+    for (int q = 1; q < groups; ++q) best = fmaxf(best, IO<T>::ld(p, (long)q * S));
+    IO<T>::st(y, i, best);
+  }
+}
+
+template <typename T>
+__global__ void maxout_bwd_kernel(const T* __restrict__ x, const T* __restrict__ y, const T* __restrict__ dy,
+                                  T* __restrict__ dx, int N, int Co, int groups, long S) {
+  GRID_STRIDE(i, (long)N * Co * S) {
+    const long s = i % S;
+    const long nc = i / S;
+    const float out = IO<T>::ld(y, i), g = IO<T>::ld(dy, i);
+    const long base = nc * groups * S + s;
+    bool done = false;
+    for (int q = 0; q < groups; ++q) {
+      const bool hit = !done && IO<T>::ld(x, base + (long)q * S) == out;
+      IO<T>::st(dx, base + (long)q * S, hit ? g : 0.f);
+      done = done || hit;
+    }
+  }
+}
+
+}  // namespace
+
+// ================================================================ C ABI
+PA_EXPORT int pa_sgemm(const float* A, long sam, long sak, const float* B, long sbk, long sbn, float* C, long ldc,
+                       long M, long N, long K, int Z1, int Z2, long bsA1, long bsB1, long bsC1, long bsA2, long bsB2,
+                       long bsC2, int kb, long kbA, long kbB, const float* bias_m, long bsBias2, float alpha, float beta,
+                       int atomic, hipStream_t st) {
+  if (M <= 0 || N <= 0) return 0;
+  if (Z1 < 1 || Z2 < 1 || kb < 1 || (long)Z1 * Z2 > 65535) return (int)hipErrorInvalidValue;
+  const long gy = (M + SBM - 1) / SBM, gx = (N + SBN - 1) / SBN;
+  if (gy > 65535 || gx > 2147483647L) return (int)hipErrorInvalidValue;
+  SgemmArgs g;
+  g.A = A; g.B = B; g.C = C; g.bias_m = bias_m; g.bsBias2 = bsBias2;
+  g.M = M; g.N = N; g.K = K;
+  g.sam = sam; g.sak = sak; g.sbk = sbk; g.sbn = sbn; g.ldc = ldc;
+  g.Z2 = Z2;
+  g.bsA1 = bsA1; g.bsB1 = bsB1; g.bsC1 = bsC1;
+  g.bsA2 = bsA2; g.bsB2 = bsB2; g.bsC2 = bsC2;
+  g.kb = kb; g.kbA = kbA; g.kbB = kbB;
+  g.alpha = alpha; g.beta = beta; g.atomic = atomic;
+  hipLaunchKernelGGL(sgemm_kernel, dim3((unsigned)gx, (unsigned)gy, (unsigned)(Z1 * Z2)), dim3(256), 0, st, g);
+  PA_LAUNCH_CHECK();
+}
+
+static Geo make_geo(const int* v) {
+  // v: C, D, H, W, OD, OH, OW, kd, kh, kw, sd, sh, sw, pd, ph, pw, dd, dh, dw
+  Geo g;
+  g.C = v[0]; g.D = v[1]; g.H = v[2]; g.W = v[3];
+  g.OD = v[4]; g.OH = v[5]; g.OW = v[6];
+  g.kd = v[7]; g.kh = v[8]; g.kw = v[9];
+  g.sd = v[10]; g.sh = v[11]; g.sw = v[12];
+  g.pd = v[13]; g.ph = v[14]; g.pw = v[15];
+  g.dd = v[16]; g.dh = v[17]; g.dw = v[18];
+  return g;
+}
+
+static bool geo_ok(const Geo& g) {
+  return g.C > 0 && g.D > 0 && g.H > 0 && g.W > 0 && g.OD > 0 && g.OH > 0 && g.OW > 0 && g.kd > 0 && g.kh > 0 &&
+         g.kw > 0 && g.sd > 0 && g.sh > 0 && g.sw > 0 && g.dd > 0 && g.dh > 0 && g.dw > 0 && g.pd >= 0 && g.ph >= 0 &&
+         g.pw >= 0;
+}
+
+PA_EXPORT int pa_vol2col(int dt, const void* x, void* col, const int* geo, int nb, hipStream_t st) {
+  const Geo g = make_geo(geo);
+  if (!geo_ok(g) || nb <= 0) return (int)hipErrorInvalidValue;
+  const long total = (long)nb * g.C * g.kd * g.kh * g.kw * g.OD * g.OH * g.OW;
+  if (dt == 1)
+    hipLaunchKernelGGL(vol2col_kernel<u16>, dim3(grid_for(total)), dim3(256), 0, st, (const u16*)x, (u16*)col, g, nb);
+  else
+    hipLaunchKernelGGL(vol2col_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)x, (float*)col,
+                       g, nb);
+  PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_col2vol(const float* col, float* x, const int* geo, int nb, int accumulate, hipStream_t st) {
+  const Geo g = make_geo(geo);
+  if (!geo_ok(g) || nb <= 0) return (int)hipErrorInvalidValue;
+  const long total = (long)nb * g.C * g.D * g.H * g.W;
+  hipLaunchKernelGGL(col2vol_kernel, dim3(grid_for(total)), dim3(256), 0, st, col, x, g, nb, accumulate);
+  PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_chan_sum(const float* y, float* out, int N, int C, long S, int accumulate, hipStream_t st) {
+  if (C <= 0 || N <= 0) return 0;
+  hipLaunchKernelGGL(chan_sum_kernel, dim3((unsigned)C), dim3(256), 0, st, y, out, N, C, S, accumulate);
+  PA_LAUNCH_CHECK();
+}
+
+static PoolGeo make_pool(long NC, const int* v) {
+  // v: D, H, W, OD, OH, OW, kd, kh, kw, sd, sh, sw, pd, ph, pw
+  PoolGeo g;
+  g.NC = NC;
+  g.D = v[0]; g.H = v[1]; g.W = v[2];
+  g.OD = v[3]; g.OH = v[4]; g.OW = v[5];
+  g.kd = v[6]; g.kh = v[7]; g.kw = v[8];
+  g.sd = v[9]; g.sh = v[10]; g.sw = v[11];
+  g.pd = v[12]; g.ph = v[13]; g.pw = v[14];
+  return g;
+}
+
+static bool pool_ok(const PoolGeo& g) {
+  return g.NC > 0 && g.D > 0 && g.H > 0 && g.W > 0 && g.OD > 0 && g.OH > 0 && g.OW > 0 && g.kd > 0 && g.kh > 0 &&
+         g.kw > 0 && g.sd > 0 && g.sh > 0 && g.sw > 0 && g.pd >= 0 && g.ph >= 0 && g.pw >= 0;
+}
+
+PA_EXPORT int pa_pool_fwd(int dt, const void* x, void* y, int* mask, long NC, const int* geo, int type, int exclusive,
+                          hipStream_t st) {
+  const PoolGeo g = make_pool(NC, geo);
+  if (!pool_ok(g)) return (int)hipErrorInvalidValue;
+  const long total = NC * g.OD * g.OH * g.OW;
+  if (dt == 1)
+    hipLaunchKernelGGL(pool_fwd_kernel<u16>, dim3(grid_for(total)), dim3(256), 0, st, (const u16*)x, (u16*)y, mask, g,
+                       type, exclusive);
+  else
+    hipLaunchKernelGGL(pool_fwd_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)x, (float*)y,
+                       mask, g, type, exclusive);
+  PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_pool_bwd(int dt, const void* dy, const int* mask, void* dx, long NC, const int* geo, int type,
+                          int exclusive, hipStream_t st) {
+  const PoolGeo g = make_pool(NC, geo);
+  if (!pool_ok(g) || (type == 0 && !mask)) return (int)hipErrorInvalidValue;
+  const long total = NC * g.D * g.H * g.W;
+  if (dt == 1)
+    hipLaunchKernelGGL(pool_bwd_kernel<u16>, dim3(grid_for(total)), dim3(256), 0, st, (const u16*)dy, mask, (u16*)dx,
+                       g, type, exclusive);
+  else
+    hipLaunchKernelGGL(pool_bwd_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)dy, mask,
+                       (float*)dx, g, type, exclusive);
+  PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_unpool(int dt, int backward, const void* src, const int* mask, void* dst, long NC, long IS, long OS,
+                        int* bad, hipStream_t st) {
+  const long total = NC * IS;
+  if (total <= 0) return 0;
+  if (!backward) {
+    if (dt == 1)
+      hipLaunchKernelGGL(unpool_fwd_kernel<u16>, dim3(grid_for(total)), dim3(256), 0, st, (const u16*)src, mask,
+                         (u16*)dst, NC, IS, OS, bad);
+    else
+      hipLaunchKernelGGL(unpool_fwd_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)src, mask,
+                         (float*)dst, NC, IS, OS, bad);
+  } else {
+    if (dt == 1)
+      hipLaunchKernelGGL(unpool_bwd_kernel<u16>, dim3(grid_for(total)), dim3(256), 0, st, (const u16*)src, mask,
+                         (u16*)dst, NC, IS, OS);
+    else
+      hipLaunchKernelGGL(unpool_bwd_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)src, mask,
+                         (float*)dst, NC, IS, OS);
+  }
+  PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_maxout(int dt, const void* x, const void* y, const void* dy, void* out, int N, int Co, int groups,
+                        long S, hipStream_t st) {
+  const long total = (long)N * Co * S;
+  if (total <= 0 || groups < 1) return 0;
+  if (!dy) {
+    if (dt == 1)
+      hipLaunchKernelGGL(maxout_fwd_kernel<u16>, dim3(grid_for(total)), dim3(256), 0, st, (const u16*)x, (u16*)out, N,
+                         Co, groups, S);
+    else
+      hipLaunchKernelGGL(maxout_fwd_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)x,
+                         (float*)out, N, Co, groups, S);
+  } else {
+    if (dt == 1)
+      hipLaunchKernelGGL(maxout_bwd_kernel<u16>, dim3(grid_for(total)), dim3(256), 0, st, (const u16*)x, (const u16*)y,
+                         (const u16*)dy, (u16*)out, N, Co, groups, S);
+    else
+      hipLaunchKernelGGL(maxout_bwd_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)x,
+                         (const float*)y, (const float*)dy, (float*)out, N, Co, groups, S);
+  }
+  PA_LAUNCH_CHECK();
+}
+
+}  // namespace pa

@@ -16,6 +16,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import conv as _conv
+from ..ops import convnd as _cnd
 
 
 def _pair(v, n=2):
@@ -218,6 +219,9 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data
     if not _nchw(x, data_format):
         y = F.conv2d(x.permute(0, 3, 1, 2), weight, bias, _pair(stride), pad, _pair(dilation), groups)
         return y.permute(0, 2, 3, 1)
+    if not isinstance(pad, str) and _cnd.supported_conv(x, weight, groups):
+        # NCHW on the GPU: vol2col + fp32 MFMA GEMM (ops/convnd.py)
+        return _cnd.conv_nd(x, weight, bias, _pair(stride), pad, _pair(dilation), groups)
     return F.conv2d(x, weight, bias, _pair(stride), pad, _pair(dilation), groups)
 
 
@@ -229,11 +233,18 @@ def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data
 
 
 def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCDHW", name=None):
+    pad = _conv_padding(padding, 3)
+    if data_format == "NCDHW" and not isinstance(pad, str) and _cnd.supported_conv(x, weight, groups):
+        return _cnd.conv_nd(x, weight, bias, _pair(stride, 3), pad, _pair(dilation, 3), groups)
     return F.conv3d(x, weight, bias, _pair(stride, 3), _conv_padding(padding, 3), _pair(dilation, 3), groups)
 
 
 def conv2d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1, dilation=1,
                      data_format="NCHW", output_size=None, name=None):
+    pad = _conv_padding(padding, 2)
+    if _nchw(x, data_format) and not isinstance(pad, str) and _cnd.supported_conv_transpose(x, weight, groups):
+        y = _cnd.conv_transpose_nd(x, weight, _pair(stride), pad, _pair(dilation), groups, _pair(output_padding))
+        return y if bias is None else y + bias.to(y.dtype).reshape(1, -1, 1, 1)
     return F.conv_transpose2d(x, weight, bias, _pair(stride), _conv_padding(padding, 2), _pair(output_padding),
                               groups, _pair(dilation))
 
@@ -256,6 +267,9 @@ def max_pool2d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_m
     if not _nchw(x, data_format) and not return_mask and _conv.supported_pool(x, ceil_mode) \
             and not isinstance(padding, str):
         return _conv.max_pool2d_nhwc(x, kernel_size, stride, _conv_padding(padding, 2))
+    if _nchw(x, data_format) and not isinstance(padding, str) and _cnd.supported_pool(x) and x.dim() == 4:
+        return _cnd.pool_nd(x, "max", _pair(kernel_size), _pair(stride), _conv_padding(padding, 2),
+                            ceil_mode=ceil_mode, return_mask=return_mask)
     if not _nchw(x, data_format):
         x = x.permute(0, 3, 1, 2)
     y = F.max_pool2d(x, _pair(kernel_size), _pair(stride), _conv_padding(padding, 2), ceil_mode=ceil_mode,
@@ -269,6 +283,10 @@ def avg_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False, exclusiv
                data_format="NCHW", name=None):
     stride = kernel_size if stride is None else stride
     nchw = _nchw(x, data_format)
+    if nchw and divisor_override is None and not isinstance(padding, str) and _cnd.supported_pool(x) \
+            and x.dim() == 4:
+        return _cnd.pool_nd(x, "avg", _pair(kernel_size), _pair(stride), _conv_padding(padding, 2), exclusive,
+                            ceil_mode)
     if not nchw:
         x = x.permute(0, 3, 1, 2)
     y = F.avg_pool2d(x, _pair(kernel_size), _pair(stride), _conv_padding(padding, 2), ceil_mode,
@@ -288,12 +306,19 @@ def avg_pool1d(x, kernel_size, stride=None, padding=0, exclusive=True, ceil_mode
 
 def max_pool3d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False, data_format="NCDHW",
                name=None):
+    if data_format == "NCDHW" and not isinstance(padding, str) and _cnd.supported_pool(x) and x.dim() == 5:
+        return _cnd.pool_nd(x, "max", _pair(kernel_size, 3), _pair(kernel_size if stride is None else stride, 3),
+                            _conv_padding(padding, 3), ceil_mode=ceil_mode, return_mask=return_mask)
     return F.max_pool3d(x, kernel_size, kernel_size if stride is None else stride, padding, ceil_mode=ceil_mode,
                         return_indices=return_mask)
 
 
 def avg_pool3d(x, kernel_size, stride=None, padding=0, ceil_mode=False, exclusive=True, divisor_override=None,
                data_format="NCDHW", name=None):
+    if (data_format == "NCDHW" and divisor_override is None and not isinstance(padding, str)
+            and _cnd.supported_pool(x) and x.dim() == 5):
+        return _cnd.pool_nd(x, "avg", _pair(kernel_size, 3), _pair(kernel_size if stride is None else stride, 3),
+                            _conv_padding(padding, 3), exclusive, ceil_mode)
     return F.avg_pool3d(x, kernel_size, kernel_size if stride is None else stride, padding, ceil_mode,
                         count_include_pad=not exclusive, divisor_override=divisor_override)
 

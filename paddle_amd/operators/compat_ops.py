@@ -214,6 +214,12 @@ def max_pool3d_with_index(ctx):
     k, s, p = ctx.attr("ksize"), ctx.attr("strides"), ctx.attr("paddings")
     if ctx.attr("global_pooling"):
         k, p = list(x.shape[2:]), [0, 0, 0]
+    from ..ops import convnd as _cnd
+    if _cnd.supported_pool(x) and x.dim() == 5:
+        y, idx = _cnd.pool_nd(x, "max", k, s, p, return_mask=True)
+        ctx.set_output("Out", y)
+        ctx.set_output("Mask", idx)
+        return
     y, idx = F.max_pool3d(x, k, s, p, return_indices=True)
     ctx.set_output("Out", y)
     ctx.set_output("Mask", idx.to(torch.int32))

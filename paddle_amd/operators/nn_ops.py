@@ -8,8 +8,9 @@ smooth_l1_loss,label_smooth,bilinear_interp,pad,pad2d,crop,im2sequence,spp,unpoo
 roi_pool}_op.* (SURVEY §2.7).
 
 On the HIP device, layer_norm / softmax / softmax_with_cross_entropy /
-lookup_table go through the hand-written gfx950 kernels (paddle_amd.ops); conv and
-pool run through PyTorch-ROCm.
+lookup_table go through the hand-written gfx950 kernels (paddle_amd.ops); conv /
+conv_transpose (2-D, 3-D, grouped) and pool / pool_with_index / unpool run on the
+channel-first kernels of csrc/kernels/convnd.hip (ops/convnd.py).
 """
 from __future__ import annotations
 
@@ -20,6 +21,7 @@ from .. import ops as K
 from ..framework import core
 from ..framework.op_kernel_type import LibraryType, register_op_kernel
 from ..framework.registry import register_op
+from ..ops import convnd as _cnd
 from ..ops import oplib as _oplib
 
 # ------------------------------------------------------------------ conv
@@ -35,6 +37,11 @@ def _conv_attrs(extra=None):
 @register_op("conv2d", ["Input", "Filter", "Bias?"], ["Output"], _conv_attrs())
 def conv2d(ctx):
     x, w = ctx.input("Input"), ctx.input("Filter")
+    b = ctx.input("Bias") if ctx.has_input("Bias") else None
+    if _cnd.supported_conv(x, w, ctx.attr("groups") or 1):
+        ctx.set_output("Output", _cnd.conv_nd(x, w, b, ctx.attr("strides"), ctx.attr("paddings"),
+                                              ctx.attr("dilations"), ctx.attr("groups") or 1))
+        return
     y = F.conv2d(x, w.to(x.dtype), ctx.input("Bias") if ctx.has_input("Bias") else None,
                  tuple(ctx.attr("strides")), tuple(ctx.attr("paddings")), tuple(ctx.attr("dilations")),
                  ctx.attr("groups") or 1)
@@ -50,6 +57,10 @@ def depthwise_conv2d(ctx):
              _conv_attrs({"strides": [1, 1, 1], "paddings": [0, 0, 0], "dilations": [1, 1, 1]}))
 def conv3d(ctx):
     x, w = ctx.input("Input"), ctx.input("Filter")
+    if _cnd.supported_conv(x, w, ctx.attr("groups") or 1):
+        ctx.set_output("Output", _cnd.conv_nd(x, w, None, ctx.attr("strides"), ctx.attr("paddings"),
+                                              ctx.attr("dilations"), ctx.attr("groups") or 1))
+        return
     y = F.conv3d(x, w.to(x.dtype), None, tuple(ctx.attr("strides")), tuple(ctx.attr("paddings")),
                  tuple(ctx.attr("dilations")), ctx.attr("groups") or 1)
     ctx.set_output("Output", y)
@@ -62,6 +73,21 @@ def conv2d_grad(ctx):
     x, w, dy = ctx.input("Input"), ctx.input("Filter"), ctx.input("Output@GRAD")
     st, pd, dl, g = (tuple(ctx.attr("strides")), tuple(ctx.attr("paddings")), tuple(ctx.attr("dilations")),
                      ctx.attr("groups") or 1)
+    if _cnd.supported_conv(x, w, g) and dy.is_cuda:
+        xs = x.detach().requires_grad_(ctx.has_output("Input@GRAD"))
+        ws = w.detach().requires_grad_(ctx.has_output("Filter@GRAD"))
+        with torch.enable_grad():
+            y = _cnd.conv_nd(xs, ws, None, st, pd, dl, g)
+            want = [t for t in (xs, ws) if t.requires_grad]
+            grads = torch.autograd.grad(y, want, dy) if want else []
+        it = iter(grads)
+        if ctx.has_output("Input@GRAD"):
+            ctx.set_output("Input@GRAD", next(it))
+        if ctx.has_output("Filter@GRAD"):
+            ctx.set_output("Filter@GRAD", next(it))
+        if ctx.has_output("Bias@GRAD"):
+            ctx.set_output("Bias@GRAD", _cnd._bias_grad(dy.float().contiguous()).to(dy.dtype))
+        return
     if ctx.has_output("Input@GRAD"):
         ctx.set_output("Input@GRAD", torch.nn.grad.conv2d_input(x.shape, w, dy, st, pd, dl, g))
     if ctx.has_output("Filter@GRAD"):
@@ -75,7 +101,10 @@ def conv2d_grad(ctx):
 def conv2d_transpose(ctx):
     x, w = ctx.input("Input"), ctx.input("Filter")
     st, pd, dl = tuple(ctx.attr("strides")), tuple(ctx.attr("paddings")), tuple(ctx.attr("dilations"))
-    y = F.conv_transpose2d(x, w.to(x.dtype), None, st, pd, 0, ctx.attr("groups") or 1, dl)
+    if _cnd.supported_conv_transpose(x, w, ctx.attr("groups") or 1):
+        y = _cnd.conv_transpose_nd(x, w, st, pd, dl, ctx.attr("groups") or 1)
+    else:
+        y = F.conv_transpose2d(x, w.to(x.dtype), None, st, pd, 0, ctx.attr("groups") or 1, dl)
     osz = ctx.attr("output_size")
     if osz:
         y = y[..., :osz[0], :osz[1]]
@@ -86,6 +115,14 @@ def conv2d_transpose(ctx):
              _conv_attrs({"strides": [1, 1, 1], "paddings": [0, 0, 0], "dilations": [1, 1, 1], "output_size": []}))
 def conv3d_transpose(ctx):
     x, w = ctx.input("Input"), ctx.input("Filter")
+    if _cnd.supported_conv_transpose(x, w, ctx.attr("groups") or 1):
+        y = _cnd.conv_transpose_nd(x, w, ctx.attr("strides"), ctx.attr("paddings"), ctx.attr("dilations"),
+                                   ctx.attr("groups") or 1)
+        osz = ctx.attr("output_size")
+        if osz:
+            y = y[..., :osz[0], :osz[1], :osz[2]]
+        ctx.set_output("Output", y)
+        return
     y = F.conv_transpose3d(x, w.to(x.dtype), None, tuple(ctx.attr("strides")), tuple(ctx.attr("paddings")), 0,
                            ctx.attr("groups") or 1, tuple(ctx.attr("dilations")))
     ctx.set_output("Output", y)
@@ -109,6 +146,10 @@ def pool2d(ctx):
     k, s, p = list(ctx.attr("ksize")), list(ctx.attr("strides")), list(ctx.attr("paddings"))
     if ctx.attr("global_pooling"):
         k, p = [x.shape[2], x.shape[3]], [0, 0]
+    if _cnd.supported_pool(x) and x.dim() == 4:
+        ctx.set_output("Out", _cnd.pool_nd(x, ctx.attr("pooling_type"), k, s, p, ctx.attr("exclusive"),
+                                           ctx.attr("ceil_mode")))
+        return
     if ctx.attr("pooling_type") == "max":
         y = F.max_pool2d(x, k, s, p, ceil_mode=ctx.attr("ceil_mode"))
     else:
@@ -124,6 +165,10 @@ def pool3d(ctx):
     k, s, p = list(ctx.attr("ksize")), list(ctx.attr("strides")), list(ctx.attr("paddings"))
     if ctx.attr("global_pooling"):
         k, p = list(x.shape[2:]), [0, 0, 0]
+    if _cnd.supported_pool(x) and x.dim() == 5:
+        ctx.set_output("Out", _cnd.pool_nd(x, ctx.attr("pooling_type"), k, s, p, ctx.attr("exclusive"),
+                                           ctx.attr("ceil_mode")))
+        return
     if ctx.attr("pooling_type") == "max":
         y = F.max_pool3d(x, k, s, p, ceil_mode=ctx.attr("ceil_mode"))
     else:
@@ -138,6 +183,11 @@ def max_pool2d_with_index(ctx):
     k, s, p = ctx.attr("ksize"), ctx.attr("strides"), ctx.attr("paddings")
     if ctx.attr("global_pooling"):
         k, p = [x.shape[2], x.shape[3]], [0, 0]
+    if _cnd.supported_pool(x) and x.dim() == 4:
+        y, idx = _cnd.pool_nd(x, "max", k, s, p, return_mask=True)
+        ctx.set_output("Out", y)
+        ctx.set_output("Mask", idx)
+        return
     y, idx = F.max_pool2d(x, k, s, p, return_indices=True)
     ctx.set_output("Out", y)
     ctx.set_output("Mask", idx.to(torch.int32))
@@ -148,6 +198,9 @@ def max_pool2d_with_index(ctx):
 def unpool(ctx):
     x, idx = ctx.input("X"), ctx.input("Indices").long()
     k, s, p = ctx.attr("ksize"), ctx.attr("strides"), ctx.attr("paddings")
+    if _cnd.supported_pool(x) and x.dim() == 4:
+        ctx.set_output("Out", _cnd.unpool2d(x, idx, k, s, p))
+        return
     ctx.set_output("Out", F.max_unpool2d(x, idx, k, s, p))
 
 

@@ -151,6 +151,15 @@ _SIGS = {
     "pa_quant_cols_t_f8": [_P, _P, _P, _I, _I, _I, _P],
     "pa_moe_reduce": [_P, _P, _P, _P, _L, _I, _I, _P],
     "pa_moe_combine_bwd": [_P, _P, _P, _P, _P, _P, _L, _I, _I, _P],
+    "pa_sgemm": [_P, _L, _L, _P, _L, _L, _P, _L, _L, _L, _L, _I, _I, _L, _L, _L, _L, _L, _L, _I, _L, _L, _P, _L, _F,
+                 _F, _I, _P],
+    "pa_vol2col": [_I, _P, _P, _P, _I, _P],
+    "pa_col2vol": [_P, _P, _P, _I, _I, _P],
+    "pa_chan_sum": [_P, _P, _I, _I, _L, _I, _P],
+    "pa_pool_fwd": [_I, _P, _P, _P, _L, _P, _I, _I, _P],
+    "pa_pool_bwd": [_I, _P, _P, _P, _L, _P, _I, _I, _P],
+    "pa_unpool": [_I, _I, _P, _P, _P, _L, _L, _L, _P, _P],
+    "pa_maxout": [_I, _P, _P, _P, _P, _I, _I, _I, _L, _P],
     "pa_flash_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _LP, _I, _I, _I, _I, _I, _I, _F, _I, _P, _P],
 }
 

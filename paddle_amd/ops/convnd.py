@@ -1,0 +1,413 @@
+"""Channel-first (NCHW / NCDHW) conv, transposed conv, pooling, unpool and maxout
+on the gfx950 kernels of ``csrc/kernels/convnd.hip`` -- the GPU kernels behind the
+Fluid ``conv2d`` / ``conv3d`` / ``conv2d_transpose`` / ``conv3d_transpose`` /
+``pool2d`` / ``pool3d`` / ``max_pool{2,3}d_with_index`` / ``unpool`` / ``maxout``
+operators (the reference runs these on cuDNN or math/{im2col,vol2col,pooling}.cu).
+
+Convolution is vol2col + an exact-fp32 MFMA GEMM (``pa_sgemm``) per chunk of
+images (chunks bound the column buffer), groups on the GEMM's second batch
+dimension; dgrad is W^T dY + col2vol (gather, no atomics); wgrad sums
+dY col^T over the images of a chunk with float-atomic accumulation into fp32.
+Transposed convolution reuses the same three pieces with the roles swapped.
+bf16 / fp16 inputs are computed in fp32 and cast back (the NHWC bf16 model path
+lives in :mod:`paddle_amd.ops.conv`).
+
+Reference: operators/conv_cudnn_op.cu.cc:43-171, conv_transpose_cudnn_op.cu.cc,
+math/vol2col.cu, math/im2col.cu, math/pooling.cu:25-1037, math/maxouting.cu,
+math/unpooling.cu, pool_op.cc (output sizes), unpool_op.cc.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+from . import _native as N
+
+_ENABLED = os.environ.get("PADDLE_AMD_CONVND", "1") != "0"
+_COL_BUDGET = 1 << 28  # floats per column chunk (1 GiB)
+_DT = {torch.float32: 0, torch.bfloat16: 1}
+
+
+def enabled():
+    return _ENABLED
+
+
+def set_enabled(flag: bool):
+    global _ENABLED
+    _ENABLED = bool(flag)
+
+
+def _ok(x):
+    return _ENABLED and x.is_cuda and x.dtype in (torch.float32, torch.bfloat16, torch.float16)
+
+
+def _tup(v, nd):
+    if isinstance(v, (list, tuple)):
+        v = [int(t) for t in v]
+        return tuple(v if len(v) == nd else v * nd if len(v) == 1 else v[:nd])
+    return (int(v),) * nd
+
+
+def _arr(vals):
+    a = (ctypes.c_int * len(vals))(*[int(v) for v in vals])
+    return a
+
+
+def sgemm(A, sam, sak, B, sbk, sbn, C, ldc, M, Nn, K, Z1=1, Z2=1, bs1=(0, 0, 0), bs2=(0, 0, 0), kb=1,
+          kbA=0, kbB=0, bias=None, bs_bias2=0, alpha=1.0, beta=0.0, atomic=False):
+    """Strided batched fp32 GEMM: C[z](m, n) = alpha * sum_b A[z, b](m, :) B[z, b](:, n) (+ bias[m] | + beta C)."""
+    if Z1 * Z2 > 65535:
+        raise ValueError("sgemm: batch too large")
+    N.call("pa_sgemm", N.ptr(A), sam, sak, N.ptr(B), sbk, sbn, N.ptr(C), ldc, M, Nn, K, int(Z1), int(Z2),
+           bs1[0], bs1[1], bs1[2], bs2[0], bs2[1], bs2[2], int(kb), kbA, kbB, N.ptr(bias), bs_bias2, float(alpha),
+           float(beta), int(bool(atomic)), N.stream())
+
+
+def _geo(C, sp, osp, k, s, p, d):
+    return _arr([C, *sp, *osp, *k, *s, *p, *d])
+
+
+def _vol2col(x, nb, geo, rows, S):
+    col = torch.empty(nb, rows, S, dtype=x.dtype, device=x.device)
+    N.call("pa_vol2col", _DT[x.dtype], N.ptr(x), N.ptr(col), geo, int(nb), N.stream())
+    return col
+
+
+def _col2vol(col, x, nb, geo, accumulate=False):
+    N.call("pa_col2vol", N.ptr(col), N.ptr(x), geo, int(nb), int(accumulate), N.stream())
+
+
+def _chunk(n, per_img, groups):
+    nb = max(1, min(n, _COL_BUDGET // max(per_img, 1)))
+    return max(1, min(nb, 65535 // max(groups, 1)))
+
+
+def _pad3(t):
+    return (1,) * (3 - len(t)) + tuple(t)
+
+
+def _pad3z(t):
+    return (0,) * (3 - len(t)) + tuple(t)
+
+
+def out_size(i, k, s, p, d):
+    return (i + 2 * p - d * (k - 1) - 1) // s + 1
+
+
+# ------------------------------------------------------------------ convolution
+
+
+def _conv_fwd(x, w, b, s, p, d, G):
+    Nn, C = x.shape[0], x.shape[1]
+    sp = tuple(x.shape[2:])
+    nd = len(sp)
+    Cout = w.shape[0]
+    k = tuple(w.shape[2:])
+    osp = tuple(out_size(sp[i], k[i], s[i], p[i], d[i]) for i in range(nd))
+    KT = 1
+    for v in k:
+        KT *= v
+    S = 1
+    for v in osp:
+        S *= v
+    Cg, Coutg = C // G, Cout // G
+    CgK = Cg * KT
+    geo = _geo(C, _pad3(sp), _pad3(osp), _pad3(k), _pad3(s), _pad3z(p), _pad3(d))
+    y = torch.empty((Nn, Cout) + osp, dtype=torch.float32, device=x.device)
+    wc = w.contiguous()
+    nb = _chunk(Nn, C * KT * S, G)
+    for n0 in range(0, Nn, nb):
+        m = min(nb, Nn - n0)
+        col = _vol2col(x[n0:n0 + m], m, geo, C * KT, S)
+        sgemm(wc, CgK, 1, col, S, 1, y[n0:n0 + m], S, Coutg, S, CgK, Z1=m, Z2=G,
+              bs1=(0, C * KT * S, Cout * S), bs2=(Coutg * CgK, CgK * S, Coutg * S), bias=b, bs_bias2=Coutg)
+    return y, geo, osp
+
+
+def _conv_dgrad(dy, w, x_shape, geo, G):
+    Nn, C = x_shape[0], x_shape[1]
+    Cout = w.shape[0]
+    KT = w[0, 0].numel()
+    S = dy[0, 0].numel()
+    Cg, Coutg = C // G, Cout // G
+    CgK = Cg * KT
+    dx = torch.empty(x_shape, dtype=torch.float32, device=dy.device)
+    nb = _chunk(Nn, C * KT * S, G)
+    for n0 in range(0, Nn, nb):
+        m = min(nb, Nn - n0)
+        col = torch.empty(m, C * KT, S, dtype=torch.float32, device=dy.device)
+        sgemm(w, 1, CgK, dy[n0:n0 + m], S, 1, col, S, CgK, S, Coutg, Z1=m, Z2=G,
+              bs1=(0, Cout * S, C * KT * S), bs2=(Coutg * CgK, Coutg * S, CgK * S))
+        _col2vol(col, dx[n0:n0 + m], m, geo)
+    return dx
+
+
+def _conv_wgrad(dy, x, w_shape, geo, G):
+    Nn, C = x.shape[0], x.shape[1]
+    Cout = w_shape[0]
+    KT = 1
+    for v in w_shape[2:]:
+        KT *= v
+    S = dy[0, 0].numel()
+    Cg, Coutg = C // G, Cout // G
+    CgK = Cg * KT
+    dw = torch.zeros(w_shape, dtype=torch.float32, device=dy.device)
+    nb = _chunk(Nn, C * KT * S, G)
+    for n0 in range(0, Nn, nb):
+        m = min(nb, Nn - n0)
+        col = _vol2col(x[n0:n0 + m], m, geo, C * KT, S)
+        # dW[g] += sum_img dY[img][g] col[img][g]^T  (one split per image, float atomics)
+        sgemm(dy[n0:n0 + m], S, 1, col, 1, S, dw, CgK, Coutg, CgK, S, Z1=m, Z2=G,
+              bs1=(Cout * S, C * KT * S, 0), bs2=(Coutg * S, CgK * S, Coutg * CgK), atomic=True)
+    return dw
+
+
+def _bias_grad(dy):
+    Nn, C = dy.shape[0], dy.shape[1]
+    S = dy[0, 0].numel()
+    db = torch.empty(C, dtype=torch.float32, device=dy.device)
+    N.call("pa_chan_sum", N.ptr(dy), N.ptr(db), Nn, C, S, 0, N.stream())
+    return db
+
+
+class _ConvNdFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, s, p, d, G):
+        dt = x.dtype
+        xf, wf = x.float().contiguous(), w.float().contiguous()
+        bf = b.float().contiguous() if b is not None else None
+        y, geo, _ = _conv_fwd(xf, wf, bf, s, p, d, G)
+        ctx.save_for_backward(xf, wf)
+        ctx.conf = (geo, G, dt, w.dtype, b is not None)
+        return y.to(dt)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xf, wf = ctx.saved_tensors
+        geo, G, dt, wdt, has_b = ctx.conf
+        dyf = dy.float().contiguous()
+        dx = _conv_dgrad(dyf, wf, tuple(xf.shape), geo, G).to(dt) if ctx.needs_input_grad[0] else None
+        dw = _conv_wgrad(dyf, xf, tuple(wf.shape), geo, G).to(wdt) if ctx.needs_input_grad[1] else None
+        db = _bias_grad(dyf).to(wdt) if has_b and ctx.needs_input_grad[2] else None
+        return dx, dw, db, None, None, None, None
+
+
+def supported_conv(x, w, groups=1):
+    return (_ok(x) and x.dim() in (4, 5) and w.dim() == x.dim() and groups >= 1 and x.shape[1] % groups == 0
+            and w.shape[0] % groups == 0 and w.shape[1] * groups == x.shape[1] and x.numel() > 0)
+
+
+def conv_nd(x, w, b=None, stride=1, padding=0, dilation=1, groups=1):
+    """x [N, C, (D,) H, W], w [Cout, C / groups, (kd,) kh, kw]."""
+    nd = x.dim() - 2
+    return _ConvNdFn.apply(x, w, b, _tup(stride, nd), _tup(padding, nd), _tup(dilation, nd), int(groups))
+
+
+# ------------------------------------------------------------------ transposed convolution
+
+
+def _convT_fwd(x, w, s, p, d, G, osp):
+    Nn, Cin = x.shape[0], x.shape[1]
+    sp = tuple(x.shape[2:])
+    k = tuple(w.shape[2:])
+    Coutg = w.shape[1]
+    Cout = Coutg * G
+    Cing = Cin // G
+    KT = w[0, 0].numel()
+    S = x[0, 0].numel()
+    CoKT = Coutg * KT
+    geo = _geo(Cout, _pad3(osp), _pad3(sp), _pad3(k), _pad3(s), _pad3z(p), _pad3(d))
+    y = torch.empty((Nn, Cout) + tuple(osp), dtype=torch.float32, device=x.device)
+    nb = _chunk(Nn, Cout * KT * S, G)
+    for n0 in range(0, Nn, nb):
+        m = min(nb, Nn - n0)
+        col = torch.empty(m, Cout * KT, S, dtype=torch.float32, device=x.device)
+        sgemm(w, 1, CoKT, x[n0:n0 + m], S, 1, col, S, CoKT, S, Cing, Z1=m, Z2=G,
+              bs1=(0, Cin * S, Cout * KT * S), bs2=(Cing * CoKT, Cing * S, CoKT * S))
+        _col2vol(col, y[n0:n0 + m], m, geo)
+    return y, geo
+
+
+class _ConvTNdFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, s, p, d, G, osp):
+        dt = x.dtype
+        xf, wf = x.float().contiguous(), w.float().contiguous()
+        y, geo = _convT_fwd(xf, wf, s, p, d, G, osp)
+        ctx.save_for_backward(xf, wf)
+        ctx.conf = (geo, G, dt, w.dtype)
+        return y.to(dt)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xf, wf = ctx.saved_tensors
+        geo, G, dt, wdt = ctx.conf
+        dyf = dy.float().contiguous()
+        Nn, Cin = xf.shape[0], xf.shape[1]
+        Coutg = wf.shape[1]
+        Cout, Cing = Coutg * G, Cin // G
+        KT = wf[0, 0].numel()
+        S = xf[0, 0].numel()
+        CoKT = Coutg * KT
+        dx = torch.empty(xf.shape, dtype=torch.float32, device=dy.device) if ctx.needs_input_grad[0] else None
+        dw = torch.zeros(wf.shape, dtype=torch.float32, device=dy.device) if ctx.needs_input_grad[1] else None
+        nb = _chunk(Nn, Cout * KT * S, G)
+        for n0 in range(0, Nn, nb):
+            m = min(nb, Nn - n0)
+            col = _vol2col(dyf[n0:n0 + m], m, geo, Cout * KT, S)
+            if dx is not None:  # dx[img][g] = W[g] col(dY)[img][g]
+                sgemm(wf, CoKT, 1, col, S, 1, dx[n0:n0 + m], S, Cing, S, CoKT, Z1=m, Z2=G,
+                      bs1=(0, Cout * KT * S, Cin * S), bs2=(Cing * CoKT, CoKT * S, Cing * S))
+            if dw is not None:  # dW[g] += x[img][g] col(dY)[img][g]^T
+                sgemm(xf[n0:n0 + m], S, 1, col, 1, S, dw, CoKT, Cing, CoKT, S, Z1=m, Z2=G,
+                      bs1=(Cin * S, Cout * KT * S, 0), bs2=(Cing * S, CoKT * S, Cing * CoKT), atomic=True)
+        return (dx.to(dt) if dx is not None else None, dw.to(wdt) if dw is not None else None,
+                None, None, None, None, None)
+
+
+def conv_transpose_nd(x, w, stride=1, padding=0, dilation=1, groups=1, output_padding=0):
+    """x [N, Cin, (D,) H, W], w [Cin, Cout / groups, (kd,) kh, kw] (Paddle / torch layout)."""
+    nd = x.dim() - 2
+    s, p, d, op = _tup(stride, nd), _tup(padding, nd), _tup(dilation, nd), _tup(output_padding, nd)
+    k = tuple(w.shape[2:])
+    osp = tuple((x.shape[2 + i] - 1) * s[i] - 2 * p[i] + d[i] * (k[i] - 1) + 1 + op[i] for i in range(nd))
+    return _ConvTNdFn.apply(x, w, s, p, d, int(groups), osp)
+
+
+def supported_conv_transpose(x, w, groups=1):
+    return (_ok(x) and x.dim() in (4, 5) and w.dim() == x.dim() and x.shape[1] == w.shape[0]
+            and x.shape[1] % groups == 0 and x.numel() > 0)
+
+
+# ------------------------------------------------------------------ pooling
+
+
+def pool_out(i, k, s, p, ceil):
+    return (i - k + 2 * p + s - 1) // s + 1 if ceil else (i - k + 2 * p) // s + 1
+
+
+class _PoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, typ, k, s, p, exclusive, ceil, need_mask):
+        x = x.contiguous()
+        dt = x.dtype
+        xc = x if dt in _DT else x.float()
+        nd = x.dim() - 2
+        sp = tuple(x.shape[2:])
+        osp = tuple(pool_out(sp[i], k[i], s[i], p[i], ceil) for i in range(nd))
+        NC = x.shape[0] * x.shape[1]
+        geo = _arr([*_pad3(sp), *_pad3(osp), *_pad3(k), *_pad3(s), *_pad3z(p)])
+        y = torch.empty(tuple(x.shape[:2]) + osp, dtype=xc.dtype, device=x.device)
+        mask = torch.empty(y.shape, dtype=torch.int32, device=x.device) if typ == 0 else None
+        N.call("pa_pool_fwd", _DT[xc.dtype], N.ptr(xc), N.ptr(y), N.ptr(mask), NC, geo, typ, int(exclusive),
+               N.stream())
+        ctx.save_for_backward(mask)
+        ctx.conf = (typ, exclusive, NC, tuple(x.shape), xc.dtype, dt, [*_pad3(sp), *_pad3(osp), *_pad3(k),
+                                                                       *_pad3(s), *_pad3z(p)])
+        if mask is not None:
+            ctx.mark_non_differentiable(mask)
+        return y.to(dt), mask
+
+    @staticmethod
+    def backward(ctx, dy, _dm):
+        (mask,) = ctx.saved_tensors
+        typ, exclusive, NC, xshape, cdt, dt, geo = ctx.conf
+        dyc = dy.contiguous().to(cdt)
+        dx = torch.empty(xshape, dtype=cdt, device=dy.device)
+        N.call("pa_pool_bwd", _DT[cdt], N.ptr(dyc), N.ptr(mask), N.ptr(dx), NC, _arr(geo), typ, int(exclusive),
+               N.stream())
+        return dx.to(dt), None, None, None, None, None, None, None
+
+
+def supported_pool(x):
+    return _ok(x) and x.dim() in (4, 5) and x.numel() > 0
+
+
+def pool_nd(x, pooling_type="max", ksize=2, stride=None, padding=0, exclusive=True, ceil_mode=False,
+            global_pooling=False, return_mask=False):
+    """Max / avg pooling over the trailing 2 or 3 dims of an NC[D]HW tensor.
+    Returns ``out`` (and the int32 in-plane argmax for max pooling if ``return_mask``)."""
+    nd = x.dim() - 2
+    k = _tup(ksize, nd)
+    s = _tup(stride if stride is not None else ksize, nd)
+    p = _tup(padding, nd)
+    if global_pooling:
+        k, p = tuple(x.shape[2:]), (0,) * nd
+    typ = 0 if pooling_type == "max" else 1
+    y, mask = _PoolFn.apply(x, typ, k, s, p, bool(exclusive), bool(ceil_mode), bool(return_mask))
+    return (y, mask) if return_mask else y
+
+
+# ------------------------------------------------------------------ unpool / maxout
+
+
+class _UnpoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, mask, osp):
+        x = x.contiguous()
+        dt = x.dtype
+        xc = x if dt in _DT else x.float()
+        m = mask.to(torch.int32).contiguous()
+        NC = x.shape[0] * x.shape[1]
+        IS, OS = x[0, 0].numel(), 1
+        for v in osp:
+            OS *= v
+        out = torch.zeros(tuple(x.shape[:2]) + tuple(osp), dtype=xc.dtype, device=x.device)
+        bad = torch.zeros(1, dtype=torch.int32, device=x.device)
+        N.call("pa_unpool", _DT[xc.dtype], 0, N.ptr(xc), N.ptr(m), N.ptr(out), NC, IS, OS, N.ptr(bad), N.stream())
+        if int(bad.item()):
+            raise ValueError("unpool: an index is outside the output plane")
+        ctx.save_for_backward(m)
+        ctx.conf = (tuple(x.shape), NC, IS, OS, xc.dtype, dt)
+        return out.to(dt)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (m,) = ctx.saved_tensors
+        xshape, NC, IS, OS, cdt, dt = ctx.conf
+        d = dout.contiguous().to(cdt)
+        dx = torch.empty(xshape, dtype=cdt, device=dout.device)
+        N.call("pa_unpool", _DT[cdt], 1, N.ptr(d), N.ptr(m), N.ptr(dx), NC, IS, OS, None, N.stream())
+        return dx.to(dt), None, None
+
+
+def unpool2d(x, indices, ksize, strides, paddings):
+    """Max unpool (unpool_op.cc: out = (in - 1) * stride - 2 * pad + ksize)."""
+    k, s, p = _tup(ksize, 2), _tup(strides, 2), _tup(paddings, 2)
+    osp = tuple((x.shape[2 + i] - 1) * s[i] - 2 * p[i] + k[i] for i in range(2))
+    return _UnpoolFn.apply(x, indices, osp)
+
+
+class _MaxoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, groups):
+        x = x.contiguous()
+        dt = x.dtype
+        xc = x if dt in _DT else x.float()
+        Nn, C = x.shape[0], x.shape[1]
+        Co = C // groups
+        S = x[0, 0].numel()
+        y = torch.empty((Nn, Co) + tuple(x.shape[2:]), dtype=xc.dtype, device=x.device)
+        N.call("pa_maxout", _DT[xc.dtype], N.ptr(xc), None, None, N.ptr(y), Nn, Co, groups, S, N.stream())
+        ctx.save_for_backward(xc, y)
+        ctx.conf = (groups, dt)
+        return y.to(dt)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, y = ctx.saved_tensors
+        groups, dt = ctx.conf
+        d = dy.contiguous().to(xc.dtype)
+        dx = torch.empty_like(xc)
+        Nn, Co = y.shape[0], y.shape[1]
+        N.call("pa_maxout", _DT[xc.dtype], N.ptr(xc), N.ptr(y), N.ptr(d), N.ptr(dx), Nn, Co, groups,
+               y[0, 0].numel(), N.stream())
+        return dx.to(dt), None
+
+
+def maxout(x, groups):
+    if x.shape[1] % groups:
+        raise ValueError("maxout: channels must be divisible by groups")
+    return _MaxoutFn.apply(x, int(groups))

@@ -128,20 +128,27 @@ def test_resnet_native_matches_torch_path():
         conv.set_enabled(native)
         try:
             m = copy.deepcopy(base).to(dtype)
-            loss = F.cross_entropy(m(x.to(dtype)).float(), y)
+            logits = m(x.to(dtype)).float()
+            loss = F.cross_entropy(logits, y)
             loss.backward()
             l1, l4 = list(m.layer1.children()), list(m.layer4.children())
             grads = [m.conv1.weight.grad, l1[0].conv2.weight.grad, l4[-1].conv3.weight.grad,
                      l4[-1].bn3.weight.grad, m.fc.weight.grad]
-            return loss.item(), [t.float().flatten() for t in grads]
+            return loss.item(), [t.float().flatten() for t in grads], logits.detach()
         finally:
             G.set_enabled(True)
             conv.set_enabled(True)
 
-    l32, g32 = run(torch.float32, False)
-    la, ga = run(torch.bfloat16, False)
-    ln, gn = run(torch.bfloat16, True)
-    assert abs(ln - l32) <= 2 * abs(la - l32) + 0.02, (ln, la, l32)
+    l32, g32, z32 = run(torch.float32, False)
+    la, ga, za = run(torch.bfloat16, False)
+    ln, gn, zn = run(torch.bfloat16, True)
+    # a random-init bf16 ResNet-50 carries ~30 % relative logit error on BOTH paths
+    # (measured: native 0.291, ATen/MIOpen 0.298), so the scalar loss gap to fp32 is
+    # noise of either sign; compare the logit error itself, plus a loose loss bound
+    rel = lambda a, b: ((a - b).norm() / b.norm()).item()  # noqa: E731
+    en, ea = rel(zn, z32), rel(za, z32)
+    assert en <= 1.25 * ea + 0.02, (en, ea)
+    assert abs(ln - l32) <= 0.15, (ln, la, l32)
     cos = lambda a, b: (a @ b / (a.norm() * b.norm())).item()  # noqa: E731
     # (a random-init bf16 ResNet-50's stem gradient is far from fp32 on either path;
     # the criterion is relative: native no worse than the vendor bf16 path)

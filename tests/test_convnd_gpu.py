@@ -1,0 +1,265 @@
+"""Channel-first conv / transposed conv / pooling / unpool / maxout kernels
+(csrc/kernels/convnd.hip via ops/convnd.py) against fp64 PyTorch references of
+the same ops: forward and both gradients, odd sizes, strides, paddings,
+dilations, groups (incl. depthwise), 2-D and 3-D; the exact-fp32 MFMA GEMM on
+strided / batched / atomic forms."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from paddle_amd.ops import convnd as C
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (37, 129, 65), (128, 128, 16), (300, 70, 513)])
+def test_sgemm_forms(M, N, K):
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    A = torch.randn(3, 2, M, K, generator=g, device=DEV)
+    B = torch.randn(3, 2, K, N, generator=g, device=DEV)
+    ref = (A.double() @ B.double())
+    # row-major A and B, batch (3, 2) on z1 x z2, bias per row (+ per z2 offset)
+    Cc = torch.empty(3, 2, M, N, device=DEV)
+    bias = torch.randn(2, M, generator=g, device=DEV)
+    C.sgemm(A, K, 1, B, N, 1, Cc, N, M, N, K, Z1=3, Z2=2, bs1=(2 * M * K, 2 * K * N, 2 * M * N),
+            bs2=(M * K, K * N, M * N), bias=bias, bs_bias2=M)
+    assert _rel(Cc, ref + bias.double()[None, :, :, None]) < 1e-6
+    # transposed operands (A given as [K, M], B as [N, K]), beta = 1
+    At = A[0, 0].t().contiguous()
+    Bt = B[0, 0].t().contiguous()
+    C0 = torch.randn(M, N, generator=g, device=DEV)
+    C1 = C0.clone()
+    C.sgemm(At, 1, M, Bt, 1, K, C1, N, M, N, K, alpha=0.5, beta=1.0)
+    assert _rel(C1, 0.5 * ref[0, 0] + C0.double()) < 1e-6
+    # k-batch (sum of the 3 z1 products in registers) and atomic split over z2
+    Ca = torch.zeros(M, N, device=DEV)
+    C.sgemm(A, K, 1, B, N, 1, Ca, N, M, N, K, Z1=1, Z2=2, bs2=(M * K, K * N, 0), kb=3, kbA=2 * M * K,
+            kbB=2 * K * N, atomic=True)
+    assert _rel(Ca, ref.sum((0, 1))) < 1e-6
+
+
+CONV2D = [
+    # (N, C, H, W, Cout, k, stride, pad, dil, groups, bias)
+    (2, 3, 9, 7, 5, (3, 3), (1, 1), (1, 1), (1, 1), 1, True),
+    (3, 8, 11, 10, 12, (3, 2), (2, 1), (0, 1), (1, 2), 4, False),
+    (2, 16, 8, 8, 16, (3, 3), (1, 1), (1, 1), (1, 1), 16, True),   # depthwise
+    (1, 64, 14, 14, 128, (1, 1), (2, 2), (0, 0), (1, 1), 1, False),
+    (4, 5, 6, 13, 7, (5, 5), (3, 2), (2, 2), (1, 1), 1, True),
+]
+
+
+@pytest.mark.parametrize("cfg", CONV2D)
+def test_conv2d_fwd_bwd(cfg):
+    Nn, Ci, H, W, Co, k, s, p, d, G, has_b = cfg
+    g = torch.Generator().manual_seed(sum(cfg[:5]))
+    x = torch.randn(Nn, Ci, H, W, generator=g, dtype=torch.float64)
+    w = torch.randn(Co, Ci // G, *k, generator=g, dtype=torch.float64) * 0.3
+    b = torch.randn(Co, generator=g, dtype=torch.float64) if has_b else None
+    xr, wr = x.clone().requires_grad_(), w.clone().requires_grad_()
+    br = b.clone().requires_grad_() if has_b else None
+    ref = F.conv2d(xr, wr, br, s, p, d, G)
+    xd, wd = x.float().to(DEV).requires_grad_(), w.float().to(DEV).requires_grad_()
+    bd = b.float().to(DEV).requires_grad_() if has_b else None
+    assert C.supported_conv(xd, wd, G)
+    y = C.conv_nd(xd, wd, bd, s, p, d, G)
+    assert y.shape == ref.shape
+    assert _rel(y, ref) < 1e-5
+    gy = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    ref.backward(gy)
+    y.backward(gy.float().to(DEV))
+    assert _rel(xd.grad, xr.grad) < 1e-5
+    assert _rel(wd.grad, wr.grad) < 1e-5
+    if has_b:
+        assert _rel(bd.grad, br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("cfg", [
+    (2, 3, (5, 6, 7), 4, (3, 3, 3), (1, 1, 1), (1, 1, 1), (1, 1, 1), 1),
+    (1, 4, (4, 9, 8), 6, (2, 3, 2), (2, 2, 1), (0, 1, 1), (1, 1, 2), 2),
+])
+def test_conv3d_fwd_bwd(cfg):
+    Nn, Ci, sp, Co, k, s, p, d, G = cfg
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(Nn, Ci, *sp, generator=g, dtype=torch.float64)
+    w = torch.randn(Co, Ci // G, *k, generator=g, dtype=torch.float64) * 0.3
+    xr, wr = x.clone().requires_grad_(), w.clone().requires_grad_()
+    ref = F.conv3d(xr, wr, None, s, p, d, G)
+    xd, wd = x.float().to(DEV).requires_grad_(), w.float().to(DEV).requires_grad_()
+    y = C.conv_nd(xd, wd, None, s, p, d, G)
+    assert _rel(y, ref) < 1e-5
+    gy = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    ref.backward(gy)
+    y.backward(gy.float().to(DEV))
+    assert _rel(xd.grad, xr.grad) < 1e-5
+    assert _rel(wd.grad, wr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("cfg", [
+    (2, 4, (5, 6), 3, (3, 3), (2, 2), (1, 1), (1, 1), 1, (0, 0)),
+    (1, 6, (4, 7), 2, (4, 3), (2, 3), (1, 0), (1, 1), 3, (1, 2)),
+    (2, 2, (3, 4, 3), 3, (3, 2, 3), (2, 1, 2), (1, 0, 1), (1, 2, 1), 1, (1, 0, 0)),
+])
+def test_conv_transpose_fwd_bwd(cfg):
+    Nn, Ci, sp, Cog, k, s, p, d, G, op = cfg
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(Nn, Ci, *sp, generator=g, dtype=torch.float64)
+    w = torch.randn(Ci, Cog, *k, generator=g, dtype=torch.float64) * 0.3
+    xr, wr = x.clone().requires_grad_(), w.clone().requires_grad_()
+    fn = F.conv_transpose2d if len(sp) == 2 else F.conv_transpose3d
+    ref = fn(xr, wr, None, s, p, op, G, d)
+    xd, wd = x.float().to(DEV).requires_grad_(), w.float().to(DEV).requires_grad_()
+    y = C.conv_transpose_nd(xd, wd, s, p, d, G, op)
+    assert y.shape == ref.shape
+    assert _rel(y, ref) < 1e-5
+    gy = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    ref.backward(gy)
+    y.backward(gy.float().to(DEV))
+    assert _rel(xd.grad, xr.grad) < 1e-5
+    assert _rel(wd.grad, wr.grad) < 1e-5
+
+
+def test_conv_bf16_input_computes_in_fp32():
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 8, 10, 10, generator=g).to(torch.bfloat16)
+    w = torch.randn(8, 8, 3, 3, generator=g).to(torch.bfloat16)
+    y = C.conv_nd(x.to(DEV), w.to(DEV), None, 1, 1, 1, 1)
+    assert y.dtype == torch.bfloat16
+    ref = F.conv2d(x.double(), w.double(), None, 1, 1)
+    assert _rel(y, ref) < 1e-2
+
+
+def _paddle_avg_ref(x, k, s, p, exclusive, ceil):
+    """pooling.cu KernelPool{2,3}D avg semantics (clamped window, divisor = clamped
+    size if exclusive else the full kernel), computed in fp64 by loops over windows."""
+    nd = x.dim() - 2
+    sp = x.shape[2:]
+    osp = [C.pool_out(sp[i], k[i], s[i], p[i], ceil) for i in range(nd)]
+    out = torch.zeros(tuple(x.shape[:2]) + tuple(osp), dtype=torch.float64)
+    import itertools
+    for o in itertools.product(*[range(v) for v in osp]):
+        lo = [max(o[i] * s[i] - p[i], 0) for i in range(nd)]
+        hi = [min(o[i] * s[i] - p[i] + k[i], sp[i]) for i in range(nd)]
+        sl = (slice(None), slice(None)) + tuple(slice(lo[i], hi[i]) for i in range(nd))
+        win = x[sl]
+        cnt = 1
+        for i in range(nd):
+            cnt *= (hi[i] - lo[i]) if exclusive else k[i]
+        out[(slice(None), slice(None)) + tuple(o)] = win.sum(tuple(range(2, 2 + nd))) / cnt if cnt else 0
+    return out
+
+
+@pytest.mark.parametrize("shape,k,s,p,exclusive,ceil", [
+    ((2, 3, 9, 8), (3, 3), (2, 2), (1, 1), True, False),
+    ((2, 3, 9, 8), (3, 2), (2, 3), (1, 0), False, True),
+    ((1, 2, 5, 6, 7), (2, 3, 2), (2, 2, 2), (0, 1, 1), True, True),
+    ((1, 2, 5, 6, 7), (3, 3, 3), (1, 2, 2), (1, 1, 0), False, False),
+])
+def test_avg_pool_fwd_bwd(shape, k, s, p, exclusive, ceil):
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(*shape, generator=g, dtype=torch.float64)
+    xr = x.clone().requires_grad_()
+    ref = _paddle_avg_ref(xr, k, s, p, exclusive, ceil)
+    xd = x.float().to(DEV).requires_grad_()
+    y = C.pool_nd(xd, "avg", k, s, p, exclusive, ceil)
+    assert y.shape == ref.shape
+    assert _rel(y, ref) < 1e-6
+    gy = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    ref.backward(gy)
+    y.backward(gy.float().to(DEV))
+    assert _rel(xd.grad, xr.grad) < 1e-6
+
+
+@pytest.mark.parametrize("shape,k,s,p", [
+    ((2, 3, 9, 8), (3, 3), (2, 2), (1, 1)),
+    ((2, 4, 7, 10), (2, 4), (1, 3), (0, 2)),
+    ((1, 2, 6, 7, 5), (2, 3, 2), (2, 2, 1), (1, 1, 0)),
+])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_max_pool_with_index_fwd_bwd(shape, k, s, p, dtype):
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(*shape, generator=g).to(dtype).double()
+    xr = x.clone().requires_grad_()
+    fn = F.max_pool2d if len(shape) == 4 else F.max_pool3d
+    ref, idx = fn(xr, k, s, p, return_indices=True)
+    xd = x.to(dtype).to(DEV).requires_grad_()
+    y, mask = C.pool_nd(xd, "max", k, s, p, return_mask=True)
+    assert torch.equal(y.double().cpu(), ref.detach())
+    assert torch.equal(mask.long().cpu(), idx)
+    gy = torch.randn(ref.shape, generator=g, dtype=torch.float64).to(dtype).double()
+    ref.backward(gy)
+    y.backward(gy.to(dtype).to(DEV))
+    assert _rel(xd.grad, xr.grad) < (1e-6 if dtype == torch.float32 else 1e-2)
+
+
+def test_unpool_and_maxout():
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(2, 3, 8, 6, generator=g)
+    pooled, idx = F.max_pool2d(x, 2, 2, return_indices=True)
+    pr = pooled.double().requires_grad_()
+    ref = F.max_unpool2d(pr, idx, 2, 2)
+    pd = pooled.to(DEV).requires_grad_()
+    out = C.unpool2d(pd, idx.to(torch.int32).to(DEV), 2, 2, 0)
+    assert torch.equal(out.double().cpu(), ref.detach())
+    gy = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    ref.backward(gy)
+    out.backward(gy.float().to(DEV))
+    assert _rel(pd.grad, pr.grad) < 1e-7
+    with pytest.raises(ValueError):
+        C.unpool2d(pd.detach(), torch.full(idx.shape, 999, dtype=torch.int32, device=DEV), 2, 2, 0)
+
+    x = torch.randn(2, 6, 4, 5, generator=g, dtype=torch.float64)
+    xr = x.clone().requires_grad_()
+    ref = xr.reshape(2, 3, 2, 4, 5).max(2).values
+    xd = x.float().to(DEV).requires_grad_()
+    y = C.maxout(xd, 2)
+    assert torch.equal(y.double().cpu(), ref.detach().float().double())
+    gy = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    ref.backward(gy)
+    y.backward(gy.float().to(DEV))
+    assert _rel(xd.grad, xr.grad) < 1e-7
+
+
+def test_fluid_conv_pool_program_matches_cpu():
+    """A Fluid conv -> pool -> conv_transpose -> fc program: forward and parameter
+    gradients on CUDAPlace (convnd kernels) equal CPUPlace (ATen) within fp32."""
+    import numpy as np
+
+    import paddle_amd.fluid as fluid
+
+    def run(place):
+        main, startup = fluid.Program(), fluid.Program()
+        main.random_seed = startup.random_seed = 11
+        with fluid.program_guard(main, startup):
+            img = fluid.layers.data("img", [3, 12, 12], dtype="float32")
+            c = fluid.layers.conv2d(img, 8, 3, padding=1, act="relu", groups=1)
+            pl = fluid.layers.pool2d(c, 2, "max", 2)
+            c2 = fluid.layers.conv2d(pl, 8, 3, padding=1, groups=4)
+            ct = fluid.layers.conv2d_transpose(c2, 4, filter_size=2, stride=2)
+            pa = fluid.layers.pool2d(ct, 3, "avg", 2, pool_padding=1)
+            loss = fluid.layers.mean(fluid.layers.fc(pa, 5))
+            fluid.optimizer.SGD(0.1).minimize(loss)
+        exe = fluid.Executor(place)
+        scope = fluid.core.Scope()
+        with fluid.scope_guard(scope):
+            exe.run(startup)
+            rs = np.random.RandomState(1)  # same initial weights on both places
+            for prm in main.global_block().all_parameters():
+                t = scope.find_var(prm.name).get_tensor()
+                t.set((rs.randn(*np.array(t).shape) * 0.2).astype("float32"), place)
+            x = np.random.RandomState(0).randn(4, 3, 12, 12).astype("float32")
+            outs = [exe.run(main, feed={"img": x}, fetch_list=[loss])[0] for _ in range(3)]
+            params = [np.array(scope.find_var(p.name).get_tensor()) for p in main.global_block().all_parameters()]
+        return np.array(outs).ravel(), params
+
+    lc, pc = run(fluid.CPUPlace())
+    lg, pg = run(fluid.CUDAPlace(0))
+    np.testing.assert_allclose(lg, lc, rtol=1e-4, atol=1e-5)
+    assert len(pc) == len(pg) == 8
+    for a, b in zip(pg, pc):
+        np.testing.assert_allclose(a, b, rtol=1e-3, atol=1e-4)

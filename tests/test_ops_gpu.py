@@ -61,6 +61,17 @@ GRAD_CASES = [
     ("elementwise_sub", {"X": _r(2, 3, 4), "Y": _r(3)}, {"axis": 1}, ["X", "Y"]),
     ("reduce_sum", {"X": _r(3, 4, 5)}, {"dim": [0, 2]}, ["X"]),
     ("reduce_mean", {"X": _r(3, 4, 5)}, {"dim": [1], "keep_dim": True}, ["X"]),
+    # channel-first conv / pool on convnd.hip (vol2col + fp32 MFMA GEMM, gather pool backward)
+    ("conv2d", {"Input": _r(2, 4, 6, 5), "Filter": _r(6, 2, 3, 3)},
+     {"strides": [2, 1], "paddings": [1, 0], "dilations": [1, 2], "groups": 2}, ["Input", "Filter"]),
+    ("conv3d", {"Input": _r(2, 3, 4, 5, 4), "Filter": _r(4, 3, 2, 3, 2)}, {"paddings": [1, 1, 0]},
+     ["Input", "Filter"]),
+    ("conv2d_transpose", {"Input": _r(2, 4, 3, 4), "Filter": _r(4, 3, 3, 3)},
+     {"strides": [2, 2], "paddings": [1, 0]}, ["Input", "Filter"]),
+    ("pool2d", {"X": _r(2, 3, 7, 6)}, {"pooling_type": "avg", "ksize": [3, 2], "strides": [2, 2],
+                                       "paddings": [1, 1], "exclusive": True}, ["X"]),
+    ("pool3d", {"X": _r(2, 2, 5, 4, 6)}, {"pooling_type": "avg", "ksize": [2, 2, 3], "strides": [2, 1, 2],
+                                          "paddings": [1, 0, 1], "exclusive": False}, ["X"]),
 ]
 
 
@@ -68,8 +79,9 @@ GRAD_CASES = [
 def test_native_op_grads_on_device(op, inputs, attrs, grad):
     t = OpTest()
     t.op_type, t.inputs, t.attrs = op, inputs, attrs
-    t.outputs = {"Out": np.zeros(1, "float32")}
-    t.check_grad(grad, ["Out"], max_relative_error=0.01, places=[_gpu_place()])
+    out = "Output" if op.startswith("conv") else "Out"
+    t.outputs = {out: np.zeros(1, "float32")}
+    t.check_grad(grad, [out], max_relative_error=0.01, places=[_gpu_place()])
 
 
 def test_sequence_pool_grad_on_device():
