@@ -354,6 +354,115 @@ __global__ void maxout_bwd_kernel(const T* __restrict__ x, const T* __restrict__
   }
 }
 
+
+// ================================================================ batch norm (NC[D]HW)
+// Per-channel reductions over (n, s) split into G slices per channel (grid C x G);
+// the statistics pass sums (x - shift) and (x - shift)^2 with shift = the channel's
+// first element (cancellation-safe without Welford), the backward pass sums dy and
+// dy * xhat.  Reference: batch_norm_op.cc (biased batch variance for the running
+// average, SavedVariance = 1 / sqrt(var + eps)), batch_norm_op.cu.cc.
+template <typename T>
+__global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                         const T* __restrict__ y, const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd, float* __restrict__ part,
+                                                         int N, int C, long S, int G, int relu) {
+  __shared__ float red[4];
+  const int c = blockIdx.x, gi = blockIdx.y;
+  const long M = (long)N * S;
+  const long chunk = (M + G - 1) / G;
+  const long lo = gi * chunk, hi = min(M, lo + chunk);
+  float a = 0.f, b = 0.f;
+  if (!dy) {
+    const float shift = IO<T>::ld(x, (long)c * S);
+    for (long i = lo + threadIdx.x; i < hi; i += 256) {
+      const long n = i / S, sidx = i % S;
+      const float v = IO<T>::ld(x, ((long)n * C + c) * S + sidx) - shift;
+      a += v;
+      b += v * v;
+    }
+  } else {
+    const float mu = mean[c], rs = rstd[c];
+    for (long i = lo + threadIdx.x; i < hi; i += 256) {
+      const long n = i / S, sidx = i % S;
+      const long off = ((long)n * C + c) * S + sidx;
+      float g = IO<T>::ld(dy, off);
+      if (relu && IO<T>::ld(y, off) <= 0.f) g = 0.f;
+      a += g;
+      b += g * (IO<T>::ld(x, off) - mu) * rs;
+    }
+  }
+  a = block_sum<256>(a, red);
+  __syncthreads();
+  b = block_sum<256>(b, red);
+  if (threadIdx.x == 0) {
+    part[((long)c * G + gi) * 2] = a;
+    part[((long)c * G + gi) * 2 + 1] = b;
+  }
+}
+
+// mode 0: training statistics -> mean, rstd, running averages (momentum)
+// mode 1: backward sums -> dbias (o0), dscale (o1)
+// mode 2: inference -> mean = running mean, rstd from the running variance
+template <typename T>
+__global__ void bn_finalize_kernel(const T* __restrict__ x, const float* __restrict__ part, int C, int G, long M,
+                                   float eps, float momentum, int mode, const float* __restrict__ run_mean,
+                                   const float* __restrict__ run_var, float* __restrict__ o0, float* __restrict__ o1,
+                                   float* __restrict__ mean_out, float* __restrict__ var_out, long S,
+                                   int unbiased) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  if (mode == 2) {
+    o0[c] = run_mean[c];
+    o1[c] = rsqrtf(run_var[c] + eps);
+    return;
+  }
+  double a = 0.0, b = 0.0;
+  for (int g = 0; g < G; ++g) {
+    a += part[((long)c * G + g) * 2];
+    b += part[((long)c * G + g) * 2 + 1];
+  }
+  if (mode == 1) {
+    o0[c] = (float)a;
+    o1[c] = (float)b;
+    return;
+  }
+  const double shift = IO<T>::ld(x, (long)c * S);
+  const double m1 = a / (double)M;
+  double var = b / (double)M - m1 * m1;
+  if (var < 0.0) var = 0.0;
+  const float mean = (float)(shift + m1);
+  o0[c] = mean;
+  o1[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (mean_out) mean_out[c] = run_mean[c] * momentum + mean * (1.f - momentum);
+  const double rv = (unbiased && M > 1) ? var * (double)M / (double)(M - 1) : var;
+  if (var_out) var_out[c] = run_var[c] * momentum + (float)rv * (1.f - momentum);
+}
+
+// forward: y = (x - mean) * rstd * scale + bias (+ relu)
+// backward: dx = scale * rstd * (g - dbias / M - xhat * dscale / M), g = dy masked by relu
+template <typename T>
+__global__ void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ dy, const T* __restrict__ y,
+                                T* __restrict__ out, const float* __restrict__ mean, const float* __restrict__ rstd,
+                                const float* __restrict__ scale, const float* __restrict__ bias,
+                                const float* __restrict__ dbias, const float* __restrict__ dscale, int C, long S,
+                                long total, long M, int relu) {
+  GRID_STRIDE(i, total) {
+    const int c = (int)((i / S) % C);
+    const float xh = (IO<T>::ld(x, i) - mean[c]) * rstd[c];
+    const float sc = scale ? scale[c] : 1.f;
+    if (!dy) {
+      float v = xh * sc + (bias ? bias[c] : 0.f);
+      if (relu && v < 0.f) v = 0.f;
+      IO<T>::st(out, i, v);
+    } else {
+      float g = IO<T>::ld(dy, i);
+      if (relu && IO<T>::ld(y, i) <= 0.f) g = 0.f;
+      const float inv = 1.f / (float)M;
+      IO<T>::st(out, i, sc * rstd[c] * (g - dbias[c] * inv - xh * dscale[c] * inv));
+    }
+  }
+}
+
 }  // namespace
 
 // ================================================================ C ABI
@@ -486,6 +595,71 @@ PA_EXPORT int pa_unpool(int dt, int backward, const void* src, const int* mask, 
       hipLaunchKernelGGL(unpool_bwd_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)src, mask,
                          (float*)dst, NC, IS, OS);
   }
+  PA_LAUNCH_CHECK();
+}
+
+
+static int bn_groups(int C, long M) {
+  long g = 2048 / (C > 0 ? C : 1);
+  const long cap = (M + 2047) / 2048;
+  if (g > cap) g = cap;
+  if (g > 1024) g = 1024;
+  return (int)(g < 1 ? 1 : g);
+}
+
+PA_EXPORT int pa_bn_nchw_groups(int C, long M) { return bn_groups(C, M); }
+
+// Training forward: stats (mean, rstd, running outputs) + normalised output.
+// part holds C * G * 2 floats (G = pa_bn_nchw_groups(C, N * S)).
+PA_EXPORT int pa_bn_nchw_fwd(int dt, const void* x, void* y, const float* scale, const float* bias,
+                             const float* run_mean, const float* run_var, float* mean_out, float* var_out,
+                             float* mean, float* rstd, float* part, int N, int C, long S, float eps, float momentum,
+                             int training, int relu, int unbiased, hipStream_t st) {
+  const long M = (long)N * S, total = M * C;
+  if (C <= 0 || M <= 0) return 0;
+  const int G = bn_groups(C, M);
+#define BN_FWD(T)                                                                                                 \
+  if (training)                                                                                                   \
+    hipLaunchKernelGGL(bn_partial_kernel<T>, dim3((unsigned)C, (unsigned)G), dim3(256), 0, st, (const T*)x,       \
+                       (const T*)nullptr, (const T*)nullptr, (const float*)nullptr, (const float*)nullptr, part, N, C, \
+                       S, G, 0);                                                                                  \
+  hipLaunchKernelGGL(bn_finalize_kernel<T>, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, (const T*)x, part, C, \
+                     G, M, eps, momentum, training ? 0 : 2, run_mean, run_var, mean, rstd, training ? mean_out : nullptr, \
+                     training ? var_out : nullptr, S, unbiased);                                                  \
+  hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_for(total)), dim3(256), 0, st, (const T*)x, (const T*)nullptr,   \
+                     (const T*)nullptr, (T*)y, mean, rstd, scale, bias, (const float*)nullptr, (const float*)nullptr, C, \
+                     S, total, M, relu);
+  if (dt == 1) {
+    BN_FWD(u16)
+  } else {
+    BN_FWD(float)
+  }
+#undef BN_FWD
+  PA_LAUNCH_CHECK();
+}
+
+// Backward: dscale, dbias (fp32, [C]) and dx.  y is the forward output (relu mask).
+PA_EXPORT int pa_bn_nchw_bwd(int dt, const void* x, const void* dy, const void* y, const float* mean,
+                             const float* rstd, const float* scale, float* dscale, float* dbias, void* dx, float* part,
+                             int N, int C, long S, int relu, hipStream_t st) {
+  const long M = (long)N * S, total = M * C;
+  if (C <= 0 || M <= 0) return 0;
+  const int G = bn_groups(C, M);
+#define BN_BWD(T)                                                                                                  \
+  hipLaunchKernelGGL(bn_partial_kernel<T>, dim3((unsigned)C, (unsigned)G), dim3(256), 0, st, (const T*)x,           \
+                     (const T*)dy, (const T*)y, mean, rstd, part, N, C, S, G, relu);                                \
+  hipLaunchKernelGGL(bn_finalize_kernel<T>, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, (const T*)x, part, C, \
+                     G, M, 0.f, 0.f, 1, (const float*)nullptr, (const float*)nullptr, dbias, dscale, (float*)nullptr, \
+                     (float*)nullptr, S, 0);                                                                        \
+  if (dx)                                                                                                          \
+    hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_for(total)), dim3(256), 0, st, (const T*)x, (const T*)dy,      \
+                       (const T*)y, (T*)dx, mean, rstd, scale, (const float*)nullptr, dbias, dscale, C, S, total, M, relu);
+  if (dt == 1) {
+    BN_BWD(u16)
+  } else {
+    BN_BWD(float)
+  }
+#undef BN_BWD
   PA_LAUNCH_CHECK();
 }
 

@@ -358,6 +358,16 @@ def batch_norm(x, running_mean, running_var, weight, bias, training=False, momen
             return _conv.batch_norm_nhwc_train(x, weight, bias, running_mean, running_var, momentum, epsilon)
         return _conv.batch_norm_nhwc_eval(x, weight, bias, running_mean, running_var, epsilon)
     nchw = _nchw(x, data_format) or x.dim() == 2
+    if (nchw and x.dim() >= 2 and _cnd.supported_bn(x) and weight is not None and bias is not None
+            and running_mean is not None and running_var is not None):
+        # channel-first on the GPU: convnd.hip batch norm (no MIOpen)
+        y, mo, vo, _, _ = _cnd.batch_norm_nchw(x, weight, bias, running_mean, running_var, momentum, epsilon,
+                                               training, unbiased_running_var=True)
+        if training:
+            with torch.no_grad():
+                running_mean.copy_(mo)
+                running_var.copy_(vo)
+        return y
     if not nchw:
         x = x.movedim(-1, 1)
     y = F.batch_norm(x, running_mean, running_var, weight, bias, training, 1.0 - momentum, epsilon)

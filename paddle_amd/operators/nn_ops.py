@@ -239,6 +239,17 @@ def batch_norm(ctx):
     nhwc = ctx.attr("data_layout") == "NHWC"
     xc = x.movedim(-1, 1) if nhwc and x.dim() > 2 else x
     test = ctx.attr("is_test") or ctx.attr("use_global_stats")
+    if _cnd.supported_bn(xc.contiguous()) and sc is not None and b is not None:
+        y, mean_out, var_out, saved_m, saved_v = _cnd.batch_norm_nchw(
+            xc.contiguous(), sc, b, m, v, mom, eps, training=not test, relu=bool(ctx.attr("fuse_with_relu")))
+        if nhwc and x.dim() > 2:
+            y = y.movedim(1, -1)
+        ctx.set_output("Y", y)
+        ctx.set_output("MeanOut", mean_out.to(m.dtype))
+        ctx.set_output("VarianceOut", var_out.to(v.dtype))
+        ctx.set_output("SavedMean", saved_m)
+        ctx.set_output("SavedVariance", saved_v)
+        return
     if test:
         y = F.batch_norm(xc, m, v, sc, b, False, 0.0, eps)
         mean_out, var_out = m, v

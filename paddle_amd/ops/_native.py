@@ -159,6 +159,9 @@ _SIGS = {
     "pa_pool_fwd": [_I, _P, _P, _P, _L, _P, _I, _I, _P],
     "pa_pool_bwd": [_I, _P, _P, _P, _L, _P, _I, _I, _P],
     "pa_unpool": [_I, _I, _P, _P, _P, _L, _L, _L, _P, _P],
+    "pa_bn_nchw_groups": [_I, _L],
+    "pa_bn_nchw_fwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _L, _F, _F, _I, _I, _I, _P],
+    "pa_bn_nchw_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _L, _I, _P],
     "pa_maxout": [_I, _P, _P, _P, _P, _I, _I, _I, _L, _P],
     "pa_flash_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _LP, _I, _I, _I, _I, _I, _I, _F, _I, _P, _P],
 }

@@ -411,3 +411,65 @@ def maxout(x, groups):
     if x.shape[1] % groups:
         raise ValueError("maxout: channels must be divisible by groups")
     return _MaxoutFn.apply(x, int(groups))
+
+
+# ------------------------------------------------------------------ batch norm (channel-first)
+
+
+def _bn_part(x, C):
+    M = x.numel() // C
+    G = int(N.lib().pa_bn_nchw_groups(C, M))
+    return torch.empty(C * G * 2, dtype=torch.float32, device=x.device)
+
+
+class _BatchNormNCHW(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, scale, bias, run_mean, run_var, momentum, eps, training, relu, unbiased):
+        x = x.contiguous()
+        dt = x.dtype
+        xc = x if dt in _DT else x.float()
+        Nn, C = x.shape[0], x.shape[1]
+        S = x[0, 0].numel() if x.dim() > 2 else 1
+        f = lambda t: t.float().contiguous() if t is not None else None  # noqa: E731
+        sc, bi, rm, rv = f(scale), f(bias), f(run_mean), f(run_var)
+        y = torch.empty_like(xc)
+        mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        mean_out = torch.empty_like(mean) if training else rm.clone()
+        var_out = torch.empty_like(mean) if training else rv.clone()
+        part = _bn_part(xc, C)
+        N.call("pa_bn_nchw_fwd", _DT[xc.dtype], N.ptr(xc), N.ptr(y), N.ptr(sc), N.ptr(bi), N.ptr(rm), N.ptr(rv),
+               N.ptr(mean_out), N.ptr(var_out), N.ptr(mean), N.ptr(rstd), N.ptr(part), Nn, C, S, float(eps),
+               float(momentum), int(training), int(relu), int(unbiased), N.stream())
+        ctx.save_for_backward(xc, y, mean, rstd, sc)
+        ctx.conf = (relu, dt, scale.dtype if scale is not None else None, bias.dtype if bias is not None else None,
+                    Nn, C, S)
+        ctx.mark_non_differentiable(mean_out, var_out, mean, rstd)
+        return y.to(dt), mean_out, var_out, mean, rstd
+
+    @staticmethod
+    def backward(ctx, dy, *_):
+        xc, y, mean, rstd, sc = ctx.saved_tensors
+        relu, dt, sdt, bdt, Nn, C, S = ctx.conf
+        d = dy.contiguous().to(xc.dtype)
+        dscale = torch.empty(C, dtype=torch.float32, device=dy.device)
+        dbias = torch.empty_like(dscale)
+        dx = torch.empty_like(xc) if ctx.needs_input_grad[0] else None
+        N.call("pa_bn_nchw_bwd", _DT[xc.dtype], N.ptr(xc), N.ptr(d), N.ptr(y), N.ptr(mean), N.ptr(rstd), N.ptr(sc),
+               N.ptr(dscale), N.ptr(dbias), N.ptr(dx), N.ptr(_bn_part(xc, C)), Nn, C, S, int(relu), N.stream())
+        return (dx.to(dt) if dx is not None else None, dscale.to(sdt) if sdt is not None else None,
+                dbias.to(bdt) if bdt is not None else None, None, None, None, None, None, None, None)
+
+
+def supported_bn(x):
+    return _ok(x) and x.dim() >= 2 and x.numel() > 0 and x.is_contiguous()
+
+
+def batch_norm_nchw(x, scale, bias, run_mean, run_var, momentum=0.9, eps=1e-5, training=True, relu=False,
+                    unbiased_running_var=False):
+    """Channel-first BatchNorm (Fluid batch_norm, NCHW / NC / NCDHW).
+    Returns (y, mean_out, var_out, saved_mean, saved_inv_std); running averages use
+    the biased batch variance (Fluid batch_norm_op.cc; ``unbiased_running_var`` for the
+    2.x layer convention) and Paddle's momentum (running = m * running + (1 - m) * batch)."""
+    return _BatchNormNCHW.apply(x, scale, bias, run_mean, run_var, float(momentum), float(eps), bool(training),
+                                bool(relu), bool(unbiased_running_var))

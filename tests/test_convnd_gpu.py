@@ -263,3 +263,64 @@ def test_fluid_conv_pool_program_matches_cpu():
     assert len(pc) == len(pg) == 8
     for a, b in zip(pg, pc):
         np.testing.assert_allclose(a, b, rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("shape", [(4, 6, 5, 7), (16, 10), (2, 3, 4, 5, 6), (1, 8, 33, 65)])
+@pytest.mark.parametrize("relu", [False, True])
+def test_batch_norm_nchw_train(shape, relu):
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(*shape, generator=g, dtype=torch.float64) * 2 + 3
+    C = shape[1]
+    sc = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
+    bi = torch.randn(C, generator=g, dtype=torch.float64)
+    rm, rv = torch.randn(C, generator=g, dtype=torch.float64), torch.rand(C, generator=g, dtype=torch.float64) + 1
+    xr, sr, br = (t.clone().requires_grad_() for t in (x, sc, bi))
+    dims = [0] + list(range(2, x.dim()))
+    shp = [1, C] + [1] * (x.dim() - 2)
+    mu, var = xr.mean(dims), xr.var(dims, unbiased=False)
+    ref = (xr - mu.reshape(shp)) / torch.sqrt(var.reshape(shp) + 1e-5) * sr.reshape(shp) + br.reshape(shp)
+    if relu:
+        ref = torch.relu(ref)
+    xd, sd, bd = (t.float().to(DEV).requires_grad_() for t in (x, sc, bi))
+    y, mo, vo, sm, sv = C_bn(xd, sd, bd, rm.float().to(DEV), rv.float().to(DEV), relu)
+    assert _rel(y, ref) < 1e-5
+    torch.testing.assert_close(mo.double().cpu(), 0.9 * rm + 0.1 * mu.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(vo.double().cpu(), 0.9 * rv + 0.1 * var.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(sv.double().cpu(), 1 / torch.sqrt(var.detach() + 1e-5), rtol=1e-5, atol=1e-6)
+    gy = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    ref.backward(gy)
+    y.backward(gy.float().to(DEV))
+    assert _rel(xd.grad, xr.grad) < 1e-4
+    assert _rel(sd.grad, sr.grad) < 1e-5
+    assert _rel(bd.grad, br.grad) < 1e-5
+
+
+def C_bn(x, s, b, rm, rv, relu):
+    return C.batch_norm_nchw(x, s, b, rm, rv, 0.9, 1e-5, training=True, relu=relu)
+
+
+def test_batch_norm_nchw_eval_and_bf16():
+    g = torch.Generator().manual_seed(10)
+    x = torch.randn(3, 5, 6, 6, generator=g)
+    sc, bi = torch.rand(5, generator=g) + 0.5, torch.randn(5, generator=g)
+    rm, rv = torch.randn(5, generator=g), torch.rand(5, generator=g) + 1
+    ref = F.batch_norm(x.double(), rm.double(), rv.double(), sc.double(), bi.double(), False, 0.0, 1e-5)
+    y, mo, vo, _, _ = C.batch_norm_nchw(x.to(DEV), sc.to(DEV), bi.to(DEV), rm.to(DEV), rv.to(DEV), training=False)
+    assert _rel(y, ref) < 1e-6
+    assert torch.equal(mo.cpu(), rm) and torch.equal(vo.cpu(), rv)
+    yb, _, _, _, _ = C.batch_norm_nchw(x.to(torch.bfloat16).to(DEV), sc.to(DEV), bi.to(DEV), rm.to(DEV), rv.to(DEV),
+                                       training=False)
+    assert yb.dtype == torch.bfloat16 and _rel(yb, ref) < 1e-2
+    # nn layer path (2.x convention: unbiased running variance, updated in place)
+    import paddle_amd as paddle
+
+    bn = paddle.nn.BatchNorm2D(5).to(DEV)
+    bn.train()
+    out = bn(x.to(DEV))
+    tr = torch.nn.BatchNorm2d(5, momentum=0.1, eps=1e-5).double()
+    with torch.no_grad():
+        tr.weight.copy_(bn.weight.double().cpu())
+        tr.bias.copy_(bn.bias.double().cpu())
+    ro = tr(x.double())
+    assert _rel(out, ro) < 1e-5
+    torch.testing.assert_close(bn._variance.double().cpu(), tr.running_var, rtol=1e-5, atol=1e-6)
