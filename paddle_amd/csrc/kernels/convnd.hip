@@ -51,13 +51,63 @@ struct SgemmArgs {
   long kbA, kbB;            // ... whose operands are offset by these strides
   float alpha, beta;
   int atomic;               // C += alpha * AB with float atomics (beta / bias ignored)
+  long ksplit;              // > 0: z1 indexes k-slices of this length (split-K, atomic)
 };
 
-constexpr int SBM = 128, SBN = 128, SBK = 16, SPAD = 4;
+constexpr int SBM = 128, SBN = 128, SBK = 32, SPAD = 4;
 
+// One k-tile of an operand, staged global -> registers -> LDS ([SBK][128 + SPAD],
+// k-major).  KF: the operand's k index is the contiguous one (A row-major / B
+// column-major); VEC: 16-B aligned float4 loads along the contiguous dimension.
+// Each of the 256 threads owns 16 elements = 4 float4.
+template <bool KF, bool VEC>
+struct TileLoader {
+  float r[16];
+  __device__ __forceinline__ void load(const float* __restrict__ P, long s_mn, long s_k, long mn0, long k0, long MN,
+                                       long K, int tid) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int q = v * 256 + tid;  // float4 slot within the 128 x 32 tile
+      int mn, kk;
+      if (KF) { mn = q >> 3; kk = (q & 7) * 4; } else { kk = q >> 5; mn = (q & 31) * 4; }
+      const long gm = mn0 + mn, gk = k0 + kk;
+      if (VEC) {
+        if (KF ? (gm < MN && gk + 3 < K) : (gk < K && gm + 3 < MN)) {
+          const f32x4 t = *reinterpret_cast<const f32x4*>(P + gm * s_mn + gk * s_k);
+          r[4 * v] = t[0]; r[4 * v + 1] = t[1]; r[4 * v + 2] = t[2]; r[4 * v + 3] = t[3];
+          continue;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long m = KF ? gm : gm + e, k = KF ? gk + e : gk;
+        r[4 * v + e] = (m < MN && k < K) ? P[m * s_mn + k * s_k] : 0.f;
+      }
+    }
+  }
+  __device__ __forceinline__ void store(float (*S)[SBM + SPAD], int tid) const {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int q = v * 256 + tid;
+      if (KF) {
+        const int mn = q >> 3, kk = (q & 7) * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) S[kk + e][mn] = r[4 * v + e];
+      } else {
+        const int kk = q >> 5, mn = (q & 31) * 4;
+        *reinterpret_cast<f32x4*>(&S[kk][mn]) = f32x4{r[4 * v], r[4 * v + 1], r[4 * v + 2], r[4 * v + 3]};
+      }
+    }
+  }
+};
+
+// 128 x 128 output tile, 4 waves of 64 x 64 (2 x 2 v_mfma_f32_32x32x2f32), k-tiles
+// of 32 double-buffered in LDS with the next tile's global loads issued before the
+// current tile's MFMAs (one barrier per k-tile).
+template <bool AK, bool BK_, bool VEC>
 __global__ __launch_bounds__(256) void sgemm_kernel(SgemmArgs g) {
-  __shared__ float As[SBK][SBM + SPAD];
-  __shared__ float Bs[SBK][SBN + SPAD];
+  __shared__ float As[2][SBK][SBM + SPAD];
+  __shared__ float Bs[2][SBK][SBN + SPAD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long z1 = blockIdx.z / g.Z2, z2 = blockIdx.z % g.Z2;
   const float* A0 = g.A + z1 * g.bsA1 + z2 * g.bsA2;
@@ -66,6 +116,13 @@ __global__ __launch_bounds__(256) void sgemm_kernel(SgemmArgs g) {
   const float* bias = g.bias_m ? g.bias_m + z2 * g.bsBias2 : nullptr;
   const long m0 = (long)blockIdx.y * SBM, n0 = (long)blockIdx.x * SBN;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  long K = g.K;
+  if (g.ksplit > 0) {  // split-K slice z1
+    const long kb0 = z1 * g.ksplit;
+    A0 += kb0 * g.sak;
+    B0 += kb0 * g.sbk;
+    K = min(g.ksplit, g.K - kb0);
+  }
   f32x16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -73,41 +130,40 @@ __global__ __launch_bounds__(256) void sgemm_kernel(SgemmArgs g) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  // loader orientation: walk the operand's contiguous dimension across lanes
-  const bool a_k_fast = g.sak == 1, b_n_fast = g.sbn == 1;
-  for (int b = 0; b < g.kb; ++b) {
-    const float* A = A0 + b * g.kbA;
-    const float* B = B0 + b * g.kbB;
-    for (long k0 = 0; k0 < g.K; k0 += SBK) {
-#pragma unroll
-      for (int e0 = 0; e0 < SBM * SBK; e0 += 256) {
-        const int e = e0 + tid;
-        int mm, kk;
-        if (a_k_fast) { mm = e / SBK; kk = e % SBK; } else { kk = e / SBM; mm = e % SBM; }
-        const long m = m0 + mm, k = k0 + kk;
-        As[kk][mm] = (m < g.M && k < g.K) ? A[m * g.sam + k * g.sak] : 0.f;
-      }
-#pragma unroll
-      for (int e0 = 0; e0 < SBN * SBK; e0 += 256) {
-        const int e = e0 + tid;
-        int nn, kk;
-        if (b_n_fast) { kk = e / SBN; nn = e % SBN; } else { nn = e / SBK; kk = e % SBK; }
-        const long n = n0 + nn, k = k0 + kk;
-        Bs[kk][nn] = (n < g.N && k < g.K) ? B[k * g.sbk + n * g.sbn] : 0.f;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int kk = 0; kk < SBK; kk += 2) {
-        const int k = kk + (lane >> 5);
-        const float a0 = As[k][wm + (lane & 31)], a1 = As[k][wm + 32 + (lane & 31)];
-        const float b0 = Bs[k][wn + (lane & 31)], b1 = Bs[k][wn + 32 + (lane & 31)];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-      }
-      __syncthreads();
+  TileLoader<AK, VEC> la;
+  TileLoader<BK_, VEC> lb;
+  const long ktiles = (K + SBK - 1) / SBK;
+  const long total = ktiles * g.kb;
+  // B(k, n) = B[k * sbk + n * sbn]: as an "MN x K" operand its mn stride is sbn
+  la.load(A0, g.sam, g.sak, m0, 0, g.M, K, tid);
+  lb.load(B0, g.sbn, g.sbk, n0, 0, g.N, K, tid);
+  la.store(As[0], tid);
+  lb.store(Bs[0], tid);
+  __syncthreads();
+  for (long t = 0; t < total; ++t) {
+    const int cur = (int)(t & 1);
+    const bool more = t + 1 < total;
+    if (more) {
+      const long tn = t + 1;
+      const long b = tn / ktiles, k0 = (tn % ktiles) * SBK;
+      la.load(A0 + b * g.kbA, g.sam, g.sak, m0, k0, g.M, K, tid);
+      lb.load(B0 + b * g.kbB, g.sbn, g.sbk, n0, k0, g.N, K, tid);
     }
+#pragma unroll
+    for (int kk = 0; kk < SBK; kk += 2) {
+      const int k = kk + (lane >> 5);
+      const float a0 = As[cur][k][wm + (lane & 31)], a1 = As[cur][k][wm + 32 + (lane & 31)];
+      const float b0 = Bs[cur][k][wn + (lane & 31)], b1 = Bs[cur][k][wn + 32 + (lane & 31)];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (more) {
+      la.store(As[cur ^ 1], tid);
+      lb.store(Bs[cur ^ 1], tid);
+    }
+    __syncthreads();
   }
   // 32x32 accumulator map: column = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
 #pragma unroll
@@ -482,8 +538,46 @@ PA_EXPORT int pa_sgemm(const float* A, long sam, long sak, const float* B, long 
   g.bsA1 = bsA1; g.bsB1 = bsB1; g.bsC1 = bsC1;
   g.bsA2 = bsA2; g.bsB2 = bsB2; g.bsC2 = bsC2;
   g.kb = kb; g.kbA = kbA; g.kbB = kbB;
-  g.alpha = alpha; g.beta = beta; g.atomic = atomic;
-  hipLaunchKernelGGL(sgemm_kernel, dim3((unsigned)gx, (unsigned)gy, (unsigned)(Z1 * Z2)), dim3(256), 0, st, g);
+  g.alpha = alpha; g.beta = beta; g.atomic = atomic; g.ksplit = 0;
+  // split-K for under-filled plain GEMMs (few output tiles, deep reduction): zero C,
+  // z1 = k-slice, float-atomic accumulation
+  const long tiles = gx * gy;
+  if (Z1 == 1 && Z2 == 1 && kb == 1 && !atomic && beta == 0.f && !bias_m && ldc == N && tiles < 192 && K >= 256) {
+    long splits = (384 + tiles - 1) / tiles;
+    if (splits > K / 128) splits = K / 128;
+    if (splits > 64) splits = 64;
+    if (splits >= 2) {
+      long ks = (K + splits - 1) / splits;
+      ks = (ks + SBK - 1) / SBK * SBK;
+      splits = (K + ks - 1) / ks;
+      if (hipMemsetAsync(C, 0, sizeof(float) * M * N, st) != hipSuccess) return (int)hipGetLastError();
+      g.ksplit = ks;
+      g.atomic = 1;
+      g.bsA1 = g.bsB1 = g.bsC1 = 0;
+      Z1 = (int)splits;
+    }
+  }
+  const dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)(Z1 * Z2));
+  g.Z2 = Z2;
+  const bool ak = sak == 1, bk = sbk == 1;
+  // float4 path: 16-B aligned bases and every non-contiguous stride a multiple of 4
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  auto m4 = [](long v) { return (v & 3) == 0; };
+  const bool vec = al(A) && al(B) && m4(ak ? sam : sak) && m4(bk ? sbn : sbk) && m4(bsA1) && m4(bsA2) && m4(bsB1) &&
+                   m4(bsB2) && m4(kbA) && m4(kbB) && (ak ? sak == 1 : sam == 1) && (bk ? sbk == 1 : sbn == 1);
+#define SG(AKv, BKv, V) hipLaunchKernelGGL((sgemm_kernel<AKv, BKv, V>), grid, dim3(256), 0, st, g)
+  if (vec) {
+    if (ak && bk) SG(true, true, true);
+    else if (ak) SG(true, false, true);
+    else if (bk) SG(false, true, true);
+    else SG(false, false, true);
+  } else {
+    if (ak && bk) SG(true, true, false);
+    else if (ak) SG(true, false, false);
+    else if (bk) SG(false, true, false);
+    else SG(false, false, false);
+  }
+#undef SG
   PA_LAUNCH_CHECK();
 }
 

@@ -17,6 +17,7 @@ import torch.nn.functional as F
 
 from ..framework import core
 from ..framework.registry import register_op
+from ..ops import blas as _blas
 from ..ops import oplib as _oplib
 
 # ------------------------------------------------------------------ mul / matmul
@@ -31,7 +32,8 @@ def mul(ctx):
     """Out = flatten(X, x_num_col_dims) @ flatten(Y, y_num_col_dims)."""
     x, y = ctx.input("X"), ctx.input("Y")
     xn, yn = ctx.attr("x_num_col_dims"), ctx.attr("y_num_col_dims")
-    out = _flat2(x, xn) @ _flat2(y, yn).to(x.dtype)
+    x2, y2 = _flat2(x, xn), _flat2(y, yn).to(x.dtype)
+    out = _blas.matmul(x2, y2) if _blas.supported(x2, y2) else x2 @ y2
     ctx.set_output("Out", out.reshape(tuple(x.shape[:xn]) + tuple(y.shape[yn:])))
 
 
@@ -46,7 +48,11 @@ def fc(ctx):
     x2 = _flat2(x, n)
     w = w.to(x2.dtype)
     act = ctx.attr("activation_type") or ""
-    if ctx.has_input("Bias"):
+    if ctx.has_input("Bias") and _blas.supported(x2, w):
+        out = _blas.fc(x2, w, ctx.input("Bias").reshape(-1).to(x2.dtype))
+    elif not ctx.has_input("Bias") and _blas.supported(x2, w):
+        out = _blas.matmul(x2, w)
+    elif ctx.has_input("Bias"):
         b = ctx.input("Bias").reshape(-1).to(x2.dtype)
         if act in ("relu", "gelu") and x2.is_cuda:
             out = torch._addmm_activation(b, x2, w, use_gelu=(act == "gelu"))
@@ -68,10 +74,12 @@ def mul_grad(ctx):
     xn, yn = ctx.attr("x_num_col_dims"), ctx.attr("y_num_col_dims")
     x2, y2 = _flat2(x, xn), _flat2(y, yn)
     d2 = dout.reshape(x2.shape[0], y2.shape[1])
+    mm = (lambda a, b: _blas.matmul(a, b)) if _blas.supported(x2, y2) and d2.dtype == x2.dtype else \
+        (lambda a, b: a @ b)
     if ctx.has_output("X@GRAD"):
-        ctx.set_output("X@GRAD", (d2 @ y2.t()).reshape(x.shape), ctx.input_lod("X"))
+        ctx.set_output("X@GRAD", mm(d2, y2.t()).reshape(x.shape), ctx.input_lod("X"))
     if ctx.has_output("Y@GRAD"):
-        ctx.set_output("Y@GRAD", (x2.t() @ d2).reshape(y.shape))
+        ctx.set_output("Y@GRAD", mm(x2.t(), d2).reshape(y.shape))
 
 
 @register_op("matmul", ["X", "Y"], ["Out"], {"transpose_X": False, "transpose_Y": False, "alpha": 1.0})
@@ -87,10 +95,13 @@ def matmul(ctx):
         x = x.transpose(-1, -2)
     if ty:
         y = y.transpose(-1, -2)
-    out = torch.matmul(x, y)
     a = ctx.attr("alpha")
-    if a != 1.0:
-        out = out * a
+    if _blas.supported(x, y):  # strided views: the transposes cost nothing
+        out = _blas.matmul(x, y, a)
+    else:
+        out = torch.matmul(x, y)
+        if a != 1.0:
+            out = out * a
     if x1:
         out = out.squeeze(-2)
     if y1:
@@ -437,6 +448,13 @@ def squared_l2_distance(ctx):
 @register_op("cos_sim", ["X", "Y"], ["Out", "XNorm~", "YNorm~"], {})
 def cos_sim(ctx):
     x, y = ctx.input("X"), ctx.input("Y")
+    from ..ops import nnmisc as _nm
+    r = _nm.cos_sim(x, y)
+    if r is not None:  # cos_sim kernels (nnmisc.hip)
+        ctx.set_output("Out", r[0])
+        ctx.set_output("XNorm", r[1])
+        ctx.set_output("YNorm", r[2])
+        return
     x2, y2 = x.reshape(x.shape[0], -1), y.reshape(y.shape[0], -1)
     xn = x2.norm(dim=1, keepdim=True)
     yn = y2.norm(dim=1, keepdim=True)

@@ -643,6 +643,11 @@ def bilinear_interp(ctx):
         if (oh <= 0 or ow <= 0) and ctx.attr("scale") > 0:
             oh, ow = int(x.shape[2] * ctx.attr("scale")), int(x.shape[3] * ctx.attr("scale"))
     mode = "bilinear" if ctx.attr("interp_method") == "bilinear" else "nearest"
+    from ..ops import nnmisc as _nm
+    r = _nm.interpolate(x, oh, ow, mode, ctx.attr("align_corners"))
+    if r is not None:  # interpolation kernels (nnmisc.hip)
+        ctx.set_output("Out", r)
+        return
     kw = {"align_corners": ctx.attr("align_corners")} if mode == "bilinear" else {}
     ctx.set_output("Out", F.interpolate(x, (oh, ow), mode=mode, **kw))
 
@@ -797,6 +802,11 @@ def row_conv(ctx):
 @register_op("conv_shift", ["X", "Y"], ["Out"], {})
 def conv_shift(ctx):
     x, y = ctx.input("X"), ctx.input("Y")
+    from ..ops import nnmisc as _nm
+    r = _nm.conv_shift(x, y)
+    if r is not None:  # conv_shift kernels (nnmisc.hip)
+        ctx.set_output("Out", r)
+        return
     M, N = x.shape[1], y.shape[1]
     half = (N - 1) // 2
     idx = (torch.arange(M, device=x.device)[:, None] + torch.arange(N, device=x.device)[None, :] - half) % M

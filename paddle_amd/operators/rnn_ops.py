@@ -257,6 +257,12 @@ def gru_unit(ctx):
 def lstm_unit(ctx):
     """Gate order {i, f, o, g} (lstm_unit_op.h:63-71); forget_bias added before the sigmoid."""
     x, cp = ctx.input("X"), ctx.input("C_prev")
+    from ..ops import nnmisc as _nm
+    r = _nm.lstm_unit(x, cp, ctx.attr("forget_bias"))
+    if r is not None:  # lstm_unit kernels (nnmisc.hip)
+        ctx.set_output("C", r[0])
+        ctx.set_output("H", r[1])
+        return
     D = cp.shape[1]
     i, f, o, g = x.split(D, dim=1)
     c = torch.sigmoid(f + ctx.attr("forget_bias")) * cp + torch.sigmoid(i) * torch.tanh(g)

@@ -324,3 +324,51 @@ def test_batch_norm_nchw_eval_and_bf16():
     ro = tr(x.double())
     assert _rel(out, ro) < 1e-5
     torch.testing.assert_close(bn._variance.double().cpu(), tr.running_var, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("shape", [((33, 70), (70, 129)), ((4, 17, 40), (40, 9)), ((3, 8, 16), (3, 16, 24)),
+                                   ((128, 512), (512, 2048))])
+@pytest.mark.parametrize("trans", [False, True])
+def test_fluid_blas_matmul_fwd_bwd(shape, trans):
+    from paddle_amd.ops import blas
+
+    sa, sb = shape
+    g = torch.Generator().manual_seed(11)
+    a = torch.randn(*sa, generator=g, dtype=torch.float64)
+    b = torch.randn(*sb, generator=g, dtype=torch.float64)
+    ar, br = a.clone().requires_grad_(), b.clone().requires_grad_()
+    ref = 0.5 * (ar @ br)
+    ad = a.float().to(DEV)
+    bd = b.float().to(DEV)
+    if trans:  # operands handed over as transposed strided views
+        ad = ad.transpose(-1, -2).contiguous().transpose(-1, -2)
+        bd = bd.transpose(-1, -2).contiguous().transpose(-1, -2)
+    ad.requires_grad_()
+    bd.requires_grad_()
+    assert blas.supported(ad, bd)
+    y = blas.matmul(ad, bd, 0.5)
+    assert _rel(y, ref) < 1e-6
+    gy = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    ref.backward(gy)
+    y.backward(gy.float().to(DEV))
+    assert _rel(ad.grad, ar.grad) < 1e-6
+    assert _rel(bd.grad, br.grad) < 1e-6
+
+
+def test_fluid_blas_fc():
+    from paddle_amd.ops import blas
+
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(37, 50, generator=g, dtype=torch.float64)
+    w = torch.randn(50, 21, generator=g, dtype=torch.float64)
+    b = torch.randn(21, generator=g, dtype=torch.float64)
+    xr, wr, br = (t.clone().requires_grad_() for t in (x, w, b))
+    ref = xr @ wr + br
+    xd, wd, bd = (t.float().to(DEV).requires_grad_() for t in (x, w, b))
+    y = blas.fc(xd, wd, bd)
+    assert _rel(y, ref) < 1e-6
+    gy = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    ref.backward(gy)
+    y.backward(gy.float().to(DEV))
+    for d_, r_ in ((xd, xr), (wd, wr), (bd, br)):
+        assert _rel(d_.grad, r_.grad) < 1e-6
