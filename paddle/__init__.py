@@ -12,6 +12,7 @@ from paddle_amd import fluid  # noqa: F401
 from paddle_amd import reader  # noqa: F401
 from paddle_amd import dataset  # noqa: F401
 from paddle_amd import dygraph  # noqa: F401
+from paddle_amd import v2  # noqa: F401
 from paddle_amd.reader import batch  # noqa: F401
 from paddle_amd.checkpoint import load, save  # noqa: F401
 from paddle_amd.hapi import Model  # noqa: F401
@@ -24,12 +25,13 @@ static = fluid
 __version__ = _pa.__version__
 for _name, _mod in (("fluid", fluid), ("reader", reader), ("dataset", dataset), ("nn", nn),
                     ("optimizer", optimizer), ("io", io), ("amp", amp), ("metric", metric), ("vision", vision),
-                    ("distributed", distributed), ("static", fluid), ("dygraph", dygraph)):
+                    ("distributed", distributed), ("static", fluid), ("dygraph", dygraph),
+                    ("v2", v2)):
     _sys.modules[__name__ + "." + _name] = _mod
 for _k, _v in list(_sys.modules.items()):
     for _src, _dst in (("paddle_amd.fluid.", "paddle.fluid."), ("paddle_amd.nn.", "paddle.nn."),
                        ("paddle_amd.distributed.", "paddle.distributed."), ("paddle_amd.optimizer.",
                                                                             "paddle.optimizer."),
-                       ("paddle_amd.vision.", "paddle.vision.")):
+                       ("paddle_amd.vision.", "paddle.vision."), ("paddle_amd.v2.", "paddle.v2.")):
         if _k.startswith(_src):
             _sys.modules[_dst + _k[len(_src):]] = _v

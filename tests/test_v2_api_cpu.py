@@ -1,0 +1,100 @@
+"""paddle.v2 facade (paddle_amd/v2): the v2 book-style flow -- init, data layers,
+fc / img_conv / embedding + sequence pooling, classification_cost with its
+evaluator, parameters.create, trainer.SGD.train with events, test, infer, and the
+v2 parameter tar format round trip (reference v2/trainer.py, parameters.py)."""
+import io
+
+import numpy as np
+
+import paddle.v2 as paddle
+
+
+def _reader(n=256, dim=16, classes=4, seed=0):
+    rs = np.random.RandomState(seed)
+    w = rs.randn(dim, classes)
+
+    def r():
+        x = rs.randn(n, dim).astype("float32")
+        y = (x @ w).argmax(1)
+        for i in range(0, n, 32):
+            yield [(x[j], int(y[j])) for j in range(i, i + 32)]
+    return r
+
+
+def test_v2_softmax_regression_trains_and_roundtrips():
+    paddle.init(use_gpu=False, trainer_count=1)
+    img = paddle.layer.data(name="pixel", type=paddle.data_type.dense_vector(16))
+    lbl = paddle.layer.data(name="label", type=paddle.data_type.integer_value(4))
+    hidden = paddle.layer.fc(input=img, size=32, act=paddle.activation.Relu())
+    pred = paddle.layer.fc(input=hidden, size=4, act=paddle.activation.Softmax())
+    cost = paddle.layer.classification_cost(input=pred, label=lbl)
+    params = paddle.parameters.create(cost)
+    assert len(params.keys()) == 4
+    opt = paddle.optimizer.Momentum(momentum=0.9, learning_rate=0.05,
+                                    regularization=paddle.optimizer.L2Regularization(rate=1e-4))
+    trainer = paddle.trainer.SGD(cost=cost, parameters=params, update_equation=opt)
+    events, costs, passes = [], [], []
+
+    def handler(e):
+        events.append(type(e).__name__)
+        if isinstance(e, paddle.event.EndIteration):
+            costs.append(e.cost)
+            assert "classification_error_evaluator" in e.metrics
+        if isinstance(e, paddle.event.EndPass):
+            passes.append(e.metrics["classification_error_evaluator"])
+
+    reader = _reader()
+    trainer.train(reader=reader, num_passes=6, event_handler=handler, feeding={"pixel": 0, "label": 1})
+    assert events[0] == "BeginPass" and events[1] == "BeginIteration" and events[-1] == "EndPass"
+    assert np.mean(costs[-8:]) < 0.6 * np.mean(costs[:8])
+    assert passes[-1] < passes[0]
+    res = trainer.test(reader=reader, feeding={"pixel": 0, "label": 1})
+    assert res.metrics["classification_error_evaluator"] < 0.3 and res.cost > 0
+    # inference on the trained parameters
+    samples = [(np.random.RandomState(5).randn(16).astype("float32"),) for _ in range(6)]
+    probs = paddle.infer(output_layer=pred, parameters=params, input=samples, feeding={"pixel": 0})
+    assert probs.shape == (6, 4)
+    np.testing.assert_allclose(probs.sum(1), 1.0, rtol=1e-5)
+    # v2 tar format round trip
+    buf = io.BytesIO()
+    trainer.save_parameter_to_tar(buf)
+    buf.seek(0)
+    loaded = paddle.parameters.Parameters.from_tar(buf)
+    for k in params.keys():
+        np.testing.assert_array_equal(loaded[k], params[k])
+    raw = buf.getvalue()
+    assert raw.count(b".protobuf") == 4
+    # perturb, then restore from the tar
+    k0 = params.keys()[0]
+    params[k0] = np.zeros(params.get_shape(k0), "float32")
+    buf.seek(0)
+    params.init_from_tar(buf)
+    np.testing.assert_array_equal(params[k0], loaded[k0])
+
+
+def test_v2_sequence_model_with_embedding_and_pooling():
+    paddle.init(use_gpu=False)
+    words = paddle.layer.data(name="words", type=paddle.data_type.integer_value_sequence(50))
+    lbl = paddle.layer.data(name="label", type=paddle.data_type.integer_value(2))
+    emb = paddle.layer.embedding(input=words, size=8)
+    pooled = paddle.layer.pooling(input=emb, pooling_type=paddle.pooling.Avg())
+    pred = paddle.layer.fc(input=pooled, size=2, act=paddle.activation.Softmax())
+    cost = paddle.layer.classification_cost(input=pred, label=lbl)
+    params = paddle.parameters.create(cost)
+    trainer = paddle.trainer.SGD(cost=cost, parameters=params,
+                                 update_equation=paddle.optimizer.Adam(learning_rate=0.05))
+    rs = np.random.RandomState(1)
+
+    def reader():
+        for _ in range(8):
+            batch = []
+            for _ in range(16):
+                y = int(rs.randint(2))
+                seq = list(rs.randint(0, 25, rs.randint(2, 6)) + 25 * y)
+                batch.append((seq, y))
+            yield batch
+
+    costs = []
+    trainer.train(reader=reader, num_passes=4,
+                  event_handler=lambda e: costs.append(e.cost) if isinstance(e, paddle.event.EndIteration) else None)
+    assert np.mean(costs[-4:]) < np.mean(costs[:4])
