@@ -99,7 +99,22 @@ def out_size(i, k, s, p, d):
 # ------------------------------------------------------------------ convolution
 
 
-def _conv_fwd(x, w, b, s, p, d, G):
+def _pointwise(k, s, p):
+    """1x1(x1) kernel, stride 1, no padding: the column matrix of an image IS the
+    image ([C][S]), so vol2col / col2vol are skipped (most ResNet bottleneck convs)."""
+    return all(v == 1 for v in k) and all(v == 1 for v in s) and all(v == 0 for v in p)
+
+
+def _pw_geo(geo):
+    """geo = (C, D, H, W, OD, OH, OW, kd, kh, kw, sd, sh, sw, pd, ph, pw, dd, dh, dw)."""
+    v = list(geo)
+    return v[7:10] == [1, 1, 1] and v[10:13] == [1, 1, 1] and v[13:16] == [0, 0, 0]
+
+
+_COL_KEEP = int(os.environ.get("PADDLE_AMD_CONV_COL_CACHE_MB", "4096")) << 20  # bytes per conv
+
+
+def _conv_fwd(x, w, b, s, p, d, G, keep=None):
     Nn, C = x.shape[0], x.shape[1]
     sp = tuple(x.shape[2:])
     nd = len(sp)
@@ -117,12 +132,22 @@ def _conv_fwd(x, w, b, s, p, d, G):
     geo = _geo(C, _pad3(sp), _pad3(osp), _pad3(k), _pad3(s), _pad3z(p), _pad3(d))
     y = torch.empty((Nn, Cout) + osp, dtype=torch.float32, device=x.device)
     wc = w.contiguous()
+    if _pointwise(k, s, p):
+        if Nn * G > 65535:
+            raise ValueError("conv: batch x groups too large")
+        sgemm(wc, CgK, 1, x, S, 1, y, S, Coutg, S, CgK, Z1=Nn, Z2=G,
+              bs1=(0, C * S, Cout * S), bs2=(Coutg * CgK, CgK * S, Coutg * S), bias=b, bs_bias2=Coutg)
+        return y, geo, osp
     nb = _chunk(Nn, C * KT * S, G)
     for n0 in range(0, Nn, nb):
         m = min(nb, Nn - n0)
         col = _vol2col(x[n0:n0 + m], m, geo, C * KT, S)
         sgemm(wc, CgK, 1, col, S, 1, y[n0:n0 + m], S, Coutg, S, CgK, Z1=m, Z2=G,
               bs1=(0, C * KT * S, Cout * S), bs2=(Coutg * CgK, CgK * S, Coutg * S), bias=b, bs_bias2=Coutg)
+        if keep is not None:
+            keep.append(col)
+    if keep is not None and sum(c.numel() * 4 for c in keep) > _COL_KEEP:
+        keep.clear()
     return y, geo, osp
 
 
@@ -134,6 +159,10 @@ def _conv_dgrad(dy, w, x_shape, geo, G):
     Cg, Coutg = C // G, Cout // G
     CgK = Cg * KT
     dx = torch.empty(x_shape, dtype=torch.float32, device=dy.device)
+    if KT == 1 and _pw_geo(geo):  # pointwise: W^T dY lands in dx directly
+        sgemm(w, 1, CgK, dy, S, 1, dx, S, CgK, S, Coutg, Z1=Nn, Z2=G,
+              bs1=(0, Cout * S, C * S), bs2=(Coutg * CgK, Coutg * S, CgK * S))
+        return dx
     nb = _chunk(Nn, C * KT * S, G)
     for n0 in range(0, Nn, nb):
         m = min(nb, Nn - n0)
@@ -144,7 +173,7 @@ def _conv_dgrad(dy, w, x_shape, geo, G):
     return dx
 
 
-def _conv_wgrad(dy, x, w_shape, geo, G):
+def _conv_wgrad(dy, x, w_shape, geo, G, cols=None):
     Nn, C = x.shape[0], x.shape[1]
     Cout = w_shape[0]
     KT = 1
@@ -155,9 +184,15 @@ def _conv_wgrad(dy, x, w_shape, geo, G):
     CgK = Cg * KT
     dw = torch.zeros(w_shape, dtype=torch.float32, device=dy.device)
     nb = _chunk(Nn, C * KT * S, G)
-    for n0 in range(0, Nn, nb):
+    pw = KT == 1 and _pw_geo(geo)
+    for ci, n0 in enumerate(range(0, Nn, nb)):
         m = min(nb, Nn - n0)
-        col = _vol2col(x[n0:n0 + m], m, geo, C * KT, S)
+        if pw:
+            col = x[n0:n0 + m]
+        elif cols:  # the forward's column chunks (same chunking)
+            col = cols[ci]
+        else:
+            col = _vol2col(x[n0:n0 + m], m, geo, C * KT, S)
         # dW[g] += sum_img dY[img][g] col[img][g]^T  (one split per image, float atomics)
         sgemm(dy[n0:n0 + m], S, 1, col, 1, S, dw, CgK, Coutg, CgK, S, Z1=m, Z2=G,
               bs1=(Cout * S, C * KT * S, 0), bs2=(Coutg * S, CgK * S, Coutg * CgK), atomic=True)
@@ -178,8 +213,10 @@ class _ConvNdFn(torch.autograd.Function):
         dt = x.dtype
         xf, wf = x.float().contiguous(), w.float().contiguous()
         bf = b.float().contiguous() if b is not None else None
-        y, geo, _ = _conv_fwd(xf, wf, bf, s, p, d, G)
+        keep = [] if ctx.needs_input_grad[1] else None  # column chunks reused by the wgrad
+        y, geo, _ = _conv_fwd(xf, wf, bf, s, p, d, G, keep)
         ctx.save_for_backward(xf, wf)
+        ctx.cols = keep
         ctx.conf = (geo, G, dt, w.dtype, b is not None)
         return y.to(dt)
 
@@ -189,7 +226,8 @@ class _ConvNdFn(torch.autograd.Function):
         geo, G, dt, wdt, has_b = ctx.conf
         dyf = dy.float().contiguous()
         dx = _conv_dgrad(dyf, wf, tuple(xf.shape), geo, G).to(dt) if ctx.needs_input_grad[0] else None
-        dw = _conv_wgrad(dyf, xf, tuple(wf.shape), geo, G).to(wdt) if ctx.needs_input_grad[1] else None
+        dw = _conv_wgrad(dyf, xf, tuple(wf.shape), geo, G, ctx.cols).to(wdt) if ctx.needs_input_grad[1] else None
+        ctx.cols = None
         db = _bias_grad(dyf).to(wdt) if has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db, None, None, None, None
 

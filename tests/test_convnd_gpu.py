@@ -51,6 +51,8 @@ CONV2D = [
     (2, 16, 8, 8, 16, (3, 3), (1, 1), (1, 1), (1, 1), 16, True),   # depthwise
     (1, 64, 14, 14, 128, (1, 1), (2, 2), (0, 0), (1, 1), 1, False),
     (4, 5, 6, 13, 7, (5, 5), (3, 2), (2, 2), (1, 1), 1, True),
+    (3, 8, 5, 7, 12, (1, 1), (1, 1), (0, 0), (1, 1), 2, True),     # pointwise: no vol2col
+    (2, 16, 9, 9, 32, (1, 1), (1, 1), (0, 0), (1, 1), 1, False),
 ]
 
 
