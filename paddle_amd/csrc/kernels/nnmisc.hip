@@ -223,7 +223,73 @@ __global__ void lstm_unit_bwd_kernel(const T* __restrict__ x, const T* __restric
   }
 }
 
+
+// ---------------------------------------------------------------- cross_entropy on probabilities
+// hard labels: y = -log(x[label]) (0 for ignore_index); soft: y = -sum lab * log(x)
+// (math/cross_entropy.cu CrossEntropyKernel / SoftCrossEntropyKernel); one wave per row
+template <typename T>
+__global__ __launch_bounds__(256) void xent_fwd_kernel(const T* __restrict__ x, const long* __restrict__ label,
+                                                       const T* __restrict__ soft, T* __restrict__ y, long rows, int D,
+                                                       long ignore) {
+  const int lane = threadIdx.x & 63;
+  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  if (!soft) {
+    if (lane == 0) {
+      const long l = label[r];
+      float v = 0.f;
+      if (l != ignore && l >= 0 && l < D) v = -logf(IO<T>::ld(x, r * D + l));
+      IO<T>::st(y, r, v);
+    }
+    return;
+  }
+  float acc = 0.f;
+  for (int d = lane; d < D; d += 64) acc -= IO<T>::ld(soft, r * D + d) * logf(IO<T>::ld(x, r * D + d));
+  acc = wave_sum(acc);
+  if (lane == 0) IO<T>::st(y, r, acc);
+}
+
+template <typename T>
+__global__ void xent_bwd_kernel(const T* __restrict__ x, const long* __restrict__ label, const T* __restrict__ soft,
+                                const T* __restrict__ dy, T* __restrict__ dx, long rows, int D, long ignore) {
+  GRID_STRIDE(i, rows * D) {
+    const long r = i / D;
+    const int d = (int)(i % D);
+    const float g = IO<T>::ld(dy, r);
+    float v;
+    if (soft) {
+      v = -g * IO<T>::ld(soft, i) / IO<T>::ld(x, i);
+    } else {
+      const long l = label[r];
+      v = (l == d && l != ignore) ? -g / IO<T>::ld(x, i) : 0.f;
+    }
+    IO<T>::st(dx, i, v);
+  }
+}
+
 }  // namespace
+
+PA_EXPORT int pa_cross_entropy(int dt, int backward, const void* x, const long* label, const void* soft,
+                               const void* dy, void* out, long rows, int D, long ignore, hipStream_t st) {
+  if (rows <= 0 || D <= 0) return 0;
+  if (!backward) {
+    const dim3 g((unsigned)((rows + 3) / 4));
+    if (dt == 1)
+      hipLaunchKernelGGL(xent_fwd_kernel<u16>, g, dim3(256), 0, st, (const u16*)x, label, (const u16*)soft, (u16*)out,
+                         rows, D, ignore);
+    else
+      hipLaunchKernelGGL(xent_fwd_kernel<float>, g, dim3(256), 0, st, (const float*)x, label, (const float*)soft,
+                         (float*)out, rows, D, ignore);
+  } else {
+    if (dt == 1)
+      hipLaunchKernelGGL(xent_bwd_kernel<u16>, dim3(grid_for(rows * D)), dim3(256), 0, st, (const u16*)x, label,
+                         (const u16*)soft, (const u16*)dy, (u16*)out, rows, D, ignore);
+    else
+      hipLaunchKernelGGL(xent_bwd_kernel<float>, dim3(grid_for(rows * D)), dim3(256), 0, st, (const float*)x, label,
+                         (const float*)soft, (const float*)dy, (float*)out, rows, D, ignore);
+  }
+  PA_LAUNCH_CHECK();
+}
 
 PA_EXPORT int pa_cos_sim(int dt, const void* x, const void* y, void* out, float* xn, float* yn, long rows, int D,
                          int y_rows, hipStream_t st) {

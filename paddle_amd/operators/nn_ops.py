@@ -387,6 +387,11 @@ def _gather_label(p, label):
 def cross_entropy(ctx):
     """-log(X[label]) with X a probability distribution (cross_entropy_op.h)."""
     x, lab = ctx.input("X"), ctx.input("Label")
+    from ..ops import nnmisc as _nm
+    r = _nm.cross_entropy(x, lab, ctx.attr("soft_label"), ctx.attr("ignore_index"))
+    if r is not None:  # math/cross_entropy.cu counterpart (nnmisc.hip)
+        ctx.set_output("Y", r)
+        return
     if ctx.attr("soft_label"):
         y = -(lab * torch.log(x)).sum(-1, keepdim=True)
     else:

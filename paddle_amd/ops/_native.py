@@ -162,6 +162,7 @@ _SIGS = {
     "pa_bn_nchw_groups": [_I, _L],
     "pa_bn_nchw_fwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _L, _F, _F, _I, _I, _I, _P],
     "pa_bn_nchw_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _L, _I, _P],
+    "pa_cross_entropy": [_I, _I, _P, _P, _P, _P, _P, _L, _I, _L, _P],
     "pa_cos_sim": [_I, _P, _P, _P, _P, _P, _L, _I, _I, _P],
     "pa_cos_sim_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _P],
     "pa_interp": [_I, _I, _P, _P, _L, _I, _I, _I, _I, _I, _I, _P],

@@ -153,3 +153,40 @@ def lstm_unit(x, c_prev, forget_bias=0.0):
     if x.shape[1] != 4 * c_prev.shape[1] or x.shape[0] != c_prev.shape[0]:
         return None
     return _tape.apply(_LstmUnitFn, x, c_prev, forget_bias)
+
+
+class _XentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, label, soft, ignore):
+        x2 = x.reshape(-1, x.shape[-1]).contiguous()
+        rows, D = x2.shape
+        y = torch.empty(rows, 1, dtype=x.dtype, device=x.device)
+        lab = label.reshape(-1).to(torch.int64).contiguous() if not soft else None
+        sl = label.reshape(rows, D).to(x.dtype).contiguous() if soft else None
+        N.call("pa_cross_entropy", _DT[x.dtype], 0, N.ptr(x2), N.ptr(lab), N.ptr(sl), None, N.ptr(y), rows, D,
+               int(ignore), N.stream())
+        ctx.save_for_backward(x2, lab if lab is not None else sl)
+        ctx.conf = (soft, int(ignore), tuple(x.shape))
+        return y.reshape(tuple(x.shape[:-1]) + (1,))
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, lab = ctx.saved_tensors
+        soft, ignore, shape = ctx.conf
+        rows, D = x2.shape
+        d = dy.reshape(rows).contiguous().to(x2.dtype)
+        dx = torch.empty_like(x2)
+        N.call("pa_cross_entropy", _DT[x2.dtype], 1, N.ptr(x2), None if soft else N.ptr(lab),
+               N.ptr(lab) if soft else None, N.ptr(d), N.ptr(dx), rows, D, ignore, N.stream())
+        return dx.reshape(shape), None, None, None
+
+
+def cross_entropy(x, label, soft_label=False, ignore_index=-100):
+    """-log(x[label]) / -sum(label * log x) over the last axis of a probability tensor, or None."""
+    if not _ok(x) or not label.is_cuda or x.dim() < 1 or x.shape[-1] == 0:
+        return None
+    if soft_label and label.shape != x.shape:
+        return None
+    if not soft_label and label.numel() != x.numel() // x.shape[-1]:
+        return None
+    return _tape.apply(_XentFn, x, label, bool(soft_label), int(ignore_index))

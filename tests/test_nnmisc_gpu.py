@@ -90,3 +90,28 @@ def test_lstm_unit(fb):
     (c2 * gc.float().to(DEV) + h2 * gh.float().to(DEV)).sum().backward()
     assert _rel(xd.grad, xr.grad) < 1e-5
     assert _rel(cd.grad, cr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("soft", [False, True])
+def test_cross_entropy_on_probabilities(soft):
+    g = torch.Generator().manual_seed(4)
+    p = torch.softmax(torch.randn(9, 7, generator=g, dtype=torch.float64), -1)
+    if soft:
+        lab = torch.softmax(torch.randn(9, 7, generator=g, dtype=torch.float64), -1)
+        pr = p.clone().requires_grad_()
+        ref = -(lab * torch.log(pr)).sum(-1, keepdim=True)
+        labd = lab.float().to(DEV)
+    else:
+        lab = torch.randint(0, 7, (9, 1), generator=g)
+        lab[3, 0] = -100  # ignored row
+        pr = p.clone().requires_grad_()
+        safe = lab.clamp_min(0)
+        ref = torch.where(lab == -100, torch.zeros(9, 1, dtype=torch.float64), -torch.log(pr.gather(1, safe)))
+        labd = lab.to(DEV)
+    pd = p.float().to(DEV).requires_grad_()
+    y = nnmisc.cross_entropy(pd, labd, soft, -100)
+    assert _rel(y, ref) < 1e-6
+    gy = torch.randn(9, 1, generator=g, dtype=torch.float64)
+    ref.backward(gy)
+    y.backward(gy.float().to(DEV))
+    assert _rel(pd.grad, pr.grad) < 1e-6
