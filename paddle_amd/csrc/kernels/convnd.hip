@@ -51,7 +51,9 @@ struct SgemmArgs {
   long kbA, kbB;            // ... whose operands are offset by these strides
   float alpha, beta;
   int atomic;               // C += alpha * AB with float atomics (beta / bias ignored)
-  long ksplit;              // > 0: z1 indexes k-slices of this length (split-K, atomic)
+  long ksplit;              // > 0: k-slices of this length (split-K, atomic)
+  int kbsplit;              // > 0: k-batch ranges of this many members (split over the k-batch, atomic)
+  int nks;                  // split mode: z1 = kbatch_slice * nks + k_slice
 };
 
 constexpr int SBM = 128, SBN = 128, SBK = 32, SPAD = 4;
@@ -117,11 +119,19 @@ __global__ __launch_bounds__(256) void sgemm_kernel(SgemmArgs g) {
   const long m0 = (long)blockIdx.y * SBM, n0 = (long)blockIdx.x * SBN;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
   long K = g.K;
-  if (g.ksplit > 0) {  // split-K slice z1
-    const long kb0 = z1 * g.ksplit;
-    A0 += kb0 * g.sak;
-    B0 += kb0 * g.sbk;
-    K = min(g.ksplit, g.K - kb0);
+  int b_lo = 0, b_hi = g.kb;
+  if (g.ksplit > 0 || g.kbsplit > 0) {  // split mode: z1 -> (k-batch slice, k slice)
+    const long zk = z1 % g.nks, zb = z1 / g.nks;
+    if (g.ksplit > 0) {
+      const long kb0 = zk * g.ksplit;
+      A0 += kb0 * g.sak;
+      B0 += kb0 * g.sbk;
+      K = min(g.ksplit, g.K - kb0);
+    }
+    if (g.kbsplit > 0) {
+      b_lo = (int)(zb * g.kbsplit);
+      b_hi = min(g.kb, b_lo + g.kbsplit);
+    }
   }
   f32x16 acc[2][2];
 #pragma unroll
@@ -133,7 +143,10 @@ __global__ __launch_bounds__(256) void sgemm_kernel(SgemmArgs g) {
   TileLoader<AK, VEC> la;
   TileLoader<BK_, VEC> lb;
   const long ktiles = (K + SBK - 1) / SBK;
-  const long total = ktiles * g.kb;
+  const long total = ktiles * (b_hi - b_lo);
+  if (total <= 0) return;  // empty split slice (uniform per workgroup: no barrier skipped by part of it)
+  A0 += b_lo * g.kbA;
+  B0 += b_lo * g.kbB;
   // B(k, n) = B[k * sbk + n * sbn]: as an "MN x K" operand its mn stride is sbn
   la.load(A0, g.sam, g.sak, m0, 0, g.M, K, tid);
   lb.load(B0, g.sbn, g.sbk, n0, 0, g.N, K, tid);
@@ -539,22 +552,40 @@ PA_EXPORT int pa_sgemm(const float* A, long sam, long sak, const float* B, long 
   g.bsA2 = bsA2; g.bsB2 = bsB2; g.bsC2 = bsC2;
   g.kb = kb; g.kbA = kbA; g.kbB = kbB;
   g.alpha = alpha; g.beta = beta; g.atomic = atomic; g.ksplit = 0;
-  // split-K for under-filled plain GEMMs (few output tiles, deep reduction): zero C,
-  // z1 = k-slice, float-atomic accumulation
-  const long tiles = gx * gy;
-  if (Z1 == 1 && Z2 == 1 && kb == 1 && !atomic && beta == 0.f && !bias_m && ldc == N && tiles < 192 && K >= 256) {
-    long splits = (384 + tiles - 1) / tiles;
-    if (splits > K / 128) splits = K / 128;
-    if (splits > 64) splits = 64;
-    if (splits >= 2) {
-      long ks = (K + splits - 1) / splits;
+  g.kbsplit = 0;
+  g.nks = 1;
+  // split for under-filled problems (few output tiles, deep reduction): the k-batch
+  // and / or K are cut into slices on z1, accumulated with float atomics (C zeroed
+  // here unless the caller already accumulates atomically)
+  const long tiles = gx * gy * Z2;
+  const bool can_zero = beta == 0.f && !bias_m && ldc == N && Z2 == 1;
+  if (Z1 == 1 && tiles < 192 && (kb > 1 || K >= 256) && (atomic || can_zero)) {
+    const long target = (384 + tiles - 1) / tiles;
+    long nb = 1, kbs = kb;
+    if (kb > 1) {
+      nb = target < kb ? target : kb;
+      kbs = (kb + nb - 1) / nb;
+      nb = (kb + kbs - 1) / kbs;
+    }
+    long nk = 1, ks = K;
+    const long rem = (target + nb - 1) / nb;
+    if (rem >= 2 && K >= 256) {
+      nk = rem;
+      if (nk > K / 128) nk = K / 128;
+      if (nk > 64) nk = 64;
+      if (nk < 1) nk = 1;
+      ks = (K + nk - 1) / nk;
       ks = (ks + SBK - 1) / SBK * SBK;
-      splits = (K + ks - 1) / ks;
-      if (hipMemsetAsync(C, 0, sizeof(float) * M * N, st) != hipSuccess) return (int)hipGetLastError();
-      g.ksplit = ks;
+      nk = (K + ks - 1) / ks;
+    }
+    if (nb * nk >= 2 && nb * nk * Z2 <= 65535) {
+      if (!atomic && hipMemsetAsync(C, 0, sizeof(float) * M * N, st) != hipSuccess) return (int)hipGetLastError();
       g.atomic = 1;
+      g.ksplit = nk > 1 ? ks : 0;
+      g.kbsplit = nb > 1 ? (int)kbs : 0;
+      g.nks = (int)nk;
       g.bsA1 = g.bsB1 = g.bsC1 = 0;
-      Z1 = (int)splits;
+      Z1 = (int)(nb * nk);
     }
   }
   const dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)(Z1 * Z2));

@@ -193,9 +193,11 @@ def _conv_wgrad(dy, x, w_shape, geo, G, cols=None):
             col = cols[ci]
         else:
             col = _vol2col(x[n0:n0 + m], m, geo, C * KT, S)
-        # dW[g] += sum_img dY[img][g] col[img][g]^T  (one split per image, float atomics)
-        sgemm(dy[n0:n0 + m], S, 1, col, 1, S, dw, CgK, Coutg, CgK, S, Z1=m, Z2=G,
-              bs1=(Cout * S, C * KT * S, 0), bs2=(Coutg * S, CgK * S, Coutg * CgK), atomic=True)
+        # dW[g] += sum_img dY[img][g] col[img][g]^T  (float atomics across chunks / splits)
+        # (images on the kernel's k-batch; the launcher splits k-batch / K over
+        # workgroups when the dW grid is small)
+        sgemm(dy[n0:n0 + m], S, 1, col, 1, S, dw, CgK, Coutg, CgK, S, Z1=1, Z2=G,
+              bs2=(Coutg * S, CgK * S, Coutg * CgK), kb=m, kbA=Cout * S, kbB=C * KT * S, atomic=True)
     return dw
 
 
@@ -299,8 +301,8 @@ class _ConvTNdFn(torch.autograd.Function):
                 sgemm(wf, CoKT, 1, col, S, 1, dx[n0:n0 + m], S, Cing, S, CoKT, Z1=m, Z2=G,
                       bs1=(0, Cout * KT * S, Cin * S), bs2=(Cing * CoKT, CoKT * S, Cing * S))
             if dw is not None:  # dW[g] += x[img][g] col(dY)[img][g]^T
-                sgemm(xf[n0:n0 + m], S, 1, col, 1, S, dw, CoKT, Cing, CoKT, S, Z1=m, Z2=G,
-                      bs1=(Cin * S, Cout * KT * S, 0), bs2=(Cing * S, CoKT * S, Cing * CoKT), atomic=True)
+                sgemm(xf[n0:n0 + m], S, 1, col, 1, S, dw, CoKT, Cing, CoKT, S, Z1=1, Z2=G,
+                      bs2=(Cing * S, CoKT * S, Cing * CoKT), kb=m, kbA=Cin * S, kbB=Cout * KT * S, atomic=True)
         return (dx.to(dt) if dx is not None else None, dw.to(wdt) if dw is not None else None,
                 None, None, None, None, None)
 
