@@ -67,18 +67,29 @@ struct TileLoader {
   float r[16];
   __device__ __forceinline__ void load(const float* __restrict__ P, long s_mn, long s_k, long mn0, long k0, long MN,
                                        long K, int tid) {
+    if (!VEC) {
+      // scalar path: element e = j * 256 + tid, consecutive lanes on the contiguous
+      // (or, when neither is, the k) dimension -> every wave load is one dense run
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int e = j * 256 + tid;
+        int mn, kk;
+        if (KF) { mn = e >> 5; kk = e & 31; } else { kk = e >> 7; mn = e & 127; }
+        const long gm = mn0 + mn, gk = k0 + kk;
+        r[j] = (gm < MN && gk < K) ? P[gm * s_mn + gk * s_k] : 0.f;
+      }
+      return;
+    }
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int q = v * 256 + tid;  // float4 slot within the 128 x 32 tile
       int mn, kk;
       if (KF) { mn = q >> 3; kk = (q & 7) * 4; } else { kk = q >> 5; mn = (q & 31) * 4; }
       const long gm = mn0 + mn, gk = k0 + kk;
-      if (VEC) {
-        if (KF ? (gm < MN && gk + 3 < K) : (gk < K && gm + 3 < MN)) {
-          const f32x4 t = *reinterpret_cast<const f32x4*>(P + gm * s_mn + gk * s_k);
-          r[4 * v] = t[0]; r[4 * v + 1] = t[1]; r[4 * v + 2] = t[2]; r[4 * v + 3] = t[3];
-          continue;
-        }
+      if (KF ? (gm < MN && gk + 3 < K) : (gk < K && gm + 3 < MN)) {
+        const f32x4 t = *reinterpret_cast<const f32x4*>(P + gm * s_mn + gk * s_k);
+        r[4 * v] = t[0]; r[4 * v + 1] = t[1]; r[4 * v + 2] = t[2]; r[4 * v + 3] = t[3];
+        continue;
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -88,6 +99,15 @@ struct TileLoader {
     }
   }
   __device__ __forceinline__ void store(float (*S)[SBM + SPAD], int tid) const {
+    if (!VEC) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int e = j * 256 + tid;
+        if (KF) S[e & 31][e >> 5] = r[j];
+        else S[e >> 7][e & 127] = r[j];
+      }
+      return;
+    }
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int q = v * 256 + tid;
