@@ -155,3 +155,131 @@ PA_EXPORT int pa_nms_bitmask(const float* boxes, const int* order, const int* co
                      normalized ? 0.f : 1.f, keep);
   PA_LAUNCH_CHECK();
 }
+
+// ---------------------------------------------------------------- box generators / target assignment
+// prior_box (prior_box_op.cu GenPriorBox): boxes [H, W, P, 4] from the per-prior
+// (w, h) list; anchor_generator (anchor_generator_op.cu GenAnchors) in pixels;
+// polygon_box_transform (PolygonBoxTransformKernel); target_assign
+// (target_assign_op.h / NegTargetAssignKernel).
+namespace pa {
+namespace {
+
+__global__ void prior_box_kernel(const float* __restrict__ bw, const float* __restrict__ bh, float* __restrict__ boxes,
+                                 float* __restrict__ vars, int H, int W, int P, float IW, float IH, float sw, float sh,
+                                 float off, int clip, float v0, float v1, float v2, float v3) {
+  const long total = (long)H * W * P;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int p = (int)(i % P), w = (int)((i / P) % W), h = (int)(i / ((long)P * W));
+    const float cx = (w + off) * sw, cy = (h + off) * sh;
+    float b[4] = {(cx - bw[p] * 0.5f) / IW, (cy - bh[p] * 0.5f) / IH, (cx + bw[p] * 0.5f) / IW,
+                  (cy + bh[p] * 0.5f) / IH};
+    for (int j = 0; j < 4; ++j) {
+      float v = b[j];
+      if (clip) v = fminf(fmaxf(v, 0.f), 1.f);
+      boxes[i * 4 + j] = v;
+    }
+    vars[i * 4] = v0;
+    vars[i * 4 + 1] = v1;
+    vars[i * 4 + 2] = v2;
+    vars[i * 4 + 3] = v3;
+  }
+}
+
+__global__ void anchor_kernel(const float* __restrict__ aw, const float* __restrict__ ah, float* __restrict__ anchors,
+                              float* __restrict__ vars, int H, int W, int A, float sw, float sh, float off, float v0,
+                              float v1, float v2, float v3) {
+  const long total = (long)H * W * A;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int a = (int)(i % A), w = (int)((i / A) % W), h = (int)(i / ((long)A * W));
+    const float xc = w * sw + off * (sw - 1.f), yc = h * sh + off * (sh - 1.f);
+    anchors[i * 4] = xc - 0.5f * (aw[a] - 1.f);
+    anchors[i * 4 + 1] = yc - 0.5f * (ah[a] - 1.f);
+    anchors[i * 4 + 2] = xc + 0.5f * (aw[a] - 1.f);
+    anchors[i * 4 + 3] = yc + 0.5f * (ah[a] - 1.f);
+    vars[i * 4] = v0;
+    vars[i * 4 + 1] = v1;
+    vars[i * 4 + 2] = v2;
+    vars[i * 4 + 3] = v3;
+  }
+}
+
+__global__ void polygon_kernel(const float* __restrict__ x, float* __restrict__ y, long NC, int C, int H, int W) {
+  const long total = NC * H * W;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int w = (int)(i % W), h = (int)((i / W) % H), c = (int)((i / ((long)W * H)) % C);
+    y[i] = (c % 2 == 0 ? (float)w : (float)h) - x[i];
+  }
+}
+
+// out[b][p][:] = x[xoff[b] + m][p % Pw][:] for m = match[b][p] >= 0, else mismatch
+__global__ void target_assign_kernel(const float* __restrict__ x, const int* __restrict__ xoff,
+                                     const long* __restrict__ match, float* __restrict__ out, float* __restrict__ wt,
+                                     int N, int P, int Pw, int K, float mismatch) {
+  const long total = (long)N * P * K;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int k = (int)(i % K);
+    const long bp = i / K;
+    const int p = (int)(bp % P), b = (int)(bp / P);
+    const long m = match[bp];
+    if (m >= 0) {
+      out[i] = x[(((long)xoff[b] + m) * Pw + (Pw > 1 ? p % Pw : 0)) * K + k];
+      if (k == 0) wt[bp] = 1.f;
+    } else {
+      out[i] = mismatch;
+      if (k == 0) wt[bp] = 0.f;
+    }
+  }
+}
+
+__global__ void neg_assign_kernel(const long* __restrict__ neg, const int* __restrict__ neg_img,
+                                  float* __restrict__ out, float* __restrict__ wt, long nneg, int P, int K,
+                                  float mismatch) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nneg * K; i += (long)gridDim.x * blockDim.x) {
+    const long e = i / K;
+    const int k = (int)(i % K);
+    const long bp = (long)neg_img[e] * P + neg[e];
+    out[bp * K + k] = mismatch;
+    if (k == 0) wt[bp] = 1.f;
+  }
+}
+
+}  // namespace
+}  // namespace pa
+
+using namespace pa;
+
+PA_EXPORT int pa_prior_box(const float* bw, const float* bh, float* boxes, float* vars, int H, int W, int P, float IW,
+                           float IH, float sw, float sh, float off, int clip, const float* v, hipStream_t st) {
+  const long total = (long)H * W * P;
+  if (total <= 0) return 0;
+  hipLaunchKernelGGL(prior_box_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, st, bw, bh, boxes, vars, H, W, P,
+                     IW, IH, sw, sh, off, clip, v[0], v[1], v[2], v[3]);
+  PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_anchor_generator(const float* aw, const float* ah, float* anchors, float* vars, int H, int W, int A,
+                                  float sw, float sh, float off, const float* v, hipStream_t st) {
+  const long total = (long)H * W * A;
+  if (total <= 0) return 0;
+  hipLaunchKernelGGL(anchor_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, st, aw, ah, anchors, vars, H, W, A,
+                     sw, sh, off, v[0], v[1], v[2], v[3]);
+  PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_polygon_box_transform(const float* x, float* y, long NC, int C, int H, int W, hipStream_t st) {
+  if (NC * H * W <= 0) return 0;
+  hipLaunchKernelGGL(polygon_kernel, dim3(stream_grid(NC * H * W, 256)), dim3(256), 0, st, x, y, NC, C, H, W);
+  PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_target_assign(const float* x, const int* xoff, const long* match, const long* neg,
+                               const int* neg_img, float* out, float* wt, int N, int P, int Pw, int K, long nneg,
+                               float mismatch, hipStream_t st) {
+  if ((long)N * P * K > 0)
+    hipLaunchKernelGGL(target_assign_kernel, dim3(stream_grid((long)N * P * K, 256)), dim3(256), 0, st, x, xoff, match,
+                       out, wt, N, P, Pw, K, mismatch);
+  if (nneg > 0)
+    hipLaunchKernelGGL(neg_assign_kernel, dim3(stream_grid(nneg * K, 256)), dim3(256), 0, st, neg, neg_img, out, wt,
+                       nneg, P, K, mismatch);
+  PA_LAUNCH_CHECK();
+}

@@ -60,6 +60,11 @@ def prior_box(ctx):
             if maxs:
                 s = math.sqrt(m * maxs[k])
                 sizes.append((s, s))
+    r = _oplib.prior_box_op(feat, H, W, IH, IW, sizes, ctx.attr("variances"), sw, sh, off, ctx.attr("clip"))
+    if r is not None:  # GenPriorBox counterpart (detect.hip)
+        ctx.set_output("Boxes", r[0].to(feat.dtype))
+        ctx.set_output("Variances", r[1].to(feat.dtype))
+        return
     dev = feat.device
     bw = torch.tensor([s[0] for s in sizes], device=dev)
     bh = torch.tensor([s[1] for s in sizes], device=dev)
@@ -89,6 +94,11 @@ def anchor_generator(ctx):
             base_h = round(base_w * ar)
             ws.append(size / sw * base_w)
             hs.append(size / sh * base_h)
+    r = _oplib.anchor_generator_op(feat, H, W, ws, hs, ctx.attr("variances"), sw, sh, off)
+    if r is not None:  # GenAnchors counterpart (detect.hip)
+        ctx.set_output("Anchors", r[0].to(feat.dtype))
+        ctx.set_output("Variances", r[1].to(feat.dtype))
+        return
     dev = feat.device
     aw, ah = torch.tensor(ws, device=dev), torch.tensor(hs, device=dev)
     xc = (torch.arange(W, device=dev) * sw + off * (sw - 1)).view(1, W, 1)
@@ -189,6 +199,13 @@ def target_assign(ctx):
     xo = ctx.input_lod("X")[-1] if ctx.input_lod("X") else [0, x.shape[0]]
     mi = ctx.input("MatchIndices").long()
     N, P = mi.shape
+    has_neg = ctx.has_input("NegIndices")
+    r = _oplib.target_assign_op(x, xo, mi, ctx.input("NegIndices") if has_neg else None,
+                                ctx.input_lod("NegIndices")[-1] if has_neg else None, ctx.attr("mismatch_value"))
+    if r is not None:  # target_assign kernels (detect.hip)
+        ctx.set_output("Out", r[0].to(x.dtype))
+        ctx.set_output("OutWeight", r[1].to(x.dtype))
+        return
     K = x.shape[-1]
     xs = x.reshape(x.shape[0], -1, K)
     out = torch.full((N, P, K), float(ctx.attr("mismatch_value")), dtype=x.dtype, device=x.device)
@@ -335,6 +352,10 @@ def multiclass_nms_native(ctx):
 @register_op("polygon_box_transform", ["Input"], ["Output"], {}, grad=None)
 def polygon_box_transform(ctx):
     x = ctx.input("Input")
+    r = _oplib.polygon_box_transform_op(x)
+    if r is not None:  # PolygonBoxTransformKernel counterpart (detect.hip)
+        ctx.set_output("Output", r)
+        return
     N, C, H, W = x.shape
     gw = torch.arange(W, device=x.device, dtype=x.dtype).view(1, 1, 1, W).expand(N, C, H, W)
     gh = torch.arange(H, device=x.device, dtype=x.dtype).view(1, 1, H, 1).expand(N, C, H, W)

@@ -162,6 +162,10 @@ _SIGS = {
     "pa_bn_nchw_groups": [_I, _L],
     "pa_bn_nchw_fwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _L, _F, _F, _I, _I, _I, _P],
     "pa_bn_nchw_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _L, _I, _P],
+    "pa_prior_box": [_P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _F, _F, _I, _P, _P],
+    "pa_anchor_generator": [_P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _P, _P],
+    "pa_polygon_box_transform": [_P, _P, _L, _I, _I, _I, _P],
+    "pa_target_assign": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _L, _F, _P],
     "pa_cross_entropy": [_I, _I, _P, _P, _P, _P, _P, _L, _I, _L, _P],
     "pa_cos_sim": [_I, _P, _P, _P, _P, _P, _L, _I, _I, _P],
     "pa_cos_sim_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _P],

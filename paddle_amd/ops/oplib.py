@@ -1132,3 +1132,75 @@ def multiclass_nms_op(boxes, scores, background, score_thr, nms_top_k, nms_thr, 
     sel = torch.arange(T, device=dev).unsqueeze(0) < torch.as_tensor(counts, device=dev).unsqueeze(1)
     off = np.concatenate([[0], np.cumsum(counts)]).astype(int).tolist()
     return rows[sel], off
+
+
+# ------------------------------------------------------------------ box generators / target_assign (detect.hip)
+
+
+def _farr(vals):
+    import ctypes
+
+    return (ctypes.c_float * len(vals))(*[float(v) for v in vals])
+
+
+def prior_box_op(feat, H, W, IH, IW, sizes, variances, step_w, step_h, offset, clip):
+    """boxes, variances [H, W, P, 4] (fp32) from the per-prior (w, h) list, or None."""
+    if not (_ENABLED and feat.is_cuda) or not sizes:
+        return None
+    dev = feat.device
+    bw = torch.tensor([s[0] for s in sizes], dtype=torch.float32, device=dev)
+    bh = torch.tensor([s[1] for s in sizes], dtype=torch.float32, device=dev)
+    P = len(sizes)
+    boxes = torch.empty(H, W, P, 4, dtype=torch.float32, device=dev)
+    var = torch.empty_like(boxes)
+    N.call("pa_prior_box", N.ptr(bw), N.ptr(bh), N.ptr(boxes), N.ptr(var), H, W, P, float(IW), float(IH),
+           float(step_w), float(step_h), float(offset), int(bool(clip)), _farr(variances), N.stream())
+    return boxes, var
+
+
+def anchor_generator_op(feat, H, W, ws, hs, variances, sw, sh, offset):
+    if not (_ENABLED and feat.is_cuda) or not ws:
+        return None
+    dev = feat.device
+    aw = torch.tensor(ws, dtype=torch.float32, device=dev)
+    ah = torch.tensor(hs, dtype=torch.float32, device=dev)
+    anchors = torch.empty(H, W, len(ws), 4, dtype=torch.float32, device=dev)
+    var = torch.empty_like(anchors)
+    N.call("pa_anchor_generator", N.ptr(aw), N.ptr(ah), N.ptr(anchors), N.ptr(var), H, W, len(ws), float(sw),
+           float(sh), float(offset), _farr(variances), N.stream())
+    return anchors, var
+
+
+def polygon_box_transform_op(x):
+    if not (_ENABLED and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4):
+        return None
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    Nn, C, H, W = x.shape
+    N.call("pa_polygon_box_transform", N.ptr(x), N.ptr(y), Nn * C, C, H, W, N.stream())
+    return y
+
+
+def target_assign_op(x, xoff, match, neg=None, neg_off=None, mismatch=0.0):
+    """x [R, Pw, K] rows of all images (LoD offsets ``xoff``), match [N, P] int64 ->
+    (out [N, P, K], weight [N, P, 1]), or None."""
+    if not (_ENABLED and x.is_cuda and x.dtype == torch.float32):
+        return None
+    dev = x.device
+    Nn, P = match.shape
+    xs = x.reshape(x.shape[0], -1, x.shape[-1]).contiguous()
+    Pw, K = xs.shape[1], xs.shape[2]
+    xo = torch.tensor(list(xoff), dtype=torch.int32, device=dev)
+    m = match.to(torch.int64).contiguous()
+    out = torch.empty(Nn, P, K, dtype=torch.float32, device=dev)
+    wt = torch.empty(Nn, P, 1, dtype=torch.float32, device=dev)
+    nneg = 0
+    ng = ni = None
+    if neg is not None:
+        ng = neg.reshape(-1).to(torch.int64).contiguous()
+        nneg = ng.numel()
+        img = [b for b in range(len(neg_off) - 1) for _ in range(neg_off[b + 1] - neg_off[b])]
+        ni = torch.tensor(img, dtype=torch.int32, device=dev)
+    N.call("pa_target_assign", N.ptr(xs), N.ptr(xo), N.ptr(m), N.ptr(ng), N.ptr(ni), N.ptr(out), N.ptr(wt), Nn, P,
+           Pw, K, nneg, float(mismatch), N.stream())
+    return out, wt
