@@ -23,6 +23,8 @@
 // (output size), pool_with_index_op.cc.
 #include "common.h"
 
+#include <type_traits>
+
 namespace pa {
 namespace {
 
@@ -52,6 +54,8 @@ struct SgemmArgs {
   float alpha, beta;
   int atomic;               // C += alpha * AB with float atomics (beta / bias ignored)
   long ksplit;              // > 0: k-slices of this length (split-K, atomic)
+  // implicit-GEMM B operand (2-D conv gather, CONVB kernels): image [C][H][W] at B
+  int cH, cW, cOW, ckh, ckw, csh, csw, cph, cpw, cdh, cdw;
   int kbsplit;              // > 0: k-batch ranges of this many members (split over the k-batch, atomic)
   int nks;                  // split mode: z1 = kbatch_slice * nks + k_slice
 };
@@ -123,10 +127,47 @@ struct TileLoader {
   }
 };
 
+// Implicit im2col B operand of a 2-D convolution: B(k = (c, kh, kw), n = (oh, ow))
+// (forward, KF = false) or B(k = (oh, ow), n = (c, kh, kw)) (weight gradient,
+// KF = true), gathered from the image with zero padding -- no column buffer.  The
+// element -> (k, n) map is the scalar TileLoader's, so one index of each pair is
+// fixed per thread and decomposed once per tile.
+template <bool KF>
+struct ConvGather {
+  float r[16];
+  __device__ __forceinline__ float at(const float* __restrict__ P, const SgemmArgs& g, long ck, long s) const {
+    const int KT = g.ckh * g.ckw;
+    const int c = (int)(ck / KT), t = (int)(ck - (long)c * KT);
+    const int kh = t / g.ckw, kw = t - kh * g.ckw;
+    const int oh = (int)(s / g.cOW), ow = (int)(s - (long)oh * g.cOW);
+    const int ih = oh * g.csh - g.cph + kh * g.cdh, iw = ow * g.csw - g.cpw + kw * g.cdw;
+    return (ih >= 0 && ih < g.cH && iw >= 0 && iw < g.cW) ? P[((long)c * g.cH + ih) * g.cW + iw] : 0.f;
+  }
+  __device__ __forceinline__ void load(const float* __restrict__ P, const SgemmArgs& g, long mn0, long k0, long MN,
+                                       long K, int tid) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int e = j * 256 + tid;
+      int mn, kk;
+      if (KF) { mn = e >> 5; kk = e & 31; } else { kk = e >> 7; mn = e & 127; }
+      const long gm = mn0 + mn, gk = k0 + kk;
+      r[j] = (gm < MN && gk < K) ? (KF ? at(P, g, gm, gk) : at(P, g, gk, gm)) : 0.f;
+    }
+  }
+  __device__ __forceinline__ void store(float (*S)[SBM + SPAD], int tid) const {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int e = j * 256 + tid;
+      if (KF) S[e & 31][e >> 5] = r[j];
+      else S[e >> 7][e & 127] = r[j];
+    }
+  }
+};
+
 // 128 x 128 output tile, 4 waves of 64 x 64 (2 x 2 v_mfma_f32_32x32x2f32), k-tiles
 // of 32 double-buffered in LDS with the next tile's global loads issued before the
 // current tile's MFMAs (one barrier per k-tile).
-template <bool AK, bool BK_, bool VEC>
+template <bool AK, bool BK_, bool VEC, bool CONVB>
 __global__ __launch_bounds__(256) void sgemm_kernel(SgemmArgs g) {
   __shared__ float As[2][SBK][SBM + SPAD];
   __shared__ float Bs[2][SBK][SBN + SPAD];
@@ -138,14 +179,15 @@ __global__ __launch_bounds__(256) void sgemm_kernel(SgemmArgs g) {
   const float* bias = g.bias_m ? g.bias_m + z2 * g.bsBias2 : nullptr;
   const long m0 = (long)blockIdx.y * SBM, n0 = (long)blockIdx.x * SBN;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  long K = g.K;
+  long K = g.K, kbase = 0;
   int b_lo = 0, b_hi = g.kb;
   if (g.ksplit > 0 || g.kbsplit > 0) {  // split mode: z1 -> (k-batch slice, k slice)
     const long zk = z1 % g.nks, zb = z1 / g.nks;
     if (g.ksplit > 0) {
       const long kb0 = zk * g.ksplit;
       A0 += kb0 * g.sak;
-      B0 += kb0 * g.sbk;
+      if (CONVB) kbase = kb0;  // gathered B: the k slice starts at kb0
+      else B0 += kb0 * g.sbk;
       K = min(g.ksplit, g.K - kb0);
     }
     if (g.kbsplit > 0) {
@@ -161,7 +203,7 @@ __global__ __launch_bounds__(256) void sgemm_kernel(SgemmArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   TileLoader<AK, VEC> la;
-  TileLoader<BK_, VEC> lb;
+  typename std::conditional<CONVB, ConvGather<BK_>, TileLoader<BK_, VEC>>::type lb;
   const long ktiles = (K + SBK - 1) / SBK;
   const long total = ktiles * (b_hi - b_lo);
   if (total <= 0) return;  // empty split slice (uniform per workgroup: no barrier skipped by part of it)
@@ -169,7 +211,8 @@ __global__ __launch_bounds__(256) void sgemm_kernel(SgemmArgs g) {
   B0 += b_lo * g.kbB;
   // B(k, n) = B[k * sbk + n * sbn]: as an "MN x K" operand its mn stride is sbn
   la.load(A0, g.sam, g.sak, m0, 0, g.M, K, tid);
-  lb.load(B0, g.sbn, g.sbk, n0, 0, g.N, K, tid);
+  if constexpr (CONVB) lb.load(B0, g, n0, kbase, g.N, kbase + K, tid);
+  else lb.load(B0, g.sbn, g.sbk, n0, 0, g.N, K, tid);
   la.store(As[0], tid);
   lb.store(Bs[0], tid);
   __syncthreads();
@@ -180,7 +223,8 @@ __global__ __launch_bounds__(256) void sgemm_kernel(SgemmArgs g) {
       const long tn = t + 1;
       const long b = tn / ktiles, k0 = (tn % ktiles) * SBK;
       la.load(A0 + b * g.kbA, g.sam, g.sak, m0, k0, g.M, K, tid);
-      lb.load(B0 + b * g.kbB, g.sbn, g.sbk, n0, k0, g.N, K, tid);
+      if constexpr (CONVB) lb.load(B0 + b * g.kbB, g, n0, kbase + k0, g.N, kbase + K, tid);
+      else lb.load(B0 + b * g.kbB, g.sbn, g.sbk, n0, k0, g.N, K, tid);
     }
 #pragma unroll
     for (int kk = 0; kk < SBK; kk += 2) {
@@ -558,7 +602,7 @@ __global__ void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ d
 PA_EXPORT int pa_sgemm(const float* A, long sam, long sak, const float* B, long sbk, long sbn, float* C, long ldc,
                        long M, long N, long K, int Z1, int Z2, long bsA1, long bsB1, long bsC1, long bsA2, long bsB2,
                        long bsC2, int kb, long kbA, long kbB, const float* bias_m, long bsBias2, float alpha, float beta,
-                       int atomic, hipStream_t st) {
+                       int atomic, const int* conv, hipStream_t st) {
   if (M <= 0 || N <= 0) return 0;
   if (Z1 < 1 || Z2 < 1 || kb < 1 || (long)Z1 * Z2 > 65535) return (int)hipErrorInvalidValue;
   const long gy = (M + SBM - 1) / SBM, gx = (N + SBN - 1) / SBN;
@@ -614,9 +658,23 @@ PA_EXPORT int pa_sgemm(const float* A, long sam, long sak, const float* B, long 
   // float4 path: 16-B aligned bases and every non-contiguous stride a multiple of 4
   auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   auto m4 = [](long v) { return (v & 3) == 0; };
+  if (conv) {  // implicit-GEMM B: conv = {H, W, OW, kh, kw, sh, sw, ph, pw, dh, dw}
+    g.cH = conv[0]; g.cW = conv[1]; g.cOW = conv[2]; g.ckh = conv[3]; g.ckw = conv[4];
+    g.csh = conv[5]; g.csw = conv[6]; g.cph = conv[7]; g.cpw = conv[8]; g.cdh = conv[9]; g.cdw = conv[10];
+    const bool va = al(A) && m4(ak ? sam : sak) && m4(bsA1) && m4(bsA2) && m4(kbA) && (ak ? sak == 1 : sam == 1);
+    if (!ak) return (int)hipErrorInvalidValue;  // the conv forms use a k-contiguous A
+    if (va) {
+      if (bk) hipLaunchKernelGGL((sgemm_kernel<true, true, true, true>), grid, dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((sgemm_kernel<true, false, true, true>), grid, dim3(256), 0, st, g);
+    } else {
+      if (bk) hipLaunchKernelGGL((sgemm_kernel<true, true, false, true>), grid, dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((sgemm_kernel<true, false, false, true>), grid, dim3(256), 0, st, g);
+    }
+    PA_LAUNCH_CHECK();
+  }
   const bool vec = al(A) && al(B) && m4(ak ? sam : sak) && m4(bk ? sbn : sbk) && m4(bsA1) && m4(bsA2) && m4(bsB1) &&
                    m4(bsB2) && m4(kbA) && m4(kbB) && (ak ? sak == 1 : sam == 1) && (bk ? sbk == 1 : sbn == 1);
-#define SG(AKv, BKv, V) hipLaunchKernelGGL((sgemm_kernel<AKv, BKv, V>), grid, dim3(256), 0, st, g)
+#define SG(AKv, BKv, V) hipLaunchKernelGGL((sgemm_kernel<AKv, BKv, V, false>), grid, dim3(256), 0, st, g)
   if (vec) {
     if (ak && bk) SG(true, true, true);
     else if (ak) SG(true, false, true);

@@ -152,7 +152,7 @@ _SIGS = {
     "pa_moe_reduce": [_P, _P, _P, _P, _L, _I, _I, _P],
     "pa_moe_combine_bwd": [_P, _P, _P, _P, _P, _P, _L, _I, _I, _P],
     "pa_sgemm": [_P, _L, _L, _P, _L, _L, _P, _L, _L, _L, _L, _I, _I, _L, _L, _L, _L, _L, _L, _I, _L, _L, _P, _L, _F,
-                 _F, _I, _P],
+                 _F, _I, _P, _P],
     "pa_vol2col": [_I, _P, _P, _P, _I, _P],
     "pa_col2vol": [_P, _P, _P, _I, _I, _P],
     "pa_chan_sum": [_P, _P, _I, _I, _L, _I, _P],

@@ -27,6 +27,12 @@ from . import _native as N
 
 _ENABLED = os.environ.get("PADDLE_AMD_CONVND", "1") != "0"
 _COL_BUDGET = 1 << 28  # floats per column chunk (1 GiB)
+# 2-D implicit GEMM (B gathered in the tile loader, no column buffer): correct but
+# measured slower than vol2col + the vectorised GEMM on Fluid ResNet-50 (58.8 vs
+# 45.1 ms of kernel time per step, profiles/r2_fluid_resnet50_fp32_ab.jsonl) -- the
+# per-element index decomposition costs more than the column round trip; kept as the
+# zero-extra-memory option.
+_IMPLICIT = os.environ.get("PADDLE_AMD_CONV_IMPLICIT", "0") == "1"
 _DT = {torch.float32: 0, torch.bfloat16: 1}
 
 
@@ -56,13 +62,13 @@ def _arr(vals):
 
 
 def sgemm(A, sam, sak, B, sbk, sbn, C, ldc, M, Nn, K, Z1=1, Z2=1, bs1=(0, 0, 0), bs2=(0, 0, 0), kb=1,
-          kbA=0, kbB=0, bias=None, bs_bias2=0, alpha=1.0, beta=0.0, atomic=False):
+          kbA=0, kbB=0, bias=None, bs_bias2=0, alpha=1.0, beta=0.0, atomic=False, conv=None):
     """Strided batched fp32 GEMM: C[z](m, n) = alpha * sum_b A[z, b](m, :) B[z, b](:, n) (+ bias[m] | + beta C)."""
     if Z1 * Z2 > 65535:
         raise ValueError("sgemm: batch too large")
     N.call("pa_sgemm", N.ptr(A), sam, sak, N.ptr(B), sbk, sbn, N.ptr(C), ldc, M, Nn, K, int(Z1), int(Z2),
            bs1[0], bs1[1], bs1[2], bs2[0], bs2[1], bs2[2], int(kb), kbA, kbB, N.ptr(bias), bs_bias2, float(alpha),
-           float(beta), int(bool(atomic)), N.stream())
+           float(beta), int(bool(atomic)), _arr(conv) if conv is not None else None, N.stream())
 
 
 def _geo(C, sp, osp, k, s, p, d):
@@ -105,6 +111,19 @@ def _pointwise(k, s, p):
     return all(v == 1 for v in k) and all(v == 1 for v in s) and all(v == 0 for v in p)
 
 
+def _conv_geo(sp, osp, k, s, p, d):
+    """implicit-GEMM geometry for pa_sgemm: H, W, OW, kh, kw, sh, sw, ph, pw, dh, dw."""
+    return [sp[0], sp[1], osp[1], k[0], k[1], s[0], s[1], p[0], p[1], d[0], d[1]]
+
+
+def _geo2(geo):
+    """(H, W, OW, kh, kw, sh, sw, ph, pw, dh, dw) of a 2-D geo array, or None for 3-D."""
+    v = list(geo)
+    if v[1] != 1 or v[4] != 1 or v[7] != 1:
+        return None
+    return [v[2], v[3], v[6], v[8], v[9], v[11], v[12], v[14], v[15], v[17], v[18]]
+
+
 def _pw_geo(geo):
     """geo = (C, D, H, W, OD, OH, OW, kd, kh, kw, sd, sh, sw, pd, ph, pw, dd, dh, dw)."""
     v = list(geo)
@@ -132,6 +151,13 @@ def _conv_fwd(x, w, b, s, p, d, G, keep=None):
     geo = _geo(C, _pad3(sp), _pad3(osp), _pad3(k), _pad3(s), _pad3z(p), _pad3(d))
     y = torch.empty((Nn, Cout) + osp, dtype=torch.float32, device=x.device)
     wc = w.contiguous()
+    if _IMPLICIT and len(sp) == 2 and not _pointwise(k, s, p) and Nn * G <= 65535:
+        # 2-D: implicit GEMM, B gathered from the image in the tile loader (no column buffer)
+        H, W = sp
+        sgemm(wc, CgK, 1, x, 0, 1, y, S, Coutg, S, CgK, Z1=Nn, Z2=G,
+              bs1=(0, C * H * W, Cout * S), bs2=(Coutg * CgK, Cg * H * W, Coutg * S), bias=b, bs_bias2=Coutg,
+              conv=_conv_geo(sp, osp, k, s, p, d))
+        return y, geo, osp
     if _pointwise(k, s, p):
         if Nn * G > 65535:
             raise ValueError("conv: batch x groups too large")
@@ -183,6 +209,14 @@ def _conv_wgrad(dy, x, w_shape, geo, G, cols=None):
     Cg, Coutg = C // G, Cout // G
     CgK = Cg * KT
     dw = torch.zeros(w_shape, dtype=torch.float32, device=dy.device)
+    g2 = _geo2(geo)
+    if _IMPLICIT and g2 is not None and not (KT == 1 and _pw_geo(geo)):
+        # 2-D: dW[g] = sum_img dY[img][g] col(x[img])[g]^T with col gathered in the
+        # loader; images on the k-batch, split over workgroups by the launcher
+        H, W = g2[0], g2[1]
+        sgemm(dy, S, 1, x, 1, 0, dw, CgK, Coutg, CgK, S, Z1=1, Z2=G,
+              bs2=(Coutg * S, Cg * H * W, Coutg * CgK), kb=Nn, kbA=Cout * S, kbB=C * H * W, atomic=True, conv=g2)
+        return dw
     nb = _chunk(Nn, C * KT * S, G)
     pw = KT == 1 and _pw_geo(geo)
     for ci, n0 in enumerate(range(0, Nn, nb)):

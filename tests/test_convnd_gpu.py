@@ -374,3 +374,10 @@ def test_fluid_blas_fc():
     y.backward(gy.float().to(DEV))
     for d_, r_ in ((xd, xr), (wd, wr), (bd, br)):
         assert _rel(d_.grad, r_.grad) < 1e-6
+
+
+def test_conv2d_implicit_gemm_mode(monkeypatch):
+    """The zero-column-buffer 2-D path (B gathered in the GEMM tile loader)."""
+    monkeypatch.setattr(C, "_IMPLICIT", True)
+    for cfg in CONV2D:
+        test_conv2d_fwd_bwd(cfg)
