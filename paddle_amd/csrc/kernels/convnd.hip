@@ -61,6 +61,9 @@ struct SgemmArgs {
 };
 
 constexpr int SBM = 128, SBN = 128, SBK = 32, SPAD = 4;
+// LDS tiles are [mn][k] with rows of SBK + KPAD floats (144 B): the 16 lanes of a
+// ds_read_b128 phase hit 16 distinct 4-bank groups
+constexpr int KPAD = 4;
 
 // One k-tile of an operand, staged global -> registers -> LDS ([SBK][128 + SPAD],
 // k-major).  KF: the operand's k index is the contiguous one (A row-major / B
@@ -102,13 +105,13 @@ struct TileLoader {
       }
     }
   }
-  __device__ __forceinline__ void store(float (*S)[SBM + SPAD], int tid) const {
+  __device__ __forceinline__ void store(float (*S)[SBK + KPAD], int tid) const {
     if (!VEC) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const int e = j * 256 + tid;
-        if (KF) S[e & 31][e >> 5] = r[j];
-        else S[e >> 7][e & 127] = r[j];
+        if (KF) S[e >> 5][e & 31] = r[j];
+        else S[e & 127][e >> 7] = r[j];
       }
       return;
     }
@@ -117,11 +120,11 @@ struct TileLoader {
       const int q = v * 256 + tid;
       if (KF) {
         const int mn = q >> 3, kk = (q & 7) * 4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) S[kk + e][mn] = r[4 * v + e];
+        *reinterpret_cast<f32x4*>(&S[mn][kk]) = f32x4{r[4 * v], r[4 * v + 1], r[4 * v + 2], r[4 * v + 3]};
       } else {
         const int kk = q >> 5, mn = (q & 31) * 4;
-        *reinterpret_cast<f32x4*>(&S[kk][mn]) = f32x4{r[4 * v], r[4 * v + 1], r[4 * v + 2], r[4 * v + 3]};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) S[mn + e][kk] = r[4 * v + e];
       }
     }
   }
@@ -154,12 +157,12 @@ struct ConvGather {
       r[j] = (gm < MN && gk < K) ? (KF ? at(P, g, gm, gk) : at(P, g, gk, gm)) : 0.f;
     }
   }
-  __device__ __forceinline__ void store(float (*S)[SBM + SPAD], int tid) const {
+  __device__ __forceinline__ void store(float (*S)[SBK + KPAD], int tid) const {
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int e = j * 256 + tid;
-      if (KF) S[e & 31][e >> 5] = r[j];
-      else S[e >> 7][e & 127] = r[j];
+      if (KF) S[e >> 5][e & 31] = r[j];
+      else S[e & 127][e >> 7] = r[j];
     }
   }
 };
@@ -169,8 +172,8 @@ struct ConvGather {
 // current tile's MFMAs (one barrier per k-tile).
 template <bool AK, bool BK_, bool VEC, bool CONVB>
 __global__ __launch_bounds__(256) void sgemm_kernel(SgemmArgs g) {
-  __shared__ float As[2][SBK][SBM + SPAD];
-  __shared__ float Bs[2][SBK][SBN + SPAD];
+  __shared__ __attribute__((aligned(16))) float As[2][SBM][SBK + KPAD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][SBN][SBK + KPAD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long z1 = blockIdx.z / g.Z2, z2 = blockIdx.z % g.Z2;
   const float* A0 = g.A + z1 * g.bsA1 + z2 * g.bsA2;
@@ -226,15 +229,23 @@ __global__ __launch_bounds__(256) void sgemm_kernel(SgemmArgs g) {
       if constexpr (CONVB) lb.load(B0 + b * g.kbB, g, n0, kbase + k0, g.N, kbase + K, tid);
       else lb.load(B0 + b * g.kbB, g.sbn, g.sbk, n0, k0, g.N, K, tid);
     }
+    // k permuted inside the tile: lanes 0-31 feed k = j, lanes 32-63 k = 16 + j for
+    // MFMA step j (the reduction order is free), so every lane reads 4 consecutive k
+    // of its row with one ds_read_b128 per operand block
+    const int kh = (lane >> 5) * 16, rl = lane & 31;
 #pragma unroll
-    for (int kk = 0; kk < SBK; kk += 2) {
-      const int k = kk + (lane >> 5);
-      const float a0 = As[cur][k][wm + (lane & 31)], a1 = As[cur][k][wm + 32 + (lane & 31)];
-      const float b0 = Bs[cur][k][wn + (lane & 31)], b1 = Bs[cur][k][wn + 32 + (lane & 31)];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    for (int j0 = 0; j0 < 16; j0 += 4) {
+      const f32x4 a0 = *reinterpret_cast<const f32x4*>(&As[cur][wm + rl][kh + j0]);
+      const f32x4 a1 = *reinterpret_cast<const f32x4*>(&As[cur][wm + 32 + rl][kh + j0]);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(&Bs[cur][wn + rl][kh + j0]);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(&Bs[cur][wn + 32 + rl][kh + j0]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[e], b0[e], acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[e], b1[e], acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[e], b0[e], acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[e], b1[e], acc[1][1], 0, 0, 0);
+      }
     }
     if (more) {
       la.store(As[cur ^ 1], tid);
