@@ -64,6 +64,10 @@ constexpr int SBM = 128, SBN = 128, SBK = 32, SPAD = 4;
 // LDS tiles are [mn][k] with rows of SBK + KPAD floats (144 B): the 16 lanes of a
 // ds_read_b128 phase hit 16 distinct 4-bank groups
 constexpr int KPAD = 4;
+// 16-B k-group swizzle by row: k -> k ^ (((row >> 2) & 7) << 2).  The transposed
+// (mn-contiguous operand) stores write 4 rows per lane; without it those rows,
+// 4 apart, hit one 16-bank slice (8-way conflicts).  Reads stay whole 16-B groups.
+__device__ __forceinline__ int ksw(int row, int k) { return k ^ (((row >> 2) & 7) << 2); }
 
 // One k-tile of an operand, staged global -> registers -> LDS ([SBK][128 + SPAD],
 // k-major).  KF: the operand's k index is the contiguous one (A row-major / B
@@ -110,8 +114,8 @@ struct TileLoader {
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const int e = j * 256 + tid;
-        if (KF) S[e >> 5][e & 31] = r[j];
-        else S[e & 127][e >> 7] = r[j];
+        if (KF) S[e >> 5][ksw(e >> 5, e & 31)] = r[j];
+        else S[e & 127][ksw(e & 127, e >> 7)] = r[j];
       }
       return;
     }
@@ -120,11 +124,11 @@ struct TileLoader {
       const int q = v * 256 + tid;
       if (KF) {
         const int mn = q >> 3, kk = (q & 7) * 4;
-        *reinterpret_cast<f32x4*>(&S[mn][kk]) = f32x4{r[4 * v], r[4 * v + 1], r[4 * v + 2], r[4 * v + 3]};
+        *reinterpret_cast<f32x4*>(&S[mn][ksw(mn, kk)]) = f32x4{r[4 * v], r[4 * v + 1], r[4 * v + 2], r[4 * v + 3]};
       } else {
         const int kk = q >> 5, mn = (q & 31) * 4;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) S[mn + e][kk] = r[4 * v + e];
+        for (int e = 0; e < 4; ++e) S[mn + e][ksw(mn + e, kk)] = r[4 * v + e];
       }
     }
   }
@@ -161,8 +165,8 @@ struct ConvGather {
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int e = j * 256 + tid;
-      if (KF) S[e >> 5][e & 31] = r[j];
-      else S[e & 127][e >> 7] = r[j];
+      if (KF) S[e >> 5][ksw(e >> 5, e & 31)] = r[j];
+      else S[e & 127][ksw(e & 127, e >> 7)] = r[j];
     }
   }
 };
@@ -235,10 +239,11 @@ __global__ __launch_bounds__(256) void sgemm_kernel(SgemmArgs g) {
     const int kh = (lane >> 5) * 16, rl = lane & 31;
 #pragma unroll
     for (int j0 = 0; j0 < 16; j0 += 4) {
-      const f32x4 a0 = *reinterpret_cast<const f32x4*>(&As[cur][wm + rl][kh + j0]);
-      const f32x4 a1 = *reinterpret_cast<const f32x4*>(&As[cur][wm + 32 + rl][kh + j0]);
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(&Bs[cur][wn + rl][kh + j0]);
-      const f32x4 b1 = *reinterpret_cast<const f32x4*>(&Bs[cur][wn + 32 + rl][kh + j0]);
+      const int ka = kh + j0;
+      const f32x4 a0 = *reinterpret_cast<const f32x4*>(&As[cur][wm + rl][ksw(wm + rl, ka)]);
+      const f32x4 a1 = *reinterpret_cast<const f32x4*>(&As[cur][wm + 32 + rl][ksw(wm + 32 + rl, ka)]);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(&Bs[cur][wn + rl][ksw(wn + rl, ka)]);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(&Bs[cur][wn + 32 + rl][ksw(wn + 32 + rl, ka)]);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[e], b0[e], acc[0][0], 0, 0, 0);
