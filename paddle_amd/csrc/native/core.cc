@@ -698,7 +698,25 @@ bool read_lod_tensor(FILE* f, Tensor* t) {
   VarDesc vd;
   parse_tensor_desc(Reader{(const unsigned char*)desc.data(), (const unsigned char*)desc.data() + desc.size()},
                     &vd);
-  for (auto d : vd.dims) PA_CHECK(d >= 0 && d < (1ll << 40), "LoDTensor: implausible dim");
+  // element count and byte total with overflow checks (dims like [2^33, 2^31] must not
+  // wrap numel to a small value), capped at 2^40 bytes and at what the file still holds
+  uint64_t count = 1;
+  for (auto d : vd.dims) {
+    PA_CHECK(d >= 0 && d < (1ll << 40), "LoDTensor: implausible dim");
+    PA_CHECK(!__builtin_mul_overflow(count, (uint64_t)d, &count), "LoDTensor: element count overflows");
+  }
+  uint64_t bytes = 0;
+  PA_CHECK(!__builtin_mul_overflow(count, (uint64_t)dt_size(vd.dtype), &bytes) && bytes <= (1ull << 40),
+           "LoDTensor: implausible byte size");
+  {
+    const long here = ftell(f);
+    if (here >= 0 && fseek(f, 0, SEEK_END) == 0) {
+      const long end = ftell(f);
+      PA_CHECK(fseek(f, here, SEEK_SET) == 0, "LoDTensor: seek failed");
+      PA_CHECK(end >= here && bytes <= (uint64_t)(end - here), "LoDTensor: declared size %llu beyond end of file",
+               (unsigned long long)bytes);
+    }
+  }
   LoD lod = t->lod;
   t->alloc(vd.dtype, vd.dims, -1);
   t->lod = lod;

@@ -235,3 +235,41 @@ def test_registered_native_ops_cover_inference_set():
     assert need <= host, need - host
     dev = set(native.registered_ops(device=True))
     assert {"mul", "fc", "matmul", "conv2d", "pool2d", "batch_norm", "softmax", "elementwise_add"} <= dev
+
+
+def _tensor_stream(dims, payload=b"", dtype=5):
+    import struct
+
+    d = bytes([0x08, dtype])
+    for x in dims:
+        v, b = x, bytearray()
+        while v >= 0x80:
+            b.append((v & 0x7F) | 0x80)
+            v >>= 7
+        b.append(v)
+        d += bytes([0x10]) + bytes(b)
+    return struct.pack("<IQ", 0, 0) + struct.pack("<Ii", 0, len(d)) + d + payload
+
+
+@pytest.mark.parametrize("dims,payload", [
+    ([2 ** 33, 2 ** 31], b""),          # numel wraps to 0 in int64 without the overflow check
+    ([2 ** 39, 2 ** 39], b"\0" * 64),   # element count overflows u64
+    ([1024, 1024], b"\0" * 64),         # declared 4 MiB, file holds 64 B
+])
+def test_native_loader_rejects_overflowing_dims(tmp_path, dims, payload):
+    """NativePaddlePredictor's params reader (csrc/native/core.cc
+    read_lod_tensor) must reject element counts that overflow and sizes beyond the
+    file, before allocating."""
+    main, startup = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, startup):
+        x = fluid.layers.data(name="x", shape=[4], dtype="float32")
+        fluid.layers.fc(x, size=3)
+    prog = native.NativeProgram(data=main.desc.serialize_to_string())
+    persist = sorted(v.name for v in main.list_vars() if v.persistable and v.name not in ("feed", "fetch"))
+    assert persist
+    with open(tmp_path / "params", "wb") as f:
+        for _ in persist:
+            f.write(_tensor_stream(dims, payload))
+    ns = native.NativeScope()
+    with pytest.raises(RuntimeError):
+        ns.load_persistables(prog, str(tmp_path), combined=str(tmp_path / "params"))
