@@ -38,7 +38,7 @@ from . import tensor_api as _tensor_api  # noqa: E402
 for _n in dir(_tensor_api):
     if not _n.startswith("_") and _n not in ("annotations", "builtins", "math", "np", "torch"):
         globals()[_n] = getattr(_tensor_api, _n)
-_tensor_api.install_tensor_methods()
+Tensor = _tensor_api.Tensor
 
 from . import amp, io, metric, nn, optimizer  # noqa: E402,F401
 from . import distributed  # noqa: E402,F401

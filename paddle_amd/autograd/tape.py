@@ -173,9 +173,24 @@ def recording():
 
 
 def apply(fn, *args):
-    """Function application that records on the active tape (if any), else
-    ``fn.apply`` under torch autograd."""
+    """Application of a fused op ``fn`` (hand-written forward / backward):
+
+    * on the active tape (bench / model step recording), if any;
+    * else, when an argument is a framework ``Tensor`` (DyGraph), on the eager
+      engine: one grad node whose backward is ``fn.backward`` (torch autograd off);
+    * else (raw torch tensors: interop with torch-native code) ``fn.apply``."""
     t = current()
     if t is not None:
         return t.apply(fn, *args)
+    from . import engine
+
+    if any(isinstance(a, engine.Tensor) for a in args):
+        if engine.is_grad_enabled():
+            out = engine.record_function(fn, args)
+            if out is not None:
+                return out
+        ctx = _Ctx(tuple(False for _ in args))
+        with torch.no_grad(), torch._C.DisableTorchFunctionSubclass():
+            out = fn.forward(ctx, *[engine._raw(a) for a in args])
+        return engine._wrap(out)
     return fn.apply(*args)

@@ -845,7 +845,7 @@ static int launch_g(const Params& p, int batch, hipStream_t st) {
   if constexpr ((GM == 1 && !AK) || (GM == 2 && (AK || BK))) {
     return -1;
   } else {
-    const bool pf = g_sched < 0 ? (!AK && !BK) : g_sched == 1;
+    const bool pf = g_sched == 1;  // measured: in-cluster prefetch loses on every form (profiles/r3_gemm_mn_forms.jsonl)
     if constexpr (GM != 2) {
       if (p.K % BKT == 0 && p.k_total % BKT == 0)  // every k-tile full: the k range check is wave-uniform
         return pf ? launch_v<AK, BK, F32, true, true, false, false, GM>(p, batch, st)

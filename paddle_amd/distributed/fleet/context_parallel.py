@@ -24,6 +24,7 @@ import torch
 
 from ... import ops
 from ...parallel import comm
+from ...autograd import tape as _tape  # noqa: E402
 
 
 def _a2a(x, group):
@@ -75,9 +76,9 @@ def ulysses_attention(q, k, v, group, causal=True, scale=None, attn_fn=None):
         return attn(q, k, v, causal=causal, scale=scale)
     if q.shape[2] % P or k.shape[2] % P:
         raise ValueError(f"Ulysses needs heads divisible by sep degree {P}")
-    qh, kh, vh = (_SeqToHead.apply(t, group) for t in (q, k, v))
+    qh, kh, vh = (_tape.apply(_SeqToHead, t, group) for t in (q, k, v))
     o = attn(qh, kh, vh, causal=causal, scale=scale)
-    return _HeadToSeq.apply(o, group)
+    return _tape.apply(_HeadToSeq, o, group)
 
 
 class _GatherSeq(torch.autograd.Function):
@@ -110,7 +111,7 @@ def allgather_kv_attention(q, k, v, group, causal=True, scale=None, attn_fn=None
         return attn(q, k, v, causal=causal, scale=scale)
     r = comm.get_rank(group)
     s = q.shape[1]
-    kf, vf = _GatherSeq.apply(k, group), _GatherSeq.apply(v, group)
+    kf, vf = _tape.apply(_GatherSeq, k, group), _tape.apply(_GatherSeq, v, group)
     if causal:
         kf, vf = kf[:, :(r + 1) * s], vf[:, :(r + 1) * s]
     return attn(q, kf, vf, causal=causal, scale=scale)
@@ -323,7 +324,7 @@ def ring_attention(q, k, v, group, causal=True, scale=None):
         return (ops.flash_attention if q.is_cuda else _attn_ref_causal)(q, k, v, causal=True, scale=scale)
     if q.shape[1] % 2:
         raise ValueError("zigzag shards hold two equal chunks: local length must be even")
-    return _RingAttnFn.apply(q, k, v, group, scale)
+    return _tape.apply(_RingAttnFn, q, k, v, group, scale)
 
 
 def _attn_ref_causal(q, k, v, causal=True, scale=None):

@@ -21,6 +21,7 @@ import torch.nn.functional as F
 from ...nn import Layer
 from ...ops import moe_route as _route
 from ...parallel import comm
+from ...autograd import tape as _tape  # noqa: E402
 
 
 class _AllToAll(torch.autograd.Function):
@@ -41,7 +42,7 @@ class _AllToAll(torch.autograd.Function):
 def all_to_all(x, in_splits, out_splits, group):
     if comm.get_world_size(group) == 1:
         return x
-    return _AllToAll.apply(x, in_splits, out_splits, group)
+    return _tape.apply(_AllToAll, x, in_splits, out_splits, group)
 
 
 class TopKGate(Layer):

@@ -20,6 +20,7 @@ from ... import ops
 from ...nn import Layer
 from ...nn import initializer as I
 from ...parallel import comm
+from ...autograd import tape as _tape  # noqa: E402
 
 
 # ------------------------------------------------------------------ autograd comm
@@ -115,23 +116,23 @@ class _ReduceScatterTokens(torch.autograd.Function):
 
 
 def copy_to_region(x, group):
-    return _CopyToRegion.apply(x, group) if comm.get_world_size(group) > 1 else x
+    return _tape.apply(_CopyToRegion, x, group) if comm.get_world_size(group) > 1 else x
 
 
 def reduce_from_region(x, group):
-    return _ReduceFromRegion.apply(x, group) if comm.get_world_size(group) > 1 else x
+    return _tape.apply(_ReduceFromRegion, x, group) if comm.get_world_size(group) > 1 else x
 
 
 def gather_last_dim(x, group):
-    return _GatherLastDim.apply(x, group)
+    return _tape.apply(_GatherLastDim, x, group)
 
 
 def all_gather_tokens(x, group):
-    return _AllGatherTokens.apply(x, group)
+    return _tape.apply(_AllGatherTokens, x, group)
 
 
 def reduce_scatter_tokens(x, group):
-    return _ReduceScatterTokens.apply(x, group)
+    return _tape.apply(_ReduceScatterTokens, x, group)
 
 
 class TPGroup:
@@ -230,7 +231,7 @@ def vocab_parallel_embedding(ids, weight, group):
     W, r = _mp(group)
     if W == 1:
         return ops.embedding(ids, weight)
-    return _VocabParallelEmbeddingFn.apply(ids, weight, r * weight.shape[0], group)
+    return _tape.apply(_VocabParallelEmbeddingFn, ids, weight, r * weight.shape[0], group)
 
 
 class VocabParallelEmbedding(Layer):
@@ -291,7 +292,7 @@ def parallel_cross_entropy(logits, label, group, ignore_index=-100, reduction="m
     if W == 1:
         loss = torch.nn.functional.cross_entropy(flat.float(), lab, ignore_index=ignore_index, reduction="none")
     else:
-        loss = _ParallelCEFn.apply(flat, lab, r * N, group, ignore_index)
+        loss = _tape.apply(_ParallelCEFn, flat, lab, r * N, group, ignore_index)
     if reduction == "none":
         return loss.reshape(label.shape)
     if reduction == "sum":

@@ -18,6 +18,8 @@ from __future__ import annotations
 
 import torch
 
+from ..autograd import engine as _eager
+
 from ..nn import Layer
 from ..parallel import comm
 
@@ -58,7 +60,10 @@ class DataParallel(Layer):
         self._cb_queued = False
         if self.W > 1:
             for p in params:
-                p.register_post_accumulate_grad_hook(self._on_grad)
+                if isinstance(p, _eager.Tensor):  # framework tensors: the eager engine's hook
+                    _eager.add_grad_ready_hook(p, self._on_grad)
+                else:
+                    p.register_post_accumulate_grad_hook(self._on_grad)
 
     def forward(self, *a, **k):
         return self._layers(*a, **k)
@@ -85,7 +90,10 @@ class DataParallel(Layer):
             self._launch(i)
             if not self._cb_queued:
                 self._cb_queued = True
-                torch.autograd.Variable._execution_engine.queue_callback(self._finish)
+                if _eager.in_backward():
+                    _eager.queue_callback(self._finish)
+                else:
+                    torch.autograd.Variable._execution_engine.queue_callback(self._finish)
 
     def _finish(self):
         self._cb_queued = False

@@ -33,6 +33,7 @@ import torch
 from ..ops import optim as fused_optim
 from ..parallel import comm
 from ..parallel.sharding import FlatShardedOptimizer, _no_decay
+from ..autograd import tape as _tape  # noqa: E402
 
 
 class _Regather(torch.autograd.Function):
@@ -156,6 +157,8 @@ class ShardedStage3:
             self.units.append(u)
             for p in u.params:
                 p.register_post_accumulate_grad_hook(lambda p, u=u: u.on_grad(p))
+                # the framework's eager engine / tape fire these at the same point
+                p.__dict__.setdefault("_pa_grad_ready_hooks", []).append(lambda p, u=u: u.on_grad(p))
             self._hook(u)
         for u in self.units:
             u.release()
@@ -173,14 +176,14 @@ class ShardedStage3:
                 idx = [i for i, o in enumerate(out) if torch.is_tensor(o) and o.requires_grad]
                 if not idx:
                     return out
-                res = _Regather.apply(u, *[out[i] for i in idx])
+                res = _tape.apply(_Regather, u, *[out[i] for i in idx])
                 res = res if isinstance(res, tuple) else (res,)
                 lst = list(out)
                 for i, t in zip(idx, res):
                     lst[i] = t
                 return tuple(lst)
             if torch.is_tensor(out) and out.requires_grad:
-                return _Regather.apply(u, out)
+                return _tape.apply(_Regather, u, out)
             return out
 
         u.module.register_forward_pre_hook(pre)

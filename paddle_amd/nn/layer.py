@@ -12,12 +12,14 @@ from collections import OrderedDict
 import torch
 
 from .. import ops
+from ..autograd import engine as _eager
 from . import initializer as I
 
 
-class ParamBase(torch.nn.Parameter):
-    """DyGraph parameter: a torch Parameter with Paddle's writable ``name``
-    (``torch.Tensor.name`` is a read-only C attribute) and ``trainable``."""
+class ParamBase(_eager.Tensor, torch.nn.Parameter):
+    """DyGraph parameter: a framework ``Tensor`` (eager-engine leaf, stop_gradient
+    False when trainable) that ``torch.nn.Module`` bookkeeping also registers as a
+    parameter, with Paddle's writable ``name`` and ``trainable``."""
 
     @property
     def name(self):

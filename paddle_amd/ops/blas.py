@@ -19,6 +19,7 @@ import os
 import torch
 
 from . import convnd as _C
+from ..autograd import tape as _tape  # noqa: E402
 
 _ENABLED = os.environ.get("PADDLE_AMD_FLUID_BLAS", "1") != "0"
 
@@ -94,7 +95,7 @@ class _MatmulFn(torch.autograd.Function):
 
 def matmul(a, b, alpha=1.0):
     """C = alpha * a @ b for 2-D / 3-D operands (3-D b needs the same batch)."""
-    return _MatmulFn.apply(a, b, float(alpha))
+    return _tape.apply(_MatmulFn, a, b, float(alpha))
 
 
 class _FcFn(torch.autograd.Function):
@@ -132,4 +133,4 @@ class _FcFn(torch.autograd.Function):
 
 def fc(x2, w, bias):
     """x2 [M, K] @ w [K, N] + bias [N]."""
-    return _FcFn.apply(x2, w, bias)
+    return _tape.apply(_FcFn, x2, w, bias)

@@ -25,6 +25,7 @@ import torch
 
 from . import _native as _nat
 from . import gemm as _G
+from ..autograd import tape as _tape  # noqa: E402
 
 
 _ENABLED = [True]
@@ -156,7 +157,7 @@ class _Conv2dNHWC(torch.autograd.Function):
 def conv2d_nhwc(x, weight, bias=None, stride=1, padding=0, dilation=1):
     """x [N, H, W, C] bf16 contiguous, weight [Cout, Cin, KH, KW] (Paddle layout)."""
     s, p, d = _pair(stride), _pair(padding), _pair(dilation)
-    return _Conv2dNHWC.apply(x, weight, bias, tuple(map(_i, s)), tuple(map(_i, p)), tuple(map(_i, d)))
+    return _tape.apply(_Conv2dNHWC, x, weight, bias, tuple(map(_i, s)), tuple(map(_i, p)), tuple(map(_i, d)))
 
 
 # ------------------------------------------------------------------ depthwise conv (dwconv.hip)
@@ -208,7 +209,7 @@ class _DwConvNHWC(torch.autograd.Function):
 def dwconv2d_nhwc(x, weight, bias=None, stride=1, padding=0, dilation=1):
     """Depthwise conv: x [N, H, W, C] bf16, weight [C * mult, 1, KH, KW]."""
     s, p, d = _pair(stride), _pair(padding), _pair(dilation)
-    return _DwConvNHWC.apply(x, weight, bias, tuple(map(_i, s)), tuple(map(_i, p)), tuple(map(_i, d)))
+    return _tape.apply(_DwConvNHWC, x, weight, bias, tuple(map(_i, s)), tuple(map(_i, p)), tuple(map(_i, d)))
 
 
 # ------------------------------------------------------------------ batch norm
@@ -287,7 +288,7 @@ def batch_norm_nhwc_train(x, weight, bias, running_mean, running_var, momentum=0
         if not relu:
             raise ValueError("the fused residual form is relu(bn(x) + residual)")
         residual = residual.contiguous()
-    return _BatchNormNHWC.apply(x, weight, bias, running_mean, running_var, float(momentum), float(eps), bool(relu),
+    return _tape.apply(_BatchNormNHWC, x, weight, bias, running_mean, running_var, float(momentum), float(eps), bool(relu),
                                 residual)
 
 
@@ -351,7 +352,7 @@ def max_pool2d_nhwc(x, kernel_size, stride=None, padding=0):
     k = tuple(map(_i, _pair(kernel_size)))
     s = tuple(map(_i, _pair(stride if stride is not None else kernel_size)))
     p = tuple(map(_i, _pair(padding)))
-    return _MaxPoolNHWC.apply(x, k, s, p)
+    return _tape.apply(_MaxPoolNHWC, x, k, s, p)
 
 
 class _GapNHWC(torch.autograd.Function):
@@ -373,4 +374,4 @@ class _GapNHWC(torch.autograd.Function):
 
 
 def global_avg_pool_nhwc(x):
-    return _GapNHWC.apply(x)
+    return _tape.apply(_GapNHWC, x)

@@ -24,6 +24,7 @@ import os
 import torch
 
 from . import _native as N
+from ..autograd import tape as _tape  # noqa: E402
 
 _ENABLED = os.environ.get("PADDLE_AMD_CONVND", "1") != "0"
 _COL_BUDGET = 1 << 28  # floats per column chunk (1 GiB)
@@ -276,7 +277,7 @@ def supported_conv(x, w, groups=1):
 def conv_nd(x, w, b=None, stride=1, padding=0, dilation=1, groups=1):
     """x [N, C, (D,) H, W], w [Cout, C / groups, (kd,) kh, kw]."""
     nd = x.dim() - 2
-    return _ConvNdFn.apply(x, w, b, _tup(stride, nd), _tup(padding, nd), _tup(dilation, nd), int(groups))
+    return _tape.apply(_ConvNdFn, x, w, b, _tup(stride, nd), _tup(padding, nd), _tup(dilation, nd), int(groups))
 
 
 # ------------------------------------------------------------------ transposed convolution
@@ -347,7 +348,7 @@ def conv_transpose_nd(x, w, stride=1, padding=0, dilation=1, groups=1, output_pa
     s, p, d, op = _tup(stride, nd), _tup(padding, nd), _tup(dilation, nd), _tup(output_padding, nd)
     k = tuple(w.shape[2:])
     osp = tuple((x.shape[2 + i] - 1) * s[i] - 2 * p[i] + d[i] * (k[i] - 1) + 1 + op[i] for i in range(nd))
-    return _ConvTNdFn.apply(x, w, s, p, d, int(groups), osp)
+    return _tape.apply(_ConvTNdFn, x, w, s, p, d, int(groups), osp)
 
 
 def supported_conv_transpose(x, w, groups=1):
@@ -410,7 +411,7 @@ def pool_nd(x, pooling_type="max", ksize=2, stride=None, padding=0, exclusive=Tr
     if global_pooling:
         k, p = tuple(x.shape[2:]), (0,) * nd
     typ = 0 if pooling_type == "max" else 1
-    y, mask = _PoolFn.apply(x, typ, k, s, p, bool(exclusive), bool(ceil_mode), bool(return_mask))
+    y, mask = _tape.apply(_PoolFn, x, typ, k, s, p, bool(exclusive), bool(ceil_mode), bool(return_mask))
     return (y, mask) if return_mask else y
 
 
@@ -451,7 +452,7 @@ def unpool2d(x, indices, ksize, strides, paddings):
     """Max unpool (unpool_op.cc: out = (in - 1) * stride - 2 * pad + ksize)."""
     k, s, p = _tup(ksize, 2), _tup(strides, 2), _tup(paddings, 2)
     osp = tuple((x.shape[2 + i] - 1) * s[i] - 2 * p[i] + k[i] for i in range(2))
-    return _UnpoolFn.apply(x, indices, osp)
+    return _tape.apply(_UnpoolFn, x, indices, osp)
 
 
 class _MaxoutFn(torch.autograd.Function):
@@ -484,7 +485,7 @@ class _MaxoutFn(torch.autograd.Function):
 def maxout(x, groups):
     if x.shape[1] % groups:
         raise ValueError("maxout: channels must be divisible by groups")
-    return _MaxoutFn.apply(x, int(groups))
+    return _tape.apply(_MaxoutFn, x, int(groups))
 
 
 # ------------------------------------------------------------------ batch norm (channel-first)
@@ -545,5 +546,5 @@ def batch_norm_nchw(x, scale, bias, run_mean, run_var, momentum=0.9, eps=1e-5, t
     Returns (y, mean_out, var_out, saved_mean, saved_inv_std); running averages use
     the biased batch variance (Fluid batch_norm_op.cc; ``unbiased_running_var`` for the
     2.x layer convention) and Paddle's momentum (running = m * running + (1 - m) * batch)."""
-    return _BatchNormNCHW.apply(x, scale, bias, run_mean, run_var, float(momentum), float(eps), bool(training),
+    return _tape.apply(_BatchNormNCHW, x, scale, bias, run_mean, run_var, float(momentum), float(eps), bool(training),
                                 bool(relu), bool(unbiased_running_var))

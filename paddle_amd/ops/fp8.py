@@ -14,6 +14,7 @@ numerics are emulated in fp32, so results match the device path to fp8 rounding.
 from __future__ import annotations
 
 import torch
+from ..autograd import tape as _tape  # noqa: E402
 
 E4M3_MAX = 448.0
 _FP8 = getattr(torch, "float8_e4m3fn", None)
@@ -97,7 +98,7 @@ def fp8_linear(x, weight, bias=None, cache=None):
                 weight._pa_fp8_cache = cache
             except Exception:  # noqa: BLE001
                 pass
-    return _FP8LinearFn.apply(x, weight, bias, cache)
+    return _tape.apply(_FP8LinearFn, x, weight, bias, cache)
 
 
 # ---------------------------------------------------------------- native fp8 GEMM

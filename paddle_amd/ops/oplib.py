@@ -309,8 +309,8 @@ def gru_step(g, h, W, D):
     if not (_ENABLED and g.is_cuda and g.dtype == torch.float32 and h.dtype == torch.float32):
         return None
     ur = g[:, :2 * D] + h @ W[:, :2 * D]
-    u, r, rh = _GruGateFn.apply(ur, h)
-    hn, c = _GruOutFn.apply(g[:, 2 * D:] + rh @ W[:, 2 * D:], u, h)
+    u, r, rh = _tape.apply(_GruGateFn, ur, h)
+    hn, c = _tape.apply(_GruOutFn, g[:, 2 * D:] + rh @ W[:, 2 * D:], u, h)
     return hn, u, r, c, rh
 
 
@@ -373,7 +373,7 @@ def ew(op, x, y):
     if any(b != a and b != 1 for a, b in zip(x.shape, y.shape)):
         return None
     if op in ("add", "sub", "mul", "div") and (x.requires_grad or y.requires_grad):
-        return _BinaryFn.apply(op, x, y)
+        return _tape.apply(_BinaryFn, op, x, y)
     if x.requires_grad or y.requires_grad:
         return None  # max / min / pow gradients stay on the torch reference
     return binary(op, x, y)
@@ -403,7 +403,7 @@ def reduce_op(op, x, dims, keep_dim=False):
     if x.requires_grad:
         if op not in ("sum", "mean"):
             return None
-        return _ReduceFn.apply(op, x, list(dims), keep_dim)
+        return _tape.apply(_ReduceFn, op, x, list(dims), keep_dim)
     return reduce(op, x, dims, keep_dim)
 
 
@@ -426,7 +426,7 @@ class _TopkFn(torch.autograd.Function):
 def topk_op(x, k):
     if not _ok(x) or x.dim() == 0 or k <= 0 or k > 64 or k > x.shape[-1]:
         return None
-    return _TopkFn.apply(x, k)
+    return _tape.apply(_TopkFn, x, k)
 
 
 class _SeqPoolFn(torch.autograd.Function):
@@ -447,7 +447,7 @@ def seq_pool_op(x, offsets, pooltype):
     """-> (out, maxindex int32) or None."""
     if not _ok(x) or pooltype.upper() not in _POOL or x.dim() == 0:
         return None
-    return _SeqPoolFn.apply(x, list(offsets), pooltype)
+    return _tape.apply(_SeqPoolFn, x, list(offsets), pooltype)
 
 
 class _GatherRowsFn(torch.autograd.Function):
@@ -469,7 +469,7 @@ def gather_rows_op(src, idx, fill=0.0):
         return None
     idx = torch.as_tensor(np.asarray(idx, dtype=np.int32)).to(src.device) if not torch.is_tensor(idx) \
         else idx.to(device=src.device, dtype=torch.int32)
-    return _GatherRowsFn.apply(src, idx, float(fill))
+    return _tape.apply(_GatherRowsFn, src, idx, float(fill))
 
 
 class _DropoutFn(torch.autograd.Function):
@@ -491,7 +491,7 @@ def dropout_op(x, p, seed=None, upscale=False):
     """-> (out, uint8 mask) on the Philox kernel, or None."""
     if not _ok(x):
         return None
-    return _DropoutFn.apply(x, float(p), seed, bool(upscale))
+    return _tape.apply(_DropoutFn, x, float(p), seed, bool(upscale))
 
 
 # ------------------------------------------------------------------ misc Fluid kernels (misc.hip)

@@ -14,6 +14,7 @@ from __future__ import annotations
 import torch
 
 from . import _native as N
+from ..autograd import tape as _tape  # noqa: E402
 
 _SUPPORTED_H = (128, 256, 512, 1024)
 
@@ -118,7 +119,7 @@ def lstm(x, w_ih, w_hh, b=None, h0=None, c0=None, lens=None, time_major=True, re
     if not persistent_ok(x, H, B):
         hs, h, c, cs = _lstm_ref(x, w_ih, w_hh, b, h0, c0, lens, cells=True)
     else:
-        hs, h, c, cs = _LstmFn.apply(x.contiguous(), _lens_dev(lens, T, B, x.device), w_ih, w_hh, b, h0, c0)
+        hs, h, c, cs = _tape.apply(_LstmFn, x.contiguous(), _lens_dev(lens, T, B, x.device), w_ih, w_hh, b, h0, c0)
     if not time_major:
         hs, cs = hs.transpose(0, 1), cs.transpose(0, 1)
     return (hs, h, c, cs) if return_cells else (hs, h, c)
@@ -257,7 +258,7 @@ def attention_lstm_decoder(enc, ep, lens, Y, h0, c0, Wsp, w, Wg):
     A = ep.shape[2]
     if enc.is_cuda and A % 512 == 0 and E % 1024 == 0 and (Ts + 32 * A) * 4 <= 160 * 1024 and \
             (Ts + 4 * E) * 4 <= 160 * 1024:
-        return _AttnDecoderFn.apply(enc, ep, lens.to(device=enc.device, dtype=torch.int32), Y, h0, c0, Wsp, w, Wg)
+        return _tape.apply(_AttnDecoderFn, enc, ep, lens.to(device=enc.device, dtype=torch.int32), Y, h0, c0, Wsp, w, Wg)
     return _attn_decoder_ref(enc, ep, lens, Y, h0, c0, Wsp, w, Wg)
 
 

@@ -1,12 +1,11 @@
 """``paddle.*`` tensor functions (creation, math, manipulation, logic, search,
-random, linalg) with Paddle 2.x signatures over PyTorch-ROCm tensors.
+random, linalg) with Paddle 2.x signatures.
 
-DyGraph tensors ARE torch tensors on the HIP device: the autograd tape is torch's,
-and every function here is a thin signature adapter (``axis``/``keepdim``/
-``num_or_sections``/``perm`` ...) so user code written for Paddle runs unchanged.
-Paddle-only Tensor conveniences (``astype``, ``stop_gradient``, ``place``,
-``clear_gradient``, ``gradient``) are installed on ``torch.Tensor`` by
-:func:`install_tensor_methods`.
+Every tensor these functions return is the framework's ``paddle.Tensor``
+(``autograd/engine.py``): storage and kernels are the PyTorch-ROCm tensor it
+wraps, gradients come from the framework's own eager engine (explicit backward
+rules, no torch autograd).  The functions map Paddle's signatures (``axis`` /
+``keepdim`` / ``num_or_sections`` / ``perm`` ...) onto the kernels.
 """
 from __future__ import annotations
 
@@ -16,9 +15,10 @@ import math
 import numpy as np
 import torch
 
+from .autograd import engine as _eager
 from .nn.layer import _to_torch_dtype
 
-Tensor = torch.Tensor
+Tensor = _eager.Tensor
 
 _DT = {"float32": torch.float32, "float64": torch.float64, "float16": torch.float16, "bfloat16": torch.bfloat16,
        "int64": torch.int64, "int32": torch.int32, "int16": torch.int16, "int8": torch.int8, "uint8": torch.uint8,
@@ -90,10 +90,9 @@ def to_tensor(data, dtype=None, place=None, stop_gradient=True):
         t = torch.from_numpy(np.ascontiguousarray(arr)) if arr.dtype != object else torch.tensor(data)
     if dt is None and t.dtype == torch.float64 and not isinstance(data, (np.ndarray, torch.Tensor)):
         dt = _default_dtype[0]
-    t = t.to(device=_dev(place), dtype=dt or t.dtype)
-    if not stop_gradient:
-        t.requires_grad_(True)
-    return t
+    with torch._C.DisableTorchFunctionSubclass():
+        t = t.to(device=_dev(place), dtype=dt or t.dtype)
+    return _eager.to_tensor_handle(t, stop_gradient=stop_gradient)
 
 
 def _shape(s):
@@ -848,62 +847,35 @@ def t(x, name=None):
     return x.t() if x.dim() == 2 else x
 
 
-def no_grad(func=None):
-    if func is None:
-        return torch.no_grad()
-    return torch.no_grad()(func)
-
-
-def enable_grad():
-    return torch.enable_grad()
-
-
-def set_grad_enabled(mode):
-    return torch.set_grad_enabled(mode)
-
-
-def is_grad_enabled():
-    return torch.is_grad_enabled()
+no_grad = _eager.no_grad
+enable_grad = _eager.enable_grad
+set_grad_enabled = _eager.set_grad_enabled
+is_grad_enabled = _eager.is_grad_enabled
 
 
 def grad(outputs, inputs, grad_outputs=None, retain_graph=None, create_graph=False, only_inputs=True,
          allow_unused=False, no_grad_vars=None):
+    """``paddle.grad`` on the framework engine (raw torch tensors: torch autograd)."""
     outs = outputs if isinstance(outputs, (list, tuple)) else [outputs]
     ins = inputs if isinstance(inputs, (list, tuple)) else [inputs]
+    if builtins.any(isinstance(t, Tensor) for t in list(outs) + list(ins)):
+        r = _eager.grad(list(outs), list(ins), grad_outputs, retain_graph, create_graph, allow_unused)
+        return r if isinstance(r, list) else [r]
     return list(torch.autograd.grad(outs, ins, grad_outputs, retain_graph, create_graph, allow_unused=allow_unused))
 
 
 # --------------------------------------------------------- Tensor method patches
-def install_tensor_methods():
-    T = torch.Tensor
-    if getattr(T, "_pa_patched", False):
-        return
+def _wrap_module_functions():
+    import types
 
-    def astype(self, dtype):
-        return self.to(_dtype(dtype))
+    g = globals()
+    for name, fn in list(g.items()):
+        if name.startswith("_") or not isinstance(fn, types.FunctionType) or fn.__module__ != __name__:
+            continue
+        if name in ("no_grad", "enable_grad", "set_grad_enabled", "is_grad_enabled",
+                    "set_default_dtype", "get_default_dtype", "set_device", "get_device", "seed", "grad"):
+            continue
+        g[name] = _eager.wraps_outputs(fn)
 
-    def _sg_get(self):
-        return not self.requires_grad
 
-    def _sg_set(self, v):
-        if self.is_leaf or not v:
-            self.requires_grad_(not v)
-
-    def clear_gradient(self, set_to_zero=True):
-        if self.grad is not None:
-            if set_to_zero:
-                self.grad.zero_()
-            else:
-                self.grad = None
-
-    def gradient(self):
-        return None if self.grad is None else self.grad.detach().cpu().numpy()
-
-    T.astype = astype
-    T.stop_gradient = property(_sg_get, _sg_set)
-    T.clear_gradient = clear_gradient
-    T.clear_grad = clear_gradient
-    T.gradient = gradient
-    T.place = property(lambda self: str(self.device).replace("cuda", "gpu"))
-    T.ndimension = T.dim
-    T._pa_patched = True
+_wrap_module_functions()

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Two rocprofv3 PMC passes over benchmarks/gemm_dw_probe.py (K-major vs MN-major dW GEMM)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+A="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"
+B="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC"
+for pass in A B; do
+  eval cs=\$$pass
+  out=/tmp/dwpmc_$pass
+  timeout -s KILL 120 rocprofv3 --pmc $cs -d $out -o run -- python3 $R/benchmarks/gemm_dw_probe.py > $R/gpurun_out/dw_pmc_$pass.log 2>&1 || { echo "pass $pass failed"; tail -5 $R/gpurun_out/dw_pmc_$pass.log; exit 1; }
+  db=$(find $out -name "*_results.db" | head -1)
+  python3 $R/tools/rocpd_pmc.py $db gemm > $R/gpurun_out/dw_pmc_$pass.txt || exit 1
+done
+echo all-passes-ok
