@@ -355,6 +355,10 @@ def _dispatch_inplace(func, outofplace, args, kwargs):
         torch._C._set_grad_enabled(prev)
     node = res.__dict__.get("_pa_node") if isinstance(res, torch.Tensor) else None
     if node is not None:
+        if not isinstance(tgt, Tensor):
+            # a raw torch tensor written in place from a tracked value becomes a framework
+            # Tensor (same object), so later ops on it are still recorded
+            tgt.__class__ = Tensor
         tgt.__dict__["_pa_node"] = node
         tgt.__dict__["_pa_idx"] = res.__dict__["_pa_idx"]
     else:

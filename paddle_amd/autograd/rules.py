@@ -665,15 +665,12 @@ def _getitem(out, a, idx, **kw):
         return (a, idx), bwd
 
     def bwd_adv(g):
-        z = torch.zeros_like(a, dtype=g.dtype)
-        items = idx if isinstance(idx, tuple) else (idx,)
-        if len(items) == 1 and _is_t(items[0]) and items[0].dtype == torch.bool:
-            z[items[0]] = g
-            return (z, None)
-        if len(items) == 1 and _is_t(items[0]):
-            return (z.index_add_(0, items[0].reshape(-1).long(), g.reshape(-1, *a.shape[1:])), None)
-        z.index_put_(tuple(i if _is_t(i) else torch.tensor(i) for i in items), g, accumulate=True)
-        return (z, None)
+        # any advanced / mixed index: the flat positions the index selects, then one
+        # index_add (duplicates accumulate)
+        pos = torch.arange(a.numel(), device=a.device).reshape(a.shape)[idx]
+        z = torch.zeros(a.numel(), dtype=g.dtype, device=g.device)
+        z.index_add_(0, pos.reshape(-1), g.reshape(-1))
+        return (z.reshape(a.shape), None)
 
     return (a, idx), bwd_adv
 

@@ -27,6 +27,7 @@ from dataclasses import dataclass, field
 
 import torch
 
+from ..autograd import engine as _eager
 from . import core
 from .proto import AttrType
 
@@ -373,13 +374,13 @@ def run_kernel_stash(info: OpInfo, ctx: KernelContext):
             n = names[i] if i < len(names) else None
             if isinstance(v, core.LoDTensor) and v.tensor is not None and v.tensor.is_floating_point() \
                     and n not in inplace:
-                t = v.tensor.detach().requires_grad_(True)
+                t = _eager.to_tensor_handle(v.tensor.detach(), stop_gradient=False)
                 leaves[(s.name, i)] = t
                 new.append(core.LoDTensor(t, v.lod()))
             else:
                 new.append(v)
         ctx.ins[s.name] = new
-    with torch.enable_grad():
+    with torch.enable_grad(), _eager.enable_grad():
         call_kernel(info, ctx)
     if info.share_lod:
         _default_share_lod(info, ctx)
@@ -387,9 +388,9 @@ def run_kernel_stash(info: OpInfo, ctx: KernelContext):
     for slot, vals in ctx.results.items():
         for i, r in enumerate(vals):
             rt = r.tensor if isinstance(r, core.LoDTensor) else r
-            if isinstance(rt, torch.Tensor) and rt.requires_grad:
+            if isinstance(rt, torch.Tensor) and _eager.tracked(rt):
                 graph_outs[(slot, i)] = rt
-                d = rt.detach()
+                d = _eager._raw(rt).detach()
                 vals[i] = core.LoDTensor(d, r.lod()) if isinstance(r, core.LoDTensor) else d
     if graph_outs and leaves:
         entry = (leaves, graph_outs)
@@ -428,11 +429,18 @@ def _stashed_vjp(fwd: OpInfo, ctx: KernelContext):
         outs.append(rt)
         gouts.append(gt.to(rt.dtype).reshape(rt.shape))
     keys = list(leaves.keys())
-    if outs and keys:
-        grads = torch.autograd.grad(outs, [leaves[k] for k in keys], gouts, allow_unused=True)
-    else:
-        grads = [None] * len(keys)
+    grads = _engine_vjp(outs, [leaves[k] for k in keys], gouts)
     return dict(zip(keys, grads))
+
+
+def _engine_vjp(outs, leaves, gouts):
+    """VJP on the framework's eager engine (explicit per-op backward rules and the
+    fused ops' own backward kernels; autograd/engine.py) -- not torch autograd."""
+    if not outs or not leaves:
+        return [None] * len(leaves)
+    r = _eager.grad(outs, leaves, [_eager._raw(g) for g in gouts], retain_graph=False, allow_unused=True)
+    r = r if isinstance(r, list) else [r]
+    return [None if g is None else _eager._raw(g) for g in r]
 
 
 def auto_grad_kernel(fwd: OpInfo, ctx: KernelContext):
@@ -450,7 +458,7 @@ def auto_grad_kernel(fwd: OpInfo, ctx: KernelContext):
         vals = []
         for i, v in enumerate(ctx.input_values(s.name)):
             if isinstance(v, core.LoDTensor) and v.tensor is not None and v.tensor.is_floating_point():
-                t = v.tensor.detach().requires_grad_(True)
+                t = _eager.to_tensor_handle(v.tensor.detach(), stop_gradient=False)
                 leaves[(s.name, i)] = t
                 vals.append(core.LoDTensor(t, v.lod()))
             else:
@@ -458,7 +466,7 @@ def auto_grad_kernel(fwd: OpInfo, ctx: KernelContext):
         fins[s.name] = vals
     fctx = KernelContext(fwd.type, fins, {s.name: [f"{s.name}#{k}" for k in range(max(1, len(ctx.input_values(s.name))))]
                                           for s in fwd.outputs}, ctx.attrs, ctx.place)
-    with torch.enable_grad():
+    with torch.enable_grad(), _eager.enable_grad():
         call_kernel(fwd, fctx)
     outs, gouts = [], []
     for s in fwd.outputs:
@@ -470,15 +478,12 @@ def auto_grad_kernel(fwd: OpInfo, ctx: KernelContext):
             rt = r.tensor if isinstance(r, core.LoDTensor) else r
             g = gvals[i]
             gt = g.tensor if isinstance(g, core.LoDTensor) else g
-            if gt is None or not isinstance(rt, torch.Tensor) or not rt.requires_grad:
+            if gt is None or not isinstance(rt, torch.Tensor) or not _eager.tracked(rt):
                 continue
             outs.append(rt)
             gouts.append(gt.to(rt.dtype).reshape(rt.shape))
     keys = list(leaves.keys())
-    if outs and keys:
-        grads = torch.autograd.grad(outs, [leaves[k] for k in keys], gouts, allow_unused=True)
-    else:
-        grads = [None] * len(keys)
+    grads = _engine_vjp(outs, [leaves[k] for k in keys], gouts)
     _write_input_grads(fwd, ctx, dict(zip(keys, grads)))
 
 
@@ -494,7 +499,7 @@ def _write_input_grads(fwd, ctx, gmap):
                 if src is None:
                     continue
                 g = torch.zeros_like(src)
-            ctx.set_output(slot, g.detach(), v.lod() if isinstance(v, core.LoDTensor) else None, i)
+            ctx.set_output(slot, _eager._raw(g).detach(), v.lod() if isinstance(v, core.LoDTensor) else None, i)
 
 
 # ---------------------------------------------------------------- compile-time shape inference

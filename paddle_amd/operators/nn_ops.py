@@ -15,6 +15,8 @@ channel-first kernels of csrc/kernels/convnd.hip (ops/convnd.py).
 from __future__ import annotations
 
 import torch
+
+from ..autograd import engine as _eager
 import torch.nn.functional as F
 
 from .. import ops as K
@@ -74,12 +76,14 @@ def conv2d_grad(ctx):
     st, pd, dl, g = (tuple(ctx.attr("strides")), tuple(ctx.attr("paddings")), tuple(ctx.attr("dilations")),
                      ctx.attr("groups") or 1)
     if _cnd.supported_conv(x, w, g) and dy.is_cuda:
-        xs = x.detach().requires_grad_(ctx.has_output("Input@GRAD"))
-        ws = w.detach().requires_grad_(ctx.has_output("Filter@GRAD"))
-        with torch.enable_grad():
+        # the HIP conv's own backward kernels through one eager-engine node
+        xs = _eager.to_tensor_handle(x.detach(), stop_gradient=not ctx.has_output("Input@GRAD"))
+        ws = _eager.to_tensor_handle(w.detach(), stop_gradient=not ctx.has_output("Filter@GRAD"))
+        with _eager.enable_grad():
             y = _cnd.conv_nd(xs, ws, None, st, pd, dl, g)
-            want = [t for t in (xs, ws) if t.requires_grad]
-            grads = torch.autograd.grad(y, want, dy) if want else []
+            want = [t for t in (xs, ws) if not t.stop_gradient]
+            grads = _eager.grad([y], want, [dy]) if want else []
+        grads = [_eager._raw(t) for t in (grads if isinstance(grads, list) else [grads])]
         it = iter(grads)
         if ctx.has_output("Input@GRAD"):
             ctx.set_output("Input@GRAD", next(it))

@@ -19,6 +19,8 @@ Decoding / metric ops are host-side integer algorithms, as in the reference.
 from __future__ import annotations
 
 import torch
+
+from ..autograd import tape as _tape
 import torch.nn.functional as F
 
 from ..framework import core
@@ -194,7 +196,7 @@ def warpctc(ctx):
     tgt = lab.reshape(-1).long()
     loss = F.ctc_loss(logp, tgt, xl, ll, blank=blank, reduction="none", zero_infinity=True)
     if norm:
-        loss = _GradScale.apply(loss, 1.0 / xl.clamp(min=1).to(loss.dtype))
+        loss = _tape.apply(_GradScale, loss, 1.0 / xl.clamp(min=1).to(loss.dtype))
     ctx.set_output("Loss", loss.unsqueeze(1).to(x.dtype))
     ctx.set_output("WarpCTCGrad", torch.zeros_like(x))
 

@@ -273,3 +273,36 @@ def test_framework_tensor_is_returned_by_paddle_api():
         assert isinstance(t, paddle.Tensor), type(t)
     assert paddle.to_tensor([1.0, 2.0]).astype("float64").dtype == torch.float64
     assert paddle.to_tensor([1.0]).place == "cpu"
+
+
+def test_fluid_lenet_trains_without_torch_autograd():
+    """Fluid static-graph LeNet: the grad ops' kernels differentiate the forward
+    kernels on the eager engine (framework/registry.py auto_grad_kernel), never on
+    torch autograd."""
+    import paddle_amd.fluid as fluid
+
+    main, startup = fluid.Program(), fluid.Program()
+    main.random_seed = startup.random_seed = 7
+    with fluid.program_guard(main, startup):
+        img = fluid.layers.data(name="img", shape=[1, 28, 28], dtype="float32")
+        lab = fluid.layers.data(name="lab", shape=[1], dtype="int64")
+        c1 = fluid.nets.simple_img_conv_pool(img, num_filters=8, filter_size=5, pool_size=2, pool_stride=2,
+                                             act="relu")
+        c2 = fluid.nets.simple_img_conv_pool(c1, num_filters=16, filter_size=5, pool_size=2, pool_stride=2,
+                                             act="relu")
+        pred = fluid.layers.fc(c2, size=10, act="softmax")
+        loss = fluid.layers.mean(fluid.layers.cross_entropy(pred, lab))
+        fluid.optimizer.Adam(learning_rate=6e-3).minimize(loss)
+    ds = paddle.vision.datasets.MNIST(mode="train", num_samples=256)
+    xs = np.stack([np.asarray(ds[i][0], dtype=np.float32).reshape(1, 28, 28) for i in range(256)])
+    ys = np.array([int(np.asarray(ds[i][1]).reshape(-1)[0]) for i in range(256)], dtype=np.int64).reshape(-1, 1)
+    exe = fluid.Executor(fluid.CPUPlace())
+    scope = fluid.core.Scope()
+    losses = []
+    with fluid.executor.scope_guard(scope), no_torch_autograd():
+        exe.run(startup)
+        for ep in range(5):
+            for b in range(0, 256, 64):
+                out, = exe.run(main, feed={"img": xs[b:b + 64], "lab": ys[b:b + 64]}, fetch_list=[loss])
+                losses.append(float(np.asarray(out).reshape(-1)[0]))
+    assert losses[-1] < losses[0] * 0.7, losses
