@@ -92,6 +92,16 @@ class Tape:
 
     def apply(self, fn, *args):
         handles = [self._handle(a) for a in args]
+        for a, h in zip(args, handles):
+            # a parameter reached this op through an op the tape did not record (a
+            # view such as w.t(), or any plain torch op): its gradient would be lost
+            if h is None and isinstance(a, torch.Tensor) and a.is_floating_point():
+                base = a._base
+                if base is not None and (base.requires_grad or getattr(base, "_pa_tape", (None,))[0] == id(self)):
+                    raise RuntimeError(
+                        f"tape: an input of {getattr(fn, '__name__', fn)} is a view of a parameter or recorded "
+                        "activation taken outside the tape; its gradient would be dropped. Use a fused op "
+                        "(e.g. ops.linear_t for x @ W^T) instead of the plain torch view.")
         ctx = _Ctx(tuple(h is not None for h in handles))
         with torch.no_grad():
             outs = fn.forward(ctx, *args)

@@ -174,9 +174,9 @@ class GPTForCausalLM(Layer):
         if self.tp:
             from ..distributed.fleet.mp_layers import parallel_cross_entropy
 
-            logits = torch.matmul(self.tp.copy_to_region(y), w.t())
+            logits = ops.linear_t(self.tp.copy_to_region(y), w)
             return logits if labels is None else parallel_cross_entropy(logits, labels, self.tp.group)
-        logits = torch.matmul(y, w.t())
+        logits = ops.linear_t(y, w)
         if labels is None:
             return logits
         return ops.softmax_cross_entropy(logits, labels, inplace_grad=True)
@@ -237,7 +237,7 @@ class GPTHeadPipe(Layer):
 
 
 def _tied_head(emb, y):
-    return torch.matmul(y, emb.word_embeddings.t())
+    return ops.linear_t(y, emb.word_embeddings)
 
 
 class GPTPretrainingCriterion:

@@ -187,7 +187,7 @@ class LlamaForCausalLM(Layer):
         if self.lm_head is not None:
             logits = ops.linear(y, self.lm_head)
         else:
-            logits = torch.matmul(y, self.embed_tokens.t())
+            logits = ops.linear_t(y, self.embed_tokens)
         if labels is None:
             return logits
         # in-place CE gradient over the logits buffer (nothing else consumes it)

@@ -966,3 +966,70 @@ def linear(x, weight, bias=None):
     if bias is not None:
         param_ready(bias)
     return _tape.apply(_LinearFn, x, weight, bias)
+
+
+# ====================================================================== tied head
+class _LinearTFn(torch.autograd.Function):
+    """y = x W^T with W stored [out, in] (a tied embedding table used as the LM head).
+
+    GPU: the hand-written GEMM in all three forms (forward both K-major; dX with W
+    MN-major; dW = dY^T X with both operands MN-major, into the fp32 main_grad when
+    the table has one).  A vocabulary that is not a multiple of 8 (GPT's 50,257) is
+    computed into an 8-aligned output buffer: the GEMM covers the first V - V % 8
+    columns, a thin product the last V % 8, then the buffer is trimmed."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        V, H = w.shape
+        x2 = x.reshape(-1, H)
+        if _G.supported(x2.shape[0], 8, H, x2, w) and V >= 8:
+            V8, Vp = V // 8 * 8, (V + 7) // 8 * 8
+            if Vp == V:
+                return _G.gemm(x2, w, x2.shape[0], V, H, a_kmaj=True, b_kmaj=True).view(*x.shape[:-1], V)
+            # 8-aligned rows of the output buffer; the last V % 8 columns by a thin product
+            buf = torch.empty(x2.shape[0], Vp, dtype=x.dtype, device=x.device)
+            _G.gemm(x2, w[:V8], x2.shape[0], V8, H, a_kmaj=True, b_kmaj=True, out=buf, ldc=Vp)
+            buf[:, V8:V] = torch.matmul(x2, w[V8:].t())
+            return buf[:, :V].contiguous().view(*x.shape[:-1], V)
+        return torch.matmul(x, w.t())
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        V, H = w.shape
+        x2 = x.reshape(-1, H)
+        dy2 = _c(dy).reshape(-1, V)
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        mg = getattr(w, "_pa_main_grad", None)
+        if V % 8 == 0 and _G.supported(x2.shape[0], H, V, x2, w, dy2):
+            dx = _G.gemm(dy2, w, x2.shape[0], H, V, a_kmaj=True, b_kmaj=False).view(x.shape) if need_x else None
+            dw = None
+            if need_w:
+                if mg is not None:
+                    fresh = getattr(w, "_pa_grad_fresh", False)
+                    w._pa_grad_fresh = False
+                    _G.gemm(dy2, x2, V, H, x2.shape[0], a_kmaj=False, b_kmaj=False, out=mg, accumulate=not fresh)
+                else:
+                    dw = _G.gemm(dy2, x2, V, H, x2.shape[0], a_kmaj=False, b_kmaj=False,
+                                 out_dtype=torch.float32).to(w.dtype)
+            return dx, dw
+        dx = torch.matmul(dy2, w).view(x.shape) if need_x else None
+        dw = None
+        if need_w:
+            g = torch.matmul(dy2.t().to(torch.float32) if mg is not None else dy2.t(), x2.to(
+                torch.float32) if mg is not None else x2)
+            if mg is not None:
+                if getattr(w, "_pa_grad_fresh", False):
+                    mg.zero_()
+                    w._pa_grad_fresh = False
+                mg.add_(g)
+            else:
+                dw = g.to(w.dtype)
+        return dx, dw
+
+
+def linear_t(x, weight):
+    """x @ weight^T for a [out, in] weight (tied LM heads), as one fused tape op."""
+    param_ready(weight)
+    return _tape.apply(_LinearTFn, x, weight)
