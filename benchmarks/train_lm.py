@@ -6,6 +6,8 @@
   python benchmarks/train_lm.py --model gpt3-13b --seq-len 2048 --micro-batch 1 --recompute
   python benchmarks/train_lm.py --model ernie-moe-21b-a3b --fp8-experts
   torchrun --nproc-per-node 8 benchmarks/train_lm.py --model gpt3-13b   # dp8 + ZeRO-1 (flat sharded AdamW)
+  python benchmarks/train_lm.py --model gpt3-13b --gpus 8 --tp 2 --pp 2 --sharding 2 --sharding-stage 3
+      # BASELINE config 4: Fleet hybrid TP x PP (1F1B) x sharding stage 3; self-launches 8 ranks
 
 Synthetic token ids, random-init weights, bf16, fused flat sharded AdamW.
 """
@@ -57,7 +59,30 @@ def main():
     ap.add_argument("--bucket-mb", type=int, default=512)
     ap.add_argument("--accum", type=int, default=1, help="gradient accumulation micro-steps per optimizer step")
     ap.add_argument("--bf16-grads", action="store_true", help="bf16 gradient buffer instead of fp32 main_grad")
-    a = ap.parse_args()
+    ap.add_argument("--gpus", type=int, default=0, help="self-launch this many ranks (torch.distributed.run)")
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (Fleet mp_degree)")
+    ap.add_argument("--pp", type=int, default=1, help="pipeline-parallel degree (1F1B)")
+    ap.add_argument("--sharding", type=int, default=1, help="sharding degree")
+    ap.add_argument("--sharding-stage", type=int, default=3)
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"], help="cpu: gloo rehearsal (tiny models)")
+    ap.add_argument("--layers", type=int, default=None, help="debug: override layer count (result INVALID)")
+    argv = sys.argv[1:]
+    a = ap.parse_args(argv)
+    if a.gpus and "WORLD_SIZE" not in os.environ:
+        import socket
+        import subprocess
+
+        sck = socket.socket()
+        sck.bind(("127.0.0.1", 0))
+        port = sck.getsockname()[1]
+        sck.close()
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        sys.exit(subprocess.call([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                                  f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1", "--master-port",
+                                  str(port), os.path.abspath(__file__)] + argv, env=env))
+    if a.tp > 1 or a.pp > 1 or a.sharding > 1:
+        return hybrid_main(a)
 
     from paddle_amd.parallel import comm
     from paddle_amd.parallel.sharding import FlatShardedOptimizer
@@ -114,6 +139,87 @@ def main():
                                      "grad_dtype": str(opt.grad_dtype), "dw_kmajor": os.environ.get("PADDLE_AMD_DW_KMAJ", "1"), "parallelism": f"dp{world}+sharding_stage1"},
                           "loss": float(loss) * a.accum,
                           "losses": [round(float(x) * a.accum, 4) for x in hist]}))
+
+
+def hybrid_main(a):
+    """Fleet hybrid parallel GPT: fleet.init -> PipelineLayer of TP blocks ->
+    fleet.distributed_model (1F1B pipeline, ZeRO-3 units on the sharding axis) ->
+    fleet.distributed_optimizer; timing contract of bench.py."""
+    import paddle_amd
+    from paddle_amd.distributed.fleet import DistributedStrategy, TPGroup, fleet
+    from paddle_amd.distributed.fleet.pipeline import PipelineLayer
+    from paddle_amd.models.gpt import GPT_CONFIGS, GPTConfig, GPTPretrainingCriterion, gpt_flops_per_token, \
+        gpt_pipeline_descs
+    from paddle_amd.parallel import comm
+
+    if not a.model.startswith("gpt"):
+        raise SystemExit("hybrid mode drives the GPT family (BASELINE config 4)")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    dp = world // (a.tp * a.pp * a.sharding)
+    if dp < 1 or dp * a.tp * a.pp * a.sharding != world:
+        raise SystemExit(f"world {world} != tp {a.tp} x pp {a.pp} x sharding {a.sharding} x dp")
+    cpu = a.device == "cpu"
+    st = DistributedStrategy()
+    st.hybrid_configs = {"dp_degree": dp, "mp_degree": a.tp, "pp_degree": a.pp, "sharding_degree": a.sharding}
+    st.sharding = a.sharding > 1
+    st.sharding_configs = {"stage": a.sharding_stage}
+    st.pipeline_configs = {"accumulate_steps": max(a.accum, a.pp), "micro_batch_size": a.micro_batch}
+    if cpu:
+        comm.init_parallel_env("gloo")
+    fleet.init(is_collective=True, strategy=st)
+    hcg = fleet.get_hybrid_communicate_group()
+    rank = comm.get_rank()
+    if cpu:
+        dev = torch.device("cpu")
+    else:
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        dev = torch.device("cuda", torch.cuda.current_device())
+    torch.manual_seed(1234)
+    cfgd = dict(GPT_CONFIGS[a.model])
+    if a.layers:
+        cfgd["num_hidden_layers"] = a.layers
+    cfgd["max_position_embeddings"] = max(cfgd.get("max_position_embeddings", 2048), a.seq_len)
+    if cpu:
+        cfgd["dtype"] = "float32"
+    cfg = GPTConfig(**cfgd, recompute=a.recompute)
+    tp = TPGroup(hcg.get_model_parallel_group())
+    layer = PipelineLayer(gpt_pipeline_descs(cfg, dev, tp), hcg=hcg, loss_fn=GPTPretrainingCriterion(tp), seed=7)
+    model = fleet.distributed_model(layer)
+    inner = paddle_amd.optimizer.AdamW(learning_rate=1e-4, parameters=list(layer.parameters()), weight_decay=0.1,
+                                       grad_clip=paddle_amd.optimizer.clip.ClipGradByGlobalNorm(1.0))
+    opt = fleet.distributed_optimizer(inner)
+    M = st.pipeline_configs["accumulate_steps"]
+    gen = torch.Generator(device="cpu").manual_seed(hcg.get_data_parallel_rank() * 131 + hcg.get_sharding_parallel_rank())
+    ids = torch.randint(0, cfg.vocab_size, (M * a.micro_batch, a.seq_len + 1), generator=gen).to(dev)
+    sync = (lambda: None) if cpu else torch.cuda.synchronize
+
+    def step():
+        return model.train_batch((ids[:, :-1], ids[:, 1:]), opt)
+
+    hist = [float(step()) for _ in range(a.warmup)]
+    comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    sync()
+    comm.barrier()
+    dt = torch.tensor([time.perf_counter() - t0], device=dev if not cpu else "cpu")
+    if world > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    sec = dt.item() / max(a.steps, 1)
+    tok = M * a.micro_batch * a.seq_len * dp * a.sharding / sec
+    if rank == 0:
+        fpt = gpt_flops_per_token(cfg, a.seq_len)
+        print(json.dumps({"metric": f"tokens/sec (whole job) {a.model} Fleet hybrid parallel", "value": round(tok, 1),
+                          "unit": "tokens/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                          "ms_per_step": round(1000 * sec, 2), "dtype": "float32" if cpu else "bf16",
+                          "data": "synthetic", "mfu_bf16_dense": round(tok * fpt / world / 2.5e15, 4),
+                          "config": {"model": a.model + (f"(DEBUG {a.layers} layers: INVALID)" if a.layers else ""),
+                                     "parallelism": f"tp{a.tp}xpp{a.pp}xsharding{a.sharding}(stage{a.sharding_stage})"
+                                                    f"xdp{dp}", "micro_batch": a.micro_batch,
+                                     "accumulate_steps": M, "seq_len": a.seq_len, "device": a.device},
+                          "loss": float(loss), "losses": [round(x, 4) for x in hist]}), flush=True)
 
 
 if __name__ == "__main__":

@@ -103,23 +103,47 @@ class _Fleet:
             raise RuntimeError("call fleet.init first")
         from .pipeline import PipelineLayer, PipelineParallel
 
+        st = self._strategy
+        stage3 = (hcg.get_sharding_parallel_world_size() > 1 and bool(getattr(st, "sharding", False))
+                  and int((getattr(st, "sharding_configs", None) or {}).get("stage", 1)) == 3)
         if hcg.get_pipe_parallel_world_size() > 1:
             if not isinstance(model, PipelineLayer):
                 raise TypeError("pp_degree > 1 needs a PipelineLayer model")
-            return PipelineParallel(model, hcg, self._strategy)
-        if hcg.get_model_parallel_world_size() > 1:
-            return TensorParallel(model, hcg, self._strategy)
-        if hcg.get_data_parallel_world_size() > 1 and hcg.get_sharding_parallel_world_size() == 1:
+            wrapped = PipelineParallel(model, hcg, st)
+        elif hcg.get_model_parallel_world_size() > 1:
+            wrapped = TensorParallel(model, hcg, st)
+        elif hcg.get_data_parallel_world_size() > 1 and hcg.get_sharding_parallel_world_size() == 1:
             from ..parallel import DataParallel
 
-            return DataParallel(model, group=hcg.get_data_parallel_group(),
-                                bucket_mb=self._strategy.fuse_grad_size_in_MB)
-        return model
+            return DataParallel(model, group=hcg.get_data_parallel_group(), bucket_mb=st.fuse_grad_size_in_MB)
+        else:
+            wrapped = model
+        if stage3:
+            # ZeRO-3 on the sharding axis INSIDE the pipeline stage / TP shard: every
+            # block of this stage becomes a gather-on-use unit; tied weights shared
+            # with another stage stay whole (their gradients are summed across the
+            # stages by the pipeline) and are counted in the norm on their first stage
+            from ..sharding import ShardedStage3
+
+            shared, skip = [], []
+            if isinstance(model, PipelineLayer):
+                for key, p in model.shared.items():
+                    shared.append(p)
+                    if min(model.shared_stages.get(key, {hcg.get_stage_id()})) != hcg.get_stage_id():
+                        skip.append(p)
+            dp_g = hcg.get_data_parallel_group() if hcg.get_data_parallel_world_size() > 1 else None
+            wrapped._sharded = ShardedStage3(
+                model, group=hcg.get_sharding_parallel_group(),
+                mp_group=hcg.get_model_parallel_group() if hcg.get_model_parallel_world_size() > 1 else None,
+                pp_group=hcg.get_pipe_parallel_group() if hcg.get_pipe_parallel_world_size() > 1 else None,
+                dp_group=dp_g, exclude=shared, norm_skip=skip)
+            self._sharded = wrapped._sharded
+        return wrapped
 
     def distributed_optimizer(self, optimizer, strategy=None):
         if strategy is not None:
             self._strategy = strategy
-        return HybridParallelOptimizer(optimizer, self._hcg, self._strategy)
+        return HybridParallelOptimizer(optimizer, self._hcg, self._strategy, sharded=getattr(self, "_sharded", None))
 
     # ---- checkpoint helpers (rank-0 writes the dp replica)
     def save_persistables(self, executor=None, dirname=None, main_program=None):
@@ -142,7 +166,7 @@ class TensorParallel(torch.nn.Module):
         src = hcg.get_model_parallel_group_src_rank()
         with torch.no_grad():
             for p in layers.parameters():
-                if not getattr(p, "is_distributed", False):
+                if not (getattr(p, "is_distributed", False) is True):
                     comm.broadcast(p.data, src=src, group=g)
 
     def forward(self, *a, **k):
@@ -150,11 +174,35 @@ class TensorParallel(torch.nn.Module):
 
 
 class HybridParallelOptimizer:
-    def __init__(self, optimizer, hcg, strategy):
+    """Steps the user's optimizer under hybrid parallelism.
+
+    * ZeRO-3 (``sharded`` engine from fleet.distributed_model): the engine owns the
+      AdamW state of its shards; the user optimizer's lr / betas / eps / weight decay
+      / global-norm clip are handed to it, and only whole (excluded, tied) parameters
+      are all-reduced here over dp x sharding before the step.
+    * otherwise: bucketed all-reduce of the gradients over the dp x sharding group
+      (``fuse_grad_size_in_MB`` buckets in fp32), global-norm clipping over mp / pp,
+      then the user optimizer."""
+
+    def __init__(self, optimizer, hcg, strategy, sharded=None):
         self._inner = optimizer
         self.hcg = hcg
         self.strategy = strategy
         self.grad_clip = getattr(optimizer, "_grad_clip", None) or getattr(optimizer, "grad_clip", None)
+        self._sharded = sharded
+        if sharded is not None:
+            max_norm = getattr(self.grad_clip, "clip_norm", self.grad_clip if isinstance(
+                self.grad_clip, (int, float)) else None)
+            sharded.grad_clip = max_norm
+            b1 = getattr(optimizer, "_beta1", None)
+            b2 = getattr(optimizer, "_beta2", None)
+            if b1 is not None and b2 is not None:
+                sharded.betas = (float(b1), float(b2))
+            if getattr(optimizer, "_epsilon", None) is not None:
+                sharded.eps = float(optimizer._epsilon)
+            wd = getattr(optimizer, "_weight_decay", None)
+            if isinstance(wd, (int, float)):
+                sharded.wd = float(wd)
 
     def __getattr__(self, k):
         return getattr(self._inner, k)
@@ -166,18 +214,27 @@ class HybridParallelOptimizer:
 
     @torch.no_grad()
     def _dp_sync(self, params):
+        """Bucketed fp32 all-reduce over dp x sharding (buckets of fuse_grad_size_in_MB)."""
         hcg = self.hcg
         W = hcg.get_dp_sharding_world_size() if hcg else 1
         ps = [p for p in params if p.grad is not None]
         if W <= 1 or not ps:
             return
-        flat = torch.cat([p.grad.reshape(-1).float() for p in ps])
-        comm.all_reduce(flat, group=hcg.get_dp_sharding_group())
-        flat /= W
-        o = 0
-        for p in ps:
-            p.grad.copy_(flat[o:o + p.numel()].view_as(p.grad))
-            o += p.numel()
+        limit = int(getattr(self.strategy, "fuse_grad_size_in_MB", 64) or 64) * 2**20 // 4
+        group = hcg.get_dp_sharding_group()
+        bucket, n = [], 0
+        for i, p in enumerate(ps):
+            bucket.append(p)
+            n += p.numel()
+            if n >= limit or i == len(ps) - 1:
+                flat = torch.cat([q.grad.reshape(-1).float() for q in bucket])
+                comm.all_reduce(flat, group=group)
+                flat /= W
+                o = 0
+                for q in bucket:
+                    q.grad.copy_(flat[o:o + q.numel()].view_as(q.grad))
+                    o += q.numel()
+                bucket, n = [], 0
 
     @torch.no_grad()
     def global_grad_norm(self, params):
@@ -191,7 +248,7 @@ class HybridParallelOptimizer:
             if p.grad is None:
                 continue
             s = p.grad.float().pow(2).sum()
-            if getattr(p, "is_distributed", False):
+            if (getattr(p, "is_distributed", False) is True):
                 dist_sq += s
             else:
                 rep_sq += s
@@ -203,6 +260,13 @@ class HybridParallelOptimizer:
         return tot.sqrt()
 
     def step(self):
+        if self._sharded is not None:
+            eng = self._sharded
+            # whole (tied) parameters: average over every data-parallel replica
+            self._dp_sync(eng.excluded)
+            lr = self._inner.get_lr() if hasattr(self._inner, "get_lr") else None
+            eng.step(lr=lr)
+            return
         params = self._params()
         from .pipeline import PipelineParallel  # noqa: F401  (pipeline syncs dp itself)
 
@@ -219,6 +283,9 @@ class HybridParallelOptimizer:
         self._inner.step()
 
     def clear_grad(self, set_to_zero=False):
+        if self._sharded is not None:
+            self._sharded.zero_grad()
+            return
         if hasattr(self._inner, "clear_grad"):
             return self._inner.clear_grad()
         return self._inner.zero_grad(set_to_none=not set_to_zero)

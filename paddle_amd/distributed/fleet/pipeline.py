@@ -26,6 +26,7 @@ import math
 import torch
 import torch.distributed as dist
 
+from ...autograd import engine as _eager
 from ...nn import Layer
 from ...parallel import comm
 
@@ -207,6 +208,21 @@ def _as_tuple(x):
     return x if isinstance(x, tuple) else (x,)
 
 
+def _needs_grad(t):
+    return t.requires_grad or _eager.tracked(t)
+
+
+def _backward(outs, grads):
+    """Reverse pass of one micro-batch: the framework's eager engine for framework
+    Tensors (DyGraph layers), torch autograd for raw torch tensors."""
+    if not outs:
+        return
+    if any(isinstance(o, _eager.Tensor) and _eager.tracked(o) for o in outs):
+        _eager.backward(outs, grads)
+    else:
+        torch.autograd.backward(outs, [g for g in grads] if any(g is not None for g in grads) else None)
+
+
 class PipelineParallel(Layer):
     def __init__(self, layers: PipelineLayer, hcg, strategy=None):
         super().__init__("pipeline_parallel")
@@ -259,7 +275,10 @@ class PipelineParallel(Layer):
 
     def _sync_grads(self):
         dp_group = self.hcg.get_data_parallel_group()
-        W = self.hcg.get_data_parallel_world_size()
+        # ZeRO-3 on the stage (fleet.distributed_model): sharded gradients were
+        # reduce-scattered during backward; whole (tied) ones are averaged by the
+        # HybridParallelOptimizer over dp x sharding
+        W = 1 if getattr(self, "_sharded", None) is not None else self.hcg.get_data_parallel_world_size()
         params = [p for p in self._layers.parameters() if p.requires_grad and p.grad is not None]
         if W > 1 and params:
             flat = torch.cat([p.grad.reshape(-1).float() for p in params])
@@ -305,12 +324,12 @@ class PipelineParallel(Layer):
             x = inputs_q.pop(0)
             out = outputs_q.pop(0)
             if self.is_last:
-                out.backward()
+                _backward([out], [None])
             else:
                 # the next stage returns one gradient per FLOATING activation, in order
                 outs = [o for o in _as_tuple(out) if o.is_floating_point()]
-                pairs = [(o, g) for o, g in zip(outs, grads) if o.requires_grad]
-                torch.autograd.backward([o for o, _ in pairs], [g for _, g in pairs])
+                pairs = [(o, g) for o, g in zip(outs, grads) if _needs_grad(o)]
+                _backward([o for o, _ in pairs], [g for _, g in pairs])
             return tuple(t.grad if (t.is_floating_point() and t.grad is not None) else torch.zeros_like(t)
                          for t in x if t.is_floating_point()) if not self.is_first else None
 

@@ -87,6 +87,14 @@ class _Unit:
         self.v = torch.zeros_like(self.master)
         self.g_shard = torch.zeros_like(self.master)
         self.local_decay_end = min(max(self.decay_end - lo, 0), self.S)
+        # which shard elements belong to tensor-parallel (mp-sharded) parameters: their
+        # squares are summed across mp ranks for the global norm, the rest counted once
+        dm = torch.zeros(self.N, dtype=torch.float32, device=self.device)
+        for p, o in zip(self.params, offs):
+            if (getattr(p, "is_distributed", False) is True):
+                dm[o:o + p.numel()] = 1.0
+        self.dist_mask = dm[lo:lo + self.S].clone()
+        self.has_dist = bool(self.dist_mask.any())
         self.nbytes = self.flat.untyped_storage().nbytes()
         self.gathered = True
         self.ready = set()
@@ -130,8 +138,23 @@ class ShardedStage3:
     identical on every rank at construction (same seed, or broadcast first)."""
 
     def __init__(self, model, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.0, group=None,
-                 grad_clip=None, no_decay_fn=None):
+                 grad_clip=None, no_decay_fn=None, *, mp_group=None, pp_group=None, dp_group=None, exclude=(),
+                 norm_skip=()):
+        """Composition with hybrid parallelism (fleet.distributed_model):
+        ``group`` is the sharding axis; ``dp_group`` an extra data-parallel axis whose
+        gradient shards are all-reduced before the step; ``mp_group`` / ``pp_group``
+        complete the global gradient norm (TP-sharded parameters summed over mp,
+        stages summed over pp); ``exclude``: parameters kept whole (tied weights shared
+        between pipeline stages; their gradients are synced by the caller) and updated
+        here with their own fp32 AdamW state; ``norm_skip``: excluded parameters
+        counted on another stage."""
         self.model, self.group = model, group
+        self.mp_group, self.pp_group, self.dp_group = mp_group, pp_group, dp_group
+        self.dpW = comm.get_world_size(dp_group) if dp_group is not None else 1
+        self.excluded = list(exclude)
+        ex_ids = {id(p) for p in self.excluded}
+        self.norm_skip = {id(p) for p in norm_skip}
+        self.ex_state = {}
         self.W, self.r = comm.get_world_size(group), comm.get_rank(group)
         self.lr, self.betas, self.eps, self.wd, self.grad_clip = lr, betas, eps, weight_decay, grad_clip
         self.step_count = 0
@@ -147,7 +170,7 @@ class ShardedStage3:
                         owner.setdefault(full, (f"{mname}.{i}", child))
         groups: dict = {}
         for n, p in named.items():
-            if not p.requires_grad:
+            if not p.requires_grad or id(p) in ex_ids:
                 continue
             key, mod = owner.get(n, ("<root>", model))
             groups.setdefault(key, (mod, []))[1].append((n, p))
@@ -197,19 +220,36 @@ class ShardedStage3:
     def step(self, lr=None):
         for u in self.units:  # units with unused parameters never completed their hook
             u.reduce_grads()
+        if self.dp_group is not None and self.dpW > 1:
+            for u in self.units:
+                comm.all_reduce(u.g_shard, group=self.dp_group)
         self.step_count += 1
         lr = self.lr if lr is None else lr
-        scale = 1.0 / self.W
+        scale = 1.0 / (self.W * self.dpW)
+        dev = self.units[0].device if self.units else self.excluded[0].device
+        clip = None
         if self.grad_clip:
-            ss = torch.zeros(1, dtype=torch.float32, device=self.units[0].device)
+            # squares of the AVERAGED gradient: (scale * g_shard)^2
+            sq = torch.zeros(2, dtype=torch.float32, device=dev)  # [tp-sharded, replicated]
             for u in self.units:
-                fused_optim.sumsq(u.g_shard, ss)
-            comm.all_reduce(ss, group=self.group)
-            norm = ss.sqrt() * scale
-            clip = torch.clamp(self.grad_clip / (norm + 1e-6), max=1.0)
+                g2 = u.g_shard.pow(2)
+                d = (g2 * u.dist_mask).sum() if u.has_dist else torch.zeros((), device=dev)
+                sq[0] += d * scale * scale
+                sq[1] += (g2.sum() - d) * scale * scale
+            comm.all_reduce(sq, group=self.group)
+            for p in self.excluded:  # whole, already averaged and identical on the sharding ranks
+                if p.grad is None or id(p) in self.norm_skip:
+                    continue
+                sq[0 if (getattr(p, "is_distributed", False) is True) else 1] += p.grad.float().pow(2).sum()
+            if self.mp_group is not None and comm.get_world_size(self.mp_group) > 1:
+                comm.all_reduce(sq[:1], group=self.mp_group)
+            tot = sq.sum().reshape(1)
+            if self.pp_group is not None and comm.get_world_size(self.pp_group) > 1:
+                comm.all_reduce(tot, group=self.pp_group)
+            clip = torch.clamp(self.grad_clip / (tot.sqrt() + 1e-6), max=1.0)
         for u in self.units:
             g = u.g_shard
-            if self.grad_clip:
+            if clip is not None:
                 g.mul_(clip * scale)
                 gs = 1.0
             else:
@@ -218,12 +258,31 @@ class ShardedStage3:
                                    eps=self.eps, weight_decay=self.wd, step=self.step_count,
                                    param_out=u.p_shard, decay_end=u.local_decay_end, grad_scale=gs)
             g.zero_()
+        for p in self.excluded:
+            if p.grad is None:
+                continue
+            st = self.ex_state.get(id(p))
+            if st is None:
+                m0 = p.detach().float().reshape(-1).clone()
+                st = self.ex_state[id(p)] = (m0, torch.zeros_like(m0), torch.zeros_like(m0))
+            master, m, v = st
+            g = p.grad.float().reshape(-1)
+            if clip is not None:
+                g = g * clip
+            out = p.data.view(-1) if p.is_contiguous() else None
+            fused_optim.adamw_flat(master, g, m, v, lr=lr, beta1=self.betas[0], beta2=self.betas[1], eps=self.eps,
+                                   weight_decay=0.0 if _no_decay("", p) else self.wd, step=self.step_count,
+                                   param_out=out)
+            if out is None:
+                p.data.copy_(master.view_as(p))
 
     def zero_grad(self):
         for u in self.units:
             u.g_shard.zero_()
             for p in u.params:
                 p.grad = None
+        for p in self.excluded:
+            p.grad = None
 
     clear_grad = zero_grad
 
