@@ -388,6 +388,8 @@ def record_function(fn, args):
         outs = [out] if single else list(out)
 
         def bwd(*gouts):
+            # hand-written backward kernels index their gradient inputs densely
+            gouts = [g.contiguous() if isinstance(g, torch.Tensor) else g for g in gouts]
             r = fn.backward(ctx, *gouts)
             return r if isinstance(r, tuple) else (r,)
 

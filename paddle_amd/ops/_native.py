@@ -215,8 +215,14 @@ def stream():
 
 
 def ptr(t):
+    """Device pointer of ``t`` for a kernel-library call.  A host tensor here would be
+    dereferenced by a HIP kernel (an illegal-address fault that takes the GPU down):
+    refuse it on the host instead (pinned host buffers are device-accessible)."""
     if t is None:
         return None
+    if not t.is_cuda and t.numel() > 0 and not t.is_pinned():
+        raise RuntimeError(f"paddle_amd kernel argument is a host tensor ({tuple(t.shape)}, {t.dtype}); "
+                           "every operand of a GPU op must live on the device")
     return _P(t.data_ptr())
 
 

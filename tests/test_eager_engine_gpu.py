@@ -21,6 +21,7 @@ def test_lenet_dygraph_gpu_trains_without_torch_autograd():
     paddle.set_device("gpu")
     try:
         model = paddle.vision.models.LeNet()
+        model.to("cuda")
         opt = paddle.optimizer.Adam(learning_rate=2e-3, parameters=model.parameters())
         ds = paddle.vision.datasets.MNIST(mode="train", num_samples=384)
         first = last = None
