@@ -3,6 +3,7 @@ today, on the LLaMA-7B shapes (T = 16384 tokens), interleaved in one process:
   dw_kk : dW = (X^T)(dY^T)^T on two HIP-transposed copies, both K-major (times
           INCLUDE the two transposes: this is the production path)
   dw_mn : dW = X^T dY straight from the stored layouts, both MN-major (tr_b16 reads)
+  dw_tx / dw_tdy: one operand transposed (x or dY) + the mixed form (times include it)
   fwd_kk: y = x W via the cached K-major W^T        fwd_kn: B = W MN-major
 each MN form under both schedules (pa_gemm_set_sched 0 / 1)."""
 import json
@@ -40,6 +41,10 @@ for name, (K, Nn) in SHAPES.items():
     forms = {
         "dw_kk": (-1, lambda: G.gemm(transpose2d(x), transpose2d(dy), K, Nn, T, a_kmaj=True, b_kmaj=True, out=mg,
                                      accumulate=True)),
+        "dw_tx": (-1, lambda: G.gemm(transpose2d(x), dy, K, Nn, T, a_kmaj=True, b_kmaj=False, out=mg,
+                                     accumulate=True)),
+        "dw_tdy": (-1, lambda: G.gemm(x, transpose2d(dy), K, Nn, T, a_kmaj=False, b_kmaj=True, out=mg,
+                                      accumulate=True)),
         "dw_mn_s0": (0, lambda: G.linear_dw(x, dy, out=mg, accumulate=True)),
         "dw_mn_s1": (1, lambda: G.linear_dw(x, dy, out=mg, accumulate=True)),
         "fwd_kk": (-1, lambda: G.gemm(x, wt, T, Nn, K, a_kmaj=True, b_kmaj=True)),

@@ -706,7 +706,7 @@ def transpose2d(x):
 # dW = X^T dY through the K-inner ("NT") GEMM form on transposed copies; see
 # csrc/kernels/transpose.hip for why.  Off on CPU (no effect on numerics).
 _DW_VIA_TRANSPOSE = True
-_DW_KMAJ = os.environ.get("PADDLE_AMD_DW_KMAJ", "1") == "1"
+_DW_KMAJ = os.environ.get("PADDLE_AMD_DW_KMAJ", "0") == "1"  # MN x MN dW = transposes + K x K (profiles/r3_dw_mn_vs_kmajor_bench_ab.txt); no transposed copies
 
 
 def _dw_nt_ok(x2, dy2):
@@ -852,6 +852,12 @@ def _linear_bwd(ctx, x, w, dy, need_dx, need_dw):
                     # far more than the two transposes cost
                     _G.gemm(transpose2d(_c(x2)), transpose2d(dy2), K, Nn, x2.shape[0], a_kmaj=True, b_kmaj=True,
                             out=mg, accumulate=not fresh)
+                elif side is None and x2.shape[0] >= 1024 and Nn >= 2 * K:
+                    # dY much wider than X (qkv, gate_up): transpose only X and run the
+                    # mixed form -- 3-8 % under the both-MN-major form at these shapes
+                    # (profiles/r3_gemm_dw_forms.jsonl), the transpose included
+                    _G.gemm(transpose2d(_c(x2)), dy2, K, Nn, x2.shape[0], a_kmaj=True, b_kmaj=False, out=mg,
+                            accumulate=not fresh)
                 elif side is None:
                     _G.linear_dw(x2, dy2, out=mg, accumulate=not fresh)
                 else:
