@@ -13,11 +13,13 @@ from __future__ import annotations
 import math
 
 import torch
+
 import torch.nn.functional as F
 
 from ..framework import core
 from ..framework.registry import register_op
 from ..ops import blas as _blas
+from ..ops import fluidk as _fk
 from ..ops import oplib as _oplib
 
 # ------------------------------------------------------------------ mul / matmul
@@ -229,61 +231,106 @@ _ew_grad("elementwise_div", lambda x, y, d: d / y, lambda x, y, d: -d * x / (y *
 
 
 # ------------------------------------------------------------------ activations
+# name -> (attrs, (a, b) from attrs, forward f(x, a, b), derivative df(x, y, a, b))
+# GPU: one templated HIP kernel pair (csrc/kernels/fluid_ops.hip, ops/fluidk.py);
+# CPU: the same formulas in torch.  Every activation has an explicit grad op
+# ``<name>_grad`` (X, Out, Out@GRAD -> X@GRAD), reference activation_op.h:877-906.
+def _sg(x):
+    return torch.sigmoid(x)
+
 
 _ACT = {
-    "relu": (lambda x, a: F.relu(x), {}),
-    "sigmoid": (lambda x, a: torch.sigmoid(x), {}),
-    "logsigmoid": (lambda x, a: F.logsigmoid(x), {}),
-    "exp": (lambda x, a: torch.exp(x), {}),
-    "tanh": (lambda x, a: torch.tanh(x), {}),
-    "tanh_shrink": (lambda x, a: x - torch.tanh(x), {}),
-    "softshrink": (lambda x, a: F.softshrink(x, a["lambda"]), {"lambda": 0.5}),
-    "sqrt": (lambda x, a: torch.sqrt(x), {}),
-    "rsqrt": (lambda x, a: torch.rsqrt(x), {}),
-    "abs": (lambda x, a: torch.abs(x), {}),
-    "ceil": (lambda x, a: torch.ceil(x), {}),
-    "floor": (lambda x, a: torch.floor(x), {}),
-    "cos": (lambda x, a: torch.cos(x), {}),
-    "sin": (lambda x, a: torch.sin(x), {}),
-    "round": (lambda x, a: torch.round(x), {}),
-    "reciprocal": (lambda x, a: torch.reciprocal(x), {}),
-    "log": (lambda x, a: torch.log(x), {}),
-    "square": (lambda x, a: x * x, {}),
-    "softplus": (lambda x, a: F.softplus(x), {}),
-    "softsign": (lambda x, a: F.softsign(x), {}),
-    "brelu": (lambda x, a: torch.clamp(x, a["t_min"], a["t_max"]), {"t_min": 0.0, "t_max": 24.0}),
-    "leaky_relu": (lambda x, a: F.leaky_relu(x, a["alpha"]), {"alpha": 0.02}),
-    "soft_relu": (lambda x, a: torch.log1p(torch.exp(torch.clamp(x, -a["threshold"], a["threshold"]))),
-                  {"threshold": 40.0}),
-    "elu": (lambda x, a: F.elu(x, a["alpha"]), {"alpha": 1.0}),
-    "relu6": (lambda x, a: torch.clamp(x, 0.0, a["threshold"]), {"threshold": 6.0}),
-    "pow": (lambda x, a: torch.pow(x, a["factor"]), {"factor": 1.0}),
-    "stanh": (lambda x, a: a["scale_b"] * torch.tanh(a["scale_a"] * x), {"scale_a": 2.0 / 3.0, "scale_b": 1.7159}),
-    "hard_shrink": (lambda x, a: F.hardshrink(x, a["threshold"]), {"threshold": 0.5}),
-    "thresholded_relu": (lambda x, a: torch.where(x > a["threshold"], x, torch.zeros_like(x)), {"threshold": 1.0}),
-    "hard_sigmoid": (lambda x, a: torch.clamp(x * a["slope"] + a["offset"], 0.0, 1.0), {"slope": 0.2, "offset": 0.5}),
-    "swish": (lambda x, a: x * torch.sigmoid(a["beta"] * x), {"beta": 1.0}),
-    "gelu": (lambda x, a: F.gelu(x), {}),
-    "silu": (lambda x, a: F.silu(x), {}),
+    "relu": ({}, None, lambda x, a, b: F.relu(x), lambda x, y, a, b: (y > 0).to(x.dtype)),
+    "sigmoid": ({}, None, lambda x, a, b: torch.sigmoid(x), lambda x, y, a, b: y * (1 - y)),
+    "logsigmoid": ({}, None, lambda x, a, b: F.logsigmoid(x), lambda x, y, a, b: _sg(-x)),
+    "exp": ({}, None, lambda x, a, b: torch.exp(x), lambda x, y, a, b: y),
+    "tanh": ({}, None, lambda x, a, b: torch.tanh(x), lambda x, y, a, b: 1 - y * y),
+    "tanh_shrink": ({}, None, lambda x, a, b: x - torch.tanh(x), lambda x, y, a, b: torch.tanh(x) ** 2),
+    "softshrink": ({"lambda": 0.5}, ("lambda", None), lambda x, a, b: F.softshrink(x, a),
+                   lambda x, y, a, b: (x.abs() > a).to(x.dtype)),
+    "sqrt": ({}, None, lambda x, a, b: torch.sqrt(x), lambda x, y, a, b: 0.5 / y),
+    "rsqrt": ({}, None, lambda x, a, b: torch.rsqrt(x), lambda x, y, a, b: -0.5 * y * y * y),
+    "abs": ({}, None, lambda x, a, b: torch.abs(x), lambda x, y, a, b: torch.sign(x)),
+    "ceil": ({}, None, lambda x, a, b: torch.ceil(x), lambda x, y, a, b: torch.zeros_like(x)),
+    "floor": ({}, None, lambda x, a, b: torch.floor(x), lambda x, y, a, b: torch.zeros_like(x)),
+    "cos": ({}, None, lambda x, a, b: torch.cos(x), lambda x, y, a, b: -torch.sin(x)),
+    "sin": ({}, None, lambda x, a, b: torch.sin(x), lambda x, y, a, b: torch.cos(x)),
+    "round": ({}, None, lambda x, a, b: torch.round(x), lambda x, y, a, b: torch.zeros_like(x)),
+    "reciprocal": ({}, None, lambda x, a, b: torch.reciprocal(x), lambda x, y, a, b: -y * y),
+    "log": ({}, None, lambda x, a, b: torch.log(x), lambda x, y, a, b: 1 / x),
+    "square": ({}, None, lambda x, a, b: x * x, lambda x, y, a, b: 2 * x),
+    "softplus": ({}, None, lambda x, a, b: F.softplus(x), lambda x, y, a, b: _sg(x)),
+    "softsign": ({}, None, lambda x, a, b: F.softsign(x), lambda x, y, a, b: 1 / (1 + x.abs()) ** 2),
+    "brelu": ({"t_min": 0.0, "t_max": 24.0}, ("t_min", "t_max"), lambda x, a, b: torch.clamp(x, a, b),
+              lambda x, y, a, b: ((x > a) & (x < b)).to(x.dtype)),
+    "leaky_relu": ({"alpha": 0.02}, ("alpha", None), lambda x, a, b: F.leaky_relu(x, a),
+                   lambda x, y, a, b: torch.where(x > 0, torch.ones_like(x), torch.full_like(x, a))),
+    "soft_relu": ({"threshold": 40.0}, ("threshold", None),
+                  lambda x, a, b: torch.log1p(torch.exp(torch.clamp(x, -a, a))),
+                  lambda x, y, a, b: ((x > -a) & (x < a)).to(x.dtype) * (1 - torch.exp(-y))),
+    "elu": ({"alpha": 1.0}, ("alpha", None), lambda x, a, b: F.elu(x, a),
+            lambda x, y, a, b: torch.where(x > 0, torch.ones_like(x), y + a)),
+    "relu6": ({"threshold": 6.0}, ("threshold", None), lambda x, a, b: torch.clamp(x, 0.0, a),
+              lambda x, y, a, b: ((x > 0) & (x < a)).to(x.dtype)),
+    "pow": ({"factor": 1.0}, ("factor", None), lambda x, a, b: torch.pow(x, a),
+            lambda x, y, a, b: a * torch.pow(x, a - 1)),
+    "stanh": ({"scale_a": 2.0 / 3.0, "scale_b": 1.7159}, ("scale_a", "scale_b"),
+              lambda x, a, b: b * torch.tanh(a * x), lambda x, y, a, b: a * b * (1 - torch.tanh(a * x) ** 2)),
+    "hard_shrink": ({"threshold": 0.5}, ("threshold", None), lambda x, a, b: F.hardshrink(x, a),
+                    lambda x, y, a, b: (x.abs() > a).to(x.dtype)),
+    "thresholded_relu": ({"threshold": 1.0}, ("threshold", None),
+                         lambda x, a, b: torch.where(x > a, x, torch.zeros_like(x)),
+                         lambda x, y, a, b: (x > a).to(x.dtype)),
+    "hard_sigmoid": ({"slope": 0.2, "offset": 0.5}, ("slope", "offset"),
+                     lambda x, a, b: torch.clamp(x * a + b, 0.0, 1.0),
+                     lambda x, y, a, b: (((x * a + b) > 0) & ((x * a + b) < 1)).to(x.dtype) * a),
+    "swish": ({"beta": 1.0}, ("beta", None), lambda x, a, b: x * torch.sigmoid(a * x),
+              lambda x, y, a, b: _sg(a * x) + a * x * _sg(a * x) * (1 - _sg(a * x))),
+    "gelu": ({}, None, lambda x, a, b: F.gelu(x),
+             lambda x, y, a, b: 0.5 * (1 + torch.erf(x / math.sqrt(2.0))) + x * torch.exp(-0.5 * x * x) /
+             math.sqrt(2 * math.pi)),
+    "silu": ({}, None, lambda x, a, b: F.silu(x), lambda x, y, a, b: _sg(x) * (1 + x * (1 - _sg(x)))),
 }
 
 
-def _make_act(name, fn, attrs):
+def _act_ab(ctx, keys):
+    if keys is None:
+        return 0.0, 0.0
+    ka, kb = keys
+    return float(ctx.attr(ka)) if ka else 0.0, float(ctx.attr(kb)) if kb else 0.0
+
+
+def _make_act(name, attrs, keys, fwd, dfn):
     @register_op(name, ["X"], ["Out"], dict(attrs, use_mkldnn=False, use_cudnn=False, is_test=False))
     def k(ctx):
-        ctx.set_output("Out", fn(ctx.input("X"), ctx.attrs))
+        x = ctx.input("X")
+        a, b = _act_ab(ctx, keys)
+        if _fk.ok(x) and not ctx.meta:
+            ctx.set_output("Out", _fk.act_fwd(name, x, a, b))
+        else:
+            ctx.set_output("Out", fwd(x, a, b))
+
+    @register_op(name + "_grad", ["X?", "Out?", "Out@GRAD"], ["X@GRAD"], dict(attrs), grad=None, no_infer=True)
+    def kg(ctx):
+        d = ctx.input("Out@GRAD")
+        x = ctx.input("X") if ctx.has_input("X") else None
+        y = ctx.input("Out") if ctx.has_input("Out") else None
+        a, b = _act_ab(ctx, keys)
+        if _fk.ok(d) and not ctx.meta:
+            ctx.set_output("X@GRAD", _fk.act_bwd(name, d, x, y, a, b))
+            return
+        if y is None:
+            y = fwd(x, a, b)
+        if x is None:
+            x = torch.zeros_like(y)
+        ctx.set_output("X@GRAD", d * dfn(x, y, a, b).to(d.dtype))
 
     k.__name__ = name
+    kg.__name__ = name + "_grad"
 
 
-for _n, (_f, _a) in _ACT.items():
-    _make_act(_n, _f, _a)
-
-
-@register_op("relu_grad", ["X", "Out", "Out@GRAD"], ["X@GRAD"], {}, grad=None, no_infer=True)
-def relu_grad(ctx):
-    out, d = ctx.input("Out"), ctx.input("Out@GRAD")
-    ctx.set_output("X@GRAD", torch.where(out > 0, d, torch.zeros_like(d)))
+for _n, (_a, _k, _f, _d) in _ACT.items():
+    _make_act(_n, _a, _k, _f, _d)
 
 
 @register_op("prelu", ["X", "Alpha"], ["Out"], {"mode": "all"})

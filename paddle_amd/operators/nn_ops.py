@@ -7,8 +7,11 @@ hinge_loss,huber_loss,log_loss,margin_rank_loss,rank_loss,modified_huber_loss,
 smooth_l1_loss,label_smooth,bilinear_interp,pad,pad2d,crop,im2sequence,spp,unpool,
 roi_pool}_op.* (SURVEY §2.7).
 
-On the HIP device, layer_norm / softmax / softmax_with_cross_entropy /
-lookup_table go through the hand-written gfx950 kernels (paddle_amd.ops); conv /
+On the HIP device, layer_norm / softmax / lookup_table go through the hand-written
+gfx950 kernels (paddle_amd.ops); softmax_with_cross_entropy (Softmax + Loss in one
+row pass, grad from the Softmax output) and the pointwise losses (hinge, huber,
+log, modified huber, sigmoid CE; explicit grad ops) through csrc/kernels/
+fluid_ops.hip (ops/fluidk.py); conv /
 conv_transpose (2-D, 3-D, grouped) and pool / pool_with_index / unpool run on the
 channel-first kernels of csrc/kernels/convnd.hip (ops/convnd.py).
 """
@@ -17,6 +20,7 @@ from __future__ import annotations
 import torch
 
 from ..autograd import engine as _eager
+from ..ops import fluidk as _fk
 import torch.nn.functional as F
 
 from .. import ops as K
@@ -410,6 +414,13 @@ def cross_entropy(ctx):
              {"soft_label": False, "ignore_index": -100, "numeric_stable_mode": True, "axis": -1})
 def softmax_with_cross_entropy(ctx):
     x, lab = ctx.input("Logits"), ctx.input("Label")
+    if _fk.ok(x) and not ctx.meta and ctx.attr("axis") in (-1, x.dim() - 1):
+        # one HIP block per row: online max / sum, then probabilities + row loss
+        soft = ctx.attr("soft_label")
+        prob, loss = _fk.softmax_ce(x, None if soft else lab, lab if soft else None, ctx.attr("ignore_index"))
+        ctx.set_output("Softmax", prob)
+        ctx.set_output("Loss", loss)
+        return
     logp = torch.log_softmax(x.float(), -1)
     if ctx.attr("soft_label"):
         loss = -(lab.float() * logp).sum(-1, keepdim=True)
@@ -427,6 +438,11 @@ def softmax_with_cross_entropy(ctx):
              grad=None, no_infer=True)
 def softmax_with_cross_entropy_grad(ctx):
     p, lab, d = ctx.input("Softmax"), ctx.input("Label"), ctx.input("Loss@GRAD")
+    if _fk.ok(p, d) and not ctx.meta and ctx.attr("axis") in (-1, p.dim() - 1):
+        soft = ctx.attr("soft_label")
+        ctx.set_output("Logits@GRAD", _fk.softmax_ce_grad(p, d, None if soft else lab, lab if soft else None,
+                                                          ctx.attr("ignore_index")))
+        return
     if ctx.attr("soft_label"):
         g = (p - lab.to(p.dtype)) * d
     else:
@@ -450,9 +466,23 @@ _REG["softmax_with_cross_entropy"].grad_maker = _swce_grad_maker
 @register_op("sigmoid_cross_entropy_with_logits", ["X", "Label"], ["Out"], {"ignore_index": -100})
 def sigmoid_ce(ctx):
     x, lab = ctx.input("X"), ctx.input("Label")
-    out = F.binary_cross_entropy_with_logits(x, lab.to(x.dtype), reduction="none")
+    if _fk.ok(x) and not ctx.meta:
+        out = _fk.loss_fwd("sigmoid_cross_entropy_with_logits", x, lab)[0]
+    else:
+        out = F.binary_cross_entropy_with_logits(x, lab.to(x.dtype), reduction="none")
     out = torch.where(lab == ctx.attr("ignore_index"), torch.zeros_like(out), out)
     ctx.set_output("Out", out)
+
+
+@register_op("sigmoid_cross_entropy_with_logits_grad", ["X", "Label", "Out?", "Out@GRAD"], ["X@GRAD", "Label@GRAD?"],
+             {"ignore_index": -100}, grad=None, no_infer=True)
+def sigmoid_ce_grad(ctx):
+    x, lab, g = ctx.input("X"), ctx.input("Label"), ctx.input("Out@GRAD")
+    if _fk.ok(x, g) and not ctx.meta:
+        gx = _fk.loss_bwd("sigmoid_cross_entropy_with_logits", x, lab, g)
+    else:
+        gx = g * (torch.sigmoid(x) - lab.to(x.dtype))
+    ctx.set_output("X@GRAD", torch.where(lab == ctx.attr("ignore_index"), torch.zeros_like(gx), gx))
 
 
 @register_op("bpr_loss", ["X", "Label"], ["Y"], {})
@@ -468,12 +498,31 @@ def bpr_loss(ctx):
 @register_op("hinge_loss", ["Logits", "Labels"], ["Loss"], {})
 def hinge_loss(ctx):
     x, y = ctx.input("Logits"), ctx.input("Labels")
+    if _fk.ok(x) and not ctx.meta:
+        ctx.set_output("Loss", _fk.loss_fwd("hinge_loss", x, y)[0])
+        return
     ctx.set_output("Loss", F.relu(1 - x * (2 * y - 1)))
+
+
+@register_op("hinge_loss_grad", ["Logits", "Labels", "Loss?", "Loss@GRAD"], ["Logits@GRAD", "Labels@GRAD?"], {},
+             grad=None, no_infer=True)
+def hinge_loss_grad(ctx):
+    x, y, g = ctx.input("Logits"), ctx.input("Labels"), ctx.input("Loss@GRAD")
+    if _fk.ok(x, g) and not ctx.meta:
+        ctx.set_output("Logits@GRAD", _fk.loss_bwd("hinge_loss", x, y, g))
+        return
+    s = 2 * y.to(x.dtype) - 1
+    ctx.set_output("Logits@GRAD", g * torch.where(x * s < 1, -s, torch.zeros_like(s)))
 
 
 @register_op("huber_loss", ["X", "Y"], ["Residual~", "Out"], {"delta": 1.0})
 def huber_loss(ctx):
     x, y = ctx.input("X"), ctx.input("Y")
+    if _fk.ok(x) and not ctx.meta:
+        out, res = _fk.loss_fwd("huber_loss", x, y, ctx.attr("delta"), want_res=True)
+        ctx.set_output("Residual", res)
+        ctx.set_output("Out", out)
+        return
     r = y - x
     d = ctx.attr("delta")
     a = r.abs()
@@ -481,11 +530,40 @@ def huber_loss(ctx):
     ctx.set_output("Out", torch.where(a <= d, 0.5 * r * r, d * (a - 0.5 * d)))
 
 
+@register_op("huber_loss_grad", ["X", "Y", "Residual", "Out?", "Out@GRAD"], ["X@GRAD", "Y@GRAD?"], {"delta": 1.0},
+             grad=None, no_infer=True)
+def huber_loss_grad(ctx):
+    x, y, r, g = ctx.input("X"), ctx.input("Y"), ctx.input("Residual"), ctx.input("Out@GRAD")
+    d = ctx.attr("delta")
+    if _fk.ok(x, g) and not ctx.meta:
+        gx = _fk.loss_bwd("huber_loss", x, y, g, res=r, a=d)
+    else:
+        gx = g * torch.where(r.abs() <= d, -r, torch.where(r > 0, torch.full_like(r, -d), torch.full_like(r, d)))
+    ctx.set_output("X@GRAD", gx)
+    if ctx.has_output("Y@GRAD"):
+        ctx.set_output("Y@GRAD", -gx)
+
+
 @register_op("log_loss", ["Predicted", "Labels"], ["Loss"], {"epsilon": 1e-4})
 def log_loss(ctx):
     p, y = ctx.input("Predicted"), ctx.input("Labels")
     e = ctx.attr("epsilon")
+    if _fk.ok(p) and not ctx.meta:
+        ctx.set_output("Loss", _fk.loss_fwd("log_loss", p, y, e)[0])
+        return
     ctx.set_output("Loss", -y * torch.log(p + e) - (1 - y) * torch.log(1 - p + e))
+
+
+@register_op("log_loss_grad", ["Predicted", "Labels", "Loss?", "Loss@GRAD"], ["Predicted@GRAD", "Labels@GRAD?"],
+             {"epsilon": 1e-4}, grad=None, no_infer=True)
+def log_loss_grad(ctx):
+    p, y, g = ctx.input("Predicted"), ctx.input("Labels"), ctx.input("Loss@GRAD")
+    e = ctx.attr("epsilon")
+    if _fk.ok(p, g) and not ctx.meta:
+        ctx.set_output("Predicted@GRAD", _fk.loss_bwd("log_loss", p, y, g, a=e))
+        return
+    y = y.to(p.dtype)
+    ctx.set_output("Predicted@GRAD", g * (-y / (p + e) + (1 - y) / (1 - p + e)))
 
 
 @register_op("margin_rank_loss", ["X1", "X2", "Label"], ["Out", "Activated~"], {"margin": 0.0})
@@ -506,9 +584,26 @@ def rank_loss(ctx):
 @register_op("modified_huber_loss", ["X", "Y"], ["IntermediateVal~", "Out"], {})
 def modified_huber_loss(ctx):
     x, y = ctx.input("X"), ctx.input("Y")
+    if _fk.ok(x) and not ctx.meta:
+        out, z = _fk.loss_fwd("modified_huber_loss", x, y, want_res=True)
+        ctx.set_output("IntermediateVal", z)
+        ctx.set_output("Out", out)
+        return
     z = x * (2 * y - 1)
     ctx.set_output("IntermediateVal", z)
     ctx.set_output("Out", torch.where(z < -1, -4 * z, torch.where(z < 1, (1 - z) ** 2, torch.zeros_like(z))))
+
+
+@register_op("modified_huber_loss_grad", ["X", "Y", "IntermediateVal", "Out?", "Out@GRAD"], ["X@GRAD", "Y@GRAD?"],
+             {}, grad=None, no_infer=True)
+def modified_huber_loss_grad(ctx):
+    x, y, z, g = ctx.input("X"), ctx.input("Y"), ctx.input("IntermediateVal"), ctx.input("Out@GRAD")
+    if _fk.ok(x, g) and not ctx.meta:
+        ctx.set_output("X@GRAD", _fk.loss_bwd("modified_huber_loss", x, y, g, res=z))
+        return
+    s = 2 * y.to(x.dtype) - 1
+    ctx.set_output("X@GRAD", g * torch.where(z < -1, -4 * s, torch.where(z < 1, -2 * (1 - z) * s,
+                                                                          torch.zeros_like(z))))
 
 
 @register_op("smooth_l1_loss", ["X", "Y", "InsideWeight?", "OutsideWeight?"], ["Diff~", "Out"], {"sigma": 1.0})

@@ -16,6 +16,7 @@ import torch.nn.functional as F
 
 from ..framework import core
 from ..framework.registry import register_op
+from ..ops import fluidk as _fk
 from ..ops import oplib as _oplib
 
 
@@ -81,12 +82,31 @@ def sequence_softmax(ctx):
     if ctx.meta:
         ctx.set_output("Out", torch.empty_like(x))
         return
+    if x.is_cuda and _fk.ok(x):
+        # one wave per sequence: max / sum / normalise over the LoD segment in one pass
+        ctx.set_output("Out", _fk.seq_softmax(flat, off).reshape(x.shape), lod)
+        return
     seg, _ = _seg_ids(off, x.device)
     n = len(off) - 1
     mx = torch.full((n,), float("-inf"), dtype=x.dtype, device=x.device).scatter_reduce(0, seg, flat, "amax")
     e = torch.exp(flat - mx[seg])
     s = torch.zeros(n, dtype=x.dtype, device=x.device).index_add_(0, seg, e)
     ctx.set_output("Out", (e / s[seg]).reshape(x.shape), lod)
+
+
+@register_op("sequence_softmax_grad", ["X?", "Out", "Out@GRAD"], ["X@GRAD"], {"use_cudnn": False}, grad=None,
+             no_infer=True)
+def sequence_softmax_grad(ctx):
+    y, g = ctx.input("Out"), ctx.input("Out@GRAD")
+    lod = ctx.input_lod("Out") or ctx.input_lod("X")
+    off = lod[-1] if lod else [0, y.shape[0]]
+    if y.is_cuda and _fk.ok(y, g):
+        ctx.set_output("X@GRAD", _fk.seq_softmax_grad(y.reshape(-1), g.reshape(-1), off).reshape(y.shape))
+        return
+    seg, _ = _seg_ids(off, y.device)
+    yf, gf = y.reshape(-1), g.reshape(-1)
+    dot = torch.zeros(len(off) - 1, dtype=y.dtype, device=y.device).index_add_(0, seg, yf * gf)
+    ctx.set_output("X@GRAD", (yf * (gf - dot[seg])).reshape(y.shape))
 
 
 @register_op("sequence_expand", ["X", "Y"], ["Out"], {"ref_level": -1}, share_lod=False)

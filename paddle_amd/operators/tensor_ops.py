@@ -12,6 +12,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from ..ops import fluidk as _fk
 from ..ops import oplib as _oplib
 
 from ..framework import core
@@ -72,13 +73,38 @@ def flatten(ctx):
     ctx.set_output("Out", x.reshape(int(np.prod(x.shape[:a])) if a else 1, -1))
 
 
+def _dev(ctx, *ts):
+    """HIP path: a device place, real (not meta) run, every operand on the device."""
+    return not ctx.meta and all(t is not None and t.is_cuda for t in ts)
+
+
+def _permute(ctx, x, perm):
+    if _dev(ctx, x) and x.dim() <= 8:
+        return _fk.permute(x, perm)
+    return x.permute(*perm).contiguous()
+
+
 @register_op("transpose", ["X"], ["Out"], {"axis": [], "use_mkldnn": False, "data_format": "AnyLayout"})
 def transpose(ctx):
-    ctx.set_output("Out", ctx.input("X").permute(*ctx.attr("axis")).contiguous())
+    ctx.set_output("Out", _permute(ctx, ctx.input("X"), list(ctx.attr("axis"))))
 
 
 _reg_t2 = register_op("transpose2", ["X"], ["Out", "XShape~"], {"axis": []})(
     lambda ctx: transpose(ctx))
+
+
+def _transpose_grad(ctx):
+    perm = list(ctx.attr("axis"))
+    inv = [0] * len(perm)
+    for i, p in enumerate(perm):
+        inv[p] = i
+    ctx.set_output("X@GRAD", _permute(ctx, ctx.input("Out@GRAD"), inv))
+
+
+register_op("transpose_grad", ["X?", "Out?", "Out@GRAD"], ["X@GRAD"], {"axis": []}, grad=None,
+            no_infer=True)(_transpose_grad)
+register_op("transpose2_grad", ["X?", "Out?", "XShape?", "Out@GRAD"], ["X@GRAD"], {"axis": []}, grad=None,
+            no_infer=True)(_transpose_grad)
 
 
 @register_op("concat", ["X*"], ["Out"], {"axis": 0})
@@ -139,7 +165,22 @@ def unstack(ctx):
 
 @register_op("expand", ["X"], ["Out"], {"expand_times": []})
 def expand(ctx):
-    ctx.set_output("Out", ctx.input("X").repeat(*ctx.attr("expand_times")))
+    x, reps = ctx.input("X"), list(ctx.attr("expand_times"))
+    if _dev(ctx, x) and len(reps) == x.dim() and 2 * x.dim() <= 8:
+        ctx.set_output("Out", _fk.tile(x, reps))
+        return
+    ctx.set_output("Out", x.repeat(*reps))
+
+
+@register_op("expand_grad", ["X", "Out?", "Out@GRAD"], ["X@GRAD"], {"expand_times": []}, grad=None, no_infer=True)
+def expand_grad(ctx):
+    x, g = ctx.input("X"), ctx.input("Out@GRAD")
+    reps = list(ctx.attr("expand_times"))
+    shp = []
+    for n, r in zip(x.shape, reps):
+        shp += [r, n]
+    red = tuple(range(0, 2 * x.dim(), 2))
+    ctx.set_output("X@GRAD", g.reshape(shp).sum(red) if red else g.clone())
 
 
 @register_op("gather", ["X", "Index"], ["Out"], {})
@@ -168,17 +209,63 @@ def slice_op(ctx):
         s = max(0, s + n if s < 0 else min(s, n))
         e = max(0, e + n if e < 0 else min(e, n))
         sl[a] = slice(s, e)
+    if _dev(ctx, x) and 0 < x.dim() <= 8:
+        ctx.set_output("Out", _fk.slice_(x, list(ctx.attr("axes")), list(ctx.attr("starts")),
+                                         list(ctx.attr("ends"))))
+        return
     ctx.set_output("Out", x[tuple(sl)])
+
+
+@register_op("slice_grad", ["Input", "Out?", "Out@GRAD"], ["Input@GRAD"], {"axes": [], "starts": [], "ends": []},
+             grad=None, no_infer=True)
+def slice_grad(ctx):
+    x, g = ctx.input("Input"), ctx.input("Out@GRAD")
+    sl = [slice(None)] * x.dim()
+    for a, s, e in zip(ctx.attr("axes"), ctx.attr("starts"), ctx.attr("ends")):
+        n = x.shape[a]
+        s = max(0, s + n if s < 0 else min(s, n))
+        e = max(0, e + n if e < 0 else min(e, n))
+        sl[a] = slice(s, e)
+    gx = torch.zeros_like(x, dtype=g.dtype)
+    gx[tuple(sl)] = g
+    ctx.set_output("Input@GRAD", gx)
 
 
 @register_op("reverse", ["X"], ["Out"], {"axis": []})
 def reverse(ctx):
-    ctx.set_output("Out", torch.flip(ctx.input("X"), list(ctx.attr("axis"))))
+    x = ctx.input("X")
+    if _dev(ctx, x) and 0 < x.dim() <= 8:
+        ctx.set_output("Out", _fk.flip(x, list(ctx.attr("axis"))))
+        return
+    ctx.set_output("Out", torch.flip(x, list(ctx.attr("axis"))))
+
+
+@register_op("reverse_grad", ["X?", "Out?", "Out@GRAD"], ["X@GRAD"], {"axis": []}, grad=None, no_infer=True)
+def reverse_grad(ctx):
+    g = ctx.input("Out@GRAD")
+    if _dev(ctx, g) and 0 < g.dim() <= 8:
+        ctx.set_output("X@GRAD", _fk.flip(g, list(ctx.attr("axis"))))
+        return
+    ctx.set_output("X@GRAD", torch.flip(g, list(ctx.attr("axis"))))
+
+
+def _cast(ctx, x, dt):
+    if _dev(ctx, x):
+        return _fk.cast(x, dt)
+    return x.to(dt)
 
 
 @register_op("cast", ["X"], ["Out"], {"in_dtype": 5, "out_dtype": 5})
 def cast(ctx):
-    ctx.set_output("Out", ctx.input("X").to(core.to_torch_dtype(ctx.attr("out_dtype"))), ctx.input_lod("X"))
+    ctx.set_output("Out", _cast(ctx, ctx.input("X"), core.to_torch_dtype(ctx.attr("out_dtype"))),
+                   ctx.input_lod("X"))
+
+
+@register_op("cast_grad", ["X", "Out?", "Out@GRAD"], ["X@GRAD"], {"in_dtype": 5, "out_dtype": 5}, grad=None,
+             no_infer=True)
+def cast_grad(ctx):
+    x, g = ctx.input("X"), ctx.input("Out@GRAD")
+    ctx.set_output("X@GRAD", _cast(ctx, g, x.dtype))
 
 
 @register_op("shape", ["Input"], ["Out"], {}, grad=None)
@@ -251,11 +338,26 @@ def _gen(ctx):
     return g
 
 
+def _philox(ctx, shape, kind, a, b):
+    """Counter-based Philox4x32-10 fill on the device (csrc/kernels/fluid_ops.hip):
+    op seed when set, else a draw from the host generator (paddle.seed / torch.manual_seed)."""
+    dt = core.to_torch_dtype(ctx.attr("dtype"))
+    if ctx.meta or ctx.device.type != "cuda" or dt not in (torch.float32, torch.bfloat16):
+        return None
+    seed = int(ctx.attr("seed", 0)) or int(torch.randint(1, 2 ** 62, (1,)).item())
+    return _fk.random(shape, kind, a, b, seed, dtype=dt, device=ctx.device)
+
+
 @register_op("uniform_random", [], ["Out"], {"shape": [], "min": -1.0, "max": 1.0, "seed": 0, "dtype": 5},
              grad=None)
 def uniform_random(ctx):
     dt = core.to_torch_dtype(ctx.attr("dtype"))
-    t = torch.empty([int(s) for s in ctx.attr("shape")], dtype=torch.float32, device=ctx.device)
+    shape = [int(s) for s in ctx.attr("shape")]
+    t = _philox(ctx, shape, "uniform", ctx.attr("min"), ctx.attr("max"))
+    if t is not None:
+        ctx.set_output("Out", t)
+        return
+    t = torch.empty(shape, dtype=torch.float32, device=ctx.device)
     if not ctx.meta:
         t.uniform_(ctx.attr("min"), ctx.attr("max"), generator=_gen(ctx))
     ctx.set_output("Out", t.to(dt))
@@ -274,7 +376,12 @@ def uniform_random_bsl(ctx):
 @register_op("gaussian_random", [], ["Out"], {"shape": [], "mean": 0.0, "std": 1.0, "seed": 0, "dtype": 5,
                                               "use_mkldnn": False}, grad=None)
 def gaussian_random(ctx):
-    t = torch.empty([int(s) for s in ctx.attr("shape")], dtype=torch.float32, device=ctx.device)
+    shape = [int(s) for s in ctx.attr("shape")]
+    t = _philox(ctx, shape, "gaussian", ctx.attr("mean"), ctx.attr("std"))
+    if t is not None:
+        ctx.set_output("Out", t)
+        return
+    t = torch.empty(shape, dtype=torch.float32, device=ctx.device)
     if not ctx.meta:
         t.normal_(ctx.attr("mean"), ctx.attr("std"), generator=_gen(ctx))
     ctx.set_output("Out", t.to(core.to_torch_dtype(ctx.attr("dtype"))))

@@ -40,6 +40,17 @@ _SIGS = {
     "pa_embedding_fwd": [_I, _P, _P, _P, _L, _I, _L, _P],
     "pa_embedding_bwd": [_I, _P, _P, _P, _L, _I, _L, _P],
     "pa_cast": [_I, _I, _P, _P, _L, _P],
+    "pa_act_fwd": [_I, _I, _P, _P, _L, _F, _F, _P],
+    "pa_act_bwd": [_I, _I, _P, _P, _P, _P, _L, _F, _F, _P],
+    "pa_softmax_ce_prob_fwd": [_I, _P, _P, _P, _P, _P, _L, _I, _L, _P],
+    "pa_softmax_ce_prob_bwd": [_I, _P, _P, _P, _P, _P, _L, _I, _L, _P],
+    "pa_cast_any": [_I, _I, _P, _P, _L, _I, _P],
+    "pa_strided_gather": [_I, _P, _P, _I, _LP, _LP, _L, _P],
+    "pa_random": [_I, _P, _L, _I, _F, _F, ctypes.c_ulonglong, _P],
+    "pa_loss_fwd": [_I, _I, _P, _P, _P, _P, _L, _F, _P],
+    "pa_loss_bwd": [_I, _I, _P, _P, _P, _P, _P, _L, _L, _F, _P],
+    "pa_seq_softmax_fwd": [_I, _P, _P, _P, _L, _P],
+    "pa_seq_softmax_bwd": [_I, _P, _P, _P, _P, _L, _P],
     "pa_softmax_ce_fwd": [_I, _P, _P, _P, _P, _P, _L, _I, _L, _P],
     "pa_softmax_ce_bwd": [_I, _P, _P, _P, _P, _P, _P, _L, _I, _L, _F, _P],
     "pa_softmax_fwd": [_I, _P, _P, _L, _I, _I, _P],
