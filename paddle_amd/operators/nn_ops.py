@@ -18,16 +18,16 @@ channel-first kernels of csrc/kernels/convnd.hip (ops/convnd.py).
 from __future__ import annotations
 
 import torch
-
-from ..autograd import engine as _eager
-from ..ops import fluidk as _fk
 import torch.nn.functional as F
 
 from .. import ops as K
+from ..autograd import engine as _eager
 from ..framework import core
 from ..framework.op_kernel_type import LibraryType, register_op_kernel
 from ..framework.registry import register_op
 from ..ops import convnd as _cnd
+from ..ops import fluidk as _fk
+from ..ops import fused as _fused
 from ..ops import oplib as _oplib
 
 # ------------------------------------------------------------------ conv
@@ -293,12 +293,56 @@ def layer_norm(ctx):
     x2 = x.reshape(int(torch.tensor(lead).prod()) if lead else 1, -1)
     sc = ctx.input("Scale") if ctx.has_input("Scale") else None
     b = ctx.input("Bias") if ctx.has_input("Bias") else None
-    y = K.layer_norm(x2, sc.reshape(-1) if sc is not None else None, b.reshape(-1) if b is not None else None,
-                     ctx.attr("epsilon"))
+    eps = ctx.attr("epsilon")
+    sc1 = sc.reshape(-1) if sc is not None else None
+    b1 = b.reshape(-1).to(x2.dtype) if b is not None else None
+    if not ctx.meta and _fused.norm_kernel_ok(x2, sc1):
+        # one HIP pass: Y plus the row statistics the grad op reads back
+        y, mean, rstd = _fused.layer_norm_stats(x2, sc1, b1, eps)
+        ctx.set_output("Y", y.reshape(x.shape))
+        ctx.set_output("Mean", mean)
+        ctx.set_output("Variance", rstd.pow(-2) - eps)
+        return
+    y = K.layer_norm(x2, sc1, b1, eps)
     xf = x2.float()
     ctx.set_output("Y", y.reshape(x.shape))
     ctx.set_output("Mean", xf.mean(1))
     ctx.set_output("Variance", xf.var(1, unbiased=False))
+
+
+@register_op("layer_norm_grad", ["X", "Scale?", "Bias?", "Mean", "Variance", "Y?", "Y@GRAD"],
+             ["X@GRAD", "Scale@GRAD?", "Bias@GRAD?"], {"epsilon": 1e-5, "begin_norm_axis": 1, "is_test": False},
+             grad=None, no_infer=True)
+def layer_norm_grad(ctx):
+    """Explicit layer_norm grad from the saved Mean / Variance (layer_norm_op.h
+    LayerNormGradKernel): the norm kernel's backward on the device, the same closed
+    form in torch on the host."""
+    x, dy = ctx.input("X"), ctx.input("Y@GRAD")
+    ax = ctx.attr("begin_norm_axis")
+    eps = ctx.attr("epsilon")
+    rows = 1
+    for d in x.shape[:ax]:
+        rows *= int(d)
+    x2, dy2 = x.reshape(rows, -1), dy.reshape(rows, -1).to(x.dtype)
+    sc = ctx.input("Scale").reshape(-1) if ctx.has_input("Scale") else None
+    has_b = ctx.has_input("Bias")
+    mean = ctx.input("Mean").reshape(-1).float()
+    rstd = torch.rsqrt(ctx.input("Variance").reshape(-1).float() + eps)
+    if _fused.norm_kernel_ok(x2, sc):
+        dx, dw, db = _fused.layer_norm_stats_grad(dy2, x2, sc, mean, rstd, has_b)
+    else:
+        xh = (x2.float() - mean[:, None]) * rstd[:, None]
+        g = dy2.float()
+        dw = (g * xh).sum(0) if sc is not None else None
+        db = g.sum(0) if has_b else None
+        gx = g * sc.float()[None, :] if sc is not None else g
+        dx = rstd[:, None] * (gx - gx.mean(1, keepdim=True) - xh * (gx * xh).mean(1, keepdim=True))
+        dx = dx.to(x.dtype)
+    ctx.set_output("X@GRAD", dx.reshape(x.shape))
+    if ctx.has_output("Scale@GRAD") and sc is not None:
+        ctx.set_output("Scale@GRAD", dw.to(sc.dtype).reshape(ctx.input("Scale").shape))
+    if ctx.has_output("Bias@GRAD") and has_b:
+        ctx.set_output("Bias@GRAD", db.to(ctx.input("Bias").dtype).reshape(ctx.input("Bias").shape))
 
 
 @register_op("lrn", ["X"], ["Out", "MidOut~"], {"n": 5, "k": 2.0, "alpha": 1e-4, "beta": 0.75})

@@ -5,6 +5,8 @@ decayed_adagrad,adadelta,rmsprop,ftrl,proximal_gd,proximal_adagrad,
 average_accumulates}_op.* (SURVEY §2.7 "Optimizers").  Dense fp32 Adam / Momentum
 on the HIP device run the fused gfx950 kernels (lr and beta-pow read from device
 memory: no host sync); SelectedRows (sparse) gradients update only their rows.
+When an output var is its input var (ParamOut == Param, Moment1Out == Moment1, as
+the optimizer pass wires them) the update is in place, with no copies.
 """
 from __future__ import annotations
 
@@ -25,12 +27,35 @@ def _lr(ctx):
     return ctx.input("LearningRate").reshape(-1)[0:1]
 
 
-def _native(ctx, kind, p, g, states, outs, lr=True, **h):
-    """Run the fused optim_ext.hip update on clones of Param / states; True when done."""
+def _inplace(ctx, in_slot, out_slot):
+    """Out var is the In var (ParamOut == Param, the optimizer pass's wiring): the
+    kernel may update the tensor in place, as the reference does (adam_op.h:223-321)."""
+    op = ctx.op
+    if op is None:
+        return False
+    try:
+        i, o = op.input(in_slot), ctx.out_names.get(out_slot) or []
+    except Exception:  # noqa: BLE001
+        return False
+    return len(i) == 1 and len(o) == 1 and i[0] == o[0]
+
+
+def _buf(ctx, t, in_slot, out_slot):
+    """The update target: ``t`` itself when updating in place, else a copy."""
+    if t is None:
+        return None
+    return t if _inplace(ctx, in_slot, out_slot) and t.is_contiguous() else t.clone()
+
+
+def _native(ctx, kind, p, g, states, outs, lr=True, in_slots=None, **h):
+    """Run the fused optim_ext.hip update -- in place on every tensor whose Out var
+    is its In var (``in_slots`` names the state inputs), on copies otherwise."""
     if not p.is_cuda:
         return False
-    p2 = p.clone()
-    s2 = [s.clone() if s is not None else None for s in states]
+    p2 = _buf(ctx, p, "Param", "ParamOut")
+    in_slots = list(in_slots or [None] * len(states))
+    s2 = [None if s is None else (_buf(ctx, s, si, so) if si and so else s.clone())
+          for s, si, so in zip(states, in_slots, outs)]
     lr_t = ctx.input("LearningRate") if lr else None
     if _oplib.opt_update_(kind, p2, g, s2, lr_t, **h) is None:
         return False
@@ -46,7 +71,7 @@ def sgd(ctx):
     p = ctx.input("Param")
     g = _grad(ctx)
     if p.is_cuda:
-        out = p.clone()
+        out = _buf(ctx, p, "Param", "ParamOut")
         if isinstance(g, core.SelectedRows):
             done = _oplib.sgd_sparse_(out, g.rows(), g.get_tensor().tensor, ctx.input("LearningRate"))
         else:
@@ -70,8 +95,8 @@ def momentum(ctx):
     p, v = ctx.input("Param"), ctx.input("Velocity")
     g = _grad(ctx)
     g = g.to_dense() if isinstance(g, core.SelectedRows) else g.tensor
-    p2, v2 = p.clone(), v.clone()
     if p.is_cuda and p.dtype == torch.float32 and p.is_contiguous():
+        p2, v2 = _buf(ctx, p, "Param", "ParamOut"), _buf(ctx, v, "Velocity", "VelocityOut")
         fopt.momentum_flat(p2.view(-1), g.contiguous().view(-1), v2.view(-1), lr=0.0,
                            lr_tensor=ctx.input("LearningRate"), mu=ctx.attr("mu"),
                            nesterov=ctx.attr("use_nesterov"))
@@ -104,7 +129,8 @@ def adam(ctx):
     p, m1, m2 = ctx.input("Param"), ctx.input("Moment1"), ctx.input("Moment2")
     b1, b2, eps = ctx.attr("beta1"), ctx.attr("beta2"), ctx.attr("epsilon")
     g = _grad(ctx)
-    p2, m1o, m2o = p.clone(), m1.clone(), m2.clone()
+    p2, m1o, m2o = (_buf(ctx, p, "Param", "ParamOut"), _buf(ctx, m1, "Moment1", "Moment1Out"),
+                    _buf(ctx, m2, "Moment2", "Moment2Out"))
     if isinstance(g, core.SelectedRows):
         # sparse Adam: merge duplicate rows, update only touched rows (SparseAdamFunctor)
         rows = torch.as_tensor(g.rows(), dtype=torch.long, device=p.device)
@@ -115,9 +141,9 @@ def adam(ctx):
         bp1, bp2 = ctx.input("Beta1Pow").reshape(-1)[0], ctx.input("Beta2Pow").reshape(-1)[0]
         mm = b1 * m1[uniq] + (1 - b1) * gm
         vv = b2 * m2[uniq] + (1 - b2) * gm * gm
-        m1o[uniq], m2o[uniq] = mm, vv
         lr_t = lr * torch.sqrt(1 - bp2) / (1 - bp1)
-        p2[uniq] = p[uniq] - lr_t * mm / (torch.sqrt(vv) + eps)
+        upd = p[uniq] - lr_t * mm / (torch.sqrt(vv) + eps)
+        m1o[uniq], m2o[uniq], p2[uniq] = mm, vv, upd
     else:
         gt = g.tensor
         if p.is_cuda and p.dtype == torch.float32 and p.is_contiguous():
@@ -167,7 +193,7 @@ def adagrad(ctx):
         p2[uniq] = p[uniq] - lr * gm / (torch.sqrt(m2[uniq]) + eps)
     else:
         g = g.tensor
-        p2, m2 = p.clone(), m.clone()
+        p2, m2 = _buf(ctx, p, "Param", "ParamOut"), _buf(ctx, m, "Moment", "MomentOut")
         if p.is_cuda and _oplib.adagrad_(p2, g, m2, ctx.input("LearningRate"), eps) is not None:
             ctx.set_output("ParamOut", p2)
             ctx.set_output("MomentOut", m2)
@@ -316,7 +342,8 @@ def _native_opt(op_type, kind, state_slots, out_slots, hyper, lr=True):
         if not isinstance(gv, core.SelectedRows):
             states = [ctx.input(s) if ctx.has_input(s) and (s != "MeanGrad" or ctx.attr("centered")) else None
                       for s in state_slots]
-            if _native(ctx, kind, ctx.input("Param"), gv.tensor, states, out_slots, lr=lr, **hyper(ctx)):
+            if _native(ctx, kind, ctx.input("Param"), gv.tensor, states, out_slots, lr=lr, in_slots=state_slots,
+                       **hyper(ctx)):
                 return
         plain(ctx)
 

@@ -11,11 +11,13 @@ per op instead of one per sequence wherever the math allows.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
 from ..framework import core
 from ..framework.registry import register_op
+from ..ops import blas as _blas
 from ..ops import fluidk as _fk
 from ..ops import oplib as _oplib
 
@@ -124,25 +126,30 @@ def sequence_expand(ctx):
     # every row is one sequence and the output carries no LoD
     xlod = xlod if len(xlod) == 1 else []
     xoff = xlod[0] if xlod else list(range(x.shape[0] + 1))
-    rows, out_off = [], [0]
-    for i in range(len(yoff) - 1):
-        rep = yoff[i + 1] - yoff[i]
-        seq = list(range(xoff[i], xoff[i + 1]))
-        for _ in range(rep):
-            rows += seq
-            out_off.append(out_off[-1] + len(seq))
-    out = _oplib.gather_rows_op(x, rows) if x.is_cuda and rows else None
+    xo = np.asarray(xoff, dtype=np.int64)
+    reps = np.diff(np.asarray(yoff, dtype=np.int64))
+    # block b = one copy of X's sequence i; rows = concatenated ranges (no per-row loop)
+    starts, lens = np.repeat(xo[:-1], reps), np.repeat(np.diff(xo), reps)
+    out_off = np.concatenate([[0], np.cumsum(lens)])
+    rows = np.repeat(starts - out_off[:-1], lens) + np.arange(int(out_off[-1]))
+    out = _oplib.gather_rows_op(x, rows) if x.is_cuda and rows.size else None
     if out is None:
-        out = x[torch.tensor(rows, dtype=torch.long, device=x.device)]
-    ctx.set_output("Out", out, [out_off] if xlod else None)
+        out = x[torch.as_tensor(rows, dtype=torch.long, device=x.device)]
+    ctx.set_output("Out", out, [out_off.tolist()] if xlod else None)
 
 
 @register_op("sequence_expand_as", ["X", "Y"], ["Out"], {}, share_lod=False)
 def sequence_expand_as(ctx):
+    """Row i of X repeated len(Y's sequence i) times (sequence_expand_as_op.h), as
+    one HIP row gather with a scatter-add backward."""
     x = ctx.input("X")
     yoff = ctx.input_lod("Y")[0]
-    reps = torch.tensor([yoff[i + 1] - yoff[i] for i in range(len(yoff) - 1)], device=x.device)
-    ctx.set_output("Out", torch.repeat_interleave(x, reps, 0), [yoff])
+    reps = np.diff(np.asarray(yoff, dtype=np.int64))
+    rows = np.repeat(np.arange(len(reps)), reps)
+    out = _oplib.gather_rows_op(x, rows) if x.is_cuda and rows.size else None
+    if out is None:
+        out = x[torch.as_tensor(rows, dtype=torch.long, device=x.device)]
+    ctx.set_output("Out", out, [list(yoff)])
 
 
 @register_op("sequence_concat", ["X*"], ["Out"], {}, share_lod=False)
@@ -161,25 +168,50 @@ def sequence_concat(ctx):
     ctx.set_output("Out", torch.cat(parts, 0), [out_off])
 
 
+def _context_index(off, T, cl, cs, up_pad, has_pad):
+    """Row map of the context projection (math/context_project.h): column block k
+    of output row r reads row r + cs + k of the same sequence; outside it, the
+    trainable padding row up_pad + (src - start) above / up_pad + (src - end) below
+    (stored after the T input rows), else -1 (zero)."""
+    o = np.asarray(off, dtype=np.int64)
+    seg = np.repeat(np.arange(len(o) - 1), np.diff(o))
+    s, e = o[seg][:, None], o[seg + 1][:, None]
+    src = np.arange(T)[:, None] + cs + np.arange(cl)[None, :]
+    idx = np.where((src >= s) & (src < e), src, -1)
+    if has_pad:
+        idx = np.where(src < s, T + up_pad + (src - s), idx)
+        idx = np.where(src >= e, T + up_pad + (src - e), idx)
+    return idx.reshape(-1)
+
+
 @register_op("sequence_conv", ["X", "Filter", "PaddingData?"], ["Out"],
              {"contextLength": 3, "contextStart": 0, "contextStride": 1, "paddingTrainable": False})
 def sequence_conv(ctx):
-    """Context projection (math/context_project.h) + GEMM with the filter."""
+    """Context projection + GEMM with the filter (sequence_conv_op.h).  The
+    projection is one HIP row gather over [X; PaddingData] (scatter-add backward
+    into both), the product the native GEMM; gradients by the eager engine."""
     x, w = ctx.input("X"), ctx.input("Filter")
     off, lod = _last_level(ctx)
     cl, cs = ctx.attr("contextLength"), ctx.attr("contextStart")
-    D = x.shape[1]
+    if ctx.attr("contextStride") != 1:
+        raise ValueError("sequence_conv: contextStride must be 1 (sequence_conv_op.cc)")
+    T, D = x.shape[0], x.shape[1]
     if ctx.meta:
-        ctx.set_output("Out", torch.empty(x.shape[0], w.shape[1], dtype=x.dtype, device="meta"))
+        ctx.set_output("Out", torch.empty(T, w.shape[1], dtype=x.dtype, device="meta"))
         return
-    cols = torch.zeros(x.shape[0], cl * D, dtype=x.dtype, device=x.device)
-    for s, e in zip(off[:-1], off[1:]):
-        for k in range(cl):
-            sh = cs + k
-            lo, hi = max(s, s - sh), min(e, e - sh)
-            if hi > lo:
-                cols[lo:hi, k * D:(k + 1) * D] = x[lo + sh:hi + sh]
-    ctx.set_output("Out", cols @ w, lod)
+    up_pad = max(0, -cs)
+    pad = ctx.input("PaddingData") if ctx.attr("paddingTrainable") and ctx.has_input("PaddingData") else None
+    idx = _context_index(off, T, cl, cs, up_pad, pad is not None)
+    table = torch.cat([x, pad.to(x.dtype)], 0) if pad is not None else x
+    cols = _oplib.gather_rows_op(table, idx) if x.is_cuda and T else None
+    if cols is None:
+        table = torch.cat([table, table.new_zeros(1, D)], 0)
+        it = torch.as_tensor(np.where(idx < 0, table.shape[0] - 1, idx), dtype=torch.long, device=x.device)
+        cols = table[it]
+    cols = cols.reshape(T, cl * D)
+    w = w.to(cols.dtype)
+    out = _blas.matmul(cols, w) if _blas.supported(cols, w) else cols @ w
+    ctx.set_output("Out", out, lod)
 
 
 @register_op("sequence_erase", ["X"], ["Out"], {"tokens": []}, share_lod=False)

@@ -88,6 +88,37 @@ class _NormFn(torch.autograd.Function):
         return dx, (dx if ctx.has_res else None), dw, db, None, None
 
 
+def layer_norm_stats(x2, w, b, eps):
+    """Fluid layer_norm forward on the norm kernel: rows of ``x2`` [N, H] ->
+    (y, mean [N] fp32, rstd [N] fp32) -- the statistics come from the same pass."""
+    Nr, H = x2.shape
+    x2 = _c(x2)
+    y = torch.empty_like(x2)
+    mean, rstd = _ws(Nr, x2.device), _ws(Nr, x2.device)
+    N.call("pa_norm_fwd", N.dt(x2), 0, N.ptr(x2), None, N.ptr(w), N.ptr(b), N.ptr(y), None, N.ptr(mean),
+           N.ptr(rstd), Nr, H, float(eps), N.stream())
+    return y, mean, rstd
+
+
+def layer_norm_stats_grad(dy2, x2, w, mean, rstd, has_b):
+    """Backward of :func:`layer_norm_stats` from the saved statistics -> (dx, dw, db)."""
+    Nr, H = x2.shape
+    x2, dy2 = _c(x2), _c(dy2)
+    dx = torch.empty_like(x2)
+    dw = torch.empty_like(w)
+    db = torch.empty_like(w) if has_b else None
+    G = min(512, (Nr + 3) // 4)
+    ws = _ws(2 * max(G, 1) * H, x2.device)
+    N.call("pa_norm_bwd", N.dt(x2), 0, N.ptr(dy2), N.ptr(x2), N.ptr(w), N.ptr(_c(mean)), N.ptr(_c(rstd)), None,
+           N.ptr(dx), N.ptr(dw), N.ptr(db), N.ptr(ws), Nr, H, N.stream())
+    return dx, dw, db
+
+
+def norm_kernel_ok(x2, w):
+    return (x2.is_cuda and w is not None and x2.dtype in (torch.float32, torch.bfloat16) and w.dtype == x2.dtype
+            and x2.shape[-1] % 8 == 0 and x2.shape[-1] <= 8192 and x2.shape[0] > 0)
+
+
 def param_ready(w):
     """Wait for a deferred parameter all-gather (``FlatShardedOptimizer`` with
     ``overlap_allgather``) before the first read of ``w`` in a step."""

@@ -50,4 +50,42 @@ GRAD_CASES = [
     ("softmax_with_cross_entropy", {"Logits": _logits, "Label": _hard}, {}, ["Logits"], "Loss"),
     ("softmax_with_cross_entropy", {"Logits": _logits, "Label": _soft}, {"soft_label": True}, ["Logits"], "Loss"),
     ("sequence_softmax", {"X": (U(7, 1, lo=-2, hi=2), [[3, 4]])}, {}, ["X"], "Out"),
+    ("layer_norm", {"X": U(2, 3, 16, lo=-2, hi=2), "Scale": U(16, lo=0.5, hi=1.5), "Bias": U(16)},
+     {"begin_norm_axis": 2, "epsilon": 1e-5}, ["X", "Scale", "Bias"], "Y"),
+    ("layer_norm", {"X": U(4, 16, lo=-2, hi=2), "Scale": U(16, lo=0.5, hi=1.5)},
+     {"begin_norm_axis": 1, "epsilon": 1e-5}, ["X", "Scale"], "Y"),
+]
+
+
+def seq_conv_ref(x, off, w, cl, cs, pad=None):
+    """Naive context projection (math/context_project.h semantics) + GEMM."""
+    T, D = x.shape
+    up = max(0, -cs)
+    cols = np.zeros((T, cl * D), dtype=np.float64)
+    for s, e in zip(off[:-1], off[1:]):
+        for r in range(s, e):
+            for k in range(cl):
+                src = r + cs + k
+                if s <= src < e:
+                    cols[r, k * D:(k + 1) * D] = x[src]
+                elif pad is not None:
+                    cols[r, k * D:(k + 1) * D] = pad[up + (src - s if src < s else src - e)]
+    return (cols @ w).astype("float32")
+
+
+_sx = U(9, 4)
+_soff = [0, 2, 7, 9]
+_sw = U(3 * 4, 5)
+_spad = U(3, 4)  # up_pad 1 + down_pad 2 (cs=-1, cl=3 -> down_pad = cs + cl - 1 = 1; extra row unused)
+SEQ_CASES = [
+    # (op, inputs, attrs, grad inputs, expected Out or None)
+    ("sequence_conv", {"X": (_sx, [[2, 5, 2]]), "Filter": _sw}, {"contextLength": 3, "contextStart": -1},
+     ["X", "Filter"], seq_conv_ref(_sx, _soff, _sw, 3, -1)),
+    ("sequence_conv", {"X": (_sx, [[2, 5, 2]]), "Filter": _sw, "PaddingData": _spad},
+     {"contextLength": 3, "contextStart": -1, "paddingTrainable": True}, ["X", "Filter", "PaddingData"],
+     seq_conv_ref(_sx, _soff, _sw, 3, -1, _spad)),
+    ("sequence_conv", {"X": (_sx, [[2, 5, 2]]), "Filter": _sw, "PaddingData": U(2, 4)},
+     {"contextLength": 3, "contextStart": 0, "paddingTrainable": True}, ["X", "PaddingData"], None),
+    ("sequence_expand_as", {"X": U(3, 2), "Y": (U(6, 1), [[1, 3, 2]])}, {}, ["X"], None),
+    ("sequence_expand", {"X": (U(4, 2), [[1, 3]]), "Y": (U(5, 1), [[2, 3]])}, {"ref_level": 0}, ["X"], None),
 ]

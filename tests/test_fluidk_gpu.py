@@ -197,3 +197,17 @@ def test_explicit_grad_op_on_device(op, inputs, attrs, grad, out):
     t.op_type, t.inputs, t.attrs = op, inputs, attrs
     t.outputs = {out: np.zeros(1, "float32")}
     t.check_grad(grad, [out], max_relative_error=0.02, places=[fluid.CUDAPlace(0)])
+
+
+from fluidk_cases import SEQ_CASES  # noqa: E402
+
+
+@pytest.mark.parametrize("op,inputs,attrs,grad,expect", SEQ_CASES, ids=[f"{c[0]}_{i}" for i, c in enumerate(SEQ_CASES)])
+def test_sequence_ops_on_device(op, inputs, attrs, grad, expect):
+    t = OpTest()
+    t.op_type, t.inputs, t.attrs = op, inputs, attrs
+    if expect is not None:
+        t.outputs = {"Out": expect}
+        t.check_output(atol=1e-4, rtol=1e-4, places=[fluid.CUDAPlace(0)])
+    t.outputs = {"Out": np.zeros(1, "float32")}
+    t.check_grad(grad, ["Out"], max_relative_error=0.02, places=[fluid.CUDAPlace(0)])

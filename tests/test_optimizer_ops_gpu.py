@@ -29,3 +29,38 @@ def test_native_kernels_are_used(monkeypatch):
         if op in ("adamax", "ftrl", "rmsprop", "lars_momentum", "adadelta", "decayed_adagrad", "proximal_gd"):
             run_case(op, inputs, outputs, attrs, fluid.CUDAPlace(0))
     assert calls and all(ok for _, ok in calls), calls
+
+
+@pytest.mark.parametrize("opt", ["sgd", "momentum", "adam", "adagrad", "rmsprop", "adamax"])
+def test_optimizer_updates_in_place_on_device(opt):
+    """Fluid program whose optimizer ops write ParamOut == Param: the device update
+    keeps the parameter's storage (no per-step clones) and matches the CPU run."""
+    import numpy as np
+
+    from paddle_amd.framework import core
+
+    def run(place):
+        prog, start = fluid.Program(), fluid.Program()
+        with fluid.program_guard(prog, start):
+            x = fluid.layers.data("x", [8], dtype="float32")
+            y = fluid.layers.fc(x, 4, param_attr=fluid.ParamAttr(name="w",
+                                initializer=fluid.initializer.Constant(0.1)), bias_attr=False)
+            loss = fluid.layers.mean(fluid.layers.square(y))
+            o = {"sgd": fluid.optimizer.SGD(0.1), "momentum": fluid.optimizer.Momentum(0.1, 0.9),
+                 "adam": fluid.optimizer.Adam(0.01), "adagrad": fluid.optimizer.Adagrad(0.1),
+                 "rmsprop": fluid.optimizer.RMSProp(0.01), "adamax": fluid.optimizer.Adamax(0.01)}[opt]
+            o.minimize(loss)
+        scope = core.Scope()
+        exe = fluid.Executor(place)
+        exe.run(start, scope=scope)
+        ptrs = []
+        xs = np.linspace(-1, 1, 3 * 8, dtype="float32").reshape(3, 8)
+        for _ in range(3):
+            exe.run(prog, feed={"x": xs}, fetch_list=[loss], scope=scope)
+            ptrs.append(scope.find_var("w").get().tensor.data_ptr())
+        return np.array(scope.find_var("w").get().tensor.cpu()), ptrs
+
+    wg, ptrs = run(fluid.CUDAPlace(0))
+    wc, _ = run(fluid.CPUPlace())
+    np.testing.assert_allclose(wg, wc, rtol=1e-4, atol=1e-6)
+    assert len(set(ptrs)) == 1, "device optimizer update reallocated the parameter"
