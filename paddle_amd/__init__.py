@@ -17,17 +17,26 @@ __version__ = "0.1.0"
 
 
 def _install_allocator():
-    """FLAGS_allocator_strategy=buddy: torch's device tensors come from the native
-    buddy allocator (csrc/runtime/allocator.cc).  Has to happen before the first
-    device allocation, hence at import."""
+    """FLAGS_allocator_strategy (default ``buddy``): torch's device tensors come from
+    the native buddy allocator (csrc/runtime/allocator.cc; reference
+    memory/detail/buddy_allocator.cc), with record_stream-ordered frees.  Any other
+    value (``naive_best_fit``, ``auto_growth``, ``torch``) keeps torch's caching
+    allocator.  It has to be swapped in before the first device allocation, hence at
+    import; devices are counted without initialising HIP."""
     import os
+    import warnings
 
-    if os.environ.get("FLAGS_allocator_strategy", "") != "buddy" or not torch.cuda.is_available():
+    if os.environ.get("FLAGS_allocator_strategy", "buddy") != "buddy":
         return
-    from . import runtime
+    try:
+        if torch.cuda.device_count() == 0:
+            return
+        from . import runtime
 
-    mb = int(os.environ.get("FLAGS_buddy_chunk_mb", "4096"))
-    runtime.use_buddy_allocator_for_torch(chunk_bytes=mb << 20)
+        mb = int(os.environ.get("FLAGS_buddy_chunk_mb", "4096"))
+        runtime.use_buddy_allocator_for_torch(chunk_bytes=mb << 20)
+    except Exception as e:  # noqa: BLE001  (torch already allocated on the device, lib missing, ...)
+        warnings.warn(f"paddle_amd: buddy allocator not installed ({e}); using torch's caching allocator")
 
 
 _install_allocator()

@@ -266,9 +266,19 @@ size_t g_torch_chunk = 4ull << 30;
 // Torch hook pools: one allocator per (device, stream).  torch's pluggable
 // allocator frees a block with the stream it was allocated on, and a block only
 // ever returns to its own stream's pool, so reuse is ordered by that stream and a
-// free needs no event or host synchronisation (cross-stream users must order
-// themselves, as with record_stream on torch's caching allocator).
+// plain free needs no event or host synchronisation.  A block that was also used
+// on other streams (Tensor.record_stream -> pa_torch_record_stream) is released
+// only after an event recorded on each of those streams at free time has
+// completed -- the caching allocator's record_stream contract.
 std::map<std::pair<int, hipStream_t>, Buddy*> g_torch;
+std::unordered_map<void*, std::vector<hipStream_t>> g_uses;  // ptr -> extra streams
+struct Deferred {
+  void* ptr;
+  int device;
+  hipStream_t stream;
+  std::vector<hipEvent_t> events;
+};
+std::vector<Deferred> g_deferred;
 
 Buddy* torch_pool(int device, hipStream_t s) {
   auto& b = g_torch[{device, s}];
@@ -278,6 +288,37 @@ Buddy* torch_pool(int device, hipStream_t s) {
     b->chunk = g_torch_chunk;
   }
   return b;
+}
+
+void release_now(void* ptr, int device, hipStream_t stream) {
+  auto it = g_torch.find({device, stream});
+  if (it != g_torch.end() && it->second->release(ptr) == 0) return;
+  for (auto& kv : g_torch)  // defensive: a block freed with another stream
+    if (kv.first.first == device && kv.second->release(ptr) == 0) return;
+}
+
+// releases the deferred blocks whose events have all completed (wait: block on them)
+void drain_deferred(bool wait) {
+  size_t keep = 0;
+  for (size_t i = 0; i < g_deferred.size(); ++i) {
+    Deferred& d = g_deferred[i];
+    bool done = true;
+    for (hipEvent_t e : d.events) {
+      hipError_t q = wait ? hipEventSynchronize(e) : hipEventQuery(e);
+      if (q == hipErrorNotReady) {
+        done = false;
+        break;
+      }
+      if (q != hipSuccess) (void)hipGetLastError();  // a failed event: treat as completed
+    }
+    if (done) {
+      for (hipEvent_t e : d.events) hipEventDestroy(e);
+      release_now(d.ptr, d.device, d.stream);
+    } else {
+      g_deferred[keep++] = std::move(d);
+    }
+  }
+  g_deferred.resize(keep);
 }
 }  // namespace
 
@@ -307,8 +348,13 @@ PA_RT_EXPORT void pa_torch_set_chunk(size_t bytes) { g_torch_chunk = bytes; }
 
 PA_RT_EXPORT void* pa_torch_malloc(ssize_t size, int device, hipStream_t stream) {
   std::lock_guard<std::mutex> g(g_mu);
+  if (!g_deferred.empty()) drain_deferred(false);
   Buddy* b = torch_pool(device, stream);
   void* p = b->alloc((size_t)size);
+  if (!p && !g_deferred.empty()) {  // blocks still waiting on other streams: wait for them
+    drain_deferred(true);
+    p = b->alloc((size_t)size);
+  }
   if (!p) {  // out of memory: return other streams' wholly free segments, retry
     for (auto& kv : g_torch)
       if (kv.first.first == device && kv.second != b) {
@@ -320,13 +366,48 @@ PA_RT_EXPORT void* pa_torch_malloc(ssize_t size, int device, hipStream_t stream)
   return p;
 }
 
+PA_RT_EXPORT void pa_torch_record_stream(void* ptr, hipStream_t stream) {
+  if (!ptr) return;
+  std::lock_guard<std::mutex> g(g_mu);
+  auto& v = g_uses[ptr];
+  for (hipStream_t s : v)
+    if (s == stream) return;
+  v.push_back(stream);
+}
+
 PA_RT_EXPORT void pa_torch_free(void* ptr, ssize_t, int device, hipStream_t stream) {
   if (!ptr) return;
   std::lock_guard<std::mutex> g(g_mu);
-  auto it = g_torch.find({device, stream});
-  if (it != g_torch.end() && it->second->release(ptr) == 0) return;
-  for (auto& kv : g_torch)  // defensive: a block freed with another stream
-    if (kv.first.first == device && kv.second->release(ptr) == 0) return;
+  auto u = g_uses.find(ptr);
+  if (u != g_uses.end()) {
+    Deferred d{ptr, device, stream, {}};
+    int prev;
+    hipGetDevice(&prev);
+    hipSetDevice(device);
+    for (hipStream_t s : u->second) {
+      if (s == stream) continue;
+      hipEvent_t e;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        hipStreamSynchronize(s);  // no event: order the reuse by waiting now
+        continue;
+      }
+      hipEventRecord(e, s);
+      d.events.push_back(e);
+    }
+    hipSetDevice(prev);
+    g_uses.erase(u);
+    if (!d.events.empty()) {
+      g_deferred.push_back(std::move(d));
+      return;
+    }
+  }
+  release_now(ptr, device, stream);
+}
+
+PA_RT_EXPORT size_t pa_torch_deferred_frees() {
+  std::lock_guard<std::mutex> g(g_mu);
+  return g_deferred.size();
 }
 
 PA_RT_EXPORT void pa_torch_stats(int device, size_t* used, size_t* reserved, size_t* peak) {

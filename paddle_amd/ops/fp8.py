@@ -1,15 +1,21 @@
-"""FP8 (OCP e4m3fn) weight GEMMs for MI355X.
+"""FP8 (OCP e4m3fn) GEMMs for MI355X on the hand-written gfx950 kernel.
 
-gfx950 MFMA runs fp8 x fp8 -> fp32 at 2x the bf16 rate (``v_mfma_f32_32x32x64_f8f6f4``
-/ the non-scaled 32x32x16 fp8 forms).  ``fp8_linear`` keeps a bf16/fp32 master
-weight (the optimizer updates it), caches its e4m3 copy + per-tensor scale keyed
-on the weight's version counter, quantises the activation with a dynamic
-per-tensor amax scale and runs the FORWARD GEMM in fp8 through hipBLASLt
-(``torch._scaled_mm``); the backward GEMMs run in bf16 against the master weight
-(straight-through estimator), the usual recipe for fp8 training of MoE experts.
+gfx950 runs block-scaled fp8 x fp8 -> fp32 MFMA (``v_mfma_scale_f32_16x16x128_f8f6f4``)
+at 2x the bf16 rate; ``gemm.hip``'s ``pa_gemm_f8`` uses it with both operands
+K-major e4m3 and fp32 per-row (A) / per-column (B) scales applied in the epilogue.
 
-On CPU (tests) or where the fp8 GEMM is unavailable the same quantise/dequantise
-numerics are emulated in fp32, so results match the device path to fp8 rounding.
+``fp8_linear`` (dense layers) keeps the bf16 master weight (the optimizer updates
+it) and caches two e4m3 images of it, rebuilt when the weight changes: columns
+quantised per output channel and transposed ([out, in], forward B operand) and rows
+quantised per input channel ([in, out], dgrad B operand).  Forward y = x W and
+dgrad dx = dy W^T run in fp8 with per-row dynamic scales of the activation / output
+gradient (quantised by fp8.hip); wgrad dW = x^T dy stays bf16 on the same native
+GEMM (accumulated in fp32) -- the usual fp8 training recipe.  The grouped expert
+GEMMs of the MoE layer use the same kernel (``gemm_f8`` below, grp_mode 1).
+
+On CPU (tests) or for shapes the kernel does not take (K % 16, N % 8) the same
+per-row / per-column quantisation is emulated in fp32, so both paths share numerics
+up to accumulation order.
 """
 from __future__ import annotations
 
@@ -18,7 +24,6 @@ from ..autograd import tape as _tape  # noqa: E402
 
 E4M3_MAX = 448.0
 _FP8 = getattr(torch, "float8_e4m3fn", None)
-_scaled_mm_ok = {}
 
 
 def quantize(x, amax=None):
@@ -29,67 +34,80 @@ def quantize(x, amax=None):
     return q, scale
 
 
-def _can_scaled_mm(dev):
-    if dev.type != "cuda" or _FP8 is None or not hasattr(torch, "_scaled_mm"):
-        return False
-    key = dev.index or 0
-    if key not in _scaled_mm_ok:
-        try:
-            a = torch.zeros(32, 32, device=dev, dtype=_FP8)
-            b = torch.zeros(32, 32, device=dev, dtype=_FP8).t()
-            one = torch.ones((), device=dev)
-            torch._scaled_mm(a, b, scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
-            _scaled_mm_ok[key] = True
-        except Exception:  # noqa: BLE001
-            _scaled_mm_ok[key] = False
-    return _scaled_mm_ok[key]
+def quant_rows_ref(x):
+    """Host / fallback twin of fp8.hip's row quantiser: x [R, K] -> (q e4m3, scale [R])."""
+    s = torch.clamp(x.detach().float().abs().amax(1), min=1e-12) / E4M3_MAX
+    q = (x.float() / s[:, None]).clamp(-E4M3_MAX, E4M3_MAX).to(_FP8)
+    return q, s
+
+
+def _native_ok(x2, w):
+    M, K = x2.shape
+    N = w.shape[1]
+    return (x2.is_cuda and w.is_cuda and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and K % 16 == 0 and N % 16 == 0 and M > 0)
 
 
 class _WeightCache:
+    """e4m3 images of one master weight [in, out]: ``fwd`` = per-output-channel
+    columns transposed to [out, in]; ``bwd`` = per-input-channel rows [in, out]."""
+
     def __init__(self):
-        self.version = -1
-        self.q = self.scale = None
+        self.fwd = VersionedCache(lambda w: tuple(t[0] for t in quant_cols_t(w[None])))
+        self.bwd = VersionedCache(lambda w: quant_rows(w.contiguous()))
 
 
-def _weight_fp8(w, cache):
-    v = w._version
-    if cache.version != v or cache.q is None:
-        # [in, out] master -> column-major [out, in]^T view for _scaled_mm's B operand
-        cache.q, cache.scale = quantize(w.detach().t().contiguous())
-        cache.version = v
-    return cache.q, cache.scale
+def _emul(aq, sa, bq, sb):
+    """sum_k aq[m, k] bq[n, k] * sa[m] * sb[n] in fp32 (CPU / fallback)."""
+    return (aq.float() * sa[:, None]) @ (bq.float() * sb[:, None]).t()
 
 
 class _FP8LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, cache):
-        x2 = x.reshape(-1, x.shape[-1])
-        wq, ws = _weight_fp8(w, cache)         # wq: [out, in] e4m3
-        xq, xs = quantize(x2)
-        if _can_scaled_mm(x.device) and x2.shape[0] % 16 == 0 and x2.shape[1] % 16 == 0 and wq.shape[0] % 16 == 0:
-            y = torch._scaled_mm(xq, wq.t(), scale_a=xs, scale_b=ws, out_dtype=torch.bfloat16)
-            y = y.to(x.dtype)
+        Kin, N = w.shape
+        x2 = x.reshape(-1, Kin)
+        M = x2.shape[0]
+        native = _native_ok(x2, w)
+        if native:
+            xq, xs = quant_rows(x2.contiguous())
+            wq, ws = cache.fwd.get(w)
+            y = gemm_f8(xq, xs, wq, ws, M, N, Kin, out=torch.empty(M, N, dtype=torch.bfloat16, device=x.device))
         else:
-            y = ((xq.float() * xs) @ (wq.float() * ws).t()).to(x.dtype)
+            xq, xs = quant_rows_ref(x2)
+            wq, ws = quant_rows_ref(w.detach().t())
+            y = _emul(xq, xs, wq, ws).to(x.dtype)
         if b is not None:
-            y = y + b
-        ctx.save_for_backward(x, w)
-        ctx.has_b = b is not None
-        return y.reshape(*x.shape[:-1], w.shape[1])
+            y = y + b.to(y.dtype)
+        ctx.save_for_backward(x2, w)
+        ctx.has_b, ctx.native, ctx.cache, ctx.xshape = b is not None, native, cache, x.shape
+        return y.reshape(*x.shape[:-1], N)
 
     @staticmethod
     def backward(ctx, g):
-        x, w = ctx.saved_tensors
-        g2 = g.reshape(-1, g.shape[-1])
-        x2 = x.reshape(-1, x.shape[-1])
-        dx = (g2 @ w.t().to(g2.dtype)).reshape(x.shape)
-        dw = (x2.t().to(g2.dtype) @ g2).to(w.dtype)
-        db = g2.sum(0).to(w.dtype) if ctx.has_b else None
-        return dx, dw, db, None
+        x2, w = ctx.saved_tensors
+        Kin, N = w.shape
+        g2 = g.reshape(-1, N)
+        M = g2.shape[0]
+        if ctx.native and g2.dtype == torch.bfloat16:
+            from . import gemm as G
+
+            gq, gs = quant_rows(g2.contiguous())
+            wq, ws = ctx.cache.bwd.get(w)
+            dx = gemm_f8(gq, gs, wq, ws, M, Kin, N, out=torch.empty(M, Kin, dtype=torch.bfloat16, device=g.device))
+            dw = G.linear_dw(x2.contiguous(), g2.contiguous()).to(w.dtype)
+        else:
+            gq, gs = quant_rows_ref(g2)
+            wq, ws = quant_rows_ref(w.detach())
+            dx = _emul(gq, gs, wq, ws).to(g2.dtype)
+            dw = (x2.t().float() @ g2.float()).to(w.dtype)
+        db = g2.float().sum(0).to(w.dtype) if ctx.has_b else None
+        return dx.reshape(ctx.xshape), dw, db, None
 
 
 def fp8_linear(x, weight, bias=None, cache=None):
-    """``x @ weight (+ bias)`` with ``weight`` [in, out] (Paddle layout) run as an fp8 GEMM."""
+    """``x @ weight (+ bias)`` with ``weight`` [in, out] (Paddle layout): forward and
+    dgrad on the fp8 MFMA GEMM, wgrad bf16."""
     if cache is None:
         cache = getattr(weight, "_pa_fp8_cache", None)
         if cache is None:

@@ -40,6 +40,7 @@ _SIGS = {
     "pa_buddy_free": ([P, P], I),
     "pa_buddy_stats": ([P, ctypes.POINTER(SZ), ctypes.POINTER(SZ), ctypes.POINTER(SZ), ctypes.POINTER(SZ)], None),
     "pa_torch_set_chunk": ([SZ], None),
+    "pa_torch_deferred_frees": ([], SZ),
     "pa_torch_stats": ([I, ctypes.POINTER(SZ), ctypes.POINTER(SZ), ctypes.POINTER(SZ)], None),
     "pa_bq_create": ([SZ], P),
     "pa_bq_push": ([P, ctypes.c_char_p, SZ], I),
@@ -244,7 +245,16 @@ def use_buddy_allocator_for_torch(chunk_bytes=4 << 30):
 
     lib().pa_torch_set_chunk(int(chunk_bytes))
     alloc = torch.cuda.memory.CUDAPluggableAllocator(_build.RUNTIME_LIB, "pa_torch_malloc", "pa_torch_free")
+    # Tensor.record_stream: frees of blocks used on other streams wait for an event
+    # on each of them (without the hook torch's pluggable path ignores record_stream)
+    rs = ctypes.cast(getattr(ctypes.CDLL(_build.RUNTIME_LIB), "pa_torch_record_stream"), ctypes.c_void_p).value
+    alloc._allocator.set_record_stream_fn(rs)
     torch.cuda.memory.change_current_allocator(alloc)
+
+
+def torch_deferred_frees():
+    """Blocks freed by torch but still waiting for another stream (record_stream)."""
+    return int(lib().pa_torch_deferred_frees())
 
 
 def torch_allocator_stats(device=0):

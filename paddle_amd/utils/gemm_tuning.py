@@ -1,11 +1,13 @@
-"""Replay of tuned library-GEMM solutions (hipBLASLt / rocBLAS) for plain linear layers.
+"""Replay of tuned library-GEMM solutions (hipBLASLt / rocBLAS), opt-in.
 
-Fused GEMM-shaped work runs in our own MFMA kernels; the plain projection GEMMs of a
-transformer go to hipBLASLt.  Its heuristic pick is not always the fastest solution
-for the wide-N / K=4096 shapes of LLaMA/GPT, so ``benchmarks/gemm_tune.py`` searches
-every solution once on the MI355X (PyTorch TunableOp) and stores the winners under
-``paddle_amd/tuning/gfx950_<model>.csv``.  ``enable(model)`` makes every later GEMM
-of that shape dispatch straight to the stored solution (no search at run time).
+The training steps of the flagship models do not use it: every LLaMA / GPT / MoE
+projection, LM head and expert GEMM runs on the hand-written gfx950 kernel
+(csrc/kernels/gemm.hip, ops/gemm.py).  What remains on the vendor library are plain
+``torch.matmul`` calls outside those paths (user code, odd shapes the native kernel
+does not take).  For those, ``benchmarks/gemm_tune.py`` searches every hipBLASLt
+solution once on the MI355X (PyTorch TunableOp) and stores the winners under
+``paddle_amd/tuning/gfx950_<model>.csv``; ``enable(model)`` makes later library GEMMs
+of those shapes dispatch straight to the stored solution (``bench.py --tuned-gemm``).
 
 The tuning file carries validator lines (PyTorch / ROCm / hipBLASLt versions); a file
 from another software stack is rejected by TunableOp and the heuristic pick is used.

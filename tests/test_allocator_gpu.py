@@ -37,3 +37,34 @@ def test_llama_tiny_under_buddy_allocator_matches_caching_allocator():
     for a, b in zip(ref["losses"], bud["losses"]):
         assert abs(a - b) <= 1e-3 * max(1.0, abs(a)), (ref["losses"], bud["losses"])
     assert bud["losses"][-1] < bud["losses"][0]
+
+
+def test_buddy_is_default_and_record_stream_defers_reuse():
+    """In this (default-configured) process torch allocates from the buddy pools; a
+    block used on a side stream (record_stream) is not handed out again until that
+    stream has passed the point where the block was freed."""
+    code = r"""
+import torch, paddle_amd
+from paddle_amd import runtime
+x = torch.empty(64 << 20, device="cuda")          # 256 MiB, default stream
+assert runtime.torch_allocator_stats()["reserved"] > 0, "buddy allocator not active"
+s = torch.cuda.Stream()
+with torch.cuda.stream(s):
+    torch.cuda._sleep(200_000_000)               # keep the side stream busy
+    y = x * 2
+x.record_stream(s)
+p = x.data_ptr()
+del x
+assert runtime.torch_deferred_frees() == 1
+z = torch.empty(64 << 20, device="cuda")
+assert z.data_ptr() != p                          # the pending block was not reused
+s.synchronize()
+w = torch.empty(16, device="cuda")                # next malloc drains completed frees
+assert runtime.torch_deferred_frees() == 0
+print("ok")
+"""
+    env = dict(os.environ)
+    env.pop("FLAGS_allocator_strategy", None)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120,
+                       cwd=ROOT)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-3000:]

@@ -1,7 +1,8 @@
 """paddle.dataset parsers on files in the real on-disk formats (reference
 python/paddle/dataset/tests/*).  No network: each test writes a miniature file in
 the upstream format (IDX gz, housing text, PTB tgz, aclImdb tgz, CIFAR binary
-tgz, ml-1m zip) into a temporary DATA_HOME and checks the parsed samples;
+tgz, ml-1m zip, WMT14/WMT16 tgz, CoNLL-05 props, 102flowers tgz + .mat) into a
+temporary DATA_HOME and checks the parsed samples;
 without files the modules fall back to synthetic samples of the same shapes."""
 import gzip
 import io
@@ -13,7 +14,8 @@ import zipfile
 import numpy as np
 import pytest
 
-from paddle_amd.dataset import cifar, common, imdb, imikolov, mnist, movielens, uci_housing
+from paddle_amd.dataset import (cifar, common, conll05, flowers, imdb, imikolov, mnist, movielens, uci_housing,
+                                wmt14, wmt16)
 
 
 @pytest.fixture
@@ -136,3 +138,83 @@ def test_synthetic_fallback_warns_once(home):
         next(iter(cifar.test10()()))
     assert x.shape == (3072,) and 0 <= y < 10
     assert sum("synthetic" in str(m.message) for m in w) == 1
+
+
+def test_wmt14_tgz(home):
+    d = home / "wmt14"
+    d.mkdir()
+    src_dict = b"<s>\n<e>\n<unk>\nle\nchat\nnoir\n"
+    trg_dict = b"<s>\n<e>\n<unk>\nthe\ncat\nblack\n"
+    train = b"le chat noir\tthe black cat\nle chien\tthe dog\nbroken line\n" + \
+        ("x " * 90).encode() + b"\tthe\n"
+    _tar(d / "wmt14.tgz", {"wmt14/src.dict": src_dict, "wmt14/trg.dict": trg_dict, "wmt14/train/train": train,
+                           "wmt14/test/test": b"chat\tcat\n"})
+    got = list(wmt14.train(dict_size=6)())
+    assert got[0] == ([0, 3, 4, 5, 1], [0, 3, 5, 4], [3, 5, 4, 1])
+    assert got[1] == ([0, 3, 2, 1], [0, 3, 2], [3, 2, 1])  # unknown words -> UNK_IDX 2
+    assert len(got) == 2  # the malformed line and the > 80-id pair are dropped
+    assert list(wmt14.test(dict_size=6)()) == [([0, 4, 1], [0, 4], [4, 1])]
+    src, trg = wmt14.get_dict(6)
+    assert src[4] == "chat" and trg[5] == "black"
+
+
+def test_wmt16_tgz_builds_frequency_dicts(home):
+    d = home / "wmt16"
+    d.mkdir()
+    train = b"a b b c\tx y y y\nb c\tz x\n"
+    _tar(d / "wmt16.tar.gz", {"wmt16/train": train, "wmt16/test": b"c a q\ty z\n", "wmt16/val": b"b\tx\n"})
+    en = wmt16.get_dict("en", 6)
+    assert list(en) == ["<s>", "<e>", "<unk>", "b", "c", "a"]  # by count, ties by first occurrence
+    got = list(wmt16.test(6, 6, "en")())
+    de = wmt16.get_dict("de", 6)
+    assert got == [([0, en["c"], en["a"], 2, 1], [0, de["y"], de["z"]], [de["y"], de["z"], 1])]
+    assert (home / "wmt16" / "en_6.dict").exists()
+    rev = list(wmt16.validation(6, 6, "de")())  # German source
+    assert rev == [([0, de["x"], 1], [0, en["b"]], [en["b"], 1])]
+
+
+def test_conll05_props_to_samples(home):
+    d = home / "conll05st"
+    d.mkdir()
+    (d / "wordDict.txt").write_text("<unk>\nThe\ncat\nsat\ndown\nbos\neos\n")
+    (d / "verbDict.txt").write_text("sit\n")
+    (d / "targetDict.txt").write_text("B-A0\nI-A0\nB-V\nI-V\nB-AM\nI-AM\n")
+    words = b"The\ncat\nsat\ndown\n\n"
+    # column 0: the predicate lemma on its row; column 1: that predicate's arguments
+    props = b"-\t(A0*\n-\t*)\nsit\t(V*)\n-\t(AM*)\n\n"
+    _tar(d / "conll05st-tests.tar.gz", {conll05.WORDS_NAME: gzip.compress(words),
+                                        conll05.PROPS_NAME: gzip.compress(props)})
+    wd, vd, ld = conll05.get_dict()
+    assert ld == {"B-A0": 0, "I-A0": 1, "B-V": 2, "I-V": 3, "B-AM": 4, "I-AM": 5, "O": 6}
+    (s,) = list(conll05.test()())
+    word, n2, n1, c0, p1, p2, pred, mark, lab = s
+    assert word == [1, 2, 3, 4]
+    assert n2 == [wd["The"]] * 4 and n1 == [wd["cat"]] * 4 and c0 == [wd["sat"]] * 4
+    assert p1 == [wd["down"]] * 4 and p2 == [wd["eos"]] * 4 and pred == [0] * 4
+    assert mark == [1, 1, 1, 1]
+    assert lab == [ld["B-A0"], ld["I-A0"], ld["B-V"], ld["B-AM"]]
+
+
+def test_flowers_tgz_and_mat(home):
+    from PIL import Image
+    from scipy.io import savemat
+
+    d = home / "flowers"
+    d.mkdir()
+    files = {}
+    for i in (1, 2, 3):
+        buf = io.BytesIO()
+        Image.fromarray(np.full((240, 300, 3), 40 * i, dtype=np.uint8)).save(buf, format="JPEG", quality=95)
+        files[f"jpg/image_{i:05d}.jpg"] = buf.getvalue()
+    _tar(d / "102flowers.tgz", files)
+    savemat(d / "imagelabels.mat", {"labels": np.array([[5, 17, 102]])})
+    savemat(d / "setid.mat", {"trnid": np.array([[2]]), "tstid": np.array([[1, 3]]), "valid": np.array([[3]])})
+    tr = list(flowers.train()())
+    assert [y for _, y in tr] == [5, 102]
+    assert all(x.shape == (3 * 224 * 224,) and x.dtype == np.float32 for x, _ in tr)
+    (x, y), = list(flowers.test()())
+    assert y == 17
+    # a flat grey image: every pixel of channel c is 80 - mean[c] (BGR order)
+    img = x.reshape(3, 224, 224)
+    for c in range(3):
+        assert abs(float(img[c].mean()) - (80 - flowers.MEAN_BGR[c])) < 2.0

@@ -178,7 +178,9 @@ def test_fp8_linear_numerics_and_grads():
     rel = ((y - ref).norm() / ref.norm()).item()
     assert rel < 0.06  # e4m3 has a 3-bit mantissa
     y.sum().backward()
-    assert torch.allclose(x.grad, torch.ones(64, 96) @ w.t(), atol=1e-5)  # bf16/fp32 straight-through backward
+    dx_ref = torch.ones(64, 96) @ w.t()
+    assert ((x.grad - dx_ref).norm() / dx_ref.norm()).item() < 0.06  # fp8 dgrad (per-row scaled)
+    assert torch.allclose(w.grad, x.detach().t() @ torch.ones(64, 96), atol=1e-4)  # wgrad unquantised
     with torch.no_grad():
         w.mul_(2.0)  # version bump -> re-quantised weight
     assert ((fp8_linear(x, w) - 2 * y).abs().max() / y.abs().max()).item() < 0.1
