@@ -131,8 +131,10 @@ def main():
                                overlap=not args.no_overlap, overlap_allgather=not args.no_overlap,
                                grad_dtype=None if args.bf16_grads else torch.float32)
     nparams = sum(p.numel() for p in model.parameters())
-    mem = (lambda: torch.cuda.memory_allocated(dev) / 2**30) if cuda else (lambda: 0.0)
-    peak = (lambda: torch.cuda.max_memory_allocated(dev) / 2**30) if cuda else (lambda: 0.0)
+    from paddle_amd import platform as _plat
+
+    mem = (lambda: _plat.memory_allocated(local) / 2**30) if cuda else (lambda: 0.0)
+    peak = (lambda: _plat.max_memory_allocated(local) / 2**30) if cuda else (lambda: 0.0)
     if cuda and os.environ.get("FLAGS_allocator_strategy") == "buddy":
         # torch's pluggable-allocator hook keeps no statistics: ask the buddy allocator
         from paddle_amd import runtime as _rt

@@ -133,7 +133,8 @@ def main():
                           "ms_per_step": round(1000 * sec, 2), "dtype": "bf16" + ("+fp8 experts" if a.fp8_experts
                                                                                     else ""),
                           "data": "synthetic", "mfu_bf16_dense": round(tok * fpt / world / 2.5e15, 4),
-                          "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
+                          "peak_mem_gib": round(__import__("paddle_amd.platform", fromlist=["x"]).max_memory_allocated(
+                              torch.cuda.current_device()) / 2**30, 1),
                           "config": {"model": a.model, "micro_batch": a.micro_batch, "grad_accum": a.accum, "seq_len": a.seq_len,
                                      "recompute": a.recompute, "grouped_experts": a.grouped_experts,
                                      "grad_dtype": str(opt.grad_dtype), "dw_kmajor": os.environ.get("PADDLE_AMD_DW_KMAJ", "1"), "parallelism": f"dp{world}+sharding_stage1"},

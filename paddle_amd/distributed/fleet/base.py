@@ -118,6 +118,11 @@ class _Fleet:
             return DataParallel(model, group=hcg.get_data_parallel_group(), bucket_mb=st.fuse_grad_size_in_MB)
         else:
             wrapped = model
+        if isinstance(model, PipelineLayer):
+            # a tied weight held by several stages enters the global grad norm once
+            # (on its first stage); its gradient is summed across them by the pipeline
+            for key, p in model.shared.items():
+                p._pa_norm_skip = min(model.shared_stages.get(key, {hcg.get_stage_id()})) != hcg.get_stage_id()
         if stage3:
             # ZeRO-3 on the sharding axis INSIDE the pipeline stage / TP shard: every
             # block of this stage becomes a gather-on-use unit; tied weights shared
@@ -245,7 +250,7 @@ class HybridParallelOptimizer:
         dist_sq = torch.zeros(1, dtype=torch.float32, device=dev)
         rep_sq = torch.zeros(1, dtype=torch.float32, device=dev)
         for p in params:
-            if p.grad is None:
+            if p.grad is None or getattr(p, "_pa_norm_skip", False):
                 continue
             s = p.grad.float().pow(2).sum()
             if (getattr(p, "is_distributed", False) is True):
@@ -280,7 +285,17 @@ class HybridParallelOptimizer:
             for p in params:
                 if p.grad is not None:
                     p.grad.mul_(coef.to(p.grad.dtype))
-        self._inner.step()
+        # the global (mp x pp) clip above replaces the user optimizer's own, which
+        # would clip again with a local norm
+        inner_clip = [(a, getattr(self._inner, a)) for a in ("_grad_clip", "grad_clip")
+                      if max_norm and getattr(self._inner, a, None) is not None]
+        for a, _ in inner_clip:
+            setattr(self._inner, a, None)
+        try:
+            self._inner.step()
+        finally:
+            for a, v in inner_clip:
+                setattr(self._inner, a, v)
 
     def clear_grad(self, set_to_zero=False):
         if self._sharded is not None:

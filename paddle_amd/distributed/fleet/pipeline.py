@@ -185,15 +185,23 @@ class _P2P:
         ops = []
         from_next = _unmeta(got_next_m.cpu(), self.device) if recv_next else None
         from_prev = _unmeta(got_prev_m.cpu(), self.device) if recv_prev else None
+        # gloo moves host memory only: device tensors are staged through the host
+        # (the RCCL path sends device buffers directly)
+        host = (lambda t: t.detach().cpu()) if not self.nccl else (lambda t: t)
+        land = []
         for t in send_next or []:
-            ops.append(dist.P2POp(dist.isend, t.contiguous(), self.next))
+            ops.append(dist.P2POp(dist.isend, host(t.contiguous()), self.next))
         for t in send_prev or []:
-            ops.append(dist.P2POp(dist.isend, t.contiguous(), self.prev))
-        for t in from_next or []:
-            ops.append(dist.P2POp(dist.irecv, t, self.next))
-        for t in from_prev or []:
-            ops.append(dist.P2POp(dist.irecv, t, self.prev))
+            ops.append(dist.P2POp(dist.isend, host(t.contiguous()), self.prev))
+        for peer, lst in ((self.next, from_next), (self.prev, from_prev)):
+            for t in lst or []:
+                buf = t if (self.nccl or not t.is_cuda) else torch.empty(t.shape, dtype=t.dtype)
+                if buf is not t:
+                    land.append((t, buf))
+                ops.append(dist.P2POp(dist.irecv, buf, peer))
         self._run(ops)
+        for t, buf in land:
+            t.copy_(buf)
         return from_next, from_prev
 
     @staticmethod

@@ -359,7 +359,7 @@ class ParallelExecutor:
             flat = torch.cat([torch.stack([p.tensor.reshape(-1).float().to(dev0) for p in per]).sum(0)
                               for _, _, per in live])
             if self._world > 1:
-                comm.all_reduce(flat)
+                self._cross_process_all_reduce(flat)
             sc_ = self._scale()
             if sc_ != 1.0:
                 flat.mul_(sc_)
@@ -375,6 +375,19 @@ class ParallelExecutor:
                     if reduce_mode and len(self._places) > 1 and r != self._owners.get(pname, 0):
                         continue
                     sc.var(n).set(core.LoDTensor(seg if r == 0 else seg.to(self._device(r)), per[0].lod()))
+
+    def _cross_process_all_reduce(self, flat):
+        """Sum over trainer processes: RCCL, or under ``FLAGS_dp_comm=direct`` the
+        one-/two-shot all-reduce over IPC-mapped peer buffers (parallel/direct.py),
+        created on first use (a collective every trainer reaches in bucket order)."""
+        if os.environ.get("FLAGS_dp_comm", "rccl") == "direct" and flat.is_cuda:
+            if getattr(self, "_direct", None) is None:
+                from ..parallel.direct import DirectAllReduce
+
+                self._direct = DirectAllReduce(max_bytes=256 << 20)
+            self._direct.all_reduce(flat)
+        else:
+            comm.all_reduce(flat)
 
     def _gather_sparse(self, i):
         """Sparse (SelectedRows) gradients: rows of every replica gathered on replica 0,

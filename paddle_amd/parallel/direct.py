@@ -10,7 +10,14 @@ collective is three or four plain kernels on the caller's stream
 * one-shot (messages <= ``one_shot_bytes``): copy-in, barrier, every rank sums
   all P stagings into its output (reads the 7 peers concurrently), barrier;
 * two-shot: copy-in, barrier, rank r reduces chunk r of all stagings into its own
-  staging, barrier, every rank gathers the P reduced chunks, barrier.
+  staging, barrier, every rank gathers the P reduced chunks, barrier;
+* reduce-scatter (ZeRO gradient shards): copy-in, barrier, rank r sums chunk r of
+  the P stagings straight into its shard, barrier;
+* all-gather (ZeRO parameter shards): copy the shard into chunk r of the own
+  staging, barrier, every rank reads the P chunks into its output, barrier.
+
+The training path uses these under ``FLAGS_dp_comm=direct``
+(parallel/sharding.py FlatShardedOptimizer); RCCL stays the default.
 
 Barriers are bounded spins on system-scope signals: a missing peer makes the op
 fail (``DirectAllReduce.check``) instead of hanging the device.  Reference
@@ -118,6 +125,69 @@ class DirectAllReduce:
             N.call("pa_p2p_gather", dt, self._stage, self._sig, self.world, self.rank, N.ptr(t), n, chunk, N.stream())
         self._barrier()  # nobody refills its staging before every peer has read it
         return t
+
+    def _dense_ok(self, *ts):
+        return all(t.is_cuda and t.is_contiguous() and t.dtype in (torch.float32, torch.bfloat16) for t in ts)
+
+    def reduce_scatter(self, out, inp):
+        """out[:] = sum over ranks of inp[rank * L:(rank + 1) * L], L = out.numel()."""
+        L = out.numel()
+        n = inp.numel()
+        if self.world == 1:
+            out.copy_(inp)
+            return out
+        es = inp.element_size()
+        if (n != L * self.world or L % 8 or out.dtype != inp.dtype or n * es > self.max_bytes
+                or not self._dense_ok(out, inp)):
+            comm.reduce_scatter(out, inp, self.group)
+            return out
+        own = _P(self._stage[self.rank])
+        N.call("pa_p2p_copy", own, N.ptr(inp), n * es, N.stream())
+        self._barrier()
+        b = self.rank * L
+        # the kernel writes out[i] for absolute i in [b, b + L): shift the base
+        N.call("pa_p2p_reduce", N.dt(inp), self._stage, self._sig, self.world, self.rank,
+               _P(out.data_ptr() - b * es), b, b + L, N.stream())
+        self._barrier()
+        return out
+
+    def all_gather(self, out, shard):
+        """out[r * L:(r + 1) * L] = shard of rank r, L = shard.numel()."""
+        L = shard.numel()
+        n = out.numel()
+        if self.world == 1:
+            out.copy_(shard)
+            return out
+        es = shard.element_size()
+        if (n != L * self.world or L % 8 or out.dtype != shard.dtype or n * es > self.max_bytes
+                or not self._dense_ok(out, shard)):
+            comm.all_gather(out, shard, self.group)
+            return out
+        N.call("pa_p2p_copy", _P(self._stage[self.rank] + self.rank * L * es), N.ptr(shard), L * es, N.stream())
+        self._barrier()
+        N.call("pa_p2p_gather", N.dt(out), self._stage, self._sig, self.world, self.rank, N.ptr(out), n, L,
+               N.stream())
+        self._barrier()
+        return out
+
+    def error_async(self):
+        """Start copying the timeout flag to the host; ``poll_error`` reads it later
+        (no stream synchronisation on the step path)."""
+        if not hasattr(self, "_err_host"):
+            self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._err_ev = None
+        self._err_host.copy_(self._err, non_blocking=True)
+        self._err_ev = torch.cuda.current_stream().record_event()
+
+    def poll_error(self):
+        """Raise if a barrier of an earlier step timed out (waits only for that copy)."""
+        ev = getattr(self, "_err_ev", None)
+        if ev is None:
+            return
+        ev.synchronize()
+        e = int(self._err_host[0])
+        if e:
+            raise RuntimeError(f"direct collectives: rank {self.rank} timed out waiting for peer {e - 1}")
 
     def close(self):
         lib = N.lib()

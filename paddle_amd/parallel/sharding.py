@@ -34,7 +34,9 @@ seed of what is done here, MI355X-first:
 """
 from __future__ import annotations
 
+import contextlib
 import math
+import os
 
 import torch
 
@@ -54,7 +56,7 @@ class FlatShardedOptimizer:
 
     def __init__(self, named_params, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1,
                  group=None, bucket_mb=256, grad_clip=None, overlap=True, stage=1,
-                 no_decay_fn=None, overlap_allgather=False, grad_dtype="auto"):
+                 no_decay_fn=None, overlap_allgather=False, grad_dtype="auto", dp_comm=None):
         named = [(n, p) for n, p in named_params if p.requires_grad]
         if not named:
             raise ValueError("no trainable parameters")
@@ -156,6 +158,16 @@ class FlatShardedOptimizer:
         # deferred all-gathers: [(bucket, cuda event | deferred callable)] in issue order
         self.overlap_allgather = bool(overlap_allgather) and self.W > 1
         self._ag_queue = []
+        # FLAGS_dp_comm=direct: reduce-scatter / all-gather over IPC-mapped peer
+        # buffers on the xGMI links (parallel/direct.py) instead of RCCL
+        self.dp_comm = os.environ.get("FLAGS_dp_comm", "rccl") if dp_comm is None else dp_comm
+        self._direct = None
+        if self.dp_comm == "direct" and self.W > 1 and dev.type == "cuda":
+            from .direct import DirectAllReduce
+
+            big = max(be - bs for bs, be, _ in buckets) * max(self.flat_grad.element_size(),
+                                                              self.flat_param.element_size())
+            self._direct = DirectAllReduce(group, max_bytes=big)
         self._hooks = []
         if self.W > 1 or self.main_grad:
             for p in self.params:
@@ -210,13 +222,15 @@ class FlatShardedOptimizer:
             fused.join_dw_streams(self.device)
         bs, be, _ = self.buckets[b]
         s0, L, so = self.shard_slices[b]
+        rs = self._direct.reduce_scatter if self._direct is not None else \
+            (lambda o, i: comm.reduce_scatter(o, i, self.group))
         if self.overlap:
             ev = torch.cuda.current_stream(self.device).record_event()
             self.comm_stream.wait_event(ev)
             with torch.cuda.stream(self.comm_stream):
-                comm.reduce_scatter(self.grad_shard[so:so + L], self.flat_grad[bs:be], self.group)
+                rs(self.grad_shard[so:so + L], self.flat_grad[bs:be])
         else:
-            comm.reduce_scatter(self.grad_shard[so:so + L], self.flat_grad[bs:be], self.group)
+            rs(self.grad_shard[so:so + L], self.flat_grad[bs:be])
 
     def _finish_comm(self):
         if self.W == 1:
@@ -249,7 +263,10 @@ class FlatShardedOptimizer:
     def _gather(self, b):
         bs, be, _ = self.buckets[b]
         s0, L, so = self.shard_slices[b]
-        comm.all_gather(self.flat_param[bs:be], self.param_shard[so:so + L], self.group)
+        if self._direct is not None:
+            self._direct.all_gather(self.flat_param[bs:be], self.param_shard[so:so + L])
+        else:
+            comm.all_gather(self.flat_param[bs:be], self.param_shard[so:so + L], self.group)
 
     def _issue_allgathers(self):
         """Queue every bucket's all-gather, forward order first (the last bucket
@@ -301,6 +318,8 @@ class FlatShardedOptimizer:
     def step(self, lr=None):
         if lr is not None:
             self.lr = lr
+        if self._direct is not None:
+            self._direct.poll_error()  # a peer timeout of the previous step raises here
         self.sync_params()
         if self.device.type == "cuda":
             fused.join_dw_streams(self.device)
@@ -319,6 +338,9 @@ class FlatShardedOptimizer:
             else:
                 for b in range(len(self.buckets)):
                     self._gather(b)
+        if self._direct is not None:
+            with torch.cuda.stream(self.comm_stream) if self.overlap else contextlib.nullcontext():
+                self._direct.error_async()
         fused.bump_weight_epoch()
 
     def zero_grad(self, set_to_none=False):

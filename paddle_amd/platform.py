@@ -91,23 +91,34 @@ def device_memory_info(dev=0):
 
 def memory_stats(dev=0):
     """Allocator + device view of memory (reference: the memory-usage VLOGs of
-    buddy_allocator.cc / gpu_info.cc)."""
-    out = {}
-    if os.environ.get("FLAGS_allocator_strategy") == "buddy":
-        from . import runtime
+    buddy_allocator.cc / gpu_info.cc): ``allocated`` / ``reserved`` / ``peak`` bytes
+    from whichever allocator backs torch (the buddy allocator's peak is the sum of
+    its per-stream pool peaks, an upper bound), plus the device's free / total."""
+    from . import runtime
 
-        out.update({f"buddy_{k}": v for k, v in runtime.torch_allocator_stats(dev).items()})
+    out = {}
+    if runtime.buddy_active():
+        st = runtime.torch_allocator_stats(dev)
+        out.update(allocated=st["used"], reserved=st["reserved"], peak=st["peak"], allocator="buddy")
     else:
-        out["allocated"] = torch.cuda.memory_allocated(dev)
-        out["reserved"] = torch.cuda.memory_reserved(dev)
-        out["peak"] = torch.cuda.max_memory_allocated(dev)
+        out.update(allocated=torch.cuda.memory_allocated(dev), reserved=torch.cuda.memory_reserved(dev),
+                   peak=torch.cuda.max_memory_allocated(dev), allocator="torch_caching")
     free, total = device_memory_info(dev)
     out.update(device_free=free, device_total=total)
     return out
+
+
+def memory_allocated(dev=0):
+    return memory_stats(dev)["allocated"]
+
+
+def max_memory_allocated(dev=0):
+    return memory_stats(dev)["peak"]
 
 
 def log_memory(tag, dev=0):
     if torch.cuda.is_available():
         st = memory_stats(dev)
         vlog(0 if os.environ.get("FLAGS_log_memory_stats") == "1" else 1,
-             f"memory[{tag}] " + " ".join(f"{k}={v / 2**30:.2f}GiB" for k, v in st.items()))
+             f"memory[{tag}] " + " ".join(f"{k}={v / 2**30:.2f}GiB" if isinstance(v, int) else f"{k}={v}"
+                                          for k, v in st.items()))

@@ -250,6 +250,16 @@ def use_buddy_allocator_for_torch(chunk_bytes=4 << 30):
     rs = ctypes.cast(getattr(ctypes.CDLL(_build.RUNTIME_LIB), "pa_torch_record_stream"), ctypes.c_void_p).value
     alloc._allocator.set_record_stream_fn(rs)
     torch.cuda.memory.change_current_allocator(alloc)
+    global _BUDDY_ACTIVE
+    _BUDDY_ACTIVE = True
+
+
+_BUDDY_ACTIVE = False
+
+
+def buddy_active():
+    """True when torch's device allocations come from the buddy allocator."""
+    return _BUDDY_ACTIVE
 
 
 def torch_deferred_frees():

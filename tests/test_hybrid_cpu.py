@@ -8,118 +8,15 @@ embedding kept whole, summed across the two stages); HybridParallelOptimizer han
 lr / betas / eps / clip to the sharded engine.  Reference seed of the sharding side:
 framework/details/multi_devices_graph_pass.cc:247 (GetAppropriateDeviceID), :412-452.
 """
-import math
-
 import pytest
-import torch
 
 from dist_util import run_dist
-from paddle_amd.models.gpt import (GPT_CONFIGS, GPTConfig, GPTPretrainingCriterion, gpt_pipeline_descs,
-                                   shard_gpt_state_dict)
-
-LR, CLIP, STEPS, M, LAYERS = 2e-3, 0.05, 3, 2, 4
-
-
-def _cfg():
-    return GPTConfig(**{**GPT_CONFIGS["gpt-tiny"], "num_hidden_layers": LAYERS}, dtype="float32")
-
-
-def _batch(step, B=8, S=16, V=512):
-    return torch.randint(0, V, (B, S + 1), generator=torch.Generator().manual_seed(100 + step))
-
-
-def _reference():
-    from paddle_amd.distributed.fleet.pipeline import PipelineLayer
-
-    cfg = _cfg()
-    crit = GPTPretrainingCriterion()
-    model = PipelineLayer(gpt_pipeline_descs(cfg, "cpu"), num_stages=1, loss_fn=crit, seed=11)
-    init = {k: v.detach().clone() for k, v in model.state_dict().items()}
-    params = [p for p in model.parameters() if p.requires_grad]
-    st = {id(p): (torch.zeros_like(p), torch.zeros_like(p)) for p in params}
-    losses = []
-    for s in range(STEPS):
-        b = _batch(s)
-        tot = 0.0
-        # 2 sharding ranks x M micro-batches, equal sizes: mean over 2M micro-batch losses
-        for mb in b.chunk(2 * M):
-            loss = crit(model(mb[:, :-1]), mb[:, 1:]) / (2 * M)
-            loss.backward()
-            tot += loss.item()
-        losses.append(tot)
-        with torch.no_grad():
-            norm = math.sqrt(sum(float(p.grad.pow(2).sum()) for p in params if p.grad is not None))
-            coef = min(1.0, CLIP / (norm + 1e-6))
-            b1, b2, eps = 0.9, 0.999, 1e-5
-            for p in params:
-                if p.grad is None:
-                    continue
-                g = p.grad * coef
-                m, v = st[id(p)]
-                m.mul_(b1).add_(g, alpha=1 - b1)
-                v.mul_(b2).addcmul_(g, g, value=1 - b2)
-                p.addcdiv_(m / (1 - b1 ** (s + 1)), (v / (1 - b2 ** (s + 1))).sqrt() + eps, value=-LR)
-                p.grad = None
-    return losses, init, {k: v.detach().clone() for k, v in model.state_dict().items()}
-
-
-def _worker(rank, world, init):
-    import paddle_amd
-    from paddle_amd.distributed.fleet import DistributedStrategy, TPGroup, fleet
-    from paddle_amd.distributed.fleet.pipeline import PipelineLayer
-
-    st = DistributedStrategy()
-    st.hybrid_configs = {"dp_degree": 1, "mp_degree": 2, "pp_degree": 2, "sharding_degree": 2}
-    st.sharding = True
-    st.sharding_configs = {"stage": 3}
-    st.pipeline_configs = {"accumulate_steps": M}
-    fleet.init(is_collective=True, strategy=st)
-    hcg = fleet.get_hybrid_communicate_group()
-    assert hcg.get_model_parallel_world_size() * hcg.get_pipe_parallel_world_size() * \
-        hcg.get_sharding_parallel_world_size() == world
-    cfg = _cfg()
-    tp = TPGroup(hcg.get_model_parallel_group())
-    layer = PipelineLayer(gpt_pipeline_descs(cfg, "cpu", tp), hcg=hcg, loss_fn=GPTPretrainingCriterion(tp), seed=11)
-    lo = layer.bounds[hcg.get_stage_id()]
-    full = {}
-    for k in layer.state_dict():
-        parts = k.split(".")
-        gk = ".".join([parts[0], str(lo + int(parts[1]))] + parts[2:])
-        full[k] = init[gk]
-    mp_r, mp_w = hcg.get_model_parallel_rank(), hcg.get_model_parallel_world_size()
-    layer.load_state_dict(shard_gpt_state_dict(full, cfg, mp_r, mp_w))
-    model = fleet.distributed_model(layer)
-    assert getattr(model, "_sharded", None) is not None
-    inner = paddle_amd.optimizer.AdamW(learning_rate=LR, parameters=list(layer.parameters()), weight_decay=0.0, epsilon=1e-5,
-                                       grad_clip=paddle_amd.optimizer.clip.ClipGradByGlobalNorm(CLIP))
-    opt = fleet.distributed_optimizer(inner)
-    sr, sw = hcg.get_sharding_parallel_rank(), hcg.get_sharding_parallel_world_size()
-    losses = []
-    for s in range(STEPS):
-        b = _batch(s).chunk(sw)[sr]
-        loss = model.train_batch((b[:, :-1], b[:, 1:]), opt)
-        t = loss.detach().reshape(1).clone()
-        torch.distributed.all_reduce(t, group=hcg.get_sharding_parallel_group())
-        losses.append(float(t) / sw)
-    sd = model._sharded.full_state_dict()
-    return losses, sd, lo, mp_r, mp_w
+from hybrid_common import M, check, reference, worker
 
 
 @pytest.mark.timeout(600)
 def test_gpt_tp2_pp2_sharding3_matches_single_process():
-    ref_losses, init, ref_final = _reference()
-    res = run_dist(_worker, 8, init)
-    cfg = _cfg()
-    for losses, sd, lo, mp_r, mp_w in res:
-        for a, b in zip(losses, ref_losses):
-            assert abs(a - b) < 2e-5, (losses, ref_losses)
-        # final parameters: this rank's TP shard of the reference's
-        full = {}
-        for k in sd:
-            parts = k.split(".")
-            full[k] = ref_final[".".join([parts[0], str(lo + int(parts[1]))] + parts[2:])]
-        want = shard_gpt_state_dict(full, cfg, mp_r, mp_w)
-        for k, v in sd.items():
-            if "position_embeddings" in k and v.shape == want[k].shape and lo > 0:
-                continue  # the head stage's copy of the shared module's position table is unused
-            torch.testing.assert_close(v.float(), want[k].float(), atol=2e-5, rtol=1e-3, msg=k)
+    # 2 sharding ranks x M micro-batches, equal sizes: mean over 2M micro-batch losses
+    ref_losses, init, ref_final = reference(2 * M)
+    res = run_dist(worker, 8, init, 2, 2, 2, "cpu")
+    check(res, ref_losses, ref_final, loss_tol=2e-5, atol=2e-5)

@@ -33,7 +33,7 @@ for step in range(steps):
     opt.zero_grad()
     losses.append(float(loss))
 torch.cuda.synchronize()
-out = {"losses": losses, "allocator": os.environ.get("FLAGS_allocator_strategy", "torch_caching")}
+out = {"losses": losses, "allocator": os.environ.get("FLAGS_allocator_strategy", "buddy")}
 if out["allocator"] == "buddy" and runtime.available():
     out["buddy"] = runtime.torch_allocator_stats(0)
 print(json.dumps(out))
