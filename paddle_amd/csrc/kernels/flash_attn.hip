@@ -1029,12 +1029,292 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_kernel3(BwdParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Backward v5: 4 waves x 32 keys = 128 keys of one (b, head) per workgroup, ONE wave
+// per SIMD, MFMA 32x32x16 throughout (v3 uses 16x16x32 on 16 keys / wave and is
+// bound by LDS operand reads: a 32x32x16 MFMA reads a quarter of the operand bytes
+// per multiply-add).  Per wave, for the whole sweep over 32-row query slices:
+// dK^T, dV^T of its 32 keys (128 accumulator registers) and its V rows (registers).
+//   S  = Q K^T and dP = dO V^T with the key on the lane (B operand = K / V rows of the
+//        wave's keys; A = Q / dO rows of the slice).  The accumulators start at
+//        -lse/scale and -delta, so p = exp2(scale_log2 * S) and dS = p * dP * scale
+//        need no further row constants;
+//   dV^T += dO^T P and dK^T += Q^T dS take P / dS straight from those accumulators as
+//        B operands (register j of k-step st is query slot 16 st + 8 hh + j, which is
+//        row 16 st + 8 (j >> 2) + 4 hh + (j & 3): the dO^T / Q^T A operands are two
+//        4-row transposed reads of the same rows);
+//   dS^T goes to LDS ([key][q], XOR-swizzled 8-B slots) and, after the slice's one
+//        barrier, wave w computes dQ^T for head dims 32w..32w+31 over the block's 128
+//        keys (A = K^T and B = dS^T, both transposed reads) and stores the bf16
+//        partial of this key block (summed per query by fa_dq_reduce_rope).
+// Every LDS operand is read two k-steps ahead of its MFMAs (three register sets,
+// sched barriers stop the compiler from hoisting all reads of the unrolled loops).
+// Q / dO / lse / delta of slice t+1 are loaded into registers during slice t and
+// written into the other LDS stage before the barrier; dS^T is double-buffered, so
+// one barrier per slice orders everything.  D = 128, Sk % 128 == 0, Sq % 32 == 0.
+__device__ __forceinline__ int ds_off(int key, int q) {
+  // [128 keys][32 q] bf16, 64-B rows; 8-B slot XOR-swizzled by key so the per-key
+  // b64 stores of 16 consecutive keys hit distinct banks
+  return key * 64 + ((((q >> 2) ^ ((key >> 1) & 7)) << 3) | ((q & 3) << 1));
+}
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void fa_bwd_kernel5(BwdParams p) {
+  constexpr int D = 128, BK = 128, BQ = 32;
+  constexpr int K_BYTES = BK * D * 2;            // 32 KB  K image (dual layout)
+  constexpr int V_BYTES = BK * D * 2;            // 32 KB  V image (row reads only, same swizzle)
+  constexpr int Q_BYTES = BQ * D * 2;            // 8 KB
+  constexpr int STAGE = 2 * Q_BYTES + 2 * BQ * 4;
+  constexpr int DSB = BK * BQ * 2;               // 8 KB  dS^T [key][q]
+  __shared__ __attribute__((aligned(16))) char smem[K_BYTES + V_BYTES + 2 * STAGE + 2 * DSB];
+  char* Ks = smem;
+  char* Vs = smem + K_BYTES;
+  char* stage0 = Vs + V_BYTES;
+  char* dsbuf0 = stage0 + 2 * STAGE;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int G = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;  // transposed-read lane roles
+  const int h = blockIdx.x, b = blockIdx.y, kb = blockIdx.z;
+  const int kvh = h / (p.Hq / p.Hkv);
+  const int n0 = kb * BK;
+  const int offs = CAUSAL ? p.Sk - p.Sq : 0;
+  const int key_w0 = n0 + 32 * w;
+  const int mykey = key_w0 + l32;
+
+  const u16* qp = p.q + (long)b * p.q_bs + (long)h * p.q_hs;
+  const u16* dop = p.dout + (long)b * p.do_bs + (long)h * p.do_hs;
+  const u16* kp = p.k + (long)b * p.k_bs + (long)kvh * p.k_hs;
+  const u16* vp = p.v + (long)b * p.v_bs + (long)kvh * p.v_hs;
+  const float* lsep = p.lse + ((long)b * p.Hq + h) * p.Sq;
+  const float* dlp = p.delta + ((long)b * p.Hq + h) * p.Sq;
+  u16* part = (u16*)p.dq_part + (((long)kb * p.B + b) * p.Hq + h) * (long)p.Sq * D;
+
+  int qstart = 0;
+  if (CAUSAL) qstart = max(0, n0 - offs);
+  qstart = (qstart / BQ) * BQ;
+
+  // ---- K and V images (dual layout) for the whole sweep
+  for (int idx = tid; idx < BK * (D / 8); idx += 256) {
+    const int row = idx >> 4, ch = idx & 15;
+    const int o = dual_off<D>(row, ch * 16);
+    *reinterpret_cast<u16x8*>(Ks + o) = *reinterpret_cast<const u16x8*>(kp + (long)(n0 + row) * p.k_ss + ch * 8);
+    *reinterpret_cast<u16x8*>(Vs + o) = *reinterpret_cast<const u16x8*>(vp + (long)(n0 + row) * p.v_ss + ch * 8);
+  }
+
+  // ---- lane-constant LDS offsets.  dual_off's XOR depends on the row only through
+  // row & 15, so every k-step / d-block / key-step variant below is one of these plus
+  // a compile-time constant (an instruction immediate), not a fresh computation.
+  const int dsw = ((l32 & 3) << 2) | ((l32 >> 2) & 3);     // swizzle of rows l32 and 32w + l32
+  int s_off[8];                                            // chunk (2 ks + hh) of a row read
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) s_off[ks] = ((2 * ks + hh) ^ dsw) << 4;
+  const int q_row = l32 * 256, k_row = (32 * w + l32) * 256;
+  // transposed reads of the slice (dO^T / Q^T): rows 4(G>>1) + qq (+8) (+16 s2 = +4096)
+  int t_off[4][2];
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int r = 4 * (G >> 1) + qq + 8 * hf;
+      t_off[db][hf] = dual_off<D>(r, (32 * db + 16 * (G & 1) + 4 * pp) * 2);
+    }
+  // dQ: K^T rows 8(G>>1) + qq (+4) (+16 ks = +4096 ks); dS^T rows likewise (+1024 ks)
+  const int kr0 = 8 * (G >> 1) + qq;
+  const int kcolb = (32 * w + 16 * (G & 1) + 4 * pp) * 2;
+  const int qcol = 16 * (G & 1) + 4 * pp;
+  const int kt_off0 = dual_off<D>(kr0, kcolb), kt_off1 = dual_off<D>(kr0 + 4, kcolb);
+  const int ds_off0 = ds_off(kr0, qcol), ds_off1 = ds_off(kr0 + 4, qcol);
+
+  // ---- slice prefetch: 2 Q chunks + 2 dO chunks per thread, lse / delta by 32 threads
+  const int srow = tid >> 3, sch = (tid & 7) * 2;   // 32 rows x 16 chunks = 512 = 2 / thread
+  const int st_off0 = dual_off<D>(srow, sch * 16), st_off1 = dual_off<D>(srow, sch * 16 + 16);
+  struct Pf {
+    u16x8 q0, q1, o0, o1;
+    float l, d;
+  };
+  auto load_regs = [&](Pf& r, int qt0) {
+    const u16* qr = qp + (long)(qt0 + srow) * p.q_ss + sch * 8;
+    const u16* orow = dop + (long)(qt0 + srow) * p.do_ss + sch * 8;
+    r.q0 = *reinterpret_cast<const u16x8*>(qr);
+    r.q1 = *reinterpret_cast<const u16x8*>(qr + 8);
+    r.o0 = *reinterpret_cast<const u16x8*>(orow);
+    r.o1 = *reinterpret_cast<const u16x8*>(orow + 8);
+    const int qi = qt0 + (tid & 31);
+    r.l = lsep[qi];
+    r.d = dlp[qi];
+  };
+  const float inv_scale = 1.f / p.scale;
+  auto store_lds = [&](const Pf& r, char* st) {
+    *reinterpret_cast<u16x8*>(st + st_off0) = r.q0;
+    *reinterpret_cast<u16x8*>(st + st_off1) = r.q1;
+    *reinterpret_cast<u16x8*>(st + Q_BYTES + st_off0) = r.o0;
+    *reinterpret_cast<u16x8*>(st + Q_BYTES + st_off1) = r.o1;
+    float* lc = (float*)(st + 2 * Q_BYTES);
+    if (tid < 32) {
+      lc[tid] = -r.l * inv_scale;  // S accumulator start: p = exp2(scale_log2 * (S - lse / scale))
+      lc[BQ + tid] = -r.d;         // dP accumulator start: dS = p * (dP - delta) * scale
+    }
+  };
+
+  // dK^T / dV^T live in AGPRs for the whole sweep: their definition before the loop
+  // and their read after it are asm statements with AGPR ("a") operands, so hipcc
+  // allocates the loop-carried values there instead of shuttling them through VGPRs
+  // around each MFMA (the MFMAs themselves stay builtins: hipcc places their hazard
+  // wait states, which it does not do for MFMAs written in inline asm)
+  f32x16 dk[4], dv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f32x16 z;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) z[e] = 0.f;
+    asm volatile("" : "=a"(dk[i]) : "0"(z));
+    asm volatile("" : "=a"(dv[i]) : "0"(z));
+  }
+
+  const int nslices = (p.Sq - qstart) / BQ;
+  Pf pf;
+  if (nslices > 0) {
+    load_regs(pf, qstart);
+    store_lds(pf, stage0);
+  }
+  lds_barrier();
+
+  for (int t = 0; t < nslices; ++t) {
+    const int q0 = qstart + t * BQ;
+    char* st = stage0 + (t & 1) * STAGE;
+    char* dsb = dsbuf0 + (t & 1) * DSB;
+    const char* Qs = st;
+    const char* Os = st + Q_BYTES;
+    const float* lc = (const float*)(st + 2 * Q_BYTES);
+    const bool more = t + 1 < nslices;
+    if (more) load_regs(pf, q0 + BQ);
+
+    const bool wave_masked = CAUSAL && (q0 + BQ - 1 + offs < key_w0);
+    const bool wave_diag = CAUSAL && !(key_w0 + 31 <= q0 + offs);
+    if (!wave_masked) {
+      // ---- S, dP (accumulators start at the row constants)
+      f32x16 sacc, dpacc;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(lc + 8 * i + 4 * hh);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(lc + BQ + 8 * i + 4 * hh);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          sacc[4 * i + j] = l4[j];
+          dpacc[4 * i + j] = d4[j];
+        }
+      }
+      bf8v sq[3], so[3], sk[3], sv[3];
+      auto sload = [&](int j, int ks) {
+        sq[j] = as_bf8(*reinterpret_cast<const u16x8*>(Qs + q_row + s_off[ks]));
+        so[j] = as_bf8(*reinterpret_cast<const u16x8*>(Os + q_row + s_off[ks]));
+        sk[j] = as_bf8(*reinterpret_cast<const u16x8*>(Ks + k_row + s_off[ks]));
+        sv[j] = as_bf8(*reinterpret_cast<const u16x8*>(Vs + k_row + s_off[ks]));
+      };
+      sload(0, 0);
+      sload(1, 1);
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        if (ks + 2 < 8) sload((ks + 2) % 3, ks + 2);
+        sacc = mfma32(sq[ks % 3], sk[ks % 3], sacc);
+        dpacc = mfma32(so[ks % 3], sv[ks % 3], dpacc);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // ---- P, dS as bf16 B operands: register r <-> query 8 (r >> 2) + 4 hh + (r & 3)
+      bf8v pB[2], dB[2];
+      const int lim = mykey - offs - q0 - 4 * hh;  // masked when 8 (r>>2) + (r&3) < lim
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float pv = __builtin_amdgcn_exp2f(sacc[r] * p.scale_log2);
+        if (wave_diag) pv = (8 * (r >> 2) + (r & 3)) >= lim ? pv : 0.f;
+        pB[r >> 3][r & 7] = (__bf16)pv;
+        dB[r >> 3][r & 7] = (__bf16)(pv * dpacc[r] * p.scale);
+      }
+      // ---- dV^T += dO^T P, dK^T += Q^T dS: 8 (d block, k-step) pairs
+      bf8v to[3], tq[3];
+      auto tload = [&](int j, int it) {
+        const int db = it >> 1, s2 = it & 1;
+        to[j] = cat_tr(tr_read(Os, t_off[db][0] + 4096 * s2), tr_read(Os, t_off[db][1] + 4096 * s2));
+        tq[j] = cat_tr(tr_read(Qs, t_off[db][0] + 4096 * s2), tr_read(Qs, t_off[db][1] + 4096 * s2));
+      };
+      tload(0, 0);
+      tload(1, 1);
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        if (it + 2 < 8) tload((it + 2) % 3, it + 2);
+        dv[it >> 1] = mfma32(to[it % 3], pB[it & 1], dv[it >> 1]);
+        dk[it >> 1] = mfma32(tq[it % 3], dB[it & 1], dk[it >> 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // ---- dS^T -> LDS [key][q]: 4 consecutive queries per 8-B store
+      const int key = 32 * w + l32;
+      const u16x8 lo = __builtin_bit_cast(u16x8, dB[0]), hi = __builtin_bit_cast(u16x8, dB[1]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const u16x8& src = i < 2 ? lo : hi;
+        const int o = 4 * (i & 1);
+        const u16x4 v4 = {src[o], src[o + 1], src[o + 2], src[o + 3]};
+        *reinterpret_cast<u16x4*>(dsb + ds_off(key, 8 * i + 4 * hh)) = v4;
+      }
+    } else {
+      const u16x4 z = {0, 0, 0, 0};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) *reinterpret_cast<u16x4*>(dsb + ds_off(32 * w + l32, 8 * i + 4 * hh)) = z;
+    }
+    if (more) store_lds(pf, stage0 + ((t + 1) & 1) * STAGE);
+    lds_barrier();
+    // ---- dQ^T[d = 32w + m][q = n] = sum over the block's 128 keys of K[key][d] dS^T[key][q]
+    f32x16 dq;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) dq[e] = 0.f;
+    bf8v qk[3], qs_[3];
+    auto qload = [&](int j, int ks) {
+      qk[j] = cat_tr(tr_read(Ks, kt_off0 + 4096 * ks), tr_read(Ks, kt_off1 + 4096 * ks));
+      qs_[j] = cat_tr(tr_read(dsb, ds_off0 + 1024 * ks), tr_read(dsb, ds_off1 + 1024 * ks));
+    };
+    qload(0, 0);
+    qload(1, 1);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      if (ks + 2 < 8) qload((ks + 2) % 3, ks + 2);
+      dq = mfma32(qk[ks % 3], qs_[ks % 3], dq);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // lane: q = q0 + l32; d = 32w + 8i + 4hh + 0..3 -> bf16 partial of this key block
+    u16* prow = part + (long)(q0 + l32) * D + 32 * w + 4 * hh;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const u16x4 v4 = {f2bf(dq[4 * i]), f2bf(dq[4 * i + 1]), f2bf(dq[4 * i + 2]), f2bf(dq[4 * i + 3])};
+      *reinterpret_cast<u16x4*>(prow + 8 * i) = v4;
+    }
+  }
+  // ---- dK / dV: element (db, r) = key mykey, d = 32db + 8(r>>2) + 4hh + (r&3)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    asm volatile("" : "+a"(dk[i]));
+    asm volatile("" : "+a"(dv[i]));
+  }
+  u16* dkp = p.dk + (long)b * p.dk_bs + (long)h * p.dk_hs + (long)mykey * p.dk_ss;
+  u16* dvp = p.dv + (long)b * p.dk_bs + (long)h * p.dk_hs + (long)mykey * p.dk_ss;
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int d = 32 * db + 8 * i + 4 * hh;
+      const u16x4 k4 = {f2bf(dk[db][4 * i]), f2bf(dk[db][4 * i + 1]), f2bf(dk[db][4 * i + 2]), f2bf(dk[db][4 * i + 3])};
+      const u16x4 v4 = {f2bf(dv[db][4 * i]), f2bf(dv[db][4 * i + 1]), f2bf(dv[db][4 * i + 2]), f2bf(dv[db][4 * i + 3])};
+      *reinterpret_cast<u16x4*>(dkp + d) = k4;
+      *reinterpret_cast<u16x4*>(dvp + d) = v4;
+    }
+}
+
 // dq_acc[b, q, h, :] = sum of the key-block partials that cover query q (v4).  The
 // causal kernel for key block kb starts at query floor(max(0, 128kb - offs) / 32) * 32
 // and writes every query from there (masked ones as zeros), so exactly those blocks
 // are summed.  One thread per 4 consecutive d (16-B loads/stores).
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256) void fa_bwd_dq_reduce(BwdParams p, int nkb) {
+__global__ __launch_bounds__(256) void fa_bwd_dq_reduce(BwdParams p, int nkb, int kblk) {
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long total = (long)p.B * p.Hq * p.Sq * (D / 4);
   if (gid >= total) return;
@@ -1049,7 +1329,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_reduce(BwdParams p, int nkb) {
   const u16* src = (const u16*)p.dq_part + ((long)b * p.Hq + h) * p.Sq * D + q * D + 4 * d4;
   for (int kb = 0; kb < nkb; ++kb) {
     if (CAUSAL) {
-      long qs = 128L * kb - offs;
+      long qs = (long)kblk * kb - offs;
       qs = qs > 0 ? (qs / 32) * 32 : 0;
       if (qs > q) break;
     }
@@ -1068,7 +1348,7 @@ template <bool CAUSAL>
 __global__ __launch_bounds__(256) void fa_dq_reduce_rope(const float* __restrict__ part, int nkb, int B,
                                                          int Sq, int Sk, int Hq, u16* __restrict__ out,
                                                          long out_ts, const float* __restrict__ cosT,
-                                                         const float* __restrict__ sinT) {
+                                                         const float* __restrict__ sinT, int kblk) {
   constexpr int D = 128, HALF = 64;
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long total = (long)B * Hq * Sq * (HALF / 4);
@@ -1084,7 +1364,7 @@ __global__ __launch_bounds__(256) void fa_dq_reduce_rope(const float* __restrict
   f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
   for (int kb = 0; kb < nkb; ++kb) {
     if (CAUSAL) {
-      long qs = 128L * kb - offs;
+      long qs = (long)kblk * kb - offs;
       qs = qs > 0 ? (qs / 32) * 32 : 0;
       if (qs > q) break;
     }
@@ -1110,7 +1390,8 @@ __global__ __launch_bounds__(256) void fa_dq_reduce_rope(const float* __restrict
 }
 
 // 0 = fa_bwd_kernel, 1 = pipelined, 2 = probe without dQ atomics (wrong dQ),
-// 3 = 8-wave MFMA16 (D = 128), 4 = v3 with per-key-block dQ partials + reduce (needs dq_part)
+// 3 = 8-wave MFMA16 (D = 128), 4 = v3 with per-key-block dQ partials + reduce (needs dq_part),
+// 5 = 4 waves x 32 keys, MFMA 32x32x16 + partials (D = 128, causal, Sk % 128, Sq % 32; else v4)
 // default: v4 (causal D = 128: 1.50 ms + 0.46 ms reduce vs v2 2.18 ms at B8 H32 S2048);
 // other shapes fall back to v2 in the launcher
 static int g_fa_bwd_variant = 4;
@@ -1125,6 +1406,17 @@ PA_EXPORT int pa_fa_bwd_set_variant(int v) {
 }
 
 PA_EXPORT int pa_fa_bwd_get_variant() { return g_fa_bwd_variant; }
+
+static bool fa_v5_ok(int Sq, int Sk, int D, int causal) {
+  return g_fa_bwd_variant == 5 && D == 128 && causal && Sk % 128 == 0 && Sq % 32 == 0 && Sq > 0;
+}
+
+// key rows per dQ partial slab of the partial-slab path (0: that path is off)
+PA_EXPORT int pa_fa_bwd_part_kblk(int Sq, int Sk, int D, int causal) {
+  if (fa_v5_ok(Sq, Sk, D, causal)) return 128;
+  if ((g_fa_bwd_variant == 4 || g_fa_bwd_variant == 5) && D == 128 && causal) return 128;
+  return 0;
+}
 
 PA_EXPORT int pa_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
                                 const long* strides /*12: q b,s,h k b,s,h v b,s,h o b,s,h*/,
@@ -1181,18 +1473,29 @@ PA_EXPORT int pa_flash_attn_bwd(const void* q, const void* k, const void* v, con
   const bool fits32 = (long)Sq * strides[1] * 2 < lim && (long)Sq * strides[13] * 2 < lim &&
                       (long)Sq * Hq * D * 4 < lim;
   int variant = fits32 ? g_fa_bwd_variant : 0;
+  if (variant == 5 && !(fa_v5_ok(Sq, Sk, D, causal) && dq_part != nullptr)) variant = 4;
   if (variant == 4 && (D != 128 || dq_part == nullptr || !causal)) variant = 1;
   if (variant != 4 && dq_acc == nullptr) return (int)hipErrorInvalidValue;
   const long rows = (long)B * Hq * Sq;
   const int lpr = D / 8;
   const long pre_threads = rows * lpr;
   BwdParams pp = p;
-  if (variant == 4) pp.dq_acc = nullptr;  // partial slabs: no accumulator to zero
+  if (variant >= 4) pp.dq_acc = nullptr;  // partial slabs: no accumulator to zero
   if (D == 128) hipLaunchKernelGGL(fa_bwd_pre_kernel<128>, dim3((pre_threads + 255) / 256), dim3(256), 0, st, pp);
   else if (D == 64) hipLaunchKernelGGL(fa_bwd_pre_kernel<64>, dim3((pre_threads + 255) / 256), dim3(256), 0, st, pp);
   else if (D == 256) hipLaunchKernelGGL(fa_bwd_pre_kernel<256>, dim3((pre_threads + 255) / 256), dim3(256), 0, st, pp);
   else return (int)hipErrorInvalidValue;
   dim3 grid(Hq, B, (Sk + 127) / 128);
+  if (variant == 5) {
+    const int nkb = Sk / 128;
+    hipLaunchKernelGGL(fa_bwd_kernel5<true>, dim3(Hq, B, nkb), dim3(256), 0, st, p);
+    if (dq_acc == nullptr) {
+      PA_LAUNCH_CHECK();
+    }
+    const long n = (long)B * Hq * Sq * (D / 4);
+    hipLaunchKernelGGL((fa_bwd_dq_reduce<128, true>), dim3((n + 255) / 256), dim3(256), 0, st, p, nkb, 128);
+    PA_LAUNCH_CHECK();
+  }
   if (D == 128 && (variant == 3 || variant == 4)) {
     const int nkb = (Sk + 127) / 128;
     dim3 g3(Hq, B, nkb);
@@ -1204,8 +1507,8 @@ PA_EXPORT int pa_flash_attn_bwd(const void* q, const void* k, const void* v, con
         PA_LAUNCH_CHECK();
       }
       const long n = (long)B * Hq * Sq * (D / 4);
-      if (causal) hipLaunchKernelGGL((fa_bwd_dq_reduce<128, true>), dim3((n + 255) / 256), dim3(256), 0, st, p, nkb);
-      else hipLaunchKernelGGL((fa_bwd_dq_reduce<128, false>), dim3((n + 255) / 256), dim3(256), 0, st, p, nkb);
+      if (causal) hipLaunchKernelGGL((fa_bwd_dq_reduce<128, true>), dim3((n + 255) / 256), dim3(256), 0, st, p, nkb, 128);
+      else hipLaunchKernelGGL((fa_bwd_dq_reduce<128, false>), dim3((n + 255) / 256), dim3(256), 0, st, p, nkb, 128);
     } else {
       if (causal) hipLaunchKernelGGL((fa_bwd_kernel3<true, false>), g3, dim3(512), 0, st, p);
       else hipLaunchKernelGGL((fa_bwd_kernel3<false, false>), g3, dim3(512), 0, st, p);
@@ -1234,15 +1537,16 @@ PA_EXPORT int pa_flash_attn_bwd(const void* q, const void* k, const void* v, con
 // = query index) and store bf16 into ``out`` rows of stride ``out_ts`` elements
 // (the dq columns of the packed dqkv gradient).  D = 128.
 PA_EXPORT int pa_fa_dq_reduce_rope(const float* part, int nkb, int B, int Sq, int Sk, int Hq, int causal,
-                                   void* out, long out_ts, const float* cosT, const float* sinT,
+                                   void* out, long out_ts, const float* cosT, const float* sinT, int kblk,
                                    hipStream_t st) {
+  if (kblk != 128 && kblk != 256) return (int)hipErrorInvalidValue;
   const long n = (long)B * Hq * Sq * 16;
   const dim3 g((unsigned)((n + 255) / 256));
   if (causal)
     hipLaunchKernelGGL(fa_dq_reduce_rope<true>, g, dim3(256), 0, st, part, nkb, B, Sq, Sk, Hq, (u16*)out,
-                       out_ts, cosT, sinT);
+                       out_ts, cosT, sinT, kblk);
   else
     hipLaunchKernelGGL(fa_dq_reduce_rope<false>, g, dim3(256), 0, st, part, nkb, B, Sq, Sk, Hq, (u16*)out,
-                       out_ts, cosT, sinT);
+                       out_ts, cosT, sinT, kblk);
   PA_LAUNCH_CHECK();
 }

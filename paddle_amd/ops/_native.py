@@ -67,7 +67,8 @@ _SIGS = {
     "pa_lstm_cell_fwd": [_P, _P, _P, _P, _P, _P, _L, _P, _L, _I, _I, _P],
     "pa_lstm_cell_bwd": [_P, _P, _L, _P, _P, _P, _P, _P, _I, _I, _P],
     "pa_lstm_persistent": [_I] + [_P] * 17 + [_I, _I, _I, _P],
-    "pa_fa_dq_reduce_rope": [_P, _I, _I, _I, _I, _I, _I, _P, _L, _P, _P, _P],
+    "pa_fa_dq_reduce_rope": [_P, _I, _I, _I, _I, _I, _I, _P, _L, _P, _P, _I, _P],
+    "pa_fa_bwd_part_kblk": [_I, _I, _I, _I],
     "pa_conv_gemm": [_P, _P, _P, _P] + [_I] * 17 + [_P],
     "pa_im2col_nhwc": [_P, _P] + [_I] * 15 + [_P],
     "pa_bn_blocks": [_L, _I],

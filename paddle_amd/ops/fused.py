@@ -225,8 +225,9 @@ def _fa_bwd(q, k, v, o, do, lse, causal, scale, dk, dv, dq_rope_out=None):
                            + _fa_strides(do) + _fa_strides(dk))
     assert dk.stride() == dv.stride()
     part = None
-    nkb = (Sk + 127) // 128
-    if D == 128 and causal and N.lib().pa_fa_bwd_get_variant() == 4:
+    kblk = N.lib().pa_fa_bwd_part_kblk(Sq, Sk, D, int(causal))
+    nkb = (Sk + kblk - 1) // kblk if kblk else 0
+    if kblk:
         # per-key-block dQ partial slabs (plain stores) summed by a reduce kernel
         part = torch.empty(nkb, B, Hq, Sq, D, dtype=torch.bfloat16, device=q.device)
     fused = part is not None and dq_rope_out is not None
@@ -239,7 +240,7 @@ def _fa_bwd(q, k, v, o, do, lse, causal, scale, dk, dv, dq_rope_out=None):
         assert cos.dtype == torch.float32 and cos.is_contiguous() and sin.is_contiguous()
         assert cos.shape[0] >= Sq and cos.shape[1] == D // 2
         N.call("pa_fa_dq_reduce_rope", N.ptr(part), nkb, B, Sq, Sk, Hq, int(causal), N.ptr(out), ts,
-               N.ptr(cos), N.ptr(sin), N.stream())
+               N.ptr(cos), N.ptr(sin), kblk, N.stream())
     return dq_acc
 
 

@@ -328,7 +328,7 @@ def test_linear_fwd_via_transposed_weight_tracks_updates():
     assert _rel(F.linear(x, w), x.float() @ w.detach().float()) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [1, 3, 4])
+@pytest.mark.parametrize("variant", [1, 3, 4, 5])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("S,Hq,Hk", [(256, 4, 4), (384, 4, 2), (200, 2, 2), (1000, 2, 1)])
 def test_flash_attention_bwd_variants(variant, causal, S, Hq, Hk):
