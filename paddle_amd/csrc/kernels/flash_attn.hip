@@ -272,6 +272,205 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdParams p) {
   }
 }
 
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void fa_fwd_kernel2(FwdParams p) {
+  constexpr int BM = 128, BN = 64;
+  constexpr int KCH = D / 8;              // 16-B chunks per row
+  constexpr int NCH = BN * KCH / 256;     // chunks per thread per tile
+  constexpr int KS = D / 16;              // k-steps over head dim
+  constexpr int DB = D / 32;              // 32-wide d blocks of O^T
+  // two K|V stages: tile t+1 is stored into the other stage while tile t is
+  // consumed, so one barrier per tile orders both the reads and the stores
+  constexpr int STG = 2 * BN * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int mt = gridDim.z - 1 - blockIdx.z;
+  const int kvh = h / (p.Hq / p.Hkv);
+  const int q0 = mt * BM;
+  const int qw = q0 + w * 32;
+  const int qrow = qw + r;
+  const int offs = CAUSAL ? p.Sk - p.Sq : 0;
+
+  const u16* qp = p.q + (long)b * p.q_bs + (long)h * p.q_hs;
+  const u16* kp = p.k + (long)b * p.k_bs + (long)kvh * p.k_hs;
+  const u16* vp = p.v + (long)b * p.v_bs + (long)kvh * p.v_hs;
+
+  bf8v qf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    u16x8 t = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (qrow < p.Sq) t = *reinterpret_cast<const u16x8*>(qp + (long)qrow * p.q_ss + ks * 16 + hh * 8);
+    qf[ks] = as_bf8(t);
+  }
+
+  int kv_end = p.Sk;
+  if (CAUSAL) kv_end = min(p.Sk, q0 + BM + offs);
+  const int nt = kv_end > 0 ? (kv_end + BN - 1) / BN : 0;
+
+  f32x16 oacc[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) oacc[i][e] = 0.f;
+  float m = -1e30f, lsum = 0.f;
+
+  u16x8 kst[NCH], vst[NCH];
+  // per-chunk element offsets within one tile (32-bit); the tile base pointers advance
+  // by BN rows per tile, so the loop does no 64-bit address arithmetic per chunk
+  int krow[NCH], koff[NCH], voff[NCH];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int idx = tid + 256 * i, row = idx / KCH, ch = idx % KCH;
+    krow[i] = row;
+    koff[i] = row * (int)p.k_ss + ch * 8;
+    voff[i] = row * (int)p.v_ss + ch * 8;
+  }
+  auto load_regs = [&](int t) {
+    const u16* kt = kp + (long)t * BN * p.k_ss;
+    const u16* vt = vp + (long)t * BN * p.v_ss;
+    const int rows_left = p.Sk - t * BN;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      if (krow[i] < rows_left) {
+        kst[i] = *reinterpret_cast<const u16x8*>(kt + koff[i]);
+        vst[i] = *reinterpret_cast<const u16x8*>(vt + voff[i]);
+      } else {
+        kst[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        vst[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    }
+  };
+  auto store_lds = [&](int stage) {
+    char* Ks = smem + stage * STG;
+    char* Vs = Ks + BN * D * 2;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int idx = tid + 256 * i, row = idx / KCH, ch = idx % KCH;
+      *reinterpret_cast<u16x8*>(Ks + k_off<D>(row, ch)) = kst[i];
+      *reinterpret_cast<u16x8*>(Vs + v_off_bytes<D>(row, ch * 16)) = vst[i];
+    }
+  };
+
+  if (nt > 0) {
+    load_regs(0);
+    store_lds(0);
+  }
+  __syncthreads();
+
+  // lane coordinates for the V^T transposed reads
+  const int g = lane >> 4, gi = lane & 15, gq = gi >> 2, gp = gi & 3;
+
+  for (int t = 0; t < nt; ++t) {
+    if (t + 1 < nt) load_regs(t + 1);
+    const char* Ks = smem + (t & 1) * STG;
+    const char* Vs = Ks + BN * D * 2;
+    const int kv0 = t * BN;
+    const bool skip = CAUSAL && (kv0 > qw + 31 + offs);
+    if (!skip) {
+      f32x16 s[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) s[c][e] = 0.f;
+      // the two key halves are independent accumulator chains: interleave them so
+      // consecutive MFMAs never wait on each other's result
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const u16x8 kf = *reinterpret_cast<const u16x8*>(Ks + k_off<D>(32 * c + r, 2 * ks + hh));
+          s[c] = mfma32(as_bf8(kf), qf[ks], s[c]);
+        }
+      }
+      const bool need_mask = (kv0 + BN > p.Sk) || (CAUSAL && (kv0 + BN - 1 > qw + offs));
+      // max over raw scores (scale > 0 commutes with max); the log2e*scale factor is
+      // folded into one fma per element; raw v_exp_f32 (no denormal fix-up path)
+      float tmax = -INFINITY;
+      if (need_mask) {
+        // element (c, e) is key kv0 + 4 hh + k(c, e), k = 32c + (e & 3) + 8 (e >> 2):
+        // valid while k < lim (lane constant per tile)
+        int lim = p.Sk - kv0 - 4 * hh;
+        if (CAUSAL) lim = min(lim, qrow + offs - kv0 - 4 * hh + 1);
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+            if (32 * c + (e & 3) + 8 * (e >> 2) >= lim) s[c][e] = -INFINITY;
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) tmax = fmaxf(tmax, s[c][e]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * p.scale_log2;
+      // lazy rescaling: keep a stale running max unless some row's max grew by more
+      // than 2^8 (exp2 values stay <= 256, safe in fp32 sums and bf16 P); the O
+      // rescale then runs on a small fraction of tiles
+      float alpha = 1.f;
+      if (__any(tmax > m + 8.f)) {
+        const float mnew = fmaxf(m, tmax);
+        alpha = __builtin_amdgcn_exp2f(m - mnew);
+        m = mnew;
+      }
+      const float mnew = m;
+      float ps = 0.f;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[c][e], p.scale_log2, -mnew));
+          s[c][e] = pv;
+          ps += pv;
+        }
+      lsum = lsum * alpha + ps;
+      if (__any(alpha != 1.f)) {
+#pragma unroll
+        for (int i = 0; i < DB; ++i)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) oacc[i][e] *= alpha;
+      }
+      // O^T += V^T P^T over 4 k-steps of 16 kv
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const int c = st >> 1, half = st & 1;
+        const bf8v pf = pack_p(s[c], 8 * half);
+        const int rowb = 32 * c + 16 * half + 4 * (g >> 1) + gq;
+#pragma unroll
+        for (int db = 0; db < DB; ++db) {
+          const int colb = (32 * db + 16 * (g & 1) + 4 * gp) * 2;
+          const s4v lo = tr_read(Vs, v_off_bytes<D>(rowb, colb));
+          const s4v hi = tr_read(Vs, v_off_bytes<D>(rowb + 8, colb));
+          oacc[db] = mfma32(cat_tr(lo, hi), pf, oacc[db]);
+        }
+      }
+    }
+    // stage (t+1)&1 was last read in iteration t-1, which every wave finished
+    // before the barrier that closed it
+    if (t + 1 < nt) store_lds((t + 1) & 1);
+    __syncthreads();
+  }
+
+  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  const float inv = ltot > 0.f ? 1.f / ltot : 0.f;
+  if (qrow < p.Sq) {
+    u16* op = p.o + (long)b * p.o_bs + (long)h * p.o_hs + (long)qrow * p.o_ss;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        const int d = 32 * db + 8 * e4 + 4 * hh;
+        u16x4 o4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o4[j] = f2bf(oacc[db][4 * e4 + j] * inv);
+        *reinterpret_cast<u16x4*>(op + d) = o4;
+      }
+    if (hh == 0)
+      p.lse[((long)b * p.Hq + h) * p.Sq + qrow] =
+          ltot > 0.f ? (m + __log2f(ltot)) * 0.69314718056f : -INFINITY;
+  }
+}
+
 // ------------------------------------------------------------------ backward
 struct BwdParams {
   const u16 *q, *k, *v, *o, *dout;
@@ -1407,6 +1606,14 @@ PA_EXPORT int pa_fa_bwd_set_variant(int v) {
 
 PA_EXPORT int pa_fa_bwd_get_variant() { return g_fa_bwd_variant; }
 
+// forward: 1 = fa_fwd_kernel, 2 = fa_fwd_kernel2 (32-bit positions / offsets, lane-
+// constant mask limit: fewer VALU per MFMA)
+static int g_fa_fwd_variant = 2;
+PA_EXPORT int pa_fa_fwd_set_variant(int v) {
+  g_fa_fwd_variant = v;
+  return 0;
+}
+
 static bool fa_v5_ok(int Sq, int Sk, int D, int causal) {
   return g_fa_bwd_variant == 5 && D == 128 && causal && Sk % 128 == 0 && Sq % 32 == 0 && Sq > 0;
 }
@@ -1432,7 +1639,11 @@ PA_EXPORT int pa_flash_attn_fwd(const void* q, const void* k, const void* v, voi
   p.B = B; p.Sq = Sq; p.Sk = Sk; p.Hq = Hq; p.Hkv = Hkv;
   p.scale_log2 = scale * 1.44269504089f;
   dim3 grid(Hq, B, (Sq + 127) / 128);
-  if (D == 128) {
+  const bool v2ok = g_fa_fwd_variant == 2 && (long)Sk * strides[4] < (1L << 31) && (long)Sk * strides[7] < (1L << 31);
+  if (D == 128 && v2ok) {
+    if (causal) hipLaunchKernelGGL((fa_fwd_kernel2<128, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((fa_fwd_kernel2<128, false>), grid, dim3(256), 0, st, p);
+  } else if (D == 128) {
     if (causal) hipLaunchKernelGGL((fa_fwd_kernel<128, true>), grid, dim3(256), 0, st, p);
     else hipLaunchKernelGGL((fa_fwd_kernel<128, false>), grid, dim3(256), 0, st, p);
   } else if (D == 64) {

@@ -61,6 +61,7 @@ _SIGS = {
     "pa_transpose2d": [_I, _P, _P, _I, _I, _L, _L, _I, _L, _L, _P],
     "pa_flash_attn_fwd": [_P, _P, _P, _P, _P, _LP, _I, _I, _I, _I, _I, _I, _F, _I, _P],
     "pa_fa_bwd_set_variant": [_I],
+    "pa_fa_fwd_set_variant": [_I],
     "pa_fa_bwd_get_variant": [],
     "pa_add_attn_fwd": [_P, _P, _P, _P, _P, _P, _L, _P, _I, _I, _I, _I, _P],
     "pa_add_attn_bwd": [_P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P],
