@@ -139,8 +139,10 @@ def _hip_ldflags() -> list[str]:
 
 def build_native(verbose: bool = False, jobs: int | None = None) -> str:
     """The native C++ executor + inference API (``csrc/native``): host kernels
-    compiled with g++ (AVX2/FMA), device kernels with hipcc for gfx950, one shared
-    library with public C++ symbols (paddle_inference_api.h) and a C ABI."""
+    compiled with g++ (AVX2/FMA), device glue kernels with hipcc for gfx950, one
+    shared library with public C++ symbols (paddle_inference_api.h) and a C ABI,
+    linked against the kernel library for GEMM / conv / pool / norm / loss /
+    optimizer kernels."""
     d = os.path.join(ROOT, "csrc", "native")
     ccs = sorted(glob.glob(os.path.join(d, "*.cc")))
     hips = sorted(glob.glob(os.path.join(d, "*.hip")))
@@ -163,8 +165,13 @@ def build_native(verbose: bool = False, jobs: int | None = None) -> str:
         with cf.ThreadPoolExecutor(max_workers=jobs or min(8, os.cpu_count() or 4)) as ex:
             list(ex.map(lambda a: _compile(a[0], a[1], a[2], verbose), todo))
     out = NATIVE_LIB
-    if todo or not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
-        cmd = [_hipcc(), "-shared", f"--offload-arch={ARCH}", "-o", out + ".tmp"] + objs + ["-pthread"] + _hip_ldflags()
+    # the device kernels call the shared kernel library (csrc/native/kernel_lib.h):
+    # link it, found next to this library at run time ($ORIGIN)
+    klib = build_kernels(verbose, jobs)
+    if (todo or not os.path.exists(out) or os.path.getmtime(klib) > os.path.getmtime(out)
+            or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs)):
+        cmd = ([_hipcc(), "-shared", f"--offload-arch={ARCH}", "-o", out + ".tmp"] + objs + ["-pthread"]
+               + [f"-L{LIBDIR}", "-lpaddle_amd_kernels", "-Wl,-rpath,$ORIGIN"] + _hip_ldflags())
         if verbose:
             print("[paddle_amd build]", " ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -419,6 +419,54 @@ PA_NAT_EXPORT int pa_nat_scope_set(void* s, const char* name, int dtype, int ndi
   });
 }
 
+// binds `name` to memory the caller owns (a torch tensor's storage): kernels read and
+// update it in place; the executor never frees it
+PA_NAT_EXPORT int pa_nat_scope_share(void* s, const char* name, int dtype, int ndim, const int64_t* dims, void* data,
+                                     int device) {
+  return guard([&] {
+    pa::Tensor t;
+    t.dtype = (pa::DT)dtype;
+    t.dims.assign(dims, dims + ndim);
+    t.device = device;
+    t.buf = std::make_shared<pa::Buffer>(data, t.nbytes(), device);
+    pa::Variable* v = static_cast<pa::Scope*>(s)->Var(name);
+    v->tensor = t;
+    return 0;
+  });
+}
+
+// describes `name` without copying: 1 found (fields filled), 0 absent / uninitialised
+PA_NAT_EXPORT int pa_nat_scope_info(void* s, const char* name, int* dtype, int* ndim, int64_t* dims, int dims_cap,
+                                    void** data, int* device) {
+  pa::Variable* v = static_cast<pa::Scope*>(s)->Find(name);
+  if (!v || !v->tensor.initialized() || (int)v->tensor.dims.size() > dims_cap) return 0;
+  const pa::Tensor& t = v->tensor;
+  *dtype = (int)t.dtype;
+  *ndim = (int)t.dims.size();
+  for (size_t k = 0; k < t.dims.size(); ++k) dims[k] = t.dims[k];
+  *data = t.raw();
+  *device = t.device;
+  return 1;
+}
+
+// synchronous copy between host (-1) / device memories
+PA_NAT_EXPORT int pa_nat_copy(void* dst, int dst_dev, const void* src, int src_dev, size_t n) {
+  return guard([&] {
+    pa::device_copy(dst, dst_dev, src, src_dev, n, nullptr);
+    if (dst_dev >= 0 && src_dev >= 0) pa::device_synchronize(dst_dev);
+    return 0;
+  });
+}
+
+// "type count" lines of the ops a device executor ran on host copies
+PA_NAT_EXPORT int pa_nat_executor_fallbacks(void* e, char* buf, int cap) {
+  std::string s;
+  for (auto& kv : static_cast<pa::Executor*>(e)->host_fallbacks) s += kv.first + " " + std::to_string(kv.second) + "\n";
+  if ((int)s.size() + 1 > cap) return -(int)s.size() - 1;
+  memcpy(buf, s.c_str(), s.size() + 1);
+  return (int)s.size();
+}
+
 // copies the tensor to host (kept alive in the scope variable `name@HOST` until the next call)
 PA_NAT_EXPORT int pa_nat_scope_get(void* s, const char* name, int* dtype, int* ndim, int64_t* dims, int dims_cap,
                                    const void** data, size_t* nbytes) {

@@ -327,6 +327,7 @@ Buffer::Buffer(size_t n, int dev) : bytes(n), device(dev) {
 }
 
 Buffer::~Buffer() {
+  if (!owned) return;
   if (device < 0) free(ptr);
   else device_free(ptr, device);
 }
@@ -418,15 +419,21 @@ std::vector<std::string> Scope::LocalNames() const {
 }
 
 // ================================================================ host worker pool
+// Each parallel_for publishes one Job; a worker takes a reference to the job under
+// the pool mutex and only ever touches that job's own counters, so a worker that
+// wakes late (after its job finished, or while the next job is being published)
+// can neither run a finished job's functor nor mix two jobs' chunk geometry.
 struct ThreadPool {
+  struct Job {
+    const std::function<void(int64_t, int64_t)>* fn;
+    int64_t n, chunk;
+    std::atomic<int64_t> next{0};
+    int active = 0;  // workers inside drain(), guarded by the pool mutex
+  };
   std::vector<std::thread> workers;
   std::mutex mu;
   std::condition_variable cv, done_cv;
-  const std::function<void(int64_t, int64_t)>* job = nullptr;
-  int64_t n = 0, chunk = 0;
-  std::atomic<int64_t> next{0};
-  int active = 0;
-  uint64_t gen = 0;
+  std::shared_ptr<Job> cur;  // guarded by mu
   bool stop = false;
   std::mutex run_mu;  // one parallel_for at a time (nested calls run serially)
 
@@ -441,27 +448,29 @@ struct ThreadPool {
     cv.notify_all();
     for (auto& t : workers) t.join();
   }
-  void drain() {
+  static void drain(Job& j) {
     for (;;) {
-      int64_t b = next.fetch_add(chunk);
-      if (b >= n) return;
-      (*job)(b, std::min(n, b + chunk));
+      const int64_t b = j.next.fetch_add(j.chunk);
+      if (b >= j.n) return;
+      (*j.fn)(b, std::min(j.n, b + j.chunk));
     }
   }
   void loop() {
-    uint64_t seen = 0;
+    const Job* last = nullptr;
     for (;;) {
+      std::shared_ptr<Job> j;
       {
         std::unique_lock<std::mutex> l(mu);
-        cv.wait(l, [&] { return stop || gen != seen; });
+        cv.wait(l, [&] { return stop || (cur && cur.get() != last); });
         if (stop) return;
-        seen = gen;
-        ++active;
+        j = cur;
+        last = j.get();
+        ++j->active;
       }
-      drain();
+      drain(*j);
       {
         std::lock_guard<std::mutex> g(mu);
-        if (--active == 0) done_cv.notify_all();
+        if (--j->active == 0) done_cv.notify_all();
       }
     }
   }
@@ -471,19 +480,19 @@ struct ThreadPool {
       fn(0, total);
       return;
     }
+    auto j = std::make_shared<Job>();
+    j->fn = &fn;
+    j->n = total;
+    j->chunk = ch;
     {
       std::lock_guard<std::mutex> g(mu);
-      job = &fn;
-      n = total;
-      chunk = ch;
-      next = 0;
-      ++gen;
+      cur = j;
     }
     cv.notify_all();
-    drain();
+    drain(*j);
     std::unique_lock<std::mutex> l(mu);
-    done_cv.wait(l, [&] { return active == 0 && next.load() >= n; });
-    job = nullptr;
+    done_cv.wait(l, [&] { return j->active == 0; });
+    cur.reset();
   }
 };
 
@@ -595,65 +604,83 @@ void Executor::RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* 
   static const std::set<std::string> agnostic = {"feed", "fetch", "reshape", "reshape2", "flatten", "flatten2",
                                                  "squeeze", "squeeze2", "unsqueeze", "unsqueeze2", "delete_var",
                                                  "reshape_grad", "reshape2_grad"};
+  auto timed = [&](const OpDesc& op, const std::function<void()>& fn) {
+    if (!profile) return fn();
+    Sync();
+    auto t0 = std::chrono::steady_clock::now();
+    fn();
+    Sync();
+    auto& e = op_time_ms[op.type];
+    e.first += 1;
+    e.second += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  };
+  // host kernel on host copies of the device inputs; results go back to HBM
+  auto host_fallback = [&](const OpDesc& op, const Kernel* k) {
+    host_fallbacks[op.type] += 1;
+    Scope& tmp = scope->NewScope();
+    for (auto& slot : op.inputs)
+      for (auto& n : slot.second) {
+        Variable* v = scope->Find(n);
+        if (v && v->tensor.initialized() && v->tensor.device >= 0) {
+          Variable* h = tmp.Var(n);
+          h->kind = v->kind;
+          h->tensor = v->tensor.to(-1, ctx_.stream);
+        }
+      }
+    device_stream_sync(ctx_.stream);
+    for (auto& slot : op.outputs)
+      for (auto& n : slot.second) {
+        Variable* v = scope->Find(n);
+        if (v && !tmp.FindLocal(n)) {
+          Variable* h = tmp.Var(n);
+          h->kind = v->kind;
+          h->list = v->list;
+          if (v->tensor.initialized()) h->tensor = v->tensor.to(-1, ctx_.stream);
+        }
+      }
+    device_stream_sync(ctx_.stream);
+    ExecContext hctx = ctx_;
+    hctx.device = -1;
+    (*k)(OpRun{op, tmp, hctx});
+    for (auto& slot : op.outputs)
+      for (auto& n : slot.second) {
+        Variable* h = tmp.FindLocal(n);
+        if (!h) continue;
+        Variable* v = scope->Find(n);
+        if (!v) v = scope->Var(n);
+        v->kind = h->kind;
+        v->list = h->list;
+        if (!h->tensor.initialized()) continue;
+        if (h->kind == VK_FETCH_LIST) {
+          v->tensor = h->tensor;
+        } else if (v->tensor.initialized() && v->tensor.buf && !v->tensor.buf->owned &&
+                   v->tensor.device == ctx_.device && v->tensor.nbytes() == h->tensor.nbytes() &&
+                   v->tensor.dtype == h->tensor.dtype) {
+          // lent (embedder-owned) buffer: update it in place so the embedder sees the result
+          device_copy(v->tensor.raw(), ctx_.device, h->tensor.raw(), -1, h->tensor.nbytes(), ctx_.stream);
+          v->tensor.dims = h->tensor.dims;
+          v->tensor.lod = h->tensor.lod;
+        } else {
+          v->tensor = h->tensor.to(ctx_.device, ctx_.stream);
+        }
+      }
+  };
   for (const OpDesc& op : block.ops) {
-    const Kernel* k = dev ? find_kernel(op.type, true) : nullptr;
-    bool host_fallback = false;
-    if (!k) {
-      k = find_kernel(op.type, false);
-      host_fallback = dev && !agnostic.count(op.type);
+    const Kernel* dk = dev ? find_kernel(op.type, true) : nullptr;
+    if (dk) {
+      try {
+        timed(op, [&] { (*dk)(OpRun{op, *scope, ctx_}); });
+        continue;
+      } catch (const Decline&) {
+      }
     }
-    PA_CHECK(k != nullptr, "no kernel registered for op type '%s'", op.type.c_str());
-    if (host_fallback) {
-      // run the host kernel on host copies of device inputs; results go back to HBM
-      Scope& tmp = scope->NewScope();
-      for (auto& slot : op.inputs)
-        for (auto& n : slot.second) {
-          Variable* v = scope->Find(n);
-          if (v && v->tensor.initialized() && v->tensor.device >= 0) {
-            Variable* h = tmp.Var(n);
-            h->kind = v->kind;
-            h->tensor = v->tensor.to(-1, ctx_.stream);
-          }
-        }
-      device_stream_sync(ctx_.stream);
-      for (auto& slot : op.outputs)
-        for (auto& n : slot.second) {
-          Variable* v = scope->Find(n);
-          if (v && !tmp.FindLocal(n)) {
-            Variable* h = tmp.Var(n);
-            h->kind = v->kind;
-            h->list = v->list;
-            if (v->tensor.initialized()) h->tensor = v->tensor.to(-1, ctx_.stream);
-          }
-        }
-      device_stream_sync(ctx_.stream);
-      ExecContext hctx = ctx_;
-      hctx.device = -1;
-      (*k)(OpRun{op, tmp, hctx});
-      for (auto& slot : op.outputs)
-        for (auto& n : slot.second) {
-          Variable* h = tmp.FindLocal(n);
-          if (!h) continue;
-          Variable* v = scope->Find(n);
-          if (!v) v = scope->Var(n);
-          v->kind = h->kind;
-          v->list = h->list;
-          if (h->tensor.initialized())
-            v->tensor = (h->kind == VK_FETCH_LIST) ? h->tensor : h->tensor.to(ctx_.device, ctx_.stream);
-        }
-      continue;
-    }
-    if (profile) {
-      Sync();
-      auto t0 = std::chrono::steady_clock::now();
-      (*k)(OpRun{op, *scope, ctx_});
-      Sync();
-      auto& e = op_time_ms[op.type];
-      e.first += 1;
-      e.second += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    } else {
-      (*k)(OpRun{op, *scope, ctx_});
-    }
+    const Kernel* k = find_kernel(op.type, false);
+    PA_CHECK(k != nullptr, dk ? "op '%s' declined its device kernel and has no host kernel"
+                              : "no kernel registered for op type '%s'", op.type.c_str());
+    if (dev && !agnostic.count(op.type))
+      timed(op, [&] { host_fallback(op, k); });
+    else
+      timed(op, [&] { (*k)(OpRun{op, *scope, ctx_}); });
   }
 }
 

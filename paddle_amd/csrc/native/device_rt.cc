@@ -60,4 +60,9 @@ void device_stream_sync(void* s) {
   if (s) HIPCHK(hipStreamSynchronize((hipStream_t)s));
 }
 
+void device_synchronize(int dev) {
+  HIPCHK(hipSetDevice(dev));
+  HIPCHK(hipDeviceSynchronize());
+}
+
 }  // namespace pa

@@ -33,6 +33,9 @@ struct Error : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
 [[noreturn]] void fail(const char* fmt, ...);
+// Thrown by a device kernel (before it touches any output) for a configuration it
+// does not cover; the executor runs the op's host kernel instead.
+struct Decline {};
 #define PA_CHECK(cond, ...) \
   do {                      \
     if (!(cond)) ::pa::fail(__VA_ARGS__); \
@@ -114,7 +117,9 @@ struct Buffer {
   void* ptr = nullptr;
   size_t bytes = 0;
   int device = -1;
+  bool owned = true;  // false: memory lent by the embedder (e.g. a torch tensor), never freed here
   Buffer(size_t n, int dev);
+  Buffer(void* p, size_t n, int dev) : ptr(p), bytes(n), device(dev), owned(false) {}
   ~Buffer();
   Buffer(const Buffer&) = delete;
   Buffer& operator=(const Buffer&) = delete;
@@ -223,6 +228,8 @@ class Executor {
   // per-op wall time accumulation (the reference's kCPU profiler in the demo)
   bool profile = false;
   std::map<std::string, std::pair<int64_t, double>> op_time_ms;  // type -> (calls, ms)
+  // device executors: ops that ran on host copies (no device kernel, or it declined)
+  std::map<std::string, int64_t> host_fallbacks;
 
  private:
   ExecContext ctx_;
@@ -248,6 +255,7 @@ void device_copy(void* dst, int dst_dev, const void* src, int src_dev, size_t n,
 void* device_stream_create(int dev);
 void device_stream_destroy(void* s);
 void device_stream_sync(void* s);
+void device_synchronize(int dev);
 int device_count();
 
 }  // namespace pa

@@ -1,13 +1,23 @@
-// gfx950 device kernels of the native executor (fp32 inference / training ops on
-// HBM-resident tensors).  Ops without a device kernel here run through the
-// executor's host fallback (inputs copied to host, outputs back to HBM).
+// gfx950 device kernels of the native executor (fp32 inference AND training ops on
+// HBM-resident tensors).
 //
-// GEMM (mul / fc / matmul / conv2d's im2col product) runs on the exact-f32 matrix
-// cores: v_mfma_f32_32x32x2_f32 over a 128x128x32 LDS-tiled block of 4 wave64s
-// (each wave a 64x64 quadrant = 2x2 MFMA tiles), operands addressed through
-// (row, k) strides so transposed layouts need no copy; bias / relu / beta fused in
-// the epilogue.  gfx950 has no xf32 path, so f32 MFMA is bit-for-bit an f32 FMA
-// chain (cdna_hip_programming.md, "FP32-input MFMA").
+// The heavy lifting runs on the shared kernel library (kernel_lib.h,
+// libpaddle_amd_kernels.so): GEMM (mul / fc / matmul and their grads) and the
+// conv2d products on pa_sgemm (exact-fp32 MFMA, strided / batched / split-K),
+// im2col / col2im on pa_vol2col / pa_col2vol, pooling on pa_pool_*, batch norm on
+// pa_bn_nchw_*, activations on pa_act_*, softmax / cross-entropy on the
+// softmax_ce / nnmisc kernels and the optimizer updates on pa_adamw / pa_momentum /
+// pa_sgd -- the same launchers, with the same call shapes, the Python Fluid
+// operators use (ops/convnd.py, ops/blas.py, operators/*), so the two engines train
+// along the same trajectory.  Only thin glue lives here: broadcast elementwise,
+// reductions, gathers / concat / split / transpose and fills.
+//
+// A device kernel may decline an op configuration it does not cover (throw
+// pa::Decline before touching any output); the executor then runs the host
+// kernel on host copies and counts the fallback (Executor::host_fallbacks).
+//
+// Reference: framework/executor.cc:125-353 (op loop), operators/{mul,conv,pool,
+// batch_norm,softmax,cross_entropy,activation,elementwise,sgd,momentum,adam}_op.*
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <string.h>
@@ -15,11 +25,10 @@
 #include <algorithm>
 
 #include "framework.h"
+#include "kernel_lib.h"
 
 namespace pa {
 namespace {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #define HIPCHK(x)                                                                  \
   do {                                                                             \
@@ -42,104 +51,49 @@ int64_t prod(const Dims& d, size_t b = 0, size_t e = (size_t)-1) {
   return n;
 }
 
-float* f32(Tensor& t) {
+float* f32(const Tensor& t) {
   PA_CHECK(t.dtype == DT::FP32, "expected float32 tensor, got %s", dt_name(t.dtype));
   PA_CHECK(t.device >= 0, "expected a device tensor");
   return t.data<float>();
 }
 
-// =============================================================== f32 MFMA GEMM
-struct GemmArgs {
-  const float* A;
-  const float* B;
-  float* C;
-  const float* bias;  // [N] or null
-  int64_t M, N, K;
-  int64_t sam, sak;  // A(m, k) = A[m*sam + k*sak]
-  int64_t sbk, sbn;  // B(k, n) = B[k*sbk + n*sbn]
-  int64_t ldc;
-  int64_t bsA, bsB, bsC;  // batch strides
-  float alpha, beta;
-  int relu;
-};
-
-constexpr int BM = 128, BN = 128, BK = 32, LPAD = 4;
-
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
-  __shared__ float As[BK][BM + LPAD];
-  __shared__ float Bs[BK][BN + LPAD];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t bz = blockIdx.z;
-  const float* A = g.A + bz * g.bsA;
-  const float* B = g.B + bz * g.bsB;
-  float* C = g.C + bz * g.bsC;
-  const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  f32x16 acc[2][2];
-  for (int i = 0; i < 2; ++i)
-    for (int j = 0; j < 2; ++j)
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  // loaders: A tile 128 x 32; when A is k-contiguous (sak == 1) a thread walks k
-  const bool a_k_fast = g.sak == 1, b_n_fast = g.sbn == 1;
-  for (int64_t k0 = 0; k0 < g.K; k0 += BK) {
-    for (int e = tid; e < BM * BK; e += 256) {
-      int mm, kk;
-      if (a_k_fast) { mm = e / BK; kk = e % BK; } else { kk = e / BM; mm = e % BM; }
-      const int64_t m = m0 + mm, k = k0 + kk;
-      As[kk][mm] = (m < g.M && k < g.K) ? A[m * g.sam + k * g.sak] : 0.f;
-    }
-    for (int e = tid; e < BN * BK; e += 256) {
-      int nn, kk;
-      if (b_n_fast) { kk = e / BN; nn = e % BN; } else { nn = e / BK; kk = e % BK; }
-      const int64_t n = n0 + nn, k = k0 + kk;
-      Bs[kk][nn] = (n < g.N && k < g.K) ? B[k * g.sbk + n * g.sbn] : 0.f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      const int k = kk + (lane >> 5);
-      const float a0 = As[k][wm + (lane & 31)], a1 = As[k][wm + 32 + (lane & 31)];
-      const float b0 = Bs[k][wn + (lane & 31)], b1 = Bs[k][wn + 32 + (lane & 31)];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-    }
-    __syncthreads();
+// Output `slot` with dims `d`.  When the output variable IS the input tensor `in`
+// (in-place op: ParamOut == Param, Out == X) its buffer is kept as is.
+float* out_f32(const OpRun& r, const std::string& slot, const Dims& d, const Tensor* in = nullptr, size_t i = 0) {
+  Tensor* o = r.out(slot, i);
+  if (!o) return nullptr;
+  if (in && o == in) {
+    PA_CHECK(o->dims == d || o->numel() == prod(d), "%s: in-place output shape mismatch", slot.c_str());
+    return f32(*o);
   }
-  // C/D map of 32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  for (int i = 0; i < 2; ++i)
-    for (int j = 0; j < 2; ++j) {
-      const int64_t n = n0 + wn + 32 * j + (lane & 31);
-      if (n >= g.N) continue;
-      const float bv = g.bias ? g.bias[n] : 0.f;
-      for (int r = 0; r < 16; ++r) {
-        const int64_t m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (m >= g.M) continue;
-        float v = g.alpha * acc[i][j][r] + bv;
-        if (g.beta != 0.f) v += g.beta * C[m * g.ldc + n];
-        if (g.relu) v = v > 0.f ? v : 0.f;
-        C[m * g.ldc + n] = v;
-      }
-    }
+  return o->alloc<float>(d, D(r));
 }
 
+// scope-held device workspace (kept across ops / runs: steady-state steps reuse it)
+float* workspace(const OpRun& r, const char* name, int64_t n) {
+  Variable* v = r.scope.Var(name);
+  if (v->tensor.initialized() && v->tensor.device == D(r) && v->tensor.numel() >= n) return f32(v->tensor);
+  return v->tensor.alloc<float>({std::max<int64_t>(n, 1)}, D(r));
+}
+
+void copy_d2d(const OpRun& r, void* dst, const void* src, size_t bytes) {
+  if (bytes && dst != src) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, S(r)));
+}
+
+// =============================================================== GEMM (pa_sgemm)
+// C[M,N] (+batch) = alpha op(A) op(B) + beta C, row-major, transposes as strides.
 void gemm(hipStream_t s, bool ta, bool tb, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
-          int64_t lda, const float* B, int64_t ldb, float beta, float* C, int64_t ldc, const float* bias = nullptr,
-          bool relu = false, int64_t batch = 1, int64_t bsA = 0, int64_t bsB = 0, int64_t bsC = 0) {
+          int64_t lda, const float* B, int64_t ldb, float beta, float* C, int64_t ldc, int64_t batch = 1,
+          int64_t bsA = 0, int64_t bsB = 0, int64_t bsC = 0) {
   if (M <= 0 || N <= 0) return;
-  GemmArgs g;
-  g.A = A; g.B = B; g.C = C; g.bias = bias;
-  g.M = M; g.N = N; g.K = K;
-  g.sam = ta ? 1 : lda; g.sak = ta ? lda : 1;
-  g.sbk = tb ? 1 : ldb; g.sbn = tb ? ldb : 1;
-  g.ldc = ldc; g.bsA = bsA; g.bsB = bsB; g.bsC = bsC;
-  g.alpha = alpha; g.beta = beta; g.relu = relu ? 1 : 0;
-  PA_CHECK(batch <= 65535, "gemm: batch %lld too large", (long long)batch);
-  dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM), (unsigned)batch);
-  PA_CHECK(grid.y <= 65535u, "gemm: M too large for the grid");
-  hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(256), 0, s, g);
-  HIPCHK(hipGetLastError());
+  PA_CHECK(batch >= 1 && batch <= 65535, "gemm: batch %lld out of range", (long long)batch);
+  PA_KL(pa_sgemm(A, ta ? 1 : lda, ta ? lda : 1, B, tb ? 1 : ldb, tb ? ldb : 1, C, ldc, M, N, K, 1, (int)batch, 0, 0,
+                 0, bsA, bsB, bsC, 1, 0, 0, nullptr, 0, alpha, beta, 0, nullptr, s));
+}
+
+__global__ void bias_rows_kernel(float* __restrict__ c, const float* __restrict__ b, int64_t M, int64_t N) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M * N; i += (int64_t)gridDim.x * blockDim.x)
+    c[i] = b[i % N];
 }
 
 // =============================================================== elementwise
@@ -187,10 +141,12 @@ __global__ void binary_pnp_kernel(int op, const float* __restrict__ x, const flo
 
 bool make_bc(const Dims& x, const Dims& y, int64_t axis, BcArgs* b, int64_t* pre, int64_t* n, int64_t* post) {
   const int64_t xr = (int64_t)x.size();
-  if ((int64_t)y.size() > xr || xr > kMaxR) return false;
-  if (axis < 0) axis = xr - (int64_t)y.size();
+  Dims yt = y;  // trailing singular dims of Y are trimmed (elementwise_op_function.h)
+  while (yt.size() > 1 && yt.back() == 1 && x != y) yt.pop_back();
+  if ((int64_t)yt.size() > xr || xr > kMaxR) return false;
+  if (axis < 0) axis = xr - (int64_t)yt.size();
   Dims yf((size_t)xr, 1);
-  for (size_t i = 0; i < y.size(); ++i) yf[(size_t)axis + i] = y[i];
+  for (size_t i = 0; i < yt.size(); ++i) yf[(size_t)axis + i] = yt[i];
   b->R = (int)xr;
   int64_t s1 = 1, s2 = 1;
   for (int64_t i = xr - 1; i >= 0; --i) {
@@ -238,72 +194,116 @@ template <int OP> void k_binary(const OpRun& r) {
     hipLaunchKernelGGL(binary_kernel, dim3(grid_for(b.n)), dim3(256), 0, S(r), b, OP, f32(x), f32(y), op);
 }
 
-enum UnOp { U_RELU, U_SIGMOID, U_TANH, U_EXP, U_LOG, U_SQRT, U_ABS, U_SQUARE, U_SCALE, U_LEAKY, U_GELU,
-            U_RELU6, U_SOFTPLUS, U_SWISH, U_HSIG, U_ELU, U_RECIP };
-
-__device__ inline float un(int op, float v, float p0, float p1) {
-  switch (op) {
-    case U_RELU: return v > 0.f ? v : 0.f;
-    case U_SIGMOID: return 1.f / (1.f + __expf(-v));
-    case U_TANH: return tanhf(v);
-    case U_EXP: return __expf(v);
-    case U_LOG: return __logf(v);
-    case U_SQRT: return sqrtf(v);
-    case U_ABS: return fabsf(v);
-    case U_SQUARE: return v * v;
-    case U_SCALE: return v * p0 + p1;
-    case U_LEAKY: return v > 0.f ? v : v * p0;
-    case U_GELU: return 0.5f * v * (1.f + erff(v * 0.70710678f));
-    case U_RELU6: return fminf(fmaxf(v, 0.f), p0);
-    case U_SOFTPLUS: return v > 20.f ? v : log1pf(__expf(v));
-    case U_SWISH: return v / (1.f + __expf(-p0 * v));
-    case U_HSIG: return fminf(1.f, fmaxf(0.f, v * p0 + p1));
-    case U_ELU: return v > 0.f ? v : p0 * (__expf(v) - 1.f);
-    default: return 1.f / v;
-  }
-}
-
-__global__ void unary_kernel(int op, float p0, float p1, const float* __restrict__ x, float* __restrict__ o,
-                             int64_t n) {
+__global__ void scale_kernel(const float* __restrict__ x, float* __restrict__ o, int64_t n, float s, float b) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    o[i] = un(op, x[i], p0, p1);
+    o[i] = x[i] * s + b;
 }
 
-void launch_unary(const OpRun& r, Tensor& x, Tensor* o, int op, float p0, float p1) {
-  Tensor xs = x;
-  LoD lod = x.lod;
-  Dims d = x.dims;
-  float* op_ = o->alloc<float>(d, D(r));
-  o->lod = lod;
-  if (xs.numel())
-    hipLaunchKernelGGL(unary_kernel, dim3(grid_for(xs.numel())), dim3(256), 0, S(r), op, p0, p1, f32(xs), op_,
-                       xs.numel());
+void launch_scale(const OpRun& r, const Tensor& x, float* o, float s, float b) {
+  if (x.numel())
+    hipLaunchKernelGGL(scale_kernel, dim3(grid_for(x.numel())), dim3(256), 0, S(r), f32(x), o, x.numel(), s, b);
 }
 
-template <int OP> void k_unary(const OpRun& r) {
-  float p0 = 0.f, p1 = 0.f;
-  switch (OP) {
-    case U_LEAKY: p0 = r.op.GetFloat("alpha", 0.02f); break;
-    case U_RELU6: p0 = r.op.GetFloat("threshold", 6.f); break;
-    case U_SWISH: p0 = r.op.GetFloat("beta", 1.f); break;
-    case U_HSIG: p0 = r.op.GetFloat("slope", 0.2f); p1 = r.op.GetFloat("offset", 0.5f); break;
-    case U_ELU: p0 = r.op.GetFloat("alpha", 1.f); break;
-    default: break;
+// elementwise_{add,sub}_grad: dX = dOut, dY = (+/-) dOut summed over Y's broadcast
+// dims ([pre, n, post] -> [n] on pa_chan_sum); other layouts decline to the host
+template <int SIGN> void k_ew_grad(const OpRun& r) {
+  Tensor& x = r.in("X");
+  Tensor& y = r.in("Y");
+  Tensor& g = r.in("Out@GRAD");
+  BcArgs b;
+  int64_t pre, n, post;
+  if (!make_bc(x.dims, y.dims, r.op.GetInt("axis", -1), &b, &pre, &n, &post)) throw Decline();
+  const Dims xd = x.dims, yd = y.dims;
+  const LoD lod = x.lod;
+  if (Tensor* dx = r.out("X@GRAD")) {
+    float* p = dx->alloc<float>(xd, D(r));
+    dx->lod = lod;
+    copy_d2d(r, p, f32(g), g.nbytes());
   }
-  launch_unary(r, r.in("X"), r.out("Out"), OP, p0, p1);
+  if (Tensor* dy = r.out("Y@GRAD")) {
+    float* p = dy->alloc<float>(yd, D(r));
+    if (pre * post == 1)
+      copy_d2d(r, p, f32(g), g.nbytes());
+    else
+      PA_KL(pa_chan_sum(f32(g), p, (int)pre, (int)n, post, 0, S(r)));
+    if (SIGN < 0) launch_scale(r, *dy, p, -1.f, 0.f);
+  }
+}
+
+// =============================================================== activations (pa_act_*)
+struct ActSpec {
+  int id;
+  const char* a_attr;
+  float a_def;
+  const char* b_attr;
+  float b_def;
+};
+
+template <int ID> ActSpec act_spec() {
+  switch (ID) {
+    case act::SOFTSHRINK: return {ID, "lambda", 0.5f, nullptr, 0.f};
+    case act::BRELU: return {ID, "t_min", 0.f, "t_max", 24.f};
+    case act::LEAKY_RELU: return {ID, "alpha", 0.02f, nullptr, 0.f};
+    case act::SOFT_RELU: return {ID, "threshold", 40.f, nullptr, 0.f};
+    case act::ELU: return {ID, "alpha", 1.f, nullptr, 0.f};
+    case act::RELU6: return {ID, "threshold", 6.f, nullptr, 0.f};
+    case act::POW: return {ID, "factor", 1.f, nullptr, 0.f};
+    case act::STANH: return {ID, "scale_a", 2.f / 3.f, "scale_b", 1.7159f};
+    case act::HARD_SHRINK: return {ID, "threshold", 0.5f, nullptr, 0.f};
+    case act::THRESHOLDED_RELU: return {ID, "threshold", 1.f, nullptr, 0.f};
+    case act::HARD_SIGMOID: return {ID, "slope", 0.2f, "offset", 0.5f};
+    case act::SWISH: return {ID, "beta", 1.f, nullptr, 0.f};
+    default: return {ID, nullptr, 0.f, nullptr, 0.f};
+  }
+}
+
+template <int ID> void k_act(const OpRun& r) {
+  const ActSpec sp = act_spec<ID>();
+  const float a = sp.a_attr ? r.op.GetFloat(sp.a_attr, sp.a_def) : 0.f;
+  const float b = sp.b_attr ? r.op.GetFloat(sp.b_attr, sp.b_def) : 0.f;
+  Tensor& x = r.in("X");
+  const LoD lod = x.lod;
+  float* o = out_f32(r, "Out", x.dims, &x);
+  r.out("Out")->lod = lod;
+  PA_KL(pa_act_fwd(ID, 0, f32(x), o, x.numel(), a, b, S(r)));
+}
+
+// <act>_grad: X, Out, Out@GRAD -> X@GRAD (whichever of X / Out the derivative reads)
+template <int ID> void k_act_grad(const OpRun& r) {
+  const ActSpec sp = act_spec<ID>();
+  const float a = sp.a_attr ? r.op.GetFloat(sp.a_attr, sp.a_def) : 0.f;
+  const float b = sp.b_attr ? r.op.GetFloat(sp.b_attr, sp.b_def) : 0.f;
+  Tensor& g = r.in("Out@GRAD");
+  Tensor* x = r.in_opt("X");
+  Tensor* y = r.in_opt("Out");
+  const Dims d = g.dims;
+  const LoD lod = x ? x->lod : g.lod;
+  Tensor* dx = r.out("X@GRAD");
+  if (!dx) return;
+  float* p = dx->alloc<float>(d, D(r));
+  dx->lod = lod;
+  PA_KL(pa_act_bwd(ID, 0, x ? f32(*x) : nullptr, y ? f32(*y) : nullptr, f32(g), p, g.numel(), a, b, S(r)));
 }
 
 void k_scale(const OpRun& r) {
   const float s = r.op.GetFloat("scale", 1.f), b = r.op.GetFloat("bias", 0.f);
   const bool after = r.op.GetBool("bias_after_scale", true);
-  launch_unary(r, r.in("X"), r.out("Out"), U_SCALE, s, after ? b : b * s);
+  Tensor& x = r.in("X");
+  const LoD lod = x.lod;
+  float* o = out_f32(r, "Out", x.dims, &x);
+  r.out("Out")->lod = lod;
+  launch_scale(r, x, o, s, after ? b : b * s);
 }
 
 void k_dropout(const OpRun& r) {
-  PA_CHECK(r.ctx.is_test || r.op.GetBool("is_test"), "dropout: device kernel is inference-only");
+  if (!(r.ctx.is_test || r.op.GetBool("is_test"))) throw Decline();  // training masks: host RNG
   const float p = r.op.GetFloat("dropout_prob", 0.5f);
   const bool upscale = r.op.GetString("dropout_implementation", "downgrade_in_infer") == "upscale_in_train";
-  launch_unary(r, r.in("X"), r.out("Out"), U_SCALE, upscale ? 1.f : 1.f - p, 0.f);
+  Tensor& x = r.in("X");
+  const LoD lod = x.lod;
+  float* o = out_f32(r, "Out", x.dims, &x);
+  r.out("Out")->lod = lod;
+  launch_scale(r, x, o, upscale ? 1.f : 1.f - p, 0.f);
 }
 
 // =============================================================== GEMM ops
@@ -322,6 +322,26 @@ void k_mul(const OpRun& r) {
   gemm(S(r), false, false, M, N, K, 1.f, f32(x), K, f32(y), N, 0.f, c, N);
 }
 
+// mul_grad (mul_op.h MulGradKernel): dX = dOut Y^T, dY = X^T dOut
+void k_mul_grad(const OpRun& r) {
+  Tensor x = r.in("X");
+  Tensor y = r.in("Y");
+  Tensor g = r.in("Out@GRAD");
+  const size_t xnc = (size_t)r.op.GetInt("x_num_col_dims", 1), ync = (size_t)r.op.GetInt("y_num_col_dims", 1);
+  const int64_t M = prod(x.dims, 0, xnc), K = prod(x.dims, xnc), N = prod(y.dims, ync);
+  PA_CHECK(g.numel() == M * N, "mul_grad: Out@GRAD %s does not match", g.shape_str().c_str());
+  if (Tensor* dx = r.out("X@GRAD")) {
+    float* p = dx->alloc<float>(x.dims, D(r));
+    dx->lod = x.lod;
+    gemm(S(r), false, true, M, K, N, 1.f, f32(g), N, f32(y), N, 0.f, p, K);
+  }
+  if (Tensor* dy = r.out("Y@GRAD")) {
+    float* p = dy->alloc<float>(y.dims, D(r));
+    gemm(S(r), true, false, K, N, M, 1.f, f32(x), K, f32(g), N, 0.f, p, N);
+  }
+}
+
+// fc (fc_op.cc): the bias pre-broadcast into C, the GEMM accumulates (beta = 1), relu in place
 void k_fc(const OpRun& r) {
   Tensor x = r.in("Input");
   Tensor w = r.in("W");
@@ -333,8 +353,12 @@ void k_fc(const OpRun& r) {
   Tensor* o = r.out("Out");
   float* c = o->alloc<float>(od, D(r));
   o->lod = x.lod;
-  gemm(S(r), false, false, M, N, K, 1.f, f32(x), K, f32(w), N, 0.f, c, N, b ? f32(*b) : nullptr,
-       r.op.GetString("activation_type") == "relu");
+  if (b && M * N)
+    hipLaunchKernelGGL(bias_rows_kernel, dim3(grid_for(M * N)), dim3(256), 0, S(r), c, f32(*b), M, N);
+  gemm(S(r), false, false, M, N, K, 1.f, f32(x), K, f32(w), N, b ? 1.f : 0.f, c, N);
+  const std::string act = r.op.GetString("activation_type");
+  if (act == "relu") PA_KL(pa_act_fwd(act::RELU, 0, c, c, M * N, 0.f, 0.f, S(r)));
+  else if (!act.empty()) fail("fc: activation %s not supported on the device", act.c_str());
 }
 
 void k_matmul(const OpRun& r) {
@@ -358,150 +382,357 @@ void k_matmul(const OpRun& r) {
   if (od.empty()) od.push_back(1);
   Tensor* o = r.out("Out");
   float* c = o->alloc<float>(od, D(r));
-  gemm(S(r), tx, ty, M, N, K, alpha, f32(x), tx ? M : K, f32(y), ty ? K : N, 0.f, c, N, nullptr, false,
-       std::max(bx, by), bx == 1 ? 0 : M * K, by == 1 ? 0 : K * N, M * N);
+  gemm(S(r), tx, ty, M, N, K, alpha, f32(x), tx ? M : K, f32(y), ty ? K : N, 0.f, c, N, std::max(bx, by),
+       bx == 1 ? 0 : M * K, by == 1 ? 0 : K * N, M * N);
 }
 
-// =============================================================== conv2d (im2col + MFMA GEMM)
-__global__ void im2col_kernel(const float* __restrict__ x, float* __restrict__ col, int C, int H, int W, int kh,
-                              int kw, int sh, int sw, int ph, int pw, int dh, int dw, int OH, int OW) {
-  const int64_t total = (int64_t)C * kh * kw * OH * OW;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int ow = (int)(i % OW);
-    int64_t t = i / OW;
-    const int oh = (int)(t % OH);
-    t /= OH;
-    const int j = (int)(t % kw);
-    t /= kw;
-    const int ii = (int)(t % kh);
-    const int c = (int)(t / kh);
-    const int ih = oh * sh - ph + ii * dh, iw = ow * sw - pw + j * dw;
-    col[i] = (ih >= 0 && ih < H && iw >= 0 && iw < W) ? x[((int64_t)c * H + ih) * W + iw] : 0.f;
+// =============================================================== conv2d (ops/convnd.py call shapes)
+constexpr int64_t kColBudget = int64_t(1) << 28;  // floats per column chunk (1 GiB)
+
+struct Conv {
+  int64_t N, C, H, W, OC, kh, kw, OH, OW, G, Cg, OCg, CgK, S;
+  bool pointwise;
+  int geo[19];  // vol2col geometry: C, D, H, W, OD, OH, OW, kd, kh, kw, sd, sh, sw, pd, ph, pw, dd, dh, dw
+  int64_t chunk() const {
+    int64_t nb = std::max<int64_t>(1, std::min<int64_t>(N, kColBudget / std::max<int64_t>(C * kh * kw * S, 1)));
+    return std::max<int64_t>(1, std::min<int64_t>(nb, 65535 / std::max<int64_t>(G, 1)));
   }
+};
+
+Conv conv_of(const OpRun& r, const Dims& xd, const Dims& wd) {
+  auto st = r.op.GetInts("strides"), pd = r.op.GetInts("paddings"), dl = r.op.GetInts("dilations");
+  if (st.empty()) st = {1, 1};
+  if (pd.empty()) pd = {0, 0};
+  if (dl.empty()) dl = {1, 1};
+  PA_CHECK(xd.size() == 4 && wd.size() == 4 && st.size() >= 2 && pd.size() >= 2 && dl.size() >= 2,
+           "conv2d: NCHW input and 2-D attributes expected");
+  Conv c;
+  c.G = std::max<int64_t>(1, r.op.GetInt("groups", 1));
+  c.N = xd[0]; c.C = xd[1]; c.H = xd[2]; c.W = xd[3];
+  c.OC = wd[0]; c.kh = wd[2]; c.kw = wd[3];
+  PA_CHECK(wd[1] * c.G == c.C && c.OC % c.G == 0, "conv2d: filter / input channel mismatch");
+  c.OH = (c.H + 2 * pd[0] - (dl[0] * (c.kh - 1) + 1)) / st[0] + 1;
+  c.OW = (c.W + 2 * pd[1] - (dl[1] * (c.kw - 1) + 1)) / st[1] + 1;
+  PA_CHECK(c.OH > 0 && c.OW > 0, "conv2d: empty output");
+  c.Cg = c.C / c.G; c.OCg = c.OC / c.G; c.CgK = c.Cg * c.kh * c.kw; c.S = c.OH * c.OW;
+  c.pointwise = c.kh == 1 && c.kw == 1 && st[0] == 1 && st[1] == 1 && pd[0] == 0 && pd[1] == 0;
+  const int64_t g[19] = {c.C, 1, c.H, c.W, 1, c.OH, c.OW, 1, c.kh, c.kw, 1, st[0], st[1], 0, pd[0], pd[1],
+                         1, dl[0], dl[1]};
+  for (int i = 0; i < 19; ++i) c.geo[i] = (int)g[i];
+  return c;
+}
+
+void sg(const OpRun& r, const float* A, long sam, long sak, const float* B, long sbk, long sbn, float* C, long ldc,
+        long M, long N, long K, int Z1, int Z2, long a1, long b1, long c1, long a2, long b2, long c2, int kb = 1,
+        long kbA = 0, long kbB = 0, const float* bias = nullptr, long bsb = 0, int atomic = 0) {
+  PA_CHECK((int64_t)Z1 * Z2 <= 65535, "conv: batch x groups too large");
+  PA_KL(pa_sgemm(A, sam, sak, B, sbk, sbn, C, ldc, M, N, K, Z1, Z2, a1, b1, c1, a2, b2, c2, kb, kbA, kbB, bias, bsb,
+                 1.f, 0.f, atomic, nullptr, S(r)));
 }
 
 void k_conv2d(const OpRun& r) {
   Tensor x = r.in("Input");
   Tensor w = r.in("Filter");
-  auto st = r.op.GetInts("strides"), pd = r.op.GetInts("paddings"), dl = r.op.GetInts("dilations");
-  if (st.empty()) st = {1, 1};
-  if (pd.empty()) pd = {0, 0};
-  if (dl.empty()) dl = {1, 1};
-  const int64_t g = std::max<int64_t>(1, r.op.GetInt("groups", 1));
-  const int64_t N = x.dims[0], C = x.dims[1], H = x.dims[2], W = x.dims[3];
-  const int64_t OC = w.dims[0], kh = w.dims[2], kw = w.dims[3];
-  PA_CHECK(w.dims[1] * g == C, "conv2d: filter / input channel mismatch");
-  const int64_t OH = (H + 2 * pd[0] - (dl[0] * (kh - 1) + 1)) / st[0] + 1;
-  const int64_t OW = (W + 2 * pd[1] - (dl[1] * (kw - 1) + 1)) / st[1] + 1;
-  Tensor* o = r.out("Output");
-  float* op = o->alloc<float>({N, OC, OH, OW}, D(r));
-  const int64_t Cg = C / g, OCg = OC / g, Kc = Cg * kh * kw, P = OH * OW;
-  Variable* cv = r.scope.Var("@conv_col@");  // im2col workspace kept across ops / runs
-  float* col = cv->tensor.alloc<float>({Kc, P}, D(r));
+  Tensor* b = r.in_opt("Bias");
+  const Conv c = conv_of(r, x.dims, w.dims);
+  float* y = r.out("Output")->alloc<float>({c.N, c.OC, c.OH, c.OW}, D(r));
   const float* xp = f32(x);
   const float* wp = f32(w);
-  for (int64_t n = 0; n < N; ++n)
-    for (int64_t gi = 0; gi < g; ++gi) {
-      hipLaunchKernelGGL(im2col_kernel, dim3(grid_for(Kc * P)), dim3(256), 0, S(r), xp + (n * C + gi * Cg) * H * W,
-                         col, (int)Cg, (int)H, (int)W, (int)kh, (int)kw, (int)st[0], (int)st[1], (int)pd[0],
-                         (int)pd[1], (int)dl[0], (int)dl[1], (int)OH, (int)OW);
-      gemm(S(r), false, false, OCg, P, Kc, 1.f, wp + gi * OCg * Kc, Kc, col, P, 0.f, op + (n * OC + gi * OCg) * P,
-           P);
-    }
+  const float* bp = b ? f32(*b) : nullptr;
+  if (c.pointwise) {
+    sg(r, wp, c.CgK, 1, xp, c.S, 1, y, c.S, c.OCg, c.S, c.CgK, (int)c.N, (int)c.G, 0, c.C * c.S, c.OC * c.S,
+       c.OCg * c.CgK, c.CgK * c.S, c.OCg * c.S, 1, 0, 0, bp, c.OCg);
+    return;
+  }
+  const int64_t nb = c.chunk(), rows = c.C * c.kh * c.kw;
+  float* col = workspace(r, "@conv_col@", nb * rows * c.S);
+  for (int64_t n0 = 0; n0 < c.N; n0 += nb) {
+    const int m = (int)std::min(nb, c.N - n0);
+    PA_KL(pa_vol2col(0, xp + n0 * c.C * c.H * c.W, col, c.geo, m, S(r)));
+    sg(r, wp, c.CgK, 1, col, c.S, 1, y + n0 * c.OC * c.S, c.S, c.OCg, c.S, c.CgK, m, (int)c.G, 0, rows * c.S,
+       c.OC * c.S, c.OCg * c.CgK, c.CgK * c.S, c.OCg * c.S, 1, 0, 0, bp, c.OCg);
+  }
 }
 
-// =============================================================== pooling / batch norm
-__global__ void pool2d_kernel(const float* __restrict__ x, float* __restrict__ o, int64_t NC, int H, int W, int OH,
-                              int OW, int kh, int kw, int sh, int sw, int ph, int pw, int is_max, int excl) {
-  const int64_t total = NC * OH * OW;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int ow = (int)(i % OW), oh = (int)((i / OW) % OH);
-    const int64_t nc = i / ((int64_t)OW * OH);
-    const int h0 = oh * sh - ph, w0 = ow * sw - pw;
-    const int h1 = min(h0 + kh, H), w1 = min(w0 + kw, W), hs = max(h0, 0), ws = max(w0, 0);
-    const float* xi = x + nc * H * W;
-    float acc = is_max ? -INFINITY : 0.f;
-    for (int h = hs; h < h1; ++h)
-      for (int w = ws; w < w1; ++w) acc = is_max ? fmaxf(acc, xi[h * W + w]) : acc + xi[h * W + w];
-    if (!is_max) acc /= (float)max(1, excl ? (h1 - hs) * (w1 - ws) : kh * kw);
-    o[i] = acc;
+// conv2d_grad (conv_op.h GemmConvGradKernel): dX = col2im(W^T dY), dW = sum_img dY col(X)^T
+// (images on the GEMM's k-batch, float-atomic split), dBias = per-channel sums of dY
+void k_conv2d_grad(const OpRun& r) {
+  Tensor x = r.in("Input");
+  Tensor w = r.in("Filter");
+  Tensor dy = r.in("Output@GRAD");
+  const Conv c = conv_of(r, x.dims, w.dims);
+  PA_CHECK(dy.numel() == c.N * c.OC * c.S, "conv2d_grad: Output@GRAD %s does not match", dy.shape_str().c_str());
+  const float* xp = f32(x);
+  const float* wp = f32(w);
+  const float* gp = f32(dy);
+  const int64_t nb = c.chunk(), rows = c.C * c.kh * c.kw;
+  Tensor* dxt = r.out("Input@GRAD");
+  Tensor* dwt = r.out("Filter@GRAD");
+  Tensor* dbt = r.out("Bias@GRAD");
+  float* col = (dxt || dwt) && !c.pointwise ? workspace(r, "@conv_col@", nb * rows * c.S) : nullptr;
+  if (dxt) {
+    float* dx = dxt->alloc<float>(x.dims, D(r));
+    if (c.pointwise) {
+      sg(r, wp, 1, c.CgK, gp, c.S, 1, dx, c.S, c.CgK, c.S, c.OCg, (int)c.N, (int)c.G, 0, c.OC * c.S, c.C * c.S,
+         c.OCg * c.CgK, c.OCg * c.S, c.CgK * c.S);
+    } else {
+      for (int64_t n0 = 0; n0 < c.N; n0 += nb) {
+        const int m = (int)std::min(nb, c.N - n0);
+        sg(r, wp, 1, c.CgK, gp + n0 * c.OC * c.S, c.S, 1, col, c.S, c.CgK, c.S, c.OCg, m, (int)c.G, 0, c.OC * c.S,
+           rows * c.S, c.OCg * c.CgK, c.OCg * c.S, c.CgK * c.S);
+        PA_KL(pa_col2vol(col, dx + n0 * c.C * c.H * c.W, c.geo, m, 0, S(r)));
+      }
+    }
   }
+  if (dwt) {
+    float* dw = dwt->alloc<float>(w.dims, D(r));
+    HIPCHK(hipMemsetAsync(dw, 0, sizeof(float) * w.numel(), S(r)));
+    for (int64_t n0 = 0; n0 < c.N; n0 += nb) {
+      const int m = (int)std::min(nb, c.N - n0);
+      const float* cp = xp + n0 * c.C * c.H * c.W;
+      if (!c.pointwise) {
+        PA_KL(pa_vol2col(0, cp, col, c.geo, m, S(r)));
+        cp = col;
+      }
+      sg(r, gp + n0 * c.OC * c.S, c.S, 1, cp, 1, c.S, dw, c.CgK, c.OCg, c.CgK, c.S, 1, (int)c.G, 0, 0, 0,
+         c.OCg * c.S, c.CgK * c.S, c.OCg * c.CgK, m, c.OC * c.S, rows * c.S, nullptr, 0, 1);
+    }
+  }
+  if (dbt) PA_KL(pa_chan_sum(gp, dbt->alloc<float>({c.OC}, D(r)), (int)c.N, (int)c.OC, c.S, 0, S(r)));
+}
+
+// =============================================================== pooling (pa_pool_*)
+struct Pool {
+  int64_t N, C, H, W, OH, OW;
+  int type, exclusive;
+  int geo[15];  // D, H, W, OD, OH, OW, kd, kh, kw, sd, sh, sw, pd, ph, pw
+};
+
+Pool pool_of(const OpRun& r, const Dims& xd) {
+  PA_CHECK(xd.size() == 4, "pool2d: NCHW input expected");
+  auto ks = r.op.GetInts("ksize"), st = r.op.GetInts("strides"), pd = r.op.GetInts("paddings");
+  if (st.empty()) st = {1, 1};
+  if (pd.empty()) pd = {0, 0};
+  Pool p;
+  p.N = xd[0]; p.C = xd[1]; p.H = xd[2]; p.W = xd[3];
+  if (r.op.GetBool("global_pooling")) {
+    ks = {p.H, p.W};
+    pd = {0, 0};
+  }
+  PA_CHECK(ks.size() >= 2 && st.size() >= 2 && pd.size() >= 2, "pool2d: 2-D attributes expected");
+  const bool ceil = r.op.GetBool("ceil_mode");
+  auto osz = [&](int64_t in, int64_t k, int64_t pp, int64_t s) {
+    return ceil ? (in - k + 2 * pp + s - 1) / s + 1 : (in - k + 2 * pp) / s + 1;
+  };
+  p.OH = osz(p.H, ks[0], pd[0], st[0]);
+  p.OW = osz(p.W, ks[1], pd[1], st[1]);
+  p.type = r.op.GetString("pooling_type", "max") == "max" ? 0 : 1;
+  p.exclusive = r.op.GetBool("exclusive", true) ? 1 : 0;
+  const int64_t g[15] = {1, p.H, p.W, 1, p.OH, p.OW, 1, ks[0], ks[1], 1, st[0], st[1], 0, pd[0], pd[1]};
+  for (int i = 0; i < 15; ++i) p.geo[i] = (int)g[i];
+  return p;
+}
+
+// max pooling keeps its in-plane argmax next to Out (var "<Out>@MASK") for the grad op
+int* pool_mask(const OpRun& r, const std::string& out_name, const Pool& p) {
+  Variable* v = r.scope.Var(out_name + "@MASK");
+  return static_cast<int*>(v->tensor.alloc(DT::INT32, {p.N, p.C, p.OH, p.OW}, D(r)));
 }
 
 void k_pool2d(const OpRun& r) {
   Tensor x = r.in("X");
-  const bool is_max = r.op.GetString("pooling_type", "max") == "max";
-  auto ks = r.op.GetInts("ksize"), st = r.op.GetInts("strides"), pd = r.op.GetInts("paddings");
-  if (st.empty()) st = {1, 1};
-  if (pd.empty()) pd = {0, 0};
-  const int64_t N = x.dims[0], C = x.dims[1], H = x.dims[2], W = x.dims[3];
-  if (r.op.GetBool("global_pooling")) {
-    ks = {H, W};
-    pd = {0, 0};
-  }
-  const bool ceil = r.op.GetBool("ceil_mode"), excl = r.op.GetBool("exclusive", true);
-  auto osz = [&](int64_t in, int64_t k, int64_t p, int64_t s) {
-    return ceil ? (in - k + 2 * p + s - 1) / s + 1 : (in - k + 2 * p) / s + 1;
-  };
-  const int64_t OH = osz(H, ks[0], pd[0], st[0]), OW = osz(W, ks[1], pd[1], st[1]);
-  float* o = r.out("Out")->alloc<float>({N, C, OH, OW}, D(r));
-  hipLaunchKernelGGL(pool2d_kernel, dim3(grid_for(N * C * OH * OW)), dim3(256), 0, S(r), f32(x), o, N * C, (int)H,
-                     (int)W, (int)OH, (int)OW, (int)ks[0], (int)ks[1], (int)st[0], (int)st[1], (int)pd[0],
-                     (int)pd[1], is_max ? 1 : 0, excl ? 1 : 0);
+  const Pool p = pool_of(r, x.dims);
+  float* o = r.out("Out")->alloc<float>({p.N, p.C, p.OH, p.OW}, D(r));
+  int* mask = p.type == 0 ? pool_mask(r, r.op.Output("Out"), p) : nullptr;
+  PA_KL(pa_pool_fwd(0, f32(x), o, mask, p.N * p.C, p.geo, p.type, p.exclusive, S(r)));
 }
 
-__global__ void bn_infer_kernel(const float* __restrict__ x, float* __restrict__ y, const float* __restrict__ sc,
-                                const float* __restrict__ bi, const float* __restrict__ mean,
-                                const float* __restrict__ var, float eps, int64_t total, int64_t C, int64_t HW,
-                                int nhwc) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t c = nhwc ? i % C : (i / HW) % C;
-    const float a = sc[c] * rsqrtf(var[c] + eps);
-    y[i] = (x[i] - mean[c]) * a + bi[c];
+void k_pool2d_grad(const OpRun& r) {
+  Tensor x = r.in("X");
+  Tensor dy = r.in("Out@GRAD");
+  const Pool p = pool_of(r, x.dims);
+  Tensor* dx = r.out("X@GRAD");
+  if (!dx) return;
+  const int* mask = nullptr;
+  if (p.type == 0) {
+    Variable* mv = r.scope.Find(r.op.Input("Out") + "@MASK");
+    if (mv && mv->tensor.initialized() && mv->tensor.device == D(r) && mv->tensor.numel() == dy.numel()) {
+      mask = mv->tensor.data<int>();
+    } else {  // forward ran elsewhere (host fallback / another executor): rebuild the argmax
+      int* m = pool_mask(r, r.op.Input("Out"), p);
+      float* tmp = workspace(r, "@pool_tmp@", dy.numel());
+      PA_KL(pa_pool_fwd(0, f32(x), tmp, m, p.N * p.C, p.geo, 0, p.exclusive, S(r)));
+      mask = m;
+    }
   }
+  float* dxp = dx->alloc<float>(x.dims, D(r));
+  PA_KL(pa_pool_bwd(0, f32(dy), mask, dxp, p.N * p.C, p.geo, p.type, p.exclusive, S(r)));
+}
+
+// =============================================================== batch norm (pa_bn_nchw_*)
+__global__ void bn_infer_nhwc_kernel(const float* __restrict__ x, float* __restrict__ y, const float* __restrict__ sc,
+                                     const float* __restrict__ bi, const float* __restrict__ mean,
+                                     const float* __restrict__ var, float eps, int64_t total, int64_t C) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = i % C;
+    y[i] = (x[i] - mean[c]) * (sc[c] * rsqrtf(var[c] + eps)) + bi[c];
+  }
+}
+
+// the output buffer of `out_slot`: the input's buffer when the op updates in place
+float* io_slot(const OpRun& r, const char* in_slot, const char* out_slot, int64_t n) {
+  Tensor& in = r.in(in_slot);
+  if (r.op.Output(out_slot) == r.op.Input(in_slot) || r.op.Output(out_slot).empty()) return f32(in);
+  return r.out(out_slot)->alloc<float>({n}, D(r));
 }
 
 void k_batch_norm(const OpRun& r) {
-  PA_CHECK(r.ctx.is_test || r.op.GetBool("is_test") || r.op.GetBool("use_global_stats"),
-           "batch_norm: device kernel is inference-only");
-  Tensor x = r.in("X");
-  const bool nhwc = r.op.GetString("data_layout", "NCHW") == "NHWC";
-  const int64_t N = x.dims[0], C = nhwc ? x.dims.back() : x.dims[1], HW = x.numel() / (N * C);
-  Dims d = x.dims;
-  float* y = r.out("Y")->alloc<float>(d, D(r));
-  hipLaunchKernelGGL(bn_infer_kernel, dim3(grid_for(x.numel())), dim3(256), 0, S(r), f32(x), y, f32(r.in("Scale")),
-                     f32(r.in("Bias")), f32(r.in("Mean")), f32(r.in("Variance")), r.op.GetFloat("epsilon", 1e-5f),
-                     x.numel(), C, HW, nhwc ? 1 : 0);
+  Tensor& x = r.in("X");
+  const bool test = r.ctx.is_test || r.op.GetBool("is_test") || r.op.GetBool("use_global_stats");
+  const float eps = r.op.GetFloat("epsilon", 1e-5f), mom = r.op.GetFloat("momentum", 0.9f);
+  const int relu = r.op.GetBool("fuse_with_relu") ? 1 : 0;
+  const Dims xd = x.dims;
+  if (r.op.GetString("data_layout", "NCHW") == "NHWC") {
+    if (!test || relu) throw Decline();
+    const int64_t C = xd.back();
+    float* y = r.out("Y")->alloc<float>(xd, D(r));
+    hipLaunchKernelGGL(bn_infer_nhwc_kernel, dim3(grid_for(x.numel())), dim3(256), 0, S(r), f32(x), y,
+                       f32(r.in("Scale")), f32(r.in("Bias")), f32(r.in("Mean")), f32(r.in("Variance")), eps,
+                       x.numel(), C);
+    return;
+  }
+  PA_CHECK(xd.size() >= 2, "batch_norm: rank");
+  const int64_t N = xd[0], C = xd[1], Sp = x.numel() / std::max<int64_t>(N * C, 1);
+  const float* xp = f32(x);
+  float* mean_out = test ? nullptr : io_slot(r, "Mean", "MeanOut", C);
+  float* var_out = test ? nullptr : io_slot(r, "Variance", "VarianceOut", C);
+  Tensor* sm = r.out("SavedMean");
+  Tensor* sv = r.out("SavedVariance");
+  float* mean = sm ? sm->alloc<float>({C}, D(r)) : workspace(r, "@bn_mean@", C);
+  float* rstd = sv ? sv->alloc<float>({C}, D(r)) : workspace(r, "@bn_rstd@", C);
+  float* part = workspace(r, "@bn_part@", C * (int64_t)pa_bn_nchw_groups((int)C, N * Sp) * 2);
+  float* y = r.out("Y")->alloc<float>(xd, D(r));
+  PA_KL(pa_bn_nchw_fwd(0, xp, y, f32(r.in("Scale")), f32(r.in("Bias")), f32(r.in("Mean")), f32(r.in("Variance")),
+                       mean_out, var_out, mean, rstd, part, (int)N, (int)C, Sp, eps, mom, test ? 0 : 1, relu, 0,
+                       S(r)));
 }
 
-// =============================================================== softmax (one wave per row)
-__global__ void softmax_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t rows, int64_t n) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const float* xr = x + row * n;
-  float* yr = y + row * n;
-  float m = -INFINITY;
-  for (int64_t j = lane; j < n; j += 64) m = fmaxf(m, xr[j]);
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  float s = 0.f;
-  for (int64_t j = lane; j < n; j += 64) s += __expf(xr[j] - m);
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  const float inv = 1.f / s;
-  for (int64_t j = lane; j < n; j += 64) yr[j] = __expf(xr[j] - m) * inv;
+// batch_norm_grad (batch_norm_op.cc BatchNormGradKernel) from SavedMean / SavedVariance (= 1/std)
+void k_batch_norm_grad(const OpRun& r) {
+  if (r.op.GetString("data_layout", "NCHW") == "NHWC") throw Decline();
+  Tensor& x = r.in("X");
+  Tensor& dy = r.in("Y@GRAD");
+  const int relu = r.op.GetBool("fuse_with_relu") ? 1 : 0;
+  Tensor* y = r.in_opt("Y");
+  if (relu && !y) throw Decline();
+  const Dims xd = x.dims;
+  const int64_t N = xd[0], C = xd[1], Sp = x.numel() / std::max<int64_t>(N * C, 1);
+  Tensor* ds = r.out("Scale@GRAD");
+  Tensor* db = r.out("Bias@GRAD");
+  float* dscale = ds ? ds->alloc<float>(r.in("Scale").dims, D(r)) : workspace(r, "@bn_dscale@", C);
+  float* dbias = db ? db->alloc<float>(r.in("Bias").dims, D(r)) : workspace(r, "@bn_dbias@", C);
+  Tensor* dxt = r.out("X@GRAD");
+  float* dx = dxt ? dxt->alloc<float>(xd, D(r)) : nullptr;
+  float* part = workspace(r, "@bn_part@", C * (int64_t)pa_bn_nchw_groups((int)C, N * Sp) * 2);
+  PA_KL(pa_bn_nchw_bwd(0, f32(x), f32(dy), y ? f32(*y) : nullptr, f32(r.in("SavedMean")),
+                       f32(r.in("SavedVariance")), f32(r.in("Scale")), dscale, dbias, dx, part, (int)N, (int)C, Sp,
+                       relu, S(r)));
+}
+
+// =============================================================== softmax / cross entropy
+int64_t last_axis_rows(const OpRun& r, const Tensor& x, int64_t* n) {
+  int64_t axis = r.op.GetInt("axis", -1);
+  if (axis < 0) axis += (int64_t)x.dims.size();
+  if (axis != (int64_t)x.dims.size() - 1) throw Decline();
+  *n = x.dims.back();
+  return *n ? x.numel() / *n : 0;
 }
 
 void k_softmax(const OpRun& r) {
-  Tensor x = r.in("X");
-  int64_t axis = r.op.GetInt("axis", -1);
-  if (axis < 0) axis += (int64_t)x.dims.size();
-  PA_CHECK(axis == (int64_t)x.dims.size() - 1, "softmax: last axis only");
-  const int64_t n = x.dims.back(), rows = x.numel() / n;
-  Tensor* o = r.out("Out");
-  Dims d = x.dims;
-  float* y = o->alloc<float>(d, D(r));
-  o->lod = x.lod;
-  hipLaunchKernelGGL(softmax_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, S(r), f32(x), y, rows, n);
+  Tensor& x = r.in("X");
+  int64_t n;
+  const int64_t rows = last_axis_rows(r, x, &n);
+  const LoD lod = x.lod;
+  float* y = out_f32(r, "Out", x.dims, &x);
+  r.out("Out")->lod = lod;
+  PA_KL(pa_softmax_fwd(0, f32(x), y, rows, (int)n, 0, S(r)));
+}
+
+void k_softmax_grad(const OpRun& r) {
+  Tensor& y = r.in("Out");
+  Tensor& g = r.in("Out@GRAD");
+  int64_t n;
+  const int64_t rows = last_axis_rows(r, y, &n);
+  Tensor* dx = r.out("X@GRAD");
+  if (!dx) return;
+  PA_KL(pa_softmax_bwd(0, f32(y), f32(g), dx->alloc<float>(y.dims, D(r)), rows, (int)n, 0, S(r)));
+}
+
+const long* hard_labels(const Tensor& l, int64_t rows) {
+  if (l.dtype != DT::INT64 || l.numel() != rows) throw Decline();
+  return l.data<long>();
+}
+
+void k_cross_entropy(const OpRun& r) {
+  Tensor& x = r.in("X");
+  Tensor& l = r.in("Label");
+  const int64_t n = x.dims.back(), rows = n ? x.numel() / n : 0;
+  const bool soft = r.op.GetBool("soft_label");
+  const long* lab = soft ? nullptr : hard_labels(l, rows);
+  if (soft && (l.dtype != DT::FP32 || l.numel() != x.numel())) throw Decline();
+  Dims od(x.dims.begin(), x.dims.end() - 1);
+  od.push_back(1);
+  const LoD lod = x.lod;
+  float* y = r.out("Y")->alloc<float>(od, D(r));
+  r.out("Y")->lod = lod;
+  PA_KL(pa_cross_entropy(0, 0, f32(x), lab, soft ? f32(l) : nullptr, nullptr, y, rows, (int)n,
+                         r.op.GetInt("ignore_index", -100), S(r)));
+}
+
+void k_cross_entropy_grad(const OpRun& r) {
+  Tensor& x = r.in("X");
+  Tensor& l = r.in("Label");
+  Tensor& g = r.in("Y@GRAD");
+  const int64_t n = x.dims.back(), rows = n ? x.numel() / n : 0;
+  const bool soft = r.op.GetBool("soft_label");
+  const long* lab = soft ? nullptr : hard_labels(l, rows);
+  if (soft && (l.dtype != DT::FP32 || l.numel() != x.numel())) throw Decline();
+  Tensor* dx = r.out("X@GRAD");
+  if (!dx) return;
+  PA_KL(pa_cross_entropy(0, 1, f32(x), lab, soft ? f32(l) : nullptr, f32(g), dx->alloc<float>(x.dims, D(r)), rows,
+                         (int)n, r.op.GetInt("ignore_index", -100), S(r)));
+}
+
+void k_softmax_ce(const OpRun& r) {
+  Tensor& x = r.in("Logits");
+  Tensor& l = r.in("Label");
+  int64_t n;
+  const int64_t rows = last_axis_rows(r, x, &n);
+  const bool soft = r.op.GetBool("soft_label");
+  const long* lab = soft ? nullptr : hard_labels(l, rows);
+  if (soft && (l.dtype != DT::FP32 || l.numel() != x.numel())) throw Decline();
+  Dims od(x.dims.begin(), x.dims.end() - 1);
+  od.push_back(1);
+  const Dims xd = x.dims;
+  float* prob = r.out("Softmax")->alloc<float>(xd, D(r));
+  float* loss = r.out("Loss")->alloc<float>(od, D(r));
+  PA_KL(pa_softmax_ce_prob_fwd(0, f32(x), lab, soft ? f32(l) : nullptr, prob, loss, rows, (int)n,
+                               r.op.GetInt("ignore_index", -100), S(r)));
+}
+
+void k_softmax_ce_grad(const OpRun& r) {
+  Tensor& p = r.in("Softmax");
+  Tensor& l = r.in("Label");
+  Tensor& g = r.in("Loss@GRAD");
+  int64_t n;
+  const int64_t rows = last_axis_rows(r, p, &n);
+  const bool soft = r.op.GetBool("soft_label");
+  const long* lab = soft ? nullptr : hard_labels(l, rows);
+  if (soft && (l.dtype != DT::FP32 || l.numel() != p.numel())) throw Decline();
+  Tensor* dx = r.out("Logits@GRAD");
+  if (!dx) return;
+  PA_KL(pa_softmax_ce_prob_bwd(0, f32(p), lab, soft ? f32(l) : nullptr, f32(g), dx->alloc<float>(p.dims, D(r)), rows,
+                               (int)n, r.op.GetInt("ignore_index", -100), S(r)));
 }
 
 // =============================================================== reductions over [pre, R, post]
@@ -531,7 +762,8 @@ template <int KIND> void k_reduce(const OpRun& r) {  // 0 sum 1 mean 2 max 3 min
       if (a < 0) a = i;
       e = i + 1;
     }
-  for (int64_t i = a; i < e; ++i) PA_CHECK(red[(size_t)i], "reduce: non-contiguous reduced dims on device");
+  for (int64_t i = a; i < e; ++i)
+    if (!red[(size_t)i]) throw Decline();  // non-contiguous reduced dims: host
   Dims od, kd;
   for (int64_t i = 0; i < R; ++i) {
     if (!red[(size_t)i]) od.push_back(x.dims[(size_t)i]);
@@ -543,10 +775,88 @@ template <int KIND> void k_reduce(const OpRun& r) {  // 0 sum 1 mean 2 max 3 min
   hipLaunchKernelGGL(reduce_kernel, dim3(grid_for(pre * post)), dim3(256), 0, S(r), f32(x), o, pre, RR, post, KIND);
 }
 
+// mean: one 1024-thread block, fixed-order tree (deterministic)
+__global__ __launch_bounds__(1024) void mean_kernel(const float* __restrict__ x, float* __restrict__ o, int64_t n) {
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) s += x[i];
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    s = threadIdx.x < 16 ? red[threadIdx.x] : 0.f;
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if (threadIdx.x == 0) o[0] = s / (float)n;
+  }
+}
+
 void k_mean(const OpRun& r) {
   Tensor x = r.in("X");
   float* o = r.out("Out")->alloc<float>({1}, D(r));
-  hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(64), 0, S(r), f32(x), o, (int64_t)1, x.numel(), (int64_t)1, 1);
+  hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(1024), 0, S(r), f32(x), o, x.numel());
+}
+
+__global__ void mean_grad_kernel(const float* __restrict__ g, float* __restrict__ dx, int64_t n) {
+  const float v = g[0] / (float)n;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dx[i] = v;
+}
+
+void k_mean_grad(const OpRun& r) {
+  Tensor& x = r.in("X");
+  Tensor& g = r.in("Out@GRAD");
+  Tensor* dx = r.out("X@GRAD");
+  if (!dx) return;
+  const Dims d = x.dims;
+  const LoD lod = x.lod;
+  float* p = dx->alloc<float>(d, D(r));
+  dx->lod = lod;
+  if (dx->numel())
+    hipLaunchKernelGGL(mean_grad_kernel, dim3(grid_for(dx->numel())), dim3(256), 0, S(r), f32(g), p, dx->numel());
+}
+
+// =============================================================== optimizers (in place when Out == In)
+int64_t opt_n(const OpRun& r) {
+  Tensor& p = r.in("Param");
+  Tensor& g = r.in("Grad");
+  if (g.dtype != DT::FP32 || g.numel() != p.numel()) throw Decline();  // e.g. SelectedRows grads: host
+  return p.numel();
+}
+
+// the update target of `in_slot` -> `out_slot`: in place, or a copy of the input
+float* opt_target(const OpRun& r, const char* in_slot, const char* out_slot) {
+  Tensor& in = r.in(in_slot);
+  if (r.op.Output(out_slot) == r.op.Input(in_slot)) return f32(in);
+  const Dims d = in.dims;
+  const float* src = f32(in);
+  float* dst = r.out(out_slot)->alloc<float>(d, D(r));
+  copy_d2d(r, dst, src, sizeof(float) * prod(d));
+  return dst;
+}
+
+void k_sgd(const OpRun& r) {
+  const int64_t n = opt_n(r);
+  float* p = opt_target(r, "Param", "ParamOut");
+  PA_KL(pa_sgd(0, p, f32(r.in("Grad")), f32(r.in("LearningRate")), n, S(r)));
+}
+
+void k_momentum(const OpRun& r) {
+  const int64_t n = opt_n(r);
+  float* p = opt_target(r, "Param", "ParamOut");
+  float* v = opt_target(r, "Velocity", "VelocityOut");
+  PA_KL(pa_momentum(0, p, f32(r.in("Grad")), v, n, 0.f, f32(r.in("LearningRate")), r.op.GetFloat("mu", 0.9f),
+                    r.op.GetBool("use_nesterov") ? 1 : 0, 0.f, 1.f, S(r)));
+}
+
+// adam_op.h: lr_t = lr sqrt(1 - beta2^t) / (1 - beta1^t), p -= lr_t m / (sqrt(v) + eps)
+void k_adam(const OpRun& r) {
+  const int64_t n = opt_n(r);
+  float* p = opt_target(r, "Param", "ParamOut");
+  float* m1 = opt_target(r, "Moment1", "Moment1Out");
+  float* m2 = opt_target(r, "Moment2", "Moment2Out");
+  PA_KL(pa_adamw(0, -1, p, f32(r.in("Grad")), m1, m2, nullptr, n, 0.f, f32(r.in("LearningRate")),
+                 r.op.GetFloat("beta1", 0.9f), r.op.GetFloat("beta2", 0.999f), r.op.GetFloat("epsilon", 1e-8f), 0.f,
+                 0.f, 0.f, f32(r.in("Beta1Pow")), f32(r.in("Beta2Pow")), n, 1.f, nullptr, 1, S(r)));
 }
 
 // =============================================================== data movement
@@ -674,11 +984,19 @@ __global__ void accumulate_kernel(float* o, const float* x, int64_t n) {
 
 void k_fill_constant(const OpRun& r) {
   const DT dt = (DT)r.op.GetInt("dtype", (int)DT::FP32);
-  PA_CHECK(dt == DT::FP32, "fill_constant: float32 only on device");
+  if (dt != DT::FP32) throw Decline();  // integer fills (counters, ids): host
   Tensor* o = r.out("Out");
   float* p = o->alloc<float>(r.op.GetInts("shape"), D(r));
   hipLaunchKernelGGL(fill_kernel, dim3(grid_for(o->numel())), dim3(256), 0, S(r), p, o->numel(),
                      r.op.GetFloat("value"));
+}
+
+void k_fill_zeros_like(const OpRun& r) {
+  Tensor& x = r.in("X");
+  if (x.dtype != DT::FP32) throw Decline();
+  const Dims d = x.dims;
+  float* p = r.out("Out")->alloc<float>(d, D(r));
+  if (prod(d)) HIPCHK(hipMemsetAsync(p, 0, sizeof(float) * prod(d), S(r)));
 }
 
 void k_sum(const OpRun& r) {
@@ -697,13 +1015,23 @@ void k_sum(const OpRun& r) {
 }  // namespace
 
 PA_DEVICE_KERNEL(mul, k_mul);
+PA_DEVICE_KERNEL(mul_grad, k_mul_grad);
 PA_DEVICE_KERNEL(fc, k_fc);
 PA_DEVICE_KERNEL(matmul, k_matmul);
 PA_DEVICE_KERNEL(conv2d, k_conv2d);
 PA_DEVICE_KERNEL(depthwise_conv2d, k_conv2d);
+PA_DEVICE_KERNEL(conv2d_grad, k_conv2d_grad);
+PA_DEVICE_KERNEL(depthwise_conv2d_grad, k_conv2d_grad);
 PA_DEVICE_KERNEL(pool2d, k_pool2d);
+PA_DEVICE_KERNEL(pool2d_grad, k_pool2d_grad);
 PA_DEVICE_KERNEL(batch_norm, k_batch_norm);
+PA_DEVICE_KERNEL(batch_norm_grad, k_batch_norm_grad);
 PA_DEVICE_KERNEL(softmax, k_softmax);
+PA_DEVICE_KERNEL(softmax_grad, k_softmax_grad);
+PA_DEVICE_KERNEL(cross_entropy, k_cross_entropy);
+PA_DEVICE_KERNEL(cross_entropy_grad, k_cross_entropy_grad);
+PA_DEVICE_KERNEL(softmax_with_cross_entropy, k_softmax_ce);
+PA_DEVICE_KERNEL(softmax_with_cross_entropy_grad, k_softmax_ce_grad);
 PA_DEVICE_KERNEL(elementwise_add, k_binary<B_ADD>);
 PA_DEVICE_KERNEL(elementwise_sub, k_binary<B_SUB>);
 PA_DEVICE_KERNEL(elementwise_mul, k_binary<B_MUL>);
@@ -711,22 +1039,45 @@ PA_DEVICE_KERNEL(elementwise_div, k_binary<B_DIV>);
 PA_DEVICE_KERNEL(elementwise_max, k_binary<B_MAX>);
 PA_DEVICE_KERNEL(elementwise_min, k_binary<B_MIN>);
 PA_DEVICE_KERNEL(elementwise_pow, k_binary<B_POW>);
-PA_DEVICE_KERNEL(relu, k_unary<U_RELU>);
-PA_DEVICE_KERNEL(sigmoid, k_unary<U_SIGMOID>);
-PA_DEVICE_KERNEL(tanh, k_unary<U_TANH>);
-PA_DEVICE_KERNEL(exp, k_unary<U_EXP>);
-PA_DEVICE_KERNEL(log, k_unary<U_LOG>);
-PA_DEVICE_KERNEL(sqrt, k_unary<U_SQRT>);
-PA_DEVICE_KERNEL(abs, k_unary<U_ABS>);
-PA_DEVICE_KERNEL(square, k_unary<U_SQUARE>);
-PA_DEVICE_KERNEL(leaky_relu, k_unary<U_LEAKY>);
-PA_DEVICE_KERNEL(gelu, k_unary<U_GELU>);
-PA_DEVICE_KERNEL(relu6, k_unary<U_RELU6>);
-PA_DEVICE_KERNEL(softplus, k_unary<U_SOFTPLUS>);
-PA_DEVICE_KERNEL(swish, k_unary<U_SWISH>);
-PA_DEVICE_KERNEL(hard_sigmoid, k_unary<U_HSIG>);
-PA_DEVICE_KERNEL(elu, k_unary<U_ELU>);
-PA_DEVICE_KERNEL(reciprocal, k_unary<U_RECIP>);
+PA_DEVICE_KERNEL(elementwise_add_grad, k_ew_grad<1>);
+PA_DEVICE_KERNEL(elementwise_sub_grad, k_ew_grad<-1>);
+#define PA_ACT(name, ID)                       \
+  PA_DEVICE_KERNEL(name, k_act<act::ID>);      \
+  PA_DEVICE_KERNEL(name##_grad, k_act_grad<act::ID>)
+PA_ACT(relu, RELU);
+PA_ACT(sigmoid, SIGMOID);
+PA_ACT(logsigmoid, LOGSIGMOID);
+PA_ACT(exp, EXP);
+PA_ACT(tanh, TANH);
+PA_ACT(tanh_shrink, TANH_SHRINK);
+PA_ACT(softshrink, SOFTSHRINK);
+PA_ACT(sqrt, SQRT);
+PA_ACT(rsqrt, RSQRT);
+PA_ACT(abs, ABS);
+PA_ACT(ceil, CEIL);
+PA_ACT(floor, FLOOR);
+PA_ACT(cos, COS);
+PA_ACT(sin, SIN);
+PA_ACT(round, ROUND);
+PA_ACT(reciprocal, RECIPROCAL);
+PA_ACT(log, LOG);
+PA_ACT(square, SQUARE);
+PA_ACT(softplus, SOFTPLUS);
+PA_ACT(softsign, SOFTSIGN);
+PA_ACT(brelu, BRELU);
+PA_ACT(leaky_relu, LEAKY_RELU);
+PA_ACT(soft_relu, SOFT_RELU);
+PA_ACT(elu, ELU);
+PA_ACT(relu6, RELU6);
+PA_ACT(pow, POW);
+PA_ACT(stanh, STANH);
+PA_ACT(hard_shrink, HARD_SHRINK);
+PA_ACT(thresholded_relu, THRESHOLDED_RELU);
+PA_ACT(hard_sigmoid, HARD_SIGMOID);
+PA_ACT(swish, SWISH);
+PA_ACT(gelu, GELU);
+PA_ACT(silu, SILU);
+#undef PA_ACT
 PA_DEVICE_KERNEL(scale, k_scale);
 PA_DEVICE_KERNEL(dropout, k_dropout);
 PA_DEVICE_KERNEL(reduce_sum, k_reduce<0>);
@@ -734,12 +1085,17 @@ PA_DEVICE_KERNEL(reduce_mean, k_reduce<1>);
 PA_DEVICE_KERNEL(reduce_max, k_reduce<2>);
 PA_DEVICE_KERNEL(reduce_min, k_reduce<3>);
 PA_DEVICE_KERNEL(mean, k_mean);
+PA_DEVICE_KERNEL(mean_grad, k_mean_grad);
+PA_DEVICE_KERNEL(sgd, k_sgd);
+PA_DEVICE_KERNEL(momentum, k_momentum);
+PA_DEVICE_KERNEL(adam, k_adam);
 PA_DEVICE_KERNEL(lookup_table, k_lookup_table);
 PA_DEVICE_KERNEL(concat, k_concat);
 PA_DEVICE_KERNEL(split, k_split);
 PA_DEVICE_KERNEL(transpose, k_transpose);
 PA_DEVICE_KERNEL(transpose2, k_transpose);
 PA_DEVICE_KERNEL(fill_constant, k_fill_constant);
+PA_DEVICE_KERNEL(fill_zeros_like, k_fill_zeros_like);
 PA_DEVICE_KERNEL(sum, k_sum);
 
 void link_device_kernels() {}

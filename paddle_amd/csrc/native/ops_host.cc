@@ -1049,6 +1049,181 @@ void k_dropout(const OpRun& r) {
   o->lod = lod;
 }
 
+// ------------------------------------------------------------ conv / pool / batch-norm gradients
+// conv_op.h GemmConvGradKernel: per (image, group) dcol = W^T dY scattered back by
+// col2im, dW += dY col(X)^T; dBias = per-channel sums of dY
+void col2im_add(const float* col, int64_t C, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
+                int64_t ph, int64_t pw, int64_t dh, int64_t dw, int64_t OH, int64_t OW, float* x) {
+  for (int64_t c = 0; c < C; ++c)
+    for (int64_t i = 0; i < kh; ++i)
+      for (int64_t j = 0; j < kw; ++j) {
+        const float* row = col + ((c * kh + i) * kw + j) * OH * OW;
+        for (int64_t oh = 0; oh < OH; ++oh) {
+          const int64_t ih = oh * sh - ph + i * dh;
+          if (ih < 0 || ih >= H) continue;
+          for (int64_t ow = 0; ow < OW; ++ow) {
+            const int64_t iw = ow * sw - pw + j * dw;
+            if (iw >= 0 && iw < W) x[(c * H + ih) * W + iw] += row[oh * OW + ow];
+          }
+        }
+      }
+}
+
+void k_conv2d_grad(const OpRun& r) {
+  Tensor x = r.in("Input");
+  Tensor& w = r.in("Filter");
+  Tensor dy = r.in("Output@GRAD");
+  auto st = r.op.GetInts("strides"), pd = r.op.GetInts("paddings"), dl = r.op.GetInts("dilations");
+  if (st.empty()) st = {1, 1};
+  if (pd.empty()) pd = {0, 0};
+  if (dl.empty()) dl = {1, 1};
+  const int64_t g = std::max<int64_t>(1, r.op.GetInt("groups", 1));
+  const int64_t N = x.dims[0], C = x.dims[1], H = x.dims[2], W = x.dims[3];
+  const int64_t OC = w.dims[0], kh = w.dims[2], kw = w.dims[3];
+  const int64_t OH = dy.dims[2], OW = dy.dims[3];
+  const int64_t Cg = C / g, OCg = OC / g, Kc = Cg * kh * kw, P = OH * OW;
+  PA_CHECK(dy.numel() == N * OC * P, "conv2d_grad: Output@GRAD %s does not match", dy.shape_str().c_str());
+  const float* xp = f32(x);
+  const float* wp = f32(w);
+  const float* gp = f32(dy);
+  Tensor* dxt = r.out("Input@GRAD");
+  Tensor* dwt = r.out("Filter@GRAD");
+  Tensor* dbt = r.out("Bias@GRAD");
+  float* dx = dxt ? dxt->alloc<float>(x.dims, -1) : nullptr;
+  float* dw = dwt ? dwt->alloc<float>(w.dims, -1) : nullptr;
+  if (dx) memset(dx, 0, sizeof(float) * x.numel());
+  if (dw) memset(dw, 0, sizeof(float) * w.numel());
+  std::vector<float> col((size_t)(Kc * P));
+  for (int64_t n = 0; n < N; ++n)
+    for (int64_t gi = 0; gi < g; ++gi) {
+      const float* dyg = gp + (n * OC + gi * OCg) * P;
+      if (dw) {
+        im2col(xp + (n * C + gi * Cg) * H * W, Cg, H, W, kh, kw, st[0], st[1], pd[0], pd[1], dl[0], dl[1], OH, OW,
+               col.data());
+        sgemm(false, true, OCg, Kc, P, 1.f, dyg, P, col.data(), P, 1.f, dw + gi * OCg * Kc, Kc);
+      }
+      if (dx) {
+        sgemm(true, false, Kc, P, OCg, 1.f, wp + gi * OCg * Kc, Kc, dyg, P, 0.f, col.data(), P);
+        col2im_add(col.data(), Cg, H, W, kh, kw, st[0], st[1], pd[0], pd[1], dl[0], dl[1], OH, OW,
+                   dx + (n * C + gi * Cg) * H * W);
+      }
+    }
+  if (dbt) {
+    float* db = dbt->alloc<float>({OC}, -1);
+    for (int64_t c = 0; c < OC; ++c) {
+      double s = 0;
+      for (int64_t n = 0; n < N; ++n)
+        for (int64_t i = 0; i < P; ++i) s += gp[(n * OC + c) * P + i];
+      db[c] = (float)s;
+    }
+  }
+}
+
+// pool_op.h PoolGradKernel / math/pooling.cc: max routes dOut to the window's first
+// maximum, avg spreads it over the counted window
+void k_pool2d_grad(const OpRun& r) {
+  Tensor x = r.in("X");
+  Tensor dy = r.in("Out@GRAD");
+  const bool is_max = r.op.GetString("pooling_type", "max") == "max";
+  auto ks = r.op.GetInts("ksize"), st = r.op.GetInts("strides"), pd = r.op.GetInts("paddings");
+  if (st.empty()) st = {1, 1};
+  if (pd.empty()) pd = {0, 0};
+  const int64_t N = x.dims[0], C = x.dims[1], H = x.dims[2], W = x.dims[3];
+  if (r.op.GetBool("global_pooling")) {
+    ks = {H, W};
+    pd = {0, 0};
+  }
+  const bool excl = r.op.GetBool("exclusive", true);
+  const int64_t OH = dy.dims[2], OW = dy.dims[3];
+  Tensor* dxt = r.out("X@GRAD");
+  if (!dxt) return;
+  float* dx = dxt->alloc<float>(x.dims, -1);
+  memset(dx, 0, sizeof(float) * x.numel());
+  const float* xp = f32(x);
+  const float* gp = f32(dy);
+  parallel_for(N * C, 4, [&](int64_t a, int64_t b) {
+    for (int64_t nc = a; nc < b; ++nc) {
+      const float* xi = xp + nc * H * W;
+      float* di = dx + nc * H * W;
+      for (int64_t oh = 0; oh < OH; ++oh)
+        for (int64_t ow = 0; ow < OW; ++ow) {
+          const int64_t h0 = oh * st[0] - pd[0], w0 = ow * st[1] - pd[1];
+          const int64_t h1 = std::min(h0 + ks[0], H), w1 = std::min(w0 + ks[1], W);
+          const int64_t hs = std::max<int64_t>(h0, 0), ws = std::max<int64_t>(w0, 0);
+          const float g = gp[(nc * OH + oh) * OW + ow];
+          if (is_max) {
+            int64_t best = -1;
+            float bv = -INFINITY;
+            for (int64_t h = hs; h < h1; ++h)
+              for (int64_t w = ws; w < w1; ++w)
+                if (best < 0 || xi[h * W + w] > bv) {
+                  bv = xi[h * W + w];
+                  best = h * W + w;
+                }
+            if (best >= 0) di[best] += g;
+          } else {
+            const int64_t cnt = excl ? (h1 - hs) * (w1 - ws) : ks[0] * ks[1];
+            const float v = g / (float)std::max<int64_t>(1, cnt);
+            for (int64_t h = hs; h < h1; ++h)
+              for (int64_t w = ws; w < w1; ++w) di[h * W + w] += v;
+          }
+        }
+    }
+  });
+}
+
+// batch_norm_op.cc BatchNormGradKernel (NCHW / NHWC) from SavedMean and
+// SavedVariance (= 1 / sqrt(var + eps)):
+//   dx = scale * rstd * (dy - mean(dy) - xhat * mean(dy * xhat))
+void k_batch_norm_grad(const OpRun& r) {
+  Tensor x = r.in("X");
+  Tensor dy = r.in("Y@GRAD");
+  Tensor& sc = r.in("Scale");
+  const float* mean = f32(r.in("SavedMean"));
+  const float* rstd = f32(r.in("SavedVariance"));
+  const bool nhwc = r.op.GetString("data_layout", "NCHW") == "NHWC";
+  const bool relu = r.op.GetBool("fuse_with_relu");
+  const int64_t N = x.dims[0], C = nhwc ? x.dims.back() : x.dims[1], HW = x.numel() / (N * C);
+  auto at = [&](int64_t n, int64_t c, int64_t i) { return nhwc ? (n * HW + i) * C + c : (n * C + c) * HW + i; };
+  const float* xp = f32(x);
+  const float* gp = f32(dy);
+  const float* yp = relu ? f32(r.in("Y")) : nullptr;
+  std::vector<float> ds((size_t)C), db((size_t)C);
+  const double M = (double)N * HW;
+  Tensor* dxt = r.out("X@GRAD");
+  float* dx = dxt ? dxt->alloc<float>(x.dims, -1) : nullptr;
+  const float* s = f32(sc);
+  for (int64_t c = 0; c < C; ++c) {
+    double sg = 0, sgx = 0;
+    for (int64_t n = 0; n < N; ++n)
+      for (int64_t i = 0; i < HW; ++i) {
+        const int64_t k = at(n, c, i);
+        const double g = (yp && yp[k] <= 0.f) ? 0.0 : gp[k];
+        sg += g;
+        sgx += g * (xp[k] - mean[c]) * rstd[c];
+      }
+    db[(size_t)c] = (float)sg;
+    ds[(size_t)c] = (float)sgx;
+    if (!dx) continue;
+    for (int64_t n = 0; n < N; ++n)
+      for (int64_t i = 0; i < HW; ++i) {
+        const int64_t k = at(n, c, i);
+        const double g = (yp && yp[k] <= 0.f) ? 0.0 : gp[k];
+        const double xh = (xp[k] - mean[c]) * rstd[c];
+        dx[k] = (float)(s[c] * rstd[c] * (g - sg / M - xh * sgx / M));
+      }
+  }
+  if (Tensor* t = r.out("Scale@GRAD")) memcpy(t->alloc<float>(sc.dims, -1), ds.data(), sizeof(float) * C);
+  if (Tensor* t = r.out("Bias@GRAD")) memcpy(t->alloc<float>(r.in("Bias").dims, -1), db.data(), sizeof(float) * C);
+}
+
+void k_fill_zeros_like(const OpRun& r) {
+  Tensor& x = r.in("X");
+  Dims d = x.dims;
+  Tensor* o = r.out("Out");
+  memset(o->alloc(x.dtype, d, -1), 0, o->nbytes());
+}
+
 // ------------------------------------------------------------ optimizers (sgd_op.h, momentum_op.h, adam_op.h)
 void k_sgd(const OpRun& r) {
   Tensor& p = r.in("Param");
@@ -1217,6 +1392,11 @@ PA_HOST_KERNEL(conv2d, k_conv2d);
 PA_HOST_KERNEL(depthwise_conv2d, k_conv2d);
 PA_HOST_KERNEL(pool2d, k_pool2d);
 PA_HOST_KERNEL(batch_norm, k_batch_norm);
+PA_HOST_KERNEL(conv2d_grad, k_conv2d_grad);
+PA_HOST_KERNEL(depthwise_conv2d_grad, k_conv2d_grad);
+PA_HOST_KERNEL(pool2d_grad, k_pool2d_grad);
+PA_HOST_KERNEL(batch_norm_grad, k_batch_norm_grad);
+PA_HOST_KERNEL(fill_zeros_like, k_fill_zeros_like);
 PA_HOST_KERNEL(dropout, k_dropout);
 PA_HOST_KERNEL(sgd, k_sgd);
 PA_HOST_KERNEL(momentum, k_momentum);

@@ -9,6 +9,10 @@ and fetches results (the only host sync).
 ``Executor(place, use_hip_graph=True)`` additionally captures a steady-state step
 of a static-shape program into a HIP graph and replays it (MI355X-first
 replacement for launch-bound inner loops; see also ``FLAGS_use_hip_graph``).
+
+``Executor(place, engine="native")`` (or ``FLAGS_executor_engine=native``) runs
+programs on the C++ executor instead (:mod:`paddle_amd.fluid.native_engine`);
+programs it cannot take (sub-blocks, LoD feeds, ops without a C++ kernel) raise.
 """
 from __future__ import annotations
 
@@ -63,9 +67,13 @@ def as_numpy(tensor):
 
 
 class Executor:
-    def __init__(self, place=None, use_hip_graph=None):
+    def __init__(self, place=None, use_hip_graph=None, engine=None):
         self.place = place or core.CPUPlace()
         self._core = BlockExecutor(self.place)
+        self.engine = engine or FLAGS.get("executor_engine") or "python"
+        if self.engine not in ("python", "native"):
+            raise ValueError(f"unknown executor engine {self.engine!r}")
+        self._native = None
         self._closed = False
         self._prog_cache = {}
         self.use_hip_graph = FLAGS.get("use_hip_graph") if use_hip_graph is None else use_hip_graph
@@ -125,6 +133,12 @@ class Executor:
             scope = global_scope()
         fetch_names = [v.name if isinstance(v, Variable) else str(v) for v in fetch_list]
         feed_names = list(feed.keys())
+        if self.engine == "native" and program.global_block().ops:
+            if self._native is None:
+                from .native_engine import NativeEngine
+
+                self._native = NativeEngine(self.place)
+            return self._native.run(program, feed, fetch_names, scope, return_numpy)
         key = (id(program), program._version, tuple(feed_names), tuple(fetch_names), feed_var_name, fetch_var_name)
         prog = self._prog_cache.get(key)
         if prog is None:

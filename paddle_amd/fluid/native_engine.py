@@ -1,0 +1,147 @@
+"""The native C++ executor as an opt-in engine behind ``fluid.Executor``.
+
+``fluid.Executor(place, engine="native")`` (or ``FLAGS_executor_engine=native``)
+runs a program's block 0 on the C++ executor of ``csrc/native`` (core.cc
+Executor::RunBlock, the counterpart of the reference's framework/executor.cc:125-353)
+instead of the Python op interpreter: the program is serialised once
+(ProgramDesc wire format) and every op dispatches to a registered C++ kernel --
+on a HIP place the gfx950 device kernels of ``ops_gpu.hip``, which run the shared
+kernel library (GEMM, conv, pool, batch norm, softmax / loss, optimizers), with a
+counted host fallback for the few configurations a device kernel declines.
+
+Parameters and optimizer state are NOT copied: each persistable variable of the
+Python scope is lent to the native scope (its torch storage pointer), so the
+optimizer ops update the very tensors the Python side sees, and a variable whose
+native buffer was re-allocated by a kernel is copied back after the run.  Feeds are
+copied in; fetches are copied out (the only host syncs of a step).
+
+Scope of the engine: dense LoDTensor programs of block 0 (no control-flow
+sub-blocks, no LoD feeds, no SelectedRows); anything else raises
+``NotImplementedError`` naming what is unsupported -- use the default engine for it.
+
+Reference: framework/executor.cc:125-353 (Executor::Run), pybind/pybind.cc:507
+(the Executor binding the Python layer drives).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .. import native
+from ..framework import core
+
+_TORCH_DT = {torch.float32: 5, torch.int64: 3, torch.int32: 2, torch.float64: 6, torch.bool: 0, torch.uint8: 20}
+_DT_TORCH = {v: k for k, v in _TORCH_DT.items()}
+
+
+class NativeEngine:
+    def __init__(self, place):
+        self.place = place
+        self.device = int(place.device_id) if isinstance(place, core.CUDAPlace) else -1
+        self._exe = native.NativeExecutor(self.device)
+        self._progs = {}
+        self._scopes = {}  # id(python scope) -> (scope ref, NativeScope, {name: (ptr, shape, dtype, tensor)})
+        self._host_ops = set(native.registered_ops(False))
+        self._dev_ops = set(native.registered_ops(True)) if self.device >= 0 else set()
+
+    # ------------------------------------------------------------------ program
+    def _program(self, program):
+        key = (id(program), program._version)
+        ent = self._progs.get(key)
+        if ent is not None and ent[0] is program:
+            return ent[1], ent[2]
+        block = program.global_block()
+        bad = sorted({op.type for op in block.ops if op.type not in self._host_ops and op.type not in self._dev_ops})
+        if bad:
+            raise NotImplementedError(f"native engine: no C++ kernel for op types {bad}")
+        subs = sorted({op.type for op in block.ops if any(k in op.attrs for k in ("sub_block", "blocks"))})
+        if subs:
+            raise NotImplementedError(f"native engine: control-flow ops with sub-blocks {subs}")
+        prog = native.NativeProgram(data=program.desc.serialize_to_string())
+        pers = [v.name for v in program.list_vars()
+                if v.persistable and v.name not in ("feed", "fetch") and v.type == core.VT.LOD_TENSOR]
+        self._progs[key] = (program, prog, pers)
+        return prog, pers
+
+    def _scope(self, scope):
+        ent = self._scopes.get(id(scope))
+        if ent is None or ent[0] is not scope:
+            ent = (scope, native.NativeScope(), {})
+            self._scopes[id(scope)] = ent
+        return ent[1], ent[2]
+
+    # ------------------------------------------------------------------ tensors
+    def _tdev(self):
+        return torch.device("cuda", self.device) if self.device >= 0 else torch.device("cpu")
+
+    def _lend(self, ns, bound, name, lt):
+        """Lends the torch storage of LoDTensor ``lt`` to the native scope as ``name``."""
+        t = lt._t
+        if t is None:
+            return
+        if t.device != self._tdev() or not t.is_contiguous() or t.dtype not in _TORCH_DT:
+            if t.dtype not in _TORCH_DT:
+                raise NotImplementedError(f"native engine: {name} has dtype {t.dtype}")
+            t = t.to(self._tdev()).contiguous()
+            lt._t = t
+        sig = (t.data_ptr(), tuple(t.shape), t.dtype)
+        if bound.get(name, (None,))[:3] != sig:
+            ns.share(name, t.data_ptr(), _TORCH_DT[t.dtype], tuple(t.shape), self.device)
+            bound[name] = sig + (t,)
+
+    def _feed(self, ns, name, data):
+        if isinstance(data, core.LoDTensor):
+            if data.lod():
+                raise NotImplementedError(f"native engine: LoD feed {name}")
+            data = data._t
+        if isinstance(data, torch.Tensor):
+            data = data.detach().cpu().numpy()
+        ns.set(name, np.ascontiguousarray(np.asarray(data)), self.device)
+
+    def _write_back(self, scope, ns, bound, name):
+        """After a run: a persistable whose native buffer moved is copied into a torch
+        tensor of the Python scope (and lent again, so later runs update it in place)."""
+        info = ns.info(name)
+        if info is None:
+            return
+        dt, shape, ptr, dev = info
+        b = bound.get(name)
+        var = scope.find_var(name) or scope.var(name)
+        lt = var.get_tensor()
+        if b is not None and b[0] == ptr:
+            if tuple(b[1]) != shape and lt._t is not None:
+                lt._t = lt._t.view(shape)
+                bound[name] = (ptr, shape, b[2], lt._t)
+            return
+        if dt not in _DT_TORCH:
+            return
+        t = torch.empty(shape, dtype=_DT_TORCH[dt], device=self._tdev())
+        if t.numel():
+            native.copy(t.data_ptr(), self.device, ptr, dev, t.numel() * t.element_size())
+        lt._t = t
+        self._lend(ns, bound, name, lt)
+
+    # ------------------------------------------------------------------ run
+    def run(self, program, feed, fetch_names, scope, return_numpy=True):
+        prog, pers = self._program(program)
+        ns, bound = self._scope(scope)
+        for name in pers:
+            var = scope.find_var(name)
+            val = var.get() if var is not None else None
+            if isinstance(val, core.LoDTensor):
+                self._lend(ns, bound, name, val)
+        for name, data in feed.items():
+            self._feed(ns, name, data)
+        if self.device >= 0:
+            torch.cuda.current_stream(self._tdev()).synchronize()  # lent tensors written by torch
+        self._exe.run(prog, ns)  # ends with a sync of the native stream
+        for name in pers:
+            self._write_back(scope, ns, bound, name)
+        outs = []
+        for n in fetch_names:
+            a = ns.get(n)
+            outs.append(a if return_numpy else core.LoDTensor(torch.from_numpy(a).to(self._tdev())))
+        return outs
+
+    def host_fallbacks(self):
+        return self._exe.host_fallbacks()

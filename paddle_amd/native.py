@@ -55,6 +55,11 @@ def lib():
             "pa_nat_scope_set": ([_P, ctypes.c_char_p, _I, _I, ctypes.POINTER(_I64), _P, _I], _I),
             "pa_nat_scope_get": ([_P, ctypes.c_char_p, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I64),
                                   _I, ctypes.POINTER(_P), ctypes.POINTER(_SZ)], _I),
+            "pa_nat_scope_share": ([_P, ctypes.c_char_p, _I, _I, ctypes.POINTER(_I64), _P, _I], _I),
+            "pa_nat_scope_info": ([_P, ctypes.c_char_p, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I64),
+                                   _I, ctypes.POINTER(_P), ctypes.POINTER(_I)], _I),
+            "pa_nat_copy": ([_P, _I, _P, _I, _SZ], _I),
+            "pa_nat_executor_fallbacks": ([_P, ctypes.c_char_p, _I], _I),
             "pa_nat_load_persistables": ([_P, _P, ctypes.c_char_p, ctypes.c_char_p, _I], _I),
             "pa_nat_registered_ops": ([ctypes.c_char_p, _I, _I], _I),
             "pa_nat_device_sgemm": ([_P, _I, _I, _I64, _I64, _I64, ctypes.c_float, _P, _I64, _P, _I64,
@@ -168,6 +173,22 @@ class NativeScope:
         buf = (ctypes.c_char * nb.value).from_address(p.value) if nb.value else b""
         return np.frombuffer(bytes(buf), dtype=_DT_TO_NP[t.value]).reshape(shape).copy()
 
+    def share(self, name, ptr, dtype_code, shape, device=-1):
+        """Binds ``name`` to caller-owned memory (``ptr``, e.g. a torch tensor's
+        storage): kernels update it in place, the executor never frees it."""
+        dims = (_I64 * max(1, len(shape)))(*shape)
+        if lib().pa_nat_scope_share(self._h, name.encode(), int(dtype_code), len(shape), dims, ptr, int(device)) != 0:
+            raise RuntimeError(_err())
+
+    def info(self, name):
+        """(dtype code, shape, data pointer, device) of ``name``, or None."""
+        t, nd, p, dev = _I(), _I(), _P(), _I()
+        d = (_I64 * 16)()
+        if not lib().pa_nat_scope_info(self._h, name.encode(), ctypes.byref(t), ctypes.byref(nd), d, 16,
+                                       ctypes.byref(p), ctypes.byref(dev)):
+            return None
+        return t.value, tuple(d[j] for j in range(nd.value)), p.value or 0, dev.value
+
     def load_persistables(self, program: NativeProgram, dirname, combined=None, device=-1):
         if lib().pa_nat_load_persistables(program._h, self._h, _b(dirname), _b(combined), int(device)) != 0:
             raise RuntimeError(_err())
@@ -186,6 +207,24 @@ class NativeExecutor:
     def run(self, program: NativeProgram, scope: NativeScope, block=0):
         if lib().pa_nat_executor_run(self._h, program._h, scope._h, int(block)) != 0:
             raise RuntimeError(f"native executor: {_err()}")
+
+    def host_fallbacks(self):
+        """{op type: count} of ops this device executor ran on host copies."""
+        buf = ctypes.create_string_buffer(1 << 16)
+        n = lib().pa_nat_executor_fallbacks(self._h, buf, len(buf))
+        if n < 0:
+            raise RuntimeError("fallback list does not fit")
+        out = {}
+        for line in buf.value.decode().splitlines():
+            k, v = line.split()
+            out[k] = int(v)
+        return out
+
+
+def copy(dst, dst_dev, src, src_dev, nbytes):
+    """Synchronous copy between host (-1) and device memories."""
+    if lib().pa_nat_copy(dst, int(dst_dev), src, int(src_dev), int(nbytes)) != 0:
+        raise RuntimeError(_err())
 
     def __del__(self):
         if getattr(self, "_h", None) and _lib is not None:

@@ -80,19 +80,13 @@ def conv2d_grad(ctx):
     st, pd, dl, g = (tuple(ctx.attr("strides")), tuple(ctx.attr("paddings")), tuple(ctx.attr("dilations")),
                      ctx.attr("groups") or 1)
     if _cnd.supported_conv(x, w, g) and dy.is_cuda:
-        # the HIP conv's own backward kernels through one eager-engine node
-        xs = _eager.to_tensor_handle(x.detach(), stop_gradient=not ctx.has_output("Input@GRAD"))
-        ws = _eager.to_tensor_handle(w.detach(), stop_gradient=not ctx.has_output("Filter@GRAD"))
-        with _eager.enable_grad():
-            y = _cnd.conv_nd(xs, ws, None, st, pd, dl, g)
-            want = [t for t in (xs, ws) if not t.stop_gradient]
-            grads = _eager.grad([y], want, [dy]) if want else []
-        grads = [_eager._raw(t) for t in (grads if isinstance(grads, list) else [grads])]
-        it = iter(grads)
-        if ctx.has_output("Input@GRAD"):
-            ctx.set_output("Input@GRAD", next(it))
-        if ctx.has_output("Filter@GRAD"):
-            ctx.set_output("Filter@GRAD", next(it))
+        # the HIP conv's dgrad / wgrad kernels directly (no forward recompute)
+        dx, dw = _cnd.conv_grads(x.detach(), w.detach(), dy, st, pd, dl, g, ctx.has_output("Input@GRAD"),
+                                 ctx.has_output("Filter@GRAD"))
+        if dx is not None:
+            ctx.set_output("Input@GRAD", dx)
+        if dw is not None:
+            ctx.set_output("Filter@GRAD", dw)
         if ctx.has_output("Bias@GRAD"):
             ctx.set_output("Bias@GRAD", _cnd._bias_grad(dy.float().contiguous()).to(dy.dtype))
         return

@@ -269,6 +269,23 @@ class _ConvNdFn(torch.autograd.Function):
         return dx, dw, db, None, None, None, None
 
 
+def conv_grads(x, w, dy, stride, padding, dilation, groups, need_x=True, need_w=True):
+    """Explicit conv data / filter gradients from (x, w, dY) -- the Fluid
+    ``conv2d_grad`` op's kernels, with no forward recompute (the column matrix of
+    the wgrad is rebuilt by vol2col).  Returns (dx | None, dw | None) in x / w dtypes."""
+    nd = x.dim() - 2
+    s, p, d = _tup(stride, nd), _tup(padding, nd), _tup(dilation, nd)
+    xf, wf = x.float().contiguous(), w.float().contiguous()
+    dyf = dy.float().contiguous()
+    sp, k = tuple(xf.shape[2:]), tuple(wf.shape[2:])
+    osp = tuple(dyf.shape[2:])
+    geo = _geo(xf.shape[1], _pad3(sp), _pad3(osp), _pad3(k), _pad3(s), _pad3z(p), _pad3(d))
+    G = int(groups)
+    dx = _conv_dgrad(dyf, wf, tuple(xf.shape), geo, G).to(x.dtype) if need_x else None
+    dw = _conv_wgrad(dyf, xf, tuple(wf.shape), geo, G).to(w.dtype) if need_w else None
+    return dx, dw
+
+
 def supported_conv(x, w, groups=1):
     return (_ok(x) and x.dim() in (4, 5) and w.dim() == x.dim() and groups >= 1 and x.shape[1] % groups == 0
             and w.shape[0] % groups == 0 and w.shape[1] * groups == x.shape[1] and x.numel() > 0)

@@ -1,0 +1,54 @@
+"""fluid.Executor(engine="native") on the CPU: the C++ executor (host kernels incl.
+conv2d_grad / pool2d_grad / batch_norm_grad) trains LeNet and a ResNet-tiny along
+the Python executor's trajectory, updating the Python scope's parameters in place.
+
+Reference: framework/executor.cc:125-353, pybind/pybind.cc:507."""
+import numpy as np
+import pytest
+
+import paddle_amd.fluid as fluid
+from native_engine_cases import build, train
+
+
+@pytest.mark.parametrize("model", ["lenet", "resnet_tiny"])
+def test_native_engine_matches_python_trajectory_cpu(model):
+    place = fluid.CPUPlace()
+    ref, ref_p, init, _ = train(model, place, "python", steps=5)
+    got, got_p, _, _ = train(model, place, "native", steps=5, init=init)
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
+    for k in ref_p:
+        np.testing.assert_allclose(got_p[k], ref_p[k], rtol=1e-4, atol=1e-5, err_msg=k)
+    assert got[-1] < got[0]
+
+
+def test_native_engine_updates_python_scope_in_place():
+    """Parameters are lent (zero-copy) to the native scope: after a native step the
+    Python scope's tensor object holds the updated values."""
+    main, startup, loss = build("lenet")
+    place = fluid.CPUPlace()
+    scope = fluid.core.Scope()
+    with fluid.executor.scope_guard(scope):
+        fluid.Executor(place).run(startup)
+        w = main.global_block().all_parameters()[0].name
+        t_before = scope.find_var(w).get_tensor()._t
+        v0 = t_before.clone()
+        exe = fluid.Executor(place, engine="native")
+        rs = np.random.RandomState(0)
+        exe.run(main, feed={"img": rs.randn(4, 1, 16, 16).astype("float32"),
+                            "label": rs.randint(0, 10, (4, 1)).astype("int64")}, fetch_list=[loss])
+        t_after = scope.find_var(w).get_tensor()._t
+        assert t_after.data_ptr() == t_before.data_ptr()
+        assert not np.allclose(t_after.numpy(), v0.numpy())
+
+
+def test_native_engine_rejects_unsupported_programs():
+    main, startup = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, startup):
+        x = fluid.layers.data("x", [4])
+        y = fluid.layers.sequence_softmax(fluid.layers.fc(x, 1))
+    exe = fluid.Executor(fluid.CPUPlace(), engine="native")
+    scope = fluid.core.Scope()
+    with fluid.executor.scope_guard(scope):
+        fluid.Executor(fluid.CPUPlace()).run(startup)
+        with pytest.raises(NotImplementedError, match="sequence_softmax"):
+            exe.run(main, feed={"x": np.zeros((2, 4), "float32")}, fetch_list=[y])
