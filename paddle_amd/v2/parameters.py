@@ -1,9 +1,12 @@
 """v2 parameters (reference v2/parameters.py): a name -> ndarray view of the v2
 session's scope, with the v2 tar format -- one member per parameter holding a
 16-byte header (uint32 version 0, uint32 value size 4, uint64 element count) and
-the raw float32 values, plus ``<name>.protobuf`` describing it.  (The reference
-stores a binary ParameterConfig proto there; this facade writes its text form
-``name: ... dims: ...``, which ``from_tar`` reads back for the shape.)"""
+the raw float32 values, plus ``<name>.protobuf`` holding the parameter's binary
+``ParameterConfig`` message (reference proto/ParameterConfig.proto:34-83; written
+at reference v2/parameters.py:350, read at :378).  The proto2 wire format is
+encoded and decoded here directly (no generated protobuf module): ``name`` (1),
+``size`` (2) and the repeated ``dims`` (9, packed or not) are interpreted, every
+other field is skipped by its wire type."""
 from __future__ import annotations
 
 import io
@@ -14,6 +17,81 @@ import numpy as np
 
 from .. import fluid
 from ._core import STATE, executor
+
+
+def _varint(v: int) -> bytes:
+    out = bytearray()
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        if not v:
+            out.append(b)
+            return bytes(out)
+        out.append(b | 0x80)
+
+
+def encode_parameter_config(name: str, dims) -> bytes:
+    """ParameterConfig{name, size, dims} in proto2 wire format (dims unpacked, the
+    proto2 default for ``repeated uint64``)."""
+    nb = name.encode()
+    size = 1
+    for d in dims:
+        size *= int(d)
+    out = bytearray(b"\x0a" + _varint(len(nb)) + nb)  # field 1, length-delimited
+    out += b"\x10" + _varint(size)  # field 2, varint
+    for d in dims:
+        out += b"\x48" + _varint(int(d))  # field 9, varint
+    return bytes(out)
+
+
+def _read_varint(buf: bytes, pos: int, end: int):
+    v = shift = 0
+    while True:
+        if pos >= end or shift > 63:
+            raise ValueError("ParameterConfig: truncated varint")
+        b = buf[pos]
+        pos += 1
+        v |= (b & 0x7F) << shift
+        if not b & 0x80:
+            return v, pos
+        shift += 7
+
+
+def decode_parameter_config(buf: bytes) -> dict:
+    """Parse a binary ParameterConfig into {"name", "size", "dims"}; raises
+    ValueError on a truncated or malformed message."""
+    pos, n = 0, len(buf)
+    out = {"name": None, "size": None, "dims": []}
+    while pos < n:
+        key, pos = _read_varint(buf, pos, n)
+        field, wt = key >> 3, key & 7
+        if wt == 0:
+            v, pos = _read_varint(buf, pos, n)
+            if field == 2:
+                out["size"] = v
+            elif field == 9:
+                out["dims"].append(v)
+        elif wt == 2:
+            ln, pos = _read_varint(buf, pos, n)
+            if pos + ln > n:
+                raise ValueError("ParameterConfig: truncated field")
+            if field == 1:
+                out["name"] = bytes(buf[pos:pos + ln]).decode()
+            elif field == 9:  # packed dims
+                sp = pos
+                while sp < pos + ln:
+                    v, sp = _read_varint(buf, sp, pos + ln)
+                    out["dims"].append(v)
+            pos += ln
+        elif wt in (1, 5):
+            pos += 8 if wt == 1 else 4
+            if pos > n:
+                raise ValueError("ParameterConfig: truncated fixed field")
+        else:
+            raise ValueError(f"ParameterConfig: unsupported wire type {wt}")
+    if out["name"] is None or out["size"] is None:
+        raise ValueError("ParameterConfig: missing required name / size")
+    return out
 
 
 def _param_names():
@@ -107,8 +185,7 @@ class Parameters:
             info.size = buf.tell()
             buf.seek(0)
             tar.addfile(info, buf)
-            conf = f"name: \"{name}\"\n" + "".join(f"dims: {d}\n" for d in self.get_shape(name))
-            cb = conf.encode()
+            cb = encode_parameter_config(name, self.get_shape(name))
             ci = tarfile.TarInfo(name=name + ".protobuf")
             ci.size = len(cb)
             tar.addfile(ci, io.BytesIO(cb))
@@ -121,9 +198,8 @@ class Parameters:
         shapes = {}
         for m in tar.getmembers():
             if m.name.endswith(".protobuf"):
-                txt = tar.extractfile(m).read().decode()
-                shapes[m.name[: -len(".protobuf")]] = tuple(int(line.split(":")[1]) for line in txt.splitlines()
-                                                             if line.startswith("dims:"))
+                conf = decode_parameter_config(tar.extractfile(m).read())
+                shapes[m.name[: -len(".protobuf")]] = tuple(conf["dims"]) or (conf["size"],)
         for m in tar.getmembers():
             if not m.name.endswith(".protobuf"):
                 buf = tar.extractfile(m)
