@@ -39,6 +39,23 @@ def _install_allocator():
         warnings.warn(f"paddle_amd: buddy allocator not installed ({e}); using torch's caching allocator")
 
 
+def _install_device_tracer():
+    """FLAGS_device_tracer=1 (or PADDLE_AMD_DEVICE_TRACER=1): register the
+    rocprofiler-sdk kernel tracer (utils/device_tracer.py) now, before anything
+    initialises the HIP runtime."""
+    import os
+
+    on = os.environ.get("PADDLE_AMD_DEVICE_TRACER", os.environ.get("FLAGS_device_tracer", "0"))
+    if on.lower() in ("1", "true", "yes"):
+        from .utils import device_tracer
+
+        if not device_tracer.install():
+            import warnings
+
+            warnings.warn(f"paddle_amd: device tracer not installed ({device_tracer.error()})")
+
+
+_install_device_tracer()
 _install_allocator()
 
 from . import ops  # noqa: E402,F401

@@ -35,6 +35,7 @@ KERNEL_LIB = os.path.join(LIBDIR, "libpaddle_amd_kernels.so")
 RUNTIME_LIB = os.path.join(LIBDIR, "libpaddle_amd_runtime.so")
 NATIVE_LIB = os.path.join(LIBDIR, "libpaddle_amd_native.so")
 NATIVE_INC = os.path.join(ROOT, "csrc", "native")
+TRACER_LIB = os.path.join(LIBDIR, "libpaddle_amd_tracer.so")
 
 
 def _hipcc() -> str:
@@ -195,12 +196,28 @@ def build_native_program(src: str, out: str, extra: list[str] | None = None) -> 
     return out
 
 
+def build_tracer(verbose: bool = False) -> str:
+    """The in-process kernel activity tracer (``csrc/tracer``): a rocprofiler-sdk
+    tool library (host C++ only, linked against librocprofiler-sdk)."""
+    srcs = sorted(glob.glob(os.path.join(ROOT, "csrc", "tracer", "*.cc")))
+    if not srcs or not os.path.exists("/opt/rocm/include/rocprofiler-sdk/rocprofiler.h"):
+        return ""
+    cxx = shutil.which("g++") or "c++"
+    cflags = ["-O2", "-fPIC", "-std=c++17", "-fvisibility=hidden", "-Wall", "-pthread",
+              "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]
+    ldflags = ["-pthread", "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lrocprofiler-sdk"]
+    return _build_lib(srcs, [], TRACER_LIB, cxx, cflags, ldflags, verbose, 1)
+
+
 def build_all(verbose: bool = False) -> list[str]:
     out = [build_kernels(verbose)]
     rt = build_runtime(verbose)
     if rt:
         out.append(rt)
     out.append(build_native(verbose))
+    tr = build_tracer(verbose)
+    if tr:
+        out.append(tr)
     return out
 
 

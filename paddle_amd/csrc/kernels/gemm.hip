@@ -43,6 +43,7 @@ constexpr int LDS_BYTES = STAGE + 128 * 528;  // 2 stages (128 KiB); C staging a
 constexpr unsigned OOB = 0xFFFFFFF0u; // voffset beyond num_records -> DMA writes zeros
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 struct Params {
@@ -79,6 +80,7 @@ struct Params {
   // Source pixel: ny = oy*sy - py + kh*dy; with a zero-insertion factor 2^uy
   // (dgrad of a stride-2^uy conv) only ny % 2^uy == 0 hits, at row ny >> uy.
   int H, W, Cc, OH, OW, KW, sy, sx, py, px, dy, dx, uy, ux;
+  int stagger;  // persistent grids: block slot (bid / 8) % 8 idles slot * stagger * ~0.5 us first
 };
 
 // LDS image of one operand of one stage: 4 "slabs" of 64 mn x 64 k (8 KiB each);
@@ -399,6 +401,13 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   };
   set_group(bz);
   if (Mb <= 0 || vb0 >= nwg) return;  // wave-uniform: nothing for this block
+  // start-time stagger (experiment knob, 0 = off): blocks of a persistent grid run
+  // identical tile sequences in lockstep, so every CU's epilogue hits HBM at once;
+  // offsetting their starts spreads those bursts
+  if (p.stagger > 0) {
+    const int slot = (blockIdx.x >> 3) & 7;
+    for (int i = 0; i < slot * p.stagger; ++i) __builtin_amdgcn_s_sleep(16);
+  }
   // ---- persistent tiles: virtual block vb = blockIdx.x + i * gridDim.x; XCD remap
   // (gridDim.x is a multiple of 8 or covers every tile, so a block keeps its XCD
   // group), then bands of 8 tile-rows for L2 reuse
@@ -726,6 +735,29 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   constexpr int PASSES = OUTF32 ? 4 : 2;
   constexpr int PI = 8 / PASSES;           // 16-row m-tiles per group per pass
   constexpr int GR = 16 * PI;              // staged rows per group per pass
+  constexpr int CPR = OUTF32 ? 64 : 32;  // 16-B chunks per 256-wide row
+  constexpr int RPI = NT / CPR;          // rows per iteration
+  constexpr int NIT = 2 * GR / RPI;      // store iterations per pass
+  const bool acc_rd = p.accumulate && !(OUTF32 && p.atomic);
+  // C descriptor based at this tile's first element (host: 256 rows of ldc fit in
+  // 32-bit offsets).  Store iteration `it` of pass `ps` covers tile row
+  // crow(it, ps) + tid / CPR (a compile-time row plus a lane row) and 16-B chunk
+  // tid % CPR; its byte offset is c_base + crow * row_bytes, or OOB (load 0 /
+  // store dropped) past M or N.  All scalars but c_base and the row test.
+  constexpr int ESZ = OUTF32 ? 4 : 2;
+  const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc(
+      (char*)p.C + (cz + (erow0 + m0) * p.ldc + n0) * ESZ, 0, (int)OOB, 0x00020000);
+  const unsigned row_bytes = (unsigned)p.ldc * ESZ;
+  const int c_row = tid / CPR;
+  const int rows_left = eMb - m0;  // rows of this tile inside M
+  const bool c_colok = n0 + (tid % CPR) * (OUTF32 ? 4 : 8) < p.N;
+  const unsigned c_base = (unsigned)c_row * row_bytes + (unsigned)((tid % CPR) * 16);
+#define C_OFF(it, ps)                                                                          \
+  ({                                                                                           \
+    const int rr0_ = (it) * RPI;                                                           \
+    const int crow_ = (rr0_ < GR ? rr0_ : 128 + rr0_ - GR) + GR * (ps);                    \
+    (c_colok && c_row + crow_ < rows_left) ? c_base + (unsigned)crow_ * row_bytes : OOB;       \
+  })
 #pragma unroll
   for (int ps = 0; ps < PASSES; ++ps) {
     // (a) fragments -> LDS (staged row = GR * wr + 16 * ii + ml)
@@ -769,36 +801,46 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
       __syncthreads();
       continue;
     }
-    // (b) LDS rows -> global, 16 B per lane, consecutive lanes along a row
-    constexpr int CPR = OUTF32 ? 64 : 32;  // 16-B chunks per 256-wide row
-    constexpr int RPI = NT / CPR;          // rows per iteration
-#pragma unroll 2
-    for (int it = 0; it < 2 * GR / RPI; ++it) {
-      const int rr = it * RPI + tid / CPR, ch = tid % CPR;
-      const int m = m0 + 128 * (rr / GR) + GR * ps + rr % GR;
-      const int n = n0 + ch * (OUTF32 ? 4 : 8);
-      const f32x4 v = *reinterpret_cast<const f32x4*>(stg + rr * ROWB + ch * 16);
-      if (m < eMb && n < p.N) {
-        char* g = (char*)p.C + (cz + (erow0 + m) * p.ldc + n) * (OUTF32 ? 4 : 2);
-        if (OUTF32) {
-          f32x4 o = v;
-          if (p.accumulate) o += *reinterpret_cast<const f32x4*>(g);
-          *reinterpret_cast<f32x4*>(g) = o;
-        } else if (p.accumulate) {
-          const u16x8 o = *reinterpret_cast<const u16x8*>(g);
-          const u16x8 c = __builtin_bit_cast(u16x8, v);
-          u16x8 w;
+    // (b) LDS rows -> global, 16 B per lane, consecutive lanes along a row, in
+    // halves of HB iterations.  C += : a half's old C values are loaded together
+    // before its stores, so a pass costs two load round trips, not one per store
+    // (vmcnt retires in issue order: a load issued after a store waits for it).
+    // Loads and stores are buffer ops on the per-tile descriptor with masked lanes
+    // sent out of range (load 0 / store dropped): uniform control flow, so hipcc
+    // counts its vmcnt waits instead of falling back to vmcnt(0) at every store.
+    constexpr int HB = F8 ? 2 : NIT / 2;  // F8 epilogues also hold the column scales
+#pragma unroll 1
+    for (int h = 0; h < NIT; h += HB) {
+      u32x4 cold[HB];
+      if (acc_rd) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) w[e] = f2bf(bf2f(c[e]) + bf2f(o[e]));
-          *reinterpret_cast<u16x8*>(g) = w;
-        } else {
-          *reinterpret_cast<f32x4*>(g) = v;
+        for (int u = 0; u < HB; ++u) cold[u] = __builtin_amdgcn_raw_buffer_load_b128(rsC, C_OFF(h + u, ps), 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < HB; ++u) {
+        const int it = h + u;
+        const int rr = it * RPI + tid / CPR, ch = tid % CPR;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(stg + rr * ROWB + ch * 16);
+        u32x4 w = __builtin_bit_cast(u32x4, v);
+        if (acc_rd) {
+          if constexpr (OUTF32) {
+            w = __builtin_bit_cast(u32x4, v + __builtin_bit_cast(f32x4, cold[u]));
+          } else {
+            const u16x8 o = __builtin_bit_cast(u16x8, cold[u]);
+            const u16x8 c = __builtin_bit_cast(u16x8, v);
+            u16x8 r;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) r[e] = f2bf(bf2f(c[e]) + bf2f(o[e]));
+            w = __builtin_bit_cast(u32x4, r);
+          }
         }
+        __builtin_amdgcn_raw_buffer_store_b128(w, rsC, C_OFF(it, ps), 0, 0);
       }
     }
     __syncthreads();  // staging reads done (next pass / next tile's DMA into stage 1)
   }
   }
+#undef C_OFF
   if (!has_next) break;
   vb = vb_next;
   m0 = m0n;
@@ -812,6 +854,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
 
 static int g_sched = -1;      // -1: per-layout default; 0 / 1: force PF_IN_CLUSTER (A/B runs)
 static int g_persistent = 1;  // 0: one tile per block (grid = tiles), for A/B runs
+static int g_stagger = 0;     // start stagger units per block slot (experiment)
 
 template <bool AK, bool BK, bool F32, bool PF, bool KFULL, bool GA = false, bool F8 = false, int GM = 0>
 static int launch_v(const Params& p, int batch, hipStream_t st) {
@@ -833,8 +876,10 @@ static int launch_v(const Params& p, int batch, hipStream_t st) {
   // persistent: one resident block per CU; grouped rows: one block per tile of the
   // flat schedule (tiles_m bounds the groups' tile rows), a single grid row
   const int grid = (GM == 1 || nwg < ncu || !g_persistent) ? nwg : ncu;
+  Params pp = p;
+  pp.stagger = grid == ncu ? g_stagger : 0;
   hipLaunchKernelGGL((gemm_kernel<AK, BK, F32, PF, KFULL, GA, F8, GM>), dim3(grid, GM == 1 ? 1 : batch), dim3(NT),
-                     LDS_BYTES, st, p);
+                     LDS_BYTES, st, pp);
   return (int)hipGetLastError();
 }
 
@@ -950,6 +995,7 @@ PA_EXPORT int pa_group_tile_table(int* grp, int G, long total_rows, hipStream_t 
 
 PA_EXPORT void pa_gemm_set_sched(int s) { gemm::g_sched = s; }
 PA_EXPORT void pa_gemm_set_persistent(int s) { gemm::g_persistent = s; }
+PA_EXPORT void pa_gemm_set_stagger(int s) { gemm::g_stagger = s; }
 
 // Returns 0 on success, a hipError on launch failure, -1 for an unsupported shape
 // (the caller checks shapes first: N a multiple of 8, K a multiple of 8 when an
@@ -983,6 +1029,7 @@ PA_EXPORT int pa_gemm(int a_kmaj, int b_kmaj, int out_f32, const void* A, const 
   p.grp_tiles = grp ? grp + batch + 1 : nullptr;  // grp_mode 1: table after the offsets
   if (p.atomic && bias) return -1;
   if (K <= 0) return -1;
+  if ((long)ldc * gemm::BM * (out_f32 ? 4 : 2) >= (long)gemm::OOB) return -1;  // per-tile C offsets are 32-bit
 #define PA_G(AK, BK, F)                                                \
   if (a_kmaj == AK && b_kmaj == BK && out_f32 == F) return gemm::launch<AK, BK, F>(p, batch, st);
   PA_G(1, 1, 0) PA_G(1, 0, 0) PA_G(0, 1, 0) PA_G(0, 0, 0)

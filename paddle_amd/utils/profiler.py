@@ -5,6 +5,11 @@
   includes the GPU (the reference used cudaEvent + CUPTI; on MI355X kernel-level
   activity comes from rocprofv3, and these ranges are also emitted as roctx
   markers when ``roctx`` is importable so rocprof traces show framework ops).
+* with the rocprofiler-sdk kernel tracer installed (``utils/device_tracer.py``,
+  ``FLAGS_device_tracer=1``; the reference's CUPTI DeviceTracer), every kernel the
+  process dispatches inside the profiling window is recorded in-process with its
+  device start/end time and the innermost enclosing RecordEvent, and the GPU
+  track of the profile is those kernels;
 * per-thread event lists are kept by the native runtime library
   (``csrc/runtime/profiler.cc``) when it is built, else in Python;
 * ``stop(sorted_key, path)`` prints the summary table (calls/total/min/max/ave,
@@ -20,7 +25,8 @@ from collections import defaultdict
 
 import torch
 
-_state = {"enabled": False, "gpu": False, "events": [], "t0": 0.0, "base": None}
+_state = {"enabled": False, "gpu": False, "events": [], "t0": 0.0, "base": None, "tracer": False,
+          "ranges": {}, "next_range": 1}
 _lock = threading.Lock()
 _tls = threading.local()
 
@@ -29,15 +35,28 @@ def is_enabled():
     return _state["enabled"]
 
 
+def _tracer():
+    from . import device_tracer
+
+    return device_tracer
+
+
 class RecordEvent:
-    __slots__ = ("name", "t", "ev0", "ev1")
+    __slots__ = ("name", "t", "ev0", "ev1", "rid")
 
     def __init__(self, name):
         self.name = name
+        self.rid = 0
 
     def __enter__(self):
         if not _state["enabled"]:
             return self
+        if _state["tracer"]:
+            with _lock:
+                self.rid = _state["next_range"]
+                _state["next_range"] += 1
+                _state["ranges"][self.rid] = self.name
+            _tracer().push_range(self.rid)
         self.t = time.perf_counter()
         if _state["gpu"]:
             self.ev0 = torch.cuda.Event(enable_timing=True)
@@ -48,6 +67,8 @@ class RecordEvent:
         if not _state["enabled"]:
             return False
         t1 = time.perf_counter()
+        if self.rid:
+            _tracer().pop_range()
         ev1 = None
         if _state["gpu"]:
             ev1 = torch.cuda.Event(enable_timing=True)
@@ -68,6 +89,18 @@ def start(state="All"):
     _state["gpu"] = state in ("GPU", "All") and torch.cuda.is_available()
     _state["events"] = []
     _state["t0"] = time.perf_counter()
+    _state["tracer"] = False
+    if state in ("GPU", "All"):
+        try:
+            dt = _tracer()
+            if dt.available():
+                dt.clear()
+                _state["ranges"], _state["next_range"] = {}, 1
+                _state["tracer_t0"] = (time.perf_counter(), dt.now_ns())
+                dt.enable()
+                _state["tracer"] = True
+        except (OSError, RuntimeError):
+            _state["tracer"] = False
     if _state["gpu"]:
         # device time origin: every range's HIP events are placed relative to it, so
         # the GPU track of the timeline is an in-process device activity trace
@@ -81,6 +114,25 @@ def start(state="All"):
 def reset():
     with _lock:
         _state["events"] = []
+
+
+def kernel_records():
+    """The in-process kernel records of the window (empty without the tracer)."""
+    if not _state.get("tracer_used"):
+        return []
+    recs = _tracer().records()
+    for r in recs:
+        r["op"] = _state["ranges"].get(r["range"], "")
+    return recs
+
+
+def _stop_tracer():
+    if _state["tracer"]:
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        _tracer().disable()
+        _state["tracer"] = False
+        _state["tracer_used"] = True
 
 
 def _gather():
@@ -114,7 +166,18 @@ def profile_dict():
     t0 = _state["t0"]
     ev = [{"name": n, "type": "CPU", "device_id": 0, "sub_device_id": tid % 1000000,
            "start_ns": int((a - t0) * 1e9), "end_ns": int((b - t0) * 1e9)} for n, tid, a, b, _ in _gather()]
-    if _state["gpu"]:
+    _stop_tracer()
+    krecs = kernel_records()
+    if krecs:
+        # kernels on the host clock: rocprofiler ns mapped through the (perf_counter,
+        # rocprofiler ns) pair taken at start(); one sub-track per HIP queue
+        h0, d0 = _state["tracer_t0"]
+        qs = {q: i for i, q in enumerate(sorted({r["queue"] for r in krecs}))}
+        ev += [{"name": r["name"], "type": "GPUKernel", "device_id": max(r["device"], 0),
+                "sub_device_id": qs[r["queue"]], "op": r["op"],
+                "start_ns": int((h0 - t0) * 1e9) + r["start_ns"] - d0,
+                "end_ns": int((h0 - t0) * 1e9) + r["end_ns"] - d0} for r in krecs]
+    elif _state["gpu"]:
         off = (_state["base_host"] - t0) * 1e3
         dev = torch.cuda.current_device()
         ev += [{"name": n, "type": "GPUKernel", "device_id": dev, "sub_device_id": 0,
@@ -146,6 +209,7 @@ def summary(sorted_key=None):
 def stop(sorted_key=None, profile_path="/tmp/profile"):
     if not _state["enabled"]:
         return None
+    _stop_tracer()
     text, items = summary(sorted_key)
     print(text)
     if profile_path:
@@ -177,5 +241,5 @@ def chrome_trace(profiles):
                             "args": {"name": f"{k}:{kind}:{e['device_id']}"}})
             out.append({"name": e["name"], "cat": "Op", "ph": "X", "pid": pids[key], "tid": e["sub_device_id"],
                         "ts": e["start_ns"] / 1e3, "dur": (e["end_ns"] - e["start_ns"]) / 1e3,
-                        "args": {"name": e["name"]}})
+                        "args": {"name": e["name"], **({"op": e["op"]} if e.get("op") else {})}})
     return json.dumps({"traceEvents": out, "displayTimeUnit": "ns"})

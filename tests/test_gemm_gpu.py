@@ -108,3 +108,25 @@ def test_gemm_splitk(M, N, K, a_kmaj, b_kmaj):
     G.gemm_splitk(a, b, M, N, K, a_kmaj=a_kmaj, b_kmaj=b_kmaj, out=out, accumulate=True)
     ref = 0.5 + af @ bf.t()
     assert torch.allclose(out, ref, atol=3e-3 * K ** 0.5, rtol=1e-4), (out - ref).abs().max()
+
+
+@pytest.mark.parametrize("out_f32", [True, False])
+@pytest.mark.parametrize("M,N,K", [(264, 136, 72), (520, 1032, 4104)])
+def test_gemm_accumulate_into_strided_output(M, N, K, out_f32):
+    """C += A B^T into a column window of a wider matrix (ldc > N): the epilogue's
+    per-tile C descriptor, its out-of-range lanes (rows past M, chunks past N) and
+    the bf16 read-modify-write; the columns outside the window stay untouched."""
+    from paddle_amd.ops import gemm as G
+
+    gen = torch.Generator(device="cuda").manual_seed(M + N + K)
+    a, af = _operand(M, K, True, gen)
+    b, bf = _operand(N, K, False, gen)
+    dt = torch.float32 if out_f32 else torch.bfloat16
+    big = torch.randn(M, N + 40, generator=gen, device="cuda").to(dt)
+    before = big.clone()
+    win = big[:, 16:16 + N]
+    G.gemm(a, b, M, N, K, a_kmaj=True, b_kmaj=False, out=win, accumulate=True)
+    ref = before[:, 16:16 + N].float() + af @ bf.t()
+    tol = (2e-3 * K ** 0.5) if out_f32 else 2e-2 * ref.abs().max().item()
+    assert (big[:, 16:16 + N].float() - ref).abs().max().item() <= tol
+    assert torch.equal(big[:, :16], before[:, :16]) and torch.equal(big[:, 16 + N:], before[:, 16 + N:])
