@@ -7,9 +7,12 @@ gating op" in the reference).  API follows Paddle's ``incubate.distributed.model
 MI355X design:
   * routing = one [T, E] gate GEMM + softmax + top-k on device; tokens are sorted by
     destination expert with a single stable argsort (no Python loops over tokens);
-  * dispatch / combine are ``all_to_all_single`` with exact (uneven) split sizes --
-    no capacity padding on the wire unless a capacity factor is set, in which case
-    overflow tokens are dropped before the exchange (GShard semantics);
+  * without a capacity factor, dispatch / combine are ``all_to_all_single`` with
+    exact (uneven) split sizes (one host read of the split sizes per layer);
+  * with a capacity factor (GShard semantics: overflow slots dropped), tokens are
+    laid out in fixed [expert, capacity] slabs and exchanged with EQUAL splits, so
+    the whole layer -- routing, dispatch, exchange, grouped expert GEMMs, combine --
+    runs without a single device->host sync (``sync_free=True``, the default);
   * experts on a rank run back to back on contiguous token slices; the EP group is
     meant to be the node's 8 GPUs (xGMI all-to-all is 7 concurrent P2P links).
 """
@@ -45,6 +48,23 @@ def all_to_all(x, in_splits, out_splits, group):
     return _tape.apply(_AllToAll, x, in_splits, out_splits, group)
 
 
+class _PeerExpertSwap(torch.autograd.Function):
+    """[a, b, C, H] -> [b, a, C, H] row blocks (peer-major <-> expert-major)."""
+
+    @staticmethod
+    def forward(ctx, x, a, b):
+        ctx.a, ctx.b = a, b
+        return x.reshape(a, b, -1, x.shape[-1]).transpose(0, 1).reshape(-1, x.shape[-1]).contiguous()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.reshape(ctx.b, ctx.a, -1, g.shape[-1]).transpose(0, 1).reshape(-1, g.shape[-1]).contiguous(), None, None
+
+
+def _swap(x, a, b):
+    return x if a == 1 or b == 1 else _tape.apply(_PeerExpertSwap, x, a, b)
+
+
 class TopKGate(Layer):
     def __init__(self, d_model, num_experts, top_k=2, gate_type="gshard", capacity_factor=None, dtype="float32"):
         super().__init__("moe_gate", dtype)
@@ -70,7 +90,7 @@ class MoELayer(Layer):
     ep_world``); global expert ``e`` lives on rank ``e // len(experts)``."""
 
     def __init__(self, d_model, experts, gate=None, top_k=2, group=None, capacity_factor=None,
-                 gate_type="gshard"):
+                 gate_type="gshard", sync_free=True):
         super().__init__("moe_layer")
         self.group = group
         self.ep = comm.get_world_size(group)
@@ -84,6 +104,7 @@ class MoELayer(Layer):
         self.gate = gate or TopKGate(d_model, self.num_experts, top_k, gate_type, capacity_factor)
         self.top_k = self.gate.top_k
         self.capacity_factor = capacity_factor
+        self.sync_free = sync_free
         self.l_aux = None
 
     def forward(self, x):
@@ -93,6 +114,8 @@ class MoELayer(Layer):
         val, idx, self.l_aux = self.gate(x)
         flat_e = idx.reshape(-1)                       # [T*k] expert of each (token, slot)
         flat_w = val.reshape(-1)
+        if self.capacity_factor is not None and self.sync_free:
+            return self._forward_capacity(x, flat_e, flat_w, T, k, E).reshape(shape)
         keep = None
         if self.capacity_factor is not None:
             cap = max(1, int(self.capacity_factor * T * k / E))
@@ -142,3 +165,30 @@ class MoELayer(Layer):
             y_sorted = torch.cat([self.experts[e](parts[e]) if parts[e].shape[0] else parts[e]
                                   for e in range(E)])
         return _route.combine(y_sorted, flat_w, pos, k).reshape(shape)
+
+    def _forward_capacity(self, x, flat_e, flat_w, T, k, E):
+        """Fixed-capacity EP layer with no host sync: send [E * cap] rows (global
+        expert-major, so peer p's block is its n_local experts' slabs), equal-split
+        all-to-all, experts on [n_local, ep * cap] padded rows (one grouped GEMM
+        chain; padding rows are computed and never combined), equal-split return."""
+        cap = max(1, int(self.capacity_factor * T * k / E))
+        src, pos = _route.capacity_routing(flat_e, T, k, E, cap)
+        send = _route.dispatch(x, src, pos, k)             # [E * cap, H]
+        nl, ep = self.n_local, self.ep
+        if ep > 1:
+            splits = [nl * cap] * ep
+            recv = all_to_all(send, splits, splits, self.group)  # [ep, nl, cap, H] from each peer
+            xe = _swap(recv, ep, nl)                         # [nl, ep, cap, H] expert-major
+        else:
+            xe = send
+        rows = ep * cap
+        if self.grouped:
+            ye = self.experts.forward_grouped(xe, [rows] * nl)
+        else:
+            ye = torch.cat([self.experts[e](xe[e * rows:(e + 1) * rows]) for e in range(nl)])
+        if ep > 1:
+            back = _swap(ye, nl, ep)                          # [ep, nl, cap, H] per destination peer
+            ys = all_to_all(back, splits, splits, self.group)
+        else:
+            ys = ye
+        return _route.combine(ys, flat_w, pos, k, padded=True)

@@ -61,14 +61,14 @@ class _DispatchFn(torch.autograd.Function):
 
 class _CombineFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ys, w, pos, k):
+    def forward(ctx, ys, w, pos, k, padded=False):
         ys = _c(ys)
         w = _c(w.float())
         T, H = pos.numel() // k, ys.shape[1]
         y = torch.empty(T, H, dtype=ys.dtype, device=ys.device)
         N.call("pa_moe_reduce", N.ptr(ys), N.ptr(pos), N.ptr(w), N.ptr(y), T, k, H, N.stream())
         ctx.save_for_backward(ys, w, pos)
-        ctx.k = k
+        ctx.k, ctx.padded = k, padded
         return y
 
     @staticmethod
@@ -77,11 +77,12 @@ class _CombineFn(torch.autograd.Function):
         dy = _c(dy)
         k, H = ctx.k, ys.shape[1]
         T = pos.numel() // k
-        dys = torch.empty_like(ys)
+        # padded (capacity) layouts have rows no slot references: their gradient is 0
+        dys = torch.zeros_like(ys) if ctx.padded else torch.empty_like(ys)
         dw = torch.empty(T * k, dtype=torch.float32, device=dy.device)
         N.call("pa_moe_combine_bwd", N.ptr(dy), N.ptr(ys), N.ptr(pos), N.ptr(w), N.ptr(dys), N.ptr(dw), T, k, H,
                N.stream())
-        return dys, dw, None, None
+        return dys, dw, None, None, None
 
 
 def dispatch(x, src, pos, k):
@@ -91,10 +92,33 @@ def dispatch(x, src, pos, k):
     return x[src.long()]
 
 
-def combine(ys, w, pos, k):
-    """ys [R, H] (sorted order), w [T*k] gate weights -> y [T, H]."""
+def capacity_routing(flat_e, T, k, E, cap):
+    """Fixed-capacity (GShard) layout, no host sync: slot s of expert e = flat_e[s]
+    goes to row e * cap + (its rank among e's slots, in slot order) when that rank
+    is below ``cap``, else it is dropped (pos = -1).  -> (src [E*cap] int32: token of
+    each row, 0 for padding rows; pos [T*k] int32).  Kept slots match ``routing``
+    with keep = rank < cap, in the same within-expert order."""
+    dev = flat_e.device
+    order = torch.argsort(flat_e, stable=True)
+    se = flat_e[order]
+    first = torch.searchsorted(se, se, right=False)
+    rank_sorted = torch.arange(se.numel(), device=dev) - first
+    rank = torch.empty_like(rank_sorted)
+    rank[order] = rank_sorted
+    keep = rank < cap
+    row = flat_e * cap + rank
+    pos = torch.where(keep, row, torch.full_like(row, -1)).to(torch.int32)
+    src = torch.zeros(E * cap, dtype=torch.int32, device=dev)
+    slots = torch.arange(T * k, device=dev)
+    src.index_put_((row[keep],), torch.div(slots[keep], k, rounding_mode="floor").to(torch.int32))
+    return src, pos
+
+
+def combine(ys, w, pos, k, padded=False):
+    """ys [R, H] (sorted order), w [T*k] gate weights -> y [T, H].  ``padded``: some
+    rows of ys are referenced by no slot (capacity layout; their gradient is 0)."""
     if _native_ok(ys):
-        return _tape.apply(_CombineFn, ys, w, pos, k)
+        return _tape.apply(_CombineFn, ys, w, pos, k, padded)
     T = pos.numel() // k
     keep = pos >= 0
     slots = keep.nonzero().squeeze(-1)

@@ -125,7 +125,7 @@ def _experts(n, d, seed):
     return out
 
 
-def _moe_worker(rank, world, cap):
+def _moe_worker(rank, world, cap, sync_free=True):
     from paddle_amd.distributed.fleet import MoELayer, TopKGate
 
     d, E, T = 16, 4, 24
@@ -149,12 +149,12 @@ def _moe_worker(rank, world, cap):
     gate.weight.data.copy_(gate_w)
     allex = _experts(E, d, 7)
     moe = MoELayer(d, allex[rank * n_local:(rank + 1) * n_local], gate=gate, group=None if world == 1 else
-                   torch.distributed.group.WORLD, capacity_factor=cap)
+                   torch.distributed.group.WORLD, capacity_factor=cap, sync_free=sync_free)
     x = xs[rank].clone().requires_grad_()
     y = moe(x)
     y.pow(2).sum().backward()
     if y_ref is None:
-        return None
+        return y.detach(), x.grad.detach(), [p.grad.detach().clone() for p in moe.parameters()]
     return (y.detach() - y_ref).abs().max().item(), (x.grad - g_ref).abs().max().item()
 
 
@@ -163,8 +163,24 @@ def test_moe_expert_parallel_matches_single():
         assert yerr < 1e-5 and gerr < 1e-5
 
 
+def _moe_cap_pair(rank, world, cap):
+    a = _moe_worker(rank, world, cap, sync_free=True)
+    b = _moe_worker(rank, world, cap, sync_free=False)
+    return ((a[0] - b[0]).abs().max().item(), (a[1] - b[1]).abs().max().item(),
+            max((ga - gb).abs().max().item() for ga, gb in zip(a[2], b[2])), int((a[0] == 0).all(1).sum()))
+
+
 def test_moe_capacity_drop_runs():
     run_dist(_moe_worker, 2, 0.5)
+
+
+def test_moe_capacity_sync_free_matches_exact_split():
+    """The fixed-capacity, equal-split exchange (no host sync) drops the same slots
+    and gives the same outputs and input / expert / gate gradients as the exact-split
+    exchange with the same capacity (reference seed: GShard capacity semantics)."""
+    for cap in (0.5, 1.0):
+        for yerr, xerr, perr, _ in run_dist(_moe_cap_pair, 2, cap):
+            assert yerr < 1e-5 and xerr < 1e-5 and perr < 1e-5, (cap, yerr, xerr, perr)
 
 
 # -------------------------------------------------------------- sharding stage 3
