@@ -11,7 +11,7 @@ STATE = {"main": fluid.Program(), "startup": fluid.Program(), "scope": fluid.cor
 
 
 def reset():
-    STATE.update(main=fluid.Program(), startup=fluid.Program(), scope=fluid.core.Scope(), data={}, metrics=[])
+    STATE.update(main=fluid.Program(), startup=fluid.Program(), scope=fluid.core.Scope(), data={}, evaluators=[])
 
 
 def guard():

@@ -29,7 +29,7 @@ class SGD:
         with fluid.scope_guard(STATE["scope"]):
             executor().run(STATE["startup"])
         parameters.restore(snap)
-        self.metrics = list(STATE.get("metrics", []))
+        self.evaluators = list(STATE.get("evaluators", []))
 
     def _feeder(self, feeding):
         names = list(STATE["data"])
@@ -41,37 +41,51 @@ class SGD:
         return fluid.DataFeeder(feed_list=[block.var(n) for n in names], place=place(), program=STATE["main"])
 
     def _run(self, program, feeder, batch):
-        fetch = [self.cost] + [v for _, v in self.metrics]
+        """One batch: fetch the cost and every evaluator's variables, feed the values
+        to the evaluators (pass statistics) and return (cost, batch metrics)."""
+        fetch = [self.cost] + [v for ev in self.evaluators for v in ev.fetch]
         with fluid.scope_guard(STATE["scope"]):
             outs = executor().run(program, feed=feeder.feed(batch), fetch_list=fetch)
-        vals = [float(np.array(o).ravel()[0]) for o in outs]
-        return vals[0], {n: v for (n, _), v in zip(self.metrics, vals[1:])}
+        outs = [np.array(o) for o in outs]
+        met, i = {}, 1
+        for ev in self.evaluators:
+            met.update(ev.eval(outs[i:i + len(ev.fetch)], len(batch)))
+            i += len(ev.fetch)
+        return float(outs[0].ravel()[0]), met
+
+    def _pass_metrics(self):
+        out = {}
+        for ev in self.evaluators:
+            out.update(ev.values())
+        return out
+
+    def _start(self):
+        for ev in self.evaluators:
+            ev.start()
 
     def train(self, reader, num_passes=1, event_handler=None, feeding=None):
         handler = event_handler or (lambda e: None)
         feeder = self._feeder(feeding)
         for pass_id in range(num_passes):
             handler(E.BeginPass(pass_id))
-            sums, n = {}, 0
+            self._start()
             for batch_id, batch in enumerate(reader()):
                 handler(E.BeginIteration(pass_id, batch_id))
                 cost, met = self._run(STATE["main"], feeder, batch)
-                for k, v in met.items():
-                    sums[k] = sums.get(k, 0.0) + v
-                n += 1
                 handler(E.EndIteration(pass_id, batch_id, cost, _Eval(met)))
-            handler(E.EndPass(pass_id, _Eval({k: v / max(n, 1) for k, v in sums.items()})))
+            handler(E.EndPass(pass_id, _Eval(self._pass_metrics())))
 
     def test(self, reader, feeding=None):
         feeder = self._feeder(feeding)
-        costs, sums, n = [], {}, 0
+        costs, n = [], 0
+        self._start()
         for batch in reader():
-            cost, met = self._run(self.test_program, feeder, batch)
+            cost, _ = self._run(self.test_program, feeder, batch)
             costs.append(cost * len(batch))
             n += len(batch)
-            for k, v in met.items():
-                sums[k] = sums.get(k, 0.0) + v * len(batch)
-        return E.TestResult(_Eval({k: v / max(n, 1) for k, v in sums.items()}), sum(costs) / max(n, 1))
+        res = E.TestResult(_Eval(self._pass_metrics()), sum(costs) / max(n, 1))
+        self._start()
+        return res
 
     def save_parameter_to_tar(self, f):
         self.parameters.to_tar(f)

@@ -138,3 +138,75 @@ def test_v2_parameter_config_wire_format():
     buf.seek(0)
     p = Parameters.from_tar(buf)
     np.testing.assert_array_equal(p["fc.w"], vals.reshape(3, 5))
+
+
+def test_v2_evaluators_pass_statistics():
+    """auc / precision_recall / sum / column_sum / pnpair accumulate over a whole
+    test pass (reference legacy Evaluator.cpp semantics) and match numpy / sklearn
+    computed from the same fetched predictions."""
+    from sklearn.metrics import roc_auc_score
+
+    paddle.init(use_gpu=False, trainer_count=1)
+    img = paddle.layer.data(name="pixel", type=paddle.data_type.dense_vector(16))
+    lbl = paddle.layer.data(name="label", type=paddle.data_type.integer_value(2))
+    qid = paddle.layer.data(name="qid", type=paddle.data_type.integer_value(4))
+    pred = paddle.layer.fc(input=img, size=2, act=paddle.activation.Softmax())
+    cost = paddle.layer.classification_cost(input=pred, label=lbl)
+    paddle.evaluator.auc(input=pred, label=lbl, name="auc")
+    paddle.evaluator.precision_recall(input=pred, label=lbl, name="pr")
+    paddle.evaluator.precision_recall(input=pred, label=lbl, positive_label=1, name="pr1")
+    paddle.evaluator.sum(input=pred, name="s")
+    paddle.evaluator.column_sum(input=pred, name="cs")
+    paddle.evaluator.pnpair(input=pred, label=lbl, query_id=qid, name="pn")
+    params = paddle.parameters.create(cost)
+    trainer = paddle.trainer.SGD(cost=cost, parameters=params,
+                                 update_equation=paddle.optimizer.Momentum(momentum=0.9, learning_rate=0.01))
+    rs = np.random.RandomState(3)
+    xs = rs.randn(96, 16).astype("float32")
+    ys = (xs[:, 0] + 0.5 * rs.randn(96) > 0).astype("int64")
+    qs = rs.randint(0, 4, 96)
+
+    def reader():
+        for i in range(0, 96, 32):
+            yield [(xs[j], int(ys[j]), int(qs[j])) for j in range(i, i + 32)]
+
+    res = trainer.test(reader=reader, feeding={"pixel": 0, "label": 1, "qid": 2})
+    m = res.metrics
+    probs = paddle.infer(output_layer=pred, parameters=params, input=[(x,) for x in xs], feeding={"pixel": 0})
+    p1 = probs[:, 1]
+    assert abs(m["auc"] - roc_auc_score(ys, p1)) < 1e-4
+    hat = probs.argmax(1)
+    tp = ((hat == 1) & (ys == 1)).sum()
+    fp = ((hat == 1) & (ys == 0)).sum()
+    fn = ((hat == 0) & (ys == 1)).sum()
+    assert abs(m["pr1.precision"] - tp / max(tp + fp, 1)) < 1e-6
+    assert abs(m["pr1.recal"] - tp / max(tp + fn, 1)) < 1e-6
+    assert abs(m["pr.micro-average-precision"] - (hat == ys).mean()) < 1e-6
+    assert abs(m["s"] - probs.sum()) < 1e-3
+    assert abs(m["cs.0"] - probs[:, 0].sum()) < 1e-3 and abs(m["cs.1"] - probs[:, 1].sum()) < 1e-3
+    pos = neg = 0.0
+    for q in range(4):
+        idx = np.nonzero(qs == q)[0]
+        for a in idx:
+            for b in idx:
+                if ys[a] > ys[b]:
+                    pos += (p1[a] > p1[b]) + 0.5 * (p1[a] == p1[b])
+                    neg += (p1[a] < p1[b]) + 0.5 * (p1[a] == p1[b])
+    assert abs(m["pn"] - pos / neg) < 1e-4
+
+
+def test_v2_chunk_and_ctc_evaluator_accumulation():
+    """Pass-level chunk P/R/F1 and CTC error are ratios of summed counts, not
+    means of per-batch ratios."""
+    from paddle_amd.v2 import evaluator as ev
+
+    c = ev._Chunk("chunk", [None, None, None])
+    c.eval([np.array([4]), np.array([5]), np.array([3])], 2)
+    c.eval([np.array([1]), np.array([5]), np.array([1])], 2)
+    v = c.values()
+    assert abs(v["chunk.precision"] - 4 / 5) < 1e-12 and abs(v["chunk.recall"] - 4 / 10) < 1e-12
+    assert abs(v["chunk.F1-score"] - 2 * 0.8 * 0.4 / 1.2) < 1e-12
+    e = ev._CtcError("ctc", [None, None])
+    e.eval([np.array([0.5, 0.0, 1.0]), np.array([3])], 3)
+    e.eval([np.array([0.25]), np.array([1])], 1)
+    assert abs(e.values()["ctc"] - 1.75 / 4) < 1e-12
