@@ -854,7 +854,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
 
 static int g_sched = -1;      // -1: per-layout default; 0 / 1: force PF_IN_CLUSTER (A/B runs)
 static int g_persistent = 1;  // 0: one tile per block (grid = tiles), for A/B runs
-static int g_stagger = 0;     // start stagger units per block slot (experiment)
+static int g_stagger = 1;     // start stagger units per block slot (profiles/r3_gemm_stagger_ab.jsonl: +0.7 % over the step GEMMs)
 
 template <bool AK, bool BK, bool F32, bool PF, bool KFULL, bool GA = false, bool F8 = false, int GM = 0>
 static int launch_v(const Params& p, int batch, hipStream_t st) {

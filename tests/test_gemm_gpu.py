@@ -130,3 +130,26 @@ def test_gemm_accumulate_into_strided_output(M, N, K, out_f32):
     tol = (2e-3 * K ** 0.5) if out_f32 else 2e-2 * ref.abs().max().item()
     assert (big[:, 16:16 + N].float() - ref).abs().max().item() <= tol
     assert torch.equal(big[:, :16], before[:, :16]) and torch.equal(big[:, 16 + N:], before[:, 16 + N:])
+
+
+@pytest.mark.parametrize("K", [64, 264, 512])
+@pytest.mark.parametrize("bias", [False, True])
+def test_gemm_persistent_multi_tile_direct_epilogue(K, bias):
+    """More output tiles than CUs (17 x 17 = 289 > 256, ragged edges): blocks of the
+    persistent grid run several tiles, so the direct-store epilogue's stores are
+    still in flight while the next tile's k-tiles 0 / 1 (pre-issued) are waited on
+    with the shifted counts; K = 64 has a single k-tile (k-tile 1 zero-fills)."""
+    from paddle_amd.ops import gemm as G
+
+    M = N = 4104
+    gen = torch.Generator(device="cuda").manual_seed(K + bias)
+    a, af = _operand(M, K, True, gen)
+    b, bf = _operand(N, K, True, gen)
+    bv = torch.randn(N, generator=gen, device="cuda").to(torch.bfloat16) if bias else None
+    c = G.gemm(a, b, M, N, K, a_kmaj=True, b_kmaj=True, bias=bv)
+    ref = af @ bf.t() + (bv.float() if bias else 0.0)
+    err = (c.float() - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item() + 1e-3, err
+    # the same product twice in a row on one stream: identical bits
+    c2 = G.gemm(a, b, M, N, K, a_kmaj=True, b_kmaj=True, bias=bv)
+    assert torch.equal(c, c2)

@@ -154,3 +154,36 @@ def test_moe_dispatch_combine_kernels():
     for a, b in zip(*outs):
         assert _rel(a, b) < 1e-2
     assert (outs[0][2][~keep] == 0).all()
+
+
+def test_moe_capacity_sync_free_layer_matches_exact_split():
+    """Fixed-capacity MoE layer (padded [expert, capacity] slabs, grouped experts on
+    the padded rows, combine with zero gradient for padding rows) vs the exact-split
+    path with the same capacity on the device: outputs and input / expert / gate
+    gradients agree."""
+    from paddle_amd.distributed.fleet import MoELayer, TopKGate
+    from paddle_amd.models.ernie_moe import ERNIE_MOE_CONFIGS, ErnieMoEConfig, ErnieMoEForCausalLM
+
+    kw = dict(ERNIE_MOE_CONFIGS["ernie-moe-tiny"])
+    kw.update(hidden_size=256, moe_intermediate_size=128, num_experts=8, top_k=2)
+    torch.manual_seed(0)
+    m = ErnieMoEForCausalLM(ErnieMoEConfig(**kw, grouped_experts=True), dev)
+    experts = m.layers[1].moe.experts
+    gate = TopKGate(256, 8, top_k=2, capacity_factor=0.75)
+    gate.weight.data = (torch.randn(256, 8, generator=torch.Generator().manual_seed(3)) * 0.3).to(dev)
+    x0 = torch.randn(384, 256, generator=torch.Generator().manual_seed(4)).to(dev).to(torch.bfloat16)
+    dy = torch.randn(384, 256, generator=torch.Generator().manual_seed(6)).to(dev).to(torch.bfloat16)
+    res = []
+    for sf in (True, False):
+        layer = MoELayer(256, experts, gate=gate, capacity_factor=0.75, sync_free=sf)
+        for p in list(experts.parameters()) + [gate.weight]:
+            p.grad = None
+        x = x0.clone().requires_grad_()
+        y = layer(x)
+        y.backward(dy)
+        res.append((y.float(), x.grad.float(), [p.grad.float().clone() for p in experts.parameters()],
+                    gate.weight.grad.float().clone()))
+    (ya, xa, pa, ga), (yb, xb, pb, gb) = res
+    assert _rel(ya, yb) < 1e-2 and _rel(xa, xb) < 2e-2 and _rel(ga, gb) < 2e-2
+    for a, b in zip(pa, pb):
+        assert _rel(a, b) < 2e-2
