@@ -131,6 +131,14 @@ class Executor:
             raise TypeError("Executor requires Program as its Parameter")
         if scope is None:
             scope = global_scope()
+        readers = getattr(program, "_py_readers", None)
+        if readers:
+            # py_reader programs run without a feed: each started reader supplies the
+            # next batch of its data vars (EOFException once it is exhausted)
+            feed = dict(feed)
+            for r in readers:
+                if r.started and not all(v.name in feed for v in r.feed_vars):
+                    feed.update(r.next_feed())
         fetch_names = [v.name if isinstance(v, Variable) else str(v) for v in fetch_list]
         feed_names = list(feed.keys())
         if self.engine == "native" and program.global_block().ops:

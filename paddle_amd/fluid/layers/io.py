@@ -26,22 +26,29 @@ def data(name, shape, append_batch_size=True, dtype="float32", lod_level=0, type
 
 
 class _PyReaderHandle:
-    """Host-side reader feeding a list of data vars (py_reader semantics).
+    """Host-side reader feeding a list of data vars (py_reader semantics, reference
+    layers/io.py:474 + operators/reader/create_py_reader_op.cc).
 
-    Backed by the native blocking queue when the runtime library is built
-    (paddle_amd.runtime.BlockingQueue), else a Python queue.  Tensors are staged
-    to pinned memory and copied to the device on a side stream (double_buffer).
+    ``start()`` runs the decorated provider on a Python thread that pushes every
+    batch into the native double-buffer pipeline (paddle_amd.runtime.
+    DoubleBufferReader, csrc/runtime/reader.cc): pinned host staging, a C++
+    prefetch thread copying the next batches to the device on its own HIP stream
+    (``use_double_buffer`` on a GPU), and a stream-ordered hand-off to the
+    executor's stream.  ``Executor.run`` pulls one batch per call for programs
+    that own a started reader; ``next_feed`` raises EOFException at the end.
+    Without the runtime library a Python queue is used instead.
     """
 
     def __init__(self, capacity, feed_vars, use_double_buffer=True):
-        import queue
-
         self.capacity = capacity
         self.feed_vars = feed_vars
-        self._q = queue.Queue(maxsize=capacity)
         self._provider = None
         self._thread = None
+        self._native = None
+        self._q = None
+        self.started = False
         self.use_double_buffer = use_double_buffer
+        self._error = None
 
     def decorate_tensor_provider(self, provider):
         p = provider
@@ -52,31 +59,80 @@ class _PyReaderHandle:
     decorate_paddle_reader = decorate_tensor_provider
     decorate_batch_generator = decorate_tensor_provider
 
+    def _make_native(self):
+        try:
+            import torch
+
+            from ... import runtime
+            if not runtime.available():
+                return None
+            dev = "cuda" if self.use_double_buffer and torch.cuda.is_available() else None
+            return runtime.DoubleBufferReader(capacity=max(1, self.capacity), nslots=2, device=dev)
+        except (OSError, RuntimeError):
+            return None
+
     def start(self):
+        import queue
         import threading
 
+        import numpy as np
+
+        if self._provider is None:
+            raise RuntimeError("py_reader: decorate a provider before start()")
+        if self._native is None:
+            self._native = self._make_native()
+        else:
+            self._native.reset()
+        if self._native is None:
+            self._q = queue.Queue(maxsize=self.capacity)
+        self._error = None
+
         def run():
-            for item in self._provider():
-                self._q.put(item)
-            self._q.put(None)
+            try:
+                for item in self._provider():
+                    arrs = [np.asarray(x.numpy() if hasattr(x, "numpy") else x) for x in item]
+                    if self._native is not None:
+                        if not self._native.push(arrs):
+                            return  # reset() closed the pipeline
+                    else:
+                        self._q.put(arrs)
+            except BaseException as e:  # surfaces in next_feed
+                self._error = e
+            finally:
+                if self._native is not None:
+                    self._native.close()
+                else:
+                    self._q.put(None)
 
         self._thread = threading.Thread(target=run, daemon=True)
         self._thread.start()
+        self.started = True
 
     def reset(self):
+        if self._native is not None:
+            self._native.close()
+        elif self._q is not None:
+            while self._q.qsize():
+                self._q.get_nowait()
         if self._thread is not None:
-            self._thread.join(timeout=1)
+            self._thread.join(timeout=5)
         self._thread = None
+        self.started = False
 
     def next_feed(self):
-        item = self._q.get()
+        if self._native is not None:
+            item = self._native.next()
+        else:
+            item = self._q.get()
+        if self._error is not None:
+            raise self._error
         if item is None:
+            self.started = False
             raise core_EOF()
         return {v.name: x for v, x in zip(self.feed_vars, item)}
 
 
-class core_EOF(Exception):
-    """EOFException raised when a reader is exhausted (platform/enforce.h EOFException)."""
+core_EOF = core.EOFException  # raised when a reader is exhausted (platform/enforce.h)
 
 
 EOFException = core_EOF
@@ -90,6 +146,10 @@ def py_reader(capacity, shapes, dtypes, lod_levels=None, name=None, use_double_b
                           append_batch_size=False))
     r = _PyReaderHandle(capacity, vars_, use_double_buffer)
     r.vars = vars_
+    prog = default_main_program()
+    if not hasattr(prog, "_py_readers"):
+        prog._py_readers = []
+    prog._py_readers.append(r)
     return r
 
 

@@ -420,3 +420,8 @@ def _switch_scope(scope):
     old = _global_scope
     _global_scope = scope
     return old
+
+
+class EOFException(Exception):
+    """Raised when a reader is exhausted (reference platform/enforce.h EOFException,
+    exposed as fluid.core.EOFException)."""

@@ -6,6 +6,7 @@ C++ RecordIO reader threads, DAG scheduler, profiler event buffers.
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import os
 import threading
@@ -49,6 +50,14 @@ _SIGS = {
     "pa_bq_close": ([P], None),
     "pa_bq_destroy": ([P], None),
     "pa_rt_free": ([P], None),
+    "pa_dbr_create": ([I, SZ, I], P),
+    "pa_dbr_push": ([P, I, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64)], I),
+    "pa_dbr_close": ([P], None),
+    "pa_dbr_next": ([P, ctypes.POINTER(ctypes.c_int64), I, I], I),
+    "pa_dbr_consume": ([P, I, ctypes.POINTER(ctypes.c_void_p), P], I),
+    "pa_dbr_queued": ([P], SZ),
+    "pa_dbr_reset": ([P], None),
+    "pa_dbr_destroy": ([P], None),
     "pa_bq_start_recordio_readers": ([P, ctypes.POINTER(ctypes.c_char_p), I, I, I], I),
     "pa_dag_run": ([I, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I), I, NODE_FN, P], I),
     "pa_prof_enable": ([I], None),
@@ -313,6 +322,88 @@ class BlockingQueue:
         try:
             if self._h:
                 lib().pa_bq_destroy(self._h)
+        except Exception:
+            pass
+
+
+# ------------------------------------------------------------------ double-buffer reader
+
+
+class DoubleBufferReader:
+    """Native py_reader pipeline (csrc/runtime/reader.cc; reference
+    operators/reader/buffered_reader.cc, lod_tensor_blocking_queue.h): ``push``
+    stages a batch of numpy arrays in pinned host memory (blocks while
+    ``capacity`` batches wait), a C++ thread copies batches to ``nslots`` device
+    slots on its own HIP stream, and ``next`` hands the oldest one to the current
+    torch stream (event wait + device-to-device copy, no host sync).  ``device``
+    None = host mode (CPU tensors, same queue logic)."""
+
+    def __init__(self, capacity=2, nslots=2, device=None):
+        import torch
+
+        self.device = device
+        self._torch = torch
+        dev = -1 if device is None else int(torch.device(device).index or 0)
+        self._h = lib().pa_dbr_create(int(nslots), int(capacity), dev)
+        if not self._h:
+            raise RuntimeError(_err())
+        self._meta = collections.deque()  # (shapes, dtypes) per pushed batch, FIFO
+        self._mu = threading.Lock()
+
+    def push(self, arrays) -> bool:
+        import numpy as np
+
+        arrs = [np.ascontiguousarray(a) for a in arrays]
+        n = len(arrs)
+        ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
+        nbytes = (ctypes.c_int64 * n)(*[a.nbytes for a in arrs])
+        with self._mu:  # meta order == queue order (one producer at a time)
+            self._meta.append(([a.shape for a in arrs], [a.dtype for a in arrs]))
+            rc = lib().pa_dbr_push(self._h, n, ptrs, nbytes)
+            if rc != 0:
+                self._meta.pop()
+        if rc == -2:
+            raise MemoryError(_err())
+        return rc == 0
+
+    def close(self):
+        lib().pa_dbr_close(self._h)
+
+    def next(self, timeout_ms=-1):
+        """The next batch as a list of tensors (on ``device``), or None at EOF."""
+        import numpy as np
+
+        torch = self._torch
+        nb = (ctypes.c_int64 * 64)()
+        s = lib().pa_dbr_next(self._h, nb, 64, int(timeout_ms))
+        if s == -1:
+            return None
+        if s == -2:
+            raise TimeoutError("DoubleBufferReader.next timed out")
+        if s < 0:
+            raise RuntimeError(_err())
+        shapes, dtypes = self._meta.popleft()
+        outs = [torch.empty(tuple(sh), dtype=torch.from_numpy(np.empty(0, dt)).dtype,
+                            device=self.device if self.device is not None else "cpu")
+                for sh, dt in zip(shapes, dtypes)]
+        dst = (ctypes.c_void_p * len(outs))(*[o.data_ptr() if o.numel() else None for o in outs])
+        stream = torch.cuda.current_stream(self.device).cuda_stream if self.device is not None else None
+        if lib().pa_dbr_consume(self._h, s, dst, stream) != 0:
+            raise RuntimeError(_err())
+        return outs
+
+    def queued(self):
+        return lib().pa_dbr_queued(self._h)
+
+    def reset(self):
+        lib().pa_dbr_reset(self._h)
+        self._meta.clear()
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().pa_dbr_destroy(self._h)
+                self._h = None
         except Exception:
             pass
 
