@@ -209,6 +209,43 @@ def build_tracer(verbose: bool = False) -> str:
     return _build_lib(srcs, [], TRACER_LIB, cxx, cflags, ldflags, verbose, 1)
 
 
+def core_ext_path() -> str:
+    import sysconfig
+
+    return os.path.join(LIBDIR, "paddle_amd_core" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+
+
+def build_core_ext(verbose: bool = False) -> str:
+    """The CPython extension ``paddle_amd_core`` (csrc/pybind): pybind11 bindings of
+    the native C++ ProgramDesc / Scope / LoDTensor / Executor (the reference's
+    pybind core), linked against libpaddle_amd_native.so."""
+    try:
+        import sysconfig
+
+        import pybind11
+    except ImportError:
+        return ""
+    srcs = sorted(glob.glob(os.path.join(ROOT, "csrc", "pybind", "*.cc")))
+    if not srcs:
+        return ""
+    native_lib = build_native(verbose)
+    out = core_ext_path()
+    hdrs = sorted(glob.glob(os.path.join(ROOT, "csrc", "native", "*.h")))
+    if os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(f) for f in srcs + hdrs + [native_lib]):
+        return out
+    cxx = shutil.which("g++") or "c++"
+    cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", f"-I{pybind11.get_include()}",
+           f"-I{sysconfig.get_paths()['include']}", "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"] + srcs + \
+        ["-o", out + ".tmp", f"-L{LIBDIR}", "-lpaddle_amd_native", "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print("[paddle_amd build]", " ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"building {out} failed:\n{r.stderr[-4000:]}")
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def build_all(verbose: bool = False) -> list[str]:
     out = [build_kernels(verbose)]
     rt = build_runtime(verbose)
@@ -218,6 +255,9 @@ def build_all(verbose: bool = False) -> list[str]:
     tr = build_tracer(verbose)
     if tr:
         out.append(tr)
+    ce = build_core_ext(verbose)
+    if ce:
+        out.append(ce)
     return out
 
 

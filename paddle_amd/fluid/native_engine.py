@@ -19,6 +19,11 @@ Scope of the engine: dense LoDTensor programs of block 0 (no control-flow
 sub-blocks, no LoD feeds, no SelectedRows); anything else raises
 ``NotImplementedError`` naming what is unsupported -- use the default engine for it.
 
+The engine drives the C++ objects through the ``paddle_amd_core`` CPython
+extension (csrc/pybind/core_module.cc, pybind11) when it is built, else through
+the ctypes C ABI of ``paddle_amd.native`` (``FLAGS_native_binding=ctypes`` forces
+the latter).
+
 Reference: framework/executor.cc:125-353 (Executor::Run), pybind/pybind.cc:507
 (the Executor binding the Python layer drives).
 """
@@ -27,6 +32,8 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+import os
+
 from .. import native
 from ..framework import core
 
@@ -34,11 +41,96 @@ _TORCH_DT = {torch.float32: 5, torch.int64: 3, torch.int32: 2, torch.float64: 6,
 _DT_TORCH = {v: k for k, v in _TORCH_DT.items()}
 
 
+class _CtypesBinding:
+    """The C ABI path (paddle_amd.native)."""
+
+    name = "ctypes"
+
+    def __init__(self, device):
+        self.exe = native.NativeExecutor(device)
+
+    program = staticmethod(lambda data: native.NativeProgram(data=data))
+    scope = staticmethod(native.NativeScope)
+
+    @staticmethod
+    def share(ns, name, ptr, dt, shape, device):
+        ns.share(name, ptr, dt, shape, device)
+
+    @staticmethod
+    def set(ns, name, arr, device):
+        ns.set(name, arr, device)
+
+    @staticmethod
+    def info(ns, name):
+        return ns.info(name)
+
+    @staticmethod
+    def get(ns, name):
+        return ns.get(name)
+
+    def run(self, prog, ns):
+        self.exe.run(prog, ns)
+
+    def host_fallbacks(self):
+        return self.exe.host_fallbacks()
+
+
+class _PybindBinding:
+    """The CPython extension path (paddle_amd_core, pybind11 over the C++ classes)."""
+
+    name = "pybind"
+
+    def __init__(self, device, mod):
+        self.C = mod
+        self.exe = mod.Executor(device)
+
+    def program(self, data):
+        return self.C.ProgramDesc(data)
+
+    def scope(self):
+        return self.C.Scope()
+
+    def share(self, ns, name, ptr, dt, shape, device):
+        ns.var(name).get_tensor().share_external(ptr, self.C.VarType(dt), list(shape), device)
+
+    def set(self, ns, name, arr, device):
+        ns.var(name).get_tensor().set(arr, device)
+
+    def info(self, ns, name):
+        v = ns.find_var(name)
+        if v is None or not v.is_initialized():
+            return None
+        t = v.get_tensor()
+        return int(t.dtype()), tuple(t.shape()), t.data_ptr(), t.device()
+
+    def get(self, ns, name):
+        v = ns.find_var(name)
+        if v is None or not v.is_initialized():
+            raise RuntimeError(f"variable {name} not found or empty")
+        return v.get_tensor().numpy()
+
+    def run(self, prog, ns):
+        self.exe.run(prog, ns)
+
+    def host_fallbacks(self):
+        return dict(self.exe.host_fallbacks)
+
+
+def _binding(device):
+    if os.environ.get("FLAGS_native_binding", "pybind") != "ctypes":
+        from .. import core_ext
+
+        mod = core_ext.module()
+        if mod is not None:
+            return _PybindBinding(device, mod)
+    return _CtypesBinding(device)
+
+
 class NativeEngine:
     def __init__(self, place):
         self.place = place
         self.device = int(place.device_id) if isinstance(place, core.CUDAPlace) else -1
-        self._exe = native.NativeExecutor(self.device)
+        self._b = _binding(self.device)
         self._progs = {}
         self._scopes = {}  # id(python scope) -> (scope ref, NativeScope, {name: (ptr, shape, dtype, tensor)})
         self._host_ops = set(native.registered_ops(False))
@@ -57,7 +149,7 @@ class NativeEngine:
         subs = sorted({op.type for op in block.ops if any(k in op.attrs for k in ("sub_block", "blocks"))})
         if subs:
             raise NotImplementedError(f"native engine: control-flow ops with sub-blocks {subs}")
-        prog = native.NativeProgram(data=program.desc.serialize_to_string())
+        prog = self._b.program(program.desc.serialize_to_string())
         pers = [v.name for v in program.list_vars()
                 if v.persistable and v.name not in ("feed", "fetch") and v.type == core.VT.LOD_TENSOR]
         self._progs[key] = (program, prog, pers)
@@ -66,7 +158,7 @@ class NativeEngine:
     def _scope(self, scope):
         ent = self._scopes.get(id(scope))
         if ent is None or ent[0] is not scope:
-            ent = (scope, native.NativeScope(), {})
+            ent = (scope, self._b.scope(), {})
             self._scopes[id(scope)] = ent
         return ent[1], ent[2]
 
@@ -86,7 +178,7 @@ class NativeEngine:
             lt._t = t
         sig = (t.data_ptr(), tuple(t.shape), t.dtype)
         if bound.get(name, (None,))[:3] != sig:
-            ns.share(name, t.data_ptr(), _TORCH_DT[t.dtype], tuple(t.shape), self.device)
+            self._b.share(ns, name, t.data_ptr(), _TORCH_DT[t.dtype], tuple(t.shape), self.device)
             bound[name] = sig + (t,)
 
     def _feed(self, ns, name, data):
@@ -96,12 +188,12 @@ class NativeEngine:
             data = data._t
         if isinstance(data, torch.Tensor):
             data = data.detach().cpu().numpy()
-        ns.set(name, np.ascontiguousarray(np.asarray(data)), self.device)
+        self._b.set(ns, name, np.ascontiguousarray(np.asarray(data)), self.device)
 
     def _write_back(self, scope, ns, bound, name):
         """After a run: a persistable whose native buffer moved is copied into a torch
         tensor of the Python scope (and lent again, so later runs update it in place)."""
-        info = ns.info(name)
+        info = self._b.info(ns, name)
         if info is None:
             return
         dt, shape, ptr, dev = info
@@ -134,14 +226,18 @@ class NativeEngine:
             self._feed(ns, name, data)
         if self.device >= 0:
             torch.cuda.current_stream(self._tdev()).synchronize()  # lent tensors written by torch
-        self._exe.run(prog, ns)  # ends with a sync of the native stream
+        self._b.run(prog, ns)  # ends with a sync of the native stream
         for name in pers:
             self._write_back(scope, ns, bound, name)
         outs = []
         for n in fetch_names:
-            a = ns.get(n)
+            a = self._b.get(ns, n)
             outs.append(a if return_numpy else core.LoDTensor(torch.from_numpy(a).to(self._tdev())))
         return outs
 
     def host_fallbacks(self):
-        return self._exe.host_fallbacks()
+        return self._b.host_fallbacks()
+
+    @property
+    def binding(self):
+        return self._b.name
