@@ -29,7 +29,7 @@ def timeit(fn, reps=20):
 
 outs, res = {}, {}
 for rnd in range(3):
-    for var in (1, 2):
+    for var in [int(v) for v in os.environ.get("VARIANTS", "1,2").split(",")]:
         N.call("pa_fa_fwd_set_variant", var)
         t = timeit(lambda: F.flash_attention(q, k, v, causal=True))
         res.setdefault(var, []).append(t)
@@ -38,4 +38,5 @@ for rnd in range(3):
 N.call("pa_fa_fwd_set_variant", 2)
 for var, ts in res.items():
     print(json.dumps({"variant": var, "ms": [round(x, 4) for x in ts], "TF_best": round(flop / min(ts) / 1e9, 1)}))
-print(json.dumps({"max_abs_diff_v1_v2": float((outs[1] - outs[2]).abs().max())}))
+ks = sorted(outs)
+print(json.dumps({f"max_abs_diff_v{ks[0]}_v{k}": float((outs[ks[0]] - outs[k]).abs().max()) for k in ks[1:]}))

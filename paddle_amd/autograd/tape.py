@@ -114,6 +114,8 @@ class Tape:
 
     # ------------------------------------------------------------------ backward
     def backward(self, loss, grad=None):
+        while _BEFORE_BACKWARD:  # e.g. an optimizer update still running on a side stream
+            _BEFORE_BACKWARD.pop(0)()
         tg = getattr(loss, "_pa_tape", None)
         if tg is None or tg[0] != id(self):
             raise RuntimeError("tape.backward: the loss was not produced on this tape")
@@ -167,6 +169,16 @@ def _add(a, b):
         if r is not None:
             return r
     return a + b
+
+
+_BEFORE_BACKWARD = []
+
+
+def before_next_backward(fn):
+    """Run ``fn`` once at the start of the next reverse pass (before any gradient
+    is written)."""
+    if fn not in _BEFORE_BACKWARD:
+        _BEFORE_BACKWARD.append(fn)
 
 
 @contextlib.contextmanager

@@ -41,6 +41,7 @@ import os
 import torch
 
 from ..ops import fused
+from ..autograd import tape as _tape
 from ..ops import optim as fused_optim
 from . import comm
 
@@ -56,7 +57,8 @@ class FlatShardedOptimizer:
 
     def __init__(self, named_params, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1,
                  group=None, bucket_mb=256, grad_clip=None, overlap=True, stage=1,
-                 no_decay_fn=None, overlap_allgather=False, grad_dtype="auto", dp_comm=None):
+                 no_decay_fn=None, overlap_allgather=False, grad_dtype="auto", dp_comm=None,
+                 overlap_update=None):
         named = [(n, p) for n, p in named_params if p.requires_grad]
         if not named:
             raise ValueError("no trainable parameters")
@@ -158,6 +160,14 @@ class FlatShardedOptimizer:
         # deferred all-gathers: [(bucket, cuda event | deferred callable)] in issue order
         self.overlap_allgather = bool(overlap_allgather) and self.W > 1
         self._ag_queue = []
+        # overlapped update (one rank): AdamW per bucket on a side stream, forward
+        # order, each parameter's first read waits only for its own bucket -- the
+        # bandwidth-bound update hides under the next forward's GEMMs
+        if overlap_update is None:
+            overlap_update = os.environ.get("FLAGS_overlap_optimizer", "1") != "0"
+        self.overlap_update = bool(overlap_update) and self.W == 1 and dev.type == "cuda"
+        self.opt_stream = torch.cuda.Stream(device=dev) if self.overlap_update else None
+        self._keep = None
         # FLAGS_dp_comm=direct: reduce-scatter / all-gather over IPC-mapped peer
         # buffers on the xGMI links (parallel/direct.py) instead of RCCL
         self.dp_comm = os.environ.get("FLAGS_dp_comm", "rccl") if dp_comm is None else dp_comm
@@ -327,6 +337,9 @@ class FlatShardedOptimizer:
         self._finish_comm()
         self.step_count += 1
         gst = self._grad_scale_tensor()
+        if self.overlap_update:
+            self._update_overlapped(gst)
+            return
         fused_optim.adamw_flat(self.master, self.grad_shard, self.m, self.v, lr=self.lr,
                                beta1=self.betas[0], beta2=self.betas[1], eps=self.eps,
                                weight_decay=self.wd, step=self.step_count, param_out=self.param_shard,
@@ -341,6 +354,34 @@ class FlatShardedOptimizer:
         if self._direct is not None:
             with torch.cuda.stream(self.comm_stream) if self.overlap else contextlib.nullcontext():
                 self._direct.error_async()
+        fused.bump_weight_epoch()
+
+    def _update_overlapped(self, gst):
+        """One-rank step: the update of bucket b runs on ``opt_stream`` after the
+        gradients are final, buckets in forward order; each parameter is marked
+        pending on its bucket's event (fused.param_ready waits for it at first use),
+        and the next reverse pass waits for all of them before it writes gradients."""
+        main = torch.cuda.current_stream(self.device)
+        self.opt_stream.wait_event(main.record_event())
+        if gst is not None:
+            gst.record_stream(self.opt_stream)
+        self._keep = gst  # read on the side stream: alive until the next step
+        for b in reversed(range(len(self.buckets))):
+            s0, L, so = self.shard_slices[b]
+            if L == 0:
+                continue
+            de = min(max(self.shard_decay_end - so, 0), L)
+            with torch.cuda.stream(self.opt_stream):
+                fused_optim.adamw_flat(self.master[so:so + L], self.grad_shard[s0:s0 + L], self.m[so:so + L],
+                                       self.v[so:so + L], lr=self.lr, beta1=self.betas[0], beta2=self.betas[1],
+                                       eps=self.eps, weight_decay=self.wd, step=self.step_count,
+                                       param_out=self.param_shard[s0:s0 + L], decay_end=de, grad_scale=1.0,
+                                       grad_scale_tensor=gst)
+                ev = self.opt_stream.record_event()
+            self._ag_queue.append((b, ev))
+            for p in self.buckets[b][2]:
+                p._pa_pending = self._param_wait
+        _tape.before_next_backward(self.sync_params)
         fused.bump_weight_epoch()
 
     def zero_grad(self, set_to_none=False):
