@@ -1,0 +1,297 @@
+"""v1 model-config DSL (reference python/paddle/trainer_config_helpers/: layers.py,
+activations.py, poolings.py, optimizers.py, evaluators.py, networks.py, attrs.py)
+and its config parser (python/paddle/trainer/config_parser.py ``parse_config``).
+
+A v1 config is a Python script that calls ``settings(...)``, builds a topology
+with ``data_layer`` / ``fc_layer`` / ... and declares ``outputs(...)``; the
+reference turns it into a ModelConfig proto for the legacy GradientMachine.  Here
+the same DSL builds the v2 facade's Fluid program (paddle_amd/v2: each layer is
+one or a few Fluid ops on the MI355X kernels), and ``parse_config`` returns a
+``TrainerConfig`` whose ``make_trainer()`` gives a v2 ``trainer.SGD`` with the
+optimizer that ``settings`` described.
+
+Data-layer types: v1 takes them from the data provider (``@provider(input_types=
+...)``); here ``data_layer(name, size, type=...)`` takes an explicit v2 data type,
+and without one a layer whose name contains ``label`` is ``integer_value(size)``,
+any other ``dense_vector(size)``.
+"""
+from __future__ import annotations
+
+import os
+
+from .. import v2
+from ..v2 import activation as _act
+from ..v2 import data_type as _dt
+from ..v2 import evaluator as _ev
+from ..v2 import layer as _l
+from ..v2 import networks as _nets
+from ..v2 import optimizer as _opt
+from ..v2 import pooling as _pool
+from ..v2._core import STATE
+
+# ------------------------------------------------------------------ activations
+TanhActivation, ReluActivation, SigmoidActivation = _act.Tanh, _act.Relu, _act.Sigmoid
+SoftmaxActivation, LinearActivation, IdentityActivation = _act.Softmax, _act.Linear, _act.Identity
+ExpActivation, AbsActivation, SquareActivation = _act.Exp, _act.Abs, _act.Square
+BReluActivation, SoftReluActivation, STanhActivation = _act.BRelu, _act.SoftRelu, _act.STanh
+
+# ------------------------------------------------------------------ poolings
+MaxPooling, AvgPooling, SumPooling, SquareRootNPooling = _pool.Max, _pool.Avg, _pool.Sum, _pool.SquareRootN
+CudnnMaxPooling, CudnnAvgPooling = _pool.Max, _pool.Avg
+
+
+# ------------------------------------------------------------------ attributes
+class ParameterAttribute:
+    def __init__(self, name=None, initial_std=None, initial_mean=None, learning_rate=None, l2_rate=None, **kw):
+        self.name, self.initial_std, self.initial_mean = name, initial_std, initial_mean
+        self.learning_rate, self.l2_rate = learning_rate, l2_rate
+
+
+class ExtraLayerAttribute:
+    def __init__(self, drop_rate=None, error_clipping_threshold=None, device=None, **kw):
+        self.drop_rate, self.error_clipping_threshold = drop_rate, error_clipping_threshold
+
+
+ParamAttr, ExtraAttr = ParameterAttribute, ExtraLayerAttribute
+
+
+# ------------------------------------------------------------------ optimizers / settings
+class L2Regularization(_opt.L2Regularization):
+    pass
+
+
+class BaseSGDOptimizer:
+    kind = None
+
+    def __init__(self, **kw):
+        self.kw = kw
+
+
+class MomentumOptimizer(BaseSGDOptimizer):
+    def __init__(self, momentum=None, sparse=False):
+        super().__init__(momentum=momentum or 0.0)
+        self.kind = _opt.Momentum
+
+
+class AdamOptimizer(BaseSGDOptimizer):
+    def __init__(self, beta1=0.9, beta2=0.999, epsilon=1e-8):
+        super().__init__(beta1=beta1, beta2=beta2, epsilon=epsilon)
+        self.kind = _opt.Adam
+
+
+class AdamaxOptimizer(BaseSGDOptimizer):
+    def __init__(self, beta1=0.9, beta2=0.999):
+        super().__init__(beta1=beta1, beta2=beta2)
+        self.kind = _opt.Adamax
+
+
+class AdaGradOptimizer(BaseSGDOptimizer):
+    def __init__(self):
+        super().__init__()
+        self.kind = _opt.AdaGrad
+
+
+class DecayedAdaGradOptimizer(BaseSGDOptimizer):
+    def __init__(self, rho=0.95, epsilon=1e-6):
+        super().__init__(rho=rho, epsilon=epsilon)
+        self.kind = _opt.DecayedAdaGrad
+
+
+class AdaDeltaOptimizer(BaseSGDOptimizer):
+    def __init__(self, rho=0.95, epsilon=1e-6):
+        super().__init__(rho=rho, epsilon=epsilon)
+        self.kind = _opt.AdaDelta
+
+
+class RMSPropOptimizer(BaseSGDOptimizer):
+    def __init__(self, rho=0.95, epsilon=1e-6):
+        super().__init__(rho=rho, epsilon=epsilon)
+        self.kind = _opt.RMSProp
+
+
+_CFG: dict = {}
+
+
+def settings(batch_size, learning_rate=1e-3, learning_method=None, regularization=None,
+             gradient_clipping_threshold=None, model_average=None, **kw):
+    """optimizers.py settings(): the optimization section of the config."""
+    _CFG.update(batch_size=int(batch_size), learning_rate=float(learning_rate),
+                learning_method=learning_method or MomentumOptimizer(), regularization=regularization,
+                gradient_clipping_threshold=gradient_clipping_threshold, extra=kw)
+
+
+def outputs(*layers):
+    out = []
+    for x in layers:
+        out.extend(x if isinstance(x, (list, tuple)) else [x])
+    _CFG["outputs"] = out
+
+
+def get_config_arg(name, type, default=None):
+    """config_parser.get_config_arg: a value of ``config_arg_str`` ("a=1,b=x")."""
+    v = _CFG.get("args", {}).get(name)
+    if v is None:
+        return default
+    if type is bool:
+        return v.lower() in ("1", "true", "t", "yes")
+    return type(v)
+
+
+# ------------------------------------------------------------------ layers
+def data_layer(name, size, height=None, width=None, type=None, **kw):
+    if type is None:
+        type = _dt.integer_value(size) if "label" in name else _dt.dense_vector(size)
+    return _l.data(name=name, type=type)
+
+
+def _one(x):
+    return x[0] if isinstance(x, (list, tuple)) and len(x) == 1 else x
+
+
+def fc_layer(input, size, act=None, name=None, param_attr=None, bias_attr=None, layer_attr=None, **kw):
+    """A list of inputs is one projection each, summed with one bias: the same as
+    one fc over their concatenation."""
+    x = _one(input)
+    if isinstance(x, (list, tuple)):
+        x = _l.concat(input=list(x))
+    out = _l.fc(input=x, size=size, act=act if act is not None else TanhActivation(), name=name)
+    if layer_attr is not None and getattr(layer_attr, "drop_rate", None):
+        out = _l.dropout(input=out, dropout_rate=layer_attr.drop_rate)
+    return out
+
+
+def embedding_layer(input, size, name=None, param_attr=None, **kw):
+    return _l.embedding(input=input, size=size)
+
+
+def img_conv_layer(input, filter_size, num_filters, num_channels=None, stride=1, padding=0, act=None, groups=1,
+                   name=None, bias_attr=None, param_attr=None, **kw):
+    return _l.img_conv(input=input, filter_size=filter_size, num_filters=num_filters, num_channels=num_channels,
+                       stride=stride, padding=padding, act=act if act is not None else ReluActivation(),
+                       groups=groups)
+
+
+def img_pool_layer(input, pool_size, stride=1, padding=0, pool_type=None, num_channels=None, name=None, **kw):
+    return _l.img_pool(input=input, pool_size=pool_size, stride=stride, padding=padding,
+                       pool_type=pool_type or MaxPooling(), num_channels=num_channels)
+
+
+def batch_norm_layer(input, act=None, name=None, **kw):
+    return _l.batch_norm(input=input, act=act if act is not None else ReluActivation())
+
+
+def dropout_layer(input, dropout_rate, name=None):
+    return _l.dropout(input=input, dropout_rate=dropout_rate)
+
+
+def concat_layer(input, act=None, name=None, **kw):
+    return _l.concat(input=input)
+
+
+def addto_layer(input, act=None, name=None, bias_attr=None, **kw):
+    from .. import fluid
+
+    with v2._core.guard():
+        s = fluid.layers.sums(list(input))
+        a = _act.act_name(act)
+        return getattr(fluid.layers, a)(s) if a else s
+
+
+def pooling_layer(input, pooling_type=None, name=None, **kw):
+    return _l.pooling(input=input, pooling_type=pooling_type or MaxPooling())
+
+
+def last_seq(input, name=None, **kw):
+    return _l.last_seq(input=input)
+
+
+def first_seq(input, name=None, **kw):
+    return _l.first_seq(input=input)
+
+
+def maxid_layer(input, name=None, **kw):
+    return _l.max_id(input=input)
+
+
+def classification_cost(input, label, name=None, evaluator=None, **kw):
+    return _l.classification_cost(input=input, label=label, name=name)
+
+
+def cross_entropy(input, label, name=None, **kw):
+    return _l.cross_entropy_cost(input=input, label=label)
+
+
+def regression_cost(input, label, name=None, **kw):
+    return _l.square_error_cost(input=input, label=label)
+
+
+mse_cost = square_error_cost = regression_cost
+
+# ------------------------------------------------------------------ networks
+simple_img_conv_pool = _nets.simple_img_conv_pool
+sequence_conv_pool = _nets.sequence_conv_pool
+simple_lstm = _nets.simple_lstm
+
+# ------------------------------------------------------------------ evaluators
+classification_error_evaluator = _ev.classification_error
+auc_evaluator = _ev.auc
+precision_recall_evaluator = _ev.precision_recall
+pnpair_evaluator = _ev.pnpair
+chunk_evaluator = _ev.chunk
+ctc_error_evaluator = _ev.ctc_error
+sum_evaluator = _ev.sum
+column_sum_evaluator = _ev.column_sum
+value_printer_evaluator = _ev.value_printer
+maxid_printer_evaluator = _ev.maxid_printer
+classification_error_printer_evaluator = _ev.classification_error_printer
+
+
+# ------------------------------------------------------------------ config parser
+class TrainerConfig:
+    """What config_parser.parse_config returns: the model (outputs, data layers,
+    parameters -- a Fluid program) and the optimization settings."""
+
+    def __init__(self, cfg):
+        self.outputs = cfg.get("outputs", [])
+        self.batch_size = cfg.get("batch_size")
+        self.learning_rate = cfg.get("learning_rate")
+        self.learning_method = cfg.get("learning_method")
+        self.regularization = cfg.get("regularization")
+        self.gradient_clipping_threshold = cfg.get("gradient_clipping_threshold")
+        self.program = STATE["main"]
+        self.input_layer_names = list(STATE["data"])
+
+    @property
+    def cost(self):
+        return self.outputs[0]
+
+    def update_equation(self):
+        m = self.learning_method or MomentumOptimizer()
+        return m.kind(learning_rate=self.learning_rate, regularization=self.regularization,
+                      gradient_clipping_threshold=self.gradient_clipping_threshold, **m.kw)
+
+    def make_trainer(self, parameters=None):
+        params = parameters or v2.parameters.create(self.cost)
+        return v2.trainer.SGD(cost=self.cost, parameters=params, update_equation=self.update_equation()), params
+
+
+def parse_config(config, config_arg_str=""):
+    """Runs a v1 config (a file path, or a callable taking no arguments) with this
+    DSL in scope and returns its TrainerConfig.  ``config_arg_str``: "k=v,k2=v2",
+    read inside the config with get_config_arg."""
+    args = dict(kv.split("=", 1) for kv in config_arg_str.split(",") if "=" in kv)
+    _CFG.clear()
+    _CFG["args"] = args
+    v2.init(use_gpu=STATE.get("use_gpu", False))
+    if callable(config):
+        config()
+    else:
+        path = os.fspath(config)
+        with open(path) as f:
+            code = compile(f.read(), path, "exec")
+        g = {k: v for k, v in globals().items() if not k.startswith("_")}
+        g["__file__"] = path
+        exec(code, g)  # noqa: S102  (a v1 config is a Python script, as in the reference)
+    if not _CFG.get("outputs"):
+        raise ValueError("the config declared no outputs(...)")
+    return TrainerConfig(_CFG)
