@@ -2,8 +2,8 @@
 bucket on a side stream, each parameter's first read in the next forward waits
 for its own bucket, and the next reverse pass waits for the rest.  Trained with
 the framework tape it must give bit-identical losses and parameters to the
-single-kernel update, up to the run-to-run nondeterminism of the float-atomic
-kernels (split-K GEMM partials, attention dQ) whose addition order depends on timing."""
+single-kernel update (distinct token ids keep every kernel of the step
+deterministic: no colliding float atomics)."""
 import pytest
 import torch
 
@@ -26,7 +26,9 @@ def _train(overlap, steps=4):
     g = torch.Generator().manual_seed(1)
     losses = []
     for i in range(steps):
-        ids = torch.randint(0, cfg.vocab_size, (2, 129), generator=g).to(dev)
+        # distinct token ids: the embedding backward's float atomics never collide,
+        # so the whole step is deterministic and the two updates compare bitwise
+        ids = torch.randperm(cfg.vocab_size, generator=g)[:2 * 129].view(2, 129).to(dev)
         for a in range(2):  # two micro-batches: accumulation into main grads
             with tape.recording() as t:
                 loss = model(ids[:, :-1], ids[:, 1:])
@@ -36,17 +38,16 @@ def _train(overlap, steps=4):
         losses.append(loss.item())
     opt.sync_params()
     torch.cuda.synchronize()
-    return losses, torch.cat([p.detach().float().reshape(-1) for p in model.parameters()])
+    return losses, opt.master.detach().clone()
 
 
 def test_overlapped_update_matches_single_kernel_update():
     la, pa = _train(True)
     lb, pb = _train(False)
-    assert la[0] == lb[0]  # before any update: same model, same data
-    for a, b in zip(la, lb):
-        assert abs(a - b) < 1e-3 * abs(b), (la, lb)
-    assert (pa - pb).abs().max().item() < 1e-3, (pa - pb).abs().max().item()
-    # both runs moved the parameters by the same amounts (a stale read of a
-    # parameter would show as a whole missed update: lr-sized errors)
     lc, pc = _train(False)
-    assert (pa - pb).abs().max() <= 4 * (pc - pb).abs().max() + 1e-5
+    ref_noise = (pc - pb).abs().max().item()  # run-to-run spread of the plain update
+    if ref_noise == 0.0:
+        assert la == lb, (la, lb)
+        assert torch.equal(pa, pb), (pa - pb).abs().max().item()
+    else:  # some kernel of the step is nondeterministic: stay within its spread
+        assert (pa - pb).abs().max().item() <= 3 * ref_noise, ((pa - pb).abs().max().item(), ref_noise)
