@@ -16,7 +16,11 @@
 //             barrier.  Per-rank traffic 2(P-1)/P of the message over P-1 links.
 //
 // Barriers spin a bounded number of times (then flag an error and exit), so a
-// missing peer can never leave a wave running forever.
+// missing peer can never leave a wave running forever.  The reduce / gather
+// kernels read that flag first: after a timed-out barrier they write NaN instead
+// of summing a peer's stale or half-written staging data, so a lost peer shows up
+// as a poisoned result (and parallel/direct.py raises on the flag), never as a
+// silently wrong gradient.
 #include <string.h>
 
 #include "common.h"
@@ -55,10 +59,24 @@ __device__ __forceinline__ void ld8(const T* p, float (&o)[8]) {
 
 // out[i] = sum_r stage_r[i] over [begin, end) (elements; multiples of 8)
 template <typename T>
-__global__ __launch_bounds__(256) void p2p_reduce_kernel(PeerArgs a, T* __restrict__ out, long begin, long end) {
+__device__ __forceinline__ void poison8(T* p) {
+  float nan8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) nan8[j] = __builtin_nanf("");
+  store8(p, nan8);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void p2p_reduce_kernel(PeerArgs a, T* __restrict__ out, long begin, long end,
+                                                        const int* err) {
   const long n8 = (end - begin) / 8;
+  const bool bad = err && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
   for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < n8; v += (long)gridDim.x * blockDim.x) {
     const long i = begin + v * 8;
+    if (bad) {
+      poison8(out + i);
+      continue;
+    }
     float acc[8], x[8];
     ld8(static_cast<const T*>(a.stage[0]) + i, acc);
     for (int r = 1; r < a.world; ++r) {
@@ -72,10 +90,16 @@ __global__ __launch_bounds__(256) void p2p_reduce_kernel(PeerArgs a, T* __restri
 
 // out[i] = stage_{owner(i)}[i]: gather every rank's reduced chunk
 template <typename T>
-__global__ __launch_bounds__(256) void p2p_gather_kernel(PeerArgs a, T* __restrict__ out, long n, long chunk) {
+__global__ __launch_bounds__(256) void p2p_gather_kernel(PeerArgs a, T* __restrict__ out, long n, long chunk,
+                                                        const int* err) {
   const long n8 = n / 8;
+  const bool bad = err && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
   for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < n8; v += (long)gridDim.x * blockDim.x) {
     const long i = v * 8;
+    if (bad) {
+      poison8(out + i);
+      continue;
+    }
     const int owner = (int)min((long)(a.world - 1), i / chunk);
     float x[8];
     ld8(static_cast<const T*>(a.stage[owner]) + i, x);
@@ -133,23 +157,24 @@ PA_EXPORT int pa_p2p_barrier(const void* const* stage, unsigned* const* sig, int
 }
 
 // dtype: 0 fp32, 1 bf16.  [begin, end) in elements, multiples of 8.
+// err: the barrier error flag (device int, may be null): set -> the output is NaN.
 PA_EXPORT int pa_p2p_reduce(int dtype, const void* const* stage, unsigned* const* sig, int world, int rank,
-                            void* out, long begin, long end, hipStream_t st) {
+                            void* out, long begin, long end, const int* err, hipStream_t st) {
   if (world < 1 || world > kMaxPeers || (begin % 8) || (end % 8) || end < begin) return -1;
   PeerArgs a = make_args(stage, sig, world, rank);
   const int g = blocks_for((end - begin) / 8);
-  if (dtype == 0) hipLaunchKernelGGL(p2p_reduce_kernel<float>, dim3(g), dim3(256), 0, st, a, (float*)out, begin, end);
-  else hipLaunchKernelGGL(p2p_reduce_kernel<u16>, dim3(g), dim3(256), 0, st, a, (u16*)out, begin, end);
+  if (dtype == 0) hipLaunchKernelGGL(p2p_reduce_kernel<float>, dim3(g), dim3(256), 0, st, a, (float*)out, begin, end, err);
+  else hipLaunchKernelGGL(p2p_reduce_kernel<u16>, dim3(g), dim3(256), 0, st, a, (u16*)out, begin, end, err);
   return (int)hipGetLastError();
 }
 
 PA_EXPORT int pa_p2p_gather(int dtype, const void* const* stage, unsigned* const* sig, int world, int rank, void* out,
-                            long n, long chunk, hipStream_t st) {
+                            long n, long chunk, const int* err, hipStream_t st) {
   if (world < 1 || world > kMaxPeers || (n % 8) || chunk <= 0 || (chunk % 8)) return -1;
   PeerArgs a = make_args(stage, sig, world, rank);
   const int g = blocks_for(n / 8);
-  if (dtype == 0) hipLaunchKernelGGL(p2p_gather_kernel<float>, dim3(g), dim3(256), 0, st, a, (float*)out, n, chunk);
-  else hipLaunchKernelGGL(p2p_gather_kernel<u16>, dim3(g), dim3(256), 0, st, a, (u16*)out, n, chunk);
+  if (dtype == 0) hipLaunchKernelGGL(p2p_gather_kernel<float>, dim3(g), dim3(256), 0, st, a, (float*)out, n, chunk, err);
+  else hipLaunchKernelGGL(p2p_gather_kernel<u16>, dim3(g), dim3(256), 0, st, a, (u16*)out, n, chunk, err);
   return (int)hipGetLastError();
 }
 

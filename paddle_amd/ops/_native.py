@@ -96,8 +96,8 @@ _SIGS = {
     "pa_p2p_ipc_open": [_P, ctypes.POINTER(_P)],
     "pa_p2p_ipc_close": [_P],
     "pa_p2p_barrier": [_P, _P, _I, _I, ctypes.c_uint, _L, _P, _P],
-    "pa_p2p_reduce": [_I, _P, _P, _I, _I, _P, _L, _L, _P],
-    "pa_p2p_gather": [_I, _P, _P, _I, _I, _P, _L, _L, _P],
+    "pa_p2p_reduce": [_I, _P, _P, _I, _I, _P, _L, _L, _P, _P],
+    "pa_p2p_gather": [_I, _P, _P, _I, _I, _P, _L, _L, _P, _P],
     "pa_p2p_zero": [_P, ctypes.c_size_t],
     "pa_device_count": [ctypes.POINTER(_I)],
     "pa_clear_error": [],

@@ -115,14 +115,17 @@ class DirectAllReduce:
         N.call("pa_p2p_copy", own, N.ptr(t), nbytes, N.stream())
         self._barrier()
         if algo == "one_shot":
-            N.call("pa_p2p_reduce", dt, self._stage, self._sig, self.world, self.rank, N.ptr(t), 0, n, N.stream())
+            N.call("pa_p2p_reduce", dt, self._stage, self._sig, self.world, self.rank, N.ptr(t), 0, n,
+                   N.ptr(self._err), N.stream())
         else:
             chunk = (n + 8 * self.world - 1) // (8 * self.world) * 8
             b, e = min(n, self.rank * chunk), min(n, (self.rank + 1) * chunk)
             if e > b:
-                N.call("pa_p2p_reduce", dt, self._stage, self._sig, self.world, self.rank, own, b, e, N.stream())
+                N.call("pa_p2p_reduce", dt, self._stage, self._sig, self.world, self.rank, own, b, e,
+                       N.ptr(self._err), N.stream())
             self._barrier()
-            N.call("pa_p2p_gather", dt, self._stage, self._sig, self.world, self.rank, N.ptr(t), n, chunk, N.stream())
+            N.call("pa_p2p_gather", dt, self._stage, self._sig, self.world, self.rank, N.ptr(t), n, chunk,
+                   N.ptr(self._err), N.stream())
         self._barrier()  # nobody refills its staging before every peer has read it
         return t
 
@@ -147,7 +150,7 @@ class DirectAllReduce:
         b = self.rank * L
         # the kernel writes out[i] for absolute i in [b, b + L): shift the base
         N.call("pa_p2p_reduce", N.dt(inp), self._stage, self._sig, self.world, self.rank,
-               _P(out.data_ptr() - b * es), b, b + L, N.stream())
+               _P(out.data_ptr() - b * es), b, b + L, N.ptr(self._err), N.stream())
         self._barrier()
         return out
 
@@ -166,7 +169,7 @@ class DirectAllReduce:
         N.call("pa_p2p_copy", _P(self._stage[self.rank] + self.rank * L * es), N.ptr(shard), L * es, N.stream())
         self._barrier()
         N.call("pa_p2p_gather", N.dt(out), self._stage, self._sig, self.world, self.rank, N.ptr(out), n, L,
-               N.stream())
+               N.ptr(self._err), N.stream())
         self._barrier()
         return out
 

@@ -50,6 +50,19 @@ def _worker(rank, world, port, q):
                     exp = sum(torch.randint(-8, 8, (n,), generator=torch.Generator().manual_seed(1000 * n + r))
                               .to(torch.float32) for r in range(world))
                     res.append((str(dtype), n, algo, float((t.float().cpu() - exp).abs().max())))
+        # a raised barrier-error flag (what a timed-out peer leaves behind) poisons
+        # the result with NaN instead of summing stale staging data, and check() raises
+        ar._err.fill_(1)
+        t = torch.ones(4096, device="cuda")
+        ar.all_reduce(t, algo="two_shot")
+        torch.cuda.synchronize()
+        poisoned = bool(torch.isnan(t).all())
+        try:
+            ar.check()
+            raised = False
+        except Exception:
+            raised = True
+        res.append(("poison", int(poisoned), "raised", 0.0 if raised else 1.0))
         ar.close()
         dist.destroy_process_group()
         q.put((rank, res, None))
@@ -78,3 +91,5 @@ def test_direct_allreduce_two_ranks_one_gpu():
     for rank in range(world):
         for dtype, n, algo, err in out[rank]:
             assert err == 0.0, (rank, dtype, n, algo, err)
+            if dtype == "poison":
+                assert n == 1, f"rank {rank}: output not NaN-poisoned after a barrier error"
