@@ -230,7 +230,7 @@ class LoDTensor:
             t = t.float()
         return t.cpu().numpy()
 
-    def __array__(self, dtype=None):
+    def __array__(self, dtype=None, copy=None):
         a = self.numpy()
         return a.astype(dtype) if dtype is not None else a
 

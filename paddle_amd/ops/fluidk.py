@@ -13,6 +13,8 @@ import ctypes
 
 import torch
 
+from ..framework import mixed_vector as _mv
+
 from . import _native as N
 
 ACTS = ["relu", "sigmoid", "logsigmoid", "exp", "tanh", "tanh_shrink", "softshrink", "sqrt", "rsqrt", "abs", "ceil",
@@ -229,7 +231,7 @@ def _check_off(offsets, n):
 def seq_softmax(x, offsets):
     _check_off(offsets, x.numel())
     x = _d(x)
-    off = torch.as_tensor(list(offsets), dtype=torch.int64, device=x.device)
+    off = _mv.device_offsets(offsets, x.device, torch.int64)
     y = torch.empty_like(x)
     N.call("pa_seq_softmax_fwd", N.dt(x), N.ptr(x), N.ptr(off), N.ptr(y), len(offsets) - 1, N.stream())
     return y
@@ -239,7 +241,7 @@ def seq_softmax_grad(y, dy, offsets):
     _check_off(offsets, y.numel())
     _same(y, dy)
     y, dy = _d(y), _d(dy)
-    off = torch.as_tensor(list(offsets), dtype=torch.int64, device=y.device)
+    off = _mv.device_offsets(offsets, y.device, torch.int64)
     dx = torch.empty_like(y)
     N.call("pa_seq_softmax_bwd", N.dt(y), N.ptr(y), N.ptr(dy), N.ptr(off), N.ptr(dx), len(offsets) - 1, N.stream())
     return dx

@@ -15,6 +15,8 @@ import os
 import numpy as np
 import torch
 
+from ..framework import mixed_vector as _mv
+
 from . import _native as N
 from ..autograd import tape as _tape
 
@@ -232,7 +234,7 @@ def seq_pool(x, offsets, pooltype, pad_value=0.0):
     x = x.contiguous()
     nseq = len(offsets) - 1
     D = x.numel() // max(x.shape[0], 1)
-    off = torch.as_tensor(np.asarray(offsets, dtype=np.int32)).to(x.device)
+    off = _mv.device_offsets(offsets, x.device, torch.int32)
     out = torch.empty((nseq,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     maxi = torch.empty((nseq,) + tuple(x.shape[1:]), dtype=torch.int32, device=x.device) if t == 3 else None
     N.call("pa_seq_pool", _DT[x.dtype], N.ptr(x), N.ptr(off), N.ptr(out), N.ptr(maxi), nseq, D, t, float(pad_value),
@@ -247,7 +249,7 @@ def seq_pool_grad(dout, offsets, pooltype, maxi, nrows):
     dout = dout.contiguous()
     nseq = len(offsets) - 1
     D = dout.numel() // max(nseq, 1)
-    off = torch.as_tensor(np.asarray(offsets, dtype=np.int32)).to(dout.device)
+    off = _mv.device_offsets(offsets, dout.device, torch.int32)
     dx = torch.zeros((nrows,) + tuple(dout.shape[1:]), dtype=dout.dtype, device=dout.device)
     N.call("pa_seq_pool_grad", _DT[dout.dtype], N.ptr(dout), N.ptr(off), N.ptr(maxi), N.ptr(dx), nseq, D, t,
            N.stream())
