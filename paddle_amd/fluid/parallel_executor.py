@@ -356,25 +356,52 @@ class ParallelExecutor:
                     live.append((i, n, per))
             if not live:
                 return
-            flat = torch.cat([torch.stack([p.tensor.reshape(-1).float().to(dev0) for p in per]).sum(0)
-                              for _, _, per in live])
+            # one flat fp32 buffer per replica (one concat on its own device), replicas
+            # sharing a device summed in place, then ONE cross-device reduction
+            # (torch.cuda.comm.reduce_add: RCCL between the GPUs of this process)
+            # instead of a copy of every parameter's gradient to device 0
+            by_dev = {}
+            for r in range(len(self._local_scopes)):
+                parts = [per[r].tensor.reshape(-1) for _, _, per in live]
+                # a fresh fp32 buffer (never a view of the replica's gradient: summed in place)
+                f = torch.cat(parts).float() if len(parts) > 1 else parts[0].to(torch.float32, copy=True)
+                d = f.device
+                if d in by_dev:
+                    by_dev[d].add_(f)
+                else:
+                    by_dev[d] = f
+            if len(by_dev) == 1:
+                flat = next(iter(by_dev.values())).to(dev0)
+            else:
+                devs = sorted(by_dev, key=lambda d: (d != dev0, d.index))
+                flat = torch.cuda.comm.reduce_add([by_dev[d] for d in devs], destination=dev0.index)
             if self._world > 1:
                 self._cross_process_all_reduce(flat)
             sc_ = self._scale()
             if sc_ != 1.0:
                 flat.mul_(sc_)
+            # the reduced buffer goes to every device once (broadcast), replicas take views
+            rdevs = [self._device(r) for r in range(len(self._local_scopes))]
+            udevs = sorted(set(rdevs), key=lambda d: (d != dev0, d.index if d.index is not None else -1))
+            if cuda and len(udevs) > 1:
+                copies = dict(zip(udevs, torch.cuda.comm.broadcast(flat, devices=[d.index for d in udevs])))
+            else:
+                copies = {d: flat if d == flat.device else flat.to(d) for d in udevs}
             off = 0
             reduce_mode = self._build_strategy.reduce_strategy == BuildStrategy.ReduceStrategy.Reduce
             for i, n, per in live:
                 t0 = per[0].tensor
                 cnt = t0.numel()
-                seg = flat[off:off + cnt].view(t0.shape).to(t0.dtype)
-                off += cnt
                 pname = self._param_grads[i][0]
+                segs = {}
                 for r, sc in enumerate(self._local_scopes):
                     if reduce_mode and len(self._places) > 1 and r != self._owners.get(pname, 0):
                         continue
-                    sc.var(n).set(core.LoDTensor(seg if r == 0 else seg.to(self._device(r)), per[0].lod()))
+                    d = rdevs[r]
+                    if d not in segs:
+                        segs[d] = copies[d][off:off + cnt].view(t0.shape).to(t0.dtype)
+                    sc.var(n).set(core.LoDTensor(segs[d], per[0].lod()))
+                off += cnt
 
     def _cross_process_all_reduce(self, flat):
         """Sum over trainer processes: RCCL, or under ``FLAGS_dp_comm=direct`` the
