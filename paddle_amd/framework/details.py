@@ -123,5 +123,8 @@ class StreamSet:
     def comm(self, dev):
         s = self._comm.get(dev)
         if s is None:
-            s = self._comm[dev] = torch.cuda.Stream(device=dev)
+            from ..platform import device_context
+
+            dc = device_context(dev)  # the device context's high-priority comm stream
+            s = self._comm[dev] = dc.comm_stream if dc is not None else torch.cuda.Stream(device=dev)
         return s

@@ -153,7 +153,11 @@ class FlatShardedOptimizer:
         self.v = torch.zeros(so, dtype=torch.float32, device=dev)
         # --- overlap machinery
         self.overlap = overlap and self.W > 1 and dev.type == "cuda"
-        self.comm_stream = torch.cuda.Stream(device=dev) if self.overlap else None
+        from ..platform import device_context
+
+        dc = device_context(dev) if dev.type == "cuda" else None
+        self.comm_stream = ((dc.comm_stream if dc is not None else torch.cuda.Stream(device=dev))
+                            if self.overlap else None)
         self._ready = [0] * len(buckets)
         self._launched = [False] * len(buckets)
         self._sync = True
@@ -166,7 +170,8 @@ class FlatShardedOptimizer:
         if overlap_update is None:
             overlap_update = os.environ.get("FLAGS_overlap_optimizer", "1") != "0"
         self.overlap_update = bool(overlap_update) and self.W == 1 and dev.type == "cuda"
-        self.opt_stream = torch.cuda.Stream(device=dev) if self.overlap_update else None
+        self.opt_stream = ((dc.aux_stream if dc is not None else torch.cuda.Stream(device=dev))
+                           if self.overlap_update else None)
         self._keep = None
         # FLAGS_dp_comm=direct: reduce-scatter / all-gather over IPC-mapped peer
         # buffers on the xGMI links (parallel/direct.py) instead of RCCL

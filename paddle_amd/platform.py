@@ -10,7 +10,13 @@ throughout the C++ core).
 * ``init_p2p(devices)`` enables peer access between every pair of the node's GPUs
   that supports it (xGMI), ``memcpy_peer(dst, src)`` copies across devices without
   staging through the host;
-* ``device_memory_info(dev)`` / ``memory_stats(dev)``.
+* ``device_memory_info(dev)`` / ``memory_stats(dev)``;
+* ``DeviceContextPool.instance().get(place)`` -> ``DeviceContext`` (reference
+  platform/device_context.h:39-179): per HIP device a compute, a high-priority
+  communication and an auxiliary stream plus an event pool, owned by the native
+  runtime (csrc/runtime/device_context.cc) and exposed to torch as external
+  streams; the ParallelExecutor's and the sharded optimizer's collective streams
+  and the overlapped optimizer update run on them.
 """
 from __future__ import annotations
 
@@ -122,3 +128,91 @@ def log_memory(tag, dev=0):
         vlog(0 if os.environ.get("FLAGS_log_memory_stats") == "1" else 1,
              f"memory[{tag}] " + " ".join(f"{k}={v / 2**30:.2f}GiB" if isinstance(v, int) else f"{k}={v}"
                                           for k, v in st.items()))
+
+
+# ------------------------------------------------------------------ device contexts
+class DeviceContext:
+    """One HIP device's streams (compute / comm / aux) and event pool."""
+
+    COMPUTE, COMM, AUX = 0, 1, 2
+
+    def __init__(self, device):
+        from . import runtime
+
+        self._rt = runtime.lib()
+        self.device = torch.device("cuda", int(device))
+        self._h = self._rt.pa_dc_get(int(self.device.index))
+        if not self._h:
+            raise RuntimeError(runtime._err())
+        self._streams = {}
+
+    def _stream(self, which):
+        s = self._streams.get(which)
+        if s is None:
+            ptr = self._rt.pa_dc_stream(self._h, which)
+            s = self._streams[which] = torch.cuda.ExternalStream(ptr, device=self.device)
+        return s
+
+    @property
+    def stream(self):
+        return self._stream(self.COMPUTE)
+
+    @property
+    def comm_stream(self):
+        return self._stream(self.COMM)
+
+    @property
+    def aux_stream(self):
+        return self._stream(self.AUX)
+
+    def stream_wait(self, waiter, other):
+        """``waiter`` stream waits on the device for the work queued on ``other``."""
+        if self._rt.pa_dc_stream_wait(self._h, int(waiter), int(other)) != 0:
+            raise RuntimeError("DeviceContext.stream_wait failed")
+
+    def wait(self):
+        """DeviceContext::Wait: block the host until every stream drained."""
+        if self._rt.pa_dc_wait(self._h) != 0:
+            raise RuntimeError("DeviceContext.wait failed")
+
+    def event_pool_stats(self):
+        return {"created": int(self._rt.pa_dc_events_created(self._h)),
+                "pooled": int(self._rt.pa_dc_events_pooled(self._h))}
+
+
+class DeviceContextPool:
+    """Per-place device contexts (DeviceContextPool::Get); CPU places have none."""
+
+    _inst = None
+
+    def __init__(self):
+        self._ctx = {}
+
+    @classmethod
+    def instance(cls):
+        if cls._inst is None:
+            cls._inst = cls()
+        return cls._inst
+
+    def get(self, place):
+        if isinstance(place, torch.device):
+            dev = place
+        elif hasattr(place, "torch_device"):
+            dev = place.torch_device()
+        else:
+            dev = torch.device(place)
+        if dev.type != "cuda":
+            return None
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        c = self._ctx.get(idx)
+        if c is None:
+            c = self._ctx[idx] = DeviceContext(idx)
+        return c
+
+
+def device_context(place):
+    """The DeviceContext of ``place`` (None for CPU, or without the runtime library)."""
+    try:
+        return DeviceContextPool.instance().get(place)
+    except (OSError, RuntimeError):
+        return None

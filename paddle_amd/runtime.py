@@ -50,6 +50,15 @@ _SIGS = {
     "pa_bq_close": ([P], None),
     "pa_bq_destroy": ([P], None),
     "pa_rt_free": ([P], None),
+    "pa_dc_get": ([I], P),
+    "pa_dc_stream": ([P, I], P),
+    "pa_dc_device": ([P], I),
+    "pa_dc_event_acquire": ([P], P),
+    "pa_dc_event_release": ([P, P], None),
+    "pa_dc_stream_wait": ([P, I, I], I),
+    "pa_dc_wait": ([P], I),
+    "pa_dc_events_created": ([P], ctypes.c_long),
+    "pa_dc_events_pooled": ([P], ctypes.c_long),
     "pa_dbr_create": ([I, SZ, I], P),
     "pa_dbr_push": ([P, I, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64)], I),
     "pa_dbr_close": ([P], None),
