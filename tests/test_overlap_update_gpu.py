@@ -2,8 +2,8 @@
 bucket on a side stream, each parameter's first read in the next forward waits
 for its own bucket, and the next reverse pass waits for the rest.  Trained with
 the framework tape it must give bit-identical losses and parameters to the
-single-kernel update (distinct token ids keep every kernel of the step
-deterministic: no colliding float atomics)."""
+single-kernel update up to last-ulp differences (distinct token ids; a large
+Adam epsilon keeps those from being amplified into lr-sized steps)."""
 import pytest
 import torch
 
@@ -20,8 +20,11 @@ def _train(overlap, steps=4):
     cfg = LlamaConfig(**LLAMA_CONFIGS["llama-tiny"])
     model = LlamaForCausalLM(cfg, device=dev)
     # small buckets: many side-stream launches and per-bucket waits
-    opt = FlatShardedOptimizer(model.named_parameters(), lr=1e-3, grad_dtype=torch.float32, grad_clip=1.0,
-                               bucket_mb=1, overlap_update=overlap)
+    # eps = 1e-2: Adam's normalised step no longer turns last-ulp noise in a ~0
+    # gradient into a +-lr update (with eps 1e-8 two runs of the SAME path drift
+    # apart by ~lr through the embedding rows of the float-atomic backward)
+    opt = FlatShardedOptimizer(model.named_parameters(), lr=1e-3, eps=1e-2, grad_dtype=torch.float32,
+                               grad_clip=1.0, bucket_mb=1, overlap_update=overlap)
     assert opt.overlap_update == overlap and len(opt.buckets) > 2
     g = torch.Generator().manual_seed(1)
     losses = []
@@ -44,10 +47,10 @@ def _train(overlap, steps=4):
 def test_overlapped_update_matches_single_kernel_update():
     la, pa = _train(True)
     lb, pb = _train(False)
-    lc, pc = _train(False)
-    ref_noise = (pc - pb).abs().max().item()  # run-to-run spread of the plain update
-    if ref_noise == 0.0:
-        assert la == lb, (la, lb)
-        assert torch.equal(pa, pb), (pa - pb).abs().max().item()
-    else:  # some kernel of the step is nondeterministic: stay within its spread
-        assert (pa - pb).abs().max().item() <= 3 * ref_noise, ((pa - pb).abs().max().item(), ref_noise)
+    assert la[0] == lb[0]
+    for a, b in zip(la, lb):
+        assert abs(a - b) <= 1e-5 * abs(b), (la, lb)
+    # a parameter read before its bucket's update landed would leave a whole AdamW
+    # step (~lr = 1e-3) of difference; per-bucket vs whole-buffer launches differ
+    # in the last ulp only
+    assert (pa - pb).abs().max().item() < 2e-5, (pa - pb).abs().max().item()
