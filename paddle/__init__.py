@@ -14,6 +14,7 @@ from paddle_amd import dataset  # noqa: F401
 from paddle_amd import dygraph  # noqa: F401
 from paddle_amd import v2  # noqa: F401
 from paddle_amd import trainer_config_helpers  # noqa: F401
+from paddle_amd import trainer  # noqa: F401
 from paddle_amd.reader import batch  # noqa: F401
 from paddle_amd.checkpoint import load, save  # noqa: F401
 from paddle_amd.hapi import Model  # noqa: F401
@@ -27,7 +28,8 @@ __version__ = _pa.__version__
 for _name, _mod in (("fluid", fluid), ("reader", reader), ("dataset", dataset), ("nn", nn),
                     ("optimizer", optimizer), ("io", io), ("amp", amp), ("metric", metric), ("vision", vision),
                     ("distributed", distributed), ("static", fluid), ("dygraph", dygraph),
-                    ("v2", v2), ("trainer_config_helpers", trainer_config_helpers)):
+                    ("v2", v2), ("trainer_config_helpers", trainer_config_helpers),
+                    ("trainer", trainer), ("trainer.PyDataProvider2", trainer.PyDataProvider2)):
     _sys.modules[__name__ + "." + _name] = _mod
 for _k, _v in list(_sys.modules.items()):
     for _src, _dst in (("paddle_amd.fluid.", "paddle.fluid."), ("paddle_amd.nn.", "paddle.nn."),

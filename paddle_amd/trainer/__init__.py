@@ -1,0 +1,136 @@
+"""The v1 trainer front end (reference paddle/legacy/trainer: TrainerMain.cpp:32
+``paddle_trainer --config=... --job=train|test|time|checkgrad``, Trainer.cpp:265
+train / :496 trainOnePass / :406 trainOneDataBatch) and the PyDataProvider2 bridge
+(python/paddle/trainer/PyDataProvider2.py ``@provider``,
+trainer_config_helpers/data_sources.py:158 ``define_py_data_sources2``).
+
+The legacy C++ GradientMachine is replaced by the v1 DSL -> Fluid program path of
+``paddle_amd.trainer_config_helpers``: ``python -m paddle_amd.trainer --config
+conf.py`` parses the config, imports the data provider module it names, feeds the
+files of its train / test lists through the ``@provider`` generator, batches them
+with the config's ``settings(batch_size=...)`` and trains with the v2 trainer
+(periodic cost logging, per-pass test, parameter tars per pass under
+``--save_dir``).
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import os
+import random
+import sys
+import time
+
+from . import PyDataProvider2  # noqa: F401
+from .PyDataProvider2 import provider  # noqa: F401
+
+
+def _file_list(path):
+    if not path:
+        return []
+    base = os.path.dirname(os.path.abspath(path))
+    out = []
+    with open(path) as f:
+        for line in f:
+            line = line.strip()
+            if line:
+                out.append(line if os.path.isabs(line) else os.path.join(base, line))
+    return out
+
+
+def _reader(source, which, batch_size, shuffle_seed=None):
+    """A v2 batch reader over one data source of the config (train or test)."""
+    if source is None:
+        return None
+    mod_name, obj_name, args = source["module"], source["obj"], source.get("args") or {}
+    files = _file_list(source["train_list" if which == "train" else "test_list"])
+    if not files:
+        return None
+    mod = importlib.import_module(mod_name)
+    prov = getattr(mod, obj_name)
+
+    def read():
+        settings = prov.make_settings(args, is_train=(which == "train"))
+        order = list(files)
+        if which == "train" and prov.should_shuffle and shuffle_seed is not None:
+            random.Random(shuffle_seed).shuffle(order)
+        batch = []
+        for fn in order:
+            for sample in prov.samples(settings, fn):
+                batch.append(sample)
+                if len(batch) == batch_size:
+                    yield batch
+                    batch = []
+        if batch:
+            yield batch
+
+    return read, prov
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(prog="paddle_trainer", description="v1 trainer front end on the Fluid engine")
+    ap.add_argument("--config", required=True)
+    ap.add_argument("--config_args", default="")
+    ap.add_argument("--job", default="train", choices=["train", "test", "time"])
+    ap.add_argument("--num_passes", type=int, default=1)
+    ap.add_argument("--log_period", type=int, default=100)
+    ap.add_argument("--save_dir", default="")
+    ap.add_argument("--init_model_path", default="")
+    ap.add_argument("--use_gpu", type=int, default=0)
+    ap.add_argument("--trainer_count", type=int, default=1)
+    ap.add_argument("--test_period", type=int, default=0, help="0: test at the end of every pass")
+    ap.add_argument("--seed", type=int, default=1)
+    a = ap.parse_args(argv)
+
+    from .. import v2
+    from .. import trainer_config_helpers as tch
+
+    v2._core.STATE["use_gpu"] = bool(a.use_gpu)
+    conf = tch.parse_config(a.config, a.config_args)
+    src = tch._CFG.get("data_sources")
+    bs = conf.batch_size or 1
+    train = _reader(src, "train", bs, shuffle_seed=a.seed)
+    test = _reader(src, "test", bs)
+    if train is None and a.job in ("train", "time"):
+        raise SystemExit("the config defines no training data (define_py_data_sources2 train_list)")
+    prov = (train or test)[1]
+    feeding = prov.feeding(conf.input_layer_names)
+    trainer, params = conf.make_trainer()
+    if a.init_model_path:
+        with open(a.init_model_path, "rb") as f:
+            params.init_from_tar(f)
+    log = []
+
+    def handler(e):
+        name = type(e).__name__
+        if name == "EndIteration" and (e.batch_id + 1) % a.log_period == 0:
+            print(f"Pass {e.pass_id}, Batch {e.batch_id + 1}, Cost {e.cost:.6f}, {e.metrics}", flush=True)
+        if name == "EndIteration":
+            log.append(e.cost)
+        if name == "EndPass":
+            msg = f"Pass {e.pass_id} done, {e.metrics}"
+            if test is not None:
+                r = trainer.test(reader=test[0], feeding=feeding)
+                msg += f"; Test cost {r.cost:.6f}, {r.metrics}"
+            print(msg, flush=True)
+            if a.save_dir:
+                d = os.path.join(a.save_dir, f"pass-{e.pass_id:05d}")
+                os.makedirs(d, exist_ok=True)
+                with open(os.path.join(d, "params.tar"), "wb") as f:
+                    params.to_tar(f)
+
+    if a.job == "train":
+        trainer.train(reader=train[0], num_passes=a.num_passes, event_handler=handler, feeding=feeding)
+    elif a.job == "test":
+        r = trainer.test(reader=(test or train)[0], feeding=feeding)
+        print(f"Test cost {r.cost:.6f}, {r.metrics}", flush=True)
+    else:  # time: throughput of the training step over one pass
+        t0 = time.perf_counter()
+        trainer.train(reader=train[0], num_passes=1, event_handler=handler, feeding=feeding)
+        dt = time.perf_counter() - t0
+        print(f"time: {len(log)} batches in {dt:.3f} s, {len(log) * bs / max(dt, 1e-9):.1f} samples/s", flush=True)
+    return log
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

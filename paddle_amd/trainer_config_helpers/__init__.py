@@ -120,6 +120,13 @@ def settings(batch_size, learning_rate=1e-3, learning_method=None, regularizatio
                 gradient_clipping_threshold=gradient_clipping_threshold, extra=kw)
 
 
+def define_py_data_sources2(train_list, test_list, module, obj, args=None):
+    """data_sources.py:158: the train / test file lists and the PyDataProvider2
+    provider ``module.obj`` (``paddle_amd.trainer`` reads them)."""
+    _CFG["data_sources"] = {"train_list": train_list, "test_list": test_list, "module": module, "obj": obj,
+                            "args": args}
+
+
 def outputs(*layers):
     out = []
     for x in layers:
