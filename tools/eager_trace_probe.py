@@ -1,0 +1,47 @@
+"""Kernels of one DyGraph ResNet-18 NHWC bf16 training step on the eager engine,
+recorded in-process by the rocprofiler-sdk tracer (FLAGS_device_tracer=1)."""
+import json
+import os
+import sys
+
+os.environ["FLAGS_device_tracer"] = "1"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import paddle  # noqa: E402
+import paddle.nn.functional as F  # noqa: E402
+from paddle_amd.utils import device_tracer as dt  # noqa: E402
+from paddle_amd.utils import profiler as P  # noqa: E402
+
+assert dt.available(), dt.error()
+paddle.seed(0)
+paddle.set_device("gpu")
+model = paddle.vision.models.resnet18(num_classes=10, data_format="NHWC")
+model.to(device="cuda", dtype=torch.bfloat16)
+opt = paddle.optimizer.Momentum(learning_rate=0.05, momentum=0.9, parameters=model.parameters())
+x = paddle.randn([8, 32, 32, 3]).astype("bfloat16")
+y = paddle.to_tensor(np.arange(8) % 10)
+
+
+def step():
+    loss = F.cross_entropy(model(x).astype("float32"), y)
+    loss.backward()
+    opt.step()
+    opt.clear_grad()
+    return loss
+
+
+step()
+torch.cuda.synchronize()
+P.start("All")
+with P.RecordEvent("train_step"):
+    step()
+recs = P.kernel_records()
+P.stop(profile_path=None)
+aten = {}
+for r in recs:
+    if "at::native" in r["name"]:
+        k = r["name"][:140]
+        aten[k] = aten.get(k, 0) + 1
+print(json.dumps({"kernels": len(recs), "aten_kernels": sum(aten.values()), "aten": aten}, indent=1))
