@@ -95,6 +95,13 @@ def disable():
         _load().pa_tracer_disable()
 
 
+def flush():
+    """Drain the buffered records of kernels that have completed so far (recording
+    continues)."""
+    if available():
+        _load().pa_tracer_flush()
+
+
 def now_ns() -> int:
     return int(_load().pa_tracer_now_ns())
 

@@ -117,8 +117,13 @@ def reset():
 
 
 def kernel_records():
-    """The in-process kernel records of the window (empty without the tracer)."""
-    if not _state.get("tracer_used"):
+    """The in-process kernel records of the window (empty without the tracer).
+    Inside an open window the device is synchronised and the buffer flushed first."""
+    if _state.get("tracer"):
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        _tracer().flush()
+    elif not _state.get("tracer_used"):
         return []
     recs = _tracer().records()
     for r in recs:

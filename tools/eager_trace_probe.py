@@ -37,11 +37,17 @@ torch.cuda.synchronize()
 P.start("All")
 with P.RecordEvent("train_step"):
     step()
-recs = P.kernel_records()
 P.stop(profile_path=None)
-aten = {}
+recs = P.kernel_records()
+aten, ours = {}, {}
+t_aten = t_all = 0
 for r in recs:
+    t_all += r["dur_ns"]
+    k = r["name"][:140]
     if "at::native" in r["name"]:
-        k = r["name"][:140]
         aten[k] = aten.get(k, 0) + 1
-print(json.dumps({"kernels": len(recs), "aten_kernels": sum(aten.values()), "aten": aten}, indent=1))
+        t_aten += r["dur_ns"]
+    else:
+        ours[k] = ours.get(k, 0) + 1
+print(json.dumps({"kernels": len(recs), "aten_kernels": sum(aten.values()), "aten_time_frac": t_aten / max(t_all, 1),
+                  "aten": aten, "other": ours}, indent=1))
