@@ -65,23 +65,28 @@ __global__ void adamw_kernel(float* __restrict__ p, const TG* __restrict__ g, fl
   }
 }
 
-// Momentum (optionally Nesterov) and plain SGD, fp32 params.
-template <typename TG>
-__global__ void momentum_kernel(float* __restrict__ p, const TG* __restrict__ g,
+// Momentum (optionally Nesterov) and plain SGD; fp32 velocity, parameters fp32 or
+// bf16 updated in place (bf16: read, fp32 update, one rounding on the store -- no
+// fp32 staging copy of a bf16 model).
+template <typename TG, typename TP>
+__global__ void momentum_kernel(TP* __restrict__ p, const TG* __restrict__ g,
                                 float* __restrict__ vel, long n, float lr,
                                 const float* __restrict__ lr_ptr, float mu, int nesterov, float wd,
                                 float gscale) {
   const float lr_ = lr_ptr ? lr_ptr[0] : lr;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long)gridDim.x * blockDim.x) {
-    const float gg = IO<TG>::ld(g, i) * gscale + wd * p[i];
+    const float pi = IO<TP>::ld(p, i);
+    const float gg = IO<TG>::ld(g, i) * gscale + wd * pi;
+    float po;
     if (vel) {
       const float v = mu * vel[i] + gg;
       vel[i] = v;
-      p[i] -= nesterov ? lr_ * (gg + mu * v) : lr_ * v;
+      po = pi - (nesterov ? lr_ * (gg + mu * v) : lr_ * v);
     } else {
-      p[i] -= lr_ * gg;
+      po = pi - lr_ * gg;
     }
+    IO<TP>::st(p, i, po);
   }
 }
 
@@ -132,9 +137,23 @@ PA_EXPORT int pa_momentum(int gdtype, float* p, const void* g, float* vel, long 
   if (n == 0) return 0;
   const int grid = stream_grid(n, 256);
   if (gdtype == 1)
-    hipLaunchKernelGGL(momentum_kernel<u16>, dim3(grid), dim3(256), 0, st, p, (const u16*)g, vel, n, lr, lr_ptr, mu, nesterov, wd, gscale);
+    hipLaunchKernelGGL((momentum_kernel<u16, float>), dim3(grid), dim3(256), 0, st, p, (const u16*)g, vel, n, lr, lr_ptr, mu, nesterov, wd, gscale);
   else
-    hipLaunchKernelGGL(momentum_kernel<float>, dim3(grid), dim3(256), 0, st, p, (const float*)g, vel, n, lr, lr_ptr, mu, nesterov, wd, gscale);
+    hipLaunchKernelGGL((momentum_kernel<float, float>), dim3(grid), dim3(256), 0, st, p, (const float*)g, vel, n, lr, lr_ptr, mu, nesterov, wd, gscale);
+  PA_LAUNCH_CHECK();
+}
+
+// pdtype: 0 fp32, 1 bf16 parameters (updated in place)
+PA_EXPORT int pa_momentum_p(int gdtype, int pdtype, void* p, const void* g, float* vel, long n, float lr,
+                            const float* lr_ptr, float mu, int nesterov, float wd, float gscale,
+                            hipStream_t st) {
+  if (n == 0) return 0;
+  const int grid = stream_grid(n, 256);
+#define PA_M(TG, TP) \
+  hipLaunchKernelGGL((momentum_kernel<TG, TP>), dim3(grid), dim3(256), 0, st, (TP*)p, (const TG*)g, vel, n, lr, lr_ptr, mu, nesterov, wd, gscale)
+  if (gdtype == 1) { if (pdtype == 1) PA_M(u16, u16); else PA_M(u16, float); }
+  else { if (pdtype == 1) PA_M(float, u16); else PA_M(float, float); }
+#undef PA_M
   PA_LAUNCH_CHECK();
 }
 

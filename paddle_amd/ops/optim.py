@@ -59,16 +59,20 @@ def momentum_flat(param, grad, velocity=None, *, lr, mu=0.9, nesterov=False, wei
     n = param.numel()
     if param.is_cuda:
         _fused.bump_weight_epoch()
-        N.call("pa_momentum", N.dt(grad), N.ptr(param), N.ptr(grad), N.ptr(velocity), n, float(lr),
-               N.ptr(lr_tensor), float(mu), int(nesterov), float(weight_decay), float(grad_scale), N.stream())
+        if param.dtype not in (torch.float32, torch.bfloat16) or not param.is_contiguous():
+            raise TypeError(f"momentum_flat: contiguous fp32 / bf16 parameter required, got {param.dtype}")
+        N.call("pa_momentum_p", N.dt(grad), N.dt(param), N.ptr(param), N.ptr(grad), N.ptr(velocity), n,
+               float(lr), N.ptr(lr_tensor), float(mu), int(nesterov), float(weight_decay), float(grad_scale),
+               N.stream())
         return param
     lr_ = float(lr_tensor.reshape(-1)[0]) if lr_tensor is not None else lr
-    g = grad.float() * grad_scale + weight_decay * param
+    pf = param.float()
+    g = grad.float() * grad_scale + weight_decay * pf
     if velocity is None:
-        param.sub_(lr_ * g)
+        param.copy_(pf - lr_ * g)
         return param
     velocity.mul_(mu).add_(g)
-    param.sub_(lr_ * (g + mu * velocity) if nesterov else lr_ * velocity)
+    param.copy_(pf - (lr_ * (g + mu * velocity) if nesterov else lr_ * velocity))
     return param
 
 

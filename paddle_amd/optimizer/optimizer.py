@@ -208,7 +208,9 @@ class Momentum(Optimizer):
         vel = self._acc("velocity", p)
         m = self._master_of(p)
         tgt = m if m is not None else p
-        if tgt.is_cuda and tgt.dtype == torch.float32 and tgt.is_contiguous() and g.is_contiguous():
+        if (tgt.is_cuda and tgt.dtype in (torch.float32, torch.bfloat16) and tgt.is_contiguous()
+                and g.is_contiguous() and g.dtype in (torch.float32, torch.bfloat16)):
+            # bf16 parameters (no master copy) update in place in the same pass
             fused_optim.momentum_flat(tgt.view(-1), g.reshape(-1), vel.view(-1), lr=lr, mu=self._momentum,
                                       nesterov=self._nesterov, grad_scale=self._rescale)
         else:
