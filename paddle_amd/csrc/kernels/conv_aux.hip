@@ -394,9 +394,39 @@ __global__ void gap_bwd_kernel(const u16* __restrict__ dy, u16* __restrict__ dx,
   }
 }
 
+// Running-statistics update for running mean / var kept in another dtype than the
+// fp32 the finalize kernel updates (a bf16-cast model): var recovered from rstd, one
+// launch for all channels instead of a chain of elementwise ops per statistic.
+template <typename T>
+__global__ void bn_running_kernel(T* __restrict__ rm, T* __restrict__ rv, const float* __restrict__ mean,
+                                  const float* __restrict__ rstd, int C, long rows, float eps, float momentum) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double r = rstd[c];
+  const double var = 1.0 / (r * r) - (double)eps;
+  const double n = (double)rows;
+  const double unb = rows > 1 ? var * n / (n - 1.0) : var;
+  IO<T>::st(rm, c, (float)(momentum * (double)IO<T>::ld(rm, c) + (1.0 - momentum) * (double)mean[c]));
+  IO<T>::st(rv, c, (float)(momentum * (double)IO<T>::ld(rv, c) + (1.0 - momentum) * unb));
+}
+
 }  // namespace pa
 
 using namespace pa;
+
+// dt: 0 fp32, 1 bf16 running statistics
+PA_EXPORT int pa_bn_running_update(int dt, void* rm, void* rv, const float* mean, const float* rstd, int C, long rows,
+                                   float eps, float momentum, hipStream_t st) {
+  if (C <= 0) return 0;
+  const int grid = (C + 255) / 256;
+  if (dt == 1)
+    hipLaunchKernelGGL(bn_running_kernel<u16>, dim3(grid), dim3(256), 0, st, (u16*)rm, (u16*)rv, mean, rstd, C, rows,
+                       eps, momentum);
+  else
+    hipLaunchKernelGGL(bn_running_kernel<float>, dim3(grid), dim3(256), 0, st, (float*)rm, (float*)rv, mean, rstd, C,
+                       rows, eps, momentum);
+  PA_LAUNCH_CHECK();
+}
 
 // C < 8 (image stems): compile-time C; a thread writes 8 consecutive columns of
 // one row (one 16-byte store) and walks (kh, kw, c) incrementally, no divisions.

@@ -57,6 +57,7 @@ _SIGS = {
     "pa_softmax_bwd": [_I, _P, _P, _P, _L, _I, _I, _P],
     "pa_adamw": [_I, _I, _P, _P, _P, _P, _P, _L, _F, _P, _F, _F, _F, _F, _F, _F, _P, _P, _L, _F, _P, _I, _P],
     "pa_momentum": [_I, _P, _P, _P, _L, _F, _P, _F, _I, _F, _F, _P],
+    "pa_bn_running_update": [_I, _P, _P, _P, _P, _I, _L, _F, _F, _P],
     "pa_momentum_p": [_I, _I, _P, _P, _P, _L, _F, _P, _F, _I, _F, _F, _P],
     "pa_sumsq": [_I, _P, _L, _P, _P],
     "pa_transpose2d": [_I, _P, _P, _I, _I, _L, _L, _I, _L, _L, _P],

@@ -246,7 +246,12 @@ class _BatchNormNHWC(torch.autograd.Function):
         _nat.call("pa_bn_fwd_train", _nat.ptr(x), _nat.ptr(y), _nat.ptr(wc), _nat.ptr(bc), wdt, _nat.ptr(rm),
                   _nat.ptr(rv), _nat.ptr(mean), _nat.ptr(rstd), _nat.ptr(part), rows, C, float(eps),
                   float(momentum), int(relu), _nat.ptr(res), _nat.stream())
-        if run_mean is not None and rm is None:  # running stats kept in another dtype: update on the side
+        if (run_mean is not None and rm is None and run_mean.dtype == torch.bfloat16 and run_var is not None
+                and run_var.dtype == torch.bfloat16 and run_mean.is_contiguous() and run_var.is_contiguous()):
+            # bf16 running stats (a bf16-cast model): one native update launch
+            _nat.call("pa_bn_running_update", 1, _nat.ptr(run_mean), _nat.ptr(run_var), _nat.ptr(mean),
+                      _nat.ptr(rstd), C, rows, float(eps), float(momentum), _nat.stream())
+        elif run_mean is not None and rm is None:  # running stats kept in another dtype: update on the side
             with torch.no_grad():
                 var = 1.0 / (rstd.double() ** 2) - eps
                 unb = var * rows / max(rows - 1, 1)

@@ -44,3 +44,25 @@ def test_dygraph_momentum_bf16_model_uses_native_update():
     # first step: v = g, p -= lr * g
     want = (ref - 0.1 * w.grad.float()).to(torch.bfloat16)
     torch.testing.assert_close(w.detach().float(), want.float(), rtol=2 ** -7, atol=1e-6)
+
+
+def test_bn_bf16_running_stats_native_update():
+    """BatchNorm of a bf16-cast model keeps bf16 running statistics: they are updated
+    by one native launch (conv_aux.hip pa_bn_running_update) from the batch mean /
+    rstd; checked against the fp32 formula (unbiased variance, momentum blend)."""
+    from paddle_amd.ops import conv as CV
+
+    torch.manual_seed(0)
+    N_, H, W, C = 4, 5, 6, 32
+    x = (torch.randn(N_, H, W, C, device="cuda") * 2 + 0.5).to(torch.bfloat16)
+    w = torch.rand(C, device="cuda") + 0.5
+    b = torch.randn(C, device="cuda")
+    rm = torch.randn(C, device="cuda").to(torch.bfloat16)
+    rv = (torch.rand(C, device="cuda") + 0.5).to(torch.bfloat16)
+    rm0, rv0 = rm.float().clone(), rv.float().clone()
+    CV._BatchNormNHWC.apply(x, w, b, rm, rv, 0.9, 1e-5, False, None)
+    torch.cuda.synchronize()
+    xf = x.float().reshape(-1, C)
+    mean, var_unb = xf.mean(0), xf.var(0, unbiased=True)
+    torch.testing.assert_close(rm.float(), (0.9 * rm0 + 0.1 * mean).to(torch.bfloat16).float(), rtol=2 ** -7, atol=1e-3)
+    torch.testing.assert_close(rv.float(), (0.9 * rv0 + 0.1 * var_unb).to(torch.bfloat16).float(), rtol=2 ** -6, atol=1e-3)
