@@ -129,6 +129,7 @@ def main():
     opt = FlatShardedOptimizer(model.named_parameters(), lr=3e-4, betas=(0.9, 0.95), eps=1e-8,
                                weight_decay=0.1, grad_clip=1.0, bucket_mb=args.bucket_mb,
                                overlap=not args.no_overlap, overlap_allgather=not args.no_overlap,
+                               overlap_update=cuda and not args.no_overlap,
                                grad_dtype=None if args.bf16_grads else torch.float32)
     nparams = sum(p.numel() for p in model.parameters())
     from paddle_amd import platform as _plat

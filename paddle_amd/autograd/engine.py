@@ -31,6 +31,8 @@ import threading
 import torch
 from torch._C import DisableTorchFunctionSubclass
 
+from ..utils import strict as _strict
+
 _TLS = threading.local()
 FALLBACK_OPS: dict = {}      # op name -> count of fallback nodes recorded
 _RULES: dict = {}             # torch callable -> rule(out, *args, **kwargs) -> (inputs, backward)
@@ -199,6 +201,15 @@ class Tensor(torch.Tensor):
     @classmethod
     def __torch_function__(cls, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}
+        if _strict.watching():
+            # framework region: covered ATen ops run on the HIP kernels
+            # (ops/aten_native.py); the rest are counted / refused in strict mode
+            with _strict.region("eager:" + _fname(func)):
+                return cls._torch_function_impl(func, args, kwargs)
+        return cls._torch_function_impl(func, args, kwargs)
+
+    @classmethod
+    def _torch_function_impl(cls, func, args, kwargs):
         with DisableTorchFunctionSubclass():
             if func in _PASS:
                 return func(*args, **kwargs)
@@ -432,6 +443,16 @@ def add_grad_ready_hook(p, fn):
 
 
 def _backward(roots, grads, retain_graph):
+    from . import tape as _tape
+
+    _tape.run_before_backward()  # e.g. an optimizer update still running on a side stream
+    if _strict.watching():
+        with _strict.region("eager:backward"):
+            return _backward_impl(roots, grads, retain_graph)
+    return _backward_impl(roots, grads, retain_graph)
+
+
+def _backward_impl(roots, grads, retain_graph):
     prev = torch.is_grad_enabled()
     torch._C._set_grad_enabled(False)
     outer = getattr(_TLS, "callbacks", None)

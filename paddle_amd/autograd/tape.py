@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import contextlib
 import threading
+import weakref
 
 import torch
 
@@ -114,8 +115,16 @@ class Tape:
 
     # ------------------------------------------------------------------ backward
     def backward(self, loss, grad=None):
-        while _BEFORE_BACKWARD:  # e.g. an optimizer update still running on a side stream
-            _BEFORE_BACKWARD.pop(0)()
+        from ..utils import strict as _strict
+
+        if _strict.counting():
+            # strict-native accounting of the reverse pass (the fused ops' backwards)
+            with _strict.region("tape:backward", native=False):
+                return self._backward(loss, grad)
+        return self._backward(loss, grad)
+
+    def _backward(self, loss, grad=None):
+        run_before_backward()  # e.g. an optimizer update still running on a side stream
         tg = getattr(loss, "_pa_tape", None)
         if tg is None or tg[0] != id(self):
             raise RuntimeError("tape.backward: the loss was not produced on this tape")
@@ -171,14 +180,32 @@ def _add(a, b):
     return a + b
 
 
+# pending callbacks, held weakly: a bound method of an optimizer that is gone (or
+# that already drained its own wait) must not keep it and its buffers alive
 _BEFORE_BACKWARD = []
 
 
 def before_next_backward(fn):
     """Run ``fn`` once at the start of the next reverse pass (before any gradient
-    is written)."""
-    if fn not in _BEFORE_BACKWARD:
-        _BEFORE_BACKWARD.append(fn)
+    is written) -- of this tape, of the eager engine, or of torch autograd."""
+    ref = weakref.WeakMethod(fn) if hasattr(fn, "__self__") else (lambda f=fn: f)
+    for r in _BEFORE_BACKWARD:
+        if r() == fn:
+            return
+    _BEFORE_BACKWARD.append(ref)
+
+
+def run_before_backward():
+    """Drain the pending callbacks (every reverse-pass entry point calls this)."""
+    while _BEFORE_BACKWARD:
+        fn = _BEFORE_BACKWARD.pop(0)()
+        if fn is not None:
+            fn()
+
+
+def cancel_before_backward(fn):
+    """Drop a pending callback (its owner already waited for what it guards)."""
+    _BEFORE_BACKWARD[:] = [r for r in _BEFORE_BACKWARD if r() is not None and r() != fn]
 
 
 @contextlib.contextmanager

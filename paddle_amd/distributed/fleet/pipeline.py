@@ -23,6 +23,8 @@ from __future__ import annotations
 
 import math
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -154,37 +156,85 @@ def _unmeta(m, device):
 
 
 class _P2P:
-    def __init__(self, hcg, device):
+    """Point-to-point activation / gradient exchange between adjacent stages.
+
+    Shapes and dtypes travel as a small metadata message only the first time a
+    (peer, direction) pair is used; afterwards both sides reuse the cached
+    metadata (static shapes across micro-batches, as in 1F1B steady state), so a
+    steady-state exchange is ONE batched isend/irecv round with no host reads.  A
+    sender whose tensors no longer match the cached metadata raises, unless the
+    exchange was built with ``dynamic_shapes=True`` (metadata every time).
+    ``meta_rounds`` / ``host_syncs`` count metadata exchanges and the device->host
+    reads they needed (tests assert both stay 0 in steady state)."""
+
+    def __init__(self, hcg, device, dynamic_shapes=None):
         self.hcg, self.device = hcg, device
         self.stage = hcg.get_stage_id()
         self.nst = hcg.get_pipe_parallel_world_size()
         self.prev = hcg.stage_rank(self.stage - 1) if self.stage > 0 else None
         self.next = hcg.stage_rank(self.stage + 1) if self.stage < self.nst - 1 else None
         self.nccl = comm.is_dist() and dist.get_backend() == "nccl"
+        if dynamic_shapes is None:
+            dynamic_shapes = os.environ.get("FLAGS_pp_dynamic_shapes", "0") == "1"
+        self.dynamic = dynamic_shapes
+        self._sent = {}   # (peer, "fwd"|"bwd") -> [(dtype, shape)] sent last
+        self._recv = {}   # (peer, "fwd"|"bwd") -> [(dtype, shape)] received last
+        self.meta_rounds = 0
+        self.host_syncs = 0
 
     def _meta_dev(self):
         return self.device if self.nccl else "cpu"
 
+    @staticmethod
+    def _sig(ts):
+        return [(t.dtype, tuple(t.shape)) for t in ts]
+
     def exchange(self, send_next=None, send_prev=None, recv_next=False, recv_prev=False):
         """One batched round: optional sends to next/prev, optional receives from
-        next/prev.  Returns (from_next, from_prev) as tensor lists."""
+        next/prev.  Returns (from_next, from_prev) as tensor lists.  Activations flow
+        forward (to next, from prev: key "fwd"), gradients backward ("bwd")."""
         mdev = self._meta_dev()
         ops = []
         got_next_m = got_prev_m = None
-        if send_next is not None:
+        # metadata only for pairs not seen yet (both sides decide identically: a
+        # pair's first use is the same exchange on the sender and the receiver)
+        need_sn = send_next is not None and (self.dynamic or (self.next, "fwd") not in self._sent)
+        need_sp = send_prev is not None and (self.dynamic or (self.prev, "bwd") not in self._sent)
+        need_rn = recv_next and (self.dynamic or (self.next, "bwd") not in self._recv)
+        need_rp = recv_prev and (self.dynamic or (self.prev, "fwd") not in self._recv)
+        for lst, key in ((send_next, (self.next, "fwd")), (send_prev, (self.prev, "bwd"))):
+            if lst is not None and not self.dynamic and key in self._sent and self._sig(lst) != self._sent[key]:
+                raise RuntimeError(f"pipeline p2p: tensors sent to rank {key[0]} changed shape/dtype "
+                                   f"({self._sent[key]} -> {self._sig(lst)}); build the pipeline with "
+                                   "dynamic_shapes=True (FLAGS_pp_dynamic_shapes=1) for variable shapes")
+        if need_sn:
             ops.append(dist.P2POp(dist.isend, _meta(send_next).to(mdev), self.next))
-        if send_prev is not None:
+        if need_sp:
             ops.append(dist.P2POp(dist.isend, _meta(send_prev).to(mdev), self.prev))
-        if recv_next:
+        if need_rn:
             got_next_m = torch.empty(1 + _MAXT * (2 + _MAXD), dtype=torch.int64, device=mdev)
             ops.append(dist.P2POp(dist.irecv, got_next_m, self.next))
-        if recv_prev:
+        if need_rp:
             got_prev_m = torch.empty(1 + _MAXT * (2 + _MAXD), dtype=torch.int64, device=mdev)
             ops.append(dist.P2POp(dist.irecv, got_prev_m, self.prev))
-        self._run(ops)
-        ops = []
-        from_next = _unmeta(got_next_m.cpu(), self.device) if recv_next else None
-        from_prev = _unmeta(got_prev_m.cpu(), self.device) if recv_prev else None
+        if ops:
+            self.meta_rounds += 1
+            self._run(ops)
+            ops = []
+        if send_next is not None:
+            self._sent[(self.next, "fwd")] = self._sig(send_next)
+        if send_prev is not None:
+            self._sent[(self.prev, "bwd")] = self._sig(send_prev)
+        for got, key in ((got_next_m, (self.next, "bwd")), (got_prev_m, (self.prev, "fwd"))):
+            if got is not None:
+                if got.is_cuda:
+                    self.host_syncs += 1
+                m = got.cpu()
+                self._recv[key] = [(t.dtype, tuple(t.shape)) for t in _unmeta(m, "meta")]
+        from_next = [torch.empty(sh, dtype=dt, device=self.device) for dt, sh in self._recv[(self.next, "bwd")]] \
+            if recv_next else None
+        from_prev = [torch.empty(sh, dtype=dt, device=self.device) for dt, sh in self._recv[(self.prev, "fwd")]] \
+            if recv_prev else None
         # gloo moves host memory only: device tensors are staged through the host
         # (the RCCL path sends device buffers directly)
         host = (lambda t: t.detach().cpu()) if not self.nccl else (lambda t: t)
@@ -307,7 +357,11 @@ class PipelineParallel(Layer):
     # ------------------------------------------------------------------ schedule
     def forward_backward_pipeline(self, data):
         dev = next(self._layers.parameters()).device
-        p2p = _P2P(self.hcg, dev)
+        # one exchange object for the life of the engine: its metadata cache makes
+        # every steady-state exchange a single batched round with no host reads
+        p2p = getattr(self, "_p2p_train", None)
+        if p2p is None or p2p.device != dev:
+            p2p = self._p2p_train = _P2P(self.hcg, dev)
         ins, labs = self._split(data)
         M = self.accumulate_steps
         warm = min(self.nst - self.stage - 1, M)

@@ -36,6 +36,10 @@ from ..parallel.sharding import FlatShardedOptimizer, _no_decay
 from ..autograd import tape as _tape  # noqa: E402
 
 
+def _tape_recording():
+    return _tape.current() is not None
+
+
 class _Regather(torch.autograd.Function):
     @staticmethod
     def forward(ctx, unit, *xs):
@@ -45,11 +49,16 @@ class _Regather(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *gs):
-        ctx.unit.gather()
+        ctx.unit.owner._enter_backward(ctx.unit)
         return (None,) + gs
 
 
 class _Unit:
+    """One transformer block (or the root remainder): its parameters are views into
+    ``flat``, whose storage exists only while the unit is in use.  State machine:
+    ``released`` -> (prefetch on the comm stream) ``inflight`` -> (first use waits
+    the event) ``gathered`` -> (post-hook) ``released``."""
+
     ALIGN = 64
 
     def __init__(self, owner, name, module, params, W, r, group, nd):
@@ -60,16 +69,22 @@ class _Unit:
         self.params = [p for _, p in decay + nodec]
         offs, off = [], 0
         self.decay_end = None
+        gaps = []
         for i, p in enumerate(self.params):
             if i == len(decay):
                 self.decay_end = off
-            off = (off + self.ALIGN - 1) // self.ALIGN * self.ALIGN
-            offs.append(off)
-            off += p.numel()
+            a = (off + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+            if a > off:
+                gaps.append((off, a))
+            offs.append(a)
+            off = a + p.numel()
         if self.decay_end is None:
             self.decay_end = off
         unit = W * self.ALIGN
         self.N = max(unit, (off + unit - 1) // unit * unit)
+        if self.N > off:
+            gaps.append((off, self.N))
+        self.gaps = gaps  # flat ranges that belong to no parameter (zeroed gradient slots)
         self.S = self.N // W
         p0 = self.params[0]
         self.dtype, self.device = p0.dtype, p0.device
@@ -82,52 +97,72 @@ class _Unit:
         lo = r * self.S
         # W == 1: the shard IS the parameter storage (never released / re-gathered)
         self.p_shard = self.flat[lo:lo + self.S] if W == 1 else self.flat[lo:lo + self.S].clone()
-        self.master = self.p_shard.float()
-        self.m = torch.zeros_like(self.master)
-        self.v = torch.zeros_like(self.master)
-        self.g_shard = torch.zeros_like(self.master)
+        self.lo = lo
         self.local_decay_end = min(max(self.decay_end - lo, 0), self.S)
         # which shard elements belong to tensor-parallel (mp-sharded) parameters: their
         # squares are summed across mp ranks for the global norm, the rest counted once
-        dm = torch.zeros(self.N, dtype=torch.float32, device=self.device)
-        for p, o in zip(self.params, offs):
-            if (getattr(p, "is_distributed", False) is True):
-                dm[o:o + p.numel()] = 1.0
-        self.dist_mask = dm[lo:lo + self.S].clone()
-        self.has_dist = bool(self.dist_mask.any())
+        self.dist_ranges = [(max(o, lo) - lo, min(o + p.numel(), lo + self.S) - lo)
+                            for p, o in zip(self.params, offs)
+                            if getattr(p, "is_distributed", False) is True and o < lo + self.S and o + p.numel() > lo]
+        self.has_dist = bool(self.dist_ranges)
         self.nbytes = self.flat.untyped_storage().nbytes()
-        self.gathered = True
+        self.state = "gathered"
+        self.event = None
         self.ready = set()
+        self.slot = None  # gradient slot (owner._gpool index) while the unit's backward runs
 
+    # ---- parameter storage
     def gather(self):
-        if self.gathered:
+        """Make the full parameters current on the compute stream."""
+        if self.state == "gathered":
+            return
+        if self.state == "inflight":
+            if self.event is not None:
+                torch.cuda.current_stream(self.device).wait_event(self.event)
+            self.event = None
+            self.state = "gathered"
             return
         self.flat.untyped_storage().resize_(self.nbytes)
-        comm.all_gather(self.flat, self.p_shard, group=self.group)
-        self.gathered = True
+        self.owner._all_gather(self.flat, self.p_shard)
+        self.state = "gathered"
+
+    def prefetch(self):
+        """Start the all-gather on the comm stream (the next unit, while this one computes)."""
+        if self.state != "released":
+            return
+        cs = self.owner.comm_stream
+        if cs is None:
+            self.gather()
+            return
+        # storage allocated on the compute stream (its owner); the comm stream writes it
+        # after everything issued so far (earlier reads of the recycled block) and the
+        # compute stream waits for the event before its first read
+        self.flat.untyped_storage().resize_(self.nbytes)
+        main = torch.cuda.current_stream(self.device)
+        cs.wait_stream(main)
+        with torch.cuda.stream(cs):
+            self.owner._all_gather(self.flat, self.p_shard)
+            self.event = cs.record_event()
+        self.state = "inflight"
 
     def release(self):
-        if not self.gathered or self.W == 1:
+        if self.state == "released" or self.W == 1:
             return
+        if self.state == "inflight":
+            self.gather()  # never free storage a comm-stream write still targets
         self.flat.untyped_storage().resize_(0)
-        self.gathered = False
+        self.state = "released"
 
+    # ---- gradients
     def on_grad(self, p):
         self.ready.add(id(p))
         if len(self.ready) == len(self.params):
             self.reduce_grads()
 
     def reduce_grads(self):
-        if not self.ready:
+        if not self.ready and self.slot is None:
             return
-        full = torch.zeros(self.N, dtype=torch.float32, device=self.device)
-        for p, o in zip(self.params, self.offs):
-            if p.grad is not None:
-                full[o:o + p.numel()].copy_(p.grad.reshape(-1))
-                p.grad = None
-        part = torch.empty(self.S, dtype=torch.float32, device=self.device)
-        comm.reduce_scatter(part, full, group=self.group)
-        self.g_shard += part
+        self.owner._reduce_unit(self)
         self.ready.clear()
         if self.owner.training_release:
             self.release()
@@ -135,11 +170,29 @@ class _Unit:
 
 class ShardedStage3:
     """ZeRO-3 / FSDP-style training engine (AdamW).  ``model`` parameters must be
-    identical on every rank at construction (same seed, or broadcast first)."""
+    identical on every rank at construction (same seed, or broadcast first).
+
+    Communication overlap (reference: the dataflow over per-device streams with
+    events, framework/details/op_handle_base.cc:42-110 and
+    threaded_ssa_graph_executor.cc:93-129): on the GPU every collective runs on the
+    DeviceContext comm stream --
+
+    * forward: when unit i starts, unit i+1's all-gather is issued on the comm
+      stream (order learned on the first step); unit i+1's first use waits for its
+      event only;
+    * backward: when the reverse pass reaches unit i, unit i-1's all-gather is
+      prefetched the same way; the fused ops write unit i's weight gradients
+      straight into an fp32 slot of a two-slot pool (``_pa_main_grad`` views), and
+      once the unit is complete its slot is reduce-scattered on the comm stream and
+      added into the rank's gradient shard while backward continues (the slot is
+      reused two units later, after its event);
+    * the data-parallel axis is one all-reduce per ~``bucket_mb`` of the contiguous
+      gradient-shard buffer (all units' shards are views of it).
+    """
 
     def __init__(self, model, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.0, group=None,
                  grad_clip=None, no_decay_fn=None, *, mp_group=None, pp_group=None, dp_group=None, exclude=(),
-                 norm_skip=()):
+                 norm_skip=(), bucket_mb=256, prefetch=True):
         """Composition with hybrid parallelism (fleet.distributed_model):
         ``group`` is the sharding axis; ``dp_group`` an extra data-parallel axis whose
         gradient shards are all-reduced before the step; ``mp_group`` / ``pp_group``
@@ -157,8 +210,10 @@ class ShardedStage3:
         self.ex_state = {}
         self.W, self.r = comm.get_world_size(group), comm.get_rank(group)
         self.lr, self.betas, self.eps, self.wd, self.grad_clip = lr, betas, eps, weight_decay, grad_clip
+        self.bucket_elems = max(1, int(bucket_mb * 2**20) // 4)
         self.step_count = 0
         self.training_release = True
+        self.prefetch = prefetch
         nd = no_decay_fn or _no_decay
         named = dict(model.named_parameters())
         owner = {}
@@ -175,28 +230,82 @@ class ShardedStage3:
             key, mod = owner.get(n, ("<root>", model))
             groups.setdefault(key, (mod, []))[1].append((n, p))
         self.units = []
+        dev = None
         for key, (mod, params) in groups.items():
             u = _Unit(self, key, mod, params, self.W, self.r, group, nd)
             self.units.append(u)
+            dev = u.device
             for p in u.params:
                 p.register_post_accumulate_grad_hook(lambda p, u=u: u.on_grad(p))
                 # the framework's eager engine / tape fire these at the same point
                 p.__dict__.setdefault("_pa_grad_ready_hooks", []).append(lambda p, u=u: u.on_grad(p))
             self._hook(u)
+        dev = dev if dev is not None else (self.excluded[0].device if self.excluded else torch.device("cpu"))
+        self.device = dev
+        # optimizer state: one contiguous fp32 buffer per kind, unit shards are views
+        tot = sum(u.S for u in self.units)
+        self.g_all = torch.zeros(tot, dtype=torch.float32, device=dev)
+        self.master_all = torch.zeros(tot, dtype=torch.float32, device=dev)
+        self.m_all = torch.zeros(tot, dtype=torch.float32, device=dev)
+        self.v_all = torch.zeros(tot, dtype=torch.float32, device=dev)
+        off = 0
+        for u in self.units:
+            u.g_shard = self.g_all[off:off + u.S]
+            u.master = self.master_all[off:off + u.S]
+            u.master.copy_(u.p_shard)
+            u.m = self.m_all[off:off + u.S]
+            u.v = self.v_all[off:off + u.S]
+            u.goff = off
+            off += u.S
+        self.dist_mask = None
+        if any(u.has_dist for u in self.units):
+            self.dist_mask = torch.zeros(tot, dtype=torch.float32, device=dev)
+            for u in self.units:
+                for a, b in u.dist_ranges:
+                    self.dist_mask[u.goff + a:u.goff + b] = 1.0
+        # comm stream + two fp32 gradient slots for the reduce-scatter pipeline
+        cuda = dev.type == "cuda"
+        if cuda:
+            from ..platform import device_context
+
+            dc = device_context(dev)
+            self.comm_stream = dc.comm_stream if dc is not None else torch.cuda.Stream(device=dev)
+        else:
+            self.comm_stream = None
+        nmax = max((u.N for u in self.units), default=0)
+        smax = max((u.S for u in self.units), default=0)
+        self._gpool = [torch.zeros(nmax, dtype=torch.float32, device=dev) for _ in range(2)]
+        self._ppool = [torch.empty(smax, dtype=torch.float32, device=dev) for _ in range(2)]
+        self._gfree = [None, None]  # comm-stream events: slot reusable
+        self._next_slot = 0
+        self._order = []   # units in forward order (learned on the first forward)
+        self._pos = {}
         for u in self.units:
             u.release()
 
+    # ------------------------------------------------------------------ collectives
+    def _all_gather(self, out, inp):
+        comm.all_gather(out, inp, group=self.group)
+
     def _hook(self, u):
         def pre(mod, args, kwargs=None):
+            if id(u) not in self._pos:
+                self._pos[id(u)] = len(self._order)
+                self._order.append(u)
             u.gather()
+            if self.prefetch:
+                i = self._pos[id(u)]
+                if i + 1 < len(self._order):
+                    self._order[i + 1].prefetch()
 
         def post(mod, args, out):
-            if not (torch.is_grad_enabled() and mod.training):
+            if not (torch.is_grad_enabled() and mod.training) and not _tape_recording():
                 u.release()
                 return out
             u.release()
             if isinstance(out, tuple):
-                idx = [i for i, o in enumerate(out) if torch.is_tensor(o) and o.requires_grad]
+                idx = [i for i, o in enumerate(out) if torch.is_tensor(o) and
+                       (o.requires_grad or (_tape_recording() and o.is_floating_point()))]
                 if not idx:
                     return out
                 res = _tape.apply(_Regather, u, *[out[i] for i in idx])
@@ -205,12 +314,67 @@ class ShardedStage3:
                 for i, t in zip(idx, res):
                     lst[i] = t
                 return tuple(lst)
-            if torch.is_tensor(out) and out.requires_grad:
+            if torch.is_tensor(out) and (out.requires_grad or _tape_recording()):
                 return _tape.apply(_Regather, u, out)
             return out
 
         u.module.register_forward_pre_hook(pre)
         u.module.register_forward_hook(post)
+
+    def _enter_backward(self, u):
+        """The reverse pass reached unit ``u``: its parameters and a gradient slot."""
+        u.gather()
+        if self.prefetch and id(u) in self._pos:
+            i = self._pos[id(u)]
+            if i > 0:
+                self._order[i - 1].prefetch()
+        self._assign_slot(u)
+
+    def _assign_slot(self, u):
+        if u.slot is not None:
+            return
+        k = self._next_slot
+        self._next_slot ^= 1
+        if self._gfree[k] is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._gfree[k])
+            self._gfree[k] = None
+        buf = self._gpool[k]
+        u.slot = k
+        for p, o in zip(u.params, u.offs):
+            p._pa_main_grad = buf[o:o + p.numel()].view_as(p)
+            p._pa_grad_fresh = True
+
+    def _reduce_unit(self, u):
+        if u.slot is None:
+            self._assign_slot(u)  # gradients arrived through autograd only (no regather node)
+        buf = self._gpool[u.slot][:u.N]
+        for p, o in zip(u.params, u.offs):
+            sl = buf[o:o + p.numel()]
+            if p.grad is not None:
+                g = p.grad.reshape(-1)
+                if getattr(p, "_pa_grad_fresh", True):
+                    sl.copy_(g)
+                else:
+                    sl.add_(g)
+                p.grad = None
+            elif getattr(p, "_pa_grad_fresh", True):
+                sl.zero_()  # no gradient this micro-step
+            p._pa_grad_fresh = False
+            p._pa_main_grad = None
+        for a, b in u.gaps:
+            buf[a:b].zero_()
+        part = self._ppool[u.slot][:u.S]
+        cs = self.comm_stream
+        if cs is not None:
+            cs.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(cs):
+                comm.reduce_scatter(part, buf, group=self.group)
+                u.g_shard.add_(part)
+                self._gfree[u.slot] = cs.record_event()
+        else:
+            comm.reduce_scatter(part, buf, group=self.group)
+            u.g_shard.add_(part)
+        u.slot = None
 
     def parameters_gathered(self):
         for u in self.units:
@@ -219,23 +383,26 @@ class ShardedStage3:
     @torch.no_grad()
     def step(self, lr=None):
         for u in self.units:  # units with unused parameters never completed their hook
-            u.reduce_grads()
+            if u.ready or u.slot is not None:
+                u.reduce_grads()
+        if self.comm_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
         if self.dp_group is not None and self.dpW > 1:
-            for u in self.units:
-                comm.all_reduce(u.g_shard, group=self.dp_group)
+            for o in range(0, self.g_all.numel(), self.bucket_elems):
+                comm.all_reduce(self.g_all[o:o + self.bucket_elems], group=self.dp_group)
         self.step_count += 1
         lr = self.lr if lr is None else lr
         scale = 1.0 / (self.W * self.dpW)
-        dev = self.units[0].device if self.units else self.excluded[0].device
+        dev = self.device
         clip = None
         if self.grad_clip:
-            # squares of the AVERAGED gradient: (scale * g_shard)^2
+            # squares of the AVERAGED gradient: (scale * g_shard)^2, over the flat buffer
             sq = torch.zeros(2, dtype=torch.float32, device=dev)  # [tp-sharded, replicated]
-            for u in self.units:
-                g2 = u.g_shard.pow(2)
-                d = (g2 * u.dist_mask).sum() if u.has_dist else torch.zeros((), device=dev)
-                sq[0] += d * scale * scale
-                sq[1] += (g2.sum() - d) * scale * scale
+            tot_sq = fused_optim.sumsq(self.g_all) if self.g_all.numel() else torch.zeros(1, device=dev)
+            d = (self.g_all.pow(2) * self.dist_mask).sum() if self.dist_mask is not None else \
+                torch.zeros((), device=dev)
+            sq[0] += d * scale * scale
+            sq[1] += (tot_sq.reshape(()) - d) * scale * scale
             comm.all_reduce(sq, group=self.group)
             for p in self.excluded:  # whole, already averaged and identical on the sharding ranks
                 if p.grad is None or id(p) in self.norm_skip:
@@ -248,16 +415,12 @@ class ShardedStage3:
                 comm.all_reduce(tot, group=self.pp_group)
             clip = torch.clamp(self.grad_clip / (tot.sqrt() + 1e-6), max=1.0)
         for u in self.units:
-            g = u.g_shard
-            if clip is not None:
-                g.mul_(clip * scale)
-                gs = 1.0
-            else:
-                gs = scale
-            fused_optim.adamw_flat(u.master, g, u.m, u.v, lr=lr, beta1=self.betas[0], beta2=self.betas[1],
-                                   eps=self.eps, weight_decay=self.wd, step=self.step_count,
-                                   param_out=u.p_shard, decay_end=u.local_decay_end, grad_scale=gs)
-            g.zero_()
+            # the clip coefficient stays on the device (read by the kernel, no host sync)
+            fused_optim.adamw_flat(u.master, u.g_shard, u.m, u.v, lr=lr, beta1=self.betas[0],
+                                   beta2=self.betas[1], eps=self.eps, weight_decay=self.wd, step=self.step_count,
+                                   param_out=u.p_shard, decay_end=u.local_decay_end, grad_scale=scale,
+                                   grad_scale_tensor=clip)
+        self.g_all.zero_()
         for p in self.excluded:
             if p.grad is None:
                 continue
@@ -277,8 +440,10 @@ class ShardedStage3:
                 p.data.copy_(master.view_as(p))
 
     def zero_grad(self):
+        if self.comm_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
+        self.g_all.zero_()
         for u in self.units:
-            u.g_shard.zero_()
             for p in u.params:
                 p.grad = None
         for p in self.excluded:

@@ -412,7 +412,11 @@ class ParallelExecutor:
                 from ..parallel.direct import DirectAllReduce
 
                 self._direct = DirectAllReduce(max_bytes=256 << 20)
+            # a barrier timeout NaN-poisons the sum: raise on the next collective
+            # instead of broadcasting and applying poisoned gradients again
+            self._direct.poll_error()
             self._direct.all_reduce(flat)
+            self._direct.error_async()
         else:
             comm.all_reduce(flat)
 

@@ -21,6 +21,7 @@ import torch
 
 from ..utils import flags as FLAGS
 from ..utils import profiler as prof
+from ..utils import strict as _strict
 from . import core
 from . import registry as R
 from .. import platform as _platform
@@ -140,7 +141,13 @@ class BlockExecutor:
             if _platform._V >= 3:
                 _platform.vlog(3, f"run op {op.type} inputs {dict(ins)} outputs {dict(outs)}")
             run = R.run_kernel_stash if (pb.stash[k] and not stash_off) else R.run_kernel
-            if profiling:
+            if _strict.watching() and place.torch_device().type == "cuda":
+                # framework region: tensor expressions inside the op kernel run on the
+                # HIP kernels (ops/aten_native.py); uncovered ATen kernels are counted
+                # (and refused under FLAGS_strict_native=1)
+                with _strict.region("fluid:" + op.type):
+                    run(info, ctx)
+            elif profiling:
                 with prof.RecordEvent(op.type):
                     run(info, ctx)
             else:

@@ -168,7 +168,10 @@ class FlatShardedOptimizer:
         # order, each parameter's first read waits only for its own bucket -- the
         # bandwidth-bound update hides under the next forward's GEMMs
         if overlap_update is None:
-            overlap_update = os.environ.get("FLAGS_overlap_optimizer", "1") != "0"
+            # opt-in: only the fused ops (ops/fused.py param_ready) and the framework
+            # tape / eager engine honour the per-bucket waits; plain torch layers and
+            # torch autograd would race the side stream
+            overlap_update = os.environ.get("FLAGS_overlap_optimizer", "0") == "1"
         self.overlap_update = bool(overlap_update) and self.W == 1 and dev.type == "cuda"
         self.opt_stream = ((dc.aux_stream if dc is not None else torch.cuda.Stream(device=dev))
                            if self.overlap_update else None)
@@ -328,6 +331,13 @@ class FlatShardedOptimizer:
         """Make every parameter current (before reading them outside the fused ops,
         e.g. for a checkpoint or an evaluation with plain torch ops)."""
         self._wait_bucket(None)
+        self._wait_update()
+
+    def _wait_update(self):
+        """The overlapped update also READS grad_shard / m / v / master on the side
+        stream: any main-stream write to them must wait for it."""
+        if self.opt_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.opt_stream)
 
     @torch.no_grad()
     def step(self, lr=None):
@@ -357,6 +367,10 @@ class FlatShardedOptimizer:
                 for b in range(len(self.buckets)):
                     self._gather(b)
         if self._direct is not None:
+            if self.overlap:
+                # the gathers (and their barriers) may have been issued on the main
+                # stream: the flag copy must come after them
+                self.comm_stream.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(self.comm_stream) if self.overlap else contextlib.nullcontext():
                 self._direct.error_async()
         fused.bump_weight_epoch()
@@ -398,6 +412,7 @@ class FlatShardedOptimizer:
                 p._pa_grad_fresh = True
             self._lazy_zero = True
             return
+        self._wait_update()  # an overlapped update may still be reading flat_grad
         self.flat_grad.zero_()
 
     def _zero_untouched(self, b):

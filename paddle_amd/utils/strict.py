@@ -1,0 +1,193 @@
+"""Strict-native mode: prove that a model or a test stayed on the framework's own
+HIP kernels.
+
+Reference behaviour: ``OperatorWithKernel::RunImpl`` looks up the kernel
+registered for the expected ``OpKernelType`` and throws when there is none
+(paddle/fluid/framework/operator.cc:665-685) -- there is no silent detour through
+another library.  Here several layers *can* fall back to ATen (PyTorch-ROCm's own
+kernels) for shapes or dtypes the HIP kernels do not cover; this module makes
+every such detour visible and, under ``FLAGS_strict_native=1``, an error:
+
+* :func:`region` brackets framework code (one Fluid op run, one eager-engine op,
+  one tensor-API call, one reverse pass).  While the outermost region is open and
+  counting is on (``FLAGS_strict_native=1`` or ``FLAGS_count_aten=1``), a
+  ``TorchDispatchMode`` classifies every ATen call that touches a GPU tensor:
+  allocation, view and metadata ops are free; anything else launches an ATen
+  device kernel and is counted in :data:`ATEN_KERNELS` under
+  ``"<region label>:<aten op>"`` -- or raises :class:`StrictNativeError` in strict
+  mode.  The framework's HIP kernels are launched through raw pointers
+  (``ops/_native.py``) and never pass through the dispatcher, so they are never
+  counted.  Code outside every region (a test's own torch oracle) is not watched.
+* :func:`fallback` is the explicit hook for code paths that know they are leaving
+  the native kernels (e.g. an op branch for an unsupported dtype):
+  :data:`FALLBACKS` counts them per site.
+
+``reset()`` clears the counters; ``report()`` returns both as plain dicts.
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+import threading
+
+import torch
+from torch.utils._python_dispatch import TorchDispatchMode
+
+ATEN_KERNELS: dict = {}   # "label:aten_op" -> ATen kernel launches on GPU tensors inside regions
+NATIVE_OPS: dict = {}     # aten op -> calls executed on the framework's HIP kernels (ops/aten_native.py)
+FALLBACKS: dict = {}      # site -> explicit fallback count
+_TLS = threading.local()
+# device types whose ATen kernels count (tests add "cpu" to exercise the watcher here)
+WATCH_DEVICES = {"cuda"}
+
+
+class StrictNativeError(RuntimeError):
+    """An ATen device kernel (or an explicit fallback) ran inside a framework region
+    under ``FLAGS_strict_native=1``."""
+
+
+def strict() -> bool:
+    return os.environ.get("FLAGS_strict_native", "0") not in ("0", "", "false", "False")
+
+
+def counting() -> bool:
+    return strict() or os.environ.get("FLAGS_count_aten", "0") not in ("0", "", "false", "False")
+
+
+_CUDA = []
+
+
+def watching() -> bool:
+    """True when a region would push the dispatch mode (native dispatch or counting)."""
+    return native_dispatch() or counting()
+
+
+def native_dispatch() -> bool:
+    """Route ATen pointwise / cast / fill / reduction ops issued inside framework
+    regions onto the HIP kernels of ops/aten_native.py (default on with a GPU)."""
+    if os.environ.get("FLAGS_native_dispatch", "1") in ("0", "false", "False"):
+        return False
+    if not _CUDA:
+        _CUDA.append(torch.cuda.is_available())
+    return _CUDA[0]
+
+
+# ATen ops that launch no device kernel: allocation, views, metadata, stream bookkeeping
+_FREE = {
+    "empty", "empty_strided", "empty_like", "new_empty", "new_empty_strided", "resize_", "set_",
+    "view", "_unsafe_view", "reshape", "as_strided", "t", "transpose", "permute", "expand", "expand_as",
+    "squeeze", "unsqueeze", "select", "slice", "narrow", "split", "split_with_sizes", "unbind", "chunk",
+    "detach", "alias", "lift_fresh", "view_as", "unflatten", "flatten", "diagonal", "movedim",
+    "record_stream", "is_same_size", "_reshape_alias", "numpy_T", "real", "conj", "resolve_conj",
+    "resolve_neg", "_conj", "_neg_view", "clone_view", "contiguous_view", "split_copy_view", "unfold",
+    "is_pinned", "size", "stride", "dim", "sym_size", "sym_stride", "sym_numel", "sym_storage_offset",
+    "_local_scalar_dense_view",
+}
+
+
+def _is_gpu(x):
+    return isinstance(x, torch.Tensor) and x.device.type in WATCH_DEVICES
+
+
+def _touches_gpu(args, kwargs):
+    dev = kwargs.get("device")
+    if dev is not None and torch.device(dev).type in WATCH_DEVICES:
+        return True  # factory op (zeros / full / empty ...) placed on the GPU
+    for a in args:
+        if _is_gpu(a):
+            return True
+        if isinstance(a, (list, tuple)) and any(_is_gpu(b) for b in a):
+            return True
+    for a in kwargs.values():
+        if _is_gpu(a):
+            return True
+    return False
+
+
+class _Watch(TorchDispatchMode):
+    def __init__(self, native):
+        super().__init__()
+        self.native = native
+
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        ns = getattr(func, "namespace", "aten")
+        name = func._schema.name.split("::")[-1] if hasattr(func, "_schema") else str(func)
+        if ns == "aten" and name not in _FREE and _touches_gpu(args, kwargs):
+            if self.native:
+                from ..ops import aten_native
+
+                r = aten_native.try_native(func, args, kwargs)
+                if r is not NotImplemented:
+                    NATIVE_OPS[name] = NATIVE_OPS.get(name, 0) + 1
+                    return r
+            # a contiguous() of an already contiguous tensor never reaches here;
+            # clone / copy_ / _to_copy do launch a copy kernel and are counted
+            labels = getattr(_TLS, "labels", None)
+            key = f"{labels[-1] if labels else '?'}:{name}"
+            ATEN_KERNELS[key] = ATEN_KERNELS.get(key, 0) + 1
+            if strict():
+                raise StrictNativeError(
+                    f"FLAGS_strict_native: ATen kernel aten::{name} launched on a GPU tensor inside "
+                    f"framework region '{labels[-1] if labels else '?'}' (no native kernel covers this call)")
+        return func(*args, **kwargs)
+
+
+@contextlib.contextmanager
+def region(label: str, native: bool = True):
+    """Bracket framework code; only the outermost region pushes the dispatch mode.
+    ``native``: also run covered ATen ops on the HIP kernels (else only count)."""
+    labels = getattr(_TLS, "labels", None)
+    if labels is None:
+        labels = _TLS.labels = []
+    outer = not labels
+    labels.append(label)
+    mode = None
+    try:
+        nat = native and native_dispatch()
+        if outer and (nat or counting()):
+            mode = _Watch(nat)
+            mode.__enter__()
+        yield
+    finally:
+        if mode is not None:
+            mode.__exit__(None, None, None)
+        labels.pop()
+
+
+@contextlib.contextmanager
+def unwatched():
+    """Temporarily leave every region (e.g. a deliberate host-side reference path
+    the caller accounts for itself)."""
+    labels = getattr(_TLS, "labels", None)
+    saved = list(labels) if labels else []
+    if labels:
+        labels.clear()
+    try:
+        from torch.utils._python_dispatch import _pop_mode_temporarily, _get_current_dispatch_mode
+
+        if saved and isinstance(_get_current_dispatch_mode(), _Watch):
+            with _pop_mode_temporarily():
+                yield
+        else:
+            yield
+    finally:
+        if labels is not None:
+            labels[:] = saved
+
+
+def fallback(site: str, on_gpu: bool = True):
+    """Record an explicit fallback off the native kernels at ``site``; raises in strict mode."""
+    FALLBACKS[site] = FALLBACKS.get(site, 0) + 1
+    if on_gpu and strict():
+        raise StrictNativeError(f"FLAGS_strict_native: '{site}' left the native kernels")
+
+
+def reset():
+    ATEN_KERNELS.clear()
+    FALLBACKS.clear()
+    NATIVE_OPS.clear()
+
+
+def report() -> dict:
+    return {"aten_kernels": dict(ATEN_KERNELS), "fallbacks": dict(FALLBACKS), "native_ops": dict(NATIVE_OPS)}

@@ -94,13 +94,16 @@ def _pp_worker(rank, world, M, steps):
     model = fleet.distributed_model(layer)
     opt = torch.optim.SGD(model.parameters(), lr=0.5)
     losses = []
+    rounds = []
     for s in range(steps):
         b = _batch(B=8, seed=s)
         losses.append(model.train_batch((b[:, :-1], b[:, 1:]), opt).item())
+        p2p = model._p2p_train
+        rounds.append((p2p.meta_rounds, p2p.host_syncs))
     lo = layer.bounds[hcg.get_stage_id()]
     params = {f"run_function.{lo + int(n.split('.')[1])}.{'.'.join(n.split('.')[2:])}": p.detach().clone()
               for n, p in layer.named_parameters()}
-    return losses, params
+    return losses, params, rounds
 
 
 @pytest.mark.parametrize("world,M", [(2, 4), (4, 8)])
@@ -109,7 +112,11 @@ def test_pipeline_1f1b_llama_matches_single(world, M):
     ref_losses, ref_model = _pp_ref(M, steps)
     ref = dict(ref_model.named_parameters())
     res = run_dist(_pp_worker, world, M, steps)
-    for losses, params in res:
+    for losses, params, rounds in res:
+        # metadata travels only in the first step; steady state: one batched round per
+        # exchange and no device->host reads
+        assert rounds[-1][0] == rounds[0][0] and rounds[0][0] <= 4, rounds
+        assert rounds[-1][1] == 0, rounds
         for a, b in zip(losses, ref_losses):
             assert abs(a - b) < 1e-5, (losses, ref_losses)
         for n, p in params.items():

@@ -10,7 +10,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _train(overlap, steps=4):
+def _train(overlap, steps=4, param_dtype_grads=False):
     from paddle_amd.autograd import tape
     from paddle_amd.models.llama import LLAMA_CONFIGS, LlamaConfig, LlamaForCausalLM
     from paddle_amd.parallel.sharding import FlatShardedOptimizer
@@ -23,7 +23,7 @@ def _train(overlap, steps=4):
     # eps = 1e-2: Adam's normalised step no longer turns last-ulp noise in a ~0
     # gradient into a +-lr update (with eps 1e-8 two runs of the SAME path drift
     # apart by ~lr through the embedding rows of the float-atomic backward)
-    opt = FlatShardedOptimizer(model.named_parameters(), lr=1e-3, eps=1e-2, grad_dtype=torch.float32,
+    opt = FlatShardedOptimizer(model.named_parameters(), lr=1e-3, eps=1e-2, grad_dtype=None if param_dtype_grads else torch.float32,
                                grad_clip=1.0, bucket_mb=1, overlap_update=overlap)
     assert opt.overlap_update == overlap and len(opt.buckets) > 2
     g = torch.Generator().manual_seed(1)
@@ -54,4 +54,15 @@ def test_overlapped_update_matches_single_kernel_update():
     # a parameter read before its bucket's update landed would leave a whole AdamW
     # step (~lr = 1e-3) of difference; per-bucket vs whole-buffer launches differ
     # in the last ulp only
+    assert (pa - pb).abs().max().item() < 1e-4, (pa - pb).abs().max().item()
+
+
+def test_overlapped_update_param_dtype_grads_eager_zero_grad():
+    """Gradients kept in the parameter dtype (no fp32 main grads): zero_grad()
+    zero-fills flat_grad on the main stream right after step() -- it must wait for
+    the side stream's update, which is still reading those gradients (ADVICE r3 #1)."""
+    la, pa = _train(True, param_dtype_grads=True)
+    lb, pb = _train(False, param_dtype_grads=True)
+    for a, b in zip(la, lb):
+        assert abs(a - b) <= 2e-4 * abs(b), (la, lb)
     assert (pa - pb).abs().max().item() < 1e-4, (pa - pb).abs().max().item()
