@@ -95,6 +95,7 @@ enum Op {
   GELU = 26, GELU_TANH = 27, SILU = 28, LEAKY = 29, ELU = 30, SOFTPLUS = 31, LOG2 = 32, ISNAN = 33,
   ISINF = 34, ISFINITE = 35, BNOT = 36, RPOW = 37, HARDSIGMOID = 38, HARDSWISH = 39, SQUARE = 40,
   CLAMP_MIN = 41, CLAMP_MAX = 42, ATAN = 43, LOG10 = 44, EXP2 = 45, FRAC = 46, MISH = 47,
+  IOTA = 48,  // nullary: a + b * (linear output index)
   // binary: x y, scalar a (alpha / slope / threshold)
   ADD = 50, SUB = 51, MUL = 52, DIV = 53, MAX = 54, MIN = 55, POW = 56, EQ = 57, NE = 58, LT = 59,
   LE = 60, GT = 61, GE = 62, LAND = 63, LOR = 64, LXOR = 65, FLOORDIV = 66, REM = 67, ATAN2 = 68,
@@ -312,6 +313,10 @@ __global__ __launch_bounds__(256) void ew_kernel(EwParams p) {
         if (NIN >= 3) zo += c * (I)p.z.st[d];
       }
     }
+    if (NIN == 0 && p.op == IOTA) {
+      stv<C>(p.out, p.odt, (long)oo, (C)(p.a + p.b * (double)i));
+      continue;
+    }
     const C x = NIN >= 1 ? ldv<C>(p.x.p, p.x.dt, (long)xo) : (C)0;
     const C y = NIN >= 2 ? ldv<C>(p.y.p, p.y.dt, (long)yo) : (C)0;
     const C z = NIN >= 3 ? ldv<C>(p.z.p, p.z.dt, (long)zo) : (C)0;
@@ -504,6 +509,47 @@ __global__ __launch_bounds__(256) void reduce_cols_kernel(RedParams p) {
   }
 }
 
+// index_select along the middle axis of a contiguous [outer, nsrc, inner] source:
+// out[o, i, j] = x[o, idx[i], j]; an index outside [0, nsrc) (negative: from the end)
+// reads zeros instead of faulting.  E = element bytes.
+template <int E>
+__global__ __launch_bounds__(256) void index_select_kernel(const char* x, char* out, const void* idx, int idx64,
+                                                           long outer, long nsrc, long inner, long nidx) {
+  const long n = outer * nidx * inner;
+  for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < n; t += (long)gridDim.x * 256) {
+    const long j = t % inner, r = t / inner, i = r % nidx, o = r / nidx;
+    long s = idx64 ? ((const long*)idx)[i] : (long)((const int*)idx)[i];
+    if (s < 0) s += nsrc;
+    char* dst = out + t * E;
+    if (s < 0 || s >= nsrc) {
+      for (int b = 0; b < E; ++b) dst[b] = 0;
+      continue;
+    }
+    const char* src = x + ((o * nsrc + s) * inner + j) * E;
+    if constexpr (E == 8) *(unsigned long*)dst = *(const unsigned long*)src;
+    else if constexpr (E == 4) *(unsigned*)dst = *(const unsigned*)src;
+    else if constexpr (E == 2) *(unsigned short*)dst = *(const unsigned short*)src;
+    else *dst = *src;
+  }
+}
+
+// inclusive prefix sum along the middle axis of a contiguous [outer, R, inner]
+// tensor; one thread per (outer, inner) column, sequential over R (exact order)
+template <class C>
+__global__ __launch_bounds__(256) void cumsum_kernel(const void* x, int xdt, void* out, int odt, long outer, long R,
+                                                     long inner) {
+  const long ncol = outer * inner;
+  for (long c = (long)blockIdx.x * 256 + threadIdx.x; c < ncol; c += (long)gridDim.x * 256) {
+    const long o = c / inner, j = c % inner;
+    C acc = (C)0;
+    for (long r = 0; r < R; ++r) {
+      const long off = (o * R + r) * inner + j;
+      acc += ldv<C>(x, xdt, off);
+      stv<C>(out, odt, off, acc);
+    }
+  }
+}
+
 }  // namespace tops
 }  // namespace pa
 
@@ -649,4 +695,30 @@ PA_EXPORT long pa_reduce_any(int op, int cdt, const void* x, int xdt, void* out,
   else PA_RED(long);
 #undef PA_RED
   return (long)hipGetLastError();
+}
+
+PA_EXPORT int pa_index_select(const void* x, int esize, long outer, long nsrc, long inner, const void* idx, int idx64,
+                              long nidx, void* out, hipStream_t st) {
+  const long n = outer * nidx * inner;
+  if (n <= 0) return 0;
+  const int g = stream_grid(n, 256) * 2;
+  switch (esize) {
+    case 1: hipLaunchKernelGGL(index_select_kernel<1>, dim3(g), dim3(256), 0, st, (const char*)x, (char*)out, idx, idx64, outer, nsrc, inner, nidx); break;
+    case 2: hipLaunchKernelGGL(index_select_kernel<2>, dim3(g), dim3(256), 0, st, (const char*)x, (char*)out, idx, idx64, outer, nsrc, inner, nidx); break;
+    case 4: hipLaunchKernelGGL(index_select_kernel<4>, dim3(g), dim3(256), 0, st, (const char*)x, (char*)out, idx, idx64, outer, nsrc, inner, nidx); break;
+    case 8: hipLaunchKernelGGL(index_select_kernel<8>, dim3(g), dim3(256), 0, st, (const char*)x, (char*)out, idx, idx64, outer, nsrc, inner, nidx); break;
+    default: return -1;
+  }
+  PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_cumsum(int cdt, const void* x, int xdt, void* out, int odt, long outer, long R, long inner,
+                        hipStream_t st) {
+  const long ncol = outer * inner;
+  if (ncol <= 0 || R <= 0) return 0;
+  const int g = stream_grid(ncol, 256);
+  if (cdt == 0) hipLaunchKernelGGL(cumsum_kernel<float>, dim3(g), dim3(256), 0, st, x, xdt, out, odt, outer, R, inner);
+  else if (cdt == 1) hipLaunchKernelGGL(cumsum_kernel<double>, dim3(g), dim3(256), 0, st, x, xdt, out, odt, outer, R, inner);
+  else hipLaunchKernelGGL(cumsum_kernel<long>, dim3(g), dim3(256), 0, st, x, xdt, out, odt, outer, R, inner);
+  PA_LAUNCH_CHECK();
 }

@@ -406,6 +406,15 @@ Scope& Scope::NewScope() {
   return *kids_.back();
 }
 
+void Scope::DropKid(Scope* kid) {
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto it = kids_.begin(); it != kids_.end(); ++it)
+    if (it->get() == kid) {
+      kids_.erase(it);
+      return;
+    }
+}
+
 void Scope::Erase(const std::string& name) {
   std::lock_guard<std::mutex> g(mu_);
   vars_.erase(name);
@@ -584,13 +593,81 @@ Executor::Executor(int device) {
   ctx_.device = device;
   if (device >= 0) {
     link_device_kernels();
-    ctx_.stream = device_stream_create(device);
+    own_stream_ = ctx_.stream = device_stream_create(device);
   }
   link_host_kernels();
 }
 
 Executor::~Executor() {
-  if (ctx_.stream) device_stream_destroy(ctx_.stream);
+  if (own_stream_) device_stream_destroy(own_stream_);
+}
+
+void Executor::SetStream(void* stream) {
+  if (ctx_.device < 0) return;
+  ctx_.stream = stream ? stream : own_stream_;
+}
+
+bool Executor::ReadBool(const Tensor& t) {
+  PA_CHECK(t.initialized() && t.numel() >= 1, "control flow: condition tensor is empty");
+  if (t.device < 0) {
+    switch (t.dtype) {
+      case DT::BOOL: case DT::UINT8: case DT::INT8: return *t.data<uint8_t>() != 0;
+      case DT::INT32: return *t.data<int32_t>() != 0;
+      case DT::INT64: return *t.data<int64_t>() != 0;
+      case DT::FP32: return *t.data<float>() != 0.f;
+      default: fail("control flow: unsupported condition dtype %s", dt_name(t.dtype));
+    }
+  }
+  Tensor h = t.to(-1, ctx_.stream);
+  device_stream_sync(ctx_.stream);
+  return ReadBool(h);
+}
+
+// while_op.cc: run the sub-block while Condition holds.  Forward semantics (the
+// reference's is_test path): one child scope holds the body's temporaries for the
+// whole loop; variables of enclosing scopes are updated in place.  Gradient
+// programs (while_grad needs per-step scopes) run on the Python engine.
+void Executor::RunWhile(const ProgramDesc& prog, const OpDesc& op, Scope* scope) {
+  const int sb = (int)op.GetInt("sub_block", -1);
+  PA_CHECK(sb >= 0 && sb < (int)prog.blocks.size(), "while: bad sub_block %d", sb);
+  const std::string cond = op.Input("Condition");
+  Variable* cv = scope->Find(cond);
+  PA_CHECK(cv != nullptr, "while: condition %s not found", cond.c_str());
+  Scope& body = scope->NewScope();
+  const BlockDesc& blk = prog.Block(sb);
+  for (const VarDesc& v : blk.vars)
+    if (!scope->Find(v.name)) body.Var(v.name)->kind = v.type;
+  int64_t iters = 0;
+  while (ReadBool(cv->tensor)) {
+    RunBlock(prog, blk, &body);
+    PA_CHECK(++iters < (int64_t)1 << 40, "while: runaway loop");
+  }
+  scope->DropKid(&body);  // device buffers of the body's temporaries are stream-ordered frees
+}
+
+// conditional_block_op.cc: run the sub-block once when the condition holds
+// (is_scalar_condition: Cond[0] != 0; else: every Input is non-empty).
+void Executor::RunConditionalBlock(const ProgramDesc& prog, const OpDesc& op, Scope* scope) {
+  const int sb = (int)op.GetInt("sub_block", -1);
+  PA_CHECK(sb >= 0 && sb < (int)prog.blocks.size(), "conditional_block: bad sub_block %d", sb);
+  bool run = true;
+  if (op.GetBool("is_scalar_condition", false)) {
+    Variable* cv = scope->Find(op.Input("Cond"));
+    PA_CHECK(cv != nullptr, "conditional_block: condition not found");
+    run = ReadBool(cv->tensor);
+  } else {
+    for (auto& n : op.Inputs("Cond")) {
+      Variable* v = scope->Find(n);
+      if (!v || !v->tensor.initialized() || v->tensor.numel() == 0) run = false;
+    }
+  }
+  if (!run) return;
+  Scope& body = scope->NewScope();
+  const BlockDesc& blk = prog.Block(sb);
+  for (const VarDesc& v : blk.vars)
+    if (!scope->Find(v.name)) body.Var(v.name)->kind = v.type;
+  RunBlock(prog, blk, &body);
+  scope->DropKid(&body);
 }
 
 void Executor::Sync() {
@@ -598,7 +675,6 @@ void Executor::Sync() {
 }
 
 void Executor::RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* scope) {
-  (void)prog;
   const bool dev = ctx_.device >= 0;
   // kernels that only move metadata / holders work on tensors of any device
   static const std::set<std::string> agnostic = {"feed", "fetch", "reshape", "reshape2", "flatten", "flatten2",
@@ -665,7 +741,17 @@ void Executor::RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* 
         }
       }
   };
+  int op_idx = -1;
   for (const OpDesc& op : block.ops) {
+    ++op_idx;
+    if (op.type == "while") {
+      timed(op, [&] { RunWhile(prog, op, scope); });
+      continue;
+    }
+    if (op.type == "conditional_block") {
+      timed(op, [&] { RunConditionalBlock(prog, op, scope); });
+      continue;
+    }
     const Kernel* dk = dev ? find_kernel(op.type, true) : nullptr;
     if (dk) {
       try {
@@ -675,6 +761,11 @@ void Executor::RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* 
       }
     }
     const Kernel* k = find_kernel(op.type, false);
+    if (k == nullptr && fallback) {
+      embedder_fallbacks[op.type] += 1;
+      timed(op, [&] { fallback(op, *scope, block.idx, op_idx); });
+      continue;
+    }
     PA_CHECK(k != nullptr, dk ? "op '%s' declined its device kernel and has no host kernel"
                               : "no kernel registered for op type '%s'", op.type.c_str());
     if (dev && !agnostic.count(op.type))

@@ -162,6 +162,7 @@ class Scope {
   Variable* Find(const std::string& name) const;    // walks up the parents
   Variable* FindLocal(const std::string& name) const;
   Scope& NewScope();
+  void DropKid(Scope* kid);  // frees a child scope created by NewScope()
   void Erase(const std::string& name);
   std::vector<std::string> LocalNames() const;
   const Scope* parent() const { return parent_; }
@@ -230,9 +231,25 @@ class Executor {
   std::map<std::string, std::pair<int64_t, double>> op_time_ms;  // type -> (calls, ms)
   // device executors: ops that ran on host copies (no device kernel, or it declined)
   std::map<std::string, int64_t> host_fallbacks;
+  // Per-op fallback for op types with no C++ kernel (the embedder's registered
+  // kernel, e.g. the Python op library behind fluid.Executor(engine="native")):
+  // called with the op, the scope it runs in, and its (block, op) position.
+  // Unset: such an op is an error (the reference's "kernel not found" enforce).
+  std::function<void(const OpDesc&, Scope&, int, int)> fallback;
+  std::map<std::string, int64_t> embedder_fallbacks;  // op type -> calls through `fallback`
+  // Runs device kernels on an embedder-owned stream (e.g. torch's current stream,
+  // so embedder kernels and ours are ordered without host syncs); null restores
+  // the executor's own stream.
+  void SetStream(void* stream);
+  // sub-block control flow (framework/executor.cc + operators/while_op.cc,
+  // conditional_block_op.cc): forward execution of `while` / `conditional_block`
+  void RunWhile(const ProgramDesc& prog, const OpDesc& op, Scope* scope);
+  void RunConditionalBlock(const ProgramDesc& prog, const OpDesc& op, Scope* scope);
 
  private:
+  bool ReadBool(const Tensor& t);
   ExecContext ctx_;
+  void* own_stream_ = nullptr;
 };
 
 // ---------------------------------------------------------------- tensor IO

@@ -1289,6 +1289,49 @@ void k_increment(const OpRun& r) {
   }
 }
 
+// compare_op.cc / logical_op.cc: elementwise comparisons and logic into BOOL.  Y
+// broadcasts as a trailing block of X (the common scalar-bound loop counter case);
+// values are compared as double (exact for the int32 / int64 counters and fp32).
+double load_d(const Tensor& t, int64_t i) {
+  switch (t.dtype) {
+    case DT::FP32: return t.data<float>()[i];
+    case DT::FP64: return t.data<double>()[i];
+    case DT::INT64: return (double)t.data<int64_t>()[i];
+    case DT::INT32: return t.data<int32_t>()[i];
+    case DT::BOOL: case DT::UINT8: return t.data<uint8_t>()[i];
+    default: fail("compare/logical: input dtype %s", dt_name(t.dtype));
+  }
+}
+
+template <class F>
+void k_binary_bool(const OpRun& r, F f) {
+  Tensor& x = r.in("X");
+  Tensor* yp = r.in_opt("Y");
+  const int64_t n = x.numel();
+  const int64_t ny = yp ? yp->numel() : 1;
+  PA_CHECK(!yp || (ny > 0 && n % ny == 0), "%s: Y (%s) does not broadcast into X (%s)", r.op.type.c_str(),
+           yp ? yp->shape_str().c_str() : "", x.shape_str().c_str());
+  Tensor xs = x;  // keep the input alive when Out aliases it
+  Tensor ys = yp ? *yp : Tensor();
+  Tensor* o = r.out("Out");
+  LoD lod = x.lod;
+  Dims d = x.dims;
+  uint8_t* p = static_cast<uint8_t*>(o->alloc(DT::BOOL, d, -1));
+  o->lod = lod;
+  for (int64_t i = 0; i < n; ++i) p[i] = f(load_d(xs, i), yp ? load_d(ys, i % ny) : 0.0) ? 1 : 0;
+}
+
+void k_less_than(const OpRun& r) { k_binary_bool(r, [](double a, double b) { return a < b; }); }
+void k_less_equal(const OpRun& r) { k_binary_bool(r, [](double a, double b) { return a <= b; }); }
+void k_greater_than(const OpRun& r) { k_binary_bool(r, [](double a, double b) { return a > b; }); }
+void k_greater_equal(const OpRun& r) { k_binary_bool(r, [](double a, double b) { return a >= b; }); }
+void k_equal(const OpRun& r) { k_binary_bool(r, [](double a, double b) { return a == b; }); }
+void k_not_equal(const OpRun& r) { k_binary_bool(r, [](double a, double b) { return a != b; }); }
+void k_logical_and(const OpRun& r) { k_binary_bool(r, [](double a, double b) { return a != 0 && b != 0; }); }
+void k_logical_or(const OpRun& r) { k_binary_bool(r, [](double a, double b) { return a != 0 || b != 0; }); }
+void k_logical_xor(const OpRun& r) { k_binary_bool(r, [](double a, double b) { return (a != 0) != (b != 0); }); }
+void k_logical_not(const OpRun& r) { k_binary_bool(r, [](double a, double) { return a == 0; }); }
+
 void k_delete_var(const OpRun& r) {
   for (auto& n : r.op.Inputs("X"))
     if (Variable* v = r.scope.Find(n)) v->tensor = Tensor();
@@ -1402,6 +1445,16 @@ PA_HOST_KERNEL(sgd, k_sgd);
 PA_HOST_KERNEL(momentum, k_momentum);
 PA_HOST_KERNEL(adam, k_adam);
 PA_HOST_KERNEL(increment, k_increment);
+PA_HOST_KERNEL(less_than, k_less_than);
+PA_HOST_KERNEL(less_equal, k_less_equal);
+PA_HOST_KERNEL(greater_than, k_greater_than);
+PA_HOST_KERNEL(greater_equal, k_greater_equal);
+PA_HOST_KERNEL(equal, k_equal);
+PA_HOST_KERNEL(not_equal, k_not_equal);
+PA_HOST_KERNEL(logical_and, k_logical_and);
+PA_HOST_KERNEL(logical_or, k_logical_or);
+PA_HOST_KERNEL(logical_xor, k_logical_xor);
+PA_HOST_KERNEL(logical_not, k_logical_not);
 PA_HOST_KERNEL(delete_var, k_delete_var);
 
 void link_host_kernels() {}

@@ -147,6 +147,22 @@ PYBIND11_MODULE(paddle_amd_core, m) {
         e.Run(p, &s, block);
         e.Sync();
       }, py::arg("program"), py::arg("scope"), py::arg("block_id") = 0)
+      .def("set_fallback", [](pa::Executor& e, py::object fn) {
+        if (fn.is_none()) {
+          e.fallback = nullptr;
+          return;
+        }
+        // called from RunBlock with the GIL released by run(): take it for the callback
+        auto keep = std::make_shared<py::object>(fn);
+        e.fallback = [keep](const pa::OpDesc& op, pa::Scope& s, int block, int idx) {
+          py::gil_scoped_acquire gil;
+          (*keep)(block, idx, py::cast(&s, py::return_value_policy::reference));
+        };
+      }, py::arg("fn"))
+      .def("set_stream", [](pa::Executor& e, uintptr_t st) { e.SetStream(reinterpret_cast<void*>(st)); },
+           py::arg("stream"))
+      .def("sync", &pa::Executor::Sync)
+      .def_readonly("embedder_fallbacks", &pa::Executor::embedder_fallbacks)
       .def_readwrite("profile", &pa::Executor::profile)
       .def_readonly("op_time_ms", &pa::Executor::op_time_ms)
       .def_readonly("host_fallbacks", &pa::Executor::host_fallbacks);

@@ -3,11 +3,16 @@
 The reference snapshot has no imperative mode; this is the north-star
 DyGraph layer: ``guard()`` selects the device, ``to_variable`` makes a tensor,
 layers are :mod:`paddle_amd.nn` layers (1.x names ``Linear``/``FC``, ``Conv2D``,
-``Pool2D``, ``BatchNorm``, ``Embedding``).  What runs where: tensors are PyTorch
-tensors and autograd is PyTorch's tape; the hot ops (GEMM / linear, attention,
-norms, softmax-CE, SwiGLU/GELU, embedding, AdamW/momentum, RoPE, NHWC conv / BN /
-pool) go to the hand-written gfx950 kernels of ``paddle_amd/csrc/kernels``; every
-other op is an ATen call.
+``Pool2D``, ``BatchNorm``, ``Embedding``).  What runs where: tensor storage is a
+PyTorch-ROCm tensor; autograd is the framework's own eager engine
+(``autograd/engine.py``: recorded grad nodes with hand-written backward rules, no
+torch.autograd); the hot ops (GEMM / linear, attention, norms, softmax-CE,
+SwiGLU/GELU, embedding, AdamW/momentum, RoPE, NHWC conv / BN / pool) are fused
+gfx950 kernels (``paddle_amd/csrc/kernels``), and the remaining pointwise / cast /
+fill / reduction tensor ops issued inside the engine run on the generic HIP
+kernels of ``csrc/kernels/tensor_ops.hip`` (``ops/aten_native.py``).  Whatever is
+still an ATen kernel is counted per op by ``utils/strict.py`` and refused under
+``FLAGS_strict_native=1``.
 """
 from __future__ import annotations
 

@@ -15,9 +15,16 @@ optimizer ops update the very tensors the Python side sees, and a variable whose
 native buffer was re-allocated by a kernel is copied back after the run.  Feeds are
 copied in; fetches are copied out (the only host syncs of a step).
 
-Scope of the engine: dense LoDTensor programs of block 0 (no control-flow
-sub-blocks, no LoD feeds, no SelectedRows); anything else raises
-``NotImplementedError`` naming what is unsupported -- use the default engine for it.
+Scope of the engine: block 0 and the sub-blocks of ``while`` /
+``conditional_block`` (run by the C++ executor itself: Executor::RunWhile /
+RunConditionalBlock), LoD-carrying feeds, and ANY op type: an op with no C++
+kernel is run by its registered Python kernel through the executor's per-op
+fallback callback (the op's inputs are zero-copy views of the native buffers, its
+outputs are lent back to the native scope), counted in ``py_fallbacks``.  On a HIP
+place the native kernels run on torch's current stream, so the two kernel
+libraries are ordered without host syncs.  Programs that need per-step scopes
+(``while_grad``, ``recurrent``, ``conditional_block_grad``) or non-tensor variables
+(SelectedRows gradients) raise ``NotImplementedError`` -- use the default engine.
 
 The engine drives the C++ objects through the ``paddle_amd_core`` CPython
 extension (csrc/pybind/core_module.cc, pybind11) when it is built, else through
@@ -29,16 +36,22 @@ Reference: framework/executor.cc:125-353 (Executor::Run), pybind/pybind.cc:507
 """
 from __future__ import annotations
 
+import ctypes
+import os
+
 import numpy as np
 import torch
-
-import os
 
 from .. import native
 from ..framework import core
 
-_TORCH_DT = {torch.float32: 5, torch.int64: 3, torch.int32: 2, torch.float64: 6, torch.bool: 0, torch.uint8: 20}
+_TORCH_DT = {torch.float32: 5, torch.int64: 3, torch.int32: 2, torch.float64: 6, torch.bool: 0, torch.uint8: 20,
+             torch.float16: 4, torch.int16: 1, torch.int8: 21, torch.bfloat16: 22}
 _DT_TORCH = {v: k for k, v in _TORCH_DT.items()}
+# control-flow ops the C++ executor runs itself, and the ones it cannot take
+_NATIVE_CF = {"while", "conditional_block"}
+_UNSUPPORTED_CF = {"while_grad", "conditional_block_grad", "recurrent", "recurrent_grad", "parallel_do",
+                   "parallel_do_grad", "go", "select"}
 
 
 class _CtypesBinding:
@@ -73,6 +86,8 @@ class _CtypesBinding:
 
     def host_fallbacks(self):
         return self.exe.host_fallbacks()
+
+    supports_fallback = False
 
 
 class _PybindBinding:
@@ -115,6 +130,8 @@ class _PybindBinding:
     def host_fallbacks(self):
         return dict(self.exe.host_fallbacks)
 
+    supports_fallback = True
+
 
 def _binding(device):
     if os.environ.get("FLAGS_native_binding", "pybind") != "ctypes":
@@ -135,6 +152,11 @@ class NativeEngine:
         self._scopes = {}  # id(python scope) -> (scope ref, NativeScope, {name: (ptr, shape, dtype, tensor)})
         self._host_ops = set(native.registered_ops(False))
         self._dev_ops = set(native.registered_ops(True)) if self.device >= 0 else set()
+        self._bexe = None
+        self._wrapped = []
+        self._keep = {}
+        self.py_fallbacks = {}  # op type -> calls run by the Python op library
+        self.py_fallback_types = set()
 
     # ------------------------------------------------------------------ program
     def _program(self, program):
@@ -142,13 +164,17 @@ class NativeEngine:
         ent = self._progs.get(key)
         if ent is not None and ent[0] is program:
             return ent[1], ent[2]
-        block = program.global_block()
-        bad = sorted({op.type for op in block.ops if op.type not in self._host_ops and op.type not in self._dev_ops})
-        if bad:
-            raise NotImplementedError(f"native engine: no C++ kernel for op types {bad}")
-        subs = sorted({op.type for op in block.ops if any(k in op.attrs for k in ("sub_block", "blocks"))})
-        if subs:
-            raise NotImplementedError(f"native engine: control-flow ops with sub-blocks {subs}")
+        all_ops = [op for b in program.blocks for op in b.ops]
+        cf = sorted({op.type for op in all_ops if op.type in _UNSUPPORTED_CF or (
+            any(k in op.attrs for k in ("sub_block", "blocks")) and op.type not in _NATIVE_CF)})
+        if cf:
+            raise NotImplementedError(f"native engine: control-flow ops needing per-step scopes {cf} "
+                                      "(use the default engine)")
+        missing = sorted({op.type for op in all_ops if op.type not in self._host_ops and op.type not in self._dev_ops
+                          and op.type not in _NATIVE_CF})
+        if missing and not self._b.supports_fallback:
+            raise NotImplementedError(f"native engine: no C++ kernel for op types {missing}")
+        self.py_fallback_types = set(missing)
         prog = self._b.program(program.desc.serialize_to_string())
         pers = [v.name for v in program.list_vars()
                 if v.persistable and v.name not in ("feed", "fetch") and v.type == core.VT.LOD_TENSOR]
@@ -182,13 +208,96 @@ class NativeEngine:
             bound[name] = sig + (t,)
 
     def _feed(self, ns, name, data):
+        lod = None
         if isinstance(data, core.LoDTensor):
-            if data.lod():
-                raise NotImplementedError(f"native engine: LoD feed {name}")
+            lod = data.lod()
             data = data._t
         if isinstance(data, torch.Tensor):
             data = data.detach().cpu().numpy()
         self._b.set(ns, name, np.ascontiguousarray(np.asarray(data)), self.device)
+        if lod:
+            if not self._b.supports_fallback:
+                raise NotImplementedError(f"native engine: LoD feed {name} needs the pybind binding")
+            ns.find_var(name).get_tensor().set_lod([list(map(int, lv)) for lv in lod])
+
+    # ------------------------------------------------------------------ per-op Python fallback
+    def _wrap(self, nt):
+        """Zero-copy torch view of a native tensor (host or device)."""
+        dt, shape, ptr, dev = int(nt.dtype()), tuple(nt.shape()), nt.data_ptr(), nt.device()
+        tdt = _DT_TORCH[dt]
+        n = int(np.prod(shape)) if shape else 1
+        if n == 0 or not ptr:
+            return torch.empty(shape, dtype=tdt, device=self._tdev() if dev >= 0 else "cpu")
+        esz = torch.empty((), dtype=tdt).element_size()
+        self._wrapped.append((ptr, ptr + n * esz))
+        if dev < 0:
+            buf = (ctypes.c_byte * (n * esz)).from_address(ptr)
+            return torch.frombuffer(buf, dtype=tdt).reshape(shape)
+        ints = {1: "|i1", 2: "<i2", 4: "<i4", 8: "<i8"}[esz]
+        holder = type("_NativeView", (), {"__cuda_array_interface__": {
+            "shape": shape, "typestr": ints, "data": (ptr, False), "version": 2, "strides": None}})()
+        return torch.as_tensor(holder, device=torch.device("cuda", dev)).view(tdt)
+
+    def _aliases_native(self, t):
+        lo = t.data_ptr()
+        hi = lo + t.numel() * t.element_size()
+        return any(lo < b and a < hi for a, b in self._wrapped)
+
+    def _py_op(self, program, scope, blk, idx, ns):
+        """Run op ``idx`` of block ``blk`` with its registered Python kernel on the
+        native scope ``ns``."""
+        from ..framework import registry as R
+        from ..framework.executor import BlockExecutor
+
+        if self._bexe is None:
+            self._bexe = BlockExecutor(self.place)
+        pb = self._bexe.prepare(program, blk)
+        info, op, ins, outs, attrs = pb.steps[idx]
+        self._wrapped = []
+        ctx_ins = {}
+        for slot, names in ins:
+            vals = []
+            for n in names:
+                v = ns.find_var(n)
+                if v is None or not v.is_initialized():
+                    vals.append(None)
+                    continue
+                nt = v.get_tensor()
+                lt = core.LoDTensor(self._wrap(nt))
+                lod = nt.lod()
+                if lod:
+                    lt.set_lod(lod)
+                vals.append(lt)
+            ctx_ins[slot] = vals
+        ctx = R.KernelContext(op.type, ctx_ins, outs, attrs, self.place, scope, op, self._bexe)
+        R.run_kernel(info, ctx)
+        self.py_fallbacks[op.type] = self.py_fallbacks.get(op.type, 0) + 1
+        keep = self._keep.setdefault(id(ns), {})
+        for slot, vals in ctx.results.items():
+            for n, v in zip(outs.get(slot, []), vals):
+                if v is None or n == R.EMPTY_VAR:
+                    continue
+                if isinstance(v, torch.Tensor):
+                    v = core.LoDTensor(v)
+                if not isinstance(v, core.LoDTensor):
+                    raise NotImplementedError(f"native engine: op {op.type} output {n} is a "
+                                              f"{type(v).__name__} (LoDTensor only)")
+                t = v.tensor
+                if t is None:
+                    continue
+                if t.device != self._tdev():
+                    t = t.to(self._tdev())
+                if t.dtype not in _TORCH_DT:
+                    raise NotImplementedError(f"native engine: op {op.type} output {n} dtype {t.dtype}")
+                if not t.is_contiguous() or self._aliases_native(t):
+                    t = t.contiguous() if not t.is_contiguous() and not self._aliases_native(t) else t.clone()
+                keep[n] = t  # alive while the native scope references it
+                var = ns.find_var(n)  # an enclosing scope's variable is updated in place
+                nt = (var if var is not None else ns.var(n)).get_tensor()
+                nt.share_external(t.data_ptr(), self._b.C.VarType(_TORCH_DT[t.dtype]), list(t.shape),
+                                  self.device)
+                nt.set_lod([list(map(int, lv)) for lv in (v.lod() or [])])
+        self._wrapped = []
 
     def _write_back(self, scope, ns, bound, name):
         """After a run: a persistable whose native buffer moved is copied into a torch
@@ -224,9 +333,18 @@ class NativeEngine:
                 self._lend(ns, bound, name, val)
         for name, data in feed.items():
             self._feed(ns, name, data)
-        if self.device >= 0:
+        if self._b.supports_fallback:
+            self._b.exe.set_fallback(lambda blk, idx, s, p=program, sc=scope: self._py_op(p, sc, blk, idx, s))
+            if self.device >= 0:
+                # one stream for both kernel libraries: no host sync between them
+                self._b.exe.set_stream(torch.cuda.current_stream(self._tdev()).cuda_stream)
+        elif self.device >= 0:
             torch.cuda.current_stream(self._tdev()).synchronize()  # lent tensors written by torch
-        self._b.run(prog, ns)  # ends with a sync of the native stream
+        try:
+            self._b.run(prog, ns)  # ends with a sync of the native stream
+        finally:
+            if self._b.supports_fallback:
+                self._b.exe.set_fallback(None)
         for name in pers:
             self._write_back(scope, ns, bound, name)
         outs = []

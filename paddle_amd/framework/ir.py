@@ -12,8 +12,8 @@ hazards are explicit edges.  Passes rewrite the graph; ``graph_to_program`` writ
 the topologically sorted ops back into the block.
 
 MI355X note: the passes that matter on this hardware are the ones that turn
-several memory-bound kernels into one (GEMM + bias epilogue in hipBLASLt's fused
-``fc``, conv+BN folding, dropout/scale removal at inference): each removed op is
+several memory-bound kernels into one (GEMM + bias epilogue of the native MFMA
+GEMM behind ``fc``, conv+BN folding, dropout/scale removal at inference): each removed op is
 one fewer full pass over HBM.
 """
 from __future__ import annotations
@@ -452,7 +452,7 @@ def _new_op(block, type, inputs, outputs, attrs):
 class FCFusePass(Pass):
     """mul(X, W) -> t; elementwise_add(t, b) -> out  ==>  fc(Input=X, W, Bias=b) -> out
     (fc_fuse_pass.cc).  With ``with_relu`` a following relu folds in as the fc
-    activation (hipBLASLt bias+ReLU epilogue, one pass over the output)."""
+    activation (bias in the native GEMM epilogue, one activation pass)."""
 
     def apply_impl(self, graph):
         d = GraphPatternDetector()

@@ -4,8 +4,8 @@ sharding stage-3".
 
 Not in the Fluid 0.14 reference; Paddle-side behaviour follows
 PaddleNLP's ``GPTForPretraining``.  MI355X design mirrors :mod:`.llama`:
-  * fused QKV ``[H, 3H]`` and MLP ``[H, 4H]`` GEMMs (hipBLASLt), Paddle ``[in, out]``
-    weights; attention runs the gfx950 flash kernel directly on strided q/k/v views
+  * fused QKV ``[H, 3H]`` and MLP ``[H, 4H]`` GEMMs on the hand-written MFMA GEMM
+    (``csrc/kernels/gemm.hip``), Paddle ``[in, out]`` weights; attention runs the gfx950 flash kernel directly on strided q/k/v views
     of the packed QKV output (no copies);
   * the residual add is fused into the following LayerNorm kernel;
   * Megatron TP (column QKV / fc1, row o-proj / fc2, vocab-parallel embedding and

@@ -6,8 +6,9 @@ reference behaviour is PaddleNLP's ``LlamaForCausalLM`` with
 (neox "rotate-half") positions, SwiGLU MLP, untied LM head.
 
 MI355X design:
-  * one fused QKV GEMM and one fused gate|up GEMM per block (hipBLASLt), weights in
-    Paddle's ``[in, out]`` layout;
+  * one fused QKV GEMM and one fused gate|up GEMM per block on the hand-written
+    gfx950 MFMA GEMM (``csrc/kernels/gemm.hip``), weights in Paddle's ``[in, out]``
+    layout;
   * rotary + causal flash attention in one autograd node on the packed QKV output
     (``ops.rope_attention``: gfx950 MFMA kernels, no q/k/v copies);
   * the residual add is fused into the following RMSNorm (``residual=`` path), so

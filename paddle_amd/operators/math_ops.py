@@ -3,9 +3,12 @@
 Parity: paddle/fluid/operators/{mul,matmul,elementwise_*,activation,scale,sum,mean,
 reduce_*,clip,clip_by_norm,cumsum,minus,sign,l1_norm,squared_l2_norm,
 squared_l2_distance,cos_sim,norm}_op.* (SURVEY §2.7 "Dense NN / math").
-Kernels are device-agnostic torch expressions; on the HIP device they run as
-hipBLASLt GEMMs / fused elementwise launches, with hand-written gfx950 kernels
-for the hot fused ops (see paddle_amd/ops).  Gradients of ops without an
+On the HIP device mul / matmul / fc run on the framework's exact-fp32 MFMA GEMM
+(``ops/blas.py`` -> ``csrc/kernels/convnd.hip``; bf16 on ``gemm.hip``), and the
+elementwise / activation / reduction expressions of the other kernels run on the
+generic strided kernels of ``csrc/kernels/tensor_ops.hip`` (native dispatch inside
+the executor's op region, ``ops/aten_native.py``).  Shapes the native GEMM does not
+cover fall back to ATen and are counted by ``utils/strict.py``.  Gradients of ops without an
 explicit ``*_grad`` kernel come from the registry's automatic VJP.
 """
 from __future__ import annotations
@@ -43,8 +46,8 @@ def mul(ctx):
 def fc(ctx):
     """Fused fully-connected op produced by ``fc_fuse_pass`` (reference fc_op.cc:154):
     Out = act(flatten(Input, in_num_col_dims) @ W + Bias).  On the HIP device the
-    bias (and ReLU/GELU) ride the hipBLASLt epilogue of one GEMM instead of
-    separate elementwise passes over the output."""
+    bias rides the epilogue of the native MFMA GEMM (``ops/blas.py`` fc); the
+    activation is one pass of the native elementwise kernels."""
     x, w = ctx.input("Input"), ctx.input("W")
     n = ctx.attr("in_num_col_dims")
     x2 = _flat2(x, n)

@@ -38,7 +38,8 @@ U = dict(copy=0, fill=1, neg=2, abs=3, exp=4, log=5, sqrt=6, rsqrt=7, sin=8, cos
          reciprocal=13, floor=14, ceil=15, round=16, trunc=17, sign=18, affine=19, pows=20, clamp=21,
          logical_not=22, erf=23, log1p=24, expm1=25, gelu=26, gelu_tanh=27, silu=28, leaky_relu=29, elu=30,
          softplus=31, log2=32, isnan=33, isinf=34, isfinite=35, bitwise_not=36, rpow=37, hardsigmoid=38,
-         hardswish=39, square=40, clamp_min=41, clamp_max=42, atan=43, log10=44, exp2=45, frac=46, mish=47)
+         hardswish=39, square=40, clamp_min=41, clamp_max=42, atan=43, log10=44, exp2=45, frac=46, mish=47,
+         iota=48)
 B = dict(add=50, sub=51, mul=52, div=53, maximum=54, minimum=55, pow=56, eq=57, ne=58, lt=59, le=60, gt=61, ge=62,
          logical_and=63, logical_or=64, logical_xor=65, floor_divide=66, remainder=67, atan2=68, fmod=69,
          threshold_backward=70, sigmoid_backward=71, tanh_backward=72, bitwise_and=73, bitwise_or=74,
@@ -62,6 +63,10 @@ def _lib():
         L.pa_ew.restype = I
         L.pa_reduce_any.argtypes = [I, I, P, I, P, I, Lg, Lg, Lg, D, P, Lg, P]
         L.pa_reduce_any.restype = Lg
+        L.pa_index_select.argtypes = [P, I, Lg, Lg, Lg, P, I, Lg, P, P]
+        L.pa_index_select.restype = I
+        L.pa_cumsum.argtypes = [I, P, I, P, I, Lg, Lg, Lg, P]
+        L.pa_cumsum.restype = I
         _lib_ready[0] = True
     return L
 
@@ -299,7 +304,7 @@ def _unary_out(x, op, shape, odt, inplace, out, a=0.0, b=0.0, cdt=None):
 
 for _n in _BIN:
     for _s in ("Tensor", "Scalar", "out", "Tensor_Tensor", "Tensor_Scalar", "Tensor_mode", "Scalar_mode",
-               "Self", "Scalar_Tensor"):
+               "Self", "Scalar_Tensor", "default"):
         HANDLERS[f"{_n}.{_s}"] = _binary
         HANDLERS[f"{_n}_.{_s}"] = _binary
 
@@ -839,3 +844,195 @@ def _softmax_bwd(name, grad, output, dim, input_dtype):
     N.call("pa_softmax_bwd", N.dt(grad), N.ptr(output), N.ptr(grad), N.ptr(dx), grad.numel() // grad.shape[-1],
            grad.shape[-1], int(name.startswith("_log")), N.stream())
     return dx
+
+
+# ---------------------------------------------------------------------------- matmul
+def _bf16_operands(a, b):
+    """(A tensor, a_kmaj, B tensor, b_kmaj) in the layouts ops/gemm.py takes, or None."""
+    if a.stride(1) == 1:
+        A, ak = a, True
+    elif a.stride(0) == 1:
+        A, ak = a.t(), False
+    else:
+        return None
+    if b.stride(0) == 1:
+        Bm, bk = b.t(), True
+    elif b.stride(1) == 1:
+        Bm, bk = b, False
+    else:
+        return None
+    return A, ak, Bm, bk
+
+
+def _mm_bf16(a, b, bias=None):
+    from . import gemm as G
+
+    M, K = a.shape
+    Nn = b.shape[1]
+    ops = _bf16_operands(a, b)
+    _need(ops is not None)
+    A, ak, Bm, bk = ops
+    _need(G.supported(M, Nn, K, A, Bm))
+    return G.gemm(A, Bm, M, Nn, K, a_kmaj=ak, b_kmaj=bk, bias=bias)
+
+
+@_h("mm.default")
+def _mm(name, self, mat2):
+    _need(_ok(self) and _ok(mat2) and self.dtype == mat2.dtype and self.dim() == 2 and mat2.dim() == 2)
+    _need(self.numel() > 0 and mat2.numel() > 0)
+    if self.dtype == torch.float32:
+        from . import blas
+
+        return blas._bmm(self, mat2)
+    _need(self.dtype == torch.bfloat16)
+    return _mm_bf16(self, mat2)
+
+
+@_h("bmm.default")
+def _bmm_h(name, self, mat2):
+    _need(_ok(self) and _ok(mat2) and self.dtype == mat2.dtype == torch.float32)
+    _need(self.dim() == 3 and mat2.dim() == 3 and self.shape[0] <= 65535 and self.numel() > 0 and mat2.numel() > 0)
+    from . import blas
+
+    return blas._bmm(self, mat2)
+
+
+@_h("addmm.default")
+def _addmm(name, bias, mat1, mat2, beta=1, alpha=1):
+    _need(_ok(bias) and _ok(mat1) and _ok(mat2) and mat1.dtype == mat2.dtype == bias.dtype)
+    _need(_sval(beta) == 1 and _sval(alpha) == 1 and mat1.numel() > 0 and mat2.numel() > 0)
+    M, K = mat1.shape
+    Nn = mat2.shape[1]
+    if mat1.dtype == torch.float32:
+        from . import convnd as _C
+
+        c = torch.empty(M, Nn, dtype=torch.float32, device=mat1.device)
+        _need(_launch(U["copy"], c, [bias], cdt=0))  # bias broadcast into C, GEMM accumulates (beta = 1)
+        _C.sgemm(mat1, mat1.stride(0), mat1.stride(1), mat2, mat2.stride(0), mat2.stride(1), c, Nn, M, Nn, K, beta=1.0)
+        return c
+    _need(mat1.dtype == torch.bfloat16 and (bias.dim() == 1 or (bias.dim() == 2 and bias.shape[0] == 1)))
+    b1 = bias.reshape(-1)
+    _need(b1.numel() == Nn and b1.is_contiguous())
+    return _mm_bf16(mat1, mat2, bias=b1)
+
+
+# ---------------------------------------------------------------------------- indexing / scans
+def _index_select_impl(x, dim, index):
+    _need(_ok(x) and _ok(index) and index.dtype in (torch.int64, torch.int32) and index.dim() <= 1)
+    nd = x.dim()
+    dim = dim % nd if nd else 0
+    src = x if x.is_contiguous() else _to_copy("_to_copy.default", x, memory_format=torch.contiguous_format)
+    idx = index.reshape(-1)
+    if not idx.is_contiguous():
+        idx = _to_copy("_to_copy.default", idx, memory_format=torch.contiguous_format)
+    shape = list(x.shape)
+    outer, nsrc, inner = math.prod(shape[:dim]), shape[dim] if nd else 1, math.prod(shape[dim + 1:])
+    shape[dim:dim + 1] = [idx.numel()] if nd else []
+    out = torch.empty(shape, dtype=x.dtype, device=x.device)
+    rc = _lib().pa_index_select(src.data_ptr(), src.element_size(), outer, nsrc, inner, idx.data_ptr(),
+                                int(idx.dtype == torch.int64), idx.numel(), out.data_ptr(), N.stream())
+    N.check(rc, "pa_index_select")
+    return out
+
+
+@_h("index_select.default")
+def _index_select(name, self, dim, index):
+    return _index_select_impl(self, dim, index)
+
+
+@_h("embedding.default")
+def _embedding(name, weight, indices, padding_idx=-1, scale_grad_by_freq=False, sparse=False):
+    _need(_ok(weight) and _ok(indices) and weight.dim() == 2)
+    flat = indices.reshape(-1)
+    out = _index_select_impl(weight, 0, flat)
+    return out.reshape(list(indices.shape) + [weight.shape[1]])
+
+
+@_h("index.Tensor")
+def _index(name, self, indices):
+    # the common case: one integer index tensor on the first dim (x[idx])
+    _need(len(indices) == 1 and indices[0] is not None and _ok(indices[0])
+          and indices[0].dtype in (torch.int64, torch.int32))
+    ix = indices[0]
+    out = _index_select_impl(self, 0, ix.reshape(-1))
+    return out.reshape(list(ix.shape) + list(self.shape[1:]))
+
+
+@_h("arange.start_step", "arange.default", "arange.start")
+def _arange(name, *args, dtype=None, layout=None, device=None, pin_memory=None):
+    _need(_factory_dev(device))
+    vals = [_sval(a) for a in args]
+    _need(all(isinstance(v, (int, float)) for v in vals))
+    if len(vals) == 1:
+        start, end, step = 0, vals[0], 1
+    elif len(vals) == 2:
+        (start, end), step = vals, 1
+    else:
+        start, end, step = vals
+    if dtype is None:
+        dtype = torch.int64 if all(isinstance(v, int) for v in (start, end, step)) else torch.get_default_dtype()
+    _need(dtype in _DT and step != 0)
+    n = max(0, math.ceil((end - start) / step))
+    out = torch.empty(n, dtype=dtype, device=device)
+    if n:
+        _need(_launch(U["iota"], out, [], a=start, b=step, cdt=_cdt(dtype) if dtype in _FLOATS else 1))
+    return out
+
+
+@_h("constant_pad_nd.default")
+def _pad(name, self, pad, value=0):
+    _need(_ok(self) and len(pad) % 2 == 0 and len(pad) // 2 <= self.dim() and all(p >= 0 for p in pad))
+    shape = list(self.shape)
+    sl = []
+    for k in range(len(pad) // 2):
+        d = self.dim() - 1 - k
+        lo, hi = pad[2 * k], pad[2 * k + 1]
+        shape[d] += lo + hi
+        sl.append((d, lo))
+    out = torch.empty(shape, dtype=self.dtype, device=self.device)
+    _need(_launch(U["fill"], out, [], a=_sval(value), cdt=_cdt(self.dtype)))
+    view = out
+    for d, lo in sl:
+        view = view.narrow(d, lo, self.shape[d])
+    _need(_launch(U["copy"], view, [self], cdt=_cdt(self.dtype)))
+    return out
+
+
+@_h("cumsum.default")
+def _cumsum(name, self, dim, dtype=None):
+    _need(_ok(self))
+    odt = dtype or (torch.int64 if self.dtype in (torch.bool, torch.uint8, torch.int8, torch.int16, torch.int32,
+                                                   torch.int64) else self.dtype)
+    _need(odt in _DT)
+    nd = self.dim()
+    dim = dim % nd if nd else 0
+    src = self if self.is_contiguous() else _to_copy("_to_copy.default", self, memory_format=torch.contiguous_format)
+    shape = list(self.shape)
+    out = torch.empty(shape, dtype=odt, device=self.device)
+    outer, R, inner = math.prod(shape[:dim]), (shape[dim] if nd else 1), math.prod(shape[dim + 1:])
+    rc = _lib().pa_cumsum(_cdt(odt), src.data_ptr(), _DT[src.dtype], out.data_ptr(), _DT[odt], outer, R, inner,
+                          N.stream())
+    N.check(rc, "pa_cumsum")
+    return out
+
+
+@_h("var.correction", "var_mean.correction", "std.correction")
+def _var(name, self, dim=None, correction=None, keepdim=False):
+    _need(_ok(self) and self.dtype in _FLOATS and self.numel() > 0)
+    corr = 1 if correction is None else _sval(correction)
+    dims = _norm_dims(dim, self.dim())
+    n = math.prod(self.shape[d] for d in dims) if dims else self.numel()
+    mean = _reduce(RED["mean"], self, dims, True, self.dtype)
+    dev = torch.empty(self.shape, dtype=torch.float32 if self.dtype != torch.float64 else torch.float64,
+                      device=self.device)
+    _need(_launch(B["sub"], dev, [self, mean], a=1.0))
+    _need(_launch(U["square"], dev, [dev]))
+    ss = _reduce(RED["sum"], dev, dims, keepdim, self.dtype, cdt=_cdt(dev.dtype))
+    var = torch.empty(ss.shape, dtype=self.dtype, device=self.device)
+    _need(_launch(U["affine"], var, [ss], a=1.0 / max(n - corr, 0) if n - corr > 0 else math.nan, b=0.0))
+    if name.startswith("std"):
+        _need(_launch(U["sqrt"], var, [var]))
+        return var
+    if name.startswith("var_mean"):
+        return var, (mean if keepdim else mean.reshape(ss.shape))
+    return var

@@ -934,7 +934,8 @@ class _LinearFn(torch.autograd.Function):
 
     If the weight carries ``_pa_main_grad`` (a view into a flat gradient buffer
     owned by the sharded DP engine), the weight-gradient GEMM accumulates straight
-    into it (hipBLASLt beta=1: dW += x^T dy, one rounding); the engine's
+    into it (the native GEMM's fp32 accumulate epilogue: dW += x^T dy, one
+    rounding; the first write after zero_grad overwrites); the engine's
     post-accumulate-grad hook still fires for w, so bucket readiness is unchanged
     -- no temporary dW, no separate accumulate kernel.  The bias is added in the
     GEMM epilogue and its gradient is one HIP column reduction (``pa_bias_act_bwd``).

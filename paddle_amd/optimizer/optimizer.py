@@ -20,6 +20,8 @@ import math
 
 import torch
 
+from ..utils import strict as _strict
+
 from ..ops import optim as fused_optim
 from .lr import LRScheduler
 
@@ -134,6 +136,10 @@ class Optimizer:
 
     # ---------------------------------------------------------------- step
     def clear_grad(self, set_to_zero=True):
+        with _strict.region("optimizer:clear_grad"):
+            self._clear_grad(set_to_zero)
+
+    def _clear_grad(self, set_to_zero):
         for p in self._parameter_list:
             if p.grad is not None:
                 if set_to_zero:
@@ -158,6 +164,11 @@ class Optimizer:
 
     @torch.no_grad()
     def step(self):
+        # framework region: the update's tensor expressions run on the HIP kernels
+        with _strict.region("optimizer:step"):
+            self._step()
+
+    def _step(self):
         self._step_count += 1
         pg = [(p, p.grad) for p in self._parameter_list if p.grad is not None and p.requires_grad]
         if self._grad_clip is not None:

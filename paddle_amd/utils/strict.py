@@ -35,6 +35,7 @@ from torch.utils._python_dispatch import TorchDispatchMode
 
 ATEN_KERNELS: dict = {}   # "label:aten_op" -> ATen kernel launches on GPU tensors inside regions
 NATIVE_OPS: dict = {}     # aten op -> calls executed on the framework's HIP kernels (ops/aten_native.py)
+SYNCS: dict = {}          # region label -> device->host scalar reads (item() / float())
 FALLBACKS: dict = {}      # site -> explicit fallback count
 _TLS = threading.local()
 # device types whose ATen kernels count (tests add "cpu" to exercise the watcher here)
@@ -89,6 +90,23 @@ def _is_gpu(x):
     return isinstance(x, torch.Tensor) and x.device.type in WATCH_DEVICES
 
 
+def _label():
+    labels = getattr(_TLS, "labels", None)
+    return labels[-1] if labels else "?"
+
+
+def _crosses_host(args, kwargs):
+    """A copy with one side in host memory (H2D / D2H transfer)."""
+    devs = set()
+    for a in list(args) + list(kwargs.values()):
+        if isinstance(a, torch.Tensor):
+            devs.add(a.device.type)
+    dev = kwargs.get("device")
+    if dev is not None:
+        devs.add(torch.device(dev).type)
+    return "cpu" in devs and len(devs) > 1
+
+
 def _touches_gpu(args, kwargs):
     dev = kwargs.get("device")
     if dev is not None and torch.device(dev).type in WATCH_DEVICES:
@@ -114,6 +132,11 @@ class _Watch(TorchDispatchMode):
         ns = getattr(func, "namespace", "aten")
         name = func._schema.name.split("::")[-1] if hasattr(func, "_schema") else str(func)
         if ns == "aten" and name not in _FREE and _touches_gpu(args, kwargs):
+            if name in ("_to_copy", "copy_") and _crosses_host(args, kwargs):
+                return func(*args, **kwargs)  # host <-> device transfer: a DMA copy, no kernel
+            if name == "_local_scalar_dense":
+                SYNCS[_label()] = SYNCS.get(_label(), 0) + 1  # device -> host read (a sync)
+                return func(*args, **kwargs)
             if self.native:
                 from ..ops import aten_native
 
@@ -187,7 +210,9 @@ def reset():
     ATEN_KERNELS.clear()
     FALLBACKS.clear()
     NATIVE_OPS.clear()
+    SYNCS.clear()
 
 
 def report() -> dict:
-    return {"aten_kernels": dict(ATEN_KERNELS), "fallbacks": dict(FALLBACKS), "native_ops": dict(NATIVE_OPS)}
+    return {"aten_kernels": dict(ATEN_KERNELS), "fallbacks": dict(FALLBACKS), "native_ops": dict(NATIVE_OPS),
+            "syncs": dict(SYNCS)}

@@ -74,7 +74,10 @@ def test_transposed_and_noncontiguous_operands():
     _check(lambda a: a[:, ::2] * 2, x, exact=True)
     _check(lambda a: a.t().contiguous(), x, exact=True)
     z = torch.randn(2, 3, 8, 8, device=dev).to(memory_format=torch.channels_last)
-    _check(lambda a: (a + 1).stride(), z, expect_native=False)
+    with S.region("test"):
+        zz = z + 1
+    assert zz.stride() == (z + 1).stride()  # channels-last activations stay channels-last
+    _check(lambda a: a + 1, z, exact=True)
 
 
 def test_unary_and_activations():
@@ -187,3 +190,28 @@ def test_strict_mode_raises_on_uncovered_op(monkeypatch):
             torch.linalg.qr(x)
     with S.region("test"):
         (x + 1).sum()  # covered: no error
+
+
+def test_indexing_scans_padding_var():
+    x = torch.randn(6, 5, 7, device=dev)
+    idx = torch.tensor([4, 0, 0, 2], device=dev)
+    _check(lambda a, i: a.index_select(1, i), x, idx, exact=True)
+    _check(lambda a, i: a[i], x, idx, exact=True)
+    w = torch.randn(20, 8, device=dev).to(torch.bfloat16)
+    ids = torch.randint(0, 20, (3, 5), device=dev)
+    _check(lambda a, i: torch.nn.functional.embedding(i, a), w, ids, exact=True)
+    _check(lambda a: torch.arange(3, 17, 2, device=dev) + 0 * a.sum().long(), x, expect_native=False)
+    _check(lambda a: torch.nn.functional.pad(a, (1, 2, 0, 3), value=-1.0), x, exact=True)
+    _check(lambda a: a.cumsum(1), x, atol=1e-5)
+    _check(lambda a: torch.var(a, 2), x, atol=1e-5)
+    _check(lambda a: torch.var_mean(a, (0, 2), keepdim=True), x, atol=1e-5)
+
+
+def test_matmul_handlers():
+    a = torch.randn(64, 48, device=dev)
+    b = torch.randn(48, 40, device=dev)
+    _check(lambda x, y: x @ y, a, b, atol=1e-4, rtol=1e-4)
+    _check(lambda x, y: torch.addmm(torch.ones(40, device=dev), x, y), a, b, atol=1e-4, rtol=1e-4)
+    ab, bb = a.to(torch.bfloat16), b.to(torch.bfloat16)
+    _check(lambda x, y: x @ y, ab, bb, atol=3e-2, rtol=2e-2)
+    _check(lambda x, y: x.t() @ y.t().contiguous().t(), ab[:48, :40].contiguous(), bb, atol=3e-2, rtol=2e-2)

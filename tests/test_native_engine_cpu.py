@@ -41,14 +41,45 @@ def test_native_engine_updates_python_scope_in_place():
         assert not np.allclose(t_after.numpy(), v0.numpy())
 
 
-def test_native_engine_rejects_unsupported_programs():
+def test_native_engine_python_fallback_lod_and_control_flow():
+    """Ops without a C++ kernel (sequence_softmax on a LoD feed) run through the
+    executor's per-op Python fallback; programs needing per-step scopes raise."""
     main, startup = fluid.Program(), fluid.Program()
     with fluid.program_guard(main, startup):
-        x = fluid.layers.data("x", [4])
+        x = fluid.layers.data("x", [4], lod_level=1)
         y = fluid.layers.sequence_softmax(fluid.layers.fc(x, 1))
+    scope = fluid.core.Scope()
+    place = fluid.CPUPlace()
+    xv = fluid.create_lod_tensor(np.random.RandomState(0).rand(5, 4).astype("float32"), [[2, 3]], place)
+    with fluid.executor.scope_guard(scope):
+        fluid.Executor(place).run(startup)
+        (ref,) = fluid.Executor(place).run(main, feed={"x": xv}, fetch_list=[y])
+        exe = fluid.Executor(place, engine="native")
+        (got,) = exe.run(main, feed={"x": xv}, fetch_list=[y])
+    np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-7)
+    assert exe._native.py_fallbacks.get("sequence_softmax") == 1
+
+
+def test_native_engine_rejects_step_scope_programs():
+    main, startup = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, startup):
+        x = fluid.layers.data("x", [4], dtype="float32")
+        x.stop_gradient = False
+        i = fluid.layers.fill_constant([1], "int64", 0)
+        n = fluid.layers.fill_constant([1], "int64", 2)
+        acc = fluid.layers.fill_constant([1, 4], "float32", 0.0)
+        cond = fluid.layers.less_than(i, n)
+        loop = fluid.layers.While(cond)
+        with loop.block():
+            fluid.layers.assign(fluid.layers.elementwise_add(acc, x), acc)
+            fluid.layers.increment(i, in_place=True)
+            fluid.layers.less_than(i, n, cond=cond)
+        loss = fluid.layers.mean(acc)
+        fluid.backward.append_backward(loss)
     exe = fluid.Executor(fluid.CPUPlace(), engine="native")
     scope = fluid.core.Scope()
     with fluid.executor.scope_guard(scope):
         fluid.Executor(fluid.CPUPlace()).run(startup)
-        with pytest.raises(NotImplementedError, match="sequence_softmax"):
-            exe.run(main, feed={"x": np.zeros((2, 4), "float32")}, fetch_list=[y])
+        if any(op.type == "while_grad" for b in main.blocks for op in b.ops):
+            with pytest.raises(NotImplementedError, match="while_grad"):
+                exe.run(main, feed={"x": np.zeros((1, 4), "float32")}, fetch_list=[loss])

@@ -49,5 +49,7 @@ for r in recs:
         t_aten += r["dur_ns"]
     else:
         ours[k] = ours.get(k, 0) + 1
+from paddle_amd.utils import strict  # noqa: E402
+
 print(json.dumps({"kernels": len(recs), "aten_kernels": sum(aten.values()), "aten_time_frac": t_aten / max(t_all, 1),
-                  "aten": aten, "other": ours}, indent=1))
+                  "aten": aten, "other": ours, "strict_report": strict.report()}, indent=1))
