@@ -63,10 +63,35 @@ __host__ __device__ __forceinline__ void bn_layout(int C, int& chunks, int& rsub
 // partial[g][0][c] = sum(x - shift), partial[g][1][c] = sum((x - shift)^2)   (fwd)
 // partial[g][0][c] = sum(dy'),       partial[g][1][c] = sum(dy' * (x - mean)) (bwd)
 // with dy' = dy * (y > 0) when relu.
+// Per-channel affine of the forward (sc = rstd * w, sf = b - mean * sc) for 8 channels:
+// the ReLU mask of relu(BN(x)) is recomputed in backward as fmaf(x, sc, sf) > 0 --
+// the same expression bn_apply_kernel evaluated -- instead of reading y back.
+__device__ __forceinline__ void bn_affine8(int ch, const float* __restrict__ mean, const float* __restrict__ rstd,
+                                           const void* __restrict__ w, const void* __restrict__ b, int wdt,
+                                           float (&sc)[8], float (&sf)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = ch * 8 + j;
+    const float ww = w ? (wdt ? bf2f(((const u16*)w)[c]) : ((const float*)w)[c]) : 1.f;
+    const float bb = b ? (wdt ? bf2f(((const u16*)b)[c]) : ((const float*)b)[c]) : 0.f;
+    sc[j] = rstd[c] * ww;
+    sf[j] = bb - mean[c] * sc[j];
+  }
+}
+
+struct BnMask {  // relu-mask source of the backward kernels
+  const u16* y;  // forward output (residual layers), or null: recompute from x
+  const float* rstd;
+  const void* w;
+  const void* b;
+  int wdt;
+};
+
 template <bool BWD>
 __global__ __launch_bounds__(BN_T) void bn_reduce_kernel(const u16* __restrict__ x, const u16* __restrict__ dy,
-                                                          const u16* __restrict__ y, const float* __restrict__ mean,
+                                                          BnMask mk, const float* __restrict__ mean,
                                                           float* __restrict__ partial, long rows, int C, int relu) {
+  const u16* __restrict__ y = mk.y;
   int chunks, rsub;
   bn_layout(C, chunks, rsub);
   extern __shared__ __attribute__((aligned(16))) float red[];  // [rsub][C] x 2
@@ -76,13 +101,14 @@ __global__ __launch_bounds__(BN_T) void bn_reduce_kernel(const u16* __restrict__
     const int ch = cb + tid % chunk_per_iter;
     const int rs = tid / chunk_per_iter;
     const bool active = ch < chunks && rs < rsub;
-    float s0[8], s1[8], sh[8];
+    float s0[8], s1[8], sh[8], msc[8], msf[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s0[j] = s1[j] = 0.f;
+    for (int j = 0; j < 8; ++j) s0[j] = s1[j] = msc[j] = msf[j] = 0.f;
     if (active) {
       if (BWD) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) sh[j] = mean[ch * 8 + j];
+        if (relu && !y) bn_affine8(ch, mean, mk.rstd, mk.w, mk.b, mk.wdt, msc, msf);
       } else {
         load8(x + ch * 8, sh);  // first pixel = shift
       }
@@ -92,11 +118,14 @@ __global__ __launch_bounds__(BN_T) void bn_reduce_kernel(const u16* __restrict__
         if (BWD) {
           float g[8];
           load8(dy + r * C + ch * 8, g);
-          if (relu) {
+          if (relu && y) {
             float yy[8];
             load8(y + r * C + ch * 8, yy);
 #pragma unroll
             for (int j = 0; j < 8; ++j) g[j] = yy[j] > 0.f ? g[j] : 0.f;
+          } else if (relu) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) g[j] = fmaf(a[j], msc[j], msf[j]) > 0.f ? g[j] : 0.f;
           }
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
@@ -245,9 +274,10 @@ __global__ __launch_bounds__(1024) void bn_finalize_bwd_kernel(const float* __re
 }
 
 // dx = k1 * dy' - k1 * k2 - k3 * (x - mean)   (fixed channel chunk per thread, as bn_apply)
-__global__ void bn_dx_kernel(const u16* __restrict__ x, const u16* __restrict__ dy, const u16* __restrict__ y,
+__global__ void bn_dx_kernel(const u16* __restrict__ x, const u16* __restrict__ dy, BnMask mk,
                              const float* __restrict__ mean, const float* __restrict__ coef, u16* __restrict__ dx,
                              long rows, int C, int relu, u16* __restrict__ dres) {
+  const u16* __restrict__ y = mk.y;
   const int chunks = C / 8;
   const long total = rows * chunks;
   const long stride = (long)gridDim.x * blockDim.x;
@@ -261,15 +291,20 @@ __global__ void bn_dx_kernel(const u16* __restrict__ x, const u16* __restrict__ 
     k3[j] = coef[2 * C + c];
     k0[j] = -coef[c] * coef[C + c] + k3[j] * mean[c];  // constant part
   }
+  float msc[8], msf[8];
+  if (relu && !y) bn_affine8(ch, mean, mk.rstd, mk.w, mk.b, mk.wdt, msc, msf);
   for (long i = i0; i < total; i += stride) {
     float a[8], g[8];
     load8(x + i * 8, a);
     load8(dy + i * 8, g);
-    if (relu) {
+    if (relu && y) {
       float yy[8];
       load8(y + i * 8, yy);
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = yy[j] > 0.f ? g[j] : 0.f;
+    } else if (relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = fmaf(a[j], msc[j], msf[j]) > 0.f ? g[j] : 0.f;
     }
     if (dres) store8(dres + i * 8, g);  // gradient of the residual input of relu(bn(x) + res)
 #pragma unroll
@@ -509,7 +544,9 @@ static void bn_ew_launch(long rows, int C, int& grid, int& block) {
 PA_EXPORT int pa_bn_blocks(long rows, int C) {
   int chunks, rsub;
   bn_layout(C, chunks, rsub);
-  long g = (rows + rsub * 64 - 1) / (rsub * 64);  // >= 64 rows per thread
+  // >= 16 rows per thread, up to 4 blocks per CU: small (late-stage) layers keep
+  // every CU streaming instead of a few hundred blocks
+  long g = (rows + rsub * 16 - 1) / (rsub * 16);
   if (g > 1024) g = 1024;
   if (g < 1) g = 1;
   return (int)g;
@@ -529,8 +566,8 @@ PA_EXPORT int pa_bn_fwd_train(const void* x, void* y, const void* w, const void*
                               float momentum, int relu, const void* res, hipStream_t st) {
   if (C % 8) return -1;
   const int G = pa_bn_blocks(rows, C);
-  hipLaunchKernelGGL(bn_reduce_kernel<false>, dim3(G), dim3(BN_T), bn_shm(C), st, (const u16*)x, nullptr, nullptr,
-                     nullptr, part, rows, C, 0);
+  hipLaunchKernelGGL(bn_reduce_kernel<false>, dim3(G), dim3(BN_T), bn_shm(C), st, (const u16*)x, nullptr,
+                     BnMask{nullptr, nullptr, nullptr, nullptr, 0}, nullptr, part, rows, C, 0);
   hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, part, G, (const u16*)x, C, rows,
                      eps, momentum, mean, rstd, run_mean, run_var, run_mean != nullptr);
   int eg, eb;
@@ -554,20 +591,30 @@ PA_EXPORT int pa_bn_apply(const void* x, void* y, const float* mean, const float
 // backward: dx, dw, db (fp32) from x, dy, the saved mean / rstd and (relu) the output y.
 // coef: 3*C floats of workspace, part: pa_bn_blocks * 2 * C floats.
 // dres (optional): also write the residual gradient (= dY masked by the ReLU)
-PA_EXPORT int pa_bn_bwd(const void* x, const void* dy, const void* y, const float* mean, const float* rstd,
-                        const void* w, int wdt, void* dx, float* dw, float* db, float* coef, float* part, long rows,
-                        int C, int relu, void* dres, hipStream_t st) {
+// y == null with relu: the ReLU mask is recomputed from x and (mean, rstd, w, b)
+// (non-residual layers need not keep their output for backward)
+PA_EXPORT int pa_bn_bwd2(const void* x, const void* dy, const void* y, const float* mean, const float* rstd,
+                         const void* w, const void* b, int wdt, void* dx, float* dw, float* db, float* coef,
+                         float* part, long rows, int C, int relu, void* dres, hipStream_t st) {
   if (C % 8) return -1;
   const int G = pa_bn_blocks(rows, C);
+  const BnMask mk{(const u16*)y, rstd, w, b, wdt};
   hipLaunchKernelGGL(bn_reduce_kernel<true>, dim3(G), dim3(BN_T), bn_shm(C), st, (const u16*)x, (const u16*)dy,
-                     (const u16*)y, mean, part, rows, C, relu);
+                     mk, mean, part, rows, C, relu);
   hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, part, G, C, rows, rstd, w, wdt,
                      dw, db, coef);
   int eg, eb;
   bn_ew_launch(rows, C, eg, eb);
-  hipLaunchKernelGGL(bn_dx_kernel, dim3(eg), dim3(eb), 0, st, (const u16*)x, (const u16*)dy, (const u16*)y, mean, coef,
+  hipLaunchKernelGGL(bn_dx_kernel, dim3(eg), dim3(eb), 0, st, (const u16*)x, (const u16*)dy, mk, mean, coef,
                      (u16*)dx, rows, C, relu, (u16*)dres);
   PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_bn_bwd(const void* x, const void* dy, const void* y, const float* mean, const float* rstd,
+                        const void* w, int wdt, void* dx, float* dw, float* db, float* coef, float* part, long rows,
+                        int C, int relu, void* dres, hipStream_t st) {
+  if (relu && !y) return -1;  // the mask source: y, or pa_bn_bwd2 with the bias
+  return pa_bn_bwd2(x, dy, y, mean, rstd, w, nullptr, wdt, dx, dw, db, coef, part, rows, C, relu, dres, st);
 }
 
 PA_EXPORT int pa_maxpool_nhwc_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C, int OH, int OW,

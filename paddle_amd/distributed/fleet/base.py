@@ -195,6 +195,16 @@ class HybridParallelOptimizer:
         self.strategy = strategy
         self.grad_clip = getattr(optimizer, "_grad_clip", None) or getattr(optimizer, "grad_clip", None)
         self._sharded = sharded
+        # dp x sharding all-reduce overlapped with backward: buckets fired from
+        # grad-ready hooks (pipelines sync their own gradients after the last
+        # micro-batch, see PipelineParallel)
+        self._bucket_sync = None
+        W = hcg.get_dp_sharding_world_size() if hcg else 1
+        if sharded is None and W > 1 and (hcg.get_pipe_parallel_world_size() if hcg else 1) == 1:
+            from .grad_sync import GradBucketAllReduce
+
+            mb = int(getattr(strategy, "fuse_grad_size_in_MB", 64) or 64)
+            self._bucket_sync = GradBucketAllReduce(self._params(), hcg.get_dp_sharding_group(), W, mb)
         if sharded is not None:
             max_norm = getattr(self.grad_clip, "clip_norm", self.grad_clip if isinstance(
                 self.grad_clip, (int, float)) else None)
@@ -276,7 +286,10 @@ class HybridParallelOptimizer:
         from .pipeline import PipelineParallel  # noqa: F401  (pipeline syncs dp itself)
 
         if not getattr(self, "_skip_dp_sync", False):
-            self._dp_sync(params)
+            if self._bucket_sync is not None:
+                self._bucket_sync.finish()
+            else:
+                self._dp_sync(params)
         clip = self.grad_clip
         max_norm = getattr(clip, "clip_norm", clip if isinstance(clip, (int, float)) else None)
         if max_norm:

@@ -19,6 +19,8 @@ MI355X design:
 from __future__ import annotations
 
 import torch
+
+from ...utils import strict as _strict
 import torch.nn.functional as F
 
 from ...nn import Layer
@@ -73,6 +75,12 @@ class TopKGate(Layer):
         self.capacity_factor = capacity_factor
 
     def forward(self, x):
+        # framework region: the fp32 router GEMM runs on the native exact-fp32 MFMA
+        # GEMM (pa_sgemm), softmax / top-k / the balance loss on the HIP kernels
+        with _strict.region("moe:gate"):
+            return self._route(x)
+
+    def _route(self, x):
         logits = x.float() @ self.weight.float()  # routing in fp32 whatever the activation dtype
         probs = F.softmax(logits, dim=-1)
         val, idx = probs.topk(self.top_k, dim=-1)

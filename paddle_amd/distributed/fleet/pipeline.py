@@ -331,6 +331,18 @@ class PipelineParallel(Layer):
             return loss / self.accumulate_steps
         return out
 
+    def _grad_sync_engine(self):
+        W = 1 if getattr(self, "_sharded", None) is not None else self.hcg.get_data_parallel_world_size()
+        if W <= 1:
+            return None
+        gs = getattr(self, "_grad_sync", None)
+        if gs is None:
+            from .grad_sync import GradBucketAllReduce
+
+            gs = self._grad_sync = GradBucketAllReduce(list(self._layers.parameters()),
+                                                       self.hcg.get_data_parallel_group(), W)
+        return gs
+
     def _sync_grads(self):
         dp_group = self.hcg.get_data_parallel_group()
         # ZeRO-3 on the stage (fleet.distributed_model): sharded gradients were
@@ -338,7 +350,11 @@ class PipelineParallel(Layer):
         # HybridParallelOptimizer over dp x sharding
         W = 1 if getattr(self, "_sharded", None) is not None else self.hcg.get_data_parallel_world_size()
         params = [p for p in self._layers.parameters() if p.requires_grad and p.grad is not None]
-        if W > 1 and params:
+        gs = getattr(self, "_grad_sync", None)
+        if W > 1 and gs is not None:
+            gs.finish()  # buckets already in flight since the last micro-batch's backward
+            gs.armed = False
+        elif W > 1 and params:
             flat = torch.cat([p.grad.reshape(-1).float() for p in params])
             comm.all_reduce(flat, group=dp_group)
             flat /= W
@@ -367,6 +383,12 @@ class PipelineParallel(Layer):
         warm = min(self.nst - self.stage - 1, M)
         inputs_q, outputs_q = [], []
         losses = []
+        # dp all-reduce of this stage's gradients, fired per bucket during the LAST
+        # micro-batch's reverse pass (earlier micro-batches only accumulate)
+        gs = self._grad_sync_engine()
+        if gs is not None:
+            gs.armed = False
+        nbwd = [0]
 
         def recv_fwd_input(i):
             if self.is_first:
@@ -385,6 +407,9 @@ class PipelineParallel(Layer):
         def run_bwd(grads):
             x = inputs_q.pop(0)
             out = outputs_q.pop(0)
+            nbwd[0] += 1
+            if gs is not None and nbwd[0] == M:
+                gs.armed = True
             if self.is_last:
                 _backward([out], [None])
             else:

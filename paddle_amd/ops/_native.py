@@ -78,6 +78,7 @@ _SIGS = {
     "pa_bn_fwd_train": [_P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _L, _I, _F, _F, _I, _P, _P],
     "pa_bn_apply": [_P, _P, _P, _P, _P, _P, _I, _L, _I, _I, _P],
     "pa_bn_bwd": [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _L, _I, _I, _P, _P],
+    "pa_bn_bwd2": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _L, _I, _I, _P, _P],
     "pa_maxpool_nhwc_fwd": [_P, _P, _P] + [_I] * 12 + [_P],
     "pa_maxpool_nhwc_bwd": [_P, _P, _P] + [_I] * 12 + [_P],
     "pa_gap_nhwc_fwd": [_P, _P, _I, _I, _I, _P],

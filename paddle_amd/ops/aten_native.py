@@ -1036,3 +1036,16 @@ def _var(name, self, dim=None, correction=None, keepdim=False):
     if name.startswith("var_mean"):
         return var, (mean if keepdim else mean.reshape(ss.shape))
     return var
+
+
+@_h("topk.default")
+def _topk(name, self, k, dim=-1, largest=True, sorted=True):
+    _need(_ok(self) and self.dtype in (torch.float32, torch.bfloat16) and largest and self.dim() >= 1)
+    _need(dim % self.dim() == self.dim() - 1 and 0 < k <= min(64, self.shape[-1]))
+    src = self if self.is_contiguous() else _to_copy("_to_copy.default", self, memory_format=torch.contiguous_format)
+    n = self.shape[-1]
+    rows = self.numel() // n
+    vals = torch.empty(list(self.shape[:-1]) + [k], dtype=self.dtype, device=self.device)
+    idx = torch.empty(list(self.shape[:-1]) + [k], dtype=torch.int64, device=self.device)
+    N.call("pa_topk", N.dt(src), N.ptr(src), N.ptr(vals), N.ptr(idx), rows, n, k, N.stream())
+    return vals, idx

@@ -257,7 +257,9 @@ class _BatchNormNHWC(torch.autograd.Function):
                 unb = var * rows / max(rows - 1, 1)
                 run_mean.mul_(momentum).add_((1 - momentum) * mean.to(run_mean.dtype))
                 run_var.mul_(momentum).add_((1 - momentum) * unb.to(run_var.dtype))
-        ctx.save_for_backward(x, y if relu else None, mean, rstd, wc)
+        # relu without a residual: backward recomputes the mask from x (y not kept)
+        ctx.save_for_backward(x, y if (relu and res is not None) else None, mean, rstd, wc,
+                              bc if (relu and res is None) else None)
         ctx.conf = (relu, wdt, w is not None, b is not None, res is not None)
         ctx.wdtype = w.dtype if w is not None else None
         ctx.bdtype = b.dtype if b is not None else None
@@ -265,7 +267,7 @@ class _BatchNormNHWC(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, mean, rstd, wc = ctx.saved_tensors
+        x, y, mean, rstd, wc, bc = ctx.saved_tensors
         relu, wdt, has_w, has_b, has_res = ctx.conf
         C = x.shape[-1]
         rows = x.numel() // C
@@ -277,9 +279,9 @@ class _BatchNormNHWC(torch.autograd.Function):
         db = torch.empty(C, dtype=torch.float32, device=x.device)
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if has_res else None
-        _nat.call("pa_bn_bwd", _nat.ptr(x), _nat.ptr(dy), _nat.ptr(y), _nat.ptr(mean), _nat.ptr(rstd), _nat.ptr(wc),
-                  wdt, _nat.ptr(dx), _nat.ptr(dw), _nat.ptr(db), _nat.ptr(coef), _nat.ptr(part), rows, C, int(relu),
-                  _nat.ptr(dres), _nat.stream())
+        _nat.call("pa_bn_bwd2", _nat.ptr(x), _nat.ptr(dy), _nat.ptr(y), _nat.ptr(mean), _nat.ptr(rstd),
+                  _nat.ptr(wc), _nat.ptr(bc), wdt, _nat.ptr(dx), _nat.ptr(dw), _nat.ptr(db), _nat.ptr(coef),
+                  _nat.ptr(part), rows, C, int(relu), _nat.ptr(dres), _nat.stream())
         return (dx, dw.to(ctx.wdtype) if has_w else None, db.to(ctx.bdtype) if has_b else None,
                 None, None, None, None, None, dres)
 

@@ -61,3 +61,55 @@ def test_resnet_tiny_bf16_nhwc_gpu_without_torch_autograd():
         assert losses[-1] < losses[0], losses
     finally:
         paddle.set_device("cpu")
+
+
+def _traj(make, place, dtype, batches, opt_make, sd=None):
+    paddle.set_device(place)
+    try:
+        model = make()
+        if sd is not None:
+            model.set_state_dict(sd)
+        if place == "gpu":
+            model.to(device="cuda", dtype=dtype)
+        opt = opt_make(model.parameters())
+        losses = []
+        with no_torch_autograd():
+            for x, y in batches:
+                xx = paddle.to_tensor(x).astype(str(dtype).split(".")[-1])
+                out = model(xx).astype("float32")
+                loss = F.cross_entropy(out, paddle.to_tensor(y))
+                loss.backward()
+                opt.step()
+                opt.clear_grad()
+                losses.append(float(loss))
+        return losses
+    finally:
+        paddle.set_device("cpu")
+
+
+def _oracle(make, dtype, shape, opt_make, steps=3, rtol=1e-3, seed=3):
+    """The same model, init and batches on the GPU (``dtype``) and in fp32 on the CPU:
+    the per-step losses must agree to ``rtol`` (a trajectory, not "loss went down")."""
+    _native.lib()
+    paddle.seed(seed)
+    ref_model = make()
+    sd = {k: v.detach().clone() for k, v in ref_model.state_dict().items()}
+    rs = np.random.RandomState(seed)
+    batches = [(rs.randn(*shape).astype("float32"), (np.arange(shape[0]) % 10).astype("int64"))
+               for _ in range(steps)]
+    cpu = _traj(make, "cpu", torch.float32, batches, opt_make, sd)
+    gpu = _traj(make, "gpu", dtype, batches, opt_make, sd)
+    for a, b in zip(cpu, gpu):
+        assert abs(a - b) <= rtol * abs(a), (cpu, gpu)
+    return cpu, gpu
+
+
+def test_lenet_fp32_gpu_trajectory_matches_cpu_fp32():
+    _oracle(paddle.vision.models.LeNet, torch.float32, (16, 1, 28, 28),
+            lambda ps: paddle.optimizer.Adam(learning_rate=2e-3, parameters=ps), rtol=1e-3)
+
+
+def test_resnet18_bf16_nhwc_gpu_trajectory_matches_cpu_fp32():
+    _oracle(lambda: paddle.vision.models.resnet18(num_classes=10, data_format="NHWC"), torch.bfloat16,
+            (8, 32, 32, 3), lambda ps: paddle.optimizer.Momentum(learning_rate=0.05, momentum=0.9, parameters=ps),
+            rtol=5e-2)

@@ -1,0 +1,7 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export PYTHONUNBUFFERED=1
+S=tools/gpu_session.sh
+bash $S "step conv_tests 300 python -u -m pytest -q --timeout 120 --timeout-method thread tests/test_conv_gpu.py" \
+ "step rn50 400 python -u benchmarks/resnet50.py --batch 256 --steps 20 --warmup 5" \
+ "step rn50_prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_rn4 -o run -- python3 benchmarks/resnet50.py --batch 256 --steps 5 --warmup 2"
