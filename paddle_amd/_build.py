@@ -120,7 +120,7 @@ def build_runtime(verbose: bool = False, jobs: int | None = None) -> str:
     cxx = shutil.which("g++") or "c++"
     cflags = ["-O2", "-fPIC", "-std=c++17", "-fvisibility=hidden", "-Wall", "-pthread",
               "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]
-    ldflags = ["-pthread", "-lz"]
+    ldflags = ["-pthread", "-lz", "-ldl"]
     tl = _torch_lib_dir()
     if tl:
         ldflags += [f"-L{tl}", f"-Wl,-rpath,{tl}", "-lamdhip64"]

@@ -426,7 +426,9 @@ def _clamp_max(name, self, max):
 
 # ---------------------------------------------------------------------------- backward pointwise
 def _bwd2(kind):
-    def h(name, grad, x, *extra):
+    def h(name, grad, x, *extra, **kw):
+        if "approximate" in kw:
+            extra = (kw["approximate"],)
         _need(_ok(grad) and _ok(x) and grad.dtype in _FLOATS)
         shape = _bshape(grad, x)
         dst = _new_out(shape, grad.dtype, like=grad)
@@ -870,10 +872,20 @@ def _mm_bf16(a, b, bias=None):
     M, K = a.shape
     Nn = b.shape[1]
     ops = _bf16_operands(a, b)
-    _need(ops is not None)
-    A, ak, Bm, bk = ops
-    _need(G.supported(M, Nn, K, A, Bm))
-    return G.gemm(A, Bm, M, Nn, K, a_kmaj=ak, b_kmaj=bk, bias=bias)
+    if ops is not None:
+        A, ak, Bm, bk = ops
+        if G.supported(M, Nn, K, A, Bm):
+            return G.gemm(A, Bm, M, Nn, K, a_kmaj=ak, b_kmaj=bk, bias=bias)
+    # shapes the bf16 MFMA kernel does not take (a dim not a multiple of 8, e.g. a
+    # 10-class head): fp32 operands on the exact-fp32 MFMA GEMM, one rounding back
+    from . import blas
+
+    af = _to_copy("_to_copy.default", a, dtype=torch.float32)
+    bf = _to_copy("_to_copy.default", b, dtype=torch.float32)
+    c = blas._bmm(af, bf)
+    if bias is not None:
+        _need(_launch(B["add"], c, [c, bias], a=1.0))
+    return _to_copy("_to_copy.default", c, dtype=a.dtype)
 
 
 @_h("mm.default")

@@ -77,8 +77,23 @@ def _is_gloo(group=None):
     return dist.get_backend(group) == "gloo"
 
 
+def _pa_comm(group, *ts):
+    """The framework-owned RCCL communicator of ``group`` (FLAGS_comm_backend=pa_rccl)
+    when every operand is a contiguous device tensor, else None (torch.distributed)."""
+    from . import rccl
+
+    if not rccl.enabled() or not all(t.is_cuda and t.is_contiguous() for t in ts):
+        return None
+    ranks = list(range(dist.get_world_size())) if group is None else dist.get_process_group_ranks(group)
+    return rccl.context_map().get(ranks, dist.get_rank())
+
+
 def all_reduce(t, op=dist.ReduceOp.SUM, group=None, async_op=False):
     if get_world_size(group) == 1:
+        return None
+    c = _pa_comm(group, t) if op == dist.ReduceOp.SUM else None
+    if c is not None:
+        c.all_reduce(t)  # stream-ordered on the current stream: nothing to wait for
         return None
     return dist.all_reduce(t, op=op, group=group, async_op=async_op)
 
@@ -96,6 +111,10 @@ def reduce_scatter(out, inp, group=None, async_op=False):
         n = out.numel()
         out.copy_(tmp.view(-1)[r * n:(r + 1) * n].view_as(out))
         return None
+    c = _pa_comm(group, out, inp)
+    if c is not None:
+        c.reduce_scatter(out, inp)
+        return None
     return dist.reduce_scatter_tensor(out, inp, group=group, async_op=async_op)
 
 
@@ -112,11 +131,20 @@ def all_gather(out, inp, group=None, async_op=False):
         for c, t in zip(chunks, tmp):
             c.copy_(t)
         return None
+    c = _pa_comm(group, out, inp)
+    if c is not None:
+        c.all_gather(out, inp)
+        return None
     return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
 
 
 def broadcast(t, src=0, group=None):
     if get_world_size(group) == 1:
+        return
+    c = _pa_comm(group, t)
+    if c is not None:
+        ranks = list(range(dist.get_world_size())) if group is None else dist.get_process_group_ranks(group)
+        c.broadcast(t, root=ranks.index(src))  # src is a global rank
         return
     dist.broadcast(t, src=src, group=group)
 

@@ -1,0 +1,220 @@
+"""Framework-owned RCCL communicators (``csrc/runtime/rccl_comm.cc``).
+
+Reference: platform/nccl_helper.h:49-123 -- ``NCCLGroupGuard`` (process-wide mutex
+around ncclGroupStart/End) and ``NCCLContextMap`` (one communicator per place,
+``InitRank`` with rank = trainer_id * ngpu + gpu_id) -- and
+operators/gen_nccl_id_op.cc:54-110 (trainer 0 generates the ncclUniqueId and sends
+it to the others over RPC).
+
+MI355X-first: one process per GPU, so :class:`CommContextMap` maps a process group
+(tuple of global ranks) to ONE :class:`Communicator` on this process's device.  The
+unique id of each communicator is created by the group's first rank and published
+in the job's TCP key-value store under a per-group, per-generation key (the
+``gen_nccl_id`` role, without an extra RPC server).  Collectives are enqueued on
+the caller's HIP stream (torch's current stream by default, or the DeviceContext
+comm stream), so they order with the kernels that produced their inputs without a
+host synchronisation, exactly like the framework's own kernels.
+
+``FLAGS_comm_backend=pa_rccl`` routes the GPU collectives of
+:mod:`paddle_amd.parallel.comm` (all-reduce, reduce-scatter, all-gather, broadcast)
+through these communicators instead of ``torch.distributed``'s ProcessGroupNCCL;
+the default stays ``torch`` (the path every multi-rank test and the scaling bench
+have exercised).
+"""
+from __future__ import annotations
+
+import contextlib
+import ctypes
+import os
+import threading
+
+import torch
+
+from .. import runtime as _rt
+
+# ncclDataType_t / ncclRedOp_t values (rccl.h)
+_DT = {torch.int8: 0, torch.uint8: 1, torch.int32: 2, torch.int64: 4, torch.float16: 6, torch.float32: 7,
+       torch.float64: 8, torch.bfloat16: 9}
+_OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "avg": 4}
+
+_lock = threading.Lock()
+_sigs_ready = [False]
+
+
+def _lib():
+    L = _rt.lib()
+    if not _sigs_ready[0]:
+        P, I, S = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+        L.pa_rccl_last_error.restype = ctypes.c_char_p
+        L.pa_rccl_unique_id.argtypes = [ctypes.c_char_p]
+        L.pa_rccl_comm_init.argtypes = [ctypes.c_char_p, I, I, I, ctypes.POINTER(P)]
+        L.pa_rccl_comm_destroy.argtypes = [P, I]
+        L.pa_rccl_async_error.argtypes = [P]
+        L.pa_rccl_all_reduce.argtypes = [P, P, S, I, I, P, P]
+        L.pa_rccl_reduce_scatter.argtypes = [P, P, S, I, I, P, P]
+        L.pa_rccl_all_gather.argtypes = [P, P, S, I, P, P]
+        L.pa_rccl_broadcast.argtypes = [P, P, S, I, I, P, P]
+        L.pa_rccl_send.argtypes = [P, S, I, I, P, P]
+        L.pa_rccl_recv.argtypes = [P, S, I, I, P, P]
+        _sigs_ready[0] = True
+    return L
+
+
+class RcclError(RuntimeError):
+    pass
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RcclError(f"{what}: {_lib().pa_rccl_last_error().decode()}")
+
+
+def available() -> bool:
+    try:
+        return bool(_lib().pa_rccl_available())
+    except Exception:
+        return False
+
+
+def unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    _check(_lib().pa_rccl_unique_id(buf), "ncclGetUniqueId")
+    return buf.raw
+
+
+def _stream(stream):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class Communicator:
+    """One RCCL communicator: ``world`` ranks, this process is ``rank``, on ``device``.
+
+    ``uid``: the clique's 128-byte unique id (the same bytes on every rank); use
+    :meth:`rendezvous` to create it on rank 0 and distribute it through a store."""
+
+    def __init__(self, uid: bytes, world: int, rank: int, device: int):
+        if len(uid) != 128:
+            raise ValueError("RCCL unique id must be 128 bytes")
+        self.world, self.rank, self.device = int(world), int(rank), int(device)
+        h = ctypes.c_void_p()
+        _check(_lib().pa_rccl_comm_init(uid, self.world, self.rank, self.device, ctypes.byref(h)),
+               "ncclCommInitRank")
+        self._h = h
+
+    @classmethod
+    def rendezvous(cls, store, key: str, world: int, rank: int, device: int, timeout_s: float = 300.0):
+        """gen_nccl_id: rank 0 publishes a fresh unique id under ``key``, every rank
+        reads it from the store (blocking) and joins the clique."""
+        if rank == 0:
+            store.set(key, unique_id())
+        store.wait([key], __import__("datetime").timedelta(seconds=timeout_s))
+        uid = store.get(key)
+        return cls(bytes(uid), world, rank, device)
+
+    # ------------------------------------------------------------------ collectives
+    def _args(self, t):
+        if not t.is_cuda or t.dtype not in _DT or not t.is_contiguous():
+            raise RcclError(f"RCCL operand must be a contiguous device tensor of a supported dtype ({t.dtype})")
+        return ctypes.c_void_p(t.data_ptr()), _DT[t.dtype]
+
+    def all_reduce(self, t, op="sum", stream=None):
+        p, dt = self._args(t)
+        _check(_lib().pa_rccl_all_reduce(p, p, t.numel(), dt, _OPS[op], self._h, _stream(stream)), "ncclAllReduce")
+
+    def reduce_scatter(self, out, inp, op="sum", stream=None):
+        po, dt = self._args(out)
+        pi, _ = self._args(inp)
+        if inp.numel() != out.numel() * self.world or inp.dtype != out.dtype:
+            raise RcclError("reduce_scatter: input must hold world x output elements of the same dtype")
+        _check(_lib().pa_rccl_reduce_scatter(pi, po, out.numel(), dt, _OPS[op], self._h, _stream(stream)),
+               "ncclReduceScatter")
+
+    def all_gather(self, out, inp, stream=None):
+        po, dt = self._args(out)
+        pi, _ = self._args(inp)
+        if out.numel() != inp.numel() * self.world or inp.dtype != out.dtype:
+            raise RcclError("all_gather: output must hold world x input elements of the same dtype")
+        _check(_lib().pa_rccl_all_gather(pi, po, inp.numel(), dt, self._h, _stream(stream)), "ncclAllGather")
+
+    def broadcast(self, t, root=0, stream=None):
+        p, dt = self._args(t)
+        _check(_lib().pa_rccl_broadcast(p, p, t.numel(), dt, int(root), self._h, _stream(stream)),
+               "ncclBroadcast")
+
+    def send(self, t, peer, stream=None):
+        p, dt = self._args(t)
+        _check(_lib().pa_rccl_send(p, t.numel(), dt, int(peer), self._h, _stream(stream)), "ncclSend")
+
+    def recv(self, t, peer, stream=None):
+        p, dt = self._args(t)
+        _check(_lib().pa_rccl_recv(p, t.numel(), dt, int(peer), self._h, _stream(stream)), "ncclRecv")
+
+    def check_async(self):
+        """Raise if the communicator hit an asynchronous error (a peer failed)."""
+        _check(_lib().pa_rccl_async_error(self._h), "communicator")
+
+    def destroy(self, abort=False):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _check(_lib().pa_rccl_comm_destroy(self._h, int(abort)), "ncclCommDestroy")
+            self._h = ctypes.c_void_p()
+
+
+@contextlib.contextmanager
+def group_guard():
+    """NCCLGroupGuard: the collectives issued inside launch as one fused group
+    (ncclGroupStart/End, serialised across host threads)."""
+    _check(_lib().pa_rccl_group_start(), "ncclGroupStart")
+    try:
+        yield
+    finally:
+        _check(_lib().pa_rccl_group_end(), "ncclGroupEnd")
+
+
+class CommContextMap:
+    """NCCLContextMap: process group (global ranks) -> this process's communicator."""
+
+    def __init__(self, store=None):
+        self._store = store
+        self._comms = {}
+        self._gen = {}
+
+    def _default_store(self):
+        if self._store is None:
+            import torch.distributed as dist
+
+            self._store = dist.distributed_c10d._get_default_store()
+        return self._store
+
+    def get(self, ranks, my_rank, device=None):
+        """The communicator of the group with global ``ranks`` (sorted) for this process
+        (global rank ``my_rank``); created on first use -- a collective over the group."""
+        key = tuple(sorted(ranks))
+        c = self._comms.get(key)
+        if c is None:
+            with _lock:
+                c = self._comms.get(key)
+                if c is None:
+                    gen = self._gen.get(key, 0)
+                    self._gen[key] = gen + 1
+                    dev = torch.cuda.current_device() if device is None else device
+                    name = f"pa_rccl/{'-'.join(map(str, key))}/{gen}"
+                    c = Communicator.rendezvous(self._default_store(), name, len(key), key.index(my_rank), dev)
+                    self._comms[key] = c
+        return c
+
+    def destroy_all(self, abort=False):
+        for c in self._comms.values():
+            c.destroy(abort)
+        self._comms.clear()
+
+
+_MAP = CommContextMap()
+
+
+def context_map() -> CommContextMap:
+    return _MAP
+
+
+def enabled() -> bool:
+    return os.environ.get("FLAGS_comm_backend", "torch") == "pa_rccl"

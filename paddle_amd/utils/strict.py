@@ -137,7 +137,8 @@ class _Watch(TorchDispatchMode):
             if name == "_local_scalar_dense":
                 SYNCS[_label()] = SYNCS.get(_label(), 0) + 1  # device -> host read (a sync)
                 return func(*args, **kwargs)
-            if self.native:
+            nat = getattr(_TLS, "natives", None)
+            if self.native and nat and nat[-1]:
                 from ..ops import aten_native
 
                 r = aten_native.try_native(func, args, kwargs)
@@ -163,19 +164,21 @@ def region(label: str, native: bool = True):
     labels = getattr(_TLS, "labels", None)
     if labels is None:
         labels = _TLS.labels = []
+        _TLS.natives = []
     outer = not labels
     labels.append(label)
+    _TLS.natives.append(bool(native))  # the innermost region decides native execution
     mode = None
     try:
-        nat = native and native_dispatch()
-        if outer and (nat or counting()):
-            mode = _Watch(nat)
+        if outer and (native_dispatch() or counting()):
+            mode = _Watch(native_dispatch())
             mode.__enter__()
         yield
     finally:
         if mode is not None:
             mode.__exit__(None, None, None)
         labels.pop()
+        _TLS.natives.pop()
 
 
 @contextlib.contextmanager
@@ -184,8 +187,10 @@ def unwatched():
     the caller accounts for itself)."""
     labels = getattr(_TLS, "labels", None)
     saved = list(labels) if labels else []
+    nsaved = list(getattr(_TLS, "natives", []) or [])
     if labels:
         labels.clear()
+        _TLS.natives.clear()
     try:
         from torch.utils._python_dispatch import _pop_mode_temporarily, _get_current_dispatch_mode
 
@@ -197,6 +202,7 @@ def unwatched():
     finally:
         if labels is not None:
             labels[:] = saved
+            _TLS.natives[:] = nsaved
 
 
 def fallback(site: str, on_gpu: bool = True):

@@ -111,5 +111,5 @@ def test_lenet_fp32_gpu_trajectory_matches_cpu_fp32():
 
 def test_resnet18_bf16_nhwc_gpu_trajectory_matches_cpu_fp32():
     _oracle(lambda: paddle.vision.models.resnet18(num_classes=10, data_format="NHWC"), torch.bfloat16,
-            (8, 32, 32, 3), lambda ps: paddle.optimizer.Momentum(learning_rate=0.05, momentum=0.9, parameters=ps),
+            (8, 32, 32, 3), lambda ps: paddle.optimizer.Momentum(learning_rate=0.01, momentum=0.9, parameters=ps),
             rtol=5e-2)
