@@ -201,9 +201,10 @@ class Tensor(torch.Tensor):
     @classmethod
     def __torch_function__(cls, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}
-        if _strict.watching():
+        if not _strict.inside() and _strict.watching():
             # framework region: covered ATen ops run on the HIP kernels
-            # (ops/aten_native.py); the rest are counted / refused in strict mode
+            # (ops/aten_native.py); the rest are counted / refused in strict mode.
+            # Inside a layer's forward the layer's region is already active.
             with _strict.region("eager:" + _fname(func)):
                 return cls._torch_function_impl(func, args, kwargs)
         return cls._torch_function_impl(func, args, kwargs)
@@ -446,7 +447,7 @@ def _backward(roots, grads, retain_graph):
     from . import tape as _tape
 
     _tape.run_before_backward()  # e.g. an optimizer update still running on a side stream
-    if _strict.watching():
+    if not _strict.inside() and _strict.watching():
         with _strict.region("eager:backward"):
             return _backward_impl(roots, grads, retain_graph)
     return _backward_impl(roots, grads, retain_graph)

@@ -324,6 +324,25 @@ __global__ __launch_bounds__(256) void ew_kernel(EwParams p) {
   }
 }
 
+// Contiguous fast path (every operand dense over the same shape, f32 / bf16, n % 8
+// == 0, 16-B aligned): 8 elements per lane per iteration with 16-B (bf16) or 2x16-B
+// (f32) vector loads -- the hot case of gradient accumulation, casts and scaling.
+template <class TI, class TO, int NIN>
+__global__ __launch_bounds__(256) void ew_vec_kernel(int op, const TI* __restrict__ x, const TI* __restrict__ y,
+                                                     const TI* __restrict__ z, TO* __restrict__ out, long n8,
+                                                     double a, double b) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    float xv[8], yv[8], zv[8], ov[8];
+    if (NIN >= 1) load8(x + i * 8, xv);
+    if (NIN >= 2) load8(y + i * 8, yv);
+    if (NIN >= 3) load8(z + i * 8, zv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      ov[j] = apply<float>(op, NIN >= 1 ? xv[j] : 0.f, NIN >= 2 ? yv[j] : 0.f, NIN >= 3 ? zv[j] : 0.f, a, b);
+    store8(out + i * 8, ov);
+  }
+}
+
 // contiguous same-dtype fast paths: fill and bf16/f32 copies-with-cast, 16 B per lane
 template <class T>
 __global__ __launch_bounds__(256) void fill16_kernel(T* out, long n16, T v) {
@@ -628,6 +647,30 @@ PA_EXPORT int pa_ew(int op, int cdt, int nin, int nd, const long* size, void* ou
       PA_LAUNCH_CHECK();
     }
   }
+  // vectorized contiguous f32 / bf16 path (float compute, ops other than the
+  // integer-only / nullary ones)
+  if (contig && cdt == 0 && nin >= 1 && n % 8 == 0 && op != IOTA && op != FILL && (odt == F32 || odt == BF16) &&
+      (p.x.dt == F32 || p.x.dt == BF16) && (nin < 2 || p.y.dt == p.x.dt) && (nin < 3 || p.z.dt == p.x.dt) &&
+      (uintptr_t)out % 16 == 0 && (uintptr_t)x % 16 == 0 && (nin < 2 || (uintptr_t)y % 16 == 0) &&
+      (nin < 3 || (uintptr_t)z % 16 == 0)) {
+    const long n8 = n / 8;
+    const int g = stream_grid(n8, 256) * 2;
+#define PA_EWV(TI, TO)                                                                                       \
+    switch (nin) {                                                                                           \
+      case 1: hipLaunchKernelGGL((ew_vec_kernel<TI, TO, 1>), dim3(g), dim3(256), 0, st, op, (const TI*)x,     \
+                                 (const TI*)y, (const TI*)z, (TO*)out, n8, a, b); break;                      \
+      case 2: hipLaunchKernelGGL((ew_vec_kernel<TI, TO, 2>), dim3(g), dim3(256), 0, st, op, (const TI*)x,     \
+                                 (const TI*)y, (const TI*)z, (TO*)out, n8, a, b); break;                      \
+      default: hipLaunchKernelGGL((ew_vec_kernel<TI, TO, 3>), dim3(g), dim3(256), 0, st, op, (const TI*)x,    \
+                                  (const TI*)y, (const TI*)z, (TO*)out, n8, a, b); break;                     \
+    }
+    if (p.x.dt == BF16 && odt == BF16) { PA_EWV(u16, u16) }
+    else if (p.x.dt == BF16) { PA_EWV(u16, float) }
+    else if (odt == BF16) { PA_EWV(float, u16) }
+    else { PA_EWV(float, float) }
+#undef PA_EWV
+    PA_LAUNCH_CHECK();
+  }
   const int g = stream_grid(n, 256) * 2;
 #define PA_EW(C, I)                                                                          \
   switch (nin) {                                                                             \
@@ -721,4 +764,12 @@ PA_EXPORT int pa_cumsum(int cdt, const void* x, int xdt, void* out, int odt, lon
   else if (cdt == 1) hipLaunchKernelGGL(cumsum_kernel<double>, dim3(g), dim3(256), 0, st, x, xdt, out, odt, outer, R, inner);
   else hipLaunchKernelGGL(cumsum_kernel<long>, dim3(g), dim3(256), 0, st, x, xdt, out, odt, outer, R, inner);
   PA_LAUNCH_CHECK();
+}
+
+// flat (contiguous, same-shape) launch with scalar arguments only: the hot path of
+// the Python dispatcher (no per-call host arrays)
+PA_EXPORT int pa_ew_flat(int op, int cdt, int nin, long n, void* out, int odt, const void* x, int xdt, const void* y,
+                         int ydt, const void* z, int zdt, double a, double b, hipStream_t st) {
+  const long size[1] = {n}, one[1] = {1};
+  return pa_ew(op, cdt, nin, 1, size, out, odt, one, x, xdt, one, y, ydt, one, z, zdt, one, a, b, st);
 }

@@ -768,10 +768,18 @@ void Executor::RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* 
     }
     PA_CHECK(k != nullptr, dk ? "op '%s' declined its device kernel and has no host kernel"
                               : "no kernel registered for op type '%s'", op.type.c_str());
-    if (dev && !agnostic.count(op.type))
-      timed(op, [&] { host_fallback(op, k); });
-    else
-      timed(op, [&] { (*k)(OpRun{op, *scope, ctx_}); });
+    try {
+      if (dev && !agnostic.count(op.type))
+        timed(op, [&] { host_fallback(op, k); });
+      else
+        timed(op, [&] { (*k)(OpRun{op, *scope, ctx_}); });
+    } catch (const Decline&) {
+      // the host kernel does not cover these dtypes / this configuration
+      PA_CHECK(fallback != nullptr, "op '%s': no kernel covers this configuration (dtype / layout)",
+               op.type.c_str());
+      embedder_fallbacks[op.type] += 1;
+      timed(op, [&] { fallback(op, *scope, block.idx, op_idx); });
+    }
   }
 }
 

@@ -20,8 +20,10 @@ int64_t prod(const Dims& d, size_t b = 0, size_t e = (size_t)-1) {
   return n;
 }
 
+// a dtype the host kernels do not cover declines the op (the executor then runs the
+// embedder's kernel for it, or reports the op as unsupported)
 float* f32(Tensor& t) {
-  PA_CHECK(t.dtype == DT::FP32, "expected float32 tensor, got %s", dt_name(t.dtype));
+  if (t.dtype != DT::FP32) throw Decline{};
   return t.data<float>();
 }
 
@@ -30,7 +32,7 @@ std::vector<int64_t> ids_of(const Tensor& t) {
   if (t.dtype == DT::INT64) memcpy(v.data(), t.raw(), v.size() * 8);
   else if (t.dtype == DT::INT32)
     for (size_t i = 0; i < v.size(); ++i) v[i] = t.data<int32_t>()[i];
-  else fail("expected an integer index tensor, got %s", dt_name(t.dtype));
+  else throw Decline{};  // not an integer index tensor
   return v;
 }
 
@@ -1248,7 +1250,7 @@ void k_momentum(const OpRun& r) {
   const bool nesterov = r.op.GetBool("use_nesterov");
   float* w = f32(*r.out("ParamOut"));
   float* vel = f32(*r.out("VelocityOut"));
-  PA_CHECK(w == f32(p) && vel == f32(v), "momentum: in-place update expected");
+  if (!(w == f32(p) && vel == f32(v))) throw Decline{};  // out-of-place update: not covered here
   const float* gp = f32(g);
   for (int64_t i = 0; i < p.numel(); ++i) {
     vel[i] = vel[i] * mu + gp[i];

@@ -175,10 +175,20 @@ class NativeEngine:
         if missing and not self._b.supports_fallback:
             raise NotImplementedError(f"native engine: no C++ kernel for op types {missing}")
         self.py_fallback_types = set(missing)
-        prog = self._b.program(program.desc.serialize_to_string())
+        src = program
+        gb = program.global_block()
+        if any(op.type in ("feed", "fetch") for op in gb.ops):
+            # a saved program carrying its own feed / fetch ops: feeds are set and
+            # fetches read by name here, so run a copy without them
+            src = program.clone()
+            b0 = src.global_block()
+            for i in reversed(range(len(b0.ops))):
+                if b0.ops[i].type in ("feed", "fetch"):
+                    b0.remove_op(i)
+        prog = self._b.program(src.desc.serialize_to_string())
         pers = [v.name for v in program.list_vars()
                 if v.persistable and v.name not in ("feed", "fetch") and v.type == core.VT.LOD_TENSOR]
-        self._progs[key] = (program, prog, pers)
+        self._progs[key] = (program, prog, pers, src)
         return prog, pers
 
     def _scope(self, scope):
@@ -334,7 +344,8 @@ class NativeEngine:
         for name, data in feed.items():
             self._feed(ns, name, data)
         if self._b.supports_fallback:
-            self._b.exe.set_fallback(lambda blk, idx, s, p=program, sc=scope: self._py_op(p, sc, blk, idx, s))
+            src = self._progs[(id(program), program._version)][3]
+            self._b.exe.set_fallback(lambda blk, idx, s, p=src, sc=scope: self._py_op(p, sc, blk, idx, s))
             if self.device >= 0:
                 # one stream for both kernel libraries: no host sync between them
                 self._b.exe.set_stream(torch.cuda.current_stream(self._tdev()).cuda_stream)

@@ -11,6 +11,8 @@ from collections import OrderedDict
 
 import torch
 
+from ..utils import strict as _strict
+
 from .. import ops
 from ..autograd import engine as _eager
 from . import initializer as I
@@ -52,6 +54,15 @@ class Layer(torch.nn.Module):
     ``set_state_dict``, ``train`` / ``eval``, ``full_name``."""
 
     _name_counter: dict = {}
+
+    def __call__(self, *args, **kwargs):
+        # one framework region per outermost layer call: every tensor op of the
+        # forward runs inside it (native dispatch / strict accounting) without a
+        # per-op region
+        if not _strict.inside() and _strict.watching():
+            with _strict.region("layer:" + type(self).__name__):
+                return super().__call__(*args, **kwargs)
+        return super().__call__(*args, **kwargs)
 
     def __init__(self, name_scope=None, dtype="float32"):
         super().__init__()

@@ -218,6 +218,13 @@ def spp(ctx):
         kh, kw = -(-H // bins), -(-W // bins)
         ph, pw = (kh * bins - H + 1) // 2, (kw * bins - W + 1) // 2
         pad = (pw, kw * bins - W - pw, ph, kh * bins - H - ph)
+        if _cnd.supported_pool(x) and kh * bins - H - ph <= ph and kw * bins - W - pw <= pw:
+            # the native NCHW pool kernel: symmetric padding (the right/bottom pad is
+            # never larger, and floor() drops the partial window it would add), max
+            # over valid pixels / exclusive average -- spp_op.h's semantics
+            o = _cnd.pool_nd(x, ctx.attr("pooling_type"), (kh, kw), (kh, kw), (ph, pw), exclusive=True)
+            outs.append(o.reshape(N, -1))
+            continue
         if ctx.attr("pooling_type") == "max":
             o = F.max_pool2d(F.pad(x, pad, value=float("-inf")), (kh, kw), (kh, kw))
         else:

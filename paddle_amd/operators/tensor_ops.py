@@ -433,7 +433,10 @@ def random_crop(ctx):
 def multiplex(ctx):
     ids = ctx.input("Ids").reshape(-1).long()
     xs = torch.stack(ctx.inputs("X"))  # K, N, ...
-    ctx.set_output("Out", xs[ids, torch.arange(xs.shape[1], device=xs.device)])
+    K, Nr = xs.shape[0], xs.shape[1]
+    # row i of candidate ids[i]: one row gather of the stacked [K*N, ...] rows
+    rows = ids * Nr + torch.arange(Nr, device=xs.device)
+    ctx.set_output("Out", xs.reshape(K * Nr, -1).index_select(0, rows).reshape(xs.shape[1:]))
 
 
 def _cmp(name, fn):

@@ -61,6 +61,8 @@ def _lib():
         LP = ctypes.POINTER(ctypes.c_long)
         L.pa_ew.argtypes = [I, I, I, I, LP, P, I, LP, P, I, LP, P, I, LP, P, I, LP, D, D, P]
         L.pa_ew.restype = I
+        L.pa_ew_flat.argtypes = [I, I, I, Lg, P, I, P, I, P, I, P, I, D, D, P]
+        L.pa_ew_flat.restype = I
         L.pa_reduce_any.argtypes = [I, I, P, I, P, I, Lg, Lg, Lg, D, P, Lg, P]
         L.pa_reduce_any.restype = Lg
         L.pa_index_select.argtypes = [P, I, Lg, Lg, Lg, P, I, Lg, P, P]
@@ -114,6 +116,20 @@ def _coalesce(shape, strides_list):
 def _launch(op, out, ins, a=0.0, b=0.0, cdt=None):
     """out[...] = op(ins...) over out's shape; inputs broadcast by stride 0.
     Returns False when the launch does not fit the kernel (caller falls back)."""
+    if cdt is None:
+        cdt = _cdt(out.dtype if not ins else ins[0].dtype)
+    if out.is_contiguous() and all(t.is_contiguous() and t.shape == out.shape for t in ins):
+        # hot path: one flat launch, scalar arguments only
+        x = ins[0] if len(ins) > 0 else None
+        y = ins[1] if len(ins) > 1 else None
+        z = ins[2] if len(ins) > 2 else None
+        rc = _lib().pa_ew_flat(op, cdt, len(ins), out.numel(), out.data_ptr(), _DT[out.dtype],
+                               x.data_ptr() if x is not None else None, _DT[x.dtype] if x is not None else 0,
+                               y.data_ptr() if y is not None else None, _DT[y.dtype] if y is not None else 0,
+                               z.data_ptr() if z is not None else None, _DT[z.dtype] if z is not None else 0,
+                               float(a), float(b), N.stream())
+        N.check(rc, "pa_ew_flat")
+        return True
     shape = list(out.shape)
     strs = [list(out.stride())]
     for t in ins:
@@ -182,11 +198,17 @@ def _h(*names):
     return deco
 
 
+_FUNC = {}  # OpOverload -> (name, handler): resolved once per overload
+
+
 def try_native(func, args, kwargs):
     """Run ``func`` (an ATen OpOverload) on the HIP kernels; NotImplemented if no handler
     covers this call."""
-    name = f"{func.overloadpacket.__name__}.{func._overloadname}"
-    h = HANDLERS.get(name)
+    ent = _FUNC.get(func)
+    if ent is None:
+        name = f"{func.overloadpacket.__name__}.{func._overloadname}"
+        ent = _FUNC[func] = (name, HANDLERS.get(name))
+    name, h = ent
     if h is None:
         return NotImplemented
     try:

@@ -58,6 +58,12 @@ def counting() -> bool:
 _CUDA = []
 
 
+def inside() -> bool:
+    """Already inside a framework region (nested framework code needs no region of
+    its own: the outer one's dispatch mode is active)."""
+    return bool(getattr(_TLS, "labels", None))
+
+
 def watching() -> bool:
     """True when a region would push the dispatch mode (native dispatch or counting)."""
     return native_dispatch() or counting()
@@ -88,6 +94,9 @@ _FREE = {
 
 def _is_gpu(x):
     return isinstance(x, torch.Tensor) and x.device.type in WATCH_DEVICES
+
+
+_META = {}  # OpOverload -> (op name, watched?)
 
 
 def _label():
@@ -129,9 +138,13 @@ class _Watch(TorchDispatchMode):
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}
-        ns = getattr(func, "namespace", "aten")
-        name = func._schema.name.split("::")[-1] if hasattr(func, "_schema") else str(func)
-        if ns == "aten" and name not in _FREE and _touches_gpu(args, kwargs):
+        meta = _META.get(func)
+        if meta is None:
+            ns = getattr(func, "namespace", "aten")
+            nm = func._schema.name.split("::")[-1] if hasattr(func, "_schema") else str(func)
+            meta = _META[func] = (nm, ns == "aten" and nm not in _FREE)
+        name, watched = meta
+        if watched and _touches_gpu(args, kwargs):
             if name in ("_to_copy", "copy_") and _crosses_host(args, kwargs):
                 return func(*args, **kwargs)  # host <-> device transfer: a DMA copy, no kernel
             if name == "_local_scalar_dense":
@@ -157,28 +170,41 @@ class _Watch(TorchDispatchMode):
         return func(*args, **kwargs)
 
 
-@contextlib.contextmanager
-def region(label: str, native: bool = True):
+class region:
     """Bracket framework code; only the outermost region pushes the dispatch mode.
-    ``native``: also run covered ATen ops on the HIP kernels (else only count)."""
-    labels = getattr(_TLS, "labels", None)
-    if labels is None:
-        labels = _TLS.labels = []
-        _TLS.natives = []
-    outer = not labels
-    labels.append(label)
-    _TLS.natives.append(bool(native))  # the innermost region decides native execution
-    mode = None
-    try:
+    ``native``: run covered ATen ops on the HIP kernels (else only count).  A plain
+    class (not a generator context manager) and one reused mode object per thread:
+    this is entered once per eager op."""
+
+    __slots__ = ("label", "native", "mode")
+
+    def __init__(self, label: str, native: bool = True):
+        self.label, self.native, self.mode = label, native, None
+
+    def __enter__(self):
+        labels = getattr(_TLS, "labels", None)
+        if labels is None:
+            labels = _TLS.labels = []
+            _TLS.natives = []
+        outer = not labels
+        labels.append(self.label)
+        _TLS.natives.append(bool(self.native))  # the innermost region decides native execution
         if outer and (native_dispatch() or counting()):
-            mode = _Watch(native_dispatch())
-            mode.__enter__()
-        yield
-    finally:
-        if mode is not None:
-            mode.__exit__(None, None, None)
-        labels.pop()
+            m = getattr(_TLS, "mode", None)
+            nat = native_dispatch()
+            if m is None or m.native != nat:
+                m = _TLS.mode = _Watch(nat)
+            m.__enter__()
+            self.mode = m
+        return self
+
+    def __exit__(self, *exc):
+        if self.mode is not None:
+            self.mode.__exit__(None, None, None)
+            self.mode = None
+        _TLS.labels.pop()
         _TLS.natives.pop()
+        return False
 
 
 @contextlib.contextmanager

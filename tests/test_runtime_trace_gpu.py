@@ -15,11 +15,11 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _kernel_counts(tmp, steps):
-    out = os.path.join(tmp, f"s{steps}")
+def _kernel_counts(tmp, steps, script=("llama_tiny_step.py",)):
+    out = os.path.join(tmp, f"{'_'.join(script)}_s{steps}".replace(".py", ""))
     env = dict(os.environ, TMPDIR="/tmp")
     cmd = [shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3", "--kernel-trace", "-d", out, "-o", "run", "--",
-           sys.executable, os.path.join(ROOT, "tools", "llama_tiny_step.py"), str(steps)]
+           sys.executable, os.path.join(ROOT, "tools", script[0]), *script[1:], str(steps)]
     subprocess.run(cmd, check=True, cwd="/tmp", env=env, timeout=240, stdout=subprocess.DEVNULL)
     dbs = [os.path.join(d, f) for d, _, fs in os.walk(out) for f in fs if f.endswith("_results.db")]
     assert dbs, f"no rocpd database under {out}"
@@ -43,3 +43,24 @@ def test_llama_tiny_step_runs_no_aten_compute_kernels(tmp_path):
     bad = sorted(k[:120] for k in per_step if not _allowed(k))
     assert not bad, f"ATen compute kernels on the step path: {bad}"
     assert any("gemm_kernel" in k for k in per_step) and any("fa_" in k for k in per_step)
+
+
+def _aten_compute(name):
+    """An ATen device kernel that computes (fills / copies are data movement)."""
+    return ("at::native" in name or name.startswith(("void at::", "at::"))) and not any(
+        k in name for k in ("FillFunctor", "copy_kernel", "direct_copy", "CatArrayBatchedCopy"))
+
+
+@pytest.mark.skipif(shutil.which("rocprofv3") is None and not os.path.exists("/opt/rocm/bin/rocprofv3"),
+                    reason="rocprofv3 not installed")
+@pytest.mark.parametrize("model", ["eager18", "fluid50"])
+def test_resnet_step_runs_no_aten_compute_kernels(tmp_path, model):
+    """DyGraph ResNet-18 bf16 (eager engine + native tensor-op dispatch) and Fluid
+    ResNet-50 (static program, native op kernels): the kernels that grow with the
+    step count include no ATen compute kernel."""
+    one = _kernel_counts(str(tmp_path), 1, ("resnet_steps.py", model))
+    three = _kernel_counts(str(tmp_path), 3, ("resnet_steps.py", model))
+    per_step = {k: three[k] - one.get(k, 0) for k in three if three[k] > one.get(k, 0)}
+    assert per_step, "no kernels recorded per step"
+    bad = sorted(k[:120] for k in per_step if _aten_compute(k))
+    assert not bad, f"ATen compute kernels on the {model} step path: {bad}"
