@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Host cost of the native tensor-op dispatch (utils/strict.py + ops/aten_native.py)
+per call, on GPU tensors: ATen add vs the same add inside a framework region (HIP
+kernel), a view op passing through the dispatch mode, and region enter/exit.
+Prints one JSON line (microseconds per call, host wall, median of 5 x 2000)."""
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from paddle_amd.utils import strict  # noqa: E402
+
+
+def t(fn, n=2000):
+    res = []
+    for _ in range(5):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        res.append((time.perf_counter() - t0) / n * 1e6)
+    torch.cuda.synchronize()
+    return round(statistics.median(res), 2)
+
+
+x = torch.randn(1024, device="cuda")
+y = torch.randn(1024, device="cuda")
+r = strict.region("bench")
+out = {
+    "aten_add_us": t(lambda: x + y),
+    "aten_view_us": t(lambda: x.view(32, 32)),
+    "empty_region_us": t(lambda: (r.__enter__(), r.__exit__(None, None, None))),
+}
+with strict.region("bench"):
+    out["native_add_in_region_us"] = t(lambda: x + y)
+    out["view_in_region_us"] = t(lambda: x.view(32, 32))
+    out["empty_in_region_us"] = t(lambda: torch.empty(1024, device="cuda"))
+    out["cast_in_region_us"] = t(lambda: x.to(torch.bfloat16))
+out["aten_cast_us"] = t(lambda: x.to(torch.bfloat16))
+print(json.dumps(out))

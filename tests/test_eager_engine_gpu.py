@@ -109,7 +109,19 @@ def test_lenet_fp32_gpu_trajectory_matches_cpu_fp32():
             lambda ps: paddle.optimizer.Adam(learning_rate=2e-3, parameters=ps), rtol=1e-3)
 
 
+def test_resnet18_fp32_nhwc_gpu_trajectory_matches_cpu_fp32():
+    """fp32 on both sides: isolates kernel/engine errors from bf16 rounding."""
+    _oracle(lambda: paddle.vision.models.resnet18(num_classes=10, data_format="NHWC"), torch.float32,
+            (16, 64, 64, 3), lambda ps: paddle.optimizer.Momentum(learning_rate=0.01, momentum=0.9, parameters=ps),
+            rtol=5e-3)
+
+
 def test_resnet18_bf16_nhwc_gpu_trajectory_matches_cpu_fp32():
+    """AMP-O2 style: bf16 parameters/activations with fp32 master weights.  BN over
+    16x2x2 values per channel in layer4 and bf16 rounding bound the agreement, so two
+    steps at 3e-2 (the first step is a pure forward check)."""
     _oracle(lambda: paddle.vision.models.resnet18(num_classes=10, data_format="NHWC"), torch.bfloat16,
-            (8, 32, 32, 3), lambda ps: paddle.optimizer.Momentum(learning_rate=0.01, momentum=0.9, parameters=ps),
-            rtol=5e-2)
+            (16, 64, 64, 3),
+            lambda ps: paddle.optimizer.Momentum(learning_rate=0.01, momentum=0.9, parameters=ps,
+                                                 multi_precision=True),
+            steps=2, rtol=3e-2)

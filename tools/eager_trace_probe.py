@@ -27,7 +27,7 @@ y = paddle.to_tensor(np.arange(8) % 10)
 
 def step():
     # an outer region labels whatever ATen work the framework's own regions miss
-    with strict.region("probe:step", native=False):
+    with strict.region("probe:step"):
         return _step()
 
 
