@@ -82,7 +82,7 @@ class GradNode:
     """One recorded op.  ``edges[i]`` is where the gradient of differentiable input i
     goes: ``(node, output_index)``, ``(None, leaf_tensor)`` or ``None``."""
 
-    __slots__ = ("name", "backward", "edges", "nout", "out_meta")
+    __slots__ = ("name", "backward", "edges", "nout", "out_meta", "accum", "prev")
 
     def __init__(self, name, backward, edges, nout, out_meta):
         self.name = name
@@ -90,6 +90,13 @@ class GradNode:
         self.edges = edges
         self.nout = nout
         self.out_meta = out_meta  # (shape, dtype, device) per output, to materialise zero grads
+        # accum: the backward may sum an input gradient INTO the gradient the engine
+        # already holds for that input (``prev[i]``, offered only when its producer
+        # marked it exclusively owned: ``_pa_acc_ok``) and return that same tensor --
+        # e.g. a conv's dX accumulated onto the residual branch's gradient in the GEMM
+        # epilogue instead of a separate add pass
+        self.accum = False
+        self.prev = None
 
     def __repr__(self):
         return f"<GradNode {self.name}>"
@@ -399,13 +406,20 @@ def record_function(fn, args):
         out = _wrap(out)
         outs = [out] if single else list(out)
 
+        holder = []
+
         def bwd(*gouts):
             # hand-written backward kernels index their gradient inputs densely
             gouts = [g.contiguous() if isinstance(g, torch.Tensor) else g for g in gouts]
+            ctx.grad_prev = holder[0].prev if holder else None
             r = fn.backward(ctx, *gouts)
+            ctx.grad_prev = None
             return r if isinstance(r, tuple) else (r,)
 
-        _record(getattr(fn, "__name__", "fused"), bwd, list(args), outs)
+        node = _record(getattr(fn, "__name__", "fused"), bwd, list(args), outs)
+        if node is not None:
+            node.accum = True
+            holder.append(node)
         return out
 
 
@@ -511,7 +525,10 @@ def _backward_impl(roots, grads, retain_graph):
             if any(g is not None for g in gouts):
                 gouts = [g if g is not None or m is None or not _is_float_dtype(m[1])
                          else torch.zeros(m[0], dtype=m[1], device=m[2]) for g, m in zip(gouts, n.out_meta)]
+                if n.accum and _ACCUM_INTO[0]:
+                    n.prev = _prev_grads(n, buffers)
                 gins = n.backward(*gouts)
+                n.prev = None
                 if not isinstance(gins, (tuple, list)):
                     gins = (gins,)
             else:
@@ -531,7 +548,8 @@ def _backward_impl(roots, grads, retain_graph):
                     continue
                 if g is not None:
                     buf = buffers.setdefault(child, [None] * child.nout)
-                    buf[tgt] = _accumulate(buf[tgt], g)
+                    cur = buf[tgt]
+                    buf[tgt] = g if g is cur else _accumulate(cur, g)  # `is`: summed in place by the backward
                 deps[child] -= 1
                 if deps[child] == 0:
                     ready.append(child)
@@ -544,6 +562,25 @@ def _backward_impl(roots, grads, retain_graph):
     finally:
         _TLS.callbacks = outer
         torch._C._set_grad_enabled(prev)
+
+
+_ACCUM_INTO = [__import__("os").environ.get("FLAGS_eager_accumulate_into", "1") != "0"]
+
+
+def _prev_grads(n, buffers):
+    """Per input edge of ``n``: the gradient already accumulated for that input when
+    its producer marked it exclusively owned (``_pa_acc_ok``), else None."""
+    out = []
+    for e in n.edges:
+        g = None
+        if e is not None and e[0] is not None:
+            b = buffers.get(e[0])
+            if b is not None:
+                g = b[e[1]]
+                if g is not None and not getattr(g, "_pa_acc_ok", False):
+                    g = None
+        out.append(g)
+    return out
 
 
 def _is_float_dtype(dt):

@@ -168,40 +168,50 @@ __global__ __launch_bounds__(BN_T) void bn_reduce_kernel(const u16* __restrict__
 
 // forward finalize: mean, rstd (saved for backward), running stats update
 // (running = m * running + (1 - m) * batch, unbiased variance), one thread per channel
-// sum the G block partials of channel c: 1024 threads = 64 channels x 16 slices, fp64
+// sum the G block partials of channel c: 1024 threads = 16 channels x 64 slices
+// (64 independent fp64 chains per channel: latency-bound G of several thousand --
+// the per-tile partials of the conv epilogue -- stays a few microseconds), tree
+// over the slices in LDS
 __device__ __forceinline__ bool bn_sum_partials(const float* __restrict__ partial, int G, int C, int& c, double& s0,
                                                 double& s1) {
-  __shared__ double red[2][16][64];
-  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  c = blockIdx.x * 64 + cl;
+  __shared__ double red[2][64][16];
+  const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  c = blockIdx.x * 16 + cl;
   double a0 = 0.0, a1 = 0.0;
   if (c < C)
-    for (int g = sl; g < G; g += 16) {
+    for (int g = sl; g < G; g += 64) {
       a0 += partial[((long)g * 2) * C + c];
       a1 += partial[((long)g * 2 + 1) * C + c];
     }
   red[0][sl][cl] = a0;
   red[1][sl][cl] = a1;
   __syncthreads();
-  if (sl != 0 || c >= C) return false;
-  s0 = s1 = 0.0;
-  for (int i = 0; i < 16; ++i) {
-    s0 += red[0][i][cl];
-    s1 += red[1][i][cl];
+  for (int h = 32; h > 0; h >>= 1) {
+    if (sl < h) {
+      red[0][sl][cl] += red[0][sl + h][cl];
+      red[1][sl][cl] += red[1][sl + h][cl];
+    }
+    __syncthreads();
   }
+  if (sl != 0 || c >= C) return false;
+  s0 = red[0][0][cl];
+  s1 = red[1][0][cl];
   return true;
 }
 
 __global__ __launch_bounds__(1024) void bn_finalize_fwd_kernel(const float* __restrict__ partial, int G,
-                                                               const u16* __restrict__ x, int C, long rows, float eps,
-                                                               float momentum, float* __restrict__ mean_out,
+                                                               const u16* __restrict__ x,
+                                                               const float* __restrict__ shiftf, int C, long rows,
+                                                               float eps, float momentum, float* __restrict__ mean_out,
                                                                float* __restrict__ rstd_out,
                                                                float* __restrict__ run_mean,
                                                                float* __restrict__ run_var, int update_running) {
   int c;
   double s0, s1;
   if (!bn_sum_partials(partial, G, C, c, s0, s1)) return;
-  const double shift = bf2f(x[c]);
+  // the shift the partials were taken about: the first pixel (bn_reduce) or a given
+  // per-channel value (conv epilogue statistics; null = 0)
+  const double shift = x ? (double)bf2f(x[c]) : shiftf ? (double)shiftf[c] : 0.0;
   const double n = (double)rows;
   const double md = s0 / n;
   double var = s1 / n - md * md;
@@ -568,8 +578,23 @@ PA_EXPORT int pa_bn_fwd_train(const void* x, void* y, const void* w, const void*
   const int G = pa_bn_blocks(rows, C);
   hipLaunchKernelGGL(bn_reduce_kernel<false>, dim3(G), dim3(BN_T), bn_shm(C), st, (const u16*)x, nullptr,
                      BnMask{nullptr, nullptr, nullptr, nullptr, 0}, nullptr, part, rows, C, 0);
-  hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, part, G, (const u16*)x, C, rows,
-                     eps, momentum, mean, rstd, run_mean, run_var, run_mean != nullptr);
+  hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3((C + 15) / 16), dim3(1024), 0, st, part, G, (const u16*)x,
+                     (const float*)nullptr, C, rows, eps, momentum, mean, rstd, run_mean, run_var, run_mean != nullptr);
+  int eg, eb;
+  bn_ew_launch(rows, C, eg, eb);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(eg), dim3(eb), 0, st, (const u16*)x, (u16*)y, mean, rstd, w, b, wdt, rows,
+                     C, relu, (const u16*)res);
+  PA_LAUNCH_CHECK();
+}
+
+// training forward from statistics the producing convolution already emitted
+// (pa_conv_sn's epilogue: part[G][2][C] about `shift`): no statistics pass over x
+PA_EXPORT int pa_bn_fwd_stats(const float* part, int G, const float* shift, const void* x, void* y, const void* w,
+                              const void* b, int wdt, float* run_mean, float* run_var, float* mean, float* rstd,
+                              long rows, int C, float eps, float momentum, int relu, const void* res, hipStream_t st) {
+  if (C % 8) return -1;
+  hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3((C + 15) / 16), dim3(1024), 0, st, part, G, (const u16*)nullptr,
+                     shift, C, rows, eps, momentum, mean, rstd, run_mean, run_var, run_mean != nullptr);
   int eg, eb;
   bn_ew_launch(rows, C, eg, eb);
   hipLaunchKernelGGL(bn_apply_kernel, dim3(eg), dim3(eb), 0, st, (const u16*)x, (u16*)y, mean, rstd, w, b, wdt, rows,
@@ -601,7 +626,7 @@ PA_EXPORT int pa_bn_bwd2(const void* x, const void* dy, const void* y, const flo
   const BnMask mk{(const u16*)y, rstd, w, b, wdt};
   hipLaunchKernelGGL(bn_reduce_kernel<true>, dim3(G), dim3(BN_T), bn_shm(C), st, (const u16*)x, (const u16*)dy,
                      mk, mean, part, rows, C, relu);
-  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, part, G, C, rows, rstd, w, wdt,
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 15) / 16), dim3(1024), 0, st, part, G, C, rows, rstd, w, wdt,
                      dw, db, coef);
   int eg, eb;
   bn_ew_launch(rows, C, eg, eb);

@@ -1042,9 +1042,21 @@ PA_EXPORT int pa_gemm(int a_kmaj, int b_kmaj, int out_f32, const void* A, const 
 //   out[(n, oy, ox)][co] = sum_{kh, kw, c} src[n, iy, ix, c] * wt[co][kh][kw][c]
 // src: [N, H, W, C] (C % 64 == 0), wt: [Cout][KH*KW*C] K-major, out: [N*OH*OW][Cout]
 // (ldc = Cout), bias [Cout] or null.  Returns -1 for shapes the kernel does not cover.
+PA_EXPORT int pa_conv_gemm_acc(const void* src, const void* wt, void* out, const void* bias, int Nb, int H, int W,
+                               int C, int OH, int OW, int Cout, int KH, int KW, int sy, int sx, int py, int px, int dy,
+                               int dx, int uy, int ux, int accumulate, hipStream_t st);
+
 PA_EXPORT int pa_conv_gemm(const void* src, const void* wt, void* out, const void* bias, int Nb, int H, int W, int C,
                            int OH, int OW, int Cout, int KH, int KW, int sy, int sx, int py, int px, int dy, int dx,
                            int uy, int ux, hipStream_t st) {
+  return pa_conv_gemm_acc(src, wt, out, bias, Nb, H, W, C, OH, OW, Cout, KH, KW, sy, sx, py, px, dy, dx, uy, ux, 0,
+                          st);
+}
+
+// accumulate: out += conv (bf16 read-modify-write in the epilogue: a gradient summed in place)
+PA_EXPORT int pa_conv_gemm_acc(const void* src, const void* wt, void* out, const void* bias, int Nb, int H, int W,
+                               int C, int OH, int OW, int Cout, int KH, int KW, int sy, int sx, int py, int px, int dy,
+                               int dx, int uy, int ux, int accumulate, hipStream_t st) {
   const long M = (long)Nb * OH * OW;
   if (M <= 0 || Cout <= 0) return 0;
   if (C % 64 || Cout % 8 || M > 0x7fffffffL || (long)Nb * H * W * C >= 0x7fffffffL || H > 32767 || W > 32767)
@@ -1054,6 +1066,7 @@ PA_EXPORT int pa_conv_gemm(const void* src, const void* wt, void* out, const voi
   p.M = (int)M; p.N = Cout; p.K = KH * KW * C;
   p.lda = C; p.ldb = p.K; p.ldc = Cout;
   p.alpha = 1.f;
+  p.accumulate = accumulate;
   p.H = H; p.W = W; p.Cc = C; p.OH = OH; p.OW = OW; p.KW = KW;
   p.sy = sy; p.sx = sx; p.py = py; p.px = px; p.dy = dy; p.dx = dx; p.uy = uy; p.ux = ux;
   p.tiles_m = (p.M + gemm::BM - 1) / gemm::BM;

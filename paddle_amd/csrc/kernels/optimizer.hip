@@ -90,6 +90,51 @@ __global__ void momentum_kernel(TP* __restrict__ p, const TG* __restrict__ g,
   }
 }
 
+// Multi-tensor Momentum: every parameter of a model in ONE launch (a DyGraph model
+// has hundreds of small parameters; one launch + host call each dominates the step
+// of a conv net).  A device table describes each tensor; block b updates chunk
+// b - chunk0 (MCHUNK elements) of the tensor whose chunk range holds b (binary
+// search over the table).  Per tensor: L2 decay `wd` on the updated value, an lr
+// multiplier, and an optional second output (the bf16 model copy of an fp32 master).
+struct MomT {
+  void* t;         // updated tensor: fp32 master, or the fp32 / bf16 parameter itself
+  void* out;       // optional model copy written with the new value (null: none)
+  const void* g;   // gradient (fp32 / bf16)
+  float* vel;      // fp32 velocity
+  long n;
+  long chunk0;     // first chunk index of this tensor
+  float wd, lr_scale;
+  int tdt, odt, gdt, pad;  // dtypes: 0 fp32, 1 bf16
+};
+constexpr int MCHUNK = 4096;
+
+__global__ __launch_bounds__(256) void momentum_multi_kernel(const MomT* __restrict__ tab, int nt, float lr,
+                                                             const float* __restrict__ lr_ptr, float mu,
+                                                             int nesterov, float gscale) {
+  const long b = blockIdx.x;
+  int lo = 0, hi = nt - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[mid].chunk0 <= b) lo = mid; else hi = mid - 1;
+  }
+  const MomT e = tab[lo];
+  const float lr_ = (lr_ptr ? lr_ptr[0] : lr) * e.lr_scale;
+  const long base = (b - e.chunk0) * MCHUNK;
+  const long end = base + MCHUNK < e.n ? base + MCHUNK : e.n;
+  for (long i = base + threadIdx.x; i < end; i += blockDim.x) {
+    const float pi = e.tdt ? bf2f(((const u16*)e.t)[i]) : ((const float*)e.t)[i];
+    const float gi = e.gdt ? bf2f(((const u16*)e.g)[i]) : ((const float*)e.g)[i];
+    const float gg = gi * gscale + e.wd * pi;
+    const float v = mu * e.vel[i] + gg;
+    e.vel[i] = v;
+    const float po = pi - lr_ * (nesterov ? gg + mu * v : v);
+    if (e.tdt) ((u16*)e.t)[i] = f2bf(po); else ((float*)e.t)[i] = po;
+    if (e.out) {
+      if (e.odt) ((u16*)e.out)[i] = f2bf(po); else ((float*)e.out)[i] = po;
+    }
+  }
+}
+
 // sum of squares (for global-norm clipping): out[0] += sum(x^2); 16-B vector loads,
 // one fp32 atomic per block.
 template <typename T>
@@ -198,3 +243,18 @@ PA_EXPORT int pa_fold_grad(int gdtype, float* dst, const void* g, long n, int fr
     hipLaunchKernelGGL(fold_grad_kernel<float>, dim3(grid), dim3(256), 0, st, dst, (const float*)g, n, fresh);
   PA_LAUNCH_CHECK();
 }
+
+// tab: device array of nt MomT entries (chunk0 ascending), total_chunks = sum of
+// ceil(n / MCHUNK); see ops/optim.py momentum_multi
+PA_EXPORT int pa_momentum_multi(const void* tab, int nt, long total_chunks, float lr, const float* lr_ptr, float mu,
+                                int nesterov, float gscale, hipStream_t st) {
+  if (nt <= 0 || total_chunks <= 0) return 0;
+  if (total_chunks > 0x7fffffffL) return -1;
+  hipLaunchKernelGGL(momentum_multi_kernel, dim3((unsigned)total_chunks), dim3(256), 0, st, (const MomT*)tab, nt, lr,
+                     lr_ptr, mu, nesterov, gscale);
+  PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_momentum_multi_entry_bytes() { return (int)sizeof(MomT); }
+PA_EXPORT int pa_momentum_multi_chunk() { return MCHUNK; }
+

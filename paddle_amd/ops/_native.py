@@ -73,6 +73,16 @@ _SIGS = {
     "pa_fa_dq_reduce_rope": [_P, _I, _I, _I, _I, _I, _I, _P, _L, _P, _P, _I, _P],
     "pa_fa_bwd_part_kblk": [_I, _I, _I, _I],
     "pa_conv_gemm": [_P, _P, _P, _P] + [_I] * 17 + [_P],
+    "pa_conv_sn": [_P, _P, _P, _P] + [_I] * 17 + [_P, _P, _P],
+    "pa_conv_sn_tiles": [_L],
+    "pa_conv_sn_acc": [_P, _P, _P, _P] + [_I] * 17 + [_P, _P, _I, _P],
+    "pa_conv_gemm_acc": [_P, _P, _P, _P] + [_I] * 18 + [_P],
+    "pa_momentum_multi": [_P, _I, _L, _F, _P, _F, _I, _F, _P],
+    "pa_momentum_multi_entry_bytes": [],
+    "pa_momentum_multi_chunk": [],
+    "pa_conv_wgrad_sn_ws": [_I] * 9,
+    "pa_conv_wgrad_sn": [_P, _P, _P, _P] + [_I] * 16 + [_P],
+    "pa_bn_fwd_stats": [_P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _L, _I, _F, _F, _I, _P, _P],
     "pa_im2col_nhwc": [_P, _P] + [_I] * 15 + [_P],
     "pa_bn_blocks": [_L, _I],
     "pa_bn_fwd_train": [_P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _L, _I, _F, _F, _I, _P, _P],

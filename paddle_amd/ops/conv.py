@@ -20,6 +20,7 @@ dtypes these kernels do not cover.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -75,7 +76,28 @@ def _im2col(x, KH, KW, s, p, d, OH, OW, Kp):
     return col
 
 
-def _conv_fwd(x, w, b, s, p, d):
+# output-channel counts up to this take the 64-wide tile kernel (csrc/kernels/convsn.hip)
+_SN_MAX = [int(os.environ.get("FLAGS_conv_sn_max_cout", "128"))]
+
+
+def _sn(x, wk, y, bias, geo, stats=None, acc=False):
+    """pa_conv_sn (64-channel tiles; optional BN statistics of y into ``stats``;
+    ``acc``: y += conv)."""
+    N, OH, OW, Cout = y.shape
+    part = shift = None
+    G = 0
+    if stats is not None:
+        G = int(_nat.lib().pa_conv_sn_tiles(N * OH * OW))
+        part = torch.empty(G * 2 * Cout, dtype=torch.float32, device=y.device)
+        shift = stats.get("shift")
+    rc = _nat.lib().pa_conv_sn_acc(_nat.ptr(x), _nat.ptr(wk), _nat.ptr(y), _nat.ptr(bias), *geo, _nat.ptr(part),
+                                   _nat.ptr(shift), int(acc), _nat.stream())
+    if rc == 0 and stats is not None:
+        stats["part"], stats["G"] = part, G
+    return rc == 0
+
+
+def _conv_fwd(x, w, b, s, p, d, stats=None):
     N, H, W, C = x.shape
     Cout, _, KH, KW = w.shape
     OH, OW = _out_hw(H, W, KH, KW, s, p, d)
@@ -85,6 +107,9 @@ def _conv_fwd(x, w, b, s, p, d):
     if C % 64 == 0:
         wk = wk.contiguous()
         y = torch.empty(N, OH, OW, Cout, dtype=x.dtype, device=x.device)
+        if Cout <= _SN_MAX[0] and _sn(x, wk, y, bias, (N, H, W, C, OH, OW, Cout, KH, KW, s[0], s[1], p[0], p[1],
+                                                       d[0], d[1], 0, 0), stats):
+            return y
         rc = _nat.lib().pa_conv_gemm(_nat.ptr(x), _nat.ptr(wk), _nat.ptr(y), _nat.ptr(bias), N, H, W, C, OH, OW,
                                      Cout, KH, KW, s[0], s[1], p[0], p[1], d[0], d[1], 0, 0, _nat.stream())
         _nat.check(rc, "pa_conv_gemm")
@@ -97,18 +122,25 @@ def _conv_fwd(x, w, b, s, p, d):
     return y.view(N, OH, OW, Cout)
 
 
-def _conv_dgrad(dy, w, x_shape, s, p, d):
+def _conv_dgrad(dy, w, x_shape, s, p, d, into=None):
+    """dX of the convolution.  ``into``: an exclusively owned gradient of x already
+    summed by the engine (e.g. the residual branch's): dX is accumulated into it in
+    the GEMM epilogue and ``into`` is returned (no separate add pass)."""
     N, H, W, C = x_shape
     Cout, _, KH, KW = w.shape
     OH, OW = dy.shape[1], dy.shape[2]
     if Cout % 64 == 0 and C % 8 == 0:
         # dX = conv(zero-inserted dY, flipped W^T): wd[c][kh][kw][co] = w[co][c][KH-1-kh][KW-1-kw]
         wd = w.to(dy.dtype).flip(2, 3).permute(1, 2, 3, 0).reshape(C, KH * KW * Cout).contiguous()
-        dx = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
+        acc = (into is not None and into.shape == (N, H, W, C) and into.dtype == dy.dtype and into.is_contiguous())
+        dx = into if acc else torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
         pyy, pxx = d[0] * (KH - 1) - p[0], d[1] * (KW - 1) - p[1]
-        rc = _nat.lib().pa_conv_gemm(_nat.ptr(dy), _nat.ptr(wd), _nat.ptr(dx), None, N, OH, OW, Cout, H, W, C, KH,
-                                     KW, 1, 1, pyy, pxx, d[0], d[1], int(math.log2(s[0])), int(math.log2(s[1])),
-                                     _nat.stream())
+        geo = (N, OH, OW, Cout, H, W, C, KH, KW, 1, 1, pyy, pxx, d[0], d[1], int(math.log2(s[0])),
+               int(math.log2(s[1])))
+        if C <= _SN_MAX[0] and _sn(dy, wd, dx, None, geo, acc=acc):
+            return dx
+        rc = _nat.lib().pa_conv_gemm_acc(_nat.ptr(dy), _nat.ptr(wd), _nat.ptr(dx), None, *geo, int(acc),
+                                         _nat.stream())
         if rc == 0:
             return dx
     # rare shapes: autograd of the torch convolution
@@ -117,12 +149,34 @@ def _conv_dgrad(dy, w, x_shape, s, p, d):
         0, 2, 3, 1).contiguous()
 
 
+# weight gradient on the gathered 64x256-tile kernel (convsn.hip): "auto" = when the
+# wide path would need an im2col buffer (k > 1 or strided) or Cout <= 128
+_WGRAD_SN = [os.environ.get("FLAGS_conv_wgrad_sn", "auto")]
+
+
+def _wgrad_sn_wanted(C, Cout, KH, KW, s):
+    m = _WGRAD_SN[0]
+    if m == "0" or C % 64 or Cout % 8:
+        return False
+    return m == "1" or KH * KW > 1 or s != (1, 1) or Cout <= 128
+
+
 def _conv_wgrad(dy, x, w_shape, s, p, d):
     N, H, W, C = x.shape
     Cout, _, KH, KW = w_shape
     OH, OW = dy.shape[1], dy.shape[2]
     M = N * OH * OW
     K = KH * KW * C
+    if _wgrad_sn_wanted(C, Cout, KH, KW, s):
+        L = _nat.lib()
+        nws = int(L.pa_conv_wgrad_sn_ws(N, H, W, C, OH, OW, Cout, KH, KW))
+        if nws >= 0:
+            ws = torch.empty(max(nws, 1), dtype=torch.float32, device=x.device) if nws > 0 else None
+            dwk = torch.empty(Cout, K, dtype=torch.float32, device=x.device)
+            rc = L.pa_conv_wgrad_sn(_nat.ptr(dy), _nat.ptr(x), _nat.ptr(dwk), _nat.ptr(ws), N, H, W, C, OH, OW, Cout,
+                                    KH, KW, s[0], s[1], p[0], p[1], d[0], d[1], 0, _nat.stream())
+            if rc == 0:
+                return dwk.reshape(Cout, KH, KW, C).permute(0, 3, 1, 2)
     if KH == 1 and KW == 1 and s == (1, 1) and p == (0, 0) and C % 8 == 0:
         col, Kp = x.reshape(M, C), C
     else:
@@ -137,8 +191,8 @@ def _conv_wgrad(dy, x, w_shape, s, p, d):
 
 class _Conv2dNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, s, p, d):
-        y = _conv_fwd(x, w, b, s, p, d)
+    def forward(ctx, x, w, b, s, p, d, stats=None):
+        y = _conv_fwd(x, w, b, s, p, d, stats)
         ctx.save_for_backward(x, w)
         ctx.conf = (s, p, d, b is not None)
         return y
@@ -148,16 +202,24 @@ class _Conv2dNHWC(torch.autograd.Function):
         x, w = ctx.saved_tensors
         s, p, d, has_b = ctx.conf
         dy = dy.contiguous()
-        dx = _conv_dgrad(dy, w, tuple(x.shape), s, p, d) if ctx.needs_input_grad[0] else None
+        into = getattr(ctx, "grad_prev", None)
+        into = into[0] if into else None
+        dx = _conv_dgrad(dy, w, tuple(x.shape), s, p, d, into) if ctx.needs_input_grad[0] else None
+        if dx is not None:
+            dx._pa_acc_ok = True  # exclusively owned: later producers may accumulate into it
         dw = _conv_wgrad(dy, x, tuple(w.shape), s, p, d).to(w.dtype) if ctx.needs_input_grad[1] else None
         db = dy.reshape(-1, dy.shape[-1]).float().sum(0).to(w.dtype) if has_b and ctx.needs_input_grad[2] else None
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None
 
 
-def conv2d_nhwc(x, weight, bias=None, stride=1, padding=0, dilation=1):
-    """x [N, H, W, C] bf16 contiguous, weight [Cout, Cin, KH, KW] (Paddle layout)."""
+def conv2d_nhwc(x, weight, bias=None, stride=1, padding=0, dilation=1, stats=None):
+    """x [N, H, W, C] bf16 contiguous, weight [Cout, Cin, KH, KW] (Paddle layout).
+    ``stats`` (a dict, optional): request the BatchNorm batch statistics of the output
+    from the conv epilogue (``stats["shift"]``: fp32 [Cout] shift, e.g. the running
+    mean, or absent); on return it holds ``part`` / ``G`` when the kernel emitted them
+    (64-channel-tile path), for :func:`batch_norm_nhwc_train`'s ``stats``."""
     s, p, d = _pair(stride), _pair(padding), _pair(dilation)
-    return _tape.apply(_Conv2dNHWC, x, weight, bias, tuple(map(_i, s)), tuple(map(_i, p)), tuple(map(_i, d)))
+    return _tape.apply(_Conv2dNHWC, x, weight, bias, tuple(map(_i, s)), tuple(map(_i, p)), tuple(map(_i, d)), stats)
 
 
 # ------------------------------------------------------------------ depthwise conv (dwconv.hip)
@@ -229,23 +291,31 @@ def _wdt(w):
 
 class _BatchNormNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, run_mean, run_var, momentum, eps, relu, res):
+    def forward(ctx, x, w, b, run_mean, run_var, momentum, eps, relu, res, stats=None):
         C = x.shape[-1]
         rows = x.numel() // C
         wdt, wc = _wdt(w)
         _, bc = _wdt(b) if b is not None else (0, None)
         if b is not None and w is not None and bc.dtype != wc.dtype:
             bc = bc.to(wc.dtype)
-        G = int(_nat.lib().pa_bn_blocks(rows, C))
-        part = torch.empty(G * 2 * C, dtype=torch.float32, device=x.device)
+        pre = stats is not None and stats.get("part") is not None
+        G = 0 if pre else int(_nat.lib().pa_bn_blocks(rows, C))
+        part = None if pre else torch.empty(G * 2 * C, dtype=torch.float32, device=x.device)
         mean = torch.empty(C, dtype=torch.float32, device=x.device)
         rstd = torch.empty(C, dtype=torch.float32, device=x.device)
         y = torch.empty_like(x)
         rm = run_mean if (run_mean is not None and run_mean.dtype == torch.float32) else None
         rv = run_var if rm is not None else None
-        _nat.call("pa_bn_fwd_train", _nat.ptr(x), _nat.ptr(y), _nat.ptr(wc), _nat.ptr(bc), wdt, _nat.ptr(rm),
-                  _nat.ptr(rv), _nat.ptr(mean), _nat.ptr(rstd), _nat.ptr(part), rows, C, float(eps),
-                  float(momentum), int(relu), _nat.ptr(res), _nat.stream())
+        if pre:
+            # statistics already emitted by the producing conv's epilogue
+            _nat.call("pa_bn_fwd_stats", _nat.ptr(stats["part"]), int(stats["G"]), _nat.ptr(stats.get("shift")),
+                      _nat.ptr(x), _nat.ptr(y), _nat.ptr(wc), _nat.ptr(bc), wdt, _nat.ptr(rm), _nat.ptr(rv),
+                      _nat.ptr(mean), _nat.ptr(rstd), rows, C, float(eps), float(momentum), int(relu),
+                      _nat.ptr(res), _nat.stream())
+        else:
+            _nat.call("pa_bn_fwd_train", _nat.ptr(x), _nat.ptr(y), _nat.ptr(wc), _nat.ptr(bc), wdt, _nat.ptr(rm),
+                      _nat.ptr(rv), _nat.ptr(mean), _nat.ptr(rstd), _nat.ptr(part), rows, C, float(eps),
+                      float(momentum), int(relu), _nat.ptr(res), _nat.stream())
         if (run_mean is not None and rm is None and run_mean.dtype == torch.bfloat16 and run_var is not None
                 and run_var.dtype == torch.bfloat16 and run_mean.is_contiguous() and run_var.is_contiguous()):
             # bf16 running stats (a bf16-cast model): one native update launch
@@ -282,12 +352,15 @@ class _BatchNormNHWC(torch.autograd.Function):
         _nat.call("pa_bn_bwd2", _nat.ptr(x), _nat.ptr(dy), _nat.ptr(y), _nat.ptr(mean), _nat.ptr(rstd),
                   _nat.ptr(wc), _nat.ptr(bc), wdt, _nat.ptr(dx), _nat.ptr(dw), _nat.ptr(db), _nat.ptr(coef),
                   _nat.ptr(part), rows, C, int(relu), _nat.ptr(dres), _nat.stream())
+        dx._pa_acc_ok = True  # fresh, exclusively owned gradients (see ops.conv._conv_dgrad's into)
+        if dres is not None:
+            dres._pa_acc_ok = True
         return (dx, dw.to(ctx.wdtype) if has_w else None, db.to(ctx.bdtype) if has_b else None,
-                None, None, None, None, None, dres)
+                None, None, None, None, None, dres, None)
 
 
 def batch_norm_nhwc_train(x, weight, bias, running_mean, running_var, momentum=0.9, eps=1e-5, relu=False,
-                          residual=None):
+                          residual=None, stats=None):
     """Training-mode BatchNorm over all axes but the last (channels), optionally
     fused with a residual add and a ReLU: relu(BN(x) + residual).
     ``momentum``: Paddle convention, running = momentum * running + (1 - momentum) * batch."""
@@ -296,7 +369,7 @@ def batch_norm_nhwc_train(x, weight, bias, running_mean, running_var, momentum=0
             raise ValueError("the fused residual form is relu(bn(x) + residual)")
         residual = residual.contiguous()
     return _tape.apply(_BatchNormNHWC, x, weight, bias, running_mean, running_var, float(momentum), float(eps), bool(relu),
-                                residual)
+                       residual, stats)
 
 
 def batch_norm_nhwc_eval(x, weight, bias, running_mean, running_var, eps=1e-5, relu=False):

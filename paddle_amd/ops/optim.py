@@ -76,6 +76,73 @@ def momentum_flat(param, grad, velocity=None, *, lr, mu=0.9, nesterov=False, wei
     return param
 
 
+class MomentumMulti:
+    """Multi-tensor Momentum (``pa_momentum_multi``): one launch updates every
+    parameter.  The per-tensor descriptor table lives on the device and is re-uploaded
+    only when a pointer changes (steady-state training re-uses the caching
+    allocator's grad addresses); uploads go through two pinned host buffers, each
+    re-used only after the copy that read it has completed (event)."""
+
+    _DT = None
+
+    def __init__(self):
+        self._key = None
+        self._dev = None
+        self._chunks = 0
+        self._nt = 0
+        self._pinned = [None, None]
+        self._events = [None, None]
+        self._flip = 0
+
+    @classmethod
+    def _dtype(cls):
+        if cls._DT is None:
+            import numpy as np
+
+            cls._DT = np.dtype([("t", "<u8"), ("out", "<u8"), ("g", "<u8"), ("vel", "<u8"), ("n", "<i8"),
+                                ("chunk0", "<i8"), ("wd", "<f4"), ("lr_scale", "<f4"), ("tdt", "<i4"),
+                                ("odt", "<i4"), ("gdt", "<i4"), ("pad", "<i4")])
+            assert cls._DT.itemsize == int(N.lib().pa_momentum_multi_entry_bytes())
+        return cls._DT
+
+    def step(self, entries, *, lr, mu, nesterov=False, grad_scale=1.0, lr_tensor=None):
+        """entries: list of (target, out_or_None, grad, velocity, weight_decay, lr_scale);
+        target / out fp32 or bf16 contiguous, velocity fp32."""
+        if not entries:
+            return
+        import numpy as np
+
+        _fused.bump_weight_epoch()
+        key = tuple((t.data_ptr(), o.data_ptr() if o is not None else 0, g.data_ptr(), v.data_ptr(), t.numel(),
+                     N.dt(t), N.dt(o) if o is not None else 0, N.dt(g), float(wd), float(ls))
+                    for t, o, g, v, wd, ls in entries)
+        if key != self._key:
+            chunk = int(N.lib().pa_momentum_multi_chunk())
+            arr = np.zeros(len(key), dtype=self._dtype())
+            c0 = 0
+            for i, (tp, op, gp, vp, n, tdt, odt, gdt, wd, ls) in enumerate(key):
+                arr[i] = (tp, op, gp, vp, n, c0, wd, ls, tdt, odt, gdt, 0)
+                c0 += (n + chunk - 1) // chunk
+            raw = torch.from_numpy(arr.view(np.uint8))
+            b = self._flip
+            self._flip ^= 1
+            if self._events[b] is not None:
+                self._events[b].synchronize()
+            if self._pinned[b] is None or self._pinned[b].numel() < raw.numel():
+                self._pinned[b] = torch.empty(raw.numel(), dtype=torch.uint8, pin_memory=True)
+            self._pinned[b][:raw.numel()].copy_(raw)
+            dev = entries[0][0].device
+            if self._dev is None or self._dev.numel() < raw.numel():
+                self._dev = torch.empty(raw.numel(), dtype=torch.uint8, device=dev)
+            self._dev[:raw.numel()].copy_(self._pinned[b][:raw.numel()], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._events[b] = ev
+            self._key, self._chunks, self._nt = key, c0, len(key)
+        N.call("pa_momentum_multi", N.ptr(self._dev), self._nt, self._chunks, float(lr), N.ptr(lr_tensor),
+               float(mu), int(nesterov), float(grad_scale), N.stream())
+
+
 def sumsq(x, out=None):
     """Sum of squares into a 1-element fp32 tensor (accumulates into ``out``)."""
     if out is None:

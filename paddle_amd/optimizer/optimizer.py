@@ -214,6 +214,44 @@ class Momentum(Optimizer):
                  grad_clip=None, multi_precision=False, rescale_grad=1.0, name=None):
         super().__init__(learning_rate, parameters, weight_decay, grad_clip, name, multi_precision)
         self._momentum, self._nesterov, self._rescale = momentum, use_nesterov, rescale_grad
+        self._multi = None
+
+    @staticmethod
+    def _multi_eligible(p):
+        g = p.grad
+        return (p.is_cuda and p.is_contiguous() and p.dtype in (torch.float32, torch.bfloat16) and g is not None
+                and g.is_contiguous() and g.dtype in (torch.float32, torch.bfloat16) and g.shape == p.shape)
+
+    def _step(self):
+        # every parameter in one multi-tensor launch (pa_momentum_multi) when the
+        # update is plain Momentum (+ L2) on device tensors -- merged_momentum
+        import os
+
+        if (self._grad_clip is None and os.environ.get("FLAGS_multi_tensor_momentum", "1") != "0"
+                and all(self._multi_eligible(p) for p in self._parameter_list
+                        if p.grad is not None and p.requires_grad)
+                and all(self._decay_coeff(g, p)[1] != "l1" for g in self._param_groups for p in g["params"])):
+            return self._step_multi()
+        return super()._step()
+
+    def _step_multi(self):
+        self._step_count += 1
+        lr = self.get_lr()
+        entries = []
+        for group in self._param_groups:
+            gl = float(group.get("learning_rate", 1.0))
+            for p in group["params"]:
+                if p.grad is None or not p.requires_grad:
+                    continue
+                coeff, kind = self._decay_coeff(group, p)
+                m = self._master_of(p)
+                vel = self._acc("velocity", p)
+                tgt = m if m is not None else p
+                entries.append((tgt.detach(), p.detach() if m is not None else None, p.grad, vel,
+                                coeff if kind == "l2" else 0.0, gl))
+        if self._multi is None:
+            self._multi = fused_optim.MomentumMulti()
+        self._multi.step(entries, lr=lr, mu=self._momentum, nesterov=self._nesterov, grad_scale=self._rescale)
 
     def _update(self, p, g, lr, group, wd):
         vel = self._acc("velocity", p)

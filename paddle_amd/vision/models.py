@@ -50,6 +50,30 @@ def _bn_relu(bn, x, residual=None):
     return torch.relu(y if residual is None else y + residual)
 
 
+def _conv_direct(conv, x):
+    """The conv layer may be run by conv2d_nhwc directly (NHWC native path, no hooks)."""
+    pad = conv._padding
+    return (isinstance(conv, nn.Conv2D) and conv._data_format == "NHWC" and conv._padding_mode == "zeros"
+            and not conv._forward_pre_hooks and not conv._forward_hooks
+            and (isinstance(pad, int) or (isinstance(pad, (list, tuple)) and len(pad) == 2))
+            and _conv.supported_conv(x, conv.weight, conv._stride, pad, conv._dilation, conv._groups))
+
+
+def _conv_bn_relu(conv, bn, x, residual=None):
+    """relu(bn(conv(x)) [+ residual]).  On the native NHWC path the BatchNorm batch
+    statistics come from the conv's epilogue (64-channel-tile kernel), so the BN
+    forward makes one pass over the conv output instead of two."""
+    if _conv_direct(conv, x) and _fusable(bn, x):
+        rm = bn._mean
+        st = {"shift": rm if (rm is not None and rm.dtype == torch.float32 and rm.is_contiguous()) else None}
+        y = _conv.conv2d_nhwc(x, conv.weight, conv.bias, conv._stride, conv._padding, conv._dilation, stats=st)
+        if residual is None or residual.shape == y.shape:
+            return _conv.batch_norm_nhwc_train(y, bn.weight, bn.bias, bn._mean, bn._variance, bn._momentum,
+                                               bn._epsilon, relu=True, residual=residual, stats=st)
+        return _bn_relu(bn, y, residual)
+    return _bn_relu(bn, conv(x), residual)
+
+
 class BasicBlock(nn.Layer):
     expansion = 1
 
@@ -67,10 +91,10 @@ class BasicBlock(nn.Layer):
 
     def forward(self, x):
         identity = x
-        out = _bn_relu(self.bn1, self.conv1(x))
+        out = _conv_bn_relu(self.conv1, self.bn1, x)
         if self.downsample is not None:
             identity = self.downsample(x)
-        return _bn_relu(self.bn2, self.conv2(out), identity)
+        return _conv_bn_relu(self.conv2, self.bn2, out, identity)
 
 
 class BottleneckBlock(nn.Layer):
@@ -93,11 +117,11 @@ class BottleneckBlock(nn.Layer):
 
     def forward(self, x):
         identity = x
-        out = _bn_relu(self.bn1, self.conv1(x))
-        out = _bn_relu(self.bn2, self.conv2(out))
+        out = _conv_bn_relu(self.conv1, self.bn1, x)
+        out = _conv_bn_relu(self.conv2, self.bn2, out)
         if self.downsample is not None:
             identity = self.downsample(x)
-        return _bn_relu(self.bn3, self.conv3(out), identity)
+        return _conv_bn_relu(self.conv3, self.bn3, out, identity)
 
 
 class ResNet(nn.Layer):

@@ -156,3 +156,97 @@ def test_resnet_native_matches_torch_path():
         cn, ca = cos(n_, r_), cos(a_, r_)
         print(f"grad {i}: cos(native, fp32) = {cn:.4f}  cos(aten bf16, fp32) = {ca:.4f}")
         assert cn >= ca - 0.05, (i, cn, ca)
+
+
+SN_CASES = [
+    # N, H, W, C, Cout, k, stride, pad  (64-channel-tile kernel, csrc/kernels/convsn.hip)
+    (2, 14, 14, 64, 64, 3, 1, 1),
+    (3, 9, 11, 128, 128, 1, 1, 0),
+    (2, 15, 13, 64, 48, 3, 2, 1),
+    (1, 7, 7, 192, 200, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("N,H,W,C,Co,k,s,p", SN_CASES)
+def test_conv_sn_matches_reference_and_emits_bn_stats(N, H, W, C, Co, k, s, p):
+    from paddle_amd.ops import conv
+
+    g = torch.Generator(device=dev).manual_seed(7 * C + Co)
+    x = torch.randn(N, H, W, C, generator=g, device=dev).to(torch.bfloat16)
+    w = (torch.randn(Co, C, k, k, generator=g, device=dev) / (C * k * k) ** 0.5).to(torch.bfloat16)
+    shift = torch.randn(Co, generator=g, device=dev) * 0.1
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float(), None, s, p).permute(0, 2, 3, 1)
+    old = conv._SN_MAX[0]
+    try:
+        conv._SN_MAX[0] = 0
+        yw = conv.conv2d_nhwc(x, w, None, s, p)
+        conv._SN_MAX[0] = 1 << 16
+        st = {"shift": shift}
+        ys = conv.conv2d_nhwc(x, w, None, s, p, stats=st)
+    finally:
+        conv._SN_MAX[0] = old
+    assert _rel(ys, ref) < 1e-2 and _rel(yw, ref) < 1e-2
+    assert st.get("part") is not None
+    G = st["G"]
+    part = st["part"].view(G, 2, Co).double()
+    d = ys.double().reshape(-1, Co) - shift.double()
+    torch.testing.assert_close(part[:, 0].sum(0), d.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(part[:, 1].sum(0), (d * d).sum(0), rtol=1e-4, atol=1e-2)
+
+
+def test_conv_bn_relu_fused_stats_match_unfused():
+    """ResNet bottleneck entry: conv -> BN(+ReLU) with the statistics from the conv
+    epilogue equals the two-pass BN (outputs, running statistics, gradients)."""
+    import paddle_amd as paddle
+    from paddle_amd import nn
+    from paddle_amd.vision import models as VM
+
+    paddle.seed(3)
+    c = nn.Conv2D(64, 64, 3, padding=1, bias_attr=False, data_format="NHWC").to(dev).to(torch.bfloat16)
+    bn = nn.BatchNorm2D(64, data_format="NHWC").to(dev)
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = (torch.randn(4, 16, 16, 64, generator=g, device=dev) + 0.5).to(torch.bfloat16)
+    states = []
+    outs = []
+    for fused in (False, True):
+        bn._mean.zero_()
+        bn._variance.fill_(1.0)
+        for prm in list(c.parameters()) + list(bn.parameters()):
+            prm.grad = None
+        xt = x.clone().requires_grad_()
+        y = VM._conv_bn_relu(c, bn, xt) if fused else VM._bn_relu(bn, c(xt))
+        y.float().pow(2).sum().backward()
+        outs.append((y.detach().float(), xt.grad.float(), c.weight.grad.float(), bn.weight.grad.float()))
+        states.append((bn._mean.clone(), bn._variance.clone()))
+    for a, b in zip(outs[0], outs[1]):
+        assert _rel(b, a) < 2e-2
+    torch.testing.assert_close(states[1][0], states[0][0], rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(states[1][1], states[0][1], rtol=1e-3, atol=1e-4)
+
+
+def test_bottleneck_residual_grad_accumulated_in_dgrad_epilogue():
+    """The block input's gradient = residual branch (BN3 backward's dres) + conv1's
+    dX: with the engine's accumulate-into protocol conv1's dgrad sums onto dres in its
+    epilogue (no add kernel); gradients must equal the plain engine sum."""
+    import paddle_amd as paddle
+    from paddle_amd.autograd import engine as E
+    from paddle_amd.vision.models import BottleneckBlock
+
+    paddle.seed(11)
+    blk = BottleneckBlock(256, 64, data_format="NHWC").to(dev).to(torch.bfloat16)
+    g = torch.Generator(device=dev).manual_seed(2)
+    x0 = torch.randn(4, 14, 14, 256, generator=g, device=dev).to(torch.bfloat16)
+    res = []
+    for on in (False, True):
+        E._ACCUM_INTO[0] = on
+        try:
+            for q in blk.parameters():
+                q.grad = None
+            x = paddle.to_tensor(x0.clone(), stop_gradient=False)
+            y = blk(x)
+            (y.astype("float32") ** 2).sum().backward()
+            res.append((x.grad.float().clone(), blk.conv1.weight.grad.float().clone()))
+        finally:
+            E._ACCUM_INTO[0] = True
+    assert _rel(res[1][0], res[0][0]) < 1e-2
+    assert _rel(res[1][1], res[0][1]) < 1e-2

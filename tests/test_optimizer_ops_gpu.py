@@ -1,6 +1,7 @@
 """The optimizer OpTest table (test_optimizer_ops_cpu.py) on CUDAPlace: dense fp32
 updates run the fused kernels of optimizer.hip / optim_ext.hip."""
 import pytest
+import torch
 
 import paddle_amd.fluid as fluid
 from test_optimizer_ops_cpu import OPT_CASES, run_case
@@ -64,3 +65,34 @@ def test_optimizer_updates_in_place_on_device(opt):
     wc, _ = run(fluid.CPUPlace())
     np.testing.assert_allclose(wg, wc, rtol=1e-4, atol=1e-6)
     assert len(set(ptrs)) == 1, "device optimizer update reallocated the parameter"
+
+
+@pytest.mark.parametrize("nesterov", [False, True])
+def test_momentum_multi_tensor_matches_per_parameter(monkeypatch, nesterov):
+    """One pa_momentum_multi launch over every parameter == the per-parameter path
+    (bf16 params with fp32 masters, fp32 params, L2 decay, a no-decay parameter, a
+    param group with an lr multiplier); the device table is re-used across steps."""
+    import paddle_amd as paddle
+
+    def run(multi):
+        monkeypatch.setenv("FLAGS_multi_tensor_momentum", "1" if multi else "0")
+        g = torch.Generator(device="cuda").manual_seed(0)
+        ps = [torch.nn.Parameter(torch.randn(*s, generator=g, device="cuda").to(dt))
+              for s, dt in [((300, 7), torch.bfloat16), ((5000,), torch.bfloat16), ((64, 3, 3, 3), torch.float32),
+                            ((13,), torch.float32), ((4097,), torch.bfloat16)]]
+        ps[3].no_weight_decay = True
+        opt = paddle.optimizer.Momentum(learning_rate=0.05, momentum=0.9, use_nesterov=nesterov,
+                                        parameters=[{"params": ps[:4]}, {"params": ps[4:], "learning_rate": 0.5}],
+                                        weight_decay=paddle.optimizer.L2Decay(1e-2), multi_precision=True)
+        for it in range(3):
+            for i, p in enumerate(ps):
+                p.grad = (torch.randn(p.shape, generator=g, device="cuda") * (i + 1)).to(
+                    torch.bfloat16 if i % 2 == 0 else torch.float32)
+            opt.step()
+        return [p.detach().float().clone() for p in ps], opt
+
+    ref, _ = run(False)
+    got, opt = run(True)
+    assert opt._multi is not None and opt._multi._nt == 5
+    for a, b in zip(got, ref):
+        torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-3)
