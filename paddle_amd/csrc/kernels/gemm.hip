@@ -81,6 +81,10 @@ struct Params {
   // (dgrad of a stride-2^uy conv) only ny % 2^uy == 0 hits, at row ny >> uy.
   int H, W, Cc, OH, OW, KW, sy, sx, py, px, dy, dx, uy, ux;
   int stagger;  // persistent grids: block slot (bid / 8) % 8 idles slot * stagger * ~0.5 us first
+  // GA (conv) kernels, bf16 out: per-channel BatchNorm statistics of the ROUNDED
+  // output about `shift` (nullable) into part[tile_m][0 / 1][N] (sum, sum of squares)
+  float* part;
+  const float* shift;
 };
 
 // LDS image of one operand of one stage: 4 "slabs" of 64 mn x 64 k (8 KiB each);
@@ -283,6 +287,15 @@ __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
+}
+
+// inclusive prefix sum inside each 16-lane DPP row: lane 16g + 15 ends with the row total
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x112, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x114, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x118, 0xf, 0xf, true));
+  return v;
 }
 
 // Bijective XCD-aware remap: blocks that share an XCD (bid % 8) get a contiguous
@@ -758,6 +771,17 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
     const int crow_ = (rr0_ < GR ? rr0_ : 128 + rr0_ - GR) + GR * (ps);                    \
     (c_colok && c_row + crow_ < rows_left) ? c_base + (unsigned)crow_ * row_bytes : OOB;       \
   })
+  // GA conv kernels with p.part: BatchNorm statistics of the stored (rounded) output,
+  // accumulated from the staged 16-B chunks this thread stores (8 channels, fixed per
+  // thread), then reduced over the 16 threads of a channel chunk through LDS
+  const bool stats = GA && !OUTF32 && p.part != nullptr;
+  float st1[8], st2[8], shc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    st1[e] = st2[e] = 0.f;
+    const int n = n0 + (tid % CPR) * 8 + e;
+    shc[e] = (stats && p.shift && n < p.N) ? p.shift[n] : 0.f;
+  }
 #pragma unroll
   for (int ps = 0; ps < PASSES; ++ps) {
     // (a) fragments -> LDS (staged row = GR * wr + 16 * ii + ml)
@@ -822,6 +846,17 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
         const int rr = it * RPI + tid / CPR, ch = tid % CPR;
         const f32x4 v = *reinterpret_cast<const f32x4*>(stg + rr * ROWB + ch * 16);
         u32x4 w = __builtin_bit_cast(u32x4, v);
+        if constexpr (GA && !OUTF32) {
+          if (stats && C_OFF(it, ps) != OOB) {
+            const u16x8 c = __builtin_bit_cast(u16x8, v);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float d = bf2f(c[e]) - shc[e];
+              st1[e] += d;
+              st2[e] += d * d;
+            }
+          }
+        }
         if (acc_rd) {
           if constexpr (OUTF32) {
             w = __builtin_bit_cast(u32x4, v + __builtin_bit_cast(f32x4, cold[u]));
@@ -838,6 +873,28 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
       }
     }
     __syncthreads();  // staging reads done (next pass / next tile's DMA into stage 1)
+  }
+  if (stats) {
+    float* red = reinterpret_cast<float*>(stg);  // [NT / CPR row groups][256 columns][2]
+    const int rg = tid / CPR, cb = (tid % CPR) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(rg * 256 + cb + e) * 2] = st1[e];
+      red[(rg * 256 + cb + e) * 2 + 1] = st2[e];
+    }
+    __syncthreads();
+    if (tid < 256 && n0 + tid < p.N) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int g = 0; g < NT / CPR; ++g) {
+        a += red[(g * 256 + tid) * 2];
+        b += red[(g * 256 + tid) * 2 + 1];
+      }
+      const long row = (long)(m0 / BM) * 2;
+      p.part[row * p.N + n0 + tid] = a;
+      p.part[(row + 1) * p.N + n0 + tid] = b;
+    }
+    __syncthreads();  // reduction reads done before the next tile's DMA into stage 1
   }
   }
 #undef C_OFF
@@ -1053,10 +1110,26 @@ PA_EXPORT int pa_conv_gemm(const void* src, const void* wt, void* out, const voi
                           st);
 }
 
+PA_EXPORT int pa_conv_gemm_stats(const void* src, const void* wt, void* out, const void* bias, int Nb, int H, int W,
+                                 int C, int OH, int OW, int Cout, int KH, int KW, int sy, int sx, int py, int px,
+                                 int dy, int dx, int uy, int ux, int accumulate, float* part, const float* shift,
+                                 hipStream_t st);
+
 // accumulate: out += conv (bf16 read-modify-write in the epilogue: a gradient summed in place)
 PA_EXPORT int pa_conv_gemm_acc(const void* src, const void* wt, void* out, const void* bias, int Nb, int H, int W,
                                int C, int OH, int OW, int Cout, int KH, int KW, int sy, int sx, int py, int px, int dy,
                                int dx, int uy, int ux, int accumulate, hipStream_t st) {
+  return pa_conv_gemm_stats(src, wt, out, bias, Nb, H, W, C, OH, OW, Cout, KH, KW, sy, sx, py, px, dy, dx, uy, ux,
+                            accumulate, nullptr, nullptr, st);
+}
+
+// part (nullable): BatchNorm statistics of the output, [ceil(M / 256)][2][Cout] about
+// `shift` (nullable, fp32 [Cout]) -- the layout of pa_conv_sn's and bn_finalize's partials
+PA_EXPORT int pa_conv_gemm_stats(const void* src, const void* wt, void* out, const void* bias, int Nb, int H, int W,
+                                 int C, int OH, int OW, int Cout, int KH, int KW, int sy, int sx, int py, int px,
+                                 int dy, int dx, int uy, int ux, int accumulate, float* part, const float* shift,
+                                 hipStream_t st) {
+  if (accumulate && part) return -1;
   const long M = (long)Nb * OH * OW;
   if (M <= 0 || Cout <= 0) return 0;
   if (C % 64 || Cout % 8 || M > 0x7fffffffL || (long)Nb * H * W * C >= 0x7fffffffL || H > 32767 || W > 32767)
@@ -1067,6 +1140,8 @@ PA_EXPORT int pa_conv_gemm_acc(const void* src, const void* wt, void* out, const
   p.lda = C; p.ldb = p.K; p.ldc = Cout;
   p.alpha = 1.f;
   p.accumulate = accumulate;
+  p.part = part;
+  p.shift = shift;
   p.H = H; p.W = W; p.Cc = C; p.OH = OH; p.OW = OW; p.KW = KW;
   p.sy = sy; p.sx = sx; p.py = py; p.px = px; p.dy = dy; p.dx = dx; p.uy = uy; p.ux = ux;
   p.tiles_m = (p.M + gemm::BM - 1) / gemm::BM;

@@ -77,6 +77,7 @@ _SIGS = {
     "pa_conv_sn_tiles": [_L],
     "pa_conv_sn_acc": [_P, _P, _P, _P] + [_I] * 17 + [_P, _P, _I, _P],
     "pa_conv_gemm_acc": [_P, _P, _P, _P] + [_I] * 18 + [_P],
+    "pa_conv_gemm_stats": [_P, _P, _P, _P] + [_I] * 18 + [_P, _P, _P],
     "pa_momentum_multi": [_P, _I, _L, _F, _P, _F, _I, _F, _P],
     "pa_momentum_multi_entry_bytes": [],
     "pa_momentum_multi_chunk": [],

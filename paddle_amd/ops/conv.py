@@ -107,9 +107,18 @@ def _conv_fwd(x, w, b, s, p, d, stats=None):
     if C % 64 == 0:
         wk = wk.contiguous()
         y = torch.empty(N, OH, OW, Cout, dtype=x.dtype, device=x.device)
-        if Cout <= _SN_MAX[0] and _sn(x, wk, y, bias, (N, H, W, C, OH, OW, Cout, KH, KW, s[0], s[1], p[0], p[1],
-                                                       d[0], d[1], 0, 0), stats):
+        geo = (N, H, W, C, OH, OW, Cout, KH, KW, s[0], s[1], p[0], p[1], d[0], d[1], 0, 0)
+        if Cout <= _SN_MAX[0] and _sn(x, wk, y, bias, geo, stats):
             return y
+        if stats is not None:
+            # 256-wide tiles: the same per-tile statistics from the staged epilogue
+            G = int(_nat.lib().pa_conv_sn_tiles(N * OH * OW))
+            part = torch.empty(G * 2 * Cout, dtype=torch.float32, device=x.device)
+            rc = _nat.lib().pa_conv_gemm_stats(_nat.ptr(x), _nat.ptr(wk), _nat.ptr(y), _nat.ptr(bias), *geo, 0,
+                                               _nat.ptr(part), _nat.ptr(stats.get("shift")), _nat.stream())
+            if rc == 0:
+                stats["part"], stats["G"] = part, G
+                return y
         rc = _nat.lib().pa_conv_gemm(_nat.ptr(x), _nat.ptr(wk), _nat.ptr(y), _nat.ptr(bias), N, H, W, C, OH, OW,
                                      Cout, KH, KW, s[0], s[1], p[0], p[1], d[0], d[1], 0, 0, _nat.stream())
         _nat.check(rc, "pa_conv_gemm")

@@ -192,6 +192,18 @@ def test_conv_sn_matches_reference_and_emits_bn_stats(N, H, W, C, Co, k, s, p):
     d = ys.double().reshape(-1, Co) - shift.double()
     torch.testing.assert_close(part[:, 0].sum(0), d.sum(0), rtol=1e-4, atol=1e-2)
     torch.testing.assert_close(part[:, 1].sum(0), (d * d).sum(0), rtol=1e-4, atol=1e-2)
+    # the 256-wide-tile kernel emits the same statistics from its staged epilogue
+    try:
+        conv._SN_MAX[0] = 0
+        st2 = {"shift": shift}
+        yw2 = conv.conv2d_nhwc(x, w, None, s, p, stats=st2)
+    finally:
+        conv._SN_MAX[0] = old
+    assert torch.equal(yw2, yw) and st2.get("part") is not None and st2["G"] == G
+    part2 = st2["part"].view(G, 2, Co).double()
+    d2 = yw2.double().reshape(-1, Co) - shift.double()
+    torch.testing.assert_close(part2[:, 0].sum(0), d2.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(part2[:, 1].sum(0), (d2 * d2).sum(0), rtol=1e-4, atol=1e-2)
 
 
 def test_conv_bn_relu_fused_stats_match_unfused():
