@@ -74,7 +74,7 @@ def main():
         wshape = (Co, C, k, k)
         for mode, key in (("0", "wgrad_wide_us"), ("1", "wgrad_sn_us")):
             _conv._WGRAD_SN[0] = mode
-            rec[key] = timeit(lambda: _conv._conv_wgrad(dyw, x, wshape, (s, s), (p, p), (1, 1)))
+            rec[key] = timeit(lambda: _conv._conv_wgrad(dyw, x, wshape, (s, s), (p, p), (1, 1), torch.bfloat16))
         _conv._WGRAD_SN[0] = "1"
         a = _conv._conv_wgrad(dyw, x, wshape, (s, s), (p, p), (1, 1)).float()
         _conv._WGRAD_SN[0] = "0"

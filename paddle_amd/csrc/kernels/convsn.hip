@@ -535,12 +535,74 @@ static int wgrad_setup(convsn::WgParams& p, const void* dyp, const void* x, int 
   return 0;
 }
 
+// sum of the split partials [S][Cout][(kh, kw, c)] written straight into the weight's
+// own layout [Cout][C][KH][KW] and dtype (fp32 or bf16): no permute / cast pass after
+__global__ void wgrad_reduce_kernel(const float* __restrict__ part, int S, int Cout, int C, int KH, int KW,
+                                    void* __restrict__ out, int out_bf16, int accumulate) {
+  const long K = (long)KH * KW * C, n = (long)Cout * K;
+  for (long o = blockIdx.x * (long)blockDim.x + threadIdx.x; o < n; o += (long)gridDim.x * blockDim.x) {
+    // o indexes [co][c][kh][kw]
+    const int kw = (int)(o % KW);
+    long t = o / KW;
+    const int kh = (int)(t % KH);
+    t /= KH;
+    const int c = (int)(t % C);
+    const long co = t / C;
+    const long src = co * K + ((long)kh * KW + kw) * C + c;
+    float a = 0.f;
+    for (int sp = 0; sp < S; ++sp) a += part[(long)sp * Cout * K + src];
+    if (out_bf16) {
+      u16* y = (u16*)out;
+      y[o] = f2bf(accumulate ? a + bf2f(y[o]) : a);
+    } else {
+      float* y = (float*)out;
+      y[o] = accumulate ? a + y[o] : a;
+    }
+  }
+}
+
 PA_EXPORT long pa_conv_wgrad_sn_ws(int Nb, int H, int W, int C, int OH, int OW, int Cout, int KH, int KW) {
   convsn::WgParams p;
   if (wgrad_setup(p, nullptr, nullptr, Nb, H, W, C, OH, OW, Cout, KH, KW, 1, 1, 0, 0, 1, 1)) return -1;
   int splits, ktps;
   wgrad_plan(p, splits, ktps);
   return splits > 1 ? (long)splits * Cout * p.K : 0;
+}
+
+// workspace floats for pa_conv_wgrad_sn_w (always staged: the reduce writes the layout)
+PA_EXPORT long pa_conv_wgrad_sn_ws2(int Nb, int H, int W, int C, int OH, int OW, int Cout, int KH, int KW) {
+  convsn::WgParams p;
+  if (wgrad_setup(p, nullptr, nullptr, Nb, H, W, C, OH, OW, Cout, KH, KW, 1, 1, 0, 0, 1, 1)) return -1;
+  int splits, ktps;
+  wgrad_plan(p, splits, ktps);
+  return (long)splits * Cout * p.K;
+}
+
+// weight gradient in the PARAMETER's layout [Cout][C][KH][KW] and dtype (w_bf16);
+// ws: pa_conv_wgrad_sn_ws2 floats
+PA_EXPORT int pa_conv_wgrad_sn_w(const void* dyp, const void* x, void* dw, int w_bf16, float* ws, int Nb, int H,
+                                 int W, int C, int OH, int OW, int Cout, int KH, int KW, int sy, int sx, int py,
+                                 int px, int dly, int dlx, int accumulate, hipStream_t st) {
+  convsn::WgParams p;
+  if (wgrad_setup(p, dyp, x, Nb, H, W, C, OH, OW, Cout, KH, KW, sy, sx, py, px, dly, dlx)) return -1;
+  if (!ws) return -2;
+  int splits, ktps;
+  wgrad_plan(p, splits, ktps);
+  p.kt_per_split = ktps;
+  p.part = ws;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)convsn::conv_wgrad_sn_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 2 * convsn::WG_STAGE);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(convsn::conv_wgrad_sn_kernel, dim3(p.tiles_co * p.tiles_n * splits), dim3(convsn::NT),
+                     2 * convsn::WG_STAGE, st, p);
+  const long n = (long)Cout * p.K;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(stream_grid(n, 256)), dim3(256), 0, st, ws, splits, Cout, C,
+                     KH, KW, dw, w_bf16, accumulate);
+  PA_LAUNCH_CHECK();
 }
 
 PA_EXPORT int pa_conv_wgrad_sn(const void* dyp, const void* x, float* dw, float* ws, int Nb, int H, int W, int C,

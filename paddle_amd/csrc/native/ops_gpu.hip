@@ -357,8 +357,13 @@ void k_fc(const OpRun& r) {
     hipLaunchKernelGGL(bias_rows_kernel, dim3(grid_for(M * N)), dim3(256), 0, S(r), c, f32(*b), M, N);
   gemm(S(r), false, false, M, N, K, 1.f, f32(x), K, f32(w), N, b ? 1.f : 0.f, c, N);
   const std::string act = r.op.GetString("activation_type");
-  if (act == "relu") PA_KL(pa_act_fwd(act::RELU, 0, c, c, M * N, 0.f, 0.f, S(r)));
+  int code = -1;
+  if (act == "relu") code = act::RELU;
+  else if (act == "tanh") code = act::TANH;
+  else if (act == "sigmoid") code = act::SIGMOID;
+  else if (act == "gelu") code = act::GELU;
   else if (!act.empty()) fail("fc: activation %s not supported on the device", act.c_str());
+  if (code >= 0) PA_KL(pa_act_fwd(code, 0, c, c, M * N, 0.f, 0.f, S(r)));
 }
 
 void k_matmul(const OpRun& r) {

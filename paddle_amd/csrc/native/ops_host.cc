@@ -5,6 +5,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
+#include <limits>
 #include <numeric>
 
 #include "framework.h"
@@ -107,9 +109,45 @@ void k_shape(const OpRun& r) {
   for (size_t i = 0; i < d.size(); ++i) p[i] = (int32_t)d[i];
 }
 
+// bf16 / fp16 <-> float on the host (round to nearest even; fp16 with subnormals)
+float bf16_to_f(uint16_t h) {
+  uint32_t u = (uint32_t)h << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+uint16_t f_to_bf16(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+float f16_to_f(uint16_t h) {
+  const uint32_t s = (uint32_t)(h & 0x8000) << 16, e = (h >> 10) & 0x1f, m = h & 0x3ff;
+  float v;
+  if (e == 0) v = std::ldexp((float)m, -24);
+  else if (e == 31) v = m ? std::numeric_limits<float>::quiet_NaN() : std::numeric_limits<float>::infinity();
+  else v = std::ldexp((float)(m | 0x400), (int)e - 25);
+  return s ? -v : v;
+}
+uint16_t f_to_f16(float f) {
+  const uint16_t s = std::signbit(f) ? 0x8000 : 0;
+  const float a = std::fabs(f);
+  if (std::isnan(f)) return (uint16_t)(s | 0x7e00);
+  if (a >= 65520.f) return (uint16_t)(s | 0x7c00);
+  if (a < 6.103515625e-05f) return (uint16_t)(s | (uint16_t)std::nearbyint(a * 16777216.f));  // subnormal
+  int e;
+  const float fr = std::frexp(a, &e);  // a = fr * 2^e, fr in [0.5, 1)
+  uint32_t m = (uint32_t)std::nearbyint(fr * 2048.f);  // 11 significant bits
+  if (m == 2048) { m = 1024; ++e; }
+  const uint32_t he = (uint32_t)(e + 14);
+  if (he >= 31) return (uint16_t)(s | 0x7c00);
+  return (uint16_t)(s | (he << 10) | (m & 0x3ff));
+}
+
 void k_cast(const OpRun& r) {
-  Tensor& x = r.in("X");
-  Tensor* o = r.out("Out");
+  // everything read from X before r.out(): creating Out may invalidate the reference
+  const Tensor& x = r.in("X");
   const DT out = (DT)r.op.GetInt("out_dtype", (int)DT::FP32);
   const int64_t n = x.numel();
   std::vector<double> tmp((size_t)n);
@@ -119,10 +157,18 @@ void k_cast(const OpRun& r) {
     case DT::INT64: for (int64_t i = 0; i < n; ++i) tmp[i] = (double)x.data<int64_t>()[i]; break;
     case DT::INT32: for (int64_t i = 0; i < n; ++i) tmp[i] = x.data<int32_t>()[i]; break;
     case DT::BOOL: case DT::UINT8: for (int64_t i = 0; i < n; ++i) tmp[i] = x.data<uint8_t>()[i]; break;
-    default: fail("cast: input dtype %s", dt_name(x.dtype));
+    case DT::BF16: for (int64_t i = 0; i < n; ++i) tmp[i] = bf16_to_f(x.data<uint16_t>()[i]); break;
+    case DT::FP16: for (int64_t i = 0; i < n; ++i) tmp[i] = f16_to_f(x.data<uint16_t>()[i]); break;
+    default: throw Decline{};
   }
-  LoD lod = x.lod;
-  Dims d = x.dims;
+  const LoD lod = x.lod;
+  const Dims d = x.dims;
+  Tensor* o = r.out("Out");
+  switch (out) {
+    case DT::FP32: case DT::FP64: case DT::INT64: case DT::INT32: case DT::BOOL: case DT::UINT8: case DT::BF16:
+    case DT::FP16: break;
+    default: throw Decline{};
+  }
   o->alloc(out, d, -1);
   o->lod = lod;
   switch (out) {
@@ -131,7 +177,9 @@ void k_cast(const OpRun& r) {
     case DT::INT64: for (int64_t i = 0; i < n; ++i) o->data<int64_t>()[i] = (int64_t)tmp[i]; break;
     case DT::INT32: for (int64_t i = 0; i < n; ++i) o->data<int32_t>()[i] = (int32_t)tmp[i]; break;
     case DT::BOOL: case DT::UINT8: for (int64_t i = 0; i < n; ++i) o->data<uint8_t>()[i] = tmp[i] != 0; break;
-    default: fail("cast: output dtype %s", dt_name(out));
+    case DT::BF16: for (int64_t i = 0; i < n; ++i) o->data<uint16_t>()[i] = f_to_bf16((float)tmp[i]); break;
+    case DT::FP16: for (int64_t i = 0; i < n; ++i) o->data<uint16_t>()[i] = f_to_f16((float)tmp[i]); break;
+    default: break;
   }
 }
 
@@ -220,6 +268,14 @@ void k_fc(const OpRun& r) {
   const std::string act = r.op.GetString("activation_type");
   if (act == "relu")
     for (int64_t i = 0; i < M * N; ++i) c[i] = c[i] > 0 ? c[i] : 0;
+  else if (act == "tanh")
+    for (int64_t i = 0; i < M * N; ++i) c[i] = tanhf(c[i]);
+  else if (act == "sigmoid")
+    for (int64_t i = 0; i < M * N; ++i) c[i] = 1.f / (1.f + expf(-c[i]));
+  else if (act == "gelu")
+    for (int64_t i = 0; i < M * N; ++i) c[i] = 0.5f * c[i] * (1.f + erff(c[i] * 0.70710678f));
+  else if (!act.empty())
+    throw Decline{};
 }
 
 // ------------------------------------------------------------ elementwise (elementwise_op_function.h)
@@ -1220,13 +1276,29 @@ void k_batch_norm_grad(const OpRun& r) {
 }
 
 void k_fill_zeros_like(const OpRun& r) {
-  Tensor& x = r.in("X");
-  Dims d = x.dims;
+  // read X's shape and dtype before r.out(): creating the output variable may
+  // rehash the scope and invalidate the reference r.in() returned
+  const Tensor& x = r.in("X");
+  const Dims d = x.dims;
+  const DT dt = x.dtype;
   Tensor* o = r.out("Out");
-  memset(o->alloc(x.dtype, d, -1), 0, o->nbytes());
+  memset(o->alloc(dt, d, -1), 0, o->nbytes());
 }
 
 // ------------------------------------------------------------ optimizers (sgd_op.h, momentum_op.h, adam_op.h)
+// the update target of `in_slot` -> `out_slot`: in place, or a copy of the input
+float* opt_target(const OpRun& r, const char* in_slot, const char* out_slot) {
+  Tensor& in = r.in(in_slot);
+  if (r.op.Output(out_slot) == r.op.Input(in_slot)) return f32(in);
+  const Dims d = in.dims;
+  const float* src = f32(in);
+  const size_t bytes = in.nbytes();
+  Tensor keep = in;  // holds the source buffer while the output is allocated
+  float* dst = r.out(out_slot)->alloc<float>(d, -1);
+  memcpy(dst, src, bytes);
+  return dst;
+}
+
 void k_sgd(const OpRun& r) {
   Tensor& p = r.in("Param");
   Tensor& g = r.in("Grad");
@@ -1262,15 +1334,17 @@ void k_adam(const OpRun& r) {
   Tensor& p = r.in("Param");
   Tensor& g = r.in("Grad");
   const float lr = f32(r.in("LearningRate"))[0];
-  float* m1 = f32(r.in("Moment1"));
-  float* m2 = f32(r.in("Moment2"));
   const float b1p = f32(r.in("Beta1Pow"))[0], b2p = f32(r.in("Beta2Pow"))[0];
   const float b1 = r.op.GetFloat("beta1", 0.9f), b2 = r.op.GetFloat("beta2", 0.999f),
               eps = r.op.GetFloat("epsilon", 1e-8f);
-  float* w = f32(p);
   const float* gp = f32(g);
+  Tensor gkeep = g;
+  (void)p;
+  float* w = opt_target(r, "Param", "ParamOut");  // out-of-place outputs (op tests) start as copies
+  float* m1 = opt_target(r, "Moment1", "Moment1Out");
+  float* m2 = opt_target(r, "Moment2", "Moment2Out");
   const float lr_t = lr * sqrtf(1 - b2p) / (1 - b1p);
-  for (int64_t i = 0; i < p.numel(); ++i) {
+  for (int64_t i = 0; i < gkeep.numel(); ++i) {
     m1[i] = b1 * m1[i] + (1 - b1) * gp[i];
     m2[i] = b2 * m2[i] + (1 - b2) * gp[i] * gp[i];
     w[i] -= lr_t * m1[i] / (sqrtf(m2[i]) + eps);

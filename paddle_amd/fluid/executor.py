@@ -12,7 +12,11 @@ replacement for launch-bound inner loops; see also ``FLAGS_use_hip_graph``).
 
 ``Executor(place, engine="native")`` (or ``FLAGS_executor_engine=native``) runs
 programs on the C++ executor instead (:mod:`paddle_amd.fluid.native_engine`);
-programs it cannot take (sub-blocks, LoD feeds, ops without a C++ kernel) raise.
+programs it cannot take (sub-blocks needing step scopes, non-LoDTensor variables)
+raise.  ``engine="auto"`` runs every program the C++ executor can take on it (ops
+without a C++ kernel run their Python kernel per op) and the rest -- and runs
+that need the interpreter's per-op hooks (profiler, NaN/Inf checks, VLOG op
+traces, HIP-graph capture, py_reader feeds) -- on the interpreter.
 """
 from __future__ import annotations
 
@@ -71,9 +75,10 @@ class Executor:
         self.place = place or core.CPUPlace()
         self._core = BlockExecutor(self.place)
         self.engine = engine or FLAGS.get("executor_engine") or "python"
-        if self.engine not in ("python", "native"):
+        if self.engine not in ("python", "native", "auto"):
             raise ValueError(f"unknown executor engine {self.engine!r}")
         self._native = None
+        self._auto = {}  # (id(program), version) -> (program, takes native)
         self._closed = False
         self._prog_cache = {}
         self.use_hip_graph = FLAGS.get("use_hip_graph") if use_hip_graph is None else use_hip_graph
@@ -141,7 +146,8 @@ class Executor:
                     feed.update(r.next_feed())
         fetch_names = [v.name if isinstance(v, Variable) else str(v) for v in fetch_list]
         feed_names = list(feed.keys())
-        if self.engine == "native" and program.global_block().ops:
+        if self.engine != "python" and program.global_block().ops and (
+                self.engine == "native" or self._auto_native(program, feed, readers)):
             if self._native is None:
                 from .native_engine import NativeEngine
 
@@ -166,6 +172,31 @@ class Executor:
         if return_numpy:
             return [as_numpy(o) for o in outs]
         return outs
+
+    def _auto_native(self, program, feed, readers):
+        """engine="auto": does this run go to the C++ executor?"""
+        from .. import platform as _platform
+        from ..utils import profiler as _prof
+
+        if (readers or self.use_hip_graph or FLAGS.get("check_nan_inf") or _prof.is_enabled()
+                or _platform.vlog_level() >= 1):
+            return False
+        key = (id(program), program._version)
+        ent = self._auto.get(key)
+        if ent is None or ent[0] is not program:
+            from .native_engine import NativeEngine
+
+            ent = (program, NativeEngine.can_run(program, self.place))
+            self._auto[key] = ent
+        if not ent[1]:
+            return False
+        for v in feed.values():
+            t = v._t if isinstance(v, core.LoDTensor) else v
+            dt = getattr(t, "dtype", None)
+            if dt is not None and str(dt).replace("torch.", "") not in (
+                    "float32", "float64", "int32", "int64", "float16", "bfloat16", "uint8", "int8", "bool"):
+                return False
+        return True
 
     def _run_block(self, program, block_idx, scope):
         self._core.run_block(program, block_idx, scope)

@@ -159,6 +159,41 @@ class NativeEngine:
         self.py_fallback_types = set()
 
     # ------------------------------------------------------------------ program
+    _VAR_OK = None
+
+    @staticmethod
+    def can_run(program, place):
+        """Can the C++ executor take ``program`` (engine="auto")?  No control flow
+        needing per-step scopes, every variable a dense LoDTensor (or the feed / fetch
+        holders), the pybind binding available when some op has no C++ kernel."""
+        VT = core.VT
+        ok_types = {VT.LOD_TENSOR, VT.FEED_MINIBATCH, VT.FETCH_LIST}
+        try:
+            native.lib()
+        except Exception:
+            return False
+        all_ops = [op for b in program.blocks for op in b.ops]
+        for op in all_ops:
+            if op.type in _UNSUPPORTED_CF or (any(k in op.attrs for k in ("sub_block", "blocks"))
+                                              and op.type not in _NATIVE_CF):
+                return False
+        for b in program.blocks:
+            for v in b.vars.values():
+                if v.type not in ok_types:
+                    return False
+                # fp64 programs (gradient checks) stay on the interpreter: the C++
+                # host kernels are fp32 / integer / bool
+                if v.type == VT.LOD_TENSOR and getattr(v, "dtype", None) == VT.FP64:
+                    return False
+        dev = isinstance(place, core.CUDAPlace)
+        kern = set(native.registered_ops(False)) | (set(native.registered_ops(True)) if dev else set())
+        if any(op.type not in kern and op.type not in _NATIVE_CF for op in all_ops):
+            from .. import core_ext
+
+            if os.environ.get("FLAGS_native_binding", "") == "ctypes" or core_ext.module() is None:
+                return False
+        return True
+
     def _program(self, program):
         key = (id(program), program._version)
         ent = self._progs.get(key)

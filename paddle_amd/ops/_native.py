@@ -83,6 +83,8 @@ _SIGS = {
     "pa_momentum_multi_chunk": [],
     "pa_conv_wgrad_sn_ws": [_I] * 9,
     "pa_conv_wgrad_sn": [_P, _P, _P, _P] + [_I] * 16 + [_P],
+    "pa_conv_wgrad_sn_ws2": [_I] * 9,
+    "pa_conv_wgrad_sn_w": [_P, _P, _P, _I, _P] + [_I] * 16 + [_P],
     "pa_bn_fwd_stats": [_P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _L, _I, _F, _F, _I, _P, _P],
     "pa_im2col_nhwc": [_P, _P] + [_I] * 15 + [_P],
     "pa_bn_blocks": [_L, _I],
@@ -238,8 +240,16 @@ def available() -> bool:
         return False
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_GET_DEVICE = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def stream():
-    return _P(torch.cuda.current_stream().cuda_stream)
+    """torch's current HIP stream of the current device, as a raw handle (the C
+    accessor: no Stream object per call -- this runs once per kernel launch)."""
+    if _RAW_STREAM is not None and _GET_DEVICE is not None:
+        return _RAW_STREAM(_GET_DEVICE())
+    return torch.cuda.current_stream().cuda_stream
 
 
 def ptr(t):

@@ -237,7 +237,31 @@ _BIN = {"add": "add", "sub": "sub", "mul": "mul", "div": "div", "maximum": "maxi
 _CMP = {"eq", "ne", "lt", "le", "gt", "ge", "logical_and", "logical_or", "logical_xor"}
 
 
+_FAST_BIN = {"add.Tensor": (0, False), "sub.Tensor": (1, False), "mul.Tensor": (2, False),
+             "add_.Tensor": (0, True), "sub_.Tensor": (1, True), "mul_.Tensor": (2, True)}
+_FAST_DT = None
+
+
 def _binary(name, self, other, alpha=1, rounding_mode=None, out=None):
+    # hot path: same-shape, same-dtype, contiguous fp32 / bf16 device tensors (the
+    # residual adds, gradient sums and scalings of a training step) -- metadata
+    # checks only, one flat launch
+    fb = _FAST_BIN.get(name)
+    if fb is not None and out is None and isinstance(other, torch.Tensor):
+        global _FAST_DT
+        if _FAST_DT is None:
+            _FAST_DT = {torch.float32: _DT[torch.float32], torch.bfloat16: _DT[torch.bfloat16]}
+        dt = self.dtype
+        code = _FAST_DT.get(dt)
+        if (code is not None and other.dtype is dt and self.is_cuda and other.is_cuda and self.dim() > 0
+                and self.shape == other.shape and self.is_contiguous() and other.is_contiguous()
+                and isinstance(alpha, (int, float))):
+            dst = self if fb[1] else torch.empty_like(self)
+            op = _FAST_OPS[fb[0]]
+            rc = _lib().pa_ew_flat(op, 0, 2, dst.numel(), dst.data_ptr(), code, self.data_ptr(), code,
+                                   other.data_ptr(), code, None, 0, float(alpha), 0.0, N.stream())
+            N.check(rc, "pa_ew_flat")
+            return dst
     base, ovl = name.split(".")
     inplace = base.endswith("_")
     base = base.rstrip("_")
@@ -323,6 +347,9 @@ def _unary_out(x, op, shape, odt, inplace, out, a=0.0, b=0.0, cdt=None):
     _need(_launch(op, dst, [x], a=a, b=b, cdt=cdt))
     return dst
 
+
+_FAST_OPS = (B["add"], B["sub"], B["mul"])
+_FAST_CODE = {torch.float32: _DT[torch.float32], torch.bfloat16: _DT[torch.bfloat16]}
 
 for _n in _BIN:
     for _s in ("Tensor", "Scalar", "out", "Tensor_Tensor", "Tensor_Scalar", "Tensor_mode", "Scalar_mode",
@@ -545,6 +572,14 @@ def _masked_fill(name, self, mask, value):
 # ---------------------------------------------------------------------------- copies, casts, fills
 @_h("copy_.default")
 def _copy(name, self, src, non_blocking=False):
+    # hot path: contiguous same-shape fp32 / bf16 device copy or cast
+    if isinstance(src, torch.Tensor) and src.is_cuda and self.is_cuda and self.shape == src.shape:
+        dc, sc = _FAST_CODE.get(self.dtype), _FAST_CODE.get(src.dtype)
+        if dc is not None and sc is not None and self.is_contiguous() and src.is_contiguous() and self.dim() > 0:
+            rc = _lib().pa_ew_flat(U["copy"], 0, 1, self.numel(), self.data_ptr(), dc, src.data_ptr(), sc, None, 0,
+                                   None, 0, 0.0, 0.0, N.stream())
+            N.check(rc, "pa_ew_flat")
+            return self
     _need(_ok(self) and isinstance(src, torch.Tensor))
     if src.device.type != "cuda":
         raise _Skip()  # host -> device transfer: a DMA copy, not a kernel
@@ -557,6 +592,16 @@ def _copy(name, self, src, non_blocking=False):
 @_h("_to_copy.default")
 def _to_copy(name, self, dtype=None, layout=None, device=None, pin_memory=None, non_blocking=False,
              memory_format=None):
+    if (device is None and memory_format in (None, torch.preserve_format) and self.is_cuda and self.dim() > 0
+            and self.is_contiguous()):
+        dt = dtype or self.dtype
+        dc, sc = _FAST_CODE.get(dt), _FAST_CODE.get(self.dtype)
+        if dc is not None and sc is not None:  # hot path: contiguous fp32 <-> bf16 cast / copy
+            dst = torch.empty(self.shape, dtype=dt, device=self.device)
+            rc = _lib().pa_ew_flat(U["copy"], 0, 1, dst.numel(), dst.data_ptr(), dc, self.data_ptr(), sc, None, 0,
+                                   None, 0, 0.0, 0.0, N.stream())
+            N.check(rc, "pa_ew_flat")
+            return dst
     _need(_ok(self))
     if device is not None and torch.device(device).type != "cuda":
         raise _Skip()
@@ -656,6 +701,20 @@ def _flip(name, self, dims):
                       _LA(*sts[0]), base, _DT[self.dtype], _LA(*sts[1]), None, 0, _LA(*([0] * _ND)), None, 0,
                       _LA(*([0] * _ND)), 0.0, 0.0, N.stream())
     N.check(rc, "pa_ew(flip)")
+    return dst
+
+
+def strided_copy(dst, src_base, src_dtype, src_strides):
+    """dst (contiguous) <- a raw source view at ``src_base`` with element strides
+    ``src_strides`` over dst's shape (negative strides allowed: flips / reversed
+    taps that a torch view cannot express).  One launch of the strided copy kernel."""
+    shp, sts = _coalesce(list(dst.shape), [list(dst.stride()), list(src_strides)])
+    if len(shp) > _ND:
+        raise RuntimeError("strided_copy: too many dimensions")
+    rc = _lib().pa_ew(U["copy"], _cdt(src_dtype), 1, len(shp), _LA(*shp), dst.data_ptr(), _DT[dst.dtype],
+                      _LA(*sts[0]), src_base, _DT[src_dtype], _LA(*sts[1]), None, 0, _LA(*([0] * _ND)), None, 0,
+                      _LA(*([0] * _ND)), 0.0, 0.0, N.stream())
+    N.check(rc, "pa_ew(strided_copy)")
     return dst
 
 

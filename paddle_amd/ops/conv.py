@@ -131,6 +131,21 @@ def _conv_fwd(x, w, b, s, p, d, stats=None):
     return y.view(N, OH, OW, Cout)
 
 
+def _dgrad_weight(w, dt):
+    """wd[c][(kh, kw, co)] = w[co][c][KH-1-kh][KW-1-kw] in ONE strided copy (transpose
+    and tap flip as negative strides of the source), cast to ``dt``."""
+    Cout, C, KH, KW = w.shape
+    if w.dtype not in (torch.float32, torch.bfloat16) or dt not in (torch.float32, torch.bfloat16):
+        return w.to(dt).flip(2, 3).permute(1, 2, 3, 0).reshape(C, KH * KW * Cout).contiguous()
+    from . import aten_native as _an
+
+    s0, s1, s2, s3 = w.stride()
+    out = torch.empty(C, KH, KW, Cout, dtype=dt, device=w.device)
+    base = w.data_ptr() + ((KH - 1) * s2 + (KW - 1) * s3) * w.element_size()
+    _an.strided_copy(out, base, w.dtype, [s1, -s2, -s3, s0])
+    return out.view(C, KH * KW * Cout)
+
+
 def _conv_dgrad(dy, w, x_shape, s, p, d, into=None):
     """dX of the convolution.  ``into``: an exclusively owned gradient of x already
     summed by the engine (e.g. the residual branch's): dX is accumulated into it in
@@ -140,7 +155,7 @@ def _conv_dgrad(dy, w, x_shape, s, p, d, into=None):
     OH, OW = dy.shape[1], dy.shape[2]
     if Cout % 64 == 0 and C % 8 == 0:
         # dX = conv(zero-inserted dY, flipped W^T): wd[c][kh][kw][co] = w[co][c][KH-1-kh][KW-1-kw]
-        wd = w.to(dy.dtype).flip(2, 3).permute(1, 2, 3, 0).reshape(C, KH * KW * Cout).contiguous()
+        wd = _dgrad_weight(w, dy.dtype)
         acc = (into is not None and into.shape == (N, H, W, C) and into.dtype == dy.dtype and into.is_contiguous())
         dx = into if acc else torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
         pyy, pxx = d[0] * (KH - 1) - p[0], d[1] * (KW - 1) - p[1]
@@ -159,7 +174,8 @@ def _conv_dgrad(dy, w, x_shape, s, p, d, into=None):
 
 
 # weight gradient on the gathered 64x256-tile kernel (convsn.hip): "auto" = when the
-# wide path would need an im2col buffer (k > 1 or strided) or Cout <= 128
+# wide path would need an im2col buffer (k > 1 or strided); measured per ResNet-50
+# shape in profiles/r4_conv_sn_probe.jsonl (1x1 stride-1 stays on the split-K GEMM)
 _WGRAD_SN = [os.environ.get("FLAGS_conv_wgrad_sn", "auto")]
 
 
@@ -167,25 +183,27 @@ def _wgrad_sn_wanted(C, Cout, KH, KW, s):
     m = _WGRAD_SN[0]
     if m == "0" or C % 64 or Cout % 8:
         return False
-    return m == "1" or KH * KW > 1 or s != (1, 1) or Cout <= 128
+    return m == "1" or KH * KW > 1 or s != (1, 1)
 
 
-def _conv_wgrad(dy, x, w_shape, s, p, d):
+def _conv_wgrad(dy, x, w_shape, s, p, d, wdtype=torch.float32):
+    """dW in the parameter's layout [Cout, C, KH, KW] (contiguous) and dtype."""
     N, H, W, C = x.shape
     Cout, _, KH, KW = w_shape
     OH, OW = dy.shape[1], dy.shape[2]
     M = N * OH * OW
     K = KH * KW * C
-    if _wgrad_sn_wanted(C, Cout, KH, KW, s):
+    if _wgrad_sn_wanted(C, Cout, KH, KW, s) and wdtype in (torch.float32, torch.bfloat16):
         L = _nat.lib()
-        nws = int(L.pa_conv_wgrad_sn_ws(N, H, W, C, OH, OW, Cout, KH, KW))
-        if nws >= 0:
-            ws = torch.empty(max(nws, 1), dtype=torch.float32, device=x.device) if nws > 0 else None
-            dwk = torch.empty(Cout, K, dtype=torch.float32, device=x.device)
-            rc = L.pa_conv_wgrad_sn(_nat.ptr(dy), _nat.ptr(x), _nat.ptr(dwk), _nat.ptr(ws), N, H, W, C, OH, OW, Cout,
-                                    KH, KW, s[0], s[1], p[0], p[1], d[0], d[1], 0, _nat.stream())
+        nws = int(L.pa_conv_wgrad_sn_ws2(N, H, W, C, OH, OW, Cout, KH, KW))
+        if nws > 0:
+            ws = torch.empty(nws, dtype=torch.float32, device=x.device)
+            dw = torch.empty(Cout, C, KH, KW, dtype=wdtype, device=x.device)
+            rc = L.pa_conv_wgrad_sn_w(_nat.ptr(dy), _nat.ptr(x), _nat.ptr(dw), int(wdtype == torch.bfloat16),
+                                      _nat.ptr(ws), N, H, W, C, OH, OW, Cout, KH, KW, s[0], s[1], p[0], p[1], d[0],
+                                      d[1], 0, _nat.stream())
             if rc == 0:
-                return dwk.reshape(Cout, KH, KW, C).permute(0, 3, 1, 2)
+                return dw
     if KH == 1 and KW == 1 and s == (1, 1) and p == (0, 0) and C % 8 == 0:
         col, Kp = x.reshape(M, C), C
     else:
@@ -195,7 +213,12 @@ def _conv_wgrad(dy, x, w_shape, s, p, d):
     # dW[co][k] = sum_m dY[m][co] col[m][k]: both operands stored [m][..] (MN-major);
     # few output tiles, very deep reduction -> split-K across the chip
     _G.gemm_splitk(dy.reshape(M, Cout), col, Cout, Kp, M, a_kmaj=False, b_kmaj=False, out=dwk)
-    return dwk[:, :K].reshape(Cout, KH, KW, C).permute(0, 3, 1, 2)
+    src = dwk[:, :K].reshape(Cout, KH, KW, C).permute(0, 3, 1, 2)
+    if KH == 1 and KW == 1 and wdtype == torch.float32:
+        return src.reshape(Cout, C, 1, 1)  # already the parameter layout
+    out = torch.empty(Cout, C, KH, KW, dtype=wdtype, device=x.device)
+    out.copy_(src)  # one pass: layout + cast
+    return out
 
 
 class _Conv2dNHWC(torch.autograd.Function):
@@ -216,7 +239,7 @@ class _Conv2dNHWC(torch.autograd.Function):
         dx = _conv_dgrad(dy, w, tuple(x.shape), s, p, d, into) if ctx.needs_input_grad[0] else None
         if dx is not None:
             dx._pa_acc_ok = True  # exclusively owned: later producers may accumulate into it
-        dw = _conv_wgrad(dy, x, tuple(w.shape), s, p, d).to(w.dtype) if ctx.needs_input_grad[1] else None
+        dw = _conv_wgrad(dy, x, tuple(w.shape), s, p, d, w.dtype) if ctx.needs_input_grad[1] else None
         db = dy.reshape(-1, dy.shape[-1]).float().sum(0).to(w.dtype) if has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db, None, None, None, None
 

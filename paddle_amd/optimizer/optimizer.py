@@ -220,7 +220,7 @@ class Momentum(Optimizer):
     def _multi_eligible(p):
         g = p.grad
         return (p.is_cuda and p.is_contiguous() and p.dtype in (torch.float32, torch.bfloat16) and g is not None
-                and g.is_contiguous() and g.dtype in (torch.float32, torch.bfloat16) and g.shape == p.shape)
+                and g.dtype in (torch.float32, torch.bfloat16) and g.shape == p.shape)
 
     def _step(self):
         # every parameter in one multi-tensor launch (pa_momentum_multi) when the
@@ -247,7 +247,8 @@ class Momentum(Optimizer):
                 m = self._master_of(p)
                 vel = self._acc("velocity", p)
                 tgt = m if m is not None else p
-                entries.append((tgt.detach(), p.detach() if m is not None else None, p.grad, vel,
+                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                entries.append((tgt.detach(), p.detach() if m is not None else None, g, vel,
                                 coeff if kind == "l2" else 0.0, gl))
         if self._multi is None:
             self._multi = fused_optim.MomentumMulti()

@@ -59,19 +59,30 @@ def _conv_direct(conv, x):
             and _conv.supported_conv(x, conv.weight, conv._stride, pad, conv._dilation, conv._groups))
 
 
-def _conv_bn_relu(conv, bn, x, residual=None):
-    """relu(bn(conv(x)) [+ residual]).  On the native NHWC path the BatchNorm batch
-    statistics come from the conv's epilogue (64-channel-tile kernel), so the BN
-    forward makes one pass over the conv output instead of two."""
+def _conv_bn_relu(conv, bn, x, residual=None, relu=True):
+    """relu(bn(conv(x)) [+ residual]) (``relu=False``: bn(conv(x))).  On the native
+    NHWC path the BatchNorm batch statistics come from the conv's epilogue, so the
+    BN forward makes one pass over the conv output instead of two."""
     if _conv_direct(conv, x) and _fusable(bn, x):
         rm = bn._mean
         st = {"shift": rm if (rm is not None and rm.dtype == torch.float32 and rm.is_contiguous()) else None}
         y = _conv.conv2d_nhwc(x, conv.weight, conv.bias, conv._stride, conv._padding, conv._dilation, stats=st)
         if residual is None or residual.shape == y.shape:
             return _conv.batch_norm_nhwc_train(y, bn.weight, bn.bias, bn._mean, bn._variance, bn._momentum,
-                                               bn._epsilon, relu=True, residual=residual, stats=st)
-        return _bn_relu(bn, y, residual)
+                                               bn._epsilon, relu=relu, residual=residual, stats=st)
+        return _bn_relu(bn, y, residual) if relu else bn(y)
+    if not relu:
+        return bn(conv(x))
     return _bn_relu(bn, conv(x), residual)
+
+
+def _downsample(ds, x):
+    """The projection shortcut: Sequential(conv, bn) through the conv-statistics path."""
+    mods = list(ds.children()) if isinstance(ds, nn.Sequential) else None
+    if (mods is not None and len(mods) == 2 and isinstance(mods[1], nn.layer_bn_types())
+            and not ds._forward_pre_hooks and not ds._forward_hooks):
+        return _conv_bn_relu(mods[0], mods[1], x, relu=False)
+    return ds(x)
 
 
 class BasicBlock(nn.Layer):
@@ -93,7 +104,7 @@ class BasicBlock(nn.Layer):
         identity = x
         out = _conv_bn_relu(self.conv1, self.bn1, x)
         if self.downsample is not None:
-            identity = self.downsample(x)
+            identity = _downsample(self.downsample, x)
         return _conv_bn_relu(self.conv2, self.bn2, out, identity)
 
 
@@ -120,7 +131,7 @@ class BottleneckBlock(nn.Layer):
         out = _conv_bn_relu(self.conv1, self.bn1, x)
         out = _conv_bn_relu(self.conv2, self.bn2, out)
         if self.downsample is not None:
-            identity = self.downsample(x)
+            identity = _downsample(self.downsample, x)
         return _conv_bn_relu(self.conv3, self.bn3, out, identity)
 
 

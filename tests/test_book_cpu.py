@@ -67,7 +67,7 @@ def _train_digits(net, place, epochs=3, tmpdir=None):
 
 
 def test_recognize_digits_mlp(tmp_path):
-    first, last, acc = _train_digits(mlp, fluid.CPUPlace(), tmpdir=str(tmp_path / "mlp"))
+    first, last, acc = _train_digits(mlp, fluid.CPUPlace(), epochs=5, tmpdir=str(tmp_path / "mlp"))
     assert last < first and acc > 0.2
 
 

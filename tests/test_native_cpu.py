@@ -141,7 +141,7 @@ def test_native_executor_trains_like_python_executor(tmp_path):
     scope = fluid.core.Scope()
     with fluid.executor.scope_guard(scope):
         exe.run(startup)
-        init = {v.name: np.asarray(scope.find_var(v.name).get_tensor().numpy())
+        init = {v.name: np.array(scope.find_var(v.name).get_tensor().numpy(), copy=True)
                 for v in main.list_vars() if v.persistable and scope.find_var(v.name) is not None
                 and v.name not in ("feed", "fetch")}
         ref = [float(np.asarray(exe.run(main, feed={"x": xs, "lab": ls}, fetch_list=[loss])[0]).reshape(-1)[0])

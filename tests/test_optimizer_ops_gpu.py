@@ -86,8 +86,7 @@ def test_momentum_multi_tensor_matches_per_parameter(monkeypatch, nesterov):
                                         weight_decay=paddle.optimizer.L2Decay(1e-2), multi_precision=True)
         for it in range(3):
             for i, p in enumerate(ps):
-                p.grad = (torch.randn(p.shape, generator=g, device="cuda") * (i + 1)).to(
-                    torch.bfloat16 if i % 2 == 0 else torch.float32)
+                p.grad = (torch.randn(p.shape, generator=g, device="cuda") * (i + 1)).to(p.dtype)
             opt.step()
         return [p.detach().float().clone() for p in ps], opt
 
