@@ -1282,7 +1282,8 @@ void k_fill_zeros_like(const OpRun& r) {
   const Dims d = x.dims;
   const DT dt = x.dtype;
   Tensor* o = r.out("Out");
-  memset(o->alloc(dt, d, -1), 0, o->nbytes());
+  void* dst = o->alloc(dt, d, -1);  // (not inside memset's argument list: o->nbytes() must see the new dims)
+  memset(dst, 0, o->nbytes());
 }
 
 // ------------------------------------------------------------ optimizers (sgd_op.h, momentum_op.h, adam_op.h)
@@ -1307,7 +1308,8 @@ void k_sgd(const OpRun& r) {
   if (po->raw() != p.raw()) {
     Dims d = p.dims;
     Tensor src = p;
-    memcpy(po->alloc<float>(d, -1), src.raw(), src.nbytes());
+    float* dst = po->alloc<float>(d, -1);
+    memcpy(dst, src.raw(), src.nbytes());
   }
   float* w = f32(*po);
   const float* gp = f32(g);

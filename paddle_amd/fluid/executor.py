@@ -10,8 +10,10 @@ and fetches results (the only host sync).
 of a static-shape program into a HIP graph and replays it (MI355X-first
 replacement for launch-bound inner loops; see also ``FLAGS_use_hip_graph``).
 
-``Executor(place, engine="native")`` (or ``FLAGS_executor_engine=native``) runs
-programs on the C++ executor instead (:mod:`paddle_amd.fluid.native_engine`);
+The default engine is ``"auto"`` (``FLAGS_executor_engine``): the C++ executor of
+``csrc/native`` (:mod:`paddle_amd.fluid.native_engine`, reference
+framework/executor.cc:125-353) for every program it can take.
+``Executor(place, engine="native")`` forces the C++ executor;
 programs it cannot take (sub-blocks needing step scopes, non-LoDTensor variables)
 raise.  ``engine="auto"`` runs every program the C++ executor can take on it (ops
 without a C++ kernel run their Python kernel per op) and the rest -- and runs

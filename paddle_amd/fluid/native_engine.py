@@ -54,6 +54,11 @@ _UNSUPPORTED_CF = {"while_grad", "conditional_block_grad", "recurrent", "recurre
                    "parallel_do_grad", "go", "select"}
 
 
+_RPC_OPS = {"send", "recv", "prefetch", "listen_and_serv", "send_barrier", "fetch_barrier", "checkpoint_notify",
+            "split_selected_rows", "merge_selected_rows", "split_ids", "merge_ids", "lookup_sparse_table",
+            "get_tensor_from_selected_rows", "gen_nccl_id"}
+
+
 class _CtypesBinding:
     """The C ABI path (paddle_amd.native)."""
 
@@ -176,6 +181,10 @@ class NativeEngine:
         for op in all_ops:
             if op.type in _UNSUPPORTED_CF or (any(k in op.attrs for k in ("sub_block", "blocks"))
                                               and op.type not in _NATIVE_CF):
+                return False
+            # SelectedRows at run time (sparse embedding grads) and the RPC ops that
+            # exchange them stay on the interpreter
+            if op.attrs.get("is_sparse") or op.attrs.get("is_distributed") or op.type in _RPC_OPS:
                 return False
         for b in program.blocks:
             for v in b.vars.values():

@@ -33,7 +33,7 @@ _DEFAULTS = {
     "allocator_strategy": "torch_caching",  # or "buddy" (native C++ buddy allocator)
     "use_hip_graph": False,
     "rccl_bucket_mb": 256,
-    "executor_engine": "python",  # fluid.Executor engine: "python" (op interpreter) or "native" (C++ executor)
+    "executor_engine": "auto",  # fluid.Executor engine: "auto" (C++ executor for every program it can take), "python" (op interpreter) or "native"
 }
 
 _values = {}

@@ -83,3 +83,43 @@ def test_native_engine_rejects_step_scope_programs():
         if any(op.type == "while_grad" for b in main.blocks for op in b.ops):
             with pytest.raises(NotImplementedError, match="while_grad"):
                 exe.run(main, feed={"x": np.zeros((1, 4), "float32")}, fetch_list=[loss])
+
+
+def test_auto_engine_takes_plain_programs_and_leaves_step_scope_programs():
+    """engine="auto" (the default): a dense training program runs on the C++ executor;
+    an fp64 program and a program with per-step-scope control flow stay on the
+    interpreter; both train identically to the interpreter."""
+    import numpy as np
+
+    import paddle_amd.fluid as fluid
+    from paddle_amd.framework import core
+
+    def build(dtype="float32"):
+        main, startup = fluid.Program(), fluid.Program()
+        main.random_seed = startup.random_seed = 3
+        with fluid.program_guard(main, startup):
+            x = fluid.layers.data(name="x", shape=[8], dtype=dtype)
+            y = fluid.layers.data(name="y", shape=[1], dtype=dtype)
+            p = fluid.layers.fc(x, size=1)
+            loss = fluid.layers.mean(fluid.layers.square_error_cost(p, y))
+            fluid.optimizer.SGD(learning_rate=0.1).minimize(loss)
+        return main, startup, loss
+
+    rs = np.random.RandomState(0)
+    xs, ys = rs.rand(16, 8).astype("float32"), rs.rand(16, 1).astype("float32")
+    res = {}
+    for eng in ("python", "auto"):
+        main, startup, loss = build()
+        exe = fluid.Executor(fluid.CPUPlace(), engine=eng)
+        with fluid.executor.scope_guard(core.Scope()):
+            fluid.Executor(fluid.CPUPlace(), engine="python").run(startup)
+            res[eng] = [float(exe.run(main, feed={"x": xs, "y": ys}, fetch_list=[loss])[0][0]) for _ in range(4)]
+        if eng == "auto":
+            assert exe._native is not None  # ran on the C++ executor
+    np.testing.assert_allclose(res["auto"], res["python"], rtol=1e-5)
+    main, startup, loss = build("float64")
+    exe = fluid.Executor(fluid.CPUPlace(), engine="auto")
+    with fluid.executor.scope_guard(core.Scope()):
+        exe.run(startup)
+        exe.run(main, feed={"x": xs.astype("float64"), "y": ys.astype("float64")}, fetch_list=[loss])
+    assert exe._native is None  # fp64: interpreter
