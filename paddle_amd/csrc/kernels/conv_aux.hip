@@ -246,7 +246,29 @@ __global__ void bn_apply_kernel(const u16* __restrict__ x, u16* __restrict__ y, 
     sc[j] = rstd[c] * ww;
     sf[j] = bb - mean[c] * sc[j];
   }
-  for (long i = i0; i < total; i += stride) {
+  // 4 chunks in flight per thread: every load of a group is issued before the first
+  // store (y may alias nothing the loads read, but the compiler cannot know that)
+  constexpr int U = 4;
+  long i = i0;
+  for (; i + (U - 1) * stride < total; i += U * stride) {
+    u16x8 xa[U], ra[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      xa[u] = *reinterpret_cast<const u16x8*>(x + (i + u * stride) * 8);
+      if (res) ra[u] = *reinterpret_cast<const u16x8*>(res + (i + u * stride) * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float a[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = fmaf(bf2f(xa[u][j]), sc[j], sf[j]) + (res ? bf2f(ra[u][j]) : 0.f);
+        a[j] = relu ? fmaxf(v, 0.f) : v;
+      }
+      store8(y + (i + u * stride) * 8, a);
+    }
+  }
+  for (; i < total; i += stride) {
     float a[8], r[8];
     load8(x + i * 8, a);
     if (res) {

@@ -539,18 +539,15 @@ static int wgrad_setup(convsn::WgParams& p, const void* dyp, const void* x, int 
 // own layout [Cout][C][KH][KW] and dtype (fp32 or bf16): no permute / cast pass after
 __global__ void wgrad_reduce_kernel(const float* __restrict__ part, int S, int Cout, int C, int KH, int KW,
                                     void* __restrict__ out, int out_bf16, int accumulate) {
-  const long K = (long)KH * KW * C, n = (long)Cout * K;
-  for (long o = blockIdx.x * (long)blockDim.x + threadIdx.x; o < n; o += (long)gridDim.x * blockDim.x) {
-    // o indexes [co][c][kh][kw]
-    const int kw = (int)(o % KW);
-    long t = o / KW;
-    const int kh = (int)(t % KH);
-    t /= KH;
-    const int c = (int)(t % C);
-    const long co = t / C;
-    const long src = co * K + ((long)kh * KW + kw) * C + c;
+  // threads walk the partials in their own order (K-contiguous: every split's read is
+  // coalesced); each sum is written once to its [co][c][kh][kw] slot
+  const long K = (long)KH * KW * C, n = (long)Cout * K, taps = (long)KH * KW;
+  for (long src = blockIdx.x * (long)blockDim.x + threadIdx.x; src < n; src += (long)gridDim.x * blockDim.x) {
+    const long co = src / K, kk = src - co * K;
+    const long c = kk % C, tap = kk / C;
+    const long o = co * K + c * taps + tap;
     float a = 0.f;
-    for (int sp = 0; sp < S; ++sp) a += part[(long)sp * Cout * K + src];
+    for (int sp = 0; sp < S; ++sp) a += part[(long)sp * n + src];
     if (out_bf16) {
       u16* y = (u16*)out;
       y[o] = f2bf(accumulate ? a + bf2f(y[o]) : a);

