@@ -341,3 +341,32 @@ def sequence_scatter(ctx):
         cols = ids[off[i]:off[i + 1]].reshape(-1).long()
         out[i].index_add_(0, cols, up[off[i]:off[i + 1]].reshape(-1))
     ctx.set_output("Out", out)
+
+
+@register_op("sequence_reverse", ["X"], ["Y"], {})
+def sequence_reverse(ctx):
+    """Reverse the rows of every sequence (later Paddle's sequence_reverse_op; the v1
+    recurrent layers' ``reverse=True``).  A gather: its VJP is the inverse gather."""
+    x = ctx.input("X")
+    off, lod = _last_level(ctx)
+    if ctx.meta:
+        ctx.set_output("Y", torch.empty_like(x, device="meta"), lod or None)
+        return
+    idx = [j for i in range(len(off) - 1) for j in range(off[i + 1] - 1, off[i] - 1, -1)]
+    ctx.set_output("Y", x[torch.tensor(idx, dtype=torch.long, device=x.device)], lod or None)
+
+
+@register_op("scale_sub_region", ["X", "Indices"], ["Out"], {"value": 1.0})
+def scale_sub_region(ctx):
+    """v1 ScaleSubRegionLayer: multiply the box [c0, c1] x [h0, h1] x [w0, w1]
+    (1-based, inclusive; one row of Indices per sample) of each [C, H, W] sample."""
+    x = ctx.input("X")
+    if ctx.meta:
+        ctx.set_output("Out", torch.empty_like(x, device="meta"))
+        return
+    ind = ctx.input("Indices").to(torch.long).reshape(x.shape[0], 6).cpu().tolist()
+    m = torch.ones_like(x)
+    v = float(ctx.attr("value"))
+    for n, (c0, c1, h0, h1, w0, w1) in enumerate(ind):
+        m[n, c0 - 1:c1, h0 - 1:h1, w0 - 1:w1] = v
+    ctx.set_output("Out", x * m)

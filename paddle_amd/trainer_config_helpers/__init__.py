@@ -28,6 +28,8 @@ from ..v2 import networks as _nets
 from ..v2 import optimizer as _opt
 from ..v2 import pooling as _pool
 from ..v2._core import STATE
+from . import layers_v1 as _v1
+from .layers_v1 import *  # noqa: F401,F403  (the rest of layers.py __all__)
 
 # ------------------------------------------------------------------ activations
 TanhActivation, ReluActivation, SigmoidActivation = _act.Tanh, _act.Relu, _act.Sigmoid
@@ -164,7 +166,7 @@ def fc_layer(input, size, act=None, name=None, param_attr=None, bias_attr=None, 
     out = _l.fc(input=x, size=size, act=act if act is not None else TanhActivation(), name=name)
     if layer_attr is not None and getattr(layer_attr, "drop_rate", None):
         out = _l.dropout(input=out, dropout_rate=layer_attr.drop_rate)
-    return out
+    return _v1._named(out, name)  # a recurrent_group memory(name=...) may read it
 
 
 def embedding_layer(input, size, name=None, param_attr=None, **kw):
@@ -192,16 +194,19 @@ def dropout_layer(input, dropout_rate, name=None):
 
 
 def concat_layer(input, act=None, name=None, **kw):
-    return _l.concat(input=input)
+    return _v1._named(_l.concat(input=input), name)
 
 
 def addto_layer(input, act=None, name=None, bias_attr=None, **kw):
     from .. import fluid
 
     with v2._core.guard():
-        s = fluid.layers.sums(list(input))
+        ins = list(input) if isinstance(input, (list, tuple)) else [input]
+        s = fluid.layers.sums(ins) if len(ins) > 1 else ins[0]
         a = _act.act_name(act)
-        return getattr(fluid.layers, a)(s) if a else s
+        out = getattr(fluid.layers, a)(s) if a and a not in ("linear", "identity") else s
+        out.v2_size = getattr(ins[0], "v2_size", None)
+        return _v1._named(out, name)
 
 
 def pooling_layer(input, pooling_type=None, name=None, **kw):

@@ -1,0 +1,176 @@
+"""The v1 layer DSL beyond the basic layers (trainer_config_helpers/layers_v1.py):
+every name of the reference layers.py ``__all__`` resolves, and the layers build
+Fluid programs that compute their v1 functions (numpy references) and train."""
+import re
+
+import numpy as np
+import pytest
+
+import paddle_amd.fluid as fluid
+import paddle_amd.trainer_config_helpers as tch
+from paddle_amd.v2 import data_type as dt
+from paddle_amd.v2._core import STATE
+
+REF = "/root/reference/python/paddle/trainer_config_helpers/layers.py"
+
+
+def test_every_reference_layer_name_resolves():
+    try:
+        src = open(REF).read()
+    except OSError:
+        pytest.skip("reference tree not present")
+    names = [x.strip().strip("\"'") for x in re.search(r"__all__ = \[(.*?)\]", src, re.S).group(1).split(",")
+             if x.strip()]
+    assert len(names) == 118
+    missing = [n for n in names if not hasattr(tch, n)]
+    assert not missing, missing
+
+
+def _run(build, feed, fetch_names=None):
+    """parse_config(build) then one forward of the program; returns the outputs."""
+    outs = {}
+
+    def conf():
+        tch.settings(batch_size=4, learning_rate=0.1)
+        res = build()
+        outs["vars"] = res if isinstance(res, (list, tuple)) else [res]
+        tch.outputs(outs["vars"][0])
+
+    tch.parse_config(conf)
+    exe = fluid.Executor(fluid.CPUPlace())
+    scope = fluid.core.Scope()
+    with fluid.executor.scope_guard(scope):
+        exe.run(STATE["startup"])
+        got = exe.run(STATE["main"], feed=feed, fetch_list=outs["vars"], return_numpy=False)
+    return [np.array(g) for g in got], scope
+
+
+def test_elementwise_and_shape_layers_match_numpy():
+    rs = np.random.RandomState(0)
+    a = rs.rand(4, 6).astype("float32") + 0.5
+    b = rs.rand(4, 6).astype("float32") + 0.5
+    w = rs.rand(4, 1).astype("float32")
+
+    def build():
+        xa = tch.data_layer(name="a", size=6)
+        xb = tch.data_layer(name="b", size=6)
+        xw = tch.data_layer(name="w", size=1)
+        return [tch.interpolation_layer(input=[xa, xb], weight=xw), tch.scaling_layer(input=xa, weight=xw),
+                tch.power_layer(input=xa, weight=xw), tch.sum_to_one_norm_layer(input=xa),
+                tch.dot_prod_layer(xa, xb), tch.out_prod_layer(xa, xb), tch.l2_distance_layer(xa, xb),
+                tch.slope_intercept_layer(xa, slope=2.0, intercept=-1.0), tch.repeat_layer(xw, 3),
+                tch.row_l2_norm_layer(xa), tch.clip_layer(xa, 0.7, 1.2), tch.rotate_layer(xa, 2, 3),
+                tch.linear_comb_layer(weights=xw, vectors=xa, size=6)]
+
+    got, _ = _run(build, {"a": a, "b": b, "w": w})
+    exp = [w * a + (1 - w) * b, w * a, a ** w, a / a.sum(1, keepdims=True), (a * b).sum(1, keepdims=True),
+           (a[:, :, None] * b[:, None, :]).reshape(4, 36), np.sqrt(((a - b) ** 2).sum(1, keepdims=True)),
+           2 * a - 1, np.repeat(w, 3, axis=1), a / np.linalg.norm(a, axis=1, keepdims=True), np.clip(a, 0.7, 1.2),
+           np.rot90(a.reshape(4, 2, 3), k=-1, axes=(1, 2)).reshape(4, 6), w * a]
+    for g, e in zip(got, exp):
+        np.testing.assert_allclose(g.reshape(e.shape), e, rtol=1e-4, atol=1e-5)
+
+
+def test_mixed_layer_projections_sum():
+    rs = np.random.RandomState(1)
+    x = rs.rand(3, 5).astype("float32")
+
+    def build():
+        xi = tch.data_layer(name="x", size=5)
+        m = tch.mixed_layer(size=5, input=[tch.full_matrix_projection(xi, size=5), tch.identity_projection(xi),
+                                           tch.dotmul_operator(xi, xi, scale=2.0)], act=tch.LinearActivation())
+        with tch.mixed_layer(size=5) as m2:
+            m2 += tch.identity_projection(xi)
+            m2 += tch.slice_projection(xi, [(0, 2), (2, 5)])
+        return [m, m2.m.out]
+
+    got, scope = _run(build, {"x": x})
+    wname = [p.name for p in STATE["main"].global_block().all_parameters()][0]
+    W = np.array(scope.find_var(wname).get_tensor())
+    np.testing.assert_allclose(got[0], x @ W + x + 2 * x * x, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(got[1], 2 * x, rtol=1e-5)
+
+
+def test_recurrent_group_memory_matches_manual_rnn():
+    """h_t = tanh(x_t W + h_{t-1} U) through recurrent_group + memory(name=...)."""
+    rs = np.random.RandomState(2)
+    lens = [3, 2]
+    x = rs.rand(sum(lens), 4).astype("float32")
+
+    def build():
+        xs = tch.data_layer(name="xs", size=4, type=dt.dense_vector_sequence(4))
+
+        def step(xt):
+            prev = tch.memory(name="h", size=3)
+            return tch.fc_layer(input=[xt, prev], size=3, act=tch.TanhActivation(), name="h")
+
+        return tch.recurrent_group(step=step, input=xs)
+
+    feed = {"xs": fluid.create_lod_tensor(x, [lens], fluid.CPUPlace())}
+    got, scope = _run(build, feed)
+    params = STATE["main"].global_block().all_parameters()
+    vals = {p.name: np.array(scope.find_var(p.name).get_tensor()) for p in params}
+    W = next(v for v in vals.values() if v.shape == (7, 3))
+    b = next((v for v in vals.values() if v.shape in ((3,), (1, 3))), np.zeros(3, "float32")).reshape(-1)
+    exp, o = [], 0
+    for n in lens:
+        h = np.zeros(3, "float32")
+        for t in range(n):
+            h = np.tanh(np.concatenate([x[o + t], h]) @ W + b)
+            exp.append(h)
+        o += n
+    np.testing.assert_allclose(got[0], np.array(exp), rtol=1e-4, atol=1e-5)
+
+
+def test_sequence_tagger_with_lstm_and_crf_trains():
+    """embedding -> mixed(full_matrix) -> lstmemory -> mixed -> crf_layer: the cost
+    falls over a few passes of a synthetic tagging task (label = word id mod 3)."""
+    rs = np.random.RandomState(3)
+
+    def conf():
+        tch.settings(batch_size=8, learning_rate=0.05, learning_method=tch.AdamOptimizer())
+        w = tch.data_layer(name="word", size=20, type=dt.integer_value_sequence(20))
+        lab = tch.data_layer(name="label", size=3, type=dt.integer_value_sequence(3))
+        emb = tch.embedding_layer(input=w, size=16)
+        g = tch.mixed_layer(size=32, input=[tch.full_matrix_projection(emb, size=32)])
+        h = tch.lstmemory(input=g)
+        feat = tch.mixed_layer(size=3, input=[tch.full_matrix_projection(h, size=3)])
+        tch.outputs(tch.crf_layer(input=feat, label=lab, size=3))
+
+    c = tch.parse_config(conf)
+    exe = fluid.Executor(fluid.CPUPlace())
+    with fluid.program_guard(STATE["main"], STATE["startup"]):
+        fluid.optimizer.Adam(learning_rate=0.05).minimize(c.cost)
+    costs = []
+    with fluid.executor.scope_guard(fluid.core.Scope()):
+        exe.run(STATE["startup"])
+        for it in range(30):
+            lens = list(rs.randint(2, 6, size=4))
+            ids = rs.randint(0, 20, size=(sum(lens), 1)).astype("int64")
+            feed = {"word": fluid.create_lod_tensor(ids, [lens], fluid.CPUPlace()),
+                    "label": fluid.create_lod_tensor(ids % 3, [lens], fluid.CPUPlace())}
+            (l,) = exe.run(STATE["main"], feed=feed, fetch_list=[c.cost])
+            costs.append(float(np.array(l).reshape(-1)[0]))
+    assert np.mean(costs[-5:]) < 0.7 * np.mean(costs[:5]), costs
+
+
+def test_costs_and_gru_forward_run():
+    rs = np.random.RandomState(4)
+    lens = [4, 3]
+
+    def build():
+        x = tch.data_layer(name="x", size=6, type=dt.dense_vector_sequence(6))
+        p = tch.data_layer(name="p", size=5)
+        y = tch.data_layer(name="y", size=5)
+        g = tch.grumemory(input=tch.mixed_layer(size=9, input=[tch.full_matrix_projection(x, size=9)]))
+        return [tch.last_seq(g), tch.multi_binary_label_cross_entropy(p, y), tch.huber_regression_cost(p, y),
+                tch.smooth_l1_cost(p, y), tch.sum_cost(p), tch.factorization_machine(p, factor_size=4)]
+
+    p = rs.rand(2, 5).astype("float32") * 0.8 + 0.1
+    y = (rs.rand(2, 5) > 0.5).astype("float32")
+    feed = {"x": fluid.create_lod_tensor(rs.rand(7, 6).astype("float32"), [lens], fluid.CPUPlace()), "p": p, "y": y}
+    got, _ = _run(build, feed)
+    assert got[0].shape == (2, 3)
+    bce = -(y * np.log(p) + (1 - y) * np.log(1 - p)).sum(1).mean()
+    np.testing.assert_allclose(float(got[1].reshape(-1)[0]), bce, rtol=1e-4)
+    np.testing.assert_allclose(float(got[4].reshape(-1)[0]), p.sum(), rtol=1e-5)
