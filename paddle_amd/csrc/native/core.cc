@@ -758,6 +758,12 @@ void Executor::RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* 
         timed(op, [&] { (*dk)(OpRun{op, *scope, ctx_}); });
         continue;
       } catch (const Decline&) {
+        // the embedder's kernel runs on the device too: prefer it to a host round trip
+        if (fallback) {
+          embedder_fallbacks[op.type] += 1;
+          timed(op, [&] { fallback(op, *scope, block.idx, op_idx); });
+          continue;
+        }
       }
     }
     const Kernel* k = find_kernel(op.type, false);

@@ -55,6 +55,19 @@ int pa_adamw(int gdtype, int pdtype, float* p, const void* g, float* m, float* v
 int pa_momentum(int gdtype, float* p, const void* g, float* vel, long n, float lr, const float* lr_ptr, float mu,
                 int nesterov, float wd, float gscale, hipStream_t st);
 int pa_sgd(int dt, void* p, const void* g, const float* lr, long n, hipStream_t st);
+// norm.hip: LayerNorm / RMSNorm rows (H % 8 == 0, H <= 8192); ws: 2 * min(512, ceil(N/4)) * H floats
+int pa_norm_fwd(int dtype, int rms, const void* x, const void* res, const void* w, const void* b, void* y,
+                void* hout, float* mean, float* rstd, long N, int H, float eps, hipStream_t st);
+int pa_norm_bwd(int dtype, int rms, const void* dy, const void* h, const void* w, const float* mean,
+                const float* rstd, const void* dres, void* dx, void* dw, void* db, float* ws, long N, int H,
+                hipStream_t st);
+// elementwise.hip / oplib.hip / misc.hip
+int pa_embedding_bwd(int dtype, const long* ids, const void* dout, float* dW, long N, int H, long padding_idx,
+                     hipStream_t st);
+int pa_topk(int dt, const void* x, void* vals, long* idx, long rows, int n, int k, hipStream_t st);
+int pa_accuracy(const long* ind, const long* lab, long rows, int k, int* correct, float* acc, int* total,
+                hipStream_t st);
+int pa_mask_mul(int dt, const void* d, const void* mask, void* out, long n, float scale, hipStream_t st);
 }
 
 // activation ids of fluid_ops.hip enum Act

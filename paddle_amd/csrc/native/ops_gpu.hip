@@ -1103,6 +1103,131 @@ PA_DEVICE_KERNEL(fill_constant, k_fill_constant);
 PA_DEVICE_KERNEL(fill_zeros_like, k_fill_zeros_like);
 PA_DEVICE_KERNEL(sum, k_sum);
 
+// =============================================================== transformer / metric ops
+// layer_norm_op.cu on the shared norm kernel (norm.hip): Y plus per-row Mean and
+// Variance (the grad op's inputs); rows of H % 8 != 0 or H > 8192 decline to the
+// Python kernel
+__global__ void rstd_to_var_kernel(const float* __restrict__ rstd, float* __restrict__ var, int64_t n, float eps) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    var[i] = 1.f / (rstd[i] * rstd[i]) - eps;
+}
+__global__ void var_to_rstd_kernel(const float* __restrict__ var, float* __restrict__ rstd, int64_t n, float eps) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    rstd[i] = rsqrtf(var[i] + eps);
+}
+
+void ln_rows(const OpRun& r, const Tensor& x, int64_t& rows, int64_t& H) {
+  const size_t ax = (size_t)r.op.GetInt("begin_norm_axis", 1);
+  rows = prod(x.dims, 0, ax);
+  H = prod(x.dims, ax);
+  if (x.dtype != DT::FP32 || H % 8 || H > 8192 || rows <= 0) throw Decline();
+}
+
+void k_layer_norm(const OpRun& r) {
+  Tensor x = r.in("X");
+  int64_t rows, H;
+  ln_rows(r, x, rows, H);
+  Tensor* sc = r.in_opt("Scale");
+  Tensor* bi = r.in_opt("Bias");
+  if ((sc && sc->dtype != DT::FP32) || (bi && bi->dtype != DT::FP32)) throw Decline();
+  const float eps = r.op.GetFloat("epsilon", 1e-5f);
+  const void* w = sc ? (const void*)f32(*sc) : nullptr;
+  const void* b = bi ? (const void*)f32(*bi) : nullptr;
+  float* y = out_f32(r, "Y", x.dims);
+  r.out("Y")->lod = x.lod;
+  float* rstd = workspace(r, "@ln_rstd@", rows);
+  float* mean = r.out("Mean") ? out_f32(r, "Mean", {rows}) : workspace(r, "@ln_mean@", rows);
+  PA_KL(pa_norm_fwd(0, 0, f32(x), nullptr, w, b, y, nullptr, mean, rstd, rows, (int)H, eps, S(r)));
+  if (r.out("Variance"))
+    hipLaunchKernelGGL(rstd_to_var_kernel, dim3(grid_for(rows)), dim3(256), 0, S(r), rstd,
+                       out_f32(r, "Variance", {rows}), rows, eps);
+}
+
+void k_layer_norm_grad(const OpRun& r) {
+  Tensor x = r.in("X");
+  int64_t rows, H;
+  ln_rows(r, x, rows, H);
+  Tensor dy = r.in("Y@GRAD");
+  Tensor mean = r.in("Mean");
+  Tensor var = r.in("Variance");
+  Tensor* sc = r.in_opt("Scale");
+  if (dy.dtype != DT::FP32 || (sc && sc->dtype != DT::FP32)) throw Decline();
+  const float eps = r.op.GetFloat("epsilon", 1e-5f);
+  float* rstd = workspace(r, "@ln_rstd@", rows);
+  hipLaunchKernelGGL(var_to_rstd_kernel, dim3(grid_for(rows)), dim3(256), 0, S(r), f32(var), rstd, rows, eps);
+  const int64_t parts = std::min<int64_t>(512, (rows + 3) / 4);
+  float* ws = workspace(r, "@ln_ws@", 2 * parts * H);
+  float* dx = r.out("X@GRAD") ? out_f32(r, "X@GRAD", x.dims) : workspace(r, "@ln_dx@", rows * H);
+  float* dw = (sc && r.out("Scale@GRAD")) ? out_f32(r, "Scale@GRAD", sc->dims) : workspace(r, "@ln_dw@", H);
+  float* db = r.out("Bias@GRAD") ? out_f32(r, "Bias@GRAD", {H}) : workspace(r, "@ln_db@", H);
+  PA_KL(pa_norm_bwd(0, 0, f32(dy), f32(x), sc ? (const void*)f32(*sc) : nullptr, f32(mean), rstd, nullptr, dx, dw,
+                    db, ws, rows, (int)H, S(r)));
+}
+
+// lookup_table_grad (dense W@GRAD): zero + scatter-add of the output rows
+void k_lookup_table_grad(const OpRun& r) {
+  if (r.op.GetBool("is_sparse")) throw Decline();  // SelectedRows gradient: the Python kernel
+  Tensor w = r.in("W");
+  Tensor ids = r.in("Ids");
+  Tensor dout = r.in("Out@GRAD");
+  if (ids.dtype != DT::INT64 || dout.dtype != DT::FP32 || w.dims.size() != 2) throw Decline();
+  const int64_t V = w.dims[0], Dm = w.dims[1], n = ids.numel();
+  float* dw = out_f32(r, "W@GRAD", w.dims);
+  HIPCHK(hipMemsetAsync(dw, 0, sizeof(float) * V * Dm, S(r)));
+  if (n) PA_KL(pa_embedding_bwd(0, ids.data<int64_t>(), f32(dout), dw, n, (int)Dm, r.op.GetInt("padding_idx", -1),
+                                S(r)));
+}
+
+// top_k (last axis, k <= 64): values + int64 indices
+void k_top_k(const OpRun& r) {
+  Tensor x = r.in("X");
+  if (x.dtype != DT::FP32 || x.dims.empty()) throw Decline();
+  const int k = r.op.GetInt("k", 1);
+  const int64_t n = x.dims.back(), rows = x.numel() / std::max<int64_t>(n, 1);
+  if (k <= 0 || k > 64 || k > n) throw Decline();
+  Dims od = x.dims;
+  od.back() = k;
+  float* vals = out_f32(r, "Out", od);
+  Tensor* it = r.out("Indices");
+  int64_t* idx = static_cast<int64_t*>(it->alloc(DT::INT64, od, D(r)));
+  r.out("Out")->lod = x.lod;
+  it->lod = x.lod;
+  PA_KL(pa_topk(0, f32(x), vals, (long*)idx, rows, (int)n, k, S(r)));
+}
+
+// accuracy (accuracy_op.cu): top-k indices vs label -> Accuracy (f32), Correct / Total (int32)
+void k_accuracy(const OpRun& r) {
+  Tensor ind = r.in("Indices");
+  Tensor lab = r.in("Label");
+  if (ind.dtype != DT::INT64 || lab.dtype != DT::INT64 || ind.dims.size() != 2) throw Decline();
+  const int64_t rows = ind.dims[0];
+  const int k = (int)ind.dims[1];
+  float* acc = out_f32(r, "Accuracy", {1});
+  int* correct = static_cast<int*>(r.out("Correct")->alloc(DT::INT32, {1}, D(r)));
+  int* total = static_cast<int*>(r.out("Total")->alloc(DT::INT32, {1}, D(r)));
+  PA_KL(pa_accuracy(ind.data<int64_t>(), lab.data<int64_t>(), rows, k, correct, acc, total, S(r)));
+}
+
+// dropout_grad with the native Philox mask (uint8): dX = dOut * mask * scale
+void k_dropout_grad(const OpRun& r) {
+  Tensor m = r.in("Mask");
+  Tensor d = r.in("Out@GRAD");
+  if (d.dtype != DT::FP32 || (m.dtype != DT::UINT8 && m.dtype != DT::BOOL)) throw Decline();
+  const float p = r.op.GetFloat("dropout_prob", 0.5f);
+  const bool upscale = r.op.GetString("dropout_implementation", "downgrade_in_infer") == "upscale_in_train";
+  const float scale = (upscale && p < 1.f) ? 1.f / (1.f - p) : 1.f;
+  float* dx = out_f32(r, "X@GRAD", d.dims);
+  r.out("X@GRAD")->lod = d.lod;
+  PA_KL(pa_mask_mul(0, f32(d), m.raw(), dx, d.numel(), scale, S(r)));
+}
+
+PA_DEVICE_KERNEL(layer_norm, k_layer_norm);
+PA_DEVICE_KERNEL(layer_norm_grad, k_layer_norm_grad);
+PA_DEVICE_KERNEL(lookup_table_grad, k_lookup_table_grad);
+PA_DEVICE_KERNEL(top_k, k_top_k);
+PA_DEVICE_KERNEL(accuracy, k_accuracy);
+PA_DEVICE_KERNEL(dropout_grad, k_dropout_grad);
+
 void link_device_kernels() {}
 
 // GEMM entry for tests / benchmarks (C ABI below)

@@ -323,6 +323,9 @@ class NativeEngine:
                     lt.set_lod(lod)
                 vals.append(lt)
             ctx_ins[slot] = vals
+        in_names = {n for _, names in ins for n in names}
+        ent = self._scopes.get(id(scope))
+        bound_names = ent[2] if ent is not None and ent[0] is scope else {}
         ctx = R.KernelContext(op.type, ctx_ins, outs, attrs, self.place, scope, op, self._bexe)
         R.run_kernel(info, ctx)
         self.py_fallbacks[op.type] = self.py_fallbacks.get(op.type, 0) + 1
@@ -345,8 +348,20 @@ class NativeEngine:
                     raise NotImplementedError(f"native engine: op {op.type} output {n} dtype {t.dtype}")
                 if not t.is_contiguous() or self._aliases_native(t):
                     t = t.contiguous() if not t.is_contiguous() and not self._aliases_native(t) else t.clone()
-                keep[n] = t  # alive while the native scope references it
                 var = ns.find_var(n)  # an enclosing scope's variable is updated in place
+                if var is not None and (n in in_names or n in bound_names) and var.is_initialized():
+                    # an in-place op (ParamOut == Param) or a lent persistable: write INTO
+                    # its buffer, so every holder of that storage (the Python scope's
+                    # parameter, optimizer state) keeps seeing one tensor
+                    cur = var.get_tensor()
+                    if (int(cur.data_ptr()) and tuple(cur.shape()) == tuple(t.shape)
+                            and _DT_TORCH.get(int(cur.dtype())) == t.dtype):
+                        dst = self._wrap(cur)
+                        if dst.data_ptr() != t.data_ptr():
+                            dst.copy_(t)
+                        cur.set_lod([list(map(int, lv)) for lv in (v.lod() or [])])
+                        continue
+                keep[n] = t  # alive while the native scope references it
                 nt = (var if var is not None else ns.var(n)).get_tensor()
                 nt.share_external(t.data_ptr(), self._b.C.VarType(_TORCH_DT[t.dtype]), list(t.shape),
                                   self.device)

@@ -1,0 +1,26 @@
+import json, os, sys, tempfile
+import numpy as np
+import paddle_amd.fluid as fluid
+
+def run(engine_startup):
+    main, st = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, st):
+        x = fluid.layers.data("x", [512])
+        h = fluid.layers.fc(x, 1024, act="relu")
+        loss = fluid.layers.mean(fluid.layers.fc(h, 256))
+        fluid.optimizer.SGD(0.01).minimize(loss)
+    place = fluid.CUDAPlace(0)
+    exe = fluid.Executor(place)
+    path = tempfile.mktemp()
+    with fluid.scope_guard(fluid.Scope()):
+        fluid.Executor(place, engine=engine_startup).run(st)
+        with fluid.profiler.profiler("All", sorted_key="total", profile_path=path):
+            for _ in range(2):
+                exe.run(main, feed={"x": np.random.rand(256, 512).astype("float32")}, fetch_list=[loss])
+    prof = json.load(open(path))
+    types = {}
+    for e in prof["events"]:
+        types[e["type"]] = types.get(e["type"], 0) + 1
+    print(engine_startup, "native used for main:", exe._native is not None, types, flush=True)
+
+run(sys.argv[1])
