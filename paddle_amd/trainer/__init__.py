@@ -71,7 +71,8 @@ def main(argv=None):
     ap = argparse.ArgumentParser(prog="paddle_trainer", description="v1 trainer front end on the Fluid engine")
     ap.add_argument("--config", required=True)
     ap.add_argument("--config_args", default="")
-    ap.add_argument("--job", default="train", choices=["train", "test", "time"])
+    ap.add_argument("--job", default="train", choices=["train", "test", "time", "checkgrad"])
+    ap.add_argument("--checkgrad_eps", type=float, default=1e-3)
     ap.add_argument("--num_passes", type=int, default=1)
     ap.add_argument("--log_period", type=int, default=100)
     ap.add_argument("--save_dir", default="")
@@ -91,10 +92,12 @@ def main(argv=None):
     bs = conf.batch_size or 1
     train = _reader(src, "train", bs, shuffle_seed=a.seed)
     test = _reader(src, "test", bs)
-    if train is None and a.job in ("train", "time"):
+    if train is None and a.job in ("train", "time", "checkgrad"):
         raise SystemExit("the config defines no training data (define_py_data_sources2 train_list)")
     prov = (train or test)[1]
     feeding = prov.feeding(conf.input_layer_names)
+    if a.job == "checkgrad":
+        return checkgrad(conf, train[0], prov.feeding(conf.input_layer_names), eps=a.checkgrad_eps, seed=a.seed)
     trainer, params = conf.make_trainer()
     if a.init_model_path:
         with open(a.init_model_path, "rb") as f:
@@ -130,6 +133,61 @@ def main(argv=None):
         dt = time.perf_counter() - t0
         print(f"time: {len(log)} batches in {dt:.3f} s, {len(log) * bs / max(dt, 1e-9):.1f} samples/s", flush=True)
     return log
+
+
+def checkgrad(conf, reader, feeding, eps=1e-3, seed=1):
+    """``--job=checkgrad`` (Trainer.cpp checkGradient): on the first training batch,
+    for every parameter compare the analytic directional derivative <dL/dp, d>
+    (the program's backward) with the central difference (L(p + eps d) - L(p - eps d))
+    / (2 eps) along a random unit direction d.  Prints one line per parameter and
+    returns {name: relative difference}."""
+    import numpy as np
+
+    from .. import fluid
+    from ..v2 import _core
+
+    STATE = _core.STATE
+    main = STATE["main"]
+    fwd = main.clone(for_test=True)
+    with _core.guard():
+        pg = fluid.backward.append_backward(conf.cost)
+    names = list(STATE["data"])
+    order = sorted(feeding.items(), key=lambda kv: kv[1]) if isinstance(feeding, dict) else \
+        [(n, i) for i, n in enumerate(feeding)]
+    names = [n for n, _ in order] or names
+    place = _core.place()
+    feeder = fluid.DataFeeder(feed_list=[main.global_block().var(n) for n in names], place=place, program=main)
+    batch = next(iter(reader()))
+    feed = feeder.feed(batch)
+    exe = fluid.Executor(place)
+    scope = fluid.core.Scope()
+    rs = np.random.RandomState(seed)
+    out = {}
+    with fluid.scope_guard(scope):
+        exe.run(STATE["startup"])
+        grads = exe.run(main, feed=feed, fetch_list=[g for _, g in pg])
+
+        def loss():
+            (v,) = exe.run(fwd, feed=feed, fetch_list=[conf.cost])
+            return float(np.array(v, dtype=np.float64).ravel()[0])
+
+        for (p, _), g in zip(pg, grads):
+            t = scope.find_var(p.name).get_tensor()
+            p0 = np.array(t.numpy(), dtype=np.float64)
+            d = rs.randn(*p0.shape)
+            d /= max(np.linalg.norm(d), 1e-12)
+            analytic = float((np.array(g, dtype=np.float64) * d).sum())
+            t.set((p0 + eps * d).astype(np.float32), place)
+            lp = loss()
+            t.set((p0 - eps * d).astype(np.float32), place)
+            lm = loss()
+            t.set(p0.astype(np.float32), place)
+            numeric = (lp - lm) / (2 * eps)
+            rel = abs(analytic - numeric) / max(abs(analytic), abs(numeric), 1e-8)
+            out[p.name] = rel
+            print(f"checkgrad {p.name}: analytic {analytic:.6e} numeric {numeric:.6e} rel diff {rel:.3e}",
+                  flush=True)
+    return out
 
 
 if __name__ == "__main__":

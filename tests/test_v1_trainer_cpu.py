@@ -71,6 +71,11 @@ def test_v1_trainer_trains_tests_and_saves(tmp_path, capsys):
         trainer.main(["--config", conf, "--job", "test", "--init_model_path", tar])
         out = capsys.readouterr().out
         assert "Test cost" in out and "classification_error_evaluator" in out
+        # --job=checkgrad: analytic vs central-difference directional derivatives
+        rel = trainer.main(["--config", conf, "--job", "checkgrad", "--checkgrad_eps", "1e-3"])
+        out = capsys.readouterr().out
+        assert len(rel) == 4 and "checkgrad" in out
+        assert max(rel.values()) < 2e-2, rel
     finally:
         os.chdir(cwd)
         sys.path.remove(d)
