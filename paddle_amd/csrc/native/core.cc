@@ -680,6 +680,11 @@ void Executor::RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* 
   static const std::set<std::string> agnostic = {"feed", "fetch", "reshape", "reshape2", "flatten", "flatten2",
                                                  "squeeze", "squeeze2", "unsqueeze", "unsqueeze2", "delete_var",
                                                  "reshape_grad", "reshape2_grad"};
+  // loop counters / flags: a declined device kernel takes the host kernel (a few
+  // bytes each way), not the embedder's
+  static const std::set<std::string> host_scalar = {"fill_constant", "increment", "less_than", "less_equal",
+                                                    "greater_than", "greater_equal", "equal", "not_equal",
+                                                    "logical_and", "logical_or", "logical_xor", "logical_not"};
   auto timed = [&](const OpDesc& op, const std::function<void()>& fn) {
     if (!profile) return fn();
     Sync();
@@ -758,8 +763,10 @@ void Executor::RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* 
         timed(op, [&] { (*dk)(OpRun{op, *scope, ctx_}); });
         continue;
       } catch (const Decline&) {
-        // the embedder's kernel runs on the device too: prefer it to a host round trip
-        if (fallback) {
+        // the embedder's kernel runs on the device too: prefer it to a host round
+        // trip (place-agnostic host kernels -- fill / shape ops -- stay native)
+        const Kernel* hk = find_kernel(op.type, false);
+        if (fallback && !(hk && (agnostic.count(op.type) || host_scalar.count(op.type)))) {
           embedder_fallbacks[op.type] += 1;
           timed(op, [&] { fallback(op, *scope, block.idx, op_idx); });
           continue;

@@ -1,4 +1,5 @@
 import json, os, sys, tempfile
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 import paddle_amd.fluid as fluid
 
