@@ -174,3 +174,29 @@ def test_costs_and_gru_forward_run():
     bce = -(y * np.log(p) + (1 - y) * np.log(1 - p)).sum(1).mean()
     np.testing.assert_allclose(float(got[1].reshape(-1)[0]), bce, rtol=1e-4)
     np.testing.assert_allclose(float(got[4].reshape(-1)[0]), p.sum(), rtol=1e-5)
+
+
+def test_sequence_reverse_and_scale_sub_region_ops():
+    from paddle_amd.fluid.layer_helper import LayerHelper
+
+    main, startup = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, startup):
+        x = fluid.layers.data(name="x", shape=[2], dtype="float32", lod_level=1)
+        img = fluid.layers.data(name="img", shape=[2, 3, 3], dtype="float32")
+        ind = fluid.layers.data(name="ind", shape=[6], dtype="int64")
+        h = LayerHelper("t")
+        y = h.create_variable_for_type_inference("float32")
+        h.append_op(type="sequence_reverse", inputs={"X": [x]}, outputs={"Y": [y]})
+        z = h.create_variable_for_type_inference("float32")
+        h.append_op(type="scale_sub_region", inputs={"X": [img], "Indices": [ind]}, outputs={"Out": [z]},
+                    attrs={"value": 3.0})
+    xs = np.arange(10, dtype="float32").reshape(5, 2)
+    im = np.ones((1, 2, 3, 3), "float32")
+    exe = fluid.Executor(fluid.CPUPlace())
+    with fluid.executor.scope_guard(fluid.core.Scope()):
+        yy, zz = exe.run(main, feed={"x": fluid.create_lod_tensor(xs, [[2, 3]], fluid.CPUPlace()), "img": im,
+                                     "ind": np.array([[1, 1, 2, 3, 1, 2]], "int64")}, fetch_list=[y, z])
+    np.testing.assert_array_equal(np.array(yy), xs[[1, 0, 4, 3, 2]])
+    exp = im.copy()
+    exp[0, 0, 1:3, 0:2] = 3.0
+    np.testing.assert_array_equal(np.array(zz), exp)
