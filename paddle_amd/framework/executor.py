@@ -146,7 +146,11 @@ class BlockExecutor:
                 # HIP kernels (ops/aten_native.py); uncovered ATen kernels are counted
                 # (and refused under FLAGS_strict_native=1)
                 with _strict.region("fluid:" + op.type):
-                    run(info, ctx)
+                    if profiling:
+                        with prof.RecordEvent(op.type):
+                            run(info, ctx)
+                    else:
+                        run(info, ctx)
             elif profiling:
                 with prof.RecordEvent(op.type):
                     run(info, ctx)

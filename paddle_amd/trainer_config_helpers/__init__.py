@@ -28,6 +28,7 @@ from ..v2 import networks as _nets
 from ..v2 import optimizer as _opt
 from ..v2 import pooling as _pool
 from ..v2._core import STATE
+from . import config_proto as _cp
 from . import layers_v1 as _v1
 from .layers_v1 import *  # noqa: F401,F403  (the rest of layers.py __all__)
 
@@ -162,8 +163,9 @@ def fc_layer(input, size, act=None, name=None, param_attr=None, bias_attr=None, 
     one fc over their concatenation."""
     x = _one(input)
     if isinstance(x, (list, tuple)):
-        x = _l.concat(input=list(x))
-    out = _l.fc(input=x, size=size, act=act if act is not None else TanhActivation(), name=name)
+        x = list(x)  # one weight per input (w0, w1, ...), summed before the bias
+    out = _l.fc(input=x, size=size, act=act if act is not None else TanhActivation(), name=name,
+                bias_attr=bias_attr)
     if layer_attr is not None and getattr(layer_attr, "drop_rate", None):
         out = _l.dropout(input=out, dropout_rate=layer_attr.drop_rate)
     return _v1._named(out, name)  # a recurrent_group memory(name=...) may read it
@@ -194,7 +196,9 @@ def dropout_layer(input, dropout_rate, name=None):
 
 
 def concat_layer(input, act=None, name=None, **kw):
-    return _v1._named(_l.concat(input=input), name)
+    ins = list(input) if isinstance(input, (list, tuple)) else [input]
+    ins = [x.build(x.size) if isinstance(x, _v1._Projection) else x for x in ins]  # concat of projections
+    return _v1._named(_l.concat(input=ins), name)
 
 
 def addto_layer(input, act=None, name=None, bias_attr=None, **kw):
@@ -261,9 +265,12 @@ classification_error_printer_evaluator = _ev.classification_error_printer
 # ------------------------------------------------------------------ config parser
 class TrainerConfig:
     """What config_parser.parse_config returns: the model (outputs, data layers,
-    parameters -- a Fluid program) and the optimization settings."""
+    parameters -- a Fluid program) and the optimization settings; ``proto()`` /
+    ``to_text()`` give the reference's TrainerConfig message (config_proto.py)."""
 
-    def __init__(self, cfg):
+    def __init__(self, cfg, rec=None):
+        self._cfg = dict(cfg)
+        self._rec = rec
         self.outputs = cfg.get("outputs", [])
         self.batch_size = cfg.get("batch_size")
         self.learning_rate = cfg.get("learning_rate")
@@ -282,6 +289,36 @@ class TrainerConfig:
         return m.kind(learning_rate=self.learning_rate, regularization=self.regularization,
                       gradient_clipping_threshold=self.gradient_clipping_threshold, **m.kw)
 
+    def model_config(self) -> dict:
+        """ModelConfig (layers, parameters, input / output layer names, root sub-model)."""
+        return _cp.model_config(self._rec, self.outputs)
+
+    @property
+    def parameter_name_map(self) -> dict:
+        """v1 parameter name (``___fc_layer_0__.w0``) -> the Fluid parameter holding it."""
+        return dict(self._rec.param_map)
+
+    def trainer_config(self) -> dict:
+        tc = {"model_config": self.model_config(), "opt_config": _cp.opt_config(self._cfg)}
+        train, test = _cp.data_configs(self._cfg)
+        if train:
+            tc["data_config"] = train
+        if test:
+            tc["test_data_config"] = test
+        if self._cfg.get("config_file"):
+            tc["config_files"] = [self._cfg["config_file"]]
+        return tc
+
+    def proto(self) -> bytes:
+        """The serialised TrainerConfig (proto/TrainerConfig.proto wire format)."""
+        return _cp.encode("TrainerConfig", self.trainer_config())
+
+    def to_text(self, whole=False) -> str:
+        """Text format of the ModelConfig (``whole``: of the TrainerConfig)."""
+        if whole:
+            return _cp.to_text("TrainerConfig", self.trainer_config()) + "\n"
+        return _cp.to_text("ModelConfig", self.model_config()) + "\n"
+
     def make_trainer(self, parameters=None):
         params = parameters or v2.parameters.create(self.cost)
         return v2.trainer.SGD(cost=self.cost, parameters=params, update_equation=self.update_equation()), params
@@ -295,15 +332,27 @@ def parse_config(config, config_arg_str=""):
     _CFG.clear()
     _CFG["args"] = args
     v2.init(use_gpu=STATE.get("use_gpu", False))
-    if callable(config):
-        config()
-    else:
-        path = os.fspath(config)
-        with open(path) as f:
-            code = compile(f.read(), path, "exec")
-        g = {k: v for k, v in globals().items() if not k.startswith("_")}
-        g["__file__"] = path
-        exec(code, g)  # noqa: S102  (a v1 config is a Python script, as in the reference)
+    rec = _cp.start()
+    try:
+        if callable(config):
+            config()
+        else:
+            path = os.fspath(config)
+            _CFG["config_file"] = path
+            with open(path) as f:
+                code = compile(f.read(), path, "exec")
+            g = {k: v for k, v in globals().items() if not k.startswith("_")}
+            g["__file__"] = path
+            exec(code, g)  # noqa: S102  (a v1 config is a Python script, as in the reference)
+    finally:
+        _cp._REC.clear()
     if not _CFG.get("outputs"):
         raise ValueError("the config declared no outputs(...)")
-    return TrainerConfig(_CFG)
+    return TrainerConfig(_CFG, rec)
+
+
+# every layer function records its LayerConfig while a config is parsed
+for _n, _f in list(globals().items()):
+    if _n in _cp._TYPE and callable(_f) and not isinstance(_f, type):
+        globals()[_n] = _cp.recorded(_n, _f)
+del _n, _f

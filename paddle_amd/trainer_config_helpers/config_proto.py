@@ -1,0 +1,572 @@
+"""The v1 config parser's protobuf output: TrainerConfig / ModelConfig / LayerConfig /
+ParameterConfig / OptimizationConfig / DataConfig (reference proto/TrainerConfig.proto,
+ModelConfig.proto, ParameterConfig.proto, DataConfig.proto), built while a config runs.
+
+The reference ``config_parser.parse_config`` turns a v1 config into a TrainerConfig
+message for the legacy GradientMachine.  Here the DSL builds a Fluid program
+(``trainer_config_helpers``), and this module records, for every layer call of the
+config, the LayerConfig the reference would emit -- the same default names
+(``__fc_layer_0__``, ``___fc_layer_0__.w0`` / ``.wbias``), layer types, sizes,
+activation names, inputs and parameters -- so ``TrainerConfig.proto()`` serialises
+a wire-compatible TrainerConfig and ``dump_config`` prints its text form
+(reference python/paddle/utils/dump_config.py).  ``parameter_name_map`` maps the
+v1 parameter names to the Fluid parameters that hold them.
+
+The wire codec is a schema-driven proto2 encoder / decoder (varint, 64-bit, 32-bit,
+length-delimited; unknown fields skipped on decode) plus a text-format printer and
+parser; tests/test_v1_config_proto_cpu.py checks the output against the reference's
+own expected protostr files.
+"""
+from __future__ import annotations
+
+import inspect
+import re
+import struct
+
+# ---------------------------------------------------------------- schemas
+# field: (name, number, kind, repeated); kind: scalar type name or a message name
+_S = {
+    "ParameterUpdaterHookConfig": [("type", 1, "string", 0), ("sparsity_ratio", 2, "double", 0)],
+    "ParameterConfig": [
+        ("name", 1, "string", 0), ("size", 2, "uint64", 0), ("learning_rate", 3, "double", 0),
+        ("momentum", 4, "double", 0), ("initial_mean", 5, "double", 0), ("initial_std", 6, "double", 0),
+        ("decay_rate", 7, "double", 0), ("decay_rate_l1", 8, "double", 0), ("dims", 9, "uint64", 1),
+        ("device", 10, "int32", 0), ("initial_strategy", 11, "int32", 0), ("initial_smart", 12, "bool", 0),
+        ("num_batches_regularization", 13, "int32", 0), ("is_sparse", 14, "bool", 0), ("format", 15, "string", 0),
+        ("sparse_remote_update", 16, "bool", 0), ("gradient_clipping_threshold", 17, "double", 0),
+        ("is_static", 18, "bool", 0), ("para_id", 19, "uint64", 0),
+        ("update_hooks", 20, "ParameterUpdaterHookConfig", 1), ("need_compact", 21, "bool", 0),
+        ("sparse_update", 22, "bool", 0), ("is_shared", 23, "bool", 0),
+        ("parameter_block_size", 24, "uint64", 0)],
+    "SliceConfig": [("start", 1, "uint32", 0), ("end", 2, "uint32", 0)],
+    "ProjectionConfig": [
+        ("type", 1, "string", 0), ("name", 2, "string", 0), ("input_size", 3, "uint64", 0),
+        ("output_size", 4, "uint64", 0), ("context_start", 5, "int32", 0), ("context_length", 6, "int32", 0),
+        ("trainable_padding", 7, "bool", 0), ("num_filters", 9, "int32", 0), ("offset", 11, "uint64", 0),
+        ("slices", 13, "SliceConfig", 1)],
+    "OperatorConfig": [
+        ("type", 1, "string", 0), ("input_indices", 2, "int32", 1), ("input_sizes", 3, "uint64", 1),
+        ("output_size", 4, "uint64", 0), ("dotmul_scale", 5, "double", 0), ("num_filters", 7, "int32", 0)],
+    "LayerInputConfig": [
+        ("input_layer_name", 1, "string", 0), ("input_parameter_name", 2, "string", 0),
+        ("proj_conf", 6, "ProjectionConfig", 0), ("input_layer_argument", 9, "string", 0)],
+    "LayerConfig": [
+        ("name", 1, "string", 0), ("type", 2, "string", 0), ("size", 3, "uint64", 0),
+        ("active_type", 4, "string", 0), ("inputs", 5, "LayerInputConfig", 1),
+        ("bias_parameter_name", 6, "string", 0), ("num_filters", 7, "uint32", 0),
+        ("shared_biases", 8, "bool", 0), ("drop_rate", 10, "double", 0), ("num_classes", 11, "uint32", 0),
+        ("device", 12, "int32", 0), ("reversed", 13, "bool", 0), ("active_gate_type", 14, "string", 0),
+        ("active_state_type", 15, "string", 0), ("num_neg_samples", 16, "int32", 0),
+        ("output_max_index", 19, "bool", 0), ("norm_by_times", 25, "bool", 0), ("coeff", 26, "double", 0),
+        ("average_strategy", 27, "string", 0), ("error_clipping_threshold", 28, "double", 0),
+        ("operator_confs", 29, "OperatorConfig", 1), ("slope", 32, "double", 0), ("intercept", 33, "double", 0),
+        ("cos_scale", 34, "double", 0), ("beam_size", 39, "uint32", 0), ("select_first", 40, "bool", 0),
+        ("trans_type", 41, "string", 0), ("selective_fc_pass_generation", 42, "bool", 0),
+        ("has_selected_colums", 43, "bool", 0), ("selective_fc_full_mul_ratio", 44, "double", 0),
+        ("use_global_stats", 46, "bool", 0), ("moving_average_fraction", 47, "double", 0),
+        ("bias_size", 48, "uint32", 0), ("user_arg", 49, "string", 0), ("height", 50, "uint64", 0),
+        ("width", 51, "uint64", 0), ("blank", 52, "uint32", 0), ("seq_pool_stride", 53, "int32", 0),
+        ("axis", 54, "int32", 0), ("offset", 55, "uint32", 1), ("shape", 56, "uint32", 1),
+        ("delta", 57, "double", 0), ("depth", 58, "uint64", 0), ("epsilon", 60, "double", 0),
+        ("factor_size", 61, "uint32", 0)],
+    "EvaluatorConfig": [
+        ("name", 1, "string", 0), ("type", 2, "string", 0), ("input_layers", 3, "string", 1),
+        ("chunk_scheme", 4, "string", 0), ("num_chunk_types", 5, "int32", 0),
+        ("classification_threshold", 6, "double", 0), ("positive_label", 7, "int32", 0),
+        ("top_k", 13, "int32", 0)],
+    "LinkConfig": [("layer_name", 1, "string", 0), ("link_name", 2, "string", 0), ("has_subseq", 3, "bool", 0)],
+    "MemoryConfig": [
+        ("layer_name", 1, "string", 0), ("link_name", 2, "string", 0), ("boot_layer_name", 3, "string", 0),
+        ("boot_bias_parameter_name", 4, "string", 0), ("boot_bias_active_type", 5, "string", 0),
+        ("is_sequence", 6, "bool", 0), ("boot_with_const_id", 7, "uint32", 0)],
+    "SubModelConfig": [
+        ("name", 1, "string", 0), ("layer_names", 2, "string", 1), ("input_layer_names", 3, "string", 1),
+        ("output_layer_names", 4, "string", 1), ("evaluator_names", 5, "string", 1),
+        ("is_recurrent_layer_group", 6, "bool", 0), ("reversed", 7, "bool", 0),
+        ("memories", 8, "MemoryConfig", 1), ("in_links", 9, "LinkConfig", 1), ("out_links", 10, "LinkConfig", 1)],
+    "ModelConfig": [
+        ("type", 1, "string", 0), ("layers", 2, "LayerConfig", 1), ("parameters", 3, "ParameterConfig", 1),
+        ("input_layer_names", 4, "string", 1), ("output_layer_names", 5, "string", 1),
+        ("evaluators", 6, "EvaluatorConfig", 1), ("sub_models", 8, "SubModelConfig", 1)],
+    "OptimizationConfig": [
+        ("batch_size", 3, "int32", 0), ("algorithm", 4, "string", 0), ("learning_rate", 7, "double", 0),
+        ("learning_rate_decay_a", 8, "double", 0), ("learning_rate_decay_b", 9, "double", 0),
+        ("l1weight", 10, "double", 0), ("l2weight", 11, "double", 0), ("learning_method", 23, "string", 0),
+        ("ada_epsilon", 24, "double", 0), ("ada_rou", 26, "double", 0),
+        ("learning_rate_schedule", 27, "string", 0), ("adam_beta1", 33, "double", 0),
+        ("adam_beta2", 34, "double", 0), ("adam_epsilon", 35, "double", 0),
+        ("gradient_clipping_threshold", 38, "double", 0)],
+    "DataConfig": [
+        ("type", 1, "string", 0), ("files", 3, "string", 0), ("for_test", 14, "bool", 0),
+        ("load_data_module", 21, "string", 0), ("load_data_object", 22, "string", 0),
+        ("load_data_args", 23, "string", 0)],
+    "TrainerConfig": [
+        ("model_config", 1, "ModelConfig", 0), ("data_config", 2, "DataConfig", 0),
+        ("opt_config", 3, "OptimizationConfig", 0), ("test_data_config", 4, "DataConfig", 0),
+        ("config_files", 5, "string", 1), ("save_dir", 6, "string", 0), ("start_pass", 8, "int32", 0),
+        ("config_file", 9, "string", 0)],
+}
+_FIELDS = {m: {f[0]: f for f in fs} for m, fs in _S.items()}
+_BYNUM = {m: {f[1]: f for f in fs} for m, fs in _S.items()}
+_VARINT = {"int32", "int64", "uint32", "uint64", "bool"}
+
+
+# ---------------------------------------------------------------- wire codec
+def _varint(v):
+    v &= (1 << 64) - 1  # negative int32/int64: ten-byte two's complement
+    out = bytearray()
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        if v:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def _key(num, wt):
+    return _varint((num << 3) | wt)
+
+
+def encode(msg, d) -> bytes:
+    """Serialise dict ``d`` as message ``msg`` (fields in schema order; repeated
+    scalars unpacked, as proto2 does without [packed = true])."""
+    out = bytearray()
+    for name, num, kind, rep in _S[msg]:
+        if name not in d or d[name] is None:
+            continue
+        vals = d[name] if rep else [d[name]]
+        for v in vals:
+            if kind in _S:
+                b = encode(kind, v)
+                out += _key(num, 2) + _varint(len(b)) + b
+            elif kind == "string":
+                b = v.encode() if isinstance(v, str) else bytes(v)
+                out += _key(num, 2) + _varint(len(b)) + b
+            elif kind == "double":
+                out += _key(num, 1) + struct.pack("<d", float(v))
+            elif kind == "float":
+                out += _key(num, 5) + struct.pack("<f", float(v))
+            else:
+                out += _key(num, 0) + _varint(int(v))
+    return bytes(out)
+
+
+def _rvarint(buf, pos):
+    r = s = 0
+    while True:
+        b = buf[pos]
+        pos += 1
+        r |= (b & 0x7F) << s
+        s += 7
+        if not b & 0x80:
+            return r, pos
+
+
+def decode(msg, buf: bytes) -> dict:
+    d: dict = {}
+    pos, n = 0, len(buf)
+    while pos < n:
+        key, pos = _rvarint(buf, pos)
+        num, wt = key >> 3, key & 7
+        f = _BYNUM[msg].get(num)
+        if wt == 0:
+            raw, pos = _rvarint(buf, pos)
+        elif wt == 1:
+            raw, pos = buf[pos:pos + 8], pos + 8
+        elif wt == 5:
+            raw, pos = buf[pos:pos + 4], pos + 4
+        elif wt == 2:
+            ln, pos = _rvarint(buf, pos)
+            raw, pos = buf[pos:pos + ln], pos + ln
+        else:
+            raise ValueError(f"{msg}: unsupported wire type {wt}")
+        if f is None:
+            continue  # unknown field
+        name, _, kind, rep = f
+        if kind in _S:
+            v = decode(kind, raw)
+        elif kind == "string":
+            v = raw.decode()
+        elif kind == "double":
+            v = struct.unpack("<d", raw)[0]
+        elif kind == "float":
+            v = struct.unpack("<f", raw)[0]
+        elif wt == 2:  # packed repeated varints
+            vals, p = [], 0
+            while p < len(raw):
+                x, p = _rvarint(raw, p)
+                vals.append(x)
+            d.setdefault(name, []).extend(vals)
+            continue
+        elif kind == "bool":
+            v = bool(raw)
+        elif kind in ("int32", "int64") and raw >= 1 << 63:
+            v = raw - (1 << 64)
+        else:
+            v = raw
+        if rep:
+            d.setdefault(name, []).append(v)
+        else:
+            d[name] = v
+    return d
+
+
+# ---------------------------------------------------------------- text format
+def _fmt_scalar(kind, v):
+    if kind == "string":
+        return '"' + v.replace("\\", "\\\\").replace('"', '\\"') + '"'
+    if kind == "bool":
+        return "true" if v else "false"
+    if kind in ("double", "float"):
+        r = repr(float(v))
+        return r if ("e" in r or "." in r or "inf" in r or "nan" in r) else r + ".0"
+    return str(int(v))
+
+
+def to_text(msg, d, indent=0) -> str:
+    pad = "  " * indent
+    lines = []
+    for name, _, kind, rep in _S[msg]:
+        if name not in d or d[name] is None:
+            continue
+        for v in (d[name] if rep else [d[name]]):
+            if kind in _S:
+                lines.append(f"{pad}{name} {{")
+                lines.append(to_text(kind, v, indent + 1))
+                lines.append(f"{pad}}}")
+            else:
+                lines.append(f"{pad}{name}: {_fmt_scalar(kind, v)}")
+    return "\n".join(x for x in lines if x)
+
+
+_TOK = re.compile(r'\s*(?:(\{)|(\})|("(?:[^"\\]|\\.)*")|([A-Za-z_][\w.\-]*)\s*:|([^\s{}]+))')
+
+
+def from_text(msg, text) -> dict:
+    """Parse protobuf text format (as the reference's *.protostr files) into a dict."""
+    toks = []
+    pos = 0
+    while pos < len(text):
+        m = _TOK.match(text, pos)
+        if not m or m.end() == pos:
+            if text[pos:].strip() == "":
+                break
+            raise ValueError(f"text format: cannot parse at {text[pos:pos + 40]!r}")
+        pos = m.end()
+        toks.append(m.groups())
+    i = 0
+
+    def parse(mname):
+        nonlocal i
+        d = {}
+        while i < len(toks):
+            ob, cb, st, key, bare = toks[i]
+            if cb:
+                i += 1
+                return d
+            if key is None and bare is not None:  # "name {" has no colon
+                key = bare
+            i += 1
+            f = _FIELDS[mname].get(key)
+            if f is None and i < len(toks) and toks[i][0]:  # unknown message field: skip its block
+                depth = 0
+                while True:
+                    depth += 1 if toks[i][0] else -1 if toks[i][1] else 0
+                    i += 1
+                    if depth == 0:
+                        break
+                continue
+            if f is not None and f[2] in _S:
+                if toks[i][0]:  # "{"
+                    i += 1
+                v = parse(f[2])
+            else:
+                _, _, vs, _, vb = toks[i]
+                i += 1
+                v = vs if vs is not None else vb
+                if f is None:
+                    continue
+                kind = f[2]
+                if kind == "string":
+                    v = bytes(v[1:-1], "utf-8").decode("unicode_escape")
+                elif kind == "bool":
+                    v = v == "true"
+                elif kind in ("double", "float"):
+                    v = float(v)
+                else:
+                    v = int(v)
+            if f is None:
+                continue
+            if f[3]:
+                d.setdefault(key, []).append(v)
+            else:
+                d[key] = v
+        return d
+
+    return parse(msg)
+
+
+# ---------------------------------------------------------------- recording
+# default-name prefixes (reference layers.py @wrap_name_default(...); None = the
+# function name) and LayerConfig types of the DSL functions
+_PREFIX = {
+    "mixed_layer": "mixed", "embedding_layer": "embedding", "printer_layer": "print", "priorbox_layer": "priorbox",
+    "multibox_loss_layer": "multibox_loss", "detection_output_layer": "detection_output",
+    "roi_pool_layer": "roi_pool", "cross_channel_norm_layer": "cross_channel_norm", "pooling_layer": "seq_pooling",
+    "lstmemory": "lstmemory", "grumemory": "gru", "seq_reshape_layer": "seqreshape", "img_conv_layer": "conv",
+    "img_pool_layer": "pool", "img_pool3d_layer": "pool3d", "upsample_layer": "upsample", "spp_layer": "spp",
+    "img_cmrnorm_layer": "crmnorm", "batch_norm_layer": "batch_norm", "addto_layer": "addto",
+    "concat_layer": "concat", "seq_concat_layer": "seqconcat", "lstm_step_layer": "lstm_step",
+    "gru_step_layer": "gru_step", "gru_step_naive_layer": "gru_step_naive", "recurrent_group": "recurrent_group",
+    "classification_cost": "cost", "pad_layer": "pad", "dropout_layer": "dropout", "switch_order_layer": "switch_order",
+    "clip_layer": "clip", "img_conv3d_layer": "conv3d", "scale_shift_layer": "scale_shift", "resize_layer": "resize",
+    "sub_seq_layer": "sub_seq", "scale_sub_region_layer": "scale_sub_region",
+}
+_TYPE = {
+    "data_layer": "data", "fc_layer": "fc", "printer_layer": "print", "priorbox_layer": "priorbox",
+    "multibox_loss_layer": "multibox_loss", "detection_output_layer": "detection_output", "roi_pool_layer": "roi_pool",
+    "cross_channel_norm_layer": "norm", "lstmemory": "lstmemory", "grumemory": "gated_recurrent",
+    "last_seq": "seqlastins", "first_seq": "seqlastins", "expand_layer": "expand", "repeat_layer": "featmap_expand",
+    "seq_reshape_layer": "seqreshape", "interpolation_layer": "interpolation", "bilinear_interp_layer": "bilinear_interp",
+    "power_layer": "power", "scaling_layer": "scaling", "trans_layer": "trans", "rotate_layer": "rotate",
+    "cos_sim": "cos", "l2_distance_layer": "l2_distance", "hsigmoid": "hsigmoid", "img_conv_layer": "exconv",
+    "img_pool_layer": "pool", "img_pool3d_layer": "pool3d", "upsample_layer": "upsample", "spp_layer": "spp",
+    "img_cmrnorm_layer": "norm", "batch_norm_layer": "batch_norm", "sum_to_one_norm_layer": "sum_to_one_norm",
+    "row_l2_norm_layer": "row_l2_norm", "addto_layer": "addto", "concat_layer": "concat",
+    "seq_concat_layer": "seqconcat", "lstm_step_layer": "lstm_step", "gru_step_layer": "gru_step",
+    "get_output_layer": "get_output", "recurrent_layer": "recurrent", "maxid_layer": "maxid",
+    "dot_prod_layer": "dot_prod", "out_prod_layer": "out_prod", "eos_layer": "eos_id", "square_error_cost": "square_error",
+    "regression_cost": "square_error", "mse_cost": "square_error", "classification_cost": "multi-class-cross-entropy",
+    "pad_layer": "pad", "conv_shift_layer": "conv_shift", "tensor_layer": "tensor", "selective_fc_layer": "selective_fc",
+    "sampling_id_layer": "sampling_id", "slope_intercept_layer": "slope_intercept", "linear_comb_layer": "convex_comb",
+    "block_expand_layer": "blockexpand", "maxout_layer": "maxout", "ctc_layer": "ctc", "warp_ctc_layer": "warp_ctc",
+    "crf_layer": "crf", "crf_decoding_layer": "crf_decoding", "nce_layer": "nce", "rank_cost": "rank-cost",
+    "lambda_cost": "lambda_cost", "cross_entropy": "multi-class-cross-entropy",
+    "cross_entropy_with_selfnorm": "multi_class_cross_entropy_with_selfnorm", "sum_cost": "sum_cost",
+    "huber_regression_cost": "huber_regression", "huber_classification_cost": "huber_classification",
+    "multi_binary_label_cross_entropy": "multi_binary_label_cross_entropy",
+    "cross_entropy_over_beam": "cross_entropy_over_beam", "smooth_l1_cost": "smooth_l1",
+    "multiplex_layer": "multiplex", "row_conv_layer": "row_conv", "prelu_layer": "prelu",
+    "switch_order_layer": "switch_order", "crop_layer": "crop", "sub_nested_seq_layer": "sub_nested_seq",
+    "clip_layer": "clip", "seq_slice_layer": "seq_slice", "kmax_seq_score_layer": "kmax_seq_score",
+    "img_conv3d_layer": "conv3d", "scale_shift_layer": "scale_shift", "resize_layer": "resize",
+    "sub_seq_layer": "subseq", "scale_sub_region_layer": "scale_sub_region",
+    "factorization_machine": "factorization_machine", "pooling_layer": "max", "mixed_layer": "mixed",
+    "embedding_layer": "mixed", "dropout_layer": "addto", "memory": "agent",
+}
+_ACT = {None: "", "linear": "", "identity": "", "exp": "exponential", "soft_relu": "softrelu"}
+# layers whose size is their input's (the reference sets size = input.size)
+_SAME_SIZE = {"trans_layer", "first_seq", "last_seq", "dropout_layer", "batch_norm_layer", "clip_layer",
+              "row_l2_norm_layer", "sum_to_one_norm_layer", "scaling_layer", "slope_intercept_layer",
+              "power_layer", "rotate_layer", "prelu_layer", "pooling_layer", "addto_layer", "expand_layer"}
+# functions that are not layers (projections / operators feed mixed / concat layers)
+_NOT_LAYERS = {"settings", "outputs", "get_config_arg", "define_py_data_sources2", "parse_config"}
+
+
+class Recorder:
+    """Per-parse state: LayerConfigs, ParameterConfigs and the variable -> layer map."""
+
+    def __init__(self):
+        self.layers = []
+        self.params = []
+        self.param_map = {}  # v1 parameter name -> Fluid parameter name
+        self.of_var = {}      # id(fluid Variable) -> layer name
+        self.vars = []        # keeps the recorded Variables alive (ids stay unique)
+        self.count = {}
+        self.inputs = []
+        self.outputs = []
+        self.depth = 0
+
+    def name_for(self, fn, given):
+        if given:
+            return given
+        pre = _PREFIX.get(fn, fn)
+        i = self.count.get(pre, 0)
+        self.count[pre] = i + 1
+        return f"__{pre}_{i}__"
+
+    def layer_name(self, v):
+        return self.of_var.get(id(v))
+
+
+_REC: list = []
+
+
+def start():
+    _REC[:] = [Recorder()]
+    return _REC[0]
+
+
+def current():
+    return _REC[0] if _REC else None
+
+
+def _vsize(v):
+    s = getattr(v, "v2_size", None)
+    if s is None:
+        sh = getattr(v, "shape", None)
+        s = int(sh[-1]) if sh else None
+    return s
+
+
+def _is_var(x):
+    return hasattr(x, "block") and hasattr(x, "name") and hasattr(x, "shape")
+
+
+def _flat_inputs(fn, args, kw):
+    """Layer inputs in signature order: Variables and projections (with .input)."""
+    try:
+        ba = inspect.signature(fn).bind_partial(*args, **kw)
+        items = [(k, v) for k, v in ba.arguments.items() if k not in ("name", "act", "size", "param_attr",
+                                                                       "bias_attr", "layer_attr")]
+    except (TypeError, ValueError):
+        items = [(None, a) for a in args] + list(kw.items())
+    out = []
+    for _, v in items:
+        for x in (v if isinstance(v, (list, tuple)) else [v]):
+            if _is_var(x):
+                out.append((x, None))
+            elif _is_var(getattr(x, "input", None)):
+                out.append((x.input, x))  # a projection / operator
+    return out
+
+
+def _param_dims(p):
+    return [int(d) for d in p.shape]
+
+
+def recorded(fn_name, fn):
+    """Wrap a DSL layer function so a call at config level records its LayerConfig."""
+
+    def wrapper(*args, **kw):
+        rec = current()
+        if rec is None or rec.depth:
+            return fn(*args, **kw)
+        from ..v2._core import STATE
+
+        blk = STATE["main"].global_block()
+        before = {p.name for p in blk.all_parameters()}
+        rec.depth += 1
+        try:
+            out = fn(*args, **kw)
+        finally:
+            rec.depth -= 1
+        new = [p for p in blk.all_parameters() if p.name not in before]
+        outs = out if isinstance(out, (list, tuple)) else [out]
+        if not outs or not _is_var(outs[0]):
+            return out
+        v = outs[0]
+        name = rec.name_for(fn_name, kw.get("name") if fn_name != "data_layer" else (kw.get("name") or args[0]))
+        ins = _flat_inputs(fn, args, kw)
+        typ = _TYPE.get(fn_name, fn_name.replace("_layer", ""))
+        act = kw.get("act")
+        from ..v2.activation import act_name
+
+        an = act_name(act) if act is not None else ("tanh" if fn_name in ("fc_layer", "selective_fc_layer") else None)
+        size = kw.get("size") if isinstance(kw.get("size"), int) else None
+        if fn_name == "data_layer":
+            size = kw.get("size", args[1] if len(args) > 1 else None)
+        if fn_name in _SAME_SIZE and ins:
+            size = _vsize(ins[0][0])
+        if fn_name == "concat_layer":
+            size = sum(_vsize(x) or 0 for x, _ in ins)
+        if size is None:
+            size = _vsize(v)
+        lc = {"name": name, "type": typ, "size": size, "active_type": _ACT.get(an, an or "")}
+        weights = [p for p in new if len(p.shape) >= 2 and not getattr(p, "_v1_bias", False)]
+        wn = {p.name for p in weights}
+        biases = [p for p in new if p.name not in wn]
+        layer_inputs = []
+        projs = any(pr is not None for _, pr in ins)
+        if fn_name == "concat_layer" and projs:
+            lc["type"] = "concat2"
+        for i, (x, pr) in enumerate(ins):
+            li = {"input_layer_name": rec.layer_name(x) or x.name}
+            if pr is not None and fn_name == "concat_layer":
+                li["proj_conf"] = {"type": getattr(pr, "v1_type", "identity"), "name": f"_{name}.w{i}",
+                                   "input_size": _vsize(x), "output_size": _vsize(x)}
+            if i < len(weights):
+                pname = f"_{name}.w{i}"
+                li["input_parameter_name"] = pname
+                rec.param_map[pname] = weights[i].name
+                dims = _param_dims(weights[i])
+                rec.params.append({"name": pname, "size": int(_prod(dims)), "initial_mean": 0.0,
+                                   "initial_std": 1.0 / max(dims[0], 1) ** 0.5, "dims": dims,
+                                   "initial_strategy": 0, "initial_smart": True})
+            layer_inputs.append(li)
+        if layer_inputs:
+            lc["inputs"] = layer_inputs
+        if biases:
+            pname = f"_{name}.wbias"
+            lc["bias_parameter_name"] = pname
+            rec.param_map[pname] = biases[0].name
+            n = int(_prod(_param_dims(biases[0])))
+            rec.params.append({"name": pname, "size": n, "initial_mean": 0.0, "initial_std": 0.0, "dims": [1, n],
+                               "initial_strategy": 0, "initial_smart": False})
+        if fn_name == "data_layer":
+            rec.inputs.append(name)
+        rec.layers.append(lc)
+        rec.of_var[id(v)] = name
+        rec.vars.append(v)
+        return out
+
+    wrapper.__name__ = fn.__name__
+    wrapper.__doc__ = fn.__doc__
+    wrapper.__wrapped__ = fn
+    return wrapper
+
+
+def _prod(xs):
+    r = 1
+    for x in xs:
+        r *= int(x)
+    return r
+
+
+def model_config(rec, outputs):
+    out_names = [rec.layer_name(o) or getattr(o, "name", str(o)) for o in outputs]
+    names = [lc["name"] for lc in rec.layers]
+    return {"type": "nn", "layers": rec.layers, "parameters": rec.params, "input_layer_names": rec.inputs,
+            "output_layer_names": out_names,
+            "sub_models": [{"name": "root", "layer_names": names, "input_layer_names": rec.inputs,
+                            "output_layer_names": out_names, "is_recurrent_layer_group": False}]}
+
+
+_METHOD = {"Momentum": "momentum", "Adam": "adam", "Adamax": "adamax", "AdaGrad": "adagrad",
+           "DecayedAdaGrad": "decayed_adagrad", "AdaDelta": "adadelta", "RMSProp": "rmsprop"}
+
+
+def opt_config(cfg):
+    m = cfg.get("learning_method")
+    kind = getattr(getattr(m, "kind", None), "__name__", "Momentum")
+    oc = {"batch_size": int(cfg.get("batch_size") or 1), "algorithm": "sgd",
+          "learning_rate": float(cfg.get("learning_rate") or 1e-3), "learning_method": _METHOD.get(kind, "momentum")}
+    kw = getattr(m, "kw", {}) or {}
+    if kind == "Adam":
+        oc.update(adam_beta1=kw.get("beta1", 0.9), adam_beta2=kw.get("beta2", 0.999),
+                  adam_epsilon=kw.get("epsilon", 1e-8))
+    reg = cfg.get("regularization")
+    rate = getattr(reg, "rate", None) or getattr(reg, "regularization_coeff", None)
+    if rate:
+        oc["l2weight"] = float(rate)
+    if cfg.get("gradient_clipping_threshold"):
+        oc["gradient_clipping_threshold"] = float(cfg["gradient_clipping_threshold"])
+    return oc
+
+
+def data_configs(cfg):
+    src = cfg.get("data_sources")
+    if not src:
+        return None, None
+    train, test, module, obj, args = (src["train_list"], src["test_list"], src["module"], src["obj"],
+                                      src.get("args"))
+
+    def dc(files, for_test):
+        if not files:
+            return None
+        return {"type": "py2", "files": files, "for_test": for_test, "load_data_module": module,
+                "load_data_object": obj, "load_data_args": "" if args is None else str(args)}
+
+    return dc(train, False), dc(test, True)

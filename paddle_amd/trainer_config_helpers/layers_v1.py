@@ -111,8 +111,9 @@ def layer_support(*attrs):
 class _Projection:
     """A deferred term of a mixed layer: ``build(size)`` emits its ops."""
 
-    def __init__(self, fn, size=None):
+    def __init__(self, fn, size=None, input=None, kind=None):
         self.fn, self.size = fn, size
+        self.input, self.v1_type = input, kind  # for the ModelConfig record (config_proto.py)
 
     def build(self, size):
         return self.fn(size if self.size is None else self.size)
@@ -120,7 +121,7 @@ class _Projection:
 
 @_export
 def full_matrix_projection(input, size=0, param_attr=None):
-    return _Projection(lambda s: _L().fc(input=input, size=s, bias_attr=False), size or None)
+    return _Projection(lambda s: _L().fc(input=input, size=s, bias_attr=False), size or None, input, "fc")
 
 
 @_export
@@ -130,7 +131,7 @@ def trans_full_matrix_projection(input, size=0, param_attr=None):
         helper = LayerHelper("trans_fc")
         w = helper.create_parameter(attr=helper.param_attr, shape=[s, _size(input)], dtype="float32")
         return _L().matmul(input, w, transpose_y=True)
-    return _Projection(build, size or None)
+    return _Projection(build, size or None, input, "trans_fc")
 
 
 @_export
@@ -138,14 +139,15 @@ def table_projection(input, size=0, param_attr=None):
     from ..v2._core import STATE
 
     vocab = STATE["data"][input.name].dim
-    return _Projection(lambda s: _L().embedding(input=input, size=[vocab, s]), size or None)
+    return _Projection(lambda s: _L().embedding(input=input, size=[vocab, s]), size or None, input, "table")
 
 
 @_export
 def identity_projection(input, offset=None, size=None):
     if offset is None:
-        return _Projection(lambda s: input, _size(input))
-    return _Projection(lambda s: _L().slice(input, axes=[1], starts=[offset], ends=[offset + s]), size)
+        return _Projection(lambda s: input, _size(input), input, "identity")
+    return _Projection(lambda s: _L().slice(input, axes=[1], starts=[offset], ends=[offset + s]), size, input,
+                       "identity_offset")
 
 
 @_export
@@ -153,7 +155,7 @@ def slice_projection(input, slices):
     def build(s):
         parts = [_L().slice(input, axes=[1], starts=[a], ends=[b]) for a, b in slices]
         return parts[0] if len(parts) == 1 else _L().concat(parts, axis=1)
-    return _Projection(build, sum(b - a for a, b in slices))
+    return _Projection(build, sum(b - a for a, b in slices), input, "slice")
 
 
 @_export
@@ -162,7 +164,7 @@ def dotmul_projection(input, param_attr=None):
         helper = LayerHelper("dotmul")
         w = helper.create_parameter(attr=helper.param_attr, shape=[_size(input)], dtype="float32")
         return _L().elementwise_mul(input, w, axis=1)
-    return _Projection(build, _size(input))
+    return _Projection(build, _size(input), input, "dot_mul")
 
 
 @_export
@@ -171,7 +173,7 @@ def scaling_projection(input, param_attr=None):
         helper = LayerHelper("scaling")
         w = helper.create_parameter(attr=helper.param_attr, shape=[1], dtype="float32")
         return _L().elementwise_mul(input, w)
-    return _Projection(build, _size(input))
+    return _Projection(build, _size(input), input, "scaling")
 
 
 @_export
@@ -201,7 +203,7 @@ def context_projection(input, context_len, context_start=None, padding_attr=Fals
         helper.append_op(type="sequence_conv", inputs={"X": [input], "Filter": [w]}, outputs={"Out": [out]},
                          attrs={"contextStride": 1, "contextStart": start, "contextLength": context_len})
         return out
-    return _Projection(build, context_len * _size(input))
+    return _Projection(build, context_len * _size(input), input, "context")
 
 
 @_export
@@ -212,7 +214,7 @@ def conv_projection(input, filter_size, num_filters, num_channels=None, stride=1
     def build(s):
         return _L().conv2d(_as_image(input, num_channels or 1), num_filters=num_filters, filter_size=filter_size,
                            stride=stride, padding=padding, groups=groups, bias_attr=False)
-    return _Projection(build, None)
+    return _Projection(build, None, input, "conv")
 
 
 conv_operator = conv_projection
@@ -734,8 +736,15 @@ def resize_layer(input, size, name=None):
 
 @_export
 def trans_layer(input, name=None, **kw):
+    """The minibatch matrix transposed ([N, size] -> [size, N]).  Like the reference
+    (size = the input's size) a following layer sees rows of the input's width, so
+    the declared shape keeps it: a consumer's weights are sized as if N == size."""
     with guard():
-        return _named(_L().transpose(input, perm=[1, 0]), name)
+        out = _L().transpose(input, perm=[1, 0])
+        w = _size(input)
+        if w:
+            out.shape = (-1, w)
+        return _named(_sized(out, w), name)
 
 
 @_export

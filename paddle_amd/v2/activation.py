@@ -20,7 +20,7 @@ Exp = _act("exp")
 Abs = _act("abs")
 Square = _act("square")
 BRelu = _act("brelu")
-SoftRelu = _act("softrelu")
+SoftRelu = _act("soft_relu")
 STanh = _act("stanh")
 
 

@@ -110,7 +110,9 @@ def test_recurrent_group_memory_matches_manual_rnn():
     got, scope = _run(build, feed)
     params = STATE["main"].global_block().all_parameters()
     vals = {p.name: np.array(scope.find_var(p.name).get_tensor()) for p in params}
-    W = next(v for v in vals.values() if v.shape == (7, 3))
+    # fc over [x_t, h_{t-1}]: one weight per input (w0 [4, 3], w1 [3, 3]), as v1
+    W = np.concatenate([next(v for v in vals.values() if v.shape == (4, 3)),
+                        next(v for v in vals.values() if v.shape == (3, 3))], 0)
     b = next((v for v in vals.values() if v.shape in ((3,), (1, 3))), np.zeros(3, "float32")).reshape(-1)
     exp, o = [], 0
     for n in lens:
