@@ -115,6 +115,32 @@ __device__ __forceinline__ float block_max(float v, float* red) {
   return t;
 }
 
+// BatchNorm backward statistics taken in the epilogue of the convolution whose data
+// gradient dY' is the gradient of the BN output y = relu(BN(x) [+ res]):
+//   part[tile][0][c] = sum g,  part[tile][1][c] = sum g * (x - mean),  g = dY' * mask
+// mask: y > 0 (residual layers, y kept), fmaf(x, rstd*w, b - mean*rstd*w) > 0 (relu,
+// recomputed as the forward evaluated it), or 1 (no relu) -- what bn_reduce_kernel<true>
+// computes, so the BN backward skips its reduction pass over dY and x.
+struct BnBwdSrc {
+  const u16* x;       // BN input [rows, C] (null: statistics off)
+  const u16* y;       // BN output (mask source) or null
+  const float* mean;  // [C]
+  const float* rstd;  // [C]
+  const void* w;      // [C] fp32 / bf16 per wdt, or null (1)
+  const void* b;      // [C] or null (0)
+  int wdt;
+  int relu;
+};
+
+// per-channel (mean, mask scale, mask shift) of channel c
+__device__ __forceinline__ void bn_bwd_coef(const BnBwdSrc& s, int c, float& mean, float& sc, float& sf) {
+  mean = s.mean[c];
+  const float ww = s.w ? (s.wdt ? bf2f(((const u16*)s.w)[c]) : ((const float*)s.w)[c]) : 1.f;
+  const float bb = s.b ? (s.wdt ? bf2f(((const u16*)s.b)[c]) : ((const float*)s.b)[c]) : 0.f;
+  sc = s.rstd[c] * ww;
+  sf = bb - mean * sc;
+}
+
 // Grid size for memory-bound grid-stride kernels (guide Guideline 11).
 static inline int stream_grid(long work_items, int block) {
   long g = (work_items + block - 1) / block;

@@ -657,6 +657,24 @@ PA_EXPORT int pa_bn_bwd2(const void* x, const void* dy, const void* y, const flo
   PA_LAUNCH_CHECK();
 }
 
+// pa_bn_bwd2 with the reduction already done: part [G][2][C] of sum dy', sum dy' (x - mean)
+// emitted by the epilogue of the convolution that produced dy (pa_conv_sn_bnbwd /
+// pa_conv_gemm_bnbwd), so only the finalize and the dx pass run.
+PA_EXPORT int pa_bn_bwd_part(const float* part, int G, const void* x, const void* dy, const void* y,
+                             const float* mean, const float* rstd, const void* w, const void* b, int wdt, void* dx,
+                             float* dw, float* db, float* coef, long rows, int C, int relu, void* dres,
+                             hipStream_t st) {
+  if (C % 8 || G <= 0) return -1;
+  const BnMask mk{(const u16*)y, rstd, w, b, wdt};
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 15) / 16), dim3(1024), 0, st, part, G, C, rows, rstd, w, wdt,
+                     dw, db, coef);
+  int eg, eb;
+  bn_ew_launch(rows, C, eg, eb);
+  hipLaunchKernelGGL(bn_dx_kernel, dim3(eg), dim3(eb), 0, st, (const u16*)x, (const u16*)dy, mk, mean, coef,
+                     (u16*)dx, rows, C, relu, (u16*)dres);
+  PA_LAUNCH_CHECK();
+}
+
 PA_EXPORT int pa_bn_bwd(const void* x, const void* dy, const void* y, const float* mean, const float* rstd,
                         const void* w, int wdt, void* dx, float* dw, float* db, float* coef, float* part, long rows,
                         int C, int relu, void* dres, hipStream_t st) {

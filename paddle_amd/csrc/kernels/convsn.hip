@@ -24,6 +24,9 @@
 //    ROUNDED outputs (shifted by `shift`, e.g. the running mean) and of their
 //    squares: part[tile_m][0 / 1][c] -- the layout bn_finalize reduces, so the
 //    BatchNorm that consumes this output skips its statistics pass over HBM.
+//    STATS == 2 (data gradient of a BN output): the BN backward's sums instead,
+//    sum g and sum g (x - mean) with g = the stored gradient under the ReLU mask
+//    (common.h BnBwdSrc), taken after an accumulate-into so they cover the final sum.
 //  * blockIdx -> tile is XCD-aware (contiguous tile ranges per XCD): neighbouring
 //    pixel tiles share their 3x3 halo rows in the same L2.
 //
@@ -53,6 +56,7 @@ struct Params {
   int H, W, C, OH, OW, KW, sy, sx, py, px, dy, dx, uy, ux;
   int tiles_m, tiles_n;
   int accumulate;  // y += result (bf16 read-modify-write; a gradient accumulated in place)
+  BnBwdSrc bs;     // STATS == 2: BatchNorm backward statistics of y (a data gradient)
 };
 
 // Physical placement of piece q (1 KiB = 8 rows x 128 B) of an operand: rows
@@ -85,7 +89,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-template <bool STATS>
+template <int STATS>
 __global__ __launch_bounds__(NT, 2) void conv_sn_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -192,13 +196,43 @@ __global__ __launch_bounds__(NT, 2) void conv_sn_kernel(Params p) {
     for (int r = 0; r < 4; ++r) {
       const int n = n0 + 16 * j + 4 * g + r;
       bv[j][r] = (p.bias && n < p.Cout) ? bf2f(p.bias[n]) : 0.f;
-      sh[j][r] = (STATS && p.shift && n < p.Cout) ? p.shift[n] : 0.f;
+      sh[j][r] = (STATS == 1 && p.shift && n < p.Cout) ? p.shift[n] : 0.f;
     }
+  float msc[4][4], msf[4][4];
+  if constexpr (STATS == 2) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + 16 * j + 4 * g + r;
+        if (n < p.Cout) {
+          bn_bwd_coef(p.bs, n, sh[j][r], msc[j][r], msf[j][r]);
+        } else {
+          sh[j][r] = msc[j][r] = msf[j][r] = 0.f;
+        }
+      }
+  }
   float s1[4][4], s2[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
+  // STATS == 2: every BN input / output chunk of the wave's rows is loaded before the
+  // first store (the compiler cannot move loads across stores to y)
+  u16x4 bxa[4][4], bya[4][4];
+  if constexpr (STATS == 2) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + 64 * wid + 16 * i + ml;
+        const int n = n0 + 16 * j + 4 * g;
+        const bool ok = m < p.M && n < p.Cout;
+        bxa[i][j] = ok ? *reinterpret_cast<const u16x4*>(p.bs.x + (long)m * p.Cout + n) : u16x4{0, 0, 0, 0};
+        bya[i][j] = (ok && p.bs.y) ? *reinterpret_cast<const u16x4*>(p.bs.y + (long)m * p.Cout + n)
+                                   : u16x4{0, 0, 0, 0};
+      }
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + 64 * wid + 16 * i + ml;
@@ -210,19 +244,30 @@ __global__ __launch_bounds__(NT, 2) void conv_sn_kernel(Params p) {
       u16x4 old = {0, 0, 0, 0};
       if (p.accumulate && ok) old = *reinterpret_cast<const u16x4*>(p.y + (long)m * p.Cout + n);
       u16x4 o;
+      u16x4 bx = {0, 0, 0, 0}, by = {0, 0, 0, 0};
+      if constexpr (STATS == 2) {
+        bx = bxa[i][j];
+        by = bya[i][j];
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         o[r] = f2bf(acc[i][j][r] + bv[j][r] + (p.accumulate ? bf2f(old[r]) : 0.f));
-        if (STATS) {
+        if (STATS == 1) {
           const float d = mok ? bf2f(o[r]) - sh[j][r] : 0.f;
           s1[j][r] += d;
           s2[j][r] += d * d;
+        } else if (STATS == 2) {
+          const float xv = bf2f(bx[r]);
+          const bool keep = !p.bs.relu || (p.bs.y ? bf2f(by[r]) > 0.f : fmaf(xv, msc[j][r], msf[j][r]) > 0.f);
+          const float gv = (ok && keep) ? bf2f(o[r]) : 0.f;
+          s1[j][r] += gv;
+          s2[j][r] += gv * (xv - sh[j][r]);
         }
       }
       if (ok) *reinterpret_cast<u16x4*>(p.y + (long)m * p.Cout + n) = o;
     }
   }
-  if constexpr (STATS) {
+  if constexpr (STATS != 0) {
     __syncthreads();  // every wave is done with the stage buffers
     float* red = reinterpret_cast<float*>(smem);  // [4 waves][64 channels][2]
 #pragma unroll
@@ -251,7 +296,7 @@ __global__ __launch_bounds__(NT, 2) void conv_sn_kernel(Params p) {
   }
 }
 
-template <bool STATS>
+template <int STATS>
 static int launch(const Params& p, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
@@ -496,7 +541,36 @@ PA_EXPORT int pa_conv_sn_acc(const void* src, const void* wt, void* out, const v
   p.tiles_n = (Cout + convsn::BNC - 1) / convsn::BNC;
   p.accumulate = accumulate;
   if (accumulate && part) return -1;
-  return part ? convsn::launch<true>(p, st) : convsn::launch<false>(p, st);
+  return part ? convsn::launch<1>(p, st) : convsn::launch<0>(p, st);
+}
+
+// Data gradient with the BatchNorm backward statistics of its (final, after an
+// optional accumulate-into) values: part [tiles_m][2][Cout] of sum g, sum g (x - mean)
+// (see BnBwdSrc); bx / by: BN input / output [M, Cout], by null = mask from bx.
+PA_EXPORT int pa_conv_sn_bnbwd(const void* src, const void* wt, void* out, int Nb, int H, int W, int C, int OH, int OW,
+                               int Cout, int KH, int KW, int sy, int sx, int py, int px, int dy, int dx, int uy, int ux,
+                               int accumulate, float* part, const void* bx, const void* by, const float* mean,
+                               const float* rstd, const void* w, const void* b, int wdt, int relu, hipStream_t st) {
+  const long M = (long)Nb * OH * OW;
+  if (M <= 0 || Cout <= 0 || !part || !bx || !mean || !rstd) return -1;
+  if (C % 64 || Cout % 8 || M > 0x7fffffffL || (long)Nb * H * W * C >= 0x7fffffffL || H > 32767 || W > 32767 ||
+      (long)Cout * KH * KW * C >= 0x7fffffffL)
+    return -1;
+  convsn::Params p{};
+  p.x = (const u16*)src;
+  p.w = (const u16*)wt;
+  p.y = (u16*)out;
+  p.part = part;
+  p.M = (int)M;
+  p.Cout = Cout;
+  p.K = KH * KW * C;
+  p.H = H; p.W = W; p.C = C; p.OH = OH; p.OW = OW; p.KW = KW;
+  p.sy = sy; p.sx = sx; p.py = py; p.px = px; p.dy = dy; p.dx = dx; p.uy = uy; p.ux = ux;
+  p.tiles_m = (int)((M + convsn::BM - 1) / convsn::BM);
+  p.tiles_n = (Cout + convsn::BNC - 1) / convsn::BNC;
+  p.accumulate = accumulate;
+  p.bs = BnBwdSrc{(const u16*)bx, (const u16*)by, mean, rstd, w, b, wdt, relu};
+  return convsn::launch<2>(p, st);
 }
 
 PA_EXPORT int pa_conv_sn_tiles(long M) { return (int)((M + convsn::BM - 1) / convsn::BM); }

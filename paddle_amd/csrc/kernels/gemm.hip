@@ -85,6 +85,9 @@ struct Params {
   // output about `shift` (nullable) into part[tile_m][0 / 1][N] (sum, sum of squares)
   float* part;
   const float* shift;
+  // GA conv kernels, bf16 out, bs.x != null: the BatchNorm BACKWARD statistics of the
+  // stored gradient instead (sum g, sum g (x - mean); common.h BnBwdSrc), into part
+  BnBwdSrc bs;
 };
 
 // LDS image of one operand of one stage: 4 "slabs" of 64 mn x 64 k (8 KiB each);
@@ -355,7 +358,8 @@ __device__ __forceinline__ void quad_mma(f32x4 (&acc)[8][4], const FA (&fa)[4][2
   }
 }
 
-template <bool AK, bool BK, bool OUTF32, bool PF_IN_CLUSTER, bool KFULL, bool GA = false, bool F8 = false, int GM = 0>
+template <bool AK, bool BK, bool OUTF32, bool PF_IN_CLUSTER, bool KFULL, bool GA = false, bool F8 = false, int GM = 0,
+          bool BNB = false>
 __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -775,13 +779,23 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   // accumulated from the staged 16-B chunks this thread stores (8 channels, fixed per
   // thread), then reduced over the 16 threads of a channel chunk through LDS
   const bool stats = GA && !OUTF32 && p.part != nullptr;
-  float st1[8], st2[8], shc[8];
+  const bool bstats = BNB && stats;  // BNB kernels: BN backward statistics (p.bs)
+  float st1[8], st2[8], shc[8], msc[8], msf[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     st1[e] = st2[e] = 0.f;
     const int n = n0 + (tid % CPR) * 8 + e;
-    shc[e] = (stats && p.shift && n < p.N) ? p.shift[n] : 0.f;
+    shc[e] = msc[e] = msf[e] = 0.f;
+    if (bstats && n < p.N)
+      bn_bwd_coef(p.bs, n, shc[e], msc[e], msf[e]);
+    else if (stats && p.shift && n < p.N)
+      shc[e] = p.shift[n];
   }
+  const long tile_off = (cz + (erow0 + m0) * p.ldc + n0) * 2;
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(
+      (char*)p.bs.x + (bstats ? tile_off : 0), 0, (int)OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc(
+      (char*)p.bs.y + (bstats && p.bs.y ? tile_off : 0), 0, (int)OOB, 0x00020000);
 #pragma unroll
   for (int ps = 0; ps < PASSES; ++ps) {
     // (a) fragments -> LDS (staged row = GR * wr + 16 * ii + ml)
@@ -832,13 +846,23 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
     // Loads and stores are buffer ops on the per-tile descriptor with masked lanes
     // sent out of range (load 0 / store dropped): uniform control flow, so hipcc
     // counts its vmcnt waits instead of falling back to vmcnt(0) at every store.
-    constexpr int HB = F8 ? 2 : NIT / 2;  // F8 epilogues also hold the column scales
+    constexpr int HB = (F8 || BNB) ? 2 : NIT / 2;  // F8 / BNB epilogues also hold column scales / x, y chunks
 #pragma unroll 1
     for (int h = 0; h < NIT; h += HB) {
       u32x4 cold[HB];
       if (acc_rd) {
 #pragma unroll
         for (int u = 0; u < HB; ++u) cold[u] = __builtin_amdgcn_raw_buffer_load_b128(rsC, C_OFF(h + u, ps), 0, 0);
+      }
+      u32x4 xo[HB], yo[HB];
+      if constexpr (BNB && GA && !OUTF32) {
+        if (bstats) {
+#pragma unroll
+          for (int u = 0; u < HB; ++u) {
+            xo[u] = __builtin_amdgcn_raw_buffer_load_b128(rsX, C_OFF(h + u, ps), 0, 0);
+            yo[u] = p.bs.y ? __builtin_amdgcn_raw_buffer_load_b128(rsY, C_OFF(h + u, ps), 0, 0) : u32x4{0, 0, 0, 0};
+          }
+        }
       }
 #pragma unroll
       for (int u = 0; u < HB; ++u) {
@@ -847,7 +871,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
         const f32x4 v = *reinterpret_cast<const f32x4*>(stg + rr * ROWB + ch * 16);
         u32x4 w = __builtin_bit_cast(u32x4, v);
         if constexpr (GA && !OUTF32) {
-          if (stats && C_OFF(it, ps) != OOB) {
+          if (stats && !bstats && C_OFF(it, ps) != OOB) {
             const u16x8 c = __builtin_bit_cast(u16x8, v);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
@@ -867,6 +891,21 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) r[e] = f2bf(bf2f(c[e]) + bf2f(o[e]));
             w = __builtin_bit_cast(u32x4, r);
+          }
+        }
+        if constexpr (BNB && GA && !OUTF32) {
+          if (bstats && C_OFF(it, ps) != OOB) {
+            const u16x8 c = __builtin_bit_cast(u16x8, w);
+            const u16x8 xb = __builtin_bit_cast(u16x8, xo[u]);
+            const u16x8 yb = __builtin_bit_cast(u16x8, yo[u]);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float xv = bf2f(xb[e]);
+              const bool keep = !p.bs.relu || (p.bs.y ? bf2f(yb[e]) > 0.f : fmaf(xv, msc[e], msf[e]) > 0.f);
+              const float gv = keep ? bf2f(c[e]) : 0.f;
+              st1[e] += gv;
+              st2[e] += gv * (xv - shc[e]);
+            }
           }
         }
         __builtin_amdgcn_raw_buffer_store_b128(w, rsC, C_OFF(it, ps), 0, 0);
@@ -913,11 +952,12 @@ static int g_sched = -1;      // -1: per-layout default; 0 / 1: force PF_IN_CLUS
 static int g_persistent = 1;  // 0: one tile per block (grid = tiles), for A/B runs
 static int g_stagger = 1;     // start stagger units per block slot (profiles/r3_gemm_stagger_ab.jsonl: +0.7 % over the step GEMMs)
 
-template <bool AK, bool BK, bool F32, bool PF, bool KFULL, bool GA = false, bool F8 = false, int GM = 0>
+template <bool AK, bool BK, bool F32, bool PF, bool KFULL, bool GA = false, bool F8 = false, int GM = 0,
+          bool BNB = false>
 static int launch_v(const Params& p, int batch, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_kernel<AK, BK, F32, PF, KFULL, GA, F8, GM>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_kernel<AK, BK, F32, PF, KFULL, GA, F8, GM, BNB>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
@@ -935,7 +975,7 @@ static int launch_v(const Params& p, int batch, hipStream_t st) {
   const int grid = (GM == 1 || nwg < ncu || !g_persistent) ? nwg : ncu;
   Params pp = p;
   pp.stagger = grid == ncu ? g_stagger : 0;
-  hipLaunchKernelGGL((gemm_kernel<AK, BK, F32, PF, KFULL, GA, F8, GM>), dim3(grid, GM == 1 ? 1 : batch), dim3(NT),
+  hipLaunchKernelGGL((gemm_kernel<AK, BK, F32, PF, KFULL, GA, F8, GM, BNB>), dim3(grid, GM == 1 ? 1 : batch), dim3(NT),
                      LDS_BYTES, st, pp);
   return (int)hipGetLastError();
 }
@@ -1123,6 +1163,12 @@ PA_EXPORT int pa_conv_gemm_acc(const void* src, const void* wt, void* out, const
                             accumulate, nullptr, nullptr, st);
 }
 
+PA_EXPORT int pa_conv_gemm_bnbwd(const void* src, const void* wt, void* out, const void* bias, int Nb, int H, int W,
+                                 int C, int OH, int OW, int Cout, int KH, int KW, int sy, int sx, int py, int px,
+                                 int dy, int dx, int uy, int ux, int accumulate, float* part, const float* shift,
+                                 const void* bx, const void* by, const float* mean, const float* rstd, const void* w,
+                                 const void* b, int wdt, int relu, hipStream_t st);
+
 // part (nullable): BatchNorm statistics of the output, [ceil(M / 256)][2][Cout] about
 // `shift` (nullable, fp32 [Cout]) -- the layout of pa_conv_sn's and bn_finalize's partials
 PA_EXPORT int pa_conv_gemm_stats(const void* src, const void* wt, void* out, const void* bias, int Nb, int H, int W,
@@ -1130,6 +1176,19 @@ PA_EXPORT int pa_conv_gemm_stats(const void* src, const void* wt, void* out, con
                                  int dy, int dx, int uy, int ux, int accumulate, float* part, const float* shift,
                                  hipStream_t st) {
   if (accumulate && part) return -1;
+  return pa_conv_gemm_bnbwd(src, wt, out, bias, Nb, H, W, C, OH, OW, Cout, KH, KW, sy, sx, py, px, dy, dx, uy, ux,
+                            accumulate, part, shift, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, st);
+}
+
+// Data gradient with the BatchNorm backward statistics of its final values (after an
+// optional accumulate-into): part [ceil(M / 256)][2][Cout] of sum g, sum g (x - mean)
+// (common.h BnBwdSrc; bx null: forward statistics about `shift` as pa_conv_gemm_stats)
+PA_EXPORT int pa_conv_gemm_bnbwd(const void* src, const void* wt, void* out, const void* bias, int Nb, int H, int W,
+                                 int C, int OH, int OW, int Cout, int KH, int KW, int sy, int sx, int py, int px,
+                                 int dy, int dx, int uy, int ux, int accumulate, float* part, const float* shift,
+                                 const void* bx, const void* by, const float* mean, const float* rstd, const void* w,
+                                 const void* b, int wdt, int relu, hipStream_t st) {
+  if (bx && (!part || !mean || !rstd)) return -1;
   const long M = (long)Nb * OH * OW;
   if (M <= 0 || Cout <= 0) return 0;
   if (C % 64 || Cout % 8 || M > 0x7fffffffL || (long)Nb * H * W * C >= 0x7fffffffL || H > 32767 || W > 32767)
@@ -1142,9 +1201,11 @@ PA_EXPORT int pa_conv_gemm_stats(const void* src, const void* wt, void* out, con
   p.accumulate = accumulate;
   p.part = part;
   p.shift = shift;
+  p.bs = BnBwdSrc{(const u16*)bx, (const u16*)by, mean, rstd, w, b, wdt, relu};
   p.H = H; p.W = W; p.Cc = C; p.OH = OH; p.OW = OW; p.KW = KW;
   p.sy = sy; p.sx = sx; p.py = py; p.px = px; p.dy = dy; p.dx = dx; p.uy = uy; p.ux = ux;
   p.tiles_m = (p.M + gemm::BM - 1) / gemm::BM;
   p.tiles_n = (p.N + gemm::BN - 1) / gemm::BN;
+  if (bx) return gemm::launch_v<true, true, false, false, true, true, false, 0, true>(p, 1, st);
   return gemm::launch_v<true, true, false, false, true, true>(p, 1, st);
 }

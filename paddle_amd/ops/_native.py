@@ -78,6 +78,8 @@ _SIGS = {
     "pa_conv_sn_acc": [_P, _P, _P, _P] + [_I] * 17 + [_P, _P, _I, _P],
     "pa_conv_gemm_acc": [_P, _P, _P, _P] + [_I] * 18 + [_P],
     "pa_conv_gemm_stats": [_P, _P, _P, _P] + [_I] * 18 + [_P, _P, _P],
+    "pa_conv_gemm_bnbwd": [_P, _P, _P, _P] + [_I] * 18 + [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P],
+    "pa_conv_sn_bnbwd": [_P, _P, _P] + [_I] * 18 + [_P, _P, _P, _P, _P, _P, _P, _I, _I, _P],
     "pa_momentum_multi": [_P, _I, _L, _F, _P, _F, _I, _F, _P],
     "pa_momentum_multi_entry_bytes": [],
     "pa_momentum_multi_chunk": [],
@@ -92,6 +94,7 @@ _SIGS = {
     "pa_bn_apply": [_P, _P, _P, _P, _P, _P, _I, _L, _I, _I, _P],
     "pa_bn_bwd": [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _L, _I, _I, _P, _P],
     "pa_bn_bwd2": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _L, _I, _I, _P, _P],
+    "pa_bn_bwd_part": [_P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _L, _I, _I, _P, _P],
     "pa_maxpool_nhwc_fwd": [_P, _P, _P] + [_I] * 12 + [_P],
     "pa_maxpool_nhwc_bwd": [_P, _P, _P] + [_I] * 12 + [_P],
     "pa_gap_nhwc_fwd": [_P, _P, _I, _I, _I, _P],

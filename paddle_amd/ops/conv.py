@@ -146,10 +146,20 @@ def _dgrad_weight(w, dt):
     return out.view(C, KH * KW * Cout)
 
 
-def _conv_dgrad(dy, w, x_shape, s, p, d, into=None):
+def _bnb_ok(bnb, shape, dt):
+    bx = bnb.get("x") if bnb else None
+    by = bnb.get("y") if bnb else None
+    return (bx is not None and tuple(bx.shape) == tuple(shape) and bx.dtype == dt and bx.is_contiguous()
+            and (by is None or (tuple(by.shape) == tuple(shape) and by.dtype == dt and by.is_contiguous())))
+
+
+def _conv_dgrad(dy, w, x_shape, s, p, d, into=None, bnb=None):
     """dX of the convolution.  ``into``: an exclusively owned gradient of x already
     summed by the engine (e.g. the residual branch's): dX is accumulated into it in
-    the GEMM epilogue and ``into`` is returned (no separate add pass)."""
+    the GEMM epilogue and ``into`` is returned (no separate add pass).
+    ``bnb`` (x is the output of a training BatchNorm, see ``batch_norm_nhwc_train``):
+    the epilogue also emits that BN's backward statistics of the final dX; the
+    partials are attached as ``dx._pa_bnpart`` (any other in-place write clears it)."""
     N, H, W, C = x_shape
     Cout, _, KH, KW = w.shape
     OH, OW = dy.shape[1], dy.shape[2]
@@ -161,10 +171,27 @@ def _conv_dgrad(dy, w, x_shape, s, p, d, into=None):
         pyy, pxx = d[0] * (KH - 1) - p[0], d[1] * (KW - 1) - p[1]
         geo = (N, OH, OW, Cout, H, W, C, KH, KW, 1, 1, pyy, pxx, d[0], d[1], int(math.log2(s[0])),
                int(math.log2(s[1])))
+        L = _nat.lib()
+        if C % 64 == 0 and _bnb_ok(bnb, (N, H, W, C), dy.dtype):
+            G = int(L.pa_conv_sn_tiles(N * H * W))
+            part = torch.empty(G * 2 * C, dtype=torch.float32, device=dy.device)
+            src = (_nat.ptr(part), _nat.ptr(bnb["x"]), _nat.ptr(bnb.get("y")), _nat.ptr(bnb["mean"]),
+                   _nat.ptr(bnb["rstd"]), _nat.ptr(bnb.get("w")), _nat.ptr(bnb.get("b")), int(bnb["wdt"]),
+                   int(bnb["relu"]))
+            if C <= _SN_MAX[0]:
+                rc = L.pa_conv_sn_bnbwd(_nat.ptr(dy), _nat.ptr(wd), _nat.ptr(dx), *geo, int(acc), *src,
+                                        _nat.stream())
+            else:
+                rc = L.pa_conv_gemm_bnbwd(_nat.ptr(dy), _nat.ptr(wd), _nat.ptr(dx), None, *geo, int(acc),
+                                          src[0], None, *src[1:], _nat.stream())
+            if rc == 0:
+                dx._pa_bnpart = (part, G, bnb["mean"])
+                return dx
+        if acc and getattr(into, "_pa_bnpart", None) is not None:
+            into._pa_bnpart = None  # its statistics no longer describe the sum
         if C <= _SN_MAX[0] and _sn(dy, wd, dx, None, geo, acc=acc):
             return dx
-        rc = _nat.lib().pa_conv_gemm_acc(_nat.ptr(dy), _nat.ptr(wd), _nat.ptr(dx), None, *geo, int(acc),
-                                         _nat.stream())
+        rc = L.pa_conv_gemm_acc(_nat.ptr(dy), _nat.ptr(wd), _nat.ptr(dx), None, *geo, int(acc), _nat.stream())
         if rc == 0:
             return dx
     # rare shapes: autograd of the torch convolution
@@ -223,10 +250,13 @@ def _conv_wgrad(dy, x, w_shape, s, p, d, wdtype=torch.float32):
 
 class _Conv2dNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, s, p, d, stats=None):
+    def forward(ctx, x, w, b, s, p, d, stats=None, bnsrc=None):
         y = _conv_fwd(x, w, b, s, p, d, stats)
         ctx.save_for_backward(x, w)
         ctx.conf = (s, p, d, b is not None)
+        if bnsrc is not None:
+            bnsrc = dict(bnsrc, y=x if bnsrc.get("y_mask") else None)
+        ctx.bnsrc = bnsrc if _bnb_ok(bnsrc, x.shape, x.dtype) else None
         return y
 
     @staticmethod
@@ -236,12 +266,13 @@ class _Conv2dNHWC(torch.autograd.Function):
         dy = dy.contiguous()
         into = getattr(ctx, "grad_prev", None)
         into = into[0] if into else None
-        dx = _conv_dgrad(dy, w, tuple(x.shape), s, p, d, into) if ctx.needs_input_grad[0] else None
+        dx = (_conv_dgrad(dy, w, tuple(x.shape), s, p, d, into, getattr(ctx, "bnsrc", None))
+              if ctx.needs_input_grad[0] else None)
         if dx is not None:
             dx._pa_acc_ok = True  # exclusively owned: later producers may accumulate into it
         dw = _conv_wgrad(dy, x, tuple(w.shape), s, p, d, w.dtype) if ctx.needs_input_grad[1] else None
         db = dy.reshape(-1, dy.shape[-1]).float().sum(0).to(w.dtype) if has_b and ctx.needs_input_grad[2] else None
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
 def conv2d_nhwc(x, weight, bias=None, stride=1, padding=0, dilation=1, stats=None):
@@ -251,7 +282,20 @@ def conv2d_nhwc(x, weight, bias=None, stride=1, padding=0, dilation=1, stats=Non
     mean, or absent); on return it holds ``part`` / ``G`` when the kernel emitted them
     (64-channel-tile path), for :func:`batch_norm_nhwc_train`'s ``stats``."""
     s, p, d = _pair(stride), _pair(padding), _pair(dilation)
-    return _tape.apply(_Conv2dNHWC, x, weight, bias, tuple(map(_i, s)), tuple(map(_i, p)), tuple(map(_i, d)), stats)
+    # x produced by a training BatchNorm (batch_norm_nhwc_train marks its output): the
+    # data gradient's epilogue computes that BN's backward statistics
+    bnsrc = getattr(x, "_pa_bnsrc", None) if _BNB[0] else None
+    return _tape.apply(_Conv2dNHWC, x, weight, bias, tuple(map(_i, s)), tuple(map(_i, p)), tuple(map(_i, d)), stats,
+                       bnsrc)
+
+
+# BatchNorm backward statistics from the consuming conv's data-gradient epilogue.
+# Off by default: measured slower end to end (ResNet-50 bs 256: 7,386 vs 7,803
+# img/s, profiles/r4_resnet50_prof_bnbwd_NEGATIVE.md) -- the separate bn_reduce pass
+# runs at full HBM bandwidth, while the x / y reads added to the dgrad epilogues
+# (short-K 1x1 convs: the epilogue is most of the kernel) are not overlapped with
+# MFMA work: +4.4 ms/step of epilogue for -2.3 ms/step of bn_reduce.
+_BNB = [os.environ.get("FLAGS_conv_bn_bwd_stats", "0") == "1"]
 
 
 # ------------------------------------------------------------------ depthwise conv (dwconv.hip)
@@ -323,7 +367,7 @@ def _wdt(w):
 
 class _BatchNormNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, run_mean, run_var, momentum, eps, relu, res, stats=None):
+    def forward(ctx, x, w, b, run_mean, run_var, momentum, eps, relu, res, stats=None, link=None):
         C = x.shape[-1]
         rows = x.numel() // C
         wdt, wc = _wdt(w)
@@ -363,6 +407,11 @@ class _BatchNormNHWC(torch.autograd.Function):
         ctx.save_for_backward(x, y if (relu and res is not None) else None, mean, rstd, wc,
                               bc if (relu and res is None) else None)
         ctx.conf = (relu, wdt, w is not None, b is not None, res is not None)
+        if link is not None and relu:
+            # what a consuming conv's dgrad epilogue needs for this BN's backward sums
+            # (no reference to y itself: y carries the link; a residual layer's mask
+            # source y is the consuming conv's own input)
+            link.update(x=x, y_mask=res is not None, mean=mean, rstd=rstd, w=wc, b=bc, wdt=wdt, relu=1)
         ctx.wdtype = w.dtype if w is not None else None
         ctx.bdtype = b.dtype if b is not None else None
         return y
@@ -373,22 +422,29 @@ class _BatchNormNHWC(torch.autograd.Function):
         relu, wdt, has_w, has_b, has_res = ctx.conf
         C = x.shape[-1]
         rows = x.numel() // C
+        bp = getattr(dy, "_pa_bnpart", None)
         dy = dy.contiguous()
-        G = int(_nat.lib().pa_bn_blocks(rows, C))
-        part = torch.empty(G * 2 * C, dtype=torch.float32, device=x.device)
         coef = torch.empty(3 * C, dtype=torch.float32, device=x.device)
         dw = torch.empty(C, dtype=torch.float32, device=x.device)
         db = torch.empty(C, dtype=torch.float32, device=x.device)
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if has_res else None
-        _nat.call("pa_bn_bwd2", _nat.ptr(x), _nat.ptr(dy), _nat.ptr(y), _nat.ptr(mean), _nat.ptr(rstd),
-                  _nat.ptr(wc), _nat.ptr(bc), wdt, _nat.ptr(dx), _nat.ptr(dw), _nat.ptr(db), _nat.ptr(coef),
-                  _nat.ptr(part), rows, C, int(relu), _nat.ptr(dres), _nat.stream())
+        if bp is not None and relu and bp[2].data_ptr() == mean.data_ptr():
+            # the reduction came from the epilogue of the conv that produced dy
+            _nat.call("pa_bn_bwd_part", _nat.ptr(bp[0]), int(bp[1]), _nat.ptr(x), _nat.ptr(dy), _nat.ptr(y),
+                      _nat.ptr(mean), _nat.ptr(rstd), _nat.ptr(wc), _nat.ptr(bc), wdt, _nat.ptr(dx), _nat.ptr(dw),
+                      _nat.ptr(db), _nat.ptr(coef), rows, C, int(relu), _nat.ptr(dres), _nat.stream())
+        else:
+            G = int(_nat.lib().pa_bn_blocks(rows, C))
+            part = torch.empty(G * 2 * C, dtype=torch.float32, device=x.device)
+            _nat.call("pa_bn_bwd2", _nat.ptr(x), _nat.ptr(dy), _nat.ptr(y), _nat.ptr(mean), _nat.ptr(rstd),
+                      _nat.ptr(wc), _nat.ptr(bc), wdt, _nat.ptr(dx), _nat.ptr(dw), _nat.ptr(db), _nat.ptr(coef),
+                      _nat.ptr(part), rows, C, int(relu), _nat.ptr(dres), _nat.stream())
         dx._pa_acc_ok = True  # fresh, exclusively owned gradients (see ops.conv._conv_dgrad's into)
         if dres is not None:
             dres._pa_acc_ok = True
         return (dx, dw.to(ctx.wdtype) if has_w else None, db.to(ctx.bdtype) if has_b else None,
-                None, None, None, None, None, dres, None)
+                None, None, None, None, None, dres, None, None)
 
 
 def batch_norm_nhwc_train(x, weight, bias, running_mean, running_var, momentum=0.9, eps=1e-5, relu=False,
@@ -400,8 +456,12 @@ def batch_norm_nhwc_train(x, weight, bias, running_mean, running_var, momentum=0
         if not relu:
             raise ValueError("the fused residual form is relu(bn(x) + residual)")
         residual = residual.contiguous()
-    return _tape.apply(_BatchNormNHWC, x, weight, bias, running_mean, running_var, float(momentum), float(eps), bool(relu),
-                       residual, stats)
+    link = {} if (relu and _BNB[0]) else None
+    y = _tape.apply(_BatchNormNHWC, x, weight, bias, running_mean, running_var, float(momentum), float(eps),
+                    bool(relu), residual, stats, link)
+    if link:
+        y._pa_bnsrc = link  # read by conv2d_nhwc when y feeds a convolution
+    return y
 
 
 def batch_norm_nhwc_eval(x, weight, bias, running_mean, running_var, eps=1e-5, relu=False):

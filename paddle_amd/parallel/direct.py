@@ -38,20 +38,25 @@ _P = ctypes.c_void_p
 
 
 class DirectAllReduce:
-    def __init__(self, group=None, max_bytes=64 << 20, one_shot_bytes=1 << 20, max_spins=1 << 25):
+    def __init__(self, group=None, max_bytes=64 << 20, one_shot_bytes=1 << 20, max_spins=1 << 25, extra_bytes=0):
+        """``extra_bytes``: a second region of the registered staging allocation, after
+        the ``max_bytes`` scratch area, handed out by :meth:`staging_tensor` -- a buffer
+        placed there (the sharded optimizer's flat gradient) is reduce-scattered in
+        place, without the copy-in pass."""
         self.group = group
         self.world = comm.get_world_size(group)
         self.rank = comm.get_rank(group)
         if not 1 <= self.world <= 8:
             raise ValueError("DirectAllReduce: 1..8 ranks (one node)")
         self.max_bytes = (int(max_bytes) + 4095) // 4096 * 4096
+        self.extra_bytes = (int(extra_bytes) + 4095) // 4096 * 4096
         self.one_shot_bytes = int(one_shot_bytes)
         self.max_spins = int(max_spins)
         self.device = torch.device("cuda", torch.cuda.current_device())
         lib = N.lib()
         self._own = []
         stage, sig = _P(), _P()
-        N.check(lib.pa_p2p_alloc(ctypes.byref(stage), self.max_bytes), "pa_p2p_alloc")
+        N.check(lib.pa_p2p_alloc(ctypes.byref(stage), self.max_bytes + self.extra_bytes), "pa_p2p_alloc")
         self._own.append(stage.value)
         N.check(lib.pa_p2p_alloc(ctypes.byref(sig), 4096), "pa_p2p_alloc")
         self._own.append(sig.value)
@@ -81,6 +86,32 @@ class DirectAllReduce:
         self._err = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.epoch = 0
         comm.barrier(group)
+
+    def staging_tensor(self, numel, dtype):
+        """A tensor over the extra region of this rank's registered staging buffer
+        (every rank places the same layout there).  Uncached device memory: stores
+        reach HBM, so peers read it straight after a barrier."""
+        es = torch.empty((), dtype=dtype).element_size()
+        if numel * es > self.extra_bytes:
+            raise ValueError(f"staging_tensor: {numel * es} bytes > the {self.extra_bytes}-byte extra region")
+        base = self._stage[self.rank] + self.max_bytes
+
+        class _Iface:  # zero-copy byte view (torch keeps this object alive with the tensor)
+            __cuda_array_interface__ = {"shape": (int(numel * es),), "typestr": "|u1", "data": (base, False),
+                                        "version": 3}
+
+        t = torch.as_tensor(_Iface(), device=self.device).view(dtype)
+        if t.data_ptr() != base:
+            raise RuntimeError("staging_tensor: torch copied the buffer instead of viewing it")
+        return t
+
+    def _in_place(self, t):
+        """Byte offset of ``t`` inside this rank's extra staging region, or None."""
+        off = t.data_ptr() - self._stage[self.rank]
+        n = t.numel() * t.element_size()
+        if self.extra_bytes and off >= self.max_bytes and off + n <= self.max_bytes + self.extra_bytes:
+            return off
+        return None
 
     # ------------------------------------------------------------------ pieces
     def _barrier(self):
@@ -140,16 +171,22 @@ class DirectAllReduce:
             out.copy_(inp)
             return out
         es = inp.element_size()
-        if (n != L * self.world or L % 8 or out.dtype != inp.dtype or n * es > self.max_bytes
+        off = self._in_place(inp) if self._dense_ok(inp) else None
+        if (n != L * self.world or L % 8 or out.dtype != inp.dtype or (off is None and n * es > self.max_bytes)
                 or not self._dense_ok(out, inp)):
             comm.reduce_scatter(out, inp, self.group)
             return out
-        own = _P(self._stage[self.rank])
-        N.call("pa_p2p_copy", own, N.ptr(inp), n * es, N.stream())
+        if off is None:
+            stages = self._stage
+            N.call("pa_p2p_copy", _P(self._stage[self.rank]), N.ptr(inp), n * es, N.stream())
+        else:
+            # the input already lives in the registered buffer at the same offset on
+            # every rank: no copy-in pass
+            stages = (_P * 8)(*[self._stage[r] + off if r < self.world else 0 for r in range(8)])
         self._barrier()
         b = self.rank * L
         # the kernel writes out[i] for absolute i in [b, b + L): shift the base
-        N.call("pa_p2p_reduce", N.dt(inp), self._stage, self._sig, self.world, self.rank,
+        N.call("pa_p2p_reduce", N.dt(inp), stages, self._sig, self.world, self.rank,
                _P(out.data_ptr() - b * es), b, b + L, N.ptr(self._err), N.stream())
         self._barrier()
         return out

@@ -107,7 +107,25 @@ class FlatShardedOptimizer:
         self.offsets = offs
         # --- flat buffers; parameters/grads become views
         self.flat_param = torch.zeros(total, dtype=dt, device=dev)
-        self.flat_grad = torch.zeros(total, dtype=self.grad_dtype, device=dev)
+        # FLAGS_dp_comm=direct: reduce-scatter / all-gather over IPC-mapped peer
+        # buffers on the xGMI links (parallel/direct.py) instead of RCCL
+        self.dp_comm = os.environ.get("FLAGS_dp_comm", "rccl") if dp_comm is None else dp_comm
+        self._direct = None
+        if self.dp_comm == "direct" and self.W > 1 and dev.type == "cuda":
+            from .direct import DirectAllReduce
+
+            ges = torch.empty((), dtype=self.grad_dtype).element_size()
+            big = max(be - bs for bs, be, _ in buckets) * max(ges, self.flat_param.element_size())
+            # FLAGS_dp_direct_inplace=1: the flat gradient itself lives in the registered
+            # staging allocation, so every bucket's reduce-scatter reads it in place
+            # (no copy-in pass over the gradients)
+            inplace = os.environ.get("FLAGS_dp_direct_inplace", "0") == "1"
+            self._direct = DirectAllReduce(group, max_bytes=big, extra_bytes=total * ges if inplace else 0)
+        if self._direct is not None and self._direct.extra_bytes:
+            self.flat_grad = self._direct.staging_tensor(total, self.grad_dtype)
+            self.flat_grad.zero_()
+        else:
+            self.flat_grad = torch.zeros(total, dtype=self.grad_dtype, device=dev)
         self._bucket_of = {}
         bi = 0
         with torch.no_grad():
@@ -176,16 +194,6 @@ class FlatShardedOptimizer:
         self.opt_stream = ((dc.aux_stream if dc is not None else torch.cuda.Stream(device=dev))
                            if self.overlap_update else None)
         self._keep = None
-        # FLAGS_dp_comm=direct: reduce-scatter / all-gather over IPC-mapped peer
-        # buffers on the xGMI links (parallel/direct.py) instead of RCCL
-        self.dp_comm = os.environ.get("FLAGS_dp_comm", "rccl") if dp_comm is None else dp_comm
-        self._direct = None
-        if self.dp_comm == "direct" and self.W > 1 and dev.type == "cuda":
-            from .direct import DirectAllReduce
-
-            big = max(be - bs for bs, be, _ in buckets) * max(self.flat_grad.element_size(),
-                                                              self.flat_param.element_size())
-            self._direct = DirectAllReduce(group, max_bytes=big)
         self._hooks = []
         if self.W > 1 or self.main_grad:
             for p in self.params:

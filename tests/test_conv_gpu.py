@@ -262,3 +262,101 @@ def test_bottleneck_residual_grad_accumulated_in_dgrad_epilogue():
             E._ACCUM_INTO[0] = True
     assert _rel(res[1][0], res[0][0]) < 1e-2
     assert _rel(res[1][1], res[0][1]) < 1e-2
+
+
+BNB_CASES = [
+    # N, H, W, C, Cout, k, stride, pad, y-mask, accumulate  (C <= 128: 64-channel tiles; else 256-wide GEMM)
+    (2, 14, 14, 64, 64, 3, 1, 1, False, False),
+    (2, 15, 13, 64, 128, 3, 2, 1, True, False),
+    (3, 9, 11, 128, 64, 1, 1, 0, False, True),
+    (2, 8, 8, 256, 64, 1, 1, 0, False, False),
+    (4, 8, 8, 256, 128, 1, 2, 0, True, True),
+]
+
+
+@pytest.mark.parametrize("N,H,W,C,Co,k,s,p,ymask,acc", BNB_CASES)
+def test_dgrad_epilogue_emits_bn_backward_stats(N, H, W, C, Co, k, s, p, ymask, acc):
+    """The conv data gradient with BatchNorm-backward statistics (pa_conv_sn_bnbwd /
+    pa_conv_gemm_bnbwd): dX unchanged, and the partials sum to sum(g), sum(g (x - mean))
+    with g = the stored dX under the ReLU mask (from y, or recomputed from x)."""
+    from paddle_amd.ops import conv
+
+    g = torch.Generator(device=dev).manual_seed(N * 31 + C + Co + k)
+    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = torch.randn(N, OH, OW, Co, generator=g, device=dev).to(torch.bfloat16)
+    w = (torch.randn(Co, C, k, k, generator=g, device=dev) / (Co * k * k) ** 0.5).to(torch.bfloat16)
+    xb = (torch.randn(N, H, W, C, generator=g, device=dev) + 0.3).to(torch.bfloat16)
+    mean = torch.randn(C, generator=g, device=dev) * 0.2
+    rstd = torch.rand(C, generator=g, device=dev) + 0.5
+    bw = torch.rand(C, generator=g, device=dev) + 0.5
+    bb = torch.randn(C, generator=g, device=dev) * 0.3
+    yb = torch.randn(N, H, W, C, generator=g, device=dev).to(torch.bfloat16) if ymask else None
+    prev = torch.randn(N, H, W, C, generator=g, device=dev).to(torch.bfloat16)
+    plain = conv._conv_dgrad(dy, w, (N, H, W, C), (s, s), (p, p), (1, 1),
+                             into=prev.clone() if acc else None)
+    bnb = {"x": xb, "y": yb, "mean": mean, "rstd": rstd, "w": bw, "b": bb, "wdt": 0, "relu": 1}
+    dx = conv._conv_dgrad(dy, w, (N, H, W, C), (s, s), (p, p), (1, 1), into=prev.clone() if acc else None, bnb=bnb)
+    assert torch.equal(dx, plain)
+    bp = getattr(dx, "_pa_bnpart", None)
+    assert bp is not None and bp[2] is mean
+    G = bp[1]
+    part = bp[0].view(G, 2, C).double().sum(0)
+    xf = xb.double().reshape(-1, C)
+    if ymask:
+        keep = yb.double().reshape(-1, C) > 0
+    else:
+        sc = rstd.double() * bw.double()
+        keep = (xf * sc + (bb.double() - mean.double() * sc)) > 0
+    gg = dx.double().reshape(-1, C) * keep
+    torch.testing.assert_close(part[0], gg.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(part[1], (gg * (xf - mean.double())).sum(0), rtol=1e-4, atol=1e-2)
+
+
+def test_resnet_blocks_bn_backward_stats_match_two_pass():
+    """Two bottleneck blocks (the second strided with a projection shortcut, so the
+    first block's output has two consuming convs and a residual-ReLU mask): every
+    gradient with the BN backward statistics taken in the consuming dgrad epilogues
+    (FLAGS_conv_bn_bwd_stats=1, off by default: measured slower) equals the
+    separate-reduction path, and the epilogue path is the one taken."""
+    import paddle_amd as paddle
+    from paddle_amd import nn
+    from paddle_amd.ops import conv
+    from paddle_amd.ops import _native as N_
+    from paddle_amd.vision.models import BottleneckBlock
+
+    paddle.seed(13)
+    ds = nn.Sequential(nn.Conv2D(256, 512, 1, stride=2, bias_attr=False, data_format="NHWC"),
+                       nn.BatchNorm2D(512, data_format="NHWC"))
+    net = nn.Sequential(BottleneckBlock(256, 64, data_format="NHWC"),
+                        BottleneckBlock(256, 128, stride=2, downsample=ds, data_format="NHWC")).to(dev)
+    net = net.to(torch.bfloat16)
+    g = torch.Generator(device=dev).manual_seed(4)
+    x0 = torch.randn(4, 16, 16, 256, generator=g, device=dev).to(torch.bfloat16)
+    real_call = N_.call
+    saved = conv._BNB[0]
+    res = []
+    for on in (False, True):
+        used = []
+
+        def counting(name, *a, **k):
+            if name == "pa_bn_bwd_part":
+                used.append(name)
+            return real_call(name, *a, **k)
+
+        conv._BNB[0] = on
+        N_.call = counting
+        try:
+            for q in net.parameters():
+                q.grad = None
+            x = paddle.to_tensor(x0.clone(), stop_gradient=False)
+            y = net(x)
+            (y.astype("float32") ** 2).mean().backward()
+            res.append([x.grad.float().clone()] + [q.grad.float().clone() for q in net.parameters()])
+        finally:
+            N_.call = real_call
+            conv._BNB[0] = saved
+        # 5 ReLU BatchNorms whose output feeds a convolution (bn1, bn2 of both blocks,
+        # bn3 of the first); the last block's bn3 and the shortcut BN have no conv consumer
+        assert len(used) == (5 if on else 0), used
+    for a, b in zip(res[0], res[1]):
+        assert _rel(b, a) < 2e-2

@@ -28,7 +28,7 @@ def _port():
     return p
 
 
-def _train(dp_comm, rank, steps=3):
+def _train(dp_comm, rank, steps=3, inplace=False):
     from paddle_amd.autograd import tape
     from paddle_amd.models.llama import LLAMA_CONFIGS, LlamaConfig, LlamaForCausalLM
     from paddle_amd.parallel.sharding import FlatShardedOptimizer
@@ -36,10 +36,17 @@ def _train(dp_comm, rank, steps=3):
     torch.manual_seed(0)
     cfg = LlamaConfig(**LLAMA_CONFIGS["llama-tiny"])
     model = LlamaForCausalLM(cfg, device="cuda")
-    opt = FlatShardedOptimizer(model.named_parameters(), lr=1e-3, weight_decay=0.1, grad_clip=1.0,
-                               grad_dtype=torch.float32, bucket_mb=1, overlap=True, overlap_allgather=True,
-                               dp_comm=dp_comm)
+    os.environ["FLAGS_dp_direct_inplace"] = "1" if inplace else "0"
+    try:
+        opt = FlatShardedOptimizer(model.named_parameters(), lr=1e-3, weight_decay=0.1, grad_clip=1.0,
+                                   grad_dtype=torch.float32, bucket_mb=1, overlap=True, overlap_allgather=True,
+                                   dp_comm=dp_comm)
+    finally:
+        os.environ.pop("FLAGS_dp_direct_inplace", None)
     assert (opt._direct is not None) == (dp_comm == "direct")
+    if inplace:
+        # the flat gradient is the registered staging region: reduce-scatters skip the copy-in
+        assert opt._direct._in_place(opt.flat_grad) is not None
     ids = torch.randint(0, cfg.vocab_size, (2, 129), generator=torch.Generator().manual_seed(10 + rank)).cuda()
     losses = []
     for _ in range(steps):
@@ -99,8 +106,10 @@ def _worker(rank, world, port, q):
         exact = _collectives_exact(rank, world)
         l_pg, p_pg, nb = _train("rccl", rank)
         l_dr, p_dr, _ = _train("direct", rank)
+        l_ip, p_ip, _ = _train("direct", rank, inplace=True)
         dist.destroy_process_group()
-        q.put((rank, (exact, l_pg, l_dr, float((p_pg - p_dr).abs().max()), nb), None))
+        q.put((rank, (exact, l_pg, l_dr, float((p_pg - p_dr).abs().max()), nb, l_ip,
+                      float((p_pg - p_ip).abs().max())), None))
     except Exception as e:  # report to the parent instead of hanging it
         import traceback
 
@@ -126,11 +135,16 @@ def test_zero1_direct_comm_matches_process_group_two_ranks_one_gpu():
             if p.is_alive():
                 p.kill()
     for rank in range(world):
-        exact, l_pg, l_dr, pdiff, nb = out[rank]
+        exact, l_pg, l_dr, pdiff, nb, l_ip, pdiff_ip = out[rank]
         assert exact == 0.0, (rank, exact)
         assert nb > 1, "the test must exercise several buckets"
         assert l_pg[0] == l_dr[0], (rank, l_pg, l_dr)
         for a, b in zip(l_pg, l_dr):
             assert abs(a - b) <= 1e-4 * abs(a), (rank, l_pg, l_dr)
         assert pdiff < 2e-2, (rank, pdiff)
+        # in-place staging (FLAGS_dp_direct_inplace): the same training
+        assert l_pg[0] == l_ip[0], (rank, l_pg, l_ip)
+        for a, b in zip(l_pg, l_ip):
+            assert abs(a - b) <= 1e-4 * abs(a), (rank, l_pg, l_ip)
+        assert pdiff_ip < 2e-2, (rank, pdiff_ip)
         assert l_pg[-1] < l_pg[0]
