@@ -81,6 +81,9 @@ def main(argv=None):
     ap.add_argument("--trainer_count", type=int, default=1)
     ap.add_argument("--test_period", type=int, default=0, help="0: test at the end of every pass")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--local", type=int, default=1, help="0: remote updates on the parameter servers")
+    ap.add_argument("--pservers", default="", help="host:port,... of distributed.pserver2 servers (--local=0)")
+    ap.add_argument("--trainer_id", type=int, default=0)
     a = ap.parse_args(argv)
 
     from .. import v2
@@ -98,7 +101,8 @@ def main(argv=None):
     feeding = prov.feeding(conf.input_layer_names)
     if a.job == "checkgrad":
         return checkgrad(conf, train[0], prov.feeding(conf.input_layer_names), eps=a.checkgrad_eps, seed=a.seed)
-    trainer, params = conf.make_trainer()
+    remote = {} if a.local else {"is_local": False, "pserver_spec": a.pservers, "trainer_id": a.trainer_id}
+    trainer, params = conf.make_trainer(**remote)
     if a.init_model_path:
         with open(a.init_model_path, "rb") as f:
             params.init_from_tar(f)

@@ -319,9 +319,11 @@ class TrainerConfig:
             return _cp.to_text("TrainerConfig", self.trainer_config()) + "\n"
         return _cp.to_text("ModelConfig", self.model_config()) + "\n"
 
-    def make_trainer(self, parameters=None):
+    def make_trainer(self, parameters=None, **remote):
+        """``remote``: is_local=False, pserver_spec=..., trainer_id=... (parameter servers)."""
         params = parameters or v2.parameters.create(self.cost)
-        return v2.trainer.SGD(cost=self.cost, parameters=params, update_equation=self.update_equation()), params
+        return v2.trainer.SGD(cost=self.cost, parameters=params, update_equation=self.update_equation(),
+                              **remote), params
 
 
 def parse_config(config, config_arg_str=""):

@@ -76,6 +76,19 @@ def test_v1_trainer_trains_tests_and_saves(tmp_path, capsys):
         out = capsys.readouterr().out
         assert len(rel) == 4 and "checkgrad" in out
         assert max(rel.values()) < 2e-2, rel
+        # --local=0: the updates run on block-sharded parameter servers (pserver2)
+        from paddle_amd.distributed import pserver2
+
+        ss = [pserver2.ParameterServer2(num_trainers=1).start() for _ in range(2)]
+        try:
+            spec = ",".join(f"127.0.0.1:{s.port}" for s in ss)
+            costs_r = trainer.main(["--config", conf, "--num_passes", "4", "--log_period", "4", "--local", "0",
+                                    "--pservers", spec])
+            assert np.mean(costs_r[-4:]) < np.mean(costs_r[:4])
+            assert all(len(s.blocks) > 0 for s in ss)
+        finally:
+            for s in ss:
+                s.stop()
     finally:
         os.chdir(cwd)
         sys.path.remove(d)
