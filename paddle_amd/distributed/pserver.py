@@ -218,6 +218,34 @@ class _Optimizer:
         return out
 
 
+class _NativeOptimizer:
+    """A parameter whose config carries ``optimizer_config`` (hex of a serialised
+    OptimizerConfig): updated by the native optimizer library
+    (csrc/runtime/param_optimizer.cc) -- the reference Go pserver's cgo optimizer."""
+
+    def __init__(self, param, config, state=None):
+        from .param_optimizer import ParameterOptimizer
+
+        self.cfg = dict(config)
+        self.p = np.ascontiguousarray(param, np.float32).copy()
+        st = bytes(np.asarray(state["native"], np.uint8)) if state and "native" in state else None
+        self._o = ParameterOptimizer(bytes.fromhex(self.cfg["optimizer_config"]), self.p, state=st)
+        self.p[...] = self._o.weights()
+
+    def update(self, g, num_samples=1):
+        self._o.update(g)
+        self.p[...] = self._o.weights()
+
+    def state(self):
+        return {"native": np.frombuffer(self._o.state(), np.uint8).copy()}
+
+
+def _make_optimizer(param, config, state=None):
+    if isinstance(config, dict) and "optimizer_config" in config:
+        return _NativeOptimizer(param, config, state)
+    return _Optimizer(param, config, state)
+
+
 # ------------------------------------------------------------------ service
 
 
@@ -243,7 +271,7 @@ class PServerService:
         self.last_checkpoint = None
         if checkpoint is not None:  # resume (service.go NewService with a checkpoint)
             for name, (param, cfg, state) in checkpoint.items():
-                self._opt[name] = _Optimizer(param, cfg, state)
+                self._opt[name] = _make_optimizer(param, cfg, state)
             self._start()
 
     # -- RPCs
@@ -251,7 +279,7 @@ class PServerService:
         if self._initialized.is_set():
             raise RuntimeError("parameters already initialized")
         with self._mu:
-            self._opt[name] = _Optimizer(_dec(param), config)
+            self._opt[name] = _make_optimizer(_dec(param), config)
         return True
 
     def finish_init_params(self):
@@ -359,7 +387,7 @@ class PServer:
         cp = load_checkpoint(store, self.reg.index)
         if cp is not None:
             for name, (param, cfg, state) in cp.items():
-                self.service._opt[name] = _Optimizer(param, cfg, state)
+                self.service._opt[name] = _make_optimizer(param, cfg, state)
             self.service._start()
         self.endpoint = self.server.endpoint
 

@@ -23,6 +23,11 @@ NODE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.c_void_p)
 
 _SIGS = {
     "pa_rt_last_error": ([], ctypes.c_char_p),
+    "pa_opt_create": ([ctypes.c_char_p, I, I, P, I, ctypes.c_char_p, I], P),
+    "pa_opt_release": ([P], I),
+    "pa_opt_update": ([P, I, P, I], I),
+    "pa_opt_get_weights": ([P, ctypes.POINTER(ctypes.c_void_p)], I),
+    "pa_opt_get_state": ([P, ctypes.POINTER(ctypes.c_char_p)], I),
     "pa_rio_writer_open": ([ctypes.c_char_p, I, I], P),
     "pa_rio_writer_write": ([P, ctypes.c_char_p, SZ], I),
     "pa_rio_writer_close": ([P], I),

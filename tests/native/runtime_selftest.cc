@@ -7,7 +7,8 @@
 // Exercises: buddy allocator (host place) with split/merge + init_mem poisoning,
 // RecordIO round trip (gzip + plain), LoDTensor stream round trip, blocking queue
 // with concurrent producers/consumers and close, DAG scheduler on a diamond graph
-// with a failing node, profiler buffers from several threads.
+// with a failing node, profiler buffers from several threads, the parameter
+// optimizer (config parse, updates, state save / resume, truncated inputs).
 #include <atomic>
 #include <cassert>
 #include <cstdio>
@@ -48,6 +49,12 @@ typedef int (*pa_node_fn)(int node, void* user);
 int pa_dag_run(int n, const int* indeg_in, const int* succ_off, const int* succ, int nthreads, pa_node_fn fn,
                void* user);
 void pa_prof_enable(int on);
+void* pa_opt_create(const unsigned char* config, int config_len, int dtype, void* param, int num_bytes,
+                    const char* state, int state_len);
+int pa_opt_release(void* h);
+int pa_opt_update(void* h, int dtype, const void* grad, int num_bytes);
+int pa_opt_get_weights(void* h, void** buf);
+int pa_opt_get_state(void* h, const char** st);
 void pa_prof_push(const char* name);
 void pa_prof_pop();
 long pa_prof_dump(const char* path);
@@ -214,6 +221,39 @@ static void test_profiler(const std::string& dir) {
   pa_prof_enable(0);
 }
 
+static void test_param_optimizer() {
+  // OptimizerConfig{optimizer: Adam(4), adam{beta_1: 0.9}, lr_policy: Const, const_lr{learning_rate: 0.01}}
+  std::vector<unsigned char> cfg = {0x08, 0x04, 0x32, 0x09, 0x09};
+  const double b1 = 0.9, lr = 0.01;
+  unsigned char d[8];
+  std::memcpy(d, &b1, 8);
+  cfg.insert(cfg.end(), d, d + 8);
+  cfg.insert(cfg.end(), {0x58, 0x00, 0x62, 0x09, 0x09});
+  std::memcpy(d, &lr, 8);
+  cfg.insert(cfg.end(), d, d + 8);
+  std::vector<float> w(1000, 1.0f), g(1000, 0.5f);
+  void* o = pa_opt_create(cfg.data(), (int)cfg.size(), 4, w.data(), (int)(w.size() * 4), nullptr, 0);
+  assert(o);
+  for (int i = 0; i < 3; ++i) assert(pa_opt_update(o, 4, g.data(), (int)(g.size() * 4)) == 0);
+  assert(pa_opt_update(o, 4, g.data(), 12) != 0);  // wrong size refused
+  const char* st = nullptr;
+  const int n = pa_opt_get_state(o, &st);
+  std::string state(st, (size_t)n);
+  void* o2 = pa_opt_create(cfg.data(), (int)cfg.size(), 4, nullptr, (int)(w.size() * 4), state.data(), n);
+  assert(o2);
+  assert(pa_opt_update(o, 4, g.data(), (int)(g.size() * 4)) == 0);
+  assert(pa_opt_update(o2, 4, g.data(), (int)(g.size() * 4)) == 0);
+  void *a = nullptr, *b = nullptr;
+  assert(pa_opt_get_weights(o, &a) == 1000 && pa_opt_get_weights(o2, &b) == 1000);
+  assert(std::memcmp(a, b, 4000) == 0);
+  for (int cut = 0; cut < n; cut += 97)  // truncated states are refused, never read past the end
+    if (void* o3 = pa_opt_create(cfg.data(), (int)cfg.size(), 4, nullptr, 4000, state.data(), cut)) pa_opt_release(o3);
+  for (int cut = 0; cut < (int)cfg.size(); ++cut)
+    if (void* o4 = pa_opt_create(cfg.data(), cut, 4, w.data(), 4000, nullptr, 0)) pa_opt_release(o4);
+  pa_opt_release(o);
+  pa_opt_release(o2);
+}
+
 int main(int argc, char** argv) {
   std::string dir = argc > 1 ? argv[1] : "/tmp";
   test_buddy();
@@ -222,6 +262,7 @@ int main(int argc, char** argv) {
   test_queue();
   test_dag();
   test_profiler(dir);
+  test_param_optimizer();
   std::printf("runtime selftest OK\n");
   return 0;
 }
