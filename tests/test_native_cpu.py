@@ -273,3 +273,40 @@ def test_native_loader_rejects_overflowing_dims(tmp_path, dims, payload):
     ns = native.NativeScope()
     with pytest.raises(RuntimeError):
         ns.load_persistables(prog, str(tmp_path), combined=str(tmp_path / "params"))
+
+
+def test_c_api_gradient_machine_matches_python(tmp_path):
+    """The legacy C-API function set (csrc/native/paddle_capi.h, capi.cc) from a plain
+    C program: a merged model (utils/merge_model.py), a program + parameter directory
+    and a shared-parameter clone give the Python executor's output."""
+    import shutil
+
+    from paddle_amd.utils.merge_model import merge_model
+
+    main, startup = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, startup):
+        x = fluid.layers.data(name="x", shape=[12], dtype="float32")
+        h = fluid.layers.fc(x, size=16, act="relu")
+        out = fluid.layers.fc(h, size=5, act="softmax")
+    exe = fluid.Executor(fluid.CPUPlace())
+    d = str(tmp_path / "mlp")
+    with fluid.executor.scope_guard(fluid.core.Scope()):
+        exe.run(startup)
+        fluid.io.save_inference_model(d, ["x"], [out], exe, main)
+    merged = merge_model(d, str(tmp_path / "mlp.merged"))
+    xs = np.random.RandomState(6).randn(7, 12).astype("float32")
+    xs.tofile(tmp_path / "in.bin")
+    ref = _python_ref(d, [xs])[0]
+    cc = shutil.which("gcc") or "cc"
+    exe_path = str(tmp_path / "capi_demo")
+    lib = _build.build_native()
+    r = subprocess.run([cc, "-O2", os.path.join(_build.NATIVE_INC, "demo", "capi_demo.c"), f"-L{_build.LIBDIR}",
+                        "-lpaddle_amd_native", f"-Wl,-rpath,{_build.LIBDIR}", "-o", exe_path],
+                       capture_output=True, text=True)
+    assert r.returncode == 0 and os.path.exists(lib), r.stderr[-3000:]
+    r = subprocess.run([exe_path, merged, os.path.join(d, "__model__"), d, str(tmp_path / "in.bin"), "7", "12",
+                        str(tmp_path / "out.bin")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "machines_agree 7 x 5" in r.stdout
+    got = np.fromfile(tmp_path / "out.bin", dtype=np.float32).reshape(7, 5)
+    np.testing.assert_allclose(got, np.asarray(ref), rtol=2e-5, atol=2e-6)
