@@ -21,6 +21,14 @@ import torch
 
 from ..utils import flags as FLAGS
 from ..utils import profiler as prof
+from ..utils import stack_trace as _stack_trace
+
+
+def _traced(run, name):
+    def f(info, ctx):
+        with _stack_trace.frame(name):
+            return run(info, ctx)
+    return f
 from ..utils import strict as _strict
 from . import core
 from . import registry as R
@@ -141,6 +149,8 @@ class BlockExecutor:
             if _platform._V >= 3:
                 _platform.vlog(3, f"run op {op.type} inputs {dict(ins)} outputs {dict(outs)}")
             run = R.run_kernel_stash if (pb.stash[k] and not stash_off) else R.run_kernel
+            if _stack_trace.enabled[0]:
+                run = _traced(run, op.type)
             if _strict.watching() and place.torch_device().type == "cuda":
                 # framework region: tensor expressions inside the op kernel run on the
                 # HIP kernels (ops/aten_native.py); uncovered ATen kernels are counted

@@ -84,6 +84,8 @@ def main(argv=None):
     ap.add_argument("--local", type=int, default=1, help="0: remote updates on the parameter servers")
     ap.add_argument("--pservers", default="", help="host:port,... of distributed.pserver2 servers (--local=0)")
     ap.add_argument("--trainer_id", type=int, default=0)
+    ap.add_argument("--log_stat", type=int, default=0, help="1: print / reset the timer statistics every log period")
+    ap.add_argument("--op_stack_trace", type=int, default=0, help="1: operator stack in errors, SIGUSR1 dumps it")
     a = ap.parse_args(argv)
 
     from .. import v2
@@ -107,11 +109,24 @@ def main(argv=None):
         with open(a.init_model_path, "rb") as f:
             params.init_from_tar(f)
     log = []
+    from ..utils import stack_trace
+    from ..utils.stat import global_stat
+
+    if a.op_stack_trace:
+        stack_trace.install()
+    t_batch = [None]
 
     def handler(e):
         name = type(e).__name__
+        if name == "BeginIteration":
+            t_batch[0] = time.perf_counter()
+        if name == "EndIteration" and t_batch[0] is not None:
+            global_stat.add("trainBatch", time.perf_counter() - t_batch[0])
         if name == "EndIteration" and (e.batch_id + 1) % a.log_period == 0:
             print(f"Pass {e.pass_id}, Batch {e.batch_id + 1}, Cost {e.cost:.6f}, {e.metrics}", flush=True)
+            if a.log_stat:
+                global_stat.print_all_status()
+                global_stat.reset()
         if name == "EndIteration":
             log.append(e.cost)
         if name == "EndPass":

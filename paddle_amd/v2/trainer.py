@@ -96,14 +96,17 @@ class SGD:
         remote = self._client is not None and program is STATE["main"]
         if remote:
             fetch = fetch + self._grads
-        with fluid.scope_guard(STATE["scope"]):
+        from ..utils.stat import global_stat
+
+        with fluid.scope_guard(STATE["scope"]), global_stat.timer("forwardBackward"):
             outs = executor().run(program, feed=feeder.feed(batch), fetch_list=fetch)
         outs = [np.array(o) for o in outs]
         if remote:
             grads = outs[len(outs) - len(self._grads):]
             outs = outs[:len(outs) - len(self._grads)]
-            new = self._client.add_gradient(dict(zip(self._names, grads)), num_samples=len(batch),
-                                            cost=float(outs[0].ravel()[0]))
+            with global_stat.timer("sendAndReceiveParameter"):
+                new = self._client.add_gradient(dict(zip(self._names, grads)), num_samples=len(batch),
+                                                cost=float(outs[0].ravel()[0]))
             for n, v in new.items():
                 self.parameters[n] = v
         met, i = {}, 1

@@ -62,9 +62,10 @@ def test_v1_trainer_trains_tests_and_saves(tmp_path, capsys):
     os.chdir(d)
     try:
         costs = trainer.main(["--config", conf, "--num_passes", "4", "--log_period", "4",
-                              "--save_dir", os.path.join(d, "out")])
+                              "--save_dir", os.path.join(d, "out"), "--log_stat", "1"])
         out = capsys.readouterr().out
         assert "Pass 3 done" in out and "Test cost" in out
+        assert "Stat=forwardBackward" in out and "Stat=trainBatch" in out  # legacy Stat timers
         assert np.mean(costs[-4:]) < np.mean(costs[:4])
         tar = os.path.join(d, "out", "pass-00003", "params.tar")
         assert os.path.exists(tar)
