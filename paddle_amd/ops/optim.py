@@ -124,6 +124,19 @@ class MomentumMulti:
                 arr[i] = (tp, op, gp, vp, n, c0, wd, ls, tdt, odt, gdt, 0)
                 c0 += (n + chunk - 1) // chunk
             raw = torch.from_numpy(arr.view(np.uint8))
+            dev = entries[0][0].device
+            if torch.cuda.is_current_stream_capturing():
+                # HIP-graph capture (graph-pool gradient addresses): a table of its own,
+                # uploaded by a captured copy from a pinned buffer kept for the graph's
+                # lifetime -- no event waits inside the capture
+                pin = torch.empty(raw.numel(), dtype=torch.uint8, pin_memory=True)
+                pin.copy_(raw)
+                d = torch.empty(raw.numel(), dtype=torch.uint8, device=dev)
+                d.copy_(pin, non_blocking=True)
+                self._graph_tables = getattr(self, "_graph_tables", []) + [(pin, d)]
+                N.call("pa_momentum_multi", N.ptr(d), len(key), c0, float(lr), N.ptr(lr_tensor), float(mu),
+                       int(nesterov), float(grad_scale), N.stream())
+                return
             b = self._flip
             self._flip ^= 1
             if self._events[b] is not None:
@@ -131,7 +144,6 @@ class MomentumMulti:
             if self._pinned[b] is None or self._pinned[b].numel() < raw.numel():
                 self._pinned[b] = torch.empty(raw.numel(), dtype=torch.uint8, pin_memory=True)
             self._pinned[b][:raw.numel()].copy_(raw)
-            dev = entries[0][0].device
             if self._dev is None or self._dev.numel() < raw.numel():
                 self._dev = torch.empty(raw.numel(), dtype=torch.uint8, device=dev)
             self._dev[:raw.numel()].copy_(self._pinned[b][:raw.numel()], non_blocking=True)
