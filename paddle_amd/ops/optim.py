@@ -127,9 +127,14 @@ class MomentumMulti:
             dev = entries[0][0].device
             if torch.cuda.is_current_stream_capturing():
                 # HIP-graph capture (graph-pool gradient addresses): a table of its own,
-                # uploaded by a captured copy from a pinned buffer kept for the graph's
-                # lifetime -- no event waits inside the capture
-                pin = torch.empty(raw.numel(), dtype=torch.uint8, pin_memory=True)
+                # uploaded by a captured copy from a spare pinned buffer set aside by an
+                # earlier eager step (no host allocation or event wait inside a capture)
+                spares = getattr(self, "_spares", [])
+                pin = next((p for p in spares if p.numel() >= raw.numel()), None)
+                if pin is None:
+                    raise RuntimeError("MomentumMulti: run one eager step before capturing it in a HIP graph")
+                spares.remove(pin)
+                pin = pin[:raw.numel()]
                 pin.copy_(raw)
                 d = torch.empty(raw.numel(), dtype=torch.uint8, device=dev)
                 d.copy_(pin, non_blocking=True)
@@ -143,6 +148,8 @@ class MomentumMulti:
                 self._events[b].synchronize()
             if self._pinned[b] is None or self._pinned[b].numel() < raw.numel():
                 self._pinned[b] = torch.empty(raw.numel(), dtype=torch.uint8, pin_memory=True)
+                # pinned buffers for up to two later HIP-graph captures of this step
+                self._spares = [torch.empty(raw.numel(), dtype=torch.uint8, pin_memory=True) for _ in range(2)]
             self._pinned[b][:raw.numel()].copy_(raw)
             if self._dev is None or self._dev.numel() < raw.numel():
                 self._dev = torch.empty(raw.numel(), dtype=torch.uint8, device=dev)
