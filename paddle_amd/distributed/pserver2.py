@@ -377,6 +377,7 @@ class ParameterClient2:
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
             self.servers.append(s)
         self.trainer_id = int(trainer_id)
+        self.timeout = float(timeout)
         self.names, self.sizes, self.shapes, self.sparse = [], {}, {}, {}
         self.block_size = {}
 
@@ -437,12 +438,16 @@ class ParameterClient2:
         else:
             import time
 
+            deadline = time.monotonic() + self.timeout
             while True:
                 st = self._call_all("getStatus", ["Empty"] * len(self.servers), [{}] * len(self.servers),
                                     [[]] * len(self.servers))
                 if all(cp.decode("GetStatusResponse", r[1]).get("status") == PSERVER_STATUS_PARAMETER_READY
                        for r in st):
                     break
+                if time.monotonic() > deadline:
+                    raise TimeoutError(f"pserver2: trainer {self.trainer_id}: parameters not ready after "
+                                       f"{self.timeout:.0f} s (trainer 0 sets them)")
                 time.sleep(0.01)
         return self.get_parameters()
 
