@@ -1418,6 +1418,138 @@ void k_delete_var(const OpRun& r) {
 }  // namespace
 
 // ---------------------------------------------------------------- registration
+
+// ---------------------------------------------------------------- sequence (LoD) ops
+// sequence_pool_op.h / math/sequence_pooling.cc over the last LoD level; an empty
+// sequence pools to 0.  Out drops the last level; MaxIndex (int32) for MAX.
+const std::vector<size_t>& last_level(const Tensor& x, const char* op) {
+  PA_CHECK(!x.lod.empty(), "%s: the input has no LoD", op);
+  return x.lod.back();
+}
+
+void k_sequence_pool(const OpRun& r) {
+  Tensor& x = r.in("X");
+  const auto& off = last_level(x, "sequence_pool");
+  const std::string pt = r.op.GetString("pooltype", "AVERAGE");
+  const int64_t n = (int64_t)off.size() - 1, D = x.dims[0] ? x.numel() / x.dims[0] : 0;
+  Dims od = x.dims;
+  od[0] = n;
+  Tensor* o = r.out("Out");
+  float* y = o->alloc<float>(od, -1);
+  int32_t* mi = nullptr;
+  if (Tensor* m = r.out("MaxIndex")) {  // always produced (a gradient program reads its shape)
+    int32_t* p = m->alloc<int32_t>(od, -1);
+    std::fill_n(p, n * D, 0);
+    if (pt == "MAX") mi = p;
+  }
+  const float* xp = f32(x);
+  parallel_for(n, 4, [&](int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i) {
+      const int64_t s = (int64_t)off[(size_t)i], e = (int64_t)off[(size_t)i + 1], len = e - s;
+      for (int64_t d = 0; d < D; ++d) {
+        float v = 0.f;
+        if (len > 0) {
+          if (pt == "SUM" || pt == "AVERAGE" || pt == "SQRT") {
+            double acc = 0;
+            for (int64_t t = s; t < e; ++t) acc += xp[t * D + d];
+            v = (float)(pt == "SUM" ? acc : pt == "AVERAGE" ? acc / (double)len : acc / std::sqrt((double)len));
+          } else if (pt == "MAX") {
+            int64_t best = s;
+            for (int64_t t = s + 1; t < e; ++t)
+              if (xp[t * D + d] > xp[best * D + d]) best = t;
+            v = xp[best * D + d];
+            if (mi) mi[i * D + d] = (int32_t)best;
+          } else if (pt == "LAST") {
+            v = xp[(e - 1) * D + d];
+          } else if (pt == "FIRST") {
+            v = xp[s * D + d];
+          } else {
+            fail("sequence_pool: unknown pooltype %s", pt.c_str());
+          }
+        } else if (mi) {
+          mi[i * D + d] = -1;
+        }
+        y[i * D + d] = v;
+      }
+    }
+  });
+  o->lod.assign(x.lod.begin(), x.lod.end() - 1);
+}
+
+// the MAX gradient goes to the first maximum, recomputed from X (the forward's
+// MaxIndex may come from another kernel)
+void k_sequence_pool_grad(const OpRun& r) {
+  Tensor& x = r.in("X");
+  Tensor& g = r.in("Out@GRAD");
+  const auto& off = last_level(x, "sequence_pool_grad");
+  const std::string pt = r.op.GetString("pooltype", "AVERAGE");
+  const int64_t n = (int64_t)off.size() - 1, D = x.dims[0] ? x.numel() / x.dims[0] : 0;
+  Tensor* dxt = r.out("X@GRAD");
+  Dims d0 = x.dims;
+  float* dx = dxt->alloc<float>(d0, -1);
+  std::fill_n(dx, x.numel(), 0.f);
+  const float* xp = f32(x);
+  const float* gp = f32(g);
+  parallel_for(n, 4, [&](int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i) {
+      const int64_t s = (int64_t)off[(size_t)i], e = (int64_t)off[(size_t)i + 1], len = e - s;
+      if (len <= 0) continue;
+      for (int64_t d = 0; d < D; ++d) {
+        const float gv = gp[i * D + d];
+        if (pt == "SUM" || pt == "AVERAGE" || pt == "SQRT") {
+          const float v = pt == "SUM" ? gv : pt == "AVERAGE" ? gv / (float)len : gv / std::sqrt((float)len);
+          for (int64_t t = s; t < e; ++t) dx[t * D + d] = v;
+        } else if (pt == "MAX") {
+          int64_t best = s;
+          for (int64_t t = s + 1; t < e; ++t)
+            if (xp[t * D + d] > xp[best * D + d]) best = t;
+          dx[best * D + d] = gv;
+        } else if (pt == "LAST") {
+          dx[(e - 1) * D + d] = gv;
+        } else {
+          dx[s * D + d] = gv;
+        }
+      }
+    }
+  });
+  dxt->lod = x.lod;
+}
+
+void k_sequence_softmax(const OpRun& r) {
+  Tensor& x = r.in("X");
+  const auto& off = last_level(x, "sequence_softmax");
+  Tensor* o = r.out("Out");
+  Dims d = x.dims;
+  float* y = o->alloc<float>(d, -1);
+  const float* xp = f32(x);
+  for (size_t i = 0; i + 1 < off.size(); ++i) {
+    const int64_t s = (int64_t)off[i], e = (int64_t)off[i + 1];
+    if (e > s) softmax_rows(xp + s, y + s, 1, e - s);
+  }
+  o->lod = x.lod;
+}
+
+void k_sequence_softmax_grad(const OpRun& r) {
+  Tensor& y = r.in("Out");
+  Tensor& g = r.in("Out@GRAD");
+  Tensor* xl = r.in_opt("X");
+  const LoD& lod = !y.lod.empty() ? y.lod : (xl ? xl->lod : y.lod);
+  PA_CHECK(!lod.empty(), "sequence_softmax_grad: no LoD");
+  const auto& off = lod.back();
+  Tensor* dxt = r.out("X@GRAD");
+  Dims d = y.dims;
+  float* dx = dxt->alloc<float>(d, -1);
+  const float* yp = f32(y);
+  const float* gp = f32(g);
+  for (size_t i = 0; i + 1 < off.size(); ++i) {
+    const int64_t s = (int64_t)off[i], e = (int64_t)off[i + 1];
+    double dot = 0;
+    for (int64_t t = s; t < e; ++t) dot += (double)yp[t] * gp[t];
+    for (int64_t t = s; t < e; ++t) dx[t] = yp[t] * (gp[t] - (float)dot);
+  }
+  dxt->lod = lod;
+}
+
 PA_HOST_KERNEL(feed, k_feed);
 PA_HOST_KERNEL(fetch, k_fetch);
 PA_HOST_KERNEL(fill_constant, k_fill_constant);
@@ -1534,6 +1666,10 @@ PA_HOST_KERNEL(logical_or, k_logical_or);
 PA_HOST_KERNEL(logical_xor, k_logical_xor);
 PA_HOST_KERNEL(logical_not, k_logical_not);
 PA_HOST_KERNEL(delete_var, k_delete_var);
+PA_HOST_KERNEL(sequence_pool, k_sequence_pool);
+PA_HOST_KERNEL(sequence_pool_grad, k_sequence_pool_grad);
+PA_HOST_KERNEL(sequence_softmax, k_sequence_softmax);
+PA_HOST_KERNEL(sequence_softmax_grad, k_sequence_softmax_grad);
 
 void link_host_kernels() {}
 

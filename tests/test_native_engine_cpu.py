@@ -42,12 +42,12 @@ def test_native_engine_updates_python_scope_in_place():
 
 
 def test_native_engine_python_fallback_lod_and_control_flow():
-    """Ops without a C++ kernel (sequence_softmax on a LoD feed) run through the
+    """Ops without a C++ kernel (sequence_conv on a LoD feed) run through the
     executor's per-op Python fallback; programs needing per-step scopes raise."""
     main, startup = fluid.Program(), fluid.Program()
     with fluid.program_guard(main, startup):
         x = fluid.layers.data("x", [4], lod_level=1)
-        y = fluid.layers.sequence_softmax(fluid.layers.fc(x, 1))
+        y = fluid.layers.sequence_conv(fluid.layers.fc(x, 3), num_filters=2, filter_size=3)
     scope = fluid.core.Scope()
     place = fluid.CPUPlace()
     xv = fluid.create_lod_tensor(np.random.RandomState(0).rand(5, 4).astype("float32"), [[2, 3]], place)
@@ -57,7 +57,7 @@ def test_native_engine_python_fallback_lod_and_control_flow():
         exe = fluid.Executor(place, engine="native")
         (got,) = exe.run(main, feed={"x": xv}, fetch_list=[y])
     np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-7)
-    assert exe._native.py_fallbacks.get("sequence_softmax") == 1
+    assert exe._native.py_fallbacks.get("sequence_conv") == 1
 
 
 def test_native_engine_rejects_step_scope_programs():
@@ -123,3 +123,47 @@ def test_auto_engine_takes_plain_programs_and_leaves_step_scope_programs():
         exe.run(startup)
         exe.run(main, feed={"x": xs.astype("float64"), "y": ys.astype("float64")}, fetch_list=[loss])
     assert exe._native is None  # fp64: interpreter
+
+
+def test_native_sequence_ops_train_like_python():
+    """sequence_pool (every pooltype) and sequence_softmax with their gradients run
+    as C++ host kernels of the native executor (no Python fallback) and follow the
+    Python executor's training trajectory on LoD feeds."""
+    main, startup = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, startup):
+        x = fluid.layers.data("x", [6], lod_level=1)
+        lab = fluid.layers.data("lab", [1], dtype="int64")
+        h = fluid.layers.fc(x, 8, act="tanh")
+        pools = [fluid.layers.sequence_pool(h, t) for t in ("sum", "average", "sqrt", "max", "last", "first")]
+        att = fluid.layers.sequence_softmax(fluid.layers.fc(h, 1))
+        pooled = fluid.layers.concat(pools + [fluid.layers.sequence_pool(fluid.layers.elementwise_mul(h, att, axis=0),
+                                                                         "sum")], axis=1)
+        pred = fluid.layers.fc(pooled, 3, act="softmax")
+        loss = fluid.layers.mean(fluid.layers.cross_entropy(pred, lab))
+        fluid.optimizer.SGD(0.3).minimize(loss)
+    startup.random_seed = 7  # the same initial weights for both engines
+    place = fluid.CPUPlace()
+    rs = np.random.RandomState(1)
+    batches = []
+    for _ in range(4):
+        lens = [3, 1, 4, 2]
+        batches.append({"x": fluid.create_lod_tensor(rs.randn(sum(lens), 6).astype("float32"), [lens], place),
+                        "lab": rs.randint(0, 3, (4, 1)).astype("int64")})
+    scope0 = fluid.core.Scope()
+    with fluid.executor.scope_guard(scope0):
+        fluid.Executor(place, engine="python").run(startup)
+    init = {v.name: np.array(scope0.find_var(v.name).get_tensor(), copy=True) for v in main.list_vars()
+            if v.persistable and scope0.find_var(v.name) is not None and v.name not in ("feed", "fetch")}
+    traj = {}
+    for eng in ("python", "native"):
+        scope = fluid.core.Scope()
+        with fluid.executor.scope_guard(scope):
+            for n, v in init.items():
+                scope.var(n).get_tensor().set(v.copy(), place)
+            exe = fluid.Executor(place, engine=eng)
+            traj[eng] = [float(np.asarray(exe.run(main, feed=b, fetch_list=[loss])[0]).reshape(-1)[0])
+                         for b in batches]
+            if eng == "native":
+                fb = dict(exe._native.py_fallbacks)
+    assert not any(k.startswith("sequence_") for k in fb), fb
+    np.testing.assert_allclose(traj["native"], traj["python"], rtol=1e-5, atol=1e-6)
