@@ -68,6 +68,12 @@ int pa_topk(int dt, const void* x, void* vals, long* idx, long rows, int n, int 
 int pa_accuracy(const long* ind, const long* lab, long rows, int k, int* correct, float* acc, int* total,
                 hipStream_t st);
 int pa_mask_mul(int dt, const void* d, const void* mask, void* out, long n, float scale, hipStream_t st);
+int pa_seq_pool(int dt, const void* x, const int* off, void* out, int* maxi, int nseq, int D, int type, float pad,
+                hipStream_t st);
+int pa_seq_pool_grad(int dt, const void* dout, const int* off, const int* maxi, void* dx, int nseq, int D, int type,
+                     hipStream_t st);
+int pa_seq_softmax_fwd(int dtype, const void* x, const long* off, void* y, long nseq, hipStream_t st);
+int pa_seq_softmax_bwd(int dtype, const void* y, const void* dy, const long* off, void* dx, long nseq, hipStream_t st);
 }
 
 // activation ids of fluid_ops.hip enum Act

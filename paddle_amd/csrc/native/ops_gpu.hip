@@ -1019,6 +1019,85 @@ void k_sum(const OpRun& r) {
 
 }  // namespace
 
+
+namespace {
+// ---------------------------------------------------------------- sequence (LoD) ops
+// sequence_pool / sequence_softmax over the last LoD level on the shared kernel
+// library (math/sequence_pooling.cu, sequence_softmax_op.cu); the level's offsets are
+// uploaded to a per-op device scratch (hipMemcpyAsync from pageable memory returns
+// once the source is staged).
+int seq_pool_type(const std::string& pt) {
+  static const char* names[] = {"SUM", "AVERAGE", "SQRT", "MAX", "LAST", "FIRST"};
+  for (int i = 0; i < 6; ++i)
+    if (pt == names[i]) return i;
+  return -1;
+}
+
+template <class T>
+T* upload_offsets(const OpRun& r, const char* name, const std::vector<size_t>& off) {
+  std::vector<T> h(off.begin(), off.end());
+  T* d = reinterpret_cast<T*>(workspace(r, name, (int64_t)(h.size() * sizeof(T) + 3) / 4));
+  HIPCHK(hipMemcpyAsync(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, S(r)));
+  return d;
+}
+
+void k_sequence_pool(const OpRun& r) {
+  Tensor x = r.in("X");
+  const int type = seq_pool_type(r.op.GetString("pooltype", "AVERAGE"));
+  if (x.dtype != DT::FP32 || x.lod.empty() || x.dims.empty() || type < 0) throw Decline();
+  const auto& off = x.lod.back();
+  const int64_t n = (int64_t)off.size() - 1, Dm = x.dims[0] ? x.numel() / x.dims[0] : 0;
+  Dims od = x.dims;
+  od[0] = n;
+  float* y = out_f32(r, "Out", od);
+  Tensor* mt = r.out("MaxIndex");
+  int* mi = mt ? static_cast<int*>(mt->alloc(DT::INT32, od, D(r))) : reinterpret_cast<int*>(workspace(r, "@sp_mi@", n * Dm));
+  if (mt) HIPCHK(hipMemsetAsync(mi, 0, sizeof(int) * n * Dm, S(r)));
+  if (n > 0 && Dm > 0) PA_KL(pa_seq_pool(0, f32(x), upload_offsets<int>(r, "@sp_off@", off), y, mi, (int)n, (int)Dm, type, 0.f, S(r)));
+  r.out("Out")->lod.assign(x.lod.begin(), x.lod.end() - 1);
+}
+
+void k_sequence_pool_grad(const OpRun& r) {
+  Tensor x = r.in("X");
+  Tensor g = r.in("Out@GRAD");
+  const int type = seq_pool_type(r.op.GetString("pooltype", "AVERAGE"));
+  if (x.dtype != DT::FP32 || g.dtype != DT::FP32 || x.lod.empty() || x.dims.empty() || type < 0) throw Decline();
+  Tensor* mt = r.in_opt("MaxIndex");
+  if (type == 3 && (!mt || mt->dtype != DT::INT32 || mt->device != D(r))) throw Decline();
+  const auto& off = x.lod.back();
+  const int64_t n = (int64_t)off.size() - 1, Dm = x.dims[0] ? x.numel() / x.dims[0] : 0;
+  float* dx = out_f32(r, "X@GRAD", x.dims);
+  r.out("X@GRAD")->lod = x.lod;
+  HIPCHK(hipMemsetAsync(dx, 0, sizeof(float) * x.numel(), S(r)));
+  if (n > 0 && Dm > 0)
+    PA_KL(pa_seq_pool_grad(0, f32(g), upload_offsets<int>(r, "@spg_off@", off), type == 3 ? mt->data<int>() : nullptr,
+                           dx, (int)n, (int)Dm, type, S(r)));
+}
+
+void k_sequence_softmax(const OpRun& r) {
+  Tensor x = r.in("X");
+  if (x.dtype != DT::FP32 || x.lod.empty()) throw Decline();
+  const auto& off = x.lod.back();
+  float* y = out_f32(r, "Out", x.dims);
+  r.out("Out")->lod = x.lod;
+  const long n = (long)off.size() - 1;
+  if (n > 0) PA_KL(pa_seq_softmax_fwd(0, f32(x), upload_offsets<long>(r, "@ss_off@", off), y, n, S(r)));
+}
+
+void k_sequence_softmax_grad(const OpRun& r) {
+  Tensor y = r.in("Out");
+  Tensor g = r.in("Out@GRAD");
+  Tensor* xl = r.in_opt("X");
+  const LoD lod = !y.lod.empty() ? y.lod : (xl ? xl->lod : LoD{});
+  if (y.dtype != DT::FP32 || g.dtype != DT::FP32 || lod.empty()) throw Decline();
+  const auto& off = lod.back();
+  float* dx = out_f32(r, "X@GRAD", y.dims);
+  r.out("X@GRAD")->lod = lod;
+  const long n = (long)off.size() - 1;
+  if (n > 0) PA_KL(pa_seq_softmax_bwd(0, f32(y), f32(g), upload_offsets<long>(r, "@ssg_off@", off), dx, n, S(r)));
+}
+}  // namespace
+
 PA_DEVICE_KERNEL(mul, k_mul);
 PA_DEVICE_KERNEL(mul_grad, k_mul_grad);
 PA_DEVICE_KERNEL(fc, k_fc);
@@ -1227,6 +1306,10 @@ PA_DEVICE_KERNEL(lookup_table_grad, k_lookup_table_grad);
 PA_DEVICE_KERNEL(top_k, k_top_k);
 PA_DEVICE_KERNEL(accuracy, k_accuracy);
 PA_DEVICE_KERNEL(dropout_grad, k_dropout_grad);
+PA_DEVICE_KERNEL(sequence_pool, k_sequence_pool);
+PA_DEVICE_KERNEL(sequence_pool_grad, k_sequence_pool_grad);
+PA_DEVICE_KERNEL(sequence_softmax, k_sequence_softmax);
+PA_DEVICE_KERNEL(sequence_softmax_grad, k_sequence_softmax_grad);
 
 void link_device_kernels() {}
 

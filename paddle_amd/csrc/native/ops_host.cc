@@ -1419,6 +1419,7 @@ void k_delete_var(const OpRun& r) {
 
 // ---------------------------------------------------------------- registration
 
+namespace {
 // ---------------------------------------------------------------- sequence (LoD) ops
 // sequence_pool_op.h / math/sequence_pooling.cc over the last LoD level; an empty
 // sequence pools to 0.  Out drops the last level; MaxIndex (int32) for MAX.
@@ -1549,6 +1550,7 @@ void k_sequence_softmax_grad(const OpRun& r) {
   }
   dxt->lod = lod;
 }
+}  // namespace
 
 PA_HOST_KERNEL(feed, k_feed);
 PA_HOST_KERNEL(fetch, k_fetch);

@@ -125,10 +125,9 @@ def test_auto_engine_takes_plain_programs_and_leaves_step_scope_programs():
     assert exe._native is None  # fp64: interpreter
 
 
-def test_native_sequence_ops_train_like_python():
-    """sequence_pool (every pooltype) and sequence_softmax with their gradients run
-    as C++ host kernels of the native executor (no Python fallback) and follow the
-    Python executor's training trajectory on LoD feeds."""
+def seq_ops_trajectories(place):
+    """(python trajectory, native trajectory, native engine's Python fallbacks) of a
+    LoD training program with sequence_pool (every pooltype) and sequence_softmax."""
     main, startup = fluid.Program(), fluid.Program()
     with fluid.program_guard(main, startup):
         x = fluid.layers.data("x", [6], lod_level=1)
@@ -142,7 +141,6 @@ def test_native_sequence_ops_train_like_python():
         loss = fluid.layers.mean(fluid.layers.cross_entropy(pred, lab))
         fluid.optimizer.SGD(0.3).minimize(loss)
     startup.random_seed = 7  # the same initial weights for both engines
-    place = fluid.CPUPlace()
     rs = np.random.RandomState(1)
     batches = []
     for _ in range(4):
@@ -165,5 +163,13 @@ def test_native_sequence_ops_train_like_python():
                          for b in batches]
             if eng == "native":
                 fb = dict(exe._native.py_fallbacks)
+    return traj["python"], traj["native"], fb
+
+
+def test_native_sequence_ops_train_like_python():
+    """sequence_pool (every pooltype) and sequence_softmax with their gradients run
+    as C++ host kernels of the native executor (no Python fallback) and follow the
+    Python executor's training trajectory on LoD feeds."""
+    ref, got, fb = seq_ops_trajectories(fluid.CPUPlace())
     assert not any(k.startswith("sequence_") for k in fb), fb
-    np.testing.assert_allclose(traj["native"], traj["python"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)

@@ -37,3 +37,14 @@ def test_native_engine_links_the_kernel_library():
     assert "libpaddle_amd_native.so" in maps and "libpaddle_amd_kernels.so" in maps
     lib = os.path.join(os.path.dirname(fluid.__file__), "..", "lib", "libpaddle_amd_native.so")
     assert os.path.exists(lib)
+
+
+def test_native_sequence_ops_device_kernels():
+    """sequence_pool / sequence_softmax (+ grads) as device kernels of the native
+    executor (ops_gpu.hip on pa_seq_pool / pa_seq_softmax_*): no host fallback, same
+    trajectory as the Python executor."""
+    from test_native_engine_cpu import seq_ops_trajectories
+
+    ref, got, fb = seq_ops_trajectories(fluid.CUDAPlace(0))
+    assert not any(k.startswith("sequence_") for k in fb), fb
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-5)
