@@ -38,6 +38,8 @@ def main():
     from paddle_amd import nn
 
     dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    if dev.type == "cuda" and os.environ.get("PA_SET_DEVICE", "0") == "1":
+        paddle.set_device("gpu")
     paddle.seed(0)
     model = paddle.vision.models.resnet50(num_classes=a.classes, data_format=a.data_format).to(dev)
     opt = paddle.optimizer.Momentum(learning_rate=0.1, momentum=0.9, parameters=model.parameters(),
@@ -72,8 +74,15 @@ def main():
                 step()
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            static_loss = step()
+        import gc
+
+        gc.collect()
+        gc.disable()  # no pinned-buffer frees (hipHostFree) from the collector mid-capture
+        try:
+            with torch.cuda.graph(g, capture_error_mode=os.environ.get("PA_CAPTURE_MODE", "thread_local")):
+                static_loss = step()
+        finally:
+            gc.enable()
 
         def run():
             g.replay()

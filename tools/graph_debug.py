@@ -11,6 +11,8 @@ from paddle_amd import nn  # noqa: E402
 
 stage = sys.argv[1]
 dev = torch.device("cuda")
+if os.environ.get("SET_DEVICE") == "1":
+    paddle.set_device("gpu")
 paddle.seed(0)
 model = paddle.vision.models.resnet50(num_classes=102, data_format="NHWC").to(dev)
 opt = paddle.optimizer.Momentum(learning_rate=0.1, momentum=0.9, parameters=model.parameters(),
