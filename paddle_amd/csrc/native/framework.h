@@ -260,6 +260,11 @@ void write_lod_tensor(FILE* f, const Tensor& t);
 void load_persistables(const ProgramDesc& prog, Scope* scope, const std::string& dir,
                        const std::string& combined_file, int device, void* stream);
 
+// sequence_expand (sequence_expand_op.h): the X row each output row copies.  X's
+// sequence i (its level-1 LoD, or row i when X has none) repeats len(Y's ref_level
+// sequence i) times; *out_lod receives the expanded level-1 LoD when X has one.
+std::vector<int64_t> sequence_expand_rows(const Tensor& x, const Tensor& y, int ref_level, LoD* out_lod);
+
 // ---------------------------------------------------------------- host math
 // C[M,N] = alpha * op(A) op(B) + beta * C, row-major, fp32, multithreaded.
 void sgemm(bool ta, bool tb, int64_t M, int64_t N, int64_t K, float alpha, const float* A, int64_t lda,

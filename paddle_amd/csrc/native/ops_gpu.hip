@@ -1096,6 +1096,52 @@ void k_sequence_softmax_grad(const OpRun& r) {
   const long n = (long)off.size() - 1;
   if (n > 0) PA_KL(pa_seq_softmax_bwd(0, f32(y), f32(g), upload_offsets<long>(r, "@ssg_off@", off), dx, n, S(r)));
 }
+
+// sequence_expand: the row map (sequence_expand_rows, host) uploaded once per op, then
+// a row gather forward and a row scatter-add (the embedding backward) for X@GRAD
+int64_t* upload_rows(const OpRun& r, const char* name, const std::vector<int64_t>& rows) {
+  int64_t* d = reinterpret_cast<int64_t*>(workspace(r, name, (int64_t)rows.size() * 2));
+  HIPCHK(hipMemcpyAsync(d, rows.data(), rows.size() * sizeof(int64_t), hipMemcpyHostToDevice, S(r)));
+  return d;
+}
+
+void k_sequence_expand(const OpRun& r) {
+  Tensor x = r.in("X");
+  if (x.dtype != DT::FP32 || x.dims.empty()) throw Decline();
+  LoD ol;
+  const auto rows = sequence_expand_rows(x, r.in("Y"), r.op.GetInt("ref_level", -1), &ol);
+  const int64_t n = (int64_t)rows.size(), Dm = x.dims[0] ? x.numel() / x.dims[0] : 0;
+  Dims od = x.dims;
+  od[0] = n;
+  float* y = out_f32(r, "Out", od);
+  r.out("Out")->lod = ol;
+  if (n > 0 && Dm > 0)
+    hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(n * Dm)), dim3(256), 0, S(r), f32(x),
+                       upload_rows(r, "@se_rows@", rows), y, n, Dm, x.dims[0], (int64_t)-1);
+}
+
+void k_sequence_expand_grad(const OpRun& r) {
+  Tensor x = r.in("X");
+  Tensor g = r.in("Out@GRAD");
+  if (x.dtype != DT::FP32 || g.dtype != DT::FP32 || x.dims.empty()) throw Decline();
+  LoD ol;
+  const auto rows = sequence_expand_rows(x, r.in("Y"), r.op.GetInt("ref_level", -1), &ol);
+  const int64_t n = (int64_t)rows.size(), Dm = x.dims[0] ? x.numel() / x.dims[0] : 0;
+  PA_CHECK(g.numel() == n * Dm, "sequence_expand_grad: Out@GRAD has %lld elements, expected %lld",
+           (long long)g.numel(), (long long)(n * Dm));
+  float* dx = out_f32(r, "X@GRAD", x.dims);
+  r.out("X@GRAD")->lod = x.lod;
+  HIPCHK(hipMemsetAsync(dx, 0, sizeof(float) * x.numel(), S(r)));
+  if (n > 0 && Dm > 0)
+    PA_KL(pa_embedding_bwd(0, reinterpret_cast<const long*>(upload_rows(r, "@seg_rows@", rows)), f32(g), dx, n,
+                           (int)Dm, -1, S(r)));
+  if (r.out("Y@GRAD")) {  // Y only shapes the expansion
+    Tensor yt = r.in("Y");
+    float* dy = out_f32(r, "Y@GRAD", yt.dims);
+    r.out("Y@GRAD")->lod = yt.lod;
+    HIPCHK(hipMemsetAsync(dy, 0, sizeof(float) * yt.numel(), S(r)));
+  }
+}
 }  // namespace
 
 PA_DEVICE_KERNEL(mul, k_mul);
@@ -1310,6 +1356,8 @@ PA_DEVICE_KERNEL(sequence_pool, k_sequence_pool);
 PA_DEVICE_KERNEL(sequence_pool_grad, k_sequence_pool_grad);
 PA_DEVICE_KERNEL(sequence_softmax, k_sequence_softmax);
 PA_DEVICE_KERNEL(sequence_softmax_grad, k_sequence_softmax_grad);
+PA_DEVICE_KERNEL(sequence_expand, k_sequence_expand);
+PA_DEVICE_KERNEL(sequence_expand_grad, k_sequence_expand_grad);
 
 void link_device_kernels() {}
 

@@ -1419,6 +1419,39 @@ void k_delete_var(const OpRun& r) {
 
 // ---------------------------------------------------------------- registration
 
+std::vector<int64_t> sequence_expand_rows(const Tensor& x, const Tensor& y, int ref_level, LoD* out_lod) {
+  PA_CHECK(!y.lod.empty(), "sequence_expand: Y has no LoD");
+  const int ref = ref_level < 0 ? (int)y.lod.size() - 1 : ref_level;
+  PA_CHECK(ref < (int)y.lod.size(), "sequence_expand: ref_level %d out of range", ref);
+  const auto& yoff = y.lod[(size_t)ref];
+  const int64_t rows_x = x.dims.empty() ? 0 : x.dims[0];
+  std::vector<int64_t> rows;
+  out_lod->clear();
+  if (yoff.size() <= 1) {  // nothing to expand against: Out = X
+    rows.resize((size_t)rows_x);
+    std::iota(rows.begin(), rows.end(), int64_t{0});
+    *out_lod = x.lod;
+    return rows;
+  }
+  std::vector<size_t> xoff;
+  if (x.lod.size() == 1) {
+    xoff = x.lod[0];
+  } else {  // every row is one sequence; the output carries no LoD
+    xoff.resize((size_t)rows_x + 1);
+    std::iota(xoff.begin(), xoff.end(), size_t{0});
+  }
+  PA_CHECK(xoff.size() == yoff.size(), "sequence_expand: X has %zu sequences, Y's level %d has %zu",
+           xoff.size() - 1, ref, yoff.size() - 1);
+  std::vector<size_t> oo{0};
+  for (size_t i = 0; i + 1 < yoff.size(); ++i)
+    for (size_t k = yoff[i]; k < yoff[i + 1]; ++k) {
+      for (size_t t = xoff[i]; t < xoff[i + 1]; ++t) rows.push_back((int64_t)t);
+      oo.push_back(rows.size());
+    }
+  if (x.lod.size() == 1) out_lod->push_back(std::move(oo));
+  return rows;
+}
+
 namespace {
 // ---------------------------------------------------------------- sequence (LoD) ops
 // sequence_pool_op.h / math/sequence_pooling.cc over the last LoD level; an empty
@@ -1550,6 +1583,45 @@ void k_sequence_softmax_grad(const OpRun& r) {
   }
   dxt->lod = lod;
 }
+
+void k_sequence_expand(const OpRun& r) {
+  Tensor& x = r.in("X");
+  LoD ol;
+  const auto rows = sequence_expand_rows(x, r.in("Y"), r.op.GetInt("ref_level", -1), &ol);
+  const int64_t D = x.dims[0] ? x.numel() / x.dims[0] : 0;
+  Dims od = x.dims;
+  od[0] = (int64_t)rows.size();
+  Tensor* o = r.out("Out");
+  float* y = o->alloc<float>(od, -1);
+  const float* xp = f32(x);
+  parallel_for((int64_t)rows.size(), 16, [&](int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i) std::copy_n(xp + rows[(size_t)i] * D, D, y + i * D);
+  });
+  o->lod = ol;
+}
+
+// X@GRAD[row] = sum of Out@GRAD over the output rows copied from it
+void k_sequence_expand_grad(const OpRun& r) {
+  Tensor& x = r.in("X");
+  Tensor& g = r.in("Out@GRAD");
+  LoD ol;
+  const auto rows = sequence_expand_rows(x, r.in("Y"), r.op.GetInt("ref_level", -1), &ol);
+  const int64_t D = x.dims[0] ? x.numel() / x.dims[0] : 0;
+  PA_CHECK(g.numel() == (int64_t)rows.size() * D, "sequence_expand_grad: Out@GRAD has %lld elements, expected %lld",
+           (long long)g.numel(), (long long)rows.size() * D);
+  Tensor* dxt = r.out("X@GRAD");
+  float* dx = dxt->alloc<float>(x.dims, -1);
+  std::fill_n(dx, x.numel(), 0.f);
+  const float* gp = f32(g);
+  for (size_t i = 0; i < rows.size(); ++i)
+    for (int64_t d = 0; d < D; ++d) dx[rows[i] * D + d] += gp[(int64_t)i * D + d];
+  dxt->lod = x.lod;
+  if (Tensor* dy = r.out("Y@GRAD")) {  // Y only shapes the expansion
+    Tensor& yt = r.in("Y");
+    std::fill_n(dy->alloc<float>(yt.dims, -1), yt.numel(), 0.f);
+    dy->lod = yt.lod;
+  }
+}
 }  // namespace
 
 PA_HOST_KERNEL(feed, k_feed);
@@ -1672,6 +1744,8 @@ PA_HOST_KERNEL(sequence_pool, k_sequence_pool);
 PA_HOST_KERNEL(sequence_pool_grad, k_sequence_pool_grad);
 PA_HOST_KERNEL(sequence_softmax, k_sequence_softmax);
 PA_HOST_KERNEL(sequence_softmax_grad, k_sequence_softmax_grad);
+PA_HOST_KERNEL(sequence_expand, k_sequence_expand);
+PA_HOST_KERNEL(sequence_expand_grad, k_sequence_expand_grad);
 
 void link_host_kernels() {}
 

@@ -127,7 +127,8 @@ def test_auto_engine_takes_plain_programs_and_leaves_step_scope_programs():
 
 def seq_ops_trajectories(place):
     """(python trajectory, native trajectory, native engine's Python fallbacks) of a
-    LoD training program with sequence_pool (every pooltype) and sequence_softmax."""
+    LoD training program with sequence_pool (every pooltype), sequence_softmax and
+    sequence_expand (a pooled vector broadcast back over its sequence)."""
     main, startup = fluid.Program(), fluid.Program()
     with fluid.program_guard(main, startup):
         x = fluid.layers.data("x", [6], lod_level=1)
@@ -135,8 +136,11 @@ def seq_ops_trajectories(place):
         h = fluid.layers.fc(x, 8, act="tanh")
         pools = [fluid.layers.sequence_pool(h, t) for t in ("sum", "average", "sqrt", "max", "last", "first")]
         att = fluid.layers.sequence_softmax(fluid.layers.fc(h, 1))
+        gate = fluid.layers.sequence_expand(pools[3], h)  # each sequence's max, on every step
         pooled = fluid.layers.concat(pools + [fluid.layers.sequence_pool(fluid.layers.elementwise_mul(h, att, axis=0),
-                                                                         "sum")], axis=1)
+                                                                         "sum"),
+                                              fluid.layers.sequence_pool(fluid.layers.elementwise_mul(h, gate),
+                                                                         "average")], axis=1)
         pred = fluid.layers.fc(pooled, 3, act="softmax")
         loss = fluid.layers.mean(fluid.layers.cross_entropy(pred, lab))
         fluid.optimizer.SGD(0.3).minimize(loss)
@@ -167,7 +171,7 @@ def seq_ops_trajectories(place):
 
 
 def test_native_sequence_ops_train_like_python():
-    """sequence_pool (every pooltype) and sequence_softmax with their gradients run
+    """sequence_pool (every pooltype), sequence_softmax and sequence_expand with their gradients run
     as C++ host kernels of the native executor (no Python fallback) and follow the
     Python executor's training trajectory on LoD feeds."""
     ref, got, fb = seq_ops_trajectories(fluid.CPUPlace())
