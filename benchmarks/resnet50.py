@@ -78,8 +78,11 @@ def main():
 
         gc.collect()
         gc.disable()  # no pinned-buffer frees (hipHostFree) from the collector mid-capture
+        # relaxed: HIP refuses hipMalloc while a stream captures in global / thread_local
+        # mode (hipErrorStreamCaptureUnsupported), and the graph pool must grow on the
+        # first capture of a step this size (profiles/r4_rn50_graph_capture.md)
         try:
-            with torch.cuda.graph(g, capture_error_mode=os.environ.get("PA_CAPTURE_MODE", "thread_local")):
+            with torch.cuda.graph(g, capture_error_mode=os.environ.get("PA_CAPTURE_MODE", "relaxed")):
                 static_loss = step()
         finally:
             gc.enable()

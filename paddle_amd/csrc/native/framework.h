@@ -264,6 +264,9 @@ void load_persistables(const ProgramDesc& prog, Scope* scope, const std::string&
 // sequence i (its level-1 LoD, or row i when X has none) repeats len(Y's ref_level
 // sequence i) times; *out_lod receives the expanded level-1 LoD when X has one.
 std::vector<int64_t> sequence_expand_rows(const Tensor& x, const Tensor& y, int ref_level, LoD* out_lod);
+// sequence_expand_as (sequence_expand_as_op.h): row i of X repeated len(Y's sequence i)
+// times; *out_lod = Y's level-1 LoD.
+std::vector<int64_t> sequence_expand_as_rows(const Tensor& x, const Tensor& y, LoD* out_lod);
 
 // ---------------------------------------------------------------- host math
 // C[M,N] = alpha * op(A) op(B) + beta * C, row-major, fp32, multithreaded.

@@ -1105,11 +1105,18 @@ int64_t* upload_rows(const OpRun& r, const char* name, const std::vector<int64_t
   return d;
 }
 
+template <bool AS>
+std::vector<int64_t> expand_rows(const OpRun& r, LoD* ol) {
+  return AS ? sequence_expand_as_rows(r.in("X"), r.in("Y"), ol)
+            : sequence_expand_rows(r.in("X"), r.in("Y"), r.op.GetInt("ref_level", -1), ol);
+}
+
+template <bool AS>
 void k_sequence_expand(const OpRun& r) {
   Tensor x = r.in("X");
   if (x.dtype != DT::FP32 || x.dims.empty()) throw Decline();
   LoD ol;
-  const auto rows = sequence_expand_rows(x, r.in("Y"), r.op.GetInt("ref_level", -1), &ol);
+  const auto rows = expand_rows<AS>(r, &ol);
   const int64_t n = (int64_t)rows.size(), Dm = x.dims[0] ? x.numel() / x.dims[0] : 0;
   Dims od = x.dims;
   od[0] = n;
@@ -1120,12 +1127,13 @@ void k_sequence_expand(const OpRun& r) {
                        upload_rows(r, "@se_rows@", rows), y, n, Dm, x.dims[0], (int64_t)-1);
 }
 
+template <bool AS>
 void k_sequence_expand_grad(const OpRun& r) {
   Tensor x = r.in("X");
   Tensor g = r.in("Out@GRAD");
   if (x.dtype != DT::FP32 || g.dtype != DT::FP32 || x.dims.empty()) throw Decline();
   LoD ol;
-  const auto rows = sequence_expand_rows(x, r.in("Y"), r.op.GetInt("ref_level", -1), &ol);
+  const auto rows = expand_rows<AS>(r, &ol);
   const int64_t n = (int64_t)rows.size(), Dm = x.dims[0] ? x.numel() / x.dims[0] : 0;
   PA_CHECK(g.numel() == n * Dm, "sequence_expand_grad: Out@GRAD has %lld elements, expected %lld",
            (long long)g.numel(), (long long)(n * Dm));
@@ -1356,8 +1364,10 @@ PA_DEVICE_KERNEL(sequence_pool, k_sequence_pool);
 PA_DEVICE_KERNEL(sequence_pool_grad, k_sequence_pool_grad);
 PA_DEVICE_KERNEL(sequence_softmax, k_sequence_softmax);
 PA_DEVICE_KERNEL(sequence_softmax_grad, k_sequence_softmax_grad);
-PA_DEVICE_KERNEL(sequence_expand, k_sequence_expand);
-PA_DEVICE_KERNEL(sequence_expand_grad, k_sequence_expand_grad);
+PA_DEVICE_KERNEL(sequence_expand, k_sequence_expand<false>);
+PA_DEVICE_KERNEL(sequence_expand_grad, k_sequence_expand_grad<false>);
+PA_DEVICE_KERNEL(sequence_expand_as, k_sequence_expand<true>);
+PA_DEVICE_KERNEL(sequence_expand_as_grad, k_sequence_expand_grad<true>);
 
 void link_device_kernels() {}
 

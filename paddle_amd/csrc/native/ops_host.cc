@@ -1452,6 +1452,29 @@ std::vector<int64_t> sequence_expand_rows(const Tensor& x, const Tensor& y, int 
   return rows;
 }
 
+std::vector<int64_t> sequence_expand_as_rows(const Tensor& x, const Tensor& y, LoD* out_lod) {
+  PA_CHECK(!y.lod.empty(), "sequence_expand_as: Y has no LoD");
+  const auto& yoff = y.lod[0];
+  PA_CHECK(!x.dims.empty() && (int64_t)yoff.size() == x.dims[0] + 1,
+           "sequence_expand_as: X has %lld rows, Y has %zu sequences", (long long)(x.dims.empty() ? 0 : x.dims[0]),
+           yoff.size() - 1);
+  std::vector<int64_t> rows;
+  rows.reserve(yoff.back());
+  for (size_t i = 0; i + 1 < yoff.size(); ++i)
+    for (size_t k = yoff[i]; k < yoff[i + 1]; ++k) rows.push_back((int64_t)i);
+  *out_lod = LoD{yoff};
+  return rows;
+}
+
+namespace {
+// the row map of sequence_expand (AS=false) / sequence_expand_as (AS=true)
+template <bool AS>
+std::vector<int64_t> expand_rows(const OpRun& r, LoD* ol) {
+  return AS ? sequence_expand_as_rows(r.in("X"), r.in("Y"), ol)
+            : sequence_expand_rows(r.in("X"), r.in("Y"), r.op.GetInt("ref_level", -1), ol);
+}
+}  // namespace
+
 namespace {
 // ---------------------------------------------------------------- sequence (LoD) ops
 // sequence_pool_op.h / math/sequence_pooling.cc over the last LoD level; an empty
@@ -1584,10 +1607,11 @@ void k_sequence_softmax_grad(const OpRun& r) {
   dxt->lod = lod;
 }
 
+template <bool AS>
 void k_sequence_expand(const OpRun& r) {
   Tensor& x = r.in("X");
   LoD ol;
-  const auto rows = sequence_expand_rows(x, r.in("Y"), r.op.GetInt("ref_level", -1), &ol);
+  const auto rows = expand_rows<AS>(r, &ol);
   const int64_t D = x.dims[0] ? x.numel() / x.dims[0] : 0;
   Dims od = x.dims;
   od[0] = (int64_t)rows.size();
@@ -1601,11 +1625,12 @@ void k_sequence_expand(const OpRun& r) {
 }
 
 // X@GRAD[row] = sum of Out@GRAD over the output rows copied from it
+template <bool AS>
 void k_sequence_expand_grad(const OpRun& r) {
   Tensor& x = r.in("X");
   Tensor& g = r.in("Out@GRAD");
   LoD ol;
-  const auto rows = sequence_expand_rows(x, r.in("Y"), r.op.GetInt("ref_level", -1), &ol);
+  const auto rows = expand_rows<AS>(r, &ol);
   const int64_t D = x.dims[0] ? x.numel() / x.dims[0] : 0;
   PA_CHECK(g.numel() == (int64_t)rows.size() * D, "sequence_expand_grad: Out@GRAD has %lld elements, expected %lld",
            (long long)g.numel(), (long long)rows.size() * D);
@@ -1744,8 +1769,10 @@ PA_HOST_KERNEL(sequence_pool, k_sequence_pool);
 PA_HOST_KERNEL(sequence_pool_grad, k_sequence_pool_grad);
 PA_HOST_KERNEL(sequence_softmax, k_sequence_softmax);
 PA_HOST_KERNEL(sequence_softmax_grad, k_sequence_softmax_grad);
-PA_HOST_KERNEL(sequence_expand, k_sequence_expand);
-PA_HOST_KERNEL(sequence_expand_grad, k_sequence_expand_grad);
+PA_HOST_KERNEL(sequence_expand, k_sequence_expand<false>);
+PA_HOST_KERNEL(sequence_expand_grad, k_sequence_expand_grad<false>);
+PA_HOST_KERNEL(sequence_expand_as, k_sequence_expand<true>);
+PA_HOST_KERNEL(sequence_expand_as_grad, k_sequence_expand_grad<true>);
 
 void link_host_kernels() {}
 

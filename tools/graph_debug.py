@@ -1,5 +1,6 @@
 """Which part of the ResNet-50 bench step breaks HIP-graph capture?
-usage: python tools/graph_debug.py STAGE  (stage: stem | fwd | bwd | step | rn18)"""
+usage: python tools/graph_debug.py STAGE  (stage: plain | stem | fwd | bwd | step)
+env: CAPTURE_MODE (global | thread_local | relaxed), SET_DEVICE=1, NO_AMP=1"""
 import os
 import sys
 
@@ -25,6 +26,8 @@ y = torch.randint(0, 102, (16, 1), device=dev)
 
 
 def step(part):
+    if part == "plain":  # a torch op alone: does capture work in this process at all?
+        return x * 2
     if part == "stem":
         return model.conv1(x)
     out = model(x)
@@ -44,7 +47,7 @@ for _ in range(2):
 torch.cuda.synchronize()
 g = torch.cuda.CUDAGraph()
 try:
-    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+    with torch.cuda.graph(g, capture_error_mode=os.environ.get("CAPTURE_MODE", "thread_local")):
         step(stage)
     print(stage, "CAPTURE OK", flush=True)
 except Exception as e:  # noqa: BLE001
