@@ -267,6 +267,10 @@ std::vector<int64_t> sequence_expand_rows(const Tensor& x, const Tensor& y, int 
 // sequence_expand_as (sequence_expand_as_op.h): row i of X repeated len(Y's sequence i)
 // times; *out_lod = Y's level-1 LoD.
 std::vector<int64_t> sequence_expand_as_rows(const Tensor& x, const Tensor& y, LoD* out_lod);
+// sequence_concat (sequence_concat_op.h): output sequence i = sequence i of every input
+// in turn.  Returns, per input, the output row of each of its rows; *out_lod = the
+// concatenated level-1 LoD.
+std::vector<std::vector<int64_t>> sequence_concat_rows(const std::vector<Tensor*>& xs, LoD* out_lod);
 
 // ---------------------------------------------------------------- host math
 // C[M,N] = alpha * op(A) op(B) + beta * C, row-major, fp32, multithreaded.

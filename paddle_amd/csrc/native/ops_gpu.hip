@@ -1150,6 +1150,57 @@ void k_sequence_expand_grad(const OpRun& r) {
     HIPCHK(hipMemsetAsync(dy, 0, sizeof(float) * yt.numel(), S(r)));
   }
 }
+
+// sequence_concat: each input's rows scattered to their output rows (forward) and
+// gathered back from Out@GRAD (backward), one launch per input over the host row map
+__global__ void scatter_rows_kernel(const float* __restrict__ x, const int64_t* __restrict__ dst,
+                                    float* __restrict__ o, int64_t n, int64_t D) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * D; i += (int64_t)gridDim.x * blockDim.x)
+    o[dst[i / D] * D + (i % D)] = x[i];
+}
+
+int64_t row_width(const Tensor& t) { return t.dims.empty() || t.dims[0] == 0 ? 0 : t.numel() / t.dims[0]; }
+
+void k_sequence_concat(const OpRun& r) {
+  auto xs = r.ins("X");
+  for (Tensor* x : xs)
+    if (x->dtype != DT::FP32 || x->dims.empty() || row_width(*x) != row_width(*xs[0])) throw Decline();
+  LoD ol;
+  const auto dst = sequence_concat_rows(xs, &ol);
+  const int64_t Dm = row_width(*xs[0]);
+  Dims od = xs[0]->dims;
+  od[0] = (int64_t)ol[0].back();
+  float* y = out_f32(r, "Out", od);
+  r.out("Out")->lod = ol;
+  for (size_t k = 0; k < xs.size(); ++k) {
+    const int64_t n = (int64_t)dst[k].size();
+    if (n == 0 || Dm == 0) continue;
+    const std::string ws = "@sc_rows" + std::to_string(k) + "@";
+    hipLaunchKernelGGL(scatter_rows_kernel, dim3(grid_for(n * Dm)), dim3(256), 0, S(r), f32(*xs[k]),
+                       upload_rows(r, ws.c_str(), dst[k]), y, n, Dm);
+  }
+}
+
+void k_sequence_concat_grad(const OpRun& r) {
+  auto xs = r.ins("X");
+  Tensor g = r.in("Out@GRAD");
+  if (g.dtype != DT::FP32) throw Decline();
+  for (Tensor* x : xs)
+    if (x->dtype != DT::FP32 || x->dims.empty()) throw Decline();
+  LoD ol;
+  const auto dst = sequence_concat_rows(xs, &ol);
+  for (size_t k = 0; k < xs.size(); ++k) {
+    Tensor* dxt = r.out("X@GRAD", k);
+    if (!dxt) continue;
+    const int64_t n = (int64_t)dst[k].size(), Dm = row_width(*xs[k]);
+    float* dx = static_cast<float*>(dxt->alloc(DT::FP32, xs[k]->dims, D(r)));
+    dxt->lod = xs[k]->lod;
+    if (n == 0 || Dm == 0) continue;
+    const std::string ws = "@scg_rows" + std::to_string(k) + "@";
+    hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(n * Dm)), dim3(256), 0, S(r), f32(g),
+                       upload_rows(r, ws.c_str(), dst[k]), dx, n, Dm, (int64_t)ol[0].back(), (int64_t)-1);
+  }
+}
 }  // namespace
 
 PA_DEVICE_KERNEL(mul, k_mul);
@@ -1368,6 +1419,8 @@ PA_DEVICE_KERNEL(sequence_expand, k_sequence_expand<false>);
 PA_DEVICE_KERNEL(sequence_expand_grad, k_sequence_expand_grad<false>);
 PA_DEVICE_KERNEL(sequence_expand_as, k_sequence_expand<true>);
 PA_DEVICE_KERNEL(sequence_expand_as_grad, k_sequence_expand_grad<true>);
+PA_DEVICE_KERNEL(sequence_concat, k_sequence_concat);
+PA_DEVICE_KERNEL(sequence_concat_grad, k_sequence_concat_grad);
 
 void link_device_kernels() {}
 

@@ -1466,6 +1466,28 @@ std::vector<int64_t> sequence_expand_as_rows(const Tensor& x, const Tensor& y, L
   return rows;
 }
 
+std::vector<std::vector<int64_t>> sequence_concat_rows(const std::vector<Tensor*>& xs, LoD* out_lod) {
+  PA_CHECK(!xs.empty(), "sequence_concat: no inputs");
+  std::vector<const std::vector<size_t>*> offs;
+  for (const Tensor* x : xs) {
+    PA_CHECK(!x->lod.empty() && !x->dims.empty(), "sequence_concat: an input has no LoD");
+    offs.push_back(&x->lod.back());
+    PA_CHECK(offs.back()->size() == offs[0]->size(), "sequence_concat: inputs hold different sequence counts");
+    PA_CHECK((int64_t)offs.back()->back() == x->dims[0], "sequence_concat: LoD does not cover the rows");
+  }
+  std::vector<std::vector<int64_t>> dst(xs.size());
+  for (size_t k = 0; k < xs.size(); ++k) dst[k].resize((size_t)xs[k]->dims[0]);
+  std::vector<size_t> oo{0};
+  int64_t row = 0;
+  for (size_t i = 0; i + 1 < offs[0]->size(); ++i) {
+    for (size_t k = 0; k < xs.size(); ++k)
+      for (size_t t = (*offs[k])[i]; t < (*offs[k])[i + 1]; ++t) dst[k][t] = row++;
+    oo.push_back((size_t)row);
+  }
+  *out_lod = LoD{oo};
+  return dst;
+}
+
 namespace {
 // the row map of sequence_expand (AS=false) / sequence_expand_as (AS=true)
 template <bool AS>
@@ -1647,6 +1669,41 @@ void k_sequence_expand_grad(const OpRun& r) {
     dy->lod = yt.lod;
   }
 }
+
+int64_t row_width(const Tensor& t) { return t.dims.empty() || t.dims[0] == 0 ? 0 : t.numel() / t.dims[0]; }
+
+void k_sequence_concat(const OpRun& r) {
+  auto xs = r.ins("X");
+  LoD ol;
+  const auto dst = sequence_concat_rows(xs, &ol);
+  const int64_t D = row_width(*xs[0]);
+  Dims od = xs[0]->dims;
+  od[0] = (int64_t)ol[0].back();
+  for (Tensor* x : xs) PA_CHECK(row_width(*x) == D, "sequence_concat: inputs differ in row width");
+  Tensor* o = r.out("Out");
+  float* y = o->alloc<float>(od, -1);
+  for (size_t k = 0; k < xs.size(); ++k) {
+    const float* xp = f32(*xs[k]);
+    for (size_t t = 0; t < dst[k].size(); ++t) std::copy_n(xp + (int64_t)t * D, D, y + dst[k][t] * D);
+  }
+  o->lod = ol;
+}
+
+void k_sequence_concat_grad(const OpRun& r) {
+  auto xs = r.ins("X");
+  Tensor& g = r.in("Out@GRAD");
+  LoD ol;
+  const auto dst = sequence_concat_rows(xs, &ol);
+  const float* gp = f32(g);
+  for (size_t k = 0; k < xs.size(); ++k) {
+    Tensor* dxt = r.out("X@GRAD", k);
+    if (!dxt) continue;
+    const int64_t D = row_width(*xs[k]);
+    float* dx = dxt->alloc<float>(xs[k]->dims, -1);
+    for (size_t t = 0; t < dst[k].size(); ++t) std::copy_n(gp + dst[k][t] * D, D, dx + (int64_t)t * D);
+    dxt->lod = xs[k]->lod;
+  }
+}
 }  // namespace
 
 PA_HOST_KERNEL(feed, k_feed);
@@ -1773,6 +1830,8 @@ PA_HOST_KERNEL(sequence_expand, k_sequence_expand<false>);
 PA_HOST_KERNEL(sequence_expand_grad, k_sequence_expand_grad<false>);
 PA_HOST_KERNEL(sequence_expand_as, k_sequence_expand<true>);
 PA_HOST_KERNEL(sequence_expand_as_grad, k_sequence_expand_grad<true>);
+PA_HOST_KERNEL(sequence_concat, k_sequence_concat);
+PA_HOST_KERNEL(sequence_concat_grad, k_sequence_concat_grad);
 
 void link_host_kernels() {}
 

@@ -36,7 +36,9 @@ def sequence_expand_as(x, y, name=None):
 
 
 def sequence_concat(input, name=None):
-    return simple_op("sequence_concat", {"X": input}, name=name)
+    out = simple_op("sequence_concat", {"X": input}, name=name)
+    out.lod_level = max(int(getattr(v, "lod_level", 0) or 0) for v in input)  # a sequence batch like its inputs
+    return out
 
 
 def sequence_conv(input, num_filters, filter_size=3, filter_stride=1, padding=None, bias_attr=None,

@@ -129,7 +129,7 @@ def seq_ops_trajectories(place):
     """(python trajectory, native trajectory, native engine's Python fallbacks) of a
     LoD training program with sequence_pool (every pooltype), sequence_softmax and
     sequence_expand / sequence_expand_as (pooled vectors broadcast back over their
-    sequences)."""
+    sequences) and sequence_concat."""
     main, startup = fluid.Program(), fluid.Program()
     with fluid.program_guard(main, startup):
         x = fluid.layers.data("x", [6], lod_level=1)
@@ -138,11 +138,14 @@ def seq_ops_trajectories(place):
         pools = [fluid.layers.sequence_pool(h, t) for t in ("sum", "average", "sqrt", "max", "last", "first")]
         att = fluid.layers.sequence_softmax(fluid.layers.fc(h, 1))
         gate = fluid.layers.sequence_expand(pools[3], h)  # each sequence's max, on every step
-        gate = fluid.layers.elementwise_add(gate, fluid.layers.sequence_expand_as(pools[1], h))
+        # X first: the elementwise ops share X's LoD (sequence_expand of a LoD-free X has none)
+        gate = fluid.layers.elementwise_add(fluid.layers.sequence_expand_as(pools[1], h), gate)
         pooled = fluid.layers.concat(pools + [fluid.layers.sequence_pool(fluid.layers.elementwise_mul(h, att, axis=0),
                                                                          "sum"),
                                               fluid.layers.sequence_pool(fluid.layers.elementwise_mul(h, gate),
-                                                                         "average")], axis=1)
+                                                                         "average"),
+                                              fluid.layers.sequence_pool(fluid.layers.sequence_concat([h, gate]),
+                                                                         "max")], axis=1)
         pred = fluid.layers.fc(pooled, 3, act="softmax")
         loss = fluid.layers.mean(fluid.layers.cross_entropy(pred, lab))
         fluid.optimizer.SGD(0.3).minimize(loss)
@@ -173,7 +176,7 @@ def seq_ops_trajectories(place):
 
 
 def test_native_sequence_ops_train_like_python():
-    """sequence_pool (every pooltype), sequence_softmax, sequence_expand(_as) with their gradients run
+    """sequence_pool (every pooltype), sequence_softmax, sequence_expand(_as), sequence_concat with their gradients run
     as C++ host kernels of the native executor (no Python fallback) and follow the
     Python executor's training trajectory on LoD feeds."""
     ref, got, fb = seq_ops_trajectories(fluid.CPUPlace())
