@@ -1672,6 +1672,36 @@ void k_sequence_expand_grad(const OpRun& r) {
 
 int64_t row_width(const Tensor& t) { return t.dims.empty() || t.dims[0] == 0 ? 0 : t.numel() / t.dims[0]; }
 
+// sequence_reshape (sequence_reshape_op.h): the same buffer viewed as [-1, new_dim];
+// offsets scale by width / new_dim.  No data moves, so one kernel serves host and
+// device tensors.
+void k_sequence_reshape(const OpRun& r) {
+  Tensor x = r.in("X");
+  const auto& off = last_level(x, "sequence_reshape");
+  const int64_t D = row_width(x), nd = r.op.GetInt("new_dim", 1);
+  PA_CHECK(nd > 0 && x.dims.size() == 2, "sequence_reshape: X must be 2-D and new_dim positive");
+  LoD ol{{}};
+  for (size_t o : off) {
+    PA_CHECK(((int64_t)o * D) % nd == 0, "sequence_reshape: a sequence of width %lld does not split into rows of %lld",
+             (long long)D, (long long)nd);
+    ol[0].push_back((size_t)((int64_t)o * D / nd));
+  }
+  Tensor* o = r.out("Out");
+  o->share(x);
+  o->dims = {x.numel() / nd, nd};
+  o->lod = ol;
+}
+
+void k_sequence_reshape_grad(const OpRun& r) {
+  Tensor x = r.in("X");
+  Tensor g = r.in("Out@GRAD");
+  PA_CHECK(g.numel() == x.numel(), "sequence_reshape_grad: Out@GRAD does not match X");
+  Tensor* dx = r.out("X@GRAD");
+  dx->share(g);
+  dx->dims = x.dims;
+  dx->lod = x.lod;
+}
+
 void k_sequence_concat(const OpRun& r) {
   auto xs = r.ins("X");
   LoD ol;
@@ -1832,6 +1862,10 @@ PA_HOST_KERNEL(sequence_expand_as, k_sequence_expand<true>);
 PA_HOST_KERNEL(sequence_expand_as_grad, k_sequence_expand_grad<true>);
 PA_HOST_KERNEL(sequence_concat, k_sequence_concat);
 PA_HOST_KERNEL(sequence_concat_grad, k_sequence_concat_grad);
+PA_HOST_KERNEL(sequence_reshape, k_sequence_reshape);
+PA_HOST_KERNEL(sequence_reshape_grad, k_sequence_reshape_grad);
+PA_DEVICE_KERNEL(sequence_reshape, k_sequence_reshape);
+PA_DEVICE_KERNEL(sequence_reshape_grad, k_sequence_reshape_grad);
 
 void link_host_kernels() {}
 

@@ -60,7 +60,9 @@ def sequence_erase(input, tokens, name=None):
 
 
 def sequence_reshape(input, new_dim):
-    return simple_op("sequence_reshape", {"X": input}, {"new_dim": new_dim})
+    out = simple_op("sequence_reshape", {"X": input}, {"new_dim": new_dim})
+    out.lod_level = max(int(getattr(input, "lod_level", 0) or 0), 1)
+    return out
 
 
 def sequence_slice(input, offset, length, name=None):

@@ -129,7 +129,7 @@ def seq_ops_trajectories(place):
     """(python trajectory, native trajectory, native engine's Python fallbacks) of a
     LoD training program with sequence_pool (every pooltype), sequence_softmax and
     sequence_expand / sequence_expand_as (pooled vectors broadcast back over their
-    sequences) and sequence_concat."""
+    sequences), sequence_concat and sequence_reshape."""
     main, startup = fluid.Program(), fluid.Program()
     with fluid.program_guard(main, startup):
         x = fluid.layers.data("x", [6], lod_level=1)
@@ -145,7 +145,9 @@ def seq_ops_trajectories(place):
                                               fluid.layers.sequence_pool(fluid.layers.elementwise_mul(h, gate),
                                                                          "average"),
                                               fluid.layers.sequence_pool(fluid.layers.sequence_concat([h, gate]),
-                                                                         "max")], axis=1)
+                                                                         "max"),
+                                              fluid.layers.sequence_pool(fluid.layers.sequence_reshape(h, 4),
+                                                                         "sum")], axis=1)
         pred = fluid.layers.fc(pooled, 3, act="softmax")
         loss = fluid.layers.mean(fluid.layers.cross_entropy(pred, lab))
         fluid.optimizer.SGD(0.3).minimize(loss)
@@ -176,7 +178,7 @@ def seq_ops_trajectories(place):
 
 
 def test_native_sequence_ops_train_like_python():
-    """sequence_pool (every pooltype), sequence_softmax, sequence_expand(_as), sequence_concat with their gradients run
+    """sequence_pool (every pooltype), sequence_softmax, sequence_expand(_as), sequence_concat, sequence_reshape with their gradients run
     as C++ host kernels of the native executor (no Python fallback) and follow the
     Python executor's training trajectory on LoD feeds."""
     ref, got, fb = seq_ops_trajectories(fluid.CPUPlace())
