@@ -66,6 +66,9 @@ def main():
     ap.add_argument("--sharding-stage", type=int, default=3)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"], help="cpu: gloo rehearsal (tiny models)")
     ap.add_argument("--layers", type=int, default=None, help="debug: override layer count (result INVALID)")
+    ap.add_argument("--fixed-batch", action="store_true",
+                    help="re-feed ONE batch every micro-step (memorisation probe; default: a pool of distinct batches)")
+    ap.add_argument("--pool", type=int, default=8, help="distinct synthetic batches cycled through")
     argv = sys.argv[1:]
     a = ap.parse_args(argv)
     if a.gpus and "WORLD_SIZE" not in os.environ:
@@ -95,11 +98,21 @@ def main():
                                bucket_mb=a.bucket_mb, grad_dtype=None if a.bf16_grads else torch.float32)
     V = cfg.vocab_size
     g = torch.Generator(device=dev).manual_seed(rank)
-    ids = torch.randint(0, V, (a.micro_batch, a.seq_len + 1), device=dev, generator=g)
+    pool = [torch.randint(0, V, (a.micro_batch, a.seq_len + 1), device=dev, generator=g)
+            for _ in range(1 if a.fixed_batch else a.pool)]
+    it = [0]
+    ce = [0.0]
+    ce_hist = []
 
     def step():
-        # Fleet accumulate_steps: gradient sync only on the last micro-step
+        # Fleet accumulate_steps: gradient sync only on the last micro-step; every
+        # micro-step takes the next batch of the pool (distinct random tokens, so the
+        # loss cannot fall by memorising one batch)
+        tot = 0.0
+        ce[0] = 0.0
         for m in range(a.accum):
+            ids = pool[it[0] % len(pool)]
+            it[0] += 1
             if m < a.accum - 1:
                 with opt.no_sync():
                     loss = model(ids[:, :-1], ids[:, 1:]) / a.accum
@@ -107,19 +120,24 @@ def main():
             else:
                 loss = model(ids[:, :-1], ids[:, 1:]) / a.accum
                 loss.backward()
+            tot = tot + loss.detach()
+            if getattr(model, "last_ce", None) is not None:
+                ce[0] = ce[0] + model.last_ce / a.accum
         opt.step()
         opt.zero_grad()
-        return loss
+        return tot
 
     hist = []
     for _ in range(a.warmup):
         hist.append(step().detach())
+        ce_hist.append(ce[0])
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss = step()
         hist.append(loss.detach())
+        ce_hist.append(ce[0])
     torch.cuda.synchronize()
     comm.barrier()
     dt = torch.tensor([time.perf_counter() - t0], device=dev)
@@ -138,8 +156,11 @@ def main():
                           "config": {"model": a.model, "micro_batch": a.micro_batch, "grad_accum": a.accum, "seq_len": a.seq_len,
                                      "recompute": a.recompute, "grouped_experts": a.grouped_experts,
                                      "grad_dtype": str(opt.grad_dtype), "dw_kmajor": os.environ.get("PADDLE_AMD_DW_KMAJ", "1"), "parallelism": f"dp{world}+sharding_stage1"},
-                          "loss": float(loss) * a.accum,
-                          "losses": [round(float(x) * a.accum, 4) for x in hist]}))
+                          "batches": "fixed" if a.fixed_batch else f"pool of {a.pool}",
+                          "loss": float(loss),
+                          "losses": [round(float(x), 4) for x in hist],
+                          **({"cross_entropy": [round(float(x), 4) for x in ce_hist]}
+                             if getattr(model, "last_ce", None) is not None else {})}))
 
 
 def hybrid_main(a):
@@ -191,10 +212,14 @@ def hybrid_main(a):
     opt = fleet.distributed_optimizer(inner)
     M = st.pipeline_configs["accumulate_steps"]
     gen = torch.Generator(device="cpu").manual_seed(hcg.get_data_parallel_rank() * 131 + hcg.get_sharding_parallel_rank())
-    ids = torch.randint(0, cfg.vocab_size, (M * a.micro_batch, a.seq_len + 1), generator=gen).to(dev)
+    pool = [torch.randint(0, cfg.vocab_size, (M * a.micro_batch, a.seq_len + 1), generator=gen).to(dev)
+            for _ in range(1 if a.fixed_batch else a.pool)]
+    it = [0]
     sync = (lambda: None) if cpu else torch.cuda.synchronize
 
     def step():
+        ids = pool[it[0] % len(pool)]
+        it[0] += 1
         return model.train_batch((ids[:, :-1], ids[:, 1:]), opt)
 
     hist = [float(step()) for _ in range(a.warmup)]

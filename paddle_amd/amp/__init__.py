@@ -67,6 +67,11 @@ class GradScaler:
     def unscale_(self, optimizer):
         if not self.enable or self._unscaled:
             return
+        # data-parallel wrappers reduce the gradients first: the inf check below then
+        # sees the same (averaged) gradients on every rank (HybridParallelOptimizer)
+        pre = getattr(optimizer, "_sync_grads_before_unscale", None)
+        if pre is not None:
+            pre()
         inv = 1.0 / self.scale_v
         # one device flag for every gradient (native isfinite kernel), one host read
         from ..ops import oplib as _oplib

@@ -614,6 +614,39 @@ __global__ void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ d
 
 }  // namespace
 
+// Deterministic split-K: the k slices write fp32 partial slabs into a per-device
+// workspace and one pass sums them in slice order (no float atomics, so the result
+// does not depend on the order in which workgroups finish).  On for every call while
+// pa_sgemm_set_deterministic(1) (FLAGS_cudnn_deterministic, the MoE router).
+static int g_sgemm_det = 0;
+static float* g_sgemm_ws[64];
+static size_t g_sgemm_ws_cap[64];
+
+__global__ __launch_bounds__(256) void sgemm_slab_sum_kernel(const float* __restrict__ ws, float* __restrict__ C,
+                                                             long mn, int ns, float beta_c) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < mn; i += (long)gridDim.x * 256) {
+    float s = 0.f;
+    for (int z = 0; z < ns; ++z) s += ws[(long)z * mn + i];
+    C[i] = beta_c != 0.f ? C[i] + s : s;
+  }
+}
+
+static float* sgemm_ws(size_t floats) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (g_sgemm_ws_cap[dev] < floats) {
+    if (g_sgemm_ws[dev]) hipFree(g_sgemm_ws[dev]);  // synchronises the device
+    g_sgemm_ws[dev] = nullptr;
+    g_sgemm_ws_cap[dev] = 0;
+    if (hipMalloc(&g_sgemm_ws[dev], floats * sizeof(float)) != hipSuccess) return nullptr;
+    g_sgemm_ws_cap[dev] = floats;
+  }
+  return g_sgemm_ws[dev];
+}
+
+PA_EXPORT void pa_sgemm_set_deterministic(int d) { g_sgemm_det = d; }
+PA_EXPORT int pa_sgemm_get_deterministic() { return g_sgemm_det; }
+
 // ================================================================ C ABI
 PA_EXPORT int pa_sgemm(const float* A, long sam, long sak, const float* B, long sbk, long sbn, float* C, long ldc,
                        long M, long N, long K, int Z1, int Z2, long bsA1, long bsB1, long bsC1, long bsA2, long bsB2,
@@ -634,6 +667,8 @@ PA_EXPORT int pa_sgemm(const float* A, long sam, long sak, const float* B, long 
   g.alpha = alpha; g.beta = beta; g.atomic = atomic; g.ksplit = 0;
   g.kbsplit = 0;
   g.nks = 1;
+  int det_ns = 0;
+  float* det_C = nullptr;
   // split for under-filled problems (few output tiles, deep reduction): the k-batch
   // and / or K are cut into slices on z1, accumulated with float atomics (C zeroed
   // here unless the caller already accumulates atomically)
@@ -658,6 +693,21 @@ PA_EXPORT int pa_sgemm(const float* A, long sam, long sak, const float* B, long 
       ks = (ks + SBK - 1) / SBK * SBK;
       nk = (K + ks - 1) / ks;
     }
+    float* ws = (g_sgemm_det && !atomic && nb * nk >= 2 && nb * nk * Z2 <= 65535)
+                    ? sgemm_ws((size_t)(nb * nk) * M * N) : nullptr;
+    if (ws) {
+      // deterministic: one slab per split, then an ordered sum into C (after launch)
+      det_C = C;
+      det_ns = (int)(nb * nk);
+      g.C = ws;
+      g.atomic = 0;
+      g.ksplit = nk > 1 ? ks : 0;
+      g.kbsplit = nb > 1 ? (int)kbs : 0;
+      g.nks = (int)nk;
+      g.bsA1 = g.bsB1 = 0;
+      g.bsC1 = M * N;
+      Z1 = det_ns;
+    } else
     if (nb * nk >= 2 && nb * nk * Z2 <= 65535) {
       if (!atomic && hipMemsetAsync(C, 0, sizeof(float) * M * N, st) != hipSuccess) return (int)hipGetLastError();
       g.atomic = 1;
@@ -670,6 +720,17 @@ PA_EXPORT int pa_sgemm(const float* A, long sam, long sak, const float* B, long 
   }
   const dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)(Z1 * Z2));
   g.Z2 = Z2;
+#define SG_DONE()                                                                                        \
+  do {                                                                                                   \
+    if (det_ns) {                                                                                        \
+      const hipError_t e_ = hipGetLastError();                                                           \
+      if (e_ != hipSuccess) return (int)e_;                                                              \
+      const long mn_ = M * N;                                                                            \
+      hipLaunchKernelGGL(sgemm_slab_sum_kernel, dim3((unsigned)std::min<long>((mn_ + 255) / 256, 4096)),  \
+                         dim3(256), 0, st, g.C, det_C, mn_, det_ns, 0.f);                                \
+    }                                                                                                    \
+    PA_LAUNCH_CHECK();                                                                                   \
+  } while (0)
   const bool ak = sak == 1, bk = sbk == 1;
   // float4 path: 16-B aligned bases and every non-contiguous stride a multiple of 4
   auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
@@ -686,7 +747,7 @@ PA_EXPORT int pa_sgemm(const float* A, long sam, long sak, const float* B, long 
       if (bk) hipLaunchKernelGGL((sgemm_kernel<true, true, false, true>), grid, dim3(256), 0, st, g);
       else hipLaunchKernelGGL((sgemm_kernel<true, false, false, true>), grid, dim3(256), 0, st, g);
     }
-    PA_LAUNCH_CHECK();
+    SG_DONE();
   }
   const bool vec = al(A) && al(B) && m4(ak ? sam : sak) && m4(bk ? sbn : sbk) && m4(bsA1) && m4(bsA2) && m4(bsB1) &&
                    m4(bsB2) && m4(kbA) && m4(kbB) && (ak ? sak == 1 : sam == 1) && (bk ? sbk == 1 : sbn == 1);
@@ -703,7 +764,8 @@ PA_EXPORT int pa_sgemm(const float* A, long sam, long sak, const float* B, long 
     else SG(false, false, false);
   }
 #undef SG
-  PA_LAUNCH_CHECK();
+  SG_DONE();
+#undef SG_DONE
 }
 
 static Geo make_geo(const int* v) {

@@ -23,6 +23,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <string>
 
 #include "framework.h"
 #include "kernel_lib.h"
@@ -1024,8 +1027,7 @@ namespace {
 // ---------------------------------------------------------------- sequence (LoD) ops
 // sequence_pool / sequence_softmax over the last LoD level on the shared kernel
 // library (math/sequence_pooling.cu, sequence_softmax_op.cu); the level's offsets are
-// uploaded to a per-op device scratch (hipMemcpyAsync from pageable memory returns
-// once the source is staged).
+// uploaded to a per-op device scratch through a pinned staging buffer (upload_host).
 int seq_pool_type(const std::string& pt) {
   static const char* names[] = {"SUM", "AVERAGE", "SQRT", "MAX", "LAST", "FIRST"};
   for (int i = 0; i < 6; ++i)
@@ -1033,12 +1035,43 @@ int seq_pool_type(const std::string& pt) {
   return -1;
 }
 
+// Host -> device upload of a small host array into the op's device scratch `name`.
+// The source is first copied into a PINNED staging buffer owned by (device, name)
+// and kept alive until the copy has executed: hipMemcpyAsync from pageable memory
+// does not promise to have consumed the source when it returns, and a caller's
+// std::vector dies with the op.  Before the staging buffer is rewritten the event
+// recorded after its previous copy is waited for.  Not capturable into a HIP graph
+// (event sync, pinned allocation): the native executor runs these ops eagerly.
+struct PinnedSlot {
+  void* host = nullptr;
+  size_t cap = 0;
+  hipEvent_t ev = nullptr;
+};
+
+void* upload_host(const OpRun& r, const char* name, const void* src, size_t bytes) {
+  static std::mutex mu;
+  static std::map<std::string, PinnedSlot> slots;
+  void* d = workspace(r, name, (int64_t)(bytes + 3) / 4);
+  if (bytes == 0) return d;
+  std::lock_guard<std::mutex> lk(mu);
+  PinnedSlot& sl = slots[std::string(name) + "@" + std::to_string(D(r))];
+  if (sl.ev) HIPCHK(hipEventSynchronize(sl.ev));
+  else HIPCHK(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
+  if (sl.cap < bytes) {
+    if (sl.host) HIPCHK(hipHostFree(sl.host));
+    sl.cap = std::max(bytes, (size_t)4096);
+    HIPCHK(hipHostMalloc(&sl.host, sl.cap, hipHostMallocDefault));
+  }
+  memcpy(sl.host, src, bytes);
+  HIPCHK(hipMemcpyAsync(d, sl.host, bytes, hipMemcpyHostToDevice, S(r)));
+  HIPCHK(hipEventRecord(sl.ev, S(r)));
+  return d;
+}
+
 template <class T>
 T* upload_offsets(const OpRun& r, const char* name, const std::vector<size_t>& off) {
   std::vector<T> h(off.begin(), off.end());
-  T* d = reinterpret_cast<T*>(workspace(r, name, (int64_t)(h.size() * sizeof(T) + 3) / 4));
-  HIPCHK(hipMemcpyAsync(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, S(r)));
-  return d;
+  return reinterpret_cast<T*>(upload_host(r, name, h.data(), h.size() * sizeof(T)));
 }
 
 void k_sequence_pool(const OpRun& r) {
@@ -1100,9 +1133,7 @@ void k_sequence_softmax_grad(const OpRun& r) {
 // sequence_expand: the row map (sequence_expand_rows, host) uploaded once per op, then
 // a row gather forward and a row scatter-add (the embedding backward) for X@GRAD
 int64_t* upload_rows(const OpRun& r, const char* name, const std::vector<int64_t>& rows) {
-  int64_t* d = reinterpret_cast<int64_t*>(workspace(r, name, (int64_t)rows.size() * 2));
-  HIPCHK(hipMemcpyAsync(d, rows.data(), rows.size() * sizeof(int64_t), hipMemcpyHostToDevice, S(r)));
-  return d;
+  return reinterpret_cast<int64_t*>(upload_host(r, name, rows.data(), rows.size() * sizeof(int64_t)));
 }
 
 template <bool AS>
@@ -1162,6 +1193,7 @@ __global__ void scatter_rows_kernel(const float* __restrict__ x, const int64_t* 
 int64_t row_width(const Tensor& t) { return t.dims.empty() || t.dims[0] == 0 ? 0 : t.numel() / t.dims[0]; }
 
 void k_sequence_concat(const OpRun& r) {
+  if (r.op.GetInt("axis", 0) != 0 || r.op.GetInt("level", 0) != 0) throw Decline();
   auto xs = r.ins("X");
   for (Tensor* x : xs)
     if (x->dtype != DT::FP32 || x->dims.empty() || row_width(*x) != row_width(*xs[0])) throw Decline();
@@ -1169,7 +1201,7 @@ void k_sequence_concat(const OpRun& r) {
   const auto dst = sequence_concat_rows(xs, &ol);
   const int64_t Dm = row_width(*xs[0]);
   Dims od = xs[0]->dims;
-  od[0] = (int64_t)ol[0].back();
+  od[0] = (int64_t)ol.back().back();
   float* y = out_f32(r, "Out", od);
   r.out("Out")->lod = ol;
   for (size_t k = 0; k < xs.size(); ++k) {
@@ -1182,6 +1214,7 @@ void k_sequence_concat(const OpRun& r) {
 }
 
 void k_sequence_concat_grad(const OpRun& r) {
+  if (r.op.GetInt("axis", 0) != 0 || r.op.GetInt("level", 0) != 0) throw Decline();
   auto xs = r.ins("X");
   Tensor g = r.in("Out@GRAD");
   if (g.dtype != DT::FP32) throw Decline();
@@ -1198,7 +1231,7 @@ void k_sequence_concat_grad(const OpRun& r) {
     if (n == 0 || Dm == 0) continue;
     const std::string ws = "@scg_rows" + std::to_string(k) + "@";
     hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(n * Dm)), dim3(256), 0, S(r), f32(g),
-                       upload_rows(r, ws.c_str(), dst[k]), dx, n, Dm, (int64_t)ol[0].back(), (int64_t)-1);
+                       upload_rows(r, ws.c_str(), dst[k]), dx, n, Dm, (int64_t)ol.back().back(), (int64_t)-1);
   }
 }
 }  // namespace

@@ -1474,6 +1474,7 @@ std::vector<std::vector<int64_t>> sequence_concat_rows(const std::vector<Tensor*
     offs.push_back(&x->lod.back());
     PA_CHECK(offs.back()->size() == offs[0]->size(), "sequence_concat: inputs hold different sequence counts");
     PA_CHECK((int64_t)offs.back()->back() == x->dims[0], "sequence_concat: LoD does not cover the rows");
+    PA_CHECK(x->lod.size() == xs[0]->lod.size(), "sequence_concat: inputs differ in LoD levels");
   }
   std::vector<std::vector<int64_t>> dst(xs.size());
   for (size_t k = 0; k < xs.size(); ++k) dst[k].resize((size_t)xs[k]->dims[0]);
@@ -1484,7 +1485,10 @@ std::vector<std::vector<int64_t>> sequence_concat_rows(const std::vector<Tensor*
       for (size_t t = (*offs[k])[i]; t < (*offs[k])[i + 1]; ++t) dst[k][t] = row++;
     oo.push_back((size_t)row);
   }
-  *out_lod = LoD{oo};
+  // reference ConcatLoD at level 0: the upper levels are X[0]'s, the finest level
+  // holds the summed sequence lengths (sequence_concat_op.h ConcatLoD)
+  *out_lod = xs[0]->lod;
+  out_lod->back() = oo;
   return dst;
 }
 
@@ -1702,13 +1706,19 @@ void k_sequence_reshape_grad(const OpRun& r) {
   dx->lod = x.lod;
 }
 
+// axis 0 at LoD level 0 only (the finest level); other forms run the Python kernel
+void seq_concat_attrs_ok(const OpRun& r) {
+  if (r.op.GetInt("axis", 0) != 0 || r.op.GetInt("level", 0) != 0) throw Decline{};
+}
+
 void k_sequence_concat(const OpRun& r) {
+  seq_concat_attrs_ok(r);
   auto xs = r.ins("X");
   LoD ol;
   const auto dst = sequence_concat_rows(xs, &ol);
   const int64_t D = row_width(*xs[0]);
   Dims od = xs[0]->dims;
-  od[0] = (int64_t)ol[0].back();
+  od[0] = (int64_t)ol.back().back();
   for (Tensor* x : xs) PA_CHECK(row_width(*x) == D, "sequence_concat: inputs differ in row width");
   Tensor* o = r.out("Out");
   float* y = o->alloc<float>(od, -1);
@@ -1720,6 +1730,7 @@ void k_sequence_concat(const OpRun& r) {
 }
 
 void k_sequence_concat_grad(const OpRun& r) {
+  seq_concat_attrs_ok(r);
   auto xs = r.ins("X");
   Tensor& g = r.in("Out@GRAD");
   LoD ol;

@@ -178,10 +178,17 @@ bool parse_config(const uint8_t* buf, int len, Opt& o) {
     else r.skip(wt);
   }
   if (!r.ok || o.kind < 1 || o.kind > 4) return false;
-  if (o.kind == 4) { o.beta1 = 0.9; o.beta2 = 0.999; o.eps = 1e-8; }
+  // proto2 defaults of OptimizerConfig.proto: AdamConfig declares none (0), Adagrad /
+  // Adadelta epsilon 1e-5, Adadelta rho 0.9
+  if (o.kind == 4) { o.beta1 = 0.0; o.beta2 = 0.0; o.eps = 0.0; }
   if (o.kind == 3) o.eps = 1e-5;
   for (int w : {3, 4, 5, 6}) parse_sub(subs[w], o, w);
-  if (!lr_set) o.lr.lr = 0.1;  // the reference's default ConstLr(0.1)
+  // an unset lr_policy reads as Const (the enum's first value), so the reference's
+  // "ConstLr(0.1)" fallback never runs: ConstLrConfig / LinearLrConfig default to
+  // learning_rate 1.0 (parameter_optimizer.cc:32-43, OptimizerConfig.proto:70-79)
+  (void)lr_set;
+  o.lr.lr = 1.0;
+  o.lr.a = o.lr.b = 0.0;
   parse_sub(subs[o.lr.policy == 1 ? 13 : 12], o, o.lr.policy == 1 ? 13 : 12);
   return true;
 }

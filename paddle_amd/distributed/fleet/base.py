@@ -74,6 +74,7 @@ class _Fleet:
             dp = world // prod
         topo = CommunicateTopology(dict(dp=dp, **deg))
         self._hcg = HybridCommunicateGroup(topo)
+        self._model_syncs_dp = False
         return self
 
     # ---- queries
@@ -115,6 +116,9 @@ class _Fleet:
         elif hcg.get_data_parallel_world_size() > 1 and hcg.get_sharding_parallel_world_size() == 1:
             from ..parallel import DataParallel
 
+            # DataParallel reduces the gradients itself (end of every backward):
+            # the optimizer wrapper must not reduce them a second time
+            self._model_syncs_dp = True
             return DataParallel(model, group=hcg.get_data_parallel_group(), bucket_mb=st.fuse_grad_size_in_MB)
         else:
             wrapped = model
@@ -148,7 +152,9 @@ class _Fleet:
     def distributed_optimizer(self, optimizer, strategy=None):
         if strategy is not None:
             self._strategy = strategy
-        return HybridParallelOptimizer(optimizer, self._hcg, self._strategy, sharded=getattr(self, "_sharded", None))
+        opt = HybridParallelOptimizer(optimizer, self._hcg, self._strategy, sharded=getattr(self, "_sharded", None),
+                                      model_syncs_dp=getattr(self, "_model_syncs_dp", False))
+        return opt
 
     # ---- checkpoint helpers (rank-0 writes the dp replica)
     def save_persistables(self, executor=None, dirname=None, main_program=None):
@@ -189,8 +195,9 @@ class HybridParallelOptimizer:
       (``fuse_grad_size_in_MB`` buckets in fp32), global-norm clipping over mp / pp,
       then the user optimizer."""
 
-    def __init__(self, optimizer, hcg, strategy, sharded=None):
+    def __init__(self, optimizer, hcg, strategy, sharded=None, model_syncs_dp=False):
         self._inner = optimizer
+        self._skip_dp_sync = bool(model_syncs_dp)
         self.hcg = hcg
         self.strategy = strategy
         self.grad_clip = getattr(optimizer, "_grad_clip", None) or getattr(optimizer, "grad_clip", None)
@@ -200,7 +207,7 @@ class HybridParallelOptimizer:
         # micro-batch, see PipelineParallel)
         self._bucket_sync = None
         W = hcg.get_dp_sharding_world_size() if hcg else 1
-        if sharded is None and W > 1 and (hcg.get_pipe_parallel_world_size() if hcg else 1) == 1:
+        if sharded is None and W > 1 and not model_syncs_dp and (hcg.get_pipe_parallel_world_size() if hcg else 1) == 1:
             from .grad_sync import GradBucketAllReduce
 
             mb = int(getattr(strategy, "fuse_grad_size_in_MB", 64) or 64)
@@ -286,10 +293,8 @@ class HybridParallelOptimizer:
         from .pipeline import PipelineParallel  # noqa: F401  (pipeline syncs dp itself)
 
         if not getattr(self, "_skip_dp_sync", False):
-            if self._bucket_sync is not None:
-                self._bucket_sync.finish()
-            else:
-                self._dp_sync(params)
+            self._sync_grads_before_unscale()
+        self._grads_synced = False
         clip = self.grad_clip
         max_norm = getattr(clip, "clip_norm", clip if isinstance(clip, (int, float)) else None)
         if max_norm:
@@ -310,7 +315,25 @@ class HybridParallelOptimizer:
             for a, v in inner_clip:
                 setattr(self._inner, a, v)
 
+    def _sync_grads_before_unscale(self):
+        """Average the gradients over dp x sharding once per step.  AMP's
+        ``GradScaler.unscale_`` calls this BEFORE it unscales and checks for inf, so
+        every rank tests the same (reduced) gradients and takes the same skip / step
+        decision; ``step()`` then finds them synced."""
+        if getattr(self, "_grads_synced", False) or self._sharded is not None:
+            return
+        if getattr(self, "_skip_dp_sync", False):
+            return
+        if self._bucket_sync is not None:
+            self._bucket_sync.finish()
+        else:
+            self._dp_sync(self._params())
+        self._grads_synced = True
+
     def clear_grad(self, set_to_zero=False):
+        self._grads_synced = False
+        if self._bucket_sync is not None:
+            self._bucket_sync.reset()  # drop what a skipped step (AMP inf) left pending
         if self._sharded is not None:
             self._sharded.zero_grad()
             return

@@ -78,6 +78,13 @@ class TopKGate(Layer):
         # framework region: the fp32 router GEMM runs on the native exact-fp32 MFMA
         # GEMM (pa_sgemm), softmax / top-k / the balance loss on the HIP kernels
         with _strict.region("moe:gate"):
+            if x.is_cuda:
+                # routing must be reproducible: a float-atomic split-K GEMM would let
+                # near-tied experts flip between two runs of the same tokens
+                from ...ops.convnd import deterministic
+
+                with deterministic():
+                    return self._route(x)
             return self._route(x)
 
     def _route(self, x):

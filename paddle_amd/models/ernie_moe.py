@@ -219,6 +219,7 @@ class ErnieMoEForCausalLM(Layer):
         if labels is None:
             return logits
         loss = ops.softmax_cross_entropy(logits, labels, inplace_grad=True)
+        self.last_ce = loss.detach()  # the next-token cross-entropy alone (loss adds the balance term)
         if aux and self.cfg.aux_loss_coeff:
             loss = loss + self.cfg.aux_loss_coeff * torch.stack(aux).mean()
         return loss

@@ -152,20 +152,50 @@ def sequence_expand_as(ctx):
     ctx.set_output("Out", out, [list(yoff)])
 
 
-@register_op("sequence_concat", ["X*"], ["Out"], {}, share_lod=False)
+def _abs_lod(lod):
+    """Every LoD level as absolute row offsets (framework ToAbsOffset)."""
+    out = [list(lv) for lv in lod]
+    for i in range(len(out) - 2, -1, -1):
+        out[i] = [out[i + 1][o] for o in lod[i]]
+    return out
+
+
+def _concat_lod(lods, level):
+    """LoD of the axis-0 concatenation at ``level`` (0 = finest): that level's
+    offsets add up over the inputs, the levels below are re-laid out sequence by
+    sequence (reference sequence_concat_op.h ConcatLoD)."""
+    n, nlev = len(lods), len(lods[0])
+    li = nlev - 1 - level
+    out = [list(lv) for lv in lods[0]]
+    out[li] = [sum(l[li][j] for l in lods) for j in range(len(lods[0][li]))]
+    for i in range(li, nlev - 1):
+        new = [0]
+        for j in range(len(lods[0][i]) - 1):
+            for k in range(n):
+                for m in range(lods[k][i][j], lods[k][i][j + 1]):
+                    new.append(new[-1] + lods[k][i + 1][m + 1] - lods[k][i + 1][m])
+        out[i + 1] = new
+    return out
+
+
+@register_op("sequence_concat", ["X*"], ["Out"], {"axis": 0, "level": 0}, share_lod=False)
 def sequence_concat(ctx):
+    """Per sequence of LoD level ``level`` (0 = the finest), the inputs' slices
+    joined along ``axis``: axis 0 stacks their rows (LoD from ConcatLoD), another
+    axis joins columns of equally long slices (LoD of X[0])."""
     xs = ctx.input_values("X")
-    offs = [v.lod()[-1] for v in xs]
-    rows, out_off = [], [0]
-    n = len(offs[0]) - 1
+    axis, level = int(ctx.attr("axis")), int(ctx.attr("level"))
+    lods = [[list(lv) for lv in v.lod()] for v in xs]
+    if not lods[0] or any(len(l) != len(lods[0]) for l in lods) or level >= len(lods[0]):
+        raise ValueError("sequence_concat: inputs need the same number of LoD levels, more than `level`")
+    li = len(lods[0]) - 1 - level
+    out_lod = _concat_lod(lods, level) if axis == 0 else lods[0]
+    abs_in = [_abs_lod(l)[li] for l in lods]
     parts = []
-    for i in range(n):
-        ln = 0
-        for v, o in zip(xs, offs):
-            parts.append(v.tensor[o[i]:o[i + 1]])
-            ln += o[i + 1] - o[i]
-        out_off.append(out_off[-1] + ln)
-    ctx.set_output("Out", torch.cat(parts, 0), [out_off])
+    for i in range(len(abs_in[0]) - 1):
+        sl = [v.tensor[a[i]:a[i + 1]] for v, a in zip(xs, abs_in)]
+        parts.append(torch.cat(sl, axis))
+    ctx.set_output("Out", torch.cat(parts, 0), out_lod)
 
 
 def _context_index(off, T, cl, cs, up_pad, has_pad):

@@ -60,6 +60,8 @@ _SIGS = {
     "pa_bn_running_update": [_I, _P, _P, _P, _P, _I, _L, _F, _F, _P],
     "pa_momentum_p": [_I, _I, _P, _P, _P, _L, _F, _P, _F, _I, _F, _F, _P],
     "pa_sumsq": [_I, _P, _L, _P, _P],
+    "pa_sgemm_set_deterministic": [_I],
+    "pa_sgemm_get_deterministic": [],
     "pa_transpose2d": [_I, _P, _P, _I, _I, _L, _L, _I, _L, _L, _P],
     "pa_flash_attn_fwd": [_P, _P, _P, _P, _P, _LP, _I, _I, _I, _I, _I, _I, _F, _I, _P],
     "pa_fa_bwd_set_variant": [_I],
@@ -231,6 +233,8 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = _I
+        if os.environ.get("FLAGS_cudnn_deterministic", "0").lower() in ("1", "true", "yes", "on"):
+            L.pa_sgemm_set_deterministic(1)  # no float-atomic split-K anywhere
         _lib = L
         return _lib
 

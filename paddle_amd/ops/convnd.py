@@ -62,6 +62,27 @@ def _arr(vals):
     return a
 
 
+class deterministic:
+    """Within the block every exact-fp32 GEMM (``pa_sgemm``) reduces split-K slices
+    through per-slice slabs summed in a fixed order instead of float atomics, so its
+    result does not depend on workgroup completion order.  Process-wide default:
+    ``FLAGS_cudnn_deterministic=1`` (the reference's determinism flag)."""
+
+    def __init__(self, on=True):
+        self.on, self.prev = int(bool(on)), None
+
+    def __enter__(self):
+        L = N.lib()
+        self.prev = int(L.pa_sgemm_get_deterministic())
+        if self.prev != self.on:
+            L.pa_sgemm_set_deterministic(self.on)
+        return self
+
+    def __exit__(self, *exc):
+        if self.prev != self.on:
+            N.lib().pa_sgemm_set_deterministic(self.prev)
+
+
 def sgemm(A, sam, sak, B, sbk, sbn, C, ldc, M, Nn, K, Z1=1, Z2=1, bs1=(0, 0, 0), bs2=(0, 0, 0), kb=1,
           kbA=0, kbB=0, bias=None, bs_bias2=0, alpha=1.0, beta=0.0, atomic=False, conv=None):
     """Strided batched fp32 GEMM: C[z](m, n) = alpha * sum_b A[z, b](m, :) B[z, b](:, n) (+ bias[m] | + beta C)."""

@@ -433,3 +433,70 @@ def test_pipeline_dp2_pp2_matches_single():
         assert launched > 0  # buckets issued during the last micro-batch's reverse pass
         for n, p in params.items():
             assert torch.allclose(p, ref[n].detach(), atol=2e-5), n
+
+
+# ------------------------------------------------------- dp x mp bucket sync: accumulation and AMP
+def _dp_mp_sync_worker(rank, world, steps, mode):
+    import paddle_amd
+    from paddle_amd.distributed.fleet import DistributedStrategy, TPGroup, fleet
+
+    st = DistributedStrategy()
+    st.hybrid_configs = {"dp_degree": 2, "mp_degree": 2}
+    fleet.init(is_collective=True, strategy=st)
+    hcg = fleet.get_hybrid_communicate_group()
+    cfg = _cfg()
+    torch.manual_seed(0)
+    full = LlamaForCausalLM(cfg, "cpu")
+    sd_full = {k: v.detach() for k, v in full.state_dict().items()}
+    tp = TPGroup(hcg.get_model_parallel_group())
+    m = LlamaForCausalLM(cfg, "cpu", tp=tp)
+    m.load_state_dict(shard_llama_state_dict(sd_full, cfg, hcg.get_model_parallel_rank(), 2))
+    model = fleet.distributed_model(m)
+    opt = fleet.distributed_optimizer(paddle_amd.optimizer.SGD(learning_rate=0.5, parameters=m.parameters()))
+    scaler = paddle_amd.amp.GradScaler(init_loss_scaling=1024.0) if mode == "amp" else None
+    dpr = hcg.get_data_parallel_rank()
+    for s in range(steps):
+        b = _batch(B=4, seed=s).chunk(2)[dpr]
+        if mode == "accum":
+            # two reverse passes before one step: the buckets launched by the first
+            # must not be written back over the accumulated gradients
+            for half in b.chunk(2):
+                (model(half[:, :-1], half[:, 1:]) / 2).backward()
+            opt.step()
+        else:
+            loss = model(b[:, :-1], b[:, 1:])
+            if s == 0 and dpr == 0:
+                loss = loss * float("inf")  # overflow on ONE data-parallel replica only
+            scaler.scale(loss).backward()
+            scaler.step(opt)
+            scaler.update()
+        opt.clear_grad()
+    gs = opt._bucket_sync
+    return hcg.get_model_parallel_rank(), {k: v.detach().clone() for k, v in m.state_dict().items()}, \
+        gs.launch_count, gs.redo_count
+
+
+def _dp_mp_sync_ref(steps, skip_first):
+    cfg = _cfg()
+    torch.manual_seed(0)
+    full = LlamaForCausalLM(cfg, "cpu")
+    opt = torch.optim.SGD(full.parameters(), lr=0.5)
+    for s in range(steps):
+        if skip_first and s == 0:
+            continue
+        b = _batch(B=4, seed=s)
+        full(b[:, :-1], b[:, 1:]).backward()
+        opt.step()
+        opt.zero_grad()
+    return cfg, {k: v.detach() for k, v in full.state_dict().items()}
+
+
+@pytest.mark.parametrize("mode", ["accum", "amp"])
+def test_fleet_dp_bucket_sync_accumulation_and_amp(mode):
+    steps = 2
+    cfg, ref = _dp_mp_sync_ref(steps, skip_first=(mode == "amp"))
+    for mp_rank, sd, launched, redo in run_dist(_dp_mp_sync_worker, 4, steps, mode):
+        assert launched > 0
+        want = shard_llama_state_dict(ref, cfg, mp_rank, 2)
+        for k in want:
+            assert torch.allclose(sd[k], want[k], atol=2e-5, rtol=1e-4), (mode, k)

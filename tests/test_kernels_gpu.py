@@ -191,7 +191,8 @@ def test_rope():
 
 
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("S,D,Hq,Hk", [(256, 128, 4, 4), (384, 128, 4, 2), (200, 64, 2, 2), (1024, 128, 2, 2)])
+@pytest.mark.parametrize("S,D,Hq,Hk", [(256, 128, 4, 4), (384, 128, 4, 2), (200, 64, 2, 2), (1024, 128, 2, 2),
+                                        (256, 128, 8, 2), (320, 128, 10, 2), (2048, 128, 5, 1)])
 def test_flash_attention(causal, S, D, Hq, Hk):
     torch.manual_seed(0)
     B = 2
@@ -210,7 +211,7 @@ def test_flash_attention(causal, S, D, Hq, Hk):
     assert _rel(v.grad, vr.grad) < 2e-2, _rel(v.grad, vr.grad)
 
 
-@pytest.mark.parametrize("S,H,Hk", [(256, 4, 4), (320, 4, 2), (1024, 8, 8)])
+@pytest.mark.parametrize("S,H,Hk", [(256, 4, 4), (320, 4, 2), (1024, 8, 8), (320, 8, 2), (512, 20, 4)])
 def test_rope_attention_packed(S, H, Hk):
     # D = 128 causal runs the partial-slab backward whose dQ epilogue is fused with
     # the inverse rotary (pa_fa_dq_reduce_rope) -- check the dq section separately

@@ -197,6 +197,15 @@ case("sequence_expand", {"X": (xse, [[1, 1, 1]]), "Y": (R(6, 1), [[2, 3, 1]])},
 xsc1, xsc2 = R(3, 2), R(4, 2)
 case("sequence_concat", {"X": [("q0", (xsc1, [[1, 2]])), ("q1", (xsc2, [[3, 1]]))]},
      {"Out": np.concatenate([xsc1[:1], xsc2[:3], xsc1[1:], xsc2[3:]])})
+# two LoD levels (reference sequence_concat_op.h ConcatLoD): level 0 joins the finest
+# sequences, level 1 the outer ones; axis 1 joins the columns of equal-length slices
+xsc3, xsc4 = R(4, 2), R(4, 2)
+case("sequence_concat", {"X": [("q2", (xsc3, [[2, 1], [1, 2, 1]])), ("q3", (xsc4, [[1, 2], [2, 1, 1]]))]},
+     {"Out": np.concatenate([xsc3[0:1], xsc4[0:2], xsc3[1:3], xsc4[2:3], xsc3[3:4], xsc4[3:4]])}, {"level": 0})
+case("sequence_concat", {"X": [("q4", (xsc3, [[2, 1], [1, 2, 1]])), ("q5", (xsc4, [[1, 2], [2, 1, 1]]))]},
+     {"Out": np.concatenate([xsc3[0:3], xsc4[0:2], xsc3[3:4], xsc4[2:4]])}, {"level": 1})
+case("sequence_concat", {"X": [("q6", (xsc3, [[1, 3]])), ("q7", (xsc4, [[1, 3]]))]},
+     {"Out": np.concatenate([xsc3, xsc4], 1)}, {"axis": 1})
 xer = np.array([[2], [1], [2], [3], [1], [5]], "int64")
 case("sequence_erase", {"X": (xer, [[4, 2]])}, {"Out": np.array([[3], [5]], "int64")}, {"tokens": [2, 1]})
 xen = np.array([[1], [2], [3], [4], [5]], "int64")

@@ -36,7 +36,8 @@ def _ref(kind, p, gs, lr, lr_at=None, **kw):
             a0 = a0 + g * g
             p = p - r * g / np.sqrt(a0 + eps) - r * dec * p
         else:
-            b1, b2, eps = kw.get("beta_1", 0.9), kw.get("beta_2", 0.999), kw.get("epsilon", 1e-8)
+            # AdamConfig declares no proto defaults: unset fields read as 0
+            b1, b2, eps = kw.get("beta_1", 0.0), kw.get("beta_2", 0.0), kw.get("epsilon", 0.0)
             a0 = b1 * a0 + (1 - b1) * g
             a1 = b2 * a1 + (1 - b2) * g * g
             p = p - r * np.sqrt(1 - b2 ** n) / (1 - b1 ** n) * (a0 / np.sqrt(a1 + eps) + dec * p)
@@ -44,7 +45,8 @@ def _ref(kind, p, gs, lr, lr_at=None, **kw):
 
 
 CASES = [("sgd", {}), ("sgd", {"momentum": 0.9, "decay": 1e-3}), ("sgd", {"momentum": 0.9, "nesterov": True}),
-         ("adadelta", {"rho": 0.95}), ("adagrad", {"decay": 1e-4}), ("adam", {"beta_1": 0.8, "decay": 1e-3})]
+         ("adadelta", {"rho": 0.95}), ("adagrad", {"decay": 1e-4}),
+         ("adam", {"beta_1": 0.8, "beta_2": 0.99, "epsilon": 1e-8, "decay": 1e-3}), ("adam", {})]
 
 
 @pytest.mark.parametrize("kind,kw", CASES)
@@ -62,7 +64,8 @@ def test_linear_lr_policy_and_state_resume():
     rs = np.random.RandomState(1)
     p0 = rs.randn(64).astype("float32")
     gs = [rs.randn(64).astype("float32") for _ in range(6)]
-    cfg = PO.optimizer_config("adam", lr=0.1, lr_policy="linear", lr_decay_a=0.01, lr_decay_b=0.05)
+    cfg = PO.optimizer_config("adam", lr=0.1, lr_policy="linear", lr_decay_a=0.01, lr_decay_b=0.05, beta_1=0.9,
+                              beta_2=0.999, epsilon=1e-8)
     full = PO.ParameterOptimizer(cfg, p0)
     for g in gs:
         full.update(g)
@@ -74,7 +77,8 @@ def test_linear_lr_policy_and_state_resume():
     for g in gs[3:]:
         resumed.update(g)
     np.testing.assert_array_equal(resumed.weights(), full.weights())
-    np.testing.assert_allclose(full.weights(), _ref("adam", p0, gs, 0.1, lr_at=lambda n: max(0.1 - 0.01 * n, 0.05)),
+    np.testing.assert_allclose(full.weights(), _ref("adam", p0, gs, 0.1, lr_at=lambda n: max(0.1 - 0.01 * n, 0.05), beta_1=0.9,
+                                                    beta_2=0.999, epsilon=1e-8),
                                rtol=1e-5, atol=1e-6)
 
 
@@ -112,10 +116,10 @@ def test_go_pserver_runs_the_native_optimizer(tmp_path):
     svc = PS.PServerService(index=0, checkpoint_interval=0, checkpoint_dir=str(tmp_path), store=store)
     rs = np.random.RandomState(2)
     w0 = rs.randn(5, 6).astype("float32")
-    cfg = {"optimizer_config": PO.optimizer_config("adam", lr=0.02, beta_1=0.85).hex()}
+    cfg = {"optimizer_config": PO.optimizer_config("adam", lr=0.02, beta_1=0.85, beta_2=0.999, epsilon=1e-8).hex()}
     svc.init_param("w", PS._enc(w0), cfg)
     svc.finish_init_params()
-    ref = PO.ParameterOptimizer(PO.optimizer_config("adam", lr=0.02, beta_1=0.85), w0)
+    ref = PO.ParameterOptimizer(PO.optimizer_config("adam", lr=0.02, beta_1=0.85, beta_2=0.999, epsilon=1e-8), w0)
     gs = [rs.randn(5, 6).astype("float32") for _ in range(4)]
     for g in gs[:2]:
         svc.send_grad("w", PS._enc(g))
@@ -128,3 +132,14 @@ def test_go_pserver_runs_the_native_optimizer(tmp_path):
         svc2.send_grad("w", PS._enc(g))
         ref.update(g)
     np.testing.assert_array_equal(PS._dec(svc2.get_param("w")), ref.weights())
+
+
+def test_unset_learning_rate_is_const_lr_one():
+    """lr_policy unset reads as Const and ConstLrConfig.learning_rate defaults to 1.0
+    (reference parameter_optimizer.cc:32-43; its ConstLr(0.1) branch is unreachable)."""
+    rs = np.random.RandomState(3)
+    p0 = rs.randn(9).astype("float32")
+    g = rs.randn(9).astype("float32")
+    o = PO.ParameterOptimizer(cp.encode("OptimizerConfig", {"optimizer": 1}), p0)
+    o.update(g)
+    np.testing.assert_allclose(o.weights(), p0 - g, rtol=1e-6, atol=1e-6)
