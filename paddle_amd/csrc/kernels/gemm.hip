@@ -88,6 +88,19 @@ struct Params {
   // GA conv kernels, bf16 out, bs.x != null: the BatchNorm BACKWARD statistics of the
   // stored gradient instead (sum g, sum g (x - mean); common.h BnBwdSrc), into part
   BnBwdSrc bs;
+  // fused epilogues of the bf16 K x K kernels (EPI template parameter, pa_gemm_epi):
+  //  1 SwiGLU forward: C = the [gate|up] tile with gate and up interleaved in blocks of
+  //    16 columns (block b: gate cols 32b..32b+15, up 32b+16..32b+31); aux = h [M][N/2]
+  //    = silu(gate) * up, computed from the stored (bf16-rounded) tile
+  //  2 SwiGLU backward: the accumulator is da [M][N]; aux = gu [M][2N] in the layout of
+  //    1; C = dgu [M][2N] (dgate, dup at gu's positions) -- da never reaches memory
+  //  3 RoPE (neox, head dim 128): columns < rope_cols are rotated in 128-column heads
+  //    by cos / sin [rope_S][64] at position row % rope_S (the packed QKV projection)
+  void* aux;
+  long ldaux;
+  const float* cosT;
+  const float* sinT;
+  int rope_cols, rope_S;
 };
 
 // LDS image of one operand of one stage: 4 "slabs" of 64 mn x 64 k (8 KiB each);
@@ -359,7 +372,7 @@ __device__ __forceinline__ void quad_mma(f32x4 (&acc)[8][4], const FA (&fa)[4][2
 }
 
 template <bool AK, bool BK, bool OUTF32, bool PF_IN_CLUSTER, bool KFULL, bool GA = false, bool F8 = false, int GM = 0,
-          bool BNB = false>
+          bool BNB = false, int EPI = 0>
 __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -846,9 +859,9 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
     // Loads and stores are buffer ops on the per-tile descriptor with masked lanes
     // sent out of range (load 0 / store dropped): uniform control flow, so hipcc
     // counts its vmcnt waits instead of falling back to vmcnt(0) at every store.
-    constexpr int HB = (F8 || BNB) ? 2 : NIT / 2;  // F8 / BNB epilogues also hold column scales / x, y chunks
+    constexpr int HB = (F8 || BNB || EPI == 3) ? 2 : NIT / 2;  // F8 / BNB / RoPE epilogues hold more per chunk
 #pragma unroll 1
-    for (int h = 0; h < NIT; h += HB) {
+    for (int h = 0; h < (EPI == 2 ? 0 : NIT); h += HB) {
       u32x4 cold[HB];
       if (acc_rd) {
 #pragma unroll
@@ -893,6 +906,30 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
             w = __builtin_bit_cast(u32x4, r);
           }
         }
+        if constexpr (EPI == 3) {
+          // neox rotation of the q / k heads: this chunk (8 of a head's 128 columns)
+          // and its partner 64 columns away, both staged in LDS
+          const int gcol = n0 + ch * 8;
+          if (gcol < p.rope_cols && C_OFF(it, ps) != OOB) {
+            const u16x8 xs = __builtin_bit_cast(u16x8, v);
+            const u16x8 xp = *reinterpret_cast<const u16x8*>(stg + rr * ROWB + (ch ^ 8) * 16);
+            const int rr0_ = it * RPI;
+            const int trow = (rr0_ < GR ? rr0_ : 128 + rr0_ - GR) + GR * ps + tid / CPR;
+            const long pos = (erow0 + m0 + trow) % p.rope_S;
+            const float* cp = p.cosT + pos * 64 + 8 * (ch & 7);
+            const float* sp = p.sinT + pos * 64 + 8 * (ch & 7);
+            const f32x4 c0 = *reinterpret_cast<const f32x4*>(cp), c1 = *reinterpret_cast<const f32x4*>(cp + 4);
+            const f32x4 s0 = *reinterpret_cast<const f32x4*>(sp), s1 = *reinterpret_cast<const f32x4*>(sp + 4);
+            const float sg = (ch & 8) ? 1.f : -1.f;
+            u16x8 r;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float co = e < 4 ? c0[e] : c1[e - 4], si = e < 4 ? s0[e] : s1[e - 4];
+              r[e] = f2bf(bf2f(xs[e]) * co + sg * bf2f(xp[e]) * si);
+            }
+            w = __builtin_bit_cast(u32x4, r);
+          }
+        }
         if constexpr (BNB && GA && !OUTF32) {
           if (bstats && C_OFF(it, ps) != OOB) {
             const u16x8 c = __builtin_bit_cast(u16x8, w);
@@ -909,6 +946,70 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
           }
         }
         __builtin_amdgcn_raw_buffer_store_b128(w, rsC, C_OFF(it, ps), 0, 0);
+      }
+    }
+    if constexpr (EPI == 1) {
+      // (c) h = silu(gate) * up: 16 chunks of 8 h columns per staged row
+      const __amdgpu_buffer_rsrc_t rsH = __builtin_amdgcn_make_buffer_rsrc(
+          (char*)p.aux + ((erow0 + m0) * p.ldaux + n0 / 2) * 2, 0, (int)OOB, 0x00020000);
+#pragma unroll 2
+      for (int it = 0; it < 2 * GR * 16 / NT; ++it) {
+        const int idx = it * NT + tid, rr = idx >> 4, k = idx & 15;
+        const int trow = (rr < GR ? rr : 128 + rr - GR) + GR * ps;
+        const int gch = 4 * (k >> 1) + (k & 1);
+        const u16x8 g = *reinterpret_cast<const u16x8*>(stg + rr * ROWB + gch * 16);
+        const u16x8 u = *reinterpret_cast<const u16x8*>(stg + rr * ROWB + (gch + 2) * 16);
+        u16x8 r;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float gv = bf2f(g[e]);
+          r[e] = f2bf(gv / (1.f + __expf(-gv)) * bf2f(u[e]));
+        }
+        const bool ok = trow < rows_left && n0 / 2 + 8 * k < p.N / 2;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, r), rsH,
+                                               ok ? (unsigned)trow * (unsigned)p.ldaux * 2u + (unsigned)k * 16u : OOB,
+                                               0, 0);
+      }
+    }
+    if constexpr (EPI == 2) {
+      // (c) SwiGLU backward from the staged da tile: for each 8-column da chunk k,
+      // gate / up of the same columns sit at 32 (k >> 1) + 8 (k & 1) (+16) of the
+      // 512-wide gu / dgu tile; four chunks per thread have their gu loads in flight
+      const __amdgpu_buffer_rsrc_t rsG = __builtin_amdgcn_make_buffer_rsrc(
+          (char*)p.aux + ((erow0 + m0) * p.ldaux + 2 * (long)n0) * 2, 0, (int)OOB, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rsD = __builtin_amdgcn_make_buffer_rsrc(
+          (char*)p.C + (cz + (erow0 + m0) * p.ldc + 2 * (long)n0) * 2, 0, (int)OOB, 0x00020000);
+#pragma unroll 1
+      for (int h0 = 0; h0 < 2 * GR * 32 / NT; h0 += 4) {
+        u32x4 gv[4], uv[4];
+        unsigned og[4], od[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int idx = (h0 + u) * NT + tid, rr = idx >> 5, k = idx & 31;
+          const int trow = (rr < GR ? rr : 128 + rr - GR) + GR * ps;
+          const unsigned col = 32u * (unsigned)(k >> 1) + 8u * (unsigned)(k & 1);
+          const bool ok = trow < rows_left && n0 + 8 * k < p.N;
+          og[u] = ok ? (unsigned)trow * (unsigned)p.ldaux * 2u + col * 2u : OOB;
+          od[u] = ok ? (unsigned)trow * (unsigned)p.ldc * 2u + col * 2u : OOB;
+          gv[u] = __builtin_amdgcn_raw_buffer_load_b128(rsG, og[u], 0, 0);
+          uv[u] = __builtin_amdgcn_raw_buffer_load_b128(rsG, ok ? og[u] + 32u : OOB, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int idx = (h0 + u) * NT + tid, rr = idx >> 5, k = idx & 31;
+          const u16x8 d = *reinterpret_cast<const u16x8*>(stg + rr * ROWB + k * 16);
+          const u16x8 g = __builtin_bit_cast(u16x8, gv[u]), up = __builtin_bit_cast(u16x8, uv[u]);
+          u16x8 dg, du;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float gf = bf2f(g[e]), uf = bf2f(up[e]), df = bf2f(d[e]);
+            const float sg = 1.f / (1.f + __expf(-gf));
+            du[e] = f2bf(df * gf * sg);
+            dg[e] = f2bf(df * uf * sg * (1.f + gf * (1.f - sg)));
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dg), rsD, od[u], 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, du), rsD, od[u] == OOB ? OOB : od[u] + 32u, 0, 0);
+        }
       }
     }
     __syncthreads();  // staging reads done (next pass / next tile's DMA into stage 1)
@@ -953,11 +1054,11 @@ static int g_persistent = 1;  // 0: one tile per block (grid = tiles), for A/B r
 static int g_stagger = 1;     // start stagger units per block slot (profiles/r3_gemm_stagger_ab.jsonl: +0.7 % over the step GEMMs)
 
 template <bool AK, bool BK, bool F32, bool PF, bool KFULL, bool GA = false, bool F8 = false, int GM = 0,
-          bool BNB = false>
+          bool BNB = false, int EPI = 0>
 static int launch_v(const Params& p, int batch, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_kernel<AK, BK, F32, PF, KFULL, GA, F8, GM, BNB>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_kernel<AK, BK, F32, PF, KFULL, GA, F8, GM, BNB, EPI>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
@@ -975,7 +1076,7 @@ static int launch_v(const Params& p, int batch, hipStream_t st) {
   const int grid = (GM == 1 || nwg < ncu || !g_persistent) ? nwg : ncu;
   Params pp = p;
   pp.stagger = grid == ncu ? g_stagger : 0;
-  hipLaunchKernelGGL((gemm_kernel<AK, BK, F32, PF, KFULL, GA, F8, GM, BNB>), dim3(grid, GM == 1 ? 1 : batch), dim3(NT),
+  hipLaunchKernelGGL((gemm_kernel<AK, BK, F32, PF, KFULL, GA, F8, GM, BNB, EPI>), dim3(grid, GM == 1 ? 1 : batch), dim3(NT),
                      LDS_BYTES, st, pp);
   return (int)hipGetLastError();
 }
@@ -1132,6 +1233,43 @@ PA_EXPORT int pa_gemm(int a_kmaj, int b_kmaj, int out_f32, const void* A, const 
   PA_G(1, 1, 0) PA_G(1, 0, 0) PA_G(0, 1, 0) PA_G(0, 0, 0)
   PA_G(1, 1, 1) PA_G(1, 0, 1) PA_G(0, 1, 1) PA_G(0, 0, 1)
 #undef PA_G
+  return -1;
+}
+
+// Fused-epilogue GEMMs, both operands K-major, bf16 C (see Params::aux):
+//   epi 1: C [M][N] = A B^T (gate|up interleaved by 16), aux = h [M][N/2] (ldaux)
+//   epi 2: aux = gu [M][2N] (ldaux), C = dgu [M][2N] (ldc) from da = A B^T
+//   epi 3: C [M][N] = A B^T with columns < rope_cols rotated (neox, 128-col heads,
+//          cos/sin [rope_S][64] fp32, position = row % rope_S)
+// K must be a multiple of 64.  Returns -1 for shapes the fused epilogues do not cover.
+PA_EXPORT int pa_gemm_epi(int epi, const void* A, const void* B, void* C, void* aux, long ldaux, int M, int N, int K,
+                          long lda, long ldb, long ldc, const float* cosT, const float* sinT, int rope_cols,
+                          int rope_S, hipStream_t st) {
+  if (M <= 0 || N <= 0) return 0;
+  if ((N & 7) || K <= 0 || (K % gemm::BKT) || (lda & 7) || (ldb & 7) || (ldc & 7)) return -1;
+  gemm::Params p{};
+  p.A = A; p.B = B; p.C = C;
+  p.M = M; p.N = N; p.K = K;
+  p.lda = lda; p.ldb = ldb; p.ldc = ldc;
+  p.alpha = 1.f;
+  p.aux = aux; p.ldaux = ldaux;
+  p.cosT = cosT; p.sinT = sinT; p.rope_cols = rope_cols; p.rope_S = rope_S;
+  p.tiles_m = (M + gemm::BM - 1) / gemm::BM;
+  p.tiles_n = (N + gemm::BN - 1) / gemm::BN;
+  const long out_w = epi == 2 ? 2L * N : N;
+  if ((long)ldc * gemm::BM * 2 >= (long)gemm::OOB || ldc < out_w) return -1;
+  if (epi == 1) {
+    if ((N % 32) || !aux || (ldaux & 7) || ldaux < N / 2 || (long)ldaux * gemm::BM * 2 >= (long)gemm::OOB) return -1;
+    return gemm::launch_v<true, true, false, false, true, false, false, 0, false, 1>(p, 1, st);
+  }
+  if (epi == 2) {
+    if ((N % 16) || !aux || (ldaux & 7) || ldaux < 2L * N || (long)ldaux * gemm::BM * 2 >= (long)gemm::OOB) return -1;
+    return gemm::launch_v<true, true, false, false, true, false, false, 0, false, 2>(p, 1, st);
+  }
+  if (epi == 3) {
+    if (!cosT || !sinT || rope_S <= 0 || (rope_cols % 128) || rope_cols > N || (M % rope_S)) return -1;
+    return gemm::launch_v<true, true, false, false, true, false, false, 0, false, 3>(p, 1, st);
+  }
   return -1;
 }
 

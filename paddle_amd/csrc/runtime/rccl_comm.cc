@@ -14,6 +14,7 @@
 // same soname resolves to that copy), so this library has no link-time RCCL
 // dependency and a missing RCCL is a clean error, not a load failure.
 #include <dlfcn.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -54,10 +55,17 @@ Rccl& rccl() {
   static Rccl r;
   static std::once_flag once;
   std::call_once(once, [] {
-    const char* names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
-    for (const char* n : names) {
-      r.h = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
-      if (r.h) break;
+    // PA_RCCL_LIBRARY: an explicit library with the same C ABI (the multi-rank CPU
+    // tests load a shared-memory fake through it)
+    const char* override_lib = getenv("PA_RCCL_LIBRARY");
+    if (override_lib && *override_lib) {
+      r.h = dlopen(override_lib, RTLD_NOW | RTLD_LOCAL);
+    } else {
+      const char* names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
+      for (const char* n : names) {
+        r.h = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
+        if (r.h) break;
+      }
     }
     if (!r.h) {
       r.err = std::string("librccl not loadable: ") + dlerror();
@@ -129,7 +137,8 @@ __attribute__((visibility("default"))) int pa_rccl_comm_init(const char* id128, 
     g_last_error = r.err;
     return -1;
   }
-  if (hipSetDevice(device) != hipSuccess) {
+  // device < 0: host buffers (a CPU test against a fake library); no device to select
+  if (device >= 0 && hipSetDevice(device) != hipSuccess) {
     g_last_error = "hipSetDevice failed";
     return -1;
   }
@@ -208,6 +217,32 @@ __attribute__((visibility("default"))) int pa_rccl_send(const void* buf, size_t 
 __attribute__((visibility("default"))) int pa_rccl_recv(void* buf, size_t count, int dtype, int peer, void* comm, void* stream) {
   ncclResult_t rc = rccl().Recv(buf, count, dtype, peer, comm, stream);
   return rc ? fail("ncclRecv", rc) : 0;
+}
+
+// All-to-all with per-peer element counts and displacements (expert-parallel token
+// exchange): one ncclSend + one ncclRecv per peer inside ONE group, so RCCL runs the
+// whole exchange as a single fused launch over the xGMI links (no torch.distributed
+// all_to_all_single, no host staging).  Zero-sized pairs are skipped.
+__attribute__((visibility("default"))) int pa_rccl_all_to_all(const void* send, void* recv, const size_t* scount,
+                                                              const size_t* sdispl, const size_t* rcount,
+                                                              const size_t* rdispl, int nranks, int dtype,
+                                                              size_t elem_bytes, void* comm, void* stream) {
+  Rccl& r = rccl();
+  if (!r.Send || !r.Recv) {
+    g_last_error = "librccl has no point-to-point symbols";
+    return -1;
+  }
+  std::lock_guard<std::recursive_mutex> lk(group_mutex());
+  ncclResult_t rc = r.GroupStart();
+  if (rc) return fail("ncclGroupStart", rc);
+  ncclResult_t first = 0;
+  for (int p = 0; p < nranks && !first; ++p) {
+    if (scount[p]) first = r.Send((const char*)send + sdispl[p] * elem_bytes, scount[p], dtype, p, comm, stream);
+    if (!first && rcount[p]) first = r.Recv((char*)recv + rdispl[p] * elem_bytes, rcount[p], dtype, p, comm, stream);
+  }
+  rc = r.GroupEnd();
+  if (first) return fail("ncclSend/ncclRecv", first);
+  return rc ? fail("ncclGroupEnd", rc) : 0;
 }
 
 }  // extern "C"

@@ -83,6 +83,12 @@ def _param(shape, device, dtype, std=None, value=None):
     return torch.nn.Parameter(t.to(dtype))
 
 
+def mlp_interleaved(cfg, tp=None) -> bool:
+    """Whether a (non tensor-parallel) LLaMA block stores gate|up interleaved."""
+    tpd = tp.world_size if tp is not None else 1
+    return tpd == 1 and cfg.intermediate_size % (2 * 8) == 0
+
+
 class LlamaDecoderLayer(Layer):
     def __init__(self, cfg: LlamaConfig, device=None, layer_idx=0, tp=None):
         super().__init__("llama_decoder")
@@ -103,6 +109,9 @@ class LlamaDecoderLayer(Layer):
         self.down_proj = _param([I // tpd, H], device, dt, std / math.sqrt(2 * cfg.num_hidden_layers))
         for n in ("input_layernorm", "post_attention_layernorm"):
             getattr(self, n).no_weight_decay = True
+        # gate|up columns interleaved in 16-column blocks (ops.interleave_gate_up) so the
+        # MLP runs as one fused node; tensor-parallel shards keep [gate | up]
+        self.mlp_interleaved = mlp_interleaved(cfg, tp)
 
     def forward(self, x, residual, cos, sin):
         cfg = self.cfg
@@ -114,15 +123,18 @@ class LlamaDecoderLayer(Layer):
             y, h = ops.rms_norm(x, self.input_layernorm, eps, residual=residual)
         if self.tp is not None:
             y = self.tp.copy_to_region(y)
-        qkv = ops.linear(y, self.qkv_proj)
-        a = ops.rope_attention(qkv, cos, sin, self.nh, self.nkv, causal=True)
+        # QKV projection with the rotary in its epilogue, then flash attention (one node)
+        a = ops.qkv_rope_attention(y, self.qkv_proj, cos, sin, self.nh, self.nkv, causal=True)
         a = ops.linear(a, self.o_proj)
         if self.tp is not None:
             a = self.tp.reduce_from_region(a)
         y2, h2 = ops.rms_norm(a, self.post_attention_layernorm, eps, residual=h)
         if self.tp is not None:
             y2 = self.tp.copy_to_region(y2)
-        m = ops.linear(ops.swiglu(ops.linear(y2, self.gate_up_proj)), self.down_proj)
+        if self.mlp_interleaved:
+            m = ops.swiglu_mlp(y2, self.gate_up_proj, self.down_proj)
+        else:
+            m = ops.linear(ops.swiglu(ops.linear(y2, self.gate_up_proj)), self.down_proj)
         if self.tp is not None:
             m = self.tp.reduce_from_region(m)
         return m, h2
@@ -211,7 +223,8 @@ def shard_llama_state_dict(full: dict, cfg: LlamaConfig, rank: int, world: int) 
             q, kk, vv = v.split([nh * D, nkv * D, nkv * D], dim=1)
             out[k] = torch.cat([t.chunk(world, dim=1)[rank] for t in (q, kk, vv)], dim=1).contiguous()
         elif k.endswith("gate_up_proj"):
-            g, u = v.split([I, I], dim=1)
+            # the full model stores gate|up interleaved (mlp_interleaved); shards are [gate | up]
+            g, u = ops.deinterleave_gate_up(v) if mlp_interleaved(cfg) else v.split([I, I], dim=1)
             out[k] = torch.cat([g.chunk(world, dim=1)[rank], u.chunk(world, dim=1)[rank]], dim=1).contiguous()
         elif k.endswith("o_proj") or k.endswith("down_proj") or k == "embed_tokens":
             out[k] = v.chunk(world, dim=0)[rank].contiguous()

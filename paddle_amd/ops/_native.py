@@ -61,6 +61,7 @@ _SIGS = {
     "pa_momentum_p": [_I, _I, _P, _P, _P, _L, _F, _P, _F, _I, _F, _F, _P],
     "pa_sumsq": [_I, _P, _L, _P, _P],
     "pa_sgemm_set_deterministic": [_I],
+    "pa_gemm_epi": [_I, _P, _P, _P, _P, _L, _I, _I, _I, _L, _L, _L, _P, _P, _I, _I, _P],
     "pa_sgemm_get_deterministic": [],
     "pa_transpose2d": [_I, _P, _P, _I, _I, _L, _L, _I, _L, _L, _P],
     "pa_flash_attn_fwd": [_P, _P, _P, _P, _P, _LP, _I, _I, _I, _I, _I, _I, _F, _I, _P],

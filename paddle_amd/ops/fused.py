@@ -384,33 +384,98 @@ class _RopeAttnFn(torch.autograd.Function):
     def backward(ctx, do):
         packed, o, lse, cos, sin = ctx.saved_tensors
         Hq, Hk, D, causal, scale = ctx.cfg
-        B, S, W = packed.shape
-        nh = Hq + 2 * Hk
-        p4 = packed.view(B, S, nh, D)
-        q, k, v = p4[:, :, :Hq], p4[:, :, Hq:Hq + Hk], p4[:, :, Hq + Hk:]
-        do = _c(do).view(B, S, Hq, D)
-        dqkv = torch.empty_like(packed)
-        d4 = dqkv.view(B, S, nh, D)
-        # dq: summed, inverse-rotated and cast straight into dqkv's dq slot when the
-        # partial-slab kernel runs (else via the fp32 accumulator + one rope pass)
-        rope_out = (dqkv, W, cos, sin)
-        if Hk == Hq:
-            dk, dv = d4[:, :, Hq:2 * Hq], d4[:, :, 2 * Hq:]
-            dq_acc = _fa_bwd(q, k, v, o, do, lse, causal, scale, dk, dv, rope_out)
-        else:
-            dk_e = torch.empty(B, S, Hq, D, dtype=packed.dtype, device=packed.device)
-            dv_e = torch.empty_like(dk_e)
-            dq_acc = _fa_bwd(q, k, v, o, do, lse, causal, scale, dk_e, dv_e, rope_out)
-            d4[:, :, Hq:Hq + Hk] = dk_e.view(B, S, Hk, Hq // Hk, D).sum(3)
-            d4[:, :, Hq + Hk:] = dv_e.view(B, S, Hk, Hq // Hk, D).sum(3)
-        if dq_acc is not None:
-            N.call("pa_rope", 0, 1, N.ptr(dq_acc), Hq * D, N.ptr(dqkv), W, N.ptr(cos), N.ptr(sin), None,
-                   B, S, Hq, Hq, D, 1, N.stream())
-        # dk: inverse rotation in place inside dqkv
-        kview = dqkv.view(B, S, nh * D)[:, :, Hq * D:]
-        N.call("pa_rope", 1, 1, N.ptr(kview), W, N.ptr(kview), W, N.ptr(cos), N.ptr(sin), None,
-               B, S, Hk, Hk, D, 1, N.stream())
-        return dqkv, None, None, None, None, None, None, None
+        return (_rope_attn_backward(packed, o, lse, cos, sin, do, Hq, Hk, D, causal, scale),
+                None, None, None, None, None, None, None)
+
+
+def _rope_attn_backward(packed, o, lse, cos, sin, do, Hq, Hk, D, causal, scale):
+    """dqkv [B, S, (Hq+2Hk)*D] (un-rotated projection gradient) of rotary + flash
+    attention, from the packed rotated q|k|v the forward saved."""
+    B, S, W = packed.shape
+    nh = Hq + 2 * Hk
+    p4 = packed.view(B, S, nh, D)
+    q, k, v = p4[:, :, :Hq], p4[:, :, Hq:Hq + Hk], p4[:, :, Hq + Hk:]
+    do = _c(do).view(B, S, Hq, D)
+    dqkv = torch.empty_like(packed)
+    d4 = dqkv.view(B, S, nh, D)
+    # dq: summed, inverse-rotated and cast straight into dqkv's dq slot when the
+    # partial-slab kernel runs (else via the fp32 accumulator + one rope pass)
+    rope_out = (dqkv, W, cos, sin)
+    if Hk == Hq:
+        dk, dv = d4[:, :, Hq:2 * Hq], d4[:, :, 2 * Hq:]
+        dq_acc = _fa_bwd(q, k, v, o, do, lse, causal, scale, dk, dv, rope_out)
+    else:
+        dk_e = torch.empty(B, S, Hq, D, dtype=packed.dtype, device=packed.device)
+        dv_e = torch.empty_like(dk_e)
+        dq_acc = _fa_bwd(q, k, v, o, do, lse, causal, scale, dk_e, dv_e, rope_out)
+        d4[:, :, Hq:Hq + Hk] = dk_e.view(B, S, Hk, Hq // Hk, D).sum(3)
+        d4[:, :, Hq + Hk:] = dv_e.view(B, S, Hk, Hq // Hk, D).sum(3)
+    if dq_acc is not None:
+        N.call("pa_rope", 0, 1, N.ptr(dq_acc), Hq * D, N.ptr(dqkv), W, N.ptr(cos), N.ptr(sin), None,
+               B, S, Hq, Hq, D, 1, N.stream())
+    # dk: inverse rotation in place inside dqkv
+    kview = dqkv.view(B, S, nh * D)[:, :, Hq * D:]
+    N.call("pa_rope", 1, 1, N.ptr(kview), W, N.ptr(kview), W, N.ptr(cos), N.ptr(sin), None,
+           B, S, Hk, Hk, D, 1, N.stream())
+    return dqkv
+
+
+class _QKVRopeAttnFn(torch.autograd.Function):
+    """The QKV projection, rotary embedding and flash attention as one node.
+
+    Forward: one GEMM whose epilogue applies the neox rotation to the q / k columns
+    (``gemm_epi(EPI_ROPE)``), writing the packed rotated q|k|v the attention kernel
+    reads -- the projection output is never re-read by a separate rotary pass.
+    Backward: the attention backward produces the un-rotated dqkv (as
+    ``_RopeAttnFn``), then the projection's dX / dW GEMMs (as ``_LinearFn``)."""
+
+    @staticmethod
+    def forward(ctx, y, w, cos, sin, Hq, Hk, D, causal, scale):
+        K, W = w.shape
+        y2 = y.reshape(-1, K)
+        T = y2.shape[0]
+        S = y.shape[-2]
+        wt = _weight_t(w, T)
+        packed = torch.empty(T, W, dtype=y.dtype, device=y.device)
+        _G.gemm_epi(_G.EPI_ROPE, _c(y2), wt, T, W, K, out=packed, cos=cos, sin=sin, rope_cols=(Hq + Hk) * D,
+                    rope_S=S)
+        packed = packed.view(*y.shape[:-1], W)
+        B = packed.shape[0]
+        p4 = packed.view(B, S, Hq + 2 * Hk, D)
+        o, lse = _fa_fwd(p4[:, :, :Hq], p4[:, :, Hq:Hq + Hk], p4[:, :, Hq + Hk:], causal, scale)
+        ctx.save_for_backward(y, w, packed, o, lse, cos, sin)
+        ctx.cfg = (Hq, Hk, D, causal, scale)
+        return o.view(B, S, Hq * D)
+
+    @staticmethod
+    def backward(ctx, do):
+        y, w, packed, o, lse, cos, sin = ctx.saved_tensors
+        Hq, Hk, D, causal, scale = ctx.cfg
+        dqkv = _rope_attn_backward(packed, o, lse, cos, sin, do, Hq, Hk, D, causal, scale)
+        dx, dw = _linear_bwd(ctx, y, w, dqkv, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        return dx, dw, None, None, None, None, None, None, None
+
+
+def _qkv_rope_fused_ok(y, w, cos, Hq, Hk):
+    K, W = w.shape
+    T = y.numel() // K
+    D = W // (Hq + 2 * Hk)
+    return (y.is_cuda and y.dtype == torch.bfloat16 and D == 128 and y.dim() == 3 and K % 64 == 0
+            and cos.dtype == torch.float32 and cos.is_contiguous() and cos.shape[-1] == 64
+            and _G.epi_supported(T, W, K, y.reshape(-1, K), w) and _weight_t(w, T) is not None)
+
+
+def qkv_rope_attention(y, w_qkv, cos, sin, num_heads, num_kv_heads=None, causal=True, scale=None):
+    """rope_attention(linear(y, w_qkv), ...) with the rotary fused into the projection
+    GEMM's epilogue on the GPU (D = 128); the unfused ops elsewhere."""
+    Hk = num_kv_heads or num_heads
+    param_ready(w_qkv)
+    D = w_qkv.shape[1] // (num_heads + 2 * Hk)
+    if scale is None:
+        scale = 1.0 / math.sqrt(D)
+    if _qkv_rope_fused_ok(y, w_qkv, cos, num_heads, Hk):
+        return _tape.apply(_QKVRopeAttnFn, y, w_qkv, cos, sin, num_heads, Hk, D, causal, scale)
+    return rope_attention(linear(y, w_qkv), cos, sin, num_heads, Hk, causal=causal, scale=scale)
 
 
 def rope_attention(qkv, cos, sin, num_heads, num_kv_heads=None, causal=True, scale=None):
@@ -556,6 +621,93 @@ def swiglu(x, y=None):
         return _tape.apply(_SwiGLUFn, x)
     g, u = x.chunk(2, -1)
     return (torch.nn.functional.silu(g.float()) * u.float()).to(x.dtype)
+
+
+# ---------------------------------------------------------------- fused SwiGLU MLP
+# gate|up projections stored interleaved in blocks of SWIGLU_BLOCK columns (block b:
+# gate columns 32b..32b+15, up columns 32b+16..32b+31), so one GEMM tile holds both
+# halves of every SwiGLU input and the activation runs in the projection's epilogue.
+SWIGLU_BLOCK = 16
+
+
+def deinterleave_gate_up(gu, block=SWIGLU_BLOCK):
+    """[..., 2I] interleaved gate|up -> (gate [..., I], up [..., I])."""
+    *lead, n2 = gu.shape
+    v = gu.reshape(*lead, n2 // (2 * block), 2, block)
+    return v[..., 0, :].reshape(*lead, n2 // 2), v[..., 1, :].reshape(*lead, n2 // 2)
+
+
+def interleave_gate_up(g, u, block=SWIGLU_BLOCK):
+    """(gate [..., I], up [..., I]) -> [..., 2I] in the interleaved layout."""
+    *lead, n = g.shape
+    return torch.stack([g.reshape(*lead, n // block, block), u.reshape(*lead, n // block, block)], -2) \
+        .reshape(*lead, 2 * n)
+
+
+def swiglu_mlp_fused_ok(x, w_gu, w_down):
+    K, N2 = w_gu.shape
+    T = x.numel() // max(K, 1)
+    return (x.is_cuda and x.dtype == torch.bfloat16 and N2 % 32 == 0 and K % 64 == 0 and w_down.shape[1] % 64 == 0
+            and _G.epi_supported(T, N2, K, x.reshape(-1, K), w_gu) and _weight_t(w_gu, T) is not None
+            and _G.epi_supported(T, N2 // 2, w_down.shape[1], x.reshape(-1, K), w_down))
+
+
+class _SwiGLUMLPFn(torch.autograd.Function):
+    """y = (silu(gate) * up) @ W_down with [gate|up] = x @ W_gu (interleaved layout).
+
+    GPU: the gate|up GEMM writes gu (kept for the backward) AND h = silu(gate) * up
+    from its epilogue (``EPI_SWIGLU_FWD``); the backward's da = dY W_down^T GEMM turns
+    into d(gate|up) in its epilogue (``EPI_SWIGLU_BWD``), so neither h's input pass nor
+    da ever reach memory; then the usual dW / dX GEMMs.  CPU / unsupported shapes:
+    the same math with torch ops."""
+
+    @staticmethod
+    def forward(ctx, x, w_gu, w_down):
+        K, N2 = w_gu.shape
+        x2 = x.reshape(-1, K)
+        T = x2.shape[0]
+        fused = swiglu_mlp_fused_ok(x, w_gu, w_down)
+        if fused:
+            gu = torch.empty(T, N2, dtype=x.dtype, device=x.device)
+            h = torch.empty(T, N2 // 2, dtype=x.dtype, device=x.device)
+            _G.gemm_epi(_G.EPI_SWIGLU_FWD, _c(x2), _weight_t(w_gu, T), T, N2, K, out=gu, aux=h)
+        else:
+            gu = _linear_fwd(x2, w_gu, None)
+            g, u = deinterleave_gate_up(gu)
+            h = (torch.nn.functional.silu(g.float()) * u.float()).to(x.dtype)
+        y = _linear_fwd(h, w_down, None)
+        ctx.save_for_backward(x, w_gu, w_down, gu, h)
+        ctx.fused = fused
+        return y.view(*x.shape[:-1], w_down.shape[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w_gu, w_down, gu, h = ctx.saved_tensors
+        Hd = w_down.shape[1]
+        dy2 = _c(dy).reshape(-1, Hd)
+        T, I = h.shape
+        if ctx.fused:
+            dgu = torch.empty(T, 2 * I, dtype=gu.dtype, device=gu.device)
+            _G.gemm_epi(_G.EPI_SWIGLU_BWD, dy2, w_down, T, I, Hd, out=dgu, aux=gu)
+        else:
+            da = (dy2.float() @ w_down.float().t())
+            g, u = deinterleave_gate_up(gu.float())
+            sg = torch.sigmoid(g)
+            dg = da * u * sg * (1 + g * (1 - sg))
+            du = da * g * sg
+            dgu = interleave_gate_up(dg, du).to(gu.dtype)
+        _, dw_down = _linear_bwd(ctx, h, w_down, dy2, False, ctx.needs_input_grad[2])
+        dx, dw_gu = _linear_bwd(ctx, x.reshape(-1, x.shape[-1]), w_gu, dgu, ctx.needs_input_grad[0],
+                                ctx.needs_input_grad[1])
+        return (dx.view(x.shape) if dx is not None else None), dw_gu, dw_down
+
+
+def swiglu_mlp(x, w_gate_up, w_down):
+    """down(silu(gate) * up) with gate|up = x @ w_gate_up stored INTERLEAVED in
+    16-column blocks (:func:`interleave_gate_up`) -- one fused node."""
+    param_ready(w_gate_up)
+    param_ready(w_down)
+    return _tape.apply(_SwiGLUMLPFn, x, w_gate_up, w_down)
 
 
 # ====================================================================== softmax CE

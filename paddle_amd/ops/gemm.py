@@ -69,6 +69,33 @@ def gemm(a, b, M, N, K, *, a_kmaj, b_kmaj, out=None, out_dtype=torch.bfloat16, b
     return out
 
 
+EPI_SWIGLU_FWD, EPI_SWIGLU_BWD, EPI_ROPE = 1, 2, 3
+
+
+def epi_supported(M, N, K, *mats) -> bool:
+    """Fused-epilogue launches (``gemm_epi``): both operands K-major, K % 64 == 0."""
+    return supported(M, N, K, *mats) and K % 64 == 0
+
+
+def gemm_epi(epi, a, b, M, N, K, *, out, aux=None, cos=None, sin=None, rope_cols=0, rope_S=0):
+    """C = A B^T (A [M, K], B [N, K], both K-major bf16) with a fused epilogue:
+
+    * ``EPI_SWIGLU_FWD``: ``out`` [M, N] = the gate|up projection, gate and up
+      interleaved in 16-column blocks; ``aux`` [M, N/2] receives silu(gate) * up;
+    * ``EPI_SWIGLU_BWD``: the product is da [M, N]; ``aux`` [M, 2N] = gate|up in the
+      same layout; ``out`` [M, 2N] receives (dgate, dup) at gate|up's positions;
+    * ``EPI_ROPE``: ``out`` [M, N] with its first ``rope_cols`` columns rotated
+      (neox) in 128-column heads by ``cos`` / ``sin`` [>= rope_S, 64] fp32 at position
+      row % rope_S."""
+    rc = _nat.lib().pa_gemm_epi(int(epi), _nat.ptr(a), _nat.ptr(b), _nat.ptr(out), _nat.ptr(aux),
+                                aux.stride(0) if aux is not None else 0, M, N, K, a.stride(0), b.stride(0),
+                                out.stride(0), _nat.ptr(cos), _nat.ptr(sin), int(rope_cols), int(rope_S),
+                                _nat.stream())
+    if rc != 0:
+        raise RuntimeError(f"pa_gemm_epi failed (rc={rc}) epi={epi} M={M} N={N} K={K}")
+    return out
+
+
 def linear_fwd(x2, w, bias=None):
     """x2 [M, K] @ w [K, N] (+ bias) -> [M, N] bf16."""
     M, K = x2.shape

@@ -15,11 +15,18 @@ the caller's HIP stream (torch's current stream by default, or the DeviceContext
 comm stream), so they order with the kernels that produced their inputs without a
 host synchronisation, exactly like the framework's own kernels.
 
-``FLAGS_comm_backend=pa_rccl`` routes the GPU collectives of
-:mod:`paddle_amd.parallel.comm` (all-reduce, reduce-scatter, all-gather, broadcast)
-through these communicators instead of ``torch.distributed``'s ProcessGroupNCCL;
-the default stays ``torch`` (the path every multi-rank test and the scaling bench
-have exercised).
+These communicators ARE the GPU communication layer: :mod:`paddle_amd.parallel.comm`
+routes every collective on contiguous device tensors -- all-reduce, reduce-scatter,
+all-gather, broadcast, the expert-parallel all-to-all (grouped ncclSend/ncclRecv)
+and the pipeline's point-to-point exchanges -- through them whenever librccl loads
+(``FLAGS_comm_backend`` = ``auto``, the default, or ``pa_rccl``).
+``FLAGS_comm_backend=torch`` keeps ``torch.distributed``'s ProcessGroupNCCL; gloo /
+host tensors always use ``torch.distributed``.
+
+Failure handling: :meth:`CommContextMap.check_health` polls every communicator's
+asynchronous error (a peer died or timed out) and aborts ALL of them
+(``ncclCommAbort``) before raising, so no rank stays blocked inside a collective;
+the elastic watchdog calls it (``distributed/elastic.py``).
 """
 from __future__ import annotations
 
@@ -56,6 +63,8 @@ def _lib():
         L.pa_rccl_broadcast.argtypes = [P, P, S, I, I, P, P]
         L.pa_rccl_send.argtypes = [P, S, I, I, P, P]
         L.pa_rccl_recv.argtypes = [P, S, I, I, P, P]
+        SP = ctypes.POINTER(ctypes.c_size_t)
+        L.pa_rccl_all_to_all.argtypes = [P, P, SP, SP, SP, SP, I, I, S, P, P]
         _sigs_ready[0] = True
     return L
 
@@ -82,7 +91,9 @@ def unique_id() -> bytes:
     return buf.raw
 
 
-def _stream(stream):
+def _stream(stream, device=0):
+    if device < 0:
+        return ctypes.c_void_p()  # host communicator (fake library): no stream
     s = stream if stream is not None else torch.cuda.current_stream()
     return ctypes.c_void_p(s.cuda_stream)
 
@@ -91,7 +102,8 @@ class Communicator:
     """One RCCL communicator: ``world`` ranks, this process is ``rank``, on ``device``.
 
     ``uid``: the clique's 128-byte unique id (the same bytes on every rank); use
-    :meth:`rendezvous` to create it on rank 0 and distribute it through a store."""
+    :meth:`rendezvous` to create it on rank 0 and distribute it through a store.
+    ``device`` < 0: host buffers (a multi-rank CPU test against a C-ABI fake)."""
 
     def __init__(self, uid: bytes, world: int, rank: int, device: int):
         if len(uid) != 128:
@@ -114,20 +126,24 @@ class Communicator:
 
     # ------------------------------------------------------------------ collectives
     def _args(self, t):
-        if not t.is_cuda or t.dtype not in _DT or not t.is_contiguous():
-            raise RcclError(f"RCCL operand must be a contiguous device tensor of a supported dtype ({t.dtype})")
+        if t.is_cuda != (self.device >= 0) or t.dtype not in _DT or not t.is_contiguous():
+            raise RcclError(f"RCCL operand must be a contiguous {'device' if self.device >= 0 else 'host'} "
+                            f"tensor of a supported dtype ({t.dtype}, {t.device})")
         return ctypes.c_void_p(t.data_ptr()), _DT[t.dtype]
+
+    def _st(self, stream):
+        return _stream(stream, self.device)
 
     def all_reduce(self, t, op="sum", stream=None):
         p, dt = self._args(t)
-        _check(_lib().pa_rccl_all_reduce(p, p, t.numel(), dt, _OPS[op], self._h, _stream(stream)), "ncclAllReduce")
+        _check(_lib().pa_rccl_all_reduce(p, p, t.numel(), dt, _OPS[op], self._h, self._st(stream)), "ncclAllReduce")
 
     def reduce_scatter(self, out, inp, op="sum", stream=None):
         po, dt = self._args(out)
         pi, _ = self._args(inp)
         if inp.numel() != out.numel() * self.world or inp.dtype != out.dtype:
             raise RcclError("reduce_scatter: input must hold world x output elements of the same dtype")
-        _check(_lib().pa_rccl_reduce_scatter(pi, po, out.numel(), dt, _OPS[op], self._h, _stream(stream)),
+        _check(_lib().pa_rccl_reduce_scatter(pi, po, out.numel(), dt, _OPS[op], self._h, self._st(stream)),
                "ncclReduceScatter")
 
     def all_gather(self, out, inp, stream=None):
@@ -135,20 +151,42 @@ class Communicator:
         pi, _ = self._args(inp)
         if out.numel() != inp.numel() * self.world or inp.dtype != out.dtype:
             raise RcclError("all_gather: output must hold world x input elements of the same dtype")
-        _check(_lib().pa_rccl_all_gather(pi, po, inp.numel(), dt, self._h, _stream(stream)), "ncclAllGather")
+        _check(_lib().pa_rccl_all_gather(pi, po, inp.numel(), dt, self._h, self._st(stream)), "ncclAllGather")
 
     def broadcast(self, t, root=0, stream=None):
         p, dt = self._args(t)
-        _check(_lib().pa_rccl_broadcast(p, p, t.numel(), dt, int(root), self._h, _stream(stream)),
+        _check(_lib().pa_rccl_broadcast(p, p, t.numel(), dt, int(root), self._h, self._st(stream)),
                "ncclBroadcast")
 
     def send(self, t, peer, stream=None):
         p, dt = self._args(t)
-        _check(_lib().pa_rccl_send(p, t.numel(), dt, int(peer), self._h, _stream(stream)), "ncclSend")
+        _check(_lib().pa_rccl_send(p, t.numel(), dt, int(peer), self._h, self._st(stream)), "ncclSend")
 
     def recv(self, t, peer, stream=None):
         p, dt = self._args(t)
-        _check(_lib().pa_rccl_recv(p, t.numel(), dt, int(peer), self._h, _stream(stream)), "ncclRecv")
+        _check(_lib().pa_rccl_recv(p, t.numel(), dt, int(peer), self._h, self._st(stream)), "ncclRecv")
+
+    def all_to_all(self, out, inp, out_splits=None, in_splits=None, stream=None):
+        """Rows of ``inp`` split by ``in_splits`` (one chunk per peer, rank order) are
+        exchanged; ``out`` receives ``out_splits`` rows from each peer.  Equal splits
+        when None.  One fused ncclSend/ncclRecv group (csrc pa_rccl_all_to_all)."""
+        po, dt = self._args(out)
+        pi, _ = self._args(inp)
+        W = self.world
+        if out.dtype != inp.dtype or out.shape[1:] != inp.shape[1:]:
+            raise RcclError("all_to_all: input and output rows must match in dtype and shape")
+        row = inp[0].numel() if inp.dim() > 1 else 1
+        ins = list(in_splits) if in_splits is not None else [inp.shape[0] // W] * W
+        outs = list(out_splits) if out_splits is not None else [out.shape[0] // W] * W
+        if len(ins) != W or len(outs) != W or sum(ins) != inp.shape[0] or sum(outs) != out.shape[0]:
+            raise RcclError("all_to_all: splits must have one entry per rank and cover the rows")
+        arr = ctypes.c_size_t * W
+        sc = arr(*[n * row for n in ins])
+        rc_ = arr(*[n * row for n in outs])
+        sd = arr(*[sum(ins[:p]) * row for p in range(W)])
+        rd = arr(*[sum(outs[:p]) * row for p in range(W)])
+        _check(_lib().pa_rccl_all_to_all(pi, po, sc, sd, rc_, rd, W, dt, inp.element_size(), self._h,
+                                         self._st(stream)), "ncclSend/ncclRecv all_to_all")
 
     def check_async(self):
         """Raise if the communicator hit an asynchronous error (a peer failed)."""
@@ -208,6 +246,22 @@ class CommContextMap:
             c.destroy(abort)
         self._comms.clear()
 
+    def check_health(self):
+        """Raise :class:`RcclError` if any communicator reports an asynchronous error;
+        every communicator is aborted first (ncclCommAbort), so the collectives other
+        host threads or streams are blocked in return instead of hanging."""
+        for key, c in list(self._comms.items()):
+            try:
+                c.check_async()
+            except RcclError as e:
+                for other in self._comms.values():
+                    try:
+                        other.destroy(abort=True)
+                    except RcclError:
+                        pass
+                self._comms.clear()
+                raise RcclError(f"communicator of ranks {list(key)} failed ({e}); all communicators aborted") from e
+
 
 _MAP = CommContextMap()
 
@@ -217,4 +271,16 @@ def context_map() -> CommContextMap:
 
 
 def enabled() -> bool:
-    return os.environ.get("FLAGS_comm_backend", "torch") == "pa_rccl"
+    """Route device collectives through the framework communicators: ``auto`` (the
+    default) whenever librccl loads, ``pa_rccl`` always, ``torch`` never."""
+    mode = os.environ.get("FLAGS_comm_backend", "auto")
+    if mode == "pa_rccl":
+        return True
+    if mode != "auto":
+        return False
+    if not _AUTO:
+        _AUTO.append(torch.cuda.is_available() and available())
+    return _AUTO[0]
+
+
+_AUTO: list = []
