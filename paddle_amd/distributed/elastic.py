@@ -9,7 +9,10 @@ for the collective (RCCL) world:
   no beat arrives for ``timeout_s`` (a collective stuck on a dead peer, a hung
   kernel, a deadlocked data loader) it dumps every thread's stack and exits the
   process with :data:`EXIT_WATCHDOG`, so the launcher can tear the group down and
-  restart it instead of hanging until the RCCL timeout.
+  restart it instead of hanging until the RCCL timeout.  Each poll also checks the
+  framework RCCL communicators' asynchronous errors (``CommContextMap.check_health``:
+  ncclCommGetAsyncError, then ncclCommAbort on all of them) and takes the same exit
+  as soon as a peer has failed.
 * :func:`maybe_inject_fault` -- ``PADDLE_FAULT_INJECT="rank:step[:kind]"``
   (kind = ``exit`` | ``raise`` | ``hang``) makes one rank fail at one step; it fires
   only in the first launch (``PADDLE_RESTART_COUNT`` == 0) so the restarted job
@@ -52,8 +55,28 @@ class Watchdog:
         if step is not None:
             self._step = step
 
+    def _comm_failed(self):
+        """Poll the framework RCCL communicators' asynchronous errors (a dead peer):
+        ``check_health`` aborts every communicator and raises -> True."""
+        try:
+            from ..parallel import rccl
+
+            if rccl._MAP._comms:
+                rccl._MAP.check_health()
+        except Exception as e:  # noqa: BLE001 - RcclError, or a library that is gone
+            sys.stderr.write(f"[watchdog:{self.name}] communicator failure: {e}\n")
+            return True
+        return False
+
     def _run(self):
         while not self._stop.wait(self._poll):
+            if self._comm_failed():
+                faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+                sys.stderr.flush()
+                if self.on_timeout is not None:
+                    self.on_timeout(self._step)
+                    return
+                os._exit(EXIT_WATCHDOG)
             idle = time.monotonic() - self._last
             if idle > self.timeout_s:
                 sys.stderr.write(f"[watchdog:{self.name}] no progress for {idle:.1f}s after step {self._step} "

@@ -222,9 +222,9 @@ def _ring_exchange(send, group):
     gn = torch.distributed.get_global_rank(group, nxt) if group is not None else nxt
     gp = torch.distributed.get_global_rank(group, prv) if group is not None else prv
     recv = torch.empty_like(send)
-    ops_ = [torch.distributed.P2POp(torch.distributed.isend, send, gn, group),
-            torch.distributed.P2POp(torch.distributed.irecv, recv, gp, group)]
-    return recv, torch.distributed.batch_isend_irecv(ops_)
+    # framework RCCL on the comm stream (overlaps the current block's attention), or
+    # batched isend/irecv on gloo
+    return recv, comm.batch_p2p([("send", send, gn), ("recv", recv, gp)], group=group, async_op=True)
 
 
 def _pairs(rank, src, P):

@@ -208,15 +208,15 @@ class _P2P:
                                    f"({self._sent[key]} -> {self._sig(lst)}); build the pipeline with "
                                    "dynamic_shapes=True (FLAGS_pp_dynamic_shapes=1) for variable shapes")
         if need_sn:
-            ops.append(dist.P2POp(dist.isend, _meta(send_next).to(mdev), self.next))
+            ops.append(("send", _meta(send_next).to(mdev), self.next))
         if need_sp:
-            ops.append(dist.P2POp(dist.isend, _meta(send_prev).to(mdev), self.prev))
+            ops.append(("send", _meta(send_prev).to(mdev), self.prev))
         if need_rn:
             got_next_m = torch.empty(1 + _MAXT * (2 + _MAXD), dtype=torch.int64, device=mdev)
-            ops.append(dist.P2POp(dist.irecv, got_next_m, self.next))
+            ops.append(("recv", got_next_m, self.next))
         if need_rp:
             got_prev_m = torch.empty(1 + _MAXT * (2 + _MAXD), dtype=torch.int64, device=mdev)
-            ops.append(dist.P2POp(dist.irecv, got_prev_m, self.prev))
+            ops.append(("recv", got_prev_m, self.prev))
         if ops:
             self.meta_rounds += 1
             self._run(ops)
@@ -240,15 +240,15 @@ class _P2P:
         host = (lambda t: t.detach().cpu()) if not self.nccl else (lambda t: t)
         land = []
         for t in send_next or []:
-            ops.append(dist.P2POp(dist.isend, host(t.contiguous()), self.next))
+            ops.append(("send", host(t.contiguous()), self.next))
         for t in send_prev or []:
-            ops.append(dist.P2POp(dist.isend, host(t.contiguous()), self.prev))
+            ops.append(("send", host(t.contiguous()), self.prev))
         for peer, lst in ((self.next, from_next), (self.prev, from_prev)):
             for t in lst or []:
                 buf = t if (self.nccl or not t.is_cuda) else torch.empty(t.shape, dtype=t.dtype)
                 if buf is not t:
                     land.append((t, buf))
-                ops.append(dist.P2POp(dist.irecv, buf, peer))
+                ops.append(("recv", buf, peer))
         self._run(ops)
         for t, buf in land:
             t.copy_(buf)
@@ -256,10 +256,9 @@ class _P2P:
 
     @staticmethod
     def _run(ops):
-        if not ops:
-            return
-        for r in dist.batch_isend_irecv(ops):
-            r.wait()
+        # the framework RCCL communicator (one ncclGroupStart/End round of device
+        # sends / receives) on GPU ranks, batched isend/irecv otherwise
+        comm.batch_p2p(ops)
 
 
 def _as_tuple(x):

@@ -77,25 +77,85 @@ def _is_gloo(group=None):
     return dist.get_backend(group) == "gloo"
 
 
+_HOST_RCCL = []  # tests: route host tensors through the framework communicators (fake librccl)
+
+
+def _group_ranks(group):
+    return list(range(dist.get_world_size())) if group is None else dist.get_process_group_ranks(group)
+
+
 def _pa_comm(group, *ts):
-    """The framework-owned RCCL communicator of ``group`` (FLAGS_comm_backend=pa_rccl)
-    when every operand is a contiguous device tensor, else None (torch.distributed)."""
+    """The framework-owned RCCL communicator of ``group`` (parallel/rccl.py) when every
+    operand is a contiguous device tensor and the framework layer is on
+    (``FLAGS_comm_backend`` auto / pa_rccl), else None (torch.distributed)."""
     from . import rccl
 
-    if not rccl.enabled() or not all(t.is_cuda and t.is_contiguous() for t in ts):
+    host = bool(_HOST_RCCL)
+    if not rccl.enabled() or not all(t.is_contiguous() and (t.is_cuda or host) for t in ts):
         return None
-    ranks = list(range(dist.get_world_size())) if group is None else dist.get_process_group_ranks(group)
-    return rccl.context_map().get(ranks, dist.get_rank())
+    if not host and dist.get_backend(group) != "nccl":
+        return None
+    dev = -1 if host else None
+    return rccl.context_map().get(_group_ranks(group), dist.get_rank(), device=dev)
+
+
+class StreamWork:
+    """Handle of a collective enqueued on the framework comm stream (the c10d ``Work``
+    contract): ``wait()`` makes the CURRENT stream wait for it, no host sync."""
+
+    def __init__(self, event):
+        self.event = event
+
+    def wait(self):
+        if self.event is not None:
+            torch.cuda.current_stream().wait_event(self.event)
+        return True
+
+    def is_completed(self):
+        return self.event is None or self.event.query()
+
+
+_COMM_STREAMS: dict = {}
+
+
+def comm_stream(device):
+    """One high-priority HIP stream per device for asynchronous collectives."""
+    s = _COMM_STREAMS.get(device)
+    if s is None:
+        s = _COMM_STREAMS[device] = torch.cuda.Stream(device=device, priority=-1)
+    return s
+
+
+def _run_pa(c, fn, ts, async_op):
+    """Run ``fn(c)`` on the framework communicator: stream-ordered on the current
+    stream, or (async_op) on the comm stream after the current stream's work, with a
+    :class:`StreamWork` to join it later (the operands are kept alive for it)."""
+    if not async_op or not ts[0].is_cuda:
+        fn(c)
+        return StreamWork(None) if async_op else None
+    cur = torch.cuda.current_stream(ts[0].device)
+    s = comm_stream(ts[0].device)
+    s.wait_stream(cur)
+    with torch.cuda.stream(s):
+        fn(c)
+    for t in ts:
+        t.record_stream(s)
+    ev = torch.cuda.Event()
+    ev.record(s)
+    return StreamWork(ev)
 
 
 def all_reduce(t, op=dist.ReduceOp.SUM, group=None, async_op=False):
     if get_world_size(group) == 1:
         return None
-    c = _pa_comm(group, t) if op == dist.ReduceOp.SUM else None
+    c = _pa_comm(group, t) if op in _RCCL_OPS else None
     if c is not None:
-        c.all_reduce(t)  # stream-ordered on the current stream: nothing to wait for
-        return None
+        return _run_pa(c, lambda cc: cc.all_reduce(t, op=_RCCL_OPS[op]), [t], async_op)
     return dist.all_reduce(t, op=op, group=group, async_op=async_op)
+
+
+_RCCL_OPS = {dist.ReduceOp.SUM: "sum", dist.ReduceOp.MAX: "max", dist.ReduceOp.MIN: "min",
+             dist.ReduceOp.PRODUCT: "prod"}
 
 
 def reduce_scatter(out, inp, group=None, async_op=False):
@@ -113,8 +173,7 @@ def reduce_scatter(out, inp, group=None, async_op=False):
         return None
     c = _pa_comm(group, out, inp)
     if c is not None:
-        c.reduce_scatter(out, inp)
-        return None
+        return _run_pa(c, lambda cc: cc.reduce_scatter(out, inp), [out, inp], async_op)
     return dist.reduce_scatter_tensor(out, inp, group=group, async_op=async_op)
 
 
@@ -133,8 +192,7 @@ def all_gather(out, inp, group=None, async_op=False):
         return None
     c = _pa_comm(group, out, inp)
     if c is not None:
-        c.all_gather(out, inp)
-        return None
+        return _run_pa(c, lambda cc: cc.all_gather(out, inp), [out, inp], async_op)
     return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
 
 
@@ -143,15 +201,20 @@ def broadcast(t, src=0, group=None):
         return
     c = _pa_comm(group, t)
     if c is not None:
-        ranks = list(range(dist.get_world_size())) if group is None else dist.get_process_group_ranks(group)
-        c.broadcast(t, root=ranks.index(src))  # src is a global rank
+        c.broadcast(t, root=_group_ranks(group).index(src))  # src is a global rank
         return
     dist.broadcast(t, src=src, group=group)
 
 
 def all_to_all(out, inp, group=None, out_splits=None, in_splits=None):
+    """Rows of ``inp`` split per peer (``in_splits``, equal when None) are exchanged;
+    ``out`` receives ``out_splits`` rows from each peer, in rank order."""
     if get_world_size(group) == 1:
         out.copy_(inp)
+        return
+    c = _pa_comm(group, out, inp)
+    if c is not None:
+        c.all_to_all(out, inp, out_splits, in_splits)  # one grouped ncclSend/ncclRecv
         return
     if _is_gloo(group):
         W = get_world_size(group)
@@ -170,6 +233,37 @@ def all_to_all(out, inp, group=None, out_splits=None, in_splits=None):
             q.wait()
         return
     dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+
+
+def batch_p2p(ops, group=None, async_op=False):
+    """One fused point-to-point round: ``ops`` = [("send" | "recv", tensor, global
+    peer rank)].  Device tensors go through the framework communicator of ``group``
+    (ncclSend / ncclRecv inside one ncclGroupStart/End, stream-ordered: a received
+    tensor is ready for the current stream's next kernels); otherwise
+    ``torch.distributed.batch_isend_irecv``.  ``async_op``: returns work handles
+    (the framework path runs on the comm stream) instead of waiting."""
+    if not ops:
+        return [] if async_op else None
+    ts = [t for _, t, _ in ops]
+    c = _pa_comm(group, *ts)
+    if c is not None:
+        from . import rccl
+
+        ranks = _group_ranks(group)
+
+        def run(cc):
+            with rccl.group_guard():
+                for kind, t, peer in ops:
+                    (cc.send if kind == "send" else cc.recv)(t, ranks.index(peer))
+
+        w = _run_pa(c, run, ts, async_op)
+        return [w] if async_op else None
+    p2p = [dist.P2POp(dist.isend if kind == "send" else dist.irecv, t, peer, group=group) for kind, t, peer in ops]
+    reqs = dist.batch_isend_irecv(p2p)
+    if async_op:
+        return reqs
+    for r in reqs:
+        r.wait()
 
 
 def new_group(ranks):

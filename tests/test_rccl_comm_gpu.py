@@ -15,6 +15,7 @@ pytestmark = pytest.mark.gpu
 
 def test_one_rank_clique_collectives():
     assert rccl.available()
+    assert rccl.enabled()  # FLAGS_comm_backend=auto: the framework layer is the GPU default
     store = dist.TCPStore("127.0.0.1", 0, 1, True, timeout=datetime.timedelta(seconds=30))
     c = rccl.Communicator.rendezvous(store, "pa_rccl/test/0", 1, 0, torch.cuda.current_device())
     x = torch.arange(1000, device="cuda", dtype=torch.float32)
@@ -30,7 +31,17 @@ def test_one_rank_clique_collectives():
     with rccl.group_guard():
         c.all_reduce(x)
         c.broadcast(out, root=0)
+    # expert-parallel all-to-all (grouped ncclSend/ncclRecv) and a self send/recv round
+    rows = torch.randn(7, 16, device="cuda", dtype=torch.bfloat16)
+    got = torch.empty_like(rows)
+    c.all_to_all(got, rows, out_splits=[7], in_splits=[7])
+    with rccl.group_guard():
+        back = torch.empty(5, device="cuda", dtype=torch.int64)
+        c.send(torch.arange(5, device="cuda"), 0)
+        c.recv(back, 0)
     torch.cuda.synchronize()
+    assert torch.equal(got, rows)
+    assert torch.equal(back, torch.arange(5, device="cuda"))
     c.check_async()
     with pytest.raises(rccl.RcclError):
         c.all_reduce(x.cpu())
