@@ -153,7 +153,9 @@ def main():
     pool = [torch.randint(0, cfg.vocab_size, (world * mb, S + 1), generator=gen)[rank * mb:(rank + 1) * mb]
             .to(dev) for _ in range(4)]
 
-    use_tape = args.autograd == "tape" and cuda and not args.recompute
+    # recompute runs on the tape too (tape.checkpoint: the segment's forward is replayed
+    # inside the reverse pass)
+    use_tape = args.autograd == "tape" and cuda
 
     def micro(x, y):
         if use_tape:

@@ -12,6 +12,7 @@
 Synthetic token ids, random-init weights, bf16, fused flat sharded AdamW.
 """
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -69,6 +70,8 @@ def main():
     ap.add_argument("--fixed-batch", action="store_true",
                     help="re-feed ONE batch every micro-step (memorisation probe; default: a pool of distinct batches)")
     ap.add_argument("--pool", type=int, default=8, help="distinct synthetic batches cycled through")
+    ap.add_argument("--autograd", default="tape", choices=["tape", "torch"],
+                    help="tape: the framework's reverse pass (torch autograd off, recompute on the tape)")
     argv = sys.argv[1:]
     a = ap.parse_args(argv)
     if a.gpus and "WORLD_SIZE" not in os.environ:
@@ -87,6 +90,7 @@ def main():
     if a.tp > 1 or a.pp > 1 or a.sharding > 1:
         return hybrid_main(a)
 
+    from paddle_amd.autograd import tape
     from paddle_amd.parallel import comm
     from paddle_amd.parallel.sharding import FlatShardedOptimizer
 
@@ -113,13 +117,17 @@ def main():
         for m in range(a.accum):
             ids = pool[it[0] % len(pool)]
             it[0] += 1
-            if m < a.accum - 1:
-                with opt.no_sync():
+            with (opt.no_sync() if m < a.accum - 1 else contextlib.nullcontext()):
+                if a.autograd == "tape":
+                    # forward recorded on the framework tape, the 1/accum scale is the
+                    # seed gradient of its reverse pass (no torch autograd anywhere)
+                    with tape.recording() as t:
+                        loss = model(ids[:, :-1], ids[:, 1:])
+                    t.backward(loss, torch.full_like(loss, 1.0 / a.accum))
+                    loss = loss.detach() / a.accum
+                else:
                     loss = model(ids[:, :-1], ids[:, 1:]) / a.accum
                     loss.backward()
-            else:
-                loss = model(ids[:, :-1], ids[:, 1:]) / a.accum
-                loss.backward()
             tot = tot + loss.detach()
             if getattr(model, "last_ce", None) is not None:
                 ce[0] = ce[0] + model.last_ce / a.accum
@@ -154,7 +162,7 @@ def main():
                           "peak_mem_gib": round(__import__("paddle_amd.platform", fromlist=["x"]).max_memory_allocated(
                               torch.cuda.current_device()) / 2**30, 1),
                           "config": {"model": a.model, "micro_batch": a.micro_batch, "grad_accum": a.accum, "seq_len": a.seq_len,
-                                     "recompute": a.recompute, "grouped_experts": a.grouped_experts,
+                                     "recompute": a.recompute, "grouped_experts": a.grouped_experts, "autograd": a.autograd,
                                      "grad_dtype": str(opt.grad_dtype), "dw_kmajor": os.environ.get("PADDLE_AMD_DW_KMAJ", "1"), "parallelism": f"dp{world}+sharding_stage1"},
                           "batches": "fixed" if a.fixed_batch else f"pool of {a.pool}",
                           "loss": float(loss),

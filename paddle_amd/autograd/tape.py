@@ -69,6 +69,8 @@ class Tape:
         self._next = 1
         self._uses = {}     # id(param) -> remaining uses on the tape
         self._params = {}   # id(param) -> param
+        self._watched = {}  # tag -> None (an input whose gradient the caller wants)
+        self._input_grads = {}  # tag -> gradient of a watched input after backward
 
     # ------------------------------------------------------------------ record
     def _tag(self, t):
@@ -76,6 +78,23 @@ class Tape:
         self._next += 1
         t._pa_tape = (id(self), tag)
         return tag
+
+    def watch(self, t):
+        """Make ``t`` (a tensor produced outside this tape: a pipeline stage's received
+        activation, a recompute segment's input) a differentiable input of the tape;
+        after :meth:`backward` its gradient is :meth:`grad` (t)."""
+        if not isinstance(t, torch.Tensor) or not t.is_floating_point():
+            return t
+        tag = self._tag(t)
+        self._watched[tag] = None
+        return t
+
+    def grad(self, t):
+        """Gradient of a watched input (None if nothing on the tape used it)."""
+        tg = getattr(t, "_pa_tape", None)
+        if tg is None or tg[0] != id(self):
+            return None
+        return self._input_grads.get(tg[1])
 
     def _handle(self, a):
         """('act', tag) for a tracked activation, ('param', p) for a leaf that
@@ -123,12 +142,31 @@ class Tape:
                 return self._backward(loss, grad)
         return self._backward(loss, grad)
 
+    def backward_multi(self, outputs, grads):
+        """Reverse pass seeded with several outputs (a pipeline stage's activations with
+        the gradients the next stage returned); ``None`` gradients seed ones."""
+        from ..utils import strict as _strict
+
+        seeds = {}
+        for o, g in zip(outputs, grads):
+            tg = getattr(o, "_pa_tape", None)
+            if tg is None or tg[0] != id(self):
+                continue  # not produced on this tape (e.g. an integer passthrough)
+            g = torch.ones_like(o) if g is None else g
+            seeds[tg[1]] = g if tg[1] not in seeds else _add(seeds[tg[1]], g)
+        if _strict.counting():
+            with _strict.region("tape:backward", native=False):
+                return self._run(seeds)
+        return self._run(seeds)
+
     def _backward(self, loss, grad=None):
-        run_before_backward()  # e.g. an optimizer update still running on a side stream
         tg = getattr(loss, "_pa_tape", None)
         if tg is None or tg[0] != id(self):
             raise RuntimeError("tape.backward: the loss was not produced on this tape")
-        grads = {tg[1]: torch.ones_like(loss) if grad is None else grad}
+        return self._run({tg[1]: torch.ones_like(loss) if grad is None else grad})
+
+    def _run(self, grads):
+        run_before_backward()  # e.g. an optimizer update still running on a side stream
         with torch.no_grad():
             for e in reversed(self.entries):
                 outg = [grads.pop(t, None) if t is not None else None for t in e.outputs]
@@ -153,6 +191,8 @@ class Tape:
                         self._param_done(p)
                 e.ctx = None
         self.entries.clear()
+        # what is left are the gradients of tensors no entry produced: watched inputs
+        self._input_grads = {t: g for t, g in grads.items() if t in self._watched}
 
     def _release(self, e):
         for h in e.inputs:
@@ -208,6 +248,88 @@ def cancel_before_backward(fn):
     _BEFORE_BACKWARD[:] = [r for r in _BEFORE_BACKWARD if r() is not None and r() != fn]
 
 
+class _RecomputeFn:
+    """One recorded entry for a whole segment ``fn(*args)`` whose activations are not
+    kept: the forward runs the segment with recording suspended (its fused ops save
+    nothing that outlives the call), the backward runs it AGAIN on a private tape --
+    inputs watched -- and differentiates that tape with the segment outputs'
+    gradients.  Parameters used inside get their gradients (main_grad / .grad) and
+    grad-ready hooks from the inner tape.  The framework's activation recomputation
+    (reference: python/paddle/fluid/backward.py builds the program's own backward;
+    this is the tape analogue of torch.utils.checkpoint)."""
+
+    @staticmethod
+    def forward(ctx, fn, *args):
+        ctx.fn = fn
+        ctx.args = args
+        # the re-run must draw the same random numbers (dropout masks)
+        ctx.rng = torch.get_rng_state()
+        ctx.cuda_rng = torch.cuda.get_rng_state() if torch.cuda.is_available() and torch.cuda.is_initialized() else None
+        with suspended():
+            out = fn(*args)
+        ctx.single = not isinstance(out, tuple)
+        return out
+
+    @staticmethod
+    def backward(ctx, *gs):
+        inner = Tape()
+        prev = current()
+        _TLS.tape = inner
+        rng = torch.get_rng_state()
+        cuda_rng = torch.cuda.get_rng_state() if ctx.cuda_rng is not None else None
+        torch.set_rng_state(ctx.rng)
+        if ctx.cuda_rng is not None:
+            torch.cuda.set_rng_state(ctx.cuda_rng)
+        try:
+            with torch.no_grad():
+                # only the inputs the outer tape differentiates (activations) are watched;
+                # constants (rotary tables, masks) stay plain tensors
+                need = ctx.needs_input_grad[1:]
+                args = [inner.watch(a.detach()) if n and isinstance(a, torch.Tensor) and a.is_floating_point() else a
+                        for a, n in zip(ctx.args, need)]
+                out = ctx.fn(*args)
+        finally:
+            _TLS.tape = prev
+            torch.set_rng_state(rng)
+            if cuda_rng is not None:
+                torch.cuda.set_rng_state(cuda_rng)
+        outs = (out,) if ctx.single else tuple(out)
+        pairs = [(o, g) for o, g in zip(outs, gs) if g is not None and isinstance(o, torch.Tensor)]
+        inner.backward_multi([o for o, _ in pairs], [g for _, g in pairs])
+        res = [inner.grad(a) if n and isinstance(a, torch.Tensor) and a.is_floating_point() else None
+               for a, n in zip(args, need)]
+        ctx.args = None
+        return (None, *res)
+
+
+def checkpoint(fn, *args):
+    """Activation recomputation on the framework tape: while recording, ``fn(*args)``
+    becomes one entry that recomputes its forward inside the reverse pass; outside a
+    recording (eager / inference) it is just ``fn(*args)``."""
+    t = current()
+    if t is None:
+        return fn(*args)
+    return t.apply(_RecomputeFn, fn, *args)
+
+
+@contextlib.contextmanager
+def suspended():
+    """Run ops without recording them (and without keeping what they save)."""
+    prev = current()
+    _TLS.tape = None
+    _TLS.suspended = getattr(_TLS, "suspended", 0) + 1
+    try:
+        with torch.no_grad():
+            yield
+    finally:
+        _TLS.suspended -= 1
+        _TLS.tape = prev
+
+
+def is_suspended():
+    return getattr(_TLS, "suspended", 0) > 0
+
+
 @contextlib.contextmanager
 def recording():
     """Record fused ops on a fresh tape with torch autograd disabled; yields the tape."""
@@ -231,6 +353,10 @@ def apply(fn, *args):
     t = current()
     if t is not None:
         return t.apply(fn, *args)
+    if is_suspended():
+        # inside a recompute segment's forward: compute, keep nothing for a backward
+        with torch.no_grad():
+            return fn.forward(_Ctx(tuple(False for _ in args)), *args)
     from . import engine
 
     if any(isinstance(a, engine.Tensor) for a in args):

@@ -67,6 +67,48 @@ def _swap(x, a, b):
     return x if a == 1 or b == 1 else _tape.apply(_PeerExpertSwap, x, a, b)
 
 
+class _TopKGateFn(torch.autograd.Function):
+    """Router: fp32 logits = x W, probs = softmax, top-k (renormalised for gshard /
+    switch), GShard balance loss E * sum_e mean_t(probs[:, e]) * frac_e (frac_e = the
+    share of tokens whose first choice is e, a constant).  Outputs (val [T, k] fp32,
+    idx [T, k] int64, l_aux scalar); the backward is analytic (top-k renormalisation,
+    balance term, softmax, then dX = dlogits W^T, dW = X^T dlogits), so the router
+    trains on the framework tape as well as under torch autograd."""
+
+    @staticmethod
+    def forward(ctx, x, w, k, renorm):
+        logits = x.float() @ w.float()
+        probs = torch.softmax(logits, dim=-1)
+        val, idx = probs.topk(k, dim=-1)
+        s = val.sum(-1, keepdim=True).clamp_min(1e-9) if renorm else None
+        valn = val / s if renorm else val
+        E = w.shape[1]
+        frac = torch.nn.functional.one_hot(idx[:, 0], E).float().mean(0)
+        l_aux = (probs.mean(0) * frac).sum() * E
+        ctx.save_for_backward(x, w, probs, idx, valn, s if s is not None else probs.new_ones(1), frac)
+        ctx.renorm = renorm
+        return valn, idx, l_aux
+
+    @staticmethod
+    def backward(ctx, dval, _didx, daux):
+        x, w, probs, idx, valn, s, frac = ctx.saved_tensors
+        T, E = probs.shape
+        dprobs = torch.zeros_like(probs)
+        if dval is not None:
+            dval = dval.float()
+            if ctx.renorm:  # v_j / sum(v): d v_j = (dval_j - sum_i dval_i valn_i) / s
+                dv = (dval - (dval * valn).sum(-1, keepdim=True)) / s
+            else:
+                dv = dval
+            dprobs.scatter_add_(1, idx, dv)
+        if daux is not None:
+            dprobs += daux.float() * E * frac.unsqueeze(0) / T
+        dlogits = probs * (dprobs - (dprobs * probs).sum(-1, keepdim=True))
+        dx = (dlogits @ w.float().t()).to(x.dtype)
+        dw = (x.float().t() @ dlogits).to(w.dtype)
+        return dx, dw, None, None
+
+
 class TopKGate(Layer):
     def __init__(self, d_model, num_experts, top_k=2, gate_type="gshard", capacity_factor=None, dtype="float32"):
         super().__init__("moe_gate", dtype)
@@ -88,16 +130,9 @@ class TopKGate(Layer):
             return self._route(x)
 
     def _route(self, x):
-        logits = x.float() @ self.weight.float()  # routing in fp32 whatever the activation dtype
-        probs = F.softmax(logits, dim=-1)
-        val, idx = probs.topk(self.top_k, dim=-1)
-        if self.gate_type != "naive" and self.top_k > 1:
-            val = val / val.sum(-1, keepdim=True).clamp_min(1e-9)
-        # GShard / Switch load-balancing loss: E * sum_e(frac_tokens_e * mean_prob_e)
-        me = probs.mean(0)
-        ce = F.one_hot(idx[:, 0], self.num_experts).float().mean(0)
-        l_aux = (me * ce).sum() * self.num_experts
-        return val, idx, l_aux
+        # routing in fp32 whatever the activation dtype; GShard / Switch balance loss
+        return _tape.apply(_TopKGateFn, x, self.weight, self.top_k,
+                           self.gate_type != "naive" and self.top_k > 1)
 
 
 class MoELayer(Layer):
@@ -123,14 +158,16 @@ class MoELayer(Layer):
         self.l_aux = None
 
     def forward(self, x):
+        from ...ops import fused as _F
+
         shape = x.shape
-        x = x.reshape(-1, shape[-1])
+        x = _F.reshape(x, (-1, shape[-1]))
         T, k, E = x.shape[0], self.top_k, self.num_experts
         val, idx, self.l_aux = self.gate(x)
         flat_e = idx.reshape(-1)                       # [T*k] expert of each (token, slot)
-        flat_w = val.reshape(-1)
+        flat_w = val                                   # [T, k] gate weights (combine reads them flat)
         if self.capacity_factor is not None and self.sync_free:
-            return self._forward_capacity(x, flat_e, flat_w, T, k, E).reshape(shape)
+            return _F.reshape(self._forward_capacity(x, flat_e, flat_w, T, k, E), shape)
         keep = None
         if self.capacity_factor is not None:
             cap = max(1, int(self.capacity_factor * T * k / E))
@@ -157,29 +194,41 @@ class MoELayer(Layer):
             recv_mat = counts_all[:, lo:hi]               # [peer, local expert]
             out_splits = recv_mat.sum(1).tolist()
             recv = all_to_all(send, in_splits, out_splits, self.group)
-            # regroup peer-major -> expert-major
-            per = recv_mat.reshape(-1).tolist()
-            chunks = list(recv.split(per))
-            by_expert = [torch.cat([chunks[p * self.n_local + e] for p in range(self.ep)])
-                         for e in range(self.n_local)]
-            # back to peer-major order
-            sizes = [[int(recv_mat[p, e]) for p in range(self.ep)] for e in range(self.n_local)]
+            # regroup peer-major [peer][expert] row blocks -> expert-major with ONE row
+            # permutation (a recorded node: gradients flow on the framework tape too)
+            nl, ep = self.n_local, self.ep
+            per = recv_mat.reshape(-1).tolist()            # block (p, e) sizes, peer-major
+            st = [0]
+            for n_ in per:
+                st.append(st[-1] + n_)
+            perm = [r for e in range(nl) for p in range(ep) for r in range(st[p * nl + e], st[p * nl + e + 1])]
+            perm_t = torch.tensor(perm, dtype=torch.long, device=recv.device)
+            xe = _F.row_gather(recv, perm_t)
+            sizes_e = [sum(int(recv_mat[p, e]) for p in range(ep)) for e in range(nl)]
             if self.grouped:
-                outs = list(self.experts.forward_grouped(torch.cat(by_expert),
-                                                         [sum(sz) for sz in sizes]).split([sum(sz) for sz in sizes]))
+                ye = self.experts.forward_grouped(xe, sizes_e)
             else:
-                outs = [self.experts[e](by_expert[e]) if by_expert[e].shape[0] else by_expert[e]
-                        for e in range(self.n_local)]
-            split_out = [list(o.split(s)) for o, s in zip(outs, sizes)]
-            back = torch.cat([split_out[e][p] for p in range(self.ep) for e in range(self.n_local)])
+                outs, o = [], 0
+                for e in range(nl):
+                    rows = torch.arange(o, o + sizes_e[e], device=xe.device)
+                    o += sizes_e[e]
+                    outs.append(self.experts[e](_F.row_gather(xe, rows)) if sizes_e[e] else _F.row_gather(xe, rows))
+                ye = _F.concat_rows(outs)
+            inv = torch.empty_like(perm_t)
+            inv[perm_t] = torch.arange(perm_t.numel(), device=perm_t.device)
+            back = _F.row_gather(ye, inv)                  # expert-major -> peer-major
             y_sorted = all_to_all(back, out_splits, in_splits, self.group)
         elif self.grouped:
             y_sorted = self.experts.forward_grouped(send, counts)
         else:
-            parts = list(send.split(counts.tolist()))
-            y_sorted = torch.cat([self.experts[e](parts[e]) if parts[e].shape[0] else parts[e]
-                                  for e in range(E)])
-        return _route.combine(y_sorted, flat_w, pos, k).reshape(shape)
+            outs, o = [], 0
+            for e, n_ in enumerate(counts.tolist()):
+                rows = torch.arange(o, o + n_, device=send.device)
+                o += n_
+                part = _F.row_gather(send, rows)
+                outs.append(self.experts[e](part) if n_ else part)
+            y_sorted = _F.concat_rows(outs)
+        return _F.reshape(_route.combine(y_sorted, flat_w, pos, k), shape)
 
     def _forward_capacity(self, x, flat_e, flat_w, T, k, E):
         """Fixed-capacity EP layer with no host sync: send [E * cap] rows (global
@@ -200,7 +249,11 @@ class MoELayer(Layer):
         if self.grouped:
             ye = self.experts.forward_grouped(xe, [rows] * nl)
         else:
-            ye = torch.cat([self.experts[e](xe[e * rows:(e + 1) * rows]) for e in range(nl)])
+            from ...ops import fused as _F
+
+            ye = _F.concat_rows([self.experts[e](_F.row_gather(xe, torch.arange(e * rows, (e + 1) * rows,
+                                                                                  device=xe.device)))
+                                 for e in range(nl)])
         if ep > 1:
             back = _swap(ye, nl, ep)                          # [ep, nl, cap, H] per destination peer
             ys = all_to_all(back, splits, splits, self.group)

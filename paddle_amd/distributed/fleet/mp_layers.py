@@ -285,19 +285,21 @@ class _ParallelCEFn(torch.autograd.Function):
 
 
 def parallel_cross_entropy(logits, label, group, ignore_index=-100, reduction="mean"):
+    from ...ops import fused as _F
+
     W, r = _mp(group)
     N = logits.shape[-1]
-    flat = logits.reshape(-1, N)
-    lab = label.reshape(-1)
+    # the nodes take the logits as produced (any leading dims): a reshape here would be
+    # a view the framework tape cannot see through
     if W == 1:
-        loss = torch.nn.functional.cross_entropy(flat.float(), lab, ignore_index=ignore_index, reduction="none")
+        loss = _F.cross_entropy_tokens(logits, label, ignore_index)
     else:
-        loss = _tape.apply(_ParallelCEFn, flat, lab, r * N, group, ignore_index)
+        loss = _tape.apply(_ParallelCEFn, logits, label, r * N, group, ignore_index)
     if reduction == "none":
-        return loss.reshape(label.shape)
+        return loss
     if reduction == "sum":
         return loss.sum()
-    return loss.sum() / (lab != ignore_index).sum().clamp(min=1)
+    return _F.mean_valid(loss, label, ignore_index)
 
 
 class ParallelCrossEntropy(Layer):

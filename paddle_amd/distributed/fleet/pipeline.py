@@ -29,6 +29,7 @@ import torch
 import torch.distributed as dist
 
 from ...autograd import engine as _eager
+from ...autograd import tape as _tape
 from ...nn import Layer
 from ...parallel import comm
 
@@ -126,7 +127,11 @@ class PipelineLayer(Layer):
     def forward(self, x):
         for i, layer in enumerate(self.run_function):
             args = x if isinstance(x, tuple) else (x,)
-            if self.recompute_interval and self.training and torch.is_grad_enabled() and i % self.recompute_interval == 0:
+            if self.recompute_interval and self.training and i % self.recompute_interval == 0 \
+                    and _tape.current() is not None:
+                x = _tape.checkpoint(layer, *args)  # recomputed on the framework tape
+            elif self.recompute_interval and self.training and torch.is_grad_enabled() \
+                    and i % self.recompute_interval == 0:
                 x = torch.utils.checkpoint.checkpoint(layer, *args, use_reentrant=False)
             else:
                 x = layer(*args)
@@ -327,7 +332,9 @@ class PipelineParallel(Layer):
             fn = self._layers.loss_fn
             lab = label if label is None or len(label) > 1 else label[0]
             loss = fn(out, lab) if fn is not None else out
-            return loss / self.accumulate_steps
+            from ...ops import fused as _F
+
+            return _F.scale(loss, 1.0 / self.accumulate_steps)
         return out
 
     def _grad_sync_engine(self):
@@ -388,15 +395,27 @@ class PipelineParallel(Layer):
         if gs is not None:
             gs.armed = False
         nbwd = [0]
+        # each micro-batch's forward is recorded on its own framework tape (torch
+        # autograd off); its reverse pass is that tape seeded with the next stage's
+        # gradients, and the received activations are the tape's watched inputs
+        use_tape = os.environ.get("FLAGS_pp_autograd", "tape") == "tape"
+        tapes_q = []
 
         def recv_fwd_input(i):
             if self.is_first:
                 return ins[i]
             _, got = p2p.exchange(recv_prev=True)
-            return tuple(t.requires_grad_() if t.is_floating_point() else t for t in got)
+            return tuple(t.requires_grad_() if (t.is_floating_point() and not use_tape) else t for t in got)
 
         def run_fwd(i, x):
-            out = self._fwd(x, labs[i])
+            if use_tape:
+                with _tape.recording() as tp:
+                    for t in x:
+                        tp.watch(t)
+                    out = self._fwd(x, labs[i])
+            else:
+                tp, out = None, self._fwd(x, labs[i])
+            tapes_q.append(tp)
             inputs_q.append(x)
             outputs_q.append(out)
             if self.is_last:
@@ -406,9 +425,20 @@ class PipelineParallel(Layer):
         def run_bwd(grads):
             x = inputs_q.pop(0)
             out = outputs_q.pop(0)
+            tp = tapes_q.pop(0)
             nbwd[0] += 1
             if gs is not None and nbwd[0] == M:
                 gs.armed = True
+            if tp is not None and not any(isinstance(o, _eager.Tensor) and _eager.tracked(o) for o in _as_tuple(out)):
+                if self.is_last:
+                    tp.backward_multi([out], [None])
+                else:
+                    outs = [o for o in _as_tuple(out) if o.is_floating_point()]
+                    tp.backward_multi(outs, list(grads))
+                if self.is_first:
+                    return None
+                return tuple(tp.grad(t) if tp.grad(t) is not None else torch.zeros_like(t)
+                             for t in x if t.is_floating_point())
             if self.is_last:
                 _backward([out], [None])
             else:

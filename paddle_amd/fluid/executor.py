@@ -2,9 +2,12 @@
 
 ``run`` clones the program once per (program, feed, fetch) signature with feed/fetch
 ops inserted (cached; the reference re-creates ops every call unless
-``use_program_cache``), feeds numpy/LoDTensor values onto the executor's place,
-interprets the block with :class:`paddle_amd.framework.executor.BlockExecutor`
-and fetches results (the only host sync).
+``use_program_cache``), feeds numpy/LoDTensor values onto the executor's place and
+runs the block on the C++ executor (``fluid/native_engine.py``; ``engine="auto"``,
+the default, for every program it can take) or on the Python op interpreter
+(:class:`paddle_amd.framework.executor.BlockExecutor`: step-scope control flow,
+SelectedRows / RPC programs, ``engine="python"``), then fetches results (the only
+host sync).
 
 ``Executor(place, use_hip_graph=True)`` additionally captures a steady-state step
 of a static-shape program into a HIP graph and replays it (MI355X-first

@@ -1,7 +1,8 @@
-"""The native C++ executor as an opt-in engine behind ``fluid.Executor``.
+"""The native C++ executor: the default engine behind ``fluid.Executor``.
 
-``fluid.Executor(place, engine="native")`` (or ``FLAGS_executor_engine=native``)
-runs a program's block 0 on the C++ executor of ``csrc/native`` (core.cc
+``fluid.Executor(place)`` (``engine="auto"``, ``FLAGS_executor_engine=auto``) runs
+every program the C++ executor can take on it, ``engine="native"`` insists on it,
+``engine="python"`` keeps the op interpreter.  It runs a program's block 0 on the C++ executor of ``csrc/native`` (core.cc
 Executor::RunBlock, the counterpart of the reference's framework/executor.cc:125-353)
 instead of the Python op interpreter: the program is serialised once
 (ProgramDesc wire format) and every op dispatches to a registered C++ kernel --

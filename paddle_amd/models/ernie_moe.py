@@ -221,5 +221,5 @@ class ErnieMoEForCausalLM(Layer):
         loss = ops.softmax_cross_entropy(logits, labels, inplace_grad=True)
         self.last_ce = loss.detach()  # the next-token cross-entropy alone (loss adds the balance term)
         if aux and self.cfg.aux_loss_coeff:
-            loss = loss + self.cfg.aux_loss_coeff * torch.stack(aux).mean()
+            loss = ops.add(loss, ops.scale(ops.stack_mean(aux), self.cfg.aux_loss_coeff))
         return loss

@@ -21,6 +21,7 @@ from dataclasses import dataclass
 import torch
 
 from .. import ops
+from ..autograd import tape as _tape
 from ..nn import Layer
 from .llama import _dt, _param
 
@@ -99,7 +100,7 @@ class GPTDecoderLayer(Layer):
         # TP it rides the GEMM epilogue
         if not self.tp:
             return ops.linear(x, w, b)
-        return self.tp.reduce_from_region(ops.linear(x, w)) + b
+        return ops.add(self.tp.reduce_from_region(ops.linear(x, w)), b)
 
     def forward(self, x, residual=None):
         cfg, eps = self.cfg, self.cfg.layer_norm_eps
@@ -139,10 +140,9 @@ class GPTEmbeddings(Layer):
             x = vocab_parallel_embedding(input_ids, self.word_embeddings, self.tp.group)
         else:
             x = ops.embedding(input_ids, self.word_embeddings)
-        S = input_ids.shape[1]
-        pos = ops.embedding(position_ids, self.position_embeddings) if position_ids is not None else \
-            self.position_embeddings[:S].unsqueeze(0)
-        return x + pos
+        if position_ids is not None:
+            return ops.add(x, ops.embedding(position_ids, self.position_embeddings))
+        return ops.position_add(x, self.position_embeddings)
 
 
 class GPTForCausalLM(Layer):
@@ -161,7 +161,9 @@ class GPTForCausalLM(Layer):
         x = self.embeddings(input_ids)
         residual = None
         for layer in self.layers:
-            if self.cfg.recompute and self.training and torch.is_grad_enabled():
+            if self.cfg.recompute and self.training and _tape.current() is not None:
+                x, residual = _tape.checkpoint(layer, x, residual)  # recomputed on the framework tape
+            elif self.cfg.recompute and self.training and torch.is_grad_enabled():
                 x, residual = torch.utils.checkpoint.checkpoint(layer, x, residual, use_reentrant=False)
             else:
                 x, residual = layer(x, residual)

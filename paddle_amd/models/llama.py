@@ -25,6 +25,7 @@ from dataclasses import dataclass, field
 import torch
 
 from .. import ops
+from ..autograd import tape as _tape
 from ..nn import Layer
 
 
@@ -181,7 +182,9 @@ class LlamaForCausalLM(Layer):
         residual = None
         cos, sin = self.rope_cos, self.rope_sin
         for layer in self.layers:
-            if self.cfg.recompute and self.training and torch.is_grad_enabled():
+            if self.cfg.recompute and self.training and _tape.current() is not None:
+                x, residual = _tape.checkpoint(layer, x, residual, cos, sin)  # recomputed on the framework tape
+            elif self.cfg.recompute and self.training and torch.is_grad_enabled():
                 x, residual = torch.utils.checkpoint.checkpoint(layer, x, residual, cos, sin,
                                                                 use_reentrant=False)
             else:

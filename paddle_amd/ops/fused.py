@@ -127,6 +127,43 @@ def param_ready(w):
         f(w)
 
 
+class _NormRefFn(torch.autograd.Function):
+    """Host / unsupported-shape RMSNorm / LayerNorm (optionally fused residual add)
+    with its analytic backward, so the reverse pass stays on the framework tape."""
+
+    @staticmethod
+    def forward(ctx, x, res, w, b, eps, rms):
+        h = x.float() + res.float() if res is not None else x.float()
+        if rms:
+            rstd = torch.rsqrt(h.pow(2).mean(-1, keepdim=True) + eps)
+            xhat = h * rstd
+        else:
+            xc = h - h.mean(-1, keepdim=True)
+            rstd = torch.rsqrt(xc.pow(2).mean(-1, keepdim=True) + eps)
+            xhat = xc * rstd
+        y = xhat * w.float()
+        if b is not None:
+            y = y + b.float()
+        ctx.save_for_backward(xhat, rstd, w)
+        ctx.meta = (rms, res is not None, b is not None, x.dtype, None if res is None else res.dtype)
+        return y.to(x.dtype), (h.to(x.dtype) if res is not None else None)
+
+    @staticmethod
+    def backward(ctx, dy, dh):
+        xhat, rstd, w = ctx.saved_tensors
+        rms, has_res, has_b, xdt, rdt = ctx.meta
+        H = xhat.shape[-1]
+        dyf = dy.float()
+        dw = (dyf * xhat).reshape(-1, H).sum(0).to(w.dtype)
+        db = dyf.reshape(-1, H).sum(0).to(w.dtype) if has_b else None
+        g = dyf * w.float()
+        proj = (g * xhat).mean(-1, keepdim=True)
+        dx = rstd * (g - xhat * proj) if rms else rstd * (g - g.mean(-1, keepdim=True) - xhat * proj)
+        if has_res and dh is not None:
+            dx = dx + dh.float()
+        return dx.to(xdt), (dx.to(rdt) if has_res else None), dw, db, None, None
+
+
 def rms_norm(x, weight, eps=1e-6, residual=None):
     """y = x * rsqrt(mean(x^2) + eps) * weight.  With ``residual``: h = x + residual,
     returns (rms_norm(h), h) with the add fused into the same pass."""
@@ -134,7 +171,7 @@ def rms_norm(x, weight, eps=1e-6, residual=None):
     if x.is_cuda:
         y, h = _tape.apply(_NormFn, x, residual, weight, None, eps, True)
         return (y, h) if residual is not None else y
-    y, h = _norm_ref(x, residual, weight, None, eps, True)
+    y, h = _tape.apply(_NormRefFn, x, residual, weight, None, eps, True)
     return (y, h) if residual is not None else y
 
 
@@ -150,7 +187,7 @@ def layer_norm(x, weight, bias=None, eps=1e-5, residual=None):
         h = x + residual if residual is not None else x
         y = torch.nn.functional.layer_norm(h, h.shape[-1:], None, bias, eps)
         return (y, h) if residual is not None else y
-    y, h = _norm_ref(x, residual, weight, bias, eps, False)
+    y, h = _tape.apply(_NormRefFn, x, residual, weight, bias, eps, False)
     return (y, h) if residual is not None else y
 
 
@@ -478,6 +515,51 @@ def qkv_rope_attention(y, w_qkv, cos, sin, num_heads, num_kv_heads=None, causal=
     return rope_attention(linear(y, w_qkv), cos, sin, num_heads, Hk, causal=causal, scale=scale)
 
 
+class _PackedAttnRefFn(torch.autograd.Function):
+    """Host / unsupported-shape attention over a packed [B, S, (Hq+2Hk)*D] projection,
+    with the neox rotary on q / k when ``cos`` is given, and its analytic backward
+    (dV = P^T dO, dS = P (dO V^T - rowsum(dO O)), dQ = s dS K, dK = s dS^T Q; the
+    rotary's backward is the inverse rotation; GQA gradients summed per kv head)."""
+
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, Hq, Hk, D, causal, scale):
+        B, S, W = qkv.shape
+        x = qkv.float().view(B, S, Hq + 2 * Hk, D)
+        q, k, v = x[:, :, :Hq], x[:, :, Hq:Hq + Hk], x[:, :, Hq + Hk:]
+        if cos is not None:
+            q, k = _rope_ref(q, cos, sin), _rope_ref(k, cos, sin)
+        r = Hq // Hk
+        ke, ve = k.repeat_interleave(r, 2), v.repeat_interleave(r, 2)
+        s_ = torch.einsum("bqhd,bkhd->bhqk", q, ke) * scale
+        if causal:
+            s_ = s_.masked_fill(torch.ones(S, S, dtype=torch.bool, device=s_.device).triu(1), float("-inf"))
+        p_ = torch.softmax(s_, -1)
+        o = torch.einsum("bhqk,bkhd->bqhd", p_, ve)
+        ctx.save_for_backward(q, ke, ve, p_, o, cos, sin)
+        ctx.meta = (Hq, Hk, D, scale, qkv.dtype)
+        return o.reshape(B, S, Hq * D).to(qkv.dtype)
+
+    @staticmethod
+    def backward(ctx, do):
+        q, ke, ve, p_, o, cos, sin = ctx.saved_tensors
+        Hq, Hk, D, scale, dt = ctx.meta
+        B, S = q.shape[:2]
+        do = do.float().view(B, S, Hq, D)
+        dv = torch.einsum("bhqk,bqhd->bkhd", p_, do)
+        dp = torch.einsum("bqhd,bkhd->bhqk", do, ve)
+        delta = (do * o).sum(-1).permute(0, 2, 1).unsqueeze(-1)
+        ds = p_ * (dp - delta) * scale
+        dq = torch.einsum("bhqk,bkhd->bqhd", ds, ke)
+        dk = torch.einsum("bhqk,bqhd->bkhd", ds, q)
+        r = Hq // Hk
+        dk = dk.view(B, S, Hk, r, D).sum(3)
+        dv = dv.view(B, S, Hk, r, D).sum(3)
+        if cos is not None:
+            dq, dk = _rope_ref(dq, cos, sin, sign=-1.0), _rope_ref(dk, cos, sin, sign=-1.0)
+        dqkv = torch.cat([dq, dk, dv], 2).reshape(B, S, (Hq + 2 * Hk) * D)
+        return dqkv.to(dt), None, None, None, None, None, None, None
+
+
 def rope_attention(qkv, cos, sin, num_heads, num_kv_heads=None, causal=True, scale=None):
     """Rotary (neox) + causal flash attention on a packed [B, S, (Hq+2Hk)*D] tensor.
     Returns [B, S, Hq*D]."""
@@ -489,11 +571,7 @@ def rope_attention(qkv, cos, sin, num_heads, num_kv_heads=None, causal=True, sca
     if qkv.is_cuda and qkv.dtype == torch.bfloat16 and D in (64, 128):
         return _tape.apply(_RopeAttnFn, qkv, cos, sin, num_heads, Hk, D, causal, scale)
     # other dtypes / head sizes: plain rotary + attention (the kernels are bf16)
-    x = qkv.view(B, S, num_heads + 2 * Hk, D)
-    q = _rope_ref(x[:, :, :num_heads], cos, sin)
-    k = _rope_ref(x[:, :, num_heads:num_heads + Hk], cos, sin)
-    v = x[:, :, num_heads + Hk:]
-    return _attn_ref(q, k, v, causal, scale).reshape(B, S, num_heads * D)
+    return _tape.apply(_PackedAttnRefFn, qkv, cos[:S], sin[:S], num_heads, Hk, D, causal, scale)
 
 
 _IDENT_ROPE = {}
@@ -553,9 +631,7 @@ def packed_attention(qkv, num_heads, causal=True, scale=None):
         scale = 1.0 / math.sqrt(D)
     if qkv.is_cuda and qkv.dtype == torch.bfloat16 and D in (64, 128):
         return _tape.apply(_PackedAttnFn, qkv, num_heads, D, causal, scale)
-    x = qkv.view(B, S, 3 * num_heads, D)
-    q, k, v = x[:, :, :num_heads], x[:, :, num_heads:2 * num_heads], x[:, :, 2 * num_heads:]
-    return _attn_ref(q, k, v, causal, scale).reshape(B, S, num_heads * D)
+    return _tape.apply(_PackedAttnRefFn, qkv, None, None, num_heads, num_heads, D, causal, scale)
 
 
 def apply_rotary(x, cos, sin, inverse=False):
@@ -619,8 +695,25 @@ def swiglu(x, y=None):
         x = torch.cat([x, y], -1)
     if x.is_cuda and (x.shape[-1] // 2) % 8 == 0:
         return _tape.apply(_SwiGLUFn, x)
-    g, u = x.chunk(2, -1)
-    return (torch.nn.functional.silu(g.float()) * u.float()).to(x.dtype)
+    return _tape.apply(_SwiGLURefFn, x)
+
+
+class _SwiGLURefFn(torch.autograd.Function):
+    """Host SwiGLU over [gate | up] with its analytic backward."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.save_for_backward(x)
+        g, u = x.float().chunk(2, -1)
+        return (torch.nn.functional.silu(g) * u).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, d):
+        (x,) = ctx.saved_tensors
+        g, u = x.float().chunk(2, -1)
+        sg = torch.sigmoid(g)
+        d = d.float()
+        return torch.cat([d * u * sg * (1 + g * (1 - sg)), d * g * sg], -1).to(x.dtype)
 
 
 # ---------------------------------------------------------------- fused SwiGLU MLP
@@ -710,6 +803,198 @@ def swiglu_mlp(x, w_gate_up, w_down):
     return _tape.apply(_SwiGLUMLPFn, x, w_gate_up, w_down)
 
 
+# ---------------------------------------------------------------- small tape ops
+# Elementwise glue that models apply to activations between fused ops (a bias added
+# after a row-parallel all-reduce, position embeddings, loss scaling / averaging):
+# each is one recorded node with its hand-written backward, so a forward recorded on
+# the framework tape never leaves it (torch autograd stays off).
+
+
+def _sum_to(g, shape):
+    """Reduce a broadcast gradient back to ``shape``."""
+    if tuple(g.shape) == tuple(shape):
+        return g
+    lead = g.dim() - len(shape)
+    dims = list(range(lead)) + [lead + i for i, n in enumerate(shape) if n == 1 and g.shape[lead + i] != 1]
+    return g.sum(dims, keepdim=False).reshape(shape) if dims else g.reshape(shape)
+
+
+class _AddFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.shapes = (a.shape, b.shape, a.dtype, b.dtype)
+        if a.is_cuda and a.shape == b.shape and a.dtype == b.dtype and a.is_contiguous() and b.is_contiguous():
+            from . import oplib
+
+            r = oplib.binary("add", a, b)
+            if r is not None:
+                return r
+        return a + b
+
+    @staticmethod
+    def backward(ctx, g):
+        sa, sb, da, db = ctx.shapes
+        return _sum_to(g, sa).to(da), _sum_to(g, sb).to(db)
+
+
+def add(a, b):
+    """a + b (b broadcast onto a, e.g. a bias) as one recorded node."""
+    return _tape.apply(_AddFn, a, b)
+
+
+class _ScaleFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, s):
+        ctx.s = s
+        return x * s
+
+    @staticmethod
+    def backward(ctx, g):
+        return g * ctx.s, None
+
+
+def scale(x, s):
+    """x * s for a Python scalar s (loss / accumulate_steps) as one recorded node."""
+    return _tape.apply(_ScaleFn, x, float(s))
+
+
+class _PositionAddFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, table):
+        S = x.shape[-2]
+        ctx.S, ctx.tshape, ctx.tdtype = S, table.shape, table.dtype
+        return x + table[:S].to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        dt = torch.zeros(ctx.tshape, dtype=torch.float32, device=g.device)
+        dt[:ctx.S] = g.float().reshape(-1, ctx.S, g.shape[-1]).sum(0)
+        return g, dt.to(ctx.tdtype)
+
+
+def position_add(x, table):
+    """x [B, S, H] + table[:S] (learned absolute position embeddings)."""
+    return _tape.apply(_PositionAddFn, x, table)
+
+
+class _MeanValidFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, loss, label, ignore_index):
+        valid = (label != ignore_index)
+        n = valid.sum().clamp_min(1).to(torch.float32)
+        ctx.save_for_backward(valid, n)
+        return (loss.float() * valid).sum() / n
+
+    @staticmethod
+    def backward(ctx, g):
+        valid, n = ctx.saved_tensors
+        return (g / n) * valid.to(torch.float32), None, None
+
+
+def mean_valid(loss, label, ignore_index=-100):
+    """Mean of per-token losses over the labels that are not ``ignore_index``."""
+    return _tape.apply(_MeanValidFn, loss, label, ignore_index)
+
+
+class _ReshapeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, shape):
+        ctx.shape = x.shape
+        return x.reshape(shape)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.reshape(ctx.shape), None
+
+
+def reshape(x, shape):
+    """x.reshape(shape) as a recorded node (a plain view of a tape activation would be
+    invisible to the tape)."""
+    return _tape.apply(_ReshapeFn, x, tuple(shape))
+
+
+class _RowGatherFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, idx):
+        ctx.save_for_backward(idx)
+        ctx.rows = x.shape[0]
+        return x.index_select(0, idx)
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        dx = torch.zeros((ctx.rows,) + tuple(g.shape[1:]), dtype=g.dtype, device=g.device)
+        return dx.index_add_(0, idx, g), None
+
+
+def row_gather(x, idx):
+    """x[idx] along rows (a permutation / selection) as a recorded node."""
+    return _tape.apply(_RowGatherFn, x, idx)
+
+
+class _ConcatRowsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *xs):
+        ctx.sizes = [x.shape[0] for x in xs]
+        return torch.cat(xs, 0)
+
+    @staticmethod
+    def backward(ctx, g):
+        return tuple(g.split(ctx.sizes, 0))
+
+
+def concat_rows(xs):
+    """torch.cat(xs, 0) as a recorded node."""
+    return _tape.apply(_ConcatRowsFn, *xs)
+
+
+class _StackMeanFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *ts):
+        ctx.n = len(ts)
+        return torch.stack([t.float() for t in ts]).mean(0)
+
+    @staticmethod
+    def backward(ctx, g):
+        return tuple(g / ctx.n for _ in range(ctx.n))
+
+
+def stack_mean(ts):
+    """Mean of same-shaped tensors (e.g. per-layer MoE balance losses)."""
+    return _tape.apply(_StackMeanFn, *ts)
+
+
+class _CrossEntropyRefFn(torch.autograd.Function):
+    """Per-token log-softmax + NLL (fp32) for host / unsupported tensors."""
+
+    @staticmethod
+    def forward(ctx, logits, label, ignore_index):
+        lf = logits.float().reshape(-1, logits.shape[-1])
+        lab = label.reshape(-1).long()
+        lse = torch.logsumexp(lf, -1)
+        safe = lab.clamp_min(0)
+        loss = lse - lf.gather(1, safe.unsqueeze(1)).squeeze(1)
+        loss = torch.where(lab == ignore_index, torch.zeros_like(loss), loss)
+        ctx.save_for_backward(lf, lab, lse)
+        ctx.meta = (logits.shape, logits.dtype, ignore_index)
+        return loss.view(label.shape)
+
+    @staticmethod
+    def backward(ctx, g):
+        lf, lab, lse = ctx.saved_tensors
+        shape, dt, ign = ctx.meta
+        p = torch.exp(lf - lse.unsqueeze(1))
+        p[torch.arange(lab.numel()), lab.clamp_min(0)] -= 1.0
+        p = p * (g.reshape(-1, 1).float() * (lab != ign).unsqueeze(1))
+        return p.view(shape).to(dt), None, None
+
+
+def cross_entropy_tokens(logits, label, ignore_index=-100):
+    """Per-token cross entropy (fp32) as one recorded node (the host path of
+    :func:`softmax_cross_entropy`)."""
+    return _tape.apply(_CrossEntropyRefFn, logits, label, ignore_index)
+
+
 # ====================================================================== softmax CE
 
 
@@ -783,15 +1068,12 @@ def softmax_cross_entropy(logits, label, ignore_index=-100, reduction="mean", in
     if logits.is_cuda:
         loss, _ = _tape.apply(_SoftmaxCEFn, logits, label, ignore_index, inplace_grad)
     else:
-        lf = logits.float().reshape(-1, logits.shape[-1])
-        loss = torch.nn.functional.cross_entropy(lf, label.reshape(-1).long(), ignore_index=ignore_index,
-                                                 reduction="none").view(label.shape)
+        loss = cross_entropy_tokens(logits, label, ignore_index)
     if reduction == "none":
         return loss
     if reduction == "sum":
         return loss.sum()
-    valid = (label != ignore_index).sum().clamp_min(1)
-    return loss.sum() / valid
+    return mean_valid(loss, label, ignore_index)
 
 
 class _SoftmaxFn(torch.autograd.Function):
@@ -863,7 +1145,28 @@ def embedding(ids, weight, padding_idx=None):
     pad = -1 if padding_idx is None else int(padding_idx)
     if weight.is_cuda and weight.shape[1] % 8 == 0:
         return _tape.apply(_EmbeddingFn, ids, weight, pad)
-    return torch.nn.functional.embedding(ids.long(), weight, padding_idx=padding_idx)
+    return _tape.apply(_EmbeddingRefFn, ids, weight, pad)
+
+
+class _EmbeddingRefFn(torch.autograd.Function):
+    """Host embedding lookup; dW is a row scatter-add (the padding row gets none)."""
+
+    @staticmethod
+    def forward(ctx, ids, w, pad):
+        ctx.save_for_backward(ids)
+        ctx.meta = (w.shape, w.dtype, pad)
+        return w[ids.long()]
+
+    @staticmethod
+    def backward(ctx, g):
+        (ids,) = ctx.saved_tensors
+        shape, dt, pad = ctx.meta
+        idx = ids.reshape(-1).long()
+        gf = g.reshape(-1, shape[1]).float()
+        if pad >= 0:
+            gf = gf * (idx != pad).unsqueeze(1)
+        dw = torch.zeros(shape, dtype=torch.float32, device=g.device).index_add_(0, idx, gf)
+        return None, dw.to(dt), None
 
 
 # ====================================================================== transpose
@@ -1135,10 +1438,12 @@ class _LinearGeluFn(torch.autograd.Function):
         if _fast_bias_ok(dg2) and dg2.dtype == z2.dtype:
             dz2, db = _bias_act_bwd(dg2, _c(z2))
         else:
-            with torch.enable_grad():
-                zz = z2.detach().requires_grad_(True)
-                gg = F.gelu(zz, approximate="tanh")
-            dz2, = torch.autograd.grad(gg, zz, dg2)
+            # analytic tanh-GELU derivative (no autograd on the host path)
+            zf = z2.float()
+            c = math.sqrt(2.0 / math.pi)
+            t = torch.tanh(c * (zf + 0.044715 * zf.pow(3)))
+            dgelu = 0.5 * (1 + t) + 0.5 * zf * (1 - t * t) * c * (1 + 3 * 0.044715 * zf * zf)
+            dz2 = (dg2.float() * dgelu).to(dg2.dtype)
             db = dz2.sum(0).to(dg.dtype)
         dz = dz2.view(z.shape)
         dx, dw = _linear_bwd(ctx, x, w, dz, ctx.needs_input_grad[0], ctx.needs_input_grad[1])

@@ -63,6 +63,7 @@ class _CombineFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ys, w, pos, k, padded=False):
         ys = _c(ys)
+        ctx.wshape = w.shape  # [T * k] or [T, k]
         w = _c(w.float())
         T, H = pos.numel() // k, ys.shape[1]
         y = torch.empty(T, H, dtype=ys.dtype, device=ys.device)
@@ -82,14 +83,30 @@ class _CombineFn(torch.autograd.Function):
         dw = torch.empty(T * k, dtype=torch.float32, device=dy.device)
         N.call("pa_moe_combine_bwd", N.ptr(dy), N.ptr(ys), N.ptr(pos), N.ptr(w), N.ptr(dys), N.ptr(dw), T, k, H,
                N.stream())
-        return dys, dw, None, None, None
+        return dys, dw.view(ctx.wshape), None, None, None
 
 
 def dispatch(x, src, pos, k):
     """x [T, H] -> rows in sorted order [R, H]."""
     if _native_ok(x):
         return _tape.apply(_DispatchFn, x, src, pos, k)
-    return x[src.long()]
+    return _tape.apply(_DispatchRefFn, x, src, pos, k)
+
+
+class _DispatchRefFn(torch.autograd.Function):
+    """Host dispatch (row gather) with its scatter-add backward."""
+
+    @staticmethod
+    def forward(ctx, x, src, pos, k):
+        ctx.save_for_backward(src)
+        ctx.T = x.shape[0]
+        return x[src.long()]
+
+    @staticmethod
+    def backward(ctx, g):
+        (src,) = ctx.saved_tensors
+        dx = torch.zeros(ctx.T, g.shape[1], dtype=g.dtype, device=g.device).index_add_(0, src.long(), g)
+        return dx, None, None, None
 
 
 def capacity_routing(flat_e, T, k, E, cap):
@@ -119,10 +136,32 @@ def combine(ys, w, pos, k, padded=False):
     rows of ys are referenced by no slot (capacity layout; their gradient is 0)."""
     if _native_ok(ys):
         return _tape.apply(_CombineFn, ys, w, pos, k, padded)
-    T = pos.numel() // k
-    keep = pos >= 0
-    slots = keep.nonzero().squeeze(-1)
-    rows = pos[slots].long()
-    y = torch.zeros(T, ys.shape[1], dtype=ys.dtype, device=ys.device)
-    contrib = ys[rows] * w[slots].unsqueeze(-1).to(ys.dtype)
-    return y.index_add(0, torch.div(slots, k, rounding_mode="floor"), contrib)
+    return _tape.apply(_CombineRefFn, ys, w, pos, k)
+
+
+class _CombineRefFn(torch.autograd.Function):
+    """Host combine: y[t] = sum_j w[t, j] ys[pos[t, j]] (dropped slots: pos -1), with
+    its backward (dys = scatter of w dy, dw = <dy, ys> per slot)."""
+
+    @staticmethod
+    def forward(ctx, ys, w, pos, k):
+        T = pos.numel() // k
+        wf = w.reshape(-1)
+        keep = pos >= 0
+        slots = keep.nonzero().squeeze(-1)
+        rows = pos[slots].long()
+        tok = torch.div(slots, k, rounding_mode="floor")
+        y = torch.zeros(T, ys.shape[1], dtype=ys.dtype, device=ys.device)
+        y.index_add_(0, tok, ys[rows] * wf[slots].unsqueeze(-1).to(ys.dtype))
+        ctx.save_for_backward(ys, wf, slots, rows, tok)
+        ctx.wshape = w.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        ys, wf, slots, rows, tok = ctx.saved_tensors
+        dys = torch.zeros_like(ys)
+        dys.index_add_(0, rows, dy[tok] * wf[slots].unsqueeze(-1).to(dy.dtype))
+        dw = torch.zeros(wf.numel(), dtype=wf.dtype, device=wf.device)
+        dw[slots] = (dy[tok].float() * ys[rows].float()).sum(-1).to(wf.dtype)
+        return dys, dw.view(ctx.wshape), None, None

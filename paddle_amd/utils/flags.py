@@ -30,7 +30,7 @@ _DEFAULTS = {
     "rpc_server_profile_path": "./profile_ps",
     "workspace_size_MB": 4096,
     # MI355X additions
-    "allocator_strategy": "torch_caching",  # or "buddy" (native C++ buddy allocator)
+    "allocator_strategy": "buddy",  # the native C++ buddy allocator behind torch (paddle_amd/__init__.py); any other value keeps torch's caching allocator
     "use_hip_graph": False,
     "rccl_bucket_mb": 256,
     "executor_engine": "auto",  # fluid.Executor engine: "auto" (C++ executor for every program it can take), "python" (op interpreter) or "native"
