@@ -28,8 +28,9 @@ def build(name, device, args):
     if name.startswith("gpt"):
         from paddle_amd.models.gpt import GPT_CONFIGS, GPTConfig, GPTForCausalLM, gpt_flops_per_token
 
-        cfg = GPTConfig(**GPT_CONFIGS[name], recompute=args.recompute, max_position_embeddings=max(2048,
-                                                                                                  args.seq_len))
+        cfgd = dict(GPT_CONFIGS[name])
+        cfgd["max_position_embeddings"] = max(cfgd.get("max_position_embeddings", 2048), args.seq_len)
+        cfg = GPTConfig(**cfgd, recompute=args.recompute)
         return GPTForCausalLM(cfg, device), cfg, gpt_flops_per_token(cfg, args.seq_len)
     if name.startswith("ernie"):
         from paddle_amd.models.ernie_moe import ERNIE_MOE_CONFIGS, ErnieMoEConfig, ErnieMoEForCausalLM

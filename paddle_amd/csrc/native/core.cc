@@ -5,6 +5,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <fstream>
@@ -420,6 +421,12 @@ void Scope::Erase(const std::string& name) {
   vars_.erase(name);
 }
 
+Scope& Scope::Root() {
+  Scope* s = this;
+  while (s->parent_) s = const_cast<Scope*>(s->parent_);
+  return *s;
+}
+
 std::vector<std::string> Scope::LocalNames() const {
   std::lock_guard<std::mutex> g(mu_);
   std::vector<std::string> out;
@@ -581,21 +588,35 @@ std::vector<Tensor*> OpRun::ins(const std::string& slot) const {
 }
 
 Tensor* OpRun::out(const std::string& slot, size_t i) const {
+  Variable* v = out_var(slot, i);
+  return v ? &v->tensor : nullptr;
+}
+
+Variable* OpRun::in_var(const std::string& slot, size_t i) const {
+  auto& names = op.Inputs(slot);
+  PA_CHECK(i < names.size(), "%s: missing input %s[%zu]", op.type.c_str(), slot.c_str(), i);
+  return var(names[i]);
+}
+
+Variable* OpRun::out_var(const std::string& slot, size_t i) const {
   auto& names = op.Outputs(slot);
   if (i >= names.size() || names[i].empty() || names[i] == "@EMPTY@") return nullptr;
   Variable* v = scope.Find(names[i]);
   if (!v) v = scope.Var(names[i]);
-  return &v->tensor;
+  return v;
 }
 
 // ================================================================ executor
 Executor::Executor(int device) {
   ctx_.device = device;
+  const char* sn = getenv("FLAGS_strict_native");
+  strict_native = sn && (strcmp(sn, "1") == 0 || strcmp(sn, "true") == 0 || strcmp(sn, "True") == 0);
   if (device >= 0) {
     link_device_kernels();
     own_stream_ = ctx_.stream = device_stream_create(device);
   }
   link_host_kernels();
+  link_control_kernels();
 }
 
 Executor::~Executor() {
@@ -623,26 +644,138 @@ bool Executor::ReadBool(const Tensor& t) {
   return ReadBool(h);
 }
 
-// while_op.cc: run the sub-block while Condition holds.  Forward semantics (the
-// reference's is_test path): one child scope holds the body's temporaries for the
-// whole loop; variables of enclosing scopes are updated in place.  Gradient
-// programs (while_grad needs per-step scopes) run on the Python engine.
+// while_op.cc: run the sub-block while Condition holds; variables of enclosing
+// scopes are updated in place.  Inference (is_test, or no StepScopes output): one
+// child scope holds the body's temporaries for the whole loop.  Training: every
+// iteration runs in a fresh child scope that is KEPT in the StepScopes variable
+// (kStepScopes), so the step-local activations survive for while_grad; the scopes
+// of the previous run are dropped when the loop runs again.
 void Executor::RunWhile(const ProgramDesc& prog, const OpDesc& op, Scope* scope) {
   const int sb = (int)op.GetInt("sub_block", -1);
   PA_CHECK(sb >= 0 && sb < (int)prog.blocks.size(), "while: bad sub_block %d", sb);
   const std::string cond = op.Input("Condition");
   Variable* cv = scope->Find(cond);
   PA_CHECK(cv != nullptr, "while: condition %s not found", cond.c_str());
-  Scope& body = scope->NewScope();
   const BlockDesc& blk = prog.Block(sb);
-  for (const VarDesc& v : blk.vars)
-    if (!scope->Find(v.name)) body.Var(v.name)->kind = v.type;
+  auto declare = [&](Scope& s) {
+    for (const VarDesc& v : blk.vars)
+      if (!scope->Find(v.name)) s.Var(v.name)->kind = v.type;
+  };
+  const std::string ss = op.Output("StepScopes");
+  const bool keep = !ss.empty() && !op.GetBool("is_test", false) && !ctx_.is_test;
   int64_t iters = 0;
+  if (!keep) {
+    Scope& body = scope->NewScope();
+    declare(body);
+    while (ReadBool(cv->tensor)) {
+      RunBlock(prog, blk, &body);
+      PA_CHECK(++iters < (int64_t)1 << 40, "while: runaway loop");
+    }
+    scope->DropKid(&body);  // device buffers of the body's temporaries are stream-ordered frees
+    return;
+  }
+  Variable* sv = scope->Find(ss);
+  if (!sv) sv = scope->Var(ss);
+  sv->kind = VK_STEP_SCOPES;
+  for (Scope* s : sv->steps) sv->steps_owner->DropKid(s);
+  sv->steps.clear();
+  sv->steps_owner = scope;
   while (ReadBool(cv->tensor)) {
-    RunBlock(prog, blk, &body);
+    Scope& step = scope->NewScope();
+    sv->steps.push_back(&step);
+    declare(step);
+    RunBlock(prog, blk, &step);
     PA_CHECK(++iters < (int64_t)1 << 40, "while: runaway loop");
   }
-  scope->DropKid(&body);  // device buffers of the body's temporaries are stream-ordered frees
+}
+
+namespace {
+// acc += x for fp32 tensors on one place; an empty `acc` takes a private copy of x
+void accumulate_into(Tensor& acc, const Tensor& x, void* stream) {
+  PA_CHECK(x.dtype == DT::FP32, "while_grad: gradient %s is not float32", dt_name(x.dtype));
+  if (!acc.initialized()) {
+    acc.alloc(DT::FP32, x.dims, x.device);
+    device_copy(acc.raw(), x.device, x.raw(), x.device, x.nbytes(), stream);
+    return;
+  }
+  PA_CHECK(acc.numel() == x.numel() && acc.device == x.device, "while_grad: step gradients differ in shape");
+  if (x.device >= 0) {
+    device_add_f32(stream, acc.data<float>(), x.data<float>(), x.numel());
+  } else {
+    float* a = acc.data<float>();
+    const float* b = x.data<float>();
+    for (int64_t i = 0; i < x.numel(); ++i) a[i] += b[i];
+  }
+}
+}  // namespace
+
+// while_op.cc WhileGradOp::RunImpl: the grad block runs once per kept step scope,
+// last step first, each time in a fresh child of that step scope (so it reads the
+// step's forward activations).  Gradients of tensor ARRAYS (DynamicRNN memories and
+// outputs) are ONE variable in the enclosing scope shared by every step (slot t
+// written by reverse step t is read by reverse step t - 1); gradients of dense
+// loop-invariant inputs (parameters, static inputs) are step-local and summed into
+// the enclosing X@GRAD; an input no step produced a gradient for gets zeros.
+void Executor::RunWhileGrad(const ProgramDesc& prog, const OpDesc& op, Scope* scope) {
+  const int sb = (int)op.GetInt("sub_block", -1);
+  PA_CHECK(sb >= 0 && sb < (int)prog.blocks.size(), "while_grad: bad sub_block %d", sb);
+  const BlockDesc& blk = prog.Block(sb);
+  const auto& xs = op.Inputs("X");
+  const auto& xgs = op.Outputs("X@GRAD");
+  Variable* sv = scope->Find(op.Input("StepScopes"));
+  PA_CHECK(sv != nullptr, "while_grad: step scopes %s not found", op.Input("StepScopes").c_str());
+  std::set<std::string> arrays, shared;
+  auto note_array = [&](const std::string& n) {
+    Variable* v = scope->Find(n);
+    if (!v || v->kind != VK_LOD_TENSOR_ARRAY) return;
+    arrays.insert(n);
+    const std::string gn = n + "@GRAD";
+    Variable* gv = scope->Find(gn);
+    if (!gv) gv = scope->Var(gn);
+    if (gv->kind != VK_LOD_TENSOR_ARRAY) {
+      gv->kind = VK_LOD_TENSOR_ARRAY;
+      gv->list.clear();
+      gv->tensor = Tensor();
+    }
+    shared.insert(gn);
+  };
+  for (auto& n : xs) note_array(n);
+  for (auto& n : op.Inputs("Out")) note_array(n);
+  std::map<std::string, Tensor> acc;
+  for (size_t k = sv->steps.size(); k-- > 0;) {
+    Scope* s = sv->steps[k];
+    Scope& gs = s->NewScope();
+    for (const VarDesc& v : blk.vars)
+      if (!v.persistable && !shared.count(v.name)) gs.Var(v.name)->kind = v.type;
+    for (size_t i = 0; i < xs.size() && i < xgs.size(); ++i)
+      if (xgs[i] != "@EMPTY@" && !arrays.count(xs[i]) && !gs.FindLocal(xgs[i])) gs.Var(xgs[i]);
+    RunBlock(prog, blk, &gs);
+    for (size_t i = 0; i < xs.size() && i < xgs.size(); ++i) {
+      if (xgs[i] == "@EMPTY@" || arrays.count(xs[i])) continue;
+      Variable* g = gs.FindLocal(xgs[i]);
+      if (g && g->tensor.initialized()) accumulate_into(acc[xgs[i]], g->tensor, ctx_.stream);
+    }
+    s->DropKid(&gs);
+  }
+  for (size_t i = 0; i < xs.size() && i < xgs.size(); ++i) {
+    if (xgs[i] == "@EMPTY@" || arrays.count(xs[i])) continue;
+    Variable* x = scope->Find(xs[i]);
+    Variable* out = scope->Find(xgs[i]);
+    if (!out) out = scope->Var(xgs[i]);
+    out->kind = VK_LOD_TENSOR;
+    auto it = acc.find(xgs[i]);
+    if (it != acc.end()) {
+      out->tensor = it->second;
+      if (x) out->tensor.lod = x->tensor.lod;
+    } else if (x && x->tensor.initialized() && x->tensor.dtype == DT::FP32) {
+      Tensor z;
+      z.alloc(DT::FP32, x->tensor.dims, x->tensor.device);
+      if (z.device >= 0) device_fill(ctx_.stream, z.raw(), DT::FP32, z.numel(), 0.0);
+      else std::fill_n(z.data<float>(), z.numel(), 0.f);
+      z.lod = x->tensor.lod;
+      out->tensor = z;
+    }
+  }
 }
 
 // conditional_block_op.cc: run the sub-block once when the condition holds
@@ -685,6 +818,17 @@ void Executor::RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* 
   static const std::set<std::string> host_scalar = {"fill_constant", "increment", "less_than", "less_equal",
                                                     "greater_than", "greater_equal", "equal", "not_equal",
                                                     "logical_and", "logical_or", "logical_xor", "logical_not"};
+  // every input is an initialised host tensor (and there is at least one)
+  auto host_inputs = [&](const OpDesc& op) {
+    int n = 0;
+    for (auto& slot : op.inputs)
+      for (auto& name : slot.second) {
+        Variable* v = scope->Find(name);
+        if (!v || !v->tensor.initialized() || v->tensor.device >= 0) return false;
+        ++n;
+      }
+    return n > 0;
+  };
   auto timed = [&](const OpDesc& op, const std::function<void()>& fn) {
     if (!profile) return fn();
     Sync();
@@ -697,6 +841,8 @@ void Executor::RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* 
   };
   // host kernel on host copies of the device inputs; results go back to HBM
   auto host_fallback = [&](const OpDesc& op, const Kernel* k) {
+    PA_CHECK(!strict_native, "FLAGS_strict_native: op '%s' has no device kernel for this configuration and "
+             "would run on host copies of its device inputs", op.type.c_str());
     host_fallbacks[op.type] += 1;
     Scope& tmp = scope->NewScope();
     for (auto& slot : op.inputs)
@@ -757,6 +903,19 @@ void Executor::RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* 
       timed(op, [&] { RunConditionalBlock(prog, op, scope); });
       continue;
     }
+    if (op.type == "while_grad") {
+      timed(op, [&] { RunWhileGrad(prog, op, scope); });
+      continue;
+    }
+    // loop counters / bounds that live on the host (fill_constant force_cpu,
+    // max_sequence_len, lod_array_length): the host kernel IS their kernel on a device
+    // place too (the reference's CPU-pinned control tensors), no round trip
+    if (dev && host_scalar.count(op.type) && host_inputs(op)) {
+      if (const Kernel* hk = find_kernel(op.type, false)) {
+        timed(op, [&] { (*hk)(OpRun{op, *scope, ctx_}); });
+        continue;
+      }
+    }
     const Kernel* dk = dev ? find_kernel(op.type, true) : nullptr;
     if (dk) {
       try {
@@ -804,7 +963,13 @@ void Executor::Run(const ProgramDesc& prog, Scope* scope, int block_id, Scope* l
     // predictors sharing one parameter scope never share them
     const bool io = v.type == VK_FEED_MINIBATCH || v.type == VK_FETCH_LIST;
     Scope* s = v.persistable && !io ? scope : tmp;
-    if (tmp->Find(v.name)) continue;
+    if (Variable* have = tmp->Find(v.name)) {
+      // temporaries start every run empty (the reference drops its local scope after
+      // a run): a tensor array left from the previous batch would be appended to /
+      // accumulated into with stale shapes
+      if (!v.persistable && have->kind == VK_LOD_TENSOR_ARRAY) have->list.clear();
+      continue;
+    }
     Variable* var = s->Var(v.name);
     var->kind = v.type;
   }

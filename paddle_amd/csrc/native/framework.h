@@ -67,7 +67,8 @@ struct Attr {
 
 // VarType.Type values that are not tensors
 enum VarKind { VK_LOD_TENSOR = 7, VK_SELECTED_ROWS = 8, VK_FEED_MINIBATCH = 9, VK_FETCH_LIST = 10,
-               VK_STEP_SCOPES = 11, VK_LOD_TENSOR_ARRAY = 13, VK_READER = 15, VK_RAW = 17 };
+               VK_STEP_SCOPES = 11, VK_LOD_RANK_TABLE = 12, VK_LOD_TENSOR_ARRAY = 13, VK_READER = 15,
+               VK_RAW = 17 };
 
 struct VarDesc {
   std::string name;
@@ -149,10 +150,28 @@ struct Tensor {
 };
 
 // ---------------------------------------------------------------- variables / scopes
+class Scope;
+
+// lod_rank_table.h: one entry per sequence of the ranked LoD level, longest first
+// (stable for equal lengths)
+struct RankItem {
+  int64_t index, length;
+};
+
 struct Variable {
   int kind = VK_LOD_TENSOR;
-  Tensor tensor;
+  Tensor tensor;             // LOD_TENSOR; SELECTED_ROWS: the value rows [rows.size(), ...]
   std::vector<Tensor> list;  // FEED_MINIBATCH / FETCH_LIST / LOD_TENSOR_ARRAY
+  // SELECTED_ROWS (selected_rows.h): row indices into a [height, ...] dense table
+  std::vector<int64_t> rows;
+  int64_t height = 0;
+  // LOD_RANK_TABLE: the ranked items and the LoD levels above the ranked one
+  std::vector<RankItem> rank;
+  LoD rank_coarse_lod;
+  // STEP_SCOPES: the per-iteration child scopes of `steps_owner` a training `while`
+  // keeps for its while_grad (while_op.cc kStepScopes); dropped when the loop reruns
+  std::vector<Scope*> steps;
+  Scope* steps_owner = nullptr;
 };
 
 class Scope {
@@ -166,6 +185,7 @@ class Scope {
   void Erase(const std::string& name);
   std::vector<std::string> LocalNames() const;
   const Scope* parent() const { return parent_; }
+  Scope& Root();  // the outermost ancestor (per-device workspaces live there)
 
  private:
   const Scope* parent_;
@@ -197,6 +217,8 @@ struct OpRun {
   std::vector<Tensor*> ins(const std::string& slot) const;
   Tensor* out(const std::string& slot, size_t i = 0) const;      // null if the slot is empty
   Variable* var(const std::string& name) const;
+  Variable* in_var(const std::string& slot, size_t i = 0) const;   // must exist
+  Variable* out_var(const std::string& slot, size_t i = 0) const;  // found or created; null if empty
 };
 
 using Kernel = std::function<void(const OpRun&)>;
@@ -214,6 +236,7 @@ struct KernelRegistrar {
 // forces the static registrars of every kernel translation unit to be linked
 void link_host_kernels();
 void link_device_kernels();
+void link_control_kernels();
 
 // ---------------------------------------------------------------- executor
 class Executor {
@@ -231,6 +254,8 @@ class Executor {
   std::map<std::string, std::pair<int64_t, double>> op_time_ms;  // type -> (calls, ms)
   // device executors: ops that ran on host copies (no device kernel, or it declined)
   std::map<std::string, int64_t> host_fallbacks;
+  // FLAGS_strict_native: a device-place op that would run on host copies is an error
+  bool strict_native = false;
   // Per-op fallback for op types with no C++ kernel (the embedder's registered
   // kernel, e.g. the Python op library behind fluid.Executor(engine="native")):
   // called with the op, the scope it runs in, and its (block, op) position.
@@ -245,6 +270,8 @@ class Executor {
   // conditional_block_op.cc): forward execution of `while` / `conditional_block`
   void RunWhile(const ProgramDesc& prog, const OpDesc& op, Scope* scope);
   void RunConditionalBlock(const ProgramDesc& prog, const OpDesc& op, Scope* scope);
+  // while_op.cc WhileGradOp: the grad block once per kept step scope, last step first
+  void RunWhileGrad(const ProgramDesc& prog, const OpDesc& op, Scope* scope);
 
  private:
   bool ReadBool(const Tensor& t);
@@ -286,5 +313,33 @@ void device_stream_destroy(void* s);
 void device_stream_sync(void* s);
 void device_synchronize(int dev);
 int device_count();
+
+// Device row movement / arithmetic behind the place-agnostic kernels of
+// ops_control.cc (tensor arrays, rank tables, SelectedRows): the row maps are built
+// on the host from LoD metadata and uploaded through the op's pinned staging buffer.
+// Row sizes are in bytes; `add` scatters accumulate fp32 rows (duplicates allowed).
+void device_gather_rows(const OpRun& r, const void* src, int64_t row_bytes, const std::vector<int64_t>& rows,
+                        void* dst);
+void device_scatter_rows(const OpRun& r, const void* src, int64_t row_bytes, const std::vector<int64_t>& rows,
+                         void* dst, bool add);
+void device_add_f32(void* stream, float* acc, const float* x, int64_t n);
+void device_copy2d(const OpRun& r, void* dst, size_t dpitch, const void* src, size_t spitch, size_t width,
+                   size_t height);
+// sparse optimizer rows on HBM: Param[rows[i]] -= lr * V[i] (atomic: duplicates add)
+void device_sgd_rows(const OpRun& r, float* p, const float* v, const std::vector<int64_t>& rows, int64_t w,
+                     const float* lr);
+// Adam on the (unique) rows of Param / Moment1 / Moment2 with the merged gradient g
+void device_adam_rows(const OpRun& r, float* p, float* m1, float* m2, const float* g,
+                      const std::vector<int64_t>& rows, int64_t w, const float* lr, const float* b1p,
+                      const float* b2p, float b1, float b2, float eps);
+void device_fill(void* stream, void* dst, DT dt, int64_t n, double v);
+
+// SelectedRows-aware paths of sum / sgd / adam (ops_control.cc): true when the op's
+// gradient / inputs were SelectedRows and the op has been run
+bool selected_rows_sum(const OpRun& r);
+bool selected_rows_sgd(const OpRun& r);
+bool selected_rows_adam(const OpRun& r);
+// lookup_table_grad with is_sparse: W@GRAD = SelectedRows{Ids, Out@GRAD rows}
+void lookup_table_grad_sparse(const OpRun& r);
 
 }  // namespace pa

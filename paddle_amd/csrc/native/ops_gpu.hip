@@ -74,7 +74,9 @@ float* out_f32(const OpRun& r, const std::string& slot, const Dims& d, const Ten
 
 // scope-held device workspace (kept across ops / runs: steady-state steps reuse it)
 float* workspace(const OpRun& r, const char* name, int64_t n) {
-  Variable* v = r.scope.Var(name);
+  // held by the root scope: ops inside per-step scopes (while / while_grad) reuse one
+  // buffer instead of allocating (and hipFree-syncing) one per step
+  Variable* v = r.scope.Root().Var(name);
   if (v->tensor.initialized() && v->tensor.device == D(r) && v->tensor.numel() >= n) return f32(v->tensor);
   return v->tensor.alloc<float>({std::max<int64_t>(n, 1)}, D(r));
 }
@@ -296,6 +298,17 @@ void k_scale(const OpRun& r) {
   float* o = out_f32(r, "Out", x.dims, &x);
   r.out("Out")->lod = lod;
   launch_scale(r, x, o, s, after ? b : b * s);
+}
+
+// scale's gradient (the auto-VJP grad op of the Python library): dX = scale * dOut
+void k_scale_grad(const OpRun& r) {
+  Tensor g = r.in("Out@GRAD");
+  Tensor* dx = r.out("X@GRAD");
+  if (!dx) return;
+  const LoD lod = g.lod;
+  float* o = out_f32(r, "X@GRAD", g.dims, &g);
+  dx->lod = lod;
+  launch_scale(r, g, o, r.op.GetFloat("scale", 1.f), 0.f);
 }
 
 void k_dropout(const OpRun& r) {
@@ -750,16 +763,16 @@ __global__ void reduce_kernel(const float* __restrict__ x, float* __restrict__ o
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t a = i / post, c = i % post;
     const float* p = x + a * R * post + c;
-    float acc = kind == 2 ? -INFINITY : kind == 3 ? INFINITY : 0.f;
+    float acc = kind == 2 ? -INFINITY : kind == 3 ? INFINITY : kind == 4 ? 1.f : 0.f;
     for (int64_t k = 0; k < R; ++k) {
       const float v = p[k * post];
-      acc = kind == 2 ? fmaxf(acc, v) : kind == 3 ? fminf(acc, v) : acc + v;
+      acc = kind == 2 ? fmaxf(acc, v) : kind == 3 ? fminf(acc, v) : kind == 4 ? acc * v : acc + v;
     }
     o[i] = kind == 1 ? acc / (float)R : acc;
   }
 }
 
-template <int KIND> void k_reduce(const OpRun& r) {  // 0 sum 1 mean 2 max 3 min
+template <int KIND> void k_reduce(const OpRun& r) {  // 0 sum 1 mean 2 max 3 min 4 prod
   Tensor x = r.in("X");
   const int64_t R = (int64_t)x.dims.size();
   std::vector<bool> red((size_t)R, r.op.GetBool("reduce_all"));
@@ -843,6 +856,7 @@ float* opt_target(const OpRun& r, const char* in_slot, const char* out_slot) {
 }
 
 void k_sgd(const OpRun& r) {
+  if (selected_rows_sgd(r)) return;
   const int64_t n = opt_n(r);
   float* p = opt_target(r, "Param", "ParamOut");
   PA_KL(pa_sgd(0, p, f32(r.in("Grad")), f32(r.in("LearningRate")), n, S(r)));
@@ -858,6 +872,7 @@ void k_momentum(const OpRun& r) {
 
 // adam_op.h: lr_t = lr sqrt(1 - beta2^t) / (1 - beta1^t), p -= lr_t m / (sqrt(v) + eps)
 void k_adam(const OpRun& r) {
+  if (selected_rows_adam(r)) return;
   const int64_t n = opt_n(r);
   float* p = opt_target(r, "Param", "ParamOut");
   float* m1 = opt_target(r, "Moment1", "Moment1Out");
@@ -990,13 +1005,33 @@ __global__ void accumulate_kernel(float* o, const float* x, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) o[i] += x[i];
 }
 
+// fill_constant_op.cc: force_cpu pins the tensor to the host (loop counters and
+// bounds the executor reads every iteration); anything else fills HBM
 void k_fill_constant(const OpRun& r) {
   const DT dt = (DT)r.op.GetInt("dtype", (int)DT::FP32);
-  if (dt != DT::FP32) throw Decline();  // integer fills (counters, ids): host
+  const double v = r.op.Has("str_value") && !r.op.GetString("str_value").empty()
+                       ? atof(r.op.GetString("str_value").c_str())
+                       : (double)r.op.GetFloat("value");
   Tensor* o = r.out("Out");
-  float* p = o->alloc<float>(r.op.GetInts("shape"), D(r));
-  hipLaunchKernelGGL(fill_kernel, dim3(grid_for(o->numel())), dim3(256), 0, S(r), p, o->numel(),
-                     r.op.GetFloat("value"));
+  if (r.op.GetBool("force_cpu", false)) {
+    o->alloc(dt, r.op.GetInts("shape"), -1);
+    const int64_t n = o->numel();
+    switch (dt) {
+      case DT::FP32: std::fill_n(o->data<float>(), n, (float)v); break;
+      case DT::FP64: std::fill_n(o->data<double>(), n, v); break;
+      case DT::INT64: std::fill_n(o->data<int64_t>(), n, (int64_t)v); break;
+      case DT::INT32: std::fill_n(o->data<int32_t>(), n, (int32_t)v); break;
+      case DT::BOOL: case DT::UINT8: std::fill_n(o->data<uint8_t>(), n, (uint8_t)v); break;
+      default: throw Decline();
+    }
+    return;
+  }
+  switch (dt) {
+    case DT::FP32: case DT::FP64: case DT::INT64: case DT::INT32: case DT::BOOL: case DT::UINT8: break;
+    default: throw Decline();
+  }
+  o->alloc(dt, r.op.GetInts("shape"), D(r));
+  device_fill(r.ctx.stream, o->raw(), dt, o->numel(), v);
 }
 
 void k_fill_zeros_like(const OpRun& r) {
@@ -1008,6 +1043,7 @@ void k_fill_zeros_like(const OpRun& r) {
 }
 
 void k_sum(const OpRun& r) {
+  if (selected_rows_sum(r)) return;
   auto xs = r.ins("X");
   std::vector<Tensor> keep;
   for (auto* t : xs) keep.push_back(*t);
@@ -1301,11 +1337,13 @@ PA_ACT(gelu, GELU);
 PA_ACT(silu, SILU);
 #undef PA_ACT
 PA_DEVICE_KERNEL(scale, k_scale);
+PA_DEVICE_KERNEL(scale_grad, k_scale_grad);
 PA_DEVICE_KERNEL(dropout, k_dropout);
 PA_DEVICE_KERNEL(reduce_sum, k_reduce<0>);
 PA_DEVICE_KERNEL(reduce_mean, k_reduce<1>);
 PA_DEVICE_KERNEL(reduce_max, k_reduce<2>);
 PA_DEVICE_KERNEL(reduce_min, k_reduce<3>);
+PA_DEVICE_KERNEL(reduce_prod, k_reduce<4>);
 PA_DEVICE_KERNEL(mean, k_mean);
 PA_DEVICE_KERNEL(mean_grad, k_mean_grad);
 PA_DEVICE_KERNEL(sgd, k_sgd);
@@ -1383,7 +1421,7 @@ void k_layer_norm_grad(const OpRun& r) {
 
 // lookup_table_grad (dense W@GRAD): zero + scatter-add of the output rows
 void k_lookup_table_grad(const OpRun& r) {
-  if (r.op.GetBool("is_sparse")) throw Decline();  // SelectedRows gradient: the Python kernel
+  if (r.op.GetBool("is_sparse")) return lookup_table_grad_sparse(r);  // SelectedRows W@GRAD
   Tensor w = r.in("W");
   Tensor ids = r.in("Ids");
   Tensor dout = r.in("Out@GRAD");
@@ -1454,6 +1492,425 @@ PA_DEVICE_KERNEL(sequence_expand_as, k_sequence_expand<true>);
 PA_DEVICE_KERNEL(sequence_expand_as_grad, k_sequence_expand_grad<true>);
 PA_DEVICE_KERNEL(sequence_concat, k_sequence_concat);
 PA_DEVICE_KERNEL(sequence_concat_grad, k_sequence_concat_grad);
+
+// =============================================================== ops that had only host kernels
+// (every one of these used to copy its inputs to the host, sync
+// twice and copy back on a HIP place)
+namespace {
+// elementwise_{mul,div}_grad over the [pre, n, post] broadcast of Y (the bias /
+// per-channel layout): dX in one pass, dY as the per-element partial reduced by
+// pa_chan_sum.  MUL: dX = g y, dY = sum g x.  DIV: dX = g / y, dY = -sum g x / y^2.
+template <bool DIV>
+__global__ void ew_muldiv_grad_kernel(const float* __restrict__ g, const float* __restrict__ x,
+                                      const float* __restrict__ y, float* __restrict__ dx,
+                                      float* __restrict__ part, int64_t total, int64_t n, int64_t post) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const float yv = y[(i / post) % n], gv = g[i];
+    if (dx) dx[i] = DIV ? gv / yv : gv * yv;
+    if (part) part[i] = DIV ? -gv * x[i] / (yv * yv) : gv * x[i];
+  }
+}
+
+template <bool DIV> void k_ew_muldiv_grad(const OpRun& r) {
+  Tensor x = r.in("X");
+  Tensor y = r.in("Y");
+  Tensor g = r.in("Out@GRAD");
+  if (x.dtype != DT::FP32 || y.dtype != DT::FP32 || g.dtype != DT::FP32 || g.numel() != x.numel()) throw Decline();
+  BcArgs b;
+  int64_t pre, n, post;
+  if (!make_bc(x.dims, y.dims, r.op.GetInt("axis", -1), &b, &pre, &n, &post)) throw Decline();
+  const int64_t total = x.numel();
+  Tensor* dxt = r.out("X@GRAD");
+  Tensor* dyt = r.out("Y@GRAD");
+  float* dx = nullptr;
+  if (dxt) {
+    dx = dxt->alloc<float>(x.dims, D(r));
+    dxt->lod = x.lod;
+  }
+  float* dy = dyt ? dyt->alloc<float>(y.dims, D(r)) : nullptr;
+  float* part = nullptr;
+  if (dy) part = (pre * post == 1) ? dy : workspace(r, "@ew_grad_part@", total);
+  if (total)
+    hipLaunchKernelGGL(ew_muldiv_grad_kernel<DIV>, dim3(grid_for(total)), dim3(256), 0, S(r), f32(g), f32(x),
+                       f32(y), dx, part, total, n, post);
+  if (dy && pre * post != 1) PA_KL(pa_chan_sum(part, dy, (int)pre, (int)n, post, 0, S(r)));
+}
+
+template <class T>
+__global__ void increment_kernel(const T* __restrict__ x, T* __restrict__ o, T step) {
+  o[0] = x[0] + step;
+}
+
+void k_increment(const OpRun& r) {
+  Tensor x = r.in("X");
+  const float step = r.op.GetFloat("step", 1.f);
+  Tensor* o = r.out("Out");
+  void* op = o->alloc(x.dtype, {1}, D(r));
+  switch (x.dtype) {
+    case DT::INT64:
+      hipLaunchKernelGGL(increment_kernel<int64_t>, dim3(1), dim3(1), 0, S(r), x.data<int64_t>(), (int64_t*)op,
+                         (int64_t)step);
+      break;
+    case DT::INT32:
+      hipLaunchKernelGGL(increment_kernel<int32_t>, dim3(1), dim3(1), 0, S(r), x.data<int32_t>(), (int32_t*)op,
+                         (int32_t)step);
+      break;
+    case DT::FP32:
+      hipLaunchKernelGGL(increment_kernel<float>, dim3(1), dim3(1), 0, S(r), x.data<float>(), (float*)op, step);
+      break;
+    default: throw Decline();
+  }
+}
+
+enum CmpOp { C_LT, C_LE, C_GT, C_GE, C_EQ, C_NE, C_AND, C_OR, C_XOR, C_NOT };
+
+template <class T>
+__global__ void compare_kernel(int op, const T* __restrict__ x, const T* __restrict__ y, uint8_t* __restrict__ o,
+                               int64_t n, int64_t ny) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const T a = x[i], b = y ? y[i % ny] : T(0);
+    bool v;
+    switch (op) {
+      case C_LT: v = a < b; break;
+      case C_LE: v = a <= b; break;
+      case C_GT: v = a > b; break;
+      case C_GE: v = a >= b; break;
+      case C_EQ: v = a == b; break;
+      case C_NE: v = a != b; break;
+      case C_AND: v = (a != T(0)) && (b != T(0)); break;
+      case C_OR: v = (a != T(0)) || (b != T(0)); break;
+      case C_XOR: v = (a != T(0)) != (b != T(0)); break;
+      default: v = a == T(0); break;
+    }
+    o[i] = v ? 1 : 0;
+  }
+}
+
+// compare_op.cc / logical_op.cc on HBM: X, Y of one dtype, Y a trailing block of X
+template <int OP> void k_compare(const OpRun& r) {
+  Tensor x = r.in("X");
+  Tensor* yp = r.in_opt("Y");
+  Tensor y = yp ? *yp : Tensor();
+  if (yp && (y.dtype != x.dtype || y.device != x.device)) throw Decline();
+  const int64_t n = x.numel(), ny = yp ? y.numel() : 1;
+  if (yp && (ny == 0 || n % ny)) throw Decline();
+  Tensor* o = r.out("Out");
+  uint8_t* op = static_cast<uint8_t*>(o->alloc(DT::BOOL, x.dims, D(r)));
+  o->lod = x.lod;
+  if (!n) return;
+  const dim3 g(grid_for(n)), bl(256);
+  switch (x.dtype) {
+    case DT::FP32:
+      hipLaunchKernelGGL(compare_kernel<float>, g, bl, 0, S(r), OP, x.data<float>(), yp ? y.data<float>() : nullptr,
+                         op, n, ny);
+      break;
+    case DT::INT64:
+      hipLaunchKernelGGL(compare_kernel<int64_t>, g, bl, 0, S(r), OP, x.data<int64_t>(),
+                         yp ? y.data<int64_t>() : nullptr, op, n, ny);
+      break;
+    case DT::INT32:
+      hipLaunchKernelGGL(compare_kernel<int32_t>, g, bl, 0, S(r), OP, x.data<int32_t>(),
+                         yp ? y.data<int32_t>() : nullptr, op, n, ny);
+      break;
+    case DT::BOOL: case DT::UINT8:
+      hipLaunchKernelGGL(compare_kernel<uint8_t>, g, bl, 0, S(r), OP, x.data<uint8_t>(),
+                         yp ? y.data<uint8_t>() : nullptr, op, n, ny);
+      break;
+    default: throw Decline();
+  }
+}
+
+void k_assign(const OpRun& r) {
+  Tensor x = r.in("X");
+  Tensor* o = r.out("Out");
+  if (o->raw() == x.raw() && o->raw()) return;  // assign onto itself
+  void* p = o->alloc(x.dtype, x.dims, D(r));
+  o->lod = x.lod;
+  copy_d2d(r, p, x.raw(), x.nbytes());
+}
+
+// cast_op.cc: any of fp32 / fp64 / int64 / int32 / bool / uint8 / bf16 / fp16 to any
+__device__ inline double cast_load(const void* p, int dt, int64_t i) {
+  switch (dt) {
+    case (int)DT::FP32: return ((const float*)p)[i];
+    case (int)DT::FP64: return ((const double*)p)[i];
+    case (int)DT::INT64: return (double)((const int64_t*)p)[i];
+    case (int)DT::INT32: return ((const int32_t*)p)[i];
+    case (int)DT::BF16: return __uint_as_float((uint32_t)((const uint16_t*)p)[i] << 16);
+    case (int)DT::FP16: return (float)((const _Float16*)p)[i];
+    default: return ((const uint8_t*)p)[i];
+  }
+}
+
+__device__ inline void cast_store(void* p, int dt, int64_t i, double v) {
+  switch (dt) {
+    case (int)DT::FP32: ((float*)p)[i] = (float)v; break;
+    case (int)DT::FP64: ((double*)p)[i] = v; break;
+    case (int)DT::INT64: ((int64_t*)p)[i] = (int64_t)v; break;
+    case (int)DT::INT32: ((int32_t*)p)[i] = (int32_t)v; break;
+    case (int)DT::BF16: {
+      const float f = (float)v;
+      const uint32_t u = __float_as_uint(f);
+      ((uint16_t*)p)[i] = (u & 0x7fffffffu) > 0x7f800000u ? (uint16_t)((u >> 16) | 0x40)
+                                                           : (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+      break;
+    }
+    case (int)DT::FP16: ((_Float16*)p)[i] = (_Float16)(float)v; break;
+    case (int)DT::BOOL: ((uint8_t*)p)[i] = v != 0.0; break;
+    default: ((uint8_t*)p)[i] = (uint8_t)v; break;
+  }
+}
+
+__global__ void cast_kernel(const void* __restrict__ x, int xdt, void* __restrict__ o, int odt, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    cast_store(o, odt, i, cast_load(x, xdt, i));
+}
+
+bool cast_dt_ok(DT t) {
+  switch (t) {
+    case DT::FP32: case DT::FP64: case DT::INT64: case DT::INT32: case DT::BOOL: case DT::UINT8: case DT::BF16:
+    case DT::FP16: return true;
+    default: return false;
+  }
+}
+
+void k_cast(const OpRun& r) {
+  Tensor x = r.in("X");
+  const DT out = (DT)r.op.GetInt("out_dtype", (int)DT::FP32);
+  if (!cast_dt_ok(x.dtype) || !cast_dt_ok(out)) throw Decline();
+  Tensor* o = r.out("Out");
+  Tensor keep = x;  // Out may alias X
+  Tensor res;
+  res.alloc(out, x.dims, D(r));
+  if (x.numel())
+    hipLaunchKernelGGL(cast_kernel, dim3(grid_for(x.numel())), dim3(256), 0, S(r), keep.raw(), (int)x.dtype,
+                       res.raw(), (int)out, x.numel());
+  res.lod = x.lod;
+  *o = res;
+}
+
+// uniform_random / gaussian_random: counter-based (splitmix64 of seed ^ index), the
+// seed is the op's `seed` attr or one draw of the executor's generator per run
+__device__ inline uint64_t mix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__device__ inline float u01(uint64_t s, int64_t i) {
+  return ((mix64(s ^ (uint64_t)i * 0xd1342543de82ef95ull) >> 40) + 0.5f) * (1.f / 16777216.f);
+}
+
+template <bool GAUSS>
+__global__ void random_kernel(float* __restrict__ o, int64_t n, uint64_t seed, float a, float b) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (GAUSS) {
+      const float u1 = u01(seed, 2 * i), u2 = u01(seed, 2 * i + 1);
+      o[i] = a + b * sqrtf(-2.f * logf(u1)) * cosf(6.283185307f * u2);
+    } else {
+      o[i] = a + (b - a) * u01(seed, i);
+    }
+  }
+}
+
+template <bool GAUSS> void k_random(const OpRun& r) {
+  const DT dt = (DT)r.op.GetInt("dtype", (int)DT::FP32);
+  if (dt != DT::FP32) throw Decline();
+  Tensor* o = r.out("Out");
+  float* p = o->alloc<float>(r.op.GetInts("shape"), D(r));
+  const int64_t s = r.op.GetInt("seed");
+  const uint64_t seed = s ? (uint64_t)s : r.ctx.rng();
+  const float a = GAUSS ? r.op.GetFloat("mean", 0.f) : r.op.GetFloat("min", -1.f);
+  const float b = GAUSS ? r.op.GetFloat("std", 1.f) : r.op.GetFloat("max", 1.f);
+  if (o->numel())
+    hipLaunchKernelGGL(random_kernel<GAUSS>, dim3(grid_for(o->numel())), dim3(256), 0, S(r), p, o->numel(), seed, a,
+                       b);
+}
+// arg_max_op.cc over [pre, n, post] (axis attr): int64 index of the first maximum
+__global__ void arg_max_kernel(const float* __restrict__ x, int64_t* __restrict__ o, int64_t pre, int64_t n,
+                               int64_t post) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < pre * post; i += (int64_t)gridDim.x * blockDim.x) {
+    const float* p = x + (i / post) * n * post + i % post;
+    float best = p[0];
+    int64_t bi = 0;
+    for (int64_t k = 1; k < n; ++k)
+      if (p[k * post] > best) {
+        best = p[k * post];
+        bi = k;
+      }
+    o[i] = bi;
+  }
+}
+
+void k_arg_max(const OpRun& r) {
+  Tensor x = r.in("X");
+  if (x.dtype != DT::FP32 || x.dims.empty()) throw Decline();
+  int64_t axis = r.op.GetInt("axis", -1);
+  if (axis < 0) axis += (int64_t)x.dims.size();
+  const int64_t pre = prod(x.dims, 0, (size_t)axis), n = x.dims[(size_t)axis], post = prod(x.dims, (size_t)axis + 1);
+  Dims od;
+  for (size_t i = 0; i < x.dims.size(); ++i)
+    if ((int64_t)i != axis) od.push_back(x.dims[i]);
+  if (od.empty()) od.push_back(1);
+  Tensor* o = r.out("Out");
+  int64_t* op = static_cast<int64_t*>(o->alloc(DT::INT64, od, D(r)));
+  if (pre * post && n)
+    hipLaunchKernelGGL(arg_max_kernel, dim3(grid_for(pre * post)), dim3(256), 0, S(r), f32(x), op, pre, n, post);
+}
+
+// shape_op.cc: the dims of Input as an int32 tensor on the executor's place
+void k_shape(const OpRun& r) {
+  const Dims d = r.in("Input").dims;
+  std::vector<int32_t> h(d.begin(), d.end());
+  Tensor* o = r.out("Out");
+  void* p = o->alloc(DT::INT32, {(int64_t)h.size()}, D(r));
+  copy_d2d(r, p, upload_host(r, "@shape@", h.data(), h.size() * 4), h.size() * 4);
+}
+}  // namespace
+
+PA_DEVICE_KERNEL(arg_max, k_arg_max);
+PA_DEVICE_KERNEL(shape, k_shape);
+PA_DEVICE_KERNEL(elementwise_mul_grad, k_ew_muldiv_grad<false>);
+PA_DEVICE_KERNEL(elementwise_div_grad, k_ew_muldiv_grad<true>);
+PA_DEVICE_KERNEL(increment, k_increment);
+PA_DEVICE_KERNEL(less_than, k_compare<C_LT>);
+PA_DEVICE_KERNEL(less_equal, k_compare<C_LE>);
+PA_DEVICE_KERNEL(greater_than, k_compare<C_GT>);
+PA_DEVICE_KERNEL(greater_equal, k_compare<C_GE>);
+PA_DEVICE_KERNEL(equal, k_compare<C_EQ>);
+PA_DEVICE_KERNEL(not_equal, k_compare<C_NE>);
+PA_DEVICE_KERNEL(logical_and, k_compare<C_AND>);
+PA_DEVICE_KERNEL(logical_or, k_compare<C_OR>);
+PA_DEVICE_KERNEL(logical_xor, k_compare<C_XOR>);
+PA_DEVICE_KERNEL(logical_not, k_compare<C_NOT>);
+PA_DEVICE_KERNEL(assign, k_assign);
+PA_DEVICE_KERNEL(cast, k_cast);
+PA_DEVICE_KERNEL(uniform_random, k_random<false>);
+PA_DEVICE_KERNEL(gaussian_random, k_random<true>);
+
+// =============================================================== row movement for ops_control.cc
+namespace {
+__global__ void gather_words_kernel(const uint32_t* __restrict__ src, const int64_t* __restrict__ rows,
+                                    uint32_t* __restrict__ dst, int64_t n, int64_t w) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * w; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = src[rows[i / w] * w + i % w];
+}
+__global__ void gather_bytes_kernel(const uint8_t* __restrict__ src, const int64_t* __restrict__ rows,
+                                    uint8_t* __restrict__ dst, int64_t n, int64_t w) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * w; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = src[rows[i / w] * w + i % w];
+}
+__global__ void scatter_words_kernel(const uint32_t* __restrict__ src, const int64_t* __restrict__ rows,
+                                     uint32_t* __restrict__ dst, int64_t n, int64_t w) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * w; i += (int64_t)gridDim.x * blockDim.x)
+    dst[rows[i / w] * w + i % w] = src[i];
+}
+__global__ void scatter_add_f32_kernel(const float* __restrict__ src, const int64_t* __restrict__ rows,
+                                       float* __restrict__ dst, int64_t n, int64_t w) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * w; i += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(dst + rows[i / w] * w + i % w, src[i]);
+}
+template <class T>
+__global__ void fill_typed_kernel(T* o, int64_t n, T v) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) o[i] = v;
+}
+}  // namespace
+
+void device_gather_rows(const OpRun& r, const void* src, int64_t row_bytes, const std::vector<int64_t>& rows,
+                        void* dst) {
+  const int64_t n = (int64_t)rows.size();
+  if (n == 0 || row_bytes == 0) return;
+  const int64_t* d = upload_rows(r, "@cf_gather_rows@", rows);
+  if (row_bytes % 4 == 0)
+    hipLaunchKernelGGL(gather_words_kernel, dim3(grid_for(n * row_bytes / 4)), dim3(256), 0, S(r),
+                       (const uint32_t*)src, d, (uint32_t*)dst, n, row_bytes / 4);
+  else
+    hipLaunchKernelGGL(gather_bytes_kernel, dim3(grid_for(n * row_bytes)), dim3(256), 0, S(r), (const uint8_t*)src,
+                       d, (uint8_t*)dst, n, row_bytes);
+}
+
+void device_scatter_rows(const OpRun& r, const void* src, int64_t row_bytes, const std::vector<int64_t>& rows,
+                         void* dst, bool add) {
+  const int64_t n = (int64_t)rows.size();
+  if (n == 0 || row_bytes == 0) return;
+  PA_CHECK(row_bytes % 4 == 0, "device_scatter_rows: row of %lld bytes", (long long)row_bytes);
+  const int64_t* d = upload_rows(r, "@cf_scatter_rows@", rows);
+  const int64_t w = row_bytes / 4;
+  if (add)
+    hipLaunchKernelGGL(scatter_add_f32_kernel, dim3(grid_for(n * w)), dim3(256), 0, S(r), (const float*)src, d,
+                       (float*)dst, n, w);
+  else
+    hipLaunchKernelGGL(scatter_words_kernel, dim3(grid_for(n * w)), dim3(256), 0, S(r), (const uint32_t*)src, d,
+                       (uint32_t*)dst, n, w);
+}
+
+void device_copy2d(const OpRun& r, void* dst, size_t dpitch, const void* src, size_t spitch, size_t width,
+                   size_t height) {
+  if (width && height)
+    HIPCHK(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDeviceToDevice, S(r)));
+}
+
+namespace {
+__global__ void sgd_rows_kernel(float* __restrict__ p, const float* __restrict__ v, const int64_t* __restrict__ rows,
+                                const float* __restrict__ lr, int64_t n, int64_t w) {
+  const float l = lr[0];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * w; i += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(p + rows[i / w] * w + i % w, -l * v[i]);
+}
+// rows are unique: one thread per element, no atomics
+__global__ void adam_rows_kernel(float* __restrict__ p, float* __restrict__ m1, float* __restrict__ m2,
+                                 const float* __restrict__ g, const int64_t* __restrict__ rows,
+                                 const float* __restrict__ lr, const float* __restrict__ b1p,
+                                 const float* __restrict__ b2p, int64_t n, int64_t w, float b1, float b2, float eps) {
+  const float lr_t = lr[0] * sqrtf(1.f - b2p[0]) / (1.f - b1p[0]);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * w; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = rows[i / w] * w + i % w;
+    const float gv = g[i];
+    const float a = b1 * m1[e] + (1.f - b1) * gv;
+    const float b = b2 * m2[e] + (1.f - b2) * gv * gv;
+    m1[e] = a;
+    m2[e] = b;
+    p[e] -= lr_t * a / (sqrtf(b) + eps);
+  }
+}
+}  // namespace
+
+void device_sgd_rows(const OpRun& r, float* p, const float* v, const std::vector<int64_t>& rows, int64_t w,
+                     const float* lr) {
+  const int64_t n = (int64_t)rows.size();
+  if (!n || !w) return;
+  hipLaunchKernelGGL(sgd_rows_kernel, dim3(grid_for(n * w)), dim3(256), 0, S(r), p, v,
+                     upload_rows(r, "@sgd_rows@", rows), lr, n, w);
+}
+
+void device_adam_rows(const OpRun& r, float* p, float* m1, float* m2, const float* g,
+                      const std::vector<int64_t>& rows, int64_t w, const float* lr, const float* b1p,
+                      const float* b2p, float b1, float b2, float eps) {
+  const int64_t n = (int64_t)rows.size();
+  if (!n || !w) return;
+  hipLaunchKernelGGL(adam_rows_kernel, dim3(grid_for(n * w)), dim3(256), 0, S(r), p, m1, m2, g,
+                     upload_rows(r, "@adam_rows@", rows), lr, b1p, b2p, n, w, b1, b2, eps);
+}
+
+void device_add_f32(void* stream, float* acc, const float* x, int64_t n) {
+  if (n) hipLaunchKernelGGL(accumulate_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, acc, x, n);
+}
+
+void device_fill(void* stream, void* dst, DT dt, int64_t n, double v) {
+  if (n <= 0) return;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g(grid_for(n)), b(256);
+  switch (dt) {
+    case DT::FP32: hipLaunchKernelGGL(fill_typed_kernel<float>, g, b, 0, s, (float*)dst, n, (float)v); break;
+    case DT::FP64: hipLaunchKernelGGL(fill_typed_kernel<double>, g, b, 0, s, (double*)dst, n, v); break;
+    case DT::INT64: hipLaunchKernelGGL(fill_typed_kernel<int64_t>, g, b, 0, s, (int64_t*)dst, n, (int64_t)v); break;
+    case DT::INT32: hipLaunchKernelGGL(fill_typed_kernel<int32_t>, g, b, 0, s, (int32_t*)dst, n, (int32_t)v); break;
+    case DT::BOOL: case DT::UINT8: case DT::INT8:
+      hipLaunchKernelGGL(fill_typed_kernel<uint8_t>, g, b, 0, s, (uint8_t*)dst, n, (uint8_t)v);
+      break;
+    default: fail("device_fill: dtype %s", dt_name(dt));
+  }
+}
 
 void link_device_kernels() {}
 

@@ -459,7 +459,22 @@ void k_scale(const OpRun& r) {
   unary([s, bias, after](float v, const OpDesc&) { return after ? v * s + bias : (v + bias) * s; })(r);
 }
 
+void k_scale_grad(const OpRun& r) {  // dX = scale * dOut (bias drops out)
+  Tensor& g = r.in("Out@GRAD");
+  Tensor gs = g;
+  Tensor* dx = r.out("X@GRAD");
+  if (!dx) return;
+  const float s = r.op.GetFloat("scale", 1.f);
+  const LoD lod = gs.lod;
+  const Dims d = gs.dims;
+  float* o = dx->alloc<float>(d, -1);
+  const float* gp = f32(gs);
+  for (int64_t i = 0; i < gs.numel(); ++i) o[i] = s * gp[i];
+  dx->lod = lod;
+}
+
 void k_sum(const OpRun& r) {
+  if (selected_rows_sum(r)) return;
   auto xs = r.ins("X");
   PA_CHECK(!xs.empty(), "sum: no inputs");
   std::vector<Tensor> keep;
@@ -920,7 +935,8 @@ void k_lookup_table(const OpRun& r) {
   o->lod = lod;
 }
 
-void k_lookup_table_grad(const OpRun& r) {  // dense W@GRAD
+void k_lookup_table_grad(const OpRun& r) {  // dense W@GRAD, or SelectedRows when is_sparse
+  if (r.op.GetBool("is_sparse")) return lookup_table_grad_sparse(r);
   Tensor& w = r.in("W");
   Tensor& ids = r.in("Ids");
   Tensor& g = r.in("Out@GRAD");
@@ -1301,6 +1317,7 @@ float* opt_target(const OpRun& r, const char* in_slot, const char* out_slot) {
 }
 
 void k_sgd(const OpRun& r) {
+  if (selected_rows_sgd(r)) return;
   Tensor& p = r.in("Param");
   Tensor& g = r.in("Grad");
   const float lr = f32(r.in("LearningRate"))[0];
@@ -1333,6 +1350,7 @@ void k_momentum(const OpRun& r) {
 }
 
 void k_adam(const OpRun& r) {
+  if (selected_rows_adam(r)) return;
   Tensor& p = r.in("Param");
   Tensor& g = r.in("Grad");
   const float lr = f32(r.in("LearningRate"))[0];
@@ -1800,6 +1818,7 @@ PA_HOST_KERNEL(hard_sigmoid, unary([](float v, const OpDesc& o) {
 PA_HOST_KERNEL(swish, unary([](float v, const OpDesc& o) { return v * sigm(o.GetFloat("beta", 1.f) * v); }));
 PA_HOST_KERNEL(pow, unary([](float v, const OpDesc& o) { return powf(v, o.GetFloat("factor", 1.f)); }));
 PA_HOST_KERNEL(scale, k_scale);
+PA_HOST_KERNEL(scale_grad, k_scale_grad);
 PA_HOST_KERNEL(relu_grad, unary_grad([](float, float y, float g, const OpDesc&) { return y > 0 ? g : 0.f; }));
 PA_HOST_KERNEL(sigmoid_grad, unary_grad([](float, float y, float g, const OpDesc&) { return g * y * (1.f - y); }));
 PA_HOST_KERNEL(tanh_grad, unary_grad([](float, float y, float g, const OpDesc&) { return g * (1.f - y * y); }));

@@ -419,7 +419,9 @@ class DynamicRNN:
         self.lod_rank_table = None
         self.max_seq_len = None
         self.step_idx = None
-        self.zero_idx = fill_constant(shape=[1], value=0, dtype="int64")
+        # loop indices live on the host (force_cpu, as in the reference): the loop
+        # condition and the array slots are read there every step
+        self.zero_idx = fill_constant(shape=[1], value=0, dtype="int64", force_cpu=True)
         self.zero_idx.stop_gradient = True
         self.mem_dict = {}
         self.output_array = []
@@ -482,7 +484,7 @@ class DynamicRNN:
     def block(self):
         if self.status != DynamicRNN.BEFORE_RNN:
             raise ValueError("rnn.block() can only be invoke once")
-        self.step_idx = fill_constant(shape=[1], dtype="int64", value=0)
+        self.step_idx = fill_constant(shape=[1], dtype="int64", value=0, force_cpu=True)
         self.step_idx.stop_gradient = False
         self.status = DynamicRNN.IN_RNN
         with self.while_op.block():

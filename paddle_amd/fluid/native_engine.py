@@ -50,8 +50,8 @@ _TORCH_DT = {torch.float32: 5, torch.int64: 3, torch.int32: 2, torch.float64: 6,
              torch.float16: 4, torch.int16: 1, torch.int8: 21, torch.bfloat16: 22}
 _DT_TORCH = {v: k for k, v in _TORCH_DT.items()}
 # control-flow ops the C++ executor runs itself, and the ones it cannot take
-_NATIVE_CF = {"while", "conditional_block"}
-_UNSUPPORTED_CF = {"while_grad", "conditional_block_grad", "recurrent", "recurrent_grad", "parallel_do",
+_NATIVE_CF = {"while", "while_grad", "conditional_block"}
+_UNSUPPORTED_CF = {"conditional_block_grad", "recurrent", "recurrent_grad", "parallel_do",
                    "parallel_do_grad", "go", "select"}
 
 
@@ -161,6 +161,7 @@ class NativeEngine:
         self._bexe = None
         self._wrapped = []
         self._keep = {}
+        self._feed_keep = {}
         self.py_fallbacks = {}  # op type -> calls run by the Python op library
         self.py_fallback_types = set()
 
@@ -173,7 +174,8 @@ class NativeEngine:
         needing per-step scopes, every variable a dense LoDTensor (or the feed / fetch
         holders), the pybind binding available when some op has no C++ kernel."""
         VT = core.VT
-        ok_types = {VT.LOD_TENSOR, VT.FEED_MINIBATCH, VT.FETCH_LIST}
+        ok_types = {VT.LOD_TENSOR, VT.FEED_MINIBATCH, VT.FETCH_LIST, VT.LOD_TENSOR_ARRAY, VT.LOD_RANK_TABLE,
+                    VT.STEP_SCOPES, VT.SELECTED_ROWS}
         try:
             native.lib()
         except Exception:
@@ -183,9 +185,9 @@ class NativeEngine:
             if op.type in _UNSUPPORTED_CF or (any(k in op.attrs for k in ("sub_block", "blocks"))
                                               and op.type not in _NATIVE_CF):
                 return False
-            # SelectedRows at run time (sparse embedding grads) and the RPC ops that
-            # exchange them stay on the interpreter
-            if op.attrs.get("is_sparse") or op.attrs.get("is_distributed") or op.type in _RPC_OPS:
+            # distributed lookup tables and the RPC ops that exchange their SelectedRows
+            # stay on the interpreter (local sparse gradients run natively)
+            if op.attrs.get("is_distributed") or op.type in _RPC_OPS:
                 return False
         for b in program.blocks:
             for v in b.vars.values():
@@ -263,13 +265,24 @@ class NativeEngine:
             bound[name] = sig + (t,)
 
     def _feed(self, ns, name, data):
+        """Lends the feed's storage to the native scope: a tensor already on the
+        executor's place (a device tensor on a HIP place) is shared as is, anything
+        else is moved there once -- no numpy round trip for device tensors."""
         lod = None
         if isinstance(data, core.LoDTensor):
             lod = data.lod()
             data = data._t
-        if isinstance(data, torch.Tensor):
-            data = data.detach().cpu().numpy()
-        self._b.set(ns, name, np.ascontiguousarray(np.asarray(data)), self.device)
+        if not isinstance(data, torch.Tensor):
+            data = torch.from_numpy(np.ascontiguousarray(np.asarray(data)))
+        t = data.detach()
+        if t.dtype not in _TORCH_DT:
+            raise NotImplementedError(f"native engine: feed {name} has dtype {t.dtype}")
+        t = t.to(self._tdev()).contiguous()
+        if t.device.type == "cuda" and data.device.type != "cuda":
+            # the host-to-device copy is on torch's stream, the native kernels on ours
+            torch.cuda.current_stream(self._tdev()).synchronize()
+        self._feed_keep[name] = t  # alive while the native scope references it
+        self._b.share(ns, name, t.data_ptr(), _TORCH_DT[t.dtype], tuple(t.shape), self.device)
         if lod:
             if not self._b.supports_fallback:
                 raise NotImplementedError(f"native engine: LoD feed {name} needs the pybind binding")

@@ -23,6 +23,8 @@ def test_book_program_native_matches_python_gpu(case):
         for a, b in zip(r, g):
             np.testing.assert_allclose(b, a, rtol=2e-4, atol=2e-5)
     assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+    # every op ran on a device kernel: no host copy-in / copy-out round trips
+    assert not exe._native.host_fallbacks(), exe._native.host_fallbacks()
 
 
 def _tiny_transformer():
@@ -61,3 +63,4 @@ def test_transformer_ops_native_matches_python_gpu():
     fb = exe._native.py_fallbacks
     for op in ("layer_norm", "layer_norm_grad", "lookup_table_grad", "top_k", "accuracy"):
         assert op not in fb, fb
+    assert not exe._native.host_fallbacks(), exe._native.host_fallbacks()
