@@ -152,7 +152,7 @@ class Tape:
             tg = getattr(o, "_pa_tape", None)
             if tg is None or tg[0] != id(self):
                 continue  # not produced on this tape (e.g. an integer passthrough)
-            g = torch.ones_like(o) if g is None else g
+            g = _ones_like(o) if g is None else g
             seeds[tg[1]] = g if tg[1] not in seeds else _add(seeds[tg[1]], g)
         if _strict.counting():
             with _strict.region("tape:backward", native=False):
@@ -163,7 +163,7 @@ class Tape:
         tg = getattr(loss, "_pa_tape", None)
         if tg is None or tg[0] != id(self):
             raise RuntimeError("tape.backward: the loss was not produced on this tape")
-        return self._run({tg[1]: torch.ones_like(loss) if grad is None else grad})
+        return self._run({tg[1]: _ones_like(loss) if grad is None else grad})
 
     def _run(self, grads):
         run_before_backward()  # e.g. an optimizer update still running on a side stream
@@ -207,6 +207,15 @@ class Tape:
         if n == 0:
             for hook in getattr(p, "_pa_grad_ready_hooks", ()):
                 hook(p)
+
+
+def _ones_like(t):
+    """The reverse pass's seed on the native fill kernel."""
+    if t.is_cuda:
+        from ..ops import oplib
+
+        return oplib.full_like(t, 1.0)
+    return torch.ones_like(t)
 
 
 def _add(a, b):

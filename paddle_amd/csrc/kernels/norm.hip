@@ -9,6 +9,8 @@
 // dgamma/dbeta are accumulated in registers across the rows a wave owns,
 // folded across the block's waves with LDS float atomics and written as one
 // fp32 partial row per block; a second tiny kernel sums the partials.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace pa {
@@ -252,11 +254,32 @@ static int launch_fwd(bool rms, const void* x, const void* res, const void* w, c
   PA_LAUNCH_CHECK();
 }
 
+// backward variant knobs for A/B runs (benchmarks/norm_bwd_ab.py): PA_NORM_BWD_G =
+// block count cap, PA_NORM_BWD_WPR2 = 1 splits rows of up to 4096 over two waves too
+static int env_int(const char* k, int def) {
+  const char* v = getenv(k);
+  return v && *v ? atoi(v) : def;
+}
+
+template <typename T, int MAXV, int WPR>
+static void launch_bwd_k(bool rms, const T* DY, const T* Hh, const T* W, const float* mean, const float* rstd,
+                         const T* DR, T* DX, float* dwp, float* dbp, long N, int H, long rpb, int G, size_t shm,
+                         hipStream_t st) {
+#define PA_NB(RMS_, DRES_) \
+  hipLaunchKernelGGL((norm_bwd_kernel<T, MAXV, RMS_, DRES_, WPR>), dim3(G), dim3(256), shm, st, DY, Hh, W, mean, rstd, DR, DX, dwp, dbp, N, H, rpb)
+  if (rms) { if (DR) PA_NB(true, true); else PA_NB(true, false); }
+  else { if (DR) PA_NB(false, true); else PA_NB(false, false); }
+#undef PA_NB
+}
+
 template <typename T, int MAXV>
 static int launch_bwd(bool rms, const void* dy, const void* h, const void* w, const float* mean,
                       const float* rstd, const void* dres, void* dx, void* dw, void* db,
                       float* ws, long N, int H, hipStream_t st) {
-  long G0 = (N + 3) / 4; int G = (int)(G0 < 512 ? G0 : 512);  // measured best of 256 / 512 / 1024 (benchmarks/norm_bench.py)
+  // (capped at 512: callers size the workspace for 512 partial rows)
+  static const int gcap = env_int("PA_NORM_BWD_G", 512) < 512 ? env_int("PA_NORM_BWD_G", 512) : 512;
+  static const int wpr2 = env_int("PA_NORM_BWD_WPR2", 0);
+  long G0 = (N + 3) / 4; int G = (int)(G0 < gcap ? G0 : gcap);  // measured best of 256 / 512 / 1024 (benchmarks/norm_bench.py)
   if (G < 1) G = 1;
   long rpb = (N + G - 1) / G;
   G = (int)((N + rpb - 1) / rpb);
@@ -273,11 +296,10 @@ static int launch_bwd(bool rms, const void* dy, const void* h, const void* w, co
   constexpr int MV = MAXV > 8 ? MAXV / 2 : MAXV;
   const T *DY = (const T*)dy, *Hh = (const T*)h, *W = (const T*)w, *DR = (const T*)dres;
   T* DX = (T*)dx;
-#define PA_NB(RMS_, DRES_) \
-  hipLaunchKernelGGL((norm_bwd_kernel<T, MV, RMS_, DRES_, WPR>), dim3(G), dim3(256), shm, st, DY, Hh, W, mean, rstd, DR, DX, dwp, dbp, N, H, rpb)
-  if (rms) { if (dres) PA_NB(true, true); else PA_NB(true, false); }
-  else { if (dres) PA_NB(false, true); else PA_NB(false, false); }
-#undef PA_NB
+  if (MAXV == 8 && wpr2)
+    launch_bwd_k<T, 4, 2>(rms, DY, Hh, W, mean, rstd, DR, DX, dwp, dbp, N, H, rpb, G, shm, st);
+  else
+    launch_bwd_k<T, MV, WPR>(rms, DY, Hh, W, mean, rstd, DR, DX, dwp, dbp, N, H, rpb, G, shm, st);
   hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 63) / 64), dim3(256), 0, st, dwp, (T*)dw, G, H);
   if (!rms && db) hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 63) / 64), dim3(256), 0, st, dbp, (T*)db, G, H);
   PA_LAUNCH_CHECK();

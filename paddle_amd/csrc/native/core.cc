@@ -741,12 +741,14 @@ void Executor::RunWhileGrad(const ProgramDesc& prog, const OpDesc& op, Scope* sc
   };
   for (auto& n : xs) note_array(n);
   for (auto& n : op.Inputs("Out")) note_array(n);
+  // incoming output gradients live in the enclosing scope: never shadowed per step
+  const std::set<std::string> out_grads(op.Inputs("Out@GRAD").begin(), op.Inputs("Out@GRAD").end());
   std::map<std::string, Tensor> acc;
   for (size_t k = sv->steps.size(); k-- > 0;) {
     Scope* s = sv->steps[k];
     Scope& gs = s->NewScope();
     for (const VarDesc& v : blk.vars)
-      if (!v.persistable && !shared.count(v.name)) gs.Var(v.name)->kind = v.type;
+      if (!v.persistable && !shared.count(v.name) && !out_grads.count(v.name)) gs.Var(v.name)->kind = v.type;
     for (size_t i = 0; i < xs.size() && i < xgs.size(); ++i)
       if (xgs[i] != "@EMPTY@" && !arrays.count(xs[i]) && !gs.FindLocal(xgs[i])) gs.Var(xgs[i]);
     RunBlock(prog, blk, &gs);
@@ -794,13 +796,74 @@ void Executor::RunConditionalBlock(const ProgramDesc& prog, const OpDesc& op, Sc
       if (!v || !v->tensor.initialized() || v->tensor.numel() == 0) run = false;
     }
   }
+  // training programs keep the block's scope in the Scope output for
+  // conditional_block_grad (empty when the block did not run)
+  const std::string sn = op.Output("Scope");
+  Variable* kept = (!sn.empty() && !ctx_.is_test) ? scope->Find(sn) : nullptr;
+  if (!sn.empty() && !ctx_.is_test && !kept) kept = scope->Var(sn);
+  if (kept) {
+    kept->kind = VK_STEP_SCOPES;
+    for (Scope* s : kept->steps) kept->steps_owner->DropKid(s);
+    kept->steps.clear();
+    kept->steps_owner = scope;
+  }
   if (!run) return;
   Scope& body = scope->NewScope();
   const BlockDesc& blk = prog.Block(sb);
   for (const VarDesc& v : blk.vars)
     if (!scope->Find(v.name)) body.Var(v.name)->kind = v.type;
   RunBlock(prog, blk, &body);
-  scope->DropKid(&body);
+  if (kept) kept->steps.push_back(&body);
+  else scope->DropKid(&body);
+}
+
+// conditional_block_op.cc ConditionalBlockGradOp: when the forward ran, the grad
+// block runs in a child of the kept scope and the block-local input gradients are
+// copied to the enclosing X@GRAD (AssignLocalGradientToGlobal); else zeros
+void Executor::RunConditionalBlockGrad(const ProgramDesc& prog, const OpDesc& op, Scope* scope) {
+  const int sb = (int)op.GetInt("sub_block", -1);
+  PA_CHECK(sb >= 0 && sb < (int)prog.blocks.size(), "conditional_block_grad: bad sub_block %d", sb);
+  const BlockDesc& blk = prog.Block(sb);
+  const auto& xs = op.Inputs("X");
+  const auto& xgs = op.Outputs("X@GRAD");
+  Variable* kept = scope->Find(op.Input("Scope"));
+  std::map<std::string, Tensor> got;
+  if (kept && !kept->steps.empty()) {
+    Scope* s = kept->steps[0];
+    Scope& gs = s->NewScope();
+    // the block's locals, except the incoming output gradients (held outside)
+    const auto& ogs = op.Inputs("Out@GRAD");
+    for (const VarDesc& v : blk.vars)
+      if (!v.persistable && std::find(ogs.begin(), ogs.end(), v.name) == ogs.end()) gs.Var(v.name)->kind = v.type;
+    for (size_t i = 0; i < xs.size() && i < xgs.size(); ++i)
+      if (xgs[i] != "@EMPTY@" && !gs.FindLocal(xgs[i])) gs.Var(xgs[i]);
+    RunBlock(prog, blk, &gs);
+    for (size_t i = 0; i < xs.size() && i < xgs.size(); ++i) {
+      if (xgs[i] == "@EMPTY@") continue;
+      Variable* g = gs.FindLocal(xgs[i]);
+      if (g && g->tensor.initialized()) accumulate_into(got[xgs[i]], g->tensor, ctx_.stream);
+    }
+    s->DropKid(&gs);
+  }
+  for (size_t i = 0; i < xs.size() && i < xgs.size(); ++i) {
+    if (xgs[i] == "@EMPTY@") continue;
+    Variable* x = scope->Find(xs[i]);
+    Variable* out = scope->Find(xgs[i]);
+    if (!out) out = scope->Var(xgs[i]);
+    out->kind = VK_LOD_TENSOR;
+    auto it = got.find(xgs[i]);
+    if (it != got.end()) {
+      out->tensor = it->second;
+      if (x) out->tensor.lod = x->tensor.lod;
+    } else if (x && x->tensor.initialized() && x->tensor.dtype == DT::FP32) {
+      Tensor z;
+      z.alloc(DT::FP32, x->tensor.dims, x->tensor.device);
+      if (z.device >= 0) device_fill(ctx_.stream, z.raw(), DT::FP32, z.numel(), 0.0);
+      else std::fill_n(z.data<float>(), z.numel(), 0.f);
+      z.lod = x->tensor.lod;
+      out->tensor = z;
+    }
+  }
 }
 
 void Executor::Sync() {
@@ -905,6 +968,10 @@ void Executor::RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* 
     }
     if (op.type == "while_grad") {
       timed(op, [&] { RunWhileGrad(prog, op, scope); });
+      continue;
+    }
+    if (op.type == "conditional_block_grad") {
+      timed(op, [&] { RunConditionalBlockGrad(prog, op, scope); });
       continue;
     }
     // loop counters / bounds that live on the host (fill_constant force_cpu,

@@ -272,6 +272,7 @@ class Executor {
   void RunConditionalBlock(const ProgramDesc& prog, const OpDesc& op, Scope* scope);
   // while_op.cc WhileGradOp: the grad block once per kept step scope, last step first
   void RunWhileGrad(const ProgramDesc& prog, const OpDesc& op, Scope* scope);
+  void RunConditionalBlockGrad(const ProgramDesc& prog, const OpDesc& op, Scope* scope);
 
  private:
   bool ReadBool(const Tensor& t);

@@ -438,6 +438,12 @@ void k_sum_grad(const OpRun& r) {
   }
 }
 
+// assign's gradient: X@GRAD is a copy of Out@GRAD
+void k_assign_grad(const OpRun& r) {
+  Tensor g = r.in("Out@GRAD");
+  if (r.out_var("X@GRAD")) set_out(r, "X@GRAD", clone(r, g));
+}
+
 // concat's gradient: Out@GRAD split along `axis` into the shapes of X
 void k_concat_grad(const OpRun& r) {
   Tensor g = r.in("Out@GRAD");
@@ -666,6 +672,7 @@ PA_ANY_KERNEL(shrink_rnn_memory_grad, k_shrink_rnn_memory_grad);
 PA_ANY_KERNEL(reorder_lod_tensor_by_rank_grad, k_reorder_lod_tensor_by_rank_grad);
 PA_ANY_KERNEL(fill_constant_batch_size_like, k_fill_constant_batch_size_like);
 PA_ANY_KERNEL(sum_grad, k_sum_grad);
+PA_ANY_KERNEL(assign_grad, k_assign_grad);
 PA_ANY_KERNEL(concat_grad, k_concat_grad);
 #undef PA_ANY_KERNEL
 

@@ -1034,12 +1034,13 @@ void k_fill_constant(const OpRun& r) {
   device_fill(r.ctx.stream, o->raw(), dt, o->numel(), v);
 }
 
-void k_fill_zeros_like(const OpRun& r) {
+void k_fill_zeros_like(const OpRun& r) {  // any dtype: all-zero bytes
   Tensor& x = r.in("X");
-  if (x.dtype != DT::FP32) throw Decline();
   const Dims d = x.dims;
-  float* p = r.out("Out")->alloc<float>(d, D(r));
-  if (prod(d)) HIPCHK(hipMemsetAsync(p, 0, sizeof(float) * prod(d), S(r)));
+  const DT dt = x.dtype;
+  Tensor* o = r.out("Out");
+  void* p = o->alloc(dt, d, D(r));
+  if (o->nbytes()) HIPCHK(hipMemsetAsync(p, 0, o->nbytes(), S(r)));
 }
 
 void k_sum(const OpRun& r) {

@@ -27,6 +27,7 @@ framework/details/multi_devices_graph_pass.cc:247 GetAppropriateDeviceID,
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -192,7 +193,7 @@ class ShardedStage3:
 
     def __init__(self, model, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.0, group=None,
                  grad_clip=None, no_decay_fn=None, *, mp_group=None, pp_group=None, dp_group=None, exclude=(),
-                 norm_skip=(), bucket_mb=256, prefetch=True):
+                 norm_skip=(), bucket_mb=256, prefetch=True, dp_comm=None):
         """Composition with hybrid parallelism (fleet.distributed_model):
         ``group`` is the sharding axis; ``dp_group`` an extra data-parallel axis whose
         gradient shards are all-reduced before the step; ``mp_group`` / ``pp_group``
@@ -200,7 +201,10 @@ class ShardedStage3:
         stages summed over pp); ``exclude``: parameters kept whole (tied weights shared
         between pipeline stages; their gradients are synced by the caller) and updated
         here with their own fp32 AdamW state; ``norm_skip``: excluded parameters
-        counted on another stage."""
+        counted on another stage.  ``dp_comm="direct"`` (or FLAGS_dp_comm=direct) runs the
+        unit all-gathers / reduce-scatters on the direct intra-node collectives of
+        parallel/direct.py (IPC-mapped peer buffers, kernels on the comm stream)
+        instead of the process group."""
         self.model, self.group = model, group
         self.mp_group, self.pp_group, self.dp_group = mp_group, pp_group, dp_group
         self.dpW = comm.get_world_size(dp_group) if dp_group is not None else 1
@@ -280,12 +284,38 @@ class ShardedStage3:
         self._next_slot = 0
         self._order = []   # units in forward order (learned on the first forward)
         self._pos = {}
+        self._direct = None
+        mode = dp_comm or os.environ.get("FLAGS_dp_comm", "rccl")
+        if mode == "direct" and cuda and self.W > 1:
+            from ..parallel.direct import DirectAllReduce
+
+            need = max([u.N * 4 for u in self.units] + [4096])
+            self._direct = DirectAllReduce(group, max_bytes=need)
         for u in self.units:
             u.release()
 
     # ------------------------------------------------------------------ collectives
     def _all_gather(self, out, inp):
-        comm.all_gather(out, inp, group=self.group)
+        if self._direct is None:
+            comm.all_gather(out, inp, group=self.group)
+            return
+        # the direct collectives share one registered staging buffer: every one of
+        # them runs on the comm stream, in issue order
+        cs, cur = self.comm_stream, torch.cuda.current_stream(self.device)
+        if cur == cs:
+            self._direct.all_gather(out, inp)
+            return
+        cs.wait_stream(cur)
+        with torch.cuda.stream(cs):
+            self._direct.all_gather(out, inp)
+        cur.wait_stream(cs)
+
+    def _reduce_scatter(self, out, inp):
+        if self._direct is None:
+            comm.reduce_scatter(out, inp, group=self.group)
+        else:
+            assert torch.cuda.current_stream(self.device) == self.comm_stream
+            self._direct.reduce_scatter(out, inp)
 
     def _hook(self, u):
         def pre(mod, args, kwargs=None):
@@ -368,7 +398,7 @@ class ShardedStage3:
         if cs is not None:
             cs.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(cs):
-                comm.reduce_scatter(part, buf, group=self.group)
+                self._reduce_scatter(part, buf)
                 u.g_shard.add_(part)
                 self._gfree[u.slot] = cs.record_event()
         else:

@@ -207,6 +207,28 @@ def _while_grad_descs(op, block, no_grad_dict, grad_to_var, callbacks):
                  outputs={"X@GRAD": x_grads}, attrs={"sub_block": grad_sub, "original_output_grad": ogs})]
 
 
+def _cond_block_grad_descs(op, block, no_grad_dict, grad_to_var, callbacks):
+    """Reference conditional_block_op.cc ConditionalBlockGradMaker: the grad block is
+    a child of the forward sub-block and runs in a child of the scope the forward
+    kept (``Scope``) -- only when the forward ran."""
+    prog = block.program
+    sub = op.attrs["sub_block"]
+    saved = prog.current_block_idx
+    grad_sub = prog.create_block(parent_idx=sub.idx)
+    no_grad_dict[sub.idx] = set(no_grad_dict[sub.idx]) | set(no_grad_dict[block.idx])
+    _append_backward_ops_(sub, list(sub.ops), grad_sub, no_grad_dict, grad_to_var, callbacks)
+    prog.current_block_idx = saved
+    no_grad = no_grad_dict[block.idx]
+    xs, outs = list(op.input("X")), list(op.output("Out"))
+    x_grads = [_append_grad_suffix_(n) if _differentiable(block, n, no_grad) else R.EMPTY_VAR for n in xs]
+    ogs = [_append_grad_suffix_(n) for n in outs if _differentiable(block, n, no_grad)]
+    return [dict(type="conditional_block_grad",
+                 inputs={"X": xs, "Cond": list(op.input("Cond")), "Out": outs, "Out@GRAD": ogs,
+                         "Scope": list(op.output("Scope"))},
+                 outputs={"X@GRAD": x_grads},
+                 attrs={"sub_block": grad_sub, "is_scalar_condition": op.attrs.get("is_scalar_condition", False)})]
+
+
 def _split_duplicate_outputs(descs):
     """A grad op that writes the same gradient from two slots (``x * x`` ->
     X@GRAD and Y@GRAD are both x@GRAD) gets the later occurrences renamed and a
@@ -254,6 +276,8 @@ def _append_backward_ops_(block, ops, target_block, no_grad_dict, grad_to_var, c
     for op in reversed(ops):
         if op.type == "while":
             descs = _while_grad_descs(op, block, no_grad_dict, grad_to_var, callbacks)
+        elif op.type == "conditional_block":
+            descs = _cond_block_grad_descs(op, block, no_grad_dict, grad_to_var, callbacks)
         else:
             descs = R.make_grad_op_descs(_OpView(op), no_grad)
         for d in _split_duplicate_outputs(descs):

@@ -50,8 +50,8 @@ _TORCH_DT = {torch.float32: 5, torch.int64: 3, torch.int32: 2, torch.float64: 6,
              torch.float16: 4, torch.int16: 1, torch.int8: 21, torch.bfloat16: 22}
 _DT_TORCH = {v: k for k, v in _TORCH_DT.items()}
 # control-flow ops the C++ executor runs itself, and the ones it cannot take
-_NATIVE_CF = {"while", "while_grad", "conditional_block"}
-_UNSUPPORTED_CF = {"conditional_block_grad", "recurrent", "recurrent_grad", "parallel_do",
+_NATIVE_CF = {"while", "while_grad", "conditional_block", "conditional_block_grad"}
+_UNSUPPORTED_CF = {"recurrent", "recurrent_grad", "parallel_do",
                    "parallel_do_grad", "go", "select"}
 
 

@@ -144,6 +144,8 @@ def conditional_block(ctx):
     else:
         run = all((c.tensor.numel() > 0) for c in conds if isinstance(c, core.LoDTensor))
     if not run:
+        if ctx.has_output("Scope"):
+            ctx.set_output("Scope", [])  # no kept scope: the grad op knows the block did not run
         return
     s = scope.new_scope()
     exe.run_block(blk.program, blk.idx, s)

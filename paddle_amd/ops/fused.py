@@ -26,6 +26,12 @@ def _ws(n: int, device, dtype=torch.float32):
     return torch.empty(n, dtype=dtype, device=device)
 
 
+
+def _oplib_fill(t, v):
+    from . import oplib
+
+    return oplib.fill_(t, v)
+
 def _c(t):
     return t if t.is_contiguous() else t.contiguous()
 
@@ -1130,7 +1136,7 @@ class _EmbeddingFn(torch.autograd.Function):
             # scatter-add straight into the fp32 main_grad (zeroed first on the first
             # write after zero_grad), like the fused linear's dW epilogue
             if getattr(w, "_pa_grad_fresh", False):
-                mg.zero_()
+                _oplib_fill(mg, 0.0)
                 w._pa_grad_fresh = False
             N.call("pa_embedding_bwd", N.dt(d), N.ptr(ids_), N.ptr(d), N.ptr(mg), ids_.numel(), H, int(ctx.pad),
                    N.stream())

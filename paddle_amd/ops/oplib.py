@@ -39,6 +39,22 @@ def _larr(vals):
 # ------------------------------------------------------------------ binary
 
 
+def fill_(t, value):
+    """t[...] = value on the elementwise kernel of tensor_ops.hip (any device dtype
+    and layout the kernel covers; else torch's fill)."""
+    if t.is_cuda and t.numel():
+        from . import aten_native as A
+
+        if t.dtype in A._DT and A._launch(A.U["fill"], t, [], a=float(value), cdt=A._cdt(t.dtype)):
+            return t
+    return t.fill_(value)
+
+
+def full_like(t, value):
+    """A new tensor shaped like ``t`` filled with ``value`` (native fill)."""
+    return fill_(torch.empty_like(t, memory_format=torch.contiguous_format), value)
+
+
 def binary(op, x, y):
     """out = x (op) y with y already broadcast-compatible (expandable) to x's shape."""
     if not _ok(x, y) or x.dtype != y.dtype or op not in _BIN or x.dim() > 6:

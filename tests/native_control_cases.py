@@ -196,3 +196,33 @@ def device_ops_feeds(steps=2):
 
 
 CASES_DEVICE_OPS = {"device_ops": (device_ops, device_ops_feeds)}
+
+
+def cond_block(flag):
+    """conditional_block training: fc inside the block, loss outside; the grads
+    flow through conditional_block_grad (zeros when the block did not run)."""
+    def build():
+        L = fluid.layers
+        x = L.data(name="x", shape=[4], dtype="float32")
+        x.stop_gradient = False
+        out = L.fill_constant_batch_size_like(x, [-1, 3], "float32", 0.0)
+        out.stop_gradient = False
+        cond = L.fill_constant([1], "bool", flag, force_cpu=True)
+        cb = L.ConditionalBlock([cond], is_scalar_condition=True)
+        with cb.block():
+            h = L.fc(x, size=3, act="tanh", param_attr=fluid.ParamAttr(name="cw"),
+                     bias_attr=fluid.ParamAttr(name="cb"))
+            L.assign(h, out)
+        loss = L.mean(L.elementwise_mul(out, out))
+        pg = fluid.backward.append_backward(loss)
+        return [loss, "x@GRAD"] + [g for _, g in pg]
+    return build
+
+
+def cond_block_feeds(steps=2):
+    rs = np.random.RandomState(5)
+    return [{"x": rs.randn(6, 4).astype("float32")} for _ in range(steps)]
+
+
+CASES["cond_block_true"] = (cond_block(True), cond_block_feeds)
+CASES["cond_block_false"] = (cond_block(False), cond_block_feeds)

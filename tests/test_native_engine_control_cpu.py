@@ -67,3 +67,32 @@ def test_every_host_kernel_has_a_device_kernel():
     agnostic = {"feed", "fetch", "reshape", "reshape2", "flatten", "flatten2", "squeeze", "squeeze2", "unsqueeze",
                 "unsqueeze2", "delete_var", "reshape_grad", "reshape2_grad"}
     assert host - dev - agnostic == set()
+
+
+def test_conditional_block_grad_matches_unconditional_program():
+    """With the condition true the block's gradients equal those of the same layers
+    outside any block; with it false every input gradient is zero."""
+    import torch
+
+    def plain():
+        L = fluid.layers
+        x = L.data(name="x", shape=[4], dtype="float32")
+        x.stop_gradient = False
+        h = L.fc(x, size=3, act="tanh", param_attr=fluid.ParamAttr(name="cw"), bias_attr=fluid.ParamAttr(name="cb"))
+        loss = L.mean(L.elementwise_mul(h, h))
+        pg = fluid.backward.append_backward(loss)
+        return [loss, "x@GRAD"] + [g for _, g in pg]
+
+    from native_control_cases import cond_block_feeds
+
+    fd = cond_block_feeds()
+    place = fluid.CPUPlace()
+    on, init, _ = run(CASES["cond_block_true"][0], fd, "python", place)
+    ref, _, _ = run(plain, fd, "python", place, init={k: v for k, v in init.items() if k in ("cw", "cb")})
+    for a, b in zip(on[0], ref[0]):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
+    off, _, _ = run(CASES["cond_block_false"][0], fd, "python", place, init=init)
+    assert float(np.asarray(off[0][0]).reshape(-1)[0]) == 0.0
+    for g in off[0][1:]:
+        assert not np.any(np.asarray(g)), g
+    del torch

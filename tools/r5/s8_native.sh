@@ -3,4 +3,5 @@ cd $GRAFT_REPO_ROOT
 export PYTHONUNBUFFERED=1
 S=tools/gpu_session.sh
 bash $S "step native_gpu 600 python -u -m pytest tests/test_native_engine_control_gpu.py tests/test_native_engine_book_gpu.py tests/test_native_engine_gpu.py tests/test_native_gpu.py tests/test_no_torch_autograd_gpu.py -v --timeout 300 --timeout-method thread -p no:cacheprovider" \
+ "step zero3_trace 300 env PA_TRACE_OUT=gpurun_out/zero3_overlap_trace.json python -u -m pytest tests/test_zero3_overlap_trace_gpu.py -v --timeout 280 --timeout-method thread -p no:cacheprovider" \
  "step strict_models 400 python -u tools/r5/strict_models.py"
