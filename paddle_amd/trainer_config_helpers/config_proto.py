@@ -378,6 +378,8 @@ class Recorder:
         self.inputs = []
         self.outputs = []
         self.depth = 0
+        self.by_name = {}     # layer name -> its LayerConfig (image dims of inputs)
+        self.parents = {}     # layer name -> parent layer names (networks.outputs DFS)
 
     def name_for(self, fn, given):
         if given:
@@ -507,7 +509,15 @@ def recorded(fn_name, fn):
                                "initial_strategy": 0, "initial_smart": False})
         if fn_name == "data_layer":
             rec.inputs.append(name)
+        # LayerOutput.parents of the reference helpers: the layer inputs, except for
+        # layers whose index / range inputs are not graph parents
+        pnames = [rec.layer_name(x) for x, _ in ins if rec.layer_name(x)]
+        rec.parents[name] = pnames[:1] if fn_name in _FIRST_PARENT_ONLY else pnames
+        extra = _EXTRA.get(fn_name)
+        if extra is not None:
+            extra(lc, args, kw, ins, rec, name)
         rec.layers.append(lc)
+        rec.by_name[name] = lc
         rec.of_var[id(v)] = name
         rec.vars.append(v)
         return out
@@ -518,6 +528,184 @@ def recorded(fn_name, fn):
     return wrapper
 
 
+# ---------------------------------------------------------------- per-type fields
+# The LayerConfig fields beyond name / type / size / activation / inputs that the
+# reference parser sets for a layer type (its Layer classes in
+# trainer/config_parser.py), derived here from the DSL call's arguments.
+def _arg(fn_args, kw, name, pos, default=None):
+    if name in kw:
+        return kw[name]
+    return fn_args[pos] if len(fn_args) > pos else default
+
+
+def _level(v, default="non-seq"):
+    return v if isinstance(v, str) else default
+
+
+def _in_lc(rec, ins, i=0):
+    if len(ins) <= i:
+        return {}
+    return rec.by_name.get(rec.layer_name(ins[i][0]) or "", {})
+
+
+def _hwd_from(lc, src):
+    """set_layer_height_width + set_layer_depth from an input layer (unset: 0, 0, 1)."""
+    lc["height"] = int(src.get("height", 0))
+    lc["width"] = int(src.get("width", 0))
+    lc["depth"] = int(src.get("depth", 1))
+
+
+def _x_data(lc, a, kw, ins, rec, name):
+    h, w, d = kw.get("height"), kw.get("width"), kw.get("depth")
+    if h and w:
+        lc["height"], lc["width"] = int(h), int(w)
+    if d:
+        lc["depth"] = int(d)
+
+
+def _x_addto(lc, a, kw, ins, rec, name):
+    src = _in_lc(rec, ins)
+    for i in range(len(ins)):
+        c = _in_lc(rec, ins, i)
+        if c.get("height"):
+            src = c
+    _hwd_from(lc, src)
+
+
+def _x_concat(lc, a, kw, ins, rec, name):
+    if lc.get("type") == "concat":
+        _hwd_from(lc, _in_lc(rec, ins))
+
+
+def _x_seqins(first):
+    def f(lc, a, kw, ins, rec, name):
+        lc["trans_type"] = _level(kw.get("agg_level"))
+        lc["seq_pool_stride"] = int(kw.get("stride", -1))
+        if first:
+            lc["select_first"] = True
+    return f
+
+
+def _x_expand(lc, a, kw, ins, rec, name):
+    lc["trans_type"] = _level(kw.get("expand_level"))
+
+
+def _x_repeat(lc, a, kw, ins, rec, name):
+    lc["num_filters"] = int(_arg(a, kw, "num_repeats", 1))
+    if not kw.get("as_row_vector", True):
+        lc["user_arg"] = "as_col_vec"
+
+
+def _act_or(kw, key, default):
+    from ..v2.activation import act_name
+
+    v = kw.get(key)
+    an = act_name(v) if v is not None else default
+    return _ACT.get(an, an)
+
+
+def _set_params(rec, name, lc, specs):
+    """Replace the layer's recorded parameters by the reference's (name, dims, std)."""
+    rec.params[:] = [p for p in rec.params if not p["name"].startswith(f"_{name}.")]
+    for pname, dims, std, smart in specs:
+        rec.params.append({"name": pname, "size": int(_prod(dims)), "initial_mean": 0.0, "initial_std": std,
+                           "dims": list(dims), "initial_strategy": 0, "initial_smart": smart})
+
+
+def _x_lstm(lc, a, kw, ins, rec, name):
+    size = int(lc.get("size") or 0) or (_vsize(ins[0][0]) or 0) // 4
+    lc["size"] = size
+    lc["reversed"] = bool(kw.get("reverse", False))
+    lc["active_gate_type"] = _act_or(kw, "gate_act", "sigmoid")
+    lc["active_state_type"] = _act_or(kw, "state_act", "tanh")
+    lc["bias_parameter_name"] = f"_{name}.wbias"
+    _set_params(rec, name, lc, [(f"_{name}.w0", [size, size, 4], 1.0 / size ** 0.5, True),
+                                (f"_{name}.wbias", [1, 7 * size], 0.0, False)])
+
+
+def _x_gru(lc, a, kw, ins, rec, name):
+    size = int(lc.get("size") or 0) or (_vsize(ins[0][0]) or 0) // 3
+    lc["size"] = size
+    lc["reversed"] = bool(kw.get("reverse", False))
+    lc["active_gate_type"] = _act_or(kw, "gate_act", "sigmoid")
+    lc["bias_parameter_name"] = f"_{name}.wbias"
+    _set_params(rec, name, lc, [(f"_{name}.w0", [size, 3 * size], 1.0 / size ** 0.5, True),
+                                (f"_{name}.wbias", [1, 3 * size], 0.0, False)])
+
+
+def _x_hsigmoid(lc, a, kw, ins, rec, name):
+    nc = int(kw.get("num_classes") or 2)
+    lc["num_classes"] = nc
+    lc["size"] = 1
+    for li in lc.get("inputs", [])[1:]:
+        li.pop("input_parameter_name", None)
+    lc["bias_parameter_name"] = f"_{name}.wbias"
+    insz = _vsize(ins[0][0]) or 0
+    # smart initialisation: std = 1 / sqrt(dims[0])
+    _set_params(rec, name, lc, [(f"_{name}.w0", [nc - 1, insz], 1.0 / (nc - 1) ** 0.5, True),
+                                (f"_{name}.wbias", [1, nc - 1], 0.0, False)])
+
+
+def _x_selective_fc(lc, a, kw, ins, rec, name):
+    lc["selective_fc_pass_generation"] = bool(kw.get("pass_generation", False))
+    lc["has_selected_colums"] = bool(kw.get("has_selected_colums", True))
+    lc["selective_fc_full_mul_ratio"] = float(kw.get("mul_ratio", 0.02))
+    for p in rec.params:
+        if p["name"] == f"_{name}.w0":
+            p["is_sparse"] = False
+
+
+_FIRST_PARENT_ONLY = {"seq_slice_layer", "sub_nested_seq_layer"}
+
+
+def _x_factor(lc, a, kw, ins, rec, name):
+    lc["factor_size"] = int(_arg(a, kw, "factor_size", 1))
+
+
+def _x_coeff(lc, a, kw, ins, rec, name):
+    lc["coeff"] = float(kw.get("coeff", 1.0))
+
+
+def _x_kmax(lc, a, kw, ins, rec, name):
+    lc.pop("size", None)
+    lc["beam_size"] = int(kw.get("beam_size", 1))
+
+
+def _x_same_size(lc, a, kw, ins, rec, name):
+    lc["size"] = _vsize(ins[0][0]) if ins else lc.get("size")
+
+
+def _x_scale_shift(lc, a, kw, ins, rec, name):
+    # one scalar scale w0 (+ scalar bias unless bias_attr=False)
+    has_b = kw.get("bias_attr", None) is not False
+    lc["inputs"] = [{"input_layer_name": rec.layer_name(ins[0][0]) or ins[0][0].name,
+                     "input_parameter_name": f"_{name}.w0"}]
+    specs = [(f"_{name}.w0", [1, 1], 1.0, True)]
+    if has_b:
+        lc["bias_parameter_name"] = f"_{name}.wbias"
+        specs.append((f"_{name}.wbias", [1, 1], 0.0, False))
+    else:
+        lc.pop("bias_parameter_name", None)
+    _set_params(rec, name, lc, specs)
+
+
+def _x_seq_slice(lc, a, kw, ins, rec, name):
+    if kw.get("ends", 1) is None:
+        lc["select_first"] = True
+    elif kw.get("starts", 1) is None:
+        lc["select_first"] = False
+
+
+_EXTRA = {
+    "factorization_machine": _x_factor, "smooth_l1_cost": _x_coeff, "kmax_seq_score_layer": _x_kmax,
+    "sampling_id_layer": _x_same_size, "scale_shift_layer": _x_scale_shift, "seq_slice_layer": _x_seq_slice,
+    "data_layer": _x_data, "addto_layer": _x_addto, "concat_layer": _x_concat,
+    "last_seq": _x_seqins(False), "first_seq": _x_seqins(True), "expand_layer": _x_expand,
+    "repeat_layer": _x_repeat, "lstmemory": _x_lstm, "grumemory": _x_gru, "hsigmoid": _x_hsigmoid,
+    "selective_fc_layer": _x_selective_fc,
+}
+
+
 def _prod(xs):
     r = 1
     for x in xs:
@@ -525,13 +713,34 @@ def _prod(xs):
     return r
 
 
+def _dfs_inputs(rec, out_names):
+    """networks.outputs: data layers in DFS post-order from each output over parents."""
+    seen, order = set(), []
+
+    def visit(n):
+        if n in seen:
+            return
+        seen.add(n)
+        for p in rec.parents.get(n, []):
+            visit(p)
+        if rec.by_name.get(n, {}).get("type") == "data":
+            order.append(n)
+
+    for o in out_names:
+        visit(o)
+    return order
+
+
 def model_config(rec, outputs):
     out_names = [rec.layer_name(o) or getattr(o, "name", str(o)) for o in outputs]
     names = [lc["name"] for lc in rec.layers]
-    return {"type": "nn", "layers": rec.layers, "parameters": rec.params, "input_layer_names": rec.inputs,
-            "output_layer_names": out_names,
-            "sub_models": [{"name": "root", "layer_names": names, "input_layer_names": rec.inputs,
-                            "output_layer_names": out_names, "is_recurrent_layer_group": False}]}
+    ins = _dfs_inputs(rec, out_names) if out_names and all(o in rec.by_name for o in out_names) else rec.inputs
+    mc = {"type": "nn", "layers": rec.layers, "parameters": rec.params, "input_layer_names": ins,
+          "output_layer_names": out_names,
+          "sub_models": [{"name": "root", "layer_names": names, "input_layer_names": ins,
+                          "output_layer_names": out_names, "is_recurrent_layer_group": False}]}
+    # proto2: an empty repeated field is an absent one
+    return {k: v for k, v in mc.items() if not (isinstance(v, list) and not v)}
 
 
 _METHOD = {"Momentum": "momentum", "Adam": "adam", "Adamax": "adamax", "AdaGrad": "adagrad",
