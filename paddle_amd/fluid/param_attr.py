@@ -41,6 +41,15 @@ class ParamAttr:
             return ParamAttr(initializer=arg)
         if isinstance(arg, bool):
             return ParamAttr._to_attr(None) if arg else False
+        if type(arg).__name__ == "ParameterAttribute":
+            # the v1 DSL's attribute (trainer_config_helpers): name / std / mean / lr
+            from .initializer import NormalInitializer
+
+            init = None
+            if getattr(arg, "initial_std", None) is not None or getattr(arg, "initial_mean", None) is not None:
+                init = NormalInitializer(loc=float(arg.initial_mean or 0.0), scale=float(arg.initial_std or 0.0))
+            lr = getattr(arg, "learning_rate", None)
+            return ParamAttr(name=arg.name, initializer=init, learning_rate=1.0 if lr is None else float(lr))
         raise TypeError(f"{type(arg)} cast to ParamAttr")
 
     def _to_kwargs(self, with_initializer=False):

@@ -37,6 +37,8 @@ TanhActivation, ReluActivation, SigmoidActivation = _act.Tanh, _act.Relu, _act.S
 SoftmaxActivation, LinearActivation, IdentityActivation = _act.Softmax, _act.Linear, _act.Identity
 ExpActivation, AbsActivation, SquareActivation = _act.Exp, _act.Abs, _act.Square
 BReluActivation, SoftReluActivation, STanhActivation = _act.BRelu, _act.SoftRelu, _act.STanh
+SequenceSoftmaxActivation, LogActivation, SqrtActivation = _act.SequenceSoftmax, _act.Log, _act.Sqrt
+ReciprocalActivation = _act.Reciprocal
 
 # ------------------------------------------------------------------ poolings
 MaxPooling, AvgPooling, SumPooling, SquareRootNPooling = _pool.Max, _pool.Avg, _pool.Sum, _pool.SquareRootN
@@ -151,7 +153,10 @@ def get_config_arg(name, type, default=None):
 def data_layer(name, size, height=None, width=None, type=None, **kw):
     if type is None:
         type = _dt.integer_value(size) if "label" in name else _dt.dense_vector(size)
-    return _l.data(name=name, type=type)
+    out = _l.data(name=name, type=type)
+    if height and width:
+        out.v2_hw = (int(height), int(width))  # image layers read [C, H, W] from it
+    return out
 
 
 def _one(x):
@@ -246,7 +251,10 @@ mse_cost = square_error_cost = regression_cost
 # ------------------------------------------------------------------ networks
 simple_img_conv_pool = _nets.simple_img_conv_pool
 sequence_conv_pool = _nets.sequence_conv_pool
-simple_lstm = _nets.simple_lstm
+from .networks_v1 import *  # noqa: E402,F401,F403  (recurrent units / groups, bidirectional RNNs, attention)
+from . import layer_math  # noqa: E402  (layer_math.exp(x), 1 + x, y * z ... on v1 layers)
+
+layer_math.install()
 
 # ------------------------------------------------------------------ evaluators
 classification_error_evaluator = _ev.classification_error

@@ -439,10 +439,23 @@ def _param_dims(p):
     return [int(d) for d in p.shape]
 
 
+def unwrap(x):
+    """A finished ``with mixed_layer(...) as m`` context stands for its layer."""
+    if type(x).__name__ == "_MixedCtx":
+        return x.m.out
+    if isinstance(x, list):
+        return [unwrap(v) for v in x]
+    if isinstance(x, tuple):
+        return tuple(unwrap(v) for v in x)
+    return x
+
+
 def recorded(fn_name, fn):
     """Wrap a DSL layer function so a call at config level records its LayerConfig."""
 
     def wrapper(*args, **kw):
+        args = tuple(unwrap(a) for a in args)
+        kw = {k: unwrap(v) for k, v in kw.items()}
         rec = current()
         if rec is None or rec.depth:
             return fn(*args, **kw)
@@ -455,6 +468,22 @@ def recorded(fn_name, fn):
             out = fn(*args, **kw)
         finally:
             rec.depth -= 1
+        if type(out).__name__ == "_MixedCtx":
+            # ``with mixed_layer(...) as m: m += ...``: recorded when the block exits
+            out.m.on_finish = lambda m, _a=args, _k=kw: _record(rec, fn_name, fn, _a, dict(_k, input=list(m.terms)),
+                                                                 m.out, before, blk)
+            return out
+        return _record(rec, fn_name, fn, args, kw, out, before, blk)
+
+    wrapper.__name__ = fn.__name__
+    wrapper.__doc__ = fn.__doc__
+    wrapper.__wrapped__ = fn
+    return wrapper
+
+
+def _record(rec, fn_name, fn, args, kw, out, before, blk):
+    """The LayerConfig (and ParameterConfigs) of one finished layer call."""
+    if True:
         new = [p for p in blk.all_parameters() if p.name not in before]
         outs = out if isinstance(out, (list, tuple)) else [out]
         if not outs or not _is_var(outs[0]):
@@ -489,6 +518,9 @@ def recorded(fn_name, fn):
             if pr is not None and fn_name == "concat_layer":
                 li["proj_conf"] = {"type": getattr(pr, "v1_type", "identity"), "name": f"_{name}.w{i}",
                                    "input_size": _vsize(x), "output_size": _vsize(x)}
+            if pr is not None and fn_name in ("mixed_layer", "embedding_layer") and getattr(pr, "v1_type", None):
+                li["proj_conf"] = {"type": _PROJ_TYPE.get(pr.v1_type, pr.v1_type), "name": f"_{name}.w{i}",
+                                   "input_size": _vsize(x), "output_size": size}
             if i < len(weights):
                 pname = f"_{name}.w{i}"
                 li["input_parameter_name"] = pname
@@ -521,11 +553,6 @@ def recorded(fn_name, fn):
         rec.of_var[id(v)] = name
         rec.vars.append(v)
         return out
-
-    wrapper.__name__ = fn.__name__
-    wrapper.__doc__ = fn.__doc__
-    wrapper.__wrapped__ = fn
-    return wrapper
 
 
 # ---------------------------------------------------------------- per-type fields
@@ -656,6 +683,19 @@ def _x_selective_fc(lc, a, kw, ins, rec, name):
 
 
 _FIRST_PARENT_ONLY = {"seq_slice_layer", "sub_nested_seq_layer"}
+_PROJ_TYPE = {"identity_offset": "identity_offset", "trans_fc": "trans_fc"}
+
+
+def _x_weight_first(lc, a, kw, ins, rec, name):
+    """scaling / interpolation / power layers list the weight layer first."""
+    if len(lc.get("inputs", [])) == 2:
+        lc["inputs"] = lc["inputs"][::-1]
+        rec.parents[name] = rec.parents.get(name, [])[::-1]
+
+
+def _x_slope(lc, a, kw, ins, rec, name):
+    lc["slope"] = kw.get("slope", 1.0)
+    lc["intercept"] = kw.get("intercept", 0.0)
 
 
 def _x_factor(lc, a, kw, ins, rec, name):
@@ -696,7 +736,24 @@ def _x_seq_slice(lc, a, kw, ins, rec, name):
         lc["select_first"] = False
 
 
+def _x_pooling(lc, a, kw, ins, rec, name):
+    """pooling_layer: MaxLayer ("max") or AverageLayer ("average" + strategy)."""
+    pt = kw.get("pooling_type")
+    kind = type(pt).__name__ if pt is not None else "Max"
+    if kind in ("Max", "MaxPooling"):
+        lc["type"] = "max"
+        if getattr(pt, "output_max_index", None) is not None:
+            lc["output_max_index"] = bool(pt.output_max_index)
+    else:
+        lc["type"] = "average"
+        lc["average_strategy"] = {"Sum": "sum", "SumPooling": "sum", "SquareRootN": "squarerootn",
+                                  "SquareRootNPooling": "squarerootn"}.get(kind, "average")
+    lc["trans_type"] = _level(kw.get("agg_level"))
+    lc["seq_pool_stride"] = int(kw.get("stride", -1))
+
+
 _EXTRA = {
+    "pooling_layer": _x_pooling, "slope_intercept_layer": _x_slope, "scaling_layer": _x_weight_first,
     "factorization_machine": _x_factor, "smooth_l1_cost": _x_coeff, "kmax_seq_score_layer": _x_kmax,
     "sampling_id_layer": _x_same_size, "scale_shift_layer": _x_scale_shift, "seq_slice_layer": _x_seq_slice,
     "data_layer": _x_data, "addto_layer": _x_addto, "concat_layer": _x_concat,

@@ -138,7 +138,8 @@ def trans_full_matrix_projection(input, size=0, param_attr=None):
 def table_projection(input, size=0, param_attr=None):
     from ..v2._core import STATE
 
-    vocab = STATE["data"][input.name].dim
+    # the id layer's vocabulary: a data layer's dim, else the layer's width
+    vocab = STATE["data"][input.name].dim if input.name in STATE["data"] else _size(input)
     return _Projection(lambda s: _L().embedding(input=input, size=[vocab, s]), size or None, input, "table")
 
 
@@ -267,6 +268,9 @@ class _MixedCtx(contextlib.AbstractContextManager):
     def __exit__(self, *exc):
         if exc[0] is None:
             self.m.finish()
+            hook = getattr(self.m, "on_finish", None)
+            if hook is not None:
+                hook(self.m)
         return False
 
     def __getattr__(self, k):  # the finished layer's Variable attributes
@@ -375,6 +379,11 @@ def memory(name, size, is_seq=False, boot_layer=None, boot_bias=None, boot_bias_
         raise RuntimeError("memory() is only valid inside a recurrent_group step function")
     rnn, mems = _RG[-1]
     m = rnn.memory(init=boot_layer) if boot_layer is not None else rnn.memory(shape=[size], value=0.0)
+    if name is None:
+        # an anonymous memory is bound later: ``m.set_input(layer)`` (LayerOutput.set_input)
+        name = f"@memory_{len(mems)}@"
+        named = _NAMED[-1]
+        m.set_input = lambda layer, _k=name, _d=named: _d.__setitem__(_k, layer)
     mems.append((name, m))
     return _sized(m, size)
 
@@ -383,6 +392,9 @@ def memory(name, size, is_seq=False, boot_layer=None, boot_bias=None, boot_bias_
 def recurrent_group(step, input, reverse=False, name=None, targetInlink=None, is_generating=False):
     """Run ``step`` over every time step of the sequence inputs (StaticInput: the same
     value each step); returns the step outputs as sequences."""
+    from .config_proto import unwrap
+
+    input = unwrap(input)
     ins = input if isinstance(input, (list, tuple)) else [input]
     with guard():
         rnn = _L().DynamicRNN()
@@ -1016,6 +1028,8 @@ def ctc_layer(input, label, size=None, name=None, norm_by_times=False, **kw):
 def nce_layer(input, label, num_classes=None, act=None, param_attr=None, weight=None, num_neg_samples=10,
               neg_distribution=None, name=None, bias_attr=None, layer_attr=None):
     x = _L().concat(list(input), axis=1) if isinstance(input, (list, tuple)) else input
+    if num_classes is None:  # reference nce_layer: the label layer's size
+        num_classes = _size(label)
     with guard():
         return _cost_out(_L().mean(_L().nce(x, label, num_total_classes=num_classes,
                                             num_neg_samples=num_neg_samples)), name)
@@ -1119,3 +1133,48 @@ def cross_entropy_over_beam(input, name=None):
             terms.append(_L().cross_entropy(prob, b.gold))
         s = terms[0] if len(terms) == 1 else _L().sums(terms)
         return _cost_out(_L().mean(s), name)
+
+
+# ------------------------------------------------------------------ operators / unwrapping
+@_export
+def conv_operator(img, filter, filter_size, num_filters, num_channels=None, stride=1, padding=0,
+                  filter_size_y=None, stride_y=None, padding_y=None, trans=False):
+    """A convolution whose filter is another layer's output (one filter set per
+    sample): a deferred term of a mixed layer, like a projection."""
+    def build(size):
+        with guard():
+            c = num_channels or 1
+            fy = filter_size_y or filter_size
+            x = _L().reshape(img, [-1, c, int(round((_size(img) // c) ** 0.5)), int(round((_size(img) // c) ** 0.5))])
+            w = _L().reshape(filter, [num_filters, c, fy, filter_size])
+            out = _op("conv2d", {"Input": [x], "Filter": [w]}, {"Output": "float32"},
+                      {"strides": [stride_y or stride, stride], "paddings": [padding_y or padding, padding],
+                       "dilations": [1, 1], "groups": 1})["Output"]
+            return _L().reshape(out, [-1, int(_prod_shape(out))]) if size else out
+    return _Projection(build, None, img, "conv_op")
+
+
+def _prod_shape(v):
+    n = 1
+    for d in (v.shape or ())[1:]:
+        n *= max(int(d), 1)
+    return n
+
+
+def _unwrap_args(fn):
+    import functools
+
+    @functools.wraps(fn)
+    def w(*args, **kw):
+        from .config_proto import unwrap
+
+        return fn(*[unwrap(a) for a in args], **{k: unwrap(v) for k, v in kw.items()})
+    return w
+
+
+# projection / operator helpers accept a finished ``with mixed_layer() as m`` context
+for _n in ("full_matrix_projection", "trans_full_matrix_projection", "table_projection", "identity_projection",
+           "slice_projection", "dotmul_projection", "scaling_projection", "dotmul_operator", "context_projection",
+           "conv_projection", "conv_operator"):
+    globals()[_n] = _unwrap_args(globals()[_n])
+del _n

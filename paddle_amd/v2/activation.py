@@ -22,6 +22,10 @@ Square = _act("square")
 BRelu = _act("brelu")
 SoftRelu = _act("soft_relu")
 STanh = _act("stanh")
+SequenceSoftmax = _act("sequence_softmax")
+Log = _act("log")
+Sqrt = _act("sqrt")
+Reciprocal = _act("reciprocal")
 
 
 class Linear(BaseActivation):

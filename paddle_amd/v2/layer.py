@@ -54,7 +54,12 @@ def embedding(input, size, param_attr=None, **kw):
 def _as_image(input, num_channels):
     if len(input.shape) == 4:
         return input
-    hw = int(round(math.sqrt(input.shape[-1] // num_channels)))
+    hw2 = getattr(input, "v2_hw", None)
+    size = getattr(input, "v2_size", None) or input.shape[-1]
+    if hw2 is not None:  # data_layer(height=, width=): [C, H, W] with C = size / (H W)
+        h, w = hw2
+        return fluid.layers.reshape(input, [-1, max(int(size) // (h * w), 1), h, w])
+    hw = int(round(math.sqrt(size // num_channels)))
     return fluid.layers.reshape(input, [-1, num_channels, hw, hw])
 
 

@@ -5,8 +5,10 @@ class BasePool:
     seq = "AVERAGE"
     img = "avg"
 
-    def __init__(self):
-        pass
+    def __init__(self, output_max_index=None, strategy=None, **kw):
+        # MaxPooling(output_max_index=True): the layer emits the arg-max index
+        self.output_max_index = output_max_index
+        self.strategy = strategy
 
 
 class Max(BasePool):
