@@ -1207,14 +1207,23 @@ PA_EXPORT void pa_gemm_set_stagger(int s) { gemm::g_stagger = s; }
 //   k_total > 0: split-K, batch b covers k in [b*K, min((b+1)*K, k_total)) (sA/sB are
 //   the k offsets of one split); atomic (fp32 C, sC = 0): every split adds its tile
 //   into C with float atomics, otherwise the caller sums the per-batch outputs
-PA_EXPORT int pa_gemm(int a_kmaj, int b_kmaj, int out_f32, const void* A, const void* B, void* C,
+static int gemm_entry(bool padded, int a_kmaj, int b_kmaj, int out_f32, const void* A, const void* B, void* C,
                       const void* bias, int M, int N, int K, long lda, long ldb, long ldc, long sA, long sB,
                       long sC, int batch, float alpha, int accumulate, int k_total, int atomic, const int* grp,
                       int grp_mode, hipStream_t st) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
   // 16-B chunks: along K for a K-major operand, along M / N for an MN-major one,
-  // along N for the output
-  if ((N & 7) || ((a_kmaj || b_kmaj) && (K & 7)) || (!a_kmaj && (M & 7))) return -1;
+  // along N for the output.  `padded` (pa_gemm_padded): the extents may be ragged
+  // when the leading dimensions are 8-aligned -- a chunk that starts inside the
+  // matrix is moved whole, so it reads / writes the row padding up to the next
+  // multiple of 8 (see pa_gemm_padded for the caller's contract)
+  if (padded) {
+    auto r8 = [](long v) { return (v + 7) & ~7L; };
+    if ((lda & 7) || (ldb & 7) || (ldc & 7) || ldc < r8(N)) return -1;
+    if (lda < (a_kmaj ? r8(K) : r8(M)) || ldb < (b_kmaj ? r8(K) : r8(N))) return -1;
+  } else if ((N & 7) || ((a_kmaj || b_kmaj) && (K & 7)) || (!a_kmaj && (M & 7))) {
+    return -1;
+  }
   gemm::Params p{};
   p.A = A; p.B = B; p.C = C; p.bias = bias;
   p.M = M; p.N = N; p.K = K;
@@ -1234,6 +1243,27 @@ PA_EXPORT int pa_gemm(int a_kmaj, int b_kmaj, int out_f32, const void* A, const 
   PA_G(1, 1, 1) PA_G(1, 0, 1) PA_G(0, 1, 1) PA_G(0, 0, 1)
 #undef PA_G
   return -1;
+}
+
+PA_EXPORT int pa_gemm(int a_kmaj, int b_kmaj, int out_f32, const void* A, const void* B, void* C,
+                      const void* bias, int M, int N, int K, long lda, long ldb, long ldc, long sA, long sB,
+                      long sC, int batch, float alpha, int accumulate, int k_total, int atomic, const int* grp,
+                      int grp_mode, hipStream_t st) {
+  return gemm_entry(false, a_kmaj, b_kmaj, out_f32, A, B, C, bias, M, N, K, lda, ldb, ldc, sA, sB, sC, batch, alpha,
+                    accumulate, k_total, atomic, grp, grp_mode, st);
+}
+
+// pa_gemm for ragged extents (a vocabulary that is not a multiple of 8: GPT's
+// 50,257-wide tied LM head) on 8-aligned row buffers.  Contract: every row of A, B
+// and C holds at least the extent rounded up to 8 elements (lda / ldb / ldc are
+// multiples of 8); the padding of a K-major operand past K and of an MN-major A
+// past M is ZERO (it enters the products); C columns N .. round8(N) are written
+// (with zeros from out-of-range B rows) -- never C memory past the padded row.
+// B rows past N (K-major B) and past K (MN-major B) are not read.
+PA_EXPORT int pa_gemm_padded(int a_kmaj, int b_kmaj, int out_f32, const void* A, const void* B, void* C,
+                             int M, int N, int K, long lda, long ldb, long ldc, int accumulate, hipStream_t st) {
+  return gemm_entry(true, a_kmaj, b_kmaj, out_f32, A, B, C, nullptr, M, N, K, lda, ldb, ldc, 0, 0, 0, 1, 1.f,
+                    accumulate, 0, 0, nullptr, 0, st);
 }
 
 // Fused-epilogue GEMMs, both operands K-major, bf16 C (see Params::aux):

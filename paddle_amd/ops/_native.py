@@ -106,6 +106,7 @@ _SIGS = {
     "pa_gemm_set_persistent": [_I],
     "pa_gemm_set_stagger": [_I],
     "pa_gemm": [_I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _L, _L, _I, _F, _I, _I, _I, _P, _I, _P],
+    "pa_gemm_padded": [_I, _I, _I, _P, _P, _P, _I, _I, _I, _L, _L, _L, _I, _P],
     "pa_splitk_reduce": [_P, _P, _L, _I, _I, _P],
     "pa_moe_gather": [_P, _P, _P, _L, _I, _P],
     "pa_group_tile_table": [_P, _I, _L, _P],

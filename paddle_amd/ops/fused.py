@@ -32,6 +32,25 @@ def _oplib_fill(t, v):
 
     return oplib.fill_(t, v)
 
+
+def _fill_native(t, v):
+    """t[...] = v (strided views too) on the native elementwise kernel."""
+    from . import aten_native as A
+
+    if not (t.is_cuda and t.dtype in A._DT and A._launch(A.U["fill"], t, [], a=float(v), cdt=A._cdt(t.dtype))):
+        t.fill_(v)
+    return t
+
+
+def _copy_native(dst, src):
+    """dst[...] = src (strided views, same shape) on the native elementwise kernel."""
+    from . import aten_native as A
+
+    if not (dst.is_cuda and dst.dtype in A._DT and src.dtype in A._DT
+            and A._launch(A.U["copy"], dst, [src], cdt=A._cdt(src.dtype))):
+        dst.copy_(src)
+    return dst
+
 def _c(t):
     return t if t.is_contiguous() else t.contiguous()
 
@@ -1476,9 +1495,10 @@ class _LinearTFn(torch.autograd.Function):
 
     GPU: the hand-written GEMM in all three forms (forward both K-major; dX with W
     MN-major; dW = dY^T X with both operands MN-major, into the fp32 main_grad when
-    the table has one).  A vocabulary that is not a multiple of 8 (GPT's 50,257) is
-    computed into an 8-aligned output buffer: the GEMM covers the first V - V % 8
-    columns, a thin product the last V % 8, then the buffer is trimmed."""
+    the table has one).  A vocabulary that is not a multiple of 8 (GPT's 50,257) runs
+    the same forms on 8-aligned row buffers (``gemm_padded``): the logits are
+    computed into [T, round8(V)] rows and the incoming gradient is laid into
+    zero-padded rows, so no product leaves the MFMA kernel."""
 
     @staticmethod
     def forward(ctx, x, w):
@@ -1486,14 +1506,14 @@ class _LinearTFn(torch.autograd.Function):
         V, H = w.shape
         x2 = x.reshape(-1, H)
         if _G.supported(x2.shape[0], 8, H, x2, w) and V >= 8:
-            V8, Vp = V // 8 * 8, (V + 7) // 8 * 8
+            Vp = (V + 7) // 8 * 8
             if Vp == V:
                 return _G.gemm(x2, w, x2.shape[0], V, H, a_kmaj=True, b_kmaj=True).view(*x.shape[:-1], V)
-            # 8-aligned rows of the output buffer; the last V % 8 columns by a thin product
             buf = torch.empty(x2.shape[0], Vp, dtype=x.dtype, device=x.device)
-            _G.gemm(x2, w[:V8], x2.shape[0], V8, H, a_kmaj=True, b_kmaj=True, out=buf, ldc=Vp)
-            buf[:, V8:V] = torch.matmul(x2, w[V8:].t())
-            return buf[:, :V].contiguous().view(*x.shape[:-1], V)
+            _G.gemm_padded(x2, w, x2.shape[0], V, H, a_kmaj=True, b_kmaj=True, out=buf)
+            out = torch.empty(x2.shape[0], V, dtype=x.dtype, device=x.device)
+            _copy_native(out, buf[:, :V])
+            return out.view(*x.shape[:-1], V)
         return torch.matmul(x, w.t())
 
     @staticmethod
@@ -1504,6 +1524,29 @@ class _LinearTFn(torch.autograd.Function):
         dy2 = _c(dy).reshape(-1, V)
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         mg = getattr(w, "_pa_main_grad", None)
+        if V % 8 and V >= 8 and _G.supported(x2.shape[0], H, 8, x2, w):
+            # ragged vocabulary: the gradient in zero-padded 8-aligned rows, then the
+            # padded GEMM forms (padding enters the K / M extents as zeros)
+            T, Vp = x2.shape[0], (V + 7) // 8 * 8
+            dyp = torch.empty(T, Vp, dtype=dy2.dtype, device=dy2.device)
+            _fill_native(dyp[:, V:], 0.0)
+            _copy_native(dyp[:, :V], dy2)
+            dx = None
+            if need_x:
+                dx = torch.empty(T, H, dtype=x.dtype, device=x.device)
+                _G.gemm_padded(dyp, w, T, H, V, a_kmaj=True, b_kmaj=False, out=dx)
+                dx = dx.view(x.shape)
+            dw = None
+            if need_w:
+                if mg is not None:
+                    fresh = getattr(w, "_pa_grad_fresh", False)
+                    w._pa_grad_fresh = False
+                    _G.gemm_padded(dyp, x2, V, H, T, a_kmaj=False, b_kmaj=False, out=mg, accumulate=not fresh)
+                else:
+                    g32 = torch.empty(V, H, dtype=torch.float32, device=x.device)
+                    _G.gemm_padded(dyp, x2, V, H, T, a_kmaj=False, b_kmaj=False, out=g32)
+                    dw = g32.to(w.dtype)
+            return dx, dw
         if V % 8 == 0 and _G.supported(x2.shape[0], H, V, x2, w, dy2):
             dx = _G.gemm(dy2, w, x2.shape[0], H, V, a_kmaj=True, b_kmaj=False).view(x.shape) if need_x else None
             dw = None

@@ -69,6 +69,19 @@ def gemm(a, b, M, N, K, *, a_kmaj, b_kmaj, out=None, out_dtype=torch.bfloat16, b
     return out
 
 
+def gemm_padded(a, b, M, N, K, *, a_kmaj, b_kmaj, out, accumulate=False):
+    """:func:`gemm` for ragged M / N / K on 8-aligned row buffers (``pa_gemm_padded``):
+    rows of ``a`` / ``b`` / ``out`` hold the extents rounded up to 8, the padding of a
+    K-major operand past K (and of an MN-major ``a`` past M) is zero, and ``out``'s
+    columns N .. round8(N) are written with zeros."""
+    rc = _nat.lib().pa_gemm_padded(int(a_kmaj), int(b_kmaj), int(out.dtype == torch.float32), _nat.ptr(a),
+                                   _nat.ptr(b), _nat.ptr(out), M, N, K, a.stride(-2), b.stride(-2), out.stride(-2),
+                                   int(accumulate), _nat.stream())
+    if rc != 0:
+        raise RuntimeError(f"pa_gemm_padded failed (rc={rc}) M={M} N={N} K={K} a_kmaj={a_kmaj} b_kmaj={b_kmaj}")
+    return out
+
+
 EPI_SWIGLU_FWD, EPI_SWIGLU_BWD, EPI_ROPE = 1, 2, 3
 
 
