@@ -116,3 +116,162 @@ PA_EXPORT int pa_moe_combine_bwd(const void* dy, const void* ys, const int* pos,
                      (const u16*)ys, pos, w, (u16*)dys, dw, T, k, H);
   PA_LAUNCH_CHECK();
 }
+
+// ---------------------------------------------------------------------------------
+// Routing without a sort: the gate's expert per slot (flat_e [n = T*k]) -> the
+// expert-sorted order of the kept slots, in ONE 1024-thread workgroup.
+//   pass 1  per-expert slot counts (LDS integer atomics: order-free, exact);
+//   scan    row offsets of each expert (thread 0, E <= 1024);
+//   pass 2  slots in chunks of 1024 in slot order: a slot's rank inside its expert =
+//           running base of the expert + earlier lanes of its wave with the same
+//           expert (64 lane reads); the 16 waves of a chunk take and advance the
+//           bases one after another (one barrier each), so within an expert the
+//           order is slot order -- the stable argsort of the torch path, exactly.
+// mode 0: every slot kept, row = off[e] + rank               (outputs pos, src, e_sorted)
+// mode 1: GShard capacity layout, row = e * cap + rank, dropped when rank >= cap
+//         (pos, src [E * cap]; padding rows get token 0)
+// mode 2: capacity drop with compact rows, row = offk[e] + rank, offk = scan of
+//         min(count, cap)                                    (pos, src, e_sorted)
+// counts[e] (int64) = kept slots of expert e in every mode.
+namespace pa {
+
+constexpr int kRouteT = 1024;
+
+__global__ __launch_bounds__(kRouteT) void moe_route_kernel(const long* __restrict__ flat_e, long n, int E, int k,
+                                                            int mode, long cap, int* __restrict__ pos,
+                                                            int* __restrict__ src, long* __restrict__ e_sorted,
+                                                            long* __restrict__ counts) {
+  __shared__ int base[1024];  // slot count per expert, then the running rank base
+  __shared__ int off[1024];   // first row of each expert (modes 0 / 2)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int e = tid; e < E; e += kRouteT) base[e] = 0;
+  if (mode == 1)
+    for (long r = tid; r < (long)E * cap; r += kRouteT) src[r] = 0;
+  __syncthreads();
+  for (long i = tid; i < n; i += kRouteT) atomicAdd(&base[(int)flat_e[i]], 1);
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int e = 0; e < E; ++e) {
+      const int kept = mode == 0 ? base[e] : (base[e] < cap ? base[e] : (int)cap);
+      counts[e] = kept;
+      off[e] = acc;
+      acc += kept;
+      base[e] = 0;
+    }
+  }
+  __syncthreads();
+  for (long c0 = 0; c0 < n; c0 += kRouteT) {
+    const long i = c0 + tid;
+    const int e = i < n ? (int)flat_e[i] : -1;
+    int r = 0, c = 0;  // rank among / count of this wave's lanes with expert e
+    for (int j = 0; j < 64; ++j) {
+      const int ej = __shfl(e, j, 64);
+      c += ej == e ? 1 : 0;
+      r += (j < lane && ej == e) ? 1 : 0;
+    }
+    int rank = 0;
+    for (int ww = 0; ww < kRouteT / 64; ++ww) {
+      if (w == ww && e >= 0) {
+        rank = base[e] + r;            // every lane of the wave reads before ...
+        if (r == c - 1) base[e] = rank + 1;  // ... the group's last lane advances the base
+      }
+      __syncthreads();
+    }
+    if (e >= 0) {
+      const bool keep = mode == 0 || rank < cap;
+      int row = -1;
+      if (keep) {
+        row = mode == 1 ? (int)(e * cap + rank) : off[e] + rank;
+        src[row] = (int)(i / k);
+        if (mode != 1) e_sorted[row] = e;
+      }
+      pos[i] = row;
+    }
+  }
+}
+
+// frac_e = share of tokens whose first choice is e (idx [T, k] int64, column 0)
+__global__ __launch_bounds__(1024) void moe_frac_kernel(const long* __restrict__ idx, long T, int k, int E,
+                                                        float* __restrict__ frac) {
+  __shared__ int cnt[1024];
+  for (int e = threadIdx.x; e < E; e += 1024) cnt[e] = 0;
+  __syncthreads();
+  for (long t = threadIdx.x; t < T; t += 1024) atomicAdd(&cnt[(int)idx[t * k]], 1);
+  __syncthreads();
+  for (int e = threadIdx.x; e < E; e += 1024) frac[e] = (float)cnt[e] / (float)(T > 0 ? T : 1);
+}
+
+// Router backward (fp32), one wave per token: with valn = the top-k probabilities
+// renormalised by s and the balance loss l = E * sum_e mean_t(p_te) frac_e
+//   dv_j   = (dval_j - sum_i dval_i valn_i) / s     (renorm; else dval_j)
+//   dp_te  = sum_j [idx_tj == e] dv_j + daux * E * frac_e / T
+//   dlogit = p * (dp - <dp, p>)
+// (the scatter_add + softmax backward of the torch formulation in one pass; k <= 64)
+__global__ __launch_bounds__(256) void moe_gate_bwd_kernel(const float* __restrict__ probs,
+                                                           const long* __restrict__ idx,
+                                                           const float* __restrict__ valn,
+                                                           const float* __restrict__ s,
+                                                           const float* __restrict__ frac,
+                                                           const float* __restrict__ dval,
+                                                           const float* __restrict__ daux, long T, int E,
+                                                           int k, int renorm, float* __restrict__ dlogits) {
+  const long t = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T) return;
+  const int lane = threadIdx.x & 63;
+  const float* p = probs + t * E;
+  float dv = 0.f;
+  if (dval) {
+    dv = lane < k ? dval[t * k + lane] : 0.f;
+    if (renorm) {
+      const float dot = wave_sum(lane < k ? dv * valn[t * k + lane] : 0.f);
+      dv = (dv - dot) / s[t];
+    }
+  }
+  const int my = lane < k ? (int)idx[t * k + lane] : -1;
+  const float ga = daux ? daux[0] * (float)E / (float)T : 0.f;
+  float part = 0.f;
+  for (int e = lane; e < E; e += 64) {
+    float dp = ga * frac[e];
+    for (int j = 0; j < k; ++j)
+      if (__shfl(my, j, 64) == e) dp += __shfl(dv, j, 64);
+    part += dp * p[e];
+  }
+  const float dot = wave_sum(part);
+  for (int e = lane; e < E; e += 64) {
+    float dp = ga * frac[e];
+    for (int j = 0; j < k; ++j)
+      if (__shfl(my, j, 64) == e) dp += __shfl(dv, j, 64);
+    dlogits[t * E + e] = p[e] * (dp - dot);
+  }
+}
+
+}  // namespace pa
+
+using namespace pa;
+
+PA_EXPORT int pa_moe_route(const long* flat_e, long n, int E, int k, int mode, long cap, int* pos, int* src,
+                           long* e_sorted, long* counts, hipStream_t st) {
+  if (E <= 0 || E > 1024 || k <= 0 || mode < 0 || mode > 2 || (mode != 0 && cap < 0)) return -1;
+  if (mode != 0 && (long)E * cap > 0x7fffffffL) return -1;
+  if (mode != 1 && !e_sorted) return -1;
+  hipLaunchKernelGGL(moe_route_kernel, dim3(1), dim3(kRouteT), 0, st, flat_e, n, E, k, mode, cap, pos, src,
+                     e_sorted, counts);
+  PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_moe_frac(const long* idx, long T, int k, int E, float* frac, hipStream_t st) {
+  if (E <= 0 || E > 1024 || k <= 0) return -1;
+  hipLaunchKernelGGL(moe_frac_kernel, dim3(1), dim3(1024), 0, st, idx, T, k, E, frac);
+  PA_LAUNCH_CHECK();
+}
+
+PA_EXPORT int pa_moe_gate_bwd(const float* probs, const long* idx, const float* valn, const float* s,
+                              const float* frac, const float* dval, const float* daux, long T, int E, int k,
+                              int renorm, float* dlogits, hipStream_t st) {
+  if (k <= 0 || k > 64 || E <= 0) return -1;
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(moe_gate_bwd_kernel, dim3((unsigned)((T + 3) / 4)), dim3(256), 0, st, probs, idx, valn, s,
+                     frac, dval, daux, T, E, k, renorm, dlogits);
+  PA_LAUNCH_CHECK();
+}

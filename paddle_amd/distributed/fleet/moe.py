@@ -83,7 +83,14 @@ class _TopKGateFn(torch.autograd.Function):
         s = val.sum(-1, keepdim=True).clamp_min(1e-9) if renorm else None
         valn = val / s if renorm else val
         E = w.shape[1]
-        frac = torch.nn.functional.one_hot(idx[:, 0], E).float().mean(0)
+        if x.is_cuda and E <= 1024:
+            from ...ops import _native as N
+
+            idx = idx.contiguous()
+            frac = torch.empty(E, dtype=torch.float32, device=x.device)
+            N.call("pa_moe_frac", N.ptr(idx), idx.shape[0], k, E, N.ptr(frac), N.stream())
+        else:
+            frac = torch.nn.functional.one_hot(idx[:, 0], E).float().mean(0)
         l_aux = (probs.mean(0) * frac).sum() * E
         ctx.save_for_backward(x, w, probs, idx, valn, s if s is not None else probs.new_ones(1), frac)
         ctx.renorm = renorm
@@ -93,6 +100,8 @@ class _TopKGateFn(torch.autograd.Function):
     def backward(ctx, dval, _didx, daux):
         x, w, probs, idx, valn, s, frac = ctx.saved_tensors
         T, E = probs.shape
+        if probs.is_cuda and idx.shape[1] <= 64:
+            return _TopKGateFn._backward_native(ctx, x, w, probs, idx, valn, s, frac, dval, daux)
         dprobs = torch.zeros_like(probs)
         if dval is not None:
             dval = dval.float()
@@ -107,6 +116,29 @@ class _TopKGateFn(torch.autograd.Function):
         dx = (dlogits @ w.float().t()).to(x.dtype)
         dw = (x.float().t() @ dlogits).to(w.dtype)
         return dx, dw, None, None
+
+    @staticmethod
+    def _backward_native(ctx, x, w, probs, idx, valn, s, frac, dval, daux):
+        """GPU backward: ``pa_moe_gate_bwd`` fuses the top-k renormalisation, the
+        scatter into dprobs, the balance term and the softmax backward into dlogits;
+        the two router GEMMs and the casts run on the framework kernels (native
+        region: aten_native's exact-fp32 GEMM, deterministic split-K)."""
+        from ...ops import _native as N
+        from ...ops.convnd import deterministic
+
+        T, E = probs.shape
+        dl = torch.empty(T, E, dtype=torch.float32, device=probs.device)
+        dv = None if dval is None else dval.float().contiguous()
+        da = None if daux is None else daux.float().reshape(1).contiguous()
+        N.call("pa_moe_gate_bwd", N.ptr(probs), N.ptr(idx), N.ptr(valn), N.ptr(s), N.ptr(frac),
+               N.ptr(dv) if dv is not None else None, N.ptr(da) if da is not None else None, T, E, idx.shape[1],
+               int(ctx.renorm), N.ptr(dl), N.stream())
+        with _strict.region("moe:gate:bwd"), deterministic():
+            wf = w if w.dtype == torch.float32 else w.float()
+            xf = x if x.dtype == torch.float32 else x.float()
+            dx = dl @ wf.t()
+            dw = xf.t() @ dl
+            return dx.to(x.dtype), dw.to(w.dtype), None, None
 
 
 class TopKGate(Layer):
@@ -168,19 +200,10 @@ class MoELayer(Layer):
         flat_w = val                                   # [T, k] gate weights (combine reads them flat)
         if self.capacity_factor is not None and self.sync_free:
             return _F.reshape(self._forward_capacity(x, flat_e, flat_w, T, k, E), shape)
-        keep = None
-        if self.capacity_factor is not None:
-            cap = max(1, int(self.capacity_factor * T * k / E))
-            order = torch.argsort(flat_e, stable=True)
-            se = flat_e[order]
-            first = torch.searchsorted(se, se, right=False)
-            rank_in_e = torch.arange(se.numel(), device=x.device) - first
-            keep = torch.empty_like(flat_e, dtype=torch.bool)
-            keep[order] = rank_in_e < cap
-        # expert-sorted kept slots: src = token of each sorted row, pos = its inverse
-        _, src, pos, e_sorted = _route.routing(flat_e, T, k, keep)
-        # per global expert, from this rank (index_add: bincount would sync on its max)
-        counts = torch.zeros(E, dtype=torch.int64, device=x.device).index_add_(0, e_sorted, torch.ones_like(e_sorted))
+        cap = None if self.capacity_factor is None else max(1, int(self.capacity_factor * T * k / E))
+        # expert-sorted kept slots: src = token of each sorted row, pos = its inverse;
+        # counts per global expert, from this rank
+        src, pos, e_sorted, counts = _route.route(flat_e, T, k, E, cap)
         send = _route.dispatch(x, src, pos, k)
         # exchange counts, then tokens: rank r receives, for each local expert, the
         # tokens of every peer (peer-major)

@@ -892,8 +892,21 @@ class _PositionAddFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        S, H = ctx.S, g.shape[-1]
+        if g.is_cuda and g.dtype == ctx.tdtype and _fast_bias_ok(g) and S * H < 2 ** 31:
+            # the table gradient is the column sum of g viewed as [B, S * H]: the bias
+            # reduction kernel (fp32 partials), rows past S zero-filled
+            g2 = _c(g)
+            B = g2.numel() // (S * H)
+            dt = torch.empty(ctx.tshape, dtype=g.dtype, device=g.device)
+            if S < ctx.tshape[0]:
+                _fill_native(dt[S:], 0.0)
+            part = _ws(int(N.lib().pa_bias_grad_blocks(B, S * H)) * S * H, g.device)
+            N.call("pa_bias_act_bwd", N.dt(g2), 0, N.ptr(g2), None, None, N.ptr(dt), N.ptr(part), B, S * H,
+                   N.stream())
+            return g, dt
         dt = torch.zeros(ctx.tshape, dtype=torch.float32, device=g.device)
-        dt[:ctx.S] = g.float().reshape(-1, ctx.S, g.shape[-1]).sum(0)
+        dt[:S] = g.float().reshape(-1, S, H).sum(0)
         return g, dt.to(ctx.tdtype)
 
 

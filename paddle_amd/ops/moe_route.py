@@ -35,6 +35,48 @@ def routing(flat_e, T, k, keep=None):
     return slots, src, pos, flat_e[slots]
 
 
+def _route_native_ok(flat_e, E):
+    return flat_e.is_cuda and flat_e.dtype == torch.int64 and 0 < E <= 1024
+
+
+def _rank_in_expert(flat_e):
+    """Rank of every slot among the slots of its expert, in slot order (torch path)."""
+    order = torch.argsort(flat_e, stable=True)
+    se = flat_e[order]
+    first = torch.searchsorted(se, se, right=False)
+    rank = torch.empty_like(order)
+    rank[order] = torch.arange(se.numel(), device=flat_e.device) - first
+    return rank
+
+
+def route(flat_e, T, k, E, cap=None):
+    """Expert-sorted layout of the kept slots -> (src [R] int32, pos [T*k] int32,
+    e_sorted [R] int64, counts [E] int64).  ``cap``: keep only the first ``cap`` slots
+    of each expert (slot order; rows stay compact).  On the GPU one workgroup of
+    ``pa_moe_route`` (a stable counting sort: no argsort, no index_put, no
+    histogram atomics on global memory); with ``cap`` the kept-row count is read back
+    to size the outputs (the torch path syncs on it the same way)."""
+    n = flat_e.numel()
+    if _route_native_ok(flat_e, E):
+        dev = flat_e.device
+        flat_e = _c(flat_e)
+        pos = torch.empty(n, dtype=torch.int32, device=dev)
+        src = torch.empty(n, dtype=torch.int32, device=dev)
+        e_sorted = torch.empty(n, dtype=torch.int64, device=dev)
+        counts = torch.empty(E, dtype=torch.int64, device=dev)
+        N.call("pa_moe_route", N.ptr(flat_e), n, E, k, 0 if cap is None else 2, -1 if cap is None else int(cap),
+               N.ptr(pos), N.ptr(src), N.ptr(e_sorted), N.ptr(counts), N.stream())
+        if cap is not None:
+            R = int(counts.sum())
+            src, e_sorted = src[:R], e_sorted[:R]
+        return src, pos, e_sorted, counts
+    keep = None if cap is None else _rank_in_expert(flat_e) < cap
+    _, src, pos, e_sorted = routing(flat_e, T, k, keep)
+    counts = torch.zeros(E, dtype=torch.int64, device=flat_e.device).index_add_(0, e_sorted,
+                                                                                torch.ones_like(e_sorted))
+    return src, pos, e_sorted, counts
+
+
 def _native_ok(x):
     return x.is_cuda and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0
 
@@ -116,12 +158,15 @@ def capacity_routing(flat_e, T, k, E, cap):
     each row, 0 for padding rows; pos [T*k] int32).  Kept slots match ``routing``
     with keep = rank < cap, in the same within-expert order."""
     dev = flat_e.device
-    order = torch.argsort(flat_e, stable=True)
-    se = flat_e[order]
-    first = torch.searchsorted(se, se, right=False)
-    rank_sorted = torch.arange(se.numel(), device=dev) - first
-    rank = torch.empty_like(rank_sorted)
-    rank[order] = rank_sorted
+    if _route_native_ok(flat_e, E):
+        flat_e = _c(flat_e)
+        pos = torch.empty(T * k, dtype=torch.int32, device=dev)
+        src = torch.empty(E * cap, dtype=torch.int32, device=dev)  # the kernel zero-fills padding rows
+        counts = torch.empty(E, dtype=torch.int64, device=dev)
+        N.call("pa_moe_route", N.ptr(flat_e), T * k, E, k, 1, int(cap), N.ptr(pos), N.ptr(src), None, N.ptr(counts),
+               N.stream())
+        return src, pos
+    rank = _rank_in_expert(flat_e)
     keep = rank < cap
     row = flat_e * cap + rank
     pos = torch.where(keep, row, torch.full_like(row, -1)).to(torch.int32)

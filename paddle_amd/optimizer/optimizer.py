@@ -140,12 +140,55 @@ class Optimizer:
             self._clear_grad(set_to_zero)
 
     def _clear_grad(self, set_to_zero):
+        if set_to_zero and self._flat_grad_zero():
+            return
         for p in self._parameter_list:
             if p.grad is not None:
                 if set_to_zero:
                     p.grad.zero_()
                 else:
                     p.grad = None
+
+    def _flat_grad_zero(self):
+        """clear_grad(set_to_zero=True) as ONE fill per (device, dtype): on the first
+        call the device gradients are re-homed as views of a flat buffer (the
+        backward's in-place accumulation keeps them there), later calls zero the
+        buffer in one launch instead of one ``zero_`` per parameter.  A gradient the
+        user rebinds (or a parameter without one) falls back to the per-tensor loop
+        for that call and the layout is rebuilt on the next."""
+        ps = [p for p in self._parameter_list if p.grad is not None]
+        if not ps:
+            return False
+        flat = getattr(self, "_pa_flat_grads", None)
+        if flat is not None and flat[0] == len(ps) and all(
+                p.grad.data_ptr() == ptr and p.grad.shape == p.shape for p, ptr in zip(ps, flat[1])):
+            from ..ops import oplib
+
+            for buf in flat[2]:
+                oplib.fill_(buf, 0.0)
+            return True
+        groups = {}
+        for p in ps:
+            if not p.grad.is_contiguous() or p.grad.dtype not in (torch.float32, torch.bfloat16, torch.float16):
+                return False
+            groups.setdefault((p.grad.device, p.grad.dtype), []).append(p)
+        bufs, ptrs = [], {}
+        from ..ops import oplib
+
+        for (dev, dt), members in groups.items():
+            # 256-B aligned slots (the vectorised kernels take 16-B rows)
+            sizes = [(m.grad.numel() + 127) // 128 * 128 for m in members]
+            buf = torch.empty(sum(sizes), dtype=dt, device=dev)
+            oplib.fill_(buf, 0.0)
+            off = 0
+            for m, n in zip(members, sizes):
+                g = buf[off:off + m.grad.numel()].view(m.grad.shape)
+                m.grad = g.as_subclass(type(m.grad)) if type(m.grad) is not torch.Tensor else g
+                ptrs[id(m)] = m.grad.data_ptr()
+                off += n
+            bufs.append(buf)
+        self._pa_flat_grads = (len(ps), [ptrs[id(p)] for p in ps], bufs)
+        return True
 
     clear_gradients = clear_grad
 

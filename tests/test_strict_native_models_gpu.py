@@ -1,0 +1,82 @@
+"""FLAGS_strict_native=1 on the model paths: one training step of
+LLaMA-tiny, GPT-tiny (50,257-wide tied LM head on the padded native GEMM) and
+ERNIE-MoE-tiny (native routing / router backward) -- forward on the framework tape,
+tape backward, flat sharded AdamW -- runs inside one framework region with every
+ATen device kernel refused (utils/strict.py raises StrictNativeError), and the Fluid
+ResNet program runs on the C++ executor with no Python-kernel or host fallback."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def strict_on():
+    old = os.environ.get("FLAGS_strict_native")
+    os.environ["FLAGS_strict_native"] = "1"
+    try:
+        yield
+    finally:
+        if old is None:
+            os.environ.pop("FLAGS_strict_native", None)
+        else:
+            os.environ["FLAGS_strict_native"] = old
+
+
+def _model(name):
+    dev = torch.device("cuda", 0)
+    if name == "llama":
+        from paddle_amd.models.llama import LLAMA_CONFIGS, LlamaConfig, LlamaForCausalLM
+
+        cfg = LlamaConfig(**dict(LLAMA_CONFIGS["llama-tiny"], hidden_size=256, intermediate_size=512,
+                                 num_attention_heads=4, max_position_embeddings=1024))
+        return LlamaForCausalLM(cfg, dev), cfg.vocab_size
+    if name == "gpt":
+        from paddle_amd.models.gpt import GPT_CONFIGS, GPTConfig, GPTForCausalLM
+
+        cfg = GPTConfig(**dict(GPT_CONFIGS["gpt-tiny"], vocab_size=50257, max_position_embeddings=1024))
+        return GPTForCausalLM(cfg, dev), cfg.vocab_size
+    from paddle_amd.models.ernie_moe import ERNIE_MOE_CONFIGS, ErnieMoEConfig, ErnieMoEForCausalLM
+
+    cfg = ErnieMoEConfig(**dict(ERNIE_MOE_CONFIGS["ernie-moe-tiny"], hidden_size=256, moe_intermediate_size=128,
+                                intermediate_size=512, grouped_experts=True, max_position_embeddings=1024))
+    return ErnieMoEForCausalLM(cfg, dev), cfg.vocab_size
+
+
+@pytest.mark.parametrize("name", ["llama", "gpt", "ernie"])
+def test_model_training_step_under_strict_native(name, strict_on):
+    from paddle_amd.autograd import tape
+    from paddle_amd.parallel.sharding import FlatShardedOptimizer
+    from paddle_amd.utils import strict
+
+    torch.manual_seed(0)
+    m, V = _model(name)
+    opt = FlatShardedOptimizer(m.named_parameters(), lr=1e-4, grad_dtype=torch.float32)
+    ids = torch.randint(0, V, (2, 257), device="cuda")
+    losses = []
+    strict.reset()
+    for _ in range(3):
+        with strict.region(f"{name}:step"):
+            with tape.recording() as t:
+                loss = m(ids[:, :-1], ids[:, 1:])
+            t.backward(loss)
+            opt.step()
+            opt.zero_grad()
+        losses.append(float(loss))
+    torch.cuda.synchronize()
+    rep = strict.report()
+    assert rep["aten_kernels"] == {} and rep["fallbacks"] == {}, rep
+    assert all(np.isfinite(losses)), losses
+
+
+def test_fluid_resnet_native_engine_under_strict_native(strict_on):
+    import paddle_amd.fluid as fluid
+    from native_engine_cases import train
+
+    _, _, _, exe = train("resnet_tiny", fluid.CUDAPlace(0), "native", steps=2)
+    assert exe._native is not None
+    assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+    assert exe._native.host_fallbacks() == {}, exe._native.host_fallbacks()
