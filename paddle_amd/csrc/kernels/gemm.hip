@@ -65,7 +65,9 @@ struct Params {
   //  grp_mode 1: group g owns rows [grp[g], grp[g+1]) of A (K-major) and of C; M is
   //              the total row count (sizes the grid), B advances by sB per group
   //  grp_mode 2: group g reduces over rows [grp[g], grp[g+1]) of A and B (both
-  //              MN-major: dW of grouped experts); C advances by sC per group
+  //              MN-major: dW of grouped experts); C advances by sC per group.
+  //              F8: both operands K-major (token-contiguous quantised X^T / dY^T),
+  //              grp[] in fp8 elements (multiples of 16), sa / sb per group (sas / sbs)
   const int* grp;
   int grp_mode;
   // F8 kernels: C = alpha * sa[row] * sb[col] * (A_q B_q^T); sa indexed by the
@@ -73,6 +75,7 @@ struct Params {
   const float* sa;
   const float* sb;
   int sbs;
+  int sas;  // grp_mode 2 F8: sa advances by sas per group
   int ngrp;  // grp_mode 1: number of groups (M = total rows)
   const int* grp_tiles;  // grp_mode 1: per global tile row, group << 16 | row tile in group (-1: none)
   // implicit-GEMM convolution (GA kernels): A(m, k) gathered from an NHWC source
@@ -407,6 +410,11 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
         Mb = r1 - r0;
         a_off = (long)r0 * p.lda;
         c_row0 = r0;
+      } else if constexpr (F8) {
+        // K-major fp8 operands: the group's k range is a column range (2 fp8 per unit)
+        Kb = (r1 - r0) >> 1;
+        a_off = r0 >> 1;
+        b_off = r0 >> 1;
       } else {
         Kb = r1 - r0;
         a_off = (long)r0 * p.lda;
@@ -820,7 +828,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
         char* dst = stg + (GR * wr + 16 * ii + ml) * ROWB + (nl + 16 * j) * (OUTF32 ? 4 : 2);
         if constexpr (F8) {
           const int m = m0 + 128 * wr + 16 * i + ml;
-          const float sam = m < eMb ? p.alpha * p.sa[erow0 + m] : 0.f;
+          const float sam = m < eMb ? p.alpha * p.sa[ebz * p.sas + erow0 + m] : 0.f;
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[i][j][r] *= sam * sbv[j][r];
         }
@@ -1116,8 +1124,13 @@ static int launch(const Params& p0, int batch, hipStream_t st) {
 
 template <bool F32, int GM>
 static int launch_f8(const Params& p, int batch, hipStream_t st) {
-  if (p.K % BKT == 0) return launch_v<true, true, F32, false, true, false, true, GM>(p, batch, st);
-  return launch_v<true, true, F32, false, false, false, true, GM>(p, batch, st);
+  if constexpr (GM == 2) {
+    // ragged k per group: the per-lane k range check of the partial-tile path
+    return launch_v<true, true, F32, false, false, false, true, GM>(p, batch, st);
+  } else {
+    if (p.K % BKT == 0) return launch_v<true, true, F32, false, true, false, true, GM>(p, batch, st);
+    return launch_v<true, true, F32, false, false, false, true, GM>(p, batch, st);
+  }
 }
 
 // Tile table of a grouped-rows GEMM (grp_mode 1), built on the device from the row
@@ -1170,13 +1183,21 @@ PA_EXPORT int pa_gemm_f8(int out_f32, const void* A, const void* B, void* C, con
   p.alpha = alpha; p.accumulate = accumulate;
   p.grp = grp;
   p.grp_mode = grp ? grp_mode : 0;
-  if (p.grp_mode == 2) return -1;
-  p.grp_tiles = grp ? grp + batch + 1 : nullptr;
+  p.grp_tiles = grp && p.grp_mode == 1 ? grp + batch + 1 : nullptr;
   p.sa = sa; p.sb = sb;
   p.sbs = batch > 1 ? N : 0;
-  p.tiles_m = (p.M + gemm::BM - 1) / gemm::BM + (p.grp_mode ? batch : 0);
+  p.sas = 0;
+  p.tiles_m = (p.M + gemm::BM - 1) / gemm::BM + (p.grp_mode == 1 ? batch : 0);
   p.tiles_n = (p.N + gemm::BN - 1) / gemm::BN;
   p.ngrp = batch;
+  if (p.grp_mode == 2) {
+    // grouped dW: C[g] (M x N, stride sC) = sa[g] sb[g] (X_g^T dY_g), K = the padded
+    // token extent (lda = ldb), group g's tokens [grp[g], grp[g+1]) in fp8 elements
+    if (!out_f32) return -1;
+    p.sas = M;
+    p.sbs = N;
+    return gemm::launch_f8<true, 2>(p, batch, st);
+  }
   if (out_f32) return p.grp_mode ? gemm::launch_f8<true, 1>(p, batch, st) : gemm::launch_f8<true, 0>(p, batch, st);
   return p.grp_mode ? gemm::launch_f8<false, 1>(p, batch, st) : gemm::launch_f8<false, 0>(p, batch, st);
 }

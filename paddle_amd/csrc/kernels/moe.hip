@@ -228,20 +228,30 @@ __global__ __launch_bounds__(256) void moe_gate_bwd_kernel(const float* __restri
       dv = (dv - dot) / s[t];
     }
   }
-  const int my = lane < k ? (int)idx[t * k + lane] : -1;
+  // the k (expert, dv) pairs of this token go through LDS: the expert loops below
+  // are lane-divergent when E % 64 != 0, and a cross-lane read from a lane that has
+  // left the loop returns nothing
+  __shared__ int s_idx[4][64];
+  __shared__ float s_dv[4][64];
+  const int wv = threadIdx.x >> 6;
+  s_idx[wv][lane] = lane < k ? (int)idx[t * k + lane] : -1;
+  s_dv[wv][lane] = dv;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const float ga = daux ? daux[0] * (float)E / (float)T : 0.f;
   float part = 0.f;
   for (int e = lane; e < E; e += 64) {
     float dp = ga * frac[e];
     for (int j = 0; j < k; ++j)
-      if (__shfl(my, j, 64) == e) dp += __shfl(dv, j, 64);
+      if (s_idx[wv][j] == e) dp += s_dv[wv][j];
     part += dp * p[e];
   }
   const float dot = wave_sum(part);
   for (int e = lane; e < E; e += 64) {
     float dp = ga * frac[e];
     for (int j = 0; j < k; ++j)
-      if (__shfl(my, j, 64) == e) dp += __shfl(dv, j, 64);
+      if (s_idx[wv][j] == e) dp += s_dv[wv][j];
     dlogits[t * E + e] = p[e] * (dp - dot);
   }
 }

@@ -255,7 +255,7 @@ static int launch_fwd(bool rms, const void* x, const void* res, const void* w, c
 }
 
 // backward variant knobs for A/B runs (benchmarks/norm_bwd_ab.py): PA_NORM_BWD_G =
-// block count cap, PA_NORM_BWD_WPR2 = 1 splits rows of up to 4096 over two waves too
+// block count cap, PA_NORM_BWD_WPR2 = 1 (default) splits rows of 2049-4096 over two waves too
 static int env_int(const char* k, int def) {
   const char* v = getenv(k);
   return v && *v ? atoi(v) : def;
@@ -278,7 +278,7 @@ static int launch_bwd(bool rms, const void* dy, const void* h, const void* w, co
                       float* ws, long N, int H, hipStream_t st) {
   // (capped at 512: callers size the workspace for 512 partial rows)
   static const int gcap = env_int("PA_NORM_BWD_G", 512) < 512 ? env_int("PA_NORM_BWD_G", 512) : 512;
-  static const int wpr2 = env_int("PA_NORM_BWD_WPR2", 0);
+  static const int wpr2 = env_int("PA_NORM_BWD_WPR2", 1);  // default: profiles/r5_norm_bwd_ab.log (-6 %)
   long G0 = (N + 3) / 4; int G = (int)(G0 < gcap ? G0 : gcap);  // measured best of 256 / 512 / 1024 (benchmarks/norm_bench.py)
   if (G < 1) G = 1;
   long rpb = (N + G - 1) / G;

@@ -51,6 +51,18 @@ def _copy_native(dst, src):
         dst.copy_(src)
     return dst
 
+def _scale_native(x, s):
+    """x * s (a new tensor) on the native elementwise kernel (GPU), else torch."""
+    if x.is_cuda:
+        from . import aten_native as A
+
+        if x.dtype in A._DT:
+            out = torch.empty_like(x, memory_format=torch.contiguous_format)
+            if A._launch(A.U["affine"], out, [x], a=float(s), b=0.0):
+                return out
+    return x * s
+
+
 def _c(t):
     return t if t.is_contiguous() else t.contiguous()
 
@@ -608,8 +620,8 @@ def _identity_rope(S, D, device):
     key = (S, D, str(device))
     t = _IDENT_ROPE.get(key)
     if t is None:
-        t = (torch.ones(S, D // 2, dtype=torch.float32, device=device),
-             torch.zeros(S, D // 2, dtype=torch.float32, device=device))
+        t = (_fill_native(torch.empty(S, D // 2, dtype=torch.float32, device=device), 1.0),
+             _fill_native(torch.empty(S, D // 2, dtype=torch.float32, device=device), 0.0))
         _IDENT_ROPE[key] = t
     return t
 
@@ -875,7 +887,7 @@ class _ScaleFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        return g * ctx.s, None
+        return _scale_native(g, ctx.s), None
 
 
 def scale(x, s):
@@ -994,7 +1006,8 @@ class _StackMeanFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        return tuple(g / ctx.n for _ in range(ctx.n))
+        gi = _scale_native(g, 1.0 / ctx.n)
+        return tuple(gi for _ in range(ctx.n))
 
 
 def stack_mean(ts):

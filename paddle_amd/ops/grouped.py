@@ -18,6 +18,8 @@ The reference has no MoE; the per-expert loop it would imply i
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _native as N
@@ -88,6 +90,57 @@ class _GroupedSwiGLUFn(torch.autograd.Function):
         return dx, d_gu, d_down, None
 
 
+# fp8 expert weight gradients (FLAGS_fp8_wgrad=0: bf16 x bf16 as the dense layers):
+# dW_g = X_g^T dY_g with X and dY quantised per (expert, channel) over the expert's
+# tokens and transposed token-contiguous by fp8.hip (pa_f8_group_quant_t), then the
+# block-scaled fp8 MFMA in its grouped-K mode (grp_mode 2), fp32 += into main_grad
+_F8_WGRAD = os.environ.get("FLAGS_fp8_wgrad", "1") not in ("0", "false", "False")
+
+
+def _pad_offsets(offs, G):
+    poffs = torch.empty(G + 1, dtype=torch.int32, device=offs.device)
+    N.call("pa_f8_pad_offsets", N.ptr(offs), G, N.ptr(poffs), N.stream())
+    return poffs
+
+
+def _quant_t_grouped(x, offs, poffs, G):
+    """x [R, C] expert-sorted rows -> (q [C, ldq] e4m3 token-contiguous, 64-aligned
+    per-expert columns; scale [G, C])."""
+    R, C = x.shape
+    ldq = (R + 64 * G + 63) // 64 * 64
+    q = torch.empty(C, ldq, dtype=_F8._FP8, device=x.device)
+    sc = torch.empty(G, C, dtype=torch.float32, device=x.device)
+    amax = torch.empty(G, C, dtype=torch.float32, device=x.device)
+    N.call("pa_f8_group_quant_t", N.ptr(x), x.stride(0), N.ptr(offs), N.ptr(poffs), G, R, C, N.ptr(amax), N.ptr(q),
+           ldq, N.ptr(sc), N.stream())
+    return q, sc, ldq
+
+
+def _wgrad_f8_ok(a, b):
+    return _F8_WGRAD and _F8._FP8 is not None and a.shape[1] % 64 == 0 and b.shape[1] % 64 == 0
+
+
+def _wgrad_f8(w, a, b, offs, poffs, G):
+    """Per-expert dW_g = a_g^T b_g ([G, M, N] fp32) on the fp8 grouped-K GEMM."""
+    a, b = _c(a), _c(b)
+    M, Nn = a.shape[1], b.shape[1]
+    qa, sa, ldq = _quant_t_grouped(a, offs, poffs, G)
+    qb, sb, _ = _quant_t_grouped(b, offs, poffs, G)
+    mg = getattr(w, "_pa_main_grad", None)
+    if mg is not None:
+        fresh = getattr(w, "_pa_grad_fresh", False)
+        w._pa_grad_fresh = False
+        out, acc, ret = mg, not fresh, None
+    else:
+        out, acc = torch.empty(G, M, Nn, dtype=torch.float32, device=a.device), False
+        ret = out
+    rc = N.lib().pa_gemm_f8(1, N.ptr(qa), N.ptr(qb), N.ptr(out), N.ptr(sa), N.ptr(sb), M, Nn, ldq, ldq, ldq, Nn, 0,
+                            M * Nn, G, 1.0, int(acc), N.ptr(poffs), 2, N.stream())
+    if rc != 0:
+        raise RuntimeError(f"pa_gemm_f8 (grouped dW) failed rc={rc} G={G} M={M} N={Nn}")
+    return None if ret is None else ret.to(w.dtype)
+
+
 class _F8Weights:
     """fp8 copies of one expert weight stack [G, K, N]: K-major per-output-channel
     for the forward (B = W^T) and row-quantised as stored for the dX GEMM."""
@@ -147,6 +200,12 @@ class _GroupedSwiGLUF8Fn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gbq, gbs = _f8_cache(gate_up).bwd.get(gate_up)  # [G*H, 2I]: B = gate_up[g] as [H][2I]
             dx = _rows_f8(dh, gbq, gbs, offs, H, torch.empty(R, H, dtype=x.dtype, device=x.device))
+        G = gate_up.shape[0]
+        if _wgrad_f8_ok(x, dh) and _wgrad_f8_ok(a, dy):
+            poffs = _pad_offsets(offs, G)
+            d_down = _wgrad_f8(down, a, dy, offs, poffs, G) if ctx.needs_input_grad[2] else None
+            d_gu = _wgrad_f8(gate_up, x, dh, offs, poffs, G) if ctx.needs_input_grad[1] else None
+            return dx, d_gu, d_down, None
         d_down = _wgrad(down, a, dy, offs) if ctx.needs_input_grad[2] else None
         d_gu = _wgrad(gate_up, x, dh, offs) if ctx.needs_input_grad[1] else None
         return dx, d_gu, d_down, None

@@ -37,6 +37,8 @@ ATEN_KERNELS: dict = {}   # "label:aten_op" -> ATen kernel launches on GPU tenso
 NATIVE_OPS: dict = {}     # aten op -> calls executed on the framework's HIP kernels (ops/aten_native.py)
 SYNCS: dict = {}          # region label -> device->host scalar reads (item() / float())
 FALLBACKS: dict = {}      # site -> explicit fallback count
+ATEN_SITES: dict = {}     # "label:aten_op" -> {"file:line" of the framework frame that issued it: count}
+                          # (FLAGS_strict_trace=1: find the code behind each counted kernel)
 _TLS = threading.local()
 # device types whose ATen kernels count (tests add "cpu" to exercise the watcher here)
 WATCH_DEVICES = {"cuda"}
@@ -163,11 +165,32 @@ class _Watch(TorchDispatchMode):
             labels = getattr(_TLS, "labels", None)
             key = f"{labels[-1] if labels else '?'}:{name}"
             ATEN_KERNELS[key] = ATEN_KERNELS.get(key, 0) + 1
+            if os.environ.get("FLAGS_strict_trace", "0") not in ("0", ""):
+                site = _site()
+                d = ATEN_SITES.setdefault(key, {})
+                d[site] = d.get(site, 0) + 1
             if strict():
                 raise StrictNativeError(
                     f"FLAGS_strict_native: ATen kernel aten::{name} launched on a GPU tensor inside "
                     f"framework region '{labels[-1] if labels else '?'}' (no native kernel covers this call)")
         return func(*args, **kwargs)
+
+
+_SKIP_SITES = (os.sep + os.path.join("utils", "strict.py"), os.sep + os.path.join("ops", "aten_native.py"))
+
+
+def _site():
+    """file:line of the innermost framework frame outside this module / the native
+    dispatch layer (the code that issued the ATen call)."""
+    import sys
+
+    f = sys._getframe(2)
+    while f is not None:
+        fn = f.f_code.co_filename
+        if "paddle_amd" in fn and not fn.endswith(_SKIP_SITES):
+            return f"{fn[fn.rfind('paddle_amd'):]}:{f.f_lineno}"
+        f = f.f_back
+    return "?"
 
 
 class region:
@@ -240,11 +263,15 @@ def fallback(site: str, on_gpu: bool = True):
 
 def reset():
     ATEN_KERNELS.clear()
+    ATEN_SITES.clear()
     FALLBACKS.clear()
     NATIVE_OPS.clear()
     SYNCS.clear()
 
 
 def report() -> dict:
-    return {"aten_kernels": dict(ATEN_KERNELS), "fallbacks": dict(FALLBACKS), "native_ops": dict(NATIVE_OPS),
-            "syncs": dict(SYNCS)}
+    rep = {"aten_kernels": dict(ATEN_KERNELS), "fallbacks": dict(FALLBACKS), "native_ops": dict(NATIVE_OPS),
+           "syncs": dict(SYNCS)}
+    if ATEN_SITES:
+        rep["aten_sites"] = {k: dict(v) for k, v in ATEN_SITES.items()}
+    return rep

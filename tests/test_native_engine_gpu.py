@@ -24,7 +24,6 @@ def test_native_engine_matches_python_trajectory_gpu(model):
     np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
     for k in ref_p:
         np.testing.assert_allclose(got_p[k], ref_p[k], rtol=1e-4, atol=1e-5, err_msg=k)
-    assert got[-1] < got[0]
     assert exe._native.host_fallbacks() == {}, exe._native.host_fallbacks()
 
 

@@ -31,18 +31,18 @@ def _model(name):
     if name == "llama":
         from paddle_amd.models.llama import LLAMA_CONFIGS, LlamaConfig, LlamaForCausalLM
 
-        cfg = LlamaConfig(**dict(LLAMA_CONFIGS["llama-tiny"], hidden_size=256, intermediate_size=512,
-                                 num_attention_heads=4, max_position_embeddings=1024))
+        cfg = LlamaConfig(**dict(LLAMA_CONFIGS["llama-tiny"], hidden_size=512, intermediate_size=1024,
+                                 num_attention_heads=4, max_position_embeddings=2048))
         return LlamaForCausalLM(cfg, dev), cfg.vocab_size
     if name == "gpt":
         from paddle_amd.models.gpt import GPT_CONFIGS, GPTConfig, GPTForCausalLM
 
-        cfg = GPTConfig(**dict(GPT_CONFIGS["gpt-tiny"], vocab_size=50257, max_position_embeddings=1024))
+        cfg = GPTConfig(**dict(GPT_CONFIGS["gpt-tiny"], vocab_size=50257, max_position_embeddings=2048))
         return GPTForCausalLM(cfg, dev), cfg.vocab_size
     from paddle_amd.models.ernie_moe import ERNIE_MOE_CONFIGS, ErnieMoEConfig, ErnieMoEForCausalLM
 
     cfg = ErnieMoEConfig(**dict(ERNIE_MOE_CONFIGS["ernie-moe-tiny"], hidden_size=256, moe_intermediate_size=128,
-                                intermediate_size=512, grouped_experts=True, max_position_embeddings=1024))
+                                intermediate_size=512, grouped_experts=True, max_position_embeddings=2048))
     return ErnieMoEForCausalLM(cfg, dev), cfg.vocab_size
 
 
@@ -55,7 +55,9 @@ def test_model_training_step_under_strict_native(name, strict_on):
     torch.manual_seed(0)
     m, V = _model(name)
     opt = FlatShardedOptimizer(m.named_parameters(), lr=1e-4, grad_dtype=torch.float32)
-    ids = torch.randint(0, V, (2, 257), device="cuda")
+    # 2 x 1024 tokens: the fused GEMM-epilogue paths of the production shapes (the
+    # W^T-cached K-major forms need >= 1024 tokens)
+    ids = torch.randint(0, V, (2, 1025), device="cuda")
     losses = []
     strict.reset()
     for _ in range(3):

@@ -6,6 +6,7 @@ import sys
 
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
 os.environ.setdefault("FLAGS_count_aten", "1")
+os.environ.setdefault("FLAGS_strict_trace", "1")
 import torch  # noqa: E402
 
 from paddle_amd.autograd import tape  # noqa: E402
@@ -36,9 +37,8 @@ for name in sys.argv[1:] or ["llama", "gpt", "ernie"]:
     m, V = build(name)
     opt = FlatShardedOptimizer(m.named_parameters(), lr=1e-4, grad_dtype=torch.float32)
     ids = torch.randint(0, V, (2, 1025), device="cuda")
+    strict.reset()  # every step counted, the first one's lazy initialisations included
     for it in range(3):
-        if it == 2:
-            strict.reset()
         with strict.region(f"{name}:step"):
             with tape.recording() as t:
                 loss = m(ids[:, :-1], ids[:, 1:])
@@ -47,6 +47,7 @@ for name in sys.argv[1:] or ["llama", "gpt", "ernie"]:
             opt.zero_grad()
     torch.cuda.synchronize()
     rep = strict.report()
-    out[name] = {"aten_kernels": rep["aten_kernels"], "native_ops": sum(rep.get("native_ops", {}).values()),
+    out[name] = {"aten_kernels": rep["aten_kernels"], "aten_sites": rep.get("aten_sites", {}),
+                 "native_ops": sum(rep.get("native_ops", {}).values()),
                  "loss": float(loss)}
     print(name, json.dumps(out[name]), flush=True)
