@@ -326,6 +326,9 @@ PA_EXPORT int pa_f8_group_quant_t(const void* x, long ldx, const int* offs, cons
   if (tiles > 0x7fffffffL || C / 64 > 65535) return -1;
   hipError_t e = hipMemsetAsync(amax, 0, sizeof(float) * (size_t)G * C, st);
   if (e != hipSuccess) return (int)e;
+  // experts without tokens get no tile: their scales stay 0 (the GEMM's 0 * s stays 0)
+  e = hipMemsetAsync(scale, 0, sizeof(float) * (size_t)G * C, st);
+  if (e != hipSuccess) return (int)e;
   dim3 grid((unsigned)tiles, C / 64);
   hipLaunchKernelGGL(pa::f8_group_amax_kernel, grid, dim3(256), 0, st, (const u16*)x, ldx, offs, poffs, G, C, amax);
   hipLaunchKernelGGL(pa::f8_group_quant_t_kernel, grid, dim3(256), 0, st, (const u16*)x, ldx, offs, poffs, G, C,
