@@ -1761,3 +1761,39 @@ PA_EXPORT int pa_fa_dq_reduce_rope(const float* part, int nkb, int B, int Sq, in
                        out_ts, cosT, sinT, kblk);
   PA_LAUNCH_CHECK();
 }
+
+// GQA backward fold: the backward kernels write dK / dV per QUERY head
+// ([B, S, Hq, D] contiguous); the kv head kh receives the sum over its `ratio` query
+// heads, stored into a strided destination (the packed dqkv's k / v slot, rows
+// `dst_ss` elements apart).  grid.y = 0: dK, 1: dV.  fp32 sums, one bf16 rounding.
+namespace pa {
+__global__ __launch_bounds__(256) void fa_gqa_fold_kernel(const u16* __restrict__ dk_e, const u16* __restrict__ dv_e,
+                                                          u16* __restrict__ dk, u16* __restrict__ dv, long rows,
+                                                          int Hq, int Hk, int D, long dst_ss) {
+  const int ratio = Hq / Hk, nc = D / 8;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= rows * Hk * nc) return;
+  const int c = (int)(idx % nc);
+  const int kh = (int)((idx / nc) % Hk);
+  const long row = idx / nc / Hk;
+  const u16* src = blockIdx.y ? dv_e : dk_e;
+  u16* dst = blockIdx.y ? dv : dk;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int r = 0; r < ratio; ++r) {
+    float v[8];
+    load8(src + ((row * Hq + (long)kh * ratio + r) * D + 8 * c), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += v[e];
+  }
+  store8(dst + row * dst_ss + (long)kh * D + 8 * c, acc);
+}
+}  // namespace pa
+
+PA_EXPORT int pa_fa_gqa_fold(const void* dk_e, const void* dv_e, void* dk, void* dv, long rows, int Hq, int Hk,
+                             int D, long dst_ss, hipStream_t st) {
+  if (Hk <= 0 || Hq % Hk || D % 8 || dst_ss % 8 || rows <= 0) return -1;
+  const long n = rows * Hk * (D / 8);
+  hipLaunchKernelGGL(pa::fa_gqa_fold_kernel, dim3((unsigned)((n + 255) / 256), 2), dim3(256), 0, st,
+                     (const u16*)dk_e, (const u16*)dv_e, (u16*)dk, (u16*)dv, rows, Hq, Hk, D, dst_ss);
+  PA_LAUNCH_CHECK();
+}

@@ -482,8 +482,10 @@ def _rope_attn_backward(packed, o, lse, cos, sin, do, Hq, Hk, D, causal, scale):
         dk_e = torch.empty(B, S, Hq, D, dtype=packed.dtype, device=packed.device)
         dv_e = torch.empty_like(dk_e)
         dq_acc = _fa_bwd(q, k, v, o, do, lse, causal, scale, dk_e, dv_e, rope_out)
-        d4[:, :, Hq:Hq + Hk] = dk_e.view(B, S, Hk, Hq // Hk, D).sum(3)
-        d4[:, :, Hq + Hk:] = dv_e.view(B, S, Hk, Hq // Hk, D).sum(3)
+        # fold the per-query-head dK / dV over each kv head's group straight into
+        # dqkv's k / v slots (one fp32-summing pass)
+        N.call("pa_fa_gqa_fold", N.ptr(dk_e), N.ptr(dv_e), N.ptr(d4[:, :, Hq:Hq + Hk]),
+               N.ptr(d4[:, :, Hq + Hk:]), B * S, Hq, Hk, D, nh * D, N.stream())
     if dq_acc is not None:
         N.call("pa_rope", 0, 1, N.ptr(dq_acc), Hq * D, N.ptr(dqkv), W, N.ptr(cos), N.ptr(sin), None,
                B, S, Hq, Hq, D, 1, N.stream())
