@@ -119,14 +119,16 @@ PA_EXPORT int pa_moe_combine_bwd(const void* dy, const void* ys, const int* pos,
 
 // ---------------------------------------------------------------------------------
 // Routing without a sort: the gate's expert per slot (flat_e [n = T*k]) -> the
-// expert-sorted order of the kept slots, in ONE 1024-thread workgroup.
-//   pass 1  per-expert slot counts (LDS integer atomics: order-free, exact);
-//   scan    row offsets of each expert (thread 0, E <= 1024);
-//   pass 2  slots in chunks of 1024 in slot order: a slot's rank inside its expert =
-//           running base of the expert + earlier lanes of its wave with the same
-//           expert (64 lane reads); the 16 waves of a chunk take and advance the
-//           bases one after another (one barrier each), so within an expert the
-//           order is slot order -- the stable argsort of the torch path, exactly.
+// expert-sorted order of the kept slots: a stable counting sort over blocks of 1024
+// slots, three launches.
+//   count  block b: its slot counts per expert, cnt[b][e] (LDS integer atomics);
+//   scan   one workgroup: per expert the running count over the blocks before b,
+//          run[b][e], and the row offsets of the experts, off[e];
+//   place  block b: a slot's rank inside its expert = run[b][e] + earlier lanes of
+//          its wave with that expert (64 lane reads) + the counts of the earlier
+//          waves of the block (the 16 waves take and advance an LDS base in turn),
+//          so within an expert the order is slot order -- the stable argsort of
+//          the torch path, exactly, with no dependence on atomic arrival order.
 // mode 0: every slot kept, row = off[e] + rank               (outputs pos, src, e_sorted)
 // mode 1: GShard capacity layout, row = e * cap + rank, dropped when rank >= cap
 //         (pos, src [E * cap]; padding rows get token 0)
@@ -137,57 +139,81 @@ namespace pa {
 
 constexpr int kRouteT = 1024;
 
-__global__ __launch_bounds__(kRouteT) void moe_route_kernel(const long* __restrict__ flat_e, long n, int E, int k,
-                                                            int mode, long cap, int* __restrict__ pos,
-                                                            int* __restrict__ src, long* __restrict__ e_sorted,
-                                                            long* __restrict__ counts) {
-  __shared__ int base[1024];  // slot count per expert, then the running rank base
-  __shared__ int off[1024];   // first row of each expert (modes 0 / 2)
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int e = tid; e < E; e += kRouteT) base[e] = 0;
-  if (mode == 1)
-    for (long r = tid; r < (long)E * cap; r += kRouteT) src[r] = 0;
+__global__ __launch_bounds__(kRouteT) void moe_route_count_kernel(const long* __restrict__ flat_e, long n, int E,
+                                                                  int* __restrict__ cnt, int mode, long cap,
+                                                                  int* __restrict__ src) {
+  __shared__ int h[1024];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < E; e += kRouteT) h[e] = 0;
+  if (mode == 1)  // padding rows of the capacity layout read token 0
+    for (long r = (long)blockIdx.x * kRouteT + tid; r < (long)E * cap; r += (long)gridDim.x * kRouteT) src[r] = 0;
   __syncthreads();
-  for (long i = tid; i < n; i += kRouteT) atomicAdd(&base[(int)flat_e[i]], 1);
+  const long i = (long)blockIdx.x * kRouteT + tid;
+  if (i < n) atomicAdd(&h[(int)flat_e[i]], 1);
   __syncthreads();
-  if (tid == 0) {
-    int acc = 0;
-    for (int e = 0; e < E; ++e) {
-      const int kept = mode == 0 ? base[e] : (base[e] < cap ? base[e] : (int)cap);
-      counts[e] = kept;
-      off[e] = acc;
-      acc += kept;
-      base[e] = 0;
+  for (int e = tid; e < E; e += kRouteT) cnt[(long)blockIdx.x * E + e] = h[e];
+}
+
+__global__ __launch_bounds__(kRouteT) void moe_route_scan_kernel(const int* __restrict__ cnt, int nb, int E, int mode,
+                                                                 long cap, int* __restrict__ run,
+                                                                 int* __restrict__ off, long* __restrict__ counts) {
+  __shared__ int sc[1024];
+  const int e = threadIdx.x;
+  int tot = 0;
+  if (e < E)
+    for (int b = 0; b < nb; ++b) {
+      run[(long)b * E + e] = tot;
+      tot += cnt[(long)b * E + e];
     }
+  const int kept = e < E ? (mode == 0 ? tot : (tot < cap ? tot : (int)cap)) : 0;
+  if (e < E) counts[e] = kept;
+  // exclusive scan of kept over the experts (Hillis-Steele in LDS)
+  sc[e] = kept;
+  __syncthreads();
+  for (int o = 1; o < kRouteT; o <<= 1) {
+    const int v = e >= o ? sc[e - o] : 0;
+    __syncthreads();
+    sc[e] += v;
+    __syncthreads();
   }
+  if (e < E) off[e] = sc[e] - kept;
+}
+
+__global__ __launch_bounds__(kRouteT) void moe_route_place_kernel(const long* __restrict__ flat_e, long n, int E,
+                                                                  int k, int mode, long cap,
+                                                                  const int* __restrict__ run,
+                                                                  const int* __restrict__ off, int* __restrict__ pos,
+                                                                  int* __restrict__ src,
+                                                                  long* __restrict__ e_sorted) {
+  __shared__ int base[1024];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int e = tid; e < E; e += kRouteT) base[e] = run[(long)blockIdx.x * E + e];
   __syncthreads();
-  for (long c0 = 0; c0 < n; c0 += kRouteT) {
-    const long i = c0 + tid;
-    const int e = i < n ? (int)flat_e[i] : -1;
-    int r = 0, c = 0;  // rank among / count of this wave's lanes with expert e
-    for (int j = 0; j < 64; ++j) {
-      const int ej = __shfl(e, j, 64);
-      c += ej == e ? 1 : 0;
-      r += (j < lane && ej == e) ? 1 : 0;
+  const long i = (long)blockIdx.x * kRouteT + tid;
+  const int e = i < n ? (int)flat_e[i] : -1;
+  int r = 0, c = 0;  // rank among / count of this wave's lanes with expert e
+  for (int j = 0; j < 64; ++j) {
+    const int ej = __shfl(e, j, 64);
+    c += ej == e ? 1 : 0;
+    r += (j < lane && ej == e) ? 1 : 0;
+  }
+  int rank = 0;
+  for (int ww = 0; ww < kRouteT / 64; ++ww) {
+    if (w == ww && e >= 0) {
+      rank = base[e] + r;                  // every lane of the wave reads before ...
+      if (r == c - 1) base[e] = rank + 1;  // ... the group's last lane advances the base
     }
-    int rank = 0;
-    for (int ww = 0; ww < kRouteT / 64; ++ww) {
-      if (w == ww && e >= 0) {
-        rank = base[e] + r;            // every lane of the wave reads before ...
-        if (r == c - 1) base[e] = rank + 1;  // ... the group's last lane advances the base
-      }
-      __syncthreads();
+    __syncthreads();
+  }
+  if (e >= 0) {
+    const bool keep = mode == 0 || rank < cap;
+    int row = -1;
+    if (keep) {
+      row = mode == 1 ? (int)(e * cap + rank) : off[e] + rank;
+      src[row] = (int)(i / k);
+      if (mode != 1) e_sorted[row] = e;
     }
-    if (e >= 0) {
-      const bool keep = mode == 0 || rank < cap;
-      int row = -1;
-      if (keep) {
-        row = mode == 1 ? (int)(e * cap + rank) : off[e] + rank;
-        src[row] = (int)(i / k);
-        if (mode != 1) e_sorted[row] = e;
-      }
-      pos[i] = row;
-    }
+    pos[i] = row;
   }
 }
 
@@ -260,13 +286,29 @@ __global__ __launch_bounds__(256) void moe_gate_bwd_kernel(const float* __restri
 
 using namespace pa;
 
+// ws: int workspace of pa_moe_route_ws(n, E) elements
+PA_EXPORT long pa_moe_route_ws(long n, int E) {
+  const long nb = (n + kRouteT - 1) / kRouteT;
+  return 2 * nb * E + E;
+}
+
 PA_EXPORT int pa_moe_route(const long* flat_e, long n, int E, int k, int mode, long cap, int* pos, int* src,
-                           long* e_sorted, long* counts, hipStream_t st) {
-  if (E <= 0 || E > 1024 || k <= 0 || mode < 0 || mode > 2 || (mode != 0 && cap < 0)) return -1;
+                           long* e_sorted, long* counts, int* ws, hipStream_t st) {
+  if (E <= 0 || E > 1024 || k <= 0 || mode < 0 || mode > 2 || (mode != 0 && cap < 0) || !ws) return -1;
   if (mode != 0 && (long)E * cap > 0x7fffffffL) return -1;
   if (mode != 1 && !e_sorted) return -1;
-  hipLaunchKernelGGL(moe_route_kernel, dim3(1), dim3(kRouteT), 0, st, flat_e, n, E, k, mode, cap, pos, src,
-                     e_sorted, counts);
+  if (n <= 0) return -1;
+  const long nb = (n + kRouteT - 1) / kRouteT;
+  if (nb > 0x7fffffffL / E) return -1;
+  int* cnt = ws;
+  int* run = ws + nb * E;
+  int* off = run + nb * E;
+  hipLaunchKernelGGL(moe_route_count_kernel, dim3((unsigned)nb), dim3(kRouteT), 0, st, flat_e, n, E, cnt, mode, cap,
+                     src);
+  hipLaunchKernelGGL(moe_route_scan_kernel, dim3(1), dim3(kRouteT), 0, st, (const int*)cnt, (int)nb, E, mode, cap,
+                     run, off, counts);
+  hipLaunchKernelGGL(moe_route_place_kernel, dim3((unsigned)nb), dim3(kRouteT), 0, st, flat_e, n, E, k, mode, cap,
+                     (const int*)run, (const int*)off, pos, src, e_sorted);
   PA_LAUNCH_CHECK();
 }
 

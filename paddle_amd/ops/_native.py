@@ -191,7 +191,7 @@ _SIGS = {
     "pa_f8_group_quant_t": [_P, _L, _P, _P, _I, _L, _I, _P, _P, _L, _P, _P],
     "pa_moe_reduce": [_P, _P, _P, _P, _L, _I, _I, _P],
     "pa_moe_combine_bwd": [_P, _P, _P, _P, _P, _P, _L, _I, _I, _P],
-    "pa_moe_route": [_P, _L, _I, _I, _I, _L, _P, _P, _P, _P, _P],
+    "pa_moe_route": [_P, _L, _I, _I, _I, _L, _P, _P, _P, _P, _P, _P],
     "pa_moe_frac": [_P, _L, _I, _I, _P, _P],
     "pa_moe_gate_bwd": [_P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _P, _P],
     "pa_sgemm": [_P, _L, _L, _P, _L, _L, _P, _L, _L, _L, _L, _I, _I, _L, _L, _L, _L, _L, _L, _I, _L, _L, _P, _L, _F,

@@ -90,11 +90,14 @@ class _GroupedSwiGLUFn(torch.autograd.Function):
         return dx, d_gu, d_down, None
 
 
-# fp8 expert weight gradients (FLAGS_fp8_wgrad=0: bf16 x bf16 as the dense layers):
-# dW_g = X_g^T dY_g with X and dY quantised per (expert, channel) over the expert's
-# tokens and transposed token-contiguous by fp8.hip (pa_f8_group_quant_t), then the
-# block-scaled fp8 MFMA in its grouped-K mode (grp_mode 2), fp32 += into main_grad
-_F8_WGRAD = os.environ.get("FLAGS_fp8_wgrad", "1") not in ("0", "false", "False")
+# fp8 expert weight gradients (FLAGS_fp8_wgrad=1; default bf16 x bf16 as the dense
+# layers): dW_g = X_g^T dY_g with X and dY quantised per (expert, channel) over the
+# expert's tokens and transposed token-contiguous by fp8.hip (pa_f8_group_quant_t),
+# then the block-scaled fp8 MFMA in its grouped-K mode (grp_mode 2), fp32 += into
+# main_grad.  Measured no faster per micro-batch (profiles/r5_moe_fp8_wgrad_NEGATIVE.md):
+# at ~1.5k tokens per expert the tile time is the fp32 main_grad read-modify-write
+# of the epilogue, not the MFMA loop.
+_F8_WGRAD = os.environ.get("FLAGS_fp8_wgrad", "0") not in ("0", "false", "False")
 
 
 def _pad_offsets(offs, G):

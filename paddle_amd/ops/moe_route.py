@@ -36,7 +36,14 @@ def routing(flat_e, T, k, keep=None):
 
 
 def _route_native_ok(flat_e, E):
-    return flat_e.is_cuda and flat_e.dtype == torch.int64 and 0 < E <= 1024
+    return flat_e.is_cuda and flat_e.dtype == torch.int64 and 0 < E <= 1024 and flat_e.numel() > 0
+
+
+def _route_ws(n, E, device):
+    """int32 workspace of pa_moe_route: per 1024-slot block the expert counts and
+    running bases, plus the expert row offsets."""
+    nb = (n + 1023) // 1024
+    return torch.empty(2 * nb * E + E, dtype=torch.int32, device=device)
 
 
 def _rank_in_expert(flat_e):
@@ -64,8 +71,9 @@ def route(flat_e, T, k, E, cap=None):
         src = torch.empty(n, dtype=torch.int32, device=dev)
         e_sorted = torch.empty(n, dtype=torch.int64, device=dev)
         counts = torch.empty(E, dtype=torch.int64, device=dev)
+        ws = _route_ws(n, E, dev)
         N.call("pa_moe_route", N.ptr(flat_e), n, E, k, 0 if cap is None else 2, -1 if cap is None else int(cap),
-               N.ptr(pos), N.ptr(src), N.ptr(e_sorted), N.ptr(counts), N.stream())
+               N.ptr(pos), N.ptr(src), N.ptr(e_sorted), N.ptr(counts), N.ptr(ws), N.stream())
         if cap is not None:
             R = int(counts.sum())
             src, e_sorted = src[:R], e_sorted[:R]
@@ -163,8 +171,9 @@ def capacity_routing(flat_e, T, k, E, cap):
         pos = torch.empty(T * k, dtype=torch.int32, device=dev)
         src = torch.empty(E * cap, dtype=torch.int32, device=dev)  # the kernel zero-fills padding rows
         counts = torch.empty(E, dtype=torch.int64, device=dev)
+        ws = _route_ws(T * k, E, dev)
         N.call("pa_moe_route", N.ptr(flat_e), T * k, E, k, 1, int(cap), N.ptr(pos), N.ptr(src), None, N.ptr(counts),
-               N.stream())
+               N.ptr(ws), N.stream())
         return src, pos
     rank = _rank_in_expert(flat_e)
     keep = rank < cap
