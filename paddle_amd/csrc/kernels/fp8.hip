@@ -196,32 +196,47 @@ PA_EXPORT int pa_quant_cols_t_f8(const void* w, void* qt, float* scale, int G, i
 }
 
 // ---------------------------------------------------------------------------------
-// Grouped expert dW in fp8 (gemm.hip grp_mode 2, F8): dW_g = X_g^T dY_g needs both
-// operands K-major over the TOKENS, i.e. the expert-sorted rows transposed.  Each
-// expert's token range [offs[g], offs[g+1]) is placed at a 64-aligned column
-// poffs[g] of the transposed image q [C][ldq] (zero-filled up to the next multiple
-// of 64), so every K-major 16-B load of the GEMM is aligned and the padding adds 0.
-// Scales are per (expert, channel): s[g, c] = amax over the expert's tokens / 448.
+// Grouped expert dW images (gemm.hip grp_mode 2 with K-major operands): dW_g =
+// X_g^T dY_g needs both operands K-major over the TOKENS, i.e. the expert-sorted rows
+// transposed.  Each expert's tokens -- gathered over up to 8 micro-batches, whose
+// rows [offs_j[g], offs_j[g+1]) are concatenated in micro-batch order -- are placed
+// at a 64-aligned column poffs[g] of the transposed image q [C][ldq] (zero-filled up
+// to the next multiple of 64), so every K-major 16-B load of the GEMM is aligned and
+// the padding adds 0.  One GEMM then reduces an expert over all micro-batches of a
+// step (one fp32 main_grad write instead of a read-modify-write per micro-batch).
+// fp8 images: s[g, c] = amax over the expert's tokens / 448, q = x / s (e4m3);
+// bf16 images: a plain transposed copy.
 namespace pa {
 
 constexpr int kGT = 64;  // tokens per tile (and the padding granule)
+constexpr int kMaxMb = 8;
 
-__global__ __launch_bounds__(1024) void f8_pad_offsets_kernel(const int* __restrict__ offs, int G,
-                                                              int* __restrict__ poffs) {
-  // serial over G <= 32768 groups in one thread: G is the expert count (<= 1024 here)
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int g = 0; g < G; ++g) {
-      poffs[g] = acc;
-      const int n = offs[g + 1] - offs[g];
-      acc += (n + kGT - 1) / kGT * kGT;
+struct MbSrc {
+  const u16* x[kMaxMb];
+  long ldx[kMaxMb];
+  const int* offs[kMaxMb];
+  int n;
+};
+
+// cum[j * G + g] = tokens of expert g in micro-batches < j (j = 0..n); poffs [G+1]
+__global__ void group_cat_offsets_kernel(MbSrc src, int G, int* __restrict__ cum, int* __restrict__ poffs) {
+  if (threadIdx.x != 0) return;
+  int acc = 0;
+  for (int g = 0; g < G; ++g) {
+    int c = 0;
+    for (int j = 0; j < src.n; ++j) {
+      cum[j * G + g] = c;
+      c += src.offs[j][g + 1] - src.offs[j][g];
     }
-    poffs[G] = acc;
+    cum[src.n * G + g] = c;
+    poffs[g] = acc;
+    acc += (c + kGT - 1) / kGT * kGT;
   }
+  poffs[G] = acc;
 }
 
 // group of padded token column pt (binary search over poffs); -1 past the end
-__device__ __forceinline__ int f8_group_of(const int* __restrict__ poffs, int G, long pt) {
+__device__ __forceinline__ int group_of(const int* __restrict__ poffs, int G, long pt) {
   if (pt >= poffs[G]) return -1;
   int lo = 0, hi = G - 1;
   while (lo < hi) {
@@ -231,24 +246,31 @@ __device__ __forceinline__ int f8_group_of(const int* __restrict__ poffs, int G,
   return lo;
 }
 
-// amax[g, c] = max |x[r, c]| over the expert's rows (amax zero-filled by the host);
-// grid (token tiles of the padded extent, C / 64), 256 threads: 8 channels per thread
-__global__ __launch_bounds__(256) void f8_group_amax_kernel(const u16* __restrict__ x, long ldx,
-                                                            const int* __restrict__ offs,
-                                                            const int* __restrict__ poffs, int G, int C,
-                                                            float* __restrict__ amax) {
+// source row of token t of expert g (t < total): micro-batch j and its row
+__device__ __forceinline__ const u16* token_row(const MbSrc& src, const int* __restrict__ cum, int G, int g, int t) {
+  int j = 0;
+  while (j + 1 < src.n && t >= cum[(j + 1) * G + g]) ++j;
+  const long r = src.offs[j][g] + (t - cum[j * G + g]);
+  return src.x[j] + r * src.ldx[j];
+}
+
+// amax[g, c] = max |x[token, c]| over the expert's tokens (amax zero-filled by the
+// host); grid (token tiles of the padded extent, C / 64), 256 threads: 8 channels
+// per thread
+__global__ __launch_bounds__(256) void group_amax_kernel(MbSrc src, const int* __restrict__ cum,
+                                                         const int* __restrict__ poffs, int G, int C,
+                                                         float* __restrict__ amax) {
   const long pt = (long)blockIdx.x * kGT;
-  const int g = f8_group_of(poffs, G, pt);
+  const int g = group_of(poffs, G, pt);
   if (g < 0) return;  // block-uniform
-  const long r0 = offs[g] + (pt - poffs[g]);
-  const long r1 = offs[g + 1];
+  const int t0 = (int)(pt - poffs[g]), tot = cum[src.n * G + g];
   const int c0 = blockIdx.y * 64;
   const int tc = threadIdx.x & 7, tr = threadIdx.x >> 3;  // 8 channel chunks x 32 rows
   float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int i = tr; i < kGT; i += 32) {
-    const long r = r0 + i;
-    if (r < r1) {
-      const u16x8 v = *reinterpret_cast<const u16x8*>(x + r * ldx + c0 + 8 * tc);
+    const int t = t0 + i;
+    if (t < tot) {
+      const u16x8 v = *reinterpret_cast<const u16x8*>(token_row(src, cum, G, g, t) + c0 + 8 * tc);
 #pragma unroll
       for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], fabsf(bf2f(v[e])));
     }
@@ -265,73 +287,110 @@ __global__ __launch_bounds__(256) void f8_group_amax_kernel(const u16* __restric
   }
 }
 
-// q[c, poffs[g] + j] = x[offs[g] + j, c] / s[g, c] for the expert's tokens, 0 in its
-// padding; s[g, c] written alongside.  grid as f8_group_amax_kernel.
-__global__ __launch_bounds__(256) void f8_group_quant_t_kernel(const u16* __restrict__ x, long ldx,
-                                                               const int* __restrict__ offs,
-                                                               const int* __restrict__ poffs, int G, int C,
-                                                               const float* __restrict__ amax,
-                                                               uint8_t* __restrict__ q, long ldq,
-                                                               float* __restrict__ scale) {
+// q[c, poffs[g] + t] = x[token t of g, c] (/ s[g, c] for fp8) for the expert's
+// tokens, 0 in its padding; fp8: s[g, c] written alongside.  grid as above.
+template <bool QUANT>
+__global__ __launch_bounds__(256) void group_image_kernel(MbSrc src, const int* __restrict__ cum,
+                                                          const int* __restrict__ poffs, int G, int C,
+                                                          const float* __restrict__ amax, void* __restrict__ qv,
+                                                          long ldq, float* __restrict__ scale) {
   const long pt = (long)blockIdx.x * kGT;
-  const int g = f8_group_of(poffs, G, pt);
+  const int g = group_of(poffs, G, pt);
   if (g < 0) return;
-  const long r0 = offs[g] + (pt - poffs[g]);
-  const long r1 = offs[g + 1];
+  const int t0 = (int)(pt - poffs[g]), tot = cum[src.n * G + g];
   const int c0 = blockIdx.y * 64;
   __shared__ u16 tile[kGT][64 + 8];  // [token][channel], rows padded against bank conflicts
   {
     const int tc = threadIdx.x & 7, tr = threadIdx.x >> 3;
     for (int i = tr; i < kGT; i += 32) {
-      const long r = r0 + i;
+      const int t = t0 + i;
       u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (r < r1) v = *reinterpret_cast<const u16x8*>(x + r * ldx + c0 + 8 * tc);
+      if (t < tot) v = *reinterpret_cast<const u16x8*>(token_row(src, cum, G, g, t) + c0 + 8 * tc);
 #pragma unroll
       for (int e = 0; e < 8; ++e) tile[i][8 * tc + e] = v[e];
     }
   }
   __syncthreads();
   const int c = threadIdx.x >> 2, j0 = (threadIdx.x & 3) * 16;  // one channel, 16 tokens
-  const float am = amax[(long)g * C + c0 + c];
-  const float s = am > 0.f ? am / kE4M3Max : 1.f;
-  const float inv = 1.f / s;
-  if ((threadIdx.x & 3) == 0) scale[(long)g * C + c0 + c] = s;
-  float f[16];
+  if constexpr (QUANT) {
+    const float am = amax[(long)g * C + c0 + c];
+    const float sc = am > 0.f ? am / kE4M3Max : 1.f;
+    const float inv = 1.f / sc;
+    if ((threadIdx.x & 3) == 0) scale[(long)g * C + c0 + c] = sc;
+    float f[16];
 #pragma unroll
-  for (int e = 0; e < 16; ++e) f[e] = clamp448(bf2f(tile[j0 + e][c]) * inv);
-  uint4 o;
-  o.x = cvt4_fp8(f[0], f[1], f[2], f[3]);
-  o.y = cvt4_fp8(f[4], f[5], f[6], f[7]);
-  o.z = cvt4_fp8(f[8], f[9], f[10], f[11]);
-  o.w = cvt4_fp8(f[12], f[13], f[14], f[15]);
-  *reinterpret_cast<uint4*>(q + (long)(c0 + c) * ldq + pt + j0) = o;
+    for (int e = 0; e < 16; ++e) f[e] = clamp448(bf2f(tile[j0 + e][c]) * inv);
+    uint4 o;
+    o.x = cvt4_fp8(f[0], f[1], f[2], f[3]);
+    o.y = cvt4_fp8(f[4], f[5], f[6], f[7]);
+    o.z = cvt4_fp8(f[8], f[9], f[10], f[11]);
+    o.w = cvt4_fp8(f[12], f[13], f[14], f[15]);
+    *reinterpret_cast<uint4*>((uint8_t*)qv + (long)(c0 + c) * ldq + pt + j0) = o;
+  } else {
+    u16x8 a, b;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      a[e] = tile[j0 + e][c];
+      b[e] = tile[j0 + 8 + e][c];
+    }
+    u16* d = (u16*)qv + (long)(c0 + c) * ldq + pt + j0;
+    *reinterpret_cast<u16x8*>(d) = a;
+    *reinterpret_cast<u16x8*>(d + 8) = b;
+  }
+}
+
+static int mb_src(MbSrc& s, int n, const void* const* xs, const long* ldx, const int* const* offs) {
+  if (n <= 0 || n > kMaxMb) return -1;
+  s.n = n;
+  for (int j = 0; j < n; ++j) {
+    if (!xs[j] || !offs[j] || (ldx[j] % 8)) return -1;
+    s.x[j] = (const u16*)xs[j];
+    s.ldx[j] = ldx[j];
+    s.offs[j] = offs[j];
+  }
+  return 0;
 }
 
 }  // namespace pa
 
-// offs [G+1] (device, expert row offsets) -> poffs [G+1] (64-aligned padded offsets)
-PA_EXPORT int pa_f8_pad_offsets(const int* offs, int G, int* poffs, hipStream_t st) {
-  if (G <= 0) return -1;
-  hipLaunchKernelGGL(pa::f8_pad_offsets_kernel, dim3(1), dim3(64), 0, st, offs, G, poffs);
+// Offsets of the concatenated grouped image: offs[j] (device int [G+1], expert row
+// offsets of micro-batch j, j < n <= 8) -> cum [(n+1) * G] (ws) and poffs [G+1].
+// Only the offset pointers of xs-less callers are read (xs may be null here).
+PA_EXPORT int pa_group_cat_offsets(int n, const int* const* offs, int G, int* cum, int* poffs, hipStream_t st) {
+  if (G <= 0 || n <= 0 || n > pa::kMaxMb) return -1;
+  pa::MbSrc s{};
+  s.n = n;
+  for (int j = 0; j < n; ++j) s.offs[j] = offs[j];
+  hipLaunchKernelGGL(pa::group_cat_offsets_kernel, dim3(1), dim3(64), 0, st, s, G, cum, poffs);
   PA_LAUNCH_CHECK();
 }
 
-// x [R, C] bf16 (row stride ldx, expert-sorted rows), C % 64 == 0 -> q [C][ldq] e4m3
-// (ldq >= R + 64 G, a multiple of 64; columns past poffs[G] untouched), scale [G][C],
-// amax [G][C] fp32 workspace (zeroed here).
-PA_EXPORT int pa_f8_group_quant_t(const void* x, long ldx, const int* offs, const int* poffs, int G, long R, int C,
-                                  float* amax, void* q, long ldq, float* scale, hipStream_t st) {
-  if (G <= 0 || C <= 0 || (C % 64) || (ldx % 8) || (ldq % 64) || ldq < R + 64L * G) return -1;
+// Transposed image of the concatenated expert rows: xs[j] [R_j, C] bf16 (row stride
+// ldx[j]), C % 64 == 0 -> q [C][ldq] (quant: e4m3 + scale [G][C], amax [G][C] fp32
+// workspace; else bf16), ldq >= sum R_j + 64 G and a multiple of 64, columns past
+// poffs[G] untouched.  cum / poffs from pa_group_cat_offsets.
+PA_EXPORT int pa_group_image(int quant, int n, const void* const* xs, const long* ldx, const int* const* offs,
+                             const int* cum, const int* poffs, int G, long R, int C, float* amax, void* q, long ldq,
+                             float* scale, hipStream_t st) {
+  pa::MbSrc s{};
+  if (pa::mb_src(s, n, xs, ldx, offs)) return -1;
+  if (G <= 0 || C <= 0 || (C % 64) || (ldq % 64) || ldq < R + 64L * G) return -1;
   const long tiles = (R + 64L * G + pa::kGT - 1) / pa::kGT;
   if (tiles > 0x7fffffffL || C / 64 > 65535) return -1;
-  hipError_t e = hipMemsetAsync(amax, 0, sizeof(float) * (size_t)G * C, st);
-  if (e != hipSuccess) return (int)e;
-  // experts without tokens get no tile: their scales stay 0 (the GEMM's 0 * s stays 0)
-  e = hipMemsetAsync(scale, 0, sizeof(float) * (size_t)G * C, st);
-  if (e != hipSuccess) return (int)e;
   dim3 grid((unsigned)tiles, C / 64);
-  hipLaunchKernelGGL(pa::f8_group_amax_kernel, grid, dim3(256), 0, st, (const u16*)x, ldx, offs, poffs, G, C, amax);
-  hipLaunchKernelGGL(pa::f8_group_quant_t_kernel, grid, dim3(256), 0, st, (const u16*)x, ldx, offs, poffs, G, C,
-                     (const float*)amax, (uint8_t*)q, ldq, scale);
+  if (quant) {
+    if (!amax || !scale) return -1;
+    hipError_t e = hipMemsetAsync(amax, 0, sizeof(float) * (size_t)G * C, st);
+    if (e != hipSuccess) return (int)e;
+    // experts without tokens get no tile: their scales stay 0 (the GEMM's 0 * s stays 0)
+    e = hipMemsetAsync(scale, 0, sizeof(float) * (size_t)G * C, st);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(pa::group_amax_kernel, grid, dim3(256), 0, st, s, cum, poffs, G, C, amax);
+    hipLaunchKernelGGL(pa::group_image_kernel<true>, grid, dim3(256), 0, st, s, cum, poffs, G, C, (const float*)amax,
+                       q, ldq, scale);
+  } else {
+    hipLaunchKernelGGL(pa::group_image_kernel<false>, grid, dim3(256), 0, st, s, cum, poffs, G, C, nullptr, q, ldq,
+                       nullptr);
+  }
   PA_LAUNCH_CHECK();
 }

@@ -66,8 +66,9 @@ struct Params {
   //              the total row count (sizes the grid), B advances by sB per group
   //  grp_mode 2: group g reduces over rows [grp[g], grp[g+1]) of A and B (both
   //              MN-major: dW of grouped experts); C advances by sC per group.
-  //              F8: both operands K-major (token-contiguous quantised X^T / dY^T),
-  //              grp[] in fp8 elements (multiples of 16), sa / sb per group (sas / sbs)
+  //              Or both K-major (token-contiguous X^T / dY^T images, 64-aligned
+  //              group columns): grp[] are column offsets; F8 additionally in fp8
+  //              elements (multiples of 16), sa / sb per group (sas / sbs)
   const int* grp;
   int grp_mode;
   // F8 kernels: C = alpha * sa[row] * sb[col] * (A_q B_q^T); sa indexed by the
@@ -410,11 +411,13 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
         Mb = r1 - r0;
         a_off = (long)r0 * p.lda;
         c_row0 = r0;
-      } else if constexpr (F8) {
-        // K-major fp8 operands: the group's k range is a column range (2 fp8 per unit)
-        Kb = (r1 - r0) >> 1;
-        a_off = r0 >> 1;
-        b_off = r0 >> 1;
+      } else if constexpr (AK && BK) {
+        // K-major operands (token-contiguous X^T / dY^T images): the group's k range
+        // is a column range; fp8 counts k in units of 2 bytes
+        constexpr int sh = F8 ? 1 : 0;
+        Kb = (r1 - r0) >> sh;
+        a_off = r0 >> sh;
+        b_off = r0 >> sh;
       } else {
         Kb = r1 - r0;
         a_off = (long)r0 * p.lda;
@@ -1093,7 +1096,7 @@ static int launch_v(const Params& p, int batch, hipStream_t st) {
 // (registers): mode 1 needs a K-major A, mode 2 two MN-major operands.
 template <bool AK, bool BK, bool F32, int GM>
 static int launch_g(const Params& p, int batch, hipStream_t st) {
-  if constexpr ((GM == 1 && !AK) || (GM == 2 && (AK || BK))) {
+  if constexpr ((GM == 1 && !AK) || (GM == 2 && AK != BK)) {
     return -1;
   } else {
     const bool pf = g_sched == 1;  // measured: in-cluster prefetch loses on every form (profiles/r3_gemm_mn_forms.jsonl)

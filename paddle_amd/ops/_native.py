@@ -186,9 +186,9 @@ _SIGS = {
     "pa_gemm_f8": [_I, _P, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _L, _I, _F, _I, _P, _I, _P],
     "pa_quant_rows_f8": [_P, _L, _P, _L, _P, _L, _I, _P],
     "pa_quant_cols_t_f8": [_P, _P, _P, _I, _I, _I, _P],
-    "pa_f8_pad_offsets": [_P, _I, _P, _P],
+    "pa_group_cat_offsets": [_I, _P, _I, _P, _P, _P],
+    "pa_group_image": [_I, _I, _P, _P, _P, _P, _P, _I, _L, _I, _P, _P, _L, _P, _P],
     "pa_fa_gqa_fold": [_P, _P, _P, _P, _L, _I, _I, _I, _L, _P],
-    "pa_f8_group_quant_t": [_P, _L, _P, _P, _I, _L, _I, _P, _P, _L, _P, _P],
     "pa_moe_reduce": [_P, _P, _P, _P, _L, _I, _I, _P],
     "pa_moe_combine_bwd": [_P, _P, _P, _P, _P, _P, _L, _I, _I, _P],
     "pa_moe_route": [_P, _L, _I, _I, _I, _L, _P, _P, _P, _P, _P, _P],

@@ -1,0 +1,37 @@
+"""Deferred weight-gradient work across the micro-batches of one optimizer step.
+
+Gradient accumulation runs the backward once per micro-batch; a weight gradient
+that accumulates into an fp32 main_grad then pays a read-modify-write of that
+main_grad per micro-batch.  While :func:`deferring` is true (the sharded
+optimizers' ``no_sync()`` -- every micro-batch but the last) an op may keep the
+operands of its weight gradient instead and compute it once, over all micro-batches,
+in the last one (``ops/grouped.py``: the experts' dW as one grouped GEMM whose K is
+every micro-batch's tokens, one main_grad write per step).  :func:`flush` computes
+whatever is still pending (called by the optimizer step before it reads main_grad).
+
+Reference counterpart: Fleet's gradient merge (``accumulate_steps``) sums per
+micro-batch gradients; the sum is the same, the order of the additions differs.
+"""
+from __future__ import annotations
+
+_STATE = {"defer": False}
+_FLUSH = []
+
+
+def deferring() -> bool:
+    return _STATE["defer"]
+
+
+def set_deferring(on: bool) -> None:
+    _STATE["defer"] = bool(on)
+
+
+def register_flush(fn) -> None:
+    if fn not in _FLUSH:
+        _FLUSH.append(fn)
+
+
+def flush() -> None:
+    """Compute every deferred weight gradient now (before main_grad is read)."""
+    for fn in _FLUSH:
+        fn()

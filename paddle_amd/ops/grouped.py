@@ -18,11 +18,13 @@ The reference has no MoE; the per-expert loop it would imply i
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import torch
 
 from . import _native as N
+from . import accum as _accum
 from ..autograd import tape as _tape
 from . import fp8 as _F8
 from . import gemm as _G
@@ -85,6 +87,10 @@ class _GroupedSwiGLUFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty(R, H, dtype=x.dtype, device=x.device)
             _G.grouped_rows(dh, gate_up, offs, b_kmaj=True, out=dx)
+        r = _expert_wgrads(gate_up, down, x, dh, a, dy, offs, False,
+                           (ctx.needs_input_grad[1], ctx.needs_input_grad[2]))
+        if r is not None:
+            return dx, r[0], r[1], None
         d_down = _wgrad(down, a, dy, offs) if ctx.needs_input_grad[2] else None
         d_gu = _wgrad(gate_up, x, dh, offs) if ctx.needs_input_grad[1] else None
         return dx, d_gu, d_down, None
@@ -100,48 +106,128 @@ class _GroupedSwiGLUFn(torch.autograd.Function):
 _F8_WGRAD = os.environ.get("FLAGS_fp8_wgrad", "0") not in ("0", "false", "False")
 
 
-def _pad_offsets(offs, G):
-    poffs = torch.empty(G + 1, dtype=torch.int32, device=offs.device)
-    N.call("pa_f8_pad_offsets", N.ptr(offs), G, N.ptr(poffs), N.stream())
-    return poffs
+def _ptrs(ts):
+    return (ctypes.c_void_p * len(ts))(*[N.ptr(t) for t in ts])
 
 
-def _quant_t_grouped(x, offs, poffs, G):
-    """x [R, C] expert-sorted rows -> (q [C, ldq] e4m3 token-contiguous, 64-aligned
-    per-expert columns; scale [G, C])."""
-    R, C = x.shape
+def _cat_offsets(offs_list, G):
+    """Concatenated expert layout of several micro-batches: cum [(n+1) * G] (tokens
+    of expert g before micro-batch j) and 64-aligned image columns poffs [G+1]."""
+    n = len(offs_list)
+    dev = offs_list[0].device
+    cum = torch.empty((n + 1) * G, dtype=torch.int32, device=dev)
+    poffs = torch.empty(G + 1, dtype=torch.int32, device=dev)
+    N.call("pa_group_cat_offsets", n, _ptrs(offs_list), G, N.ptr(cum), N.ptr(poffs), N.stream())
+    return cum, poffs
+
+
+def _image(xs, offs_list, cum, poffs, G, quant):
+    """Transposed token-contiguous image [C, ldq] of the experts' rows of every
+    micro-batch (e4m3 + per-(expert, channel) scales, or bf16)."""
+    xs = [_c(x) for x in xs]
+    R, C = sum(x.shape[0] for x in xs), xs[0].shape[1]
     ldq = (R + 64 * G + 63) // 64 * 64
-    q = torch.empty(C, ldq, dtype=_F8._FP8, device=x.device)
-    sc = torch.empty(G, C, dtype=torch.float32, device=x.device)
-    amax = torch.empty(G, C, dtype=torch.float32, device=x.device)
-    N.call("pa_f8_group_quant_t", N.ptr(x), x.stride(0), N.ptr(offs), N.ptr(poffs), G, R, C, N.ptr(amax), N.ptr(q),
-           ldq, N.ptr(sc), N.stream())
+    dev = xs[0].device
+    q = torch.empty(C, ldq, dtype=_F8._FP8 if quant else torch.bfloat16, device=dev)
+    sc = amax = None
+    if quant:
+        sc = torch.empty(G, C, dtype=torch.float32, device=dev)
+        amax = torch.empty(G, C, dtype=torch.float32, device=dev)
+    ld = (ctypes.c_long * len(xs))(*[x.stride(0) for x in xs])
+    N.call("pa_group_image", int(quant), len(xs), _ptrs(xs), ld, _ptrs(offs_list), N.ptr(cum), N.ptr(poffs), G, R, C,
+           N.ptr(amax), N.ptr(q), ldq, N.ptr(sc), N.stream())
     return q, sc, ldq
 
 
-def _wgrad_f8_ok(a, b):
-    return _F8_WGRAD and _F8._FP8 is not None and a.shape[1] % 64 == 0 and b.shape[1] % 64 == 0
+def _image_ok(*ts):
+    return all(t.shape[1] % 64 == 0 and t.dtype == torch.bfloat16 for t in ts)
 
 
-def _wgrad_f8(w, a, b, offs, poffs, G):
-    """Per-expert dW_g = a_g^T b_g ([G, M, N] fp32) on the fp8 grouped-K GEMM."""
-    a, b = _c(a), _c(b)
-    M, Nn = a.shape[1], b.shape[1]
-    qa, sa, ldq = _quant_t_grouped(a, offs, poffs, G)
-    qb, sb, _ = _quant_t_grouped(b, offs, poffs, G)
+def _wgrad_images(w, a_list, b_list, offs_list, G, fp8):
+    """dW_g = sum_j a_j[g]^T b_j[g] over the micro-batches j ([G, M, N]) as ONE grouped
+    GEMM over the K-major images: into main_grad (overwrite on the step's first
+    write, else +=) or a fresh fp32 tensor (returned in w's dtype)."""
+    cum, poffs = _cat_offsets(offs_list, G)
+    qa, sa, ldq = _image(a_list, offs_list, cum, poffs, G, fp8)
+    qb, sb, _ = _image(b_list, offs_list, cum, poffs, G, fp8)
+    M, Nn = a_list[0].shape[1], b_list[0].shape[1]
     mg = getattr(w, "_pa_main_grad", None)
     if mg is not None:
         fresh = getattr(w, "_pa_grad_fresh", False)
         w._pa_grad_fresh = False
         out, acc, ret = mg, not fresh, None
     else:
-        out, acc = torch.empty(G, M, Nn, dtype=torch.float32, device=a.device), False
+        out, acc = torch.empty(G, M, Nn, dtype=torch.float32, device=qa.device), False
         ret = out
-    rc = N.lib().pa_gemm_f8(1, N.ptr(qa), N.ptr(qb), N.ptr(out), N.ptr(sa), N.ptr(sb), M, Nn, ldq, ldq, ldq, Nn, 0,
-                            M * Nn, G, 1.0, int(acc), N.ptr(poffs), 2, N.stream())
-    if rc != 0:
-        raise RuntimeError(f"pa_gemm_f8 (grouped dW) failed rc={rc} G={G} M={M} N={Nn}")
+    if fp8:
+        rc = N.lib().pa_gemm_f8(1, N.ptr(qa), N.ptr(qb), N.ptr(out), N.ptr(sa), N.ptr(sb), M, Nn, ldq, ldq, ldq, Nn,
+                                0, M * Nn, G, 1.0, int(acc), N.ptr(poffs), 2, N.stream())
+        if rc != 0:
+            raise RuntimeError(f"pa_gemm_f8 (grouped dW) failed rc={rc} G={G} M={M} N={Nn}")
+    else:
+        _G.gemm(qa, qb, M, Nn, ldq, a_kmaj=True, b_kmaj=True, out=out[0], accumulate=acc, batch=G, sA=0, sB=0,
+                sC=out.stride(0), ldc=out.stride(1), grp=poffs, grp_mode=2)
     return None if ret is None else ret.to(w.dtype)
+
+
+def _wgrad_f8_ok(a, b):
+    return _F8_WGRAD and _F8._FP8 is not None and _image_ok(a, b)
+
+
+def _wgrad_f8(w, a, b, offs, G):
+    """Per-expert dW_g = a_g^T b_g ([G, M, N] fp32) on the fp8 grouped-K GEMM."""
+    return _wgrad_images(w, [a], [b], [offs], G, True)
+
+
+# ---- expert dW over all micro-batches of a step (ops/accum.py)
+# key: id(gate_up) -> [(gate_up, down, x, dh, a, dy, offs, fp8)] of the deferred
+# micro-batches; each entry holds the operands of one micro-batch's two dW GEMMs
+_STASH = {}
+_MAX_MB = 8  # csrc/kernels/fp8.hip kMaxMb
+_DEFER_ON = os.environ.get("FLAGS_defer_expert_wgrad", "1") not in ("0", "false", "False")
+
+
+def _defer_ok(gate_up, down, x, dh, a, dy):
+    return (_DEFER_ON and getattr(gate_up, "_pa_main_grad", None) is not None
+            and getattr(down, "_pa_main_grad", None) is not None and _image_ok(x, dh, a, dy))
+
+
+def _expert_wgrads(gate_up, down, x, dh, a, dy, offs, fp8, needs):
+    """The two expert dW of one micro-batch: deferred while accum.deferring(), else
+    computed over every deferred micro-batch plus this one in one GEMM each.
+    Returns (d_gate_up, d_down), or None when the regular per-micro-batch path
+    applies (nothing deferred, or no main_grad to accumulate into)."""
+    if not _defer_ok(gate_up, down, x, dh, a, dy):
+        return None
+    key = id(gate_up)
+    lst = _STASH.get(key, [])
+    if _accum.deferring() and len(lst) < _MAX_MB - 1:
+        _STASH.setdefault(key, []).append((gate_up, down, x, dh, a, dy, offs, fp8))
+        return None, None
+    if not lst:
+        return None
+    _STASH.pop(key, None)
+    return _flush_entries(lst + [(gate_up, down, x, dh, a, dy, offs, fp8)], needs)
+
+
+def _flush_entries(ents, needs=(True, True)):
+    gate_up, down = ents[0][0], ents[0][1]
+    G = gate_up.shape[0]
+    fp8 = _F8_WGRAD and ents[0][7] and _F8._FP8 is not None
+    offs = [e[6] for e in ents]
+    d_down = _wgrad_images(down, [e[4] for e in ents], [e[5] for e in ents], offs, G, fp8) if needs[1] else None
+    d_gu = _wgrad_images(gate_up, [e[2] for e in ents], [e[3] for e in ents], offs, G, fp8) if needs[0] else None
+    return d_gu, d_down
+
+
+def _flush_all():
+    """Deferred experts whose last micro-batch never came (accum.flush)."""
+    while _STASH:
+        _, ents = _STASH.popitem()
+        _flush_entries(ents)
+
+
+_accum.register_flush(_flush_all)
 
 
 class _F8Weights:
@@ -204,10 +290,13 @@ class _GroupedSwiGLUF8Fn(torch.autograd.Function):
             gbq, gbs = _f8_cache(gate_up).bwd.get(gate_up)  # [G*H, 2I]: B = gate_up[g] as [H][2I]
             dx = _rows_f8(dh, gbq, gbs, offs, H, torch.empty(R, H, dtype=x.dtype, device=x.device))
         G = gate_up.shape[0]
+        r = _expert_wgrads(gate_up, down, x, dh, a, dy, offs, True,
+                           (ctx.needs_input_grad[1], ctx.needs_input_grad[2]))
+        if r is not None:
+            return dx, r[0], r[1], None
         if _wgrad_f8_ok(x, dh) and _wgrad_f8_ok(a, dy):
-            poffs = _pad_offsets(offs, G)
-            d_down = _wgrad_f8(down, a, dy, offs, poffs, G) if ctx.needs_input_grad[2] else None
-            d_gu = _wgrad_f8(gate_up, x, dh, offs, poffs, G) if ctx.needs_input_grad[1] else None
+            d_down = _wgrad_f8(down, a, dy, offs, G) if ctx.needs_input_grad[2] else None
+            d_gu = _wgrad_f8(gate_up, x, dh, offs, G) if ctx.needs_input_grad[1] else None
             return dx, d_gu, d_down, None
         d_down = _wgrad(down, a, dy, offs) if ctx.needs_input_grad[2] else None
         d_gu = _wgrad(gate_up, x, dh, offs) if ctx.needs_input_grad[1] else None

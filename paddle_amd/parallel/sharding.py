@@ -40,6 +40,8 @@ import os
 
 import torch
 
+from ..ops import accum as _accum
+
 from ..ops import fused
 from ..autograd import tape as _tape
 from ..ops import optim as fused_optim
@@ -204,14 +206,18 @@ class FlatShardedOptimizer:
 
     # ------------------------------------------------------------------ comm
     def no_sync(self):
-        """Context manager: accumulate micro-batch gradients without communicating."""
+        """Context manager: accumulate micro-batch gradients without communicating.
+        Inside it, ops may also defer weight-gradient work to the step's last
+        micro-batch (``ops/accum.py``: the experts' dW as one GEMM per step)."""
         opt = self
 
         class _Ctx:
             def __enter__(self_):
                 opt._sync = False
+                _accum.set_deferring(True)
 
             def __exit__(self_, *a):
+                _accum.set_deferring(False)
                 opt._sync = True
                 opt._ready = [0] * len(opt.buckets)
 
@@ -351,6 +357,7 @@ class FlatShardedOptimizer:
     def step(self, lr=None):
         if lr is not None:
             self.lr = lr
+        _accum.flush()  # weight gradients still deferred (no final micro-batch came)
         if self._direct is not None:
             self._direct.poll_error()  # a peer timeout of the previous step raises here
         self.sync_params()

@@ -189,40 +189,91 @@ def test_moe_capacity_sync_free_layer_matches_exact_split():
         assert _rel(a, b) < 2e-2
 
 
+@pytest.mark.parametrize("fp8", [False, True])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("counts", [COUNTS, MANY])
-def test_grouped_dw_fp8(accumulate, counts):
-    """fp8 expert dW (per-(expert, channel) e4m3 quantisation transposed into 64-aligned
-    token-contiguous segments + the fp8 MFMA's grouped-K mode) against the fp32 per-expert
-    product: relative Frobenius error at e4m3 resolution, empty experts untouched."""
+@pytest.mark.parametrize("nmb", [1, 3])
+def test_grouped_dw_images(fp8, accumulate, nmb):
+    """Expert dW over the K-major token images (fp8.hip pa_group_image: expert rows of
+    several micro-batches concatenated per expert into 64-aligned segments, bf16 or
+    e4m3 with per-(expert, channel) scales) and the grouped-K GEMM, against the fp32
+    sum over micro-batches of the per-expert products; experts without tokens get 0."""
     from paddle_amd.ops import grouped as GR
     from paddle_amd.ops import gemm as G
 
-    g = torch.Generator(device=dev).manual_seed(11)
-    M, Nn, R = 192, 320, sum(counts)
-    o = _offs(counts)
-    a = torch.randn(R, M, generator=g, device=dev).to(torch.bfloat16)
-    b = (torch.randn(R, Nn, generator=g, device=dev) * 1e-3).to(torch.bfloat16)  # gradient-sized
-    offs = G.group_table(torch.tensor(o, dtype=torch.int32, device=dev), R)
-    E = len(counts)
-    poffs = GR._pad_offsets(offs, E)
+    g = torch.Generator(device=dev).manual_seed(11 + nmb)
+    M, Nn = 192, 320
+    E = len(COUNTS)
+    mbs = []
+    for j in range(nmb):
+        counts = COUNTS if j % 2 == 0 else MANY[:E]
+        R = sum(counts)
+        a = torch.randn(R, M, generator=g, device=dev).to(torch.bfloat16)
+        b = (torch.randn(R, Nn, generator=g, device=dev) * 1e-3).to(torch.bfloat16)  # gradient-sized
+        o = _offs(counts)
+        mbs.append((a, b, o, G.group_table(torch.tensor(o, dtype=torch.int32, device=dev), R), counts))
+    cum, poffs = GR._cat_offsets([m[3] for m in mbs], E)
+    tot = [sum(m[4][e] for m in mbs) for e in range(E)]
     pl = poffs.cpu().tolist()
-    assert all(p % 64 == 0 for p in pl) and all(pl[e + 1] - pl[e] == (c + 63) // 64 * 64 for e, c in enumerate(counts))
+    assert all(p % 64 == 0 for p in pl) and all(pl[e + 1] - pl[e] == (c + 63) // 64 * 64 for e, c in enumerate(tot))
     w = torch.zeros(E, M, Nn, device=dev)
     init = torch.randn(E, M, Nn, generator=g, device=dev) * 1e-3
     if accumulate:
         w._pa_main_grad = init.clone()
         w._pa_grad_fresh = False
-        assert GR._wgrad_f8(w, a, b, offs, poffs, E) is None
+        assert GR._wgrad_images(w, [m[0] for m in mbs], [m[1] for m in mbs], [m[3] for m in mbs], E, fp8) is None
         got = w._pa_main_grad
     else:
-        got = GR._wgrad_f8(w, a, b, offs, poffs, E)
+        got = GR._wgrad_images(w, [m[0] for m in mbs], [m[1] for m in mbs], [m[3] for m in mbs], E, fp8)
+    tol = 6e-2 if fp8 else 1e-2
     for e in range(E):
-        ref = a[o[e]:o[e + 1]].float().t() @ b[o[e]:o[e + 1]].float()
-        base = init[e] if accumulate else torch.zeros_like(ref)
+        ref = sum(m[0][m[2][e]:m[2][e + 1]].float().t() @ m[1][m[2][e]:m[2][e + 1]].float() for m in mbs)
+        base = init[e] if accumulate else torch.zeros(M, Nn, device=dev)
         d = got[e] - base
-        if counts[e] == 0:
+        if tot[e] == 0:
             assert not torch.any(d), e
             continue
         err = (d - ref).norm() / ref.norm().clamp_min(1e-30)
-        assert err < 6e-2, (e, counts[e], float(err))
+        assert err < tol, (e, tot[e], float(err))
+
+
+def test_ernie_moe_deferred_expert_dw_matches_per_microbatch():
+    """accum.deferring() (the optimizer's no_sync): the expert dW of the first
+    micro-batches is computed with the last one in one grouped GEMM; the main_grad
+    after the step equals the per-micro-batch accumulation."""
+    from paddle_amd.autograd import tape
+    from paddle_amd.models.ernie_moe import ERNIE_MOE_CONFIGS, ErnieMoEConfig, ErnieMoEForCausalLM
+    from paddle_amd.ops import accum, grouped as GR
+    from paddle_amd.parallel.sharding import FlatShardedOptimizer
+
+    def grads(defer):
+        torch.manual_seed(0)
+        cfg = ErnieMoEConfig(**dict(ERNIE_MOE_CONFIGS["ernie-moe-tiny"], hidden_size=256, moe_intermediate_size=128,
+                                    intermediate_size=512, grouped_experts=True, max_position_embeddings=512,
+                                    num_experts=8))
+        m = ErnieMoEForCausalLM(cfg, torch.device(dev))
+        opt = FlatShardedOptimizer(m.named_parameters(), lr=0.0, grad_dtype=torch.float32)
+        gen = torch.Generator().manual_seed(5)
+        for j in range(3):
+            ids = torch.randint(0, cfg.vocab_size, (2, 257), generator=gen).to(dev)
+            ctx = opt.no_sync() if (defer and j < 2) else __import__("contextlib").nullcontext()
+            with ctx:
+                with tape.recording() as t:
+                    loss = m(ids[:, :-1], ids[:, 1:])
+                t.backward(loss)
+        assert not GR._STASH
+        torch.cuda.synchronize()
+        return {n: p._pa_main_grad.clone() for n, p in m.named_parameters() if "gate_up" in n or "down" in n}
+
+    old = GR._DEFER_ON
+    try:
+        GR._DEFER_ON = False
+        ref = grads(False)
+        GR._DEFER_ON = True
+        got = grads(True)
+    finally:
+        GR._DEFER_ON = old
+        accum.set_deferring(False)
+    assert ref.keys() == got.keys() and ref
+    for n in ref:
+        err = (got[n] - ref[n]).norm() / ref[n].norm().clamp_min(1e-30)
+        assert err < 1e-2, (n, float(err))
