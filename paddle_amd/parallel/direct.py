@@ -17,7 +17,8 @@ collective is three or four plain kernels on the caller's stream
   staging, barrier, every rank reads the P chunks into its output, barrier.
 
 The training path uses these under ``FLAGS_dp_comm=direct``
-(parallel/sharding.py FlatShardedOptimizer); RCCL stays the default.
+(parallel/sharding.py FlatShardedOptimizer, distributed/sharding.py ShardedStage3);
+the framework RCCL communicators (parallel/rccl.py) stay the default.
 
 Barriers are bounded spins on system-scope signals: a missing peer makes the op
 fail (``DirectAllReduce.check``) instead of hanging the device.  Reference
@@ -37,12 +38,26 @@ from . import comm
 _P = ctypes.c_void_p
 
 
+def _env_int(name, default):
+    import os
+
+    v = os.environ.get(name, "")
+    return int(v) if v.strip() else default
+
+
 class DirectAllReduce:
-    def __init__(self, group=None, max_bytes=64 << 20, one_shot_bytes=1 << 20, max_spins=1 << 25, extra_bytes=0):
+    def __init__(self, group=None, max_bytes=None, one_shot_bytes=None, max_spins=None, extra_bytes=0):
         """``extra_bytes``: a second region of the registered staging allocation, after
         the ``max_bytes`` scratch area, handed out by :meth:`staging_tensor` -- a buffer
         placed there (the sharded optimizer's flat gradient) is reduce-scattered in
-        place, without the copy-in pass."""
+        place, without the copy-in pass.  Unset sizes come from the flags
+        ``FLAGS_direct_max_bytes`` (scratch staging, default 64 MiB),
+        ``FLAGS_direct_one_shot_bytes`` (one-shot / two-shot switch, default 1 MiB:
+        below it the 7 concurrent peer reads of one-shot beat the extra barrier of
+        two-shot) and ``FLAGS_direct_max_spins`` (barrier spin bound)."""
+        max_bytes = _env_int("FLAGS_direct_max_bytes", 64 << 20) if max_bytes is None else max_bytes
+        one_shot_bytes = _env_int("FLAGS_direct_one_shot_bytes", 1 << 20) if one_shot_bytes is None else one_shot_bytes
+        max_spins = _env_int("FLAGS_direct_max_spins", 1 << 25) if max_spins is None else max_spins
         self.group = group
         self.world = comm.get_world_size(group)
         self.rank = comm.get_rank(group)

@@ -34,6 +34,15 @@ _DEFAULTS = {
     "use_hip_graph": False,
     "rccl_bucket_mb": 256,
     "executor_engine": "auto",  # fluid.Executor engine: "auto" (C++ executor for every program it can take), "python" (op interpreter) or "native"
+    "strict_native": False,  # utils/strict.py: an ATen device kernel (or host fallback of the C++ executor) inside a framework region is an error
+    "count_aten": False,  # utils/strict.py: count ATen device kernels per region without raising
+    "strict_trace": False,  # utils/strict.py: record the framework call site of each counted ATen kernel
+    "dp_comm": "rccl",  # data-parallel gradient path: "rccl" (framework communicators) or "direct" (parallel/direct.py peer kernels)
+    "direct_max_bytes": 64 << 20,  # parallel/direct.py scratch staging per rank
+    "direct_one_shot_bytes": 1 << 20,  # one-shot / two-shot all-reduce switch
+    "direct_max_spins": 1 << 25,  # bounded signal-barrier spins before a peer is declared lost
+    "defer_expert_wgrad": True,  # ops/grouped.py: experts' dW once per step over all micro-batches (ops/accum.py)
+    "fp8_wgrad": False,  # ops/grouped.py: fp8 expert dW (measured slower, profiles/r5_moe_fp8_wgrad_NEGATIVE.md)
 }
 
 _values = {}
