@@ -39,6 +39,7 @@ SYNCS: dict = {}          # region label -> device->host scalar reads (item() / 
 FALLBACKS: dict = {}      # site -> explicit fallback count
 ATEN_SITES: dict = {}     # "label:aten_op" -> {"file:line" of the framework frame that issued it: count}
                           # (FLAGS_strict_trace=1: find the code behind each counted kernel)
+NATIVE_SITES: dict = {}   # aten op -> {"file:line": count} of the calls run natively (FLAGS_strict_trace=1)
 _TLS = threading.local()
 # device types whose ATen kernels count (tests add "cpu" to exercise the watcher here)
 WATCH_DEVICES = {"cuda"}
@@ -159,6 +160,10 @@ class _Watch(TorchDispatchMode):
                 r = aten_native.try_native(func, args, kwargs)
                 if r is not NotImplemented:
                     NATIVE_OPS[name] = NATIVE_OPS.get(name, 0) + 1
+                    if os.environ.get("FLAGS_strict_trace", "0") not in ("0", ""):
+                        d = NATIVE_SITES.setdefault(name, {})
+                        site = _site()
+                        d[site] = d.get(site, 0) + 1
                     return r
             # a contiguous() of an already contiguous tensor never reaches here;
             # clone / copy_ / _to_copy do launch a copy kernel and are counted
@@ -264,6 +269,7 @@ def fallback(site: str, on_gpu: bool = True):
 def reset():
     ATEN_KERNELS.clear()
     ATEN_SITES.clear()
+    NATIVE_SITES.clear()
     FALLBACKS.clear()
     NATIVE_OPS.clear()
     SYNCS.clear()
@@ -274,4 +280,6 @@ def report() -> dict:
            "syncs": dict(SYNCS)}
     if ATEN_SITES:
         rep["aten_sites"] = {k: dict(v) for k, v in ATEN_SITES.items()}
+    if NATIVE_SITES:
+        rep["native_sites"] = {k: dict(v) for k, v in NATIVE_SITES.items()}
     return rep
