@@ -96,7 +96,16 @@ def _pa_comm(group, *ts):
     if not host and dist.get_backend(group) != "nccl":
         return None
     dev = -1 if host else None
-    return rccl.context_map().get(_group_ranks(group), dist.get_rank(), device=dev)
+    try:
+        return rccl.context_map().get(_group_ranks(group), dist.get_rank(), device=dev)
+    except rccl.RcclError as e:
+        # under the default ``auto`` mode a communicator that cannot be created (every
+        # rank sees the same librccl / device setup) leaves the collectives on c10d's
+        # ProcessGroupNCCL -- RCCL as well -- instead of failing the job
+        if os.environ.get("FLAGS_comm_backend", "auto") != "auto" or host:
+            raise
+        rccl.disable_auto(f"framework RCCL communicator unavailable ({e}); using torch.distributed")
+        return None
 
 
 class StreamWork:

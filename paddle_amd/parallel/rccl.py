@@ -284,3 +284,12 @@ def enabled() -> bool:
 
 
 _AUTO: list = []
+
+
+def disable_auto(reason: str) -> None:
+    """``auto`` mode: stop routing collectives through the framework communicators
+    (the caller falls back to torch.distributed), with one warning."""
+    import warnings
+
+    warnings.warn(reason, RuntimeWarning, stacklevel=2)
+    _AUTO[:] = [False]
