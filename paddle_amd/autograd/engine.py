@@ -603,6 +603,11 @@ def _leaf_add(leaf, g, torch_roots=None):
             g = g.to(leaf.dtype)
         if leaf.grad is None:
             leaf.grad = g.as_subclass(Tensor) if not isinstance(g, Tensor) else g
+        elif leaf.grad.is_cuda:
+            from ..ops import oplib
+
+            with DisableTorchFunctionSubclass():
+                oplib.add_(leaf.grad, g)  # direct kernel launch (no dispatch-mode hop)
         else:
             leaf.grad.add_(g)
     for hook in leaf.__dict__.get("_pa_grad_ready_hooks", ()):

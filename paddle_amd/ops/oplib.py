@@ -50,6 +50,18 @@ def fill_(t, value):
     return t.fill_(value)
 
 
+def add_(a, b):
+    """a += b in place on the elementwise kernel (same shape; b's dtype may differ):
+    a direct launch, no pass through the ATen dispatcher or the native-dispatch mode."""
+    if a.is_cuda and b.is_cuda and a.shape == b.shape and a.numel():
+        from . import aten_native as A
+
+        if a.dtype in A._DT and b.dtype in A._DT and A._launch(A.B["add"], a, [a, b], a=1.0,
+                                                                 cdt=A._cdt(a.dtype)):
+            return a
+    return a.add_(b)
+
+
 def full_like(t, value):
     """A new tensor shaped like ``t`` filled with ``value`` (native fill)."""
     return fill_(torch.empty_like(t, memory_format=torch.contiguous_format), value)
