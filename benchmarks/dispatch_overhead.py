@@ -41,4 +41,21 @@ with strict.region("bench"):
     out["empty_in_region_us"] = t(lambda: torch.empty(1024, device="cuda"))
     out["cast_in_region_us"] = t(lambda: x.to(torch.bfloat16))
 out["aten_cast_us"] = t(lambda: x.to(torch.bfloat16))
+# framework hot paths that bypass the dispatch mode: direct kernel launches
+from paddle_amd.ops import aten_native as A, oplib  # noqa: E402
+
+out["direct_add_inplace_us"] = t(lambda: oplib.add_(x, y))
+out["aten_add_inplace_us"] = t(lambda: x.add_(y))
+out["direct_fill_us"] = t(lambda: oplib.fill_(x, 0.0))
+z = torch.empty_like(x)
+out["direct_add_out_us"] = t(lambda: A._launch(A.B["add"], z, [x, y], a=1.0))
+
+
+class _Pass(torch.utils._python_dispatch.TorchDispatchMode):
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        return func(*args, **(kwargs or {}))
+
+
+with _Pass():  # the bare cost of a Python dispatch-mode hop around the ATen kernel
+    out["aten_add_under_passthrough_mode_us"] = t(lambda: x + y)
 print(json.dumps(out))

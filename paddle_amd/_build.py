@@ -182,6 +182,47 @@ def build_native(verbose: bool = False, jobs: int | None = None) -> str:
     return out
 
 
+FASTOPS_LIB = os.path.join(LIBDIR, "pa_fastops.so")
+
+
+def build_fastops(verbose: bool = False) -> str:
+    """The C++ launch entry for the hot elementwise ops (``csrc/fastops``): a CPython
+    extension against torch's C++ API (tensor unpacking without Python) that calls
+    the kernel library's ``pa_ew_flat``.  Optional: skipped when torch's headers are
+    not available."""
+    src = os.path.join(ROOT, "csrc", "fastops", "fastops.cc")
+    if not os.path.exists(src):
+        return ""
+    import sysconfig
+
+    import torch
+    from torch.utils import cpp_extension as ce
+
+    klib = build_kernels(verbose)
+    out = FASTOPS_LIB
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    flags = ["-O2", "-fPIC", "-std=c++17", "-shared", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+             "-DTORCH_EXTENSION_NAME=pa_fastops", "-DTORCH_API_INCLUDE_EXTENSION_H", "-w"]
+    flags += [f"-I{p}" for p in ce.include_paths()] + [f"-I{sysconfig.get_paths()['include']}"]
+    tl = _torch_lib_dir()
+    libs = [f"-L{tl}", f"-Wl,-rpath,{tl}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python",
+            f"-L{LIBDIR}", "-lpaddle_amd_kernels", "-Wl,-rpath,$ORIGIN"]
+    stamp = hashlib.sha1(" ".join(flags + libs).encode()).hexdigest()
+    if not _needs(out, [src, klib], stamp):
+        return out
+    cxx = shutil.which("g++") or "c++"
+    cmd = [cxx] + flags + [src, "-o", out + ".tmp"] + libs
+    if verbose:
+        print("[paddle_amd build]", " ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"fastops build failed:\n{r.stderr[-4000:]}")
+    os.replace(out + ".tmp", out)
+    with open(out + ".flags", "w") as f:
+        f.write(stamp)
+    return out
+
+
 def build_native_program(src: str, out: str, extra: list[str] | None = None) -> str:
     """Compiles a C++ program against the native library's public headers
     (paddle_inference_api.h / framework.h) and links libpaddle_amd_native.so."""
@@ -258,6 +299,9 @@ def build_all(verbose: bool = False) -> list[str]:
     ce = build_core_ext(verbose)
     if ce:
         out.append(ce)
+    fo = build_fastops(verbose)
+    if fo:
+        out.append(fo)
     return out
 
 

@@ -1,0 +1,96 @@
+// C++ entry for the hottest framework tensor ops (elementwise add / scale / cast /
+// copy / fill on contiguous same-shape device tensors): unpacks the torch tensors in
+// C++ and launches the kernel library's flat elementwise kernel (tensor_ops.hip
+// pa_ew_flat) on the caller's stream.  The Python dispatch path pays ~5 us per call in
+// argument marshalling (profiles/r5_dispatch_cost.md); this entry is what
+// ops/aten_native.py's hot path and the framework's direct callers (oplib.add_ /
+// fill_, the eager engine's gradient accumulation) use when it is built.
+// Returns false when the call does not fit (the caller takes the general path).
+#include <torch/extension.h>
+
+extern "C" int pa_ew_flat(int op, int cdt, int nin, long n, void* out, int odt, const void* x, int xdt,
+                          const void* y, int ydt, const void* z, int zdt, double a, double b, void* st);
+
+namespace {
+
+int dt_code(c10::ScalarType s) {
+  switch (s) {
+    case c10::ScalarType::Float: return 0;
+    case c10::ScalarType::BFloat16: return 1;
+    case c10::ScalarType::Half: return 2;
+    case c10::ScalarType::Double: return 3;
+    case c10::ScalarType::Long: return 4;
+    case c10::ScalarType::Int: return 5;
+    case c10::ScalarType::Short: return 6;
+    case c10::ScalarType::Char: return 7;
+    case c10::ScalarType::Byte: return 8;
+    case c10::ScalarType::Bool: return 9;
+    default: return -1;
+  }
+}
+
+// compute type: 0 fp32 (every float type but double), 1 fp64, 2 integer
+int cdt_of(c10::ScalarType s) {
+  if (s == c10::ScalarType::Double) return 1;
+  if (c10::isFloatingType(s)) return 0;
+  return 2;
+}
+
+bool fits(const at::Tensor& out, const at::Tensor* ins, int nin) {
+  if (!out.is_cuda() || !out.is_contiguous() || dt_code(out.scalar_type()) < 0) return false;
+  for (int i = 0; i < nin; ++i) {
+    const at::Tensor& t = ins[i];
+    if (!t.is_cuda() || !t.is_contiguous() || t.sizes() != out.sizes() || dt_code(t.scalar_type()) < 0 ||
+        t.device() != out.device())
+      return false;
+  }
+  return true;
+}
+
+bool launch(int op, int cdt, const at::Tensor& out, const at::Tensor* ins, int nin, double a, double b,
+            int64_t stream) {
+  if (!fits(out, ins, nin)) return false;
+  const long n = out.numel();
+  if (n == 0) return true;
+  if (cdt < 0) cdt = cdt_of(nin ? ins[0].scalar_type() : out.scalar_type());
+  const void* p[3] = {nullptr, nullptr, nullptr};
+  int d[3] = {0, 0, 0};
+  for (int i = 0; i < nin; ++i) {
+    p[i] = ins[i].data_ptr();
+    d[i] = dt_code(ins[i].scalar_type());
+  }
+  const int rc = pa_ew_flat(op, cdt, nin, n, out.data_ptr(), dt_code(out.scalar_type()), p[0], d[0], p[1], d[1],
+                            p[2], d[2], a, b, reinterpret_cast<void*>(stream));
+  TORCH_CHECK(rc == 0, "pa_ew_flat failed (rc=", rc, ", op=", op, ")");
+  return true;
+}
+
+bool ew0(int op, int cdt, const at::Tensor& out, double a, double b, int64_t stream) {
+  return launch(op, cdt, out, nullptr, 0, a, b, stream);
+}
+
+bool ew1(int op, int cdt, const at::Tensor& out, const at::Tensor& x, double a, double b, int64_t stream) {
+  return launch(op, cdt, out, &x, 1, a, b, stream);
+}
+
+bool ew2(int op, int cdt, const at::Tensor& out, const at::Tensor& x, const at::Tensor& y, double a, double b,
+         int64_t stream) {
+  const at::Tensor ins[2] = {x, y};
+  return launch(op, cdt, out, ins, 2, a, b, stream);
+}
+
+bool ew3(int op, int cdt, const at::Tensor& out, const at::Tensor& x, const at::Tensor& y, const at::Tensor& z,
+         double a, double b, int64_t stream) {
+  const at::Tensor ins[3] = {x, y, z};
+  return launch(op, cdt, out, ins, 3, a, b, stream);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(pa_fastops, m) {
+  m.doc() = "C++ launch entry for the framework's flat elementwise kernels";
+  m.def("ew0", &ew0, "out = op() (fill / iota)");
+  m.def("ew1", &ew1, "out = op(x)");
+  m.def("ew2", &ew2, "out = op(x, y)");
+  m.def("ew3", &ew3, "out = op(x, y, z)");
+}

@@ -259,6 +259,31 @@ _RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 _GET_DEVICE = getattr(torch._C, "_cuda_getDevice", None)
 
 
+_FAST = []
+
+
+def fastops():
+    """The C++ launch entry for flat elementwise ops (csrc/fastops, built by
+    _build.build_fastops), or None when it is not built / loadable."""
+    if not _FAST:
+        mod = None
+        path = os.path.join(os.path.dirname(_build.KERNEL_LIB), "pa_fastops.so")
+        if os.path.exists(path) and os.environ.get("FLAGS_fastops", "1") not in ("0", "false", "False"):
+            try:
+                import importlib.machinery
+                import importlib.util
+
+                lib()  # the kernel library first (RTLD_GLOBAL): the extension links it
+                loader = importlib.machinery.ExtensionFileLoader("pa_fastops", path)
+                spec = importlib.util.spec_from_file_location("pa_fastops", path, loader=loader)
+                mod = importlib.util.module_from_spec(spec)
+                loader.exec_module(mod)
+            except Exception:  # pragma: no cover - a stale / ABI-mismatched build
+                mod = None
+        _FAST.append(mod)
+    return _FAST[0]
+
+
 def stream():
     """torch's current HIP stream of the current device, as a raw handle (the C
     accessor: no Stream object per call -- this runs once per kernel launch)."""

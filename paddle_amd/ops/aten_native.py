@@ -113,9 +113,22 @@ def _coalesce(shape, strides_list):
     return shp, [[sts[k] for _, sts in out] for k in range(len(strides_list))]
 
 
+_FASTFN = []
+
+
+def _fast_fns():
+    F = N.fastops()
+    _FASTFN.append((F.ew0, F.ew1, F.ew2, F.ew3) if F is not None else None)
+    return _FASTFN[0]
+
+
 def _launch(op, out, ins, a=0.0, b=0.0, cdt=None):
     """out[...] = op(ins...) over out's shape; inputs broadcast by stride 0.
     Returns False when the launch does not fit the kernel (caller falls back)."""
+    fns = _FASTFN[0] if _FASTFN else _fast_fns()
+    if fns is not None and len(ins) <= 3 and fns[len(ins)](op, -1 if cdt is None else cdt, out, *ins, float(a),
+                                                              float(b), N.stream()):
+        return True  # contiguous same-shape operands: the C++ entry (csrc/fastops)
     if cdt is None:
         cdt = _cdt(out.dtype if not ins else ins[0].dtype)
     if out.is_contiguous() and all(t.is_contiguous() and t.shape == out.shape for t in ins):
