@@ -47,6 +47,12 @@ from paddle_amd.ops import aten_native as A, oplib  # noqa: E402
 out["direct_add_inplace_us"] = t(lambda: oplib.add_(x, y))
 out["aten_add_inplace_us"] = t(lambda: x.add_(y))
 out["direct_fill_us"] = t(lambda: oplib.fill_(x, 0.0))
+from paddle_amd.ops import _native as _N  # noqa: E402
+
+F = _N.fastops()
+if F is not None:
+    out["fastops_add_inplace_us"] = t(lambda: F.add_(x, y, 1.0))
+    out["fastops_bin_add_us"] = t(lambda: F.bin(50, x, y, 1.0, False))
 z = torch.empty_like(x)
 out["direct_add_out_us"] = t(lambda: A._launch(A.B["add"], z, [x, y], a=1.0))
 

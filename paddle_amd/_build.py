@@ -204,8 +204,9 @@ def build_fastops(verbose: bool = False) -> str:
     flags = ["-O2", "-fPIC", "-std=c++17", "-shared", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
              "-DTORCH_EXTENSION_NAME=pa_fastops", "-DTORCH_API_INCLUDE_EXTENSION_H", "-w"]
     flags += [f"-I{p}" for p in ce.include_paths()] + [f"-I{sysconfig.get_paths()['include']}"]
+    flags += ["-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]  # the HIP runtime headers c10/hip/HIPStream.h needs
     tl = _torch_lib_dir()
-    libs = [f"-L{tl}", f"-Wl,-rpath,{tl}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python",
+    libs = [f"-L{tl}", f"-Wl,-rpath,{tl}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_python",
             f"-L{LIBDIR}", "-lpaddle_amd_kernels", "-Wl,-rpath,$ORIGIN"]
     stamp = hashlib.sha1(" ".join(flags + libs).encode()).hexdigest()
     if not _needs(out, [src, klib], stamp):

@@ -6,6 +6,7 @@
 // ops/aten_native.py's hot path and the framework's direct callers (oplib.add_ /
 // fill_, the eager engine's gradient accumulation) use when it is built.
 // Returns false when the call does not fit (the caller takes the general path).
+#include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
 extern "C" int pa_ew_flat(int op, int cdt, int nin, long n, void* out, int odt, const void* x, int xdt,
@@ -85,9 +86,41 @@ bool ew3(int op, int cdt, const at::Tensor& out, const at::Tensor& x, const at::
   return launch(op, cdt, out, ins, 3, a, b, stream);
 }
 
+void* current_stream(const at::Tensor& t) { return c10::hip::getCurrentHIPStream(t.get_device()).stream(); }
+
+// The binary hot path of the native dispatch (add / sub / mul, out-of-place or in
+// place): every check, the allocation and the launch in C++, on the current stream.
+// Returns None when the call does not fit (the Python handler's general path).
+py::object bin(int op, const at::Tensor& self, const at::Tensor& other, double alpha, bool inplace) {
+  const auto dt = self.scalar_type();
+  if ((dt != c10::ScalarType::Float && dt != c10::ScalarType::BFloat16) || other.scalar_type() != dt ||
+      !self.is_cuda() || !other.is_cuda() || self.dim() == 0 || self.sizes() != other.sizes() ||
+      !self.is_contiguous() || !other.is_contiguous() || self.device() != other.device())
+    return py::none();
+  at::Tensor dst = inplace ? self : at::empty_like(self, at::MemoryFormat::Contiguous);
+  const int code = dt_code(dt);
+  const int rc = pa_ew_flat(op, 0, 2, dst.numel(), dst.data_ptr(), code, self.data_ptr(), code, other.data_ptr(), code,
+                            nullptr, 0, alpha, 0.0, current_stream(self));
+  TORCH_CHECK(rc == 0, "pa_ew_flat failed (rc=", rc, ")");
+  return py::cast(dst);
+}
+
+// Direct framework callers: a += alpha * b, t[...] = v (current stream).
+bool add_(const at::Tensor& a, const at::Tensor& b, double alpha) {
+  const at::Tensor ins[2] = {a, b};
+  return a.is_cuda() && launch(50, -1, a, ins, 2, alpha, 0.0, reinterpret_cast<int64_t>(current_stream(a)));
+}
+
+bool fill_(const at::Tensor& t, double v) {
+  return t.is_cuda() && launch(1, -1, t, nullptr, 0, v, 0.0, reinterpret_cast<int64_t>(current_stream(t)));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(pa_fastops, m) {
+  m.def("bin", &bin, "binary hot path (op, self, other, alpha, inplace) -> tensor or None");
+  m.def("add_", &add_, "a += alpha * b on the current stream");
+  m.def("fill_", &fill_, "t[...] = v on the current stream");
   m.doc() = "C++ launch entry for the framework's flat elementwise kernels";
   m.def("ew0", &ew0, "out = op() (fill / iota)");
   m.def("ew1", &ew1, "out = op(x)");

@@ -261,6 +261,11 @@ def _binary(name, self, other, alpha=1, rounding_mode=None, out=None):
     # checks only, one flat launch
     fb = _FAST_BIN.get(name)
     if fb is not None and out is None and isinstance(other, torch.Tensor):
+        fns = _FASTFN[0] if _FASTFN else _fast_fns()
+        if fns is not None and isinstance(alpha, (int, float)):
+            r = N.fastops().bin(_FAST_OPS[fb[0]], self, other, float(alpha), fb[1])  # all in C++
+            if r is not None:
+                return r
         global _FAST_DT
         if _FAST_DT is None:
             _FAST_DT = {torch.float32: _DT[torch.float32], torch.bfloat16: _DT[torch.bfloat16]}

@@ -43,7 +43,12 @@ def fill_(t, value):
     """t[...] = value on the elementwise kernel of tensor_ops.hip (any device dtype
     and layout the kernel covers; else torch's fill)."""
     if t.is_cuda and t.numel():
+        from . import _native as N
         from . import aten_native as A
+
+        F = N.fastops()
+        if F is not None and F.fill_(t, float(value)):
+            return t
 
         if t.dtype in A._DT and A._launch(A.U["fill"], t, [], a=float(value), cdt=A._cdt(t.dtype)):
             return t
@@ -54,7 +59,12 @@ def add_(a, b):
     """a += b in place on the elementwise kernel (same shape; b's dtype may differ):
     a direct launch, no pass through the ATen dispatcher or the native-dispatch mode."""
     if a.is_cuda and b.is_cuda and a.shape == b.shape and a.numel():
+        from . import _native as N
         from . import aten_native as A
+
+        F = N.fastops()
+        if F is not None and F.add_(a, b, 1.0):
+            return a
 
         if a.dtype in A._DT and b.dtype in A._DT and A._launch(A.B["add"], a, [a, b], a=1.0,
                                                                  cdt=A._cdt(a.dtype)):
