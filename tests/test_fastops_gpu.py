@@ -34,11 +34,11 @@ def test_fastops_elementwise_matches_torch():
 
 
 def test_direct_callers_use_fastops():
-    from paddle_amd.ops import aten_native as A, oplib
+    from paddle_amd.ops import _native as N, oplib
 
     g = torch.ones(64, device="cuda", dtype=torch.bfloat16)
     oplib.add_(g, torch.full_like(g, 2.0))
     assert torch.all(g == 3)
     oplib.fill_(g, 0.0)
     assert not torch.any(g)
-    assert A._FASTFN and A._FASTFN[0] is not None
+    assert N.fastops() is not None
