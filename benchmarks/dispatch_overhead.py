@@ -53,6 +53,7 @@ F = _N.fastops()
 if F is not None:
     out["fastops_add_inplace_us"] = t(lambda: F.add_(x, y, 1.0))
     out["fastops_bin_add_us"] = t(lambda: F.bin(50, x, y, 1.0, False))
+    out["fastops_cast_us"] = t(lambda: F.cast(x, 1))
 z = torch.empty_like(x)
 out["direct_add_out_us"] = t(lambda: A._launch(A.B["add"], z, [x, y], a=1.0))
 

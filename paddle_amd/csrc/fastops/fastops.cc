@@ -105,6 +105,41 @@ py::object bin(int op, const at::Tensor& self, const at::Tensor& other, double a
   return py::cast(dst);
 }
 
+c10::ScalarType from_code(int c) {
+  switch (c) {
+    case 0: return c10::ScalarType::Float;
+    case 1: return c10::ScalarType::BFloat16;
+    case 2: return c10::ScalarType::Half;
+    case 3: return c10::ScalarType::Double;
+    case 4: return c10::ScalarType::Long;
+    case 5: return c10::ScalarType::Int;
+    case 6: return c10::ScalarType::Short;
+    case 7: return c10::ScalarType::Char;
+    case 8: return c10::ScalarType::Byte;
+    case 9: return c10::ScalarType::Bool;
+    default: return c10::ScalarType::Undefined;
+  }
+}
+
+// The cast / copy hot path of the native dispatch (_to_copy / clone of a contiguous
+// device tensor into dtype code `dc`): allocation and launch in C++.  None when the
+// call does not fit.
+py::object cast(const at::Tensor& self, int dc) {
+  const auto odt = from_code(dc);
+  const int sc = dt_code(self.scalar_type());
+  if (odt == c10::ScalarType::Undefined || sc < 0 || !self.is_cuda() || self.dim() == 0 || !self.is_contiguous())
+    return py::none();
+  at::Tensor dst = at::empty(self.sizes(), self.options().dtype(odt));
+  if (self.numel() == 0) return py::cast(dst);
+  // compute in the source's class unless a float is written from an integer source
+  const int cdt = c10::isFloatingType(self.scalar_type()) || !c10::isFloatingType(odt) ? cdt_of(self.scalar_type())
+                                                                                      : cdt_of(odt);
+  const int rc = pa_ew_flat(0, cdt, 1, dst.numel(), dst.data_ptr(), dc, self.data_ptr(), sc, nullptr, 0, nullptr, 0,
+                            0.0, 0.0, current_stream(self));
+  TORCH_CHECK(rc == 0, "pa_ew_flat failed (rc=", rc, ")");
+  return py::cast(dst);
+}
+
 // Direct framework callers: a += alpha * b, t[...] = v (current stream).
 bool add_(const at::Tensor& a, const at::Tensor& b, double alpha) {
   const at::Tensor ins[2] = {a, b};
@@ -119,6 +154,7 @@ bool fill_(const at::Tensor& t, double v) {
 
 PYBIND11_MODULE(pa_fastops, m) {
   m.def("bin", &bin, "binary hot path (op, self, other, alpha, inplace) -> tensor or None");
+  m.def("cast", &cast, "contiguous copy / cast into dtype code -> tensor or None");
   m.def("add_", &add_, "a += alpha * b on the current stream");
   m.def("fill_", &fill_, "t[...] = v on the current stream");
   m.doc() = "C++ launch entry for the framework's flat elementwise kernels";

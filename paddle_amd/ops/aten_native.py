@@ -613,6 +613,12 @@ def _to_copy(name, self, dtype=None, layout=None, device=None, pin_memory=None, 
     if (device is None and memory_format in (None, torch.preserve_format) and self.is_cuda and self.dim() > 0
             and self.is_contiguous()):
         dt = dtype or self.dtype
+        code = _DT.get(dt)
+        F = N.fastops()
+        if F is not None and code is not None:
+            r = F.cast(self, code)  # checks, allocation and launch in C++
+            if r is not None:
+                return r
         dc, sc = _FAST_CODE.get(dt), _FAST_CODE.get(self.dtype)
         if dc is not None and sc is not None:  # hot path: contiguous fp32 <-> bf16 cast / copy
             dst = torch.empty(self.shape, dtype=dt, device=self.device)

@@ -27,6 +27,11 @@ def test_fastops_elementwise_matches_torch():
         assert torch.equal(o32, x.float())
         assert F.ew0(A.U["fill"], -1, out, 3.0, 0.0, st)
         assert torch.all(out == 3)
+    for src, dc, dt in ((torch.float32, 1, torch.bfloat16), (torch.bfloat16, 0, torch.float32),
+                        (torch.int64, 0, torch.float32), (torch.float32, 4, torch.int64)):
+        x = (torch.randn(33, 8, device="cuda") * 10).to(src)
+        r = F.cast(x, dc)
+        assert r.dtype == dt and torch.equal(r, x.to(dt))
     # broadcast / non-contiguous operands: declined
     x = torch.randn(8, 4, device="cuda")
     assert not F.ew2(A.B["add"], -1, torch.empty_like(x), x, torch.randn(4, device="cuda"), 1.0, 0.0, st)
