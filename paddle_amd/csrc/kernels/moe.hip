@@ -149,7 +149,10 @@ __global__ __launch_bounds__(kRouteT) void moe_route_count_kernel(const long* __
     for (long r = (long)blockIdx.x * kRouteT + tid; r < (long)E * cap; r += (long)gridDim.x * kRouteT) src[r] = 0;
   __syncthreads();
   const long i = (long)blockIdx.x * kRouteT + tid;
-  if (i < n) atomicAdd(&h[(int)flat_e[i]], 1);
+  if (i < n) {
+    const long e = flat_e[i];
+    if (e >= 0 && e < E) atomicAdd(&h[(int)e], 1);  // an out-of-range expert id is dropped, never indexed
+  }
   __syncthreads();
   for (int e = tid; e < E; e += kRouteT) cnt[(long)blockIdx.x * E + e] = h[e];
 }
@@ -190,7 +193,8 @@ __global__ __launch_bounds__(kRouteT) void moe_route_place_kernel(const long* __
   for (int e = tid; e < E; e += kRouteT) base[e] = run[(long)blockIdx.x * E + e];
   __syncthreads();
   const long i = (long)blockIdx.x * kRouteT + tid;
-  const int e = i < n ? (int)flat_e[i] : -1;
+  const long ev = i < n ? flat_e[i] : -1;
+  const int e = ev >= 0 && ev < E ? (int)ev : -1;
   int r = 0, c = 0;  // rank among / count of this wave's lanes with expert e
   for (int j = 0; j < 64; ++j) {
     const int ej = __shfl(e, j, 64);
@@ -214,6 +218,8 @@ __global__ __launch_bounds__(kRouteT) void moe_route_place_kernel(const long* __
       if (mode != 1) e_sorted[row] = e;
     }
     pos[i] = row;
+  } else if (i < n) {
+    pos[i] = -1;  // out-of-range expert id: the slot is dropped
   }
 }
 
