@@ -1401,3 +1401,43 @@ PA_EXPORT int pa_conv_gemm_bnbwd(const void* src, const void* wt, void* out, con
   if (bx) return gemm::launch_v<true, true, false, false, true, true, false, 0, true>(p, 1, st);
   return gemm::launch_v<true, true, false, false, true, true>(p, 1, st);
 }
+
+// Split-K epilogue: out[m, n] (bf16, row stride ldc) = sum_s part[s][m][n] (+ bias[n]).
+// The GEMM of a shape with too few 256x256 tiles to fill the chip (e.g. T = 4096 tokens
+// x 5120 outputs = 320 tiles on 256 CUs: two rounds for 1.25 rounds of work) runs as
+// S k-slices into fp32 slabs; this pass sums them in a fixed order (deterministic).
+namespace pa {
+__global__ __launch_bounds__(256) void gemm_splitk_sum_kernel(const float* __restrict__ part, int S, long M, int N,
+                                                            const void* __restrict__ bias, int bias_f32,
+                                                            u16* __restrict__ out, long ldc) {
+  const int nc = N / 8;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= M * nc) return;
+  const long m = idx / nc;
+  const int n0 = (int)(idx % nc) * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < S; ++s) {
+    float v[8];
+    load8(part + ((long)s * M + m) * N + n0, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += v[e];
+  }
+  if (bias) {
+    float bv[8];
+    if (bias_f32) load8((const float*)bias + n0, bv);
+    else load8((const u16*)bias + n0, bv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += bv[e];
+  }
+  store8(out + m * ldc + n0, acc);
+}
+}  // namespace pa
+
+PA_EXPORT int pa_gemm_splitk_sum(const float* part, int S, long M, int N, const void* bias, int bias_f32, void* out,
+                               long ldc, hipStream_t st) {
+  if (S <= 0 || M <= 0 || N <= 0 || (N % 8) || (ldc % 8)) return -1;
+  const long n = M * (N / 8);
+  hipLaunchKernelGGL(pa::gemm_splitk_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, S, M, N,
+                     bias, bias_f32, (u16*)out, ldc);
+  PA_LAUNCH_CHECK();
+}

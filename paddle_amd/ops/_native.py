@@ -189,6 +189,7 @@ _SIGS = {
     "pa_group_cat_offsets": [_I, _P, _I, _P, _P, _P],
     "pa_group_image": [_I, _I, _P, _P, _P, _P, _P, _I, _L, _I, _P, _P, _L, _P, _P],
     "pa_fa_gqa_fold": [_P, _P, _P, _P, _L, _I, _I, _I, _L, _P],
+    "pa_gemm_splitk_sum": [_P, _I, _L, _I, _P, _I, _P, _L, _P],
     "pa_moe_reduce": [_P, _P, _P, _P, _L, _I, _I, _P],
     "pa_moe_combine_bwd": [_P, _P, _P, _P, _P, _P, _L, _I, _I, _P],
     "pa_moe_route": [_P, _L, _I, _I, _I, _L, _P, _P, _P, _P, _P, _P],

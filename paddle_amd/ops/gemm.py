@@ -46,10 +46,74 @@ def supported(M, N, K, *mats) -> bool:
     return True
 
 
+_SPLITK = os.environ.get("FLAGS_gemm_splitk", "1") not in ("0", "false", "False")
+_NCU = []
+
+
+def _num_cu():
+    if not _NCU:
+        _NCU.append(torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count)
+    return _NCU[0]
+
+
+def split_k_for(M, N, K):
+    """k-slices for a GEMM whose 256x256 tile count leaves the last round of the
+    persistent grid mostly idle (320 tiles on 256 CUs run two rounds for 1.25 rounds of
+    work).  Cost of s slices, in units of the ideal GEMM time: 1 / (filled fraction of
+    the tile rounds) + the fp32 slab traffic of the slices and the summing pass,
+    (4s + 2) bytes per output against the GEMM's 2K flops at ~1.45 PF / ~4.5 TB/s.  A
+    split is taken when it saves >= 10 %; 1 = no split."""
+    if not _SPLITK:
+        return 1
+    ncu = _num_cu()
+    tiles = ((M + 255) // 256) * ((N + 255) // 256)
+    if tiles >= 4 * ncu:
+        return 1
+
+    def eff(t):
+        return t / (((t + ncu - 1) // ncu) * ncu)
+
+    base = 1.0 / eff(tiles)
+    best, best_s = base, 1
+    for s in (2, 3, 4, 6, 8):
+        if K // s < 1024:
+            break
+        c = 1.0 / eff(tiles * s) + (4 * s + 2) * 161.0 / K
+        if c < best:
+            best, best_s = c, s
+    return best_s if best < 0.9 * base else 1
+
+
+def _gemm_splitk(a, b, M, N, K, s, a_kmaj, b_kmaj, out, bias):
+    """bf16 C = A.B (+ bias) as ``s`` k-slices into fp32 slabs and one summing pass."""
+    ks = ((K + s - 1) // s + 63) // 64 * 64
+    s = (K + ks - 1) // ks
+    lda, ldb = a.stride(-2), b.stride(-2)
+    part = torch.empty(s, M, N, dtype=torch.float32, device=a.device)
+    rc = _nat.lib().pa_gemm(int(a_kmaj), int(b_kmaj), 1, _nat.ptr(a), _nat.ptr(b), _nat.ptr(part), None, M, N, ks,
+                            lda, ldb, N, ks if a_kmaj else ks * lda, ks if b_kmaj else ks * ldb, M * N, s, 1.0, 0, K,
+                            0, None, 0, _nat.stream())
+    if rc != 0:
+        raise RuntimeError(f"pa_gemm (split-K {s}) failed (rc={rc}) M={M} N={N} K={K}")
+    _nat.call("pa_gemm_splitk_sum", _nat.ptr(part), s, M, N, _nat.ptr(bias), int(bias is not None and
+                                                                                bias.dtype == torch.float32),
+              _nat.ptr(out), out.stride(-2), _nat.stream())
+    return out
+
+
 def gemm(a, b, M, N, K, *, a_kmaj, b_kmaj, out=None, out_dtype=torch.bfloat16, bias=None, alpha=1.0,
          accumulate=False, batch=1, sA=0, sB=0, sC=0, ldc=None, k_total=0, atomic=False, grp=None, grp_mode=0):
     """Raw launcher.  ``a``/``b``: bf16 CUDA tensors with unit inner stride, row
-    stride = their ld.  ``out``: [M, ldc] (bf16 or fp32) written or accumulated."""
+    stride = their ld.  ``out``: [M, ldc] (bf16 or fp32) written or accumulated.
+    A plain bf16-out GEMM with too few tiles for the chip runs split-K
+    (:func:`split_k_for`)."""
+    if (batch == 1 and not accumulate and not k_total and not atomic and grp is None and alpha == 1.0
+            and (out is None or out.dtype == torch.bfloat16) and out_dtype == torch.bfloat16 and ldc is None):
+        s = split_k_for(M, N, K)
+        if s > 1:
+            if out is None:
+                out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+            return _gemm_splitk(a, b, M, N, K, s, a_kmaj, b_kmaj, out, bias)
     if out is None:
         out = torch.empty(M, N, dtype=out_dtype, device=a.device) if batch == 1 else \
             torch.empty(batch, M, N, dtype=out_dtype, device=a.device)
