@@ -222,17 +222,29 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
 // Column sum of a [G, H] fp32 partial matrix into out[H] (dtype T).  Each block
 // owns 64 columns; its 4 waves split the G rows and fold through LDS, so H/64
 // blocks x 4 waves cover the chip even for H = 4096 (64 blocks).
+// 16 waves per 64 columns (each sums G/16 partial rows, fixed order), grid.y = 1 or
+// 2 partial sets (dW, and dB for LayerNorm) in one launch: with 4 waves the 128
+// dependent loads per thread at G = 512 left this pass latency-bound (~38 us at H 5120).
 template <typename T>
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, T* __restrict__ out, int G, int H) {
-  __shared__ float red[4][64];
+__global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ part0, T* __restrict__ out0,
+                                                      const float* __restrict__ part1, T* __restrict__ out1, int G,
+                                                      int H) {
+  __shared__ float red[16][64];
+  const float* part = blockIdx.y ? part1 : part0;
+  T* out = blockIdx.y ? out1 : out0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   float s = 0.f;
   if (c < H)
-    for (int g = w; g < G; g += 4) s += part[(long)g * H + c];
+    for (int g = w; g < G; g += 16) s += part[(long)g * H + c];
   red[w][lane] = s;
   __syncthreads();
-  if (w == 0 && c < H) IO<T>::st(out, c, red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
+  if (w == 0 && c < H) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][lane];
+    IO<T>::st(out, c, t);
+  }
 }
 
 template <typename T, int MAXV>
@@ -300,8 +312,9 @@ static int launch_bwd(bool rms, const void* dy, const void* h, const void* w, co
     launch_bwd_k<T, 4, 2>(rms, DY, Hh, W, mean, rstd, DR, DX, dwp, dbp, N, H, rpb, G, shm, st);
   else
     launch_bwd_k<T, MV, WPR>(rms, DY, Hh, W, mean, rstd, DR, DX, dwp, dbp, N, H, rpb, G, shm, st);
-  hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 63) / 64), dim3(256), 0, st, dwp, (T*)dw, G, H);
-  if (!rms && db) hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 63) / 64), dim3(256), 0, st, dbp, (T*)db, G, H);
+  const bool two = !rms && db;
+  hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 63) / 64, two ? 2 : 1), dim3(1024), 0, st, dwp, (T*)dw,
+                     two ? dbp : dwp, two ? (T*)db : (T*)dw, G, H);
   PA_LAUNCH_CHECK();
 }
 
