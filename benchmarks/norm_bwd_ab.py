@@ -13,17 +13,20 @@ CHILD = r"""
 import json, sys, torch
 sys.path.insert(0, %r)
 from paddle_amd.ops import _native as N
-T, H = 16384, 4096
+T, H, RMS = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
 dy = torch.randn(T, H, device="cuda", dtype=torch.bfloat16)
 h = torch.randn(T, H, device="cuda", dtype=torch.bfloat16)
 dres = torch.randn(T, H, device="cuda", dtype=torch.bfloat16)
 w = torch.rand(H, device="cuda", dtype=torch.bfloat16)
 rstd = torch.rand(T, device="cuda") + 0.5
 dx = torch.empty_like(h); dw = torch.empty_like(w)
-ws = torch.empty(2 * 512 * H, device="cuda")
+ws = torch.empty(2 * 1024 * H, device="cuda")
+mean = torch.randn(T, device="cuda")
+b = torch.rand(H, device="cuda", dtype=torch.bfloat16)
+db = torch.empty_like(w)
 def run():
-    N.call("pa_norm_bwd", 1, 1, N.ptr(dy), N.ptr(h), N.ptr(w), None, N.ptr(rstd), N.ptr(dres), N.ptr(dx),
-           N.ptr(dw), None, N.ptr(ws), T, H, N.stream())
+    N.call("pa_norm_bwd", 1, RMS, N.ptr(dy), N.ptr(h), N.ptr(w), None if RMS else N.ptr(mean), N.ptr(rstd),
+           N.ptr(dres), N.ptr(dx), N.ptr(dw), None if RMS else N.ptr(db), N.ptr(ws), T, H, N.stream())
 for _ in range(5): run()
 torch.cuda.synchronize()
 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -36,9 +39,13 @@ print(json.dumps({"ms": round(ms, 4), "TBps": round(4 * T * H * 2 / ms / 1e9, 2)
                   "dx_sum": float(ref.double().sum()), "dw_sum": float(dw.double().sum())}))
 """ % ROOT
 
-for name, env in (("base", {}), ("wpr2", {"PA_NORM_BWD_WPR2": "1"}), ("g256", {"PA_NORM_BWD_G": "256"}),
-                  ("wpr2_g256", {"PA_NORM_BWD_WPR2": "1", "PA_NORM_BWD_G": "256"})):
-    e = dict(os.environ, **env)
-    out = subprocess.run([sys.executable, "-c", CHILD], env=e, capture_output=True, text=True, timeout=300)
-    line = out.stdout.strip().splitlines()[-1] if out.stdout.strip() else out.stderr[-500:]
-    print(json.dumps({"variant": name, **(json.loads(line) if line.startswith("{") else {"error": line})}), flush=True)
+SHAPES = [(16384, 4096, 1), (4096, 5120, 0)]  # LLaMA-7B RMSNorm, GPT-3 13B LayerNorm (mb 2)
+for T_, H_, rms in SHAPES:
+    for name, env in (("g512", {"PA_NORM_BWD_G": "512"}), ("g1024", {"PA_NORM_BWD_G": "1024"}),
+                      ("g256", {"PA_NORM_BWD_G": "256"})):
+        e = dict(os.environ, **env)
+        out = subprocess.run([sys.executable, "-c", CHILD, str(T_), str(H_), str(rms)], env=e, capture_output=True,
+                             text=True, timeout=300)
+        line = out.stdout.strip().splitlines()[-1] if out.stdout.strip() else out.stderr[-500:]
+        print(json.dumps({"shape": [T_, H_, rms], "variant": name,
+                          **(json.loads(line) if line.startswith("{") else {"error": line})}), flush=True)

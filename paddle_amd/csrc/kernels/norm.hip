@@ -288,8 +288,8 @@ template <typename T, int MAXV>
 static int launch_bwd(bool rms, const void* dy, const void* h, const void* w, const float* mean,
                       const float* rstd, const void* dres, void* dx, void* dw, void* db,
                       float* ws, long N, int H, hipStream_t st) {
-  // (capped at 512: callers size the workspace for 512 partial rows)
-  static const int gcap = env_int("PA_NORM_BWD_G", 512) < 512 ? env_int("PA_NORM_BWD_G", 512) : 512;
+  // (capped at 1024: callers size the workspace for 1024 partial rows)
+  static const int gcap = env_int("PA_NORM_BWD_G", 512) < 1024 ? env_int("PA_NORM_BWD_G", 512) : 1024;
   static const int wpr2 = env_int("PA_NORM_BWD_WPR2", 1);  // default: profiles/r5_norm_bwd_ab.log (-6 %)
   long G0 = (N + 3) / 4; int G = (int)(G0 < gcap ? G0 : gcap);  // measured best of 256 / 512 / 1024 (benchmarks/norm_bench.py)
   if (G < 1) G = 1;

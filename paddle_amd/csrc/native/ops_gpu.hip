@@ -1411,7 +1411,7 @@ void k_layer_norm_grad(const OpRun& r) {
   const float eps = r.op.GetFloat("epsilon", 1e-5f);
   float* rstd = workspace(r, "@ln_rstd@", rows);
   hipLaunchKernelGGL(var_to_rstd_kernel, dim3(grid_for(rows)), dim3(256), 0, S(r), f32(var), rstd, rows, eps);
-  const int64_t parts = std::min<int64_t>(512, (rows + 3) / 4);
+  const int64_t parts = std::min<int64_t>(1024, (rows + 3) / 4);  // the kernel's block cap (norm.hip)
   float* ws = workspace(r, "@ln_ws@", 2 * parts * H);
   float* dx = r.out("X@GRAD") ? out_f32(r, "X@GRAD", x.dims) : workspace(r, "@ln_dx@", rows * H);
   float* dw = (sc && r.out("Scale@GRAD")) ? out_f32(r, "Scale@GRAD", sc->dims) : workspace(r, "@ln_dw@", H);

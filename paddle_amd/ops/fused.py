@@ -117,7 +117,7 @@ class _NormFn(torch.autograd.Function):
         dx = torch.empty_like(h)
         dw = torch.empty_like(w)
         db = torch.empty_like(w) if ctx.has_b else None
-        G = min(512, (Nr + 3) // 4)
+        G = min(1024, (Nr + 3) // 4)  # workspace for the kernel's block cap (norm.hip)
         ws = _ws(2 * max(G, 1) * H, h.device)
         N.call("pa_norm_bwd", N.dt(h), int(ctx.rms), N.ptr(dy2), N.ptr(h), N.ptr(w), N.ptr(mean), N.ptr(rstd),
                N.ptr(dres), N.ptr(dx), N.ptr(dw), N.ptr(db), N.ptr(ws), Nr, H, N.stream())
@@ -144,7 +144,7 @@ def layer_norm_stats_grad(dy2, x2, w, mean, rstd, has_b):
     dx = torch.empty_like(x2)
     dw = torch.empty_like(w)
     db = torch.empty_like(w) if has_b else None
-    G = min(512, (Nr + 3) // 4)
+    G = min(1024, (Nr + 3) // 4)  # workspace for the kernel's block cap (norm.hip)
     ws = _ws(2 * max(G, 1) * H, x2.device)
     N.call("pa_norm_bwd", N.dt(x2), 0, N.ptr(dy2), N.ptr(x2), N.ptr(w), N.ptr(_c(mean)), N.ptr(_c(rstd)), None,
            N.ptr(dx), N.ptr(dw), N.ptr(db), N.ptr(ws), Nr, H, N.stream())
