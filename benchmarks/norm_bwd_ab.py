@@ -41,8 +41,8 @@ print(json.dumps({"ms": round(ms, 4), "TBps": round(4 * T * H * 2 / ms / 1e9, 2)
 
 SHAPES = [(16384, 4096, 1), (4096, 5120, 0)]  # LLaMA-7B RMSNorm, GPT-3 13B LayerNorm (mb 2)
 for T_, H_, rms in SHAPES:
-    for name, env in (("g512", {"PA_NORM_BWD_G": "512"}), ("g1024", {"PA_NORM_BWD_G": "1024"}),
-                      ("g256", {"PA_NORM_BWD_G": "256"})):
+    for name, env in (("rpb4_g512", {"PA_NORM_BWD_RPB": "4"}), ("rpb16", {"PA_NORM_BWD_RPB": "16"}),
+                      ("rpb32", {"PA_NORM_BWD_RPB": "32"}), ("rpb64", {"PA_NORM_BWD_RPB": "64"})):
         e = dict(os.environ, **env)
         out = subprocess.run([sys.executable, "-c", CHILD, str(T_), str(H_), str(rms)], env=e, capture_output=True,
                              text=True, timeout=300)
