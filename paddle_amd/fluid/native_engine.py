@@ -199,11 +199,21 @@ class NativeEngine:
                     return False
         dev = isinstance(place, core.CUDAPlace)
         kern = set(native.registered_ops(False)) | (set(native.registered_ops(True)) if dev else set())
-        if any(op.type not in kern and op.type not in _NATIVE_CF for op in all_ops):
+        fallback = [op for op in all_ops if op.type not in kern and op.type not in _NATIVE_CF]
+        if fallback:
             from .. import core_ext
 
             if os.environ.get("FLAGS_native_binding", "") == "ctypes" or core_ext.module() is None:
                 return False
+            # the per-op Python fallback bridges dense tensors only: an op without a C++
+            # kernel that reads or writes a tensor array / rank table / step scopes /
+            # SelectedRows keeps the program on the interpreter
+            vtype = {n: v.type for b in program.blocks for n, v in b.vars.items()}
+            dense = {VT.LOD_TENSOR, VT.FEED_MINIBATCH, VT.FETCH_LIST}
+            for op in fallback:
+                names = [n for ns in list(op.inputs.values()) + list(op.outputs.values()) for n in ns]
+                if any(vtype.get(n, VT.LOD_TENSOR) not in dense for n in names):
+                    return False
         return True
 
     def _program(self, program):
