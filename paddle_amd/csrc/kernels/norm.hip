@@ -291,9 +291,10 @@ static int launch_bwd(bool rms, const void* dy, const void* h, const void* w, co
   // (capped at 1024: callers size the workspace for 1024 partial rows)
   static const int gcap = env_int("PA_NORM_BWD_G", 512) < 1024 ? env_int("PA_NORM_BWD_G", 512) : 1024;
   static const int wpr2 = env_int("PA_NORM_BWD_WPR2", 1);  // default: profiles/r5_norm_bwd_ab.log (-6 %)
-  // rows per block >= PA_NORM_BWD_RPB (default 32): measured best at both [16384, 4096]
-  // (512 blocks) and [4096, 5120] (fewer blocks, less partial-sum traffic), norm_bwd_ab.py
-  static const int rpb_min = env_int("PA_NORM_BWD_RPB", 32) > 0 ? env_int("PA_NORM_BWD_RPB", 32) : 4;
+  // rows per block >= PA_NORM_BWD_RPB (default 16): [16384, 4096] 0.158 ms at 512 blocks,
+  // [4096, 5120] LayerNorm 0.081 ms at 256 blocks vs 0.114 at 512 / 0.116 at 128
+  // (profiles/r5_norm_bwd_ab.log)
+  static const int rpb_min = env_int("PA_NORM_BWD_RPB", 16) > 0 ? env_int("PA_NORM_BWD_RPB", 16) : 4;
   long G0 = (N + rpb_min - 1) / rpb_min; int G = (int)(G0 < gcap ? G0 : gcap);
   if (G < 1) G = 1;
   long rpb = (N + G - 1) / G;
