@@ -293,7 +293,7 @@ static int launch_bwd(bool rms, const void* dy, const void* h, const void* w, co
   static const int wpr2 = env_int("PA_NORM_BWD_WPR2", 1);  // default: profiles/r5_norm_bwd_ab.log (-6 %)
   // rows per block >= PA_NORM_BWD_RPB (default 16): [16384, 4096] 0.158 ms at 512 blocks,
   // [4096, 5120] LayerNorm 0.081 ms at 256 blocks vs 0.114 at 512 / 0.116 at 128
-  // (profiles/r5_norm_bwd_ab.log)
+  // (profiles/r5_norm_bwd_rpb_ab.log)
   static const int rpb_min = env_int("PA_NORM_BWD_RPB", 16) > 0 ? env_int("PA_NORM_BWD_RPB", 16) : 4;
   long G0 = (N + rpb_min - 1) / rpb_min; int G = (int)(G0 < gcap ? G0 : gcap);
   if (G < 1) G = 1;
