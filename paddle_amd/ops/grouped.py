@@ -201,6 +201,9 @@ def _expert_wgrads(gate_up, down, x, dh, a, dy, offs, fp8, needs):
         return None
     key = id(gate_up)
     lst = _STASH.get(key, [])
+    if lst and lst[0][0] is not gate_up:  # a stale entry of a freed layer that reused the id
+        _STASH.pop(key, None)
+        lst = []
     if _accum.deferring() and len(lst) < _MAX_MB - 1:
         _STASH.setdefault(key, []).append((gate_up, down, x, dh, a, dy, offs, fp8))
         return None, None

@@ -169,7 +169,8 @@ class Optimizer:
             return True
         groups = {}
         for p in ps:
-            if not p.grad.is_contiguous() or p.grad.dtype not in (torch.float32, torch.bfloat16, torch.float16):
+            if (p.grad.layout != torch.strided or not p.grad.is_contiguous()
+                    or p.grad.dtype not in (torch.float32, torch.bfloat16, torch.float16)):
                 return False
             groups.setdefault((p.grad.device, p.grad.dtype), []).append(p)
         bufs, ptrs = [], {}
