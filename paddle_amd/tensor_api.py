@@ -101,16 +101,37 @@ def _shape(s):
     return [int(x) if not torch.is_tensor(x) else int(x.item()) for x in ([s] if isinstance(s, int) else s)]
 
 
+def _filled(shape, value, dtype, device):
+    """A new tensor of ``value``: on a GPU the framework's fill kernel (ops/oplib.py ->
+    tensor_ops.hip / csrc/fastops), no ATen fill."""
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    if dev.type == "cuda" and not isinstance(value, complex):
+        from .ops import oplib
+
+        with torch._C.DisableTorchFunctionSubclass():
+            return oplib.fill_(torch.empty(shape, dtype=dtype, device=dev), value)
+    return torch.full(shape, value, dtype=dtype, device=dev)
+
+
+def _filled_like(x, value, dtype):
+    dt = _dtype(dtype) or x.dtype
+    if x.is_cuda:
+        return _filled(list(x.shape), value, dt, x.device)
+    return torch.full_like(x, value, dtype=dt)
+
+
 def zeros(shape, dtype=None, name=None):
-    return torch.zeros(_shape(shape), dtype=_dtype(dtype) or _default_dtype[0], device=_dev())
+    return _filled(_shape(shape), 0, _dtype(dtype) or _default_dtype[0], _dev())
 
 
 def ones(shape, dtype=None, name=None):
-    return torch.ones(_shape(shape), dtype=_dtype(dtype) or _default_dtype[0], device=_dev())
+    return _filled(_shape(shape), 1, _dtype(dtype) or _default_dtype[0], _dev())
 
 
 def full(shape, fill_value, dtype=None, name=None):
-    return torch.full(_shape(shape), fill_value, dtype=_dtype(dtype) or _default_dtype[0], device=_dev())
+    if torch.is_tensor(fill_value):
+        fill_value = fill_value.item()
+    return _filled(_shape(shape), fill_value, _dtype(dtype) or _default_dtype[0], _dev())
 
 
 def empty(shape, dtype=None, name=None):
@@ -118,15 +139,17 @@ def empty(shape, dtype=None, name=None):
 
 
 def zeros_like(x, dtype=None, name=None):
-    return torch.zeros_like(x, dtype=_dtype(dtype))
+    return _filled_like(x, 0, dtype)
 
 
 def ones_like(x, dtype=None, name=None):
-    return torch.ones_like(x, dtype=_dtype(dtype))
+    return _filled_like(x, 1, dtype)
 
 
 def full_like(x, fill_value, dtype=None, name=None):
-    return torch.full_like(x, fill_value, dtype=_dtype(dtype))
+    if torch.is_tensor(fill_value):
+        fill_value = fill_value.item()
+    return _filled_like(x, fill_value, dtype)
 
 
 def empty_like(x, dtype=None, name=None):
