@@ -1104,6 +1104,10 @@ static int launch_g(const Params& p, int batch, hipStream_t st) {
       if (p.K % BKT == 0 && p.k_total % BKT == 0)  // every k-tile full: the k range check is wave-uniform
         return pf ? launch_v<AK, BK, F32, true, true, false, false, GM>(p, batch, st)
                   : launch_v<AK, BK, F32, false, true, false, false, GM>(p, batch, st);
+    } else if constexpr (AK && BK) {
+      // grouped-K over token images: every group's column range is a multiple of 64
+      // (fp8.hip pa_group_image pads each expert to 64 tokens), so k-tiles are full
+      if (p.K % BKT == 0) return launch_v<AK, BK, F32, false, true, false, false, GM>(p, batch, st);
     }
     return pf ? launch_v<AK, BK, F32, true, false, false, false, GM>(p, batch, st)
               : launch_v<AK, BK, F32, false, false, false, false, GM>(p, batch, st);
