@@ -7,6 +7,8 @@
 // batch_norm_op.cu.cc:170 (cuDNN BN), math/pooling.cu:25-189 (pool2d fwd/bwd).
 // Layout here is NHWC throughout, so a 16-byte vector is 8 consecutive channels
 // of one pixel; every kernel moves 16 B per lane (guide Guideline 13).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace pa {
@@ -229,6 +231,9 @@ __global__ __launch_bounds__(1024) void bn_finalize_fwd_kernel(const float* __re
 // y = (x - mean) * rstd * w + b (+ relu); w, b fp32 or bf16 per `wdt` (0 f32, 1 bf16).
 // The launch makes the thread count a multiple of C/8, so a thread keeps one channel
 // chunk for its whole grid-stride loop and folds (mean, rstd, w, b) into one FMA.
+// U chunks in flight per thread; NT: non-temporal stores (the output is read by the next
+// conv, not by this kernel: keep it out of the way of the streaming loads)
+template <int U, bool NT>
 __global__ void bn_apply_kernel(const u16* __restrict__ x, u16* __restrict__ y, const float* __restrict__ mean,
                                 const float* __restrict__ rstd, const void* __restrict__ w, const void* __restrict__ b,
                                 int wdt, long rows, int C, int relu, const u16* __restrict__ res) {
@@ -246,9 +251,8 @@ __global__ void bn_apply_kernel(const u16* __restrict__ x, u16* __restrict__ y, 
     sc[j] = rstd[c] * ww;
     sf[j] = bb - mean[c] * sc[j];
   }
-  // 4 chunks in flight per thread: every load of a group is issued before the first
+  // U chunks in flight per thread: every load of a group is issued before the first
   // store (y may alias nothing the loads read, but the compiler cannot know that)
-  constexpr int U = 4;
   long i = i0;
   for (; i + (U - 1) * stride < total; i += U * stride) {
     u16x8 xa[U], ra[U];
@@ -265,7 +269,14 @@ __global__ void bn_apply_kernel(const u16* __restrict__ x, u16* __restrict__ y, 
         const float v = fmaf(bf2f(xa[u][j]), sc[j], sf[j]) + (res ? bf2f(ra[u][j]) : 0.f);
         a[j] = relu ? fmaxf(v, 0.f) : v;
       }
-      store8(y + (i + u * stride) * 8, a);
+      if constexpr (NT) {
+        u16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(a[j]);
+        __builtin_nontemporal_store(o, reinterpret_cast<u16x8*>(y + (i + u * stride) * 8));
+      } else {
+        store8(y + (i + u * stride) * 8, a);
+      }
     }
   }
   for (; i < total; i += stride) {
@@ -283,6 +294,27 @@ __global__ void bn_apply_kernel(const u16* __restrict__ x, u16* __restrict__ y, 
       a[j] = relu ? fmaxf(v, 0.f) : v;
     }
     store8(y + i * 8, a);
+  }
+}
+
+// A/B knob PA_BN_APPLY: 0 = 4 chunks in flight, 1 = 8, 2 = 4 + non-temporal stores,
+// 3 = 8 + non-temporal stores
+static int bn_apply_variant() {
+  static const int v = [] {
+    const char* e = getenv("PA_BN_APPLY");
+    return e && *e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+static void launch_bn_apply(dim3 g, dim3 blk, hipStream_t st, const u16* x, u16* y, const float* mean,
+                            const float* rstd, const void* w, const void* b, int wdt, long rows, int C, int relu,
+                            const u16* res) {
+  switch (bn_apply_variant()) {
+    case 1: hipLaunchKernelGGL((bn_apply_kernel<8, false>), g, blk, 0, st, x, y, mean, rstd, w, b, wdt, rows, C, relu, res); break;
+    case 2: hipLaunchKernelGGL((bn_apply_kernel<4, true>), g, blk, 0, st, x, y, mean, rstd, w, b, wdt, rows, C, relu, res); break;
+    case 3: hipLaunchKernelGGL((bn_apply_kernel<8, true>), g, blk, 0, st, x, y, mean, rstd, w, b, wdt, rows, C, relu, res); break;
+    default: hipLaunchKernelGGL((bn_apply_kernel<4, false>), g, blk, 0, st, x, y, mean, rstd, w, b, wdt, rows, C, relu, res);
   }
 }
 
@@ -604,7 +636,7 @@ PA_EXPORT int pa_bn_fwd_train(const void* x, void* y, const void* w, const void*
                      (const float*)nullptr, C, rows, eps, momentum, mean, rstd, run_mean, run_var, run_mean != nullptr);
   int eg, eb;
   bn_ew_launch(rows, C, eg, eb);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(eg), dim3(eb), 0, st, (const u16*)x, (u16*)y, mean, rstd, w, b, wdt, rows,
+  launch_bn_apply(dim3(eg), dim3(eb), st, (const u16*)x, (u16*)y, mean, rstd, w, b, wdt, rows,
                      C, relu, (const u16*)res);
   PA_LAUNCH_CHECK();
 }
@@ -619,7 +651,7 @@ PA_EXPORT int pa_bn_fwd_stats(const float* part, int G, const float* shift, cons
                      shift, C, rows, eps, momentum, mean, rstd, run_mean, run_var, run_mean != nullptr);
   int eg, eb;
   bn_ew_launch(rows, C, eg, eb);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(eg), dim3(eb), 0, st, (const u16*)x, (u16*)y, mean, rstd, w, b, wdt, rows,
+  launch_bn_apply(dim3(eg), dim3(eb), st, (const u16*)x, (u16*)y, mean, rstd, w, b, wdt, rows,
                      C, relu, (const u16*)res);
   PA_LAUNCH_CHECK();
 }
@@ -630,7 +662,7 @@ PA_EXPORT int pa_bn_apply(const void* x, void* y, const float* mean, const float
   if (C % 8) return -1;
   int eg, eb;
   bn_ew_launch(rows, C, eg, eb);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(eg), dim3(eb), 0, st, (const u16*)x, (u16*)y, mean, rstd, w, b, wdt, rows,
+  launch_bn_apply(dim3(eg), dim3(eb), st, (const u16*)x, (u16*)y, mean, rstd, w, b, wdt, rows,
                      C, relu, (const u16*)nullptr);
   PA_LAUNCH_CHECK();
 }
