@@ -297,12 +297,21 @@ __global__ void bn_apply_kernel(const u16* __restrict__ x, u16* __restrict__ y, 
   }
 }
 
+// A/B knob PA_BN_DX: 1 (default) = 4 chunks in flight + non-temporal stores, 0 = one at a time
+static int bn_dx_unroll() {
+  static const int v = [] {
+    const char* e = getenv("PA_BN_DX");
+    return e && *e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 // A/B knob PA_BN_APPLY: 0 = 4 chunks in flight, 1 = 8, 2 = 4 + non-temporal stores,
 // 3 = 8 + non-temporal stores
 static int bn_apply_variant() {
   static const int v = [] {
     const char* e = getenv("PA_BN_APPLY");
-    return e && *e ? atoi(e) : 0;
+    return e && *e ? atoi(e) : 2;  // default: 4 in flight + non-temporal stores (benchmarks/bn_apply_ab.py)
   }();
   return v;
 }
@@ -340,7 +349,7 @@ __global__ __launch_bounds__(1024) void bn_finalize_bwd_kernel(const float* __re
 // dx = k1 * dy' - k1 * k2 - k3 * (x - mean)   (fixed channel chunk per thread, as bn_apply)
 __global__ void bn_dx_kernel(const u16* __restrict__ x, const u16* __restrict__ dy, BnMask mk,
                              const float* __restrict__ mean, const float* __restrict__ coef, u16* __restrict__ dx,
-                             long rows, int C, int relu, u16* __restrict__ dres) {
+                             long rows, int C, int relu, u16* __restrict__ dres, int unroll) {
   const u16* __restrict__ y = mk.y;
   const int chunks = C / 8;
   const long total = rows * chunks;
@@ -357,7 +366,41 @@ __global__ void bn_dx_kernel(const u16* __restrict__ x, const u16* __restrict__ 
   }
   float msc[8], msf[8];
   if (relu && !y) bn_affine8(ch, mean, mk.rstd, mk.w, mk.b, mk.wdt, msc, msf);
-  for (long i = i0; i < total; i += stride) {
+  long i = i0;
+  // 4 chunks in flight (all loads of a group before its stores), non-temporal stores
+  constexpr int U = 4;
+  for (; unroll && i + (U - 1) * stride < total; i += U * stride) {
+    u16x8 xa[U], ga[U], ya[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      xa[u] = *reinterpret_cast<const u16x8*>(x + (i + u * stride) * 8);
+      ga[u] = *reinterpret_cast<const u16x8*>(dy + (i + u * stride) * 8);
+      if (relu && y) ya[u] = *reinterpret_cast<const u16x8*>(y + (i + u * stride) * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float a[8], g[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        a[j] = bf2f(xa[u][j]);
+        g[j] = bf2f(ga[u][j]);
+        if (relu && y) g[j] = bf2f(ya[u][j]) > 0.f ? g[j] : 0.f;
+        else if (relu) g[j] = fmaf(a[j], msc[j], msf[j]) > 0.f ? g[j] : 0.f;
+      }
+      const long o = (i + u * stride) * 8;
+      if (dres) {
+        u16x8 r;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = f2bf(g[j]);
+        __builtin_nontemporal_store(r, reinterpret_cast<u16x8*>(dres + o));
+      }
+      u16x8 d;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = f2bf(fmaf(k1[j], g[j], fmaf(-k3[j], a[j], k0[j])));
+      __builtin_nontemporal_store(d, reinterpret_cast<u16x8*>(dx + o));
+    }
+  }
+  for (; i < total; i += stride) {
     float a[8], g[8];
     load8(x + i * 8, a);
     load8(dy + i * 8, g);
@@ -597,7 +640,12 @@ static void bn_ew_launch(long rows, int C, int& grid, int& block) {
   block = chunks >= 256 ? 256 : 256 / chunks * chunks;
   long threads_needed = rows * chunks;
   long g = (threads_needed + block - 1) / block;
-  const long cap = 2048;
+  // block cap (PA_BN_EW_CAP, default 8192): at 2048 a [12544, 2048] tensor left each
+  // thread ~6 chunks with the tail ones serialised (2.5x a plain copy's time)
+  static const long cap = [] {
+    const char* e = getenv("PA_BN_EW_CAP");
+    return e && *e ? atol(e) : 8192L;
+  }();
   if (g > cap) g = cap;
   // total threads must be a multiple of chunks
   while (((long)g * block) % chunks) ++g;
@@ -685,7 +733,7 @@ PA_EXPORT int pa_bn_bwd2(const void* x, const void* dy, const void* y, const flo
   int eg, eb;
   bn_ew_launch(rows, C, eg, eb);
   hipLaunchKernelGGL(bn_dx_kernel, dim3(eg), dim3(eb), 0, st, (const u16*)x, (const u16*)dy, mk, mean, coef,
-                     (u16*)dx, rows, C, relu, (u16*)dres);
+                     (u16*)dx, rows, C, relu, (u16*)dres, bn_dx_unroll());
   PA_LAUNCH_CHECK();
 }
 
@@ -703,7 +751,7 @@ PA_EXPORT int pa_bn_bwd_part(const float* part, int G, const void* x, const void
   int eg, eb;
   bn_ew_launch(rows, C, eg, eb);
   hipLaunchKernelGGL(bn_dx_kernel, dim3(eg), dim3(eb), 0, st, (const u16*)x, (const u16*)dy, mk, mean, coef,
-                     (u16*)dx, rows, C, relu, (u16*)dres);
+                     (u16*)dx, rows, C, relu, (u16*)dres, bn_dx_unroll());
   PA_LAUNCH_CHECK();
 }
 
