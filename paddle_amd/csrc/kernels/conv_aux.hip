@@ -640,11 +640,12 @@ static void bn_ew_launch(long rows, int C, int& grid, int& block) {
   block = chunks >= 256 ? 256 : 256 / chunks * chunks;
   long threads_needed = rows * chunks;
   long g = (threads_needed + block - 1) / block;
-  // block cap (PA_BN_EW_CAP, default 8192): at 2048 a [12544, 2048] tensor left each
-  // thread ~6 chunks with the tail ones serialised (2.5x a plain copy's time)
+  // block cap (PA_BN_EW_CAP, default 2048): each thread loads its 8 channels'
+  // parameters once, so fewer, longer-running threads amortise that prologue -- 8192
+  // measured 11 % slower end to end on ResNet-50 (profiles/r5_bn_ew_ab.md)
   static const long cap = [] {
     const char* e = getenv("PA_BN_EW_CAP");
-    return e && *e ? atol(e) : 8192L;
+    return e && *e ? atol(e) : 2048L;
   }();
   if (g > cap) g = cap;
   // total threads must be a multiple of chunks
