@@ -68,16 +68,44 @@ __host__ __device__ __forceinline__ void bn_layout(int C, int& chunks, int& rsub
 // Per-channel affine of the forward (sc = rstd * w, sf = b - mean * sc) for 8 channels:
 // the ReLU mask of relu(BN(x)) is recomputed in backward as fmaf(x, sc, sf) > 0 --
 // the same expression bn_apply_kernel evaluated -- instead of reading y back.
+// 8 per-channel values from c0 (a multiple of 8): two 16-B loads for fp32 / one for bf16
+// when the base is 16-B aligned (every framework allocation is), else element loads
+__device__ __forceinline__ void chan8(const void* __restrict__ p, int bf16, int c0, float def, float (&o)[8]) {
+  if (!p) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = def;
+  } else if (((uintptr_t)p & 15) == 0) {
+    if (bf16) {
+      const u16x8 v = *reinterpret_cast<const u16x8*>((const u16*)p + c0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = bf2f(v[j]);
+    } else {
+      const f32x4 a = *reinterpret_cast<const f32x4*>((const float*)p + c0);
+      const f32x4 b = *reinterpret_cast<const f32x4*>((const float*)p + c0 + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[j] = a[j];
+        o[4 + j] = b[j];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = bf16 ? bf2f(((const u16*)p)[c0 + j]) : ((const float*)p)[c0 + j];
+  }
+}
+
 __device__ __forceinline__ void bn_affine8(int ch, const float* __restrict__ mean, const float* __restrict__ rstd,
                                            const void* __restrict__ w, const void* __restrict__ b, int wdt,
                                            float (&sc)[8], float (&sf)[8]) {
+  float ww[8], bb[8], mm[8], rr[8];
+  chan8(w, wdt, ch * 8, 1.f, ww);
+  chan8(b, wdt, ch * 8, 0.f, bb);
+  chan8(mean, 0, ch * 8, 0.f, mm);
+  chan8(rstd, 0, ch * 8, 0.f, rr);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int c = ch * 8 + j;
-    const float ww = w ? (wdt ? bf2f(((const u16*)w)[c]) : ((const float*)w)[c]) : 1.f;
-    const float bb = b ? (wdt ? bf2f(((const u16*)b)[c]) : ((const float*)b)[c]) : 0.f;
-    sc[j] = rstd[c] * ww;
-    sf[j] = bb - mean[c] * sc[j];
+    sc[j] = rr[j] * ww[j];
+    sf[j] = bb[j] - mm[j] * sc[j];
   }
 }
 
@@ -243,14 +271,7 @@ __global__ void bn_apply_kernel(const u16* __restrict__ x, u16* __restrict__ y, 
   const long i0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
   const int ch = (int)(i0 % chunks);
   float sc[8], sf[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int c = ch * 8 + j;
-    const float ww = w ? (wdt ? bf2f(((const u16*)w)[c]) : ((const float*)w)[c]) : 1.f;
-    const float bb = b ? (wdt ? bf2f(((const u16*)b)[c]) : ((const float*)b)[c]) : 0.f;
-    sc[j] = rstd[c] * ww;
-    sf[j] = bb - mean[c] * sc[j];
-  }
+  bn_affine8(ch, mean, rstd, w, b, wdt, sc, sf);
   // U chunks in flight per thread: every load of a group is issued before the first
   // store (y may alias nothing the loads read, but the compiler cannot know that)
   long i = i0;
@@ -356,14 +377,13 @@ __global__ void bn_dx_kernel(const u16* __restrict__ x, const u16* __restrict__ 
   const long stride = (long)gridDim.x * blockDim.x;
   const long i0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
   const int ch = (int)(i0 % chunks);
-  float k1[8], k0[8], k3[8];
+  float k1[8], k0[8], k3[8], k2[8], mm[8];
+  chan8(coef, 0, ch * 8, 0.f, k1);
+  chan8(coef + C, 0, ch * 8, 0.f, k2);
+  chan8(coef + 2 * C, 0, ch * 8, 0.f, k3);
+  chan8(mean, 0, ch * 8, 0.f, mm);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int c = ch * 8 + j;
-    k1[j] = coef[c];
-    k3[j] = coef[2 * C + c];
-    k0[j] = -coef[c] * coef[C + c] + k3[j] * mean[c];  // constant part
-  }
+  for (int j = 0; j < 8; ++j) k0[j] = -k1[j] * k2[j] + k3[j] * mm[j];  // constant part
   float msc[8], msf[8];
   if (relu && !y) bn_affine8(ch, mean, mk.rstd, mk.w, mk.b, mk.wdt, msc, msf);
   long i = i0;
