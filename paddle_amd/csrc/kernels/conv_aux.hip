@@ -318,11 +318,12 @@ __global__ void bn_apply_kernel(const u16* __restrict__ x, u16* __restrict__ y, 
   }
 }
 
-// A/B knob PA_BN_DX: 1 (default) = 4 chunks in flight + non-temporal stores, 0 = one at a time
+// A/B knob PA_BN_DX: 1 = 4 chunks in flight + non-temporal stores, 0 (default) = one
+// at a time -- the unrolled form measured 2 % slower on ResNet-50 (profiles/r5_bn_ew_ab.md)
 static int bn_dx_unroll() {
   static const int v = [] {
     const char* e = getenv("PA_BN_DX");
-    return e && *e ? atoi(e) : 1;
+    return e && *e ? atoi(e) : 0;
   }();
   return v;
 }
