@@ -117,7 +117,8 @@ struct BnMask {  // relu-mask source of the backward kernels
   int wdt;
 };
 
-template <bool BWD>
+// UNR (backward only): two rows' loads in flight per thread before their sums
+template <bool BWD, bool UNR = false>
 __global__ __launch_bounds__(BN_T) void bn_reduce_kernel(const u16* __restrict__ x, const u16* __restrict__ dy,
                                                           BnMask mk, const float* __restrict__ mean,
                                                           float* __restrict__ partial, long rows, int C, int relu) {
@@ -142,7 +143,32 @@ __global__ __launch_bounds__(BN_T) void bn_reduce_kernel(const u16* __restrict__
       } else {
         load8(x + ch * 8, sh);  // first pixel = shift
       }
-      for (long r = (long)blockIdx.x * rsub + rs; r < rows; r += (long)gridDim.x * rsub) {
+      long r = (long)blockIdx.x * rsub + rs;
+      const long step = (long)gridDim.x * rsub;
+      if constexpr (BWD && UNR) {
+        for (; r + step < rows; r += 2 * step) {
+          u16x8 xa[2], ga[2], ya[2];
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const long o = (r + u * step) * C + ch * 8;
+            xa[u] = *reinterpret_cast<const u16x8*>(x + o);
+            ga[u] = *reinterpret_cast<const u16x8*>(dy + o);
+            if (relu && y) ya[u] = *reinterpret_cast<const u16x8*>(y + o);
+          }
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float a = bf2f(xa[u][j]);
+              float g = bf2f(ga[u][j]);
+              if (relu && y) g = bf2f(ya[u][j]) > 0.f ? g : 0.f;
+              else if (relu) g = fmaf(a, msc[j], msf[j]) > 0.f ? g : 0.f;
+              s0[j] += g;
+              s1[j] += g * (a - sh[j]);
+            }
+        }
+      }
+      for (; r < rows; r += step) {
         float a[8];
         load8(x + r * C + ch * 8, a);
         if (BWD) {
@@ -316,6 +342,15 @@ __global__ void bn_apply_kernel(const u16* __restrict__ x, u16* __restrict__ y, 
     }
     store8(y + i * 8, a);
   }
+}
+
+// A/B knob PA_BN_RED_UNR: 1 = two rows in flight in the backward statistics pass
+static int bn_red_unroll() {
+  static const int v = [] {
+    const char* e = getenv("PA_BN_RED_UNR");
+    return e && *e ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 // A/B knob PA_BN_DX: 1 = 4 chunks in flight + non-temporal stores, 0 (default) = one
@@ -748,7 +783,11 @@ PA_EXPORT int pa_bn_bwd2(const void* x, const void* dy, const void* y, const flo
   if (C % 8) return -1;
   const int G = pa_bn_blocks(rows, C);
   const BnMask mk{(const u16*)y, rstd, w, b, wdt};
-  hipLaunchKernelGGL(bn_reduce_kernel<true>, dim3(G), dim3(BN_T), bn_shm(C), st, (const u16*)x, (const u16*)dy,
+if (bn_red_unroll())
+      hipLaunchKernelGGL((bn_reduce_kernel<true, true>), dim3(G), dim3(BN_T), bn_shm(C), st, (const u16*)x, (const u16*)dy,
+                     mk, mean, part, rows, C, relu);
+  else
+      hipLaunchKernelGGL(bn_reduce_kernel<true>, dim3(G), dim3(BN_T), bn_shm(C), st, (const u16*)x, (const u16*)dy,
                      mk, mean, part, rows, C, relu);
   hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 15) / 16), dim3(1024), 0, st, part, G, C, rows, rstd, w, wdt,
                      dw, db, coef);
