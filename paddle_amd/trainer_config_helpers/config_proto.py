@@ -430,6 +430,8 @@ def _flat_inputs(fn, args, kw):
         for x in (v if isinstance(v, (list, tuple)) else [v]):
             if _is_var(x):
                 out.append((x, None))
+            elif getattr(x, "v1_operands", None):
+                out.extend((o, x) for o in x.v1_operands)  # an operator reads each operand layer
             elif _is_var(getattr(x, "input", None)):
                 out.append((x.input, x))  # a projection / operator
     return out

@@ -181,7 +181,9 @@ def scaling_projection(input, param_attr=None):
 def dotmul_operator(a=None, b=None, scale=1, **kw):
     a = kw.get("x", a)
     b = kw.get("y", b)
-    return _Projection(lambda s: _L().scale(_L().elementwise_mul(a, b), scale=float(scale)), _size(a))
+    op = _Projection(lambda s: _L().scale(_L().elementwise_mul(a, b), scale=float(scale)), _size(a))
+    op.v1_operands = [a, b]  # an operator reads two layers (config_proto.py records both inputs)
+    return op
 
 
 @_export
@@ -713,11 +715,21 @@ def conv_shift_layer(a, b, name=None, **kw):
 @_export
 def gated_unit_layer(input, size, act=None, name=None, gate_attr=None, gate_param_attr=None, gate_bias_attr=True,
                      inproj_attr=None, inproj_param_attr=None, inproj_bias_attr=True, layer_attr=None):
-    """act(x W + b) * sigmoid(x V + c) (gated linear unit)."""
-    with guard():
-        proj = _L().fc(input=input, size=size, act=_act.act_name(act) or None)
-        gate = _L().fc(input=input, size=size, act="sigmoid")
-        return _named(_sized(_L().elementwise_mul(proj, gate), size), name)
+    """act(x W + b) * sigmoid(x V + c) (gated linear unit).  A composite, as in the
+    reference (trainer_config_helpers/layers.py gated_unit_layer): the layers
+    <name>_input_proj (fc), <name>_gate (fc, sigmoid) and <name>_gated_act (mixed
+    layer with a dot_mul operator), each recorded in the ModelConfig."""
+    from . import config_proto as _cp
+    from . import fc_layer as _fc, mixed_layer as _mixed  # the recorded (package-level) layer functions
+
+    rec = _cp.current()
+    if name is None:
+        name = rec.name_for("gated_unit_layer", None) if rec is not None else "__gated_unit_layer__"
+    proj = _fc(input=input, size=size, act=act or _act.Tanh(), name=f"{name}_input_proj",
+               param_attr=inproj_param_attr, bias_attr=inproj_bias_attr)
+    gate = _fc(input=input, size=size, act=_act.Sigmoid(), name=f"{name}_gate",
+               param_attr=gate_param_attr, bias_attr=gate_bias_attr)
+    return _mixed(size=size, input=[dotmul_operator(a=proj, b=gate)], name=f"{name}_gated_act", bias_attr=False)
 
 
 @_export
@@ -785,12 +797,25 @@ def row_conv_layer(input, context_len, act=None, name=None, param_attr=None, **k
 
 @_export
 def prelu_layer(input, name=None, partial_sum=1, channel_shared=None, num_channels=None, param_attr=None, **kw):
+    """Parametric ReLU with one slope per `partial_sum` consecutive elements of the
+    row (reference layers.py prelu_layer / PReluLayer): channel_shared=True -> one
+    slope for the row, False -> one per channel of num_channels.  Slopes [1, size /
+    partial_sum], initialised to 0.25; the row is viewed as [n_slopes, partial_sum]."""
+    size = _size(input)
+    if channel_shared is not None:
+        partial_sum = size if channel_shared else size // (num_channels or 1)
+    if partial_sum <= 0 or size % partial_sum:
+        raise ValueError(f"prelu_layer: partial_sum {partial_sum} must divide the layer size {size}")
+    n_w = size // partial_sum
     with guard():
-        mode = "all" if (channel_shared or partial_sum != 1) else "channel"
-        x = input if len(input.shape) == 4 else _L().reshape(input, [-1, _size(input), 1, 1])
-        y = _L().prelu(x, mode=mode)
-        return _named(_sized(_L().reshape(y, [-1, _size(input)]) if len(input.shape) != 4 else y, _size(input)),
-                      name)
+        helper = LayerHelper("prelu", param_attr=param_attr)
+        alpha = helper.create_parameter(attr=helper.param_attr, shape=[1, n_w], dtype="float32",
+                                        default_initializer=fluid.initializer.Constant(0.25))
+        x = _L().reshape(input, [-1, n_w, partial_sum, 1])
+        y = helper.create_variable_for_type_inference("float32")
+        helper.append_op(type="prelu", inputs={"X": x, "Alpha": alpha}, outputs={"Out": y}, attrs={"mode": "channel"})
+        y = _L().reshape(y, list(input.shape) if len(input.shape) == 4 else [-1, size])
+        return _named(_sized(y, size), name)
 
 
 @_export

@@ -85,10 +85,89 @@ def _fm():
     tch.outputs(tch.factorization_machine(input=tch.data_layer(name="data", size=1024), factor_size=10))
 
 
+def _smooth_l1():
+    tch.outputs(tch.smooth_l1_cost(input=tch.data_layer(name="input", size=300),
+                                   label=tch.data_layer(name="label", size=300)))
+
+
+def _hsigmoid():
+    tch.settings(learning_rate=1e-4, batch_size=1000)
+    din = tch.data_layer(name="data", size=100)
+    label = tch.data_layer(name="label", size=10)
+    tch.outputs(tch.hsigmoid(input=din, label=label, num_classes=10))
+
+
+def _row_conv():
+    tch.settings(batch_size=1000, learning_rate=1e-5)
+    tch.outputs(tch.row_conv_layer(input=tch.data_layer(name="data", size=2560), context_len=19,
+                                   act=tch.ReluActivation()))
+
+
+def _scale_shift():
+    din = tch.data_layer(name="data", size=100)
+    tch.outputs(tch.scale_shift_layer(input=din, bias_attr=False), tch.scale_shift_layer(input=din))
+
+
+def _prelu():
+    din = tch.data_layer(name="input", size=300, height=10, width=10)
+    tch.prelu_layer(input=din, num_channels=3)
+    tch.prelu_layer(input=din, partial_sum=1, num_channels=3)
+    tch.prelu_layer(input=din, partial_sum=5, num_channels=3)
+    tch.prelu_layer(input=din, channel_shared=True, num_channels=3)
+    tch.outputs(tch.prelu_layer(input=din, channel_shared=False, num_channels=3))
+
+
+def _resize():
+    tch.outputs(tch.resize_layer(input=tch.data_layer(name="input", size=300), size=150))
+
+
+def _multiplex():
+    tch.settings(batch_size=1000, learning_rate=1e-5)
+    index = tch.data_layer(name="index", size=1)
+    ds = [tch.data_layer(name="data%d" % i, size=30) for i in (1, 2, 3)]
+    tch.outputs(tch.multiplex_layer([index] + ds))
+
+
+def _expand():
+    tch.settings(batch_size=1000, learning_rate=1e-5)
+    din = tch.data_layer(name="data", size=30)
+    seq = tch.data_layer(name="data_seq", size=30)
+    tch.outputs(tch.expand_layer(input=din, expand_as=seq, expand_level=tch.ExpandLevel.FROM_SEQUENCE),
+                tch.expand_layer(input=din, expand_as=seq, expand_level=tch.ExpandLevel.FROM_NO_SEQUENCE))
+
+
+def _gated_unit():
+    ex = tch.ExtraLayerAttribute(error_clipping_threshold=100.0)
+    tch.outputs(tch.gated_unit_layer(size=512, input=tch.data_layer(name="input", size=256),
+                                     act=tch.TanhActivation(), gate_attr=ex,
+                                     gate_param_attr=tch.ParamAttr(initial_std=1e-4),
+                                     gate_bias_attr=tch.ParamAttr(initial_std=1), inproj_attr=ex,
+                                     inproj_param_attr=tch.ParamAttr(initial_std=1e-4),
+                                     inproj_bias_attr=tch.ParamAttr(initial_std=1), layer_attr=ex))
+
+
+def _seq_slice():
+    seq = tch.data_layer("word", size=128)
+    starts = tch.data_layer("starts", size=5)
+    ends = tch.data_layer("ends", size=5)
+    tch.outputs(tch.seq_slice_layer(input=seq, starts=starts, ends=ends),
+                tch.seq_slice_layer(input=seq, starts=starts, ends=None),
+                tch.seq_slice_layer(input=seq, starts=None, ends=ends))
+
+
+def _kmax_seq_score():
+    scores = tch.fc_layer(input=tch.data_layer(name="input_seq", size=128), size=1, act=tch.ExpActivation())
+    tch.outputs(tch.kmax_seq_score_layer(input=scores, beam_size=5))
+
+
 CONFIGS = {"test_fc": _fc, "layer_activations": _activations, "util_layers": _util,
            "last_first_seq": _last_first_seq, "test_l2_distance_layer": _l2_distance,
            "test_repeat_layer": _repeat, "test_clip_layer": _clip, "test_dot_prod_layer": _dot_prod,
-           "test_row_l2_norm_layer": _row_l2_norm, "test_factorization_machine": _fm}
+           "test_row_l2_norm_layer": _row_l2_norm, "test_factorization_machine": _fm,
+           "test_smooth_l1": _smooth_l1, "test_hsigmoid": _hsigmoid, "test_row_conv": _row_conv,
+           "test_scale_shift_layer": _scale_shift, "test_prelu_layer": _prelu, "test_resize_layer": _resize,
+           "test_multiplex_layer": _multiplex, "test_expand_layer": _expand, "test_gated_unit_layer": _gated_unit,
+           "test_seq_slice_layer": _seq_slice, "test_kmax_seq_socre_layer": _kmax_seq_score}
 
 
 def _core(mc):

@@ -202,3 +202,27 @@ def test_sequence_reverse_and_scale_sub_region_ops():
     exp = im.copy()
     exp[0, 0, 1:3, 0:2] = 3.0
     np.testing.assert_array_equal(np.array(zz), exp)
+
+
+def test_prelu_partial_sum_and_gated_unit_match_numpy():
+    """prelu_layer: one slope per partial_sum consecutive elements (slopes 0.25 at
+    init); gated_unit_layer = tanh(x W + b) * sigmoid(x V + c) over its recorded parts."""
+    rs = np.random.RandomState(2)
+    x = (rs.rand(4, 12).astype("float32") - 0.5)
+
+    def build():
+        xi = tch.data_layer(name="x", size=12)
+        return [tch.prelu_layer(input=xi, partial_sum=4), tch.gated_unit_layer(input=xi, size=3)]
+
+    got, scope = _run(build, {"x": x})
+    ps = {p.name: np.array(scope.find_var(p.name).get_tensor()) for p in STATE["main"].global_block().all_parameters()}
+    (alpha,) = [v for v in ps.values() if v.shape == (1, 3)]
+    slopes = np.repeat(alpha.reshape(-1), 4)
+    np.testing.assert_allclose(got[0], np.where(x > 0, x, slopes * x), rtol=1e-6)
+    assert np.allclose(alpha, 0.25)
+    ws = [v for v in ps.values() if v.shape == (12, 3)]
+    bs = [v.reshape(-1) for v in ps.values() if v.size == 3 and v.shape != (1, 3)]
+    assert len(ws) == 2 and len(bs) == 2
+    sig = lambda z: 1 / (1 + np.exp(-z))  # noqa: E731
+    exp = np.tanh(x @ ws[0] + bs[0]) * sig(x @ ws[1] + bs[1])
+    np.testing.assert_allclose(got[1], exp, rtol=1e-4, atol=1e-5)
