@@ -234,16 +234,16 @@ def maxid_layer(input, name=None, **kw):
     return _l.max_id(input=input)
 
 
-def classification_cost(input, label, name=None, evaluator=None, **kw):
-    return _l.classification_cost(input=input, label=label, name=name)
+def classification_cost(input, label, weight=None, name=None, evaluator=None, **kw):
+    return _l.classification_cost(input=input, label=label, name=name, weight=weight)
 
 
-def cross_entropy(input, label, name=None, **kw):
-    return _l.cross_entropy_cost(input=input, label=label)
+def cross_entropy(input, label, weight=None, name=None, **kw):
+    return _l.cross_entropy_cost(input=input, label=label, weight=weight)
 
 
-def regression_cost(input, label, name=None, **kw):
-    return _l.square_error_cost(input=input, label=label)
+def regression_cost(input, label, weight=None, name=None, **kw):
+    return _l.square_error_cost(input=input, label=label, weight=weight)
 
 
 mse_cost = square_error_cost = regression_cost

@@ -427,6 +427,8 @@ def _flat_inputs(fn, args, kw):
         items = [(None, a) for a in args] + list(kw.items())
     out = []
     for _, v in items:
+        if isinstance(v, dict):  # **kw of the DSL function (e.g. a cost's weight layer)
+            v = [w for k, w in v.items() if k not in ("name", "act", "size", "param_attr", "bias_attr", "layer_attr")]
         for x in (v if isinstance(v, (list, tuple)) else [v]):
             if _is_var(x):
                 out.append((x, None))
@@ -506,7 +508,9 @@ def _record(rec, fn_name, fn, args, kw, out, before, blk):
         if fn_name == "concat_layer":
             size = sum(_vsize(x) or 0 for x, _ in ins)
         if size is None:
-            size = _vsize(v)
+            sh = list(getattr(v, "shape", []) or [])
+            # an image layer's size is C * H * W (the reference's LayerConfig.size)
+            size = _prod(sh[1:]) if len(sh) >= 4 and getattr(v, "v2_size", None) is None else _vsize(v)
         lc = {"name": name, "type": typ, "size": size, "active_type": _ACT.get(an, an or "")}
         weights = [p for p in new if len(p.shape) >= 2 and not getattr(p, "_v1_bias", False)]
         wn = {p.name for p in weights}
@@ -645,6 +649,7 @@ def _x_lstm(lc, a, kw, ins, rec, name):
     size = int(lc.get("size") or 0) or (_vsize(ins[0][0]) or 0) // 4
     lc["size"] = size
     lc["reversed"] = bool(kw.get("reverse", False))
+    lc["active_type"] = _act_or(kw, "act", "tanh")
     lc["active_gate_type"] = _act_or(kw, "gate_act", "sigmoid")
     lc["active_state_type"] = _act_or(kw, "state_act", "tanh")
     lc["bias_parameter_name"] = f"_{name}.wbias"
@@ -656,6 +661,7 @@ def _x_gru(lc, a, kw, ins, rec, name):
     size = int(lc.get("size") or 0) or (_vsize(ins[0][0]) or 0) // 3
     lc["size"] = size
     lc["reversed"] = bool(kw.get("reverse", False))
+    lc["active_type"] = _act_or(kw, "act", "tanh")
     lc["active_gate_type"] = _act_or(kw, "gate_act", "sigmoid")
     lc["bias_parameter_name"] = f"_{name}.wbias"
     _set_params(rec, name, lc, [(f"_{name}.w0", [size, 3 * size], 1.0 / size ** 0.5, True),
@@ -754,7 +760,62 @@ def _x_pooling(lc, a, kw, ins, rec, name):
     lc["seq_pool_stride"] = int(kw.get("stride", -1))
 
 
+def _x_batch_norm(lc, a, kw, ins, rec, name):
+    """BatchNormLayer: the input three times (scale w0, moving mean w1, moving
+    variance w2, the last two static), a [1, C] bias, default act relu."""
+    src = _in_lc(rec, ins)
+    c = int(kw.get("num_channels") or 0)
+    if not c:
+        hw = int(src.get("height", 0) or 0) * int(src.get("width", 0) or 0) * int(src.get("depth", 1) or 1)
+        c = (lc["size"] // hw) if hw else lc["size"]
+    lc["active_type"] = _act_or(kw, "act", "relu")
+    x = ins[0][0]
+    lc["inputs"] = [{"input_layer_name": rec.layer_name(x) or x.name, "input_parameter_name": f"_{name}.w{i}"}
+                    for i in range(3)]
+    lc["bias_parameter_name"] = f"_{name}.wbias"
+    lc["moving_average_fraction"] = float(kw.get("moving_average_fraction", 0.9))
+    lc["epsilon"] = float(kw.get("epsilon", 1e-5))
+    _hwd_from(lc, src)
+    _set_params(rec, name, lc, [(f"_{name}.w0", [c], 0.0, False), (f"_{name}.w1", [1, c], 0.0, False),
+                                (f"_{name}.w2", [1, c], 0.0, False), (f"_{name}.wbias", [1, c], 0.0, False)])
+    for p in rec.params:
+        if p["name"] == f"_{name}.w0":
+            p["initial_mean"], p["dims"] = 1.0, []  # the reference leaves the scale's dims unset
+        elif p["name"] in (f"_{name}.w1", f"_{name}.w2"):
+            p["is_static"] = p["is_shared"] = True
+
+
+def _x_nce(lc, a, kw, ins, rec, name):
+    """NCELayer: sigmoid, a [num_classes, in_size] weight on the input only (label and
+    sample-weight layers carry none), a [1, num_classes] bias."""
+    x, lab = ins[0][0], ins[1][0] if len(ins) > 1 else None
+    nc = int(kw.get("num_classes") or (_vsize(lab) if lab is not None else 0) or 0)
+    lc["active_type"] = _act_or(kw, "act", "sigmoid")
+    for li in lc.get("inputs", [])[1:]:
+        li.pop("input_parameter_name", None)
+    lc["inputs"][0]["input_parameter_name"] = f"_{name}.w0"
+    lc["bias_parameter_name"] = f"_{name}.wbias"
+    lc["num_classes"] = nc
+    lc["num_neg_samples"] = int(kw.get("num_neg_samples", 10))
+    _set_params(rec, name, lc, [(f"_{name}.w0", [nc, _vsize(x) or 0], 1.0 / max(_vsize(x) or 1, 1) ** 0.5, True),
+                                (f"_{name}.wbias", [1, nc], 0.0, False)])
+
+
+def _x_conv(lc, a, kw, ins, rec, name):
+    """ConvLayer (exconv): filter parameter without dims, [num_filters, 1] shared
+    biases."""
+    for p in rec.params:
+        if p["name"] == f"_{name}.w0":
+            p["dims"] = []
+            p["initial_std"] = (2.0 / max(p["size"] // max(int(kw.get("num_filters") or 1), 1), 1)) ** 0.5
+        elif p["name"] == f"_{name}.wbias":
+            p["dims"] = [p["size"], 1]
+    lc["num_filters"] = int(kw.get("num_filters") or 0)
+    lc["shared_biases"] = True
+
+
 _EXTRA = {
+    "batch_norm_layer": _x_batch_norm, "nce_layer": _x_nce, "img_conv_layer": _x_conv,
     "pooling_layer": _x_pooling, "slope_intercept_layer": _x_slope, "scaling_layer": _x_weight_first,
     "factorization_machine": _x_factor, "smooth_l1_cost": _x_coeff, "kmax_seq_score_layer": _x_kmax,
     "sampling_id_layer": _x_same_size, "scale_shift_layer": _x_scale_shift, "seq_slice_layer": _x_seq_slice,

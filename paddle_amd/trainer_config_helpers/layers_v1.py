@@ -833,8 +833,22 @@ def factorization_machine(input, factor_size, act=None, name=None, param_attr=No
 
 @_export
 def printer_layer(input, format=None, name=None):
+    """Print the layers' values at run time; recorded as a "print" LayerConfig (no
+    output of its own: the config keeps using the printed layers)."""
+    from . import config_proto as _cp
+
+    ins = input if isinstance(input, (list, tuple)) else [input]
+    rec = _cp.current()
+    if rec is not None and not rec.depth:
+        lname = rec.name_for("print", name)
+        srcs = [rec.layer_name(x) or x.name for x in ins]
+        lc = {"name": lname, "type": "print", "active_type": "",
+              "inputs": [{"input_layer_name": n} for n in srcs],
+              "user_arg": format or "\n".join(f"layer={n} %s" for n in srcs)}
+        rec.layers.append(lc)
+        rec.by_name[lname] = lc
+        rec.parents[lname] = srcs
     with guard():
-        ins = input if isinstance(input, (list, tuple)) else [input]
         for x in ins:
             _L().Print(x, message=format or x.name)
     return input

@@ -127,19 +127,27 @@ def classification_cost(input, label, name=None, evaluator=None, **kw):
     from . import evaluator as E
 
     with guard():
-        cost = fluid.layers.mean(fluid.layers.cross_entropy(input=input, label=label))
+        cost = fluid.layers.mean(_weighted(fluid.layers.cross_entropy(input=input, label=label), kw.get("weight")))
     E.classification_error(input, label)
     return cost
 
 
+def _weighted(cost, weight):
+    """Per-sample cost times the sample weight layer ([N, 1]) of a weighted v1 cost."""
+    return cost if weight is None else fluid.layers.elementwise_mul(cost, weight)
+
+
 def cross_entropy_cost(input, label, **kw):
     with guard():
-        return fluid.layers.mean(fluid.layers.cross_entropy(input=input, label=label))
+        return fluid.layers.mean(_weighted(fluid.layers.cross_entropy(input=input, label=label), kw.get("weight")))
 
 
 def square_error_cost(input, label, **kw):
     with guard():
-        return fluid.layers.mean(fluid.layers.square_error_cost(input=input, label=label))
+        # per-sample sum of squares (reference SumOfSquaresCostLayer), batch mean
+        c = _weighted(fluid.layers.reduce_sum(fluid.layers.square_error_cost(input=input, label=label), dim=1,
+                                              keep_dim=True), kw.get("weight"))
+        return fluid.layers.mean(c)
 
 
 mse_cost = regression_cost = square_error_cost

@@ -160,6 +160,87 @@ def _kmax_seq_score():
     tch.outputs(tch.kmax_seq_score_layer(input=scores, beam_size=5))
 
 
+def _bi_gru():
+    tch.settings(batch_size=1000, learning_rate=1e-4)
+    tch.outputs(tch.bidirectional_gru(input=tch.data_layer(name="data", size=120), size=40, return_seq=True))
+
+
+def _gru():
+    tch.settings(batch_size=1000, learning_rate=1e-4)
+    tch.outputs(tch.grumemory(input=tch.data_layer(name="data", size=120), size=40, reverse=True,
+                              gate_act=tch.TanhActivation(), act=tch.SigmoidActivation()))
+
+
+def _lstm():
+    tch.settings(batch_size=1000, learning_rate=1e-5)
+    tch.outputs(tch.lstmemory(input=tch.data_layer(name="data", size=128), reverse=True,
+                              gate_act=tch.TanhActivation(), act=tch.TanhActivation(), size=32))
+
+
+def _cost_weight():
+    tch.settings(learning_rate=1e-4, batch_size=1000)
+    data = tch.data_layer(name="input", size=300)
+    lbl = tch.data_layer(name="label", size=1)
+    wt = tch.data_layer(name="weight", size=1)
+    fc = tch.fc_layer(input=data, size=10, act=tch.SoftmaxActivation())
+    tch.outputs(tch.classification_cost(input=fc, label=lbl, weight=wt),
+                tch.square_error_cost(input=fc, label=lbl, weight=wt),
+                tch.nce_layer(input=fc, label=tch.data_layer(name="multi_class_label", size=500), weight=wt))
+
+
+def _pad():
+    tch.settings(batch_size=1000, learning_rate=1e-5)
+    data = tch.data_layer(name="data", size=2016, height=48, width=42)
+    conv = tch.img_conv_layer(input=data, filter_size=3, num_channels=1, num_filters=16, padding=1,
+                              act=tch.LinearActivation(), bias_attr=True)
+    pool = tch.img_pool_layer(input=conv, pool_size=2, stride=2, pool_type=tch.MaxPooling())
+    tch.outputs(tch.pad_layer(input=pool, pad_c=[2, 3], pad_h=[1, 2], pad_w=[3, 1]))
+
+
+def _print():
+    tch.settings(learning_rate=1e-4, batch_size=1000)
+    din = tch.data_layer(name="input", size=100)
+    tch.print_layer(input=din)
+    tch.outputs(din)
+
+
+def _seq_concat_reshape():
+    tch.settings(batch_size=1000, learning_rate=1e-5)
+    d1 = tch.data_layer(name="data1", size=30)
+    d2 = tch.data_layer(name="data2", size=30)
+    tch.outputs([tch.seq_concat_layer(a=d1, b=d2), tch.seq_reshape_layer(input=d1, reshape_size=5)])
+
+
+def _spp():
+    tch.settings(batch_size=100, learning_rate=1e-5)
+    data = tch.data_layer(name="data", size=3200, height=20, width=10)
+    tch.outputs(tch.spp_layer(input=data, pyramid_height=2, num_channels=16, pool_type=tch.MaxPooling()))
+
+
+def _bn3d():
+    tch.settings(batch_size=1000, learning_rate=1e-4)
+    d = tch.data_layer(name="data3D", size=120 * 3, width=20, height=6, depth=3)
+    tch.outputs(tch.batch_norm_layer(d, num_channels=1, img3D=True))
+
+
+def _scale_sub_region():
+    tch.settings(batch_size=1000, learning_rate=1e-5)
+    data = tch.data_layer(name="data", size=2016, height=48, width=42)
+    indices = tch.data_layer(name="indices", size=6)
+    tch.outputs(tch.scale_sub_region_layer(input=data, indices=indices, value=0.0))
+
+
+def _unused():
+    tch.settings(batch_size=1000, learning_rate=1e-4)
+    tch.outputs(tch.sampling_id_layer(input=tch.data_layer(name="probs", size=100)))
+
+
+def _sub_nested_seq():
+    data = tch.data_layer(name="input_seq", size=300)
+    sel = tch.data_layer(name="input", size=5)
+    tch.outputs(tch.sub_nested_seq_layer(input=data, selected_indices=sel))
+
+
 CONFIGS = {"test_fc": _fc, "layer_activations": _activations, "util_layers": _util,
            "last_first_seq": _last_first_seq, "test_l2_distance_layer": _l2_distance,
            "test_repeat_layer": _repeat, "test_clip_layer": _clip, "test_dot_prod_layer": _dot_prod,
@@ -167,7 +248,12 @@ CONFIGS = {"test_fc": _fc, "layer_activations": _activations, "util_layers": _ut
            "test_smooth_l1": _smooth_l1, "test_hsigmoid": _hsigmoid, "test_row_conv": _row_conv,
            "test_scale_shift_layer": _scale_shift, "test_prelu_layer": _prelu, "test_resize_layer": _resize,
            "test_multiplex_layer": _multiplex, "test_expand_layer": _expand, "test_gated_unit_layer": _gated_unit,
-           "test_seq_slice_layer": _seq_slice, "test_kmax_seq_socre_layer": _kmax_seq_score}
+           "test_seq_slice_layer": _seq_slice, "test_kmax_seq_socre_layer": _kmax_seq_score,
+           "test_bi_grumemory": _bi_gru, "test_grumemory_layer": _gru, "test_lstmemory_layer": _lstm,
+           "test_cost_layers_with_weight": _cost_weight, "test_pad": _pad, "test_print_layer": _print,
+           "test_seq_concat_reshape": _seq_concat_reshape, "test_spp_layer": _spp, "test_BatchNorm3D": _bn3d,
+           "test_scale_sub_region_layer": _scale_sub_region, "unused_layers": _unused,
+           "test_sub_nested_seq_select_layer": _sub_nested_seq}
 
 
 def _core(mc):

@@ -226,3 +226,28 @@ def test_prelu_partial_sum_and_gated_unit_match_numpy():
     sig = lambda z: 1 / (1 + np.exp(-z))  # noqa: E731
     exp = np.tanh(x @ ws[0] + bs[0]) * sig(x @ ws[1] + bs[1])
     np.testing.assert_allclose(got[1], exp, rtol=1e-4, atol=1e-5)
+
+
+def test_weighted_costs_scale_each_sample():
+    """classification_cost / square_error_cost with a weight layer: mean over the
+    batch of weight_i * cost_i (reference CostLayer with a weight input)."""
+    rs = np.random.RandomState(3)
+    p = rs.rand(4, 5).astype("float32") + 0.1
+    p /= p.sum(1, keepdims=True)
+    lab = rs.randint(0, 5, (4, 1)).astype("int64")
+    w = rs.rand(4, 1).astype("float32")
+    y = rs.rand(4, 5).astype("float32")
+
+    def build():
+        xp = tch.data_layer(name="p", size=5)
+        xl = tch.data_layer(name="lab", size=1)
+        xw = tch.data_layer(name="w", size=1)
+        xy = tch.data_layer(name="y", size=5)
+        return [tch.classification_cost(input=xp, label=xl, weight=xw),
+                tch.square_error_cost(input=xp, label=xy, weight=xw)]
+
+    got, _ = _run(build, {"p": p, "lab": lab, "w": w, "y": y})
+    ce = -np.log(p[np.arange(4), lab[:, 0]])
+    np.testing.assert_allclose(float(np.asarray(got[0]).reshape(-1)[0]), float((ce * w[:, 0]).mean()), rtol=1e-5)
+    se = ((p - y) ** 2).sum(1)
+    np.testing.assert_allclose(float(np.asarray(got[1]).reshape(-1)[0]), float((se * w[:, 0]).mean()), rtol=1e-5)
