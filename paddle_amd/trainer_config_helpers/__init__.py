@@ -170,7 +170,7 @@ def fc_layer(input, size, act=None, name=None, param_attr=None, bias_attr=None, 
     if isinstance(x, (list, tuple)):
         x = list(x)  # one weight per input (w0, w1, ...), summed before the bias
     out = _l.fc(input=x, size=size, act=act if act is not None else TanhActivation(), name=name,
-                bias_attr=bias_attr)
+                param_attr=param_attr, bias_attr=bias_attr)
     if layer_attr is not None and getattr(layer_attr, "drop_rate", None):
         out = _l.dropout(input=out, dropout_rate=layer_attr.drop_rate)
     return _v1._named(out, name)  # a recurrent_group memory(name=...) may read it
@@ -184,7 +184,8 @@ def img_conv_layer(input, filter_size, num_filters, num_channels=None, stride=1,
                    name=None, bias_attr=None, param_attr=None, **kw):
     return _l.img_conv(input=input, filter_size=filter_size, num_filters=num_filters, num_channels=num_channels,
                        stride=stride, padding=padding, act=act if act is not None else ReluActivation(),
-                       groups=groups)
+                       groups=groups, bias_attr=bias_attr, param_attr=param_attr, trans=kw.get("trans", False),
+                       dilation=kw.get("dilation", 1))
 
 
 def img_pool_layer(input, pool_size, stride=1, padding=0, pool_type=None, num_channels=None, name=None, **kw):

@@ -360,7 +360,8 @@ _ACT = {None: "", "linear": "", "identity": "", "exp": "exponential", "soft_relu
 # layers whose size is their input's (the reference sets size = input.size)
 _SAME_SIZE = {"trans_layer", "first_seq", "last_seq", "dropout_layer", "batch_norm_layer", "clip_layer",
               "row_l2_norm_layer", "sum_to_one_norm_layer", "scaling_layer", "slope_intercept_layer",
-              "power_layer", "rotate_layer", "prelu_layer", "pooling_layer", "addto_layer", "expand_layer"}
+              "power_layer", "rotate_layer", "prelu_layer", "pooling_layer", "addto_layer", "expand_layer",
+              "img_cmrnorm_layer"}
 # functions that are not layers (projections / operators feed mixed / concat layers)
 _NOT_LAYERS = {"settings", "outputs", "get_config_arg", "define_py_data_sources2", "parse_config"}
 
@@ -409,7 +410,10 @@ def _vsize(v):
     s = getattr(v, "v2_size", None)
     if s is None:
         sh = getattr(v, "shape", None)
-        s = int(sh[-1]) if sh else None
+        if sh and len(sh) >= 4:  # an image [N, C, H, W]: the layer size is C * H * W
+            s = _prod(sh[1:])
+        else:
+            s = int(sh[-1]) if sh else None
     return s
 
 
@@ -437,6 +441,15 @@ def _flat_inputs(fn, args, kw):
             elif _is_var(getattr(x, "input", None)):
                 out.append((x.input, x))  # a projection / operator
     return out
+
+
+def _attr_name(attr, i):
+    """The user-given parameter name of input i's ParamAttr (a list holds one per input)."""
+    if isinstance(attr, (list, tuple)):
+        attr = attr[i] if i < len(attr) else None
+    if attr is None or isinstance(attr, bool):
+        return None
+    return getattr(attr, "name", None)
 
 
 def _param_dims(p):
@@ -508,10 +521,9 @@ def _record(rec, fn_name, fn, args, kw, out, before, blk):
         if fn_name == "concat_layer":
             size = sum(_vsize(x) or 0 for x, _ in ins)
         if size is None:
-            sh = list(getattr(v, "shape", []) or [])
-            # an image layer's size is C * H * W (the reference's LayerConfig.size)
-            size = _prod(sh[1:]) if len(sh) >= 4 and getattr(v, "v2_size", None) is None else _vsize(v)
+            size = _vsize(v)
         lc = {"name": name, "type": typ, "size": size, "active_type": _ACT.get(an, an or "")}
+        by_pname = {p.name: p for p in blk.all_parameters()}
         weights = [p for p in new if len(p.shape) >= 2 and not getattr(p, "_v1_bias", False)]
         wn = {p.name for p in weights}
         biases = [p for p in new if p.name not in wn]
@@ -527,7 +539,16 @@ def _record(rec, fn_name, fn, args, kw, out, before, blk):
             if pr is not None and fn_name in ("mixed_layer", "embedding_layer") and getattr(pr, "v1_type", None):
                 li["proj_conf"] = {"type": _PROJ_TYPE.get(pr.v1_type, pr.v1_type), "name": f"_{name}.w{i}",
                                    "input_size": _vsize(x), "output_size": size}
-            if i < len(weights):
+            uname = _attr_name(kw.get("param_attr"), i)
+            if uname is not None and uname in by_pname:  # ParamAttr(name=...): a named, possibly shared, weight
+                li["input_parameter_name"] = uname
+                if uname not in rec.param_map:
+                    rec.param_map[uname] = uname
+                    dims = _param_dims(by_pname[uname])
+                    rec.params.append({"name": uname, "size": int(_prod(dims)), "initial_mean": 0.0,
+                                       "initial_std": 1.0 / max(dims[0], 1) ** 0.5, "dims": dims,
+                                       "initial_strategy": 0, "initial_smart": True})
+            elif i < len(weights):
                 pname = f"_{name}.w{i}"
                 li["input_parameter_name"] = pname
                 rec.param_map[pname] = weights[i].name
@@ -538,7 +559,15 @@ def _record(rec, fn_name, fn, args, kw, out, before, blk):
             layer_inputs.append(li)
         if layer_inputs:
             lc["inputs"] = layer_inputs
-        if biases:
+        bname = _attr_name(kw.get("bias_attr"), 0)
+        if bname is not None and bname in by_pname:
+            lc["bias_parameter_name"] = bname
+            if bname not in rec.param_map:
+                rec.param_map[bname] = bname
+                n = int(_prod(_param_dims(by_pname[bname])))
+                rec.params.append({"name": bname, "size": n, "initial_mean": 0.0, "initial_std": 0.0,
+                                   "dims": [1, n], "initial_strategy": 0, "initial_smart": False})
+        elif biases:
             pname = f"_{name}.wbias"
             lc["bias_parameter_name"] = pname
             rec.param_map[pname] = biases[0].name
@@ -765,6 +794,9 @@ def _x_batch_norm(lc, a, kw, ins, rec, name):
     variance w2, the last two static), a [1, C] bias, default act relu."""
     src = _in_lc(rec, ins)
     c = int(kw.get("num_channels") or 0)
+    xs = list(getattr(ins[0][0], "shape", []) or [])
+    if not c and len(xs) >= 4:
+        c = int(xs[1])
     if not c:
         hw = int(src.get("height", 0) or 0) * int(src.get("width", 0) or 0) * int(src.get("depth", 1) or 1)
         c = (lc["size"] // hw) if hw else lc["size"]
@@ -812,6 +844,8 @@ def _x_conv(lc, a, kw, ins, rec, name):
             p["dims"] = [p["size"], 1]
     lc["num_filters"] = int(kw.get("num_filters") or 0)
     lc["shared_biases"] = True
+    if kw.get("trans"):
+        lc["type"] = "exconvt"
 
 
 _EXTRA = {

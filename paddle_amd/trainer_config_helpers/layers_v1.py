@@ -1014,8 +1014,10 @@ def detection_output_layer(input_loc, input_conf, priorbox, num_classes, nms_thr
 @_export
 def roi_pool_layer(input, rois, pooled_width, pooled_height, spatial_scale, num_channels=None, name=None):
     with guard():
-        return _named(_L().roi_pool(input, rois, pooled_height=pooled_height, pooled_width=pooled_width,
-                                    spatial_scale=spatial_scale), name)
+        out = _L().roi_pool(input, rois, pooled_height=pooled_height, pooled_width=pooled_width,
+                            spatial_scale=spatial_scale)
+        c = num_channels or (int(input.shape[1]) if len(input.shape) == 4 else 1)
+        return _named(_sized(out, c * pooled_height * pooled_width), name)
 
 
 # ------------------------------------------------------------------ costs

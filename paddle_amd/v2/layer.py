@@ -67,9 +67,16 @@ def img_conv(input, filter_size, num_filters, num_channels=None, stride=1, paddi
              param_attr=None, bias_attr=None, name=None, **kw):
     with guard():
         x = _as_image(input, num_channels or 1)
-        out = fluid.layers.conv2d(x, num_filters, filter_size, stride=stride, padding=padding, groups=groups,
-                                  act=_act(act, A.Relu), param_attr=_attr.to_fluid(param_attr),
-                                  bias_attr=_attr.to_fluid(bias_attr), name=name)
+        if kw.get("trans"):  # v1 trans=True: the transposed (fractionally strided) convolution, exconvt
+            out = fluid.layers.conv2d_transpose(x, num_filters, filter_size=filter_size, stride=stride,
+                                                padding=padding, dilation=kw.get("dilation", 1), groups=groups,
+                                                act=_act(act, A.Relu), param_attr=_attr.to_fluid(param_attr),
+                                                bias_attr=_attr.to_fluid(bias_attr), name=name)
+        else:
+            out = fluid.layers.conv2d(x, num_filters, filter_size, stride=stride, padding=padding,
+                                      dilation=kw.get("dilation", 1), groups=groups, act=_act(act, A.Relu),
+                                      param_attr=_attr.to_fluid(param_attr), bias_attr=_attr.to_fluid(bias_attr),
+                                      name=name)
     return out
 
 

@@ -241,6 +241,78 @@ def _sub_nested_seq():
     tch.outputs(tch.sub_nested_seq_layer(input=data, selected_indices=sel))
 
 
+def _conv(inp, nc, nf, **kw):
+    return tch.img_conv_layer(input=inp, filter_size=kw.pop("filter_size", 3), num_channels=nc, num_filters=nf,
+                              padding=kw.pop("padding", 1), act=tch.LinearActivation(),
+                              bias_attr=kw.pop("bias_attr", True), **kw)
+
+
+def _maxout():
+    tch.settings(batch_size=1000, learning_rate=1e-5)
+    data = tch.data_layer(name="data", size=2304, height=48, width=48)
+    mo = tch.maxout_layer(input=_conv(data, 1, 16), num_channels=16, groups=2)
+    pool = tch.img_pool_layer(input=mo, num_channels=8, pool_size=2, stride=2, pool_type=tch.MaxPooling())
+    mo2 = tch.maxout_layer(input=_conv(pool, 8, 128), num_channels=128, groups=4)
+    block = tch.block_expand_layer(input=mo2, num_channels=32, stride_x=1, stride_y=1, block_x=1, block_y=6)
+    tch.outputs(tch.fc_layer(input=block, size=384, bias_attr=False))
+
+
+def _bilinear():
+    tch.settings(batch_size=1000, learning_rate=1e-5)
+    data = tch.data_layer(name="data", size=2304)
+    bil = tch.bilinear_interp_layer(input=_conv(data, 1, 16), out_size_x=64, out_size_y=64)
+    pool = tch.img_pool_layer(input=bil, num_channels=16, pool_size=2, stride=2, pool_type=tch.MaxPooling())
+    tch.outputs(tch.fc_layer(input=pool, size=384, bias_attr=False))
+
+
+def _img(trans):
+    def f():
+        tch.settings(learning_rate=1e-3, batch_size=1000)
+        n = 227 if trans else 256
+        img = tch.data_layer(name="image", size=n * n)
+        kw = {"trans": True} if trans else {"dilation": (1, 1)}
+        conv = tch.img_conv_layer(input=img, num_channels=1, num_filters=64, filter_size=(32, 32), padding=(1, 1),
+                                  stride=(1, 1), act=tch.LinearActivation(), **kw)
+        bn = tch.batch_norm_layer(input=conv, act=tch.ReluActivation())
+        norm = tch.img_cmrnorm_layer(input=bn, size=32)
+        pool = tch.img_pool_layer(input=conv, pool_size=32, pool_type=tch.MaxPooling())
+        tch.outputs(pool, norm)
+    return f
+
+
+def _seq_pooling():
+    tch.settings(learning_rate=1e-4, batch_size=1000)
+    din = tch.data_layer(name="dat_in", size=100)
+    pts = [tch.MaxPooling, tch.AvgPooling, tch.SumPooling]
+    opts = [tch.pooling_layer(input=din, agg_level=al, pooling_type=pt())
+            for pt in pts for al in (tch.AggregateLevel.TO_SEQUENCE, tch.AggregateLevel.TO_NO_SEQUENCE)]
+    opts += [tch.pooling_layer(input=din, agg_level=tch.AggregateLevel.TO_NO_SEQUENCE, pooling_type=pt(), stride=5)
+             for pt in pts]
+    opts.append(tch.pooling_layer(input=din, pooling_type=tch.MaxPooling(output_max_index=True)))
+    tch.outputs(opts)
+
+
+def _shared_fc():
+    tch.settings(learning_rate=1e-4, batch_size=1000)
+    a = tch.data_layer(name="feature_a", size=200)
+    b = tch.data_layer(name="feature_b", size=200)
+    fc_p = tch.ParamAttr(name="fc_param", initial_max=1.0, initial_min=-1.0)
+    b_p = tch.ParamAttr(name="bias_param", initial_mean=0.0, initial_std=0.0)
+    sm_p = tch.ParamAttr(name="softmax_param", initial_max=1.0, initial_min=-1.0)
+    ha = tch.fc_layer(input=a, size=200, param_attr=fc_p, bias_attr=b_p)
+    hb = tch.fc_layer(input=b, size=200, param_attr=fc_p, bias_attr=b_p)
+    pred = tch.fc_layer(input=[ha, hb], param_attr=[sm_p, sm_p], bias_attr=False, size=10,
+                        act=tch.SoftmaxActivation())
+    tch.outputs(tch.classification_cost(input=pred, label=tch.data_layer(name="label", size=10)))
+
+
+def _roi_pool():
+    data = tch.data_layer(name="data", size=3 * 14 * 14, height=14, width=14)
+    rois = tch.data_layer(name="rois", size=10)
+    tch.outputs(tch.roi_pool_layer(input=_conv(data, 3, 16), rois=rois, pooled_width=7, pooled_height=7,
+                                   spatial_scale=1. / 16))
+
+
 CONFIGS = {"test_fc": _fc, "layer_activations": _activations, "util_layers": _util,
            "last_first_seq": _last_first_seq, "test_l2_distance_layer": _l2_distance,
            "test_repeat_layer": _repeat, "test_clip_layer": _clip, "test_dot_prod_layer": _dot_prod,
@@ -253,7 +325,9 @@ CONFIGS = {"test_fc": _fc, "layer_activations": _activations, "util_layers": _ut
            "test_cost_layers_with_weight": _cost_weight, "test_pad": _pad, "test_print_layer": _print,
            "test_seq_concat_reshape": _seq_concat_reshape, "test_spp_layer": _spp, "test_BatchNorm3D": _bn3d,
            "test_scale_sub_region_layer": _scale_sub_region, "unused_layers": _unused,
-           "test_sub_nested_seq_select_layer": _sub_nested_seq}
+           "test_sub_nested_seq_select_layer": _sub_nested_seq, "test_maxout": _maxout,
+           "test_bilinear_interp": _bilinear, "img_layers": _img(False), "img_trans_layers": _img(True),
+           "test_sequence_pooling": _seq_pooling, "shared_fc": _shared_fc, "test_roi_pool_layer": _roi_pool}
 
 
 def _core(mc):

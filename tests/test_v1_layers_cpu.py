@@ -251,3 +251,26 @@ def test_weighted_costs_scale_each_sample():
     np.testing.assert_allclose(float(np.asarray(got[0]).reshape(-1)[0]), float((ce * w[:, 0]).mean()), rtol=1e-5)
     se = ((p - y) ** 2).sum(1)
     np.testing.assert_allclose(float(np.asarray(got[1]).reshape(-1)[0]), float((se * w[:, 0]).mean()), rtol=1e-5)
+
+
+def test_param_attr_name_shares_weights():
+    """Two fc layers with ParamAttr(name='fc_param') use one parameter: equal inputs
+    give equal outputs, and the program holds a single fc_param / bias_param."""
+    rs = np.random.RandomState(4)
+    x = rs.rand(3, 6).astype("float32")
+
+    def build():
+        a = tch.data_layer(name="fa", size=6)
+        b = tch.data_layer(name="fb", size=6)
+        pa = tch.ParamAttr(name="fc_param", initial_max=1.0, initial_min=-1.0)
+        ba = tch.ParamAttr(name="bias_param", initial_mean=0.0, initial_std=0.0)
+        return [tch.fc_layer(input=a, size=4, param_attr=pa, bias_attr=ba),
+                tch.fc_layer(input=b, size=4, param_attr=pa, bias_attr=ba)]
+
+    got, scope = _run(build, {"fa": x, "fb": x})
+    names = [p.name for p in STATE["main"].global_block().all_parameters()]
+    assert sorted(names) == ["bias_param", "fc_param"], names
+    W = np.array(scope.find_var("fc_param").get_tensor())
+    assert W.min() >= -1.0 and W.max() <= 1.0 and W.std() > 0.1  # uniform [-1, 1]
+    np.testing.assert_allclose(got[0], got[1], rtol=1e-6)
+    np.testing.assert_allclose(got[0], np.tanh(x @ W), rtol=1e-5, atol=1e-6)
