@@ -97,9 +97,10 @@ _S = {
         ("adam_beta2", 34, "double", 0), ("adam_epsilon", 35, "double", 0),
         ("gradient_clipping_threshold", 38, "double", 0)],
     "DataConfig": [
-        ("type", 1, "string", 0), ("files", 3, "string", 0), ("for_test", 14, "bool", 0),
-        ("load_data_module", 21, "string", 0), ("load_data_object", 22, "string", 0),
-        ("load_data_args", 23, "string", 0)],
+        ("type", 1, "string", 0), ("files", 3, "string", 0), ("async_load_data", 12, "bool", 0),
+        ("for_test", 14, "bool", 0), ("load_data_module", 21, "string", 0), ("load_data_object", 22, "string", 0),
+        ("load_data_args", 23, "string", 0), ("data_ratio", 25, "int32", 0), ("is_main_data", 26, "bool", 0),
+        ("usage_ratio", 27, "double", 0)],
     "TrainerConfig": [
         ("model_config", 1, "ModelConfig", 0), ("data_config", 2, "DataConfig", 0),
         ("opt_config", 3, "OptimizationConfig", 0), ("test_data_config", 4, "DataConfig", 0),
@@ -361,7 +362,7 @@ _ACT = {None: "", "linear": "", "identity": "", "exp": "exponential", "soft_relu
 _SAME_SIZE = {"trans_layer", "first_seq", "last_seq", "dropout_layer", "batch_norm_layer", "clip_layer",
               "row_l2_norm_layer", "sum_to_one_norm_layer", "scaling_layer", "slope_intercept_layer",
               "power_layer", "rotate_layer", "prelu_layer", "pooling_layer", "addto_layer", "expand_layer",
-              "img_cmrnorm_layer"}
+              "img_cmrnorm_layer", "crf_layer"}
 # functions that are not layers (projections / operators feed mixed / concat layers)
 _NOT_LAYERS = {"settings", "outputs", "get_config_arg", "define_py_data_sources2", "parse_config"}
 
@@ -725,9 +726,47 @@ _PROJ_TYPE = {"identity_offset": "identity_offset", "trans_fc": "trans_fc"}
 
 def _x_weight_first(lc, a, kw, ins, rec, name):
     """scaling / interpolation / power layers list the weight layer first."""
-    if len(lc.get("inputs", [])) == 2:
-        lc["inputs"] = lc["inputs"][::-1]
-        rec.parents[name] = rec.parents.get(name, [])[::-1]
+    n = len(lc.get("inputs", []))
+    if n >= 2:  # the weight is the last argument of the DSL call
+        lc["inputs"] = lc["inputs"][-1:] + lc["inputs"][:-1]
+        ps = rec.parents.get(name, [])
+        rec.parents[name] = ps[-1:] + ps[:-1]
+
+
+def _x_cos(lc, a, kw, ins, rec, name):
+    """cos_sim: a vector against a matrix of `size` rows is the "cos_vm" layer."""
+    size = int(kw.get("size", 1) or 1)
+    lc["size"] = size
+    if size > 1:
+        lc["type"] = "cos_vm"
+    lc["cos_scale"] = float(kw.get("scale", 1.0))
+
+
+def _x_no_size(lc, a, kw, ins, rec, name):
+    lc.pop("size", None)  # the reference leaves this cost's size unset
+
+
+def _x_tensor(lc, a, kw, ins, rec, name):
+    """TensorLayer: one [a, b, size] weight on the first input, a [1, size] bias."""
+    size = int(lc["size"])
+    da, db = _vsize(ins[0][0]) or 0, _vsize(ins[1][0]) or 0
+    fl = rec.param_map.pop(f"_{name}.w1", None)
+    if fl is not None:
+        rec.param_map[f"_{name}.wbias"] = fl
+    for li in lc.get("inputs", [])[1:]:
+        li.pop("input_parameter_name", None)
+    lc["bias_parameter_name"] = f"_{name}.wbias"
+    _set_params(rec, name, lc, [(f"_{name}.w0", [da, db, size], 1.0 / max(da, 1) ** 0.5, True),
+                                (f"_{name}.wbias", [1, size], 0.0, False)])
+
+
+def _x_ctc(lc, a, kw, ins, rec, name):
+    """CTC costs: size = number of classes incl. the blank = label size + 1."""
+    size = kw.get("size")
+    lc["size"] = int(size) if size else (_vsize(ins[1][0]) or 0) + 1
+    lc["norm_by_times"] = bool(kw.get("norm_by_times", False))
+    if "blank" in kw:
+        lc["blank"] = int(kw["blank"])
 
 
 def _x_slope(lc, a, kw, ins, rec, name):
@@ -851,6 +890,9 @@ def _x_conv(lc, a, kw, ins, rec, name):
 _EXTRA = {
     "batch_norm_layer": _x_batch_norm, "nce_layer": _x_nce, "img_conv_layer": _x_conv,
     "pooling_layer": _x_pooling, "slope_intercept_layer": _x_slope, "scaling_layer": _x_weight_first,
+    "interpolation_layer": _x_weight_first, "power_layer": _x_weight_first,
+    "ctc_layer": _x_ctc, "warp_ctc_layer": _x_ctc, "cos_sim": _x_cos, "tensor_layer": _x_tensor,
+    "cross_entropy_with_selfnorm": _x_no_size,
     "factorization_machine": _x_factor, "smooth_l1_cost": _x_coeff, "kmax_seq_score_layer": _x_kmax,
     "sampling_id_layer": _x_same_size, "scale_shift_layer": _x_scale_shift, "seq_slice_layer": _x_seq_slice,
     "data_layer": _x_data, "addto_layer": _x_addto, "concat_layer": _x_concat,
@@ -926,10 +968,17 @@ def data_configs(cfg):
     train, test, module, obj, args = (src["train_list"], src["test_list"], src["module"], src["obj"],
                                       src.get("args"))
 
+    def pick(v, i):  # define_py_data_sources2: a (train, test) pair of modules / objects / args
+        return v[i] if isinstance(v, (list, tuple)) else v
+
     def dc(files, for_test):
         if not files:
             return None
-        return {"type": "py2", "files": files, "for_test": for_test, "load_data_module": module,
-                "load_data_object": obj, "load_data_args": "" if args is None else str(args)}
+        i = int(for_test)
+        a = pick(args, i)
+        return {"type": "py2", "files": files, "async_load_data": False, "for_test": for_test,
+                "load_data_module": pick(module, i), "load_data_object": pick(obj, i),
+                "load_data_args": "" if a is None else str(a), "data_ratio": 1, "is_main_data": True,
+                "usage_ratio": 1.0}
 
     return dc(train, False), dc(test, True)

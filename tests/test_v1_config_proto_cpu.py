@@ -313,6 +313,82 @@ def _roi_pool():
                                    spatial_scale=1. / 16))
 
 
+def _math_ops():
+    tch.settings(batch_size=1000, learning_rate=1e-5)
+    lm = tch.layer_math
+    x = tch.data_layer(name="data", size=100)
+    for f in (lm.exp, lm.sqrt, lm.reciprocal, lm.log, lm.abs, lm.sigmoid, lm.tanh, lm.square, lm.relu):
+        x = f(x)
+    y = 1 + x
+    y = y + 1
+    y = x + y
+    y = y - x
+    y = y - 2
+    y = 2 - y
+    y = 2 * y
+    y = y * 3
+    z = tch.data_layer(name="data_2", size=1)
+    y = y * z
+    y = z * y
+    y = y + z
+    y = z + y
+    tch.outputs(y)
+
+
+def _cost_layers():
+    tch.settings(learning_rate=1e-4, batch_size=1000)
+    seq_in = tch.data_layer(name="input", size=200)
+    labels = tch.data_layer(name="labels", size=5000)
+    probs = tch.data_layer(name="probs", size=10)
+    xe_label = tch.data_layer(name="xe-label", size=10)
+    hidden = tch.fc_layer(input=seq_in, size=4)
+    tch.outputs(
+        tch.ctc_layer(input=seq_in, label=labels),
+        tch.warp_ctc_layer(input=seq_in, label=labels, blank=0),
+        tch.crf_layer(input=hidden, label=tch.data_layer(name="crf_label", size=4)),
+        tch.rank_cost(left=tch.data_layer(name="left", size=1), right=tch.data_layer(name="right", size=1),
+                      label=tch.data_layer(name="label", size=1)),
+        tch.lambda_cost(input=tch.data_layer(name="list_feature", size=100),
+                        score=tch.data_layer(name="list_scores", size=1)),
+        tch.cross_entropy(input=probs, label=xe_label),
+        tch.cross_entropy_with_selfnorm(input=probs, label=xe_label),
+        tch.huber_regression_cost(input=seq_in, label=labels),
+        tch.huber_classification_cost(input=tch.data_layer(name="huber_probs", size=1),
+                                      label=tch.data_layer(name="huber_label", size=1)),
+        tch.multi_binary_label_cross_entropy(input=probs, label=xe_label),
+        tch.sum_cost(input=hidden),
+        tch.nce_layer(input=hidden, label=labels))
+
+
+def _recursive():
+    tch.settings(batch_size=1000, learning_rate=1e-5)
+    enc = tch.data_layer(name="data", size=100)
+    for _ in range(32):
+        enc = tch.addto_layer([enc, enc])
+    tch.outputs(tch.fc_layer(input=tch.fc_layer(input=enc, size=32, act=tch.ReluActivation()), size=10,
+                             act=tch.SoftmaxActivation()))
+
+
+def _split_ds():
+    tch.define_py_data_sources2(train_list="train.list", test_list="test.list", module=["a", "b"], obj=("c", "d"))
+    tch.settings(learning_rate=1e-3, batch_size=1000)
+    tch.outputs(tch.data_layer(name="a", size=10))
+
+
+def _ntm():
+    tch.settings(batch_size=1000, learning_rate=1e-5)
+    w = tch.data_layer(name="w", size=1)
+    a = tch.data_layer(name="a", size=100)
+    b = tch.data_layer(name="b", size=100)
+    c = tch.data_layer(name="c", size=200)
+    d = tch.data_layer(name="d", size=31)
+    tch.outputs(tch.interpolation_layer(input=[a, b], weight=w), tch.power_layer(input=a, weight=w),
+                tch.scaling_layer(input=a, weight=w), tch.cos_sim(a=a, b=b), tch.cos_sim(a=a, b=c, size=2),
+                tch.sum_to_one_norm_layer(input=a), tch.conv_shift_layer(a=a, b=d),
+                tch.tensor_layer(a=a, b=b, size=1000), tch.slope_intercept_layer(input=a, slope=0.7, intercept=0.9),
+                tch.linear_comb_layer(weights=b, vectors=c))
+
+
 CONFIGS = {"test_fc": _fc, "layer_activations": _activations, "util_layers": _util,
            "last_first_seq": _last_first_seq, "test_l2_distance_layer": _l2_distance,
            "test_repeat_layer": _repeat, "test_clip_layer": _clip, "test_dot_prod_layer": _dot_prod,
@@ -327,7 +403,9 @@ CONFIGS = {"test_fc": _fc, "layer_activations": _activations, "util_layers": _ut
            "test_scale_sub_region_layer": _scale_sub_region, "unused_layers": _unused,
            "test_sub_nested_seq_select_layer": _sub_nested_seq, "test_maxout": _maxout,
            "test_bilinear_interp": _bilinear, "img_layers": _img(False), "img_trans_layers": _img(True),
-           "test_sequence_pooling": _seq_pooling, "shared_fc": _shared_fc, "test_roi_pool_layer": _roi_pool}
+           "test_sequence_pooling": _seq_pooling, "shared_fc": _shared_fc, "test_roi_pool_layer": _roi_pool,
+           "math_ops": _math_ops, "test_cost_layers": _cost_layers, "test_recursive_topology": _recursive,
+           "test_split_datasource": _split_ds, "test_ntm_layers": _ntm}
 
 
 def _core(mc):
@@ -345,7 +423,16 @@ def test_model_config_matches_reference_protostr(name):
         pytest.skip("reference protostr not present")
     c = tch.parse_config(CONFIGS[name])
     got = _core(c.model_config())
-    exp = _core(cp.from_text("ModelConfig", open(path).read()))
+    text = open(path).read()
+    if text.startswith("model_config {"):  # a whole TrainerConfig: its data configs must match too
+        tc = cp.from_text("TrainerConfig", text)
+        mine = c.trainer_config()
+        for k in ("data_config", "test_data_config"):
+            if k in tc:
+                assert {f: mine[k].get(f) for f in tc[k]} == tc[k], k
+        exp = _core(tc["model_config"])
+    else:
+        exp = _core(cp.from_text("ModelConfig", text))
     assert got[0] == exp[0]
     assert got[1] == exp[1]
     assert got[2:] == exp[2:]
