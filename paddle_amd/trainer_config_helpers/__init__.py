@@ -133,9 +133,13 @@ def define_py_data_sources2(train_list, test_list, module, obj, args=None):
 
 
 def outputs(*layers):
-    out = []
+    if "outputs" not in _CFG:  # the model's input layers are traced from the first call's outputs
+        _CFG["first_outputs"] = [v for x in layers for v in (x if isinstance(x, (list, tuple)) else [x])]
+    out = list(_CFG.get("outputs") or [])  # repeated outputs(...) calls add up (reference Outputs)
     for x in layers:
-        out.extend(x if isinstance(x, (list, tuple)) else [x])
+        for v in (x if isinstance(x, (list, tuple)) else [x]):
+            if all(v is not o for o in out):
+                out.append(v)
     _CFG["outputs"] = out
 
 
@@ -156,6 +160,8 @@ def data_layer(name, size, height=None, width=None, type=None, **kw):
     out = _l.data(name=name, type=type)
     if height and width:
         out.v2_hw = (int(height), int(width))  # image layers read [C, H, W] from it
+        if kw.get("depth"):
+            out.v2_dhw = (int(kw["depth"]), int(height), int(width))  # 3-D layers: [C, D, H, W]
     return out
 
 
@@ -300,7 +306,7 @@ class TrainerConfig:
 
     def model_config(self) -> dict:
         """ModelConfig (layers, parameters, input / output layer names, root sub-model)."""
-        return _cp.model_config(self._rec, self.outputs)
+        return _cp.model_config(self._rec, self.outputs, self._cfg.get("first_outputs"))
 
     @property
     def parameter_name_map(self) -> dict:

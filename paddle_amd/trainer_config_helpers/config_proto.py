@@ -742,6 +742,32 @@ def _x_cos(lc, a, kw, ins, rec, name):
     lc["cos_scale"] = float(kw.get("scale", 1.0))
 
 
+def _x_reorder(order, size=None):
+    """Layers whose LayerConfig lists the inputs in another order than the DSL call
+    (detection_output: priorbox, loc, conf; multibox_loss: priorbox, label, loc, conf)."""
+    def f(lc, a, kw, ins, rec, name):
+        by = {k: i for i, k in enumerate(("input_loc", "input_conf", "priorbox", "label"))}
+        li = lc.get("inputs", [])
+        lc["inputs"] = [li[by[k]] for k in order if by[k] < len(li)]
+        rec.parents[name] = [x["input_layer_name"] for x in lc["inputs"]]
+        if size is not None:
+            lc["size"] = size(kw)
+    return f
+
+
+def _x_beam(lc, a, kw, ins, rec, name):
+    """cross_entropy_over_beam: (scores, selected candidates, gold) of every beam."""
+    beams = kw.get("input") if "input" in kw else (a[0] if a else [])
+    beams = beams if isinstance(beams, (list, tuple)) else [beams]
+    ls = []
+    for b in beams:
+        for v in (b.candidate_scores, b.selected_candidates, b.gold):
+            ls.append({"input_layer_name": rec.layer_name(v) or v.name})
+    lc["inputs"] = ls
+    rec.parents[name] = [x["input_layer_name"] for x in ls]
+    lc.pop("size", None)
+
+
 def _x_no_size(lc, a, kw, ins, rec, name):
     lc.pop("size", None)  # the reference leaves this cost's size unset
 
@@ -884,7 +910,14 @@ def _x_conv(lc, a, kw, ins, rec, name):
     lc["num_filters"] = int(kw.get("num_filters") or 0)
     lc["shared_biases"] = True
     if kw.get("trans"):
-        lc["type"] = "exconvt"
+        lc["type"] = "deconv3d" if lc["type"] == "conv3d" else "exconvt"
+        if lc["type"] == "deconv3d":  # the reference sizes the deconv3d filter with num_filters / groups
+            nf, g = int(kw.get("num_filters") or 1), int(kw.get("groups") or 1)
+            fs = kw.get("filter_size", 1)
+            k3 = _prod(fs) if isinstance(fs, (list, tuple)) else int(fs) ** 3
+            for p in rec.params:
+                if p["name"] == f"_{name}.w0":
+                    p["size"] = nf * (nf // g) * k3
 
 
 _EXTRA = {
@@ -892,7 +925,11 @@ _EXTRA = {
     "pooling_layer": _x_pooling, "slope_intercept_layer": _x_slope, "scaling_layer": _x_weight_first,
     "interpolation_layer": _x_weight_first, "power_layer": _x_weight_first,
     "ctc_layer": _x_ctc, "warp_ctc_layer": _x_ctc, "cos_sim": _x_cos, "tensor_layer": _x_tensor,
-    "cross_entropy_with_selfnorm": _x_no_size,
+    "cross_entropy_with_selfnorm": _x_no_size, "cross_entropy_over_beam": _x_beam,
+    "detection_output_layer": _x_reorder(("priorbox", "input_loc", "input_conf"),
+                                         lambda kw: int(kw.get("keep_top_k", 200)) * 7),
+    "multibox_loss_layer": _x_reorder(("priorbox", "label", "input_loc", "input_conf")),
+    "img_conv3d_layer": _x_conv,
     "factorization_machine": _x_factor, "smooth_l1_cost": _x_coeff, "kmax_seq_score_layer": _x_kmax,
     "sampling_id_layer": _x_same_size, "scale_shift_layer": _x_scale_shift, "seq_slice_layer": _x_seq_slice,
     "data_layer": _x_data, "addto_layer": _x_addto, "concat_layer": _x_concat,
@@ -927,10 +964,13 @@ def _dfs_inputs(rec, out_names):
     return order
 
 
-def model_config(rec, outputs):
+def model_config(rec, outputs, first_outputs=None):
     out_names = [rec.layer_name(o) or getattr(o, "name", str(o)) for o in outputs]
     names = [lc["name"] for lc in rec.layers]
-    ins = _dfs_inputs(rec, out_names) if out_names and all(o in rec.by_name for o in out_names) else rec.inputs
+    # input layers: DFS from the outputs of the first outputs(...) call (the reference
+    # sets input_layer_names once, there)
+    src = [rec.layer_name(o) or getattr(o, "name", str(o)) for o in (first_outputs or outputs)]
+    ins = _dfs_inputs(rec, src) if src and all(o in rec.by_name for o in src) else rec.inputs
     mc = {"type": "nn", "layers": rec.layers, "parameters": rec.params, "input_layer_names": ins,
           "output_layer_names": out_names,
           "sub_models": [{"name": "root", "layer_names": names, "input_layer_names": ins,

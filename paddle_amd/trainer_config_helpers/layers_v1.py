@@ -563,7 +563,9 @@ def seq_slice_layer(input, starts, ends, name=None):
     """Slice each sequence: rows [starts, ends) (index tensors, one per sequence)."""
     with guard():
         length = _L().elementwise_sub(ends, starts) if ends is not None else None
-        return _named(_sized(_L().sequence_slice(input, starts, length), _size(input)), name)
+        out = _L().sequence_slice(input, starts, length)
+        out.shape = (-1, _size(input))  # rows of the input's width (a LoD-level slice)
+        return _named(_sized(out, _size(input)), name)
 
 
 @_export
@@ -932,16 +934,32 @@ def img_pool3d_layer(input, pool_size, num_channels=None, stride=1, padding=0, p
 
     with guard():
         ptype = "avg" if isinstance(pool_type, _pool.Avg) else "max"
-        return _named(_L().pool3d(input, pool_size=pool_size, pool_type=ptype, pool_stride=stride,
-                                  pool_padding=padding), name)
+        return _named(_L().pool3d(_as_volume(input, num_channels), pool_size=pool_size, pool_type=ptype,
+                                  pool_stride=stride, pool_padding=padding, ceil_mode=True), name)
+
+
+def _as_volume(input, num_channels):
+    """[N, C * D * H * W] rows of a data_layer(depth=, height=, width=) as [N, C, D, H, W]."""
+    if len(input.shape) == 5:
+        return input
+    dhw = getattr(input, "v2_dhw", None)
+    if dhw is None:
+        raise ValueError("3-D layers need an input with depth / height / width (data_layer(depth=...))")
+    d, h, w = dhw
+    return _L().reshape(input, [-1, num_channels or max(_size(input) // (d * h * w), 1), d, h, w])
 
 
 @_export
 def img_conv3d_layer(input, filter_size, num_filters, num_channels=None, stride=1, padding=0, act=None, groups=1,
                      name=None, bias_attr=None, param_attr=None, **kw):
     with guard():
-        return _named(_L().conv3d(input, num_filters=num_filters, filter_size=filter_size, stride=stride,
-                                  padding=padding, groups=groups, act=_act.act_name(act) or None), name)
+        x = _as_volume(input, num_channels)
+        conv = _L().conv3d_transpose if kw.get("trans") else _L().conv3d
+        from ..v2 import attr as _attr
+
+        return _named(conv(x, num_filters=num_filters, filter_size=filter_size, stride=stride, padding=padding,
+                           groups=groups, act=_act.act_name(act) or None, param_attr=_attr.to_fluid(param_attr),
+                           bias_attr=_attr.to_fluid(bias_attr)), name)
 
 
 @_export

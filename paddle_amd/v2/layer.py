@@ -83,7 +83,9 @@ def img_conv(input, filter_size, num_filters, num_channels=None, stride=1, paddi
 def img_pool(input, pool_size, stride=1, padding=0, pool_type=None, num_channels=None, name=None, **kw):
     with guard():
         x = _as_image(input, num_channels or 1)
-        out = fluid.layers.pool2d(x, pool_size, (pool_type or P.Max()).img, stride, pool_padding=padding)
+        # v1 / v2 image pooling rounds the output size up (ceil mode, reference PoolLayer)
+        out = fluid.layers.pool2d(x, pool_size, (pool_type or P.Max()).img, stride, pool_padding=padding,
+                                  ceil_mode=kw.get("ceil_mode", True))
     return out
 
 

@@ -389,6 +389,71 @@ def _ntm():
                 tch.linear_comb_layer(weights=b, vectors=c))
 
 
+def _pool3d():
+    tch.settings(batch_size=100, learning_rate=1e-5)
+    d2 = tch.data_layer(name="data_2d", size=6000, height=20, width=10)
+    tch.outputs(tch.img_pool_layer(name="pool___2d", input=d2, num_channels=30, pool_size=5, stride=3, padding=1,
+                                   pool_type=tch.AvgPooling()))
+    d3 = tch.data_layer(name="data_3d_1", size=60000, depth=10, height=20, width=10)
+    tch.outputs(tch.img_pool3d_layer(name="pool_3d_1", input=d3, num_channels=30, pool_size=5, stride=3, padding=1,
+                                     pool_type=tch.AvgPooling()))
+    tch.outputs(tch.img_pool3d_layer(name="pool_3d_2", input=d3, num_channels=30, pool_size=[5, 5, 5],
+                                     stride=[3, 3, 3], padding=[1, 1, 1], pool_type=tch.MaxPooling()))
+
+
+def _conv3d(trans):
+    def f():
+        tch.settings(batch_size=1000, learning_rate=1e-5)
+        data = tch.data_layer(name="data", size=12096 * 3, height=48, width=42, depth=6)
+        pre = "deconv3d" if trans else "conv3d"
+        kw = dict(input=data, num_filters=16, num_channels=3, groups=1, bias_attr=True, shared_biases=True,
+                  trans=trans, layer_type=pre, act=tch.LinearActivation())
+        tch.img_conv3d_layer(name=pre + "_1", filter_size=3, stride=2, padding=1, **kw)
+        tch.outputs(tch.img_conv3d_layer(name=pre + "_2", filter_size=[3, 3, 3], stride=[2, 2, 2],
+                                         padding=[1, 1, 1], **kw))
+    return f
+
+
+def _multibox():
+    tch.settings(batch_size=1000, learning_rate=1e-5)
+    loc = tch.data_layer(name="input_loc", size=16, height=16, width=1)
+    conf = tch.data_layer(name="input_conf", size=8, height=1, width=8)
+    prior = tch.data_layer(name="priorbox", size=32, height=4, width=8)
+    label = tch.data_layer(name="label", size=24, height=4, width=6)
+    tch.outputs(tch.multibox_loss_layer(input_loc=loc, input_conf=conf, priorbox=prior, label=label, num_classes=21,
+                                        overlap_threshold=0.5, neg_pos_ratio=3.0, neg_overlap=0.5, background_id=0,
+                                        name="test_multibox_loss"))
+
+
+def _detection_output():
+    tch.settings(batch_size=1000, learning_rate=1e-5)
+    loc = tch.data_layer(name="input_loc", size=16, height=16, width=1)
+    conf = tch.data_layer(name="input_conf", size=8, height=1, width=8)
+    prior = tch.data_layer(name="priorbox", size=32, height=4, width=8)
+    tch.outputs(tch.detection_output_layer(input_loc=loc, input_conf=conf, priorbox=prior, num_classes=21,
+                                           nms_threshold=0.45, nms_top_k=400, keep_top_k=200,
+                                           confidence_threshold=0.01, background_id=0, name="test_detection_output"))
+
+
+def _xe_over_beam():
+    states = tch.data_layer(name="sentence_states", size=32)
+    scores = tch.data_layer(name="sentence_scores", size=1)
+    top_sent = tch.kmax_seq_score_layer(input=scores, beam_size=5)
+    top_sen = tch.sub_nested_seq_layer(input=states, selected_indices=top_sent)
+    start_scores = tch.fc_layer(input=top_sen, size=1, act=tch.LinearActivation())
+    top_start = tch.kmax_seq_score_layer(input=scores, beam_size=5)
+    spans = tch.seq_slice_layer(input=top_sen, starts=top_start, ends=None)
+    end_scores = tch.fc_layer(input=spans, size=1, act=tch.LinearActivation())
+    top_end = tch.kmax_seq_score_layer(input=end_scores, beam_size=5)
+    sid = tch.data_layer(name="sentences_ids", size=1)
+    st = tch.data_layer(name="start_ids", size=1)
+    en = tch.data_layer(name="end_ids", size=1)
+    tch.outputs(tch.cross_entropy_over_beam(input=[
+        tch.BeamInput(candidate_scores=scores, selected_candidates=top_sent, gold=sid),
+        tch.BeamInput(candidate_scores=start_scores, selected_candidates=top_start, gold=st),
+        tch.BeamInput(candidate_scores=end_scores, selected_candidates=top_end, gold=en)]))
+
+
 CONFIGS = {"test_fc": _fc, "layer_activations": _activations, "util_layers": _util,
            "last_first_seq": _last_first_seq, "test_l2_distance_layer": _l2_distance,
            "test_repeat_layer": _repeat, "test_clip_layer": _clip, "test_dot_prod_layer": _dot_prod,
@@ -405,7 +470,10 @@ CONFIGS = {"test_fc": _fc, "layer_activations": _activations, "util_layers": _ut
            "test_bilinear_interp": _bilinear, "img_layers": _img(False), "img_trans_layers": _img(True),
            "test_sequence_pooling": _seq_pooling, "shared_fc": _shared_fc, "test_roi_pool_layer": _roi_pool,
            "math_ops": _math_ops, "test_cost_layers": _cost_layers, "test_recursive_topology": _recursive,
-           "test_split_datasource": _split_ds, "test_ntm_layers": _ntm}
+           "test_split_datasource": _split_ds, "test_ntm_layers": _ntm, "test_pooling3D_layer": _pool3d,
+           "test_conv3d_layer": _conv3d(False), "test_deconv3d_layer": _conv3d(True),
+           "test_multibox_loss_layer": _multibox, "test_detection_output_layer": _detection_output,
+           "test_cross_entropy_over_beam": _xe_over_beam}
 
 
 def _core(mc):
