@@ -85,6 +85,8 @@ def main():
     ap.add_argument("--master-port", type=int, default=0)
     ap.add_argument("--autograd", default="tape", choices=["tape", "torch"],
                     help="tape: the framework's own reverse pass (torch autograd off); torch: torch.autograd")
+    ap.add_argument("--dtype", default=None, choices=["bfloat16", "float32"],
+                    help="debug only (CPU tests): override the model dtype; GPU results must stay bf16")
     argv = sys.argv[1:]
     args = ap.parse_args(argv)
 
@@ -103,8 +105,11 @@ def main():
         raise SystemExit(f"[bench] rank {rank}: WORLD_SIZE={world} but --gpus {args.gpus}")
     cuda = args.device == "cuda"
     if world > 1:
-        comm.init_parallel_env("nccl" if cuda else "gloo")
-        log(f"[bench] {'RCCL' if cuda else 'gloo'} world={world} rank={rank} local={local}")
+        # GPU: every device collective on the framework's own RCCL communicators; the c10d
+        # default group is gloo (store + host barriers only), so no ProcessGroupNCCL
+        # communicators exist and a communicator that cannot be built fails the run
+        comm.init_parallel_env("pa_rccl" if cuda else "gloo")
+        log(f"[bench] {comm.backend_name()} world={world} rank={rank} local={local}")
     if cuda:
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
@@ -122,6 +127,8 @@ def main():
     if args.layers:
         cfgd["num_hidden_layers"] = args.layers
     cfgd["max_position_embeddings"] = max(args.seq_len, cfgd.get("max_position_embeddings", 2048))
+    if args.dtype:
+        cfgd["dtype"] = args.dtype
     cfg = LlamaConfig(**cfgd, recompute=args.recompute)
     t0 = time.time()
     model = LlamaForCausalLM(cfg, device=dev)
@@ -155,7 +162,7 @@ def main():
 
     # recompute runs on the tape too (tape.checkpoint: the segment's forward is replayed
     # inside the reverse pass)
-    use_tape = args.autograd == "tape" and cuda
+    use_tape = args.autograd == "tape"
 
     def micro(x, y):
         if use_tape:
@@ -199,11 +206,11 @@ def main():
     el = time.perf_counter() - t0
     elt = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
-        torch.distributed.all_reduce(elt, op=torch.distributed.ReduceOp.MAX)
+        comm.all_reduce(elt, op=torch.distributed.ReduceOp.MAX)
     el = float(elt.item())
-    lt = (l.detach().float() * args.accum).reshape(1)
+    lt = (l.detach().float() * args.accum).reshape(1).contiguous()
     if world > 1:
-        torch.distributed.all_reduce(lt)
+        comm.all_reduce(lt)
     final_loss = float(lt.item()) / world
     tokens_per_step = world * args.accum * mb * S
     tps = tokens_per_step * args.steps / el
@@ -242,6 +249,9 @@ def main():
                 "grad_dtype": str(opt.grad_dtype).replace("torch.", ""),
                 "autograd": "tape" if use_tape else "torch",
                 "device": args.device,
+                "comm_backend": comm.backend_name(),
+                "bucket_mb": args.bucket_mb,
+                "dp_comm": opt.dp_comm if world > 1 else None,
             },
             "final_loss": round(final_loss, 5),
         }

@@ -470,6 +470,9 @@ class ShardedStage3:
                 p.data.copy_(master.view_as(p))
 
     def zero_grad(self):
+        from ..ops import accum as _accum
+
+        _accum.discard()  # deferred dW of an abandoned accumulation (ops/accum.py)
         if self.comm_stream is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
         self.g_all.zero_()

@@ -111,8 +111,35 @@ class LlamaDecoderLayer(Layer):
         for n in ("input_layernorm", "post_attention_layernorm"):
             getattr(self, n).no_weight_decay = True
         # gate|up columns interleaved in 16-column blocks (ops.interleave_gate_up) so the
-        # MLP runs as one fused node; tensor-parallel shards keep [gate | up]
+        # MLP runs as one fused node; tensor-parallel shards keep [gate | up].  The
+        # interleaving is an in-memory layout only: state dicts always carry the
+        # canonical [gate | up] matrix (_save_to_state_dict / _pa_state_in below), so
+        # checkpoints load the same whatever layout the loading model uses.
         self.mlp_interleaved = mlp_interleaved(cfg, tp)
+
+    # state-dict format version of gate_up_proj: 2 = canonical [gate | up] (always)
+    _version = 2
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        super()._save_to_state_dict(destination, prefix, keep_vars)
+        k = prefix + "gate_up_proj"
+        if self.mlp_interleaved and k in destination:
+            g, u = ops.deinterleave_gate_up(destination[k].detach())
+            destination[k] = torch.cat([g, u], -1)
+
+    def _pa_state_in(self, name, value):
+        """Canonical [gate | up] checkpoint tensor -> this layer's in-memory layout."""
+        if name == "gate_up_proj" and self.mlp_interleaved:
+            I = value.shape[-1] // 2
+            return ops.interleave_gate_up(value[..., :I], value[..., I:])
+        return value
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing, unexpected, errors):
+        k = prefix + "gate_up_proj"
+        if k in state_dict:
+            state_dict = dict(state_dict)
+            state_dict[k] = self._pa_state_in("gate_up_proj", state_dict[k])
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing, unexpected, errors)
 
     def forward(self, x, residual, cos, sin):
         cfg = self.cfg
@@ -215,7 +242,8 @@ class LlamaForCausalLM(Layer):
 
 def shard_llama_state_dict(full: dict, cfg: LlamaConfig, rank: int, world: int) -> dict:
     """Full (single-rank) LLaMA state dict -> tensor-parallel shard ``rank`` of ``world``
-    (column splits keep the [q|k|v] and [gate|up] packing per rank)."""
+    (column splits keep the [q|k|v] and [gate|up] packing per rank).  ``full`` is in
+    the canonical state-dict layout ([gate | up], ``LlamaDecoderLayer._version`` 2)."""
     if world == 1:
         return dict(full)
     D = cfg.head_dim
@@ -226,8 +254,7 @@ def shard_llama_state_dict(full: dict, cfg: LlamaConfig, rank: int, world: int) 
             q, kk, vv = v.split([nh * D, nkv * D, nkv * D], dim=1)
             out[k] = torch.cat([t.chunk(world, dim=1)[rank] for t in (q, kk, vv)], dim=1).contiguous()
         elif k.endswith("gate_up_proj"):
-            # the full model stores gate|up interleaved (mlp_interleaved); shards are [gate | up]
-            g, u = ops.deinterleave_gate_up(v) if mlp_interleaved(cfg) else v.split([I, I], dim=1)
+            g, u = v.split([I, I], dim=1)
             out[k] = torch.cat([g.chunk(world, dim=1)[rank], u.chunk(world, dim=1)[rank]], dim=1).contiguous()
         elif k.endswith("o_proj") or k.endswith("down_proj") or k == "embed_tokens":
             out[k] = v.chunk(world, dim=0)[rank].contiguous()

@@ -116,14 +116,21 @@ class Layer(torch.nn.Module):
         return parameter
 
     def set_state_dict(self, state_dict, use_structured_name=True):
-        own = self.state_dict()
+        own = self.state_dict().keys()
         missing = []
         with torch.no_grad():
-            for k, v in own.items():
+            for k in own:
                 if k in state_dict:
+                    # the live tensor (state_dict() entries may be converted copies)
+                    *path, attr = k.split(".")
+                    mod = self.get_submodule(".".join(path)) if path else self
+                    v = getattr(mod, attr)
                     src = state_dict[k]
                     if not torch.is_tensor(src):
                         src = torch.as_tensor(src)
+                    conv = getattr(mod, "_pa_state_in", None)
+                    if conv is not None:  # checkpoint layout -> in-memory layout
+                        src = conv(attr, src)
                     v.copy_(src.to(v.dtype).view(v.shape))
                 else:
                     missing.append(k)

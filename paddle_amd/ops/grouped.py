@@ -231,6 +231,7 @@ def _flush_all():
 
 
 _accum.register_flush(_flush_all)
+_accum.register_discard(_STASH.clear)
 
 
 class _F8Weights:

@@ -41,8 +41,11 @@ def _larr(vals):
 
 def fill_(t, value):
     """t[...] = value on the elementwise kernel of tensor_ops.hip (any device dtype
-    and layout the kernel covers; else torch's fill)."""
-    if t.is_cuda and t.numel():
+    and layout the kernel covers; else torch's fill).  The kernel takes the value as a
+    double: integer fills beyond 2**53 (int64 sentinels) take torch's exact fill."""
+    exact = not (not t.dtype.is_floating_point and not t.dtype.is_complex and isinstance(value, int)
+                 and abs(value) > 2 ** 53)
+    if t.is_cuda and t.numel() and exact:
         from . import _native as N
         from . import aten_native as A
 

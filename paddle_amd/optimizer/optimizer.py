@@ -136,6 +136,9 @@ class Optimizer:
 
     # ---------------------------------------------------------------- step
     def clear_grad(self, set_to_zero=True):
+        from ..ops import accum as _accum
+
+        _accum.discard()  # deferred dW of an abandoned accumulation (ops/accum.py)
         with _strict.region("optimizer:clear_grad"):
             self._clear_grad(set_to_zero)
 

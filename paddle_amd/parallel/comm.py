@@ -25,8 +25,17 @@ def env_rank_world():
     return rank, world, local
 
 
+_PA_ONLY: list = []  # init_parallel_env("pa_rccl"): device collectives ONLY on framework RCCL
+
+
 def init_parallel_env(backend: str | None = None, timeout_s: float = 1800.0):
-    """Initialise the default process group once (idempotent).  Returns (rank, world)."""
+    """Initialise the default process group once (idempotent).  Returns (rank, world).
+
+    ``backend="pa_rccl"``: the c10d default group is gloo -- used only for its TCP
+    store (communicator rendezvous) and host-side barriers -- and every device
+    collective runs on the framework's own RCCL communicators (``parallel/rccl.py``);
+    if one cannot be created the job fails instead of falling back, so each rank holds
+    exactly one set of RCCL communicators (no ProcessGroupNCCL ones)."""
     rank, world, local = env_rank_world()
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
@@ -34,6 +43,10 @@ def init_parallel_env(backend: str | None = None, timeout_s: float = 1800.0):
         return 0, 1
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "pa_rccl":
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        _PA_ONLY[:] = [True]
+        backend = "gloo"
     if backend == "nccl":
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -91,21 +104,39 @@ def _pa_comm(group, *ts):
     from . import rccl
 
     host = bool(_HOST_RCCL)
-    if not rccl.enabled() or not all(t.is_contiguous() and (t.is_cuda or host) for t in ts):
+    forced = bool(_PA_ONLY)
+    if forced and any(t.is_cuda for t in ts) and not all(t.is_contiguous() for t in ts):
+        # the c10d group is gloo in this mode: a device collective must not slip onto it
+        raise RuntimeError("pa_rccl-only process group: device collectives need contiguous operands")
+    if not (forced or rccl.enabled()) or not all(t.is_contiguous() and (t.is_cuda or host) for t in ts):
         return None
-    if not host and dist.get_backend(group) != "nccl":
+    if not host and not forced and dist.get_backend(group) != "nccl":
         return None
     dev = -1 if host else None
     try:
         return rccl.context_map().get(_group_ranks(group), dist.get_rank(), device=dev)
-    except rccl.RcclError as e:
-        # under the default ``auto`` mode a communicator that cannot be created (every
-        # rank sees the same librccl / device setup) leaves the collectives on c10d's
-        # ProcessGroupNCCL -- RCCL as well -- instead of failing the job
-        if os.environ.get("FLAGS_comm_backend", "auto") != "auto" or host:
+    except rccl.RcclUnavailable as e:
+        # the go / no-go verdict is agreed through the store by every rank of the group
+        # before any ncclCommInitRank (rccl.CommContextMap.get), so under the default
+        # ``auto`` mode ALL ranks fall back to c10d's ProcessGroupNCCL together (or, in
+        # the explicit modes, all raise) -- no rank is left blocked in a collective
+        if forced or os.environ.get("FLAGS_comm_backend", "auto") != "auto":
             raise
         rccl.disable_auto(f"framework RCCL communicator unavailable ({e}); using torch.distributed")
         return None
+
+
+def backend_name(group=None) -> str:
+    """Which layer carries this group's device collectives: ``pa_rccl`` (framework
+    communicators), ``c10d_nccl`` (torch.distributed's ProcessGroupNCCL), ``gloo`` or
+    ``none`` (one rank)."""
+    from . import rccl
+
+    if not is_dist():
+        return "none"
+    if _PA_ONLY or (rccl.enabled() and dist.get_backend(group) == "nccl"):
+        return "pa_rccl"
+    return "c10d_nccl" if dist.get_backend(group) == "nccl" else "gloo"
 
 
 class StreamWork:
@@ -173,6 +204,9 @@ def reduce_scatter(out, inp, group=None, async_op=False):
     if W == 1:
         out.copy_(inp)
         return None
+    c = _pa_comm(group, out, inp)
+    if c is not None:
+        return _run_pa(c, lambda cc: cc.reduce_scatter(out, inp), [out, inp], async_op)
     if _is_gloo(group):
         tmp = inp.clone()
         dist.all_reduce(tmp, group=group)
@@ -180,9 +214,6 @@ def reduce_scatter(out, inp, group=None, async_op=False):
         n = out.numel()
         out.copy_(tmp.view(-1)[r * n:(r + 1) * n].view_as(out))
         return None
-    c = _pa_comm(group, out, inp)
-    if c is not None:
-        return _run_pa(c, lambda cc: cc.reduce_scatter(out, inp), [out, inp], async_op)
     return dist.reduce_scatter_tensor(out, inp, group=group, async_op=async_op)
 
 
@@ -192,6 +223,9 @@ def all_gather(out, inp, group=None, async_op=False):
     if W == 1:
         out.copy_(inp)
         return None
+    c = _pa_comm(group, out, inp)
+    if c is not None:
+        return _run_pa(c, lambda cc: cc.all_gather(out, inp), [out, inp], async_op)
     if _is_gloo(group):
         chunks = list(out.view(W, -1).unbind(0))
         tmp = [torch.empty_like(c) for c in chunks]
@@ -199,9 +233,6 @@ def all_gather(out, inp, group=None, async_op=False):
         for c, t in zip(chunks, tmp):
             c.copy_(t)
         return None
-    c = _pa_comm(group, out, inp)
-    if c is not None:
-        return _run_pa(c, lambda cc: cc.all_gather(out, inp), [out, inp], async_op)
     return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
 
 

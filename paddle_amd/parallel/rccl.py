@@ -32,6 +32,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import math
 import os
 import threading
 
@@ -71,6 +72,35 @@ def _lib():
 
 class RcclError(RuntimeError):
     pass
+
+
+class RcclUnavailable(RcclError):
+    """Raised on EVERY rank of a group when any of its ranks cannot create its
+    communicator (the verdict is agreed through the store before ncclCommInitRank)."""
+
+
+def _local_ready(device: int) -> bool:
+    """What this rank can check alone before joining a clique: librccl loads and (for a
+    device communicator) the device index exists."""
+    if not available():
+        return False
+    if device < 0:
+        return True
+    try:
+        return 0 <= device < torch.cuda.device_count()
+    except Exception:
+        return False
+
+
+def agree(store, key: str, world: int, rank: int, ok: bool, timeout_s: float = 300.0) -> list:
+    """Every rank publishes ``ok`` under ``key`` and reads everyone's: returns the
+    (group-local) ranks that reported failure -- the same list on every rank."""
+    import datetime
+
+    store.set(f"{key}/ready/{rank}", b"1" if ok else b"0")
+    keys = [f"{key}/ready/{r}" for r in range(world)]
+    store.wait(keys, datetime.timedelta(seconds=timeout_s))
+    return [r for r, k in enumerate(keys) if bytes(store.get(k)) != b"1"]
 
 
 def _check(rc, what):
@@ -175,7 +205,7 @@ class Communicator:
         W = self.world
         if out.dtype != inp.dtype or out.shape[1:] != inp.shape[1:]:
             raise RcclError("all_to_all: input and output rows must match in dtype and shape")
-        row = inp[0].numel() if inp.dim() > 1 else 1
+        row = math.prod(inp.shape[1:])  # 1 for 1-D; works for zero-row sends
         ins = list(in_splits) if in_splits is not None else [inp.shape[0] // W] * W
         outs = list(out_splits) if out_splits is not None else [out.shape[0] // W] * W
         if len(ins) != W or len(outs) != W or sum(ins) != inp.shape[0] or sum(outs) != out.shape[0]:
@@ -237,7 +267,15 @@ class CommContextMap:
                     self._gen[key] = gen + 1
                     dev = torch.cuda.current_device() if device is None else device
                     name = f"pa_rccl/{'-'.join(map(str, key))}/{gen}"
-                    c = Communicator.rendezvous(self._default_store(), name, len(key), key.index(my_rank), dev)
+                    store = self._default_store()
+                    # collective go / no-go BEFORE ncclCommInitRank: a rank that cannot
+                    # build its communicator (librccl missing, bad device) must not leave
+                    # its peers blocked inside the init -- every rank sees the same
+                    # verdict, so an ``auto`` fallback is taken by all ranks or by none
+                    bad = agree(store, name, len(key), key.index(my_rank), _local_ready(dev))
+                    if bad:
+                        raise RcclUnavailable(f"framework RCCL unavailable on group ranks {bad} of {list(key)}")
+                    c = Communicator.rendezvous(store, name, len(key), key.index(my_rank), dev)
                     self._comms[key] = c
         return c
 

@@ -216,8 +216,10 @@ class FlatShardedOptimizer:
                 opt._sync = False
                 _accum.set_deferring(True)
 
-            def __exit__(self_, *a):
+            def __exit__(self_, exc_type, *a):
                 _accum.set_deferring(False)
+                if exc_type is not None:
+                    _accum.discard()  # a failed micro-batch: its deferred dW operands are stale
                 opt._sync = True
                 opt._ready = [0] * len(opt.buckets)
 
@@ -419,6 +421,7 @@ class FlatShardedOptimizer:
         fused.bump_weight_epoch()
 
     def zero_grad(self, set_to_none=False):
+        _accum.discard()  # deferred dW of an abandoned accumulation must not leak into the next step
         if self.main_grad:
             # lazy zero: the first gradient write of the next step overwrites its
             # slice (fused dW GEMM with beta = 0, or copy_ in the hook); slices that

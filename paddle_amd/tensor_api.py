@@ -115,8 +115,12 @@ def _filled(shape, value, dtype, device):
 
 def _filled_like(x, value, dtype):
     dt = _dtype(dtype) or x.dtype
-    if x.is_cuda:
-        return _filled(list(x.shape), value, dt, x.device)
+    if x.is_cuda and not isinstance(value, complex):
+        from .ops import oplib
+
+        # empty_like keeps x's memory format (channels-last stays channels-last)
+        with torch._C.DisableTorchFunctionSubclass():
+            return oplib.fill_(torch.empty_like(x, dtype=dt), value)
     return torch.full_like(x, value, dtype=dt)
 
 

@@ -215,3 +215,23 @@ def test_matmul_handlers():
     ab, bb = a.to(torch.bfloat16), b.to(torch.bfloat16)
     _check(lambda x, y: x @ y, ab, bb, atol=3e-2, rtol=2e-2)
     _check(lambda x, y: x.t() @ y.t().contiguous().t(), ab[:48, :40].contiguous(), bb, atol=3e-2, rtol=2e-2)
+
+
+def test_full_int64_beyond_double_precision_and_like_memory_format():
+    """the fill kernel takes a double; int64 values beyond 2**53 must stay
+    exact, and *_like creation keeps the input's memory format."""
+    import paddle_amd.tensor_api as T
+
+    big = 2 ** 62 + 1
+    t = T.full([2], big, "int64")
+    assert t.tolist() == [big, big]
+    m = torch.iinfo(torch.int64).max
+    assert T.full([3], m, "int64").tolist() == [m] * 3
+    from paddle_amd.ops import oplib
+
+    z = torch.empty(4, dtype=torch.int64, device=dev)
+    assert oplib.fill_(z, big).tolist() == [big] * 4
+    assert oplib.fill_(z, -m).tolist() == [-m] * 4
+    x = torch.randn(2, 3, 4, 5, device=dev).to(memory_format=torch.channels_last)
+    y = T.ones_like(x)
+    assert y.is_contiguous(memory_format=torch.channels_last) and bool((y == 1).all())

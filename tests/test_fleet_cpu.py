@@ -3,6 +3,8 @@ against a single-process reference run of the same model on the same data."""
 import pytest
 import torch
 
+from paddle_amd import ops
+
 from dist_util import assert_adam_close, run_dist
 from paddle_amd.distributed.topology import CommunicateTopology
 from paddle_amd.models.llama import (LLAMA_CONFIGS, LlamaConfig, LlamaForCausalLM, LlamaPretrainingCriterion,
@@ -39,7 +41,10 @@ def _tp_worker(rank, world):
     b = _batch()
     loss_ref = full(b[:, :-1], b[:, 1:])
     loss_ref.backward()
-    grads_ref = {n: p.grad for n, p in full.named_parameters()}
+    # gradients in the canonical (state-dict) layout: gate_up de-interleaved like weights
+    grads_ref = {n: (torch.cat(ops.deinterleave_gate_up(p.grad), -1)
+                     if n.endswith("gate_up_proj") and full.layers[0].mlp_interleaved else p.grad)
+                 for n, p in full.named_parameters()}
     tp = TPGroup(None)
     m = LlamaForCausalLM(cfg, "cpu", tp=tp)
     sd = shard_llama_state_dict({k: v.detach() for k, v in full.state_dict().items()}, cfg, rank, world)

@@ -277,3 +277,51 @@ def test_ernie_moe_deferred_expert_dw_matches_per_microbatch():
     for n in ref:
         err = (got[n] - ref[n]).norm() / ref[n].norm().clamp_min(1e-30)
         assert err < 1e-2, (n, float(err))
+
+
+def test_abandoned_accumulation_does_not_leak_deferred_expert_dw():
+    """no_sync micro-batches followed by zero_grad WITHOUT a step (an AMP
+    inf skip, a discarded batch) must not leave their deferred expert-dW operands in
+    the stash: the next step's main_grad equals the non-deferred path's."""
+    from paddle_amd.autograd import tape
+    from paddle_amd.models.ernie_moe import ERNIE_MOE_CONFIGS, ErnieMoEConfig, ErnieMoEForCausalLM
+    from paddle_amd.ops import accum, grouped as GR
+    from paddle_amd.parallel.sharding import FlatShardedOptimizer
+
+    def grads(defer):
+        torch.manual_seed(0)
+        cfg = ErnieMoEConfig(**dict(ERNIE_MOE_CONFIGS["ernie-moe-tiny"], hidden_size=256, moe_intermediate_size=128,
+                                    intermediate_size=512, grouped_experts=True, max_position_embeddings=512,
+                                    num_experts=8))
+        m = ErnieMoEForCausalLM(cfg, torch.device(dev))
+        opt = FlatShardedOptimizer(m.named_parameters(), lr=0.0, grad_dtype=torch.float32)
+        gen = torch.Generator().manual_seed(6)
+        batches = [torch.randint(0, cfg.vocab_size, (2, 257), generator=gen).to(dev) for _ in range(3)]
+        # abandoned accumulation: one no_sync micro-batch, then zero_grad with no step
+        with opt.no_sync():
+            with tape.recording() as t:
+                loss = m(batches[0][:, :-1], batches[0][:, 1:])
+            t.backward(loss)
+        opt.zero_grad()
+        assert not GR._STASH
+        for j in (1, 2):
+            ctx = opt.no_sync() if (defer and j == 1) else __import__("contextlib").nullcontext()
+            with ctx:
+                with tape.recording() as t:
+                    loss = m(batches[j][:, :-1], batches[j][:, 1:])
+                t.backward(loss)
+        torch.cuda.synchronize()
+        return {n: p._pa_main_grad.clone() for n, p in m.named_parameters() if "gate_up" in n or "down" in n}
+
+    old = GR._DEFER_ON
+    try:
+        GR._DEFER_ON = False
+        ref = grads(False)
+        GR._DEFER_ON = True
+        got = grads(True)
+    finally:
+        GR._DEFER_ON = old
+        accum.set_deferring(False)
+    for n in ref:
+        err = (got[n] - ref[n]).norm() / ref[n].norm().clamp_min(1e-30)
+        assert err < 1e-2, (n, float(err))

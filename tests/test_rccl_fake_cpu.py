@@ -167,3 +167,55 @@ def _watchdog_worker(rank, world, lib):
 def test_watchdog_exits_on_peer_failure(fake_lib):
     for ok, left in run_dist(_watchdog_worker, 2, fake_lib):
         assert ok and left == 0
+
+
+def _zero_row_worker(rank, world, lib):
+    """an expert-parallel rank with no routed tokens sends zero rows."""
+    comm, _ = _setup(lib)
+    # rank 0 sends nothing to anyone; every other rank sends one row to each peer
+    ins = [0 if rank == 0 else 1] * world
+    inp = torch.full((sum(ins), 3), float(rank))
+    outs = [0 if p == 0 else 1 for p in range(world)]
+    out = torch.empty(sum(outs), 3)
+    comm.all_to_all(out, inp, out_splits=outs, in_splits=ins)
+    empty = torch.empty(0, 3)
+    comm.all_to_all(torch.empty(0, 3), empty, out_splits=[0] * world, in_splits=[0] * world)
+    return out
+
+
+def test_all_to_all_with_zero_rows(fake_lib):
+    W = 3
+    for r, out in enumerate(run_dist(_zero_row_worker, W, fake_lib)):
+        assert torch.equal(out, torch.cat([torch.full((1, 3), float(p)) for p in range(1, W)]))
+
+
+def _agree_worker(rank, world, lib, mode):
+    """One rank cannot build its communicator: the go / no-go verdict is agreed through
+    the store, so EVERY rank takes the same branch -- all fall back to torch.distributed
+    under ``auto``, all raise under ``pa_rccl`` -- and nobody hangs in the init."""
+    import warnings
+
+    comm, rccl = _setup(lib)
+    os.environ["FLAGS_comm_backend"] = mode
+    rccl._AUTO[:] = [True]
+    if rank == 1:
+        rccl._local_ready = lambda dev: False
+    x = torch.full((4,), float(rank + 1))
+    try:
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            comm.all_reduce(x)
+        outcome = "ok"
+    except rccl.RcclUnavailable:
+        outcome = "raised"
+    return outcome, x, len(rccl.context_map()._comms), bool(rccl._AUTO and rccl._AUTO[0])
+
+
+def test_unavailable_rank_gives_one_verdict_for_all(fake_lib):
+    W = 3
+    for outcome, x, ncomm, auto_on in run_dist(_agree_worker, W, fake_lib, "auto"):
+        # every rank fell back together: the sum ran on gloo, no communicator was built
+        assert outcome == "ok" and ncomm == 0 and not auto_on
+        assert torch.equal(x, torch.full((4,), float(sum(range(1, W + 1)))))
+    for outcome, _, ncomm, _ in run_dist(_agree_worker, W, fake_lib, "pa_rccl"):
+        assert outcome == "raised" and ncomm == 0
