@@ -23,9 +23,11 @@ kernel is run by its registered Python kernel through the executor's per-op
 fallback callback (the op's inputs are zero-copy views of the native buffers, its
 outputs are lent back to the native scope), counted in ``py_fallbacks``.  On a HIP
 place the native kernels run on torch's current stream, so the two kernel
-libraries are ordered without host syncs.  Programs that need per-step scopes
-(``while_grad``, ``recurrent``, ``conditional_block_grad``) or non-tensor variables
-(SelectedRows gradients) raise ``NotImplementedError`` -- use the default engine.
+libraries are ordered without host syncs.  ``while_grad`` / ``conditional_block_grad``
+run natively over kept step scopes (core.cc RunWhile / RunWhileGrad), as do tensor
+arrays, rank tables and SelectedRows gradients with the sparse SGD / Adam kernels.
+What still goes to the interpreter (``framework/executor.py``): ``recurrent``, ``parallel_do``,
+``go`` / ``select`` and the RPC / pserver ops (``_UNSUPPORTED_CF``, ``_RPC_OPS``).
 
 The engine drives the C++ objects through the ``paddle_amd_core`` CPython
 extension (csrc/pybind/core_module.cc, pybind11) when it is built, else through
