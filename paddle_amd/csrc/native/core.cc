@@ -617,6 +617,7 @@ Executor::Executor(int device) {
   }
   link_host_kernels();
   link_control_kernels();
+  link_rnn_kernels();
 }
 
 Executor::~Executor() {

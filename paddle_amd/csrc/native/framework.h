@@ -237,6 +237,7 @@ struct KernelRegistrar {
 void link_host_kernels();
 void link_device_kernels();
 void link_control_kernels();
+void link_rnn_kernels();
 
 // ---------------------------------------------------------------- executor
 class Executor {

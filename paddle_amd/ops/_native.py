@@ -218,6 +218,8 @@ _SIGS = {
     "pa_lstm_unit": [_I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _F, _P],
     "pa_maxout": [_I, _P, _P, _P, _P, _I, _I, _I, _L, _P],
     "pa_flash_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _LP, _I, _I, _I, _I, _I, _I, _F, _I, _P, _P],
+    "pa_fa_bwd_split_ok": [_I, _I, _I, _I, _I, _I, _LP],
+    "pa_fa_bwd_split": [_P] * 10 + [_LP, _I, _I, _I, _I, _I, _I, _F, _I, _P, _P, _P],
 }
 
 

@@ -318,6 +318,34 @@ def _fa_bwd(q, k, v, o, do, lse, causal, scale, dk, dv, dq_rope_out=None):
     return dq_acc
 
 
+_FA_SPLIT = os.environ.get("FLAGS_fa_bwd_split", "1") not in ("0", "false", "False")
+
+
+def _fa_bwd_split(q, k, v, o, do, lse, causal, scale, dq, dk, dv, cos=None, sin=None):
+    """The two-kernel flash-attention backward (csrc/kernels/fa_bwd_split.hip): dQ
+    (query-stationary, computes delta itself) then dK / dV (key-stationary, GQA group
+    summed in registers), bf16 results written straight into ``dq`` [B, Sq, Hq, D] and
+    ``dk`` / ``dv`` [B, Sk, Hkv, D] (any strides with unit D stride), with the inverse
+    rotary applied to dq / dk when ``cos`` / ``sin`` are given.  Returns False (nothing
+    written) when the shape is not covered (D != 128, 32-bit offsets)."""
+    if not _FA_SPLIT:
+        return False
+    B, Sq, Hq, D = q.shape
+    Sk, Hk = k.shape[1], k.shape[2]
+    st = ctypes_long_array(_fa_strides(q) + _fa_strides(k) + _fa_strides(v) + _fa_strides(o) + _fa_strides(do)
+                           + _fa_strides(dq) + _fa_strides(dk) + _fa_strides(dv))
+    if not N.lib().pa_fa_bwd_split_ok(B, Sq, Sk, Hq, Hk, D, st):
+        return False
+    if cos is not None:
+        assert cos.dtype == torch.float32 and cos.is_contiguous() and sin.is_contiguous()
+        assert cos.shape[0] >= max(Sq, Sk) and cos.shape[1] == D // 2
+    ld2 = torch.empty(B, Hq, Sq, 2, dtype=torch.float32, device=q.device)
+    N.call("pa_fa_bwd_split", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(o), N.ptr(do), N.ptr(lse), N.ptr(ld2),
+           N.ptr(dq), N.ptr(dk), N.ptr(dv), st, B, Sq, Sk, Hq, Hk, D, float(scale), int(causal),
+           N.ptr(cos), N.ptr(sin), N.stream())
+    return True
+
+
 def ctypes_long_array(vals):
     import ctypes
     return (ctypes.c_long * len(vals))(*[int(x) for x in vals])
@@ -337,6 +365,10 @@ class _FlashAttnFn(torch.autograd.Function):
         do = _c(do)
         B, Sq, Hq, D = q.shape
         Sk, Hk = k.shape[1], k.shape[2]
+        dq = torch.empty_like(q)
+        dkk, dvv = torch.empty_like(k), torch.empty_like(v)
+        if _fa_bwd_split(q, k, v, o, do, lse, ctx.causal, ctx.scale, dq, dkk, dvv):
+            return dq, dkk, dvv, None, None
         dk = torch.empty(B, Sk, Hq, D, dtype=q.dtype, device=q.device)
         dv = torch.empty_like(dk)
         dq_acc = _fa_bwd(q, k, v, o, do, lse, ctx.causal, ctx.scale, dk, dv)
@@ -472,6 +504,11 @@ def _rope_attn_backward(packed, o, lse, cos, sin, do, Hq, Hk, D, causal, scale):
     do = _c(do).view(B, S, Hq, D)
     dqkv = torch.empty_like(packed)
     d4 = dqkv.view(B, S, nh, D)
+    # two-kernel backward: dq / dk inverse-rotated, GQA-summed and stored in bf16 straight
+    # into dqkv's slots -- no dQ slabs, no reduce, no dk rotary pass, no GQA fold
+    if _fa_bwd_split(q, k, v, o, do, lse, causal, scale, d4[:, :, :Hq], d4[:, :, Hq:Hq + Hk],
+                     d4[:, :, Hq + Hk:], cos, sin):
+        return dqkv
     # dq: summed, inverse-rotated and cast straight into dqkv's dq slot when the
     # partial-slab kernel runs (else via the fp32 accumulator + one rope pass)
     rope_out = (dqkv, W, cos, sin)
@@ -653,6 +690,9 @@ class _PackedAttnFn(torch.autograd.Function):
         do = _c(do).view(B, S, H, D)
         dqkv = torch.empty_like(qkv)
         d4 = dqkv.view(B, S, 3 * H, D)
+        if _fa_bwd_split(p4[:, :, :H], p4[:, :, H:2 * H], p4[:, :, 2 * H:], o, do, lse, causal, scale,
+                         d4[:, :, :H], d4[:, :, H:2 * H], d4[:, :, 2 * H:]):
+            return dqkv, None, None, None, None
         cos, sin = _identity_rope(S, D, qkv.device)
         dq_acc = _fa_bwd(p4[:, :, :H], p4[:, :, H:2 * H], p4[:, :, 2 * H:], o, do, lse, causal, scale,
                          d4[:, :, H:2 * H], d4[:, :, 2 * H:], (dqkv, W, cos, sin))

@@ -341,12 +341,45 @@ def test_flash_attention_bwd_variants(variant, causal, S, Hq, Hk):
     v = torch.randn(B, S, Hk, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
     do = torch.randn(B, S, Hq, D, device=dev, dtype=torch.bfloat16)
     _native.call("pa_fa_bwd_set_variant", variant)
+    split, F._FA_SPLIT = F._FA_SPLIT, False  # the single-kernel variants, not the split path
     try:
         o = F.flash_attention(q, k, v, causal=causal)
         o.backward(do)
     finally:
         _native.call("pa_fa_bwd_set_variant", 4)
+        F._FA_SPLIT = split
     qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
     F._attn_ref(qr, kr, vr, causal, 1 / math.sqrt(D)).backward(do.float())
     for a, b_ in ((q.grad, qr.grad), (k.grad, kr.grad), (v.grad, vr.grad)):
         assert _rel(a, b_) < 2e-2, _rel(a, b_)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("Sq,Sk,Hq,Hk", [(192, 320, 4, 2), (320, 192, 2, 2), (64, 64, 2, 1), (130, 130, 3, 3),
+                                          (2048, 2048, 2, 2)])
+def test_flash_attention_split_bwd(causal, Sq, Sk, Hq, Hk):
+    """The two-kernel backward (fa_bwd_split.hip) on ragged / unequal query and key
+    lengths and GQA groups, against the fp32 reference; it must be the path taken."""
+    if causal and Sq > Sk:
+        pytest.skip("causal with Sq > Sk leaves query rows with no key (NaN in the reference)")
+    torch.manual_seed(2)
+    B, D = 2, 128
+    q = torch.randn(B, Sq, Hq, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, Sk, Hk, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, Sk, Hk, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    do = torch.randn(B, Sq, Hq, D, device=dev, dtype=torch.bfloat16)
+    calls = []
+    orig = F._fa_bwd_split
+    F._fa_bwd_split = lambda *a, **kw: calls.append(1) or orig(*a, **kw)
+    try:
+        o = F.flash_attention(q, k, v, causal=causal)
+        o.backward(do)
+    finally:
+        F._fa_bwd_split = orig
+    assert calls and F._FA_SPLIT
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = F._attn_ref(qr, kr, vr, causal, 1 / math.sqrt(D))
+    orf.backward(do.float())
+    assert _rel(o, orf) < 1e-2
+    for n, a, b_ in (("dq", q.grad, qr.grad), ("dk", k.grad, kr.grad), ("dv", v.grad, vr.grad)):
+        assert _rel(a, b_) < 2e-2, (n, _rel(a, b_))

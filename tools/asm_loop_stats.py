@@ -20,7 +20,7 @@ for i, l in enumerate(body):
         tgt = m.group(1) or m.group(2)
         if tgt in labels and labels[tgt] < i:
             n = sum("mfma" in x for x in body[labels[tgt]:i])
-            if n >= 32:
+            if n >= int(__import__("os").environ.get("MIN_MFMA", "32")):
                 cands.append((i - labels[tgt], labels[tgt], i))
 # innermost loop that carries the matrix work (the k-loop), not the tile loop
 _, lo, hi = min(cands)
