@@ -618,6 +618,7 @@ Executor::Executor(int device) {
   link_host_kernels();
   link_control_kernels();
   link_rnn_kernels();
+  link_struct_kernels();
 }
 
 Executor::~Executor() {

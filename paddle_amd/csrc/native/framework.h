@@ -238,6 +238,7 @@ void link_host_kernels();
 void link_device_kernels();
 void link_control_kernels();
 void link_rnn_kernels();
+void link_struct_kernels();
 
 // ---------------------------------------------------------------- executor
 class Executor {

@@ -1915,6 +1915,12 @@ void device_fill(void* stream, void* dst, DT dt, int64_t n, double v) {
 
 void link_device_kernels() {}
 
+// helpers for the device kernels of other translation units (device_util.h)
+void* device_upload(const OpRun& r, const char* name, const void* src, size_t bytes) {
+  return upload_host(r, name, src, bytes);
+}
+float* device_workspace(const OpRun& r, const char* name, int64_t n) { return workspace(r, name, n); }
+
 // GEMM entry for tests / benchmarks (C ABI below)
 void device_sgemm(void* stream, bool ta, bool tb, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
                   int64_t lda, const float* B, int64_t ldb, float beta, float* C, int64_t ldc) {

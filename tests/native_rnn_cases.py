@@ -77,3 +77,63 @@ CASES = {
     "gru": (gru_net(), {}),
     "gru_rev_h0": (gru_net(rev=True, h0=True), {"h0": True}),
 }
+
+
+# ---------------------------------------------------------------------------------
+# book label_semantic_roles (tests/book/test_label_semantic_roles.py db_lstm) at toy
+# sizes: 8 LoD feature slots -> embeddings (one shared, frozen; is_sparse ones) -> fc
+# -> sums -> a stack of dynamic_lstm alternating direction (relu candidate, sigmoid
+# cell) -> linear_chain_crf cost with SGD on exponential_decay; crf_decoding fetched.
+WD, LD, PD, MD = 30, 7, 6, 2  # word / label / predicate dicts, mark dict
+
+
+def srl(depth=3, hidden=8, word_dim=4, mark_dim=3):
+    def build():
+        names = ["word", "verb", "ctx_n2", "ctx_n1", "ctx_0", "ctx_p1", "ctx_p2", "mark"]
+        feats = {n: fluid.layers.data(name=n, shape=[1], dtype="int64", lod_level=1) for n in names}
+        target = fluid.layers.data(name="target", shape=[1], dtype="int64", lod_level=1)
+        pred_emb = fluid.layers.embedding(input=feats["verb"], size=[PD, word_dim], is_sparse=True,
+                                          param_attr="vemb")
+        mark_emb = fluid.layers.embedding(input=feats["mark"], size=[MD, mark_dim], is_sparse=True)
+        embs = [fluid.layers.embedding(size=[WD, word_dim], input=feats[n],
+                                       param_attr=fluid.ParamAttr(name="emb", trainable=False))
+                for n in ("word", "ctx_n2", "ctx_n1", "ctx_0", "ctx_p1", "ctx_p2")]
+        embs += [pred_emb, mark_emb]
+        h0 = fluid.layers.sums(input=[fluid.layers.fc(input=e, size=hidden) for e in embs])
+        lstm = fluid.layers.dynamic_lstm(input=fluid.layers.fc(h0, 4 * hidden), size=4 * hidden,
+                                         candidate_activation="relu", gate_activation="sigmoid",
+                                         cell_activation="sigmoid")[0]
+        tmp = [h0, lstm]
+        for i in range(1, depth):
+            mix = fluid.layers.sums(input=[fluid.layers.fc(input=tmp[0], size=hidden),
+                                           fluid.layers.fc(input=tmp[1], size=hidden)])
+            lstm = fluid.layers.dynamic_lstm(input=fluid.layers.fc(mix, 4 * hidden), size=4 * hidden,
+                                             candidate_activation="relu", gate_activation="sigmoid",
+                                             cell_activation="sigmoid", is_reverse=(i % 2) == 1)[0]
+            tmp = [mix, lstm]
+        feature = fluid.layers.sums(input=[fluid.layers.fc(input=tmp[0], size=LD, act="tanh"),
+                                           fluid.layers.fc(input=tmp[1], size=LD, act="tanh")])
+        crf_cost = fluid.layers.linear_chain_crf(input=feature, label=target,
+                                                 param_attr=fluid.ParamAttr(name="crfw", learning_rate=0.5))
+        avg = fluid.layers.mean(crf_cost)
+        fluid.optimizer.SGD(learning_rate=fluid.layers.exponential_decay(
+            learning_rate=0.05, decay_steps=3, decay_rate=0.5, staircase=True)).minimize(avg)
+        decode = fluid.layers.crf_decoding(input=feature, param_attr=fluid.ParamAttr(name="crfw"))
+        return [avg, decode]
+    return build
+
+
+def srl_feeds(steps=4):
+    out = []
+    for seed in range(steps):
+        rs = np.random.RandomState(100 + seed)
+        lens = rs.randint(2, 8, 4).tolist()
+        off = np.concatenate([[0], np.cumsum(lens)]).tolist()
+        n = off[-1]
+
+        def ids(hi):
+            return core.LoDTensor(torch.from_numpy(rs.randint(0, hi, (n, 1)).astype("int64")), [off])
+        fd = {k: ids(WD) for k in ("word", "ctx_n2", "ctx_n1", "ctx_0", "ctx_p1", "ctx_p2")}
+        fd.update(verb=ids(PD), mark=ids(MD), target=ids(LD))
+        out.append(fd)
+    return out

@@ -20,3 +20,18 @@ def test_native_rnn_matches_interpreter(case):
     for a, b in zip(ref, got):
         np.testing.assert_allclose(b[0], a[0], rtol=1e-5, atol=1e-6)
     assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+
+
+def test_book_label_semantic_roles_native():
+    """The book SRL model (db_lstm + linear_chain_crf + crf_decoding, SGD with
+    exponential_decay) runs entirely on the C++ executor and follows the interpreter."""
+    from native_rnn_cases import srl, srl_feeds
+
+    fd = srl_feeds(4)
+    place = fluid.CPUPlace()
+    ref, init, _ = run(srl(), fd, "python", place)
+    got, _, exe = run(srl(), fd, "native", place, init)
+    for a, b in zip(ref, got):
+        np.testing.assert_allclose(b[0], a[0], rtol=1e-5, atol=1e-6)
+        np.testing.assert_array_equal(b[1], a[1])
+    assert not exe._native.py_fallbacks, exe._native.py_fallbacks

@@ -1,0 +1,44 @@
+"""The LoD lstm / gru programs of test_native_rnn_cpu.py on a HIP place: the device
+kernels (csrc/native/ops_rnn_gpu.hip -- one pa_sgemm per time step plus a fused cell
+kernel) run every recurrent op, forward and grad, with no Python-kernel fallback and
+no host round trip, following the interpreter on the same device to 2e-4."""
+import numpy as np
+import pytest
+
+import paddle_amd.fluid as fluid
+
+from native_control_cases import run
+from native_rnn_cases import CASES, feeds
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_native_rnn_matches_interpreter_gpu(case):
+    build, kw = CASES[case]
+    fd = feeds(4, **kw)
+    place = fluid.CUDAPlace(0)
+    ref, init, _ = run(build, fd, "python", place)
+    got, _, exe = run(build, fd, "native", place, init)
+    for a, b in zip(ref, got):
+        np.testing.assert_allclose(b[0], a[0], rtol=2e-4, atol=2e-5)
+    eng = exe._native
+    assert not eng.py_fallbacks, eng.py_fallbacks
+    assert not eng.host_fallbacks(), eng.host_fallbacks()
+
+
+def test_book_label_semantic_roles_native_gpu():
+    """Book SRL (db_lstm + linear_chain_crf + crf_decoding) on the device kernels:
+    no Python fallback, no host round trip; decoded paths equal the interpreter's."""
+    from native_rnn_cases import srl, srl_feeds
+
+    fd = srl_feeds(4)
+    place = fluid.CUDAPlace(0)
+    ref, init, _ = run(srl(), fd, "python", place)
+    got, _, exe = run(srl(), fd, "native", place, init)
+    for a, b in zip(ref, got):
+        np.testing.assert_allclose(b[0], a[0], rtol=2e-4, atol=2e-5)
+        np.testing.assert_array_equal(b[1], a[1])
+    eng = exe._native
+    assert not eng.py_fallbacks, eng.py_fallbacks
+    assert not eng.host_fallbacks(), eng.host_fallbacks()
