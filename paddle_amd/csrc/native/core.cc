@@ -619,6 +619,8 @@ Executor::Executor(int device) {
   link_control_kernels();
   link_rnn_kernels();
   link_struct_kernels();
+  link_beam_kernels();
+  link_optim_kernels();
 }
 
 Executor::~Executor() {
@@ -894,11 +896,53 @@ void Executor::RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* 
       }
     return n > 0;
   };
+  // the reference's InferShape ShareLoD("X", "Out") default (the Python op library's
+  // register_op share_lod=True): an output with no LoD and as many rows as the first
+  // LoD-carrying input takes that input's LoD; the ops registered share_lod=False there
+  // are exempt (their kernels set the output LoD themselves)
+  auto share_lod = [&](const OpDesc& op) {
+    static const std::set<std::string> exempt = {
+        "array_to_lod_tensor", "array_to_lod_tensor_grad", "attention_lstm", "conditional_block",
+        "conditional_block_grad", "feed", "fetch", "fusion_seqexpand_concat_fc", "go", "gru_unit",
+        "hierarchical_sigmoid", "linear_chain_crf", "lod_rank_table", "lod_reset", "lod_tensor_to_array",
+        "lod_tensor_to_array_grad", "lstm_unit", "merge_lod_tensor", "nce", "parallel_do", "read",
+        "read_from_array", "read_from_array_grad", "recurrent", "reorder_lod_tensor_by_rank",
+        "reorder_lod_tensor_by_rank_grad", "select", "sequence_concat", "sequence_erase", "sequence_expand",
+        "sequence_expand_as", "sequence_pad", "sequence_pool", "sequence_reshape", "sequence_scatter",
+        "sequence_slice", "sequence_unpad", "shrink_rnn_memory", "shrink_rnn_memory_grad", "split_lod_tensor",
+        "warpctc", "while", "while_grad", "write_to_array", "write_to_array_grad", "beam_search",
+        "beam_search_decode", "crf_decoding"};
+    if (exempt.count(op.type)) return;
+    const Tensor* first = nullptr;
+    for (auto& slot : op.inputs) {
+      if (slot.second.empty()) continue;
+      Variable* v = scope->Find(slot.second[0]);
+      if (v && v->kind == VK_LOD_TENSOR && v->tensor.initialized() && !v->tensor.lod.empty()) {
+        first = &v->tensor;
+        break;
+      }
+    }
+    if (!first || first->dims.empty()) return;
+    const LoD lod = first->lod;
+    const int64_t rows = first->dims[0];
+    for (auto& slot : op.outputs)
+      for (auto& n : slot.second) {
+        Variable* v = scope->Find(n);
+        if (v && v->kind == VK_LOD_TENSOR && v->tensor.initialized() && v->tensor.lod.empty() &&
+            !v->tensor.dims.empty() && v->tensor.dims[0] == rows)
+          v->tensor.lod = lod;
+      }
+  };
   auto timed = [&](const OpDesc& op, const std::function<void()>& fn) {
-    if (!profile) return fn();
+    if (!profile) {
+      fn();
+      share_lod(op);
+      return;
+    }
     Sync();
     auto t0 = std::chrono::steady_clock::now();
     fn();
+    share_lod(op);
     Sync();
     auto& e = op_time_ms[op.type];
     e.first += 1;

@@ -239,6 +239,8 @@ void link_device_kernels();
 void link_control_kernels();
 void link_rnn_kernels();
 void link_struct_kernels();
+void link_beam_kernels();
+void link_optim_kernels();
 
 // ---------------------------------------------------------------- executor
 class Executor {

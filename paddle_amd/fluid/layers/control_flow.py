@@ -72,6 +72,11 @@ def array_write(x, i, array=None):
     if array is None:
         array = helper.create_variable(name=f"{helper.name}.out", type=core.VT.LOD_TENSOR_ARRAY, dtype=x.dtype)
     helper.append_op(type="write_to_array", inputs={"X": [x], "I": [i]}, outputs={"Out": [array]})
+    # compile-time WriteToArrayInferShape: the array's desc carries its element shape
+    # and LoD level (tensor_array_read_write_op.cc), which array_read hands on
+    if not array.shape and x.shape:
+        array.shape = tuple(x.shape)
+        array.lod_level = x.lod_level
     return array
 
 
@@ -79,6 +84,9 @@ def array_read(array, i):
     helper = LayerHelper("array_read", **locals())
     out = helper.create_variable_for_type_inference(dtype=array.dtype)
     helper.append_op(type="read_from_array", inputs={"X": [array], "I": [i]}, outputs={"Out": [out]})
+    if array.shape:  # ReadFromArrayInferShape (compile time): the element shape of the array
+        out.shape = tuple(array.shape)
+        out.lod_level = array.lod_level
     return out
 
 

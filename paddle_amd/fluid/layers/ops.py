@@ -53,7 +53,14 @@ def gaussian_random(shape, mean=0.0, std=1.0, seed=0, dtype="float32"):
 
 def _logic(op, unary=False):
     def f(x, y=None, out=None, name=None):
-        return simple_op(op, {"X": x} if unary else {"X": x, "Y": y}, dtype="bool", name=name)
+        ins = {"X": x} if unary else {"X": x, "Y": y}
+        if out is None:
+            return simple_op(op, ins, dtype="bool", name=name)
+        # write into the given variable (e.g. a While condition updated in the loop body)
+        from ..layer_helper import LayerHelper
+
+        LayerHelper(op, name=name).append_op(type=op, inputs=ins, outputs={"Out": [out]})
+        return out
 
     f.__name__ = op
     return f

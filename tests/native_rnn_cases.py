@@ -137,3 +137,104 @@ def srl_feeds(steps=4):
         fd.update(verb=ids(PD), mark=ids(MD), target=ids(LD))
         out.append(fd)
     return out
+
+
+# ---------------------------------------------------------------------------------
+# book machine_translation (tests/book/test_machine_translation.py) at toy sizes:
+# training = LSTM encoder + DynamicRNN decoder, Adagrad with L2 decay; decoding =
+# the While loop with topk + beam_search over tensor arrays + beam_search_decode.
+MT_DICT, MT_WORD, MT_HID, MT_BEAM, MT_MAXLEN, MT_END = 20, 6, 8, 2, 4, 3
+
+
+def _mt_encoder():
+    src = fluid.layers.data(name="src_word_id", shape=[1], dtype="int64", lod_level=1)
+    emb = fluid.layers.embedding(input=src, size=[MT_DICT, MT_WORD], param_attr=fluid.ParamAttr(name="vemb"))
+    fc1 = fluid.layers.fc(input=emb, size=MT_HID * 4, act="tanh")
+    hid, _ = fluid.layers.dynamic_lstm(input=fc1, size=MT_HID * 4)
+    return fluid.layers.sequence_last_step(input=hid)
+
+
+def mt_train():
+    ctx = _mt_encoder()
+    trg = fluid.layers.data(name="target_language_word", shape=[1], dtype="int64", lod_level=1)
+    trg_emb = fluid.layers.embedding(input=trg, size=[MT_DICT, MT_WORD], param_attr=fluid.ParamAttr(name="vemb"))
+    rnn = fluid.layers.DynamicRNN()
+    with rnn.block():
+        w = rnn.step_input(trg_emb)
+        pre = rnn.memory(init=ctx)
+        cur = fluid.layers.fc(input=[w, pre], size=MT_HID, act="tanh")
+        score = fluid.layers.fc(input=cur, size=MT_DICT, act="softmax")
+        rnn.update_memory(pre, cur)
+        rnn.output(score)
+    label = fluid.layers.data(name="target_language_next_word", shape=[1], dtype="int64", lod_level=1)
+    avg = fluid.layers.mean(fluid.layers.cross_entropy(input=rnn(), label=label))
+    fluid.optimizer.Adagrad(learning_rate=0.1, regularization=fluid.regularizer.L2DecayRegularizer(
+        regularization_coeff=0.01)).minimize(avg)
+    return [avg]
+
+
+def mt_decode():
+    pd = fluid.layers
+    ctx = _mt_encoder()
+    array_len = pd.fill_constant(shape=[1], dtype="int64", value=MT_MAXLEN)
+    counter = pd.zeros(shape=[1], dtype="int64", force_cpu=True)
+    state_array = pd.create_array("float32")
+    pd.array_write(ctx, array=state_array, i=counter)
+    ids_array, scores_array = pd.create_array("int64"), pd.create_array("float32")
+    init_ids = pd.data(name="init_ids", shape=[1], dtype="int64", lod_level=2)
+    init_scores = pd.data(name="init_scores", shape=[1], dtype="float32", lod_level=2)
+    pd.array_write(init_ids, array=ids_array, i=counter)
+    pd.array_write(init_scores, array=scores_array, i=counter)
+    cond = pd.less_than(x=counter, y=array_len)
+    loop = pd.While(cond=cond)
+    with loop.block():
+        pre_ids = pd.array_read(array=ids_array, i=counter)
+        pre_state = pd.array_read(array=state_array, i=counter)
+        pre_score = pd.array_read(array=scores_array, i=counter)
+        pre_state_exp = pd.sequence_expand(pre_state, pre_score)
+        pre_ids_emb = pd.embedding(input=pre_ids, size=[MT_DICT, MT_WORD], param_attr=fluid.ParamAttr(name="vemb"))
+        cur = pd.fc(input=[pre_state_exp, pre_ids_emb], size=MT_HID, act="tanh")
+        cur_lod = pd.lod_reset(x=cur, y=pre_score)
+        score = pd.fc(input=cur_lod, size=MT_DICT, act="softmax")
+        topk_scores, topk_idx = pd.topk(score, k=MT_BEAM)
+        accu = pd.elementwise_add(x=pd.log(topk_scores), y=pd.reshape(pre_score, shape=[-1]), axis=0)
+        sel_ids, sel_scores = pd.beam_search(pre_ids, pre_score, topk_idx, accu, MT_BEAM, end_id=MT_END, level=0)
+        pd.increment(x=counter, value=1, in_place=True)
+        pd.array_write(cur, array=state_array, i=counter)
+        pd.array_write(sel_ids, array=ids_array, i=counter)
+        pd.array_write(sel_scores, array=scores_array, i=counter)
+        length_cond = pd.less_than(x=counter, y=array_len)
+        finish_cond = pd.logical_not(pd.is_empty(x=sel_ids))
+        pd.logical_and(x=length_cond, y=finish_cond, out=cond)
+    tids, tscores = pd.beam_search_decode(ids=ids_array, scores=scores_array, beam_size=MT_BEAM, end_id=MT_END)
+    return [tids, tscores]
+
+
+def _mt_words(rs, n, lo=1, hi=6):
+    lens = rs.randint(lo, hi, n).tolist()
+    off = np.concatenate([[0], np.cumsum(lens)]).tolist()
+    return core.LoDTensor(torch.from_numpy(rs.randint(0, MT_DICT, (off[-1], 1)).astype("int64")), [off]), off
+
+
+def mt_train_feeds(steps=4):
+    out = []
+    for seed in range(steps):
+        rs = np.random.RandomState(200 + seed)
+        src, _ = _mt_words(rs, 3)
+        trg, off = _mt_words(rs, 3)
+        nxt = core.LoDTensor(torch.from_numpy(rs.randint(0, MT_DICT, (off[-1], 1)).astype("int64")), [off])
+        out.append({"src_word_id": src, "target_language_word": trg, "target_language_next_word": nxt})
+    return out
+
+
+def mt_decode_feeds(steps=2):
+    out = []
+    for seed in range(steps):
+        rs = np.random.RandomState(300 + seed)
+        n = 2
+        src, _ = _mt_words(rs, n)
+        lod = [list(range(n + 1)), list(range(n + 1))]
+        init_ids = core.LoDTensor(torch.zeros(n, 1, dtype=torch.int64), lod)
+        init_scores = core.LoDTensor(torch.ones(n, 1, dtype=torch.float32), lod)
+        out.append({"src_word_id": src, "init_ids": init_ids, "init_scores": init_scores})
+    return out

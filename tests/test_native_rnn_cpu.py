@@ -35,3 +35,25 @@ def test_book_label_semantic_roles_native():
         np.testing.assert_allclose(b[0], a[0], rtol=1e-5, atol=1e-6)
         np.testing.assert_array_equal(b[1], a[1])
     assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+
+
+def test_book_machine_translation_train_and_beam_decode_native():
+    """Book machine_translation: the training program (LSTM encoder, DynamicRNN
+    decoder, Adagrad + L2) and the beam-search decoding program (While, topk,
+    beam_search over tensor arrays, beam_search_decode) on the C++ executor."""
+    from native_rnn_cases import mt_decode, mt_decode_feeds, mt_train, mt_train_feeds
+
+    place = fluid.CPUPlace()
+    fd = mt_train_feeds(4)
+    ref, init, _ = run(mt_train, fd, "python", place)
+    got, _, exe = run(mt_train, fd, "native", place, init)
+    for a, b in zip(ref, got):
+        np.testing.assert_allclose(b[0], a[0], rtol=1e-5, atol=1e-6)
+    assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+    fd = mt_decode_feeds(2)
+    ref, init, _ = run(mt_decode, fd, "python", place)
+    got, _, exe = run(mt_decode, fd, "native", place, init)
+    for a, b in zip(ref, got):
+        np.testing.assert_array_equal(b[0], a[0])
+        np.testing.assert_allclose(b[1], a[1], rtol=1e-5, atol=1e-6)
+    assert not exe._native.py_fallbacks, exe._native.py_fallbacks

@@ -42,3 +42,28 @@ def test_book_label_semantic_roles_native_gpu():
     eng = exe._native
     assert not eng.py_fallbacks, eng.py_fallbacks
     assert not eng.host_fallbacks(), eng.host_fallbacks()
+
+
+def test_book_machine_translation_native_gpu():
+    """Book machine_translation train + beam decode on a HIP place: the recurrent,
+    optimizer (adagrad) and decoding ops run natively (beam_search /
+    beam_search_decode are place-agnostic kernels over their few-KB inputs, as the
+    reference registers them CPU-only)."""
+    from native_rnn_cases import mt_decode, mt_decode_feeds, mt_train, mt_train_feeds
+
+    place = fluid.CUDAPlace(0)
+    fd = mt_train_feeds(4)
+    ref, init, _ = run(mt_train, fd, "python", place)
+    got, _, exe = run(mt_train, fd, "native", place, init)
+    for a, b in zip(ref, got):
+        np.testing.assert_allclose(b[0], a[0], rtol=2e-4, atol=2e-5)
+    assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+    assert not exe._native.host_fallbacks(), exe._native.host_fallbacks()
+    fd = mt_decode_feeds(2)
+    ref, init, _ = run(mt_decode, fd, "python", place)
+    got, _, exe = run(mt_decode, fd, "native", place, init)
+    for a, b in zip(ref, got):
+        np.testing.assert_array_equal(b[0], a[0])
+        np.testing.assert_allclose(b[1], a[1], rtol=2e-4, atol=2e-5)
+    assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+    assert not exe._native.host_fallbacks(), exe._native.host_fallbacks()
