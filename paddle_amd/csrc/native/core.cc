@@ -621,6 +621,7 @@ Executor::Executor(int device) {
   link_struct_kernels();
   link_beam_kernels();
   link_optim_kernels();
+  link_seq_kernels();
 }
 
 Executor::~Executor() {

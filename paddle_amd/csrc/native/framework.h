@@ -241,6 +241,7 @@ void link_rnn_kernels();
 void link_struct_kernels();
 void link_beam_kernels();
 void link_optim_kernels();
+void link_seq_kernels();
 
 // ---------------------------------------------------------------- executor
 class Executor {

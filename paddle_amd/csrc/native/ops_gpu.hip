@@ -1114,8 +1114,9 @@ T* upload_offsets(const OpRun& r, const char* name, const std::vector<size_t>& o
 void k_sequence_pool(const OpRun& r) {
   Tensor x = r.in("X");
   const int type = seq_pool_type(r.op.GetString("pooltype", "AVERAGE"));
-  if (x.dtype != DT::FP32 || x.lod.empty() || x.dims.empty() || type < 0) throw Decline();
-  const auto& off = x.lod.back();
+  if (x.dtype != DT::FP32 || x.dims.empty() || type < 0) throw Decline();
+  // no LoD: one sequence of all rows (the Python op library's _last_level)
+  const std::vector<size_t> off = x.lod.empty() ? std::vector<size_t>{0, (size_t)x.dims[0]} : x.lod.back();
   const int64_t n = (int64_t)off.size() - 1, Dm = x.dims[0] ? x.numel() / x.dims[0] : 0;
   Dims od = x.dims;
   od[0] = n;
@@ -1124,17 +1125,17 @@ void k_sequence_pool(const OpRun& r) {
   int* mi = mt ? static_cast<int*>(mt->alloc(DT::INT32, od, D(r))) : reinterpret_cast<int*>(workspace(r, "@sp_mi@", n * Dm));
   if (mt) HIPCHK(hipMemsetAsync(mi, 0, sizeof(int) * n * Dm, S(r)));
   if (n > 0 && Dm > 0) PA_KL(pa_seq_pool(0, f32(x), upload_offsets<int>(r, "@sp_off@", off), y, mi, (int)n, (int)Dm, type, 0.f, S(r)));
-  r.out("Out")->lod.assign(x.lod.begin(), x.lod.end() - 1);
+  if (!x.lod.empty()) r.out("Out")->lod.assign(x.lod.begin(), x.lod.end() - 1);
 }
 
 void k_sequence_pool_grad(const OpRun& r) {
   Tensor x = r.in("X");
   Tensor g = r.in("Out@GRAD");
   const int type = seq_pool_type(r.op.GetString("pooltype", "AVERAGE"));
-  if (x.dtype != DT::FP32 || g.dtype != DT::FP32 || x.lod.empty() || x.dims.empty() || type < 0) throw Decline();
+  if (x.dtype != DT::FP32 || g.dtype != DT::FP32 || x.dims.empty() || type < 0) throw Decline();
   Tensor* mt = r.in_opt("MaxIndex");
   if (type == 3 && (!mt || mt->dtype != DT::INT32 || mt->device != D(r))) throw Decline();
-  const auto& off = x.lod.back();
+  const std::vector<size_t> off = x.lod.empty() ? std::vector<size_t>{0, (size_t)x.dims[0]} : x.lod.back();
   const int64_t n = (int64_t)off.size() - 1, Dm = x.dims[0] ? x.numel() / x.dims[0] : 0;
   float* dx = out_f32(r, "X@GRAD", x.dims);
   r.out("X@GRAD")->lod = x.lod;

@@ -768,6 +768,8 @@ void k_reshape(const OpRun& r) {
   Dims nd = infer_shape(x.dims, shape);
   *o = x;  // shares the buffer
   o->dims = nd;
+  // the LoD travels only while the rows it indexes do (ShareLoD of an unchanged batch)
+  if (nd.empty() || x.dims.empty() || nd[0] != x.dims[0]) o->lod.clear();
   if (Tensor* xs = r.out("XShape")) {
     Dims d{0};
     d.insert(d.end(), x.dims.begin(), x.dims.end());
@@ -1523,14 +1525,17 @@ namespace {
 // ---------------------------------------------------------------- sequence (LoD) ops
 // sequence_pool_op.h / math/sequence_pooling.cc over the last LoD level; an empty
 // sequence pools to 0.  Out drops the last level; MaxIndex (int32) for MAX.
-const std::vector<size_t>& last_level(const Tensor& x, const char* op) {
-  PA_CHECK(!x.lod.empty(), "%s: the input has no LoD", op);
+// the finest LoD level; a tensor without LoD is ONE sequence of all its rows (the
+// Python op library's _last_level)
+std::vector<size_t> last_level(const Tensor& x, const char* op) {
+  (void)op;
+  if (x.lod.empty()) return {0, (size_t)(x.dims.empty() ? 0 : x.dims[0])};
   return x.lod.back();
 }
 
 void k_sequence_pool(const OpRun& r) {
   Tensor& x = r.in("X");
-  const auto& off = last_level(x, "sequence_pool");
+  const auto off = last_level(x, "sequence_pool");
   const std::string pt = r.op.GetString("pooltype", "AVERAGE");
   const int64_t n = (int64_t)off.size() - 1, D = x.dims[0] ? x.numel() / x.dims[0] : 0;
   Dims od = x.dims;
@@ -1574,7 +1579,7 @@ void k_sequence_pool(const OpRun& r) {
       }
     }
   });
-  o->lod.assign(x.lod.begin(), x.lod.end() - 1);
+  if (!x.lod.empty()) o->lod.assign(x.lod.begin(), x.lod.end() - 1);
 }
 
 // the MAX gradient goes to the first maximum, recomputed from X (the forward's
@@ -1582,7 +1587,7 @@ void k_sequence_pool(const OpRun& r) {
 void k_sequence_pool_grad(const OpRun& r) {
   Tensor& x = r.in("X");
   Tensor& g = r.in("Out@GRAD");
-  const auto& off = last_level(x, "sequence_pool_grad");
+  const auto off = last_level(x, "sequence_pool_grad");
   const std::string pt = r.op.GetString("pooltype", "AVERAGE");
   const int64_t n = (int64_t)off.size() - 1, D = x.dims[0] ? x.numel() / x.dims[0] : 0;
   Tensor* dxt = r.out("X@GRAD");

@@ -238,3 +238,53 @@ def mt_decode_feeds(steps=2):
         init_scores = core.LoDTensor(torch.ones(n, 1, dtype=torch.float32), lod)
         out.append({"src_word_id": src, "init_ids": init_ids, "init_scores": init_scores})
     return out
+
+
+# ---------------------------------------------------------------------------------
+# sequence row-map ops (ops_seq.cc): a text-CNN (sequence_conv + pool, the book
+# understand_sentiment conv net) plus pad / unpad / slice / erase / mask / enumerate
+# on the same LoD batch, trained end to end.
+def seq_ops_net():
+    def build():
+        words = fluid.layers.data(name="words", shape=[1], lod_level=1, dtype="int64")
+        label = fluid.layers.data(name="label", shape=[1], dtype="int64")
+        off = fluid.layers.data(name="off", shape=[1], dtype="int64", append_batch_size=False)
+        ln = fluid.layers.data(name="len", shape=[1], dtype="int64", append_batch_size=False)
+        kept = fluid.layers.sequence_erase(words, tokens=[3, 7])
+        emb = fluid.layers.embedding(input=kept, size=[V, E])
+        conv = fluid.nets.sequence_conv_pool(input=emb, num_filters=H, filter_size=3, act="tanh", pool_type="max")
+        pad_v = fluid.layers.fill_constant(shape=[1], dtype="float32", value=0.0)
+        padded, lens = fluid.layers.sequence_pad(emb, pad_v)
+        back = fluid.layers.sequence_unpad(padded * 2.0, lens)
+        sl = fluid.layers.sequence_slice(back, off, ln)
+        pooled = fluid.layers.sequence_pool(sl, "sum")
+        mask = fluid.layers.cast(fluid.layers.sequence_mask(lens, maxlen=6, dtype="float32"), "float32")
+        enum = fluid.layers.sequence_enumerate(kept, win_size=2)
+        enum.stop_gradient = True  # integer ids: no gradient path
+        enum_emb = fluid.layers.sequence_pool(fluid.layers.embedding(
+            input=fluid.layers.reshape(enum, [-1, 1]), size=[V, E]), "sum")
+        logit = fluid.layers.fc(input=conv, size=3, act="softmax")
+        # (compile-time shapes of the padded branch are not needed: reduce it to scalars)
+        loss = fluid.layers.mean(fluid.layers.cross_entropy(input=logit, label=label)) + \
+            fluid.layers.mean(pooled) * 0.05 + fluid.layers.mean(mask) * 0.01 + fluid.layers.mean(enum_emb) * 0.02
+        fluid.optimizer.SGD(learning_rate=0.3).minimize(loss)
+        return [loss]
+    return build
+
+
+def seq_ops_feeds(steps=4):
+    out = []
+    for seed in range(steps):
+        rs = np.random.RandomState(400 + seed)
+        lens = rs.randint(3, 8, 4).tolist()
+        off = np.concatenate([[0], np.cumsum(lens)]).tolist()
+        ids = rs.randint(0, V, (off[-1], 1)).astype("int64")
+        ids[ids == 3] = 4  # keep every sequence non-empty after the erase of 3 / 7
+        ids[ids == 7] = 8
+        ids[off[0], 0] = 3   # one erasable token per batch
+        fd = {"words": core.LoDTensor(torch.from_numpy(ids), [off]),
+              "label": core.LoDTensor(torch.from_numpy(rs.randint(0, 3, (len(lens), 1)).astype("int64"))),
+              "off": core.LoDTensor(torch.from_numpy(np.array([[1], [0], [1], [0]], dtype="int64"))),
+              "len": core.LoDTensor(torch.from_numpy(np.array([[1], [2], [1], [2]], dtype="int64")))}
+        out.append(fd)
+    return out

@@ -42,12 +42,12 @@ def test_native_engine_updates_python_scope_in_place():
 
 
 def test_native_engine_python_fallback_lod_and_control_flow():
-    """Ops without a C++ kernel (sequence_conv on a LoD feed) run through the
-    executor's per-op Python fallback; programs needing per-step scopes raise."""
+    """Ops without a C++ kernel (row_conv on a LoD feed) run through the executor's
+    per-op Python fallback with their LoD intact."""
     main, startup = fluid.Program(), fluid.Program()
     with fluid.program_guard(main, startup):
         x = fluid.layers.data("x", [4], lod_level=1)
-        y = fluid.layers.sequence_conv(fluid.layers.fc(x, 3), num_filters=2, filter_size=3)
+        y = fluid.layers.row_conv(fluid.layers.fc(x, 3), future_context_size=2)
     scope = fluid.core.Scope()
     place = fluid.CPUPlace()
     xv = fluid.create_lod_tensor(np.random.RandomState(0).rand(5, 4).astype("float32"), [[2, 3]], place)
@@ -57,7 +57,7 @@ def test_native_engine_python_fallback_lod_and_control_flow():
         exe = fluid.Executor(place, engine="native")
         (got,) = exe.run(main, feed={"x": xv}, fetch_list=[y])
     np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-7)
-    assert exe._native.py_fallbacks.get("sequence_conv") == 1
+    assert exe._native.py_fallbacks.get("row_conv") == 1
 
 
 def test_native_engine_rejects_step_scope_programs():

@@ -57,3 +57,15 @@ def test_book_machine_translation_train_and_beam_decode_native():
         np.testing.assert_array_equal(b[0], a[0])
         np.testing.assert_allclose(b[1], a[1], rtol=1e-5, atol=1e-6)
     assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+
+
+def test_sequence_row_map_ops_native():
+    from native_rnn_cases import seq_ops_feeds, seq_ops_net
+
+    fd = seq_ops_feeds(4)
+    place = fluid.CPUPlace()
+    ref, init, _ = run(seq_ops_net(), fd, "python", place)
+    got, _, exe = run(seq_ops_net(), fd, "native", place, init)
+    for a, b in zip(ref, got):
+        np.testing.assert_allclose(b[0], a[0], rtol=1e-5, atol=1e-6)
+    assert not exe._native.py_fallbacks, exe._native.py_fallbacks

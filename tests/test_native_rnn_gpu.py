@@ -67,3 +67,18 @@ def test_book_machine_translation_native_gpu():
         np.testing.assert_allclose(b[1], a[1], rtol=2e-4, atol=2e-5)
     assert not exe._native.py_fallbacks, exe._native.py_fallbacks
     assert not exe._native.host_fallbacks(), exe._native.host_fallbacks()
+
+
+def test_sequence_row_map_ops_native_gpu():
+    """sequence_conv / pad / unpad / slice / erase / mask / enumerate (ops_seq.cc:
+    row maps on the host, rows moved by the device gather / scatter kernels)."""
+    from native_rnn_cases import seq_ops_feeds, seq_ops_net
+
+    fd = seq_ops_feeds(4)
+    place = fluid.CUDAPlace(0)
+    ref, init, _ = run(seq_ops_net(), fd, "python", place)
+    got, _, exe = run(seq_ops_net(), fd, "native", place, init)
+    for a, b in zip(ref, got):
+        np.testing.assert_allclose(b[0], a[0], rtol=2e-4, atol=2e-5)
+    assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+    assert not exe._native.host_fallbacks(), exe._native.host_fallbacks()

@@ -46,8 +46,8 @@ def _model(name):
     return ErnieMoEForCausalLM(cfg, dev), cfg.vocab_size
 
 
-@pytest.mark.parametrize("name", ["llama", "gpt", "ernie"])
-def test_model_training_step_under_strict_native(name, strict_on):
+def _steps(name, strict_mode):
+    """Three training steps from seed 0; returns (losses, strict report)."""
     from paddle_amd.autograd import tape
     from paddle_amd.parallel.sharding import FlatShardedOptimizer
     from paddle_amd.utils import strict
@@ -57,11 +57,12 @@ def test_model_training_step_under_strict_native(name, strict_on):
     opt = FlatShardedOptimizer(m.named_parameters(), lr=1e-4, grad_dtype=torch.float32)
     # 2 x 1024 tokens: the fused GEMM-epilogue paths of the production shapes (the
     # W^T-cached K-major forms need >= 1024 tokens)
-    ids = torch.randint(0, V, (2, 1025), device="cuda")
+    g = torch.Generator().manual_seed(1)
+    ids = torch.randint(0, V, (2, 1025), generator=g).cuda()
     losses = []
     strict.reset()
     for _ in range(3):
-        with strict.region(f"{name}:step"):
+        with strict.region(f"{name}:step") if strict_mode else __import__("contextlib").nullcontext():
             with tape.recording() as t:
                 loss = m(ids[:, :-1], ids[:, 1:])
             t.backward(loss)
@@ -69,9 +70,20 @@ def test_model_training_step_under_strict_native(name, strict_on):
             opt.zero_grad()
         losses.append(float(loss))
     torch.cuda.synchronize()
-    rep = strict.report()
+    return losses, strict.report()
+
+
+@pytest.mark.parametrize("name", ["llama", "gpt", "ernie"])
+def test_model_training_step_under_strict_native(name, monkeypatch):
+    """The strict run refuses every ATen kernel AND trains along the same loss
+    trajectory as the unrestricted run of the same seeds (not just finite losses)."""
+    monkeypatch.delenv("FLAGS_strict_native", raising=False)
+    free, _ = _steps(name, False)
+    monkeypatch.setenv("FLAGS_strict_native", "1")
+    losses, rep = _steps(name, True)
     assert rep["aten_kernels"] == {} and rep["fallbacks"] == {}, rep
     assert all(np.isfinite(losses)), losses
+    np.testing.assert_allclose(losses, free, rtol=2e-3, atol=1e-4)
 
 
 def test_fluid_resnet_native_engine_under_strict_native(strict_on):
