@@ -622,6 +622,7 @@ Executor::Executor(int device) {
   link_beam_kernels();
   link_optim_kernels();
   link_seq_kernels();
+  link_io_kernels();
 }
 
 Executor::~Executor() {

@@ -242,6 +242,7 @@ void link_struct_kernels();
 void link_beam_kernels();
 void link_optim_kernels();
 void link_seq_kernels();
+void link_io_kernels();
 
 // ---------------------------------------------------------------- executor
 class Executor {
