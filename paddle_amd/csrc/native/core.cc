@@ -623,6 +623,7 @@ Executor::Executor(int device) {
   link_optim_kernels();
   link_seq_kernels();
   link_io_kernels();
+  link_tensor_kernels();
 }
 
 Executor::~Executor() {

@@ -243,6 +243,7 @@ void link_beam_kernels();
 void link_optim_kernels();
 void link_seq_kernels();
 void link_io_kernels();
+void link_tensor_kernels();
 
 // ---------------------------------------------------------------- executor
 class Executor {

@@ -288,3 +288,72 @@ def seq_ops_feeds(steps=4):
               "len": core.LoDTensor(torch.from_numpy(np.array([[1], [2], [1], [2]], dtype="int64")))}
         out.append(fd)
     return out
+
+
+# ---------------------------------------------------------------------------------
+# StaticRNN (layers.StaticRNN: a fixed-length RNN over the time-major first dim; the
+# reference's recurrent op, here unrolled at build time into the block) trained end
+# to end -- tests/unittests/test_recurrent_op.py's RecurrentOpTest1 cell.
+SR_T, SR_B, SR_D = 4, 3, 5
+
+
+def static_rnn():
+    def build():
+        x = fluid.layers.data(name="x", shape=[SR_T, SR_B, SR_D], dtype="float32", append_batch_size=False)
+        h0 = fluid.layers.data(name="h0", shape=[SR_B, SR_D], dtype="float32", append_batch_size=False)
+        x.stop_gradient = h0.stop_gradient = False
+        rnn = fluid.layers.StaticRNN()
+        with rnn.step():
+            h_pre = rnn.memory(init=h0)
+            xt = rnn.step_input(x)
+            h = fluid.layers.scale(fluid.layers.elementwise_add(
+                fluid.layers.fc(xt, SR_D, bias_attr=False), fluid.layers.fc(h_pre, SR_D, bias_attr=False)), 0.5)
+            h = fluid.layers.tanh(h)
+            rnn.update_memory(h_pre, h)
+            rnn.output(h)
+        out = rnn()
+        loss = fluid.layers.mean(fluid.layers.square(out))
+        fluid.optimizer.Momentum(learning_rate=0.2, momentum=0.9).minimize(loss)
+        return [loss]
+    return build
+
+
+def static_rnn_feeds(steps=4):
+    out = []
+    for seed in range(steps):
+        rs = np.random.RandomState(500 + seed)
+        out.append({"x": core.LoDTensor(torch.from_numpy(rs.randn(SR_T, SR_B, SR_D).astype("float32"))),
+                    "h0": core.LoDTensor(torch.from_numpy(rs.randn(SR_B, SR_D).astype("float32")))})
+    return out
+
+
+LY_B = 3
+
+
+def layout_net():
+    """slice (multi-axis, negative start) / transpose / unstack / stack / expand /
+    unsqueeze / squeeze / flatten between two fc layers: every layout op and its
+    gradient on the C++ executor."""
+    def build():
+        x = fluid.layers.data(name="x", shape=[LY_B, 6, 8], dtype="float32", append_batch_size=False)
+        h = fluid.layers.fc(x, 8, num_flatten_dims=2, bias_attr=False)
+        a = fluid.layers.slice(h, axes=[1, 2], starts=[1, -6], ends=[5, 100])       # [B, 4, 6]
+        t = fluid.layers.transpose(a, [0, 2, 1])                                    # [B, 6, 4]
+        parts = fluid.layers.unstack(t, axis=1)                                     # 6 x [B, 4]
+        s = fluid.layers.stack(parts[::2], axis=2)                                  # [B, 4, 3]
+        e = fluid.layers.expand(s, [1, 1, 2])                                       # [B, 4, 6]
+        q = fluid.layers.squeeze(fluid.layers.unsqueeze(e, [1]), [1])
+        f = fluid.layers.flatten(q, axis=1)                                         # [B, 24]
+        y = fluid.layers.fc(f, 5, bias_attr=False)
+        loss = fluid.layers.mean(fluid.layers.square(y))
+        fluid.optimizer.SGD(learning_rate=0.1).minimize(loss)
+        return [loss, e]
+    return build
+
+
+def layout_feeds(steps=4):
+    out = []
+    for seed in range(steps):
+        rs = np.random.RandomState(700 + seed)
+        out.append({"x": core.LoDTensor(torch.from_numpy(rs.randn(LY_B, 6, 8).astype("float32")))})
+    return out

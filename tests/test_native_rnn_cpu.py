@@ -69,3 +69,28 @@ def test_sequence_row_map_ops_native():
     for a, b in zip(ref, got):
         np.testing.assert_allclose(b[0], a[0], rtol=1e-5, atol=1e-6)
     assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+
+
+def test_static_rnn_native():
+    from native_rnn_cases import static_rnn, static_rnn_feeds
+
+    fd = static_rnn_feeds(4)
+    place = fluid.CPUPlace()
+    ref, init, _ = run(static_rnn(), fd, "python", place)
+    got, _, exe = run(static_rnn(), fd, "native", place, init)
+    for a, b in zip(ref, got):
+        np.testing.assert_allclose(b[0], a[0], rtol=1e-5, atol=1e-6)
+    assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+
+
+def test_layout_ops_native():
+    from native_rnn_cases import layout_feeds, layout_net
+
+    fd = layout_feeds(4)
+    place = fluid.CPUPlace()
+    ref, init, _ = run(layout_net(), fd, "python", place)
+    got, _, exe = run(layout_net(), fd, "native", place, init)
+    for a, b in zip(ref, got):
+        np.testing.assert_allclose(b[0], a[0], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(b[1], a[1], rtol=1e-5, atol=1e-6)
+    assert not exe._native.py_fallbacks, exe._native.py_fallbacks

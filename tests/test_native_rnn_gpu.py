@@ -82,3 +82,22 @@ def test_sequence_row_map_ops_native_gpu():
         np.testing.assert_allclose(b[0], a[0], rtol=2e-4, atol=2e-5)
     assert not exe._native.py_fallbacks, exe._native.py_fallbacks
     assert not exe._native.host_fallbacks(), exe._native.host_fallbacks()
+
+
+@pytest.mark.parametrize("case", ["static_rnn", "layout"])
+def test_layout_ops_native_gpu(case):
+    """The unrolled StaticRNN (slice / squeeze / stack per step) and the layout-op
+    chain on a HIP place: ops_tensor.hip's strided-box kernel moves every tensor."""
+    import native_rnn_cases as C
+
+    build, feeds_fn = {"static_rnn": (C.static_rnn, C.static_rnn_feeds),
+                       "layout": (C.layout_net, C.layout_feeds)}[case]
+    fd = feeds_fn(4)
+    place = fluid.CUDAPlace(0)
+    ref, init, _ = run(build(), fd, "python", place)
+    got, _, exe = run(build(), fd, "native", place, init)
+    for a, b in zip(ref, got):
+        for x, y in zip(a, b):
+            np.testing.assert_allclose(y, x, rtol=2e-4, atol=2e-5)
+    assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+    assert not exe._native.host_fallbacks(), exe._native.host_fallbacks()
