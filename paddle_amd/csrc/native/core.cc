@@ -624,6 +624,7 @@ Executor::Executor(int device) {
   link_seq_kernels();
   link_io_kernels();
   link_tensor_kernels();
+  link_rnn_unit_kernels();
 }
 
 Executor::~Executor() {

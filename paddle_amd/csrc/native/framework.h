@@ -244,6 +244,7 @@ void link_optim_kernels();
 void link_seq_kernels();
 void link_io_kernels();
 void link_tensor_kernels();
+void link_rnn_unit_kernels();
 
 // ---------------------------------------------------------------- executor
 class Executor {

@@ -70,7 +70,26 @@ def feeds(steps=4, h0=False, c0=False):
     return out
 
 
+def lstmp_net(peep=True, rev=False, proj_act="tanh"):
+    def build():
+        words = fluid.layers.data(name="words", shape=[1], lod_level=1, dtype="int64")
+        label = fluid.layers.data(name="label", shape=[1], dtype="int64")
+        emb = fluid.layers.embedding(input=words, size=[V, E])
+        proj = fluid.layers.fc(input=emb, size=4 * H)
+        r, c = fluid.layers.dynamic_lstmp(input=proj, size=4 * H, proj_size=4, use_peepholes=peep, is_reverse=rev,
+                                          proj_activation=proj_act)
+        last = fluid.layers.sequence_pool(r, "last")
+        cl = fluid.layers.sequence_pool(c, "average")
+        logit = fluid.layers.fc(input=[last, cl], size=3, act="softmax")
+        loss = fluid.layers.mean(fluid.layers.cross_entropy(input=logit, label=label))
+        fluid.optimizer.SGD(learning_rate=0.5).minimize(loss)
+        return [loss]
+    return build
+
+
 CASES = {
+    "lstmp_peep": (lstmp_net(), {}),
+    "lstmp_rev_nopeep_relu": (lstmp_net(peep=False, rev=True, proj_act="relu"), {}),
     "lstm_peep": (lstm_net(), {}),
     "lstm_rev_relu_srl": (lstm_net(rev=True, cand="relu", cell="sigmoid"), {}),
     "lstm_nopeep_h0": (lstm_net(peep=False, h0=True), {"h0": True, "c0": True}),
@@ -356,4 +375,36 @@ def layout_feeds(steps=4):
     for seed in range(steps):
         rs = np.random.RandomState(700 + seed)
         out.append({"x": core.LoDTensor(torch.from_numpy(rs.randn(LY_B, 6, 8).astype("float32")))})
+    return out
+
+
+UN_B, UN_D, UN_T = 4, 5, 3
+
+
+def units_net():
+    """gru_unit and lstm_unit unrolled over UN_T dense steps (the StaticRNN-free way
+    the reference's unit tests drive them), trained with SGD."""
+    def build():
+        x = fluid.layers.data(name="x", shape=[UN_T, UN_B, UN_D], dtype="float32", append_batch_size=False)
+        h = fluid.layers.data(name="h", shape=[UN_B, UN_D], dtype="float32", append_batch_size=False)
+        c = fluid.layers.data(name="c", shape=[UN_B, UN_D], dtype="float32", append_batch_size=False)
+        h.stop_gradient = c.stop_gradient = False
+        hg, hl, cl = h, h, c
+        for t in range(UN_T):
+            xt = fluid.layers.reshape(fluid.layers.slice(x, axes=[0], starts=[t], ends=[t + 1]), [UN_B, UN_D])
+            gin = fluid.layers.fc(xt, 3 * UN_D, bias_attr=False)
+            hg, _, _ = fluid.layers.gru_unit(gin, hg, 3 * UN_D)
+            hl, cl = fluid.layers.lstm_unit(xt, hl, cl, forget_bias=0.5)
+        loss = fluid.layers.mean(fluid.layers.square(fluid.layers.elementwise_add(hg, hl)))
+        fluid.optimizer.SGD(learning_rate=0.3).minimize(loss)
+        return [loss]
+    return build
+
+
+def units_feeds(steps=4):
+    out = []
+    for seed in range(steps):
+        rs = np.random.RandomState(900 + seed)
+        out.append({k: core.LoDTensor(torch.from_numpy(rs.randn(*s).astype("float32")))
+                    for k, s in (("x", (UN_T, UN_B, UN_D)), ("h", (UN_B, UN_D)), ("c", (UN_B, UN_D)))})
     return out

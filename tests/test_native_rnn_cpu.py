@@ -94,3 +94,16 @@ def test_layout_ops_native():
         np.testing.assert_allclose(b[0], a[0], rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(b[1], a[1], rtol=1e-5, atol=1e-6)
     assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+
+
+def test_rnn_unit_ops_native():
+    """gru_unit / lstm_unit (+ grads) on the one-source host kernels of ops_rnn_unit.hip."""
+    from native_rnn_cases import units_feeds, units_net
+
+    fd = units_feeds(4)
+    place = fluid.CPUPlace()
+    ref, init, _ = run(units_net(), fd, "python", place)
+    got, _, exe = run(units_net(), fd, "native", place, init)
+    for a, b in zip(ref, got):
+        np.testing.assert_allclose(b[0], a[0], rtol=1e-5, atol=1e-6)
+    assert not exe._native.py_fallbacks, exe._native.py_fallbacks

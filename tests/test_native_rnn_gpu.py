@@ -84,14 +84,15 @@ def test_sequence_row_map_ops_native_gpu():
     assert not exe._native.host_fallbacks(), exe._native.host_fallbacks()
 
 
-@pytest.mark.parametrize("case", ["static_rnn", "layout"])
+@pytest.mark.parametrize("case", ["static_rnn", "layout", "units"])
 def test_layout_ops_native_gpu(case):
     """The unrolled StaticRNN (slice / squeeze / stack per step) and the layout-op
     chain on a HIP place: ops_tensor.hip's strided-box kernel moves every tensor."""
     import native_rnn_cases as C
 
     build, feeds_fn = {"static_rnn": (C.static_rnn, C.static_rnn_feeds),
-                       "layout": (C.layout_net, C.layout_feeds)}[case]
+                       "layout": (C.layout_net, C.layout_feeds),
+                       "units": (C.units_net, C.units_feeds)}[case]
     fd = feeds_fn(4)
     place = fluid.CUDAPlace(0)
     ref, init, _ = run(build(), fd, "python", place)
