@@ -625,6 +625,7 @@ Executor::Executor(int device) {
   link_io_kernels();
   link_tensor_kernels();
   link_rnn_unit_kernels();
+  link_conv3d_kernels();
 }
 
 Executor::~Executor() {

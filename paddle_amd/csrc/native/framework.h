@@ -245,6 +245,7 @@ void link_seq_kernels();
 void link_io_kernels();
 void link_tensor_kernels();
 void link_rnn_unit_kernels();
+void link_conv3d_kernels();
 
 // ---------------------------------------------------------------- executor
 class Executor {

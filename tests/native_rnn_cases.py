@@ -408,3 +408,29 @@ def units_feeds(steps=4):
         out.append({k: core.LoDTensor(torch.from_numpy(rs.randn(*s).astype("float32")))
                     for k, s in (("x", (UN_T, UN_B, UN_D)), ("h", (UN_B, UN_D)), ("c", (UN_B, UN_D)))})
     return out
+
+
+def vol_net():
+    """conv3d (padding, stride, groups, bias) + max / avg (exclusive=False, ceil_mode)
+    pool3d, trained with Momentum: the NCDHW ops and their grads on the C++ executor."""
+    def build():
+        x = fluid.layers.data(name="x", shape=[2, 5, 6, 8], dtype="float32")
+        label = fluid.layers.data(name="label", shape=[1], dtype="int64")
+        c1 = fluid.layers.conv3d(x, 4, 3, stride=[1, 2, 1], padding=1, act="relu")
+        p1 = fluid.layers.pool3d(c1, 2, "max", pool_stride=2, ceil_mode=True)
+        c2 = fluid.layers.conv3d(p1, 4, [1, 2, 2], padding=[0, 1, 0], groups=2, dilation=[1, 1, 2])
+        p2 = fluid.layers.pool3d(c2, 2, "avg", pool_stride=1, pool_padding=1, exclusive=False)
+        logit = fluid.layers.fc(input=p2, size=3, act="softmax")
+        loss = fluid.layers.mean(fluid.layers.cross_entropy(input=logit, label=label))
+        fluid.optimizer.Momentum(learning_rate=0.05, momentum=0.9).minimize(loss)
+        return [loss]
+    return build
+
+
+def vol_feeds(steps=4):
+    out = []
+    for seed in range(steps):
+        rs = np.random.RandomState(1100 + seed)
+        out.append({"x": core.LoDTensor(torch.from_numpy(rs.randn(3, 2, 5, 6, 8).astype("float32"))),
+                    "label": core.LoDTensor(torch.from_numpy(rs.randint(0, 3, (3, 1)).astype("int64")))})
+    return out

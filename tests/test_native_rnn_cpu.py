@@ -107,3 +107,15 @@ def test_rnn_unit_ops_native():
     for a, b in zip(ref, got):
         np.testing.assert_allclose(b[0], a[0], rtol=1e-5, atol=1e-6)
     assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+
+
+def test_conv3d_pool3d_native():
+    from native_rnn_cases import vol_feeds, vol_net
+
+    fd = vol_feeds(4)
+    place = fluid.CPUPlace()
+    ref, init, _ = run(vol_net(), fd, "python", place)
+    got, _, exe = run(vol_net(), fd, "native", place, init)
+    for a, b in zip(ref, got):
+        np.testing.assert_allclose(b[0], a[0], rtol=1e-5, atol=1e-6)
+    assert not exe._native.py_fallbacks, exe._native.py_fallbacks
