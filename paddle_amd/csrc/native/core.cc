@@ -626,6 +626,7 @@ Executor::Executor(int device) {
   link_tensor_kernels();
   link_rnn_unit_kernels();
   link_conv3d_kernels();
+  link_loss_kernels();
 }
 
 Executor::~Executor() {

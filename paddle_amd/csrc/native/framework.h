@@ -246,6 +246,7 @@ void link_io_kernels();
 void link_tensor_kernels();
 void link_rnn_unit_kernels();
 void link_conv3d_kernels();
+void link_loss_kernels();
 
 // ---------------------------------------------------------------- executor
 class Executor {

@@ -881,6 +881,11 @@ def roi_pool(ctx):
     ROI start and clipped to the map; an empty bin gives 0 with Argmax -1."""
     x, rois = ctx.input("X"), ctx.input("ROIs")
     ph, pw, sc = ctx.attr("pooled_height"), ctx.attr("pooled_width"), ctx.attr("spatial_scale")
+    if ctx.meta:
+        shape = (rois.shape[0], x.shape[1], ph, pw)
+        ctx.set_output("Out", torch.empty(shape, dtype=x.dtype, device="meta"))
+        ctx.set_output("Argmax", torch.empty(shape, dtype=torch.int64, device="meta"))
+        return
     batch_ids = _roi_batch_ids(ctx, rois)
     import math
 

@@ -434,3 +434,63 @@ def vol_feeds(steps=4):
         out.append({"x": core.LoDTensor(torch.from_numpy(rs.randn(3, 2, 5, 6, 8).astype("float32"))),
                     "label": core.LoDTensor(torch.from_numpy(rs.randint(0, 3, (3, 1)).astype("int64")))})
     return out
+
+
+LS_C = 6
+
+
+def losses_net():
+    """warpctc (norm_by_times), nce (custom negatives), hsigmoid and roi_pool heads
+    summed into one loss, plus edit_distance between two id sequences; Momentum."""
+    def build():
+        feat = fluid.layers.data(name="feat", shape=[E], lod_level=1, dtype="float32")
+        lab = fluid.layers.data(name="lab", shape=[1], lod_level=1, dtype="int64")
+        logits = fluid.layers.fc(feat, LS_C)
+        ctc = fluid.layers.mean(fluid.layers.warpctc(logits, lab, blank=0, norm_by_times=True))
+        x = fluid.layers.data(name="x", shape=[E], dtype="float32")
+        y = fluid.layers.data(name="y", shape=[1], dtype="int64")
+        h = fluid.layers.fc(x, E, act="tanh")
+        nce = fluid.layers.mean(fluid.layers.nce(h, y, num_total_classes=9, num_neg_samples=3))
+        op = fluid.default_main_program().global_block().ops[-3]
+        assert op.type == "nce", op.type
+        op.set_attr("custom_neg_classes", [1, 4, 7])
+        hs = fluid.layers.mean(fluid.layers.hsigmoid(h, y, num_classes=9))
+        img = fluid.layers.data(name="img", shape=[2, 6, 7], dtype="float32")
+        rois = fluid.layers.data(name="rois", shape=[4], lod_level=1, dtype="float32")
+        fmap = fluid.layers.conv2d(img, 3, 3, padding=1)
+        pooled = fluid.layers.roi_pool(fmap, rois, pooled_height=2, pooled_width=3, spatial_scale=0.5)
+        rp = fluid.layers.mean(fluid.layers.square(fluid.layers.fc(pooled, 2)))
+        loss = fluid.layers.sums([ctc, nce, hs, rp])
+        fluid.optimizer.Momentum(learning_rate=0.05, momentum=0.9).minimize(loss)
+        hyp = fluid.layers.data(name="hyp", shape=[1], lod_level=1, dtype="int64")
+        dist, _ = fluid.layers.edit_distance(hyp, lab, normalized=True)
+        return [loss, dist]
+    return build
+
+
+def losses_feeds(steps=4):
+    out = []
+    for seed in range(steps):
+        rs = np.random.RandomState(1300 + seed)
+        tl = [5, 3, 7]
+        ll = [2, 1, 3]
+        to = np.concatenate([[0], np.cumsum(tl)]).tolist()
+        lo = np.concatenate([[0], np.cumsum(ll)]).tolist()
+        hl = [3, 2, 2]
+        ho = np.concatenate([[0], np.cumsum(hl)]).tolist()
+        R = [2, 1]
+        ro = np.concatenate([[0], np.cumsum(R)]).tolist()
+        boxes = []
+        for _ in range(sum(R)):
+            x1, y1 = rs.randint(0, 8), rs.randint(0, 6)
+            boxes.append([x1, y1, x1 + rs.randint(1, 6), y1 + rs.randint(1, 6)])
+        out.append({
+            "feat": core.LoDTensor(torch.from_numpy(rs.randn(to[-1], E).astype("float32")), [to]),
+            "lab": core.LoDTensor(torch.from_numpy(rs.randint(1, LS_C, (lo[-1], 1)).astype("int64")), [lo]),
+            "x": core.LoDTensor(torch.from_numpy(rs.randn(4, E).astype("float32"))),
+            "y": core.LoDTensor(torch.from_numpy(rs.randint(0, 9, (4, 1)).astype("int64"))),
+            "img": core.LoDTensor(torch.from_numpy(rs.randn(2, 2, 6, 7).astype("float32"))),
+            "rois": core.LoDTensor(torch.from_numpy(np.array(boxes, dtype="float32")), [ro]),
+            "hyp": core.LoDTensor(torch.from_numpy(rs.randint(1, LS_C, (ho[-1], 1)).astype("int64")), [ho]),
+        })
+    return out

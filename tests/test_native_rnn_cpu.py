@@ -119,3 +119,18 @@ def test_conv3d_pool3d_native():
     for a, b in zip(ref, got):
         np.testing.assert_allclose(b[0], a[0], rtol=1e-5, atol=1e-6)
     assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+
+
+def test_structured_losses_native():
+    """warpctc / nce / hierarchical_sigmoid / roi_pool (+grads) and edit_distance on
+    ops_loss.hip's host kernels."""
+    from native_rnn_cases import losses_feeds, losses_net
+
+    fd = losses_feeds(4)
+    place = fluid.CPUPlace()
+    ref, init, _ = run(losses_net(), fd, "python", place)
+    got, _, exe = run(losses_net(), fd, "native", place, init)
+    for a, b in zip(ref, got):
+        np.testing.assert_allclose(b[0], a[0], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(b[1], a[1], rtol=1e-6)
+    assert not exe._native.py_fallbacks, exe._native.py_fallbacks

@@ -84,7 +84,7 @@ def test_sequence_row_map_ops_native_gpu():
     assert not exe._native.host_fallbacks(), exe._native.host_fallbacks()
 
 
-@pytest.mark.parametrize("case", ["static_rnn", "layout", "units", "vol"])
+@pytest.mark.parametrize("case", ["static_rnn", "layout", "units", "vol", "losses"])
 def test_layout_ops_native_gpu(case):
     """The unrolled StaticRNN (slice / squeeze / stack per step) and the layout-op
     chain on a HIP place: ops_tensor.hip's strided-box kernel moves every tensor."""
@@ -93,7 +93,8 @@ def test_layout_ops_native_gpu(case):
     build, feeds_fn = {"static_rnn": (C.static_rnn, C.static_rnn_feeds),
                        "layout": (C.layout_net, C.layout_feeds),
                        "units": (C.units_net, C.units_feeds),
-                       "vol": (C.vol_net, C.vol_feeds)}[case]
+                       "vol": (C.vol_net, C.vol_feeds),
+                       "losses": (C.losses_net, C.losses_feeds)}[case]
     fd = feeds_fn(4)
     place = fluid.CUDAPlace(0)
     ref, init, _ = run(build(), fd, "python", place)
