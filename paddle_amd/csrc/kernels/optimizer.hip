@@ -7,6 +7,10 @@
 // step is one grid-stride launch; bf16 grads are read and the bf16 model copy is
 // written in the same pass as the fp32 master update (no separate cast kernel).
 // lr / beta-pow may come from device memory (static-graph ops) or by value.
+#include <stdlib.h>
+
+#include <algorithm>
+
 #include "common.h"
 
 namespace pa {
@@ -62,6 +66,103 @@ __global__ void adamw_kernel(float* __restrict__ p, const TG* __restrict__ g, fl
     float pp = p[e] * (1.f - lr_ * decay) - step * mm / (sqrtf(vv) * rc2 + eps_);
     p[e] = pp; m[e] = mm; v[e] = vv;
     if (pout) IO<TP>::st(pout, e, pp);
+  }
+}
+
+// Streaming AdamW, 8 elements per lane per trip: every operand of a trip (2 x 16 B
+// of p, m, v and g, or one 16 B bf16 g) is loaded before any arithmetic, so each lane
+// keeps 7-8 vector loads in flight; the state is touched exactly once per step, so
+// NT loads / stores would keep it from evicting the GEMM operands' L2 lines
+// (nontemporal == 1; measured slower, kept as an A/B arm).  fp32 master + fp32 m / v are 28 of the 30 B per element.
+template <typename T, int NT>
+__device__ __forceinline__ T ld_s(const T* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <typename T, int NT>
+__device__ __forceinline__ void st_s(T v, T* p) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+typedef unsigned short u16x8_t __attribute__((ext_vector_type(8)));
+
+template <typename TG, typename TP, int NT>
+__global__ __launch_bounds__(256) void adamw8_kernel(float* __restrict__ p, const TG* __restrict__ g,
+                                                     float* __restrict__ m, float* __restrict__ v,
+                                                     TP* __restrict__ pout, long n8, float lr,
+                                                     const float* __restrict__ lr_ptr, float b1, float b2,
+                                                     float eps, float wd, float bc1, float bc2,
+                                                     const float* __restrict__ b1pow,
+                                                     const float* __restrict__ b2pow, long decay_end,
+                                                     float gscale, const float* __restrict__ gscale_ptr,
+                                                     int lr_t_eps) {
+  const float lr_ = lr_ptr ? lr_ptr[0] : lr;
+  const float c1 = b1pow ? 1.f - b1pow[0] : bc1;
+  const float c2 = b2pow ? 1.f - b2pow[0] : bc2;
+  const float gs = gscale_ptr ? gscale_ptr[0] * gscale : gscale;
+  const float step = lr_ / c1;
+  const float rc2 = rsqrtf(c2);
+  const float eps_ = lr_t_eps ? eps * rc2 : eps;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const long e = i * 8;
+    f32x4 p0 = ld_s<f32x4, NT>(reinterpret_cast<const f32x4*>(p + e));
+    f32x4 p1 = ld_s<f32x4, NT>(reinterpret_cast<const f32x4*>(p + e + 4));
+    f32x4 m0 = ld_s<f32x4, NT>(reinterpret_cast<const f32x4*>(m + e));
+    f32x4 m1 = ld_s<f32x4, NT>(reinterpret_cast<const f32x4*>(m + e + 4));
+    f32x4 v0 = ld_s<f32x4, NT>(reinterpret_cast<const f32x4*>(v + e));
+    f32x4 v1 = ld_s<f32x4, NT>(reinterpret_cast<const f32x4*>(v + e + 4));
+    float gg[8];
+    if constexpr (sizeof(TG) == 4) {
+      const f32x4 g0 = ld_s<f32x4, NT>(reinterpret_cast<const f32x4*>(g + e));
+      const f32x4 g1 = ld_s<f32x4, NT>(reinterpret_cast<const f32x4*>(g + e + 4));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        gg[j] = g0[j] * gs;
+        gg[4 + j] = g1[j] * gs;
+      }
+    } else {
+      const u16x8_t gb = ld_s<u16x8_t, NT>(reinterpret_cast<const u16x8_t*>(g + e));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gg[j] = bf2f(gb[j]) * gs;
+    }
+    float pp[8], mm[8], vv[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pp[j] = p0[j]; pp[4 + j] = p1[j];
+      mm[j] = m0[j]; mm[4 + j] = m1[j];
+      vv[j] = v0[j]; vv[4 + j] = v1[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mm[j] = b1 * mm[j] + (1.f - b1) * gg[j];
+      vv[j] = b2 * vv[j] + (1.f - b2) * gg[j] * gg[j];
+      const float decay = (e + j) < decay_end ? wd : 0.f;
+      pp[j] = pp[j] * (1.f - lr_ * decay) - step * mm[j] / (sqrtf(vv[j]) * rc2 + eps_);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      p0[j] = pp[j]; p1[j] = pp[4 + j];
+      m0[j] = mm[j]; m1[j] = mm[4 + j];
+      v0[j] = vv[j]; v1[j] = vv[4 + j];
+    }
+    st_s<f32x4, NT>(p0, reinterpret_cast<f32x4*>(p + e));
+    st_s<f32x4, NT>(p1, reinterpret_cast<f32x4*>(p + e + 4));
+    st_s<f32x4, NT>(m0, reinterpret_cast<f32x4*>(m + e));
+    st_s<f32x4, NT>(m1, reinterpret_cast<f32x4*>(m + e + 4));
+    st_s<f32x4, NT>(v0, reinterpret_cast<f32x4*>(v + e));
+    st_s<f32x4, NT>(v1, reinterpret_cast<f32x4*>(v + e + 4));
+    if (pout) {
+      if constexpr (sizeof(TP) == 2) {
+        u16x8_t o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(pp[j]);
+        st_s<u16x8_t, NT>(o, reinterpret_cast<u16x8_t*>(pout + e));
+      } else {
+        st_s<f32x4, NT>(p0, reinterpret_cast<f32x4*>(pout + e));
+        st_s<f32x4, NT>(p1, reinterpret_cast<f32x4*>(pout + e + 4));
+      }
+    }
   }
 }
 
@@ -167,6 +268,40 @@ PA_EXPORT int pa_adamw(int gdtype, int pdtype, float* p, const void* g, float* m
                        const float* b2pow, long decay_end, float gscale, const float* gscale_ptr,
                        int lr_t_eps, hipStream_t st) {
   if (n == 0) return 0;
+  // PA_ADAMW_MODE: 0 the 4-wide kernel, 1 (default) the 8-wide kernel, 2 8-wide with
+  // non-temporal state traffic.  1e9 elements (benchmarks/adamw_bw.py, 30 B / element):
+  // 4.65 / 4.77 / 3.15 TB/s -- NT stores cost a third here.  The 8-wide kernel takes
+  // the 16 B-aligned body; the 4-wide kernel finishes the (< 8 element) tail.
+  static const int mode = [] {
+    const char* s = getenv("PA_ADAMW_MODE");
+    return s ? atoi(s) : 1;
+  }();
+  const bool aligned = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(m) |
+                         reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(g) |
+                         reinterpret_cast<uintptr_t>(pout)) & 15) == 0;
+  if (mode > 0 && aligned && n >= 8) {
+    const long n8 = n / 8;
+    const int grid8 = (int)std::min<long>((n8 + 255) / 256, 8192);
+#define PA_A8(TG, TP, NTV) \
+  hipLaunchKernelGGL((adamw8_kernel<TG, TP, NTV>), dim3(grid8), dim3(256), 0, st, p, (const TG*)g, m, v, (TP*)pout, n8, lr, lr_ptr, b1, b2, eps, wd, bc1, bc2, b1pow, b2pow, decay_end, gscale, gscale_ptr, lr_t_eps)
+#define PA_A8N(TG, TP) \
+  if (mode == 2) PA_A8(TG, TP, 1); else PA_A8(TG, TP, 0)
+    if (gdtype == 1) { if (pdtype == 1) { PA_A8N(u16, u16); } else { PA_A8N(u16, float); } }
+    else { if (pdtype == 1) { PA_A8N(float, u16); } else { PA_A8N(float, float); } }
+#undef PA_A8N
+#undef PA_A8
+    const long done = n8 * 8;
+    if (done == n) PA_LAUNCH_CHECK();
+    // tail on the 4-wide kernel (its own tail loop covers the last < 4 elements)
+    const int gs = gdtype == 1 ? 2 : 4, ps = pdtype == 1 ? 2 : 4;
+    p += done;
+    m += done;
+    v += done;
+    g = (const char*)g + done * gs;
+    if (pout) pout = (char*)pout + done * ps;
+    n -= done;
+    decay_end -= done;
+  }
   const int grid = stream_grid((n + 3) / 4, 256);
 #define PA_A(TG, TP) \
   hipLaunchKernelGGL((adamw_kernel<TG, TP>), dim3(grid), dim3(256), 0, st, p, (const TG*)g, m, v, (TP*)pout, n, lr, lr_ptr, b1, b2, eps, wd, bc1, bc2, b1pow, b2pow, decay_end, gscale, gscale_ptr, lr_t_eps)

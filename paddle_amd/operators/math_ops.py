@@ -173,6 +173,11 @@ def _make_ew(name, fn):
     @register_op(name, ["X", "Y"], ["Out"], {"axis": -1, "use_mkldnn": False})
     def k(ctx):
         x, y = ctx.input("X"), ctx.input("Y")
+        if x.device != y.device:  # data transform: a host scalar (force_cpu counter) joins the other place
+            if y.numel() <= x.numel():
+                y = y.to(x.device)
+            else:
+                x = x.to(y.device)
         yb = bcast_y(x, y, ctx.attr("axis")).to(x.dtype)
         out = _oplib.ew(_EW_NATIVE[name], x, yb) if (x.is_cuda and name in _EW_NATIVE) else None
         ctx.set_output("Out", out if out is not None else fn(x, yb))

@@ -1,0 +1,10 @@
+#!/bin/bash
+# native-executor GPU tests (new kernels) + the 1-GPU headline bench
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_native_rnn_gpu.py > gpurun_out/r6_native_rnn_gpu.log 2>&1; rc=$?
+tail -25 gpurun_out/r6_native_rnn_gpu.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r6_bench.log 2>&1 || { tail -30 gpurun_out/r6_bench.log; exit 1; }
+tail -3 gpurun_out/r6_bench.log
