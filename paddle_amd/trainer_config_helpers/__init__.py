@@ -47,9 +47,11 @@ CudnnMaxPooling, CudnnAvgPooling = _pool.Max, _pool.Avg
 
 # ------------------------------------------------------------------ attributes
 class ParameterAttribute:
-    def __init__(self, name=None, initial_std=None, initial_mean=None, learning_rate=None, l2_rate=None, **kw):
+    def __init__(self, name=None, initial_std=None, initial_mean=None, learning_rate=None, l2_rate=None,
+                 initial_max=None, initial_min=None, is_static=False, **kw):
         self.name, self.initial_std, self.initial_mean = name, initial_std, initial_mean
         self.learning_rate, self.l2_rate = learning_rate, l2_rate
+        self.initial_max, self.initial_min, self.is_static = initial_max, initial_min, is_static
 
 
 class ExtraLayerAttribute:
@@ -320,8 +322,10 @@ class TrainerConfig:
             tc["data_config"] = train
         if test:
             tc["test_data_config"] = test
-        if self._cfg.get("config_file"):
-            tc["config_files"] = [self._cfg["config_file"]]
+        # (config_files lists only Import()-ed sub-configs in the reference, never the
+        # main config file itself)
+        tc["save_dir"] = "./output/model"
+        tc["start_pass"] = 0
         return tc
 
     def proto(self) -> bytes:

@@ -39,36 +39,105 @@ _S = {
         ("sparse_update", 22, "bool", 0), ("is_shared", 23, "bool", 0),
         ("parameter_block_size", 24, "uint64", 0)],
     "SliceConfig": [("start", 1, "uint32", 0), ("end", 2, "uint32", 0)],
+    "ImageConfig": [("channels", 2, "uint32", 0), ("img_size", 8, "uint32", 0), ("img_size_y", 9, "uint32", 0),
+                    ("img_size_z", 10, "uint32", 0)],
+    "ConvConfig": [
+        ("filter_size", 1, "uint32", 0), ("channels", 2, "uint32", 0), ("stride", 3, "uint32", 0),
+        ("padding", 4, "uint32", 0), ("groups", 5, "uint32", 0), ("filter_channels", 6, "uint32", 0),
+        ("output_x", 7, "uint32", 0), ("img_size", 8, "uint32", 0), ("caffe_mode", 9, "bool", 0),
+        ("filter_size_y", 10, "uint32", 0), ("padding_y", 11, "uint32", 0), ("stride_y", 12, "uint32", 0),
+        ("output_y", 13, "uint32", 0), ("img_size_y", 14, "uint32", 0), ("dilation", 15, "uint32", 0),
+        ("dilation_y", 16, "uint32", 0), ("filter_size_z", 17, "uint32", 0), ("padding_z", 18, "uint32", 0),
+        ("stride_z", 19, "uint32", 0), ("output_z", 20, "uint32", 0), ("img_size_z", 21, "uint32", 0)],
+    "PoolConfig": [
+        ("pool_type", 1, "string", 0), ("channels", 2, "uint32", 0), ("size_x", 3, "uint32", 0),
+        ("start", 4, "uint32", 0), ("stride", 5, "uint32", 0), ("output_x", 6, "uint32", 0),
+        ("img_size", 7, "uint32", 0), ("padding", 8, "uint32", 0), ("size_y", 9, "uint32", 0),
+        ("stride_y", 10, "uint32", 0), ("output_y", 11, "uint32", 0), ("img_size_y", 12, "uint32", 0),
+        ("padding_y", 13, "uint32", 0), ("size_z", 14, "uint32", 0), ("stride_z", 15, "uint32", 0),
+        ("output_z", 16, "uint32", 0), ("img_size_z", 17, "uint32", 0), ("padding_z", 18, "uint32", 0),
+        ("exclude_mode", 19, "bool", 0)],
+    "SppConfig": [("image_conf", 1, "ImageConfig", 0), ("pool_type", 2, "string", 0),
+                  ("pyramid_height", 3, "uint32", 0)],
+    "NormConfig": [
+        ("norm_type", 1, "string", 0), ("channels", 2, "uint32", 0), ("size", 3, "uint32", 0),
+        ("scale", 4, "double", 0), ("pow", 5, "double", 0), ("output_x", 6, "uint32", 0),
+        ("img_size", 7, "uint32", 0), ("blocked", 8, "bool", 0), ("output_y", 9, "uint32", 0),
+        ("img_size_y", 10, "uint32", 0)],
+    "BlockExpandConfig": [
+        ("channels", 1, "uint32", 0), ("stride_x", 2, "uint32", 0), ("stride_y", 3, "uint32", 0),
+        ("padding_x", 4, "uint32", 0), ("padding_y", 5, "uint32", 0), ("block_x", 6, "uint32", 0),
+        ("block_y", 7, "uint32", 0), ("output_x", 8, "uint32", 0), ("output_y", 9, "uint32", 0),
+        ("img_size_x", 10, "uint32", 0), ("img_size_y", 11, "uint32", 0)],
+    "MaxOutConfig": [("image_conf", 1, "ImageConfig", 0), ("groups", 2, "uint32", 0)],
+    "RowConvConfig": [("context_length", 1, "uint32", 0)],
+    "BilinearInterpConfig": [("image_conf", 1, "ImageConfig", 0), ("out_size_x", 2, "uint32", 0),
+                             ("out_size_y", 3, "uint32", 0)],
+    "PriorBoxConfig": [("min_size", 1, "uint32", 1), ("max_size", 2, "uint32", 1), ("aspect_ratio", 3, "float", 1),
+                       ("variance", 4, "float", 1)],
+    "PadConfig": [("image_conf", 1, "ImageConfig", 0), ("pad_c", 2, "uint32", 1), ("pad_h", 3, "uint32", 1),
+                  ("pad_w", 4, "uint32", 1)],
+    "ReshapeConfig": [("height_axis", 1, "uint32", 1), ("width_axis", 2, "uint32", 1)],
+    "MultiBoxLossConfig": [
+        ("num_classes", 1, "uint32", 0), ("overlap_threshold", 2, "float", 0), ("neg_pos_ratio", 3, "float", 0),
+        ("neg_overlap", 4, "float", 0), ("background_id", 5, "uint32", 0), ("input_num", 6, "uint32", 0),
+        ("height", 7, "uint32", 0), ("width", 8, "uint32", 0)],
+    "DetectionOutputConfig": [
+        ("num_classes", 1, "uint32", 0), ("nms_threshold", 2, "float", 0), ("nms_top_k", 3, "uint32", 0),
+        ("background_id", 4, "uint32", 0), ("input_num", 5, "uint32", 0), ("keep_top_k", 6, "uint32", 0),
+        ("confidence_threshold", 7, "float", 0), ("height", 8, "uint32", 0), ("width", 9, "uint32", 0)],
+    "ClipConfig": [("min", 1, "double", 0), ("max", 2, "double", 0)],
+    "UpsampleConfig": [
+        ("image_conf", 1, "ImageConfig", 0), ("scale", 2, "uint32", 0), ("scale_y", 3, "uint32", 0),
+        ("pad_out_x", 4, "bool", 0), ("pad_out_y", 5, "bool", 0), ("upsample_size", 6, "uint32", 0),
+        ("upsample_size_y", 7, "uint32", 0)],
+    "ROIPoolConfig": [("pooled_width", 1, "uint32", 0), ("pooled_height", 2, "uint32", 0),
+                      ("spatial_scale", 3, "float", 0), ("height", 4, "uint32", 0), ("width", 5, "uint32", 0)],
+    "ScaleSubRegionConfig": [("image_conf", 1, "ImageConfig", 0), ("value", 2, "float", 0)],
     "ProjectionConfig": [
         ("type", 1, "string", 0), ("name", 2, "string", 0), ("input_size", 3, "uint64", 0),
         ("output_size", 4, "uint64", 0), ("context_start", 5, "int32", 0), ("context_length", 6, "int32", 0),
-        ("trainable_padding", 7, "bool", 0), ("num_filters", 9, "int32", 0), ("offset", 11, "uint64", 0),
-        ("slices", 13, "SliceConfig", 1)],
+        ("trainable_padding", 7, "bool", 0), ("conv_conf", 8, "ConvConfig", 0), ("num_filters", 9, "int32", 0),
+        ("offset", 11, "uint64", 0), ("pool_conf", 12, "PoolConfig", 0), ("slices", 13, "SliceConfig", 1)],
     "OperatorConfig": [
         ("type", 1, "string", 0), ("input_indices", 2, "int32", 1), ("input_sizes", 3, "uint64", 1),
-        ("output_size", 4, "uint64", 0), ("dotmul_scale", 5, "double", 0), ("num_filters", 7, "int32", 0)],
+        ("output_size", 4, "uint64", 0), ("dotmul_scale", 5, "double", 0), ("conv_conf", 6, "ConvConfig", 0),
+        ("num_filters", 7, "int32", 0)],
     "LayerInputConfig": [
         ("input_layer_name", 1, "string", 0), ("input_parameter_name", 2, "string", 0),
-        ("proj_conf", 6, "ProjectionConfig", 0), ("input_layer_argument", 9, "string", 0)],
+        ("conv_conf", 3, "ConvConfig", 0), ("pool_conf", 4, "PoolConfig", 0), ("norm_conf", 5, "NormConfig", 0),
+        ("proj_conf", 6, "ProjectionConfig", 0), ("block_expand_conf", 7, "BlockExpandConfig", 0),
+        ("image_conf", 8, "ImageConfig", 0), ("input_layer_argument", 9, "string", 0),
+        ("bilinear_interp_conf", 10, "BilinearInterpConfig", 0), ("maxout_conf", 11, "MaxOutConfig", 0),
+        ("spp_conf", 12, "SppConfig", 0), ("priorbox_conf", 13, "PriorBoxConfig", 0), ("pad_conf", 14, "PadConfig", 0),
+        ("row_conv_conf", 15, "RowConvConfig", 0), ("multibox_loss_conf", 16, "MultiBoxLossConfig", 0),
+        ("detection_output_conf", 17, "DetectionOutputConfig", 0), ("clip_conf", 18, "ClipConfig", 0),
+        ("scale_sub_region_conf", 19, "ScaleSubRegionConfig", 0), ("roi_pool_conf", 20, "ROIPoolConfig", 0),
+        ("upsample_conf", 21, "UpsampleConfig", 0)],
     "LayerConfig": [
         ("name", 1, "string", 0), ("type", 2, "string", 0), ("size", 3, "uint64", 0),
         ("active_type", 4, "string", 0), ("inputs", 5, "LayerInputConfig", 1),
         ("bias_parameter_name", 6, "string", 0), ("num_filters", 7, "uint32", 0),
-        ("shared_biases", 8, "bool", 0), ("drop_rate", 10, "double", 0), ("num_classes", 11, "uint32", 0),
-        ("device", 12, "int32", 0), ("reversed", 13, "bool", 0), ("active_gate_type", 14, "string", 0),
-        ("active_state_type", 15, "string", 0), ("num_neg_samples", 16, "int32", 0),
-        ("output_max_index", 19, "bool", 0), ("norm_by_times", 25, "bool", 0), ("coeff", 26, "double", 0),
+        ("shared_biases", 8, "bool", 0), ("partial_sum", 9, "uint32", 0), ("drop_rate", 10, "double", 0),
+        ("num_classes", 11, "uint32", 0), ("device", 12, "int32", 0), ("reversed", 13, "bool", 0),
+        ("active_gate_type", 14, "string", 0), ("active_state_type", 15, "string", 0),
+        ("num_neg_samples", 16, "int32", 0), ("neg_sampling_dist", 17, "double", 1),
+        ("output_max_index", 19, "bool", 0), ("softmax_selfnorm_alpha", 21, "double", 0),
+        ("directions", 24, "bool", 1), ("norm_by_times", 25, "bool", 0), ("coeff", 26, "double", 0),
         ("average_strategy", 27, "string", 0), ("error_clipping_threshold", 28, "double", 0),
-        ("operator_confs", 29, "OperatorConfig", 1), ("slope", 32, "double", 0), ("intercept", 33, "double", 0),
-        ("cos_scale", 34, "double", 0), ("beam_size", 39, "uint32", 0), ("select_first", 40, "bool", 0),
+        ("operator_confs", 29, "OperatorConfig", 1), ("NDCG_num", 30, "int32", 0), ("max_sort_size", 31, "int32", 0),
+        ("slope", 32, "double", 0), ("intercept", 33, "double", 0),
+        ("cos_scale", 34, "double", 0), ("data_norm_strategy", 36, "string", 0), ("bos_id", 37, "uint32", 0),
+        ("eos_id", 38, "uint32", 0), ("beam_size", 39, "uint32", 0), ("select_first", 40, "bool", 0),
         ("trans_type", 41, "string", 0), ("selective_fc_pass_generation", 42, "bool", 0),
         ("has_selected_colums", 43, "bool", 0), ("selective_fc_full_mul_ratio", 44, "double", 0),
+        ("selective_fc_parallel_plain_mul_thread_num", 45, "uint32", 0),
         ("use_global_stats", 46, "bool", 0), ("moving_average_fraction", 47, "double", 0),
         ("bias_size", 48, "uint32", 0), ("user_arg", 49, "string", 0), ("height", 50, "uint64", 0),
         ("width", 51, "uint64", 0), ("blank", 52, "uint32", 0), ("seq_pool_stride", 53, "int32", 0),
         ("axis", 54, "int32", 0), ("offset", 55, "uint32", 1), ("shape", 56, "uint32", 1),
-        ("delta", 57, "double", 0), ("depth", 58, "uint64", 0), ("epsilon", 60, "double", 0),
-        ("factor_size", 61, "uint32", 0)],
+        ("delta", 57, "double", 0), ("depth", 58, "uint64", 0), ("reshape_conf", 59, "ReshapeConfig", 0),
+        ("epsilon", 60, "double", 0), ("factor_size", 61, "uint32", 0)],
     "EvaluatorConfig": [
         ("name", 1, "string", 0), ("type", 2, "string", 0), ("input_layers", 3, "string", 1),
         ("chunk_scheme", 4, "string", 0), ("num_chunk_types", 5, "int32", 0),
@@ -89,12 +158,20 @@ _S = {
         ("input_layer_names", 4, "string", 1), ("output_layer_names", 5, "string", 1),
         ("evaluators", 6, "EvaluatorConfig", 1), ("sub_models", 8, "SubModelConfig", 1)],
     "OptimizationConfig": [
-        ("batch_size", 3, "int32", 0), ("algorithm", 4, "string", 0), ("learning_rate", 7, "double", 0),
-        ("learning_rate_decay_a", 8, "double", 0), ("learning_rate_decay_b", 9, "double", 0),
-        ("l1weight", 10, "double", 0), ("l2weight", 11, "double", 0), ("learning_method", 23, "string", 0),
-        ("ada_epsilon", 24, "double", 0), ("ada_rou", 26, "double", 0),
-        ("learning_rate_schedule", 27, "string", 0), ("adam_beta1", 33, "double", 0),
-        ("adam_beta2", 34, "double", 0), ("adam_epsilon", 35, "double", 0),
+        ("batch_size", 3, "int32", 0), ("algorithm", 4, "string", 0),
+        ("num_batches_per_send_parameter", 5, "int32", 0), ("num_batches_per_get_parameter", 6, "int32", 0),
+        ("learning_rate", 7, "double", 0), ("learning_rate_decay_a", 8, "double", 0),
+        ("learning_rate_decay_b", 9, "double", 0), ("l1weight", 10, "double", 0), ("l2weight", 11, "double", 0),
+        ("c1", 12, "double", 0), ("backoff", 13, "double", 0), ("owlqn_steps", 14, "int32", 0),
+        ("max_backoff", 15, "int32", 0), ("l2weight_zero_iter", 17, "int32", 0),
+        ("average_window", 18, "double", 0), ("max_average_window", 19, "int64", 0),
+        ("learning_method", 23, "string", 0), ("ada_epsilon", 24, "double", 0),
+        ("do_average_in_cpu", 25, "bool", 0), ("ada_rou", 26, "double", 0),
+        ("learning_rate_schedule", 27, "string", 0), ("delta_add_rate", 28, "double", 0),
+        ("mini_batch_size", 29, "int32", 0), ("use_sparse_remote_updater", 30, "bool", 0),
+        ("center_parameter_update_method", 31, "string", 0), ("shrink_parameter_value", 32, "double", 0),
+        ("adam_beta1", 33, "double", 0), ("adam_beta2", 34, "double", 0), ("adam_epsilon", 35, "double", 0),
+        ("learning_rate_args", 36, "string", 0), ("async_lagged_grad_discard_ratio", 37, "double", 0),
         ("gradient_clipping_threshold", 38, "double", 0)],
     "DataConfig": [
         ("type", 1, "string", 0), ("files", 3, "string", 0), ("async_load_data", 12, "bool", 0),
@@ -104,8 +181,8 @@ _S = {
     "TrainerConfig": [
         ("model_config", 1, "ModelConfig", 0), ("data_config", 2, "DataConfig", 0),
         ("opt_config", 3, "OptimizationConfig", 0), ("test_data_config", 4, "DataConfig", 0),
-        ("config_files", 5, "string", 1), ("save_dir", 6, "string", 0), ("start_pass", 8, "int32", 0),
-        ("config_file", 9, "string", 0)],
+        ("config_files", 5, "string", 1), ("save_dir", 6, "string", 0), ("init_model_path", 7, "string", 0),
+        ("start_pass", 8, "int32", 0), ("config_file", 9, "string", 0)],
 }
 _FIELDS = {m: {f[0]: f for f in fs} for m, fs in _S.items()}
 _BYNUM = {m: {f[1]: f for f in fs} for m, fs in _S.items()}
@@ -192,8 +269,10 @@ def decode(msg, buf: bytes) -> dict:
             v = raw.decode()
         elif kind == "double":
             v = struct.unpack("<d", raw)[0]
-        elif kind == "float":
-            v = struct.unpack("<f", raw)[0]
+        elif kind == "float":  # the shortest decimal that round-trips in float32 (as text format prints it)
+            import numpy as np
+
+            v = float(str(np.float32(struct.unpack("<f", raw)[0])))
         elif wt == 2:  # packed repeated varints
             vals, p = [], 0
             while p < len(raw):
@@ -245,8 +324,10 @@ def to_text(msg, d, indent=0) -> str:
 _TOK = re.compile(r'\s*(?:(\{)|(\})|("(?:[^"\\]|\\.)*")|([A-Za-z_][\w.\-]*)\s*:|([^\s{}]+))')
 
 
-def from_text(msg, text) -> dict:
-    """Parse protobuf text format (as the reference's *.protostr files) into a dict."""
+def from_text(msg, text, strict=False) -> dict:
+    """Parse protobuf text format (as the reference's *.protostr files) into a dict.
+    A field the schema does not know is skipped -- or, with ``strict``, kept as
+    ``"?<name>": True`` so a comparison against a recorded message reports it."""
     toks = []
     pos = 0
     while pos < len(text):
@@ -278,6 +359,8 @@ def from_text(msg, text) -> dict:
                     i += 1
                     if depth == 0:
                         break
+                if strict:
+                    d["?" + key] = True
                 continue
             if f is not None and f[2] in _S:
                 if toks[i][0]:  # "{"
@@ -288,6 +371,8 @@ def from_text(msg, text) -> dict:
                 i += 1
                 v = vs if vs is not None else vb
                 if f is None:
+                    if strict:
+                        d["?" + key] = True
                     continue
                 kind = f[2]
                 if kind == "string":
@@ -381,6 +466,7 @@ class Recorder:
         self.outputs = []
         self.depth = 0
         self.by_name = {}     # layer name -> its LayerConfig (image dims of inputs)
+        self.evaluators = []  # EvaluatorConfigs (classification_cost's default evaluator)
         self.parents = {}     # layer name -> parent layer names (networks.outputs DFS)
 
     def name_for(self, fn, given):
@@ -451,6 +537,35 @@ def _attr_name(attr, i):
     if attr is None or isinstance(attr, bool):
         return None
     return getattr(attr, "name", None)
+
+
+def _apply_pattr(prec, attr):
+    """ParameterAttribute semantics (reference attrs.py): initial_max / min -> uniform
+    (strategy 1, mean / std the interval's centre / half width); an explicit mean or
+    std -> normal with those; either way no smart init.  learning_rate, l2_rate
+    (decay_rate) and is_static carried over."""
+    if attr is None or isinstance(attr, bool):
+        return
+    mx, mn = getattr(attr, "initial_max", None), getattr(attr, "initial_min", None)
+    std, mean = getattr(attr, "initial_std", None), getattr(attr, "initial_mean", None)
+    if mx is not None or mn is not None:
+        mx, mn = float(mx if mx is not None else 0.0), float(mn if mn is not None else 0.0)
+        prec.update(initial_mean=(mx + mn) / 2, initial_std=(mx - mn) / 2, initial_strategy=1, initial_smart=False)
+    elif std is not None or mean is not None:
+        prec.update(initial_mean=float(mean or 0.0), initial_std=float(std if std is not None else 0.01),
+                    initial_strategy=0, initial_smart=False)
+    if getattr(attr, "learning_rate", None) is not None:
+        prec["learning_rate"] = float(attr.learning_rate)
+    if getattr(attr, "l2_rate", None) is not None:
+        prec["decay_rate"] = float(attr.l2_rate)
+    if getattr(attr, "is_static", False):
+        prec["is_static"] = True
+
+
+def _pattr(attr, i):
+    if isinstance(attr, (list, tuple)):
+        return attr[i] if i < len(attr) else None
+    return attr
 
 
 def _param_dims(p):
@@ -549,6 +664,7 @@ def _record(rec, fn_name, fn, args, kw, out, before, blk):
                     rec.params.append({"name": uname, "size": int(_prod(dims)), "initial_mean": 0.0,
                                        "initial_std": 1.0 / max(dims[0], 1) ** 0.5, "dims": dims,
                                        "initial_strategy": 0, "initial_smart": True})
+                    _apply_pattr(rec.params[-1], _pattr(kw.get("param_attr"), i))
             elif i < len(weights):
                 pname = f"_{name}.w{i}"
                 li["input_parameter_name"] = pname
@@ -557,6 +673,7 @@ def _record(rec, fn_name, fn, args, kw, out, before, blk):
                 rec.params.append({"name": pname, "size": int(_prod(dims)), "initial_mean": 0.0,
                                    "initial_std": 1.0 / max(dims[0], 1) ** 0.5, "dims": dims,
                                    "initial_strategy": 0, "initial_smart": True})
+                _apply_pattr(rec.params[-1], _pattr(kw.get("param_attr"), i))
             layer_inputs.append(li)
         if layer_inputs:
             lc["inputs"] = layer_inputs
@@ -568,6 +685,7 @@ def _record(rec, fn_name, fn, args, kw, out, before, blk):
                 n = int(_prod(_param_dims(by_pname[bname])))
                 rec.params.append({"name": bname, "size": n, "initial_mean": 0.0, "initial_std": 0.0,
                                    "dims": [1, n], "initial_strategy": 0, "initial_smart": False})
+                _apply_pattr(rec.params[-1], kw.get("bias_attr"))
         elif biases:
             pname = f"_{name}.wbias"
             lc["bias_parameter_name"] = pname
@@ -575,12 +693,19 @@ def _record(rec, fn_name, fn, args, kw, out, before, blk):
             n = int(_prod(_param_dims(biases[0])))
             rec.params.append({"name": pname, "size": n, "initial_mean": 0.0, "initial_std": 0.0, "dims": [1, n],
                                "initial_strategy": 0, "initial_smart": False})
+            _apply_pattr(rec.params[-1], kw.get("bias_attr"))
         if fn_name == "data_layer":
             rec.inputs.append(name)
         # LayerOutput.parents of the reference helpers: the layer inputs, except for
         # layers whose index / range inputs are not graph parents
         pnames = [rec.layer_name(x) for x, _ in ins if rec.layer_name(x)]
         rec.parents[name] = pnames[:1] if fn_name in _FIRST_PARENT_ONLY else pnames
+        la = kw.get("layer_attr")
+        if la is not None:
+            if getattr(la, "drop_rate", None):
+                lc["drop_rate"] = float(la.drop_rate)
+            if getattr(la, "error_clipping_threshold", None):
+                lc["error_clipping_threshold"] = float(la.error_clipping_threshold)
         extra = _EXTRA.get(fn_name)
         if extra is not None:
             extra(lc, args, kw, ins, rec, name)
@@ -616,6 +741,86 @@ def _hwd_from(lc, src):
     lc["height"] = int(src.get("height", 0))
     lc["width"] = int(src.get("width", 0))
     lc["depth"] = int(src.get("depth", 1))
+
+
+# ---- image geometry (reference config_parser.py get_img_size / cnn_output_size /
+# parse_conv / parse_pool / parse_norm / parse_image, re-derived from the layer
+# records: an input layer's size, height, width, depth and its output channels,
+# kept as the private "_num_filters" key -- LayerOutput.num_filters)
+def _xy(kw, key, default):
+    """A DSL size argument that may be an (x, y[, z]) sequence; key_y overrides y."""
+    v = kw.get(key, default)
+    if isinstance(v, (list, tuple)):
+        x, y = int(v[0]), int(v[1])
+    else:
+        x = y = int(v)
+    if kw.get(key + "_y") is not None:
+        y = int(kw[key + "_y"])
+    return x, y
+
+
+def _z(kw, key, default_x):
+    v = kw.get(key)
+    if isinstance(v, (list, tuple)) and len(v) > 2:
+        return int(v[2])
+    if kw.get(key + "_z") is not None:
+        return int(kw[key + "_z"])
+    return default_x
+
+
+def _out_size(img, k, pad, stride, caffe, dil=1):
+    import math
+
+    fs = (k - 1) * dil + 1
+    o = (2 * pad + img - fs) / float(stride)
+    return 1 + int(math.floor(o) if caffe else math.ceil(o))
+
+
+def _img_size(k, out, pad, stride, caffe, dil=1):
+    fs = (k - 1) * dil + 1
+    v = (out - 1) * stride + fs - 2 * pad
+    return v if caffe else v + 1
+
+
+def _channels(kw, rec, ins, key="num_channels"):
+    c = kw.get(key)
+    if c:
+        return int(c)
+    src = _in_lc(rec, ins)
+    if src.get("_num_filters"):
+        return int(src["_num_filters"])
+    hwd = int(src.get("height") or 0) * int(src.get("width") or 0) * int(src.get("depth") or 1)
+    if hwd and src.get("size"):
+        return int(src["size"]) // hwd
+    sh = list(getattr(ins[0][0], "shape", []) or []) if ins else []
+    return int(sh[1]) if len(sh) >= 4 else int(src.get("size") or _vsize(ins[0][0]) or 1)
+
+
+def _img_wh(rec, ins, c):
+    src = _in_lc(rec, ins)
+    size = int(src.get("size") or _vsize(ins[0][0]) or 0)
+    pix = size // max(c, 1)
+    w = int(src.get("width") or 0) or int(pix ** 0.5)
+    h = int(src.get("height") or 0) or (pix // w if w else 0)
+    return w, h
+
+
+def _img_whd(rec, ins):
+    src = _in_lc(rec, ins)
+    return int(src.get("width") or 0), int(src.get("height") or 0), int(src.get("depth") or 1)
+
+
+def _image_conf(rec, ins, c, three_d=False):
+    if three_d:
+        w, h, d = _img_whd(rec, ins)
+        return {"channels": c, "img_size": w, "img_size_y": h, "img_size_z": d}
+    w, h = _img_wh(rec, ins, c)
+    return {"channels": c, "img_size": w, "img_size_y": h}
+
+
+def _pool_type(pt, default="max"):
+    kind = type(pt).__name__ if pt is not None else default
+    return "avg-projection" if kind.startswith(("Avg", "CudnnAvg")) else "max-projection"
 
 
 def _x_data(lc, a, kw, ins, rec, name):
@@ -856,12 +1061,16 @@ def _x_pooling(lc, a, kw, ins, rec, name):
 
 def _x_batch_norm(lc, a, kw, ins, rec, name):
     """BatchNormLayer: the input three times (scale w0, moving mean w1, moving
-    variance w2, the last two static), a [1, C] bias, default act relu."""
+    variance w2, the last two static), a [1, C] bias, default act relu; image_conf of
+    the input (parse_image / parse_image3d), height / width (/ depth) only when the
+    input has an image size."""
     src = _in_lc(rec, ins)
-    c = int(kw.get("num_channels") or 0)
-    xs = list(getattr(ins[0][0], "shape", []) or [])
-    if not c and len(xs) >= 4:
-        c = int(xs[1])
+    three_d = bool(kw.get("img3D"))
+    c = int(kw.get("num_channels") or src.get("_num_filters") or 0)
+    if not c:
+        xs = list(getattr(ins[0][0], "shape", []) or [])
+        if len(xs) >= 4 and not src.get("height"):
+            c = int(xs[1])
     if not c:
         hw = int(src.get("height", 0) or 0) * int(src.get("width", 0) or 0) * int(src.get("depth", 1) or 1)
         c = (lc["size"] // hw) if hw else lc["size"]
@@ -869,10 +1078,17 @@ def _x_batch_norm(lc, a, kw, ins, rec, name):
     x = ins[0][0]
     lc["inputs"] = [{"input_layer_name": rec.layer_name(x) or x.name, "input_parameter_name": f"_{name}.w{i}"}
                     for i in range(3)]
+    lc["inputs"][0]["image_conf"] = _image_conf(rec, ins, c, three_d)
     lc["bias_parameter_name"] = f"_{name}.wbias"
     lc["moving_average_fraction"] = float(kw.get("moving_average_fraction", 0.9))
     lc["epsilon"] = float(kw.get("epsilon", 1e-5))
-    _hwd_from(lc, src)
+    if src.get("width") or src.get("height"):
+        ic = lc["inputs"][0]["image_conf"]
+        lc["height"], lc["width"], lc["depth"] = ic["img_size_y"], ic["img_size"], ic.get("img_size_z", 1)
+    else:
+        for k in ("height", "width", "depth"):
+            lc.pop(k, None)
+    lc["_num_filters"] = c
     _set_params(rec, name, lc, [(f"_{name}.w0", [c], 0.0, False), (f"_{name}.w1", [1, c], 0.0, False),
                                 (f"_{name}.w2", [1, c], 0.0, False), (f"_{name}.wbias", [1, c], 0.0, False)])
     for p in rec.params:
@@ -894,30 +1110,295 @@ def _x_nce(lc, a, kw, ins, rec, name):
     lc["bias_parameter_name"] = f"_{name}.wbias"
     lc["num_classes"] = nc
     lc["num_neg_samples"] = int(kw.get("num_neg_samples", 10))
-    _set_params(rec, name, lc, [(f"_{name}.w0", [nc, _vsize(x) or 0], 1.0 / max(_vsize(x) or 1, 1) ** 0.5, True),
+    _set_params(rec, name, lc, [(f"_{name}.w0", [nc, _vsize(x) or 0], 1.0 / max(nc, 1) ** 0.5, True),
                                 (f"_{name}.wbias", [1, nc], 0.0, False)])
 
 
 def _x_conv(lc, a, kw, ins, rec, name):
-    """ConvLayer (exconv): filter parameter without dims, [num_filters, 1] shared
-    biases."""
+    """ConvLayer (exconv / exconvt / conv3d / deconv3d): conv_conf of the input
+    (parse_conv / parse_conv3d), the output image as the layer's height / width
+    (/ depth), filter parameter without dims, [num_filters, 1] shared biases."""
+    three_d = lc["type"] == "conv3d"
+    trans = bool(kw.get("trans"))
+    nf = int(kw.get("num_filters") or 0)
+    g = int(kw.get("groups") or 1)
+    c = _channels(kw, rec, ins)
+    fs, fsy = _xy(kw, "filter_size", 1)
     for p in rec.params:
         if p["name"] == f"_{name}.w0":
             p["dims"] = []
-            p["initial_std"] = (2.0 / max(p["size"] // max(int(kw.get("num_filters") or 1), 1), 1)) ** 0.5
+            if p.get("initial_smart"):  # layers.py: smart init -> std sqrt(2 / (filter_size^2 C))
+                p["initial_std"] = (2.0 / (fs * fs * c)) ** 0.5
+                p["initial_smart"] = False
         elif p["name"] == f"_{name}.wbias":
             p["dims"] = [p["size"], 1]
-    lc["num_filters"] = int(kw.get("num_filters") or 0)
+    lc["num_filters"] = nf
     lc["shared_biases"] = True
-    if kw.get("trans"):
-        lc["type"] = "deconv3d" if lc["type"] == "conv3d" else "exconvt"
-        if lc["type"] == "deconv3d":  # the reference sizes the deconv3d filter with num_filters / groups
-            nf, g = int(kw.get("num_filters") or 1), int(kw.get("groups") or 1)
-            fs = kw.get("filter_size", 1)
-            k3 = _prod(fs) if isinstance(fs, (list, tuple)) else int(fs) ** 3
+    lc["_num_filters"] = nf
+    st, sty = _xy(kw, "stride", 1)
+    pd, pdy = _xy(kw, "padding", 0)
+    cc = {"filter_size": fs, "channels": c, "stride": st, "padding": pd, "groups": g,
+          "filter_channels": (nf if trans else c) // g, "caffe_mode": True, "filter_size_y": fsy,
+          "padding_y": pdy, "stride_y": sty}
+    if three_d:
+        fsz, stz, pdz = _z(kw, "filter_size", fs), _z(kw, "stride", st), _z(kw, "padding", pd)
+        w, h, d = _img_whd(rec, ins)
+        cc.update(filter_size_z=fsz, padding_z=pdz, stride_z=stz)
+        if trans:
+            cc.update(output_x=w, output_y=h, output_z=d, img_size=_img_size(fs, w, pd, st, True),
+                      img_size_y=_img_size(fsy, h, pdy, sty, True), img_size_z=_img_size(fsz, d, pdz, stz, True))
+            lc["height"], lc["width"], lc["depth"] = cc["img_size_y"], cc["img_size"], cc["img_size_z"]
+        else:
+            cc.update(img_size=w, img_size_y=h, img_size_z=d, output_x=_out_size(w, fs, pd, st, True),
+                      output_y=_out_size(h, fsy, pdy, sty, True), output_z=_out_size(d, fsz, pdz, stz, True))
+            lc["height"], lc["width"], lc["depth"] = cc["output_y"], cc["output_x"], cc["output_z"]
+    else:
+        dl, dly = _xy(kw, "dilation", 1)
+        cc.update(dilation=dl, dilation_y=dly)
+        w, h = _img_wh(rec, ins, c)
+        if trans:
+            cc.update(output_x=w, output_y=h, img_size=_img_size(fs, w, pd, st, True, dl),
+                      img_size_y=_img_size(fsy, h, pdy, sty, True, dly))
+            lc["height"], lc["width"] = cc["img_size_y"], cc["img_size"]
+        else:
+            cc.update(img_size=w, img_size_y=h, output_x=_out_size(w, fs, pd, st, True, dl),
+                      output_y=_out_size(h, fsy, pdy, sty, True, dly))
+            lc["height"], lc["width"] = cc["output_y"], cc["output_x"]
+    if lc.get("inputs"):
+        lc["inputs"][0]["conv_conf"] = cc
+    if trans:
+        lc["type"] = "deconv3d" if three_d else "exconvt"
+        if three_d:  # the reference sizes the deconv3d filter with num_filters / groups
+            fsz = cc["filter_size_z"]
             for p in rec.params:
                 if p["name"] == f"_{name}.w0":
-                    p["size"] = nf * (nf // g) * k3
+                    p["size"] = nf * (nf // g) * fs * fsy * fsz
+
+
+def _x_img_pool(lc, a, kw, ins, rec, name):
+    """PoolLayer / Pool3DLayer: pool_conf (parse_pool / parse_pool3d; ceil_mode ->
+    output sizes rounded up), the output image as height / width (/ depth)."""
+    three_d = lc["type"] == "pool3d"
+    c = _channels(kw, rec, ins)
+    kw = dict(kw)
+    kw.setdefault("pool_size", a[1] if len(a) > 1 else 1)
+    kx, ky = _xy(kw, "pool_size", 1)
+    st, sty = _xy(kw, "stride", 1)
+    pd, pdy = _xy(kw, "padding", 0)
+    caffe = not kw.get("ceil_mode", True)
+    pc = {"pool_type": _pool_type(kw.get("pool_type")), "channels": c, "size_x": kx, "stride": st,
+          "padding": pd, "size_y": ky, "stride_y": sty, "padding_y": pdy}
+    if three_d:
+        kz, stz, pdz = _z(kw, "pool_size", kx), _z(kw, "stride", st), _z(kw, "padding", pd)
+        w, h, d = _img_whd(rec, ins)
+        pc.update(size_z=kz, stride_z=stz, padding_z=pdz, img_size=w, img_size_y=h, img_size_z=d,
+                  output_x=_out_size(w, kx, pd, st, caffe), output_y=_out_size(h, ky, pdy, sty, caffe),
+                  output_z=_out_size(d, kz, pdz, stz, caffe))
+        lc["height"], lc["width"], lc["depth"] = pc["output_y"], pc["output_x"], pc["output_z"]
+    else:
+        w, h = _img_wh(rec, ins, c)
+        pc.update(img_size=w, img_size_y=h, output_x=_out_size(w, kx, pd, st, caffe),
+                  output_y=_out_size(h, ky, pdy, sty, caffe))
+        if kw.get("exclude_mode") is not None:
+            pc["exclude_mode"] = bool(kw["exclude_mode"])
+        lc["height"], lc["width"] = pc["output_y"], pc["output_x"]
+    lc["_num_filters"] = c
+    if lc.get("inputs"):
+        lc["inputs"][0]["pool_conf"] = pc
+
+
+def _x_cmrnorm(lc, a, kw, ins, rec, name):
+    """NormLayer (cmrnorm-projection): norm_conf with scale / size, the input image."""
+    c = _channels(kw, rec, ins)
+    size = int(kw.get("size", a[1] if len(a) > 1 else 5))
+    w, h = _img_wh(rec, ins, c)
+    nc = {"norm_type": "cmrnorm-projection", "channels": c, "size": size,
+          "scale": float(kw.get("scale", 0.0128)) / size, "pow": float(kw.get("power", 0.75)), "output_x": w,
+          "img_size": w, "blocked": False, "output_y": h, "img_size_y": h}
+    if lc.get("inputs"):
+        lc["inputs"][0]["norm_conf"] = nc
+    lc["height"], lc["width"] = h, w
+    lc["_num_filters"] = c
+
+
+def _chain(*fs):
+    def f(lc, a, kw, ins, rec, name):
+        for g in fs:
+            g(lc, a, kw, ins, rec, name)
+    return f
+
+
+def _conf0(key, make):
+    """Put make(...) as inputs[0][key] (a per-input sub-config of the layer)."""
+    def f(lc, a, kw, ins, rec, name):
+        if lc.get("inputs"):
+            lc["inputs"][0][key] = make(lc, a, kw, ins, rec, name)
+    return f
+
+
+def _x_clip(lc, a, kw, ins, rec, name):
+    lc["inputs"][0]["clip_conf"] = {"min": float(_arg(a, kw, "min", 1)), "max": float(_arg(a, kw, "max", 2))}
+
+
+def _x_row_conv(lc, a, kw, ins, rec, name):
+    lc["inputs"][0]["row_conv_conf"] = {"context_length": int(_arg(a, kw, "context_len", 1))}
+
+
+def _x_maxout(lc, a, kw, ins, rec, name):
+    c = _channels(kw, rec, ins)
+    g = int(_arg(a, kw, "groups", 1))
+    ic = _image_conf(rec, ins, c)
+    lc["inputs"][0]["maxout_conf"] = {"image_conf": ic, "groups": g}
+    lc["height"], lc["width"] = ic["img_size_y"], ic["img_size"]
+    lc["_num_filters"] = c // g
+
+
+def _x_pad(lc, a, kw, ins, rec, name):
+    c = _channels(kw, rec, ins)
+    pc, ph, pw = (list(kw.get(k) or [0, 0]) for k in ("pad_c", "pad_h", "pad_w"))
+    ic = _image_conf(rec, ins, c)
+    lc["inputs"][0]["pad_conf"] = {"image_conf": ic, "pad_c": pc, "pad_h": ph, "pad_w": pw}
+    lc["height"], lc["width"] = ic["img_size_y"] + sum(ph), ic["img_size"] + sum(pw)
+    lc["_num_filters"] = c + sum(pc)
+
+
+def _x_spp(lc, a, kw, ins, rec, name):
+    c = _channels(kw, rec, ins)
+    ph = int(kw.get("pyramid_height") or 1)
+    lc["inputs"][0]["spp_conf"] = {"image_conf": _image_conf(rec, ins, c),
+                                   "pool_type": _pool_type(kw.get("pool_type")), "pyramid_height": ph}
+    lc["height"], lc["width"] = 1, (4 ** ph - 1) // 3
+    lc["_num_filters"] = c
+
+
+def _x_roi_pool(lc, a, kw, ins, rec, name):
+    pw, ph = int(kw.get("pooled_width", 1)), int(kw.get("pooled_height", 1))
+    lc["inputs"][0]["roi_pool_conf"] = {"pooled_width": pw, "pooled_height": ph,
+                                        "spatial_scale": float(kw.get("spatial_scale", 1.0))}
+    lc["height"], lc["width"] = ph, pw
+    lc["_num_filters"] = _channels(kw, rec, ins)
+
+
+def _x_scale_sub_region(lc, a, kw, ins, rec, name):
+    c = _channels(kw, rec, ins)
+    ic = _image_conf(rec, ins, c)
+    lc["inputs"][0]["scale_sub_region_conf"] = {"image_conf": ic, "value": float(_arg(a, kw, "value", 2))}
+    lc["height"], lc["width"] = ic["img_size_y"], ic["img_size"]
+    lc["_num_filters"] = c
+
+
+def _x_bilinear(lc, a, kw, ins, rec, name):
+    c = _channels(kw, rec, ins)
+    ox, oy = int(kw.get("out_size_x") or 0), int(kw.get("out_size_y") or 0)
+    lc["inputs"][0]["bilinear_interp_conf"] = {"image_conf": _image_conf(rec, ins, c), "out_size_x": ox,
+                                               "out_size_y": oy}
+    lc["height"], lc["width"] = oy, ox
+    lc["_num_filters"] = c
+
+
+def _x_detection_output(lc, a, kw, ins, rec, name):
+    lc["inputs"][0]["detection_output_conf"] = {
+        "num_classes": int(kw.get("num_classes")), "nms_threshold": float(kw.get("nms_threshold", 0.45)),
+        "nms_top_k": int(kw.get("nms_top_k", 400)), "background_id": int(kw.get("background_id", 0)),
+        "input_num": len(kw["input_loc"]) if isinstance(kw.get("input_loc"), (list, tuple)) else 1,
+        "keep_top_k": int(kw.get("keep_top_k", 200)),
+        "confidence_threshold": float(kw.get("confidence_threshold", 0.01))}
+
+
+def _x_multibox_loss(lc, a, kw, ins, rec, name):
+    lc["inputs"][0]["multibox_loss_conf"] = {
+        "num_classes": int(kw.get("num_classes")), "overlap_threshold": float(kw.get("overlap_threshold", 0.5)),
+        "neg_pos_ratio": float(kw.get("neg_pos_ratio", 3.0)), "neg_overlap": float(kw.get("neg_overlap", 0.5)),
+        "background_id": int(kw.get("background_id", 0)),
+        "input_num": len(kw["input_loc"]) if isinstance(kw.get("input_loc"), (list, tuple)) else 1}
+
+
+def _x_prelu(lc, a, kw, ins, rec, name):
+    src = _in_lc(rec, ins)
+    size = int(src.get("size") or _vsize(ins[0][0]) or 0)
+    ps = int(kw.get("partial_sum", 1))
+    cs = kw.get("channel_shared")
+    if cs is not None:
+        c = _channels(kw, rec, ins)
+        hw = int(src.get("height") or 0) * int(src.get("width") or 0)
+        ps = hw * c if cs else hw
+    lc["partial_sum"] = ps
+    lc["height"], lc["width"], lc["depth"] = (int(src.get("height") or 0), int(src.get("width") or 0),
+                                              int(src.get("depth") or 1))
+    for p in rec.params:
+        if p["name"] == f"_{name}.w0":
+            p["size"], p["dims"] = size // ps, [1, size // ps]
+            if p.get("initial_smart"):  # layers.py prelu_layer: ParamAttr(initial_mean=0.25, initial_std=0.0)
+                p.update(initial_mean=0.25, initial_std=0.0, initial_smart=False)
+
+
+def _x_reversed(lc, a, kw, ins, rec, name):
+    lc["reversed"] = bool(kw.get("reverse", False))
+
+
+def _x_mixed(lc, a, kw, ins, rec, name):
+    """MixedLayer operators (operator_confs): each names the positions of its operand
+    inputs; operand inputs carry no parameter."""
+    ops, seen = [], {}
+    for i, (x, pr) in enumerate(ins):
+        if pr is None or not getattr(pr, "v1_operands", None):
+            continue
+        if id(pr) not in seen:
+            seen[id(pr)] = len(ops)
+            kind, scale = getattr(pr, "v1_operator", ("dot_mul", 1.0))
+            ops.append({"type": kind, "input_indices": [], "input_sizes": [], "output_size": lc.get("size"),
+                        "dotmul_scale": scale})
+        op = ops[seen[id(pr)]]
+        op["input_indices"].append(i)
+        op["input_sizes"].append(_vsize(x))
+        if i < len(lc.get("inputs", [])):
+            lc["inputs"][i].pop("input_parameter_name", None)
+    if ops:
+        lc["operator_confs"] = ops
+
+
+def _x_block_expand(lc, a, kw, ins, rec, name):
+    c = _channels(kw, rec, ins)
+    bx, by = int(kw.get("block_x", 0)), int(kw.get("block_y", 0))
+    sx, sy = int(kw.get("stride_x", 0)), int(kw.get("stride_y", 0))
+    px, py = int(kw.get("padding_x", 0)), int(kw.get("padding_y", 0))
+    ix, iy = int(kw.get("img_size_x", 0) or 0), int(kw.get("img_size_y", 0) or 0)
+    lc["inputs"][0]["block_expand_conf"] = {
+        "channels": c, "stride_x": sx, "stride_y": sy, "padding_x": px, "padding_y": py, "block_x": bx, "block_y": by,
+        "output_x": _out_size(ix, bx, px, sx, False) if ix else 0,
+        "output_y": _out_size(iy, by, py, sy, False) if iy else 0, "img_size_x": ix, "img_size_y": iy}
+    lc["size"] = bx * by * c
+
+
+def _x_cost_coeff(lc, a, kw, ins, rec, name):
+    lc["coeff"] = float(kw.get("coeff", 1.0))
+
+
+def _x_classification_cost(lc, a, kw, ins, rec, name):
+    """classification_cost: coeff, and its default classification_error_evaluator over
+    (prediction, label[, weight])."""
+    lc["coeff"] = float(kw.get("coeff", 1.0))
+    if kw.get("evaluator", True) is None or kw.get("evaluator") is False:
+        return
+    n = "classification_error_evaluator"
+    k = sum(1 for e in rec.evaluators if e["type"] == "classification_error")
+    rec.evaluators.append({"name": n if k == 0 else f"{n}_{k}", "type": "classification_error",
+                           "input_layers": [x["input_layer_name"] for x in lc.get("inputs", [])]})
+
+
+def _x_huber_reg(lc, a, kw, ins, rec, name):
+    lc["coeff"] = float(kw.get("coeff", 1.0))
+    lc["delta"] = float(kw.get("delta", 1.0))
+
+
+def _x_selfnorm(lc, a, kw, ins, rec, name):
+    lc["softmax_selfnorm_alpha"] = float(kw.get("softmax_selfnorm_alpha", 0.1))
+    lc["coeff"] = float(kw.get("coeff", 1.0))
+
+
+def _x_lambda(lc, a, kw, ins, rec, name):
+    lc["NDCG_num"] = int(kw.get("NDCG_num", 5))
+    lc["max_sort_size"] = int(kw.get("max_sort_size", -1))
 
 
 _EXTRA = {
@@ -925,11 +1406,22 @@ _EXTRA = {
     "pooling_layer": _x_pooling, "slope_intercept_layer": _x_slope, "scaling_layer": _x_weight_first,
     "interpolation_layer": _x_weight_first, "power_layer": _x_weight_first,
     "ctc_layer": _x_ctc, "warp_ctc_layer": _x_ctc, "cos_sim": _x_cos, "tensor_layer": _x_tensor,
-    "cross_entropy_with_selfnorm": _x_no_size, "cross_entropy_over_beam": _x_beam,
-    "detection_output_layer": _x_reorder(("priorbox", "input_loc", "input_conf"),
-                                         lambda kw: int(kw.get("keep_top_k", 200)) * 7),
-    "multibox_loss_layer": _x_reorder(("priorbox", "label", "input_loc", "input_conf")),
-    "img_conv3d_layer": _x_conv,
+    "cross_entropy_with_selfnorm": _chain(_x_no_size, _x_selfnorm), "cross_entropy_over_beam": _x_beam,
+    "detection_output_layer": _chain(_x_reorder(("priorbox", "input_loc", "input_conf"),
+                                                lambda kw: int(kw.get("keep_top_k", 200)) * 7),
+                                     _x_detection_output),
+    "multibox_loss_layer": _chain(_x_reorder(("priorbox", "label", "input_loc", "input_conf")), _x_multibox_loss),
+    "clip_layer": _x_clip, "row_conv_layer": _x_row_conv, "maxout_layer": _x_maxout, "pad_layer": _x_pad,
+    "spp_layer": _x_spp, "roi_pool_layer": _x_roi_pool, "scale_sub_region_layer": _x_scale_sub_region,
+    "bilinear_interp_layer": _x_bilinear, "prelu_layer": _x_prelu, "recurrent_layer": _x_reversed,
+    "crf_layer": _x_cost_coeff, "rank_cost": _x_cost_coeff, "cross_entropy": _x_cost_coeff,
+    "huber_regression_cost": _x_huber_reg, "huber_classification_cost": _x_cost_coeff,
+    "multi_binary_label_cross_entropy": _x_cost_coeff, "sum_cost": _x_cost_coeff,
+    "classification_cost": _x_classification_cost, "square_error_cost": _x_cost_coeff, "regression_cost": _x_cost_coeff,
+    "mse_cost": _x_cost_coeff, "lambda_cost": _x_lambda, "mixed_layer": _x_mixed,
+    "block_expand_layer": _x_block_expand,
+    "img_conv3d_layer": _x_conv, "img_pool_layer": _x_img_pool, "img_pool3d_layer": _x_img_pool,
+    "img_cmrnorm_layer": _x_cmrnorm,
     "factorization_machine": _x_factor, "smooth_l1_cost": _x_coeff, "kmax_seq_score_layer": _x_kmax,
     "sampling_id_layer": _x_same_size, "scale_shift_layer": _x_scale_shift, "seq_slice_layer": _x_seq_slice,
     "data_layer": _x_data, "addto_layer": _x_addto, "concat_layer": _x_concat,
@@ -972,11 +1464,22 @@ def model_config(rec, outputs, first_outputs=None):
     src = [rec.layer_name(o) or getattr(o, "name", str(o)) for o in (first_outputs or outputs)]
     ins = _dfs_inputs(rec, src) if src and all(o in rec.by_name for o in src) else rec.inputs
     mc = {"type": "nn", "layers": rec.layers, "parameters": rec.params, "input_layer_names": ins,
-          "output_layer_names": out_names,
+          "output_layer_names": out_names, "evaluators": rec.evaluators,
           "sub_models": [{"name": "root", "layer_names": names, "input_layer_names": ins,
-                          "output_layer_names": out_names, "is_recurrent_layer_group": False}]}
-    # proto2: an empty repeated field is an absent one
-    return {k: v for k, v in mc.items() if not (isinstance(v, list) and not v)}
+                          "output_layer_names": out_names, "evaluator_names": [e["name"] for e in rec.evaluators],
+                          "is_recurrent_layer_group": False}]}
+    return _proto2_clean(mc)
+
+
+def _proto2_clean(d):
+    """proto2: an empty repeated field is an absent one; "_"-prefixed keys are the
+    recorder's own bookkeeping, not message fields."""
+    if isinstance(d, dict):
+        return {k: _proto2_clean(v) for k, v in d.items()
+                if not k.startswith("_") and not (isinstance(v, list) and not v)}
+    if isinstance(d, list):
+        return [_proto2_clean(x) for x in d]
+    return d
 
 
 _METHOD = {"Momentum": "momentum", "Adam": "adam", "Adamax": "adamax", "AdaGrad": "adagrad",
@@ -984,14 +1487,31 @@ _METHOD = {"Momentum": "momentum", "Adam": "adam", "Adamax": "adamax", "AdaGrad"
 
 
 def opt_config(cfg):
+    """OptimizationConfig as the reference's settings() leaves it: every field it
+    assigns, at its default unless the config set it (optimizers.py settings /
+    config_parser.py default_optimization_config)."""
     m = cfg.get("learning_method")
     kind = getattr(getattr(m, "kind", None), "__name__", "Momentum")
+    ex = cfg.get("extra") or {}
     oc = {"batch_size": int(cfg.get("batch_size") or 1), "algorithm": "sgd",
-          "learning_rate": float(cfg.get("learning_rate") or 1e-3), "learning_method": _METHOD.get(kind, "momentum")}
+          "learning_rate": float(cfg.get("learning_rate") or 1e-3),
+          "learning_rate_decay_a": float(ex.get("learning_rate_decay_a", 0.0)),
+          "learning_rate_decay_b": float(ex.get("learning_rate_decay_b", 0.0)), "l1weight": 0.1, "l2weight": 0.0,
+          "c1": 0.0001, "backoff": 0.5, "owlqn_steps": 10, "max_backoff": 5, "l2weight_zero_iter": 0,
+          "average_window": 0.0, "learning_method": _METHOD.get(kind, "momentum"), "ada_epsilon": 1e-6,
+          "do_average_in_cpu": False, "ada_rou": 0.95,
+          "learning_rate_schedule": str(ex.get("learning_rate_schedule", "poly")), "delta_add_rate": 1.0,
+          "shrink_parameter_value": 0.0, "adam_beta1": 0.9, "adam_beta2": 0.999, "adam_epsilon": 1e-8,
+          "learning_rate_args": str(ex.get("learning_rate_args", "")), "async_lagged_grad_discard_ratio": 1.5}
     kw = getattr(m, "kw", {}) or {}
     if kind == "Adam":
         oc.update(adam_beta1=kw.get("beta1", 0.9), adam_beta2=kw.get("beta2", 0.999),
                   adam_epsilon=kw.get("epsilon", 1e-8))
+    elif kind in ("AdaGrad", "DecayedAdaGrad", "AdaDelta", "RMSProp"):
+        if kw.get("epsilon") is not None:
+            oc["ada_epsilon"] = float(kw["epsilon"])
+        if kw.get("rho") is not None:
+            oc["ada_rou"] = float(kw["rho"])
     reg = cfg.get("regularization")
     rate = getattr(reg, "rate", None) or getattr(reg, "regularization_coeff", None)
     if rate:

@@ -183,6 +183,7 @@ def dotmul_operator(a=None, b=None, scale=1, **kw):
     b = kw.get("y", b)
     op = _Projection(lambda s: _L().scale(_L().elementwise_mul(a, b), scale=float(scale)), _size(a))
     op.v1_operands = [a, b]  # an operator reads two layers (config_proto.py records both inputs)
+    op.v1_operator = ("dot_mul", float(scale))
     return op
 
 
@@ -728,10 +729,11 @@ def gated_unit_layer(input, size, act=None, name=None, gate_attr=None, gate_para
     if name is None:
         name = rec.name_for("gated_unit_layer", None) if rec is not None else "__gated_unit_layer__"
     proj = _fc(input=input, size=size, act=act or _act.Tanh(), name=f"{name}_input_proj",
-               param_attr=inproj_param_attr, bias_attr=inproj_bias_attr)
+               param_attr=inproj_param_attr, bias_attr=inproj_bias_attr, layer_attr=inproj_attr)
     gate = _fc(input=input, size=size, act=_act.Sigmoid(), name=f"{name}_gate",
-               param_attr=gate_param_attr, bias_attr=gate_bias_attr)
-    return _mixed(size=size, input=[dotmul_operator(a=proj, b=gate)], name=f"{name}_gated_act", bias_attr=False)
+               param_attr=gate_param_attr, bias_attr=gate_bias_attr, layer_attr=gate_attr)
+    return _mixed(size=size, input=[dotmul_operator(a=proj, b=gate)], name=f"{name}_gated_act", bias_attr=False,
+                  layer_attr=layer_attr)
 
 
 @_export

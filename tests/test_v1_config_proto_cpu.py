@@ -562,4 +562,4 @@ def test_dump_config_cli(tmp_path, capsys):
     assert mc["layers"][1]["size"] == 5 and mc["layers"][1]["active_type"] == "softmax"
     assert dump_config.main([str(cfg), "n=5", "--whole"]) == 0
     tc = cp.from_text("TrainerConfig", capsys.readouterr().out)
-    assert tc["opt_config"]["batch_size"] == 10 and tc["config_files"] == [str(cfg)]
+    assert tc["opt_config"]["batch_size"] == 10 and "config_files" not in tc  # (only Import()-ed files)
