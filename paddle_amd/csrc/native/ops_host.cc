@@ -1805,7 +1805,7 @@ PA_HOST_KERNEL(square, unary([](float v, const OpDesc&) { return v * v; }));
 PA_HOST_KERNEL(reciprocal, unary([](float v, const OpDesc&) { return 1.f / v; }));
 PA_HOST_KERNEL(ceil, unary([](float v, const OpDesc&) { return ceilf(v); }));
 PA_HOST_KERNEL(floor, unary([](float v, const OpDesc&) { return floorf(v); }));
-PA_HOST_KERNEL(round, unary([](float v, const OpDesc&) { return roundf(v); }));
+PA_HOST_KERNEL(round, unary([](float v, const OpDesc&) { return nearbyintf(v); }));  // half to even
 PA_HOST_KERNEL(softplus, unary([](float v, const OpDesc&) { return v > 20.f ? v : log1pf(expf(v)); }));
 PA_HOST_KERNEL(softsign, unary([](float v, const OpDesc&) { return v / (1.f + fabsf(v)); }));
 PA_HOST_KERNEL(gelu, unary([](float v, const OpDesc&) { return 0.5f * v * (1.f + erff(v * 0.70710678f)); }));
@@ -1824,6 +1824,102 @@ PA_HOST_KERNEL(swish, unary([](float v, const OpDesc& o) { return v * sigm(o.Get
 PA_HOST_KERNEL(pow, unary([](float v, const OpDesc& o) { return powf(v, o.GetFloat("factor", 1.f)); }));
 PA_HOST_KERNEL(scale, k_scale);
 PA_HOST_KERNEL(scale_grad, k_scale_grad);
+// the rest of the activation table of fluid_ops.hip (act_f / act_df), on the host
+PA_HOST_KERNEL(cos, unary([](float v, const OpDesc&) { return cosf(v); }));
+PA_HOST_KERNEL(sin, unary([](float v, const OpDesc&) { return sinf(v); }));
+PA_HOST_KERNEL(rsqrt, unary([](float v, const OpDesc&) { return 1.f / sqrtf(v); }));
+PA_HOST_KERNEL(silu, unary([](float v, const OpDesc&) { return v * sigm(v); }));
+PA_HOST_KERNEL(tanh_shrink, unary([](float v, const OpDesc&) { return v - tanhf(v); }));
+PA_HOST_KERNEL(hard_shrink, unary([](float v, const OpDesc& o) {
+                 const float t = o.GetFloat("threshold", 0.5f);
+                 return (v > t || v < -t) ? v : 0.f;
+               }));
+PA_HOST_KERNEL(softshrink, unary([](float v, const OpDesc& o) {
+                 const float l = o.GetFloat("lambda", 0.5f);
+                 return v > l ? v - l : (v < -l ? v + l : 0.f);
+               }));
+PA_HOST_KERNEL(soft_relu, unary([](float v, const OpDesc& o) {
+                 const float t = o.GetFloat("threshold", 40.f);
+                 return log1pf(expf(std::min(std::max(v, -t), t)));
+               }));
+PA_HOST_KERNEL(stanh, unary([](float v, const OpDesc& o) {
+                 return o.GetFloat("scale_b", 1.7159f) * tanhf(o.GetFloat("scale_a", 2.f / 3.f) * v);
+               }));
+PA_HOST_KERNEL(thresholded_relu, unary([](float v, const OpDesc& o) { return v > o.GetFloat("threshold", 1.f) ? v : 0.f; }));
+PA_HOST_KERNEL(abs_grad, unary_grad([](float x, float, float g, const OpDesc&) {
+                 return g * (x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f));
+               }));
+PA_HOST_KERNEL(ceil_grad, unary_grad([](float, float, float, const OpDesc&) { return 0.f; }));
+PA_HOST_KERNEL(floor_grad, unary_grad([](float, float, float, const OpDesc&) { return 0.f; }));
+PA_HOST_KERNEL(round_grad, unary_grad([](float, float, float, const OpDesc&) { return 0.f; }));
+PA_HOST_KERNEL(cos_grad, unary_grad([](float x, float, float g, const OpDesc&) { return -g * sinf(x); }));
+PA_HOST_KERNEL(sin_grad, unary_grad([](float x, float, float g, const OpDesc&) { return g * cosf(x); }));
+PA_HOST_KERNEL(sqrt_grad, unary_grad([](float, float y, float g, const OpDesc&) { return g * 0.5f / y; }));
+PA_HOST_KERNEL(rsqrt_grad, unary_grad([](float, float y, float g, const OpDesc&) { return -0.5f * g * y * y * y; }));
+PA_HOST_KERNEL(reciprocal_grad, unary_grad([](float, float y, float g, const OpDesc&) { return -g * y * y; }));
+PA_HOST_KERNEL(log_grad, unary_grad([](float x, float, float g, const OpDesc&) { return g / x; }));
+PA_HOST_KERNEL(logsigmoid_grad, unary_grad([](float x, float, float g, const OpDesc&) { return g * sigm(-x); }));
+PA_HOST_KERNEL(softplus_grad, unary_grad([](float x, float, float g, const OpDesc&) { return g * sigm(x); }));
+PA_HOST_KERNEL(softsign_grad, unary_grad([](float x, float, float g, const OpDesc&) {
+                 const float d = 1.f + fabsf(x);
+                 return g / (d * d);
+               }));
+PA_HOST_KERNEL(silu_grad, unary_grad([](float x, float, float g, const OpDesc&) {
+                 const float s = sigm(x);
+                 return g * s * (1.f + x * (1.f - s));
+               }));
+PA_HOST_KERNEL(gelu_grad, unary_grad([](float x, float, float g, const OpDesc&) {
+                 return g * (0.5f * (1.f + erff(x * 0.70710678118654752f)) +
+                             x * 0.3989422804014327f * expf(-0.5f * x * x));
+               }));
+PA_HOST_KERNEL(tanh_shrink_grad, unary_grad([](float x, float, float g, const OpDesc&) {
+                 const float t = tanhf(x);
+                 return g * t * t;
+               }));
+PA_HOST_KERNEL(hard_shrink_grad, unary_grad([](float x, float, float g, const OpDesc& o) {
+                 const float t = o.GetFloat("threshold", 0.5f);
+                 return (x > t || x < -t) ? g : 0.f;
+               }));
+PA_HOST_KERNEL(softshrink_grad, unary_grad([](float x, float, float g, const OpDesc& o) {
+                 const float l = o.GetFloat("lambda", 0.5f);
+                 return (x > l || x < -l) ? g : 0.f;
+               }));
+PA_HOST_KERNEL(brelu_grad, unary_grad([](float x, float, float g, const OpDesc& o) {
+                 return (x > o.GetFloat("t_min", 0.f) && x < o.GetFloat("t_max", 24.f)) ? g : 0.f;
+               }));
+PA_HOST_KERNEL(leaky_relu_grad, unary_grad([](float x, float, float g, const OpDesc& o) {
+                 return x > 0.f ? g : g * o.GetFloat("alpha", 0.02f);
+               }));
+PA_HOST_KERNEL(soft_relu_grad, unary_grad([](float x, float y, float g, const OpDesc& o) {
+                 const float t = o.GetFloat("threshold", 40.f);
+                 return (x > -t && x < t) ? g * (1.f - expf(-y)) : 0.f;
+               }));
+PA_HOST_KERNEL(elu_grad, unary_grad([](float x, float y, float g, const OpDesc& o) {
+                 return x > 0.f ? g : g * (y + o.GetFloat("alpha", 1.f));
+               }));
+PA_HOST_KERNEL(relu6_grad, unary_grad([](float x, float, float g, const OpDesc& o) {
+                 return (x > 0.f && x < o.GetFloat("threshold", 6.f)) ? g : 0.f;
+               }));
+PA_HOST_KERNEL(pow_grad, unary_grad([](float x, float, float g, const OpDesc& o) {
+                 const float f = o.GetFloat("factor", 1.f);
+                 return g * f * powf(x, f - 1.f);
+               }));
+PA_HOST_KERNEL(stanh_grad, unary_grad([](float x, float, float g, const OpDesc& o) {
+                 const float a = o.GetFloat("scale_a", 2.f / 3.f), b = o.GetFloat("scale_b", 1.7159f);
+                 const float t = tanhf(a * x);
+                 return g * a * b * (1.f - t * t);
+               }));
+PA_HOST_KERNEL(thresholded_relu_grad, unary_grad([](float x, float, float g, const OpDesc& o) {
+                 return x > o.GetFloat("threshold", 1.f) ? g : 0.f;
+               }));
+PA_HOST_KERNEL(hard_sigmoid_grad, unary_grad([](float x, float, float g, const OpDesc& o) {
+                 const float t = o.GetFloat("slope", 0.2f) * x + o.GetFloat("offset", 0.5f);
+                 return (t > 0.f && t < 1.f) ? g * o.GetFloat("slope", 0.2f) : 0.f;
+               }));
+PA_HOST_KERNEL(swish_grad, unary_grad([](float x, float, float g, const OpDesc& o) {
+                 const float b = o.GetFloat("beta", 1.f), s = sigm(b * x);
+                 return g * (s + b * x * s * (1.f - s));
+               }));
 PA_HOST_KERNEL(relu_grad, unary_grad([](float, float y, float g, const OpDesc&) { return y > 0 ? g : 0.f; }));
 PA_HOST_KERNEL(sigmoid_grad, unary_grad([](float, float y, float g, const OpDesc&) { return g * y * (1.f - y); }));
 PA_HOST_KERNEL(tanh_grad, unary_grad([](float, float y, float g, const OpDesc&) { return g * (1.f - y * y); }));
