@@ -627,6 +627,7 @@ Executor::Executor(int device) {
   link_rnn_unit_kernels();
   link_conv3d_kernels();
   link_loss_kernels();
+  link_misc_kernels();
 }
 
 Executor::~Executor() {

@@ -247,6 +247,7 @@ void link_tensor_kernels();
 void link_rnn_unit_kernels();
 void link_conv3d_kernels();
 void link_loss_kernels();
+void link_misc_kernels();
 
 // ---------------------------------------------------------------- executor
 class Executor {
