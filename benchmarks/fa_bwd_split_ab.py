@@ -27,8 +27,10 @@ do = torch.randn(B, S, H * D, device=dev, dtype=torch.bfloat16)
 flop_bwd = 10 * B * H * S * S * D / 2  # 5 GEMMs, causal half
 
 
-def run(split):
+def run(split, variant=1):
     F._FA_SPLIT = split
+    from paddle_amd.ops import _native as N
+    N.lib().pa_fa_bwd_split_set_variant(variant)
     return F._rope_attn_backward(packed, o, lse, cos, sin, do, H, Hk, D, True, scale)
 
 
@@ -47,11 +49,11 @@ def timeit(fn, reps=10):
 res = {}
 outs = {}
 for rnd in range(3):
-    for arm in ("split", "fused_v4"):
-        t = timeit(lambda: run(arm == "split"))
+    for arm in ("split", "split_nopipe", "fused_v4"):
+        t = timeit(lambda: run(arm != "fused_v4", 0 if arm == "split_nopipe" else 1))
         res.setdefault(arm, []).append(t)
         if rnd == 0:
-            outs[arm] = run(arm == "split").float()
+            outs[arm] = run(arm != "fused_v4", 0 if arm == "split_nopipe" else 1).float()
 F._FA_SPLIT = True
 for arm, ts in res.items():
     print(json.dumps({"arm": arm, "shape": [B, H, Hk, S, D], "ms": [round(x, 4) for x in ts],
@@ -60,5 +62,7 @@ a, b = outs["split"].view(B, S, nh, D), outs["fused_v4"].view(B, S, nh, D)
 rel = {n: float((a[:, :, sl] - b[:, :, sl]).norm() / b[:, :, sl].norm())
        for n, sl in (("dq", slice(0, H)), ("dk", slice(H, H + Hk)), ("dv", slice(H + Hk, nh)))}
 print(json.dumps({"rel_diff_split_vs_fused": rel}))
+c = outs["split_nopipe"].view(B, S, nh, D)
+print(json.dumps({"maxabs_pipe_vs_nopipe": float((a - c).abs().max())}))
 ft = timeit(lambda: F._fa_fwd(p4[:, :, :H], p4[:, :, H:H + Hk], p4[:, :, H + Hk:], True, scale))
 print(json.dumps({"fwd_ms": round(ft, 4), "fwd_TF": round(4 * B * H * S * S * D / 2 / ft / 1e9, 1)}))

@@ -39,6 +39,8 @@
 // LDS reads of the compute phase are inline asm so hipcc does not put a vmcnt(0) in
 // front of them for the in-flight DMA (the same reason as gemm.hip's Frag<false>);
 // their results are fenced by lgkmcnt waits that name the registers.
+#include <type_traits>
+
 #include "common.h"
 
 namespace pa {
@@ -50,6 +52,7 @@ typedef __attribute__((address_space(3))) void* lds_vp;
 
 constexpr int D = 128;
 constexpr int KCH = D / 8;  // 16-B chunks per row
+static int g_variant = 1;   // pa_fa_bwd_split_set_variant
 
 struct Params {
   const u16 *q, *k, *v, *o, *dout;
@@ -329,7 +332,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(Params p) {
 // other stage after them, one barrier per slice.  Every LDS address is a lane
 // constant plus an immediate (the step loop is unrolled over the two stages), so the
 // slice body issues no address arithmetic.
-template <bool CAUSAL, bool ROPE>
+template <bool CAUSAL, bool ROPE, bool PIPE>
 __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(Params p) {
   constexpr int BK = 128, BQ = 64, KS = D / 16, DB = D / 32;
   constexpr int KIMG = BK * D * 2;    // 32 KiB
@@ -352,6 +355,18 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(Params p) {
     u16x8 t = {0, 0, 0, 0, 0, 0, 0, 0};
     if (mykey < p.Sk) t = *reinterpret_cast<const u16x8*>(vp + (long)mykey * p.v_ss + ks * 16 + hh * 8);
     vf[ks] = as_bf8(t);
+  }
+  // K rows of this lane's key (B operand of S = Q K^T), register-resident in the PIPE
+  // body: K[mykey][16 ks + 8 hh + j]
+  bf8v kf[KS];
+  if constexpr (PIPE) {
+    const u16* kp_ = p.k + (long)b * p.k_bs + (long)kvh * p.k_hs;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      u16x8 t = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (mykey < p.Sk) t = *reinterpret_cast<const u16x8*>(kp_ + (long)mykey * p.k_ss + ks * 16 + hh * 8);
+      kf[ks] = as_bf8(t);
+    }
   }
   // K rows n0 .. n0 + 127 -> the row image (each wave reads back only its 32 rows)
   for (int idx = tid; idx < BK * KCH; idx += 256) {
@@ -508,6 +523,130 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(Params p) {
     }
   };
 
+  // ---- software-pipelined slice (PIPE): both 32-query halves live at once, in program
+  // order S/dP(0), S/dP(1), softmax(0), dK/dV(0), softmax(1), dK/dV(1) in ONE basic
+  // block (the mask is a template constant, no branches), so the scheduler can put the
+  // exp / mask / pack VALU of one half under the other half's independent MFMAs --
+  // with one wave per SIMD nothing else hides them.
+  // S / dP of one half: Q / dO rows in two groups of 4 k-steps, the second group's
+  // reads in flight under the first group's MFMAs (fences that let VALU / SALU
+  // through, so the other half's softmax can still fill the MFMA gaps)
+  constexpr int FENCE = 0x0002 | 0x0004 | 0x0400;  // VALU, SALU, TRANS may cross
+  auto sdp = [&](const char* Qs, int c, f32x16& sacc, f32x16& dpacc) {
+    const char* Os = Qs + QT;
+    const char* L = Qs + 2 * QT;
+    u16x8 qa[KS], oa[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS / 2; ++ks) {
+      qa[ks] = *reinterpret_cast<const u16x8*>(Qs + a_off[ks] + c * 8192);
+      oa[ks] = *reinterpret_cast<const u16x8*>(Os + a_off[ks] + c * 8192);
+    }
+#pragma unroll
+    for (int e4 = 0; e4 < 4; ++e4) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(L + l_off + (32 * c + 8 * e4) * 4);
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(L + l_off + (BQ + 32 * c + 8 * e4) * 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sacc[4 * e4 + j] = a[j];
+        dpacc[4 * e4 + j] = d4[j];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(FENCE);
+#pragma unroll
+    for (int ks = KS / 2; ks < KS; ++ks) {
+      qa[ks] = *reinterpret_cast<const u16x8*>(Qs + a_off[ks] + c * 8192);
+      oa[ks] = *reinterpret_cast<const u16x8*>(Os + a_off[ks] + c * 8192);
+    }
+    __builtin_amdgcn_sched_barrier(FENCE);
+#pragma unroll
+    for (int ks = 0; ks < KS / 2; ++ks) {
+      sacc = mfma32(as_bf8(qa[ks]), kf[ks], sacc);
+      dpacc = mfma32(as_bf8(oa[ks]), vf[ks], dpacc);
+    }
+    __builtin_amdgcn_sched_barrier(FENCE);
+#pragma unroll
+    for (int ks = KS / 2; ks < KS; ++ks) {
+      sacc = mfma32(as_bf8(qa[ks]), kf[ks], sacc);
+      dpacc = mfma32(as_bf8(oa[ks]), vf[ks], dpacc);
+    }
+  };
+  // mask as data: element e is live iff lo <= 8 (e >> 2) + (e & 3) < hi (lane values)
+  auto softmax = [&](f32x16& sacc, f32x16& dpacc, int lo, int hi, auto maskc) {
+    constexpr bool MASK = decltype(maskc)::value;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      float pv = __builtin_amdgcn_exp2f(sacc[e] * p.scale_log2);
+      if (MASK) {
+        const int qe = 8 * (e >> 2) + (e & 3);
+        pv = (qe >= lo && qe < hi) ? pv : 0.f;
+      }
+      sacc[e] = pv;
+      dpacc[e] = pv * dpacc[e];
+    }
+  };
+  // all 32 transposed reads of a half are issued before its first MFMA (a fence keeps
+  // the scheduler from sinking each read next to its use, which exposed the LDS
+  // latency once per MFMA)
+  auto kvacc = [&](const char* Qs, int c, const f32x16& sacc, const f32x16& dpacc) {
+    const char* Os = Qs + QT;
+    s4v A[2][DB][4];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int rb = (32 * c + 16 * st) * 256;
+#pragma unroll
+      for (int db = 0; db < DB; ++db) {
+        A[st][db][0] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(Os + rb + t_off[db][0]));
+        A[st][db][1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(Os + rb + t_off[db][1]));
+        A[st][db][2] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(Qs + rb + t_off[db][0]));
+        A[st][db][3] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(Qs + rb + t_off[db][1]));
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const bf8v pf = pack8(sacc, 8 * st);
+      const bf8v sf = pack8(dpacc, 8 * st);
+#pragma unroll
+      for (int db = 0; db < DB; ++db) {
+        dv[db] = mfma32(cat_tr(A[st][db][0], A[st][db][1]), pf, dv[db]);
+        dk[db] = mfma32(cat_tr(A[st][db][2], A[st][db][3]), sf, dk[db]);
+      }
+    }
+  };
+  auto slice_pipe = [&](const char* Qs, int step, int lo0, int hi0, int lo1, int hi1, auto maskc) {
+    (void)step;
+    f32x16 s0, d0, s1, d1;
+    sdp(Qs, 0, s0, d0);
+    sdp(Qs, 1, s1, d1);
+    softmax(s0, d0, lo0, hi0, maskc);
+    kvacc(Qs, 0, s0, d0);
+    softmax(s1, d1, lo1, hi1, maskc);
+    kvacc(Qs, 1, s1, d1);
+  };
+  // both halves active: the pipelined body (masked only where a half needs it)
+  auto slice_any = [&](const char* Qs, int step) {
+    const int qt0 = qstart + (step % nslice) * BQ;
+    bool act = true, need = false;
+    int lo[2], hi[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int q32 = qt0 + 32 * c;
+      act = act && !((CAUSAL && kw0 > q32 + 31 + offs) || q32 >= p.Sq);
+      need = need || (CAUSAL && kw0 + 31 > q32 + offs) || q32 + 32 > p.Sq || kw0 + 32 > p.Sk;
+      // live: q < Sq, mykey < Sk, causal mykey <= q + offs, q = q32 + 4 hh + qe
+      lo[c] = CAUSAL ? mykey - offs - q32 - 4 * hh : -1;
+      hi[c] = p.Sq - q32 - 4 * hh;
+      if (mykey >= p.Sk) hi[c] = -1;
+    }
+    if (!act) {
+      slice(Qs, step);
+    } else if (need) {
+      slice_pipe(Qs, step, lo[0], hi[0], lo[1], hi[1], std::integral_constant<bool, true>());
+    } else {
+      slice_pipe(Qs, step, lo[0], hi[0], lo[1], hi[1], std::integral_constant<bool, false>());
+    }
+  };
+
   char* const st0 = smem + KIMG;
   char* const st1 = st0 + STG;
   if (nsteps > 0) {
@@ -517,12 +656,14 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(Params p) {
   __syncthreads();
   for (int step = 0; step < nsteps; step += 2) {
     if (step + 1 < nsteps) load_regs(step + 1);
-    slice(st0, step);
+    if constexpr (PIPE) slice_any(st0, step);
+    else slice(st0, step);
     if (step + 1 < nsteps) store_lds(st1);
     __syncthreads();
     if (step + 1 >= nsteps) break;
     if (step + 2 < nsteps) load_regs(step + 2);
-    slice(st1, step + 1);
+    if constexpr (PIPE) slice_any(st1, step + 1);
+    else slice(st1, step + 1);
     if (step + 2 < nsteps) store_lds(st0);
     __syncthreads();
   }
@@ -578,6 +719,9 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(Params p) {
 
 using namespace pa;
 
+// A/B knob (benchmarks/fa_bwd_split_ab.py): bit 0 = the software-pipelined dK/dV slice
+PA_EXPORT void pa_fa_bwd_split_set_variant(int v) { fab::g_variant = v; }
+
 // Whether the split backward takes this problem (else the caller uses pa_flash_attn_bwd).
 PA_EXPORT int pa_fa_bwd_split_ok(int B, int Sq, int Sk, int Hq, int Hkv, int D, const long* strides /*24*/) {
   if (D != 128 || Hkv <= 0 || Hq % Hkv || Sq <= 0 || Sk <= 0 || B <= 0) return 0;
@@ -615,7 +759,10 @@ PA_EXPORT int pa_fa_bwd_split(const void* q, const void* k, const void* v, const
   const dim3 gq(Hq, B, (Sq + 127) / 128), gk(Hkv, B, (Sk + 127) / 128);
 #define PA_FAB_LAUNCH(C, R)                                                                  \
   hipLaunchKernelGGL((fab::fa_bwd_dq_kernel<C, R>), gq, dim3(256), 0, st, p);               \
-  hipLaunchKernelGGL((fab::fa_bwd_dkdv_kernel<C, R>), gk, dim3(256), 0, st, p);
+  if ((fab::g_variant & 1) && C)                                                             \
+    hipLaunchKernelGGL((fab::fa_bwd_dkdv_kernel<C, R, true>), gk, dim3(256), 0, st, p);     \
+  else                                                                                       \
+    hipLaunchKernelGGL((fab::fa_bwd_dkdv_kernel<C, R, false>), gk, dim3(256), 0, st, p);
   if (causal) {
     if (rope) { PA_FAB_LAUNCH(true, true) } else { PA_FAB_LAUNCH(true, false) }
   } else {

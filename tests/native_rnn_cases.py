@@ -106,7 +106,7 @@ CASES = {
 WD, LD, PD, MD = 30, 7, 6, 2  # word / label / predicate dicts, mark dict
 
 
-def srl(depth=3, hidden=8, word_dim=4, mark_dim=3):
+def srl(depth=3, hidden=8, word_dim=4, mark_dim=3, extra=False):
     def build():
         names = ["word", "verb", "ctx_n2", "ctx_n1", "ctx_0", "ctx_p1", "ctx_p2", "mark"]
         feats = {n: fluid.layers.data(name=n, shape=[1], dtype="int64", lod_level=1) for n in names}
@@ -123,6 +123,7 @@ def srl(depth=3, hidden=8, word_dim=4, mark_dim=3):
                                          candidate_activation="relu", gate_activation="sigmoid",
                                          cell_activation="sigmoid")[0]
         tmp = [h0, lstm]
+        dbg = [h0, lstm]
         for i in range(1, depth):
             mix = fluid.layers.sums(input=[fluid.layers.fc(input=tmp[0], size=hidden),
                                            fluid.layers.fc(input=tmp[1], size=hidden)])
@@ -130,6 +131,7 @@ def srl(depth=3, hidden=8, word_dim=4, mark_dim=3):
                                              candidate_activation="relu", gate_activation="sigmoid",
                                              cell_activation="sigmoid", is_reverse=(i % 2) == 1)[0]
             tmp = [mix, lstm]
+            dbg += [mix, lstm]
         feature = fluid.layers.sums(input=[fluid.layers.fc(input=tmp[0], size=LD, act="tanh"),
                                            fluid.layers.fc(input=tmp[1], size=LD, act="tanh")])
         crf_cost = fluid.layers.linear_chain_crf(input=feature, label=target,
@@ -138,6 +140,8 @@ def srl(depth=3, hidden=8, word_dim=4, mark_dim=3):
         fluid.optimizer.SGD(learning_rate=fluid.layers.exponential_decay(
             learning_rate=0.05, decay_steps=3, decay_rate=0.5, staircase=True)).minimize(avg)
         decode = fluid.layers.crf_decoding(input=feature, param_attr=fluid.ParamAttr(name="crfw"))
+        if extra:
+            return [avg, decode, feature, crf_cost] + dbg
         return [avg, decode]
     return build
 
