@@ -18,9 +18,14 @@ def go(engine, init=None, steps=3):
     main.random_seed = startup.random_seed = 7
     with fluid.unique_name.guard(), fluid.program_guard(main, startup):
         fetch = srl()()
-    lr = [v for v in main.list_vars() if "learning_rate" in v.name]
+    sgd = [op for op in main.global_block().ops if op.type == "sgd"]
+    lrn = sgd[0].input("LearningRate")[0]
+    lr = [main.global_block().var(lrn)]
+    print("lr op chain:", [(op.type, op.input_arg_names, op.output_arg_names) for op in main.global_block().ops
+                           if op.type in ("increment", "cast", "elementwise_div", "floor", "elementwise_pow",
+                                          "scale", "fill_constant", "elementwise_mul")][:12])
     scope = core.Scope()
-    place = fluid.CUDAPlace(0)
+    place = fluid.CPUPlace() if os.environ.get("SRL_CPU") else fluid.CUDAPlace(0)
     out = []
     with fluid.executor.scope_guard(scope):
         fluid.Executor(place, engine="python").run(startup)
