@@ -1060,7 +1060,296 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Params p) {
 #undef DMA_B
 }
 
-static int g_sched = -1;      // -1: per-layout default; 0 / 1: force PF_IN_CLUSTER (A/B runs)
+// ---------------------------------------------------------------------------------
+// Weight-gradient GEMM with an MN-major operand, one wave per SIMD:
+//   C (fp32, =|+=) alpha * sum_k A(m, k) B(n, k),  K % 64 == 0, no bias / batch.
+// The two-wave kernel above owns a 128 x 64 output per wave; with an MN-major operand
+// every 16 x 32 fragment costs two ds_read_b64_tr_b16, so its LDS-issue share doubles
+// and the matrix pipe falls to ~60 % busy (profiles/r4_gemm_forms_pmc.md).  Here 256
+// threads = 4 waves (2 M x 2 N) each own 128 x 128: 64 f32x4 accumulators (256
+// registers, the AGPR half of the 512-entry file that one wave per SIMD has), and
+// every fragment read feeds 8 MFMAs instead of 4-8, so a k32 step is 16 fragment
+// loads under 64 MFMAs (1024 matrix cycles).  With no second wave on the SIMD to
+// hide LDS latency, the next k32 step's fragments are read INSIDE the current
+// step's MFMA stream (double-buffered registers).  Same LDS image, swizzles, LDS-DMA
+// and XCD tile order as the kernel above; one barrier per 64-deep k-tile:
+//   [step kk0 of tile t | reads kk1 of t] wait, barrier, DMA(t+2) into t's stage,
+//   [step kk1 of t | reads kk0 of t+1]
+// so each DMA lands under two k32 steps (2048 matrix cycles).
+constexpr int NT1 = 256;
+
+// Fragment registers of the one-wave kernel.  Every read is an asm ds_read with an
+// IMMEDIATE offset from one of a few per-lane base addresses (the swizzle depends on
+// the lane only), so no per-fragment address is ever materialised -- hipcc would
+// otherwise hoist one loop-invariant address per fragment (64+ VGPRs) and spill.
+//  K-major: base[kk] = slab row (l & 15), chunk (4 kk + (l >> 4)) ^ ((l & 15) >> 1);
+//           fragment f (32-mn block f / 2, half f % 2) at + 4096 (f / 2) + 2048 (f % 2)
+//  MN-major: base[c] (c = f % 4) = k row 8 (l >> 4) + ((l & 15) >> 2), chunk
+//           (2 c ^ swz(k)) + ((l & 3) >> 1), + 8 (l & 1); + 8192 (f / 4) + 4096 kk
+template <bool KMAJ>
+struct F1w {
+  bf16x8 v;
+  s16x4 x, y;
+  // off must fold to a constant (unrolled loops): it becomes the instruction's offset
+  __device__ __forceinline__ void load(unsigned a, int off) {
+    if constexpr (KMAJ) {
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(off));
+    } else {
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(x) : "v"(a), "i"(off));
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(y) : "v"(a), "i"(off + 512));
+    }
+  }
+  __device__ __forceinline__ void wait() {
+    if constexpr (KMAJ) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v));
+    else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(x), "+v"(y));
+  }
+  __device__ __forceinline__ bf16x8 get() const {
+    if constexpr (KMAJ) {
+      return v;
+    } else {
+      i16x8 t = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+      return __builtin_bit_cast(bf16x8, t);
+    }
+  }
+};
+
+// per-lane base addresses of one operand (stage 0) for this wave's 128-wide block
+// starting at 32-mn block `u0` (a multiple of 4); [kk] for K-major, [c] for MN-major
+template <bool KMAJ>
+__device__ __forceinline__ void f1w_bases(unsigned (&b)[4], unsigned opnd, int u0, int lane) {
+  if constexpr (KMAJ) {
+    const int row = lane & 15;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = (4 * kk + (lane >> 4)) ^ ((row >> 1) & 7);
+      b[kk] = opnd + (unsigned)(u0 * 4096 + row * 128 + ch * 16);
+    }
+    b[2] = b[3] = 0;
+  } else {
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    const int k0 = 8 * g + q;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int ch = ((2 * c) ^ mn_swz(k0)) + (pp >> 1);
+      b[c] = opnd + (unsigned)((u0 >> 1) * 8192 + k0 * 128 + ch * 16 + 8 * (pp & 1));
+    }
+  }
+}
+
+// read fragment F (compile-time after unrolling) of k-half KK from bases b (+ stage)
+#define F1W_LOAD(KMAJ, FR, b, F, KK)                                              \
+  do {                                                                            \
+    if constexpr (KMAJ)                                                           \
+      FR.load(b[(KK)], 4096 * ((F) >> 1) + 2048 * ((F) & 1));            \
+    else                                                                          \
+      FR.load(b[(F) & 3], 8192 * ((F) >> 2) + 4096 * (KK));             \
+  } while (0)
+
+template <bool AK, bool BK>
+__global__ __launch_bounds__(NT1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm1w_kernel(Params p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int M = p.M, N = p.N, K = p.K;
+  const int tiles_m = p.tiles_m, nwg = tiles_m * p.tiles_n;
+  // XCD-aware tile order, bands of 8 tile rows (as tile_of above)
+  int m0, n0;
+  {
+    const int t = xcd_remap(blockIdx.x, nwg);
+    constexpr int BAND = 8;
+    const int band = t / (BAND * p.tiles_n);
+    const int m_in_band = min(BAND, tiles_m - band * BAND);
+    const int tin = t - band * BAND * p.tiles_n;
+    m0 = (band * BAND + tin % m_in_band) * BM;
+    n0 = (tin / m_in_band) * BN;
+  }
+  const unsigned a_bytes = AK ? (unsigned)(((long)(M - 1) * p.lda + K) * 2) : (unsigned)(((long)(K - 1) * p.lda + M) * 2);
+  const unsigned b_bytes = BK ? (unsigned)(((long)(N - 1) * p.ldb + K) * 2) : (unsigned)(((long)(K - 1) * p.ldb + N) * 2);
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, 0, b_bytes, 0x00020000);
+  // DMA plan: wave w fills slab w (64 mn x 64 k, 8 pieces of 1 KiB) of A and of B
+  unsigned offA[8], offB[8];
+#pragma unroll
+  for (int pc = 0; pc < 8; ++pc) {
+    int mn, k;
+    dma_coords<AK>(wid, pc, lane, mn, k);
+    int g = m0 + mn;
+    offA[pc] = g >= M ? OOB : (AK ? (unsigned)(((long)g * p.lda + k) * 2) : (unsigned)(((long)k * p.lda + g) * 2));
+    dma_coords<BK>(wid, pc, lane, mn, k);
+    g = n0 + mn;
+    offB[pc] = g >= N ? OOB : (BK ? (unsigned)(((long)g * p.ldb + k) * 2) : (unsigned)(((long)k * p.ldb + g) * 2));
+  }
+  const int nk = K / BKT;
+  auto dma = [&](int kt) {
+    char* st = smem + (kt & 1) * STAGE;
+    const unsigned ka = AK ? (unsigned)(kt * BKT * 2) : (unsigned)((long)kt * BKT * p.lda * 2);
+    const unsigned kb = BK ? (unsigned)(kt * BKT * 2) : (unsigned)((long)kt * BKT * p.ldb * 2);
+#pragma unroll
+    for (int pc = 0; pc < 8; ++pc)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(st + wid * 8192 + pc * 1024),
+                                               16, offA[pc] == OOB ? OOB : offA[pc] + ka, 0, 0, 0);
+#pragma unroll
+    for (int pc = 0; pc < 8; ++pc)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB,
+                                               (__attribute__((address_space(3))) void*)(st + OPND + wid * 8192 + pc * 1024),
+                                               16, offB[pc] == OOB ? OOB : offB[pc] + kb, 0, 0, 0);
+  };
+
+  // accumulators pinned to AGPRs for the whole tile (defined and read by asm with "a"
+  // operands, as fa_bwd_split.hip): otherwise hipcc keeps them in VGPRs and spills
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      asm volatile("" : "=a"(acc[i][j]) : "0"(z));
+    }
+  // fragment f (0..7) of this wave: 32-mn block 4 w + f / 2, 16-row half f % 2
+  F1w<AK> a0[8], a1[8];
+  F1w<BK> b0[8], b1[8];
+  unsigned baA[4], baB[4];
+  const unsigned lds0 = lds_addr(smem);
+  f1w_bases<AK>(baA, lds0, 4 * wr, lane);
+  f1w_bases<BK>(baB, lds0 + OPND, 4 * wc, lane);
+
+  dma(0);
+  if (nk > 1) dma(1);
+  if (nk > 1) {
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    wait_vm0();
+  }
+  bar();
+#pragma unroll
+  for (int f = 0; f < 8; ++f) {
+    F1W_LOAD(AK, a0[f], baA, f, 0);
+    F1W_LOAD(BK, b0[f], baB, f, 0);
+  }
+
+  // one k32 step on (FA, FB): 16 groups of 4 MFMAs, with the 16 fragment reads of the
+  // next step (bases NBA / NBB, k-half KK) spread over the first 12 groups
+#define STEP1W(FA, FB, NA, NB, NBA, NBB, KK, DO)                                                     \
+  _Pragma("unroll") for (int g_ = 0; g_ < 16; ++g_) {                                                 \
+    const int i_ = g_ >> 1, j0_ = 4 * (g_ & 1);                                                       \
+    /* the empty asm statements are ordered with the reads and pin each group of 4 */                  \
+    /* MFMAs between them: the DAG scheduler places pure MFMAs anywhere otherwise */                   \
+    asm volatile("" : "+a"(acc[i_][j0_]), "+a"(acc[i_][j0_ + 1]), "+a"(acc[i_][j0_ + 2]), "+a"(acc[i_][j0_ + 3])); \
+    _Pragma("unroll") for (int j_ = j0_; j_ < j0_ + 4; ++j_)                                          \
+      acc[i_][j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j_].get(), FA[i_].get(), acc[i_][j_], 0, 0, 0); \
+    asm volatile("" : "+a"(acc[i_][j0_]), "+a"(acc[i_][j0_ + 1]), "+a"(acc[i_][j0_ + 2]), "+a"(acc[i_][j0_ + 3])); \
+    /* read r goes out after group 3 r / 4: groups 12-15 (256 matrix cycles) cover */                  \
+    /* the last read's latency before the next step waits for it */                                   \
+    _Pragma("unroll") for (int r_ = 0; r_ < 16; ++r_) {                                               \
+      if ((DO) && (3 * r_) / 4 == g_) {                                                               \
+        if (r_ & 1)                                                                                   \
+          F1W_LOAD(BK, NB[r_ >> 1], NBB, r_ >> 1, KK);                                                \
+        else                                                                                          \
+          F1W_LOAD(AK, NA[r_ >> 1], NBA, r_ >> 1, KK);                                                \
+      }                                                                                               \
+    }                                                                                                 \
+  }
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const unsigned so = (kt & 1) ? (unsigned)STAGE : 0u, sn = (unsigned)STAGE - so;
+    unsigned cA[4], cB[4], nA[4], nB[4];  // this / the next stage's bases
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      cA[c] = baA[c] + so;
+      cB[c] = baB[c] + so;
+      nA[c] = baA[c] + sn;
+      nB[c] = baB[c] + sn;
+    }
+    // ---- k32 step 0 of tile kt; reads of step 1 (same stage)
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      a0[f].wait();
+      b0[f].wait();
+    }
+    __builtin_amdgcn_s_setprio(1);
+    STEP1W(a0, b0, a1, b1, cA, cB, 1, true)
+    __builtin_amdgcn_s_setprio(0);
+    // every wave's reads of stage kt done and DMA(kt+1) landed -> stage kt is free
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      a1[f].wait();
+      b1[f].wait();
+    }
+    wait_vm0();
+    bar();
+    if (kt + 2 < nk) dma(kt + 2);
+    // ---- k32 step 1 of tile kt; reads of the next tile's step 0
+    __builtin_amdgcn_s_setprio(1);
+    // (the last tile reads the other stage too: stale, unused, and keeps the loop
+    // body branch-free so the accumulators keep one register assignment)
+    STEP1W(a1, b1, a0, b0, nA, nB, 0, true)
+    __builtin_amdgcn_s_setprio(0);
+  }
+#pragma unroll
+  for (int f = 0; f < 8; ++f) {
+    a0[f].wait();
+    b0[f].wait();
+  }
+#undef STEP1W
+#undef F1W_LOAD
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+  // ---- epilogue: C (fp32) =|+= alpha * acc, straight from the registers.  Lane holds
+  // C[m = 16 i + (l & 15)][n = 16 j + 4 (l >> 4) + r] of its 128 x 128; each 16-B
+  // access is 4 consecutive n.  Per-tile descriptor, out-of-range lanes sent OOB.
+  const __amdgpu_buffer_rsrc_t rsC =
+      __builtin_amdgcn_make_buffer_rsrc((char*)p.C + ((long)m0 * p.ldc + n0) * 4, 0, (int)OOB, 0x00020000);
+  const int ml = 128 * wr + (lane & 15), nl = 128 * wc + 4 * (lane >> 4);
+  const unsigned rb = (unsigned)p.ldc * 4u;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = ml + 16 * i;
+    unsigned off[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = nl + 16 * j;
+      off[j] = (m0 + m < M && n0 + n < N) ? (unsigned)m * rb + (unsigned)n * 4u : OOB;
+    }
+    u32x4 old[8];
+    if (p.accumulate) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) old[j] = __builtin_amdgcn_raw_buffer_load_b128(rsC, off[j], 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      f32x4 v = p.alpha * acc[i][j];
+      if (p.accumulate) v += __builtin_bit_cast(f32x4, old[j]);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsC, off[j], 0, 0);
+    }
+  }
+}
+
+// route fp32 weight-gradient GEMMs with an MN-major operand to gemm1w_kernel: OFF by
+// default -- measured 0.75-0.85x of the two-wave kernel on every LLaMA dW shape
+// (profiles/r6_gemm_dw_1wave_NEGATIVE.md); pa_gemm_set_dw1w(1) selects it
+static int g_dw1w = 0;
+
+template <bool AK, bool BK>
+static int launch_1w(const Params& p0, hipStream_t st) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)gemm1w_kernel<AK, BK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       2 * STAGE);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  Params p = p0;
+  p.tiles_m = (p.M + BM - 1) / BM;
+  p.tiles_n = (p.N + BN - 1) / BN;
+  hipLaunchKernelGGL((gemm1w_kernel<AK, BK>), dim3(p.tiles_m * p.tiles_n), dim3(NT1), 2 * STAGE, st, p);
+  return (int)hipGetLastError();
+}
+
+static int g_sched = -1;     // -1: per-layout default; 0 / 1: force PF_IN_CLUSTER (A/B runs)
 static int g_persistent = 1;  // 0: one tile per block (grid = tiles), for A/B runs
 static int g_stagger = 1;     // start stagger units per block slot (profiles/r3_gemm_stagger_ab.jsonl: +0.7 % over the step GEMMs)
 
@@ -1222,6 +1511,7 @@ PA_EXPORT int pa_group_tile_table(int* grp, int G, long total_rows, hipStream_t 
 PA_EXPORT void pa_gemm_set_sched(int s) { gemm::g_sched = s; }
 PA_EXPORT void pa_gemm_set_persistent(int s) { gemm::g_persistent = s; }
 PA_EXPORT void pa_gemm_set_stagger(int s) { gemm::g_stagger = s; }
+PA_EXPORT void pa_gemm_set_dw1w(int s) { gemm::g_dw1w = s; }
 
 // Returns 0 on success, a hipError on launch failure, -1 for an unsupported shape
 // (the caller checks shapes first: N a multiple of 8, K a multiple of 8 when an
@@ -1265,6 +1555,13 @@ static int gemm_entry(bool padded, int a_kmaj, int b_kmaj, int out_f32, const vo
   if (p.atomic && bias) return -1;
   if (K <= 0) return -1;
   if ((long)ldc * gemm::BM * (out_f32 ? 4 : 2) >= (long)gemm::OOB) return -1;  // per-tile C offsets are 32-bit
+  // fp32 weight gradients with an MN-major operand: the one-wave-per-SIMD kernel
+  if (gemm::g_dw1w && out_f32 && !(a_kmaj && b_kmaj) && !padded && !bias && batch == 1 && !grp && !k_total &&
+      !p.atomic && K % gemm::BKT == 0) {
+    if (a_kmaj) return gemm::launch_1w<true, false>(p, st);
+    if (b_kmaj) return gemm::launch_1w<false, true>(p, st);
+    return gemm::launch_1w<false, false>(p, st);
+  }
 #define PA_G(AK, BK, F)                                                \
   if (a_kmaj == AK && b_kmaj == BK && out_f32 == F) return gemm::launch<AK, BK, F>(p, batch, st);
   PA_G(1, 1, 0) PA_G(1, 0, 0) PA_G(0, 1, 0) PA_G(0, 0, 0)

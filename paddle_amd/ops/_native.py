@@ -105,6 +105,7 @@ _SIGS = {
     "pa_gemm_set_sched": [_I],
     "pa_gemm_set_persistent": [_I],
     "pa_gemm_set_stagger": [_I],
+    "pa_gemm_set_dw1w": [_I],
     "pa_gemm": [_I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _L, _L, _L, _L, _L, _L, _I, _F, _I, _I, _I, _P, _I, _P],
     "pa_gemm_padded": [_I, _I, _I, _P, _P, _P, _I, _I, _I, _L, _L, _L, _I, _P],
     "pa_splitk_reduce": [_P, _P, _L, _I, _I, _P],

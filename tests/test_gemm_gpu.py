@@ -153,3 +153,31 @@ def test_gemm_persistent_multi_tile_direct_epilogue(K, bias):
     # the same product twice in a row on one stream: identical bits
     c2 = G.gemm(a, b, M, N, K, a_kmaj=True, b_kmaj=True, bias=bv)
     assert torch.equal(c, c2)
+
+
+@pytest.mark.parametrize("M,N,K", [(264, 136, 64), (1000, 776, 4096), (512, 1024, 8192), (4096, 512, 192)])
+@pytest.mark.parametrize("a_kmaj,b_kmaj", [(True, False), (False, False), (False, True)])
+@pytest.mark.parametrize("accumulate", [True, False])
+def test_gemm_dw_one_wave_kernel(M, N, K, a_kmaj, b_kmaj, accumulate):
+    """The one-wave-per-SIMD weight-gradient kernel (gemm1w_kernel, selected by
+    pa_gemm_set_dw1w(1); off by default, measured slower): fp32 reference, ragged
+    M / N edges, one and several k-tiles, and the same result as the two-wave kernel."""
+    from paddle_amd.ops import _native as NL
+    from paddle_amd.ops import gemm as G
+
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    a, af = _operand(M, K, a_kmaj, gen)
+    b, bf = _operand(N, K, b_kmaj, gen)
+    c0 = torch.randn(M, N, generator=gen, device="cuda")
+    outs = []
+    try:
+        for v in (1, 0):
+            NL.lib().pa_gemm_set_dw1w(v)
+            c = c0.clone() if accumulate else torch.full((M, N), float("nan"), device="cuda")
+            G.gemm(a, b, M, N, K, a_kmaj=a_kmaj, b_kmaj=b_kmaj, out=c, accumulate=accumulate, alpha=0.75)
+            outs.append(c)
+    finally:
+        NL.lib().pa_gemm_set_dw1w(0)
+    ref = 0.75 * (af @ bf.t()) + (c0 if accumulate else 0)
+    assert torch.allclose(outs[0], ref, atol=2e-3 * K ** 0.5, rtol=1e-4), (outs[0] - ref).abs().max()
+    assert (outs[0] - outs[1]).abs().max().item() <= 1e-3 * K ** 0.5
