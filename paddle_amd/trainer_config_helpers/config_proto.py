@@ -441,6 +441,7 @@ _TYPE = {
     "sub_seq_layer": "subseq", "scale_sub_region_layer": "scale_sub_region",
     "factorization_machine": "factorization_machine", "pooling_layer": "max", "mixed_layer": "mixed",
     "embedding_layer": "mixed", "dropout_layer": "addto", "memory": "agent",
+    "recurrent_group": "recurrent_layer_group",
 }
 _ACT = {None: "", "linear": "", "identity": "", "exp": "exponential", "soft_relu": "softrelu"}
 # layers whose size is their input's (the reference sets size = input.size)
@@ -448,6 +449,8 @@ _SAME_SIZE = {"trans_layer", "first_seq", "last_seq", "dropout_layer", "batch_no
               "row_l2_norm_layer", "sum_to_one_norm_layer", "scaling_layer", "slope_intercept_layer",
               "power_layer", "rotate_layer", "prelu_layer", "pooling_layer", "addto_layer", "expand_layer",
               "img_cmrnorm_layer", "crf_layer"}
+# projections without a parameter (they take no weight of the mixed layer's)
+_PARAMLESS = {"identity", "identity_offset", "slice"}
 # functions that are not layers (projections / operators feed mixed / concat layers)
 _NOT_LAYERS = {"settings", "outputs", "get_config_arg", "define_py_data_sources2", "parse_config"}
 
@@ -468,6 +471,9 @@ class Recorder:
         self.by_name = {}     # layer name -> its LayerConfig (image dims of inputs)
         self.evaluators = []  # EvaluatorConfigs (classification_cost's default evaluator)
         self.parents = {}     # layer name -> parent layer names (networks.outputs DFS)
+        self.groups = []      # open recurrent_group records (innermost last)
+        self.sub_models = []  # finished recurrent_group SubModelConfigs
+        self.inner = set()    # layer names that belong to a recurrent group
 
     def name_for(self, fn, given):
         if given:
@@ -594,6 +600,10 @@ def recorded(fn_name, fn):
             return fn(*args, **kw)
         from ..v2._core import STATE
 
+        if fn_name == "recurrent_group":
+            return _record_group(rec, fn, args, kw)
+        if fn_name == "memory" and rec.groups:
+            return _record_memory(rec, fn, args, kw)
         blk = STATE["main"].global_block()
         before = {p.name for p in blk.all_parameters()}
         rec.depth += 1
@@ -623,6 +633,11 @@ def _record(rec, fn_name, fn, args, kw, out, before, blk):
             return out
         v = outs[0]
         name = rec.name_for(fn_name, kw.get("name") if fn_name != "data_layer" else (kw.get("name") or args[0]))
+        base = name  # projection names inside a recurrent group keep the unsuffixed layer name
+        if rec.groups:
+            name = f"{base}@{rec.groups[-1]['name']}"
+            rec.groups[-1]["layer_names"].append(name)
+            rec.inner.add(name)
         ins = _flat_inputs(fn, args, kw)
         typ = _TYPE.get(fn_name, fn_name.replace("_layer", ""))
         act = kw.get("act")
@@ -645,17 +660,27 @@ def _record(rec, fn_name, fn, args, kw, out, before, blk):
         biases = [p for p in new if p.name not in wn]
         layer_inputs = []
         projs = any(pr is not None for _, pr in ins)
+        # user-named weights: the layer's param_attr (one per input when a list), else a
+        # projection's own; they are not handed out by position
+        unames = []
+        for i, (x, pr) in enumerate(ins):
+            un = _attr_name(kw.get("param_attr"), i)
+            if un is None and pr is not None:
+                un = _attr_name(getattr(pr, "v1_param_attr", None), 0)
+            unames.append(un)
+        weights = [p for p in weights if p.name not in set(unames)]
+        wi = 0
         if fn_name == "concat_layer" and projs:
             lc["type"] = "concat2"
         for i, (x, pr) in enumerate(ins):
             li = {"input_layer_name": rec.layer_name(x) or x.name}
             if pr is not None and fn_name == "concat_layer":
-                li["proj_conf"] = {"type": getattr(pr, "v1_type", "identity"), "name": f"_{name}.w{i}",
+                li["proj_conf"] = {"type": getattr(pr, "v1_type", "identity"), "name": f"_{base}.w{i}",
                                    "input_size": _vsize(x), "output_size": _vsize(x)}
             if pr is not None and fn_name in ("mixed_layer", "embedding_layer") and getattr(pr, "v1_type", None):
-                li["proj_conf"] = {"type": _PROJ_TYPE.get(pr.v1_type, pr.v1_type), "name": f"_{name}.w{i}",
+                li["proj_conf"] = {"type": _PROJ_TYPE.get(pr.v1_type, pr.v1_type), "name": f"_{base}.w{i}",
                                    "input_size": _vsize(x), "output_size": size}
-            uname = _attr_name(kw.get("param_attr"), i)
+            uname = unames[i]
             if uname is not None and uname in by_pname:  # ParamAttr(name=...): a named, possibly shared, weight
                 li["input_parameter_name"] = uname
                 if uname not in rec.param_map:
@@ -664,12 +689,14 @@ def _record(rec, fn_name, fn, args, kw, out, before, blk):
                     rec.params.append({"name": uname, "size": int(_prod(dims)), "initial_mean": 0.0,
                                        "initial_std": 1.0 / max(dims[0], 1) ** 0.5, "dims": dims,
                                        "initial_strategy": 0, "initial_smart": True})
-                    _apply_pattr(rec.params[-1], _pattr(kw.get("param_attr"), i))
-            elif i < len(weights):
+                    _apply_pattr(rec.params[-1], _pattr(kw.get("param_attr"), i) if pr is None or
+                             getattr(pr, "v1_param_attr", None) is None else pr.v1_param_attr)
+            elif wi < len(weights) and (pr is None or getattr(pr, "v1_type", None) not in _PARAMLESS):
                 pname = f"_{name}.w{i}"
                 li["input_parameter_name"] = pname
-                rec.param_map[pname] = weights[i].name
-                dims = _param_dims(weights[i])
+                rec.param_map[pname] = weights[wi].name
+                dims = _param_dims(weights[wi])
+                wi += 1
                 rec.params.append({"name": pname, "size": int(_prod(dims)), "initial_mean": 0.0,
                                    "initial_std": 1.0 / max(dims[0], 1) ** 0.5, "dims": dims,
                                    "initial_strategy": 0, "initial_smart": True})
@@ -714,6 +741,101 @@ def _record(rec, fn_name, fn, args, kw, out, before, blk):
         rec.of_var[id(v)] = name
         rec.vars.append(v)
         return out
+
+
+def _add_layer(rec, lc, var=None, parents=()):
+    rec.layers.append(lc)
+    rec.by_name[lc["name"]] = lc
+    rec.parents[lc["name"]] = list(parents)
+    if var is not None:
+        rec.of_var[id(var)] = lc["name"]
+        rec.vars.append(var)
+
+
+def _record_memory(rec, fn, args, kw):
+    """memory() inside a recurrent group (config_parser.py Memory / RecurrentLayerGroup):
+    an ``agent`` layer ``<name>+delay1@<group>`` (``__memory_<k>__@<group>`` when
+    anonymous, k counting every memory() call), linked to the group's layer of that
+    name in the group's ``memories``."""
+    g = rec.groups[-1]
+    name = _arg(args, kw, "name", 0)
+    size = _arg(args, kw, "size", 1)
+    boot = _arg(args, kw, "boot_layer", 3)
+    k = rec.count.get("memory", 0)
+    rec.count["memory"] = k + 1
+    agent = f"{name}+delay1@{g['name']}" if name else f"__memory_{k}__@{g['name']}"
+    out = fn(*args, **kw)
+    _add_layer(rec, {"name": agent, "type": "agent", "size": size, "active_type": ""}, out)
+    g["layer_names"].append(agent)
+    rec.inner.add(agent)
+    ent = {"layer_name": f"{name}@{g['name']}" if name else None, "link_name": agent}
+    if boot is not None and rec.layer_name(boot):
+        ent["boot_layer_name"] = rec.layer_name(boot)
+    g["memories"].append(ent)
+    if not name and hasattr(out, "set_input"):
+        bind = out.set_input
+
+        def set_input(layer, _b=bind, _e=ent):
+            _b(layer)
+            _e["layer_name"] = rec.layer_name(layer)
+        out.set_input = set_input
+    return out
+
+
+def _record_group(rec, fn, args, kw):
+    """recurrent_group (config_parser.py RecurrentLayerGroupBegin / End): a
+    ``recurrent_layer_group`` layer, one ``scatter_agent`` per sequence input
+    (``<input>@<group>``), the step's layers named ``<layer>@<group>``, one
+    ``gather_agent`` per step output under the output's own name, and a
+    SubModelConfig with the memories and in / out links."""
+    from .layers_v1 import StaticInput, SubsequenceInput
+
+    step = _arg(args, kw, "step", 0)
+    inp = _arg(args, kw, "input", 1)
+    reverse = bool(_arg(args, kw, "reverse", 2, False))
+    gname = rec.name_for("recurrent_group", _arg(args, kw, "name", 3))
+    _add_layer(rec, {"name": gname, "type": "recurrent_layer_group", "active_type": ""})
+    g = {"name": gname, "layer_names": [], "is_recurrent_layer_group": True, "reversed": reverse, "memories": [],
+         "in_links": [], "out_links": [], "_outs": []}
+    ins = list(inp) if isinstance(inp, (list, tuple)) else [inp]
+
+    def step_rec(*sargs):
+        for x, a in zip(ins, sargs):
+            if isinstance(x, StaticInput):
+                continue
+            outer = x.input if isinstance(x, SubsequenceInput) else x
+            on = rec.layer_name(outer) or outer.name
+            agent = f"{on}@{gname}"
+            _add_layer(rec, {"name": agent, "type": "scatter_agent", "size": _vsize(outer), "active_type": ""}, a,
+                       [on])
+            g["layer_names"].append(agent)
+            rec.inner.add(agent)
+            g["in_links"].append({"layer_name": on, "link_name": agent})
+        res = step(*sargs)
+        g["_outs"] = list(res) if isinstance(res, (list, tuple)) else [res]
+        return res
+
+    a2, kw2 = list(args), dict(kw)
+    if "step" in kw2:
+        kw2["step"] = step_rec
+    else:
+        a2[0] = step_rec
+    rec.groups.append(g)
+    try:
+        out = fn(*a2, **kw2)
+    finally:
+        rec.groups.pop()
+    outs = list(out) if isinstance(out, (list, tuple)) else [out]
+    for inner, o in zip(g["_outs"], outs):
+        iname = rec.layer_name(inner)
+        if not iname:
+            continue
+        gather = iname.rsplit("@", 1)[0]
+        _add_layer(rec, {"name": gather, "type": "gather_agent", "size": _vsize(inner), "active_type": ""}, o,
+                   [iname])
+        g["out_links"].append({"layer_name": iname, "link_name": gather})
+    rec.sub_models.append(g)
+    return out
 
 
 # ---------------------------------------------------------------- per-type fields
@@ -1401,7 +1523,48 @@ def _x_lambda(lc, a, kw, ins, rec, name):
     lc["max_sort_size"] = int(kw.get("max_sort_size", -1))
 
 
+def _x_lstm_step(lc, a, kw, ins, rec, name):
+    """LstmStepLayer: gate / state activations, no input weights, a [1, 3 size]
+    peephole bias (config_parser.py LstmStepLayer)."""
+    lc["active_type"] = _ACT.get(_act_or(kw, "act", "tanh"), _act_or(kw, "act", "tanh"))
+    lc["active_gate_type"] = _act_or(kw, "gate_act", "sigmoid")
+    lc["active_state_type"] = _act_or(kw, "state_act", "tanh")
+    for li in lc.get("inputs", []):
+        li.pop("input_parameter_name", None)
+    battr = kw.get("bias_attr")
+    if battr is False:
+        return
+    n = 3 * int(lc["size"])
+    bname = _attr_name(battr, 0) or f"_{name}.wbias"
+    lc["bias_parameter_name"] = bname
+    if bname not in rec.param_map:
+        rec.param_map[bname] = bname
+        rec.params.append({"name": bname, "size": n, "initial_mean": 0.0, "initial_std": 0.0, "dims": [1, n],
+                           "initial_strategy": 0, "initial_smart": False})
+        _apply_pattr(rec.params[-1], battr)
+
+
+def _x_gru_step(lc, a, kw, ins, rec, name):
+    """GruStepLayer: the [size, 3 size] weight belongs to the input (0) only."""
+    lc["active_type"] = _ACT.get(_act_or(kw, "act", "tanh"), _act_or(kw, "act", "tanh"))
+    lc["active_gate_type"] = _act_or(kw, "gate_act", "sigmoid")
+    for li in lc.get("inputs", [])[1:]:
+        pn = li.pop("input_parameter_name", None)
+        if pn is not None and pn.startswith(f"_{name}."):
+            rec.params[:] = [p for p in rec.params if p["name"] != pn]
+            rec.param_map.pop(pn, None)
+
+
+def _x_get_output(lc, a, kw, ins, rec, name):
+    """GetOutputLayer: the input names which output of the source layer it reads."""
+    arg = _arg(a, kw, "arg_name", 1)
+    if lc.get("inputs") and arg:
+        lc["inputs"][0]["input_layer_argument"] = arg
+
+
 _EXTRA = {
+    "lstm_step_layer": _x_lstm_step, "gru_step_layer": _x_gru_step, "gru_step_naive_layer": _x_gru_step,
+    "get_output_layer": _x_get_output,
     "batch_norm_layer": _x_batch_norm, "nce_layer": _x_nce, "img_conv_layer": _x_conv,
     "pooling_layer": _x_pooling, "slope_intercept_layer": _x_slope, "scaling_layer": _x_weight_first,
     "interpolation_layer": _x_weight_first, "power_layer": _x_weight_first,
@@ -1463,11 +1626,12 @@ def model_config(rec, outputs, first_outputs=None):
     # sets input_layer_names once, there)
     src = [rec.layer_name(o) or getattr(o, "name", str(o)) for o in (first_outputs or outputs)]
     ins = _dfs_inputs(rec, src) if src and all(o in rec.by_name for o in src) else rec.inputs
-    mc = {"type": "nn", "layers": rec.layers, "parameters": rec.params, "input_layer_names": ins,
-          "output_layer_names": out_names, "evaluators": rec.evaluators,
-          "sub_models": [{"name": "root", "layer_names": names, "input_layer_names": ins,
+    root = [n for n in names if n not in rec.inner]
+    mc = {"type": "recurrent_nn" if rec.sub_models else "nn", "layers": rec.layers, "parameters": rec.params,
+          "input_layer_names": ins, "output_layer_names": out_names, "evaluators": rec.evaluators,
+          "sub_models": [{"name": "root", "layer_names": root, "input_layer_names": ins,
                           "output_layer_names": out_names, "evaluator_names": [e["name"] for e in rec.evaluators],
-                          "is_recurrent_layer_group": False}]}
+                          "is_recurrent_layer_group": False}] + list(rec.sub_models)}
     return _proto2_clean(mc)
 
 

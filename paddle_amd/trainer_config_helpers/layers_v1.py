@@ -119,9 +119,26 @@ class _Projection:
         return self.fn(size if self.size is None else self.size)
 
 
+def _fluid_attr(a):
+    """A v1 ParameterAttribute as a fluid ParamAttr (a named one is shared by name)."""
+    if a is None or a is True:
+        return None
+    if a is False:
+        return False
+    if isinstance(a, fluid.ParamAttr):
+        return a
+    init = None
+    if getattr(a, "initial_std", None) is not None:
+        init = fluid.initializer.Normal(loc=getattr(a, "initial_mean", None) or 0.0, scale=a.initial_std)
+    return fluid.ParamAttr(name=getattr(a, "name", None), initializer=init)
+
+
 @_export
 def full_matrix_projection(input, size=0, param_attr=None):
-    return _Projection(lambda s: _L().fc(input=input, size=s, bias_attr=False), size or None, input, "fc")
+    pr = _Projection(lambda s: _L().fc(input=input, size=s, bias_attr=False, param_attr=_fluid_attr(param_attr)),
+                     size or None, input, "fc")
+    pr.v1_param_attr = param_attr  # a named weight is recorded (and shared) under its own name
+    return pr
 
 
 @_export
@@ -458,10 +475,16 @@ def gru_step_layer(input, output_mem, size=None, act=None, name=None, gate_act=N
                    param_attr=None, **kw):
     """One GRU step: input = projected gates [N, 3H], output_mem = h_{t-1}."""
     size = size or _size(output_mem)
+    blk = fluid.default_main_program().global_block()
+    before = {p.name for p in blk.all_parameters()}
     with guard():
         h, _, _ = _L().gru_unit(input=input, hidden=output_mem, size=3 * size,
                                 activation=_act.act_name(act) or "tanh",
-                                gate_activation=_act.act_name(gate_act) or "sigmoid")
+                                gate_activation=_act.act_name(gate_act) or "sigmoid",
+                                param_attr=_fluid_attr(param_attr), bias_attr=_fluid_attr(bias_attr))
+    for p in blk.all_parameters():  # the [1, 3 size] gate bias is a bias, not a second weight
+        if p.name not in before and len(p.shape) == 2 and p.shape[0] == 1:
+            p._v1_bias = True
     return _named(_sized(h, size), name)
 
 
