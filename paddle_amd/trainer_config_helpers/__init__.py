@@ -185,7 +185,9 @@ def fc_layer(input, size, act=None, name=None, param_attr=None, bias_attr=None, 
 
 
 def embedding_layer(input, size, name=None, param_attr=None, **kw):
-    return _l.embedding(input=input, size=size)
+    out = _l.embedding(input=input, size=size)
+    out.v2_size = size  # the v1 layer width (a table projection), whatever the id layout
+    return out
 
 
 def img_conv_layer(input, filter_size, num_filters, num_channels=None, stride=1, padding=0, act=None, groups=1,

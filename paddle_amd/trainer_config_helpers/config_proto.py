@@ -522,7 +522,7 @@ def _flat_inputs(fn, args, kw):
                                                                        "bias_attr", "layer_attr")]
     except (TypeError, ValueError):
         items = [(None, a) for a in args] + list(kw.items())
-    out = []
+    out, later = [], []
     for _, v in items:
         if isinstance(v, dict):  # **kw of the DSL function (e.g. a cost's weight layer)
             v = [w for k, w in v.items() if k not in ("name", "act", "size", "param_attr", "bias_attr", "layer_attr")]
@@ -530,10 +530,13 @@ def _flat_inputs(fn, args, kw):
             if _is_var(x):
                 out.append((x, None))
             elif getattr(x, "v1_operands", None):
-                out.extend((o, x) for o in x.v1_operands)  # an operator reads each operand layer
+                # an operator (config_parser.py MixedLayer): its first operand takes the
+                # operator's place among the inputs, the others follow all the inputs
+                out.append((x.v1_operands[0], x))
+                later.extend((o, x) for o in x.v1_operands[1:])
             elif _is_var(getattr(x, "input", None)):
                 out.append((x.input, x))  # a projection / operator
-    return out
+    return out + later
 
 
 def _attr_name(attr, i):
@@ -575,7 +578,8 @@ def _pattr(attr, i):
 
 
 def _param_dims(p):
-    return [int(d) for d in p.shape]
+    d = [int(v) for v in p.shape]
+    return [1] + d if len(d) == 1 else d  # a vector weight (dot_mul / scaling) is [1, n]
 
 
 def unwrap(x):
@@ -655,7 +659,8 @@ def _record(rec, fn_name, fn, args, kw, out, before, blk):
             size = _vsize(v)
         lc = {"name": name, "type": typ, "size": size, "active_type": _ACT.get(an, an or "")}
         by_pname = {p.name: p for p in blk.all_parameters()}
-        weights = [p for p in new if len(p.shape) >= 2 and not getattr(p, "_v1_bias", False)]
+        weights = [p for p in new if (len(p.shape) >= 2 or getattr(p, "_v1_weight", False))
+                   and not getattr(p, "_v1_bias", False)]
         wn = {p.name for p in weights}
         biases = [p for p in new if p.name not in wn]
         layer_inputs = []
@@ -677,7 +682,8 @@ def _record(rec, fn_name, fn, args, kw, out, before, blk):
             if pr is not None and fn_name == "concat_layer":
                 li["proj_conf"] = {"type": getattr(pr, "v1_type", "identity"), "name": f"_{base}.w{i}",
                                    "input_size": _vsize(x), "output_size": _vsize(x)}
-            if pr is not None and fn_name in ("mixed_layer", "embedding_layer") and getattr(pr, "v1_type", None):
+            if (pr is not None and fn_name in ("mixed_layer", "embedding_layer") and getattr(pr, "v1_type", None)
+                    and not getattr(pr, "v1_operands", None)):
                 li["proj_conf"] = {"type": _PROJ_TYPE.get(pr.v1_type, pr.v1_type), "name": f"_{base}.w{i}",
                                    "input_size": _vsize(x), "output_size": size}
             uname = unames[i]
@@ -691,11 +697,14 @@ def _record(rec, fn_name, fn, args, kw, out, before, blk):
                                        "initial_strategy": 0, "initial_smart": True})
                     _apply_pattr(rec.params[-1], _pattr(kw.get("param_attr"), i) if pr is None or
                              getattr(pr, "v1_param_attr", None) is None else pr.v1_param_attr)
-            elif wi < len(weights) and (pr is None or getattr(pr, "v1_type", None) not in _PARAMLESS):
+            elif wi < len(weights) and (pr is None or (getattr(pr, "v1_type", None) not in _PARAMLESS
+                                                      and not getattr(pr, "v1_operands", None))):
                 pname = f"_{name}.w{i}"
                 li["input_parameter_name"] = pname
                 rec.param_map[pname] = weights[wi].name
                 dims = _param_dims(weights[wi])
+                if pr is not None and getattr(pr, "v1_type", None) == "fc" and size and _vsize(x):
+                    dims = [int(_vsize(x)), int(size)]  # v1: [input width, layer width] whatever the id layout
                 wi += 1
                 rec.params.append({"name": pname, "size": int(_prod(dims)), "initial_mean": 0.0,
                                    "initial_std": 1.0 / max(dims[0], 1) ** 0.5, "dims": dims,
@@ -1458,9 +1467,62 @@ def _x_reversed(lc, a, kw, ins, rec, name):
     lc["reversed"] = bool(kw.get("reverse", False))
 
 
+def _conv_conf_of(cv, img_side):
+    """ConvConfig of a conv / convt projection or operator over a square image."""
+    fs, st, pd, c, g = cv["filter_size"], cv["stride"], cv["padding"], cv["channels"], cv.get("groups", 1)
+    fy, sy = cv.get("filter_size_y") or fs, cv.get("stride_y") or st
+    py = cv.get("padding_y") if cv.get("padding_y") is not None else pd
+    conf = {"filter_size": fs, "channels": c, "stride": st, "padding": pd, "groups": g, "caffe_mode": True,
+            "filter_size_y": fy, "padding_y": py, "stride_y": sy}
+    if cv.get("trans"):
+        out = (img_side - 1) * st + fs - 2 * pd
+        conf.update(filter_channels=cv["num_filters"] // g, output_x=img_side, img_size=out, output_y=img_side,
+                    img_size_y=(img_side - 1) * sy + fy - 2 * py)
+    else:
+        conf.update(filter_channels=c // g, output_x=_out_size(img_side, fs, pd, st, True), img_size=img_side,
+                    output_y=_out_size(img_side, fy, py, sy, True), img_size_y=img_side)
+    return conf
+
+
+def _conv_out_size(cv, conf):
+    return cv["num_filters"] * (conf["img_size"] * conf["img_size_y"] if cv.get("trans") else
+                                conf["output_x"] * conf["output_y"])
+
+
 def _x_mixed(lc, a, kw, ins, rec, name):
-    """MixedLayer operators (operator_confs): each names the positions of its operand
-    inputs; operand inputs carry no parameter."""
+    """MixedLayer terms beyond plain projections: operators (operator_confs naming the
+    positions of their operand inputs, which carry no parameter), context projections
+    (window / trainable padding rows) and conv / convt projections (ConvConfig, a
+    dimensionless filter parameter)."""
+    base = name.split("@")[0]
+    for i, (x, pr) in enumerate(ins):
+        li = lc["inputs"][i] if i < len(lc.get("inputs", [])) else None
+        if li is None or pr is None or getattr(pr, "v1_operands", None):
+            continue
+        if getattr(pr, "v1_context", None) is not None:
+            start, length = pr.v1_context
+            li["proj_conf"].update(context_start=start, context_length=length, trainable_padding=True)
+            pad = max(0, -start) + max(0, start + length - 1)
+            pn = li.get("input_parameter_name") or f"_{name}.w{i}"
+            li["input_parameter_name"] = pn
+            rec.params[:] = [p for p in rec.params if p["name"] != pn]
+            rec.params.append({"name": pn, "size": pad * _vsize(x), "initial_mean": 0.0, "initial_std": 0.0,
+                               "dims": [pad, _vsize(x)], "initial_strategy": 0, "initial_smart": False})
+        cv = getattr(pr, "v1_conv", None)
+        if cv is not None:
+            side = int(round((_vsize(x) // cv["channels"]) ** 0.5))
+            conf = _conv_conf_of(cv, side)
+            osz = _conv_out_size(cv, conf)
+            li["proj_conf"].update(type="convt" if cv.get("trans") else "conv", name=f"_{base}.w{i}",
+                                   output_size=osz, conv_conf=conf, num_filters=cv["num_filters"])
+            pn = li.get("input_parameter_name") or f"_{name}.w{i}"
+            li["input_parameter_name"] = pn
+            fs = cv["filter_size"]
+            n = cv["num_filters"] * (cv["channels"] // cv.get("groups", 1)) * fs * fs
+            rec.params[:] = [p for p in rec.params if p["name"] != pn]
+            rec.params.append({"name": pn, "size": n, "initial_mean": 0.0,
+                               "initial_std": (2.0 / (fs * fs * cv["channels"])) ** 0.5, "initial_strategy": 0,
+                               "initial_smart": False})
     ops, seen = [], {}
     for i, (x, pr) in enumerate(ins):
         if pr is None or not getattr(pr, "v1_operands", None):
@@ -1468,8 +1530,14 @@ def _x_mixed(lc, a, kw, ins, rec, name):
         if id(pr) not in seen:
             seen[id(pr)] = len(ops)
             kind, scale = getattr(pr, "v1_operator", ("dot_mul", 1.0))
-            ops.append({"type": kind, "input_indices": [], "input_sizes": [], "output_size": lc.get("size"),
-                        "dotmul_scale": scale})
+            oc = {"type": kind, "input_indices": [], "input_sizes": [], "output_size": lc.get("size")}
+            cv = getattr(pr, "v1_conv", None)
+            if cv is not None:
+                conf = _conv_conf_of(cv, int(round((_vsize(x) // cv["channels"]) ** 0.5)))
+                oc.update(output_size=_conv_out_size(cv, conf), conv_conf=conf, num_filters=cv["num_filters"])
+            else:
+                oc["dotmul_scale"] = scale
+            ops.append(oc)
         op = ops[seen[id(pr)]]
         op["input_indices"].append(i)
         op["input_sizes"].append(_vsize(x))
@@ -1562,7 +1630,15 @@ def _x_get_output(lc, a, kw, ins, rec, name):
         lc["inputs"][0]["input_layer_argument"] = arg
 
 
+def _x_embedding(lc, a, kw, ins, rec, name):
+    """embedding_layer: a mixed layer over one table projection."""
+    if lc.get("inputs"):
+        lc["inputs"][0]["proj_conf"] = {"type": "table", "name": f"_{name.split('@')[0]}.w0",
+                                        "input_size": _vsize(ins[0][0]), "output_size": lc["size"]}
+
+
 _EXTRA = {
+    "embedding_layer": _x_embedding,
     "lstm_step_layer": _x_lstm_step, "gru_step_layer": _x_gru_step, "gru_step_naive_layer": _x_gru_step,
     "get_output_layer": _x_get_output,
     "batch_norm_layer": _x_batch_norm, "nce_layer": _x_nce, "img_conv_layer": _x_conv,

@@ -181,6 +181,7 @@ def dotmul_projection(input, param_attr=None):
     def build(s):
         helper = LayerHelper("dotmul")
         w = helper.create_parameter(attr=helper.param_attr, shape=[_size(input)], dtype="float32")
+        w._v1_weight = True  # a [1, size] weight in the v1 record, not a bias
         return _L().elementwise_mul(input, w, axis=1)
     return _Projection(build, _size(input), input, "dot_mul")
 
@@ -190,6 +191,7 @@ def scaling_projection(input, param_attr=None):
     def build(s):
         helper = LayerHelper("scaling")
         w = helper.create_parameter(attr=helper.param_attr, shape=[1], dtype="float32")
+        w._v1_weight = True
         return _L().elementwise_mul(input, w)
     return _Projection(build, _size(input), input, "scaling")
 
@@ -224,18 +226,32 @@ def context_projection(input, context_len, context_start=None, padding_attr=Fals
         helper.append_op(type="sequence_conv", inputs={"X": [input], "Filter": [w]}, outputs={"Out": [out]},
                          attrs={"contextStride": 1, "contextStart": start, "contextLength": context_len})
         return out
-    return _Projection(build, context_len * _size(input), input, "context")
+    pr = _Projection(build, context_len * _size(input), input, "context")
+    pr.v1_context = (start, context_len)
+    return pr
 
 
 @_export
 def conv_projection(input, filter_size, num_filters, num_channels=None, stride=1, padding=0, groups=1,
-                    param_attr=None, **kw):
+                    param_attr=None, trans=False, **kw):
+    """A convolution (trans: transposed convolution) of an image layer as a mixed-layer
+    term, flattened to [N, C * H * W]."""
     from ..v2.layer import _as_image
 
     def build(s):
-        return _L().conv2d(_as_image(input, num_channels or 1), num_filters=num_filters, filter_size=filter_size,
-                           stride=stride, padding=padding, groups=groups, bias_attr=False)
-    return _Projection(build, None, input, "conv")
+        x = _as_image(input, num_channels or 1)
+        if trans:
+            out = _L().conv2d_transpose(x, num_filters=num_filters, filter_size=filter_size, stride=stride,
+                                        padding=padding, groups=groups, bias_attr=False)
+        else:
+            out = _L().conv2d(x, num_filters=num_filters, filter_size=filter_size, stride=stride, padding=padding,
+                              groups=groups, bias_attr=False)
+        n = _conv_flat(input, num_channels or 1, filter_size, stride, padding, num_filters, trans)
+        return _sized(_L().reshape(out, [-1, n]), n)
+    pr = _Projection(build, None, input, "convt" if trans else "conv")
+    pr.v1_conv = dict(filter_size=filter_size, num_filters=num_filters, channels=num_channels or 1, stride=stride,
+                      padding=padding, groups=groups, trans=trans)
+    return pr
 
 
 conv_operator = conv_projection
@@ -1229,13 +1245,32 @@ def conv_operator(img, filter, filter_size, num_filters, num_channels=None, stri
         with guard():
             c = num_channels or 1
             fy = filter_size_y or filter_size
-            x = _L().reshape(img, [-1, c, int(round((_size(img) // c) ** 0.5)), int(round((_size(img) // c) ** 0.5))])
-            w = _L().reshape(filter, [num_filters, c, fy, filter_size])
-            out = _op("conv2d", {"Input": [x], "Filter": [w]}, {"Output": "float32"},
-                      {"strides": [stride_y or stride, stride], "paddings": [padding_y or padding, padding],
-                       "dilations": [1, 1], "groups": 1})["Output"]
-            return _L().reshape(out, [-1, int(_prod_shape(out))]) if size else out
-    return _Projection(build, None, img, "conv_op")
+            side = int(round((_size(img) // c) ** 0.5))
+            x = _L().reshape(img, [-1, c, side, side])
+            attrs = {"strides": [stride_y or stride, stride], "paddings": [padding_y or padding, padding],
+                     "dilations": [1, 1], "groups": 1}
+            if trans:
+                w = _L().reshape(filter, [c, num_filters, fy, filter_size])
+                out = _op("conv2d_transpose", {"Input": [x], "Filter": [w]}, {"Output": "float32"}, attrs)["Output"]
+            else:
+                w = _L().reshape(filter, [num_filters, c, fy, filter_size])
+                out = _op("conv2d", {"Input": [x], "Filter": [w]}, {"Output": "float32"}, attrs)["Output"]
+            n = _conv_flat(img, c, filter_size, stride, padding, num_filters, trans)
+            return _sized(_L().reshape(out, [-1, n]), n)
+    op = _Projection(build, None, img, "convt_op" if trans else "conv_op")
+    op.v1_operands = [img, filter]  # the image and the filter layer (config_proto.py operator_confs)
+    op.v1_operator = ("convt" if trans else "conv", 1.0)
+    op.v1_conv = dict(filter_size=filter_size, num_filters=num_filters, channels=num_channels or 1, stride=stride,
+                      padding=padding, groups=1, trans=trans, filter_size_y=filter_size_y, stride_y=stride_y,
+                      padding_y=padding_y)
+    return op
+
+
+def _conv_flat(img, c, f, s, p, nf, trans):
+    """C * H * W of a (transposed) convolution of a square image layer."""
+    side = int(round((_size(img) // c) ** 0.5))
+    o = (side - 1) * s + f - 2 * p if trans else (side + 2 * p - f) // s + 1
+    return int(nf * o * o)
 
 
 def _prod_shape(v):
