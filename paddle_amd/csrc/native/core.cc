@@ -546,7 +546,30 @@ std::unordered_map<std::string, Kernel>& reg(bool device) {
 
 void register_kernel(const std::string& type, bool device, Kernel k) { reg(device)[type] = std::move(k); }
 
+// FLAGS_native_py_ops=a,b,...: these op types run on the embedder's fallback (the
+// Python op library) even where a C++ kernel exists -- for bisecting an engine
+// divergence one op family at a time (fluid/native_engine.py reads the same flag)
+static const std::set<std::string>& forced_fallback() {
+  static const std::set<std::string> s = [] {
+    std::set<std::string> out;
+    const char* e = getenv("FLAGS_native_py_ops");
+    std::string cur;
+    for (const char* c = e ? e : ""; ; ++c) {
+      if (*c == ',' || *c == 0) {
+        if (!cur.empty()) out.insert(cur);
+        cur.clear();
+        if (*c == 0) break;
+      } else {
+        cur += *c;
+      }
+    }
+    return out;
+  }();
+  return s;
+}
+
 const Kernel* find_kernel(const std::string& type, bool device) {
+  if (!forced_fallback().empty() && forced_fallback().count(type)) return nullptr;
   auto& r = reg(device);
   auto it = r.find(type);
   return it == r.end() ? nullptr : &it->second;
@@ -554,7 +577,8 @@ const Kernel* find_kernel(const std::string& type, bool device) {
 
 std::vector<std::string> registered_ops(bool device) {
   std::vector<std::string> out;
-  for (auto& kv : reg(device)) out.push_back(kv.first);
+  for (auto& kv : reg(device))
+    if (!forced_fallback().count(kv.first)) out.push_back(kv.first);
   return out;
 }
 
@@ -628,6 +652,7 @@ Executor::Executor(int device) {
   link_conv3d_kernels();
   link_loss_kernels();
   link_misc_kernels();
+  link_more_kernels();
 }
 
 Executor::~Executor() {
@@ -791,6 +816,224 @@ void Executor::RunWhileGrad(const ProgramDesc& prog, const OpDesc& op, Scope* sc
   }
 }
 
+namespace {
+const std::vector<std::string>& str_attr(const OpDesc& op, const char* name) {
+  static const std::vector<std::string> none;
+  auto it = op.attrs.find(name);
+  return it == op.attrs.end() ? none : it->second.strings;
+}
+
+// a [T, ...] tensor's row t as a fresh tensor on its own place
+Tensor time_row(const Tensor& x, int64_t t, void* stream) {
+  Tensor r;
+  std::vector<int64_t> d(x.dims.begin() + 1, x.dims.end());
+  r.alloc(x.dtype, d, x.device);
+  const size_t rb = r.nbytes();
+  device_copy(r.raw(), r.device, static_cast<const char*>(x.raw()) + (size_t)t * rb, x.device, rb, stream);
+  return r;
+}
+
+// dst[t] = src, allocating dst as [T] + src.dims (zero-filled) on the first write
+void put_row(Tensor& dst, int64_t T, int64_t t, const Tensor& src, void* stream) {
+  std::vector<int64_t> d{T};
+  d.insert(d.end(), src.dims.begin(), src.dims.end());
+  if (!dst.initialized() || dst.dims != d || dst.device != src.device || dst.dtype != src.dtype) {
+    dst = Tensor();
+    dst.alloc(src.dtype, d, src.device);
+    if (dst.device >= 0) device_fill(stream, dst.raw(), dst.dtype, dst.numel(), 0.0);
+    else memset(dst.raw(), 0, dst.nbytes());
+  }
+  const size_t rb = src.nbytes();
+  device_copy(static_cast<char*>(dst.raw()) + (size_t)t * rb, dst.device, src.raw(), src.device, rb, stream);
+}
+
+Tensor zeros_like_f32(const Tensor& x, void* stream) {
+  Tensor z;
+  z.alloc(DT::FP32, x.dims, x.device);
+  if (z.device >= 0) device_fill(stream, z.raw(), DT::FP32, z.numel(), 0.0);
+  else std::fill_n(z.data<float>(), z.numel(), 0.f);
+  return z;
+}
+}  // namespace
+
+// recurrent_op.cc RecurrentOp::RunImpl (StaticRNN): step t of the time-major inputs
+// runs the sub-block in its own child scope, where the block-local variables named
+// like the outer `inputs` hold row t, the ex-states hold the previous step's states
+// (initial_states at the first step) and the `outputs` rows are stacked back into
+// the outer [T, ...] outputs.  reverse: t runs T-1 .. 0.  Training keeps the step
+// scopes (StepScopes output) for recurrent_grad.
+void Executor::RunRecurrent(const ProgramDesc& prog, const OpDesc& op, Scope* scope) {
+  const int sb = (int)op.GetInt("sub_block", -1);
+  PA_CHECK(sb >= 0 && sb < (int)prog.blocks.size(), "recurrent: bad sub_block %d", sb);
+  const BlockDesc& blk = prog.Block(sb);
+  const auto& xs = op.Inputs("inputs");
+  const auto& inits = op.Inputs("initial_states");
+  const auto& outs = op.Outputs("outputs");
+  const auto& ex = str_attr(op, "ex_states");
+  const auto& st = str_attr(op, "states");
+  PA_CHECK(ex.size() == st.size() && ex.size() == inits.size(), "recurrent: %zu ex_states, %zu states, %zu initial",
+           ex.size(), st.size(), inits.size());
+  PA_CHECK(!xs.empty(), "recurrent: no inputs");
+  const bool reverse = op.GetBool("reverse", false);
+  Variable* x0 = scope->Find(xs[0]);
+  PA_CHECK(x0 && x0->tensor.initialized() && !x0->tensor.dims.empty(), "recurrent: input %s is empty", xs[0].c_str());
+  const int64_t T = x0->tensor.dims[0];
+  const std::string ss = op.Output("step_scopes");
+  const bool keep = !ss.empty() && !ctx_.is_test && !op.GetBool("is_test", false);
+  Variable* sv = nullptr;
+  if (keep) {
+    sv = scope->Find(ss);
+    if (!sv) sv = scope->Var(ss);
+    sv->kind = VK_STEP_SCOPES;
+    for (Scope* s : sv->steps) sv->steps_owner->DropKid(s);
+    sv->steps.clear();
+    sv->steps_owner = scope;
+  }
+  std::vector<Tensor> prev(ex.size());
+  for (size_t i = 0; i < inits.size(); ++i) {
+    Variable* v = scope->Find(inits[i]);
+    PA_CHECK(v && v->tensor.initialized(), "recurrent: initial state %s is empty", inits[i].c_str());
+    prev[i] = v->tensor;
+  }
+  std::vector<Tensor> stacked(outs.size());
+  for (int64_t k = 0; k < T; ++k) {
+    const int64_t t = reverse ? T - 1 - k : k;
+    Scope& s = scope->NewScope();
+    for (const VarDesc& v : blk.vars)
+      if (!v.persistable) s.Var(v.name)->kind = v.type;
+    for (auto& n : xs) {
+      Variable* x = scope->Find(n);
+      PA_CHECK(x && x->tensor.initialized() && x->tensor.dims.size() >= 1 && x->tensor.dims[0] == T,
+               "recurrent: input %s is not [%lld, ...]", n.c_str(), (long long)T);
+      s.Var(n)->tensor = time_row(x->tensor, t, ctx_.stream);
+    }
+    for (size_t i = 0; i < ex.size(); ++i) s.Var(ex[i])->tensor = prev[i];
+    RunBlock(prog, blk, &s);
+    for (size_t i = 0; i < st.size(); ++i) {
+      Variable* v = s.FindLocal(st[i]);
+      PA_CHECK(v && v->tensor.initialized(), "recurrent: state %s not produced at step %lld", st[i].c_str(),
+               (long long)t);
+      prev[i] = v->tensor;
+    }
+    for (size_t j = 0; j < outs.size(); ++j) {
+      Variable* v = s.FindLocal(outs[j]);
+      PA_CHECK(v && v->tensor.initialized(), "recurrent: output %s not produced at step %lld", outs[j].c_str(),
+               (long long)t);
+      put_row(stacked[j], T, t, v->tensor, ctx_.stream);
+    }
+    if (keep) sv->steps.push_back(&s);
+    else scope->DropKid(&s);
+  }
+  for (size_t j = 0; j < outs.size(); ++j) {
+    Variable* o = scope->Find(outs[j]);
+    if (!o) o = scope->Var(outs[j]);
+    o->kind = VK_LOD_TENSOR;
+    o->tensor = stacked[j];
+  }
+}
+
+// recurrent_op.cc RecurrentGradOp::RunImpl: the grad block runs in a child of every
+// kept step scope, last step first.  Per step the block-local output gradients hold
+// row t of the outer ones, each state's gradient additionally takes the ex-state
+// gradient the later step produced (the link the forward made between them); row t
+// of every input gradient is copied out, parameter gradients are summed over the
+// steps, and the first step's ex-state gradients are the initial-state gradients.
+void Executor::RunRecurrentGrad(const ProgramDesc& prog, const OpDesc& op, Scope* scope) {
+  const int sb = (int)op.GetInt("sub_block", -1);
+  PA_CHECK(sb >= 0 && sb < (int)prog.blocks.size(), "recurrent_grad: bad sub_block %d", sb);
+  const BlockDesc& blk = prog.Block(sb);
+  const auto& xs = op.Inputs("inputs");
+  const auto& inits = op.Inputs("initial_states");
+  const auto& params = op.Inputs("parameters");
+  const auto& outs = op.Inputs("outputs");
+  const auto& ogs = op.Inputs("outputs@GRAD");
+  const auto& xgs = op.Outputs("inputs@GRAD");
+  const auto& igs = op.Outputs("initial_states@GRAD");
+  const auto& pgs = op.Outputs("parameters@GRAD");
+  const auto& ex = str_attr(op, "ex_states");
+  const auto& st = str_attr(op, "states");
+  const bool reverse = op.GetBool("reverse", false);
+  Variable* sv = scope->Find(op.Input("step_scopes"));
+  PA_CHECK(sv != nullptr, "recurrent_grad: step scopes %s not found", op.Input("step_scopes").c_str());
+  const int64_t T = (int64_t)sv->steps.size();
+  auto g = [](const std::string& n) { return n + "@GRAD"; };
+  auto live = [](const std::vector<std::string>& v, size_t i) { return i < v.size() && v[i] != "@EMPTY@" && !v[i].empty(); };
+  // outer output gradients by output position (the slot lists only differentiable ones)
+  std::map<std::string, Tensor> og_outer;
+  for (auto& n : ogs) {
+    Variable* v = scope->Find(n);
+    if (v && v->tensor.initialized()) og_outer[n] = v->tensor;
+  }
+  std::vector<Tensor> carry(ex.size()), xg_acc(xs.size());
+  std::map<std::string, Tensor> pacc;
+  for (int64_t k = T; k-- > 0;) {
+    const int64_t t = reverse ? T - 1 - k : k;
+    Scope* s = sv->steps[k];
+    Scope& gs = s->NewScope();
+    for (const VarDesc& v : blk.vars)
+      if (!v.persistable) gs.Var(v.name)->kind = v.type;
+    // <name>@GRAD@EXT of every step output / state: row t of its outer gradient plus
+    // the later step's ex-state gradient, zeros when neither exists (the grad block
+    // adds it to its own contributions: fluid/backward.py _recurrent_grad_descs)
+    std::vector<std::string> linked(st.begin(), st.end());
+    for (auto& o : outs)
+      if (std::find(linked.begin(), linked.end(), o) == linked.end()) linked.push_back(o);
+    for (auto& n : linked) {
+      Tensor ext;
+      auto it = og_outer.find(g(n));
+      if (it != og_outer.end()) ext = time_row(it->second, t, ctx_.stream);
+      auto si = std::find(st.begin(), st.end(), n);
+      if (si != st.end() && carry[si - st.begin()].initialized())
+        accumulate_into(ext, carry[si - st.begin()], ctx_.stream);  // += or a private copy
+      if (!ext.initialized()) {
+        Variable* fv = s->FindLocal(n);
+        PA_CHECK(fv && fv->tensor.initialized(), "recurrent_grad: step variable %s not kept", n.c_str());
+        ext = zeros_like_f32(fv->tensor, ctx_.stream);
+      }
+      gs.Var(g(n) + "@EXT")->tensor = ext;
+    }
+    RunBlock(prog, blk, &gs);
+    for (size_t j = 0; j < xs.size(); ++j) {
+      if (!live(xgs, j)) continue;
+      Variable* v = gs.FindLocal(g(xs[j]));
+      Tensor r = v && v->tensor.initialized() ? v->tensor : Tensor();
+      if (!r.initialized()) {
+        Variable* x = scope->Find(xs[j]);
+        r = zeros_like_f32(time_row(x->tensor, t, ctx_.stream), ctx_.stream);
+      }
+      put_row(xg_acc[j], T, t, r, ctx_.stream);
+    }
+    for (size_t j = 0; j < params.size(); ++j) {
+      if (!live(pgs, j)) continue;
+      Variable* v = gs.FindLocal(g(params[j]));
+      if (v && v->tensor.initialized()) accumulate_into(pacc[pgs[j]], v->tensor, ctx_.stream);
+    }
+    for (size_t i = 0; i < ex.size(); ++i) {
+      Variable* v = gs.FindLocal(g(ex[i]));
+      carry[i] = Tensor();
+      if (v && v->tensor.initialized()) accumulate_into(carry[i], v->tensor, ctx_.stream);
+    }
+    s->DropKid(&gs);
+  }
+  auto set_out = [&](const std::string& name, const Tensor& val, const std::string& like) {
+    Variable* o = scope->Find(name);
+    if (!o) o = scope->Var(name);
+    o->kind = VK_LOD_TENSOR;
+    if (val.initialized()) {
+      o->tensor = val;
+    } else {
+      Variable* x = scope->Find(like);
+      if (x && x->tensor.initialized() && x->tensor.dtype == DT::FP32) o->tensor = zeros_like_f32(x->tensor, ctx_.stream);
+    }
+  };
+  for (size_t j = 0; j < xs.size(); ++j)
+    if (live(xgs, j)) set_out(xgs[j], xg_acc[j], xs[j]);
+  for (size_t j = 0; j < params.size(); ++j)
+    if (live(pgs, j)) set_out(pgs[j], pacc.count(pgs[j]) ? pacc[pgs[j]] : Tensor(), params[j]);
+  for (size_t i = 0; i < inits.size(); ++i)
+    if (live(igs, i)) set_out(igs[i], i < carry.size() ? carry[i] : Tensor(), inits[i]);
+}
+
 // conditional_block_op.cc: run the sub-block once when the condition holds
 // (is_scalar_condition: Cond[0] != 0; else: every Input is non-empty).
 void Executor::RunConditionalBlock(const ProgramDesc& prog, const OpDesc& op, Scope* scope) {
@@ -903,6 +1146,48 @@ void Executor::RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* 
       }
     return n > 0;
   };
+  // a loop-control op mixing host and device SCALARS (a force_cpu counter against a
+  // device-filled bound, a host condition and-ed with a device is_empty flag): its
+  // kernel place is the host (the reference's compare / logical ops with force_cpu
+  // and their data transform), so the device scalars are read over and the result
+  // stays on the host where the loop reads it
+  auto host_scalar_mix = [&](const OpDesc& op) {
+    int host = 0, n = 0;
+    for (auto& slot : op.inputs)
+      for (auto& name : slot.second) {
+        Variable* v = scope->Find(name);
+        if (!v || v->kind != VK_LOD_TENSOR || !v->tensor.initialized() || v->tensor.numel() > 1) return false;
+        host += v->tensor.device < 0;
+        ++n;
+      }
+    return n > 0 && host > 0;
+  };
+  auto run_host_scalars = [&](const OpDesc& op, const Kernel* k) {
+    Scope& tmp = scope->NewScope();
+    for (auto& slot : op.inputs)
+      for (auto& name : slot.second) {
+        Variable* v = scope->Find(name);
+        if (v->tensor.device >= 0) {
+          Variable* h = tmp.Var(name);
+          h->kind = v->kind;
+          h->tensor = v->tensor.to(-1, ctx_.stream);
+        }
+      }
+    device_stream_sync(ctx_.stream);
+    ExecContext hctx = ctx_;
+    hctx.device = -1;
+    (*k)(OpRun{op, tmp, hctx});
+    // an output that shadows a copied input (in place) moves out as a host tensor
+    for (auto& slot : op.outputs)
+      for (auto& name : slot.second) {
+        Variable* h = tmp.FindLocal(name);
+        if (!h || !h->tensor.initialized()) continue;
+        Variable* v = scope->Find(name);
+        if (!v) v = scope->Var(name);
+        v->tensor = h->tensor;
+      }
+    scope->DropKid(&tmp);
+  };
   // the reference's InferShape ShareLoD("X", "Out") default (the Python op library's
   // register_op share_lod=True): an output with no LoD and as many rows as the first
   // LoD-carrying input takes that input's LoD; the ops registered share_lod=False there
@@ -913,7 +1198,7 @@ void Executor::RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* 
         "conditional_block_grad", "feed", "fetch", "fusion_seqexpand_concat_fc", "go", "gru_unit",
         "hierarchical_sigmoid", "linear_chain_crf", "lod_rank_table", "lod_reset", "lod_tensor_to_array",
         "lod_tensor_to_array_grad", "lstm_unit", "merge_lod_tensor", "nce", "parallel_do", "read",
-        "read_from_array", "read_from_array_grad", "recurrent", "reorder_lod_tensor_by_rank",
+        "read_from_array", "read_from_array_grad", "recurrent", "recurrent_grad", "reorder_lod_tensor_by_rank",
         "reorder_lod_tensor_by_rank_grad", "select", "sequence_concat", "sequence_erase", "sequence_expand",
         "sequence_expand_as", "sequence_pad", "sequence_pool", "sequence_reshape", "sequence_scatter",
         "sequence_slice", "sequence_unpad", "shrink_rnn_memory", "shrink_rnn_memory_grad", "split_lod_tensor",
@@ -1008,9 +1293,29 @@ void Executor::RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* 
         }
       }
   };
+  // an op's outputs start without LoD (the reference's InferShape ShareLoD runs every
+  // time): temporaries keep their buffers from run to run, and a LoD left over from
+  // the previous batch must not survive into an output whose kernel does not set one
+  // (share_lod fills it from the inputs afterwards).  In-place outputs keep theirs.
+  auto clear_out_lod = [&](const OpDesc& op) {
+    for (auto& slot : op.outputs)
+      for (auto& n : slot.second) {
+        if (n.empty() || n == "@EMPTY@") continue;
+        bool inplace = false;
+        for (auto& is : op.inputs)
+          for (auto& m : is.second) inplace = inplace || m == n;
+        if (inplace) continue;
+        Variable* v = scope->Find(n);
+        if (v && v->kind == VK_LOD_TENSOR && !v->tensor.lod.empty()) v->tensor.lod.clear();
+      }
+  };
   int op_idx = -1;
   for (const OpDesc& op : block.ops) {
     ++op_idx;
+    if (op.type != "while" && op.type != "conditional_block" && op.type != "while_grad" &&
+        op.type != "conditional_block_grad" && op.type != "recurrent" && op.type != "recurrent_grad" &&
+        op.type != "feed" && op.type != "fetch")
+      clear_out_lod(op);
     if (op.type == "while") {
       timed(op, [&] { RunWhile(prog, op, scope); });
       continue;
@@ -1027,12 +1332,26 @@ void Executor::RunBlock(const ProgramDesc& prog, const BlockDesc& block, Scope* 
       timed(op, [&] { RunConditionalBlockGrad(prog, op, scope); });
       continue;
     }
+    if (op.type == "recurrent") {
+      timed(op, [&] { RunRecurrent(prog, op, scope); });
+      continue;
+    }
+    if (op.type == "recurrent_grad") {
+      timed(op, [&] { RunRecurrentGrad(prog, op, scope); });
+      continue;
+    }
     // loop counters / bounds that live on the host (fill_constant force_cpu,
     // max_sequence_len, lod_array_length): the host kernel IS their kernel on a device
     // place too (the reference's CPU-pinned control tensors), no round trip
     if (dev && host_scalar.count(op.type) && host_inputs(op)) {
       if (const Kernel* hk = find_kernel(op.type, false)) {
         timed(op, [&] { (*hk)(OpRun{op, *scope, ctx_}); });
+        continue;
+      }
+    }
+    if (dev && host_scalar.count(op.type) && host_scalar_mix(op)) {
+      if (const Kernel* hk = find_kernel(op.type, false)) {
+        timed(op, [&] { run_host_scalars(op, hk); });
         continue;
       }
     }

@@ -248,6 +248,7 @@ void link_rnn_unit_kernels();
 void link_conv3d_kernels();
 void link_loss_kernels();
 void link_misc_kernels();
+void link_more_kernels();
 
 // ---------------------------------------------------------------- executor
 class Executor {
@@ -284,6 +285,10 @@ class Executor {
   // while_op.cc WhileGradOp: the grad block once per kept step scope, last step first
   void RunWhileGrad(const ProgramDesc& prog, const OpDesc& op, Scope* scope);
   void RunConditionalBlockGrad(const ProgramDesc& prog, const OpDesc& op, Scope* scope);
+  // recurrent_op.cc RecurrentOp / RecurrentGradOp (StaticRNN): one kept step scope
+  // per time step, states linked step to step
+  void RunRecurrent(const ProgramDesc& prog, const OpDesc& op, Scope* scope);
+  void RunRecurrentGrad(const ProgramDesc& prog, const OpDesc& op, Scope* scope);
 
  private:
   bool ReadBool(const Tensor& t);

@@ -1092,8 +1092,30 @@ void* upload_host(const OpRun& r, const char* name, const void* src, size_t byte
   if (bytes == 0) return d;
   std::lock_guard<std::mutex> lk(mu);
   PinnedSlot& sl = slots[std::string(name) + "@" + std::to_string(D(r))];
-  if (sl.ev) HIPCHK(hipEventSynchronize(sl.ev));
-  else HIPCHK(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIPCHK(hipStreamIsCapturing(S(r), &cs));
+  if (cs != hipStreamCaptureStatusNone) {
+    // inside a HIP graph capture the copy's source must stay valid for every replay:
+    // a dedicated pinned buffer, never reused or freed (the slot's event is not touched)
+    static std::vector<void*> graph_bufs;
+    void* h = nullptr;
+    HIPCHK(hipHostMalloc(&h, bytes, hipHostMallocDefault));
+    memcpy(h, src, bytes);
+    HIPCHK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, S(r)));
+    graph_bufs.push_back(h);
+    return d;
+  }
+  if (sl.ev) {
+    if (hipEventSynchronize(sl.ev) != hipSuccess) {
+      // an event that cannot be waited on (recorded into a since-abandoned capture):
+      // retire the slot -- its buffer may still be referenced, so it is not freed
+      (void)hipGetLastError();
+      sl.ev = nullptr;
+      sl.host = nullptr;
+      sl.cap = 0;
+    }
+  }
+  if (!sl.ev) HIPCHK(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
   if (sl.cap < bytes) {
     if (sl.host) HIPCHK(hipHostFree(sl.host));
     sl.cap = std::max(bytes, (size_t)4096);

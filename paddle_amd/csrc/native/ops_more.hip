@@ -1,0 +1,1602 @@
+// More pointwise losses, shape ops and optimizers of the native executor, host AND
+// device from one source (any_place.h): hinge_loss (+grad), modified_huber_loss
+// (+grad), rank_loss (+grad), margin_rank_loss (+grad), l1_norm (+grad), reverse
+// (+grad), pad (+grad), pad_constant_like (+grad), prelu (+grad), iou_similarity,
+// arg_min, fill, assign_value, proximal_gd, proximal_adagrad, matmul_grad, cos_sim
+// (+grad), multiplex (+grad), crop (+grad), norm (+grad), conv_shift (+grad),
+// bilinear_tensor_product (+grad), maxout (+grad), fake_quantize_abs_max,
+// fake_dequantize_max_abs (+grad), rnn_memory_helper (+grad), lod_reset_grad,
+// scatter_grad, polygon_box_transform, argsort, row_conv (+grad), lrn (+grad).
+//
+// Semantics: reference operators/{hinge_loss,modified_huber_loss,rank_loss,
+// margin_rank_loss,l1_norm,reverse,pad,pad_constant_like,prelu,iou_similarity,
+// arg_min_max_base,fill,assign_value,proximal_gd,proximal_adagrad}_op.h; the Python
+// kernels of operators/{nn,math,tensor,detection,optimizer}_ops.py compute the same
+// functions and the auto-VJP grad ops their derivatives (slots: the forward inputs,
+// outputs and Out@GRAD; <input>@GRAD out).  fp32 data (other dtypes decline to the
+// embedder's kernel); index tensors int64 / int32.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include <vector>
+
+#include "any_place.h"
+
+namespace pa {
+namespace {
+
+using any::f32;
+using Dims = std::vector<int64_t>;
+
+__host__ __device__ inline void acc_add(float* p, float v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  atomicAdd(p, v);
+#else
+  *p += v;
+#endif
+}
+
+int place_of(const OpRun& r) { return r.ctx.device >= 0 ? r.ctx.device : -1; }
+bool on_dev(const OpRun& r) { return r.ctx.device >= 0; }
+
+float* new_like(const OpRun& r, const Tensor& like, Tensor* keep) {
+  float* p = keep->alloc<float>(like.dims, place_of(r));
+  keep->lod = like.lod;
+  return p;
+}
+
+// an optional gradient output: its tensor when the grad op asks for it, else null
+float* grad_out(const OpRun& r, const char* slot, const Tensor& like, Tensor* keep) {
+  if (r.op.Outputs(slot).empty() || !r.out_var(slot)) return nullptr;
+  return new_like(r, like, keep);
+}
+
+void set(const OpRun& r, const char* slot, const Tensor& t) {
+  if (Tensor* o = r.out(slot)) *o = t;
+}
+
+// ---------------------------------------------------------------- pointwise losses
+struct Hinge {
+  const float *x, *y;
+  float* o;
+  __host__ __device__ void operator()(int64_t i) const { o[i] = fmaxf(0.f, 1.f - x[i] * (2.f * y[i] - 1.f)); }
+};
+struct HingeGrad {
+  const float *x, *y, *g;
+  float* dx;
+  __host__ __device__ void operator()(int64_t i) const {
+    const float s = 2.f * y[i] - 1.f;
+    dx[i] = x[i] * s < 1.f ? -s * g[i] : 0.f;
+  }
+};
+
+void k_hinge(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("Logits");
+  Tensor& y = r.in("Labels");
+  if (x.numel() != y.numel()) throw Decline{};
+  Tensor o;
+  any::run(r, dev, x.numel(), Hinge{f32(x, dev), f32(y, dev), new_like(r, x, &o)});
+  set(r, "Loss", o);
+}
+
+void k_hinge_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("Logits");
+  Tensor d;
+  float* dx = grad_out(r, "Logits@GRAD", x, &d);
+  if (dx) any::run(r, dev, x.numel(), HingeGrad{f32(x, dev), f32(r.in("Labels"), dev), f32(r.in("Loss@GRAD"), dev), dx});
+  if (dx) set(r, "Logits@GRAD", d);
+}
+
+struct ModHuber {
+  const float *x, *y;
+  float *z, *o;
+  __host__ __device__ void operator()(int64_t i) const {
+    const float v = x[i] * (2.f * y[i] - 1.f);
+    z[i] = v;
+    o[i] = v < -1.f ? -4.f * v : (v < 1.f ? (1.f - v) * (1.f - v) : 0.f);
+  }
+};
+struct ModHuberGrad {
+  const float *y, *z, *g;
+  float* dx;
+  __host__ __device__ void operator()(int64_t i) const {
+    const float v = z[i], s = 2.f * y[i] - 1.f;
+    dx[i] = g[i] * (v < -1.f ? -4.f * s : (v < 1.f ? -2.f * (1.f - v) * s : 0.f));
+  }
+};
+
+void k_mod_huber(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor& y = r.in("Y");
+  if (x.numel() != y.numel()) throw Decline{};
+  Tensor z, o;
+  any::run(r, dev, x.numel(), ModHuber{f32(x, dev), f32(y, dev), new_like(r, x, &z), new_like(r, x, &o)});
+  set(r, "IntermediateVal", z);
+  set(r, "Out", o);
+}
+
+void k_mod_huber_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor d;
+  float* dx = grad_out(r, "X@GRAD", x, &d);
+  if (!dx) return;
+  any::run(r, dev, x.numel(),
+           ModHuberGrad{f32(r.in("Y"), dev), f32(r.in("IntermediateVal"), dev), f32(r.in("Out@GRAD"), dev), dx});
+  set(r, "X@GRAD", d);
+}
+
+// rank_loss: log(1 + e^(l - r)) - label (l - r)
+struct RankLoss {
+  const float *lab, *l, *rt;
+  float* o;
+  __host__ __device__ void operator()(int64_t i) const {
+    const float d = l[i] - rt[i];
+    o[i] = log1pf(expf(d)) - lab[i] * d;
+  }
+};
+struct RankLossGrad {
+  const float *lab, *l, *rt, *g;
+  float *dl, *dr;
+  __host__ __device__ void operator()(int64_t i) const {
+    const float d = l[i] - rt[i];
+    const float s = 1.f / (1.f + expf(-d)) - lab[i];
+    if (dl) dl[i] = g[i] * s;
+    if (dr) dr[i] = -g[i] * s;
+  }
+};
+
+struct RankLabelGrad {
+  const float *l, *rt, *g;
+  float* o;
+  __host__ __device__ void operator()(int64_t i) const { o[i] = -(l[i] - rt[i]) * g[i]; }
+};
+
+void k_rank_loss(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& l = r.in("Left");
+  Tensor o;
+  if (r.in("Right").numel() != l.numel() || r.in("Label").numel() != l.numel()) throw Decline{};
+  any::run(r, dev, l.numel(), RankLoss{f32(r.in("Label"), dev), f32(l, dev), f32(r.in("Right"), dev), new_like(r, l, &o)});
+  set(r, "Out", o);
+}
+
+void k_rank_loss_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& l = r.in("Left");
+  Tensor dL, dR, dLab;
+  float* dl = grad_out(r, "Left@GRAD", l, &dL);
+  float* dr = grad_out(r, "Right@GRAD", r.in("Right"), &dR);
+  float* dlab = grad_out(r, "Label@GRAD", r.in("Label"), &dLab);
+  any::run(r, dev, l.numel(),
+           RankLossGrad{f32(r.in("Label"), dev), f32(l, dev), f32(r.in("Right"), dev), f32(r.in("Out@GRAD"), dev), dl, dr});
+  if (dlab) {  // d/dlabel = -(l - r) g
+    any::run(r, dev, l.numel(), RankLabelGrad{f32(l, dev), f32(r.in("Right"), dev), f32(r.in("Out@GRAD"), dev), dlab});
+    set(r, "Label@GRAD", dLab);
+  }
+  if (dl) set(r, "Left@GRAD", dL);
+  if (dr) set(r, "Right@GRAD", dR);
+}
+
+// margin_rank_loss: relu(-label (x1 - x2) + margin); Activated = 1 where positive
+struct MarginRank {
+  const float *x1, *x2, *lab;
+  float *o, *act;
+  float margin;
+  __host__ __device__ void operator()(int64_t i) const {
+    const float v = -lab[i] * (x1[i] - x2[i]) + margin;
+    o[i] = fmaxf(v, 0.f);
+    act[i] = v > 0.f ? 1.f : 0.f;
+  }
+};
+struct MarginRankGrad {
+  const float *x1, *x2, *lab, *g;
+  float *d1, *d2, *dlab;
+  float margin;
+  __host__ __device__ void operator()(int64_t i) const {
+    const float v = -lab[i] * (x1[i] - x2[i]) + margin;
+    const float a = v > 0.f ? g[i] : 0.f;
+    if (d1) d1[i] = -lab[i] * a;
+    if (d2) d2[i] = lab[i] * a;
+    if (dlab) dlab[i] = -(x1[i] - x2[i]) * a;
+  }
+};
+
+void k_margin_rank(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x1 = r.in("X1");
+  if (r.in("X2").numel() != x1.numel() || r.in("Label").numel() != x1.numel()) throw Decline{};
+  Tensor o, a;
+  any::run(r, dev, x1.numel(),
+           MarginRank{f32(x1, dev), f32(r.in("X2"), dev), f32(r.in("Label"), dev), new_like(r, x1, &o),
+                      new_like(r, x1, &a), r.op.GetFloat("margin", 0.f)});
+  set(r, "Out", o);
+  set(r, "Activated", a);
+}
+
+void k_margin_rank_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x1 = r.in("X1");
+  Tensor d1, d2, dl;
+  float* p1 = grad_out(r, "X1@GRAD", x1, &d1);
+  float* p2 = grad_out(r, "X2@GRAD", r.in("X2"), &d2);
+  float* pl = grad_out(r, "Label@GRAD", r.in("Label"), &dl);
+  any::run(r, dev, x1.numel(),
+           MarginRankGrad{f32(x1, dev), f32(r.in("X2"), dev), f32(r.in("Label"), dev), f32(r.in("Out@GRAD"), dev), p1, p2,
+                          pl, r.op.GetFloat("margin", 0.f)});
+  if (p1) set(r, "X1@GRAD", d1);
+  if (p2) set(r, "X2@GRAD", d2);
+  if (pl) set(r, "Label@GRAD", dl);
+}
+
+// ---------------------------------------------------------------- l1_norm
+struct AbsSumChunk {
+  const float* x;
+  float* out;
+  int64_t n, chunk;
+  __host__ __device__ void operator()(int64_t c) const {
+    float s = 0.f;
+    const int64_t a = c * chunk, b = a + chunk < n ? a + chunk : n;
+    for (int64_t i = a; i < b; ++i) s += fabsf(x[i]);
+    acc_add(out, s);
+  }
+};
+
+void k_l1_norm(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor o;
+  float* op = o.alloc<float>({1}, place_of(r));
+  any::zero(r, dev, op, 1);
+  const int64_t n = x.numel(), chunk = 4096, nc = (n + chunk - 1) / chunk;
+  // host: chunks in order on one thread (deterministic sum); device: one atomic per chunk
+  if (dev) any::run(r, dev, nc, AbsSumChunk{f32(x, dev), op, n, chunk});
+  else AbsSumChunk{f32(x, dev), op, n, n > 0 ? n : 1}(0);
+  set(r, "Out", o);
+}
+
+struct L1Grad {
+  const float *x, *g;
+  float* dx;
+  __host__ __device__ void operator()(int64_t i) const {
+    dx[i] = g[0] * (x[i] > 0.f ? 1.f : (x[i] < 0.f ? -1.f : 0.f));
+  }
+};
+
+void k_l1_norm_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor d;
+  float* dx = grad_out(r, "X@GRAD", x, &d);
+  if (!dx) return;
+  any::run(r, dev, x.numel(), L1Grad{f32(x, dev), f32(r.in("Out@GRAD"), dev), dx});
+  set(r, "X@GRAD", d);
+}
+
+// ---------------------------------------------------------------- N-d index maps
+constexpr int kMaxD = 8;
+struct Shape {
+  int nd;
+  int64_t d[kMaxD];
+};
+
+Shape shape_of(const Dims& d) {
+  PA_CHECK((int)d.size() <= kMaxD, "tensor rank %d above %d", (int)d.size(), kMaxD);
+  Shape s{(int)d.size(), {}};
+  for (int i = 0; i < s.nd; ++i) s.d[i] = d[i];
+  return s;
+}
+
+// out[o] = in[i] with, per dim, i_k = flip_k ? D_k - 1 - o_k : o_k - off_k; outside the
+// input: `fill` (pad) -- one functor for reverse, pad, pad_constant_like, their grads
+struct Remap {
+  const float* in;
+  float* out;
+  Shape os, is;
+  int64_t off[kMaxD];
+  int flip[kMaxD];
+  float fill;
+  __host__ __device__ void operator()(int64_t o) const {
+    int64_t rem = o, idx = 0, stride = 1;
+    bool inside = true;
+    int64_t coord[kMaxD];
+    for (int k = os.nd - 1; k >= 0; --k) {
+      coord[k] = rem % os.d[k];
+      rem /= os.d[k];
+    }
+    for (int k = os.nd - 1; k >= 0; --k) {
+      const int64_t c = flip[k] ? is.d[k] - 1 - coord[k] : coord[k] - off[k];
+      if (c < 0 || c >= is.d[k]) inside = false;
+      idx += c * stride;
+      stride *= is.d[k];
+    }
+    out[o] = inside ? in[idx] : fill;
+  }
+};
+
+void remap(const OpRun& r, const Tensor& in, const Dims& odims, const std::vector<int64_t>& off,
+           const std::vector<int>& flip, float fill, Tensor* out) {
+  const bool dev = on_dev(r);
+  Remap m{f32(in, dev), out->alloc<float>(odims, place_of(r)), shape_of(odims), shape_of(in.dims), {}, {}, fill};
+  for (int k = 0; k < kMaxD; ++k) {
+    m.off[k] = k < (int)off.size() ? off[k] : 0;
+    m.flip[k] = k < (int)flip.size() ? flip[k] : 0;
+  }
+  any::run(r, dev, out->numel(), m);
+}
+
+std::vector<int> flip_axes(const OpRun& r, int nd) {
+  std::vector<int> f(nd, 0);
+  for (int64_t a : r.op.GetInts("axis")) {
+    const int k = (int)(a < 0 ? a + nd : a);
+    PA_CHECK(k >= 0 && k < nd, "reverse: axis %lld out of range", (long long)a);
+    f[k] = 1;
+  }
+  return f;
+}
+
+void k_reverse(const OpRun& r) {
+  Tensor& x = r.in("X");
+  Tensor o;
+  remap(r, x, x.dims, {}, flip_axes(r, (int)x.dims.size()), 0.f, &o);
+  o.lod = x.lod;
+  set(r, "Out", o);
+}
+
+void k_reverse_grad(const OpRun& r) {
+  Tensor& g = r.in("Out@GRAD");
+  if (r.op.Outputs("X@GRAD").empty() || !r.out_var("X@GRAD")) return;
+  Tensor o;
+  remap(r, g, g.dims, {}, flip_axes(r, (int)g.dims.size()), 0.f, &o);
+  set(r, "X@GRAD", o);
+}
+
+void k_pad(const OpRun& r) {
+  Tensor& x = r.in("X");
+  const auto p = r.op.GetInts("paddings");
+  const int nd = (int)x.dims.size();
+  if ((int)p.size() != 2 * nd) throw Decline{};
+  Dims od(nd);
+  std::vector<int64_t> off(nd);
+  for (int k = 0; k < nd; ++k) {
+    od[k] = x.dims[k] + p[2 * k] + p[2 * k + 1];
+    off[k] = p[2 * k];
+  }
+  Tensor o;
+  remap(r, x, od, off, {}, r.op.GetFloat("pad_value", 0.f), &o);
+  set(r, "Out", o);
+}
+
+// pad's gradient: the window of Out@GRAD the input occupies
+void k_pad_grad(const OpRun& r) {
+  Tensor& x = r.in("X");
+  Tensor& g = r.in("Out@GRAD");
+  if (r.op.Outputs("X@GRAD").empty() || !r.out_var("X@GRAD")) return;
+  const auto p = r.op.GetInts("paddings");
+  const int nd = (int)x.dims.size();
+  if ((int)p.size() != 2 * nd) throw Decline{};
+  std::vector<int64_t> off(nd);
+  for (int k = 0; k < nd; ++k) off[k] = -p[2 * k];
+  Tensor o;
+  remap(r, g, x.dims, off, {}, 0.f, &o);
+  set(r, "X@GRAD", o);
+}
+
+// pad_constant_like: Y padded at the end of every dim up to X's shape
+void k_pad_constant_like(const OpRun& r) {
+  Tensor& x = r.in("X");
+  Tensor& y = r.in("Y");
+  if (x.dims.size() != y.dims.size()) throw Decline{};
+  Tensor o;
+  remap(r, y, x.dims, {}, {}, r.op.GetFloat("pad_value", 0.f), &o);
+  set(r, "Out", o);
+}
+
+void k_pad_constant_like_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& y = r.in("Y");
+  Tensor& g = r.in("Out@GRAD");
+  if (!r.op.Outputs("Y@GRAD").empty() && r.out_var("Y@GRAD")) {
+    Tensor o;
+    remap(r, g, y.dims, {}, {}, 0.f, &o);
+    set(r, "Y@GRAD", o);
+  }
+  Tensor dx;
+  if (float* p = grad_out(r, "X@GRAD", r.in("X"), &dx)) {  // X only gives the shape
+    any::zero(r, dev, p, dx.numel());
+    set(r, "X@GRAD", dx);
+  }
+}
+
+// ---------------------------------------------------------------- prelu
+// alpha index of element i: 0 (all), channel (i / inner) % C, element i % (C * inner)
+struct PRelu {
+  const float *x, *a;
+  float* o;
+  int mode;
+  int64_t C, inner;
+  __host__ __device__ int64_t ai(int64_t i) const {
+    return mode == 0 ? 0 : (mode == 1 ? (i / inner) % C : i % (C * inner));
+  }
+  __host__ __device__ void operator()(int64_t i) const { o[i] = x[i] > 0.f ? x[i] : a[ai(i)] * x[i]; }
+};
+struct PReluGradX {
+  PRelu p;
+  const float* g;
+  float* dx;
+  __host__ __device__ void operator()(int64_t i) const { dx[i] = g[i] * (p.x[i] > 0.f ? 1.f : p.a[p.ai(i)]); }
+};
+// dAlpha[j] = sum over the elements using alpha j of g x (x <= 0); one lane per alpha
+struct PReluGradA {
+  PRelu p;
+  const float* g;
+  float* da;
+  int64_t n, per;  // elements, elements per alpha (all: n)
+  __host__ __device__ void operator()(int64_t j) const {
+    float s = 0.f;
+    if (p.mode == 0) {
+      for (int64_t i = 0; i < n; ++i) s += p.x[i] > 0.f ? 0.f : g[i] * p.x[i];
+    } else if (p.mode == 1) {
+      for (int64_t b = 0; b < n / (p.C * p.inner); ++b)
+        for (int64_t k = 0; k < p.inner; ++k) {
+          const int64_t i = (b * p.C + j) * p.inner + k;
+          s += p.x[i] > 0.f ? 0.f : g[i] * p.x[i];
+        }
+    } else {
+      for (int64_t i = j; i < n; i += per) s += p.x[i] > 0.f ? 0.f : g[i] * p.x[i];
+    }
+    da[j] = s;
+  }
+};
+
+PRelu prelu_of(const OpRun& r, bool dev, float* out) {
+  Tensor& x = r.in("X");
+  Tensor& a = r.in("Alpha");
+  const std::string mode = r.op.GetString("mode", "all");
+  PRelu p{f32(x, dev), f32(a, dev), out, 0, 1, 1};
+  if (mode == "channel") {
+    if (x.dims.size() < 2) throw Decline{};
+    p.mode = 1;
+    p.C = x.dims[1];
+    for (size_t k = 2; k < x.dims.size(); ++k) p.inner *= x.dims[k];
+    if (a.numel() != p.C) throw Decline{};
+  } else if (mode == "element") {
+    p.mode = 2;
+    p.C = x.dims.empty() ? 1 : x.numel() / x.dims[0];
+    if (a.numel() != p.C) throw Decline{};
+  } else if (a.numel() < 1) {
+    throw Decline{};
+  }
+  return p;
+}
+
+void k_prelu(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor o;
+  float* op = new_like(r, x, &o);
+  any::run(r, dev, x.numel(), prelu_of(r, dev, op));
+  set(r, "Out", o);
+}
+
+void k_prelu_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  const float* g = f32(r.in("Out@GRAD"), dev);
+  PRelu p = prelu_of(r, dev, nullptr);
+  Tensor dX, dA;
+  if (float* dx = grad_out(r, "X@GRAD", x, &dX)) {
+    any::run(r, dev, x.numel(), PReluGradX{p, g, dx});
+    set(r, "X@GRAD", dX);
+  }
+  if (float* da = grad_out(r, "Alpha@GRAD", r.in("Alpha"), &dA)) {
+    const int64_t na = r.in("Alpha").numel();
+    any::run(r, dev, p.mode == 0 ? 1 : na, PReluGradA{p, g, da, x.numel(), p.mode == 2 ? p.C : x.numel()}, 1);
+    set(r, "Alpha@GRAD", dA);
+  }
+}
+
+// ---------------------------------------------------------------- iou_similarity
+struct Iou {
+  const float *a, *b;
+  float* o;
+  int64_t M;
+  float one;
+  __host__ __device__ void operator()(int64_t k) const {
+    const float* p = a + (k / M) * 4;
+    const float* q = b + (k % M) * 4;
+    const float aa = (p[2] - p[0] + one) * (p[3] - p[1] + one);
+    const float ab = (q[2] - q[0] + one) * (q[3] - q[1] + one);
+    const float w = fmaxf(fminf(p[2], q[2]) - fmaxf(p[0], q[0]) + one, 0.f);
+    const float h = fmaxf(fminf(p[3], q[3]) - fmaxf(p[1], q[1]) + one, 0.f);
+    const float in = w * h;
+    o[k] = in / fmaxf(aa + ab - in, 1e-10f);
+  }
+};
+
+void k_iou(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor& y = r.in("Y");
+  if (x.dims.size() != 2 || y.dims.size() != 2 || x.dims[1] != 4 || y.dims[1] != 4) throw Decline{};
+  Tensor o;
+  float* op = o.alloc<float>({x.dims[0], y.dims[0]}, place_of(r));
+  o.lod = x.lod;
+  any::run(r, dev, x.dims[0] * y.dims[0],
+           Iou{f32(x, dev), f32(y, dev), op, y.dims[0], r.op.GetBool("box_normalized", true) ? 0.f : 1.f});
+  set(r, "Out", o);
+}
+
+// ---------------------------------------------------------------- arg_min
+struct ArgMin {
+  const float* x;
+  int64_t* o;
+  int64_t outer, n, inner;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t a = t / inner, b = t % inner;
+    const float* p = x + a * n * inner + b;
+    int64_t best = 0;
+    float bv = p[0];
+    for (int64_t k = 1; k < n; ++k)
+      if (p[k * inner] < bv) {
+        bv = p[k * inner];
+        best = k;
+      }
+    o[t] = best;
+  }
+};
+
+void k_arg_min(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  const int nd = (int)x.dims.size();
+  int64_t ax = r.op.GetInt("axis", 0);
+  if (ax < 0) ax += nd;
+  if (nd == 0 || ax < 0 || ax >= nd || x.dims[ax] == 0) throw Decline{};
+  int64_t outer = 1, inner = 1;
+  for (int k = 0; k < ax; ++k) outer *= x.dims[k];
+  for (int k = (int)ax + 1; k < nd; ++k) inner *= x.dims[k];
+  Dims od;
+  for (int k = 0; k < nd; ++k)
+    if (k != ax) od.push_back(x.dims[k]);
+  Tensor o;
+  int64_t* op = static_cast<int64_t*>(o.alloc(DT::INT64, od, place_of(r)));
+  any::run(r, dev, outer * inner, ArgMin{f32(x, dev), op, outer, x.dims[ax], inner});
+  set(r, "Out", o);
+}
+
+// ---------------------------------------------------------------- fill / assign_value
+// a host constant of the op's dtype written to the op's place
+void write_values(const OpRun& r, DT dt, const Dims& shape, const std::vector<double>& vals, const char* slot) {
+  Tensor o;
+  void* p = o.alloc(dt, shape, place_of(r));
+  const int64_t n = o.numel();
+  if ((int64_t)vals.size() != n) fail("%s: %zu values for %lld elements", r.op.type.c_str(), vals.size(), (long long)n);
+  std::vector<char> h((size_t)o.nbytes());
+  for (int64_t i = 0; i < n; ++i) {
+    switch (dt) {
+      case DT::FP32: reinterpret_cast<float*>(h.data())[i] = (float)vals[i]; break;
+      case DT::FP64: reinterpret_cast<double*>(h.data())[i] = vals[i]; break;
+      case DT::INT32: reinterpret_cast<int32_t*>(h.data())[i] = (int32_t)vals[i]; break;
+      case DT::INT64: reinterpret_cast<int64_t*>(h.data())[i] = (int64_t)vals[i]; break;
+      case DT::BOOL: case DT::UINT8: reinterpret_cast<uint8_t*>(h.data())[i] = (uint8_t)(vals[i] != 0); break;
+      default: throw Decline{};
+    }
+  }
+  if (n) device_copy(p, o.device, h.data(), -1, o.nbytes(), r.ctx.stream);
+  set(r, slot, o);
+}
+
+void k_fill(const OpRun& r) {
+  std::vector<double> v;
+  for (float f : r.op.GetFloats("value")) v.push_back(f);
+  write_values(r, (DT)r.op.GetInt("dtype", 5), r.op.GetInts("shape"), v, "Out");
+}
+
+void k_assign_value(const OpRun& r) {
+  std::vector<double> v;
+  for (float f : r.op.GetFloats("fp32_values")) v.push_back(f);
+  if (v.empty())
+    for (int64_t i : r.op.GetInts("int32_values")) v.push_back((double)i);
+  write_values(r, (DT)r.op.GetInt("dtype", 5), r.op.GetInts("shape"), v, "Out");
+}
+
+// ---------------------------------------------------------------- proximal optimizers
+struct ProxGD {
+  const float *p, *g, *lr;
+  float* out;
+  float l1, l2;
+  __host__ __device__ void operator()(int64_t i) const {
+    const float a = lr[0], prox = p[i] - a * g[i];
+    const float s = prox > 0.f ? 1.f : (prox < 0.f ? -1.f : 0.f);
+    out[i] = s * fmaxf(fabsf(prox) - a * l1, 0.f) / (1.f + a * l2);
+  }
+};
+struct ProxAdagrad {
+  const float *p, *m, *g, *lr;
+  float *out, *mout;
+  float l1, l2;
+  __host__ __device__ void operator()(int64_t i) const {
+    const float m2 = m[i] + g[i] * g[i];
+    const float a = lr[0] / sqrtf(m2), prox = p[i] - a * g[i];
+    const float s = prox > 0.f ? 1.f : (prox < 0.f ? -1.f : 0.f);
+    out[i] = s * fmaxf(fabsf(prox) - a * l1, 0.f) / (1.f + a * l2);
+    mout[i] = m2;
+  }
+};
+
+// an in-place output keeps its buffer (ParamOut = Param)
+float* inplace_out(const OpRun& r, const char* slot, const Tensor& like) {
+  Tensor* o = r.out(slot);
+  if (o->raw() == like.raw() && o->initialized()) return o->data<float>();
+  return o->alloc<float>(like.dims, place_of(r));
+}
+
+void k_proximal_gd(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& p = r.in("Param");
+  Tensor& g = r.in("Grad");
+  if (g.numel() != p.numel()) throw Decline{};
+  const float* lr = f32(r.in("LearningRate"), dev);
+  const float *pp = f32(p, dev), *gp = f32(g, dev);
+  any::run(r, dev, p.numel(), ProxGD{pp, gp, lr, inplace_out(r, "ParamOut", p), r.op.GetFloat("l1", 0.f),
+                                     r.op.GetFloat("l2", 0.f)});
+}
+
+void k_proximal_adagrad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& p = r.in("Param");
+  Tensor& m = r.in("Moment");
+  Tensor& g = r.in("Grad");
+  if (g.numel() != p.numel() || m.numel() != p.numel()) throw Decline{};
+  const float* lr = f32(r.in("LearningRate"), dev);
+  const float *pp = f32(p, dev), *mp = f32(m, dev), *gp = f32(g, dev);
+  any::run(r, dev, p.numel(),
+           ProxAdagrad{pp, mp, gp, lr, inplace_out(r, "ParamOut", p), inplace_out(r, "MomentOut", m),
+                       r.op.GetFloat("l1", 0.f), r.op.GetFloat("l2", 0.f)});
+}
+
+// ---------------------------------------------------------------- matmul_grad
+// Out = alpha op(X) op(Y) per batch (rank-1 operands promoted, a batch of 1 broadcast):
+//   d op(X) = alpha dOut op(Y)^T, d op(Y) = alpha op(X)^T dOut, stored back through
+//   the transposes; a broadcast operand's gradient sums over the batches
+void k_matmul_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor& y = r.in("Y");
+  Tensor& g = r.in("Out@GRAD");
+  const bool tx = r.op.GetBool("transpose_X"), ty = r.op.GetBool("transpose_Y");
+  const float alpha = r.op.GetFloat("alpha", 1.f);
+  Dims xd = x.dims, yd = y.dims;
+  if (xd.size() == 1) xd = tx ? Dims{xd[0], 1} : Dims{1, xd[0]};
+  if (yd.size() == 1) yd = ty ? Dims{1, yd[0]} : Dims{yd[0], 1};
+  const int64_t xr = xd[xd.size() - 2], xc = xd.back(), yr = yd[yd.size() - 2], yc = yd.back();
+  const int64_t M = tx ? xc : xr, K = tx ? xr : xc, N = ty ? yr : yc;
+  if ((ty ? yc : yr) != K) throw Decline{};
+  int64_t bx = 1, by = 1;
+  for (size_t i = 0; i + 2 < xd.size(); ++i) bx *= xd[i];
+  for (size_t i = 0; i + 2 < yd.size(); ++i) by *= yd[i];
+  if (!(bx == by || bx == 1 || by == 1)) throw Decline{};
+  const int64_t B = bx > by ? bx : by;
+  if (g.numel() != B * M * N) throw Decline{};
+  const float *xp = f32(x, dev), *yp = f32(y, dev), *gp = f32(g, dev);
+  Tensor dX, dY;
+  if (float* dx = grad_out(r, "X@GRAD", x, &dX)) {
+    for (int64_t b = 0; b < B; ++b) {
+      const float* gb = gp + b * M * N;
+      const float* yb = yp + (by == 1 ? 0 : b * K * N);
+      float* db = dx + (bx == 1 ? 0 : b * M * K);
+      const float beta = (bx == 1 && b > 0) ? 1.f : 0.f;
+      if (!tx)  // dX [M, K] = g op(Y)^T
+        any::gemm(r, dev, false, !ty, M, K, N, alpha, gb, N, yb, ty ? K : N, beta, db, K);
+      else      // dX [K, M] = op(Y) g^T
+        any::gemm(r, dev, ty, true, K, M, N, alpha, yb, ty ? K : N, gb, N, beta, db, M);
+    }
+    set(r, "X@GRAD", dX);
+  }
+  if (float* dy = grad_out(r, "Y@GRAD", y, &dY)) {
+    for (int64_t b = 0; b < B; ++b) {
+      const float* gb = gp + b * M * N;
+      const float* xb = xp + (bx == 1 ? 0 : b * M * K);
+      float* db = dy + (by == 1 ? 0 : b * K * N);
+      const float beta = (by == 1 && b > 0) ? 1.f : 0.f;
+      if (!ty)  // dY [K, N] = op(X)^T g
+        any::gemm(r, dev, !tx, false, K, N, M, alpha, xb, tx ? M : K, gb, N, beta, db, N);
+      else      // dY [N, K] = g^T op(X)
+        any::gemm(r, dev, true, tx, N, K, M, alpha, gb, N, xb, tx ? M : K, beta, db, K);
+    }
+    set(r, "Y@GRAD", dY);
+  }
+}
+
+// ---------------------------------------------------------------- cos_sim
+// Out[i] = <x_i, y_i> / (|x_i| |y_i|) over rows (Y may be one row, broadcast)
+struct CosSim {
+  const float *x, *y;
+  float *o, *xn, *yn;
+  int64_t D, ybc;
+  __host__ __device__ void operator()(int64_t i) const {
+    const float* a = x + i * D;
+    const float* b = y + (ybc ? 0 : i * D);
+    float ab = 0.f, aa = 0.f, bb = 0.f;
+    for (int64_t k = 0; k < D; ++k) {
+      ab += a[k] * b[k];
+      aa += a[k] * a[k];
+      bb += b[k] * b[k];
+    }
+    xn[i] = sqrtf(aa);
+    if (!ybc || i == 0) yn[ybc ? 0 : i] = sqrtf(bb);
+    o[i] = ab / (sqrtf(aa) * sqrtf(bb));
+  }
+};
+// dx_i = g_i (y_i / (|x||y|) - out_i x_i / |x|^2); dy likewise (summed over rows when broadcast)
+struct CosSimGradX {
+  const float *x, *y, *o, *xn, *yn, *g;
+  float* dx;
+  int64_t D, ybc;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t i = t / D, k = t % D;
+    const float a = x[t], b = y[(ybc ? 0 : i * D) + k];
+    const float nx = xn[i], ny = yn[ybc ? 0 : i];
+    dx[t] = g[i] * (b / (nx * ny) - o[i] * a / (nx * nx));
+  }
+};
+struct CosSimGradY {
+  const float *x, *y, *o, *xn, *yn, *g;
+  float* dy;
+  int64_t D, rows, ybc;
+  __host__ __device__ void operator()(int64_t t) const {
+    if (!ybc) {
+      const int64_t i = t / D;
+      const float a = x[t], b = y[t], nx = xn[i], ny = yn[i];
+      dy[t] = g[i] * (a / (nx * ny) - o[i] * b / (ny * ny));
+      return;
+    }
+    const int64_t k = t;  // one lane per column of the broadcast row
+    const float b = y[k], ny = yn[0];
+    float s = 0.f;
+    for (int64_t i = 0; i < rows; ++i) s += g[i] * (x[i * D + k] / (xn[i] * ny) - o[i] * b / (ny * ny));
+    dy[k] = s;
+  }
+};
+
+void k_cos_sim(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor& y = r.in("Y");
+  if (x.dims.empty() || y.dims.empty()) throw Decline{};
+  const int64_t rows = x.dims[0], D = rows ? x.numel() / rows : 0;
+  const int64_t yrows = y.dims[0];
+  if (y.numel() != yrows * D || !(yrows == rows || yrows == 1)) throw Decline{};
+  Tensor o, xn, yn;
+  float* op = o.alloc<float>({rows, 1}, place_of(r));
+  float* xp = xn.alloc<float>({rows, 1}, place_of(r));
+  float* yp = yn.alloc<float>({yrows, 1}, place_of(r));
+  o.lod = x.lod;
+  any::run(r, dev, rows, CosSim{f32(x, dev), f32(y, dev), op, xp, yp, D, yrows == 1 && rows > 1 ? 1 : 0});
+  set(r, "Out", o);
+  set(r, "XNorm", xn);
+  set(r, "YNorm", yn);
+}
+
+void k_cos_sim_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor& y = r.in("Y");
+  const int64_t rows = x.dims[0], D = rows ? x.numel() / rows : 0;
+  const int64_t ybc = y.dims[0] == 1 && rows > 1 ? 1 : 0;
+  const float *xp = f32(x, dev), *yp = f32(y, dev), *op = f32(r.in("Out"), dev);
+  const float *xn = f32(r.in("XNorm"), dev), *yn = f32(r.in("YNorm"), dev), *gp = f32(r.in("Out@GRAD"), dev);
+  Tensor dX, dY;
+  if (float* dx = grad_out(r, "X@GRAD", x, &dX)) {
+    any::run(r, dev, x.numel(), CosSimGradX{xp, yp, op, xn, yn, gp, dx, D, ybc});
+    set(r, "X@GRAD", dX);
+  }
+  if (float* dy = grad_out(r, "Y@GRAD", y, &dY)) {
+    any::run(r, dev, ybc ? D : y.numel(), CosSimGradY{xp, yp, op, xn, yn, gp, dy, D, rows, ybc});
+    set(r, "Y@GRAD", dY);
+  }
+}
+
+// ---------------------------------------------------------------- multiplex
+// Out[i] = X[ids[i]][i]; the candidates' row pointers go in a small table
+struct Multiplex {
+  const int64_t* ids;
+  const float* const* xs;
+  float* o;
+  int64_t D;
+  __host__ __device__ void operator()(int64_t t) const { o[t] = xs[ids[t / D]][t]; }
+};
+struct MultiplexGrad {
+  const int64_t* ids;
+  float* const* dxs;  // null entries: no gradient wanted
+  const float* g;
+  int64_t K, D;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t sel = ids[t / D];
+    for (int64_t k = 0; k < K; ++k)
+      if (dxs[k]) dxs[k][t] = k == sel ? g[t] : 0.f;
+  }
+};
+
+template <class P>
+P* ptr_table(const OpRun& r, bool dev, const char* name, const std::vector<P>& v, std::vector<P>* keep) {
+  *keep = v;
+  if (!dev) return keep->data();
+  return (P*)device_upload(r, name, keep->data(), keep->size() * sizeof(P));
+}
+
+void k_multiplex(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& ids = r.in("Ids");
+  auto xs = r.ins("X");
+  if (xs.empty() || ids.dtype != DT::INT64 || (ids.device >= 0) != dev) throw Decline{};
+  const Tensor& x0 = *xs[0];
+  const int64_t rows = x0.dims.empty() ? 0 : x0.dims[0], D = rows ? x0.numel() / rows : 0;
+  if (ids.numel() != rows) throw Decline{};
+  std::vector<const float*> ptrs;
+  for (Tensor* t : xs) {
+    if (t->numel() != x0.numel()) throw Decline{};
+    ptrs.push_back(f32(*t, dev));
+  }
+  std::vector<const float*> keep;
+  const float* const* tab = ptr_table(r, dev, "@mpx_ptrs@", ptrs, &keep);
+  Tensor o;
+  float* op = new_like(r, x0, &o);
+  any::run(r, dev, rows * D, Multiplex{ids.data<int64_t>(), tab, op, D});
+  set(r, "Out", o);
+}
+
+void k_multiplex_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& ids = r.in("Ids");
+  auto xs = r.ins("X");
+  if (xs.empty() || ids.dtype != DT::INT64 || (ids.device >= 0) != dev) throw Decline{};
+  const int64_t rows = xs[0]->dims[0], D = rows ? xs[0]->numel() / rows : 0;
+  const auto& gnames = r.op.Outputs("X@GRAD");
+  std::vector<Tensor> grads(xs.size());
+  std::vector<float*> ptrs(xs.size(), nullptr);
+  for (size_t k = 0; k < xs.size() && k < gnames.size(); ++k)
+    if (gnames[k] != "@EMPTY@" && !gnames[k].empty()) ptrs[k] = new_like(r, *xs[k], &grads[k]);
+  std::vector<float*> keep;
+  float* const* tab = ptr_table(r, dev, "@mpxg_ptrs@", ptrs, &keep);
+  any::run(r, dev, rows * D, MultiplexGrad{ids.data<int64_t>(), tab, f32(r.in("Out@GRAD"), dev), (int64_t)xs.size(), D});
+  for (size_t k = 0; k < xs.size() && k < gnames.size(); ++k)
+    if (ptrs[k]) *r.out("X@GRAD", k) = grads[k];
+}
+
+// ---------------------------------------------------------------- crop
+void k_crop(const OpRun& r) {
+  Tensor& x = r.in("X");
+  Dims shape;
+  if (Tensor* y = r.in_opt("Y")) shape = y->dims;
+  else shape = r.op.GetInts("shape");
+  auto off = r.op.GetInts("offsets");
+  if (shape.size() != x.dims.size()) throw Decline{};
+  if (off.empty()) off.assign(x.dims.size(), 0);
+  std::vector<int64_t> neg(off.size());
+  for (size_t k = 0; k < off.size(); ++k) neg[k] = -off[k];
+  Tensor o;
+  remap(r, x, shape, neg, {}, 0.f, &o);
+  set(r, "Out", o);
+}
+
+void k_crop_grad(const OpRun& r) {
+  Tensor& x = r.in("X");
+  Tensor& g = r.in("Out@GRAD");
+  if (r.op.Outputs("X@GRAD").empty() || !r.out_var("X@GRAD")) return;
+  auto off = r.op.GetInts("offsets");
+  if (off.empty()) off.assign(x.dims.size(), 0);
+  Tensor o;
+  remap(r, g, x.dims, off, {}, 0.f, &o);
+  set(r, "X@GRAD", o);
+}
+
+// ---------------------------------------------------------------- norm (L2 along an axis)
+struct NormFwd {
+  const float* x;
+  float *o, *n;
+  int64_t A, inner;
+  float eps;
+  __host__ __device__ void operator()(int64_t t) const {  // t = outer * inner + j
+    const int64_t a0 = (t / inner) * A * inner + t % inner;
+    float s = 0.f;
+    for (int64_t k = 0; k < A; ++k) s += x[a0 + k * inner] * x[a0 + k * inner];
+    const float nv = sqrtf(s + eps);
+    n[t] = nv;
+    for (int64_t k = 0; k < A; ++k) o[a0 + k * inner] = x[a0 + k * inner] / nv;
+  }
+};
+struct NormBwd {
+  const float *x, *n, *g;
+  float* dx;
+  int64_t A, inner;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t a0 = (t / inner) * A * inner + t % inner;
+    const float nv = n[t];
+    float dot = 0.f;
+    for (int64_t k = 0; k < A; ++k) dot += g[a0 + k * inner] * x[a0 + k * inner];
+    for (int64_t k = 0; k < A; ++k) {
+      const float xv = x[a0 + k * inner];
+      dx[a0 + k * inner] = g[a0 + k * inner] / nv - xv * dot / (nv * nv * nv);
+    }
+  }
+};
+
+void norm_geom(const Tensor& x, int64_t ax, int64_t* outer, int64_t* A, int64_t* inner) {
+  const int nd = (int)x.dims.size();
+  if (ax < 0) ax += nd;
+  if (ax < 0 || ax >= nd) throw Decline{};
+  *outer = 1;
+  *inner = 1;
+  for (int k = 0; k < ax; ++k) *outer *= x.dims[k];
+  for (int k = (int)ax + 1; k < nd; ++k) *inner *= x.dims[k];
+  *A = x.dims[ax];
+}
+
+void k_norm(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  int64_t outer, A, inner;
+  norm_geom(x, r.op.GetInt("axis", 1), &outer, &A, &inner);
+  Tensor o, n;
+  Dims nd = x.dims;
+  int64_t ax = r.op.GetInt("axis", 1);
+  if (ax < 0) ax += (int64_t)nd.size();
+  nd[ax] = 1;
+  float* np_ = n.alloc<float>(nd, place_of(r));
+  any::run(r, dev, outer * inner, NormFwd{f32(x, dev), new_like(r, x, &o), np_, A, inner, r.op.GetFloat("epsilon", 1e-10f)});
+  set(r, "Out", o);
+  set(r, "Norm", n);
+}
+
+void k_norm_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  int64_t outer, A, inner;
+  norm_geom(x, r.op.GetInt("axis", 1), &outer, &A, &inner);
+  Tensor d;
+  float* dx = grad_out(r, "X@GRAD", x, &d);
+  if (!dx) return;
+  any::run(r, dev, outer * inner, NormBwd{f32(x, dev), f32(r.in("Norm"), dev), f32(r.in("Out@GRAD"), dev), dx, A, inner});
+  set(r, "X@GRAD", d);
+}
+
+// ---------------------------------------------------------------- conv_shift (circular)
+struct ConvShift {
+  const float *x, *y;
+  float* o;
+  int64_t M, N;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t b = t / M, i = t % M, half = (N - 1) / 2;
+    float s = 0.f;
+    for (int64_t j = 0; j < N; ++j) s += x[b * M + ((i + j - half) % M + M) % M] * y[b * N + j];
+    o[t] = s;
+  }
+};
+struct ConvShiftGradX {
+  const float *y, *g;
+  float* dx;
+  int64_t M, N;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t b = t / M, m = t % M, half = (N - 1) / 2;
+    float s = 0.f;
+    for (int64_t j = 0; j < N; ++j) s += g[b * M + ((m - j + half) % M + M) % M] * y[b * N + j];
+    dx[t] = s;
+  }
+};
+struct ConvShiftGradY {
+  const float *x, *g;
+  float* dy;
+  int64_t M, N;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t b = t / N, j = t % N, half = (N - 1) / 2;
+    float s = 0.f;
+    for (int64_t i = 0; i < M; ++i) s += g[b * M + i] * x[b * M + ((i + j - half) % M + M) % M];
+    dy[t] = s;
+  }
+};
+
+void k_conv_shift(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor& y = r.in("Y");
+  if (x.dims.size() != 2 || y.dims.size() != 2 || x.dims[0] != y.dims[0]) throw Decline{};
+  Tensor o;
+  any::run(r, dev, x.numel(), ConvShift{f32(x, dev), f32(y, dev), new_like(r, x, &o), x.dims[1], y.dims[1]});
+  set(r, "Out", o);
+}
+
+void k_conv_shift_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor& y = r.in("Y");
+  const float* g = f32(r.in("Out@GRAD"), dev);
+  Tensor dX, dY;
+  if (float* dx = grad_out(r, "X@GRAD", x, &dX)) {
+    any::run(r, dev, x.numel(), ConvShiftGradX{f32(y, dev), g, dx, x.dims[1], y.dims[1]});
+    set(r, "X@GRAD", dX);
+  }
+  if (float* dy = grad_out(r, "Y@GRAD", y, &dY)) {
+    any::run(r, dev, y.numel(), ConvShiftGradY{f32(x, dev), g, dy, x.dims[1], y.dims[1]});
+    set(r, "Y@GRAD", dY);
+  }
+}
+
+// ---------------------------------------------------------------- bilinear_tensor_product
+// out[b, k] = x_b^T W_k y_b (+ bias[k])
+struct Btp {
+  const float *x, *y, *w, *bias;
+  float* o;
+  int64_t K, I, J;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t b = t / K, k = t % K;
+    float s = bias ? bias[k] : 0.f;
+    for (int64_t i = 0; i < I; ++i) {
+      float t2 = 0.f;
+      for (int64_t j = 0; j < J; ++j) t2 += w[(k * I + i) * J + j] * y[b * J + j];
+      s += x[b * I + i] * t2;
+    }
+    o[t] = s;
+  }
+};
+struct BtpGradX {
+  const float *y, *w, *g;
+  float* dx;
+  int64_t K, I, J;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t b = t / I, i = t % I;
+    float s = 0.f;
+    for (int64_t k = 0; k < K; ++k) {
+      float t2 = 0.f;
+      for (int64_t j = 0; j < J; ++j) t2 += w[(k * I + i) * J + j] * y[b * J + j];
+      s += g[b * K + k] * t2;
+    }
+    dx[t] = s;
+  }
+};
+struct BtpGradY {
+  const float *x, *w, *g;
+  float* dy;
+  int64_t K, I, J;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t b = t / J, j = t % J;
+    float s = 0.f;
+    for (int64_t k = 0; k < K; ++k) {
+      float t2 = 0.f;
+      for (int64_t i = 0; i < I; ++i) t2 += x[b * I + i] * w[(k * I + i) * J + j];
+      s += g[b * K + k] * t2;
+    }
+    dy[t] = s;
+  }
+};
+struct BtpGradW {
+  const float *x, *y, *g;
+  float* dw;
+  int64_t B, K, I, J;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t k = t / (I * J), i = (t / J) % I, j = t % J;
+    float s = 0.f;
+    for (int64_t b = 0; b < B; ++b) s += g[b * K + k] * x[b * I + i] * y[b * J + j];
+    dw[t] = s;
+  }
+};
+
+void k_btp(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor& y = r.in("Y");
+  Tensor& w = r.in("Weight");
+  Tensor* bias = r.in_opt("Bias");
+  if (x.dims.size() != 2 || y.dims.size() != 2 || w.dims.size() != 3) throw Decline{};
+  const int64_t B = x.dims[0], K = w.dims[0], I = w.dims[1], J = w.dims[2];
+  if (x.dims[1] != I || y.dims[1] != J || y.dims[0] != B) throw Decline{};
+  Tensor o;
+  float* op = o.alloc<float>({B, K}, place_of(r));
+  any::run(r, dev, B * K, Btp{f32(x, dev), f32(y, dev), f32(w, dev), bias ? f32(*bias, dev) : nullptr, op, K, I, J});
+  set(r, "Out", o);
+}
+
+void k_btp_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor& y = r.in("Y");
+  Tensor& w = r.in("Weight");
+  const int64_t B = x.dims[0], K = w.dims[0], I = w.dims[1], J = w.dims[2];
+  const float *xp = f32(x, dev), *yp = f32(y, dev), *wp = f32(w, dev), *g = f32(r.in("Out@GRAD"), dev);
+  Tensor dX, dY, dW, dB;
+  if (float* p = grad_out(r, "X@GRAD", x, &dX)) {
+    any::run(r, dev, B * I, BtpGradX{yp, wp, g, p, K, I, J});
+    set(r, "X@GRAD", dX);
+  }
+  if (float* p = grad_out(r, "Y@GRAD", y, &dY)) {
+    any::run(r, dev, B * J, BtpGradY{xp, wp, g, p, K, I, J});
+    set(r, "Y@GRAD", dY);
+  }
+  if (float* p = grad_out(r, "Weight@GRAD", w, &dW)) {
+    any::run(r, dev, K * I * J, BtpGradW{xp, yp, g, p, B, K, I, J});
+    set(r, "Weight@GRAD", dW);
+  }
+  if (Tensor* bt = r.in_opt("Bias")) {
+    if (float* p = grad_out(r, "Bias@GRAD", *bt, &dB)) {
+      any::run(r, dev, K, any::ColSum{g, p, B, K, 0});
+      set(r, "Bias@GRAD", dB);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- maxout
+struct Maxout {
+  const float* x;
+  float* o;
+  int64_t Co, G, HW;
+  __host__ __device__ void operator()(int64_t t) const {  // t over [N, Co, HW]
+    const int64_t n = t / (Co * HW), c = (t / HW) % Co, s = t % HW;
+    const float* p = x + ((n * Co + c) * G) * HW + s;
+    float m = p[0];
+    for (int64_t k = 1; k < G; ++k) m = fmaxf(m, p[k * HW]);
+    o[t] = m;
+  }
+};
+struct MaxoutGrad {
+  const float *x, *o, *g;
+  float* dx;
+  int64_t Co, G, HW;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t n = t / (Co * HW), c = (t / HW) % Co, s = t % HW;
+    const int64_t base = ((n * Co + c) * G) * HW + s;
+    bool done = false;  // the gradient goes to the first maximal element
+    for (int64_t k = 0; k < G; ++k) {
+      const bool hit = !done && x[base + k * HW] == o[t];
+      dx[base + k * HW] = hit ? g[t] : 0.f;
+      done = done || hit;
+    }
+  }
+};
+
+void k_maxout(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  const int64_t G = r.op.GetInt("groups", 1);
+  if (x.dims.size() != 4 || G <= 0 || x.dims[1] % G) throw Decline{};
+  const int64_t N = x.dims[0], Co = x.dims[1] / G, HW = x.dims[2] * x.dims[3];
+  Tensor o;
+  float* op = o.alloc<float>({N, Co, x.dims[2], x.dims[3]}, place_of(r));
+  any::run(r, dev, N * Co * HW, Maxout{f32(x, dev), op, Co, G, HW});
+  set(r, "Out", o);
+}
+
+void k_maxout_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  const int64_t G = r.op.GetInt("groups", 1);
+  if (x.dims.size() != 4 || G <= 0 || x.dims[1] % G) throw Decline{};
+  const int64_t N = x.dims[0], Co = x.dims[1] / G, HW = x.dims[2] * x.dims[3];
+  Tensor d;
+  float* dx = grad_out(r, "X@GRAD", x, &d);
+  if (!dx) return;
+  any::run(r, dev, N * Co * HW, MaxoutGrad{f32(x, dev), f32(r.in("Out"), dev), f32(r.in("Out@GRAD"), dev), dx, Co, G, HW});
+  set(r, "X@GRAD", d);
+}
+
+// ---------------------------------------------------------------- fake (de)quantisation
+struct AbsMaxChunk {
+  const float* x;
+  float* part;
+  int64_t n, chunk;
+  __host__ __device__ void operator()(int64_t c) const {
+    float m = 0.f;
+    const int64_t a = c * chunk, b = a + chunk < n ? a + chunk : n;
+    for (int64_t i = a; i < b; ++i) m = fmaxf(m, fabsf(x[i]));
+    part[c] = m;
+  }
+};
+struct MaxOf {
+  const float* part;
+  float* out;
+  int64_t nc;
+  __host__ __device__ void operator()(int64_t) const {
+    float m = 0.f;
+    for (int64_t c = 0; c < nc; ++c) m = fmaxf(m, part[c]);
+    out[0] = m;
+  }
+};
+struct Quant {
+  const float *x, *s;
+  float* o;
+  float bins;
+  __host__ __device__ void operator()(int64_t i) const { o[i] = rintf(x[i] / fmaxf(s[0], 1e-30f) * bins); }
+};
+
+void k_fake_quant_abs_max(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  const int64_t n = x.numel(), chunk = 4096, nc = (n + chunk - 1) / chunk;
+  std::vector<float> hp;
+  float* part = any::scratch(r, dev, "@fq_part@", nc, &hp);
+  Tensor sc, o;
+  float* sp = sc.alloc<float>({1}, place_of(r));
+  any::run(r, dev, nc, AbsMaxChunk{f32(x, dev), part, n, chunk});
+  any::run(r, dev, 1, MaxOf{part, sp, nc});
+  const float bins = (float)((1 << (r.op.GetInt("bit_length", 8) - 1)) - 1);
+  any::run(r, dev, n, Quant{f32(x, dev), sp, new_like(r, x, &o), bins});
+  set(r, "Out", o);
+  set(r, "OutScale", sc);
+}
+
+struct Dequant {
+  const float *x, *s;
+  float* o;
+  float inv;
+  __host__ __device__ void operator()(int64_t i) const { o[i] = x[i] * s[0] * inv; }
+};
+struct DequantGradScale {
+  const float *x, *g;
+  float* ds;
+  int64_t n;
+  float inv;
+  __host__ __device__ void operator()(int64_t) const {
+    float s = 0.f;
+    for (int64_t i = 0; i < n; ++i) s += g[i] * x[i];
+    ds[0] = s * inv;
+  }
+};
+
+void k_fake_dequant(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor o;
+  any::run(r, dev, x.numel(), Dequant{f32(x, dev), f32(r.in("Scale"), dev), new_like(r, x, &o),
+                                      1.f / r.op.GetFloat("max_range", 127.f)});
+  set(r, "Out", o);
+}
+
+void k_fake_dequant_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  const float inv = 1.f / r.op.GetFloat("max_range", 127.f);
+  const float* g = f32(r.in("Out@GRAD"), dev);
+  Tensor dX, dS;
+  if (float* p = grad_out(r, "X@GRAD", x, &dX)) {
+    any::run(r, dev, x.numel(), Dequant{g, f32(r.in("Scale"), dev), p, inv});
+    set(r, "X@GRAD", dX);
+  }
+  if (float* p = grad_out(r, "Scale@GRAD", r.in("Scale"), &dS)) {
+    any::run(r, dev, 1, DequantGradScale{f32(x, dev), g, p, x.numel(), inv});
+    set(r, "Scale@GRAD", dS);
+  }
+}
+
+// ---------------------------------------------------------------- identity-like grads
+void copy_out(const OpRun& r, const Tensor& src, const char* slot, const LoD& lod) {
+  const bool dev = on_dev(r);
+  Tensor o;
+  any::copy(r, dev, o.alloc<float>(src.dims, place_of(r)), f32(src, dev), src.numel());
+  o.lod = lod;
+  set(r, slot, o);
+}
+
+// rnn_memory_helper: Out shares X (StaticRNN memories); its gradient passes through
+void k_rnn_memory_helper(const OpRun& r) { *r.out("Out") = r.in("X"); }
+
+void k_rnn_memory_helper_grad(const OpRun& r) {
+  if (r.op.Outputs("X@GRAD").empty() || !r.out_var("X@GRAD")) return;
+  Tensor& x = r.in("X");
+  if (Tensor* g = r.in_opt("Out@GRAD")) {
+    copy_out(r, *g, "X@GRAD", x.lod);
+  } else {
+    Tensor z;
+    any::zero(r, on_dev(r), new_like(r, x, &z), x.numel());
+    set(r, "X@GRAD", z);
+  }
+}
+
+// lod_reset's gradient: Out@GRAD with X's LoD
+void k_lod_reset_grad(const OpRun& r) {
+  if (r.op.Outputs("X@GRAD").empty() || !r.out_var("X@GRAD")) return;
+  copy_out(r, r.in("Out@GRAD"), "X@GRAD", r.in("X").lod);
+}
+
+// scatter's gradient: dX = g (rows written by an overwriting scatter zeroed), dUpdates = g[ids]
+struct RowGather {
+  const float* g;
+  const int64_t* ids;
+  float* o;
+  int64_t D;
+  __host__ __device__ void operator()(int64_t t) const { o[t] = g[ids[t / D] * D + t % D]; }
+};
+struct RowZero {
+  const int64_t* ids;
+  float* o;
+  int64_t D;
+  __host__ __device__ void operator()(int64_t t) const { o[ids[t / D] * D + t % D] = 0.f; }
+};
+
+void k_scatter_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& ids = r.in("Ids");
+  Tensor& g = r.in("Out@GRAD");
+  if (ids.dtype != DT::INT64 || (ids.device >= 0) != dev || g.dims.empty()) throw Decline{};
+  const int64_t D = g.numel() / g.dims[0], n = ids.numel();
+  Tensor dX, dU;
+  if (float* p = grad_out(r, "X@GRAD", r.in("X"), &dX)) {
+    any::copy(r, dev, p, f32(g, dev), g.numel());
+    if (r.op.GetBool("overwrite", true)) any::run(r, dev, n * D, RowZero{ids.data<int64_t>(), p, D});
+    set(r, "X@GRAD", dX);
+  }
+  if (float* p = grad_out(r, "Updates@GRAD", r.in("Updates"), &dU)) {
+    any::run(r, dev, n * D, RowGather{f32(g, dev), ids.data<int64_t>(), p, D});
+    set(r, "Updates@GRAD", dU);
+  }
+}
+
+// ---------------------------------------------------------------- polygon_box_transform
+struct PolyBox {
+  const float* x;
+  float* o;
+  int64_t C, H, W;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t w = t % W, h = (t / W) % H, c = (t / (W * H)) % C;
+    o[t] = (c % 2 == 0 ? (float)w : (float)h) - x[t];
+  }
+};
+
+void k_polygon_box(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("Input");
+  if (x.dims.size() != 4) throw Decline{};
+  Tensor o;
+  any::run(r, dev, x.numel(), PolyBox{f32(x, dev), new_like(r, x, &o), x.dims[1], x.dims[2], x.dims[3]});
+  set(r, "Output", o);
+}
+
+// ---------------------------------------------------------------- argsort
+// ascending along `axis`, one lane per line: stable insertion sort of (value, index)
+struct ArgSort {
+  const float* x;
+  float* v;
+  int64_t* idx;
+  int64_t n, inner;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t base = (t / inner) * n * inner + t % inner;
+    for (int64_t k = 0; k < n; ++k) {
+      const float xv = x[base + k * inner];
+      int64_t j = k;
+      while (j > 0 && v[base + (j - 1) * inner] > xv) {
+        v[base + j * inner] = v[base + (j - 1) * inner];
+        idx[base + j * inner] = idx[base + (j - 1) * inner];
+        --j;
+      }
+      v[base + j * inner] = xv;
+      idx[base + j * inner] = k;
+    }
+  }
+};
+
+void k_argsort(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  const int nd = (int)x.dims.size();
+  int64_t ax = r.op.GetInt("axis", -1);
+  if (ax < 0) ax += nd;
+  if (nd == 0 || ax < 0 || ax >= nd) throw Decline{};
+  int64_t outer = 1, inner = 1;
+  for (int k = 0; k < ax; ++k) outer *= x.dims[k];
+  for (int k = (int)ax + 1; k < nd; ++k) inner *= x.dims[k];
+  Tensor v, i;
+  float* vp = new_like(r, x, &v);
+  int64_t* ip = static_cast<int64_t*>(i.alloc(DT::INT64, x.dims, place_of(r)));
+  any::run(r, dev, outer * inner, ArgSort{f32(x, dev), vp, ip, x.dims[ax], inner});
+  set(r, "Out", v);
+  set(r, "Indices", i);
+}
+
+// ---------------------------------------------------------------- row_conv (lookahead)
+// out[t] = sum_{k < ctx, t + k in t's sequence} x[t + k] * w[k]   (elementwise per feature)
+struct RowConv {
+  const float *x, *w;
+  const int* seq_end;  // end row of each row's sequence
+  float* o;
+  int64_t D, ctx;
+  __host__ __device__ void operator()(int64_t i) const {
+    const int64_t t = i / D, d = i % D, e = seq_end[t];
+    float s = 0.f;
+    for (int64_t k = 0; k < ctx && t + k < e; ++k) s += x[(t + k) * D + d] * w[k * D + d];
+    o[i] = s;
+  }
+};
+struct RowConvGradX {
+  const float *g, *w;
+  const int* seq_start;
+  float* dx;
+  int64_t D, ctx;
+  __host__ __device__ void operator()(int64_t i) const {
+    const int64_t t = i / D, d = i % D, st = seq_start[t];
+    float s = 0.f;
+    for (int64_t k = 0; k < ctx && t - k >= st; ++k) s += g[(t - k) * D + d] * w[k * D + d];
+    dx[i] = s;
+  }
+};
+struct RowConvGradW {
+  const float *g, *x;
+  const int* seq_end;
+  float* dw;
+  int64_t T, D;
+  __host__ __device__ void operator()(int64_t i) const {
+    const int64_t k = i / D, d = i % D;
+    float s = 0.f;
+    for (int64_t t = 0; t < T; ++t)
+      if (t + k < seq_end[t]) s += g[t * D + d] * x[(t + k) * D + d];
+    dw[i] = s;
+  }
+};
+
+void row_bounds(const Tensor& x, std::vector<int>* st, std::vector<int>* en) {
+  const int64_t T = x.dims[0];
+  std::vector<size_t> off = x.lod.empty() ? std::vector<size_t>{0, (size_t)T} : x.lod[0];
+  st->assign((size_t)T, 0);
+  en->assign((size_t)T, 0);
+  for (size_t s = 0; s + 1 < off.size(); ++s)
+    for (size_t t = off[s]; t < off[s + 1] && (int64_t)t < T; ++t) {
+      (*st)[t] = (int)off[s];
+      (*en)[t] = (int)off[s + 1];
+    }
+}
+
+void k_row_conv(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor& w = r.in("Filter");
+  if (x.dims.size() != 2 || w.dims.size() != 2 || w.dims[1] != x.dims[1]) throw Decline{};
+  std::vector<int> st, en;
+  row_bounds(x, &st, &en);
+  Tensor o;
+  any::run(r, dev, x.numel(),
+           RowConv{f32(x, dev), f32(w, dev), any::ints(r, dev, "@rowconv_end@", en), new_like(r, x, &o), x.dims[1],
+                   w.dims[0]});
+  set(r, "Out", o);
+}
+
+void k_row_conv_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor& w = r.in("Filter");
+  const float* g = f32(r.in("Out@GRAD"), dev);
+  std::vector<int> st, en;
+  row_bounds(x, &st, &en);
+  Tensor dX, dW;
+  if (float* p = grad_out(r, "X@GRAD", x, &dX)) {
+    any::run(r, dev, x.numel(),
+             RowConvGradX{g, f32(w, dev), any::ints(r, dev, "@rowconv_start@", st), p, x.dims[1], w.dims[0]});
+    set(r, "X@GRAD", dX);
+  }
+  if (float* p = grad_out(r, "Filter@GRAD", w, &dW)) {
+    any::run(r, dev, w.numel(),
+             RowConvGradW{g, f32(x, dev), any::ints(r, dev, "@rowconv_end2@", en), p, x.dims[0], x.dims[1]});
+    set(r, "Filter@GRAD", dW);
+  }
+}
+
+// ---------------------------------------------------------------- lrn (across channels)
+// mid = k + alpha * sum_{c' in [c - (n-1)/2, c + n/2]} x_c'^2, out = x mid^-beta
+struct Lrn {
+  const float* x;
+  float *o, *mid;
+  int64_t C, HW, n;
+  float k, alpha, beta;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t c = (t / HW) % C, base = t - c * HW;
+    float s = 0.f;
+    for (int64_t q = c - (n - 1) / 2; q <= c + n / 2; ++q)
+      if (q >= 0 && q < C) s += x[base + q * HW] * x[base + q * HW];
+    const float m = k + alpha * s;
+    mid[t] = m;
+    o[t] = x[t] * powf(m, -beta);
+  }
+};
+// dx_c = g_c mid_c^-b - 2 a b x_c sum_{c': c in window(c')} g_c' out_c' / mid_c'
+struct LrnGrad {
+  const float *x, *o, *mid, *g;
+  float* dx;
+  int64_t C, HW, n;
+  float alpha, beta;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t c = (t / HW) % C, base = t - c * HW;
+    float s = 0.f;
+    for (int64_t q = c - n / 2; q <= c + (n - 1) / 2; ++q)
+      if (q >= 0 && q < C) s += g[base + q * HW] * o[base + q * HW] / mid[base + q * HW];
+    dx[t] = g[t] * powf(mid[t], -beta) - 2.f * alpha * beta * x[t] * s;
+  }
+};
+
+void k_lrn(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  if (x.dims.size() != 4) throw Decline{};
+  Tensor o, m;
+  any::run(r, dev, x.numel(),
+           Lrn{f32(x, dev), new_like(r, x, &o), new_like(r, x, &m), x.dims[1], x.dims[2] * x.dims[3],
+               r.op.GetInt("n", 5), r.op.GetFloat("k", 2.f), r.op.GetFloat("alpha", 1e-4f), r.op.GetFloat("beta", 0.75f)});
+  set(r, "Out", o);
+  set(r, "MidOut", m);
+}
+
+void k_lrn_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  if (x.dims.size() != 4) throw Decline{};
+  Tensor d;
+  float* dx = grad_out(r, "X@GRAD", x, &d);
+  if (!dx) return;
+  any::run(r, dev, x.numel(),
+           LrnGrad{f32(x, dev), f32(r.in("Out"), dev), f32(r.in("MidOut"), dev), f32(r.in("Out@GRAD"), dev), dx,
+                   x.dims[1], x.dims[2] * x.dims[3], r.op.GetInt("n", 5), r.op.GetFloat("alpha", 1e-4f),
+                   r.op.GetFloat("beta", 0.75f)});
+  set(r, "X@GRAD", d);
+}
+
+}  // namespace
+
+#define PA_ANY_KERNEL(name, fn) \
+  PA_HOST_KERNEL(name, fn);     \
+  PA_DEVICE_KERNEL(name, fn)
+
+PA_ANY_KERNEL(hinge_loss, k_hinge);
+PA_ANY_KERNEL(hinge_loss_grad, k_hinge_grad);
+PA_ANY_KERNEL(modified_huber_loss, k_mod_huber);
+PA_ANY_KERNEL(modified_huber_loss_grad, k_mod_huber_grad);
+PA_ANY_KERNEL(rank_loss, k_rank_loss);
+PA_ANY_KERNEL(rank_loss_grad, k_rank_loss_grad);
+PA_ANY_KERNEL(margin_rank_loss, k_margin_rank);
+PA_ANY_KERNEL(margin_rank_loss_grad, k_margin_rank_grad);
+PA_ANY_KERNEL(l1_norm, k_l1_norm);
+PA_ANY_KERNEL(l1_norm_grad, k_l1_norm_grad);
+PA_ANY_KERNEL(reverse, k_reverse);
+PA_ANY_KERNEL(reverse_grad, k_reverse_grad);
+PA_ANY_KERNEL(pad, k_pad);
+PA_ANY_KERNEL(pad_grad, k_pad_grad);
+PA_ANY_KERNEL(pad_constant_like, k_pad_constant_like);
+PA_ANY_KERNEL(pad_constant_like_grad, k_pad_constant_like_grad);
+PA_ANY_KERNEL(prelu, k_prelu);
+PA_ANY_KERNEL(prelu_grad, k_prelu_grad);
+PA_ANY_KERNEL(iou_similarity, k_iou);
+PA_ANY_KERNEL(arg_min, k_arg_min);
+PA_ANY_KERNEL(fill, k_fill);
+PA_ANY_KERNEL(assign_value, k_assign_value);
+PA_ANY_KERNEL(proximal_gd, k_proximal_gd);
+PA_ANY_KERNEL(proximal_adagrad, k_proximal_adagrad);
+PA_ANY_KERNEL(matmul_grad, k_matmul_grad);
+PA_ANY_KERNEL(cos_sim, k_cos_sim);
+PA_ANY_KERNEL(cos_sim_grad, k_cos_sim_grad);
+PA_ANY_KERNEL(multiplex, k_multiplex);
+PA_ANY_KERNEL(multiplex_grad, k_multiplex_grad);
+PA_ANY_KERNEL(crop, k_crop);
+PA_ANY_KERNEL(crop_grad, k_crop_grad);
+PA_ANY_KERNEL(norm, k_norm);
+PA_ANY_KERNEL(norm_grad, k_norm_grad);
+PA_ANY_KERNEL(conv_shift, k_conv_shift);
+PA_ANY_KERNEL(conv_shift_grad, k_conv_shift_grad);
+PA_ANY_KERNEL(bilinear_tensor_product, k_btp);
+PA_ANY_KERNEL(bilinear_tensor_product_grad, k_btp_grad);
+PA_ANY_KERNEL(maxout, k_maxout);
+PA_ANY_KERNEL(maxout_grad, k_maxout_grad);
+PA_ANY_KERNEL(fake_quantize_abs_max, k_fake_quant_abs_max);
+PA_ANY_KERNEL(fake_dequantize_max_abs, k_fake_dequant);
+PA_ANY_KERNEL(fake_dequantize_max_abs_grad, k_fake_dequant_grad);
+PA_ANY_KERNEL(rnn_memory_helper, k_rnn_memory_helper);
+PA_ANY_KERNEL(rnn_memory_helper_grad, k_rnn_memory_helper_grad);
+PA_ANY_KERNEL(lod_reset_grad, k_lod_reset_grad);
+PA_ANY_KERNEL(scatter_grad, k_scatter_grad);
+PA_ANY_KERNEL(polygon_box_transform, k_polygon_box);
+PA_ANY_KERNEL(argsort, k_argsort);
+PA_ANY_KERNEL(row_conv, k_row_conv);
+PA_ANY_KERNEL(row_conv_grad, k_row_conv_grad);
+PA_ANY_KERNEL(lrn, k_lrn);
+PA_ANY_KERNEL(lrn_grad, k_lrn_grad);
+
+void link_more_kernels() {}
+
+}  // namespace pa

@@ -229,6 +229,63 @@ def _cond_block_grad_descs(op, block, no_grad_dict, grad_to_var, callbacks):
                  attrs={"sub_block": grad_sub, "is_scalar_condition": op.attrs.get("is_scalar_condition", False)})]
 
 
+def _recurrent_grad_descs(op, block, no_grad_dict, grad_to_var, callbacks):
+    """Reference recurrent_op.cc RecurrentGradOpDescMaker: the grad block is a child
+    of the step block (it reads each step's activations from the kept step scopes);
+    recurrent_grad links the state gradients step to step and stacks / sums the
+    per-step input and parameter gradients (RecurrentGradOp::RunImpl)."""
+    prog = block.program
+    sub = op.attrs["sub_block"]
+    saved = prog.current_block_idx
+    grad_sub = prog.create_block(parent_idx=sub.idx)
+    no_grad_dict[sub.idx] = set(no_grad_dict[sub.idx]) | set(no_grad_dict[block.idx])
+    _append_backward_ops_(sub, list(sub.ops), grad_sub, no_grad_dict, grad_to_var, callbacks)
+    prog.current_block_idx = saved
+    no_grad = no_grad_dict[block.idx]
+    # The gradient of a step output / state arrives from outside the block (row t of
+    # the output gradient, the later step's ex-state gradient) as <name>@GRAD@EXT,
+    # which recurrent_grad always sets; the block adds it to whatever its own ops
+    # accumulated for <name>@GRAD (a state also consumed inside the step), or takes
+    # it as is.  Without this the block's sum of its own contributions would
+    # overwrite the incoming gradient.
+    linked = list(dict.fromkeys(list(op.attrs.get("states", [])) + list(op.output("outputs"))))
+    for n in linked:
+        gname = _append_grad_suffix_(n)
+        ext = gname + "@EXT"
+        src = sub._find_var_recursive(n)
+        for nm in (ext, gname + "@LOCAL"):
+            if not grad_sub.has_var(nm):
+                grad_sub.create_var(name=nm, dtype=src.dtype if src is not None else "float32",
+                                    shape=src.shape if src is not None else None)
+        writers = [i for i, gop in enumerate(grad_sub.ops) if gname in gop.output_arg_names]
+        if writers:
+            last = writers[-1]
+            grad_sub.ops[last].rename_output(gname, gname + "@LOCAL")
+            grad_sub.insert_op(last + 1, type="sum", inputs={"X": [gname + "@LOCAL", ext]}, outputs={"Out": [gname]},
+                               attrs={R.OP_ROLE_ATTR: R.OpRole.Backward})
+        else:
+            if not grad_sub.has_var(gname):
+                grad_sub.create_var(name=gname, dtype=src.dtype if src is not None else "float32",
+                                    shape=src.shape if src is not None else None)
+            grad_sub.insert_op(0, type="assign", inputs={"X": [ext]}, outputs={"Out": [gname]},
+                               attrs={R.OP_ROLE_ATTR: R.OpRole.Backward})
+
+    def grads(names):
+        return [_append_grad_suffix_(n) if _differentiable(block, n, no_grad) else R.EMPTY_VAR for n in names]
+
+    xs, inits, params = list(op.input("inputs")), list(op.input("initial_states")), list(op.input("parameters"))
+    outs = list(op.output("outputs"))
+    ogs = [_append_grad_suffix_(n) for n in outs if _differentiable(block, n, no_grad)]
+    attrs = {k: op.attrs[k] for k in ("ex_states", "states", "reverse", "is_train") if k in op.attrs}
+    attrs["sub_block"] = grad_sub
+    return [dict(type="recurrent_grad",
+                 inputs={"inputs": xs, "initial_states": inits, "parameters": params, "outputs": outs,
+                         "outputs@GRAD": ogs, "step_scopes": list(op.output("step_scopes"))},
+                 outputs={"inputs@GRAD": grads(xs), "initial_states@GRAD": grads(inits),
+                          "parameters@GRAD": grads(params)},
+                 attrs=attrs)]
+
+
 def _split_duplicate_outputs(descs):
     """A grad op that writes the same gradient from two slots (``x * x`` ->
     X@GRAD and Y@GRAD are both x@GRAD) gets the later occurrences renamed and a
@@ -278,6 +335,8 @@ def _append_backward_ops_(block, ops, target_block, no_grad_dict, grad_to_var, c
             descs = _while_grad_descs(op, block, no_grad_dict, grad_to_var, callbacks)
         elif op.type == "conditional_block":
             descs = _cond_block_grad_descs(op, block, no_grad_dict, grad_to_var, callbacks)
+        elif op.type == "recurrent":
+            descs = _recurrent_grad_descs(op, block, no_grad_dict, grad_to_var, callbacks)
         else:
             descs = R.make_grad_op_descs(_OpView(op), no_grad)
         for d in _split_duplicate_outputs(descs):

@@ -24,9 +24,10 @@ fallback callback (the op's inputs are zero-copy views of the native buffers, it
 outputs are lent back to the native scope), counted in ``py_fallbacks``.  On a HIP
 place the native kernels run on torch's current stream, so the two kernel
 libraries are ordered without host syncs.  ``while_grad`` / ``conditional_block_grad``
-run natively over kept step scopes (core.cc RunWhile / RunWhileGrad), as do tensor
+run natively over kept step scopes (core.cc RunWhile / RunWhileGrad), as do
+``recurrent`` / ``recurrent_grad`` (RunRecurrent / RunRecurrentGrad), tensor
 arrays, rank tables and SelectedRows gradients with the sparse SGD / Adam kernels.
-What still goes to the interpreter (``framework/executor.py``): ``recurrent``, ``parallel_do``,
+What still goes to the interpreter (``framework/executor.py``): ``parallel_do``,
 ``go`` / ``select`` and the RPC / pserver ops (``_UNSUPPORTED_CF``, ``_RPC_OPS``).
 
 The engine drives the C++ objects through the ``paddle_amd_core`` CPython
@@ -52,8 +53,8 @@ _TORCH_DT = {torch.float32: 5, torch.int64: 3, torch.int32: 2, torch.float64: 6,
              torch.float16: 4, torch.int16: 1, torch.int8: 21, torch.bfloat16: 22}
 _DT_TORCH = {v: k for k, v in _TORCH_DT.items()}
 # control-flow ops the C++ executor runs itself, and the ones it cannot take
-_NATIVE_CF = {"while", "while_grad", "conditional_block", "conditional_block_grad"}
-_UNSUPPORTED_CF = {"recurrent", "recurrent_grad", "parallel_do",
+_NATIVE_CF = {"while", "while_grad", "conditional_block", "conditional_block_grad", "recurrent", "recurrent_grad"}
+_UNSUPPORTED_CF = {"parallel_do",
                    "parallel_do_grad", "go", "select"}
 
 
@@ -88,6 +89,10 @@ class _CtypesBinding:
     @staticmethod
     def get(ns, name):
         return ns.get(name)
+
+    @staticmethod
+    def lod(ns, name):
+        return None  # the C ABI has no LoD read-back
 
     def run(self, prog, ns):
         self.exe.run(prog, ns)
@@ -131,6 +136,10 @@ class _PybindBinding:
         if v is None or not v.is_initialized():
             raise RuntimeError(f"variable {name} not found or empty")
         return v.get_tensor().numpy()
+
+    def lod(self, ns, name):
+        v = ns.find_var(name)
+        return [list(level) for level in v.get_tensor().lod()] if v is not None and v.is_initialized() else None
 
     def run(self, prog, ns):
         self.exe.run(prog, ns)
@@ -446,7 +455,10 @@ class NativeEngine:
         outs = []
         for n in fetch_names:
             a = self._b.get(ns, n)
-            outs.append(a if return_numpy else core.LoDTensor(torch.from_numpy(a).to(self._tdev())))
+            if return_numpy:
+                outs.append(a)
+            else:  # a LoDTensor fetch keeps the variable's LoD
+                outs.append(core.LoDTensor(torch.from_numpy(a).to(self._tdev()), self._b.lod(ns, n) or None))
         return outs
 
     def host_fallbacks(self):

@@ -23,6 +23,7 @@ Slot spec syntax: ``"X"`` plain, ``"X*"`` duplicable, ``"X?"`` dispensable,
 from __future__ import annotations
 
 import copy
+import weakref
 from dataclasses import dataclass, field
 
 import torch
@@ -337,7 +338,8 @@ def _make_auto_grad_info(fwd_type):
 # Forward graphs kept for the auto-VJP grad ops of a training program: the forward
 # op runs once under autograd (BlockExecutor marks the ops whose grads are auto
 # and present in the program) and its grad op takes the VJP of the stashed graph
-# instead of re-running the forward kernel.  Keyed by id() of every output tensor
+# instead of re-running the forward kernel.  Keyed by id() of every output tensor (with a
+# weak reference that must still resolve to that same tensor)
 # the forward op stored in the scope; cleared at the start of every top-level run.
 _STASH: dict = {}
 
@@ -396,7 +398,10 @@ def run_kernel_stash(info: OpInfo, ctx: KernelContext):
         entry = (leaves, graph_outs)
         for (slot, i) in graph_outs:
             r = ctx.results[slot][i]
-            _STASH[id(r.tensor if isinstance(r, core.LoDTensor) else r)] = entry
+            t = r.tensor if isinstance(r, core.LoDTensor) else r
+            # keyed by id, validated by identity: an id recycled after the output
+            # object died never picks up another op's graph
+            _STASH[id(t)] = (weakref.ref(t), entry)
     return ctx.results
 
 
@@ -406,8 +411,11 @@ def _stashed_vjp(fwd: OpInfo, ctx: KernelContext):
         for v in ctx.input_values(s.name):
             t = v.tensor if isinstance(v, core.LoDTensor) else v
             if isinstance(t, torch.Tensor) and id(t) in _STASH:
-                entry = _STASH[id(t)]
-                break
+                ref, e = _STASH[id(t)]
+                if ref() is t:
+                    entry = e
+                    break
+                _STASH.pop(id(t), None)  # a recycled id: the stashed forward is gone
         if entry is not None:
             break
     if entry is None:

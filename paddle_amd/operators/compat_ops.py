@@ -28,6 +28,7 @@ import torch
 import torch.nn.functional as F
 
 from ..framework import core
+from ..framework import registry as R
 from ..framework.registry import register_op
 from .nn_ops import _conv_attrs, conv2d_transpose
 
@@ -77,6 +78,89 @@ def recurrent(ctx):
     if ctx.has_output("step_scopes"):
         ctx.set_output("step_scopes", scopes)
 
+
+
+@register_op("recurrent_grad", ["inputs*?", "initial_states*?", "parameters*?", "outputs*?", "outputs@GRAD*?",
+                                "step_scopes?"], ["inputs@GRAD*?", "initial_states@GRAD*?", "parameters@GRAD*?"],
+             {"ex_states": [], "states": [], "sub_block": None, "reverse": False, "is_train": True},
+             grad=None, no_infer=True, share_lod=False)
+def recurrent_grad(ctx):
+    """recurrent_op.cc RecurrentGradOp::RunImpl: the grad block once per kept step
+    scope, last step first; block-local output gradients hold row t of the outer ones
+    plus, for states, the ex-state gradient of the later step; input gradient rows are
+    stacked, parameter gradients summed, and the first step's ex-state gradients are
+    the initial-state gradients (the C++ executor's RunRecurrentGrad does the same)."""
+    from .control_flow_grad import _grad_scope_vars
+
+    op, scope, exe = ctx.op, ctx.scope, ctx.executor
+    blk = ctx.attr("sub_block")
+    program = blk.program
+    steps = ctx.input_value("step_scopes") or []
+    T = len(steps)
+    order = list(range(T - 1, -1, -1)) if ctx.attr("reverse") else list(range(T))
+    ex, st = list(ctx.attr("ex_states")), list(ctx.attr("states"))
+    xs, inits, params = op.input("inputs"), op.input("initial_states"), op.input("parameters")
+    xgs, igs, pgs = op.output("inputs@GRAD"), op.output("initial_states@GRAD"), op.output("parameters@GRAD")
+    g = lambda n: n + "@GRAD"  # noqa: E731
+    og_outer = {}
+    for n in op.input("outputs@GRAD"):
+        v = scope.find_var(n)
+        val = v.get() if v is not None else None
+        if isinstance(val, core.LoDTensor) and val.tensor is not None:
+            og_outer[n] = val.tensor
+    carry = [None] * len(ex)
+    rows = [[None] * T for _ in xs]
+    pacc = {}
+    for k in range(T - 1, -1, -1):
+        t, s = order[k], steps[k]
+        gs = s.new_scope()
+        _grad_scope_vars(program, gs, blk.idx, set())
+        # <name>@GRAD@EXT of every step output / state: row t of its outer gradient
+        # plus the later step's ex-state gradient, zeros when neither exists (the
+        # grad block adds it to its own contributions: backward.py _recurrent_grad_descs)
+        for n in dict.fromkeys(st + list(op.input("outputs"))):
+            ext = og_outer[g(n)][t].clone() if g(n) in og_outer else None
+            if n in st and carry[st.index(n)] is not None:
+                c = carry[st.index(n)]
+                ext = c.clone() if ext is None else ext + c
+            if ext is None:
+                ext = torch.zeros_like(s.find_local_var(n).get().tensor)
+            gs.var(g(n) + "@EXT").set(core.LoDTensor(ext))
+        exe.run_block(program, blk.idx, gs, create_vars=False)
+
+        def local(n):
+            v = gs.find_local_var(n)
+            val = v.get() if v is not None else None
+            return val.tensor if isinstance(val, core.LoDTensor) and val.tensor is not None else None
+        for j, x in enumerate(xs):
+            if xgs and j < len(xgs) and xgs[j] != R.EMPTY_VAR:
+                rows[j][t] = local(g(x))
+        for j, p in enumerate(params):
+            if pgs and j < len(pgs) and pgs[j] != R.EMPTY_VAR:
+                r = local(g(p))
+                if r is not None:
+                    pacc[pgs[j]] = r.clone() if pgs[j] not in pacc else pacc[pgs[j]] + r
+        carry = [None if local(g(e)) is None else local(g(e)).clone() for e in ex]
+        if gs in getattr(s, "_kids", ()):
+            s._kids.remove(gs)
+
+    def value(n):
+        v = scope.find_var(n)
+        val = v.get() if v is not None else None
+        return val.tensor if isinstance(val, core.LoDTensor) else val
+    for j, x in enumerate(xs):
+        if not xgs or j >= len(xgs) or xgs[j] == R.EMPTY_VAR:
+            continue
+        xv = value(x)
+        r = [rows[j][t] if rows[j][t] is not None else torch.zeros_like(xv[t]) for t in range(T)]
+        scope.var(xgs[j]).set(core.LoDTensor(torch.stack(r, 0)))
+    for j, p in enumerate(params):
+        if pgs and j < len(pgs) and pgs[j] != R.EMPTY_VAR:
+            scope.var(pgs[j]).set(core.LoDTensor(pacc[pgs[j]] if pgs[j] in pacc else torch.zeros_like(value(p))))
+    for i, n in enumerate(inits):
+        if igs and i < len(igs) and igs[i] != R.EMPTY_VAR:
+            c = carry[i] if i < len(carry) else None
+            scope.var(igs[i]).set(core.LoDTensor(c if c is not None else torch.zeros_like(value(n))))
 
 # ---------------------------------------------------------------- parallel_do
 @register_op("parallel_do", ["inputs*?", "parameters*?", "places?"], ["outputs*?", "parallel_scopes?"],

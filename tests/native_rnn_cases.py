@@ -498,3 +498,57 @@ def losses_feeds(steps=4):
             "hyp": core.LoDTensor(torch.from_numpy(rs.randint(1, LS_C, (ho[-1], 1)).astype("int64")), [ho]),
         })
     return out
+
+
+# ---------------------------------------------------------------------------------
+# The reference StaticRNN's op: `recurrent` over a hand-built step block (two time-major
+# inputs, two linked states, a trainable initial state), its recurrent_grad, SGD.
+RT, RB, RD, RH = 5, 3, 4, 6
+
+
+def recurrent_net(reverse=False):
+    def build():
+        from paddle_amd.fluid.framework import VarType
+
+        main = fluid.default_main_program()
+        gb = main.global_block()
+        x1 = fluid.layers.data(name="rx1", shape=[RT, RB, RD], dtype="float32", append_batch_size=False)
+        x2 = fluid.layers.data(name="rx2", shape=[RT, RB, RH], dtype="float32", append_batch_size=False)
+        x1.stop_gradient = False
+        h0 = fluid.layers.create_parameter([RB, RH], "float32", name="rh0")
+        c0 = fluid.layers.fill_constant([RB, RH], "float32", 0.5)
+        w = fluid.layers.create_parameter([RD, RH], "float32", name="rw")
+        u = fluid.layers.create_parameter([RH, RH], "float32", name="ru")
+        sub = main.create_block()
+        v = {}
+        for n, shp in (("rx1", [RB, RD]), ("rx2", [RB, RH]), ("h_pre", [RB, RH]), ("c_pre", [RB, RH]), ("a", [RB, RH]),
+                       ("b", [RB, RH]), ("s1", [RB, RH]), ("s2", [RB, RH]), ("h", [RB, RH]), ("c", [RB, RH]),
+                       ("y", [RB, RH])):
+            v[n] = sub.create_var(name=n, dtype="float32", shape=shp)
+        sub.append_op(type="mul", inputs={"X": [v["rx1"]], "Y": [w]}, outputs={"Out": [v["a"]]})
+        sub.append_op(type="mul", inputs={"X": [v["h_pre"]], "Y": [u]}, outputs={"Out": [v["b"]]})
+        sub.append_op(type="elementwise_add", inputs={"X": [v["a"]], "Y": [v["b"]]}, outputs={"Out": [v["s1"]]})
+        sub.append_op(type="elementwise_add", inputs={"X": [v["s1"]], "Y": [v["rx2"]]}, outputs={"Out": [v["s2"]]})
+        sub.append_op(type="tanh", inputs={"X": [v["s2"]]}, outputs={"Out": [v["h"]]})
+        sub.append_op(type="elementwise_mul", inputs={"X": [v["c_pre"]], "Y": [v["h"]]}, outputs={"Out": [v["c"]]})
+        sub.append_op(type="elementwise_add", inputs={"X": [v["c"]], "Y": [v["h"]]}, outputs={"Out": [v["y"]]})
+        main.rollback()
+        out = gb.create_var(name="y", dtype="float32", shape=[RT, RB, RH])
+        hs = gb.create_var(name="h", dtype="float32", shape=[RT, RB, RH])
+        scopes = gb.create_var(name="rnn_scopes", type=VarType.STEP_SCOPES)
+        gb.append_op(type="recurrent", inputs={"inputs": [x1, x2], "initial_states": [h0, c0], "parameters": [w, u]},
+                     outputs={"outputs": [out, hs], "step_scopes": [scopes]},
+                     attrs={"ex_states": ["h_pre", "c_pre"], "states": ["h", "c"], "sub_block": sub,
+                            "reverse": reverse})
+        loss = fluid.layers.mean(out * out) + fluid.layers.mean(hs)
+        fluid.optimizer.SGD(learning_rate=0.1).minimize(loss)
+        return [loss, out, "rx1@GRAD", "rh0@GRAD", "rw@GRAD", "ru@GRAD"]
+    return build
+
+
+def recurrent_feeds(steps):
+    out = []
+    for k in range(steps):
+        rs = np.random.RandomState(300 + k)
+        out.append({"rx1": rs.randn(RT, RB, RD).astype("float32"), "rx2": rs.randn(RT, RB, RH).astype("float32")})
+    return out

@@ -134,3 +134,43 @@ def test_structured_losses_native():
         np.testing.assert_allclose(b[0], a[0], rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(b[1], a[1], rtol=1e-6)
     assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+
+
+@pytest.mark.parametrize("reverse", [False, True])
+def test_recurrent_op_native_matches_interpreter(reverse):
+    """The `recurrent` op (the reference StaticRNN's) and its recurrent_grad run on the
+    C++ executor over kept step scopes (core.cc RunRecurrent / RunRecurrentGrad): two
+    inputs, two linked states, a trainable initial state, SGD; the loss trajectory and
+    every gradient match the interpreter, and an independent torch unroll."""
+    import torch
+
+    from native_rnn_cases import recurrent_feeds, recurrent_net
+
+    fd = recurrent_feeds(3)
+    place = fluid.CPUPlace()
+    ref, init, _ = run(recurrent_net(reverse), fd, "python", place)
+    init0 = {k: v.copy() for k, v in init.items()}  # the runs train their scope's arrays in place
+    got, _, exe = run(recurrent_net(reverse), fd, "native", place, init)
+    init = init0
+    for a, b in zip(ref, got):
+        for x, y in zip(a, b):
+            np.testing.assert_allclose(y, x, rtol=1e-5, atol=1e-6)
+    assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+    # step 0 against torch autograd
+    W = torch.tensor(init["rw"], requires_grad=True)
+    U = torch.tensor(init["ru"], requires_grad=True)
+    H0 = torch.tensor(init["rh0"], requires_grad=True)
+    X1 = torch.tensor(fd[0]["rx1"], requires_grad=True)
+    X2 = torch.tensor(fd[0]["rx2"])
+    h, c = H0, torch.full_like(H0, 0.5)
+    ys, hs = [None] * 5, [None] * 5
+    for t in (range(4, -1, -1) if reverse else range(5)):
+        h = torch.tanh(X1[t] @ W + h @ U + X2[t])
+        c = c * h
+        ys[t], hs[t] = c + h, h
+    Y, Hs = torch.stack(ys), torch.stack(hs)
+    loss = (Y * Y).mean() + Hs.mean()
+    loss.backward()
+    np.testing.assert_allclose(got[0][0], loss.detach().numpy().reshape(got[0][0].shape), rtol=1e-5)
+    for arr, ref_t in zip(got[0][2:], (X1, H0, W, U)):
+        np.testing.assert_allclose(arr, ref_t.grad.numpy(), rtol=1e-4, atol=1e-6)

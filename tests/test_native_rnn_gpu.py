@@ -84,7 +84,7 @@ def test_sequence_row_map_ops_native_gpu():
     assert not exe._native.host_fallbacks(), exe._native.host_fallbacks()
 
 
-@pytest.mark.parametrize("case", ["static_rnn", "layout", "units", "vol", "losses"])
+@pytest.mark.parametrize("case", ["static_rnn", "layout", "units", "vol", "losses", "recurrent", "recurrent_rev"])
 def test_layout_ops_native_gpu(case):
     """The unrolled StaticRNN (slice / squeeze / stack per step) and the layout-op
     chain on a HIP place: ops_tensor.hip's strided-box kernel moves every tensor."""
@@ -94,7 +94,9 @@ def test_layout_ops_native_gpu(case):
                        "layout": (C.layout_net, C.layout_feeds),
                        "units": (C.units_net, C.units_feeds),
                        "vol": (C.vol_net, C.vol_feeds),
-                       "losses": (C.losses_net, C.losses_feeds)}[case]
+                       "losses": (C.losses_net, C.losses_feeds),
+                       "recurrent": (lambda: C.recurrent_net(False), C.recurrent_feeds),
+                       "recurrent_rev": (lambda: C.recurrent_net(True), C.recurrent_feeds)}[case]
     fd = feeds_fn(4)
     place = fluid.CUDAPlace(0)
     ref, init, _ = run(build(), fd, "python", place)
