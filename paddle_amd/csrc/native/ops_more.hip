@@ -6,7 +6,9 @@
 // (+grad), multiplex (+grad), crop (+grad), norm (+grad), conv_shift (+grad),
 // bilinear_tensor_product (+grad), maxout (+grad), fake_quantize_abs_max,
 // fake_dequantize_max_abs (+grad), rnn_memory_helper (+grad), lod_reset_grad,
-// scatter_grad, polygon_box_transform, argsort, row_conv (+grad), lrn (+grad).
+// scatter_grad, polygon_box_transform, argsort, row_conv (+grad), lrn (+grad),
+// split_lod_tensor / merge_lod_tensor (IfElse), max_pool2d_with_index / unpool (+grads),
+// box_coder, mean_iou.
 //
 // Semantics: reference operators/{hinge_loss,modified_huber_loss,rank_loss,
 // margin_rank_loss,l1_norm,reverse,pad,pad_constant_like,prelu,iou_similarity,
@@ -1538,6 +1540,405 @@ void k_lrn_grad(const OpRun& r) {
   set(r, "X@GRAD", d);
 }
 
+// ---------------------------------------------------------------- IfElse row routing
+// split_lod_tensor: the rows of X where Mask holds / does not, in order; the row maps
+// are built on the host from the (small) mask
+std::vector<uint8_t> host_mask(const OpRun& r, const Tensor& m) {
+  std::vector<uint8_t> h((size_t)m.numel());
+  Tensor hm = m.device >= 0 ? m.to(-1, r.ctx.stream) : m;
+  if (m.device >= 0) device_stream_sync(r.ctx.stream);
+  for (int64_t i = 0; i < m.numel(); ++i) {
+    switch (hm.dtype) {
+      case DT::BOOL: case DT::UINT8: case DT::INT8: h[i] = hm.data<uint8_t>()[i] != 0; break;
+      case DT::INT32: h[i] = hm.data<int32_t>()[i] != 0; break;
+      case DT::INT64: h[i] = hm.data<int64_t>()[i] != 0; break;
+      case DT::FP32: h[i] = hm.data<float>()[i] != 0.f; break;
+      default: throw Decline{};
+    }
+  }
+  return h;
+}
+
+struct RowCopy {  // dst row k = src row rows[k]
+  const float* src;
+  const int* rows;
+  float* dst;
+  int64_t D;
+  __host__ __device__ void operator()(int64_t t) const { dst[t] = src[(int64_t)rows[t / D] * D + t % D]; }
+};
+struct RowPut {  // dst row rows[k] = src row k
+  const float* src;
+  const int* rows;
+  float* dst;
+  int64_t D;
+  __host__ __device__ void operator()(int64_t t) const { dst[(int64_t)rows[t / D] * D + t % D] = src[t]; }
+};
+
+void k_split_lod_tensor(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  const auto m = host_mask(r, r.in("Mask"));
+  if (x.dims.empty() || (int64_t)m.size() != x.dims[0]) throw Decline{};
+  const int64_t D = x.numel() / x.dims[0];
+  std::vector<int> tr, fl;
+  for (size_t i = 0; i < m.size(); ++i) (m[i] ? tr : fl).push_back((int)i);
+  for (int side = 0; side < 2; ++side) {
+    const auto& rows = side ? fl : tr;
+    Dims d = x.dims;
+    d[0] = (int64_t)rows.size();
+    Tensor o;
+    float* op = o.alloc<float>(d, place_of(r));
+    any::run(r, dev, (int64_t)rows.size() * D,
+             RowCopy{f32(x, dev), any::ints(r, dev, side ? "@split_f@" : "@split_t@", rows), op, D});
+    set(r, side ? "OutFalse" : "OutTrue", o);
+  }
+}
+
+void k_merge_lod_tensor(const OpRun& r) {
+  const bool dev = on_dev(r);
+  const auto m = host_mask(r, r.in("Mask"));
+  Tensor* t = r.in_opt("InTrue");
+  Tensor* f = r.in_opt("InFalse");
+  const Tensor* ref = t && t->numel() ? t : f;
+  if (!ref || ref->dims.empty()) throw Decline{};
+  const int64_t D = ref->numel() / ref->dims[0];
+  std::vector<int> tr, fl;
+  for (size_t i = 0; i < m.size(); ++i) (m[i] ? tr : fl).push_back((int)i);
+  Dims d = ref->dims;
+  d[0] = (int64_t)m.size();
+  Tensor o;
+  float* op = o.alloc<float>(d, place_of(r));
+  any::zero(r, dev, op, o.numel());
+  if (t && t->numel()) {
+    if (t->dims[0] != (int64_t)tr.size()) throw Decline{};
+    any::run(r, dev, (int64_t)tr.size() * D, RowPut{f32(*t, dev), any::ints(r, dev, "@merge_t@", tr), op, D});
+  }
+  if (f && f->numel()) {
+    if (f->dims[0] != (int64_t)fl.size()) throw Decline{};
+    any::run(r, dev, (int64_t)fl.size() * D, RowPut{f32(*f, dev), any::ints(r, dev, "@merge_f@", fl), op, D});
+  }
+  set(r, "Out", o);
+}
+
+// their gradients: split's is the merge of the two branch gradients (a missing one
+// contributes zeros), merge's the split of Out@GRAD (X only gives the row count)
+void k_split_lod_tensor_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  const auto m = host_mask(r, r.in("Mask"));
+  Tensor d;
+  float* dx = grad_out(r, "X@GRAD", x, &d);
+  if (!dx) return;
+  if (x.dims.empty() || (int64_t)m.size() != x.dims[0]) throw Decline{};
+  const int64_t D = x.numel() / x.dims[0];
+  any::zero(r, dev, dx, x.numel());
+  std::vector<int> tr, fl;
+  for (size_t i = 0; i < m.size(); ++i) (m[i] ? tr : fl).push_back((int)i);
+  Tensor* gt = r.in_opt("OutTrue@GRAD");
+  Tensor* gf = r.in_opt("OutFalse@GRAD");
+  if (gt && gt->numel() && !tr.empty())
+    any::run(r, dev, (int64_t)tr.size() * D, RowPut{f32(*gt, dev), any::ints(r, dev, "@splitg_t@", tr), dx, D});
+  if (gf && gf->numel() && !fl.empty())
+    any::run(r, dev, (int64_t)fl.size() * D, RowPut{f32(*gf, dev), any::ints(r, dev, "@splitg_f@", fl), dx, D});
+  d.lod = x.lod;
+  set(r, "X@GRAD", d);
+}
+
+void k_merge_lod_tensor_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& g = r.in("Out@GRAD");
+  const auto m = host_mask(r, r.in("Mask"));
+  if (g.dims.empty() || (int64_t)m.size() != g.dims[0]) throw Decline{};
+  const int64_t D = g.numel() / g.dims[0];
+  std::vector<int> tr, fl;
+  for (size_t i = 0; i < m.size(); ++i) (m[i] ? tr : fl).push_back((int)i);
+  for (int side = 0; side < 2; ++side) {
+    const char* slot = side ? "InFalse@GRAD" : "InTrue@GRAD";
+    if (r.op.Outputs(slot).empty() || !r.out_var(slot)) continue;
+    const auto& rows = side ? fl : tr;
+    Dims dd = g.dims;
+    dd[0] = (int64_t)rows.size();
+    Tensor o;
+    float* op = o.alloc<float>(dd, place_of(r));
+    any::run(r, dev, (int64_t)rows.size() * D, RowCopy{f32(g, dev), any::ints(r, dev, side ? "@mergeg_f@" : "@mergeg_t@", rows), op, D});
+    set(r, slot, o);
+  }
+  Tensor dx;
+  if (float* p = grad_out(r, "X@GRAD", r.in("X"), &dx)) {
+    any::zero(r, dev, p, dx.numel());
+    set(r, "X@GRAD", dx);
+  }
+}
+
+// ---------------------------------------------------------------- max_pool2d_with_index / unpool
+struct MaxPoolIdx {
+  const float* x;
+  float* o;
+  int32_t* mask;
+  int64_t H, W, OH, OW, kh, kw, sh, sw, ph, pw;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t ow = t % OW, oh = (t / OW) % OH, plane = t / (OW * OH);
+    const float* p = x + plane * H * W;
+    float best = -INFINITY;
+    int64_t bi = -1;
+    for (int64_t i = 0; i < kh; ++i)
+      for (int64_t j = 0; j < kw; ++j) {
+        const int64_t h = oh * sh - ph + i, w = ow * sw - pw + j;
+        if (h < 0 || h >= H || w < 0 || w >= W) continue;
+        const float v = p[h * W + w];
+        if (bi < 0 || v > best) {
+          best = v;
+          bi = h * W + w;
+        }
+      }
+    o[t] = best;
+    mask[t] = (int32_t)bi;
+  }
+};
+// scatter-add of the pooled gradient to the recorded positions (windows may overlap)
+struct MaxPoolIdxGrad {
+  const float* g;
+  const int32_t* mask;
+  float* dx;
+  int64_t HW, OHW;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t plane = t / OHW;
+    if (mask[t] >= 0) acc_add(dx + plane * HW + mask[t], g[t]);
+  }
+};
+
+void pool_attrs(const OpRun& r, const Tensor& x, int64_t* kh, int64_t* kw, int64_t* sh, int64_t* sw, int64_t* ph,
+                int64_t* pw) {
+  auto k = r.op.GetInts("ksize"), st = r.op.GetInts("strides"), pd = r.op.GetInts("paddings");
+  if (k.size() != 2 || st.size() != 2 || pd.size() != 2 || x.dims.size() != 4) throw Decline{};
+  *kh = k[0], *kw = k[1], *sh = st[0], *sw = st[1], *ph = pd[0], *pw = pd[1];
+  if (r.op.GetBool("global_pooling", false)) {
+    *kh = x.dims[2], *kw = x.dims[3], *ph = 0, *pw = 0;
+  }
+}
+
+void k_max_pool2d_idx(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  int64_t kh, kw, sh, sw, ph, pw;
+  pool_attrs(r, x, &kh, &kw, &sh, &sw, &ph, &pw);
+  const int64_t H = x.dims[2], W = x.dims[3], OH = (H + 2 * ph - kh) / sh + 1, OW = (W + 2 * pw - kw) / sw + 1;
+  Tensor o, m;
+  float* op = o.alloc<float>({x.dims[0], x.dims[1], OH, OW}, place_of(r));
+  int32_t* mp = static_cast<int32_t*>(m.alloc(DT::INT32, {x.dims[0], x.dims[1], OH, OW}, place_of(r)));
+  any::run(r, dev, o.numel(), MaxPoolIdx{f32(x, dev), op, mp, H, W, OH, OW, kh, kw, sh, sw, ph, pw});
+  set(r, "Out", o);
+  set(r, "Mask", m);
+}
+
+void k_max_pool2d_idx_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor& m = r.in("Mask");
+  Tensor& g = r.in("Out@GRAD");
+  if (m.dtype != DT::INT32 || (m.device >= 0) != dev) throw Decline{};
+  Tensor d;
+  float* dx = grad_out(r, "X@GRAD", x, &d);
+  if (!dx) return;
+  any::zero(r, dev, dx, x.numel());
+  any::run(r, dev, g.numel(),
+           MaxPoolIdxGrad{f32(g, dev), m.data<int32_t>(), dx, x.dims[2] * x.dims[3], g.dims[2] * g.dims[3]}, 1 << 30);
+  set(r, "X@GRAD", d);
+}
+
+struct Unpool {
+  const float* x;
+  const int32_t* idx;
+  float* o;
+  int64_t HW, OHW;
+  __host__ __device__ void operator()(int64_t t) const { o[(t / HW) * OHW + idx[t]] = x[t]; }
+};
+struct UnpoolGrad {
+  const float* g;
+  const int32_t* idx;
+  float* dx;
+  int64_t HW, OHW;
+  __host__ __device__ void operator()(int64_t t) const { dx[t] = g[(t / HW) * OHW + idx[t]]; }
+};
+
+void unpool_geom(const OpRun& r, const Tensor& x, int64_t* OH, int64_t* OW) {
+  auto k = r.op.GetInts("ksize"), st = r.op.GetInts("strides"), pd = r.op.GetInts("paddings");
+  if (k.size() != 2 || st.size() != 2 || pd.size() != 2 || x.dims.size() != 4) throw Decline{};
+  *OH = (x.dims[2] - 1) * st[0] - 2 * pd[0] + k[0];
+  *OW = (x.dims[3] - 1) * st[1] - 2 * pd[1] + k[1];
+}
+
+void k_unpool(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor& idx = r.in("Indices");
+  if (idx.dtype != DT::INT32 || (idx.device >= 0) != dev || idx.numel() != x.numel()) throw Decline{};
+  int64_t OH, OW;
+  unpool_geom(r, x, &OH, &OW);
+  Tensor o;
+  float* op = o.alloc<float>({x.dims[0], x.dims[1], OH, OW}, place_of(r));
+  any::zero(r, dev, op, o.numel());
+  any::run(r, dev, x.numel(), Unpool{f32(x, dev), idx.data<int32_t>(), op, x.dims[2] * x.dims[3], OH * OW});
+  set(r, "Out", o);
+}
+
+void k_unpool_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Tensor& idx = r.in("Indices");
+  if (idx.dtype != DT::INT32 || (idx.device >= 0) != dev) throw Decline{};
+  int64_t OH, OW;
+  unpool_geom(r, x, &OH, &OW);
+  Tensor d;
+  float* dx = grad_out(r, "X@GRAD", x, &d);
+  if (!dx) return;
+  any::run(r, dev, x.numel(),
+           UnpoolGrad{f32(r.in("Out@GRAD"), dev), idx.data<int32_t>(), dx, x.dims[2] * x.dims[3], OH * OW});
+  set(r, "X@GRAD", d);
+}
+
+// ---------------------------------------------------------------- box_coder
+struct BoxCoder {
+  const float *prior, *var, *tgt;
+  float* o;
+  int64_t M, tgt3;
+  int encode;
+  float one;
+  __host__ __device__ void operator()(int64_t t) const {  // t over [N, M]
+    const int64_t n = t / M, m = t % M;
+    const float* p = prior + m * 4;
+    const float pw = p[2] - p[0] + one, ph = p[3] - p[1] + one;
+    const float pcx = (p[0] + p[2]) / 2.f, pcy = (p[1] + p[3]) / 2.f;
+    float* out = o + t * 4;
+    if (encode) {
+      const float* b = tgt + n * 4;
+      const float tw = b[2] - b[0] + one, th = b[3] - b[1] + one;
+      const float tcx = (b[0] + b[2]) / 2.f, tcy = (b[1] + b[3]) / 2.f;
+      float v[4] = {(tcx - pcx) / pw, (tcy - pcy) / ph, logf(fabsf(tw / pw)), logf(fabsf(th / ph))};
+      for (int k = 0; k < 4; ++k) out[k] = var ? v[k] / var[m * 4 + k] : v[k];
+    } else {
+      const float* d = tgt + (tgt3 ? t * 4 : n * 4);
+      const float v0 = var ? var[m * 4] : 1.f, v1 = var ? var[m * 4 + 1] : 1.f;
+      const float v2 = var ? var[m * 4 + 2] : 1.f, v3 = var ? var[m * 4 + 3] : 1.f;
+      const float cx = v0 * d[0] * pw + pcx, cy = v1 * d[1] * ph + pcy;
+      const float w = expf(v2 * d[2]) * pw, h = expf(v3 * d[3]) * ph;
+      out[0] = cx - w / 2.f;
+      out[1] = cy - h / 2.f;
+      out[2] = cx + w / 2.f - one;
+      out[3] = cy + h / 2.f - one;
+    }
+  }
+};
+
+void k_box_coder(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& prior = r.in("PriorBox");
+  Tensor& tgt = r.in("TargetBox");
+  Tensor* var = r.in_opt("PriorBoxVar");
+  const std::string ct = r.op.GetString("code_type", "encode_center_size");
+  const bool encode = ct.rfind("encode", 0) == 0 || ct.rfind("Encode", 0) == 0;
+  if (prior.dims.size() != 2 || prior.dims[1] != 4 || tgt.dims.empty() || tgt.dims.back() != 4) throw Decline{};
+  if (var && var->numel() != prior.numel()) throw Decline{};
+  const int64_t M = prior.dims[0], N = tgt.dims[0];
+  const bool t3 = tgt.dims.size() == 3;
+  if (t3 && (encode || tgt.dims[1] != M)) throw Decline{};
+  Tensor o;
+  float* op = o.alloc<float>({N, M, 4}, place_of(r));
+  o.lod = tgt.lod;
+  any::run(r, dev, N * M,
+           BoxCoder{f32(prior, dev), var ? f32(*var, dev) : nullptr, f32(tgt, dev), op, M, t3 ? 1 : 0, encode ? 1 : 0,
+                    r.op.GetBool("box_normalized", true) ? 0.f : 1.f});
+  set(r, "OutputBox", o);
+}
+
+// ---------------------------------------------------------------- mean_iou
+__host__ __device__ inline void acc_add_i(int32_t* p, int32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  atomicAdd(p, v);
+#else
+  *p += v;
+#endif
+}
+template <class T>
+struct IouHist {
+  const T *p, *l;
+  int32_t *correct, *wrong;
+  int64_t C;
+  __host__ __device__ void operator()(int64_t i) const {
+    const int64_t a = (int64_t)p[i], b = (int64_t)l[i];
+    if (a == b) {
+      if (b >= 0 && b < C) acc_add_i(correct + b, 1);
+    } else {
+      if (a >= 0 && a < C) acc_add_i(wrong + a, 1);
+      if (b >= 0 && b < C) acc_add_i(wrong + b, 1);
+    }
+  }
+};
+struct IouAdd {
+  const int32_t* in;
+  int32_t* acc;
+  __host__ __device__ void operator()(int64_t c) const { acc[c] += in[c]; }
+};
+struct IouMean {
+  const int32_t *correct, *wrong;
+  const float* const* extra;
+  int64_t C, nextra;
+  float* out;
+  __host__ __device__ void operator()(int64_t) const {
+    double s = 0.0;
+    int64_t n = 0;
+    for (int64_t c = 0; c < C; ++c) {
+      const int64_t den = (int64_t)correct[c] + wrong[c];
+      if (den > 0) {
+        s += (double)correct[c] / (double)den;
+        ++n;
+      }
+    }
+    double m = n ? s / (double)n : 0.0;
+    for (int64_t k = 0; k < nextra; ++k) m += (double)extra[k][0];
+    out[0] = (float)m;
+  }
+};
+
+void k_mean_iou(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& p = r.in("Predictions");
+  Tensor& l = r.in("Labels");
+  const int64_t C = r.op.GetInt("num_classes", 2);
+  if (p.numel() != l.numel() || p.dtype != l.dtype || (p.device >= 0) != dev || (l.device >= 0) != dev) throw Decline{};
+  Tensor co, wr, mi;
+  int32_t* cp = static_cast<int32_t*>(co.alloc(DT::INT32, {C}, place_of(r)));
+  int32_t* wp = static_cast<int32_t*>(wr.alloc(DT::INT32, {C}, place_of(r)));
+  if (dev) {
+    PA_HIPCHK(hipMemsetAsync(cp, 0, C * 4, dev_stream(r)));
+    PA_HIPCHK(hipMemsetAsync(wp, 0, C * 4, dev_stream(r)));
+  } else {
+    memset(cp, 0, C * 4);
+    memset(wp, 0, C * 4);
+  }
+  const int64_t serial = int64_t(1) << 60;  // host: one thread (plain increments)
+  if (p.dtype == DT::INT32) any::run(r, dev, p.numel(), IouHist<int32_t>{p.data<int32_t>(), l.data<int32_t>(), cp, wp, C}, serial);
+  else if (p.dtype == DT::INT64) any::run(r, dev, p.numel(), IouHist<int64_t>{p.data<int64_t>(), l.data<int64_t>(), cp, wp, C}, serial);
+  else throw Decline{};
+  for (Tensor* t : r.ins("InWrongs")) {
+    if (t->dtype != DT::INT32 || t->numel() != C) throw Decline{};
+    any::run(r, dev, C, IouAdd{t->data<int32_t>(), wp}, serial);
+  }
+  for (Tensor* t : r.ins("InCorrects")) {
+    if (t->dtype != DT::INT32 || t->numel() != C) throw Decline{};
+    any::run(r, dev, C, IouAdd{t->data<int32_t>(), cp}, serial);
+  }
+  std::vector<const float*> ex;
+  for (Tensor* t : r.ins("InMeanIou")) ex.push_back(f32(*t, dev));
+  std::vector<const float*> keep;
+  const float* const* tab = ex.empty() ? nullptr : ptr_table(r, dev, "@miou_ptrs@", ex, &keep);
+  float* mp = mi.alloc<float>({1}, place_of(r));
+  any::run(r, dev, 1, IouMean{cp, wp, tab, C, (int64_t)ex.size(), mp});
+  set(r, "OutMeanIou", mi);
+  set(r, "OutWrong", wr);
+  set(r, "OutCorrect", co);
+}
+
 }  // namespace
 
 #define PA_ANY_KERNEL(name, fn) \
@@ -1596,6 +1997,16 @@ PA_ANY_KERNEL(row_conv, k_row_conv);
 PA_ANY_KERNEL(row_conv_grad, k_row_conv_grad);
 PA_ANY_KERNEL(lrn, k_lrn);
 PA_ANY_KERNEL(lrn_grad, k_lrn_grad);
+PA_ANY_KERNEL(split_lod_tensor, k_split_lod_tensor);
+PA_ANY_KERNEL(merge_lod_tensor, k_merge_lod_tensor);
+PA_ANY_KERNEL(split_lod_tensor_grad, k_split_lod_tensor_grad);
+PA_ANY_KERNEL(merge_lod_tensor_grad, k_merge_lod_tensor_grad);
+PA_ANY_KERNEL(max_pool2d_with_index, k_max_pool2d_idx);
+PA_ANY_KERNEL(max_pool2d_with_index_grad, k_max_pool2d_idx_grad);
+PA_ANY_KERNEL(unpool, k_unpool);
+PA_ANY_KERNEL(unpool_grad, k_unpool_grad);
+PA_ANY_KERNEL(box_coder, k_box_coder);
+PA_ANY_KERNEL(mean_iou, k_mean_iou);
 
 void link_more_kernels() {}
 

@@ -42,22 +42,23 @@ def test_native_engine_updates_python_scope_in_place():
 
 
 def test_native_engine_python_fallback_lod_and_control_flow():
-    """Ops without a C++ kernel (row_conv on a LoD feed) run through the executor's
-    per-op Python fallback with their LoD intact."""
+    """Ops without a C++ kernel (ctc_align after a LoD feed) run through the executor's
+    per-op Python fallback with their LoD intact (input and output)."""
     main, startup = fluid.Program(), fluid.Program()
     with fluid.program_guard(main, startup):
         x = fluid.layers.data("x", [4], lod_level=1)
-        y = fluid.layers.row_conv(fluid.layers.fc(x, 3), future_context_size=2)
+        y = fluid.layers.ctc_greedy_decoder(fluid.layers.softmax(fluid.layers.fc(x, 3)), blank=0)
     scope = fluid.core.Scope()
     place = fluid.CPUPlace()
-    xv = fluid.create_lod_tensor(np.random.RandomState(0).rand(5, 4).astype("float32"), [[2, 3]], place)
+    xv = fluid.create_lod_tensor(np.random.RandomState(0).rand(7, 4).astype("float32"), [[3, 4]], place)
     with fluid.executor.scope_guard(scope):
         fluid.Executor(place).run(startup)
-        (ref,) = fluid.Executor(place).run(main, feed={"x": xv}, fetch_list=[y])
+        (ref,) = fluid.Executor(place).run(main, feed={"x": xv}, fetch_list=[y], return_numpy=False)
         exe = fluid.Executor(place, engine="native")
-        (got,) = exe.run(main, feed={"x": xv}, fetch_list=[y])
-    np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-7)
-    assert exe._native.py_fallbacks.get("row_conv") == 1
+        (got,) = exe.run(main, feed={"x": xv}, fetch_list=[y], return_numpy=False)
+    np.testing.assert_array_equal(np.array(got.tensor), np.array(ref.tensor))
+    assert got.lod() == ref.lod()
+    assert exe._native.py_fallbacks.get("ctc_align") == 1
 
 
 def test_native_engine_rejects_step_scope_programs():

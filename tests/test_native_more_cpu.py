@@ -188,6 +188,49 @@ def case_argsort_polygon(x, lab, idx):
     return L.elementwise_add(L.mean(L.square(h)), L.elementwise_add(L.mean(v), L.mean(pb)))
 
 
+def case_ifelse(x, lab, idx):
+    h = _head(x)
+    col = L.slice(lab, axes=[1], starts=[0], ends=[1])
+    cond = L.less_than(col, L.fill_constant([1], "float32", 0.0))
+    ie = L.IfElse(cond)
+    with ie.true_block():
+        t = ie.input(h)
+        ie.output(L.scale(t, 2.0))
+    with ie.false_block():
+        f = ie.input(h)
+        ie.output(L.square(f))
+    out = ie()[0]
+    return L.mean(out)
+
+
+def case_pool_index_unpool(x, lab, idx):
+    img = L.reshape(_head(x, 16), [-1, 1, 4, 4])
+    p, m = simple_op("max_pool2d_with_index", {"X": [img]}, {"ksize": [2, 2], "strides": [2, 2], "paddings": [0, 0],
+                                                             "global_pooling": False}, extra_outputs=("Mask",))
+    up = simple_op("unpool", {"X": [p], "Indices": [m]}, {"unpooling_type": "max", "ksize": [2, 2],
+                                                          "strides": [2, 2], "paddings": [0, 0]})
+    return L.elementwise_add(L.mean(L.square(up)), L.mean(p))
+
+
+def case_box_coder_mean_iou(x, lab, idx):
+    h = _head(x)
+    a = L.slice(lab, axes=[1], starts=[0], ends=[2])
+    prior = L.concat([a, L.elementwise_add(a, L.exp(L.slice(lab, axes=[1], starts=[2], ends=[4])))], axis=1)
+    tb = L.concat([a, L.elementwise_add(a, L.exp(L.slice(lab, axes=[1], starts=[4], ends=[6])))], axis=1)
+    enc = simple_op("box_coder", {"PriorBox": [prior], "TargetBox": [tb]},
+                    {"code_type": "encode_center_size", "box_normalized": False}, out_slot="OutputBox",
+                    stop_gradient=True)
+    dec = simple_op("box_coder", {"PriorBox": [prior], "TargetBox": [L.slice(h, axes=[1], starts=[0], ends=[4])]},
+                    {"code_type": "decode_center_size", "box_normalized": True}, out_slot="OutputBox",
+                    stop_gradient=True)
+    pred = L.slice(idx, axes=[0], starts=[0], ends=[4])
+    miou, _, _ = simple_op("mean_iou", {"Predictions": [pred], "Labels": [L.fill_constant([4, 1], "int64", 2)]},
+                           {"num_classes": 4}, out_slot="OutMeanIou", dtype="float32",
+                           extra_outputs=("OutWrong", "OutCorrect"), stop_gradient=True)
+    extra = L.elementwise_add(L.elementwise_add(L.mean(enc), L.mean(dec)), miou)
+    return L.elementwise_add(L.mean(L.square(h)), extra)
+
+
 CASES = {k[5:]: v for k, v in globals().items() if k.startswith("case_")}
 
 
