@@ -8,7 +8,8 @@
 // fake_dequantize_max_abs (+grad), rnn_memory_helper (+grad), lod_reset_grad,
 // scatter_grad, polygon_box_transform, argsort, row_conv (+grad), lrn (+grad),
 // split_lod_tensor / merge_lod_tensor (IfElse), max_pool2d_with_index / unpool (+grads),
-// box_coder, mean_iou.
+// box_coder, mean_iou, bilinear / nearest interpolation (+grads), pad2d (+grad),
+// im2sequence (+grad), fc_grad.
 //
 // Semantics: reference operators/{hinge_loss,modified_huber_loss,rank_loss,
 // margin_rank_loss,l1_norm,reverse,pad,pad_constant_like,prelu,iou_similarity,
@@ -1939,6 +1940,305 @@ void k_mean_iou(const OpRun& r) {
   set(r, "OutCorrect", co);
 }
 
+// ---------------------------------------------------------------- bilinear / nearest interpolation
+// torch conventions (what the Python kernel computes): align_corners: src = dst (in-1)/(out-1);
+// else src = (dst + 0.5) in/out - 0.5 clamped at 0; nearest: src = floor(dst in/out)
+struct Interp {
+  const float* x;
+  float* o;
+  int64_t H, W, OH, OW;
+  int bilinear, align;
+  __host__ __device__ void coord(int64_t d, int64_t in, int64_t out, int64_t* i0, int64_t* i1, float* l) const {
+    if (!bilinear) {
+      int64_t s = (int64_t)floorf((float)d * (float)in / (float)out);
+      *i0 = *i1 = s < in - 1 ? s : in - 1;
+      *l = 0.f;
+      return;
+    }
+    float src = align ? (out > 1 ? (float)d * (float)(in - 1) / (float)(out - 1) : 0.f)
+                      : fmaxf(((float)d + 0.5f) * (float)in / (float)out - 0.5f, 0.f);
+    int64_t a = (int64_t)floorf(src);
+    if (a > in - 1) a = in - 1;
+    *i0 = a;
+    *i1 = a + 1 < in ? a + 1 : in - 1;
+    *l = src - (float)a;
+  }
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t ow = t % OW, oh = (t / OW) % OH, plane = t / (OW * OH);
+    int64_t y0, y1, x0, x1;
+    float ly, lx;
+    coord(oh, H, OH, &y0, &y1, &ly);
+    coord(ow, W, OW, &x0, &x1, &lx);
+    const float* p = x + plane * H * W;
+    o[t] = (1.f - ly) * ((1.f - lx) * p[y0 * W + x0] + lx * p[y0 * W + x1]) +
+           ly * ((1.f - lx) * p[y1 * W + x0] + lx * p[y1 * W + x1]);
+  }
+};
+struct InterpGrad {
+  Interp f;
+  const float* g;
+  float* dx;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t ow = t % f.OW, oh = (t / f.OW) % f.OH, plane = t / (f.OW * f.OH);
+    int64_t y0, y1, x0, x1;
+    float ly, lx;
+    f.coord(oh, f.H, f.OH, &y0, &y1, &ly);
+    f.coord(ow, f.W, f.OW, &x0, &x1, &lx);
+    float* p = dx + plane * f.H * f.W;
+    const float gv = g[t];
+    acc_add(p + y0 * f.W + x0, gv * (1.f - ly) * (1.f - lx));
+    acc_add(p + y0 * f.W + x1, gv * (1.f - ly) * lx);
+    acc_add(p + y1 * f.W + x0, gv * ly * (1.f - lx));
+    acc_add(p + y1 * f.W + x1, gv * ly * lx);
+  }
+};
+
+Interp interp_of(const OpRun& r, const Tensor& x, int64_t* oh, int64_t* ow) {
+  if (x.dims.size() != 4) throw Decline{};
+  if (Tensor* os = r.in_opt("OutSize")) {
+    Tensor h = os->device >= 0 ? os->to(-1, r.ctx.stream) : *os;
+    if (os->device >= 0) device_stream_sync(r.ctx.stream);
+    if (h.numel() != 2 || h.dtype != DT::INT32) throw Decline{};
+    *oh = h.data<int32_t>()[0];
+    *ow = h.data<int32_t>()[1];
+  } else {
+    *oh = r.op.GetInt("out_h", -1);
+    *ow = r.op.GetInt("out_w", -1);
+    const float sc = r.op.GetFloat("scale", 0.f);
+    if ((*oh <= 0 || *ow <= 0) && sc > 0.f) {
+      *oh = (int64_t)(x.dims[2] * sc);
+      *ow = (int64_t)(x.dims[3] * sc);
+    }
+  }
+  if (*oh <= 0 || *ow <= 0) throw Decline{};
+  return Interp{nullptr, nullptr, x.dims[2], x.dims[3], *oh, *ow,
+                r.op.GetString("interp_method", "bilinear") == "bilinear" ? 1 : 0,
+                r.op.GetBool("align_corners", true) ? 1 : 0};
+}
+
+void k_interp(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  int64_t oh, ow;
+  Interp f = interp_of(r, x, &oh, &ow);
+  Tensor o;
+  f.x = f32(x, dev);
+  f.o = o.alloc<float>({x.dims[0], x.dims[1], oh, ow}, place_of(r));
+  any::run(r, dev, o.numel(), f);
+  set(r, "Out", o);
+}
+
+void k_interp_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  int64_t oh, ow;
+  Interp f = interp_of(r, x, &oh, &ow);
+  Tensor d;
+  float* dx = grad_out(r, "X@GRAD", x, &d);
+  if (!dx) return;
+  any::zero(r, dev, dx, x.numel());
+  Tensor& g = r.in("Out@GRAD");
+  any::run(r, dev, g.numel(), InterpGrad{f, f32(g, dev), dx}, int64_t(1) << 60);
+  set(r, "X@GRAD", d);
+}
+
+// ---------------------------------------------------------------- pad2d
+// constant / reflect / edge padding of [N, C, H, W] (or NHWC); gradient: the adjoint
+struct Pad2d {
+  const float* x;
+  float* o;
+  int64_t C, H, W, OH, OW, pt, pl;
+  int mode, nhwc;
+  float value;
+  __host__ __device__ int64_t src(int64_t i, int64_t n) const {  // -1: constant pad
+    if (i >= 0 && i < n) return i;
+    if (mode == 0) return -1;
+    if (mode == 1) {  // reflect (no edge repeat)
+      i = i < 0 ? -i : 2 * (n - 1) - i;
+      return i;
+    }
+    return i < 0 ? 0 : n - 1;  // edge
+  }
+  __host__ __device__ int64_t in_index(int64_t t, int64_t* out_ok) const {
+    int64_t n, c, h, w;
+    if (nhwc) {
+      c = t % C;
+      w = (t / C) % OW;
+      h = (t / (C * OW)) % OH;
+      n = t / (C * OW * OH);
+    } else {
+      w = t % OW;
+      h = (t / OW) % OH;
+      c = (t / (OW * OH)) % C;
+      n = t / (OW * OH * C);
+    }
+    const int64_t sh = src(h - pt, H), sw = src(w - pl, W);
+    *out_ok = sh >= 0 && sw >= 0;
+    if (!*out_ok) return 0;
+    return nhwc ? ((n * H + sh) * W + sw) * C + c : ((n * C + c) * H + sh) * W + sw;
+  }
+  __host__ __device__ void operator()(int64_t t) const {
+    int64_t ok;
+    const int64_t i = in_index(t, &ok);
+    o[t] = ok ? x[i] : value;
+  }
+};
+struct Pad2dGrad {
+  Pad2d f;
+  const float* g;
+  float* dx;
+  __host__ __device__ void operator()(int64_t t) const {
+    int64_t ok;
+    const int64_t i = f.in_index(t, &ok);
+    if (ok) acc_add(dx + i, g[t]);
+  }
+};
+
+Pad2d pad2d_of(const OpRun& r, const Tensor& x) {
+  auto p = r.op.GetInts("paddings");
+  if (x.dims.size() != 4 || p.size() != 4) throw Decline{};
+  const std::string mode = r.op.GetString("mode", "constant");
+  const bool nhwc = r.op.GetString("data_format", "NCHW") == "NHWC";
+  const int64_t C = nhwc ? x.dims[3] : x.dims[1], H = nhwc ? x.dims[1] : x.dims[2], W = nhwc ? x.dims[2] : x.dims[3];
+  Pad2d f{nullptr, nullptr, C, H, W, H + p[0] + p[1], W + p[2] + p[3], p[0], p[2],
+          mode == "constant" ? 0 : (mode == "reflect" ? 1 : 2), nhwc ? 1 : 0, r.op.GetFloat("pad_value", 0.f)};
+  if (f.mode == 1 && (p[0] >= H || p[1] >= H || p[2] >= W || p[3] >= W)) throw Decline{};
+  return f;
+}
+
+void k_pad2d(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Pad2d f = pad2d_of(r, x);
+  Dims od = f.nhwc ? Dims{x.dims[0], f.OH, f.OW, f.C} : Dims{x.dims[0], f.C, f.OH, f.OW};
+  Tensor o;
+  f.x = f32(x, dev);
+  f.o = o.alloc<float>(od, place_of(r));
+  any::run(r, dev, o.numel(), f);
+  set(r, "Out", o);
+}
+
+void k_pad2d_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Pad2d f = pad2d_of(r, x);
+  Tensor d;
+  float* dx = grad_out(r, "X@GRAD", x, &d);
+  if (!dx) return;
+  any::zero(r, dev, dx, x.numel());
+  Tensor& g = r.in("Out@GRAD");
+  any::run(r, dev, g.numel(), Pad2dGrad{f, f32(g, dev), dx}, int64_t(1) << 60);
+  set(r, "X@GRAD", d);
+}
+
+// ---------------------------------------------------------------- im2sequence
+// Out[n L + l, (c kh + i) kw + j] = xpad[n, c, oh sh + i, ow sw + j], LoD [0, L, 2L, ...]
+struct Im2Seq {
+  const float* x;
+  float* o;
+  int64_t C, H, W, OH, OW, kh, kw, sh, sw, pt, pl;
+  __host__ __device__ int64_t src(int64_t t) const {
+    const int64_t CK = C * kh * kw, col = t % CK, row = t / CK;
+    const int64_t L = OH * OW, n = row / L, l = row % L, oh = l / OW, ow = l % OW;
+    const int64_t c = col / (kh * kw), i = (col / kw) % kh, j = col % kw;
+    const int64_t h = oh * sh + i - pt, w = ow * sw + j - pl;
+    if (h < 0 || h >= H || w < 0 || w >= W) return -1;
+    return ((n * C + c) * H + h) * W + w;
+  }
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t s = src(t);
+    o[t] = s >= 0 ? x[s] : 0.f;
+  }
+};
+struct Im2SeqGrad {
+  Im2Seq f;
+  const float* g;
+  float* dx;
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t s = f.src(t);
+    if (s >= 0) acc_add(dx + s, g[t]);
+  }
+};
+
+Im2Seq im2seq_of(const OpRun& r, const Tensor& x) {
+  auto k = r.op.GetInts("kernels"), st = r.op.GetInts("strides"), p = r.op.GetInts("paddings");
+  if (x.dims.size() != 4 || k.size() != 2 || st.size() != 2 || p.size() != 4) throw Decline{};
+  const int64_t H = x.dims[2], W = x.dims[3];
+  const int64_t OH = (H + p[0] + p[2] - k[0]) / st[0] + 1, OW = (W + p[1] + p[3] - k[1]) / st[1] + 1;
+  return Im2Seq{nullptr, nullptr, x.dims[1], H, W, OH, OW, k[0], k[1], st[0], st[1], p[0], p[1]};
+}
+
+void k_im2sequence(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Im2Seq f = im2seq_of(r, x);
+  const int64_t N = x.dims[0], L = f.OH * f.OW;
+  Tensor o;
+  f.x = f32(x, dev);
+  f.o = o.alloc<float>({N * L, f.C * f.kh * f.kw}, place_of(r));
+  std::vector<size_t> lod;
+  for (int64_t n = 0; n <= N; ++n) lod.push_back((size_t)(n * L));
+  o.lod = {lod};
+  any::run(r, dev, o.numel(), f);
+  set(r, "Out", o);
+}
+
+void k_im2sequence_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("X");
+  Im2Seq f = im2seq_of(r, x);
+  Tensor d;
+  float* dx = grad_out(r, "X@GRAD", x, &d);
+  if (!dx) return;
+  any::zero(r, dev, dx, x.numel());
+  Tensor& g = r.in("Out@GRAD");
+  any::run(r, dev, g.numel(), Im2SeqGrad{f, f32(g, dev), dx}, int64_t(1) << 60);
+  set(r, "X@GRAD", d);
+}
+
+// ---------------------------------------------------------------- fc_grad
+// Out = act(flatten(Input) W + Bias), act in {none, relu}
+struct ReluMask {
+  const float *g, *out;
+  float* d;
+  __host__ __device__ void operator()(int64_t i) const { d[i] = out[i] > 0.f ? g[i] : 0.f; }
+};
+
+void k_fc_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  Tensor& x = r.in("Input");
+  Tensor& w = r.in("W");
+  const std::string act = r.op.GetString("activation_type", "");
+  if (!act.empty() && act != "relu") throw Decline{};
+  const size_t nc = (size_t)r.op.GetInt("in_num_col_dims", 1);
+  int64_t M = 1;
+  for (size_t k = 0; k < nc && k < x.dims.size(); ++k) M *= x.dims[k];
+  const int64_t K = M ? x.numel() / M : 0, N = w.dims.size() == 2 ? w.dims[1] : 0;
+  if (w.dims.size() != 2 || w.dims[0] != K) throw Decline{};
+  const float* g = f32(r.in("Out@GRAD"), dev);
+  std::vector<float> hs;
+  if (act == "relu") {
+    float* m = any::scratch(r, dev, "@fcg_mask@", M * N, &hs);
+    any::run(r, dev, M * N, ReluMask{g, f32(r.in("Out"), dev), m});
+    g = m;
+  }
+  Tensor dX, dW, dB;
+  if (float* p = grad_out(r, "Input@GRAD", x, &dX)) {
+    any::gemm(r, dev, false, true, M, K, N, 1.f, g, N, f32(w, dev), N, 0.f, p, K);
+    set(r, "Input@GRAD", dX);
+  }
+  if (float* p = grad_out(r, "W@GRAD", w, &dW)) {
+    any::gemm(r, dev, true, false, K, N, M, 1.f, f32(x, dev), K, g, N, 0.f, p, N);
+    set(r, "W@GRAD", dW);
+  }
+  if (Tensor* b = r.in_opt("Bias")) {
+    if (float* p = grad_out(r, "Bias@GRAD", *b, &dB)) {
+      any::run(r, dev, N, any::ColSum{g, p, M, N, 0});
+      set(r, "Bias@GRAD", dB);
+    }
+  }
+}
+
 }  // namespace
 
 #define PA_ANY_KERNEL(name, fn) \
@@ -2007,6 +2307,15 @@ PA_ANY_KERNEL(unpool, k_unpool);
 PA_ANY_KERNEL(unpool_grad, k_unpool_grad);
 PA_ANY_KERNEL(box_coder, k_box_coder);
 PA_ANY_KERNEL(mean_iou, k_mean_iou);
+PA_ANY_KERNEL(bilinear_interp, k_interp);
+PA_ANY_KERNEL(bilinear_interp_grad, k_interp_grad);
+PA_ANY_KERNEL(nearest_interp, k_interp);
+PA_ANY_KERNEL(nearest_interp_grad, k_interp_grad);
+PA_ANY_KERNEL(pad2d, k_pad2d);
+PA_ANY_KERNEL(pad2d_grad, k_pad2d_grad);
+PA_ANY_KERNEL(im2sequence, k_im2sequence);
+PA_ANY_KERNEL(im2sequence_grad, k_im2sequence_grad);
+PA_ANY_KERNEL(fc_grad, k_fc_grad);
 
 void link_more_kernels() {}
 

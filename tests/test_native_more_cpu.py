@@ -231,6 +231,47 @@ def case_box_coder_mean_iou(x, lab, idx):
     return L.elementwise_add(L.mean(L.square(h)), extra)
 
 
+def _img(x, c=2, h=3, w=2):
+    return L.reshape(_head(x, c * h * w), [-1, c, h, w])
+
+
+def case_interp(x, lab, idx):
+    img = _img(x)
+    a = simple_op("bilinear_interp", {"X": [img]}, {"out_h": 5, "out_w": 4, "interp_method": "bilinear",
+                                                     "align_corners": True})
+    b = simple_op("bilinear_interp", {"X": [img]}, {"out_h": 4, "out_w": 3, "interp_method": "bilinear",
+                                                     "align_corners": False})
+    c = simple_op("nearest_interp", {"X": [img]}, {"out_h": 6, "out_w": 5, "interp_method": "nearest",
+                                                    "align_corners": False})
+    return L.elementwise_add(L.elementwise_add(L.mean(L.square(a)), L.mean(L.square(b))), L.mean(L.square(c)))
+
+
+def case_pad2d(x, lab, idx):
+    img = _img(x)
+    outs = [simple_op("pad2d", {"X": [img]}, {"paddings": [1, 0, 1, 1], "mode": m, "pad_value": 0.3,
+                                               "data_format": "NCHW"}) for m in ("constant", "reflect", "edge")]
+    nhwc = simple_op("pad2d", {"X": [L.transpose(img, [0, 2, 3, 1])]},
+                     {"paddings": [0, 1, 1, 0], "mode": "edge", "pad_value": 0.0, "data_format": "NHWC"})
+    tot = L.mean(L.square(nhwc))
+    for o in outs:
+        tot = L.elementwise_add(tot, L.mean(L.square(o)))
+    return tot
+
+
+def case_im2sequence(x, lab, idx):
+    img = _img(x, 2, 3, 3)
+    seq = simple_op("im2sequence", {"X": [img]}, {"kernels": [2, 2], "strides": [1, 1], "paddings": [0, 1, 1, 0]})
+    return L.mean(L.square(seq))
+
+
+def case_fc_grad(x, lab, idx):
+    w = L.create_parameter([5, 4], "float32")
+    b = L.create_parameter([4], "float32")
+    o1 = simple_op("fc", {"Input": [x], "W": [w], "Bias": [b]}, {"in_num_col_dims": 1, "activation_type": "relu"})
+    o2 = simple_op("fc", {"Input": [x], "W": [w]}, {"in_num_col_dims": 1, "activation_type": ""})
+    return L.elementwise_add(L.mean(L.square(o1)), L.mean(o2))
+
+
 CASES = {k[5:]: v for k, v in globals().items() if k.startswith("case_")}
 
 
