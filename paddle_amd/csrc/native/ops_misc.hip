@@ -692,13 +692,15 @@ void k_gather_grad(const OpRun& r) {
 }
 
 template <class I>
-struct ScatterRows {  // overwrite (in index order on the host; last writer wins, as index_put)
+struct ScatterRows {  // overwrite: the LAST update of a repeated id wins (index_put's host order)
   const float* up;
   const I* idx;
   float* o;
-  int64_t W, rows;
+  int64_t W, rows, n;
   __host__ __device__ void operator()(int64_t i) const {
     const int64_t k = i / W, dst = (int64_t)idx[k];
+    for (int64_t j = k + 1; j < n; ++j)  // a later write to the same row owns it (parallel-safe)
+      if ((int64_t)idx[j] == dst) return;
     if (dst >= 0 && dst < rows) o[dst * W + i % W] = up[i];
   }
 };
@@ -710,7 +712,6 @@ void k_scatter(const OpRun& r) {
   Tensor& up = r.in("Updates");
   if ((idx.device >= 0) != dev) throw Decline{};
   const bool overwrite = r.op.GetBool("overwrite", true);
-  if (overwrite && dev) throw Decline{};  // duplicate ids: the write order is the interpreter's
   const int64_t rows = x.dims[0], W = x.numel() / std::max<int64_t>(rows, 1), n = idx.numel();
   if (up.numel() != n * W) throw Decline{};
   Tensor o;
@@ -719,8 +720,8 @@ void k_scatter(const OpRun& r) {
   const float* upp = f32(up, dev);
   const int64_t grain = dev ? 4096 : kSerial;
   if (overwrite) {
-    by_index(idx, [&](const int64_t* p) { any::run(r, dev, n * W, ScatterRows<int64_t>{upp, p, op, W, rows}, grain); },
-             [&](const int32_t* p) { any::run(r, dev, n * W, ScatterRows<int32_t>{upp, p, op, W, rows}, grain); });
+    by_index(idx, [&](const int64_t* p) { any::run(r, dev, n * W, ScatterRows<int64_t>{upp, p, op, W, rows, n}, grain); },
+             [&](const int32_t* p) { any::run(r, dev, n * W, ScatterRows<int32_t>{upp, p, op, W, rows, n}, grain); });
   } else {
     by_index(idx, [&](const int64_t* p) { any::run(r, dev, n * W, ScatterAddRows<int64_t>{upp, p, op, W, rows}, grain); },
              [&](const int32_t* p) { any::run(r, dev, n * W, ScatterAddRows<int32_t>{upp, p, op, W, rows}, grain); });
