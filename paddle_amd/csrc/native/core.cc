@@ -653,6 +653,7 @@ Executor::Executor(int device) {
   link_loss_kernels();
   link_misc_kernels();
   link_more_kernels();
+  link_extra_kernels();
 }
 
 Executor::~Executor() {

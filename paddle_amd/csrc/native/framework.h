@@ -249,6 +249,7 @@ void link_conv3d_kernels();
 void link_loss_kernels();
 void link_misc_kernels();
 void link_more_kernels();
+void link_extra_kernels();
 
 // ---------------------------------------------------------------- executor
 class Executor {

@@ -1,5 +1,6 @@
-// conv3d / conv3d_grad and pool3d / pool3d_grad (NCDHW) on the native executor,
-// host AND device.
+// conv3d / conv3d_grad, pool3d / pool3d_grad (NCDHW) and the transposed convolutions
+// conv2d_transpose / depthwise_conv2d_transpose / conv3d_transpose (+grads) on the
+// native executor, host AND device.
 //
 // Semantics: reference operators/conv_op.h GemmConvKernel / GemmConvGradKernel with
 // math/vol2col.{cc,cu} (a column matrix of [C/g * kd * kh * kw, OD * OH * OW] per
@@ -41,14 +42,15 @@ struct Conv3 {
   int geo[19];
 };
 
-Conv3 conv3_of(const OpRun& r, const Dims& xd, const Dims& wd) {
-  PA_CHECK(xd.size() == 5 && wd.size() == 5, "conv3d: NCDHW input and [OC, C/g, kd, kh, kw] filter expected");
-  const auto st = ints3(r, "strides", 1), pd = ints3(r, "paddings", 0), dl = ints3(r, "dilations", 1);
+// the GEMM-conv geometry of input [N, C, D, H, W] and filter [OC, C/g, kd, kh, kw]
+Conv3 conv3_make(const char* op, const Dims& xd, const Dims& wd, const Dims& st, const Dims& pd, const Dims& dl,
+                 int64_t G) {
+  PA_CHECK(xd.size() == 5 && wd.size() == 5, "%s: NCDHW input and [OC, C/g, kd, kh, kw] filter expected", op);
   Conv3 c;
-  c.G = std::max<int64_t>(1, r.op.GetInt("groups", 1));
+  c.G = std::max<int64_t>(1, G);
   c.N = xd[0]; c.C = xd[1]; c.D = xd[2]; c.H = xd[3]; c.W = xd[4];
   c.OC = wd[0]; c.kd = wd[2]; c.kh = wd[3]; c.kw = wd[4];
-  PA_CHECK(wd[1] * c.G == c.C && c.OC % c.G == 0, "conv3d: filter / input channel mismatch");
+  PA_CHECK(wd[1] * c.G == c.C && c.OC % c.G == 0, "%s: filter / input channel mismatch", op);
   const int64_t k[3] = {c.kd, c.kh, c.kw}, in[3] = {c.D, c.H, c.W};
   int64_t o[3];
   for (int i = 0; i < 3; ++i) {
@@ -56,7 +58,7 @@ Conv3 conv3_of(const OpRun& r, const Dims& xd, const Dims& wd) {
     c.pd[i] = pd[(size_t)i];
     c.dl[i] = dl[(size_t)i];
     o[i] = (in[i] + 2 * pd[(size_t)i] - (dl[(size_t)i] * (k[i] - 1) + 1)) / st[(size_t)i] + 1;
-    PA_CHECK(o[i] > 0, "conv3d: empty output");
+    PA_CHECK(o[i] > 0, "%s: empty output", op);
   }
   c.OD = o[0]; c.OH = o[1]; c.OW = o[2];
   c.Cg = c.C / c.G; c.OCg = c.OC / c.G;
@@ -67,6 +69,11 @@ Conv3 conv3_of(const OpRun& r, const Dims& xd, const Dims& wd) {
                          pd[0], pd[1], pd[2], dl[0], dl[1], dl[2]};
   for (int i = 0; i < 19; ++i) c.geo[i] = (int)g[i];
   return c;
+}
+
+Conv3 conv3_of(const OpRun& r, const Dims& xd, const Dims& wd) {
+  return conv3_make("conv3d", xd, wd, ints3(r, "strides", 1), ints3(r, "paddings", 0), ints3(r, "dilations", 1),
+                    r.op.GetInt("groups", 1));
 }
 
 // ---------------------------------------------------------------- host vol2col
@@ -122,13 +129,10 @@ float* f32h(const Tensor& t) {
   return t.data<float>();
 }
 
-void k_conv3d_host(const OpRun& r) {
-  Tensor x = r.in("Input");
-  Tensor w = r.in("Filter");
-  Tensor* b = r.in_opt("Bias");
-  const Conv3 c = conv3_of(r, x.dims, w.dims);
-  float* y = r.out("Output")->alloc<float>({c.N, c.OC, c.OD, c.OH, c.OW}, -1);
-  const float *xp = f32h(x), *wp = f32h(w), *bp = b ? f32h(*b) : nullptr;
+// The three GEMM-conv passes, parameterised by role so that conv3d and the
+// transposed convolutions (whose forward is a conv's data gradient) share them.
+// y = conv(x, w) (+ bias)
+void conv_fwd_h(const Conv3& c, const float* xp, const float* wp, const float* bp, float* y) {
   std::vector<float> col((size_t)(c.K * c.S));
   for (int64_t n = 0; n < c.N; ++n)
     for (int64_t g = 0; g < c.G; ++g) {
@@ -141,6 +145,39 @@ void k_conv3d_host(const OpRun& r) {
     }
 }
 
+// dx = conv's data gradient of dy (dx overwritten)
+void conv_dx_h(const Conv3& c, const float* wp, const float* gp, float* dx) {
+  memset(dx, 0, sizeof(float) * (size_t)(c.N * c.C * c.I));
+  std::vector<float> col((size_t)(c.K * c.S));
+  for (int64_t n = 0; n < c.N; ++n)
+    for (int64_t g = 0; g < c.G; ++g) {
+      sgemm(true, false, c.K, c.S, c.OCg, 1.f, wp + g * c.OCg * c.K, c.K, gp + (n * c.OC + g * c.OCg) * c.S, c.S,
+            0.f, col.data(), c.S);
+      col2vol_add(c, col.data(), dx + (n * c.C + g * c.Cg) * c.I);
+    }
+}
+
+// dw = conv's filter gradient of (x, dy) (dw overwritten)
+void conv_dw_h(const Conv3& c, const float* xp, const float* gp, float* dw) {
+  memset(dw, 0, sizeof(float) * (size_t)(c.OC * c.K));
+  std::vector<float> col((size_t)(c.K * c.S));
+  for (int64_t n = 0; n < c.N; ++n)
+    for (int64_t g = 0; g < c.G; ++g) {
+      vol2col(c, xp + (n * c.C + g * c.Cg) * c.I, col.data());
+      sgemm(false, true, c.OCg, c.K, c.S, 1.f, gp + (n * c.OC + g * c.OCg) * c.S, c.S, col.data(), c.S, 1.f,
+            dw + g * c.OCg * c.K, c.K);
+    }
+}
+
+void k_conv3d_host(const OpRun& r) {
+  Tensor x = r.in("Input");
+  Tensor w = r.in("Filter");
+  Tensor* b = r.in_opt("Bias");
+  const Conv3 c = conv3_of(r, x.dims, w.dims);
+  const float *xp = f32h(x), *wp = f32h(w), *bp = b ? f32h(*b) : nullptr;
+  conv_fwd_h(c, xp, wp, bp, r.out("Output")->alloc<float>({c.N, c.OC, c.OD, c.OH, c.OW}, -1));
+}
+
 void k_conv3d_grad_host(const OpRun& r) {
   Tensor x = r.in("Input");
   Tensor w = r.in("Filter");
@@ -151,23 +188,8 @@ void k_conv3d_grad_host(const OpRun& r) {
   Tensor* dxt = r.out("Input@GRAD");
   Tensor* dwt = r.out("Filter@GRAD");
   Tensor* dbt = r.out("Bias@GRAD");
-  float* dx = dxt ? dxt->alloc<float>(x.dims, -1) : nullptr;
-  float* dw = dwt ? dwt->alloc<float>(w.dims, -1) : nullptr;
-  if (dx) memset(dx, 0, sizeof(float) * (size_t)x.numel());
-  if (dw) memset(dw, 0, sizeof(float) * (size_t)w.numel());
-  std::vector<float> col((size_t)(c.K * c.S));
-  for (int64_t n = 0; n < c.N; ++n)
-    for (int64_t g = 0; g < c.G; ++g) {
-      const float* dyg = gp + (n * c.OC + g * c.OCg) * c.S;
-      if (dw) {
-        vol2col(c, xp + (n * c.C + g * c.Cg) * c.I, col.data());
-        sgemm(false, true, c.OCg, c.K, c.S, 1.f, dyg, c.S, col.data(), c.S, 1.f, dw + g * c.OCg * c.K, c.K);
-      }
-      if (dx) {
-        sgemm(true, false, c.K, c.S, c.OCg, 1.f, wp + g * c.OCg * c.K, c.K, dyg, c.S, 0.f, col.data(), c.S);
-        col2vol_add(c, col.data(), dx + (n * c.C + g * c.Cg) * c.I);
-      }
-    }
+  if (dxt) conv_dx_h(c, wp, gp, dxt->alloc<float>(x.dims, -1));
+  if (dwt) conv_dw_h(c, xp, gp, dwt->alloc<float>(w.dims, -1));
   if (dbt) {
     float* db = dbt->alloc<float>({c.OC}, -1);
     for (int64_t o = 0; o < c.OC; ++o) {
@@ -195,13 +217,7 @@ void sg(const OpRun& r, const float* A, long sam, long sak, const float* B, long
                  1.f, 0.f, atomic, nullptr, dev_stream(r)));
 }
 
-void k_conv3d_dev(const OpRun& r) {
-  Tensor x = r.in("Input");
-  Tensor w = r.in("Filter");
-  Tensor* b = r.in_opt("Bias");
-  const Conv3 c = conv3_of(r, x.dims, w.dims);
-  float* y = r.out("Output")->alloc<float>({c.N, c.OC, c.OD, c.OH, c.OW}, dev_id(r));
-  const float *xp = dev_f32(x), *wp = dev_f32(w), *bp = b ? dev_f32(*b) : nullptr;
+void conv_fwd_d(const OpRun& r, const Conv3& c, const float* xp, const float* wp, const float* bp, float* y) {
   const int64_t nb = chunk(c), rows = c.C * c.kd * c.kh * c.kw;
   float* col = device_workspace(r, "@conv_col@", nb * rows * c.S);
   for (int64_t n0 = 0; n0 < c.N; n0 += nb) {
@@ -212,6 +228,38 @@ void k_conv3d_dev(const OpRun& r) {
   }
 }
 
+void conv_dx_d(const OpRun& r, const Conv3& c, const float* wp, const float* gp, float* dx) {
+  const int64_t nb = chunk(c), rows = c.C * c.kd * c.kh * c.kw;
+  float* col = device_workspace(r, "@conv_col@", nb * rows * c.S);
+  for (int64_t n0 = 0; n0 < c.N; n0 += nb) {
+    const int m = (int)std::min(nb, c.N - n0);
+    sg(r, wp, 1, c.K, gp + n0 * c.OC * c.S, c.S, 1, col, c.S, c.K, c.S, c.OCg, m, (int)c.G, 0, c.OC * c.S,
+       rows * c.S, c.OCg * c.K, c.OCg * c.S, c.K * c.S);
+    PA_KL(pa_col2vol(col, dx + n0 * c.C * c.I, c.geo, m, 0, dev_stream(r)));
+  }
+}
+
+void conv_dw_d(const OpRun& r, const Conv3& c, const float* xp, const float* gp, float* dw) {
+  const int64_t nb = chunk(c), rows = c.C * c.kd * c.kh * c.kw;
+  float* col = device_workspace(r, "@conv_col@", nb * rows * c.S);
+  PA_HIPCHK(hipMemsetAsync(dw, 0, sizeof(float) * (size_t)(c.OC * c.K), dev_stream(r)));
+  for (int64_t n0 = 0; n0 < c.N; n0 += nb) {
+    const int m = (int)std::min(nb, c.N - n0);
+    PA_KL(pa_vol2col(0, xp + n0 * c.C * c.I, col, c.geo, m, dev_stream(r)));
+    sg(r, gp + n0 * c.OC * c.S, c.S, 1, col, 1, c.S, dw, c.K, c.OCg, c.K, c.S, 1, (int)c.G, 0, 0, 0,
+       c.OCg * c.S, c.K * c.S, c.OCg * c.K, m, c.OC * c.S, rows * c.S, nullptr, 0, 1);
+  }
+}
+
+void k_conv3d_dev(const OpRun& r) {
+  Tensor x = r.in("Input");
+  Tensor w = r.in("Filter");
+  Tensor* b = r.in_opt("Bias");
+  const Conv3 c = conv3_of(r, x.dims, w.dims);
+  float* y = r.out("Output")->alloc<float>({c.N, c.OC, c.OD, c.OH, c.OW}, dev_id(r));
+  conv_fwd_d(r, c, dev_f32(x), dev_f32(w), b ? dev_f32(*b) : nullptr, y);
+}
+
 void k_conv3d_grad_dev(const OpRun& r) {
   Tensor x = r.in("Input");
   Tensor w = r.in("Filter");
@@ -219,32 +267,92 @@ void k_conv3d_grad_dev(const OpRun& r) {
   const Conv3 c = conv3_of(r, x.dims, w.dims);
   PA_CHECK(dy.numel() == c.N * c.OC * c.S, "conv3d_grad: Output@GRAD %s does not match", dy.shape_str().c_str());
   const float *xp = dev_f32(x), *wp = dev_f32(w), *gp = dev_f32(dy);
-  const int64_t nb = chunk(c), rows = c.C * c.kd * c.kh * c.kw;
   Tensor* dxt = r.out("Input@GRAD");
   Tensor* dwt = r.out("Filter@GRAD");
   Tensor* dbt = r.out("Bias@GRAD");
-  hipStream_t s = dev_stream(r);
-  float* col = (dxt || dwt) ? device_workspace(r, "@conv_col@", nb * rows * c.S) : nullptr;
-  if (dxt) {
-    float* dx = dxt->alloc<float>(x.dims, dev_id(r));
-    for (int64_t n0 = 0; n0 < c.N; n0 += nb) {
-      const int m = (int)std::min(nb, c.N - n0);
-      sg(r, wp, 1, c.K, gp + n0 * c.OC * c.S, c.S, 1, col, c.S, c.K, c.S, c.OCg, m, (int)c.G, 0, c.OC * c.S,
-         rows * c.S, c.OCg * c.K, c.OCg * c.S, c.K * c.S);
-      PA_KL(pa_col2vol(col, dx + n0 * c.C * c.I, c.geo, m, 0, s));
-    }
+  if (dxt) conv_dx_d(r, c, wp, gp, dxt->alloc<float>(x.dims, dev_id(r)));
+  if (dwt) conv_dw_d(r, c, xp, gp, dwt->alloc<float>(w.dims, dev_id(r)));
+  if (dbt) PA_KL(pa_chan_sum(gp, dbt->alloc<float>({c.OC}, dev_id(r)), (int)c.N, (int)c.OC, c.S, 0, dev_stream(r)));
+}
+
+// ---------------------------------------------------------------- transposed convolution
+// conv{2,3}d_transpose / depthwise_conv2d_transpose (reference operators/
+// conv_transpose_op.h: col = W^T x per image and group, col2im into the output).
+// Input [N, Cin, (D,) H, W], Filter [Cin, OC/g, (kd,) kh, kw]; the output extent is
+// (in - 1) * stride - 2 pad + dilation (k - 1) + 1.  Computed as the data gradient of
+// the conv that maps the output back onto the input (that conv's filter is exactly
+// Filter), so forward = conv dgrad, Input@GRAD = conv forward of Output@GRAD and
+// Filter@GRAD = that conv's wgrad of (Output@GRAD, Input).  2-D ops run as depth 1.
+struct ConvT {
+  Conv3 c;       // the conv from the transposed op's output to its input
+  Dims out;      // the transposed op's output dims
+};
+
+ConvT convt_of(const OpRun& r, const Dims& xd0, const Dims& wd0) {
+  const bool two = xd0.size() == 4;
+  const char* op = r.op.type.c_str();
+  PA_CHECK((two && wd0.size() == 4) || (xd0.size() == 5 && wd0.size() == 5),
+           "%s: NC(D)HW input and [Cin, OC/g, (kd,) kh, kw] filter expected", op);
+  const size_t nd = two ? 2 : 3;
+  auto attr = [&](const char* name, int64_t def) {
+    auto v = r.op.GetInts(name);
+    if (v.empty()) v.assign(nd, def);
+    PA_CHECK(v.size() == nd, "%s: %s must have %d values", op, name, (int)nd);
+    if (two) v.insert(v.begin(), name[0] == 'p' ? 0 : 1);
+    return v;
+  };
+  const Dims st = attr("strides", 1), pd = attr("paddings", 0), dl = attr("dilations", 1);
+  Dims xd = xd0, wd = wd0;
+  if (two) {
+    xd.insert(xd.begin() + 2, 1);
+    wd.insert(wd.begin() + 2, 1);
   }
-  if (dwt) {
-    float* dw = dwt->alloc<float>(w.dims, dev_id(r));
-    PA_HIPCHK(hipMemsetAsync(dw, 0, sizeof(float) * (size_t)w.numel(), s));
-    for (int64_t n0 = 0; n0 < c.N; n0 += nb) {
-      const int m = (int)std::min(nb, c.N - n0);
-      PA_KL(pa_vol2col(0, xp + n0 * c.C * c.I, col, c.geo, m, s));
-      sg(r, gp + n0 * c.OC * c.S, c.S, 1, col, 1, c.S, dw, c.K, c.OCg, c.K, c.S, 1, (int)c.G, 0, 0, 0,
-         c.OCg * c.S, c.K * c.S, c.OCg * c.K, m, c.OC * c.S, rows * c.S, nullptr, 0, 1);
-    }
+  const int64_t G = std::max<int64_t>(1, r.op.GetInt("groups", 1));
+  Dims yd = {xd[0], wd[1] * G};
+  for (int i = 0; i < 3; ++i) {
+    const int64_t o = (xd[(size_t)i + 2] - 1) * st[(size_t)i] - 2 * pd[(size_t)i] +
+                      dl[(size_t)i] * (wd[(size_t)i + 2] - 1) + 1;
+    PA_CHECK(o > 0, "%s: empty output", op);
+    yd.push_back(o);
   }
-  if (dbt) PA_KL(pa_chan_sum(gp, dbt->alloc<float>({c.OC}, dev_id(r)), (int)c.N, (int)c.OC, c.S, 0, s));
+  const auto osz = r.op.GetInts("output_size");
+  for (size_t i = 0; i < osz.size(); ++i)
+    if (osz[i] != yd[yd.size() - osz.size() + i]) throw Decline{};  // trimmed output sizes: the embedder's kernel
+  ConvT t;
+  t.c = conv3_make(op, yd, wd, st, pd, dl, G);
+  PA_CHECK(t.c.OD == xd[2] && t.c.OH == xd[3] && t.c.OW == xd[4] && t.c.OC == xd[1], "%s: geometry mismatch", op);
+  t.out = yd;
+  if (two) t.out.erase(t.out.begin() + 2);
+  return t;
+}
+
+void k_convt(const OpRun& r) {
+  Tensor x = r.in("Input");
+  Tensor w = r.in("Filter");
+  const ConvT t = convt_of(r, x.dims, w.dims);
+  const bool dev = x.device >= 0;
+  float* y = r.out("Output")->alloc<float>(t.out, dev ? dev_id(r) : -1);
+  if (dev) conv_dx_d(r, t.c, dev_f32(w), dev_f32(x), y);
+  else conv_dx_h(t.c, f32h(w), f32h(x), y);
+}
+
+void k_convt_grad(const OpRun& r) {
+  Tensor x = r.in("Input");
+  Tensor w = r.in("Filter");
+  Tensor dy = r.in("Output@GRAD");
+  const ConvT t = convt_of(r, x.dims, w.dims);
+  PA_CHECK(dy.numel() == t.c.N * t.c.C * t.c.I, "%s: Output@GRAD %s does not match", r.op.type.c_str(),
+           dy.shape_str().c_str());
+  const bool dev = x.device >= 0;
+  Tensor* dxt = r.op.Outputs("Input@GRAD").empty() ? nullptr : r.out("Input@GRAD");
+  Tensor* dwt = r.op.Outputs("Filter@GRAD").empty() ? nullptr : r.out("Filter@GRAD");
+  if (dev) {
+    if (dxt) conv_fwd_d(r, t.c, dev_f32(dy), dev_f32(w), nullptr, dxt->alloc<float>(x.dims, dev_id(r)));
+    if (dwt) conv_dw_d(r, t.c, dev_f32(dy), dev_f32(x), dwt->alloc<float>(w.dims, dev_id(r)));
+  } else {
+    if (dxt) conv_fwd_h(t.c, f32h(dy), f32h(w), nullptr, dxt->alloc<float>(x.dims, -1));
+    if (dwt) conv_dw_h(t.c, f32h(dy), f32h(x), dwt->alloc<float>(w.dims, -1));
+  }
 }
 
 // ---------------------------------------------------------------- pool3d
@@ -417,6 +525,14 @@ PA_DEVICE_KERNEL(conv3d, k_conv3d_dev);
 PA_DEVICE_KERNEL(conv3d_grad, k_conv3d_grad_dev);
 PA_DEVICE_KERNEL(pool3d, k_pool3d_dev);
 PA_DEVICE_KERNEL(pool3d_grad, k_pool3d_grad_dev);
+#define PA_CONVT(name)             \
+  PA_HOST_KERNEL(name, k_convt);   \
+  PA_DEVICE_KERNEL(name, k_convt); \
+  PA_HOST_KERNEL(name##_grad, k_convt_grad); \
+  PA_DEVICE_KERNEL(name##_grad, k_convt_grad)
+PA_CONVT(conv2d_transpose);
+PA_CONVT(depthwise_conv2d_transpose);
+PA_CONVT(conv3d_transpose);
 
 void link_conv3d_kernels() {}
 

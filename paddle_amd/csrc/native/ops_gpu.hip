@@ -1741,7 +1741,14 @@ template <bool GAUSS> void k_random(const OpRun& r) {
   const DT dt = (DT)r.op.GetInt("dtype", (int)DT::FP32);
   if (dt != DT::FP32) throw Decline();
   Tensor* o = r.out("Out");
-  float* p = o->alloc<float>(r.op.GetInts("shape"), D(r));
+  Dims shape = r.op.GetInts("shape");
+  if (r.op.type.find("batch_size_like") != std::string::npos) {  // batch_size_like.h
+    const Tensor& in = r.in("Input");
+    const size_t oi = (size_t)r.op.GetInt("output_dim_idx", 0), ii = (size_t)r.op.GetInt("input_dim_idx", 0);
+    PA_CHECK(oi < shape.size() && ii < in.dims.size(), "%s: dim index out of range", r.op.type.c_str());
+    shape[oi] = in.dims[ii];
+  }
+  float* p = o->alloc<float>(shape, D(r));
   const int64_t s = r.op.GetInt("seed");
   const uint64_t seed = s ? (uint64_t)s : r.ctx.rng();
   const float a = GAUSS ? r.op.GetFloat("mean", 0.f) : r.op.GetFloat("min", -1.f);
@@ -1811,6 +1818,8 @@ PA_DEVICE_KERNEL(assign, k_assign);
 PA_DEVICE_KERNEL(cast, k_cast);
 PA_DEVICE_KERNEL(uniform_random, k_random<false>);
 PA_DEVICE_KERNEL(gaussian_random, k_random<true>);
+PA_DEVICE_KERNEL(uniform_random_batch_size_like, k_random<false>);
+PA_DEVICE_KERNEL(gaussian_random_batch_size_like, k_random<true>);
 
 // =============================================================== row movement for ops_control.cc
 namespace {

@@ -74,9 +74,21 @@ void k_fill_constant(const OpRun& r) {
   }
 }
 
+// the shape attr; the *_batch_size_like forms take shape[output_dim_idx] from
+// Input.dims[input_dim_idx] (batch_size_like.h)
+Dims random_shape(const OpRun& r) {
+  Dims shape = r.op.GetInts("shape");
+  if (r.op.type.find("batch_size_like") == std::string::npos) return shape;
+  const Tensor& in = r.in("Input");
+  const size_t oi = (size_t)r.op.GetInt("output_dim_idx", 0), ii = (size_t)r.op.GetInt("input_dim_idx", 0);
+  PA_CHECK(oi < shape.size() && ii < in.dims.size(), "%s: dim index out of range", r.op.type.c_str());
+  shape[oi] = in.dims[ii];
+  return shape;
+}
+
 void k_uniform_random(const OpRun& r) {
   Tensor* o = r.out("Out");
-  float* p = o->alloc<float>(r.op.GetInts("shape"), -1);
+  float* p = o->alloc<float>(random_shape(r), -1);
   const int64_t seed = r.op.GetInt("seed");
   std::mt19937_64 g(seed ? (uint64_t)seed : r.ctx.rng());
   std::uniform_real_distribution<float> d(r.op.GetFloat("min", -1.f), r.op.GetFloat("max", 1.f));
@@ -85,7 +97,7 @@ void k_uniform_random(const OpRun& r) {
 
 void k_gaussian_random(const OpRun& r) {
   Tensor* o = r.out("Out");
-  float* p = o->alloc<float>(r.op.GetInts("shape"), -1);
+  float* p = o->alloc<float>(random_shape(r), -1);
   const int64_t seed = r.op.GetInt("seed");
   std::mt19937_64 g(seed ? (uint64_t)seed : r.ctx.rng());
   std::normal_distribution<float> d(r.op.GetFloat("mean", 0.f), r.op.GetFloat("std", 1.f));
@@ -319,7 +331,7 @@ Bc broadcast(const Dims& x, const Dims& y0, int64_t axis) {
   return b;
 }
 
-template <class F> void ew_apply(const Bc& b, const float* x, const float* y, float* o, F f) {
+template <class T, class F> void ew_apply(const Bc& b, const T* x, const T* y, T* o, F f) {
   const int64_t n = prod(b.out);
   const size_t R = b.out.size();
   if (R == 0) {
@@ -337,11 +349,11 @@ template <class F> void ew_apply(const Bc& b, const float* x, const float* y, fl
         ox += k * b.sx[d];
         oy += k * b.sy[d];
       }
-      float* op = o + row * inner;
+      T* op = o + row * inner;
       if (ix == 1 && iy == 1)
         for (int64_t j = 0; j < inner; ++j) op[j] = f(x[ox + j], y[oy + j]);
       else if (ix == 1 && iy == 0) {
-        const float yv = y[oy];
+        const T yv = y[oy];
         for (int64_t j = 0; j < inner; ++j) op[j] = f(x[ox + j], yv);
       } else
         for (int64_t j = 0; j < inner; ++j) op[j] = f(x[ox + j * ix], y[oy + j * iy]);
@@ -357,7 +369,15 @@ template <class F> Kernel ew_kernel(F f) {
     LoD lod = x.lod;
     Tensor* o = r.out("Out");
     Tensor xs = x, ys = y;  // keep inputs alive if Out aliases one of them
-    ew_apply(b, f32(xs), f32(ys), o->alloc<float>(b.out, -1), f);
+    if (xs.dtype == DT::FP32 || ys.dtype != xs.dtype || xs.device >= 0 || ys.device >= 0) {
+      ew_apply(b, f32(xs), f32(ys), o->alloc<float>(b.out, -1), f);
+    } else if (xs.dtype == DT::INT64) {  // integer index arithmetic (elementwise_op.h int kernels)
+      ew_apply(b, xs.data<int64_t>(), ys.data<int64_t>(), static_cast<int64_t*>(o->alloc(DT::INT64, b.out, -1)), f);
+    } else if (xs.dtype == DT::INT32) {
+      ew_apply(b, xs.data<int32_t>(), ys.data<int32_t>(), static_cast<int32_t*>(o->alloc(DT::INT32, b.out, -1)), f);
+    } else {
+      throw Decline{};
+    }
     o->lod = lod;
   };
 }
@@ -1116,10 +1136,11 @@ void k_dropout(const OpRun& r) {
     float* mk = mt ? mt->alloc<float>(d, -1) : nullptr;
     std::uniform_real_distribution<float> u(0.f, 1.f);
     for (int64_t i = 0; i < n; ++i) {
+      // Mask holds 0 / 1 (dropout_op.h); the upscale factor applies to Out and, in
+      // dropout_grad, to the gradient
       const bool keep = u(r.ctx.rng) >= p;
-      const float m = keep ? (upscale ? 1.f / (1.f - p) : 1.f) : 0.f;
-      if (mk) mk[i] = m;
-      op[i] = xp[i] * m;
+      if (mk) mk[i] = keep ? 1.f : 0.f;
+      op[i] = keep ? xp[i] * (upscale && p < 1.f ? 1.f / (1.f - p) : 1.f) : 0.f;
     }
   }
   o->lod = lod;
@@ -1775,6 +1796,8 @@ PA_HOST_KERNEL(fetch, k_fetch);
 PA_HOST_KERNEL(fill_constant, k_fill_constant);
 PA_HOST_KERNEL(uniform_random, k_uniform_random);
 PA_HOST_KERNEL(gaussian_random, k_gaussian_random);
+PA_HOST_KERNEL(uniform_random_batch_size_like, k_uniform_random);
+PA_HOST_KERNEL(gaussian_random_batch_size_like, k_gaussian_random);
 PA_HOST_KERNEL(assign, k_assign);
 PA_HOST_KERNEL(shape, k_shape);
 PA_HOST_KERNEL(cast, k_cast);
@@ -1782,13 +1805,13 @@ PA_HOST_KERNEL(mul, k_mul);
 PA_HOST_KERNEL(mul_grad, k_mul_grad);
 PA_HOST_KERNEL(matmul, k_matmul);
 PA_HOST_KERNEL(fc, k_fc);
-PA_HOST_KERNEL(elementwise_add, ew_kernel([](float a, float b) { return a + b; }));
-PA_HOST_KERNEL(elementwise_sub, ew_kernel([](float a, float b) { return a - b; }));
-PA_HOST_KERNEL(elementwise_mul, ew_kernel([](float a, float b) { return a * b; }));
-PA_HOST_KERNEL(elementwise_div, ew_kernel([](float a, float b) { return a / b; }));
-PA_HOST_KERNEL(elementwise_max, ew_kernel([](float a, float b) { return a > b ? a : b; }));
-PA_HOST_KERNEL(elementwise_min, ew_kernel([](float a, float b) { return a < b ? a : b; }));
-PA_HOST_KERNEL(elementwise_pow, ew_kernel([](float a, float b) { return powf(a, b); }));
+PA_HOST_KERNEL(elementwise_add, ew_kernel([](auto a, auto b) { return a + b; }));
+PA_HOST_KERNEL(elementwise_sub, ew_kernel([](auto a, auto b) { return a - b; }));
+PA_HOST_KERNEL(elementwise_mul, ew_kernel([](auto a, auto b) { return a * b; }));
+PA_HOST_KERNEL(elementwise_div, ew_kernel([](auto a, auto b) { return a / b; }));
+PA_HOST_KERNEL(elementwise_max, ew_kernel([](auto a, auto b) { return a > b ? a : b; }));
+PA_HOST_KERNEL(elementwise_min, ew_kernel([](auto a, auto b) { return a < b ? a : b; }));
+PA_HOST_KERNEL(elementwise_pow, ew_kernel([](auto a, auto b) { return (decltype(a))powf((float)a, (float)b); }));
 PA_HOST_KERNEL(elementwise_add_grad, k_ew_grad<0>);
 PA_HOST_KERNEL(elementwise_sub_grad, k_ew_grad<1>);
 PA_HOST_KERNEL(elementwise_mul_grad, k_ew_grad<2>);

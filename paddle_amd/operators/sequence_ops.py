@@ -366,11 +366,12 @@ def lod_reset(ctx):
 def sequence_scatter(ctx):
     x, ids, up = ctx.input("X"), ctx.input("Ids"), ctx.input("Updates")
     off = ctx.input_lod("Ids")[0]
-    out = x.clone()
-    for i in range(len(off) - 1):
-        cols = ids[off[i]:off[i + 1]].reshape(-1).long()
-        out[i].index_add_(0, cols, up[off[i]:off[i + 1]].reshape(-1))
-    ctx.set_output("Out", out)
+    # one out-of-place accumulating index_put: differentiable in X and Updates
+    # (sequence_scatter_op.h: Updates@GRAD[k] = Out@GRAD[seq(k), Ids[k]])
+    rows = torch.repeat_interleave(torch.arange(len(off) - 1, device=x.device),
+                                   torch.tensor([off[i + 1] - off[i] for i in range(len(off) - 1)], device=x.device))
+    cols = ids.reshape(-1).long()
+    ctx.set_output("Out", x.index_put((rows, cols), up.reshape(-1).to(x.dtype), accumulate=True))
 
 
 @register_op("sequence_reverse", ["X"], ["Y"], {})
