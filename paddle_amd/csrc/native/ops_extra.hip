@@ -2,8 +2,12 @@
 // remaining random / quantisation / averaging ops of the native executor, host AND
 // device from one source (any_place.h): prior_box, anchor_generator, spp (+grad),
 // fused_elemwise_activation (+grad), auc, precision_recall, positive_negative_pair,
-// average_accumulates, fake_quantize_range_abs_max, bipartite_match, target_assign;
-// plus the host twins of the device-only layer_norm (+grad) and dropout_grad.
+// average_accumulates, fake_quantize_range_abs_max, bipartite_match, target_assign,
+// reduce_*_grad, elementwise_{max,min,pow}_grad, elementwise_{floordiv,mod},
+// sequence_reverse / sequence_scatter (+grads), kldiv_loss / bpr_loss (+grads),
+// shuffle_channel / scale_sub_region (+grads), size, lars_momentum,
+// max_pool3d_with_index (+grad), chunk_eval, sampling_id, random_crop, print; plus the
+// host twins of the device-only layer_norm (+grad) and dropout_grad.
 //
 // Semantics: reference operators/detection/{prior_box,anchor_generator,
 // bipartite_match,target_assign}_op.h, operators/{spp,fused_elemwise_activation,auc,
@@ -19,7 +23,11 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <stdio.h>
+#include <string.h>
+
 #include <algorithm>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -1673,6 +1681,356 @@ void k_lars_momentum(const OpRun& r) {
   set(r, "VelocityOut", vo);
 }
 
+// ---------------------------------------------------------------- max_pool3d_with_index
+// pooling_op.h MaxPool3dWithIndexFunctor: the window's first maximum and its flat
+// index inside the [D, H, W] volume; the gradient scatters back through that index
+__host__ __device__ inline void acc_add(float* p, float v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  atomicAdd(p, v);
+#else
+  *p += v;
+#endif
+}
+struct MaxPool3Idx {
+  const float* x;
+  float* o;
+  int32_t* mask;
+  int64_t in[3], out[3], k[3], st[3], pd[3];
+  __host__ __device__ void operator()(int64_t t) const {
+    const int64_t ow = t % out[2], oh = (t / out[2]) % out[1], od = (t / (out[2] * out[1])) % out[0],
+                  plane = t / (out[0] * out[1] * out[2]);
+    const float* p = x + plane * in[0] * in[1] * in[2];
+    float best = -INFINITY;
+    int64_t bi = -1;
+    for (int64_t a = 0; a < k[0]; ++a)
+      for (int64_t b = 0; b < k[1]; ++b)
+        for (int64_t c = 0; c < k[2]; ++c) {
+          const int64_t d = od * st[0] - pd[0] + a, h = oh * st[1] - pd[1] + b, w = ow * st[2] - pd[2] + c;
+          if (d < 0 || d >= in[0] || h < 0 || h >= in[1] || w < 0 || w >= in[2]) continue;
+          const int64_t at = (d * in[1] + h) * in[2] + w;
+          if (bi < 0 || p[at] > best) {
+            best = p[at];
+            bi = at;
+          }
+        }
+    o[t] = best;
+    mask[t] = (int32_t)bi;
+  }
+};
+struct MaxPool3IdxGrad {
+  const float* g;
+  const int32_t* mask;
+  float* dx;
+  int64_t I, O;
+  __host__ __device__ void operator()(int64_t t) const {
+    if (mask[t] >= 0) acc_add(dx + (t / O) * I + mask[t], g[t]);
+  }
+};
+
+MaxPool3Idx pool3_idx_geo(const OpRun& r, const Tensor& x) {
+  PA_CHECK(x.dims.size() == 5, "max_pool3d_with_index: NCDHW input expected");
+  auto k = r.op.GetInts("ksize"), st = r.op.GetInts("strides"), pd = r.op.GetInts("paddings");
+  if (k.size() != 3 || st.size() != 3 || pd.size() != 3) throw Decline{};
+  MaxPool3Idx g{};
+  for (int i = 0; i < 3; ++i) {
+    g.in[i] = x.dims[(size_t)i + 2];
+    g.k[i] = r.op.GetBool("global_pooling") ? g.in[i] : k[(size_t)i];
+    g.st[i] = st[(size_t)i];
+    g.pd[i] = r.op.GetBool("global_pooling") ? 0 : pd[(size_t)i];
+    g.out[i] = (g.in[i] + 2 * g.pd[i] - g.k[i]) / g.st[i] + 1;
+    PA_CHECK(g.out[i] > 0, "max_pool3d_with_index: empty output");
+  }
+  return g;
+}
+
+void k_max_pool3d_idx(const OpRun& r) {
+  const bool dev = on_dev(r);
+  const Tensor& x = r.in("X");
+  MaxPool3Idx g = pool3_idx_geo(r, x);
+  const Dims od = {x.dims[0], x.dims[1], g.out[0], g.out[1], g.out[2]};
+  Tensor o, m;
+  g.x = f32(x, dev);
+  g.o = o.alloc<float>(od, place_of(r));
+  g.mask = static_cast<int32_t*>(m.alloc(DT::INT32, od, place_of(r)));
+  any::run(r, dev, o.numel(), g);
+  set(r, "Out", o);
+  set(r, "Mask", m);
+}
+
+void k_max_pool3d_idx_grad(const OpRun& r) {
+  const bool dev = on_dev(r);
+  const Tensor& x = r.in("X");
+  const Tensor& m = r.in("Mask");
+  const Tensor& g = r.in("Out@GRAD");
+  if (m.dtype != DT::INT32 || (m.device >= 0) != dev || !wants(r, "X@GRAD")) {
+    if (!wants(r, "X@GRAD")) return;
+    throw Decline{};
+  }
+  Tensor d;
+  float* dx = d.alloc<float>(x.dims, place_of(r));
+  any::zero(r, dev, dx, x.numel());
+  const int64_t I = x.dims[2] * x.dims[3] * x.dims[4], O = g.dims[2] * g.dims[3] * g.dims[4];
+  any::run(r, dev, g.numel(), MaxPool3IdxGrad{f32(g, dev), m.data<int32_t>(), dx, I, O}, 1 << 30);
+  set(r, "X@GRAD", d);
+}
+
+// ---------------------------------------------------------------- chunk_eval
+// chunk_eval_op.h: chunks (begin, end, type) of every sequence under the IOB / IOE /
+// IOBES / plain tagging scheme (label = tag + n_tags * type, type == num_chunk_types
+// is "outside"), excluded types dropped; counts of inferred, labelled and matching
+// chunks, then precision / recall / F1.  One work item per sequence; the chunks of
+// the inference are listed in a per-sequence scratch and matched by a merge (both
+// lists come out ordered by begin).
+struct ChunkScheme {
+  int64_t ntag, tb, ti, te, ts, other;
+  const int* excl;
+  int nexcl;
+  __host__ __device__ bool ends(int64_t pt, int64_t pty, int64_t t, int64_t ty) const {
+    if (pty == other) return false;
+    if (ty == other || ty != pty) return true;
+    if (pt == tb || pt == ti) return t == tb || t == ts;
+    return pt == te || pt == ts;
+  }
+  __host__ __device__ bool begins(int64_t pt, int64_t pty, int64_t t, int64_t ty) const {
+    if (pty == other) return ty != other;
+    if (ty == other) return false;
+    if (ty != pty || t == tb || t == ts) return true;
+    if (t == ti || t == te) return pt == te || pt == ts;
+    return false;
+  }
+  __host__ __device__ bool kept(int64_t ty) const {
+    for (int k = 0; k < nexcl; ++k)
+      if (excl[k] == ty) return false;
+    return true;
+  }
+  // calls emit(begin, end, type) for every kept chunk of labels[a, b)
+  template <class E>
+  __host__ __device__ void scan(Idx v, int64_t a, int64_t b, E& emit) const {
+    int64_t tag = -1, typ = other, start = 0;
+    bool inside = false;
+    for (int64_t i = a; i < b; ++i) {
+      const int64_t pt = tag, pty = typ, lab = v[i];
+      tag = lab % ntag;
+      typ = lab / ntag;
+      if (inside && ends(pt, pty, tag, typ)) {
+        if (kept(pty)) emit(start, i - 1, pty);
+        inside = false;
+      }
+      if (begins(pt, pty, tag, typ)) {
+        start = i;
+        inside = true;
+      }
+    }
+    if (inside && kept(typ)) emit(start, b - 1, typ);
+  }
+};
+struct ChunkList {
+  int64_t* buf;
+  int64_t n;
+  __host__ __device__ void operator()(int64_t s, int64_t e, int64_t t) {
+    buf[3 * n] = s;
+    buf[3 * n + 1] = e;
+    buf[3 * n + 2] = t;
+    ++n;
+  }
+};
+struct ChunkMatch {
+  const int64_t* buf;
+  int64_t n, k, nl, nc;
+  __host__ __device__ void operator()(int64_t s, int64_t e, int64_t t) {
+    ++nl;
+    while (k < n && buf[3 * k] < s) ++k;
+    if (k < n && buf[3 * k] == s && buf[3 * k + 1] == e && buf[3 * k + 2] == t) ++nc;
+  }
+};
+struct ChunkSeq {
+  Idx inf, lab;
+  const int* off;
+  int64_t* scratch;  // 3 per token
+  int64_t* counts;   // [nseq, 3]
+  ChunkScheme sc;
+  __host__ __device__ void operator()(int64_t q) const {
+    const int64_t a = off[q], b = off[q + 1];
+    ChunkList li{scratch + 3 * a, 0};
+    sc.scan(inf, a, b, li);
+    ChunkMatch m{li.buf, li.n, 0, 0, 0};
+    sc.scan(lab, a, b, m);
+    counts[3 * q] = li.n;
+    counts[3 * q + 1] = m.nl;
+    counts[3 * q + 2] = m.nc;
+  }
+};
+struct ChunkTotals {
+  const int64_t* counts;
+  int64_t nseq;
+  float *p, *rc, *f1;
+  int64_t *ni, *nl, *nc;
+  __host__ __device__ void operator()(int64_t) const {
+    int64_t a = 0, b = 0, c = 0;
+    for (int64_t q = 0; q < nseq; ++q) {
+      a += counts[3 * q];
+      b += counts[3 * q + 1];
+      c += counts[3 * q + 2];
+    }
+    const double pr = a ? (double)c / (double)a : 0.0, re = b ? (double)c / (double)b : 0.0;
+    p[0] = (float)pr;
+    rc[0] = (float)re;
+    f1[0] = c ? (float)(2.0 * pr * re / (pr + re)) : 0.f;
+    ni[0] = a;
+    nl[0] = b;
+    nc[0] = c;
+  }
+};
+
+void k_chunk_eval(const OpRun& r) {
+  const bool dev = on_dev(r);
+  const Tensor& inf = r.in("Inference");
+  const Tensor& lab = r.in("Label");
+  PA_CHECK(inf.numel() == lab.numel(), "chunk_eval: Inference does not match Label");
+  const std::vector<int> off = offsets_of(lab, lab.numel());
+  const int64_t nseq = (int64_t)off.size() - 1;
+  const std::string scheme = r.op.GetString("chunk_scheme", "IOB");
+  ChunkScheme sc;
+  if (scheme == "IOB") sc = {2, 0, 1, -1, -1, 0, nullptr, 0};
+  else if (scheme == "IOE") sc = {2, -1, 0, 1, -1, 0, nullptr, 0};
+  else if (scheme == "IOBES") sc = {4, 0, 1, 2, 3, 0, nullptr, 0};
+  else if (scheme == "plain") sc = {1, -1, -1, -1, -1, 0, nullptr, 0};
+  else PA_CHECK(false, "chunk_eval: unknown chunk_scheme %s", scheme.c_str());
+  sc.other = r.op.GetInt("num_chunk_types", 1);
+  std::vector<int> excl;
+  for (int64_t t : r.op.GetInts("excluded_chunk_types")) excl.push_back((int)t);
+  sc.excl = any::ints(r, dev, "@chunk_excl@", excl);
+  sc.nexcl = (int)excl.size();
+  Tensor work, cnt;
+  int64_t* wp = work.alloc<int64_t>({std::max<int64_t>(1, 3 * inf.numel())}, place_of(r));
+  int64_t* cp = cnt.alloc<int64_t>({std::max<int64_t>(1, 3 * nseq)}, place_of(r));
+  any::run(r, dev, nseq, ChunkSeq{idx_of(inf, dev), idx_of(lab, dev), any::ints(r, dev, "@chunk_off@", off), wp, cp, sc},
+           1);
+  Tensor pt, rt, ft, it, lt, ct;
+  any::run(r, dev, 1, ChunkTotals{cp, nseq, pt.alloc<float>({1}, place_of(r)), rt.alloc<float>({1}, place_of(r)),
+                                  ft.alloc<float>({1}, place_of(r)), it.alloc<int64_t>({1}, place_of(r)),
+                                  lt.alloc<int64_t>({1}, place_of(r)), ct.alloc<int64_t>({1}, place_of(r))});
+  set(r, "Precision", pt);
+  set(r, "Recall", rt);
+  set(r, "F1-Score", ft);
+  set(r, "NumInferChunks", it);
+  set(r, "NumLabelChunks", lt);
+  set(r, "NumCorrectChunks", ct);
+}
+
+// ---------------------------------------------------------------- sampling_id / random_crop
+// sampling_id_op.h: per row, the first column whose running probability sum reaches a
+// uniform draw in [min, max) (draws from the executor's RNG, or `seed`)
+struct SampleRow {
+  const float *x, *u;
+  int64_t* o;
+  int64_t C;
+  __host__ __device__ void operator()(int64_t i) const {
+    float s = 0.f;
+    int64_t pick = C - 1;
+    for (int64_t j = 0; j < C; ++j) {
+      s += x[i * C + j];
+      if (s >= u[i]) {
+        pick = j;
+        break;
+      }
+    }
+    o[i] = pick;
+  }
+};
+
+void k_sampling_id(const OpRun& r) {
+  const bool dev = on_dev(r);
+  const Tensor& x = r.in("X");
+  PA_CHECK(x.dims.size() == 2, "sampling_id: 2-D X expected");
+  const int64_t N = x.dims[0], seed = r.op.GetInt("seed");
+  std::mt19937_64 g(seed ? (uint64_t)seed : r.ctx.rng());
+  std::uniform_real_distribution<float> d(r.op.GetFloat("min", 0.f), r.op.GetFloat("max", 1.f));
+  std::vector<int> u((size_t)N);
+  for (auto& v : u) {
+    const float f = d(g);
+    memcpy(&v, &f, sizeof(float));
+  }
+  Tensor o;
+  any::run(r, dev, N, SampleRow{f32(x, dev), (const float*)any::ints(r, dev, "@sampling_u@", u),
+                                o.alloc<int64_t>({N}, place_of(r)), x.dims[1]}, 64);
+  set(r, "Out", o);
+}
+
+// random_crop_op.h: a random window of `shape` over the trailing dims of every
+// instance (offsets from the executor's RNG); SeedOut carries the seed on
+struct CropND {
+  const float* x;
+  float* o;
+  int R;
+  int64_t xd[8], od[8], st[8];
+  __host__ __device__ void operator()(int64_t i) const {
+    int64_t src = 0, mul = 1, rem = i;
+    for (int d = R - 1; d >= 0; --d) {
+      const int64_t c = rem % od[d];
+      rem /= od[d];
+      src += (c + st[d]) * mul;
+      mul *= xd[d];
+    }
+    o[i] = x[src];
+  }
+};
+
+void k_random_crop(const OpRun& r) {
+  const bool dev = on_dev(r);
+  const Tensor& x = r.in("X");
+  const auto shape = r.op.GetInts("shape");
+  const int R = (int)x.dims.size(), k = (int)shape.size();
+  PA_CHECK(R <= 8 && k <= R, "random_crop: shape longer than X");
+  CropND f{};
+  f.x = f32(x, dev);
+  f.R = R;
+  Dims od = x.dims;
+  for (int d = 0; d < R; ++d) {
+    f.xd[d] = x.dims[(size_t)d];
+    f.st[d] = 0;
+  }
+  for (int i = 0; i < k; ++i) {
+    const int d = R - k + i;
+    PA_CHECK(shape[(size_t)i] <= x.dims[(size_t)d], "random_crop: crop larger than X");
+    od[(size_t)d] = shape[(size_t)i];
+    std::uniform_int_distribution<int64_t> u(0, x.dims[(size_t)d] - shape[(size_t)i]);
+    f.st[d] = u(r.ctx.rng);
+  }
+  for (int d = 0; d < R; ++d) f.od[d] = od[(size_t)d];
+  Tensor o;
+  f.o = o.alloc<float>(od, place_of(r));
+  any::run(r, dev, o.numel(), f);
+  set(r, "Out", o);
+  if (Tensor* so = r.out("SeedOut")) *so = r.in("Seed");
+}
+
+// ---------------------------------------------------------------- print
+// print_op.cc: message, name, shape, LoD and the first `summarize` values of In
+// (a host copy on a HIP place); Out shares In
+void k_print(const OpRun& r) {
+  const Tensor& in = r.in("In");
+  const Tensor h = in.device >= 0 ? in.to(-1, r.ctx.stream) : in;
+  int64_t n = h.numel();
+  const int64_t lim = r.op.GetInt("summarize", -1);
+  if (lim > 0 && lim < n) n = lim;
+  std::string s = r.op.GetString("message") + " " + r.op.Input("In") + " shape=" + in.shape_str() + " data=[";
+  char buf[64];
+  for (int64_t i = 0; i < n; ++i) {
+    switch (h.dtype) {
+      case DT::FP32: snprintf(buf, sizeof buf, "%g", (double)h.data<float>()[i]); break;
+      case DT::FP64: snprintf(buf, sizeof buf, "%g", h.data<double>()[i]); break;
+      case DT::INT64: snprintf(buf, sizeof buf, "%lld", (long long)h.data<int64_t>()[i]); break;
+      case DT::INT32: snprintf(buf, sizeof buf, "%d", h.data<int32_t>()[i]); break;
+      default: snprintf(buf, sizeof buf, "?"); break;
+    }
+    s += (i ? ", " : "") + std::string(buf);
+  }
+  printf("%s]\n", s.c_str());
+  fflush(stdout);
+  if (Tensor* o = r.out("Out")) *o = in;
+}
+
 }  // namespace
 
 #define PA_ANY_KERNEL(name, fn) \
@@ -1720,6 +2078,12 @@ PA_ANY_KERNEL(scale_sub_region, k_scale_sub_region);
 PA_ANY_KERNEL(scale_sub_region_grad, k_scale_sub_region);
 PA_ANY_KERNEL(size, k_size);
 PA_ANY_KERNEL(lars_momentum, k_lars_momentum);
+PA_ANY_KERNEL(max_pool3d_with_index, k_max_pool3d_idx);
+PA_ANY_KERNEL(max_pool3d_with_index_grad, k_max_pool3d_idx_grad);
+PA_ANY_KERNEL(chunk_eval, k_chunk_eval);
+PA_ANY_KERNEL(sampling_id, k_sampling_id);
+PA_ANY_KERNEL(random_crop, k_random_crop);
+PA_ANY_KERNEL(print, k_print);
 
 void link_extra_kernels() {}
 

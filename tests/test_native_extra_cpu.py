@@ -236,6 +236,43 @@ def case_shuffle_scale_sub(x, lab, idx):
     return _sq(L.elementwise_mul(ss, _img(x, 4, 3, 2)))
 
 
+def case_pool3d_index(x, lab, idx):
+    vol = L.reshape(_head(x, 2 * 4 * 4 * 2), [-1, 2, 4, 4, 2])
+    a, _ = simple_op("max_pool3d_with_index", {"X": [vol]}, {"ksize": [2, 2, 2], "strides": [2, 2, 2],
+                                                              "paddings": [0, 0, 0], "global_pooling": False},
+                     extra_outputs=("Mask",))
+    b, _ = simple_op("max_pool3d_with_index", {"X": [vol]}, {"ksize": [3, 2, 2], "strides": [1, 2, 1],
+                                                              "paddings": [1, 0, 1], "global_pooling": False},
+                     extra_outputs=("Mask",))
+    return L.elementwise_add(_sq(a), _sq(b))
+
+
+def _tags(vals, lod):
+    t = simple_op("assign_value", {}, {"shape": [len(vals), 1], "dtype": 2, "int32_values": vals}, dtype="int32",
+                  stop_gradient=True)
+    return L.lod_reset(t, target_lod=lod)
+
+
+def case_chunk_eval(x, lab, idx):
+    h = _head(x)
+    lod = [0, 4, 9, 12]
+    inf = _tags([0, 1, 4, 2, 3, 3, 0, 1, 1, 4, 0, 2], lod)
+    gold = _tags([0, 1, 4, 2, 2, 3, 0, 1, 4, 4, 0, 1], lod)
+    outs = simple_op("chunk_eval", {"Inference": [inf], "Label": [gold]},
+                     {"num_chunk_types": 2, "chunk_scheme": "IOB", "excluded_chunk_types": []}, out_slot="Precision",
+                     extra_outputs=("Recall", "F1-Score", "NumInferChunks", "NumLabelChunks", "NumCorrectChunks"),
+                     stop_gradient=True)
+    inf2 = _tags([0, 1, 2, 8, 3, 4, 5, 6, 7, 8, 4, 6], lod)
+    gold2 = _tags([0, 1, 2, 8, 3, 4, 6, 6, 7, 8, 4, 7], lod)
+    outs2 = simple_op("chunk_eval", {"Inference": [inf2], "Label": [gold2]},
+                      {"num_chunk_types": 2, "chunk_scheme": "IOBES", "excluded_chunk_types": [1]},
+                      out_slot="Precision",
+                      extra_outputs=("Recall", "F1-Score", "NumInferChunks", "NumLabelChunks", "NumCorrectChunks"),
+                      stop_gradient=True)
+    extra = _sum(*[L.cast(o, "float32") for o in list(outs) + list(outs2)])
+    return L.elementwise_add(_sq(h), extra)
+
+
 CASES = {k[5:]: v for k, v in globals().items() if k.startswith("case_")}
 
 
@@ -353,4 +390,31 @@ def test_dropout_grad_native_host():
     np.testing.assert_allclose(y[keep], xv[keep] / 0.7, rtol=1e-6)
     np.testing.assert_allclose(gx, np.where(keep, 2.0 / 0.7, 0.0), rtol=1e-6)
     assert 0.5 < keep.mean() < 0.9
+    assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+
+
+def test_sampling_crop_print_native(capfd):
+    """sampling_id (a valid column per row, biased to the heavy one), random_crop (a
+    window of X), print (the message on stdout, Out sharing In) on the C++ executor."""
+    def build():
+        p = L.data(name="p", shape=[4], dtype="float32")
+        v = L.data(name="v", shape=[3, 5], dtype="float32")
+        ids = simple_op("sampling_id", {"X": [p]}, {"min": 0.0, "max": 1.0, "seed": 5}, dtype="int64",
+                        stop_gradient=True)
+        seed = L.fill_constant([1], "int64", 7)
+        crop, _ = simple_op("random_crop", {"X": [v], "Seed": [seed]}, {"shape": [2, 3], "startup_seed": 0},
+                            extra_outputs=("SeedOut",), stop_gradient=True)
+        shown = simple_op("print", {"In": [crop]}, {"message": "crop-native", "summarize": 4}, stop_gradient=True)
+        return [ids, crop, shown]
+    probs = np.tile(np.array([[0.05, 0.05, 0.85, 0.05]], "float32"), (400, 1))
+    vol = np.arange(8 * 15, dtype="float32").reshape(8, 3, 5)
+    got, _, exe = run(build, [{"p": core.LoDTensor(torch.from_numpy(probs)),
+                               "v": core.LoDTensor(torch.from_numpy(vol))}], "native", fluid.CPUPlace())
+    ids, crop, shown = got[0]
+    assert ids.shape == (400,) and ids.min() >= 0 and ids.max() <= 3 and (ids == 2).mean() > 0.75
+    assert crop.shape == (8, 2, 3)
+    r0, c0 = divmod(int(crop[0, 0, 0]) % 15, 5)
+    np.testing.assert_array_equal(crop, vol[:, r0:r0 + 2, c0:c0 + 3])
+    np.testing.assert_array_equal(shown, crop)
+    assert "crop-native" in capfd.readouterr().out
     assert not exe._native.py_fallbacks, exe._native.py_fallbacks
