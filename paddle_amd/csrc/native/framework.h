@@ -251,6 +251,11 @@ void link_misc_kernels();
 void link_more_kernels();
 void link_extra_kernels();
 
+// one-source kernels of ops_extra.hip that other kernel files fall back to
+void layer_norm_any(const OpRun& r);
+void layer_norm_grad_any(const OpRun& r);
+void elementwise_int_any(const OpRun& r, int op);  // 0 add 1 sub 2 mul 3 div 4 max 5 min
+
 // ---------------------------------------------------------------- executor
 class Executor {
  public:

@@ -48,6 +48,9 @@ void set(const OpRun& r, const char* slot, const Tensor& t) {
 
 bool wants(const OpRun& r, const char* slot) { return !r.op.Outputs(slot).empty() && r.out_var(slot); }
 
+// Y's [pre, n, post] placement in X (elementwise_op_function.h); below
+bool bc_geo(const Dims& xd, const Dims& yd0, int64_t axis, int64_t* pre, int64_t* n, int64_t* post);
+
 // an int64 / int32 index tensor of the op's place
 struct Idx {
   const int64_t* l;
@@ -929,98 +932,156 @@ void ln_geom(const OpRun& r, const Tensor& x, int64_t* rows, int64_t* H) {
   *H = x.numel() / std::max<int64_t>(*rows, 1);
 }
 
-void k_layer_norm_host(const OpRun& r) {
+struct LnFwd {
+  const float *x, *w, *b;
+  float *y, *mean, *var;
+  int64_t H;
+  float eps;
+  __host__ __device__ void operator()(int64_t i) const {
+    const float* xr = x + i * H;
+    double s = 0.0;
+    for (int64_t j = 0; j < H; ++j) s += xr[j];
+    const double mu = s / (double)H;
+    double v = 0.0;
+    for (int64_t j = 0; j < H; ++j) v += ((double)xr[j] - mu) * ((double)xr[j] - mu);
+    v /= (double)H;
+    const float m = (float)mu, rs = (float)(1.0 / sqrt(v + (double)eps));
+    for (int64_t j = 0; j < H; ++j) {
+      float o = (xr[j] - m) * rs;
+      if (w) o *= w[j];
+      if (b) o += b[j];
+      y[i * H + j] = o;
+    }
+    mean[i] = m;
+    var[i] = (float)v;
+  }
+};
+struct LnBwdX {
+  const float *x, *g, *mean, *var, *w;
+  float* dx;
+  int64_t H;
+  float eps;
+  __host__ __device__ void operator()(int64_t i) const {
+    const float rs = 1.f / sqrtf(var[i] + eps), m = mean[i];
+    const float *xr = x + i * H, *gr = g + i * H;
+    double sg = 0.0, sgx = 0.0;
+    for (int64_t j = 0; j < H; ++j) {
+      const float gx = w ? gr[j] * w[j] : gr[j];
+      sg += gx;
+      sgx += (double)gx * (double)((xr[j] - m) * rs);
+    }
+    const float mg = (float)(sg / (double)H), mgx = (float)(sgx / (double)H);
+    for (int64_t j = 0; j < H; ++j) {
+      const float gx = w ? gr[j] * w[j] : gr[j], xh = (xr[j] - m) * rs;
+      dx[i * H + j] = rs * (gx - mg - xh * mgx);
+    }
+  }
+};
+struct LnBwdW {
+  const float *x, *g, *mean, *var;
+  float *dw, *db;
+  int64_t rows, H;
+  float eps;
+  __host__ __device__ void operator()(int64_t j) const {
+    double sw = 0.0, sb = 0.0;
+    for (int64_t i = 0; i < rows; ++i) {
+      const float rs = 1.f / sqrtf(var[i] + eps), gv = g[i * H + j];
+      sw += (double)gv * (double)((x[i * H + j] - mean[i]) * rs);
+      sb += gv;
+    }
+    if (dw) dw[j] = (float)sw;
+    if (db) db[j] = (float)sb;
+  }
+};
+
+}  // namespace
+
+// layer_norm (+grad) on either place, one work item per row (per column for the
+// parameter gradients): the host kernel, and the device path for the shapes the
+// fused norm kernel of the library does not take (ops_gpu.hip k_layer_norm)
+void layer_norm_any(const OpRun& r) {
+  const bool dev = on_dev(r);
   const Tensor& x = r.in("X");
   int64_t rows, H;
   ln_geom(r, x, &rows, &H);
   Tensor* sc = r.in_opt("Scale");
   Tensor* bi = r.in_opt("Bias");
-  const float* xp = f32(x, false);
-  const float* wp = sc ? f32(*sc, false) : nullptr;
-  const float* bp = bi ? f32(*bi, false) : nullptr;
-  const float eps = r.op.GetFloat("epsilon", 1e-5f);
   Tensor y, mt, vt;
-  float* yp = y.alloc<float>(x.dims, -1);
+  float* yp = y.alloc<float>(x.dims, place_of(r));
   y.lod = x.lod;
-  float* mp = mt.alloc<float>({rows}, -1);
-  float* vp = vt.alloc<float>({rows}, -1);
-  parallel_for(rows, 8, [&](int64_t a, int64_t b) {
-    for (int64_t i = a; i < b; ++i) {
-      const float* xr = xp + i * H;
-      double s = 0.0;
-      for (int64_t j = 0; j < H; ++j) s += xr[j];
-      const double mean = s / (double)H;
-      double v = 0.0;
-      for (int64_t j = 0; j < H; ++j) v += ((double)xr[j] - mean) * ((double)xr[j] - mean);
-      v /= (double)H;
-      const float m = (float)mean, rs = (float)(1.0 / sqrt(v + (double)eps));
-      for (int64_t j = 0; j < H; ++j) {
-        float o = (xr[j] - m) * rs;
-        if (wp) o *= wp[j];
-        if (bp) o += bp[j];
-        yp[i * H + j] = o;
-      }
-      mp[i] = m;
-      vp[i] = (float)v;
-    }
-  });
+  any::run(r, dev, rows, LnFwd{f32(x, dev), sc ? f32(*sc, dev) : nullptr, bi ? f32(*bi, dev) : nullptr, yp,
+                               mt.alloc<float>({rows}, place_of(r)), vt.alloc<float>({rows}, place_of(r)), H,
+                               r.op.GetFloat("epsilon", 1e-5f)}, 8);
   set(r, "Y", y);
   set(r, "Mean", mt);
   set(r, "Variance", vt);
 }
 
-void k_layer_norm_grad_host(const OpRun& r) {
+void layer_norm_grad_any(const OpRun& r) {
+  const bool dev = on_dev(r);
   const Tensor& x = r.in("X");
   int64_t rows, H;
   ln_geom(r, x, &rows, &H);
   Tensor* sc = r.in_opt("Scale");
-  const float* xp = f32(x, false);
-  const float* gp = f32(r.in("Y@GRAD"), false);
-  const float* mp = f32(r.in("Mean"), false);
-  const float* vp = f32(r.in("Variance"), false);
-  const float* wp = sc ? f32(*sc, false) : nullptr;
-  const float eps = r.op.GetFloat("epsilon", 1e-5f);
-  Tensor dxt, dwt, dbt;
-  float* dx = wants(r, "X@GRAD") ? dxt.alloc<float>(x.dims, -1) : nullptr;
-  float* dw = (sc && wants(r, "Scale@GRAD")) ? dwt.alloc<float>(sc->dims, -1) : nullptr;
   Tensor* bi = r.in_opt("Bias");
-  float* db = (bi && wants(r, "Bias@GRAD")) ? dbt.alloc<float>(bi->dims, -1) : nullptr;
-  if (dx)
-    parallel_for(rows, 8, [&](int64_t a, int64_t b) {
-      for (int64_t i = a; i < b; ++i) {
-        const float rs = 1.f / sqrtf(vp[i] + eps), m = mp[i];
-        const float *xr = xp + i * H, *gr = gp + i * H;
-        double sg = 0.0, sgx = 0.0;
-        for (int64_t j = 0; j < H; ++j) {
-          const float gx = wp ? gr[j] * wp[j] : gr[j];
-          sg += gx;
-          sgx += (double)gx * (double)((xr[j] - m) * rs);
-        }
-        const float mg = (float)(sg / (double)H), mgx = (float)(sgx / (double)H);
-        for (int64_t j = 0; j < H; ++j) {
-          const float gx = wp ? gr[j] * wp[j] : gr[j], xh = (xr[j] - m) * rs;
-          dx[i * H + j] = rs * (gx - mg - xh * mgx);
-        }
-      }
-    });
-  if (dw || db)
-    parallel_for(H, 64, [&](int64_t a, int64_t b) {
-      for (int64_t j = a; j < b; ++j) {
-        double sw = 0.0, sb = 0.0;
-        for (int64_t i = 0; i < rows; ++i) {
-          const float rs = 1.f / sqrtf(vp[i] + eps);
-          const float g = gp[i * H + j];
-          sw += (double)g * (double)((xp[i * H + j] - mp[i]) * rs);
-          sb += g;
-        }
-        if (dw) dw[j] = (float)sw;
-        if (db) db[j] = (float)sb;
-      }
-    });
+  const float eps = r.op.GetFloat("epsilon", 1e-5f);
+  const float *xp = f32(x, dev), *gp = f32(r.in("Y@GRAD"), dev), *mp = f32(r.in("Mean"), dev),
+              *vp = f32(r.in("Variance"), dev);
+  Tensor dxt, dwt, dbt;
+  float* dx = wants(r, "X@GRAD") ? dxt.alloc<float>(x.dims, place_of(r)) : nullptr;
+  float* dw = (sc && wants(r, "Scale@GRAD")) ? dwt.alloc<float>(sc->dims, place_of(r)) : nullptr;
+  float* db = (bi && wants(r, "Bias@GRAD")) ? dbt.alloc<float>(bi->dims, place_of(r)) : nullptr;
+  if (dx) any::run(r, dev, rows, LnBwdX{xp, gp, mp, vp, sc ? f32(*sc, dev) : nullptr, dx, H, eps}, 8);
+  if (dw || db) any::run(r, dev, H, LnBwdW{xp, gp, mp, vp, dw, db, rows, H, eps}, 64);
   if (dx) set(r, "X@GRAD", dxt);
   if (dw) set(r, "Scale@GRAD", dwt);
   if (db) set(r, "Bias@GRAD", dbt);
 }
+
+// integer elementwise_{add,sub,mul,div,max,min} on either place (index arithmetic;
+// the float kernels live in ops_host.cc / ops_gpu.hip); Y broadcast as [pre, n, post]
+template <class T>
+struct EwInt {
+  const T *x, *y;
+  T* o;
+  int64_t n, post;
+  int op;
+  __host__ __device__ void operator()(int64_t i) const {
+    const T a = x[i], b = y[(i / post) % n];
+    T v;
+    switch (op) {
+      case 0: v = a + b; break;
+      case 1: v = a - b; break;
+      case 2: v = a * b; break;
+      case 3: v = b ? a / b : 0; break;
+      case 4: v = a > b ? a : b; break;
+      default: v = a < b ? a : b; break;
+    }
+    o[i] = v;
+  }
+};
+
+void elementwise_int_any(const OpRun& r, int op) {
+  const bool dev = on_dev(r);
+  const Tensor& x = r.in("X");
+  const Tensor& y = r.in("Y");
+  int64_t pre, n, post;
+  if (op > 5 || x.dtype != y.dtype || (x.device >= 0) != dev || (y.device >= 0) != dev ||
+      !bc_geo(x.dims, y.dims, r.op.GetInt("axis", -1), &pre, &n, &post))
+    throw Decline{};
+  Tensor o;
+  void* p = o.alloc(x.dtype, x.dims, place_of(r));
+  o.lod = x.lod;
+  if (x.dtype == DT::INT64)
+    any::run(r, dev, x.numel(), EwInt<int64_t>{x.data<int64_t>(), y.data<int64_t>(), (int64_t*)p, n, post, op});
+  else if (x.dtype == DT::INT32)
+    any::run(r, dev, x.numel(), EwInt<int32_t>{x.data<int32_t>(), y.data<int32_t>(), (int32_t*)p, n, post, op});
+  else
+    throw Decline{};
+  set(r, "Out", o);
+}
+
+namespace {
 
 void k_dropout_grad_host(const OpRun& r) {
   const Tensor& m = r.in("Mask");
@@ -2031,6 +2092,162 @@ void k_print(const OpRun& r) {
   if (Tensor* o = r.out("Out")) *o = in;
 }
 
+// ---------------------------------------------------------------- multiclass_nms / mine_hard_examples
+// Variable-length outputs decided by sequential greedy loops: the reference runs
+// both on the CPU only (multiclass_nms_op.cc, mine_hard_examples_op.cc).  Here the
+// host computes them; on a HIP place the (small) inputs are staged to the host on
+// the op's stream and the result is uploaded back.
+Tensor host_view(const OpRun& r, const Tensor& t) { return t.device >= 0 ? t.to(-1, r.ctx.stream) : t; }
+void put(const OpRun& r, const char* slot, Tensor h, const LoD& lod) {
+  Tensor o = on_dev(r) ? h.to(r.ctx.device, r.ctx.stream) : h;
+  o.lod = lod;
+  set(r, slot, o);
+}
+
+float box_iou(const float* a, const float* b, bool norm) {
+  const float one = norm ? 0.f : 1.f;
+  const float aa = (a[2] - a[0] + one) * (a[3] - a[1] + one), ab = (b[2] - b[0] + one) * (b[3] - b[1] + one);
+  const float w = std::max(std::min(a[2], b[2]) - std::max(a[0], b[0]) + one, 0.f);
+  const float h = std::max(std::min(a[3], b[3]) - std::max(a[1], b[1]) + one, 0.f);
+  const float inter = w * h;
+  return inter / std::max(aa + ab - inter, 1e-10f);
+}
+
+// multiclass_nms: per image and non-background class, greedy NMS over the boxes
+// scoring above score_threshold (nms_top_k best first, adaptive threshold with
+// nms_eta); the image's detections [label, score, x0, y0, x1, y1] sorted by score,
+// keep_top_k kept; one row of -1 when nothing survives anywhere
+void k_multiclass_nms(const OpRun& r) {
+  const Tensor bt = host_view(r, r.in("BBoxes"));
+  const Tensor st = host_view(r, r.in("Scores"));
+  PA_CHECK(st.dims.size() == 3 && bt.dims.size() == 3 && bt.dims[2] == 4, "multiclass_nms: [N, C, M] scores and "
+           "[N, M, 4] boxes expected");
+  if (r.ctx.device >= 0) PA_HIPCHK(hipStreamSynchronize((hipStream_t)r.ctx.stream));
+  const float* boxes = f32(bt, false);
+  const float* scores = f32(st, false);
+  const int64_t N = st.dims[0], C = st.dims[1], M = st.dims[2];
+  const int64_t bg = r.op.GetInt("background_label", 0), top_k = r.op.GetInt("nms_top_k", 400),
+                keep_k = r.op.GetInt("keep_top_k", 200);
+  const float sthr = r.op.GetFloat("score_threshold", 0.01f), nthr = r.op.GetFloat("nms_threshold", 0.3f),
+              eta = r.op.GetFloat("nms_eta", 1.f);
+  const bool norm = r.op.GetBool("normalized", true);
+  std::vector<float> rows;
+  std::vector<size_t> off = {0};
+  for (int64_t b = 0; b < N; ++b) {
+    struct Det {
+      float c, s;
+      int64_t i;
+    };
+    std::vector<Det> dets;
+    const float* bb = boxes + b * M * 4;
+    for (int64_t c = 0; c < C; ++c) {
+      if (c == bg) continue;
+      const float* sc = scores + (b * C + c) * M;
+      std::vector<int64_t> order;
+      for (int64_t m = 0; m < M; ++m)
+        if (sc[m] > sthr) order.push_back(m);
+      std::stable_sort(order.begin(), order.end(), [&](int64_t u, int64_t v) { return sc[u] > sc[v]; });
+      if (top_k > -1 && (int64_t)order.size() > top_k) order.resize((size_t)top_k);
+      float adaptive = nthr;
+      std::vector<int64_t> kept;
+      for (size_t q = 0; q < order.size(); ++q) {
+        const int64_t i = order[q];
+        bool ok = true;
+        for (int64_t j : kept)
+          if (box_iou(bb + i * 4, bb + j * 4, norm) > adaptive) {
+            ok = false;
+            break;
+          }
+        if (!ok) continue;
+        kept.push_back(i);
+        if (eta < 1.f && adaptive > 0.5f) adaptive *= eta;
+      }
+      for (int64_t i : kept) dets.push_back({(float)c, sc[i], i});
+    }
+    std::stable_sort(dets.begin(), dets.end(), [](const Det& u, const Det& v) { return u.s > v.s; });
+    if (keep_k > -1 && (int64_t)dets.size() > keep_k) dets.resize((size_t)keep_k);
+    for (const Det& d : dets) {
+      rows.push_back(d.c);
+      rows.push_back(d.s);
+      for (int k = 0; k < 4; ++k) rows.push_back(bb[d.i * 4 + k]);
+    }
+    off.push_back(rows.size() / 6);
+  }
+  if (rows.empty()) {
+    rows.assign(6, -1.f);
+    off = {0, 1};
+  }
+  Tensor h;
+  memcpy(h.alloc<float>({(int64_t)rows.size() / 6, 6}, -1), rows.data(), rows.size() * sizeof(float));
+  put(r, "Out", h, {off});
+}
+
+// mine_hard_examples: max_negative takes, per image, the unmatched priors under
+// neg_dist_threshold with the largest classification loss, neg_pos_ratio per
+// positive; hard_example takes the sample_size largest (cls + loc) losses and unmatches
+// the positives left out.  NegIndices (LoD per image, ascending) and the updated
+// match indices
+void k_mine_hard_examples(const OpRun& r) {
+  const Tensor cl = host_view(r, r.in("ClsLoss"));
+  Tensor* locp = r.in_opt("LocLoss");
+  const Tensor loc = locp ? host_view(r, *locp) : Tensor();
+  const Tensor mi0 = host_view(r, r.in("MatchIndices"));
+  const Tensor md = host_view(r, r.in("MatchDist"));
+  if (r.ctx.device >= 0) PA_HIPCHK(hipStreamSynchronize((hipStream_t)r.ctx.stream));
+  PA_CHECK(mi0.dims.size() == 2, "mine_hard_examples: [N, P] MatchIndices expected");
+  const int64_t N = mi0.dims[0], P = mi0.dims[1];
+  const float* cls = f32(cl, false);
+  const float* lp = locp ? f32(loc, false) : nullptr;
+  const float* dist = f32(md, false);
+  const Idx mi = idx_of(mi0, false);
+  const std::string kind = r.op.GetString("mining_type", "max_negative");
+  const float ratio = r.op.GetFloat("neg_pos_ratio", 1.f), dthr = r.op.GetFloat("neg_dist_threshold", 0.5f);
+  const int64_t sample = r.op.GetInt("sample_size", 0);
+  Tensor upd;
+  int32_t* up = static_cast<int32_t*>(upd.alloc(DT::INT32, {N, P}, -1));
+  for (int64_t k = 0; k < N * P; ++k) up[k] = (int32_t)mi[k];
+  std::vector<int32_t> negs;
+  std::vector<size_t> off = {0};
+  for (int64_t b = 0; b < N; ++b) {
+    std::vector<float> loss((size_t)P);
+    for (int64_t p = 0; p < P; ++p)
+      loss[(size_t)p] = cls[b * P + p] + ((lp && kind == "hard_example") ? lp[b * P + p] : 0.f);
+    std::vector<int64_t> cand;
+    int64_t k;
+    if (kind == "max_negative") {
+      int64_t npos = 0;
+      for (int64_t p = 0; p < P; ++p) {
+        if (up[b * P + p] >= 0) ++npos;
+        else if (dist[b * P + p] < dthr) cand.push_back(p);
+      }
+      k = std::min<int64_t>((int64_t)((float)npos * ratio), (int64_t)cand.size());
+    } else {
+      for (int64_t p = 0; p < P; ++p) cand.push_back(p);
+      k = std::min<int64_t>(sample, P);
+    }
+    std::stable_sort(cand.begin(), cand.end(), [&](int64_t u, int64_t v) { return loss[(size_t)u] > loss[(size_t)v]; });
+    cand.resize((size_t)std::max<int64_t>(k, 0));
+    std::sort(cand.begin(), cand.end());
+    if (kind == "hard_example") {
+      std::vector<char> keep((size_t)P, 0);
+      for (int64_t p : cand) keep[(size_t)p] = 1;
+      for (int64_t p = 0; p < P; ++p)
+        if (up[b * P + p] >= 0 && !keep[(size_t)p]) up[b * P + p] = -1;
+      std::vector<int64_t> neg;
+      for (int64_t p : cand)
+        if (up[b * P + p] < 0) neg.push_back(p);
+      cand.swap(neg);
+    }
+    for (int64_t p : cand) negs.push_back((int32_t)p);
+    off.push_back(negs.size());
+  }
+  Tensor nt;
+  int32_t* np_ = static_cast<int32_t*>(nt.alloc(DT::INT32, {(int64_t)negs.size(), 1}, -1));
+  if (!negs.empty()) memcpy(np_, negs.data(), negs.size() * sizeof(int32_t));
+  put(r, "NegIndices", nt, {off});
+  put(r, "UpdatedMatchIndices", upd, {});
+}
+
 }  // namespace
 
 #define PA_ANY_KERNEL(name, fn) \
@@ -2050,8 +2267,8 @@ PA_ANY_KERNEL(average_accumulates, k_average_accumulates);
 PA_ANY_KERNEL(fake_quantize_range_abs_max, k_fake_quant_range);
 PA_ANY_KERNEL(bipartite_match, k_bipartite_match);
 PA_ANY_KERNEL(target_assign, k_target_assign);
-PA_HOST_KERNEL(layer_norm, k_layer_norm_host);
-PA_HOST_KERNEL(layer_norm_grad, k_layer_norm_grad_host);
+PA_HOST_KERNEL(layer_norm, layer_norm_any);
+PA_HOST_KERNEL(layer_norm_grad, layer_norm_grad_any);
 PA_HOST_KERNEL(dropout_grad, k_dropout_grad_host);
 
 PA_ANY_KERNEL(reduce_sum_grad, k_reduce_grad<0>);
@@ -2084,6 +2301,8 @@ PA_ANY_KERNEL(chunk_eval, k_chunk_eval);
 PA_ANY_KERNEL(sampling_id, k_sampling_id);
 PA_ANY_KERNEL(random_crop, k_random_crop);
 PA_ANY_KERNEL(print, k_print);
+PA_ANY_KERNEL(multiclass_nms, k_multiclass_nms);
+PA_ANY_KERNEL(mine_hard_examples, k_mine_hard_examples);
 
 void link_extra_kernels() {}
 

@@ -182,6 +182,7 @@ bool make_bc(const Dims& x, const Dims& y, int64_t axis, BcArgs* b, int64_t* pre
 template <int OP> void k_binary(const OpRun& r) {
   Tensor x = r.in("X");
   Tensor y = r.in("Y");
+  if ((x.dtype == DT::INT64 || x.dtype == DT::INT32) && OP != B_POW) return elementwise_int_any(r, (int)OP);
   BcArgs b;
   int64_t pre, n, post;
   const bool pnp = make_bc(x.dims, y.dims, r.op.GetInt("axis", -1), &b, &pre, &n, &post);
@@ -1395,17 +1396,19 @@ __global__ void var_to_rstd_kernel(const float* __restrict__ var, float* __restr
     rstd[i] = rsqrtf(var[i] + eps);
 }
 
-void ln_rows(const OpRun& r, const Tensor& x, int64_t& rows, int64_t& H) {
+// the fused norm kernel's shapes; others run the one-source row kernels
+bool ln_rows(const OpRun& r, const Tensor& x, int64_t& rows, int64_t& H) {
   const size_t ax = (size_t)r.op.GetInt("begin_norm_axis", 1);
   rows = prod(x.dims, 0, ax);
   H = prod(x.dims, ax);
-  if (x.dtype != DT::FP32 || H % 8 || H > 8192 || rows <= 0) throw Decline();
+  if (x.dtype != DT::FP32 || rows <= 0) throw Decline();
+  return H % 8 == 0 && H <= 8192;
 }
 
 void k_layer_norm(const OpRun& r) {
   Tensor x = r.in("X");
   int64_t rows, H;
-  ln_rows(r, x, rows, H);
+  if (!ln_rows(r, x, rows, H)) return layer_norm_any(r);
   Tensor* sc = r.in_opt("Scale");
   Tensor* bi = r.in_opt("Bias");
   if ((sc && sc->dtype != DT::FP32) || (bi && bi->dtype != DT::FP32)) throw Decline();
@@ -1425,7 +1428,7 @@ void k_layer_norm(const OpRun& r) {
 void k_layer_norm_grad(const OpRun& r) {
   Tensor x = r.in("X");
   int64_t rows, H;
-  ln_rows(r, x, rows, H);
+  if (!ln_rows(r, x, rows, H)) return layer_norm_grad_any(r);
   Tensor dy = r.in("Y@GRAD");
   Tensor mean = r.in("Mean");
   Tensor var = r.in("Variance");

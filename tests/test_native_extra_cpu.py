@@ -273,6 +273,38 @@ def case_chunk_eval(x, lab, idx):
     return L.elementwise_add(_sq(h), extra)
 
 
+def case_nms_mining(x, lab, idx):
+    h = _head(x)
+    corner = L.reshape(_head(x, 12), [-1, 3, 4])
+    lo = L.slice(corner, axes=[2], starts=[0], ends=[2])
+    boxes = L.concat([lo, L.elementwise_add(lo, L.exp(L.slice(corner, axes=[2], starts=[2], ends=[4])))], axis=2)
+    boxes.stop_gradient = True
+    scores = L.sigmoid(L.reshape(_head(x, 9), [-1, 3, 3]))
+    scores.stop_gradient = True
+    nms = simple_op("multiclass_nms", {"BBoxes": [boxes], "Scores": [scores]},
+                    {"background_label": 0, "score_threshold": 0.3, "nms_top_k": 2, "nms_threshold": 0.4,
+                     "nms_eta": 1.0, "keep_top_k": 3, "normalized": False}, stop_gradient=True)
+    cls = L.abs(_head(x, 6))
+    cls.stop_gradient = True
+    match = simple_op("assign_value", {}, {"shape": [4, 6], "dtype": 2,
+                                           "int32_values": [0, -1, -1, 1, -1, -1, -1, -1, -1, -1, -1, 2,
+                                                            1, 0, -1, -1, -1, -1, -1, 3, -1, -1, 0, -1]},
+                      dtype="int32", stop_gradient=True)
+    dist = L.scale(L.sigmoid(_head(x, 6)), 0.8)
+    dist.stop_gradient = True
+    neg, upd = simple_op("mine_hard_examples", {"ClsLoss": [cls], "MatchIndices": [match], "MatchDist": [dist]},
+                         {"neg_pos_ratio": 2.0, "neg_dist_threshold": 0.5, "sample_size": 0,
+                          "mining_type": "max_negative"}, out_slot="NegIndices", dtype="int32",
+                         extra_outputs=("UpdatedMatchIndices",), stop_gradient=True)
+    hneg, hupd = simple_op("mine_hard_examples", {"ClsLoss": [cls], "LocLoss": [L.abs(_head(x, 6))],
+                                                  "MatchIndices": [match], "MatchDist": [dist]},
+                           {"neg_pos_ratio": 1.0, "neg_dist_threshold": 0.5, "sample_size": 3,
+                            "mining_type": "hard_example"}, out_slot="NegIndices", dtype="int32",
+                           extra_outputs=("UpdatedMatchIndices",), stop_gradient=True)
+    extra = _sum(L.mean(nms), *[L.mean(L.cast(t, "float32")) for t in (neg, upd, hneg, hupd)])
+    return L.elementwise_add(_sq(h), extra)
+
+
 CASES = {k[5:]: v for k, v in globals().items() if k.startswith("case_")}
 
 
