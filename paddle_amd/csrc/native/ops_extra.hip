@@ -2248,6 +2248,53 @@ void k_mine_hard_examples(const OpRun& r) {
   put(r, "UpdatedMatchIndices", upd, {});
 }
 
+// ---------------------------------------------------------------- fusion_lstm / fusion_gru
+// fusion_{lstm,gru}_op.cc: XX = X WeightX (+ Bias for the GRU) in one GEMM over all
+// time steps, then the recurrence of lstm / gru over XX with WeightH.  The recurrence
+// is the registered lstm / gru kernel of this place, run on a derived op desc (same
+// scope, same stream): XX lands in the XX output (or a scope temporary), the
+// recurrence writes Hidden (and Cell).
+void k_fusion_rnn(const OpRun& r) {
+  const bool dev = on_dev(r);
+  const bool gru = r.op.type == "fusion_gru";
+  const Tensor& x = r.in("X");
+  const Tensor& wx = r.in("WeightX");
+  PA_CHECK(x.dims.size() == 2 && wx.dims.size() == 2 && wx.dims[0] == x.dims[1], "%s: X [T, M], WeightX [M, G]",
+           r.op.type.c_str());
+  const int64_t T = x.dims[0], M = x.dims[1], G = wx.dims[1];
+  std::string xx_name = r.op.Output("XX");
+  if (xx_name.empty()) xx_name = r.op.Output("Hidden") + "@fusion_xx";
+  Tensor& xx = r.scope.Var(xx_name)->tensor;
+  float* xp = xx.alloc<float>({T, G}, place_of(r));
+  any::gemm(r, dev, false, false, T, G, M, 1.f, f32(x, dev), M, f32(wx, dev), G, 0.f, xp, G);
+  Tensor* bias = r.in_opt("Bias");
+  if (gru && bias) {
+    PA_CHECK(bias->numel() == G, "fusion_gru: Bias must be [1, 3D]");
+    any::run(r, dev, T * G, FusedFwd{xp, f32(*bias, dev), xp, nullptr, FusedGeo{G, 1, 1, 0, 0, 1.f}});
+  }
+  xx.lod = x.lod;
+  OpDesc sub;
+  sub.type = gru ? "gru" : "lstm";
+  auto pass = [&](const char* from, const char* to, std::vector<std::pair<std::string, std::vector<std::string>>>& v,
+                  bool input) {
+    const auto& names = input ? r.op.Inputs(from) : r.op.Outputs(from);
+    if (!names.empty()) v.push_back({to, names});
+  };
+  sub.inputs.push_back({"Input", {xx_name}});
+  pass("H0", "H0", sub.inputs, true);
+  pass("WeightH", "Weight", sub.inputs, true);
+  if (!gru) {
+    pass("C0", "C0", sub.inputs, true);
+    pass("Bias", "Bias", sub.inputs, true);
+    pass("Cell", "Cell", sub.outputs, false);
+  }
+  pass("Hidden", "Hidden", sub.outputs, false);
+  sub.attrs = r.op.attrs;
+  const Kernel* k = find_kernel(sub.type, dev);
+  if (!k) throw Decline{};
+  (*k)(OpRun{sub, r.scope, r.ctx});
+}
+
 }  // namespace
 
 #define PA_ANY_KERNEL(name, fn) \
@@ -2303,6 +2350,8 @@ PA_ANY_KERNEL(random_crop, k_random_crop);
 PA_ANY_KERNEL(print, k_print);
 PA_ANY_KERNEL(multiclass_nms, k_multiclass_nms);
 PA_ANY_KERNEL(mine_hard_examples, k_mine_hard_examples);
+PA_ANY_KERNEL(fusion_lstm, k_fusion_rnn);
+PA_ANY_KERNEL(fusion_gru, k_fusion_rnn);
 
 void link_extra_kernels() {}
 

@@ -450,3 +450,35 @@ def test_sampling_crop_print_native(capfd):
     np.testing.assert_array_equal(shown, crop)
     assert "crop-native" in capfd.readouterr().out
     assert not exe._native.py_fallbacks, exe._native.py_fallbacks
+
+
+def fusion_rnn_build():
+    """fusion_lstm / fusion_gru (inference ops: XX = X WeightX, then the recurrence)."""
+    x = L.data(name="xs", shape=[5], dtype="float32", lod_level=1)
+    D = 3
+    cp = lambda shape: L.create_parameter(shape, "float32")  # noqa: E731
+    h, c, _ = simple_op("fusion_lstm", {"X": [x], "WeightX": [cp([5, 4 * D])], "WeightH": [cp([D, 4 * D])],
+                                        "Bias": [cp([1, 4 * D])]},
+                        {"use_peepholes": False, "is_reverse": False, "gate_activation": "sigmoid",
+                         "cell_activation": "tanh", "candidate_activation": "tanh", "use_seq": True},
+                        out_slot="Hidden", extra_outputs=("Cell", "XX"), stop_gradient=True)
+    g, _ = simple_op("fusion_gru", {"X": [x], "WeightX": [cp([5, 3 * D])], "WeightH": [cp([D, 3 * D])],
+                                    "Bias": [cp([1, 3 * D])]},
+                     {"activation": "tanh", "gate_activation": "sigmoid", "is_reverse": True, "use_seq": True},
+                     out_slot="Hidden", extra_outputs=("XX",), stop_gradient=True)
+    return [h, c, g]
+
+
+def fusion_feeds():
+    rs = np.random.RandomState(3)
+    t = core.LoDTensor(torch.from_numpy(rs.randn(9, 5).astype("float32")))
+    t.set_lod([[0, 3, 5, 9]])
+    return [{"xs": t}]
+
+
+def test_fusion_rnn_native_host():
+    ref, init, _ = run(fusion_rnn_build, fusion_feeds(), "python", fluid.CPUPlace())
+    got, _, exe = run(fusion_rnn_build, fusion_feeds(), "native", fluid.CPUPlace(), init)
+    for u, v in zip(ref[0], got[0]):
+        np.testing.assert_allclose(v, u, rtol=1e-5, atol=1e-6)
+    assert not exe._native.py_fallbacks, exe._native.py_fallbacks
