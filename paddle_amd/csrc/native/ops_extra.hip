@@ -2295,6 +2295,88 @@ void k_fusion_rnn(const OpRun& r) {
   (*k)(OpRun{sub, r.scope, r.ctx});
 }
 
+// ---------------------------------------------------------------- fusion_seqexpand_concat_fc
+// fusion_seqexpand_concat_fc_op.cc: X[0] [T, M0] carries the sequences, X[k>0] [N,
+// Mk] one row per sequence expanded over its steps; FCOut = concat(...) FCWeight (+
+// FCBias), Out = act(FCOut) with act in identity / relu / sigmoid / tanh
+struct ExpandConcat {
+  const float* const* xs;  // device / host array of the inputs
+  const int* widths;       // Mk, prefix-summed: [0, M0, M0 + M1, ...]
+  const int* off;          // sequence offsets of X[0]
+  float* o;
+  int64_t nx, nseq, W;
+  __host__ __device__ void operator()(int64_t i) const {
+    const int64_t t = i / W, c = i % W;
+    int64_t k = 0;
+    while (k + 1 < nx && widths[k + 1] <= c) ++k;
+    const int64_t col = c - widths[k], mk = widths[k + 1] - widths[k];
+    if (k == 0) {
+      o[i] = xs[0][t * mk + col];
+      return;
+    }
+    int64_t lo = 0, hi = nseq;
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) / 2;
+      if (off[mid] <= t) lo = mid;
+      else hi = mid;
+    }
+    o[i] = xs[k][lo * mk + col];
+  }
+};
+struct BiasAct {
+  const float* b;
+  float *fc, *out;
+  int64_t N;
+  int act;  // 0 identity 1 relu 2 sigmoid 3 tanh
+  __host__ __device__ void operator()(int64_t i) const {
+    float v = fc[i] + (b ? b[i % N] : 0.f);
+    fc[i] = v;
+    out[i] = act == 1 ? fmaxf(v, 0.f) : act == 2 ? 1.f / (1.f + expf(-v)) : act == 3 ? tanhf(v) : v;
+  }
+};
+
+void k_seqexpand_concat_fc(const OpRun& r) {
+  const bool dev = on_dev(r);
+  const std::vector<Tensor*> xs = r.ins("X");
+  PA_CHECK(!xs.empty() && xs[0]->dims.size() == 2, "fusion_seqexpand_concat_fc: 2-D X[0] expected");
+  const int64_t T = xs[0]->dims[0];
+  const std::vector<int> off = offsets_of(*xs[0], T);
+  const int64_t nseq = (int64_t)off.size() - 1;
+  std::vector<int> widths = {0};
+  std::vector<int> ptrs;  // the input pointers, as int pairs for the upload helper
+  for (size_t k = 0; k < xs.size(); ++k) {
+    PA_CHECK(xs[k]->dims.size() == 2 && (k == 0 || xs[k]->dims[0] == nseq),
+             "fusion_seqexpand_concat_fc: X[%d] must have one row per sequence", (int)k);
+    widths.push_back(widths.back() + (int)xs[k]->dims[1]);
+    const float* p = f32(*xs[k], dev);
+    int pair[2];
+    memcpy(pair, &p, sizeof(p));
+    ptrs.push_back(pair[0]);
+    ptrs.push_back(pair[1]);
+  }
+  const int64_t W = widths.back();
+  const Tensor& w = r.in("FCWeight");
+  PA_CHECK(w.dims.size() == 2 && w.dims[0] == W, "fusion_seqexpand_concat_fc: FCWeight must be [sum M, N]");
+  const int64_t N = w.dims[1];
+  std::vector<float> hcat;
+  float* cat = any::scratch(r, dev, "@seqexpand_cat@", T * W, &hcat);
+  any::run(r, dev, T * W, ExpandConcat{(const float* const*)any::ints(r, dev, "@seqexpand_ptrs@", ptrs),
+                                       any::ints(r, dev, "@seqexpand_w@", widths),
+                                       any::ints(r, dev, "@seqexpand_off@", off), cat, (int64_t)xs.size(), nseq, W});
+  Tensor fc, out;
+  float* fp = fc.alloc<float>({T, N}, place_of(r));
+  float* op = out.alloc<float>({T, N}, place_of(r));
+  any::gemm(r, dev, false, false, T, N, W, 1.f, cat, W, f32(w, dev), N, 0.f, fp, N);
+  const std::string a = r.op.GetString("fc_activation", "identity");
+  const int act = a == "relu" ? 1 : a == "sigmoid" ? 2 : a == "tanh" ? 3 : 0;
+  PA_CHECK(act || a == "identity" || a.empty(), "fusion_seqexpand_concat_fc: activation %s", a.c_str());
+  Tensor* b = r.in_opt("FCBias");
+  any::run(r, dev, T * N, BiasAct{b ? f32(*b, dev) : nullptr, fp, op, N, act});
+  out.lod = xs[0]->lod;
+  set(r, "FCOut", fc);
+  set(r, "Out", out);
+}
+
 }  // namespace
 
 #define PA_ANY_KERNEL(name, fn) \
@@ -2352,6 +2434,7 @@ PA_ANY_KERNEL(multiclass_nms, k_multiclass_nms);
 PA_ANY_KERNEL(mine_hard_examples, k_mine_hard_examples);
 PA_ANY_KERNEL(fusion_lstm, k_fusion_rnn);
 PA_ANY_KERNEL(fusion_gru, k_fusion_rnn);
+PA_ANY_KERNEL(fusion_seqexpand_concat_fc, k_seqexpand_concat_fc);
 
 void link_extra_kernels() {}
 

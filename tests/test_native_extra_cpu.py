@@ -453,7 +453,8 @@ def test_sampling_crop_print_native(capfd):
 
 
 def fusion_rnn_build():
-    """fusion_lstm / fusion_gru (inference ops: XX = X WeightX, then the recurrence)."""
+    """fusion_lstm / fusion_gru (inference ops: XX = X WeightX, then the recurrence) and
+    fusion_seqexpand_concat_fc."""
     x = L.data(name="xs", shape=[5], dtype="float32", lod_level=1)
     D = 3
     cp = lambda shape: L.create_parameter(shape, "float32")  # noqa: E731
@@ -466,14 +467,17 @@ def fusion_rnn_build():
                                     "Bias": [cp([1, 3 * D])]},
                      {"activation": "tanh", "gate_activation": "sigmoid", "is_reverse": True, "use_seq": True},
                      out_slot="Hidden", extra_outputs=("XX",), stop_gradient=True)
-    return [h, c, g]
+    y = L.data(name="ys", shape=[2], dtype="float32")
+    fo, _ = simple_op("fusion_seqexpand_concat_fc", {"X": [x, y], "FCWeight": [cp([7, 4])], "FCBias": [cp([4])]},
+                      {"fc_activation": "tanh"}, extra_outputs=("FCOut",), stop_gradient=True)
+    return [h, c, g, fo]
 
 
 def fusion_feeds():
     rs = np.random.RandomState(3)
     t = core.LoDTensor(torch.from_numpy(rs.randn(9, 5).astype("float32")))
     t.set_lod([[0, 3, 5, 9]])
-    return [{"xs": t}]
+    return [{"xs": t, "ys": core.LoDTensor(torch.from_numpy(rs.randn(3, 2).astype("float32")))}]
 
 
 def test_fusion_rnn_native_host():
