@@ -27,6 +27,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <map>
 #include <random>
 #include <string>
 #include <vector>
@@ -2377,6 +2378,147 @@ void k_seqexpand_concat_fc(const OpRun& r) {
   set(r, "Out", out);
 }
 
+// ---------------------------------------------------------------- detection_map
+// detection_map_op.h (VOC mAP): per image and class, detections by descending score
+// claim the unused ground truth of best IoU >= overlap_threshold (difficult ground
+// truth skipped unless evaluate_difficult); per class AP from the cumulative TP / FP
+// curve ("integral" or "11point"), MAP their mean over non-background classes with
+// positives.  Outputs the per-class positive counts and the (score, tp) / (score, fp)
+// records.  Host loops as the reference's CPU kernel; staged through the host on a HIP
+// place.
+double iou_plain(const double* a, const double* b) {
+  const double ix = std::max(0.0, std::min(a[2], b[2]) - std::max(a[0], b[0]));
+  const double iy = std::max(0.0, std::min(a[3], b[3]) - std::max(a[1], b[1]));
+  const double inter = ix * iy;
+  const double ua = (a[2] - a[0]) * (a[3] - a[1]) + (b[2] - b[0]) * (b[3] - b[1]) - inter;
+  return ua > 0 ? inter / ua : 0.0;
+}
+
+void k_detection_map(const OpRun& r) {
+  const Tensor dt = host_view(r, r.in("DetectRes"));
+  const Tensor gt = host_view(r, r.in("Label"));
+  if (r.ctx.device >= 0) PA_HIPCHK(hipStreamSynchronize((hipStream_t)r.ctx.stream));
+  PA_CHECK(dt.dims.size() == 2 && dt.dims[1] == 6 && gt.dims.size() == 2 && (gt.dims[1] == 5 || gt.dims[1] == 6),
+           "detection_map: DetectRes [D, 6] and Label [G, 5 or 6] expected");
+  const float* det = f32(dt, false);
+  const float* lab = f32(gt, false);
+  const int64_t GW = gt.dims[1];
+  const bool has_diff = GW == 6, eval_diff = r.op.GetBool("evaluate_difficult", true);
+  const double thr = r.op.GetFloat("overlap_threshold", 0.5f);
+  const int64_t bg = r.op.GetInt("background_label", 0);
+  const std::vector<int> doff = offsets_of(dt, dt.dims[0]), goff = offsets_of(gt, gt.dims[0]);
+  std::map<int64_t, int64_t> pos;
+  std::map<int64_t, std::vector<std::pair<double, int>>> rec;
+  for (size_t i = 0; i + 1 < goff.size(); ++i) {
+    const int64_t g0 = goff[i], g1 = goff[i + 1];
+    const int64_t d0 = i + 1 < doff.size() ? doff[i] : 0, d1 = i + 1 < doff.size() ? doff[i + 1] : 0;
+    for (int64_t g = g0; g < g1; ++g) {
+      const bool diff = has_diff && lab[g * GW + 1] != 0.f;
+      if (eval_diff || !diff) ++pos[(int64_t)lab[g * GW]];
+    }
+    std::map<int64_t, std::vector<int64_t>> by_class;
+    for (int64_t d = d0; d < d1; ++d) by_class[(int64_t)det[d * 6]].push_back(d);
+    for (auto& kv : by_class) {
+      const int64_t c = kv.first;
+      std::vector<int64_t>& ds = kv.second;
+      std::stable_sort(ds.begin(), ds.end(), [&](int64_t a, int64_t b) { return det[a * 6 + 1] > det[b * 6 + 1]; });
+      std::vector<int64_t> gs;
+      for (int64_t g = g0; g < g1; ++g)
+        if ((int64_t)lab[g * GW] == c) gs.push_back(g);
+      std::vector<char> used(gs.size(), 0);
+      for (int64_t d : ds) {
+        double box[4], best = -1.0;
+        for (int k = 0; k < 4; ++k) box[k] = det[d * 6 + 2 + k];
+        int64_t bj = -1;
+        for (size_t j = 0; j < gs.size(); ++j) {
+          double gb[4];
+          for (int k = 0; k < 4; ++k) gb[k] = lab[gs[j] * GW + GW - 4 + k];
+          const double o = iou_plain(box, gb);
+          if (o > best) {
+            best = o;
+            bj = (int64_t)j;
+          }
+        }
+        int tp = 0;
+        if (best >= thr) {
+          const bool diff = has_diff && lab[gs[(size_t)bj] * GW + 1] != 0.f;
+          if (!eval_diff && diff) continue;
+          if (!used[(size_t)bj]) {
+            tp = 1;
+            used[(size_t)bj] = 1;
+          }
+        }
+        rec[c].push_back({(double)det[d * 6 + 1], tp});
+      }
+    }
+  }
+  const bool eleven = r.op.GetString("ap_type", "integral") == "11point";
+  double ap_sum = 0.0;
+  int64_t n_ap = 0;
+  for (const auto& kv : pos) {
+    const int64_t c = kv.first, npos = kv.second;
+    if (c == bg || npos == 0) continue;
+    std::vector<std::pair<double, int>> rs = rec.count(c) ? rec[c] : std::vector<std::pair<double, int>>();
+    std::stable_sort(rs.begin(), rs.end(), [](const std::pair<double, int>& a, const std::pair<double, int>& b) {
+      return a.first > b.first;
+    });
+    std::vector<double> recall, prec;
+    double tps = 0, fps = 0;
+    for (const auto& e : rs) {
+      tps += e.second;
+      fps += 1 - e.second;
+      recall.push_back(tps / (double)npos);
+      prec.push_back(tps / std::max(tps + fps, 1e-12));
+    }
+    double ap = 0.0;
+    if (eleven) {
+      for (int t = 0; t <= 10; ++t) {
+        double m = 0.0;
+        bool any = false;
+        for (size_t k = 0; k < recall.size(); ++k)
+          if (recall[k] >= t * 0.1) {  // np.linspace(0, 1, 11)
+            m = any ? std::max(m, prec[k]) : prec[k];
+            any = true;
+          }
+        ap += m;
+      }
+      ap /= 11.0;
+    } else {
+      double prev = 0.0;
+      for (size_t k = 0; k < recall.size(); ++k) {
+        ap += prec[k] * (recall[k] - prev);
+        prev = recall[k];
+      }
+    }
+    ap_sum += ap;
+    ++n_ap;
+  }
+  Tensor mt, pt, tt, ft;
+  mt.alloc<float>({1}, -1)[0] = n_ap ? (float)(ap_sum / (double)n_ap) : 0.f;
+  const int64_t npc = std::max<int64_t>(1, (int64_t)pos.size());
+  int32_t* pp = static_cast<int32_t*>(pt.alloc(DT::INT32, {npc, 1}, -1));
+  pp[0] = 0;
+  int64_t q = 0;
+  for (const auto& kv : pos) pp[q++] = (int32_t)kv.second;
+  int64_t nrec = 0;
+  for (const auto& kv : rec) nrec += (int64_t)kv.second.size();
+  float* tp = tt.alloc<float>({std::max<int64_t>(1, nrec), 2}, -1);
+  float* fp = ft.alloc<float>({std::max<int64_t>(1, nrec), 2}, -1);
+  tp[0] = tp[1] = fp[0] = fp[1] = 0.f;
+  q = 0;
+  for (const auto& kv : rec)
+    for (const auto& e : kv.second) {
+      tp[2 * q] = fp[2 * q] = (float)e.first;
+      tp[2 * q + 1] = (float)e.second;
+      fp[2 * q + 1] = (float)(1 - e.second);
+      ++q;
+    }
+  put(r, "MAP", mt, {});
+  put(r, "AccumPosCount", pt, {});
+  put(r, "AccumTruePos", tt, {});
+  put(r, "AccumFalsePos", ft, {});
+}
+
 }  // namespace
 
 #define PA_ANY_KERNEL(name, fn) \
@@ -2435,6 +2577,7 @@ PA_ANY_KERNEL(mine_hard_examples, k_mine_hard_examples);
 PA_ANY_KERNEL(fusion_lstm, k_fusion_rnn);
 PA_ANY_KERNEL(fusion_gru, k_fusion_rnn);
 PA_ANY_KERNEL(fusion_seqexpand_concat_fc, k_seqexpand_concat_fc);
+PA_ANY_KERNEL(detection_map, k_detection_map);
 
 void link_extra_kernels() {}
 

@@ -305,6 +305,31 @@ def case_nms_mining(x, lab, idx):
     return L.elementwise_add(_sq(h), extra)
 
 
+def _fconst(vals, shape, lod):
+    t = simple_op("assign_value", {}, {"shape": shape, "dtype": 5, "fp32_values": vals}, dtype="float32",
+                  stop_gradient=True)
+    return L.lod_reset(t, target_lod=lod)
+
+
+def case_detection_map(x, lab, idx):
+    h = _head(x)
+    det = _fconst([1, 0.9, 0.1, 0.1, 0.5, 0.5, 1, 0.8, 0.12, 0.1, 0.5, 0.52, 2, 0.7, 0.5, 0.5, 0.9, 0.9,
+                   2, 0.95, 0.0, 0.0, 0.3, 0.3, 1, 0.6, 0.55, 0.5, 0.9, 0.95, 2, 0.3, 0.1, 0.1, 0.2, 0.2],
+                  [6, 6], [0, 3, 6])
+    gt = _fconst([1, 0, 0.1, 0.1, 0.5, 0.5, 2, 1, 0.5, 0.5, 0.9, 0.9, 2, 0, 0.0, 0.0, 0.3, 0.3,
+                  1, 0, 0.5, 0.5, 0.9, 0.9, 2, 0, 0.6, 0.6, 0.8, 0.8],
+                 [5, 6], [0, 2, 5])
+    outs = []
+    for ap, diff in (("integral", True), ("11point", False)):
+        m, pc, tp, fp = simple_op("detection_map", {"DetectRes": [det], "Label": [gt]},
+                                  {"class_num": 3, "background_label": 0, "overlap_threshold": 0.5,
+                                   "evaluate_difficult": diff, "ap_type": ap}, out_slot="MAP",
+                                  extra_outputs=("AccumPosCount", "AccumTruePos", "AccumFalsePos"),
+                                  stop_gradient=True)
+        outs += [m, L.mean(L.cast(pc, "float32")), L.mean(tp), L.mean(fp)]
+    return L.elementwise_add(_sq(h), _sum(*outs))
+
+
 CASES = {k[5:]: v for k, v in globals().items() if k.startswith("case_")}
 
 
