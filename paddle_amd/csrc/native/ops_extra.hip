@@ -2519,6 +2519,145 @@ void k_detection_map(const OpRun& r) {
   put(r, "AccumFalsePos", ft, {});
 }
 
+// ---------------------------------------------------------------- attention_lstm
+// attention_lstm_op.cc: per step, attention scores relu(x_l . aw[:M] (+ ab) + c . aw[M:])
+// (optionally scaled and re-biased through relu) softmaxed over the sequence, the
+// attended input lx = sum_l a_l x_l, then an LSTM step with gates {forget, input,
+// output, candidate} from lx W[D:] + h W[:D] + b.  One work item per sequence runs all
+// its steps (the batch-wide step count, state frozen past the sequence's end, as the
+// reference's last-step intermediates see it).
+__host__ __device__ inline float act_of(int a, float v) {
+  switch (a) {
+    case 0: return 1.f / (1.f + expf(-v));
+    case 1: return tanhf(v);
+    case 2: return fmaxf(v, 0.f);
+    default: return v;
+  }
+}
+int act_code(const std::string& s) {
+  if (s == "sigmoid") return 0;
+  if (s == "tanh") return 1;
+  if (s == "relu") return 2;
+  PA_CHECK(s == "identity" || s.empty(), "attention_lstm: activation %s", s.c_str());
+  return 3;
+}
+struct AttLstm {
+  const float *x, *ax, *aw, *sc, *scb, *W, *b, *c0, *h0;
+  const int* off;
+  float *H, *C, *work, *fc_last, *lx_last, *g_last;
+  int64_t N, M, D, L;
+  int ag, ac, acand;
+  __host__ __device__ void operator()(int64_t n) const {
+    const int64_t a = off[n], len = off[n + 1] - off[n];
+    float* fc = work + n * (L + M + 6 * D);
+    float* lx = fc + L;
+    float* g = lx + M;
+    float* c = g + 4 * D;
+    float* h = c + D;
+    for (int64_t d = 0; d < D; ++d) {
+      c[d] = c0[n * D + d];
+      h[d] = h0 ? h0[n * D + d] : 0.f;
+    }
+    for (int64_t t = 0; t < L; ++t) {
+      float cb = 0.f;
+      for (int64_t d = 0; d < D; ++d) cb += c[d] * aw[M + d];
+      float mx = -INFINITY;
+      for (int64_t l = 0; l < len; ++l) {
+        float v = fmaxf(ax[a + l] + cb, 0.f);
+        if (sc) {
+          v *= sc[0];
+          v = fmaxf(v + (scb ? scb[0] : 0.f), 0.f);
+        }
+        fc[l] = v;
+        mx = fmaxf(mx, v);
+      }
+      float den = 0.f;
+      for (int64_t l = 0; l < len; ++l) {
+        fc[l] = expf(fc[l] - mx);
+        den += fc[l];
+      }
+      for (int64_t l = 0; l < L; ++l) fc[l] = l < len ? fc[l] / den : 0.f;
+      for (int64_t m = 0; m < M; ++m) {
+        float v = 0.f;
+        for (int64_t l = 0; l < len; ++l) v += fc[l] * x[(a + l) * M + m];
+        lx[m] = v;
+      }
+      for (int64_t j = 0; j < 4 * D; ++j) {
+        float v = 0.f;
+        for (int64_t m = 0; m < M; ++m) v += lx[m] * W[(D + m) * 4 * D + j];
+        for (int64_t d = 0; d < D; ++d) v += h[d] * W[d * 4 * D + j];
+        g[j] = v + b[j];
+      }
+      const bool alive = t < len;
+      for (int64_t d = 0; d < D; ++d) {
+        const float f = act_of(ag, g[d]), i = act_of(ag, g[D + d]), o = act_of(ag, g[2 * D + d]),
+                    cand = act_of(acand, g[3 * D + d]);
+        const float cn = f * c[d] + i * cand, hn = act_of(ac, cn) * o;
+        if (alive) {
+          H[(a + t) * D + d] = hn;
+          C[(a + t) * D + d] = cn;
+          c[d] = cn;
+          h[d] = hn;
+        }
+      }
+    }
+    if (n == N - 1) {
+      for (int64_t l = 0; l < L; ++l) fc_last[l] = fc[l];
+      for (int64_t m = 0; m < M; ++m) lx_last[m] = lx[m];
+      for (int64_t j = 0; j < 4 * D; ++j) g_last[j] = g[j];
+    }
+  }
+};
+struct AttScore {
+  const float *x, *aw, *ab;
+  float* ax;
+  int64_t M;
+  __host__ __device__ void operator()(int64_t t) const {
+    float v = ab ? ab[0] : 0.f;
+    for (int64_t m = 0; m < M; ++m) v += x[t * M + m] * aw[m];
+    ax[t] = v;
+  }
+};
+
+void k_attention_lstm(const OpRun& r) {
+  const bool dev = on_dev(r);
+  const Tensor& x = r.in("X");
+  PA_CHECK(x.dims.size() == 2 && !x.lod.empty(), "attention_lstm: LoD X [T, M] expected");
+  const std::vector<int> off = offsets_of(x, x.dims[0]);
+  const int64_t T = x.dims[0], M = x.dims[1], N = (int64_t)off.size() - 1;
+  const Tensor& W = r.in("LSTMWeight");
+  const int64_t D = W.dims[1] / 4;
+  PA_CHECK(W.dims.size() == 2 && W.dims[0] == D + M, "attention_lstm: LSTMWeight must be [D + M, 4D]");
+  int64_t L = 0;
+  for (int64_t n = 0; n < N; ++n) L = std::max<int64_t>(L, off[(size_t)n + 1] - off[(size_t)n]);
+  auto opt = [&](const char* slot) -> const float* {
+    Tensor* t = r.in_opt(slot);
+    return t ? f32(*t, dev) : nullptr;
+  };
+  Tensor ax, H, C, fcl, lxl, gl;
+  float* axp = ax.alloc<float>({T, 1}, place_of(r));
+  const float* aw = f32(r.in("AttentionWeight"), dev);
+  any::run(r, dev, T, AttScore{f32(x, dev), aw, opt("AttentionBias"), axp, M}, 64);
+  std::vector<float> hw;
+  float* work = any::scratch(r, dev, "@att_lstm_work@", N * (L + M + 6 * D), &hw);
+  AttLstm f{f32(x, dev), axp, aw, opt("AttentionScalar"), opt("AttentionScalarBias"), f32(W, dev),
+            f32(r.in("LSTMBias"), dev), f32(r.in("C0"), dev), opt("H0"), any::ints(r, dev, "@att_lstm_off@", off),
+            H.alloc<float>({T, D}, place_of(r)), C.alloc<float>({T, D}, place_of(r)), work,
+            fcl.alloc<float>({L, 1}, place_of(r)), lxl.alloc<float>({1, M}, place_of(r)),
+            gl.alloc<float>({1, 4 * D}, place_of(r)), N, M, D, L,
+            act_code(r.op.GetString("gate_activation", "sigmoid")), act_code(r.op.GetString("cell_activation", "tanh")),
+            act_code(r.op.GetString("candidate_activation", "tanh"))};
+  any::run(r, dev, N, f, 1);
+  H.lod = x.lod;
+  C.lod = x.lod;
+  set(r, "Hidden", H);
+  set(r, "Cell", C);
+  set(r, "AttentionedX", ax);
+  set(r, "AttentionFCOut", fcl);
+  set(r, "LSTMX", lxl);
+  set(r, "LSTMOUT", gl);
+}
+
 }  // namespace
 
 #define PA_ANY_KERNEL(name, fn) \
@@ -2578,6 +2717,7 @@ PA_ANY_KERNEL(fusion_lstm, k_fusion_rnn);
 PA_ANY_KERNEL(fusion_gru, k_fusion_rnn);
 PA_ANY_KERNEL(fusion_seqexpand_concat_fc, k_seqexpand_concat_fc);
 PA_ANY_KERNEL(detection_map, k_detection_map);
+PA_ANY_KERNEL(attention_lstm, k_attention_lstm);
 
 void link_extra_kernels() {}
 

@@ -479,7 +479,7 @@ def test_sampling_crop_print_native(capfd):
 
 def fusion_rnn_build():
     """fusion_lstm / fusion_gru (inference ops: XX = X WeightX, then the recurrence) and
-    fusion_seqexpand_concat_fc."""
+    fusion_seqexpand_concat_fc, attention_lstm."""
     x = L.data(name="xs", shape=[5], dtype="float32", lod_level=1)
     D = 3
     cp = lambda shape: L.create_parameter(shape, "float32")  # noqa: E731
@@ -495,14 +495,23 @@ def fusion_rnn_build():
     y = L.data(name="ys", shape=[2], dtype="float32")
     fo, _ = simple_op("fusion_seqexpand_concat_fc", {"X": [x, y], "FCWeight": [cp([7, 4])], "FCBias": [cp([4])]},
                       {"fc_activation": "tanh"}, extra_outputs=("FCOut",), stop_gradient=True)
-    return [h, c, g, fo]
+    c0 = L.data(name="c0", shape=[D], dtype="float32")
+    ah, ac, _, _, _, _ = simple_op(
+        "attention_lstm", {"X": [x], "C0": [c0], "AttentionWeight": [cp([5 + D, 1])], "AttentionBias": [cp([1, 1])],
+                           "AttentionScalar": [cp([1, 1])], "AttentionScalarBias": [cp([1, 1])],
+                           "LSTMWeight": [cp([D + 5, 4 * D])], "LSTMBias": [cp([1, 4 * D])]},
+        {"gate_activation": "sigmoid", "cell_activation": "tanh", "candidate_activation": "tanh"},
+        out_slot="Hidden", extra_outputs=("Cell", "AttentionedX", "AttentionFCOut", "LSTMX", "LSTMOUT"),
+        stop_gradient=True)
+    return [h, c, g, fo, ah, ac]
 
 
 def fusion_feeds():
     rs = np.random.RandomState(3)
     t = core.LoDTensor(torch.from_numpy(rs.randn(9, 5).astype("float32")))
     t.set_lod([[0, 3, 5, 9]])
-    return [{"xs": t, "ys": core.LoDTensor(torch.from_numpy(rs.randn(3, 2).astype("float32")))}]
+    return [{"xs": t, "ys": core.LoDTensor(torch.from_numpy(rs.randn(3, 2).astype("float32"))),
+             "c0": core.LoDTensor(torch.from_numpy(rs.randn(3, 3).astype("float32")))}]
 
 
 def test_fusion_rnn_native_host():
