@@ -27,6 +27,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <map>
 #include <random>
 #include <string>
@@ -2658,6 +2659,99 @@ void k_attention_lstm(const OpRun& r) {
   set(r, "LSTMOUT", gl);
 }
 
+// ---------------------------------------------------------------- generate_proposals
+// generate_proposals_op.cc (RPN): per image, the pre_nms_topN best anchors decode
+// their deltas (x Variances), clip to the image, drop boxes under min_size * scale,
+// greedy NMS (pixel IoU, adaptive eta), post_nms_topN kept.  Host loops as the
+// reference's CPU kernel; staged through the host on a HIP place.
+std::vector<int64_t> greedy_nms(const std::vector<std::array<float, 4>>& boxes, const std::vector<float>& sc,
+                                float thr, float eta) {
+  std::vector<int64_t> order(boxes.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = (int64_t)i;
+  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return sc[(size_t)a] > sc[(size_t)b]; });
+  std::vector<int64_t> keep;
+  float adaptive = thr;
+  while (!order.empty()) {
+    const int64_t i = order[0];
+    keep.push_back(i);
+    std::vector<int64_t> rest;
+    for (size_t q = 1; q < order.size(); ++q)
+      if (box_iou(boxes[(size_t)i].data(), boxes[(size_t)order[q]].data(), false) <= adaptive) rest.push_back(order[q]);
+    order.swap(rest);
+    if (eta < 1.f && adaptive > 0.5f) adaptive *= eta;
+  }
+  return keep;
+}
+
+void k_generate_proposals(const OpRun& r) {
+  const Tensor st = host_view(r, r.in("Scores"));
+  const Tensor dt = host_view(r, r.in("BboxDeltas"));
+  const Tensor it = host_view(r, r.in("ImInfo"));
+  const Tensor at = host_view(r, r.in("Anchors"));
+  Tensor* vp = r.in_opt("Variances");
+  const Tensor vt = vp ? host_view(r, *vp) : Tensor();
+  if (r.ctx.device >= 0) PA_HIPCHK(hipStreamSynchronize((hipStream_t)r.ctx.stream));
+  PA_CHECK(st.dims.size() == 4, "generate_proposals: Scores [N, A, H, W] expected");
+  const int64_t N = st.dims[0], A = st.dims[1], H = st.dims[2], W = st.dims[3], K = A * H * W;
+  PA_CHECK(dt.numel() == N * 4 * K && at.numel() == 4 * K, "generate_proposals: deltas / anchors do not match");
+  const float *sp = f32(st, false), *dp = f32(dt, false), *ip = f32(it, false), *ap = f32(at, false);
+  const float* var = vp ? f32(vt, false) : nullptr;
+  const int64_t pre = r.op.GetInt("pre_nms_topN", 6000), post = r.op.GetInt("post_nms_topN", 1000);
+  const float nthr = r.op.GetFloat("nms_thresh", 0.5f), eta = r.op.GetFloat("eta", 1.f);
+  const float clampv = (float)log(1000.0 / 16);
+  std::vector<float> rois, probs;
+  std::vector<size_t> off = {0};
+  const int64_t IW = it.dims.back();
+  for (int64_t b = 0; b < N; ++b) {
+    std::vector<float> s((size_t)K);
+    for (int64_t a = 0; a < A; ++a)
+      for (int64_t hw = 0; hw < H * W; ++hw) s[(size_t)(hw * A + a)] = sp[(b * A + a) * H * W + hw];
+    std::vector<int64_t> order((size_t)K);
+    for (int64_t i = 0; i < K; ++i) order[(size_t)i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int64_t u, int64_t v) { return s[(size_t)u] > s[(size_t)v]; });
+    if (pre > 0 && (int64_t)order.size() > pre) order.resize((size_t)pre);
+    const float ih = ip[b * IW], iw = ip[b * IW + 1];
+    const float ms = (float)((double)r.op.GetFloat("min_size", 0.1f) * (double)ip[b * IW + 2]);
+    std::vector<std::array<float, 4>> boxes;
+    std::vector<float> ss;
+    for (int64_t i : order) {
+      const int64_t a = i % A, hw = i / A;
+      const float* an = ap + i * 4;
+      float d[4];
+      for (int k = 0; k < 4; ++k) d[k] = dp[((b * A + a) * 4 + k) * H * W + hw] * (var ? var[i * 4 + k] : 1.f);
+      const float aw = an[2] - an[0] + 1.f, ah = an[3] - an[1] + 1.f;
+      const float acx = an[0] + 0.5f * aw, acy = an[1] + 0.5f * ah;
+      const float cx = d[0] * aw + acx, cy = d[1] * ah + acy;
+      const float w = expf(std::min(d[2], clampv)) * aw, h = expf(std::min(d[3], clampv)) * ah;
+      std::array<float, 4> bx = {cx - w / 2, cy - h / 2, cx + w / 2 - 1, cy + h / 2 - 1};
+      bx[0] = std::min(std::max(bx[0], 0.f), iw - 1);
+      bx[2] = std::min(std::max(bx[2], 0.f), iw - 1);
+      bx[1] = std::min(std::max(bx[1], 0.f), ih - 1);
+      bx[3] = std::min(std::max(bx[3], 0.f), ih - 1);
+      if (bx[2] - bx[0] + 1 >= ms && bx[3] - bx[1] + 1 >= ms) {
+        boxes.push_back(bx);
+        ss.push_back(s[(size_t)i]);
+      }
+    }
+    std::vector<int64_t> keep = greedy_nms(boxes, ss, nthr, eta);
+    if (post > 0 && (int64_t)keep.size() > post) keep.resize((size_t)post);
+    for (int64_t k : keep) {
+      for (int q = 0; q < 4; ++q) rois.push_back(boxes[(size_t)k][(size_t)q]);
+      probs.push_back(ss[(size_t)k]);
+    }
+    off.push_back(probs.size());
+  }
+  Tensor ro, pr;
+  float* rp = ro.alloc<float>({(int64_t)probs.size(), 4}, -1);
+  float* pp = pr.alloc<float>({(int64_t)probs.size(), 1}, -1);
+  if (!probs.empty()) {
+    memcpy(rp, rois.data(), rois.size() * sizeof(float));
+    memcpy(pp, probs.data(), probs.size() * sizeof(float));
+  }
+  put(r, "RpnRois", ro, {off});
+  put(r, "RpnRoiProbs", pr, {off});
+}
+
 }  // namespace
 
 #define PA_ANY_KERNEL(name, fn) \
@@ -2718,6 +2812,7 @@ PA_ANY_KERNEL(fusion_gru, k_fusion_rnn);
 PA_ANY_KERNEL(fusion_seqexpand_concat_fc, k_seqexpand_concat_fc);
 PA_ANY_KERNEL(detection_map, k_detection_map);
 PA_ANY_KERNEL(attention_lstm, k_attention_lstm);
+PA_ANY_KERNEL(generate_proposals, k_generate_proposals);
 
 void link_extra_kernels() {}
 

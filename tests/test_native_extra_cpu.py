@@ -330,6 +330,27 @@ def case_detection_map(x, lab, idx):
     return L.elementwise_add(_sq(h), _sum(*outs))
 
 
+def case_generate_proposals(x, lab, idx):
+    h = _head(x)
+    sc = L.sigmoid(L.reshape(_head(x, 2 * 2 * 3), [-1, 2, 2, 3]))
+    dl = L.scale(L.reshape(_head(x, 8 * 2 * 3), [-1, 8, 2, 3]), 0.3)
+    feat = L.reshape(_head(x, 6), [-1, 1, 2, 3])
+    anchors, var = simple_op("anchor_generator", {"Input": [feat]},
+                             {"anchor_sizes": [8.0, 16.0], "aspect_ratios": [1.0], "variances": [1.0, 1.0, 1.0, 1.0],
+                              "stride": [8.0, 8.0], "offset": 0.5}, out_slot="Anchors",
+                             extra_outputs=("Variances",), stop_gradient=True)
+    info = simple_op("assign_value", {}, {"shape": [4, 3], "dtype": 5,
+                                          "fp32_values": [20.0, 28.0, 1.0, 24.0, 24.0, 0.5, 16.0, 30.0, 2.0,
+                                                          30.0, 30.0, 1.0]}, dtype="float32", stop_gradient=True)
+    for v in (sc, dl):
+        v.stop_gradient = True
+    rois, probs = simple_op("generate_proposals", {"Scores": [sc], "BboxDeltas": [dl], "ImInfo": [info],
+                                                   "Anchors": [anchors], "Variances": [var]},
+                            {"pre_nms_topN": 10, "post_nms_topN": 5, "nms_thresh": 0.6, "min_size": 2.0, "eta": 1.0},
+                            out_slot="RpnRois", extra_outputs=("RpnRoiProbs",), stop_gradient=True)
+    return L.elementwise_add(_sq(h), L.elementwise_add(L.scale(L.mean(rois), 0.01), L.mean(probs)))
+
+
 CASES = {k[5:]: v for k, v in globals().items() if k.startswith("case_")}
 
 
