@@ -2752,6 +2752,39 @@ void k_generate_proposals(const OpRun& r) {
   put(r, "RpnRoiProbs", pr, {off});
 }
 
+// ---------------------------------------------------------------- ctc_align
+// ctc_align_op.h: per sequence, drop blanks and (merge_repeated) repeats of the
+// previous token; a single -1 when everything was removed.  Variable-length output:
+// host loop (the reference's CPU kernel), staged through the host on a HIP place.
+void k_ctc_align(const OpRun& r) {
+  const Tensor in = host_view(r, r.in("Input"));
+  if (r.ctx.device >= 0) PA_HIPCHK(hipStreamSynchronize((hipStream_t)r.ctx.stream));
+  const Idx x = idx_of(in, false);
+  const std::vector<int> off = offsets_of(in, in.numel());
+  const int64_t blank = r.op.GetInt("blank", 0);
+  const bool merge = r.op.GetBool("merge_repeated", true);
+  std::vector<int64_t> out;
+  std::vector<size_t> noff = {0};
+  for (size_t q = 0; q + 1 < off.size(); ++q) {
+    bool have_prev = false;
+    int64_t prev = 0;
+    for (int64_t i = off[q]; i < off[q + 1]; ++i) {
+      const int64_t v = x[i];
+      if (v != blank && !(merge && have_prev && v == prev)) out.push_back(v);
+      prev = v;
+      have_prev = true;
+    }
+    noff.push_back(out.size());
+  }
+  if (out.empty()) {
+    out = {-1};
+    noff = {0, 1};
+  }
+  Tensor h;
+  memcpy(h.alloc<int64_t>({(int64_t)out.size(), 1}, -1), out.data(), out.size() * sizeof(int64_t));
+  put(r, "Output", h, {noff});
+}
+
 }  // namespace
 
 #define PA_ANY_KERNEL(name, fn) \
@@ -2813,6 +2846,7 @@ PA_ANY_KERNEL(fusion_seqexpand_concat_fc, k_seqexpand_concat_fc);
 PA_ANY_KERNEL(detection_map, k_detection_map);
 PA_ANY_KERNEL(attention_lstm, k_attention_lstm);
 PA_ANY_KERNEL(generate_proposals, k_generate_proposals);
+PA_ANY_KERNEL(ctc_align, k_ctc_align);
 
 void link_extra_kernels() {}
 

@@ -41,24 +41,40 @@ def test_native_engine_updates_python_scope_in_place():
         assert not np.allclose(t_after.numpy(), v0.numpy())
 
 
+def _lod_identity_op():
+    """A Python-only op type (registered here, no C++ kernel anywhere): Out = X with
+    X's LoD."""
+    from paddle_amd.framework.registry import OP_REGISTRY, register_op
+    if "test_lod_identity" not in OP_REGISTRY:
+        @register_op("test_lod_identity", ["X"], ["Out"], {}, grad=None, no_infer=True)
+        def test_lod_identity(ctx):
+            ctx.set_output("Out", ctx.input("X").clone(), ctx.input_lod("X"))
+
+
 def test_native_engine_python_fallback_lod_and_control_flow():
-    """Ops without a C++ kernel (ctc_align after a LoD feed) run through the executor's
-    per-op Python fallback with their LoD intact (input and output)."""
+    """An op without a C++ kernel (a Python-only op after ctc_align's LoD output) runs
+    through the executor's per-op Python fallback with its LoD intact (input and
+    output); ctc_align itself runs natively."""
+    from paddle_amd.fluid.layers.layer_utils import simple_op
+
+    _lod_identity_op()
     main, startup = fluid.Program(), fluid.Program()
     with fluid.program_guard(main, startup):
         x = fluid.layers.data("x", [4], lod_level=1)
         y = fluid.layers.ctc_greedy_decoder(fluid.layers.softmax(fluid.layers.fc(x, 3)), blank=0)
+        z = simple_op("test_lod_identity", {"X": [y]}, {}, dtype="int64", stop_gradient=True)
     scope = fluid.core.Scope()
     place = fluid.CPUPlace()
     xv = fluid.create_lod_tensor(np.random.RandomState(0).rand(7, 4).astype("float32"), [[3, 4]], place)
     with fluid.executor.scope_guard(scope):
         fluid.Executor(place).run(startup)
-        (ref,) = fluid.Executor(place).run(main, feed={"x": xv}, fetch_list=[y], return_numpy=False)
+        ref = fluid.Executor(place).run(main, feed={"x": xv}, fetch_list=[y, z], return_numpy=False)
         exe = fluid.Executor(place, engine="native")
-        (got,) = exe.run(main, feed={"x": xv}, fetch_list=[y], return_numpy=False)
-    np.testing.assert_array_equal(np.array(got.tensor), np.array(ref.tensor))
-    assert got.lod() == ref.lod()
-    assert exe._native.py_fallbacks.get("ctc_align") == 1
+        got = exe.run(main, feed={"x": xv}, fetch_list=[y, z], return_numpy=False)
+    for g, r in zip(got, ref):
+        np.testing.assert_array_equal(np.array(g.tensor), np.array(r.tensor))
+        assert g.lod() == r.lod()
+    assert exe._native.py_fallbacks == {"test_lod_identity": 1}, exe._native.py_fallbacks
 
 
 def test_native_engine_rejects_step_scope_programs():
